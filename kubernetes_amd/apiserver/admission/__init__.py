@@ -1,0 +1,93 @@
+"""Admission framework: ordered chains of mutating then validating plugins.
+
+Parity: `staging/src/k8s.io/apiserver/pkg/admission` (`Interface`, `MutationInterface`,
+`ValidationInterface`, `Attributes`, plugin registry by name) and the
+`--admission-control` ordered list (`cmd/kube-apiserver/app/options/plugins.go:51,82`).
+"""
+from __future__ import annotations
+
+CREATE, UPDATE, DELETE, CONNECT = "CREATE", "UPDATE", "DELETE", "CONNECT"
+
+
+class AdmissionError(Exception):
+    def __init__(self, message, code=403, reason="Forbidden"):
+        super().__init__(message)
+        self.code = code
+        self.reason = reason
+
+
+class Attributes:
+    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind", "options")
+
+    def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind="", options=None):
+        self.operation = operation
+        self.resource = resource
+        self.subresource = subresource
+        self.namespace = namespace
+        self.name = name
+        self.obj = obj
+        self.old = old
+        self.user = user
+        self.kind = kind
+        self.options = options
+
+
+class Plugin:
+    name = ""
+    operations = (CREATE, UPDATE, DELETE, CONNECT)
+
+    def __init__(self, server=None, config=None):
+        self.server = server
+        self.config = config or {}
+
+    def handles(self, op):
+        return op in self.operations
+
+    # Mutating plugins override admit(); validating plugins override validate().
+    def admit(self, a: Attributes):
+        return None
+
+    def validate(self, a: Attributes):
+        return None
+
+
+REGISTRY: dict[str, type] = {}
+
+
+def register(cls):
+    REGISTRY[cls.name] = cls
+    return cls
+
+
+class Chain:
+    def __init__(self, plugins):
+        self.plugins = plugins
+        self._mut = [p for p in plugins if type(p).admit is not Plugin.admit]
+        self._val = [p for p in plugins if type(p).validate is not Plugin.validate]
+
+    def admit(self, a: Attributes):
+        for p in self._mut:
+            if p.handles(a.operation):
+                p.admit(a)
+
+    def validate(self, a: Attributes):
+        for p in self._val:
+            if p.handles(a.operation):
+                p.validate(a)
+
+
+DEFAULT_PLUGINS = [
+    "NamespaceLifecycle", "LimitRanger", "ServiceAccount", "DefaultTolerationSeconds",
+    "Priority", "ResourceV2", "ExtendedResourceToleration", "NodeRestriction", "ResourceQuota",
+]
+
+
+def new_chain(names, server=None, configs=None):
+    from . import plugins  # noqa: F401 - registers built-ins
+    configs = configs or {}
+    out = []
+    for n in names:
+        if n not in REGISTRY:
+            raise ValueError(f"unknown admission plugin {n!r}")
+        out.append(REGISTRY[n](server, configs.get(n)))
+    return Chain(out)

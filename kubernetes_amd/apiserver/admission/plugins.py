@@ -1,0 +1,317 @@
+"""Built-in admission plugins.
+
+  * ResourceV2 — the fork's device-request normaliser
+    (`plugin/pkg/admission/resourcev2/admission.go:32-118`), keyed to `amd.com/gpu` and
+    configurable (the reference hard-codes `nvidia.com/gpu` at :64,79).
+  * ResourceQuota — also counts pod-level ExtendedResources, closing the reference's gap
+    where GPU quota went unenforced after ResourceV2 stripped container limits
+    (`pkg/quota/evaluator/core/pods.go:299-335`).
+  * NamespaceLifecycle, LimitRanger, ServiceAccount, DefaultTolerationSeconds, Priority,
+    ExtendedResourceToleration, NodeRestriction, AlwaysPullImages, AlwaysAdmit, AlwaysDeny,
+    PodNodeSelector — per `plugin/pkg/admission/*`.
+"""
+from __future__ import annotations
+
+import os
+
+from ...api import core
+from ...api.meta import new_uid
+from ...api.quantity import Quantity, parse_quantity
+from . import CREATE, DELETE, UPDATE, AdmissionError, Attributes, Plugin, register
+
+SYSTEM_NAMESPACES = ("default", "kube-system", "kube-public")
+
+
+@register
+class ResourceV2(Plugin):
+    name = "ResourceV2"
+    operations = (CREATE, UPDATE)
+
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        names = (config or {}).get("resourceNames") or os.environ.get("KAMD_RESOURCEV2_NAMES", core.AMD_GPU)
+        self.names = set(names.split(",")) if isinstance(names, str) else set(names)
+
+    def admit(self, a: Attributes):
+        if a.subresource or a.resource != "pods":
+            return
+        pod = a.obj
+        if not isinstance(pod, dict) or pod.get("kind", "Pod") != "Pod":
+            raise AdmissionError(f"expected Pod but got {type(pod).__name__}", 400, "BadRequest")
+        spec = pod.setdefault("spec", {})
+        ers = spec.get("extendedResources")
+        if ers is None:
+            ers = []
+        changed = False
+        for key in ("initContainers", "containers"):
+            for c in spec.get(key) or ():
+                res = c.get("resources") or {}
+                limits = res.get("limits") or {}
+                for rname in [r for r in limits if r in self.names]:
+                    val = limits[rname]
+                    name = new_uid()
+                    c["extendedResourceRequests"] = [name]
+                    ers.append({"name": name,
+                                "resources": {"limits": {rname: val}, "requests": {rname: val}},
+                                "affinity": {}})
+                    limits.pop(rname, None)
+                    (res.get("requests") or {}).pop(rname, None)
+                    changed = True
+        if changed:
+            spec["extendedResources"] = ers
+
+
+@register
+class NamespaceLifecycle(Plugin):
+    name = "NamespaceLifecycle"
+
+    def validate(self, a: Attributes):
+        if a.resource == "namespaces":
+            if a.operation == DELETE and a.name in SYSTEM_NAMESPACES:
+                raise AdmissionError(f"namespace {a.name} is immutable (system namespace)")
+            return
+        if not a.namespace or a.operation != CREATE:
+            return
+        if a.resource in ("events", "subjectaccessreviews", "tokenreviews"):
+            return
+        ns = self.server.get_object("namespaces", None, a.namespace) if self.server else None
+        if ns is None:
+            if a.namespace in SYSTEM_NAMESPACES:
+                return
+            raise AdmissionError(f"namespaces \"{a.namespace}\" not found", 404, "NotFound")
+        if (ns.get("status") or {}).get("phase") == "Terminating" or (ns.get("metadata") or {}).get("deletionTimestamp"):
+            raise AdmissionError(f"unable to create new content in namespace {a.namespace} because it is being terminated")
+
+
+@register
+class ServiceAccount(Plugin):
+    name = "ServiceAccount"
+    operations = (CREATE,)
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        spec.setdefault("serviceAccountName", "default")
+
+
+@register
+class DefaultTolerationSeconds(Plugin):
+    name = "DefaultTolerationSeconds"
+    operations = (CREATE,)
+    KEYS = ("node.alpha.kubernetes.io/notReady", "node.alpha.kubernetes.io/unreachable")
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        tols = spec.get("tolerations") or []
+        have = {t.get("key") for t in tols}
+        for k in self.KEYS:
+            if k not in have:
+                tols.append({"key": k, "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": 300})
+        spec["tolerations"] = tols
+
+
+@register
+class ExtendedResourceToleration(Plugin):
+    """Pods requesting an extended resource tolerate the taint named after it
+    (`plugin/pkg/admission/extendedresourcetoleration`). Considers pod-level ERs too."""
+    name = "ExtendedResourceToleration"
+    operations = (CREATE, UPDATE)
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        names = set()
+        for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
+            for k in core.container_requests(c):
+                if core.is_extended_resource_name(k):
+                    names.add(k)
+        for per in spec.get("extendedResources") or ():
+            try:
+                names.add(core.pod_extended_resource_name(per))
+            except ValueError:
+                pass
+        if not names:
+            return
+        tols = spec.get("tolerations") or []
+        have = {(t.get("key"), t.get("operator")) for t in tols}
+        for n in sorted(names):
+            if (n, "Exists") not in have:
+                tols.append({"key": n, "operator": "Exists", "effect": "NoSchedule"})
+        spec["tolerations"] = tols
+
+
+@register
+class Priority(Plugin):
+    name = "Priority"
+    operations = (CREATE,)
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        pcn = spec.get("priorityClassName")
+        if not pcn:
+            default = None
+            if self.server:
+                for pc in self.server.list_objects("priorityclasses"):
+                    if pc.get("globalDefault"):
+                        default = pc
+                spec.setdefault("priority", int(default.get("value", 0)) if default else 0)
+            return
+        if pcn in ("system-cluster-critical", "system-node-critical"):
+            spec["priority"] = 2000000000 if pcn == "system-cluster-critical" else 2000001000
+            return
+        pc = self.server.get_object("priorityclasses", None, pcn) if self.server else None
+        if pc is None:
+            raise AdmissionError(f"no PriorityClass with name {pcn} was found", 403)
+        spec["priority"] = int(pc.get("value", 0))
+
+
+@register
+class LimitRanger(Plugin):
+    """Applies Container default requests/limits from LimitRange objects and enforces max."""
+    name = "LimitRanger"
+    operations = (CREATE, UPDATE)
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource or not self.server:
+            return
+        lrs = self.server.list_objects("limitranges", a.namespace)
+        if not lrs:
+            return
+        for lr in lrs:
+            for item in (lr.get("spec") or {}).get("limits") or ():
+                if item.get("type") != "Container":
+                    continue
+                for c in a.obj.get("spec", {}).get("containers") or ():
+                    res = c.setdefault("resources", {})
+                    lim = res.setdefault("limits", {})
+                    req = res.setdefault("requests", {})
+                    for k, v in (item.get("default") or {}).items():
+                        lim.setdefault(k, v)
+                    for k, v in (item.get("defaultRequest") or {}).items():
+                        req.setdefault(k, v)
+                    for k, v in (item.get("max") or {}).items():
+                        if k in lim and parse_quantity(str(lim[k])) > parse_quantity(str(v)):
+                            raise AdmissionError(f"maximum {k} usage per Container is {v}, but limit is {lim[k]}")
+
+
+@register
+class NodeRestriction(Plugin):
+    """Nodes (users `system:node:<name>`) may only modify their own Node and pods bound to them."""
+    name = "NodeRestriction"
+
+    def validate(self, a):
+        u = a.user
+        if not u or not u.name.startswith("system:node:"):
+            return
+        node = u.name[len("system:node:"):]
+        if a.resource == "nodes" and a.name and a.name != node:
+            raise AdmissionError(f"node {node!r} cannot modify node {a.name!r}")
+        if a.resource == "pods" and a.operation in (UPDATE, DELETE) and a.old is not None:
+            if (a.old.get("spec") or {}).get("nodeName") != node:
+                raise AdmissionError(f"node {node!r} can only modify pods bound to it")
+
+
+@register
+class AlwaysPullImages(Plugin):
+    name = "AlwaysPullImages"
+    operations = (CREATE, UPDATE)
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        spec = a.obj.get("spec") or {}
+        for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
+            c["imagePullPolicy"] = "Always"
+
+
+@register
+class PodNodeSelector(Plugin):
+    """Merges the namespace annotation `scheduler.alpha.kubernetes.io/node-selector`."""
+    name = "PodNodeSelector"
+    operations = (CREATE,)
+    ANN = "scheduler.alpha.kubernetes.io/node-selector"
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource or not self.server:
+            return
+        ns = self.server.get_object("namespaces", None, a.namespace)
+        sel = ((ns or {}).get("metadata") or {}).get("annotations", {}).get(self.ANN)
+        if not sel:
+            return
+        spec = a.obj.setdefault("spec", {})
+        nsel = spec.setdefault("nodeSelector", {})
+        for term in sel.split(","):
+            if "=" in term:
+                k, v = term.split("=", 1)
+                if k.strip() in nsel and nsel[k.strip()] != v.strip():
+                    raise AdmissionError("pod node label selector conflicts with its project node label selector")
+                nsel[k.strip()] = v.strip()
+
+
+@register
+class AlwaysAdmit(Plugin):
+    name = "AlwaysAdmit"
+
+
+@register
+class AlwaysDeny(Plugin):
+    name = "AlwaysDeny"
+
+    def validate(self, a):
+        raise AdmissionError("admission control is denying all modifications")
+
+
+def pod_usage(pod) -> dict[str, Quantity]:
+    """Quota usage of a pod, including the fork's pod-level extended resources."""
+    if core.pod_is_terminal(pod):
+        return {}
+    use: dict[str, Quantity] = {"pods": Quantity(1), "count/pods": Quantity(1)}
+    for k, v in core.pod_requests(pod).items():
+        use["requests." + k] = v
+        if k in ("cpu", "memory"):
+            use[k] = v
+        if core.is_extended_resource_name(k):
+            use[k] = v
+    for per in (pod.get("spec") or {}).get("extendedResources") or ():
+        try:
+            rn = core.pod_extended_resource_name(per)
+            n = Quantity(core.pod_extended_resource_count(per))
+        except (ValueError, KeyError):
+            continue
+        for key in ("requests." + rn, rn):
+            use[key] = use[key] + n if key in use else n
+    return use
+
+
+@register
+class ResourceQuota(Plugin):
+    name = "ResourceQuota"
+    operations = (CREATE,)
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource or not self.server:
+            return
+        quotas = self.server.list_objects("resourcequotas", a.namespace)
+        if not quotas:
+            return
+        new = pod_usage(a.obj)
+        used: dict[str, Quantity] = {}
+        for p in self.server.list_objects("pods", a.namespace):
+            for k, v in pod_usage(p).items():
+                used[k] = used[k] + v if k in used else v
+        for qo in quotas:
+            hard = (qo.get("spec") or {}).get("hard") or {}
+            for k, hv in hard.items():
+                if k not in new:
+                    continue
+                total = used.get(k, Quantity(0)) + new[k]
+                if total > parse_quantity(str(hv)):
+                    raise AdmissionError(
+                        f"exceeded quota: {qo['metadata']['name']}, requested: {k}={new[k]}, "
+                        f"used: {k}={used.get(k, Quantity(0))}, limited: {k}={hv}")

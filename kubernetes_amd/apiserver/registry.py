@@ -1,0 +1,258 @@
+"""Per-resource REST strategies (create/update/status/delete semantics).
+
+Parity:
+  * generic `Store` CRUD: `staging/src/k8s.io/apiserver/pkg/registry/generic/registry/store.go:262-1153`
+  * pod strategy + graceful delete: `pkg/registry/core/pod/strategy.go`
+  * **BindingREST with devices** (fork F6): `pkg/registry/core/pod/storage/storage.go:139-210`
+    — one atomic update sets `spec.nodeName`, merges annotations, writes
+    `spec.extendedResources[i].assigned` from `target.extendedResourceBinding[name]` and
+    sets `PodScheduled=True`. Added checks: the binding must cover
+    every requested ER with exactly the requested count, and a device may not be bound
+    to two live pods on the same node.
+"""
+from __future__ import annotations
+
+import random
+import time
+
+from ..api import core, validation
+from ..api.meta import new_uid, now_rfc3339
+from ..api.quantity import parse_quantity
+
+
+class APIError(Exception):
+    def __init__(self, code, reason, message, details=None):
+        super().__init__(message)
+        self.code, self.reason, self.message, self.details = code, reason, message, details
+
+
+def not_found(ri, name):
+    return APIError(404, "NotFound", f'{ri.group_resource} "{name}" not found',
+                    {"name": name, "group": ri.group, "kind": ri.plural})
+
+
+def already_exists(ri, name):
+    return APIError(409, "AlreadyExists", f'{ri.group_resource} "{name}" already exists',
+                    {"name": name, "group": ri.group, "kind": ri.plural})
+
+
+def conflict(ri, name, msg):
+    return APIError(409, "Conflict", f'Operation cannot be fulfilled on {ri.group_resource} "{name}": {msg}',
+                    {"name": name, "group": ri.group, "kind": ri.plural})
+
+
+def invalid(ri, name, errs):
+    return APIError(422, "Invalid", f'{ri.kind} "{name}" is invalid: ' + "; ".join(str(e) for e in errs),
+                    {"name": name, "group": ri.group, "kind": ri.kind,
+                     "causes": [{"reason": "FieldValue" + e.type.replace(" ", ""), "message": e.detail, "field": e.field} for e in errs]})
+
+
+def bad_request(msg):
+    return APIError(400, "BadRequest", msg)
+
+
+_GEN_CHARS = "bcdfghjklmnpqrstvwxz2456789"
+
+
+def generate_name(base):
+    return base + "".join(random.choice(_GEN_CHARS) for _ in range(5))
+
+
+class Strategy:
+    """Default strategy: spec+status updated together, no status subresource."""
+    has_status = True      # exposes /status; main updates ignore status changes
+    bump_generation = True
+
+    def __init__(self, ri):
+        self.ri = ri
+
+    def prepare_create(self, obj):
+        pass
+
+    def prepare_update(self, new, old):
+        if self.has_status and "status" in old:
+            new["status"] = old["status"]
+
+    def prepare_status_update(self, new, old):
+        for k in list(new.keys()):
+            if k not in ("status", "metadata", "kind", "apiVersion"):
+                new.pop(k)
+        for k, v in old.items():
+            if k not in ("status", "metadata"):
+                new[k] = v
+        # status updates may not touch labels etc. except through main resource
+        nm, om = new.get("metadata", {}), old.get("metadata", {})
+        for k in ("labels", "annotations", "finalizers", "ownerReferences", "deletionTimestamp",
+                  "deletionGracePeriodSeconds"):
+            if k in om:
+                nm[k] = om[k]
+            else:
+                nm.pop(k, None)
+
+    def validate(self, obj):
+        fn = validation.VALIDATORS.get(self.ri.kind)
+        return fn(obj) if fn else validation.validate_generic(obj, self.ri.namespaced)
+
+    def validate_update(self, new, old):
+        return self.validate(new)
+
+    def graceful_seconds(self, obj, opts) -> int:
+        """0 = delete immediately."""
+        return 0
+
+
+class PodStrategy(Strategy):
+    def prepare_create(self, pod):
+        core.set_defaults_pod(pod)
+        pod["status"] = {"phase": core.POD_PENDING, "qosClass": qos_class(pod)}
+
+    def prepare_update(self, new, old):
+        super().prepare_update(new, old)
+        # scheduler-owned fields are only written through pods/binding
+        ns, os_ = new.setdefault("spec", {}), old.get("spec") or {}
+        if os_.get("nodeName"):
+            ns["nodeName"] = os_["nodeName"]
+        if os_.get("extendedResources") and ns.get("extendedResources"):
+            amap = {r.get("name"): r.get("assigned") for r in os_["extendedResources"]}
+            for r in ns["extendedResources"]:
+                if amap.get(r.get("name")):
+                    r["assigned"] = amap[r["name"]]
+
+    def validate_update(self, new, old):
+        errs = validation.validate_pod(new)
+        ns, os_ = new.get("spec") or {}, old.get("spec") or {}
+        mutable = ("containers", "initContainers", "activeDeadlineSeconds", "tolerations")
+        for k in set(ns) | set(os_):
+            if k in mutable:
+                continue
+            if ns.get(k) != os_.get(k):
+                errs.append(validation.FieldError("Forbidden", f"spec.{k}", "pod updates may not change fields other than "
+                                                  "`spec.containers[*].image`, `spec.initContainers[*].image`, "
+                                                  "`spec.activeDeadlineSeconds` or `spec.tolerations`"))
+        for key in ("containers", "initContainers"):
+            a, b = ns.get(key) or [], os_.get(key) or []
+            if len(a) != len(b):
+                errs.append(validation.FieldError("Forbidden", f"spec.{key}", "may not add or remove containers"))
+                continue
+            for x, y in zip(a, b):
+                x2, y2 = dict(x), dict(y)
+                x2.pop("image", None)
+                y2.pop("image", None)
+                if x2 != y2:
+                    errs.append(validation.FieldError("Forbidden", f"spec.{key}", "pod updates may only change the image"))
+        return errs
+
+    def graceful_seconds(self, pod, opts):
+        spec = pod.get("spec") or {}
+        if not spec.get("nodeName") or core.pod_is_terminal(pod):
+            return 0
+        g = (opts or {}).get("gracePeriodSeconds")
+        if g is None:
+            g = spec.get("terminationGracePeriodSeconds", 30)
+        return max(int(g), 0)
+
+
+class NodeStrategy(Strategy):
+    bump_generation = False
+
+    def prepare_create(self, node):
+        node.setdefault("spec", {})
+        node.setdefault("status", {})
+
+
+class NamespaceStrategy(Strategy):
+    def prepare_create(self, ns):
+        ns.setdefault("spec", {}).setdefault("finalizers", ["kubernetes"])
+        ns["status"] = {"phase": "Active"}
+
+
+class NoStatusStrategy(Strategy):
+    has_status = False
+
+
+def qos_class(pod) -> str:
+    """`qos.GetPodQOS`."""
+    requests, limits, guaranteed = {}, {}, True
+    for c in (pod.get("spec") or {}).get("containers") or ():
+        res = c.get("resources") or {}
+        r, lim = res.get("requests") or {}, res.get("limits") or {}
+        for k in ("cpu", "memory"):
+            if k in r and parse_quantity(str(r[k])).value != 0:
+                requests[k] = True
+            if k in lim and parse_quantity(str(lim[k])).value != 0:
+                limits[k] = True
+            if k not in lim or (k in r and str(r[k]) != str(lim[k]) and parse_quantity(str(r[k])) != parse_quantity(str(lim[k]))):
+                guaranteed = False
+    if not requests and not limits:
+        return "BestEffort"
+    if guaranteed and len(limits) == 2:
+        return "Guaranteed"
+    return "Burstable"
+
+
+STRATEGIES = {"pods": PodStrategy, "nodes": NodeStrategy, "namespaces": NamespaceStrategy,
+              "events": NoStatusStrategy, "configmaps": NoStatusStrategy, "secrets": NoStatusStrategy,
+              "serviceaccounts": NoStatusStrategy, "endpoints": NoStatusStrategy,
+              "limitranges": NoStatusStrategy, "priorityclasses": NoStatusStrategy,
+              "leases": NoStatusStrategy, "roles": NoStatusStrategy, "rolebindings": NoStatusStrategy,
+              "clusterroles": NoStatusStrategy, "clusterrolebindings": NoStatusStrategy,
+              "controllerrevisions": NoStatusStrategy, "storageclasses": NoStatusStrategy}
+
+
+def strategy_for(ri):
+    return STRATEGIES.get(ri.plural, Strategy)(ri)
+
+
+def init_object_meta(obj, ri, namespace):
+    m = obj.setdefault("metadata", {})
+    if not m.get("name") and m.get("generateName"):
+        m["name"] = generate_name(m["generateName"])
+    if ri.namespaced:
+        if m.get("namespace") and namespace and m["namespace"] != namespace:
+            raise bad_request("the namespace of the provided object does not match the namespace sent on the request")
+        m["namespace"] = namespace or m.get("namespace") or "default"
+    else:
+        m.pop("namespace", None)
+    m["uid"] = new_uid()
+    m["creationTimestamp"] = now_rfc3339()
+    m.pop("deletionTimestamp", None)
+    m.pop("deletionGracePeriodSeconds", None)
+    if ri.plural not in ("nodes", "events", "namespaces"):
+        m["generation"] = 1
+    obj["kind"] = ri.kind
+    obj["apiVersion"] = ri.group_version
+
+
+def apply_binding(pod, binding) -> None:
+    """Fork `setPodHostAndAnnotations` + `assignPod` (storage.go:155-210), mutating `pod`."""
+    target = binding.get("target") or {}
+    node = target.get("name", "")
+    if not node:
+        raise bad_request("Binding target name is required")
+    spec = pod.setdefault("spec", {})
+    meta = pod.setdefault("metadata", {})
+    if meta.get("deletionTimestamp"):
+        raise APIError(409, "Conflict", f"pod {meta.get('name')} is being deleted, cannot be assigned to a host")
+    if spec.get("nodeName"):
+        raise APIError(409, "Conflict", f"pod {meta.get('name')} is already assigned to node \"{spec['nodeName']}\"")
+    spec["nodeName"] = node
+    ann = (binding.get("metadata") or {}).get("annotations")
+    if ann:
+        meta.setdefault("annotations", {}).update(ann)
+    erb = target.get("extendedResourceBinding") or {}
+    for per in spec.get("extendedResources") or ():
+        got = erb.get(per.get("name"))
+        if got is None:
+            raise bad_request(f"binding does not assign extended resource {per.get('name')}")
+        ids = list(got.get("resources") or [])
+        want = core.pod_extended_resource_count(per)
+        if len(ids) != want or len(set(ids)) != len(ids):
+            raise bad_request(f"extended resource {per.get('name')}: binding assigns {len(ids)} distinct devices, pod requests {want}")
+        per["assigned"] = ids
+    st = pod.setdefault("status", {})
+    core.set_condition(st, {"type": core.COND_POD_SCHEDULED, "status": "True",
+                            "lastProbeTime": None, "lastTransitionTime": now_rfc3339()})
+
+
+def deletion_stamp(grace: int):
+    return now_rfc3339(time.time() + grace)

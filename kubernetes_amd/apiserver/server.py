@@ -1,0 +1,736 @@
+"""kube-apiserver equivalent: REST + watch over HTTP/1.1 on an embedded MVCC store.
+
+Parity map:
+  * handler chain (`staging/src/k8s.io/apiserver/pkg/server/config.go:530-551`): panic
+    recovery → request info → authentication → max-in-flight → authorization → handler.
+  * create/update/patch/delete/list/watch handlers (`staging/src/k8s.io/apiserver/pkg/endpoints/handlers/*.go`),
+    mutating admission before validation, validating admission after
+    (`handlers/create.go:80-111`).
+  * `pods/binding` (fork F6) and `/bindings`, `pods/status`, `nodes/status`,
+    `namespaces/{ns}/finalize`, `pods/eviction`, `pods/log` (proxied to the kubelet).
+  * discovery (`/api`, `/apis`, `/api/v1`, `/apis/<g>/<v>`), `/healthz`, `/version`, `/metrics`.
+
+The store and watch cache live in this process; every write is committed to the MVCC
+store and dispatched to watchers synchronously on the event loop, so a watcher can never
+observe revisions out of order and reads are always consistent with the last write.
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import logging
+import time
+
+from ..api import codec, core, meta as m
+from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
+from ..api.meta import fast_copy, now_rfc3339
+from ..storage.mvcc import MVCCStore
+from ..utils.httpserver import HTTPServer, Response, StreamResponse
+from ..utils.metrics import Registry
+from ..utils.patch import JSONPatchError, apply_patch
+from . import admission as adm
+from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, build_authorizer
+from .cacher import ADDED, DELETED, MODIFIED, GoneError, ResourceCache
+from .registry import (APIError, already_exists, apply_binding, bad_request, conflict, deletion_stamp,
+                       init_object_meta, invalid, not_found, strategy_for)
+
+log = logging.getLogger("apiserver")
+
+VERSION = {"major": "1", "minor": "9", "gitVersion": "v1.9.0-amd.0", "platform": "linux/amd64",
+           "goVersion": "n/a", "compiler": "cpython"}
+
+_READ_VERBS = {"GET": "get", "HEAD": "get"}
+
+
+def _json(status, obj):
+    return Response(status, codec.dumpb(obj))
+
+
+def _err(e: APIError):
+    return Response(e.code, codec.dumpb(m.status_obj(e.code, e.reason, e.message, e.details)))
+
+
+class APIServer:
+    def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
+                 tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
+                 max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
+                 kubelet_port_resolver=None):
+        self.store = store or MVCCStore()
+        self.caches: dict[str, ResourceCache] = {}
+        self.strategies = {}
+        self.storage_codec = codec.StorageCodec(storage_media_type)
+        self.watch_window = watch_window
+        for ri in m.RESOURCES:
+            self._install(ri)
+        names = adm.DEFAULT_PLUGINS if admission_plugins is None else admission_plugins
+        self.admission = adm.new_chain(names, self, admission_config)
+        self.authn = TokenAuthenticator(token_file, tokens) if (token_file or tokens) else None
+        self.authz = build_authorizer(authorization_modes, self)
+        self.max_inflight = max_requests_inflight
+        self.max_mutating = max_mutating_inflight
+        self.inflight = 0
+        self.inflight_mut = 0
+        self.http = HTTPServer(self.handle)
+        self.kubelet_port_resolver = kubelet_port_resolver
+        # fork fix: node -> {(resource, deviceID): pod key}
+        self.node_devices: dict[str, dict[tuple, str]] = {}
+        self.metrics = Registry()
+        self.m_requests = self.metrics.counter("apiserver_request_count", "Counter of apiserver requests",
+                                               ("verb", "resource", "subresource", "code"))
+        self.m_latency = self.metrics.histogram("apiserver_request_latencies_seconds", "Request latency",
+                                                ("verb", "resource"), (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 5))
+        self.m_watchers = self.metrics.gauge("apiserver_registered_watchers", "Number of watchers", ("kind",))
+        self.m_inflight = self.metrics.gauge("apiserver_current_inflight_requests", "In-flight requests", ("requestKind",))
+        self.m_dropped = self.metrics.counter("apiserver_dropped_requests", "Requests dropped with 429", ("requestKind",))
+        self.metrics.register_collector(self._collect)
+        self._load_from_store()
+        self.bootstrap()
+
+    # ------------------------------------------------------------------
+    def _install(self, ri):
+        self.caches[ri.plural] = ResourceCache(ri.plural, self.watch_window)
+        self.strategies[ri.plural] = strategy_for(ri)
+
+    def _collect(self):
+        out = ["# TYPE etcd_object_counts gauge"]
+        for plural, c in sorted(self.caches.items()):
+            if c.by_key:
+                out.append(f'etcd_object_counts{{resource="{plural}"}} {len(c.by_key)}')
+        out.append("# TYPE apiserver_storage_revision gauge")
+        out.append(f"apiserver_storage_revision {self.store.revision}")
+        return out
+
+    def _load_from_store(self):
+        """Rebuild the watch caches after a restart (WAL replay)."""
+        if not self.store.revision or self.store.revision <= 1:
+            return
+        for ri in m.RESOURCES:
+            kvs, _, _ = self.store.range(m.prefix_for(ri))
+            cache = self.caches[ri.plural]
+            for kv in kvs:
+                obj = self.storage_codec.decode(kv.value)
+                obj.setdefault("metadata", {})["resourceVersion"] = str(kv.mod_rev)
+                raw = codec.dumpb(obj)
+                cache.by_key[kv.key] = cache.make_entry(obj, raw, kv.mod_rev)
+                if ri.plural == "pods":
+                    self._index_pod(kv.key, None, obj)
+            cache.rev = self.store.revision
+
+    def bootstrap(self):
+        for ns in ("default", "kube-system", "kube-public"):
+            if self.get_object("namespaces", None, ns) is None:
+                self.create(m.BY_PLURAL["namespaces"], None, {"metadata": {"name": ns}}, admit=False)
+
+    # ------------------------------------------------------------------
+    # object-level API (admission plugins, controllers in-process, tests)
+    def get_object(self, plural, namespace, name):
+        ri = m.BY_PLURAL[plural]
+        e = self.caches[plural].get(m.key_for(ri, namespace, name))
+        return e.obj if e else None
+
+    def list_objects(self, plural, namespace=None):
+        ri = m.BY_PLURAL[plural]
+        prefix = m.prefix_for(ri, namespace if ri.namespaced else None)
+        return [e.obj for k, e in self.caches[plural].by_key.items() if k.startswith(prefix)]
+
+    # ------------------------------------------------------------------
+    # commit path
+    def _commit(self, ri, key, etype, obj, prev):
+        """Write obj (already fully prepared) to the store and the cache. Returns Entry."""
+        rev = self.store.revision + 1
+        obj["metadata"]["resourceVersion"] = str(rev)
+        raw = codec.dumpb(obj)
+        stored = raw if self.storage_codec.media_type == codec.JSON else self.storage_codec.encode(obj)
+        if etype == ADDED:
+            ev = self.store.create(key, stored)
+            if ev is None:
+                raise already_exists(ri, m.name_of(obj))
+        elif etype == MODIFIED:
+            ok, ev = self.store.update(key, stored, prev.rev)
+            if not ok:
+                raise conflict(ri, m.name_of(obj), "the object has been modified; please apply your changes to the latest version and try again")
+        else:
+            ok, ev = self.store.delete(key, prev.rev)
+            if not ok:
+                raise conflict(ri, m.name_of(obj), "the object has been modified")
+        assert ev.kv.mod_rev == rev, (ev.kv.mod_rev, rev)
+        cache = self.caches[ri.plural]
+        entry = cache.make_entry(obj, raw, rev)
+        if ri.plural == "pods":
+            self._index_pod(key, prev.obj if prev else None, None if etype == DELETED else obj)
+        cache.apply(etype, key, entry, prev)
+        return entry
+
+    def _index_pod(self, key, old, new):
+        if old is not None:
+            node = (old.get("spec") or {}).get("nodeName")
+            if node:
+                idx = self.node_devices.get(node)
+                if idx:
+                    for rn, ids in core.pod_assigned_devices(old).items():
+                        for i in ids:
+                            if idx.get((rn, i)) == key:
+                                del idx[(rn, i)]
+        if new is not None and not core.pod_is_terminal(new):
+            node = (new.get("spec") or {}).get("nodeName")
+            if node:
+                idx = self.node_devices.setdefault(node, {})
+                for rn, ids in core.pod_assigned_devices(new).items():
+                    for i in ids:
+                        idx[(rn, i)] = key
+
+    # ------------------------------------------------------------------
+    # verbs
+    def create(self, ri, namespace, obj, user=None, admit=True, subresource=""):
+        if not isinstance(obj, dict):
+            raise bad_request("body must be a JSON object")
+        init_object_meta(obj, ri, namespace)
+        strat = self.strategies[ri.plural]
+        strat.prepare_create(obj)
+        ns = m.namespace_of(obj) if ri.namespaced else None
+        if admit:
+            a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
+            self._admit(a)
+        errs = strat.validate(obj)
+        if errs:
+            raise invalid(ri, m.name_of(obj), errs)
+        if admit:
+            self._validate_admission(a)
+        key = m.key_for(ri, ns, m.name_of(obj))
+        if key in self.caches[ri.plural].by_key:
+            raise already_exists(ri, m.name_of(obj))
+        return self._commit(ri, key, ADDED, obj, None)
+
+    def _admit(self, a):
+        try:
+            self.admission.admit(a)
+        except adm.AdmissionError as e:
+            raise APIError(e.code, e.reason, str(e))
+
+    def _validate_admission(self, a):
+        try:
+            self.admission.validate(a)
+        except adm.AdmissionError as e:
+            raise APIError(e.code, e.reason, str(e))
+
+    def _existing(self, ri, namespace, name):
+        key = m.key_for(ri, namespace, name)
+        e = self.caches[ri.plural].get(key)
+        if e is None:
+            raise not_found(ri, name)
+        return key, e
+
+    def update(self, ri, namespace, name, obj, user=None, subresource=""):
+        if not isinstance(obj, dict):
+            raise bad_request("body must be a JSON object")
+        key, prev = self._existing(ri, namespace, name)
+        old = prev.obj
+        om, nm = old["metadata"], obj.setdefault("metadata", {})
+        if nm.get("name") and nm["name"] != name:
+            raise bad_request("the name of the object does not match the name on the URL")
+        want_rv = nm.get("resourceVersion")
+        if want_rv and want_rv != om.get("resourceVersion"):
+            raise conflict(ri, name, "the object has been modified; please apply your changes to the latest version and try again")
+        if nm.get("uid") and nm["uid"] != om.get("uid"):
+            raise conflict(ri, name, "Precondition failed: UID in precondition does not match")
+        for k in ("uid", "creationTimestamp", "name", "namespace", "selfLink", "generation", "deletionTimestamp",
+                  "deletionGracePeriodSeconds"):
+            if k in om:
+                nm[k] = om[k]
+            else:
+                nm.pop(k, None)
+        obj["kind"], obj["apiVersion"] = ri.kind, ri.group_version
+        strat = self.strategies[ri.plural]
+        if subresource == "status":
+            strat.prepare_status_update(obj, old)
+        elif subresource == "":
+            strat.prepare_update(obj, old)
+            if strat.bump_generation and "generation" in om:
+                if {k: v for k, v in obj.items() if k not in ("metadata", "status")} != \
+                        {k: v for k, v in old.items() if k not in ("metadata", "status")}:
+                    nm["generation"] = om["generation"] + 1
+        a = adm.Attributes(adm.UPDATE, ri.plural, subresource, namespace, name, obj, old, user, ri.kind)
+        self._admit(a)
+        errs = strat.validate_update(obj, old) if subresource == "" else strat.validate(obj)
+        if errs:
+            raise invalid(ri, name, errs)
+        self._validate_admission(a)
+        # finalizers drained on an object that is being deleted -> delete it now
+        if nm.get("deletionTimestamp") and not nm.get("finalizers") and self._grace_expired(ri, obj):
+            return self._commit(ri, key, DELETED, obj, prev)
+        nm["resourceVersion"] = om.get("resourceVersion")
+        if obj == old:
+            return prev  # no-op update: no write, no event (etcd3 GuaranteedUpdate byte-equal short cut)
+        return self._commit(ri, key, MODIFIED, obj, prev)
+
+    def _grace_expired(self, ri, obj):
+        if ri.plural != "pods":
+            return True
+        g = obj["metadata"].get("deletionGracePeriodSeconds")
+        return not g
+
+    def guaranteed_update(self, ri, namespace, name, fn, user=None, subresource=""):
+        """Internal read-modify-write (used by binding, eviction)."""
+        key, prev = self._existing(ri, namespace, name)
+        obj = fast_copy(prev.obj)
+        fn(obj)
+        return self._commit(ri, key, MODIFIED, obj, prev)
+
+    def patch(self, ri, namespace, name, content_type, patch_body, user=None, subresource=""):
+        key, prev = self._existing(ri, namespace, name)
+        try:
+            patch = codec.loads(patch_body)
+            new = apply_patch(content_type, fast_copy(prev.obj), patch)
+        except (JSONPatchError, ValueError) as e:
+            if isinstance(e, ValueError) and "unsupported patch type" in str(e):
+                raise APIError(415, "UnsupportedMediaType", str(e))
+            raise APIError(422, "Invalid", f"the patch could not be applied: {e}")
+        if not isinstance(patch, dict) or "resourceVersion" not in (patch.get("metadata") or {}):
+            new.setdefault("metadata", {})["resourceVersion"] = prev.obj["metadata"].get("resourceVersion")
+        return self.update(ri, namespace, name, new, user, subresource)
+
+    def delete(self, ri, namespace, name, opts=None, user=None):
+        """Returns (Entry, deleted_now)."""
+        opts = opts or {}
+        key, prev = self._existing(ri, namespace, name)
+        old = prev.obj
+        pre = opts.get("preconditions") or {}
+        if pre.get("uid") and pre["uid"] != old["metadata"].get("uid"):
+            raise conflict(ri, name, f"Precondition failed: UID in precondition: {pre['uid']}, UID in object meta: {old['metadata'].get('uid')}")
+        a = adm.Attributes(adm.DELETE, ri.plural, "", namespace, name, None, old, user, ri.kind, opts)
+        self._admit(a)
+        self._validate_admission(a)
+        strat = self.strategies[ri.plural]
+        obj = fast_copy(old)
+        om = obj["metadata"]
+        grace = strat.graceful_seconds(old, opts)
+        fins = list(om.get("finalizers") or [])
+        pol = opts.get("propagationPolicy")
+        if opts.get("orphanDependents") is True:
+            pol = "Orphan"
+        if pol == "Orphan" and "orphan" not in fins and ri.plural not in ("pods", "events"):
+            fins.append("orphan")
+        elif pol == "Foreground" and "foregroundDeletion" not in fins:
+            fins.append("foregroundDeletion")
+        if ri.plural == "namespaces":
+            if (obj.get("spec") or {}).get("finalizers"):
+                if not om.get("deletionTimestamp"):
+                    om["deletionTimestamp"] = now_rfc3339()
+                    obj.setdefault("status", {})["phase"] = "Terminating"
+                    return self._commit(ri, key, MODIFIED, obj, prev), False
+                return prev, False
+        if grace > 0:
+            cur = om.get("deletionGracePeriodSeconds")
+            if cur is not None and cur <= grace:
+                return prev, False  # already deleting with a shorter grace period
+            om["deletionTimestamp"] = deletion_stamp(grace)
+            om["deletionGracePeriodSeconds"] = grace
+            if fins:
+                om["finalizers"] = fins
+            return self._commit(ri, key, MODIFIED, obj, prev), False
+        if fins:
+            changed = om.get("finalizers") != fins or not om.get("deletionTimestamp") or om.get("deletionGracePeriodSeconds")
+            om["finalizers"] = fins
+            om.setdefault("deletionTimestamp", now_rfc3339())
+            om["deletionGracePeriodSeconds"] = 0
+            if not changed:
+                return prev, False
+            return self._commit(ri, key, MODIFIED, obj, prev), False
+        om["deletionGracePeriodSeconds"] = 0
+        om.setdefault("deletionTimestamp", now_rfc3339())
+        return self._commit(ri, key, DELETED, obj, prev), True
+
+    def bind(self, namespace, name, binding, user=None):
+        """POST pods/{name}/binding (fork F6) with the duplicate-device guard."""
+        ri = m.BY_PLURAL["pods"]
+        key, prev = self._existing(ri, namespace, name)
+        a = adm.Attributes(adm.CREATE, "pods", "binding", namespace, name, binding, prev.obj, user, "Binding")
+        self._admit(a)
+        self._validate_admission(a)
+        pod = fast_copy(prev.obj)
+        try:
+            apply_binding(pod, binding)
+        except APIError:
+            raise
+        node = pod["spec"]["nodeName"]
+        idx = self.node_devices.get(node) or {}
+        for rn, ids in core.pod_assigned_devices(pod).items():
+            for i in ids:
+                owner = idx.get((rn, i))
+                if owner is not None and owner != key:
+                    raise APIError(409, "Conflict", f"device {rn}/{i} on node {node} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
+        return self._commit(ri, key, MODIFIED, pod, prev)
+
+    def evict(self, namespace, name, eviction, user=None):
+        ri = m.BY_PLURAL["pods"]
+        # PodDisruptionBudget check
+        pod = self.get_object("pods", namespace, name)
+        if pod is None:
+            raise not_found(ri, name)
+        labels = (pod.get("metadata") or {}).get("labels") or {}
+        from ..api.labels import label_selector_as_selector
+        for pdb in self.list_objects("poddisruptionbudgets", namespace):
+            sel = label_selector_as_selector((pdb.get("spec") or {}).get("selector"))
+            if sel.matches(labels):
+                allowed = (pdb.get("status") or {}).get("disruptionsAllowed", (pdb.get("status") or {}).get("podDisruptionsAllowed", 0))
+                if allowed <= 0:
+                    raise APIError(429, "TooManyRequests", "Cannot evict pod as it would violate the pod's disruption budget.")
+        return self.delete(ri, namespace, name, (eviction or {}).get("deleteOptions") or {}, user)
+
+    # ------------------------------------------------------------------
+    # HTTP
+    async def start(self, host="127.0.0.1", port=0):
+        return await self.http.start(host, port)
+
+    async def stop(self):
+        await self.http.stop()
+
+    def _parse_path(self, path):
+        """Returns (ri, namespace, name, subresource, watch) or a discovery/special marker."""
+        parts = [p for p in path.split("/") if p]
+        if not parts:
+            return None
+        if parts[0] == "api":
+            if len(parts) == 1:
+                return ("discovery", "api")
+            if parts[1] != "v1":
+                return None
+            group, version, rest = "", "v1", parts[2:]
+        elif parts[0] == "apis":
+            if len(parts) == 1:
+                return ("discovery", "apis")
+            if len(parts) == 2:
+                return ("discovery", "group", parts[1])
+            group, version, rest = parts[1], parts[2], parts[3:]
+        else:
+            return None
+        if not rest:
+            return ("discovery", "resources", group, version)
+        watch = False
+        if rest[0] == "watch":
+            watch = True
+            rest = rest[1:]
+        ns = None
+        if rest[0] == "namespaces" and len(rest) >= 3 and not (len(rest) == 3 and rest[2] in ("status", "finalize")):
+            ns = rest[1]
+            rest = rest[2:]
+        plural = rest[0]
+        ri = m.BY_PLURAL.get(plural)
+        if ri is None or ri.group != group:
+            if plural == "bindings" and ns:
+                return ("bindings", ns)
+            return None
+        if ri.version != version and not (group == "apps" and version in ("v1", "v1beta1", "v1beta2")) \
+                and not (group == "batch" and version in ("v1", "v1beta1", "v2alpha1")) \
+                and not (group == "policy" and version in ("v1beta1", "v1")):
+            return None
+        name = rest[1] if len(rest) > 1 else None
+        sub = "/".join(rest[2:]) if len(rest) > 2 else ""
+        return (ri, ns, name, sub, watch)
+
+    async def handle(self, req):
+        t0 = time.perf_counter()
+        verb = req.method
+        resource = ""
+        sub = ""
+        code = 500
+        try:
+            p = req.path
+            if p == "/healthz" or p.startswith("/healthz/") or p in ("/livez", "/readyz"):
+                code = 200
+                return Response(200, b"ok", "text/plain")
+            if p == "/metrics":
+                code = 200
+                return Response(200, self.metrics.render(), "text/plain; version=0.0.4")
+            if p == "/version":
+                code = 200
+                return _json(200, VERSION)
+            user = ANONYMOUS
+            if self.authn is not None:
+                user = self.authn.authenticate(req.headers)
+                if user is None:
+                    code = 401
+                    return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))
+            req.user = user
+            parsed = self._parse_path(p)
+            if parsed is None:
+                code = 404
+                return _json(404, m.status_obj(404, "NotFound", f"the server could not find the requested resource ({p})"))
+            if parsed[0] == "discovery":
+                code = 200
+                return self._discovery(parsed)
+            if parsed[0] == "bindings":
+                resource, sub = "pods", "binding"
+                body = codec.loads(req.body)
+                self._authorize(user, "create", parsed[1], "pods", "binding", m.name_of(body), "", p)
+                self.bind(parsed[1], m.name_of(body), body, user)
+                code = 201
+                return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
+            ri, ns, name, sub, watch = parsed
+            resource = ri.plural
+            is_watch = watch or req.query.get("watch") in ("true", "1")
+            mutating = verb not in ("GET", "HEAD")
+            # max-in-flight (WithMaxInFlightLimit): non-watch requests only
+            if not is_watch:
+                if mutating:
+                    if self.inflight_mut >= self.max_mutating:
+                        self.m_dropped.labels("mutating").inc()
+                        code = 429
+                        return Response(429, codec.dumpb(m.status_obj(429, "TooManyRequests", "Too many requests, please try again later.")),
+                                        headers={"Retry-After": "1"})
+                elif self.inflight >= self.max_inflight:
+                    self.m_dropped.labels("readOnly").inc()
+                    code = 429
+                    return Response(429, codec.dumpb(m.status_obj(429, "TooManyRequests", "Too many requests, please try again later.")),
+                                    headers={"Retry-After": "1"})
+            if ri.namespaced is False:
+                ns = None
+            if not is_watch:
+                if mutating:
+                    self.inflight_mut += 1
+                else:
+                    self.inflight += 1
+            try:
+                resp = await self._dispatch(req, ri, ns, name, sub, is_watch, user)
+            finally:
+                if not is_watch:
+                    if mutating:
+                        self.inflight_mut -= 1
+                    else:
+                        self.inflight -= 1
+            code = getattr(resp, "status", 200)
+            return resp
+        except APIError as e:
+            code = e.code
+            return _err(e)
+        except (ValueError, SelectorError) as e:
+            code = 400
+            return _json(400, m.status_obj(400, "BadRequest", str(e)))
+        finally:
+            self.m_requests.labels(verb, resource, sub, code).inc()
+            if resource:
+                self.m_latency.labels(verb, resource).observe(time.perf_counter() - t0)
+
+    def _authorize(self, user, verb, ns, resource, sub, name, group, path):
+        ok, why = self.authz.authorize(AttributesRecord(user, verb, ns or "", resource, sub, name or "", group, path))
+        if not ok:
+            raise APIError(403, "Forbidden", why or "forbidden")
+
+    async def _dispatch(self, req, ri, ns, name, sub, is_watch, user):
+        method = req.method
+        q = req.query
+        if method in ("GET", "HEAD"):
+            if is_watch:
+                self._authorize(user, "watch", ns, ri.plural, sub, name, ri.group, req.path)
+                return self._watch(req, ri, ns, name)
+            if name is None:
+                self._authorize(user, "list", ns, ri.plural, "", "", ri.group, req.path)
+                return self._list(req, ri, ns)
+            if sub == "log" and ri.plural == "pods":
+                self._authorize(user, "get", ns, "pods", "log", name, "", req.path)
+                return await self._pod_log(ns, name, q)
+            self._authorize(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
+            key = m.key_for(ri, ns, name)
+            e = self.caches[ri.plural].get(key)
+            if e is None:
+                raise not_found(ri, name)
+            return Response(200, e.raw)
+        body = req.body
+        if method == "POST":
+            if name is not None and sub == "binding" and ri.plural == "pods":
+                self._authorize(user, "create", ns, "pods", "binding", name, "", req.path)
+                self.bind(ns, name, codec.loads(body), user)
+                return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
+            if name is not None and sub == "eviction" and ri.plural == "pods":
+                self._authorize(user, "create", ns, "pods", "eviction", name, "", req.path)
+                self.evict(ns, name, codec.loads(body) if body else {}, user)
+                return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
+            if name is not None:
+                raise APIError(405, "MethodNotAllowed", "POST to a named resource is not allowed")
+            self._authorize(user, "create", ns, ri.plural, "", "", ri.group, req.path)
+            obj = codec.loads(body)
+            if ri.namespaced and ns is None:
+                ns = (obj.get("metadata") or {}).get("namespace") or "default"
+            e = self.create(ri, ns, obj, user)
+            return Response(201, e.raw)
+        if name is None:
+            if method == "DELETE":
+                return self._delete_collection(req, ri, ns, user)
+            raise APIError(405, "MethodNotAllowed", f"{method} requires a name")
+        if method == "PUT":
+            if ri.plural == "namespaces" and sub == "finalize":
+                self._authorize(user, "update", None, "namespaces", "finalize", name, "", req.path)
+                return self._finalize_namespace(name, codec.loads(body), user)
+            self._authorize(user, "update", ns, ri.plural, sub, name, ri.group, req.path)
+            e = self.update(ri, ns, name, codec.loads(body), user, sub)
+            return Response(200, e.raw)
+        if method == "PATCH":
+            self._authorize(user, "patch", ns, ri.plural, sub, name, ri.group, req.path)
+            e = self.patch(ri, ns, name, req.headers.get("content-type", "application/merge-patch+json"), body, user, sub)
+            return Response(200, e.raw)
+        if method == "DELETE":
+            self._authorize(user, "delete", ns, ri.plural, "", name, ri.group, req.path)
+            opts = codec.loads(body) if body else {}
+            if "gracePeriodSeconds" in q:
+                opts["gracePeriodSeconds"] = int(q["gracePeriodSeconds"])
+            if "propagationPolicy" in q:
+                opts["propagationPolicy"] = q["propagationPolicy"]
+            e, _ = self.delete(ri, ns, name, opts, user)
+            return Response(200, e.raw)
+        raise APIError(405, "MethodNotAllowed", f"method {method} not allowed")
+
+    def _finalize_namespace(self, name, obj, user):
+        ri = m.BY_PLURAL["namespaces"]
+        key, prev = self._existing(ri, None, name)
+        new = fast_copy(prev.obj)
+        new.setdefault("spec", {})["finalizers"] = list((obj.get("spec") or {}).get("finalizers") or [])
+        if new["metadata"].get("deletionTimestamp") and not new["spec"]["finalizers"] and not new["metadata"].get("finalizers"):
+            e = self._commit(ri, key, DELETED, new, prev)
+        else:
+            e = self._commit(ri, key, MODIFIED, new, prev)
+        return Response(200, e.raw)
+
+    def _delete_collection(self, req, ri, ns, user):
+        self._authorize(user, "deletecollection", ns, ri.plural, "", "", ri.group, req.path)
+        ls = parse_labels(req.query.get("labelSelector")) if req.query.get("labelSelector") else None
+        fs = parse_field_selector(req.query.get("fieldSelector")) if req.query.get("fieldSelector") else None
+        opts = codec.loads(req.body) if req.body else {}
+        items = []
+        for e in self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs):
+            try:
+                d, _ = self.delete(ri, m.namespace_of(e.obj) or None, m.name_of(e.obj), opts, user)
+                items.append(d.obj)
+            except APIError as err:
+                if err.code != 404:
+                    raise
+        return _json(200, {"kind": ri.list_kind, "apiVersion": ri.group_version,
+                           "metadata": {"resourceVersion": str(self.store.revision)}, "items": items})
+
+    def _list(self, req, ri, ns):
+        q = req.query
+        ls = parse_labels(q.get("labelSelector")) if q.get("labelSelector") else None
+        fs = parse_field_selector(q.get("fieldSelector")) if q.get("fieldSelector") else None
+        entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
+        limit = int(q.get("limit") or 0)
+        cont = q.get("continue")
+        rv = str(self.store.revision)
+        next_token = None
+        if cont:
+            try:
+                tok = codec.loads(base64.urlsafe_b64decode(cont.encode()))
+                start = tok["start"]
+                rv = tok.get("rv", rv)
+            except Exception:
+                raise bad_request("continue key is not valid")
+            entries = [e for e in entries if m.ns_name(e.obj) > start]
+        if limit and len(entries) > limit:
+            entries = entries[:limit]
+            next_token = base64.urlsafe_b64encode(codec.dumpb({"rv": rv, "start": m.ns_name(entries[-1].obj)})).decode()
+        md = '"resourceVersion":"%s"' % rv
+        if next_token:
+            md += ',"continue":"%s"' % next_token
+        body = b'{"kind":"%s","apiVersion":"%s","metadata":{%s},"items":[' % (
+            ri.list_kind.encode(), ri.group_version.encode(), md.encode()) + b",".join(e.raw for e in entries) + b"]}"
+        return Response(200, body)
+
+    def _watch(self, req, ri, ns, name):
+        q = req.query
+        rv = q.get("resourceVersion")
+        fsel = q.get("fieldSelector")
+        if name:
+            fsel = (fsel + "," if fsel else "") + f"metadata.name={name}"
+        timeout = float(q.get("timeoutSeconds") or 0) or None
+        cache = self.caches[ri.plural]
+        send_initial = not rv or rv == "0"
+        from_rev = int(rv) if rv and rv != "0" else None
+        if from_rev is not None and cache.events and from_rev < cache.events[0][0] - 1 \
+                and len(cache.events) == cache.events.maxlen:
+            raise APIError(410, "Expired", f"too old resource version: {from_rev} ({cache.events[0][0] - 1})")
+        server = self
+
+        async def run(writer):
+            try:
+                w = cache.add_watcher(writer, ns, q.get("labelSelector"), fsel, from_rev, send_initial)
+            except GoneError as e:
+                writer.write(codec.dumpb({"type": "ERROR", "object": m.status_obj(410, "Expired", str(e))}) + b"\n")
+                return
+            server.m_watchers.labels(ri.kind).inc()
+            try:
+                fut = writer.wait_closed()
+                if timeout:
+                    await asyncio.wait_for(asyncio.shield(fut), timeout)
+                else:
+                    await fut
+            except asyncio.TimeoutError:
+                pass
+            finally:
+                w.stop()
+                server.m_watchers.labels(ri.kind).dec()
+
+        return StreamResponse(run)
+
+    async def _pod_log(self, ns, name, q):
+        pod = self.get_object("pods", ns, name)
+        if pod is None:
+            raise not_found(m.BY_PLURAL["pods"], name)
+        node = (pod.get("spec") or {}).get("nodeName")
+        if not node:
+            raise bad_request(f"pod {name} is not scheduled")
+        nobj = self.get_object("nodes", None, node)
+        port = ((nobj or {}).get("status") or {}).get("daemonEndpoints", {}).get("kubeletEndpoint", {}).get("Port")
+        addr = "127.0.0.1"
+        for a in ((nobj or {}).get("status") or {}).get("addresses") or ():
+            if a.get("type") == "InternalIP":
+                addr = a.get("address")
+        if not port:
+            raise APIError(503, "ServiceUnavailable", f"node {node} has no kubelet endpoint")
+        from ..client.http import HTTPClient
+        c = HTTPClient(f"http://{addr}:{port}")
+        try:
+            qs = "&".join(f"{k}={v}" for k, v in q.items())
+            st, body = await c.request("GET", f"/containerLogs/{ns}/{name}/{q.get('container', '')}" + (f"?{qs}" if qs else ""))
+        finally:
+            await c.close()
+        return Response(st, body, "text/plain")
+
+    def _discovery(self, parsed):
+        kind = parsed[1]
+        if kind == "api":
+            return _json(200, {"kind": "APIVersions", "versions": ["v1"],
+                               "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": "127.0.0.1"}]})
+        groups = {}
+        for ri in m.RESOURCES:
+            if ri.group:
+                groups.setdefault(ri.group, set()).add(ri.version)
+        if kind == "apis":
+            return _json(200, {"kind": "APIGroupList", "apiVersion": "v1", "groups": [
+                {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in sorted(vs)],
+                 "preferredVersion": {"groupVersion": f"{g}/{sorted(vs)[-1]}", "version": sorted(vs)[-1]}}
+                for g, vs in sorted(groups.items())]})
+        if kind == "group":
+            g = parsed[2]
+            if g not in groups:
+                raise APIError(404, "NotFound", f"group {g} not found")
+            vs = sorted(groups[g])
+            return _json(200, {"kind": "APIGroup", "apiVersion": "v1", "name": g,
+                               "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in vs],
+                               "preferredVersion": {"groupVersion": f"{g}/{vs[-1]}", "version": vs[-1]}})
+        group, version = parsed[2], parsed[3]
+        res = []
+        for ri in m.RESOURCES:
+            if ri.group != group or ri.version != version:
+                continue
+            verbs = ["create", "delete", "deletecollection", "get", "list", "patch", "update", "watch"]
+            res.append({"name": ri.plural, "singularName": "", "namespaced": ri.namespaced, "kind": ri.kind,
+                        "verbs": verbs, "shortNames": list(ri.short)})
+            if self.strategies[ri.plural].has_status:
+                res.append({"name": ri.plural + "/status", "singularName": "", "namespaced": ri.namespaced,
+                            "kind": ri.kind, "verbs": ["get", "patch", "update"]})
+            if ri.plural == "pods":
+                res.append({"name": "pods/binding", "singularName": "", "namespaced": True, "kind": "Binding", "verbs": ["create"]})
+                res.append({"name": "pods/eviction", "singularName": "", "namespaced": True, "kind": "Eviction", "verbs": ["create"]})
+                res.append({"name": "pods/log", "singularName": "", "namespaced": True, "kind": "Pod", "verbs": ["get"]})
+        if not res:
+            raise APIError(404, "NotFound", f"{group}/{version} not found")
+        gv = f"{group}/{version}" if group else version
+        return _json(200, {"kind": "APIResourceList", "groupVersion": gv, "resources": res})

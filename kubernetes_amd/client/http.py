@@ -1,0 +1,179 @@
+"""Asyncio HTTP/1.1 client with a keep-alive connection pool and chunked watch streams.
+
+Plays the role of client-go's `rest.Request` transport (`staging/src/k8s.io/client-go/rest/request.go:486-745`).
+Supports `http://host:port`, `https://` (ssl context) and `unix:///path.sock` endpoints.
+"""
+from __future__ import annotations
+
+import asyncio
+import ssl as _ssl
+from urllib.parse import urlparse
+
+
+class HTTPError(Exception):
+    def __init__(self, status, body):
+        super().__init__(f"HTTP {status}: {body[:500]!r}")
+        self.status = status
+        self.body = body
+
+
+class _Conn:
+    __slots__ = ("reader", "writer")
+
+    def __init__(self, reader, writer):
+        self.reader, self.writer = reader, writer
+
+    def close(self):
+        try:
+            self.writer.close()
+        except Exception:
+            pass
+
+
+async def _read_response(reader):
+    line = await reader.readline()
+    if not line:
+        raise ConnectionError("connection closed")
+    parts = line.split(b" ", 2)
+    status = int(parts[1])
+    headers = {}
+    while True:
+        h = await reader.readline()
+        if h in (b"\r\n", b"\n", b""):
+            break
+        k, _, v = h.decode("latin-1").partition(":")
+        headers[k.strip().lower()] = v.strip()
+    return status, headers
+
+
+async def _read_body(reader, headers):
+    if headers.get("transfer-encoding", "").lower() == "chunked":
+        out = bytearray()
+        while True:
+            ln = await reader.readline()
+            n = int(ln.strip().split(b";")[0], 16)
+            if n == 0:
+                await reader.readline()
+                break
+            out += await reader.readexactly(n)
+            await reader.readline()
+        return bytes(out)
+    n = int(headers.get("content-length", "0") or 0)
+    return await reader.readexactly(n) if n else b""
+
+
+class HTTPClient:
+    def __init__(self, base_url: str, token: str | None = None, ssl_context=None, max_conns: int = 16,
+                 timeout: float = 60.0):
+        self.base_url = base_url
+        u = urlparse(base_url)
+        self.unix = u.scheme == "unix"
+        self.path_prefix = ""
+        if self.unix:
+            self.sock_path = u.path
+            self.host_header = "localhost"
+        else:
+            self.host = u.hostname or "127.0.0.1"
+            self.port = u.port or (443 if u.scheme == "https" else 80)
+            self.host_header = f"{self.host}:{self.port}"
+            self.path_prefix = u.path.rstrip("/")
+        self.ssl = ssl_context
+        if u.scheme == "https" and ssl_context is None:
+            self.ssl = _ssl.create_default_context()
+            self.ssl.check_hostname = False
+            self.ssl.verify_mode = _ssl.CERT_NONE
+        self.token = token
+        self._idle: list[_Conn] = []
+        self._sem = asyncio.Semaphore(max_conns)
+        self.timeout = timeout
+        self._closed = False
+
+    async def _open(self):
+        if self.unix:
+            r, w = await asyncio.open_unix_connection(self.sock_path, limit=1 << 24)
+        else:
+            r, w = await asyncio.open_connection(self.host, self.port, ssl=self.ssl, limit=1 << 24)
+        return _Conn(r, w)
+
+    def _head(self, method, path, body, content_type, extra):
+        h = f"{method} {self.path_prefix}{path} HTTP/1.1\r\nHost: {self.host_header}\r\n"
+        if self.token:
+            h += f"Authorization: Bearer {self.token}\r\n"
+        if body is not None:
+            h += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n"
+        if extra:
+            h += "".join(f"{k}: {v}\r\n" for k, v in extra.items())
+        return (h + "\r\n").encode()
+
+    async def request(self, method, path, body: bytes | None = None, content_type="application/json", headers=None):
+        async with self._sem:
+            for attempt in range(2):
+                conn = self._idle.pop() if self._idle else None
+                fresh = conn is None
+                if conn is None:
+                    conn = await self._open()
+                try:
+                    conn.writer.write(self._head(method, path, body, content_type, headers) + (body or b""))
+                    status, hdrs = await asyncio.wait_for(_read_response(conn.reader), self.timeout)
+                    data = await _read_body(conn.reader, hdrs)
+                except (ConnectionError, asyncio.IncompleteReadError, OSError):
+                    conn.close()
+                    if fresh or attempt:
+                        raise
+                    continue  # stale keep-alive connection; retry once on a new one
+                except asyncio.TimeoutError:
+                    conn.close()
+                    raise
+                if hdrs.get("connection", "").lower() == "close":
+                    conn.close()
+                else:
+                    self._idle.append(conn)
+                return status, data
+
+    async def stream(self, method, path, headers=None):
+        """Open a streaming GET; returns (status, async line iterator, closer)."""
+        conn = await self._open()
+        conn.writer.write(self._head(method, path, None, None, headers))
+        status, hdrs = await _read_response(conn.reader)
+        if status != 200:
+            body = await _read_body(conn.reader, hdrs)
+            conn.close()
+            raise HTTPError(status, body)
+        chunked = hdrs.get("transfer-encoding", "").lower() == "chunked"
+        reader = conn.reader
+
+        async def lines():
+            buf = b""
+            try:
+                while True:
+                    if chunked:
+                        ln = await reader.readline()
+                        if not ln:
+                            return
+                        n = int(ln.strip().split(b";")[0] or b"0", 16)
+                        if n == 0:
+                            return
+                        data = await reader.readexactly(n)
+                        await reader.readline()
+                    else:
+                        data = await reader.read(1 << 16)
+                        if not data:
+                            return
+                    buf += data
+                    while True:
+                        i = buf.find(b"\n")
+                        if i < 0:
+                            break
+                        line, buf = buf[:i], buf[i + 1:]
+                        if line.strip():
+                            yield line
+            except (ConnectionError, asyncio.IncompleteReadError, OSError, ValueError):
+                return
+
+        return status, lines(), conn.close
+
+    async def close(self):
+        self._closed = True
+        for c in self._idle:
+            c.close()
+        self._idle.clear()

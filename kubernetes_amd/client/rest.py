@@ -1,0 +1,229 @@
+"""Typed REST client ("clientset") over `HTTPClient`.
+
+Parity: client-go typed clients + `rest.Request` verbs (`staging/src/k8s.io/client-go/rest/request.go`),
+client-side QPS/Burst token bucket (`util/flowcontrol`), `errors.IsNotFound/IsConflict/IsAlreadyExists`.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from urllib.parse import quote, urlencode
+
+from ..api import codec, meta as m
+from .http import HTTPClient
+
+
+class APIStatusError(Exception):
+    def __init__(self, code, status):
+        self.code = code
+        self.status = status if isinstance(status, dict) else {"message": str(status)}
+        self.reason = self.status.get("reason", "")
+        super().__init__(f"{code} {self.reason}: {self.status.get('message', '')}")
+
+
+def is_not_found(e):
+    return isinstance(e, APIStatusError) and e.code == 404
+
+
+def is_conflict(e):
+    return isinstance(e, APIStatusError) and e.code == 409 and e.reason == "Conflict"
+
+
+def is_already_exists(e):
+    return isinstance(e, APIStatusError) and e.code == 409 and e.reason == "AlreadyExists"
+
+
+def is_gone(e):
+    return isinstance(e, APIStatusError) and e.code == 410
+
+
+class TokenBucket:
+    def __init__(self, qps, burst):
+        self.qps, self.burst = qps, burst
+        self.tokens = burst
+        self.t = time.monotonic()
+
+    async def wait(self):
+        while True:
+            now = time.monotonic()
+            self.tokens = min(self.burst, self.tokens + (now - self.t) * self.qps)
+            self.t = now
+            if self.tokens >= 1:
+                self.tokens -= 1
+                return
+            await asyncio.sleep((1 - self.tokens) / self.qps)
+
+
+def resource_path(resource: str, namespace=None, name=None, subresource="", watch=False):
+    ri = m.lookup(resource)
+    if ri is None:
+        raise ValueError(f"unknown resource {resource!r}")
+    base = "/api/v1" if not ri.group else f"/apis/{ri.group}/{ri.version}"
+    p = base
+    if watch:
+        p += "/watch"
+    if ri.namespaced and namespace:
+        p += f"/namespaces/{quote(namespace)}"
+    p += f"/{ri.plural}"
+    if name:
+        p += f"/{quote(name)}"
+    if subresource:
+        p += f"/{subresource}"
+    return p
+
+
+class Client:
+    def __init__(self, url: str, token=None, qps: float | None = None, burst: int = 10, max_conns=16,
+                 user_agent="kubernetes-amd", ssl_context=None, timeout=60.0):
+        self.url = url
+        self.http = HTTPClient(url, token=token, ssl_context=ssl_context, max_conns=max_conns, timeout=timeout)
+        self.limiter = TokenBucket(qps, burst) if qps else None
+        self.user_agent = user_agent
+
+    async def close(self):
+        await self.http.close()
+
+    async def _do(self, method, path, body=None, content_type="application/json", ok=(200, 201)):
+        if self.limiter:
+            await self.limiter.wait()
+        data = None if body is None else (body if isinstance(body, (bytes, bytearray)) else codec.dumpb(body))
+        st, resp = await self.http.request(method, path, data, content_type)
+        if st not in ok:
+            try:
+                status = codec.loads(resp)
+            except Exception:
+                status = {"message": resp.decode(errors="replace")}
+            raise APIStatusError(st, status)
+        return codec.loads(resp) if resp else None
+
+    async def raw(self, method, path, body=None, content_type="application/json"):
+        return await self.http.request(method, path, body, content_type)
+
+    # -- verbs -----------------------------------------------------------
+    async def get(self, resource, name, namespace=None, subresource=""):
+        return await self._do("GET", resource_path(resource, namespace, name, subresource))
+
+    async def list(self, resource, namespace=None, label_selector=None, field_selector=None, limit=0,
+                   cont=None, resource_version=None):
+        q = {}
+        if label_selector:
+            q["labelSelector"] = label_selector
+        if field_selector:
+            q["fieldSelector"] = field_selector
+        if limit:
+            q["limit"] = str(limit)
+        if cont:
+            q["continue"] = cont
+        if resource_version is not None:
+            q["resourceVersion"] = resource_version
+        path = resource_path(resource, namespace)
+        if q:
+            path += "?" + urlencode(q)
+        return await self._do("GET", path)
+
+    async def list_all(self, resource, namespace=None, label_selector=None, field_selector=None, chunk=500):
+        out, cont, rv = [], None, None
+        while True:
+            lst = await self.list(resource, namespace, label_selector, field_selector, limit=chunk, cont=cont)
+            out.extend(lst.get("items") or [])
+            rv = lst["metadata"].get("resourceVersion")
+            cont = lst["metadata"].get("continue")
+            if not cont:
+                return out, rv
+
+    async def create(self, resource, obj, namespace=None):
+        ns = namespace or (obj.get("metadata") or {}).get("namespace")
+        return await self._do("POST", resource_path(resource, ns), obj)
+
+    async def update(self, resource, obj, namespace=None, subresource=""):
+        md = obj.get("metadata") or {}
+        ns = namespace or md.get("namespace")
+        return await self._do("PUT", resource_path(resource, ns, md["name"], subresource), obj)
+
+    async def update_status(self, resource, obj, namespace=None):
+        return await self.update(resource, obj, namespace, "status")
+
+    async def patch(self, resource, name, patch, namespace=None, patch_type="merge", subresource=""):
+        ct = {"merge": "application/merge-patch+json", "strategic": "application/strategic-merge-patch+json",
+              "json": "application/json-patch+json"}[patch_type]
+        return await self._do("PATCH", resource_path(resource, namespace, name, subresource), patch, ct)
+
+    async def delete(self, resource, name, namespace=None, grace_period=None, propagation=None, uid=None):
+        opts = {"kind": "DeleteOptions", "apiVersion": "v1"}
+        if grace_period is not None:
+            opts["gracePeriodSeconds"] = grace_period
+        if propagation:
+            opts["propagationPolicy"] = propagation
+        if uid:
+            opts["preconditions"] = {"uid": uid}
+        return await self._do("DELETE", resource_path(resource, namespace, name), opts)
+
+    async def delete_collection(self, resource, namespace=None, label_selector=None):
+        path = resource_path(resource, namespace)
+        if label_selector:
+            path += "?" + urlencode({"labelSelector": label_selector})
+        return await self._do("DELETE", path)
+
+    async def bind(self, namespace, name, node, extended_resource_binding=None, annotations=None, uid=None):
+        target = {"kind": "Node", "apiVersion": "v1", "name": node}
+        if extended_resource_binding:
+            target["extendedResourceBinding"] = extended_resource_binding
+        body = {"kind": "Binding", "apiVersion": "v1", "metadata": {"name": name, "namespace": namespace},
+                "target": target}
+        if annotations:
+            body["metadata"]["annotations"] = annotations
+        if uid:
+            body["metadata"]["uid"] = uid
+        return await self._do("POST", resource_path("pods", namespace, name, "binding"), body)
+
+    async def evict(self, namespace, name, grace_period=None):
+        body = {"kind": "Eviction", "apiVersion": "policy/v1beta1", "metadata": {"name": name, "namespace": namespace}}
+        if grace_period is not None:
+            body["deleteOptions"] = {"gracePeriodSeconds": grace_period}
+        return await self._do("POST", resource_path("pods", namespace, name, "eviction"), body)
+
+    async def watch(self, resource, namespace=None, resource_version=None, label_selector=None,
+                    field_selector=None, timeout_seconds=None):
+        """Async iterator of (event_type, object). Closes when the server ends the stream."""
+        q = {"watch": "true"}
+        if resource_version is not None:
+            q["resourceVersion"] = str(resource_version)
+        if label_selector:
+            q["labelSelector"] = label_selector
+        if field_selector:
+            q["fieldSelector"] = field_selector
+        if timeout_seconds:
+            q["timeoutSeconds"] = str(int(timeout_seconds))
+        path = resource_path(resource, namespace) + "?" + urlencode(q)
+        try:
+            _, lines, closer = await self.http.stream("GET", path)
+        except Exception as e:
+            from .http import HTTPError
+            if isinstance(e, HTTPError):
+                try:
+                    st = codec.loads(e.body)
+                except Exception:
+                    st = {"message": e.body.decode(errors="replace")}
+                raise APIStatusError(e.status, st)
+            raise
+        return _WatchStream(lines, closer)
+
+
+class _WatchStream:
+    def __init__(self, lines, closer):
+        self._lines = lines
+        self._closer = closer
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        line = await self._lines.__anext__()
+        ev = codec.loads(line)
+        if ev.get("type") == "ERROR":
+            obj = ev.get("object") or {}
+            raise APIStatusError(obj.get("code", 500), obj)
+        return ev["type"], ev["object"]
+
+    def close(self):
+        self._closer()

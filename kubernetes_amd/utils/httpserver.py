@@ -1,0 +1,237 @@
+"""Minimal, fast asyncio HTTP/1.1 server (keep-alive, pipelining-safe, chunked streaming).
+
+The reference's apiserver runs Go's net/http with HTTP/2; here the control plane lives on
+host sockets (SURVEY §2.4 "Distributed comms backend"), so the transport is a lean
+Protocol-based HTTP/1.1 implementation: one parse per request, no per-request
+allocations beyond the header dict, responses written with a single `transport.write`.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+from urllib.parse import parse_qs, unquote
+
+log = logging.getLogger("httpserver")
+
+REASONS = {
+    200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
+    401: "Unauthorized", 403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed",
+    406: "Not Acceptable", 409: "Conflict", 410: "Gone", 413: "Payload Too Large",
+    415: "Unsupported Media Type", 422: "Unprocessable Entity", 429: "Too Many Requests",
+    500: "Internal Server Error", 503: "Service Unavailable", 504: "Gateway Timeout",
+}
+
+
+class Request:
+    __slots__ = ("method", "path", "raw_path", "query", "headers", "body", "transport", "user", "info")
+
+    def __init__(self, method, target, headers, body, transport):
+        self.method = method
+        if "?" in target:
+            p, qs = target.split("?", 1)
+            self.query = {k: v[-1] for k, v in parse_qs(qs, keep_blank_values=True).items()}
+        else:
+            p, self.query = target, {}
+        self.raw_path = p
+        self.path = unquote(p)
+        self.headers = headers
+        self.body = body
+        self.transport = transport
+        self.user = None
+        self.info = None
+
+
+class Response:
+    __slots__ = ("status", "body", "content_type", "headers")
+
+    def __init__(self, status=200, body=b"", content_type="application/json", headers=None):
+        self.status = status
+        self.body = body if isinstance(body, (bytes, bytearray)) else str(body).encode()
+        self.content_type = content_type
+        self.headers = headers
+
+
+class StreamResponse:
+    """Returned by a handler that wants to stream (watch). `run(writer)` is awaited with a
+    ChunkWriter; the connection is closed afterwards."""
+
+    __slots__ = ("run", "content_type")
+
+    def __init__(self, run, content_type="application/json"):
+        self.run = run
+        self.content_type = content_type
+
+
+class ChunkWriter:
+    __slots__ = ("transport", "closed", "_proto")
+
+    def __init__(self, transport, proto):
+        self.transport = transport
+        self._proto = proto
+        self.closed = False
+
+    def write(self, data: bytes):
+        if self.closed or self.transport.is_closing():
+            self.closed = True
+            return False
+        self.transport.write(b"%x\r\n%s\r\n" % (len(data), data))
+        return True
+
+    async def drain(self):
+        await self._proto.drain()
+
+    def end(self):
+        if not self.closed and not self.transport.is_closing():
+            self.transport.write(b"0\r\n\r\n")
+        self.closed = True
+
+    def wait_closed(self):
+        """Future resolved when the peer closes the connection."""
+        p = self._proto
+        if p.close_fut is None:
+            p.close_fut = asyncio.get_running_loop().create_future()
+            if self.transport.is_closing():
+                p.close_fut.set_result(None)
+        return p.close_fut
+
+
+class _Conn(asyncio.Protocol):
+    def __init__(self, server):
+        self.server = server
+        self.buf = bytearray()
+        self.transport = None
+        self.pending = []
+        self.busy = False
+        self.streaming = False
+        self._paused = False
+        self._drain_waiter = None
+        self.close_fut = None
+
+    def connection_made(self, transport):
+        self.transport = transport
+        self.server._conns.add(self)
+
+    def connection_lost(self, exc):
+        self.server._conns.discard(self)
+        self.streaming = False
+        if self.close_fut is not None and not self.close_fut.done():
+            self.close_fut.set_result(None)
+        if self._drain_waiter and not self._drain_waiter.done():
+            self._drain_waiter.set_result(None)
+
+    def pause_writing(self):
+        self._paused = True
+
+    def resume_writing(self):
+        self._paused = False
+        if self._drain_waiter and not self._drain_waiter.done():
+            self._drain_waiter.set_result(None)
+
+    async def drain(self):
+        if self._paused and not self.transport.is_closing():
+            self._drain_waiter = asyncio.get_running_loop().create_future()
+            await self._drain_waiter
+
+    def data_received(self, data):
+        self.buf += data
+        while True:
+            req = self._parse()
+            if req is None:
+                break
+            self.pending.append(req)
+        if self.pending and not self.busy:
+            self.busy = True
+            asyncio.ensure_future(self._serve())
+
+    def _parse(self):
+        buf = self.buf
+        end = buf.find(b"\r\n\r\n")
+        if end < 0:
+            if len(buf) > 1 << 20:
+                self.transport.close()
+            return None
+        head = bytes(buf[:end]).decode("latin-1")
+        lines = head.split("\r\n")
+        try:
+            method, target, _ = lines[0].split(" ", 2)
+        except ValueError:
+            self.transport.close()
+            return None
+        headers = {}
+        for ln in lines[1:]:
+            k, _, v = ln.partition(":")
+            headers[k.strip().lower()] = v.strip()
+        clen = int(headers.get("content-length", "0") or 0)
+        if len(buf) < end + 4 + clen:
+            return None
+        body = bytes(buf[end + 4:end + 4 + clen])
+        del buf[:end + 4 + clen]
+        return Request(method, target, headers, body, self.transport)
+
+    async def _serve(self):
+        try:
+            while self.pending:
+                req = self.pending.pop(0)
+                try:
+                    resp = await self.server.handler(req)
+                except Exception as e:  # pragma: no cover - defensive
+                    log.exception("handler error")
+                    resp = Response(500, b'{"kind":"Status","status":"Failure","message":%s,"code":500}' % repr(str(e)).encode())
+                if self.transport.is_closing():
+                    return
+                if isinstance(resp, StreamResponse):
+                    self.streaming = True
+                    self.transport.write(
+                        ("HTTP/1.1 200 OK\r\nContent-Type: %s\r\nTransfer-Encoding: chunked\r\n"
+                         "Cache-Control: no-cache, private\r\n\r\n" % resp.content_type).encode())
+                    w = ChunkWriter(self.transport, self)
+                    try:
+                        await resp.run(w)
+                    except (ConnectionError, asyncio.CancelledError):
+                        pass
+                    finally:
+                        w.end()
+                        self.streaming = False
+                    self.transport.close()
+                    return
+                hdr = "HTTP/1.1 %d %s\r\nContent-Type: %s\r\nContent-Length: %d\r\n" % (
+                    resp.status, REASONS.get(resp.status, "OK"), resp.content_type, len(resp.body))
+                if resp.headers:
+                    hdr += "".join("%s: %s\r\n" % kv for kv in resp.headers.items())
+                close = req.headers.get("connection", "").lower() == "close"
+                if close:
+                    hdr += "Connection: close\r\n"
+                self.transport.write(hdr.encode() + b"\r\n" + resp.body)
+                if close:
+                    self.transport.close()
+                    return
+        finally:
+            self.busy = False
+
+
+class HTTPServer:
+    def __init__(self, handler):
+        self.handler = handler
+        self._server = None
+        self._conns = set()
+        self.port = None
+
+    async def start(self, host="127.0.0.1", port=0, ssl=None):
+        loop = asyncio.get_running_loop()
+        self._server = await loop.create_server(lambda: _Conn(self), host, port, ssl=ssl, backlog=4096,
+                                                reuse_address=True)
+        self.port = self._server.sockets[0].getsockname()[1]
+        return self.port
+
+    async def start_unix(self, path):
+        loop = asyncio.get_running_loop()
+        self._server = await loop.create_unix_server(lambda: _Conn(self), path)
+        return path
+
+    async def stop(self):
+        if self._server:
+            self._server.close()
+            for c in list(self._conns):
+                if c.transport:
+                    c.transport.close()
+            await self._server.wait_closed()
