@@ -1,0 +1,101 @@
+"""Build every native component in-tree (C++ with g++, HIP for gfx950 with hipcc).
+
+    python -m kubernetes_amd.native.build [--force] [--only NAME]
+
+Targets land in kubernetes_amd/native/{lib,bin}/ so they travel with the repo snapshot to
+the GPU box (git-ignored, not gpurun-ignored). Incremental: a target is rebuilt only when a
+source is newer than it.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+from . import BIN_DIR, LIB_DIR, SRC_DIR
+
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("KAMD_OFFLOAD_ARCH", "gfx950")
+
+
+def _s(*p):
+    return os.path.join(SRC_DIR, *p)
+
+
+def targets():
+    cxx = ["g++", "-O2", "-std=c++17", "-Wall", "-fPIC"]
+    hip = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+    return {
+        "kamd_smi": ([_s("amdsmi_shim", "kamd_smi.cc"), _s("amdsmi_shim", "kamd_smi.h")],
+                     os.path.join(LIB_DIR, "libkamd_smi.so"),
+                     cxx + ["-shared", f"-I{ROCM}/include", _s("amdsmi_shim", "kamd_smi.cc"), "-ldl"]),
+        "kamd_store": ([_s("store", "mvcc_store.cc")], os.path.join(LIB_DIR, "libkamd_store.so"),
+                       cxx + ["-O3", "-shared", _s("store", "mvcc_store.cc")]),
+        "kamd_oci": ([_s("oci", "oci_devices.cc")], os.path.join(LIB_DIR, "libkamd_oci.so"),
+                     cxx + ["-shared", _s("oci", "oci_devices.cc")]),
+        "pause": ([_s("pause", "pause.cc")], os.path.join(BIN_DIR, "pause"),
+                  ["g++", "-Os", "-Wall", "-Werror", "-static", _s("pause", "pause.cc")]),
+        "orphan": ([_s("pause", "orphan.cc")], os.path.join(BIN_DIR, "orphan"),
+                   ["g++", "-Os", "-Wall", _s("pause", "orphan.cc")]),
+        "kamd_hip": ([_s("hip", "kamd_hip.hip")], os.path.join(LIB_DIR, "libkamd_hip.so"),
+                     hip + ["-shared", _s("hip", "kamd_hip.hip")]),
+        "hip_vector_add": ([_s("hip", "vector_add_main.hip"), _s("hip", "kamd_hip.hip")],
+                           os.path.join(BIN_DIR, "hip-vector-add"),
+                           hip + [_s("hip", "vector_add_main.hip"), _s("hip", "kamd_hip.hip")]),
+        "xgmi_probe": ([_s("hip", "xgmi_probe.cc")], os.path.join(BIN_DIR, "xgmi-probe"),
+                       [HIPCC, f"--offload-arch={ARCH}", "-O2", "-x", "hip", _s("hip", "xgmi_probe.cc"),
+                        f"-I{ROCM}/include", f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]),
+    }
+
+
+def _stale(srcs, out):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.exists(s) and os.path.getmtime(s) > t for s in srcs)
+
+
+def build(force=False, only=None, verbose=True):
+    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(BIN_DIR, exist_ok=True)
+    jobs = []
+    for name, (srcs, out, cmd) in targets().items():
+        if only and name not in only:
+            continue
+        if not all(os.path.exists(s) for s in srcs if s.endswith((".cc", ".hip"))):
+            continue
+        if force or _stale(srcs, out):
+            jobs.append((name, out, cmd + ["-o", out]))
+    failures = []
+
+    def run(job):
+        name, out, cmd = job
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        return name, out, r
+
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for name, out, r in ex.map(run, jobs):
+            if r.returncode != 0:
+                failures.append(name)
+                print(f"[build] {name} FAILED\n{r.stderr[-4000:]}", file=sys.stderr)
+            elif verbose:
+                print(f"[build] {name} -> {os.path.relpath(out)}")
+    if failures:
+        raise RuntimeError(f"native build failed: {failures}")
+    return [j[1] for j in jobs]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", nargs="*")
+    a = ap.parse_args()
+    build(a.force, a.only)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,416 @@
+// kamd_hip — HIP/CDNA4 (gfx950) kernels used by the orchestrator's GPU paths.
+//
+//  * vector_add        — the GPU e2e workload. MI355X-native replacement for the reference's
+//                        cuda-vector-add test image (test/images/cuda-vector-add/Dockerfile,
+//                        used by test/e2e/scheduling/nvidia-gpus.go:51-113): 1-D grid of
+//                        ceil(N/256) blocks x 256 threads, N = 50000 floats by default.
+//  * gemm_bf16_nt      — MFMA (v_mfma_f32_16x16x32_bf16) LDS-tiled GEMM, C = A · Bᵀ, used by the
+//                        device-plugin burn-in diagnostic (matrix-core health + throughput, the
+//                        role DCGM diag plays in the NVIDIA stack) and by the workload payload.
+//  * hbm_copy          — 16 B/lane streaming copy: HBM3E bandwidth health probe.
+//
+// Everything is exported through a C ABI (extern "C") so the Python side binds with ctypes
+// and passes torch tensor pointers + the current HIP stream.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+static thread_local char g_err[256];
+
+static int check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+#define HC(x)                              \
+  do {                                     \
+    if (check((x), #x) != 0) return -1;    \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// vector_add
+__global__ void __launch_bounds__(256) vector_add_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                          float* __restrict__ c, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) c[i] = a[i] + b[i];
+}
+
+// ---------------------------------------------------------------------------
+// MFMA GEMM: C[M,N] = A[M,K] · B[N,K]ᵀ   (A, B bf16 row-major; C fp32 or bf16)
+//
+// Block tile 128x128, BK = 64, 256 threads = 4 waves in a 2x2 grid; each wave owns a 64x64
+// sub-tile = 4x4 MFMA 16x16 tiles (16 f32x4 accumulators). LDS holds one A and one B tile
+// (128 rows x 64 bf16 = 128 B per row) per stage, double buffered (64 KiB). Rows are stored
+// with the 16-byte chunk index XOR-swizzled by ((row >> 1) & 7) so that the 16 lanes of each
+// ds_read_b128 group (16 consecutive rows, same k chunk) cover all 64 banks exactly once.
+// Global->LDS is register-staged (prefetch tile t+1 into VGPRs while computing tile t).
+// The block id is remapped so blocks sharing an XCD (bid % 8) take consecutive tiles (T1).
+namespace gemm {
+constexpr int BM = 128, BN = 128, BK = 64, THREADS = 256;
+constexpr int ROW_BYTES = BK * 2;                // 128 B
+constexpr int TILE_BYTES = BM * ROW_BYTES;       // 16 KiB
+constexpr int CHUNKS = TILE_BYTES / 16;          // 1024 16-B chunks per tile
+constexpr int LOADS = CHUNKS / THREADS;          // 4 per thread per operand
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * ROW_BYTES + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // bijective: blocks with the same (bid % 8) — the same XCD under round-robin dispatch —
+  // get a contiguous range of tile ids (shared A rows stay in that XCD's L2)
+  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+template <typename OutT>
+__device__ __forceinline__ void store_out(OutT* p, float v);
+template <>
+__device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void store_out<__bf16>(__bf16* p, float v) { *p = (__bf16)v; }
+
+template <typename OutT>
+__global__ void __launch_bounds__(THREADS, 2)
+gemm_bf16_nt_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
+                    int M, int N, int K, int ldc, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // [2 stages][A|B] tiles
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  // group 8 tile-rows together (L2 reuse of B columns across consecutive tiles)
+  const int GROUP = 8;
+  const int group_id = t / (GROUP * tiles_n);
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (t % (GROUP * tiles_n)) % gsz;
+  const int tn = (t % (GROUP * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[LOADS], rb[LOADS];
+  const int ktiles = (K + BK - 1) / BK;
+
+  auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int c = tid + i * THREADS;           // chunk id within the tile
+      const int row = c >> 3, ch = c & 7;
+      const int kk = k0 + ch * 8;
+      const int ga = m0 + row, gb = n0 + row;
+      uint4 z = {0u, 0u, 0u, 0u};
+      ra[i] = (ga < M && kk < K) ? *reinterpret_cast<const uint4*>(A + (size_t)ga * K + kk) : z;
+      rb[i] = (gb < N && kk < K) ? *reinterpret_cast<const uint4*>(B + (size_t)gb * K + kk) : z;
+    }
+  };
+  auto sstore = [&](int stage) {
+    unsigned char* la = lds + stage * 2 * TILE_BYTES;
+    unsigned char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int c = tid + i * THREADS;
+      const int row = c >> 3, ch = c & 7;
+      *reinterpret_cast<uint4*>(la + swz(row, ch)) = ra[i];
+      *reinterpret_cast<uint4*>(lb + swz(row, ch)) = rb[i];
+    }
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int frow = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int stage = kt & 1;
+    if (kt + 1 < ktiles) gload(kt + 1);  // prefetch next tile into VGPRs
+    const unsigned char* la = lds + stage * 2 * TILE_BYTES;
+    const unsigned char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[4], bfr[4];
+      const int ch = ks * 4 + fq;  // 16-B chunk holding k = ks*32 + 8*fq .. +7
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm + i * 16 + frow, ch));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn + j * 16 + frow, ch));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < ktiles) sstore(stage ^ 1);
+    __syncthreads();
+  }
+  // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + j * 16 + frow;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + i * 16 + fq * 4 + r;
+        if (row < M && col < N) store_out<OutT>(C + (size_t)row * ldc + col, alpha * acc[i][j][r]);
+      }
+    }
+}
+}  // namespace gemm
+
+// ---------------------------------------------------------------------------
+// HBM streaming copy, 16 B per lane, grid-stride
+__global__ void __launch_bounds__(256) hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ void fill_bf16_kernel(u16* p, size_t n, uint32_t seed, float scale) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    float f = ((float)(x & 0xFFFFFF) / 16777216.0f * 2.f - 1.f) * scale;  // uniform [-scale, scale)
+    __bf16 b = (__bf16)f;
+    p[i] = *reinterpret_cast<u16*>(&b);
+  }
+}
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* kamd_hip_last_error() { return g_err; }
+
+int kamd_hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int kamd_hip_device_arch(int dev, char* out, int len) {
+  hipDeviceProp_t p;
+  HC(hipGetDeviceProperties(&p, dev));
+  snprintf(out, len, "%s", p.gcnArchName);
+  return 0;
+}
+
+// async launches on a caller stream (torch tensors)
+int kamd_vector_add_launch(const float* a, const float* b, float* c, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(vector_add_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a, b, c, n);
+  return check(hipGetLastError(), "vector_add launch");
+}
+
+int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N, int K, int ldc, float alpha,
+                             int out_fp32, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (K % 8 != 0) {
+    snprintf(g_err, sizeof g_err, "gemm_bf16_nt: K (%d) must be a multiple of 8", K);
+    return -1;
+  }
+  if ((((uintptr_t)A) | ((uintptr_t)B)) & 15) {
+    snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
+    return -1;
+  }
+  const int tiles = ((M + gemm::BM - 1) / gemm::BM) * ((N + gemm::BN - 1) / gemm::BN);
+  const size_t lds = 2 * 2 * gemm::TILE_BYTES;
+  if (out_fp32) {
+    hipLaunchKernelGGL(gemm::gemm_bf16_nt_kernel<float>, dim3(tiles), dim3(gemm::THREADS), lds, stream,
+                       (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+  } else {
+    hipLaunchKernelGGL(gemm::gemm_bf16_nt_kernel<__bf16>, dim3(tiles), dim3(gemm::THREADS), lds, stream,
+                       (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+  }
+  return check(hipGetLastError(), "gemm launch");
+}
+
+int kamd_hbm_copy_launch(const void* src, void* dst, size_t bytes, hipStream_t stream) {
+  size_t n = bytes / 16;
+  int blocks = 256 * 8;
+  hipLaunchKernelGGL(hbm_copy_kernel, dim3(blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, n);
+  return check(hipGetLastError(), "hbm_copy launch");
+}
+
+// --- self-contained diagnostics (allocate, run, verify, free) -------------
+
+// vectorAdd sample semantics: returns 0 and prints nothing; *max_err = max |c - (a+b)|.
+int kamd_diag_vector_add(int dev, int n, float* max_err) {
+  HC(hipSetDevice(dev));
+  std::vector<float> ha(n), hb(n), hc(n);
+  for (int i = 0; i < n; ++i) {
+    ha[i] = (float)((i * 1103515245u + 12345u) % 10007) / 10007.f;
+    hb[i] = (float)((i * 2654435761u + 7u) % 10009) / 10009.f;
+  }
+  float *da = nullptr, *db = nullptr, *dc = nullptr;
+  size_t bytes = (size_t)n * sizeof(float);
+  HC(hipMalloc(&da, bytes));
+  HC(hipMalloc(&db, bytes));
+  HC(hipMalloc(&dc, bytes));
+  HC(hipMemcpy(da, ha.data(), bytes, hipMemcpyHostToDevice));
+  HC(hipMemcpy(db, hb.data(), bytes, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(vector_add_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, da, db, dc, n);
+  HC(hipGetLastError());
+  HC(hipMemcpy(hc.data(), dc, bytes, hipMemcpyDeviceToHost));
+  float e = 0.f;
+  for (int i = 0; i < n; ++i) {
+    float d = hc[i] - (ha[i] + hb[i]);
+    if (d < 0) d = -d;
+    if (d > e) e = d;
+  }
+  *max_err = e;
+  hipFree(da);
+  hipFree(db);
+  hipFree(dc);
+  return 0;
+}
+
+// MFMA burn-in: random bf16 operands, `iters` timed GEMMs of M=N=K=`size`; result checked on
+// a sampled set of output elements against an fp64 host dot product.
+int kamd_diag_mfma(int dev, int size, int iters, double* tflops, double* max_rel_err) {
+  HC(hipSetDevice(dev));
+  const int M = size, N = size, K = size;
+  u16 *A = nullptr, *B = nullptr;
+  float* C = nullptr;
+  HC(hipMalloc(&A, (size_t)M * K * 2));
+  HC(hipMalloc(&B, (size_t)N * K * 2));
+  HC(hipMalloc(&C, (size_t)M * N * 4));
+  hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, 0, A, (size_t)M * K, 0x1234u, 1.f);
+  hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, 0, B, (size_t)N * K, 0x9876u, 1.f);
+  HC(hipGetLastError());
+  if (kamd_gemm_bf16_nt_launch(A, B, C, M, N, K, N, 1.f, 1, 0) != 0) return -1;  // warm-up
+  hipEvent_t e0, e1;
+  HC(hipEventCreate(&e0));
+  HC(hipEventCreate(&e1));
+  HC(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i)
+    if (kamd_gemm_bf16_nt_launch(A, B, C, M, N, K, N, 1.f, 1, 0) != 0) return -1;
+  HC(hipEventRecord(e1, 0));
+  HC(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HC(hipEventElapsedTime(&ms, e0, e1));
+  *tflops = 2.0 * M * N * (double)K * iters / (ms * 1e-3) / 1e12;
+  // verify 256 sampled outputs
+  std::vector<u16> ha((size_t)M * K), hb((size_t)N * K);
+  std::vector<float> hc((size_t)M * N);
+  HC(hipMemcpy(ha.data(), A, ha.size() * 2, hipMemcpyDeviceToHost));
+  HC(hipMemcpy(hb.data(), B, hb.size() * 2, hipMemcpyDeviceToHost));
+  HC(hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost));
+  auto bf = [](u16 v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return (double)f; };
+  double worst = 0;
+  for (int s = 0; s < 256; ++s) {
+    int i = (int)((s * 7919u) % (unsigned)M), j = (int)((s * 104729u + 13u) % (unsigned)N);
+    double ref = 0, mag = 0;
+    for (int k = 0; k < K; ++k) {
+      double p = bf(ha[(size_t)i * K + k]) * bf(hb[(size_t)j * K + k]);
+      ref += p;
+      mag += p < 0 ? -p : p;
+    }
+    double err = hc[(size_t)i * N + j] - ref;
+    if (err < 0) err = -err;
+    double rel = err / (mag > 1e-30 ? mag : 1.0);
+    if (rel > worst) worst = rel;
+  }
+  *max_rel_err = worst;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(A);
+  hipFree(B);
+  hipFree(C);
+  return 0;
+}
+
+int kamd_diag_hbm(int dev, size_t bytes, int iters, double* gbps) {
+  HC(hipSetDevice(dev));
+  void *s = nullptr, *d = nullptr;
+  HC(hipMalloc(&s, bytes));
+  HC(hipMalloc(&d, bytes));
+  HC(hipMemset(s, 1, bytes));
+  kamd_hbm_copy_launch(s, d, bytes, 0);
+  hipEvent_t e0, e1;
+  HC(hipEventCreate(&e0));
+  HC(hipEventCreate(&e1));
+  HC(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) kamd_hbm_copy_launch(s, d, bytes, 0);
+  HC(hipEventRecord(e1, 0));
+  HC(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HC(hipEventElapsedTime(&ms, e0, e1));
+  *gbps = 2.0 * (double)bytes * iters / (ms * 1e-3) / 1e9;  // read + write
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(s);
+  hipFree(d);
+  return 0;
+}
+
+// Persistent per-GPU payload context (warm HIP context + buffers): the stub runtime's
+// "container start" for GPU pods runs vector_add on the pod's device and verifies it.
+struct kamd_payload {
+  int dev;
+  int n;
+  float *a, *b, *c;
+  float* host;
+  hipStream_t stream;
+};
+
+void* kamd_payload_create(int dev, int n) {
+  if (hipSetDevice(dev) != hipSuccess) return nullptr;
+  kamd_payload* p = new kamd_payload();
+  p->dev = dev;
+  p->n = n;
+  size_t bytes = (size_t)n * sizeof(float);
+  if (hipMalloc(&p->a, bytes) != hipSuccess || hipMalloc(&p->b, bytes) != hipSuccess ||
+      hipMalloc(&p->c, bytes) != hipSuccess || hipHostMalloc(&p->host, bytes) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete p;
+    return nullptr;
+  }
+  for (int i = 0; i < n; ++i) p->host[i] = (float)(i % 1000);
+  hipMemcpy(p->a, p->host, bytes, hipMemcpyHostToDevice);
+  hipMemcpy(p->b, p->host, bytes, hipMemcpyHostToDevice);
+  return p;
+}
+
+// Runs one payload; returns 0 if c == a + b on sampled elements.
+int kamd_payload_run(void* h) {
+  kamd_payload* p = (kamd_payload*)h;
+  if (hipSetDevice(p->dev) != hipSuccess) return -1;
+  hipLaunchKernelGGL(vector_add_kernel, dim3((p->n + 255) / 256), dim3(256), 0, p->stream, p->a, p->b, p->c, p->n);
+  float probe[4];
+  const int idx[4] = {0, p->n / 3, p->n / 2, p->n - 1};
+  for (int k = 0; k < 4; ++k)
+    hipMemcpyAsync(&probe[k], p->c + idx[k], sizeof(float), hipMemcpyDeviceToHost, p->stream);
+  if (hipStreamSynchronize(p->stream) != hipSuccess) return -1;
+  for (int k = 0; k < 4; ++k)
+    if (probe[k] != 2.f * (float)(idx[k] % 1000)) return 1;
+  return 0;
+}
+
+void kamd_payload_destroy(void* h) {
+  kamd_payload* p = (kamd_payload*)h;
+  if (!p) return;
+  hipSetDevice(p->dev);
+  hipStreamDestroy(p->stream);
+  hipFree(p->a);
+  hipFree(p->b);
+  hipFree(p->c);
+  hipHostFree(p->host);
+  delete p;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// xgmi-probe — RCCL all-reduce over the GPUs visible to this process (one RCCL rank per GPU,
+// single-process multi-device mode). Reports algorithm and bus bandwidth like rccl-tests:
+// busBW = algBW * 2(n-1)/n. Used as (a) a device-plugin/e2e check that an allocated GPU set
+// really sits in one fully connected xGMI hive and (b) a link-health probe.
+// SURVEY §2.3 "Collective over the GPU fabric".
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#define HIPCHK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+#define NCCLCHK(x) do { ncclResult_t r = (x); if (r != ncclSuccess) { fprintf(stderr, "%s: %s\n", #x, ncclGetErrorString(r)); return 1; } } while (0)
+
+int main(int argc, char** argv) {
+  size_t mib = argc > 1 ? (size_t)atol(argv[1]) : 256;
+  int iters = argc > 2 ? atoi(argv[2]) : 20;
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (n < 1) { fprintf(stderr, "no devices\n"); return 2; }
+  size_t count = mib * (1 << 20) / sizeof(float);
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) devs[i] = i;
+  std::vector<ncclComm_t> comms(n);
+  NCCLCHK(ncclCommInitAll(comms.data(), n, devs.data()));
+  std::vector<float*> buf(n);
+  std::vector<hipStream_t> st(n);
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(i));
+    HIPCHK(hipMalloc(&buf[i], count * sizeof(float)));
+    HIPCHK(hipStreamCreate(&st[i]));
+    std::vector<float> h(1024, (float)(i + 1));
+    for (size_t off = 0; off < count; off += 1024)
+      HIPCHK(hipMemcpy(buf[i] + off, h.data(), sizeof(float) * (count - off < 1024 ? count - off : 1024), hipMemcpyHostToDevice));
+  }
+  auto run = [&](int k) -> int {
+    for (int it = 0; it < k; ++it) {
+      NCCLCHK(ncclGroupStart());
+      for (int i = 0; i < n; ++i) NCCLCHK(ncclAllReduce(buf[i], buf[i], count, ncclFloat, ncclSum, comms[i], st[i]));
+      NCCLCHK(ncclGroupEnd());
+    }
+    for (int i = 0; i < n; ++i) { HIPCHK(hipSetDevice(i)); HIPCHK(hipStreamSynchronize(st[i])); }
+    return 0;
+  };
+  if (run(1)) return 1;
+  // correctness after one all-reduce: every element == n(n+1)/2
+  float expect = (float)n * (n + 1) / 2, got = 0;
+  HIPCHK(hipSetDevice(0));
+  HIPCHK(hipMemcpy(&got, buf[0] + count / 2, sizeof(float), hipMemcpyDeviceToHost));
+  hipEvent_t e0, e1;
+  HIPCHK(hipSetDevice(0));
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, st[0]));
+  if (run(iters)) return 1;
+  HIPCHK(hipSetDevice(0));
+  HIPCHK(hipEventRecord(e1, st[0]));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  double t = ms / 1e3 / iters;
+  double algbw = (double)count * sizeof(float) / t / 1e9;
+  double busbw = n > 1 ? algbw * 2.0 * (n - 1) / n : 0.0;
+  printf("{\"ranks\": %d, \"bytes\": %zu, \"time_us\": %.1f, \"algbw_GBps\": %.2f, \"busbw_GBps\": %.2f, \"correct\": %s}\n",
+         n, count * sizeof(float), t * 1e6, algbw, busbw, got == expect ? "true" : "false");
+  for (int i = 0; i < n; ++i) { ncclCommDestroy(comms[i]); hipSetDevice(i); hipFree(buf[i]); }
+  return got == expect ? 0 : 3;
+}
