@@ -1,0 +1,205 @@
+"""DeviceManager + device plugin protocol (fork F7/F8/F9).
+
+Mirrors the reference's unit tests: `manager_test.go:87-171` (TestManagerPluginHandling: two
+stub plugins, capacity add/remove, health-only changes), `:173` (re-registration),
+`endpoint_test.go`, `device_store_test.go`, `plugin_watcher_test.go:65,119`.
+"""
+import asyncio
+import os
+
+import pytest
+
+from kubernetes_amd.deviceplugin import api
+from kubernetes_amd.deviceplugin.amdgpu import AMDGPUPlugin
+from kubernetes_amd.deviceplugin.server import DevicePluginServer, device
+from kubernetes_amd.kubelet.devicemanager.manager import AdmitError, ManagerImpl
+from kubernetes_amd.kubelet.devicemanager.stores import DeviceStore, merge_init_responses
+from kubernetes_amd.kubelet.devicemanager.watcher import PluginWatcher
+from kubernetes_amd.native import amdsmi
+
+
+async def until(pred, timeout=5.0):
+    t = asyncio.get_running_loop().time() + timeout
+    while not pred():
+        if asyncio.get_running_loop().time() > t:
+            raise TimeoutError("condition not met")
+        await asyncio.sleep(0.01)
+
+
+def test_device_store_diff():
+    s = DeviceStore()
+    a, u, d = s.update([device("a"), device("b")])
+    assert [x.ID for x in a] == ["a", "b"] and not u and not d
+    a, u, d = s.update([device("a", api.UNHEALTHY), device("c")])
+    assert [x.ID for x in a] == ["c"] and [x.ID for x in u] == ["a"] and [x.ID for x in d] == ["b"]
+    a, u, d = s.update([device("a", api.UNHEALTHY), device("c")])
+    assert not a and not u and not d
+
+
+def test_watcher_layout_rules(tmp_path, run):
+    async def main():
+        import socket
+        w = PluginWatcher(str(tmp_path))
+        w.start()
+        os.makedirs(tmp_path / "amd.com")
+        s = socket.socket(socket.AF_UNIX)
+        s.bind(str(tmp_path / "amd.com" / "p.sock"))
+        # a socket in the root is ignored; a directory inside a domain is ignored
+        s2 = socket.socket(socket.AF_UNIX)
+        s2.bind(str(tmp_path / "root.sock"))
+        os.makedirs(tmp_path / "amd.com" / "subdir")
+        p = await asyncio.wait_for(w.added.get(), 5)
+        assert p == str(tmp_path / "amd.com" / "p.sock")
+        os.unlink(tmp_path / "amd.com" / "p.sock")
+        r = await asyncio.wait_for(w.removed.get(), 5)
+        assert r == p
+        assert w.added.empty()
+        w.stop()
+        s.close()
+        s2.close()
+    run(main())
+
+
+def test_manager_plugin_handling(tmp_path, run):
+    async def main():
+        m = ManagerImpl(str(tmp_path))
+        await m.start()
+        p1 = DevicePluginServer("vendor.com/foo", str(tmp_path / "vendor.com" / "foo.sock"),
+                                [device("d1"), device("d2")])
+        p2 = DevicePluginServer("vendor.com/bar", str(tmp_path / "vendor.com" / "bar.sock"), [device("x")])
+        await p1.start()
+        await p2.start()
+        await until(lambda: set(m.get_capacity()[0]) == {"vendor.com/foo", "vendor.com/bar"})
+        await p1.registered.wait()
+        cap, removed = m.get_capacity()
+        assert set(cap["vendor.com/foo"]["resources"]) == {"d1", "d2"} and not removed
+        # health-only change propagates
+        p1.update([device("d1", api.UNHEALTHY), device("d2")])
+        await until(lambda: m.get_capacity()[0]["vendor.com/foo"]["resources"]["d1"]["health"] == api.UNHEALTHY)
+        # deleting every device removes the resource and reports it once
+        p2.update([])
+        await until(lambda: "vendor.com/bar" not in m.get_capacity()[0])
+        # plugin death: stream ends -> devices deleted
+        await p1.stop()
+        await until(lambda: "vendor.com/foo" not in m.get_capacity()[0])
+        await p2.stop()
+        await m.stop()
+    run(main())
+
+
+def test_registration_rejects_wrong_domain_and_version(tmp_path, run):
+    async def main():
+        m = ManagerImpl(str(tmp_path))
+        await m.start()
+        bad = DevicePluginServer("other.com/gpu", str(tmp_path / "amd.com" / "bad.sock"), [device("z")])
+        await bad.start()
+        await until(lambda: bad.registration_status is not None)
+        assert bad.registration_status[0] is False and "domain" in bad.registration_status[1]
+        old = DevicePluginServer("amd.com/gpu", str(tmp_path / "amd.com" / "old.sock"), [device("z")],
+                                 supported_versions=("v1alpha1",))
+        await old.start()
+        await until(lambda: old.registration_status is not None)
+        assert old.registration_status[0] is False
+        assert m.get_capacity()[0] == {}
+        await bad.stop()
+        await old.stop()
+        await m.stop()
+    run(main())
+
+
+def test_reregistration_carries_store(tmp_path, run):
+    async def main():
+        m = ManagerImpl(str(tmp_path))
+        await m.start()
+        p1 = DevicePluginServer("amd.com/gpu", str(tmp_path / "amd.com" / "a.sock"), [device("g0"), device("g1")])
+        await p1.start()
+        await until(lambda: "amd.com/gpu" in m.get_capacity()[0])
+        e1 = m.handler.endpoint("amd.com/gpu")
+        # the same resource re-registers on a new socket with one device changed
+        p2 = DevicePluginServer("amd.com/gpu", str(tmp_path / "amd.com" / "b.sock"), [device("g0"), device("g2")])
+        await p2.start()
+        await until(lambda: m.handler.endpoint("amd.com/gpu") is not e1)
+        await until(lambda: set(m.get_capacity()[0]["amd.com/gpu"]["resources"]) == {"g0", "g2"})
+        # stopping the OLD plugin must not delete the new endpoint's devices
+        await p1.stop()
+        await asyncio.sleep(0.2)
+        assert set(m.get_capacity()[0]["amd.com/gpu"]["resources"]) == {"g0", "g2"}
+        await p2.stop()
+        await m.stop()
+    run(main())
+
+
+def _pod(uid, assigned, name="p"):
+    return {"metadata": {"name": name, "namespace": "default", "uid": uid},
+            "spec": {"containers": [{"name": "c", "extendedResourceRequests": ["er1"]}],
+                     "extendedResources": [{"name": "er1", "resources": {"limits": {"amd.com/gpu": str(len(assigned))},
+                                                                         "requests": {"amd.com/gpu": str(len(assigned))}},
+                                            "assigned": assigned}]}}
+
+
+def test_amdgpu_plugin_admit_and_init_container(tmp_path, run):
+    async def main():
+        smi = amdsmi.SMI(fixture=amdsmi.fixture_file(8))
+        plugin = AMDGPUPlugin(str(tmp_path), smi=smi, health_interval=0, dev_root="/dev")
+        ids = [g.device_id_str for g in plugin.gpus]
+        active = []
+        m = ManagerImpl(str(tmp_path))
+        await m.start(lambda: active)
+        await plugin.start()
+        await until(lambda: "amd.com/gpu" in m.get_capacity()[0])
+        cap = m.get_capacity()[0]["amd.com/gpu"]["resources"]
+        assert len(cap) == 8
+        attrs = cap[ids[2]]["attributes"]
+        assert attrs["amd.com/arch"] == "gfx950" and attrs["amd.com/product"] == "MI355X"
+        assert attrs["amd.com/memory"] == "294912" and attrs["amd.com/hbm"] == "288Gi"
+        assert attrs["amd.com/render-minor"] == "130"
+        pod = _pod("u1", [ids[1], ids[2]])
+        await m.admit_pod(pod)
+        active.append(pod)
+        assert m.pod_resources(pod)["annotations"]["amd.com/gpu-devices"] == f"{ids[1]},{ids[2]}"
+        opts = await m.init_container(pod, pod["spec"]["containers"][0])
+        paths = [d["pathOnHost"] for d in opts["devices"]]
+        assert paths == ["/dev/kfd", "/dev/dri/renderD129", "/dev/dri/renderD130"]
+        envs = {e["name"]: e["value"] for e in opts["envs"]}
+        assert envs["AMD_VISIBLE_DEVICES"] == "1,2" and envs["AMD_GPU_ARCH"] == "gfx950"
+        # duplicate assignment to a second active pod is rejected by the kubelet
+        with pytest.raises(AdmitError):
+            await m.admit_pod(_pod("u2", [ids[2]], "q"))
+        # unknown / unhealthy devices are rejected
+        with pytest.raises(AdmitError):
+            await m.admit_pod(_pod("u3", ["GPU-nope"], "r"))
+        smi.fake_set_ecc(5, 3)
+        assert plugin.poll_health()
+        await until(lambda: m.get_capacity()[0]["amd.com/gpu"]["resources"][ids[5]]["health"] == api.UNHEALTHY)
+        with pytest.raises(AdmitError):
+            await m.admit_pod(_pod("u4", [ids[5]], "s"))
+        smi.fake_set_ecc(5, 0)
+        await plugin.stop()
+        await m.stop()
+    run(main())
+
+
+def test_admit_waits_for_plugin_after_restart(tmp_path, run):
+    async def main():
+        m = ManagerImpl(str(tmp_path), registration_grace=5.0)
+        await m.start()
+        plugin = DevicePluginServer("amd.com/gpu", str(tmp_path / "amd.com" / "g.sock"), [device("g0")])
+
+        async def late():
+            await asyncio.sleep(0.3)
+            await plugin.start()
+        t = asyncio.ensure_future(late())
+        await m.admit_pod(_pod("u1", ["g0"]))  # would fail immediately in the reference
+        await t
+        await plugin.stop()
+        await m.stop()
+    run(main())
+
+
+def test_merge_init_responses_first_wins():
+    R = api.DP["InitContainerResponse"]
+    r1 = R(spec=api.DP["ContainerSpec"](envs={"A": "1"}, devices=[api.DP["DeviceSpec"](container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")]))
+    r2 = R(spec=api.DP["ContainerSpec"](envs={"A": "2", "B": "3"}, devices=[api.DP["DeviceSpec"](container_path="/dev/kfd", host_path="/dev/other")]))
+    o = merge_init_responses([r1, r2])
+    assert o["envs"] == [{"name": "A", "value": "1"}, {"name": "B", "value": "3"}]
+    assert [d["pathOnHost"] for d in o["devices"]] == ["/dev/kfd"]
