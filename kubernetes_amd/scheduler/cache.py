@@ -1,0 +1,320 @@
+"""Scheduler cache: NodeInfo aggregation, the fork's per-device ER manager, assumed pods.
+
+Parity:
+  * `plugin/pkg/scheduler/schedulercache/cache.go:40-462` — AssumePod / FinishBinding /
+    ForgetPod / AddPod / UpdatePod / RemovePod, assumed-pod TTL expiry, node add/update/remove.
+  * `plugin/pkg/scheduler/schedulercache/node_info.go` — requested / non-zero requested /
+    allocatable, host ports, taints, conditions, generation.
+  * `plugin/pkg/scheduler/schedulercache/extended_resources.go:25-210` (fork F5) — per node
+    allocatable / available / used device maps; SetNode reconciles from
+    `Node.status.extendedResources`; AddPod / RemovePod move `Assigned` IDs.
+
+Fixes: assumed pods carry their device assignment (item 1) so back-to-back
+bin-packing can never double-assign; the reference deep-copied `Available()` per node per
+pod — here allocation works on the live map with a scratch "taken" set (item 9);
+RemoveNode actually drops state (quirk Q8).
+"""
+from __future__ import annotations
+
+import time
+
+from ..api import core
+from ..api.meta import ns_name
+from ..api.quantity import Quantity, parse_quantity
+
+DEFAULT_MILLI_CPU = 100                 # priorities/util/non_zero.go
+DEFAULT_MEMORY = 200 * 1024 * 1024
+
+
+def _q(v) -> Quantity:
+    return parse_quantity(v) if isinstance(v, str) else Quantity(v)
+
+
+class PodInfo:
+    """Parsed, cached resource view of a pod (computed once per pod version)."""
+    __slots__ = ("milli_cpu", "memory", "ephemeral", "scalars", "nz_cpu", "nz_mem", "ports", "er", "assigned")
+
+    def __init__(self, pod):
+        req = core.pod_requests(pod)
+        self.milli_cpu = req["cpu"].milli_value() if "cpu" in req else 0
+        self.memory = req["memory"].int_value() if "memory" in req else 0
+        self.ephemeral = req["ephemeral-storage"].int_value() if "ephemeral-storage" in req else 0
+        self.scalars = {k: v.int_value() for k, v in req.items()
+                        if k not in ("cpu", "memory", "ephemeral-storage", "pods")}
+        self.nz_cpu = self.milli_cpu or DEFAULT_MILLI_CPU
+        self.nz_mem = self.memory or DEFAULT_MEMORY
+        spec = pod.get("spec") or {}
+        ports = []
+        for c in spec.get("containers") or ():
+            for p in c.get("ports") or ():
+                if p.get("hostPort"):
+                    ports.append((p.get("hostIP", "0.0.0.0"), p.get("protocol", "TCP"), p["hostPort"]))
+        self.ports = ports
+        er = []
+        for per in spec.get("extendedResources") or ():
+            try:
+                rn = core.pod_extended_resource_name(per)
+                n = core.pod_extended_resource_count(per)
+            except (ValueError, KeyError):
+                continue
+            er.append((per.get("name"), rn, n, (per.get("affinity") or {}).get("required") or []))
+        self.er = er
+        self.assigned = core.pod_assigned_devices(pod)
+
+
+class ERManager:
+    def __init__(self):
+        self.allocatable: dict[str, dict[str, dict]] = {}
+        self.available: dict[str, dict[str, dict]] = {}
+        self.used: dict[str, dict[str, str]] = {}     # rname -> {device id: pod key}
+
+    def clone(self):
+        c = ERManager()
+        c.allocatable = {k: dict(v) for k, v in self.allocatable.items()}
+        c.available = {k: dict(v) for k, v in self.available.items()}
+        c.used = {k: dict(v) for k, v in self.used.items()}
+        return c
+
+    def add_pod(self, key, assigned: dict):
+        for rn, ids in assigned.items():
+            used = self.used.setdefault(rn, {})
+            avail = self.available.get(rn)
+            for i in ids:
+                used[i] = key
+                if avail is not None:
+                    avail.pop(i, None)
+
+    def remove_pod(self, key, assigned: dict):
+        for rn, ids in assigned.items():
+            used = self.used.get(rn)
+            if not used:
+                continue
+            alloc = self.allocatable.get(rn, {})
+            avail = self.available.setdefault(rn, {})
+            for i in ids:
+                if used.get(i) == key:
+                    del used[i]
+                    if i in alloc:
+                        avail[i] = alloc[i]
+            if not used:
+                del self.used[rn]
+
+    def set_node(self, node):
+        ers = ((node.get("status") or {}).get("extendedResources")) or {}
+        self.allocatable = {rn: dict((dom or {}).get("resources") or {}) for rn, dom in ers.items()}
+        self.available = {}
+        for rn, devs in self.allocatable.items():
+            used = self.used.get(rn, {})
+            self.available[rn] = {i: d for i, d in devs.items() if i not in used}
+
+    def free_count(self, rname, healthy_only=True) -> int:
+        avail = self.available.get(rname)
+        if not avail:
+            return 0
+        if not healthy_only:
+            return len(avail)
+        return sum(1 for d in avail.values() if d.get("health", core.HEALTHY) == core.HEALTHY)
+
+
+class NodeInfo:
+    __slots__ = ("node", "name", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
+                 "req_cpu", "req_mem", "req_eph", "req_scalars", "nz_cpu", "nz_mem", "pods", "ports", "er", "generation",
+                 "ready", "unschedulable", "mem_pressure", "disk_pressure", "gpu_total")
+
+    def __init__(self, name=""):
+        self.node = None
+        self.name = name
+        self.labels = {}
+        self.taints = []
+        self.alloc_cpu = self.alloc_mem = self.alloc_eph = self.alloc_pods = 0
+        self.alloc_scalars = {}
+        self.req_cpu = self.req_mem = self.req_eph = 0
+        self.req_scalars = {}
+        self.nz_cpu = self.nz_mem = 0
+        self.pods: dict[str, tuple] = {}   # key -> (pod, PodInfo)
+        self.ports = set()
+        self.er = ERManager()
+        self.generation = 0
+        self.ready = True
+        self.unschedulable = False
+        self.mem_pressure = False
+        self.disk_pressure = False
+        self.gpu_total = 0
+
+    def set_node(self, node):
+        self.node = node
+        self.name = node["metadata"]["name"]
+        self.labels = node["metadata"].get("labels") or {}
+        spec = node.get("spec") or {}
+        st = node.get("status") or {}
+        self.taints = spec.get("taints") or []
+        self.unschedulable = bool(spec.get("unschedulable"))
+        alloc = st.get("allocatable") or st.get("capacity") or {}
+        self.alloc_cpu = _q(alloc["cpu"]).milli_value() if "cpu" in alloc else 0
+        self.alloc_mem = _q(alloc["memory"]).int_value() if "memory" in alloc else 0
+        self.alloc_eph = _q(alloc["ephemeral-storage"]).int_value() if "ephemeral-storage" in alloc else 0
+        self.alloc_pods = _q(alloc["pods"]).int_value() if "pods" in alloc else 110
+        self.alloc_scalars = {k: _q(v).int_value() for k, v in alloc.items()
+                              if k not in ("cpu", "memory", "ephemeral-storage", "pods")}
+        self.ready = True
+        self.mem_pressure = self.disk_pressure = False
+        for c in st.get("conditions") or ():
+            t, s = c.get("type"), c.get("status")
+            if t == "Ready":
+                self.ready = s == "True"
+            elif t == "MemoryPressure":
+                self.mem_pressure = s == "True"
+            elif t == "DiskPressure":
+                self.disk_pressure = s == "True"
+        self.er.set_node(node)
+        self.gpu_total = len(self.er.allocatable.get(core.AMD_GPU, {}))
+        self.generation += 1
+
+    def add_pod(self, key, pod, pi: PodInfo):
+        if key in self.pods:
+            self.remove_pod(key)
+        self.pods[key] = (pod, pi)
+        self.req_cpu += pi.milli_cpu
+        self.req_mem += pi.memory
+        self.req_eph += pi.ephemeral
+        for k, v in pi.scalars.items():
+            self.req_scalars[k] = self.req_scalars.get(k, 0) + v
+        self.nz_cpu += pi.nz_cpu
+        self.nz_mem += pi.nz_mem
+        for p in pi.ports:
+            self.ports.add(p)
+        self.er.add_pod(key, pi.assigned)
+        self.generation += 1
+
+    def remove_pod(self, key):
+        ent = self.pods.pop(key, None)
+        if ent is None:
+            return False
+        _, pi = ent
+        self.req_cpu -= pi.milli_cpu
+        self.req_mem -= pi.memory
+        self.req_eph -= pi.ephemeral
+        for k, v in pi.scalars.items():
+            self.req_scalars[k] = self.req_scalars.get(k, 0) - v
+        self.nz_cpu -= pi.nz_cpu
+        self.nz_mem -= pi.nz_mem
+        for p in pi.ports:
+            self.ports.discard(p)
+        self.er.remove_pod(key, pi.assigned)
+        self.generation += 1
+        return True
+
+
+class SchedulerCache:
+    def __init__(self, assumed_ttl=30.0):
+        self.nodes: dict[str, NodeInfo] = {}
+        self.pod_states: dict[str, tuple] = {}   # key -> (pod, node name)
+        self.assumed: dict[str, float] = {}      # key -> deadline (0 until binding finished)
+        self.ttl = assumed_ttl
+        self.anti_pods: dict[str, dict] = {}     # pods with required anti-affinity (symmetry check)
+
+    def _track(self, key, pod):
+        aff = ((pod.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
+        if aff.get("requiredDuringSchedulingIgnoredDuringExecution"):
+            self.anti_pods[key] = pod
+        else:
+            self.anti_pods.pop(key, None)
+
+    def _node(self, name):
+        ni = self.nodes.get(name)
+        if ni is None:
+            ni = self.nodes[name] = NodeInfo(name)
+        return ni
+
+    # -- pods ---------------------------------------------------------------
+    def assume_pod(self, pod):
+        key = ns_name(pod)
+        if key in self.pod_states:
+            raise ValueError(f"pod {key} is in the cache, so can't be assumed")
+        node = pod["spec"]["nodeName"]
+        self._node(node).add_pod(key, pod, PodInfo(pod))
+        self.pod_states[key] = (pod, node)
+        self.assumed[key] = 0.0
+        self._track(key, pod)
+
+    def finish_binding(self, pod):
+        key = ns_name(pod)
+        if key in self.assumed:
+            self.assumed[key] = time.monotonic() + self.ttl
+
+    def forget_pod(self, pod):
+        key = ns_name(pod)
+        st = self.pod_states.get(key)
+        if st is None or key not in self.assumed:
+            return
+        self._node(st[1]).remove_pod(key)
+        del self.pod_states[key]
+        del self.assumed[key]
+        self.anti_pods.pop(key, None)
+
+    def add_pod(self, pod):
+        """Confirmed (bound) pod from the informer. An assumed pod is replaced by the API
+        object; unlike the reference (cache.go:232-245) its devices are re-added, which is a
+        no-op when the assumed copy already carried them (our assume() sets them)."""
+        key = ns_name(pod)
+        node = pod["spec"]["nodeName"]
+        st = self.pod_states.get(key)
+        if st is not None:
+            self._node(st[1]).remove_pod(key)
+        self._node(node).add_pod(key, pod, PodInfo(pod))
+        self.pod_states[key] = (pod, node)
+        self.assumed.pop(key, None)
+        self._track(key, pod)
+
+    def update_pod(self, old, new):
+        self.add_pod(new)
+
+    def remove_pod(self, pod):
+        key = ns_name(pod)
+        st = self.pod_states.pop(key, None)
+        self.assumed.pop(key, None)
+        self.anti_pods.pop(key, None)
+        if st is not None:
+            ni = self.nodes.get(st[1])
+            if ni is not None:
+                ni.remove_pod(key)
+                if ni.node is None and not ni.pods:
+                    del self.nodes[st[1]]
+
+    def is_assumed(self, pod):
+        return ns_name(pod) in self.assumed
+
+    def get_pod(self, key):
+        st = self.pod_states.get(key)
+        return st[0] if st else None
+
+    def cleanup_expired(self, now=None):
+        now = time.monotonic() if now is None else now
+        for key, dl in list(self.assumed.items()):
+            if dl and dl < now:
+                pod, node = self.pod_states[key]
+                self._node(node).remove_pod(key)
+                del self.pod_states[key]
+                del self.assumed[key]
+
+    # -- nodes --------------------------------------------------------------
+    def add_node(self, node):
+        self._node(node["metadata"]["name"]).set_node(node)
+
+    update_node = lambda self, old, new: self.add_node(new)  # noqa: E731
+
+    def remove_node(self, node):
+        name = node["metadata"]["name"]
+        ni = self.nodes.get(name)
+        if ni is None:
+            return
+        if ni.pods:
+            # keep pod accounting until the pods are deleted (cache.go RemoveNode)
+            ni.node = None
+            ni.er = ERManager()
+            ni.generation += 1
+        else:
+            del self.nodes[name]
+
+    def node_list(self):
+        return [ni for ni in self.nodes.values() if ni.node is not None]

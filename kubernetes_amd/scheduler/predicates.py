@@ -1,0 +1,188 @@
+"""Fit predicates. Parity: `plugin/pkg/scheduler/algorithm/predicates/predicates.go:202-1465`
+(PodFitsResources :583-690, GeneralPredicates :965, host ports, node selector/affinity, taints,
+memory/disk pressure, node condition, inter-pod affinity) and the default provider set
+(`plugin/pkg/scheduler/algorithmprovider/defaults/defaults.go:67-255`).
+
+Every predicate has signature `(pod, PodInfo, NodeInfo, ctx) -> reason or None`.
+"""
+from __future__ import annotations
+
+from ..api import core
+from ..api.labels import SelectorError, label_selector_as_selector, node_selector_requirements_as_selector
+
+
+def check_node_condition(pod, pi, ni, ctx):
+    if not ni.ready:
+        return "node(s) were not ready"
+    if ni.unschedulable and not ctx.tolerates_unschedulable:
+        return "node(s) were unschedulable"
+    return None
+
+
+def pod_fits_resources(pod, pi, ni, ctx):
+    if len(ni.pods) + 1 > ni.alloc_pods:
+        return "Insufficient pods"
+    if pi.milli_cpu and ni.req_cpu + pi.milli_cpu > ni.alloc_cpu:
+        return "Insufficient cpu"
+    if pi.memory and ni.req_mem + pi.memory > ni.alloc_mem:
+        return "Insufficient memory"
+    if pi.ephemeral and ni.alloc_eph and ni.req_eph + pi.ephemeral > ni.alloc_eph:
+        return "Insufficient ephemeral-storage"
+    for k, v in pi.scalars.items():
+        if ni.req_scalars.get(k, 0) + v > ni.alloc_scalars.get(k, 0):
+            return f"Insufficient {k}"
+    return None
+
+
+def pod_fits_host(pod, pi, ni, ctx):
+    want = (pod.get("spec") or {}).get("nodeName")
+    if want and want != ni.name:
+        return "node(s) didn't match the requested hostname"
+    return None
+
+
+def pod_fits_host_ports(pod, pi, ni, ctx):
+    for ip, proto, port in pi.ports:
+        for oip, oproto, oport in ni.ports:
+            if oport == port and oproto == proto and (ip == oip or "0.0.0.0" in (ip, oip)):
+                return "node(s) didn't have free ports for the requested pod ports"
+    return None
+
+
+def _node_affinity_terms(pod):
+    aff = ((pod.get("spec") or {}).get("affinity") or {}).get("nodeAffinity") or {}
+    req = aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
+    return req.get("nodeSelectorTerms")
+
+
+def _term_matches(term, ni):
+    exprs = term.get("matchExpressions") or []
+    fields = term.get("matchFields") or []
+    if not exprs and not fields:
+        return False
+    if exprs:
+        try:
+            if not node_selector_requirements_as_selector(exprs).matches(ni.labels):
+                return False
+        except SelectorError:
+            return False
+    for f in fields:
+        if f.get("key") == "metadata.name":
+            vals = f.get("values") or []
+            op = f.get("operator")
+            if (op == "In" and ni.name not in vals) or (op == "NotIn" and ni.name in vals):
+                return False
+    return True
+
+
+def match_node_selector(pod, pi, ni, ctx):
+    spec = pod.get("spec") or {}
+    ns = spec.get("nodeSelector")
+    if ns:
+        labels = ni.labels
+        for k, v in ns.items():
+            if labels.get(k) != v:
+                return "node(s) didn't match node selector"
+    terms = _node_affinity_terms(pod)
+    if terms is not None:
+        if not any(_term_matches(t, ni) for t in terms):
+            return "node(s) didn't match node selector"
+    return None
+
+
+def pod_tolerates_node_taints(pod, pi, ni, ctx):
+    if not ni.taints:
+        return None
+    tols = (pod.get("spec") or {}).get("tolerations") or []
+    for t in ni.taints:
+        if t.get("effect") not in (core.TAINT_NO_SCHEDULE, core.TAINT_NO_EXECUTE):
+            continue
+        if not core.tolerates(tols, t):
+            return "node(s) had taints that the pod didn't tolerate"
+    return None
+
+
+def check_node_memory_pressure(pod, pi, ni, ctx):
+    if ni.mem_pressure and pi.milli_cpu == 0 and pi.memory == 0:
+        return "node(s) had memory pressure"
+    return None
+
+
+def check_node_disk_pressure(pod, pi, ni, ctx):
+    if ni.disk_pressure:
+        return "node(s) had disk pressure"
+    return None
+
+
+def _pod_matches_term(pod_labels, pod_ns, term, owner_ns):
+    nss = term.get("namespaces") or [owner_ns]
+    if pod_ns not in nss:
+        return False
+    try:
+        return label_selector_as_selector(term.get("labelSelector")).matches(pod_labels)
+    except SelectorError:
+        return False
+
+
+def match_inter_pod_affinity(pod, pi, ni, ctx):
+    """Required pod (anti-)affinity by topologyKey; also honours existing pods' anti-affinity."""
+    spec = pod.get("spec") or {}
+    aff = spec.get("affinity") or {}
+    pa = (aff.get("podAffinity") or {}).get("requiredDuringSchedulingIgnoredDuringExecution") or []
+    paa = (aff.get("podAntiAffinity") or {}).get("requiredDuringSchedulingIgnoredDuringExecution") or []
+    ns = pod["metadata"].get("namespace", "default")
+    labels = pod["metadata"].get("labels") or {}
+    if not pa and not paa and not ctx.any_anti_affinity:
+        return None
+    by_topo = ctx.pods_by_topology
+    for term in pa:
+        key = term.get("topologyKey", "")
+        val = ni.labels.get(key)
+        if val is None:
+            return "node(s) didn't match pod affinity rules"
+        ok = any(_pod_matches_term(p["metadata"].get("labels") or {}, p["metadata"].get("namespace"), term, ns)
+                 for p in by_topo(key, val))
+        if not ok:
+            # the first pod of a group may land anywhere if it matches its own term and no
+            # other pod in the cluster does (predicates.go satisfiesPodsAffinityAntiAffinity)
+            if ctx.any_pod_matches(term, ns) or not _pod_matches_term(labels, ns, term, ns):
+                return "node(s) didn't match pod affinity rules"
+    for term in paa:
+        key = term.get("topologyKey", "")
+        val = ni.labels.get(key)
+        if val is None:
+            continue
+        for p in by_topo(key, val):
+            if _pod_matches_term(p["metadata"].get("labels") or {}, p["metadata"].get("namespace"), term, ns):
+                return "node(s) didn't match pod anti-affinity rules"
+    # symmetric: existing pods' anti-affinity against this pod
+    if ctx.any_anti_affinity:
+        for p, term in ctx.anti_affinity_terms:
+            key = term.get("topologyKey", "")
+            val = ni.labels.get(key)
+            if val is None:
+                continue
+            pnode = ctx.node_of(p)
+            if pnode is None or pnode.labels.get(key) != val:
+                continue
+            if _pod_matches_term(labels, ns, term, p["metadata"].get("namespace", "default")):
+                return "node(s) didn't satisfy existing pods anti-affinity rules"
+    return None
+
+
+PREDICATES = {
+    "CheckNodeCondition": check_node_condition,
+    "HostName": pod_fits_host,
+    "PodFitsResources": pod_fits_resources,
+    "PodFitsHostPorts": pod_fits_host_ports,
+    "MatchNodeSelector": match_node_selector,
+    "PodToleratesNodeTaints": pod_tolerates_node_taints,
+    "CheckNodeMemoryPressure": check_node_memory_pressure,
+    "CheckNodeDiskPressure": check_node_disk_pressure,
+    "MatchInterPodAffinity": match_inter_pod_affinity,
+}
+
+# evaluation order: cheap & selective first (predicates ordering in later reference versions)
+DEFAULT_PREDICATES = ["CheckNodeCondition", "HostName", "PodFitsResources", "MatchNodeSelector",
+                      "PodFitsHostPorts", "PodToleratesNodeTaints", "CheckNodeMemoryPressure",
+                      "CheckNodeDiskPressure", "MatchInterPodAffinity"]

@@ -1,0 +1,231 @@
+"""kube-scheduler equivalent: informers → queue → scheduleOne → assume → async bind.
+
+Parity: `plugin/pkg/scheduler/scheduler.go:170-497` (`Run`, `scheduleOne`, `schedule`, `assume`,
+`bind` in a goroutine), the factory's informer wiring and cache handlers
+(`plugin/pkg/scheduler/factory/factory.go:554-829`, scheduled-pod field selector
+`spec.nodeName!=,status.phase!=Succeeded,status.phase!=Failed`), the binder with the fork's
+`Target.ExtendedResources` (`scheduler.go:481-492`, `factory.go:1241-1244`), events
+`Scheduled` / `FailedScheduling` and the metrics of `plugin/pkg/scheduler/metrics/metrics.go:33-50`.
+
+Fix: `assume()` writes the device binding into the assumed pod's
+`spec.extendedResources[].assigned` before `AssumePod`, so the cache reserves those devices
+immediately and the next pod in the same burst cannot receive them.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+
+from ..api import core
+from ..api.meta import fast_copy, ns_name, now_rfc3339
+from ..client.events import EventRecorder
+from ..client.informer import Informer
+from ..client.rest import APIStatusError, is_not_found
+from ..utils.httpserver import HTTPServer, Response
+from ..utils.metrics import MICRO_BUCKETS, Registry
+from .cache import SchedulerCache
+from .generic import FitError, GenericScheduler
+from .queue import SchedulingQueue
+
+log = logging.getLogger("scheduler")
+
+DEFAULT_SCHEDULER = "default-scheduler"
+
+
+class Scheduler:
+    def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
+                 percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
+                 update_unschedulable_status=True):
+        self.client = client
+        self.name = scheduler_name
+        self.cache = SchedulerCache()
+        self.queue = SchedulingQueue()
+        self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
+        self.recorder = EventRecorder(client, scheduler_name, enabled=emit_events)
+        self.update_unschedulable_status = update_unschedulable_status
+        self.metrics = Registry()
+        self.m_e2e = self.metrics.histogram("scheduler_e2e_scheduling_latency_microseconds",
+                                            "E2e scheduling latency (scheduling algorithm + binding)", (), MICRO_BUCKETS)
+        self.m_algo = self.metrics.histogram("scheduler_scheduling_algorithm_latency_microseconds",
+                                             "Scheduling algorithm latency", (), MICRO_BUCKETS)
+        self.m_bind = self.metrics.histogram("scheduler_binding_latency_microseconds", "Binding latency", (), MICRO_BUCKETS)
+        self.m_attempts = self.metrics.counter("scheduler_schedule_attempts_total", "Scheduling attempts", ("result",))
+        self.m_pending = self.metrics.gauge("scheduler_pending_pods", "Pods in the scheduling queue", ("queue",))
+        self.scheduled = 0
+        self.bind_sem = asyncio.Semaphore(max_binds_in_flight)
+        self._tasks = []
+        self._binds = set()
+        self.http = None
+        self.pod_informer = Informer(client, "pods", field_selector="status.phase!=Succeeded,status.phase!=Failed")
+        self.node_informer = Informer(client, "nodes")
+
+    # -- informer handlers -------------------------------------------------
+    def _responsible(self, pod):
+        return (pod.get("spec") or {}).get("schedulerName", DEFAULT_SCHEDULER) == self.name
+
+    def _on_pod_add(self, pod):
+        if (pod.get("spec") or {}).get("nodeName"):
+            self.cache.add_pod(pod)
+            return
+        if self._responsible(pod) and not pod["metadata"].get("deletionTimestamp"):
+            self.queue.add(pod)
+
+    def _on_pod_update(self, old, new):
+        assigned_new = bool((new.get("spec") or {}).get("nodeName"))
+        if assigned_new:
+            if not (old.get("spec") or {}).get("nodeName"):
+                self.queue.delete(old)
+            self.cache.add_pod(new)
+            return
+        if self._responsible(new):
+            if new["metadata"].get("deletionTimestamp"):
+                self.queue.delete(new)
+            else:
+                self.queue.update(old, new)
+
+    def _on_pod_delete(self, pod):
+        if (pod.get("spec") or {}).get("nodeName") or self.cache.get_pod(ns_name(pod)) is not None:
+            self.cache.remove_pod(pod)
+            self.queue.move_all_to_active()   # capacity was freed
+        else:
+            self.queue.delete(pod)
+
+    def _on_node_add(self, node):
+        self.cache.add_node(node)
+        self.queue.move_all_to_active()
+
+    def _on_node_update(self, old, new):
+        self.cache.add_node(new)
+        if _node_capacity_changed(old, new):
+            self.queue.move_all_to_active()
+
+    def _on_node_delete(self, node):
+        self.cache.remove_node(node)
+
+    # -- scheduling loop ---------------------------------------------------------
+    async def run(self, metrics_port=None):
+        self.recorder.start()
+        self.node_informer.add_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
+        self.pod_informer.add_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
+        self.node_informer.start()
+        await self.node_informer.wait_synced(60)
+        self.pod_informer.start()
+        await self.pod_informer.wait_synced(60)
+        if metrics_port is not None:
+            self.http = HTTPServer(self._http)
+            await self.http.start("127.0.0.1", metrics_port)
+        self._tasks.append(asyncio.ensure_future(self._housekeeping()))
+        while True:
+            ent = await self.queue.pop()
+            if ent is None:
+                return
+            self.schedule_one(*ent[:2])
+            # yield so informer deliveries and bind completions interleave with the loop
+            await asyncio.sleep(0)
+
+    async def _housekeeping(self):
+        while True:
+            await asyncio.sleep(1.0)
+            self.cache.cleanup_expired()
+            self.queue.flush_unschedulable_leftover()
+            self.m_pending.labels("active").set(len(self.queue.active))
+            self.m_pending.labels("unschedulable").set(len(self.queue.unschedulable))
+
+    def schedule_one(self, pod, pi):
+        t0 = time.perf_counter()
+        try:
+            host, erb = self.algo.schedule(pod, pi)
+        except FitError as e:
+            self.m_attempts.labels("unschedulable").inc()
+            self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
+            self.queue.add_unschedulable(pod)
+            if self.update_unschedulable_status:
+                asyncio.ensure_future(self._set_unschedulable(pod, str(e)))
+            return None
+        except Exception as e:  # pragma: no cover - defensive
+            log.exception("scheduling %s failed", ns_name(pod))
+            self.m_attempts.labels("error").inc()
+            self.queue.add_backoff(pod)
+            self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
+            return None
+        self.m_algo.observe((time.perf_counter() - t0) * 1e6)
+        assumed = fast_copy(pod)
+        assumed["spec"]["nodeName"] = host
+        for per in assumed["spec"].get("extendedResources") or ():
+            got = erb.get(per.get("name"))
+            if got is not None:
+                per["assigned"] = list(got["resources"])
+        try:
+            self.cache.assume_pod(assumed)
+        except ValueError as e:
+            log.warning("assume failed: %s", e)
+            return None
+        t = asyncio.ensure_future(self._bind(pod, assumed, host, erb, t0))
+        self._binds.add(t)
+        t.add_done_callback(self._binds.discard)
+        return host
+
+    async def _bind(self, pod, assumed, host, erb, t0):
+        md = pod["metadata"]
+        async with self.bind_sem:
+            tb = time.perf_counter()
+            try:
+                await self.client.bind(md.get("namespace", "default"), md["name"], host, erb or None)
+            except (APIStatusError, ConnectionError, OSError, asyncio.TimeoutError) as e:
+                self.cache.forget_pod(assumed)
+                self.m_attempts.labels("error").inc()
+                self.recorder.event(pod, "Warning", "FailedScheduling", f"Binding rejected: {e}")
+                if not (isinstance(e, APIStatusError) and is_not_found(e)):
+                    self.queue.add_backoff(pod)
+                return
+            self.cache.finish_binding(assumed)
+        now = time.perf_counter()
+        self.m_bind.observe((now - tb) * 1e6)
+        self.m_e2e.observe((now - t0) * 1e6)
+        self.m_attempts.labels("scheduled").inc()
+        self.scheduled += 1
+        self.queue.backoff.forget(ns_name(pod))
+        self.recorder.event(pod, "Normal", "Scheduled", f"Successfully assigned {md['name']} to {host}")
+
+    async def _set_unschedulable(self, pod, msg):
+        md = pod["metadata"]
+        cond = {"type": core.COND_POD_SCHEDULED, "status": "False", "reason": "Unschedulable", "message": msg,
+                "lastProbeTime": None, "lastTransitionTime": now_rfc3339()}
+        old = core.get_condition(pod.get("status"), core.COND_POD_SCHEDULED)
+        if old and old.get("status") == "False" and old.get("message") == msg:
+            return
+        try:
+            await self.client.patch("pods", md["name"], {"status": {"conditions": [cond]}}, md.get("namespace"),
+                                    "strategic", "status")
+        except Exception as e:
+            log.debug("could not update pod condition: %s", e)
+
+    async def _http(self, req):
+        if req.path == "/metrics":
+            return Response(200, self.metrics.render(), "text/plain; version=0.0.4")
+        if req.path == "/healthz":
+            return Response(200, b"ok", "text/plain")
+        return Response(404, b"not found", "text/plain")
+
+    async def stop(self):
+        self.queue.close()
+        for t in self._tasks:
+            t.cancel()
+        self.pod_informer.stop()
+        self.node_informer.stop()
+        self.recorder.stop()
+        if self.http:
+            await self.http.stop()
+
+    async def wait_binds(self):
+        while self._binds:
+            await asyncio.gather(*list(self._binds), return_exceptions=True)
+
+
+def _node_capacity_changed(old, new):
+    os_, ns = old.get("status") or {}, new.get("status") or {}
+    return (os_.get("allocatable") != ns.get("allocatable") or os_.get("extendedResources") != ns.get("extendedResources")
+            or (old.get("spec") or {}) != (new.get("spec") or {})
+            or old["metadata"].get("labels") != new["metadata"].get("labels")
+            or [c.get("status") for c in os_.get("conditions") or ()] != [c.get("status") for c in ns.get("conditions") or ()])

@@ -1,0 +1,132 @@
+"""Topology-aware extended-resource (device) allocator — the scheduler's ER step (fork F4),
+re-designed for MI355X xGMI hives.
+
+Reference behaviour (`plugin/pkg/scheduler/core/extended_resources.go:42-183`): for every
+surviving node, greedily take the first N devices (Go map iteration order) that match the
+pod's attribute selector; no health check; no topology.
+
+MI355X-first design:
+  * only Healthy devices are candidates (the kubelet would reject the others anyway);
+  * selectors are quantity-aware (`amd.com/hbm Gt 256Gi`, `amd.com/memory Gt 200000`);
+  * an N-GPU request is placed inside ONE xGMI hive — RCCL rings are per-link bound, so an
+    N-GPU job wants N GPUs that can drive N-1 links each. The hive with the fewest free
+    devices that still fits is chosen (best fit: keeps whole hives free for big jobs);
+    inside it, a NUMA node that holds the whole set is preferred; every chosen device must
+    report at least N-1 healthy xGMI links;
+  * single-GPU pods pack into the most-used hive / NUMA node first (anti-fragmentation);
+  * `amd.com/xgmi-policy` pod annotation: `required` (fail rather than span hives) or
+    `preferred` (default: span hives only when no single hive fits, with a low score);
+  * deterministic order (device index) instead of map order.
+Returns a binding `{er_name: {"resources": [ids]}}` plus a 0..10 topology score used by the
+`XGMITopology` priority.
+"""
+from __future__ import annotations
+
+from ..api import core
+from ..api.labels import SelectorError, node_selector_requirements_as_selector
+
+POLICY_ANNOTATION = "amd.com/xgmi-policy"
+REQUIRED, PREFERRED = "required", "preferred"
+
+
+class Request:
+    """One pod-level extended resource request, with its selector compiled once."""
+    __slots__ = ("name", "rname", "count", "selector", "error")
+
+    def __init__(self, name, rname, count, required):
+        self.name, self.rname, self.count = name, rname, count
+        self.error = None
+        try:
+            self.selector = node_selector_requirements_as_selector(required) if required else None
+        except SelectorError as e:
+            self.selector = None
+            self.error = str(e)
+
+
+def _idx(dev):
+    try:
+        return int((dev.get("attributes") or {}).get(core.ATTR_INDEX, 1 << 30))
+    except ValueError:
+        return 1 << 30
+
+
+def _links(dev):
+    try:
+        return int((dev.get("attributes") or {}).get(core.ATTR_XGMI_LINKS, 7))
+    except ValueError:
+        return 0
+
+
+def allocate(requests, er, policy=PREFERRED):
+    """requests: list[Request]; er: ERManager of the node.
+    Returns (binding, score, reason). binding is None on failure."""
+    binding = {}
+    taken: set = set()
+    score_sum = 0.0
+    for r in requests:
+        if r.error:
+            return None, 0, r.error
+        avail = er.available.get(r.rname)
+        if not avail:
+            return None, 0, f"Insufficient {r.rname}"
+        need_links = r.count - 1 if r.count > 1 else 0
+        sel = r.selector
+        cands = []
+        for did, dev in avail.items():
+            if did in taken or dev.get("health", core.HEALTHY) != core.HEALTHY:
+                continue
+            attrs = dev.get("attributes") or {}
+            if sel is not None and not sel.matches(attrs):
+                continue
+            if need_links and _links(dev) < need_links:
+                continue
+            cands.append((did, dev))
+        if len(cands) < r.count:
+            return None, 0, f"Insufficient {r.rname}"
+        ids, s = _pick(cands, r.count, policy)
+        if ids is None:
+            return None, 0, f"no single xGMI hive has {r.count} free {r.rname}"
+        binding[r.name] = {"resources": ids}
+        taken.update(ids)
+        score_sum += s
+    return binding, (score_sum / len(requests)) if requests else 10.0, ""
+
+
+def _group(cands, key):
+    g = {}
+    for did, dev in cands:
+        g.setdefault((dev.get("attributes") or {}).get(key, ""), []).append((did, dev))
+    return g
+
+
+def _pick(cands, n, policy):
+    hives = _group(cands, core.ATTR_HIVE)
+    fitting = [(len(v), h, v) for h, v in hives.items() if len(v) >= n]
+    if fitting:
+        # best fit: the hive with the fewest free devices that still holds n
+        fitting.sort(key=lambda t: (t[0], t[1]))
+        free, _, devs = fitting[0]
+        numas = _group(devs, core.ATTR_NUMA)
+        nf = [(len(v), k, v) for k, v in numas.items() if len(v) >= n]
+        if nf:
+            nf.sort(key=lambda t: (t[0], t[1]))
+            chosen = sorted(nf[0][2], key=lambda x: _idx(x[1]))[:n]
+            numa_bonus = 1.0
+        else:
+            # fill NUMA nodes largest-first so the set spans as few as possible
+            chosen = []
+            for _, _, v in sorted(((len(v), k, v) for k, v in numas.items()), key=lambda t: (-t[0], t[1])):
+                chosen.extend(sorted(v, key=lambda x: _idx(x[1])))
+            chosen = chosen[:n]
+            numa_bonus = 0.0
+        # 10 for a perfect fit, decreasing with leftover fragments in that hive
+        leftover = free - n
+        score = 9.0 - min(leftover, 8) / 8.0 * 4.0 + numa_bonus
+        return [d for d, _ in chosen], score
+    if policy == REQUIRED and n > 1:
+        return None, 0
+    # span hives: largest hives first, deterministic
+    chosen = []
+    for _, _, v in sorted(((len(v), h, v) for h, v in hives.items()), key=lambda t: (-t[0], t[1])):
+        chosen.extend(sorted(v, key=lambda x: _idx(x[1])))
+    return [d for d, _ in chosen[:n]], 1.0

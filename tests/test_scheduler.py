@@ -1,0 +1,198 @@
+"""Scheduler: ER allocation (fork F4/F5 tests `extended_resources_test.go:59-193`,
+`node_info_test.go`), topology-aware placement, the assume fix, end-to-end with the API server."""
+import asyncio
+
+import pytest
+
+from kubernetes_amd.api import core
+from kubernetes_amd.apiserver.server import APIServer
+from kubernetes_amd.client.rest import Client
+from kubernetes_amd.scheduler.cache import ERManager, NodeInfo, PodInfo, SchedulerCache
+from kubernetes_amd.scheduler.generic import FitError, GenericScheduler
+from kubernetes_amd.scheduler.scheduler import Scheduler
+from kubernetes_amd.scheduler.topology import REQUIRED, Request, allocate
+
+
+def gpu_dev(i, hive="h0", numa="0", mem="294912", health=core.HEALTHY, links="7", arch="gfx950"):
+    return {"id": f"g{i}", "health": health, "attributes": {
+        core.ATTR_INDEX: str(i), core.ATTR_HIVE: hive, core.ATTR_NUMA: numa, core.ATTR_MEMORY: mem,
+        core.ATTR_HBM: f"{int(mem) // 1024}Gi", core.ATTR_XGMI_LINKS: links, core.ATTR_ARCH: arch}}
+
+
+def node(name, devs, cpu="64", mem="512Gi", labels=None, taints=None):
+    return {"metadata": {"name": name, "labels": labels or {}},
+            "spec": {"taints": taints or []},
+            "status": {"allocatable": {"cpu": cpu, "memory": mem, "pods": "110"},
+                       "conditions": [{"type": "Ready", "status": "True"}],
+                       "extendedResources": {core.AMD_GPU: {"resources": {d["id"]: d for d in devs}}}}}
+
+
+def gpu_pod(name, n, required=None, annotations=None, ns="default"):
+    return {"metadata": {"name": name, "namespace": ns, "uid": "uid-" + name, "annotations": annotations or {}},
+            "spec": {"containers": [{"name": "c", "image": "x", "extendedResourceRequests": ["er"]}],
+                     "extendedResources": [{"name": "er", "resources": {"limits": {core.AMD_GPU: str(n)},
+                                                                        "requests": {core.AMD_GPU: str(n)}},
+                                            "affinity": {"required": required or []}}]}}
+
+
+def er_of(devs):
+    e = ERManager()
+    e.set_node(node("n", devs))
+    return e
+
+
+def test_selectors_gt_lt_in_and_quantities():
+    devs = [gpu_dev(0, mem="8000"), gpu_dev(1, mem="294912"), gpu_dev(2, mem="294912", arch="gfx942")]
+    e = er_of(devs)
+    r = Request("er", core.AMD_GPU, 1, [{"key": core.ATTR_MEMORY, "operator": "Gt", "values": ["100000"]},
+                                        {"key": core.ATTR_ARCH, "operator": "In", "values": ["gfx950"]}])
+    b, _, _ = allocate([r], e)
+    assert b == {"er": {"resources": ["g1"]}}
+    # quantity-aware: hbm > 256Gi
+    r = Request("er", core.AMD_GPU, 2, [{"key": core.ATTR_HBM, "operator": "Gt", "values": ["256Gi"]}])
+    b, _, _ = allocate([r], e)
+    assert sorted(b["er"]["resources"]) == ["g1", "g2"]
+    r = Request("er", core.AMD_GPU, 1, [{"key": core.ATTR_MEMORY, "operator": "Lt", "values": ["9000"]}])
+    assert allocate([r], e)[0] == {"er": {"resources": ["g0"]}}
+    r = Request("er", core.AMD_GPU, 3, [{"key": core.ATTR_MEMORY, "operator": "Gt", "values": ["100000"]}])
+    b, _, why = allocate([r], e)
+    assert b is None and "Insufficient" in why
+
+
+def test_unhealthy_devices_not_allocated():
+    e = er_of([gpu_dev(0, health=core.UNHEALTHY), gpu_dev(1)])
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 1, [])], e)
+    assert b == {"er": {"resources": ["g1"]}}
+    assert allocate([Request("er", core.AMD_GPU, 2, [])], e)[0] is None
+
+
+def test_hive_and_numa_aware_multi_gpu():
+    # two hives of 4; hive h1 has only 3 free -> a 4-GPU pod must take h0 entirely
+    devs = [gpu_dev(i, hive="h0" if i < 4 else "h1", numa="0" if i < 4 else "1") for i in range(8)]
+    e = er_of(devs)
+    e.add_pod("x/y", {core.AMD_GPU: ["g7"]})
+    b, score, _ = allocate([Request("er", core.AMD_GPU, 4, [])], e)
+    assert sorted(b["er"]["resources"]) == ["g0", "g1", "g2", "g3"]
+    # a 2-GPU pod best-fits into the partially used hive h1
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 2, [])], e)
+    assert sorted(b["er"]["resources"]) == ["g4", "g5"]
+    # 5 GPUs: no hive fits; preferred spans, required fails
+    b, s, _ = allocate([Request("er", core.AMD_GPU, 5, [])], e)
+    assert b is not None and len(b["er"]["resources"]) == 5 and s <= 1
+    b, _, why = allocate([Request("er", core.AMD_GPU, 5, [])], e, REQUIRED)
+    assert b is None and "hive" in why
+
+
+def test_single_gpu_packs_used_hive_first():
+    devs = [gpu_dev(i, hive="h0" if i < 4 else "h1") for i in range(8)]
+    e = er_of(devs)
+    e.add_pod("a/b", {core.AMD_GPU: ["g0"]})
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 1, [])], e)
+    assert b["er"]["resources"] == ["g1"]
+
+
+def test_link_health_gates_multi_gpu():
+    devs = [gpu_dev(i, links="7" if i != 2 else "1") for i in range(4)]
+    e = er_of(devs)
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 4, [])], e)
+    assert b is None
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 3, [])], e)
+    assert sorted(b["er"]["resources"]) == ["g0", "g1", "g3"]
+
+
+def test_assume_reserves_devices_binpack_8_single_gpu_pods():
+    """BASELINE config 3: 8 single-GPU pods on one 8-GPU node, back to back before any bind
+    completes — every pod must get a distinct device (the reference could double-assign)."""
+    cache = SchedulerCache()
+    cache.add_node(node("mi355x-0", [gpu_dev(i) for i in range(8)]))
+    gs = GenericScheduler(cache)
+    got = []
+    for i in range(8):
+        p = gpu_pod(f"p{i}", 1)
+        host, erb = gs.schedule(p)
+        assumed = dict(p, spec=dict(p["spec"], nodeName=host,
+                                    extendedResources=[dict(p["spec"]["extendedResources"][0], assigned=erb["er"]["resources"])]))
+        cache.assume_pod(assumed)
+        got.extend(erb["er"]["resources"])
+    assert sorted(got) == [f"g{i}" for i in range(8)]
+    with pytest.raises(FitError) as ei:
+        gs.schedule(gpu_pod("p9", 1))
+    assert "Insufficient amd.com/gpu" in str(ei.value)
+
+
+def test_predicates_taints_selector_resources():
+    cache = SchedulerCache()
+    cache.add_node(node("a", [gpu_dev(0)], labels={"zone": "z1"},
+                        taints=[{"key": core.AMD_GPU, "effect": "NoSchedule"}]))
+    cache.add_node(node("b", [gpu_dev(0)], cpu="1", labels={"zone": "z2"}))
+    gs = GenericScheduler(cache)
+    p = gpu_pod("p", 1)
+    p["spec"]["containers"][0]["resources"] = {"requests": {"cpu": "2"}}
+    with pytest.raises(FitError) as ei:
+        gs.schedule(p)
+    msg = str(ei.value)
+    assert "taints" in msg and "Insufficient cpu" in msg
+    p["spec"]["tolerations"] = [{"key": core.AMD_GPU, "operator": "Exists", "effect": "NoSchedule"}]
+    assert gs.schedule(p)[0] == "a"
+    p2 = gpu_pod("q", 1)
+    p2["spec"]["nodeSelector"] = {"zone": "z2"}
+    assert gs.schedule(p2)[0] == "b"
+
+
+def test_gpu_binpacking_prefers_fuller_node():
+    cache = SchedulerCache()
+    cache.add_node(node("empty", [gpu_dev(i) for i in range(8)]))
+    cache.add_node(node("half", [gpu_dev(i) for i in range(8)]))
+    p0 = gpu_pod("x", 4)
+    p0["spec"]["nodeName"] = "half"
+    p0["spec"]["extendedResources"][0]["assigned"] = ["g0", "g1", "g2", "g3"]
+    cache.add_pod(p0)
+    gs = GenericScheduler(cache)
+    assert gs.schedule(gpu_pod("y", 4))[0] == "half"
+    assert gs.schedule(gpu_pod("z", 8))[0] == "empty"
+
+
+def test_end_to_end_scheduler_binds_distinct_devices(run):
+    async def main():
+        s = APIServer()
+        port = await s.start()
+        c = Client(f"http://127.0.0.1:{port}")
+        await c.create("nodes", node("mi355x-0", [gpu_dev(i) for i in range(8)]))
+        await c.update_status("nodes", node("mi355x-0", [gpu_dev(i) for i in range(8)]) | {"metadata": (await c.get("nodes", "mi355x-0"))["metadata"]})
+        sched = Scheduler(Client(f"http://127.0.0.1:{port}"))
+        task = asyncio.ensure_future(sched.run())
+        for i in range(8):
+            await c.create("pods", {"metadata": {"name": f"p{i}", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "c", "image": "x",
+                                                             "resources": {"limits": {core.AMD_GPU: "1"}}}]}})
+        await c.create("pods", {"metadata": {"name": "big", "namespace": "default"},
+                                "spec": {"containers": [{"name": "c", "image": "x",
+                                                         "resources": {"limits": {core.AMD_GPU: "4"}}}]}})
+        for _ in range(200):
+            pods = (await c.list("pods", "default"))["items"]
+            bound = [p for p in pods if p["spec"].get("nodeName")]
+            if len(bound) == 8:
+                break
+            await asyncio.sleep(0.02)
+        ids = [i for p in bound for i in p["spec"]["extendedResources"][0]["assigned"]]
+        assert len(bound) == 8 and len(set(ids)) == 8
+        big = await c.get("pods", "big", "default")
+        assert not big["spec"].get("nodeName")
+        # free 4 GPUs -> the 4-GPU pod schedules
+        for i in range(4):
+            await c.delete("pods", f"p{i}", "default", grace_period=0)
+        for _ in range(200):
+            big = await c.get("pods", "big", "default")
+            if big["spec"].get("nodeName"):
+                break
+            await asyncio.sleep(0.02)
+        assert len(big["spec"]["extendedResources"][0]["assigned"]) == 4
+        cond = core.get_condition(big["status"], core.COND_POD_SCHEDULED)
+        assert cond["status"] == "True"
+        evs = (await c.list("events", "default"))["items"]
+        assert any(e["reason"] == "FailedScheduling" for e in evs)
+        task.cancel()
+        await sched.stop()
+        await c.close()
+        await s.stop()
+    run(main())
