@@ -1,0 +1,142 @@
+"""In-process local cluster (the role of `hack/local-up-cluster.sh` and the integration-test
+master of `test/integration/framework/master_utils.go`): API server + scheduler + N kubelets,
+each with the amd.com/gpu device plugin (fake AMD SMI fixture, or the real one on a GPU box)
+registering over the real gRPC/unix-socket path.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import shutil
+import tempfile
+
+from .apiserver.server import APIServer
+from .client.rest import Client
+from .deviceplugin.amdgpu import AMDGPUPlugin
+from .kubelet.devicemanager.manager import ManagerImpl
+from .kubelet.kubelet import Kubelet
+from .kubelet.runtime.process import ProcessRuntime
+from .kubelet.runtime.stub import StubRuntime
+from .native import amdsmi
+from .scheduler.scheduler import Scheduler
+
+
+class NodeHandle:
+    def __init__(self, name, kubelet, plugin, dm, runtime, plugins_dir):
+        self.name, self.kubelet, self.plugin, self.dm, self.runtime, self.plugins_dir = (
+            name, kubelet, plugin, dm, runtime, plugins_dir)
+
+
+class LocalCluster:
+    def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
+                 emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
+                 health_interval=0.0, rocm_mount=None):
+        self.n_nodes = nodes
+        self.gpus = gpus_per_node
+        self.runtime_kind = runtime
+        self.real = real_gpus
+        self.hives = hives
+        self.own_dir = workdir is None
+        self.dir = workdir or tempfile.mkdtemp(prefix="kamd-cluster-")
+        self.emit_events = emit_events
+        self.payload = payload
+        self.admission = admission_plugins
+        self.scheduler_kwargs = scheduler_kwargs or {}
+        self.kubelet_http = kubelet_http
+        self.health_interval = health_interval
+        self.rocm_mount = rocm_mount
+        self.api = None
+        self.url = None
+        self.client = None
+        self.scheduler = None
+        self.nodes: list[NodeHandle] = []
+        self._sched_task = None
+        self.smi = None
+
+    async def start(self):
+        self.api = APIServer(admission_plugins=self.admission)
+        port = await self.api.start()
+        self.url = f"http://127.0.0.1:{port}"
+        self.client = Client(self.url)
+        if self.gpus:
+            fixture = None if self.real else amdsmi.fixture_file(self.gpus, hives=self.hives)
+            self.smi = amdsmi.SMI(fixture=fixture)
+        self.scheduler = Scheduler(Client(self.url), emit_events=self.emit_events, **self.scheduler_kwargs)
+        self._sched_task = asyncio.ensure_future(self.scheduler.run())
+        for i in range(self.n_nodes):
+            await self.add_node(f"node-{i}" if not self.real else f"mi355x-{i}")
+        await self.wait_nodes_ready()
+        return self
+
+    async def add_node(self, name):
+        ndir = os.path.join(self.dir, name)
+        plugins_dir = os.path.join(ndir, "device-plugin", "plugins")
+        os.makedirs(plugins_dir, exist_ok=True)
+        dm = ManagerImpl(plugins_dir)
+        if self.runtime_kind == "process":
+            rt = ProcessRuntime(os.path.join(ndir, "runtime"))
+        else:
+            rt = StubRuntime(payload=self.payload)
+        kl = Kubelet(Client(self.url), name, rt, dm, emit_events=self.emit_events,
+                     http_port=0 if self.kubelet_http else None)
+        kl.smi = self.smi
+        plugin = None
+        await kl.run()
+        if self.gpus:
+            plugin = AMDGPUPlugin(plugins_dir, smi=self.smi, health_interval=self.health_interval,
+                                  rocm_mount=self.rocm_mount)
+            await plugin.start()
+        h = NodeHandle(name, kl, plugin, dm, rt, plugins_dir)
+        self.nodes.append(h)
+        return h
+
+    async def wait_nodes_ready(self, timeout=30):
+        want = self.gpus
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        while loop.time() < end:
+            ok = 0
+            for n in self.nodes:
+                ni = self.scheduler.cache.nodes.get(n.name)
+                if ni is not None and ni.node is not None and (not want or ni.gpu_total >= (len(n.plugin.gpus) if n.plugin else 0)):
+                    ok += 1
+            if ok == len(self.nodes):
+                return
+            await asyncio.sleep(0.02)
+        raise TimeoutError("nodes not ready in the scheduler cache")
+
+    async def wait_pod(self, name, ns="default", phase="Running", timeout=30):
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        pod = None
+        while loop.time() < end:
+            try:
+                pod = await self.client.get("pods", name, ns)
+            except Exception:
+                pod = None
+            if pod is not None and (pod.get("status") or {}).get("phase") == phase:
+                return pod
+            await asyncio.sleep(0.02)
+        raise TimeoutError(f"pod {ns}/{name} not {phase}: {pod and pod.get('status')}")
+
+    async def stop(self):
+        for n in self.nodes:
+            if n.plugin:
+                await n.plugin.stop()
+            await n.kubelet.stop()
+        if self.scheduler:
+            await self.scheduler.stop()
+        if self._sched_task:
+            self._sched_task.cancel()
+        if self.client:
+            await self.client.close()
+        if self.api:
+            await self.api.stop()
+        if self.own_dir:
+            shutil.rmtree(self.dir, ignore_errors=True)
+
+    async def __aenter__(self):
+        return await self.start()
+
+    async def __aexit__(self, *exc):
+        await self.stop()

@@ -1,0 +1,97 @@
+"""Container runtime interface used by the kubelet (the CRI's RuntimeService, in-process).
+
+Parity: CRI `RuntimeService` (`pkg/kubelet/apis/cri/v1alpha1/runtime/api.proto:17-104`:
+RunPodSandbox / StopPodSandbox / RemovePodSandbox / CreateContainer / StartContainer /
+StopContainer / RemoveContainer / ContainerStatus / ListContainers) and
+`kubecontainer.RunContainerOptions` (envs, devices, mounts, annotations from the device
+manager, `pkg/kubelet/container/runtime.go`).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+CREATED, RUNNING, EXITED, UNKNOWN = "CONTAINER_CREATED", "CONTAINER_RUNNING", "CONTAINER_EXITED", "CONTAINER_UNKNOWN"
+
+
+@dataclass
+class RunContainerOptions:
+    envs: list = field(default_factory=list)          # [{"name","value"}]
+    devices: list = field(default_factory=list)       # [{"pathOnHost","pathInContainer","permissions"}]
+    mounts: list = field(default_factory=list)        # [{"containerPath","hostPath","readOnly"}]
+    annotations: list = field(default_factory=list)   # [{"name","value"}]
+
+    @classmethod
+    def from_device_opts(cls, d):
+        return cls(list(d.get("envs") or []), list(d.get("devices") or []), list(d.get("mounts") or []),
+                   list(d.get("annotations") or []))
+
+    def env_dict(self):
+        return {e["name"]: e["value"] for e in self.envs}
+
+
+@dataclass
+class ContainerStatus:
+    id: str
+    name: str
+    state: str = CREATED
+    created_at: float = field(default_factory=time.time)
+    started_at: float = 0.0
+    finished_at: float = 0.0
+    exit_code: int = 0
+    reason: str = ""
+    message: str = ""
+    image: str = ""
+    log_path: str = ""
+
+
+class RuntimeError_(Exception):
+    pass
+
+
+class Runtime:
+    """Base class. `on_exit(cb)` registers cb(pod_uid, container_id) for event-driven PLEG."""
+    name = "base"
+
+    def __init__(self):
+        self._exit_cbs = []
+
+    def on_exit(self, cb):
+        self._exit_cbs.append(cb)
+
+    def _fire_exit(self, pod_uid, cid):
+        for cb in self._exit_cbs:
+            cb(pod_uid, cid)
+
+    async def version(self):
+        return {"runtimeName": self.name, "runtimeVersion": "1.0", "runtimeApiVersion": "v1alpha1"}
+
+    async def run_pod_sandbox(self, pod, annotations: dict) -> str:
+        raise NotImplementedError
+
+    async def stop_pod_sandbox(self, sandbox_id: str):
+        raise NotImplementedError
+
+    async def remove_pod_sandbox(self, sandbox_id: str):
+        raise NotImplementedError
+
+    async def create_container(self, sandbox_id: str, pod, container, opts: RunContainerOptions) -> str:
+        raise NotImplementedError
+
+    async def start_container(self, cid: str):
+        raise NotImplementedError
+
+    async def stop_container(self, cid: str, timeout: float):
+        raise NotImplementedError
+
+    async def remove_container(self, cid: str):
+        raise NotImplementedError
+
+    def container_status(self, cid: str) -> ContainerStatus | None:
+        raise NotImplementedError
+
+    async def container_logs(self, cid: str, tail: int | None = None) -> bytes:
+        return b""
+
+    def list_containers(self):
+        return []

@@ -1,0 +1,211 @@
+"""Process runtime — runs containers as host child processes (no docker/containerd in this image).
+
+  * sandbox  = the native `pause` binary (native/pause/pause.cc) in its own session, holding the
+               pod's lifetime like the pause container of a docker sandbox;
+  * container = `command + args` as a child process in its own process group, stdout/stderr to
+               `<root>/containers/<id>/log`; an OCI `config.json` with the injected GPU devices
+               is written into the container bundle (`runtime/oci.py`) for audit/OCI runtimes;
+  * images   = a local image map (`IMAGES`) resolves well-known images to built executables,
+               e.g. `kubernetes-amd/hip-vector-add` → native/bin/hip-vector-add;
+  * GPUs     = without device namespaces the runtime narrows HIP enumeration itself:
+               `AMD_VISIBLE_DEVICES` from the device plugin becomes `HIP_VISIBLE_DEVICES`.
+Exit is observed by awaiting the child (event-driven PLEG), like a CRI event stream.
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import json
+import os
+import signal
+import time
+
+from ...native import BIN_DIR
+from . import oci
+from .base import CREATED, EXITED, RUNNING, ContainerStatus, Runtime, RunContainerOptions
+
+IMAGES = {
+    "kubernetes-amd/hip-vector-add": [os.path.join(BIN_DIR, "hip-vector-add")],
+    "kubernetes-amd/xgmi-probe": [os.path.join(BIN_DIR, "xgmi-probe")],
+    "kubernetes-amd/pause": [os.path.join(BIN_DIR, "pause")],
+    "busybox": ["/bin/sh"],
+}
+
+
+def resolve_command(container):
+    cmd = list(container.get("command") or [])
+    args = list(container.get("args") or [])
+    if not cmd:
+        img = (container.get("image") or "").split("@")[0]
+        base = img.rsplit(":", 1)[0] if ":" in img.split("/")[-1] else img
+        cmd = list(IMAGES.get(base, []))
+        if not cmd:
+            raise FileNotFoundError(f"image {img!r} has no local entrypoint and no command was given")
+    return cmd + args
+
+
+class ProcessRuntime(Runtime):
+    name = "process"
+
+    def __init__(self, root_dir: str, inherit_env: bool = True):
+        super().__init__()
+        self.root = os.path.abspath(root_dir)
+        os.makedirs(os.path.join(self.root, "containers"), exist_ok=True)
+        os.makedirs(os.path.join(self.root, "sandboxes"), exist_ok=True)
+        self._ids = itertools.count(1)
+        self.sandboxes: dict[str, dict] = {}
+        self.containers: dict[str, ContainerStatus] = {}
+        self.meta: dict[str, dict] = {}
+        self.inherit_env = inherit_env
+
+    async def run_pod_sandbox(self, pod, annotations):
+        sid = f"sb{next(self._ids)}-{pod['metadata']['uid'][:8]}"
+        d = os.path.join(self.root, "sandboxes", sid)
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "annotations.json"), "w") as f:
+            json.dump(annotations or {}, f)
+        proc = await asyncio.create_subprocess_exec(os.path.join(BIN_DIR, "pause"), start_new_session=True,
+                                                    stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL)
+        self.sandboxes[sid] = {"proc": proc, "dir": d, "pod_uid": pod["metadata"]["uid"], "annotations": annotations}
+        return sid
+
+    async def stop_pod_sandbox(self, sid):
+        sb = self.sandboxes.get(sid)
+        if not sb:
+            return
+        for cid, m in list(self.meta.items()):
+            if m["sandbox"] == sid:
+                await self.stop_container(cid, 2)
+        p = sb["proc"]
+        if p.returncode is None:
+            try:
+                p.terminate()
+                await asyncio.wait_for(p.wait(), 5)
+            except (ProcessLookupError, asyncio.TimeoutError):
+                try:
+                    p.kill()
+                except ProcessLookupError:
+                    pass
+
+    async def remove_pod_sandbox(self, sid):
+        await self.stop_pod_sandbox(sid)
+        for cid, m in list(self.meta.items()):
+            if m["sandbox"] == sid:
+                await self.remove_container(cid)
+        self.sandboxes.pop(sid, None)
+
+    async def create_container(self, sid, pod, container, opts: RunContainerOptions):
+        cid = f"process://{next(self._ids)}-{container['name']}"
+        d = os.path.join(self.root, "containers", cid.split("://", 1)[1])
+        os.makedirs(d, exist_ok=True)
+        argv = resolve_command(container)
+        env = dict(os.environ) if self.inherit_env else {"PATH": os.environ.get("PATH", "/usr/bin:/bin")}
+        for e in container.get("env") or ():
+            if "value" in e:
+                env[e["name"]] = str(e["value"])
+        dev_env = opts.env_dict()
+        env.update(dev_env)
+        env.pop("ROCR_VISIBLE_DEVICES", None)
+        env.pop("CUDA_VISIBLE_DEVICES", None)
+        if "AMD_VISIBLE_DEVICES" in dev_env:
+            env["HIP_VISIBLE_DEVICES"] = dev_env["AMD_VISIBLE_DEVICES"]
+        else:
+            env["HIP_VISIBLE_DEVICES"] = "-1"   # a container without allocated GPUs sees none
+        sb = self.sandboxes.get(sid) or {}
+        spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts,
+                              sandbox_pid=getattr(sb.get("proc"), "pid", None))
+        with open(os.path.join(d, "config.json"), "w") as f:
+            json.dump(spec, f, indent=1)
+        st = ContainerStatus(cid, container["name"], CREATED, image=container.get("image", ""),
+                             log_path=os.path.join(d, "log"))
+        self.containers[cid] = st
+        self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "argv": argv, "env": env,
+                          "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec}
+        return cid
+
+    @staticmethod
+    def _gpu_pod(opts):
+        return any("/dev/dri/" in x.get("pathOnHost", "") for x in opts.devices)
+
+    async def start_container(self, cid):
+        m = self.meta[cid]
+        st = self.containers[cid]
+        log = open(st.log_path, "ab")
+        try:
+            proc = await asyncio.create_subprocess_exec(*m["argv"], env=m["env"], cwd=m["cwd"], stdout=log,
+                                                        stderr=asyncio.subprocess.STDOUT, start_new_session=True)
+        except OSError as e:
+            log.close()
+            st.state = EXITED
+            st.exit_code = 128
+            st.reason = "StartError"
+            st.message = str(e)
+            st.finished_at = time.time()
+            raise
+        finally:
+            pass
+        log.close()
+        m["proc"] = proc
+        st.state = RUNNING
+        st.started_at = time.time()
+        asyncio.ensure_future(self._wait(cid, proc))
+
+    async def _wait(self, cid, proc):
+        code = await proc.wait()
+        st = self.containers.get(cid)
+        if st is None:
+            return
+        if st.state != EXITED:
+            st.state = EXITED
+            st.exit_code = code if code >= 0 else 128 - code
+            st.reason = "Completed" if code == 0 else "Error"
+            st.finished_at = time.time()
+        self._fire_exit(self.meta[cid]["pod_uid"], cid)
+
+    async def stop_container(self, cid, timeout):
+        m = self.meta.get(cid)
+        if not m or m["proc"] is None or m["proc"].returncode is not None:
+            st = self.containers.get(cid)
+            if st is not None and st.state != EXITED:
+                st.state = EXITED
+                st.finished_at = time.time()
+            return
+        proc = m["proc"]
+        try:
+            os.killpg(proc.pid, signal.SIGTERM)
+            await asyncio.wait_for(proc.wait(), max(timeout, 0.01))
+        except (ProcessLookupError, PermissionError):
+            pass
+        except asyncio.TimeoutError:
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            await proc.wait()
+        st = self.containers[cid]
+        if st.state != EXITED:
+            st.state = EXITED
+            st.exit_code = 143
+            st.reason = "Killed"
+            st.finished_at = time.time()
+
+    async def remove_container(self, cid):
+        await self.stop_container(cid, 0)
+        self.containers.pop(cid, None)
+        self.meta.pop(cid, None)
+
+    def container_status(self, cid):
+        return self.containers.get(cid)
+
+    def list_containers(self):
+        return list(self.containers.values())
+
+    async def container_logs(self, cid, tail=None):
+        st = self.containers.get(cid)
+        if st is None or not os.path.exists(st.log_path):
+            return b""
+        with open(st.log_path, "rb") as f:
+            data = f.read()
+        if tail:
+            data = b"\n".join(data.splitlines()[-tail:]) + b"\n"
+        return data

@@ -1,0 +1,147 @@
+"""End-to-end on one node (the reference's `test/e2e_node/gpu_device_plugin.go:46-143` and
+BASELINE configs 1-4): plugin registration → node capacity → scheduling with device IDs →
+kubelet admission → device injection → pod Running → deletion frees devices."""
+import asyncio
+import json
+import os
+
+import pytest
+
+from kubernetes_amd.api import core
+from kubernetes_amd.cluster import LocalCluster
+
+
+def gpu_pod(name, n=1, cmd=None, image="kubernetes-amd/hip-vector-add", policy="Always", selector=None, ann=None):
+    c = {"name": "c", "image": image, "resources": {"limits": {core.AMD_GPU: str(n)}}}
+    if cmd:
+        c["command"] = cmd
+    p = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default", "annotations": ann or {}},
+         "spec": {"containers": [c], "restartPolicy": policy}}
+    if selector:
+        p["spec"]["nodeSelector"] = selector
+    return p
+
+
+def test_node_capacity_and_gpu_pods_stub_runtime(run):
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8) as cl:
+            c = cl.client
+            node = await c.get("nodes", "node-0")
+            assert node["status"]["capacity"][core.AMD_GPU] == "8"
+            devs = node["status"]["extendedResources"][core.AMD_GPU]["resources"]
+            assert len(devs) == 8
+            assert node["metadata"]["labels"]["amd.com/gpu.product"] == "MI355X"
+            # config 0: CPU-only pod
+            await c.create("pods", {"metadata": {"name": "nginx"}, "spec": {"containers": [{"name": "n", "image": "nginx"}]}})
+            await cl.wait_pod("nginx")
+            # config 3: bin-pack 8 single-GPU pods
+            for i in range(8):
+                await c.create("pods", gpu_pod(f"g{i}"))
+            ids = []
+            for i in range(8):
+                p = await cl.wait_pod(f"g{i}")
+                ids += p["spec"]["extendedResources"][0]["assigned"]
+                assert p["status"]["containerStatuses"][0]["ready"]
+            assert len(set(ids)) == 8
+            # the 9th GPU pod is unschedulable
+            await c.create("pods", gpu_pod("g8"))
+            await asyncio.sleep(0.3)
+            p = await c.get("pods", "g8", "default")
+            assert not p["spec"].get("nodeName")
+            # delete one -> the pending pod gets the freed device
+            freed = (await c.get("pods", "g3", "default"))["spec"]["extendedResources"][0]["assigned"]
+            await c.delete("pods", "g3", "default")
+            p = await cl.wait_pod("g8", timeout=10)
+            assert p["spec"]["extendedResources"][0]["assigned"] == freed
+    run(main(), timeout=120)
+
+
+def test_multi_gpu_hive_and_selector(run):
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8, hives=2) as cl:
+            c = cl.client
+            # config 4: 4-GPU pod lands inside one hive
+            await c.create("pods", gpu_pod("four", 4, ann={"amd.com/xgmi-policy": "required"}))
+            p = await cl.wait_pod("four")
+            node = await c.get("nodes", p["spec"]["nodeName"])
+            devs = node["status"]["extendedResources"][core.AMD_GPU]["resources"]
+            hives = {devs[i]["attributes"][core.ATTR_HIVE] for i in p["spec"]["extendedResources"][0]["assigned"]}
+            assert len(hives) == 1
+            # config 5: attribute selector hbm > 256Gi, arch in (gfx950) via explicit extendedResources
+            sel = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sel", "namespace": "default"},
+                   "spec": {"containers": [{"name": "c", "image": "x", "extendedResourceRequests": ["gpu"]}],
+                            "extendedResources": [{"name": "gpu", "resources": {"limits": {core.AMD_GPU: "2"}},
+                                                   "affinity": {"required": [
+                                                       {"key": core.ATTR_HBM, "operator": "Gt", "values": ["256Gi"]},
+                                                       {"key": core.ATTR_ARCH, "operator": "In", "values": ["gfx950"]}]}}]}}
+            await c.create("pods", sel)
+            p = await cl.wait_pod("sel")
+            assert len(p["spec"]["extendedResources"][0]["assigned"]) == 2
+            # unsatisfiable selector stays pending with a FailedScheduling event
+            bad = json.loads(json.dumps(sel))
+            bad["metadata"]["name"] = "bad"
+            bad["spec"]["extendedResources"][0]["affinity"]["required"] = [
+                {"key": core.ATTR_ARCH, "operator": "In", "values": ["gfx942"]}]
+            await c.create("pods", bad)
+            await asyncio.sleep(0.3)
+            p = await c.get("pods", "bad", "default")
+            assert not p["spec"].get("nodeName")
+            cond = core.get_condition(p["status"], core.COND_POD_SCHEDULED)
+            assert cond and cond["status"] == "False"
+    run(main(), timeout=120)
+
+
+def test_process_runtime_injects_devices(run):
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=2, runtime="process") as cl:
+            c = cl.client
+            await c.create("pods", gpu_pod("env", 1, cmd=["/bin/sh", "-c", "echo HIP=$HIP_VISIBLE_DEVICES AMD=$AMD_VISIBLE_DEVICES"],
+                                           policy="Never"))
+            p = await cl.wait_pod("env", phase="Succeeded", timeout=20)
+            assert p["status"]["containerStatuses"][0]["state"]["terminated"]["exitCode"] == 0
+            rt = cl.nodes[0].runtime
+            cs = rt.list_containers()[0]
+            log = open(cs.log_path).read()
+            idx = p["spec"]["extendedResources"][0]["assigned"]
+            assert "HIP=" in log and "AMD=" in log
+            spec = json.load(open(os.path.join(os.path.dirname(cs.log_path), "config.json")))
+            # /dev/kfd and the render node were requested; on a GPU-less host they are recorded as missing
+            ann = spec["annotations"]
+            want = {"/dev/kfd"}
+            assert want <= set(ann.get("amd.com/missing-device-nodes", "").split(",")) | {d["path"] for d in spec["linux"]["devices"]}
+            assert ann["amd.com/gpu-render-nodes"].startswith("renderD")
+            del idx
+    run(main(), timeout=120)
+
+
+def test_failing_payload_fails_pod(run):
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=1, payload=lambda opts: False) as cl:
+            await cl.client.create("pods", gpu_pod("bad", 1, policy="Never"))
+            p = await cl.wait_pod("bad", phase="Failed", timeout=20)
+            assert p["status"]["containerStatuses"][0]["state"]["terminated"]["exitCode"] == 1
+    run(main(), timeout=60)
+
+
+def test_unhealthy_device_reduces_capacity(run):
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=4) as cl:
+            n = cl.nodes[0]
+            cl.smi.fake_set_ecc(2, 7)
+            assert n.plugin.poll_health()
+            for _ in range(200):
+                node = await cl.client.get("nodes", n.name)
+                if node["status"]["capacity"][core.AMD_GPU] == "3":
+                    break
+                await asyncio.sleep(0.02)
+            assert node["status"]["capacity"][core.AMD_GPU] == "3"
+            bad = n.plugin.gpus[2].device_id_str
+            assert node["status"]["extendedResources"][core.AMD_GPU]["resources"][bad]["health"] == "Unhealthy"
+            for i in range(3):
+                await cl.client.create("pods", gpu_pod(f"p{i}"))
+            got = []
+            for i in range(3):
+                got += (await cl.wait_pod(f"p{i}"))["spec"]["extendedResources"][0]["assigned"]
+            assert bad not in got
+            cl.smi.fake_set_ecc(2, 0)
+    run(main(), timeout=60)
