@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: GPU pods/sec + pod-startup latency, kubemark density on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Setup (BASELINE.json: "GPU pods/sec scheduled + p50 pod-startup latency, 8xMI355X kubemark density"):
+  * rank 0 starts the control plane as separate processes — kube-apiserver (embedded MVCC
+    store) and kube-scheduler — before anything touches the GPU;
+  * every rank (one per GPU) hosts `--nodes-per-rank` kubemark hollow nodes, each a real kubelet
+    with the real DeviceManager and an amd.com/gpu device plugin over gRPC advertising 8 MI355X
+    (fake AMD SMI fixture, one xGMI hive), and a stub container runtime whose GPU containers run
+    a real HIP vector_add payload on the rank's own MI355X at container start;
+  * every rank generates load for its share: `8 x nodes-per-rank` single-GPU pods per step
+    (weak scaling: per-GPU work is fixed), created through the API (ResourceV2 admission),
+    scheduled with device IDs, admitted by the kubelet, started, observed Running on a watch,
+    then deleted (graceful; kubelet finalizes) and observed gone — one step = one full
+    saturation/churn cycle of the rank's share of the cluster.
+`value` = total pods / wall time over all ranks (max over ranks). Startup latency percentiles
+are over every pod of the timed steps. Data: synthetic pods, stub containers.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "GPU pods/sec scheduled + p50 pod-startup latency, 8×MI355X kubemark density"
+BASELINE_DENSITY_PODS_PER_S = 8.0        # test/e2e/scalability/density.go:55-57 (MinPodsPerSecondThroughput)
+BASELINE_SCHED_WARN_PODS_PER_S = 100.0   # test/integration/scheduler_perf/scheduler_test.go:35-36
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def spawn_control_plane(tmp, args):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = HERE + os.pathsep + env.get("PYTHONPATH", "")
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    pf = os.path.join(tmp, "apiserver.port")
+    api = subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf,
+                            "--storage-engine", args.storage_engine],
+                           env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "apiserver.log"), "w"))
+    t = time.time()
+    while not os.path.exists(pf):
+        if api.poll() is not None:
+            raise RuntimeError("apiserver exited: " + open(os.path.join(tmp, "apiserver.log")).read()[-2000:])
+        if time.time() - t > 120:
+            raise TimeoutError("apiserver did not start")
+        time.sleep(0.05)
+    url = f"http://127.0.0.1:{open(pf).read().strip()}"
+    sched = subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.scheduler", "--master", url,
+                              "--percentage-of-nodes-to-score", str(args.percentage_of_nodes_to_score)]
+                             + (["--no-events"] if args.no_events else []),
+                             env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "scheduler.log"), "w"))
+    return url, [api, sched]
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        self.cuda = False
+
+    def init(self):
+        import torch
+        self.torch = torch
+        self.cuda = torch.cuda.is_available()
+        if self.cuda:
+            torch.cuda.set_device(self.local_rank)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl" if self.cuda else "gloo")
+            self.dist = dist
+
+    def broadcast(self, obj):
+        if self.world == 1:
+            return obj
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+        if self.cuda:
+            self.torch.cuda.synchronize()
+
+    def allgather(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+
+async def rank_main(args, d: Dist, url):
+    from kubernetes_amd.client.rest import Client
+    from kubernetes_amd.kubemark.density import DensityRunner, interval_rates, pct
+    from kubernetes_amd.kubemark.hollow import HollowCluster
+
+    loop = asyncio.get_running_loop()
+
+    async def abarrier():
+        await loop.run_in_executor(None, d.barrier)
+
+    payload = None
+    payload_fn = None
+    if d.cuda and args.payload != "off":
+        from kubernetes_amd.ops.hip_kernels import Payload
+        payload = Payload(d.local_rank)
+        payload_fn = lambda opts: payload.run()  # noqa: E731
+    hollow = HollowCluster(url, args.nodes_per_rank, prefix=f"r{d.rank}", gpus=args.gpus_per_node,
+                           payload=payload_fn, emit_events=not args.no_events)
+    await hollow.start()
+    await hollow.wait_registered()
+    # wait until every rank's nodes are visible with their GPUs
+    c = Client(url)
+    want_nodes = d.world * args.nodes_per_rank
+    t = time.time()
+    while True:
+        nodes = (await c.list("nodes"))["items"]
+        ok = [n for n in nodes if int((n["status"].get("capacity") or {}).get("amd.com/gpu", "0")) == args.gpus_per_node]
+        if len(ok) >= want_nodes:
+            break
+        if time.time() - t > 120:
+            raise TimeoutError(f"only {len(ok)}/{want_nodes} GPU nodes ready")
+        await asyncio.sleep(0.05)
+    await c.close()
+    pods_per_step = args.pods_per_rank or args.nodes_per_rank * args.gpus_per_node // args.gpus_per_pod
+    runner = DensityRunner(url, d.rank, pods_per_step=pods_per_step, gpus_per_pod=args.gpus_per_pod)
+    await runner.start()
+    await abarrier()
+    for w in range(args.warmup):
+        await runner.step(f"w{w}")
+        await abarrier()
+    results = []
+    await abarrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        results.append(await runner.step(k))
+        if k + 1 < args.steps:
+            await abarrier()
+    await abarrier()
+    elapsed = time.perf_counter() - t0
+    lat = [x for r in results for x in r["latencies"]]
+    sched_times = []
+    off = 0.0
+    for r in results:
+        sched_times += [off + s for s in r["scheduled_times"]]
+        off += r["cycle_s"]
+    stats = {"elapsed": elapsed, "lat": lat, "pods": sum(r["pods"] for r in results),
+             "to_running": [r["to_running_s"] for r in results], "cycle": [r["cycle_s"] for r in results],
+             "payload_runs": sum(getattr(k.runtime, "payload_runs", 0) for k in hollow.nodes),
+             "payload_failures": sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes),
+             "sched_rates": interval_rates(sched_times)}
+    allstats = await loop.run_in_executor(None, d.allgather, stats)
+    await runner.stop()
+    # keep serving other ranks' pods until everyone is done
+    await abarrier()
+    await hollow.stop()
+    if payload is not None:
+        payload.close()
+    return allstats
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes-per-rank", type=int, default=8)
+    ap.add_argument("--gpus-per-node", type=int, default=8)
+    ap.add_argument("--gpus-per-pod", type=int, default=1)
+    ap.add_argument("--pods-per-rank", type=int, default=0)
+    ap.add_argument("--percentage-of-nodes-to-score", type=int, default=100)
+    ap.add_argument("--payload", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--storage-engine", default="native", choices=["native", "python"])
+    ap.add_argument("--no-events", action="store_true")
+    args = ap.parse_args()
+    d = Dist()
+    tmp = tempfile.mkdtemp(prefix="kamd-bench-")
+    procs = []
+    url = None
+    try:
+        if d.rank == 0:
+            url, procs = spawn_control_plane(tmp, args)   # before any GPU init
+        d.init()
+        url = d.broadcast(url)
+        allstats = asyncio.run(rank_main(args, d, url))
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    if d.rank != 0:
+        return
+    from kubernetes_amd.kubemark.density import pct
+    elapsed = max(s["elapsed"] for s in allstats)
+    pods = sum(s["pods"] for s in allstats)
+    lat = [x for s in allstats for x in s["lat"]]
+    value = pods / elapsed
+    n = d.world
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "pods/s", "n_gpus": n, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": round(value / BASELINE_DENSITY_PODS_PER_S, 2), "dtype": "bf16",
+        "data": "synthetic GPU-requesting pods, stub containers (HIP vector_add payload on the rank's MI355X)"
+        if any(s["payload_runs"] for s in allstats) else "synthetic GPU-requesting pods, stub containers",
+        "config": {"model": "kubemark-density/8xMI355X-hollow-nodes/1-GPU-pods", "global_batch": pods // args.steps,
+                   "seq_len": None, "parallelism": f"ranks{n}", "hollow_nodes": n * args.nodes_per_rank,
+                   "gpus_per_node": args.gpus_per_node, "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
+                   "gpus_per_pod": args.gpus_per_pod},
+        "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
+        "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
+        "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],
+        "sched_rate_avg_pods_per_s": round(sum(s["sched_rates"][0] for s in allstats), 1),
+        "vs_scheduler_perf_warn_threshold": round(value / BASELINE_SCHED_WARN_PODS_PER_S, 2),
+        "payload_runs": sum(s["payload_runs"] for s in allstats),
+        "payload_failures": sum(s["payload_failures"] for s in allstats),
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

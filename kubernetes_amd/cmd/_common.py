@@ -1,0 +1,38 @@
+"""Shared bits for the component entry points."""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import signal
+
+
+def setup_logging(v: int = 0):
+    lvl = logging.WARNING if v <= 0 else (logging.INFO if v == 1 else logging.DEBUG)
+    logging.basicConfig(level=lvl, format="%(asctime)s %(levelname).1s %(name)s] %(message)s")
+
+
+def write_port_file(path, port):
+    if path:
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(str(port))
+        os.replace(tmp, path)
+
+
+def run_until_signal(main_coro_factory):
+    """Run an asyncio component until SIGINT/SIGTERM."""
+    async def runner():
+        loop = asyncio.get_running_loop()
+        stop = asyncio.Event()
+        for s in (signal.SIGINT, signal.SIGTERM):
+            try:
+                loop.add_signal_handler(s, stop.set)
+            except NotImplementedError:
+                pass
+        comp = await main_coro_factory()
+        await stop.wait()
+        closer = getattr(comp, "stop", None)
+        if closer is not None:
+            await closer()
+    asyncio.run(runner())

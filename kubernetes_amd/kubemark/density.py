@@ -1,0 +1,143 @@
+"""Density load generator and measurement (kubemark density / scheduler_perf equivalent).
+
+Metric definitions follow the reference:
+  * startup latency = watch-observed `Running` minus creation (`test/e2e/scalability/density.go:799-803`);
+    measured here with a monotonic client clock (create request sent → Running observed on the
+    watch), because `creationTimestamp` has 1 s resolution;
+  * throughput = pods per second (saturation: all pods Running) and the scheduled-pods rate
+    sampled per second (`test/integration/scheduler_perf/scheduler_test.go:131-182`), reporting
+    the average and the worst 1-s interval.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+
+from ..api import core
+from ..client.rest import APIStatusError, Client
+
+
+def gpu_pod(name, ns, labels, gpus=1, selector=None, annotations=None):
+    c = {"name": "gpu", "image": "kubernetes-amd/hip-vector-add:1", "resources": {"limits": {core.AMD_GPU: str(gpus)}}}
+    p = {"apiVersion": "v1", "kind": "Pod",
+         "metadata": {"name": name, "namespace": ns, "labels": labels, "annotations": dict(annotations or {})},
+         "spec": {"containers": [c], "restartPolicy": "Never", "terminationGracePeriodSeconds": 1}}
+    if selector:
+        p["spec"]["nodeSelector"] = selector
+    return p
+
+
+def pct(vals, q):
+    if not vals:
+        return float("nan")
+    s = sorted(vals)
+    k = min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))
+    return s[k]
+
+
+class DensityRunner:
+    def __init__(self, master, rank=0, namespace="density", pods_per_step=64, gpus_per_pod=1, concurrency=128):
+        self.client = Client(master, max_conns=64)
+        self.rank = rank
+        self.ns = namespace
+        self.pods_per_step = pods_per_step
+        self.gpus_per_pod = gpus_per_pod
+        self.concurrency = concurrency
+        self.created: dict[str, float] = {}
+        self.scheduled: dict[str, float] = {}
+        self.running: dict[str, float] = {}
+        self.gone: dict[str, float] = {}
+        self._watch_task = None
+        self._stream = None
+        self._changed = asyncio.Event()
+        self.selector = f"density-rank={rank}"
+
+    async def start(self):
+        try:
+            await self.client.create("namespaces", {"metadata": {"name": self.ns}})
+        except APIStatusError as e:
+            if e.code != 409:
+                raise
+        lst = await self.client.list("pods", self.ns, label_selector=self.selector)
+        self._stream = await self.client.watch("pods", self.ns, lst["metadata"]["resourceVersion"],
+                                               label_selector=self.selector)
+        self._watch_task = asyncio.ensure_future(self._watch())
+
+    async def _watch(self):
+        async for etype, pod in self._stream:
+            name = pod["metadata"]["name"]
+            now = time.monotonic()
+            if etype == "DELETED":
+                self.gone.setdefault(name, now)
+            else:
+                if (pod.get("spec") or {}).get("nodeName") and name not in self.scheduled:
+                    self.scheduled[name] = now
+                if (pod.get("status") or {}).get("phase") == core.POD_RUNNING and name not in self.running:
+                    self.running[name] = now
+            self._changed.set()
+
+    async def _wait(self, pred, timeout):
+        end = time.monotonic() + timeout
+        while not pred():
+            left = end - time.monotonic()
+            if left <= 0:
+                raise TimeoutError("density step timed out")
+            self._changed.clear()
+            try:
+                await asyncio.wait_for(self._changed.wait(), min(left, 1.0))
+            except asyncio.TimeoutError:
+                pass
+
+    async def step(self, k, timeout=300):
+        names = [f"r{self.rank}-s{k}-{i}" for i in range(self.pods_per_step)]
+        labels = {"density-rank": str(self.rank), "density-step": str(k)}
+        sem = asyncio.Semaphore(self.concurrency)
+        t0 = time.monotonic()
+
+        async def create(n):
+            async with sem:
+                self.created[n] = time.monotonic()
+                await self.client.create("pods", gpu_pod(n, self.ns, labels, self.gpus_per_pod), self.ns)
+
+        await asyncio.gather(*(create(n) for n in names))
+        t_created = time.monotonic()
+        await self._wait(lambda: all(n in self.running for n in names), timeout)
+        t_running = time.monotonic()
+
+        async def delete(n):
+            async with sem:
+                try:
+                    await self.client.delete("pods", n, self.ns)
+                except APIStatusError as e:
+                    if e.code != 404:
+                        raise
+
+        await asyncio.gather(*(delete(n) for n in names))
+        await self._wait(lambda: all(n in self.gone for n in names), timeout)
+        t_gone = time.monotonic()
+        lat = [self.running[n] - self.created[n] for n in names]
+        sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)
+        return {"pods": len(names), "create_s": t_created - t0, "to_running_s": t_running - t0,
+                "cycle_s": t_gone - t0, "latencies": lat, "scheduled_times": [s - t0 for s in sched]}
+
+    async def stop(self):
+        if self._stream:
+            self._stream.close()
+        if self._watch_task:
+            self._watch_task.cancel()
+        await self.client.close()
+
+
+def interval_rates(times, bucket=1.0):
+    """Scheduled pods per 1-s interval (scheduler_perf sampling); returns (avg, min) over full buckets."""
+    if not times:
+        return 0.0, 0.0
+    end = max(times)
+    n = int(end // bucket)
+    if n < 1:
+        return len(times) / max(end, 1e-9), len(times) / max(end, 1e-9)
+    counts = [0] * (n + 1)
+    for t in times:
+        counts[min(int(t // bucket), n)] += 1
+    full = counts[:n]
+    return sum(full) / (n * bucket), min(full) / bucket
