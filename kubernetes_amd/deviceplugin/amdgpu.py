@@ -31,7 +31,8 @@ log = logging.getLogger("amdgpu-plugin")
 
 
 def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None) -> dict:
-    hbm_gib = g.vram_total_mb // 1024
+    # usable VRAM is reported a few MiB below the 288 GB HBM3E stack size: round up to GiB
+    hbm_gib = -(-g.vram_total_mb // 1024)
     attrs = {
         core.ATTR_ARCH: g.arch or "unknown",
         core.ATTR_PRODUCT: g.product,
@@ -80,7 +81,7 @@ class AMDGPUPlugin(DevicePluginServer):
             g0 = self.gpus[0]
             labels = {"amd.com/gpu.arch": g0.arch, "amd.com/gpu.product": g0.product,
                       "amd.com/gpu.count": str(len(self.gpus)),
-                      "amd.com/gpu.hbm": f"{g0.vram_total_mb // 1024}Gi"}
+                      "amd.com/gpu.hbm": f"{-(-g0.vram_total_mb // 1024)}Gi"}
         super().__init__(core.AMD_GPU, os.path.join(plugins_dir, "amd.com", socket_name), devs,
                          init_timeout=init_timeout, labels=labels)
         self._health_task = None

@@ -453,7 +453,8 @@ struct SmiBackend : Backend {
     memset(&p, 0, sizeof p);
     if (f.amdsmi_get_power_info && f.amdsmi_get_power_info(h, &p) == AMDSMI_STATUS_SUCCESS) {
       o->power_w = p.current_socket_power != 0xFFFFFFFFu ? p.current_socket_power : p.average_socket_power;
-      o->power_limit_w = p.power_limit;
+      // some drivers report the cap in microwatts
+      o->power_limit_w = p.power_limit > 100000u ? p.power_limit / 1000000u : p.power_limit;
     }
     int64_t t = 0;
     if (f.amdsmi_get_temp_metric && f.amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &t) == AMDSMI_STATUS_SUCCESS)
@@ -498,7 +499,15 @@ struct SmiBackend : Backend {
   }
 };
 
-std::unique_ptr<Backend> g_b;
+// The backend is deliberately NOT destroyed during static destruction: tearing AMD SMI down
+// after the HIP runtime / other libraries have begun unloading crashes the process at exit.
+// kamd_shutdown() is the explicit teardown.
+struct BackendHolder {
+  std::unique_ptr<Backend> p;
+  ~BackendHolder() { (void)p.release(); }
+};
+BackendHolder g_hold;
+#define g_b g_hold.p
 
 }  // namespace
 
