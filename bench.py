@@ -199,7 +199,15 @@ def main():
             url, procs = spawn_control_plane(tmp, args)   # before any GPU init
         d.init()
         url = d.broadcast(url)
-        allstats = asyncio.run(rank_main(args, d, url))
+        if os.environ.get("KAMD_PROFILE_DIR"):
+            import cProfile
+            pr = cProfile.Profile()
+            pr.enable()
+            allstats = asyncio.run(rank_main(args, d, url))
+            pr.disable()
+            pr.dump_stats(os.path.join(os.environ["KAMD_PROFILE_DIR"], f"rank{d.rank}.prof"))
+        else:
+            allstats = asyncio.run(rank_main(args, d, url))
     finally:
         for p in procs:
             p.terminate()

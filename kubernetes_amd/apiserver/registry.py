@@ -109,14 +109,18 @@ class PodStrategy(Strategy):
     def prepare_update(self, new, old):
         super().prepare_update(new, old)
         # scheduler-owned fields are only written through pods/binding
-        ns, os_ = new.setdefault("spec", {}), old.get("spec") or {}
+        os_ = old.get("spec") or {}
+        ns = new["spec"] = dict(new.get("spec") or {})   # never mutate structure shared with the cache
         if os_.get("nodeName"):
             ns["nodeName"] = os_["nodeName"]
         if os_.get("extendedResources") and ns.get("extendedResources"):
             amap = {r.get("name"): r.get("assigned") for r in os_["extendedResources"]}
+            ers = []
             for r in ns["extendedResources"]:
-                if amap.get(r.get("name")):
-                    r["assigned"] = amap[r["name"]]
+                if amap.get(r.get("name")) and r.get("assigned") != amap[r["name"]]:
+                    r = dict(r, assigned=amap[r["name"]])
+                ers.append(r)
+            ns["extendedResources"] = ers
 
     def validate_update(self, new, old):
         errs = validation.validate_pod(new)

@@ -225,7 +225,9 @@ class APIServer:
             raise bad_request("body must be a JSON object")
         key, prev = self._existing(ri, namespace, name)
         old = prev.obj
-        om, nm = old["metadata"], obj.setdefault("metadata", {})
+        obj = dict(obj)
+        om = old["metadata"]
+        nm = obj["metadata"] = dict(obj.get("metadata") or {})
         if nm.get("name") and nm["name"] != name:
             raise bad_request("the name of the object does not match the name on the URL")
         want_rv = nm.get("resourceVersion")
@@ -280,7 +282,9 @@ class APIServer:
         key, prev = self._existing(ri, namespace, name)
         try:
             patch = codec.loads(patch_body)
-            new = apply_patch(content_type, fast_copy(prev.obj), patch)
+            # merge / strategic patches build new dicts along the patched paths only and share
+            # the rest with the cached object (copy-on-write); update() never mutates shared parts
+            new = apply_patch(content_type, prev.obj, patch)
         except (JSONPatchError, ValueError) as e:
             if isinstance(e, ValueError) and "unsupported patch type" in str(e):
                 raise APIError(415, "UnsupportedMediaType", str(e))
@@ -301,8 +305,10 @@ class APIServer:
         self._admit(a)
         self._validate_admission(a)
         strat = self.strategies[ri.plural]
-        obj = fast_copy(old)
-        om = obj["metadata"]
+        obj = dict(old)                      # copy-on-write: only metadata/status are rewritten
+        om = obj["metadata"] = dict(old["metadata"])
+        if "status" in old and isinstance(old["status"], dict):
+            obj["status"] = dict(old["status"])
         grace = strat.graceful_seconds(old, opts)
         fins = list(om.get("finalizers") or [])
         pol = opts.get("propagationPolicy")
@@ -347,11 +353,18 @@ class APIServer:
         a = adm.Attributes(adm.CREATE, "pods", "binding", namespace, name, binding, prev.obj, user, "Binding")
         self._admit(a)
         self._validate_admission(a)
-        pod = fast_copy(prev.obj)
-        try:
-            apply_binding(pod, binding)
-        except APIError:
-            raise
+        old = prev.obj
+        pod = dict(old)   # copy-on-write of exactly what apply_binding rewrites
+        pod["metadata"] = dict(old["metadata"])
+        if "annotations" in old["metadata"]:
+            pod["metadata"]["annotations"] = dict(old["metadata"]["annotations"])
+        pod["spec"] = dict(old.get("spec") or {})
+        if pod["spec"].get("extendedResources"):
+            pod["spec"]["extendedResources"] = [dict(r) for r in pod["spec"]["extendedResources"]]
+        pod["status"] = dict(old.get("status") or {})
+        if "conditions" in pod["status"]:
+            pod["status"]["conditions"] = list(pod["status"]["conditions"])
+        apply_binding(pod, binding)
         node = pod["spec"]["nodeName"]
         idx = self.node_devices.get(node) or {}
         for rn, ids in core.pod_assigned_devices(pod).items():

@@ -35,4 +35,18 @@ def run_until_signal(main_coro_factory):
         closer = getattr(comp, "stop", None)
         if closer is not None:
             await closer()
+    prof_dir = os.environ.get("KAMD_PROFILE_DIR")
+    if prof_dir:
+        # pprof-equivalent: whole-process cProfile dump at shutdown (reference: /debug/pprof)
+        import cProfile
+        import sys
+        pr = cProfile.Profile()
+        pr.enable()
+        try:
+            asyncio.run(runner())
+        finally:
+            pr.disable()
+            os.makedirs(prof_dir, exist_ok=True)
+            pr.dump_stats(os.path.join(prof_dir, os.path.basename(sys.argv[0]).replace(".py", "") + f".{os.getpid()}.prof"))
+        return
     asyncio.run(runner())

@@ -62,40 +62,73 @@ class PodInfo:
         self.assigned = core.pod_assigned_devices(pod)
 
 
+def _hive(dev):
+    return (dev.get("attributes") or {}).get(core.ATTR_HIVE, "")
+
+
+def _healthy(dev):
+    return dev.get("health", core.HEALTHY) == core.HEALTHY
+
+
 class ERManager:
+    """Per-node device accounting. Besides the reference's allocatable/available/used maps it
+    keeps, per resource, the healthy free devices grouped by xGMI hive (`hive_free`) and their
+    count (`nfree`), maintained incrementally so the scheduler's filter is O(hives), not
+    O(devices), per node."""
+
+    __slots__ = ("allocatable", "available", "used", "hive_free", "nfree")
+
     def __init__(self):
         self.allocatable: dict[str, dict[str, dict]] = {}
         self.available: dict[str, dict[str, dict]] = {}
-        self.used: dict[str, dict[str, str]] = {}     # rname -> {device id: pod key}
+        self.used: dict[str, dict[str, str]] = {}              # rname -> {device id: pod key}
+        self.hive_free: dict[str, dict[str, dict]] = {}        # rname -> {hive: {id: dev}} (healthy, free)
+        self.nfree: dict[str, int] = {}
 
     def clone(self):
         c = ERManager()
         c.allocatable = {k: dict(v) for k, v in self.allocatable.items()}
         c.available = {k: dict(v) for k, v in self.available.items()}
         c.used = {k: dict(v) for k, v in self.used.items()}
+        c.hive_free = {k: {h: dict(d) for h, d in v.items()} for k, v in self.hive_free.items()}
+        c.nfree = dict(self.nfree)
         return c
+
+    def _take(self, rn, i):
+        avail = self.available.get(rn)
+        if avail is None:
+            return
+        dev = avail.pop(i, None)
+        if dev is not None and _healthy(dev):
+            hf = self.hive_free[rn].get(_hive(dev))
+            if hf is not None and hf.pop(i, None) is not None:
+                self.nfree[rn] -= 1
+
+    def _give(self, rn, i):
+        dev = self.allocatable.get(rn, {}).get(i)
+        if dev is None:
+            return
+        self.available.setdefault(rn, {})[i] = dev
+        if _healthy(dev):
+            self.hive_free.setdefault(rn, {}).setdefault(_hive(dev), {})[i] = dev
+            self.nfree[rn] = self.nfree.get(rn, 0) + 1
 
     def add_pod(self, key, assigned: dict):
         for rn, ids in assigned.items():
             used = self.used.setdefault(rn, {})
-            avail = self.available.get(rn)
             for i in ids:
                 used[i] = key
-                if avail is not None:
-                    avail.pop(i, None)
+                self._take(rn, i)
 
     def remove_pod(self, key, assigned: dict):
         for rn, ids in assigned.items():
             used = self.used.get(rn)
             if not used:
                 continue
-            alloc = self.allocatable.get(rn, {})
-            avail = self.available.setdefault(rn, {})
             for i in ids:
                 if used.get(i) == key:
                     del used[i]
-                    if i in alloc:
-                        avail[i] = alloc[i]
+                    self._give(rn, i)
             if not used:
                 del self.used[rn]
 
@@ -103,17 +136,26 @@ class ERManager:
         ers = ((node.get("status") or {}).get("extendedResources")) or {}
         self.allocatable = {rn: dict((dom or {}).get("resources") or {}) for rn, dom in ers.items()}
         self.available = {}
+        self.hive_free = {}
+        self.nfree = {}
         for rn, devs in self.allocatable.items():
             used = self.used.get(rn, {})
-            self.available[rn] = {i: d for i, d in devs.items() if i not in used}
+            av = self.available[rn] = {}
+            hf = self.hive_free[rn] = {}
+            n = 0
+            for i, d in devs.items():
+                if i in used:
+                    continue
+                av[i] = d
+                if _healthy(d):
+                    hf.setdefault(_hive(d), {})[i] = d
+                    n += 1
+            self.nfree[rn] = n
 
     def free_count(self, rname, healthy_only=True) -> int:
-        avail = self.available.get(rname)
-        if not avail:
-            return 0
-        if not healthy_only:
-            return len(avail)
-        return sum(1 for d in avail.values() if d.get("health", core.HEALTHY) == core.HEALTHY)
+        if healthy_only:
+            return self.nfree.get(rname, 0)
+        return len(self.available.get(rname) or ())
 
 
 class NodeInfo:

@@ -2,27 +2,33 @@
 
 Parity: `plugin/pkg/scheduler/core/generic_scheduler.go:109-365` (`Schedule`, `findNodesThatFit`
 with the fork's `GetExtendedResources` call at :354-358, `PrioritizeNodes` :509, `selectHost`
-round-robin among ties :177) and `algorithm.ScheduleAlgorithm.Schedule` returning
-`(host, ExtendedResourceBinding)` (fork: scheduler_interface.go:49).
+round-robin among ties :177), `algorithm.ScheduleAlgorithm.Schedule` returning
+`(host, ExtendedResourceBinding)` (fork: scheduler_interface.go:49), and the equivalence cache
+(`plugin/pkg/scheduler/core/equivalence_cache.go`).
 
 Differences by design:
-  * predicates, the device allocation and scoring run in ONE pass per node (no separate
-    Parallelize(16) fan-outs, no per-node deep copy of available devices);
-  * a node that cannot possibly hold the pod's device count is rejected in O(1) before any
-    predicate runs;
-  * `percentage_of_nodes_to_score` (later-Kubernetes knob): stop filtering once enough feasible
-    nodes are found, starting each cycle where the previous one stopped (fairness). 100 = the
-    reference behaviour (score every node).
+  * predicates, the device-fit check and the raw priority values run in ONE pass per node;
+    the device binding is materialised only for the selected node (no separate Parallelize(16)
+    fan-outs, no per-node deep copy of available devices);
+  * a node that cannot hold the pod's device count is rejected in O(1) (per-hive free counts);
+  * equivalence cache: pods of one equivalence class (same resource/selector/toleration/device
+    shape — e.g. every replica of a job, every density pod) reuse each node's evaluation
+    until that node's generation changes. A bind touches one node, so the next pod of the
+    class re-evaluates one node instead of all of them. Disabled for pods whose placement
+    depends on other nodes' pods (inter-pod affinity) and when extenders are configured;
+  * `percentage_of_nodes_to_score` (later-Kubernetes knob), default 100 = reference behaviour.
 """
 from __future__ import annotations
 
+import json
 import logging
+from collections import OrderedDict
 
 from ..api import core
 from . import predicates as P
 from . import priorities as PR
 from .cache import PodInfo, SchedulerCache
-from .topology import POLICY_ANNOTATION, PREFERRED, Request, allocate
+from .topology import POLICY_ANNOTATION, PREFERRED, Request, allocate, fast_path, feasible
 
 log = logging.getLogger("scheduler")
 
@@ -42,7 +48,7 @@ class FitError(Exception):
 class CycleContext:
     """Per-pod scheduling-cycle state shared by predicates and priorities."""
 
-    def __init__(self, cache: SchedulerCache, pod):
+    def __init__(self, cache: SchedulerCache, pod, with_affinity=True):
         self.cache = cache
         spec = pod.get("spec") or {}
         self.tolerates_unschedulable = any(
@@ -55,7 +61,7 @@ class CycleContext:
         self.owner_uid = ref
         self.node_affinity_prefs = PR.compile_node_affinity_prefs(pod)
         self.topo_scores = {}
-        self.anti_affinity_terms = cache_anti_affinity(cache)
+        self.anti_affinity_terms = cache_anti_affinity(cache) if with_affinity else []
         self.any_anti_affinity = bool(self.anti_affinity_terms)
 
     def pods_by_topology(self, key, val):
@@ -85,9 +91,32 @@ def cache_anti_affinity(cache):
     return out
 
 
+def _has_pod_affinity(pod):
+    aff = (pod.get("spec") or {}).get("affinity") or {}
+    return bool(aff.get("podAffinity") or aff.get("podAntiAffinity"))
+
+
+def equivalence_key(pod) -> str:
+    """Everything predicates/priorities read from the pod, minus per-pod identity (names,
+    UIDs, the ResourceV2-generated ER names)."""
+    spec = pod.get("spec") or {}
+    md = pod.get("metadata") or {}
+    owner = None
+    for r in md.get("ownerReferences") or ():
+        if r.get("controller"):
+            owner = r.get("uid")
+    ers = [((per.get("resources") or {}).get("limits"), (per.get("affinity") or {}).get("required"))
+           for per in spec.get("extendedResources") or ()]
+    ctrs = [(c.get("resources"), [p.get("hostPort") for p in c.get("ports") or () if p.get("hostPort")])
+            for c in (spec.get("containers") or []) + (spec.get("initContainers") or [])]
+    proj = (md.get("namespace"), owner, spec.get("nodeName"), spec.get("nodeSelector"), spec.get("affinity"),
+            spec.get("tolerations"), ers, ctrs, (md.get("annotations") or {}).get(POLICY_ANNOTATION))
+    return json.dumps(proj, sort_keys=True, separators=(",", ":"))
+
+
 class GenericScheduler:
     def __init__(self, cache: SchedulerCache, predicates=None, priorities=None, percentage_of_nodes_to_score=100,
-                 extenders=None):
+                 extenders=None, equivalence_cache=True, ecache_classes=256):
         self.cache = cache
         names = predicates or P.DEFAULT_PREDICATES
         self.predicates = [(n, P.PREDICATES[n]) for n in names]
@@ -98,11 +127,28 @@ class GenericScheduler:
         self._next_start = 0
         self._last_node_index = 0
         self._check_affinity = "MatchInterPodAffinity" in names
+        self.use_ecache = equivalence_cache
+        self.ecache: OrderedDict[str, dict] = OrderedDict()
+        self.ecache_classes = ecache_classes
+        self.ecache_hits = 0
+        self.ecache_misses = 0
 
     def num_feasible_to_find(self, n):
         if self.pct >= 100 or n < 100:
             return n
         return max(100, n * self.pct // 100)
+
+    def _active_priorities(self, pi, ctx):
+        out = []
+        for name, w, fn, reverse, norm in self.priorities:
+            if name in ("XGMITopologyPriority", "GPUBinPackingPriority") and not pi.er:
+                continue
+            if name == "SelectorSpreadPriority" and not ctx.owner_uid:
+                continue
+            if name == "NodeAffinityPriority" and not ctx.node_affinity_prefs:
+                continue
+            out.append((name, w, fn, reverse, norm))
+        return out
 
     def schedule(self, pod, pi: PodInfo | None = None):
         """Returns (node_name, extended_resource_binding)."""
@@ -110,13 +156,26 @@ class GenericScheduler:
         if not nodes:
             raise FitError(pod, 0, {})
         pi = pi or PodInfo(pod)
-        ctx = CycleContext(self.cache, pod) if (self._check_affinity or pi.er) else _LiteContext(self.cache, pod)
+        affinity_sensitive = self._check_affinity and (_has_pod_affinity(pod) or bool(self.cache.anti_pods))
+        ctx = CycleContext(self.cache, pod, with_affinity=affinity_sensitive)
         policy = ((pod["metadata"].get("annotations") or {}).get(POLICY_ANNOTATION) or PREFERRED)
         reqs = [Request(name, rn, n, sel) for name, rn, n, sel in pi.er]
+        fast = bool(reqs) and fast_path(reqs)
         need = {}
         for r in reqs:
             need[r.rname] = need.get(r.rname, 0) + r.count
-        feasible, bindings, failed = [], {}, {}
+        prios = self._active_priorities(pi, ctx)
+        ec = None
+        if self.use_ecache and not affinity_sensitive and not self.extenders and (fast or not reqs):
+            key = equivalence_key(pod)
+            ec = self.ecache.get(key)
+            if ec is None:
+                ec = self.ecache[key] = {}
+                if len(self.ecache) > self.ecache_classes:
+                    self.ecache.popitem(last=False)
+            else:
+                self.ecache.move_to_end(key)
+        fnodes, raws, bindings, failed = [], [], {}, {}
         want = self.num_feasible_to_find(len(nodes))
         n = len(nodes)
         start = self._next_start % n
@@ -125,7 +184,22 @@ class GenericScheduler:
         for off in range(n):
             ni = nodes[(start + off) % n]
             checked += 1
+            if ec is not None:
+                ent = ec.get(ni.name)
+                if ent is not None and ent[0] == ni.generation:
+                    self.ecache_hits += 1
+                    if ent[1]:
+                        failed[ni.name] = ent[1]
+                        continue
+                    ctx.topo_scores[ni.name] = ent[2]
+                    fnodes.append(ni)
+                    raws.append(ent[3])
+                    if len(fnodes) >= want:
+                        break
+                    continue
+                self.ecache_misses += 1
             reason = None
+            score = None
             for rn, cnt in need.items():
                 if ni.er.free_count(rn) < cnt:
                     reason = f"Insufficient {rn}"
@@ -136,76 +210,75 @@ class GenericScheduler:
                     if reason:
                         break
             if reason is None and reqs:
-                binding, score, reason = allocate(reqs, ni.er, policy)
-                if binding is not None:
-                    bindings[ni.name] = binding
+                if fast:
+                    ok, score, reason = feasible(reqs, ni.er, policy)
+                    if ok:
+                        reason = None
+                else:
+                    binding, score, reason = allocate(reqs, ni.er, policy)
+                    if binding is not None:
+                        bindings[ni.name] = binding
+                        reason = None
+            raw = None
+            if reason is None:
+                if score is not None:
                     ctx.topo_scores[ni.name] = score
-                    reason = reason or None
+                raw = tuple(fn(pod, pi, ni, ctx) for _, _, fn, _, _ in prios)
+            if ec is not None:
+                ec[ni.name] = (ni.generation, reason, score, raw)
             if reason:
                 failed[ni.name] = reason
                 continue
-            feasible.append(ni)
-            if len(feasible) >= want:
+            fnodes.append(ni)
+            raws.append(raw)
+            if len(fnodes) >= want:
                 break
         self._next_start = start + checked
         for ext in self.extenders:
-            feasible, efailed = ext.filter(pod, feasible)
+            keep, efailed = ext.filter(pod, fnodes)
             failed.update(efailed)
-        if not feasible:
+            keepset = {k.name for k in keep}
+            raws = [r for f, r in zip(fnodes, raws) if f.name in keepset]
+            fnodes = [f for f in fnodes if f.name in keepset]
+        if not fnodes:
             raise FitError(pod, n, failed)
-        if len(feasible) == 1:
-            host = feasible[0].name
-            return host, bindings.get(host, {})
-        scores = self.prioritize(pod, pi, feasible, ctx)
-        for ext in self.extenders:
-            for name, s in ext.prioritize(pod, feasible).items():
-                scores[name] = scores.get(name, 0) + s
-        host = self.select_host(scores, feasible)
+        if len(fnodes) == 1:
+            host = fnodes[0].name
+        else:
+            scores = self._combine(prios, fnodes, raws)
+            for ext in self.extenders:
+                for name, s in ext.prioritize(pod, fnodes).items():
+                    scores[name] = scores.get(name, 0) + s
+            host = self.select_host(scores, fnodes)
+        if fast:
+            # materialise the device binding for the chosen node only
+            binding, _, reason = allocate(reqs, self.cache.nodes[host].er, policy)
+            if binding is None:  # cannot happen: feasible() and allocate() agree
+                raise FitError(pod, n, {host: reason})
+            return host, binding
         return host, bindings.get(host, {})
 
-    def prioritize(self, pod, pi, nodes, ctx):
-        total = {ni.name: 0.0 for ni in nodes}
-        for name, w, fn, reverse, norm in self.priorities:
-            if name == "XGMITopologyPriority" and not pi.er:
-                continue
-            if name == "GPUBinPackingPriority" and not pi.er:
-                continue
-            if name == "SelectorSpreadPriority" and not ctx.owner_uid:
-                continue
-            if name == "NodeAffinityPriority" and not ctx.node_affinity_prefs:
-                continue
-            raw = [fn(pod, pi, ni, ctx) for ni in nodes]
+    @staticmethod
+    def _combine(prios, nodes, raws):
+        total = [0.0] * len(nodes)
+        for j, (_, w, _, reverse, norm) in enumerate(prios):
+            col = [r[j] for r in raws]
             if norm:
-                raw = PR.normalize(raw, reverse)
-            for ni, s in zip(nodes, raw):
-                total[ni.name] += w * s
-        return total
+                col = PR.normalize(col, reverse)
+            for i, s in enumerate(col):
+                total[i] += w * s
+        return {ni.name: t for ni, t in zip(nodes, total)}
+
+    def prioritize(self, pod, pi, nodes, ctx):
+        prios = self._active_priorities(pi, ctx)
+        raws = [tuple(fn(pod, pi, ni, ctx) for _, _, fn, _, _ in prios) for ni in nodes]
+        return self._combine(prios, nodes, raws)
 
     def select_host(self, scores, nodes):
         best = max(scores.values())
         ties = [ni.name for ni in nodes if scores[ni.name] == best]
         self._last_node_index += 1
         return ties[self._last_node_index % len(ties)]
-
-
-class _LiteContext(CycleContext):
-    """Context without the cluster-wide anti-affinity scan (no affinity predicate, no devices)."""
-
-    def __init__(self, cache, pod):
-        self.cache = cache
-        spec = pod.get("spec") or {}
-        self.tolerates_unschedulable = any(
-            t.get("key") == "node.kubernetes.io/unschedulable" and t.get("operator") == "Exists"
-            for t in spec.get("tolerations") or ())
-        ref = None
-        for r in pod["metadata"].get("ownerReferences") or ():
-            if r.get("controller"):
-                ref = r.get("uid")
-        self.owner_uid = ref
-        self.node_affinity_prefs = PR.compile_node_affinity_prefs(pod)
-        self.topo_scores = {}
-        self.anti_affinity_terms = []
-        self.any_anti_affinity = False
 
 
 def pod_is_gpu(pod) -> bool:

@@ -57,6 +57,50 @@ def _links(dev):
         return 0
 
 
+def _score(free, n, numa_fit):
+    # 10 for a perfect fit, decreasing with leftover fragments in the chosen hive
+    return 9.0 - min(free - n, 8) / 8.0 * 4.0 + (1.0 if numa_fit else 0.0)
+
+
+def fast_path(requests) -> bool:
+    """Feasibility + score can be computed from the per-hive free lists alone."""
+    return len(requests) == 1 and requests[0].selector is None and not requests[0].error
+
+
+def feasible(requests, er, policy=PREFERRED):
+    """Filter-phase check for a single selector-less request (the common case): returns
+    (ok, score, reason) without materialising a binding. Must agree with `allocate()`."""
+    r = requests[0]
+    n = r.count
+    hives = er.hive_free.get(r.rname)
+    if not hives or er.nfree.get(r.rname, 0) < n:
+        return False, 0, f"Insufficient {r.rname}"
+    need_links = n - 1 if n > 1 else 0
+    best = None
+    total = 0
+    for h, devs in hives.items():
+        if need_links:
+            c = sum(1 for d in devs.values() if _links(d) >= need_links)
+        else:
+            c = len(devs)
+        total += c
+        if c >= n and (best is None or (c, h) < best[:2]):
+            best = (c, h, devs)
+    if best is not None:
+        c, _, devs = best
+        numa = {}
+        for d in devs.values():
+            if not need_links or _links(d) >= need_links:
+                k = (d.get("attributes") or {}).get(core.ATTR_NUMA, "")
+                numa[k] = numa.get(k, 0) + 1
+        return True, _score(c, n, any(v >= n for v in numa.values())), ""
+    if total < n:
+        return False, 0, f"Insufficient {r.rname}"
+    if policy == REQUIRED and n > 1:
+        return False, 0, f"no single xGMI hive has {n} free {r.rname}"
+    return True, 1.0, ""
+
+
 def allocate(requests, er, policy=PREFERRED):
     """requests: list[Request]; er: ERManager of the node.
     Returns (binding, score, reason). binding is None on failure."""
@@ -72,7 +116,9 @@ def allocate(requests, er, policy=PREFERRED):
         need_links = r.count - 1 if r.count > 1 else 0
         sel = r.selector
         cands = []
-        for did, dev in avail.items():
+        hf = er.hive_free.get(r.rname)
+        it = ((i, d) for devs in hf.values() for i, d in devs.items()) if hf is not None else avail.items()
+        for did, dev in it:
             if did in taken or dev.get("health", core.HEALTHY) != core.HEALTHY:
                 continue
             attrs = dev.get("attributes") or {}
@@ -119,10 +165,7 @@ def _pick(cands, n, policy):
                 chosen.extend(sorted(v, key=lambda x: _idx(x[1])))
             chosen = chosen[:n]
             numa_bonus = 0.0
-        # 10 for a perfect fit, decreasing with leftover fragments in that hive
-        leftover = free - n
-        score = 9.0 - min(leftover, 8) / 8.0 * 4.0 + numa_bonus
-        return [d for d, _ in chosen], score
+        return [d for d, _ in chosen], _score(free, n, numa_bonus > 0)
     if policy == REQUIRED and n > 1:
         return None, 0
     # span hives: largest hives first, deterministic

@@ -17,7 +17,7 @@ MERGE_KEYS = {
 
 def merge_patch(target, patch):
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
+        return patch  # the decoded patch document is owned by the request: share, don't copy
     if not isinstance(target, dict):
         target = {}
     out = dict(target)
@@ -33,11 +33,11 @@ def strategic_merge_patch(target, patch, field=None):
     if not isinstance(patch, dict):
         if isinstance(patch, list) and isinstance(target, list):
             return _merge_list(target, patch, field)
-        return copy.deepcopy(patch)
+        return patch  # the decoded patch document is owned by the request: share, don't copy
     if patch.get("$patch") == "replace":
         p = dict(patch)
         p.pop("$patch")
-        return copy.deepcopy(p)
+        return p
     if not isinstance(target, dict):
         target = {}
     out = dict(target)
@@ -65,7 +65,7 @@ def _merge_list(target, patch, field):
                 if x not in res:
                     res.append(x)
             return res
-        return copy.deepcopy(patch)
+        return patch  # the decoded patch document is owned by the request: share, don't copy
     res = [dict(x) if isinstance(x, dict) else x for x in target]
     for item in patch:
         kv = item.get(key)

@@ -196,3 +196,42 @@ def test_end_to_end_scheduler_binds_distinct_devices(run):
         await c.close()
         await s.stop()
     run(main())
+
+
+def test_equivalence_cache_matches_uncached_decisions():
+    """The equivalence cache must not change any decision (equivalence_cache.go contract)."""
+    import random
+    rng = random.Random(7)
+    caches = [SchedulerCache(), SchedulerCache()]
+    for c in caches:
+        for k in range(6):
+            c.add_node(node(f"n{k}", [gpu_dev(i, hive="h0" if i < 4 else "h1", numa=str(i // 4)) for i in range(8)],
+                            cpu=str(8 + k), labels={"zone": f"z{k % 2}"}))
+    scheds = [GenericScheduler(caches[0], equivalence_cache=True), GenericScheduler(caches[1], equivalence_cache=False)]
+    live = []
+    for step in range(300):
+        if live and rng.random() < 0.35:
+            victim = live.pop(rng.randrange(len(live)))
+            for c in caches:
+                c.remove_pod(victim)
+            continue
+        n = rng.choice([1, 1, 1, 2, 4])
+        p = gpu_pod(f"p{step}", n)
+        p["spec"]["containers"][0]["resources"] = {"requests": {"cpu": rng.choice(["500m", "1", "2"])}}
+        if rng.random() < 0.2:
+            p["spec"]["nodeSelector"] = {"zone": "z1"}
+        out = []
+        for s in scheds:
+            try:
+                out.append(s.schedule(p))
+            except FitError as e:
+                out.append(("fit", str(e)))
+        assert out[0] == out[1], (step, out)
+        if out[0][0] != "fit":
+            host, erb = out[0]
+            ap = dict(p, spec=dict(p["spec"], nodeName=host,
+                                   extendedResources=[dict(p["spec"]["extendedResources"][0], assigned=erb["er"]["resources"])]))
+            for c in caches:
+                c.assume_pod(ap)
+            live.append(ap)
+    assert scheds[0].ecache_hits > 0
