@@ -30,7 +30,7 @@ class NodeHandle:
 class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
-                 health_interval=0.0, rocm_mount=None):
+                 health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
@@ -52,6 +52,9 @@ class LocalCluster:
         self.nodes: list[NodeHandle] = []
         self._sched_task = None
         self.smi = None
+        self.controllers = controllers            # None = no controller manager; list/["*"] = enabled set
+        self.controller_options = controller_options or {}
+        self.cm = None
 
     async def start(self):
         self.api = APIServer(admission_plugins=self.admission)
@@ -66,6 +69,10 @@ class LocalCluster:
         for i in range(self.n_nodes):
             await self.add_node(f"node-{i}" if not self.real else f"mi355x-{i}")
         await self.wait_nodes_ready()
+        if self.controllers is not None:
+            from .controllers.manager import ControllerManager
+            self.cm = ControllerManager(Client(self.url), self.controllers, self.controller_options)
+            await self.cm.start()
         return self
 
     async def add_node(self, name):
@@ -119,7 +126,20 @@ class LocalCluster:
             await asyncio.sleep(0.02)
         raise TimeoutError(f"pod {ns}/{name} not {phase}: {pod and pod.get('status')}")
 
+    async def wait_for(self, pred, timeout=30, interval=0.02):
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        last = None
+        while loop.time() < end:
+            last = await pred()
+            if last:
+                return last
+            await asyncio.sleep(interval)
+        raise TimeoutError(f"condition not met (last={last!r})")
+
     async def stop(self):
+        if self.cm is not None:
+            await self.cm.stop()
         for n in self.nodes:
             if n.plugin:
                 await n.plugin.stop()

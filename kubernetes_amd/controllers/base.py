@@ -1,0 +1,148 @@
+"""Controller framework: shared informers + rate-limited work queue + N async workers.
+
+Parity: the pattern every controller in `pkg/controller/*` follows (informer event handlers
+enqueue keys; `processNextWorkItem` → `syncHandler(key)`; errors re-queued with
+`AddRateLimited`, success `Forget`) and `controller.ControllerExpectations`
+(`pkg/controller/controller_utils.go`) which stops a controller from acting twice on the same
+intent before its informer has observed the result.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+
+from ..api import meta as m
+from ..api.labels import label_selector_as_selector
+from ..client.events import EventRecorder
+from ..parallel.workqueue import RateLimitingQueue
+
+log = logging.getLogger("controller")
+
+
+class Expectations:
+    """Per-key outstanding creates/deletes; satisfied when both reach 0 or the entry expires."""
+
+    TTL = 300.0
+
+    def __init__(self):
+        self._e: dict[str, list] = {}   # key -> [adds, dels, timestamp]
+
+    def expect(self, key, adds=0, dels=0):
+        self._e[key] = [adds, dels, time.monotonic()]
+
+    def raise_(self, key, adds=0, dels=0):
+        e = self._e.setdefault(key, [0, 0, time.monotonic()])
+        e[0] += adds
+        e[1] += dels
+
+    def observe_add(self, key):
+        e = self._e.get(key)
+        if e:
+            e[0] -= 1
+
+    def observe_del(self, key):
+        e = self._e.get(key)
+        if e:
+            e[1] -= 1
+
+    def satisfied(self, key):
+        e = self._e.get(key)
+        if e is None:
+            return True
+        if e[0] <= 0 and e[1] <= 0:
+            return True
+        return time.monotonic() - e[2] > self.TTL
+
+    def delete(self, key):
+        self._e.pop(key, None)
+
+
+class Controller:
+    name = "controller"
+    workers = 4
+
+    def __init__(self, client, factory, recorder: EventRecorder | None = None):
+        self.client = client
+        self.factory = factory
+        self.queue = RateLimitingQueue(self.name)
+        self.recorder = recorder or EventRecorder(client, f"{self.name}-controller")
+        self._tasks = []
+        self.syncs = 0
+
+    # subclasses: register informers/handlers in setup(), implement sync(key)
+    def setup(self):
+        raise NotImplementedError
+
+    async def sync(self, key):
+        raise NotImplementedError
+
+    def enqueue(self, obj_or_key):
+        key = obj_or_key if isinstance(obj_or_key, str) else m.ns_name(obj_or_key)
+        self.queue.add(key)
+
+    async def _worker(self):
+        while True:
+            key, shutdown = await self.queue.get()
+            if shutdown:
+                return
+            try:
+                await self.sync(key)
+                self.queue.forget(key)
+                self.syncs += 1
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:
+                log.debug("%s sync %s failed: %s", self.name, key, e)
+                self.queue.add_rate_limited(key)
+            finally:
+                self.queue.done(key)
+
+    def start(self):
+        self.recorder.start()
+        self._tasks = [asyncio.ensure_future(self._worker()) for _ in range(self.workers)]
+
+    def stop(self):
+        self.queue.shutdown()
+        for t in self._tasks:
+            t.cancel()
+        self.recorder.stop()
+
+
+def split_key(key):
+    if "/" in key:
+        ns, name = key.split("/", 1)
+        return ns, name
+    return None, key
+
+
+def controller_ref(obj):
+    return m.controller_of(obj)
+
+
+def selector_of(obj):
+    return label_selector_as_selector((obj.get("spec") or {}).get("selector"))
+
+
+def pod_is_active(pod):
+    st = (pod.get("status") or {}).get("phase")
+    return st not in ("Succeeded", "Failed") and not (pod.get("metadata") or {}).get("deletionTimestamp")
+
+
+def pod_is_ready(pod):
+    for c in (pod.get("status") or {}).get("conditions") or ():
+        if c.get("type") == "Ready":
+            return c.get("status") == "True"
+    return False
+
+
+def pod_from_template(template, owner, generate_name, namespace):
+    tmd = (template or {}).get("metadata") or {}
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"generateName": generate_name, "namespace": namespace,
+                        "labels": dict(tmd.get("labels") or {}), "annotations": dict(tmd.get("annotations") or {}),
+                        "ownerReferences": [m.owner_reference(owner)]},
+           "spec": m.fast_copy((template or {}).get("spec") or {})}
+    if not pod["metadata"]["annotations"]:
+        del pod["metadata"]["annotations"]
+    return pod

@@ -1,0 +1,226 @@
+"""DaemonSet and StatefulSet controllers.
+
+DaemonSet parity: `pkg/controller/daemon/daemon_controller.go` (nodeShouldRunDaemonPod: node
+selector / affinity / taints-tolerations, one pod per eligible node, delete pods on nodes that
+no longer qualify, status counts). Design choice: instead of the 1.9 behaviour of writing
+`spec.nodeName` directly, each daemon pod is pinned with required node affinity
+(`matchFields metadata.name`) and goes through the scheduler — so a DaemonSet requesting
+`amd.com/gpu` (e.g. a per-node GPU burn-in / xGMI probe) gets real device IDs allocated.
+
+StatefulSet parity: `pkg/controller/statefulset/stateful_set_control.go` — ordinal pods
+`<name>-<i>`, OrderedReady (create i only when 0..i-1 are Running and Ready, delete from the
+highest ordinal) or Parallel pod management, RollingUpdate by revision hash in reverse
+ordinal order, status replicas / readyReplicas / currentRevision / updateRevision.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import json
+
+from ..api import meta as m
+from ..client.rest import APIStatusError, is_already_exists, is_not_found
+from ..scheduler import predicates as P
+from ..scheduler.cache import NodeInfo, PodInfo
+from .base import Controller, controller_ref, pod_from_template, pod_is_active, pod_is_ready, split_key
+
+DS_TOLERATIONS = [
+    {"key": "node.alpha.kubernetes.io/notReady", "operator": "Exists", "effect": "NoExecute"},
+    {"key": "node.alpha.kubernetes.io/unreachable", "operator": "Exists", "effect": "NoExecute"},
+    {"key": "node.kubernetes.io/unschedulable", "operator": "Exists", "effect": "NoSchedule"},
+]
+
+
+class _Ctx:
+    tolerates_unschedulable = True
+
+
+def node_should_run(ds, node) -> bool:
+    tmpl = (ds.get("spec") or {}).get("template") or {}
+    pod = {"metadata": {"name": "probe", "namespace": ds["metadata"]["namespace"]},
+           "spec": m.fast_copy(tmpl.get("spec") or {})}
+    pod["spec"]["tolerations"] = list(pod["spec"].get("tolerations") or []) + DS_TOLERATIONS
+    ni = NodeInfo()
+    ni.set_node(node)
+    pi = PodInfo(pod)
+    for fn in (P.match_node_selector, P.pod_tolerates_node_taints):
+        if fn(pod, pi, ni, _Ctx()):
+            return False
+    return True
+
+
+class DaemonSetController(Controller):
+    name = "daemonset"
+
+    def setup(self):
+        self.ds_inf = self.factory.get("daemonsets")
+        self.node_inf = self.factory.get("nodes")
+        self.pod_inf = self.factory.get("pods")
+        self.ds_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+        self.node_inf.add_handler(self._all, lambda o, n: self._all(n), self._all)
+        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
+        if "controllerUID" not in self.pod_inf.store.indexers:
+            self.pod_inf.store.add_indexer("controllerUID", lambda p: [r["uid"] for r in (p["metadata"].get("ownerReferences") or ()) if r.get("controller")])
+        self._inflight: dict[str, set] = {}
+
+    def _all(self, _obj):
+        for ds in self.ds_inf.list():
+            self.enqueue(ds)
+
+    def _pod(self, pod):
+        ref = controller_ref(pod)
+        if ref and ref.get("kind") == "DaemonSet":
+            self.enqueue(f"{pod['metadata']['namespace']}/{ref['name']}")
+
+    @staticmethod
+    def _target_node(pod):
+        nn = (pod.get("spec") or {}).get("nodeName")
+        if nn:
+            return nn
+        aff = ((pod.get("spec") or {}).get("affinity") or {}).get("nodeAffinity") or {}
+        for t in (aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}).get("nodeSelectorTerms") or ():
+            for f in t.get("matchFields") or ():
+                if f.get("key") == "metadata.name" and f.get("values"):
+                    return f["values"][0]
+        return None
+
+    async def sync(self, key):
+        ds = self.ds_inf.get(key)
+        if ds is None or ds["metadata"].get("deletionTimestamp"):
+            return
+        ns, name = split_key(key)
+        pods = [p for p in self.pod_inf.store.by_index("controllerUID", ds["metadata"]["uid"]) if pod_is_active(p)]
+        by_node: dict[str, list] = {}
+        for p in pods:
+            by_node.setdefault(self._target_node(p), []).append(p)
+        want = {n["metadata"]["name"] for n in self.node_inf.list() if node_should_run(ds, n)}
+        creating = self._inflight.setdefault(key, set())
+        creating &= want - set(by_node)
+        tmpl = (ds.get("spec") or {}).get("template") or {}
+        todo = [n for n in sorted(want) if n not in by_node and n not in creating]
+        dels = [p for node, ps in by_node.items() if node not in want for p in ps]
+        dels += [p for node, ps in by_node.items() if node in want for p in ps[1:]]
+
+        async def create(node):
+            pod = pod_from_template(tmpl, ds, f"{name}-", ns)
+            spec = pod["spec"]
+            spec["tolerations"] = list(spec.get("tolerations") or []) + DS_TOLERATIONS
+            aff = spec.setdefault("affinity", {}).setdefault("nodeAffinity", {})
+            aff["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [
+                {"matchFields": [{"key": "metadata.name", "operator": "In", "values": [node]}]}]}
+            creating.add(node)
+            await self.client.create("pods", pod, ns)
+
+        await asyncio.gather(*(create(n) for n in todo), return_exceptions=True)
+        for p in dels:
+            try:
+                await self.client.delete("pods", p["metadata"]["name"], ns)
+            except APIStatusError:
+                pass
+        ready = sum(1 for ps in by_node.values() for p in ps if pod_is_ready(p))
+        st = {"desiredNumberScheduled": len(want), "currentNumberScheduled": len([n for n in by_node if n in want]),
+              "numberMisscheduled": len([n for n in by_node if n not in want and n]), "numberReady": ready,
+              "numberAvailable": ready, "updatedNumberScheduled": len([n for n in by_node if n in want]),
+              "observedGeneration": ds["metadata"].get("generation", 1)}
+        if {k: (ds.get("status") or {}).get(k) for k in st} != st:
+            try:
+                await self.client.patch("daemonsets", name, {"status": st}, ns, "merge", "status")
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise
+
+
+class StatefulSetController(Controller):
+    name = "statefulset"
+    workers = 2
+
+    def setup(self):
+        self.ss_inf = self.factory.get("statefulsets")
+        self.pod_inf = self.factory.get("pods")
+        self.ss_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
+
+    def _pod(self, pod):
+        ref = controller_ref(pod)
+        if ref and ref.get("kind") == "StatefulSet":
+            self.enqueue(f"{pod['metadata']['namespace']}/{ref['name']}")
+
+    async def sync(self, key):
+        ss = self.ss_inf.get(key)
+        if ss is None or ss["metadata"].get("deletionTimestamp"):
+            return
+        ns, name = split_key(key)
+        spec = ss.get("spec") or {}
+        replicas = int(spec.get("replicas", 1))
+        parallel = spec.get("podManagementPolicy") == "Parallel"
+        tmpl = spec.get("template") or {}
+        rev = hashlib.sha256(json.dumps(tmpl, sort_keys=True).encode()).hexdigest()[:10]
+        rev_name = f"{name}-{rev}"
+        uid = ss["metadata"]["uid"]
+        pods = {}
+        for p in self.pod_inf.list():
+            if p["metadata"].get("namespace") == ns and (controller_ref(p) or {}).get("uid") == uid:
+                try:
+                    pods[int(p["metadata"]["name"].rsplit("-", 1)[1])] = p
+                except (ValueError, IndexError):
+                    continue
+        # create / replace missing ordinals
+        for i in range(replicas):
+            p = pods.get(i)
+            if p is not None and (p.get("status") or {}).get("phase") in ("Failed", "Succeeded"):
+                await self._delete(p)
+                return
+            if p is None:
+                pod = pod_from_template(tmpl, ss, "", ns)
+                pod["metadata"].pop("generateName")
+                pod["metadata"]["name"] = f"{name}-{i}"
+                pod["metadata"]["labels"]["statefulset.kubernetes.io/pod-name"] = f"{name}-{i}"
+                pod["metadata"]["labels"]["controller-revision-hash"] = rev_name
+                pod["spec"]["hostname"] = f"{name}-{i}"
+                if spec.get("serviceName"):
+                    pod["spec"]["subdomain"] = spec["serviceName"]
+                try:
+                    await self.client.create("pods", pod, ns)
+                except APIStatusError as e:
+                    if not is_already_exists(e):
+                        raise
+                if not parallel:
+                    break
+            elif not parallel and not (pod_is_ready(p) and (p.get("status") or {}).get("phase") == "Running"):
+                break
+        # scale down from the highest ordinal
+        extra = sorted((i for i in pods if i >= replicas), reverse=True)
+        for i in extra:
+            p = pods[i]
+            if not p["metadata"].get("deletionTimestamp"):
+                await self._delete(p)
+            if not parallel:
+                break
+        # rolling update: replace the highest-ordinal pod on an old revision, one at a time
+        if (spec.get("updateStrategy") or {}).get("type", "RollingUpdate") == "RollingUpdate" and not extra:
+            all_ready = all(pods.get(i) is not None and pod_is_ready(pods[i]) for i in range(replicas))
+            if all_ready:
+                for i in sorted(range(replicas), reverse=True):
+                    p = pods[i]
+                    if (p["metadata"].get("labels") or {}).get("controller-revision-hash") != rev_name:
+                        await self._delete(p)
+                        break
+        cur = [p for i, p in pods.items() if i < replicas]
+        st = {"replicas": len(cur), "readyReplicas": sum(1 for p in cur if pod_is_ready(p)),
+              "currentReplicas": sum(1 for p in cur if (p["metadata"].get("labels") or {}).get("controller-revision-hash") == rev_name),
+              "updatedReplicas": sum(1 for p in cur if (p["metadata"].get("labels") or {}).get("controller-revision-hash") == rev_name),
+              "currentRevision": rev_name, "updateRevision": rev_name,
+              "observedGeneration": ss["metadata"].get("generation", 1)}
+        if {k: (ss.get("status") or {}).get(k) for k in st} != st:
+            try:
+                await self.client.patch("statefulsets", name, {"status": st}, ns, "merge", "status")
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise
+
+    async def _delete(self, p):
+        try:
+            await self.client.delete("pods", p["metadata"]["name"], p["metadata"]["namespace"])
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise

@@ -1,0 +1,188 @@
+"""ServiceAccount, Endpoints, ResourceQuota (status) and Disruption (PDB status) controllers.
+
+Parity: `pkg/controller/serviceaccount` (a `default` ServiceAccount in every namespace),
+`pkg/controller/endpoint/endpoints_controller.go` (Endpoints = ready / not-ready pod IPs of
+the service selector, per port), `pkg/controller/resourcequota` (status.used recomputed —
+including the fork's pod-level GPU requests, see admission/plugins.pod_usage),
+`pkg/controller/disruption/disruption.go` (PDB currentHealthy / desiredHealthy /
+disruptionsAllowed).
+"""
+from __future__ import annotations
+
+from ..api.labels import label_selector_as_selector, selector_from_set
+from ..api.quantity import Quantity
+from ..apiserver.admission.plugins import pod_usage
+from ..client.rest import APIStatusError, is_already_exists, is_not_found
+from .base import Controller, pod_is_ready, split_key
+
+
+class ServiceAccountController(Controller):
+    name = "serviceaccount"
+    workers = 1
+
+    def setup(self):
+        self.ns_inf = self.factory.get("namespaces")
+        self.sa_inf = self.factory.get("serviceaccounts")
+        self.ns_inf.add_handler(lambda n: self.enqueue(n["metadata"]["name"]), None, None)
+        self.sa_inf.add_handler(None, None, lambda sa: self.enqueue(sa["metadata"]["namespace"]))
+
+    async def sync(self, key):
+        ns = self.ns_inf.get(key)
+        if ns is None or ns["metadata"].get("deletionTimestamp"):
+            return
+        if self.sa_inf.get(f"{key}/default") is not None:
+            return
+        try:
+            await self.client.create("serviceaccounts", {"metadata": {"name": "default", "namespace": key}}, key)
+        except APIStatusError as e:
+            if not (is_already_exists(e) or e.code in (403, 404)):
+                raise
+
+
+class EndpointsController(Controller):
+    name = "endpoint"
+
+    def setup(self):
+        self.svc_inf = self.factory.get("services")
+        self.pod_inf = self.factory.get("pods")
+        self.ep_inf = self.factory.get("endpoints")
+        self.svc_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), self.enqueue)
+        self.pod_inf.add_handler(self._pod, lambda o, n: (self._pod(o), self._pod(n)), self._pod)
+
+    def _pod(self, pod):
+        ns = pod["metadata"].get("namespace")
+        labels = pod["metadata"].get("labels") or {}
+        for svc in self.svc_inf.list():
+            sel = (svc.get("spec") or {}).get("selector")
+            if svc["metadata"].get("namespace") == ns and sel and selector_from_set(sel).matches(labels):
+                self.enqueue(svc)
+
+    async def sync(self, key):
+        ns, name = split_key(key)
+        svc = self.svc_inf.get(key)
+        if svc is None:
+            try:
+                await self.client.delete("endpoints", name, ns)
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise
+            return
+        sel = (svc.get("spec") or {}).get("selector")
+        if not sel:
+            return
+        s = selector_from_set(sel)
+        ready, not_ready = [], []
+        for p in self.pod_inf.list():
+            if p["metadata"].get("namespace") != ns or not s.matches(p["metadata"].get("labels") or {}):
+                continue
+            ip = (p.get("status") or {}).get("podIP")
+            if not ip or p["metadata"].get("deletionTimestamp"):
+                continue
+            addr = {"ip": ip, "nodeName": (p.get("spec") or {}).get("nodeName"),
+                    "targetRef": {"kind": "Pod", "namespace": ns, "name": p["metadata"]["name"], "uid": p["metadata"]["uid"]}}
+            (ready if pod_is_ready(p) else not_ready).append(addr)
+        ports = [{"name": pt.get("name", ""), "port": pt.get("targetPort", pt.get("port")), "protocol": pt.get("protocol", "TCP")}
+                 for pt in (svc.get("spec") or {}).get("ports") or ()]
+        subsets = []
+        if ready or not_ready:
+            ss = {"ports": ports}
+            if ready:
+                ss["addresses"] = sorted(ready, key=lambda a: a["ip"])
+            if not_ready:
+                ss["notReadyAddresses"] = sorted(not_ready, key=lambda a: a["ip"])
+            subsets.append(ss)
+        cur = self.ep_inf.get(key)
+        if cur is not None and (cur.get("subsets") or []) == subsets:
+            return
+        ep = {"apiVersion": "v1", "kind": "Endpoints", "metadata": {"name": name, "namespace": ns,
+                                                                    "labels": svc["metadata"].get("labels") or {}},
+              "subsets": subsets}
+        if cur is None:
+            try:
+                await self.client.create("endpoints", ep, ns)
+                return
+            except APIStatusError as e:
+                if not is_already_exists(e):
+                    raise
+        await self.client.patch("endpoints", name, {"subsets": subsets}, ns)
+
+
+class ResourceQuotaController(Controller):
+    name = "resourcequota"
+    workers = 2
+
+    def setup(self):
+        self.rq_inf = self.factory.get("resourcequotas")
+        self.pod_inf = self.factory.get("pods")
+        self.rq_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
+
+    def _pod(self, pod):
+        ns = pod["metadata"].get("namespace")
+        for q in self.rq_inf.list():
+            if q["metadata"].get("namespace") == ns:
+                self.enqueue(q)
+
+    async def sync(self, key):
+        q = self.rq_inf.get(key)
+        if q is None:
+            return
+        ns, name = split_key(key)
+        hard = (q.get("spec") or {}).get("hard") or {}
+        used: dict[str, Quantity] = {}
+        for p in self.pod_inf.list():
+            if p["metadata"].get("namespace") != ns:
+                continue
+            for k, v in pod_usage(p).items():
+                used[k] = used[k] + v if k in used else v
+        st = {"hard": dict(hard), "used": {k: str(used.get(k, Quantity(0))) for k in hard}}
+        if (q.get("status") or {}) == st:
+            return
+        await self.client.patch("resourcequotas", name, {"status": st}, ns, "merge", "status")
+
+
+class DisruptionController(Controller):
+    name = "disruption"
+    workers = 2
+
+    def setup(self):
+        self.pdb_inf = self.factory.get("poddisruptionbudgets")
+        self.pod_inf = self.factory.get("pods")
+        self.pdb_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
+
+    def _pod(self, pod):
+        for pdb in self.pdb_inf.list():
+            if pdb["metadata"].get("namespace") == pod["metadata"].get("namespace"):
+                self.enqueue(pdb)
+
+    async def sync(self, key):
+        pdb = self.pdb_inf.get(key)
+        if pdb is None:
+            return
+        ns, name = split_key(key)
+        spec = pdb.get("spec") or {}
+        sel = label_selector_as_selector(spec.get("selector"))
+        pods = [p for p in self.pod_inf.list() if p["metadata"].get("namespace") == ns
+                and sel.matches(p["metadata"].get("labels") or {}) and not p["metadata"].get("deletionTimestamp")]
+        healthy = sum(1 for p in pods if pod_is_ready(p))
+        expected = len(pods)
+        if "minAvailable" in spec:
+            v = spec["minAvailable"]
+            desired = _abs(v, expected)
+        elif "maxUnavailable" in spec:
+            desired = max(0, expected - _abs(spec["maxUnavailable"], expected))
+        else:
+            desired = expected
+        st = {"currentHealthy": healthy, "desiredHealthy": desired, "expectedPods": expected,
+              "disruptionsAllowed": max(0, healthy - desired), "observedGeneration": pdb["metadata"].get("generation", 1)}
+        if {k: (pdb.get("status") or {}).get(k) for k in st} == st:
+            return
+        await self.client.patch("poddisruptionbudgets", name, {"status": st}, ns, "merge", "status")
+
+
+def _abs(v, total):
+    if isinstance(v, str) and v.endswith("%"):
+        import math
+        return int(math.ceil(float(v[:-1]) * total / 100.0))
+    return int(v)

@@ -106,6 +106,7 @@ class Kubelet:
         self.started = asyncio.Event()
         self.plugin_labels = {}
         self.informer_node_labels = {}
+        self._stopped = False
         self.smi = None   # set by the node agent when the real/fake AMD SMI is available (stats)
 
     # ------------------------------------------------------------------
@@ -127,6 +128,8 @@ class Kubelet:
         self.started.set()
 
     async def stop(self):
+        self._stopped = True
+        self._status_dirty.set()
         self.informer.stop()
         for t in self._tasks:
             t.cancel()
@@ -226,8 +229,10 @@ class Kubelet:
             log.warning("node status update failed: %s", e)
 
     async def _node_status_loop(self):
+        # exits on the _stopped flag, not only on cancellation: on Python 3.10 asyncio.wait_for
+        # can swallow a CancelledError that races with the inner future completing
         last = 0.0
-        while True:
+        while not self._stopped:
             timeout = max(0.0, self.status_freq - (time.monotonic() - last))
             try:
                 await asyncio.wait_for(self._status_dirty.wait(), timeout)
@@ -235,6 +240,8 @@ class Kubelet:
             except asyncio.TimeoutError:
                 pass
             self._status_dirty.clear()
+            if self._stopped:
+                return
             await self.update_node_status()
             last = time.monotonic()
 
