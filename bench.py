@@ -77,7 +77,9 @@ class Dist:
     def init(self):
         import torch
         self.torch = torch
-        self.cuda = torch.cuda.is_available()
+        # KAMD_BENCH_FORCE_CPU=1: rehearse N ranks with gloo and no GPU payload (e.g. 8 ranks on
+        # a 1-GPU box) — measures the control plane's scaling only
+        self.cuda = torch.cuda.is_available() and not os.environ.get("KAMD_BENCH_FORCE_CPU")
         if self.cuda:
             torch.cuda.set_device(self.local_rank)
         if self.world > 1:

@@ -1,0 +1,649 @@
+"""kubectl — command-line client.
+
+Parity: the cobra tree of `pkg/kubectl/cmd/cmd.go:216+` — create, apply, get, describe, delete,
+logs, label, annotate, patch, replace, scale, cordon, uncordon, drain, taint, top, rollout
+(status / history / undo), run, expose, version, api-versions, api-resources, cluster-info,
+config (view / use-context / set-cluster / set-context / get-contexts), explain, wait,
+auth can-i; kubeconfig loading (`staging/src/k8s.io/client-go/tools/clientcmd/loader.go:52`).
+Commands that need streaming sessions (exec / attach / port-forward / cp) report that the
+runtime does not support them.
+
+    python -m kubernetes_amd.kubectl get pods -o wide
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+import yaml
+
+from ..api import core, meta as m
+from ..client.rest import APIStatusError, Client, is_already_exists, is_not_found
+from . import printers
+
+DEFAULT_KUBECONFIG = os.path.expanduser("~/.kube/config")
+
+
+# ---------------------------------------------------------------------------
+# kubeconfig
+def load_kubeconfig(path=None):
+    path = path or os.environ.get("KUBECONFIG") or DEFAULT_KUBECONFIG
+    if not os.path.exists(path):
+        return {"apiVersion": "v1", "kind": "Config", "clusters": [], "contexts": [], "users": [], "current-context": ""}, path
+    with open(path) as f:
+        return yaml.safe_load(f) or {}, path
+
+
+def save_kubeconfig(cfg, path):
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f, sort_keys=False)
+
+
+def resolve_server(args):
+    if args.server:
+        return args.server, args.token, args.namespace
+    cfg, _ = load_kubeconfig(args.kubeconfig)
+    ctxname = args.context or cfg.get("current-context")
+    ctx = next((c["context"] for c in cfg.get("contexts") or () if c["name"] == ctxname), None)
+    server = os.environ.get("KUBERNETES_MASTER", "http://127.0.0.1:8080")
+    token = args.token
+    ns = args.namespace
+    if ctx:
+        cl = next((c["cluster"] for c in cfg.get("clusters") or () if c["name"] == ctx.get("cluster")), {})
+        us = next((u["user"] for u in cfg.get("users") or () if u["name"] == ctx.get("user")), {})
+        server = cl.get("server", server)
+        token = token or us.get("token")
+        ns = ns or ctx.get("namespace")
+    return server, token, ns
+
+
+# ---------------------------------------------------------------------------
+def read_manifests(paths):
+    docs = []
+    for p in paths:
+        files = []
+        if p == "-":
+            text = sys.stdin.read()
+            files.append(text)
+        elif os.path.isdir(p):
+            for fn in sorted(os.listdir(p)):
+                if fn.endswith((".yaml", ".yml", ".json")):
+                    files.append(open(os.path.join(p, fn)).read())
+        else:
+            files.append(open(p).read())
+        for text in files:
+            for d in yaml.safe_load_all(text):
+                if not d:
+                    continue
+                if d.get("kind", "").endswith("List") and "items" in d:
+                    docs.extend(d["items"])
+                else:
+                    docs.append(d)
+    return docs
+
+
+def ri_for_obj(o):
+    ri = m.BY_KIND.get(o.get("kind", ""))
+    if ri is None:
+        raise SystemExit(f"error: unable to recognize kind {o.get('kind')!r}")
+    return ri
+
+
+def split_targets(targets):
+    """['pods', 'a', 'b'] / ['pods/a', 'nodes/b'] / ['pod,node'] -> [(ri, name|None)]"""
+    out = []
+    if not targets:
+        raise SystemExit("error: You must specify the type of resource")
+    if "/" in targets[0]:
+        for t in targets:
+            r, n = t.split("/", 1)
+            ri = m.lookup(r)
+            if ri is None:
+                raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
+            out.append((ri, n))
+        return out
+    kinds = targets[0].split(",")
+    names = targets[1:]
+    for k in kinds:
+        ri = m.lookup(k)
+        if ri is None:
+            raise SystemExit(f'error: the server doesn\'t have a resource type "{k}"')
+        if names:
+            out.extend((ri, n) for n in names)
+        else:
+            out.append((ri, None))
+    return out
+
+
+class Kubectl:
+    def __init__(self, args, out=sys.stdout):
+        self.a = args
+        self.out = out
+        server, token, ns = resolve_server(args)
+        self.server = server
+        self.ns = ns or "default"
+        self.client = Client(server, token=token)
+
+    def p(self, *s):
+        print(*s, file=self.out)
+
+    def ns_for(self, ri, obj=None):
+        if not ri.namespaced:
+            return None
+        if obj is not None and (obj.get("metadata") or {}).get("namespace"):
+            return obj["metadata"]["namespace"]
+        return self.ns
+
+    # -- commands -----------------------------------------------------------------
+    async def cmd_get(self):
+        a = self.a
+        if a.filename:
+            objs = []
+            for d in read_manifests(a.filename):
+                ri = ri_for_obj(d)
+                objs.append(await self.client.get(ri.plural, d["metadata"]["name"], self.ns_for(ri, d)))
+            self.p(printers.render(objs, a.output, wide=a.output == "wide"))
+            return
+        for ri, name in split_targets(a.targets):
+            ns = None if (a.all_namespaces or not ri.namespaced) else self.ns
+            if name:
+                obj = await self.client.get(ri.plural, name, ns)
+                self.p(printers.render([obj], a.output, ri.kind, a.output == "wide"))
+                continue
+            lst = await self.client.list(ri.plural, ns, a.selector, a.field_selector)
+            items = lst.get("items") or []
+            for o in items:
+                o.setdefault("kind", ri.kind)
+            if a.watch:
+                self.p(printers.render(items, a.output, ri.kind, a.output == "wide", a.all_namespaces))
+                st = await self.client.watch(ri.plural, ns, lst["metadata"]["resourceVersion"], a.selector, a.field_selector)
+                async for t, o in st:
+                    rows, h = printers.rows_for(ri.kind, [o], a.output == "wide")
+                    self.p(printers.table(rows, h).splitlines()[-1])
+                return
+            self.p(printers.render(items, a.output, ri.kind, a.output == "wide", a.all_namespaces, list_obj=lst if a.output in ("json", "yaml") else None))
+
+    async def cmd_describe(self):
+        for ri, name in split_targets(self.a.targets):
+            ns = None if not ri.namespaced else self.ns
+            if name:
+                objs = [await self.client.get(ri.plural, name, ns)]
+            else:
+                objs = (await self.client.list(ri.plural, ns, self.a.selector))["items"]
+            for o in objs:
+                o.setdefault("kind", ri.kind)
+                evs = []
+                try:
+                    fs = f"involvedObject.name={o['metadata']['name']},involvedObject.kind={ri.kind}"
+                    evs = (await self.client.list("events", o["metadata"].get("namespace") or "default", field_selector=fs))["items"]
+                except APIStatusError:
+                    pass
+                self.p(printers.describe(o, evs))
+                self.p("")
+
+    async def _apply_one(self, d, mode):
+        ri = ri_for_obj(d)
+        ns = self.ns_for(ri, d)
+        if ri.namespaced:
+            d.setdefault("metadata", {})["namespace"] = ns
+        name = d["metadata"].get("name")
+        verb = "created"
+        if mode == "create":
+            await self.client.create(ri.plural, d, ns)
+        elif mode == "replace":
+            cur = await self.client.get(ri.plural, name, ns)
+            d["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
+            await self.client.update(ri.plural, d, ns)
+            verb = "replaced"
+        else:  # apply: create or merge with last-applied annotation
+            ann = "kubectl.kubernetes.io/last-applied-configuration"
+            d["metadata"].setdefault("annotations", {})[ann] = json.dumps(d, sort_keys=True)
+            try:
+                await self.client.create(ri.plural, d, ns)
+            except APIStatusError as e:
+                if not is_already_exists(e):
+                    raise
+                await self.client.patch(ri.plural, name, d, ns, "strategic")
+                verb = "configured"
+        self.p(f"{ri.kind.lower()}/{name} {verb}")
+
+    async def cmd_create(self):
+        for d in read_manifests(self.a.filename):
+            await self._apply_one(d, "create")
+
+    async def cmd_apply(self):
+        for d in read_manifests(self.a.filename):
+            await self._apply_one(d, "apply")
+
+    async def cmd_replace(self):
+        for d in read_manifests(self.a.filename):
+            await self._apply_one(d, "replace")
+
+    async def cmd_delete(self):
+        a = self.a
+        targets = []
+        if a.filename:
+            for d in read_manifests(a.filename):
+                ri = ri_for_obj(d)
+                targets.append((ri, d["metadata"]["name"], self.ns_for(ri, d)))
+        else:
+            for ri, name in split_targets(a.targets):
+                ns = self.ns if ri.namespaced else None
+                if name:
+                    targets.append((ri, name, ns))
+                elif a.all or a.selector:
+                    for o in (await self.client.list(ri.plural, ns, a.selector))["items"]:
+                        targets.append((ri, o["metadata"]["name"], ns))
+                else:
+                    raise SystemExit("error: resource(s) were provided, but no name, label selector, or --all flag specified")
+        for ri, name, ns in targets:
+            try:
+                await self.client.delete(ri.plural, name, ns, grace_period=a.grace_period,
+                                         propagation=None if a.cascade else "Orphan")
+                self.p(f'{ri.kind.lower()} "{name}" deleted')
+            except APIStatusError as e:
+                if is_not_found(e) and a.ignore_not_found:
+                    continue
+                raise
+
+    async def cmd_logs(self):
+        a = self.a
+        name = a.pod.split("/", 1)[-1]
+        q = f"?container={a.container}" if a.container else ""
+        if a.tail is not None:
+            q += ("&" if q else "?") + f"tailLines={a.tail}"
+        st, body = await self.client.raw("GET", f"/api/v1/namespaces/{self.ns}/pods/{name}/log{q}")
+        if st != 200:
+            raise SystemExit(f"error: {body.decode(errors='replace')}")
+        self.out.write(body.decode(errors="replace"))
+
+    async def _meta_edit(self, field):
+        a = self.a
+        ri = m.lookup(a.resource.split("/")[0])
+        names = [a.resource.split("/", 1)[1]] if "/" in a.resource else [a.name]
+        kv = a.pairs
+        patch = {}
+        for p in kv:
+            if p.endswith("-"):
+                patch[p[:-1]] = None
+            else:
+                k, _, v = p.partition("=")
+                patch[k] = v
+        for n in names:
+            await self.client.patch(ri.plural, n, {"metadata": {field: patch}}, self.ns if ri.namespaced else None)
+            self.p(f"{ri.kind.lower()}/{n} {'labeled' if field == 'labels' else 'annotated'}")
+
+    async def cmd_label(self):
+        await self._meta_edit("labels")
+
+    async def cmd_annotate(self):
+        await self._meta_edit("annotations")
+
+    async def cmd_patch(self):
+        a = self.a
+        (ri, name), = split_targets(a.targets)
+        patch = json.loads(a.patch) if a.patch.strip().startswith(("{", "[")) else yaml.safe_load(a.patch)
+        await self.client.patch(ri.plural, name, patch, self.ns if ri.namespaced else None, a.type)
+        self.p(f"{ri.kind.lower()}/{name} patched")
+
+    async def cmd_scale(self):
+        a = self.a
+        for ri, name in split_targets(a.targets):
+            await self.client.patch(ri.plural, name, {"spec": {"replicas": a.replicas}}, self.ns)
+            self.p(f"{ri.kind.lower()}/{name} scaled")
+
+    async def _cordon(self, name, flag):
+        await self.client.patch("nodes", name, {"spec": {"unschedulable": flag or None}})
+        self.p(f"node/{name} {'cordoned' if flag else 'uncordoned'}")
+
+    async def cmd_cordon(self):
+        await self._cordon(self.a.node, True)
+
+    async def cmd_uncordon(self):
+        await self._cordon(self.a.node, False)
+
+    async def cmd_drain(self):
+        a = self.a
+        await self._cordon(a.node, True)
+        pods = (await self.client.list("pods", None, field_selector=f"spec.nodeName={a.node}"))["items"]
+        for p in pods:
+            ref = m.controller_of(p)
+            if ref and ref.get("kind") == "DaemonSet" and a.ignore_daemonsets:
+                continue
+            if not ref and not a.force:
+                raise SystemExit(f"error: pod {p['metadata']['name']} is not managed by a controller (use --force)")
+            try:
+                await self.client.evict(p["metadata"]["namespace"], p["metadata"]["name"], a.grace_period)
+                self.p(f"pod/{p['metadata']['name']} evicted")
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise
+        self.p(f"node/{a.node} drained")
+
+    async def cmd_taint(self):
+        a = self.a
+        node = await self.client.get("nodes", a.node)
+        taints = list((node.get("spec") or {}).get("taints") or [])
+        for t in a.taints:
+            if t.endswith("-"):
+                key = t[:-1].split(":")[0].split("=")[0]
+                taints = [x for x in taints if x["key"] != key]
+            else:
+                kv, _, eff = t.partition(":")
+                k, _, v = kv.partition("=")
+                taints = [x for x in taints if not (x["key"] == k and x["effect"] == eff)]
+                taints.append({"key": k, "value": v, "effect": eff} if v else {"key": k, "effect": eff})
+        await self.client.patch("nodes", a.node, {"spec": {"taints": taints or None}})
+        self.p(f"node/{a.node} tainted")
+
+    async def cmd_top(self):
+        a = self.a
+        nodes = (await self.client.list("nodes"))["items"]
+        pods = (await self.client.list("pods"))["items"]
+        if a.what in ("node", "nodes"):
+            rows = []
+            for n in nodes:
+                name = n["metadata"]["name"]
+                devs = ((n.get("status") or {}).get("extendedResources") or {}).get(core.AMD_GPU, {}).get("resources") or {}
+                used = sum(len(printers.pod_gpus(p)) for p in pods if (p.get("spec") or {}).get("nodeName") == name
+                           and not core.pod_is_terminal(p))
+                rows.append([name, len(devs), used, f"{(100 * used // len(devs)) if devs else 0}%",
+                             sum(1 for d in devs.values() if d.get("health") != "Healthy")])
+            self.p(printers.table(rows, ["NAME", "GPUS", "GPUS-ALLOCATED", "GPU%", "UNHEALTHY"]))
+        else:
+            rows = [[p["metadata"].get("namespace"), p["metadata"]["name"], (p.get("spec") or {}).get("nodeName") or "<none>",
+                     len(printers.pod_gpus(p)), ",".join(printers.pod_gpus(p)) or "<none>"]
+                    for p in pods if printers.pod_gpus(p)]
+            self.p(printers.table(rows, ["NAMESPACE", "NAME", "NODE", "GPUS", "DEVICES"]))
+
+    async def cmd_rollout(self):
+        a = self.a
+        (ri, name), = split_targets(a.targets)
+        if a.action == "status":
+            t = time.time()
+            while True:
+                d = await self.client.get(ri.plural, name, self.ns)
+                st, spec = d.get("status") or {}, d.get("spec") or {}
+                want = spec.get("replicas", 1)
+                if st.get("updatedReplicas") == want and st.get("availableReplicas") == want and st.get("replicas") == want:
+                    self.p(f'deployment "{name}" successfully rolled out')
+                    return
+                if not a.watch or time.time() - t > a.timeout:
+                    self.p(f"Waiting for rollout to finish: {st.get('updatedReplicas', 0)} of {want} updated replicas are available...")
+                    if not a.watch:
+                        return
+                    raise SystemExit(1)
+                await asyncio.sleep(0.2)
+        elif a.action == "history":
+            uid = (await self.client.get(ri.plural, name, self.ns))["metadata"]["uid"]
+            rss = [r for r in (await self.client.list("replicasets", self.ns))["items"] if (m.controller_of(r) or {}).get("uid") == uid]
+            rows = sorted([[int((r["metadata"].get("annotations") or {}).get("deployment.kubernetes.io/revision", 0)), "<none>"] for r in rss])
+            self.p(printers.table(rows, ["REVISION", "CHANGE-CAUSE"]))
+        elif a.action == "undo":
+            await self.client.patch(ri.plural, name, {"spec": {"rollbackTo": {"revision": a.to_revision}}}, self.ns)
+            self.p(f"deployment.apps/{name} rolled back")
+
+    async def cmd_run(self):
+        a = self.a
+        c = {"name": a.name, "image": a.image}
+        if a.command:
+            c["command"] = a.command
+        if a.gpus:
+            c["resources"] = {"limits": {core.AMD_GPU: str(a.gpus)}}
+        pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": a.name, "namespace": self.ns, "labels": {"run": a.name}},
+               "spec": {"containers": [c], "restartPolicy": a.restart}}
+        await self.client.create("pods", pod, self.ns)
+        self.p(f"pod/{a.name} created")
+
+    async def cmd_expose(self):
+        a = self.a
+        (ri, name), = split_targets(a.targets)
+        obj = await self.client.get(ri.plural, name, self.ns)
+        sel = (obj["metadata"].get("labels") if ri.kind == "Pod" else
+               ((obj.get("spec") or {}).get("selector") or {}).get("matchLabels")) or {}
+        svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": a.name or name, "namespace": self.ns},
+               "spec": {"selector": sel, "ports": [{"port": a.port, "targetPort": a.target_port or a.port}]}}
+        await self.client.create("services", svc, self.ns)
+        self.p(f"service/{a.name or name} exposed")
+
+    async def cmd_version(self):
+        st, body = await self.client.raw("GET", "/version")
+        from ..apiserver.server import VERSION
+        self.p(f"Client Version: {VERSION['gitVersion']}")
+        if st == 200:
+            self.p(f"Server Version: {json.loads(body)['gitVersion']}")
+
+    async def cmd_api_versions(self):
+        _, body = await self.client.raw("GET", "/apis")
+        self.p("v1")
+        for g in json.loads(body)["groups"]:
+            for v in g["versions"]:
+                self.p(v["groupVersion"])
+
+    async def cmd_api_resources(self):
+        rows = [[r.plural, ",".join(r.short), r.group_version, str(r.namespaced).lower(), r.kind] for r in m.RESOURCES]
+        self.p(printers.table(rows, ["NAME", "SHORTNAMES", "APIVERSION", "NAMESPACED", "KIND"]))
+
+    async def cmd_cluster_info(self):
+        self.p(f"Kubernetes master is running at {self.server}")
+
+    async def cmd_explain(self):
+        ri = m.lookup(self.a.resource.split(".")[0])
+        if ri is None:
+            raise SystemExit(f"error: couldn't find resource for {self.a.resource}")
+        self.p(f"KIND:     {ri.kind}\nVERSION:  {ri.group_version}\n")
+        if ri.kind == "Pod":
+            self.p("FIELDS (MI355X device model, fork ResourceV2):\n"
+                   "   spec.extendedResources[]   <[]PodExtendedResource>  pod-level device requests\n"
+                   "      name                    <string>  unique name referenced by containers\n"
+                   "      resources.limits        <map>     exactly one entry, e.g. amd.com/gpu: 4\n"
+                   "      affinity.required[]     <[]ResourceSelector> key/operator(In,NotIn,Exists,DoesNotExist,Gt,Lt)/values\n"
+                   "                              keys: amd.com/arch amd.com/product amd.com/memory amd.com/hbm\n"
+                   "                                    amd.com/xgmi-hive amd.com/numa amd.com/partition amd.com/ecc\n"
+                   "      assigned[]              <[]string> device IDs (written by pods/binding)\n"
+                   "   spec.containers[].extendedResourceRequests <[]string> names of extendedResources")
+
+    async def cmd_wait(self):
+        a = self.a
+        (ri, name), = split_targets(a.targets)
+        cond = a.for_.split("=", 1)[1] if "=" in a.for_ else a.for_
+        t = time.time()
+        while time.time() - t < a.timeout:
+            try:
+                o = await self.client.get(ri.plural, name, self.ns if ri.namespaced else None)
+            except APIStatusError as e:
+                if a.for_ == "delete" and is_not_found(e):
+                    self.p(f"{ri.kind.lower()}/{name} deleted")
+                    return
+                raise
+            if a.for_.startswith("condition="):
+                c = core.get_condition(o.get("status"), cond)
+                if c and c.get("status") == "True":
+                    self.p(f"{ri.kind.lower()}/{name} condition met")
+                    return
+            await asyncio.sleep(0.1)
+        raise SystemExit(f"error: timed out waiting for the condition on {ri.plural}/{name}")
+
+    async def cmd_auth(self):
+        a = self.a
+        ri = m.lookup(a.resource)
+        st, body = await self.client.raw("GET", f"{'/api/v1' if not ri.group else f'/apis/{ri.group}/{ri.version}'}"
+                                         f"{'/namespaces/' + self.ns if ri.namespaced else ''}/{ri.plural}?limit=1")
+        self.p("yes" if st == 200 else "no")
+
+    async def cmd_unsupported(self):
+        raise SystemExit(f"error: '{self.a.command}' needs a streaming runtime session, which the process/stub runtimes do not provide")
+
+
+def cmd_config(a):
+    cfg, path = load_kubeconfig(a.kubeconfig)
+    if a.action == "view":
+        print(yaml.safe_dump(cfg, sort_keys=False).rstrip())
+    elif a.action == "current-context":
+        print(cfg.get("current-context", ""))
+    elif a.action == "get-contexts":
+        rows = [["*" if c["name"] == cfg.get("current-context") else "", c["name"], c["context"].get("cluster", ""),
+                 c["context"].get("user", ""), c["context"].get("namespace", "")] for c in cfg.get("contexts") or ()]
+        print(printers.table(rows, ["CURRENT", "NAME", "CLUSTER", "AUTHINFO", "NAMESPACE"]))
+    elif a.action == "use-context":
+        cfg["current-context"] = a.name
+        save_kubeconfig(cfg, path)
+        print(f'Switched to context "{a.name}".')
+    elif a.action == "set-cluster":
+        cl = [c for c in cfg.setdefault("clusters", []) if c["name"] != a.name]
+        cl.append({"name": a.name, "cluster": {"server": a.server_url}})
+        cfg["clusters"] = cl
+        save_kubeconfig(cfg, path)
+        print(f'Cluster "{a.name}" set.')
+    elif a.action == "set-credentials":
+        us = [u for u in cfg.setdefault("users", []) if u["name"] != a.name]
+        us.append({"name": a.name, "user": {"token": a.user_token}})
+        cfg["users"] = us
+        save_kubeconfig(cfg, path)
+        print(f'User "{a.name}" set.')
+    elif a.action == "set-context":
+        cs = [c for c in cfg.setdefault("contexts", []) if c["name"] != a.name]
+        cs.append({"name": a.name, "context": {"cluster": a.cluster, "user": a.user, "namespace": a.ctx_namespace or "default"}})
+        cfg["contexts"] = cs
+        save_kubeconfig(cfg, path)
+        print(f'Context "{a.name}" modified.')
+
+
+def build_parser():
+    ap = argparse.ArgumentParser("kubectl")
+    ap.add_argument("-s", "--server")
+    ap.add_argument("--token")
+    ap.add_argument("--kubeconfig")
+    ap.add_argument("--context")
+    ap.add_argument("-n", "--namespace")
+    sub = ap.add_subparsers(dest="command", required=True)
+
+    def add(name, **kw):
+        return sub.add_parser(name, **kw)
+
+    g = add("get")
+    g.add_argument("targets", nargs="*")
+    g.add_argument("-o", "--output", default="")
+    g.add_argument("-l", "--selector")
+    g.add_argument("--field-selector")
+    g.add_argument("-A", "--all-namespaces", action="store_true")
+    g.add_argument("-w", "--watch", action="store_true")
+    g.add_argument("-f", "--filename", action="append")
+    d = add("describe")
+    d.add_argument("targets", nargs="+")
+    d.add_argument("-l", "--selector")
+    for name in ("create", "apply", "replace"):
+        c = add(name)
+        c.add_argument("-f", "--filename", action="append", required=True)
+    de = add("delete")
+    de.add_argument("targets", nargs="*")
+    de.add_argument("-f", "--filename", action="append")
+    de.add_argument("-l", "--selector")
+    de.add_argument("--all", action="store_true")
+    de.add_argument("--grace-period", type=int, default=None)
+    de.add_argument("--cascade", type=lambda s: s.lower() != "false", default=True)
+    de.add_argument("--ignore-not-found", action="store_true")
+    lg = add("logs")
+    lg.add_argument("pod")
+    lg.add_argument("-c", "--container")
+    lg.add_argument("--tail", type=int)
+    for name in ("label", "annotate"):
+        la = add(name)
+        la.add_argument("resource")
+        la.add_argument("name", nargs="?")
+        la.add_argument("pairs", nargs="+")
+    pa = add("patch")
+    pa.add_argument("targets", nargs="+")
+    pa.add_argument("-p", "--patch", required=True)
+    pa.add_argument("--type", default="strategic", choices=["strategic", "merge", "json"])
+    sc = add("scale")
+    sc.add_argument("targets", nargs="+")
+    sc.add_argument("--replicas", type=int, required=True)
+    for name in ("cordon", "uncordon"):
+        add(name).add_argument("node")
+    dr = add("drain")
+    dr.add_argument("node")
+    dr.add_argument("--ignore-daemonsets", action="store_true")
+    dr.add_argument("--force", action="store_true")
+    dr.add_argument("--grace-period", type=int, default=None)
+    ta = add("taint")
+    ta.add_argument("nodes_kw", choices=["nodes", "node", "no"])
+    ta.add_argument("node")
+    ta.add_argument("taints", nargs="+")
+    tp = add("top")
+    tp.add_argument("what", choices=["node", "nodes", "pod", "pods"])
+    ro = add("rollout")
+    ro.add_argument("action", choices=["status", "history", "undo"])
+    ro.add_argument("targets", nargs="+")
+    ro.add_argument("--to-revision", type=int, default=0)
+    ro.add_argument("-w", "--watch", type=lambda s: s.lower() != "false", default=True)
+    ro.add_argument("--timeout", type=float, default=300)
+    rn = add("run")
+    rn.add_argument("name")
+    rn.add_argument("--image", required=True)
+    rn.add_argument("--gpus", type=int, default=0, help="request N amd.com/gpu")
+    rn.add_argument("--restart", default="Always")
+    rn.add_argument("command", nargs="*")
+    ex = add("expose")
+    ex.add_argument("targets", nargs="+")
+    ex.add_argument("--port", type=int, required=True)
+    ex.add_argument("--target-port", type=int)
+    ex.add_argument("--name")
+    add("version")
+    add("api-versions")
+    add("api-resources")
+    add("cluster-info")
+    e = add("explain")
+    e.add_argument("resource")
+    w = add("wait")
+    w.add_argument("targets", nargs="+")
+    w.add_argument("--for", dest="for_", required=True)
+    w.add_argument("--timeout", type=float, default=30)
+    au = add("auth")
+    au.add_argument("can_i", choices=["can-i"])
+    au.add_argument("verb")
+    au.add_argument("resource")
+    for name in ("exec", "attach", "port-forward", "cp", "edit", "proxy"):
+        add(name).add_argument("rest", nargs="*")
+    cf = add("config")
+    cf.add_argument("action", choices=["view", "current-context", "get-contexts", "use-context", "set-cluster",
+                                       "set-context", "set-credentials"])
+    cf.add_argument("name", nargs="?")
+    cf.add_argument("--server", dest="server_url")
+    cf.add_argument("--cluster")
+    cf.add_argument("--user")
+    cf.add_argument("--token", dest="user_token")
+    cf.add_argument("--namespace", dest="ctx_namespace")
+    return ap
+
+
+def main(argv=None, out=sys.stdout):
+    ap = build_parser()
+    a = ap.parse_args(argv)
+    if a.command == "config":
+        cmd_config(a)
+        return 0
+    k = Kubectl(a, out)
+    name = "cmd_" + a.command.replace("-", "_")
+    if a.command in ("exec", "attach", "port-forward", "cp", "edit", "proxy"):
+        name = "cmd_unsupported"
+
+    async def go():
+        try:
+            await getattr(k, name)()
+        finally:
+            await k.client.close()
+    try:
+        asyncio.run(go())
+    except APIStatusError as e:
+        print(f"Error from server ({e.reason}): {e.status.get('message', '')}", file=sys.stderr)
+        return 1
+    except (ConnectionError, OSError) as e:
+        print(f"The connection to the server {k.server} was refused - did you specify the right host or port? ({e})", file=sys.stderr)
+        return 1
+    return 0

@@ -1,0 +1,249 @@
+"""kubectl output printers: human tables, describe, json/yaml/name/jsonpath/custom-columns.
+
+Parity: `pkg/printers` (table handlers per kind, `-o wide`, describe). Fork gap closed
+(SURVEY §7.4 item 5): pods show their assigned GPUs and nodes their device inventory with
+health and MI355X attributes.
+"""
+from __future__ import annotations
+
+import json
+import re
+import time
+
+import yaml
+
+from ..api import core
+from ..api.meta import parse_rfc3339
+
+
+def age(ts):
+    t = parse_rfc3339(ts)
+    if t is None:
+        return "<unknown>"
+    d = max(0, int(time.time() - t))
+    if d < 120:
+        return f"{d}s"
+    if d < 7200:
+        return f"{d // 60}m"
+    if d < 172800:
+        return f"{d // 3600}h"
+    return f"{d // 86400}d"
+
+
+def pod_status(p):
+    st = p.get("status") or {}
+    if p["metadata"].get("deletionTimestamp"):
+        return "Terminating"
+    reason = st.get("reason")
+    if reason:
+        return reason
+    for cs in st.get("containerStatuses") or ():
+        s = cs.get("state") or {}
+        if "waiting" in s and s["waiting"].get("reason"):
+            return s["waiting"]["reason"]
+        if "terminated" in s and st.get("phase") not in ("Succeeded",):
+            return s["terminated"].get("reason", "Terminated")
+    return st.get("phase", "Unknown")
+
+
+def pod_gpus(p):
+    return [i for per in (p.get("spec") or {}).get("extendedResources") or () for i in per.get("assigned") or ()]
+
+
+def table(rows, headers):
+    rows = [[str(c) for c in r] for r in rows]
+    widths = [max([len(h)] + [len(r[i]) for r in rows]) for i, h in enumerate(headers)]
+    out = ["   ".join(h.ljust(w) for h, w in zip(headers, widths)).rstrip()]
+    for r in rows:
+        out.append("   ".join(c.ljust(w) for c, w in zip(r, widths)).rstrip())
+    return "\n".join(out)
+
+
+def rows_for(kind, items, wide=False, all_ns=False):
+    if kind == "Pod":
+        h = ["NAME", "READY", "STATUS", "RESTARTS", "AGE"]
+        if wide:
+            h += ["IP", "NODE", "GPUS"]
+        rows = []
+        for p in items:
+            cs = (p.get("status") or {}).get("containerStatuses") or []
+            n = len((p.get("spec") or {}).get("containers") or [])
+            r = [p["metadata"]["name"], f"{sum(1 for c in cs if c.get('ready'))}/{n}", pod_status(p),
+                 sum(c.get("restartCount", 0) for c in cs), age(p["metadata"].get("creationTimestamp"))]
+            if wide:
+                g = pod_gpus(p)
+                r += [(p.get("status") or {}).get("podIP", "<none>"), (p.get("spec") or {}).get("nodeName") or "<none>",
+                      ",".join(x[-8:] for x in g) or "<none>"]
+            rows.append(r)
+    elif kind == "Node":
+        h = ["NAME", "STATUS", "ROLES", "AGE", "VERSION", "GPU"]
+        if wide:
+            h += ["INTERNAL-IP", "GPU-PRODUCT", "ARCH", "HBM"]
+        rows = []
+        for n in items:
+            ready = core.get_condition(n.get("status"), "Ready")
+            s = "Ready" if ready and ready.get("status") == "True" else "NotReady"
+            if (n.get("spec") or {}).get("unschedulable"):
+                s += ",SchedulingDisabled"
+            cap = (n.get("status") or {}).get("capacity") or {}
+            devs = ((n.get("status") or {}).get("extendedResources") or {}).get(core.AMD_GPU, {}).get("resources") or {}
+            r = [n["metadata"]["name"], s, "<none>", age(n["metadata"].get("creationTimestamp")),
+                 ((n.get("status") or {}).get("nodeInfo") or {}).get("kubeletVersion", ""),
+                 f"{cap.get(core.AMD_GPU, '0')}/{len(devs)}"]
+            if wide:
+                attrs = next(iter(devs.values()), {}).get("attributes", {}) if devs else {}
+                ip = next((a["address"] for a in (n.get("status") or {}).get("addresses") or () if a.get("type") == "InternalIP"), "")
+                r += [ip, attrs.get(core.ATTR_PRODUCT, "<none>"), attrs.get(core.ATTR_ARCH, "<none>"), attrs.get(core.ATTR_HBM, "<none>")]
+            rows.append(r)
+    elif kind in ("ReplicaSet", "ReplicationController"):
+        h = ["NAME", "DESIRED", "CURRENT", "READY", "AGE"]
+        rows = [[o["metadata"]["name"], (o.get("spec") or {}).get("replicas", 1), (o.get("status") or {}).get("replicas", 0),
+                 (o.get("status") or {}).get("readyReplicas", 0), age(o["metadata"].get("creationTimestamp"))] for o in items]
+    elif kind == "Deployment":
+        h = ["NAME", "DESIRED", "CURRENT", "UP-TO-DATE", "AVAILABLE", "AGE"]
+        rows = [[o["metadata"]["name"], (o.get("spec") or {}).get("replicas", 1), (o.get("status") or {}).get("replicas", 0),
+                 (o.get("status") or {}).get("updatedReplicas", 0), (o.get("status") or {}).get("availableReplicas", 0),
+                 age(o["metadata"].get("creationTimestamp"))] for o in items]
+    elif kind == "Job":
+        h = ["NAME", "DESIRED", "SUCCESSFUL", "AGE"]
+        rows = [[o["metadata"]["name"], (o.get("spec") or {}).get("completions", 1), (o.get("status") or {}).get("succeeded", 0),
+                 age(o["metadata"].get("creationTimestamp"))] for o in items]
+    elif kind == "Event":
+        h = ["LAST SEEN", "TYPE", "REASON", "OBJECT", "MESSAGE"]
+        rows = [[age(o.get("lastTimestamp")), o.get("type", ""), o.get("reason", ""),
+                 f"{(o.get('involvedObject') or {}).get('kind', '').lower()}/{(o.get('involvedObject') or {}).get('name', '')}",
+                 o.get("message", "")] for o in items]
+    elif kind == "Namespace":
+        h = ["NAME", "STATUS", "AGE"]
+        rows = [[o["metadata"]["name"], (o.get("status") or {}).get("phase", ""), age(o["metadata"].get("creationTimestamp"))] for o in items]
+    else:
+        h = ["NAME", "AGE"]
+        rows = [[o["metadata"]["name"], age(o["metadata"].get("creationTimestamp"))] for o in items]
+    if all_ns and kind != "Node":
+        h = ["NAMESPACE"] + h
+        rows = [[o["metadata"].get("namespace", "")] + r for o, r in zip(items, rows)]
+    return rows, h
+
+
+def jsonpath(obj, expr):
+    """A useful subset of kubectl jsonpath: {.a.b[0].c}, {.items[*].metadata.name}, literal text."""
+    def ev(path, cur):
+        toks = re.findall(r"\.([^.\[\]]+)|\[(\*|\d+)\]", path)
+        vals = [cur]
+        for name, idx in toks:
+            nxt = []
+            for v in vals:
+                if name:
+                    if isinstance(v, dict) and name in v:
+                        nxt.append(v[name])
+                elif idx == "*":
+                    if isinstance(v, list):
+                        nxt.extend(v)
+                else:
+                    if isinstance(v, list) and int(idx) < len(v):
+                        nxt.append(v[int(idx)])
+            vals = nxt
+        return vals
+
+    out = []
+    for lit, path in re.findall(r"([^{]*)(?:\{([^}]*)\})?", expr):
+        out.append(lit)
+        if path:
+            vals = ev(path, obj)
+            out.append(" ".join(json.dumps(v) if isinstance(v, (dict, list)) else str(v) for v in vals))
+    return "".join(out)
+
+
+def render(objs, output, kind=None, wide=False, all_ns=False, list_obj=None):
+    if output == "json":
+        return json.dumps(list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else {"kind": "List", "apiVersion": "v1", "items": objs}), indent=4)
+    if output == "yaml":
+        return yaml.safe_dump(list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else {"kind": "List", "apiVersion": "v1", "items": objs}), sort_keys=False).rstrip()
+    if output == "name":
+        return "\n".join(f"{(o.get('kind') or kind or '').lower()}/{o['metadata']['name']}" for o in objs)
+    if output and output.startswith("jsonpath="):
+        target = list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else {"items": objs})
+        return jsonpath(target, output[len("jsonpath="):])
+    if output and output.startswith("custom-columns="):
+        cols = [c.split(":", 1) for c in output[len("custom-columns="):].split(",")]
+        rows = [[jsonpath(o, "{" + p + "}") or "<none>" for _, p in cols] for o in objs]
+        return table(rows, [h for h, _ in cols])
+    if not objs:
+        return "No resources found."
+    rows, h = rows_for(kind or objs[0].get("kind"), objs, wide or output == "wide", all_ns)
+    return table(rows, h)
+
+
+def describe(obj, events=()):
+    kind = obj.get("kind")
+    md = obj["metadata"]
+    lines = [f"Name:         {md['name']}"]
+    if md.get("namespace"):
+        lines.append(f"Namespace:    {md['namespace']}")
+    lines.append(f"Labels:       {', '.join(f'{k}={v}' for k, v in (md.get('labels') or {}).items()) or '<none>'}")
+    lines.append(f"Annotations:  {', '.join(f'{k}={v}' for k, v in (md.get('annotations') or {}).items()) or '<none>'}")
+    lines.append(f"CreationTimestamp: {md.get('creationTimestamp')}")
+    if kind == "Pod":
+        spec, st = obj.get("spec") or {}, obj.get("status") or {}
+        lines += [f"Node:         {spec.get('nodeName') or '<none>'}", f"Status:       {pod_status(obj)}",
+                  f"IP:           {st.get('podIP', '')}", f"QoS Class:    {st.get('qosClass', '')}"]
+        ers = spec.get("extendedResources") or []
+        if ers:
+            lines.append("Extended Resources:")
+            for per in ers:
+                lim = (per.get("resources") or {}).get("limits") or {}
+                lines.append(f"  {per.get('name')}:")
+                lines.append(f"    Request:   {', '.join(f'{k}={v}' for k, v in lim.items())}")
+                req = (per.get("affinity") or {}).get("required") or []
+                if req:
+                    lines.append("    Affinity:  " + "; ".join(f"{r.get('key')} {r.get('operator')} {','.join(r.get('values') or [])}" for r in req))
+                lines.append(f"    Assigned:  {', '.join(per.get('assigned') or []) or '<pending>'}")
+        lines.append("Containers:")
+        cstat = {c["name"]: c for c in st.get("containerStatuses") or ()}
+        for c in spec.get("containers") or ():
+            lines.append(f"  {c['name']}:")
+            lines.append(f"    Image:   {c.get('image')}")
+            s = cstat.get(c["name"], {})
+            if s:
+                state = next(iter((s.get("state") or {}).keys()), "unknown")
+                lines.append(f"    State:   {state.capitalize()}")
+                lines.append(f"    Ready:   {s.get('ready')}")
+                lines.append(f"    Restart Count: {s.get('restartCount', 0)}")
+            if c.get("extendedResourceRequests"):
+                lines.append(f"    Extended Resource Requests: {', '.join(c['extendedResourceRequests'])}")
+        lines.append("Conditions:")
+        for cd in st.get("conditions") or ():
+            lines.append(f"  {cd.get('type'):<16} {cd.get('status')}")
+    elif kind == "Node":
+        st = obj.get("status") or {}
+        lines.append("Conditions:")
+        for cd in st.get("conditions") or ():
+            lines.append(f"  {cd.get('type'):<16} {cd.get('status'):<8} {cd.get('reason', '')}")
+        lines.append("Capacity:")
+        for k, v in (st.get("capacity") or {}).items():
+            lines.append(f"  {k}: {v}")
+        lines.append("Allocatable:")
+        for k, v in (st.get("allocatable") or {}).items():
+            lines.append(f"  {k}: {v}")
+        for rn, dom in (st.get("extendedResources") or {}).items():
+            lines.append(f"Extended Resources ({rn}):")
+            for did, d in sorted(((dom or {}).get("resources") or {}).items(), key=lambda kv: kv[1].get("attributes", {}).get(core.ATTR_INDEX, "")):
+                a = d.get("attributes") or {}
+                lines.append(f"  {did}  {d.get('health')}  {a.get(core.ATTR_PRODUCT, '')} {a.get(core.ATTR_ARCH, '')} "
+                             f"hbm={a.get(core.ATTR_HBM, '')} hive={a.get(core.ATTR_HIVE, '')} numa={a.get(core.ATTR_NUMA, '')} "
+                             f"render=renderD{a.get(core.ATTR_RENDER_MINOR, '?')}")
+        taints = (obj.get("spec") or {}).get("taints") or []
+        lines.append(f"Taints:       {', '.join(t['key'] + ':' + t['effect'] for t in taints) or '<none>'}")
+        lines.append(f"Unschedulable: {bool((obj.get('spec') or {}).get('unschedulable'))}")
+    else:
+        for k in ("spec", "status"):
+            if k in obj:
+                lines.append(f"{k.capitalize()}:")
+                lines += ["  " + ln for ln in yaml.safe_dump(obj[k], sort_keys=False).rstrip().splitlines()]
+    if events:
+        lines.append("Events:")
+        rows, h = rows_for("Event", list(events))
+        lines += ["  " + ln for ln in table(rows, h).splitlines()]
+    else:
+        lines.append("Events:       <none>")
+    return "\n".join(lines)
