@@ -74,7 +74,8 @@ FIELD_FUNCS = {"pods": pod_fields, "nodes": node_fields}
 
 
 class Watcher:
-    __slots__ = ("writer", "namespace", "label_sel", "field_sel", "closed", "index_value", "cache", "bookmarks")
+    __slots__ = ("writer", "namespace", "label_sel", "field_sel", "closed", "index_value", "cache", "bookmarks",
+                 "_pending", "_loop")
 
     def __init__(self, cache, writer, namespace, label_sel, field_sel, index_value):
         self.cache = cache
@@ -85,6 +86,8 @@ class Watcher:
         self.index_value = index_value
         self.closed = False
         self.bookmarks = False
+        self._pending = None   # events coalesced until the end of this loop iteration
+        self._loop = None
 
     def matches(self, e: Entry) -> bool:
         if self.namespace and e.fields.get("metadata.namespace") != self.namespace:
@@ -108,7 +111,21 @@ class Watcher:
             log.warning("terminating slow watcher on %s", self.cache.resource)
             self.stop()
             return
-        w.write(data)
+        # coalesce: all events dispatched in one event-loop iteration go out as ONE chunk /
+        # one send() — under load this removes most per-event syscalls
+        if self._pending is None:
+            self._pending = [data]
+            if self._loop is None:
+                import asyncio
+                self._loop = asyncio.get_event_loop()
+            self._loop.call_soon(self._flush)
+        else:
+            self._pending.append(data)
+
+    def _flush(self):
+        p, self._pending = self._pending, None
+        if p and not self.closed:
+            self.writer.write(p[0] if len(p) == 1 else b"".join(p))
 
     def stop(self):
         if not self.closed:

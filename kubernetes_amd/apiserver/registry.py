@@ -96,6 +96,17 @@ class Strategy:
     def validate_update(self, new, old):
         return self.validate(new)
 
+    _PHASES = {"Pending", "Running", "Succeeded", "Failed", "Unknown", "Active", "Terminating", ""}
+
+    def validate_status(self, obj):
+        errs = validation.validate_object_meta(obj, self.ri.namespaced)
+        st = obj.get("status")
+        if st is not None and not isinstance(st, dict):
+            errs.append(validation.invalid("status", "must be an object"))
+        elif st and st.get("phase", "") not in self._PHASES:
+            errs.append(validation.not_supported("status.phase", st.get("phase")))
+        return errs
+
     def graceful_seconds(self, obj, opts) -> int:
         """0 = delete immediately."""
         return 0

@@ -253,7 +253,9 @@ class APIServer:
                     nm["generation"] = om["generation"] + 1
         a = adm.Attributes(adm.UPDATE, ri.plural, subresource, namespace, name, obj, old, user, ri.kind)
         self._admit(a)
-        errs = strat.validate_update(obj, old) if subresource == "" else strat.validate(obj)
+        # a status update keeps the (already validated) spec, so only metadata + status are checked
+        # (reference: ValidatePodStatusUpdate / ValidateNodeUpdate on the status subresource)
+        errs = strat.validate_update(obj, old) if subresource == "" else strat.validate_status(obj)
         if errs:
             raise invalid(ri, name, errs)
         self._validate_admission(a)
