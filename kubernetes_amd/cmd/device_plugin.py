@@ -1,0 +1,47 @@
+"""amd.com/gpu device plugin daemon (+ optional amd-smi Prometheus exporter).
+
+    python -m kubernetes_amd.cmd.device_plugin --plugins-dir /var/lib/kubelet/device-plugin/plugins
+"""
+from __future__ import annotations
+
+import argparse
+
+from ..deviceplugin import api
+from ..deviceplugin.amdgpu import AMDGPUPlugin
+from ..native import amdsmi
+from ._common import run_until_signal, setup_logging
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("amdgpu-device-plugin")
+    ap.add_argument("--plugins-dir", default=api.DEVICE_PLUGINS_PATH)
+    ap.add_argument("--socket-name", default="amdgpu.sock")
+    ap.add_argument("--fixture", default=None, help="fake AMD SMI fixture (JSON) instead of the real GPUs")
+    ap.add_argument("--fake-gpus", type=int, default=0, help="generate an N x MI355X fixture")
+    ap.add_argument("--health-interval", type=float, default=5.0)
+    ap.add_argument("--rocm-mount", default=None, help="bind the ROCm userspace read-only into GPU containers")
+    ap.add_argument("--exporter-port", type=int, default=None)
+    ap.add_argument("--node-name", default="")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    setup_logging(a.v)
+
+    async def start():
+        fixture = a.fixture or (amdsmi.fixture_file(a.fake_gpus) if a.fake_gpus else None)
+        smi = amdsmi.SMI(fixture=fixture)
+        p = AMDGPUPlugin(a.plugins_dir, smi=smi, socket_name=a.socket_name, health_interval=a.health_interval,
+                         rocm_mount=a.rocm_mount)
+        await p.start()
+        print(f"amd.com/gpu plugin serving {len(p.gpus)} GPU(s) on {p.socket_path}", flush=True)
+        if a.exporter_port is not None:
+            from ..monitoring.exporter import AMDSMIExporter
+            ex = AMDSMIExporter(smi, a.node_name, health_fn=lambda i: p._health.get(i))
+            port = await ex.start("0.0.0.0", a.exporter_port)
+            print(f"amd-smi exporter on :{port}", flush=True)
+        return p
+
+    run_until_signal(start)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,33 @@
+"""kubemark hollow-node entry point (reference: cmd/kubemark/hollow-node.go:46-160): N hollow
+kubelets in one process, each with a fake 8 x MI355X amd.com/gpu plugin."""
+from __future__ import annotations
+
+import argparse
+
+from ..kubemark.hollow import HollowCluster
+from ._common import run_until_signal, setup_logging
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("hollow-node")
+    ap.add_argument("--master", required=True)
+    ap.add_argument("--count", type=int, default=10)
+    ap.add_argument("--name-prefix", default="hollow")
+    ap.add_argument("--gpus-per-node", type=int, default=8)
+    ap.add_argument("--hives", type=int, default=1)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    setup_logging(a.v)
+
+    async def start():
+        h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives)
+        await h.start()
+        await h.wait_registered()
+        print(f"{a.count} hollow nodes registered ({a.gpus_per_node} GPUs each)", flush=True)
+        return h
+
+    run_until_signal(start)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,52 @@
+"""kubelet entry point (reference: cmd/kubelet/app/server.go:98-777)."""
+from __future__ import annotations
+
+import argparse
+import os
+
+from ..client.rest import Client
+from ..deviceplugin import api
+from ..kubelet.devicemanager.manager import ManagerImpl, ManagerStub
+from ..kubelet.kubelet import Kubelet
+from ..kubelet.runtime.process import ProcessRuntime
+from ..kubelet.runtime.stub import StubRuntime
+from ..utils.features import DefaultFeatureGate
+from ._common import run_until_signal, setup_logging
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("kubelet")
+    ap.add_argument("--api-servers", "--master", dest="master", required=True)
+    ap.add_argument("--hostname-override", default=os.uname().nodename)
+    ap.add_argument("--root-dir", default="/var/lib/kubelet")
+    ap.add_argument("--device-plugins-dir", default=None)
+    ap.add_argument("--container-runtime", default="process", choices=["process", "stub"])
+    ap.add_argument("--port", type=int, default=10250)
+    ap.add_argument("--address", default="127.0.0.1")
+    ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
+    ap.add_argument("--max-pods", type=int, default=110)
+    ap.add_argument("--node-labels", default="")
+    ap.add_argument("--feature-gates", default="")
+    ap.add_argument("--token", default=None)
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    setup_logging(a.v)
+    DefaultFeatureGate.set(a.feature_gates)
+
+    async def start():
+        client = Client(a.master, token=a.token, max_conns=32)
+        pdir = a.device_plugins_dir or os.path.join(a.root_dir, "device-plugin", "plugins")
+        dm = ManagerImpl(pdir) if DefaultFeatureGate("DevicePlugins") else ManagerStub()
+        rt = ProcessRuntime(os.path.join(a.root_dir, "runtime")) if a.container_runtime == "process" else StubRuntime()
+        labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
+        kl = Kubelet(client, a.hostname_override, rt, dm, pods=a.max_pods, labels=labels,
+                     node_status_update_frequency=a.node_status_update_frequency, http_port=a.port, address=a.address)
+        await kl.run()
+        print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port})", flush=True)
+        return kl
+
+    run_until_signal(start)
+
+
+if __name__ == "__main__":
+    main()

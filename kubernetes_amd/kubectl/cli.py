@@ -391,8 +391,8 @@ class Kubectl:
     async def cmd_run(self):
         a = self.a
         c = {"name": a.name, "image": a.image}
-        if a.command:
-            c["command"] = a.command
+        if a.run_command:
+            c["command"] = a.run_command
         if a.gpus:
             c["resources"] = {"limits": {core.AMD_GPU: str(a.gpus)}}
         pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": a.name, "namespace": self.ns, "labels": {"run": a.name}},
@@ -588,7 +588,7 @@ def build_parser():
     rn.add_argument("--image", required=True)
     rn.add_argument("--gpus", type=int, default=0, help="request N amd.com/gpu")
     rn.add_argument("--restart", default="Always")
-    rn.add_argument("command", nargs="*")
+    rn.add_argument("run_command", nargs="*", metavar="command")
     ex = add("expose")
     ex.add_argument("targets", nargs="+")
     ex.add_argument("--port", type=int, required=True)
