@@ -467,6 +467,13 @@ class APIServer:
                     code = 401
                     return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))
             req.user = user
+            if req.body and req.headers.get("content-type", "").startswith(codec.PROTOBUF):
+                # protobuf request bodies (`application/vnd.kubernetes.protobuf`, k8s\0 envelope)
+                from ..api import protobuf as pb
+                try:
+                    req.body = codec.dumpb(pb.decode_object(req.body))
+                except pb.ProtobufError as e:
+                    raise APIError(415, "UnsupportedMediaType", str(e))
             parsed = self._parse_path(p)
             if parsed is None:
                 code = 404
@@ -514,6 +521,11 @@ class APIServer:
                     else:
                         self.inflight -= 1
             code = getattr(resp, "status", 200)
+            if codec.PROTOBUF in req.headers.get("accept", "") and isinstance(resp, Response) and resp.body[:1] == b"{":
+                from ..api import protobuf as pb
+                obj = codec.loads(resp.body)
+                if pb.supported(obj.get("kind", "")):
+                    resp = Response(resp.status, pb.encode_object(obj), codec.PROTOBUF)
             return resp
         except APIError as e:
             code = e.code
