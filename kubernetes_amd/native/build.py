@@ -35,6 +35,8 @@ def targets():
                      cxx + ["-shared", f"-I{ROCM}/include", _s("amdsmi_shim", "kamd_smi.cc"), "-ldl"]),
         "kamd_store": ([_s("store", "mvcc_store.cc")], os.path.join(LIB_DIR, "libkamd_store.so"),
                        cxx + ["-O3", "-shared", _s("store", "mvcc_store.cc")]),
+        "kamd_etcd": ([_s("store", "mvcc_store.cc")], os.path.join(BIN_DIR, "kamd-etcd"),
+                      cxx + ["-O3", "-DKAMD_STORE_SERVER", _s("store", "mvcc_store.cc")]),
         "kamd_oci": ([_s("oci", "oci_devices.cc")], os.path.join(LIB_DIR, "libkamd_oci.so"),
                      cxx + ["-shared", _s("oci", "oci_devices.cc")]),
         "pause": ([_s("pause", "pause.cc")], os.path.join(BIN_DIR, "pause"),

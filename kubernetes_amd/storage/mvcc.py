@@ -39,6 +39,13 @@ class Event:
         self.type, self.kv, self.prev = type_, kv, prev
 
 
+class TxnResult:
+    __slots__ = ("ok", "rev", "failed", "current")
+
+    def __init__(self, ok, rev, failed=-1, current=None):
+        self.ok, self.rev, self.failed, self.current = ok, rev, failed, current
+
+
 class MVCCStore:
     """Thread-safe; all mutations are serialized under one lock like etcd's apply loop."""
 
@@ -89,27 +96,31 @@ class MVCCStore:
             old = self._history.popleft()
             self._compact_rev = old.kv.mod_rev
 
-    def _apply_put(self, key, value):
-        self._rev += 1
+    def _apply_put(self, key, value, rev=None):
+        if rev is None:
+            self._rev += 1
+            rev = self._rev
         prev = self._data.get(key)
         if prev is None:
-            kv = KV(key, value, self._rev, self._rev, 1)
+            kv = KV(key, value, rev, rev, 1)
             bisect.insort(self._keys, key)
         else:
-            kv = KV(key, value, prev.create_rev, self._rev, prev.version + 1)
+            kv = KV(key, value, prev.create_rev, rev, prev.version + 1)
         self._data[key] = kv
         ev = Event(PUT, kv, prev)
         self._record(ev)
         return ev
 
-    def _apply_delete(self, key):
+    def _apply_delete(self, key, rev=None, tombstone=None):
         prev = self._data.pop(key, None)
         if prev is None:
             return None
-        self._rev += 1
+        if rev is None:
+            self._rev += 1
+            rev = self._rev
         i = bisect.bisect_left(self._keys, key)
         del self._keys[i]
-        ev = Event(DELETE, KV(key, None, prev.create_rev, self._rev, 0), prev)
+        ev = Event(DELETE, KV(key, tombstone, prev.create_rev, rev, 0), prev)
         self._record(ev)
         return ev
 
@@ -158,6 +169,37 @@ class MVCCStore:
                 return False, cur
             self._log(DELETE, key, None)
             return True, self._apply_delete(key)
+
+    def txn(self, cmps, ops):
+        """etcd Txn(If cmps Then ops) under ONE revision; same encoding as `storage.wire`
+        (cmps: (kind, key, arg, value); ops: (kind, key, value[, rv_token])). Returns a
+        `TxnResult`-like object: ok, rev, failed (index of the first false compare), current."""
+        with self._lock:
+            for i, (kind, key, arg, val) in enumerate(cmps):
+                cur = self._data.get(key)
+                ok = ((cur.mod_rev == arg if cur else arg == 0) if kind == 0 else
+                      cur is not None if kind == 1 else cur is None if kind == 2 else
+                      cur is not None and cur.value == val)
+                if not ok:
+                    return TxnResult(False, self._rev, i, cur)
+            rev = self._rev + 1
+            rs = str(rev).encode()
+            changed = False
+            for op in ops:
+                kind, key, val = op[0], op[1], op[2]
+                if kind >= 2 and val is not None:
+                    val = val.replace(op[3], rs)
+                if kind in (0, 2):
+                    self._log(PUT, key, val)
+                    self._apply_put(key, val, rev)
+                    changed = True
+                elif key in self._data:
+                    self._log(DELETE, key, None)
+                    self._apply_delete(key, rev, val if kind == 3 else None)
+                    changed = True
+            if changed:
+                self._rev = rev
+            return TxnResult(True, self._rev)
 
     def range(self, prefix: str, limit: int = 0, start_after: str | None = None):
         """Returns (list[KV], more: bool, revision)."""

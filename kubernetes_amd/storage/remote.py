@@ -1,0 +1,226 @@
+"""asyncio client for the native store server (`kamd-etcd`) + a helper that runs one.
+
+Several API server worker processes share one `kamd-etcd` (the role etcd plays for a set of
+kube-apiservers, reference `staging/src/k8s.io/apiserver/pkg/storage/etcd3/store.go`): every
+worker commits with compare-and-swap transactions and feeds its own watch cache from a single
+ordered watch stream, so all workers observe the same revision order.
+
+Requests are pipelined on one connection (ids matched to futures); watch events arrive on the
+same connection as frames tagged with the watch id and are delivered synchronously to the
+callback, in store order.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import struct
+import subprocess
+import tempfile
+import time
+
+from ..native import BIN_DIR
+from . import wire
+from .mvcc import CompactedError, TxnResult
+
+_hdr = struct.Struct("<IIB")
+
+
+class StoreError(Exception):
+    pass
+
+
+class _Proto(asyncio.Protocol):
+    def __init__(self, owner):
+        self.owner = owner
+        self.buf = bytearray()
+        self.transport = None
+
+    def connection_made(self, transport):
+        self.transport = transport
+
+    def data_received(self, data):
+        buf = self.buf
+        buf += data
+        off = 0
+        n = len(buf)
+        owner = self.owner
+        while n - off >= 9:
+            ln, rid, st = _hdr.unpack_from(buf, off)
+            if n - off - 4 < ln:
+                break
+            payload = bytes(buf[off + 9:off + 4 + ln])
+            off += 4 + ln
+            owner._frame(rid, st, payload)
+        if off:
+            del buf[:off]
+
+    def connection_lost(self, exc):
+        self.owner._lost(exc)
+
+
+class RemoteStore:
+    def __init__(self, address: str):
+        self.address = address
+        self._proto = None
+        self._next = 1
+        self._pending: dict[int, asyncio.Future] = {}
+        self._watches: dict[int, callable] = {}
+        self.closed = False
+
+    async def connect(self):
+        loop = asyncio.get_running_loop()
+        if self.address.startswith("unix://"):
+            _, self._proto = await loop.create_unix_connection(lambda: _Proto(self), self.address[len("unix://"):])
+        else:
+            hp = self.address.split("://", 1)[-1]
+            host, port = hp.rsplit(":", 1)
+            _, self._proto = await loop.create_connection(lambda: _Proto(self), host, int(port))
+        return self
+
+    # -- framing ------------------------------------------------------------
+    def _send(self, op, payload=b""):
+        if self._proto is None or self.closed:
+            raise StoreError("store connection closed")
+        rid = self._next
+        self._next += 1
+        fut = asyncio.get_running_loop().create_future()
+        self._pending[rid] = fut
+        self._proto.transport.write(_hdr.pack(len(payload) + 5, rid, op) + payload)
+        return rid, fut
+
+    def _frame(self, rid, st, payload):
+        if st == wire.EVENT:
+            cb = self._watches.get(rid)
+            if cb is not None:
+                t = payload[0]
+                kv, _ = wire.decode_kv(payload, 1)
+                cb(t, kv)
+            return
+        fut = self._pending.pop(rid, None)
+        if fut is not None and not fut.done():
+            fut.set_result((st, payload))
+
+    def _lost(self, exc):
+        self.closed = True
+        for fut in self._pending.values():
+            if not fut.done():
+                fut.set_exception(StoreError(f"store connection lost: {exc}"))
+        self._pending.clear()
+        for cb in list(self._watches.values()):
+            try:
+                cb(None, None)  # stream end
+            except Exception:
+                pass
+        self._watches.clear()
+
+    # -- API ----------------------------------------------------------------
+    async def txn(self, cmps, ops) -> TxnResult:
+        _, fut = self._send(wire.TXN, wire.encode_txn(cmps, ops))
+        st, p = await fut
+        if st == wire.OK:
+            return TxnResult(True, struct.unpack_from("<q", p)[0])
+        if st == wire.FAILED:
+            idx, kv, rev = wire.decode_failed(p)
+            return TxnResult(False, rev, idx, kv)
+        raise StoreError(f"txn failed with status {st}")
+
+    async def get(self, key):
+        kb = key.encode()
+        _, fut = self._send(wire.GET, struct.pack("<I", len(kb)) + kb)
+        st, p = await fut
+        if st == wire.NOT_FOUND:
+            return None
+        return wire.decode_kv(p)[0]
+
+    async def range(self, prefix, limit=0, start_after=None):
+        _, fut = self._send(wire.RANGE, wire.encode_range(prefix, limit, start_after))
+        st, p = await fut
+        return wire.decode_range(p)
+
+    async def revision(self):
+        _, fut = self._send(wire.REV)
+        st, p = await fut
+        return struct.unpack_from("<q", p)[0]
+
+    async def compact(self, rev):
+        _, fut = self._send(wire.COMPACT, struct.pack("<q", rev))
+        await fut
+
+    async def watch(self, prefix, from_rev, callback):
+        """callback(type, kv) for each event with mod_rev > from_rev (0 = only new events);
+        callback(None, None) when the stream ends. Returns the store revision at subscribe."""
+        pb = prefix.encode()
+        rid, fut = self._send(wire.WATCH, struct.pack("<q", from_rev) + struct.pack("<I", len(pb)) + pb)
+        # register before the reply: replayed events directly follow the OK frame
+        self._watches[rid] = callback
+        st, p = await fut
+        if st == wire.COMPACTED:
+            self._watches.pop(rid, None)
+            raise CompactedError(from_rev)
+        return struct.unpack_from("<q", p)[0]
+
+    async def close(self):
+        self.closed = True
+        if self._proto is not None and self._proto.transport is not None:
+            self._proto.transport.close()
+
+
+class StoreServer:
+    """Runs `kamd-etcd` as a child process on a unix socket (or TCP port)."""
+
+    def __init__(self, socket_path=None, wal=None, history=500_000, tcp=False):
+        self.dir = None
+        if socket_path is None and not tcp:
+            self.dir = tempfile.mkdtemp(prefix="kamd-etcd-")
+            socket_path = os.path.join(self.dir, "store.sock")
+        self.socket_path = socket_path
+        self.tcp = tcp
+        self.wal = wal
+        self.history = history
+        self.proc = None
+        self.address = None
+
+    def start(self, timeout=10.0):
+        exe = os.path.join(BIN_DIR, "kamd-etcd")
+        if not os.path.exists(exe):
+            raise StoreError(f"{exe} not built (python -m kubernetes_amd.native.build)")
+        cmd = [exe, "--history", str(self.history)]
+        port_file = None
+        if self.tcp:
+            port_file = tempfile.mktemp(prefix="kamd-etcd-port-")
+            cmd += ["--listen-tcp", "0", "--port-file", port_file]
+        else:
+            cmd += ["--listen-unix", self.socket_path]
+        if self.wal:
+            cmd += ["--wal", self.wal]
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            if self.proc.poll() is not None:
+                raise StoreError(f"kamd-etcd exited with {self.proc.returncode}")
+            if self.tcp and os.path.exists(port_file) and os.path.getsize(port_file):
+                with open(port_file) as f:
+                    self.address = f"tcp://127.0.0.1:{int(f.read())}"
+                os.unlink(port_file)
+                return self.address
+            if not self.tcp and os.path.exists(self.socket_path):
+                self.address = f"unix://{self.socket_path}"
+                return self.address
+            time.sleep(0.01)
+        raise StoreError("kamd-etcd did not start")
+
+    def stop(self):
+        if self.proc and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
+        if self.dir:
+            try:
+                if os.path.exists(self.socket_path):
+                    os.unlink(self.socket_path)
+                os.rmdir(self.dir)
+            except OSError:
+                pass

@@ -1,0 +1,712 @@
+// kamd-etcd — native MVCC key-value store with etcd-v3 semantics, embeddable (C ABI, libkamd_store.so)
+// and servable (kamd-etcd binary, unix/TCP socket, binary protocol, watch streams).
+//
+// What the API server needs from etcd (reference staging/src/k8s.io/apiserver/pkg/storage/etcd3/store.go:128-666):
+// one cluster revision; per-key create/mod revision and version; multi-key transactions with
+// compare-and-swap (GuaranteedUpdate, conditional delete, and here also the device-claim keys that
+// make GPU double-assignment impossible across API server workers); ordered range with limit +
+// start key; watch from a revision with a bounded history (compaction -> "compacted" error); WAL.
+//
+// Resource versions are injected by the store: a put op may name a token (random per API server
+// worker, so user data cannot collide with it) whose occurrences in the value are replaced by the
+// decimal commit revision, so a worker encodes an object ONCE without knowing the revision
+// another worker may take concurrently.
+//
+// Protocol (little endian). Request frame:  u32 len | u32 id | u8 op | payload
+//                           Response frame: u32 len | u32 id | u8 status | payload
+//   TXN(1):   u16 ncmp {u8 kind(0 modrev==,1 exists,2 absent,3 value==) u32 klen key i64 arg u32 vlen val}
+//             u16 nops {u8 kind(0 put,1 del,2 put+inject,3 del+tombstone) u32 klen key u32 vlen val
+//                       [kinds 2,3: u32 tlen token]}
+//             -> status 0: i64 rev | status 1 (compare failed): u16 idx of failed compare, kv of that key
+//   GET(2):   u32 klen key -> status 0: kv | status 4 not found
+//   RANGE(3): u32 plen prefix u32 limit u32 salen start_after -> i64 rev u8 more u32 n {kv}
+//   WATCH(4): i64 from_rev u32 plen prefix -> status 0 i64 rev, then EVENT frames (status 8) on the same
+//             id: u8 type(0 put,1 del) kv(with prev? no) ; status 3 if from_rev is compacted
+//   REV(5):   -> i64 rev
+//   COMPACT(6): i64 rev
+//   kv = i64 create_rev i64 mod_rev i64 version u32 klen key u32 vlen val
+//   A kind-3 delete carries the "tombstone" (final object state) reported in the delete event
+//   instead of the last stored value; it is not stored.
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <deque>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace kamd {
+
+struct KV {
+  int64_t create_rev = 0, mod_rev = 0, version = 0;
+  std::string value;
+};
+
+struct Event {
+  uint8_t type;  // 0 put, 1 delete
+  int64_t rev;
+  std::string key;
+  std::shared_ptr<KV> kv;  // state after the event (for delete: last value, version 0)
+};
+
+struct Cmp {
+  uint8_t kind;
+  std::string key;
+  int64_t arg;
+  std::string val;
+};
+
+struct Op {
+  uint8_t kind;  // 0 put, 1 delete, 2 put with RV injection, 3 delete with tombstone + RV injection
+  std::string key;
+  std::string val;
+  std::string token;  // kinds 2/3: every occurrence in val is replaced by the commit revision
+};
+
+static void inject(std::string* v, const std::string& token, const std::string& rs) {
+  if (token.empty()) return;
+  size_t pos = 0;
+  while ((pos = v->find(token, pos)) != std::string::npos) {
+    v->replace(pos, token.size(), rs);
+    pos += rs.size();
+  }
+}
+
+class Engine {
+ public:
+  explicit Engine(size_t history_cap = 200000) : cap_(history_cap) {}
+
+  int64_t rev() const { return rev_; }
+  int64_t compacted() const { return compact_rev_; }
+
+  bool open_wal(const std::string& path) {
+    replay(path);
+    wal_ = fopen(path.c_str(), "ab");
+    return wal_ != nullptr;
+  }
+  ~Engine() {
+    if (wal_) fclose(wal_);
+  }
+
+  const KV* get(const std::string& k) const {
+    auto it = data_.find(k);
+    return it == data_.end() ? nullptr : it->second.get();
+  }
+
+  // returns -1 on success (rev in *rev_out), otherwise index of the failed compare
+  int txn(const std::vector<Cmp>& cmps, const std::vector<Op>& ops, int64_t* rev_out, std::vector<Event>* evs) {
+    for (size_t i = 0; i < cmps.size(); ++i) {
+      const Cmp& c = cmps[i];
+      const KV* kv = get(c.key);
+      bool ok = false;
+      switch (c.kind) {
+        case 0: ok = kv ? kv->mod_rev == c.arg : c.arg == 0; break;
+        case 1: ok = kv != nullptr; break;
+        case 2: ok = kv == nullptr; break;
+        case 3: ok = kv != nullptr && kv->value == c.val; break;
+      }
+      if (!ok) return (int)i;
+    }
+    int64_t r = rev_ + 1;
+    std::string rs = std::to_string(r);
+    size_t changes = 0;
+    for (size_t oi = 0; oi < ops.size(); ++oi) {
+      const Op& o = ops[oi];
+      bool last = oi + 1 == ops.size();
+      if (o.kind == 0 || o.kind == 2) {
+        std::string v = o.val;
+        inject(&v, o.token, rs);
+        auto& slot = data_[o.key];
+        auto nk = std::make_shared<KV>();
+        nk->mod_rev = r;
+        nk->value = std::move(v);
+        if (slot) {
+          nk->create_rev = slot->create_rev;
+          nk->version = slot->version + 1;
+        } else {
+          nk->create_rev = r;
+          nk->version = 1;
+        }
+        slot = nk;
+        record(Event{0, r, o.key, nk}, evs);
+        log_wal(0, last, o.key, nk->value);
+        ++changes;
+      } else {
+        auto it = data_.find(o.key);
+        if (it == data_.end()) {
+          if (last && changes) log_wal(1, true, o.key, "");  // keep the txn terminated in the WAL
+          continue;
+        }
+        auto dk = std::make_shared<KV>(*it->second);
+        dk->mod_rev = r;
+        dk->version = 0;
+        if (o.kind == 3) {  // tombstone: final object state reported to watchers, not stored
+          dk->value = o.val;
+          inject(&dk->value, o.token, rs);
+        }
+        data_.erase(it);
+        record(Event{1, r, o.key, dk}, evs);
+        log_wal(1, last, o.key, "");
+        ++changes;
+      }
+    }
+    if (changes) {
+      rev_ = r;
+      if (wal_) fflush(wal_);
+    }
+    *rev_out = rev_;
+    return -1;
+  }
+
+  // range over keys with prefix, optionally strictly after start_after
+  int64_t range(const std::string& prefix, uint32_t limit, const std::string& start_after,
+                std::vector<std::pair<const std::string*, const KV*>>* out, bool* more) const {
+    auto it = start_after.empty() ? data_.lower_bound(prefix) : data_.upper_bound(start_after);
+    *more = false;
+    for (; it != data_.end(); ++it) {
+      if (it->first.compare(0, prefix.size(), prefix) != 0) break;
+      if (limit && out->size() >= limit) {
+        *more = true;
+        break;
+      }
+      out->push_back({&it->first, it->second.get()});
+    }
+    return rev_;
+  }
+
+  // events with rev > from; false if compacted
+  bool since(int64_t from, const std::string& prefix, std::vector<const Event*>* out) const {
+    if (from < compact_rev_) return false;
+    size_t lo = 0, hi = hist_.size();
+    while (lo < hi) {
+      size_t mid = (lo + hi) / 2;
+      if (hist_[mid].rev <= from) lo = mid + 1; else hi = mid;
+    }
+    for (size_t i = lo; i < hist_.size(); ++i)
+      if (hist_[i].key.compare(0, prefix.size(), prefix) == 0) out->push_back(&hist_[i]);
+    return true;
+  }
+
+  void compact(int64_t r) {
+    while (!hist_.empty() && hist_.front().rev <= r) hist_.pop_front();
+    if (r > compact_rev_) compact_rev_ = r;
+  }
+
+  size_t size() const { return data_.size(); }
+
+ private:
+  void record(Event&& e, std::vector<Event>* evs) {
+    if (evs) evs->push_back(e);
+    hist_.push_back(std::move(e));
+    if (hist_.size() > cap_) {
+      compact_rev_ = hist_.front().rev;
+      hist_.pop_front();
+    }
+  }
+  // WAL record: u8 op | u8 last-op-of-txn | u32 klen | u32 vlen | key | value. Replay regroups
+  // records into their transactions so revisions survive a restart exactly; a torn tail (partial
+  // record or unterminated transaction) is dropped.
+  void log_wal(uint8_t op, bool last, const std::string& k, const std::string& v) {
+    if (!wal_) return;
+    uint32_t kl = (uint32_t)k.size(), vl = (uint32_t)v.size();
+    uint8_t end = last ? 1 : 0;
+    fwrite(&op, 1, 1, wal_);
+    fwrite(&end, 1, 1, wal_);
+    fwrite(&kl, 4, 1, wal_);
+    fwrite(&vl, 4, 1, wal_);
+    fwrite(k.data(), 1, kl, wal_);
+    fwrite(v.data(), 1, vl, wal_);
+  }
+  void replay(const std::string& path) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return;
+    std::vector<Op> ops;
+    for (;;) {
+      uint8_t op, end;
+      uint32_t kl, vl;
+      if (fread(&op, 1, 1, f) != 1 || fread(&end, 1, 1, f) != 1 || fread(&kl, 4, 1, f) != 1 ||
+          fread(&vl, 4, 1, f) != 1)
+        break;
+      std::string k(kl, '\0'), v(vl, '\0');
+      if ((kl && fread(&k[0], 1, kl, f) != kl) || (vl && fread(&v[0], 1, vl, f) != vl)) break;  // torn tail
+      ops.push_back(Op{op, k, v, ""});
+      if (end) {
+        int64_t r;
+        FILE* save = wal_;
+        wal_ = nullptr;
+        txn({}, ops, &r, nullptr);
+        wal_ = save;
+        ops.clear();
+      }
+    }
+    fclose(f);
+  }
+
+  std::map<std::string, std::shared_ptr<KV>> data_;
+  std::deque<Event> hist_;
+  size_t cap_;
+  int64_t rev_ = 1;  // etcd starts at 1
+  int64_t compact_rev_ = 0;
+  FILE* wal_ = nullptr;
+};
+
+// ---------------------------------------------------------------------------
+// wire helpers
+struct Reader {
+  const char* p;
+  const char* e;
+  bool ok = true;
+  template <typename T>
+  T get() {
+    T v{};
+    if (e - p < (long)sizeof(T)) { ok = false; return v; }
+    memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+  }
+  std::string str() {
+    uint32_t n = get<uint32_t>();
+    if (!ok || e - p < (long)n) { ok = false; return {}; }
+    std::string s(p, n);
+    p += n;
+    return s;
+  }
+};
+
+struct Writer {
+  std::string b;
+  template <typename T>
+  void put(T v) { b.append(reinterpret_cast<const char*>(&v), sizeof(T)); }
+  void str(const std::string& s) { put<uint32_t>((uint32_t)s.size()); b.append(s); }
+  void kv(const std::string& k, const KV& v) {
+    put<int64_t>(v.create_rev);
+    put<int64_t>(v.mod_rev);
+    put<int64_t>(v.version);
+    str(k);
+    str(v.value);
+  }
+};
+
+bool parse_txn(Reader& r, std::vector<Cmp>* cmps, std::vector<Op>* ops) {
+  uint16_t nc = r.get<uint16_t>();
+  for (uint16_t i = 0; i < nc && r.ok; ++i) {
+    Cmp c;
+    c.kind = r.get<uint8_t>();
+    c.key = r.str();
+    c.arg = r.get<int64_t>();
+    c.val = r.str();
+    if (c.kind > 3) return false;
+    cmps->push_back(std::move(c));
+  }
+  uint16_t no = r.get<uint16_t>();
+  for (uint16_t i = 0; i < no && r.ok; ++i) {
+    Op o;
+    o.kind = r.get<uint8_t>();
+    o.key = r.str();
+    o.val = r.str();
+    if (o.kind >= 2) o.token = r.str();
+    if (o.kind > 3) return false;
+    ops->push_back(std::move(o));
+  }
+  return r.ok;
+}
+
+}  // namespace kamd
+
+// ===========================================================================
+// C ABI (libkamd_store.so): synchronous engine for in-process use and differential tests.
+extern "C" {
+struct kamd_store {
+  kamd::Engine eng;
+  std::string out;  // last result buffer
+  explicit kamd_store(size_t cap) : eng(cap) {}
+};
+
+kamd_store* kamd_store_open(const char* wal_path, uint64_t history_cap) {
+  auto* s = new kamd_store(history_cap ? history_cap : 200000);
+  if (wal_path && *wal_path && !s->eng.open_wal(wal_path)) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+void kamd_store_close(kamd_store* s) { delete s; }
+int64_t kamd_store_rev(kamd_store* s) { return s->eng.rev(); }
+int64_t kamd_store_compacted(kamd_store* s) { return s->eng.compacted(); }
+uint64_t kamd_store_size(kamd_store* s) { return s->eng.size(); }
+
+// txn request encoded exactly like the TXN wire payload; returns -1 ok (rev in *rev) or the failed index
+int kamd_store_txn(kamd_store* s, const char* req, uint32_t len, int64_t* rev) {
+  kamd::Reader r{req, req + len};
+  std::vector<kamd::Cmp> cmps;
+  std::vector<kamd::Op> ops;
+  if (!kamd::parse_txn(r, &cmps, &ops)) return -2;
+  return s->eng.txn(cmps, ops, rev, nullptr);
+}
+
+// results are written into an internal buffer: *out / *out_len valid until the next call
+int kamd_store_get(kamd_store* s, const char* key, uint32_t klen, const char** out, uint32_t* out_len) {
+  const kamd::KV* kv = s->eng.get(std::string(key, klen));
+  if (!kv) return 0;
+  kamd::Writer w;
+  w.kv(std::string(key, klen), *kv);
+  s->out.swap(w.b);
+  *out = s->out.data();
+  *out_len = (uint32_t)s->out.size();
+  return 1;
+}
+
+int kamd_store_range(kamd_store* s, const char* prefix, uint32_t plen, uint32_t limit, const char* start, uint32_t slen,
+                     const char** out, uint32_t* out_len) {
+  std::vector<std::pair<const std::string*, const kamd::KV*>> res;
+  bool more = false;
+  int64_t rev = s->eng.range(std::string(prefix, plen), limit, std::string(start ? start : "", slen), &res, &more);
+  kamd::Writer w;
+  w.put<int64_t>(rev);
+  w.put<uint8_t>(more ? 1 : 0);
+  w.put<uint32_t>((uint32_t)res.size());
+  for (auto& kv : res) w.kv(*kv.first, *kv.second);
+  s->out.swap(w.b);
+  *out = s->out.data();
+  *out_len = (uint32_t)s->out.size();
+  return (int)res.size();
+}
+
+int kamd_store_since(kamd_store* s, int64_t from, const char* prefix, uint32_t plen, const char** out, uint32_t* out_len) {
+  std::vector<const kamd::Event*> evs;
+  if (!s->eng.since(from, std::string(prefix, plen), &evs)) return -1;
+  kamd::Writer w;
+  w.put<uint32_t>((uint32_t)evs.size());
+  for (auto* e : evs) {
+    w.put<uint8_t>(e->type);
+    w.kv(e->key, *e->kv);
+  }
+  s->out.swap(w.b);
+  *out = s->out.data();
+  *out_len = (uint32_t)s->out.size();
+  return (int)evs.size();
+}
+
+void kamd_store_compact(kamd_store* s, int64_t rev) { s->eng.compact(rev); }
+}  // extern "C"
+
+// ===========================================================================
+// server (kamd-etcd)
+#ifdef KAMD_STORE_SERVER
+namespace kamd {
+
+struct Conn {
+  int fd;
+  std::string in, out;
+  bool want_write = false;
+};
+
+struct Watch {
+  Conn* conn;
+  uint32_t id;
+  std::string prefix;
+};
+
+class Server {
+ public:
+  Server(Engine* e) : eng_(e) {}
+
+  int listen_unix(const char* path) {
+    int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    sockaddr_un a{};
+    a.sun_family = AF_UNIX;
+    snprintf(a.sun_path, sizeof a.sun_path, "%s", path);
+    unlink(path);
+    if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, 1024) < 0) { perror("bind/listen"); return -1; }
+    add_listener(fd);
+    return fd;
+  }
+
+  int listen_tcp(int port, int* bound) {
+    int fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    a.sin_port = htons((uint16_t)port);
+    if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, 1024) < 0) { perror("bind/listen"); return -1; }
+    socklen_t l = sizeof a;
+    getsockname(fd, (sockaddr*)&a, &l);
+    *bound = ntohs(a.sin_port);
+    add_listener(fd);
+    return fd;
+  }
+
+  void run() {
+    epoll_event evs[256];
+    for (;;) {
+      int n = epoll_wait(ep_, evs, 256, 1000);
+      for (int i = 0; i < n; ++i) {
+        int fd = evs[i].data.fd;
+        if (listeners_.count(fd)) { accept_all(fd); continue; }
+        auto it = conns_.find(fd);
+        if (it == conns_.end()) continue;
+        Conn* c = it->second.get();
+        if (evs[i].events & (EPOLLHUP | EPOLLERR)) { close_conn(c); continue; }
+        if (evs[i].events & EPOLLIN) {
+          if (!read_conn(c)) { close_conn(c); continue; }
+        }
+        if (evs[i].events & EPOLLOUT) flush(c);
+      }
+      // flush every connection with pending output once per loop (coalesces watch events)
+      for (Conn* c : dirty_) flush(c);
+      dirty_.clear();
+    }
+  }
+
+ private:
+  void add_listener(int fd) {
+    if (ep_ < 0) ep_ = epoll_create1(EPOLL_CLOEXEC);
+    epoll_event e{};
+    e.events = EPOLLIN;
+    e.data.fd = fd;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+    listeners_[fd] = 1;
+  }
+
+  void accept_all(int lfd) {
+    for (;;) {
+      int fd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) return;
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      auto c = std::make_unique<Conn>();
+      c->fd = fd;
+      epoll_event e{};
+      e.events = EPOLLIN | EPOLLRDHUP;
+      e.data.fd = fd;
+      epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+      conns_[fd] = std::move(c);
+    }
+  }
+
+  void close_conn(Conn* c) {
+    for (size_t i = 0; i < watches_.size();) {
+      if (watches_[i].conn == c) { watches_[i] = watches_.back(); watches_.pop_back(); } else ++i;
+    }
+    epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+    close(c->fd);
+    dirty_.erase(std::remove(dirty_.begin(), dirty_.end(), c), dirty_.end());
+    conns_.erase(c->fd);
+  }
+
+  bool read_conn(Conn* c) {
+    char buf[1 << 16];
+    for (;;) {
+      ssize_t n = read(c->fd, buf, sizeof buf);
+      if (n > 0) { c->in.append(buf, (size_t)n); continue; }
+      if (n == 0) return false;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      return false;
+    }
+    size_t off = 0;
+    while (c->in.size() - off >= 9) {
+      uint32_t len;
+      memcpy(&len, c->in.data() + off, 4);
+      if (c->in.size() - off - 4 < len) break;
+      uint32_t id;
+      memcpy(&id, c->in.data() + off + 4, 4);
+      uint8_t op = (uint8_t)c->in[off + 8];
+      handle(c, id, op, c->in.data() + off + 9, len - 5);
+      off += 4 + len;
+    }
+    c->in.erase(0, off);
+    return true;
+  }
+
+  void reply(Conn* c, uint32_t id, uint8_t status, const std::string& payload) {
+    uint32_t len = (uint32_t)(payload.size() + 5);
+    c->out.append(reinterpret_cast<const char*>(&len), 4);
+    c->out.append(reinterpret_cast<const char*>(&id), 4);
+    c->out.push_back((char)status);
+    c->out.append(payload);
+    mark(c);
+  }
+
+  void mark(Conn* c) {
+    if (!c->want_write) {
+      c->want_write = true;
+      dirty_.push_back(c);
+    }
+  }
+
+  void flush(Conn* c) {
+    while (!c->out.empty()) {
+      ssize_t n = write(c->fd, c->out.data(), c->out.size());
+      if (n > 0) { c->out.erase(0, (size_t)n); continue; }
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        epoll_event e{};
+        e.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+        e.data.fd = c->fd;
+        epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
+        c->want_write = false;
+        return;
+      }
+      break;
+    }
+    c->want_write = false;
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP;
+    e.data.fd = c->fd;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
+  }
+
+  void dispatch(const std::vector<Event>& evs) {
+    if (watches_.empty()) return;
+    for (const Event& ev : evs) {
+      for (Watch& w : watches_) {
+        if (ev.key.compare(0, w.prefix.size(), w.prefix) != 0) continue;
+        Writer pw;
+        pw.put<uint8_t>(ev.type);
+        pw.kv(ev.key, *ev.kv);
+        reply(w.conn, w.id, 8, pw.b);
+      }
+    }
+  }
+
+  void handle(Conn* c, uint32_t id, uint8_t op, const char* p, uint32_t n) {
+    Reader r{p, p + n};
+    Writer w;
+    switch (op) {
+      case 1: {  // TXN
+        std::vector<Cmp> cmps;
+        std::vector<Op> ops;
+        if (!parse_txn(r, &cmps, &ops)) { reply(c, id, 9, ""); return; }
+        int64_t rev;
+        std::vector<Event> evs;
+        int failed = eng_->txn(cmps, ops, &rev, &evs);
+        if (failed < 0) {
+          w.put<int64_t>(rev);
+          reply(c, id, 0, w.b);
+          dispatch(evs);
+        } else {
+          w.put<uint16_t>((uint16_t)failed);
+          const KV* kv = eng_->get(cmps[failed].key);
+          w.put<uint8_t>(kv ? 1 : 0);
+          if (kv) w.kv(cmps[failed].key, *kv);
+          w.put<int64_t>(eng_->rev());
+          reply(c, id, 1, w.b);
+        }
+        return;
+      }
+      case 2: {  // GET
+        std::string k = r.str();
+        const KV* kv = eng_->get(k);
+        if (!kv) { w.put<int64_t>(eng_->rev()); reply(c, id, 4, w.b); return; }
+        w.kv(k, *kv);
+        w.put<int64_t>(eng_->rev());
+        reply(c, id, 0, w.b);
+        return;
+      }
+      case 3: {  // RANGE
+        std::string prefix = r.str();
+        uint32_t limit = r.get<uint32_t>();
+        std::string sa = r.str();
+        std::vector<std::pair<const std::string*, const KV*>> res;
+        bool more;
+        int64_t rev = eng_->range(prefix, limit, sa, &res, &more);
+        w.put<int64_t>(rev);
+        w.put<uint8_t>(more ? 1 : 0);
+        w.put<uint32_t>((uint32_t)res.size());
+        for (auto& kv : res) w.kv(*kv.first, *kv.second);
+        reply(c, id, 0, w.b);
+        return;
+      }
+      case 4: {  // WATCH
+        int64_t from = r.get<int64_t>();
+        std::string prefix = r.str();
+        std::vector<const Event*> evs;
+        if (from > 0 && !eng_->since(from, prefix, &evs)) {
+          w.put<int64_t>(eng_->compacted());
+          reply(c, id, 3, w.b);
+          return;
+        }
+        w.put<int64_t>(eng_->rev());
+        reply(c, id, 0, w.b);
+        for (const Event* e : evs) {
+          Writer pw;
+          pw.put<uint8_t>(e->type);
+          pw.kv(e->key, *e->kv);
+          reply(c, id, 8, pw.b);
+        }
+        watches_.push_back(Watch{c, id, prefix});
+        return;
+      }
+      case 5:
+        w.put<int64_t>(eng_->rev());
+        reply(c, id, 0, w.b);
+        return;
+      case 6:
+        eng_->compact(r.get<int64_t>());
+        reply(c, id, 0, "");
+        return;
+      default:
+        reply(c, id, 9, "");
+    }
+  }
+
+  Engine* eng_;
+  int ep_ = -1;
+  std::unordered_map<int, int> listeners_;
+  std::unordered_map<int, std::unique_ptr<Conn>> conns_;
+  std::vector<Watch> watches_;
+  std::vector<Conn*> dirty_;
+};
+
+}  // namespace kamd
+
+int main(int argc, char** argv) {
+  signal(SIGPIPE, SIG_IGN);
+  const char* unix_path = nullptr;
+  const char* wal = nullptr;
+  const char* port_file = nullptr;
+  int tcp_port = -1;
+  size_t hist = 500000;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&](void) { return i + 1 < argc ? argv[++i] : ""; };
+    if (a == "--listen-unix") unix_path = val();
+    else if (a == "--listen-tcp") tcp_port = atoi(val());
+    else if (a == "--wal") wal = val();
+    else if (a == "--history") hist = (size_t)atol(val());
+    else if (a == "--port-file") port_file = val();
+    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--wal FILE] [--history N]\n"); return 2; }
+  }
+  kamd::Engine eng(hist);
+  if (wal && !eng.open_wal(wal)) { perror("wal"); return 1; }
+  kamd::Server srv(&eng);
+  if (unix_path && srv.listen_unix(unix_path) < 0) return 1;
+  if (tcp_port >= 0) {
+    int bound = 0;
+    if (srv.listen_tcp(tcp_port, &bound) < 0) return 1;
+    if (port_file) {
+      FILE* f = fopen(port_file, "w");
+      fprintf(f, "%d", bound);
+      fclose(f);
+    }
+  }
+  fprintf(stderr, "kamd-etcd: serving (rev %lld, %zu keys)\n", (long long)eng.rev(), eng.size());
+  srv.run();
+  return 0;
+}
+#endif
