@@ -48,8 +48,12 @@ def spawn_control_plane(tmp, args):
     env["PYTHONPATH"] = HERE + os.pathsep + env.get("PYTHONPATH", "")
     env.pop("HIP_VISIBLE_DEVICES", None)
     pf = os.path.join(tmp, "apiserver.port")
+    workers = args.apiserver_workers
+    if workers <= 0:   # auto: one worker per 2 ranks, up to 4 (each rank adds ~1 core of API load)
+        workers = min(4, max(1, int(os.environ.get("WORLD_SIZE", "1")) // 2))
+    args.apiserver_workers = workers
     api = subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf,
-                            "--storage-engine", args.storage_engine],
+                            "--storage-engine", args.storage_engine, "--workers", str(workers)],
                            env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "apiserver.log"), "w"))
     t = time.time()
     while not os.path.exists(pf):
@@ -191,6 +195,8 @@ def main():
     ap.add_argument("--payload", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--storage-engine", default="native", choices=["native", "python"])
     ap.add_argument("--no-events", action="store_true")
+    ap.add_argument("--apiserver-workers", type=int, default=0,
+                    help="API server processes over one native store (0 = auto by world size)")
     args = ap.parse_args()
     d = Dist()
     tmp = tempfile.mkdtemp(prefix="kamd-bench-")
@@ -200,7 +206,7 @@ def main():
         if d.rank == 0:
             url, procs = spawn_control_plane(tmp, args)   # before any GPU init
         d.init()
-        url = d.broadcast(url)
+        url, d.broadcast_done_workers = d.broadcast((url, args.apiserver_workers))
         if os.environ.get("KAMD_PROFILE_DIR"):
             import cProfile
             pr = cProfile.Profile()
@@ -235,7 +241,7 @@ def main():
         "config": {"model": "kubemark-density/8xMI355X-hollow-nodes/1-GPU-pods", "global_batch": pods // args.steps,
                    "seq_len": None, "parallelism": f"ranks{n}", "hollow_nodes": n * args.nodes_per_rank,
                    "gpus_per_node": args.gpus_per_node, "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
-                   "gpus_per_pod": args.gpus_per_pod},
+                   "gpus_per_pod": args.gpus_per_pod, "apiserver_workers": d.broadcast_done_workers},
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
         "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
         "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],

@@ -1,7 +1,12 @@
-"""Same write-path workload against an API server running in its own process
-(`python -m kubernetes_amd.cmd.apiserver`), so the numbers are server-side only."""
+"""Same write-path workload against an API server running in its own process(es)
+(`python -m kubernetes_amd.cmd.apiserver [--workers N]`), driven by several client processes,
+so the numbers are server-side only.
+
+    python benchmarks/apiserver_remote.py --pods 8000 --client-procs 4 --extra "--workers 4"
+"""
 import argparse
 import asyncio
+import multiprocessing as mp
 import os
 import subprocess
 import sys
@@ -13,9 +18,7 @@ sys.path.insert(0, ROOT)
 from kubernetes_amd.client.rest import Client  # noqa: E402
 
 
-async def run(url, a):
-    c0 = Client(url)
-    await c0.create("nodes", {"metadata": {"name": "n0"}})
+async def run(url, a, proc, start_at):
     ws = []
     for _ in range(a.watchers):
         w = await Client(url).watch("pods", None, "0")
@@ -25,29 +28,42 @@ async def run(url, a):
                 pass
         ws.append(asyncio.ensure_future(drain()))
     clients = [Client(url) for _ in range(a.clients)]
-    n_per = a.pods // a.clients
+    n_per = a.pods // a.client_procs // a.clients
 
     async def worker(ci, c):
         for i in range(n_per):
-            name = f"p{ci}-{i}"
+            name = f"p{proc}-{ci}-{i}"
             p = await c.create("pods", {"metadata": {"name": name, "namespace": "default"},
                                         "spec": {"containers": [{"name": "c", "image": "x",
                                                                  "resources": {"limits": {"amd.com/gpu": "1"}}}]}})
             er = p["spec"]["extendedResources"][0]["name"]
-            await c.bind("default", name, "n0", {er: {"resources": [f"g-{ci}-{i}"]}})
+            await c.bind("default", name, "n0", {er: {"resources": [f"g-{proc}-{ci}-{i}"]}})
             await c.patch("pods", name, {"status": {"phase": "Running"}}, "default", "merge", "status")
             await c.delete("pods", name, "default")
             await c.delete("pods", name, "default", grace_period=0)
+    while time.time() < start_at:
+        await asyncio.sleep(0.005)
     t = time.perf_counter()
     await asyncio.gather(*(worker(i, c) for i, c in enumerate(clients)))
-    dt = time.perf_counter() - t
-    print(f"{a.pods / dt:.0f} pod-cycles/s, {a.pods * 5 / dt:.0f} writes/s, {dt * 1e6 / (a.pods * 5):.1f} us/write")
+    return time.perf_counter() - t, n_per * a.clients
+
+
+def _proc(args):
+    url, a, proc, start_at = args
+    return asyncio.run(run(url, a, proc, start_at))
+
+
+async def _setup(url):
+    c = Client(url)
+    await c.create("nodes", {"metadata": {"name": "n0"}})
+    await c.close()
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pods", type=int, default=4000)
-    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--clients", type=int, default=64, help="concurrent clients per client process")
+    ap.add_argument("--client-procs", type=int, default=1)
     ap.add_argument("--watchers", type=int, default=3)
     ap.add_argument("--extra", default="")
     a = ap.parse_args()
@@ -59,7 +75,15 @@ def main():
     while not os.path.exists(pf):
         time.sleep(0.05)
     try:
-        asyncio.run(run(f"http://127.0.0.1:{open(pf).read()}", a))
+        url = f"http://127.0.0.1:{open(pf).read()}"
+        asyncio.run(_setup(url))
+        start_at = time.time() + 1.0 + 0.2 * a.client_procs
+        with mp.get_context("spawn").Pool(a.client_procs) as pool:
+            res = pool.map(_proc, [(url, a, i, start_at) for i in range(a.client_procs)])
+        dt = max(r[0] for r in res)
+        pods = sum(r[1] for r in res)
+        print(f"{a.extra or 'single process'}: {pods / dt:.0f} pod-cycles/s, {pods * 5 / dt:.0f} writes/s, "
+              f"{dt * 1e6 / (pods * 5):.1f} us/write")
     finally:
         p.terminate()
         p.wait()

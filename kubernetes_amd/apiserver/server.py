@@ -10,20 +10,31 @@ Parity map:
     `namespaces/{ns}/finalize`, `pods/eviction`, `pods/log` (proxied to the kubelet).
   * discovery (`/api`, `/apis`, `/api/v1`, `/apis/<g>/<v>`), `/healthz`, `/version`, `/metrics`.
 
-The store and watch cache live in this process; every write is committed to the MVCC
-store and dispatched to watchers synchronously on the event loop, so a watcher can never
-observe revisions out of order and reads are always consistent with the last write.
+Two storage modes:
+  * embedded (default): the MVCC store lives in this process; every write is committed and
+    dispatched to watchers synchronously on the event loop, so a watcher can never observe
+    revisions out of order and reads are always consistent with the last write.
+  * shared (`store="unix:///…"` / `"tcp://…"`): several API server worker processes share
+    one native `kamd-etcd` (like several kube-apiservers share etcd). A worker commits with a
+    compare-and-swap transaction, the store injects the revision into the encoded object, and
+    every worker's watch cache is fed ONLY from the store's ordered watch stream — a write is
+    acknowledged once this worker's cache has applied its revision (read-your-writes). Device
+    assignments are claimed with per-device keys in the same transaction, so no two pods can
+    be bound to one GPU even when the binds race through different workers. A stale cache
+    shows up as a failed compare; the request is re-run once the cache caught up.
 """
 from __future__ import annotations
 
 import asyncio
 import base64
 import logging
+import secrets
 import time
 
 from ..api import codec, core, meta as m
 from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
 from ..api.meta import fast_copy, now_rfc3339
+from ..storage import wire
 from ..storage.mvcc import MVCCStore
 from ..utils.httpserver import HTTPServer, Response, StreamResponse
 from ..utils.metrics import Registry
@@ -50,12 +61,42 @@ def _err(e: APIError):
     return Response(e.code, codec.dumpb(m.status_obj(e.code, e.reason, e.message, e.details)))
 
 
+class _Stale(Exception):
+    """Shared-store compare failed: this worker's cache is behind revision `rev`."""
+
+    def __init__(self, rev):
+        super().__init__(rev)
+        self.rev = rev
+
+
+def _run_sync(coro):
+    """Drive a coroutine that never suspends (embedded-store commit path) to completion."""
+    try:
+        coro.send(None)
+    except StopIteration as e:
+        return e.value
+    coro.close()
+    raise RuntimeError("embedded-store operation suspended")
+
+
+DEVICE_PREFIX = "/kamd/devices/"   # claim keys, outside /registry/ so watch caches never see them
+
+
 class APIServer:
     def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
                  max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
                  kubelet_port_resolver=None):
-        self.store = store or MVCCStore()
+        self.remote_address = store if isinstance(store, str) else None
+        self.rstore = None            # RemoteStore once started (shared mode)
+        self.store = None if self.remote_address else (store or MVCCStore())
+        self._applied_rev = 0
+        self._rev_waiters: list = []  # heap of (rev, seq, future)
+        self._waiter_seq = 0
+        self._mine: dict = {}         # (key, rev) -> Entry committed by this worker
+        self._rv_token = ("@rv-" + secrets.token_hex(12) + "@").encode()
+        self._key_locks: dict = {}
+        self.store_healthy = True
         self.caches: dict[str, ResourceCache] = {}
         self.strategies = {}
         self.storage_codec = codec.StorageCodec(storage_media_type)
@@ -83,8 +124,14 @@ class APIServer:
         self.m_inflight = self.metrics.gauge("apiserver_current_inflight_requests", "In-flight requests", ("requestKind",))
         self.m_dropped = self.metrics.counter("apiserver_dropped_requests", "Requests dropped with 429", ("requestKind",))
         self.metrics.register_collector(self._collect)
-        self._load_from_store()
-        self.bootstrap()
+        if self.store is not None:
+            self._load_from_store()
+            _run_sync(self.bootstrap())
+
+    @property
+    def revision(self) -> int:
+        """Latest revision reflected in this server's caches."""
+        return self.store.revision if self.store is not None else self._applied_rev
 
     # ------------------------------------------------------------------
     def _install(self, ri):
@@ -97,7 +144,7 @@ class APIServer:
             if c.by_key:
                 out.append(f'etcd_object_counts{{resource="{plural}"}} {len(c.by_key)}')
         out.append("# TYPE apiserver_storage_revision gauge")
-        out.append(f"apiserver_storage_revision {self.store.revision}")
+        out.append(f"apiserver_storage_revision {self.revision}")
         return out
 
     def _load_from_store(self):
@@ -116,10 +163,164 @@ class APIServer:
                     self._index_pod(kv.key, None, obj)
             cache.rev = self.store.revision
 
-    def bootstrap(self):
+    async def bootstrap(self):
         for ns in ("default", "kube-system", "kube-public"):
             if self.get_object("namespaces", None, ns) is None:
-                self.create(m.BY_PLURAL["namespaces"], None, {"metadata": {"name": ns}}, admit=False)
+                try:
+                    await self._retrying(lambda: self.create(m.BY_PLURAL["namespaces"], None,
+                                                             {"metadata": {"name": ns}}, admit=False))
+                except APIError as e:
+                    if e.code != 409:   # another worker created it first
+                        raise
+
+    # ------------------------------------------------------------------
+    # shared-store mode
+    async def _start_remote(self):
+        from ..storage.remote import RemoteStore
+        self.rstore = await RemoteStore(self.remote_address).connect()
+        # one RANGE is an atomic snapshot (the store is single-threaded); watch from its revision
+        kvs, _, rev = await self.rstore.range("/registry/")
+        for kv in kvs:
+            self._ingest(0, kv, dispatch=False)
+        self._applied_rev = rev
+        for c in self.caches.values():
+            c.rev = rev
+        await self.rstore.watch("/registry/", rev, self._on_store_event)
+        await self.bootstrap()
+
+    def _decode_value(self, kv):
+        v = kv.value
+        if v[:4] == codec.MAGIC:
+            obj = self.storage_codec.decode(v)
+            obj.setdefault("metadata", {})["resourceVersion"] = str(kv.mod_rev)
+            return obj, codec.dumpb(obj)
+        return codec.loads(v), v
+
+    def _ingest(self, t, kv, dispatch=True):
+        parts = kv.key.split("/", 3)
+        cache = self.caches.get(parts[2]) if len(parts) > 3 else None
+        if cache is None:
+            return
+        entry = self._mine.pop((kv.key, kv.mod_rev), None)
+        if entry is None:
+            obj, raw = self._decode_value(kv)
+            entry = cache.make_entry(obj, raw, kv.mod_rev)
+        prev = cache.by_key.get(kv.key)
+        if not dispatch:
+            cache.by_key[kv.key] = entry
+            return
+        etype = DELETED if t == wire.OP_DELETE else (MODIFIED if prev is not None else ADDED)
+        if etype == DELETED and prev is None:
+            return
+        cache.apply(etype, kv.key, entry, prev)
+
+    def _on_store_event(self, t, kv):
+        if t is None:
+            if self.store_healthy:
+                log.error("store watch stream ended; this API server worker is now unhealthy")
+            self.store_healthy = False
+            for _, _, f in self._rev_waiters:
+                if not f.done():
+                    f.set_exception(APIError(503, "ServiceUnavailable", "storage unavailable"))
+            self._rev_waiters.clear()
+            return
+        try:
+            self._ingest(t, kv)
+        except Exception:
+            log.exception("failed to apply store event %s@%d", kv.key, kv.mod_rev)
+        if kv.mod_rev > self._applied_rev:
+            self._applied_rev = kv.mod_rev
+            w = self._rev_waiters
+            if w and w[0][0] <= kv.mod_rev:
+                import heapq
+                while w and w[0][0] <= kv.mod_rev:
+                    _, _, f = heapq.heappop(w)
+                    if not f.done():
+                        f.set_result(None)
+
+    async def _wait_applied(self, rev, timeout=30.0):
+        if rev <= self._applied_rev:
+            return
+        if not self.store_healthy:
+            raise APIError(503, "ServiceUnavailable", "storage unavailable")
+        import heapq
+        f = asyncio.get_running_loop().create_future()
+        self._waiter_seq += 1
+        heapq.heappush(self._rev_waiters, (rev, self._waiter_seq, f))
+        try:
+            await asyncio.wait_for(f, timeout)
+        except asyncio.TimeoutError:
+            raise APIError(504, "Timeout", f"timed out waiting for revision {rev} to be observed")
+
+    async def _retrying(self, op, attempts=64):
+        """Re-run an operation whose compare failed on a stale cache (shared mode)."""
+        for i in range(attempts):
+            try:
+                return await op()
+            except _Stale as e:
+                if i == attempts - 1:
+                    raise APIError(409, "Conflict", "the object has been modified concurrently; please retry")
+                await self._wait_applied(e.rev)
+
+    @staticmethod
+    def _device_keys(pod):
+        if pod is None or core.pod_is_terminal(pod):
+            return set()
+        node = (pod.get("spec") or {}).get("nodeName")
+        if not node:
+            return set()
+        return {f"{DEVICE_PREFIX}{node}/{rn}/{i}" for rn, ids in core.pod_assigned_devices(pod).items() for i in ids}
+
+    async def _commit_remote(self, ri, key, etype, obj, prev):
+        md = obj["metadata"]
+        tok = self._rv_token
+        json_storage = self.storage_codec.media_type == codec.JSON
+        if json_storage:
+            md["resourceVersion"] = tok.decode()
+            raw_t = codec.dumpb(obj)
+            stored = raw_t
+        else:
+            md.pop("resourceVersion", None)
+            raw_t = None
+            stored = self.storage_codec.encode(obj)
+        cmps = [(wire.CMP_MOD_REV, key, prev.rev if prev is not None else 0, None)]
+        if etype == DELETED:
+            tomb = raw_t if raw_t is not None else codec.dumpb(dict(obj, metadata=dict(md, resourceVersion=tok.decode())))
+            ops = [(wire.OP_DELETE_TOMBSTONE, key, tomb, tok)]
+        elif json_storage:
+            ops = [(wire.OP_PUT_INJECT, key, stored, tok)]
+        else:
+            ops = [(wire.OP_PUT, key, stored)]   # binary values are never rewritten
+        if ri.plural == "pods":
+            old_d = self._device_keys(prev.obj if prev is not None else None)
+            new_d = set() if etype == DELETED else self._device_keys(obj)
+            kb = key.encode()
+            for dk in sorted(new_d - old_d):
+                cmps.append((wire.CMP_ABSENT, dk, 0, None))
+                ops.append((wire.OP_PUT, dk, kb))
+            for dk in sorted(old_d - new_d):
+                ops.append((wire.OP_DELETE, dk, None))
+        cache = self.caches[ri.plural]
+        done = []
+
+        def on_ok(rev):
+            rs = str(rev)
+            md["resourceVersion"] = rs
+            raw = raw_t.replace(tok, rs.encode()) if raw_t is not None else codec.dumpb(obj)
+            entry = cache.make_entry(obj, raw, rev)
+            self._mine[(key, rev)] = entry
+            done.append(entry)
+
+        res = await self.rstore.txn(cmps, ops, on_ok)
+        if not res.ok:
+            if res.failed == 0:
+                raise _Stale(res.rev)
+            owner = res.current.value.decode() if res.current is not None else "?"
+            dev = cmps[res.failed][1][len(DEVICE_PREFIX):]
+            raise APIError(409, "Conflict", f"device {dev} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
+        await self._wait_applied(res.rev)
+        self._mine.pop((key, res.rev), None)
+        return done[0]
 
     # ------------------------------------------------------------------
     # object-level API (admission plugins, controllers in-process, tests)
@@ -135,8 +336,13 @@ class APIServer:
 
     # ------------------------------------------------------------------
     # commit path
-    def _commit(self, ri, key, etype, obj, prev):
+    async def _commit(self, ri, key, etype, obj, prev):
         """Write obj (already fully prepared) to the store and the cache. Returns Entry."""
+        if self.rstore is not None:
+            return await self._commit_remote(ri, key, etype, obj, prev)
+        return self._commit_local(ri, key, etype, obj, prev)
+
+    def _commit_local(self, ri, key, etype, obj, prev):
         rev = self.store.revision + 1
         obj["metadata"]["resourceVersion"] = str(rev)
         raw = codec.dumpb(obj)
@@ -181,7 +387,7 @@ class APIServer:
 
     # ------------------------------------------------------------------
     # verbs
-    def create(self, ri, namespace, obj, user=None, admit=True, subresource=""):
+    async def create(self, ri, namespace, obj, user=None, admit=True, subresource=""):
         if not isinstance(obj, dict):
             raise bad_request("body must be a JSON object")
         init_object_meta(obj, ri, namespace)
@@ -199,7 +405,7 @@ class APIServer:
         key = m.key_for(ri, ns, m.name_of(obj))
         if key in self.caches[ri.plural].by_key:
             raise already_exists(ri, m.name_of(obj))
-        return self._commit(ri, key, ADDED, obj, None)
+        return await self._commit(ri, key, ADDED, obj, None)
 
     def _admit(self, a):
         try:
@@ -220,7 +426,7 @@ class APIServer:
             raise not_found(ri, name)
         return key, e
 
-    def update(self, ri, namespace, name, obj, user=None, subresource=""):
+    async def update(self, ri, namespace, name, obj, user=None, subresource=""):
         if not isinstance(obj, dict):
             raise bad_request("body must be a JSON object")
         key, prev = self._existing(ri, namespace, name)
@@ -261,11 +467,11 @@ class APIServer:
         self._validate_admission(a)
         # finalizers drained on an object that is being deleted -> delete it now
         if nm.get("deletionTimestamp") and not nm.get("finalizers") and self._grace_expired(ri, obj):
-            return self._commit(ri, key, DELETED, obj, prev)
+            return await self._commit(ri, key, DELETED, obj, prev)
         nm["resourceVersion"] = om.get("resourceVersion")
         if obj == old:
             return prev  # no-op update: no write, no event (etcd3 GuaranteedUpdate byte-equal short cut)
-        return self._commit(ri, key, MODIFIED, obj, prev)
+        return await self._commit(ri, key, MODIFIED, obj, prev)
 
     def _grace_expired(self, ri, obj):
         if ri.plural != "pods":
@@ -273,14 +479,14 @@ class APIServer:
         g = obj["metadata"].get("deletionGracePeriodSeconds")
         return not g
 
-    def guaranteed_update(self, ri, namespace, name, fn, user=None, subresource=""):
+    async def guaranteed_update(self, ri, namespace, name, fn, user=None, subresource=""):
         """Internal read-modify-write (used by binding, eviction)."""
         key, prev = self._existing(ri, namespace, name)
         obj = fast_copy(prev.obj)
         fn(obj)
-        return self._commit(ri, key, MODIFIED, obj, prev)
+        return await self._commit(ri, key, MODIFIED, obj, prev)
 
-    def patch(self, ri, namespace, name, content_type, patch_body, user=None, subresource=""):
+    async def patch(self, ri, namespace, name, content_type, patch_body, user=None, subresource=""):
         key, prev = self._existing(ri, namespace, name)
         try:
             patch = codec.loads(patch_body)
@@ -293,9 +499,9 @@ class APIServer:
             raise APIError(422, "Invalid", f"the patch could not be applied: {e}")
         if not isinstance(patch, dict) or "resourceVersion" not in (patch.get("metadata") or {}):
             new.setdefault("metadata", {})["resourceVersion"] = prev.obj["metadata"].get("resourceVersion")
-        return self.update(ri, namespace, name, new, user, subresource)
+        return await self.update(ri, namespace, name, new, user, subresource)
 
-    def delete(self, ri, namespace, name, opts=None, user=None):
+    async def delete(self, ri, namespace, name, opts=None, user=None):
         """Returns (Entry, deleted_now)."""
         opts = opts or {}
         key, prev = self._existing(ri, namespace, name)
@@ -325,7 +531,7 @@ class APIServer:
                 if not om.get("deletionTimestamp"):
                     om["deletionTimestamp"] = now_rfc3339()
                     obj.setdefault("status", {})["phase"] = "Terminating"
-                    return self._commit(ri, key, MODIFIED, obj, prev), False
+                    return (await self._commit(ri, key, MODIFIED, obj, prev)), False
                 return prev, False
         if grace > 0:
             cur = om.get("deletionGracePeriodSeconds")
@@ -335,7 +541,7 @@ class APIServer:
             om["deletionGracePeriodSeconds"] = grace
             if fins:
                 om["finalizers"] = fins
-            return self._commit(ri, key, MODIFIED, obj, prev), False
+            return (await self._commit(ri, key, MODIFIED, obj, prev)), False
         if fins:
             changed = om.get("finalizers") != fins or not om.get("deletionTimestamp") or om.get("deletionGracePeriodSeconds")
             om["finalizers"] = fins
@@ -343,12 +549,12 @@ class APIServer:
             om["deletionGracePeriodSeconds"] = 0
             if not changed:
                 return prev, False
-            return self._commit(ri, key, MODIFIED, obj, prev), False
+            return (await self._commit(ri, key, MODIFIED, obj, prev)), False
         om["deletionGracePeriodSeconds"] = 0
         om.setdefault("deletionTimestamp", now_rfc3339())
-        return self._commit(ri, key, DELETED, obj, prev), True
+        return (await self._commit(ri, key, DELETED, obj, prev)), True
 
-    def bind(self, namespace, name, binding, user=None):
+    async def bind(self, namespace, name, binding, user=None):
         """POST pods/{name}/binding (fork F6) with the duplicate-device guard."""
         ri = m.BY_PLURAL["pods"]
         key, prev = self._existing(ri, namespace, name)
@@ -368,15 +574,16 @@ class APIServer:
             pod["status"]["conditions"] = list(pod["status"]["conditions"])
         apply_binding(pod, binding)
         node = pod["spec"]["nodeName"]
-        idx = self.node_devices.get(node) or {}
-        for rn, ids in core.pod_assigned_devices(pod).items():
-            for i in ids:
-                owner = idx.get((rn, i))
-                if owner is not None and owner != key:
-                    raise APIError(409, "Conflict", f"device {rn}/{i} on node {node} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
-        return self._commit(ri, key, MODIFIED, pod, prev)
+        if self.store is not None:   # shared mode: the store enforces this with device claim keys
+            idx = self.node_devices.get(node) or {}
+            for rn, ids in core.pod_assigned_devices(pod).items():
+                for i in ids:
+                    owner = idx.get((rn, i))
+                    if owner is not None and owner != key:
+                        raise APIError(409, "Conflict", f"device {node}/{rn}/{i} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
+        return await self._commit(ri, key, MODIFIED, pod, prev)
 
-    def evict(self, namespace, name, eviction, user=None):
+    async def evict(self, namespace, name, eviction, user=None):
         ri = m.BY_PLURAL["pods"]
         # PodDisruptionBudget check
         pod = self.get_object("pods", namespace, name)
@@ -390,15 +597,20 @@ class APIServer:
                 allowed = (pdb.get("status") or {}).get("disruptionsAllowed", (pdb.get("status") or {}).get("podDisruptionsAllowed", 0))
                 if allowed <= 0:
                     raise APIError(429, "TooManyRequests", "Cannot evict pod as it would violate the pod's disruption budget.")
-        return self.delete(ri, namespace, name, (eviction or {}).get("deleteOptions") or {}, user)
+        return await self.delete(ri, namespace, name, (eviction or {}).get("deleteOptions") or {}, user)
 
     # ------------------------------------------------------------------
     # HTTP
-    async def start(self, host="127.0.0.1", port=0):
-        return await self.http.start(host, port)
+    async def start(self, host="127.0.0.1", port=0, reuse_port=False):
+        if self.remote_address and self.rstore is None:
+            await self._start_remote()
+        return await self.http.start(host, port, reuse_port=reuse_port)
 
     async def stop(self):
         await self.http.stop()
+        if self.rstore is not None:
+            self.store_healthy = False   # a deliberate close, not a store failure
+            await self.rstore.close()
 
     def _parse_path(self, path):
         """Returns (ri, namespace, name, subresource, watch) or a discovery/special marker."""
@@ -485,7 +697,7 @@ class APIServer:
                 resource, sub = "pods", "binding"
                 body = codec.loads(req.body)
                 self._authorize(user, "create", parsed[1], "pods", "binding", m.name_of(body), "", p)
-                self.bind(parsed[1], m.name_of(body), body, user)
+                await self._retrying(lambda: self.bind(parsed[1], m.name_of(body), body, user))
                 code = 201
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             ri, ns, name, sub, watch = parsed
@@ -513,7 +725,26 @@ class APIServer:
                 else:
                     self.inflight += 1
             try:
-                resp = await self._dispatch(req, ri, ns, name, sub, is_watch, user)
+                if self.rstore is not None and mutating:
+                    # writes to one object through THIS worker queue up instead of racing on
+                    # compare-and-swap; cross-worker races are resolved by _retrying
+                    lock = None
+                    if name is not None:
+                        lk = (ri.plural, ns, name)
+                        lock = self._key_locks.get(lk)
+                        if lock is None:
+                            lock = self._key_locks[lk] = asyncio.Lock()
+                    try:
+                        if lock is not None:
+                            async with lock:
+                                resp = await self._retrying(lambda: self._dispatch(req, ri, ns, name, sub, is_watch, user))
+                        else:
+                            resp = await self._retrying(lambda: self._dispatch(req, ri, ns, name, sub, is_watch, user))
+                    finally:
+                        if lock is not None and not lock.locked() and not lock._waiters:
+                            self._key_locks.pop(lk, None)
+                else:
+                    resp = await self._dispatch(req, ri, ns, name, sub, is_watch, user)
             finally:
                 if not is_watch:
                     if mutating:
@@ -566,11 +797,11 @@ class APIServer:
         if method == "POST":
             if name is not None and sub == "binding" and ri.plural == "pods":
                 self._authorize(user, "create", ns, "pods", "binding", name, "", req.path)
-                self.bind(ns, name, codec.loads(body), user)
+                await self.bind(ns, name, codec.loads(body), user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None and sub == "eviction" and ri.plural == "pods":
                 self._authorize(user, "create", ns, "pods", "eviction", name, "", req.path)
-                self.evict(ns, name, codec.loads(body) if body else {}, user)
+                await self.evict(ns, name, codec.loads(body) if body else {}, user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None:
                 raise APIError(405, "MethodNotAllowed", "POST to a named resource is not allowed")
@@ -578,22 +809,22 @@ class APIServer:
             obj = codec.loads(body)
             if ri.namespaced and ns is None:
                 ns = (obj.get("metadata") or {}).get("namespace") or "default"
-            e = self.create(ri, ns, obj, user)
+            e = await self.create(ri, ns, obj, user)
             return Response(201, e.raw)
         if name is None:
             if method == "DELETE":
-                return self._delete_collection(req, ri, ns, user)
+                return await self._delete_collection(req, ri, ns, user)
             raise APIError(405, "MethodNotAllowed", f"{method} requires a name")
         if method == "PUT":
             if ri.plural == "namespaces" and sub == "finalize":
                 self._authorize(user, "update", None, "namespaces", "finalize", name, "", req.path)
-                return self._finalize_namespace(name, codec.loads(body), user)
+                return await self._finalize_namespace(name, codec.loads(body), user)
             self._authorize(user, "update", ns, ri.plural, sub, name, ri.group, req.path)
-            e = self.update(ri, ns, name, codec.loads(body), user, sub)
+            e = await self.update(ri, ns, name, codec.loads(body), user, sub)
             return Response(200, e.raw)
         if method == "PATCH":
             self._authorize(user, "patch", ns, ri.plural, sub, name, ri.group, req.path)
-            e = self.patch(ri, ns, name, req.headers.get("content-type", "application/merge-patch+json"), body, user, sub)
+            e = await self.patch(ri, ns, name, req.headers.get("content-type", "application/merge-patch+json"), body, user, sub)
             return Response(200, e.raw)
         if method == "DELETE":
             self._authorize(user, "delete", ns, ri.plural, "", name, ri.group, req.path)
@@ -602,22 +833,22 @@ class APIServer:
                 opts["gracePeriodSeconds"] = int(q["gracePeriodSeconds"])
             if "propagationPolicy" in q:
                 opts["propagationPolicy"] = q["propagationPolicy"]
-            e, _ = self.delete(ri, ns, name, opts, user)
+            e, _ = await self.delete(ri, ns, name, opts, user)
             return Response(200, e.raw)
         raise APIError(405, "MethodNotAllowed", f"method {method} not allowed")
 
-    def _finalize_namespace(self, name, obj, user):
+    async def _finalize_namespace(self, name, obj, user):
         ri = m.BY_PLURAL["namespaces"]
         key, prev = self._existing(ri, None, name)
         new = fast_copy(prev.obj)
         new.setdefault("spec", {})["finalizers"] = list((obj.get("spec") or {}).get("finalizers") or [])
         if new["metadata"].get("deletionTimestamp") and not new["spec"]["finalizers"] and not new["metadata"].get("finalizers"):
-            e = self._commit(ri, key, DELETED, new, prev)
+            e = await self._commit(ri, key, DELETED, new, prev)
         else:
-            e = self._commit(ri, key, MODIFIED, new, prev)
+            e = await self._commit(ri, key, MODIFIED, new, prev)
         return Response(200, e.raw)
 
-    def _delete_collection(self, req, ri, ns, user):
+    async def _delete_collection(self, req, ri, ns, user):
         self._authorize(user, "deletecollection", ns, ri.plural, "", "", ri.group, req.path)
         ls = parse_labels(req.query.get("labelSelector")) if req.query.get("labelSelector") else None
         fs = parse_field_selector(req.query.get("fieldSelector")) if req.query.get("fieldSelector") else None
@@ -625,13 +856,13 @@ class APIServer:
         items = []
         for e in self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs):
             try:
-                d, _ = self.delete(ri, m.namespace_of(e.obj) or None, m.name_of(e.obj), opts, user)
+                d, _ = await self.delete(ri, m.namespace_of(e.obj) or None, m.name_of(e.obj), opts, user)
                 items.append(d.obj)
             except APIError as err:
                 if err.code != 404:
                     raise
         return _json(200, {"kind": ri.list_kind, "apiVersion": ri.group_version,
-                           "metadata": {"resourceVersion": str(self.store.revision)}, "items": items})
+                           "metadata": {"resourceVersion": str(self.revision)}, "items": items})
 
     def _list(self, req, ri, ns):
         q = req.query
@@ -640,7 +871,7 @@ class APIServer:
         entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
         limit = int(q.get("limit") or 0)
         cont = q.get("continue")
-        rv = str(self.store.revision)
+        rv = str(self.revision)
         next_token = None
         if cont:
             try:

@@ -1,7 +1,24 @@
-"""kube-apiserver entry point (reference: cmd/kube-apiserver/app/server.go:102-132)."""
+"""kube-apiserver entry point (reference: cmd/kube-apiserver/app/server.go:102-132).
+
+    python -m kubernetes_amd.cmd.apiserver --port 8080                  # one process, embedded store
+    python -m kubernetes_amd.cmd.apiserver --port 8080 --workers 4      # kamd-etcd + 4 worker processes
+    python -m kubernetes_amd.cmd.apiserver --etcd-servers unix:///run/kamd-etcd.sock   # join a store
+
+With `--workers N` (N > 1) this process becomes a supervisor: it starts the native store
+(`kamd-etcd`, optionally with a WAL) and N API server worker processes that all listen on the
+same port (SO_REUSEPORT — the kernel spreads client connections over them), the way several
+kube-apiserver replicas sit in front of one etcd. If any child dies, the supervisor stops all
+of them and exits non-zero.
+"""
 from __future__ import annotations
 
 import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
 
 from ..api import codec
 from ..apiserver.server import APIServer
@@ -9,7 +26,7 @@ from ..storage.mvcc import MVCCStore
 from ._common import run_until_signal, setup_logging, write_port_file
 
 
-def main(argv=None):
+def _parser():
     ap = argparse.ArgumentParser("kube-apiserver")
     ap.add_argument("--bind-address", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8080)
@@ -19,17 +36,90 @@ def main(argv=None):
     ap.add_argument("--token-auth-file", default=None)
     ap.add_argument("--storage-media-type", default=codec.JSON)
     ap.add_argument("--storage-engine", default="native", choices=["native", "python"])
-    ap.add_argument("--etcd-wal", default=None, help="durable WAL path for the embedded store")
+    ap.add_argument("--etcd-wal", default=None, help="durable WAL path for the store")
+    ap.add_argument("--etcd-servers", default=None, help="shared native store address (unix://PATH or tcp://HOST:PORT)")
+    ap.add_argument("--workers", type=int, default=1, help="API server worker processes sharing one native store")
+    ap.add_argument("--reuse-port", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--max-requests-inflight", type=int, default=4000)
     ap.add_argument("--max-mutating-requests-inflight", type=int, default=2000)
     ap.add_argument("--watch-cache-size", type=int, default=200000)
     ap.add_argument("-v", type=int, default=0)
-    a = ap.parse_args(argv)
+    return ap
+
+
+def _free_port(host):
+    s = socket.socket()
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    s.bind((host, 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def supervise(a):
+    from ..storage.remote import StoreServer
+    store = StoreServer(wal=a.etcd_wal)
+    addr = store.start()
+    port = a.port or _free_port(a.bind_address)
+    base = [sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--bind-address", a.bind_address,
+            "--port", str(port), "--reuse-port", "--etcd-servers", addr,
+            "--authorization-mode", a.authorization_mode, "--storage-media-type", a.storage_media_type,
+            "--max-requests-inflight", str(a.max_requests_inflight),
+            "--max-mutating-requests-inflight", str(a.max_mutating_requests_inflight),
+            "--watch-cache-size", str(a.watch_cache_size), "-v", str(a.v)]
+    if a.admission_control:
+        base += ["--admission-control", a.admission_control]
+    if a.token_auth_file:
+        base += ["--token-auth-file", a.token_auth_file]
+    ready_dir = store.dir or os.path.dirname(store.socket_path)
+    children = []
+    stopping = []
+
+    def _stop(*_):
+        stopping.append(1)
+    signal.signal(signal.SIGTERM, _stop)
+    signal.signal(signal.SIGINT, _stop)
+    rc = 0
+    try:
+        for i in range(a.workers):
+            pf = os.path.join(ready_dir, f"worker{i}.port")
+            children.append((subprocess.Popen(base + ["--port-file", pf]), pf))
+        t0 = time.time()
+        while not all(os.path.exists(pf) for _, pf in children):
+            if any(p.poll() is not None for p, _ in children) or time.time() - t0 > 120 or stopping:
+                raise RuntimeError("API server workers failed to start")
+            time.sleep(0.02)
+        write_port_file(a.port_file, port)
+        print(f"kube-apiserver: {a.workers} workers on http://{a.bind_address}:{port}, store {addr}", flush=True)
+        while not stopping:
+            dead = [p for p, _ in children if p.poll() is not None]
+            if dead or store.proc.poll() is not None:
+                print("kube-apiserver: a worker or the store exited; shutting down", file=sys.stderr, flush=True)
+                rc = 1
+                break
+            time.sleep(0.2)
+    finally:
+        for p, _ in children:
+            if p.poll() is None:
+                p.terminate()
+        for p, _ in children:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        store.stop()
+    return rc
+
+
+def main(argv=None):
+    a = _parser().parse_args(argv)
     setup_logging(a.v)
+    if a.workers > 1 and not a.etcd_servers:
+        sys.exit(supervise(a))
 
     async def start():
-        store = None
-        if a.storage_engine == "native":
+        store = a.etcd_servers
+        if store is None and a.storage_engine == "native":
             try:
                 from ..storage.native_store import NativeMVCCStore
                 store = NativeMVCCStore(wal_path=a.etcd_wal)
@@ -42,9 +132,10 @@ def main(argv=None):
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
                       max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size)
-        port = await s.start(a.bind_address, a.port)
+        port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
-        print(f"kube-apiserver listening on http://{a.bind_address}:{port}", flush=True)
+        if not a.reuse_port:
+            print(f"kube-apiserver listening on http://{a.bind_address}:{port}", flush=True)
         return s
 
     run_until_signal(start)

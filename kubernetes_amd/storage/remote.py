@@ -65,6 +65,7 @@ class RemoteStore:
         self._next = 1
         self._pending: dict[int, asyncio.Future] = {}
         self._watches: dict[int, callable] = {}
+        self._on_ok: dict[int, callable] = {}
         self.closed = False
 
     async def connect(self):
@@ -96,6 +97,11 @@ class RemoteStore:
                 kv, _ = wire.decode_kv(payload, 1)
                 cb(t, kv)
             return
+        cb = self._on_ok.pop(rid, None) if self._on_ok else None
+        if cb is not None and st == wire.OK:
+            # synchronous commit hook: runs before any later frame (e.g. the watch event of this
+            # very commit) is processed
+            cb(struct.unpack_from("<q", payload)[0])
         fut = self._pending.pop(rid, None)
         if fut is not None and not fut.done():
             fut.set_result((st, payload))
@@ -114,8 +120,11 @@ class RemoteStore:
         self._watches.clear()
 
     # -- API ----------------------------------------------------------------
-    async def txn(self, cmps, ops) -> TxnResult:
-        _, fut = self._send(wire.TXN, wire.encode_txn(cmps, ops))
+    async def txn(self, cmps, ops, on_ok=None) -> TxnResult:
+        """on_ok(rev) is called synchronously when the commit reply arrives."""
+        rid, fut = self._send(wire.TXN, wire.encode_txn(cmps, ops))
+        if on_ok is not None:
+            self._on_ok[rid] = on_ok
         st, p = await fut
         if st == wire.OK:
             return TxnResult(True, struct.unpack_from("<q", p)[0])

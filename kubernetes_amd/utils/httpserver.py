@@ -216,10 +216,12 @@ class HTTPServer:
         self._conns = set()
         self.port = None
 
-    async def start(self, host="127.0.0.1", port=0, ssl=None):
+    async def start(self, host="127.0.0.1", port=0, ssl=None, reuse_port=False):
+        """reuse_port: several worker processes listen on one port; the kernel spreads
+        incoming connections across them (SO_REUSEPORT)."""
         loop = asyncio.get_running_loop()
         self._server = await loop.create_server(lambda: _Conn(self), host, port, ssl=ssl, backlog=4096,
-                                                reuse_address=True)
+                                                reuse_address=True, reuse_port=reuse_port or None)
         self.port = self._server.sockets[0].getsockname()[1]
         return self.port
 

@@ -1,0 +1,169 @@
+"""Several API server workers sharing one native store (kamd-etcd): cross-worker visibility,
+watch ordering, CAS retries on stale caches, and the cross-worker GPU double-assignment guard."""
+import asyncio
+
+import pytest
+
+from kubernetes_amd.apiserver.server import APIServer
+from kubernetes_amd.client.rest import APIStatusError, Client
+from kubernetes_amd.storage.remote import StoreServer
+
+
+def gpu_pod(name, n=1):
+    return {"metadata": {"name": name, "namespace": "default"},
+            "spec": {"containers": [{"name": "c", "image": "x", "resources": {"limits": {"amd.com/gpu": str(n)}}}]}}
+
+
+@pytest.fixture
+def store():
+    s = StoreServer()
+    addr = s.start()
+    yield addr
+    s.stop()
+
+
+async def _workers(addr, n=2):
+    servers, clients = [], []
+    for _ in range(n):
+        s = APIServer(store=addr)
+        port = await s.start()
+        servers.append(s)
+        clients.append(Client(f"http://127.0.0.1:{port}"))
+    return servers, clients
+
+
+async def _close(servers, clients):
+    for c in clients:
+        await c.close()
+    for s in servers:
+        await s.stop()
+
+
+async def _eventually(fn, timeout=5.0):
+    t = asyncio.get_running_loop().time() + timeout
+    while True:
+        try:
+            r = await fn()
+            if r:
+                return r
+        except APIStatusError:
+            pass
+        if asyncio.get_running_loop().time() > t:
+            raise AssertionError("condition not met")
+        await asyncio.sleep(0.01)
+
+
+def test_cross_worker_crud_and_watch(run, store):
+    async def main():
+        servers, (a, b) = await _workers(store)
+        try:
+            # bootstrap raced between workers: namespaces exist exactly once
+            nss = (await a.list("namespaces"))["items"]
+            assert sorted(n["metadata"]["name"] for n in nss) == ["default", "kube-public", "kube-system"]
+            events = []
+            w = await b.watch("pods", "default", "0")
+
+            async def drain():
+                async for typ, obj in w:
+                    events.append((typ, obj["metadata"]["name"], obj["metadata"]["resourceVersion"]))
+            t = asyncio.ensure_future(drain())
+            p = await a.create("pods", gpu_pod("p1"))
+            assert p["metadata"]["resourceVersion"].isdigit()
+            got = await _eventually(lambda: b.get("pods", "p1", "default"))
+            assert got == p                              # byte-identical object via the other worker
+            await b.patch("pods", "p1", {"metadata": {"labels": {"x": "1"}}}, "default")
+            await a.delete("pods", "p1", "default")
+            await _eventually(lambda: asyncio.sleep(0, len(events) >= 3))
+            assert [e[0] for e in events] == ["ADDED", "MODIFIED", "DELETED"]
+            revs = [int(e[2]) for e in events]
+            assert revs == sorted(revs)
+            t.cancel()
+        finally:
+            await _close(servers, [a, b])
+    run(main())
+
+
+def test_concurrent_patches_retry_on_stale_cache(run, store):
+    async def main():
+        servers, (a, b) = await _workers(store)
+        try:
+            await a.create("configmaps", {"metadata": {"name": "cm", "namespace": "default"}, "data": {}})
+            await _eventually(lambda: b.get("configmaps", "cm", "default"))
+            # 40 merge patches of distinct keys racing through both workers: none may be lost
+            await asyncio.gather(*((a if i % 2 else b).patch("configmaps", "cm", {"data": {f"k{i}": str(i)}}, "default")
+                                   for i in range(40)))
+            cm = await _eventually(lambda: a.get("configmaps", "cm", "default"))
+            final = await _eventually(lambda: _if(a.get("configmaps", "cm", "default"), lambda o: len(o["data"]) == 40))
+            assert final["data"] == {f"k{i}": str(i) for i in range(40)} and cm
+            # a PUT with a stale resourceVersion is still a 409
+            stale = dict(final, metadata=dict(final["metadata"], resourceVersion="3"))
+            with pytest.raises(APIStatusError) as ei:
+                await b.update("configmaps", stale)
+            assert ei.value.code == 409
+        finally:
+            await _close(servers, [a, b])
+    run(main())
+
+
+async def _if(coro, pred):
+    o = await coro
+    return o if pred(o) else None
+
+
+def test_device_claims_across_workers(run, store):
+    async def main():
+        servers, (a, b) = await _workers(store)
+        try:
+            await a.create("nodes", {"metadata": {"name": "n0"}})
+            pa = await a.create("pods", gpu_pod("pa"))
+            pb = await a.create("pods", gpu_pod("pb"))
+            await _eventually(lambda: b.get("pods", "pb", "default"))
+            era, erb = pa["spec"]["extendedResources"][0]["name"], pb["spec"]["extendedResources"][0]["name"]
+            # two binds of the SAME GPU racing through different workers: exactly one wins
+            res = await asyncio.gather(a.bind("default", "pa", "n0", {era: {"resources": ["GPU-0"]}}),
+                                       b.bind("default", "pb", "n0", {erb: {"resources": ["GPU-0"]}}),
+                                       return_exceptions=True)
+            errs = [r for r in res if isinstance(r, Exception)]
+            assert len(errs) == 1 and isinstance(errs[0], APIStatusError) and errs[0].code == 409
+            assert "already assigned" in str(errs[0])
+            winner = "pa" if not isinstance(res[0], Exception) else "pb"
+            loser = "pb" if winner == "pa" else "pa"
+            lerr = erb if loser == "pb" else era
+            # deleting the winner releases the claim (grace 0), then the loser can bind it
+            await a.delete("pods", winner, "default", grace_period=0)
+            await _eventually(lambda: _absent(b, winner))
+            await b.bind("default", loser, "n0", {lerr: {"resources": ["GPU-0"]}})
+            p = await _eventually(lambda: _if(a.get("pods", loser, "default"), lambda o: o["spec"].get("nodeName")))
+            assert p["spec"]["extendedResources"][0]["assigned"] == ["GPU-0"]
+            # a terminal pod releases its devices too
+            await a.patch("pods", loser, {"status": {"phase": "Succeeded"}}, "default", "merge", "status")
+            pc = await a.create("pods", gpu_pod("pc"))
+            await _eventually(lambda: b.get("pods", "pc", "default"))
+            await b.bind("default", "pc", "n0", {pc["spec"]["extendedResources"][0]["name"]: {"resources": ["GPU-0"]}})
+        finally:
+            await _close(servers, [a, b])
+    run(main())
+
+
+async def _absent(c, name):
+    try:
+        await c.get("pods", name, "default")
+        return False
+    except APIStatusError as e:
+        return e.code == 404
+
+
+def test_worker_restart_reloads_state(run, store):
+    async def main():
+        servers, (a,) = await _workers(store, 1)
+        await a.create("pods", gpu_pod("keep"))
+        await _close(servers, [a])
+        servers, (b,) = await _workers(store, 1)
+        try:
+            p = await b.get("pods", "keep", "default")
+            assert p["metadata"]["name"] == "keep"
+            lst = await b.list("pods", "default")
+            assert int(lst["metadata"]["resourceVersion"]) >= int(p["metadata"]["resourceVersion"])
+        finally:
+            await _close(servers, [b])
+    run(main())
