@@ -43,15 +43,39 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_budget():
+    """CPUs this job may use: affinity mask capped by the cgroup v2 quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def control_plane_shape(world, workers=0, shards=0):
+    """API server workers and scheduler shards for `world` ranks (0 = auto). Each rank (hollow
+    kubelets + density client) needs about one core; the control plane gets what is left, and
+    parallel processes only pay off when they have cores of their own."""
+    spare = cpu_budget() - world - 1
+    if workers <= 0:
+        workers = max(1, min(4, spare // 6))
+    if shards <= 0:
+        shards = max(1, min(4, spare // 6))
+    return workers, shards
+
+
 def spawn_control_plane(tmp, args):
     env = dict(os.environ)
     env["PYTHONPATH"] = HERE + os.pathsep + env.get("PYTHONPATH", "")
     env.pop("HIP_VISIBLE_DEVICES", None)
     pf = os.path.join(tmp, "apiserver.port")
-    workers = args.apiserver_workers
-    if workers <= 0:   # auto: one worker per 2 ranks, up to 4 (each rank adds ~1 core of API load)
-        workers = min(4, max(1, int(os.environ.get("WORLD_SIZE", "1")) // 2))
-    args.apiserver_workers = workers
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    workers, shards = control_plane_shape(world, args.apiserver_workers, args.scheduler_shards)
+    args.apiserver_workers, args.scheduler_shards = workers, shards
     api = subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf,
                             "--storage-engine", args.storage_engine, "--workers", str(workers)],
                            env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "apiserver.log"), "w"))
@@ -64,7 +88,8 @@ def spawn_control_plane(tmp, args):
         time.sleep(0.05)
     url = f"http://127.0.0.1:{open(pf).read().strip()}"
     sched = subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.scheduler", "--master", url,
-                              "--percentage-of-nodes-to-score", str(args.percentage_of_nodes_to_score)]
+                              "--percentage-of-nodes-to-score", str(args.percentage_of_nodes_to_score),
+                              "--shards", str(shards)]
                              + (["--no-events"] if args.no_events else []),
                              env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "scheduler.log"), "w"))
     return url, [api, sched]
@@ -112,7 +137,29 @@ class Dist:
         return out
 
 
-async def rank_main(args, d: Dist, url):
+def _cp_cpu(procs):
+    """CPU seconds (user+sys) used so far by the control-plane processes, by component."""
+    out = {}
+    if not procs:
+        return out
+    import psutil
+    for name, pid in procs:
+        try:
+            ps = [psutil.Process(pid)]
+            ps += ps[0].children(recursive=True)
+        except psutil.NoSuchProcess:
+            continue
+        for p in ps:
+            try:
+                t = p.cpu_times()
+                comp = "store" if p.name() == "kamd-etcd" else name
+            except psutil.NoSuchProcess:
+                continue
+            out[comp] = out.get(comp, 0.0) + t.user + t.system
+    return out
+
+
+async def rank_main(args, d: Dist, url, cp_procs=()):
     from kubernetes_amd.client.rest import Client
     from kubernetes_amd.kubemark.density import DensityRunner, interval_rates, pct
     from kubernetes_amd.kubemark.hollow import HollowCluster
@@ -154,6 +201,8 @@ async def rank_main(args, d: Dist, url):
         await abarrier()
     results = []
     await abarrier()
+    cp0 = _cp_cpu(cp_procs)
+    my0 = time.process_time()
     t0 = time.perf_counter()
     for k in range(args.steps):
         results.append(await runner.step(k))
@@ -161,6 +210,8 @@ async def rank_main(args, d: Dist, url):
             await abarrier()
     await abarrier()
     elapsed = time.perf_counter() - t0
+    my_cpu = time.process_time() - my0
+    cp1 = _cp_cpu(cp_procs)
     lat = [x for r in results for x in r["latencies"]]
     sched_times = []
     off = 0.0
@@ -171,7 +222,8 @@ async def rank_main(args, d: Dist, url):
              "to_running": [r["to_running_s"] for r in results], "cycle": [r["cycle_s"] for r in results],
              "payload_runs": sum(getattr(k.runtime, "payload_runs", 0) for k in hollow.nodes),
              "payload_failures": sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes),
-             "sched_rates": interval_rates(sched_times)}
+             "sched_rates": interval_rates(sched_times), "cpu_s": my_cpu,
+             "cp_cpu_s": {k: cp1.get(k, 0.0) - cp0.get(k, 0.0) for k in cp1}}
     allstats = await loop.run_in_executor(None, d.allgather, stats)
     await runner.stop()
     # keep serving other ranks' pods until everyone is done
@@ -196,7 +248,9 @@ def main():
     ap.add_argument("--storage-engine", default="native", choices=["native", "python"])
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--apiserver-workers", type=int, default=0,
-                    help="API server processes over one native store (0 = auto by world size)")
+                    help="API server processes over one native store (0 = auto from the CPU budget)")
+    ap.add_argument("--scheduler-shards", type=int, default=0,
+                    help="parallel scheduler shard processes (0 = auto from the CPU budget)")
     args = ap.parse_args()
     d = Dist()
     tmp = tempfile.mkdtemp(prefix="kamd-bench-")
@@ -206,16 +260,17 @@ def main():
         if d.rank == 0:
             url, procs = spawn_control_plane(tmp, args)   # before any GPU init
         d.init()
-        url, d.broadcast_done_workers = d.broadcast((url, args.apiserver_workers))
+        url, d.broadcast_done_workers, d.shards = d.broadcast((url, args.apiserver_workers, args.scheduler_shards))
+        cp = [("apiserver", procs[0].pid), ("scheduler", procs[1].pid)] if procs else []
         if os.environ.get("KAMD_PROFILE_DIR"):
             import cProfile
             pr = cProfile.Profile()
             pr.enable()
-            allstats = asyncio.run(rank_main(args, d, url))
+            allstats = asyncio.run(rank_main(args, d, url, cp))
             pr.disable()
             pr.dump_stats(os.path.join(os.environ["KAMD_PROFILE_DIR"], f"rank{d.rank}.prof"))
         else:
-            allstats = asyncio.run(rank_main(args, d, url))
+            allstats = asyncio.run(rank_main(args, d, url, cp))
     finally:
         for p in procs:
             p.terminate()
@@ -241,7 +296,8 @@ def main():
         "config": {"model": "kubemark-density/8xMI355X-hollow-nodes/1-GPU-pods", "global_batch": pods // args.steps,
                    "seq_len": None, "parallelism": f"ranks{n}", "hollow_nodes": n * args.nodes_per_rank,
                    "gpus_per_node": args.gpus_per_node, "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
-                   "gpus_per_pod": args.gpus_per_pod, "apiserver_workers": d.broadcast_done_workers},
+                   "gpus_per_pod": args.gpus_per_pod, "apiserver_workers": d.broadcast_done_workers,
+                   "scheduler_shards": d.shards},
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
         "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
         "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],
@@ -249,6 +305,11 @@ def main():
         "vs_scheduler_perf_warn_threshold": round(value / BASELINE_SCHED_WARN_PODS_PER_S, 2),
         "payload_runs": sum(s["payload_runs"] for s in allstats),
         "payload_failures": sum(s["payload_failures"] for s in allstats),
+        # where the host CPU goes (timed region): ms of CPU per pod, by component
+        "cpu_ms_per_pod": {k: round(v * 1000 / max(pods, 1), 3) for k, v in
+                           dict(sum_ranks=sum(s["cpu_s"] for s in allstats),
+                                **{c: sum(s["cp_cpu_s"].get(c, 0.0) for s in allstats)
+                                   for c in ("apiserver", "scheduler", "store")}).items()},
     }
     print(json.dumps(out), flush=True)
 

@@ -23,11 +23,26 @@ ADDED, MODIFIED, DELETED, BOOKMARK, ERROR = "ADDED", "MODIFIED", "DELETED", "BOO
 
 
 class Entry:
-    __slots__ = ("obj", "raw", "rev", "fields", "labels")
+    """One cached object version. `obj` may be decoded lazily: an API server worker that only
+    relays another worker's write needs the raw bytes (GET/LIST/watch payload) and the index
+    fields/labels (watch + list filtering) — not the decoded object."""
+    __slots__ = ("_obj", "raw", "rev", "fields", "labels")
 
-    def __init__(self, obj, raw, rev, fields):
-        self.obj, self.raw, self.rev, self.fields = obj, raw, rev, fields
-        self.labels = (obj.get("metadata") or {}).get("labels") or {}
+    def __init__(self, obj, raw, rev, fields, labels=None):
+        self._obj, self.raw, self.rev, self.fields = obj, raw, rev, fields
+        self.labels = labels if obj is None else ((obj.get("metadata") or {}).get("labels") or {})
+
+    @property
+    def obj(self):
+        o = self._obj
+        if o is None:
+            o = self._obj = codec.loads(self.raw)
+        return o
+
+    @property
+    def sort_key(self):
+        f = self.fields
+        return f.get("metadata.namespace", "") + "/" + f.get("metadata.name", "")
 
 
 class GoneError(Exception):
@@ -163,7 +178,7 @@ class ResourceCache:
             if field_sel is not None and not field_sel.matches(e.fields):
                 continue
             out.append(e)
-        out.sort(key=lambda e: e.obj["metadata"].get("namespace", "") + "/" + e.obj["metadata"]["name"])
+        out.sort(key=lambda e: e.sort_key)
         return out
 
     # -- writes -----------------------------------------------------------

@@ -41,7 +41,7 @@ from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
 from . import admission as adm
 from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, build_authorizer
-from .cacher import ADDED, DELETED, MODIFIED, GoneError, ResourceCache
+from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache
 from .registry import (APIError, already_exists, apply_binding, bad_request, conflict, deletion_stamp,
                        init_object_meta, invalid, not_found, strategy_for)
 
@@ -80,6 +80,7 @@ def _run_sync(coro):
 
 
 DEVICE_PREFIX = "/kamd/devices/"   # claim keys, outside /registry/ so watch caches never see them
+_FRAME = b"\x00KH"                 # shared-store value framing (index header + object)
 
 
 class APIServer:
@@ -190,6 +191,8 @@ class APIServer:
 
     def _decode_value(self, kv):
         v = kv.value
+        if v[:3] == _FRAME:
+            v = v[7 + int.from_bytes(v[3:7], "little"):]
         if v[:4] == codec.MAGIC:
             obj = self.storage_codec.decode(v)
             obj.setdefault("metadata", {})["resourceVersion"] = str(kv.mod_rev)
@@ -203,8 +206,16 @@ class APIServer:
             return
         entry = self._mine.pop((kv.key, kv.mod_rev), None)
         if entry is None:
-            obj, raw = self._decode_value(kv)
-            entry = cache.make_entry(obj, raw, kv.mod_rev)
+            v = kv.value
+            if v[:3] == _FRAME:
+                # another worker's write: keep the bytes, decode only the small index header;
+                # the object itself is decoded on first use (Entry.obj)
+                hl = int.from_bytes(v[3:7], "little")
+                fields, labels = codec.loads(v[7:7 + hl])
+                entry = Entry(None, v[7 + hl:], kv.mod_rev, fields, labels)
+            else:
+                obj, raw = self._decode_value(kv)
+                entry = cache.make_entry(obj, raw, kv.mod_rev)
         prev = cache.by_key.get(kv.key)
         if not dispatch:
             cache.by_key[kv.key] = entry
@@ -274,11 +285,15 @@ class APIServer:
     async def _commit_remote(self, ri, key, etype, obj, prev):
         md = obj["metadata"]
         tok = self._rv_token
+        cache = self.caches[ri.plural]
         json_storage = self.storage_codec.media_type == codec.JSON
+        # value framing: [00 'K' 'H' | u32 len | index header (fields, labels) | object]
+        hdr = codec.dumpb([cache.fields_fn(obj), md.get("labels") or {}])
+        frame = _FRAME + len(hdr).to_bytes(4, "little") + hdr
         if json_storage:
             md["resourceVersion"] = tok.decode()
             raw_t = codec.dumpb(obj)
-            stored = raw_t
+            stored = frame + raw_t
         else:
             md.pop("resourceVersion", None)
             raw_t = None
@@ -286,7 +301,7 @@ class APIServer:
         cmps = [(wire.CMP_MOD_REV, key, prev.rev if prev is not None else 0, None)]
         if etype == DELETED:
             tomb = raw_t if raw_t is not None else codec.dumpb(dict(obj, metadata=dict(md, resourceVersion=tok.decode())))
-            ops = [(wire.OP_DELETE_TOMBSTONE, key, tomb, tok)]
+            ops = [(wire.OP_DELETE_TOMBSTONE, key, frame + tomb, tok)]
         elif json_storage:
             ops = [(wire.OP_PUT_INJECT, key, stored, tok)]
         else:
@@ -880,10 +895,10 @@ class APIServer:
                 rv = tok.get("rv", rv)
             except Exception:
                 raise bad_request("continue key is not valid")
-            entries = [e for e in entries if m.ns_name(e.obj) > start]
+            entries = [e for e in entries if e.sort_key > start]
         if limit and len(entries) > limit:
             entries = entries[:limit]
-            next_token = base64.urlsafe_b64encode(codec.dumpb({"rv": rv, "start": m.ns_name(entries[-1].obj)})).decode()
+            next_token = base64.urlsafe_b64encode(codec.dumpb({"rv": rv, "start": entries[-1].sort_key})).decode()
         md = '"resourceVersion":"%s"' % rv
         if next_token:
             md += ',"continue":"%s"' % next_token

@@ -1,16 +1,29 @@
-"""kube-scheduler entry point (reference: plugin/cmd/kube-scheduler/app/server.go:320-552)."""
+"""kube-scheduler entry point (reference: plugin/cmd/kube-scheduler/app/server.go:320-552).
+
+    python -m kubernetes_amd.cmd.scheduler --master URL                 # one scheduler
+    python -m kubernetes_amd.cmd.scheduler --master URL --shards 4      # 4 parallel shards
+
+`--shards N` makes this process a supervisor of N scheduler processes (`--shard-index i
+--shard-count N`), each owning a hash partition of the pods and preferring a hash partition of
+the nodes; bind conflicts between shards are resolved by the API server's device-claim guard
+(see `kubernetes_amd/scheduler/scheduler.py`).
+"""
 from __future__ import annotations
 
 import argparse
 import asyncio
 import json
+import signal
+import subprocess
+import sys
+import time
 
 from ..client.rest import Client
 from ..scheduler.scheduler import Scheduler
 from ._common import run_until_signal, setup_logging
 
 
-def main(argv=None):
+def _parser():
     ap = argparse.ArgumentParser("kube-scheduler")
     ap.add_argument("--master", required=True)
     ap.add_argument("--scheduler-name", default="default-scheduler")
@@ -20,9 +33,49 @@ def main(argv=None):
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--kube-api-qps", type=float, default=None)
     ap.add_argument("--leader-elect", action="store_true")
+    ap.add_argument("--shards", type=int, default=1, help="run N parallel scheduler shard processes")
+    ap.add_argument("--shard-index", type=int, default=0)
+    ap.add_argument("--shard-count", type=int, default=1)
     ap.add_argument("-v", type=int, default=0)
-    a = ap.parse_args(argv)
+    return ap
+
+
+def supervise(argv, n):
+    """Run n shard processes; stop all when one exits or on SIGTERM/SIGINT."""
+    base = [a for a in argv if not a.startswith("--shards")]
+    if "--shards" in argv:
+        i = argv.index("--shards")
+        base = argv[:i] + argv[i + 2:]
+    stopping = []
+    signal.signal(signal.SIGTERM, lambda *_: stopping.append(1))
+    signal.signal(signal.SIGINT, lambda *_: stopping.append(1))
+    procs = [subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.scheduler", *base,
+                               "--shard-index", str(i), "--shard-count", str(n)]) for i in range(n)]
+    rc = 0
+    try:
+        while not stopping:
+            if any(p.poll() is not None for p in procs):
+                rc = 1
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return rc
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = _parser().parse_args(argv)
     setup_logging(a.v)
+    if a.shards > 1:
+        sys.exit(supervise(argv, a.shards))
     preds = prios = None
     if a.policy_config_file:
         with open(a.policy_config_file) as f:
@@ -34,10 +87,11 @@ def main(argv=None):
     async def start():
         client = Client(a.master, qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
-                      emit_events=not a.no_events)
+                      emit_events=not a.no_events, shard_index=a.shard_index, shard_count=a.shard_count)
         if a.leader_elect:
             from ..client.leaderelection import LeaderElector
-            le = LeaderElector(client, "kube-system", "kube-scheduler")
+            lock = "kube-scheduler" if a.shard_count == 1 else f"kube-scheduler-shard-{a.shard_index}"
+            le = LeaderElector(client, "kube-system", lock)
             await le.acquire()
         asyncio.ensure_future(s.run(metrics_port=a.metrics_port))
         return s

@@ -132,6 +132,7 @@ class GenericScheduler:
         self.ecache_classes = ecache_classes
         self.ecache_hits = 0
         self.ecache_misses = 0
+        self.prefer = None   # node name -> bool: a scheduler shard's own nodes win among feasible ones
 
     def num_feasible_to_find(self, n):
         if self.pct >= 100 or n < 100:
@@ -242,6 +243,11 @@ class GenericScheduler:
             fnodes = [f for f in fnodes if f.name in keepset]
         if not fnodes:
             raise FitError(pod, n, failed)
+        if self.prefer is not None and len(fnodes) > 1:
+            own = [i for i, ni in enumerate(fnodes) if self.prefer(ni.name)]
+            if own and len(own) < len(fnodes):
+                fnodes = [fnodes[i] for i in own]
+                raws = [raws[i] for i in own]
         if len(fnodes) == 1:
             host = fnodes[0].name
         else:

@@ -39,6 +39,7 @@ class SchedulingQueue:
         self.unschedulable: dict[str, tuple] = {}
         self.nominated: dict[str, str] = {}     # pod key -> node
         self.backoff = PodBackoff()
+        self.conflict_backoff = PodBackoff(0.005, 0.5)   # lost bind races between scheduler shards
         self._ev = asyncio.Event()
         self._timers = {}
         self.unschedulable_flush = unschedulable_flush
@@ -84,6 +85,7 @@ class SchedulingQueue:
         self.nominated.pop(key, None)
         self._cancel_timer(key)
         self.backoff.forget(key)
+        self.conflict_backoff.forget(key)
 
     def add_unschedulable(self, pod):
         key = ns_name(pod)
@@ -91,10 +93,11 @@ class SchedulingQueue:
             return
         self.unschedulable[key] = (pod, None, time.monotonic())
 
-    def add_backoff(self, pod):
-        """Re-queue after the pod's backoff (binding errors, API errors)."""
+    def add_backoff(self, pod, conflict=False):
+        """Re-queue after the pod's backoff (binding errors, API errors; `conflict`: a bind lost
+        to another scheduler shard — short backoff, the winner's binding is already in flight)."""
         key = ns_name(pod)
-        d = self.backoff.next(key)
+        d = (self.conflict_backoff if conflict else self.backoff).next(key)
         self._cancel_timer(key)
         loop = asyncio.get_event_loop()
         self._timers[key] = loop.call_later(d, self._timer_fire, key, pod)

@@ -7,6 +7,14 @@ Parity: `plugin/pkg/scheduler/scheduler.go:170-497` (`Run`, `scheduleOne`, `sche
 `Target.ExtendedResources` (`scheduler.go:481-492`, `factory.go:1241-1244`), events
 `Scheduled` / `FailedScheduling` and the metrics of `plugin/pkg/scheduler/metrics/metrics.go:33-50`.
 
+Scale-out (MI355X clusters with many nodes): `shard_count > 1` runs several scheduler
+processes in parallel with optimistic concurrency (Omega-style shared state). Each shard owns
+the pods whose `namespace/name` hashes to it, keeps the FULL cluster view from the informers,
+and prefers the nodes that hash to it, so shards rarely compete for one node. When two shards
+still pick the same GPU, the API server's device-claim guard rejects the second bind (409);
+that shard forgets its assumption and retries after a short conflict backoff, by which time
+the winner's binding has reached its cache.
+
 Fix: `assume()` writes the device binding into the assumed pod's
 `spec.extendedResources[].assigned` before `AssumePod`, so the cache reserves those devices
 immediately and the next pod in the same burst cannot receive them.
@@ -16,6 +24,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import time
+import zlib
 
 from ..api import core
 from ..api.meta import fast_copy, ns_name, now_rfc3339
@@ -36,12 +45,16 @@ DEFAULT_SCHEDULER = "default-scheduler"
 class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
-                 update_unschedulable_status=True):
+                 update_unschedulable_status=True, shard_index=0, shard_count=1):
         self.client = client
         self.name = scheduler_name
         self.cache = SchedulerCache()
         self.queue = SchedulingQueue()
         self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
+        self.shard_index, self.shard_count = shard_index, shard_count
+        if shard_count > 1:
+            self.algo.prefer = lambda node: shard_of(node, shard_count) == shard_index
+        self.conflicts = 0
         self.recorder = EventRecorder(client, scheduler_name, enabled=emit_events)
         self.update_unschedulable_status = update_unschedulable_status
         self.metrics = Registry()
@@ -62,7 +75,12 @@ class Scheduler:
 
     # -- informer handlers -------------------------------------------------
     def _responsible(self, pod):
-        return (pod.get("spec") or {}).get("schedulerName", DEFAULT_SCHEDULER) == self.name
+        if (pod.get("spec") or {}).get("schedulerName", DEFAULT_SCHEDULER) != self.name:
+            return False
+        if self.shard_count > 1:
+            md = pod["metadata"]
+            return shard_of(f"{md.get('namespace', '')}/{md['name']}", self.shard_count) == self.shard_index
+        return True
 
     def _on_pod_add(self, pod):
         if (pod.get("spec") or {}).get("nodeName"):
@@ -175,6 +193,11 @@ class Scheduler:
             except (APIStatusError, ConnectionError, OSError, asyncio.TimeoutError) as e:
                 self.cache.forget_pod(assumed)
                 self.m_attempts.labels("error").inc()
+                if isinstance(e, APIStatusError) and e.code == 409 and "already assigned" in str(e):
+                    # lost a device race to another scheduler shard: retry soon, no event spam
+                    self.conflicts += 1
+                    self.queue.add_backoff(pod, conflict=True)
+                    return
                 self.recorder.event(pod, "Warning", "FailedScheduling", f"Binding rejected: {e}")
                 if not (isinstance(e, APIStatusError) and is_not_found(e)):
                     self.queue.add_backoff(pod)
@@ -186,6 +209,7 @@ class Scheduler:
         self.m_attempts.labels("scheduled").inc()
         self.scheduled += 1
         self.queue.backoff.forget(ns_name(pod))
+        self.queue.conflict_backoff.forget(ns_name(pod))
         self.recorder.event(pod, "Normal", "Scheduled", f"Successfully assigned {md['name']} to {host}")
 
     async def _set_unschedulable(self, pod, msg):
@@ -221,6 +245,10 @@ class Scheduler:
     async def wait_binds(self):
         while self._binds:
             await asyncio.gather(*list(self._binds), return_exceptions=True)
+
+
+def shard_of(key: str, count: int) -> int:
+    return zlib.crc32(key.encode()) % count
 
 
 def _node_capacity_changed(old, new):
