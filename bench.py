@@ -197,7 +197,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     await runner.start()
     await abarrier()
     for w in range(args.warmup):
-        await runner.step(f"w{w}")
+        await runner.step(f"w{w}", timeout=args.step_timeout)
         await abarrier()
     results = []
     await abarrier()
@@ -205,7 +205,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     my0 = time.process_time()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        results.append(await runner.step(k))
+        results.append(await runner.step(k, timeout=args.step_timeout))
         if k + 1 < args.steps:
             await abarrier()
     await abarrier()
@@ -249,6 +249,7 @@ def main():
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--apiserver-workers", type=int, default=0,
                     help="API server processes over one native store (0 = auto from the CPU budget)")
+    ap.add_argument("--step-timeout", type=float, default=120.0, help="fail (with diagnostics) if a step stalls")
     ap.add_argument("--scheduler-shards", type=int, default=0,
                     help="parallel scheduler shard processes (0 = auto from the CPU budget)")
     args = ap.parse_args()

@@ -90,10 +90,13 @@ FIELD_FUNCS = {"pods": pod_fields, "nodes": node_fields}
 
 class Watcher:
     __slots__ = ("writer", "namespace", "label_sel", "field_sel", "closed", "index_value", "cache", "bookmarks",
-                 "_pending", "_loop")
+                 "_pending", "_loop", "min_rev")
 
     def __init__(self, cache, writer, namespace, label_sel, field_sel, index_value):
         self.cache = cache
+        # events at or below this revision are already reflected in what the client has (its
+        # list came from a worker that was further ahead than this one): never re-send them
+        self.min_rev = 0
         self.writer = writer
         self.namespace = namespace
         self.label_sel = label_sel
@@ -215,8 +218,9 @@ class ResourceCache:
             targets |= self._unindexed
         else:
             targets = self.watchers
+        rev = entry.rev
         for w in list(targets):
-            if w.closed:
+            if w.closed or rev <= w.min_rev:
                 continue
             cur = etype != DELETED and w.matches(entry)
             was = prev is not None and w.matches(prev)
@@ -240,6 +244,8 @@ class ResourceCache:
         fs = parse_field_selector(field_selector) if field_selector else None
         idx = fs.requires("spec.nodeName") if (fs is not None and self.resource == "pods") else None
         w = Watcher(self, writer, namespace, ls, fs, idx)
+        if from_rev is not None and not send_initial:
+            w.min_rev = from_rev
         # initial state / replay (synchronous, so no event can interleave)
         if send_initial:
             for e in self.by_key.values():

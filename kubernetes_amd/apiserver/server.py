@@ -69,6 +69,14 @@ class _Stale(Exception):
         self.rev = rev
 
 
+class _Missing(Exception):
+    """Shared-store cache miss: the object may exist in the store already (this worker lags)."""
+
+    def __init__(self, key, error):
+        super().__init__(key)
+        self.key, self.error = key, error
+
+
 def _run_sync(coro):
     """Drive a coroutine that never suspends (embedded-store commit path) to completion."""
     try:
@@ -124,6 +132,9 @@ class APIServer:
         self.m_watchers = self.metrics.gauge("apiserver_registered_watchers", "Number of watchers", ("kind",))
         self.m_inflight = self.metrics.gauge("apiserver_current_inflight_requests", "In-flight requests", ("requestKind",))
         self.m_dropped = self.metrics.counter("apiserver_dropped_requests", "Requests dropped with 429", ("requestKind",))
+        self.m_retries = self.metrics.counter("apiserver_shared_store_retries_total",
+                                              "Requests re-run because this worker's cache lagged the shared store",
+                                              ("reason",))
         self.metrics.register_collector(self._collect)
         if self.store is not None:
             self._load_from_store()
@@ -264,14 +275,25 @@ class APIServer:
             raise APIError(504, "Timeout", f"timed out waiting for revision {rev} to be observed")
 
     async def _retrying(self, op, attempts=64):
-        """Re-run an operation whose compare failed on a stale cache (shared mode)."""
+        """Re-run an operation whose compare failed on a stale cache, or which missed an object
+        this worker has not seen yet (shared mode)."""
         for i in range(attempts):
             try:
                 return await op()
             except _Stale as e:
+                self.m_retries.labels("stale").inc()
                 if i == attempts - 1:
                     raise APIError(409, "Conflict", "the object has been modified concurrently; please retry")
                 await self._wait_applied(e.rev)
+            except _Missing as e:
+                self.m_retries.labels("miss").inc()
+                kv = await self.rstore.get(e.key)
+                if kv is None or i == attempts - 1:
+                    raise e.error
+                await self._wait_applied(kv.mod_rev)
+
+    async def _async_existing(self, ri, namespace, name):
+        return self._existing(ri, namespace, name)
 
     @staticmethod
     def _device_keys(pod):
@@ -438,6 +460,8 @@ class APIServer:
         key = m.key_for(ri, namespace, name)
         e = self.caches[ri.plural].get(key)
         if e is None:
+            if self.rstore is not None:
+                raise _Missing(key, not_found(ri, name))
             raise not_found(ri, name)
         return key, e
 
@@ -601,9 +625,7 @@ class APIServer:
     async def evict(self, namespace, name, eviction, user=None):
         ri = m.BY_PLURAL["pods"]
         # PodDisruptionBudget check
-        pod = self.get_object("pods", namespace, name)
-        if pod is None:
-            raise not_found(ri, name)
+        pod = self._existing(ri, namespace, name)[1].obj
         labels = (pod.get("metadata") or {}).get("labels") or {}
         from ..api.labels import label_selector_as_selector
         for pdb in self.list_objects("poddisruptionbudgets", namespace):
@@ -805,6 +827,9 @@ class APIServer:
             self._authorize(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
             key = m.key_for(ri, ns, name)
             e = self.caches[ri.plural].get(key)
+            if e is None and self.rstore is not None:
+                # shared mode: a miss may only mean this worker lags the writer — ask the store
+                _, e = await self._retrying(lambda: self._async_existing(ri, ns, name))
             if e is None:
                 raise not_found(ri, name)
             return Response(200, e.raw)

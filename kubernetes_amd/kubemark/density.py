@@ -11,6 +11,7 @@ Metric definitions follow the reference:
 from __future__ import annotations
 
 import asyncio
+import collections
 import time
 
 from ..api import core
@@ -76,12 +77,27 @@ class DensityRunner:
                     self.running[name] = now
             self._changed.set()
 
-    async def _wait(self, pred, timeout):
+    async def _diagnose(self, names, phase):
+        """What the pods that never reached `phase` look like (for the timeout error)."""
+        missing = [n for n in names if n not in (self.running if phase == "running" else self.gone)]
+        out = collections.Counter()
+        for n in missing[:50]:
+            try:
+                p = await self.client.get("pods", n, self.ns)
+                st = (p.get("status") or {})
+                out[(st.get("phase"), bool((p.get("spec") or {}).get("nodeName")),
+                     bool(p["metadata"].get("deletionTimestamp")))] += 1
+            except APIStatusError as e:
+                out[("http", e.code)] += 1
+        return f"{len(missing)} pods not {phase}; sample (phase, bound, deleting): {dict(out)}; " \
+               f"watch alive: {self._watch_task is not None and not self._watch_task.done()}"
+
+    async def _wait(self, pred, timeout, names=(), phase=""):
         end = time.monotonic() + timeout
         while not pred():
             left = end - time.monotonic()
             if left <= 0:
-                raise TimeoutError("density step timed out")
+                raise TimeoutError("density step timed out: " + await self._diagnose(names, phase))
             self._changed.clear()
             try:
                 await asyncio.wait_for(self._changed.wait(), min(left, 1.0))
@@ -101,7 +117,7 @@ class DensityRunner:
 
         await asyncio.gather(*(create(n) for n in names))
         t_created = time.monotonic()
-        await self._wait(lambda: all(n in self.running for n in names), timeout)
+        await self._wait(lambda: all(n in self.running for n in names), timeout, names, "running")
         t_running = time.monotonic()
 
         async def delete(n):
@@ -113,7 +129,7 @@ class DensityRunner:
                         raise
 
         await asyncio.gather(*(delete(n) for n in names))
-        await self._wait(lambda: all(n in self.gone for n in names), timeout)
+        await self._wait(lambda: all(n in self.gone for n in names), timeout, names, "gone")
         t_gone = time.monotonic()
         lat = [self.running[n] - self.created[n] for n in names]
         sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)

@@ -145,6 +145,68 @@ def test_device_claims_across_workers(run, store):
     run(main())
 
 
+def test_read_and_bind_right_after_write_on_other_worker(run, store):
+    """A worker that has not yet applied another worker's write must not answer 404 for it."""
+    async def main():
+        servers, (a, b) = await _workers(store)
+        # make worker b lag: its store events are applied 30 ms late (in order)
+        rs = servers[1].rstore
+        wid = next(iter(rs._watches))
+        orig, backlog = rs._watches[wid], []
+        loop = asyncio.get_running_loop()
+
+        def late(t, kv):
+            backlog.append((t, kv))
+            loop.call_later(0.03, lambda: orig(*backlog.pop(0)))
+        rs._watches[wid] = late
+        try:
+            await a.create("nodes", {"metadata": {"name": "n0"}})
+            for i in range(10):
+                p = await a.create("pods", gpu_pod(f"q{i}"))
+                got = await b.get("pods", f"q{i}", "default")          # no polling
+                assert got["metadata"]["uid"] == p["metadata"]["uid"]
+                er = p["spec"]["extendedResources"][0]["name"]
+                p2 = await a.create("pods", gpu_pod(f"r{i}"))
+                await b.bind("default", f"r{i}", "n0", {p2["spec"]["extendedResources"][0]["name"]: {"resources": [f"G{i}"]}})
+                assert er
+            assert servers[1].m_retries.value("miss") >= 10     # the lag path really ran
+        finally:
+            await _close(servers, [a, b])
+    run(main())
+
+
+def test_watch_from_newer_list_on_lagging_worker(run, store):
+    """List on a worker that is ahead, watch on one that lags: no replay of what the list had."""
+    async def main():
+        servers, (a, b) = await _workers(store)
+        rs = servers[1].rstore
+        wid = next(iter(rs._watches))
+        orig, backlog = rs._watches[wid], []
+        loop = asyncio.get_running_loop()
+
+        def late(t, kv):
+            backlog.append((t, kv))
+            loop.call_later(0.1, lambda: orig(*backlog.pop(0)))
+        rs._watches[wid] = late
+        try:
+            await a.create("configmaps", {"metadata": {"name": "old", "namespace": "default"}})
+            lst = await a.list("configmaps", "default")
+            w = await b.watch("configmaps", "default", lst["metadata"]["resourceVersion"])
+            seen = []
+
+            async def drain():
+                async for typ, obj in w:
+                    seen.append((typ, obj["metadata"]["name"]))
+            t = asyncio.ensure_future(drain())
+            await a.create("configmaps", {"metadata": {"name": "new", "namespace": "default"}})
+            await asyncio.sleep(0.4)
+            assert seen == [("ADDED", "new")]
+            t.cancel()
+        finally:
+            await _close(servers, [a, b])
+    run(main())
+
+
 async def _absent(c, name):
     try:
         await c.get("pods", name, "default")
