@@ -43,6 +43,17 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _xgmi4_summary(allstats):
+    from kubernetes_amd.kubemark.density import pct
+    xs = [s["xgmi4"] for s in allstats if "xgmi4" in s]
+    if not xs:
+        return {}
+    lat = [x for s in xs for x in s["lat"]]
+    return {"xgmi4_pods_per_s": round(sum(s["pods"] for s in xs) / max(max(s["t"] for s in xs), 1e-9), 2),
+            "xgmi4_p50_startup_ms": round(pct(lat, 0.5) * 1000, 2),
+            "xgmi4_single_hive_fraction": round(sum(s["single_hive"] for s in xs) / max(1, sum(s["total"] for s in xs)), 4)}
+
+
 def cpu_budget():
     """CPUs this job may use: affinity mask capped by the cgroup v2 quota."""
     n = len(os.sched_getaffinity(0))
@@ -57,14 +68,18 @@ def cpu_budget():
 
 
 def control_plane_shape(world, workers=0, shards=0):
-    """API server workers and scheduler shards for `world` ranks (0 = auto). Each rank (hollow
-    kubelets + density client) needs about one core; the control plane gets what is left, and
-    parallel processes only pay off when they have cores of their own."""
-    spare = cpu_budget() - world - 1
+    """API server workers and scheduler shards for `world` ranks (0 = auto).
+
+    Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep): with one rank the single API
+    server + scheduler are fastest; from 2 ranks on, parallel API server workers over the
+    native store and 2 scheduler shards win, up to 4 workers once ranks use most cores.
+    More cores (a whole 8-GPU node) allow 4 shards as well."""
+    cpus = cpu_budget()
+    spare = cpus - world - 1
     if workers <= 0:
-        workers = max(1, min(4, spare // 6))
+        workers = 1 if world == 1 or spare < 3 else (2 if world <= 4 else 4)
     if shards <= 0:
-        shards = max(1, min(4, spare // 6))
+        shards = 1 if world == 1 or spare < 3 else (4 if cpus >= 64 else 2)
     return workers, shards
 
 
@@ -224,8 +239,37 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
              "payload_failures": sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes),
              "sched_rates": interval_rates(sched_times), "cpu_s": my_cpu,
              "cp_cpu_s": {k: cp1.get(k, 0.0) - cp0.get(k, 0.0) for k in cp1}}
-    allstats = await loop.run_in_executor(None, d.allgather, stats)
     await runner.stop()
+    # secondary workload (outside the timed region, not part of `value`): 4-GPU pods that must
+    # land on one fully connected xGMI hive (BASELINE: "4-GPU xGMI-hive workload")
+    if args.xgmi4_steps and args.gpus_per_node >= 4:
+        await abarrier()
+        r4 = DensityRunner(url, d.rank, namespace="density-xgmi4",
+                           pods_per_step=args.nodes_per_rank * args.gpus_per_node // 4, gpus_per_pod=4,
+                           annotations={"amd.com/xgmi-policy": "required"})
+        await r4.start()
+        x_lat, x_pods, x_t = [], 0, 0.0
+        c = Client(url)
+        hive = {}
+        for n in (await c.list("nodes"))["items"]:
+            for rn, dom in ((n.get("status") or {}).get("extendedResources") or {}).items():
+                for i, dev in ((dom or {}).get("resources") or {}).items():
+                    hive[(n["metadata"]["name"], i)] = (dev.get("attributes") or {}).get("amd.com/xgmi-hive", "")
+        await c.close()
+        single = total = 0
+        for k in range(args.xgmi4_steps):
+            await abarrier()
+            r = await r4.step(f"x{k}", timeout=args.step_timeout)
+            x_lat += r["latencies"]
+            x_pods += r["pods"]
+            x_t += r["cycle_s"]
+            for name in r["names"]:
+                node, ids = r4.assigned.get(name, (None, []))
+                total += 1
+                single += len(ids) == 4 and len({hive.get((node, i)) for i in ids}) == 1
+        await r4.stop()
+        stats["xgmi4"] = {"lat": x_lat, "pods": x_pods, "t": x_t, "single_hive": single, "total": total}
+    allstats = await loop.run_in_executor(None, d.allgather, stats)
     # keep serving other ranks' pods until everyone is done
     await abarrier()
     await hollow.stop()
@@ -249,6 +293,8 @@ def main():
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--apiserver-workers", type=int, default=0,
                     help="API server processes over one native store (0 = auto from the CPU budget)")
+    ap.add_argument("--xgmi4-steps", type=int, default=2,
+                    help="untimed secondary steps of 4-GPU xGMI-hive pods (0 = skip)")
     ap.add_argument("--step-timeout", type=float, default=120.0, help="fail (with diagnostics) if a step stalls")
     ap.add_argument("--scheduler-shards", type=int, default=0,
                     help="parallel scheduler shard processes (0 = auto from the CPU budget)")
@@ -306,6 +352,7 @@ def main():
         "vs_scheduler_perf_warn_threshold": round(value / BASELINE_SCHED_WARN_PODS_PER_S, 2),
         "payload_runs": sum(s["payload_runs"] for s in allstats),
         "payload_failures": sum(s["payload_failures"] for s in allstats),
+        **_xgmi4_summary(allstats),
         # where the host CPU goes (timed region): ms of CPU per pod, by component
         "cpu_ms_per_pod": {k: round(v * 1000 / max(pods, 1), 3) for k, v in
                            dict(sum_ranks=sum(s["cpu_s"] for s in allstats),

@@ -37,7 +37,8 @@ def pct(vals, q):
 
 
 class DensityRunner:
-    def __init__(self, master, rank=0, namespace="density", pods_per_step=64, gpus_per_pod=1, concurrency=128):
+    def __init__(self, master, rank=0, namespace="density", pods_per_step=64, gpus_per_pod=1, concurrency=128,
+                 annotations=None):
         self.client = Client(master, max_conns=64)
         self.rank = rank
         self.ns = namespace
@@ -48,6 +49,8 @@ class DensityRunner:
         self.scheduled: dict[str, float] = {}
         self.running: dict[str, float] = {}
         self.gone: dict[str, float] = {}
+        self.assigned: dict[str, tuple] = {}     # pod -> (node, [device ids]) as observed Running
+        self.annotations = dict(annotations or {})
         self._watch_task = None
         self._stream = None
         self._changed = asyncio.Event()
@@ -75,6 +78,8 @@ class DensityRunner:
                     self.scheduled[name] = now
                 if (pod.get("status") or {}).get("phase") == core.POD_RUNNING and name not in self.running:
                     self.running[name] = now
+                    self.assigned[name] = (pod["spec"].get("nodeName"),
+                                           [i for ids in core.pod_assigned_devices(pod).values() for i in ids])
             self._changed.set()
 
     async def _diagnose(self, names, phase):
@@ -113,7 +118,8 @@ class DensityRunner:
         async def create(n):
             async with sem:
                 self.created[n] = time.monotonic()
-                await self.client.create("pods", gpu_pod(n, self.ns, labels, self.gpus_per_pod), self.ns)
+                await self.client.create("pods", gpu_pod(n, self.ns, labels, self.gpus_per_pod,
+                                                         annotations=self.annotations), self.ns)
 
         await asyncio.gather(*(create(n) for n in names))
         t_created = time.monotonic()
@@ -133,7 +139,7 @@ class DensityRunner:
         t_gone = time.monotonic()
         lat = [self.running[n] - self.created[n] for n in names]
         sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)
-        return {"pods": len(names), "create_s": t_created - t0, "to_running_s": t_running - t0,
+        return {"pods": len(names), "names": names, "create_s": t_created - t0, "to_running_s": t_running - t0,
                 "cycle_s": t_gone - t0, "latencies": lat, "scheduled_times": [s - t0 for s in sched]}
 
     async def stop(self):
