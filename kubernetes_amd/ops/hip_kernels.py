@@ -46,6 +46,7 @@ def load():
         L.kamd_payload_run.argtypes = [vp]
         L.kamd_payload_destroy.argtypes = [vp]
         L.kamd_hip_device_arch.argtypes = [i, ctypes.c_char_p, i]
+        L.kamd_gemm_set_path.argtypes = [i]
         _lib = L
     return _lib
 
@@ -92,6 +93,12 @@ def gemm_bf16_nt(a, b, out_fp32=True, alpha=1.0):
     _raise(load().kamd_gemm_bf16_nt_launch(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, N, float(alpha),
                                            1 if out_fp32 else 0, _stream(a)), "gemm_bf16_nt")
     return out
+
+
+def set_gemm_path(path: int):
+    """0 = auto (256x256 global_load_lds kernel when M, N % 256 == 0 and K % 64 == 0),
+    1 = always the 128x128 register-staged kernel (A/B comparisons, odd shapes)."""
+    load().kamd_gemm_set_path(int(path))
 
 
 def hbm_copy(src, dst):

@@ -23,6 +23,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 static thread_local char g_err[256];
+static int g_gemm_path = 0;   // 0 auto (256-tile glds path when the shape allows), 1 force the 128-tile kernel
 
 static int check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
@@ -172,6 +173,114 @@ gemm_bf16_nt_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* 
 }  // namespace gemm
 
 // ---------------------------------------------------------------------------
+// Large-tile path (M, N multiples of 256, K multiple of 64): 256x256x64 tiles, 8 waves (2 M x 4 N),
+// each wave a 128x64 output patch = 8x4 MFMA 16x16x32 tiles (128 accumulator VGPRs).
+// Operands are staged HBM -> LDS with global_load_lds (16 B / lane, no VGPR round trip) into two
+// LDS buffers (128 KiB, ONE __shared__ array): the loads for K-tile t+1 are in flight while the
+// MFMAs consume K-tile t. The LDS image is lane-linear per wave instruction, so the bank swizzle
+// is applied to the per-lane GLOBAL address: 16-B slot s of LDS row r holds k-chunk s ^ ((r>>1)&7),
+// which makes each 16-lane ds_read_b128 group (16 consecutive rows, same chunk) conflict-free.
+namespace gemm256 {
+using gemm::xcd_remap;
+using gemm::store_out;
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int TILE_BYTES = BM * BK * 2;        // one operand tile: 256 rows x 128 B
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // A | B
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;     // double buffered: 128 KiB
+constexpr int GLDS_PER_OPERAND = TILE_BYTES / (THREADS * 16);  // 4
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename OutT>
+__global__ void __launch_bounds__(THREADS, 1)
+gemm_bf16_nt_256_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
+                        int M, int N, int K, int ldc, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  // groups of 4 tile-rows walk the tile-columns together: B panels are re-read from L2
+  const int GROUP = 4;
+  const int group_id = t / (GROUP * tiles_n);
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (t % (GROUP * tiles_n)) % gsz;
+  const int tn = (t % (GROUP * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // per-thread global source offsets (elements) of its 4 A and 4 B staging chunks
+  size_t a_off[GLDS_PER_OPERAND], b_off[GLDS_PER_OPERAND];
+#pragma unroll
+  for (int j = 0; j < GLDS_PER_OPERAND; ++j) {
+    const int q = j * THREADS + tid;             // 16-B chunk index in the LDS image
+    const int row = q >> 3, slot = q & 7;
+    const int kc = slot ^ ((row >> 1) & 7);      // logical k-chunk stored in this slot
+    a_off[j] = (size_t)(m0 + row) * K + kc * 8;
+    b_off[j] = (size_t)(n0 + row) * K + kc * 8;
+  }
+  auto stage = [&](int buf, int kt) {
+    unsigned char* base = lds + buf * STAGE_BYTES + wid * 1024;   // wave-uniform; lane adds 16*lane
+    const size_t k0 = (size_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < GLDS_PER_OPERAND; ++j) {
+      __builtin_amdgcn_global_load_lds((const void*)(A + a_off[j] + k0), (lds_void*)(base + j * THREADS * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(B + b_off[j] + k0), (lds_void*)(base + TILE_BYTES + j * THREADS * 16), 16, 0, 0);
+    }
+  };
+
+  const int wr = wid >> 2, wc = wid & 3;         // wave's 128x64 patch
+  const int frow = lane & 15, fq = lane >> 4;
+  const int lsw = (frow >> 1) & 7;               // rows i*16+frow all have swizzle (frow>>1)&7
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) stage(cur ^ 1, kt + 1);
+    const unsigned char* la = lds + cur * STAGE_BYTES + (wr * 128 + frow) * 128;
+    const unsigned char* lb = lds + cur * STAGE_BYTES + TILE_BYTES + (wc * 64 + frow) * 128;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int off = ((ks * 4 + fq) ^ lsw) << 4;
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * 128 + off);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * 128 + off);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + frow;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
+        store_out<OutT>(C + (size_t)row * ldc + col, alpha * acc[i][j][r]);
+      }
+    }
+}
+}  // namespace gemm256
+
+// ---------------------------------------------------------------------------
 // HBM streaming copy, 16 B per lane, grid-stride
 __global__ void __launch_bounds__(256) hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -195,6 +304,8 @@ __global__ void fill_bf16_kernel(u16* p, size_t n, uint32_t seed, float scale) {
 extern "C" {
 
 const char* kamd_hip_last_error() { return g_err; }
+
+void kamd_gemm_set_path(int path) { g_gemm_path = path; }
 
 int kamd_hip_device_count() {
   int n = 0;
@@ -226,6 +337,24 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
   if ((((uintptr_t)A) | ((uintptr_t)B)) & 15) {
     snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
     return -1;
+  }
+  if (g_gemm_path != 1 && M % gemm256::BM == 0 && N % gemm256::BN == 0 && K % gemm256::BK == 0) {
+    static bool attr_set = false;
+    if (!attr_set) {   // > 64 KiB of dynamic LDS must be opted into per kernel
+      HC(hipFuncSetAttribute((const void*)gemm256::gemm_bf16_nt_256_kernel<float>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemm256::LDS_BYTES));
+      HC(hipFuncSetAttribute((const void*)gemm256::gemm_bf16_nt_256_kernel<__bf16>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemm256::LDS_BYTES));
+      attr_set = true;
+    }
+    const int tiles256 = (M / gemm256::BM) * (N / gemm256::BN);
+    if (out_fp32)
+      hipLaunchKernelGGL(gemm256::gemm_bf16_nt_256_kernel<float>, dim3(tiles256), dim3(gemm256::THREADS),
+                         gemm256::LDS_BYTES, stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+    else
+      hipLaunchKernelGGL(gemm256::gemm_bf16_nt_256_kernel<__bf16>, dim3(tiles256), dim3(gemm256::THREADS),
+                         gemm256::LDS_BYTES, stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+    return check(hipGetLastError(), "gemm256 launch");
   }
   const int tiles = ((M + gemm::BM - 1) / gemm::BM) * ((N + gemm::BN - 1) / gemm::BN);
   const size_t lds = 2 * 2 * gemm::TILE_BYTES;

@@ -77,3 +77,27 @@ def test_real_amdsmi_enumerates_mi355x():
     assert g.product in ("MI355X", "MI350X"), g
     assert g.vram_total_mb > 250_000, g
     assert os.path.exists(f"/dev/dri/renderD{g.render_minor}")
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1024), (2048, 1024, 4096)])
+def test_gemm_both_paths_match_reference(hk, M, N, K):
+    """The 256-tile glds kernel and the 128-tile kernel against an fp32 torch reference."""
+    torch.manual_seed(1)
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    ref = a.float() @ b.float().T
+    try:
+        for path in (0, 1):
+            hk.set_gemm_path(path)
+            out = hk.gemm_bf16_nt(a, b, out_fp32=True)
+            torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * (K ** 0.5))
+    finally:
+        hk.set_gemm_path(0)
+
+
+def test_gemm256_identity_asymmetric(hk):
+    n = 256
+    a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(n * n, device="cuda").reshape(n, n) % 7 - 3).to(torch.bfloat16)
+    torch.testing.assert_close(hk.gemm_bf16_nt(a, b), b.float().T, rtol=0, atol=0)
+    torch.testing.assert_close(hk.gemm_bf16_nt(b, a), b.float(), rtol=0, atol=0)
