@@ -47,6 +47,7 @@ def load():
         L.kamd_payload_destroy.argtypes = [vp]
         L.kamd_hip_device_arch.argtypes = [i, ctypes.c_char_p, i]
         L.kamd_gemm_set_path.argtypes = [i]
+        L.kamd_hbm_copy_config.argtypes = [i, i]
         _lib = L
     return _lib
 
@@ -99,6 +100,12 @@ def set_gemm_path(path: int):
     """0 = auto (256x256 global_load_lds kernel when M, N % 256 == 0 and K % 64 == 0),
     1 = always the 128x128 register-staged kernel (A/B comparisons, odd shapes)."""
     load().kamd_gemm_set_path(int(path))
+
+
+def hbm_copy_config(variant: int = 0, blocks: int = 0):
+    """variant 0: flat, one 16-B element per lane (default, ~6.2 TB/s); 1: grid-stride;
+    2: 4 non-temporal loads in flight per lane; 3: the same without the hints."""
+    load().kamd_hbm_copy_config(int(variant), int(blocks))
 
 
 def hbm_copy(src, dst):

@@ -288,6 +288,45 @@ __global__ void __launch_bounds__(256) hbm_copy_kernel(const uint4* __restrict__
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
+// 4 independent 16-B loads in flight per lane before the stores (64 B/lane/iteration), streaming
+// (non-temporal) hints so the copy does not sweep the L2 / Infinity Cache.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) hbm_copy_x4_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    u32x4 a = __builtin_nontemporal_load(src + i);
+    u32x4 b = __builtin_nontemporal_load(src + i + stride);
+    u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+    u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+    __builtin_nontemporal_store(a, dst + i);
+    __builtin_nontemporal_store(b, dst + i + stride);
+    __builtin_nontemporal_store(c, dst + i + 2 * stride);
+    __builtin_nontemporal_store(d, dst + i + 3 * stride);
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+// one 16-B element per lane, no loop: a grid of n/256 workgroups
+__global__ void __launch_bounds__(256) hbm_copy_flat_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+// x4 without the non-temporal hints
+__global__ void __launch_bounds__(256) hbm_copy_x4p_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    u32x4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+static int g_copy_variant = 0;   // 0: flat (one element per lane), 1: grid-stride, 2: x4 non-temporal, 3: x4 plain
+static int g_copy_blocks = 0;    // 0: default grid
+
 __global__ void fill_bf16_kernel(u16* p, size_t n, uint32_t seed, float scale) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -370,9 +409,25 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
 
 int kamd_hbm_copy_launch(const void* src, void* dst, size_t bytes, hipStream_t stream) {
   size_t n = bytes / 16;
-  int blocks = 256 * 8;
-  hipLaunchKernelGGL(hbm_copy_kernel, dim3(blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, n);
+  // measured on MI355X (profiles/r1_hbm): flat 6.2 TB/s, grid-stride loops 4.7-5.3 TB/s
+  if (g_copy_variant == 1) {
+    hipLaunchKernelGGL(hbm_copy_kernel, dim3(256 * 8), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, n);
+  } else if (g_copy_variant == 2) {
+    const int blocks = g_copy_blocks > 0 ? g_copy_blocks : 256 * 8;   // 8 WGs (32 waves) per CU
+    hipLaunchKernelGGL(hbm_copy_x4_kernel, dim3(blocks), dim3(256), 0, stream, (const u32x4*)src, (u32x4*)dst, n);
+  } else if (g_copy_variant == 3) {
+    const int blocks = g_copy_blocks > 0 ? g_copy_blocks : 256 * 8;
+    hipLaunchKernelGGL(hbm_copy_x4p_kernel, dim3(blocks), dim3(256), 0, stream, (const u32x4*)src, (u32x4*)dst, n);
+  } else {
+    hipLaunchKernelGGL(hbm_copy_flat_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const u32x4*)src,
+                       (u32x4*)dst, n);
+  }
   return check(hipGetLastError(), "hbm_copy launch");
+}
+
+void kamd_hbm_copy_config(int variant, int blocks) {
+  g_copy_variant = variant;
+  g_copy_blocks = blocks;
 }
 
 // --- self-contained diagnostics (allocate, run, verify, free) -------------
