@@ -95,7 +95,7 @@ class APIServer:
     def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
                  max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
-                 kubelet_port_resolver=None):
+                 kubelet_port_resolver=None, audit=None):
         self.remote_address = store if isinstance(store, str) else None
         self.rstore = None            # RemoteStore once started (shared mode)
         self.store = None if self.remote_address else (store or MVCCStore())
@@ -122,6 +122,8 @@ class APIServer:
         self.inflight_mut = 0
         self.http = HTTPServer(self.handle)
         self.kubelet_port_resolver = kubelet_port_resolver
+        self.audit = audit            # audit.AuditLogger or None
+        self.enable_profiling = True  # --profiling (reference default true)
         # fork fix: node -> {(resource, deviceID): pod key}
         self.node_devices: dict[str, dict[tuple, str]] = {}
         self.metrics = Registry()
@@ -709,6 +711,11 @@ class APIServer:
             if p == "/version":
                 code = 200
                 return _json(200, VERSION)
+            if p.startswith("/debug/pprof") and self.enable_profiling:
+                from ..utils.profiling import handle_debug
+                resp = await handle_debug(req)
+                code = resp.status
+                return resp
             user = ANONYMOUS
             if self.authn is not None:
                 user = self.authn.authenticate(req.headers)
@@ -804,7 +811,13 @@ class APIServer:
         finally:
             self.m_requests.labels(verb, resource, sub, code).inc()
             if resource:
-                self.m_latency.labels(verb, resource).observe(time.perf_counter() - t0)
+                dt = time.perf_counter() - t0
+                self.m_latency.labels(verb, resource).observe(dt)
+                if dt > 0.5 and verb != "GET":
+                    # utiltrace LogIfLong (registry/store.go: 500 ms) for slow mutating calls
+                    log.warning('Trace "%s %s" (code %s) total %.1f ms', verb, req.path, code, dt * 1e3)
+            if self.audit is not None and resource:
+                self.audit.log(req, verb, resource, sub, code)
 
     def _authorize(self, user, verb, ns, resource, sub, name, group, path):
         ok, why = self.authz.authorize(AttributesRecord(user, verb, ns or "", resource, sub, name or "", group, path))

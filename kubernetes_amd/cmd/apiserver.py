@@ -43,6 +43,8 @@ def _parser():
     ap.add_argument("--max-requests-inflight", type=int, default=4000)
     ap.add_argument("--max-mutating-requests-inflight", type=int, default=2000)
     ap.add_argument("--watch-cache-size", type=int, default=200000)
+    ap.add_argument("--audit-log-path", default=None, help="write audit events (JSON lines) here; '-' = stdout")
+    ap.add_argument("--audit-policy-file", default=None, help="audit policy YAML (rules: level/users/verbs/resources)")
     ap.add_argument("-v", type=int, default=0)
     return ap
 
@@ -83,7 +85,12 @@ def supervise(a):
     try:
         for i in range(a.workers):
             pf = os.path.join(ready_dir, f"worker{i}.port")
-            children.append((subprocess.Popen(base + ["--port-file", pf]), pf))
+            extra = []
+            if a.audit_log_path:   # one audit file per worker process (no interleaved writes)
+                extra += ["--audit-log-path", a.audit_log_path if a.audit_log_path == "-" else f"{a.audit_log_path}.w{i}"]
+                if a.audit_policy_file:
+                    extra += ["--audit-policy-file", a.audit_policy_file]
+            children.append((subprocess.Popen(base + extra + ["--port-file", pf]), pf))
         t0 = time.time()
         while not all(os.path.exists(pf) for _, pf in children):
             if any(p.poll() is not None for p, _ in children) or time.time() - t0 > 120 or stopping:
@@ -128,10 +135,15 @@ def main(argv=None):
         if store is None:
             store = MVCCStore(wal_path=a.etcd_wal)
         plugins = a.admission_control.split(",") if a.admission_control else None
+        audit = None
+        if a.audit_log_path:
+            from ..apiserver.audit import AuditLogger, Policy
+            audit = AuditLogger(a.audit_log_path, Policy.load(a.audit_policy_file) if a.audit_policy_file else None)
         s = APIServer(store=store, admission_plugins=plugins, token_file=a.token_auth_file,
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
-                      max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size)
+                      max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size,
+                      audit=audit)
         port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
         if not a.reuse_port:

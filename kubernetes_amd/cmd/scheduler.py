@@ -33,6 +33,7 @@ def _parser():
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--kube-api-qps", type=float, default=None)
     ap.add_argument("--leader-elect", action="store_true")
+    ap.add_argument("--disable-preemption", action="store_true")
     ap.add_argument("--shards", type=int, default=1, help="run N parallel scheduler shard processes")
     ap.add_argument("--shard-index", type=int, default=0)
     ap.add_argument("--shard-count", type=int, default=1)
@@ -77,17 +78,21 @@ def main(argv=None):
     if a.shards > 1:
         sys.exit(supervise(argv, a.shards))
     preds = prios = None
+    extenders = []
     if a.policy_config_file:
+        from ..scheduler.extender import HTTPExtender
         with open(a.policy_config_file) as f:
             pol = json.load(f)
         preds = [p["name"] for p in pol.get("predicates") or []] or None
         if pol.get("priorities") is not None:
             prios = {p["name"]: int(p.get("weight", 1)) for p in pol["priorities"]}
+        extenders = [HTTPExtender.from_config(e) for e in pol.get("extenders") or []]
 
     async def start():
         client = Client(a.master, qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
-                      emit_events=not a.no_events, shard_index=a.shard_index, shard_count=a.shard_count)
+                      emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,
+                      shard_count=a.shard_count, preemption=not a.disable_preemption)
         if a.leader_elect:
             from ..client.leaderelection import LeaderElector
             lock = "kube-scheduler" if a.shard_count == 1 else f"kube-scheduler-shard-{a.shard_index}"

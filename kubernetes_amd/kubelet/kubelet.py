@@ -589,6 +589,9 @@ class Kubelet:
         if p == "/stats/summary":
             from .stats import summary
             return Response(200, codec.dumpb(summary(self)))
+        if p.startswith("/debug/pprof"):
+            from ..utils.profiling import handle_debug
+            return await handle_debug(req)
         return Response(404, b"not found", "text/plain")
 
 

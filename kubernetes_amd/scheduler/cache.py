@@ -212,6 +212,19 @@ class NodeInfo:
         self.gpu_total = len(self.er.allocatable.get(core.AMD_GPU, {}))
         self.generation += 1
 
+    def clone(self):
+        """Independent copy for what-if evaluation (preemption)."""
+        c = NodeInfo(self.name)
+        for s in ("node", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
+                  "req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "generation", "ready", "unschedulable",
+                  "mem_pressure", "disk_pressure", "gpu_total"):
+            setattr(c, s, getattr(self, s))
+        c.req_scalars = dict(self.req_scalars)
+        c.pods = dict(self.pods)
+        c.ports = set(self.ports)
+        c.er = self.er.clone()
+        return c
+
     def add_pod(self, key, pod, pi: PodInfo):
         if key in self.pods:
             self.remove_pod(key)

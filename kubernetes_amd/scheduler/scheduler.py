@@ -33,6 +33,7 @@ from ..client.informer import Informer
 from ..client.rest import APIStatusError, is_not_found
 from ..utils.httpserver import HTTPServer, Response
 from ..utils.metrics import MICRO_BUCKETS, Registry
+from ..utils.trace import Trace
 from .cache import SchedulerCache
 from .generic import FitError, GenericScheduler
 from .queue import SchedulingQueue
@@ -45,7 +46,7 @@ DEFAULT_SCHEDULER = "default-scheduler"
 class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
-                 update_unschedulable_status=True, shard_index=0, shard_count=1):
+                 update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True):
         self.client = client
         self.name = scheduler_name
         self.cache = SchedulerCache()
@@ -65,6 +66,8 @@ class Scheduler:
         self.m_bind = self.metrics.histogram("scheduler_binding_latency_microseconds", "Binding latency", (), MICRO_BUCKETS)
         self.m_attempts = self.metrics.counter("scheduler_schedule_attempts_total", "Scheduling attempts", ("result",))
         self.m_pending = self.metrics.gauge("scheduler_pending_pods", "Pods in the scheduling queue", ("queue",))
+        self.m_preemptions = self.metrics.counter("scheduler_total_preemption_attempts", "Preemptions that evicted victims")
+        self.preemption = preemption
         self.scheduled = 0
         self.bind_sem = asyncio.Semaphore(max_binds_in_flight)
         self._tasks = []
@@ -151,15 +154,20 @@ class Scheduler:
             self.m_pending.labels("unschedulable").set(len(self.queue.unschedulable))
 
     def schedule_one(self, pod, pi):
-        t0 = time.perf_counter()
+        tr = Trace(f"Scheduling {ns_name(pod)}")
+        t0 = tr.start
         try:
             host, erb = self.algo.schedule(pod, pi)
+            tr.step(f"Computing predicates, device allocation and priorities -> {host}")
+            tr.log_if_long(0.1, log)
         except FitError as e:
             self.m_attempts.labels("unschedulable").inc()
             self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
             self.queue.add_unschedulable(pod)
             if self.update_unschedulable_status:
                 asyncio.ensure_future(self._set_unschedulable(pod, str(e)))
+            if self.preemption:
+                self._try_preempt(pod, pi)
             return None
         except Exception as e:  # pragma: no cover - defensive
             log.exception("scheduling %s failed", ns_name(pod))
@@ -212,6 +220,41 @@ class Scheduler:
         self.queue.conflict_backoff.forget(ns_name(pod))
         self.recorder.event(pod, "Normal", "Scheduled", f"Successfully assigned {md['name']} to {host}")
 
+    def _try_preempt(self, pod, pi):
+        """scheduler.go preempt(): pick a node + minimal lower-priority victims, nominate the
+        node on the preemptor and delete the victims; the preemptor is retried when the
+        victims' deletions free their resources (pod delete events re-activate the queue)."""
+        from .preemption import preempt
+        try:
+            node, victims = preempt(self.algo, pod, pi)
+        except Exception:  # pragma: no cover - defensive
+            log.exception("preemption for %s failed", ns_name(pod))
+            return
+        if node is None or not victims:
+            return
+        self.m_preemptions.inc()
+        md = pod["metadata"]
+        asyncio.ensure_future(self._nominate(pod, node))
+        for v in victims:
+            vmd = v["metadata"]
+            self.recorder.event(v, "Normal", "Preempted", f"by {md.get('namespace')}/{md['name']} on node {node}")
+            asyncio.ensure_future(self._delete_victim(vmd.get("namespace"), vmd["name"]))
+
+    async def _nominate(self, pod, node):
+        md = pod["metadata"]
+        try:
+            await self.client.patch("pods", md["name"], {"status": {"nominatedNodeName": node}}, md.get("namespace"),
+                                    "merge", "status")
+        except Exception as e:
+            log.debug("could not nominate %s: %s", md["name"], e)
+
+    async def _delete_victim(self, ns, name):
+        try:
+            await self.client.delete("pods", name, ns)
+        except APIStatusError as e:
+            if not is_not_found(e):
+                log.warning("deleting preemption victim %s/%s: %s", ns, name, e)
+
     async def _set_unschedulable(self, pod, msg):
         md = pod["metadata"]
         cond = {"type": core.COND_POD_SCHEDULED, "status": "False", "reason": "Unschedulable", "message": msg,
@@ -230,6 +273,9 @@ class Scheduler:
             return Response(200, self.metrics.render(), "text/plain; version=0.0.4")
         if req.path == "/healthz":
             return Response(200, b"ok", "text/plain")
+        if req.path.startswith("/debug/pprof"):
+            from ..utils.profiling import handle_debug
+            return await handle_debug(req)
         return Response(404, b"not found", "text/plain")
 
     async def stop(self):
