@@ -24,6 +24,8 @@ from __future__ import annotations
 import asyncio
 import itertools
 import logging
+import os
+import tempfile
 import time
 
 from ..api import core
@@ -35,7 +37,9 @@ from ..client.rest import APIStatusError, is_conflict, is_not_found
 from ..utils.httpserver import HTTPServer, Response
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from .devicemanager.manager import AdmitError, ManagerStub
+from .prober import ProbeManager
 from .runtime.base import EXITED, RUNNING, RunContainerOptions
+from .volumes import VolumeError, VolumeManager
 
 log = logging.getLogger("kubelet")
 
@@ -44,7 +48,7 @@ _ip_counter = itertools.count(2)
 
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
-                 "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen")
+                 "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes")
 
     def __init__(self, pod):
         self.uid = pod["metadata"]["uid"]
@@ -63,13 +67,18 @@ class PodState:
         self.last_status = None
         self.running_at = None
         self.first_seen = time.time()
+        self.volumes = None            # {volume name: host path} once mounted
 
 
 class Kubelet:
     def __init__(self, client, node_name, runtime, device_manager=None, cpu="128", memory="2Ti", pods=110,
                  labels=None, node_status_update_frequency=10.0, status_debounce=0.02, http_port=None,
-                 emit_events=True, register=True, metrics=None, address="127.0.0.1", max_status_inflight=64):
+                 emit_events=True, register=True, metrics=None, address="127.0.0.1", max_status_inflight=64,
+                 root_dir=None):
         self.client = client
+        self.root_dir = root_dir or os.path.join(tempfile.gettempdir(), f"kamd-kubelet-{node_name}")
+        self.volumes = VolumeManager(client, os.path.join(self.root_dir, "pods"))
+        self.probes = ProbeManager(runtime, self._on_readiness, self._on_liveness_failure)
         self.node_name = node_name
         self.runtime = runtime
         self.dm = device_manager or ManagerStub()
@@ -135,6 +144,7 @@ class Kubelet:
             t.cancel()
         for t in list(self._workers.values()):
             t.cancel()
+        self.probes.stop()
         await self.dm.stop()
         self.recorder.stop()
         if self.http:
@@ -298,7 +308,7 @@ class Kubelet:
         for k, v in need.items():
             if k in ("cpu", "memory") and k in self.capacity:
                 cap = parse_quantity(self.capacity[k])
-                if used.get(k, 0) + v > cap:
+                if (used[k] + v if k in used else v) > cap:
                     return f"OutOf{k}", f"Node didn't have enough resource: {k}"
         sel = (pod.get("spec") or {}).get("nodeSelector") or {}
         labels = {**self._node_object()["metadata"]["labels"]}
@@ -360,6 +370,18 @@ class Kubelet:
         pod = st.pod
         spec = pod.get("spec") or {}
         rt = self.runtime
+        if st.volumes is None:
+            if spec.get("volumes"):
+                try:
+                    st.volumes = await self.volumes.setup(pod, self.node_name, st.ip)
+                except (VolumeError, APIStatusError, OSError) as e:
+                    # volumemanager WaitForAttachAndMount: report, retry on the next sync
+                    self.recorder.event(pod, "Warning", "FailedMount", f"Unable to mount volumes for pod: {e}")
+                    await self._report(st)
+                    asyncio.get_running_loop().call_later(2.0, self._resync, st.uid)
+                    return
+            else:
+                st.volumes = {}
         if st.sandbox is None:
             ann = {}
             pr = self.dm.pod_resources(pod)
@@ -411,17 +433,56 @@ class Kubelet:
         except Exception as e:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: device plugin InitContainer failed: {e}")
             return None
+        spec_c = c
+        if c.get("volumeMounts") or c.get("envFrom") or any("valueFrom" in e or "$(" in str(e.get("value", ""))
+                                                             for e in c.get("env") or ()):
+            try:
+                spec_c = dict(c, env=await self.volumes.env_for(st.pod, c, self.node_name, st.ip), envFrom=[])
+                for m in self.volumes.mounts_for(c, st.volumes or {}):
+                    opts.mounts.append(m)
+                for m in c.get("volumeMounts") or ():
+                    opts.envs.append({"name": "KUBERNETES_VOLUME_" + m["name"].upper().replace("-", "_"),
+                                      "value": (st.volumes or {}).get(m["name"], "")})
+            except (VolumeError, APIStatusError) as e:
+                self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
+                asyncio.get_running_loop().call_later(2.0, self._resync, st.uid)
+                return None
         try:
-            cid = await self.runtime.create_container(st.sandbox, st.pod, c, opts)
+            cid = await self.runtime.create_container(st.sandbox, st.pod, spec_c, opts)
             self.m_runtime_ops.labels("create_container").inc()
             await self.runtime.start_container(cid)
             self.m_runtime_ops.labels("start_container").inc()
         except Exception as e:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
             return None
+        if c.get("livenessProbe") or c.get("readinessProbe"):
+            self.probes.start(st.uid, st.pod, c, cid)
         return cid
 
+    def _resync(self, uid):
+        st = self.pods.get(uid)
+        if st is not None and not st.terminated and uid not in self._pending:
+            self._dispatch(st.pod, "sync")
+
+    def _on_readiness(self, uid, cname, ok):
+        st = self.pods.get(uid)
+        if st is not None:
+            self._resync(uid)
+
+    def _on_liveness_failure(self, uid, cname, cid, msg):
+        st = self.pods.get(uid)
+        if st is None or st.containers.get(cname) != cid:
+            return
+        self.recorder.event(st.pod, "Warning", "Unhealthy", f"Liveness probe failed: {msg}")
+        self.recorder.event(st.pod, "Normal", "Killing", f"Killing container {cname}: failed liveness probe")
+
+        async def kill():
+            await self.runtime.stop_container(cid, 0)
+            self._resync(uid)
+        asyncio.ensure_future(kill())
+
     async def _kill_pod(self, st: PodState, grace):
+        self.probes.remove_pod(st.uid)
         rt = self.runtime
         for cid in list(st.containers.values()) + list(st.init_containers.values()):
             if cid is not None:
@@ -437,6 +498,9 @@ class Kubelet:
         if st.sandbox is not None:
             await self.runtime.remove_pod_sandbox(st.sandbox)
             st.sandbox = None
+        if st.volumes:
+            self.volumes.teardown(pod)
+            st.volumes = None
         try:
             await self.client.delete("pods", md["name"], md.get("namespace"), grace_period=0, uid=md["uid"])
         except APIStatusError as e:
@@ -451,6 +515,7 @@ class Kubelet:
         rt = self.runtime
         statuses, init_statuses = [], []
         running = terminated_ok = terminated_bad = waiting = 0
+        not_ready = 0
         for c in spec.get("containers") or ():
             cid = st.containers.get(c["name"])
             cs = rt.container_status(cid) if cid else None
@@ -460,6 +525,9 @@ class Kubelet:
                 waiting += 1
             elif cs.state == RUNNING:
                 running += 1
+                if c.get("readinessProbe") and not self.probes.ready(st.uid, c["name"]):
+                    s["ready"] = False
+                    not_ready += 1
             elif cs.state == EXITED:
                 if cs.exit_code == 0:
                     terminated_ok += 1
@@ -496,7 +564,7 @@ class Kubelet:
                 phase = core.POD_SUCCEEDED
         else:
             phase = core.POD_PENDING if waiting else core.POD_RUNNING
-        ready = phase == core.POD_RUNNING and running == n
+        ready = phase == core.POD_RUNNING and running == n and not not_ready
         now = now_rfc3339()
         old_conds = {c["type"]: c for c in (pod.get("status") or {}).get("conditions") or ()}
 

@@ -1,0 +1,136 @@
+"""Liveness / readiness probes.
+
+Parity: `pkg/kubelet/prober` — `prober.go` (exec via the runtime's ExecSync, HTTP GET with
+success = 200 <= code < 400, TCP connect), `worker.go` (one worker per container and probe
+type: `initialDelaySeconds`, `periodSeconds` (10), `timeoutSeconds` (1), `successThreshold` (1),
+`failureThreshold` (3); a readiness result starts as Failure until the first success, liveness
+as Success), `prober_manager.go` (results feed the container's `ready` and the kubelet kills a
+container whose liveness probe fails, restarting it per the pod's restartPolicy).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+
+log = logging.getLogger("kubelet.prober")
+
+
+def _port(container, port):
+    if isinstance(port, int) or (isinstance(port, str) and port.isdigit()):
+        return int(port)
+    for p in container.get("ports") or ():
+        if p.get("name") == port:
+            return int(p["containerPort"])
+    raise ValueError(f"unknown named port {port!r}")
+
+
+async def run_probe(runtime, pod, container, cid, probe, pod_ip="127.0.0.1"):
+    """Returns (success, message)."""
+    timeout = float(probe.get("timeoutSeconds") or 1)
+    try:
+        if "exec" in probe:
+            rc, out = await runtime.exec_sync(cid, probe["exec"].get("command") or [], timeout)
+            return rc == 0, out.decode(errors="replace")[-256:] if isinstance(out, bytes) else str(out)
+        if "httpGet" in probe:
+            h = probe["httpGet"]
+            host = h.get("host") or pod_ip
+            port = _port(container, h.get("port"))
+            path = h.get("path") or "/"
+            hdrs = "".join(f"{x['name']}: {x['value']}\r\n" for x in h.get("httpHeaders") or ())
+            r, w = await asyncio.wait_for(asyncio.open_connection(host, port), timeout)
+            try:
+                w.write(f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nUser-Agent: kube-probe/1.9\r\n{hdrs}"
+                        f"Connection: close\r\n\r\n".encode())
+                line = await asyncio.wait_for(r.readline(), timeout)
+            finally:
+                w.close()
+            parts = line.split()
+            code = int(parts[1]) if len(parts) > 1 else 0
+            return 200 <= code < 400, f"HTTP probe status {code}"
+        if "tcpSocket" in probe:
+            t = probe["tcpSocket"]
+            r, w = await asyncio.wait_for(asyncio.open_connection(t.get("host") or pod_ip, _port(container, t["port"])),
+                                          timeout)
+            w.close()
+            return True, ""
+    except (OSError, asyncio.TimeoutError, ValueError, NotImplementedError) as e:
+        return False, f"probe error: {e}"
+    return False, "probe has no handler"
+
+
+class _Worker:
+    def __init__(self, mgr, uid, pod, container, cid, kind, probe):
+        self.mgr, self.uid, self.pod, self.container, self.cid, self.kind, self.probe = (
+            mgr, uid, pod, container, cid, kind, probe)
+        self.result = kind == "liveness"          # readiness starts "not ready"
+        self.ok_run = self.fail_run = 0
+        self.task = asyncio.ensure_future(self.run())
+
+    async def run(self):
+        p = self.probe
+        period = float(p.get("periodSeconds") or 10)
+        succ_th = int(p.get("successThreshold") or 1)
+        fail_th = int(p.get("failureThreshold") or 3)
+        await asyncio.sleep(float(p.get("initialDelaySeconds") or 0))
+        while True:
+            ok, msg = await run_probe(self.mgr.runtime, self.pod, self.container, self.cid, p, self.mgr.pod_ip(self.uid))
+            if ok:
+                self.ok_run += 1
+                self.fail_run = 0
+            else:
+                self.fail_run += 1
+                self.ok_run = 0
+            new = self.result
+            if ok and self.ok_run >= succ_th:
+                new = True
+            elif not ok and self.fail_run >= fail_th:
+                new = False
+            if new != self.result:
+                self.result = new
+                self.mgr.changed(self, msg)
+                if self.kind == "liveness" and not new:
+                    return   # the container is being killed; a new worker follows the restart
+            await asyncio.sleep(period)
+
+    def stop(self):
+        self.task.cancel()
+
+
+class ProbeManager:
+    def __init__(self, runtime, on_readiness, on_liveness_failure, pod_ip=lambda uid: "127.0.0.1"):
+        self.runtime = runtime
+        self.on_readiness = on_readiness
+        self.on_liveness_failure = on_liveness_failure
+        self.pod_ip = pod_ip
+        self.workers: dict[tuple, _Worker] = {}   # (uid, container, kind) -> worker
+
+    def start(self, uid, pod, container, cid):
+        for kind in ("readiness", "liveness"):
+            p = container.get(f"{kind}Probe")
+            key = (uid, container["name"], kind)
+            old = self.workers.pop(key, None)
+            if old is not None:
+                old.stop()
+            if p:
+                self.workers[key] = _Worker(self, uid, pod, container, cid, kind, p)
+
+    def ready(self, uid, cname):
+        """None when the container has no readiness probe."""
+        w = self.workers.get((uid, cname, "readiness"))
+        return None if w is None else w.result
+
+    def changed(self, w, msg):
+        if w.kind == "readiness":
+            self.on_readiness(w.uid, w.container["name"], w.result)
+        elif not w.result:
+            log.info("liveness probe of %s/%s failed: %s", w.uid, w.container["name"], msg)
+            self.on_liveness_failure(w.uid, w.container["name"], w.cid, msg)
+
+    def remove_pod(self, uid):
+        for key in [k for k in self.workers if k[0] == uid]:
+            self.workers.pop(key).stop()
+
+    def stop(self):
+        for w in self.workers.values():
+            w.stop()
+        self.workers.clear()

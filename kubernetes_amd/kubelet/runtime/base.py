@@ -93,5 +93,9 @@ class Runtime:
     async def container_logs(self, cid: str, tail: int | None = None) -> bytes:
         return b""
 
+    async def exec_sync(self, cid: str, cmd: list, timeout: float) -> tuple:
+        """CRI ExecSync: run cmd in the container's context; returns (exit code, output bytes)."""
+        raise NotImplementedError(f"{self.name} runtime does not support exec")
+
     def list_containers(self):
         return []

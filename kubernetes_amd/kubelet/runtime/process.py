@@ -197,6 +197,27 @@ class ProcessRuntime(Runtime):
     def container_status(self, cid):
         return self.containers.get(cid)
 
+    async def exec_sync(self, cid, cmd, timeout):
+        m = self.meta.get(cid)
+        st = self.containers.get(cid)
+        if m is None or st is None or st.state != RUNNING:
+            return 126, b"container is not running"
+        try:
+            proc = await asyncio.create_subprocess_exec(*cmd, env=m["env"], cwd=m["cwd"], stdout=asyncio.subprocess.PIPE,
+                                                        stderr=asyncio.subprocess.STDOUT, start_new_session=True)
+        except OSError as e:
+            return 127, str(e).encode()
+        try:
+            out, _ = await asyncio.wait_for(proc.communicate(), timeout)
+        except asyncio.TimeoutError:
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            await proc.wait()
+            return 124, b"timeout"
+        return proc.returncode, out
+
     def list_containers(self):
         return list(self.containers.values())
 

@@ -35,6 +35,7 @@ class StubRuntime(Runtime):
         self.payload_runs = 0
         self.payload_failures = 0
         self._timers = {}
+        self.exec_codes: dict[tuple, int] = {}
 
     async def run_pod_sandbox(self, pod, annotations):
         sid = f"sb-{next(self._ids)}"
@@ -67,7 +68,8 @@ class StubRuntime(Runtime):
         elif len(cmd) == 2 and cmd[0] == "sleep":
             run_s = float(cmd[1])
         self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "opts": opts, "run_s": run_s,
-                          "container": container}
+                          "container": container,
+                          "exec_code": (pod["metadata"].get("annotations") or {}).get("kubemark.amd.com/exec-exit-code", 0)}
         return cid
 
     async def start_container(self, cid):
@@ -122,6 +124,17 @@ class StubRuntime(Runtime):
 
     def container_status(self, cid):
         return self.containers.get(cid)
+
+    async def exec_sync(self, cid, cmd, timeout):
+        """Fake exec: exit code from `exec_codes[(pod uid, container)]`, else the pod annotation
+        `kubemark.amd.com/exec-exit-code`, else 0 (lets tests flip probe results)."""
+        st, m = self.containers.get(cid), self.meta.get(cid)
+        if st is None or st.state != RUNNING:
+            return 126, b"container is not running"
+        key = (m["pod_uid"], st.name)
+        if key in self.exec_codes:
+            return self.exec_codes[key], b""
+        return int(m.get("exec_code", 0)), b""
 
     def list_containers(self):
         return list(self.containers.values())

@@ -1,0 +1,241 @@
+"""Pod volumes and container environment, kubelet side.
+
+Parity:
+  * `pkg/kubelet/volumemanager` + the in-tree plugins that need no cloud or network storage:
+    `pkg/volume/empty_dir` (node disk or `medium: Memory` = tmpfs, here /dev/shm),
+    `pkg/volume/host_path` (with `type: DirectoryOrCreate|FileOrCreate|Directory|File`),
+    `pkg/volume/configmap`, `pkg/volume/secret` (keys → files, `items` remap, `defaultMode`),
+    `pkg/volume/downwardapi` and `pkg/volume/projected` (a mix of the three);
+  * `pkg/kubelet/kubelet_pods.go` `makeEnvironmentVariables` — `env[].valueFrom` (fieldRef,
+    resourceFieldRef, configMapKeyRef, secretKeyRef) and `envFrom` (configMapRef/secretRef with
+    `prefix`), `$(VAR)` expansion against earlier entries.
+
+A volume is materialised under `<pods dir>/<pod uid>/volumes/<name>`; each `volumeMount` becomes a
+bind mount {containerPath, hostPath, readOnly} in the container's run options (the OCI bundle's
+`mounts`). The process runtime has no mount namespace, so it also exports each mount's host path
+as `KUBERNETES_VOLUME_<NAME>` to the process.
+"""
+from __future__ import annotations
+
+import base64
+import os
+import re
+import shutil
+
+from ..api.quantity import parse_quantity
+from ..client.rest import APIStatusError
+
+
+class VolumeError(Exception):
+    pass
+
+
+def _write_files(d, data: dict, items=None, mode=0o644, binary=False):
+    os.makedirs(d, exist_ok=True)
+    keys = {i["key"]: i.get("path", i["key"]) for i in items} if items else {k: k for k in data}
+    for k, rel in keys.items():
+        if k not in data:
+            raise VolumeError(f"key {k!r} not found")
+        p = os.path.join(d, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        v = data[k]
+        raw = base64.b64decode(v) if binary else str(v).encode()
+        tmp = p + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(raw)
+        os.chmod(tmp, mode)
+        os.replace(tmp, p)
+
+
+def _field(pod, path, node_name=None, pod_ip=None):
+    md = pod.get("metadata") or {}
+    if path == "metadata.name":
+        return md.get("name", "")
+    if path == "metadata.namespace":
+        return md.get("namespace", "")
+    if path == "metadata.uid":
+        return md.get("uid", "")
+    if path == "spec.nodeName":
+        return node_name or (pod.get("spec") or {}).get("nodeName", "")
+    if path == "spec.serviceAccountName":
+        return (pod.get("spec") or {}).get("serviceAccountName", "")
+    if path == "status.podIP":
+        return pod_ip or (pod.get("status") or {}).get("podIP", "")
+    if path == "status.hostIP":
+        return (pod.get("status") or {}).get("hostIP", "")
+    if path in ("metadata.labels", "metadata.annotations"):
+        m = md.get(path.split(".")[1]) or {}
+        return "\n".join(f'{k}="{v}"' for k, v in sorted(m.items()))
+    mm = re.fullmatch(r"metadata\.(labels|annotations)\['(.+)'\]", path)
+    if mm:
+        return (md.get(mm.group(1)) or {}).get(mm.group(2), "")
+    raise VolumeError(f"unsupported fieldRef {path!r}")
+
+
+def _resource_field(container, ref):
+    res = container.get("resources") or {}
+    r = ref["resource"]
+    kind, name = r.split(".", 1)
+    q = (res.get(kind) or {}).get(name)
+    if q is None and kind == "requests":
+        q = (res.get("limits") or {}).get(name)
+    if q is None:
+        return "0"
+    v = parse_quantity(str(q)).value / parse_quantity(str(ref.get("divisor", "1"))).value   # Fractions
+    # round up like the reference (ExtractResourceValueByContainerName)
+    return str(-(-v.numerator // v.denominator))
+
+
+class VolumeManager:
+    def __init__(self, client, root):
+        self.client = client
+        self.root = root
+
+    def pod_dir(self, pod):
+        return os.path.join(self.root, pod["metadata"]["uid"])
+
+    async def _get(self, kind, ns, name, optional):
+        try:
+            return await self.client.get(kind, name, ns)
+        except APIStatusError as e:
+            if e.code == 404 and optional:
+                return None
+            raise VolumeError(f"{kind[:-1]} {ns}/{name} not found" if e.code == 404 else str(e))
+
+    async def setup(self, pod, node_name=None, pod_ip=None) -> dict:
+        """Materialise every volume of the pod; returns {volume name: host path}."""
+        ns = pod["metadata"].get("namespace", "default")
+        base = os.path.join(self.pod_dir(pod), "volumes")
+        out = {}
+        for v in (pod.get("spec") or {}).get("volumes") or ():
+            name = v["name"]
+            d = os.path.join(base, name)
+            if "emptyDir" in v:
+                if (v["emptyDir"] or {}).get("medium") == "Memory" and os.path.isdir("/dev/shm"):
+                    d = os.path.join("/dev/shm", "kamd-" + pod["metadata"]["uid"], name)
+                os.makedirs(d, exist_ok=True)
+            elif "hostPath" in v:
+                hp = v["hostPath"]
+                d = hp["path"]
+                t = hp.get("type", "")
+                if t == "DirectoryOrCreate":
+                    os.makedirs(d, exist_ok=True)
+                elif t == "FileOrCreate" and not os.path.exists(d):
+                    os.makedirs(os.path.dirname(d), exist_ok=True)
+                    open(d, "a").close()
+                elif t == "Directory" and not os.path.isdir(d):
+                    raise VolumeError(f"hostPath {d} is not a directory")
+                elif t == "File" and not os.path.isfile(d):
+                    raise VolumeError(f"hostPath {d} is not a file")
+            elif "configMap" in v or "secret" in v:
+                await self._cm_secret(ns, v, d)
+            elif "downwardAPI" in v:
+                self._downward(pod, v["downwardAPI"], d, node_name, pod_ip)
+            elif "projected" in v:
+                for src in v["projected"].get("sources") or ():
+                    if "configMap" in src or "secret" in src:
+                        await self._cm_secret(ns, src, d)
+                    elif "downwardAPI" in src:
+                        self._downward(pod, src["downwardAPI"], d, node_name, pod_ip)
+            else:
+                raise VolumeError(f"volume {name}: unsupported volume source {sorted(k for k in v if k != 'name')}")
+            out[name] = d
+        return out
+
+    async def _cm_secret(self, ns, v, d):
+        if "configMap" in v:
+            src = v["configMap"]
+            obj = await self._get("configmaps", ns, src["name"], src.get("optional"))
+            data = dict((obj or {}).get("data") or {})
+            binary = False
+            if obj and obj.get("binaryData"):
+                for k, b in obj["binaryData"].items():
+                    data[k] = base64.b64decode(b).decode("latin-1")
+        else:
+            src = v["secret"]
+            obj = await self._get("secrets", ns, src.get("secretName") or src.get("name"), src.get("optional"))
+            data = dict((obj or {}).get("data") or {})
+            for k, s in ((obj or {}).get("stringData") or {}).items():
+                data[k] = base64.b64encode(s.encode()).decode()
+            binary = True
+        _write_files(d, data, src.get("items"), int(src.get("defaultMode", 0o644)), binary)
+
+    def _downward(self, pod, spec, d, node_name, pod_ip):
+        data = {}
+        items = []
+        for it in spec.get("items") or ():
+            if "fieldRef" in it:
+                data[it["path"]] = _field(pod, it["fieldRef"]["fieldPath"], node_name, pod_ip)
+            items.append({"key": it["path"], "path": it["path"]})
+        _write_files(d, data, items, int(spec.get("defaultMode", 0o644)))
+
+    def mounts_for(self, container, vols: dict):
+        out = []
+        for m in container.get("volumeMounts") or ():
+            hp = vols.get(m["name"])
+            if hp is None:
+                raise VolumeError(f"volumeMount {m['name']!r} refers to no pod volume")
+            if m.get("subPath"):
+                hp = os.path.join(hp, m["subPath"])
+                os.makedirs(hp, exist_ok=True)
+            out.append({"containerPath": m["mountPath"], "hostPath": hp, "readOnly": bool(m.get("readOnly"))})
+        return out
+
+    def teardown(self, pod):
+        shutil.rmtree(self.pod_dir(pod), ignore_errors=True)
+        shm = os.path.join("/dev/shm", "kamd-" + pod["metadata"]["uid"])
+        if os.path.isdir(shm):
+            shutil.rmtree(shm, ignore_errors=True)
+
+    async def env_for(self, pod, container, node_name=None, pod_ip=None):
+        """Resolved container environment (list of {name, value})."""
+        ns = pod["metadata"].get("namespace", "default")
+        env: dict[str, str] = {}
+        order = []
+
+        def put(k, v):
+            if k not in env:
+                order.append(k)
+            env[k] = v
+        for ef in container.get("envFrom") or ():
+            pre = ef.get("prefix", "")
+            if "configMapRef" in ef:
+                r = ef["configMapRef"]
+                obj = await self._get("configmaps", ns, r["name"], r.get("optional"))
+                for k, v in ((obj or {}).get("data") or {}).items():
+                    put(pre + k, str(v))
+            elif "secretRef" in ef:
+                r = ef["secretRef"]
+                obj = await self._get("secrets", ns, r["name"], r.get("optional"))
+                for k, v in ((obj or {}).get("data") or {}).items():
+                    put(pre + k, base64.b64decode(v).decode(errors="replace"))
+        for e in container.get("env") or ():
+            name = e["name"]
+            if "value" in e:
+                val = re.sub(r"\$\(([A-Za-z_][A-Za-z0-9_]*)\)", lambda m: env.get(m.group(1), m.group(0)), str(e["value"]))
+                put(name, val)
+                continue
+            vf = e.get("valueFrom") or {}
+            if "fieldRef" in vf:
+                put(name, _field(pod, vf["fieldRef"]["fieldPath"], node_name, pod_ip))
+            elif "resourceFieldRef" in vf:
+                put(name, _resource_field(container, vf["resourceFieldRef"]))
+            elif "configMapKeyRef" in vf:
+                r = vf["configMapKeyRef"]
+                obj = await self._get("configmaps", ns, r["name"], r.get("optional"))
+                if obj is not None:
+                    if r["key"] not in (obj.get("data") or {}):
+                        if not r.get("optional"):
+                            raise VolumeError(f"configmap {r['name']} has no key {r['key']}")
+                    else:
+                        put(name, str(obj["data"][r["key"]]))
+            elif "secretKeyRef" in vf:
+                r = vf["secretKeyRef"]
+                obj = await self._get("secrets", ns, r["name"], r.get("optional"))
+                if obj is not None:
+                    if r["key"] not in (obj.get("data") or {}):
+                        if not r.get("optional"):
+                            raise VolumeError(f"secret {r['name']} has no key {r['key']}")
+                    else:
+                        put(name, base64.b64decode(obj["data"][r["key"]]).decode(errors="replace"))
+        return [{"name": k, "value": env[k]} for k in order]
