@@ -30,7 +30,7 @@ class NodeHandle:
 class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
-                 health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None):
+                 health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
@@ -54,6 +54,7 @@ class LocalCluster:
         self.smi = None
         self.controllers = controllers            # None = no controller manager; list/["*"] = enabled set
         self.controller_options = controller_options or {}
+        self.kubelet_kwargs = kubelet_kwargs or {}
         self.cm = None
 
     async def start(self):
@@ -85,7 +86,7 @@ class LocalCluster:
         else:
             rt = StubRuntime(payload=self.payload)
         kl = Kubelet(Client(self.url), name, rt, dm, emit_events=self.emit_events,
-                     http_port=0 if self.kubelet_http else None)
+                     http_port=0 if self.kubelet_http else None, root_dir=ndir, **self.kubelet_kwargs)
         kl.smi = self.smi
         plugin = None
         await kl.run()

@@ -28,6 +28,11 @@ def main(argv=None):
     ap.add_argument("--node-labels", default="")
     ap.add_argument("--feature-gates", default="")
     ap.add_argument("--token", default=None)
+    ap.add_argument("--cpu-manager-policy", default="none", choices=["none", "static"])
+    ap.add_argument("--reserved-cpus", type=int, default=1, help="CPUs kept out of the static policy's exclusive pool")
+    ap.add_argument("--pod-manifest-path", default=None, help="directory of static pod manifests (JSON/YAML)")
+    ap.add_argument("--eviction-hard", default="memory.available<100Mi",
+                    help="hard eviction thresholds, e.g. memory.available<100Mi,nodefs.available<5%%")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -40,7 +45,9 @@ def main(argv=None):
         rt = ProcessRuntime(os.path.join(a.root_dir, "runtime")) if a.container_runtime == "process" else StubRuntime()
         labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
         kl = Kubelet(client, a.hostname_override, rt, dm, pods=a.max_pods, labels=labels,
-                     node_status_update_frequency=a.node_status_update_frequency, http_port=a.port, address=a.address)
+                     node_status_update_frequency=a.node_status_update_frequency, http_port=a.port, address=a.address,
+                     root_dir=a.root_dir, cpu_manager_policy=a.cpu_manager_policy, reserved_cpus=a.reserved_cpus,
+                     pod_manifest_path=a.pod_manifest_path, eviction_hard=a.eviction_hard)
         await kl.run()
         print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port})", flush=True)
         return kl

@@ -1,0 +1,121 @@
+"""Static pods from a manifest directory, mirrored into the API.
+
+Parity: `pkg/kubelet/config/file.go` (poll `--pod-manifest-path` every 20 s; JSON or YAML pod
+manifests; the pod name gets `-<nodeName>`, namespace defaults to `default`, a hash of the
+manifest identifies the version) and `pkg/kubelet/pod/mirror_client.go` (a mirror pod with the
+`kubernetes.io/config.mirror` annotation represents the static pod in the API; it is re-created
+when deleted and replaced when the manifest changes; removing the file deletes it).
+
+Here the mirror pod is also how the pod is run: it is created bound to this node
+(`spec.nodeName`), so the kubelet's normal informer path admits and starts it.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import json
+import logging
+import os
+
+from ..client.rest import APIStatusError
+
+log = logging.getLogger("kubelet.config")
+
+CONFIG_SOURCE = "kubernetes.io/config.source"
+CONFIG_HASH = "kubernetes.io/config.hash"
+CONFIG_MIRROR = "kubernetes.io/config.mirror"
+
+
+def load_manifests(path):
+    out = []
+    if not path or not os.path.isdir(path):
+        return out
+    for fn in sorted(os.listdir(path)):
+        if fn.startswith(".") or not fn.endswith((".json", ".yaml", ".yml")):
+            continue
+        full = os.path.join(path, fn)
+        try:
+            with open(full) as f:
+                text = f.read()
+            if fn.endswith(".json"):
+                doc = json.loads(text)
+            else:
+                import yaml
+                doc = yaml.load(text, Loader=yaml.SafeLoader)
+        except (OSError, ValueError, Exception) as e:   # a bad file must not stop the others
+            log.warning("static pod manifest %s: %s", full, e)
+            continue
+        if isinstance(doc, dict) and doc.get("kind", "Pod") == "Pod":
+            out.append((full, doc, hashlib.sha256(text.encode()).hexdigest()[:16]))
+    return out
+
+
+class StaticPodSource:
+    def __init__(self, kubelet, path, period=20.0):
+        self.kl = kubelet
+        self.path = path
+        self.period = period
+        self.known: dict[tuple, str] = {}     # (ns, name) -> hash
+        self._task = None
+
+    def start(self):
+        self._task = asyncio.ensure_future(self._loop())
+
+    def stop(self):
+        if self._task:
+            self._task.cancel()
+
+    async def _loop(self):
+        while True:
+            try:
+                await self.sync()
+            except Exception:
+                log.exception("static pod sync failed")
+            await asyncio.sleep(self.period)
+
+    def _mirror(self, doc, h):
+        pod = json.loads(json.dumps(doc))
+        md = pod.setdefault("metadata", {})
+        md["name"] = f"{md.get('name', 'static')}-{self.kl.node_name}"
+        md.setdefault("namespace", "default")
+        ann = md.setdefault("annotations", {})
+        ann.update({CONFIG_SOURCE: "file", CONFIG_HASH: h, CONFIG_MIRROR: h})
+        for k in ("uid", "resourceVersion", "creationTimestamp"):
+            md.pop(k, None)
+        pod.setdefault("spec", {})["nodeName"] = self.kl.node_name
+        pod.pop("status", None)
+        pod["apiVersion"], pod["kind"] = "v1", "Pod"
+        return pod
+
+    async def sync(self):
+        c = self.kl.client
+        seen = set()
+        for _, doc, h in load_manifests(self.path):
+            pod = self._mirror(doc, h)
+            key = (pod["metadata"]["namespace"], pod["metadata"]["name"])
+            seen.add(key)
+            try:
+                cur = await c.get("pods", key[1], key[0])
+            except APIStatusError as e:
+                if e.code != 404:
+                    raise
+                cur = None
+            if cur is not None and ((cur["metadata"].get("annotations") or {}).get(CONFIG_MIRROR) != h
+                                    or cur["metadata"].get("deletionTimestamp")):
+                if not cur["metadata"].get("deletionTimestamp"):
+                    await c.delete("pods", key[1], key[0], grace_period=0)
+                continue     # re-created on the next pass once gone
+            if cur is None:
+                try:
+                    await c.create("pods", pod, key[0])
+                except APIStatusError as e:
+                    if e.code != 409:
+                        log.warning("creating mirror pod %s/%s: %s", key[0], key[1], e)
+            self.known[key] = h
+        for key in [k for k in self.known if k not in seen]:
+            self.known.pop(key)
+            try:
+                await c.delete("pods", key[1], key[0], grace_period=0)
+            except APIStatusError as e:
+                if e.code != 404:
+                    log.warning("deleting mirror pod %s/%s: %s", key[0], key[1], e)

@@ -74,8 +74,21 @@ class Kubelet:
     def __init__(self, client, node_name, runtime, device_manager=None, cpu="128", memory="2Ti", pods=110,
                  labels=None, node_status_update_frequency=10.0, status_debounce=0.02, http_port=None,
                  emit_events=True, register=True, metrics=None, address="127.0.0.1", max_status_inflight=64,
-                 root_dir=None):
+                 root_dir=None, cpu_manager_policy="none", cpu_topology=None, reserved_cpus=1,
+                 pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0):
         self.client = client
+        self.pod_manifest_path = pod_manifest_path
+        self.static_pods = None
+        self.eviction = None
+        self.eviction_interval = eviction_interval
+        if eviction_hard:
+            from .eviction import EvictionManager, parse_thresholds
+            self.eviction = EvictionManager(parse_thresholds(eviction_hard), eviction_signals)
+        self.cpu_manager = None
+        if cpu_manager_policy == "static":
+            from .cpumanager import CPUTopology, StaticPolicy
+            self.cpu_manager = StaticPolicy(cpu_topology or CPUTopology.discover(), reserved_cpus,
+                                            os.path.join(root_dir or tempfile.gettempdir(), f"cpu_manager_state.{node_name}"))
         self.root_dir = root_dir or os.path.join(tempfile.gettempdir(), f"kamd-kubelet-{node_name}")
         self.volumes = VolumeManager(client, os.path.join(self.root_dir, "pods"))
         self.probes = ProbeManager(runtime, self._on_readiness, self._on_liveness_failure)
@@ -134,12 +147,39 @@ class Kubelet:
         self.informer.start()
         self._tasks.append(asyncio.ensure_future(self._node_status_loop()))
         await self.informer.wait_synced(60)
+        if self.pod_manifest_path:
+            from .config import StaticPodSource
+            self.static_pods = StaticPodSource(self, self.pod_manifest_path)
+            self.static_pods.start()
+        if self.eviction is not None:
+            self._tasks.append(asyncio.ensure_future(self._eviction_loop()))
         self.started.set()
+
+    async def _eviction_loop(self):
+        """eviction_manager.go synchronize(): observe, set pressure conditions, evict <= 1 pod."""
+        last_conds = set()
+        while not self._stopped:
+            running = [s.pod for s in self.pods.values() if s.admitted and not s.terminated and not s.rejected]
+            victim, msg = self.eviction.select_victim(running)
+            conds = set(self.eviction.conditions)
+            if conds != last_conds:
+                last_conds = conds
+                self._status_dirty.set()
+            if victim is not None:
+                st = self.pods.get(victim["metadata"]["uid"])
+                if st is not None:
+                    self.recorder.event(victim, "Warning", "Evicted", msg)
+                    await self._kill_pod(st, 0)
+                    await self._write_status(st, {"phase": core.POD_FAILED, "reason": "Evicted", "message": msg,
+                                                  "conditions": (victim.get("status") or {}).get("conditions") or []})
+            await asyncio.sleep(self.eviction_interval)
 
     async def stop(self):
         self._stopped = True
         self._status_dirty.set()
         self.informer.stop()
+        if self.static_pods is not None:
+            self.static_pods.stop()
         for t in self._tasks:
             t.cancel()
         for t in list(self._workers.values()):
@@ -174,14 +214,18 @@ class Kubelet:
             ers[rname] = dom
         # plugin labels (e.g. amd.com/gpu.product=MI355X) become node labels
         now = now_rfc3339()
+        mem_p = self.eviction is not None and self.eviction.has("MemoryPressure")
+        disk_p = self.eviction is not None and self.eviction.has("DiskPressure")
         st = {"capacity": capacity, "allocatable": dict(capacity),
               "conditions": [
                   {"type": "Ready", "status": "True", "reason": "KubeletReady", "message": "kubelet is posting ready status",
                    "lastHeartbeatTime": now, "lastTransitionTime": now},
-                  {"type": "MemoryPressure", "status": "False", "reason": "KubeletHasSufficientMemory", "lastHeartbeatTime": now,
-                   "lastTransitionTime": now},
-                  {"type": "DiskPressure", "status": "False", "reason": "KubeletHasNoDiskPressure", "lastHeartbeatTime": now,
-                   "lastTransitionTime": now}],
+                  {"type": "MemoryPressure", "status": "True" if mem_p else "False",
+                   "reason": "KubeletHasInsufficientMemory" if mem_p else "KubeletHasSufficientMemory",
+                   "lastHeartbeatTime": now, "lastTransitionTime": now},
+                  {"type": "DiskPressure", "status": "True" if disk_p else "False",
+                   "reason": "KubeletHasDiskPressure" if disk_p else "KubeletHasNoDiskPressure",
+                   "lastHeartbeatTime": now, "lastTransitionTime": now}],
               "addresses": [{"type": "InternalIP", "address": self.address}, {"type": "Hostname", "address": self.node_name}],
               "daemonEndpoints": {"kubeletEndpoint": {"Port": self.http_port or 0}},
               "nodeInfo": {"kubeletVersion": "v1.9.0-amd.0", "containerRuntimeVersion": f"{self.runtime.name}://1.0",
@@ -324,6 +368,8 @@ class Kubelet:
         except AdmitError as e:
             return "UnexpectedAdmissionError", f"Pod admission failed: {e}"
         r = self._general_predicates(pod)
+        if r is None and self.eviction is not None:
+            r = self.eviction.admit(pod)
         return r
 
     # ------------------------------------------------------------------
@@ -447,6 +493,15 @@ class Kubelet:
                 self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
                 asyncio.get_running_loop().call_later(2.0, self._resync, st.uid)
                 return None
+        if self.cpu_manager is not None:
+            from .cpumanager import format_cpulist
+            try:
+                cpus = self.cpu_manager.allocate(st.pod, c, self._gpu_numa(st.pod))
+            except ValueError as e:
+                self.recorder.event(st.pod, "Warning", "Failed", f"Error: cpu manager: {e}")
+                return None
+            opts.envs.append({"name": "KAMD_CPUSET", "value": format_cpulist(cpus)})
+            opts.annotations.append({"name": "io.kubernetes.cpuset", "value": format_cpulist(cpus)})
         try:
             cid = await self.runtime.create_container(st.sandbox, st.pod, spec_c, opts)
             self.m_runtime_ops.labels("create_container").inc()
@@ -458,6 +513,22 @@ class Kubelet:
         if c.get("livenessProbe") or c.get("readinessProbe"):
             self.probes.start(st.uid, st.pod, c, cid)
         return cid
+
+    def _gpu_numa(self, pod):
+        """NUMA nodes of the devices assigned to the pod (amd.com/numa attribute)."""
+        assigned = core.pod_assigned_devices(pod)
+        if not assigned:
+            return ()
+        store = getattr(self.dm, "store", None)
+        res = getattr(store, "resources", {}) if store is not None else {}
+        out = set()
+        for rn, ids in assigned.items():
+            devs = (res.get(rn) or {}).get("resources") or {}
+            for i in ids:
+                n = ((devs.get(i) or {}).get("attributes") or {}).get(core.ATTR_NUMA)
+                if n is not None and str(n).isdigit():
+                    out.add(int(n))
+        return tuple(sorted(out))
 
     def _resync(self, uid):
         st = self.pods.get(uid)
@@ -483,6 +554,8 @@ class Kubelet:
 
     async def _kill_pod(self, st: PodState, grace):
         self.probes.remove_pod(st.uid)
+        if self.cpu_manager is not None:
+            self.cpu_manager.release_pod(st.uid)
         rt = self.runtime
         for cid in list(st.containers.values()) + list(st.init_containers.values()):
             if cid is not None:
@@ -600,6 +673,8 @@ class Kubelet:
             del created
         if st.terminated and st.sandbox is not None and status["phase"] in (core.POD_SUCCEEDED, core.POD_FAILED):
             await self.runtime.stop_pod_sandbox(st.sandbox)
+            if self.cpu_manager is not None:
+                self.cpu_manager.release_pod(st.uid)
         await self._write_status(st, status)
 
     async def _write_status(self, st: PodState, status):

@@ -64,6 +64,8 @@ def build_spec(pod, container, opts: RunContainerOptions, rootfs="rootfs", hostn
                   "namespaces": [{"type": t} for t in ("pid", "ipc", "uts", "mount")] +
                                 ([{"type": "network", "path": f"/proc/{sandbox_pid}/ns/net"}] if sandbox_pid else [{"type": "network"}])},
     }
+    if "io.kubernetes.cpuset" in annotations:   # cpu manager (static policy) exclusive cpus
+        spec["linux"]["resources"]["cpu"] = {"cpus": annotations["io.kubernetes.cpuset"]}
     return spec
 
 

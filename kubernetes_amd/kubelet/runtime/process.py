@@ -131,9 +131,17 @@ class ProcessRuntime(Runtime):
         m = self.meta[cid]
         st = self.containers[cid]
         log = open(st.log_path, "ab")
+        pre = None
+        if m["env"].get("KAMD_CPUSET") and hasattr(os, "sched_setaffinity"):
+            # cpu manager's cpuset (cgroup cpuset.cpus in a real runtime): pin before exec
+            from ..cpumanager import parse_cpulist
+            cpus = set(parse_cpulist(m["env"]["KAMD_CPUSET"])) & set(os.sched_getaffinity(0))
+            if cpus:
+                pre = lambda: os.sched_setaffinity(0, cpus)  # noqa: E731
         try:
             proc = await asyncio.create_subprocess_exec(*m["argv"], env=m["env"], cwd=m["cwd"], stdout=log,
-                                                        stderr=asyncio.subprocess.STDOUT, start_new_session=True)
+                                                        stderr=asyncio.subprocess.STDOUT, start_new_session=True,
+                                                        preexec_fn=pre)
         except OSError as e:
             log.close()
             st.state = EXITED

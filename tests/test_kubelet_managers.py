@@ -1,0 +1,162 @@
+"""Kubelet managers: CPU manager static policy (GPU-NUMA aligned), eviction manager, static pods."""
+import asyncio
+import json
+import os
+
+from kubernetes_amd.api import core
+from kubernetes_amd.cluster import LocalCluster
+from kubernetes_amd.kubelet.cpumanager import CPUTopology, StaticPolicy, format_cpulist, parse_cpulist, take_by_topology
+from kubernetes_amd.kubelet.eviction import EvictionManager, parse_thresholds
+
+
+def test_cpulist_roundtrip_and_topology_take():
+    assert parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert format_cpulist([11, 0, 1, 2, 3, 8, 10]) == "0-3,8,10-11"
+    t = CPUTopology.synthetic(sockets=2, cores_per_socket=8, threads_per_core=2)
+    # whole physical cores (hyperthread pairs) first
+    assert take_by_topology(t, set(t.cpus), 4) == [0, 1, 16, 17]
+    # a full socket when asked for one
+    assert take_by_topology(t, set(t.cpus), 16) == list(range(0, 8)) + list(range(16, 24))
+    # NUMA preference (GPUs on socket 1)
+    assert {t.cpus[c].numa for c in take_by_topology(t, set(t.cpus), 6, prefer_numa=[1])} == {1}
+
+
+def test_static_policy_exclusive_and_checkpoint(tmp_path):
+    t = CPUTopology.synthetic(2, 4, 2)
+    sf = str(tmp_path / "state")
+    p = StaticPolicy(t, reserved=1, state_file=sf)
+    assert len(p.shared_pool()) == 15
+    g = {"metadata": {"uid": "u1"}, "status": {"qosClass": "Guaranteed"}}
+    c = {"name": "c", "resources": {"requests": {"cpu": "4"}, "limits": {"cpu": "4"}}}
+    cpus = p.allocate(g, c, prefer_numa=(1,))
+    assert len(cpus) == 4 and all(t.cpus[x].numa == 1 for x in cpus)
+    assert not set(cpus) & set(p.shared_pool())
+    # fractional or burstable -> shared pool
+    assert p.allocate({"metadata": {"uid": "u2"}, "status": {"qosClass": "Guaranteed"}},
+                      {"name": "c", "resources": {"requests": {"cpu": "1500m"}}}) == p.shared_pool()
+    # checkpoint survives a restart
+    p2 = StaticPolicy(t, reserved=1, state_file=sf)
+    assert p2.assignments == {"u1/c": cpus}
+    p2.release_pod("u1")
+    assert len(p2.shared_pool()) == 15
+    assert json.load(open(sf))["entries"] == {}
+
+
+def test_cpu_manager_in_kubelet_aligns_with_gpu_numa(run):
+    async def main():
+        topo = CPUTopology.synthetic(2, 8, 2)
+        async with LocalCluster(nodes=1, gpus_per_node=8,
+                                kubelet_kwargs={"cpu_manager_policy": "static", "cpu_topology": topo}) as cl:
+            c = cl.client
+            # GPUs 4-7 are on NUMA 1 in the fixture (numa_per=4): request 8 GPUs... take the second half by
+            # first occupying the first four
+            pod = {"metadata": {"name": "g", "namespace": "default"},
+                   "spec": {"containers": [{"name": "c", "image": "x",
+                                            "resources": {"limits": {"cpu": "4", "memory": "1Gi", core.AMD_GPU: "2"},
+                                                          "requests": {"cpu": "4", "memory": "1Gi"}}}]}}
+            await c.create("pods", pod)
+            p = await cl.wait_pod("g")
+            assert p["status"]["qosClass"] == "Guaranteed"
+            kl = cl.nodes[0].kubelet
+            cpus = kl.cpu_manager.assignments[p["metadata"]["uid"] + "/c"]
+            numas = set(kl._gpu_numa(p))
+            assert len(cpus) == 4 and {topo.cpus[x].numa for x in cpus} <= numas
+            await c.delete("pods", "g", "default")
+            for _ in range(500):
+                if not kl.cpu_manager.assignments:
+                    break
+                await asyncio.sleep(0.02)
+            assert not kl.cpu_manager.assignments
+    run(main(), timeout=60)
+
+
+def test_eviction_thresholds_rank_and_admit():
+    th = parse_thresholds("memory.available<100Mi,nodefs.available<10%")
+    sig = {"memory.available": (50 << 20, 1 << 30), "nodefs.available": (50, 100)}
+    em = EvictionManager(th, lambda: sig, usage_fn=lambda p: int(p["metadata"]["name"][-1]))
+    pods = [{"metadata": {"name": "g1"}, "status": {"qosClass": "Guaranteed"}, "spec": {}},
+            {"metadata": {"name": "b2"}, "status": {"qosClass": "BestEffort"}, "spec": {"priority": 5}},
+            {"metadata": {"name": "b3"}, "status": {"qosClass": "BestEffort"}, "spec": {}}]
+    v, msg = em.select_victim(pods)
+    assert v["metadata"]["name"] == "b3" and "memory" in msg      # BestEffort, lower priority first
+    assert em.has("MemoryPressure") and not em.has("DiskPressure")
+    assert em.admit({"status": {"qosClass": "BestEffort"}})[0] == "Evicted"
+    assert em.admit({"status": {"qosClass": "Burstable"}}) is None
+    sig["memory.available"] = (900 << 20, 1 << 30)
+    em.observe()
+    assert not em.has("MemoryPressure")
+
+
+def test_eviction_in_kubelet(run):
+    sig = {"memory.available": (8 << 30, 16 << 30)}
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=0,
+                                kubelet_kwargs={"eviction_hard": "memory.available<1Gi", "eviction_signals": lambda: sig,
+                                                "eviction_interval": 0.05}) as cl:
+            c = cl.client
+            for n, res in (("be", {}), ("bu", {"requests": {"memory": "1Gi"}})):
+                await c.create("pods", {"metadata": {"name": n, "namespace": "default"},
+                                        "spec": {"containers": [{"name": "c", "image": "x", "resources": res}]}})
+                await cl.wait_pod(n)
+            sig["memory.available"] = (100 << 20, 16 << 30)
+            p = await cl.wait_pod("be", phase="Failed", timeout=10)
+            assert p["status"]["reason"] == "Evicted"
+            for _ in range(300):
+                node = await c.get("nodes", "node-0")
+                if any(x["type"] == "MemoryPressure" and x["status"] == "True" for x in node["status"]["conditions"]):
+                    break
+                await asyncio.sleep(0.05)
+            else:
+                raise AssertionError("MemoryPressure not reported")
+            # BestEffort pods: the scheduler keeps them off (CheckNodeMemoryPressure) and the
+            # kubelet rejects one bound directly to the node
+            await c.create("pods", {"metadata": {"name": "be2", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "c", "image": "x"}]}})
+            await c.create("pods", {"metadata": {"name": "be3", "namespace": "default"},
+                                    "spec": {"nodeName": "node-0", "containers": [{"name": "c", "image": "x"}]}})
+            p = await cl.wait_pod("be3", phase="Failed", timeout=10)
+            assert p["status"]["reason"] == "Evicted"
+            p = await c.get("pods", "be2", "default")
+            assert "memory pressure" in p["status"]["conditions"][0]["message"]
+    run(main(), timeout=60)
+
+
+def test_static_pods_mirror(run, tmp_path):
+    d = tmp_path / "manifests"
+    d.mkdir()
+    (d / "web.yaml").write_text("apiVersion: v1\nkind: Pod\nmetadata:\n  name: web\nspec:\n  containers:\n  - name: c\n    image: x\n")
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=0, kubelet_kwargs={"pod_manifest_path": str(d)}) as cl:
+            kl = cl.nodes[0].kubelet
+            kl.static_pods.period = 0.1
+            p = await cl.wait_pod("web-node-0", timeout=10)
+            assert p["metadata"]["annotations"]["kubernetes.io/config.source"] == "file"
+            assert p["spec"]["nodeName"] == "node-0"
+            # deleting the mirror pod re-creates it
+            uid = p["metadata"]["uid"]
+            await cl.client.delete("pods", "web-node-0", "default", grace_period=0)
+
+            async def recreated():
+                try:
+                    q = await cl.client.get("pods", "web-node-0", "default")
+                    return q["metadata"]["uid"] != uid and q["status"].get("phase") == "Running"
+                except Exception:
+                    return False
+            for _ in range(200):
+                if await recreated():
+                    break
+                await asyncio.sleep(0.05)
+            assert await recreated()
+            # removing the manifest deletes the mirror pod
+            os.remove(d / "web.yaml")
+            for _ in range(200):
+                try:
+                    await cl.client.get("pods", "web-node-0", "default")
+                except Exception:
+                    break
+                await asyncio.sleep(0.05)
+            else:
+                raise AssertionError("mirror pod not deleted")
+    run(main(), timeout=60)
