@@ -88,6 +88,7 @@ def _run_sync(coro):
 
 
 DEVICE_PREFIX = "/kamd/devices/"   # claim keys, outside /registry/ so watch caches never see them
+ENC_PREFIX = b"k8s:enc:"          # encrypted-at-rest value (storage/value.py)
 _FRAME = b"\x00KH"                 # shared-store value framing (index header + object)
 
 
@@ -95,7 +96,13 @@ class APIServer:
     def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
                  max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
-                 kubelet_port_resolver=None, audit=None):
+                 kubelet_port_resolver=None, audit=None, encryption_config=None):
+        # encryption at rest (--experimental-encryption-provider-config): plural -> PrefixTransformers
+        self.transformers = {}
+        if encryption_config:
+            from ..storage.value import load_encryption_config
+            self.transformers = (encryption_config if isinstance(encryption_config, dict)
+                                 and "kind" not in encryption_config else load_encryption_config(encryption_config))
         self.remote_address = store if isinstance(store, str) else None
         self.rstore = None            # RemoteStore once started (shared mode)
         self.store = None if self.remote_address else (store or MVCCStore())
@@ -110,6 +117,7 @@ class APIServer:
         self.strategies = {}
         self.storage_codec = codec.StorageCodec(storage_media_type)
         self.watch_window = watch_window
+        self._store_res = {}          # etcd key segment (`pods`, `roles.rbac.authorization.k8s.io`) -> plural
         for ri in m.RESOURCES:
             self._install(ri)
         names = adm.DEFAULT_PLUGINS if admission_plugins is None else admission_plugins
@@ -151,6 +159,27 @@ class APIServer:
     def _install(self, ri):
         self.caches[ri.plural] = ResourceCache(ri.plural, self.watch_window)
         self.strategies[ri.plural] = strategy_for(ri)
+        self._store_res[m.prefix_for(ri).split("/")[2]] = ri.plural
+
+    def _cache_for_key(self, key):
+        parts = key.split("/", 3)
+        if len(parts) <= 3:
+            return None, None
+        plural = self._store_res.get(parts[2])
+        return plural, (self.caches.get(plural) if plural else None)
+
+    def _seal(self, plural, key, data: bytes) -> bytes:
+        t = self.transformers.get(plural)
+        return data if t is None else t.to_storage(data, key.encode())
+
+    def _unseal(self, key, data: bytes) -> bytes:
+        if data[:8] != ENC_PREFIX:
+            return data
+        plural, _ = self._cache_for_key(key)
+        t = self.transformers.get(plural)
+        if t is None:
+            raise APIError(500, "InternalError", f"stored value of {key} is encrypted but no provider is configured")
+        return t.from_storage(data, key.encode())[0]
 
     def _collect(self):
         out = ["# TYPE etcd_object_counts gauge"]
@@ -169,7 +198,7 @@ class APIServer:
             kvs, _, _ = self.store.range(m.prefix_for(ri))
             cache = self.caches[ri.plural]
             for kv in kvs:
-                obj = self.storage_codec.decode(kv.value)
+                obj = self.storage_codec.decode(self._unseal(kv.key, kv.value))
                 obj.setdefault("metadata", {})["resourceVersion"] = str(kv.mod_rev)
                 raw = codec.dumpb(obj)
                 cache.by_key[kv.key] = cache.make_entry(obj, raw, kv.mod_rev)
@@ -206,6 +235,10 @@ class APIServer:
         v = kv.value
         if v[:3] == _FRAME:
             v = v[7 + int.from_bytes(v[3:7], "little"):]
+        if v[:8] == ENC_PREFIX:
+            obj = self.storage_codec.decode(self._unseal(kv.key, v))
+            obj.setdefault("metadata", {})["resourceVersion"] = str(kv.mod_rev)
+            return obj, codec.dumpb(obj)
         if v[:4] == codec.MAGIC:
             obj = self.storage_codec.decode(v)
             obj.setdefault("metadata", {})["resourceVersion"] = str(kv.mod_rev)
@@ -213,8 +246,7 @@ class APIServer:
         return codec.loads(v), v
 
     def _ingest(self, t, kv, dispatch=True):
-        parts = kv.key.split("/", 3)
-        cache = self.caches.get(parts[2]) if len(parts) > 3 else None
+        _, cache = self._cache_for_key(kv.key)
         if cache is None:
             return
         entry = self._mine.pop((kv.key, kv.mod_rev), None)
@@ -310,7 +342,8 @@ class APIServer:
         md = obj["metadata"]
         tok = self._rv_token
         cache = self.caches[ri.plural]
-        json_storage = self.storage_codec.media_type == codec.JSON
+        sealed = ri.plural in self.transformers
+        json_storage = self.storage_codec.media_type == codec.JSON and not sealed
         # value framing: [00 'K' 'H' | u32 len | index header (fields, labels) | object]
         hdr = codec.dumpb([cache.fields_fn(obj), md.get("labels") or {}])
         frame = _FRAME + len(hdr).to_bytes(4, "little") + hdr
@@ -321,9 +354,12 @@ class APIServer:
         else:
             md.pop("resourceVersion", None)
             raw_t = None
-            stored = self.storage_codec.encode(obj)
+            stored = self._seal(ri.plural, key, self.storage_codec.encode(obj))
         cmps = [(wire.CMP_MOD_REV, key, prev.rev if prev is not None else 0, None)]
-        if etype == DELETED:
+        if etype == DELETED and sealed:
+            # no plaintext index header or tombstone for encrypted resources
+            ops = [(wire.OP_DELETE_TOMBSTONE, key, self._seal(ri.plural, key, codec.dumpb(obj)), tok)]
+        elif etype == DELETED:
             tomb = raw_t if raw_t is not None else codec.dumpb(dict(obj, metadata=dict(md, resourceVersion=tok.decode())))
             ops = [(wire.OP_DELETE_TOMBSTONE, key, frame + tomb, tok)]
         elif json_storage:
@@ -386,6 +422,8 @@ class APIServer:
         obj["metadata"]["resourceVersion"] = str(rev)
         raw = codec.dumpb(obj)
         stored = raw if self.storage_codec.media_type == codec.JSON else self.storage_codec.encode(obj)
+        if ri.plural in self.transformers:
+            stored = self._seal(ri.plural, key, stored)
         if etype == ADDED:
             ev = self.store.create(key, stored)
             if ev is None:

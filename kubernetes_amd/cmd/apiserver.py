@@ -45,6 +45,8 @@ def _parser():
     ap.add_argument("--watch-cache-size", type=int, default=200000)
     ap.add_argument("--audit-log-path", default=None, help="write audit events (JSON lines) here; '-' = stdout")
     ap.add_argument("--audit-policy-file", default=None, help="audit policy YAML (rules: level/users/verbs/resources)")
+    ap.add_argument("--experimental-encryption-provider-config", dest="encryption_config", default=None,
+                    help="EncryptionConfig YAML: encrypt the listed resources at rest (aescbc/aesgcm/secretbox/kms)")
     ap.add_argument("-v", type=int, default=0)
     return ap
 
@@ -73,6 +75,8 @@ def supervise(a):
         base += ["--admission-control", a.admission_control]
     if a.token_auth_file:
         base += ["--token-auth-file", a.token_auth_file]
+    if a.encryption_config:
+        base += ["--experimental-encryption-provider-config", a.encryption_config]
     ready_dir = store.dir or os.path.dirname(store.socket_path)
     children = []
     stopping = []
@@ -143,7 +147,7 @@ def main(argv=None):
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
                       max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size,
-                      audit=audit)
+                      audit=audit, encryption_config=a.encryption_config)
         port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
         if not a.reuse_port:

@@ -4,6 +4,7 @@ Built in-tree by `python -m kubernetes_amd.native.build` (also `__graft_entry__.
   lib/libkamd_smi.so     AMD SMI shim (native/amdsmi_shim)
   lib/libkamd_store.so   MVCC KV engine (native/store)
   lib/libkamd_oci.so     OCI device-injection helper (native/oci)
+  lib/libkamd_crypto.so  AES-CBC/GCM, NaCl secretbox, x509 issue/verify (native/crypto, OpenSSL)
   lib/libkamd_hip.so     HIP/CDNA4 kernels: vector_add, MFMA diag GEMM, HBM bandwidth (gfx950)
   bin/pause, bin/orphan  pod-sandbox PID 1 and its reaper test helper (native/pause)
 """

@@ -39,6 +39,8 @@ def targets():
                       cxx + ["-O3", "-DKAMD_STORE_SERVER", _s("store", "mvcc_store.cc")]),
         "kamd_oci": ([_s("oci", "oci_devices.cc")], os.path.join(LIB_DIR, "libkamd_oci.so"),
                      cxx + ["-shared", _s("oci", "oci_devices.cc")]),
+        "kamd_crypto": ([_s("crypto", "kamd_crypto.cc")], os.path.join(LIB_DIR, "libkamd_crypto.so"),
+                        cxx + ["-O2", "-shared", _s("crypto", "kamd_crypto.cc"), "-lcrypto"]),
         "pause": ([_s("pause", "pause.cc")], os.path.join(BIN_DIR, "pause"),
                   ["g++", "-Os", "-Wall", "-Werror", "-static", _s("pause", "pause.cc")]),
         "orphan": ([_s("pause", "orphan.cc")], os.path.join(BIN_DIR, "orphan"),
