@@ -36,7 +36,7 @@ from ..api.labels import SelectorError, parse as parse_labels, parse_field_selec
 from ..api.meta import fast_copy, now_rfc3339
 from ..storage import wire
 from ..storage.mvcc import MVCCStore
-from ..utils.httpserver import HTTPServer, Response, StreamResponse
+from ..utils.httpserver import HTTPServer, Response, StreamResponse, UpgradeResponse
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
 from . import admission as adm
@@ -875,6 +875,9 @@ class APIServer:
             if sub == "log" and ri.plural == "pods":
                 self._authorize(user, "get", ns, "pods", "log", name, "", req.path)
                 return await self._pod_log(ns, name, q)
+            if sub in ("exec", "attach", "portforward") and ri.plural == "pods":
+                self._authorize(user, "get", ns, "pods", sub, name, "", req.path)
+                return await self._pod_stream(req, ns, name, sub)
             self._authorize(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
             key = m.key_for(ri, ns, name)
             e = self.caches[ri.plural].get(key)
@@ -890,6 +893,9 @@ class APIServer:
                 self._authorize(user, "create", ns, "pods", "binding", name, "", req.path)
                 await self.bind(ns, name, codec.loads(body), user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
+            if name is not None and sub in ("exec", "attach", "portforward") and ri.plural == "pods":
+                self._authorize(user, "create", ns, "pods", sub, name, "", req.path)
+                return await self._pod_stream(req, ns, name, sub)
             if name is not None and sub == "eviction" and ri.plural == "pods":
                 self._authorize(user, "create", ns, "pods", "eviction", name, "", req.path)
                 await self.evict(ns, name, codec.loads(body) if body else {}, user)
@@ -1018,7 +1024,9 @@ class APIServer:
 
         return StreamResponse(run)
 
-    async def _pod_log(self, ns, name, q):
+    def _kubelet_of(self, ns, name):
+        """(pod, kubelet host, kubelet port) — the node connection info the reference resolves in
+        `pkg/registry/core/pod/strategy.go` ResourceLocation / streamLocation."""
         pod = self.get_object("pods", ns, name)
         if pod is None:
             raise not_found(m.BY_PLURAL["pods"], name)
@@ -1033,6 +1041,59 @@ class APIServer:
                 addr = a.get("address")
         if not port:
             raise APIError(503, "ServiceUnavailable", f"node {node} has no kubelet endpoint")
+        return pod, addr, port
+
+    async def _pod_stream(self, req, ns, name, sub):
+        """pods/exec, pods/attach (framed stream) and pods/portforward (Upgrade: tcp) proxied to
+        the node's kubelet (`pkg/registry/core/pod/rest/subresources.go` ExecREST/PortForwardREST)."""
+        from urllib.parse import parse_qs, urlencode
+        pod, addr, port = self._kubelet_of(ns, name)
+        q = parse_qs(req.qs or "")
+        if sub == "portforward":
+            pport = (q.get("port") or q.get("ports") or [""])[0]
+            if not pport:
+                raise bad_request("port is required")
+            if "upgrade" not in req.headers.get("connection", "").lower():
+                raise bad_request("port-forward needs Connection: Upgrade")
+            from ..cri.server import splice
+            from ..cri.streaming import open_port_forward
+            url = f"http://{addr}:{port}/portForward/{ns}/{name}"
+
+            async def run(reader, writer):
+                ur, uw = await open_port_forward(url, int(pport))
+                await splice(reader, writer, ur, uw)
+            return UpgradeResponse(run)
+        containers = (pod.get("spec") or {}).get("containers") or [{}]
+        cname = (q.get("container") or [containers[0].get("name", "")])[0]
+        names = {c.get("name") for c in containers} | {c.get("name") for c in (pod.get("spec") or {}).get("initContainers") or ()}
+        if cname not in names:
+            raise bad_request(f"container {cname} is not valid for pod {name}")
+        target = f"http://{addr}:{port}/{sub}/{ns}/{name}/{cname}"
+        if q.get("command"):
+            target += "?" + urlencode([("command", c) for c in q["command"]])
+        from ..cri.streaming import _open
+
+        async def relay(w):
+            r, uw, status, _ = await _open(target)
+            try:
+                if status != 200:
+                    body = await r.read(4096)
+                    msg = b"\x01" + body
+                    w.transport.write(b"%x\r\n%s\r\n" % (len(msg), msg))
+                    w.transport.write(b"2\r\n\x03" + b"1" + b"\r\n")
+                    return
+                while True:
+                    line = await r.readuntil(b"\r\n")
+                    size = int(line.strip(), 16)
+                    if size == 0:
+                        break
+                    w.transport.write(line + await r.readexactly(size + 2))
+            finally:
+                uw.close()
+        return StreamResponse(relay, "application/vnd.kamd.stream")
+
+    async def _pod_log(self, ns, name, q):
+        _, addr, port = self._kubelet_of(ns, name)
         from ..client.http import HTTPClient
         c = HTTPClient(f"http://{addr}:{port}")
         try:
@@ -1079,6 +1140,10 @@ class APIServer:
                 res.append({"name": "pods/binding", "singularName": "", "namespaced": True, "kind": "Binding", "verbs": ["create"]})
                 res.append({"name": "pods/eviction", "singularName": "", "namespaced": True, "kind": "Eviction", "verbs": ["create"]})
                 res.append({"name": "pods/log", "singularName": "", "namespaced": True, "kind": "Pod", "verbs": ["get"]})
+                for sr in ("exec", "attach", "portforward"):
+                    res.append({"name": f"pods/{sr}", "singularName": "", "namespaced": True,
+                                "kind": "PodExecOptions" if sr != "portforward" else "PodPortForwardOptions",
+                                "verbs": ["create", "get"]})
         if not res:
             raise APIError(404, "NotFound", f"{group}/{version} not found")
         gv = f"{group}/{version}" if group else version

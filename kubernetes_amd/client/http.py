@@ -130,6 +130,15 @@ class HTTPClient:
                     self._idle.append(conn)
                 return status, data
 
+    async def open_raw(self, method, path, headers=None, body=None):
+        """Send one request on a dedicated connection and return (status, headers, reader,
+        writer) with the body unread — for exec streams and `Upgrade: tcp` port-forward tunnels."""
+        conn = await self._open()
+        conn.writer.write(self._head(method, path, body, "application/octet-stream", headers) + (body or b""))
+        await conn.writer.drain()
+        status, hdrs = await _read_response(conn.reader)
+        return status, hdrs, conn.reader, conn.writer
+
     async def stream(self, method, path, headers=None):
         """Open a streaming GET; returns (status, async line iterator, closer)."""
         conn = await self._open()

@@ -76,12 +76,14 @@ class LocalCluster:
             await self.cm.start()
         return self
 
-    async def add_node(self, name):
+    async def add_node(self, name, runtime=None):
         ndir = os.path.join(self.dir, name)
         plugins_dir = os.path.join(ndir, "device-plugin", "plugins")
         os.makedirs(plugins_dir, exist_ok=True)
         dm = ManagerImpl(plugins_dir)
-        if self.runtime_kind == "process":
+        if runtime is not None:
+            rt = runtime
+        elif self.runtime_kind == "process":
             rt = ProcessRuntime(os.path.join(ndir, "runtime"))
         else:
             rt = StubRuntime(payload=self.payload)

@@ -1,0 +1,41 @@
+"""kamd-cri: a standalone CRI (v1alpha1) runtime daemon on a unix socket — the role the
+dockershim's gRPC endpoint plays for the reference kubelet (`unix:///var/run/dockershim.sock`,
+`cmd/kubelet/app/options/options.go:196`; `pkg/kubelet/dockershim/remote/docker_server.go`).
+
+    python -m kubernetes_amd.cmd.cri --listen /var/run/kamd-cri.sock --runtime process
+    python -m kubernetes_amd.cmd.kubelet --container-runtime remote \
+        --container-runtime-endpoint unix:///var/run/kamd-cri.sock ...
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+from ..cri.server import CRIServer
+from ..kubelet.runtime.process import ProcessRuntime
+from ..kubelet.runtime.stub import StubRuntime
+from ._common import run_until_signal, setup_logging
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("kamd-cri")
+    ap.add_argument("--listen", default="/var/run/kamd-cri.sock")
+    ap.add_argument("--runtime", default="process", choices=["process", "stub"])
+    ap.add_argument("--root-dir", default="/var/lib/kamd-cri")
+    ap.add_argument("-v", type=int, default=0)
+    a = ap.parse_args(argv)
+    setup_logging(a.v)
+
+    async def start():
+        rt = ProcessRuntime(os.path.join(a.root_dir, "containers")) if a.runtime == "process" else StubRuntime()
+        os.makedirs(os.path.dirname(os.path.abspath(a.listen)), exist_ok=True)
+        srv = await CRIServer(rt, a.listen).start()
+        print(f"kamd-cri serving CRI v1alpha1 ({rt.name} runtime) on unix://{a.listen}, "
+              f"streaming on 127.0.0.1:{srv.streaming.port}", flush=True)
+        return srv
+
+    run_until_signal(start)
+
+
+if __name__ == "__main__":
+    main()

@@ -20,7 +20,14 @@ def main(argv=None):
     ap.add_argument("--hostname-override", default=os.uname().nodename)
     ap.add_argument("--root-dir", default="/var/lib/kubelet")
     ap.add_argument("--device-plugins-dir", default=None)
-    ap.add_argument("--container-runtime", default="process", choices=["process", "stub"])
+    ap.add_argument("--container-runtime", default="process", choices=["process", "stub", "remote"])
+    ap.add_argument("--container-runtime-endpoint", default="unix:///var/run/kamd-cri.sock",
+                    help="CRI endpoint for --container-runtime=remote (kamd-cri or any v1alpha1 CRI runtime)")
+    ap.add_argument("--runtime-request-timeout", type=float, default=120.0)
+    ap.add_argument("--pleg-relist-period", type=float, default=1.0, help="generic PLEG relist period (remote runtime)")
+    ap.add_argument("--image-gc-high-threshold", type=int, default=85)
+    ap.add_argument("--image-gc-low-threshold", type=int, default=80)
+    ap.add_argument("--image-fs-capacity", default="0", help="image filesystem size for image GC (e.g. 100Gi; 0 = off)")
     ap.add_argument("--port", type=int, default=10250)
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
@@ -42,12 +49,21 @@ def main(argv=None):
         client = Client(a.master, token=a.token, max_conns=32)
         pdir = a.device_plugins_dir or os.path.join(a.root_dir, "device-plugin", "plugins")
         dm = ManagerImpl(pdir) if DefaultFeatureGate("DevicePlugins") else ManagerStub()
-        rt = ProcessRuntime(os.path.join(a.root_dir, "runtime")) if a.container_runtime == "process" else StubRuntime()
+        if a.container_runtime == "remote":
+            from ..cri.remote import RemoteRuntime
+            rt = await RemoteRuntime(a.container_runtime_endpoint, a.runtime_request_timeout, a.pleg_relist_period).connect()
+        elif a.container_runtime == "process":
+            rt = ProcessRuntime(os.path.join(a.root_dir, "runtime"))
+        else:
+            rt = StubRuntime()
+        from ..api.quantity import parse_quantity
+        cap = int(parse_quantity(a.image_fs_capacity).value) if a.image_fs_capacity not in ("", "0") else 0
+        image_gc = {"capacity_bytes": cap, "high": a.image_gc_high_threshold, "low": a.image_gc_low_threshold} if cap else None
         labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
         kl = Kubelet(client, a.hostname_override, rt, dm, pods=a.max_pods, labels=labels,
                      node_status_update_frequency=a.node_status_update_frequency, http_port=a.port, address=a.address,
                      root_dir=a.root_dir, cpu_manager_policy=a.cpu_manager_policy, reserved_cpus=a.reserved_cpus,
-                     pod_manifest_path=a.pod_manifest_path, eviction_hard=a.eviction_hard)
+                     pod_manifest_path=a.pod_manifest_path, eviction_hard=a.eviction_hard, image_gc=image_gc)
         await kl.run()
         print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port})", flush=True)
         return kl

@@ -21,6 +21,7 @@ import time
 from ..client.rest import Client
 from ..scheduler.scheduler import Scheduler
 from ._common import run_until_signal, setup_logging
+from ..utils.tasks import spawn
 
 
 def _parser():
@@ -98,7 +99,7 @@ def main(argv=None):
             lock = "kube-scheduler" if a.shard_count == 1 else f"kube-scheduler-shard-{a.shard_index}"
             le = LeaderElector(client, "kube-system", lock)
             await le.acquire()
-        asyncio.ensure_future(s.run(metrics_port=a.metrics_port))
+        spawn(s.run(metrics_port=a.metrics_port))
         return s
 
     run_until_signal(start)

@@ -476,8 +476,191 @@ class Kubectl:
                                          f"{'/namespaces/' + self.ns if ri.namespaced else ''}/{ri.plural}?limit=1")
         self.p("yes" if st == 200 else "no")
 
-    async def cmd_unsupported(self):
-        raise SystemExit(f"error: '{self.a.command}' needs a streaming runtime session, which the process/stub runtimes do not provide")
+    # -- streaming: exec / attach / port-forward / cp / proxy / edit ------------------------
+    def _pod_path(self, name, sub):
+        return f"/api/v1/namespaces/{self.ns}/pods/{name}/{sub}"
+
+    async def _exec(self, pod, container, command):
+        """pods/exec stream -> (exit code, stdout, stderr) (`pkg/kubectl/cmd/exec.go`)."""
+        from urllib.parse import urlencode
+        from ..cri.streaming import read_frames
+        q = [("command", c) for c in command] + ([("container", container)] if container else [])
+        st, hdrs, r, w = await self.client.http.open_raw("POST", self._pod_path(pod, "exec") + "?" + urlencode(q))
+        try:
+            if st != 200:
+                from ..client.http import _read_body
+                body = await _read_body(r, hdrs)
+                try:
+                    msg = json.loads(body).get("message", body.decode())
+                except ValueError:
+                    msg = body.decode(errors="replace")
+                raise SystemExit(f"error: unable to exec in pod {pod}: {msg}")
+            return await read_frames(r)
+        finally:
+            w.close()
+
+    async def cmd_exec(self):
+        a = self.a
+        rest = list(a.exec_command or [])
+        container = a.container
+        if "--" in rest:
+            pre, cmd = rest[:rest.index("--")], rest[rest.index("--") + 1:]
+            i = 0
+            while i < len(pre):        # flags given after the pod name but before `--`
+                if pre[i] in ("-c", "--container") and i + 1 < len(pre):
+                    container = pre[i + 1]
+                    i += 2
+                else:
+                    i += 1
+        else:
+            cmd = rest
+        if not cmd:
+            raise SystemExit("error: you must specify at least one command for the container")
+        rc, out, err = await self._exec(a.pod, container, cmd)
+        self.out.write(out.decode(errors="replace"))
+        if err:
+            sys.stderr.write(err.decode(errors="replace"))
+        self.rc = rc
+
+    async def cmd_attach(self):
+        from ..cri.streaming import read_frames
+        a = self.a
+        path = self._pod_path(a.pod, "attach") + (f"?container={a.container}" if a.container else "")
+        st, hdrs, r, w = await self.client.http.open_raw("POST", path)
+        try:
+            if st != 200:
+                raise SystemExit(f"error: unable to attach to pod {a.pod}: HTTP {st}")
+            rc, out, _ = await read_frames(r)
+            self.out.write(out.decode(errors="replace"))
+        finally:
+            w.close()
+
+    async def cmd_port_forward(self):
+        """`kubectl port-forward POD [LOCAL:]REMOTE ...` (`pkg/kubectl/cmd/portforward.go`)."""
+        from ..cri.server import splice
+        a = self.a
+        pod = a.pod.split("/", 1)[-1]
+        servers, served = [], [0]
+        done = asyncio.Event()
+        for spec in a.ports:
+            lp, _, rp = spec.partition(":")
+            local, remote = (int(lp), int(rp)) if rp else (int(lp), int(lp))
+
+            def handler(remote=remote):
+                async def h(reader, writer):
+                    st, _, ur, uw = await self.client.http.open_raw(
+                        "POST", self._pod_path(pod, "portforward") + f"?port={remote}",
+                        {"Connection": "Upgrade", "Upgrade": "tcp"})
+                    if st != 101:
+                        writer.close()
+                        uw.close()
+                        return
+                    await splice(reader, writer, ur, uw)
+                    served[0] += 1
+                    if a.max_connections and served[0] >= a.max_connections:
+                        done.set()
+                return h
+            srv = await asyncio.start_server(handler(), a.address, local)
+            servers.append(srv)
+            self.p(f"Forwarding from {a.address}:{srv.sockets[0].getsockname()[1]} -> {remote}")
+        if hasattr(self.out, "flush"):
+            self.out.flush()
+        try:
+            await done.wait()
+        finally:
+            for srv in servers:
+                srv.close()
+
+    async def cmd_cp(self):
+        """`kubectl cp` over exec: pod->local streams `cat`; local->pod ships the file base64-encoded
+        in the exec command (files up to 1 MiB; the reference pipes a tar stream over stdin)."""
+        a = self.a
+        src, dst = a.src, a.dst
+        if ":" in src and not os.path.exists(src):
+            pod, path = src.split(":", 1)
+            rc, out, err = await self._exec(pod.split("/")[-1], a.container, ["cat", path])
+            if rc != 0:
+                raise SystemExit(f"error: {err.decode() or out.decode()}")
+            with open(dst, "wb") as f:
+                f.write(out)
+            return
+        pod, path = dst.split(":", 1)
+        with open(src, "rb") as f:
+            data = f.read()
+        if len(data) > 1 << 20:
+            raise SystemExit("error: kubectl cp into a pod supports files up to 1 MiB")
+        import base64
+        b64 = base64.b64encode(data).decode()
+        rc, out, err = await self._exec(pod.split("/")[-1], a.container,
+                                        ["sh", "-c", f"printf %s '{b64}' | base64 -d > '{path}'"])
+        if rc != 0:
+            raise SystemExit(f"error: {err.decode() or out.decode()}")
+
+    async def cmd_proxy(self):
+        """`kubectl proxy`: a local HTTP endpoint forwarding to the API server with this
+        kubeconfig's credentials (`pkg/kubectl/proxy/proxy_server.go`)."""
+        from ..utils.httpserver import HTTPServer, Response, StreamResponse
+        a = self.a
+        http = self.client.http
+
+        async def handle(req):
+            path = req.raw_path + (("?" + req.qs) if req.qs else "")
+            if req.query.get("watch") in ("true", "1") or "/watch/" in req.raw_path:
+                st, hdrs, r, w = await http.open_raw(req.method, path)
+
+                async def relay(cw):
+                    try:
+                        while True:
+                            line = await r.readuntil(b"\r\n")
+                            n = int(line.strip(), 16)
+                            if n == 0:
+                                break
+                            cw.write(await r.readexactly(n))
+                            await r.readexactly(2)
+                    finally:
+                        w.close()
+                return StreamResponse(relay, hdrs.get("content-type", "application/json"))
+            st, body = await http.request(req.method, path, req.body or None,
+                                          req.headers.get("content-type", "application/json"))
+            return Response(st, body)
+        srv = HTTPServer(handle)
+        port = await srv.start(a.address, a.port)
+        self.p(f"Starting to serve on {a.address}:{port}")
+        if hasattr(self.out, "flush"):
+            self.out.flush()
+        try:
+            if a.serve_seconds:
+                await asyncio.sleep(a.serve_seconds)
+            else:
+                await asyncio.Event().wait()
+        finally:
+            await srv.stop()
+
+    async def cmd_edit(self):
+        """`kubectl edit`: dump YAML, run $EDITOR, PUT the result if it changed."""
+        import subprocess
+        import tempfile
+        (ri, name), = split_targets(self.a.targets)
+        obj = await self.client.get(ri.plural, name, self.ns_for(ri))
+        text = yaml.safe_dump(obj, sort_keys=False)
+        with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
+            f.write(text)
+            path = f.name
+        try:
+            editor = os.environ.get("KUBE_EDITOR") or os.environ.get("EDITOR") or "vi"
+            rc = subprocess.call(editor.split() + [path])
+            if rc != 0:
+                raise SystemExit(f"error: editor exited with {rc}")
+            with open(path) as f:
+                new_text = f.read()
+        finally:
+            os.unlink(path)
+        if new_text == text:
+            self.p("Edit cancelled, no changes made.")
+            return
+        new = yaml.safe_load(new_text)
+        await self.client.update(ri.plural, new, self.ns_for(ri))
+        self.p(f"{ri.kind.lower()}/{name} edited")
 
 
 def cmd_config(a):
@@ -608,8 +791,30 @@ def build_parser():
     au.add_argument("can_i", choices=["can-i"])
     au.add_argument("verb")
     au.add_argument("resource")
-    for name in ("exec", "attach", "port-forward", "cp", "edit", "proxy"):
-        add(name).add_argument("rest", nargs="*")
+    exq = add("exec")
+    exq.add_argument("pod")
+    exq.add_argument("-c", "--container")
+    exq.add_argument("-i", "--stdin", action="store_true")
+    exq.add_argument("-t", "--tty", action="store_true")
+    exq.add_argument("exec_command", nargs=argparse.REMAINDER)
+    at = add("attach")
+    at.add_argument("pod")
+    at.add_argument("-c", "--container")
+    pf = add("port-forward")
+    pf.add_argument("pod")
+    pf.add_argument("ports", nargs="+")
+    pf.add_argument("--address", default="127.0.0.1")
+    pf.add_argument("--max-connections", type=int, default=0, help=argparse.SUPPRESS)
+    cpp = add("cp")
+    cpp.add_argument("src")
+    cpp.add_argument("dst")
+    cpp.add_argument("-c", "--container")
+    px = add("proxy")
+    px.add_argument("-p", "--port", type=int, default=8001)
+    px.add_argument("--address", default="127.0.0.1")
+    px.add_argument("--serve-seconds", type=float, default=0, help=argparse.SUPPRESS)
+    ed = add("edit")
+    ed.add_argument("targets", nargs="+")
     cf = add("config")
     cf.add_argument("action", choices=["view", "current-context", "get-contexts", "use-context", "set-cluster",
                                        "set-context", "set-credentials"])
@@ -629,9 +834,8 @@ def main(argv=None, out=sys.stdout):
         cmd_config(a)
         return 0
     k = Kubectl(a, out)
+    k.rc = 0
     name = "cmd_" + a.command.replace("-", "_")
-    if a.command in ("exec", "attach", "port-forward", "cp", "edit", "proxy"):
-        name = "cmd_unsupported"
 
     async def go():
         try:
@@ -646,4 +850,4 @@ def main(argv=None, out=sys.stdout):
     except (ConnectionError, OSError) as e:
         print(f"The connection to the server {k.server} was refused - did you specify the right host or port? ({e})", file=sys.stderr)
         return 1
-    return 0
+    return k.rc

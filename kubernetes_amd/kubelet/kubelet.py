@@ -40,6 +40,7 @@ from .devicemanager.manager import AdmitError, ManagerStub
 from .prober import ProbeManager
 from .runtime.base import EXITED, RUNNING, RunContainerOptions
 from .volumes import VolumeError, VolumeManager
+from ..utils.tasks import spawn
 
 log = logging.getLogger("kubelet")
 
@@ -48,7 +49,8 @@ _ip_counter = itertools.count(2)
 
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
-                 "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes")
+                 "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
+                 "waiting")
 
     def __init__(self, pod):
         self.uid = pod["metadata"]["uid"]
@@ -68,6 +70,7 @@ class PodState:
         self.running_at = None
         self.first_seen = time.time()
         self.volumes = None            # {volume name: host path} once mounted
+        self.waiting: dict[str, tuple] = {}   # container -> (reason, message) while it cannot start
 
 
 class Kubelet:
@@ -75,7 +78,8 @@ class Kubelet:
                  labels=None, node_status_update_frequency=10.0, status_debounce=0.02, http_port=None,
                  emit_events=True, register=True, metrics=None, address="127.0.0.1", max_status_inflight=64,
                  root_dir=None, cpu_manager_policy="none", cpu_topology=None, reserved_cpus=1,
-                 pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0):
+                 pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0,
+                 image_service=None, image_gc=None, image_backoff=10.0):
         self.client = client
         self.pod_manifest_path = pod_manifest_path
         self.static_pods = None
@@ -125,6 +129,22 @@ class Kubelet:
         self.http = None
         self.node_uid = None
         self.runtime.on_exit(self._on_container_exit)
+        # image manager (pkg/kubelet/images): the CRI image service of a remote runtime, or an
+        # in-process image store for the in-process runtimes
+        if image_service is None:
+            image_service = getattr(runtime, "images", None)
+        if image_service is None:
+            from ..cri.server import ImageStore, LocalImageService, host_image_resolver, stub_image_resolver
+            image_service = LocalImageService(ImageStore(stub_image_resolver if runtime.name == "stub" else host_image_resolver))
+        from .images import ImageGCManager, ImageManager
+        self.image_service = image_service
+        self.images = ImageManager(image_service, self.recorder, backoff_initial=image_backoff)
+        self.image_gc = None
+        if image_gc:
+            self.image_gc = ImageGCManager(image_service, int(image_gc.get("capacity_bytes", 0)), self._images_in_use,
+                                           image_gc.get("high", 85), image_gc.get("low", 80), image_gc.get("min_age", 120.0),
+                                           last_used=self.images.last_used)
+            self.image_gc_period = float(image_gc.get("period", 300.0))
         self.started = asyncio.Event()
         self.plugin_labels = {}
         self.informer_node_labels = {}
@@ -153,7 +173,25 @@ class Kubelet:
             self.static_pods.start()
         if self.eviction is not None:
             self._tasks.append(asyncio.ensure_future(self._eviction_loop()))
+        if self.image_gc is not None:
+            self._tasks.append(asyncio.ensure_future(self._image_gc_loop()))
         self.started.set()
+
+    def _images_in_use(self):
+        return {c.get("image", "") for s in self.pods.values() if not s.deleted
+                for c in list((s.pod.get("spec") or {}).get("containers") or ()) +
+                list((s.pod.get("spec") or {}).get("initContainers") or ())}
+
+    async def _image_gc_loop(self):
+        """image_gc_manager.go: GarbageCollect every ImageGCPeriod (5 min)."""
+        while not self._stopped:
+            await asyncio.sleep(self.image_gc_period)
+            try:
+                freed = await self.image_gc.garbage_collect()
+                if freed:
+                    log.info("image GC freed %d bytes", freed)
+            except Exception as e:
+                log.warning("image garbage collection failed: %s", e)
 
     async def _eviction_loop(self):
         """eviction_manager.go synchronize(): observe, set pressure conditions, evict <= 1 pod."""
@@ -474,6 +512,16 @@ class Kubelet:
         await self._report(st)
 
     async def _start(self, st, c):
+        from .images import ImagePullError
+        try:
+            await self.images.ensure_image_exists(st.pod, c)
+            st.waiting.pop(c["name"], None)
+        except ImagePullError as e:
+            st.waiting[c["name"]] = (e.reason, e.message)
+            await self._report(st)
+            asyncio.get_running_loop().call_later(max(0.05, self.images.retry_after(c.get("image", ""))),
+                                                  self._resync, st.uid)
+            return None
         try:
             opts = RunContainerOptions.from_device_opts(await self.dm.init_container(st.pod, c))
         except Exception as e:
@@ -550,7 +598,7 @@ class Kubelet:
         async def kill():
             await self.runtime.stop_container(cid, 0)
             self._resync(uid)
-        asyncio.ensure_future(kill())
+        spawn(kill())
 
     async def _kill_pod(self, st: PodState, grace):
         self.probes.remove_pod(st.uid)
@@ -592,7 +640,7 @@ class Kubelet:
         for c in spec.get("containers") or ():
             cid = st.containers.get(c["name"])
             cs = rt.container_status(cid) if cid else None
-            s = _container_status(c, cs, st.restarts.get(c["name"], 0))
+            s = _container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"]))
             statuses.append(s)
             if cs is None:
                 waiting += 1
@@ -612,7 +660,7 @@ class Kubelet:
         for c in spec.get("initContainers") or ():
             cid = st.init_containers.get(c["name"])
             cs = rt.container_status(cid) if cid else None
-            init_statuses.append(_container_status(c, cs, st.restarts.get(c["name"], 0)))
+            init_statuses.append(_container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"])))
             if cs is None or cs.state != EXITED or cs.exit_code != 0:
                 init_done = False
         policy = spec.get("restartPolicy", "Always")
@@ -735,6 +783,10 @@ class Kubelet:
         if p.startswith("/debug/pprof"):
             from ..utils.profiling import handle_debug
             return await handle_debug(req)
+        from . import server_streaming
+        r = await server_streaming.handle(self, req)
+        if r is not None:
+            return r
         return Response(404, b"not found", "text/plain")
 
 
@@ -750,10 +802,13 @@ def _ts(t):
     return now_rfc3339(t) if t else None
 
 
-def _container_status(c, cs, restarts):
+def _container_status(c, cs, restarts, waiting=None):
     s = {"name": c["name"], "image": c.get("image", ""), "imageID": "", "restartCount": restarts, "ready": False}
     if cs is None:
-        s["state"] = {"waiting": {"reason": "ContainerCreating"}}
+        if waiting:
+            s["state"] = {"waiting": {"reason": waiting[0], "message": waiting[1]}}
+        else:
+            s["state"] = {"waiting": {"reason": "ContainerCreating"}}
         return s
     s["containerID"] = cs.id
     if cs.state == RUNNING:

@@ -23,6 +23,7 @@ import time
 from ...native import BIN_DIR
 from . import oci
 from .base import CREATED, EXITED, RUNNING, ContainerStatus, Runtime, RunContainerOptions
+from ...utils.tasks import spawn
 
 IMAGES = {
     "kubernetes-amd/hip-vector-add": [os.path.join(BIN_DIR, "hip-vector-add")],
@@ -156,7 +157,7 @@ class ProcessRuntime(Runtime):
         m["proc"] = proc
         st.state = RUNNING
         st.started_at = time.time()
-        asyncio.ensure_future(self._wait(cid, proc))
+        spawn(self._wait(cid, proc))
 
     async def _wait(self, cid, proc):
         code = await proc.wait()

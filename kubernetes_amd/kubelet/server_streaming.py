@@ -1,0 +1,125 @@
+"""Kubelet server streaming endpoints: /exec, /attach, /run, /portForward.
+
+Parity: `pkg/kubelet/server/server.go:303-360` (routes `/run/{ns}/{pod}/{container}`,
+`/exec/{ns}/{pod}/{container}`, `/attach/...`, `/portForward/{ns}/{pod}`, with optional `{uid}`)
+and `getExec`/`getPortForward` (`:600-700`): with a CRI runtime the kubelet obtains a streaming
+URL from the runtime (`Exec`/`PortForward` RPCs) and proxies it; for the in-process runtimes it
+serves the stream itself. Exec streams use the framed protocol of `cri/server.py`; stdin is
+not supported (non-interactive exec, like `kubectl exec` without `-i`).
+"""
+from __future__ import annotations
+
+import asyncio
+from urllib.parse import parse_qs
+
+from ..cri.server import splice
+from ..utils.httpserver import Response, StreamResponse, UpgradeResponse
+
+
+def _frames(rc, out):
+    body = b""
+    if out:
+        p = b"\x01" + (out if isinstance(out, bytes) else str(out).encode())
+        body += b"%x\r\n%s\r\n" % (len(p), p)
+    p = b"\x03" + str(rc).encode()
+    return body + b"%x\r\n%s\r\n" % (len(p), p)
+
+
+def _find(kubelet, parts, with_container=True):
+    """parts after the verb: ns, pod, [uid,] container"""
+    if len(parts) < (3 if with_container else 2):
+        return None, None, "bad path"
+    ns, name = parts[0], parts[1]
+    uid = kubelet.by_key.get(f"{ns}/{name}")
+    st = kubelet.pods.get(uid) if uid else None
+    if st is None:
+        return None, None, f"pod {ns}/{name} not found"
+    if not with_container:
+        return st, None, None
+    cname = parts[-1]
+    cid = st.containers.get(cname) or st.init_containers.get(cname)
+    if cid is None:
+        return st, None, f"container {cname} not found in pod {ns}/{name}"
+    return st, cid, None
+
+
+async def handle(kubelet, req):
+    """Returns a Response / StreamResponse / UpgradeResponse, or None if the path is not ours."""
+    p = req.path
+    verb = p.split("/", 2)[1] if p.count("/") >= 2 else ""
+    if verb not in ("exec", "run", "attach", "portForward"):
+        return None
+    parts = [x for x in p.split("/")[2:] if x]
+    rt = kubelet.runtime
+    if verb in ("exec", "run", "attach"):
+        st, cid, err = _find(kubelet, parts)
+        if err:
+            return Response(404, err.encode(), "text/plain")
+        q = parse_qs(req.qs or "")
+        cmd = q.get("command") or q.get("cmd") or []
+        if verb == "run":   # /run returns the combined output as the body (runInContainer)
+            rc, out = await rt.exec_sync(cid, cmd, 60)
+            return Response(200 if rc == 0 else 500, out, "text/plain")
+        if verb == "attach":
+            data = await rt.container_logs(cid)
+            return StreamResponse(_static(_frames(0, data)), "application/vnd.kamd.stream")
+        if hasattr(rt, "exec_url"):
+            url = await rt.exec_url(cid, cmd)
+            return StreamResponse(_proxy_exec(url), "application/vnd.kamd.stream")
+        rc, out = await rt.exec_sync(cid, cmd, float(q.get("timeout", ["300"])[0]))
+        return StreamResponse(_static(_frames(rc, out)), "application/vnd.kamd.stream")
+    # portForward
+    st, _, err = _find(kubelet, parts, with_container=False)
+    if err:
+        return Response(404, err.encode(), "text/plain")
+    port = int(req.query.get("port") or 0)
+    if not port:
+        return Response(400, b"port is required", "text/plain")
+    if "upgrade" not in req.headers.get("connection", "").lower():
+        return Response(400, b"port-forward needs Connection: Upgrade", "text/plain")
+    if hasattr(rt, "port_forward_url"):
+        url = await rt.port_forward_url(st.sandbox, [port])
+        from ..cri.streaming import open_port_forward
+
+        async def run(reader, writer):
+            ur, uw = await open_port_forward(url, port)
+            await splice(reader, writer, ur, uw)
+        return UpgradeResponse(run)
+
+    async def run_local(reader, writer):
+        # in-process runtimes: pods share the host network namespace
+        try:
+            ur, uw = await asyncio.open_connection("127.0.0.1", port)
+        except OSError:
+            writer.close()
+            return
+        await splice(reader, writer, ur, uw)
+    return UpgradeResponse(run_local)
+
+
+def _static(raw):
+    async def run(w):
+        w.transport.write(raw)
+    return run
+
+
+def _proxy_exec(url):
+    from ..cri.streaming import _open
+
+    async def run(w):
+        r, uw, status, _ = await _open(url)
+        try:
+            if status != 200:
+                w.transport.write(_frames(126, f"exec refused by runtime: HTTP {status}".encode()))
+                return
+            # forward the runtime's chunked frames verbatim (already framed)
+            while True:
+                line = await r.readuntil(b"\r\n")
+                size = int(line.strip(), 16)
+                if size == 0:
+                    break
+                data = await r.readexactly(size + 2)
+                w.transport.write(line + data)
+        finally:
+            uw.close()
+    return run

@@ -37,6 +37,7 @@ from ..utils.trace import Trace
 from .cache import SchedulerCache
 from .generic import FitError, GenericScheduler
 from .queue import SchedulingQueue
+from ..utils.tasks import spawn
 
 log = logging.getLogger("scheduler")
 
@@ -165,7 +166,7 @@ class Scheduler:
             self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
             self.queue.add_unschedulable(pod)
             if self.update_unschedulable_status:
-                asyncio.ensure_future(self._set_unschedulable(pod, str(e)))
+                spawn(self._set_unschedulable(pod, str(e)))
             if self.preemption:
                 self._try_preempt(pod, pi)
             return None
@@ -234,11 +235,11 @@ class Scheduler:
             return
         self.m_preemptions.inc()
         md = pod["metadata"]
-        asyncio.ensure_future(self._nominate(pod, node))
+        spawn(self._nominate(pod, node))
         for v in victims:
             vmd = v["metadata"]
             self.recorder.event(v, "Normal", "Preempted", f"by {md.get('namespace')}/{md['name']} on node {node}")
-            asyncio.ensure_future(self._delete_victim(vmd.get("namespace"), vmd["name"]))
+            spawn(self._delete_victim(vmd.get("namespace"), vmd["name"]))
 
     async def _nominate(self, pod, node):
         md = pod["metadata"]

@@ -23,7 +23,7 @@ REASONS = {
 
 
 class Request:
-    __slots__ = ("method", "path", "raw_path", "query", "headers", "body", "transport", "user", "info")
+    __slots__ = ("method", "path", "raw_path", "query", "qs", "headers", "body", "transport", "user", "info")
 
     def __init__(self, method, target, headers, body, transport):
         self.method = method
@@ -31,7 +31,8 @@ class Request:
             p, qs = target.split("?", 1)
             self.query = {k: v[-1] for k, v in parse_qs(qs, keep_blank_values=True).items()}
         else:
-            p, self.query = target, {}
+            p, self.query, qs = target, {}, ""
+        self.qs = qs
         self.raw_path = p
         self.path = unquote(p)
         self.headers = headers
@@ -60,6 +61,18 @@ class StreamResponse:
     def __init__(self, run, content_type="application/json"):
         self.run = run
         self.content_type = content_type
+
+
+class UpgradeResponse:
+    """Returned by a handler that switches the connection to another protocol
+    (`Connection: Upgrade`): `101 Switching Protocols` is sent, then `run(reader, writer)` owns
+    the raw byte stream (stream-style reader/writer over the same transport)."""
+
+    __slots__ = ("run", "protocol")
+
+    def __init__(self, run, protocol="tcp"):
+        self.run = run
+        self.protocol = protocol
 
 
 class ChunkWriter:
@@ -141,7 +154,10 @@ class _Conn(asyncio.Protocol):
             self.pending.append(req)
         if self.pending and not self.busy:
             self.busy = True
-            asyncio.ensure_future(self._serve())
+            # the loop only keeps weak references to tasks: hold this one until it finishes
+            t = asyncio.ensure_future(self._serve())
+            self.server._tasks.add(t)
+            t.add_done_callback(self.server._tasks.discard)
 
     def _parse(self):
         buf = self.buf
@@ -179,6 +195,9 @@ class _Conn(asyncio.Protocol):
                     resp = Response(500, b'{"kind":"Status","status":"Failure","message":%s,"code":500}' % repr(str(e)).encode())
                 if self.transport.is_closing():
                     return
+                if isinstance(resp, UpgradeResponse):
+                    await self._upgrade(resp)
+                    return
                 if isinstance(resp, StreamResponse):
                     self.streaming = True
                     self.transport.write(
@@ -209,11 +228,39 @@ class _Conn(asyncio.Protocol):
             self.busy = False
 
 
+    async def _upgrade(self, resp):
+        loop = asyncio.get_running_loop()
+        reader = asyncio.StreamReader(loop=loop)
+        proto = asyncio.StreamReaderProtocol(reader, loop=loop)
+        self.transport.write(("HTTP/1.1 101 Switching Protocols\r\nConnection: Upgrade\r\nUpgrade: %s\r\n\r\n"
+                              % resp.protocol).encode())
+        rest = bytes(self.buf)
+        self.buf.clear()
+        self.transport.set_protocol(proto)
+        proto.connection_made(self.transport)
+        if rest:
+            reader.feed_data(rest)
+        writer = asyncio.StreamWriter(self.transport, proto, reader, loop)
+        self.streaming = True
+        # StreamReaderProtocol references its reader only weakly: keep both ends reachable
+        self.upgraded = (reader, writer)
+        try:
+            await resp.run(reader, writer)
+        except (ConnectionError, asyncio.CancelledError):
+            pass
+        finally:
+            self.streaming = False
+            self.upgraded = None
+            self.transport.close()
+            self.server._conns.discard(self)   # connection_lost now goes to the new protocol
+
+
 class HTTPServer:
     def __init__(self, handler):
         self.handler = handler
         self._server = None
         self._conns = set()
+        self._tasks = set()
         self.port = None
 
     async def start(self, host="127.0.0.1", port=0, ssl=None, reuse_port=False):
