@@ -205,7 +205,31 @@ def qos_class(pod) -> str:
     return "Burstable"
 
 
-STRATEGIES = {"pods": PodStrategy, "nodes": NodeStrategy, "namespaces": NamespaceStrategy,
+class ServiceStrategy(Strategy):
+    """`pkg/registry/core/service/strategy.go`: status subresource (load balancer ingress);
+    allocation lives in `service_alloc` (done by the API server before validation)."""
+
+    def prepare_update(self, new, old):
+        super().prepare_update(new, old)
+        ns, os_ = new.setdefault("spec", {}), old.get("spec") or {}
+        if not ns.get("clusterIP") and os_.get("clusterIP") and ns.get("type", "ClusterIP") != "ExternalName":
+            ns["clusterIP"] = os_["clusterIP"]
+        if ns.get("type", "ClusterIP") in ("NodePort", "LoadBalancer"):
+            old_np = {(p.get("port"), p.get("protocol", "TCP")): p.get("nodePort") for p in os_.get("ports") or ()}
+            for p in ns.get("ports") or ():
+                if not p.get("nodePort") and old_np.get((p.get("port"), p.get("protocol", "TCP"))):
+                    p["nodePort"] = old_np[(p.get("port"), p.get("protocol", "TCP"))]
+
+    def validate(self, obj):
+        from .service_alloc import validate_service
+        return validate_service(obj)
+
+    def validate_update(self, new, old):
+        from .service_alloc import validate_service_update
+        return validate_service_update(new, old)
+
+
+STRATEGIES = {"pods": PodStrategy, "services": ServiceStrategy, "nodes": NodeStrategy, "namespaces": NamespaceStrategy,
               "events": NoStatusStrategy, "configmaps": NoStatusStrategy, "secrets": NoStatusStrategy,
               "serviceaccounts": NoStatusStrategy, "endpoints": NoStatusStrategy,
               "limitranges": NoStatusStrategy, "priorityclasses": NoStatusStrategy,

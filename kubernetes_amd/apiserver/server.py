@@ -96,7 +96,10 @@ class APIServer:
     def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
                  max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
-                 kubelet_port_resolver=None, audit=None, encryption_config=None):
+                 kubelet_port_resolver=None, audit=None, encryption_config=None,
+                 service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767)):
+        from .service_alloc import ServiceAllocator
+        self.svc_alloc = ServiceAllocator(service_cluster_ip_range, service_node_port_range)
         # encryption at rest (--experimental-encryption-provider-config): plural -> PrefixTransformers
         self.transformers = {}
         if encryption_config:
@@ -215,6 +218,18 @@ class APIServer:
                 except APIError as e:
                     if e.code != 409:   # another worker created it first
                         raise
+        # the `kubernetes` service on the first IP of the service range
+        # (pkg/master/controller.go CreateOrUpdateMasterServiceIfNeeded)
+        if self.get_object("services", "default", "kubernetes") is None:
+            svc = {"metadata": {"name": "kubernetes", "namespace": "default",
+                                "labels": {"component": "apiserver", "provider": "kubernetes"}},
+                   "spec": {"clusterIP": self.svc_alloc.kubernetes_ip, "type": "ClusterIP", "sessionAffinity": "None",
+                            "ports": [{"name": "https", "port": 443, "protocol": "TCP", "targetPort": 6443}]}}
+            try:
+                await self._retrying(lambda: self.create(m.BY_PLURAL["services"], "default", svc, admit=False))
+            except APIError as e:
+                if e.code not in (409, 422):
+                    raise
 
     # ------------------------------------------------------------------
     # shared-store mode
@@ -329,6 +344,15 @@ class APIServer:
     async def _async_existing(self, ri, namespace, name):
         return self._existing(ri, namespace, name)
 
+    def _claim_keys(self, ri, obj):
+        """Keys that must be absent in the store for `obj` to be written (shared mode): GPU device
+        assignments of pods, ClusterIPs / NodePorts of services."""
+        if ri.plural == "pods":
+            return self._device_keys(obj)
+        if ri.plural == "services":
+            return self.svc_alloc.claim_keys(obj)
+        return set()
+
     @staticmethod
     def _device_keys(pod):
         if pod is None or core.pod_is_terminal(pod):
@@ -366,9 +390,9 @@ class APIServer:
             ops = [(wire.OP_PUT_INJECT, key, stored, tok)]
         else:
             ops = [(wire.OP_PUT, key, stored)]   # binary values are never rewritten
-        if ri.plural == "pods":
-            old_d = self._device_keys(prev.obj if prev is not None else None)
-            new_d = set() if etype == DELETED else self._device_keys(obj)
+        if ri.plural in ("pods", "services"):
+            old_d = self._claim_keys(ri, prev.obj if prev is not None else None)
+            new_d = set() if etype == DELETED else self._claim_keys(ri, obj)
             kb = key.encode()
             for dk in sorted(new_d - old_d):
                 cmps.append((wire.CMP_ABSENT, dk, 0, None))
@@ -391,7 +415,10 @@ class APIServer:
             if res.failed == 0:
                 raise _Stale(res.rev)
             owner = res.current.value.decode() if res.current is not None else "?"
-            dev = cmps[res.failed][1][len(DEVICE_PREFIX):]
+            claim = cmps[res.failed][1]
+            if not claim.startswith(DEVICE_PREFIX):
+                raise APIError(409, "Conflict", f"{claim.rsplit('/', 1)[-1]} is already allocated to {owner}")
+            dev = claim[len(DEVICE_PREFIX):]
             raise APIError(409, "Conflict", f"device {dev} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
         await self._wait_applied(res.rev)
         self._mine.pop((key, res.rev), None)
@@ -474,6 +501,8 @@ class APIServer:
         if admit:
             a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
             self._admit(a)
+        if ri.plural == "services":
+            return await self._create_service(ri, ns, obj, a if admit else None)
         errs = strat.validate(obj)
         if errs:
             raise invalid(ri, m.name_of(obj), errs)
@@ -483,6 +512,32 @@ class APIServer:
         if key in self.caches[ri.plural].by_key:
             raise already_exists(ri, m.name_of(obj))
         return await self._commit(ri, key, ADDED, obj, None)
+
+    async def _create_service(self, ri, ns, obj, a):
+        from .service_alloc import AllocationError
+        strat = self.strategies[ri.plural]
+        key = m.key_for(ri, ns, m.name_of(obj))
+        base = fast_copy(obj)
+        for attempt in range(8):
+            obj = fast_copy(base)
+            try:
+                auto = self.svc_alloc.allocate(obj, self.list_objects("services"))
+            except AllocationError as e:
+                raise APIError(e.code, "Invalid" if e.code == 422 else "InternalError", str(e))
+            errs = strat.validate(obj)
+            if errs:
+                raise invalid(ri, m.name_of(obj), errs)
+            if a is not None:
+                a.obj = obj
+                self._validate_admission(a)
+            if key in self.caches[ri.plural].by_key:
+                raise already_exists(ri, m.name_of(obj))
+            try:
+                return await self._commit(ri, key, ADDED, obj, None)
+            except APIError as e:
+                # another API server worker allocated the same IP / port first: pick again
+                if e.code != 409 or "already allocated" not in e.message or not auto or attempt == 7:
+                    raise
 
     def _admit(self, a):
         try:
@@ -681,7 +736,25 @@ class APIServer:
     async def start(self, host="127.0.0.1", port=0, reuse_port=False):
         if self.remote_address and self.rstore is None:
             await self._start_remote()
-        return await self.http.start(host, port, reuse_port=reuse_port)
+        port = await self.http.start(host, port, reuse_port=reuse_port)
+        await self._reconcile_master_endpoints("127.0.0.1" if host in ("0.0.0.0", "") else host, port)
+        return port
+
+    async def _reconcile_master_endpoints(self, ip, port):
+        """Endpoints of the `kubernetes` service = this API server (master EndpointReconciler)."""
+        subsets = [{"addresses": [{"ip": ip}], "ports": [{"name": "https", "port": port, "protocol": "TCP"}]}]
+        ri = m.BY_PLURAL["endpoints"]
+        cur = self.get_object("endpoints", "default", "kubernetes")
+        try:
+            if cur is None:
+                await self._retrying(lambda: self.create(ri, "default", {"metadata": {"name": "kubernetes", "namespace": "default"},
+                                                                          "subsets": subsets}, admit=False))
+            elif cur.get("subsets") != subsets:
+                await self._retrying(lambda: self.guaranteed_update(ri, "default", "kubernetes",
+                                                                    lambda o: o.__setitem__("subsets", subsets)))
+        except APIError as e:
+            if e.code != 409:
+                log.warning("master endpoints reconcile failed: %s", e)
 
     async def stop(self):
         await self.http.stop()

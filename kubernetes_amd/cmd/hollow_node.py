@@ -15,11 +15,31 @@ def main(argv=None):
     ap.add_argument("--name-prefix", default="hollow")
     ap.add_argument("--gpus-per-node", type=int, default=8)
     ap.add_argument("--hives", type=int, default=1)
+    ap.add_argument("--morph", default="kubelet", choices=["kubelet", "proxy"],
+                    help="kubelet: hollow kubelets; proxy: hollow kube-proxies over a fake iptables (hollow-node.go:139+)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
 
     async def start():
+        if a.morph == "proxy":
+            from ..client.rest import Client
+            from ..proxy.iptables import FakeIptables
+            from ..proxy.server import ProxyServer
+
+            class Proxies:
+                def __init__(self):
+                    self.items = [ProxyServer(Client(a.master), f"{a.name_prefix}-{i}", "iptables", iptables=FakeIptables())
+                                  for i in range(a.count)]
+
+                async def stop(self):
+                    for p in self.items:
+                        await p.stop()
+            ps = Proxies()
+            for p in ps.items:
+                await p.start()
+            print(f"{a.count} hollow proxies syncing (fake iptables)", flush=True)
+            return ps
         h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives)
         await h.start()
         await h.wait_registered()

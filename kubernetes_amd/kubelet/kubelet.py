@@ -427,6 +427,8 @@ class Kubelet:
             if core.pod_is_terminal(pod):
                 return
             st = self.pods[uid] = PodState(pod)
+            if getattr(self.runtime, "shares_host_network", False) or (pod.get("spec") or {}).get("hostNetwork"):
+                st.ip = self.address     # no network namespace: the pod is reachable on the node address
             self.by_key[_key(pod)] = uid
         else:
             st.pod = pod

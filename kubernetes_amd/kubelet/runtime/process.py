@@ -47,6 +47,7 @@ def resolve_command(container):
 
 class ProcessRuntime(Runtime):
     name = "process"
+    shares_host_network = True     # containers are host processes: pod IP = node address
 
     def __init__(self, root_dir: str, inherit_env: bool = True):
         super().__init__()
