@@ -95,7 +95,25 @@ RESOURCES = [
     ResourceInfo("autoscaling", "v1", "HorizontalPodAutoscaler", "horizontalpodautoscalers", True, ("hpa",)),
     ResourceInfo("storage.k8s.io", "v1", "StorageClass", "storageclasses", False, ("sc",)),
     ResourceInfo("apiextensions.k8s.io", "v1beta1", "CustomResourceDefinition", "customresourcedefinitions", False, ("crd",)),
+    ResourceInfo("admissionregistration.k8s.io", "v1beta1", "MutatingWebhookConfiguration",
+                 "mutatingwebhookconfigurations", False, ()),
+    ResourceInfo("admissionregistration.k8s.io", "v1beta1", "ValidatingWebhookConfiguration",
+                 "validatingwebhookconfigurations", False, ()),
+    ResourceInfo("apiregistration.k8s.io", "v1beta1", "APIService", "apiservices", False, ()),
+    ResourceInfo("certificates.k8s.io", "v1beta1", "CertificateSigningRequest", "certificatesigningrequests", False, ("csr",)),
+    ResourceInfo("networking.k8s.io", "v1", "NetworkPolicy", "networkpolicies", True, ("netpol",)),
+    ResourceInfo("extensions", "v1beta1", "Ingress", "ingresses", True, ("ing",)),
+    ResourceInfo("policy", "v1beta1", "PodSecurityPolicy", "podsecuritypolicies", False, ("psp",)),
+    ResourceInfo("settings.k8s.io", "v1alpha1", "PodPreset", "podpresets", True, ()),
+    ResourceInfo("storage.k8s.io", "v1beta1", "VolumeAttachment", "volumeattachments", False, ()),
+    # virtual (create-only, never stored): answered from the authenticator / authorizer
+    ResourceInfo("authentication.k8s.io", "v1", "TokenReview", "tokenreviews", False, ()),
+    ResourceInfo("authorization.k8s.io", "v1", "SubjectAccessReview", "subjectaccessreviews", False, ()),
+    ResourceInfo("authorization.k8s.io", "v1", "SelfSubjectAccessReview", "selfsubjectaccessreviews", False, ()),
+    ResourceInfo("authorization.k8s.io", "v1", "LocalSubjectAccessReview", "localsubjectaccessreviews", True, ()),
 ]
+
+VIRTUAL = {"tokenreviews", "subjectaccessreviews", "selfsubjectaccessreviews", "localsubjectaccessreviews"}
 
 BY_PLURAL = {r.plural: r for r in RESOURCES}
 BY_KIND = {r.kind: r for r in RESOURCES}
@@ -117,8 +135,18 @@ def register(ri: ResourceInfo):
     """Add a resource (CRDs)."""
     if ri.plural not in BY_PLURAL:
         RESOURCES.append(ri)
+    else:
+        RESOURCES[:] = [r for r in RESOURCES if r.plural != ri.plural] + [ri]
     BY_PLURAL[ri.plural] = ri
     BY_KIND[ri.kind] = ri
+
+
+def unregister(ri: ResourceInfo):
+    if BY_PLURAL.get(ri.plural) == ri:
+        del BY_PLURAL[ri.plural]
+        RESOURCES[:] = [r for r in RESOURCES if r != ri]
+    if BY_KIND.get(ri.kind) == ri:
+        del BY_KIND[ri.kind]
 
 
 def key_for(ri: ResourceInfo, namespace: str | None, name: str) -> str:

@@ -26,7 +26,7 @@ class FieldError:
         self.type, self.field, self.detail = type_, field, detail
 
     def __str__(self):
-        return f"{self.field}: {self.type}: {self.detail}"
+        return f"{self.field}: {self.type}: {self.detail}" if self.detail != "" else f"{self.field}: {self.type}"
 
     __repr__ = __str__
 

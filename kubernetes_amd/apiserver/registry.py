@@ -235,7 +235,10 @@ STRATEGIES = {"pods": PodStrategy, "services": ServiceStrategy, "nodes": NodeStr
               "limitranges": NoStatusStrategy, "priorityclasses": NoStatusStrategy,
               "leases": NoStatusStrategy, "roles": NoStatusStrategy, "rolebindings": NoStatusStrategy,
               "clusterroles": NoStatusStrategy, "clusterrolebindings": NoStatusStrategy,
-              "controllerrevisions": NoStatusStrategy, "storageclasses": NoStatusStrategy}
+              "controllerrevisions": NoStatusStrategy, "storageclasses": NoStatusStrategy,
+              "mutatingwebhookconfigurations": NoStatusStrategy, "validatingwebhookconfigurations": NoStatusStrategy,
+              "networkpolicies": NoStatusStrategy, "podsecuritypolicies": NoStatusStrategy,
+              "podpresets": NoStatusStrategy}
 
 
 def strategy_for(ri):

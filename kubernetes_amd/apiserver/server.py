@@ -99,7 +99,11 @@ class APIServer:
                  kubelet_port_resolver=None, audit=None, encryption_config=None,
                  service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767)):
         from .service_alloc import ServiceAllocator
+        from .extensions import Aggregator, CRDManager, WebhookDispatcher
         self.svc_alloc = ServiceAllocator(service_cluster_ip_range, service_node_port_range)
+        self.webhooks = WebhookDispatcher(self)
+        self.crds = CRDManager(self)
+        self.aggregator = Aggregator(self)
         # encryption at rest (--experimental-encryption-provider-config): plural -> PrefixTransformers
         self.transformers = {}
         if encryption_config:
@@ -164,6 +168,23 @@ class APIServer:
         self.strategies[ri.plural] = strategy_for(ri)
         self._store_res[m.prefix_for(ri).split("/")[2]] = ri.plural
 
+    def install_resource(self, ri):
+        """Serve a new resource (CRD established)."""
+        m.register(ri)
+        if ri.plural not in self.caches:
+            self._install(ri)
+
+    def uninstall_resource(self, ri):
+        self.caches.pop(ri.plural, None)
+        self.strategies.pop(ri.plural, None)
+        self._store_res = {k: v for k, v in self._store_res.items() if v != ri.plural}
+        m.unregister(ri)
+
+    def _observe(self, plural, obj, deleted):
+        """Side effects of objects entering / leaving the caches on every worker."""
+        if plural == "customresourcedefinitions" and obj is not None:
+            self.crds.observe(obj, deleted)
+
     def _cache_for_key(self, key):
         parts = key.split("/", 3)
         if len(parts) <= 3:
@@ -207,6 +228,7 @@ class APIServer:
                 cache.by_key[kv.key] = cache.make_entry(obj, raw, kv.mod_rev)
                 if ri.plural == "pods":
                     self._index_pod(kv.key, None, obj)
+                self._observe(ri.plural, obj, False)
             cache.rev = self.store.revision
 
     async def bootstrap(self):
@@ -277,13 +299,18 @@ class APIServer:
                 obj, raw = self._decode_value(kv)
                 entry = cache.make_entry(obj, raw, kv.mod_rev)
         prev = cache.by_key.get(kv.key)
+        plural = cache.resource
         if not dispatch:
             cache.by_key[kv.key] = entry
+            if plural == "customresourcedefinitions":
+                self._observe(plural, entry.obj, False)
             return
         etype = DELETED if t == wire.OP_DELETE else (MODIFIED if prev is not None else ADDED)
         if etype == DELETED and prev is None:
             return
         cache.apply(etype, kv.key, entry, prev)
+        if plural == "customresourcedefinitions":
+            self._observe(plural, entry.obj if etype != DELETED else prev.obj, etype == DELETED)
 
     def _on_store_event(self, t, kv):
         if t is None:
@@ -469,6 +496,8 @@ class APIServer:
         if ri.plural == "pods":
             self._index_pod(key, prev.obj if prev else None, None if etype == DELETED else obj)
         cache.apply(etype, key, entry, prev)
+        if ri.plural == "customresourcedefinitions":
+            self._observe(ri.plural, obj, etype == DELETED)
         return entry
 
     def _index_pod(self, key, old, new):
@@ -501,17 +530,47 @@ class APIServer:
         if admit:
             a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
             self._admit(a)
+            obj = await self._mutating_webhooks(a, ri)
         if ri.plural == "services":
             return await self._create_service(ri, ns, obj, a if admit else None)
-        errs = strat.validate(obj)
+        errs = self._validate_new(ri, strat, obj)
         if errs:
             raise invalid(ri, m.name_of(obj), errs)
         if admit:
             self._validate_admission(a)
+            await self._validating_webhooks(a, ri)
         key = m.key_for(ri, ns, m.name_of(obj))
         if key in self.caches[ri.plural].by_key:
             raise already_exists(ri, m.name_of(obj))
         return await self._commit(ri, key, ADDED, obj, None)
+
+    # ------------------------------------------------------------------ extension hooks
+    _NO_WEBHOOKS = ("mutatingwebhookconfigurations", "validatingwebhookconfigurations")
+
+    async def _mutating_webhooks(self, a, ri):
+        if ri.plural not in self._NO_WEBHOOKS and self.webhooks.has_any():
+            await self.webhooks.run(a, ri, True)
+        return a.obj
+
+    async def _validating_webhooks(self, a, ri):
+        if ri.plural not in self._NO_WEBHOOKS and self.webhooks.has_any():
+            await self.webhooks.run(a, ri, False)
+
+    def _validate_new(self, ri, strat, obj, old=None):
+        if ri.plural == "customresourcedefinitions":
+            from .extensions import validate_crd
+            errs = validate_crd(obj)
+            if not errs and old is None:
+                self.crds.prepare(obj)
+            return errs
+        errs = strat.validate(obj) if old is None else strat.validate_update(obj, old)
+        if ri.plural in self.crds.schemas:
+            from ..api.validation import FieldError
+            for e in self.crds.validate_object(ri, obj):
+                fld, _, rest = e.partition(": ")
+                typ, _, detail = rest.partition(": ")
+                errs = list(errs) + [FieldError(typ, fld, detail)]
+        return errs
 
     async def _create_service(self, ri, ns, obj, a):
         from .service_alloc import AllocationError
@@ -593,12 +652,15 @@ class APIServer:
                     nm["generation"] = om["generation"] + 1
         a = adm.Attributes(adm.UPDATE, ri.plural, subresource, namespace, name, obj, old, user, ri.kind)
         self._admit(a)
+        obj = await self._mutating_webhooks(a, ri)
+        nm = obj["metadata"]
         # a status update keeps the (already validated) spec, so only metadata + status are checked
         # (reference: ValidatePodStatusUpdate / ValidateNodeUpdate on the status subresource)
-        errs = strat.validate_update(obj, old) if subresource == "" else strat.validate_status(obj)
+        errs = self._validate_new(ri, strat, obj, old) if subresource == "" else strat.validate_status(obj)
         if errs:
             raise invalid(ri, name, errs)
         self._validate_admission(a)
+        await self._validating_webhooks(a, ri)
         # finalizers drained on an object that is being deleted -> delete it now
         if nm.get("deletionTimestamp") and not nm.get("finalizers") and self._grace_expired(ri, obj):
             return await self._commit(ri, key, DELETED, obj, prev)
@@ -646,6 +708,16 @@ class APIServer:
         a = adm.Attributes(adm.DELETE, ri.plural, "", namespace, name, None, old, user, ri.kind, opts)
         self._admit(a)
         self._validate_admission(a)
+        await self._validating_webhooks(a, ri)
+        if ri.plural == "customresourcedefinitions" and m.name_of(old) in self.crds.installed:
+            # finalizer controller: custom objects go before their definition
+            cri = self.crds.installed[m.name_of(old)]
+            for o in list(self.list_objects(cri.plural)):
+                try:
+                    await self.delete(cri, m.namespace_of(o) or None, m.name_of(o), {}, user)
+                except APIError as e:
+                    if e.code != 404:
+                        raise
         strat = self.strategies[ri.plural]
         obj = dict(old)                      # copy-on-write: only metadata/status are rewritten
         om = obj["metadata"] = dict(old["metadata"])
@@ -781,6 +853,9 @@ class APIServer:
             group, version, rest = parts[1], parts[2], parts[3:]
         else:
             return None
+        if group and self.aggregator.lookup(group, version) is not None and \
+                not any(r.group == group and r.version == version for r in m.RESOURCES if r.plural in self.caches):
+            return ("aggregated", self.aggregator.lookup(group, version))
         if not rest:
             return ("discovery", "resources", group, version)
         watch = False
@@ -793,7 +868,7 @@ class APIServer:
             rest = rest[2:]
         plural = rest[0]
         ri = m.BY_PLURAL.get(plural)
-        if ri is None or ri.group != group:
+        if ri is None or ri.group != group or plural not in self.caches:
             if plural == "bindings" and ns:
                 return ("bindings", ns)
             return None
@@ -848,6 +923,10 @@ class APIServer:
             if parsed[0] == "discovery":
                 code = 200
                 return self._discovery(parsed)
+            if parsed[0] == "aggregated":
+                resp = await self.aggregator.proxy(req, parsed[1])
+                code = resp.status
+                return resp
             if parsed[0] == "bindings":
                 resource, sub = "pods", "binding"
                 body = codec.loads(req.body)
@@ -975,6 +1054,8 @@ class APIServer:
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None:
                 raise APIError(405, "MethodNotAllowed", "POST to a named resource is not allowed")
+            if ri.plural in m.VIRTUAL:
+                return self._review(ri, ns, codec.loads(body), user, req)
             self._authorize(user, "create", ns, ri.plural, "", "", ri.group, req.path)
             obj = codec.loads(body)
             if ri.namespaced and ns is None:
@@ -1006,6 +1087,43 @@ class APIServer:
             e, _ = await self.delete(ri, ns, name, opts, user)
             return Response(200, e.raw)
         raise APIError(405, "MethodNotAllowed", f"method {method} not allowed")
+
+    def _review(self, ri, ns, body, user, req):
+        """TokenReview / SubjectAccessReview / SelfSubjectAccessReview / LocalSubjectAccessReview
+        (`pkg/registry/authentication/tokenreview`, `pkg/registry/authorization/*`): answered by
+        this server's authenticator / authorizer, never stored."""
+        from .auth import User
+        out = dict(body)
+        out["kind"], out["apiVersion"] = ri.kind, ri.group_version
+        out.setdefault("metadata", {})
+        sp = body.get("spec") or {}
+        if ri.plural == "tokenreviews":
+            self._authorize(user, "create", None, ri.plural, "", "", ri.group, req.path)
+            u = self.authn.authenticate({"authorization": f"Bearer {sp.get('token', '')}"}) if self.authn else None
+            out["status"] = {"authenticated": u is not None}
+            if u is not None:
+                out["status"]["user"] = {"username": u.name, "uid": u.uid or "", "groups": list(u.groups)}
+            return _json(201, out)
+        if ri.plural == "selfsubjectaccessreviews":
+            subj = user
+        else:
+            self._authorize(user, "create", ns, ri.plural, "", "", ri.group, req.path)
+            subj = User(sp.get("user", ""), sp.get("uid", ""), list(sp.get("groups") or ()))
+        ra = sp.get("resourceAttributes")
+        nra = sp.get("nonResourceAttributes")
+        if ra is not None:
+            rns = ns if ri.plural == "localsubjectaccessreviews" else ra.get("namespace", "")
+            rec = AttributesRecord(subj, ra.get("verb", ""), rns or "", ra.get("resource", ""), ra.get("subresource", ""),
+                                   ra.get("name", ""), ra.get("group", ""), "", True)
+        elif nra is not None:
+            rec = AttributesRecord(subj, (nra.get("verb") or "get").lower(), "", "", "", "", "", nra.get("path", ""), False)
+        else:
+            raise bad_request("spec.resourceAttributes or spec.nonResourceAttributes is required")
+        ok, why = self.authz.authorize(rec)
+        out["status"] = {"allowed": bool(ok)}
+        if why:
+            out["status"]["reason"] = why
+        return _json(201, out)
 
     async def _finalize_namespace(self, name, obj, user):
         ri = m.BY_PLURAL["namespaces"]
@@ -1185,6 +1303,8 @@ class APIServer:
         for ri in m.RESOURCES:
             if ri.group:
                 groups.setdefault(ri.group, set()).add(ri.version)
+        for g, vs in self.aggregator.groups().items():
+            groups.setdefault(g, set()).update(vs)
         if kind == "apis":
             return _json(200, {"kind": "APIGroupList", "apiVersion": "v1", "groups": [
                 {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in sorted(vs)],

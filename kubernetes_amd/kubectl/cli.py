@@ -132,6 +132,37 @@ class Kubectl:
     def p(self, *s):
         print(*s, file=self.out)
 
+    async def discover(self):
+        """RESTMapper refresh from discovery (`pkg/kubectl/cmd/util/factory`'s deferred discovery
+        mapper): registers CRD / aggregated resources the static table does not know."""
+        st, body = await self.client.raw("GET", "/apis")
+        if st != 200:
+            return
+        for g in json.loads(body).get("groups") or ():
+            gv = (g.get("preferredVersion") or {}).get("groupVersion")
+            if not gv:
+                continue
+            st, body = await self.client.raw("GET", f"/apis/{gv}")
+            if st != 200:
+                continue
+            group, version = gv.split("/", 1)
+            for r in json.loads(body).get("resources") or ():
+                if "/" in r["name"] or m.BY_PLURAL.get(r["name"]):
+                    continue
+                m.register(m.ResourceInfo(group, version, r["kind"], r["name"], bool(r.get("namespaced")),
+                                          tuple(r.get("shortNames") or ())))
+
+    def _unknown_names(self):
+        a = self.a
+        names = []
+        for t in getattr(a, "targets", None) or []:
+            names += [x.split("/", 1)[0] for x in (t.split(",") if "/" not in t else [t])]
+            if "/" not in t:
+                break
+        if getattr(a, "resource", None):
+            names.append(a.resource.split(".")[0])
+        return [n for n in names if m.lookup(n) is None]
+
     def ns_for(self, ri, obj=None):
         if not ri.namespaced:
             return None
@@ -839,6 +870,11 @@ def main(argv=None, out=sys.stdout):
 
     async def go():
         try:
+            if k._unknown_names() or getattr(a, "filename", None):
+                try:
+                    await k.discover()
+                except (ConnectionError, OSError, ValueError):
+                    pass
             await getattr(k, name)()
         finally:
             await k.client.close()

@@ -1,0 +1,238 @@
+"""API extension points: mutating/validating admission webhooks, CustomResourceDefinitions with
+openAPIV3Schema validation, API aggregation (APIService proxying), access/token reviews.
+
+Parity: `staging/src/k8s.io/apiserver/pkg/admission/plugin/webhook/*/admission_test.go`,
+`test/integration/apiextensions` (CRD lifecycle), `staging/src/k8s.io/kube-aggregator` proxy tests,
+`pkg/registry/authorization/subjectaccessreview/rest_test.go`.
+"""
+import asyncio
+import base64
+import json
+
+import pytest
+
+from kubernetes_amd.apiserver.server import APIServer
+from kubernetes_amd.client.rest import APIStatusError, Client
+from kubernetes_amd.utils.httpserver import HTTPServer, Response
+
+
+async def _server(**kw):
+    s = APIServer(**kw)
+    port = await s.start()
+    return s, Client(f"http://127.0.0.1:{port}"), port
+
+
+async def _webhook_backend():
+    seen = []
+
+    async def h(req):
+        review = json.loads(req.body)
+        r = review["request"]
+        seen.append((req.path, r["operation"], r["resource"]["resource"], r["userInfo"]["username"]))
+        if req.path == "/mutate":
+            patch = [{"op": "add", "path": "/metadata/labels", "value": {"mutated-by": "webhook"}}]
+            resp = {"uid": r["uid"], "allowed": True, "patchType": "JSONPatch",
+                    "patch": base64.b64encode(json.dumps(patch).encode()).decode()}
+        else:
+            bad = (r.get("object") or {}).get("metadata", {}).get("name", "").startswith("forbidden")
+            resp = {"uid": r["uid"], "allowed": not bad}
+            if bad:
+                resp["result"] = {"code": 403, "message": "names starting with forbidden are not allowed"}
+        return Response(200, json.dumps({"kind": "AdmissionReview", "apiVersion": "admission.k8s.io/v1beta1",
+                                         "response": resp}).encode())
+    srv = HTTPServer(h)
+    port = await srv.start("127.0.0.1", 0)
+    return srv, port, seen
+
+
+def test_admission_webhooks(run):
+    async def main():
+        s, c, _ = await _server()
+        wsrv, wport, seen = await _webhook_backend()
+        try:
+            rules = [{"operations": ["CREATE"], "apiGroups": [""], "apiVersions": ["v1"], "resources": ["configmaps"]}]
+            await c.create("mutatingwebhookconfigurations", {"metadata": {"name": "m"}, "webhooks": [
+                {"name": "label.amd.com", "rules": rules, "clientConfig": {"url": f"http://127.0.0.1:{wport}/mutate"}}]})
+            await c.create("validatingwebhookconfigurations", {"metadata": {"name": "v"}, "webhooks": [
+                {"name": "deny.amd.com", "rules": rules, "clientConfig": {"url": f"http://127.0.0.1:{wport}/validate"}}]})
+            cm = await c.create("configmaps", {"metadata": {"name": "ok", "namespace": "default"}, "data": {}})
+            assert cm["metadata"]["labels"] == {"mutated-by": "webhook"}
+            with pytest.raises(APIStatusError) as e:
+                await c.create("configmaps", {"metadata": {"name": "forbidden-1", "namespace": "default"}})
+            assert e.value.code == 403 and "denied the request" in e.value.status["message"]
+            # rules don't match secrets -> no calls
+            n = len(seen)
+            await c.create("secrets", {"metadata": {"name": "s", "namespace": "default"}})
+            assert len(seen) == n
+            # namespaceSelector: the hook only applies to labelled namespaces
+            await c.patch("mutatingwebhookconfigurations", "m", {"webhooks": [
+                {"name": "label.amd.com", "rules": rules, "namespaceSelector": {"matchLabels": {"inject": "yes"}},
+                 "clientConfig": {"url": f"http://127.0.0.1:{wport}/mutate"}}]})
+            cm2 = await c.create("configmaps", {"metadata": {"name": "plain", "namespace": "default"}})
+            assert "labels" not in cm2["metadata"]
+            # failurePolicy: an unreachable hook fails closed by default, open with Ignore
+            await c.create("validatingwebhookconfigurations", {"metadata": {"name": "dead"}, "webhooks": [
+                {"name": "dead.amd.com", "rules": rules, "clientConfig": {"url": "http://127.0.0.1:1/x"}}]})
+            with pytest.raises(APIStatusError) as e:
+                await c.create("configmaps", {"metadata": {"name": "x1", "namespace": "default"}})
+            assert e.value.code == 500
+            await c.patch("validatingwebhookconfigurations", "dead", {"webhooks": [
+                {"name": "dead.amd.com", "failurePolicy": "Ignore", "rules": rules,
+                 "clientConfig": {"url": "http://127.0.0.1:1/x"}}]})
+            await c.create("configmaps", {"metadata": {"name": "x2", "namespace": "default"}})
+        finally:
+            await c.close()
+            await s.stop()
+            await wsrv.stop()
+    run(main())
+
+
+CRD = {"apiVersion": "apiextensions.k8s.io/v1beta1", "kind": "CustomResourceDefinition",
+       "metadata": {"name": "gpujobs.amd.com"},
+       "spec": {"group": "amd.com", "version": "v1", "scope": "Namespaced",
+                "names": {"plural": "gpujobs", "singular": "gpujob", "kind": "GPUJob", "shortNames": ["gj"]},
+                "validation": {"openAPIV3Schema": {"properties": {"spec": {
+                    "type": "object", "required": ["gpus"],
+                    "properties": {"gpus": {"type": "integer", "minimum": 1, "maximum": 8},
+                                   "arch": {"type": "string", "enum": ["gfx950", "gfx942"]}}}}}}}}
+
+
+def test_crd_lifecycle(run):
+    async def main():
+        s, c, port = await _server()
+        try:
+            crd = await c.create("customresourcedefinitions", json.loads(json.dumps(CRD)))
+            conds = {x["type"]: x["status"] for x in crd["status"]["conditions"]}
+            assert conds == {"NamesAccepted": "True", "Established": "True"}
+            assert crd["status"]["acceptedNames"]["listKind"] == "GPUJobList"
+            st, body = await c.raw("GET", "/apis/amd.com/v1")
+            assert st == 200 and json.loads(body)["resources"][0]["name"] == "gpujobs"
+            st, body = await c.raw("POST", "/apis/amd.com/v1/namespaces/default/gpujobs",
+                                   json.dumps({"apiVersion": "amd.com/v1", "kind": "GPUJob", "metadata": {"name": "j1"},
+                                               "spec": {"gpus": 4, "arch": "gfx950"}}).encode())
+            assert st == 201, body
+            st, body = await c.raw("POST", "/apis/amd.com/v1/namespaces/default/gpujobs",
+                                   json.dumps({"apiVersion": "amd.com/v1", "kind": "GPUJob", "metadata": {"name": "j2"},
+                                               "spec": {"gpus": 16, "arch": "sm90"}}).encode())
+            assert st == 422
+            msg = json.loads(body)["message"]
+            assert "spec.gpus" in msg and "spec.arch" in msg
+            st, body = await c.raw("POST", "/apis/amd.com/v1/namespaces/default/gpujobs",
+                                   json.dumps({"metadata": {"name": "j3"}, "spec": {}}).encode())
+            assert st == 422 and "spec.gpus: Required value" in json.loads(body)["message"]
+            st, body = await c.raw("GET", "/apis/amd.com/v1/namespaces/default/gpujobs")
+            assert [i["metadata"]["name"] for i in json.loads(body)["items"]] == ["j1"]
+            # a second CRD claiming the same plural is not established
+            dup = json.loads(json.dumps(CRD))
+            dup["metadata"]["name"] = "gpujobs.other.io"
+            dup["spec"]["group"] = "other.io"
+            d = await c.create("customresourcedefinitions", dup)
+            assert {x["type"]: x["status"] for x in d["status"]["conditions"]}["Established"] == "False"
+            # deleting the CRD removes its objects and the endpoint
+            await c.delete("customresourcedefinitions", "gpujobs.amd.com")
+            st, _ = await c.raw("GET", "/apis/amd.com/v1/namespaces/default/gpujobs")
+            assert st == 404
+            assert not [k for k in s.store.range("/registry/")[0] if k.key.startswith("/registry/gpujobs")]
+        finally:
+            await c.close()
+            await s.stop()
+    run(main())
+
+
+def test_aggregated_apiservice(run):
+    async def main():
+        s, c, _ = await _server()
+
+        async def backend(req):
+            return Response(200, json.dumps({"kind": "Metrics", "path": req.path, "user": req.headers.get("x-remote-user")}).encode())
+        b = HTTPServer(backend)
+        bport = await b.start("127.0.0.1", 0)
+        try:
+            await c.create("services", {"metadata": {"name": "metrics-server", "namespace": "kube-system"},
+                                        "spec": {"ports": [{"port": 443}]}})
+            await c.create("endpoints", {"metadata": {"name": "metrics-server", "namespace": "kube-system"},
+                                         "subsets": [{"addresses": [{"ip": "127.0.0.1"}], "ports": [{"port": bport}]}]})
+            await c.create("apiservices", {"metadata": {"name": "v1beta1.metrics.k8s.io"},
+                                           "spec": {"group": "metrics.k8s.io", "version": "v1beta1", "insecureSkipTLSVerify": True,
+                                                    "groupPriorityMinimum": 100, "versionPriority": 100,
+                                                    "service": {"namespace": "kube-system", "name": "metrics-server"}}})
+            st, body = await c.raw("GET", "/apis/metrics.k8s.io/v1beta1/nodes")
+            assert st == 200 and json.loads(body)["path"] == "/apis/metrics.k8s.io/v1beta1/nodes"
+            st, body = await c.raw("GET", "/apis")
+            assert "metrics.k8s.io" in [g["name"] for g in json.loads(body)["groups"]]
+        finally:
+            await c.close()
+            await s.stop()
+            await b.stop()
+    run(main())
+
+
+def test_access_reviews_with_rbac(run):
+    async def main():
+        from kubernetes_amd.apiserver.auth import User
+        s, c, _ = await _server(tokens={"admin-token": User("admin", "1", ["system:masters"]), "bob-token": User("bob", "2", [])},
+                                authorization_modes=("RBAC",))
+        admin = c
+        admin.http.token = "admin-token"
+        bob = Client(c.url, token="bob-token")
+        try:
+            await admin.create("roles", {"metadata": {"name": "reader", "namespace": "default"},
+                                         "rules": [{"apiGroups": [""], "resources": ["pods"], "verbs": ["get", "list"]}]})
+            await admin.create("rolebindings", {"metadata": {"name": "bob-reader", "namespace": "default"},
+                                                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": "reader"},
+                                                "subjects": [{"kind": "User", "name": "bob"}]})
+            sar = await admin.create("subjectaccessreviews", {"spec": {"user": "bob", "resourceAttributes": {
+                "namespace": "default", "verb": "list", "resource": "pods"}}})
+            assert sar["status"]["allowed"] is True
+            sar = await admin.create("subjectaccessreviews", {"spec": {"user": "bob", "resourceAttributes": {
+                "namespace": "default", "verb": "delete", "resource": "pods"}}})
+            assert sar["status"]["allowed"] is False
+            ssar = await bob.create("selfsubjectaccessreviews", {"spec": {"resourceAttributes": {
+                "namespace": "default", "verb": "get", "resource": "pods"}}})
+            assert ssar["status"]["allowed"] is True
+            tr = await admin.create("tokenreviews", {"spec": {"token": "bob-token"}})
+            assert tr["status"]["authenticated"] and tr["status"]["user"]["username"] == "bob"
+            tr = await admin.create("tokenreviews", {"spec": {"token": "nope"}})
+            assert tr["status"]["authenticated"] is False
+            with pytest.raises(APIStatusError):
+                await bob.create("subjectaccessreviews", {"spec": {"user": "x", "resourceAttributes": {"verb": "get"}}})
+        finally:
+            await bob.close()
+            await c.close()
+            await s.stop()
+    run(main())
+
+
+def test_kubectl_discovers_crd(run, tmp_path):
+    async def setup():
+        s, c, port = await _server()
+        crd = json.loads(json.dumps(CRD))
+        crd["metadata"]["name"] = "mi355xreservations.sched.amd.com"
+        crd["spec"].update({"group": "sched.amd.com", "names": {"plural": "mi355xreservations", "kind": "MI355XReservation",
+                                                                 "shortNames": ["mres"]}})
+        crd["spec"].pop("validation")
+        await c.create("customresourcedefinitions", crd)
+        await c.raw("POST", "/apis/sched.amd.com/v1/namespaces/default/mi355xreservations",
+                    json.dumps({"metadata": {"name": "r1"}, "spec": {"gpus": 8}}).encode())
+        await c.close()
+        return s, port
+
+    import asyncio as aio
+    import threading
+    loop = aio.new_event_loop()
+    s, port = loop.run_until_complete(setup())
+    t = threading.Thread(target=loop.run_forever, daemon=True)
+    t.start()
+    try:
+        # kubectl in its own process knows nothing about the CRD until it asks discovery
+        import os
+        import subprocess
+        import sys
+        r = subprocess.run([sys.executable, "-m", "kubernetes_amd.kubectl", "-s", f"http://127.0.0.1:{port}", "get", "mres"],
+                           capture_output=True, text=True, timeout=60,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr
+        assert "r1" in r.stdout
+    finally:
+        loop.call_soon_threadsafe(loop.stop)
+        t.join(5)
