@@ -33,6 +33,9 @@ class TokenAuthenticator:
                     groups = row[3].split(",") if len(row) > 3 and row[3] else []
                     self.tokens[row[0]] = User(row[1], row[2], groups + ["system:authenticated"])
 
+    def authenticate_token(self, token):
+        return self.tokens.get(token)
+
     def authenticate(self, headers):
         h = headers.get("authorization", "")
         if h.lower().startswith("bearer "):

@@ -1,0 +1,242 @@
+"""Request authenticators beyond the token file.
+
+Parity (`staging/src/k8s.io/apiserver/pkg/authentication`, `pkg/kubeapiserver/authenticator/config.go`):
+  * x509 client certificates — `request/x509/x509.go`: CommonName = user, Organization = groups,
+    chain verified against `--client-ca-file` (the TLS layer does the verification);
+  * bootstrap tokens — `plugin/pkg/auth/authenticator/token/bootstrap/bootstrap.go`: `<id>.<secret>`
+    looked up in `kube-system/bootstrap-token-<id>` (type `bootstrap.kubernetes.io/token`,
+    `usage-bootstrap-authentication: "true"`, not expired), user `system:bootstrap:<id>`, groups
+    `system:bootstrappers` + `auth-extra-groups`;
+  * service-account JWTs — `pkg/serviceaccount/jwt.go`: RS256 / ES256 signed with
+    `--service-account-key-file`, issuer `kubernetes/serviceaccount`, the referenced secret and
+    service account must still exist (`--service-account-lookup`), user
+    `system:serviceaccount:<ns>:<name>`, groups `system:serviceaccounts[:<ns>]`;
+  * webhook token review — `plugin/pkg/authenticator/token/webhook`: POST a TokenReview to a
+    remote service, results cached for `--authentication-token-webhook-cache-ttl` (2 min);
+  * union with anonymous fallback — `request/union`, `--anonymous-auth`.
+JWT signatures are computed by the native crypto library (OpenSSL EVP).
+"""
+from __future__ import annotations
+
+import base64
+import hmac
+import json
+import re
+import time
+
+from ..api.meta import parse_rfc3339
+from ..native import crypto
+from .auth import ANONYMOUS, User
+
+SA_ISSUER = "kubernetes/serviceaccount"
+BOOTSTRAP_RE = re.compile(r"^([a-z0-9]{6})\.([a-z0-9]{16})$")
+
+
+def b64url(b: bytes) -> str:
+    return base64.urlsafe_b64encode(b).rstrip(b"=").decode()
+
+
+def b64url_decode(s: str) -> bytes:
+    return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+
+
+def _der_to_raw(sig: bytes, n=32) -> bytes:
+    """DER ECDSA signature -> JOSE r||s."""
+    i = 2 if sig[1] < 0x80 else 2 + (sig[1] & 0x7F)
+    rl = sig[i + 1]
+    r = int.from_bytes(sig[i + 2:i + 2 + rl], "big")
+    j = i + 2 + rl
+    sl = sig[j + 1]
+    s = int.from_bytes(sig[j + 2:j + 2 + sl], "big")
+    return r.to_bytes(n, "big") + s.to_bytes(n, "big")
+
+
+def _raw_to_der(raw: bytes) -> bytes:
+    def integer(v):
+        b = v.to_bytes((v.bit_length() + 8) // 8 or 1, "big")
+        return b"\x02" + bytes([len(b)]) + b
+    h = len(raw) // 2
+    body = integer(int.from_bytes(raw[:h], "big")) + integer(int.from_bytes(raw[h:], "big"))
+    return b"\x30" + bytes([len(body)]) + body
+
+
+def jwt_sign(key_pem: str, claims: dict) -> str:
+    alg = "ES256" if "EC PRIVATE" in key_pem or _is_ec(key_pem) else "RS256"
+    head = b64url(json.dumps({"alg": alg, "typ": "JWT"}, separators=(",", ":")).encode())
+    body = b64url(json.dumps(claims, separators=(",", ":")).encode())
+    sig = crypto.sign(key_pem, f"{head}.{body}".encode())
+    if alg == "ES256":
+        sig = _der_to_raw(sig)
+    return f"{head}.{body}.{b64url(sig)}"
+
+
+def _is_ec(key_pem):
+    try:
+        return "BEGIN PUBLIC KEY" in crypto.public_key(key_pem) and len(crypto.public_key(key_pem)) < 300
+    except crypto.CryptoError:
+        return False
+
+
+def jwt_verify(pub_pems, token: str):
+    """Returns the claims if the signature verifies against one of the keys, else None."""
+    try:
+        h, b, s = token.split(".")
+        head = json.loads(b64url_decode(h))
+        claims = json.loads(b64url_decode(b))
+        sig = b64url_decode(s)
+    except (ValueError, json.JSONDecodeError):
+        return None
+    if head.get("alg") not in ("RS256", "ES256"):
+        return None
+    if head["alg"] == "ES256":
+        sig = _raw_to_der(sig)
+    data = f"{h}.{b}".encode()
+    for k in pub_pems:
+        if crypto.verify(k, data, sig):
+            return claims
+    return None
+
+
+class X509Authenticator:
+    def authenticate_request(self, req):
+        t = getattr(req, "transport", None)
+        cert = t.get_extra_info("peercert") if t is not None else None
+        if not cert:
+            return None
+        cn, orgs = "", []
+        for rdn in cert.get("subject") or ():
+            for k, v in rdn:
+                if k == "commonName":
+                    cn = v
+                elif k == "organizationName":
+                    orgs.append(v)
+        if not cn:
+            return None
+        return User(cn, "", orgs + ["system:authenticated"])
+
+
+def _secret_data(sec, key):
+    v = (sec.get("data") or {}).get(key)
+    if v is not None:
+        try:
+            return base64.b64decode(v).decode()
+        except Exception:
+            return None
+    return (sec.get("stringData") or {}).get(key)
+
+
+class BootstrapTokenAuthenticator:
+    def __init__(self, server):
+        self.server = server
+
+    def authenticate_token(self, token):
+        mt = BOOTSTRAP_RE.match(token)
+        if not mt:
+            return None
+        tid, tsecret = mt.groups()
+        sec = self.server.get_object("secrets", "kube-system", f"bootstrap-token-{tid}")
+        if sec is None or sec.get("type") != "bootstrap.kubernetes.io/token":
+            return False
+        if _secret_data(sec, "token-id") != tid or not hmac.compare_digest(_secret_data(sec, "token-secret") or "", tsecret):
+            return False
+        if (_secret_data(sec, "usage-bootstrap-authentication") or "") != "true":
+            return False
+        exp = _secret_data(sec, "expiration")
+        if exp and (parse_rfc3339(exp) or 0) < time.time():
+            return False
+        groups = ["system:bootstrappers"] + [g for g in (_secret_data(sec, "auth-extra-groups") or "").split(",") if g]
+        return User(f"system:bootstrap:{tid}", "", groups + ["system:authenticated"])
+
+
+class ServiceAccountAuthenticator:
+    def __init__(self, public_keys, server=None, lookup=True):
+        self.keys = list(public_keys)
+        self.server = server
+        self.lookup = lookup
+
+    def authenticate_token(self, token):
+        if token.count(".") != 2:
+            return None
+        claims = jwt_verify(self.keys, token)
+        if claims is None or claims.get("iss") != SA_ISSUER:
+            return None if claims is None else False
+        ns = claims.get("kubernetes.io/serviceaccount/namespace")
+        name = claims.get("kubernetes.io/serviceaccount/service-account.name")
+        uid = claims.get("kubernetes.io/serviceaccount/service-account.uid", "")
+        secret = claims.get("kubernetes.io/serviceaccount/secret.name")
+        if not ns or not name:
+            return False
+        if self.lookup and self.server is not None:
+            sa = self.server.get_object("serviceaccounts", ns, name)
+            if sa is None or (uid and sa["metadata"].get("uid") != uid):
+                return False
+            if secret and self.server.get_object("secrets", ns, secret) is None:
+                return False
+        return User(f"system:serviceaccount:{ns}:{name}", uid,
+                    ["system:serviceaccounts", f"system:serviceaccounts:{ns}", "system:authenticated"])
+
+
+def service_account_token(key_pem, sa, secret_name):
+    md = sa["metadata"]
+    return jwt_sign(key_pem, {"iss": SA_ISSUER, "sub": f"system:serviceaccount:{md['namespace']}:{md['name']}",
+                              "kubernetes.io/serviceaccount/namespace": md["namespace"],
+                              "kubernetes.io/serviceaccount/secret.name": secret_name,
+                              "kubernetes.io/serviceaccount/service-account.name": md["name"],
+                              "kubernetes.io/serviceaccount/service-account.uid": md.get("uid", "")})
+
+
+class WebhookTokenAuthenticator:
+    def __init__(self, url, ttl=120.0, ssl_context=None):
+        self.url = url
+        self.ttl = ttl
+        self.ssl = ssl_context
+        self.cache: dict = {}
+
+    def authenticate_token(self, token):
+        hit = self.cache.get(token)
+        now = time.monotonic()
+        if hit is not None and now - hit[1] < self.ttl:
+            return hit[0]
+        import urllib.request
+        body = json.dumps({"apiVersion": "authentication.k8s.io/v1", "kind": "TokenReview",
+                           "spec": {"token": token}}).encode()
+        req = urllib.request.Request(self.url, body, {"Content-Type": "application/json"})
+        try:
+            with urllib.request.urlopen(req, timeout=10, context=self.ssl) as r:
+                st = (json.loads(r.read()).get("status") or {})
+        except OSError:
+            return None
+        u = None
+        if st.get("authenticated"):
+            us = st.get("user") or {}
+            u = User(us.get("username", ""), us.get("uid", ""), list(us.get("groups") or []) + ["system:authenticated"])
+        self.cache[token] = (u if u else False, now)
+        return u if u else False
+
+
+class UnionAuthenticator:
+    """Tries request authenticators (x509), then bearer-token authenticators in order.
+    A token rejected by every authenticator -> 401; no credentials -> anonymous (if allowed)."""
+
+    def __init__(self, request_authenticators=(), token_authenticators=(), anonymous=True):
+        self.req_auth = list(request_authenticators)
+        self.tok_auth = list(token_authenticators)
+        self.anonymous = anonymous
+
+    def authenticate_request(self, req):
+        for a in self.req_auth:
+            u = a.authenticate_request(req)
+            if u is not None:
+                return u
+        return self.authenticate(req.headers)
+
+    def authenticate(self, headers):
+        h = headers.get("authorization", "")
+        if h.lower().startswith("bearer "):
+            tok = h[7:].strip()
+            for a in self.tok_auth:
+                u = a.authenticate_token(tok) if hasattr(a, "authenticate_token") else a.tokens.get(tok)
+                if u:
+                    return u
+            return None
+        return ANONYMOUS if self.anonymous else None

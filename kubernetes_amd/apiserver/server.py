@@ -97,7 +97,11 @@ class APIServer:
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
                  max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
                  kubelet_port_resolver=None, audit=None, encryption_config=None,
-                 service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767)):
+                 service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767),
+                 tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
+                 service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
+                 anonymous_auth=True):
+        self.tls = (tls_cert_file, tls_private_key_file, client_ca_file)
         from .service_alloc import ServiceAllocator
         from .extensions import Aggregator, CRDManager, WebhookDispatcher
         self.svc_alloc = ServiceAllocator(service_cluster_ip_range, service_node_port_range)
@@ -129,7 +133,23 @@ class APIServer:
             self._install(ri)
         names = adm.DEFAULT_PLUGINS if admission_plugins is None else admission_plugins
         self.admission = adm.new_chain(names, self, admission_config)
-        self.authn = TokenAuthenticator(token_file, tokens) if (token_file or tokens) else None
+        self.authn = None
+        if token_file or tokens or client_ca_file or service_account_key_files or enable_bootstrap_token_auth \
+                or authentication_token_webhook or not anonymous_auth:
+            from . import authn as an
+            from ..native import crypto as _crypto
+            toks = [TokenAuthenticator(token_file, tokens)] if (token_file or tokens) else []
+            if enable_bootstrap_token_auth:
+                toks.append(an.BootstrapTokenAuthenticator(self))
+            if service_account_key_files:
+                keys = []
+                for f in service_account_key_files:
+                    with open(f) as fh:
+                        keys.append(_crypto.public_key(fh.read()))
+                toks.append(an.ServiceAccountAuthenticator(keys, self, service_account_lookup))
+            if authentication_token_webhook:
+                toks.append(an.WebhookTokenAuthenticator(authentication_token_webhook))
+            self.authn = an.UnionAuthenticator([an.X509Authenticator()] if client_ca_file else [], toks, anonymous_auth)
         self.authz = build_authorizer(authorization_modes, self)
         self.max_inflight = max_requests_inflight
         self.max_mutating = max_mutating_inflight
@@ -808,7 +828,16 @@ class APIServer:
     async def start(self, host="127.0.0.1", port=0, reuse_port=False):
         if self.remote_address and self.rstore is None:
             await self._start_remote()
-        port = await self.http.start(host, port, reuse_port=reuse_port)
+        ctx = None
+        cert, key, ca = self.tls
+        if cert:
+            import ssl
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(cert, key)
+            if ca:
+                ctx.verify_mode = ssl.CERT_OPTIONAL    # x509 client-certificate authentication
+                ctx.load_verify_locations(ca)
+        port = await self.http.start(host, port, ssl=ctx, reuse_port=reuse_port)
         await self._reconcile_master_endpoints("127.0.0.1" if host in ("0.0.0.0", "") else host, port)
         return port
 
@@ -904,7 +933,8 @@ class APIServer:
                 return resp
             user = ANONYMOUS
             if self.authn is not None:
-                user = self.authn.authenticate(req.headers)
+                ar = getattr(self.authn, "authenticate_request", None)
+                user = ar(req) if ar is not None else self.authn.authenticate(req.headers)
                 if user is None:
                     code = 401
                     return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))

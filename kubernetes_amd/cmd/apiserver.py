@@ -47,6 +47,16 @@ def _parser():
     ap.add_argument("--audit-policy-file", default=None, help="audit policy YAML (rules: level/users/verbs/resources)")
     ap.add_argument("--experimental-encryption-provider-config", dest="encryption_config", default=None,
                     help="EncryptionConfig YAML: encrypt the listed resources at rest (aescbc/aesgcm/secretbox/kms)")
+    ap.add_argument("--tls-cert-file", default=None)
+    ap.add_argument("--tls-private-key-file", default=None)
+    ap.add_argument("--client-ca-file", default=None, help="enable x509 client certificate authentication")
+    ap.add_argument("--service-account-key-file", action="append", default=[])
+    ap.add_argument("--service-account-lookup", type=lambda v: v.lower() != "false", default=True)
+    ap.add_argument("--enable-bootstrap-token-auth", action="store_true")
+    ap.add_argument("--authentication-token-webhook-url", default=None)
+    ap.add_argument("--anonymous-auth", type=lambda v: v.lower() != "false", default=True)
+    ap.add_argument("--service-cluster-ip-range", default="10.0.0.0/24")
+    ap.add_argument("--service-node-port-range", default="30000-32767")
     ap.add_argument("-v", type=int, default=0)
     return ap
 
@@ -147,7 +157,14 @@ def main(argv=None):
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
                       max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size,
-                      audit=audit, encryption_config=a.encryption_config)
+                      audit=audit, encryption_config=a.encryption_config,
+                      service_cluster_ip_range=a.service_cluster_ip_range,
+                      service_node_port_range=tuple(int(x) for x in a.service_node_port_range.split("-")),
+                      tls_cert_file=a.tls_cert_file, tls_private_key_file=a.tls_private_key_file,
+                      client_ca_file=a.client_ca_file, service_account_key_files=a.service_account_key_file,
+                      service_account_lookup=a.service_account_lookup,
+                      enable_bootstrap_token_auth=a.enable_bootstrap_token_auth,
+                      authentication_token_webhook=a.authentication_token_webhook_url, anonymous_auth=a.anonymous_auth)
         port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
         if not a.reuse_port:

@@ -16,8 +16,22 @@ from ..api import core
 from ..cluster import LocalCluster
 
 
-async def gpu_pod_e2e(timeout=120):
-    async with LocalCluster(nodes=1, gpus_per_node=8, runtime="process", real_gpus=True) as cl:
+async def gpu_pod_e2e(timeout=120, cri=False):
+    """cri=True: the kubelet drives the pod through the CRI gRPC socket (RemoteRuntime + PLEG
+    relist) of a kamd-cri server backed by the process runtime — the dockershim topology."""
+    srv = rt_remote = None
+    async with LocalCluster(nodes=0 if cri else 1, gpus_per_node=8, runtime="process", real_gpus=True) as cl:
+        if cri:
+            import tempfile
+            from ..cri.remote import RemoteRuntime
+            from ..cri.server import CRIServer
+            from ..kubelet.runtime.process import ProcessRuntime
+            d = tempfile.mkdtemp(prefix="kamd-cri-")
+            backend = ProcessRuntime(os.path.join(d, "rt"))
+            srv = await CRIServer(backend, os.path.join(d, "cri.sock")).start()
+            rt_remote = await RemoteRuntime(os.path.join(d, "cri.sock"), relist_period=0.1).connect()
+            await cl.add_node("mi355x-cri", runtime=rt_remote)
+            await cl.wait_nodes_ready()
         node = await cl.client.get("nodes", cl.nodes[0].name)
         cap = int(node["status"]["capacity"].get(core.AMD_GPU, "0"))
         assert cap >= 1, node["status"]
@@ -27,7 +41,7 @@ async def gpu_pod_e2e(timeout=120):
                                         "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
         await cl.client.create("pods", pod)
         p = await cl.wait_pod("vector-add", phase="Succeeded", timeout=timeout)
-        rt = cl.nodes[0].runtime
+        rt = srv.rt if cri else cl.nodes[0].runtime
         cs = rt.list_containers()[0]
         logs = open(cs.log_path).read()
         spec = json.load(open(os.path.join(os.path.dirname(cs.log_path), "config.json")))
@@ -38,6 +52,10 @@ async def gpu_pod_e2e(timeout=120):
                       p["spec"]["extendedResources"][0]["assigned"][0]]["attributes"]}
         assert "Test PASSED" in logs, logs
         assert "/dev/kfd" in paths and any(x.startswith("/dev/dri/renderD") for x in paths), paths
+        if cri:
+            await rt_remote.close()
+            await srv.stop()
+            result["runtime"] = rt_remote.runtime_name
         return result
 
 

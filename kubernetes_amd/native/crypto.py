@@ -55,6 +55,12 @@ def _L():
         L.kc_verify_cert.restype = _l
         L.kc_cert_not_after.argtypes = [_c]
         L.kc_cert_not_after.restype = _l
+        L.kc_sign.argtypes = [_c, _c, _l, _b, _l]
+        L.kc_sign.restype = _l
+        L.kc_public_key.argtypes = [_c, _b, _l]
+        L.kc_public_key.restype = _l
+        L.kc_verify.argtypes = [_c, _c, _l, _c, _l]
+        L.kc_verify.restype = _l
         _lib = L
     return _lib
 
@@ -198,3 +204,20 @@ def verify_cert(cert_pem: str, ca_pem: str) -> tuple[bool, str]:
 
 def cert_not_after(pem: str) -> int:
     return _L().kc_cert_not_after(_e(pem))
+
+
+def sign(key_pem: str, data: bytes) -> bytes:
+    """RS256 (RSA key) or DER ECDSA-SHA256 (EC key) signature."""
+    out = ctypes.create_string_buffer(1024)
+    n = _L().kc_sign(_e(key_pem), data, len(data), out, 1024)
+    if n < 0:
+        raise CryptoError("signing failed")
+    return out.raw[:n]
+
+
+def public_key(pem: str) -> str:
+    return _text(_L().kc_public_key, _e(pem))
+
+
+def verify(pub_pem: str, data: bytes, sig: bytes) -> bool:
+    return _L().kc_verify(_e(pub_pem), data, len(data), sig, len(sig)) == 1

@@ -447,4 +447,60 @@ long kc_cert_not_after(const char* pem) {
   return r;
 }
 
+// ---------------------------------------------------------------- signatures (JWT RS256 / ES256)
+// Sign `data` with the private key (RSA: PKCS#1 v1.5 SHA-256; EC: ECDSA SHA-256, DER). Returns the
+// signature length written to out, or -1.
+long kc_sign(const char* key_pem, const uint8_t* data, long n, uint8_t* out, long cap) {
+  EVP_PKEY* k = load_key(key_pem);
+  if (!k) return -1;
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  size_t sl = 0;
+  long r = -1;
+  if (EVP_DigestSignInit(ctx, nullptr, EVP_sha256(), nullptr, k) == 1 &&
+      EVP_DigestSign(ctx, nullptr, &sl, data, (size_t)n) == 1 && (long)sl <= cap &&
+      EVP_DigestSign(ctx, out, &sl, data, (size_t)n) == 1)
+    r = (long)sl;
+  EVP_MD_CTX_free(ctx);
+  EVP_PKEY_free(k);
+  return r;
+}
+
+// PEM of the public key of a private key / certificate / public key.
+long kc_public_key(const char* pem, char* out, long cap) {
+  EVP_PKEY* k = load_key(pem);
+  if (!k) {
+    X509* c = load_cert(pem);
+    if (c) { k = X509_get_pubkey(c); X509_free(c); }
+  }
+  if (!k) {
+    BIO* b = BIO_new_mem_buf(pem, -1);
+    k = PEM_read_bio_PUBKEY(b, nullptr, nullptr, nullptr);
+    BIO_free(b);
+  }
+  if (!k) return fail(out, cap, "no key");
+  BIO* b = BIO_new(BIO_s_mem());
+  PEM_write_bio_PUBKEY(b, k);
+  long r = put(out, cap, bio_str(b));
+  BIO_free(b);
+  EVP_PKEY_free(k);
+  return r;
+}
+
+// 1 = valid, 0 = invalid signature, -1 = bad key.
+long kc_verify(const char* pub_pem, const uint8_t* data, long n, const uint8_t* sig, long sl) {
+  BIO* b = BIO_new_mem_buf(pub_pem, -1);
+  EVP_PKEY* k = PEM_read_bio_PUBKEY(b, nullptr, nullptr, nullptr);
+  BIO_free(b);
+  if (!k) return -1;
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  long r = 0;
+  if (EVP_DigestVerifyInit(ctx, nullptr, EVP_sha256(), nullptr, k) == 1 &&
+      EVP_DigestVerify(ctx, sig, (size_t)sl, data, (size_t)n) == 1)
+    r = 1;
+  EVP_MD_CTX_free(ctx);
+  EVP_PKEY_free(k);
+  ERR_clear_error();
+  return r;
+}
+
 }  // extern "C"

@@ -17,6 +17,17 @@ def test_real_gpu_pod_runs_hip_vector_add(run):
     assert len(kfd) >= 2
 
 
+def test_real_gpu_pod_over_cri(run):
+    """Same GPU pod, kubelet -> CRI gRPC (kamd-cri, process runtime) -> hip-vector-add on the MI355X."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kubernetes_amd.e2e.smoke import gpu_pod_e2e
+    r = run(gpu_pod_e2e(cri=True), timeout=300)
+    assert r["runtime"] == "kamd-process"
+    assert "Test PASSED" in r["log"]
+
+
 def test_real_plugin_capacity_and_health(run):
     import asyncio
     from kubernetes_amd.cluster import LocalCluster
