@@ -14,6 +14,7 @@ from .daemonset import DaemonSetController, StatefulSetController
 from .deployment import DeploymentController
 from .job import CronJobController, JobController
 from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleController, PodGCController
+from .podautoscaler import HorizontalController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
 
@@ -35,6 +36,7 @@ CONTROLLERS = {
     "endpoint": EndpointsController,
     "resourcequota": ResourceQuotaController,
     "disruption": DisruptionController,
+    "horizontalpodautoscaling": HorizontalController,
 }
 
 

@@ -372,25 +372,73 @@ class Kubectl:
         await self.client.patch("nodes", a.node, {"spec": {"taints": taints or None}})
         self.p(f"node/{a.node} tainted")
 
+    async def _metrics(self, path):
+        st, body = await self.client.raw("GET", "/apis/metrics.k8s.io/v1beta1" + path)
+        return {(i["metadata"].get("namespace"), i["metadata"]["name"]): i for i in json.loads(body).get("items") or ()} \
+            if st == 200 else {}
+
     async def cmd_top(self):
+        """`kubectl top` (`pkg/kubectl/cmd/top_node.go`, `top_pod.go`) over metrics.k8s.io, with the
+        MI355X columns: allocated GPUs per node and per-pod GPU utilization."""
         a = self.a
         nodes = (await self.client.list("nodes"))["items"]
         pods = (await self.client.list("pods"))["items"]
         if a.what in ("node", "nodes"):
+            nm = await self._metrics("/nodes")
             rows = []
             for n in nodes:
                 name = n["metadata"]["name"]
                 devs = ((n.get("status") or {}).get("extendedResources") or {}).get(core.AMD_GPU, {}).get("resources") or {}
                 used = sum(len(printers.pod_gpus(p)) for p in pods if (p.get("spec") or {}).get("nodeName") == name
                            and not core.pod_is_terminal(p))
-                rows.append([name, len(devs), used, f"{(100 * used // len(devs)) if devs else 0}%",
+                u = (nm.get((None, name)) or {}).get("usage") or {}
+                rows.append([name, u.get("cpu", "<unknown>"), u.get("memory", "<unknown>"), len(devs), used,
+                             f"{(100 * used // len(devs)) if devs else 0}%",
                              sum(1 for d in devs.values() if d.get("health") != "Healthy")])
-            self.p(printers.table(rows, ["NAME", "GPUS", "GPUS-ALLOCATED", "GPU%", "UNHEALTHY"]))
+            self.p(printers.table(rows, ["NAME", "CPU(cores)", "MEMORY(bytes)", "GPUS", "GPUS-ALLOCATED", "GPU%", "UNHEALTHY"]))
         else:
-            rows = [[p["metadata"].get("namespace"), p["metadata"]["name"], (p.get("spec") or {}).get("nodeName") or "<none>",
-                     len(printers.pod_gpus(p)), ",".join(printers.pod_gpus(p)) or "<none>"]
-                    for p in pods if printers.pod_gpus(p)]
-            self.p(printers.table(rows, ["NAMESPACE", "NAME", "NODE", "GPUS", "DEVICES"]))
+            pm = await self._metrics(f"/namespaces/{self.ns}/pods")
+            rows = []
+            for p in pods:
+                if p["metadata"].get("namespace") != self.ns or core.pod_is_terminal(p):
+                    continue
+                mt = pm.get((self.ns, p["metadata"]["name"])) or {}
+                cpu = sum(int(str(c["usage"].get("cpu", "0m")).rstrip("m") or 0) for c in mt.get("containers") or ())
+                mem = sum(int(str(c["usage"].get("memory", "0Ki")).rstrip("Ki") or 0) for c in mt.get("containers") or ())
+                gpu = [c["usage"].get(core.AMD_GPU) for c in mt.get("containers") or () if core.AMD_GPU in c.get("usage", {})]
+                rows.append([p["metadata"]["name"], f"{cpu}m" if mt else "<unknown>", f"{mem // 1024}Mi" if mt else "<unknown>",
+                             ",".join(printers.pod_gpus(p)) or "<none>", (gpu[0] + "%") if gpu else "<none>"])
+            self.p(printers.table(rows, ["NAME", "CPU(cores)", "MEMORY(bytes)", "GPUS", "GPU-UTIL"]))
+
+    async def cmd_autoscale(self):
+        """`kubectl autoscale deployment/x --min --max --cpu-percent` (`pkg/kubectl/cmd/autoscale.go`);
+        `--gpu-percent` targets MI355X utilization through `spec.metrics`."""
+        a = self.a
+        (ri, name), = split_targets(a.targets)
+        spec = {"scaleTargetRef": {"apiVersion": ri.group_version, "kind": ri.kind, "name": name},
+                "maxReplicas": a.max}
+        if a.min:
+            spec["minReplicas"] = a.min
+        if a.gpu_percent:
+            spec["metrics"] = [{"type": "Resource", "resource": {"name": core.AMD_GPU, "targetAverageUtilization": a.gpu_percent}}]
+        elif a.cpu_percent:
+            spec["targetCPUUtilizationPercentage"] = a.cpu_percent
+        await self.client.create("horizontalpodautoscalers", {"metadata": {"name": a.name or name, "namespace": self.ns},
+                                                              "spec": spec}, self.ns)
+        self.p(f"{ri.kind.lower()}.{ri.group or 'core'} \"{name}\" autoscaled")
+
+    async def cmd_certificate(self):
+        """`kubectl certificate approve|deny CSR...` (`pkg/kubectl/cmd/certificates.go`)."""
+        a = self.a
+        for n in a.names:
+            csr = await self.client.get("certificatesigningrequests", n)
+            conds = [c for c in (csr.get("status") or {}).get("conditions") or () if c.get("type") not in ("Approved", "Denied")]
+            typ = "Approved" if a.action == "approve" else "Denied"
+            conds.append({"type": typ, "reason": "KubectlApprove" if typ == "Approved" else "KubectlDeny",
+                          "message": f"This CSR was {typ.lower()} by kubectl certificate {a.action}."})
+            csr.setdefault("status", {})["conditions"] = conds
+            await self.client.update("certificatesigningrequests", csr, subresource="approval")
+            self.p(f"certificatesigningrequest.certificates.k8s.io/{n} {typ.lower()}")
 
     async def cmd_rollout(self):
         a = self.a
@@ -846,6 +894,16 @@ def build_parser():
     px.add_argument("--serve-seconds", type=float, default=0, help=argparse.SUPPRESS)
     ed = add("edit")
     ed.add_argument("targets", nargs="+")
+    aut = add("autoscale")
+    aut.add_argument("targets", nargs="+")
+    aut.add_argument("--min", type=int, default=0)
+    aut.add_argument("--max", type=int, required=True)
+    aut.add_argument("--cpu-percent", type=int, default=0)
+    aut.add_argument("--gpu-percent", type=int, default=0, help="target MI355X utilization (amd.com/gpu)")
+    aut.add_argument("--name")
+    cert = add("certificate")
+    cert.add_argument("action", choices=["approve", "deny"])
+    cert.add_argument("names", nargs="+")
     cf = add("config")
     cf.add_argument("action", choices=["view", "current-context", "get-contexts", "use-context", "set-cluster",
                                        "set-context", "set-credentials"])

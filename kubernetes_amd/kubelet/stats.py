@@ -50,9 +50,52 @@ def accelerator_stats(kubelet, ids):
     return out
 
 
+SIM_CPU = "kubemark.amd.com/cpu-millicores"       # stub runtime: simulated usage (kubemark)
+SIM_MEM = "kubemark.amd.com/memory-bytes"
+SIM_GPU = "kubemark.amd.com/gpu-utilization"
+
+
+def _proc_usage(pid):
+    """(cumulative CPU ns, RSS bytes) of a process tree root (cAdvisor reads the cgroup)."""
+    import os
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        cpu = (int(fields[11]) + int(fields[12])) * (1_000_000_000 // os.sysconf("SC_CLK_TCK"))
+        with open(f"/proc/{pid}/statm") as f:
+            rss = int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+        return cpu, rss
+    except (OSError, IndexError, ValueError):
+        return None
+
+
+def container_usage(kubelet, pod, cid, now):
+    """{usageNanoCores, usageCoreNanoSeconds, workingSetBytes} for one container."""
+    ann = pod["metadata"].get("annotations") or {}
+    if SIM_CPU in ann or SIM_MEM in ann:
+        milli = float(ann.get(SIM_CPU, 0))
+        return {"usageNanoCores": int(milli * 1e6), "usageCoreNanoSeconds": 0, "workingSetBytes": int(float(ann.get(SIM_MEM, 0)))}
+    meta = (getattr(kubelet.runtime, "meta", {}) or {}).get(cid) or {}
+    proc = meta.get("proc")
+    if proc is None or getattr(proc, "returncode", 1) is not None:
+        return None
+    u = _proc_usage(proc.pid)
+    if u is None:
+        return None
+    cpu, rss = u
+    prev = kubelet._cpu_samples.get(cid)
+    kubelet._cpu_samples[cid] = (now, cpu)
+    nano_cores = int((cpu - prev[1]) / max(1e-9, now - prev[0])) if prev and now > prev[0] else 0
+    return {"usageNanoCores": nano_cores, "usageCoreNanoSeconds": cpu, "workingSetBytes": rss}
+
+
 def summary(kubelet):
     now = now_rfc3339()
+    t = time.time()
+    if not hasattr(kubelet, "_cpu_samples"):
+        kubelet._cpu_samples = {}
     pods = []
+    node_cpu = node_mem = 0
     for st in kubelet.pods.values():
         pod = st.pod
         md = pod["metadata"]
@@ -60,12 +103,24 @@ def summary(kubelet):
         for c in (pod.get("spec") or {}).get("containers") or ():
             ids = core.pod_extended_resource_assigned(core.AMD_GPU, c, pod) if c.get("extendedResourceRequests") else []
             cs = {"name": c["name"], "startTime": st.start_time, "cpu": {"time": now}, "memory": {"time": now}}
+            cid = st.containers.get(c["name"])
+            u = container_usage(kubelet, pod, cid, t) if cid else None
+            if u is not None:
+                cs["cpu"].update(usageNanoCores=u["usageNanoCores"], usageCoreNanoSeconds=u["usageCoreNanoSeconds"])
+                cs["memory"].update(workingSetBytes=u["workingSetBytes"], usageBytes=u["workingSetBytes"])
+                node_cpu += u["usageNanoCores"]
+                node_mem += u["workingSetBytes"]
             acc = accelerator_stats(kubelet, ids)
+            sim_gpu = (md.get("annotations") or {}).get(SIM_GPU)
+            if acc and sim_gpu is not None:
+                for a in acc:
+                    a["dutyCycle"] = int(float(sim_gpu))
             if acc:
                 cs["accelerators"] = acc
             containers.append(cs)
         pods.append({"podRef": {"name": md["name"], "namespace": md.get("namespace", ""), "uid": md["uid"]},
                      "startTime": st.start_time, "containers": containers})
-    return {"node": {"nodeName": kubelet.node_name, "startTime": now, "cpu": {"time": now}, "memory": {"time": now},
+    return {"node": {"nodeName": kubelet.node_name, "startTime": now,
+                     "cpu": {"time": now, "usageNanoCores": node_cpu}, "memory": {"time": now, "workingSetBytes": node_mem},
                      "systemContainers": [{"name": "kubelet", "startTime": now}]},
             "pods": pods, "time": time.time()}
