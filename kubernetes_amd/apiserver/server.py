@@ -546,6 +546,12 @@ class APIServer:
         init_object_meta(obj, ri, namespace)
         strat = self.strategies[ri.plural]
         strat.prepare_create(obj)
+        if ri.plural == "certificatesigningrequests":
+            # the requester's identity is recorded by the server, never trusted from the body
+            sp = obj.setdefault("spec", {})
+            u = user or ANONYMOUS
+            sp["username"], sp["uid"], sp["groups"] = u.name, u.uid or "", list(u.groups or ())
+            obj["status"] = {}
         ns = m.namespace_of(obj) if ri.namespaced else None
         if admit:
             a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
@@ -662,7 +668,14 @@ class APIServer:
                 nm.pop(k, None)
         obj["kind"], obj["apiVersion"] = ri.kind, ri.group_version
         strat = self.strategies[ri.plural]
-        if subresource == "status":
+        if subresource == "approval" and ri.plural == "certificatesigningrequests":
+            # CSR approval subresource: only status.conditions may change
+            # (pkg/registry/certificates/certificates/strategy.go approvalStrategy)
+            conds = (obj.get("status") or {}).get("conditions") or []
+            obj = fast_copy(old)
+            obj["metadata"] = nm
+            obj.setdefault("status", {})["conditions"] = conds
+        elif subresource == "status":
             strat.prepare_status_update(obj, old)
         elif subresource == "":
             strat.prepare_update(obj, old)

@@ -1,0 +1,345 @@
+"""Identity controllers: service-account tokens, bootstrap signer / token cleaner, CSR approving
+and signing, cluster-role aggregation, node TTL.
+
+Parity:
+  * `pkg/controller/serviceaccount/tokens_controller.go` — every ServiceAccount gets a
+    `kubernetes.io/service-account-token` secret `<sa>-token-<5 chars>` holding a signed JWT,
+    `ca.crt` and `namespace`, annotated with the SA name/uid and referenced from `sa.secrets`;
+    token secrets whose SA is gone are deleted;
+  * `pkg/controller/bootstrap/bootstrapsigner.go` — `kube-public/cluster-info` gets a detached
+    JWS (`<b64 header>..<b64 HMAC-SHA256>`, key = `<id>.<secret>`) per signing bootstrap token
+    under `jws-kubeconfig-<id>`; `tokencleaner.go` deletes expired bootstrap token secrets;
+  * `pkg/controller/certificates/approver/sarapprove.go:82-229` — auto-approve node client
+    CSRs (O=system:nodes, CN=system:node:*, usages exactly {key encipherment, digital signature,
+    client auth}) when a SubjectAccessReview allows `create certificatesigningrequests/nodeclient`
+    (or `/selfnodeclient` when the requester is the node itself);
+  * `pkg/controller/certificates/signer/cfssl_signer.go` — approved CSRs are signed by the
+    cluster CA (`--cluster-signing-cert-file/--cluster-signing-key-file`, 1 year);
+  * `pkg/controller/clusterroleaggregation` — `aggregationRule.clusterRoleSelectors` -> rules;
+  * `pkg/controller/ttl/ttl_controller.go` — node annotation `node.alpha.kubernetes.io/ttl`
+    from cluster size (0 s up to 100 nodes, 15 s to 500, 30 s to 1000, 60 s to 2000, 300 s beyond).
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import hashlib
+import hmac
+import json
+import random
+import time
+
+from ..api.labels import label_selector_as_selector
+from ..api.meta import parse_rfc3339
+from ..client.rest import APIStatusError, is_already_exists, is_not_found
+from .base import Controller, split_key
+
+SA_TOKEN = "kubernetes.io/service-account-token"
+SA_NAME_ANN = "kubernetes.io/service-account.name"
+SA_UID_ANN = "kubernetes.io/service-account.uid"
+BOOTSTRAP = "bootstrap.kubernetes.io/token"
+
+
+def _b64(v: str) -> str:
+    return base64.b64encode(v.encode()).decode()
+
+
+def _sdata(sec, k):
+    v = (sec.get("data") or {}).get(k)
+    try:
+        return base64.b64decode(v).decode() if v is not None else None
+    except Exception:
+        return None
+
+
+class TokensController(Controller):
+    name = "serviceaccount-token"
+    workers = 2
+
+    def __init__(self, client, factory, private_key=None, private_key_file=None, root_ca=None, root_ca_file=None, **kw):
+        super().__init__(client, factory, **kw)
+        if private_key_file:
+            with open(private_key_file) as f:
+                private_key = f.read()
+        if root_ca_file:
+            with open(root_ca_file) as f:
+                root_ca = f.read()
+        self.key = private_key
+        self.root_ca = root_ca or ""
+
+    def setup(self):
+        self.sa_inf = self.factory.get("serviceaccounts")
+        self.sec_inf = self.factory.get("secrets")
+        self.sa_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), self.enqueue)
+        self.sec_inf.add_handler(self._secret, None, self._secret)
+
+    def _secret(self, sec):
+        if sec.get("type") == SA_TOKEN:
+            ann = sec["metadata"].get("annotations") or {}
+            self.enqueue(f"{sec['metadata']['namespace']}/{ann.get(SA_NAME_ANN, '')}")
+
+    def _tokens_of(self, ns, name, uid):
+        return [s for s in self.sec_inf.list() if s.get("type") == SA_TOKEN and s["metadata"].get("namespace") == ns
+                and (s["metadata"].get("annotations") or {}).get(SA_NAME_ANN) == name]
+
+    async def sync(self, key):
+        if not self.key:
+            return
+        ns, name = split_key(key)
+        sa = self.sa_inf.get(key)
+        toks = self._tokens_of(ns, name, None)
+        if sa is None:
+            for t in toks:     # SA deleted: its tokens go
+                try:
+                    await self.client.delete("secrets", t["metadata"]["name"], ns)
+                except APIStatusError as e:
+                    if not is_not_found(e):
+                        raise
+            return
+        uid = sa["metadata"].get("uid", "")
+        live = [t for t in toks if (t["metadata"].get("annotations") or {}).get(SA_UID_ANN) == uid]
+        if not live:
+            from ..apiserver.authn import service_account_token
+            sname = f"{name}-token-{''.join(random.choice('bcdfghjklmnpqrstvwxz2456789') for _ in range(5))}"
+            sec = {"metadata": {"name": sname, "namespace": ns, "annotations": {SA_NAME_ANN: name, SA_UID_ANN: uid}},
+                   "type": SA_TOKEN,
+                   "data": {"token": _b64(service_account_token(self.key, sa, sname)), "namespace": _b64(ns),
+                            "ca.crt": _b64(self.root_ca)}}
+            try:
+                await self.client.create("secrets", sec, ns)
+            except APIStatusError as e:
+                if not is_already_exists(e):
+                    raise
+            live = [sec]
+        refs = [r.get("name") for r in sa.get("secrets") or ()]
+        want = refs + [t["metadata"]["name"] for t in live if t["metadata"]["name"] not in refs]
+        if want != refs:
+            await self.client.patch("serviceaccounts", name, {"secrets": [{"name": n} for n in want]}, ns)
+
+
+def jws_detached(token_id, token_secret, payload: str) -> str:
+    header = base64.urlsafe_b64encode(json.dumps({"alg": "HS256", "kid": token_id}, separators=(",", ":")).encode()).rstrip(b"=")
+    body = base64.urlsafe_b64encode(payload.encode()).rstrip(b"=")
+    sig = hmac.new(f"{token_id}.{token_secret}".encode(), header + b"." + body, hashlib.sha256).digest()
+    return (header + b".." + base64.urlsafe_b64encode(sig).rstrip(b"=")).decode()
+
+
+class BootstrapSignerController(Controller):
+    name = "bootstrapsigner"
+    workers = 1
+
+    def setup(self):
+        self.cm_inf = self.factory.get("configmaps", "kube-public")
+        self.sec_inf = self.factory.get("secrets", "kube-system")
+        self.cm_inf.add_handler(lambda o: self.enqueue("kube-public/cluster-info"), lambda o, n: self.enqueue("kube-public/cluster-info"), None)
+        self.sec_inf.add_handler(lambda o: self.enqueue("kube-public/cluster-info"),
+                                 lambda o, n: self.enqueue("kube-public/cluster-info"),
+                                 lambda o: self.enqueue("kube-public/cluster-info"))
+
+    async def sync(self, key):
+        cm = self.cm_inf.get("kube-public/cluster-info")
+        if cm is None:
+            return
+        kc = (cm.get("data") or {}).get("kubeconfig")
+        if kc is None:
+            return
+        sigs = {}
+        now = time.time()
+        for s in self.sec_inf.list():
+            if s.get("type") != BOOTSTRAP or _sdata(s, "usage-bootstrap-signing") != "true":
+                continue
+            exp = _sdata(s, "expiration")
+            if exp and (parse_rfc3339(exp) or 0) < now:
+                continue
+            tid, tsec = _sdata(s, "token-id"), _sdata(s, "token-secret")
+            if tid and tsec:
+                sigs[f"jws-kubeconfig-{tid}"] = jws_detached(tid, tsec, kc)
+        data = {k: v for k, v in (cm.get("data") or {}).items() if not k.startswith("jws-kubeconfig-")}
+        data.update(sigs)
+        if data != cm.get("data"):
+            cm = dict(cm, data=data)
+            await self.client.update("configmaps", cm, "kube-public")
+
+
+class TokenCleanerController(Controller):
+    name = "tokencleaner"
+    workers = 1
+
+    def setup(self):
+        self.sec_inf = self.factory.get("secrets", "kube-system")
+        self.sec_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+        self._tick = None
+
+    def start(self):
+        super().start()
+        self._tick = asyncio.ensure_future(self._ticker())
+
+    def stop(self):
+        super().stop()
+        if self._tick:
+            self._tick.cancel()
+
+    async def _ticker(self):
+        while True:
+            await asyncio.sleep(5)
+            for s in self.sec_inf.list():
+                if s.get("type") == BOOTSTRAP:
+                    self.enqueue(s)
+
+    async def sync(self, key):
+        s = self.sec_inf.get(key)
+        if s is None or s.get("type") != BOOTSTRAP:
+            return
+        exp = _sdata(s, "expiration")
+        if exp and (parse_rfc3339(exp) or 0) < time.time():
+            ns, name = split_key(key)
+            try:
+                await self.client.delete("secrets", name, ns)
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise
+
+
+KUBELET_CLIENT_USAGES = {"key encipherment", "digital signature", "client auth"}
+
+
+def _approval(csr):
+    for c in (csr.get("status") or {}).get("conditions") or ():
+        if c.get("type") in ("Approved", "Denied"):
+            return c["type"]
+    return None
+
+
+def _csr_pem(csr):
+    return base64.b64decode((csr.get("spec") or {}).get("request", "")).decode()
+
+
+class CSRApprovingController(Controller):
+    name = "csrapproving"
+    workers = 1
+
+    def setup(self):
+        self.csr_inf = self.factory.get("certificatesigningrequests")
+        self.csr_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+
+    async def sync(self, key):
+        from ..native import crypto
+        csr = self.csr_inf.get(key)
+        if csr is None or (csr.get("status") or {}).get("certificate") or _approval(csr):
+            return
+        sp = csr.get("spec") or {}
+        try:
+            cn, orgs = crypto.csr_subject(_csr_pem(csr))
+        except Exception:
+            return
+        if orgs != ["system:nodes"] or not cn.startswith("system:node:") or set(sp.get("usages") or ()) != KUBELET_CLIENT_USAGES \
+                or len(sp.get("usages") or ()) != 3:
+            return
+        sub = "selfnodeclient" if sp.get("username") == cn else "nodeclient"
+        sar = await self.client.create("subjectaccessreviews", {"spec": {
+            "user": sp.get("username", ""), "uid": sp.get("uid", ""), "groups": sp.get("groups") or [],
+            "resourceAttributes": {"group": "certificates.k8s.io", "resource": "certificatesigningrequests",
+                                   "verb": "create", "subresource": sub}}})
+        if not (sar.get("status") or {}).get("allowed"):
+            return
+        csr = dict(csr)
+        st = dict(csr.get("status") or {})
+        st["conditions"] = list(st.get("conditions") or []) + [
+            {"type": "Approved", "reason": "AutoApproved",
+             "message": "Auto approving self kubelet client certificate after SubjectAccessReview." if sub == "selfnodeclient"
+             else "Auto approving kubelet client certificate after SubjectAccessReview."}]
+        csr["status"] = st
+        await self.client.update("certificatesigningrequests", csr, subresource="approval")
+
+
+class CSRSigningController(Controller):
+    name = "csrsigning"
+    workers = 1
+
+    def __init__(self, client, factory, ca_cert=None, ca_key=None, cert_file=None, key_file=None, days=365, **kw):
+        super().__init__(client, factory, **kw)
+        if cert_file:
+            with open(cert_file) as f:
+                ca_cert = f.read()
+        if key_file:
+            with open(key_file) as f:
+                ca_key = f.read()
+        self.ca_cert, self.ca_key, self.days = ca_cert, ca_key, days
+
+    def setup(self):
+        self.csr_inf = self.factory.get("certificatesigningrequests")
+        self.csr_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
+
+    async def sync(self, key):
+        from ..native import crypto
+        csr = self.csr_inf.get(key)
+        if not self.ca_cert or csr is None or (csr.get("status") or {}).get("certificate") or _approval(csr) != "Approved":
+            return
+        usages = set((csr.get("spec") or {}).get("usages") or ())
+        usage = "client" if "server auth" not in usages else ("server" if "client auth" not in usages else "both")
+        cert = crypto.issue_cert(csr_pem=_csr_pem(csr), ca_cert=self.ca_cert, ca_key=self.ca_key, days=self.days, usage=usage)
+        csr = dict(csr)
+        csr["status"] = dict(csr.get("status") or {}, certificate=base64.b64encode(cert.encode()).decode())
+        await self.client.update_status("certificatesigningrequests", csr)
+
+
+class ClusterRoleAggregationController(Controller):
+    name = "clusterroleaggregation"
+    workers = 1
+
+    def setup(self):
+        self.cr_inf = self.factory.get("clusterroles")
+        self.cr_inf.add_handler(self._any, lambda o, n: self._any(n), self._any)
+
+    def _any(self, _):
+        for cr in self.cr_inf.list():
+            if cr.get("aggregationRule"):
+                self.enqueue(cr)
+
+    async def sync(self, key):
+        cr = self.cr_inf.get(key)
+        if cr is None or not cr.get("aggregationRule"):
+            return
+        rules = []
+        sels = [label_selector_as_selector(s) for s in cr["aggregationRule"].get("clusterRoleSelectors") or ()]
+        for other in sorted(self.cr_inf.list(), key=lambda o: o["metadata"]["name"]):
+            if other["metadata"]["name"] == cr["metadata"]["name"]:
+                continue
+            if any(s.matches(other["metadata"].get("labels") or {}) for s in sels):
+                for r in other.get("rules") or ():
+                    if r not in rules:
+                        rules.append(r)
+        if rules != (cr.get("rules") or []):
+            await self.client.update("clusterroles", dict(cr, rules=rules))
+
+
+TTL_ANN = "node.alpha.kubernetes.io/ttl"
+TTL_BOUNDARIES = ((100, 0), (500, 15), (1000, 30), (2000, 60))
+
+
+def ttl_for(n):
+    for limit, ttl in TTL_BOUNDARIES:
+        if n <= limit:
+            return ttl
+    return 300
+
+
+class TTLController(Controller):
+    name = "ttl"
+    workers = 1
+
+    def setup(self):
+        self.node_inf = self.factory.get("nodes")
+        self.node_inf.add_handler(self._all, lambda o, n: self.enqueue(n), self._all)
+
+    def _all(self, _):
+        for n in self.node_inf.list():
+            self.enqueue(n)
+
+    async def sync(self, key):
+        node = self.node_inf.get(key)
+        if node is None:
+            return
+        want = str(ttl_for(len(self.node_inf.list())))
+        if (node["metadata"].get("annotations") or {}).get(TTL_ANN) != want:
+            await self.client.patch("nodes", key, {"metadata": {"annotations": {TTL_ANN: want}}})

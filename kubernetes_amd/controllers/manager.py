@@ -14,6 +14,8 @@ from .daemonset import DaemonSetController, StatefulSetController
 from .deployment import DeploymentController
 from .job import CronJobController, JobController
 from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleController, PodGCController
+from .certificates import (BootstrapSignerController, ClusterRoleAggregationController, CSRApprovingController,
+                           CSRSigningController, TokenCleanerController, TokensController, TTLController)
 from .podautoscaler import HorizontalController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
@@ -37,6 +39,13 @@ CONTROLLERS = {
     "resourcequota": ResourceQuotaController,
     "disruption": DisruptionController,
     "horizontalpodautoscaling": HorizontalController,
+    "serviceaccount-token": TokensController,
+    "bootstrapsigner": BootstrapSignerController,
+    "tokencleaner": TokenCleanerController,
+    "csrapproving": CSRApprovingController,
+    "csrsigning": CSRSigningController,
+    "clusterroleaggregation": ClusterRoleAggregationController,
+    "ttl": TTLController,
 }
 
 
