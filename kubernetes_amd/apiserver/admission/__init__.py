@@ -78,7 +78,7 @@ class Chain:
 
 DEFAULT_PLUGINS = [
     "NamespaceLifecycle", "LimitRanger", "ServiceAccount", "DefaultTolerationSeconds",
-    "Priority", "ResourceV2", "ExtendedResourceToleration", "NodeRestriction", "ResourceQuota",
+    "Priority", "ResourceV2", "ExtendedResourceToleration", "DefaultStorageClass", "NodeRestriction", "ResourceQuota",
 ]
 
 

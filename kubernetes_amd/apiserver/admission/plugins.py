@@ -255,6 +255,29 @@ class PodNodeSelector(Plugin):
 
 
 @register
+class DefaultStorageClass(Plugin):
+    """`plugin/pkg/admission/storageclass/setdefault/admission.go`: a claim without a class gets
+    the StorageClass annotated `storageclass.kubernetes.io/is-default-class=true` (error if several)."""
+    name = "DefaultStorageClass"
+    operations = (CREATE,)
+    ANN = ("storageclass.kubernetes.io/is-default-class", "storageclass.beta.kubernetes.io/is-default-class")
+
+    def admit(self, a):
+        if a.resource != "persistentvolumeclaims" or a.subresource:
+            return
+        spec = a.obj.setdefault("spec", {})
+        if "storageClassName" in spec or (a.obj.get("metadata", {}).get("annotations") or {}).get(
+                "volume.beta.kubernetes.io/storage-class") is not None:
+            return
+        defaults = [sc for sc in self.server.list_objects("storageclasses")
+                    if any((sc["metadata"].get("annotations") or {}).get(k) == "true" for k in self.ANN)]
+        if len(defaults) > 1:
+            raise AdmissionError(f"{len(defaults)} default StorageClasses were found", 403)
+        if defaults:
+            spec["storageClassName"] = defaults[0]["metadata"]["name"]
+
+
+@register
 class AlwaysAdmit(Plugin):
     name = "AlwaysAdmit"
 

@@ -96,7 +96,8 @@ class Strategy:
     def validate_update(self, new, old):
         return self.validate(new)
 
-    _PHASES = {"Pending", "Running", "Succeeded", "Failed", "Unknown", "Active", "Terminating", ""}
+    _PHASES = {"Pending", "Running", "Succeeded", "Failed", "Unknown", "Active", "Terminating", "",
+               "Available", "Bound", "Released", "Lost"}   # pods, namespaces, PVs / PVCs
 
     def validate_status(self, obj):
         errs = validation.validate_object_meta(obj, self.ri.namespaced)

@@ -17,6 +17,7 @@ from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleContr
 from .certificates import (BootstrapSignerController, ClusterRoleAggregationController, CSRApprovingController,
                            CSRSigningController, TokenCleanerController, TokensController, TTLController)
 from .podautoscaler import HorizontalController
+from .volume import PersistentVolumeController, PVCProtectionController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
 
@@ -46,6 +47,8 @@ CONTROLLERS = {
     "csrsigning": CSRSigningController,
     "clusterroleaggregation": ClusterRoleAggregationController,
     "ttl": TTLController,
+    "persistentvolume-binder": PersistentVolumeController,
+    "pvc-protection": PVCProtectionController,
 }
 
 

@@ -131,6 +131,8 @@ class VolumeManager:
                 await self._cm_secret(ns, v, d)
             elif "downwardAPI" in v:
                 self._downward(pod, v["downwardAPI"], d, node_name, pod_ip)
+            elif "persistentVolumeClaim" in v:
+                d = await self._pvc_path(ns, v["persistentVolumeClaim"])
             elif "projected" in v:
                 for src in v["projected"].get("sources") or ():
                     if "configMap" in src or "secret" in src:
@@ -141,6 +143,21 @@ class VolumeManager:
                 raise VolumeError(f"volume {name}: unsupported volume source {sorted(k for k in v if k != 'name')}")
             out[name] = d
         return out
+
+    async def _pvc_path(self, ns, src):
+        """persistentVolumeClaim -> the bound PV's hostPath / local path
+        (`pkg/volume/util/operationexecutor` mounts the PV the claim is bound to)."""
+        pvc = await self._get("persistentvolumeclaims", ns, src.get("claimName", ""), False)
+        vol = (pvc.get("spec") or {}).get("volumeName")
+        if not vol or (pvc.get("status") or {}).get("phase") != "Bound":
+            raise VolumeError(f"persistentvolumeclaim {ns}/{src.get('claimName')} is not bound")
+        pv = await self._get("persistentvolumes", None, vol, False)
+        sp = pv.get("spec") or {}
+        path = (sp.get("hostPath") or {}).get("path") or (sp.get("local") or {}).get("path")
+        if not path:
+            raise VolumeError(f"persistentvolume {vol}: only hostPath / local volumes can be mounted on this node")
+        os.makedirs(path, exist_ok=True)
+        return path
 
     async def _cm_secret(self, ns, v, d):
         if "configMap" in v:

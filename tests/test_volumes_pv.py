@@ -1,0 +1,117 @@
+"""PersistentVolume binding, hostPath dynamic provisioning, reclaim policies, PVC protection,
+DefaultStorageClass admission, and a pod mounting a claim.
+
+Parity: `pkg/controller/volume/persistentvolume/binder_test.go` / `provision_test.go` /
+`delete_test.go` / `recycle_test.go`, `pkg/controller/volume/pvcprotection`,
+`plugin/pkg/admission/storageclass/setdefault/admission_test.go`.
+"""
+import asyncio
+import os
+import sys
+import time
+
+from kubernetes_amd.cluster import LocalCluster
+from kubernetes_amd.controllers.volume import best_match
+
+
+def pv(name, size, cls="", modes=("ReadWriteOnce",), policy="Retain", path="/tmp/x", labels=None):
+    return {"metadata": {"name": name, "labels": labels or {}},
+            "spec": {"capacity": {"storage": size}, "accessModes": list(modes), "storageClassName": cls,
+                     "persistentVolumeReclaimPolicy": policy, "hostPath": {"path": path}}, "status": {"phase": "Available"}}
+
+
+def pvc(name, size, cls=None, modes=("ReadWriteOnce",), selector=None):
+    sp = {"accessModes": list(modes), "resources": {"requests": {"storage": size}}}
+    if cls is not None:
+        sp["storageClassName"] = cls
+    if selector:
+        sp["selector"] = selector
+    return {"metadata": {"name": name, "namespace": "default", "uid": "u-" + name}, "spec": sp}
+
+
+def test_best_match():
+    pvs = [pv("big", "100Gi"), pv("small", "10Gi"), pv("rwx", "5Gi", modes=("ReadWriteMany",)),
+           pv("fast", "20Gi", cls="fast"), pv("lab", "50Gi", labels={"tier": "gold"})]
+    assert best_match(pvs, pvc("c", "8Gi"))["metadata"]["name"] == "small"
+    assert best_match(pvs, pvc("c", "11Gi"))["metadata"]["name"] == "lab"
+    assert best_match(pvs, pvc("c", "1Gi", modes=("ReadWriteMany",)))["metadata"]["name"] == "rwx"
+    assert best_match(pvs, pvc("c", "1Gi", cls="fast"))["metadata"]["name"] == "fast"
+    assert best_match(pvs, pvc("c", "1Gi", selector={"matchLabels": {"tier": "gold"}}))["metadata"]["name"] == "lab"
+    assert best_match(pvs, pvc("c", "1Ti")) is None
+
+
+def test_pv_lifecycle_end_to_end(run, tmp_path):
+    async def main():
+        cl = LocalCluster(nodes=1, gpus_per_node=0, runtime="process", workdir=str(tmp_path / "c"),
+                          controllers=["persistentvolume-binder", "pvc-protection"],
+                          controller_options={"persistentvolume-binder": {"hostpath_root": str(tmp_path / "hp")}})
+        await cl.start()
+        c = cl.client
+        try:
+            # static PV + claim -> Bound
+            os.makedirs(tmp_path / "static", exist_ok=True)
+            await c.create("persistentvolumes", pv("static-pv", "10Gi", path=str(tmp_path / "static"), policy="Retain"))
+            await c.create("persistentvolumeclaims", pvc("data", "5Gi", cls=""))
+
+            async def bound(name):
+                p = await c.get("persistentvolumeclaims", name, "default")
+                return p if (p.get("status") or {}).get("phase") == "Bound" else None
+            b = await cl.wait_for(lambda: bound("data"), 15)
+            assert b["spec"]["volumeName"] == "static-pv"
+            assert "kubernetes.io/pvc-protection" in b["metadata"]["finalizers"]
+            v = await c.get("persistentvolumes", "static-pv")
+            assert v["status"]["phase"] == "Bound" and v["spec"]["claimRef"]["name"] == "data"
+            # default StorageClass + dynamic hostPath provisioning
+            await c.create("storageclasses", {"metadata": {"name": "local", "annotations": {
+                "storageclass.kubernetes.io/is-default-class": "true"}}, "provisioner": "kubernetes.io/host-path",
+                "reclaimPolicy": "Delete"})
+            created = await c.create("persistentvolumeclaims", pvc("scratch", "1Gi"))
+            assert created["spec"]["storageClassName"] == "local"
+            s = await cl.wait_for(lambda: bound("scratch"), 15)
+            dyn = await c.get("persistentvolumes", s["spec"]["volumeName"])
+            path = dyn["spec"]["hostPath"]["path"]
+            assert path.startswith(str(tmp_path / "hp")) and os.path.isdir(path)
+            # a pod writes into the claim through the kubelet's volume manager
+            await c.create("pods", {"metadata": {"name": "writer", "namespace": "default"}, "spec": {
+                "restartPolicy": "Never", "volumes": [{"name": "d", "persistentVolumeClaim": {"claimName": "scratch"}}],
+                "containers": [{"name": "w", "image": "busybox", "volumeMounts": [{"name": "d", "mountPath": "/data"}],
+                                "command": ["sh", "-c", "echo gfx950 > $KUBERNETES_VOLUME_D/out.txt"]}]}})
+            await cl.wait_pod("writer", phase="Succeeded", timeout=20)
+            assert open(os.path.join(path, "out.txt")).read().strip() == "gfx950"
+            # PVC protection: delete while the (finished) pod exists is fine since it is terminal
+            await c.delete("persistentvolumeclaims", "scratch", "default")
+
+            async def gone(kind, name, ns=None):
+                try:
+                    await c.get(kind, name, ns)
+                    return False
+                except Exception:
+                    return True
+            await cl.wait_for(lambda: gone("persistentvolumeclaims", "scratch", "default"), 15)
+            # reclaim Delete: PV and its directory are removed
+            await cl.wait_for(lambda: gone("persistentvolumes", dyn["metadata"]["name"]), 15)
+            assert not os.path.exists(path)
+            # reclaim Retain: the static PV is Released, not deleted
+            await c.delete("persistentvolumeclaims", "data", "default")
+
+            async def released():
+                v = await c.get("persistentvolumes", "static-pv")
+                return (v.get("status") or {}).get("phase") == "Released"
+            await cl.wait_for(released, 15)
+            # a claim in use by a running pod stays (finalizer) until the pod is gone
+            await c.create("persistentvolumes", pv("pv2", "1Gi", path=str(tmp_path / "pv2"), policy="Retain"))
+            await c.create("persistentvolumeclaims", pvc("busy", "1Gi", cls=""))
+            await cl.wait_for(lambda: bound("busy"), 15)
+            await c.create("pods", {"metadata": {"name": "user", "namespace": "default"}, "spec": {
+                "volumes": [{"name": "d", "persistentVolumeClaim": {"claimName": "busy"}}],
+                "containers": [{"name": "u", "image": "busybox", "command": [sys.executable, "-c", "import time; time.sleep(60)"]}]}})
+            await cl.wait_pod("user", timeout=20)
+            await c.delete("persistentvolumeclaims", "busy", "default")
+            await asyncio.sleep(0.5)
+            still = await c.get("persistentvolumeclaims", "busy", "default")
+            assert still["metadata"].get("deletionTimestamp")
+            await c.delete("pods", "user", "default", grace_period=0)
+            await cl.wait_for(lambda: gone("persistentvolumeclaims", "busy", "default"), 20)
+        finally:
+            await cl.stop()
+    run(main(), timeout=120)
