@@ -274,8 +274,21 @@ def validate_generic(obj, namespaced):
     return validate_object_meta(obj, namespaced)
 
 
+def is_path_segment_name(s):
+    """`path.IsValidPathSegmentName` — RBAC object names may contain ':' (system:node ...)."""
+    return bool(s) and s not in (".", "..") and "/" not in s and "%" not in s
+
+
+def _rbac(namespaced):
+    return lambda obj: validate_object_meta(obj, namespaced, is_path_segment_name)
+
+
 VALIDATORS = {
     "Pod": validate_pod,
     "Node": validate_node,
     "Namespace": validate_namespace,
+    "Role": _rbac(True),
+    "RoleBinding": _rbac(True),
+    "ClusterRole": _rbac(False),
+    "ClusterRoleBinding": _rbac(False),
 }

@@ -124,18 +124,156 @@ class RBACAuthorizer:
 
 
 class NodeAuthorizer:
-    """Nodes may read/write what their pods need; everything else defers to the next authorizer."""
+    """`plugin/pkg/auth/authorizer/node/node_authorizer.go`: a node (`system:node:<name>` in
+    `system:nodes`) may `get` a secret / configmap / PVC / PV only when a pod bound to it
+    references the object (the reference walks a pod -> object graph; here the graph is read from
+    the API server's pod cache); the rest of the node's working set (its Node, pods, events,
+    endpoints, services, leases, CSRs) is allowed; anything else defers to the next authorizer."""
 
-    RESOURCES = {"nodes", "pods", "events", "configmaps", "secrets", "persistentvolumeclaims",
-                 "persistentvolumes", "endpoints", "services", "leases"}
+    GRAPH = {"secrets", "configmaps", "persistentvolumeclaims", "persistentvolumes"}
+    RESOURCES = {"nodes", "pods", "events", "endpoints", "services", "leases", "certificatesigningrequests"}
+
+    def __init__(self, server=None):
+        self.server = server
+
+    def _related(self, node, a):
+        if self.server is None:
+            return True
+        for p in self.server.list_objects("pods"):
+            if (p.get("spec") or {}).get("nodeName") != node:
+                continue
+            sp = p.get("spec") or {}
+            ns = p["metadata"].get("namespace")
+            if a.resource == "persistentvolumes":
+                for v in sp.get("volumes") or ():
+                    c = (v.get("persistentVolumeClaim") or {}).get("claimName")
+                    pvc = self.server.get_object("persistentvolumeclaims", ns, c) if c else None
+                    if pvc and (pvc.get("spec") or {}).get("volumeName") == a.name:
+                        return True
+                continue
+            if ns != a.namespace:
+                continue
+            if a.resource == "secrets":
+                names = {v["secret"].get("secretName") for v in sp.get("volumes") or () if "secret" in v}
+                names |= {r.get("name") for r in sp.get("imagePullSecrets") or ()}
+                for c in (sp.get("containers") or []) + (sp.get("initContainers") or []):
+                    for e in c.get("env") or ():
+                        names.add(((e.get("valueFrom") or {}).get("secretKeyRef") or {}).get("name"))
+                    for ef in c.get("envFrom") or ():
+                        names.add((ef.get("secretRef") or {}).get("name"))
+                for v in sp.get("volumes") or ():
+                    for src in (v.get("projected") or {}).get("sources") or ():
+                        names.add((src.get("secret") or {}).get("name"))
+            elif a.resource == "configmaps":
+                names = {(v.get("configMap") or {}).get("name") for v in sp.get("volumes") or ()}
+                for c in (sp.get("containers") or []) + (sp.get("initContainers") or []):
+                    for e in c.get("env") or ():
+                        names.add(((e.get("valueFrom") or {}).get("configMapKeyRef") or {}).get("name"))
+                    for ef in c.get("envFrom") or ():
+                        names.add((ef.get("configMapRef") or {}).get("name"))
+                for v in sp.get("volumes") or ():
+                    for src in (v.get("projected") or {}).get("sources") or ():
+                        names.add((src.get("configMap") or {}).get("name"))
+            else:
+                names = {(v.get("persistentVolumeClaim") or {}).get("claimName") for v in sp.get("volumes") or ()}
+            if a.name in names:
+                return True
+        return False
 
     def authorize(self, a):
         u = a.user
         if not u.name.startswith("system:node:") or "system:nodes" not in (u.groups or []):
             return None, ""
+        node = u.name[len("system:node:"):]
+        if a.resource in self.GRAPH:
+            if a.verb == "get" and a.name and self._related(node, a):
+                return True, ""
+            return False, f'no path found to object {a.resource}/{a.name} from node "{node}"'
         if a.resource in self.RESOURCES:
             return True, ""
         return None, ""
+
+
+class ABACAuthorizer:
+    """`pkg/auth/authorizer/abac/abac.go`: one JSON policy per line
+    (`{"apiVersion":"abac.authorization.kubernetes.io/v1beta1","kind":"Policy","spec":{...}}`);
+    spec fields user / group / namespace / resource / apiGroup / readonly / nonResourcePath,
+    `*` wildcards; the first matching policy allows."""
+
+    READONLY = {"get", "list", "watch"}
+
+    def __init__(self, path=None, policies=None):
+        self.policies = list(policies or [])
+        if path:
+            import json
+            with open(path) as f:
+                for line in f:
+                    line = line.strip()
+                    if line and not line.startswith("#"):
+                        p = json.loads(line)
+                        self.policies.append(p.get("spec", p))
+
+    @staticmethod
+    def _m(want, have):
+        return want == "*" or want == have
+
+    def authorize(self, a):
+        u = a.user
+        for p in self.policies:
+            if p.get("user") and not self._m(p["user"], u.name):
+                continue
+            if p.get("group") and not (p["group"] == "*" or p["group"] in (u.groups or [])):
+                continue
+            if not p.get("user") and not p.get("group"):
+                continue
+            if p.get("readonly") and a.verb not in self.READONLY:
+                continue
+            if a.resource_request:
+                if not (self._m(p.get("namespace", ""), a.namespace) and self._m(p.get("resource", ""), a.resource)
+                        and self._m(p.get("apiGroup", ""), a.group)):
+                    continue
+            else:
+                np = p.get("nonResourcePath", "")
+                if not (np == "*" or np == a.path or (np.endswith("*") and a.path.startswith(np[:-1]))):
+                    continue
+            return True, ""
+        return None, ""
+
+
+class WebhookAuthorizer:
+    """`staging/src/k8s.io/apiserver/plugin/pkg/authorizer/webhook`: SubjectAccessReview POSTed to
+    a remote service; allowed answers cached 5 min, denied 30 s."""
+
+    def __init__(self, url, allow_ttl=300.0, deny_ttl=30.0, ssl_context=None):
+        self.url, self.allow_ttl, self.deny_ttl, self.ssl = url, allow_ttl, deny_ttl, ssl_context
+        self.cache = {}
+
+    def authorize(self, a):
+        import json
+        import time
+        import urllib.request
+        u = a.user
+        spec = {"user": u.name, "groups": list(u.groups or ()), "uid": u.uid or ""}
+        if a.resource_request:
+            spec["resourceAttributes"] = {"namespace": a.namespace, "verb": a.verb, "group": a.group,
+                                          "resource": a.resource, "subresource": a.subresource, "name": a.name}
+        else:
+            spec["nonResourceAttributes"] = {"path": a.path, "verb": a.verb}
+        key = json.dumps(spec, sort_keys=True)
+        hit = self.cache.get(key)
+        now = time.monotonic()
+        if hit is not None and now < hit[1]:
+            return hit[0]
+        body = json.dumps({"apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview", "spec": spec}).encode()
+        try:
+            req = urllib.request.Request(self.url, body, {"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=10, context=self.ssl) as r:
+                st = json.loads(r.read()).get("status") or {}
+        except OSError as e:
+            return False, f"webhook authorizer error: {e}"
+        res = (True, "") if st.get("allowed") else ((False, st.get("reason", "")) if st.get("denied") else (None, st.get("reason", "")))
+        self.cache[key] = (res, now + (self.allow_ttl if res[0] else self.deny_ttl))
+        return res
 
 
 class UnionAuthorizer:
@@ -163,7 +301,11 @@ def build_authorizer(modes, server):
         elif m == "RBAC":
             azs.append(RBACAuthorizer(server))
         elif m == "Node":
-            azs.append(NodeAuthorizer())
+            azs.append(NodeAuthorizer(server))
+        elif m == "ABAC":
+            azs.append(ABACAuthorizer(getattr(server, "abac_policy_file", None)))
+        elif m == "Webhook":
+            azs.append(WebhookAuthorizer(getattr(server, "authorization_webhook_url", None)))
         else:
             raise ValueError(f"unknown authorization mode {m}")
     return UnionAuthorizer(azs)

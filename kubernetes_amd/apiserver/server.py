@@ -100,7 +100,10 @@ class APIServer:
                  service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767),
                  tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
                  service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
-                 anonymous_auth=True):
+                 anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None):
+        self.abac_policy_file = authorization_policy_file
+        self.authorization_webhook_url = authorization_webhook_url
+        self.authorization_modes = tuple(authorization_modes)
         self.tls = (tls_cert_file, tls_private_key_file, client_ca_file)
         from .service_alloc import ServiceAllocator
         from .extensions import Aggregator, CRDManager, WebhookDispatcher
@@ -260,6 +263,9 @@ class APIServer:
                 except APIError as e:
                     if e.code != 409:   # another worker created it first
                         raise
+        if "RBAC" in self.authorization_modes:
+            from .bootstrappolicy import ensure_bootstrap_policy
+            await ensure_bootstrap_policy(self)
         # the `kubernetes` service on the first IP of the service range
         # (pkg/master/controller.go CreateOrUpdateMasterServiceIfNeeded)
         if self.get_object("services", "default", "kubernetes") is None:

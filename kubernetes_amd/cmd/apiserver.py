@@ -55,6 +55,8 @@ def _parser():
     ap.add_argument("--enable-bootstrap-token-auth", action="store_true")
     ap.add_argument("--authentication-token-webhook-url", default=None)
     ap.add_argument("--anonymous-auth", type=lambda v: v.lower() != "false", default=True)
+    ap.add_argument("--authorization-policy-file", default=None, help="ABAC policy (JSON lines)")
+    ap.add_argument("--authorization-webhook-url", default=None)
     ap.add_argument("--service-cluster-ip-range", default="10.0.0.0/24")
     ap.add_argument("--service-node-port-range", default="30000-32767")
     ap.add_argument("-v", type=int, default=0)
@@ -164,7 +166,9 @@ def main(argv=None):
                       client_ca_file=a.client_ca_file, service_account_key_files=a.service_account_key_file,
                       service_account_lookup=a.service_account_lookup,
                       enable_bootstrap_token_auth=a.enable_bootstrap_token_auth,
-                      authentication_token_webhook=a.authentication_token_webhook_url, anonymous_auth=a.anonymous_auth)
+                      authentication_token_webhook=a.authentication_token_webhook_url, anonymous_auth=a.anonymous_auth,
+                      authorization_policy_file=a.authorization_policy_file,
+                      authorization_webhook_url=a.authorization_webhook_url)
         port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
         if not a.reuse_port:
