@@ -1,0 +1,405 @@
+"""Security and policy admission plugins.
+
+  * PodSecurityPolicy — `plugin/pkg/admission/security/podsecuritypolicy/admission.go` +
+    `pkg/security/podsecuritypolicy`: the pod must validate against at least one PSP the
+    requesting user (or the pod's service account) may `use`; the first policy (by name) that
+    validates without mutation wins, else the first that validates after defaulting
+    (runAsUser MustRunAs range default, default add-capabilities, read-only root fs default);
+    the chosen policy is recorded in annotation `kubernetes.io/psp`. Checked fields: privileged,
+    hostNetwork / hostPID / hostIPC, hostPorts ranges, volume types (`*` allowed),
+    allowedHostPaths prefixes, allowed / required-drop capabilities, runAsUser
+    (MustRunAs ranges / MustRunAsNonRoot / RunAsAny), readOnlyRootFilesystem,
+    allowPrivilegeEscalation. MI355X: a PSP can forbid device access by volume type (hostPath
+    `/dev`) — GPU devices themselves are injected by the kubelet only for allocated IDs.
+  * PodPreset — `plugin/pkg/admission/podpreset/admission.go`: presets whose selector matches
+    the pod's labels merge env / envFrom / volumes / volumeMounts into every container (conflicts
+    reject the preset), annotation `podpreset.admission.kubernetes.io/podpreset-<name>: <rv>`;
+    opt-out annotation `podpreset.admission.kubernetes.io/exclude: "true"`.
+  * EventRateLimit — `plugin/pkg/admission/eventratelimit`: token buckets on event creation per
+    Server / Namespace / User (qps, burst); over the limit -> 429.
+  * PodTolerationRestriction — `plugin/pkg/admission/podtolerationrestriction`: namespace
+    annotations `scheduler.alpha.kubernetes.io/defaultTolerations` are merged in and
+    `.../tolerationsWhitelist` is enforced.
+  * DenyEscalatingExec / DenyExecOnPrivileged — `plugin/pkg/admission/exec`: no exec/attach into
+    privileged or host-namespace pods.
+  * SecurityContextDeny — `plugin/pkg/admission/securitycontext/scdeny`: rejects pods setting
+    SELinux options / runAsUser / supplementalGroups / fsGroup.
+  * OwnerReferencesPermissionEnforcement — `plugin/pkg/admission/gc`: setting
+    `blockOwnerDeletion` requires `update` on the owner's `finalizers` subresource.
+  * ImagePolicyWebhook — `plugin/pkg/admission/imagepolicy`: an ImageReview is POSTed to a
+    backend; default-deny on backend failure unless `defaultAllow`.
+"""
+from __future__ import annotations
+
+import json
+import time
+
+from ...api.labels import label_selector_as_selector
+from . import CONNECT, CREATE, UPDATE, AdmissionError, Plugin, register
+
+PSP_ANN = "kubernetes.io/psp"
+
+
+def _sc(c):
+    return c.get("securityContext") or {}
+
+
+def _containers(spec):
+    return list(spec.get("initContainers") or []) + list(spec.get("containers") or [])
+
+
+def _in_ranges(v, ranges):
+    return any(int(r.get("min", 0)) <= v <= int(r.get("max", 0)) for r in ranges or ())
+
+
+class PSPEvaluator:
+    """Validate (and default) one pod against one PodSecurityPolicy. Returns (errors, mutated pod)."""
+
+    def __init__(self, psp):
+        self.psp = psp
+        self.sp = psp.get("spec") or {}
+
+    def check(self, pod):
+        import copy
+        pod = copy.deepcopy(pod)
+        sp, errs = self.sp, []
+        spec = pod.setdefault("spec", {})
+        name = self.psp["metadata"]["name"]
+        for f in ("hostNetwork", "hostPID", "hostIPC"):
+            if spec.get(f) and not sp.get(f):
+                errs.append(f"{f}: Invalid value: true: {f} is not allowed to be used")
+        vols = sp.get("volumes") or []
+        for v in spec.get("volumes") or ():
+            kind = next((k for k in v if k != "name"), "")
+            if "*" not in vols and kind not in vols:
+                errs.append(f"volumes: {kind} volumes are not allowed to be used")
+            if kind == "hostPath" and sp.get("allowedHostPaths"):
+                p = v["hostPath"].get("path", "")
+                if not any(p == a.get("pathPrefix") or p.startswith(a.get("pathPrefix", "").rstrip("/") + "/")
+                           for a in sp["allowedHostPaths"]):
+                    errs.append(f"volumes.hostPath.path: {p} is not allowed to be used")
+        host_ports = sp.get("hostPorts") or []
+        allowed_caps = set(sp.get("allowedCapabilities") or [])
+        required_drop = set(sp.get("requiredDropCapabilities") or [])
+        default_add = list(sp.get("defaultAddCapabilities") or [])
+        rau = sp.get("runAsUser") or {"rule": "RunAsAny"}
+        for c in _containers(spec):
+            sc = c.setdefault("securityContext", {})
+            cn = c.get("name", "")
+            if sc.get("privileged") and not sp.get("privileged"):
+                errs.append(f"containers[{cn}].securityContext.privileged: Privileged containers are not allowed")
+            for port in c.get("ports") or ():
+                hp = port.get("hostPort")
+                if hp and not _in_ranges(int(hp), host_ports):
+                    errs.append(f"containers[{cn}].hostPort: Invalid value: {hp}: Host port {hp} is not allowed to be used")
+            caps = sc.setdefault("capabilities", {}) if (default_add or required_drop or sc.get("capabilities")) else {}
+            if caps is not None and (default_add or required_drop):
+                add = list(caps.get("add") or [])
+                for d in default_add:
+                    if d not in add:
+                        add.append(d)
+                if add:
+                    caps["add"] = add
+                drop = list(caps.get("drop") or [])
+                for d in sorted(required_drop):
+                    if d not in drop:
+                        drop.append(d)
+                if drop:
+                    caps["drop"] = drop
+            for cap in (sc.get("capabilities") or {}).get("add") or ():
+                if cap in required_drop:
+                    errs.append(f"containers[{cn}].capabilities.add: capability {cap} may not be added")
+                elif "*" not in allowed_caps and cap not in allowed_caps and cap not in default_add:
+                    errs.append(f"containers[{cn}].capabilities.add: capability may not be added: {cap}")
+            rule = rau.get("rule", "RunAsAny")
+            uid = sc.get("runAsUser", _sc(spec).get("runAsUser"))
+            if rule == "MustRunAs":
+                if uid is None:
+                    rng = (rau.get("ranges") or [{"min": 1}])[0]
+                    sc["runAsUser"] = int(rng["min"])
+                elif not _in_ranges(int(uid), rau.get("ranges")):
+                    errs.append(f"containers[{cn}].runAsUser: Invalid value: {uid}: UID on container {cn} does not match required range")
+            elif rule == "MustRunAsNonRoot":
+                if uid == 0 or (uid is None and not sc.get("runAsNonRoot") and not _sc(spec).get("runAsNonRoot")):
+                    if uid == 0:
+                        errs.append(f"containers[{cn}].runAsUser: Invalid value: 0: running with the root UID is forbidden")
+                    else:
+                        sc["runAsNonRoot"] = True
+            if sp.get("readOnlyRootFilesystem"):
+                if sc.get("readOnlyRootFilesystem") is False:
+                    errs.append(f"containers[{cn}].securityContext.readOnlyRootFilesystem: Invalid value: false: "
+                                "ReadOnlyRootFilesystem must be set to true")
+                sc.setdefault("readOnlyRootFilesystem", True)
+            if sp.get("allowPrivilegeEscalation") is False:
+                if sc.get("allowPrivilegeEscalation"):
+                    errs.append(f"containers[{cn}].securityContext.allowPrivilegeEscalation: Invalid value: true: "
+                                "Allowing privilege escalation for containers is not allowed")
+                sc.setdefault("allowPrivilegeEscalation", False)
+            if not sc:
+                c.pop("securityContext", None)
+        pod.setdefault("metadata", {}).setdefault("annotations", {})[PSP_ANN] = name
+        return [f"{name}: {e}" for e in errs], pod
+
+
+@register
+class PodSecurityPolicy(Plugin):
+    name = "PodSecurityPolicy"
+    operations = (CREATE, UPDATE)
+
+    def _can_use(self, user, psp, ns, sa_name):
+        from ..auth import AttributesRecord, User
+        az = getattr(self.server, "authz", None)
+        if az is None:
+            return True
+        name = psp["metadata"]["name"]
+        subjects = [user] if user is not None else []
+        if sa_name:
+            subjects.append(User(f"system:serviceaccount:{ns}:{sa_name}", "",
+                                 ["system:serviceaccounts", f"system:serviceaccounts:{ns}", "system:authenticated"]))
+        for u in subjects:
+            for scope in (ns, ""):
+                ok, _ = az.authorize(AttributesRecord(u, "use", scope, "podsecuritypolicies", "", name, "policy", "", True))
+                if ok:
+                    return True
+        return False
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        if a.operation == UPDATE:
+            return   # the reference re-validates only on create for pods (spec is immutable)
+        psps = sorted(self.server.list_objects("podsecuritypolicies"), key=lambda p: p["metadata"]["name"])
+        spec = a.obj.get("spec") or {}
+        usable = [p for p in psps if self._can_use(a.user, p, a.namespace, spec.get("serviceAccountName"))]
+        if not usable:
+            raise AdmissionError(f'pods "{a.name}" is forbidden: no providers available to validate pod request')
+        import copy
+        orig = copy.deepcopy(a.obj)
+        allerrs, fallback = [], None
+        for p in usable:
+            errs, mutated = PSPEvaluator(p).check(a.obj)
+            if errs:
+                allerrs += errs
+                continue
+            unchanged = {k: v for k, v in mutated.items() if k != "metadata"} == {k: v for k, v in orig.items() if k != "metadata"}
+            if unchanged:
+                a.obj.clear()
+                a.obj.update(mutated)
+                return
+            if fallback is None:
+                fallback = mutated
+        if fallback is not None:
+            a.obj.clear()
+            a.obj.update(fallback)
+            return
+        raise AdmissionError(f'pods "{a.name}" is forbidden: unable to validate against any pod security policy: {allerrs}')
+
+
+@register
+class PodPreset(Plugin):
+    name = "PodPreset"
+    operations = (CREATE,)
+    EXCLUDE = "podpreset.admission.kubernetes.io/exclude"
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource:
+            return
+        pod = a.obj
+        md = pod.setdefault("metadata", {})
+        if (md.get("annotations") or {}).get(self.EXCLUDE) == "true":
+            return
+        labels = md.get("labels") or {}
+        spec = pod.setdefault("spec", {})
+        for pp in sorted(self.server.list_objects("podpresets", a.namespace), key=lambda p: p["metadata"]["name"]):
+            ps = pp.get("spec") or {}
+            if not label_selector_as_selector(ps.get("selector")).matches(labels):
+                continue
+            vols = {v["name"]: v for v in spec.get("volumes") or ()}
+            conflict = any(v["name"] in vols and vols[v["name"]] != v for v in ps.get("volumes") or ())
+            for c in spec.get("containers") or ():
+                env = {e["name"]: e for e in c.get("env") or ()}
+                mounts = {m["mountPath"]: m for m in c.get("volumeMounts") or ()}
+                conflict |= any(e["name"] in env and env[e["name"]] != e for e in ps.get("env") or ())
+                conflict |= any(m["mountPath"] in mounts and mounts[m["mountPath"]] != m for m in ps.get("volumeMounts") or ())
+            if conflict:
+                continue   # reference: event + skip the conflicting preset
+            for v in ps.get("volumes") or ():
+                if v["name"] not in vols:
+                    spec.setdefault("volumes", []).append(v)
+            for c in spec.get("containers") or ():
+                for e in ps.get("env") or ():
+                    if e["name"] not in {x["name"] for x in c.get("env") or ()}:
+                        c.setdefault("env", []).append(e)
+                for ef in ps.get("envFrom") or ():
+                    c.setdefault("envFrom", []).append(ef)
+                for m in ps.get("volumeMounts") or ():
+                    if m["mountPath"] not in {x["mountPath"] for x in c.get("volumeMounts") or ()}:
+                        c.setdefault("volumeMounts", []).append(m)
+            md.setdefault("annotations", {})[f"podpreset.admission.kubernetes.io/podpreset-{pp['metadata']['name']}"] = \
+                pp["metadata"].get("resourceVersion", "")
+
+
+class _Bucket:
+    def __init__(self, qps, burst):
+        self.qps, self.burst = float(qps), float(burst)
+        self.tokens, self.t = float(burst), time.monotonic()
+
+    def take(self):
+        now = time.monotonic()
+        self.tokens = min(self.burst, self.tokens + (now - self.t) * self.qps)
+        self.t = now
+        if self.tokens >= 1:
+            self.tokens -= 1
+            return True
+        return False
+
+
+@register
+class EventRateLimit(Plugin):
+    name = "EventRateLimit"
+    operations = (CREATE,)
+
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        self.limits = (config or {}).get("limits") or [{"type": "Server", "qps": 5000, "burst": 20000}]
+        self.buckets: dict = {}
+
+    def validate(self, a):
+        if a.resource != "events":
+            return
+        for lim in self.limits:
+            t = lim.get("type", "Server")
+            key = (t, "" if t == "Server" else a.namespace if t == "Namespace" else getattr(a.user, "name", ""))
+            b = self.buckets.get(key)
+            if b is None:
+                b = self.buckets[key] = _Bucket(lim.get("qps", 10), lim.get("burst", 100))
+            if not b.take():
+                raise AdmissionError("limit reached on type %s for key %s" % (t, key[1]), 429, "TooManyRequests")
+
+
+@register
+class PodTolerationRestriction(Plugin):
+    name = "PodTolerationRestriction"
+    operations = (CREATE, UPDATE)
+    DEFAULT = "scheduler.alpha.kubernetes.io/defaultTolerations"
+    WHITELIST = "scheduler.alpha.kubernetes.io/tolerationsWhitelist"
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource or a.operation != CREATE:
+            return
+        ns = self.server.get_object("namespaces", None, a.namespace) if self.server else None
+        ann = ((ns or {}).get("metadata") or {}).get("annotations") or {}
+        spec = a.obj.setdefault("spec", {})
+        if self.DEFAULT in ann:
+            have = spec.get("tolerations") or []
+            for t in json.loads(ann[self.DEFAULT]):
+                if not any(x.get("key") == t.get("key") and x.get("effect") == t.get("effect") for x in have):
+                    have.append(t)
+            spec["tolerations"] = have
+        # whitelist verification right after the merge, in the mutating phase like the reference
+        # (`admission.go:149-167`): plugins later in the chain may still add tolerations
+        if self.WHITELIST not in ann:
+            return
+        wl = json.loads(ann[self.WHITELIST])
+        for t in (a.obj.get("spec") or {}).get("tolerations") or ():
+            ok = any(w.get("key") == t.get("key") and w.get("operator", "Equal") == t.get("operator", "Equal")
+                     and w.get("value") == t.get("value") and w.get("effect") == t.get("effect") for w in wl)
+            if not ok:
+                raise AdmissionError("pod tolerations (possibly merged with namespace default tolerations) conflict "
+                                     "with its namespace whitelist")
+
+
+@register
+class DenyEscalatingExec(Plugin):
+    name = "DenyEscalatingExec"
+    operations = (CONNECT, CREATE)
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource not in ("exec", "attach"):
+            return
+        pod = self.server.get_object("pods", a.namespace, a.name) if self.server else None
+        if pod is None:
+            return
+        spec = pod.get("spec") or {}
+        if spec.get("hostPID") or spec.get("hostIPC"):
+            raise AdmissionError("cannot exec into or attach to a container using host pid or ipc")
+        if any(_sc(c).get("privileged") for c in _containers(spec)):
+            raise AdmissionError("cannot exec into or attach to a privileged container")
+
+
+@register
+class SecurityContextDeny(Plugin):
+    name = "SecurityContextDeny"
+    operations = (CREATE, UPDATE)
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource or a.obj is None:
+            return
+        spec = a.obj.get("spec") or {}
+        psc = spec.get("securityContext") or {}
+        for f in ("supplementalGroups", "seLinuxOptions", "runAsUser", "fsGroup"):
+            if f in psc:
+                raise AdmissionError(f"pod.Spec.SecurityContext.{f} is forbidden")
+        for c in _containers(spec):
+            for f in ("seLinuxOptions", "runAsUser"):
+                if f in _sc(c):
+                    raise AdmissionError(f"SecurityContext.{f} is forbidden")
+
+
+@register
+class OwnerReferencesPermissionEnforcement(Plugin):
+    name = "OwnerReferencesPermissionEnforcement"
+    operations = (CREATE, UPDATE)
+
+    def validate(self, a):
+        if a.obj is None or a.subresource:
+            return
+        new = [r for r in (a.obj.get("metadata") or {}).get("ownerReferences") or () if r.get("blockOwnerDeletion")]
+        old = {r.get("uid") for r in ((a.old or {}).get("metadata") or {}).get("ownerReferences") or () if r.get("blockOwnerDeletion")}
+        added = [r for r in new if r.get("uid") not in old]
+        if not added:
+            return
+        from ...api import meta as m
+        from ..auth import AttributesRecord
+        for r in added:
+            ri = m.BY_KIND.get(r.get("kind"))
+            if ri is None:
+                continue
+            ok, _ = self.server.authz.authorize(AttributesRecord(a.user, "update", a.namespace if ri.namespaced else "",
+                                                                 ri.plural, "finalizers", r.get("name", ""), ri.group, "", True))
+            if not ok:
+                raise AdmissionError(f"cannot set blockOwnerDeletion if an ownerReference refers to a resource you can't set "
+                                     f"finalizers on: User \"{getattr(a.user, 'name', '')}\" cannot update {ri.plural}/finalizers")
+
+
+@register
+class ImagePolicyWebhook(Plugin):
+    name = "ImagePolicyWebhook"
+    operations = (CREATE, UPDATE)
+
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        cfg = config or {}
+        self.url = cfg.get("url")
+        self.default_allow = bool(cfg.get("defaultAllow", False))
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource or a.obj is None or not self.url:
+            return
+        import urllib.request
+        spec = a.obj.get("spec") or {}
+        review = {"apiVersion": "imagepolicy.k8s.io/v1alpha1", "kind": "ImageReview",
+                  "spec": {"containers": [{"image": c.get("image", "")} for c in _containers(spec)],
+                           "annotations": {k: v for k, v in ((a.obj.get("metadata") or {}).get("annotations") or {}).items()
+                                           if ".image-policy.k8s.io/" in k},
+                           "namespace": a.namespace}}
+        try:
+            req = urllib.request.Request(self.url, json.dumps(review).encode(), {"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=10) as r:
+                st = json.loads(r.read()).get("status") or {}
+        except OSError as e:
+            if self.default_allow:
+                return
+            raise AdmissionError(f"image policy webhook backend denied one or more images: {e}")
+        if not st.get("allowed"):
+            raise AdmissionError(f"image policy webhook backend denied one or more images: {st.get('reason', '')}")

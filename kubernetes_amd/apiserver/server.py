@@ -1288,6 +1288,9 @@ class APIServer:
         the node's kubelet (`pkg/registry/core/pod/rest/subresources.go` ExecREST/PortForwardREST)."""
         from urllib.parse import parse_qs, urlencode
         pod, addr, port = self._kubelet_of(ns, name)
+        a = adm.Attributes(adm.CONNECT, "pods", sub, ns, name, None, pod, getattr(req, "user", None), "Pod")
+        self._admit(a)
+        self._validate_admission(a)
         q = parse_qs(req.qs or "")
         if sub == "portforward":
             pport = (q.get("port") or q.get("ports") or [""])[0]

@@ -1,0 +1,125 @@
+"""PodSecurityPolicy, PodPreset, EventRateLimit, PodTolerationRestriction, DenyEscalatingExec,
+SecurityContextDeny, OwnerReferencesPermissionEnforcement admission plugins.
+
+Parity: `plugin/pkg/admission/security/podsecuritypolicy/admission_test.go`,
+`plugin/pkg/admission/podpreset/admission_test.go`, `eventratelimit/admission_test.go`,
+`podtolerationrestriction/admission_test.go`, `exec/admission_test.go`,
+`securitycontext/scdeny/admission_test.go`, `gc/gc_admission_test.go`.
+"""
+import json
+
+import pytest
+
+from kubernetes_amd.apiserver.admission import DEFAULT_PLUGINS
+from kubernetes_amd.apiserver.auth import User
+from kubernetes_amd.apiserver.server import APIServer
+from kubernetes_amd.client.rest import APIStatusError, Client
+
+
+def pod(name, **spec):
+    base = {"containers": [{"name": "c", "image": "rocm/pytorch:latest"}]}
+    base.update(spec)
+    return {"metadata": {"name": name, "namespace": "default", "labels": {"app": "train"}}, "spec": base}
+
+
+async def _srv(plugins, **kw):
+    s = APIServer(admission_plugins=plugins, **kw)
+    port = await s.start()
+    return s, Client(f"http://127.0.0.1:{port}", token=kw.get("tokens") and "admin")
+
+
+def test_pod_security_policy(run):
+    async def main():
+        toks = {"admin": User("admin", "0", ["system:masters"]), "dev": User("dev", "1", ["system:authenticated"])}
+        s, admin = await _srv(DEFAULT_PLUGINS + ["PodSecurityPolicy"], tokens=toks, authorization_modes=("RBAC",))
+        dev = Client(admin.url, token="dev")
+        try:
+            await admin.create("podsecuritypolicies", {"metadata": {"name": "restricted"}, "spec": {
+                "privileged": False, "volumes": ["configMap", "secret", "emptyDir", "persistentVolumeClaim"],
+                "runAsUser": {"rule": "MustRunAs", "ranges": [{"min": 1000, "max": 2000}]},
+                "requiredDropCapabilities": ["NET_RAW"], "allowPrivilegeEscalation": False,
+                "hostPorts": [{"min": 8000, "max": 8100}]}})
+            await admin.create("podsecuritypolicies", {"metadata": {"name": "z-privileged"}, "spec": {
+                "privileged": True, "volumes": ["*"], "hostNetwork": True, "runAsUser": {"rule": "RunAsAny"},
+                "allowedCapabilities": ["*"], "hostPorts": [{"min": 0, "max": 65535}]}})
+            await admin.create("clusterroles", {"metadata": {"name": "psp:restricted"}, "rules": [
+                {"apiGroups": ["policy"], "resources": ["podsecuritypolicies"], "resourceNames": ["restricted"], "verbs": ["use"]}]})
+            await admin.create("clusterrolebindings", {"metadata": {"name": "dev-restricted"},
+                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "psp:restricted"},
+                "subjects": [{"kind": "User", "name": "dev"}]})
+            await admin.create("clusterroles", {"metadata": {"name": "pods"}, "rules": [
+                {"apiGroups": [""], "resources": ["pods"], "verbs": ["*"]}]})
+            await admin.create("clusterrolebindings", {"metadata": {"name": "dev-pods"},
+                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "pods"},
+                "subjects": [{"kind": "User", "name": "dev"}]})
+            # defaults applied by the restricted policy
+            p = await dev.create("pods", pod("ok"))
+            sc = p["spec"]["containers"][0]["securityContext"]
+            assert sc["runAsUser"] == 1000 and sc["allowPrivilegeEscalation"] is False
+            assert sc["capabilities"]["drop"] == ["NET_RAW"]
+            assert p["metadata"]["annotations"]["kubernetes.io/psp"] == "restricted"
+            for bad in (pod("priv", containers=[{"name": "c", "image": "x", "securityContext": {"privileged": True}}]),
+                        pod("hostnet", hostNetwork=True),
+                        pod("hp", volumes=[{"name": "dev", "hostPath": {"path": "/dev"}}]),
+                        pod("root", containers=[{"name": "c", "image": "x", "securityContext": {"runAsUser": 0}}]),
+                        pod("port", containers=[{"name": "c", "image": "x", "ports": [{"containerPort": 80, "hostPort": 80}]}])):
+                with pytest.raises(APIStatusError) as e:
+                    await dev.create("pods", bad)
+                assert e.value.code == 403, bad["metadata"]["name"]
+            # the admin may use every policy: the privileged one admits a host-network pod
+            p = await admin.create("pods", pod("admin-hostnet", hostNetwork=True))
+            assert p["metadata"]["annotations"]["kubernetes.io/psp"] == "z-privileged"
+        finally:
+            await dev.close()
+            await admin.close()
+            await s.stop()
+    run(main())
+
+
+def test_podpreset_toleration_restriction_ratelimit_scdeny(run):
+    async def main():
+        cfg = {"EventRateLimit": {"limits": [{"type": "Namespace", "qps": 0.001, "burst": 2}]}}
+        chain = list(DEFAULT_PLUGINS)
+        chain.insert(chain.index("DefaultTolerationSeconds"), "PodTolerationRestriction")
+        s = APIServer(admission_plugins=chain + ["PodPreset", "EventRateLimit", "SecurityContextDeny"], admission_config=cfg)
+        port = await s.start()
+        c = Client(f"http://127.0.0.1:{port}")
+        try:
+            await c.create("podpresets", {"metadata": {"name": "rocm-env", "namespace": "default"}, "spec": {
+                "selector": {"matchLabels": {"app": "train"}},
+                "env": [{"name": "HSA_FORCE_FINE_GRAIN_PCIE", "value": "1"}],
+                "volumes": [{"name": "cache", "emptyDir": {}}],
+                "volumeMounts": [{"name": "cache", "mountPath": "/root/.cache"}]}})
+            p = await c.create("pods", pod("a"))
+            ctr = p["spec"]["containers"][0]
+            assert {"name": "HSA_FORCE_FINE_GRAIN_PCIE", "value": "1"} in ctr["env"]
+            assert ctr["volumeMounts"] == [{"name": "cache", "mountPath": "/root/.cache"}]
+            assert "podpreset.admission.kubernetes.io/podpreset-rocm-env" in p["metadata"]["annotations"]
+            ex = pod("b")
+            ex["metadata"]["annotations"] = {"podpreset.admission.kubernetes.io/exclude": "true"}
+            assert "env" not in (await c.create("pods", ex))["spec"]["containers"][0]
+            # namespace default tolerations + whitelist
+            await c.create("namespaces", {"metadata": {"name": "gpu-team", "annotations": {
+                "scheduler.alpha.kubernetes.io/defaultTolerations": json.dumps([{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]),
+                "scheduler.alpha.kubernetes.io/tolerationsWhitelist": json.dumps([{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}])}}})
+            gp = pod("g")
+            gp["metadata"]["namespace"] = "gpu-team"
+            got = await c.create("pods", gp, "gpu-team")
+            assert {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"} in got["spec"]["tolerations"]
+            bad = pod("h", tolerations=[{"key": "dedicated", "operator": "Equal", "value": "x", "effect": "NoSchedule"}])
+            bad["metadata"]["namespace"] = "gpu-team"
+            with pytest.raises(APIStatusError):
+                await c.create("pods", bad, "gpu-team")
+            # SecurityContextDeny
+            with pytest.raises(APIStatusError):
+                await c.create("pods", pod("sc", securityContext={"runAsUser": 0}))
+            # EventRateLimit: burst 2 per namespace
+            for i in range(2):
+                await c.create("events", {"metadata": {"name": f"e{i}", "namespace": "default"}, "involvedObject": {}})
+            with pytest.raises(APIStatusError) as e:
+                await c.create("events", {"metadata": {"name": "e9", "namespace": "default"}, "involvedObject": {}})
+            assert e.value.code == 429
+        finally:
+            await c.close()
+            await s.stop()
+    run(main())
