@@ -10,7 +10,13 @@ from ._common import run_until_signal, setup_logging
 
 def main(argv=None):
     ap = argparse.ArgumentParser("kube-controller-manager")
-    ap.add_argument("--master", required=True)
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--service-account-private-key-file", default=None)
+    ap.add_argument("--root-ca-file", default=None)
+    ap.add_argument("--cluster-signing-cert-file", default=None)
+    ap.add_argument("--cluster-signing-key-file", default=None)
+    ap.add_argument("--horizontal-pod-autoscaler-sync-period", type=float, default=30.0)
     ap.add_argument("--controllers", default="*", help=f"comma list; '*' = all of {sorted(CONTROLLERS)}, '-name' disables")
     ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
     ap.add_argument("--pod-eviction-timeout", type=float, default=300.0)
@@ -21,12 +27,19 @@ def main(argv=None):
     setup_logging(a.v)
 
     async def start():
-        client = Client(a.master, max_conns=64)
+        if a.kubeconfig:
+            from ..client.clientcmd import client_from
+            client = client_from(a.kubeconfig, max_conns=64)
+        else:
+            client = Client(a.master or "http://127.0.0.1:8080", max_conns=64)
         if a.leader_elect:
             from ..client.leaderelection import LeaderElector
             await LeaderElector(client, "kube-system", "kube-controller-manager").acquire()
         opts = {"nodelifecycle": {"grace": a.node_monitor_grace_period, "pod_eviction_timeout": a.pod_eviction_timeout},
-                "podgc": {"terminated_pod_gc_threshold": a.terminated_pod_gc_threshold}}
+                "podgc": {"terminated_pod_gc_threshold": a.terminated_pod_gc_threshold},
+                "serviceaccount-token": {"private_key_file": a.service_account_private_key_file, "root_ca_file": a.root_ca_file},
+                "csrsigning": {"cert_file": a.cluster_signing_cert_file, "key_file": a.cluster_signing_key_file},
+                "horizontalpodautoscaling": {"sync_period": a.horizontal_pod_autoscaler_sync_period}}
         return await ControllerManager(client, a.controllers.split(","), opts).start()
 
     run_until_signal(start)

@@ -16,7 +16,11 @@ from ._common import run_until_signal, setup_logging
 
 def main(argv=None):
     ap = argparse.ArgumentParser("kubelet")
-    ap.add_argument("--api-servers", "--master", dest="master", required=True)
+    ap.add_argument("--api-servers", "--master", dest="master", default=None)
+    ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--bootstrap-kubeconfig", default=None,
+                    help="TLS bootstrap: obtain a client certificate via a CSR with these credentials, "
+                         "then write --kubeconfig")
     ap.add_argument("--hostname-override", default=os.uname().nodename)
     ap.add_argument("--root-dir", default="/var/lib/kubelet")
     ap.add_argument("--device-plugins-dir", default=None)
@@ -46,7 +50,15 @@ def main(argv=None):
     DefaultFeatureGate.set(a.feature_gates)
 
     async def start():
-        client = Client(a.master, token=a.token, max_conns=32)
+        if a.bootstrap_kubeconfig and a.kubeconfig and not os.path.exists(a.kubeconfig):
+            from ..kubelet.certificate import bootstrap_client_certificate
+            await bootstrap_client_certificate(a.bootstrap_kubeconfig, a.kubeconfig, a.hostname_override,
+                                               os.path.join(a.root_dir, "pki"))
+        if a.kubeconfig:
+            from ..client.clientcmd import client_from
+            client = client_from(a.kubeconfig, max_conns=32)
+        else:
+            client = Client(a.master or "http://127.0.0.1:8080", token=a.token, max_conns=32)
         pdir = a.device_plugins_dir or os.path.join(a.root_dir, "device-plugin", "plugins")
         dm = ManagerImpl(pdir) if DefaultFeatureGate("DevicePlugins") else ManagerStub()
         if a.container_runtime == "remote":

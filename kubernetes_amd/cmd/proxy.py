@@ -11,7 +11,8 @@ from ._common import run_until_signal, setup_logging
 
 def main(argv=None):
     ap = argparse.ArgumentParser("kube-proxy")
-    ap.add_argument("--master", required=True)
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--hostname-override", default=os.uname().nodename)
     ap.add_argument("--proxy-mode", default="iptables", choices=["iptables", "ipvs", "userspace"])
     ap.add_argument("--cluster-cidr", default="")
@@ -38,7 +39,12 @@ def main(argv=None):
             elif a.proxy_mode == "ipvs":
                 from ..proxy.ipvs import ExecIPVS
                 ipvs = ExecIPVS()
-        ps = ProxyServer(Client(a.master, token=a.token), a.hostname_override, a.proxy_mode, a.cluster_cidr,
+        if a.kubeconfig:
+            from ..client.clientcmd import client_from
+            client = client_from(a.kubeconfig)
+        else:
+            client = Client(a.master or "http://127.0.0.1:8080", token=a.token)
+        ps = ProxyServer(client, a.hostname_override, a.proxy_mode, a.cluster_cidr,
                          a.masquerade_all, a.iptables_sync_period, a.iptables_min_sync_period,
                          healthz_port=a.healthz_port, metrics_port=a.metrics_port, iptables=iptables, ipvs=ipvs,
                          ipvs_scheduler=a.ipvs_scheduler, bind=a.bind_address)

@@ -26,7 +26,8 @@ from ..utils.tasks import spawn
 
 def _parser():
     ap = argparse.ArgumentParser("kube-scheduler")
-    ap.add_argument("--master", required=True)
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--scheduler-name", default="default-scheduler")
     ap.add_argument("--policy-config-file", default=None, help="JSON Policy {predicates:[{name}], priorities:[{name,weight}]}")
     ap.add_argument("--percentage-of-nodes-to-score", type=int, default=100)
@@ -90,7 +91,11 @@ def main(argv=None):
         extenders = [HTTPExtender.from_config(e) for e in pol.get("extenders") or []]
 
     async def start():
-        client = Client(a.master, qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
+        if a.kubeconfig:
+            from ..client.clientcmd import client_from
+            client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
+        else:
+            client = Client(a.master or "http://127.0.0.1:8080", qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
                       emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,
                       shard_count=a.shard_count, preemption=not a.disable_preemption)

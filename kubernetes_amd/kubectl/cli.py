@@ -45,21 +45,15 @@ def save_kubeconfig(cfg, path):
 
 
 def resolve_server(args):
+    """-> (server, token, namespace, ssl context) from flags or the kubeconfig (client-go clientcmd)."""
     if args.server:
-        return args.server, args.token, args.namespace
-    cfg, _ = load_kubeconfig(args.kubeconfig)
-    ctxname = args.context or cfg.get("current-context")
-    ctx = next((c["context"] for c in cfg.get("contexts") or () if c["name"] == ctxname), None)
-    server = os.environ.get("KUBERNETES_MASTER", "http://127.0.0.1:8080")
-    token = args.token
-    ns = args.namespace
-    if ctx:
-        cl = next((c["cluster"] for c in cfg.get("clusters") or () if c["name"] == ctx.get("cluster")), {})
-        us = next((u["user"] for u in cfg.get("users") or () if u["name"] == ctx.get("user")), {})
-        server = cl.get("server", server)
-        token = token or us.get("token")
-        ns = ns or ctx.get("namespace")
-    return server, token, ns
+        return args.server, args.token, args.namespace, None
+    from ..client import clientcmd
+    cfg, path = load_kubeconfig(args.kubeconfig)
+    r = clientcmd.resolve(cfg, args.context, os.path.dirname(os.path.abspath(path)))
+    if r is None:
+        return os.environ.get("KUBERNETES_MASTER", "http://127.0.0.1:8080"), args.token, args.namespace, None
+    return r.server, args.token or r.token, args.namespace or r.namespace, r.ssl_context
 
 
 # ---------------------------------------------------------------------------
@@ -124,10 +118,10 @@ class Kubectl:
     def __init__(self, args, out=sys.stdout):
         self.a = args
         self.out = out
-        server, token, ns = resolve_server(args)
+        server, token, ns, ctx = resolve_server(args)
         self.server = server
         self.ns = ns or "default"
-        self.client = Client(server, token=token)
+        self.client = Client(server, token=token, ssl_context=ctx)
 
     def p(self, *s):
         print(*s, file=self.out)
