@@ -31,6 +31,11 @@ BOUND_BY_CONTROLLER = "pv.kubernetes.io/bound-by-controller"
 PROVISIONED_BY = "pv.kubernetes.io/provisioned-by"
 HOSTPATH_PROVISIONER = "kubernetes.io/host-path"
 PVC_PROTECTION = "kubernetes.io/pvc-protection"
+SELECTED_NODE = "volume.kubernetes.io/selected-node"
+
+
+def md_ann(o):
+    return o["metadata"].get("annotations") or {}
 
 
 def _cap(obj, path):
@@ -131,7 +136,13 @@ class PersistentVolumeController(Controller):
                 if ref.get("namespace") == ns and ref.get("name") == name and ref.get("uid") in (None, "", pvc["metadata"]["uid"]):
                     pv = cand
                     break
-            if pv is None:
+            if pv is None and self._delayed(pvc):
+                # WaitForFirstConsumer: the scheduler picks the PV (claimRef) or the node
+                # (selected-node annotation) once a consuming pod is placed
+                if not (md_ann(pvc).get(SELECTED_NODE)):
+                    await self._claim_status(pvc, "Pending")
+                    return
+            elif pv is None:
                 pv = best_match(self.pv_inf.list(), pvc)
         if pv is None:
             pv = await self._provision(pvc)
@@ -139,6 +150,10 @@ class PersistentVolumeController(Controller):
                 await self._claim_status(pvc, "Pending")
                 return
         await self._bind(pv, pvc)
+
+    def _delayed(self, pvc):
+        sc = self.sc_inf.get(claim_class(pvc)) if claim_class(pvc) else None
+        return bool(sc) and sc.get("volumeBindingMode") == "WaitForFirstConsumer"
 
     async def _claim_status(self, pvc, phase):
         if (pvc.get("status") or {}).get("phase") != phase:
@@ -161,6 +176,9 @@ class PersistentVolumeController(Controller):
                        "accessModes": sp.get("accessModes") or ["ReadWriteOnce"],
                        "persistentVolumeReclaimPolicy": sc.get("reclaimPolicy") or "Delete",
                        "storageClassName": cls, "hostPath": {"path": path},
+                       **({"nodeAffinity": {"required": {"nodeSelectorTerms": [{"matchExpressions": [
+                           {"key": "kubernetes.io/hostname", "operator": "In", "values": [md_ann(pvc)[SELECTED_NODE]]}]}]}}}
+                          if md_ann(pvc).get(SELECTED_NODE) else {}),
                        "claimRef": {"kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": md["namespace"],
                                     "name": md["name"], "uid": md["uid"]}}}
         try:

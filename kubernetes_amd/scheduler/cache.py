@@ -21,6 +21,7 @@ import time
 from ..api import core
 from ..api.meta import ns_name
 from ..api.quantity import Quantity, parse_quantity
+from .volumes import VolumeLister, VolumeInfo
 
 DEFAULT_MILLI_CPU = 100                 # priorities/util/non_zero.go
 DEFAULT_MEMORY = 200 * 1024 * 1024
@@ -32,7 +33,8 @@ def _q(v) -> Quantity:
 
 class PodInfo:
     """Parsed, cached resource view of a pod (computed once per pod version)."""
-    __slots__ = ("milli_cpu", "memory", "ephemeral", "scalars", "nz_cpu", "nz_mem", "ports", "er", "assigned")
+    __slots__ = ("milli_cpu", "memory", "ephemeral", "scalars", "nz_cpu", "nz_mem", "ports", "er", "assigned", "volumes",
+                 "limits")
 
     def __init__(self, pod):
         req = core.pod_requests(pod)
@@ -60,6 +62,15 @@ class PodInfo:
             er.append((per.get("name"), rn, n, (per.get("affinity") or {}).get("required") or []))
         self.er = er
         self.assigned = core.pod_assigned_devices(pod)
+        self.volumes = VolumeInfo(pod)
+        lim_cpu = lim_mem = 0
+        for c in spec.get("containers") or ():
+            lim = (c.get("resources") or {}).get("limits") or {}
+            if "cpu" in lim:
+                lim_cpu += _q(lim["cpu"]).milli_value()
+            if "memory" in lim:
+                lim_mem += _q(lim["memory"]).int_value()
+        self.limits = (lim_cpu, lim_mem)
 
 
 def _hive(dev):
@@ -161,7 +172,7 @@ class ERManager:
 class NodeInfo:
     __slots__ = ("node", "name", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
                  "req_cpu", "req_mem", "req_eph", "req_scalars", "nz_cpu", "nz_mem", "pods", "ports", "er", "generation",
-                 "ready", "unschedulable", "mem_pressure", "disk_pressure", "gpu_total")
+                 "ready", "unschedulable", "mem_pressure", "disk_pressure", "gpu_total", "images")
 
     def __init__(self, name=""):
         self.node = None
@@ -182,6 +193,7 @@ class NodeInfo:
         self.mem_pressure = False
         self.disk_pressure = False
         self.gpu_total = 0
+        self.images = {}
 
     def set_node(self, node):
         self.node = node
@@ -210,6 +222,11 @@ class NodeInfo:
                 self.disk_pressure = s == "True"
         self.er.set_node(node)
         self.gpu_total = len(self.er.allocatable.get(core.AMD_GPU, {}))
+        imgs = {}
+        for im in (node.get("status") or {}).get("images") or ():
+            for n in im.get("names") or ():
+                imgs[n] = im.get("sizeBytes", 0)
+        self.images = imgs
         self.generation += 1
 
     def clone(self):
@@ -217,7 +234,7 @@ class NodeInfo:
         c = NodeInfo(self.name)
         for s in ("node", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
                   "req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "generation", "ready", "unschedulable",
-                  "mem_pressure", "disk_pressure", "gpu_total"):
+                  "mem_pressure", "disk_pressure", "gpu_total", "images"):
             setattr(c, s, getattr(self, s))
         c.req_scalars = dict(self.req_scalars)
         c.pods = dict(self.pods)
@@ -267,6 +284,7 @@ class SchedulerCache:
         self.assumed: dict[str, float] = {}      # key -> deadline (0 until binding finished)
         self.ttl = assumed_ttl
         self.anti_pods: dict[str, dict] = {}     # pods with required anti-affinity (symmetry check)
+        self.volumes = VolumeLister()
 
     def _track(self, key, pod):
         aff = ((pod.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}

@@ -63,6 +63,30 @@ class CycleContext:
         self.topo_scores = {}
         self.anti_affinity_terms = cache_anti_affinity(cache) if with_affinity else []
         self.any_anti_affinity = bool(self.anti_affinity_terms)
+        self.volumes = cache.volumes
+        self.pod = pod
+        self.affinity_prefs = _preferred_pod_affinity(pod)
+        self._aff_counts = None
+
+    def pod_affinity_counts(self):
+        """[(signed weight, topology key, {topology value: matching pods})] for the pod's
+        preferred (anti-)affinity terms, computed once per cycle."""
+        if self._aff_counts is None:
+            out = []
+            ns = self.pod["metadata"].get("namespace", "default")
+            for w, term in self.affinity_prefs:
+                key = term.get("topologyKey", "")
+                counts = {}
+                for ni in self.cache.nodes.values():
+                    v = ni.labels.get(key)
+                    if v is None:
+                        continue
+                    for p, _ in ni.pods.values():
+                        if P._pod_matches_term(p["metadata"].get("labels") or {}, p["metadata"].get("namespace"), term, ns):
+                            counts[v] = counts.get(v, 0) + 1
+                out.append((w, key, counts))
+            self._aff_counts = out
+        return self._aff_counts
 
     def pods_by_topology(self, key, val):
         for ni in self.cache.nodes.values():
@@ -80,6 +104,15 @@ class CycleContext:
     def node_of(self, pod):
         st = self.cache.pod_states.get(f"{pod['metadata'].get('namespace')}/{pod['metadata']['name']}")
         return self.cache.nodes.get(st[1]) if st else None
+
+
+def _preferred_pod_affinity(pod):
+    aff = (pod.get("spec") or {}).get("affinity") or {}
+    out = []
+    for kind, sign in (("podAffinity", 1.0), ("podAntiAffinity", -1.0)):
+        for wt in (aff.get(kind) or {}).get("preferredDuringSchedulingIgnoredDuringExecution") or ():
+            out.append((sign * float(wt.get("weight", 0)), wt.get("podAffinityTerm") or {}))
+    return out
 
 
 def cache_anti_affinity(cache):
@@ -127,6 +160,7 @@ class GenericScheduler:
         self._next_start = 0
         self._last_node_index = 0
         self._check_affinity = "MatchInterPodAffinity" in names
+        self.predicates_novol = [(n, f) for n, f in self.predicates if n not in P.VOLUME_PREDICATES]
         self.use_ecache = equivalence_cache
         self.ecache: OrderedDict[str, dict] = OrderedDict()
         self.ecache_classes = ecache_classes
@@ -148,6 +182,8 @@ class GenericScheduler:
                 continue
             if name == "NodeAffinityPriority" and not ctx.node_affinity_prefs:
                 continue
+            if name == "InterPodAffinityPriority" and not ctx.affinity_prefs:
+                continue
             out.append((name, w, fn, reverse, norm))
         return out
 
@@ -167,7 +203,12 @@ class GenericScheduler:
             need[r.rname] = need.get(r.rname, 0) + r.count
         prios = self._active_priorities(pi, ctx)
         ec = None
-        if self.use_ecache and not affinity_sensitive and not self.extenders and (fast or not reqs):
+        if pi.volumes:
+            preds_for_pod = self.predicates
+        else:
+            preds_for_pod = self.predicates_novol
+        if self.use_ecache and not affinity_sensitive and not self.extenders and (fast or not reqs) \
+                and not pi.volumes and not ctx.affinity_prefs:
             key = equivalence_key(pod)
             ec = self.ecache.get(key)
             if ec is None:
@@ -180,7 +221,7 @@ class GenericScheduler:
         want = self.num_feasible_to_find(len(nodes))
         n = len(nodes)
         start = self._next_start % n
-        preds = self.predicates
+        preds = preds_for_pod
         checked = 0
         for off in range(n):
             ni = nodes[(start + off) % n]
@@ -269,7 +310,9 @@ class GenericScheduler:
         total = [0.0] * len(nodes)
         for j, (_, w, _, reverse, norm) in enumerate(prios):
             col = [r[j] for r in raws]
-            if norm:
+            if norm == "minmax":
+                col = PR.normalize_minmax(col)
+            elif norm:
                 col = PR.normalize(col, reverse)
             for i, s in enumerate(col):
                 total[i] += w * s

@@ -1,7 +1,8 @@
 """Fit predicates. Parity: `plugin/pkg/scheduler/algorithm/predicates/predicates.go:202-1465`
 (PodFitsResources :583-690, GeneralPredicates :965, host ports, node selector/affinity, taints,
 memory/disk pressure, node condition, inter-pod affinity) and the default provider set
-(`plugin/pkg/scheduler/algorithmprovider/defaults/defaults.go:67-255`).
+(`plugin/pkg/scheduler/algorithmprovider/defaults/defaults.go:67-255`); the volume predicates live
+in `volumes.py`.
 
 Every predicate has signature `(pod, PodInfo, NodeInfo, ctx) -> reason or None`.
 """
@@ -170,6 +171,8 @@ def match_inter_pod_affinity(pod, pi, ni, ctx):
     return None
 
 
+from . import volumes as V  # noqa: E402
+
 PREDICATES = {
     "CheckNodeCondition": check_node_condition,
     "HostName": pod_fits_host,
@@ -180,9 +183,20 @@ PREDICATES = {
     "CheckNodeMemoryPressure": check_node_memory_pressure,
     "CheckNodeDiskPressure": check_node_disk_pressure,
     "MatchInterPodAffinity": match_inter_pod_affinity,
+    "NoDiskConflict": V.no_disk_conflict,
+    "MaxEBSVolumeCount": V.max_volume_count("ebs"),
+    "MaxGCEPDVolumeCount": V.max_volume_count("gce-pd"),
+    "MaxAzureDiskVolumeCount": V.max_volume_count("azure-disk"),
+    "NoVolumeZoneConflict": V.no_volume_zone_conflict,
+    "CheckVolumeBinding": V.check_volume_binding,
 }
+
+# predicates that only ever reject pods carrying volumes (skipped for volume-less pods)
+VOLUME_PREDICATES = {"NoDiskConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
+                     "NoVolumeZoneConflict", "CheckVolumeBinding"}
 
 # evaluation order: cheap & selective first (predicates ordering in later reference versions)
 DEFAULT_PREDICATES = ["CheckNodeCondition", "HostName", "PodFitsResources", "MatchNodeSelector",
                       "PodFitsHostPorts", "PodToleratesNodeTaints", "CheckNodeMemoryPressure",
-                      "CheckNodeDiskPressure", "MatchInterPodAffinity"]
+                      "CheckNodeDiskPressure", "NoVolumeZoneConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount",
+                      "MaxAzureDiskVolumeCount", "NoDiskConflict", "CheckVolumeBinding", "MatchInterPodAffinity"]

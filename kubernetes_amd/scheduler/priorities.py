@@ -1,6 +1,6 @@
 """Node scoring. Parity: `plugin/pkg/scheduler/algorithm/priorities/*` (LeastRequested,
 MostRequested, BalancedResourceAllocation, SelectorSpread, NodeAffinity, TaintToleration,
-NodePreferAvoidPods) with the default weights of `algorithmprovider/defaults/defaults.go`.
+NodePreferAvoidPods, InterPodAffinity, ImageLocality, ResourceLimits) with the default weights of `algorithmprovider/defaults/defaults.go`.
 
 MI355X additions:
   * XGMITopology   — the allocator's hive/NUMA fit score (scheduler/topology.py), weight 2;
@@ -96,7 +96,45 @@ def gpu_bin_packing(pod, pi, ni, ctx):
     return MAX * (1.0 - free_after / total)
 
 
-# name -> (fn, reverse normalization?, normalize?)
+MIN_IMG, MAX_IMG = 23 * 1024 * 1024, 1000 * 1024 * 1024
+
+
+def image_locality(pod, pi, ni, ctx):
+    """`image_locality.go`: total size of the pod's images already on the node, mapped to
+    1..10 between 23 MB and 1000 MB (0 below)."""
+    if not ni.images:
+        return 0.0
+    total = 0
+    for c in (pod.get("spec") or {}).get("containers") or ():
+        total += ni.images.get(c.get("image", ""), 0)
+    if total < MIN_IMG:
+        return 0.0
+    if total >= MAX_IMG:
+        return MAX
+    return float(int(MAX * (total - MIN_IMG) / (MAX_IMG - MIN_IMG)) + 1)
+
+
+def resource_limits(pod, pi, ni, ctx):
+    """`resource_limits.go`: 1 when the node's allocatable can satisfy the pod's cpu or memory limit."""
+    cpu, mem = pi.limits
+    if (cpu and ni.alloc_cpu >= cpu) or (mem and ni.alloc_mem >= mem):
+        return 1.0
+    return 0.0
+
+
+def inter_pod_affinity(pod, pi, ni, ctx):
+    """`interpod_affinity.go` CalculateInterPodAffinityPriority for the incoming pod's preferred
+    terms: +weight per matching pod in the node's topology domain (affinity), −weight (anti);
+    min-max normalized to 0..10."""
+    s = 0.0
+    for weight, key, counts in ctx.pod_affinity_counts():
+        v = ni.labels.get(key)
+        if v is not None:
+            s += weight * counts.get(v, 0)
+    return s
+
+
+# name -> (fn, reverse normalization?, normalize? True | False | "minmax")
 PRIORITIES = {
     "LeastRequestedPriority": (least_requested, False, False),
     "MostRequestedPriority": (most_requested, False, False),
@@ -107,11 +145,15 @@ PRIORITIES = {
     "NodePreferAvoidPodsPriority": (node_prefer_avoid_pods, False, False),
     "XGMITopologyPriority": (xgmi_topology, False, False),
     "GPUBinPackingPriority": (gpu_bin_packing, False, False),
+    "ImageLocalityPriority": (image_locality, False, False),
+    "ResourceLimitsPriority": (resource_limits, False, False),
+    "InterPodAffinityPriority": (inter_pod_affinity, False, "minmax"),
 }
 
 DEFAULT_PRIORITIES = {
     "LeastRequestedPriority": 1, "BalancedResourceAllocation": 1, "SelectorSpreadPriority": 1,
     "NodeAffinityPriority": 1, "TaintTolerationPriority": 1, "NodePreferAvoidPodsPriority": 10000,
+    "InterPodAffinityPriority": 1,
     "XGMITopologyPriority": 2, "GPUBinPackingPriority": 1,
 }
 
@@ -126,6 +168,13 @@ def compile_node_affinity_prefs(pod):
             continue
         out.append((float(t.get("weight", 0)), sel))
     return out
+
+
+def normalize_minmax(scores):
+    lo, hi = min(scores), max(scores)
+    if hi == lo:
+        return [0.0 for _ in scores]
+    return [MAX * (v - lo) / (hi - lo) for v in scores]
 
 
 def normalize(scores, reverse):

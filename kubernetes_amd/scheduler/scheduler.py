@@ -34,9 +34,10 @@ from ..client.rest import APIStatusError, is_not_found
 from ..utils.httpserver import HTTPServer, Response
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from ..utils.trace import Trace
-from .cache import SchedulerCache
+from .cache import PodInfo, SchedulerCache
 from .generic import FitError, GenericScheduler
 from .queue import SchedulingQueue
+from .volumes import SELECTED_NODE_ANN, plan_bindings
 from ..utils.tasks import spawn
 
 log = logging.getLogger("scheduler")
@@ -76,6 +77,9 @@ class Scheduler:
         self.http = None
         self.pod_informer = Informer(client, "pods", field_selector="status.phase!=Succeeded,status.phase!=Failed")
         self.node_informer = Informer(client, "nodes")
+        self.pvc_informer = Informer(client, "persistentvolumeclaims")
+        self.pv_informer = Informer(client, "persistentvolumes")
+        self.sc_informer = Informer(client, "storageclasses")
 
     # -- informer handlers -------------------------------------------------
     def _responsible(self, pod):
@@ -125,13 +129,44 @@ class Scheduler:
     def _on_node_delete(self, node):
         self.cache.remove_node(node)
 
+    def _volume_handlers(self):
+        vl = self.cache.volumes
+
+        def key(o):
+            md = o["metadata"]
+            return f"{md['namespace']}/{md['name']}" if md.get("namespace") else md["name"]
+
+        def put(d, moved=True):
+            def h(*objs):
+                o = objs[-1]
+                d[key(o)] = o
+                if d is vl.pvs and ((o.get("spec") or {}).get("claimRef")):
+                    vl.assumed_pvs.pop(key(o), None)
+                if moved:
+                    self.queue.move_all_to_active()
+            return h
+
+        def drop(d):
+            def h(o):
+                d.pop(key(o), None)
+                vl.assumed_pvs.pop(key(o), None)
+            return h
+        self.pvc_informer.add_handler(put(vl.pvcs), put(vl.pvcs), drop(vl.pvcs))
+        self.pv_informer.add_handler(put(vl.pvs), put(vl.pvs), drop(vl.pvs))
+        self.sc_informer.add_handler(put(vl.classes), put(vl.classes), drop(vl.classes))
+
     # -- scheduling loop ---------------------------------------------------------
     async def run(self, metrics_port=None):
         self.recorder.start()
         self.node_informer.add_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
         self.pod_informer.add_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
+        self._volume_handlers()
+        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
+            inf.start()
         self.node_informer.start()
         await self.node_informer.wait_synced(60)
+        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
+            await inf.wait_synced(60)
         self.pod_informer.start()
         await self.pod_informer.wait_synced(60)
         if metrics_port is not None:
@@ -155,6 +190,8 @@ class Scheduler:
             self.m_pending.labels("unschedulable").set(len(self.queue.unschedulable))
 
     def schedule_one(self, pod, pi):
+        if pi is None:
+            pi = PodInfo(pod)
         tr = Trace(f"Scheduling {ns_name(pod)}")
         t0 = tr.start
         try:
@@ -188,19 +225,43 @@ class Scheduler:
         except ValueError as e:
             log.warning("assume failed: %s", e)
             return None
-        t = asyncio.ensure_future(self._bind(pod, assumed, host, erb, t0))
+        vplan = None
+        if pi is not None and pi.volumes.claims:
+            # volumebinder AssumePodVolumes: reserve the chosen PVs in the cache now
+            vplan = plan_bindings(self.cache.volumes, pod, self.cache.nodes[host].labels, host)
+            for kind, pvc, pv in vplan:
+                if kind == "bind":
+                    self.cache.volumes.assumed_pvs[pv["metadata"]["name"]] = pvc
+        t = asyncio.ensure_future(self._bind(pod, assumed, host, erb, t0, vplan))
         self._binds.add(t)
         t.add_done_callback(self._binds.discard)
         return host
 
-    async def _bind(self, pod, assumed, host, erb, t0):
+    async def _bind_volumes(self, plan, host):
+        """volumebinder BindPodVolumes: pre-bind PVs (claimRef) / mark claims for provisioning."""
+        for kind, pvc, pv in plan:
+            md = pvc["metadata"]
+            if kind == "bind":
+                ref = {"kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": md["namespace"],
+                       "name": md["name"], "uid": md.get("uid")}
+                await self.client.patch("persistentvolumes", pv["metadata"]["name"], {"spec": {"claimRef": ref}})
+            else:
+                await self.client.patch("persistentvolumeclaims", md["name"],
+                                        {"metadata": {"annotations": {SELECTED_NODE_ANN: host}}}, md["namespace"])
+
+    async def _bind(self, pod, assumed, host, erb, t0, vplan=None):
         md = pod["metadata"]
         async with self.bind_sem:
             tb = time.perf_counter()
             try:
+                if vplan:
+                    await self._bind_volumes(vplan, host)
                 await self.client.bind(md.get("namespace", "default"), md["name"], host, erb or None)
             except (APIStatusError, ConnectionError, OSError, asyncio.TimeoutError) as e:
                 self.cache.forget_pod(assumed)
+                for kind, _pvc, pv in vplan or ():
+                    if kind == "bind":
+                        self.cache.volumes.assumed_pvs.pop(pv["metadata"]["name"], None)
                 self.m_attempts.labels("error").inc()
                 if isinstance(e, APIStatusError) and e.code == 409 and "already assigned" in str(e):
                     # lost a device race to another scheduler shard: retry soon, no event spam
@@ -285,6 +346,8 @@ class Scheduler:
             t.cancel()
         self.pod_informer.stop()
         self.node_informer.stop()
+        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
+            inf.stop()
         self.recorder.stop()
         if self.http:
             await self.http.stop()
