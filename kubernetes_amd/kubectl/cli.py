@@ -23,7 +23,7 @@ import yaml
 
 from ..api import core, meta as m
 from ..client.rest import APIStatusError, Client, is_already_exists, is_not_found
-from . import printers
+from . import extra, printers
 
 DEFAULT_KUBECONFIG = os.path.expanduser("~/.kube/config")
 
@@ -114,7 +114,7 @@ def split_targets(targets):
     return out
 
 
-class Kubectl:
+class Kubectl(extra.ExtraCommands):
     def __init__(self, args, out=sys.stdout):
         self.a = args
         self.out = out
@@ -238,6 +238,11 @@ class Kubectl:
         self.p(f"{ri.kind.lower()}/{name} {verb}")
 
     async def cmd_create(self):
+        if self.a.generator:
+            await self._create_generated(self.a.generator)
+            return
+        if not self.a.filename:
+            raise SystemExit("error: must specify one of -f and a resource generator (e.g. create namespace NAME)")
         for d in read_manifests(self.a.filename):
             await self._apply_one(d, "create")
 
@@ -544,6 +549,10 @@ class Kubectl:
 
     async def cmd_auth(self):
         a = self.a
+        if a.action == "reconcile":
+            for d in read_manifests(a.filename or []):
+                await self._reconcile(d)
+            return
         ri = m.lookup(a.resource)
         st, body = await self.client.raw("GET", f"{'/api/v1' if not ri.group else f'/apis/{ri.group}/{ri.version}'}"
                                          f"{'/namespaces/' + self.ns if ri.namespaced else ''}/{ri.plural}?limit=1")
@@ -795,7 +804,11 @@ def build_parser():
     d.add_argument("-l", "--selector")
     for name in ("create", "apply", "replace"):
         c = add(name)
-        c.add_argument("-f", "--filename", action="append", required=True)
+        c.add_argument("-f", "--filename", action="append", required=name != "create")
+        if name == "create":
+            c.add_argument("--dry-run", action="store_true")
+            c.add_argument("-o", "--output", default="")
+            c.add_argument("generator", nargs=argparse.REMAINDER)
     de = add("delete")
     de.add_argument("targets", nargs="*")
     de.add_argument("-f", "--filename", action="append")
@@ -861,9 +874,10 @@ def build_parser():
     w.add_argument("--for", dest="for_", required=True)
     w.add_argument("--timeout", type=float, default=30)
     au = add("auth")
-    au.add_argument("can_i", choices=["can-i"])
-    au.add_argument("verb")
-    au.add_argument("resource")
+    au.add_argument("action", choices=["can-i", "reconcile"])
+    au.add_argument("verb", nargs="?")
+    au.add_argument("resource", nargs="?")
+    au.add_argument("-f", "--filename", action="append")
     exq = add("exec")
     exq.add_argument("pod")
     exq.add_argument("-c", "--container")
@@ -898,6 +912,7 @@ def build_parser():
     cert = add("certificate")
     cert.add_argument("action", choices=["approve", "deny"])
     cert.add_argument("names", nargs="+")
+    extra.add_parsers(add)
     cf = add("config")
     cf.add_argument("action", choices=["view", "current-context", "get-contexts", "use-context", "set-cluster",
                                        "set-context", "set-credentials"])
@@ -910,12 +925,50 @@ def build_parser():
     return ap
 
 
+GLOBAL_FLAGS = {"-s", "--server", "--token", "--kubeconfig", "--context", "-n", "--namespace"}
+
+
+def hoist_global_flags(argv):
+    """kubectl accepts its persistent flags anywhere (cobra); move them before the command."""
+    front, rest, i = [], [], 0
+    while i < len(argv):
+        t = argv[i]
+        if t == "--":
+            rest += argv[i:]
+            break
+        if t in GLOBAL_FLAGS and i + 1 < len(argv):
+            front += [t, argv[i + 1]]
+            i += 2
+            continue
+        if t.split("=", 1)[0] in GLOBAL_FLAGS and "=" in t:
+            front.append(t)
+            i += 1
+            continue
+        rest.append(t)
+        i += 1
+    return front + rest
+
+
 def main(argv=None, out=sys.stdout):
     ap = build_parser()
+    argv = hoist_global_flags(list(sys.argv[1:] if argv is None else argv))
     a = ap.parse_args(argv)
     if a.command == "config":
         cmd_config(a)
         return 0
+    if a.command == "completion":
+        print(extra.completion(a.shell, ap), file=out)
+        return 0
+    if a.command == "options":
+        print(extra.OPTIONS, file=out)
+        return 0
+    if a.command == "plugin":
+        if not a.plugin_name:
+            for n, p in sorted(extra.find_plugins().items()):
+                print(f"  {n:<20}{p.get('shortDesc', '')}", file=out)
+            return 0
+        return extra.run_plugin(a.plugin_name, a.plugin_args, {"server": a.server, "namespace": a.namespace,
+                                                              "kubeconfig": a.kubeconfig, "token": a.token})
     k = Kubectl(a, out)
     k.rc = 0
     name = "cmd_" + a.command.replace("-", "_")

@@ -127,3 +127,114 @@ def test_misc_commands(cluster):
     assert "extendedResources" in k(cluster, "explain", "pods")[1]
     rc, out = k(cluster, "get", "pods", "nope")
     assert rc == 1
+
+
+def _get(cluster, *args):
+    rc, out = k(cluster, "get", *args, "-o", "json")
+    assert rc == 0, out
+    return json.loads(out)
+
+
+def test_create_generators(cluster, tmp_path):
+    assert k(cluster, "create", "namespace", "gen")[0] == 0
+    assert k(cluster, "-n", "gen", "create", "configmap", "cfg", "--from-literal", "a=1", "--from-literal", "b=2")[0] == 0
+    assert _get(cluster, "-n", "gen", "configmap", "cfg")["data"] == {"a": "1", "b": "2"}
+    assert k(cluster, "-n", "gen", "create", "secret", "generic", "s1", "--from-literal", "pw=hunter2")[0] == 0
+    import base64
+    assert base64.b64decode(_get(cluster, "-n", "gen", "secret", "s1")["data"]["pw"]) == b"hunter2"
+    assert k(cluster, "-n", "gen", "create", "serviceaccount", "robot")[0] == 0
+    assert k(cluster, "-n", "gen", "create", "role", "reader", "--verb", "get", "--verb", "list", "--resource", "pods")[0] == 0
+    assert k(cluster, "-n", "gen", "create", "rolebinding", "rb", "--role", "reader", "--serviceaccount", "gen:robot")[0] == 0
+    rb = _get(cluster, "-n", "gen", "rolebinding", "rb")
+    assert rb["subjects"] == [{"kind": "ServiceAccount", "namespace": "gen", "name": "robot"}]
+    assert k(cluster, "-n", "gen", "create", "quota", "q", "--hard", "pods=10,amd.com/gpu=4")[0] == 0
+    assert _get(cluster, "-n", "gen", "resourcequota", "q")["spec"]["hard"]["amd.com/gpu"] == "4"
+    assert k(cluster, "-n", "gen", "create", "service", "clusterip", "web", "--tcp", "80:8080")[0] == 0
+    assert _get(cluster, "-n", "gen", "service", "web")["spec"]["ports"][0]["targetPort"] == 8080
+    assert k(cluster, "-n", "gen", "create", "deployment", "trainer", "--image", "rocm/pytorch", "--gpus", "1")[0] == 0
+    d = _get(cluster, "-n", "gen", "deployment", "trainer")
+    assert d["spec"]["template"]["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "1"
+    rc, out = k(cluster, "create", "--dry-run", "-o", "yaml", "priorityclass", "high", "--value", "1000")
+    assert rc == 0 and yaml.safe_load(out)["value"] == 1000
+
+
+def test_set_commands(cluster):
+    k(cluster, "create", "namespace", "setns")
+    assert k(cluster, "-n", "setns", "create", "deployment", "app", "--image", "busybox:1")[0] == 0
+    assert k(cluster, "-n", "setns", "set", "image", "deployment/app", "busybox=busybox:2")[0] == 0
+    assert k(cluster, "-n", "setns", "set", "resources", "deployment/app", "--limits", "cpu=2,memory=1Gi")[0] == 0
+    assert k(cluster, "-n", "setns", "set", "env", "deployment/app", "MODE=fast", "HIP_VISIBLE_DEVICES=0")[0] == 0
+    assert k(cluster, "-n", "setns", "set", "env", "deployment/app", "MODE-")[0] == 0
+    assert k(cluster, "-n", "setns", "set", "serviceaccount", "deployment/app", "default")[0] == 0
+    c = _get(cluster, "-n", "setns", "deployment", "app")["spec"]["template"]["spec"]
+    ctr = c["containers"][0]
+    assert ctr["image"] == "busybox:2" and ctr["resources"]["limits"] == {"cpu": "2", "memory": "1Gi"}
+    assert ctr["env"] == [{"name": "HIP_VISIBLE_DEVICES", "value": "0"}] and c["serviceAccountName"] == "default"
+
+
+def test_rolling_update_rc(cluster):
+    k(cluster, "create", "namespace", "ru")
+    rc_obj = {"apiVersion": "v1", "kind": "ReplicationController", "metadata": {"name": "web", "namespace": "ru"},
+              "spec": {"replicas": 2, "selector": {"app": "web"},
+                       "template": {"metadata": {"labels": {"app": "web"}},
+                                    "spec": {"containers": [{"name": "web", "image": "nginx:1"}]}}}}
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
+        yaml.safe_dump(rc_obj, f)
+    assert k(cluster, "create", "-f", f.name)[0] == 0
+    wait(lambda: (_get(cluster, "-n", "ru", "rc", "web").get("status") or {}).get("readyReplicas") == 2)
+    rc, out = k(cluster, "-n", "ru", "rolling-update", "web", "--image", "nginx:2", "--timeout", "60")
+    assert rc == 0, out
+    assert 'replicationcontroller "web" rolling updated' in out
+    cur = _get(cluster, "-n", "ru", "rc", "web")
+    assert cur["spec"]["template"]["spec"]["containers"][0]["image"] == "nginx:2" and cur["spec"]["replicas"] == 2
+
+    def settled():
+        pods = [p for p in _get(cluster, "-n", "ru", "pods")["items"] if not p["metadata"].get("deletionTimestamp")]
+        return len(pods) == 2 and all(p["spec"]["containers"][0]["image"] == "nginx:2" for p in pods)
+    wait(settled, 30)
+
+
+def test_convert_diff_completion_plugin_options_reconcile(cluster, tmp_path, monkeypatch):
+    dep = {"apiVersion": "extensions/v1beta1", "kind": "Deployment", "metadata": {"name": "old", "namespace": "default"},
+           "spec": {"template": {"metadata": {"labels": {"a": "b"}}, "spec": {"containers": [{"name": "c", "image": "x"}]}}}}
+    p = tmp_path / "d.yaml"
+    p.write_text(yaml.safe_dump(dep))
+    rc, out = k(cluster, "convert", "-f", str(p))
+    assert rc == 0 and yaml.safe_load(out)["apiVersion"] == "apps/v1"
+
+    cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "difftest", "namespace": "default"}, "data": {"k": "1"}}
+    p2 = tmp_path / "cm.yaml"
+    p2.write_text(yaml.safe_dump(cm))
+    assert k(cluster, "apply", "-f", str(p2))[0] == 0
+    rc, out = k(cluster, "alpha", "diff", "-f", str(p2))
+    assert rc == 0 and out.strip() == ""
+    cm["data"]["k"] = "2"
+    p2.write_text(yaml.safe_dump(cm))
+    rc, out = k(cluster, "alpha", "diff", "-f", str(p2))
+    assert rc == 1 and "-  k: '1'" in out and "+  k: '2'" in out
+
+    rc, out = k(cluster, "completion", "bash")
+    assert rc == 0 and "rolling-update" in out and "complete -F _kubectl kubectl" in out
+    rc, out = k(cluster, "options")
+    assert "--kubeconfig" in out
+
+    plug = tmp_path / "plugins" / "hello"
+    plug.mkdir(parents=True)
+    (plug / "plugin.yaml").write_text(yaml.safe_dump({"name": "hello", "shortDesc": "says hello",
+                                                      "command": "echo hello-$KUBECTL_PLUGINS_CURRENT_NAMESPACE > out.txt"}))
+    monkeypatch.setenv("KUBECTL_PLUGINS_PATH", str(tmp_path / "plugins"))
+    rc, out = k(cluster, "plugin")
+    assert "hello" in out and "says hello" in out
+    assert k(cluster, "-n", "kube-system", "plugin", "hello")[0] == 0
+    assert (plug / "out.txt").read_text().strip() == "hello-kube-system"
+
+    role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole", "metadata": {"name": "recon"},
+            "rules": [{"apiGroups": [""], "resources": ["pods"], "verbs": ["get"]}]}
+    p3 = tmp_path / "r.yaml"
+    p3.write_text(yaml.safe_dump(role))
+    assert k(cluster, "auth", "reconcile", "-f", str(p3))[0] == 0
+    role["rules"].append({"apiGroups": [""], "resources": ["nodes"], "verbs": ["list"]})
+    p3.write_text(yaml.safe_dump(role))
+    assert k(cluster, "auth", "reconcile", "-f", str(p3))[0] == 0
+    assert len(_get(cluster, "clusterrole", "recon")["rules"]) == 2
