@@ -72,14 +72,16 @@ class Policy:
 
 
 class AuditLogger:
-    def __init__(self, path, policy: Policy | None = None, max_body=64 << 10):
+    def __init__(self, path, policy: Policy | None = None, max_body=64 << 10, webhook=None):
         self.path = path
         self.policy = policy or Policy()
         self.max_body = max_body
         self._buf = []
         self._lock = threading.Lock()
         self._scheduled = False
+        self.stdout = path == "-"
         self.f = open(path, "a", buffering=1 << 16) if path not in ("-", None) else None
+        self.webhook = webhook        # WebhookBackend or None
 
     def log(self, req, method, resource, sub, code, response_body=None):
         parsed_ns = name = None
@@ -147,17 +149,92 @@ class AuditLogger:
         if not buf:
             return
         data = "\n".join(buf) + "\n"
-        if self.f is None:
-            os.write(1, data.encode())
-        else:
+        if self.f is not None:
             self.f.write(data)
             self.f.flush()
+        elif self.stdout:
+            os.write(1, data.encode())
+        if self.webhook is not None:
+            self.webhook.enqueue(buf)
 
     def close(self):
         self.flush()
         if self.f is not None:
             self.f.close()
             self.f = None
+        if self.webhook is not None:
+            self.webhook.close()
+
+
+class WebhookBackend:
+    """Batching audit webhook (`staging/src/k8s.io/apiserver/plugin/pkg/audit/webhook/webhook.go`,
+    `--audit-webhook-config-file` kubeconfig naming the remote server): events are buffered
+    (10 000) and POSTed as an `audit.k8s.io/v1beta1` EventList in batches of up to 400, at
+    least every `max_wait` seconds, from a background thread so request handling never blocks;
+    a failed batch is retried with backoff, then dropped."""
+
+    def __init__(self, kubeconfig, max_batch=400, max_wait=1.0, buffer=10000, retries=3):
+        from ..client import clientcmd
+        cfg, p = clientcmd.load(kubeconfig)
+        r = clientcmd.resolve(cfg, None, os.path.dirname(os.path.abspath(p)))
+        if r is None:
+            raise ValueError(f"audit webhook kubeconfig {kubeconfig}: no usable context")
+        self.url, self.token, self.ssl = r.server, r.token, r.ssl_context
+        self.max_batch, self.max_wait, self.buffer, self.retries = max_batch, max_wait, buffer, retries
+        self._q = []
+        self._cv = threading.Condition()
+        self._closed = False
+        self.sent = self.dropped = 0
+        self._t = threading.Thread(target=self._run, name="audit-webhook", daemon=True)
+        self._t.start()
+
+    def enqueue(self, lines):
+        with self._cv:
+            room = self.buffer - len(self._q)
+            if room < len(lines):
+                self.dropped += len(lines) - max(room, 0)
+                lines = lines[:max(room, 0)]
+            self._q.extend(lines)
+            if len(self._q) >= self.max_batch:
+                self._cv.notify()
+
+    def _post(self, batch):
+        import urllib.request
+        body = ('{"kind":"EventList","apiVersion":"audit.k8s.io/v1beta1","metadata":{},"items":[' +
+                ",".join(batch) + "]}").encode()
+        hdr = {"Content-Type": "application/json"}
+        if self.token:
+            hdr["Authorization"] = f"Bearer {self.token}"
+        delay = 0.1
+        for _ in range(self.retries):
+            try:
+                req = urllib.request.Request(self.url, data=body, headers=hdr, method="POST")
+                with urllib.request.urlopen(req, timeout=10, context=self.ssl) as r:
+                    r.read()
+                self.sent += len(batch)
+                return
+            except OSError:
+                time.sleep(delay)
+                delay *= 2
+        self.dropped += len(batch)
+
+    def _run(self):
+        while True:
+            with self._cv:
+                if not self._q and not self._closed:
+                    self._cv.wait(self.max_wait)
+                batch, self._q = self._q[:self.max_batch], self._q[self.max_batch:]
+                done = self._closed and not self._q
+            if batch:
+                self._post(batch)
+            if done:
+                return
+
+    def close(self, timeout=10.0):
+        with self._cv:
+            self._closed = True
+            self._cv.notify()
+        self._t.join(timeout)
 
 
 def now():

@@ -240,3 +240,176 @@ class UnionAuthenticator:
                     return u
             return None
         return ANONYMOUS if self.anonymous else None
+
+
+# ------------------------------------------------------------------------------------ JWK <-> PEM
+def _der_len(n):
+    if n < 0x80:
+        return bytes([n])
+    b = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([0x80 | len(b)]) + b
+
+
+def _tlv(tag, body):
+    return bytes([tag]) + _der_len(len(body)) + body
+
+
+def _der_int(v):
+    b = v.to_bytes(max(1, (v.bit_length() + 7) // 8), "big")
+    if b[0] & 0x80:
+        b = b"\x00" + b
+    return _tlv(0x02, b)
+
+
+_RSA_ALG = _tlv(0x30, bytes.fromhex("06092a864886f70d010101") + b"\x05\x00")
+_EC_ALG = _tlv(0x30, bytes.fromhex("06072a8648ce3d0201") + bytes.fromhex("06082a8648ce3d030107"))
+
+
+def _pem(der):
+    b = base64.b64encode(der).decode()
+    return "-----BEGIN PUBLIC KEY-----\n" + "\n".join(b[i:i + 64] for i in range(0, len(b), 64)) + "\n-----END PUBLIC KEY-----\n"
+
+
+def jwk_to_pem(jwk: dict) -> str:
+    """RSA (`n`, `e`) or P-256 EC (`x`, `y`) JWK → SubjectPublicKeyInfo PEM."""
+    if jwk.get("kty") == "RSA":
+        n = int.from_bytes(b64url_decode(jwk["n"]), "big")
+        e = int.from_bytes(b64url_decode(jwk["e"]), "big")
+        key = _tlv(0x30, _der_int(n) + _der_int(e))
+        return _pem(_tlv(0x30, _RSA_ALG + _tlv(0x03, b"\x00" + key)))
+    if jwk.get("kty") == "EC" and jwk.get("crv", "P-256") == "P-256":
+        pt = b"\x04" + b64url_decode(jwk["x"]).rjust(32, b"\x00") + b64url_decode(jwk["y"]).rjust(32, b"\x00")
+        return _pem(_tlv(0x30, _EC_ALG + _tlv(0x03, b"\x00" + pt)))
+    raise ValueError(f"unsupported JWK kty={jwk.get('kty')} crv={jwk.get('crv')}")
+
+
+def _read_tlv(b, i):
+    tag = b[i]
+    ln = b[i + 1]
+    i += 2
+    if ln & 0x80:
+        k = ln & 0x7F
+        ln = int.from_bytes(b[i:i + k], "big")
+        i += k
+    return tag, b[i:i + ln], i + ln
+
+
+def pem_to_jwk(pem: str, kid: str = "") -> dict:
+    """Inverse of `jwk_to_pem` (used to publish keys in a JWKS document)."""
+    pub = crypto.public_key(pem)
+    der = base64.b64decode("".join(l for l in pub.splitlines() if not l.startswith("-----")))
+    _, spki, _ = _read_tlv(der, 0)
+    _, alg, j = _read_tlv(spki, 0)
+    _, bits, _ = _read_tlv(spki, j)
+    key = bits[1:]
+    out = {"kid": kid, "use": "sig"}
+    if alg.startswith(bytes.fromhex("06092a864886f70d010101")):
+        _, seq, _ = _read_tlv(key, 0)
+        _, n, k = _read_tlv(seq, 0)
+        _, e, _ = _read_tlv(seq, k)
+        out.update(kty="RSA", alg="RS256", n=b64url(n.lstrip(b"\x00")), e=b64url(e))
+    else:
+        out.update(kty="EC", alg="ES256", crv="P-256", x=b64url(key[1:33]), y=b64url(key[33:65]))
+    return out
+
+
+class OIDCAuthenticator:
+    """OpenID Connect ID-token authenticator.
+
+    Parity: `staging/src/k8s.io/apiserver/plugin/pkg/authenticator/token/oidc/oidc.go` (1.9):
+    keys from the issuer's discovery document (`/.well-known/openid-configuration` →
+    `jwks_uri`, refreshed on an unknown `kid`), `iss` must equal the issuer URL, `aud` must
+    contain the client id, `exp` in the future, `email_verified` required when the username
+    claim is `email`; usernames from any other claim are prefixed with `<issuer>#` unless a
+    prefix is configured (`--oidc-username-prefix`, `-` disables); groups from
+    `--oidc-groups-claim` (string or list) with `--oidc-groups-prefix`; `--oidc-required-claim`.
+    `keys` may be given directly (air-gapped clusters without a reachable issuer).
+    """
+
+    def __init__(self, issuer_url, client_id, username_claim="sub", username_prefix=None, groups_claim=None,
+                 groups_prefix="", ca_file=None, required_claims=None, keys=None, refresh_interval=10.0):
+        self.issuer = issuer_url.rstrip("/")
+        self.client_id = client_id
+        self.username_claim = username_claim
+        if username_prefix is None:
+            username_prefix = "" if username_claim == "email" else self.issuer + "#"
+        self.username_prefix = "" if username_prefix == "-" else username_prefix
+        self.groups_claim = groups_claim
+        self.groups_prefix = groups_prefix or ""
+        self.ca_file = ca_file
+        self.required = dict(required_claims or {})
+        self.keys = dict(keys or {})       # kid -> PEM
+        self.refresh_interval = refresh_interval
+        self._last_fetch = 0.0
+        self._fetching = None
+        if not self.keys:
+            self.refresh()
+
+    def refresh(self):
+        """Fetch the issuer's keys on a background thread (the request path never blocks on
+        the network; tokens are rejected until keys are known, as in the reference)."""
+        import threading
+        if self._fetching is not None and self._fetching.is_alive():
+            return self._fetching
+        self._fetching = threading.Thread(target=self._fetch, name="oidc-keys", daemon=True)
+        self._fetching.start()
+        return self._fetching
+
+    def _fetch(self):
+        import ssl
+        import urllib.request
+        now = time.monotonic()
+        if now - self._last_fetch < self.refresh_interval:
+            return
+        self._last_fetch = now
+        ctx = ssl.create_default_context(cafile=self.ca_file) if self.issuer.startswith("https") else None
+        try:
+            with urllib.request.urlopen(self.issuer + "/.well-known/openid-configuration", timeout=5, context=ctx) as r:
+                disc = json.loads(r.read())
+            with urllib.request.urlopen(disc["jwks_uri"], timeout=5, context=ctx) as r:
+                jwks = json.loads(r.read())
+        except (OSError, ValueError, KeyError):
+            return
+        keys = {}
+        for k in jwks.get("keys") or ():
+            try:
+                keys[k.get("kid", "")] = jwk_to_pem(k)
+            except (ValueError, KeyError):
+                continue
+        if keys:
+            self.keys = keys
+
+    def authenticate_token(self, token):
+        if token.count(".") != 2:
+            return None
+        try:
+            head = json.loads(b64url_decode(token.split(".")[0]))
+        except (ValueError, json.JSONDecodeError):
+            return None
+        kid = head.get("kid", "")
+        if not self.keys or (kid and kid not in self.keys):
+            self.refresh()
+        cands = [self.keys[kid]] if kid in self.keys else list(self.keys.values())
+        claims = jwt_verify(cands, token) if cands else None
+        if claims is None:
+            return None
+        if claims.get("iss") != self.issuer:
+            return None
+        aud = claims.get("aud")
+        if self.client_id not in (aud if isinstance(aud, list) else [aud]):
+            return None
+        if claims.get("exp") is None or claims["exp"] < time.time():
+            return None
+        for k, v in self.required.items():
+            if claims.get(k) != v:
+                return None
+        name = claims.get(self.username_claim)
+        if not isinstance(name, str) or not name:
+            return None
+        if self.username_claim == "email" and claims.get("email_verified") is False:
+            return None
+        groups = []
+        if self.groups_claim:
+            g = claims.get(self.groups_claim)
+            groups = [g] if isinstance(g, str) else list(g or [])
+        return User(self.username_prefix + name, "", [self.groups_prefix + x for x in groups] + ["system:authenticated"])

@@ -100,7 +100,7 @@ class APIServer:
                  service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767),
                  tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
                  service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
-                 anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None):
+                 anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None, oidc=None):
         self.abac_policy_file = authorization_policy_file
         self.authorization_webhook_url = authorization_webhook_url
         self.authorization_modes = tuple(authorization_modes)
@@ -111,6 +111,8 @@ class APIServer:
         self.webhooks = WebhookDispatcher(self)
         self.crds = CRDManager(self)
         self.aggregator = Aggregator(self)
+        from .openapi import OpenAPICache
+        self.openapi = OpenAPICache(VERSION["gitVersion"])
         # encryption at rest (--experimental-encryption-provider-config): plural -> PrefixTransformers
         self.transformers = {}
         if encryption_config:
@@ -138,7 +140,7 @@ class APIServer:
         self.admission = adm.new_chain(names, self, admission_config)
         self.authn = None
         if token_file or tokens or client_ca_file or service_account_key_files or enable_bootstrap_token_auth \
-                or authentication_token_webhook or not anonymous_auth:
+                or authentication_token_webhook or not anonymous_auth or oidc:
             from . import authn as an
             from ..native import crypto as _crypto
             toks = [TokenAuthenticator(token_file, tokens)] if (token_file or tokens) else []
@@ -152,6 +154,8 @@ class APIServer:
                 toks.append(an.ServiceAccountAuthenticator(keys, self, service_account_lookup))
             if authentication_token_webhook:
                 toks.append(an.WebhookTokenAuthenticator(authentication_token_webhook))
+            if oidc:
+                toks.append(oidc if isinstance(oidc, an.OIDCAuthenticator) else an.OIDCAuthenticator(**oidc))
             self.authn = an.UnionAuthenticator([an.X509Authenticator()] if client_ca_file else [], toks, anonymous_auth)
         self.authz = build_authorizer(authorization_modes, self)
         self.max_inflight = max_requests_inflight
@@ -958,6 +962,14 @@ class APIServer:
                     code = 401
                     return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))
             req.user = user
+            if p in ("/openapi/v2", "/swagger.json", "/swagger-2.0.0.json"):
+                schemas = {}
+                for plural, sch in self.crds.schemas.items():
+                    ri = m.BY_PLURAL.get(plural)
+                    if ri is not None and sch:
+                        schemas[(ri.group, ri.version, ri.kind)] = sch
+                code = 200
+                return Response(200, self.openapi.get(schemas), "application/json")
             if req.body and req.headers.get("content-type", "").startswith(codec.PROTOBUF):
                 # protobuf request bodies (`application/vnd.kubernetes.protobuf`, k8s\0 envelope)
                 from ..api import protobuf as pb

@@ -59,8 +59,47 @@ def _parser():
     ap.add_argument("--authorization-webhook-url", default=None)
     ap.add_argument("--service-cluster-ip-range", default="10.0.0.0/24")
     ap.add_argument("--service-node-port-range", default="30000-32767")
+    ap.add_argument("--oidc-issuer-url", default=None)
+    ap.add_argument("--oidc-client-id", default=None)
+    ap.add_argument("--oidc-username-claim", default="sub")
+    ap.add_argument("--oidc-username-prefix", default=None)
+    ap.add_argument("--oidc-groups-claim", default=None)
+    ap.add_argument("--oidc-groups-prefix", default="")
+    ap.add_argument("--oidc-ca-file", default=None)
+    ap.add_argument("--oidc-required-claim", action="append", default=[], help="key=value")
+    ap.add_argument("--audit-webhook-config-file", default=None, help="kubeconfig naming the audit webhook")
+    ap.add_argument("--audit-webhook-batch-max-size", type=int, default=400)
+    ap.add_argument("--audit-webhook-batch-max-wait", type=float, default=1.0)
     ap.add_argument("-v", type=int, default=0)
     return ap
+
+
+# flags the multi-worker supervisor sets itself for each worker
+_SUPERVISOR_OWNED = {"workers", "port", "port_file", "etcd_wal", "etcd_servers", "reuse_port", "bind_address",
+                     "audit_log_path", "audit_policy_file", "v"}
+
+
+def passthrough_args(a, parser=None):
+    """Every explicitly set flag except the supervisor-owned ones, re-rendered for a worker."""
+    parser = parser or _parser()
+    out = []
+    for act in parser._actions:  # noqa: SLF001 - argparse has no public action list
+        if not act.option_strings or act.dest in _SUPERVISOR_OWNED or act.dest == "help":
+            continue
+        v = getattr(a, act.dest, None)
+        if v == act.default or v is None:
+            continue
+        flag = act.option_strings[-1]
+        if isinstance(act, argparse._StoreTrueAction):  # noqa: SLF001
+            out.append(flag)
+        elif isinstance(v, list):
+            for x in v:
+                out += [flag, str(x)]
+        elif isinstance(v, bool):
+            out += [flag, "true" if v else "false"]
+        else:
+            out += [flag, str(v)]
+    return out
 
 
 def _free_port(host):
@@ -79,16 +118,7 @@ def supervise(a):
     port = a.port or _free_port(a.bind_address)
     base = [sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--bind-address", a.bind_address,
             "--port", str(port), "--reuse-port", "--etcd-servers", addr,
-            "--authorization-mode", a.authorization_mode, "--storage-media-type", a.storage_media_type,
-            "--max-requests-inflight", str(a.max_requests_inflight),
-            "--max-mutating-requests-inflight", str(a.max_mutating_requests_inflight),
-            "--watch-cache-size", str(a.watch_cache_size), "-v", str(a.v)]
-    if a.admission_control:
-        base += ["--admission-control", a.admission_control]
-    if a.token_auth_file:
-        base += ["--token-auth-file", a.token_auth_file]
-    if a.encryption_config:
-        base += ["--experimental-encryption-provider-config", a.encryption_config]
+            "-v", str(a.v)] + passthrough_args(a)
     ready_dir = store.dir or os.path.dirname(store.socket_path)
     children = []
     stopping = []
@@ -152,9 +182,18 @@ def main(argv=None):
             store = MVCCStore(wal_path=a.etcd_wal)
         plugins = a.admission_control.split(",") if a.admission_control else None
         audit = None
-        if a.audit_log_path:
-            from ..apiserver.audit import AuditLogger, Policy
-            audit = AuditLogger(a.audit_log_path, Policy.load(a.audit_policy_file) if a.audit_policy_file else None)
+        if a.audit_log_path or a.audit_webhook_config_file:
+            from ..apiserver.audit import AuditLogger, Policy, WebhookBackend
+            wh = (WebhookBackend(a.audit_webhook_config_file, a.audit_webhook_batch_max_size, a.audit_webhook_batch_max_wait)
+                  if a.audit_webhook_config_file else None)
+            audit = AuditLogger(a.audit_log_path, Policy.load(a.audit_policy_file) if a.audit_policy_file else None,
+                                webhook=wh)
+        oidc = None
+        if a.oidc_issuer_url:
+            oidc = {"issuer_url": a.oidc_issuer_url, "client_id": a.oidc_client_id,
+                    "username_claim": a.oidc_username_claim, "username_prefix": a.oidc_username_prefix,
+                    "groups_claim": a.oidc_groups_claim, "groups_prefix": a.oidc_groups_prefix, "ca_file": a.oidc_ca_file,
+                    "required_claims": dict(x.split("=", 1) for x in a.oidc_required_claim)}
         s = APIServer(store=store, admission_plugins=plugins, token_file=a.token_auth_file,
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
@@ -168,7 +207,7 @@ def main(argv=None):
                       enable_bootstrap_token_auth=a.enable_bootstrap_token_auth,
                       authentication_token_webhook=a.authentication_token_webhook_url, anonymous_auth=a.anonymous_auth,
                       authorization_policy_file=a.authorization_policy_file,
-                      authorization_webhook_url=a.authorization_webhook_url)
+                      authorization_webhook_url=a.authorization_webhook_url, oidc=oidc)
         port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
         if not a.reuse_port:
