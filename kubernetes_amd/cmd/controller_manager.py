@@ -22,6 +22,11 @@ def main(argv=None):
     ap.add_argument("--pod-eviction-timeout", type=float, default=300.0)
     ap.add_argument("--terminated-pod-gc-threshold", type=int, default=12500)
     ap.add_argument("--leader-elect", action="store_true")
+    ap.add_argument("--allocate-node-cidrs", action="store_true")
+    ap.add_argument("--cluster-cidr", default="10.244.0.0/16")
+    ap.add_argument("--node-cidr-mask-size", type=int, default=24)
+    ap.add_argument("--loadbalancer-ip-range", default="",
+                    help="on-prem LoadBalancer pool ('10.0.5.10-10.0.5.50' or a CIDR); enables the service controller")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -39,8 +44,15 @@ def main(argv=None):
                 "podgc": {"terminated_pod_gc_threshold": a.terminated_pod_gc_threshold},
                 "serviceaccount-token": {"private_key_file": a.service_account_private_key_file, "root_ca_file": a.root_ca_file},
                 "csrsigning": {"cert_file": a.cluster_signing_cert_file, "key_file": a.cluster_signing_key_file},
-                "horizontalpodautoscaling": {"sync_period": a.horizontal_pod_autoscaler_sync_period}}
-        return await ControllerManager(client, a.controllers.split(","), opts).start()
+                "horizontalpodautoscaling": {"sync_period": a.horizontal_pod_autoscaler_sync_period},
+                "nodeipam": {"cluster_cidr": a.cluster_cidr, "node_cidr_mask_size": a.node_cidr_mask_size},
+                "service": {"ip_range": a.loadbalancer_ip_range}}
+        enabled = a.controllers.split(",")
+        if a.allocate_node_cidrs:
+            enabled.append("nodeipam")
+        if a.loadbalancer_ip_range:
+            enabled.append("service")
+        return await ControllerManager(client, enabled, opts).start()
 
     run_until_signal(start)
 

@@ -44,6 +44,18 @@ def main(argv=None):
     ap.add_argument("--pod-manifest-path", default=None, help="directory of static pod manifests (JSON/YAML)")
     ap.add_argument("--eviction-hard", default="memory.available<100Mi",
                     help="hard eviction thresholds, e.g. memory.available<100Mi,nodefs.available<5%%")
+    ap.add_argument("--network-plugin", default="", choices=["", "cni", "kubenet"])
+    ap.add_argument("--cni-conf-dir", default="/etc/cni/net.d")
+    ap.add_argument("--cni-bin-dir", default="/opt/cni/bin")
+    ap.add_argument("--pod-cidr", default=None, help="standalone mode: pod CIDR when no API node spec provides one")
+    ap.add_argument("--cluster-dns", default="", help="comma-separated DNS server IPs for ClusterFirst pods")
+    ap.add_argument("--cluster-domain", default="cluster.local")
+    ap.add_argument("--resolv-conf", default="/etc/resolv.conf")
+    ap.add_argument("--hostport-holder", type=lambda v: v.lower() != "false", default=True,
+                    help="open and hold the host ports of pods in their own network namespace")
+    ap.add_argument("--minimum-container-ttl-duration", type=float, default=0.0)
+    ap.add_argument("--maximum-dead-containers-per-container", type=int, default=1)
+    ap.add_argument("--maximum-dead-containers", type=int, default=-1)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -72,10 +84,20 @@ def main(argv=None):
         cap = int(parse_quantity(a.image_fs_capacity).value) if a.image_fs_capacity not in ("", "0") else 0
         image_gc = {"capacity_bytes": cap, "high": a.image_gc_high_threshold, "low": a.image_gc_low_threshold} if cap else None
         labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
+        from ..kubelet import network as net
+        plugin = net.new_plugin(a.network_plugin, os.path.join(a.root_dir, "network"), a.cni_conf_dir, a.cni_bin_dir)
+        if a.pod_cidr:
+            plugin.set_pod_cidr(a.pod_cidr)
+        dns = net.DNSConfigurer(a.cluster_dns.split(","), a.cluster_domain, a.resolv_conf)
+        hostports = net.HostportManager(a.hostport_holder)
+        container_gc = {"min_age": a.minimum_container_ttl_duration,
+                        "max_per_pod_container": a.maximum_dead_containers_per_container,
+                        "max_containers": a.maximum_dead_containers}
         kl = Kubelet(client, a.hostname_override, rt, dm, pods=a.max_pods, labels=labels,
                      node_status_update_frequency=a.node_status_update_frequency, http_port=a.port, address=a.address,
                      root_dir=a.root_dir, cpu_manager_policy=a.cpu_manager_policy, reserved_cpus=a.reserved_cpus,
-                     pod_manifest_path=a.pod_manifest_path, eviction_hard=a.eviction_hard, image_gc=image_gc)
+                     pod_manifest_path=a.pod_manifest_path, eviction_hard=a.eviction_hard, image_gc=image_gc,
+                     network_plugin=plugin, dns=dns, hostports=hostports, container_gc=container_gc)
         await kl.run()
         print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port})", flush=True)
         return kl

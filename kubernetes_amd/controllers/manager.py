@@ -17,6 +17,7 @@ from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleContr
 from .certificates import (BootstrapSignerController, ClusterRoleAggregationController, CSRApprovingController,
                            CSRSigningController, TokenCleanerController, TokensController, TTLController)
 from .podautoscaler import HorizontalController
+from .network import NodeIPAMController, ServiceLBController
 from .volume import PersistentVolumeController, PVCProtectionController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
@@ -49,14 +50,21 @@ CONTROLLERS = {
     "ttl": TTLController,
     "persistentvolume-binder": PersistentVolumeController,
     "pvc-protection": PVCProtectionController,
+    "nodeipam": NodeIPAMController,
+    "service": ServiceLBController,
 }
+
+
+# like ControllersDisabledByDefault: "*" does not start these (name them explicitly, or the
+# command line enables them from --allocate-node-cidrs / --loadbalancer-ip-range)
+DISABLED_BY_DEFAULT = {"nodeipam", "service"}
 
 
 def resolve(enabled):
     names = set()
     for e in enabled or ["*"]:
         if e == "*":
-            names |= set(CONTROLLERS)
+            names |= set(CONTROLLERS) - DISABLED_BY_DEFAULT
         elif e.startswith("-"):
             names.discard(e[1:])
         else:

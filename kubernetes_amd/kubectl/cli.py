@@ -287,6 +287,8 @@ class Kubectl(extra.ExtraCommands):
         q = f"?container={a.container}" if a.container else ""
         if a.tail is not None:
             q += ("&" if q else "?") + f"tailLines={a.tail}"
+        if a.previous:
+            q += ("&" if q else "?") + "previous=true"
         st, body = await self.client.raw("GET", f"/api/v1/namespaces/{self.ns}/pods/{name}/log{q}")
         if st != 200:
             raise SystemExit(f"error: {body.decode(errors='replace')}")
@@ -821,6 +823,7 @@ def build_parser():
     lg.add_argument("pod")
     lg.add_argument("-c", "--container")
     lg.add_argument("--tail", type=int)
+    lg.add_argument("-p", "--previous", action="store_true")
     for name in ("label", "annotate"):
         la = add(name)
         la.add_argument("resource")

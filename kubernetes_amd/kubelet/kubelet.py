@@ -50,7 +50,7 @@ _ip_counter = itertools.count(2)
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
                  "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
-                 "waiting")
+                 "waiting", "net_mounts", "net_setup", "previous", "backoff")
 
     def __init__(self, pod):
         self.uid = pod["metadata"]["uid"]
@@ -71,6 +71,10 @@ class PodState:
         self.first_seen = time.time()
         self.volumes = None            # {volume name: host path} once mounted
         self.waiting: dict[str, tuple] = {}   # container -> (reason, message) while it cannot start
+        self.net_mounts = []                  # /etc/hosts + /etc/resolv.conf bind mounts
+        self.net_setup = False                # network plugin SetUpPod done for the sandbox
+        self.previous: dict[str, str] = {}    # container name -> last dead instance (logs --previous)
+        self.backoff: dict[str, list] = {}    # container name -> [next restart allowed at, current delay]
 
 
 class Kubelet:
@@ -79,8 +83,16 @@ class Kubelet:
                  emit_events=True, register=True, metrics=None, address="127.0.0.1", max_status_inflight=64,
                  root_dir=None, cpu_manager_policy="none", cpu_topology=None, reserved_cpus=1,
                  pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0,
-                 image_service=None, image_gc=None, image_backoff=10.0):
+                 image_service=None, image_gc=None, image_backoff=10.0, network_plugin=None, dns=None,
+                 hostports=None, container_gc=None, crash_backoff=(10.0, 300.0)):
         self.client = client
+        from .network import NetworkPlugin
+        self.network = network_plugin or NetworkPlugin()
+        self.dns = dns                       # network.DNSConfigurer or None
+        self.hostports = hostports           # network.HostportManager or None
+        self.container_gc = container_gc     # ContainerGC policy dict or None
+        self.crash_backoff = crash_backoff   # (initial, max) restart back-off, kubelet.go backOffPeriod/MaxContainerBackOff
+        self.pod_cidr = None
         self.pod_manifest_path = pod_manifest_path
         self.static_pods = None
         self.eviction = None
@@ -175,6 +187,8 @@ class Kubelet:
             self._tasks.append(asyncio.ensure_future(self._eviction_loop()))
         if self.image_gc is not None:
             self._tasks.append(asyncio.ensure_future(self._image_gc_loop()))
+        if self.container_gc is not None:
+            self._tasks.append(asyncio.ensure_future(self._container_gc_loop()))
         self.started.set()
 
     def _images_in_use(self):
@@ -223,6 +237,8 @@ class Kubelet:
         for t in list(self._workers.values()):
             t.cancel()
         self.probes.stop()
+        if self.hostports is not None:
+            self.hostports.close()
         await self.dm.stop()
         self.recorder.stop()
         if self.http:
@@ -254,10 +270,15 @@ class Kubelet:
         now = now_rfc3339()
         mem_p = self.eviction is not None and self.eviction.has("MemoryPressure")
         disk_p = self.eviction is not None and self.eviction.has("DiskPressure")
+        net_err = self.network.status()
+        ready = ({"type": "Ready", "status": "True", "reason": "KubeletReady", "message": "kubelet is posting ready status",
+                  "lastHeartbeatTime": now, "lastTransitionTime": now} if not net_err else
+                 {"type": "Ready", "status": "False", "reason": "KubeletNotReady",
+                  "message": f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady message:{net_err}",
+                  "lastHeartbeatTime": now, "lastTransitionTime": now})
         st = {"capacity": capacity, "allocatable": dict(capacity),
               "conditions": [
-                  {"type": "Ready", "status": "True", "reason": "KubeletReady", "message": "kubelet is posting ready status",
-                   "lastHeartbeatTime": now, "lastTransitionTime": now},
+                  ready,
                   {"type": "MemoryPressure", "status": "True" if mem_p else "False",
                    "reason": "KubeletHasInsufficientMemory" if mem_p else "KubeletHasSufficientMemory",
                    "lastHeartbeatTime": now, "lastTransitionTime": now},
@@ -287,6 +308,7 @@ class Kubelet:
             try:
                 got = await self.client.create("nodes", node)
                 self.node_uid = got["metadata"]["uid"]
+                self._observe_pod_cidr(got)
                 return
             except APIStatusError as e:
                 if e.code == 409:
@@ -301,12 +323,21 @@ class Kubelet:
             except (ConnectionError, OSError):
                 await asyncio.sleep(0.2)
 
+    def _observe_pod_cidr(self, node):
+        """`updatePodCIDR`: hand the node's spec.podCIDR to the network plugin once it appears."""
+        cidr = ((node or {}).get("spec") or {}).get("podCIDR")
+        if cidr and cidr != self.pod_cidr:
+            self.pod_cidr = cidr
+            self.network.set_pod_cidr(cidr)
+            self._status_dirty.set()
+
     async def update_node_status(self):
         self._collect_plugin_labels()
         st = self._node_status()
         try:
             patch = {"status": st}
-            await self.client.patch("nodes", self.node_name, patch, None, "merge", "status")
+            got = await self.client.patch("nodes", self.node_name, patch, None, "merge", "status")
+            self._observe_pod_cidr(got)
             if self.plugin_labels:
                 cur = self.informer_node_labels
                 if any(cur.get(k) != v for k, v in self.plugin_labels.items()):
@@ -418,6 +449,7 @@ class Kubelet:
         if op == "delete":
             if st is not None:
                 await self._kill_pod(st, 0)
+                await self._teardown_network(st)
                 st.deleted = True
                 self.pods.pop(uid, None)
                 self.by_key.pop(_key(pod), None)
@@ -475,6 +507,10 @@ class Kubelet:
                 ann.update(pr["annotations"])
             st.sandbox = await rt.run_pod_sandbox(pod, ann)
             self.m_runtime_ops.labels("run_podsandbox").inc()
+            st.net_setup = False
+        if not st.net_setup:
+            if not await self._setup_network(st):
+                return
         # init containers, sequentially
         for c in spec.get("initContainers") or ():
             cid = st.init_containers.get(c["name"])
@@ -505,9 +541,15 @@ class Kubelet:
                 cs = rt.container_status(cid)
                 if cs is not None and cs.state == EXITED:
                     restart = policy == "Always" or (policy == "OnFailure" and cs.exit_code != 0)
+                    if restart and not md_deleting(pod) and self._in_backoff(st, c, cs):
+                        continue
                     if restart and not md_deleting(pod):
                         st.restarts[c["name"]] = st.restarts.get(c["name"], 0) + 1
-                        await rt.remove_container(cid)
+                        # keep one dead instance per container (container GC's MaxPerPodContainer=1)
+                        old = st.previous.get(c["name"])
+                        if old is not None:
+                            await rt.remove_container(old)
+                        st.previous[c["name"]] = cid
                         cid = None
             if cid is None:
                 st.containers[c["name"]] = await self._start(st, c)
@@ -530,6 +572,7 @@ class Kubelet:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: device plugin InitContainer failed: {e}")
             return None
         spec_c = c
+        opts.mounts.extend(st.net_mounts)
         if c.get("volumeMounts") or c.get("envFrom") or any("valueFrom" in e or "$(" in str(e.get("value", ""))
                                                              for e in c.get("env") or ()):
             try:
@@ -602,6 +645,126 @@ class Kubelet:
             self._resync(uid)
         spawn(kill())
 
+    def _in_backoff(self, st: PodState, c, cs):
+        """kuberuntime `doBackOff`: the first restart is immediate; later ones wait
+        initial·2^k (capped). A container that ran for 2×max before failing starts over."""
+        init, cap = self.crash_backoff
+        if not init:
+            return False
+        now = time.monotonic()
+        ent = st.backoff.get(c["name"])
+        ran = (cs.finished_at or 0) - (cs.started_at or 0)
+        if ent is not None and ran > 2 * cap:
+            ent = None
+        if ent is None:
+            st.backoff[c["name"]] = [now + init, init]
+            st.waiting.pop(c["name"], None)
+            return False
+        if now < ent[0]:
+            md = st.pod["metadata"]
+            st.waiting[c["name"]] = ("CrashLoopBackOff", f"Back-off {ent[1]:g}s restarting failed container={c['name']} "
+                                                         f"pod={md['name']}_{md.get('namespace', 'default')}({st.uid})")
+            asyncio.get_running_loop().call_later(ent[0] - now + 0.01, self._resync, st.uid)
+            return True
+        delay = min(ent[1] * 2, cap)
+        st.backoff[c["name"]] = [now + delay, delay]
+        st.waiting.pop(c["name"], None)
+        return False
+
+    async def garbage_collect_containers(self, now=None):
+        """`pkg/kubelet/container_gc.go` + `kuberuntime_gc.go`: dead containers older than
+        `min_age` are evictable; keep at most `max_per_pod_container` per (pod, container) and
+        `max_containers` overall (oldest first); containers of pods the kubelet no longer
+        tracks are always removed. Returns the removed container ids."""
+        pol = self.container_gc or {}
+        now = now or time.time()
+        min_age = float(pol.get("min_age", 0.0))
+        per = int(pol.get("max_per_pod_container", 1))
+        total = int(pol.get("max_containers", -1))
+        live = set()
+        evictable = []            # (finished_at, cid, st, name)
+        for st in self.pods.values():
+            live.update(x for x in st.containers.values() if x)
+            live.update(x for x in st.init_containers.values() if x)
+            for name, cid in list(st.previous.items()):
+                cs = self.runtime.container_status(cid)
+                if cs is None:
+                    st.previous.pop(name, None)
+                    continue
+                if now - (cs.finished_at or cs.created_at) >= min_age:
+                    evictable.append((cs.finished_at or cs.created_at, cid, st, name))
+        removed = []
+        keep = evictable
+        if per >= 0:
+            keep = []
+            by_key = {}
+            for ent in sorted(evictable, reverse=True):
+                k = (ent[2].uid, ent[3])
+                by_key[k] = by_key.get(k, 0) + 1
+                (keep if by_key[k] <= per else removed).append(ent)
+        if total >= 0 and len(keep) > total:
+            keep.sort()
+            removed += keep[:len(keep) - total]
+        out = []
+        for _, cid, st, name in removed:
+            await self.runtime.remove_container(cid)
+            if st.previous.get(name) == cid:
+                st.previous.pop(name, None)
+            out.append(cid)
+        for cs in list(self.runtime.list_containers()):
+            if cs.state == EXITED and cs.id not in live and not any(cs.id in st.previous.values() for st in self.pods.values()) \
+                    and now - (cs.finished_at or cs.created_at) >= min_age:
+                await self.runtime.remove_container(cs.id)
+                out.append(cs.id)
+        return out
+
+    async def _container_gc_loop(self):
+        period = float((self.container_gc or {}).get("period", 60.0))
+        while not self._stopped:
+            await asyncio.sleep(period)
+            try:
+                await self.garbage_collect_containers()
+            except Exception as e:  # noqa: BLE001 - GC failures are logged and retried
+                log.warning("container garbage collection failed: %s", e)
+
+    async def _setup_network(self, st: PodState):
+        """SetUpPod through the network plugin (own-netns runtimes), host ports, and the
+        kubelet-managed /etc/hosts + /etc/resolv.conf."""
+        from .network import NetworkError
+        pod = st.pod
+        host_net = bool((pod.get("spec") or {}).get("hostNetwork")) or getattr(self.runtime, "shares_host_network", False)
+        try:
+            if not host_net:
+                ip = await self.network.setup_pod(pod, st.sandbox, getattr(self.runtime, "netns_of", lambda s: "")(st.sandbox))
+                if ip:
+                    st.ip = ip
+                if self.hostports is not None:
+                    self.hostports.add(pod, st.ip)
+        except NetworkError as e:
+            self.recorder.event(pod, "Warning", "FailedCreatePodSandBox", f"Failed to set up pod network: {e}")
+            await self.runtime.remove_pod_sandbox(st.sandbox)
+            st.sandbox = None
+            await self._report(st)
+            asyncio.get_running_loop().call_later(2.0, self._resync, st.uid)
+            return False
+        if self.dns is not None:
+            st.net_mounts = self.dns.write_pod_files(os.path.join(self.root_dir, "pods", st.uid), pod, st.ip)
+        st.net_setup = True
+        return True
+
+    async def _teardown_network(self, st: PodState):
+        if not st.net_setup:
+            return
+        st.net_setup = False
+        if self.hostports is not None:
+            self.hostports.remove(st.pod)
+        host_net = bool((st.pod.get("spec") or {}).get("hostNetwork")) or getattr(self.runtime, "shares_host_network", False)
+        if not host_net and st.sandbox is not None:
+            try:
+                await self.network.teardown_pod(st.pod, st.sandbox)
+            except Exception as e:  # noqa: BLE001 - teardown is best effort, like the reference
+                log.warning("network teardown for %s: %s", st.uid, e)
+
     async def _kill_pod(self, st: PodState, grace):
         self.probes.remove_pod(st.uid)
         if self.cpu_manager is not None:
@@ -618,6 +781,7 @@ class Kubelet:
         """Containers are dead: report final status, then remove the pod object (grace 0)."""
         pod = st.pod
         md = pod["metadata"]
+        await self._teardown_network(st)
         if st.sandbox is not None:
             await self.runtime.remove_pod_sandbox(st.sandbox)
             st.sandbox = None
@@ -774,7 +938,13 @@ class Kubelet:
                     return Response(404, b"pod not found", "text/plain")
                 if not cname:
                     cname = ((st.pod.get("spec") or {}).get("containers") or [{}])[0].get("name", "")
-                cid = st.containers.get(cname) or st.init_containers.get(cname)
+                if req.query.get("previous") in ("true", "1"):
+                    cid = st.previous.get(cname)
+                    if cid is None:
+                        return Response(400, f'previous terminated container "{cname}" in pod "{name}" not found'.encode(),
+                                        "text/plain")
+                else:
+                    cid = st.containers.get(cname) or st.init_containers.get(cname)
                 if cid is None:
                     return Response(404, b"container not found", "text/plain")
                 tail = int(req.query["tailLines"]) if "tailLines" in req.query else None
@@ -806,6 +976,13 @@ def _ts(t):
 
 def _container_status(c, cs, restarts, waiting=None):
     s = {"name": c["name"], "image": c.get("image", ""), "imageID": "", "restartCount": restarts, "ready": False}
+    if cs is not None and waiting and waiting[0] == "CrashLoopBackOff" and cs.state == EXITED:
+        s["containerID"] = cs.id
+        s["state"] = {"waiting": {"reason": waiting[0], "message": waiting[1]}}
+        s["lastState"] = {"terminated": {"exitCode": cs.exit_code, "reason": cs.reason or "Error",
+                                         "startedAt": _ts(cs.started_at), "finishedAt": _ts(cs.finished_at),
+                                         "containerID": cs.id}}
+        return s
     if cs is None:
         if waiting:
             s["state"] = {"waiting": {"reason": waiting[0], "message": waiting[1]}}

@@ -1,0 +1,453 @@
+"""Pod networking for the kubelet: network plugins (CNI, kubenet), host-local IPAM, DNS
+configuration and host ports.
+
+Parity:
+  * `pkg/kubelet/network/plugins.go` (`NetworkPlugin`: Init / SetUpPod / TearDownPod /
+    GetPodNetworkStatus / Status, `Event(NET_PLUGIN_EVENT_POD_CIDR_CHANGE)`);
+  * `pkg/kubelet/network/cni/cni.go` (first config in `--cni-conf-dir` by name, `.conf` or
+    `.conflist`; plugins exec'd from `--cni-bin-dir` with `CNI_COMMAND/CNI_CONTAINERID/CNI_NETNS/
+    CNI_IFNAME/CNI_PATH/CNI_ARGS` and the network config on stdin; chained plugins get
+    `prevResult`; DEL runs in reverse order);
+  * `pkg/kubelet/network/kubenet/kubenet_linux.go` (bridge `cbr0` + host-local IPAM over the
+    node's `spec.podCIDR`, status error until the CIDR is known) — host-local here is
+    `HostLocalIPAM`, the same on-disk layout as the CNI host-local plugin (one file per reserved
+    IP holding the container id, `last_reserved_ip`);
+  * `pkg/kubelet/network/dns/dns.go` (`ClusterFirst` / `ClusterFirstWithHostNet` / `Default` /
+    `None`+`dnsConfig`, search path `<ns>.svc.<domain> svc.<domain> <domain>` + host searches,
+    `ndots:5`, at most 3 nameservers / 6 search domains / 256 characters) and the kubelet-managed
+    `/etc/hosts` (`kubelet_pods.go` `makeHostsMount`, hostAliases);
+  * `pkg/kubelet/network/hostport/hostport_manager.go` (`KUBE-HOSTPORTS` → `KUBE-HP-<hash>` DNAT
+    chains; the host port's socket is opened and held so nothing else can take it).
+
+With the in-process runtimes pods share the node's network namespace, so the plugins allocate
+and record addresses (and CNI plugins get an empty `CNI_NETNS`); an OCI runtime with its own
+namespaces gets the same calls with a real netns path.
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import hashlib
+import ipaddress
+import json
+import logging
+import os
+import socket
+
+log = logging.getLogger("kubelet.network")
+
+MAX_NS, MAX_SEARCH, MAX_SEARCH_CHARS = 3, 6, 256
+
+
+class NetworkError(Exception):
+    pass
+
+
+# ------------------------------------------------------------------------------------ IPAM
+class HostLocalIPAM:
+    def __init__(self, data_dir, cidr=None):
+        self.dir = data_dir
+        self.net = None
+        if cidr:
+            self.set_cidr(cidr)
+
+    def set_cidr(self, cidr):
+        self.net = ipaddress.ip_network(cidr, strict=False)
+        os.makedirs(self.dir, exist_ok=True)
+
+    @property
+    def gateway(self):
+        return str(self.net.network_address + 1) if self.net else None
+
+    def _reserved(self):
+        out = {}
+        for fn in os.listdir(self.dir) if os.path.isdir(self.dir) else ():
+            if fn == "last_reserved_ip":
+                continue
+            try:
+                ipaddress.ip_address(fn)
+            except ValueError:
+                continue
+            with open(os.path.join(self.dir, fn)) as f:
+                out[fn] = f.read().strip()
+        return out
+
+    def allocate(self, container_id):
+        if self.net is None:
+            raise NetworkError("no pod CIDR configured")
+        used = self._reserved()
+        for ip, cid in used.items():
+            if cid == container_id:
+                return ip
+        hosts = self.net.num_addresses - 2
+        start = 2
+        try:
+            with open(os.path.join(self.dir, "last_reserved_ip")) as f:
+                last = ipaddress.ip_address(f.read().strip())
+            if last in self.net:
+                start = int(last) - int(self.net.network_address) + 1
+        except (OSError, ValueError):
+            pass
+        for i in range(hosts):
+            off = 2 + ((start - 2 + i) % (hosts - 1))
+            ip = str(self.net.network_address + off)
+            if ip in used:
+                continue
+            try:
+                fd = os.open(os.path.join(self.dir, ip), os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o644)
+            except FileExistsError:
+                continue
+            with os.fdopen(fd, "w") as f:
+                f.write(container_id)
+            with open(os.path.join(self.dir, "last_reserved_ip"), "w") as f:
+                f.write(ip)
+            return ip
+        raise NetworkError(f"no IP addresses available in range set: {self.net}")
+
+    def release(self, container_id):
+        for ip, cid in self._reserved().items():
+            if cid == container_id:
+                os.unlink(os.path.join(self.dir, ip))
+
+
+# ------------------------------------------------------------------------------------ plugins
+class NetworkPlugin:
+    name = "noop"
+
+    def set_pod_cidr(self, cidr):
+        pass
+
+    def status(self):
+        return None
+
+    async def setup_pod(self, pod, sandbox_id, netns=""):
+        return None
+
+    async def teardown_pod(self, pod, sandbox_id, netns=""):
+        pass
+
+
+class KubenetPlugin(NetworkPlugin):
+    name = "kubenet"
+
+    def __init__(self, data_dir, bridge="cbr0", mtu=1460):
+        self.ipam = HostLocalIPAM(os.path.join(data_dir, "networks", "kubenet"))
+        self.bridge, self.mtu = bridge, mtu
+        self.cidr = None
+
+    def set_pod_cidr(self, cidr):
+        if cidr and cidr != self.cidr:
+            self.cidr = cidr
+            self.ipam.set_cidr(cidr)
+            log.info("kubenet: pod CIDR %s, bridge %s gateway %s", cidr, self.bridge, self.ipam.gateway)
+
+    def status(self):
+        if self.cidr is None:
+            return "Kubenet does not have netConfig. This is most likely due to lack of PodCIDR"
+        return None
+
+    async def setup_pod(self, pod, sandbox_id, netns=""):
+        if self.cidr is None:
+            raise NetworkError(self.status())
+        return self.ipam.allocate(sandbox_id)
+
+    async def teardown_pod(self, pod, sandbox_id, netns=""):
+        self.ipam.release(sandbox_id)
+
+
+class CNIPlugin(NetworkPlugin):
+    name = "cni"
+
+    def __init__(self, conf_dir="/etc/cni/net.d", bin_dirs=("/opt/cni/bin",), pod_cidr=None):
+        self.conf_dir = conf_dir
+        self.bin_dirs = list(bin_dirs)
+        self.pod_cidr = pod_cidr
+        self.net = None
+        self._load()
+
+    def _load(self):
+        if not os.path.isdir(self.conf_dir):
+            self.net = None
+            return
+        for fn in sorted(os.listdir(self.conf_dir)):
+            if not fn.endswith((".conf", ".conflist", ".json")):
+                continue
+            with open(os.path.join(self.conf_dir, fn)) as f:
+                try:
+                    conf = json.load(f)
+                except ValueError:
+                    continue
+            if "plugins" in conf:
+                self.net = {"name": conf.get("name", ""), "cniVersion": conf.get("cniVersion", "0.3.1"),
+                            "plugins": conf["plugins"]}
+            else:
+                self.net = {"name": conf.get("name", ""), "cniVersion": conf.get("cniVersion", "0.2.0"), "plugins": [conf]}
+            return
+
+    def set_pod_cidr(self, cidr):
+        self.pod_cidr = cidr
+
+    def status(self):
+        if self.net is None:
+            self._load()
+        if self.net is None:
+            return "cni config uninitialized"
+        return None
+
+    def _find(self, typ):
+        for d in self.bin_dirs:
+            p = os.path.join(d, typ)
+            if os.access(p, os.X_OK):
+                return p
+        raise NetworkError(f'failed to find plugin "{typ}" in path {self.bin_dirs}')
+
+    async def _exec(self, cmd, plugin_conf, pod, sandbox_id, netns, prev=None):
+        conf = dict(plugin_conf, name=self.net["name"], cniVersion=self.net["cniVersion"])
+        if prev is not None:
+            conf["prevResult"] = prev
+        if self.pod_cidr and isinstance(conf.get("ipam"), dict) and conf["ipam"].get("subnet") == "usePodCidr":
+            conf["ipam"] = dict(conf["ipam"], subnet=self.pod_cidr)
+        md = pod["metadata"]
+        env = dict(os.environ, CNI_COMMAND=cmd, CNI_CONTAINERID=sandbox_id, CNI_NETNS=netns or "", CNI_IFNAME="eth0",
+                   CNI_PATH=os.pathsep.join(self.bin_dirs),
+                   CNI_ARGS=f"IgnoreUnknown=1;K8S_POD_NAMESPACE={md.get('namespace', 'default')};"
+                            f"K8S_POD_NAME={md['name']};K8S_POD_INFRA_CONTAINER_ID={sandbox_id}")
+        p = await asyncio.create_subprocess_exec(self._find(conf["type"]), stdin=asyncio.subprocess.PIPE,
+                                                 stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.PIPE, env=env)
+        out, err = await p.communicate(json.dumps(conf).encode())
+        if p.returncode != 0:
+            try:
+                msg = json.loads(out).get("msg", "")
+            except ValueError:
+                msg = (out or err).decode(errors="replace")
+            raise NetworkError(f"CNI {cmd} {conf['type']}: {msg.strip() or 'exit ' + str(p.returncode)}")
+        if cmd == "ADD" and out.strip():
+            return json.loads(out)
+        return prev
+
+    async def setup_pod(self, pod, sandbox_id, netns=""):
+        if self.status():
+            raise NetworkError(self.status())
+        res = None
+        for pc in self.net["plugins"]:
+            res = await self._exec("ADD", pc, pod, sandbox_id, netns, res)
+        return result_ip(res)
+
+    async def teardown_pod(self, pod, sandbox_id, netns=""):
+        if self.net is None:
+            return
+        for pc in reversed(self.net["plugins"]):
+            try:
+                await self._exec("DEL", pc, pod, sandbox_id, netns)
+            except NetworkError as e:
+                log.warning("%s", e)
+
+
+def result_ip(res):
+    """IPv4 address from a CNI result (0.3.x `ips[]` or 0.2.0 `ip4.ip`)."""
+    if not res:
+        return None
+    for ip in res.get("ips") or ():
+        addr = ip.get("address", "")
+        if ip.get("version", "4") == "4" and addr:
+            return addr.split("/")[0]
+    ip4 = (res.get("ip4") or {}).get("ip")
+    return ip4.split("/")[0] if ip4 else None
+
+
+def new_plugin(name, data_dir, cni_conf_dir="/etc/cni/net.d", cni_bin_dir="/opt/cni/bin"):
+    if name in (None, "", "noop"):
+        return NetworkPlugin()
+    if name == "kubenet":
+        return KubenetPlugin(data_dir)
+    if name == "cni":
+        return CNIPlugin(cni_conf_dir, cni_bin_dir.split(","))
+    raise ValueError(f"unknown network plugin {name!r}")
+
+
+# ------------------------------------------------------------------------------------ DNS
+def parse_resolv_conf(path):
+    ns, search, opts = [], [], []
+    try:
+        with open(path) as f:
+            for line in f:
+                parts = line.split("#", 1)[0].split()
+                if not parts:
+                    continue
+                if parts[0] == "nameserver" and len(parts) > 1:
+                    ns.append(parts[1])
+                elif parts[0] == "search":
+                    search = parts[1:]
+                elif parts[0] == "options":
+                    opts += parts[1:]
+    except OSError:
+        pass
+    return ns, search, opts
+
+
+def _fit_search(search):
+    out, n = [], 0
+    for s in search:
+        if s in out:
+            continue
+        if len(out) >= MAX_SEARCH or n + len(s) + (1 if out else 0) > MAX_SEARCH_CHARS:
+            break
+        out.append(s)
+        n += len(s) + (1 if len(out) > 1 else 0)
+    return out
+
+
+class DNSConfigurer:
+    def __init__(self, cluster_dns=(), cluster_domain="cluster.local", resolv_conf="/etc/resolv.conf"):
+        self.cluster_dns = [x for x in cluster_dns if x]
+        self.domain = cluster_domain
+        self.resolv_conf = resolv_conf
+
+    def pod_dns(self, pod):
+        spec = pod.get("spec") or {}
+        policy = spec.get("dnsPolicy") or "ClusterFirst"
+        host_ns, host_search, host_opts = parse_resolv_conf(self.resolv_conf) if self.resolv_conf else ([], [], [])
+        if policy == "ClusterFirst" and spec.get("hostNetwork"):
+            policy = "Default"
+        if policy == "ClusterFirstWithHostNet":
+            policy = "ClusterFirst"
+        if policy == "None":
+            ns, search, opts = [], [], []
+        elif policy == "Default" or not self.cluster_dns:
+            ns, search, opts = list(host_ns), list(host_search), list(host_opts)
+        else:
+            pns = pod["metadata"].get("namespace", "default")
+            ns = list(self.cluster_dns)
+            search = [f"{pns}.svc.{self.domain}", f"svc.{self.domain}", self.domain] + host_search
+            opts = ["ndots:5"]
+        cfg = spec.get("dnsConfig") or {}
+        ns += [x for x in cfg.get("nameservers") or () if x not in ns]
+        search += [x for x in cfg.get("searches") or () if x not in search]
+        for o in cfg.get("options") or ():
+            name = o.get("name")
+            opts = [x for x in opts if x.split(":")[0] != name]
+            opts.append(f"{name}:{o['value']}" if o.get("value") is not None else name)
+        return ns[:MAX_NS], _fit_search(search), opts
+
+    def resolv_text(self, pod):
+        ns, search, opts = self.pod_dns(pod)
+        lines = [f"nameserver {x}" for x in ns]
+        if search:
+            lines.append("search " + " ".join(search))
+        if opts:
+            lines.append("options " + " ".join(opts))
+        return "\n".join(lines) + "\n"
+
+    def hosts_text(self, pod, ip):
+        spec = pod.get("spec") or {}
+        md = pod["metadata"]
+        lines = ["# Kubernetes-managed hosts file.", "127.0.0.1\tlocalhost", "::1\tlocalhost ip6-localhost ip6-loopback",
+                 "fe00::0\tip6-localnet", "fe00::0\tip6-mcastprefix", "fe00::1\tip6-allnodes", "fe00::2\tip6-allrouters"]
+        host = spec.get("hostname") or md["name"]
+        if ip:
+            if spec.get("subdomain"):
+                fqdn = f"{host}.{spec['subdomain']}.{md.get('namespace', 'default')}.svc.{self.domain}"
+                lines.append(f"{ip}\t{fqdn}\t{host}")
+            else:
+                lines.append(f"{ip}\t{host}")
+        if spec.get("hostAliases"):
+            lines.append("\n# Entries added by HostAliases.")
+            for a in spec["hostAliases"]:
+                lines.append(f"{a.get('ip')}\t" + "\t".join(a.get("hostnames") or ()))
+        return "\n".join(lines) + "\n"
+
+    def write_pod_files(self, pod_dir, pod, ip):
+        """Write `etc-hosts` and `resolv.conf` under the pod dir; returns the container mounts."""
+        os.makedirs(pod_dir, exist_ok=True)
+        mounts = []
+        spec = pod.get("spec") or {}
+        if not spec.get("hostNetwork"):
+            hp = os.path.join(pod_dir, "etc-hosts")
+            with open(hp, "w") as f:
+                f.write(self.hosts_text(pod, ip))
+            mounts.append({"containerPath": "/etc/hosts", "hostPath": hp, "readOnly": False})
+        rp = os.path.join(pod_dir, "resolv.conf")
+        with open(rp, "w") as f:
+            f.write(self.resolv_text(pod))
+        mounts.append({"containerPath": "/etc/resolv.conf", "hostPath": rp, "readOnly": False})
+        return mounts
+
+
+# ------------------------------------------------------------------------------------ hostports
+def _chain(name, proto, port):
+    h = hashlib.sha256(f"{name}{port}{proto}".encode()).digest()
+    return "KUBE-HP-" + base64.b32encode(h).decode()[:16]
+
+
+class HostportManager:
+    def __init__(self, hold_sockets=True):
+        self.hold = hold_sockets
+        self.held: dict[tuple, socket.socket] = {}          # (proto, hostIP, port) -> socket
+        self.mappings: dict[str, list] = {}                 # pod uid -> [(proto, hostIP, hostPort, containerPort, podIP, name)]
+
+    @staticmethod
+    def pod_mappings(pod, ip):
+        out = []
+        md = pod["metadata"]
+        full = f"{md['name']}_{md.get('namespace', 'default')}"
+        for c in (pod.get("spec") or {}).get("containers") or ():
+            for p in c.get("ports") or ():
+                if p.get("hostPort"):
+                    out.append((p.get("protocol", "TCP").lower(), p.get("hostIP", ""), int(p["hostPort"]),
+                                int(p["containerPort"]), ip, full))
+        return out
+
+    def add(self, pod, ip):
+        if (pod.get("spec") or {}).get("hostNetwork"):
+            return []
+        maps = self.pod_mappings(pod, ip)
+        opened = []
+        try:
+            for proto, hip, hport, _, _, _ in maps:
+                key = (proto, hip, hport)
+                if key in self.held or not self.hold:
+                    continue
+                s = socket.socket(socket.AF_INET, socket.SOCK_STREAM if proto == "tcp" else socket.SOCK_DGRAM)
+                try:
+                    s.bind((hip or "0.0.0.0", hport))
+                    if proto == "tcp":
+                        s.listen(1)
+                except OSError as e:
+                    s.close()
+                    raise NetworkError(f'cannot open "{proto}:{hport}" for the pod\'s host port: {e}')
+                self.held[key] = s
+                opened.append(key)
+        except NetworkError:
+            for k in opened:
+                self.held.pop(k).close()
+            raise
+        self.mappings[pod["metadata"]["uid"]] = maps
+        return maps
+
+    def remove(self, pod):
+        maps = self.mappings.pop(pod["metadata"]["uid"], [])
+        for proto, hip, hport, _, _, _ in maps:
+            s = self.held.pop((proto, hip, hport), None)
+            if s is not None:
+                s.close()
+
+    def rules(self):
+        """`iptables-restore` input for the nat table."""
+        lines = ["*nat", ":KUBE-HOSTPORTS - [0:0]"]
+        body = []
+        for maps in self.mappings.values():
+            for proto, hip, hport, cport, ip, name in maps:
+                ch = _chain(name, proto, hport)
+                lines.append(f":{ch} - [0:0]")
+                dst = f" -d {hip}/32" if hip else ""
+                body.append(f'-A KUBE-HOSTPORTS -m comment --comment "{name} hostport {hport}" -m {proto} -p {proto}'
+                            f"{dst} --dport {hport} -j {ch}")
+                body.append(f'-A {ch} -m comment --comment "{name} hostport {hport}" -s {ip}/32 -j KUBE-MARK-MASQ')
+                body.append(f'-A {ch} -m comment --comment "{name} hostport {hport}" -m {proto} -p {proto} '
+                            f"-j DNAT --to-destination {ip}:{cport}")
+        return "\n".join(lines + body + ["COMMIT"]) + "\n"
+
+    def close(self):
+        for s in self.held.values():
+            s.close()
+        self.held.clear()
