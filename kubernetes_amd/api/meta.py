@@ -78,6 +78,7 @@ RESOURCES = [
     ResourceInfo("", "v1", "ReplicationController", "replicationcontrollers", True, ("rc",)),
     ResourceInfo("", "v1", "PersistentVolume", "persistentvolumes", False, ("pv",)),
     ResourceInfo("", "v1", "PersistentVolumeClaim", "persistentvolumeclaims", True, ("pvc",)),
+    ResourceInfo("", "v1", "PodTemplate", "podtemplates", True, ()),
     ResourceInfo("apps", "v1", "ReplicaSet", "replicasets", True, ("rs",)),
     ResourceInfo("apps", "v1", "Deployment", "deployments", True, ("deploy",)),
     ResourceInfo("apps", "v1", "DaemonSet", "daemonsets", True, ("ds",)),
@@ -117,6 +118,46 @@ VIRTUAL = {"tokenreviews", "subjectaccessreviews", "selfsubjectaccessreviews", "
 
 BY_PLURAL = {r.plural: r for r in RESOURCES}
 BY_KIND = {r.kind: r for r in RESOURCES}
+
+# Additional group/versions a resource is served under (`pkg/master/master.go` installs the
+# same storage under every enabled version: e.g. Deployments under apps/v1, apps/v1beta2,
+# apps/v1beta1 and extensions/v1beta1). Objects are stored once, in the canonical version;
+# responses carry the requested apiVersion.
+_ALIAS_TABLE = {
+    ("extensions", "v1beta1"): ("deployments", "daemonsets", "replicasets", "podsecuritypolicies", "networkpolicies"),
+    ("apps", "v1beta1"): ("deployments", "statefulsets", "controllerrevisions"),
+    ("apps", "v1beta2"): ("deployments", "daemonsets", "replicasets", "statefulsets", "controllerrevisions"),
+    ("batch", "v2alpha1"): ("cronjobs",),
+    ("autoscaling", "v2beta1"): ("horizontalpodautoscalers",),
+    ("rbac.authorization.k8s.io", "v1beta1"): ("roles", "rolebindings", "clusterroles", "clusterrolebindings"),
+    ("rbac.authorization.k8s.io", "v1alpha1"): ("roles", "rolebindings", "clusterroles", "clusterrolebindings"),
+    ("storage.k8s.io", "v1beta1"): ("storageclasses",),
+    ("authentication.k8s.io", "v1beta1"): ("tokenreviews",),
+    ("authorization.k8s.io", "v1beta1"): ("subjectaccessreviews", "selfsubjectaccessreviews", "localsubjectaccessreviews"),
+    ("events.k8s.io", "v1beta1"): ("events",),
+}
+ALIASES = {(g, v, p): p for (g, v), ps in _ALIAS_TABLE.items() for p in ps}
+
+
+def served_versions():
+    """{group: {version, ...}} over canonical resources and aliases."""
+    out = {}
+    for r in RESOURCES:
+        out.setdefault(r.group, set()).add(r.version)
+    for (g, v, _p) in ALIASES:
+        out.setdefault(g, set()).add(v)
+    return out
+
+
+def version_priority(v: str):
+    """Kubernetes version ordering (`apimachinery/pkg/version/helpers.go`): GA > beta > alpha,
+    higher major first, higher minor first — as a sort key (largest = most preferred)."""
+    import re
+    mt = re.fullmatch(r"v(\d+)(?:(alpha|beta)(\d+))?", v)
+    if not mt:
+        return (-1, 0, 0, v)
+    major, kind, minor = int(mt.group(1)), mt.group(2), int(mt.group(3) or 0)
+    return ({None: 2, "beta": 1, "alpha": 0}[kind], major, minor, v)
 
 
 def lookup(name: str) -> ResourceInfo | None:

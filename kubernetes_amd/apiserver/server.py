@@ -92,6 +92,29 @@ ENC_PREFIX = b"k8s:enc:"          # encrypted-at-rest value (storage/value.py)
 _FRAME = b"\x00KH"                 # shared-store value framing (index header + object)
 
 
+
+def _requested_gv(path):
+    parts = path.split("/", 4)
+    if len(parts) > 2 and parts[1] == "api":
+        return parts[2]
+    if len(parts) > 3 and parts[1] == "apis":
+        return f"{parts[2]}/{parts[3]}"
+    return ""
+
+
+def _rewrite_gv(body, canonical, served):
+    """apiVersion of an object / list (and its items) → the version the client asked for."""
+    try:
+        o = codec.loads(body)
+    except ValueError:
+        return body
+    if o.get("apiVersion") == canonical:
+        o["apiVersion"] = served
+    for it in o.get("items") or ():
+        if isinstance(it, dict) and it.get("apiVersion") in (canonical, None):
+            it["apiVersion"] = served
+    return codec.dumpb(o)
+
 class APIServer:
     def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
@@ -100,7 +123,8 @@ class APIServer:
                  service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767),
                  tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
                  service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
-                 anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None, oidc=None):
+                 anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None, oidc=None,
+                 component_endpoints=None):
         self.abac_policy_file = authorization_policy_file
         self.authorization_webhook_url = authorization_webhook_url
         self.authorization_modes = tuple(authorization_modes)
@@ -111,6 +135,8 @@ class APIServer:
         self.webhooks = WebhookDispatcher(self)
         self.crds = CRDManager(self)
         self.aggregator = Aggregator(self)
+        self.component_endpoints = component_endpoints if component_endpoints is not None else {
+            "scheduler": "http://127.0.0.1:10251/healthz", "controller-manager": "http://127.0.0.1:10252/healthz"}
         from .openapi import OpenAPICache
         self.openapi = OpenAPICache(VERSION["gitVersion"])
         # encryption at rest (--experimental-encryption-provider-config): plural -> PrefixTransformers
@@ -919,14 +945,15 @@ class APIServer:
             ns = rest[1]
             rest = rest[2:]
         plural = rest[0]
+        if plural == "componentstatuses" and group == "" and ns is None:
+            return ("componentstatuses", rest[1] if len(rest) > 1 else None)
         ri = m.BY_PLURAL.get(plural)
-        if ri is None or ri.group != group or plural not in self.caches:
+        aliased = (group, version, plural) in m.ALIASES
+        if ri is None or (ri.group != group and not aliased) or plural not in self.caches:
             if plural == "bindings" and ns:
                 return ("bindings", ns)
             return None
-        if ri.version != version and not (group == "apps" and version in ("v1", "v1beta1", "v1beta2")) \
-                and not (group == "batch" and version in ("v1", "v1beta1", "v2alpha1")) \
-                and not (group == "policy" and version in ("v1beta1", "v1")):
+        if ri.version != version and not aliased:
             return None
         name = rest[1] if len(rest) > 1 else None
         sub = "/".join(rest[2:]) if len(rest) > 2 else ""
@@ -988,6 +1015,12 @@ class APIServer:
                 resp = await self.aggregator.proxy(req, parsed[1])
                 code = resp.status
                 return resp
+            if parsed[0] == "componentstatuses":
+                resource = "componentstatuses"
+                self._authorize(user, "get" if parsed[1] else "list", None, "componentstatuses", "", parsed[1] or "", "", p)
+                resp = await self._component_statuses(parsed[1])
+                code = resp.status
+                return resp
             if parsed[0] == "bindings":
                 resource, sub = "pods", "binding"
                 body = codec.loads(req.body)
@@ -997,6 +1030,18 @@ class APIServer:
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             ri, ns, name, sub, watch = parsed
             resource = ri.plural
+            served = _requested_gv(p)
+            if served != ri.group_version:
+                # served under an alias group/version: store canonical, answer in the requested one
+                req.served_gv = served
+                if req.body and req.body[:1] == b"{":
+                    try:
+                        bo = codec.loads(req.body)
+                        if bo.get("apiVersion") == served:
+                            bo["apiVersion"] = ri.group_version
+                            req.body = codec.dumpb(bo)
+                    except ValueError:
+                        pass
             is_watch = watch or req.query.get("watch") in ("true", "1")
             mutating = verb not in ("GET", "HEAD")
             # max-in-flight (WithMaxInFlightLimit): non-watch requests only
@@ -1047,6 +1092,9 @@ class APIServer:
                     else:
                         self.inflight -= 1
             code = getattr(resp, "status", 200)
+            gv = getattr(req, "served_gv", None)
+            if gv and isinstance(resp, Response) and resp.body[:1] == b"{" and code < 300:
+                resp = Response(resp.status, _rewrite_gv(resp.body, ri.group_version, gv), resp.content_type)
             if codec.PROTOBUF in req.headers.get("accept", "") and isinstance(resp, Response) and resp.body[:1] == b"{":
                 from ..api import protobuf as pb
                 obj = codec.loads(resp.body)
@@ -1347,6 +1395,41 @@ class APIServer:
                 uw.close()
         return StreamResponse(relay, "application/vnd.kamd.stream")
 
+    async def _component_statuses(self, name=None):
+        """`pkg/registry/core/componentstatus/rest.go`: probe the scheduler, the controller
+        manager and the store; one ComponentStatus each with a Healthy condition."""
+        from ..client.http import HTTPClient
+
+        async def probe(comp, url):
+            if url is None:
+                try:
+                    ok = self.store is not None
+                    msg = '{"health": "true"}' if ok else "no store"
+                except Exception as e:  # noqa: BLE001
+                    ok, msg = False, str(e)
+            else:
+                base, _, path = url.partition("/healthz")
+                c = HTTPClient(base, timeout=1.0)
+                try:
+                    st, body = await asyncio.wait_for(c.request("GET", "/healthz" + path), 1.5)
+                    ok, msg = st == 200, body.decode(errors="replace")
+                except (OSError, ConnectionError, asyncio.TimeoutError, ValueError) as e:
+                    ok, msg = False, f"Get {url}: {e or type(e).__name__}"
+                finally:
+                    await c.close()
+            cond = {"type": "Healthy", "status": "True" if ok else "False", "message": msg if ok else ""}
+            if not ok:
+                cond["error"] = msg
+            return {"kind": "ComponentStatus", "apiVersion": "v1", "metadata": {"name": comp}, "conditions": [cond]}
+        targets = dict(self.component_endpoints)
+        targets.setdefault("etcd-0", None)
+        if name is not None:
+            if name not in targets:
+                raise APIError(404, "NotFound", f'componentstatuses "{name}" not found')
+            return _json(200, await probe(name, targets[name]))
+        items = await asyncio.gather(*(probe(k, v) for k, v in sorted(targets.items())))
+        return _json(200, {"kind": "ComponentStatusList", "apiVersion": "v1", "metadata": {}, "items": list(items)})
+
     async def _pod_log(self, ns, name, q):
         _, addr, port = self._kubelet_of(ns, name)
         from ..client.http import HTTPClient
@@ -1363,29 +1446,29 @@ class APIServer:
         if kind == "api":
             return _json(200, {"kind": "APIVersions", "versions": ["v1"],
                                "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": "127.0.0.1"}]})
-        groups = {}
-        for ri in m.RESOURCES:
-            if ri.group:
-                groups.setdefault(ri.group, set()).add(ri.version)
+        groups = {g: set(vs) for g, vs in m.served_versions().items() if g}
         for g, vs in self.aggregator.groups().items():
             groups.setdefault(g, set()).update(vs)
+
+        def ordered(vs):   # preferred (highest priority) first, as the reference lists them
+            return sorted(vs, key=m.version_priority, reverse=True)
         if kind == "apis":
             return _json(200, {"kind": "APIGroupList", "apiVersion": "v1", "groups": [
-                {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in sorted(vs)],
-                 "preferredVersion": {"groupVersion": f"{g}/{sorted(vs)[-1]}", "version": sorted(vs)[-1]}}
+                {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in ordered(vs)],
+                 "preferredVersion": {"groupVersion": f"{g}/{ordered(vs)[0]}", "version": ordered(vs)[0]}}
                 for g, vs in sorted(groups.items())]})
         if kind == "group":
             g = parsed[2]
             if g not in groups:
                 raise APIError(404, "NotFound", f"group {g} not found")
-            vs = sorted(groups[g])
+            vs = ordered(groups[g])
             return _json(200, {"kind": "APIGroup", "apiVersion": "v1", "name": g,
                                "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in vs],
-                               "preferredVersion": {"groupVersion": f"{g}/{vs[-1]}", "version": vs[-1]}})
+                               "preferredVersion": {"groupVersion": f"{g}/{vs[0]}", "version": vs[0]}})
         group, version = parsed[2], parsed[3]
         res = []
         for ri in m.RESOURCES:
-            if ri.group != group or ri.version != version:
+            if not ((ri.group == group and ri.version == version) or (group, version, ri.plural) in m.ALIASES):
                 continue
             verbs = ["create", "delete", "deletecollection", "get", "list", "patch", "update", "watch"]
             res.append({"name": ri.plural, "singularName": "", "namespaced": ri.namespaced, "kind": ri.kind,
@@ -1401,6 +1484,9 @@ class APIServer:
                     res.append({"name": f"pods/{sr}", "singularName": "", "namespaced": True,
                                 "kind": "PodExecOptions" if sr != "portforward" else "PodPortForwardOptions",
                                 "verbs": ["create", "get"]})
+        if group == "" and version == "v1":
+            res.append({"name": "componentstatuses", "singularName": "", "namespaced": False, "kind": "ComponentStatus",
+                        "verbs": ["get", "list"], "shortNames": ["cs"]})
         if not res:
             raise APIError(404, "NotFound", f"{group}/{version} not found")
         gv = f"{group}/{version}" if group else version

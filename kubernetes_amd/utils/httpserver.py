@@ -23,7 +23,7 @@ REASONS = {
 
 
 class Request:
-    __slots__ = ("method", "path", "raw_path", "query", "qs", "headers", "body", "transport", "user", "info")
+    __slots__ = ("method", "path", "raw_path", "query", "qs", "headers", "body", "transport", "user", "info", "served_gv")
 
     def __init__(self, method, target, headers, body, transport):
         self.method = method
@@ -40,6 +40,7 @@ class Request:
         self.transport = transport
         self.user = None
         self.info = None
+        self.served_gv = None
 
 
 class Response:
