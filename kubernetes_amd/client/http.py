@@ -88,6 +88,14 @@ class HTTPClient:
         self.timeout = timeout
         self._closed = False
 
+    def set_ssl_context(self, ctx):
+        """Swap the TLS context (client-certificate rotation): idle connections made with the
+        old credential are closed; new connections present the new certificate."""
+        self.ssl = ctx
+        idle, self._idle = self._idle, []
+        for c in idle:
+            c.close()
+
     async def _open(self):
         if self.unix:
             r, w = await asyncio.open_unix_connection(self.sock_path, limit=1 << 24)

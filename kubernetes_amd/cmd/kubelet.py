@@ -56,6 +56,10 @@ def main(argv=None):
     ap.add_argument("--minimum-container-ttl-duration", type=float, default=0.0)
     ap.add_argument("--maximum-dead-containers-per-container", type=int, default=1)
     ap.add_argument("--maximum-dead-containers", type=int, default=-1)
+    ap.add_argument("--rotate-certificates", action="store_true",
+                    help="rotate the kubelet client certificate (CSR) as it approaches expiry")
+    ap.add_argument("--config", default=None, help="KubeletConfiguration file (kubeletconfig/v1alpha1)")
+    ap.add_argument("--dynamic-config-dir", default=None, help="enable Dynamic Kubelet Config; checkpoints live here")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -93,12 +97,30 @@ def main(argv=None):
         container_gc = {"min_age": a.minimum_container_ttl_duration,
                         "max_per_pod_container": a.maximum_dead_containers_per_container,
                         "max_containers": a.maximum_dead_containers}
-        kl = Kubelet(client, a.hostname_override, rt, dm, pods=a.max_pods, labels=labels,
-                     node_status_update_frequency=a.node_status_update_frequency, http_port=a.port, address=a.address,
-                     root_dir=a.root_dir, cpu_manager_policy=a.cpu_manager_policy, reserved_cpus=a.reserved_cpus,
-                     pod_manifest_path=a.pod_manifest_path, eviction_hard=a.eviction_hard, image_gc=image_gc,
-                     network_plugin=plugin, dns=dns, hostports=hostports, container_gc=container_gc)
+        extra = {}
+        if a.config:
+            from ..kubelet.kubeletconfig import load, to_kwargs
+            with open(a.config) as f:
+                extra = to_kwargs(load(f.read()))
+        if a.dynamic_config_dir:
+            from ..kubelet.kubeletconfig import startup_checkpoint, to_kwargs
+            ck = startup_checkpoint(a.dynamic_config_dir)   # restart path: start on the assigned checkpoint
+            if ck is not None:
+                extra.update(to_kwargs(ck))
+            extra["dynamic_config_dir"] = a.dynamic_config_dir
+        base = dict(pods=a.max_pods, node_status_update_frequency=a.node_status_update_frequency,
+                    cpu_manager_policy=a.cpu_manager_policy, eviction_hard=a.eviction_hard, dns=dns,
+                    pod_manifest_path=a.pod_manifest_path, container_gc=container_gc)
+        base.update(extra)
+        kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
+                     http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,
+                     image_gc=image_gc, network_plugin=plugin, hostports=hostports, **base)
         await kl.run()
+        if a.rotate_certificates and a.kubeconfig:
+            import asyncio
+            from ..kubelet.certificate import CertificateRotator
+            rot = CertificateRotator(a.kubeconfig, a.hostname_override, os.path.join(a.root_dir, "pki"), client)
+            kl._tasks.append(asyncio.ensure_future(rot.run()))
         print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port})", flush=True)
         return kl
 

@@ -84,7 +84,7 @@ class Kubelet:
                  root_dir=None, cpu_manager_policy="none", cpu_topology=None, reserved_cpus=1,
                  pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0,
                  image_service=None, image_gc=None, image_backoff=10.0, network_plugin=None, dns=None,
-                 hostports=None, container_gc=None, crash_backoff=(10.0, 300.0)):
+                 hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None):
         self.client = client
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
@@ -93,6 +93,10 @@ class Kubelet:
         self.container_gc = container_gc     # ContainerGC policy dict or None
         self.crash_backoff = crash_backoff   # (initial, max) restart back-off, kubelet.go backOffPeriod/MaxContainerBackOff
         self.pod_cidr = None
+        self.dynamic = None
+        if dynamic_config_dir:
+            from .kubeletconfig import DynamicConfig
+            self.dynamic = DynamicConfig(self, dynamic_config_dir)
         self.pod_manifest_path = pod_manifest_path
         self.static_pods = None
         self.eviction = None
@@ -289,6 +293,8 @@ class Kubelet:
               "daemonEndpoints": {"kubeletEndpoint": {"Port": self.http_port or 0}},
               "nodeInfo": {"kubeletVersion": "v1.9.0-amd.0", "containerRuntimeVersion": f"{self.runtime.name}://1.0",
                            "operatingSystem": "linux", "architecture": "amd64", "machineID": self.node_name}}
+        if self.dynamic is not None:
+            st["conditions"].append(dict(self.dynamic.condition, lastHeartbeatTime=now, lastTransitionTime=now))
         if ers:
             st["extendedResources"] = ers
         return st
@@ -323,8 +329,40 @@ class Kubelet:
             except (ConnectionError, OSError):
                 await asyncio.sleep(0.2)
 
+    def apply_config(self, cfg):
+        """Hot-apply a (dynamic) KubeletConfiguration; None restores the local configuration."""
+        if not hasattr(self, "_local_config"):
+            self._local_config = {"pods": self.capacity["pods"], "status_freq": self.status_freq, "eviction": self.eviction,
+                                  "container_gc": self.container_gc, "dns": self.dns,
+                                  "image_gc": (self.image_gc.high, self.image_gc.low) if self.image_gc else None}
+        if cfg is None:
+            lc = self._local_config
+            self.capacity["pods"], self.status_freq = lc["pods"], lc["status_freq"]
+            self.eviction, self.container_gc, self.dns = lc["eviction"], lc["container_gc"], lc["dns"]
+            if self.image_gc is not None and lc["image_gc"]:
+                self.image_gc.high, self.image_gc.low = lc["image_gc"]
+            self._status_dirty.set()
+            return
+        from .kubeletconfig import eviction_string, to_kwargs
+        kw = to_kwargs(cfg)
+        self.capacity["pods"] = str(kw["pods"])
+        self.status_freq = kw["node_status_update_frequency"]
+        self.container_gc = kw["container_gc"]
+        if "dns" in kw:
+            self.dns = kw["dns"]
+        if self.image_gc is not None:
+            self.image_gc.high = int(cfg["imageGCHighThresholdPercent"])
+            self.image_gc.low = int(cfg["imageGCLowThresholdPercent"])
+        ev = eviction_string(cfg.get("evictionHard"))
+        if ev:
+            from .eviction import EvictionManager, parse_thresholds
+            self.eviction = EvictionManager(parse_thresholds(ev), getattr(self.eviction, "signals_fn", None))
+        self._status_dirty.set()
+
     def _observe_pod_cidr(self, node):
         """`updatePodCIDR`: hand the node's spec.podCIDR to the network plugin once it appears."""
+        if self.dynamic is not None:
+            spawn(self.dynamic.observe_node(node))
         cidr = ((node or {}).get("spec") or {}).get("podCIDR")
         if cidr and cidr != self.pod_cidr:
             self.pod_cidr = cidr

@@ -55,6 +55,8 @@ def _L():
         L.kc_verify_cert.restype = _l
         L.kc_cert_not_after.argtypes = [_c]
         L.kc_cert_not_after.restype = _l
+        L.kc_cert_not_before.argtypes = [_c]
+        L.kc_cert_not_before.restype = _l
         L.kc_sign.argtypes = [_c, _c, _l, _b, _l]
         L.kc_sign.restype = _l
         L.kc_public_key.argtypes = [_c, _b, _l]
@@ -200,6 +202,10 @@ def verify_cert(cert_pem: str, ca_pem: str) -> tuple[bool, str]:
     out = ctypes.create_string_buffer(1024)
     rc = _L().kc_verify_cert(_e(cert_pem), _e(ca_pem), out, 1024)
     return rc == 0, out.value.decode(errors="replace")
+
+
+def cert_not_before(pem: str) -> int:
+    return _L().kc_cert_not_before(_e(pem))
 
 
 def cert_not_after(pem: str) -> int:

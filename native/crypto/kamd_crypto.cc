@@ -447,6 +447,16 @@ long kc_cert_not_after(const char* pem) {
   return r;
 }
 
+long kc_cert_not_before(const char* pem) {
+  X509* c = load_cert(pem);
+  if (!c) return -1;
+  struct tm t;
+  long r = -1;
+  if (ASN1_TIME_to_tm(X509_get0_notBefore(c), &t) == 1) r = (long)timegm(&t);
+  X509_free(c);
+  return r;
+}
+
 // ---------------------------------------------------------------- signatures (JWT RS256 / ES256)
 // Sign `data` with the private key (RSA: PKCS#1 v1.5 SHA-256; EC: ECDSA SHA-256, DER). Returns the
 // signature length written to out, or -1.

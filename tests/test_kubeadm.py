@@ -132,6 +132,15 @@ def test_init_join_tls_bootstrap(run, tmp_path):
             from kubernetes_amd.client.rest import APIStatusError
             with pytest.raises(APIStatusError):             # NodeRestriction: cannot touch another node
                 await n.patch("nodes", "master-0", {"metadata": {"labels": {"x": "y"}}})
+            # client-certificate rotation over the current credential (selfnodeclient CSR)
+            from kubernetes_amd.kubelet.certificate import CertificateRotator
+            rot = CertificateRotator(conf, "gpu-0", str(tmp_path / "node" / "pki"), n)
+            assert not await rot.maybe_rotate()              # fresh certificate: not due
+            assert await rot.maybe_rotate(now=crypto.cert_not_after(cert) - 60)
+            kc2, _ = clientcmd.load(conf)
+            cert2 = base64.b64decode(kc2["users"][0]["user"]["client-certificate-data"]).decode()
+            assert cert2 != cert and crypto.cert_subject(cert2) == ("system:node:gpu-0", ["system:nodes"])
+            assert (await n.get("nodes", "gpu-0"))["metadata"]["name"] == "gpu-0"   # live client on the new cert
             await n.close()
 
             # kubeadm token create/list/delete through the CLI (its own event loop, in a thread)
