@@ -29,7 +29,7 @@ def main(argv=None):
     async def start():
         rt = ProcessRuntime(os.path.join(a.root_dir, "containers")) if a.runtime == "process" else StubRuntime()
         os.makedirs(os.path.dirname(os.path.abspath(a.listen)), exist_ok=True)
-        srv = await CRIServer(rt, a.listen).start()
+        srv = await CRIServer(rt, a.listen, checkpoint_dir=os.path.join(a.root_dir, "sandbox")).start()
         print(f"kamd-cri serving CRI v1alpha1 ({rt.name} runtime) on unix://{a.listen}, "
               f"streaming on 127.0.0.1:{srv.streaming.port}", flush=True)
         return srv

@@ -56,6 +56,8 @@ def main(argv=None):
     ap.add_argument("--minimum-container-ttl-duration", type=float, default=0.0)
     ap.add_argument("--maximum-dead-containers-per-container", type=int, default=1)
     ap.add_argument("--maximum-dead-containers", type=int, default=-1)
+    ap.add_argument("--bootstrap-checkpoint-path", default=None,
+                    help="checkpoint pods annotated node.kubernetes.io/bootstrap-checkpoint=true here")
     ap.add_argument("--rotate-certificates", action="store_true",
                     help="rotate the kubelet client certificate (CSR) as it approaches expiry")
     ap.add_argument("--config", default=None, help="KubeletConfiguration file (kubeletconfig/v1alpha1)")
@@ -110,7 +112,8 @@ def main(argv=None):
             extra["dynamic_config_dir"] = a.dynamic_config_dir
         base = dict(pods=a.max_pods, node_status_update_frequency=a.node_status_update_frequency,
                     cpu_manager_policy=a.cpu_manager_policy, eviction_hard=a.eviction_hard, dns=dns,
-                    pod_manifest_path=a.pod_manifest_path, container_gc=container_gc)
+                    pod_manifest_path=a.pod_manifest_path, container_gc=container_gc,
+                    bootstrap_checkpoint_path=a.bootstrap_checkpoint_path)
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,

@@ -248,6 +248,10 @@ async def splice(r1, w1, r2, w2):
             pass
 
 
+def _ck_key(sid):
+    return sid.replace("://", "_").replace("/", "_")
+
+
 def _pairs(d):
     return {k: v for k, v in (d or {}).items()}
 
@@ -255,9 +259,13 @@ def _pairs(d):
 class CRIServer:
     """Serves RuntimeService + ImageService for `runtime` on `socket_path`."""
 
-    def __init__(self, runtime, socket_path, image_resolver=None):
+    def __init__(self, runtime, socket_path, image_resolver=None, checkpoint_dir=None):
         self.rt = runtime
         self.path = socket_path
+        self.checkpoints = None
+        if checkpoint_dir:
+            from ..utils.checkpoint import CheckpointManager
+            self.checkpoints = CheckpointManager(checkpoint_dir)
         self.images = ImageStore(image_resolver or (stub_image_resolver if runtime.name == "stub" else host_image_resolver))
         self.sandboxes: dict[str, dict] = {}
         self.cmeta: dict[str, dict] = {}
@@ -265,9 +273,27 @@ class CRIServer:
         self.server = None
         self.pod_cidr = ""
 
+    def _restore_checkpoints(self):
+        """Sandboxes checkpointed by a previous run come back NOTREADY (their processes are gone),
+        so the kubelet sees them, tears their network down and removes them
+        (`docker_sandbox.go` ListPodSandbox over checkpoints)."""
+        if self.checkpoints is None:
+            return
+        for sid, ck in self.checkpoints.load_all():
+            if sid in self.sandboxes:
+                continue
+            md = A.MSG["PodSandboxMetadata"](name=ck.get("name", ""), namespace=ck.get("namespace", ""),
+                                             uid=ck.get("uid", ""), attempt=0)
+            self.sandboxes[sid] = {"pod": {"metadata": {"name": ck.get("name"), "namespace": ck.get("namespace"),
+                                                        "uid": ck.get("uid")}, "spec": {}},
+                                   "metadata": md, "labels": ck.get("labels") or {}, "annotations": {},
+                                   "created": ck.get("created", 0.0), "state": A.SANDBOX_NOTREADY,
+                                   "ip": (ck.get("data") or {}).get("ip", ""), "restored": True}
+
     async def start(self):
         if os.path.exists(self.path):
             os.unlink(self.path)
+        self._restore_checkpoints()
         await self.streaming.start()
         self.server = grpc.aio.server()
         self.server.add_generic_rpc_handlers((generic_handler(A.RUNTIME_SERVICE, A.RUNTIME_METHODS, self),
@@ -297,6 +323,14 @@ class CRIServer:
         sid = await self.rt.run_pod_sandbox(pod, ann)
         self.sandboxes[sid] = {"pod": pod, "metadata": c.metadata, "labels": _pairs(c.labels), "annotations": ann,
                                "created": time.time(), "state": A.SANDBOX_READY, "ip": ann.get("kubernetes-amd.io/pod-ip", "")}
+        if self.checkpoints is not None:
+            ports = [{"protocol": pm.protocol, "container_port": pm.container_port, "host_port": pm.host_port}
+                     for pm in c.port_mappings]
+            self.checkpoints.create(_ck_key(sid), {
+                "version": "v1", "name": c.metadata.name, "namespace": c.metadata.namespace, "uid": c.metadata.uid,
+                "labels": _pairs(c.labels), "created": self.sandboxes[sid]["created"],
+                "data": {"port_mappings": ports, "host_network": bool((pod.get("spec") or {}).get("hostNetwork")),
+                         "ip": self.sandboxes[sid]["ip"]}})
         return A.MSG["RunPodSandboxResponse"](pod_sandbox_id=sid)
 
     def _sandbox(self, sid, ctx=None):
@@ -307,14 +341,17 @@ class CRIServer:
 
     async def StopPodSandbox(self, req, ctx):
         sb = self.sandboxes.get(req.pod_sandbox_id)
-        if sb is not None:
+        if sb is not None and not sb.get("restored"):
             await self.rt.stop_pod_sandbox(req.pod_sandbox_id)
             sb["state"] = A.SANDBOX_NOTREADY
         return A.MSG["StopPodSandboxResponse"]()
 
     async def RemovePodSandbox(self, req, ctx):
+        if self.checkpoints is not None:
+            self.checkpoints.remove(_ck_key(req.pod_sandbox_id))
         if req.pod_sandbox_id in self.sandboxes:
-            await self.rt.remove_pod_sandbox(req.pod_sandbox_id)
+            if not self.sandboxes[req.pod_sandbox_id].get("restored"):
+                await self.rt.remove_pod_sandbox(req.pod_sandbox_id)
             self.sandboxes.pop(req.pod_sandbox_id, None)
             for cid in [k for k, m in self.cmeta.items() if m["sandbox"] == req.pod_sandbox_id]:
                 self.cmeta.pop(cid, None)

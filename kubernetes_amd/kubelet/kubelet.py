@@ -47,6 +47,9 @@ log = logging.getLogger("kubelet")
 _ip_counter = itertools.count(2)
 
 
+BOOTSTRAP_CHECKPOINT = "node.kubernetes.io/bootstrap-checkpoint"
+
+
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
                  "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
@@ -84,7 +87,8 @@ class Kubelet:
                  root_dir=None, cpu_manager_policy="none", cpu_topology=None, reserved_cpus=1,
                  pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0,
                  image_service=None, image_gc=None, image_backoff=10.0, network_plugin=None, dns=None,
-                 hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None):
+                 hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
+                 bootstrap_checkpoint_path=None):
         self.client = client
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
@@ -93,6 +97,10 @@ class Kubelet:
         self.container_gc = container_gc     # ContainerGC policy dict or None
         self.crash_backoff = crash_backoff   # (initial, max) restart back-off, kubelet.go backOffPeriod/MaxContainerBackOff
         self.pod_cidr = None
+        self.pod_checkpoints = None
+        if bootstrap_checkpoint_path:
+            from ..utils.checkpoint import CheckpointManager
+            self.pod_checkpoints = CheckpointManager(bootstrap_checkpoint_path)
         self.dynamic = None
         if dynamic_config_dir:
             from .kubeletconfig import DynamicConfig
@@ -179,6 +187,10 @@ class Kubelet:
         self.dm.add_capacity_listener(lambda r: self._status_dirty.set())
         if self.register:
             await self._register_node()
+        if self.pod_checkpoints is not None:
+            restored = self._restore_checkpointed_pods()
+            if restored:
+                log.info("started %d pods from bootstrap checkpoints", restored)
         self.informer.add_handler(self._on_add, self._on_update, self._on_delete)
         self.informer.start()
         self._tasks.append(asyncio.ensure_future(self._node_status_loop()))
@@ -419,9 +431,32 @@ class Kubelet:
 
     def _dispatch(self, pod, op):
         uid = pod["metadata"]["uid"]
+        if self.pod_checkpoints is not None:
+            self._checkpoint_pod(pod, op)
         self._pending[uid] = (pod, op)
         if uid not in self._workers:
             self._workers[uid] = asyncio.ensure_future(self._worker(uid))
+
+    def _checkpoint_pod(self, pod, op):
+        """`pkg/kubelet/checkpoint`: pods annotated `node.kubernetes.io/bootstrap-checkpoint: "true"`
+        are kept on disk so a restarting kubelet can run them before the API is reachable
+        (self-hosted control planes)."""
+        key = "Pod" + pod["metadata"]["uid"]
+        ann = (pod["metadata"].get("annotations") or {}).get(BOOTSTRAP_CHECKPOINT)
+        if op == "delete" or ann != "true" or core.pod_is_terminal(pod):
+            self.pod_checkpoints.remove(key)
+        else:
+            self.pod_checkpoints.create(key, {"version": "v1", "pod": pod})
+
+    def _restore_checkpointed_pods(self):
+        n = 0
+        for _, ck in self.pod_checkpoints.load_all():
+            pod = ck.get("pod")
+            if pod and (pod.get("spec") or {}).get("nodeName") in (None, "", self.node_name):
+                pod.setdefault("spec", {})["nodeName"] = self.node_name
+                self._dispatch(pod, "add")
+                n += 1
+        return n
 
     def _on_container_exit(self, pod_uid, cid):
         st = self.pods.get(pod_uid)
