@@ -32,6 +32,8 @@ def _parser():
     ap.add_argument("--port", type=int, default=8080)
     ap.add_argument("--port-file", default=None, help="write the bound port here (use with --port 0)")
     ap.add_argument("--admission-control", default=None, help="comma separated ordered plugin list")
+    ap.add_argument("--admission-control-config-file", default=None,
+                    help="AdmissionConfiguration: plugins[{name, path | configuration}]")
     ap.add_argument("--authorization-mode", default="AlwaysAllow")
     ap.add_argument("--token-auth-file", default=None)
     ap.add_argument("--storage-media-type", default=codec.JSON)
@@ -72,6 +74,24 @@ def _parser():
     ap.add_argument("--audit-webhook-batch-max-wait", type=float, default=1.0)
     ap.add_argument("-v", type=int, default=0)
     return ap
+
+
+def load_admission_config(path):
+    """`apiserver.k8s.io/v1alpha1 AdmissionConfiguration` → {plugin name: config dict}
+    (`staging/src/k8s.io/apiserver/pkg/admission/config.go`: `configuration` inline or `path`
+    to a file, relative to the admission config's directory)."""
+    import yaml
+    with open(path) as f:
+        doc = yaml.safe_load(f) or {}
+    out = {}
+    for p in doc.get("plugins") or ():
+        cfg = p.get("configuration")
+        if cfg is None and p.get("path"):
+            fp = p["path"] if os.path.isabs(p["path"]) else os.path.join(os.path.dirname(os.path.abspath(path)), p["path"])
+            with open(fp) as f:
+                cfg = yaml.safe_load(f)
+        out[p["name"]] = cfg or {}
+    return out
 
 
 # flags the multi-worker supervisor sets itself for each worker
@@ -181,6 +201,7 @@ def main(argv=None):
         if store is None:
             store = MVCCStore(wal_path=a.etcd_wal)
         plugins = a.admission_control.split(",") if a.admission_control else None
+        adm_cfg = load_admission_config(a.admission_control_config_file) if a.admission_control_config_file else None
         audit = None
         if a.audit_log_path or a.audit_webhook_config_file:
             from ..apiserver.audit import AuditLogger, Policy, WebhookBackend
@@ -194,7 +215,7 @@ def main(argv=None):
                     "username_claim": a.oidc_username_claim, "username_prefix": a.oidc_username_prefix,
                     "groups_claim": a.oidc_groups_claim, "groups_prefix": a.oidc_groups_prefix, "ca_file": a.oidc_ca_file,
                     "required_claims": dict(x.split("=", 1) for x in a.oidc_required_claim)}
-        s = APIServer(store=store, admission_plugins=plugins, token_file=a.token_auth_file,
+        s = APIServer(store=store, admission_plugins=plugins, admission_config=adm_cfg, token_file=a.token_auth_file,
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
                       max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size,

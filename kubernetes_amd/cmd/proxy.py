@@ -26,9 +26,12 @@ def main(argv=None):
     ap.add_argument("--fake-dataplane", action="store_true",
                     help="record iptables/IPVS state without touching the kernel (kubemark hollow proxy)")
     ap.add_argument("--token", default=None)
+    ap.add_argument("--config", default=None, help="KubeProxyConfiguration file (kubeproxy.config.k8s.io/v1alpha1)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
+    if a.config:
+        apply_config_file(a, a.config)
 
     async def start():
         iptables = ipvs = None
@@ -53,6 +56,41 @@ def main(argv=None):
         return ps
 
     run_until_signal(start)
+
+
+def _dur(v):
+    from ..kubelet.kubeletconfig import parse_duration
+    return parse_duration(v)
+
+
+def apply_config_file(a, path):
+    """`pkg/proxy/apis/kubeproxyconfig` KubeProxyConfiguration → flag values (the file wins,
+    as `--config` does in the reference)."""
+    import yaml
+    with open(path) as f:
+        c = yaml.safe_load(f) or {}
+    if c.get("kind", "KubeProxyConfiguration") != "KubeProxyConfiguration":
+        raise SystemExit(f"kube-proxy: {path}: expected kind KubeProxyConfiguration")
+    a.proxy_mode = c.get("mode") or a.proxy_mode
+    a.cluster_cidr = c.get("clusterCIDR", a.cluster_cidr)
+    a.bind_address = c.get("bindAddress", a.bind_address)
+    a.hostname_override = c.get("hostnameOverride") or a.hostname_override
+    ipt = c.get("iptables") or {}
+    a.masquerade_all = ipt.get("masqueradeAll", a.masquerade_all)
+    if "syncPeriod" in ipt:
+        a.iptables_sync_period = _dur(ipt["syncPeriod"])
+    if "minSyncPeriod" in ipt:
+        a.iptables_min_sync_period = _dur(ipt["minSyncPeriod"])
+    ipvs = c.get("ipvs") or {}
+    a.ipvs_scheduler = ipvs.get("scheduler") or a.ipvs_scheduler
+    for key, attr in (("healthzBindAddress", "healthz_port"), ("metricsBindAddress", "metrics_port")):
+        v = c.get(key)
+        if v and ":" in str(v):
+            setattr(a, attr, int(str(v).rsplit(":", 1)[1]))
+    kc = (c.get("clientConnection") or {}).get("kubeconfig")
+    if kc:
+        a.kubeconfig = kc
+    return a
 
 
 if __name__ == "__main__":

@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import argparse
 import asyncio
-import json
 import signal
 import subprocess
 import sys
@@ -39,6 +38,10 @@ def _parser():
     ap.add_argument("--shards", type=int, default=1, help="run N parallel scheduler shard processes")
     ap.add_argument("--shard-index", type=int, default=0)
     ap.add_argument("--shard-count", type=int, default=1)
+    ap.add_argument("--config", default=None, help="KubeSchedulerConfiguration file")
+    ap.add_argument("--algorithm-provider", default=None, help="DefaultProvider | ClusterAutoscalerProvider")
+    ap.add_argument("--policy-configmap", default=None, help="ConfigMap holding the Policy under policy.cfg")
+    ap.add_argument("--policy-configmap-namespace", default="kube-system")
     ap.add_argument("-v", type=int, default=0)
     return ap
 
@@ -79,23 +82,38 @@ def main(argv=None):
     setup_logging(a.v)
     if a.shards > 1:
         sys.exit(supervise(argv, a.shards))
-    preds = prios = None
-    extenders = []
-    if a.policy_config_file:
-        from ..scheduler.extender import HTTPExtender
-        with open(a.policy_config_file) as f:
-            pol = json.load(f)
-        preds = [p["name"] for p in pol.get("predicates") or []] or None
-        if pol.get("priorities") is not None:
-            prios = {p["name"]: int(p.get("weight", 1)) for p in pol["priorities"]}
-        extenders = [HTTPExtender.from_config(e) for e in pol.get("extenders") or []]
+    from ..scheduler import policy as SP
+    if a.config:
+        with open(a.config) as f:
+            cc = SP.load_component_config(f.read())
+        src = cc.get("algorithmSource") or {}
+        pol = src.get("policy") or {}
+        a.algorithm_provider = src.get("provider") or a.algorithm_provider
+        a.policy_config_file = ((pol.get("file") or {}).get("path")) or a.policy_config_file
+        if pol.get("configMap"):
+            a.policy_configmap = pol["configMap"].get("name")
+            a.policy_configmap_namespace = pol["configMap"].get("namespace", "kube-system")
+        a.scheduler_name = cc.get("schedulerName", a.scheduler_name)
+        a.leader_elect = (cc.get("leaderElection") or {}).get("leaderElect", a.leader_elect)
+        conn = cc.get("clientConnection") or {}
+        a.kubeconfig = conn.get("kubeconfig") or a.kubeconfig
+        a.kube_api_qps = conn.get("qps", a.kube_api_qps)
+        a.disable_preemption = cc.get("disablePreemption", a.disable_preemption)
+        a.percentage_of_nodes_to_score = cc.get("percentageOfNodesToScore", a.percentage_of_nodes_to_score)
+        mb = cc.get("metricsBindAddress")
+        if mb and ":" in mb:
+            a.metrics_port = int(mb.rsplit(":", 1)[1])
 
     async def start():
+        from ..scheduler.extender import HTTPExtender
         if a.kubeconfig:
             from ..client.clientcmd import client_from
             client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
         else:
             client = Client(a.master or "http://127.0.0.1:8080", qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
+        preds, prios, ext_cfgs = await SP.resolve_algorithm(client, a.algorithm_provider, a.policy_config_file,
+                                                            a.policy_configmap, a.policy_configmap_namespace)
+        extenders = [HTTPExtender.from_config(e) for e in ext_cfgs]
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
                       emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,
                       shard_count=a.shard_count, preemption=not a.disable_preemption)
