@@ -24,6 +24,7 @@ COMPONENTS = {
     "amd-smi-exporter": "amd_smi_exporter",
     "hollow-node": "hollow_node", "kubemark": "hollow_node",
     "local-up": "local_up", "local-up-cluster": "local_up",
+    "csi-hostpath": "csi_hostpath",
 }
 
 

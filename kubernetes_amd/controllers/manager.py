@@ -17,6 +17,7 @@ from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleContr
 from .certificates import (BootstrapSignerController, ClusterRoleAggregationController, CSRApprovingController,
                            CSRSigningController, TokenCleanerController, TokensController, TTLController)
 from .podautoscaler import HorizontalController
+from .attachdetach import AttachDetachController, ExternalAttacher
 from .network import NodeIPAMController, ServiceLBController
 from .volume import PersistentVolumeController, PVCProtectionController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
@@ -52,12 +53,14 @@ CONTROLLERS = {
     "pvc-protection": PVCProtectionController,
     "nodeipam": NodeIPAMController,
     "service": ServiceLBController,
+    "attachdetach": AttachDetachController,
+    "csi-attacher": ExternalAttacher,
 }
 
 
 # like ControllersDisabledByDefault: "*" does not start these (name them explicitly, or the
 # command line enables them from --allocate-node-cidrs / --loadbalancer-ip-range)
-DISABLED_BY_DEFAULT = {"nodeipam", "service"}
+DISABLED_BY_DEFAULT = {"nodeipam", "service", "csi-attacher"}
 
 
 def resolve(enabled):

@@ -118,7 +118,8 @@ class Kubelet:
             self.cpu_manager = StaticPolicy(cpu_topology or CPUTopology.discover(), reserved_cpus,
                                             os.path.join(root_dir or tempfile.gettempdir(), f"cpu_manager_state.{node_name}"))
         self.root_dir = root_dir or os.path.join(tempfile.gettempdir(), f"kamd-kubelet-{node_name}")
-        self.volumes = VolumeManager(client, os.path.join(self.root_dir, "pods"))
+        self.volumes = VolumeManager(client, os.path.join(self.root_dir, "pods"), os.path.join(self.root_dir, "plugins"),
+                                     node_name)
         self.probes = ProbeManager(runtime, self._on_readiness, self._on_liveness_failure)
         self.node_name = node_name
         self.runtime = runtime
@@ -523,6 +524,10 @@ class Kubelet:
             if st is not None:
                 await self._kill_pod(st, 0)
                 await self._teardown_network(st)
+                if st.volumes:
+                    await self.volumes.unpublish(st.pod)
+                    self.volumes.teardown(st.pod)
+                    st.volumes = None
                 st.deleted = True
                 self.pods.pop(uid, None)
                 self.by_key.pop(_key(pod), None)
@@ -859,6 +864,7 @@ class Kubelet:
             await self.runtime.remove_pod_sandbox(st.sandbox)
             st.sandbox = None
         if st.volumes:
+            await self.volumes.unpublish(pod)
             self.volumes.teardown(pod)
             st.volumes = None
         try:

@@ -87,9 +87,13 @@ def _resource_field(container, ref):
 
 
 class VolumeManager:
-    def __init__(self, client, root):
+    def __init__(self, client, root, csi_plugins_dir=None, node_name=None, attach_timeout=60.0):
         self.client = client
         self.root = root
+        self.csi_dir = csi_plugins_dir
+        self.node_name = node_name
+        self.attach_timeout = attach_timeout
+        self.csi_published: dict[str, list] = {}     # pod uid -> [(driver, volume handle, target)]
 
     def pod_dir(self, pod):
         return os.path.join(self.root, pod["metadata"]["uid"])
@@ -132,7 +136,7 @@ class VolumeManager:
             elif "downwardAPI" in v:
                 self._downward(pod, v["downwardAPI"], d, node_name, pod_ip)
             elif "persistentVolumeClaim" in v:
-                d = await self._pvc_path(ns, v["persistentVolumeClaim"])
+                d = await self._pvc_path(ns, v["persistentVolumeClaim"], pod, name, node_name)
             elif "projected" in v:
                 for src in v["projected"].get("sources") or ():
                     if "configMap" in src or "secret" in src:
@@ -144,20 +148,75 @@ class VolumeManager:
             out[name] = d
         return out
 
-    async def _pvc_path(self, ns, src):
-        """persistentVolumeClaim -> the bound PV's hostPath / local path
-        (`pkg/volume/util/operationexecutor` mounts the PV the claim is bound to)."""
+    async def _pvc_path(self, ns, src, pod=None, vol_name=None, node_name=None):
+        """persistentVolumeClaim -> the bound PV's hostPath / local path, or a CSI volume
+        published by its driver (`pkg/volume/util/operationexecutor` mounts the PV the claim is
+        bound to)."""
         pvc = await self._get("persistentvolumeclaims", ns, src.get("claimName", ""), False)
         vol = (pvc.get("spec") or {}).get("volumeName")
         if not vol or (pvc.get("status") or {}).get("phase") != "Bound":
             raise VolumeError(f"persistentvolumeclaim {ns}/{src.get('claimName')} is not bound")
         pv = await self._get("persistentvolumes", None, vol, False)
         sp = pv.get("spec") or {}
+        if sp.get("csi"):
+            return await self._csi_publish(pod, vol, sp, node_name or self.node_name)
         path = (sp.get("hostPath") or {}).get("path") or (sp.get("local") or {}).get("path")
         if not path:
             raise VolumeError(f"persistentvolume {vol}: only hostPath / local volumes can be mounted on this node")
         os.makedirs(path, exist_ok=True)
         return path
+
+    async def _csi_publish(self, pod, pv_name, sp, node_name):
+        """`pkg/volume/csi/csi_attacher.go` WaitForAttach (the VolumeAttachment the attach/detach
+        controller created must report `attached`) then `csi_mounter.go` SetUpAt:
+        NodePublishVolume to `<pod dir>/volumes/kubernetes.io~csi/<pv>/mount`."""
+        import asyncio
+        from ..csi import api as CSI
+        from ..csi.driver import CSIClient
+        src = sp["csi"]
+        driver, handle = src["driver"], src["volumeHandle"]
+        va_name = CSI.attachment_name(pv_name, driver, node_name)
+        deadline = asyncio.get_running_loop().time() + self.attach_timeout
+        info = {}
+        while True:
+            try:
+                va = await self.client.get("volumeattachments", va_name)
+                st = va.get("status") or {}
+                if st.get("attached"):
+                    info = st.get("attachmentMetadata") or {}
+                    break
+                if st.get("attachError"):
+                    raise VolumeError(f"attach of {pv_name} failed: {st['attachError'].get('message')}")
+            except APIStatusError as e:
+                if e.code != 404:
+                    raise
+            if asyncio.get_running_loop().time() > deadline:
+                raise VolumeError(f"volume {pv_name} is not attached to {node_name} (VolumeAttachment {va_name})")
+            await asyncio.sleep(0.05)
+        target = os.path.join(self.pod_dir(pod), "volumes", "kubernetes.io~csi", pv_name, "mount")
+        c = CSIClient(CSI.socket_path(self.csi_dir, driver))
+        try:
+            await c.node_publish(handle, target, bool(src.get("readOnly")), info, src.get("volumeAttributes"),
+                                 sp.get("accessModes"), src.get("fsType", ""))
+        except Exception as e:  # noqa: BLE001 - surfaced as a mount failure, retried by the kubelet
+            raise VolumeError(f"NodePublishVolume {handle} via {driver}: {e}")
+        finally:
+            await c.close()
+        self.csi_published.setdefault(pod["metadata"]["uid"], []).append((driver, handle, target))
+        return target
+
+    async def unpublish(self, pod):
+        """CSI NodeUnpublishVolume for every volume published for the pod (TearDownAt)."""
+        from ..csi import api as CSI
+        from ..csi.driver import CSIClient
+        for driver, handle, target in self.csi_published.pop(pod["metadata"]["uid"], []):
+            c = CSIClient(CSI.socket_path(self.csi_dir, driver))
+            try:
+                await c.node_unpublish(handle, target)
+            except Exception:  # noqa: BLE001 - best effort like the reference's unmount retries
+                pass
+            finally:
+                await c.close()
 
     async def _cm_secret(self, ns, v, d):
         if "configMap" in v:
