@@ -97,8 +97,9 @@ def gemm_bf16_nt(a, b, out_fp32=True, alpha=1.0):
 
 
 def set_gemm_path(path: int):
-    """0 = auto (256x256 global_load_lds kernel when M, N % 256 == 0 and K % 64 == 0),
-    1 = always the 128x128 register-staged kernel (A/B comparisons, odd shapes)."""
+    """0 = auto (8-phase 256x256 global_load_lds kernel when M, N % 256 == 0, K % 64 == 0 and
+    K >= 128; the 2-barrier 256x256 kernel for K == 64), 1 = always the 128x128 register-staged
+    kernel, 2 = the 2-barrier 256x256 kernel (A/B comparisons)."""
     load().kamd_gemm_set_path(int(path))
 
 

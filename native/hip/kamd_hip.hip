@@ -23,7 +23,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 static thread_local char g_err[256];
-static int g_gemm_path = 0;   // 0 auto (256-tile glds path when the shape allows), 1 force the 128-tile kernel
+static int g_gemm_path = 0;   // 0 auto (8-phase 256-tile path when the shape allows), 1 force the 128-tile kernel,
+                              // 2 force the 2-barrier 256-tile glds kernel
 
 static int check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
@@ -281,6 +282,183 @@ gemm_bf16_nt_256_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Ou
 }  // namespace gemm256
 
 // ---------------------------------------------------------------------------
+// 8-phase 256x256 path (the default when M, N % 256 == 0, K % 64 == 0, K/64 >= 2).
+// Same tile/wave geometry as gemm256 (8 waves 2M x 4N, 128x64 output per wave), but the K-loop is
+// split into 4 phases per K-tile, one per C-quadrant of the wave (64 rows x 32 cols = 16 MFMAs):
+//   wait(vmcnt) + s_barrier -> ds_read this phase's fragments -> issue ONE half-tile prefetch
+//   (2 x global_load_lds, 16 KiB) -> s_barrier -> lgkmcnt(0) -> setprio(1) MFMAs setprio(0)
+// LDS holds 2 K-tiles x 4 half-tiles, each half holding the rows ONE phase consumes (see below),
+// 128 KiB in ONE dynamic array. A half-tile's slot is refilled for K-tile t+2 as soon as its only
+// ds_read (phase 0/2/0/1 for h0/h1/h2/h3) is behind a barrier, so ~5 half-tiles (10 glds per
+// thread) stay in flight and the waits are counted (vmcnt(10)), never vmcnt(0) in steady state.
+namespace gemm8 {
+using gemm::xcd_remap;
+using gemm::store_out;
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int HALF_BYTES = 128 * BK * 2;          // 16 KiB: 128 rows x 64 bf16
+constexpr int TILE_BYTES = 4 * HALF_BYTES;        // A0 A1 B0 B1
+constexpr int LDS_BYTES = 2 * TILE_BYTES;         // 128 KiB
+typedef __attribute__((address_space(3))) void lds_void;
+
+#define KAMD_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#define KAMD_WAIT_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#define KAMD_BARRIER()                          \
+  do {                                          \
+    asm volatile("" ::: "memory");              \
+    __builtin_amdgcn_s_barrier();               \
+    asm volatile("" ::: "memory");              \
+  } while (0)
+
+template <typename OutT>
+__global__ void __launch_bounds__(THREADS, 1)
+gemm_bf16_nt_8ph_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
+                        int M, int N, int K, int ldc, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int GROUP = 4;
+  const int group_id = t / (GROUP * tiles_n);
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (t % (GROUP * tiles_n)) % gsz;
+  const int tn = (t % (GROUP * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // Half-tiles are split by the PHASE that first reads them, not by contiguous rows:
+  //   h0 = A rows {wr*128 + 0..63}   (quadrant row mq = 0 of both wave rows)   read in phase 0
+  //   h1 = A rows {wr*128 + 64..127} (mq = 1)                                 read in phase 2
+  //   h2 = B rows {wc*64 + 0..31}    (quadrant col nq = 0 of all 4 wave cols) read in phase 0
+  //   h3 = B rows {wc*64 + 32..63}   (nq = 1)                                 read in phase 1
+  // Local row r of a half sits at r*128 B with 16-B slot s holding k-chunk s ^ ((r >> 1) & 7).
+  // Half h of K-tile kt lives in slot ((kt & 1) * 4 + h); each thread stages 2 chunks per half.
+  size_t offA[2], offB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = j * THREADS + tid, r = q >> 3, slot = q & 7;
+    const int kc = slot ^ ((r >> 1) & 7);
+    offA[j] = (size_t)((r >> 6) * 128 + (r & 63)) * K + (kc << 3);
+    offB[j] = (size_t)((r >> 5) * 64 + (r & 31)) * K + (kc << 3);
+  }
+  const u16* half_src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 64) * K, B + (size_t)n0 * K,
+                            B + (size_t)(n0 + 32) * K};
+  auto stage = [&](int kt, int h) {
+    unsigned char* dst = lds + ((kt & 1) * 4 + h) * HALF_BYTES + wid * 1024;
+    const u16* src = half_src[h] + (size_t)kt * BK;
+    const size_t* off = h < 2 ? offA : offB;
+    __builtin_amdgcn_global_load_lds((const void*)(src + off[0]), (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + off[1]), (lds_void*)(dst + THREADS * 16), 16, 0, 0);
+  };
+
+  const int wr = wid >> 2, wc = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4, lsw = (frow >> 1) & 7;
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment registers, one set per quadrant row / column: af[mq][ks][i], bfr[nq][ks][j]
+  bf16x8 af[2][2][4], bfr[2][2][2];
+
+  auto read_a = [&](int kt, int mq) {
+    const unsigned char* base = lds + ((kt & 1) * 4 + mq) * HALF_BYTES + (wr * 64 + frow) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[mq][ks][i] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+  };
+  auto read_b = [&](int kt, int nq) {
+    const unsigned char* base = lds + ((kt & 1) * 4 + 2 + nq) * HALF_BYTES + (wc * 32 + frow) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[nq][ks][j] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+  };
+  auto mma = [&](int mq, int nq) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mq][ks][i], bfr[nq][ks][j], acc[mq][nq][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // Software pipeline: each phase ds_reads the fragments the NEXT phase needs while its MFMAs run
+  // on registers loaded one phase earlier (h3 at p0, h1 at p1, next tile's h0 at p2 and h2 at p3).
+  // Every phase starts with lgkmcnt(0) (the previous phase's reads landed) + counted vmcnt + one
+  // barrier, which both publishes the glds data (RAW) and frees the slots read so far (WAR).
+  // Tile u+2's halves are issued one per phase (h0 h2 h3 h1 at p0..p3) into tile u's slots.
+  const int nt = K / BK;   // >= 2 (checked by the launcher)
+  stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+  stage(1, 0); stage(1, 2); stage(1, 3); stage(1, 1);
+  KAMD_WAIT_VM(12);                    // h0(0), h2(0) landed (6 half-tiles may still fly)
+  KAMD_BARRIER();
+  read_a(0, 0);
+  read_b(0, 0);
+  for (int kt = 0; kt < nt; ++kt) {
+    const bool far = kt + 2 < nt, near = kt + 1 < nt;
+    // p0: MFMA (0,0); read h3(kt) -> b1; issue h0(kt+2)
+    KAMD_WAIT_LGKM0();
+    if (near) KAMD_WAIT_VM(10); else KAMD_WAIT_VM(0);
+    KAMD_BARRIER();
+    read_b(kt, 1);
+    if (far) stage(kt + 2, 0);
+    mma(0, 0);
+    // p1: MFMA (0,1); read h1(kt) -> a1; issue h2(kt+2)
+    KAMD_WAIT_LGKM0();
+    if (far) KAMD_WAIT_VM(10); else KAMD_WAIT_VM(0);
+    KAMD_BARRIER();
+    read_a(kt, 1);
+    if (far) stage(kt + 2, 2);
+    mma(0, 1);
+    // p2: MFMA (1,0); read h0(kt+1) -> a0; issue h3(kt+2)
+    KAMD_WAIT_LGKM0();
+    if (far) KAMD_WAIT_VM(10); else KAMD_WAIT_VM(0);
+    KAMD_BARRIER();
+    if (near) read_a(kt + 1, 0);
+    if (far) stage(kt + 2, 3);
+    mma(1, 0);
+    // p3: MFMA (1,1); read h2(kt+1) -> b0; issue h1(kt+2)
+    KAMD_WAIT_LGKM0();
+    if (far) KAMD_WAIT_VM(10); else KAMD_WAIT_VM(0);
+    KAMD_BARRIER();
+    if (near) read_b(kt + 1, 0);
+    if (far) stage(kt + 2, 1);
+    mma(1, 1);
+  }
+  // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = n0 + wc * 64 + nq * 32 + j * 16 + frow;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wr * 128 + mq * 64 + i * 16 + fq * 4 + r;
+            store_out<OutT>(C + (size_t)row * ldc + col, alpha * acc[mq][nq][i][j][r]);
+          }
+        }
+}
+#undef KAMD_WAIT_VM
+#undef KAMD_WAIT_LGKM0
+#undef KAMD_BARRIER
+}  // namespace gemm8
+
+// ---------------------------------------------------------------------------
 // HBM streaming copy, 16 B per lane, grid-stride
 __global__ void __launch_bounds__(256) hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -376,6 +554,24 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
   if ((((uintptr_t)A) | ((uintptr_t)B)) & 15) {
     snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
     return -1;
+  }
+  if (g_gemm_path == 0 && M % gemm8::BM == 0 && N % gemm8::BN == 0 && K % gemm8::BK == 0 && K / gemm8::BK >= 2) {
+    static bool attr8 = false;
+    if (!attr8) {
+      HC(hipFuncSetAttribute((const void*)gemm8::gemm_bf16_nt_8ph_kernel<float>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemm8::LDS_BYTES));
+      HC(hipFuncSetAttribute((const void*)gemm8::gemm_bf16_nt_8ph_kernel<__bf16>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemm8::LDS_BYTES));
+      attr8 = true;
+    }
+    const int tiles = (M / gemm8::BM) * (N / gemm8::BN);
+    if (out_fp32)
+      hipLaunchKernelGGL(gemm8::gemm_bf16_nt_8ph_kernel<float>, dim3(tiles), dim3(gemm8::THREADS), gemm8::LDS_BYTES,
+                         stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+    else
+      hipLaunchKernelGGL(gemm8::gemm_bf16_nt_8ph_kernel<__bf16>, dim3(tiles), dim3(gemm8::THREADS), gemm8::LDS_BYTES,
+                         stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+    return check(hipGetLastError(), "gemm8 launch");
   }
   if (g_gemm_path != 1 && M % gemm256::BM == 0 && N % gemm256::BN == 0 && K % gemm256::BK == 0) {
     static bool attr_set = false;

@@ -79,15 +79,17 @@ def test_real_amdsmi_enumerates_mi355x():
     assert os.path.exists(f"/dev/dri/renderD{g.render_minor}")
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1024), (2048, 1024, 4096)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 256, 128), (512, 512, 192), (512, 768, 1024),
+                                   (2048, 1024, 4096)])
 def test_gemm_both_paths_match_reference(hk, M, N, K):
-    """The 256-tile glds kernel and the 128-tile kernel against an fp32 torch reference."""
+    """Every GEMM path against an fp32 torch reference: 0 = 8-phase 256-tile (K-tile counts 2, 3
+    exercise its prologue / tail waits), 1 = 128-tile register-staged, 2 = 2-barrier 256-tile glds."""
     torch.manual_seed(1)
     a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     b = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     ref = a.float() @ b.float().T
     try:
-        for path in (0, 1):
+        for path in (0, 1, 2):
             hk.set_gemm_path(path)
             out = hk.gemm_bf16_nt(a, b, out_fp32=True)
             torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * (K ** 0.5))
