@@ -277,6 +277,42 @@ class DefaultStorageClass(Plugin):
             spec["storageClassName"] = defaults[0]["metadata"]["name"]
 
 
+def _storage(pvc):
+    from ...api.quantity import parse_quantity
+    v = (((pvc or {}).get("spec") or {}).get("resources") or {}).get("requests", {}).get("storage")
+    return parse_quantity(str(v)).value if v is not None else 0
+
+
+@register
+class PersistentVolumeClaimResize(Plugin):
+    """`plugin/pkg/admission/persistentvolume/resize/admission.go`: a claim may only grow, only
+    when bound, only when its StorageClass sets `allowVolumeExpansion: true`, and only when the
+    bound volume's type can be expanded (here: hostPath volumes from the built-in provisioner,
+    local and CSI volumes)."""
+    name = "PersistentVolumeClaimResize"
+    operations = (UPDATE,)
+    EXPANDABLE = ("hostPath", "local", "csi")
+
+    def validate(self, a):
+        if a.resource != "persistentvolumeclaims" or a.subresource or a.old is None:
+            return
+        new, old = _storage(a.obj), _storage(a.old)
+        if new <= old:
+            if new < old:
+                raise AdmissionError("spec.resources.requests.storage: field can not be less than previous value", 403)
+            return
+        if ((a.old.get("status") or {}).get("phase") != "Bound") or not (a.old.get("spec") or {}).get("volumeName"):
+            raise AdmissionError("Only bound persistent volume claims can be expanded", 403)
+        cls = (a.old.get("spec") or {}).get("storageClassName") or ""
+        sc = self.server.get_object("storageclasses", None, cls) if cls else None
+        if not sc or not sc.get("allowVolumeExpansion"):
+            raise AdmissionError("only dynamically provisioned pvc can be resized and the storageclass that provisions "
+                                 "the pvc must support resize", 403)
+        pv = self.server.get_object("persistentvolumes", None, a.old["spec"]["volumeName"])
+        if pv is None or not any(k in (pv.get("spec") or {}) for k in self.EXPANDABLE):
+            raise AdmissionError("volume plugin does not support resize", 403)
+
+
 @register
 class AlwaysAdmit(Plugin):
     name = "AlwaysAdmit"

@@ -19,7 +19,7 @@ from .certificates import (BootstrapSignerController, ClusterRoleAggregationCont
 from .podautoscaler import HorizontalController
 from .attachdetach import AttachDetachController, ExternalAttacher
 from .network import NodeIPAMController, ServiceLBController
-from .volume import PersistentVolumeController, PVCProtectionController
+from .volume import ExpandController, PersistentVolumeController, PVCProtectionController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
 
@@ -54,6 +54,7 @@ CONTROLLERS = {
     "nodeipam": NodeIPAMController,
     "service": ServiceLBController,
     "attachdetach": AttachDetachController,
+    "persistentvolume-expander": ExpandController,
     "csi-attacher": ExternalAttacher,
 }
 

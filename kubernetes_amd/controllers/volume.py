@@ -244,6 +244,56 @@ class PersistentVolumeController(Controller):
             await self.client.patch("persistentvolumes", name, {"status": {"phase": "Available"}}, None, "merge", "status")
 
 
+class ExpandController(Controller):
+    """`pkg/controller/volume/expand/expand_controller.go`: a bound claim whose requested size
+    exceeds `status.capacity` is expanded — the volume plugin grows the backing volume
+    (`ExpandVolumeDevice`; host-path and local volumes are directories, so that is a no-op,
+    CSI volumes would call the driver), the PV's `spec.capacity` is raised, and the claim's
+    `status.capacity` is updated. Volumes that need a file-system resize on the node get the
+    `FileSystemResizePending` condition instead, which the kubelet clears after resizing."""
+    name = "expand"
+    workers = 1
+    FS_RESIZE = ()       # plugin kinds whose file system is grown by the kubelet after the device
+
+    def setup(self):
+        self.pvc_inf = self.factory.get("persistentvolumeclaims")
+        self.pv_inf = self.factory.get("persistentvolumes")
+        self.pvc_inf.add_handler(self._maybe, lambda o, n: self._maybe(n), None)
+
+    def _maybe(self, pvc):
+        if (pvc.get("status") or {}).get("phase") == "Bound" and _cap(pvc, "requests") > self._status_cap(pvc):
+            self.enqueue("/".join((pvc["metadata"]["namespace"], pvc["metadata"]["name"])))
+
+    @staticmethod
+    def _status_cap(pvc):
+        q = ((pvc.get("status") or {}).get("capacity") or {}).get("storage")
+        return parse_quantity(str(q)).value if q is not None else 0
+
+    async def sync(self, key):
+        pvc = self.pvc_inf.get(key)
+        if pvc is None or (pvc.get("status") or {}).get("phase") != "Bound":
+            return
+        want = ((pvc.get("spec") or {}).get("resources") or {}).get("requests", {}).get("storage")
+        if _cap(pvc, "requests") <= self._status_cap(pvc):
+            return
+        pv = self.pv_inf.get((pvc.get("spec") or {}).get("volumeName", ""))
+        if pv is None:
+            return
+        if _cap(pv, "capacity") < _cap(pvc, "requests"):
+            await self.client.patch("persistentvolumes", pv["metadata"]["name"], {"spec": {"capacity": {"storage": want}}})
+        ns, name = split_key(key)
+        kind = next((k for k in ("hostPath", "local", "csi") if k in (pv.get("spec") or {})), "")
+        if kind in self.FS_RESIZE:
+            await self.client.patch("persistentvolumeclaims", name, {"status": {"conditions": [
+                {"type": "FileSystemResizePending", "status": "True",
+                 "message": "Waiting for user to (re-)start a pod to finish file system resize of volume on node."}]}},
+                ns, "merge", "status")
+            return
+        await self.client.patch("persistentvolumeclaims", name, {"status": {"capacity": {"storage": want},
+                                                                            "conditions": None}}, ns, "merge", "status")
+        self.recorder.event(pvc, "Normal", "VolumeResizeSuccessful", f"volume {pv['metadata']['name']} resized to {want}")
+
+
 class PVCProtectionController(Controller):
     name = "pvc-protection"
     workers = 1

@@ -148,3 +148,15 @@ def test_default_addons_reconcile(run):
                 await c.close()
                 await s.stop()
     run(main())
+
+
+def test_gendocs_all_components(tmp_path):
+    from kubernetes_amd.cmd import gendocs
+    files = gendocs.generate(str(tmp_path / "md"), "md")
+    assert len(files) == len(gendocs.COMPONENTS)
+    kubectl = (tmp_path / "md" / "kubectl.md").read_text()
+    assert "## kubectl rolling-update" in kubectl and "## kubectl set image" in kubectl
+    assert "--feature-gates" in (tmp_path / "md" / "kubelet.md").read_text()
+    man = gendocs.generate(str(tmp_path / "man"), "man", ["kubeadm"])
+    assert any(p.endswith("kubeadm-join.1") for p in man)
+    assert gendocs.generate(str(tmp_path / "y"), "yaml", ["kube-scheduler"])

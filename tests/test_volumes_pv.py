@@ -115,3 +115,48 @@ def test_pv_lifecycle_end_to_end(run, tmp_path):
         finally:
             await cl.stop()
     run(main(), timeout=120)
+
+
+def test_pvc_expansion(run, tmp_path):
+    """PersistentVolumeClaimResize admission + expand controller
+    (plugin/pkg/admission/persistentvolume/resize, pkg/controller/volume/expand)."""
+    from kubernetes_amd.apiserver.admission import DEFAULT_PLUGINS
+    from kubernetes_amd.client.rest import APIStatusError
+
+    async def main():
+        cl = LocalCluster(nodes=1, gpus_per_node=0, workdir=str(tmp_path / "c"),
+                          admission_plugins=list(DEFAULT_PLUGINS) + ["PersistentVolumeClaimResize"],
+                          controllers=["persistentvolume-binder", "persistentvolume-expander"],
+                          controller_options={"persistentvolume-binder": {"hostpath_root": str(tmp_path / "hp")}})
+        await cl.start()
+        c = cl.client
+        try:
+            await c.create("storageclasses", {"metadata": {"name": "grow"}, "provisioner": "kubernetes.io/host-path",
+                                              "allowVolumeExpansion": True})
+            await c.create("storageclasses", {"metadata": {"name": "fixed"}, "provisioner": "kubernetes.io/host-path"})
+            await c.create("persistentvolumeclaims", pvc("a", "1Gi", cls="grow"), "default")
+            await c.create("persistentvolumeclaims", pvc("b", "1Gi", cls="fixed"), "default")
+
+            async def bound(name):
+                p = await c.get("persistentvolumeclaims", name, "default")
+                return p if (p.get("status") or {}).get("phase") == "Bound" else None
+            await cl.wait_for(lambda: bound("a"), 15)
+            await cl.wait_for(lambda: bound("b"), 15)
+            await c.patch("persistentvolumeclaims", "a", {"spec": {"resources": {"requests": {"storage": "3Gi"}}}}, "default")
+
+            async def grown():
+                p = await c.get("persistentvolumeclaims", "a", "default")
+                return p if ((p.get("status") or {}).get("capacity") or {}).get("storage") == "3Gi" else None
+            p = await cl.wait_for(grown, 15)
+            pv = await c.get("persistentvolumes", p["spec"]["volumeName"])
+            assert pv["spec"]["capacity"]["storage"] == "3Gi"
+            for name, size in (("a", "2Gi"), ("b", "2Gi")):        # shrink / class without expansion
+                try:
+                    await c.patch("persistentvolumeclaims", name, {"spec": {"resources": {"requests": {"storage": size}}}},
+                                  "default")
+                    raise AssertionError(f"resize of {name} to {size} must be rejected")
+                except APIStatusError as e:
+                    assert e.code == 403
+        finally:
+            await cl.stop()
+    run(main(), timeout=60)
