@@ -58,6 +58,8 @@ def main(argv=None):
     ap.add_argument("--maximum-dead-containers", type=int, default=-1)
     ap.add_argument("--bootstrap-checkpoint-path", default=None,
                     help="checkpoint pods annotated node.kubernetes.io/bootstrap-checkpoint=true here")
+    ap.add_argument("--volume-plugin-dir", default="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
+                    help="FlexVolume driver directory (<vendor>~<driver>/<driver>)")
     ap.add_argument("--rotate-certificates", action="store_true",
                     help="rotate the kubelet client certificate (CSR) as it approaches expiry")
     ap.add_argument("--config", default=None, help="KubeletConfiguration file (kubeletconfig/v1alpha1)")
@@ -113,7 +115,7 @@ def main(argv=None):
         base = dict(pods=a.max_pods, node_status_update_frequency=a.node_status_update_frequency,
                     cpu_manager_policy=a.cpu_manager_policy, eviction_hard=a.eviction_hard, dns=dns,
                     pod_manifest_path=a.pod_manifest_path, container_gc=container_gc,
-                    bootstrap_checkpoint_path=a.bootstrap_checkpoint_path)
+                    bootstrap_checkpoint_path=a.bootstrap_checkpoint_path, volume_plugin_dir=a.volume_plugin_dir)
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,

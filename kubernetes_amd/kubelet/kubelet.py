@@ -88,7 +88,7 @@ class Kubelet:
                  pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0,
                  image_service=None, image_gc=None, image_backoff=10.0, network_plugin=None, dns=None,
                  hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
-                 bootstrap_checkpoint_path=None):
+                 bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec"):
         self.client = client
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
@@ -119,7 +119,7 @@ class Kubelet:
                                             os.path.join(root_dir or tempfile.gettempdir(), f"cpu_manager_state.{node_name}"))
         self.root_dir = root_dir or os.path.join(tempfile.gettempdir(), f"kamd-kubelet-{node_name}")
         self.volumes = VolumeManager(client, os.path.join(self.root_dir, "pods"), os.path.join(self.root_dir, "plugins"),
-                                     node_name)
+                                     node_name, flex_plugins_dir=volume_plugin_dir)
         self.probes = ProbeManager(runtime, self._on_readiness, self._on_liveness_failure)
         self.node_name = node_name
         self.runtime = runtime

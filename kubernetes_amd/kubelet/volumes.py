@@ -87,7 +87,11 @@ def _resource_field(container, ref):
 
 
 class VolumeManager:
-    def __init__(self, client, root, csi_plugins_dir=None, node_name=None, attach_timeout=60.0):
+    def __init__(self, client, root, csi_plugins_dir=None, node_name=None, attach_timeout=60.0,
+                 flex_plugins_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec"):
+        self.flex_dir = flex_plugins_dir
+        self.flex_mounted: dict[str, list] = {}      # pod uid -> [(driver path, target)]
+        self.flex_inited: dict[str, dict] = {}       # driver path -> init capabilities
         self.client = client
         self.root = root
         self.csi_dir = csi_plugins_dir
@@ -137,6 +141,10 @@ class VolumeManager:
                 self._downward(pod, v["downwardAPI"], d, node_name, pod_ip)
             elif "persistentVolumeClaim" in v:
                 d = await self._pvc_path(ns, v["persistentVolumeClaim"], pod, name, node_name)
+            elif "flexVolume" in v:
+                d = await self._flex_mount(pod, name, v["flexVolume"], d)
+            elif "gitRepo" in v:
+                await self._git_repo(v["gitRepo"], d)
             elif "projected" in v:
                 for src in v["projected"].get("sources") or ():
                     if "configMap" in src or "secret" in src:
@@ -158,6 +166,9 @@ class VolumeManager:
             raise VolumeError(f"persistentvolumeclaim {ns}/{src.get('claimName')} is not bound")
         pv = await self._get("persistentvolumes", None, vol, False)
         sp = pv.get("spec") or {}
+        if sp.get("flexVolume") and pod is not None:
+            d = os.path.join(self.pod_dir(pod), "volumes", "flexvolume", vol)
+            return await self._flex_mount(pod, vol, sp["flexVolume"], d)
         if sp.get("csi"):
             return await self._csi_publish(pod, vol, sp, node_name or self.node_name)
         path = (sp.get("hostPath") or {}).get("path") or (sp.get("local") or {}).get("path")
@@ -205,8 +216,81 @@ class VolumeManager:
         self.csi_published.setdefault(pod["metadata"]["uid"], []).append((driver, handle, target))
         return target
 
+    async def _flex_call(self, driver_path, *args):
+        """`pkg/volume/flexvolume/driver-call.go`: exec the driver, parse its JSON status."""
+        import asyncio
+        import json as _json
+        p = await asyncio.create_subprocess_exec(driver_path, *args, stdout=asyncio.subprocess.PIPE,
+                                                 stderr=asyncio.subprocess.PIPE)
+        out, err = await p.communicate()
+        try:
+            st = _json.loads(out or b"{}")
+        except ValueError:
+            raise VolumeError(f"flexvolume {driver_path} {args[0]}: invalid output {out[:200]!r} {err[:200]!r}")
+        if st.get("status") == "Not supported":
+            return st
+        if st.get("status") != "Success":
+            raise VolumeError(f"flexvolume {driver_path} {args[0]} failed: {st.get('message', '')}")
+        return st
+
+    async def _flex_mount(self, pod, vol_name, src, target):
+        """FlexVolume (`pkg/volume/flexvolume`): `init` once per driver, then
+        `mount <target> <json options>` with the user options plus the kubernetes.io/* keys
+        (fsType, readwrite, pod name/namespace/uid, serviceAccount.name, pvOrVolumeName, secret/*)."""
+        import json as _json
+        vendor_driver = src.get("driver", "")
+        vendor, _, drv = vendor_driver.rpartition("/")
+        path = os.path.join(self.flex_dir, f"{vendor}~{drv}" if vendor else drv, drv)
+        if not os.access(path, os.X_OK):
+            raise VolumeError(f"flexvolume driver {vendor_driver} not found at {path}")
+        if path not in self.flex_inited:
+            self.flex_inited[path] = (await self._flex_call(path, "init")).get("capabilities") or {}
+        md = pod["metadata"]
+        opts = dict(src.get("options") or {})
+        opts.update({"kubernetes.io/fsType": src.get("fsType", ""),
+                     "kubernetes.io/readwrite": "ro" if src.get("readOnly") else "rw",
+                     "kubernetes.io/pod.name": md["name"], "kubernetes.io/pod.namespace": md.get("namespace", "default"),
+                     "kubernetes.io/pod.uid": md["uid"], "kubernetes.io/pvOrVolumeName": vol_name,
+                     "kubernetes.io/serviceAccount.name": (pod.get("spec") or {}).get("serviceAccountName", "default")})
+        if src.get("secretRef"):
+            sec = await self._get("secrets", md.get("namespace", "default"), src["secretRef"]["name"], False)
+            for k, v in (sec.get("data") or {}).items():
+                opts[f"kubernetes.io/secret/{k}"] = v
+        os.makedirs(target, exist_ok=True)
+        await self._flex_call(path, "mount", target, _json.dumps(opts))
+        self.flex_mounted.setdefault(md["uid"], []).append((path, target))
+        return target
+
+    async def _git_repo(self, src, d):
+        """gitRepo volume (`pkg/volume/git_repo`): `git clone -- <repo> [<directory>]`, then
+        `git checkout <revision>` + `git reset --hard` when a revision is given."""
+        import asyncio
+        os.makedirs(d, exist_ok=True)
+        if os.listdir(d):
+            return
+        args = ["clone", "--", src["repository"]] + ([src["directory"]] if src.get("directory") else [])
+        p = await asyncio.create_subprocess_exec("git", *args, cwd=d, stdout=asyncio.subprocess.PIPE,
+                                                 stderr=asyncio.subprocess.PIPE)
+        _, err = await p.communicate()
+        if p.returncode != 0:
+            raise VolumeError(f"git clone {src['repository']}: {err.decode(errors='replace').strip()}")
+        if src.get("revision"):
+            sub = src.get("directory") or os.path.basename(src["repository"].rstrip("/")).removesuffix(".git")
+            repo = d if src.get("directory") == "." else os.path.join(d, sub)
+            for cmd in (["checkout", src["revision"]], ["reset", "--hard"]):
+                p = await asyncio.create_subprocess_exec("git", *cmd, cwd=repo, stdout=asyncio.subprocess.PIPE,
+                                                         stderr=asyncio.subprocess.PIPE)
+                _, err = await p.communicate()
+                if p.returncode != 0:
+                    raise VolumeError(f"git {' '.join(cmd)}: {err.decode(errors='replace').strip()}")
+
     async def unpublish(self, pod):
-        """CSI NodeUnpublishVolume for every volume published for the pod (TearDownAt)."""
+        """FlexVolume `unmount` and CSI NodeUnpublishVolume for the pod's volumes (TearDownAt)."""
+        for path, target in self.flex_mounted.pop(pod["metadata"]["uid"], []):
+            try:
+                await self._flex_call(path, "unmount", target)
+            except VolumeError:
+                pass
         from ..csi import api as CSI
         from ..csi.driver import CSIClient
         for driver, handle, target in self.csi_published.pop(pod["metadata"]["uid"], []):
