@@ -73,13 +73,26 @@ def control_plane_shape(world, workers=0, shards=0):
     Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep): with one rank the single API
     server + scheduler are fastest; from 2 ranks on, parallel API server workers over the
     native store and 2 scheduler shards win, up to 4 workers once ranks use most cores.
-    More cores (a whole 8-GPU node) allow 4 shards as well."""
+    On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — one API
+    server worker and one scheduler shard per rank, up to 8 each — so per-rank work (weak
+    scaling) is met by per-rank control-plane capacity instead of a fixed-size control plane."""
     cpus = cpu_budget()
     spare = cpus - world - 1
+    big = cpus >= 64
     if workers <= 0:
-        workers = 1 if world == 1 or spare < 3 else (2 if world <= 4 else 4)
+        if world == 1 or spare < 3:
+            workers = 1
+        elif big:
+            workers = min(8, world, max(1, spare // 6))
+        else:
+            workers = 2 if world <= 4 else 4
     if shards <= 0:
-        shards = 1 if world == 1 or spare < 3 else (4 if cpus >= 64 else 2)
+        if world == 1 or spare < 3:
+            shards = 1
+        elif big:
+            shards = min(8, world, max(1, spare // 6))
+        else:
+            shards = 2
     return workers, shards
 
 
