@@ -40,3 +40,19 @@ def test_real_plugin_capacity_and_health(run):
             devs = node["status"]["extendedResources"]["amd.com/gpu"]["resources"]
             assert all(d["health"] == "Healthy" for d in devs.values())
     run(main(), timeout=120)
+
+
+@pytest.mark.gpu
+def test_e2e_gpu_spec_on_real_mi355x(run):
+    """The e2e framework's [Feature:GPU] spec (mirror of test/e2e/scheduling/nvidia-gpus.go)
+    against a one-node cluster on the real MI355X: two pods get distinct GPUs and both print
+    'Test PASSED' from the HIP vector add."""
+    from kubernetes_amd.cluster import LocalCluster
+    from kubernetes_amd.e2e import specs  # noqa: F401
+    from kubernetes_amd.e2e.framework import run_specs
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8, runtime="process", real_gpus=True, kubelet_http=True) as cl:
+            res = await run_specs(cl.url, focus="Feature:GPU", timeout=150)
+        assert len(res) == 1 and res[0].ok, res[0].error if res else "no spec ran"
+    run(main(), timeout=200)
