@@ -101,6 +101,8 @@ RESOURCES = [
     ResourceInfo("admissionregistration.k8s.io", "v1beta1", "ValidatingWebhookConfiguration",
                  "validatingwebhookconfigurations", False, ()),
     ResourceInfo("apiregistration.k8s.io", "v1beta1", "APIService", "apiservices", False, ()),
+    ResourceInfo("admissionregistration.k8s.io", "v1alpha1", "InitializerConfiguration",
+                 "initializerconfigurations", False, ()),
     ResourceInfo("certificates.k8s.io", "v1beta1", "CertificateSigningRequest", "certificatesigningrequests", False, ("csr",)),
     ResourceInfo("networking.k8s.io", "v1", "NetworkPolicy", "networkpolicies", True, ("netpol",)),
     ResourceInfo("extensions", "v1beta1", "Ingress", "ingresses", True, ("ing",)),

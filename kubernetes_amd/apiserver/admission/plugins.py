@@ -313,6 +313,60 @@ class PersistentVolumeClaimResize(Plugin):
             raise AdmissionError("volume plugin does not support resize", 403)
 
 
+def _rule_matches(rule, group, version, resource):
+    def ok(vals, v):
+        return not vals or "*" in vals or v in vals
+    return ok(rule.get("apiGroups"), group) and ok(rule.get("apiVersions"), version) and ok(rule.get("resources"), resource)
+
+
+@register
+class Initializers(Plugin):
+    """`staging/src/k8s.io/apiserver/pkg/admission/plugin/initialization/initialization.go`
+    (alpha): on CREATE, the initializers of every `InitializerConfiguration` whose rules match
+    the resource are written to `metadata.initializers.pending`; the object stays hidden from
+    list/watch (unless `includeUninitialized=true`) until each initializer controller removes
+    its own entry — the head of the list — by UPDATE. An emptied list is dropped, which makes
+    the object visible (watchers see it ADDED)."""
+    name = "Initializers"
+    operations = (CREATE, UPDATE)
+
+    def admit(self, a):
+        if a.subresource or a.resource in ("initializerconfigurations", "events"):
+            return
+        md = a.obj.setdefault("metadata", {})
+        if a.operation == CREATE:
+            if md.get("initializers") is not None:
+                return                    # explicitly set by the creator
+            from ...api import meta as m
+            ri = m.BY_PLURAL.get(a.resource)
+            group, version = (ri.group, ri.version) if ri else ("", "v1")
+            pending = []
+            for cfg in self.server.list_objects("initializerconfigurations"):
+                for init in cfg.get("initializers") or ():
+                    if any(_rule_matches(r, group, version, a.resource) for r in init.get("rules") or ()):
+                        if init["name"] not in [p["name"] for p in pending]:
+                            pending.append({"name": init["name"]})
+            if pending:
+                md["initializers"] = {"pending": pending}
+            return
+        ini = md.get("initializers")
+        if ini is not None and not ini.get("pending") and not ini.get("result"):
+            md.pop("initializers", None)
+
+    def validate(self, a):
+        if a.operation != UPDATE or a.old is None or a.subresource:
+            return
+        old = ((a.old.get("metadata") or {}).get("initializers") or {}).get("pending") or []
+        new = ((a.obj.get("metadata") or {}).get("initializers") or {}).get("pending") or []
+        if not old:
+            if new:
+                raise AdmissionError("initializers may not be added to an initialized object", 403)
+            return
+        if new and [p["name"] for p in new] != [p["name"] for p in old] and \
+                [p["name"] for p in new] != [p["name"] for p in old[1:]]:
+            raise AdmissionError("initializers may only be removed from the front of metadata.initializers.pending", 403)
+
+
 @register
 class AlwaysAdmit(Plugin):
     name = "AlwaysAdmit"

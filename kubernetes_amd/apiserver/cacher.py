@@ -45,6 +45,9 @@ class Entry:
         return f.get("metadata.namespace", "") + "/" + f.get("metadata.name", "")
 
 
+UNINITIALIZED = "metadata.uninitialized"
+
+
 class GoneError(Exception):
     pass
 
@@ -186,7 +189,12 @@ class ResourceCache:
 
     # -- writes -----------------------------------------------------------
     def make_entry(self, obj, raw, rev):
-        return Entry(obj, raw, rev, self.fields_fn(obj))
+        fields = self.fields_fn(obj)
+        if ((obj.get("metadata") or {}).get("initializers") or {}).get("pending"):
+            # alpha Initializers: uninitialized objects are hidden from list/watch unless the
+            # client passes includeUninitialized=true (the server adds this field selector)
+            fields = dict(fields, **{UNINITIALIZED: "true"})
+        return Entry(obj, raw, rev, fields)
 
     def apply(self, etype: str, key: str, entry: Entry, prev: Entry | None):
         """Record + dispatch one committed change (entry is the new state; for DELETED the

@@ -164,6 +164,7 @@ class APIServer:
             self._install(ri)
         names = adm.DEFAULT_PLUGINS if admission_plugins is None else admission_plugins
         self.admission = adm.new_chain(names, self, admission_config)
+        self.initializers_enabled = "Initializers" in names
         self.authn = None
         if token_file or tokens or client_ca_file or service_account_key_files or enable_bootstrap_token_auth \
                 or authentication_token_webhook or not anonymous_auth or oidc:
@@ -1261,10 +1262,17 @@ class APIServer:
         return _json(200, {"kind": ri.list_kind, "apiVersion": ri.group_version,
                            "metadata": {"resourceVersion": str(self.revision)}, "items": items})
 
+    def _hide_uninitialized(self, q, fsel):
+        if not self.initializers_enabled or q.get("includeUninitialized") in ("true", "1"):
+            return fsel
+        from .cacher import UNINITIALIZED
+        return (fsel + "," if fsel else "") + f"{UNINITIALIZED}!=true"
+
     def _list(self, req, ri, ns):
         q = req.query
         ls = parse_labels(q.get("labelSelector")) if q.get("labelSelector") else None
-        fs = parse_field_selector(q.get("fieldSelector")) if q.get("fieldSelector") else None
+        fsel = self._hide_uninitialized(q, q.get("fieldSelector"))
+        fs = parse_field_selector(fsel) if fsel else None
         entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
         limit = int(q.get("limit") or 0)
         cont = q.get("continue")
@@ -1294,6 +1302,7 @@ class APIServer:
         fsel = q.get("fieldSelector")
         if name:
             fsel = (fsel + "," if fsel else "") + f"metadata.name={name}"
+        fsel = self._hide_uninitialized(q, fsel)
         timeout = float(q.get("timeoutSeconds") or 0) or None
         cache = self.caches[ri.plural]
         send_initial = not rv or rv == "0"
