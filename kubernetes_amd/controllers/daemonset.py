@@ -15,13 +15,12 @@ ordinal order, status replicas / readyReplicas / currentRevision / updateRevisio
 from __future__ import annotations
 
 import asyncio
-import hashlib
-import json
 
 from ..api import meta as m
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
 from ..scheduler import predicates as P
 from ..scheduler.cache import NodeInfo, PodInfo
+from .history import REVISION_HASH, ensure_revision, revisions_of
 from .base import Controller, controller_ref, pod_from_template, pod_is_active, pod_is_ready, split_key
 
 DS_TOLERATIONS = [
@@ -61,6 +60,7 @@ class DaemonSetController(Controller):
         self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
         if "controllerUID" not in self.pod_inf.store.indexers:
             self.pod_inf.store.add_indexer("controllerUID", lambda p: [r["uid"] for r in (p["metadata"].get("ownerReferences") or ()) if r.get("controller")])
+        self.rev_inf = self.factory.get("controllerrevisions")
         self._inflight: dict[str, set] = {}
 
     def _all(self, _obj):
@@ -97,12 +97,29 @@ class DaemonSetController(Controller):
         creating = self._inflight.setdefault(key, set())
         creating &= want - set(by_node)
         tmpl = (ds.get("spec") or {}).get("template") or {}
+        spec = ds.get("spec") or {}
+        rev = await ensure_revision(self.client, ds, "DaemonSet", tmpl,
+                                    revisions_of(self.rev_inf.list(), ds["metadata"]["uid"]),
+                                    int(spec.get("revisionHistoryLimit", 10)))
+        h = rev["metadata"]["labels"][REVISION_HASH]
         todo = [n for n in sorted(want) if n not in by_node and n not in creating]
         dels = [p for node, ps in by_node.items() if node not in want for p in ps]
         dels += [p for node, ps in by_node.items() if node in want for p in ps[1:]]
+        # RollingUpdate (apps/v1 default): replace pods of older revisions, at most maxUnavailable
+        # (default 1) nodes without a ready pod at a time; OnDelete waits for manual deletion
+        strategy = spec.get("updateStrategy") or {}
+        if strategy.get("type", "RollingUpdate") == "RollingUpdate" and not todo:
+            max_unavail = int(((strategy.get("rollingUpdate") or {}).get("maxUnavailable")) or 1)
+            unavailable = sum(1 for n in want if not any(pod_is_ready(p) for p in by_node.get(n, ())))
+            stale = [ps[0] for node, ps in sorted(by_node.items()) if node in want and ps
+                     and (ps[0]["metadata"].get("labels") or {}).get(REVISION_HASH) != h
+                     and not ps[0]["metadata"].get("deletionTimestamp")]
+            budget = max(0, max_unavail - unavailable)
+            dels += [p for p in stale if not pod_is_ready(p)] + [p for p in stale if pod_is_ready(p)][:budget]
 
         async def create(node):
             pod = pod_from_template(tmpl, ds, f"{name}-", ns)
+            pod["metadata"]["labels"][REVISION_HASH] = h
             spec = pod["spec"]
             spec["tolerations"] = list(spec.get("tolerations") or []) + DS_TOLERATIONS
             aff = spec.setdefault("affinity", {}).setdefault("nodeAffinity", {})
@@ -120,7 +137,9 @@ class DaemonSetController(Controller):
         ready = sum(1 for ps in by_node.values() for p in ps if pod_is_ready(p))
         st = {"desiredNumberScheduled": len(want), "currentNumberScheduled": len([n for n in by_node if n in want]),
               "numberMisscheduled": len([n for n in by_node if n not in want and n]), "numberReady": ready,
-              "numberAvailable": ready, "updatedNumberScheduled": len([n for n in by_node if n in want]),
+              "numberAvailable": ready,
+              "updatedNumberScheduled": len([n for n, ps in by_node.items() if n in want and ps and
+                                             (ps[0]["metadata"].get("labels") or {}).get(REVISION_HASH) == h]),
               "observedGeneration": ds["metadata"].get("generation", 1)}
         if {k: (ds.get("status") or {}).get(k) for k in st} != st:
             try:
@@ -137,6 +156,7 @@ class StatefulSetController(Controller):
     def setup(self):
         self.ss_inf = self.factory.get("statefulsets")
         self.pod_inf = self.factory.get("pods")
+        self.rev_inf = self.factory.get("controllerrevisions")
         self.ss_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
         self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
 
@@ -154,8 +174,10 @@ class StatefulSetController(Controller):
         replicas = int(spec.get("replicas", 1))
         parallel = spec.get("podManagementPolicy") == "Parallel"
         tmpl = spec.get("template") or {}
-        rev = hashlib.sha256(json.dumps(tmpl, sort_keys=True).encode()).hexdigest()[:10]
-        rev_name = f"{name}-{rev}"
+        rev_obj = await ensure_revision(self.client, ss, "StatefulSet", tmpl,
+                                        revisions_of(self.rev_inf.list(), ss["metadata"]["uid"]),
+                                        int(spec.get("revisionHistoryLimit", 10)))
+        rev_name = rev_obj["metadata"]["name"]
         uid = ss["metadata"]["uid"]
         pods = {}
         for p in self.pod_inf.list():

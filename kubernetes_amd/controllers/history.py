@@ -1,0 +1,60 @@
+"""ControllerRevision history for DaemonSets and StatefulSets.
+
+Parity: `pkg/controller/history/controller_history.go` — a revision is a ControllerRevision named
+`<owner>-<hash>` owned (controller ref) by the workload, labelled `controller-revision-hash`,
+with `data` = the pod template patch and a monotonically increasing `revision`; an existing
+revision whose data equals the current template is reused (and re-numbered to the newest, as
+on a rollback); revisions beyond `revisionHistoryLimit` (default 10) are pruned oldest first,
+never the current one.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+
+from ..client.rest import APIStatusError, is_already_exists, is_not_found
+
+REVISION_HASH = "controller-revision-hash"
+
+
+def revision_hash(template) -> str:
+    return hashlib.sha256(json.dumps(template or {}, sort_keys=True).encode()).hexdigest()[:10]
+
+
+def revisions_of(lister_items, owner_uid):
+    out = [r for r in lister_items
+           if any(o.get("uid") == owner_uid and o.get("controller") for o in r["metadata"].get("ownerReferences") or ())]
+    return sorted(out, key=lambda r: int(r.get("revision", 0)))
+
+
+async def ensure_revision(client, owner, kind, template, existing, limit=10):
+    """The ControllerRevision for `template` (created or promoted), pruning old history."""
+    md = owner["metadata"]
+    ns, h = md["namespace"], revision_hash(template)
+    name = f"{md['name']}-{h}"
+    newest = max((int(r.get("revision", 0)) for r in existing), default=0)
+    cur = next((r for r in existing if r["metadata"]["name"] == name), None)
+    if cur is None:
+        rev = {"apiVersion": "apps/v1", "kind": "ControllerRevision",
+               "metadata": {"name": name, "namespace": ns, "labels": {REVISION_HASH: h},
+                            "ownerReferences": [{"apiVersion": "apps/v1", "kind": kind, "name": md["name"],
+                                                 "uid": md["uid"], "controller": True, "blockOwnerDeletion": True}]},
+               "data": {"spec": {"template": template}}, "revision": newest + 1}
+        try:
+            cur = await client.create("controllerrevisions", rev, ns)
+        except APIStatusError as e:
+            if not is_already_exists(e):
+                raise
+            cur = await client.get("controllerrevisions", name, ns)
+    elif int(cur.get("revision", 0)) < newest:
+        # rolled back to an older template: it becomes the newest revision again
+        cur = await client.patch("controllerrevisions", name, {"revision": newest + 1}, ns)
+    keep = [r for r in existing if r["metadata"]["name"] != name]
+    excess = len(keep) + 1 - max(1, limit)
+    for r in sorted(keep, key=lambda r: int(r.get("revision", 0)))[:max(0, excess)]:
+        try:
+            await client.delete("controllerrevisions", r["metadata"]["name"], ns)
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise
+    return cur

@@ -459,6 +459,23 @@ class Kubectl(extra.ExtraCommands):
                         return
                     raise SystemExit(1)
                 await asyncio.sleep(0.2)
+        elif a.action in ("history", "undo") and ri.kind in ("DaemonSet", "StatefulSet"):
+            from ..controllers.history import revisions_of
+            obj = await self.client.get(ri.plural, name, self.ns)
+            revs = revisions_of((await self.client.list("controllerrevisions", self.ns))["items"], obj["metadata"]["uid"])
+            if a.action == "history":
+                rows = [[int(r.get("revision", 0)), (r["metadata"].get("annotations") or {}).get(
+                    "kubernetes.io/change-cause", "<none>")] for r in revs]
+                self.p(printers.table(rows, ["REVISION", "CHANGE-CAUSE"]))
+                return
+            if len(revs) < 2 and not a.to_revision:
+                raise SystemExit(f"error: no rollout history found for {ri.kind.lower()} \"{name}\"")
+            target = next((r for r in revs if int(r.get("revision", 0)) == a.to_revision), None) if a.to_revision \
+                else revs[-2]
+            if target is None:
+                raise SystemExit(f"error: unable to find specified revision {a.to_revision} in history")
+            await self.client.patch(ri.plural, name, {"spec": {"template": target["data"]["spec"]["template"]}}, self.ns)
+            self.p(f"{ri.kind.lower()}.apps/{name} rolled back")
         elif a.action == "history":
             uid = (await self.client.get(ri.plural, name, self.ns))["metadata"]["uid"]
             rss = [r for r in (await self.client.list("replicasets", self.ns))["items"] if (m.controller_of(r) or {}).get("uid") == uid]

@@ -238,3 +238,32 @@ def test_convert_diff_completion_plugin_options_reconcile(cluster, tmp_path, mon
     p3.write_text(yaml.safe_dump(role))
     assert k(cluster, "auth", "reconcile", "-f", str(p3))[0] == 0
     assert len(_get(cluster, "clusterrole", "recon")["rules"]) == 2
+
+
+def test_daemonset_revisions_rolling_update_and_undo(cluster):
+    """ControllerRevision history (pkg/controller/history) + DaemonSet RollingUpdate +
+    kubectl rollout history/undo for daemonsets."""
+    k(cluster, "create", "namespace", "dsrev")
+    ds = {"apiVersion": "apps/v1", "kind": "DaemonSet", "metadata": {"name": "agent", "namespace": "dsrev"},
+          "spec": {"selector": {"matchLabels": {"app": "agent"}},
+                   "template": {"metadata": {"labels": {"app": "agent"}},
+                                "spec": {"containers": [{"name": "c", "image": "agent:v1"}]}}}}
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
+        yaml.safe_dump(ds, f)
+    assert k(cluster, "create", "-f", f.name)[0] == 0
+
+    def pods_with(image):
+        ps = [p for p in _get(cluster, "-n", "dsrev", "pods")["items"] if not p["metadata"].get("deletionTimestamp")]
+        return len(ps) == 2 and all(p["spec"]["containers"][0]["image"] == image for p in ps)
+    wait(lambda: pods_with("agent:v1"), 30)
+    assert k(cluster, "-n", "dsrev", "set", "image", "daemonset/agent", "c=agent:v2")[0] == 0
+    wait(lambda: pods_with("agent:v2"), 60)
+    revs = _get(cluster, "-n", "dsrev", "controllerrevisions")["items"]
+    assert sorted(r["revision"] for r in revs) == [1, 2]
+    rc, out = k(cluster, "-n", "dsrev", "rollout", "history", "daemonset/agent")
+    assert rc == 0 and "REVISION" in out and "2" in out
+    assert k(cluster, "-n", "dsrev", "rollout", "undo", "daemonset/agent")[0] == 0
+    wait(lambda: pods_with("agent:v1"), 60)
+    revs = _get(cluster, "-n", "dsrev", "controllerrevisions")["items"]
+    assert max(revs, key=lambda r: r["revision"])["data"]["spec"]["template"]["spec"]["containers"][0]["image"] == "agent:v1"
