@@ -60,6 +60,10 @@ def main(argv=None):
                     help="checkpoint pods annotated node.kubernetes.io/bootstrap-checkpoint=true here")
     ap.add_argument("--volume-plugin-dir", default="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
                     help="FlexVolume driver directory (<vendor>~<driver>/<driver>)")
+    ap.add_argument("--manifest-url", default=None, help="HTTP pod source (polled every 20 s)")
+    ap.add_argument("--manifest-url-header", action="append", default=[], help="key:value header for --manifest-url")
+    ap.add_argument("--kube-reserved", default="", help="e.g. cpu=1,memory=2Gi (subtracted from allocatable)")
+    ap.add_argument("--system-reserved", default="", help="e.g. cpu=500m,memory=1Gi")
     ap.add_argument("--rotate-certificates", action="store_true",
                     help="rotate the kubelet client certificate (CSR) as it approaches expiry")
     ap.add_argument("--config", default=None, help="KubeletConfiguration file (kubeletconfig/v1alpha1)")
@@ -115,7 +119,11 @@ def main(argv=None):
         base = dict(pods=a.max_pods, node_status_update_frequency=a.node_status_update_frequency,
                     cpu_manager_policy=a.cpu_manager_policy, eviction_hard=a.eviction_hard, dns=dns,
                     pod_manifest_path=a.pod_manifest_path, container_gc=container_gc,
-                    bootstrap_checkpoint_path=a.bootstrap_checkpoint_path, volume_plugin_dir=a.volume_plugin_dir)
+                    bootstrap_checkpoint_path=a.bootstrap_checkpoint_path, volume_plugin_dir=a.volume_plugin_dir,
+                    manifest_url=a.manifest_url,
+                    manifest_url_headers=dict(h.split(":", 1) for h in a.manifest_url_header if ":" in h),
+                    kube_reserved=dict(kv.split("=", 1) for kv in a.kube_reserved.split(",") if "=" in kv),
+                    system_reserved=dict(kv.split("=", 1) for kv in a.system_reserved.split(",") if "=" in kv))
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,

@@ -50,10 +50,32 @@ def load_manifests(path):
     return out
 
 
+def parse_manifest_text(text, origin):
+    """One pod, or a List / v1 PodList of pods, in JSON or YAML."""
+    import yaml
+    try:
+        doc = json.loads(text) if text.lstrip().startswith("{") else yaml.load(text, Loader=yaml.SafeLoader)
+    except (ValueError, yaml.YAMLError) as e:
+        log.warning("pod manifest from %s: %s", origin, e)
+        return []
+    docs = doc.get("items") or [] if isinstance(doc, dict) and doc.get("kind", "").endswith("List") else [doc]
+    return [(origin, d, hashlib.sha256(json.dumps(d, sort_keys=True).encode()).hexdigest()[:16])
+            for d in docs if isinstance(d, dict) and d.get("kind", "Pod") == "Pod"]
+
+
+def load_url(url, headers=None, timeout=10.0):
+    """`pkg/kubelet/config/http.go`: GET --manifest-url (with --manifest-url-header) every poll."""
+    import urllib.request
+    req = urllib.request.Request(url, headers=dict(headers or {}))
+    with urllib.request.urlopen(req, timeout=timeout) as r:
+        return parse_manifest_text(r.read().decode(), url)
+
+
 class StaticPodSource:
-    def __init__(self, kubelet, path, period=20.0):
+    def __init__(self, kubelet, path, period=20.0, url=None, url_headers=None):
         self.kl = kubelet
         self.path = path
+        self.url, self.url_headers = url, url_headers
         self.period = period
         self.known: dict[tuple, str] = {}     # (ns, name) -> hash
         self._task = None
@@ -73,13 +95,13 @@ class StaticPodSource:
                 log.exception("static pod sync failed")
             await asyncio.sleep(self.period)
 
-    def _mirror(self, doc, h):
+    def _mirror(self, doc, h, source="file"):
         pod = json.loads(json.dumps(doc))
         md = pod.setdefault("metadata", {})
         md["name"] = f"{md.get('name', 'static')}-{self.kl.node_name}"
         md.setdefault("namespace", "default")
         ann = md.setdefault("annotations", {})
-        ann.update({CONFIG_SOURCE: "file", CONFIG_HASH: h, CONFIG_MIRROR: h})
+        ann.update({CONFIG_SOURCE: source, CONFIG_HASH: h, CONFIG_MIRROR: h})
         for k in ("uid", "resourceVersion", "creationTimestamp"):
             md.pop(k, None)
         pod.setdefault("spec", {})["nodeName"] = self.kl.node_name
@@ -87,11 +109,24 @@ class StaticPodSource:
         pod["apiVersion"], pod["kind"] = "v1", "Pod"
         return pod
 
+    async def _sources(self):
+        out = [(d, h, "file") for _, d, h in load_manifests(self.path)] if self.path else []
+        if self.url:
+            try:
+                got = await asyncio.get_running_loop().run_in_executor(None, load_url, self.url, self.url_headers)
+            except OSError as e:
+                log.warning("manifest url %s: %s", self.url, e)
+                # an unreachable URL keeps the pods it last served (http.go only replaces on success)
+                return out, True
+            out += [(d, h, "http") for _, d, h in got]
+        return out, False
+
     async def sync(self):
         c = self.kl.client
         seen = set()
-        for _, doc, h in load_manifests(self.path):
-            pod = self._mirror(doc, h)
+        sources, url_failed = await self._sources()
+        for doc, h, src in sources:
+            pod = self._mirror(doc, h, src)
             key = (pod["metadata"]["namespace"], pod["metadata"]["name"])
             seen.add(key)
             try:
@@ -113,6 +148,8 @@ class StaticPodSource:
                         log.warning("creating mirror pod %s/%s: %s", key[0], key[1], e)
             self.known[key] = h
         for key in [k for k in self.known if k not in seen]:
+            if url_failed:
+                continue
             self.known.pop(key)
             try:
                 await c.delete("pods", key[1], key[0], grace_period=0)

@@ -95,6 +95,12 @@ class EvictionManager:
                 del self.conditions[c]
         return met
 
+    def hard_memory_bytes(self):
+        """The memory.available hard threshold in bytes (percent thresholds count as 0 here:
+        node allocatable needs an absolute value)."""
+        return sum(int(getattr(t, "value", 0) or 0) for t in self.thresholds
+                   if getattr(t, "signal", "") == "memory.available")
+
     def has(self, condition):
         return condition in self.conditions
 

@@ -88,7 +88,8 @@ class Kubelet:
                  pod_manifest_path=None, eviction_hard=None, eviction_signals=None, eviction_interval=10.0,
                  image_service=None, image_gc=None, image_backoff=10.0, network_plugin=None, dns=None,
                  hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
-                 bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec"):
+                 bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
+                 manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None):
         self.client = client
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
@@ -106,6 +107,8 @@ class Kubelet:
             from .kubeletconfig import DynamicConfig
             self.dynamic = DynamicConfig(self, dynamic_config_dir)
         self.pod_manifest_path = pod_manifest_path
+        self.manifest_url, self.manifest_url_headers = manifest_url, manifest_url_headers
+        self.reserved = [dict(kube_reserved or {}), dict(system_reserved or {})]
         self.static_pods = None
         self.eviction = None
         self.eviction_interval = eviction_interval
@@ -196,9 +199,10 @@ class Kubelet:
         self.informer.start()
         self._tasks.append(asyncio.ensure_future(self._node_status_loop()))
         await self.informer.wait_synced(60)
-        if self.pod_manifest_path:
+        if self.pod_manifest_path or self.manifest_url:
             from .config import StaticPodSource
-            self.static_pods = StaticPodSource(self, self.pod_manifest_path)
+            self.static_pods = StaticPodSource(self, self.pod_manifest_path, url=self.manifest_url,
+                                               url_headers=self.manifest_url_headers)
             self.static_pods.start()
         if self.eviction is not None:
             self._tasks.append(asyncio.ensure_future(self._eviction_loop()))
@@ -293,7 +297,7 @@ class Kubelet:
                  {"type": "Ready", "status": "False", "reason": "KubeletNotReady",
                   "message": f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady message:{net_err}",
                   "lastHeartbeatTime": now, "lastTransitionTime": now})
-        st = {"capacity": capacity, "allocatable": dict(capacity),
+        st = {"capacity": capacity, "allocatable": self._allocatable(capacity),
               "conditions": [
                   ready,
                   {"type": "MemoryPressure", "status": "True" if mem_p else "False",
@@ -311,6 +315,24 @@ class Kubelet:
         if ers:
             st["extendedResources"] = ers
         return st
+
+    def _allocatable(self, capacity):
+        """`pkg/kubelet/cm/node_container_manager.go` GetNodeAllocatableReservation:
+        allocatable = capacity − kube-reserved − system-reserved − hard eviction threshold
+        (memory.available), floored at zero."""
+        if not any(self.reserved) and self.eviction is None:
+            return dict(capacity)
+        out = dict(capacity)
+        for res in ("cpu", "memory", "ephemeral-storage"):
+            if res not in capacity:
+                continue
+            total = parse_quantity(str(capacity[res]))
+            cut = sum(parse_quantity(str(r[res])).milli_value() for r in self.reserved if res in r)
+            if res == "memory" and self.eviction is not None:
+                cut += self.eviction.hard_memory_bytes() * 1000
+            left = max(0, total.milli_value() - cut)
+            out[res] = f"{left}m" if res == "cpu" else str(left // 1000)
+        return out
 
     def _collect_plugin_labels(self):
         labels = {}
@@ -681,6 +703,15 @@ class Kubelet:
         except Exception as e:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
             return None
+        post = ((c.get("lifecycle") or {}).get("postStart"))
+        if post:
+            # `pkg/kubelet/lifecycle/handlers.go` RunHandler: a failed postStart kills the container
+            from .prober import run_probe
+            ok, msg = await run_probe(self.runtime, st.pod, c, cid, dict(post, timeoutSeconds=30), st.ip)
+            if not ok:
+                self.recorder.event(st.pod, "Warning", "FailedPostStartHook", f"PostStart hook failed: {msg}")
+                await self.runtime.stop_container(cid, 0)
+                return cid
         if c.get("livenessProbe") or c.get("readinessProbe"):
             self.probes.start(st.uid, st.pod, c, cid)
         return cid
@@ -848,6 +879,24 @@ class Kubelet:
         if self.cpu_manager is not None:
             self.cpu_manager.release_pod(st.uid)
         rt = self.runtime
+        spec = st.pod.get("spec") or {}
+        by_name = {c["name"]: c for c in spec.get("containers") or ()}
+        from .prober import run_probe
+        pre = [(name, cid, (by_name[name].get("lifecycle") or {}).get("preStop")) for name, cid in st.containers.items()
+               if cid is not None and name in by_name]
+        hooks = [(name, cid, h) for name, cid, h in pre if h]
+        if hooks:
+            # preStop handlers run (concurrently) within the grace period before the stop signal
+            budget = float(grace if grace is not None else spec.get("terminationGracePeriodSeconds", 30))
+
+            async def hook(name, cid, h):
+                ok, msg = await run_probe(rt, st.pod, by_name[name], cid, dict(h, timeoutSeconds=max(budget, 1.0)), st.ip)
+                if not ok:
+                    self.recorder.event(st.pod, "Warning", "FailedPreStopHook", f"PreStop hook failed: {msg}")
+            try:
+                await asyncio.wait_for(asyncio.gather(*(hook(*x) for x in hooks)), max(budget, 0.5))
+            except asyncio.TimeoutError:
+                pass
         for cid in list(st.containers.values()) + list(st.init_containers.values()):
             if cid is not None:
                 await rt.stop_container(cid, min(float(grace or 0), 2.0))

@@ -1,0 +1,108 @@
+"""Container lifecycle hooks (postStart / preStop), node-allocatable reservations and the HTTP
+pod source (--manifest-url). Reference: pkg/kubelet/lifecycle/handlers.go,
+pkg/kubelet/cm/node_container_manager.go, pkg/kubelet/config/http.go."""
+import json
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from kubernetes_amd.api.quantity import parse_quantity
+from kubernetes_amd.cluster import LocalCluster
+
+
+def test_post_start_and_pre_stop_hooks(run, tmp_path):
+    marks = tmp_path / "marks"
+    marks.mkdir()
+
+    async def main():
+        cl = LocalCluster(nodes=1, gpus_per_node=0, runtime="process", workdir=str(tmp_path / "c"))
+        await cl.start()
+        c = cl.client
+        try:
+            await c.create("pods", {"metadata": {"name": "hooked"}, "spec": {"containers": [{
+                "name": "c", "image": "busybox", "command": ["sh", "-c", "sleep 30"],
+                "lifecycle": {"postStart": {"exec": {"command": ["sh", "-c", f"echo up > {marks}/post"]}},
+                              "preStop": {"exec": {"command": ["sh", "-c", f"echo down > {marks}/pre"]}}}}]}},
+                "default")
+
+            async def running():
+                p = await c.get("pods", "hooked", "default")
+                return p if (p.get("status") or {}).get("phase") == "Running" else None
+            await cl.wait_for(running, 20)
+            assert (marks / "post").read_text().strip() == "up"
+            assert not (marks / "pre").exists()
+            await c.delete("pods", "hooked", "default", grace_period=5)
+
+            async def stopped():
+                return (marks / "pre").exists()
+            await cl.wait_for(stopped, 20)
+            assert (marks / "pre").read_text().strip() == "down"
+            # a failing postStart kills the container and records the event
+            await c.create("pods", {"metadata": {"name": "badhook"}, "spec": {"restartPolicy": "Never", "containers": [{
+                "name": "c", "image": "busybox", "command": ["sh", "-c", "sleep 30"],
+                "lifecycle": {"postStart": {"exec": {"command": ["sh", "-c", "exit 7"]}}}}]}}, "default")
+
+            async def failed_event():
+                evs = (await c.list("events", "default"))["items"]
+                return any(e.get("reason") == "FailedPostStartHook" and e["involvedObject"]["name"] == "badhook" for e in evs)
+            await cl.wait_for(failed_event, 20)
+        finally:
+            await cl.stop()
+    run(main(), timeout=90)
+
+
+def test_node_allocatable_reservations(run, tmp_path):
+    async def main():
+        cl = LocalCluster(nodes=1, gpus_per_node=0, workdir=str(tmp_path / "c"),
+                          kubelet_kwargs={"cpu": "16", "memory": "64Gi", "kube_reserved": {"cpu": "1", "memory": "2Gi"},
+                                          "system_reserved": {"cpu": "500m", "memory": "1Gi"},
+                                          "eviction_hard": "memory.available<512Mi"})
+        await cl.start()
+        try:
+            n = await cl.client.get("nodes", "node-0")
+            cap, alloc = n["status"]["capacity"], n["status"]["allocatable"]
+            assert parse_quantity(cap["cpu"]).milli_value() == 16000
+            assert parse_quantity(alloc["cpu"]).milli_value() == 14500
+            want_mem = (64 << 30) - (2 << 30) - (1 << 30) - (512 << 20)
+            assert parse_quantity(alloc["memory"]).int_value() == want_mem
+        finally:
+            await cl.stop()
+    run(main(), timeout=60)
+
+
+def test_http_pod_source(run, tmp_path):
+    manifest = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "from-url", "namespace": "kube-system"},
+                "spec": {"containers": [{"name": "c", "image": "busybox"}]}}
+    served = {"body": json.dumps(manifest).encode(), "auth": []}
+
+    class H(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            served["auth"].append(self.headers.get("X-Token"))
+            self.send_response(200)
+            self.end_headers()
+            self.wfile.write(served["body"])
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    url = f"http://127.0.0.1:{srv.server_address[1]}/pods.json"
+
+    async def main():
+        cl = LocalCluster(nodes=0, gpus_per_node=0, workdir=str(tmp_path / "c"))
+        await cl.start()
+        try:
+            cl.kubelet_kwargs = {"manifest_url": url, "manifest_url_headers": {"X-Token": "abc"}}
+            await cl.add_node("node-0")
+
+            async def mirrored():
+                try:
+                    return await cl.client.get("pods", "from-url-node-0", "kube-system")
+                except Exception:
+                    return None
+            p = await cl.wait_for(mirrored, 20)
+            assert p["metadata"]["annotations"]["kubernetes.io/config.source"] == "http"
+            assert served["auth"][0] == "abc"
+        finally:
+            await cl.stop()
+            srv.shutdown()
+    run(main(), timeout=60)
