@@ -33,8 +33,14 @@ def mem_q(b):
 
 
 class MetricsServer:
-    def __init__(self, client, resolution=60.0):
+    def __init__(self, client, resolution=60.0, history_path=None):
         self.client = client
+        # JSON-lines usage history for the InitialResources admission plugin (the reference's
+        # heapster → influxdb sink): one sample per container per scrape, keyed by image.
+        self.history = None
+        if history_path:
+            from .apiserver.admission.estimation import UsageHistory
+            self.history = UsageHistory(history_path)
         self.resolution = resolution
         self.nodes: dict = {}       # node -> NodeMetrics
         self.pods: dict = {}        # (ns, name) -> PodMetrics
@@ -87,6 +93,22 @@ class MetricsServer:
                     "timestamp": ts, "window": f"{int(self.resolution)}s", "containers": cs}
         self.nodes, self.pods = nodes_out, pods_out
         self.scrapes += 1
+        if self.history is not None and pods_out:
+            await self._record_history(pods_out)
+
+    async def _record_history(self, pods_out):
+        images = {}
+        for p in (await self.client.list("pods"))["items"]:
+            md = p["metadata"]
+            for c in (p.get("spec") or {}).get("containers") or ():
+                images[(md.get("namespace"), md["name"], c["name"])] = c.get("image", "")
+        now = time.time()
+        for (ns, name), pm in pods_out.items():
+            for c in pm["containers"]:
+                img = images.get((ns, name, c["name"]))
+                if img:
+                    self.history.record(ns, img, int(c["usage"]["cpu"].rstrip("m")),
+                                        int(c["usage"]["memory"].rstrip("Ki")) * 1024, ts=now)
 
     async def _loop(self):
         while True:
@@ -178,12 +200,14 @@ def main(argv=None):
     ap.add_argument("--metric-resolution", type=float, default=60.0)
     ap.add_argument("--bind-address", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--usage-history-file", default=None,
+                    help="append per-container usage samples (InitialResources data source)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
 
     async def start():
-        ms = await MetricsServer(Client(a.master), a.metric_resolution).start(a.bind_address, a.port)
+        ms = await MetricsServer(Client(a.master), a.metric_resolution, a.usage_history_file).start(a.bind_address, a.port)
         print(f"metrics-server serving {GROUP}/{VERSION} on {a.bind_address}:{ms.port}", flush=True)
         return ms
     run_until_signal(start)
