@@ -155,4 +155,18 @@ def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local"):
                                                         "command": [sys.executable, "-m", "kubernetes_amd.cmd.device_plugin"],
                                                         "volumeMounts": [{"name": "dp", "mountPath": "/var/lib/kubelet/device-plugins"}]}],
                                         "volumes": [{"name": "dp", "hostPath": {"path": "/var/lib/kubelet/device-plugins"}}]}}}},
+        {"apiVersion": "apps/v1", "kind": "DaemonSet",
+         "metadata": {"name": "node-problem-detector", "namespace": "kube-system",
+                      "labels": dict(lab, **{"k8s-app": "node-problem-detector"})},
+         "spec": {"selector": {"matchLabels": {"k8s-app": "node-problem-detector"}},
+                  "template": {"metadata": {"labels": {"k8s-app": "node-problem-detector"}},
+                               "spec": {"hostNetwork": True,
+                                        "tolerations": [{"operator": "Exists", "effect": "NoSchedule"}],
+                                        "containers": [{"name": "node-problem-detector", "image": "kubernetes-amd/hyperkube",
+                                                        "command": [sys.executable, "-m", "kubernetes_amd.cmd.npd",
+                                                                    "--kernel-log", "/var/log/kern.log", "--amd-smi"],
+                                                        "env": [{"name": "NODE_NAME",
+                                                                 "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
+                                                        "volumeMounts": [{"name": "log", "mountPath": "/var/log", "readOnly": True}]}],
+                                        "volumes": [{"name": "log", "hostPath": {"path": "/var/log"}}]}}}},
     ]

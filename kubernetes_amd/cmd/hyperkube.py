@@ -25,6 +25,7 @@ COMPONENTS = {
     "hollow-node": "hollow_node", "kubemark": "hollow_node",
     "local-up": "local_up", "local-up-cluster": "local_up",
     "csi-hostpath": "csi_hostpath",
+    "node-problem-detector": "npd", "npd": "npd",
     "gendocs": "gendocs",
 }
 

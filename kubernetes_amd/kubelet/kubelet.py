@@ -408,8 +408,10 @@ class Kubelet:
         self._collect_plugin_labels()
         st = self._node_status()
         try:
+            # strategic merge (conditions keyed by type), as the reference's PatchNodeStatus, so
+            # conditions owned by others (node-problem-detector) survive the kubelet's heartbeat
             patch = {"status": st}
-            got = await self.client.patch("nodes", self.node_name, patch, None, "merge", "status")
+            got = await self.client.patch("nodes", self.node_name, patch, None, "strategic", "status")
             self._observe_pod_cidr(got)
             if self.plugin_labels:
                 cur = self.informer_node_labels
