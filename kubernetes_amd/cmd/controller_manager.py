@@ -25,6 +25,10 @@ def main(argv=None):
     ap.add_argument("--allocate-node-cidrs", action="store_true")
     ap.add_argument("--cluster-cidr", default="10.244.0.0/16")
     ap.add_argument("--node-cidr-mask-size", type=int, default=24)
+    ap.add_argument("--configure-cloud-routes", action="store_true",
+                    help="run the route controller: program a route to every node's pod CIDR (with --allocate-node-cidrs)")
+    ap.add_argument("--route-table", default="ip", choices=("ip", "memory"),
+                    help="where routes go: 'ip' (ip route on this gateway host) or 'memory'")
     ap.add_argument("--loadbalancer-ip-range", default="",
                     help="on-prem LoadBalancer pool ('10.0.5.10-10.0.5.50' or a CIDR); enables the service controller")
     ap.add_argument("-v", type=int, default=0)
@@ -46,10 +50,13 @@ def main(argv=None):
                 "csrsigning": {"cert_file": a.cluster_signing_cert_file, "key_file": a.cluster_signing_key_file},
                 "horizontalpodautoscaling": {"sync_period": a.horizontal_pod_autoscaler_sync_period},
                 "nodeipam": {"cluster_cidr": a.cluster_cidr, "node_cidr_mask_size": a.node_cidr_mask_size},
+                "route": {"cluster_cidr": a.cluster_cidr, "routes": a.route_table},
                 "service": {"ip_range": a.loadbalancer_ip_range}}
         enabled = a.controllers.split(",")
         if a.allocate_node_cidrs:
             enabled.append("nodeipam")
+            if a.configure_cloud_routes:
+                enabled.append("route")
         if a.loadbalancer_ip_range:
             enabled.append("service")
         return await ControllerManager(client, enabled, opts).start()

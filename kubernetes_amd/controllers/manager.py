@@ -18,7 +18,7 @@ from .certificates import (BootstrapSignerController, ClusterRoleAggregationCont
                            CSRSigningController, TokenCleanerController, TokensController, TTLController)
 from .podautoscaler import HorizontalController
 from .attachdetach import AttachDetachController, ExternalAttacher
-from .network import NodeIPAMController, ServiceLBController
+from .network import NodeIPAMController, RouteController, ServiceLBController
 from .volume import ExpandController, PersistentVolumeController, PVCProtectionController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
@@ -52,6 +52,7 @@ CONTROLLERS = {
     "persistentvolume-binder": PersistentVolumeController,
     "pvc-protection": PVCProtectionController,
     "nodeipam": NodeIPAMController,
+    "route": RouteController,
     "service": ServiceLBController,
     "attachdetach": AttachDetachController,
     "persistentvolume-expander": ExpandController,
@@ -61,7 +62,7 @@ CONTROLLERS = {
 
 # like ControllersDisabledByDefault: "*" does not start these (name them explicitly, or the
 # command line enables them from --allocate-node-cidrs / --loadbalancer-ip-range)
-DISABLED_BY_DEFAULT = {"nodeipam", "service", "csi-attacher"}
+DISABLED_BY_DEFAULT = {"nodeipam", "route", "service", "csi-attacher"}
 
 
 def resolve(enabled):

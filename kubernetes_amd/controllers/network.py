@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ipaddress
 
+from ..api.meta import now_rfc3339
 from ..client.rest import APIStatusError, is_not_found
 from .base import Controller, split_key
 
@@ -185,3 +186,133 @@ class ServiceLBController(Controller):
         if cur != [{"ip": ip}]:
             await self.client.patch("services", name, {"status": {"loadBalancer": {"ingress": [{"ip": ip}]}}}, ns,
                                     "merge", "status")
+
+
+class MemoryRoutes:
+    """Route table behind the route controller (the reference's `cloudprovider.Routes`):
+    `list()` → [{"name", "targetNode", "destinationCIDR", "blackhole"}], `create(hint, route)`,
+    `delete(route)`. This one keeps the table in memory (tests, single-host clusters)."""
+
+    def __init__(self, routes=None):
+        self.routes: dict[str, dict] = {r["name"]: dict(r) for r in routes or ()}
+        self.fail: set[str] = set()          # target nodes whose creation fails (fault injection)
+
+    def list(self):
+        return [dict(r) for r in self.routes.values()]
+
+    def create(self, hint, route):
+        if route["targetNode"] in self.fail:
+            raise RuntimeError(f"route to {route['targetNode']} refused")
+        self.routes[hint] = dict(route, name=hint, blackhole=False)
+
+    def delete(self, route):
+        self.routes.pop(route["name"], None)
+
+
+class IPRoutes(MemoryRoutes):
+    """On-prem route table on a gateway host: `ip route replace <podCIDR> via <node InternalIP>`
+    (`ip route del` on removal). `runner` executes argv lists (injected for tests / dry-run)."""
+
+    def __init__(self, node_ip, runner=None):
+        super().__init__()
+        self.node_ip = node_ip               # node name -> InternalIP
+        import subprocess
+        self.runner = runner or (lambda argv: subprocess.run(argv, check=True, capture_output=True))
+
+    def create(self, hint, route):
+        ip = self.node_ip(route["targetNode"])
+        if not ip:
+            raise RuntimeError(f"node {route['targetNode']} has no InternalIP")
+        self.runner(["ip", "route", "replace", route["destinationCIDR"], "via", ip])
+        super().create(hint, route)
+
+    def delete(self, route):
+        self.runner(["ip", "route", "del", route["destinationCIDR"]])
+        super().delete(route)
+
+
+class RouteController(Controller):
+    """`pkg/controller/route/route_controller.go:123-262`: every node with a `spec.podCIDR`
+    gets a route to it (created with the node UID as name hint, up to `MAX_RETRIES` tries,
+    `FailedToCreateRoute` event on failure); the node's `NetworkUnavailable` condition is set
+    False/`RouteCreated` once its route exists and True/`NoRouteCreated` when creation failed;
+    routes inside the cluster CIDR that are blackholes or point at a node with a different (or
+    no) CIDR are deleted. On-prem there is no cloud route API, so the table is pluggable
+    (`MemoryRoutes`, `IPRoutes`). All nodes reconcile under one key, as the reference's
+    periodic `reconcileNodeRoutes`."""
+    name = "route"
+    workers = 1
+    MAX_RETRIES = 5
+    KEY = "routes"
+
+    def __init__(self, client, factory, cluster_cidr="10.244.0.0/16", routes=None, **kw):
+        super().__init__(client, factory, **kw)
+        self.cluster = ipaddress.ip_network(cluster_cidr, strict=False)
+        if routes == "ip":
+            routes = IPRoutes(self._node_ip)
+        self.routes = routes if routes not in (None, "memory") else MemoryRoutes()
+
+    def _node_ip(self, name):
+        node = self.node_inf.get(name) or {}
+        return next((a["address"] for a in (node.get("status") or {}).get("addresses") or ()
+                     if a.get("type") == "InternalIP"), None)
+
+    def setup(self):
+        self.node_inf = self.factory.get("nodes")
+        self.node_inf.add_handler(lambda n: self.enqueue(self.KEY), lambda o, n: self.enqueue(self.KEY),
+                                  lambda n: self.enqueue(self.KEY))
+
+    def _responsible(self, route):
+        try:
+            return ipaddress.ip_network(route["destinationCIDR"], strict=False).subnet_of(self.cluster)
+        except (ValueError, TypeError):
+            return False
+
+    async def _set_condition(self, node_name, created):
+        now = now_rfc3339()
+        cond = ({"type": "NetworkUnavailable", "status": "False", "reason": "RouteCreated",
+                 "message": "RouteController created a route"} if created else
+                {"type": "NetworkUnavailable", "status": "True", "reason": "NoRouteCreated",
+                 "message": "RouteController failed to create a route"})
+        cond.update(lastHeartbeatTime=now, lastTransitionTime=now)
+        try:
+            await self.client.patch("nodes", node_name, {"status": {"conditions": [cond]}}, None, "strategic", "status")
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise
+
+    async def sync(self, key):
+        nodes = self.node_inf.list()
+        table = self.routes.list()
+        by_target = {r["targetNode"]: r for r in table if r.get("targetNode")}
+        cidrs = {}
+        for node in nodes:
+            name = node["metadata"]["name"]
+            cidr = (node.get("spec") or {}).get("podCIDR")
+            if not cidr:
+                continue
+            cidrs[name] = cidr
+            r = by_target.get(name)
+            if r is None or r["destinationCIDR"] != cidr:
+                route = {"targetNode": name, "destinationCIDR": cidr}
+                err = None
+                for _ in range(self.MAX_RETRIES):
+                    try:
+                        self.routes.create(node["metadata"].get("uid") or name, route)
+                        err = None
+                        break
+                    except Exception as e:  # noqa: BLE001 - provider errors are retried, then reported
+                        err = e
+                await self._set_condition(name, err is None)
+                if err is not None:
+                    self.recorder.event({"kind": "Node", "metadata": {"name": name, "uid": name, "namespace": ""}},
+                                        "Warning", "FailedToCreateRoute",
+                                        f"Could not create route {cidr} for node {name}: {err}")
+            else:
+                cur = next((c for c in (node.get("status") or {}).get("conditions") or ()
+                            if c.get("type") == "NetworkUnavailable"), None)
+                if cur is None or cur.get("status") != "False":
+                    await self._set_condition(name, True)
+        for r in table:
+            if self._responsible(r) and (r.get("blackhole") or cidrs.get(r.get("targetNode")) != r["destinationCIDR"]):
+                self.routes.delete(r)
