@@ -123,10 +123,13 @@ class AddonManager:
             await asyncio.sleep(self.period)
 
 
-def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local"):
-    """Manifests for the built-in add-ons (written by `kubeadm` / local-up)."""
+def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local", master="http://127.0.0.1:8080"):
+    """Manifests for the built-in add-ons (written by `kubeadm` / local-up). `master` is the API
+    server URL the hostNetwork add-ons (node-problem-detector) talk to."""
     lab = {MODE: RECONCILE}
     import sys
+
+    from ..deviceplugin.api import DEVICE_MANAGER_PATH
     return [
         {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "kube-dns", "namespace": "kube-system",
                                                                     "labels": dict(lab)}},
@@ -153,8 +156,10 @@ def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local"):
                                         "nodeSelector": {"feature.node.kubernetes.io/amd-gpu": "true"},
                                         "containers": [{"name": "amd-gpu-device-plugin", "image": "kubernetes-amd/hyperkube",
                                                         "command": [sys.executable, "-m", "kubernetes_amd.cmd.device_plugin"],
-                                                        "volumeMounts": [{"name": "dp", "mountPath": "/var/lib/kubelet/device-plugins"}]}],
-                                        "volumes": [{"name": "dp", "hostPath": {"path": "/var/lib/kubelet/device-plugins"}}]}}}},
+                                                        "volumeMounts": [{"name": "dp", "mountPath": DEVICE_MANAGER_PATH}]}],
+                                        # the fork's kubelet watches <DeviceManagerPath>/plugins (quirk Q5:
+                                        # the reference's GKE add-on mounts the upstream path and never registers)
+                                        "volumes": [{"name": "dp", "hostPath": {"path": DEVICE_MANAGER_PATH}}]}}}},
         {"apiVersion": "apps/v1", "kind": "DaemonSet",
          "metadata": {"name": "node-problem-detector", "namespace": "kube-system",
                       "labels": dict(lab, **{"k8s-app": "node-problem-detector"})},
@@ -164,7 +169,7 @@ def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local"):
                                         "tolerations": [{"operator": "Exists", "effect": "NoSchedule"}],
                                         "containers": [{"name": "node-problem-detector", "image": "kubernetes-amd/hyperkube",
                                                         "command": [sys.executable, "-m", "kubernetes_amd.cmd.npd",
-                                                                    "--kernel-log", "/var/log/kern.log", "--amd-smi"],
+                                                                    "--master", master, "--kernel-log", "/var/log/kern.log", "--amd-smi"],
                                                         "env": [{"name": "NODE_NAME",
                                                                  "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
                                                         "volumeMounts": [{"name": "log", "mountPath": "/var/log", "readOnly": True}]}],

@@ -25,6 +25,7 @@ import json
 import logging
 import os
 import re
+import stat
 from dataclasses import dataclass, field
 
 from ..api.meta import now_rfc3339
@@ -92,6 +93,49 @@ def default_kernel_monitor(log_path="/dev/kmsg") -> MonitorConfig:
     }, log_path)
 
 
+def _is_char_device(path) -> bool:
+    try:
+        return stat.S_ISCHR(os.stat(path).st_mode)
+    except OSError:
+        return False
+
+
+def parse_kmsg_record(rec: bytes) -> list:
+    """One /dev/kmsg record -> its message line(s). The header `prio,seq,ts,flags[,..];` is
+    dropped; continuation lines (leading space, `KEY=value` device metadata) are skipped;
+    `\\xNN` escapes the kernel applies to non-printable bytes are undone."""
+    text = rec.decode(errors="replace")
+    head, sep, body = text.partition(";")
+    if not sep or not head[:1].isdigit():
+        body = text                          # not a record header: treat as a plain line
+    lines = []
+    for i, ln in enumerate(body.split("\n")):
+        if i > 0 and (not ln or ln.startswith(" ")):
+            continue
+        if "\\x" in ln:
+            ln = re.sub(r"\\x([0-9a-fA-F]{2})", lambda mt: chr(int(mt.group(1), 16)), ln)
+        if ln:
+            lines.append(ln)
+    return lines
+
+
+def apiserver_url(master=None, env=None) -> str:
+    """Where an add-on pod finds the API server: --master, then $KUBERNETES_MASTER, then the
+    in-cluster service env ($KUBERNETES_SERVICE_HOST/_PORT; 443 is the service port that
+    forwards to the secure port, so only an explicit non-443 port is used as plain HTTP),
+    then the local insecure port — add-ons run hostNetwork on the control-plane node, as the
+    DNS add-on assumes (`cmd/dns.py`)."""
+    env = os.environ if env is None else env
+    if master:
+        return master
+    if env.get("KUBERNETES_MASTER"):
+        return env["KUBERNETES_MASTER"]
+    host, port = env.get("KUBERNETES_SERVICE_HOST"), env.get("KUBERNETES_SERVICE_PORT", "443")
+    if host and port not in ("443", "6443"):
+        return f"http://{host}:{port}"
+    return "http://127.0.0.1:8080"
+
+
 class NodeProblemDetector:
     """One per node. `check_once()` (tests) or `start()` (poll loop)."""
 
@@ -110,6 +154,7 @@ class NodeProblemDetector:
         self._dirty = True
         self._last_sent = 0.0
         self._offsets: dict[str, int] = {}
+        self._kmsg: dict[str, int] = {}          # record-device path -> non-blocking fd
         self._ecc_base: dict[int, int] = {}
         self._links_base: dict[int, int] = {}
         self._task = None
@@ -144,6 +189,8 @@ class NodeProblemDetector:
 
     # -- log monitors ----------------------------------------------------------
     def _new_lines(self, m: MonitorConfig):
+        if m.log_path in self._kmsg or _is_char_device(m.log_path):
+            return self._kmsg_lines(m)
         try:
             size = os.path.getsize(m.log_path)
         except OSError:
@@ -165,6 +212,49 @@ class NodeProblemDetector:
         cut = data.rfind(b"\n") + 1
         self._offsets[m.log_path] = off + cut
         return data[:cut].decode(errors="replace").splitlines()
+
+    def _kmsg_lines(self, m: MonitorConfig):
+        """/dev/kmsg is a record device: its size reads as 0 and every read() returns one
+        record `prio,seq,ts_us,flags[,...];message\\n` followed by ` KEY=value` continuation
+        lines. Open it non-blocking once, skip the backlog (unless lookback is asked: the
+        kernel then replays its ring buffer from the first record), read until EAGAIN.
+        NPD v0.4's kmsg watcher (`pkg/systemlogmonitor/logwatchers/kmsg`) reads it the same way."""
+        fd = self._kmsg.get(m.log_path)
+        if fd is None:
+            try:
+                fd = os.open(m.log_path, os.O_RDONLY | os.O_NONBLOCK)
+            except OSError as e:
+                log.warning("cannot open %s: %s", m.log_path, e)
+                return []
+            if not m.lookback_lines:
+                try:
+                    os.lseek(fd, 0, os.SEEK_END)        # SEEK_END = "after the newest record"
+                except OSError:
+                    pass
+            self._kmsg[m.log_path] = fd
+        out = []
+        while True:
+            try:
+                rec = os.read(fd, 8192)
+            except BlockingIOError:
+                break
+            except OSError as e:
+                if e.errno == 32:      # EPIPE: records were overwritten before we read them; continue
+                    continue
+                log.warning("reading %s failed: %s", m.log_path, e)
+                break
+            if not rec:
+                break
+            out.extend(parse_kmsg_record(rec))
+        return out
+
+    def close(self):
+        for fd in self._kmsg.values():
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+        self._kmsg.clear()
 
     def _scan_logs(self):
         for m in self.monitors:
@@ -246,6 +336,7 @@ class NodeProblemDetector:
                 pass
         await self.recorder.flush(1.0)
         self.recorder.stop()
+        self.close()
 
 
 def load_monitor(path, log_path=None) -> MonitorConfig:
@@ -253,30 +344,45 @@ def load_monitor(path, log_path=None) -> MonitorConfig:
         return MonitorConfig.from_dict(json.load(f), log_path)
 
 
-def main(argv=None):
+def parse_args(argv=None):
     import argparse
-    import sys
-
-    from ..client.rest import Client
-    from ..native import amdsmi
     ap = argparse.ArgumentParser("node-problem-detector")
-    in_cluster = (f"http://{os.environ['KUBERNETES_SERVICE_HOST']}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}"
-                  if os.environ.get("KUBERNETES_SERVICE_HOST") else None)
-    ap.add_argument("--apiserver-override", "--master", dest="master", default=in_cluster,
-                    required=in_cluster is None)
+    ap.add_argument("--apiserver-override", "--master", dest="master", default=None,
+                    help="API server URL (default: $KUBERNETES_MASTER, the in-cluster service, or http://127.0.0.1:8080)")
+    ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--hostname-override", default=os.environ.get("NODE_NAME") or os.uname().nodename)
     ap.add_argument("--system-log-monitors", default="", help="comma-separated monitor JSON files")
-    ap.add_argument("--kernel-log", default="/dev/kmsg", help="log for the built-in kernel monitor")
+    ap.add_argument("--kernel-log", default="/dev/kmsg",
+                    help="log for the built-in kernel monitor: /dev/kmsg (record device) or a text log such as /var/log/kern.log")
     ap.add_argument("--amd-smi", action="store_true", help="enable the AMD SMI GPU monitor")
     ap.add_argument("--smi-fixture", default=None)
     ap.add_argument("--period", type=float, default=1.0)
-    args = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, stream=sys.stderr)
+    return ap.parse_args(argv)
+
+
+def build_detector(args):
+    """argv -> (client, NodeProblemDetector) without starting anything (tests use this with the
+    DaemonSet manifest's own command line)."""
+    from ..client.clientcmd import client_from
+    from ..client.rest import Client
+    from ..native import amdsmi
     mons = [load_monitor(p) for p in args.system_log_monitors.split(",") if p] or [default_kernel_monitor(args.kernel_log)]
+    for m in mons:
+        if not os.path.exists(m.log_path):
+            log.warning("log %s does not exist yet; the monitor starts reading once it appears", m.log_path)
     smi = amdsmi.SMI(args.smi_fixture) if (args.amd_smi or args.smi_fixture) else None
+    client = client_from(args.kubeconfig) if args.kubeconfig else Client(apiserver_url(args.master))
+    return client, NodeProblemDetector(client, args.hostname_override, mons, smi, args.period)
+
+
+def main(argv=None):
+    import sys
+    args = parse_args(argv)
+    logging.basicConfig(level=logging.INFO, stream=sys.stderr)
 
     async def run():
-        npd = await NodeProblemDetector(Client(args.master), args.hostname_override, mons, smi, args.period).start()
+        _, det = build_detector(args)
+        npd = await det.start()
         try:
             await asyncio.Event().wait()
         finally:

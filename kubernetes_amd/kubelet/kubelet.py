@@ -348,6 +348,7 @@ class Kubelet:
         for attempt in range(50):
             try:
                 got = await self.client.create("nodes", node)
+                self._published_ers = set(node["status"].get("extendedResources") or ())
                 self.node_uid = got["metadata"]["uid"]
                 self._observe_pod_cidr(got)
                 return
@@ -404,14 +405,40 @@ class Kubelet:
             self.network.set_pod_cidr(cidr)
             self._status_dirty.set()
 
+    def _device_status_patch(self, st):
+        """A merge patch only ever adds map keys, so device state that went away must be
+        spelled out (`pkg/kubelet/kubelet_node_status.go:608-623` zeroes the capacity of the
+        resources `GetCapacity` reports removed):
+          * a resource published before but gone now: capacity/allocatable "0" and its
+            `extendedResources` entry deleted (null);
+          * a resource still present: its domain is sent with `$patch: replace`, so device IDs
+            the plugin dropped disappear instead of lingering as Healthy on the server (the
+            scheduler cache allocates from that map)."""
+        st = dict(st)
+        ers = st.get("extendedResources") or {}
+        gone = getattr(self, "_published_ers", set()) - set(ers)
+        if not ers and not gone:
+            return st
+        out = {r: dict(dom, **{"$patch": "replace"}) for r, dom in ers.items()}
+        if gone:
+            st["capacity"] = dict(st["capacity"])
+            st["allocatable"] = dict(st["allocatable"])
+            for r in gone:
+                st["capacity"][r] = "0"
+                st["allocatable"][r] = "0"
+                out[r] = None
+        st["extendedResources"] = out
+        return st
+
     async def update_node_status(self):
         self._collect_plugin_labels()
         st = self._node_status()
         try:
             # strategic merge (conditions keyed by type), as the reference's PatchNodeStatus, so
             # conditions owned by others (node-problem-detector) survive the kubelet's heartbeat
-            patch = {"status": st}
+            patch = {"status": self._device_status_patch(st)}
             got = await self.client.patch("nodes", self.node_name, patch, None, "strategic", "status")
+            self._published_ers = set(st.get("extendedResources") or ())
             self._observe_pod_cidr(got)
             if self.plugin_labels:
                 cur = self.informer_node_labels

@@ -203,3 +203,53 @@ def test_merge_init_responses_first_wins():
     o = merge_init_responses([r1, r2])
     assert o["envs"] == [{"name": "A", "value": "1"}, {"name": "B", "value": "3"}]
     assert [d["pathOnHost"] for d in o["devices"]] == ["/dev/kfd"]
+
+
+def test_node_status_drops_removed_devices_and_resources(tmp_path, run):
+    """Unregistering a plugin (or dropping one of its devices) must reach the API server: the
+    node-status patch only adds map keys otherwise, and the scheduler cache would keep
+    allocating the stale Healthy IDs. Reference: `kubelet_node_status.go:608-623`
+    zeroes removed resources."""
+    from kubernetes_amd.cluster import LocalCluster
+
+    async def main():
+        import tempfile
+        cl = LocalCluster(nodes=1, gpus_per_node=0, emit_events=False,
+                          workdir=tempfile.mkdtemp(prefix="kdm", dir="/tmp"))   # unix socket path < 108 chars
+        await cl.start()
+        n = cl.nodes[0]
+        p = DevicePluginServer("amd.com/gpu", os.path.join(n.plugins_dir, "amd.com", "stub.sock"),
+                               [device("g0"), device("g1"), device("g2")])
+        try:
+            await p.start()
+
+            async def server_devs():
+                node = await cl.client.get("nodes", n.name)
+                dom = (node["status"].get("extendedResources") or {}).get("amd.com/gpu")
+                return node, (set(dom["resources"]) if dom else None)
+            await cl.wait_for(lambda: _eq(server_devs, {"g0", "g1", "g2"}))
+            p.update([device("g0"), device("g2")])
+            node = await cl.wait_for(lambda: _eq(server_devs, {"g0", "g2"}))
+            assert node["status"]["capacity"]["amd.com/gpu"] == "2"
+            ni = cl.scheduler.cache.nodes[n.name]
+            await cl.wait_for(lambda: _const(set(ni.er.allocatable.get("amd.com/gpu", {})) == {"g0", "g2"}))
+            await p.stop()
+            node = await cl.wait_for(lambda: _eq(server_devs, None))
+            assert node["status"]["capacity"]["amd.com/gpu"] == "0"
+            assert node["status"]["allocatable"]["amd.com/gpu"] == "0"
+            await cl.wait_for(lambda: _const("amd.com/gpu" not in cl.scheduler.cache.nodes[n.name].er.allocatable))
+        finally:
+            try:
+                await p.stop()
+            finally:
+                await cl.stop()
+    run(main())
+
+
+async def _eq(fn, want):
+    node, got = await fn()
+    return node if got == want else None
+
+
+async def _const(v):
+    return v

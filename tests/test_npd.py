@@ -91,3 +91,56 @@ def test_npd_custom_monitor_file(tmp_path):
     npd = NodeProblemDetector(None, "n", [m])
     npd._scan_logs()          # lookback: the existing line is read
     assert npd.recorder.emitted[0][1] == "CorruptDockerImage"
+
+
+def test_parse_kmsg_record():
+    from kubernetes_amd.addons.npd import parse_kmsg_record
+    rec = (b"3,1234,5678901,-;amdgpu 0000:05:00.0: amdgpu: ring gfx_0.0.0 timeout, signaled seq=1\n"
+           b" SUBSYSTEM=pci\n DEVICE=+pci:0000:05:00.0\n")
+    assert parse_kmsg_record(rec) == ["amdgpu 0000:05:00.0: amdgpu: ring gfx_0.0.0 timeout, signaled seq=1"]
+    assert parse_kmsg_record(b"6,7,8,c;tab\\x09here\n") == ["tab\there"]
+
+
+def test_npd_reads_record_device(tmp_path, monkeypatch):
+    """/dev/kmsg reads as size 0: the monitor must read it record by record."""
+    import os
+
+    from kubernetes_amd.addons import npd as npd_mod
+    fifo = str(tmp_path / "kmsg")
+    os.mkfifo(fifo)
+    monkeypatch.setattr(npd_mod, "_is_char_device", lambda p: p == fifo)
+    wfd = None
+    det = NodeProblemDetector(None, "n", [default_kernel_monitor(fifo)])
+    try:
+        assert det._new_lines(det.monitors[0]) == []          # opens non-blocking, nothing yet
+        wfd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+        os.write(wfd, b"3,99,100,-;amdgpu 0000:75:00.0: amdgpu: GPU reset(2) failed\n SUBSYSTEM=pci\n")
+        det._scan_logs()
+        c = det.conditions["AMDGPUHardwareError"]
+        assert c["status"] == "True" and c["reason"] == "AMDGPUResetFailed"
+        assert "SUBSYSTEM" not in c["message"]
+    finally:
+        det.close()
+        if wfd is not None:
+            os.close(wfd)
+
+
+def test_npd_daemonset_argv_reaches_apiserver(monkeypatch):
+    """The add-on manifest's own command line must parse and point at a reachable API server
+    even without KUBERNETES_SERVICE_HOST (argparse used to exit)."""
+    from kubernetes_amd.addons.manager import default_addons
+    from kubernetes_amd.addons.npd import apiserver_url, build_detector, parse_args
+    monkeypatch.delenv("KUBERNETES_SERVICE_HOST", raising=False)
+    monkeypatch.delenv("KUBERNETES_MASTER", raising=False)
+    ds = [o for o in default_addons() if o["metadata"]["name"] == "node-problem-detector"][0]
+    cmd = ds["spec"]["template"]["spec"]["containers"][0]["command"]
+    i = cmd.index("kubernetes_amd.cmd.npd")
+    args = parse_args(cmd[i + 1:] + ["--smi-fixture", amdsmi.fixture_file(2, seed="npdargv")])
+    client, det = build_detector(args)
+    assert client.url.startswith("http://127.0.0.1:8080")
+    assert det.monitors[0].log_path == "/var/log/kern.log"
+    assert apiserver_url(None, {}) == "http://127.0.0.1:8080"
+    assert apiserver_url(None, {"KUBERNETES_SERVICE_HOST": "10.96.0.1", "KUBERNETES_SERVICE_PORT": "443"}) == "http://127.0.0.1:8080"
+    assert apiserver_url(None, {"KUBERNETES_MASTER": "http://10.0.0.1:8080"}) == "http://10.0.0.1:8080"
+    dp = [o for o in default_addons() if o["metadata"]["name"] == "amd-gpu-device-plugin"][0]
+    assert dp["spec"]["template"]["spec"]["volumes"][0]["hostPath"]["path"] == "/var/lib/kubelet/device-plugin"
