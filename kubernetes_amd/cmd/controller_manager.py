@@ -29,6 +29,8 @@ def main(argv=None):
                     help="run the route controller: program a route to every node's pod CIDR (with --allocate-node-cidrs)")
     ap.add_argument("--route-table", default="ip", choices=("ip", "memory"),
                     help="where routes go: 'ip' (ip route on this gateway host) or 'memory'")
+    ap.add_argument("--route-reconciliation-period", type=float, default=10.0,
+                    help="seconds between full route reconciliations (besides node events)")
     ap.add_argument("--loadbalancer-ip-range", default="",
                     help="on-prem LoadBalancer pool ('10.0.5.10-10.0.5.50' or a CIDR); enables the service controller")
     ap.add_argument("-v", type=int, default=0)
@@ -50,7 +52,8 @@ def main(argv=None):
                 "csrsigning": {"cert_file": a.cluster_signing_cert_file, "key_file": a.cluster_signing_key_file},
                 "horizontalpodautoscaling": {"sync_period": a.horizontal_pod_autoscaler_sync_period},
                 "nodeipam": {"cluster_cidr": a.cluster_cidr, "node_cidr_mask_size": a.node_cidr_mask_size},
-                "route": {"cluster_cidr": a.cluster_cidr, "routes": a.route_table},
+                "route": {"cluster_cidr": a.cluster_cidr, "routes": a.route_table,
+                          "reconcile_period": a.route_reconciliation_period},
                 "service": {"ip_range": a.loadbalancer_ip_range}}
         enabled = a.controllers.split(",")
         if a.allocate_node_cidrs:

@@ -16,6 +16,7 @@ Parity:
 """
 from __future__ import annotations
 
+import asyncio
 import ipaddress
 
 from ..api.meta import now_rfc3339
@@ -206,18 +207,71 @@ class MemoryRoutes:
         self.routes[hint] = dict(route, name=hint, blackhole=False)
 
     def delete(self, route):
-        self.routes.pop(route["name"], None)
+        # a route is identified by name AND destination: a stale listing can name a route that
+        # has since been re-created under the same hint for a new CIDR
+        cur = self.routes.get(route["name"])
+        if cur is not None and cur["destinationCIDR"] == route["destinationCIDR"]:
+            del self.routes[route["name"]]
 
 
 class IPRoutes(MemoryRoutes):
     """On-prem route table on a gateway host: `ip route replace <podCIDR> via <node InternalIP>`
-    (`ip route del` on removal). `runner` executes argv lists (injected for tests / dry-run)."""
+    (`ip route del` on removal). `list()` reads the kernel table (`ip -o route show root
+    <clusterCIDR>`), mapping each gateway back to its node through the nodes' InternalIPs and
+    reporting `blackhole`/`unreachable`/`prohibit` entries as blackholes, so routes deleted or
+    added behind the controller's back — or left over from before a restart — are reconciled.
+    Connected (`dev`-only) routes, e.g. the gateway's own bridge, are never reported.
+    `runner` executes argv lists and returns their stdout (str/bytes/CompletedProcess); a
+    runner that returns nothing (dry-run) falls back to the in-memory view."""
 
-    def __init__(self, node_ip, runner=None):
+    BLACKHOLE_TYPES = ("blackhole", "unreachable", "prohibit")
+
+    def __init__(self, node_ip, runner=None, cluster_cidr="0.0.0.0/0", node_by_ip=None):
         super().__init__()
         self.node_ip = node_ip               # node name -> InternalIP
+        self.node_by_ip = node_by_ip or (lambda ip: None)
+        self.cluster_cidr = cluster_cidr
         import subprocess
-        self.runner = runner or (lambda argv: subprocess.run(argv, check=True, capture_output=True))
+        self.runner = runner or (lambda argv: subprocess.run(argv, check=True, capture_output=True, text=True).stdout)
+
+    @staticmethod
+    def _text(out):
+        if out is None:
+            return None
+        out = getattr(out, "stdout", out)
+        return out.decode() if isinstance(out, (bytes, bytearray)) else out
+
+    def parse(self, text):
+        routes = []
+        for ln in text.splitlines():
+            f = ln.split()
+            if not f:
+                continue
+            kind = "unicast"
+            if f[0] in self.BLACKHOLE_TYPES + ("unicast", "local", "broadcast", "multicast", "throw", "nat"):
+                kind, f = f[0], f[1:]
+            if not f or kind not in ("unicast",) + self.BLACKHOLE_TYPES:
+                continue
+            dst = f[0]
+            if "/" not in dst:
+                dst += "/32"
+            if kind in self.BLACKHOLE_TYPES:
+                routes.append({"name": f"{kind}:{dst}", "targetNode": "", "destinationCIDR": dst, "blackhole": True,
+                               "type": kind})
+                continue
+            if "via" not in f:
+                continue                      # connected route: not a node route
+            gw = f[f.index("via") + 1]
+            node = self.node_by_ip(gw) or ""
+            routes.append({"name": f"{node or gw}:{dst}", "targetNode": node, "destinationCIDR": dst,
+                           "blackhole": False, "via": gw})
+        return routes
+
+    def list(self):
+        text = self._text(self.runner(["ip", "-o", "route", "show", "root", self.cluster_cidr]))
+        if text is None:
+            return super().list()
+        return self.parse(text)
 
     def create(self, hint, route):
         ip = self.node_ip(route["targetNode"])
@@ -227,7 +281,10 @@ class IPRoutes(MemoryRoutes):
         super().create(hint, route)
 
     def delete(self, route):
-        self.runner(["ip", "route", "del", route["destinationCIDR"]])
+        argv = ["ip", "route", "del"]
+        if route.get("blackhole"):
+            argv.append(route.get("type") or "blackhole")
+        self.runner(argv + [route["destinationCIDR"]])
         super().delete(route)
 
 
@@ -245,11 +302,12 @@ class RouteController(Controller):
     MAX_RETRIES = 5
     KEY = "routes"
 
-    def __init__(self, client, factory, cluster_cidr="10.244.0.0/16", routes=None, **kw):
+    def __init__(self, client, factory, cluster_cidr="10.244.0.0/16", routes=None, reconcile_period=10.0, **kw):
         super().__init__(client, factory, **kw)
+        self.reconcile_period = reconcile_period
         self.cluster = ipaddress.ip_network(cluster_cidr, strict=False)
         if routes == "ip":
-            routes = IPRoutes(self._node_ip)
+            routes = IPRoutes(self._node_ip, cluster_cidr=str(self.cluster), node_by_ip=self._node_by_ip)
         self.routes = routes if routes not in (None, "memory") else MemoryRoutes()
 
     def _node_ip(self, name):
@@ -257,10 +315,29 @@ class RouteController(Controller):
         return next((a["address"] for a in (node.get("status") or {}).get("addresses") or ()
                      if a.get("type") == "InternalIP"), None)
 
+    def _node_by_ip(self, ip):
+        for node in self.node_inf.list():
+            if any(a.get("type") == "InternalIP" and a.get("address") == ip
+                   for a in (node.get("status") or {}).get("addresses") or ()):
+                return node["metadata"]["name"]
+        return None
+
     def setup(self):
         self.node_inf = self.factory.get("nodes")
         self.node_inf.add_handler(lambda n: self.enqueue(self.KEY), lambda o, n: self.enqueue(self.KEY),
                                   lambda n: self.enqueue(self.KEY))
+
+    def start(self):
+        """Besides node events, reconcile every `reconcile_period` seconds
+        (`route_controller.go` Run: `wait.NonSlidingUntil(reconcileNodeRoutes, syncPeriod)`,
+        --route-reconciliation-period, default 10 s): the table can change outside the controller."""
+        super().start()
+
+        async def periodic():
+            while True:
+                await asyncio.sleep(self.reconcile_period)
+                self.enqueue(self.KEY)
+        self._tasks.append(asyncio.ensure_future(periodic()))
 
     def _responsible(self, route):
         try:
@@ -313,6 +390,8 @@ class RouteController(Controller):
                             if c.get("type") == "NetworkUnavailable"), None)
                 if cur is None or cur.get("status") != "False":
                     await self._set_condition(name, True)
-        for r in table:
+        # re-list: the creates above may have replaced entries of the first listing (a node
+        # whose podCIDR changed keeps its name hint), which must not be deleted as stale
+        for r in self.routes.list():
             if self._responsible(r) and (r.get("blackhole") or cidrs.get(r.get("targetNode")) != r["destinationCIDR"]):
                 self.routes.delete(r)

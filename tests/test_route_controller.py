@@ -70,3 +70,68 @@ def test_ip_routes_provider():
         assert "no InternalIP" in str(e)
     else:
         raise AssertionError("expected failure")
+
+
+def test_ip_routes_lists_kernel_table():
+    """`list()` reads the kernel table: gateways map back to nodes, blackhole and
+    unreachable entries are blackholes, connected routes are not node routes."""
+    out = ("10.244.1.0/24 via 10.0.0.11 dev eth0 \n"
+           "10.244.2.0/24 via 10.0.0.99 dev eth0 proto static\n"
+           "blackhole 10.244.7.0/24 \n"
+           "unreachable 10.244.8.0/24 \n"
+           "10.244.0.0/24 dev cni0 proto kernel scope link src 10.244.0.1\n")
+    calls = []
+
+    def runner(argv):
+        calls.append(argv)
+        return out if argv[:3] == ["ip", "-o", "route"] else None
+    t = IPRoutes({"gpu-1": "10.0.0.11"}.get, runner=runner, cluster_cidr="10.244.0.0/16",
+                 node_by_ip={"10.0.0.11": "gpu-1"}.get)
+    rs = {r["destinationCIDR"]: r for r in t.list()}
+    assert calls[0] == ["ip", "-o", "route", "show", "root", "10.244.0.0/16"]
+    assert rs["10.244.1.0/24"]["targetNode"] == "gpu-1" and not rs["10.244.1.0/24"]["blackhole"]
+    assert rs["10.244.2.0/24"]["targetNode"] == ""          # gateway of no known node: stale
+    assert rs["10.244.7.0/24"]["blackhole"] and rs["10.244.8.0/24"]["blackhole"]
+    assert "10.244.0.0/24" not in rs
+    t.delete(rs["10.244.8.0/24"])
+    assert calls[-1] == ["ip", "route", "del", "unreachable", "10.244.8.0/24"]
+
+
+def test_route_follows_pod_cidr_change_and_periodic_reconcile(run):
+    """A node whose podCIDR changes keeps one route (the re-created route under the same name
+    hint is not deleted as stale), and a route removed outside the controller comes back on the
+    periodic reconcile without any node event."""
+    table = MemoryRoutes()
+
+    async def main():
+        s = APIServer()
+        c = Client(f"http://127.0.0.1:{await s.start()}")
+        await c.create("nodes", {"metadata": {"name": "n1"}, "spec": {"podCIDR": "10.244.1.0/24"}, "status": {}})
+        cm = await ControllerManager(c, ["route"], {"route": {"cluster_cidr": "10.244.0.0/16", "routes": table,
+                                                              "reconcile_period": 0.2}}).start()
+        try:
+            async def dests():
+                for _ in range(200):
+                    await asyncio.sleep(0.02)
+                    yield sorted(r["destinationCIDR"] for r in table.list())
+            async for d in dests():
+                if d == ["10.244.1.0/24"]:
+                    break
+            n = await c.get("nodes", "n1")
+            n["spec"]["podCIDR"] = "10.244.5.0/24"
+            await c.update("nodes", n)
+            async for d in dests():
+                if d == ["10.244.5.0/24"]:
+                    break
+            await asyncio.sleep(0.3)
+            assert sorted(r["destinationCIDR"] for r in table.list()) == ["10.244.5.0/24"]
+            table.routes.clear()                     # deleted behind the controller's back
+            async for d in dests():
+                if d == ["10.244.5.0/24"]:
+                    break
+            assert sorted(r["destinationCIDR"] for r in table.list()) == ["10.244.5.0/24"]
+        finally:
+            await cm.stop()
+            await c.close()
+            await s.stop()
+    run(main())
