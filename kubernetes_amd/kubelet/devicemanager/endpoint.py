@@ -79,6 +79,7 @@ class Endpoint:
         self.labels = {}
         self._call = None
         self._stopped = False
+        self.superseded = False      # a re-registration took over this endpoint's device store
 
     async def init(self):
         info = await self.stub.GetPluginInfo(api.DP["GetPluginInfoRequest"](), timeout=1.0)
@@ -99,9 +100,12 @@ class Endpoint:
         except asyncio.CancelledError:
             pass
         finally:
-            _, _, deleted = self.store.update([])
-            if deleted:
-                self.store.fire(self.resource_name, [], [], deleted)
+            # the stream ended: report every device deleted — unless a re-registering endpoint
+            # already owns this store (its devices live on under the new plugin)
+            if not self.superseded:
+                _, _, deleted = self.store.update([])
+                if deleted:
+                    self.store.fire(self.resource_name, [], [], deleted)
 
     async def init_container(self, req):
         return await self.stub.InitContainer(req, timeout=float(self.init_timeout))
@@ -146,16 +150,19 @@ class EndpointHandler:
         old = self.endpoints.get(name)
         if old is not None:
             e.store = old.store           # carry devices over to the new endpoint
+            old.superseded = True         # its stream ending from now on must not delete them
         else:
             e.store = DeviceStore(self.callback)
         if self.swap_hook is not None:
             await self.swap_hook(e)
-        old = self.endpoints.get(name)
+        # the old endpoint may have ended (and left the table) while we were suspended
+        cur = self.endpoints.get(name)
         self.endpoints[name] = e
         self._tasks[e] = asyncio.ensure_future(self._track(e))
-        if old is not None and old is not e:
-            old.store = AlwaysEmptyDeviceStore()   # silence before stopping
-            await old.stop()
+        for o in {x for x in (old, cur) if x is not None and x is not e}:
+            o.superseded = True
+            o.store = AlwaysEmptyDeviceStore()     # silence before stopping
+            await o.stop()
         return e
 
     async def _track(self, e: Endpoint):

@@ -56,6 +56,33 @@ def targets():
     }
 
 
+SAN_DIR = os.path.join(os.path.dirname(BIN_DIR), "san")
+SAN_FLAGS = {
+    # host-code sanitizers only: GPU-side ASan / xnack+ code objects are not available on the MI355X pool
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def sanitizer_targets():
+    """Sanitized builds of the native host code (SURVEY §5.2 race detection: the reference's
+    `KUBE_RACE=-race`): ASan+UBSan for the store engine/server, TSan for the multi-threaded
+    AMD SMI shim. Output under kubernetes_amd/native/san/<kind>/."""
+    base = ["g++", "-O1", "-g", "-std=c++17", "-Wall"]
+    asan, tsan = os.path.join(SAN_DIR, "asan"), os.path.join(SAN_DIR, "tsan")
+    store = _s("store", "mvcc_store.cc")
+    return {
+        "asan_kamd_etcd": ([store], os.path.join(asan, "kamd-etcd"),
+                           base + SAN_FLAGS["asan"] + ["-DKAMD_STORE_SERVER", store]),
+        "asan_store_fuzz": ([store, _s("tests", "store_fuzz.cc")], os.path.join(asan, "store_fuzz"),
+                            base + SAN_FLAGS["asan"] + [_s("tests", "store_fuzz.cc")]),
+        "tsan_smi_threads": ([_s("amdsmi_shim", "kamd_smi.cc"), _s("amdsmi_shim", "kamd_smi.h"), _s("tests", "smi_threads.cc")],
+                             os.path.join(tsan, "smi_threads"),
+                             base + SAN_FLAGS["tsan"] + [f"-I{ROCM}/include", _s("tests", "smi_threads.cc"),
+                                                         _s("amdsmi_shim", "kamd_smi.cc"), "-ldl", "-lpthread"]),
+    }
+
+
 def _stale(srcs, out):
     if not os.path.exists(out):
         return True
@@ -63,11 +90,13 @@ def _stale(srcs, out):
     return any(os.path.exists(s) and os.path.getmtime(s) > t for s in srcs)
 
 
-def build(force=False, only=None, verbose=True):
+def build(force=False, only=None, verbose=True, sanitize=False):
     os.makedirs(LIB_DIR, exist_ok=True)
     os.makedirs(BIN_DIR, exist_ok=True)
     jobs = []
-    for name, (srcs, out, cmd) in targets().items():
+    tg = sanitizer_targets() if sanitize else targets()
+    for name, (srcs, out, cmd) in tg.items():
+        os.makedirs(os.path.dirname(out), exist_ok=True)
         if only and name not in only:
             continue
         if not all(os.path.exists(s) for s in srcs if s.endswith((".cc", ".hip"))):
@@ -97,8 +126,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", nargs="*")
+    ap.add_argument("--sanitize", action="store_true", help="build the ASan/UBSan/TSan variants + native test drivers")
     a = ap.parse_args()
-    build(a.force, a.only)
+    build(a.force, a.only, sanitize=a.sanitize)
 
 
 if __name__ == "__main__":

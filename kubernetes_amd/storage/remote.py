@@ -202,7 +202,9 @@ class StoreServer:
         self.address = None
 
     def start(self, timeout=10.0):
-        exe = os.path.join(BIN_DIR, "kamd-etcd")
+        # KAMD_ETCD_BIN: run another build of the server (the ASan/UBSan one in
+        # native/san/asan/ for the sanitizer tier); KAMD_ETCD_LOG_DIR: keep its stderr there
+        exe = os.environ.get("KAMD_ETCD_BIN") or os.path.join(BIN_DIR, "kamd-etcd")
         if not os.path.exists(exe):
             raise StoreError(f"{exe} not built (python -m kubernetes_amd.native.build)")
         cmd = [exe, "--history", str(self.history)]
@@ -214,7 +216,14 @@ class StoreServer:
             cmd += ["--listen-unix", self.socket_path]
         if self.wal:
             cmd += ["--wal", self.wal]
-        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+        log_dir = os.environ.get("KAMD_ETCD_LOG_DIR")
+        err = subprocess.DEVNULL
+        if log_dir:
+            os.makedirs(log_dir, exist_ok=True)
+            err = open(os.path.join(log_dir, f"kamd-etcd.{os.getpid()}.{id(self)}.log"), "ab")
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=err, start_new_session=True)
+        if err is not subprocess.DEVNULL:
+            err.close()
         deadline = time.time() + timeout
         while time.time() < deadline:
             if self.proc.poll() is not None:

@@ -12,6 +12,7 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -22,8 +23,10 @@
 namespace {
 
 std::mutex g_mu;
-std::string g_err;
-int g_backend = KAMD_BACKEND_NONE;
+// errno-style: each thread sees the error of its own last call (kamd_last_error() is read
+// without the lock, so a shared string would race with another thread's set_err)
+thread_local std::string g_err;
+std::atomic<int> g_backend{KAMD_BACKEND_NONE};   // read lock-free by kamd_backend()
 
 void set_err(const std::string& s) { g_err = s; }
 
@@ -531,7 +534,7 @@ int kamd_init(const char* fixture) {
   return g_backend;
 }
 
-int kamd_backend(void) { return g_backend; }
+int kamd_backend(void) { return g_backend.load(); }
 
 int kamd_device_count(void) {
   std::lock_guard<std::mutex> l(g_mu);

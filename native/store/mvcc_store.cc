@@ -452,9 +452,11 @@ class Server {
     return fd;
   }
 
-  void run() {
+  // returns when SIGTERM/SIGINT set *stop (a clean exit: destructors run, so leak checkers and
+  // the WAL's final fclose see a normal shutdown)
+  void run(volatile sig_atomic_t* stop) {
     epoll_event evs[256];
-    for (;;) {
+    while (!*stop) {
       int n = epoll_wait(ep_, evs, 256, 1000);
       for (int i = 0; i < n; ++i) {
         int fd = evs[i].data.fd;
@@ -675,8 +677,15 @@ class Server {
 
 }  // namespace kamd
 
+static volatile sig_atomic_t g_stop = 0;
+static void on_term(int) { g_stop = 1; }
+
 int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
+  struct sigaction sa{};
+  sa.sa_handler = on_term;   // no SA_RESTART: epoll_wait returns EINTR and the loop sees g_stop
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
   const char* unix_path = nullptr;
   const char* wal = nullptr;
   const char* port_file = nullptr;
@@ -706,7 +715,8 @@ int main(int argc, char** argv) {
     }
   }
   fprintf(stderr, "kamd-etcd: serving (rev %lld, %zu keys)\n", (long long)eng.rev(), eng.size());
-  srv.run();
+  srv.run(&g_stop);
+  if (unix_path) unlink(unix_path);
   return 0;
 }
 #endif

@@ -253,3 +253,46 @@ async def _eq(fn, want):
 
 async def _const(v):
     return v
+
+
+def test_reregistration_interleaving_shim(tmp_path, run):
+    """`endpoint_handler_test.go:153` TestReRegistration with the instrumented store shim
+    (`endpoint_store_shim.go`): the swap is paused, the shim checks that the new endpoint shares
+    the old endpoint's device store, and — the harder interleaving — the OLD plugin dies while
+    the swap is paused. Re-registration must never report the carried-over devices deleted, and
+    the superseded endpoint must still be stopped."""
+    from kubernetes_amd.kubelet.devicemanager.endpoint import EndpointHandler
+
+    async def main():
+        calls = []
+        h = EndpointHandler(lambda n, a, u, d: calls.append((n, [x.ID for x in a], [x.ID for x in u], [x.ID for x in d])))
+        dom = tmp_path / "amd.com"
+        p1 = DevicePluginServer("amd.com/gpu", str(dom / "p1.sock"), [device("Dev1"), device("Dev2")])
+        p2 = DevicePluginServer("amd.com/gpu", str(dom / "p2.sock"), [device("Dev1"), device("Dev2")])
+        await p1.start()
+        e1 = await h.new_endpoint(p1.socket_path, "amd.com")
+        await until(lambda: len(calls) == 1)
+        assert calls[0] == ("amd.com/gpu", ["Dev1", "Dev2"], [], [])
+        await p2.start()
+        seen = {}
+
+        async def shim(new):
+            old = h.endpoint("amd.com/gpu")
+            seen["old"], seen["new"] = old, new
+            assert old is e1 and new.store is old.store and len(old.store.devices_list()) == 2
+            await p1.stop()                       # the old plugin dies inside the swap window
+            await asyncio.sleep(0.3)
+        h.swap_hook = shim
+        e2 = await h.new_endpoint(p2.socket_path, "amd.com")
+        await asyncio.sleep(0.2)
+        assert seen["new"] is e2
+        assert not any(c[3] for c in calls), calls                  # nothing reported deleted
+        assert h.endpoint("amd.com/gpu") is e2
+        assert sorted(d.ID for d in h.devices()["amd.com/gpu"]) == ["Dev1", "Dev2"]
+        assert e1._stopped                                           # superseded endpoint stopped
+        await e2.stop()                                              # stop time: devices deleted once
+        await until(lambda: any(c[3] for c in calls))
+        assert [c[3] for c in calls if c[3]] == [["Dev1", "Dev2"]]
+        await h.stop()
+        await p2.stop()
+    run(main())
