@@ -68,6 +68,12 @@ def main(argv=None):
                     help="rotate the kubelet client certificate (CSR) as it approaches expiry")
     ap.add_argument("--config", default=None, help="KubeletConfiguration file (kubeletconfig/v1alpha1)")
     ap.add_argument("--dynamic-config-dir", default=None, help="enable Dynamic Kubelet Config; checkpoints live here")
+    ap.add_argument("--cgroups-per-qos", type=lambda v: v.lower() != "false", default=False,
+                    help="create the QoS and pod cgroup hierarchy under --cgroup-root")
+    ap.add_argument("--cgroup-root", default="/sys/fs/cgroup/kubepods.slice",
+                    help="cgroup v2 directory delegated to the kubelet (with --cgroups-per-qos)")
+    ap.add_argument("--experimental-allowed-unsafe-sysctls", default="",
+                    help="comma-separated unsafe sysctls or prefix* patterns pods may request")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -127,7 +133,9 @@ def main(argv=None):
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,
-                     image_gc=image_gc, network_plugin=plugin, hostports=hostports, **base)
+                     image_gc=image_gc, network_plugin=plugin, hostports=hostports,
+                     cgroup_root=a.cgroup_root if a.cgroups_per_qos else None,
+                     allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x], **base)
         await kl.run()
         if a.rotate_certificates and a.kubeconfig:
             import asyncio

@@ -194,3 +194,4 @@ CONTAINER_NAME = "io.kubernetes.container.name"
 # CRI server sees exactly what the kubelet would have passed it in-process
 POD_SPEC_ANNOTATION = "kubernetes-amd.io/pod"
 CONTAINER_SPEC_ANNOTATION = "kubernetes-amd.io/container"
+CGROUP_PARENT_ANNOTATION = "kubernetes-amd.io/cgroup-parent"   # pod cgroup (runtime joins it)

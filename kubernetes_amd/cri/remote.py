@@ -23,6 +23,7 @@ import time
 import grpc
 
 from ..deviceplugin.api import _Stub
+from ..kubelet.sysctl import SysctlAdmitHandler
 from ..kubelet.runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, ContainerStatus, Runtime, RuntimeError_
 from . import api as A
 
@@ -110,7 +111,8 @@ class RemoteRuntime(Runtime):
                                                  namespace=md.get("namespace", ""), attempt=0),
             hostname=(pod.get("spec") or {}).get("hostname") or md.get("name", ""),
             log_directory=f"/var/log/pods/{md.get('uid', '')}", port_mappings=ports,
-            labels=self._pod_labels(pod), annotations=ann)
+            labels=self._pod_labels(pod), annotations=ann,
+            linux=A.MSG["LinuxPodSandboxConfig"](sysctls=SysctlAdmitHandler.pod_sysctls(pod)))
 
     async def run_pod_sandbox(self, pod, annotations):
         r = await self._call("RunPodSandbox", A.MSG["RunPodSandboxRequest"](config=self._sandbox_config(pod, annotations)))
@@ -135,6 +137,8 @@ class RemoteRuntime(Runtime):
         envs += [A.MSG["KeyValue"](key=e["name"], value=str(e["value"])) for e in opts.envs]
         ann = {a["name"]: a["value"] for a in opts.annotations}
         ann[A.CONTAINER_SPEC_ANNOTATION] = json.dumps(container, separators=(",", ":"))
+        if opts.cgroup_parent:
+            ann[A.CGROUP_PARENT_ANNOTATION] = opts.cgroup_parent
         labels = {A.POD_NAME: md.get("name", ""), A.POD_NAMESPACE: md.get("namespace", ""),
                   A.POD_UID: md.get("uid", ""), A.CONTAINER_NAME: container["name"]}
         cfg = A.MSG["ContainerConfig"](
@@ -146,7 +150,9 @@ class RemoteRuntime(Runtime):
                                    readonly=bool(m.get("readOnly"))) for m in opts.mounts],
             devices=[A.MSG["Device"](container_path=d.get("pathInContainer", ""), host_path=d.get("pathOnHost", ""),
                                      permissions=d.get("permissions", "rwm")) for d in opts.devices],
-            labels=labels, annotations=ann, log_path=f"{container['name']}/0.log")
+            labels=labels, annotations=ann, log_path=f"{container['name']}/0.log",
+            linux=A.MSG["LinuxContainerConfig"](resources=A.MSG["LinuxContainerResources"](
+                oom_score_adj=opts.oom_score_adj or 0)))
         r = await self._call("CreateContainer", A.MSG["CreateContainerRequest"](
             pod_sandbox_id=sid, config=cfg, sandbox_config=self._sandbox_config(pod, {})))
         st = ContainerStatus(r.container_id, container["name"], CREATED, image=container.get("image", ""))

@@ -403,8 +403,11 @@ class CRIServer:
         else:
             container["env"] = [{"name": kv.key, "value": kv.value} for kv in c.envs]
             envs = []
+        res = c.linux.resources if c.HasField("linux") else None
         opts = RunContainerOptions(envs=envs, devices=devices, mounts=mounts,
-                                   annotations=[{"name": k, "value": v} for k, v in ann.items()])
+                                   annotations=[{"name": k, "value": v} for k, v in ann.items()],
+                                   oom_score_adj=(res.oom_score_adj if res is not None and res.oom_score_adj else None),
+                                   cgroup_parent=ann.get(A.CGROUP_PARENT_ANNOTATION))
         try:
             cid = await self.rt.create_container(req.pod_sandbox_id, sb["pod"], container, opts)
         except (FileNotFoundError, OSError, ValueError) as e:

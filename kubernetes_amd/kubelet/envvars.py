@@ -1,0 +1,69 @@
+"""Service environment variables for containers (`pkg/kubelet/envvars/envvars.go`,
+`kubelet_pods.go` getServiceEnvVarMap).
+
+Every container sees, for each service of its namespace plus the `kubernetes` master service of
+the `default` namespace (headless services, whose ClusterIP is None, are skipped):
+
+    {NAME}_SERVICE_HOST=<clusterIP>          {NAME}_SERVICE_PORT=<first port>
+    {NAME}_SERVICE_PORT_{PORTNAME}=<port>    (named ports)
+    {NAME}_PORT=tcp://<ip>:<first port>      (Docker-link compatible variables, per port:)
+    {NAME}_PORT_<port>_<PROTO>=tcp://<ip>:<port>   …_PROTO / …_PORT / …_ADDR
+
+with NAME the upper-cased service name, '-' → '_'. The container's own `env` wins on a clash
+(it is applied after these).
+"""
+from __future__ import annotations
+
+MASTER_NAMESPACE = "default"
+MASTER_SERVICES = ("kubernetes",)
+
+
+def _upper(s: str) -> str:
+    return s.upper().replace("-", "_")
+
+
+def _ip_set(svc) -> bool:
+    ip = (svc.get("spec") or {}).get("clusterIP")
+    return bool(ip) and ip != "None"
+
+
+def service_map(services, namespace) -> dict:
+    out = {}
+    for svc in services:
+        if not _ip_set(svc):
+            continue
+        md = svc["metadata"]
+        name, ns = md["name"], md.get("namespace", "default")
+        if ns == namespace:
+            out[name] = svc
+        elif ns == MASTER_NAMESPACE and name in MASTER_SERVICES:
+            out.setdefault(name, svc)
+    return out
+
+
+def from_services(services) -> list:
+    env = []
+    for svc in sorted(services, key=lambda s: s["metadata"]["name"]):
+        name = _upper(svc["metadata"]["name"])
+        spec = svc.get("spec") or {}
+        ip = spec["clusterIP"]
+        ports = spec.get("ports") or []
+        env.append({"name": f"{name}_SERVICE_HOST", "value": ip})
+        if ports:
+            env.append({"name": f"{name}_SERVICE_PORT", "value": str(ports[0]["port"])})
+        for p in ports:
+            if p.get("name"):
+                env.append({"name": f"{name}_SERVICE_PORT_{_upper(p['name'])}", "value": str(p["port"])})
+        for i, p in enumerate(ports):
+            proto = (p.get("protocol") or "TCP").lower()
+            url = f"{proto}://{ip}:{p['port']}"
+            prefix = f"{name}_PORT_{p['port']}_{proto.upper()}"
+            if i == 0:
+                env.append({"name": f"{name}_PORT", "value": url})
+            env += [{"name": prefix, "value": url}, {"name": f"{prefix}_PROTO", "value": proto},
+                    {"name": f"{prefix}_PORT", "value": str(p["port"])}, {"name": f"{prefix}_ADDR", "value": ip}]
+    return env
+
+
+def service_env(services, namespace) -> list:
+    return from_services(service_map(services, namespace).values())

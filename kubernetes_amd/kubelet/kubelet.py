@@ -39,6 +39,7 @@ from ..utils.metrics import MICRO_BUCKETS, Registry
 from .devicemanager.manager import AdmitError, ManagerStub
 from .prober import ProbeManager
 from .runtime.base import EXITED, RUNNING, RunContainerOptions
+from .qos import oom_score_adj
 from .volumes import VolumeError, VolumeManager
 from ..utils.tasks import spawn
 
@@ -89,8 +90,16 @@ class Kubelet:
                  image_service=None, image_gc=None, image_backoff=10.0, network_plugin=None, dns=None,
                  hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
                  bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
-                 manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None):
+                 manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None,
+                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True):
         self.client = client
+        from .preemption import CriticalPodAdmissionHandler
+        from .sysctl import SysctlAdmitHandler
+        self.sysctls = SysctlAdmitHandler(allowed_unsafe_sysctls)
+        self.cgroup_root = cgroup_root            # --cgroup-root with --cgroups-per-qos (None: off)
+        self.cgroups = None
+        self.service_env = service_env            # inject {SVC}_SERVICE_HOST/... (pkg/kubelet/envvars)
+        self.svc_informer = None
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
         self.dns = dns                       # network.DNSConfigurer or None
@@ -173,6 +182,7 @@ class Kubelet:
                                            image_gc.get("high", 85), image_gc.get("low", 80), image_gc.get("min_age", 120.0),
                                            last_used=self.images.last_used)
             self.image_gc_period = float(image_gc.get("period", 300.0))
+        self.preemption = CriticalPodAdmissionHandler(self.active_pods, self._preempt, self.recorder)
         self.started = asyncio.Event()
         self.plugin_labels = {}
         self.informer_node_labels = {}
@@ -189,6 +199,15 @@ class Kubelet:
             self.http_port = await self.http.start(self.address, self.http_port)
         await self.dm.start(self.active_pods)
         self.dm.add_capacity_listener(lambda r: self._status_dirty.set())
+        if self.cgroup_root:
+            from .cgroups import CgroupManager
+            alloc = self._allocatable(self.capacity)
+            self.cgroups = CgroupManager(self.cgroup_root, {
+                "cpu": parse_quantity(str(alloc["cpu"])).milli_value(),
+                "memory": parse_quantity(str(alloc["memory"])).value}).start()
+        if self.service_env:
+            self.svc_informer = Informer(self.client, "services")
+            self.svc_informer.start()
         if self.register:
             await self._register_node()
         if self.pod_checkpoints is not None:
@@ -251,6 +270,8 @@ class Kubelet:
         self._stopped = True
         self._status_dirty.set()
         self.informer.stop()
+        if self.svc_informer is not None:
+            self.svc_informer.stop()
         if self.static_pods is not None:
             self.static_pods.stop()
         for t in self._tasks:
@@ -555,13 +576,56 @@ class Kubelet:
                 return "MatchNodeSelector", "Predicate MatchNodeSelector failed"
         return None
 
+    def _shortfall(self, pod) -> dict:
+        """Resources this pod lacks on the node ({cpu: milli, memory: bytes, pods: n}), the input
+        of critical-pod preemption."""
+        need = core.pod_requests(pod)
+        used = {"cpu": 0, "memory": 0}
+        n = 0
+        for other in self.active_pods():
+            if other["metadata"]["uid"] == pod["metadata"]["uid"]:
+                continue
+            n += 1
+            for k, v in core.pod_requests(other).items():
+                if k in used:
+                    used[k] += v.milli_value() if k == "cpu" else v.value
+        out = {}
+        if n + 1 > int(self.capacity["pods"]):
+            out["pods"] = n + 1 - int(self.capacity["pods"])
+        for k in ("cpu", "memory"):
+            if k in need and k in self.capacity:
+                cap = parse_quantity(self.capacity[k])
+                cap_v = cap.milli_value() if k == "cpu" else cap.value
+                want = need[k].milli_value() if k == "cpu" else need[k].value
+                if used[k] + want > cap_v:
+                    out[k] = used[k] + want - cap_v
+        return out
+
+    async def _preempt(self, victim, status):
+        st = self.pods.get(victim["metadata"]["uid"])
+        if st is None:
+            return
+        await self._kill_pod(st, 0)
+        st.terminated = True
+        await self._write_status(st, dict(status, conditions=(victim.get("status") or {}).get("conditions") or []))
+
     async def _admit(self, st: PodState):
         pod = st.pod
+        r = self.sysctls.admit(pod)
+        if r is not None:
+            return r
         try:
             await self.dm.admit_pod(pod)
         except AdmitError as e:
             return "UnexpectedAdmissionError", f"Pod admission failed: {e}"
         r = self._general_predicates(pod)
+        if r is not None and r[0] in ("OutOfcpu", "OutOfmemory", "OutOfpods"):
+            # `pkg/kubelet/preemption`: a critical pod evicts lower-QoS pods instead of failing
+            try:
+                if await self.preemption.handle_admission_failure(pod, self._shortfall(pod)):
+                    r = self._general_predicates(pod)
+            except ValueError as e:
+                log.warning("critical pod %s: preemption impossible: %s", pod["metadata"].get("name"), e)
         if r is None and self.eviction is not None:
             r = self.eviction.admit(pod)
         return r
@@ -583,6 +647,8 @@ class Kubelet:
                 self.pods.pop(uid, None)
                 self.by_key.pop(_key(pod), None)
                 self.dm.delete_pod(uid)
+                if self.cgroups is not None:
+                    self.cgroups.destroy_pod(uid)
             return
         if st is None:
             if core.pod_is_terminal(pod):
@@ -630,6 +696,8 @@ class Kubelet:
             else:
                 st.volumes = {}
         if st.sandbox is None:
+            if self.cgroups is not None:
+                self.cgroups.ensure_pod(pod)
             ann = {}
             pr = self.dm.pod_resources(pod)
             if pr:
@@ -684,6 +752,12 @@ class Kubelet:
                 st.containers[c["name"]] = await self._start(st, c)
         await self._report(st)
 
+    def _service_env(self, pod):
+        if self.svc_informer is None or not self.svc_informer.synced.is_set():
+            return []
+        from .envvars import service_env
+        return service_env(self.svc_informer.list(), pod["metadata"].get("namespace", "default"))
+
     async def _start(self, st, c):
         from .images import ImagePullError
         try:
@@ -702,10 +776,15 @@ class Kubelet:
             return None
         spec_c = c
         opts.mounts.extend(st.net_mounts)
-        if c.get("volumeMounts") or c.get("envFrom") or any("valueFrom" in e or "$(" in str(e.get("value", ""))
-                                                             for e in c.get("env") or ()):
+        opts.oom_score_adj = oom_score_adj(st.pod, c, parse_quantity(self.capacity["memory"]).value)
+        if self.cgroups is not None:
+            opts.cgroup_parent = self.cgroups.pod_dir(st.pod)
+        svc_env = self._service_env(st.pod)
+        if svc_env or c.get("volumeMounts") or c.get("envFrom") or any(
+                "valueFrom" in e or "$(" in str(e.get("value", "")) for e in c.get("env") or ()):
             try:
-                spec_c = dict(c, env=await self.volumes.env_for(st.pod, c, self.node_name, st.ip), envFrom=[])
+                spec_c = dict(c, env=await self.volumes.env_for(st.pod, c, self.node_name, st.ip, base_env=svc_env),
+                              envFrom=[])
                 for m in self.volumes.mounts_for(c, st.volumes or {}):
                     opts.mounts.append(m)
                 for m in c.get("volumeMounts") or ():

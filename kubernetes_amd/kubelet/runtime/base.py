@@ -20,6 +20,8 @@ class RunContainerOptions:
     devices: list = field(default_factory=list)       # [{"pathOnHost","pathInContainer","permissions"}]
     mounts: list = field(default_factory=list)        # [{"containerPath","hostPath","readOnly"}]
     annotations: list = field(default_factory=list)   # [{"name","value"}]
+    oom_score_adj: int | None = None                  # qos.oom_score_adj (CRI LinuxContainerResources)
+    cgroup_parent: str | None = None                  # pod cgroup directory (cgroups.CgroupManager)
 
     @classmethod
     def from_device_opts(cls, d):

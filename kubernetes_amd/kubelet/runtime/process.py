@@ -45,6 +45,29 @@ def resolve_command(container):
     return cmd + args
 
 
+def _child_setup(cpus, oom_adj, cgroup):
+    """Runs in the forked child before exec: what a container runtime applies to the container's
+    init process — cpuset pinning, the kubelet's OOM score adjustment, pod cgroup membership.
+    Failures are ignored (an unprivileged kubelet can raise but not lower oom_score_adj, and
+    may not own a cgroup subtree)."""
+    def pre():
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+        if oom_adj is not None:
+            try:
+                with open("/proc/self/oom_score_adj", "w") as f:
+                    f.write(str(oom_adj))
+            except OSError:
+                pass
+        if cgroup:
+            try:
+                with open(os.path.join(cgroup, "cgroup.procs"), "w") as f:
+                    f.write("0")            # "0" = the writing process itself
+            except OSError:
+                pass
+    return pre
+
+
 class ProcessRuntime(Runtime):
     name = "process"
     shares_host_network = True     # containers are host processes: pod IP = node address
@@ -122,7 +145,8 @@ class ProcessRuntime(Runtime):
                              log_path=os.path.join(d, "log"))
         self.containers[cid] = st
         self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "argv": argv, "env": env,
-                          "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec}
+                          "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec,
+                          "oom_score_adj": opts.oom_score_adj, "cgroup": opts.cgroup_parent}
         return cid
 
     @staticmethod
@@ -133,13 +157,14 @@ class ProcessRuntime(Runtime):
         m = self.meta[cid]
         st = self.containers[cid]
         log = open(st.log_path, "ab")
-        pre = None
+        cpus = None
         if m["env"].get("KAMD_CPUSET") and hasattr(os, "sched_setaffinity"):
             # cpu manager's cpuset (cgroup cpuset.cpus in a real runtime): pin before exec
             from ..cpumanager import parse_cpulist
-            cpus = set(parse_cpulist(m["env"]["KAMD_CPUSET"])) & set(os.sched_getaffinity(0))
-            if cpus:
-                pre = lambda: os.sched_setaffinity(0, cpus)  # noqa: E731
+            cpus = set(parse_cpulist(m["env"]["KAMD_CPUSET"])) & set(os.sched_getaffinity(0)) or None
+        pre = None
+        if cpus or m.get("oom_score_adj") is not None or m.get("cgroup"):
+            pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
         try:
             proc = await asyncio.create_subprocess_exec(*m["argv"], env=m["env"], cwd=m["cwd"], stdout=log,
                                                         stderr=asyncio.subprocess.STDOUT, start_new_session=True,

@@ -347,8 +347,10 @@ class VolumeManager:
         if os.path.isdir(shm):
             shutil.rmtree(shm, ignore_errors=True)
 
-    async def env_for(self, pod, container, node_name=None, pod_ip=None):
-        """Resolved container environment (list of {name, value})."""
+    async def env_for(self, pod, container, node_name=None, pod_ip=None, base_env=()):
+        """Resolved container environment (list of {name, value}). `base_env` (the service
+        variables) comes first: envFrom and the container's own env override it, and `$(VAR)`
+        references can name it (`kubelet_pods.go` makeEnvironmentVariables)."""
         ns = pod["metadata"].get("namespace", "default")
         env: dict[str, str] = {}
         order = []
@@ -357,6 +359,8 @@ class VolumeManager:
             if k not in env:
                 order.append(k)
             env[k] = v
+        for e in base_env:
+            put(e["name"], e["value"])
         for ef in container.get("envFrom") or ():
             pre = ef.get("prefix", "")
             if "configMapRef" in ef:
