@@ -123,7 +123,8 @@ class AddonManager:
             await asyncio.sleep(self.period)
 
 
-def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local", master="http://127.0.0.1:8080"):
+def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local", master="http://127.0.0.1:8080",
+                   elasticsearch="http://elasticsearch-logging.kube-system:9200"):
     """Manifests for the built-in add-ons (written by `kubeadm` / local-up). `master` is the API
     server URL the hostNetwork add-ons (node-problem-detector) talk to."""
     lab = {MODE: RECONCILE}
@@ -174,4 +175,26 @@ def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local", master="
                                                                  "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
                                                         "volumeMounts": [{"name": "log", "mountPath": "/var/log", "readOnly": True}]}],
                                         "volumes": [{"name": "log", "hostPath": {"path": "/var/log"}}]}}}},
+        # cluster/addons/fluentd-elasticsearch: node logging agent shipping /var/log/containers
+        {"apiVersion": "apps/v1", "kind": "DaemonSet",
+         "metadata": {"name": "log-shipper", "namespace": "kube-system",
+                      "labels": dict(lab, **{"k8s-app": "log-shipper"})},
+         "spec": {"selector": {"matchLabels": {"k8s-app": "log-shipper"}},
+                  "template": {"metadata": {"labels": {"k8s-app": "log-shipper"}},
+                               "spec": {"hostNetwork": True, "priorityClassName": "system-node-critical",
+                                        "tolerations": [{"operator": "Exists", "effect": "NoSchedule"}],
+                                        "containers": [{"name": "log-shipper", "image": "kubernetes-amd/hyperkube",
+                                                        "command": [sys.executable, "-m", "kubernetes_amd.cmd.log_shipper",
+                                                                    "--master", master, "--log-dir", "/var/log/containers",
+                                                                    "--pos-file", "/var/log/es-containers.log.pos",
+                                                                    "--elasticsearch", elasticsearch],
+                                                        "env": [{"name": "NODE_NAME",
+                                                                 "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
+                                                        "volumeMounts": [{"name": "log", "mountPath": "/var/log"}]}],
+                                        "volumes": [{"name": "log", "hostPath": {"path": "/var/log"}}]}}}},
+        # cluster/addons/storage-class: the default class (node-local host-path provisioner)
+        {"apiVersion": "storage.k8s.io/v1", "kind": "StorageClass",
+         "metadata": {"name": "standard", "labels": {MODE: ENSURE},
+                      "annotations": {"storageclass.beta.kubernetes.io/is-default-class": "true"}},
+         "provisioner": "kubernetes.io/host-path", "reclaimPolicy": "Delete"},
     ]

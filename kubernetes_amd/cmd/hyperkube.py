@@ -25,7 +25,7 @@ COMPONENTS = {
     "hollow-node": "hollow_node", "kubemark": "hollow_node",
     "local-up": "local_up", "local-up-cluster": "local_up",
     "csi-hostpath": "csi_hostpath",
-    "node-problem-detector": "npd", "npd": "npd",
+    "node-problem-detector": "npd", "npd": "npd", "log-shipper": "log_shipper", "fluentd": "log_shipper",
     "gendocs": "gendocs",
 }
 

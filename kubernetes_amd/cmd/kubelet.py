@@ -74,6 +74,8 @@ def main(argv=None):
                     help="cgroup v2 directory delegated to the kubelet (with --cgroups-per-qos)")
     ap.add_argument("--experimental-allowed-unsafe-sysctls", default="",
                     help="comma-separated unsafe sysctls or prefix* patterns pods may request")
+    ap.add_argument("--container-log-dir", default="/var/log/containers",
+                    help="where <pod>_<namespace>_<container>-<id>.log symlinks for logging agents go ('' = off)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -135,6 +137,7 @@ def main(argv=None):
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,
                      image_gc=image_gc, network_plugin=plugin, hostports=hostports,
                      cgroup_root=a.cgroup_root if a.cgroups_per_qos else None,
+                     container_log_dir=a.container_log_dir or None,
                      allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x], **base)
         await kl.run()
         if a.rotate_certificates and a.kubeconfig:

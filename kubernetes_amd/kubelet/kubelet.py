@@ -91,8 +91,12 @@ class Kubelet:
                  hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
                  bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
                  manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None,
-                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True):
+                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, container_log_dir=None):
         self.client = client
+        # /var/log/containers/<pod>_<ns>_<container>-<id>.log symlinks to the runtime's log
+        # files (kuberuntime legacyLogSymlink): what node logging agents tail
+        self.container_log_dir = container_log_dir
+        self._log_links: dict[str, str] = {}      # container id -> symlink path
         from .preemption import CriticalPodAdmissionHandler
         from .sysctl import SysctlAdmitHandler
         self.sysctls = SysctlAdmitHandler(allowed_unsafe_sysctls)
@@ -533,7 +537,7 @@ class Kubelet:
 
     def _on_container_exit(self, pod_uid, cid):
         st = self.pods.get(pod_uid)
-        if st is not None and pod_uid not in self._pending:
+        if st is not None and not st.deleted and pod_uid not in self._pending:
             self._dispatch(st.pod, "sync")
 
     async def _worker(self, uid):
@@ -637,6 +641,7 @@ class Kubelet:
         st = self.pods.get(uid)
         if op == "delete":
             if st is not None:
+                st.deleted = True          # before the kill: container-exit callbacks must not resync it
                 await self._kill_pod(st, 0)
                 await self._teardown_network(st)
                 if st.volumes:
@@ -649,9 +654,14 @@ class Kubelet:
                 self.dm.delete_pod(uid)
                 if self.cgroups is not None:
                     self.cgroups.destroy_pod(uid)
+                for cid in list(st.containers.values()) + list(st.init_containers.values()) + list(st.previous.values()):
+                    if cid:
+                        self._unlink_log(cid)
             return
         if st is None:
-            if core.pod_is_terminal(pod):
+            # an internal resync (container exit, back-off timer) of a pod already deleted must
+            # not resurrect it: only informer add/update events create pod state
+            if core.pod_is_terminal(pod) or op == "sync":
                 return
             st = self.pods[uid] = PodState(pod)
             if getattr(self.runtime, "shares_host_network", False) or (pod.get("spec") or {}).get("hostNetwork"):
@@ -746,11 +756,38 @@ class Kubelet:
                         old = st.previous.get(c["name"])
                         if old is not None:
                             await rt.remove_container(old)
+                            self._unlink_log(old)
                         st.previous[c["name"]] = cid
                         cid = None
             if cid is None:
                 st.containers[c["name"]] = await self._start(st, c)
         await self._report(st)
+
+    def _link_log(self, pod, cname, cid):
+        cs = self.runtime.container_status(cid)
+        target = getattr(cs, "log_path", "") if cs is not None else ""
+        if not target:
+            return
+        md = pod["metadata"]
+        # the id part must not contain '-' (logging agents split `<container>-<id>` at the last one)
+        bare = "".join(ch for ch in cid.split("://", 1)[-1] if ch.isalnum())
+        link = os.path.join(self.container_log_dir, f"{md['name']}_{md.get('namespace', 'default')}_{cname}-{bare}.log")
+        try:
+            os.makedirs(self.container_log_dir, exist_ok=True)
+            if os.path.lexists(link):
+                os.unlink(link)
+            os.symlink(os.path.abspath(target), link)
+            self._log_links[cid] = link
+        except OSError as e:
+            log.warning("container log symlink %s: %s", link, e)
+
+    def _unlink_log(self, cid):
+        link = self._log_links.pop(cid, None)
+        if link:
+            try:
+                os.unlink(link)
+            except OSError:
+                pass
 
     def _service_env(self, pod):
         if self.svc_informer is None or not self.svc_informer.synced.is_set():
@@ -811,6 +848,8 @@ class Kubelet:
         except Exception as e:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
             return None
+        if self.container_log_dir:
+            self._link_log(st.pod, c["name"], cid)
         post = ((c.get("lifecycle") or {}).get("postStart"))
         if post:
             # `pkg/kubelet/lifecycle/handlers.go` RunHandler: a failed postStart kills the container
@@ -925,6 +964,7 @@ class Kubelet:
         out = []
         for _, cid, st, name in removed:
             await self.runtime.remove_container(cid)
+            self._unlink_log(cid)
             if st.previous.get(name) == cid:
                 st.previous.pop(name, None)
             out.append(cid)
@@ -932,6 +972,7 @@ class Kubelet:
             if cs.state == EXITED and cs.id not in live and not any(cs.id in st.previous.values() for st in self.pods.values()) \
                     and now - (cs.finished_at or cs.created_at) >= min_age:
                 await self.runtime.remove_container(cs.id)
+                self._unlink_log(cs.id)
                 out.append(cs.id)
         return out
 
@@ -1018,8 +1059,11 @@ class Kubelet:
         md = pod["metadata"]
         await self._teardown_network(st)
         if st.sandbox is not None:
-            await self.runtime.remove_pod_sandbox(st.sandbox)
+            await self.runtime.remove_pod_sandbox(st.sandbox)     # removes its containers too
             st.sandbox = None
+            for cid in list(st.containers.values()) + list(st.init_containers.values()) + list(st.previous.values()):
+                if cid:
+                    self._unlink_log(cid)
         if st.volumes:
             await self.volumes.unpublish(pod)
             self.volumes.teardown(pod)

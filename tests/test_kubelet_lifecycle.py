@@ -106,3 +106,30 @@ def test_http_pod_source(run, tmp_path):
             await cl.stop()
             srv.shutdown()
     run(main(), timeout=60)
+
+
+def test_deleted_pod_is_not_resurrected_by_container_exit(run, tmp_path):
+    """Regression: stopping a deleted pod's containers fires the runtime's exit callback; the
+    resulting internal resync used to re-create the pod's kubelet state (and restart it)."""
+    async def main():
+        cl = LocalCluster(nodes=1, gpus_per_node=0, runtime="process", workdir=str(tmp_path / "c"))
+        await cl.start()
+        c = cl.client
+        kl = cl.nodes[0].kubelet
+        try:
+            await c.create("pods", {"metadata": {"name": "short"}, "spec": {"containers": [{
+                "name": "c", "image": "busybox", "command": ["sh", "-c", "sleep 30"]}]}}, "default")
+            await cl.wait_pod("short")
+            n_started = len(kl.runtime.list_containers())
+            await c.delete("pods", "short", "default", grace_period=0)
+
+            async def forgotten():
+                return not kl.pods and not kl._workers
+            await cl.wait_for(forgotten, 20)
+            import asyncio
+            await asyncio.sleep(0.3)
+            assert not kl.pods
+            assert len(kl.runtime.list_containers()) <= n_started      # nothing was started again
+        finally:
+            await cl.stop()
+    run(main(), timeout=60)
