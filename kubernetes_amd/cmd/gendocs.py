@@ -20,7 +20,8 @@ import yaml
 COMPONENTS = {"kube-apiserver": "apiserver", "kube-controller-manager": "controller_manager",
               "kube-scheduler": "scheduler", "kubelet": "kubelet", "kube-proxy": "proxy", "kubectl": "kubectl",
               "kubeadm": "kubeadm", "kube-dns": "dns", "kube-addon-manager": "addon_manager", "kamd-cri": "cri",
-              "amd-gpu-device-plugin": "device_plugin", "csi-hostpath": "csi_hostpath"}
+              "amd-gpu-device-plugin": "device_plugin", "csi-hostpath": "csi_hostpath",
+              "node-problem-detector": "npd", "log-shipper": "log_shipper", "amd-smi-exporter": "amd_smi_exporter"}
 
 
 class _Captured(Exception):
@@ -110,6 +111,16 @@ def to_man(path, parser):
 def to_yaml(path, parser):
     return {"name": " ".join(path), "synopsis": (parser.description or "").strip(),
             "usage": parser.format_usage().strip(), "options": _options(parser)}
+
+
+def parsers():
+    """{"component sub command": parser} for every component and sub-command (hack/verify.py's
+    flag checks walk these)."""
+    out = {}
+    for comp, mod in COMPONENTS.items():
+        for path, sp in walk(capture_parser(mod), [comp]):
+            out[" ".join(path)] = sp
+    return out
 
 
 def generate(out_dir, fmt="md", components=None):

@@ -1,3 +1,4 @@
+"""`python -m kubernetes_amd.kubectl` entry point."""
 import sys
 
 from .cli import main
