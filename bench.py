@@ -96,6 +96,38 @@ def control_plane_shape(world, workers=0, shards=0):
     return workers, shards
 
 
+def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
+    """Hollow-node processes per rank (0 = auto): kubemark runs one process per hollow node;
+    here the rank's nodes are spread over up to 4 processes so kubelet work uses several cores,
+    bounded by the CPUs left after ranks and the control plane."""
+    if want > 0:
+        return max(1, min(want, nodes_per_rank))
+    spare = cpu_budget() - world - workers - shards - 1
+    return max(1, min(nodes_per_rank, 4, spare // max(1, world)))
+
+
+def spawn_hollow_procs(args, url, rank, nprocs, tmp, payload_socket):
+    """Start the rank's hollow nodes in `nprocs` child processes (none touches the GPU: GPU
+    payloads go to the rank's PayloadServer)."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = HERE + os.pathsep + env.get("PYTHONPATH", "")
+    base, extra = divmod(args.nodes_per_rank, nprocs)
+    procs = []
+    for j in range(nprocs):
+        n = base + (1 if j < extra else 0)
+        if n == 0:
+            continue
+        cmd = [sys.executable, "-m", "kubernetes_amd.cmd.hollow_node", "--master", url, "--count", str(n),
+               "--name-prefix", f"r{rank}p{j}", "--gpus-per-node", str(args.gpus_per_node)]
+        if payload_socket:
+            cmd += ["--payload-socket", payload_socket]
+        if args.no_events:
+            cmd.append("--no-events")
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL,
+                                      stderr=open(os.path.join(tmp, f"hollow-r{rank}p{j}.log"), "w")))
+    return procs
+
+
 def spawn_control_plane(tmp, args):
     env = dict(os.environ)
     env["PYTHONPATH"] = HERE + os.pathsep + env.get("PYTHONPATH", "")
@@ -203,10 +235,19 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         from kubernetes_amd.ops.hip_kernels import Payload
         payload = Payload(d.local_rank)
         payload_fn = lambda opts: payload.run()  # noqa: E731
-    hollow = HollowCluster(url, args.nodes_per_rank, prefix=f"r{d.rank}", gpus=args.gpus_per_node,
-                           payload=payload_fn, emit_events=not args.no_events)
-    await hollow.start()
-    await hollow.wait_registered()
+    hollow, hprocs, psrv = None, [], None
+    if args.hollow_procs > 1:
+        from kubernetes_amd.kubemark.payload import PayloadServer
+        sock = None
+        if payload is not None:
+            sock = os.path.join(tempfile.mkdtemp(prefix="kamd-pl-"), "payload.sock")
+            psrv = await PayloadServer(payload.run, sock).start()
+        hprocs = spawn_hollow_procs(args, url, d.rank, args.hollow_procs, tempfile.mkdtemp(prefix="kamd-hollow-"), sock)
+    else:
+        hollow = HollowCluster(url, args.nodes_per_rank, prefix=f"r{d.rank}", gpus=args.gpus_per_node,
+                               payload=payload_fn, emit_events=not args.no_events)
+        await hollow.start()
+        await hollow.wait_registered()
     # wait until every rank's nodes are visible with their GPUs
     c = Client(url)
     want_nodes = d.world * args.nodes_per_rank
@@ -218,6 +259,9 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
             break
         if time.time() - t > 120:
             raise TimeoutError(f"only {len(ok)}/{want_nodes} GPU nodes ready")
+        dead = [p.args for p in hprocs if p.poll() is not None]
+        if dead:
+            raise RuntimeError(f"hollow-node process exited: {dead[0]}")
         await asyncio.sleep(0.05)
     await c.close()
     pods_per_step = args.pods_per_rank or args.nodes_per_rank * args.gpus_per_node // args.gpus_per_pod
@@ -248,8 +292,10 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         off += r["cycle_s"]
     stats = {"elapsed": elapsed, "lat": lat, "pods": sum(r["pods"] for r in results),
              "to_running": [r["to_running_s"] for r in results], "cycle": [r["cycle_s"] for r in results],
-             "payload_runs": sum(getattr(k.runtime, "payload_runs", 0) for k in hollow.nodes),
-             "payload_failures": sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes),
+             "payload_runs": (psrv.runs if psrv else sum(getattr(k.runtime, "payload_runs", 0) for k in hollow.nodes)
+                              if hollow or psrv else 0),
+             "payload_failures": (psrv.failures if psrv else sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes)
+                                  if hollow or psrv else 0),
              "sched_rates": interval_rates(sched_times), "cpu_s": my_cpu,
              "cp_cpu_s": {k: cp1.get(k, 0.0) - cp0.get(k, 0.0) for k in cp1}}
     await runner.stop()
@@ -285,7 +331,17 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     allstats = await loop.run_in_executor(None, d.allgather, stats)
     # keep serving other ranks' pods until everyone is done
     await abarrier()
-    await hollow.stop()
+    if hollow is not None:
+        await hollow.stop()
+    for p in hprocs:
+        p.terminate()
+    for p in hprocs:
+        try:
+            await loop.run_in_executor(None, p.wait, 10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    if psrv is not None:
+        await psrv.stop()
     if payload is not None:
         payload.close()
     return allstats
@@ -311,6 +367,8 @@ def main():
     ap.add_argument("--step-timeout", type=float, default=120.0, help="fail (with diagnostics) if a step stalls")
     ap.add_argument("--scheduler-shards", type=int, default=0,
                     help="parallel scheduler shard processes (0 = auto from the CPU budget)")
+    ap.add_argument("--hollow-procs", type=int, default=0,
+                    help="hollow-node processes per rank (0 = auto from the CPU budget; 1 = in the rank process)")
     args = ap.parse_args()
     d = Dist()
     tmp = tempfile.mkdtemp(prefix="kamd-bench-")
@@ -321,6 +379,8 @@ def main():
             url, procs = spawn_control_plane(tmp, args)   # before any GPU init
         d.init()
         url, d.broadcast_done_workers, d.shards = d.broadcast((url, args.apiserver_workers, args.scheduler_shards))
+        args.hollow_procs = hollow_procs_for(d.world, args.nodes_per_rank, d.broadcast_done_workers, d.shards,
+                                             args.hollow_procs)
         cp = [("apiserver", procs[0].pid), ("scheduler", procs[1].pid)] if procs else []
         if os.environ.get("KAMD_PROFILE_DIR"):
             import cProfile
@@ -357,7 +417,7 @@ def main():
                    "seq_len": None, "parallelism": f"ranks{n}", "hollow_nodes": n * args.nodes_per_rank,
                    "gpus_per_node": args.gpus_per_node, "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
                    "gpus_per_pod": args.gpus_per_pod, "apiserver_workers": d.broadcast_done_workers,
-                   "scheduler_shards": d.shards},
+                   "scheduler_shards": d.shards, "hollow_procs_per_rank": args.hollow_procs},
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
         "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
         "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],

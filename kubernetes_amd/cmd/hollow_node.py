@@ -17,6 +17,11 @@ def main(argv=None):
     ap.add_argument("--hives", type=int, default=1)
     ap.add_argument("--morph", default="kubelet", choices=["kubelet", "proxy"],
                     help="kubelet: hollow kubelets; proxy: hollow kube-proxies over a fake iptables (hollow-node.go:139+)")
+    ap.add_argument("--payload-socket", default=None,
+                    help="run each GPU container's payload through this PayloadServer (the rank holding the GPU)")
+    ap.add_argument("--no-events", action="store_true")
+    ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
+    ap.add_argument("--ready-file", default=None, help="touched once every node's device plugin registered")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -40,9 +45,16 @@ def main(argv=None):
                 await p.start()
             print(f"{a.count} hollow proxies syncing (fake iptables)", flush=True)
             return ps
-        h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives)
+        payload = None
+        if a.payload_socket:
+            from ..kubemark.payload import PayloadClient
+            payload = PayloadClient(a.payload_socket)
+        h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives, payload=payload,
+                          emit_events=not a.no_events, status_freq=a.node_status_update_frequency)
         await h.start()
         await h.wait_registered()
+        if a.ready_file:
+            open(a.ready_file, "w").close()
         print(f"{a.count} hollow nodes registered ({a.gpus_per_node} GPUs each)", flush=True)
         return h
 

@@ -13,6 +13,7 @@ Containers may declare a run time with the annotation `kubemark.amd.com/run-seco
 from __future__ import annotations
 
 import asyncio
+import inspect
 import itertools
 import time
 
@@ -84,7 +85,10 @@ class StubRuntime(Runtime):
             self.payload_runs += 1
             ok = False
             try:
-                ok = bool(self.payload(opts))
+                res = self.payload(opts)
+                if inspect.isawaitable(res):     # e.g. kubemark.payload.PayloadClient (another process)
+                    res = await res
+                ok = bool(res)
             except Exception as e:  # payload crash = container crash
                 st.message = str(e)
             if not ok:

@@ -1,0 +1,51 @@
+"""bench.py contract (the driver's headline measurement): one JSON line with the metric, value
+(whole-job pods/s), steps/warmup, weak scaling, config — for N=1 in one process and for N=2
+ranks under torch.distributed.run (gloo on CPU here; RCCL on MI355X), with hollow nodes both
+in the rank process and in child processes."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, out[-3000:]
+    return json.loads(lines[0])
+
+
+def _check(d, n, steps, warmup):
+    assert d["metric"].startswith("GPU pods/sec scheduled") and d["unit"] == "pods/s"
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["value"] > 0
+    assert d["config"]["model"] == "kubemark-density/8xMI355X-hollow-nodes/1-GPU-pods"
+    assert d["config"]["hollow_nodes"] == n * d["config"]["hollow_nodes"] // n
+    assert d["vs_baseline"] == round(d["value"] / 8.0, 2)
+    assert d["p50_startup_ms"] > 0 and d["payload_failures"] == 0
+
+
+def test_bench_single_rank_hollow_processes():
+    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1")
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--nodes-per-rank", "2",
+                        "--hollow-procs", "2", "--xgmi4-steps", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    _check(d, 1, 2, 1)
+    assert d["config"]["hollow_procs_per_rank"] == 2 and d["config"]["global_batch"] == 16
+    assert d["xgmi4_single_hive_fraction"] == 1.0
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29731", "bench.py", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--nodes-per-rank", "2", "--xgmi4-steps", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    _check(d, 2, 2, 1)
+    assert d["config"]["parallelism"] == "ranks2" and d["config"]["hollow_nodes"] == 4
+    assert d["config"]["global_batch"] == 32                 # weak scaling: 2 ranks x 2 nodes x 8 GPUs
