@@ -26,6 +26,7 @@ Two storage modes:
 from __future__ import annotations
 
 import asyncio
+import os
 import base64
 import logging
 import secrets
@@ -36,7 +37,7 @@ from ..api.labels import SelectorError, parse as parse_labels, parse_field_selec
 from ..api.meta import fast_copy, now_rfc3339
 from ..storage import wire
 from ..storage.mvcc import MVCCStore
-from ..utils.httpserver import HTTPServer, Response, StreamResponse, UpgradeResponse
+from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
 from . import admission as adm
@@ -147,6 +148,8 @@ class APIServer:
                                  and "kind" not in encryption_config else load_encryption_config(encryption_config))
         self.remote_address = store if isinstance(store, str) else None
         self.rstore = None            # RemoteStore once started (shared mode)
+        self.fanout = None            # FanoutClient: watches served by kamd-etcd (shared mode)
+        self.fanout_enabled = os.environ.get("KAMD_WATCH_FANOUT", "1") != "0"
         self.store = None if self.remote_address else (store or MVCCStore())
         self._applied_rev = 0
         self._rev_waiters: list = []  # heap of (rev, seq, future)
@@ -203,6 +206,8 @@ class APIServer:
         self.m_watchers = self.metrics.gauge("apiserver_registered_watchers", "Number of watchers", ("kind",))
         self.m_inflight = self.metrics.gauge("apiserver_current_inflight_requests", "In-flight requests", ("requestKind",))
         self.m_dropped = self.metrics.counter("apiserver_dropped_requests", "Requests dropped with 429", ("requestKind",))
+        self.m_fanout = self.metrics.counter("apiserver_watch_fanout_handoffs_total",
+                                             "Watches handed to the store's native fan-out", ("resource",))
         self.m_retries = self.metrics.counter("apiserver_shared_store_retries_total",
                                               "Requests re-run because this worker's cache lagged the shared store",
                                               ("reason",))
@@ -315,6 +320,8 @@ class APIServer:
     async def _start_remote(self):
         from ..storage.remote import RemoteStore
         self.rstore = await RemoteStore(self.remote_address).connect()
+        from ..storage.remote import FanoutClient
+        self.fanout = FanoutClient.for_store(self.remote_address) if self.fanout_enabled else None
         # one RANGE is an atomic snapshot (the store is single-threaded); watch from its revision
         kvs, _, rev = await self.rstore.range("/registry/")
         for kv in kvs:
@@ -1296,6 +1303,26 @@ class APIServer:
             ri.list_kind.encode(), ri.group_version.encode(), md.encode()) + b",".join(e.raw for e in entries) + b"]}"
         return Response(200, body)
 
+    def _fanout_spec(self, req, ri, ns, label_selector, field_selector):
+        """Requirements for kamd-etcd's watch fan-out, or None when this watch must stay here:
+        TLS connections (the TLS session lives in this process), encrypted or non-JSON storage
+        (the store cannot read the index frame), quantity comparisons in label selectors."""
+        if self.fanout is None or ri.plural in self.transformers or self.storage_codec.media_type != codec.JSON:
+            return None
+        if req.transport is None or req.transport.get_extra_info("sslcontext") is not None:
+            return None
+        reqs = []
+        if label_selector:
+            for r in parse_labels(label_selector).reqs:
+                op = {"=": "=", "==": "=", "!=": "!=", "in": "in", "notin": "notin", "exists": "exists", "!": "!"}.get(r.op)
+                if op is None:
+                    return None
+                reqs.append((0, op, r.key, list(r.values)))
+        if field_selector:
+            for k, op, v in parse_field_selector(field_selector).terms:
+                reqs.append((1, "!=" if op == "!=" else "=", k, [v]))
+        return reqs
+
     def _watch(self, req, ri, ns, name):
         q = req.query
         rv = q.get("resourceVersion")
@@ -1304,6 +1331,13 @@ class APIServer:
             fsel = (fsel + "," if fsel else "") + f"metadata.name={name}"
         fsel = self._hide_uninitialized(q, fsel)
         timeout = float(q.get("timeoutSeconds") or 0) or None
+        reqs = self._fanout_spec(req, ri, ns, q.get("labelSelector"), fsel)
+        if reqs is not None:
+            # shared-store mode: the store streams this watch itself (C++ fan-out)
+            send_initial = not rv or rv == "0"
+            msg = self.fanout.encode(m.prefix_for(ri, ns), send_initial, 0 if send_initial else int(rv), timeout, reqs)
+            self.m_fanout.labels(ri.plural).inc()
+            return HandoffResponse(lambda fd: self.fanout.handoff(fd, msg))
         cache = self.caches[ri.plural]
         send_initial = not rv or rv == "0"
         from_rev = int(rv) if rv and rv != "0" else None

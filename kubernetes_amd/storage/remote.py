@@ -186,6 +186,51 @@ class RemoteStore:
             self._proto.transport.close()
 
 
+class FanoutClient:
+    """Hands an accepted watch connection to `kamd-etcd`'s watch fan-out (SCM_RIGHTS over the
+    `<store socket>.watch` unix socket) with its spec; the store then serves the HTTP chunked
+    watch stream itself (see native/store/mvcc_store.cc "Watch fan-out")."""
+
+    LABEL, FIELD = 0, 1
+    OPS = {"=": 0, "==": 0, "!=": 1, "in": 2, "notin": 3, "exists": 4, "!": 5}
+
+    def __init__(self, path):
+        self.path = path
+
+    @classmethod
+    def for_store(cls, address):
+        if address and address.startswith("unix://"):
+            p = address[len("unix://"):] + ".watch"
+            if os.path.exists(p):
+                return cls(p)
+        return None
+
+    @staticmethod
+    def _s(b: bytes) -> bytes:
+        return struct.pack("<I", len(b)) + b
+
+    def encode(self, prefix, send_initial, from_rev, timeout, reqs) -> bytes:
+        """reqs: [(target, op, key, [values])] with op one of OPS."""
+        out = struct.pack("<BBqd", 1, 1 if send_initial else 0, int(from_rev or 0), float(timeout or 0))
+        out += self._s(prefix.encode())
+        out += struct.pack("<H", len(reqs))
+        for target, op, key, vals in reqs:
+            out += struct.pack("<BB", target, self.OPS[op]) + self._s(key.encode()) + struct.pack("<H", len(vals))
+            for v in vals:
+                out += self._s(str(v).encode())
+        return struct.pack("<I", len(out)) + out
+
+    def handoff(self, fd, msg: bytes):
+        import socket
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        try:
+            s.settimeout(5.0)
+            s.connect(self.path)
+            socket.send_fds(s, [msg], [fd])
+        finally:
+            s.close()
+
+
 class StoreServer:
     """Runs `kamd-etcd` as a child process on a unix socket (or TCP port)."""
 
@@ -213,7 +258,8 @@ class StoreServer:
             port_file = tempfile.mktemp(prefix="kamd-etcd-port-")
             cmd += ["--listen-tcp", "0", "--port-file", port_file]
         else:
-            cmd += ["--listen-unix", self.socket_path]
+            # watch fan-out handoffs next to the store socket (FanoutClient.for_store)
+            cmd += ["--listen-unix", self.socket_path, "--listen-handoff", self.socket_path + ".watch"]
         if self.wal:
             cmd += ["--wal", self.wal]
         log_dir = os.environ.get("KAMD_ETCD_LOG_DIR")
@@ -249,8 +295,9 @@ class StoreServer:
                 self.proc.wait()
         if self.dir:
             try:
-                if os.path.exists(self.socket_path):
-                    os.unlink(self.socket_path)
+                for p in (self.socket_path, self.socket_path + ".watch"):
+                    if os.path.exists(p):
+                        os.unlink(p)
                 os.rmdir(self.dir)
             except OSError:
                 pass

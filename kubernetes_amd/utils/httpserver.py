@@ -76,6 +76,17 @@ class UpgradeResponse:
         self.protocol = protocol
 
 
+class HandoffResponse:
+    """Returned by a handler that gives the whole connection to another process: `run(fd)`
+    receives a duplicate of the client socket (e.g. to pass it with SCM_RIGHTS); this server
+    then forgets the connection without writing anything (the other process owns the reply)."""
+
+    __slots__ = ("run",)
+
+    def __init__(self, run):
+        self.run = run
+
+
 class ChunkWriter:
     __slots__ = ("transport", "closed", "_proto")
 
@@ -198,6 +209,19 @@ class _Conn(asyncio.Protocol):
                     return
                 if isinstance(resp, UpgradeResponse):
                     await self._upgrade(resp)
+                    return
+                if isinstance(resp, HandoffResponse):
+                    import os
+                    sock = self.transport.get_extra_info("socket")
+                    fd = os.dup(sock.fileno())
+                    try:
+                        resp.run(fd)
+                    except OSError:
+                        log.exception("connection handoff failed")
+                    finally:
+                        os.close(fd)
+                    # close only this process's descriptor: the peer's process now holds the socket
+                    self.transport.abort()
                     return
                 if isinstance(resp, StreamResponse):
                     self.streaming = True

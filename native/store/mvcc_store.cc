@@ -37,6 +37,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
+#include <time.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -60,7 +61,8 @@ struct Event {
   uint8_t type;  // 0 put, 1 delete
   int64_t rev;
   std::string key;
-  std::shared_ptr<KV> kv;  // state after the event (for delete: last value, version 0)
+  std::shared_ptr<KV> kv;    // state after the event (for delete: last value, version 0)
+  std::shared_ptr<KV> prev;  // state before the event (null for a create)
 };
 
 struct Cmp {
@@ -131,6 +133,7 @@ class Engine {
         std::string v = o.val;
         inject(&v, o.token, rs);
         auto& slot = data_[o.key];
+        std::shared_ptr<KV> before = slot;
         auto nk = std::make_shared<KV>();
         nk->mod_rev = r;
         nk->value = std::move(v);
@@ -142,7 +145,7 @@ class Engine {
           nk->version = 1;
         }
         slot = nk;
-        record(Event{0, r, o.key, nk}, evs);
+        record(Event{0, r, o.key, nk, before}, evs);
         log_wal(0, last, o.key, nk->value);
         ++changes;
       } else {
@@ -158,8 +161,9 @@ class Engine {
           dk->value = o.val;
           inject(&dk->value, o.token, rs);
         }
+        std::shared_ptr<KV> before = it->second;
         data_.erase(it);
-        record(Event{1, r, o.key, dk}, evs);
+        record(Event{1, r, o.key, dk, before}, evs);
         log_wal(1, last, o.key, "");
         ++changes;
       }
@@ -207,6 +211,14 @@ class Engine {
   }
 
   size_t size() const { return data_.size(); }
+
+  template <typename F>
+  void for_prefix(const std::string& prefix, F f) const {
+    for (auto it = data_.lower_bound(prefix); it != data_.end(); ++it) {
+      if (it->first.compare(0, prefix.size(), prefix) != 0) break;
+      f(it->first, *it->second);
+    }
+  }
 
  private:
   void record(Event&& e, std::vector<Event>* evs) {
@@ -421,6 +433,155 @@ struct Watch {
   std::string prefix;
 };
 
+
+// ---------------------------------------------------------------------------
+// Watch fan-out: Kubernetes watch streams served by the store itself.
+//
+// An API server worker that accepted `GET /api/v1/pods?watch=1` (and authorized it) hands the
+// client's socket to this process over the handoff listener (SCM_RIGHTS) together with the
+// watch spec: key prefix, start revision or "send the initial state", timeout and the label /
+// field requirements. From then on this single epoll loop writes the HTTP chunked watch stream
+// (`{"type":"ADDED","object":{...}}` lines, the reference's cacher.go watch format) straight
+// from committed transactions, so the per-event fan-out to hundreds of kubelets, scheduler
+// shards and informers costs a header parse and a memcpy per matching watcher here instead of
+// Python work in every API server worker (reference: staging/.../apiserver/pkg/storage/cacher.go
+// dispatchEvent + indexed watchers). Values must carry the shared-store index frame
+// (00 'K' 'H' | u32 len | JSON [fields, labels] | object JSON).
+struct Index {
+  bool ok = false;
+  std::map<std::string, std::string> fields, labels;
+  size_t body = 0;  // offset of the object JSON in the value
+};
+
+struct JsonCursor {
+  const char* p;
+  const char* e;
+  bool ok = true;
+  void ws() { while (p < e && (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r')) ++p; }
+  bool eat(char c) { ws(); if (p < e && *p == c) { ++p; return true; } return false; }
+  static void utf8(std::string* o, unsigned cp) {
+    if (cp < 0x80) o->push_back((char)cp);
+    else if (cp < 0x800) { o->push_back((char)(0xC0 | (cp >> 6))); o->push_back((char)(0x80 | (cp & 0x3F))); }
+    else { o->push_back((char)(0xE0 | (cp >> 12))); o->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+           o->push_back((char)(0x80 | (cp & 0x3F))); }
+  }
+  bool str(std::string* o) {
+    ws();
+    if (p >= e || *p != '"') return ok = false;
+    ++p;
+    while (p < e && *p != '"') {
+      if (*p == '\\') {
+        if (++p >= e) return ok = false;
+        char c = *p++;
+        switch (c) {
+          case 'n': o->push_back('\n'); break;
+          case 't': o->push_back('\t'); break;
+          case 'r': o->push_back('\r'); break;
+          case 'b': o->push_back('\b'); break;
+          case 'f': o->push_back('\f'); break;
+          case 'u': {
+            if (e - p < 4) return ok = false;
+            unsigned cp = (unsigned)strtoul(std::string(p, 4).c_str(), nullptr, 16);
+            p += 4;
+            utf8(o, cp);
+            break;
+          }
+          default: o->push_back(c);
+        }
+      } else {
+        o->push_back(*p++);
+      }
+    }
+    if (p >= e) return ok = false;
+    ++p;
+    return true;
+  }
+  // {"k":"v",...} with string values (anything else fails the parse)
+  bool obj(std::map<std::string, std::string>* m) {
+    if (!eat('{')) return ok = false;
+    if (eat('}')) return true;
+    do {
+      std::string k, v;
+      if (!str(&k) || !eat(':') || !str(&v)) return ok = false;
+      (*m)[k] = v;
+    } while (eat(','));
+    return eat('}') || (ok = false);
+  }
+};
+
+static Index parse_index(const std::string& v) {
+  Index ix;
+  if (v.size() < 7 || v[0] != '\0' || v[1] != 'K' || v[2] != 'H') return ix;
+  uint32_t hl;
+  memcpy(&hl, v.data() + 3, 4);
+  if (7 + (size_t)hl > v.size()) return ix;
+  JsonCursor c{v.data() + 7, v.data() + 7 + hl};
+  if (!c.eat('[') || !c.obj(&ix.fields) || !c.eat(',') || !c.obj(&ix.labels) || !c.eat(']')) return ix;
+  ix.body = 7 + hl;
+  ix.ok = true;
+  return ix;
+}
+
+struct Requirement {
+  uint8_t target;  // 0 label, 1 field
+  uint8_t op;      // 0 =, 1 !=, 2 in, 3 notin, 4 exists, 5 !exists
+  std::string key;
+  std::vector<std::string> vals;
+  bool matches(const Index& ix) const {
+    const auto& m = target == 0 ? ix.labels : ix.fields;
+    auto it = m.find(key);
+    // a field that is absent reads as "" (fields.Set semantics); labels keep presence
+    bool has = it != m.end() || target == 1;
+    const std::string empty;
+    const std::string& v = it != m.end() ? it->second : empty;
+    auto in = [&]() { return std::find(vals.begin(), vals.end(), v) != vals.end(); };
+    switch (op) {
+      case 0: case 2: return has && in();
+      case 1: case 3: return !has || !in();
+      case 4: return it != m.end();
+      case 5: return it == m.end();
+    }
+    return false;
+  }
+};
+
+struct FanWatch {
+  int fd = -1;
+  std::string prefix;
+  int64_t min_rev = 0;
+  std::vector<Requirement> reqs;
+  std::string out;
+  bool dead = false;
+  double deadline = 0;  // CLOCK_MONOTONIC seconds, 0 = none
+  bool matches(const Index& ix) const {
+    if (!ix.ok) return false;
+    for (const auto& r : reqs)
+      if (!r.matches(ix)) return false;
+    return true;
+  }
+};
+
+static double mono_now() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void chunk(std::string* out, const char* type, const std::string& v, size_t body) {
+  // {"type":"X","object":<object JSON>}\n as one HTTP chunk
+  static const char pre[] = "{\"type\":\"";
+  static const char mid[] = "\",\"object\":";
+  size_t n = (sizeof pre - 1) + strlen(type) + (sizeof mid - 1) + (v.size() - body) + 2;
+  char hex[24];
+  int hl = snprintf(hex, sizeof hex, "%zx\r\n", n);
+  out->append(hex, (size_t)hl);
+  out->append(pre, sizeof pre - 1);
+  out->append(type);
+  out->append(mid, sizeof mid - 1);
+  out->append(v, body, std::string::npos);
+  out->append("}\n\r\n", 4);
+}
+
 class Server {
  public:
   Server(Engine* e) : eng_(e) {}
@@ -433,6 +594,18 @@ class Server {
     unlink(path);
     if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, 1024) < 0) { perror("bind/listen"); return -1; }
     add_listener(fd);
+    return fd;
+  }
+
+  int listen_handoff(const char* path) {
+    int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    sockaddr_un a{};
+    a.sun_family = AF_UNIX;
+    snprintf(a.sun_path, sizeof a.sun_path, "%s", path);
+    unlink(path);
+    if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, 1024) < 0) { perror("bind/listen handoff"); return -1; }
+    add_listener(fd);
+    handoff_listeners_[fd] = 1;
     return fd;
   }
 
@@ -457,10 +630,24 @@ class Server {
   void run(volatile sig_atomic_t* stop) {
     epoll_event evs[256];
     while (!*stop) {
-      int n = epoll_wait(ep_, evs, 256, 1000);
+      int n = epoll_wait(ep_, evs, 256, next_timeout_ms());
       for (int i = 0; i < n; ++i) {
         int fd = evs[i].data.fd;
+        if (handoff_listeners_.count(fd)) { accept_handoffs(fd); continue; }
         if (listeners_.count(fd)) { accept_all(fd); continue; }
+        if (handoffs_.count(fd)) { read_handoff(fd); continue; }
+        auto fw = fan_.find(fd);
+        if (fw != fan_.end()) {
+          FanWatch* w = fw->second.get();
+          if (evs[i].events & (EPOLLHUP | EPOLLERR | EPOLLRDHUP)) { close_fan(w); continue; }
+          if (evs[i].events & EPOLLIN) {
+            char junk[4096];
+            ssize_t r = read(fd, junk, sizeof junk);
+            if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK)) { close_fan(w); continue; }
+          }
+          if (evs[i].events & EPOLLOUT) flush_fan(w);
+          continue;
+        }
         auto it = conns_.find(fd);
         if (it == conns_.end()) continue;
         Conn* c = it->second.get();
@@ -473,6 +660,10 @@ class Server {
       // flush every connection with pending output once per loop (coalesces watch events)
       for (Conn* c : dirty_) flush(c);
       dirty_.clear();
+      for (FanWatch* w : fan_dirty_) flush_fan(w);
+      fan_dirty_.clear();
+      expire_fan();
+      reap_fan();
     }
   }
 
@@ -601,6 +792,7 @@ class Server {
           w.put<int64_t>(rev);
           reply(c, id, 0, w.b);
           dispatch(evs);
+          fan_dispatch(evs);
         } else {
           w.put<uint16_t>((uint16_t)failed);
           const KV* kv = eng_->get(cmps[failed].key);
@@ -667,6 +859,241 @@ class Server {
     }
   }
 
+
+  // -- watch fan-out ---------------------------------------------------------
+  struct Handoff {
+    std::string buf;
+    int client = -1;
+  };
+
+  int next_timeout_ms() {
+    double soonest = 0;
+    for (auto& kv : fan_)
+      if (kv.second->deadline > 0 && (soonest == 0 || kv.second->deadline < soonest)) soonest = kv.second->deadline;
+    if (soonest == 0) return 1000;
+    double ms = (soonest - mono_now()) * 1000.0;
+    return ms < 0 ? 0 : (ms > 1000 ? 1000 : (int)ms + 1);
+  }
+
+  void accept_handoffs(int lfd) {
+    for (;;) {
+      int fd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) return;
+      epoll_event e{};
+      e.events = EPOLLIN | EPOLLRDHUP;
+      e.data.fd = fd;
+      epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+      handoffs_[fd] = Handoff{};
+    }
+  }
+
+  void drop_handoff(int fd) {
+    auto it = handoffs_.find(fd);
+    if (it != handoffs_.end() && it->second.client >= 0) close(it->second.client);
+    handoffs_.erase(fd);
+    epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+    close(fd);
+  }
+
+  void read_handoff(int fd) {
+    Handoff& h = handoffs_[fd];
+    for (;;) {
+      char data[8192];
+      char ctl[CMSG_SPACE(sizeof(int))];
+      iovec iov{data, sizeof data};
+      msghdr mh{};
+      mh.msg_iov = &iov;
+      mh.msg_iovlen = 1;
+      mh.msg_control = ctl;
+      mh.msg_controllen = sizeof ctl;
+      ssize_t n = recvmsg(fd, &mh, MSG_CMSG_CLOEXEC);
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;   // wait for the rest
+      if (n <= 0) { drop_handoff(fd); return; }
+      for (cmsghdr* c = CMSG_FIRSTHDR(&mh); c; c = CMSG_NXTHDR(&mh, c)) {
+        if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS) {
+          int got;
+          memcpy(&got, CMSG_DATA(c), sizeof got);
+          if (h.client >= 0) close(got); else h.client = got;
+        }
+      }
+      h.buf.append(data, (size_t)n);
+      if (h.buf.size() >= 4) {
+        uint32_t len;
+        memcpy(&len, h.buf.data(), 4);
+        if (h.buf.size() >= 4 + (size_t)len) {
+          int client = h.client;
+          std::string msg = h.buf.substr(4, len);
+          h.client = -1;
+          drop_handoff(fd);                     // one watch per handoff connection
+          if (client >= 0) start_fan(client, msg);
+          return;
+        }
+      }
+    }
+  }
+
+  void start_fan(int client, const std::string& msg) {
+    Reader r{msg.data(), msg.data() + msg.size()};
+    auto w = std::make_unique<FanWatch>();
+    w->fd = client;
+    uint8_t ver = r.get<uint8_t>();
+    uint8_t send_initial = r.get<uint8_t>();
+    int64_t from = r.get<int64_t>();
+    double timeout = r.get<double>();
+    w->prefix = r.str();
+    uint16_t nreq = r.get<uint16_t>();
+    for (uint16_t i = 0; i < nreq && r.ok; ++i) {
+      Requirement q;
+      q.target = r.get<uint8_t>();
+      q.op = r.get<uint8_t>();
+      q.key = r.str();
+      uint16_t nv = r.get<uint16_t>();
+      for (uint16_t j = 0; j < nv && r.ok; ++j) q.vals.push_back(r.str());
+      w->reqs.push_back(std::move(q));
+    }
+    if (!r.ok || ver != 1) { close(client); return; }
+    int fl = fcntl(client, F_GETFL);
+    fcntl(client, F_SETFL, fl | O_NONBLOCK);
+    int one = 1;
+    setsockopt(client, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (timeout > 0) w->deadline = mono_now() + timeout;
+    w->out = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n"
+             "Cache-Control: no-cache, private\r\n\r\n";
+    if (send_initial) {
+      eng_->for_prefix(w->prefix, [&](const std::string&, const KV& kv) {
+        Index ix = parse_index(kv.value);
+        if (w->matches(ix)) chunk(&w->out, "ADDED", kv.value, ix.body);
+      });
+    } else if (from > 0) {
+      std::vector<const Event*> evs;
+      if (!eng_->since(from, w->prefix, &evs)) {
+        char b[512];
+        snprintf(b, sizeof b,
+                 "{\"type\":\"ERROR\",\"object\":{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"metadata\":{},"
+                 "\"status\":\"Failure\",\"message\":\"too old resource version: %lld (%lld)\",\"reason\":\"Expired\","
+                 "\"code\":410}}\n", (long long)from, (long long)eng_->compacted());
+        char hex[24];
+        int hl = snprintf(hex, sizeof hex, "%zx\r\n", strlen(b));
+        w->out.append(hex, (size_t)hl).append(b).append("\r\n0\r\n\r\n");
+        w->dead = true;   // close once written
+      } else {
+        for (const Event* e : evs) fan_one(w.get(), *e);
+      }
+      w->min_rev = from;
+    }
+    FanWatch* raw = w.get();
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP;
+    e.data.fd = client;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, client, &e);
+    fan_[client] = std::move(w);
+    flush_fan(raw);
+  }
+
+  // one event into one watch (cacher.go dispatch rules: a MODIFIED object that stops matching is
+  // a DELETED for that watcher, one that starts matching an ADDED)
+  void fan_one(FanWatch* w, const Event& ev, const Index* cur = nullptr, const Index* prv = nullptr) {
+    if (ev.key.compare(0, w->prefix.size(), w->prefix) != 0 || ev.rev <= w->min_rev) return;
+    Index c0, p0;
+    if (!cur) { c0 = parse_index(ev.kv->value); cur = &c0; }
+    if (!prv) { if (ev.prev) p0 = parse_index(ev.prev->value); prv = &p0; }
+    bool now = w->matches(*cur);
+    bool was = ev.prev && w->matches(*prv);
+    const std::string& v = ev.kv->value;
+    if (ev.type == 0) {
+      if (now && was) chunk(&w->out, "MODIFIED", v, cur->body);
+      else if (now) chunk(&w->out, "ADDED", v, cur->body);
+      else if (was) chunk(&w->out, "DELETED", v, cur->body);
+      else return;
+    } else {
+      if (!(now || was) || !cur->ok) return;
+      chunk(&w->out, "DELETED", v, cur->body);
+    }
+    mark_fan(w);
+  }
+
+  void fan_dispatch(const std::vector<Event>& evs) {
+    if (fan_.empty()) return;
+    for (const Event& ev : evs) {
+      Index cur, prv;
+      bool parsed = false;
+      for (auto& kv : fan_) {
+        FanWatch* w = kv.second.get();
+        if (w->dead || ev.key.compare(0, w->prefix.size(), w->prefix) != 0) continue;
+        if (!parsed) {
+          cur = parse_index(ev.kv->value);
+          if (ev.prev) prv = parse_index(ev.prev->value);
+          parsed = true;
+        }
+        fan_one(w, ev, &cur, &prv);
+      }
+    }
+  }
+
+  void mark_fan(FanWatch* w) {
+    if (!w->out.empty()) fan_dirty_.push_back(w);
+  }
+
+  void flush_fan(FanWatch* w) {
+    while (!w->out.empty()) {
+      ssize_t n = write(w->fd, w->out.data(), w->out.size());
+      if (n > 0) { w->out.erase(0, (size_t)n); continue; }
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (w->out.size() > (64u << 20)) { w->dead = true; w->out.clear(); return; }   // slow watcher
+        epoll_event e{};
+        e.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+        e.data.fd = w->fd;
+        epoll_ctl(ep_, EPOLL_CTL_MOD, w->fd, &e);
+        return;
+      }
+      w->dead = true;
+      w->out.clear();
+      return;
+    }
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP;
+    e.data.fd = w->fd;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, w->fd, &e);
+  }
+
+  void expire_fan() {
+    double now = 0;
+    for (auto& kv : fan_) {
+      FanWatch* w = kv.second.get();
+      if (w->deadline <= 0 || w->dead) continue;
+      if (now == 0) now = mono_now();
+      if (now >= w->deadline) {
+        w->out.append("0\r\n\r\n");   // end of the chunked body: the watch timed out normally
+        w->dead = true;
+        flush_fan(w);
+      }
+    }
+  }
+
+  void close_fan(FanWatch* w) {
+    w->dead = true;
+    w->out.clear();
+  }
+
+  void reap_fan() {
+    for (auto it = fan_.begin(); it != fan_.end();) {
+      FanWatch* w = it->second.get();
+      if (w->dead && w->out.empty()) {
+        fan_dirty_.erase(std::remove(fan_dirty_.begin(), fan_dirty_.end(), w), fan_dirty_.end());
+        epoll_ctl(ep_, EPOLL_CTL_DEL, w->fd, nullptr);
+        close(w->fd);
+        it = fan_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+
+  std::unordered_map<int, int> handoff_listeners_;
+  std::unordered_map<int, Handoff> handoffs_;
+  std::map<int, std::unique_ptr<FanWatch>> fan_;
+  std::vector<FanWatch*> fan_dirty_;
+
   Engine* eng_;
   int ep_ = -1;
   std::unordered_map<int, int> listeners_;
@@ -689,6 +1116,7 @@ int main(int argc, char** argv) {
   const char* unix_path = nullptr;
   const char* wal = nullptr;
   const char* port_file = nullptr;
+  const char* handoff_path = nullptr;
   int tcp_port = -1;
   size_t hist = 500000;
   for (int i = 1; i < argc; ++i) {
@@ -699,12 +1127,14 @@ int main(int argc, char** argv) {
     else if (a == "--wal") wal = val();
     else if (a == "--history") hist = (size_t)atol(val());
     else if (a == "--port-file") port_file = val();
-    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--wal FILE] [--history N]\n"); return 2; }
+    else if (a == "--listen-handoff") handoff_path = val();
+    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--listen-handoff PATH] [--wal FILE] [--history N]\n"); return 2; }
   }
   kamd::Engine eng(hist);
   if (wal && !eng.open_wal(wal)) { perror("wal"); return 1; }
   kamd::Server srv(&eng);
   if (unix_path && srv.listen_unix(unix_path) < 0) return 1;
+  if (handoff_path && srv.listen_handoff(handoff_path) < 0) return 1;
   if (tcp_port >= 0) {
     int bound = 0;
     if (srv.listen_tcp(tcp_port, &bound) < 0) return 1;
@@ -717,6 +1147,7 @@ int main(int argc, char** argv) {
   fprintf(stderr, "kamd-etcd: serving (rev %lld, %zu keys)\n", (long long)eng.rev(), eng.size());
   srv.run(&g_stop);
   if (unix_path) unlink(unix_path);
+  if (handoff_path) unlink(handoff_path);
   return 0;
 }
 #endif

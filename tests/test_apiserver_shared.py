@@ -229,3 +229,60 @@ def test_worker_restart_reloads_state(run, store):
         finally:
             await _close(servers, [b])
     run(main())
+
+
+def test_native_watch_fanout_semantics(run, store):
+    """Watches on shared-store workers are served by kamd-etcd's C++ fan-out: selector
+    transitions (ADDED when an object starts matching, DELETED when it stops), resume from a
+    resourceVersion, initial state, field selectors indexed by node, timeoutSeconds, and 410 for
+    a compacted version. The same semantics as the in-process cacher (cacher.go dispatchEvent)."""
+    from kubernetes_amd.storage.remote import RemoteStore
+
+    async def main():
+        servers, (a, b) = await _workers(store)
+        try:
+            assert servers[0].fanout is not None
+            sel_events, node_events = [], []
+            w1 = await b.watch("pods", "default", "0", label_selector="app=hip,tier!=db")
+            w2 = await a.watch("pods", None, "0", field_selector="spec.nodeName=gpu-node-1")
+
+            async def drain(w, out):
+                async for typ, obj in w:
+                    out.append((typ, obj["metadata"]["name"]))
+            t1 = asyncio.ensure_future(drain(w1, sel_events))
+            t2 = asyncio.ensure_future(drain(w2, node_events))
+            await a.create("pods", dict(gpu_pod("x1"), metadata={"name": "x1", "namespace": "default",
+                                                                  "labels": {"app": "hip"}}))
+            await a.create("pods", dict(gpu_pod("x2"), metadata={"name": "x2", "namespace": "default",
+                                                                  "labels": {"app": "other"}}))
+            await b.patch("pods", "x2", {"metadata": {"labels": {"app": "hip"}}}, "default")      # starts matching
+            await a.patch("pods", "x1", {"metadata": {"labels": {"tier": "db"}}}, "default")      # stops matching
+            p = await a.get("pods", "x2", "default")
+            er = p["spec"]["extendedResources"][0]["name"]
+            await a.bind("default", "x2", "gpu-node-1", {er: {"resources": ["g0"]}})
+            await a.delete("pods", "x2", "default", grace_period=0)
+            await _eventually(lambda: asyncio.sleep(0, len(sel_events) >= 4 and len(node_events) >= 2))
+            assert sel_events == [("ADDED", "x1"), ("ADDED", "x2"), ("DELETED", "x1"), ("MODIFIED", "x2"),
+                                  ("DELETED", "x2")][:len(sel_events)] and len(sel_events) == 5
+            assert node_events == [("ADDED", "x2"), ("DELETED", "x2")]
+            # resume from a resourceVersion: exactly the later changes
+            rv = (await a.list("pods", "default"))["metadata"]["resourceVersion"]
+            await a.patch("pods", "x1", {"metadata": {"labels": {"more": "1"}}}, "default")
+            w3 = await b.watch("pods", "default", rv, timeout_seconds=1)
+            got = [(t, o["metadata"]["name"]) async for t, o in w3]        # ends at the timeout
+            assert got == [("MODIFIED", "x1")]
+            # a compacted version is 410 Gone, delivered as an ERROR event
+            rs = await RemoteStore(store).connect()
+            await rs.compact(int(rv) + 1)
+            from kubernetes_amd.client.rest import APIStatusError as _E
+            w4 = await a.watch("pods", "default", "2", timeout_seconds=2)
+            with pytest.raises(_E) as ei:
+                [x async for x in w4]
+            assert ei.value.code == 410
+            m = (await a.http.request("GET", "/metrics", None, "text/plain"))[1].decode()
+            assert "apiserver_watch_fanout_handoffs_total" in m
+            t1.cancel()
+            t2.cancel()
+        finally:
+            await _close(servers, [a, b])
+    run(main())
