@@ -70,9 +70,10 @@ def cpu_budget():
 def control_plane_shape(world, workers=0, shards=0):
     """API server workers and scheduler shards for `world` ranks (0 = auto).
 
-    Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep): with one rank the single API
-    server + scheduler are fastest; from 2 ranks on, parallel API server workers over the
-    native store and 2 scheduler shards win, up to 4 workers once ranks use most cores.
+    Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep, profiles/r2_scale): with one rank the
+    single API server + scheduler are fastest; from 2 ranks on, parallel API server workers over
+    the native store (watches served by its C++ fan-out) and 2 scheduler shards, 4 workers from
+    4 ranks on.
     On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — one API
     server worker and one scheduler shard per rank, up to 8 each — so per-rank work (weak
     scaling) is met by per-rank control-plane capacity instead of a fixed-size control plane."""
@@ -85,7 +86,7 @@ def control_plane_shape(world, workers=0, shards=0):
         elif big:
             workers = min(8, world, max(1, spare // 6))
         else:
-            workers = 2 if world <= 4 else 4
+            workers = 2 if world < 4 else 4
     if shards <= 0:
         if world == 1 or spare < 3:
             shards = 1
@@ -102,8 +103,10 @@ def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
     bounded by the CPUs left after ranks and the control plane."""
     if want > 0:
         return max(1, min(want, nodes_per_rank))
-    spare = cpu_budget() - world - workers - shards - 1
-    return max(1, min(nodes_per_rank, 4, spare // max(1, world)))
+    # hollow kubelets are mostly waiting on the control plane: mild oversubscription pays
+    # (profiles/r2_hollow_procs, r2_scale: N=4 on 16 CPUs 1868 -> 2578 pods/s with 2 per rank)
+    spare = cpu_budget() - workers - shards - 1
+    return max(1, min(nodes_per_rank, 4, max(2, spare // max(1, world))))
 
 
 def spawn_hollow_procs(args, url, rank, nprocs, tmp, payload_socket):
