@@ -22,14 +22,28 @@ def main(argv=None):
     ap.add_argument("--listen", default="/var/run/kamd-cri.sock")
     ap.add_argument("--runtime", default="process", choices=["process", "stub"])
     ap.add_argument("--root-dir", default="/var/lib/kamd-cri")
+    ap.add_argument("--hooks-dir", default=None,
+                    help="runtime hooks (JSON {runtime, annotations, images}) choosing a runtime per container "
+                         "(the fork's dockershim hooks.d); both runtimes are then available")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
 
     async def start():
         rt = ProcessRuntime(os.path.join(a.root_dir, "containers")) if a.runtime == "process" else StubRuntime()
+        hook_task = None
+        if a.hooks_dir:
+            import asyncio
+
+            from ..kubelet.runtime.hooks import HookedRuntime, HookService
+            runtimes = {"process": rt if a.runtime == "process" else ProcessRuntime(os.path.join(a.root_dir, "containers")),
+                        "stub": rt if a.runtime == "stub" else StubRuntime()}
+            hooks = HookService(a.hooks_dir, available_runtimes=runtimes).load()
+            rt = HookedRuntime(runtimes, a.runtime, hooks)
+            hook_task = asyncio.ensure_future(hooks.watch())
         os.makedirs(os.path.dirname(os.path.abspath(a.listen)), exist_ok=True)
         srv = await CRIServer(rt, a.listen, checkpoint_dir=os.path.join(a.root_dir, "sandbox")).start()
+        srv.hook_task = hook_task
         print(f"kamd-cri serving CRI v1alpha1 ({rt.name} runtime) on unix://{a.listen}, "
               f"streaming on 127.0.0.1:{srv.streaming.port}", flush=True)
         return srv

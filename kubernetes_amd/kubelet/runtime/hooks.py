@@ -11,9 +11,12 @@ kept as a generic annotation/image → runtime selector (e.g. to pick a sandboxe
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import logging
 import os
+
+from .base import Runtime
 
 log = logging.getLogger("hooks")
 
@@ -27,6 +30,7 @@ class HookService:
         self.hooks: dict[str, dict] = {}
 
     def load(self):
+        self._loaded = self._snapshot()      # what the hook set reflects (watch() compares to it)
         self.hooks.clear()
         if not os.path.isdir(self.dir):
             return self
@@ -52,6 +56,22 @@ class HookService:
         h.setdefault("images", [])
         return h
 
+    def _snapshot(self):
+        try:
+            return sorted((f, os.stat(os.path.join(self.dir, f)).st_mtime_ns) for f in os.listdir(self.dir)
+                          if f.endswith(".json"))
+        except OSError:
+            return []
+
+    async def watch(self, period=1.0):
+        """fsnotify equivalent (`docker_hooks.go` Start: Create/Write/Remove events reload the
+        hooks): the directory is re-scanned when its JSON files or their mtimes change."""
+        while True:
+            await asyncio.sleep(period)
+            if self._snapshot() != getattr(self, "_loaded", None):
+                self.load()
+                log.info("hooks reloaded: %s", {k: v["runtime"] for k, v in self.hooks.items()})
+
     def is_valid(self, h):
         return h["runtime"] in self.available
 
@@ -65,3 +85,81 @@ class HookService:
                 if any(t.startswith(prefix) for t in tags):
                     return h["runtime"]
         return None
+
+
+class HookedRuntime(Runtime):
+    """The dockershim side of F11: several low-level runtimes behind one CRI runtime, the hook
+    service picking one per container (`docker_container.go:116-133` sets HostConfig.Runtime).
+    Sandboxes start in the default runtime; a container routed elsewhere gets a companion
+    sandbox there (created on first use), and every later call for it goes to that runtime."""
+
+    def __init__(self, runtimes: dict, default: str, hooks: HookService):
+        super().__init__()
+        self.runtimes = runtimes
+        self.default = default
+        self.hooks = hooks
+        self.name = runtimes[default].name
+        self.sandboxes: dict[str, dict] = {}      # sid -> {runtime name: sid in that runtime}
+        self.owner: dict[str, str] = {}           # container id -> runtime name
+        self.chosen: dict[str, str] = {}          # container id -> runtime chosen by a hook (audit)
+        self.images = getattr(runtimes[default], "images", None)
+        for rt in runtimes.values():
+            rt.on_exit(self._fire_exit)
+
+    def _rt(self, cid):
+        return self.runtimes[self.owner.get(cid, self.default)]
+
+    async def version(self):
+        return await self.runtimes[self.default].version()
+
+    async def run_pod_sandbox(self, pod, annotations):
+        sid = await self.runtimes[self.default].run_pod_sandbox(pod, annotations)
+        self.sandboxes[sid] = {self.default: sid, "_pod": pod, "_ann": dict(annotations or {})}
+        return sid
+
+    async def stop_pod_sandbox(self, sid):
+        for name, sub in list((self.sandboxes.get(sid) or {self.default: sid}).items()):
+            if not name.startswith("_"):
+                await self.runtimes[name].stop_pod_sandbox(sub)
+
+    async def remove_pod_sandbox(self, sid):
+        for name, sub in list((self.sandboxes.pop(sid, None) or {self.default: sid}).items()):
+            if not name.startswith("_"):
+                await self.runtimes[name].remove_pod_sandbox(sub)
+
+    async def create_container(self, sid, pod, container, opts):
+        ann = {a["name"]: a["value"] for a in opts.annotations}
+        name = self.hooks.get_runtime(container.get("image", ""), ann) or self.default
+        if name not in self.runtimes:
+            name = self.default
+        sb = self.sandboxes.setdefault(sid, {self.default: sid, "_pod": pod, "_ann": {}})
+        if name not in sb:
+            sb[name] = await self.runtimes[name].run_pod_sandbox(sb["_pod"], sb["_ann"])
+        cid = await self.runtimes[name].create_container(sb[name], pod, container, opts)
+        self.owner[cid] = name
+        if name != self.default:
+            self.chosen[cid] = name
+        return cid
+
+    async def start_container(self, cid):
+        await self._rt(cid).start_container(cid)
+
+    async def stop_container(self, cid, timeout):
+        await self._rt(cid).stop_container(cid, timeout)
+
+    async def remove_container(self, cid):
+        await self._rt(cid).remove_container(cid)
+        self.owner.pop(cid, None)
+        self.chosen.pop(cid, None)
+
+    def container_status(self, cid):
+        return self._rt(cid).container_status(cid)
+
+    async def container_logs(self, cid, tail=None):
+        return await self._rt(cid).container_logs(cid, tail)
+
+    async def exec_sync(self, cid, cmd, timeout):
+        return await self._rt(cid).exec_sync(cid, cmd, timeout)
+
+    def list_containers(self):
+        return [c for rt in self.runtimes.values() for c in rt.list_containers()]
