@@ -212,6 +212,13 @@ class _Conn(asyncio.Protocol):
                     return
                 if isinstance(resp, HandoffResponse):
                     import os
+                    # earlier pipelined responses still buffered here must reach the peer first
+                    for _ in range(200):
+                        if self.transport.is_closing() or not self.transport.get_write_buffer_size():
+                            break
+                        await asyncio.sleep(0.005)
+                    if self.transport.is_closing():
+                        return
                     sock = self.transport.get_extra_info("socket")
                     fd = os.dup(sock.fileno())
                     try:
