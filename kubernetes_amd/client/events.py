@@ -40,7 +40,7 @@ class EventRecorder:
             w.cancel()
         self._workers = []
 
-    def event(self, obj, etype: str, reason: str, message: str):
+    def event(self, obj, etype: str, reason: str, message: str, field_path: str = ""):
         self.emitted.append((etype, reason, message))
         if len(self.emitted) > 1000:
             del self.emitted[:500]
@@ -48,7 +48,7 @@ class EventRecorder:
             return
         md = obj.get("metadata") or {}
         ns = md.get("namespace") or "default"
-        key = (md.get("uid"), reason, message)
+        key = (md.get("uid"), field_path, reason, message)
         now = now_rfc3339()
         prev = self._agg.get(key)
         if prev is not None and time.time() - prev["_t"] < 600:
@@ -63,7 +63,8 @@ class EventRecorder:
                   "involvedObject": {"kind": obj.get("kind", ""), "namespace": md.get("namespace", ""),
                                      "name": md.get("name", ""), "uid": md.get("uid", ""),
                                      "apiVersion": obj.get("apiVersion", "v1"),
-                                     "resourceVersion": md.get("resourceVersion", "")},
+                                     "resourceVersion": md.get("resourceVersion", ""),
+                                     **({"fieldPath": field_path} if field_path else {})},
                   "reason": reason, "message": message, "type": etype, "source": self.source,
                   "firstTimestamp": now, "lastTimestamp": now, "count": 1}
             self._agg[key] = dict(ev, _t=time.time())

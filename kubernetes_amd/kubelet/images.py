@@ -55,6 +55,8 @@ class ImageManager:
         present = await self.service.image_status(image)
         if present is not None and policy != "Always":
             self.last_used[present["id"]] = time.time()
+            # image_manager.go EnsureImageExists: "already present" is reported every time
+            self._event(pod, "Normal", "Pulled", f'Container image "{image}" already present on machine')
             return present["id"]
         if policy == "Never":
             msg = f'Container image "{image}" is not present with pull policy of Never'

@@ -81,6 +81,14 @@ class PodState:
         self.backoff: dict[str, list] = {}    # container name -> [next restart allowed at, current delay]
 
 
+def _field_path(pod, c):
+    """`ref.GetPartialReference` fieldPath of a container (`spec.containers{name}`)."""
+    spec = pod.get("spec") or {}
+    if any(ic.get("name") == c["name"] for ic in spec.get("initContainers") or ()):
+        return f"spec.initContainers{{{c['name']}}}"
+    return f"spec.containers{{{c['name']}}}"
+
+
 class Kubelet:
     def __init__(self, client, node_name, runtime, device_manager=None, cpu="128", memory="2Ti", pods=110,
                  labels=None, node_status_update_frequency=10.0, status_debounce=0.02, http_port=None,
@@ -843,8 +851,11 @@ class Kubelet:
         try:
             cid = await self.runtime.create_container(st.sandbox, st.pod, spec_c, opts)
             self.m_runtime_ops.labels("create_container").inc()
+            # kuberuntime_container.go startContainer: CreatedContainer / StartedContainer events
+            self.recorder.event(st.pod, "Normal", "Created", "Created container", field_path=_field_path(st.pod, c))
             await self.runtime.start_container(cid)
             self.m_runtime_ops.labels("start_container").inc()
+            self.recorder.event(st.pod, "Normal", "Started", "Started container", field_path=_field_path(st.pod, c))
         except Exception as e:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
             return None
@@ -1046,8 +1057,13 @@ class Kubelet:
                 await asyncio.wait_for(asyncio.gather(*(hook(*x) for x in hooks)), max(budget, 0.5))
             except asyncio.TimeoutError:
                 pass
-        for cid in list(st.containers.values()) + list(st.init_containers.values()):
+        for name, cid in list(st.containers.items()) + list(st.init_containers.items()):
             if cid is not None:
+                cs = rt.container_status(cid)
+                if cs is not None and cs.state != EXITED:
+                    # kuberuntime_container.go killContainer: KillingContainer event
+                    self.recorder.event(st.pod, "Normal", "Killing", f"Killing container with id {cid}:Need to kill Pod",
+                                        field_path=_field_path(st.pod, {"name": name}))
                 await rt.stop_container(cid, min(float(grace or 0), 2.0))
         if st.sandbox is not None:
             await rt.stop_pod_sandbox(st.sandbox)

@@ -133,3 +133,33 @@ def test_deleted_pod_is_not_resurrected_by_container_exit(run, tmp_path):
         finally:
             await cl.stop()
     run(main(), timeout=60)
+
+
+def test_container_lifecycle_events(run, tmp_path):
+    """The kubelet reports Pulled / Created / Started per container and Killing on deletion
+    (`kuberuntime_container.go`, `images/image_manager.go`), referencing the container by
+    fieldPath `spec.containers{name}` like `kubectl describe pod` shows."""
+    async def main():
+        cl = LocalCluster(nodes=1, gpus_per_node=0, workdir=str(tmp_path / "c"))
+        await cl.start()
+        c = cl.client
+        try:
+            await c.create("pods", {"metadata": {"name": "ev"}, "spec": {"containers": [
+                {"name": "main", "image": "busybox"}]}}, "default")
+            await cl.wait_pod("ev")
+            await c.delete("pods", "ev", "default")
+
+            async def killed():
+                evs = [e for e in (await c.list("events", "default"))["items"] if e["involvedObject"]["name"] == "ev"]
+                return evs if any(e["reason"] == "Killing" for e in evs) else None
+            evs = await cl.wait_for(killed, 20)
+            by = {e["reason"]: e for e in evs}
+            for r in ("Scheduled", "Pulled", "Created", "Started", "Killing"):
+                assert r in by, (r, sorted(by))
+            assert by["Started"]["involvedObject"]["fieldPath"] == "spec.containers{main}"
+            assert by["Pulled"]["message"] in ('Successfully pulled image "busybox"',
+                                               'Container image "busybox" already present on machine')
+            assert by["Started"]["source"]["component"] == "kubelet"
+        finally:
+            await cl.stop()
+    run(main(), timeout=60)
