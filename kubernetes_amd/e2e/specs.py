@@ -148,3 +148,204 @@ async def gpu_vector_add(f):
     assert all(assigned), assigned
     if n == 2:
         assert set(assigned[0]).isdisjoint(assigned[1]), assigned
+
+
+@conformance("Pods should be updated (labels) and the update observed by a watch")
+async def pod_update(f):
+    await f.client.create("pods", _pod("upd", "sleep 3600", restart="Always"), f.ns)
+    await f.pod_phase("upd", ("Running",))
+    lst = await f.client.list("pods", f.ns, label_selector="time=updated")
+    assert not lst["items"]
+    w = await f.client.watch("pods", f.ns, lst["metadata"]["resourceVersion"], label_selector="time=updated")
+    await f.client.patch("pods", "upd", {"metadata": {"labels": {"time": "updated"}}}, f.ns)
+    async for typ, obj in w:
+        assert typ == "ADDED" and obj["metadata"]["name"] == "upd"      # starts matching the selector
+        break
+    w.close()
+
+
+@conformance("InitContainer should invoke init containers in order before the app container")
+async def init_containers(f):
+    p = _pod("init", "cat $KUBERNETES_VOLUME_WORK/order 2>/dev/null; echo main")
+    p["spec"]["volumes"] = [{"name": "work", "emptyDir": {}}]
+    p["spec"]["initContainers"] = [
+        {"name": "init1", "image": BUSYBOX, "command": ["sh", "-c", "echo init1 >> $KUBERNETES_VOLUME_WORK/order"],
+         "volumeMounts": [{"name": "work", "mountPath": "/work"}]},
+        {"name": "init2", "image": BUSYBOX, "command": ["sh", "-c", "echo init2 >> $KUBERNETES_VOLUME_WORK/order"],
+         "volumeMounts": [{"name": "work", "mountPath": "/work"}]}]
+    p["spec"]["containers"][0]["volumeMounts"] = [{"name": "work", "mountPath": "/work"}]
+    await f.client.create("pods", p, f.ns)
+    got = await f.pod_phase("init", ("Succeeded",))
+    out = await f.logs("init")
+    assert out.split() == ["init1", "init2", "main"], out
+    assert all(s["state"].get("terminated", {}).get("exitCode") == 0 for s in got["status"]["initContainerStatuses"])
+
+
+@conformance("Probing container with a failing liveness probe should be restarted")
+async def liveness_restart(f):
+    p = _pod("live", "sleep 3600", restart="Always")
+    p["spec"]["containers"][0]["livenessProbe"] = {"exec": {"command": ["sh", "-c", "exit 1"]},
+                                                   "periodSeconds": 1, "failureThreshold": 1}
+    await f.client.create("pods", p, f.ns)
+
+    async def restarted():
+        x = await f.client.get("pods", "live", f.ns)
+        cs = (x.get("status") or {}).get("containerStatuses") or [{}]
+        return x if cs[0].get("restartCount", 0) >= 1 else None
+    await f.wait(restarted, 60, "liveness restart")
+
+
+@conformance("Probing container with a readiness probe should not be ready until it succeeds and never restart")
+async def readiness(f):
+    p = _pod("ready", "sleep 3600", restart="Always")
+    p["spec"]["containers"][0]["readinessProbe"] = {"exec": {"command": ["sh", "-c", "test -e /proc/self"]},
+                                                    "initialDelaySeconds": 1, "periodSeconds": 1}
+    await f.client.create("pods", p, f.ns)
+
+    async def ready():
+        x = await f.client.get("pods", "ready", f.ns)
+        c = core.get_condition(x.get("status"), "Ready")
+        return x if c and c.get("status") == "True" else None
+    x = await f.wait(ready, 60, "pod ready")
+    assert x["status"]["containerStatuses"][0].get("restartCount", 0) == 0
+
+
+@conformance("Job should run a job to completion with the requested completions")
+async def job_completion(f):
+    j = {"metadata": {"name": "pi"}, "spec": {"completions": 3, "parallelism": 2, "template": {
+        "metadata": {"labels": {"job": "pi"}},
+        "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "echo 3.14"]}]}}}}
+    await f.client.create("jobs", j, f.ns)
+
+    async def done():
+        x = await f.client.get("jobs", "pi", f.ns)
+        return x if (x.get("status") or {}).get("succeeded") == 3 else None
+    x = await f.wait(done, 90, "job completion")
+    assert any(c.get("type") == "Complete" and c.get("status") == "True" for c in x["status"].get("conditions") or ())
+
+
+@conformance("ReplicaSet should adopt a matching orphan pod and keep the replica count")
+async def replicaset_adoption(f):
+    await f.client.create("pods", _pod("orphan", "sleep 3600", restart="Always"), f.ns)
+    await f.pod_phase("orphan", ("Running",))
+    rs = {"metadata": {"name": "orphan"}, "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "orphan"}},
+          "template": {"metadata": {"labels": {"app": "orphan"}}, "spec": {"containers": [
+              {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("replicasets", rs, f.ns)
+
+    async def adopted():
+        pods = (await f.client.list("pods", f.ns, label_selector="app=orphan"))["items"]
+        owned = [p for p in pods if any(o.get("kind") == "ReplicaSet" for o in p["metadata"].get("ownerReferences") or ())]
+        return pods if len(pods) == 2 and len(owned) == 2 else None
+    pods = await f.wait(adopted, 60, "orphan adopted")
+    assert "orphan" in [p["metadata"]["name"] for p in pods]
+
+
+@conformance("StatefulSet should create pods in order with stable names")
+async def statefulset_order(f):
+    await f.client.create("services", {"metadata": {"name": "db"}, "spec": {"clusterIP": "None", "selector": {"app": "db"},
+                                                                            "ports": [{"port": 80}]}}, f.ns)
+    ss = {"metadata": {"name": "db"}, "spec": {"serviceName": "db", "replicas": 3, "selector": {"matchLabels": {"app": "db"}},
+          "template": {"metadata": {"labels": {"app": "db"}}, "spec": {"containers": [
+              {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("statefulsets", ss, f.ns)
+
+    async def all_running():
+        pods = (await f.client.list("pods", f.ns, label_selector="app=db"))["items"]
+        run = [p for p in pods if (p.get("status") or {}).get("phase") == "Running"]
+        return pods if len(run) == 3 else None
+    pods = await f.wait(all_running, 90, "statefulset pods")
+    assert sorted(p["metadata"]["name"] for p in pods) == ["db-0", "db-1", "db-2"]
+    created = sorted(pods, key=lambda p: p["metadata"]["creationTimestamp"])
+    assert created[0]["metadata"]["name"] == "db-0"
+
+
+@conformance("DaemonSet should run one daemon pod on every schedulable node")
+async def daemonset_per_node(f):
+    nodes = [n["metadata"]["name"] for n in (await f.client.list("nodes"))["items"]
+             if not (n.get("spec") or {}).get("unschedulable")]
+    ds = {"metadata": {"name": "agent"}, "spec": {"selector": {"matchLabels": {"app": "agent"}}, "template": {
+        "metadata": {"labels": {"app": "agent"}}, "spec": {"containers": [
+            {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("daemonsets", ds, f.ns)
+
+    async def everywhere():
+        pods = (await f.client.list("pods", f.ns, label_selector="app=agent"))["items"]
+        placed = sorted((p.get("spec") or {}).get("nodeName") or "" for p in pods)
+        return placed if placed == sorted(nodes) else None
+    await f.wait(everywhere, 60, "daemon pods on every node")
+
+
+@conformance("ConfigMap should be consumable via environment variables (envFrom)")
+async def configmap_envfrom(f):
+    await f.client.create("configmaps", {"metadata": {"name": "envcm"}, "data": {"GPU_ARCH": "gfx950"}}, f.ns)
+    p = _pod("envfrom", "echo ARCH=$CFG_GPU_ARCH")
+    p["spec"]["containers"][0]["envFrom"] = [{"prefix": "CFG_", "configMapRef": {"name": "envcm"}}]
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("envfrom", ("Succeeded",))
+    assert "ARCH=gfx950" in await f.logs("envfrom")
+
+
+@conformance("Downward API volume should provide the pod's labels as a file")
+async def downward_volume(f):
+    p = _pod("dvol", "cat $KUBERNETES_VOLUME_PODINFO/labels")
+    p["metadata"]["labels"]["gpu"] = "mi355x"
+    p["spec"]["volumes"] = [{"name": "podinfo", "downwardAPI": {"items": [
+        {"path": "labels", "fieldRef": {"fieldPath": "metadata.labels"}}]}}]
+    p["spec"]["containers"][0]["volumeMounts"] = [{"name": "podinfo", "mountPath": "/etc/podinfo"}]
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("dvol", ("Succeeded",))
+    assert 'gpu="mi355x"' in await f.logs("dvol")
+
+
+@conformance("Events should be sent by the scheduler and the kubelet about a pod")
+async def pod_events(f):
+    await f.client.create("pods", _pod("evpod", "sleep 3600", restart="Always"), f.ns)
+    await f.pod_phase("evpod", ("Running",))
+
+    async def reported():
+        evs = [e for e in (await f.client.list("events", f.ns))["items"] if e["involvedObject"]["name"] == "evpod"]
+        sources = {(e["source"].get("component"), e["reason"]) for e in evs}
+        return sources if {("default-scheduler", "Scheduled"), ("kubelet", "Started")} <= sources else None
+    await f.wait(reported, 30, "scheduler + kubelet events")
+
+
+@conformance("ResourceQuota should capture the usage of a pod and reject pods over the quota")
+async def resource_quota(f):
+    await f.client.create("resourcequotas", {"metadata": {"name": "q"}, "spec": {"hard": {"pods": "1"}}}, f.ns)
+
+    async def tracked():
+        q = await f.client.get("resourcequotas", "q", f.ns)
+        return q if ((q.get("status") or {}).get("hard") or {}).get("pods") == "1" else None
+    await f.wait(tracked, 30, "quota status")
+    await f.client.create("pods", _pod("q1", "sleep 3600", restart="Always"), f.ns)
+
+    async def used():
+        q = await f.client.get("resourcequotas", "q", f.ns)
+        return q if ((q.get("status") or {}).get("used") or {}).get("pods") == "1" else None
+    await f.wait(used, 30, "quota usage")
+    try:
+        await f.client.create("pods", _pod("q2", "sleep 3600"), f.ns)
+    except Exception as e:  # noqa: BLE001
+        assert "exceeded quota" in str(e), e
+    else:
+        raise AssertionError("a pod over the quota was admitted")
+
+
+@conformance("Garbage collector should delete the pods of a deleted ReplicaSet")
+async def gc_cascade(f):
+    rs = {"metadata": {"name": "gcrs"}, "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "gcrs"}},
+          "template": {"metadata": {"labels": {"app": "gcrs"}}, "spec": {"containers": [
+              {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("replicasets", rs, f.ns)
+
+    async def two():
+        pods = (await f.client.list("pods", f.ns, label_selector="app=gcrs"))["items"]
+        return pods if len(pods) == 2 else None
+    await f.wait(two, 60, "replicas")
+    await f.client.delete("replicasets", "gcrs", f.ns)
+
+    async def collected():
+        pods = (await f.client.list("pods", f.ns, label_selector="app=gcrs"))["items"]
+        return True if not pods else None
+    await f.wait(collected, 60, "dependents collected")
