@@ -150,7 +150,8 @@ class APIServer:
         self.rstore = None            # RemoteStore once started (shared mode)
         self.fanout = None            # FanoutClient: watches served by kamd-etcd (shared mode)
         self.fanout_enabled = os.environ.get("KAMD_WATCH_FANOUT", "1") != "0"
-        self.store = None if self.remote_address else (store or MVCCStore())
+        # `store or ...` would be wrong: an empty store has len() == 0 and is falsy
+        self.store = None if self.remote_address else (store if store is not None else MVCCStore())
         self._applied_rev = 0
         self._rev_waiters: list = []  # heap of (rev, seq, future)
         self._waiter_seq = 0
