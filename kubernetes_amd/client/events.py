@@ -2,7 +2,11 @@
 broadcaster → sink, aggregation of repeated events by incrementing `count`).
 
 Events are queued and written by a small async worker pool so the caller's hot loop
-(scheduleOne, pod sync) never waits on the API server.
+(scheduleOne, pod sync) never waits on the API server. Like the reference, delivery is best
+effort and bounded: an optional QPS/burst limit on event writes (the kubelet's
+`--event-qps=5 --event-burst=10`, `pkg/kubelet/apis/kubeletconfig` EventRecordQPS/EventBurst,
+applied to its event client) and a bounded queue (`record.maxQueuedEvents` = 1000) past which
+new events are dropped rather than slowing the component down.
 """
 from __future__ import annotations
 
@@ -16,8 +20,8 @@ log = logging.getLogger("events")
 
 
 class EventRecorder:
-    def __init__(self, client, component: str, host: str = "", workers: int = 4, max_queue: int = 10000,
-                 enabled: bool = True):
+    def __init__(self, client, component: str, host: str = "", workers: int = 4, max_queue: int = 1000,
+                 enabled: bool = True, qps: float = 0.0, burst: int = 0):
         self.client = client
         self.source = {"component": component}
         if host:
@@ -29,6 +33,9 @@ class EventRecorder:
         self.sent = 0
         self.dropped = 0
         self._agg: dict[tuple, dict] = {}   # (involved uid, reason, message) -> last event
+        self.qps, self.burst = qps, max(1, burst or int(qps) or 1)
+        self._tokens = float(self.burst)
+        self._last = time.monotonic()
         self.emitted: list = []             # for tests: (type, reason, message)
 
     def start(self):
@@ -76,9 +83,22 @@ class EventRecorder:
         except asyncio.QueueFull:
             self.dropped += 1
 
+    async def _take(self):
+        """Token bucket in front of the API writes (client rate limiter on the event client)."""
+        while True:
+            now = time.monotonic()
+            self._tokens = min(self.burst, self._tokens + (now - self._last) * self.qps)
+            self._last = now
+            if self._tokens >= 1.0:
+                self._tokens -= 1.0
+                return
+            await asyncio.sleep((1.0 - self._tokens) / self.qps)
+
     async def _work(self):
         while True:
             ev = await self.q.get()
+            if self.qps > 0:
+                await self._take()
             upd = ev.pop("_update", False)
             try:
                 if upd:

@@ -76,6 +76,8 @@ def main(argv=None):
                     help="comma-separated unsafe sysctls or prefix* patterns pods may request")
     ap.add_argument("--container-log-dir", default="/var/log/containers",
                     help="where <pod>_<namespace>_<container>-<id>.log symlinks for logging agents go ('' = off)")
+    ap.add_argument("--event-qps", type=float, default=5.0, help="limit event creations per second (0 = unlimited)")
+    ap.add_argument("--event-burst", type=int, default=10, help="burst of event creations (with --event-qps > 0)")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -131,7 +133,8 @@ def main(argv=None):
                     manifest_url=a.manifest_url,
                     manifest_url_headers=dict(h.split(":", 1) for h in a.manifest_url_header if ":" in h),
                     kube_reserved=dict(kv.split("=", 1) for kv in a.kube_reserved.split(",") if "=" in kv),
-                    system_reserved=dict(kv.split("=", 1) for kv in a.system_reserved.split(",") if "=" in kv))
+                    system_reserved=dict(kv.split("=", 1) for kv in a.system_reserved.split(",") if "=" in kv),
+                    event_qps=a.event_qps, event_burst=a.event_burst)
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,

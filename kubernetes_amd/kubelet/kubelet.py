@@ -99,7 +99,8 @@ class Kubelet:
                  hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
                  bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
                  manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None,
-                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, container_log_dir=None):
+                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, container_log_dir=None,
+                 event_qps=5.0, event_burst=10):
         self.client = client
         # /var/log/containers/<pod>_<ns>_<container>-<id>.log symlinks to the runtime's log
         # files (kuberuntime legacyLogSymlink): what node logging agents tail
@@ -164,7 +165,10 @@ class Kubelet:
         self._status_sem = asyncio.Semaphore(max_status_inflight)
         self._status_inflight: dict[str, asyncio.Task] = {}
         self._status_next: dict[str, tuple] = {}
-        self.recorder = EventRecorder(client, "kubelet", node_name, workers=2, enabled=emit_events)
+        # event writes are rate limited like the reference kubelet's event client
+        # (--event-qps 5 / --event-burst 10; 0 = unlimited)
+        self.recorder = EventRecorder(client, "kubelet", node_name, workers=2, enabled=emit_events,
+                                      qps=event_qps, burst=event_burst)
         self.metrics = metrics or Registry()
         m = self.metrics
         self.m_start = m.histogram("kubelet_pod_start_latency_microseconds",

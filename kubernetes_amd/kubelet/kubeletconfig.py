@@ -39,6 +39,8 @@ DEFAULTS = {
     "minimumContainerTTLDuration": "0s",
     "maxPerPodContainerCount": 1,
     "maxContainerCount": -1,
+    "eventRecordQPS": 5,
+    "eventBurst": 10,
 }
 
 
@@ -115,7 +117,8 @@ def to_kwargs(cfg):
           "cpu_manager_policy": cfg["cpuManagerPolicy"], "eviction_hard": eviction_string(cfg["evictionHard"]) or None,
           "container_gc": {"min_age": parse_duration(cfg["minimumContainerTTLDuration"]),
                            "max_per_pod_container": int(cfg["maxPerPodContainerCount"]),
-                           "max_containers": int(cfg["maxContainerCount"])}}
+                           "max_containers": int(cfg["maxContainerCount"])},
+          "event_qps": float(cfg["eventRecordQPS"]), "event_burst": int(cfg["eventBurst"])}
     if cfg.get("clusterDNS"):
         kw["dns"] = DNSConfigurer(cfg["clusterDNS"], cfg["clusterDomain"])
     if cfg.get("podManifestPath"):
