@@ -34,7 +34,7 @@ import time
 
 from ..api import codec, core, meta as m
 from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
-from ..api.meta import fast_copy, now_rfc3339
+from ..api.meta import parse_rfc3339, fast_copy, now_rfc3339
 from ..storage import wire
 from ..storage.mvcc import MVCCStore
 from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
@@ -125,8 +125,12 @@ class APIServer:
                  tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
                  service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
                  anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None, oidc=None,
-                 component_endpoints=None):
+                 component_endpoints=None, event_ttl=3600.0):
         self.abac_policy_file = authorization_policy_file
+        # --event-ttl: events expire this long after their last write (the reference stores them
+        # with an etcd lease, `pkg/registry/core/event/storage/storage.go` ttlFunc)
+        self.event_ttl = event_ttl
+        self._reaper = None
         self.authorization_webhook_url = authorization_webhook_url
         self.authorization_modes = tuple(authorization_modes)
         self.tls = (tls_cert_file, tls_private_key_file, client_ca_file)
@@ -897,7 +901,42 @@ class APIServer:
                 ctx.load_verify_locations(ca)
         port = await self.http.start(host, port, ssl=ctx, reuse_port=reuse_port)
         await self._reconcile_master_endpoints("127.0.0.1" if host in ("0.0.0.0", "") else host, port)
+        if self.event_ttl and self._reaper is None:
+            self._reaper = asyncio.ensure_future(self._event_reaper())
         return port
+
+    def expired_events(self, now=None):
+        """Events whose last write (lastTimestamp, else creationTimestamp) is older than the TTL."""
+        now = time.time() if now is None else now
+        out = []
+        for key, e in list(self.caches["events"].by_key.items()):
+            o = e.obj
+            t = parse_rfc3339(o.get("lastTimestamp")) or parse_rfc3339((o.get("metadata") or {}).get("creationTimestamp"))
+            if t is not None and now - t > self.event_ttl:
+                out.append(o)
+        return out
+
+    async def reap_events(self, now=None):
+        n = 0
+        ri = m.BY_PLURAL["events"]
+        for o in self.expired_events(now):
+            md = o["metadata"]
+            try:
+                await self._retrying(lambda md=md: self.delete(ri, md.get("namespace"), md["name"], {}))
+                n += 1
+            except APIError as e:
+                if e.code not in (404, 409):       # another worker reaped it first
+                    log.warning("event TTL delete of %s failed: %s", md["name"], e)
+        return n
+
+    async def _event_reaper(self):
+        period = max(1.0, min(60.0, self.event_ttl / 4))
+        while True:
+            await asyncio.sleep(period)
+            try:
+                await self.reap_events()
+            except Exception as e:  # noqa: BLE001 - keep reaping
+                log.warning("event TTL reaper pass failed: %s", e)
 
     async def _reconcile_master_endpoints(self, ip, port):
         """Endpoints of the `kubernetes` service = this API server (master EndpointReconciler)."""
@@ -916,6 +955,9 @@ class APIServer:
                 log.warning("master endpoints reconcile failed: %s", e)
 
     async def stop(self):
+        if self._reaper is not None:
+            self._reaper.cancel()
+            self._reaper = None
         await self.http.stop()
         if self.rstore is not None:
             self.store_healthy = False   # a deliberate close, not a store failure

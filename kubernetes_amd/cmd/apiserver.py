@@ -45,6 +45,7 @@ def _parser():
     ap.add_argument("--max-requests-inflight", type=int, default=4000)
     ap.add_argument("--max-mutating-requests-inflight", type=int, default=2000)
     ap.add_argument("--watch-cache-size", type=int, default=200000)
+    ap.add_argument("--event-ttl", default="1h", help="amount of time to retain events (e.g. 1h, 30m, 90s)")
     ap.add_argument("--audit-log-path", default=None, help="write audit events (JSON lines) here; '-' = stdout")
     ap.add_argument("--audit-policy-file", default=None, help="audit policy YAML (rules: level/users/verbs/resources)")
     ap.add_argument("--experimental-encryption-provider-config", dest="encryption_config", default=None,
@@ -184,6 +185,11 @@ def supervise(a):
     return rc
 
 
+def _duration(v):
+    from ..kubelet.kubeletconfig import parse_duration
+    return parse_duration(v)
+
+
 def main(argv=None):
     a = _parser().parse_args(argv)
     setup_logging(a.v)
@@ -219,6 +225,7 @@ def main(argv=None):
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
                       max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size,
+                      event_ttl=_duration(a.event_ttl),
                       audit=audit, encryption_config=a.encryption_config,
                       service_cluster_ip_range=a.service_cluster_ip_range,
                       service_node_port_range=tuple(int(x) for x in a.service_node_port_range.split("-")),

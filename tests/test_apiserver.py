@@ -204,3 +204,33 @@ def test_gpu_quota_enforced(run):
             await c.close()
             await s.stop()
     run(main())
+
+
+def test_event_ttl_reaper(run):
+    """--event-ttl: events are deleted once their last write is older than the TTL (the
+    reference attaches an etcd lease to every event write)."""
+    import time as _t
+
+    from kubernetes_amd.apiserver.server import APIServer as _S
+    from kubernetes_amd.client.rest import Client as _C
+
+    async def main():
+        s = _S(event_ttl=3600)
+        c = _C(f"http://127.0.0.1:{await s.start()}")
+        try:
+            old = _t.strftime("%Y-%m-%dT%H:%M:%SZ", _t.gmtime(_t.time() - 7200))
+            for name, ts in (("stale", old), ("fresh", None)):
+                ev = {"metadata": {"name": name, "namespace": "default"}, "reason": "Started", "message": "m",
+                      "involvedObject": {"kind": "Pod", "name": "p", "namespace": "default"}, "type": "Normal",
+                      "count": 1}
+                if ts:
+                    ev["firstTimestamp"] = ev["lastTimestamp"] = ts
+                await c.create("events", ev, "default")
+            assert [o["metadata"]["name"] for o in s.expired_events()] == ["stale"]
+            assert await s.reap_events() == 1
+            names = [e["metadata"]["name"] for e in (await c.list("events", "default"))["items"]]
+            assert names == ["fresh"]
+        finally:
+            await c.close()
+            await s.stop()
+    run(main())
