@@ -76,6 +76,12 @@ def main(argv=None):
                     help="comma-separated unsafe sysctls or prefix* patterns pods may request")
     ap.add_argument("--container-log-dir", default="/var/log/containers",
                     help="where <pod>_<namespace>_<container>-<id>.log symlinks for logging agents go ('' = off)")
+    ap.add_argument("--anonymous-auth", type=lambda v: v.lower() != "false", default=True,
+                    help="allow anonymous requests to the kubelet API (system:anonymous)")
+    ap.add_argument("--authentication-token-webhook", action="store_true",
+                    help="authenticate bearer tokens with TokenReviews against the API server")
+    ap.add_argument("--authorization-mode", default="AlwaysAllow", choices=["AlwaysAllow", "Webhook"],
+                    help="Webhook: SubjectAccessReview per request (resource nodes, subresource by path)")
     ap.add_argument("--event-qps", type=float, default=5.0, help="limit event creations per second (0 = unlimited)")
     ap.add_argument("--event-burst", type=int, default=10, help="burst of event creations (with --event-qps > 0)")
     ap.add_argument("-v", type=int, default=0)
@@ -135,6 +141,10 @@ def main(argv=None):
                     kube_reserved=dict(kv.split("=", 1) for kv in a.kube_reserved.split(",") if "=" in kv),
                     system_reserved=dict(kv.split("=", 1) for kv in a.system_reserved.split(",") if "=" in kv),
                     event_qps=a.event_qps, event_burst=a.event_burst)
+        if not a.anonymous_auth or a.authentication_token_webhook or a.authorization_mode != "AlwaysAllow":
+            from ..kubelet.server_auth import KubeletAuth
+            base["auth"] = KubeletAuth(client, a.hostname_override, a.anonymous_auth,
+                                       a.authentication_token_webhook, a.authorization_mode)
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
                      http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,

@@ -100,8 +100,11 @@ class Kubelet:
                  bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
                  manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None,
                  cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, container_log_dir=None,
-                 event_qps=5.0, event_burst=10):
+                 event_qps=5.0, event_burst=10, auth=None, node_log_dir="/var/log"):
         self.client = client
+        self.auth = auth                      # server_auth.KubeletAuth for the :10250 API (None: open)
+        self.node_log_dir = node_log_dir      # served read-only under /logs/
+        self._last_status_loop = time.monotonic()
         # /var/log/containers/<pod>_<ns>_<container>-<id>.log symlinks to the runtime's log
         # files (kuberuntime legacyLogSymlink): what node logging agents tail
         self.container_log_dir = container_log_dir
@@ -495,6 +498,7 @@ class Kubelet:
         # can swallow a CancelledError that races with the inner future completing
         last = 0.0
         while not self._stopped:
+            self._last_status_loop = time.monotonic()
             timeout = max(0.0, self.status_freq - (time.monotonic() - last))
             try:
                 await asyncio.wait_for(self._status_dirty.wait(), timeout)
@@ -800,6 +804,53 @@ class Kubelet:
                 os.unlink(link)
             except OSError:
                 pass
+
+    def current_config(self):
+        """KubeletConfiguration (kubeletconfig/v1alpha1) of the running kubelet (/configz)."""
+        return {"kind": "KubeletConfiguration", "apiVersion": "kubeletconfig/v1alpha1",
+                "maxPods": int(self.capacity["pods"]), "nodeStatusUpdateFrequency": f"{self.status_freq:g}s",
+                "eventRecordQPS": self.recorder.qps, "eventBurst": self.recorder.burst,
+                "cpuManagerPolicy": "static" if self.cpu_manager is not None else "none",
+                "cgroupsPerQOS": self.cgroups is not None, "cgroupRoot": self.cgroup_root or "",
+                "kubeReserved": self.reserved[0], "systemReserved": self.reserved[1],
+                "podManifestPath": self.pod_manifest_path or "", "featureGates": {"DevicePlugins": True}}
+
+    def running_pods(self):
+        """/runningpods/: pods as the container runtime sees them (`kubelet.GetRunningPods`)."""
+        items = []
+        for st in self.pods.values():
+            running = []
+            for name, cid in st.containers.items():
+                cs = self.runtime.container_status(cid) if cid else None
+                if cs is not None and cs.state == RUNNING:
+                    running.append((name, cid))
+            if not running:
+                continue
+            md = st.pod["metadata"]
+            images = {c["name"]: c.get("image", "") for c in (st.pod.get("spec") or {}).get("containers") or ()}
+            items.append({"metadata": {"name": md["name"], "namespace": md.get("namespace", ""), "uid": md["uid"]},
+                          "spec": {"containers": [{"name": n, "image": images.get(n, "")} for n, _ in running]},
+                          "status": {"containerStatuses": [{"name": n, "containerID": c} for n, c in running]}})
+        return {"kind": "PodList", "apiVersion": "v1", "metadata": {}, "items": items}
+
+    def _node_logs(self, rel):
+        """/logs/: read-only view of the node's log directory (`server.go` getLogs)."""
+        base = os.path.realpath(self.node_log_dir)
+        target = os.path.realpath(os.path.join(base, rel))
+        if target != base and not target.startswith(base + os.sep):
+            return Response(403, b"path escapes the log directory", "text/plain")
+        if os.path.isdir(target):
+            try:
+                names = sorted(os.listdir(target))
+            except OSError as e:
+                return Response(403, str(e).encode(), "text/plain")
+            return Response(200, "".join(n + ("/" if os.path.isdir(os.path.join(target, n)) else "") + "\n"
+                                         for n in names).encode(), "text/plain")
+        try:
+            with open(target, "rb") as f:
+                return Response(200, f.read(), "text/plain")
+        except OSError:
+            return Response(404, b"not found", "text/plain")
 
     def _service_env(self, pod):
         if self.svc_informer is None or not self.svc_informer.synced.is_set():
@@ -1220,8 +1271,26 @@ class Kubelet:
     # HTTP (kubelet server :10250 subset)
     async def _http(self, req):
         p = req.path
-        if p == "/healthz":
+        if self.auth is not None:
+            denied = await self.auth.check(req)
+            if denied is not None:
+                return Response(denied[0], denied[1].encode(), "text/plain")
+        if p in ("/healthz", "/healthz/ping"):
             return Response(200, b"ok", "text/plain")
+        if p == "/healthz/syncloop":
+            age = time.monotonic() - self._last_status_loop
+            limit = max(60.0, 3 * self.status_freq)
+            return (Response(200, b"ok", "text/plain") if age < limit else
+                    Response(500, f"sync loop has not run for {age:.0f}s".encode(), "text/plain"))
+        if p == "/spec" or p == "/spec/":
+            from .stats import machine_info
+            return Response(200, codec_dumpb(machine_info(self)))
+        if p == "/configz":
+            return Response(200, codec_dumpb({"kubeletconfig": self.current_config()}))
+        if p.rstrip("/") == "/runningpods":
+            return Response(200, codec_dumpb(self.running_pods()))
+        if p == "/logs" or p.startswith("/logs/"):
+            return self._node_logs(p[len("/logs"):].lstrip("/"))
         if p == "/metrics":
             return Response(200, self.metrics.render(), "text/plain; version=0.0.4")
         from ..api import codec
@@ -1260,6 +1329,11 @@ class Kubelet:
         if r is not None:
             return r
         return Response(404, b"not found", "text/plain")
+
+
+def codec_dumpb(obj):
+    from ..api import codec
+    return codec.dumpb(obj)
 
 
 def md_deleting(pod):

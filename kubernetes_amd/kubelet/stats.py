@@ -124,3 +124,48 @@ def summary(kubelet):
                      "cpu": {"time": now, "usageNanoCores": node_cpu}, "memory": {"time": now, "workingSetBytes": node_mem},
                      "systemContainers": [{"name": "kubelet", "startTime": now}]},
             "pods": pods, "time": time.time()}
+
+
+def _read(path, default=""):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return default
+
+
+def machine_info(kubelet):
+    """/spec: cAdvisor `MachineInfo` (num_cores, memory_capacity, machine_id, system_uuid,
+    boot_id, topology by NUMA node) for this node, plus the AMD accelerators the device plugin
+    advertises (the role cAdvisor's accelerator collector plays). Capacity values are the
+    kubelet's own (hollow nodes report their configured capacity)."""
+    import os
+
+    from ..api.quantity import parse_quantity
+    cap = kubelet.capacity
+    topo = []
+    node_dir = "/sys/devices/system/node"
+    try:
+        nodes = sorted(int(d[4:]) for d in os.listdir(node_dir) if d.startswith("node") and d[4:].isdigit())
+    except OSError:
+        nodes = []
+    for n in nodes:
+        cpus = _read(f"{node_dir}/node{n}/cpulist")
+        mem = 0
+        for ln in _read(f"{node_dir}/node{n}/meminfo").splitlines():
+            if "MemTotal" in ln:
+                mem = int(ln.split()[-2]) * 1024
+        topo.append({"node_id": n, "memory": mem, "cpulist": cpus})
+    accels = []
+    for dev_id, dev in sorted(_gpu_index(kubelet.dm).items()):
+        attrs = dev.get("attributes") or {}
+        accels.append({"make": "amd", "model": attrs.get("amd.com/product", ""), "id": dev_id,
+                       "arch": attrs.get("amd.com/arch", ""), "numa_node": attrs.get("amd.com/numa", ""),
+                       "xgmi_hive": attrs.get("amd.com/xgmi-hive", ""),
+                       "memory_total_mib": int(attrs.get("amd.com/memory", "0") or 0), "health": dev.get("health", "")})
+    return {"num_cores": int(parse_quantity(str(cap["cpu"])).value),
+            "memory_capacity": int(parse_quantity(str(cap["memory"])).value),
+            "machine_id": _read("/etc/machine-id") or kubelet.node_name,
+            "system_uuid": _read("/sys/class/dmi/id/product_uuid") or kubelet.node_name,
+            "boot_id": _read("/proc/sys/kernel/random/boot_id"),
+            "topology": topo, "accelerators": accels, "cloud_provider": "None", "instance_type": "Unknown"}
