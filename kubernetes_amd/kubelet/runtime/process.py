@@ -17,6 +17,7 @@ import asyncio
 import itertools
 import json
 import os
+import shutil
 import signal
 import time
 
@@ -45,11 +46,37 @@ def resolve_command(container):
     return cmd + args
 
 
+CONTAINER_INIT = os.path.join(BIN_DIR, "container-init")
+
+
+def _init_argv(argv, env, cpus, oom_adj, cgroup):
+    """Prefix argv with the native container-init helper (native/pause/container_init.cc), which
+    applies the cpuset, OOM score and cgroup and then execs the entrypoint — so the spawn needs
+    no Python pre-exec hook and can use vfork (a hook forces a full fork of the kubelet: ~3 ms
+    of kubelet CPU per container instead of ~0.5 ms). The entrypoint is resolved here so a
+    missing binary is still a StartError rather than exit 127 of the helper."""
+    exe = argv[0]
+    if os.sep not in exe:
+        found = shutil.which(exe, path=env.get("PATH", os.defpath))
+        if found is None:
+            raise FileNotFoundError(2, "No such file or directory", exe)
+    elif not os.access(exe, os.X_OK):
+        raise FileNotFoundError(2, "No such file or directory", exe)
+    pre = [CONTAINER_INIT]
+    if cpus:
+        pre += ["-c", ",".join(str(c) for c in sorted(cpus))]
+    if oom_adj is not None:
+        pre += ["-o", str(int(oom_adj))]
+    if cgroup:
+        pre += ["-g", cgroup]
+    return pre + ["--"] + list(argv)
+
+
 def _child_setup(cpus, oom_adj, cgroup):
-    """Runs in the forked child before exec: what a container runtime applies to the container's
-    init process — cpuset pinning, the kubelet's OOM score adjustment, pod cgroup membership.
-    Failures are ignored (an unprivileged kubelet can raise but not lower oom_score_adj, and
-    may not own a cgroup subtree)."""
+    """Fallback when container-init is not built: runs in the forked child before exec — cpuset
+    pinning, the kubelet's OOM score adjustment, pod cgroup membership. Failures are ignored
+    (an unprivileged kubelet can raise but not lower oom_score_adj, and may not own a cgroup
+    subtree)."""
     def pre():
         if cpus:
             os.sched_setaffinity(0, cpus)
@@ -140,7 +167,7 @@ class ProcessRuntime(Runtime):
         spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts,
                               sandbox_pid=getattr(sb.get("proc"), "pid", None))
         with open(os.path.join(d, "config.json"), "w") as f:
-            json.dump(spec, f, indent=1)
+            json.dump(spec, f, separators=(",", ":"))
         st = ContainerStatus(cid, container["name"], CREATED, image=container.get("image", ""),
                              log_path=os.path.join(d, "log"))
         self.containers[cid] = st
@@ -163,10 +190,14 @@ class ProcessRuntime(Runtime):
             from ..cpumanager import parse_cpulist
             cpus = set(parse_cpulist(m["env"]["KAMD_CPUSET"])) & set(os.sched_getaffinity(0)) or None
         pre = None
-        if cpus or m.get("oom_score_adj") is not None or m.get("cgroup"):
-            pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
+        argv = m["argv"]
         try:
-            proc = await asyncio.create_subprocess_exec(*m["argv"], env=m["env"], cwd=m["cwd"], stdout=log,
+            if cpus or m.get("oom_score_adj") is not None or m.get("cgroup"):
+                if os.access(CONTAINER_INIT, os.X_OK):
+                    argv = _init_argv(argv, m["env"], cpus, m.get("oom_score_adj"), m.get("cgroup"))
+                else:
+                    pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
+            proc = await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=m["cwd"], stdout=log,
                                                         stderr=asyncio.subprocess.STDOUT, start_new_session=True,
                                                         preexec_fn=pre)
         except OSError as e:
@@ -177,8 +208,6 @@ class ProcessRuntime(Runtime):
             st.message = str(e)
             st.finished_at = time.time()
             raise
-        finally:
-            pass
         log.close()
         m["proc"] = proc
         st.state = RUNNING

@@ -1,0 +1,223 @@
+"""Single-node density and kubelet resource usage (the reference's `test/e2e_node/density_test.go`
+and `resource_usage_test.go`, BASELINE.md "node perf" rows).
+
+One real kubelet runs in its own process (process runtime: every container is a real child
+process) against an API server + scheduler in other processes, and a sampler reads the kubelet
+process's CPU and RSS (the reference samples kubelet and runtime with a standalone cAdvisor).
+Two workloads, as in the reference:
+  * batch: N pods created at once; per-pod create → Running latency percentiles and the time
+    until the whole batch runs (thresholds p50/p90/p99 ≤ 16/18/20 s, batch ≤ 25 s for N=10,
+    `density_test.go:71-91`);
+  * sequential: with B background pods running, N pods created one after the other, each
+    waited for (thresholds 5/9/10 s, `density_test.go:213-228`);
+  * the kubelet's CPU (cores) p50/p95 and RSS over the density run (thresholds 0.30/0.50 cores
+    and 100 MiB, `density_test.go:76-83`), sampled every second like the reference's standalone
+    cAdvisor (`resource_collector.go:56`, housekeeping 1 s);
+  * steady-state resource tracking with every pod running (`resource_usage_test.go:65-78,
+    136-182`: settle, then monitor; kubelet limits for 10 pods p50 ≤ 0.30 / p95 ≤ 0.35 cores,
+    RSS ≤ 200 MiB), plus kubelet CPU-seconds spent per started pod.
+
+    python -m kubernetes_amd.kubemark.node_density --batch 10 --sequential 10 --background 50
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+from ..client.rest import Client
+from .density import pct
+
+THRESHOLDS = {"batch": {"p50": 16.0, "p90": 18.0, "p99": 20.0, "all": 25.0},
+              "sequential": {"p50": 5.0, "p90": 9.0, "p99": 10.0},
+              "kubelet_cpu": {"p50": 0.30, "p95": 0.50}, "kubelet_rss_mib": 100.0,
+              "steady_kubelet_cpu": {"p50": 0.30, "p95": 0.35}, "steady_kubelet_rss_mib": 200.0}
+
+
+def _spawn(args, tmp, name):
+    env = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    return subprocess.Popen([sys.executable, "-m"] + args, env=env, stdout=subprocess.DEVNULL,
+                            stderr=open(os.path.join(tmp, f"{name}.log"), "w"))
+
+
+class Sampler:
+    """CPU (cores) and RSS of one process, sampled every `period` seconds."""
+
+    def __init__(self, pid, period=1.0):
+        import psutil
+        self.p = psutil.Process(pid)
+        self.period = period
+        self.cpu, self.rss = [], []
+        self._task = None
+
+    def cpu_seconds(self):
+        return sum(self.p.cpu_times()[:2])
+
+    def reset(self):
+        self.cpu, self.rss = [], []
+
+    async def _run(self):
+        last_t, last_cpu = time.monotonic(), self.cpu_seconds()
+        while True:
+            await asyncio.sleep(self.period)
+            t, cpu = time.monotonic(), self.cpu_seconds()
+            self.cpu.append((cpu - last_cpu) / max(t - last_t, 1e-6))
+            self.rss.append(self.p.memory_info().rss)
+            last_t, last_cpu = t, cpu
+
+    def start(self):
+        self._task = asyncio.ensure_future(self._run())
+        return self
+
+    def stop(self):
+        if self._task:
+            self._task.cancel()
+
+
+def _pod(name, sleep=3600):
+    return {"metadata": {"name": name, "labels": {"density": "node"}},
+            "spec": {"restartPolicy": "Never", "terminationGracePeriodSeconds": 1,
+                     "containers": [{"name": "c", "image": "busybox", "command": ["sleep", str(sleep)]}]}}
+
+
+async def _wait_running(client, ns, names, timeout):
+    """name -> time observed Running (watch), within timeout."""
+    seen = {}
+    lst = await client.list("pods", ns)
+    for p in lst["items"]:
+        if (p.get("status") or {}).get("phase") == "Running":
+            seen[p["metadata"]["name"]] = time.monotonic()
+    w = await client.watch("pods", ns, lst["metadata"]["resourceVersion"])
+    end = time.monotonic() + timeout
+
+    async def drain():
+        async for _, p in w:
+            if (p.get("status") or {}).get("phase") == "Running":
+                seen.setdefault(p["metadata"]["name"], time.monotonic())
+            if all(n in seen for n in names):
+                return
+    try:
+        await asyncio.wait_for(drain(), max(0.1, end - time.monotonic()))
+    finally:
+        w.close()
+    return seen
+
+
+async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0, monitor=10.0, period=1.0):
+    tmp = tempfile.mkdtemp(prefix="kamd-node-density-")
+    pf = os.path.join(tmp, "api.port")
+    procs = [_spawn(["kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf], tmp, "apiserver")]
+    try:
+        t = time.time()
+        while not os.path.exists(pf):
+            if time.time() - t > 60:
+                raise TimeoutError("apiserver did not start")
+            await asyncio.sleep(0.05)
+        url = f"http://127.0.0.1:{open(pf).read().strip()}"
+        procs.append(_spawn(["kubernetes_amd.cmd.scheduler", "--master", url], tmp, "scheduler"))
+        kl = _spawn(["kubernetes_amd.cmd.kubelet", "--api-servers", url, "--hostname-override", "density-node",
+                     "--root-dir", os.path.join(tmp, "kubelet"), "--container-runtime", "process", "--port", "0",
+                     "--container-log-dir", "", "--max-pods", str(background + batch + sequential + 10)],
+                    tmp, "kubelet")
+        procs.append(kl)
+        c = Client(url)
+        t = time.time()
+        while True:
+            nodes = (await c.list("nodes"))["items"]
+            if nodes and any(x.get("type") == "Ready" and x.get("status") == "True"
+                             for x in nodes[0]["status"].get("conditions") or ()):
+                break
+            if time.time() - t > 60:
+                raise TimeoutError("kubelet did not register")
+            await asyncio.sleep(0.1)
+        sampler = Sampler(kl.pid, period).start()
+        cpu0 = sampler.cpu_seconds()
+        ns = "density"
+        await c.create("namespaces", {"metadata": {"name": ns}})
+        # batch: all at once
+        names = [f"batch-{i}" for i in range(batch)]
+        created = {}
+        t0 = time.monotonic()
+        for n in names:
+            created[n] = time.monotonic()
+            await c.create("pods", _pod(n), ns)
+        seen = await _wait_running(c, ns, names, timeout)
+        batch_lat = [seen[n] - created[n] for n in names if n in seen]
+        batch_all = max(seen[n] for n in names) - t0 if len(seen) >= len(names) else float("inf")
+        # background pods, then sequential creations
+        bg = [f"bg-{i}" for i in range(background)]
+        for n in bg:
+            await c.create("pods", _pod(n), ns)
+        await _wait_running(c, ns, bg, timeout)
+        seq_lat = []
+        for i in range(sequential):
+            n = f"seq-{i}"
+            t1 = time.monotonic()
+            await c.create("pods", _pod(n), ns)
+            s2 = await _wait_running(c, ns, [n], timeout)
+            if n in s2:
+                seq_lat.append(s2[n] - t1)
+        cpu_per_pod = (sampler.cpu_seconds() - cpu0) / max(1, batch + background + sequential)
+        await asyncio.sleep(period)        # the sample covering the last start
+        cpu = sorted(sampler.cpu) or [0.0]
+        rss = max(sampler.rss or [0])
+        # steady state: every pod running, nothing changing
+        await asyncio.sleep(settle)
+        sampler.reset()
+        await asyncio.sleep(monitor)
+        sampler.stop()
+        steady = sorted(sampler.cpu) or [0.0]
+        await c.close()
+        out = {
+            "batch": {"pods": batch, "p50_s": round(pct(batch_lat, .5), 3), "p90_s": round(pct(batch_lat, .9), 3),
+                      "p99_s": round(pct(batch_lat, .99), 3), "all_running_s": round(batch_all, 3)},
+            "sequential": {"pods": sequential, "background": background, "p50_s": round(pct(seq_lat, .5), 3),
+                           "p90_s": round(pct(seq_lat, .9), 3), "p99_s": round(pct(seq_lat, .99), 3)},
+            "kubelet_cpu_cores": {"p50": round(pct(cpu, .5), 3), "p95": round(pct(cpu, .95), 3)},
+            "kubelet_rss_mib": round(rss / 2**20, 1),
+            "kubelet_cpu_s_per_pod": round(cpu_per_pod, 4),
+            "steady": {"pods": batch + background + sequential, "monitor_s": monitor,
+                       "kubelet_cpu_cores": {"p50": round(pct(steady, .5), 3), "p95": round(pct(steady, .95), 3)},
+                       "kubelet_rss_mib": round(max(sampler.rss or [0]) / 2**20, 1)},
+            "thresholds": THRESHOLDS,
+        }
+        out["within_thresholds"] = (
+            out["batch"]["p50_s"] <= THRESHOLDS["batch"]["p50"] and out["batch"]["p99_s"] <= THRESHOLDS["batch"]["p99"]
+            and out["batch"]["all_running_s"] <= THRESHOLDS["batch"]["all"]
+            and out["sequential"]["p99_s"] <= THRESHOLDS["sequential"]["p99"]
+            and out["kubelet_cpu_cores"]["p50"] <= THRESHOLDS["kubelet_cpu"]["p50"]
+            and out["kubelet_cpu_cores"]["p95"] <= THRESHOLDS["kubelet_cpu"]["p95"]
+            and out["kubelet_rss_mib"] <= THRESHOLDS["kubelet_rss_mib"]
+            and out["steady"]["kubelet_cpu_cores"]["p95"] <= THRESHOLDS["steady_kubelet_cpu"]["p95"]
+            and out["steady"]["kubelet_rss_mib"] <= THRESHOLDS["steady_kubelet_rss_mib"])
+        return out
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("node-density")
+    ap.add_argument("--batch", type=int, default=10)
+    ap.add_argument("--sequential", type=int, default=10)
+    ap.add_argument("--background", type=int, default=50)
+    ap.add_argument("--monitor", type=float, default=10.0, help="steady-state monitoring seconds")
+    ap.add_argument("--period", type=float, default=1.0, help="CPU/RSS sampling period (cAdvisor housekeeping)")
+    a = ap.parse_args(argv)
+    print(json.dumps(asyncio.run(run(a.batch, a.sequential, a.background, monitor=a.monitor, period=a.period))))
+
+
+if __name__ == "__main__":
+    main()

@@ -43,6 +43,8 @@ def targets():
                         cxx + ["-O2", "-shared", _s("crypto", "kamd_crypto.cc"), "-lcrypto"]),
         "pause": ([_s("pause", "pause.cc")], os.path.join(BIN_DIR, "pause"),
                   ["g++", "-Os", "-Wall", "-Werror", "-static", _s("pause", "pause.cc")]),
+        "container_init": ([_s("pause", "container_init.cc")], os.path.join(BIN_DIR, "container-init"),
+                           ["g++", "-O2", "-Wall", "-Werror", "-static", _s("pause", "container_init.cc")]),
         "orphan": ([_s("pause", "orphan.cc")], os.path.join(BIN_DIR, "orphan"),
                    ["g++", "-Os", "-Wall", _s("pause", "orphan.cc")]),
         "kamd_hip": ([_s("hip", "kamd_hip.hip")], os.path.join(LIB_DIR, "libkamd_hip.so"),

@@ -145,3 +145,31 @@ def test_unhealthy_device_reduces_capacity(run):
             assert bad not in got
             cl.smi.fake_set_ecc(2, 0)
     run(main(), timeout=60)
+
+
+def test_container_init_applies_attributes_and_starts(tmp_path):
+    """native container-init: cpuset + OOM score applied before exec; unknown binary → 127."""
+    import subprocess
+    from kubernetes_amd.kubelet.runtime.process import CONTAINER_INIT, _init_argv
+    if not os.access(CONTAINER_INIT, os.X_OK):
+        pytest.skip("container-init not built")
+    cpu = min(os.sched_getaffinity(0))
+    argv = _init_argv(["sh", "-c", "cat /proc/self/oom_score_adj; grep Cpus_allowed_list /proc/self/status"],
+                      {"PATH": os.environ["PATH"]}, {cpu}, 700, str(tmp_path / "nocgroup"))
+    out = subprocess.run(argv, capture_output=True, text=True, check=True).stdout.split()
+    assert out[0] == "700" and out[-1] == str(cpu)
+    with pytest.raises(FileNotFoundError):
+        _init_argv(["no-such-binary-xyz"], {"PATH": "/nonexistent"}, None, 1, None)
+    assert subprocess.run([CONTAINER_INIT, "--", "/nonexistent/x"], capture_output=True).returncode == 127
+
+
+def test_node_density_benchmark_small():
+    """e2e_node density/resource-usage equivalent (kubemark/node_density.py) on a tiny config:
+    real kubelet process + process runtime, latencies and kubelet CPU/RSS reported."""
+    from kubernetes_amd.kubemark import node_density
+    out = asyncio.run(node_density.run(batch=3, sequential=2, background=3, monitor=1.0, settle=0.5, period=0.5))
+    assert out["batch"]["pods"] == 3 and out["batch"]["all_running_s"] < 25
+    assert out["sequential"]["p99_s"] < 10
+    assert 0 < out["kubelet_rss_mib"] < 200
+    assert out["kubelet_cpu_s_per_pod"] > 0
+    assert "steady" in out and out["steady"]["pods"] == 8
