@@ -17,7 +17,8 @@ class AdmissionError(Exception):
 
 
 class Attributes:
-    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind", "options")
+    __slots__ = ("operation", "resource", "subresource", "namespace", "name", "obj", "old", "user", "kind", "options",
+                 "prefetched")
 
     def __init__(self, operation, resource, subresource, namespace, name, obj, old=None, user=None, kind="", options=None):
         self.operation = operation
@@ -30,6 +31,7 @@ class Attributes:
         self.user = user
         self.kind = kind
         self.options = options
+        self.prefetched = None   # objects the server read ahead for plugins (uncached resources)
 
 
 class Plugin:

@@ -415,7 +415,9 @@ class ResourceQuota(Plugin):
             return
         new = pod_usage(a.obj)
         used: dict[str, Quantity] = {}
-        for p in self.server.list_objects("pods", a.namespace):
+        pods = a.prefetched["pods"] if a.prefetched and "pods" in a.prefetched else \
+            self.server.list_objects("pods", a.namespace)
+        for p in pods:
             for k, v in pod_usage(p).items():
                 used[k] = used[k] + v if k in used else v
         for qo in quotas:

@@ -317,7 +317,7 @@ class DenyEscalatingExec(Plugin):
     def validate(self, a):
         if a.resource != "pods" or a.subresource not in ("exec", "attach"):
             return
-        pod = self.server.get_object("pods", a.namespace, a.name) if self.server else None
+        pod = a.old if a.old is not None else (self.server.get_object("pods", a.namespace, a.name) if self.server else None)
         if pod is None:
             return
         spec = pod.get("spec") or {}

@@ -188,13 +188,16 @@ class ResourceCache:
         return out
 
     # -- writes -----------------------------------------------------------
-    def make_entry(self, obj, raw, rev):
+    def index_fields(self, obj):
         fields = self.fields_fn(obj)
         if ((obj.get("metadata") or {}).get("initializers") or {}).get("pending"):
             # alpha Initializers: uninitialized objects are hidden from list/watch unless the
             # client passes includeUninitialized=true (the server adds this field selector)
             fields = dict(fields, **{UNINITIALIZED: "true"})
-        return Entry(obj, raw, rev, fields)
+        return fields
+
+    def make_entry(self, obj, raw, rev):
+        return Entry(obj, raw, rev, self.index_fields(obj))
 
     def apply(self, etype: str, key: str, entry: Entry, prev: Entry | None):
         """Record + dispatch one committed change (entry is the new state; for DELETED the

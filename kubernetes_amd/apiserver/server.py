@@ -22,6 +22,10 @@ Two storage modes:
     assignments are claimed with per-device keys in the same transaction, so no two pods can
     be bound to one GPU even when the binds race through different workers. A stale cache
     shows up as a failed compare; the request is re-run once the cache caught up.
+    High-churn resources (pods, events) are NOT cached by shared-mode workers: their reads go
+    to the store (GET/RANGE), their watches to the store's native fan-out, and the worker's
+    store watch excludes them — so a worker's CPU per pod does not grow with the number of
+    workers (each worker ingesting every pod event capped multi-worker scaling).
 """
 from __future__ import annotations
 
@@ -36,13 +40,13 @@ from ..api import codec, core, meta as m
 from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
 from ..api.meta import parse_rfc3339, fast_copy, now_rfc3339
 from ..storage import wire
-from ..storage.mvcc import MVCCStore
+from ..storage.mvcc import CompactedError, MVCCStore
 from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
 from . import admission as adm
 from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, build_authorizer
-from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache
+from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, event_bytes
 from .registry import (APIError, already_exists, apply_binding, bad_request, conflict, deletion_stamp,
                        init_object_meta, invalid, not_found, strategy_for)
 
@@ -157,6 +161,7 @@ class APIServer:
         # `store or ...` would be wrong: an empty store has len() == 0 and is falsy
         self.store = None if self.remote_address else (store if store is not None else MVCCStore())
         self._applied_rev = 0
+        self.uncached: frozenset = frozenset()   # shared mode: resources read from the store
         self._rev_waiters: list = []  # heap of (rev, seq, future)
         self._waiter_seq = 0
         self._mine: dict = {}         # (key, rev) -> Entry committed by this worker
@@ -327,15 +332,53 @@ class APIServer:
         self.rstore = await RemoteStore(self.remote_address).connect()
         from ..storage.remote import FanoutClient
         self.fanout = FanoutClient.for_store(self.remote_address) if self.fanout_enabled else None
+        self.uncached = self._uncached_resources()
+        excl = tuple(m.prefix_for(m.BY_PLURAL[p]) for p in sorted(self.uncached))
         # one RANGE is an atomic snapshot (the store is single-threaded); watch from its revision
         kvs, _, rev = await self.rstore.range("/registry/")
         for kv in kvs:
-            self._ingest(0, kv, dispatch=False)
+            if not (excl and kv.key.startswith(excl)):
+                self._ingest(0, kv, dispatch=False)
         self._applied_rev = rev
         for c in self.caches.values():
             c.rev = rev
-        await self.rstore.watch("/registry/", rev, self._on_store_event)
+        await self.rstore.watch("/registry/", rev, self._on_store_event, exclude=excl)
         await self.bootstrap()
+
+    def _uncached_resources(self):
+        """Resources this shared-mode worker serves from the store instead of a watch cache:
+        pods and events, unless something here must read them synchronously (the Node
+        authorizer's pod graph) or their watches cannot be handed to the store's fan-out
+        (encrypted / non-JSON storage, TLS client connections). KAMD_SHARED_CACHE_ALL=1 keeps
+        every resource cached."""
+        if os.environ.get("KAMD_SHARED_CACHE_ALL") == "1" or self.fanout is None or self.tls[0] \
+                or self.storage_codec.media_type != codec.JSON or "Node" in self.authorization_modes:
+            return frozenset()
+        return frozenset(p for p in ("pods", "events") if p not in self.transformers)
+
+    def _entry_from_kv(self, plural, kv):
+        """Entry for a stored value without decoding the object: shared-store values carry the
+        index header (fields, labels) in front of the object JSON."""
+        v = kv.value
+        if v[:3] == _FRAME:
+            hl = int.from_bytes(v[3:7], "little")
+            fields, labels = codec.loads(v[7:7 + hl])
+            return Entry(None, v[7 + hl:], kv.mod_rev, fields, labels)
+        obj, raw = self._decode_value(kv)
+        return self.caches[plural].make_entry(obj, raw, kv.mod_rev)
+
+    async def _store_entries(self, ri, ns=None, label_sel=None, field_sel=None):
+        """(entries, revision) of an uncached resource straight from the store, key order."""
+        kvs, _, rev = await self.rstore.range(m.prefix_for(ri, ns if ri.namespaced else None))
+        out = []
+        for kv in kvs:
+            e = self._entry_from_kv(ri.plural, kv)
+            if label_sel is not None and not label_sel.matches(e.labels):
+                continue
+            if field_sel is not None and not field_sel.matches(e.fields):
+                continue
+            out.append(e)
+        return out, rev
 
     def _decode_value(self, kv):
         v = kv.value
@@ -357,16 +400,9 @@ class APIServer:
             return
         entry = self._mine.pop((kv.key, kv.mod_rev), None)
         if entry is None:
-            v = kv.value
-            if v[:3] == _FRAME:
-                # another worker's write: keep the bytes, decode only the small index header;
-                # the object itself is decoded on first use (Entry.obj)
-                hl = int.from_bytes(v[3:7], "little")
-                fields, labels = codec.loads(v[7:7 + hl])
-                entry = Entry(None, v[7 + hl:], kv.mod_rev, fields, labels)
-            else:
-                obj, raw = self._decode_value(kv)
-                entry = cache.make_entry(obj, raw, kv.mod_rev)
+            # another worker's write: keep the bytes, decode only the small index header; the
+            # object itself is decoded on first use (Entry.obj)
+            entry = self._entry_from_kv(cache.resource, kv)
         prev = cache.by_key.get(kv.key)
         plural = cache.resource
         if not dispatch:
@@ -382,6 +418,9 @@ class APIServer:
             self._observe(plural, entry.obj if etype != DELETED else prev.obj, etype == DELETED)
 
     def _on_store_event(self, t, kv):
+        if t == wire.PROGRESS:        # only excluded (uncached) keys changed, up to revision `kv`
+            self._advance(kv)
+            return
         if t is None:
             if self.store_healthy:
                 log.error("store watch stream ended; this API server worker is now unhealthy")
@@ -395,12 +434,15 @@ class APIServer:
             self._ingest(t, kv)
         except Exception:
             log.exception("failed to apply store event %s@%d", kv.key, kv.mod_rev)
-        if kv.mod_rev > self._applied_rev:
-            self._applied_rev = kv.mod_rev
+        self._advance(kv.mod_rev)
+
+    def _advance(self, rev):
+        if rev > self._applied_rev:
+            self._applied_rev = rev
             w = self._rev_waiters
-            if w and w[0][0] <= kv.mod_rev:
+            if w and w[0][0] <= rev:
                 import heapq
-                while w and w[0][0] <= kv.mod_rev:
+                while w and w[0][0] <= rev:
                     _, _, f = heapq.heappop(w)
                     if not f.done():
                         f.set_result(None)
@@ -438,6 +480,17 @@ class APIServer:
                 await self._wait_applied(kv.mod_rev)
 
     async def _async_existing(self, ri, namespace, name):
+        return await self._aexisting(ri, namespace, name)
+
+    async def _aexisting(self, ri, namespace, name):
+        """(key, Entry) of an existing object: from the store for uncached resources, else from
+        this worker's cache (`_existing`)."""
+        if ri.plural in self.uncached:
+            key = m.key_for(ri, namespace, name)
+            kv = await self.rstore.get(key)
+            if kv is None:
+                raise not_found(ri, name)
+            return key, self._entry_from_kv(ri.plural, kv)
         return self._existing(ri, namespace, name)
 
     def _claim_keys(self, ri, obj):
@@ -465,7 +518,7 @@ class APIServer:
         sealed = ri.plural in self.transformers
         json_storage = self.storage_codec.media_type == codec.JSON and not sealed
         # value framing: [00 'K' 'H' | u32 len | index header (fields, labels) | object]
-        hdr = codec.dumpb([cache.fields_fn(obj), md.get("labels") or {}])
+        hdr = codec.dumpb([cache.index_fields(obj), md.get("labels") or {}])
         frame = _FRAME + len(hdr).to_bytes(4, "little") + hdr
         if json_storage:
             md["resourceVersion"] = tok.decode()
@@ -496,6 +549,7 @@ class APIServer:
             for dk in sorted(old_d - new_d):
                 ops.append((wire.OP_DELETE, dk, None))
         cache = self.caches[ri.plural]
+        uncached = ri.plural in self.uncached
         done = []
 
         def on_ok(rev):
@@ -503,12 +557,18 @@ class APIServer:
             md["resourceVersion"] = rs
             raw = raw_t.replace(tok, rs.encode()) if raw_t is not None else codec.dumpb(obj)
             entry = cache.make_entry(obj, raw, rev)
-            self._mine[(key, rev)] = entry
+            if not uncached:
+                self._mine[(key, rev)] = entry
             done.append(entry)
 
         res = await self.rstore.txn(cmps, ops, on_ok)
         if not res.ok:
             if res.failed == 0:
+                if uncached:
+                    # read from the store, not a lagging cache: the object really changed
+                    if etype == ADDED:
+                        raise already_exists(ri, m.name_of(obj))
+                    raise _Stale(0)
                 raise _Stale(res.rev)
             owner = res.current.value.decode() if res.current is not None else "?"
             claim = cmps[res.failed][1]
@@ -516,6 +576,8 @@ class APIServer:
                 raise APIError(409, "Conflict", f"{claim.rsplit('/', 1)[-1]} is already allocated to {owner}")
             dev = claim[len(DEVICE_PREFIX):]
             raise APIError(409, "Conflict", f"device {dev} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
+        if uncached:
+            return done[0]
         await self._wait_applied(res.rev)
         self._mine.pop((key, res.rev), None)
         return done[0]
@@ -523,11 +585,15 @@ class APIServer:
     # ------------------------------------------------------------------
     # object-level API (admission plugins, controllers in-process, tests)
     def get_object(self, plural, namespace, name):
+        if plural in self.uncached:
+            raise RuntimeError(f"{plural} are not cached by this shared-store worker; read them from the store")
         ri = m.BY_PLURAL[plural]
         e = self.caches[plural].get(m.key_for(ri, namespace, name))
         return e.obj if e else None
 
     def list_objects(self, plural, namespace=None):
+        if plural in self.uncached:
+            raise RuntimeError(f"{plural} are not cached by this shared-store worker; read them from the store")
         ri = m.BY_PLURAL[plural]
         prefix = m.prefix_for(ri, namespace if ri.namespaced else None)
         return [e.obj for k, e in self.caches[plural].by_key.items() if k.startswith(prefix)]
@@ -604,6 +670,9 @@ class APIServer:
         ns = m.namespace_of(obj) if ri.namespaced else None
         if admit:
             a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
+            if ri.plural == "pods" and "pods" in self.uncached and self.list_objects("resourcequotas", ns):
+                # ResourceQuota sums the namespace's pods: hand it the store's current list
+                a.prefetched = {"pods": [e.obj for e in (await self._store_entries(ri, ns))[0]]}
             self._admit(a)
             obj = await self._mutating_webhooks(a, ri)
         if ri.plural == "services":
@@ -697,7 +766,7 @@ class APIServer:
     async def update(self, ri, namespace, name, obj, user=None, subresource=""):
         if not isinstance(obj, dict):
             raise bad_request("body must be a JSON object")
-        key, prev = self._existing(ri, namespace, name)
+        key, prev = await self._aexisting(ri, namespace, name)
         old = prev.obj
         obj = dict(obj)
         om = old["metadata"]
@@ -759,13 +828,13 @@ class APIServer:
 
     async def guaranteed_update(self, ri, namespace, name, fn, user=None, subresource=""):
         """Internal read-modify-write (used by binding, eviction)."""
-        key, prev = self._existing(ri, namespace, name)
+        key, prev = await self._aexisting(ri, namespace, name)
         obj = fast_copy(prev.obj)
         fn(obj)
         return await self._commit(ri, key, MODIFIED, obj, prev)
 
     async def patch(self, ri, namespace, name, content_type, patch_body, user=None, subresource=""):
-        key, prev = self._existing(ri, namespace, name)
+        key, prev = await self._aexisting(ri, namespace, name)
         try:
             patch = codec.loads(patch_body)
             # merge / strategic patches build new dicts along the patched paths only and share
@@ -782,7 +851,7 @@ class APIServer:
     async def delete(self, ri, namespace, name, opts=None, user=None):
         """Returns (Entry, deleted_now)."""
         opts = opts or {}
-        key, prev = self._existing(ri, namespace, name)
+        key, prev = await self._aexisting(ri, namespace, name)
         old = prev.obj
         pre = opts.get("preconditions") or {}
         if pre.get("uid") and pre["uid"] != old["metadata"].get("uid"):
@@ -845,7 +914,7 @@ class APIServer:
     async def bind(self, namespace, name, binding, user=None):
         """POST pods/{name}/binding (fork F6) with the duplicate-device guard."""
         ri = m.BY_PLURAL["pods"]
-        key, prev = self._existing(ri, namespace, name)
+        key, prev = await self._aexisting(ri, namespace, name)
         a = adm.Attributes(adm.CREATE, "pods", "binding", namespace, name, binding, prev.obj, user, "Binding")
         self._admit(a)
         self._validate_admission(a)
@@ -874,7 +943,7 @@ class APIServer:
     async def evict(self, namespace, name, eviction, user=None):
         ri = m.BY_PLURAL["pods"]
         # PodDisruptionBudget check
-        pod = self._existing(ri, namespace, name)[1].obj
+        pod = (await self._aexisting(ri, namespace, name))[1].obj
         labels = (pod.get("metadata") or {}).get("labels") or {}
         from ..api.labels import label_selector_as_selector
         for pdb in self.list_objects("poddisruptionbudgets", namespace):
@@ -907,10 +976,12 @@ class APIServer:
 
     def expired_events(self, now=None):
         """Events whose last write (lastTimestamp, else creationTimestamp) is older than the TTL."""
+        return self._expired([e.obj for e in list(self.caches["events"].by_key.values())], now)
+
+    def _expired(self, events, now=None):
         now = time.time() if now is None else now
         out = []
-        for key, e in list(self.caches["events"].by_key.items()):
-            o = e.obj
+        for o in events:
             t = parse_rfc3339(o.get("lastTimestamp")) or parse_rfc3339((o.get("metadata") or {}).get("creationTimestamp"))
             if t is not None and now - t > self.event_ttl:
                 out.append(o)
@@ -919,7 +990,12 @@ class APIServer:
     async def reap_events(self, now=None):
         n = 0
         ri = m.BY_PLURAL["events"]
-        for o in self.expired_events(now):
+        if "events" in self.uncached:
+            entries, _ = await self._store_entries(ri)
+            expired = self._expired([e.obj for e in entries], now)
+        else:
+            expired = self.expired_events(now)
+        for o in expired:
             md = o["metadata"]
             try:
                 await self._retrying(lambda md=md: self.delete(ri, md.get("namespace"), md["name"], {}))
@@ -1183,6 +1259,8 @@ class APIServer:
                 return self._watch(req, ri, ns, name)
             if name is None:
                 self._authorize(user, "list", ns, ri.plural, "", "", ri.group, req.path)
+                if ri.plural in self.uncached:
+                    return await self._list_store(req, ri, ns)
                 return self._list(req, ri, ns)
             if sub == "log" and ri.plural == "pods":
                 self._authorize(user, "get", ns, "pods", "log", name, "", req.path)
@@ -1191,6 +1269,8 @@ class APIServer:
                 self._authorize(user, "get", ns, "pods", sub, name, "", req.path)
                 return await self._pod_stream(req, ns, name, sub)
             self._authorize(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
+            if ri.plural in self.uncached:
+                return Response(200, (await self._aexisting(ri, ns, name))[1].raw)
             key = m.key_for(ri, ns, name)
             e = self.caches[ri.plural].get(key)
             if e is None and self.rstore is not None:
@@ -1302,7 +1382,11 @@ class APIServer:
         fs = parse_field_selector(req.query.get("fieldSelector")) if req.query.get("fieldSelector") else None
         opts = codec.loads(req.body) if req.body else {}
         items = []
-        for e in self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs):
+        if ri.plural in self.uncached:
+            entries = (await self._store_entries(ri, ns, ls, fs))[0]
+        else:
+            entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
+        for e in entries:
             try:
                 d, _ = await self.delete(ri, m.namespace_of(e.obj) or None, m.name_of(e.obj), opts, user)
                 items.append(d.obj)
@@ -1324,9 +1408,19 @@ class APIServer:
         fsel = self._hide_uninitialized(q, q.get("fieldSelector"))
         fs = parse_field_selector(fsel) if fsel else None
         entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
+        return self._list_response(q, ri, entries, str(self.revision))
+
+    async def _list_store(self, req, ri, ns):
+        q = req.query
+        ls = parse_labels(q.get("labelSelector")) if q.get("labelSelector") else None
+        fsel = self._hide_uninitialized(q, q.get("fieldSelector"))
+        fs = parse_field_selector(fsel) if fsel else None
+        entries, rev = await self._store_entries(ri, ns, ls, fs)
+        return self._list_response(q, ri, entries, str(rev))
+
+    def _list_response(self, q, ri, entries, rv):
         limit = int(q.get("limit") or 0)
         cont = q.get("continue")
-        rv = str(self.revision)
         next_token = None
         if cont:
             try:
@@ -1366,6 +1460,72 @@ class APIServer:
                 reqs.append((1, "!=" if op == "!=" else "=", k, [v]))
         return reqs
 
+    def _watch_store(self, ri, ns, label_selector, field_selector, rv, timeout):
+        """Watch of an uncached resource that the store's fan-out cannot serve (a TLS client,
+        quantity label selectors): a store watch of its own, filtered here. Without the previous
+        object state, a change that leaves the selector is reported as DELETED even if the
+        client never had the object (informers ignore unknown deletes)."""
+        from ..storage.remote import RemoteStore
+        ls = parse_labels(label_selector) if label_selector else None
+        fs = parse_field_selector(field_selector) if field_selector else None
+        prefix = m.prefix_for(ri, ns if ri.namespaced else None)
+        server = self
+
+        def ok(e):
+            return (ls is None or ls.matches(e.labels)) and (fs is None or fs.matches(e.fields))
+
+        async def run(writer):
+            st = await RemoteStore(server.remote_address).connect()
+            done = asyncio.get_running_loop().create_future()
+            seen: dict = {}
+            try:
+                if not rv or rv == "0":
+                    kvs, _, frm = await st.range(prefix)
+                    for kv in kvs:
+                        e = server._entry_from_kv(ri.plural, kv)
+                        if ok(e):
+                            seen[kv.key] = True
+                            writer.write(event_bytes(ADDED, e.raw))
+                else:
+                    frm = int(rv)
+
+                def on_event(t, kv):
+                    if t is None:
+                        if not done.done():
+                            done.set_result(None)
+                        return
+                    if t == wire.PROGRESS:
+                        return
+                    e = server._entry_from_kv(ri.plural, kv)
+                    cur = t != wire.OP_DELETE and ok(e)
+                    was = seen.get(kv.key, kv.version > 1 or t == wire.OP_DELETE)
+                    if t == wire.OP_DELETE:
+                        if was or ok(e):
+                            writer.write(event_bytes(DELETED, e.raw))
+                        seen.pop(kv.key, None)
+                    elif cur:
+                        writer.write(event_bytes(MODIFIED if was and kv.version > 1 else ADDED, e.raw))
+                        seen[kv.key] = True
+                    elif was:
+                        writer.write(event_bytes(DELETED, e.raw))
+                        seen[kv.key] = False
+                try:
+                    await st.watch(prefix, frm, on_event)
+                except CompactedError:
+                    writer.write(codec.dumpb({"type": "ERROR", "object": m.status_obj(410, "Expired", f"too old resource version: {frm}")}) + b"\n")
+                    return
+                server.m_watchers.labels(ri.kind).inc()
+                try:
+                    waits = [done, asyncio.ensure_future(writer.wait_closed())]
+                    await asyncio.wait(waits, timeout=timeout, return_when=asyncio.FIRST_COMPLETED)
+                    waits[1].cancel()
+                finally:
+                    server.m_watchers.labels(ri.kind).dec()
+            finally:
+                await st.close()
+
+        return StreamResponse(run)
+
     def _watch(self, req, ri, ns, name):
         q = req.query
         rv = q.get("resourceVersion")
@@ -1381,6 +1541,8 @@ class APIServer:
             msg = self.fanout.encode(m.prefix_for(ri, ns), send_initial, 0 if send_initial else int(rv), timeout, reqs)
             self.m_fanout.labels(ri.plural).inc()
             return HandoffResponse(lambda fd: self.fanout.handoff(fd, msg))
+        if ri.plural in self.uncached:
+            return self._watch_store(ri, ns, q.get("labelSelector"), fsel, rv, timeout)
         cache = self.caches[ri.plural]
         send_initial = not rv or rv == "0"
         from_rev = int(rv) if rv and rv != "0" else None
@@ -1410,12 +1572,15 @@ class APIServer:
 
         return StreamResponse(run)
 
-    def _kubelet_of(self, ns, name):
+    async def _kubelet_of(self, ns, name):
         """(pod, kubelet host, kubelet port) — the node connection info the reference resolves in
         `pkg/registry/core/pod/strategy.go` ResourceLocation / streamLocation."""
-        pod = self.get_object("pods", ns, name)
-        if pod is None:
-            raise not_found(m.BY_PLURAL["pods"], name)
+        if "pods" in self.uncached:
+            pod = (await self._aexisting(m.BY_PLURAL["pods"], ns, name))[1].obj
+        else:
+            pod = self.get_object("pods", ns, name)
+            if pod is None:
+                raise not_found(m.BY_PLURAL["pods"], name)
         node = (pod.get("spec") or {}).get("nodeName")
         if not node:
             raise bad_request(f"pod {name} is not scheduled")
@@ -1433,7 +1598,7 @@ class APIServer:
         """pods/exec, pods/attach (framed stream) and pods/portforward (Upgrade: tcp) proxied to
         the node's kubelet (`pkg/registry/core/pod/rest/subresources.go` ExecREST/PortForwardREST)."""
         from urllib.parse import parse_qs, urlencode
-        pod, addr, port = self._kubelet_of(ns, name)
+        pod, addr, port = await self._kubelet_of(ns, name)
         a = adm.Attributes(adm.CONNECT, "pods", sub, ns, name, None, pod, getattr(req, "user", None), "Pod")
         self._admit(a)
         self._validate_admission(a)
@@ -1517,7 +1682,7 @@ class APIServer:
         return _json(200, {"kind": "ComponentStatusList", "apiVersion": "v1", "metadata": {}, "items": list(items)})
 
     async def _pod_log(self, ns, name, q):
-        _, addr, port = self._kubelet_of(ns, name)
+        _, addr, port = await self._kubelet_of(ns, name)
         from ..client.http import HTTPClient
         c = HTTPClient(f"http://{addr}:{port}")
         try:

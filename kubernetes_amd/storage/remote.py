@@ -109,6 +109,12 @@ class RemoteStore:
                 kv, _ = wire.decode_kv(payload, 1)
                 cb(t, kv)
             return
+        if st == wire.PROGRESS:
+            # excluded keys changed up to this revision (watch(..., exclude=...))
+            cb = self._watches.get(rid)
+            if cb is not None:
+                cb(wire.PROGRESS, struct.unpack_from("<q", payload)[0])
+            return
         cb = self._on_ok.pop(rid, None) if self._on_ok else None
         if cb is not None and st == wire.OK:
             # synchronous commit hook: runs before any later frame (e.g. the watch event of this
@@ -167,11 +173,16 @@ class RemoteStore:
         _, fut = self._send(wire.COMPACT, struct.pack("<q", rev))
         await fut
 
-    async def watch(self, prefix, from_rev, callback):
+    async def watch(self, prefix, from_rev, callback, exclude=()):
         """callback(type, kv) for each event with mod_rev > from_rev (0 = only new events);
-        callback(None, None) when the stream ends. Returns the store revision at subscribe."""
+        callback(None, None) when the stream ends. Returns the store revision at subscribe.
+        Keys under an `exclude` prefix are not delivered; instead callback(wire.PROGRESS, rev)
+        reports (coalesced) that the store moved on to `rev`."""
         pb = prefix.encode()
-        rid, fut = self._send(wire.WATCH, struct.pack("<q", from_rev) + struct.pack("<I", len(pb)) + pb)
+        payload = struct.pack("<q", from_rev) + struct.pack("<I", len(pb)) + pb
+        if exclude:
+            payload += struct.pack("<H", len(exclude)) + b"".join(wire._s(x.encode()) for x in exclude)
+        rid, fut = self._send(wire.WATCH, payload)
         # register before the reply: replayed events directly follow the OK frame
         self._watches[rid] = callback
         st, p = await fut

@@ -16,7 +16,7 @@ OP_PUT, OP_DELETE, OP_PUT_INJECT, OP_DELETE_TOMBSTONE = 0, 1, 2, 3
 # request ops
 TXN, GET, RANGE, WATCH, REV, COMPACT = 1, 2, 3, 4, 5, 6
 # statuses
-OK, FAILED, COMPACTED, NOT_FOUND, EVENT, BAD = 0, 1, 3, 4, 8, 9
+OK, FAILED, COMPACTED, NOT_FOUND, EVENT, BAD, PROGRESS = 0, 1, 3, 4, 8, 9, 10
 
 _u32 = struct.Struct("<I")
 _i64 = struct.Struct("<q")

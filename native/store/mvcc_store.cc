@@ -20,8 +20,12 @@
 //             -> status 0: i64 rev | status 1 (compare failed): u16 idx of failed compare, kv of that key
 //   GET(2):   u32 klen key -> status 0: kv | status 4 not found
 //   RANGE(3): u32 plen prefix u32 limit u32 salen start_after -> i64 rev u8 more u32 n {kv}
-//   WATCH(4): i64 from_rev u32 plen prefix -> status 0 i64 rev, then EVENT frames (status 8) on the same
-//             id: u8 type(0 put,1 del) kv(with prev? no) ; status 3 if from_rev is compacted
+//   WATCH(4): i64 from_rev u32 plen prefix [u16 nexcl {u32 len excluded_prefix}]
+//             -> status 0 i64 rev, then EVENT frames (status 8) on the same id: u8 type(0 put,1 del) kv;
+//             status 3 if from_rev is compacted. Keys under an excluded prefix are not sent; instead
+//             the watch gets at most one PROGRESS frame (status 10: i64 rev) per event-loop pass, so
+//             a client that waits for "my cache has seen revision R" still advances (API server
+//             workers exclude the resources they read from the store instead of caching).
 //   REV(5):   -> i64 rev
 //   COMPACT(6): i64 rev
 //   kv = i64 create_rev i64 mod_rev i64 version u32 klen key u32 vlen val
@@ -431,6 +435,14 @@ struct Watch {
   Conn* conn;
   uint32_t id;
   std::string prefix;
+  std::vector<std::string> excl;
+  int64_t progress = 0;  // latest excluded revision not yet reported
+
+  bool excluded(const std::string& key) const {
+    for (const std::string& x : excl)
+      if (key.compare(0, x.size(), x) == 0) return true;
+    return false;
+  }
 };
 
 
@@ -657,6 +669,7 @@ class Server {
         }
         if (evs[i].events & EPOLLOUT) flush(c);
       }
+      if (progress_pending_) send_progress();
       // flush every connection with pending output once per loop (coalesces watch events)
       for (Conn* c : dirty_) flush(c);
       dirty_.clear();
@@ -764,11 +777,27 @@ class Server {
     epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
   }
 
+  void send_progress() {
+    progress_pending_ = false;
+    for (Watch& w : watches_) {
+      if (!w.progress) continue;
+      Writer pw;
+      pw.put<int64_t>(w.progress);
+      w.progress = 0;
+      reply(w.conn, w.id, 10, pw.b);
+    }
+  }
+
   void dispatch(const std::vector<Event>& evs) {
     if (watches_.empty()) return;
     for (const Event& ev : evs) {
       for (Watch& w : watches_) {
         if (ev.key.compare(0, w.prefix.size(), w.prefix) != 0) continue;
+        if (!w.excl.empty() && w.excluded(ev.key)) {
+          w.progress = ev.rev;
+          progress_pending_ = true;
+          continue;
+        }
         Writer pw;
         pw.put<uint8_t>(ev.type);
         pw.kv(ev.key, *ev.kv);
@@ -829,6 +858,12 @@ class Server {
       case 4: {  // WATCH
         int64_t from = r.get<int64_t>();
         std::string prefix = r.str();
+        Watch nw{c, id, prefix};
+        if (r.p + 2 <= r.e) {
+          uint16_t nx = r.get<uint16_t>();
+          for (uint16_t i = 0; i < nx && r.ok; ++i) nw.excl.push_back(r.str());
+          if (!r.ok) { reply(c, id, 9, ""); return; }
+        }
         std::vector<const Event*> evs;
         if (from > 0 && !eng_->since(from, prefix, &evs)) {
           w.put<int64_t>(eng_->compacted());
@@ -838,12 +873,13 @@ class Server {
         w.put<int64_t>(eng_->rev());
         reply(c, id, 0, w.b);
         for (const Event* e : evs) {
+          if (!nw.excl.empty() && nw.excluded(e->key)) continue;
           Writer pw;
           pw.put<uint8_t>(e->type);
           pw.kv(e->key, *e->kv);
           reply(c, id, 8, pw.b);
         }
-        watches_.push_back(Watch{c, id, prefix});
+        watches_.push_back(std::move(nw));
         return;
       }
       case 5:
@@ -1099,6 +1135,7 @@ class Server {
   std::unordered_map<int, int> listeners_;
   std::unordered_map<int, std::unique_ptr<Conn>> conns_;
   std::vector<Watch> watches_;
+  bool progress_pending_ = false;
   std::vector<Conn*> dirty_;
 };
 

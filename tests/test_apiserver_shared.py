@@ -145,8 +145,11 @@ def test_device_claims_across_workers(run, store):
     run(main())
 
 
-def test_read_and_bind_right_after_write_on_other_worker(run, store):
-    """A worker that has not yet applied another worker's write must not answer 404 for it."""
+def test_read_and_bind_right_after_write_on_other_worker(run, store, monkeypatch):
+    """A worker that has not yet applied another worker's write must not answer 404 for it
+    (pods cached on every worker here, so the cache-lag path is what runs)."""
+    monkeypatch.setenv("KAMD_SHARED_CACHE_ALL", "1")
+
     async def main():
         servers, (a, b) = await _workers(store)
         # make worker b lag: its store events are applied 30 ms late (in order)
@@ -283,6 +286,95 @@ def test_native_watch_fanout_semantics(run, store):
             assert "apiserver_watch_fanout_handoffs_total" in m
             t1.cancel()
             t2.cancel()
+        finally:
+            await _close(servers, [a, b])
+    run(main())
+
+
+def test_uncached_pods_and_events_read_from_store(run, store):
+    """Shared-mode workers do not cache pods/events: reads hit the store (no lag to wait for),
+    the worker's store watch excludes them (progress frames still advance its revision), list
+    selectors, conflicts, device claims, quota admission, TTL reaping and the non-fan-out watch
+    fallback all work from the store."""
+    from kubernetes_amd.storage import wire
+
+    async def main():
+        servers, (a, b) = await _workers(store)
+        try:
+            assert servers[0].uncached == {"pods", "events"} and servers[1].uncached == {"pods", "events"}
+            await a.create("nodes", {"metadata": {"name": "n0"}})
+            for i in range(5):
+                p = await a.create("pods", dict(gpu_pod(f"u{i}"), metadata={"name": f"u{i}", "namespace": "default",
+                                                                            "labels": {"i": str(i)}}))
+                got = await b.get("pods", f"u{i}", "default")       # no polling: read from the store
+                assert got == p
+            assert not servers[0].caches["pods"].by_key and not servers[1].caches["pods"].by_key
+            # the last writes were pods only: b's applied revision still reaches them (PROGRESS)
+            rv = int(p["metadata"]["resourceVersion"])
+            await asyncio.wait_for(servers[1]._wait_applied(rv), 5)
+            lst = await b.list("pods", "default", label_selector="i in (1,3)")
+            assert [x["metadata"]["name"] for x in lst["items"]] == ["u1", "u3"]
+            assert int(lst["metadata"]["resourceVersion"]) >= rv
+            lim = await b.list("pods", "default", limit=2)
+            assert len(lim["items"]) == 2 and lim["metadata"].get("continue")
+            # stale update → 409; fresh one works through the other worker
+            cur = await a.get("pods", "u0", "default")
+            with pytest.raises(APIStatusError) as ei:
+                await b.update("pods", dict(cur, metadata=dict(cur["metadata"], resourceVersion="1")), "default")
+            assert ei.value.code == 409
+            cur["metadata"].setdefault("labels", {})["fresh"] = "1"
+            assert (await b.update("pods", cur, "default"))["metadata"]["labels"]["fresh"] == "1"
+            with pytest.raises(APIStatusError) as ei:
+                await b.create("pods", gpu_pod("u0"))
+            assert ei.value.code == 409
+            # device claims across workers
+            p0 = await b.get("pods", "u0", "default")
+            p1 = await b.get("pods", "u1", "default")
+            await a.bind("default", "u0", "n0", {p0["spec"]["extendedResources"][0]["name"]: {"resources": ["G0"]}})
+            with pytest.raises(APIStatusError) as ei:
+                await b.bind("default", "u1", "n0", {p1["spec"]["extendedResources"][0]["name"]: {"resources": ["G0"]}})
+            assert ei.value.code == 409
+            # quota admission sums the namespace's pods read from the store
+            await a.create("namespaces", {"metadata": {"name": "q"}})
+            await a.create("resourcequotas", {"metadata": {"name": "rq", "namespace": "q"},
+                                              "spec": {"hard": {"pods": "2"}}}, "q")
+            await _eventually(lambda: b.get("resourcequotas", "rq", "q"))
+            for i in range(2):
+                await b.create("pods", {"metadata": {"name": f"q{i}", "namespace": "q"},
+                                        "spec": {"containers": [{"name": "c", "image": "x"}]}}, "q")
+            with pytest.raises(APIStatusError) as ei:
+                await b.create("pods", {"metadata": {"name": "q2", "namespace": "q"},
+                                        "spec": {"containers": [{"name": "c", "image": "x"}]}}, "q")
+            assert ei.value.code == 403
+            # watch that the fan-out cannot serve (quantity selector) → store-watch fallback
+            w = await b.watch("pods", "default", "0", label_selector="i>2")
+            seen = []
+
+            async def drain():
+                async for typ, obj in w:
+                    seen.append((typ, obj["metadata"]["name"]))
+                    if ("DELETED", "u4") in seen:
+                        return
+            t = asyncio.ensure_future(drain())
+            await _eventually(lambda: asyncio.sleep(0, result=("ADDED", "u4") in seen))
+            assert ("ADDED", "u3") in seen and not any(n in ("u0", "u1", "u2") for _, n in seen)
+            await a.delete("pods", "u4", "default")
+            await asyncio.wait_for(t, 5)
+            w.close()
+            assert servers[1].m_fanout.value("pods") == 0     # nothing above used the fan-out
+            # events: uncached, TTL reaping reads them from the store
+            await a.create("events", {"metadata": {"name": "e1", "namespace": "default"},
+                                      "involvedObject": {"kind": "Pod", "name": "u0", "namespace": "default"},
+                                      "reason": "X", "message": "m", "type": "Normal",
+                                      "lastTimestamp": "2000-01-01T00:00:00Z"}, "default")
+            assert (await b.get("events", "e1", "default"))["reason"] == "X"
+            assert await servers[1].reap_events() == 1
+            with pytest.raises(APIStatusError):
+                await a.get("events", "e1", "default")
+            assert not servers[0].caches["events"].by_key
+            with pytest.raises(RuntimeError):
+                servers[0].list_objects("pods")
+            assert wire.PROGRESS == 10
         finally:
             await _close(servers, [a, b])
     run(main())
