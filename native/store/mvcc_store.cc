@@ -564,6 +564,9 @@ struct FanWatch {
   std::vector<Requirement> reqs;
   std::string out;
   bool dead = false;
+  bool queued = false;    // in fan_dirty_
+  bool node_indexed = false;
+  std::string node_key;   // spec.nodeName=X requirement: the watch lives in fan_by_node_[X]
   double deadline = 0;  // CLOCK_MONOTONIC seconds, 0 = none
   bool matches(const Index& ix) const {
     if (!ix.ok) return false;
@@ -673,7 +676,10 @@ class Server {
       // flush every connection with pending output once per loop (coalesces watch events)
       for (Conn* c : dirty_) flush(c);
       dirty_.clear();
-      for (FanWatch* w : fan_dirty_) flush_fan(w);
+      for (FanWatch* w : fan_dirty_) {
+        w->queued = false;
+        flush_fan(w);
+      }
       fan_dirty_.clear();
       expire_fan();
       reap_fan();
@@ -988,6 +994,13 @@ class Server {
       w->reqs.push_back(std::move(q));
     }
     if (!r.ok || ver != 1) { close(client); return; }
+    for (const Requirement& q : w->reqs)
+      if (q.target == 1 && q.op == 0 && q.vals.size() == 1 && q.key == "spec.nodeName") {
+        // kubelets watch their own node's pods (cacher.go's nodeName-indexed watchers)
+        w->node_indexed = true;
+        w->node_key = q.vals[0];
+        break;
+      }
     int fl = fcntl(client, F_GETFL);
     fcntl(client, F_SETFL, fl | O_NONBLOCK);
     int one = 1;
@@ -1022,6 +1035,8 @@ class Server {
     e.events = EPOLLIN | EPOLLRDHUP;
     e.data.fd = client;
     epoll_ctl(ep_, EPOLL_CTL_ADD, client, &e);
+    if (raw->node_indexed) fan_by_node_[raw->node_key].push_back(raw);
+    else fan_other_.push_back(raw);
     fan_[client] = std::move(w);
     flush_fan(raw);
   }
@@ -1048,26 +1063,51 @@ class Server {
     mark_fan(w);
   }
 
+  // Per event: the unindexed watches, plus the watches of the node the object is on now and
+  // was on before (O(matching watchers), not O(all watchers), with one watch per kubelet).
   void fan_dispatch(const std::vector<Event>& evs) {
     if (fan_.empty()) return;
     for (const Event& ev : evs) {
       Index cur, prv;
       bool parsed = false;
-      for (auto& kv : fan_) {
-        FanWatch* w = kv.second.get();
+      auto parse = [&]() {
+        if (parsed) return;
+        cur = parse_index(ev.kv->value);
+        if (ev.prev) prv = parse_index(ev.prev->value);
+        parsed = true;
+      };
+      for (FanWatch* w : fan_other_) {
         if (w->dead || ev.key.compare(0, w->prefix.size(), w->prefix) != 0) continue;
-        if (!parsed) {
-          cur = parse_index(ev.kv->value);
-          if (ev.prev) prv = parse_index(ev.prev->value);
-          parsed = true;
-        }
+        parse();
         fan_one(w, ev, &cur, &prv);
+      }
+      if (fan_by_node_.empty()) continue;
+      parse();
+      static const std::string kNode = "spec.nodeName";
+      auto node_of = [](const Index& ix) -> std::string {
+        auto it = ix.fields.find(kNode);
+        return it == ix.fields.end() ? std::string() : it->second;
+      };
+      std::string a = node_of(cur);
+      auto bucket = [&](const std::string& n) {
+        auto it = fan_by_node_.find(n);
+        if (it == fan_by_node_.end()) return;
+        for (FanWatch* w : it->second)
+          if (!w->dead) fan_one(w, ev, &cur, &prv);
+      };
+      bucket(a);
+      if (ev.prev) {
+        std::string b = node_of(prv);
+        if (b != a) bucket(b);
       }
     }
   }
 
   void mark_fan(FanWatch* w) {
-    if (!w->out.empty()) fan_dirty_.push_back(w);
+    if (!w->out.empty() && !w->queued) {
+      w->queued = true;
+      fan_dirty_.push_back(w);
+    }
   }
 
   void flush_fan(FanWatch* w) {
@@ -1116,6 +1156,16 @@ class Server {
       FanWatch* w = it->second.get();
       if (w->dead && w->out.empty()) {
         fan_dirty_.erase(std::remove(fan_dirty_.begin(), fan_dirty_.end(), w), fan_dirty_.end());
+        auto drop = [w](std::vector<FanWatch*>* v) { v->erase(std::remove(v->begin(), v->end(), w), v->end()); };
+        if (w->node_indexed) {
+          auto b = fan_by_node_.find(w->node_key);
+          if (b != fan_by_node_.end()) {
+            drop(&b->second);
+            if (b->second.empty()) fan_by_node_.erase(b);
+          }
+        } else {
+          drop(&fan_other_);
+        }
         epoll_ctl(ep_, EPOLL_CTL_DEL, w->fd, nullptr);
         close(w->fd);
         it = fan_.erase(it);
@@ -1129,6 +1179,8 @@ class Server {
   std::unordered_map<int, Handoff> handoffs_;
   std::map<int, std::unique_ptr<FanWatch>> fan_;
   std::vector<FanWatch*> fan_dirty_;
+  std::vector<FanWatch*> fan_other_;
+  std::unordered_map<std::string, std::vector<FanWatch*>> fan_by_node_;
 
   Engine* eng_;
   int ep_ = -1;
