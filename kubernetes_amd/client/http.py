@@ -148,7 +148,7 @@ class HTTPClient:
         return status, hdrs, conn.reader, conn.writer
 
     async def stream(self, method, path, headers=None):
-        """Open a streaming GET; returns (status, async line iterator, closer)."""
+        """Open a streaming GET; returns (status, async iterator of line batches, closer)."""
         conn = await self._open()
         conn.writer.write(self._head(method, path, None, None, headers))
         status, hdrs = await _read_response(conn.reader)
@@ -159,35 +159,48 @@ class HTTPClient:
         chunked = hdrs.get("transfer-encoding", "").lower() == "chunked"
         reader = conn.reader
 
-        async def lines():
-            buf = b""
+        async def batches():
+            """Lists of complete lines: everything that arrived in one read is parsed and handed
+            over at once (a watch server coalesces events per send), so a consumer pays one
+            await per batch, not per event."""
+            raw = bytearray()
+            pay = bytearray()
+            done = False
             try:
-                while True:
-                    if chunked:
-                        ln = await reader.readline()
-                        if not ln:
-                            return
-                        n = int(ln.strip().split(b";")[0] or b"0", 16)
-                        if n == 0:
-                            return
-                        data = await reader.readexactly(n)
-                        await reader.readline()
+                while not done:
+                    data = await reader.read(1 << 18)
+                    if not data:
+                        done = True
+                    elif chunked:
+                        raw += data
+                        pos = 0
+                        while True:
+                            j = raw.find(b"\r\n", pos)
+                            if j < 0:
+                                break
+                            n = int(bytes(raw[pos:j]).split(b";")[0].strip() or b"0", 16)
+                            if n == 0:
+                                done = True
+                                break
+                            end = j + 2 + n
+                            if len(raw) < end + 2:
+                                break
+                            pay += raw[j + 2:end]
+                            pos = end + 2
+                        if pos:
+                            del raw[:pos]
                     else:
-                        data = await reader.read(1 << 16)
-                        if not data:
-                            return
-                    buf += data
-                    while True:
-                        i = buf.find(b"\n")
-                        if i < 0:
-                            break
-                        line, buf = buf[:i], buf[i + 1:]
-                        if line.strip():
-                            yield line
+                        pay += data
+                    k = pay.rfind(b"\n")
+                    if k >= 0:
+                        out = [ln for ln in bytes(pay[:k]).split(b"\n") if ln.strip()]
+                        del pay[:k + 1]
+                        if out:
+                            yield out
             except (ConnectionError, asyncio.IncompleteReadError, OSError, ValueError):
                 return
 
-        return status, lines(), conn.close
+        return status, batches(), conn.close
 
     async def close(self):
         self._closed = True

@@ -165,8 +165,9 @@ class Informer:
                                              self.field_selector, self.watch_timeout)
                 self._stream = st
                 backoff = 0.05
-                async for etype, obj in st:
-                    self._handle(etype, obj)
+                async for evs in st.batches():
+                    for etype, obj in evs:
+                        self._handle(etype, obj)
                 st.close()
             except asyncio.CancelledError:
                 raise

@@ -6,6 +6,7 @@ client-side QPS/Burst token bucket (`util/flowcontrol`), `errors.IsNotFound/IsCo
 from __future__ import annotations
 
 import asyncio
+import collections
 import time
 from urllib.parse import quote, urlencode
 
@@ -209,21 +210,45 @@ class Client:
         return _WatchStream(lines, closer)
 
 
+def _event(line):
+    ev = codec.loads(line)
+    if ev.get("type") == "ERROR":
+        obj = ev.get("object") or {}
+        raise APIStatusError(obj.get("code", 500), obj)
+    return ev["type"], ev["object"]
+
+
 class _WatchStream:
-    def __init__(self, lines, closer):
-        self._lines = lines
+    """Watch events, one at a time (`async for typ, obj in stream`) or per received batch
+    (`async for evs in stream.batches()`, what informers use: one await per network read)."""
+
+    def __init__(self, batches, closer):
+        self._batches = batches
         self._closer = closer
+        self._pending = collections.deque()
 
     def __aiter__(self):
         return self
 
     async def __anext__(self):
-        line = await self._lines.__anext__()
-        ev = codec.loads(line)
-        if ev.get("type") == "ERROR":
-            obj = ev.get("object") or {}
-            raise APIStatusError(obj.get("code", 500), obj)
-        return ev["type"], ev["object"]
+        while not self._pending:
+            self._pending.extend(await self._batches.__anext__())
+        return _event(self._pending.popleft())
+
+    async def batches(self):
+        if self._pending:
+            lines, self._pending = list(self._pending), collections.deque()
+            yield [_event(ln) for ln in lines]
+        async for lines in self._batches:
+            out = []
+            for ln in lines:
+                try:
+                    out.append(_event(ln))
+                except APIStatusError:
+                    if out:
+                        yield out
+                    raise
+            yield out
 
     def close(self):
         self._closer()

@@ -68,18 +68,19 @@ class DensityRunner:
         self._watch_task = asyncio.ensure_future(self._watch())
 
     async def _watch(self):
-        async for etype, pod in self._stream:
-            name = pod["metadata"]["name"]
-            now = time.monotonic()
-            if etype == "DELETED":
-                self.gone.setdefault(name, now)
-            else:
-                if (pod.get("spec") or {}).get("nodeName") and name not in self.scheduled:
-                    self.scheduled[name] = now
-                if (pod.get("status") or {}).get("phase") == core.POD_RUNNING and name not in self.running:
-                    self.running[name] = now
-                    self.assigned[name] = (pod["spec"].get("nodeName"),
-                                           [i for ids in core.pod_assigned_devices(pod).values() for i in ids])
+        async for evs in self._stream.batches():
+            now = time.monotonic()      # when this read arrived (one timestamp per batch)
+            for etype, pod in evs:
+                name = pod["metadata"]["name"]
+                if etype == "DELETED":
+                    self.gone.setdefault(name, now)
+                else:
+                    if (pod.get("spec") or {}).get("nodeName") and name not in self.scheduled:
+                        self.scheduled[name] = now
+                    if (pod.get("status") or {}).get("phase") == core.POD_RUNNING and name not in self.running:
+                        self.running[name] = now
+                        self.assigned[name] = (pod["spec"].get("nodeName"),
+                                               [i for ids in core.pod_assigned_devices(pod).values() for i in ids])
             self._changed.set()
 
     async def _diagnose(self, names, phase):

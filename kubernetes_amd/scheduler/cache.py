@@ -332,6 +332,21 @@ class SchedulerCache:
         key = ns_name(pod)
         node = pod["spec"]["nodeName"]
         st = self.pod_states.get(key)
+        if st is not None and st[1] == node:
+            old = st[0]
+            if old.get("spec") == pod.get("spec") and \
+                    (old.get("metadata") or {}).get("labels") == (pod.get("metadata") or {}).get("labels"):
+                # the bound copy of an assumed pod, or a status / metadata-only update (kubelet
+                # status, graceful deletion): nothing the scheduler accounts for changed — keep
+                # the parsed PodInfo, swap the object
+                ni = self._node(node)
+                ent = ni.pods.get(key)
+                if ent is not None:
+                    ni.pods[key] = (pod, ent[1])
+                    self.pod_states[key] = (pod, node)
+                    self.assumed.pop(key, None)
+                    self._track(key, pod)
+                    return
         if st is not None:
             self._node(st[1]).remove_pod(key)
         self._node(node).add_pod(key, pod, PodInfo(pod))
