@@ -16,6 +16,7 @@ from collections import deque
 
 from ..api import codec
 from ..api.labels import parse as parse_labels, parse_field_selector
+from ..api.sharding import shard_matches
 
 log = logging.getLogger("cacher")
 
@@ -93,7 +94,7 @@ FIELD_FUNCS = {"pods": pod_fields, "nodes": node_fields}
 
 class Watcher:
     __slots__ = ("writer", "namespace", "label_sel", "field_sel", "closed", "index_value", "cache", "bookmarks",
-                 "_pending", "_loop", "min_rev")
+                 "_pending", "_loop", "min_rev", "shard")
 
     def __init__(self, cache, writer, namespace, label_sel, field_sel, index_value):
         self.cache = cache
@@ -106,6 +107,7 @@ class Watcher:
         self.field_sel = field_sel
         self.index_value = index_value
         self.closed = False
+        self.shard = None      # (index, count): scheduler-shard selection (api/sharding.py)
         self.bookmarks = False
         self._pending = None   # events coalesced until the end of this loop iteration
         self._loop = None
@@ -116,6 +118,8 @@ class Watcher:
         if self.label_sel is not None and not self.label_sel.matches(e.labels):
             return False
         if self.field_sel is not None and not self.field_sel.matches(e.fields):
+            return False
+        if self.shard is not None and not shard_matches(e.fields, e.labels, *self.shard):
             return False
         return True
 
@@ -250,11 +254,13 @@ class ResourceCache:
                     w.send(enc(DELETED))
 
     # -- watchers ---------------------------------------------------------
-    def add_watcher(self, writer, namespace, label_selector, field_selector, from_rev: int | None, send_initial: bool):
+    def add_watcher(self, writer, namespace, label_selector, field_selector, from_rev: int | None, send_initial: bool,
+                    shard=None):
         ls = parse_labels(label_selector) if label_selector else None
         fs = parse_field_selector(field_selector) if field_selector else None
         idx = fs.requires("spec.nodeName") if (fs is not None and self.resource == "pods") else None
         w = Watcher(self, writer, namespace, ls, fs, idx)
+        w.shard = shard
         if from_rev is not None and not send_initial:
             w.min_rev = from_rev
         # initial state / replay (synchronous, so no event can interleave)

@@ -39,6 +39,7 @@ import time
 from ..api import codec, core, meta as m
 from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
 from ..api.meta import parse_rfc3339, fast_copy, now_rfc3339
+from ..api.sharding import QUERY_PARAM, SHARD_OFFSET_LABEL, parse_shard, shard_matches
 from ..storage import wire
 from ..storage.mvcc import CompactedError, MVCCStore
 from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
@@ -1407,8 +1408,19 @@ class APIServer:
         ls = parse_labels(q.get("labelSelector")) if q.get("labelSelector") else None
         fsel = self._hide_uninitialized(q, q.get("fieldSelector"))
         fs = parse_field_selector(fsel) if fsel else None
-        entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
+        entries = self._shard_filter(q, self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs))
         return self._list_response(q, ri, entries, str(self.revision))
+
+    @staticmethod
+    def _shard(q):
+        v = q.get(QUERY_PARAM)
+        return parse_shard(v) if v else None
+
+    def _shard_filter(self, q, entries):
+        sh = self._shard(q)
+        if sh is None:
+            return entries
+        return [e for e in entries if shard_matches(e.fields, e.labels, *sh)]
 
     async def _list_store(self, req, ri, ns):
         q = req.query
@@ -1416,7 +1428,7 @@ class APIServer:
         fsel = self._hide_uninitialized(q, q.get("fieldSelector"))
         fs = parse_field_selector(fsel) if fsel else None
         entries, rev = await self._store_entries(ri, ns, ls, fs)
-        return self._list_response(q, ri, entries, str(rev))
+        return self._list_response(q, ri, self._shard_filter(q, entries), str(rev))
 
     def _list_response(self, q, ri, entries, rv):
         limit = int(q.get("limit") or 0)
@@ -1440,7 +1452,7 @@ class APIServer:
             ri.list_kind.encode(), ri.group_version.encode(), md.encode()) + b",".join(e.raw for e in entries) + b"]}"
         return Response(200, body)
 
-    def _fanout_spec(self, req, ri, ns, label_selector, field_selector):
+    def _fanout_spec(self, req, ri, ns, label_selector, field_selector, shard=None):
         """Requirements for kamd-etcd's watch fan-out, or None when this watch must stay here:
         TLS connections (the TLS session lives in this process), encrypted or non-JSON storage
         (the store cannot read the index frame), quantity comparisons in label selectors."""
@@ -1458,9 +1470,11 @@ class APIServer:
         if field_selector:
             for k, op, v in parse_field_selector(field_selector).terms:
                 reqs.append((1, "!=" if op == "!=" else "=", k, [v]))
+        if shard is not None:
+            reqs.append((0, "shard", SHARD_OFFSET_LABEL, [shard[1], shard[0]]))
         return reqs
 
-    def _watch_store(self, ri, ns, label_selector, field_selector, rv, timeout):
+    def _watch_store(self, ri, ns, label_selector, field_selector, rv, timeout, shard=None):
         """Watch of an uncached resource that the store's fan-out cannot serve (a TLS client,
         quantity label selectors): a store watch of its own, filtered here. Without the previous
         object state, a change that leaves the selector is reported as DELETED even if the
@@ -1472,7 +1486,8 @@ class APIServer:
         server = self
 
         def ok(e):
-            return (ls is None or ls.matches(e.labels)) and (fs is None or fs.matches(e.fields))
+            return (ls is None or ls.matches(e.labels)) and (fs is None or fs.matches(e.fields)) and \
+                (shard is None or shard_matches(e.fields, e.labels, *shard))
 
         async def run(writer):
             st = await RemoteStore(server.remote_address).connect()
@@ -1534,7 +1549,8 @@ class APIServer:
             fsel = (fsel + "," if fsel else "") + f"metadata.name={name}"
         fsel = self._hide_uninitialized(q, fsel)
         timeout = float(q.get("timeoutSeconds") or 0) or None
-        reqs = self._fanout_spec(req, ri, ns, q.get("labelSelector"), fsel)
+        shard = self._shard(q)
+        reqs = self._fanout_spec(req, ri, ns, q.get("labelSelector"), fsel, shard)
         if reqs is not None:
             # shared-store mode: the store streams this watch itself (C++ fan-out)
             send_initial = not rv or rv == "0"
@@ -1542,7 +1558,7 @@ class APIServer:
             self.m_fanout.labels(ri.plural).inc()
             return HandoffResponse(lambda fd: self.fanout.handoff(fd, msg))
         if ri.plural in self.uncached:
-            return self._watch_store(ri, ns, q.get("labelSelector"), fsel, rv, timeout)
+            return self._watch_store(ri, ns, q.get("labelSelector"), fsel, rv, timeout, shard)
         cache = self.caches[ri.plural]
         send_initial = not rv or rv == "0"
         from_rev = int(rv) if rv and rv != "0" else None
@@ -1553,7 +1569,7 @@ class APIServer:
 
         async def run(writer):
             try:
-                w = cache.add_watcher(writer, ns, q.get("labelSelector"), fsel, from_rev, send_initial)
+                w = cache.add_watcher(writer, ns, q.get("labelSelector"), fsel, from_rev, send_initial, shard)
             except GoneError as e:
                 writer.write(codec.dumpb({"type": "ERROR", "object": m.status_obj(410, "Expired", str(e))}) + b"\n")
                 return

@@ -57,6 +57,21 @@ class _FakeWatch:
             raise StopAsyncIteration
         return ev
 
+    async def batches(self):
+        """Same contract as the real stream: lists of events (everything queued so far)."""
+        while True:
+            ev = await self.q.get()
+            if ev is None:
+                return
+            out = [ev]
+            while not self.q.empty():
+                nxt = self.q.get_nowait()
+                if nxt is None:
+                    yield out
+                    return
+                out.append(nxt)
+            yield out
+
     def close(self):
         self._on_close(self.q)
         self.q.put_nowait(None)
@@ -161,7 +176,7 @@ class FakeClient:
         return {"kind": (ri.kind if ri else "") + "List", "apiVersion": ri.group_version if ri else "v1",
                 "metadata": {"resourceVersion": str(next(self.rv))}, "items": items}
 
-    async def list_all(self, resource, namespace=None, label_selector=None, field_selector=None, chunk=500):
+    async def list_all(self, resource, namespace=None, label_selector=None, field_selector=None, chunk=500, **_kw):
         lst = await self.list(resource, namespace, label_selector, field_selector)
         return lst["items"], lst["metadata"]["resourceVersion"]
 
@@ -246,7 +261,7 @@ class FakeClient:
         return await self.delete("pods", name, namespace)
 
     async def watch(self, resource, namespace=None, resource_version=None, label_selector=None, field_selector=None,
-                    timeout_seconds=None):
+                    timeout_seconds=None, **_kw):
         self._react(Action("watch", resource, namespace))
         q: asyncio.Queue = asyncio.Queue()
         ent = (namespace, q)

@@ -81,8 +81,9 @@ class Indexer:
 
 class Informer:
     def __init__(self, client, resource, namespace=None, label_selector=None, field_selector=None,
-                 indexers=None, watch_timeout=300):
+                 indexers=None, watch_timeout=300, extra_query=None):
         self.client = client
+        self.extra_query = extra_query
         self.resource = resource
         self.namespace = namespace
         self.label_selector = label_selector
@@ -126,7 +127,8 @@ class Informer:
                 log.exception("informer handler for %s failed", self.resource)
 
     async def _list(self):
-        items, rv = await self.client.list_all(self.resource, self.namespace, self.label_selector, self.field_selector)
+        items, rv = await self.client.list_all(self.resource, self.namespace, self.label_selector, self.field_selector,
+                                               extra=self.extra_query)
         seen = set()
         for o in items:
             k = key_func(o)
@@ -162,7 +164,7 @@ class Informer:
                 if self.rv is None:
                     await self._list()
                 st = await self.client.watch(self.resource, self.namespace, self.rv, self.label_selector,
-                                             self.field_selector, self.watch_timeout)
+                                             self.field_selector, self.watch_timeout, extra=self.extra_query)
                 self._stream = st
                 backoff = 0.05
                 async for evs in st.batches():

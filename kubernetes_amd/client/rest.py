@@ -105,8 +105,8 @@ class Client:
         return await self._do("GET", resource_path(resource, namespace, name, subresource))
 
     async def list(self, resource, namespace=None, label_selector=None, field_selector=None, limit=0,
-                   cont=None, resource_version=None):
-        q = {}
+                   cont=None, resource_version=None, extra=None):
+        q = dict(extra or {})
         if label_selector:
             q["labelSelector"] = label_selector
         if field_selector:
@@ -122,10 +122,12 @@ class Client:
             path += "?" + urlencode(q)
         return await self._do("GET", path)
 
-    async def list_all(self, resource, namespace=None, label_selector=None, field_selector=None, chunk=500):
+    async def list_all(self, resource, namespace=None, label_selector=None, field_selector=None, chunk=500,
+                       extra=None):
         out, cont, rv = [], None, None
         while True:
-            lst = await self.list(resource, namespace, label_selector, field_selector, limit=chunk, cont=cont)
+            lst = await self.list(resource, namespace, label_selector, field_selector, limit=chunk, cont=cont,
+                                  extra=extra)
             out.extend(lst.get("items") or [])
             rv = lst["metadata"].get("resourceVersion")
             cont = lst["metadata"].get("continue")
@@ -184,9 +186,11 @@ class Client:
         return await self._do("POST", resource_path("pods", namespace, name, "eviction"), body)
 
     async def watch(self, resource, namespace=None, resource_version=None, label_selector=None,
-                    field_selector=None, timeout_seconds=None):
-        """Async iterator of (event_type, object). Closes when the server ends the stream."""
-        q = {"watch": "true"}
+                    field_selector=None, timeout_seconds=None, extra=None):
+        """Async iterator of (event_type, object). Closes when the server ends the stream.
+        `extra`: additional query parameters (e.g. {"kamdShard": "i/n"})."""
+        q = dict(extra or {})
+        q["watch"] = "true"
         if resource_version is not None:
             q["resourceVersion"] = str(resource_version)
         if label_selector:

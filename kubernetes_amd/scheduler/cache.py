@@ -406,3 +406,14 @@ class SchedulerCache:
 
     def node_list(self):
         return [ni for ni in self.nodes.values() if ni.node is not None]
+
+    def drop_node(self, name):
+        """Forget a node and every pod accounted on it (a partitioned scheduler shard that no
+        longer owns the node)."""
+        ni = self.nodes.pop(name, None)
+        if ni is None:
+            return
+        for key in list(ni.pods):
+            self.pod_states.pop(key, None)
+            self.assumed.pop(key, None)
+            self.anti_pods.pop(key, None)

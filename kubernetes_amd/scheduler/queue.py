@@ -87,6 +87,9 @@ class SchedulingQueue:
         self.backoff.forget(key)
         self.conflict_backoff.forget(key)
 
+    def unschedulable_pods(self):
+        return [ent[0] for ent in self.unschedulable.values()]
+
     def add_unschedulable(self, pod):
         key = ns_name(pod)
         if key in self.active:

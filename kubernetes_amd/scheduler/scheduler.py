@@ -8,12 +8,19 @@ Parity: `plugin/pkg/scheduler/scheduler.go:170-497` (`Run`, `scheduleOne`, `sche
 `Scheduled` / `FailedScheduling` and the metrics of `plugin/pkg/scheduler/metrics/metrics.go:33-50`.
 
 Scale-out (MI355X clusters with many nodes): `shard_count > 1` runs several scheduler
-processes in parallel with optimistic concurrency (Omega-style shared state). Each shard owns
-the pods whose `namespace/name` hashes to it, keeps the FULL cluster view from the informers,
-and prefers the nodes that hash to it, so shards rarely compete for one node. When two shards
-still pick the same GPU, the API server's device-claim guard rejects the second bind (409);
-that shard forgets its assumption and retries after a short conflict backoff, by which time
-the winner's binding has reached its cache.
+processes in parallel over a PARTITION of the cluster, so no shard processes every pod event:
+  * nodes: shard i owns every node whose index in the sorted node-name list is i mod n, and
+    keeps pod accounting only for those, fed by one `spec.nodeName=<node>` watch per owned
+    node (served by the store's node-indexed fan-out);
+  * pods: shard i lists/watches only the unassigned pods selected by `?kamdShard=i/n`
+    ((crc32(namespace/name) + offset label) mod n, api/sharding.py), evaluated server side;
+  * a pod that fits none of the shard's nodes is handed to the next shard by bumping its
+    `scheduler.kamd.io/shard-offset` label (`scheduler.kamd.io/shard-hops` counts the hops);
+    after a full round it is reported unschedulable (and preemption is tried) on the last shard,
+    and it is offered to the next shard again every `rehandoff_period` seconds.
+Per-shard work is O(cluster pods / n). Trade-off: inter-pod (anti-)affinity is evaluated
+against the pods on the shard's own nodes. GPU double assignment stays impossible: the API
+server's device-claim guard rejects a conflicting bind (409) and the shard retries.
 
 Fix: `assume()` writes the device binding into the assumed pod's
 `spec.extendedResources[].assigned` before `AssumePod`, so the cache reserves those devices
@@ -28,6 +35,7 @@ import zlib
 
 from ..api import core
 from ..api.meta import fast_copy, ns_name, now_rfc3339
+from ..api.sharding import QUERY_PARAM, SHARD_OFFSET_LABEL, offset_of
 from ..client.events import EventRecorder
 from ..client.informer import Informer
 from ..client.rest import APIStatusError, is_not_found
@@ -43,20 +51,26 @@ from ..utils.tasks import spawn
 log = logging.getLogger("scheduler")
 
 DEFAULT_SCHEDULER = "default-scheduler"
+SHARD_HOPS_ANNOTATION = "scheduler.kamd.io/shard-hops"
 
 
 class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
-                 update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True):
+                 update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True,
+                 rehandoff_period=10.0):
         self.client = client
         self.name = scheduler_name
         self.cache = SchedulerCache()
         self.queue = SchedulingQueue()
         self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
         self.shard_index, self.shard_count = shard_index, shard_count
-        if shard_count > 1:
-            self.algo.prefer = lambda node: shard_of(node, shard_count) == shard_index
+        self.partitioned = shard_count > 1
+        self.rehandoff_period = rehandoff_period
+        self.all_nodes: dict[str, dict] = {}          # partitioned: every node object
+        self.owned: dict[str, Informer] = {}          # partitioned: owned node -> its pod informer
+        self._owned_ready: set = set()
+        self.handoffs = 0
         self.conflicts = 0
         self.recorder = EventRecorder(client, scheduler_name, enabled=emit_events)
         self.update_unschedulable_status = update_unschedulable_status
@@ -75,7 +89,13 @@ class Scheduler:
         self._tasks = []
         self._binds = set()
         self.http = None
-        self.pod_informer = Informer(client, "pods", field_selector="status.phase!=Succeeded,status.phase!=Failed")
+        if self.partitioned:
+            # only this shard's unassigned pods; assigned pods come from the per-node informers
+            self.pod_informer = Informer(client, "pods",
+                                         field_selector="spec.nodeName=,status.phase!=Succeeded,status.phase!=Failed",
+                                         extra_query={QUERY_PARAM: f"{shard_index}/{shard_count}"})
+        else:
+            self.pod_informer = Informer(client, "pods", field_selector="status.phase!=Succeeded,status.phase!=Failed")
         self.node_informer = Informer(client, "nodes")
         self.pvc_informer = Informer(client, "persistentvolumeclaims")
         self.pv_informer = Informer(client, "persistentvolumes")
@@ -83,12 +103,113 @@ class Scheduler:
 
     # -- informer handlers -------------------------------------------------
     def _responsible(self, pod):
-        if (pod.get("spec") or {}).get("schedulerName", DEFAULT_SCHEDULER) != self.name:
+        # partitioned shards get only their pods from the server (kamdShard selection)
+        return (pod.get("spec") or {}).get("schedulerName", DEFAULT_SCHEDULER) == self.name
+
+    # -- partitioned shards: unassigned pods + owned nodes --------------------------
+    def _on_unassigned_add(self, pod):
+        if not (pod.get("spec") or {}).get("nodeName") and self._responsible(pod) \
+                and not pod["metadata"].get("deletionTimestamp"):
+            self.queue.add(pod)
+
+    def _on_unassigned_update(self, old, new):
+        if not self._responsible(new):
+            return
+        if new["metadata"].get("deletionTimestamp") or (new.get("spec") or {}).get("nodeName"):
+            self.queue.delete(new)
+        else:
+            self.queue.update(old, new)
+
+    def _on_unassigned_delete(self, pod):
+        # bound (now on some node's informer), deleted, or handed to another shard
+        self.queue.delete(pod)
+
+    def _on_owned_pod_delete(self, pod):
+        self.cache.remove_pod(pod)
+        self.queue.move_all_to_active()   # capacity was freed
+
+    def _owns(self, names):
+        return {n for i, n in enumerate(sorted(names)) if i % self.shard_count == self.shard_index}
+
+    def _rebalance(self):
+        want = self._owns(self.all_nodes)
+        for name in [n for n in self.owned if n not in want]:
+            self.owned.pop(name).stop()
+            self._owned_ready.discard(name)
+            self.cache.drop_node(name)
+        for name in want:
+            if name in self.owned:
+                continue
+            inf = Informer(self.client, "pods", field_selector=f"spec.nodeName={name},status.phase!=Succeeded,"
+                                                               "status.phase!=Failed")
+            inf.add_handler(self.cache.add_pod, lambda old, new: self.cache.add_pod(new), self._on_owned_pod_delete)
+            self.owned[name] = inf
+            inf.start()
+            spawn(self._node_ready(name, inf))
+
+    async def _node_ready(self, name, inf):
+        """A node becomes schedulable for this shard once its pods are known."""
+        while not inf.has_synced():
+            if self.owned.get(name) is not inf:
+                return
+            await asyncio.sleep(0.01)
+        if self.owned.get(name) is inf and name in self.all_nodes:
+            self._owned_ready.add(name)
+            self.cache.add_node(self.all_nodes[name])
+            self.queue.move_all_to_active()
+
+    def _on_part_node_add(self, node):
+        name = node["metadata"]["name"]
+        known = name in self.all_nodes
+        self.all_nodes[name] = node
+        if not known:
+            self._rebalance()
+        elif name in self._owned_ready:
+            self.cache.add_node(node)
+
+    def _on_part_node_update(self, old, new):
+        name = new["metadata"]["name"]
+        self.all_nodes[name] = new
+        if name in self._owned_ready:
+            self.cache.add_node(new)
+            if _node_capacity_changed(old, new):
+                self.queue.move_all_to_active()
+
+    def _on_part_node_delete(self, node):
+        if self.all_nodes.pop(node["metadata"]["name"], None) is not None:
+            self._rebalance()
+
+    def _handoff(self, pod, msg):
+        """Pass a pod this shard cannot place to the next shard; False once it has been
+        through every shard (then it is unschedulable here)."""
+        md = pod["metadata"]
+        hops = int((md.get("annotations") or {}).get(SHARD_HOPS_ANNOTATION, "0") or 0)
+        if hops >= self.shard_count - 1:
             return False
-        if self.shard_count > 1:
-            md = pod["metadata"]
-            return shard_of(f"{md.get('namespace', '')}/{md['name']}", self.shard_count) == self.shard_index
+        self.queue.delete(pod)
+        self.handoffs += 1
+        spawn(self._patch_shard(pod, offset_of(md.get("labels")) + 1, hops + 1))
         return True
+
+    async def _patch_shard(self, pod, offset, hops):
+        md = pod["metadata"]
+        try:
+            await self.client.patch("pods", md["name"], {"metadata": {
+                "labels": {SHARD_OFFSET_LABEL: str(offset)},
+                "annotations": {SHARD_HOPS_ANNOTATION: str(hops)}}}, md.get("namespace"))
+        except APIStatusError as e:
+            if not is_not_found(e):
+                log.warning("handing %s to the next shard failed: %s", ns_name(pod), e)
+                self.queue.add_backoff(pod)
+
+    async def _rehandoff_loop(self):
+        """Unschedulable pods are offered to the next shard again (its capacity may have freed)."""
+        while True:
+            await asyncio.sleep(self.rehandoff_period)
+            for pod in list(self.queue.unschedulable_pods()):
+                self.queue.delete(pod)
+                self.handoffs += 1
+                spawn(self._patch_shard(pod, offset_of(pod["metadata"].get("labels")) + 1, 0))
 
     def _on_pod_add(self, pod):
         if (pod.get("spec") or {}).get("nodeName"):
@@ -158,13 +279,23 @@ class Scheduler:
     # -- scheduling loop ---------------------------------------------------------
     async def run(self, metrics_port=None):
         self.recorder.start()
-        self.node_informer.add_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
-        self.pod_informer.add_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
+        if self.partitioned:
+            self.node_informer.add_handler(self._on_part_node_add, self._on_part_node_update, self._on_part_node_delete)
+            self.pod_informer.add_handler(self._on_unassigned_add, self._on_unassigned_update,
+                                          self._on_unassigned_delete)
+            self._tasks.append(asyncio.ensure_future(self._rehandoff_loop()))
+        else:
+            self.node_informer.add_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
+            self.pod_informer.add_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
         self._volume_handlers()
         for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
             inf.start()
         self.node_informer.start()
         await self.node_informer.wait_synced(60)
+        if self.partitioned:
+            t = time.monotonic()
+            while len(self._owned_ready) < len(self.owned) and time.monotonic() - t < 60:
+                await asyncio.sleep(0.01)
         for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
             await inf.wait_synced(60)
         self.pod_informer.start()
@@ -199,6 +330,8 @@ class Scheduler:
             tr.step(f"Computing predicates, device allocation and priorities -> {host}")
             tr.log_if_long(0.1, log)
         except FitError as e:
+            if self.partitioned and self._handoff(pod, str(e)):
+                return None
             self.m_attempts.labels("unschedulable").inc()
             self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
             self.queue.add_unschedulable(pod)
@@ -346,6 +479,8 @@ class Scheduler:
             t.cancel()
         self.pod_informer.stop()
         self.node_informer.stop()
+        for inf in self.owned.values():
+            inf.stop()
         for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
             inf.stop()
         self.recorder.stop()

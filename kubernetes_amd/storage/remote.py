@@ -203,7 +203,8 @@ class FanoutClient:
     watch stream itself (see native/store/mvcc_store.cc "Watch fan-out")."""
 
     LABEL, FIELD = 0, 1
-    OPS = {"=": 0, "==": 0, "!=": 1, "in": 2, "notin": 3, "exists": 4, "!": 5}
+    # "shard": key = the offset label, values = [count, index] (api/sharding.py)
+    OPS = {"=": 0, "==": 0, "!=": 1, "in": 2, "notin": 3, "exists": 4, "!": 5, "shard": 6}
 
     def __init__(self, path):
         self.path = path

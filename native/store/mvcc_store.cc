@@ -31,6 +31,7 @@
 //   kv = i64 create_rev i64 mod_rev i64 version u32 klen key u32 vlen val
 //   A kind-3 delete carries the "tombstone" (final object state) reported in the delete event
 //   instead of the last stored value; it is not stored.
+#include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -534,12 +535,52 @@ static Index parse_index(const std::string& v) {
   return ix;
 }
 
+static uint32_t crc32_ieee(const std::string& s) {   // zlib.crc32
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (unsigned char ch : s) c = table[(c ^ ch) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+// scheduler-shard selection (kubernetes_amd/api/sharding.py): (crc32("ns/name") + offset label) % n == i
+static bool shard_match(const Index& ix, const std::string& offset_label, int64_t n, int64_t i) {
+  if (n < 1) return false;
+  auto ns = ix.fields.find("metadata.namespace");
+  auto nm = ix.fields.find("metadata.name");
+  std::string key = (ns == ix.fields.end() ? std::string() : ns->second) + "/" +
+                    (nm == ix.fields.end() ? std::string() : nm->second);
+  int64_t off = 0;
+  auto ol = ix.labels.find(offset_label);
+  if (ol != ix.labels.end() && !ol->second.empty()) {
+    const char* b = ol->second.c_str();
+    char* e = nullptr;
+    errno = 0;
+    long long v = strtoll(b, &e, 10);
+    bool ok = errno == 0 && e && *e == 0 && !isspace((unsigned char)b[0]) && v >= -(1LL << 31) && v <= (1LL << 31);
+    off = ok ? v : 0;
+  }
+  int64_t h = ((int64_t)crc32_ieee(key) + off) % n;
+  if (h < 0) h += n;
+  return h == i;
+}
+
 struct Requirement {
   uint8_t target;  // 0 label, 1 field
-  uint8_t op;      // 0 =, 1 !=, 2 in, 3 notin, 4 exists, 5 !exists
+  uint8_t op;      // 0 =, 1 !=, 2 in, 3 notin, 4 exists, 5 !exists, 6 shard (key = offset label, vals = [n, i])
   std::string key;
   std::vector<std::string> vals;
   bool matches(const Index& ix) const {
+    if (op == 6)
+      return vals.size() == 2 && shard_match(ix, key, atoll(vals[0].c_str()), atoll(vals[1].c_str()));
     const auto& m = target == 0 ? ix.labels : ix.fields;
     auto it = m.find(key);
     // a field that is absent reads as "" (fields.Set semantics); labels keep presence

@@ -378,3 +378,35 @@ def test_uncached_pods_and_events_read_from_store(run, store):
         finally:
             await _close(servers, [a, b])
     run(main())
+
+
+def test_shard_selection_native_matches_python(run, store):
+    """`?kamdShard=i/n`: kamd-etcd's native fan-out and the API server's list filter select the
+    same pods (zlib CRC-32 of namespace/name + the offset label, malformed offsets read as 0)."""
+    from kubernetes_amd.api.sharding import SHARD_OFFSET_LABEL
+
+    async def main():
+        servers, (a,) = await _workers(store, 1)
+        try:
+            offs = ["", "1", "12", "x", "99999999999", "7"]
+            for i in range(30):
+                md = {"name": f"s{i}", "namespace": "default"}
+                if offs[i % len(offs)]:
+                    md["labels"] = {SHARD_OFFSET_LABEL: offs[i % len(offs)]}
+                await a.create("pods", dict(gpu_pod(f"s{i}"), metadata=md))
+            seen_all = []
+            for k in range(3):
+                listed = {p["metadata"]["name"] for p in
+                          (await a.list("pods", "default", extra={"kamdShard": f"{k}/3"}))["items"]}
+                w = await a.watch("pods", "default", "0", timeout_seconds=1, extra={"kamdShard": f"{k}/3"})
+                watched = {o["metadata"]["name"] async for _, o in w}
+                assert listed == watched and listed
+                seen_all += listed
+            assert sorted(seen_all) == sorted(f"s{i}" for i in range(30))     # a partition
+            assert servers[0].m_fanout.value("pods") >= 3
+            with pytest.raises(APIStatusError) as ei:
+                await a.list("pods", "default", extra={"kamdShard": "3/3"})
+            assert ei.value.code == 400
+        finally:
+            await _close(servers, [a])
+    run(main())

@@ -235,3 +235,82 @@ def test_equivalence_cache_matches_uncached_decisions():
                 c.assume_pod(ap)
             live.append(ap)
     assert scheds[0].ecache_hits > 0
+
+
+def _sharded_run(run, shared):
+    """Two partitioned scheduler shards: each sees only its own unassigned pods and its own
+    nodes' pods; pods that do not fit are handed to the other shard; nothing is double-assigned."""
+    from kubernetes_amd.api.sharding import shard_of_key
+
+    async def main():
+        store = None
+        if shared:
+            from kubernetes_amd.storage.remote import StoreServer
+            store = StoreServer()
+            s = APIServer(store=store.start())
+        else:
+            s = APIServer()
+        port = await s.start()
+        c = Client(f"http://127.0.0.1:{port}")
+        for name, n in (("a-node", 8), ("b-node", 1)):
+            await c.create("nodes", node(name, [gpu_dev(i) for i in range(n)]))
+            await c.update_status("nodes", node(name, [gpu_dev(i) for i in range(n)]) | {"metadata": (await c.get("nodes", name))["metadata"]})
+        scheds = [Scheduler(Client(f"http://127.0.0.1:{port}"), shard_index=i, shard_count=2, rehandoff_period=0.3)
+                  for i in range(2)]
+        tasks = [asyncio.ensure_future(x.run()) for x in scheds]
+
+        def pod(name):
+            return {"metadata": {"name": name, "namespace": "default"},
+                    "spec": {"containers": [{"name": "c", "image": "x", "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
+        names = [f"p{i}" for i in range(9)]
+        assert sum(shard_of_key(f"default/{n}", 2) == 1 for n in names) >= 2   # b-node (1 GPU) overflows
+        for n in names:
+            await c.create("pods", pod(n))
+
+        async def bound():
+            return [p for p in (await c.list("pods", "default"))["items"] if p["spec"].get("nodeName")]
+        for _ in range(300):
+            b = await bound()
+            if len(b) == 9:
+                break
+            await asyncio.sleep(0.02)
+        ids = [(p["spec"]["nodeName"], i) for p in b for i in p["spec"]["extendedResources"][0]["assigned"]]
+        assert len(b) == 9 and len(set(ids)) == 9
+        assert sum(x.handoffs for x in scheds) >= 1
+        assert set(scheds[0].owned) == {"a-node"} and set(scheds[1].owned) == {"b-node"}
+        assert all(n in scheds[0].cache.nodes for n in ("a-node",)) and "b-node" not in scheds[0].cache.nodes
+        # cluster full: the 10th pod goes round both shards and is reported unschedulable
+        await c.create("pods", pod("late"))
+        for _ in range(300):
+            evs = (await c.list("events", "default"))["items"]
+            if any(e["reason"] == "FailedScheduling" and e["involvedObject"]["name"] == "late" for e in evs):
+                break
+            await asyncio.sleep(0.02)
+        else:
+            raise AssertionError("no FailedScheduling for the overflow pod")
+        # capacity frees on either node: the pod is picked up (same shard or re-offered)
+        victim = next(p for p in b if p["spec"]["nodeName"] == "b-node")
+        await c.delete("pods", victim["metadata"]["name"], "default", grace_period=0)
+        for _ in range(300):
+            late = await c.get("pods", "late", "default")
+            if late["spec"].get("nodeName"):
+                break
+            await asyncio.sleep(0.02)
+        assert late["spec"].get("nodeName") == "b-node"
+        for t in tasks:
+            t.cancel()
+        for x in scheds:
+            await x.stop()
+        await c.close()
+        await s.stop()
+        if store is not None:
+            store.stop()
+    run(main())
+
+
+def test_partitioned_scheduler_shards_embedded(run):
+    _sharded_run(run, shared=False)
+
+
+def test_partitioned_scheduler_shards_shared_store_fanout(run):
+    _sharded_run(run, shared=True)
