@@ -70,10 +70,10 @@ def cpu_budget():
 def control_plane_shape(world, workers=0, shards=0):
     """API server workers and scheduler shards for `world` ranks (0 = auto).
 
-    Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep, profiles/r2_scale): with one rank the
-    single API server + scheduler are fastest; from 2 ranks on, parallel API server workers over
-    the native store (watches served by its C++ fan-out) and 2 scheduler shards, 4 workers from
-    4 ranks on.
+    Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep, profiles/r2_scale, r2_partitioned): with
+    one rank the single API server + scheduler are fastest; from 2 ranks on, parallel API server
+    workers over the native store (watches served by its C++ fan-out) and as many partitioned
+    scheduler shards (N=4: w=4 s=4 3184 pods/s vs w=4 s=2 2727).
     On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — one API
     server worker and one scheduler shard per rank, up to 8 each — so per-rank work (weak
     scaling) is met by per-rank control-plane capacity instead of a fixed-size control plane."""
@@ -93,7 +93,7 @@ def control_plane_shape(world, workers=0, shards=0):
         elif big:
             shards = min(8, world, max(1, spare // 6))
         else:
-            shards = 2
+            shards = 2 if world < 4 else 4
     return workers, shards
 
 
@@ -295,6 +295,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         off += r["cycle_s"]
     stats = {"elapsed": elapsed, "lat": lat, "pods": sum(r["pods"] for r in results),
              "to_running": [r["to_running_s"] for r in results], "cycle": [r["cycle_s"] for r in results],
+             "phases": {k: [r[k] for r in results] for k in ("create_s", "to_running_s", "delete_issued_s", "cycle_s")},
              "payload_runs": (psrv.runs if psrv else sum(getattr(k.runtime, "payload_runs", 0) for k in hollow.nodes)
                               if hollow or psrv else 0),
              "payload_failures": (psrv.failures if psrv else sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes)
@@ -424,6 +425,10 @@ def main():
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
         "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
         "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],
+        # mean over steps of the slowest rank: pods created / all Running / deletes issued / all gone
+        "step_phases_ms": {k: round(1000 * sum(max(s["phases"][k][i] for s in allstats) for i in range(args.steps))
+                                    / max(1, args.steps), 2)
+                           for k in ("create_s", "to_running_s", "delete_issued_s", "cycle_s")},
         "sched_rate_avg_pods_per_s": round(sum(s["sched_rates"][0] for s in allstats), 1),
         "vs_scheduler_perf_warn_threshold": round(value / BASELINE_SCHED_WARN_PODS_PER_S, 2),
         "payload_runs": sum(s["payload_runs"] for s in allstats),

@@ -136,12 +136,14 @@ class DensityRunner:
                         raise
 
         await asyncio.gather(*(delete(n) for n in names))
+        t_deleted = time.monotonic()
         await self._wait(lambda: all(n in self.gone for n in names), timeout, names, "gone")
         t_gone = time.monotonic()
         lat = [self.running[n] - self.created[n] for n in names]
         sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)
         return {"pods": len(names), "names": names, "create_s": t_created - t0, "to_running_s": t_running - t0,
-                "cycle_s": t_gone - t0, "latencies": lat, "scheduled_times": [s - t0 for s in sched]}
+                "delete_issued_s": t_deleted - t0, "cycle_s": t_gone - t0, "latencies": lat,
+                "scheduled_times": [s - t0 for s in sched]}
 
     async def stop(self):
         if self._stream:

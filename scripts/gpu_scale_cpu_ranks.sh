@@ -8,7 +8,7 @@ summ() { python - "$1" "$2" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][0])
 c = d["config"]
-print(f"{sys.argv[2]}: {d['value']} pods/s p50={d['p50_startup_ms']} p99={d['p99_startup_ms']} step={d['ms_per_step']}ms w={c['apiserver_workers']} s={c['scheduler_shards']} hp={c.get('hollow_procs_per_rank')} cpu/pod={d['cpu_ms_per_pod']}")
+print(f"{sys.argv[2]}: {d['value']} pods/s p50={d['p50_startup_ms']} p99={d['p99_startup_ms']} step={d['ms_per_step']}ms w={c['apiserver_workers']} s={c['scheduler_shards']} hp={c.get('hollow_procs_per_rank')} cpu/pod={d['cpu_ms_per_pod']} phases={d.get('step_phases_ms')}")
 PY
 }
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/scale/n1.log 2>&1 || { tail -30 gpurun_out/scale/n1.log; exit 1; }
