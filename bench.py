@@ -276,7 +276,8 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         await abarrier()
     results = []
     await abarrier()
-    cp0 = _cp_cpu(cp_procs)
+    hollow_pids = [("hollow", p.pid) for p in hprocs]
+    cp0 = _cp_cpu(list(cp_procs) + hollow_pids)
     my0 = time.process_time()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -286,7 +287,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     await abarrier()
     elapsed = time.perf_counter() - t0
     my_cpu = time.process_time() - my0
-    cp1 = _cp_cpu(cp_procs)
+    cp1 = _cp_cpu(list(cp_procs) + hollow_pids)
     lat = [x for r in results for x in r["latencies"]]
     sched_times = []
     off = 0.0
@@ -438,7 +439,7 @@ def main():
         "cpu_ms_per_pod": {k: round(v * 1000 / max(pods, 1), 3) for k, v in
                            dict(sum_ranks=sum(s["cpu_s"] for s in allstats),
                                 **{c: sum(s["cp_cpu_s"].get(c, 0.0) for s in allstats)
-                                   for c in ("apiserver", "scheduler", "store")}).items()},
+                                   for c in ("apiserver", "scheduler", "store", "hollow")}).items()},
     }
     print(json.dumps(out), flush=True)
 

@@ -90,6 +90,10 @@ class SchedulingQueue:
     def unschedulable_pods(self):
         return [ent[0] for ent in self.unschedulable.values()]
 
+    def unschedulable_since(self):
+        """(pod, monotonic time it was marked unschedulable)."""
+        return [(ent[0], ent[2]) for ent in self.unschedulable.values()]
+
     def add_unschedulable(self, pod):
         key = ns_name(pod)
         if key in self.active:

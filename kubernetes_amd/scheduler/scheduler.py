@@ -17,7 +17,8 @@ processes in parallel over a PARTITION of the cluster, so no shard processes eve
   * a pod that fits none of the shard's nodes is handed to the next shard by bumping its
     `scheduler.kamd.io/shard-offset` label (`scheduler.kamd.io/shard-hops` counts the hops);
     after a full round it is reported unschedulable (and preemption is tried) on the last shard,
-    and it is offered to the next shard again every `rehandoff_period` seconds.
+    and it is offered to the next shard again once it has waited `rehandoff_period` seconds (the
+    capacity it needs may have freed on another shard's nodes).
 Per-shard work is O(cluster pods / n). Trade-off: inter-pod (anti-)affinity is evaluated
 against the pods on the shard's own nodes. GPU double assignment stays impossible: the API
 server's device-claim guard rejects a conflicting bind (409) and the shard retries.
@@ -58,7 +59,7 @@ class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
                  update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True,
-                 rehandoff_period=10.0):
+                 rehandoff_period=1.0):
         self.client = client
         self.name = scheduler_name
         self.cache = SchedulerCache()
@@ -204,9 +205,13 @@ class Scheduler:
 
     async def _rehandoff_loop(self):
         """Unschedulable pods are offered to the next shard again (its capacity may have freed)."""
+        tick = max(0.05, self.rehandoff_period / 4)
         while True:
-            await asyncio.sleep(self.rehandoff_period)
-            for pod in list(self.queue.unschedulable_pods()):
+            await asyncio.sleep(tick)
+            now = time.monotonic()
+            for pod, since in list(self.queue.unschedulable_since()):
+                if now - since < self.rehandoff_period:
+                    continue
                 self.queue.delete(pod)
                 self.handoffs += 1
                 spawn(self._patch_shard(pod, offset_of(pod["metadata"].get("labels")) + 1, 0))
