@@ -70,10 +70,10 @@ def cpu_budget():
 def control_plane_shape(world, workers=0, shards=0):
     """API server workers and scheduler shards for `world` ranks (0 = auto).
 
-    Measured on a 16-CPU MI355X box (profiles/r1_cp_sweep, profiles/r2_scale, r2_partitioned): with
-    one rank the single API server + scheduler are fastest; from 2 ranks on, parallel API server
-    workers over the native store (watches served by its C++ fan-out) and as many partitioned
-    scheduler shards (N=4: w=4 s=4 3184 pods/s vs w=4 s=2 2727).
+    Measured on a 16-CPU MI355X box (profiles/r2_partitioned: n1_shapes, scale_r2d): since API
+    workers read pods from the store instead of caching every pod event, 2 workers + 2
+    partitioned scheduler shards beat the single in-process-store API server already at N=1
+    (1946-2086 vs 1574-1793 pods/s, p99 19 vs 62-90 ms); N=4: w=4 s=4 3184 vs w=4 s=2 2727.
     On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — one API
     server worker and one scheduler shard per rank, up to 8 each — so per-rank work (weak
     scaling) is met by per-rank control-plane capacity instead of a fixed-size control plane."""
@@ -81,17 +81,17 @@ def control_plane_shape(world, workers=0, shards=0):
     spare = cpus - world - 1
     big = cpus >= 64
     if workers <= 0:
-        if world == 1 or spare < 3:
+        if spare < 3:
             workers = 1
         elif big:
-            workers = min(8, world, max(1, spare // 6))
+            workers = min(8, max(2, world), max(1, spare // 6))
         else:
             workers = 2 if world < 4 else 4
     if shards <= 0:
-        if world == 1 or spare < 3:
+        if spare < 3:
             shards = 1
         elif big:
-            shards = min(8, world, max(1, spare // 6))
+            shards = min(8, max(2, world), max(1, spare // 6))
         else:
             shards = 2 if world < 4 else 4
     return workers, shards
