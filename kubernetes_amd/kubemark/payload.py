@@ -15,31 +15,49 @@ import os
 
 
 class PayloadServer:
+    """`run` is `() -> bool` (one start) or an object with `run_batch(k) -> [bool]` (e.g.
+    `ops.hip_kernels.Payload`): the starts that arrived in one read are run as ONE batch —
+    k kernel launches, one verify kernel, one stream sync — on a worker thread, so the rank's
+    event loop keeps serving its watches while the GPU works."""
+
     def __init__(self, run, path):
-        self.run = run                  # () -> bool, e.g. ops.hip_kernels.Payload(dev).run
+        self.run = run
+        self._batch = getattr(run, "run_batch", None) or getattr(getattr(run, "__self__", None), "run_batch", None)
         self.path = path
         self.runs = 0
         self.failures = 0
+        self.batches = 0
         self._srv = None
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(1, thread_name_prefix="payload")   # one HIP caller at a time
+
+    def _run_many(self, k):
+        if self._batch is not None:
+            return self._batch(k)
+        out = []
+        for _ in range(k):
+            try:
+                out.append(bool(self.run()))
+            except Exception:  # noqa: BLE001 - a crashing payload is a failed container
+                out.append(False)
+        return out
 
     async def _serve(self, reader, writer):
+        loop = asyncio.get_running_loop()
         try:
             while True:
                 req = await reader.read(4096)
                 if not req:
                     break
-                out = bytearray()
-                for _ in range(len(req)):            # one byte per request
-                    ok = False
-                    self.runs += 1
-                    try:
-                        ok = bool(self.run())
-                    except Exception:  # noqa: BLE001 - a crashing payload is a failed container
-                        ok = False
-                    if not ok:
-                        self.failures += 1
-                    out += b"1" if ok else b"0"
-                writer.write(bytes(out))
+                k = len(req)                         # one byte per request
+                try:
+                    oks = await loop.run_in_executor(self._pool, self._run_many, k)
+                except Exception:  # noqa: BLE001
+                    oks = [False] * k
+                self.runs += k
+                self.batches += 1
+                self.failures += sum(1 for ok in oks if not ok)
+                writer.write(b"".join(b"1" if ok else b"0" for ok in oks))
         except (ConnectionError, asyncio.CancelledError):
             pass
         finally:
@@ -55,6 +73,7 @@ class PayloadServer:
         if self._srv is not None:
             self._srv.close()
             await self._srv.wait_closed()
+        self._pool.shutdown(wait=True)
         try:
             os.unlink(self.path)
         except OSError:
@@ -70,6 +89,7 @@ class PayloadClient:
         self._pending: collections.deque = collections.deque()
         self._reader_task = None
         self._lock = asyncio.Lock()
+        self._queued = 0
 
     async def _connect(self):
         r, w = await asyncio.open_unix_connection(self.path)
@@ -98,10 +118,19 @@ class PayloadClient:
             async with self._lock:
                 if self._w is None:
                     await self._connect()
-        fut = asyncio.get_running_loop().create_future()
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
         self._pending.append(fut)
-        self._w.write(b"R")
+        # container starts issued in one loop iteration leave in ONE write -> one GPU batch
+        if not self._queued:
+            loop.call_soon(self._flush)
+        self._queued += 1
         return await fut
+
+    def _flush(self):
+        n, self._queued = self._queued, 0
+        if n and self._w is not None:
+            self._w.write(b"R" * n)
 
     async def close(self):
         if self._w is not None:

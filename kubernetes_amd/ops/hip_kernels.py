@@ -44,6 +44,7 @@ def load():
         L.kamd_payload_create.argtypes = [i, i]
         L.kamd_payload_create.restype = vp
         L.kamd_payload_run.argtypes = [vp]
+        L.kamd_payload_run_batch.argtypes = [vp, i, ctypes.POINTER(ctypes.c_int)]
         L.kamd_payload_destroy.argtypes = [vp]
         L.kamd_hip_device_arch.argtypes = [i, ctypes.c_char_p, i]
         L.kamd_gemm_set_path.argtypes = [i]
@@ -143,8 +144,22 @@ class Payload:
             raise HIPError(f"payload create on device {dev} failed")
         self.dev = dev
 
+    MAX_BATCH = 256   # PAYLOAD_SLOTS in native/hip/kamd_hip.hip
+
     def run(self) -> bool:
         return load().kamd_payload_run(self.h) == 0
+
+    def run_batch(self, k: int) -> list:
+        """k container starts at once: k vector_add launches, one verify kernel, one sync.
+        Returns one pass/fail per start. Thread-safe for a single caller thread at a time."""
+        out = []
+        while k > 0:
+            m = min(k, self.MAX_BATCH)
+            ok = (ctypes.c_int * m)()
+            rc = load().kamd_payload_run_batch(self.h, m, ok)
+            out += [False] * m if rc < 0 else [bool(x) for x in ok]
+            k -= m
+        return out
 
     def close(self):
         if self.h:

@@ -740,22 +740,65 @@ int kamd_diag_hbm(int dev, size_t bytes, int iters, double* gbps) {
 
 // Persistent per-GPU payload context (warm HIP context + buffers): the stub runtime's
 // "container start" for GPU pods runs vector_add on the pod's device and verifies it.
+// Container-start payload. One call = one GPU container start = one vector_add launch into its
+// own output slot; a batch of k starts (k container starts that reached the rank together) is
+// k launches + ONE verify kernel that checks sampled elements of every slot and writes a pass
+// flag per start straight into pinned host memory, then ONE stream sync — instead of k
+// launch + pageable-memcpy + sync round trips.
+constexpr int PAYLOAD_SLOTS = 256;
+
 struct kamd_payload {
   int dev;
   int n;
-  float *a, *b, *c;
+  float *a, *b, *c;        // c: PAYLOAD_SLOTS output slots of n floats
   float* host;
+  int* flags;              // pinned host, PAYLOAD_SLOTS pass flags
+  int next;                // next output slot (round robin)
   hipStream_t stream;
 };
 
+__device__ __forceinline__ void payload_samples(int n, int* idx) {
+  idx[0] = 0;
+  idx[1] = n / 3;
+  idx[2] = n / 2;
+  idx[3] = n - 1;
+}
+
+__global__ void __launch_bounds__(256) payload_poison_kernel(float* __restrict__ c, int n, int first, int k) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k) return;
+  float* cs = c + (size_t)((first + j) % PAYLOAD_SLOTS) * n;
+  int idx[4];
+  payload_samples(n, idx);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cs[idx[q]] = -1.f;   // never a valid a + b (both >= 0)
+}
+
+__global__ void __launch_bounds__(256) payload_verify_kernel(const float* __restrict__ c, int n, int first, int k,
+                                                             int* __restrict__ flags) {
+  // one thread per start: 4 sampled elements of its slot must equal a + b = 2 * (i % 1000)
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k) return;
+  const int slot = (first + j) % PAYLOAD_SLOTS;
+  const float* cs = c + (size_t)slot * n;
+  int idx[4];
+  payload_samples(n, idx);
+  int ok = 1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ok &= cs[idx[q]] == 2.f * (float)(idx[q] % 1000);
+  flags[j] = ok;
+}
+
 void* kamd_payload_create(int dev, int n) {
-  if (hipSetDevice(dev) != hipSuccess) return nullptr;
+  if (n < 1 || hipSetDevice(dev) != hipSuccess) return nullptr;
   kamd_payload* p = new kamd_payload();
   p->dev = dev;
   p->n = n;
+  p->next = 0;
   size_t bytes = (size_t)n * sizeof(float);
   if (hipMalloc(&p->a, bytes) != hipSuccess || hipMalloc(&p->b, bytes) != hipSuccess ||
-      hipMalloc(&p->c, bytes) != hipSuccess || hipHostMalloc(&p->host, bytes) != hipSuccess ||
+      hipMalloc(&p->c, bytes * PAYLOAD_SLOTS) != hipSuccess || hipHostMalloc(&p->host, bytes) != hipSuccess ||
+      hipHostMalloc(&p->flags, PAYLOAD_SLOTS * sizeof(int)) != hipSuccess ||
       hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
     delete p;
     return nullptr;
@@ -766,19 +809,35 @@ void* kamd_payload_create(int dev, int n) {
   return p;
 }
 
+// Runs k payloads (1 <= k <= PAYLOAD_SLOTS); ok[j] = 1 if start j computed c == a + b.
+// Returns 0 when every start passed, 1 if any failed verification, -1 on a HIP error.
+int kamd_payload_run_batch(void* h, int k, int* ok) {
+  kamd_payload* p = (kamd_payload*)h;
+  if (!p || k < 1 || k > PAYLOAD_SLOTS) return -1;
+  if (hipSetDevice(p->dev) != hipSuccess) return -1;
+  const int first = p->next;
+  // a stale slot must not pass by itself: poison the sampled elements of every slot first
+  hipLaunchKernelGGL(payload_poison_kernel, dim3((k + 255) / 256), dim3(256), 0, p->stream, p->c, p->n, first, k);
+  for (int j = 0; j < k; ++j) {
+    float* cs = p->c + (size_t)((first + j) % PAYLOAD_SLOTS) * p->n;
+    hipLaunchKernelGGL(vector_add_kernel, dim3((p->n + 255) / 256), dim3(256), 0, p->stream, p->a, p->b, cs, p->n);
+  }
+  p->next = (first + k) % PAYLOAD_SLOTS;
+  hipLaunchKernelGGL(payload_verify_kernel, dim3((k + 255) / 256), dim3(256), 0, p->stream, p->c, p->n, first, k,
+                     p->flags);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->stream) != hipSuccess) return -1;
+  int all = 1;
+  for (int j = 0; j < k; ++j) {
+    ok[j] = p->flags[j];
+    all &= ok[j];
+  }
+  return all ? 0 : 1;
+}
+
 // Runs one payload; returns 0 if c == a + b on sampled elements.
 int kamd_payload_run(void* h) {
-  kamd_payload* p = (kamd_payload*)h;
-  if (hipSetDevice(p->dev) != hipSuccess) return -1;
-  hipLaunchKernelGGL(vector_add_kernel, dim3((p->n + 255) / 256), dim3(256), 0, p->stream, p->a, p->b, p->c, p->n);
-  float probe[4];
-  const int idx[4] = {0, p->n / 3, p->n / 2, p->n - 1};
-  for (int k = 0; k < 4; ++k)
-    hipMemcpyAsync(&probe[k], p->c + idx[k], sizeof(float), hipMemcpyDeviceToHost, p->stream);
-  if (hipStreamSynchronize(p->stream) != hipSuccess) return -1;
-  for (int k = 0; k < 4; ++k)
-    if (probe[k] != 2.f * (float)(idx[k] % 1000)) return 1;
-  return 0;
+  int ok = 0;
+  return kamd_payload_run_batch(h, 1, &ok);
 }
 
 void kamd_payload_destroy(void* h) {
@@ -790,6 +849,7 @@ void kamd_payload_destroy(void* h) {
   hipFree(p->b);
   hipFree(p->c);
   hipHostFree(p->host);
+  hipHostFree(p->flags);
   delete p;
 }
 

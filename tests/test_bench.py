@@ -49,3 +49,38 @@ def test_bench_two_ranks_gloo():
     _check(d, 2, 2, 1)
     assert d["config"]["parallelism"] == "ranks2" and d["config"]["hollow_nodes"] == 4
     assert d["config"]["global_batch"] == 32                 # weak scaling: 2 ranks x 2 nodes x 8 GPUs
+
+
+def test_payload_server_batches_starts(run, tmp_path):
+    """Hollow-node processes ask the rank's PayloadServer for GPU payload runs: starts issued
+    together are answered as one batch (run_batch), failures are reported per start."""
+    import asyncio
+    from kubernetes_amd.kubemark.payload import PayloadClient, PayloadServer
+
+    class Fake:
+        def __init__(self):
+            self.calls = []
+
+        def run(self):
+            return True
+
+        def run_batch(self, k):
+            self.calls.append(k)
+            return [i % 5 != 4 for i in range(k)]
+
+    async def main():
+        f = Fake()
+        srv = await PayloadServer(f.run, str(tmp_path / "p.sock")).start()
+        cl = PayloadClient(str(tmp_path / "p.sock"))
+        oks = await asyncio.gather(*(cl() for _ in range(10)))
+        assert oks.count(False) >= 1 and srv.runs == 10 and srv.failures == oks.count(False)
+        assert max(f.calls) > 1                          # coalesced into batches
+        # a plain callable works too (one run per start)
+        srv2 = await PayloadServer(lambda: True, str(tmp_path / "q.sock")).start()
+        cl2 = PayloadClient(str(tmp_path / "q.sock"))
+        assert await asyncio.gather(*(cl2() for _ in range(4))) == [True] * 4
+        for c in (cl, cl2):
+            await c.close()
+        for s in (srv, srv2):
+            await s.stop()
+    run(main())

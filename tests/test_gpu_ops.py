@@ -103,3 +103,14 @@ def test_gemm256_identity_asymmetric(hk):
     b = (torch.arange(n * n, device="cuda").reshape(n, n) % 7 - 3).to(torch.bfloat16)
     torch.testing.assert_close(hk.gemm_bf16_nt(a, b), b.float().T, rtol=0, atol=0)
     torch.testing.assert_close(hk.gemm_bf16_nt(b, a), b.float(), rtol=0, atol=0)
+
+
+def test_payload_batch(hk):
+    """k container starts in one batch: k launches + one verify kernel + one sync, every start verified."""
+    p = hk.Payload(0)
+    try:
+        assert p.run_batch(1) == [True]
+        assert p.run_batch(300) == [True] * 300          # > one slot ring: split into batches
+        assert all(p.run() for _ in range(3))
+    finally:
+        p.close()
