@@ -297,6 +297,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     stats = {"elapsed": elapsed, "lat": lat, "pods": sum(r["pods"] for r in results),
              "to_running": [r["to_running_s"] for r in results], "cycle": [r["cycle_s"] for r in results],
              "phases": {k: [r[k] for r in results] for k in ("create_s", "to_running_s", "delete_issued_s", "cycle_s")},
+             "api_lat": {v: [x for r in results for x in r["api_latencies"][v]] for v in ("create", "delete")},
              "payload_runs": (psrv.runs if psrv else sum(getattr(k.runtime, "payload_runs", 0) for k in hollow.nodes)
                               if hollow or psrv else 0),
              "payload_failures": (psrv.failures if psrv else sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes)
@@ -430,6 +431,10 @@ def main():
         "step_phases_ms": {k: round(1000 * sum(max(s["phases"][k][i] for s in allstats) for i in range(args.steps))
                                     / max(1, args.steps), 2)
                            for k in ("create_s", "to_running_s", "delete_issued_s", "cycle_s")},
+        # client-observed API call latency under load (reference SLO: non-list p99 <= 1 s,
+        # test/e2e/framework/metrics_util.go:52-59)
+        "api_call_ms": {v: {q: round(pct([x for s in allstats for x in s["api_lat"][v]], p) * 1000, 2)
+                            for q, p in (("p50", 0.5), ("p99", 0.99))} for v in ("create", "delete")},
         "sched_rate_avg_pods_per_s": round(sum(s["sched_rates"][0] for s in allstats), 1),
         "vs_scheduler_perf_warn_threshold": round(value / BASELINE_SCHED_WARN_PODS_PER_S, 2),
         "payload_runs": sum(s["payload_runs"] for s in allstats),

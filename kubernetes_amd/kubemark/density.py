@@ -116,11 +116,14 @@ class DensityRunner:
         sem = asyncio.Semaphore(self.concurrency)
         t0 = time.monotonic()
 
+        api_lat = {"create": [], "delete": []}
+
         async def create(n):
             async with sem:
-                self.created[n] = time.monotonic()
+                self.created[n] = t = time.monotonic()
                 await self.client.create("pods", gpu_pod(n, self.ns, labels, self.gpus_per_pod,
                                                          annotations=self.annotations), self.ns)
+                api_lat["create"].append(time.monotonic() - t)
 
         await asyncio.gather(*(create(n) for n in names))
         t_created = time.monotonic()
@@ -129,11 +132,13 @@ class DensityRunner:
 
         async def delete(n):
             async with sem:
+                t = time.monotonic()
                 try:
                     await self.client.delete("pods", n, self.ns)
                 except APIStatusError as e:
                     if e.code != 404:
                         raise
+                api_lat["delete"].append(time.monotonic() - t)
 
         await asyncio.gather(*(delete(n) for n in names))
         t_deleted = time.monotonic()
@@ -143,7 +148,7 @@ class DensityRunner:
         sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)
         return {"pods": len(names), "names": names, "create_s": t_created - t0, "to_running_s": t_running - t0,
                 "delete_issued_s": t_deleted - t0, "cycle_s": t_gone - t0, "latencies": lat,
-                "scheduled_times": [s - t0 for s in sched]}
+                "scheduled_times": [s - t0 for s in sched], "api_latencies": api_lat}
 
     async def stop(self):
         if self._stream:

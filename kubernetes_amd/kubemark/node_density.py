@@ -15,7 +15,10 @@ Two workloads, as in the reference:
     cAdvisor (`resource_collector.go:56`, housekeeping 1 s);
   * steady-state resource tracking with every pod running (`resource_usage_test.go:65-78,
     136-182`: settle, then monitor; kubelet limits for 10 pods p50 ≤ 0.30 / p95 ≤ 0.35 cores,
-    RSS ≤ 200 MiB), plus kubelet CPU-seconds spent per started pod.
+    RSS ≤ 200 MiB), plus kubelet CPU-seconds spent per started pod;
+  * `--runtime remote`: the kubelet talks CRI to a separate `kamd-cri` process (the reference's
+    dockershim/docker split), whose CPU and RSS are tracked too (thresholds p50 ≤ 0.40 / p95 ≤
+    0.60 cores, RSS ≤ 500 MiB, `density_test.go:76-83`).
 
     python -m kubernetes_amd.kubemark.node_density --batch 10 --sequential 10 --background 50
 """
@@ -36,7 +39,8 @@ from .density import pct
 THRESHOLDS = {"batch": {"p50": 16.0, "p90": 18.0, "p99": 20.0, "all": 25.0},
               "sequential": {"p50": 5.0, "p90": 9.0, "p99": 10.0},
               "kubelet_cpu": {"p50": 0.30, "p95": 0.50}, "kubelet_rss_mib": 100.0,
-              "steady_kubelet_cpu": {"p50": 0.30, "p95": 0.35}, "steady_kubelet_rss_mib": 200.0}
+              "steady_kubelet_cpu": {"p50": 0.30, "p95": 0.35}, "steady_kubelet_rss_mib": 200.0,
+              "runtime_cpu": {"p50": 0.40, "p95": 0.60}, "runtime_rss_mib": 500.0}
 
 
 def _spawn(args, tmp, name):
@@ -110,7 +114,8 @@ async def _wait_running(client, ns, names, timeout):
     return seen
 
 
-async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0, monitor=10.0, period=1.0):
+async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0, monitor=10.0, period=1.0,
+              runtime="process"):
     tmp = tempfile.mkdtemp(prefix="kamd-node-density-")
     pf = os.path.join(tmp, "api.port")
     procs = [_spawn(["kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf], tmp, "apiserver")]
@@ -122,9 +127,21 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             await asyncio.sleep(0.05)
         url = f"http://127.0.0.1:{open(pf).read().strip()}"
         procs.append(_spawn(["kubernetes_amd.cmd.scheduler", "--master", url], tmp, "scheduler"))
+        rt_args, rt_proc = ["--container-runtime", "process"], None
+        if runtime == "remote":
+            sock = os.path.join(tmp, "cri.sock")
+            rt_proc = _spawn(["kubernetes_amd.cmd.cri", "--listen", sock, "--runtime", "process",
+                              "--root-dir", os.path.join(tmp, "cri")], tmp, "cri")
+            procs.append(rt_proc)
+            t = time.time()
+            while not os.path.exists(sock):
+                if time.time() - t > 60:
+                    raise TimeoutError("kamd-cri did not start")
+                await asyncio.sleep(0.05)
+            rt_args = ["--container-runtime", "remote", "--container-runtime-endpoint", f"unix://{sock}"]
         kl = _spawn(["kubernetes_amd.cmd.kubelet", "--api-servers", url, "--hostname-override", "density-node",
-                     "--root-dir", os.path.join(tmp, "kubelet"), "--container-runtime", "process", "--port", "0",
-                     "--container-log-dir", "", "--max-pods", str(background + batch + sequential + 10)],
+                     "--root-dir", os.path.join(tmp, "kubelet"), "--port", "0",
+                     "--container-log-dir", "", "--max-pods", str(background + batch + sequential + 10)] + rt_args,
                     tmp, "kubelet")
         procs.append(kl)
         c = Client(url)
@@ -138,6 +155,7 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
                 raise TimeoutError("kubelet did not register")
             await asyncio.sleep(0.1)
         sampler = Sampler(kl.pid, period).start()
+        rts = Sampler(rt_proc.pid, period).start() if rt_proc is not None else None
         cpu0 = sampler.cpu_seconds()
         ns = "density"
         await c.create("namespaces", {"metadata": {"name": ns}})
@@ -168,11 +186,15 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
         await asyncio.sleep(period)        # the sample covering the last start
         cpu = sorted(sampler.cpu) or [0.0]
         rss = max(sampler.rss or [0])
+        rt_cpu = sorted(rts.cpu) if rts is not None else None
+        rt_rss = max(rts.rss or [0]) if rts is not None else None
         # steady state: every pod running, nothing changing
         await asyncio.sleep(settle)
         sampler.reset()
         await asyncio.sleep(monitor)
         sampler.stop()
+        if rts is not None:
+            rts.stop()
         steady = sorted(sampler.cpu) or [0.0]
         await c.close()
         out = {
@@ -186,8 +208,13 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             "steady": {"pods": batch + background + sequential, "monitor_s": monitor,
                        "kubelet_cpu_cores": {"p50": round(pct(steady, .5), 3), "p95": round(pct(steady, .95), 3)},
                        "kubelet_rss_mib": round(max(sampler.rss or [0]) / 2**20, 1)},
+            "runtime": runtime,
             "thresholds": THRESHOLDS,
         }
+        if rt_cpu is not None:
+            rt_cpu = rt_cpu or [0.0]
+            out["runtime_cpu_cores"] = {"p50": round(pct(rt_cpu, .5), 3), "p95": round(pct(rt_cpu, .95), 3)}
+            out["runtime_rss_mib"] = round(rt_rss / 2**20, 1)
         out["within_thresholds"] = (
             out["batch"]["p50_s"] <= THRESHOLDS["batch"]["p50"] and out["batch"]["p99_s"] <= THRESHOLDS["batch"]["p99"]
             and out["batch"]["all_running_s"] <= THRESHOLDS["batch"]["all"]
@@ -196,7 +223,9 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             and out["kubelet_cpu_cores"]["p95"] <= THRESHOLDS["kubelet_cpu"]["p95"]
             and out["kubelet_rss_mib"] <= THRESHOLDS["kubelet_rss_mib"]
             and out["steady"]["kubelet_cpu_cores"]["p95"] <= THRESHOLDS["steady_kubelet_cpu"]["p95"]
-            and out["steady"]["kubelet_rss_mib"] <= THRESHOLDS["steady_kubelet_rss_mib"])
+            and out["steady"]["kubelet_rss_mib"] <= THRESHOLDS["steady_kubelet_rss_mib"]
+            and (rt_cpu is None or (out["runtime_cpu_cores"]["p95"] <= THRESHOLDS["runtime_cpu"]["p95"]
+                                    and out["runtime_rss_mib"] <= THRESHOLDS["runtime_rss_mib"])))
         return out
     finally:
         for p in procs:
@@ -215,8 +244,11 @@ def main(argv=None):
     ap.add_argument("--background", type=int, default=50)
     ap.add_argument("--monitor", type=float, default=10.0, help="steady-state monitoring seconds")
     ap.add_argument("--period", type=float, default=1.0, help="CPU/RSS sampling period (cAdvisor housekeeping)")
+    ap.add_argument("--runtime", default="process", choices=["process", "remote"],
+                    help="remote: kubelet -> CRI -> a separate kamd-cri process (tracked as the runtime)")
     a = ap.parse_args(argv)
-    print(json.dumps(asyncio.run(run(a.batch, a.sequential, a.background, monitor=a.monitor, period=a.period))))
+    print(json.dumps(asyncio.run(run(a.batch, a.sequential, a.background, monitor=a.monitor, period=a.period,
+                                     runtime=a.runtime))))
 
 
 if __name__ == "__main__":

@@ -173,3 +173,13 @@ def test_node_density_benchmark_small():
     assert 0 < out["kubelet_rss_mib"] < 200
     assert out["kubelet_cpu_s_per_pod"] > 0
     assert "steady" in out and out["steady"]["pods"] == 8
+
+
+def test_node_density_remote_runtime_small():
+    """Same benchmark with the kubelet talking CRI to a separate kamd-cri process, whose CPU and
+    RSS are reported as the runtime's (the reference's dockershim/docker split)."""
+    from kubernetes_amd.kubemark import node_density
+    out = asyncio.run(node_density.run(batch=2, sequential=1, background=1, monitor=0.5, settle=0.2, period=0.5,
+                                       runtime="remote"))
+    assert out["runtime"] == "remote" and out["batch"]["all_running_s"] < 25
+    assert 0 < out["runtime_rss_mib"] < 500 and "p95" in out["runtime_cpu_cores"]
