@@ -427,6 +427,7 @@ def main():
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
         "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
         "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],
+        "step_ms_max": round(1000 * max(max(s["cycle"]) for s in allstats), 2),
         # mean over steps of the slowest rank: pods created / all Running / deletes issued / all gone
         "step_phases_ms": {k: round(1000 * sum(max(s["phases"][k][i] for s in allstats) for i in range(args.steps))
                                     / max(1, args.steps), 2)

@@ -17,8 +17,8 @@ processes in parallel over a PARTITION of the cluster, so no shard processes eve
   * a pod that fits none of the shard's nodes is handed to the next shard by bumping its
     `scheduler.kamd.io/shard-offset` label (`scheduler.kamd.io/shard-hops` counts the hops);
     after a full round it is reported unschedulable (and preemption is tried) on the last shard,
-    and it is offered to the next shard again once it has waited `rehandoff_period` seconds (the
-    capacity it needs may have freed on another shard's nodes).
+    and it is offered to the next shard again after `rehandoff_period` seconds, doubling per round
+    up to 10 s (the capacity it needs may have freed on another shard's nodes).
 Per-shard work is O(cluster pods / n). Trade-off: inter-pod (anti-)affinity is evaluated
 against the pods on the shard's own nodes. GPU double assignment stays impossible: the API
 server's device-claim guard rejects a conflicting bind (409) and the shard retries.
@@ -59,7 +59,7 @@ class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
                  update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True,
-                 rehandoff_period=1.0):
+                 rehandoff_period=0.2):
         self.client = client
         self.name = scheduler_name
         self.cache = SchedulerCache()
@@ -71,6 +71,7 @@ class Scheduler:
         self.all_nodes: dict[str, dict] = {}          # partitioned: every node object
         self.owned: dict[str, Informer] = {}          # partitioned: owned node -> its pod informer
         self._owned_ready: set = set()
+        self._rehandoff_delay: dict = {}             # pod key -> current re-offer delay (doubling)
         self.handoffs = 0
         self.conflicts = 0
         self.recorder = EventRecorder(client, scheduler_name, enabled=emit_events)
@@ -124,6 +125,8 @@ class Scheduler:
     def _on_unassigned_delete(self, pod):
         # bound (now on some node's informer), deleted, or handed to another shard
         self.queue.delete(pod)
+        if (pod.get("spec") or {}).get("nodeName") or pod["metadata"].get("deletionTimestamp"):
+            self._rehandoff_delay.pop(ns_name(pod), None)
 
     def _on_owned_pod_delete(self, pod):
         self.cache.remove_pod(pod)
@@ -205,13 +208,18 @@ class Scheduler:
 
     async def _rehandoff_loop(self):
         """Unschedulable pods are offered to the next shard again (its capacity may have freed)."""
-        tick = max(0.05, self.rehandoff_period / 4)
+        tick = max(0.02, self.rehandoff_period / 4)
         while True:
             await asyncio.sleep(tick)
             now = time.monotonic()
             for pod, since in list(self.queue.unschedulable_since()):
-                if now - since < self.rehandoff_period:
+                key = ns_name(pod)
+                delay = self._rehandoff_delay.get(key, self.rehandoff_period)
+                if now - since < delay:
                     continue
+                self._rehandoff_delay[key] = min(delay * 2, 10.0)
+                if len(self._rehandoff_delay) > 100_000:
+                    self._rehandoff_delay.clear()
                 self.queue.delete(pod)
                 self.handoffs += 1
                 spawn(self._patch_shard(pod, offset_of(pod["metadata"].get("labels")) + 1, 0))
