@@ -270,6 +270,8 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     pods_per_step = args.pods_per_rank or args.nodes_per_rank * args.gpus_per_node // args.gpus_per_pod
     runner = DensityRunner(url, d.rank, pods_per_step=pods_per_step, gpus_per_pod=args.gpus_per_pod)
     await runner.start()
+    from kubernetes_amd.cmd._common import tune_gc
+    tune_gc()        # same GC settings as the control-plane components
     await abarrier()
     for w in range(args.warmup):
         await runner.step(f"w{w}", timeout=args.step_timeout)

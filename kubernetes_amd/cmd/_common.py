@@ -20,6 +20,24 @@ def write_port_file(path, port):
         os.replace(tmp, path)
 
 
+def tune_gc():
+    """Long-running components allocate mostly acyclic JSON dicts (freed by refcounting), so the
+    cyclic collector only adds pauses: a full collection over a large heap stalls the event loop
+    for tens of ms (visible as API call p99 spikes). Young collections run 70x less often, and
+    everything alive once the component is up moves to the permanent generation (`gc.freeze`).
+    KAMD_GC_THRESHOLD="a,b,c" overrides the thresholds ("0" disables the collector)."""
+    import gc
+    v = os.environ.get("KAMD_GC_THRESHOLD", "50000,20,100")
+    if v.strip() == "0":
+        gc.disable()
+    else:
+        try:
+            gc.set_threshold(*(int(x) for x in v.split(",")))
+        except (TypeError, ValueError):
+            pass
+    gc.freeze()
+
+
 def run_until_signal(main_coro_factory):
     """Run an asyncio component until SIGINT/SIGTERM."""
     async def runner():
@@ -31,6 +49,7 @@ def run_until_signal(main_coro_factory):
             except NotImplementedError:
                 pass
         comp = await main_coro_factory()
+        tune_gc()
         await stop.wait()
         closer = getattr(comp, "stop", None)
         if closer is not None:
