@@ -142,7 +142,7 @@ class RemoteRuntime(Runtime):
         labels = {A.POD_NAME: md.get("name", ""), A.POD_NAMESPACE: md.get("namespace", ""),
                   A.POD_UID: md.get("uid", ""), A.CONTAINER_NAME: container["name"]}
         cfg = A.MSG["ContainerConfig"](
-            metadata=A.MSG["ContainerMetadata"](name=container["name"], attempt=0),
+            metadata=A.MSG["ContainerMetadata"](name=container["name"], attempt=int(opts.attempt or 0)),
             image=A.MSG["ImageSpec"](image=container.get("image", "")),
             command=list(container.get("command") or []), args=list(container.get("args") or []),
             working_dir=container.get("workingDir") or "", envs=envs,
@@ -234,6 +234,36 @@ class RemoteRuntime(Runtime):
 
     def list_containers(self):
         return list(self.cache.values())
+
+    async def pod_states(self):
+        """ListPodSandbox + ListContainers of the runtime, grouped by the pod-uid label; every
+        listed container enters this client's status cache (so the restarted kubelet's PLEG
+        tracks the adopted containers too)."""
+        out: dict = {}
+        sbs = await self._call("ListPodSandbox", A.MSG["ListPodSandboxRequest"]())
+        for sb in sbs.items:
+            uid = sb.labels.get(A.POD_UID, "") or sb.metadata.uid
+            ip = None
+            try:
+                st = await self._call("PodSandboxStatus", A.MSG["PodSandboxStatusRequest"](pod_sandbox_id=sb.id))
+                ip = st.status.network.ip or None
+            except Exception:  # noqa: BLE001 - the sandbox may be going away
+                pass
+            out.setdefault(uid, {"sandboxes": [], "containers": []})["sandboxes"].append(
+                (sb.id, sb.state == A.SANDBOX_READY, ip))
+        cs = await self._call("ListContainers", A.MSG["ListContainersRequest"]())
+        for c in cs.containers:
+            uid = c.labels.get(A.POD_UID, "")
+            name = c.labels.get(A.CONTAINER_NAME, "") or c.metadata.name
+            if c.id not in self.cache:
+                st = ContainerStatus(c.id, name, _STATES.get(c.state, UNKNOWN), image=c.image.image)
+                st._sandbox = c.pod_sandbox_id
+                self.cache[c.id] = st
+                self.pod_of[c.id] = uid
+                await self._refresh(c.id)
+            out.setdefault(uid, {"sandboxes": [], "containers": []})["containers"].append(
+                (name, c.id, c.metadata.attempt, c.created_at / 1e9 if c.created_at else 0.0, c.pod_sandbox_id))
+        return out
 
     async def container_logs(self, cid, tail=None):
         st = self.cache.get(cid)

@@ -97,14 +97,16 @@ class ManagerImpl:
                 self.pod_cache.delete_pod(uid)
 
     async def _wait_registered(self, rname):
+        # the resource exists once the plugin registered AND its first ListAndWatch snapshot
+        # landed; registration alone (the event) can precede the snapshot, so re-check on every
+        # registration and at least every 10 ms
         deadline = time.monotonic() + self.registration_grace
         while not self.store.has_resource(rname) and time.monotonic() < deadline:
             self._registered.clear()
             try:
-                await asyncio.wait_for(self._registered.wait(), max(0.0, deadline - time.monotonic()))
+                await asyncio.wait_for(self._registered.wait(), max(0.0, min(0.01, deadline - time.monotonic())))
             except asyncio.TimeoutError:
-                break
-            await asyncio.sleep(0)  # let the first ListAndWatch snapshot land
+                pass
 
     async def admit_pod(self, pod):
         self._lazy_pod_delete()

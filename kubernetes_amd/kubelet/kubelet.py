@@ -54,7 +54,7 @@ BOOTSTRAP_CHECKPOINT = "node.kubernetes.io/bootstrap-checkpoint"
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
                  "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
-                 "waiting", "net_mounts", "net_setup", "previous", "backoff")
+                 "waiting", "net_mounts", "net_setup", "previous", "backoff", "adopted")
 
     def __init__(self, pod):
         self.uid = pod["metadata"]["uid"]
@@ -79,6 +79,7 @@ class PodState:
         self.net_setup = False                # network plugin SetUpPod done for the sandbox
         self.previous: dict[str, str] = {}    # container name -> last dead instance (logs --previous)
         self.backoff: dict[str, list] = {}    # container name -> [next restart allowed at, current delay]
+        self.adopted = False                  # sandbox/containers found in the runtime after a kubelet restart
 
 
 def _field_path(pod, c):
@@ -164,6 +165,9 @@ class Kubelet:
         self._workers: dict[str, asyncio.Task] = {}
         self._pending: dict[str, tuple] = {}
         self._tasks = []
+        self._adoptable: dict = {}
+        self.orphan_grace = 10.0   # s after the first sync before unknown runtime pods are removed
+        self.adopted_pods = 0
         self._status_dirty = asyncio.Event()
         self._status_sem = asyncio.Semaphore(max_status_inflight)
         self._status_inflight: dict[str, asyncio.Task] = {}
@@ -233,10 +237,18 @@ class Kubelet:
             restored = self._restore_checkpointed_pods()
             if restored:
                 log.info("started %d pods from bootstrap checkpoints", restored)
+        try:
+            # kubelet restart: what the runtime still runs is adopted, not started again
+            self._adoptable = await self.runtime.pod_states()
+        except Exception as e:  # noqa: BLE001 - a runtime that cannot list starts from scratch
+            log.warning("listing runtime pods for adoption failed: %s", e)
+            self._adoptable = {}
         self.informer.add_handler(self._on_add, self._on_update, self._on_delete)
         self.informer.start()
         self._tasks.append(asyncio.ensure_future(self._node_status_loop()))
         await self.informer.wait_synced(60)
+        if self._adoptable:
+            self._tasks.append(asyncio.ensure_future(self._remove_orphans(self.orphan_grace)))
         if self.pod_manifest_path or self.manifest_url:
             from .config import StaticPodSource
             self.static_pods = StaticPodSource(self, self.pod_manifest_path, url=self.manifest_url,
@@ -683,6 +695,8 @@ class Kubelet:
             if getattr(self.runtime, "shares_host_network", False) or (pod.get("spec") or {}).get("hostNetwork"):
                 st.ip = self.address     # no network namespace: the pod is reachable on the node address
             self.by_key[_key(pod)] = uid
+            if self._adoptable:
+                await self._adopt(st)
         else:
             st.pod = pod
         md = pod["metadata"]
@@ -697,6 +711,8 @@ class Kubelet:
             if r is not None:
                 reason, msg = r
                 st.rejected = reason
+                if st.adopted:
+                    await self._kill_pod(st, 0)
                 self.recorder.event(pod, "Warning", reason, msg)
                 await self._write_status(st, {"phase": core.POD_FAILED, "reason": reason, "message": msg,
                                               "conditions": (pod.get("status") or {}).get("conditions") or []})
@@ -875,6 +891,7 @@ class Kubelet:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: device plugin InitContainer failed: {e}")
             return None
         spec_c = c
+        opts.attempt = st.restarts.get(c["name"], 0)
         opts.mounts.extend(st.net_mounts)
         opts.oom_score_adj = oom_score_adj(st.pod, c, parse_quantity(self.capacity["memory"]).value)
         if self.cgroups is not None:
@@ -1050,6 +1067,71 @@ class Kubelet:
                 await self.garbage_collect_containers()
             except Exception as e:  # noqa: BLE001 - GC failures are logged and retried
                 log.warning("container garbage collection failed: %s", e)
+
+    async def _adopt(self, st: PodState):
+        """Take over the sandbox and containers the runtime still runs for this pod after a
+        kubelet restart (kuberuntime `computePodActions` keeps running containers whose pod is
+        known). Device admission (AdmitPod) still runs again — the fork rebuilds its per-pod
+        plugin state that way — but nothing is restarted."""
+        ps = self._adoptable.pop(st.uid, None)
+        if not ps:
+            return
+        ready = [sb for sb in ps["sandboxes"] if sb[1]]
+        if not ready:
+            for sid, _, _ in ps["sandboxes"]:           # a dead sandbox: start the pod afresh
+                await self.runtime.remove_pod_sandbox(sid)
+            return
+        sid, _, ip = ready[-1]
+        for osid, _, _ in ps["sandboxes"]:
+            if osid != sid:
+                await self.runtime.remove_pod_sandbox(osid)
+        spec = st.pod.get("spec") or {}
+        init_names = {c["name"] for c in spec.get("initContainers") or ()}
+        names = {c["name"] for c in spec.get("containers") or ()}
+        by_name: dict = {}
+        for name, cid, attempt, created, csid in ps["containers"]:
+            if csid == sid and (name in names or name in init_names):
+                by_name.setdefault(name, []).append((created, attempt, cid))
+        st.sandbox = sid
+        st.adopted = True
+        self.adopted_pods += 1
+        for name, lst in by_name.items():
+            lst.sort()
+            _, attempt, cid = lst[-1]
+            if name in init_names:
+                st.init_containers[name] = cid
+            else:
+                st.containers[name] = cid
+                if len(lst) > 1:
+                    st.previous[name] = lst[-2][2]
+            st.restarts[name] = int(attempt or 0)
+        status = st.pod.get("status") or {}
+        st.start_time = status.get("startTime") or now_rfc3339()
+        host_net = bool(spec.get("hostNetwork")) or getattr(self.runtime, "shares_host_network", False)
+        if not host_net:
+            st.ip = ip or status.get("podIP") or st.ip
+            if self.hostports is not None:
+                self.hostports.add(st.pod, st.ip)
+        if self.dns is not None:
+            st.net_mounts = self.dns.write_pod_files(os.path.join(self.root_dir, "pods", st.uid), st.pod, st.ip)
+        st.net_setup = True
+        log.info("adopted running pod %s (sandbox %s, %d containers)", st.pod["metadata"].get("name"), sid,
+                 len(st.containers))
+
+    async def _remove_orphans(self, grace):
+        """Runtime pods no source knows about once the kubelet has synced (deleted while it was
+        down): stop and remove them, like the kubelet's cleanup of orphaned pods."""
+        await asyncio.sleep(grace)
+        left, self._adoptable = self._adoptable, {}
+        for uid, ps in left.items():
+            if uid in self.pods:
+                continue
+            for sid, _, _ in ps["sandboxes"]:
+                try:
+                    await self.runtime.stop_pod_sandbox(sid)
+                    await self.runtime.remove_pod_sandbox(sid)
+                except Exception as e:  # noqa: BLE001 - best effort
+                    log.warning("removing orphaned sandbox %s: %s", sid, e)
 
     async def _setup_network(self, st: PodState):
         """SetUpPod through the network plugin (own-netns runtimes), host ports, and the

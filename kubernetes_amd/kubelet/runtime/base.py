@@ -22,6 +22,7 @@ class RunContainerOptions:
     annotations: list = field(default_factory=list)   # [{"name","value"}]
     oom_score_adj: int | None = None                  # qos.oom_score_adj (CRI LinuxContainerResources)
     cgroup_parent: str | None = None                  # pod cgroup directory (cgroups.CgroupManager)
+    attempt: int = 0                                  # restart count (CRI ContainerMetadata.attempt)
 
     @classmethod
     def from_device_opts(cls, d):
@@ -101,3 +102,11 @@ class Runtime:
 
     def list_containers(self):
         return []
+
+    async def pod_states(self) -> dict:
+        """What survives a kubelet restart (kuberuntime `GetPods`): pod uid -> {"sandboxes":
+        [(sandbox id, ready, ip or None)], "containers": [(container name, id, attempt, created_at,
+        sandbox id)]}.
+        The restarted kubelet adopts them instead of starting the pod again. Runtimes whose state
+        does not outlive the kubelet return {}."""
+        return {}

@@ -173,7 +173,8 @@ class ProcessRuntime(Runtime):
         self.containers[cid] = st
         self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "argv": argv, "env": env,
                           "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec,
-                          "oom_score_adj": opts.oom_score_adj, "cgroup": opts.cgroup_parent}
+                          "oom_score_adj": opts.oom_score_adj, "cgroup": opts.cgroup_parent,
+                          "attempt": opts.attempt}
         return cid
 
     @staticmethod
@@ -213,6 +214,20 @@ class ProcessRuntime(Runtime):
         st.state = RUNNING
         st.started_at = time.time()
         spawn(self._wait(cid, proc))
+
+    async def pod_states(self):
+        """In-process state only: the containers outlive the kubelet object (e.g. a restarted
+        kubelet in the same process), not the kubelet process."""
+        out: dict = {}
+        for sid, sb in self.sandboxes.items():
+            alive = sb["proc"].returncode is None
+            out.setdefault(sb["pod_uid"], {"sandboxes": [], "containers": []})["sandboxes"].append((sid, alive, None))
+        for cid, m in self.meta.items():
+            st = self.containers.get(cid)
+            if st is not None:
+                out.setdefault(m["pod_uid"], {"sandboxes": [], "containers": []})["containers"].append(
+                    (st.name, cid, m.get("attempt", 0), st.created_at, m["sandbox"]))
+        return out
 
     async def _wait(self, cid, proc):
         code = await proc.wait()

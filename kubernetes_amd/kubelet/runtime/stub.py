@@ -143,6 +143,18 @@ class StubRuntime(Runtime):
     def list_containers(self):
         return list(self.containers.values())
 
+    async def pod_states(self):
+        out: dict = {}
+        for sid, sb in self.sandboxes.items():
+            out.setdefault(sb["pod_uid"], {"sandboxes": [], "containers": []})["sandboxes"].append(
+                (sid, sb["state"] == "SANDBOX_READY", None))
+        for cid, m in self.meta.items():
+            st = self.containers.get(cid)
+            if st is not None:
+                out.setdefault(m["pod_uid"], {"sandboxes": [], "containers": []})["containers"].append(
+                    (st.name, cid, getattr(m["opts"], "attempt", 0), st.created_at, m["sandbox"]))
+        return out
+
     async def container_logs(self, cid, tail=None):
         st = self.containers.get(cid)
         return b"" if st is None else f"stub container {st.name} ({st.state})\n".encode()

@@ -237,3 +237,50 @@ def test_kubelet_on_remote_runtime(run, tmp_path):
             await rt.close()
             await srv.stop()
     run(main(), timeout=60)
+
+
+def test_kubelet_restart_adopts_pods_over_cri(run, tmp_path):
+    """kubelet restart with the runtime in its own process (the CRI split): the new kubelet
+    lists sandboxes and containers (ListPodSandbox / ListContainers, pod-uid labels) and adopts
+    them — same container ids, restart counts kept from the CRI attempt — instead of starting
+    the pods again."""
+    from kubernetes_amd.cluster import LocalCluster
+    from kubernetes_amd.kubelet.devicemanager.manager import ManagerStub
+    from kubernetes_amd.kubelet.kubelet import Kubelet
+    from kubernetes_amd.client.rest import Client
+
+    async def main():
+        sock = str(tmp_path / "cri.sock")
+        srv = await CRIServer(StubRuntime(), sock).start()
+        rt = await RemoteRuntime(sock, relist_period=0.05).connect()
+        cl = LocalCluster(nodes=0, gpus_per_node=0)
+        await cl.start()
+        rt2 = None
+        try:
+            h = await cl.add_node("n-cri", runtime=rt)
+            c = cl.client
+            await c.create("pods", {"metadata": {"name": "keep", "namespace": "default"},
+                                    "spec": {"nodeName": "n-cri", "containers": [{"name": "c", "image": "img:1"}]}})
+            p = await cl.wait_pod("keep")
+            cid = p["status"]["containerStatuses"][0]["containerID"]
+            await h.kubelet.stop()
+            await rt.close()
+            # a new runtime client + kubelet, as after a kubelet process restart
+            rt2 = await RemoteRuntime(sock, relist_period=0.05).connect()
+            kl2 = Kubelet(Client(cl.url), "n-cri", rt2, ManagerStub(), root_dir=str(tmp_path / "kl2"))
+            await kl2.run()
+            h.kubelet = kl2
+            await cl.wait_for(lambda: asyncio.sleep(0, result=kl2.adopted_pods == 1), timeout=10)
+            await asyncio.sleep(0.3)
+            p = await c.get("pods", "keep", "default")
+            cs = p["status"]["containerStatuses"][0]
+            assert cs["containerID"] == cid and cs["restartCount"] == 0 and p["status"]["phase"] == "Running"
+            lst = await srv.rt.pod_states()
+            assert sum(len(v["sandboxes"]) for v in lst.values()) == 1     # nothing started twice
+            assert sum(len(v["containers"]) for v in lst.values()) == 1
+        finally:
+            await cl.stop()
+            if rt2 is not None:
+                await rt2.close()
+            await srv.stop()
+    run(main(), timeout=60)

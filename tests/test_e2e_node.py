@@ -183,3 +183,64 @@ def test_node_density_remote_runtime_small():
                                        runtime="remote"))
     assert out["runtime"] == "remote" and out["batch"]["all_running_s"] < 25
     assert 0 < out["runtime_rss_mib"] < 500 and "p95" in out["runtime_cpu_cores"]
+
+
+def test_gpu_device_plugin_restart_and_plugin_removal(run):
+    """The reference's e2e_node GPU device-plugin test (`test/e2e_node/gpu_device_plugin.go:46-143`):
+    pods get distinct GPUs; after a kubelet restart the pods keep running with the same
+    containers and device assignment (the new kubelet adopts them and re-runs AdmitPod); after
+    the device plugin is deleted, GPU capacity drops to 0 and the pods keep running."""
+    from kubernetes_amd.client.rest import Client
+    from kubernetes_amd.kubelet.devicemanager.manager import ManagerImpl
+    from kubernetes_amd.kubelet.kubelet import Kubelet
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8) as cl:
+            c = cl.client
+            h = cl.nodes[0]
+            for n in ("gp0", "gp1", "gp2"):
+                await c.create("pods", gpu_pod(n, cmd=["sleep", "3600"]))
+            before = {}
+            for n in ("gp0", "gp1", "gp2"):
+                p = await cl.wait_pod(n)
+                before[n] = (p["spec"]["extendedResources"][0]["assigned"], p["status"]["containerStatuses"][0]["containerID"])
+            assert set(before["gp1"][0]).isdisjoint(before["gp2"][0])
+            gone_uid = (await c.get("pods", "gp0", "default"))["metadata"]["uid"]
+            # restart the kubelet on the same runtime and plugin directory; gp0 is force-deleted
+            # while it is down (its sandbox becomes an orphan the new kubelet removes)
+            await h.kubelet.stop()
+            await c.delete("pods", "gp0", "default", grace_period=0)
+            dm2 = ManagerImpl(h.plugins_dir)
+            kl2 = Kubelet(Client(cl.url), h.name, h.runtime, dm2, root_dir=os.path.join(cl.dir, h.name))
+            kl2.smi = cl.smi
+            kl2.orphan_grace = 0.2
+            await kl2.run()
+            h.kubelet, h.dm = kl2, dm2
+            await cl.wait_for(lambda: asyncio.sleep(0, result=kl2.adopted_pods == 2), timeout=10)
+            for n in ("gp1", "gp2"):
+                p = await cl.wait_pod(n)
+                cs = p["status"]["containerStatuses"][0]
+                assert (p["spec"]["extendedResources"][0]["assigned"], cs["containerID"]) == before[n]
+                assert cs["restartCount"] == 0 and cs["ready"]
+            await cl.wait_for(lambda: asyncio.sleep(0, result=all(
+                dm2.pod_resources(kl2.pods[u].pod) is not None for u in kl2.pods)), timeout=10)
+            await cl.wait_for(lambda: asyncio.sleep(0, result=not any(
+                sb["pod_uid"] == gone_uid for sb in h.runtime.sandboxes.values())), timeout=10)
+            # a new pod after the restart still gets a GPU nobody holds
+            await c.create("pods", gpu_pod("gp3", cmd=["sleep", "3600"]))
+            p3 = await cl.wait_pod("gp3")
+            taken = set(before["gp1"][0]) | set(before["gp2"][0])
+            assert taken.isdisjoint(p3["spec"]["extendedResources"][0]["assigned"])
+            # delete the device plugin: capacity goes to 0, running pods are untouched
+            await h.plugin.stop()
+            h.plugin = None
+
+            async def zero():
+                node = await c.get("nodes", h.name)
+                return node["status"]["capacity"].get(core.AMD_GPU) in ("0", None)
+            await cl.wait_for(zero, timeout=15)
+            for n in ("gp1", "gp2"):
+                p = await c.get("pods", n, "default")
+                assert p["status"]["phase"] == "Running"
+                assert p["status"]["containerStatuses"][0]["containerID"] == before[n][1]
+    run(main(), timeout=120)
