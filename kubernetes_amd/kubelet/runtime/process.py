@@ -10,6 +10,13 @@
   * GPUs     = without device namespaces the runtime narrows HIP enumeration itself:
                `AMD_VISIBLE_DEVICES` from the device plugin becomes `HIP_VISIBLE_DEVICES`.
 Exit is observed by awaiting the child (event-driven PLEG), like a CRI event stream.
+
+Restart survival (docker keeps containers when the kubelet restarts): every sandbox and
+container writes `state.json` next to its files (pid + kernel start time, pod uid, name, CRI
+attempt, exit code once known). A runtime constructed on the same root re-adopts the processes
+that are still alive (same pid AND start time, so a recycled pid is never adopted) and watches
+them with a pidfd; their exit code is unknowable (not our children) and reads as 255
+"ExitCodeUnknown". `pod_states()` hands them to the restarted kubelet.
 """
 from __future__ import annotations
 
@@ -24,6 +31,77 @@ import time
 from ...native import BIN_DIR
 from . import oci
 from .base import CREATED, EXITED, RUNNING, ContainerStatus, Runtime, RunContainerOptions
+
+UNKNOWN_EXIT = 255
+
+
+def _start_ticks(pid):
+    """Kernel start time of pid (clock ticks since boot, /proc/<pid>/stat field 22) or None."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            data = f.read()
+        return int(data[data.rindex(")") + 2:].split()[19])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+class _AdoptedProcess:
+    """A process started by an earlier runtime instance (not our child): asyncio.Process-like
+    pid / returncode / wait / terminate / kill, exit observed through a pidfd."""
+
+    def __init__(self, pid, ticks):
+        self.pid, self.ticks = pid, ticks
+        self.returncode = None if _start_ticks(pid) == ticks else UNKNOWN_EXIT
+        self._done = None
+
+    async def wait(self):
+        if self.returncode is not None:
+            return self.returncode
+        loop = asyncio.get_running_loop()
+        if self._done is None:
+            self._done = loop.create_future()
+            try:
+                fd = os.pidfd_open(self.pid)
+            except (OSError, AttributeError):
+                fd = None
+            if fd is not None:
+                def ready():
+                    loop.remove_reader(fd)
+                    os.close(fd)
+                    self.returncode = UNKNOWN_EXIT
+                    if not self._done.done():
+                        self._done.set_result(None)
+                loop.add_reader(fd, ready)
+            else:
+                async def poll():
+                    while _start_ticks(self.pid) == self.ticks:
+                        await asyncio.sleep(0.2)
+                    self.returncode = UNKNOWN_EXIT
+                    self._done.set_result(None)
+                spawn(poll())
+        await asyncio.shield(self._done)
+        return self.returncode
+
+    def terminate(self):
+        os.kill(self.pid, signal.SIGTERM)
+
+    def kill(self):
+        os.kill(self.pid, signal.SIGKILL)
+
+
+def _write_state(d, state):
+    tmp = os.path.join(d, "state.json.tmp")
+    with open(tmp, "w") as f:
+        json.dump(state, f, separators=(",", ":"))
+    os.replace(tmp, os.path.join(d, "state.json"))
+
+
+def _read_state(d):
+    try:
+        with open(os.path.join(d, "state.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 from ...utils.tasks import spawn
 
 IMAGES = {
@@ -104,11 +182,74 @@ class ProcessRuntime(Runtime):
         self.root = os.path.abspath(root_dir)
         os.makedirs(os.path.join(self.root, "containers"), exist_ok=True)
         os.makedirs(os.path.join(self.root, "sandboxes"), exist_ok=True)
-        self._ids = itertools.count(1)
         self.sandboxes: dict[str, dict] = {}
         self.containers: dict[str, ContainerStatus] = {}
         self.meta: dict[str, dict] = {}
         self.inherit_env = inherit_env
+        self._ids = itertools.count(self._load_state() + 1)
+
+    def _load_state(self) -> int:
+        """Re-adopt sandboxes/containers an earlier runtime instance on this root left running
+        (or exited with a recorded code). Returns the highest id in use."""
+        top = 0
+        sdir = os.path.join(self.root, "sandboxes")
+        for sid in sorted(os.listdir(sdir)):
+            st = _read_state(os.path.join(sdir, sid))
+            try:
+                top = max(top, int(sid[2:].split("-", 1)[0]))
+            except ValueError:
+                pass
+            if not st:
+                continue
+            self.sandboxes[sid] = {"proc": _AdoptedProcess(st["pid"], st.get("ticks")), "dir": os.path.join(sdir, sid),
+                                   "pod_uid": st["pod_uid"], "annotations": st.get("annotations") or {}}
+        cdir = os.path.join(self.root, "containers")
+        for name in sorted(os.listdir(cdir)):
+            d = os.path.join(cdir, name)
+            st = _read_state(d)
+            try:
+                top = max(top, int(name.split("-", 1)[0]))
+            except ValueError:
+                pass
+            if not st or st.get("sandbox") not in self.sandboxes:
+                continue
+            cid = st["id"]
+            cs = ContainerStatus(cid, st["name"], CREATED, image=st.get("image", ""), log_path=os.path.join(d, "log"))
+            cs.created_at = st.get("created_at", cs.created_at)
+            cs.started_at = st.get("started_at", 0.0)
+            proc = None
+            if "exit_code" in st:
+                cs.state, cs.exit_code, cs.reason = EXITED, st["exit_code"], st.get("reason", "")
+                cs.finished_at = st.get("finished_at", 0.0)
+            elif st.get("pid"):
+                proc = _AdoptedProcess(st["pid"], st.get("ticks"))
+                if proc.returncode is None:
+                    cs.state = RUNNING
+                else:
+                    cs.state, cs.exit_code, cs.reason = EXITED, UNKNOWN_EXIT, "ExitCodeUnknown"
+                    cs.finished_at = time.time()
+            self.containers[cid] = cs
+            self.meta[cid] = {"sandbox": st["sandbox"], "pod_uid": st["pod_uid"], "argv": st.get("argv") or [],
+                              "env": st.get("env") or {}, "cwd": st.get("cwd"), "proc": proc, "dir": d, "spec": None,
+                              "oom_score_adj": None, "cgroup": None, "attempt": st.get("attempt", 0),
+                              "adopted": proc is not None and proc.returncode is None}
+        return top
+
+    def _container_state(self, cid, **extra):
+        m, cs = self.meta.get(cid), self.containers.get(cid)
+        if m is None or cs is None:
+            return
+        proc = m.get("proc")
+        st = {"id": cid, "name": cs.name, "pod_uid": m["pod_uid"], "sandbox": m["sandbox"], "attempt": m.get("attempt", 0),
+              "image": cs.image, "created_at": cs.created_at, "started_at": cs.started_at, "argv": m["argv"],
+              "env": m["env"], "cwd": m["cwd"]}
+        if proc is not None:
+            st["pid"], st["ticks"] = proc.pid, _start_ticks(proc.pid)
+        st.update(extra)
+        try:
+            _write_state(m["dir"], st)
+        except OSError:
+            pass
 
     async def run_pod_sandbox(self, pod, annotations):
         sid = f"sb{next(self._ids)}-{pod['metadata']['uid'][:8]}"
@@ -119,6 +260,8 @@ class ProcessRuntime(Runtime):
         proc = await asyncio.create_subprocess_exec(os.path.join(BIN_DIR, "pause"), start_new_session=True,
                                                     stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL)
         self.sandboxes[sid] = {"proc": proc, "dir": d, "pod_uid": pod["metadata"]["uid"], "annotations": annotations}
+        _write_state(d, {"pod_uid": pod["metadata"]["uid"], "pid": proc.pid, "ticks": _start_ticks(proc.pid),
+                         "annotations": annotations or {}})
         return sid
 
     async def stop_pod_sandbox(self, sid):
@@ -144,7 +287,12 @@ class ProcessRuntime(Runtime):
         for cid, m in list(self.meta.items()):
             if m["sandbox"] == sid:
                 await self.remove_container(cid)
-        self.sandboxes.pop(sid, None)
+        sb = self.sandboxes.pop(sid, None)
+        if sb is not None:
+            try:
+                os.unlink(os.path.join(sb["dir"], "state.json"))
+            except OSError:
+                pass
 
     async def create_container(self, sid, pod, container, opts: RunContainerOptions):
         cid = f"process://{next(self._ids)}-{container['name']}"
@@ -213,11 +361,15 @@ class ProcessRuntime(Runtime):
         m["proc"] = proc
         st.state = RUNNING
         st.started_at = time.time()
+        self._container_state(cid)
         spawn(self._wait(cid, proc))
 
     async def pod_states(self):
-        """In-process state only: the containers outlive the kubelet object (e.g. a restarted
-        kubelet in the same process), not the kubelet process."""
+        """Sandboxes/containers of this runtime, including the ones re-adopted from state.json
+        after a restart (their exits are watched from here on)."""
+        for cid, m in self.meta.items():
+            if m.pop("adopted", False):
+                spawn(self._wait(cid, m["proc"]))
         out: dict = {}
         for sid, sb in self.sandboxes.items():
             alive = sb["proc"].returncode is None
@@ -237,8 +389,10 @@ class ProcessRuntime(Runtime):
         if st.state != EXITED:
             st.state = EXITED
             st.exit_code = code if code >= 0 else 128 - code
-            st.reason = "Completed" if code == 0 else "Error"
+            st.reason = ("Completed" if code == 0 else "Error") if code != UNKNOWN_EXIT or \
+                not isinstance(proc, _AdoptedProcess) else "ExitCodeUnknown"
             st.finished_at = time.time()
+        self._container_state(cid, exit_code=st.exit_code, reason=st.reason, finished_at=st.finished_at)
         self._fire_exit(self.meta[cid]["pod_uid"], cid)
 
     async def stop_container(self, cid, timeout):
@@ -271,7 +425,12 @@ class ProcessRuntime(Runtime):
     async def remove_container(self, cid):
         await self.stop_container(cid, 0)
         self.containers.pop(cid, None)
-        self.meta.pop(cid, None)
+        m = self.meta.pop(cid, None)
+        if m is not None:
+            try:
+                os.unlink(os.path.join(m["dir"], "state.json"))
+            except OSError:
+                pass
 
     def container_status(self, cid):
         return self.containers.get(cid)

@@ -244,3 +244,45 @@ def test_gpu_device_plugin_restart_and_plugin_removal(run):
                 assert p["status"]["phase"] == "Running"
                 assert p["status"]["containerStatuses"][0]["containerID"] == before[n][1]
     run(main(), timeout=120)
+
+
+def test_process_runtime_state_survives_runtime_restart(tmp_path):
+    """A new ProcessRuntime on the same root (a restarted kubelet process) re-adopts the live
+    sandbox and container from their state.json (pid + kernel start time), watches the adopted
+    container's exit through a pidfd, keeps recorded exit codes, and never adopts a dead pid."""
+    from kubernetes_amd.kubelet.runtime.base import EXITED, RUNNING, RunContainerOptions
+    from kubernetes_amd.kubelet.runtime.process import ProcessRuntime
+
+    async def main():
+        pod = {"metadata": {"name": "p", "namespace": "default", "uid": "uid-1234"}, "spec": {}}
+        a = ProcessRuntime(str(tmp_path / "rt"))
+        sid = await a.run_pod_sandbox(pod, {})
+        c1 = await a.create_container(sid, pod, {"name": "long", "command": ["sleep", "30"]}, RunContainerOptions(attempt=2))
+        await a.start_container(c1)
+        c2 = await a.create_container(sid, pod, {"name": "short", "command": ["sh", "-c", "exit 3"]}, RunContainerOptions())
+        await a.start_container(c2)
+        for _ in range(200):
+            if a.container_status(c2).state == EXITED:
+                break
+            await asyncio.sleep(0.01)
+        b = ProcessRuntime(str(tmp_path / "rt"))                       # "restarted" runtime
+        states = await b.pod_states()
+        ps = states["uid-1234"]
+        assert ps["sandboxes"] == [(sid, True, None)]
+        got = {name: (cid, attempt) for name, cid, attempt, _, _ in ps["containers"]}
+        assert got["long"] == (c1, 2) and b.container_status(c1).state == RUNNING
+        assert b.container_status(c2).state == EXITED and b.container_status(c2).exit_code == 3
+        exits = []
+        b.on_exit(lambda uid, cid: exits.append(cid))
+        await b.stop_container(c1, 1)
+        assert b.container_status(c1).state == EXITED
+        for _ in range(200):
+            if c1 in exits:
+                break
+            await asyncio.sleep(0.01)
+        assert c1 in exits
+        await b.remove_pod_sandbox(sid)
+        c = ProcessRuntime(str(tmp_path / "rt"))
+        assert await c.pod_states() == {}                              # removed state is gone
+        await a.remove_pod_sandbox(sid)
+    asyncio.run(main())
