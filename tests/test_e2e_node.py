@@ -286,3 +286,91 @@ def test_process_runtime_state_survives_runtime_restart(tmp_path):
         assert await c.pod_states() == {}                              # removed state is gone
         await a.remove_pod_sandbox(sid)
     asyncio.run(main())
+
+
+def test_kubelet_process_restart_keeps_pods_running(tmp_path):
+    """A real kubelet process (process runtime) is stopped and started again on the same root
+    dir: the pod's container process survives, the new kubelet adopts it (same container id,
+    restart count 0), and deleting the pod afterwards still kills it."""
+    import signal
+    import subprocess
+    import sys
+    import time as _t
+    from kubernetes_amd.client.rest import Client
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+
+    def spawn(args, name):
+        return subprocess.Popen([sys.executable, "-m"] + args, env=env, stdout=subprocess.DEVNULL,
+                                stderr=open(tmp_path / f"{name}.log", "w"))
+
+    pf = tmp_path / "api.port"
+    procs = [spawn(["kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", str(pf)], "api")]
+    kl_args = None
+    try:
+        t0 = _t.time()
+        while not pf.exists():
+            assert _t.time() - t0 < 60
+            _t.sleep(0.05)
+        url = f"http://127.0.0.1:{pf.read_text().strip()}"
+        procs.append(spawn(["kubernetes_amd.cmd.scheduler", "--master", url], "sched"))
+        kl_args = ["kubernetes_amd.cmd.kubelet", "--api-servers", url, "--hostname-override", "restart-node",
+                   "--root-dir", str(tmp_path / "kubelet"), "--container-runtime", "process", "--port", "0",
+                   "--container-log-dir", ""]
+        kl = spawn(kl_args, "kubelet1")
+
+        async def main():
+            nonlocal kl
+            c = Client(url)
+
+            async def wait(pred, timeout=30):
+                end = _t.time() + timeout
+                while _t.time() < end:
+                    v = await pred()
+                    if v:
+                        return v
+                    await asyncio.sleep(0.05)
+                raise AssertionError("timeout")
+
+            async def running():
+                try:
+                    p = await c.get("pods", "survivor", "default")
+                except Exception:
+                    return None
+                return p if (p.get("status") or {}).get("phase") == "Running" else None
+            await wait(lambda: c.list("nodes"))
+            await c.create("pods", {"metadata": {"name": "survivor", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "300"]}]}})
+            p = await wait(running)
+            cid = p["status"]["containerStatuses"][0]["containerID"]
+            state = json.load(open(tmp_path / "kubelet" / "runtime" / "containers" / cid.split("://")[1] / "state.json"))
+            pid = state["pid"]
+            kl.send_signal(signal.SIGTERM)
+            kl.wait(20)
+            os.kill(pid, 0)                                   # the container outlived the kubelet
+            kl = spawn(kl_args, "kubelet2")
+            await asyncio.sleep(2.0)
+            p = await wait(running)
+            cs = p["status"]["containerStatuses"][0]
+            assert cs["containerID"] == cid and cs["restartCount"] == 0
+            os.kill(pid, 0)
+            await c.delete("pods", "survivor", "default")
+
+            async def dead():
+                try:
+                    os.kill(pid, 0)
+                except ProcessLookupError:
+                    return True
+                return False
+            await wait(dead)
+            await c.close()
+        asyncio.run(main())
+    finally:
+        for p in procs + ([kl] if kl_args else []):
+            p.terminate()
+        for p in procs + ([kl] if kl_args else []):
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
