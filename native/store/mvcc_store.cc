@@ -52,6 +52,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -60,6 +61,9 @@ namespace kamd {
 struct KV {
   int64_t create_rev = 0, mod_rev = 0, version = 0;
   std::string value;
+  // server-side parse cache of the value's index frame (watch fan-out): a value is immutable, so
+  // its header is parsed once — as an event's new state and again as the next event's `prev`
+  mutable std::shared_ptr<void> aux;
 };
 
 struct Event {
@@ -426,6 +430,34 @@ void kamd_store_compact(kamd_store* s, int64_t rev) { s->eng.compact(rev); }
 #ifdef KAMD_STORE_SERVER
 namespace kamd {
 
+// KAMD_ETCD_PROFILE=1: time spent per activity, printed to stderr at shutdown (where the
+// store's CPU goes under a given API load; there is no perf on the GPU boxes).
+struct Prof {
+  bool on = false;
+  const char* names[12] = {"read+parse", "txn", "get", "range", "watch", "dispatch(workers)", "fan_dispatch",
+                           "flush(conns)", "flush(fan)", "progress", "handoff", "other"};
+  double ns[12] = {0};
+  uint64_t n[12] = {0};
+  static double now() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e9 + ts.tv_nsec;
+  }
+  void add(int k, double t0) { ns[k] += now() - t0; ++n[k]; }
+  void print() const {
+    if (!on) return;
+    double tot = 0;
+    for (double v : ns) tot += v;
+    fprintf(stderr, "kamd-etcd profile (ms total / count / us avg):\n");
+    for (int k = 0; k < 12; ++k)
+      if (n[k]) fprintf(stderr, "  %-18s %10.1f ms %10llu %8.2f us  %5.1f%%\n", names[k], ns[k] / 1e6,
+                        (unsigned long long)n[k], ns[k] / 1e3 / n[k], tot ? 100 * ns[k] / tot : 0);
+  }
+};
+static Prof g_prof;
+#define KPROF_BEGIN double _kp0 = g_prof.on ? Prof::now() : 0
+#define KPROF_END(k) do { if (g_prof.on) g_prof.add((k), _kp0); } while (0)
+
 struct Conn {
   int fd;
   std::string in, out;
@@ -460,15 +492,27 @@ struct Watch {
 // Python work in every API server worker (reference: staging/.../apiserver/pkg/storage/cacher.go
 // dispatchEvent + indexed watchers). Values must carry the shared-store index frame
 // (00 'K' 'H' | u32 len | JSON [fields, labels] | object JSON).
+// Field/label maps of a value's index frame as views into the value (decoded copies only for
+// strings with JSON escapes, kept in `owned`): no allocation per key in the common case.
+typedef std::vector<std::pair<std::string_view, std::string_view>> SVMap;
+
+static const std::string_view* sv_find(const SVMap& m, std::string_view k) {
+  for (const auto& kv : m)
+    if (kv.first == k) return &kv.second;
+  return nullptr;
+}
+
 struct Index {
   bool ok = false;
-  std::map<std::string, std::string> fields, labels;
+  SVMap fields, labels;
+  std::deque<std::string> owned;
   size_t body = 0;  // offset of the object JSON in the value
 };
 
 struct JsonCursor {
   const char* p;
   const char* e;
+  Index* ix;
   bool ok = true;
   void ws() { while (p < e && (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r')) ++p; }
   bool eat(char c) { ws(); if (p < e && *p == c) { ++p; return true; } return false; }
@@ -478,64 +522,94 @@ struct JsonCursor {
     else { o->push_back((char)(0xE0 | (cp >> 12))); o->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
            o->push_back((char)(0x80 | (cp & 0x3F))); }
   }
-  bool str(std::string* o) {
+  bool str(std::string_view* out) {
     ws();
     if (p >= e || *p != '"') return ok = false;
-    ++p;
+    const char* s0 = ++p;
+    while (p < e && *p != '"' && *p != '\\') ++p;
+    if (p < e && *p == '"') {           // no escapes: a view into the value
+      *out = std::string_view(s0, (size_t)(p - s0));
+      ++p;
+      return true;
+    }
+    std::string o(s0, (size_t)(p - s0));
     while (p < e && *p != '"') {
       if (*p == '\\') {
         if (++p >= e) return ok = false;
         char c = *p++;
         switch (c) {
-          case 'n': o->push_back('\n'); break;
-          case 't': o->push_back('\t'); break;
-          case 'r': o->push_back('\r'); break;
-          case 'b': o->push_back('\b'); break;
-          case 'f': o->push_back('\f'); break;
+          case 'n': o.push_back('\n'); break;
+          case 't': o.push_back('\t'); break;
+          case 'r': o.push_back('\r'); break;
+          case 'b': o.push_back('\b'); break;
+          case 'f': o.push_back('\f'); break;
           case 'u': {
             if (e - p < 4) return ok = false;
             unsigned cp = (unsigned)strtoul(std::string(p, 4).c_str(), nullptr, 16);
             p += 4;
-            utf8(o, cp);
+            utf8(&o, cp);
             break;
           }
-          default: o->push_back(c);
+          default: o.push_back(c);
         }
       } else {
-        o->push_back(*p++);
+        o.push_back(*p++);
       }
     }
     if (p >= e) return ok = false;
     ++p;
+    ix->owned.push_back(std::move(o));
+    *out = ix->owned.back();
     return true;
   }
   // {"k":"v",...} with string values (anything else fails the parse)
-  bool obj(std::map<std::string, std::string>* m) {
+  bool obj(SVMap* m) {
     if (!eat('{')) return ok = false;
     if (eat('}')) return true;
     do {
-      std::string k, v;
+      std::string_view k, v;
       if (!str(&k) || !eat(':') || !str(&v)) return ok = false;
-      (*m)[k] = v;
+      bool dup = false;
+      for (auto& kv : *m)
+        if (kv.first == k) { kv.second = v; dup = true; break; }
+      if (!dup) m->emplace_back(k, v);
     } while (eat(','));
     return eat('}') || (ok = false);
   }
 };
 
-static Index parse_index(const std::string& v) {
-  Index ix;
-  if (v.size() < 7 || v[0] != '\0' || v[1] != 'K' || v[2] != 'H') return ix;
+static void parse_index_into(const std::string& v, Index* ix) {
+  if (v.size() < 7 || v[0] != '\0' || v[1] != 'K' || v[2] != 'H') return;
   uint32_t hl;
   memcpy(&hl, v.data() + 3, 4);
-  if (7 + (size_t)hl > v.size()) return ix;
-  JsonCursor c{v.data() + 7, v.data() + 7 + hl};
-  if (!c.eat('[') || !c.obj(&ix.fields) || !c.eat(',') || !c.obj(&ix.labels) || !c.eat(']')) return ix;
-  ix.body = 7 + hl;
-  ix.ok = true;
-  return ix;
+  if (7 + (size_t)hl > v.size()) return;
+  JsonCursor c{v.data() + 7, v.data() + 7 + hl, ix};
+  ix->fields.reserve(8);
+  if (!c.eat('[') || !c.obj(&ix->fields) || !c.eat(',') || !c.obj(&ix->labels) || !c.eat(']')) {
+    ix->fields.clear();
+    ix->labels.clear();
+    return;
+  }
+  ix->body = 7 + hl;
+  ix->ok = true;
 }
 
-static uint32_t crc32_ieee(const std::string& s) {   // zlib.crc32
+// the parsed index frame of a stored value, cached on the KV
+static const Index& index_of(const KV& kv) {
+  if (!kv.aux) {
+    auto ix = std::make_shared<Index>();
+    parse_index_into(kv.value, ix.get());
+    kv.aux = ix;
+  }
+  return *static_cast<const Index*>(kv.aux.get());
+}
+
+static const Index& empty_index() {
+  static const Index e;
+  return e;
+}
+
+static uint32_t crc32_ieee(std::string_view s) {   // zlib.crc32
   static uint32_t table[256];
   static bool init = false;
   if (!init) {
@@ -554,14 +628,18 @@ static uint32_t crc32_ieee(const std::string& s) {   // zlib.crc32
 // scheduler-shard selection (kubernetes_amd/api/sharding.py): (crc32("ns/name") + offset label) % n == i
 static bool shard_match(const Index& ix, const std::string& offset_label, int64_t n, int64_t i) {
   if (n < 1) return false;
-  auto ns = ix.fields.find("metadata.namespace");
-  auto nm = ix.fields.find("metadata.name");
-  std::string key = (ns == ix.fields.end() ? std::string() : ns->second) + "/" +
-                    (nm == ix.fields.end() ? std::string() : nm->second);
+  const std::string_view* ns = sv_find(ix.fields, "metadata.namespace");
+  const std::string_view* nm = sv_find(ix.fields, "metadata.name");
+  std::string key;
+  key.reserve(64);
+  if (ns) key.append(ns->data(), ns->size());
+  key.push_back('/');
+  if (nm) key.append(nm->data(), nm->size());
   int64_t off = 0;
-  auto ol = ix.labels.find(offset_label);
-  if (ol != ix.labels.end() && !ol->second.empty()) {
-    const char* b = ol->second.c_str();
+  const std::string_view* ol = sv_find(ix.labels, offset_label);
+  if (ol && !ol->empty()) {
+    std::string lv(ol->data(), ol->size());
+    const char* b = lv.c_str();
     char* e = nullptr;
     errno = 0;
     long long v = strtoll(b, &e, 10);
@@ -581,18 +659,20 @@ struct Requirement {
   bool matches(const Index& ix) const {
     if (op == 6)
       return vals.size() == 2 && shard_match(ix, key, atoll(vals[0].c_str()), atoll(vals[1].c_str()));
-    const auto& m = target == 0 ? ix.labels : ix.fields;
-    auto it = m.find(key);
+    const std::string_view* it = sv_find(target == 0 ? ix.labels : ix.fields, key);
     // a field that is absent reads as "" (fields.Set semantics); labels keep presence
-    bool has = it != m.end() || target == 1;
-    const std::string empty;
-    const std::string& v = it != m.end() ? it->second : empty;
-    auto in = [&]() { return std::find(vals.begin(), vals.end(), v) != vals.end(); };
+    bool has = it != nullptr || target == 1;
+    std::string_view v = it ? *it : std::string_view();
+    auto in = [&]() {
+      for (const std::string& x : vals)
+        if (v == x) return true;
+      return false;
+    };
     switch (op) {
       case 0: case 2: return has && in();
       case 1: case 3: return !has || !in();
-      case 4: return it != m.end();
-      case 5: return it == m.end();
+      case 4: return it != nullptr;
+      case 5: return it == nullptr;
     }
     return false;
   }
@@ -713,15 +793,27 @@ class Server {
         }
         if (evs[i].events & EPOLLOUT) flush(c);
       }
-      if (progress_pending_) send_progress();
-      // flush every connection with pending output once per loop (coalesces watch events)
-      for (Conn* c : dirty_) flush(c);
-      dirty_.clear();
-      for (FanWatch* w : fan_dirty_) {
-        w->queued = false;
-        flush_fan(w);
+      if (progress_pending_) {
+        KPROF_BEGIN;
+        send_progress();
+        KPROF_END(9);
       }
-      fan_dirty_.clear();
+      // flush every connection with pending output once per loop (coalesces watch events)
+      {
+        KPROF_BEGIN;
+        for (Conn* c : dirty_) flush(c);
+        dirty_.clear();
+        KPROF_END(7);
+      }
+      {
+        KPROF_BEGIN;
+        for (FanWatch* w : fan_dirty_) {
+          w->queued = false;
+          flush_fan(w);
+        }
+        fan_dirty_.clear();
+        KPROF_END(8);
+      }
       expire_fan();
       reap_fan();
     }
@@ -764,6 +856,11 @@ class Server {
   }
 
   bool read_conn(Conn* c) {
+    KPROF_BEGIN;
+    struct Done {
+      double t0;
+      ~Done() { if (g_prof.on) g_prof.add(0, t0); }
+    } done{_kp0};
     char buf[1 << 16];
     for (;;) {
       ssize_t n = read(c->fd, buf, sizeof buf);
@@ -858,17 +955,27 @@ class Server {
     Writer w;
     switch (op) {
       case 1: {  // TXN
+        KPROF_BEGIN;
         std::vector<Cmp> cmps;
         std::vector<Op> ops;
         if (!parse_txn(r, &cmps, &ops)) { reply(c, id, 9, ""); return; }
         int64_t rev;
         std::vector<Event> evs;
         int failed = eng_->txn(cmps, ops, &rev, &evs);
+        KPROF_END(1);
         if (failed < 0) {
           w.put<int64_t>(rev);
           reply(c, id, 0, w.b);
-          dispatch(evs);
-          fan_dispatch(evs);
+          {
+            KPROF_BEGIN;
+            dispatch(evs);
+            KPROF_END(5);
+          }
+          {
+            KPROF_BEGIN;
+            fan_dispatch(evs);
+            KPROF_END(6);
+          }
         } else {
           w.put<uint16_t>((uint16_t)failed);
           const KV* kv = eng_->get(cmps[failed].key);
@@ -880,6 +987,11 @@ class Server {
         return;
       }
       case 2: {  // GET
+        KPROF_BEGIN;
+        struct Done {
+          double t0;
+          ~Done() { if (g_prof.on) g_prof.add(2, t0); }
+        } done{_kp0};
         std::string k = r.str();
         const KV* kv = eng_->get(k);
         if (!kv) { w.put<int64_t>(eng_->rev()); reply(c, id, 4, w.b); return; }
@@ -889,6 +1001,11 @@ class Server {
         return;
       }
       case 3: {  // RANGE
+        KPROF_BEGIN;
+        struct Done {
+          double t0;
+          ~Done() { if (g_prof.on) g_prof.add(3, t0); }
+        } done{_kp0};
         std::string prefix = r.str();
         uint32_t limit = r.get<uint32_t>();
         std::string sa = r.str();
@@ -1051,7 +1168,7 @@ class Server {
              "Cache-Control: no-cache, private\r\n\r\n";
     if (send_initial) {
       eng_->for_prefix(w->prefix, [&](const std::string&, const KV& kv) {
-        Index ix = parse_index(kv.value);
+        const Index& ix = index_of(kv);
         if (w->matches(ix)) chunk(&w->out, "ADDED", kv.value, ix.body);
       });
     } else if (from > 0) {
@@ -1086,9 +1203,8 @@ class Server {
   // a DELETED for that watcher, one that starts matching an ADDED)
   void fan_one(FanWatch* w, const Event& ev, const Index* cur = nullptr, const Index* prv = nullptr) {
     if (ev.key.compare(0, w->prefix.size(), w->prefix) != 0 || ev.rev <= w->min_rev) return;
-    Index c0, p0;
-    if (!cur) { c0 = parse_index(ev.kv->value); cur = &c0; }
-    if (!prv) { if (ev.prev) p0 = parse_index(ev.prev->value); prv = &p0; }
+    if (!cur) cur = &index_of(*ev.kv);
+    if (!prv) prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
     bool now = w->matches(*cur);
     bool was = ev.prev && w->matches(*prv);
     const std::string& v = ev.kv->value;
@@ -1109,38 +1225,42 @@ class Server {
   void fan_dispatch(const std::vector<Event>& evs) {
     if (fan_.empty()) return;
     for (const Event& ev : evs) {
-      Index cur, prv;
-      bool parsed = false;
+      const Index* cur = nullptr;
+      const Index* prv = nullptr;
       auto parse = [&]() {
-        if (parsed) return;
-        cur = parse_index(ev.kv->value);
-        if (ev.prev) prv = parse_index(ev.prev->value);
-        parsed = true;
+        if (cur) return;
+        cur = &index_of(*ev.kv);
+        prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
       };
       for (FanWatch* w : fan_other_) {
         if (w->dead || ev.key.compare(0, w->prefix.size(), w->prefix) != 0) continue;
         parse();
-        fan_one(w, ev, &cur, &prv);
+        fan_one(w, ev, cur, prv);
       }
       if (fan_by_node_.empty()) continue;
       parse();
-      static const std::string kNode = "spec.nodeName";
       auto node_of = [](const Index& ix) -> std::string {
-        auto it = ix.fields.find(kNode);
-        return it == ix.fields.end() ? std::string() : it->second;
+        const std::string_view* it = sv_find(ix.fields, "spec.nodeName");
+        return it ? std::string(it->data(), it->size()) : std::string();
       };
-      std::string a = node_of(cur);
+      std::string a = node_of(*cur);
       auto bucket = [&](const std::string& n) {
         auto it = fan_by_node_.find(n);
         if (it == fan_by_node_.end()) return;
         for (FanWatch* w : it->second)
-          if (!w->dead) fan_one(w, ev, &cur, &prv);
+          if (!w->dead) fan_one(w, ev, cur, prv);
       };
       bucket(a);
       if (ev.prev) {
-        std::string b = node_of(prv);
+        std::string b = node_of(*prv);
         if (b != a) bucket(b);
       }
+    }
+    // a superseded value's parse is not needed again (resumed watches re-parse on demand):
+    // the cache lives on current values only, so history memory does not grow with it
+    for (const Event& ev : evs) {
+      if (ev.prev) ev.prev->aux.reset();
+      if (ev.type == 1) ev.kv->aux.reset();   // a tombstone is never a current value
     }
   }
 
@@ -1275,7 +1395,9 @@ int main(int argc, char** argv) {
     }
   }
   fprintf(stderr, "kamd-etcd: serving (rev %lld, %zu keys)\n", (long long)eng.rev(), eng.size());
+  kamd::g_prof.on = getenv("KAMD_ETCD_PROFILE") && *getenv("KAMD_ETCD_PROFILE") == '1';
   srv.run(&g_stop);
+  kamd::g_prof.print();
   if (unix_path) unlink(unix_path);
   if (handoff_path) unlink(handoff_path);
   return 0;
