@@ -435,7 +435,7 @@ namespace kamd {
 struct Prof {
   bool on = false;
   const char* names[12] = {"read+parse", "txn", "get", "range", "watch", "dispatch(workers)", "fan_dispatch",
-                           "flush(conns)", "flush(fan)", "progress", "handoff", "other"};
+                           "flush(conns)", "flush(fan)", "progress", "handoff", "fan writes (#)"};
   double ns[12] = {0};
   uint64_t n[12] = {0};
   static double now() {
@@ -1274,6 +1274,7 @@ class Server {
   void flush_fan(FanWatch* w) {
     while (!w->out.empty()) {
       ssize_t n = write(w->fd, w->out.data(), w->out.size());
+      if (g_prof.on) ++g_prof.n[11];   // "other": count of fan-out write() calls
       if (n > 0) { w->out.erase(0, (size_t)n); continue; }
       if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
         if (w->out.size() > (64u << 20)) { w->dead = true; w->out.clear(); return; }   // slow watcher
