@@ -24,7 +24,7 @@ typedef unsigned short u16;
 
 static thread_local char g_err[256];
 static int g_gemm_path = 0;   // 0 auto (8-phase 256-tile path when the shape allows), 1 force the 128-tile kernel,
-                              // 2 force the 2-barrier 256-tile glds kernel
+                              // 2 force the 2-barrier 256-tile glds kernel, 3 the ping-pong 256-tile kernel
 
 static int check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
@@ -459,6 +459,177 @@ gemm_bf16_nt_8ph_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Ou
 }  // namespace gemm8
 
 // ---------------------------------------------------------------------------
+// Ping-pong 256x256 path (cdna_hip_programming.md "The 256² 8-phase template": wave groups
+// staggered by one barrier). Same tile / wave geometry as gemm8 (8 waves = 2 groups (wave rows)
+// x 4 wave columns, 128x64 output per wave, 4 C-quadrants of 16 MFMA 16x16x32 per K-tile), but
+// every phase is   [ds_read this quadrant's fragments, stage glds] BARRIER [lgkmcnt(0), MFMAs] BARRIER
+// and group 1 runs ONE barrier behind group 0: between any two barriers one group's MFMA segment
+// sits beside the other group's load segment on every SIMD (each SIMD holds one wave of each
+// group), so the matrix pipe is fed while the partner wave waits on LDS and barriers.
+//   LDS: 2 K-tile parities x {A half 0 = rows 0..127 (group 0), A half 1 (group 1), B half 0 =
+//   cols 0..127, B half 1} x 16 KiB = 128 KiB; rows of 128 B with the conflict-free slot swizzle
+//   s ^ ((r >> 1) & 7) applied on the global side of global_load_lds.
+//   K-tile kt+1 is staged into the other parity during K-tile kt: A halves in phase 0, B halves
+//   in phase 1 (4 glds per thread); phase 3's load segment retires them (vmcnt(0)) before the
+//   barrier that precedes the first read of kt+1 (WAR on that parity: its last reads, K-tile
+//   kt-1 phase 2, were retired by lgkmcnt(0) one full segment before the first restage).
+namespace gemmpp {
+using gemm::xcd_remap;
+using gemm::store_out;
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int HALF_BYTES = 128 * BK * 2;          // 16 KiB
+constexpr int TILE_BYTES = 4 * HALF_BYTES;        // A0 A1 B0 B1 of one K-tile
+constexpr int LDS_BYTES = 2 * TILE_BYTES;         // 128 KiB
+typedef __attribute__((address_space(3))) void lds_void;
+
+#define KAMD_PP_BARRIER()                       \
+  do {                                          \
+    asm volatile("" ::: "memory");              \
+    __builtin_amdgcn_s_barrier();               \
+    asm volatile("" ::: "memory");              \
+  } while (0)
+#define KAMD_PP_LGKM0()                                   \
+  do {                                                    \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
+    __builtin_amdgcn_sched_barrier(0);                    \
+  } while (0)
+#define KAMD_PP_VM0()                                     \
+  do {                                                    \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      \
+    __builtin_amdgcn_sched_barrier(0);                    \
+  } while (0)
+
+template <typename OutT>
+__global__ void __launch_bounds__(THREADS, 1)
+gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
+                       int M, int N, int K, int ldc, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int GROUP = 4;
+  const int group_id = t / (GROUP * tiles_n);
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (t % (GROUP * tiles_n)) % gsz;
+  const int tn = (t % (GROUP * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: thread covers chunks q = j*512 + tid (j = 0, 1) of a half: row q>>3, slot q&7
+  size_t off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = j * THREADS + tid, r = q >> 3, slot = q & 7;
+    off[j] = (size_t)r * K + ((slot ^ ((r >> 1) & 7)) << 3);
+  }
+  const u16* src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 128) * K, B + (size_t)n0 * K,
+                       B + (size_t)(n0 + 128) * K};
+  auto stage = [&](int kt, int h) {
+    unsigned char* dst = lds + ((kt & 1) * 4 + h) * HALF_BYTES + wid * 1024;
+    const u16* s = src[h] + (size_t)kt * BK;
+    __builtin_amdgcn_global_load_lds((const void*)(s + off[0]), (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(s + off[1]), (lds_void*)(dst + THREADS * 16), 16, 0, 0);
+  };
+
+  const int wr = wid >> 2, wc = wid & 3;           // group = wave row
+  const int frow = lane & 15, fq = lane >> 4, lsw = (frow >> 1) & 7;
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][2][4], bfr[2][2][2];
+  auto read_a = [&](int kt, int mq) {
+    const unsigned char* base = lds + ((kt & 1) * 4 + wr) * HALF_BYTES + (mq * 64 + frow) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[mq][ks][i] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+  };
+  auto read_b = [&](int kt, int nq) {
+    const unsigned char* base = lds + ((kt & 1) * 4 + 2 + (wc >> 1)) * HALF_BYTES + ((wc & 1) * 64 + nq * 32 + frow) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[nq][ks][j] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+  };
+  auto mma = [&](int mq, int nq) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mq][ks][i], bfr[nq][ks][j], acc[mq][nq][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = K / BK;
+  stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
+  KAMD_PP_VM0();
+  KAMD_PP_BARRIER();                  // K-tile 0 published to every wave
+  if (wr == 1) KAMD_PP_BARRIER();     // group 1 runs one barrier behind group 0
+  for (int kt = 0; kt < nt; ++kt) {
+    const bool more = kt + 1 < nt;
+    // phase 0: A quadrant row 0 + B quadrant col 0; stage A halves of kt+1
+    read_a(kt, 0);
+    read_b(kt, 0);
+    if (more) { stage(kt + 1, 0); stage(kt + 1, 1); }
+    KAMD_PP_BARRIER();
+    KAMD_PP_LGKM0();
+    mma(0, 0);
+    KAMD_PP_BARRIER();
+    // phase 1: B quadrant col 1; stage B halves of kt+1
+    read_b(kt, 1);
+    if (more) { stage(kt + 1, 2); stage(kt + 1, 3); }
+    KAMD_PP_BARRIER();
+    KAMD_PP_LGKM0();
+    mma(0, 1);
+    KAMD_PP_BARRIER();
+    // phase 2: A quadrant row 1
+    read_a(kt, 1);
+    KAMD_PP_BARRIER();
+    KAMD_PP_LGKM0();
+    mma(1, 0);
+    KAMD_PP_BARRIER();
+    // phase 3: no reads; retire this wave's staging of kt+1 before the next K-tile's reads
+    if (more) KAMD_PP_VM0();
+    KAMD_PP_BARRIER();
+    mma(1, 1);
+    KAMD_PP_BARRIER();
+  }
+  if (wr == 0) KAMD_PP_BARRIER();     // balance group 1's extra barrier
+  // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = n0 + wc * 64 + nq * 32 + j * 16 + frow;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wr * 128 + mq * 64 + i * 16 + fq * 4 + r;
+            store_out<OutT>(C + (size_t)row * ldc + col, alpha * acc[mq][nq][i][j][r]);
+          }
+        }
+}
+#undef KAMD_PP_BARRIER
+#undef KAMD_PP_LGKM0
+#undef KAMD_PP_VM0
+}  // namespace gemmpp
+
+// ---------------------------------------------------------------------------
 // HBM streaming copy, 16 B per lane, grid-stride
 __global__ void __launch_bounds__(256) hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -554,6 +725,24 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
   if ((((uintptr_t)A) | ((uintptr_t)B)) & 15) {
     snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
     return -1;
+  }
+  if (g_gemm_path == 3 && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
+    static bool attrpp = false;
+    if (!attrpp) {
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
+      attrpp = true;
+    }
+    const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
+    if (out_fp32)
+      hipLaunchKernelGGL(gemmpp::gemm_bf16_nt_pp_kernel<float>, dim3(tiles), dim3(gemmpp::THREADS), gemmpp::LDS_BYTES,
+                         stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+    else
+      hipLaunchKernelGGL(gemmpp::gemm_bf16_nt_pp_kernel<__bf16>, dim3(tiles), dim3(gemmpp::THREADS), gemmpp::LDS_BYTES,
+                         stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+    return check(hipGetLastError(), "gemm ping-pong launch");
   }
   if (g_gemm_path == 0 && M % gemm8::BM == 0 && N % gemm8::BN == 0 && K % gemm8::BK == 0 && K / gemm8::BK >= 2) {
     static bool attr8 = false;
