@@ -498,6 +498,11 @@ typedef __attribute__((address_space(3))) void lds_void;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      \
     __builtin_amdgcn_sched_barrier(0);                    \
   } while (0)
+#define KAMD_WAIT_VMN(n)                                  \
+  do {                                                    \
+    asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); \
+    __builtin_amdgcn_sched_barrier(0);                    \
+  } while (0)
 
 template <typename OutT>
 __global__ void __launch_bounds__(THREADS, 1)
@@ -516,20 +521,31 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
   const int tn = (t % (GROUP * tiles_n)) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // staging: thread covers chunks q = j*512 + tid (j = 0, 1) of a half: row q>>3, slot q&7
-  size_t off[2];
+  // Half-tiles are split by the PHASE that first reads them (as in gemm8), so each phase waits
+  // only for its own data with a counted vmcnt and 3 half-tiles stay in flight:
+  //   h0 = A rows {g*128 + 0..63}  (mq = 0 of both groups)   read in phase 0
+  //   h1 = A rows {g*128 + 64..127} (mq = 1)                read in phase 2
+  //   h2 = B rows {wc*64 + 0..31}   (nq = 0, all 4 columns) read in phase 0
+  //   h3 = B rows {wc*64 + 32..63}  (nq = 1)                read in phase 1
+  // During K-tile kt, phase p stages half ORDER[p] = h0, h2, h3, h1 of K-tile kt+1 (2 glds per
+  // thread); the waits: vmcnt(4) after staging in phases 0, 1 and 3 (the half the next read
+  // segment needs is then the oldest outstanding one).
+  size_t offA[2], offB[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int q = j * THREADS + tid, r = q >> 3, slot = q & 7;
-    off[j] = (size_t)r * K + ((slot ^ ((r >> 1) & 7)) << 3);
+    const int kc = slot ^ ((r >> 1) & 7);
+    offA[j] = (size_t)((r >> 6) * 128 + (r & 63)) * K + (kc << 3);
+    offB[j] = (size_t)((r >> 5) * 64 + (r & 31)) * K + (kc << 3);
   }
-  const u16* src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 128) * K, B + (size_t)n0 * K,
-                       B + (size_t)(n0 + 128) * K};
+  const u16* half_src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 64) * K, B + (size_t)n0 * K,
+                            B + (size_t)(n0 + 32) * K};
   auto stage = [&](int kt, int h) {
     unsigned char* dst = lds + ((kt & 1) * 4 + h) * HALF_BYTES + wid * 1024;
-    const u16* s = src[h] + (size_t)kt * BK;
-    __builtin_amdgcn_global_load_lds((const void*)(s + off[0]), (lds_void*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(s + off[1]), (lds_void*)(dst + THREADS * 16), 16, 0, 0);
+    const u16* src = half_src[h] + (size_t)kt * BK;
+    const size_t* off = h < 2 ? offA : offB;
+    __builtin_amdgcn_global_load_lds((const void*)(src + off[0]), (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + off[1]), (lds_void*)(dst + THREADS * 16), 16, 0, 0);
   };
 
   const int wr = wid >> 2, wc = wid & 3;           // group = wave row
@@ -544,16 +560,16 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[2][2][4], bfr[2][2][2];
-  auto read_a = [&](int kt, int mq) {
-    const unsigned char* base = lds + ((kt & 1) * 4 + wr) * HALF_BYTES + (mq * 64 + frow) * 128;
+  auto read_a = [&](int kt, int mq) {   // half h = mq, local rows wr*64 + ...
+    const unsigned char* base = lds + ((kt & 1) * 4 + mq) * HALF_BYTES + (wr * 64 + frow) * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         af[mq][ks][i] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
   };
-  auto read_b = [&](int kt, int nq) {
-    const unsigned char* base = lds + ((kt & 1) * 4 + 2 + (wc >> 1)) * HALF_BYTES + ((wc & 1) * 64 + nq * 32 + frow) * 128;
+  auto read_b = [&](int kt, int nq) {   // half h = 2 + nq, local rows wc*32 + ...
+    const unsigned char* base = lds + ((kt & 1) * 4 + 2 + nq) * HALF_BYTES + (wc * 32 + frow) * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -573,35 +589,37 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
   };
 
   const int nt = K / BK;
-  stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
+  stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
   KAMD_PP_VM0();
   KAMD_PP_BARRIER();                  // K-tile 0 published to every wave
   if (wr == 1) KAMD_PP_BARRIER();     // group 1 runs one barrier behind group 0
   for (int kt = 0; kt < nt; ++kt) {
     const bool more = kt + 1 < nt;
-    // phase 0: A quadrant row 0 + B quadrant col 0; stage A halves of kt+1
-    read_a(kt, 0);
+    // phase 0: read B nq=0, A mq=0 (h2, h0); stage h0(kt+1); then h3(kt) must land for phase 1
     read_b(kt, 0);
-    if (more) { stage(kt + 1, 0); stage(kt + 1, 1); }
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(kt, 0);
+    if (more) { stage(kt + 1, 0); KAMD_WAIT_VMN(4); } else { KAMD_WAIT_VMN(2); }
     KAMD_PP_BARRIER();
     KAMD_PP_LGKM0();
     mma(0, 0);
     KAMD_PP_BARRIER();
-    // phase 1: B quadrant col 1; stage B halves of kt+1
+    // phase 1: read B nq=1 (h3); stage h2(kt+1); then h1(kt) must land for phase 2
     read_b(kt, 1);
-    if (more) { stage(kt + 1, 2); stage(kt + 1, 3); }
+    if (more) { stage(kt + 1, 2); KAMD_WAIT_VMN(4); } else { KAMD_PP_VM0(); }
     KAMD_PP_BARRIER();
     KAMD_PP_LGKM0();
     mma(0, 1);
     KAMD_PP_BARRIER();
-    // phase 2: A quadrant row 1
+    // phase 2: read A mq=1 (h1); stage h3(kt+1)
     read_a(kt, 1);
+    if (more) stage(kt + 1, 3);
     KAMD_PP_BARRIER();
     KAMD_PP_LGKM0();
     mma(1, 0);
     KAMD_PP_BARRIER();
-    // phase 3: no reads; retire this wave's staging of kt+1 before the next K-tile's reads
-    if (more) KAMD_PP_VM0();
+    // phase 3: no reads; stage h1(kt+1); then h0, h2 of kt+1 must land for its phase 0
+    if (more) { stage(kt + 1, 1); KAMD_WAIT_VMN(4); }
     KAMD_PP_BARRIER();
     mma(1, 1);
     KAMD_PP_BARRIER();
@@ -627,6 +645,7 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
 #undef KAMD_PP_BARRIER
 #undef KAMD_PP_LGKM0
 #undef KAMD_PP_VM0
+#undef KAMD_WAIT_VMN
 }  // namespace gemmpp
 
 // ---------------------------------------------------------------------------
