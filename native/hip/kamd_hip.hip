@@ -504,7 +504,10 @@ typedef __attribute__((address_space(3))) void lds_void;
     __builtin_amdgcn_sched_barrier(0);                    \
   } while (0)
 
-template <typename OutT>
+constexpr int EPI_STRIDE = 68;                    // fp32 row pitch of the LDS epilogue (bank spread)
+constexpr int EPI_BYTES = 8 * 64 * EPI_STRIDE * 4;  // 8 waves x 64 x 68 fp32 = 136 KiB
+
+template <typename OutT, bool TUNED>
 __global__ void __launch_bounds__(THREADS, 1)
 gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
                        int M, int N, int K, int ldc, float alpha) {
@@ -577,7 +580,7 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
         bfr[nq][ks][j] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
   };
   auto mma = [&](int mq, int nq) {
-    __builtin_amdgcn_s_setprio(1);
+    if (!TUNED) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -585,10 +588,13 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mq][ks][i], bfr[nq][ks][j], acc[mq][nq][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (!TUNED) __builtin_amdgcn_s_setprio(0);
   };
 
   const int nt = K / BK;
+  // TUNED: static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per
+  // SIMD" item 4) instead of per-segment flips
+  if (TUNED && wr == 1) __builtin_amdgcn_s_setprio(1);
   stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
   KAMD_PP_VM0();
   KAMD_PP_BARRIER();                  // K-tile 0 published to every wave
@@ -625,6 +631,43 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
     KAMD_PP_BARRIER();
   }
   if (wr == 0) KAMD_PP_BARRIER();     // balance group 1's extra barrier
+  if (TUNED) {
+    // epilogue through LDS (free now: every wave is past its last read and glds): each wave
+    // transposes a 64x64 fp32 quadrant row to row-major, then writes 16-B vectors (256 B per
+    // 16 lanes of a row) instead of 4-B scattered stores
+    __builtin_amdgcn_s_setprio(0);
+    float* ep = reinterpret_cast<float*>(lds) + wid * (64 * EPI_STRIDE);
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq) {
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[(i * 16 + fq * 4 + r) * EPI_STRIDE + nq * 32 + j * 16 + frow] = alpha * acc[mq][nq][i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int c4 = lane & 15;
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int row = it * 4 + (lane >> 4);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * EPI_STRIDE + c4 * 4);
+        OutT* dst = C + (size_t)(m0 + wr * 128 + mq * 64 + row) * ldc + n0 + wc * 64 + c4 * 4;
+        if constexpr (sizeof(OutT) == 4) {
+          *reinterpret_cast<f32x4*>(dst) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) store_out<OutT>(dst + e, v[e]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return;
+  }
   // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
@@ -745,22 +788,37 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
     snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
     return -1;
   }
-  if (g_gemm_path == 3 && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
+  if ((g_gemm_path == 3 || g_gemm_path == 4) && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
     static bool attrpp = false;
     if (!attrpp) {
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float>,
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float, false>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16>,
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16, false>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::EPI_BYTES));
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::EPI_BYTES));
       attrpp = true;
     }
     const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
-    if (out_fp32)
-      hipLaunchKernelGGL(gemmpp::gemm_bf16_nt_pp_kernel<float>, dim3(tiles), dim3(gemmpp::THREADS), gemmpp::LDS_BYTES,
-                         stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
-    else
-      hipLaunchKernelGGL(gemmpp::gemm_bf16_nt_pp_kernel<__bf16>, dim3(tiles), dim3(gemmpp::THREADS), gemmpp::LDS_BYTES,
-                         stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+    const bool tuned = g_gemm_path == 4;
+    const size_t lds = tuned ? gemmpp::EPI_BYTES : gemmpp::LDS_BYTES;
+    if (out_fp32) {
+      if (tuned)
+        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, true>), dim3(tiles), dim3(gemmpp::THREADS), lds,
+                           stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+      else
+        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, false>), dim3(tiles), dim3(gemmpp::THREADS), lds,
+                           stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+    } else {
+      if (tuned)
+        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, true>), dim3(tiles), dim3(gemmpp::THREADS), lds,
+                           stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+      else
+        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, false>), dim3(tiles), dim3(gemmpp::THREADS), lds,
+                           stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+    }
     return check(hipGetLastError(), "gemm ping-pong launch");
   }
   if (g_gemm_path == 0 && M % gemm8::BM == 0 && N % gemm8::BN == 0 && K % gemm8::BK == 0 && K / gemm8::BK >= 2) {

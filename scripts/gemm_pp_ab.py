@@ -14,13 +14,16 @@ for (m, n, k) in ((256, 256, 64), (512, 768, 128), (1024, 512, 320), (2048, 2048
     a = (torch.rand(m, k, device=dev) * 2 - 1).to(torch.bfloat16)
     b = (torch.rand(n, k, device=dev) * 2 - 1).to(torch.bfloat16)
     ref = a.float() @ b.float().t()
-    for path in (3, 0):
+    for path in (4, 3, 0):
         h.set_gemm_path(path)
         c = h.gemm_bf16_nt(a, b)
         torch.cuda.synchronize()
         err = ((c - ref).abs().max() / ref.abs().max()).item()
-        print(f"check {m}x{n}x{k} path={path}: max_rel_err={err:.2e}", flush=True)
-        assert err < 1e-2, (m, n, k, path, err)
+        cb = h.gemm_bf16_nt(a, b, out_fp32=False).float()
+        torch.cuda.synchronize()
+        errb = ((cb - ref).abs().max() / ref.abs().max()).item()
+        print(f"check {m}x{n}x{k} path={path}: max_rel_err={err:.2e} (bf16 out {errb:.2e})", flush=True)
+        assert err < 1e-2 and errb < 2e-2, (m, n, k, path, err, errb)
 
 
 def bench(fn, iters):
@@ -41,12 +44,13 @@ for size, iters in ((4096, 50), (8192, 20), (16384, 5)):
     flops = 2.0 * size * size * kdim
     out = {}
     for rep in range(2):
-        for path in (3, 0):
+        for path in (4, 3, 0):
             h.set_gemm_path(path)
             dt = bench(lambda: h.gemm_bf16_nt(a, b), iters)
             out.setdefault(path, []).append(flops / dt / 1e12)
         dt = bench(lambda: a @ b.t(), iters)
         out.setdefault("torch", []).append(flops / dt / 1e12)
-    print(f"{size}x{size}x{kdim}: ping-pong {max(out[3]):.0f} TF/s  8-phase {max(out[0]):.0f} TF/s  "
-          f"torch {max(out['torch']):.0f} TF/s  pp/torch {max(out[3]) / max(out['torch']):.2f}", flush=True)
+    print(f"{size}x{size}x{kdim}: pp-tuned {max(out[4]):.0f}  ping-pong {max(out[3]):.0f}  8-phase {max(out[0]):.0f}  "
+          f"torch {max(out['torch']):.0f} TF/s  best/torch {max(max(out[4]), max(out[3])) / max(out['torch']):.2f}",
+          flush=True)
 h.set_gemm_path(0)
