@@ -507,7 +507,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int EPI_STRIDE = 68;                    // fp32 row pitch of the LDS epilogue (bank spread)
 constexpr int EPI_BYTES = 8 * 64 * EPI_STRIDE * 4;  // 8 waves x 64 x 68 fp32 = 136 KiB
 
-template <typename OutT, bool TUNED>
+// VARIANT bit 0: static priority for the second half instead of per-segment setprio flips;
+// bit 1: LDS-staged 16-B epilogue
+template <typename OutT, int VARIANT>
 __global__ void __launch_bounds__(THREADS, 1)
 gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
                        int M, int N, int K, int ldc, float alpha) {
@@ -580,7 +582,7 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
         bfr[nq][ks][j] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
   };
   auto mma = [&](int mq, int nq) {
-    if (!TUNED) __builtin_amdgcn_s_setprio(1);
+    if (!(VARIANT & 1)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -588,13 +590,13 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mq][ks][i], bfr[nq][ks][j], acc[mq][nq][i][j], 0, 0, 0);
-    if (!TUNED) __builtin_amdgcn_s_setprio(0);
+    if (!(VARIANT & 1)) __builtin_amdgcn_s_setprio(0);
   };
 
   const int nt = K / BK;
   // TUNED: static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per
   // SIMD" item 4) instead of per-segment flips
-  if (TUNED && wr == 1) __builtin_amdgcn_s_setprio(1);
+  if ((VARIANT & 1) && wr == 1) __builtin_amdgcn_s_setprio(1);
   stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
   KAMD_PP_VM0();
   KAMD_PP_BARRIER();                  // K-tile 0 published to every wave
@@ -631,7 +633,7 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
     KAMD_PP_BARRIER();
   }
   if (wr == 0) KAMD_PP_BARRIER();     // balance group 1's extra barrier
-  if (TUNED) {
+  if (VARIANT & 2) {
     // epilogue through LDS (free now: every wave is past its last read and glds): each wave
     // transposes a 64x64 fp32 quadrant row to row-major, then writes 16-B vectors (256 B per
     // 16 lanes of a row) instead of 4-B scattered stores
@@ -788,37 +790,38 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
     snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
     return -1;
   }
-  if ((g_gemm_path == 3 || g_gemm_path == 4) && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
-    static bool attrpp = false;
-    if (!attrpp) {
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float, false>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16, false>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float, true>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::EPI_BYTES));
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16, true>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::EPI_BYTES));
-      attrpp = true;
-    }
+  if (g_gemm_path >= 3 && g_gemm_path <= 6 && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
+    // path 3: variant 0, 4: LDS epilogue, 5: static priority, 6: both
+    const int variant = g_gemm_path == 3 ? 0 : g_gemm_path == 4 ? 2 : g_gemm_path == 5 ? 1 : 3;
+    const size_t lds = (variant & 2) ? gemmpp::EPI_BYTES : gemmpp::LDS_BYTES;
     const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
-    const bool tuned = g_gemm_path == 4;
-    const size_t lds = tuned ? gemmpp::EPI_BYTES : gemmpp::LDS_BYTES;
+#define KAMD_PP_LAUNCH(T, V)                                                                                   \
+  do {                                                                                                         \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<T, V>,                                \
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                           \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<T, V>), dim3(tiles), dim3(gemmpp::THREADS), lds, stream, \
+                       (const u16*)A, (const u16*)B, (T*)C, M, N, K, ldc, alpha);                              \
+  } while (0)
     if (out_fp32) {
-      if (tuned)
-        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, true>), dim3(tiles), dim3(gemmpp::THREADS), lds,
-                           stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
-      else
-        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, false>), dim3(tiles), dim3(gemmpp::THREADS), lds,
-                           stream, (const u16*)A, (const u16*)B, (float*)C, M, N, K, ldc, alpha);
+      switch (variant) {
+        case 0: KAMD_PP_LAUNCH(float, 0); break;
+        case 1: KAMD_PP_LAUNCH(float, 1); break;
+        case 2: KAMD_PP_LAUNCH(float, 2); break;
+        default: KAMD_PP_LAUNCH(float, 3); break;
+      }
     } else {
-      if (tuned)
-        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, true>), dim3(tiles), dim3(gemmpp::THREADS), lds,
-                           stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
-      else
-        hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, false>), dim3(tiles), dim3(gemmpp::THREADS), lds,
-                           stream, (const u16*)A, (const u16*)B, (__bf16*)C, M, N, K, ldc, alpha);
+      switch (variant) {
+        case 0: KAMD_PP_LAUNCH(__bf16, 0); break;
+        case 1: KAMD_PP_LAUNCH(__bf16, 1); break;
+        case 2: KAMD_PP_LAUNCH(__bf16, 2); break;
+        default: KAMD_PP_LAUNCH(__bf16, 3); break;
+      }
     }
+#undef KAMD_PP_LAUNCH
     return check(hipGetLastError(), "gemm ping-pong launch");
   }
   if (g_gemm_path == 0 && M % gemm8::BM == 0 && N % gemm8::BN == 0 && K % gemm8::BK == 0 && K / gemm8::BK >= 2) {
