@@ -545,8 +545,8 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
   }
   const u16* half_src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 64) * K, B + (size_t)n0 * K,
                             B + (size_t)(n0 + 32) * K};
-  auto stage = [&](int kt, int h) {
-    unsigned char* dst = lds + ((kt & 1) * 4 + h) * HALF_BYTES + wid * 1024;
+  auto stage = [&](int kt, const int par, int h) {
+    unsigned char* dst = lds + (par * 4 + h) * HALF_BYTES + wid * 1024;
     const u16* src = half_src[h] + (size_t)kt * BK;
     const size_t* off = h < 2 ? offA : offB;
     __builtin_amdgcn_global_load_lds((const void*)(src + off[0]), (lds_void*)dst, 16, 0, 0);
@@ -565,16 +565,16 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[2][2][4], bfr[2][2][2];
-  auto read_a = [&](int kt, int mq) {   // half h = mq, local rows wr*64 + ...
-    const unsigned char* base = lds + ((kt & 1) * 4 + mq) * HALF_BYTES + (wr * 64 + frow) * 128;
+  auto read_a = [&](const int par, int mq) {   // half h = mq, local rows wr*64 + ...
+    const unsigned char* base = lds + (par * 4 + mq) * HALF_BYTES + (wr * 64 + frow) * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         af[mq][ks][i] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
   };
-  auto read_b = [&](int kt, int nq) {   // half h = 2 + nq, local rows wc*32 + ...
-    const unsigned char* base = lds + ((kt & 1) * 4 + 2 + nq) * HALF_BYTES + (wc * 32 + frow) * 128;
+  auto read_b = [&](const int par, int nq) {   // half h = 2 + nq, local rows wc*32 + ...
+    const unsigned char* base = lds + (par * 4 + 2 + nq) * HALF_BYTES + (wc * 32 + frow) * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -597,41 +597,48 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
   // TUNED: static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per
   // SIMD" item 4) instead of per-segment flips
   if ((VARIANT & 1) && wr == 1) __builtin_amdgcn_s_setprio(1);
-  stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+  stage(0, 0, 0); stage(0, 0, 2); stage(0, 0, 3); stage(0, 0, 1);
   KAMD_PP_VM0();
   KAMD_PP_BARRIER();                  // K-tile 0 published to every wave
   if (wr == 1) KAMD_PP_BARRIER();     // group 1 runs one barrier behind group 0
-  for (int kt = 0; kt < nt; ++kt) {
-    const bool more = kt + 1 < nt;
+  // one K-tile; `par` = kt & 1 is a literal at each call site (the loop is unrolled by 2), so LDS
+  // addresses fold to constants
+  auto ktile = [&](int kt, const int par, const bool more) {
     // phase 0: read B nq=0, A mq=0 (h2, h0); stage h0(kt+1); then h3(kt) must land for phase 1
-    read_b(kt, 0);
+    read_b(par, 0);
     __builtin_amdgcn_sched_barrier(0);
-    read_a(kt, 0);
-    if (more) { stage(kt + 1, 0); KAMD_WAIT_VMN(4); } else { KAMD_WAIT_VMN(2); }
+    read_a(par, 0);
+    if (more) { stage(kt + 1, par ^ 1, 0); KAMD_WAIT_VMN(4); } else { KAMD_WAIT_VMN(2); }
     KAMD_PP_BARRIER();
     KAMD_PP_LGKM0();
     mma(0, 0);
     KAMD_PP_BARRIER();
     // phase 1: read B nq=1 (h3); stage h2(kt+1); then h1(kt) must land for phase 2
-    read_b(kt, 1);
-    if (more) { stage(kt + 1, 2); KAMD_WAIT_VMN(4); } else { KAMD_PP_VM0(); }
+    read_b(par, 1);
+    if (more) { stage(kt + 1, par ^ 1, 2); KAMD_WAIT_VMN(4); } else { KAMD_PP_VM0(); }
     KAMD_PP_BARRIER();
     KAMD_PP_LGKM0();
     mma(0, 1);
     KAMD_PP_BARRIER();
     // phase 2: read A mq=1 (h1); stage h3(kt+1)
-    read_a(kt, 1);
-    if (more) stage(kt + 1, 3);
+    read_a(par, 1);
+    if (more) stage(kt + 1, par ^ 1, 3);
     KAMD_PP_BARRIER();
     KAMD_PP_LGKM0();
     mma(1, 0);
     KAMD_PP_BARRIER();
     // phase 3: no reads; stage h1(kt+1); then h0, h2 of kt+1 must land for its phase 0
-    if (more) { stage(kt + 1, 1); KAMD_WAIT_VMN(4); }
+    if (more) { stage(kt + 1, par ^ 1, 1); KAMD_WAIT_VMN(4); }
     KAMD_PP_BARRIER();
     mma(1, 1);
     KAMD_PP_BARRIER();
+  };
+  int kt = 0;
+  for (; kt + 1 < nt; kt += 2) {
+    ktile(kt, 0, true);
+    ktile(kt + 1, 1, kt + 2 < nt);
   }
+  if (kt < nt) ktile(kt, 0, false);
   if (wr == 0) KAMD_PP_BARRIER();     // balance group 1's extra barrier
   if (VARIANT & 2) {
     // epilogue through LDS (free now: every wave is past its last read and glds): each wave
