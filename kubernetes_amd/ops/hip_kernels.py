@@ -98,10 +98,10 @@ def gemm_bf16_nt(a, b, out_fp32=True, alpha=1.0):
 
 
 def set_gemm_path(path: int):
-    """0 = auto (8-phase 256x256 global_load_lds kernel when M, N % 256 == 0, K % 64 == 0 and
-    K >= 128; the 2-barrier 256x256 kernel for K == 64), 1 = always the 128x128 register-staged
-    kernel, 2 = the 2-barrier 256x256 kernel, 3 = the ping-pong 256x256 kernel (wave groups
-    staggered by one barrier), 4 = ping-pong with static priority + LDS-staged epilogue."""
+    """0 = auto (the ping-pong 256x256 global_load_lds kernel — wave groups staggered by one
+    barrier — when M, N % 256 == 0 and K % 64 == 0, else the 128x128 kernel), 1 = always the
+    128x128 register-staged kernel, 2 = the 2-barrier 256x256 kernel, 3 = ping-pong, 4-6 =
+    ping-pong variants (LDS epilogue / static priority / both), 7 = the 8-phase 256x256 kernel."""
     load().kamd_gemm_set_path(int(path))
 
 

@@ -4,7 +4,8 @@
 //                        cuda-vector-add test image (test/images/cuda-vector-add/Dockerfile,
 //                        used by test/e2e/scheduling/nvidia-gpus.go:51-113): 1-D grid of
 //                        ceil(N/256) blocks x 256 threads, N = 50000 floats by default.
-//  * gemm_bf16_nt      — MFMA (v_mfma_f32_16x16x32_bf16) LDS-tiled GEMM, C = A · Bᵀ, used by the
+//  * gemm_bf16_nt      — MFMA (v_mfma_f32_16x16x32_bf16) LDS-tiled GEMM, C = A · Bᵀ (default: the
+//                        ping-pong 256x256 kernel, 0.87-0.89x hipBLASLt on MI355X), used by the
 //                        device-plugin burn-in diagnostic (matrix-core health + throughput, the
 //                        role DCGM diag plays in the NVIDIA stack) and by the workload payload.
 //  * hbm_copy          — 16 B/lane streaming copy: HBM3E bandwidth health probe.
@@ -23,8 +24,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 static thread_local char g_err[256];
-static int g_gemm_path = 0;   // 0 auto (8-phase 256-tile path when the shape allows), 1 force the 128-tile kernel,
-                              // 2 force the 2-barrier 256-tile glds kernel, 3 the ping-pong 256-tile kernel
+static int g_gemm_path = 0;   // 0 auto (ping-pong 256-tile kernel when the shape allows), 1 force the 128-tile
+                              // kernel, 2 the 2-barrier 256-tile glds kernel, 3-6 ping-pong variants, 7 the 8-phase
+                              // 256-tile kernel
 
 static int check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
@@ -797,9 +799,9 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
     snprintf(g_err, sizeof g_err, "gemm_bf16_nt: A/B must be 16-byte aligned");
     return -1;
   }
-  if (g_gemm_path >= 3 && g_gemm_path <= 6 && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
+  if ((g_gemm_path == 0 || (g_gemm_path >= 3 && g_gemm_path <= 6)) && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
     // path 3: variant 0, 4: LDS epilogue, 5: static priority, 6: both
-    const int variant = g_gemm_path == 3 ? 0 : g_gemm_path == 4 ? 2 : g_gemm_path == 5 ? 1 : 3;
+    const int variant = g_gemm_path <= 3 ? 0 : g_gemm_path == 4 ? 2 : g_gemm_path == 5 ? 1 : 3;
     const size_t lds = (variant & 2) ? gemmpp::EPI_BYTES : gemmpp::LDS_BYTES;
     const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
 #define KAMD_PP_LAUNCH(T, V)                                                                                   \
@@ -831,7 +833,7 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
 #undef KAMD_PP_LAUNCH
     return check(hipGetLastError(), "gemm ping-pong launch");
   }
-  if (g_gemm_path == 0 && M % gemm8::BM == 0 && N % gemm8::BN == 0 && K % gemm8::BK == 0 && K / gemm8::BK >= 2) {
+  if (g_gemm_path == 7 && M % gemm8::BM == 0 && N % gemm8::BN == 0 && K % gemm8::BK == 0 && K / gemm8::BK >= 2) {
     static bool attr8 = false;
     if (!attr8) {
       HC(hipFuncSetAttribute((const void*)gemm8::gemm_bf16_nt_8ph_kernel<float>,

@@ -80,19 +80,22 @@ def test_real_amdsmi_enumerates_mi355x():
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 256, 128), (512, 512, 192), (512, 768, 1024),
-                                   (2048, 1024, 4096)])
+                                   (2048, 1024, 4096), (768, 512, 320)])
 def test_gemm_both_paths_match_reference(hk, M, N, K):
-    """Every GEMM path against an fp32 torch reference: 0 = 8-phase 256-tile (K-tile counts 2, 3
-    exercise its prologue / tail waits), 1 = 128-tile register-staged, 2 = 2-barrier 256-tile glds."""
+    """Every GEMM path against an fp32 torch reference: 0/3 = ping-pong 256-tile (K-tile counts 1,
+    2, 3 exercise its unrolled pairs, odd tail and counted-vmcnt waits), 4-6 its variants, 1 =
+    128-tile register-staged, 2 = 2-barrier 256-tile glds, 7 = 8-phase 256-tile."""
     torch.manual_seed(1)
     a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     b = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     ref = a.float() @ b.float().T
     try:
-        for path in (0, 1, 2):
+        for path in (0, 1, 2, 4, 5, 6, 7):
             hk.set_gemm_path(path)
             out = hk.gemm_bf16_nt(a, b, out_fp32=True)
             torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * (K ** 0.5))
+            outb = hk.gemm_bf16_nt(a, b, out_fp32=False).float()
+            torch.testing.assert_close(outb, ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
     finally:
         hk.set_gemm_path(0)
 
