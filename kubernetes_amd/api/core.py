@@ -30,6 +30,9 @@ ATTR_RENDER_MINOR = "amd.com/render-minor"
 ATTR_CARD_MINOR = "amd.com/card-minor"
 ATTR_INDEX = "amd.com/index"
 ATTR_PARTITION = "amd.com/partition"      # SPX / DPX / QPX / CPX
+ATTR_SOCKET = "amd.com/socket"            # physical package: partitions of one MI355X share it
+ATTR_PARTITION_ID = "amd.com/partition-id"
+ATTR_MEMORY_PARTITION = "amd.com/memory-partition"   # NPS1 / NPS2
 ATTR_ECC = "amd.com/ecc"                  # uncorrectable ECC count
 ATTR_CUS = "amd.com/compute-units"
 ATTR_UUID = "amd.com/uuid"

@@ -30,12 +30,14 @@ class NodeHandle:
 class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
-                 health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None):
+                 health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None,
+                 partition="SPX"):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
         self.real = real_gpus
         self.hives = hives
+        self.partition = partition             # fake backend: SPX/DPX/QPX/CPX compute partitions
         self.own_dir = workdir is None
         self.dir = workdir or tempfile.mkdtemp(prefix="kamd-cluster-")
         self.emit_events = emit_events
@@ -63,7 +65,7 @@ class LocalCluster:
         self.url = f"http://127.0.0.1:{port}"
         self.client = Client(self.url)
         if self.gpus:
-            fixture = None if self.real else amdsmi.fixture_file(self.gpus, hives=self.hives)
+            fixture = None if self.real else amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition)
             self.smi = amdsmi.SMI(fixture=fixture)
         self.scheduler = Scheduler(Client(self.url), emit_events=self.emit_events, **self.scheduler_kwargs)
         self._sched_task = asyncio.ensure_future(self.scheduler.run())

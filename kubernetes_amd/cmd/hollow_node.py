@@ -15,6 +15,8 @@ def main(argv=None):
     ap.add_argument("--name-prefix", default="hollow")
     ap.add_argument("--gpus-per-node", type=int, default=8)
     ap.add_argument("--hives", type=int, default=1)
+    ap.add_argument("--partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"],
+                    help="compute-partition mode of the fake MI355X packages (CPX: 8 logical devices each)")
     ap.add_argument("--morph", default="kubelet", choices=["kubelet", "proxy"],
                     help="kubelet: hollow kubelets; proxy: hollow kube-proxies over a fake iptables (hollow-node.go:139+)")
     ap.add_argument("--payload-socket", default=None,
@@ -50,7 +52,8 @@ def main(argv=None):
             from ..kubemark.payload import PayloadClient
             payload = PayloadClient(a.payload_socket)
         h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives, payload=payload,
-                          emit_events=not a.no_events, status_freq=a.node_status_update_frequency)
+                          emit_events=not a.no_events, status_freq=a.node_status_update_frequency,
+                          partition=a.partition)
         await h.start()
         await h.wait_registered()
         if a.ready_file:

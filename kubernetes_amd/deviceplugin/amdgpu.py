@@ -8,6 +8,7 @@ Replaces the out-of-tree NVIDIA plugin the reference targets (NVML enumeration,
       amd.com/arch=gfx950  amd.com/product=MI355X  amd.com/memory=<MiB>  amd.com/hbm=288Gi
       amd.com/xgmi-hive=<hex>  amd.com/numa=<n>  amd.com/bdf  amd.com/render-minor
       amd.com/index  amd.com/partition=SPX|CPX…  amd.com/ecc=<uncorrectable>  amd.com/compute-units
+      amd.com/socket (physical package)  amd.com/partition-id  amd.com/memory-partition=NPS1|NPS2
   * InitContainer injects the shared `/dev/kfd` plus one `/dev/dri/renderD<minor>` per GPU
     (no vendor runtime, no NVML/CUDA shim) and, optionally, the ROCm userspace read-only;
     `AMD_VISIBLE_DEVICES` lists the host HIP ordinals (informational, like
@@ -46,7 +47,14 @@ def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None) -> dict:
         core.ATTR_INDEX: str(g.hip_id if g.hip_id >= 0 else g.index),
         core.ATTR_PARTITION: g.compute_partition or "SPX",
         core.ATTR_CUS: str(g.compute_units),
+        # compute partitions (DPX/QPX/CPX) of one package share its socket: the scheduler packs
+        # multi-partition requests onto as few packages as possible
+        core.ATTR_SOCKET: str(g.socket if g.socket >= 0 else g.index),
     }
+    if g.partition_id >= 0:
+        attrs[core.ATTR_PARTITION_ID] = str(g.partition_id)
+    if g.memory_partition:
+        attrs[core.ATTR_MEMORY_PARTITION] = g.memory_partition
     if m is not None:
         attrs[core.ATTR_ECC] = str(m.ecc_uncorrectable)
         attrs[core.ATTR_XGMI_LINKS] = str(m.xgmi_links_up)

@@ -26,12 +26,13 @@ class HollowCluster:
     """A set of hollow nodes sharing one process / event loop / API client pool."""
 
     def __init__(self, master, count, prefix="hollow", gpus=8, hives=1, payload=None, workdir=None,
-                 emit_events=False, status_freq=10.0, max_conns=32):
+                 emit_events=False, status_freq=10.0, max_conns=32, partition="SPX"):
         self.master = master
         self.count = count
         self.prefix = prefix
         self.gpus = gpus
         self.hives = hives
+        self.partition = partition
         self.payload = payload
         self.own_dir = workdir is None
         self.dir = workdir or tempfile.mkdtemp(prefix=f"kamd-{prefix}-")
@@ -44,7 +45,7 @@ class HollowCluster:
 
     async def start(self):
         if self.gpus:
-            self.smi = amdsmi.SMI(fixture=amdsmi.fixture_file(self.gpus, hives=self.hives))
+            self.smi = amdsmi.SMI(fixture=amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition))
         for i in range(self.count):
             name = f"{self.prefix}-{i}"
             pdir = os.path.join(self.dir, name, "plugins")

@@ -33,6 +33,7 @@ class _Info(ctypes.Structure):
         ("hip_id", ctypes.c_int32), ("xgmi_hive_id", ctypes.c_uint64), ("xgmi_node_id", ctypes.c_uint64),
         ("numa_node", ctypes.c_int32), ("kfd_id", ctypes.c_uint64), ("partition_id", ctypes.c_int32),
         ("compute_partition", ctypes.c_char * 32), ("serial", ctypes.c_char * STR),
+        ("socket", ctypes.c_int32), ("memory_partition", ctypes.c_char * 16),
     ]
 
 
@@ -77,6 +78,8 @@ class GPU:
     partition_id: int
     compute_partition: str
     serial: str
+    socket: int = -1               # physical package: compute partitions of one MI355X share it
+    memory_partition: str = ""     # NPS1 / NPS2
 
     @property
     def product(self) -> str:
@@ -91,9 +94,12 @@ class GPU:
 
     @property
     def device_id_str(self) -> str:
-        """Stable plugin device ID (Device.ID, ≤63 chars): prefer the ASIC UUID."""
+        """Stable plugin device ID (Device.ID, ≤63 chars): prefer the ASIC UUID. Compute
+        partitions of one package may share its UUID, so a partition's ID carries `-p<id>`."""
+        suffix = f"-p{self.partition_id}" if self.compute_partition not in ("", "SPX") and self.partition_id >= 0 else ""
         if self.uuid:
-            return ("GPU-" + self.uuid)[:63] if not self.uuid.startswith("GPU-") else self.uuid[:63]
+            base = self.uuid if self.uuid.startswith("GPU-") else "GPU-" + self.uuid
+            return base[:63 - len(suffix)] + suffix
         return f"GPU-{self.bdf or self.index}"
 
 
@@ -133,6 +139,10 @@ class Proc:
 
 _lib = None
 _lock = threading.Lock()
+
+
+# logical devices per MI355X package in each compute-partition mode (8 XCDs per package)
+PARTITIONS_PER_SOCKET = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
 
 
 class SMIError(RuntimeError):
@@ -220,21 +230,31 @@ class SMI:
         return [[self.link(i, j) for j in range(n)] for i in range(n)]
 
 
-def mi355x_fixture(n=8, hive_id=0x3C4D5E6F7081, hives=1, partition="SPX", numa_per=4, seed="node0") -> dict:
+def mi355x_fixture(n=8, hive_id=0x3C4D5E6F7081, hives=1, partition="SPX", numa_per=4, seed="node0",
+                   memory_partition="NPS1") -> dict:
     """Fixture for an n-GPU MI355X UBB node (8 OAMs, all-to-all xGMI: 7 links per GPU).
-    `hives` > 1 splits the GPUs into several hives (to exercise hive-aware allocation)."""
+    `hives` > 1 splits the GPUs into several hives (to exercise hive-aware allocation).
+
+    `partition` is the compute-partition mode: SPX exposes each package as one device, DPX /
+    QPX / CPX split its 8 XCDs into 2 / 4 / 8 logical devices, each with its own render node,
+    1/k of the CUs and 1/k of the HBM (as AMD SMI reports a partition). Partitions of one
+    package share `socket` and its xGMI links."""
+    per = PARTITIONS_PER_SOCKET.get(partition, 1)
     devs = []
     per_hive = max(1, n // hives)
     for i in range(n):
         h = hive_id + (i // per_hive)
-        devs.append({
-            "uuid": f"{seed}-{i:02d}ff-75a3-00{i}0-9c1e-{0x5f3c0000 + i:08x}",
-            "bdf": f"0000:{0x05 + 0x10 * i:02x}:00.0", "market_name": "AMD Instinct MI355X", "arch": "gfx950",
-            "device_id": 0x75A3, "vram_total_mb": 294912, "compute_units": 256, "render_minor": 128 + i,
-            "card_minor": i, "xgmi_hive_id": h, "xgmi_node_id": i, "numa_node": i // numa_per,
-            "partition": partition, "serial": f"{seed}-SN{i:04d}", "xgmi_links_total": 7,
-            "xgmi_links_up": 7 if per_hive == 8 else per_hive - 1,
-        })
+        for p in range(per):
+            k = i * per + p
+            uid = f"{seed}-{i:02d}ff-75a3-00{i}0-9c1e-{0x5f3c0000 + i:08x}"
+            devs.append({
+                "uuid": uid, "bdf": f"0000:{0x05 + 0x10 * i:02x}:00.{p}", "market_name": "AMD Instinct MI355X",
+                "arch": "gfx950", "device_id": 0x75A3, "vram_total_mb": 294912 // per, "compute_units": 256 // per,
+                "render_minor": 128 + k, "card_minor": k, "hsa_id": k, "hip_id": k, "xgmi_hive_id": h,
+                "xgmi_node_id": i, "numa_node": i // numa_per, "partition": partition, "partition_id": p,
+                "socket": i, "memory_partition": memory_partition, "serial": f"{seed}-SN{i:04d}",
+                "xgmi_links_total": 7, "xgmi_links_up": 7 if per_hive == 8 else per_hive - 1,
+            })
     return {"devices": devs}
 
 

@@ -14,6 +14,12 @@ MI355X-first design:
     inside it, a NUMA node that holds the whole set is preferred; every chosen device must
     report at least N-1 healthy xGMI links;
   * single-GPU pods pack into the most-used hive / NUMA node first (anti-fragmentation);
+  * compute partitions (SPX/DPX/QPX/CPX: 1/2/4/8 logical devices per package, sharing its
+    `amd.com/socket`) — partitions of one package talk over the on-package fabric, so a
+    k-partition request takes the fewest packages (whole free packages first, the tail
+    best-fit into the package with the fewest free partitions that holds it); a 1-partition
+    pod fills partly used packages before opening a fresh one. The xGMI link requirement
+    counts packages, not partitions (a CPX request for 8 spans one package: no links needed);
   * `amd.com/xgmi-policy` pod annotation: `required` (fail rather than span hives) or
     `preferred` (default: span hives only when no single hive fits, with a low score);
   * deterministic order (device index) instead of map order.
@@ -24,6 +30,9 @@ from __future__ import annotations
 
 from ..api import core
 from ..api.labels import SelectorError, node_selector_requirements_as_selector
+
+# logical devices per MI355X package per compute-partition mode (8 XCDs per package)
+PARTITIONS_PER_SOCKET = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
 
 POLICY_ANNOTATION = "amd.com/xgmi-policy"
 REQUIRED, PREFERRED = "required", "preferred"
@@ -57,6 +66,22 @@ def _links(dev):
         return 0
 
 
+def _pps(dev):
+    return PARTITIONS_PER_SOCKET.get((dev.get("attributes") or {}).get(core.ATTR_PARTITION, "SPX"), 1)
+
+
+def _need_links(dev, n):
+    """xGMI links each device of an n-device set must have: one per OTHER package spanned."""
+    if n <= 1:
+        return 0
+    p = _pps(dev)
+    return n - 1 if p == 1 else -(-n // p) - 1
+
+
+def _sock(did, dev):
+    return (dev.get("attributes") or {}).get(core.ATTR_SOCKET, did)
+
+
 def _score(free, n, numa_fit):
     # 10 for a perfect fit, decreasing with leftover fragments in the chosen hive
     return 9.0 - min(free - n, 8) / 8.0 * 4.0 + (1.0 if numa_fit else 0.0)
@@ -75,6 +100,16 @@ def feasible(requests, er, policy=PREFERRED):
     hives = er.hive_free.get(r.rname)
     if not hives or er.nfree.get(r.rname, 0) < n:
         return False, 0, f"Insufficient {r.rname}"
+    first = next((d for devs in hives.values() for d in devs.values()), None)
+    if first is not None and _pps(first) > 1:
+        # compute-partitioned node: the package-level plan decides feasibility and score
+        cands = [(i, d) for devs in hives.values() for i, d in devs.items() if _links(d) >= _need_links(d, n)]
+        if len(cands) < n:
+            return False, 0, f"Insufficient {r.rname}"
+        ids, sc = _pick(cands, n, policy)
+        if ids is None:
+            return False, 0, f"no single xGMI hive has {n} free {r.rname}"
+        return True, sc, ""
     need_links = n - 1 if n > 1 else 0
     best = None
     total = 0
@@ -113,7 +148,6 @@ def allocate(requests, er, policy=PREFERRED):
         avail = er.available.get(r.rname)
         if not avail:
             return None, 0, f"Insufficient {r.rname}"
-        need_links = r.count - 1 if r.count > 1 else 0
         sel = r.selector
         cands = []
         hf = er.hive_free.get(r.rname)
@@ -124,7 +158,7 @@ def allocate(requests, er, policy=PREFERRED):
             attrs = dev.get("attributes") or {}
             if sel is not None and not sel.matches(attrs):
                 continue
-            if need_links and _links(dev) < need_links:
+            if r.count > 1 and _links(dev) < _need_links(dev, r.count):
                 continue
             cands.append((did, dev))
         if len(cands) < r.count:
@@ -152,6 +186,8 @@ def _pick(cands, n, policy):
         # best fit: the hive with the fewest free devices that still holds n
         fitting.sort(key=lambda t: (t[0], t[1]))
         free, _, devs = fitting[0]
+        if any(_pps(d) > 1 for _, d in devs):
+            return _pick_partitions(devs, n)
         numas = _group(devs, core.ATTR_NUMA)
         nf = [(len(v), k, v) for k, v in numas.items() if len(v) >= n]
         if nf:
@@ -173,3 +209,34 @@ def _pick(cands, n, policy):
     for _, _, v in sorted(((len(v), h, v) for h, v in hives.items()), key=lambda t: (-t[0], t[1])):
         chosen.extend(sorted(v, key=lambda x: _idx(x[1])))
     return [d for d, _ in chosen[:n]], 1.0
+
+
+def _pick_partitions(devs, n):
+    """Place n compute partitions inside one hive on the fewest packages. Whole free packages
+    are taken largest-first; the tail goes to the package with the fewest free partitions that
+    still holds it (best fit), so partly used packages fill up before fresh ones are opened.
+    Score: 10 for a set that spans the minimum number of packages and leaves no stranded free
+    partitions on them, lower for each partition left behind on a touched package."""
+    socks = {}
+    for did, dev in devs:
+        socks.setdefault(_sock(did, dev), []).append((did, dev))
+    for v in socks.values():
+        v.sort(key=lambda x: _idx(x[1]))
+    order = sorted(socks, key=lambda k: (-len(socks[k]), str(k)))
+    chosen, rem, used, left = [], n, 0, 0
+    while rem > 0 and order:
+        fit = [k for k in order if len(socks[k]) >= rem]
+        if fit:
+            k = min(fit, key=lambda k: (len(socks[k]), str(k)))
+        else:
+            k = order[0]
+        order.remove(k)
+        take = socks[k][:rem]
+        chosen.extend(take)
+        left += len(socks[k]) - len(take)
+        rem -= len(take)
+        used += 1
+    p = max(_pps(d) for _, d in devs)
+    minimal = -(-n // p)
+    score = 9.0 - min(left, p) / p * 4.0 + (1.0 if used <= minimal else 0.0)
+    return [d for d, _ in chosen], score

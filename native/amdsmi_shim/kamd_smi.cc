@@ -188,6 +188,8 @@ struct FakeBackend : Backend {
       in.numa_node = (int32_t)d.num("numa_node", idx / 4);
       in.kfd_id = (uint64_t)d.num("kfd_id", 1000 + idx);
       in.partition_id = (int32_t)d.num("partition_id", 0);
+      in.socket = (int32_t)d.num("socket", idx);
+      copy_str(in.memory_partition, sizeof in.memory_partition, d.str("memory_partition", "NPS1"));
       kamd_metrics_t& m = fd.m;
       m.gfx_activity = (uint32_t)d.num("gfx_activity", 0);
       m.umc_activity = (uint32_t)d.num("umc_activity", 0);
@@ -208,11 +210,13 @@ struct FakeBackend : Backend {
     int n = (int)devs.size();
     links.assign(n, std::vector<kamd_link_t>(n));
     // default topology: same hive id => xGMI, 1 hop (MI355X UBB: every GPU has a direct link
-    // to each of the other 7); different hive => PCIe, 2 hops.
+    // to each of the other 7); different hive => PCIe, 2 hops. Compute partitions of one
+    // package (CPX/DPX/QPX) reach each other over the on-package fabric: 0 hops, weight 5.
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) {
         kamd_link_t& l = links[i][j];
         if (i == j) { l.type = 0; l.hops = 0; l.weight = 0; l.p2p = 1; continue; }
+        if (devs[i].info.socket == devs[j].info.socket) { l.type = 2; l.hops = 0; l.weight = 5; l.p2p = 1; continue; }
         bool same = devs[i].info.xgmi_hive_id != 0 && devs[i].info.xgmi_hive_id == devs[j].info.xgmi_hive_id;
         l.type = same ? 2 : 1;
         l.hops = same ? 1 : 2;
@@ -278,6 +282,7 @@ struct FakeBackend : Backend {
   X(amdsmi_get_gpu_xgmi_link_status,                                                             \
     amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_xgmi_link_status_t*))                     \
   X(amdsmi_get_gpu_compute_partition, amdsmi_status_t (*)(amdsmi_processor_handle, char*, uint32_t)) \
+  X(amdsmi_get_gpu_memory_partition, amdsmi_status_t (*)(amdsmi_processor_handle, char*, uint32_t)) \
   X(amdsmi_get_gpu_process_list,                                                                 \
     amdsmi_status_t (*)(amdsmi_processor_handle, uint32_t*, amdsmi_proc_info_t*))                \
   X(amdsmi_get_clock_info, amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_clk_type_t, amdsmi_clk_info_t*)) \
@@ -293,6 +298,7 @@ struct SmiBackend : Backend {
   void* lib = nullptr;
   SmiFns f;
   std::vector<amdsmi_processor_handle> gpus;
+  std::vector<int32_t> socket_of;   // per entry of gpus: index of its amdsmi socket handle
 
   std::string code(amdsmi_status_t s) {
     const char* msg = nullptr;
@@ -331,20 +337,22 @@ struct SmiBackend : Backend {
             t != AMDSMI_PROCESSOR_TYPE_AMD_GPU)
           continue;
         gpus.push_back(h);
+        socket_of.push_back((int32_t)i);
       }
     }
     // order by HIP enumeration id when available, so index == HIP device ordinal
     if (f.amdsmi_get_gpu_enumeration_info) {
-      std::vector<std::pair<uint32_t, amdsmi_processor_handle>> ord;
+      struct Ent { uint32_t k; amdsmi_processor_handle h; int32_t sock; };
+      std::vector<Ent> ord;
       for (size_t i = 0; i < gpus.size(); ++i) {
         amdsmi_enumeration_info_t e;
         memset(&e, 0, sizeof e);
         uint32_t k = (uint32_t)i;
         if (f.amdsmi_get_gpu_enumeration_info(gpus[i], &e) == AMDSMI_STATUS_SUCCESS) k = e.hip_id;
-        ord.push_back({k, gpus[i]});
+        ord.push_back({k, gpus[i], socket_of[i]});
       }
-      std::stable_sort(ord.begin(), ord.end(), [](auto& a, auto& b) { return a.first < b.first; });
-      for (size_t i = 0; i < ord.size(); ++i) gpus[i] = ord[i].second;
+      std::stable_sort(ord.begin(), ord.end(), [](const Ent& a, const Ent& b) { return a.k < b.k; });
+      for (size_t i = 0; i < ord.size(); ++i) { gpus[i] = ord[i].h; socket_of[i] = ord[i].sock; }
     }
     return true;
   }
@@ -364,6 +372,7 @@ struct SmiBackend : Backend {
     o->render_minor = -1;
     o->card_minor = -1;
     o->partition_id = -1;
+    o->socket = socket_of[i];
     unsigned int ul = sizeof o->uuid;
     if (f.amdsmi_get_gpu_device_uuid) f.amdsmi_get_gpu_device_uuid(h, &ul, o->uuid);
     amdsmi_bdf_t bdf;
@@ -418,6 +427,8 @@ struct SmiBackend : Backend {
       o->numa_node = numa;
     if (f.amdsmi_get_gpu_compute_partition)
       f.amdsmi_get_gpu_compute_partition(h, o->compute_partition, sizeof o->compute_partition);
+    if (f.amdsmi_get_gpu_memory_partition)
+      f.amdsmi_get_gpu_memory_partition(h, o->memory_partition, sizeof o->memory_partition);
     return 0;
   }
 

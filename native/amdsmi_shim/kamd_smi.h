@@ -40,6 +40,8 @@ typedef struct {
   int32_t partition_id;      // current compute partition index on the physical GPU
   char compute_partition[32];// SPX / DPX / QPX / CPX
   char serial[KAMD_STR];
+  int32_t socket;            // physical package (OAM) index: compute partitions of one GPU share it
+  char memory_partition[16]; // NPS1 / NPS2
 } kamd_device_info_t;
 
 typedef struct {

@@ -91,6 +91,35 @@ def test_multi_gpu_hive_and_selector(run):
     run(main(), timeout=120)
 
 
+def test_cpx_partitioned_node_end_to_end(run):
+    """A node whose 2 MI355X packages run in CPX mode advertises 16 logical devices; a
+    4-partition pod lands on ONE package and its container gets those 4 render nodes."""
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=2, partition="CPX", runtime="process") as cl:
+            c = cl.client
+            node = await c.get("nodes", "node-0")
+            assert node["status"]["capacity"][core.AMD_GPU] == "16"
+            devs = node["status"]["extendedResources"][core.AMD_GPU]["resources"]
+            assert {d["attributes"][core.ATTR_PARTITION] for d in devs.values()} == {"CPX"}
+            await c.create("pods", gpu_pod("one", 1, cmd=["/bin/sleep", "60"]))
+            p1 = await cl.wait_pod("one", timeout=20)
+            await c.create("pods", gpu_pod("four", 4, cmd=["/bin/sleep", "60"]))
+            p4 = await cl.wait_pod("four", timeout=20)
+            a1 = p1["spec"]["extendedResources"][0]["assigned"]
+            a4 = p4["spec"]["extendedResources"][0]["assigned"]
+            sock = lambda i: devs[i]["attributes"][core.ATTR_SOCKET]   # noqa: E731
+            # the 4-partition pod packs into the package the first pod opened (best fit)
+            assert len({sock(i) for i in a4}) == 1 and sock(a4[0]) == sock(a1[0]) and not set(a1) & set(a4)
+            rt = cl.nodes[0].runtime
+            want = sorted(f"renderD{devs[i]['attributes'][core.ATTR_RENDER_MINOR]}" for i in a4)
+            specs = []
+            for x in rt.list_containers():
+                spec = json.load(open(os.path.join(os.path.dirname(x.log_path), "config.json")))
+                specs.append(sorted(spec["annotations"]["amd.com/gpu-render-nodes"].split(",")))
+            assert want in specs
+    run(main(), timeout=120)
+
+
 def test_process_runtime_injects_devices(run):
     async def main():
         async with LocalCluster(nodes=1, gpus_per_node=2, runtime="process") as cl:

@@ -37,6 +37,19 @@ def test_fake_backend_two_hives():
     assert topo[0][4].type == amdsmi.LINK_PCIE and not topo[0][4].p2p
 
 
+def test_fake_backend_cpx_partitions():
+    """CPX mode: each MI355X package exposes 8 logical devices (one XCD, 32 CUs, 1/8 of the
+    HBM, own render node) sharing the package's socket; NPS is reported per device."""
+    smi = amdsmi.SMI(fixture=amdsmi.fixture_file(2, partition="CPX", memory_partition="NPS2"))
+    gs = smi.gpus()
+    assert len(gs) == 16 and len({g.device_id_str for g in gs}) == 16
+    assert {g.render_minor for g in gs} == set(range(128, 144))
+    assert [g.socket for g in gs] == [0] * 8 + [1] * 8 and [g.partition_id for g in gs[:8]] == list(range(8))
+    assert all(g.compute_units == 32 and g.vram_total_mb == 294912 // 8 and g.memory_partition == "NPS2" for g in gs)
+    on_pkg, off_pkg = smi.link(0, 7), smi.link(0, 8)
+    assert on_pkg.hops == 0 and on_pkg.weight < off_pkg.weight and off_pkg.type == amdsmi.LINK_XGMI
+
+
 def test_bad_fixture(tmp_path):
     p = tmp_path / "bad.json"
     p.write_text("{nope")

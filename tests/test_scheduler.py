@@ -1,6 +1,7 @@
 """Scheduler: ER allocation (fork F4/F5 tests `extended_resources_test.go:59-193`,
 `node_info_test.go`), topology-aware placement, the assume fix, end-to-end with the API server."""
 import asyncio
+import os
 
 import pytest
 
@@ -314,3 +315,75 @@ def test_partitioned_scheduler_shards_embedded(run):
 
 def test_partitioned_scheduler_shards_shared_store_fanout(run):
     _sharded_run(run, shared=True)
+
+
+# -- compute partitions (CPX/QPX): logical devices that share an MI355X package ----------------
+
+def cpx_devs(sockets=2, per=8, part="CPX", hive="h0", links="7"):
+    """Device entries as the amd.com/gpu plugin advertises them for a CPX node (fixture-built)."""
+    from kubernetes_amd.deviceplugin.amdgpu import gpu_attributes
+    from kubernetes_amd.native import amdsmi
+    if not os.path.exists(amdsmi.lib_path()):
+        out = []
+        for s in range(sockets):
+            for p in range(per):
+                d = gpu_dev(s * per + p, hive=hive, links=links)
+                d["attributes"].update({core.ATTR_PARTITION: part, core.ATTR_SOCKET: str(s),
+                                        core.ATTR_PARTITION_ID: str(p)})
+                out.append(d)
+        return out
+    smi = amdsmi.SMI(fixture=amdsmi.fixture_file(sockets, partition=part, seed="cpx"))
+    out = []
+    for g in smi.gpus():
+        a = gpu_attributes(g, smi.metrics(g.index))
+        a[core.ATTR_HIVE] = hive
+        a[core.ATTR_XGMI_LINKS] = links
+        out.append({"id": f"g{g.index}", "health": core.HEALTHY, "attributes": a})
+    return out
+
+
+def _sockets(e, ids):
+    return {e.available[core.AMD_GPU][i]["attributes"][core.ATTR_SOCKET] for i in ids}
+
+
+def test_cpx_partitions_pack_into_one_package():
+    devs = cpx_devs(2)
+    assert {d["attributes"][core.ATTR_PARTITION] for d in devs} == {"CPX"} and len(devs) == 16
+    e = er_of(devs)
+    # 8 partitions = one whole package; with only 1 xGMI link up they still fit (no links used)
+    b, score, _ = allocate([Request("er", core.AMD_GPU, 8, [])], er_of(cpx_devs(2, links="0")))
+    assert b is not None and len(_sockets(e, b["er"]["resources"])) == 1 and score == 10.0
+    # single partitions fill a package before opening the next one
+    e.add_pod("a/b", {core.AMD_GPU: ["g0"]})
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 1, [])], e)
+    assert b["er"]["resources"] == ["g1"]
+    # a 4-partition pod fits in ONE package; the used one (6 free) is the best fit
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 4, [])], e)
+    assert _sockets(e, b["er"]["resources"]) == {"0"}
+    # 12 partitions: the whole free package + 4 of the used one (fewest packages)
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 12, [])], e)
+    ids = b["er"]["resources"]
+    assert len(ids) == 12 and len(_sockets(e, ids)) == 2 and "g0" not in ids
+
+
+def test_cpx_multi_package_needs_links_per_package():
+    # 16 partitions span 2 packages -> each needs >= 1 xGMI link
+    assert allocate([Request("er", core.AMD_GPU, 16, [])], er_of(cpx_devs(2, links="0")))[0] is None
+    b, _, _ = allocate([Request("er", core.AMD_GPU, 16, [])], er_of(cpx_devs(2, links="1")))
+    assert b is not None and len(b["er"]["resources"]) == 16
+
+
+def test_cpx_scheduler_prefers_node_with_partly_used_package():
+    cache = SchedulerCache()
+    cache.add_node(node("fresh", cpx_devs(2)))
+    cache.add_node(node("used", cpx_devs(2)))
+    p0 = gpu_pod("x", 3)
+    p0["spec"]["nodeName"] = "used"
+    p0["spec"]["extendedResources"][0]["assigned"] = ["g0", "g1", "g2"]
+    cache.add_pod(p0)
+    gs = GenericScheduler(cache)
+    host, erb = gs.schedule(gpu_pod("y", 5))           # fills package 0 of "used" exactly
+    assert host == "used" and sorted(erb["er"]["resources"]) == [f"g{i}" for i in range(3, 8)]
+    # selector on the partition mode / per-partition compute units
+    host, _ = gs.schedule(gpu_pod("z", 1, required=[{"key": core.ATTR_CUS, "operator": "Lt", "values": ["64"]}]))
+    assert host in ("fresh", "used")
