@@ -31,13 +31,14 @@ class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
                  health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None,
-                 partition="SPX"):
+                 partition="SPX", burn_in=None):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
         self.real = real_gpus
         self.hives = hives
         self.partition = partition             # fake backend: SPX/DPX/QPX/CPX compute partitions
+        self.burn_in = burn_in                 # deviceplugin.burnin.BurnIn: gate GPUs on the HIP acceptance test
         self.own_dir = workdir is None
         self.dir = workdir or tempfile.mkdtemp(prefix="kamd-cluster-")
         self.emit_events = emit_events
@@ -96,7 +97,7 @@ class LocalCluster:
         await kl.run()
         if self.gpus:
             plugin = AMDGPUPlugin(plugins_dir, smi=self.smi, health_interval=self.health_interval,
-                                  rocm_mount=self.rocm_mount)
+                                  rocm_mount=self.rocm_mount, burn_in=self.burn_in)
             await plugin.start()
         h = NodeHandle(name, kl, plugin, dm, rt, plugins_dir)
         self.nodes.append(h)

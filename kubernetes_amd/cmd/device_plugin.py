@@ -22,6 +22,10 @@ def main(argv=None):
     ap.add_argument("--rocm-mount", default=None, help="bind the ROCm userspace read-only into GPU containers")
     ap.add_argument("--exporter-port", type=int, default=None)
     ap.add_argument("--node-name", default="")
+    ap.add_argument("--burn-in", action="store_true",
+                    help="gate every GPU on the HIP acceptance test (vector_add, MFMA GEMM, HBM copy) before offering it")
+    ap.add_argument("--burn-in-min-tflops", type=float, default=700.0)
+    ap.add_argument("--burn-in-min-hbm-gbps", type=float, default=3000.0)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -29,8 +33,12 @@ def main(argv=None):
     async def start():
         fixture = a.fixture or (amdsmi.fixture_file(a.fake_gpus) if a.fake_gpus else None)
         smi = amdsmi.SMI(fixture=fixture)
+        burn_in = None
+        if a.burn_in:
+            from ..deviceplugin.burnin import BurnIn
+            burn_in = BurnIn(min_tflops=a.burn_in_min_tflops, min_hbm_gbps=a.burn_in_min_hbm_gbps)
         p = AMDGPUPlugin(a.plugins_dir, smi=smi, socket_name=a.socket_name, health_interval=a.health_interval,
-                         rocm_mount=a.rocm_mount)
+                         rocm_mount=a.rocm_mount, burn_in=burn_in)
         await p.start()
         print(f"amd.com/gpu plugin serving {len(p.gpus)} GPU(s) on {p.socket_path}", flush=True)
         if a.exporter_port is not None:

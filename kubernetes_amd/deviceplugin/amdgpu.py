@@ -13,6 +13,9 @@ Replaces the out-of-tree NVIDIA plugin the reference targets (NVML enumeration,
     (no vendor runtime, no NVML/CUDA shim) and, optionally, the ROCm userspace read-only;
     `AMD_VISIBLE_DEVICES` lists the host HIP ordinals (informational, like
     NVIDIA_VISIBLE_DEVICES) — a non-isolating runtime turns it into HIP_VISIBLE_DEVICES.
+  * burn-in (optional, deviceplugin/burnin.py): each GPU runs the framework's HIP vector_add,
+    MFMA GEMM and HBM-copy kernels before it is offered; it stays Unhealthy until it passes,
+    and the measured TFLOP/s and GB/s become attributes (`amd.com/mfma-tflops`, `amd.com/hbm-gbps`);
   * health: a device turns Unhealthy when its uncorrectable ECC count rises above the
     baseline seen at start, when an xGMI link goes down, or (real backend) when its render
     node disappears; the change is pushed on every open ListAndWatch stream.
@@ -26,7 +29,12 @@ import os
 from ..api import core
 from ..native import amdsmi
 from . import api
+from .burnin import FAILED, PASSED, PENDING
 from .server import DevicePluginServer, device
+
+ATTR_BURN_IN = "amd.com/burn-in"          # pending / passed / failed
+ATTR_MFMA_TFLOPS = "amd.com/mfma-tflops"  # measured bf16 MFMA GEMM throughput
+ATTR_HBM_GBPS = "amd.com/hbm-gbps"        # measured HBM copy bandwidth
 
 log = logging.getLogger("amdgpu-plugin")
 
@@ -64,8 +72,13 @@ def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None) -> dict:
 class AMDGPUPlugin(DevicePluginServer):
     def __init__(self, plugins_dir: str, smi: amdsmi.SMI | None = None, socket_name="amdgpu.sock",
                  health_interval=5.0, dev_root="/dev", rocm_mount: str | None = None, indices=None,
-                 check_dev_nodes: bool | None = None, init_timeout=10):
+                 check_dev_nodes: bool | None = None, init_timeout=10, burn_in=None):
         self.smi = smi or amdsmi.SMI()
+        # optional acceptance test (deviceplugin/burnin.py): devices stay Unhealthy until it
+        # passes; `burn_in` is a BurnIn or any object with run(hip_index) -> BurnInResult
+        self.burn_in = burn_in
+        self._burn: dict[str, object] = {}        # device id -> BurnInResult (absent = pending)
+        self._burn_task = None
         self.dev_root = dev_root
         self.rocm_mount = rocm_mount
         self.health_interval = health_interval
@@ -83,7 +96,7 @@ class AMDGPUPlugin(DevicePluginServer):
             self._links_base[g.index] = m.xgmi_links_up
             h = self._check(g, m)
             self._health[g.device_id_str] = h
-            devs.append(device(g.device_id_str, h, gpu_attributes(g, m)))
+            devs.append(self._device(g, m, h))
         labels = {}
         if self.gpus:
             g0 = self.gpus[0]
@@ -95,7 +108,21 @@ class AMDGPUPlugin(DevicePluginServer):
         self._health_task = None
 
     # -- health -------------------------------------------------------------
+    def _device(self, g: amdsmi.GPU, m: amdsmi.Metrics, health: str):
+        attrs = gpu_attributes(g, m)
+        if self.burn_in is not None:
+            r = self._burn.get(g.device_id_str)
+            attrs[ATTR_BURN_IN] = PENDING if r is None else (PASSED if r.ok else FAILED)
+            if r is not None and r.tflops:
+                attrs[ATTR_MFMA_TFLOPS] = str(int(r.tflops))
+                attrs[ATTR_HBM_GBPS] = str(int(r.hbm_gbps))
+        return device(g.device_id_str, health, attrs)
+
     def _check(self, g: amdsmi.GPU, m: amdsmi.Metrics) -> str:
+        if self.burn_in is not None:
+            r = self._burn.get(g.device_id_str)
+            if r is None or not r.ok:
+                return api.UNHEALTHY
         if m.ecc_uncorrectable > self._ecc_base.get(g.index, 0):
             return api.UNHEALTHY
         if m.xgmi_links_up < self._links_base.get(g.index, 0):
@@ -104,7 +131,7 @@ class AMDGPUPlugin(DevicePluginServer):
             return api.UNHEALTHY
         return api.HEALTHY
 
-    def poll_health(self) -> bool:
+    def poll_health(self, force=False) -> bool:
         """Re-evaluate health; push a new list if anything changed. Returns True if changed."""
         changed = False
         devs = []
@@ -115,10 +142,33 @@ class AMDGPUPlugin(DevicePluginServer):
                 log.warning("device %s health %s -> %s", g.device_id_str, self._health.get(g.device_id_str), h)
                 self._health[g.device_id_str] = h
                 changed = True
-            devs.append(device(g.device_id_str, h, gpu_attributes(g, m)))
-        if changed:
+            devs.append(self._device(g, m, h))
+        if changed or force:
             self.update(devs)
         return changed
+
+    async def run_burn_in(self):
+        """Run the acceptance test on every device (one worker thread per GPU: the HIP calls
+        release the GIL and each thread binds its own device), publishing each result as it
+        lands. Returns {device id: BurnInResult}."""
+        loop = asyncio.get_running_loop()
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max(1, len(self.gpus)), thread_name_prefix="burn-in")
+
+        async def one(g):
+            r = await loop.run_in_executor(pool, self.burn_in.run, g.hip_id if g.hip_id >= 0 else g.index)
+            self._burn[g.device_id_str] = r
+            if r.ok:
+                log.info("burn-in passed on %s: %.0f TFLOP/s MFMA bf16, %.0f GB/s HBM (%.1f s)",
+                         g.device_id_str, r.tflops, r.hbm_gbps, r.seconds)
+            else:
+                log.error("burn-in FAILED on %s: %s", g.device_id_str, r.reason)
+            self.poll_health(force=True)
+        try:
+            await asyncio.gather(*(one(g) for g in self.gpus))
+        finally:
+            pool.shutdown(wait=False)
+        return dict(self._burn)
 
     async def _health_loop(self):
         while True:
@@ -132,11 +182,15 @@ class AMDGPUPlugin(DevicePluginServer):
         await super().start()
         if self.health_interval:
             self._health_task = asyncio.ensure_future(self._health_loop())
+        if self.burn_in is not None:
+            self._burn_task = asyncio.ensure_future(self.run_burn_in())
         return self
 
     async def stop(self, grace=0.1):
         if self._health_task:
             self._health_task.cancel()
+        if self._burn_task:
+            self._burn_task.cancel()
         await super().stop(grace)
 
     # -- allocation hooks -------------------------------------------------------------

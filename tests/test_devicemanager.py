@@ -5,6 +5,7 @@ stub plugins, capacity add/remove, health-only changes), `:173` (re-registration
 `endpoint_test.go`, `device_store_test.go`, `plugin_watcher_test.go:65,119`.
 """
 import asyncio
+import threading
 import os
 
 import pytest
@@ -174,6 +175,61 @@ def test_amdgpu_plugin_admit_and_init_container(tmp_path, run):
         with pytest.raises(AdmitError):
             await m.admit_pod(_pod("u4", [ids[5]], "s"))
         smi.fake_set_ecc(5, 0)
+        await plugin.stop()
+        await m.stop()
+    run(main())
+
+
+def test_burn_in_gates_devices_and_publishes_measurements(tmp_path, run):
+    """With a burn-in configured, GPUs are offered Unhealthy (`amd.com/burn-in=pending`) until
+    their acceptance test passes; a GPU that fails stays Unhealthy; measured TFLOP/s and GB/s
+    become attributes the scheduler's selectors can use."""
+    from kubernetes_amd.deviceplugin.amdgpu import ATTR_BURN_IN, ATTR_HBM_GBPS, ATTR_MFMA_TFLOPS
+    from kubernetes_amd.deviceplugin.burnin import BurnIn, BurnInResult
+    from kubernetes_amd.scheduler.cache import ERManager
+    from kubernetes_amd.scheduler.topology import Request, allocate
+
+    class FakeBurnIn(BurnIn):
+        def __init__(self):
+            super().__init__(min_tflops=700, min_hbm_gbps=3000)
+            self.release = threading.Event()
+
+        def run(self, i):
+            self.release.wait(5)
+            r = BurnInResult(ok=False, tflops=1400.0 - 100 * i, hbm_gbps=6000.0, mfma_rel_err=1e-4)
+            if i == 3:
+                r.tflops = 350.0                       # throttled part
+            r.reason = self.judge(r)
+            r.ok = not r.reason
+            return r
+
+    async def main():
+        smi = amdsmi.SMI(fixture=amdsmi.fixture_file(4, seed="burn"))
+        bi = FakeBurnIn()
+        plugin = AMDGPUPlugin(str(tmp_path), smi=smi, health_interval=0, burn_in=bi)
+        ids = [g.device_id_str for g in plugin.gpus]
+        m = ManagerImpl(str(tmp_path))
+        await m.start(lambda: [])
+        await plugin.start()
+        await until(lambda: "amd.com/gpu" in m.get_capacity()[0])
+        cap = m.get_capacity()[0]["amd.com/gpu"]["resources"]
+        assert all(d["health"] == api.UNHEALTHY and d["attributes"][ATTR_BURN_IN] == "pending" for d in cap.values())
+        with pytest.raises(AdmitError):
+            await m.admit_pod(_pod("u0", [ids[0]]))
+        bi.release.set()
+        await until(lambda: all(d["attributes"][ATTR_BURN_IN] != "pending"
+                                for d in m.get_capacity()[0]["amd.com/gpu"]["resources"].values()))
+        cap = m.get_capacity()[0]["amd.com/gpu"]["resources"]
+        assert [cap[i]["health"] for i in ids] == [api.HEALTHY] * 3 + [api.UNHEALTHY]
+        assert cap[ids[3]]["attributes"][ATTR_BURN_IN] == "failed" and "350" in plugin._burn[ids[3]].reason
+        assert cap[ids[1]]["attributes"][ATTR_MFMA_TFLOPS] == "1300" and cap[ids[1]]["attributes"][ATTR_HBM_GBPS] == "6000"
+        await m.admit_pod(_pod("u1", [ids[0]]))
+        # a pod can ask for the fastest parts only
+        er = ERManager()
+        er.set_node({"metadata": {"name": "n"}, "status": {"extendedResources": m.get_capacity()[0]}})
+        b, _, _ = allocate([Request("er", "amd.com/gpu", 2, [{"key": ATTR_MFMA_TFLOPS, "operator": "Gt",
+                                                               "values": ["1250"]}])], er)
+        assert sorted(b["er"]["resources"]) == sorted(ids[:2])
         await plugin.stop()
         await m.stop()
     run(main())

@@ -56,3 +56,38 @@ def test_e2e_gpu_spec_on_real_mi355x(run):
             res = await run_specs(cl.url, focus="Feature:GPU", timeout=150)
         assert len(res) == 1 and res[0].ok, res[0].error if res else "no spec ran"
     run(main(), timeout=200)
+
+
+def test_burn_in_gates_real_gpus_then_pod_runs(run):
+    """The plugin's acceptance test on the real MI355X: HIP vector_add exact, MFMA bf16 GEMM
+    8192^3 within tolerance and >= 700 TFLOP/s, HBM copy >= 3000 GB/s; only then does the GPU
+    turn Healthy, carry its measured numbers, and take a pod."""
+    import asyncio
+    from kubernetes_amd.api import core
+    from kubernetes_amd.cluster import LocalCluster
+    from kubernetes_amd.deviceplugin.burnin import BurnIn
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8, real_gpus=True, burn_in=BurnIn()) as cl:
+            plugin = cl.nodes[0].plugin
+            loop = asyncio.get_running_loop()
+            end = loop.time() + 90
+            while loop.time() < end and len(plugin._burn) < len(plugin.gpus):
+                await asyncio.sleep(0.2)
+            for i, r in plugin._burn.items():
+                print(i, r)
+            passed = {i: r for i, r in plugin._burn.items() if r.ok}
+            assert passed, plugin._burn
+            for r in passed.values():
+                assert r.tflops >= 700 and r.hbm_gbps >= 3000 and r.mfma_rel_err < 1e-2 and r.vadd_err == 0
+            await asyncio.sleep(0.5)
+            node = await cl.client.get("nodes", cl.nodes[0].name)
+            devs = node["status"]["extendedResources"][core.AMD_GPU]["resources"]
+            for i in passed:
+                assert devs[i]["health"] == "Healthy" and devs[i]["attributes"]["amd.com/burn-in"] == "passed"
+                assert int(devs[i]["attributes"]["amd.com/mfma-tflops"]) >= 700
+            await cl.client.create("pods", {"metadata": {"name": "after-burn-in"}, "spec": {"containers": [
+                {"name": "c", "image": "kubernetes-amd/hip-vector-add", "resources": {"limits": {core.AMD_GPU: "1"}}}]}})
+            p = await cl.wait_pod("after-burn-in", timeout=30)
+            assert p["spec"]["extendedResources"][0]["assigned"][0] in passed
+    run(main(), timeout=150)
