@@ -36,7 +36,7 @@ def targets():
         "kamd_store": ([_s("store", "mvcc_store.cc")], os.path.join(LIB_DIR, "libkamd_store.so"),
                        cxx + ["-O3", "-shared", _s("store", "mvcc_store.cc")]),
         "kamd_etcd": ([_s("store", "mvcc_store.cc")], os.path.join(BIN_DIR, "kamd-etcd"),
-                      cxx + ["-O3", "-DKAMD_STORE_SERVER", _s("store", "mvcc_store.cc")]),
+                      cxx + ["-O3", "-pthread", "-DKAMD_STORE_SERVER", _s("store", "mvcc_store.cc")]),
         "kamd_oci": ([_s("oci", "oci_devices.cc")], os.path.join(LIB_DIR, "libkamd_oci.so"),
                      cxx + ["-shared", _s("oci", "oci_devices.cc")]),
         "kamd_crypto": ([_s("crypto", "kamd_crypto.cc")], os.path.join(LIB_DIR, "libkamd_crypto.so"),
@@ -75,7 +75,10 @@ def sanitizer_targets():
     store = _s("store", "mvcc_store.cc")
     return {
         "asan_kamd_etcd": ([store], os.path.join(asan, "kamd-etcd"),
-                           base + SAN_FLAGS["asan"] + ["-DKAMD_STORE_SERVER", store]),
+                           base + SAN_FLAGS["asan"] + ["-pthread", "-DKAMD_STORE_SERVER", store]),
+        # the store thread and the watch fan-out thread share the event queue and KV lifetimes
+        "tsan_kamd_etcd": ([store], os.path.join(tsan, "kamd-etcd"),
+                           base + SAN_FLAGS["tsan"] + ["-pthread", "-DKAMD_STORE_SERVER", store]),
         "asan_store_fuzz": ([store, _s("tests", "store_fuzz.cc")], os.path.join(asan, "store_fuzz"),
                             base + SAN_FLAGS["asan"] + [_s("tests", "store_fuzz.cc")]),
         "tsan_smi_threads": ([_s("amdsmi_shim", "kamd_smi.cc"), _s("amdsmi_shim", "kamd_smi.h"), _s("tests", "smi_threads.cc")],

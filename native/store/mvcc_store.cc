@@ -42,17 +42,21 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <time.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -163,12 +167,16 @@ class Engine {
           if (last && changes) log_wal(1, true, o.key, "");  // keep the txn terminated in the WAL
           continue;
         }
-        auto dk = std::make_shared<KV>(*it->second);
+        // field by field: `aux` belongs to the watch fan-out thread and is never read here
+        auto dk = std::make_shared<KV>();
+        dk->create_rev = it->second->create_rev;
         dk->mod_rev = r;
         dk->version = 0;
         if (o.kind == 3) {  // tombstone: final object state reported to watchers, not stored
           dk->value = o.val;
           inject(&dk->value, o.token, rs);
+        } else {
+          dk->value = it->second->value;
         }
         std::shared_ptr<KV> before = it->second;
         data_.erase(it);
@@ -225,7 +233,7 @@ class Engine {
   void for_prefix(const std::string& prefix, F f) const {
     for (auto it = data_.lower_bound(prefix); it != data_.end(); ++it) {
       if (it->first.compare(0, prefix.size(), prefix) != 0) break;
-      f(it->first, *it->second);
+      f(it->first, it->second);
     }
   }
 
@@ -462,6 +470,7 @@ struct Conn {
   int fd;
   std::string in, out;
   bool want_write = false;
+  bool pollout = false;   // EPOLLOUT currently registered (MOD only on a change: one syscall less per flush)
 };
 
 struct Watch {
@@ -689,6 +698,11 @@ struct FanWatch {
   bool node_indexed = false;
   std::string node_key;   // spec.nodeName=X requirement: the watch lives in fan_by_node_[X]
   double deadline = 0;  // CLOCK_MONOTONIC seconds, 0 = none
+  bool pollout = false;
+  // set by the store thread at handoff, consumed by the fan-out thread when it adopts the watch
+  bool send_initial = false;
+  std::vector<std::shared_ptr<KV>> initial;   // snapshot of the prefix (list + watch)
+  std::vector<Event> replay;                   // events after the requested resourceVersion
   bool matches(const Index& ix) const {
     if (!ix.ok) return false;
     for (const auto& r : reqs)
@@ -717,6 +731,318 @@ static void chunk(std::string* out, const char* type, const std::string& v, size
   out->append(v, body, std::string::npos);
   out->append("}\n\r\n", 4);
 }
+
+// Watch fan-out thread. Kubernetes watch streams handed over by the API server workers are
+// served here, off the store thread: the store thread commits transactions and answers
+// workers, then posts each loop pass's events (one lock per pass) and any newly handed-over
+// watch, in commit order; this thread matches them against the watches' selectors (index
+// parse cached on the value), formats the chunks and writes the sockets. Ordering: a watch is
+// adopted after every event that precedes its snapshot / replay and before every later one, so
+// nothing is lost or sent twice. The store thread never touches KV::aux (the parse cache).
+class FanOut {
+ public:
+  ~FanOut() { stop(); }
+
+  void start() {
+    ep_ = epoll_create1(EPOLL_CLOEXEC);
+    evfd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event e{};
+    e.events = EPOLLIN;
+    e.data.fd = evfd_;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, evfd_, &e);
+    th_ = std::thread([this] { loop(); });
+  }
+
+  void stop() {
+    if (!th_.joinable()) return;
+    stop_.store(true);
+    wake();
+    th_.join();
+    for (auto& kv : fan_) close(kv.first);
+    fan_.clear();
+    close(evfd_);
+    close(ep_);
+  }
+
+  // store thread: queue a committed transaction's events / a new watch (order preserved)
+  void post(std::vector<Event>&& evs) {
+    if (watches_.load(std::memory_order_acquire) == 0) return;   // nobody to tell
+    if (pending_.empty() || !pending_.back().evs_only) pending_.emplace_back();
+    auto& b = pending_.back().evs;
+    if (b.empty()) b = std::move(evs);
+    else for (Event& e : evs) b.push_back(std::move(e));
+  }
+  void post(std::unique_ptr<FanWatch> w) {
+    pending_.emplace_back();
+    pending_.back().evs_only = false;
+    pending_.back().w = std::move(w);
+    watches_.fetch_add(1, std::memory_order_acq_rel);   // before any later event is posted
+  }
+  // store thread, once per loop pass: hand everything queued to the fan-out thread
+  void commit() {
+    if (pending_.empty()) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (Msg& m : pending_) q_.push_back(std::move(m));
+    }
+    pending_.clear();
+    wake();
+  }
+
+ private:
+  struct Msg {
+    bool evs_only = true;
+    std::vector<Event> evs;
+    std::unique_ptr<FanWatch> w;
+  };
+
+  void wake() {
+    uint64_t one = 1;
+    ssize_t r = write(evfd_, &one, sizeof one);
+    (void)r;
+  }
+
+  void loop() {
+    epoll_event evs[256];
+    std::vector<Msg> work;
+    while (!stop_.load()) {
+      int n = epoll_wait(ep_, evs, 256, next_timeout_ms());
+      for (int i = 0; i < n; ++i) {
+        int fd = evs[i].data.fd;
+        if (fd == evfd_) {
+          uint64_t v;
+          ssize_t r = read(evfd_, &v, sizeof v);
+          (void)r;
+          continue;
+        }
+        auto fw = fan_.find(fd);
+        if (fw == fan_.end()) continue;
+        FanWatch* w = fw->second.get();
+        if (evs[i].events & (EPOLLHUP | EPOLLERR | EPOLLRDHUP)) { close_fan(w); continue; }
+        if (evs[i].events & EPOLLIN) {
+          char junk[4096];
+          ssize_t r = read(fd, junk, sizeof junk);
+          if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK)) { close_fan(w); continue; }
+        }
+        if (evs[i].events & EPOLLOUT) flush_fan(w);
+      }
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        work.swap(q_);
+      }
+      for (Msg& m : work) {
+        if (m.w) adopt(std::move(m.w));
+        else if (!m.evs.empty()) {
+          KPROF_BEGIN;
+          fan_dispatch(m.evs);
+          KPROF_END(6);
+        }
+      }
+      work.clear();
+      {
+        KPROF_BEGIN;
+        for (FanWatch* w : fan_dirty_) {
+          w->queued = false;
+          flush_fan(w);
+        }
+        fan_dirty_.clear();
+        KPROF_END(8);
+      }
+      expire_fan();
+      reap_fan();
+    }
+  }
+
+  void adopt(std::unique_ptr<FanWatch> w) {
+    FanWatch* raw = w.get();
+    if (w->send_initial) {
+      for (const auto& kv : w->initial) {
+        const Index& ix = index_of(*kv);
+        if (w->matches(ix)) chunk(&w->out, "ADDED", kv->value, ix.body);
+      }
+    }
+    for (const Event& e : w->replay) fan_one(raw, e);
+    w->initial.clear();
+    w->initial.shrink_to_fit();
+    w->replay.clear();
+    w->replay.shrink_to_fit();
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP;
+    e.data.fd = raw->fd;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, raw->fd, &e);
+    if (raw->node_indexed) fan_by_node_[raw->node_key].push_back(raw);
+    else fan_other_.push_back(raw);
+    fan_[raw->fd] = std::move(w);
+    flush_fan(raw);
+  }
+
+  int next_timeout_ms() {
+    double soonest = 0;
+    for (auto& kv : fan_)
+      if (kv.second->deadline > 0 && (soonest == 0 || kv.second->deadline < soonest)) soonest = kv.second->deadline;
+    if (soonest == 0) return 1000;
+    double ms = (soonest - mono_now()) * 1000.0;
+    return ms < 0 ? 0 : (ms > 1000 ? 1000 : (int)ms + 1);
+  }
+
+  // one event into one watch (cacher.go dispatch rules: a MODIFIED object that stops matching is
+  // a DELETED for that watcher, one that starts matching an ADDED)
+  void fan_one(FanWatch* w, const Event& ev, const Index* cur = nullptr, const Index* prv = nullptr) {
+    if (ev.key.compare(0, w->prefix.size(), w->prefix) != 0 || ev.rev <= w->min_rev) return;
+    if (!cur) cur = &index_of(*ev.kv);
+    if (!prv) prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
+    bool now = w->matches(*cur);
+    bool was = ev.prev && w->matches(*prv);
+    const std::string& v = ev.kv->value;
+    if (ev.type == 0) {
+      if (now && was) chunk(&w->out, "MODIFIED", v, cur->body);
+      else if (now) chunk(&w->out, "ADDED", v, cur->body);
+      else if (was) chunk(&w->out, "DELETED", v, cur->body);
+      else return;
+    } else {
+      if (!(now || was) || !cur->ok) return;
+      chunk(&w->out, "DELETED", v, cur->body);
+    }
+    mark_fan(w);
+  }
+
+  // Per event: the unindexed watches, plus the watches of the node the object is on now and
+  // was on before (O(matching watchers), not O(all watchers), with one watch per kubelet).
+  void fan_dispatch(const std::vector<Event>& evs) {
+    if (fan_.empty()) return;
+    for (const Event& ev : evs) {
+      const Index* cur = nullptr;
+      const Index* prv = nullptr;
+      auto parse = [&]() {
+        if (cur) return;
+        cur = &index_of(*ev.kv);
+        prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
+      };
+      for (FanWatch* w : fan_other_) {
+        if (w->dead || ev.key.compare(0, w->prefix.size(), w->prefix) != 0) continue;
+        parse();
+        fan_one(w, ev, cur, prv);
+      }
+      if (fan_by_node_.empty()) continue;
+      parse();
+      auto node_of = [](const Index& ix) -> std::string_view {
+        const std::string_view* it = sv_find(ix.fields, "spec.nodeName");
+        return it ? *it : std::string_view();
+      };
+      std::string_view a = node_of(*cur);
+      auto bucket = [&](std::string_view n) {
+        auto it = fan_by_node_.find(std::string(n));
+        if (it == fan_by_node_.end()) return;
+        for (FanWatch* w : it->second)
+          if (!w->dead) fan_one(w, ev, cur, prv);
+      };
+      bucket(a);
+      if (ev.prev) {
+        std::string_view b = node_of(*prv);
+        if (b != a) bucket(b);
+      }
+    }
+    // a superseded value's parse is not needed again (resumed watches re-parse on demand):
+    // the cache lives on current values only, so history memory does not grow with it
+    for (const Event& ev : evs) {
+      if (ev.prev) ev.prev->aux.reset();
+      if (ev.type == 1) ev.kv->aux.reset();   // a tombstone is never a current value
+    }
+  }
+
+  void mark_fan(FanWatch* w) {
+    if (!w->out.empty() && !w->queued) {
+      w->queued = true;
+      fan_dirty_.push_back(w);
+    }
+  }
+
+  void set_pollout(FanWatch* w, bool on) {
+    if (w->pollout == on) return;
+    w->pollout = on;
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP | (on ? EPOLLOUT : 0);
+    e.data.fd = w->fd;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, w->fd, &e);
+  }
+
+  void flush_fan(FanWatch* w) {
+    while (!w->out.empty()) {
+      ssize_t n = write(w->fd, w->out.data(), w->out.size());
+      if (g_prof.on) ++g_prof.n[11];   // count of fan-out write() calls
+      if (n > 0) { w->out.erase(0, (size_t)n); continue; }
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (w->out.size() > (64u << 20)) { w->dead = true; w->out.clear(); return; }   // slow watcher
+        set_pollout(w, true);
+        return;
+      }
+      w->dead = true;
+      w->out.clear();
+      return;
+    }
+    set_pollout(w, false);
+  }
+
+  void expire_fan() {
+    double now = 0;
+    for (auto& kv : fan_) {
+      FanWatch* w = kv.second.get();
+      if (w->deadline <= 0 || w->dead) continue;
+      if (now == 0) now = mono_now();
+      if (now >= w->deadline) {
+        w->out.append("0\r\n\r\n");   // end of the chunked body: the watch timed out normally
+        w->dead = true;
+        flush_fan(w);
+      }
+    }
+  }
+
+  void close_fan(FanWatch* w) {
+    w->dead = true;
+    w->out.clear();
+  }
+
+  void reap_fan() {
+    for (auto it = fan_.begin(); it != fan_.end();) {
+      FanWatch* w = it->second.get();
+      if (w->dead && w->out.empty()) {
+        fan_dirty_.erase(std::remove(fan_dirty_.begin(), fan_dirty_.end(), w), fan_dirty_.end());
+        auto drop = [w](std::vector<FanWatch*>* v) { v->erase(std::remove(v->begin(), v->end(), w), v->end()); };
+        if (w->node_indexed) {
+          auto b = fan_by_node_.find(w->node_key);
+          if (b != fan_by_node_.end()) {
+            drop(&b->second);
+            if (b->second.empty()) fan_by_node_.erase(b);
+          }
+        } else {
+          drop(&fan_other_);
+        }
+        epoll_ctl(ep_, EPOLL_CTL_DEL, w->fd, nullptr);
+        close(w->fd);
+        it = fan_.erase(it);
+        watches_.fetch_sub(1, std::memory_order_acq_rel);
+      } else {
+        ++it;
+      }
+    }
+  }
+
+  // store thread only
+  std::vector<Msg> pending_;
+  // shared
+  std::mutex mu_;
+  std::vector<Msg> q_;
+  std::atomic<bool> stop_{false};
+  std::atomic<int> watches_{0};   // posted and not yet reaped
+  std::thread th_;
+  int ep_ = -1;
+  int evfd_ = -1;
+  // fan-out thread only
+  std::map<int, std::unique_ptr<FanWatch>> fan_;
+  std::vector<FanWatch*> fan_dirty_;
+  std::vector<FanWatch*> fan_other_;
+  std::unordered_map<std::string, std::vector<FanWatch*>> fan_by_node_;
+};
 
 class Server {
  public:
@@ -764,26 +1090,15 @@ class Server {
   // returns when SIGTERM/SIGINT set *stop (a clean exit: destructors run, so leak checkers and
   // the WAL's final fclose see a normal shutdown)
   void run(volatile sig_atomic_t* stop) {
+    fan_.start();
     epoll_event evs[256];
     while (!*stop) {
-      int n = epoll_wait(ep_, evs, 256, next_timeout_ms());
+      int n = epoll_wait(ep_, evs, 256, 1000);
       for (int i = 0; i < n; ++i) {
         int fd = evs[i].data.fd;
         if (handoff_listeners_.count(fd)) { accept_handoffs(fd); continue; }
         if (listeners_.count(fd)) { accept_all(fd); continue; }
         if (handoffs_.count(fd)) { read_handoff(fd); continue; }
-        auto fw = fan_.find(fd);
-        if (fw != fan_.end()) {
-          FanWatch* w = fw->second.get();
-          if (evs[i].events & (EPOLLHUP | EPOLLERR | EPOLLRDHUP)) { close_fan(w); continue; }
-          if (evs[i].events & EPOLLIN) {
-            char junk[4096];
-            ssize_t r = read(fd, junk, sizeof junk);
-            if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK)) { close_fan(w); continue; }
-          }
-          if (evs[i].events & EPOLLOUT) flush_fan(w);
-          continue;
-        }
         auto it = conns_.find(fd);
         if (it == conns_.end()) continue;
         Conn* c = it->second.get();
@@ -793,6 +1108,8 @@ class Server {
         }
         if (evs[i].events & EPOLLOUT) flush(c);
       }
+      // this pass's committed events and new watches go to the fan-out thread in one batch
+      fan_.commit();
       if (progress_pending_) {
         KPROF_BEGIN;
         send_progress();
@@ -805,18 +1122,8 @@ class Server {
         dirty_.clear();
         KPROF_END(7);
       }
-      {
-        KPROF_BEGIN;
-        for (FanWatch* w : fan_dirty_) {
-          w->queued = false;
-          flush_fan(w);
-        }
-        fan_dirty_.clear();
-        KPROF_END(8);
-      }
-      expire_fan();
-      reap_fan();
     }
+    fan_.stop();
   }
 
  private:
@@ -900,25 +1207,28 @@ class Server {
     }
   }
 
+  void set_pollout(Conn* c, bool on) {
+    if (c->pollout == on) return;
+    c->pollout = on;
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP | (on ? EPOLLOUT : 0);
+    e.data.fd = c->fd;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
+  }
+
   void flush(Conn* c) {
     while (!c->out.empty()) {
       ssize_t n = write(c->fd, c->out.data(), c->out.size());
       if (n > 0) { c->out.erase(0, (size_t)n); continue; }
       if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        epoll_event e{};
-        e.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
-        e.data.fd = c->fd;
-        epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
+        set_pollout(c, true);
         c->want_write = false;
         return;
       }
       break;
     }
     c->want_write = false;
-    epoll_event e{};
-    e.events = EPOLLIN | EPOLLRDHUP;
-    e.data.fd = c->fd;
-    epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
+    set_pollout(c, false);
   }
 
   void send_progress() {
@@ -971,11 +1281,7 @@ class Server {
             dispatch(evs);
             KPROF_END(5);
           }
-          {
-            KPROF_BEGIN;
-            fan_dispatch(evs);
-            KPROF_END(6);
-          }
+          fan_.post(std::move(evs));
         } else {
           w.put<uint16_t>((uint16_t)failed);
           const KV* kv = eng_->get(cmps[failed].key);
@@ -1065,15 +1371,6 @@ class Server {
     std::string buf;
     int client = -1;
   };
-
-  int next_timeout_ms() {
-    double soonest = 0;
-    for (auto& kv : fan_)
-      if (kv.second->deadline > 0 && (soonest == 0 || kv.second->deadline < soonest)) soonest = kv.second->deadline;
-    if (soonest == 0) return 1000;
-    double ms = (soonest - mono_now()) * 1000.0;
-    return ms < 0 ? 0 : (ms > 1000 ? 1000 : (int)ms + 1);
-  }
 
   void accept_handoffs(int lfd) {
     for (;;) {
@@ -1167,10 +1464,9 @@ class Server {
     w->out = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n"
              "Cache-Control: no-cache, private\r\n\r\n";
     if (send_initial) {
-      eng_->for_prefix(w->prefix, [&](const std::string&, const KV& kv) {
-        const Index& ix = index_of(kv);
-        if (w->matches(ix)) chunk(&w->out, "ADDED", kv.value, ix.body);
-      });
+      // the snapshot is taken here, in commit order; the fan-out thread parses and formats it
+      w->send_initial = true;
+      eng_->for_prefix(w->prefix, [&](const std::string&, const std::shared_ptr<KV>& kv) { w->initial.push_back(kv); });
     } else if (from > 0) {
       std::vector<const Event*> evs;
       if (!eng_->since(from, w->prefix, &evs)) {
@@ -1184,165 +1480,17 @@ class Server {
         w->out.append(hex, (size_t)hl).append(b).append("\r\n0\r\n\r\n");
         w->dead = true;   // close once written
       } else {
-        for (const Event* e : evs) fan_one(w.get(), *e);
+        w->replay.reserve(evs.size());
+        for (const Event* e : evs) w->replay.push_back(*e);
       }
       w->min_rev = from;
     }
-    FanWatch* raw = w.get();
-    epoll_event e{};
-    e.events = EPOLLIN | EPOLLRDHUP;
-    e.data.fd = client;
-    epoll_ctl(ep_, EPOLL_CTL_ADD, client, &e);
-    if (raw->node_indexed) fan_by_node_[raw->node_key].push_back(raw);
-    else fan_other_.push_back(raw);
-    fan_[client] = std::move(w);
-    flush_fan(raw);
-  }
-
-  // one event into one watch (cacher.go dispatch rules: a MODIFIED object that stops matching is
-  // a DELETED for that watcher, one that starts matching an ADDED)
-  void fan_one(FanWatch* w, const Event& ev, const Index* cur = nullptr, const Index* prv = nullptr) {
-    if (ev.key.compare(0, w->prefix.size(), w->prefix) != 0 || ev.rev <= w->min_rev) return;
-    if (!cur) cur = &index_of(*ev.kv);
-    if (!prv) prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
-    bool now = w->matches(*cur);
-    bool was = ev.prev && w->matches(*prv);
-    const std::string& v = ev.kv->value;
-    if (ev.type == 0) {
-      if (now && was) chunk(&w->out, "MODIFIED", v, cur->body);
-      else if (now) chunk(&w->out, "ADDED", v, cur->body);
-      else if (was) chunk(&w->out, "DELETED", v, cur->body);
-      else return;
-    } else {
-      if (!(now || was) || !cur->ok) return;
-      chunk(&w->out, "DELETED", v, cur->body);
-    }
-    mark_fan(w);
-  }
-
-  // Per event: the unindexed watches, plus the watches of the node the object is on now and
-  // was on before (O(matching watchers), not O(all watchers), with one watch per kubelet).
-  void fan_dispatch(const std::vector<Event>& evs) {
-    if (fan_.empty()) return;
-    for (const Event& ev : evs) {
-      const Index* cur = nullptr;
-      const Index* prv = nullptr;
-      auto parse = [&]() {
-        if (cur) return;
-        cur = &index_of(*ev.kv);
-        prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
-      };
-      for (FanWatch* w : fan_other_) {
-        if (w->dead || ev.key.compare(0, w->prefix.size(), w->prefix) != 0) continue;
-        parse();
-        fan_one(w, ev, cur, prv);
-      }
-      if (fan_by_node_.empty()) continue;
-      parse();
-      auto node_of = [](const Index& ix) -> std::string {
-        const std::string_view* it = sv_find(ix.fields, "spec.nodeName");
-        return it ? std::string(it->data(), it->size()) : std::string();
-      };
-      std::string a = node_of(*cur);
-      auto bucket = [&](const std::string& n) {
-        auto it = fan_by_node_.find(n);
-        if (it == fan_by_node_.end()) return;
-        for (FanWatch* w : it->second)
-          if (!w->dead) fan_one(w, ev, cur, prv);
-      };
-      bucket(a);
-      if (ev.prev) {
-        std::string b = node_of(*prv);
-        if (b != a) bucket(b);
-      }
-    }
-    // a superseded value's parse is not needed again (resumed watches re-parse on demand):
-    // the cache lives on current values only, so history memory does not grow with it
-    for (const Event& ev : evs) {
-      if (ev.prev) ev.prev->aux.reset();
-      if (ev.type == 1) ev.kv->aux.reset();   // a tombstone is never a current value
-    }
-  }
-
-  void mark_fan(FanWatch* w) {
-    if (!w->out.empty() && !w->queued) {
-      w->queued = true;
-      fan_dirty_.push_back(w);
-    }
-  }
-
-  void flush_fan(FanWatch* w) {
-    while (!w->out.empty()) {
-      ssize_t n = write(w->fd, w->out.data(), w->out.size());
-      if (g_prof.on) ++g_prof.n[11];   // "other": count of fan-out write() calls
-      if (n > 0) { w->out.erase(0, (size_t)n); continue; }
-      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        if (w->out.size() > (64u << 20)) { w->dead = true; w->out.clear(); return; }   // slow watcher
-        epoll_event e{};
-        e.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
-        e.data.fd = w->fd;
-        epoll_ctl(ep_, EPOLL_CTL_MOD, w->fd, &e);
-        return;
-      }
-      w->dead = true;
-      w->out.clear();
-      return;
-    }
-    epoll_event e{};
-    e.events = EPOLLIN | EPOLLRDHUP;
-    e.data.fd = w->fd;
-    epoll_ctl(ep_, EPOLL_CTL_MOD, w->fd, &e);
-  }
-
-  void expire_fan() {
-    double now = 0;
-    for (auto& kv : fan_) {
-      FanWatch* w = kv.second.get();
-      if (w->deadline <= 0 || w->dead) continue;
-      if (now == 0) now = mono_now();
-      if (now >= w->deadline) {
-        w->out.append("0\r\n\r\n");   // end of the chunked body: the watch timed out normally
-        w->dead = true;
-        flush_fan(w);
-      }
-    }
-  }
-
-  void close_fan(FanWatch* w) {
-    w->dead = true;
-    w->out.clear();
-  }
-
-  void reap_fan() {
-    for (auto it = fan_.begin(); it != fan_.end();) {
-      FanWatch* w = it->second.get();
-      if (w->dead && w->out.empty()) {
-        fan_dirty_.erase(std::remove(fan_dirty_.begin(), fan_dirty_.end(), w), fan_dirty_.end());
-        auto drop = [w](std::vector<FanWatch*>* v) { v->erase(std::remove(v->begin(), v->end(), w), v->end()); };
-        if (w->node_indexed) {
-          auto b = fan_by_node_.find(w->node_key);
-          if (b != fan_by_node_.end()) {
-            drop(&b->second);
-            if (b->second.empty()) fan_by_node_.erase(b);
-          }
-        } else {
-          drop(&fan_other_);
-        }
-        epoll_ctl(ep_, EPOLL_CTL_DEL, w->fd, nullptr);
-        close(w->fd);
-        it = fan_.erase(it);
-      } else {
-        ++it;
-      }
-    }
+    fan_.post(std::move(w));
   }
 
   std::unordered_map<int, int> handoff_listeners_;
   std::unordered_map<int, Handoff> handoffs_;
-  std::map<int, std::unique_ptr<FanWatch>> fan_;
-  std::vector<FanWatch*> fan_dirty_;
-  std::vector<FanWatch*> fan_other_;
-  std::unordered_map<std::string, std::vector<FanWatch*>> fan_by_node_;
+  FanOut fan_;
 
   Engine* eng_;
   int ep_ = -1;

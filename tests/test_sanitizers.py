@@ -67,6 +67,22 @@ def test_shared_store_server_asan(san_build, tmp_path):
         assert _clean(text), f"{f.name}:\n{text[-4000:]}"
 
 
+def test_shared_store_server_tsan(san_build, tmp_path):
+    """kamd-etcd runs two threads (store + watch fan-out, sharing the event queue and the KV
+    objects' lifetimes and parse cache): the multi-worker API server suite against its TSan build."""
+    logs = tmp_path / "etcd-logs"
+    env = dict(os.environ, KAMD_ETCD_BIN=os.path.join(san_build, "tsan", "kamd-etcd"), KAMD_ETCD_LOG_DIR=str(logs),
+               TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        "tests/test_apiserver_shared.py"], cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    files = list(logs.iterdir())
+    assert files, "the sanitized server never ran"
+    for f in files:
+        text = f.read_text(errors="replace")
+        assert _clean(text), f"{f.name}:\n{text[-4000:]}"
+
+
 def test_asyncio_debug_mode_devicemanager_and_scheduler():
     """asyncio debug mode over the device-manager / scheduler suites: a coroutine that is
     never awaited or a loop-thread violation is an error, not a silent warning."""
