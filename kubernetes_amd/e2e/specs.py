@@ -349,3 +349,256 @@ async def gc_cascade(f):
         pods = (await f.client.list("pods", f.ns, label_selector="app=gcrs"))["items"]
         return True if not pods else None
     await f.wait(collected, 60, "dependents collected")
+
+
+# -- more of test/e2e/common, apps, apimachinery, network (round 2) ---------------------------
+
+def _vol_cat(mount, var, path):
+    # container runtimes mount the volume at `mount`; the process runtime has no mount namespace
+    # and exposes the host path in KUBERNETES_VOLUME_<NAME>
+    return f"cat {mount}/{path} 2>/dev/null || cat ${var}/{path}"
+
+
+@conformance("Secrets should be consumable from pods in volume")
+async def secret_volume(f):
+    await f.client.create("secrets", {"metadata": {"name": "sv"}, "data": {"data-1": base64.b64encode(b"value-1").decode()}}, f.ns)
+    p = _pod("secvol", _vol_cat("/etc/secret", "KUBERNETES_VOLUME_S", "data-1"))
+    p["spec"]["containers"][0]["volumeMounts"] = [{"name": "s", "mountPath": "/etc/secret", "readOnly": True}]
+    p["spec"]["volumes"] = [{"name": "s", "secret": {"secretName": "sv"}}]
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("secvol", ("Succeeded",))
+    assert "value-1" in await f.logs("secvol")
+
+
+@conformance("Projected should combine a configMap, a secret and the downward API in one volume")
+async def projected_volume(f):
+    await f.client.create("configmaps", {"metadata": {"name": "pcm"}, "data": {"c": "from-cm"}}, f.ns)
+    await f.client.create("secrets", {"metadata": {"name": "psec"}, "data": {"s": base64.b64encode(b"from-secret").decode()}}, f.ns)
+    cat = " && ".join(_vol_cat("/etc/p", "KUBERNETES_VOLUME_P", x) for x in ("c", "s", "podname"))
+    p = _pod("proj", cat)
+    p["spec"]["containers"][0]["volumeMounts"] = [{"name": "p", "mountPath": "/etc/p"}]
+    p["spec"]["volumes"] = [{"name": "p", "projected": {"sources": [
+        {"configMap": {"name": "pcm"}}, {"secret": {"name": "psec"}},
+        {"downwardAPI": {"items": [{"path": "podname", "fieldRef": {"fieldPath": "metadata.name"}}]}}]}}]
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("proj", ("Succeeded",))
+    out = await f.logs("proj")
+    assert "from-cm" in out and "from-secret" in out and "proj" in out, out
+
+
+@conformance("EmptyDir volumes should carry data from an init container to the app container")
+async def emptydir_init(f):
+    w = "echo shared-data > /data/f 2>/dev/null || echo shared-data > $KUBERNETES_VOLUME_D/f"
+    p = _pod("ed", _vol_cat("/data", "KUBERNETES_VOLUME_D", "f"))
+    p["spec"]["initContainers"] = [{"name": "w", "image": BUSYBOX, "command": ["sh", "-c", w],
+                                    "volumeMounts": [{"name": "d", "mountPath": "/data"}]}]
+    p["spec"]["containers"][0]["volumeMounts"] = [{"name": "d", "mountPath": "/data"}]
+    p["spec"]["volumes"] = [{"name": "d", "emptyDir": {}}]
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("ed", ("Succeeded",))
+    assert "shared-data" in await f.logs("ed")
+
+
+@conformance("Container lifecycle hook should execute a postStart exec hook")
+async def poststart_hook(f):
+    mark = "echo hooked > /data/h 2>/dev/null || echo hooked > $KUBERNETES_VOLUME_D/h"
+    wait = ("for i in $(seq 1 100); do (cat /data/h 2>/dev/null || cat $KUBERNETES_VOLUME_D/h 2>/dev/null) && exit 0; "
+            "sleep 0.1; done; exit 1")
+    p = _pod("hook", wait)
+    c = p["spec"]["containers"][0]
+    c["volumeMounts"] = [{"name": "d", "mountPath": "/data"}]
+    c["lifecycle"] = {"postStart": {"exec": {"command": ["sh", "-c", mark]}}}
+    p["spec"]["volumes"] = [{"name": "d", "emptyDir": {}}]
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("hook", ("Succeeded",))
+    assert "hooked" in await f.logs("hook")
+
+
+@conformance("Job should fail once its pods exceed backoffLimit")
+async def job_backoff_limit(f):
+    job = {"metadata": {"name": "failing"}, "spec": {"backoffLimit": 1, "template": {"spec": {
+        "restartPolicy": "Never", "containers": [{"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "exit 3"]}]}}}}
+    await f.client.create("jobs", job, f.ns)
+
+    async def failed():
+        j = await f.client.get("jobs", "failing", f.ns)
+        conds = (j.get("status") or {}).get("conditions") or []
+        return j if any(c["type"] == "Failed" and c["status"] == "True" for c in conds) else None
+    j = await f.wait(failed, 60, "job Failed condition")
+    reason = [c for c in j["status"]["conditions"] if c["type"] == "Failed"][0].get("reason")
+    assert reason == "BackoffLimitExceeded", reason
+
+
+@conformance("Eviction API should honour a PodDisruptionBudget")
+async def eviction_pdb(f):
+    for i in range(2):
+        p = _pod(f"pdb{i}", "sleep 3600", restart="Always")
+        p["metadata"]["labels"] = {"app": "pdb"}
+        await f.client.create("pods", p, f.ns)
+    for i in range(2):
+        await f.pod_phase(f"pdb{i}", ("Running",))
+    await f.client.create("poddisruptionbudgets", {"metadata": {"name": "b"}, "spec": {
+        "minAvailable": 2, "selector": {"matchLabels": {"app": "pdb"}}}}, f.ns)
+
+    async def computed():
+        b = await f.client.get("poddisruptionbudgets", "b", f.ns)
+        st = b.get("status") or {}
+        return b if st.get("expectedPods") == 2 or st.get("currentHealthy") == 2 else None
+    await f.wait(computed, 30, "PDB status")
+    try:
+        await f.client.evict(f.ns, "pdb0")
+    except Exception as e:  # noqa: BLE001
+        assert "429" in str(e) or "disruption budget" in str(e), e
+    else:
+        raise AssertionError("eviction violating the budget was allowed")
+    await f.client.patch("poddisruptionbudgets", "b", {"spec": {"minAvailable": 1}}, f.ns)
+
+    async def allowed():
+        b = await f.client.get("poddisruptionbudgets", "b", f.ns)
+        return b if (b.get("status") or {}).get("disruptionsAllowed", 0) >= 1 else None
+    await f.wait(allowed, 30, "disruptionsAllowed >= 1")
+    await f.client.evict(f.ns, "pdb0")
+
+    async def gone():
+        pods = (await f.client.list("pods", f.ns, label_selector="app=pdb"))["items"]
+        return True if all(p["metadata"]["name"] != "pdb0" or p["metadata"].get("deletionTimestamp") for p in pods) else None
+    await f.wait(gone, 30, "evicted pod deleted")
+
+
+@conformance("LimitRange should default container requests and limits")
+async def limit_range_defaults(f):
+    await f.client.create("limitranges", {"metadata": {"name": "lr"}, "spec": {"limits": [{
+        "type": "Container", "default": {"cpu": "300m", "memory": "200Mi"},
+        "defaultRequest": {"cpu": "100m", "memory": "100Mi"}}]}}, f.ns)
+    created = await f.client.create("pods", _pod("lrpod", "true"), f.ns)
+    res = created["spec"]["containers"][0].get("resources") or {}
+    assert res.get("requests", {}).get("cpu") == "100m" and res.get("limits", {}).get("memory") == "200Mi", res
+
+
+@conformance("CustomResourceDefinition should serve CRUD of custom resources")
+async def crd_crud(f):
+    crd = {"apiVersion": "apiextensions.k8s.io/v1beta1", "kind": "CustomResourceDefinition",
+           "metadata": {"name": f"gpujobs{f.ns.replace('-', '')}.e2e.amd.com"},
+           "spec": {"group": "e2e.amd.com", "version": "v1", "scope": "Namespaced",
+                    "names": {"plural": f"gpujobs{f.ns.replace('-', '')}", "kind": "GpuJob"}}}
+    await f.client.create("customresourcedefinitions", crd)
+    plural = crd["spec"]["names"]["plural"]
+    base = f"/apis/e2e.amd.com/v1/namespaces/{f.ns}/{plural}"
+
+    do = f.client._do
+
+    async def served():
+        try:
+            await do("GET", base)
+            return True
+        except Exception:  # noqa: BLE001
+            return None
+    try:
+        await f.wait(served, 30, "CRD served")
+        obj = {"apiVersion": "e2e.amd.com/v1", "kind": "GpuJob", "metadata": {"name": "j1"}, "spec": {"gpus": 4}}
+        await do("POST", base, obj)
+        got = await do("GET", base + "/j1")
+        assert got["spec"]["gpus"] == 4
+        items = (await do("GET", base))["items"]
+        assert [i["metadata"]["name"] for i in items] == ["j1"]
+        await do("DELETE", base + "/j1")
+    finally:
+        await f.client.delete("customresourcedefinitions", crd["metadata"]["name"])
+
+
+@conformance("Watchers should observe add, update and delete notifications on configmaps")
+async def watch_configmaps(f):
+    import asyncio
+    seen = []
+    w = await f.client.watch("configmaps", f.ns, label_selector="watch=e2e")
+
+    async def consume():
+        async for typ, obj in w:
+            seen.append((typ, obj["metadata"]["name"], (obj.get("data") or {}).get("k")))
+            if typ == "DELETED":
+                return
+    t = asyncio.ensure_future(consume())
+    try:
+        cm = {"metadata": {"name": "wcm", "labels": {"watch": "e2e"}}, "data": {"k": "1"}}
+        await f.client.create("configmaps", cm, f.ns)
+        await f.client.patch("configmaps", "wcm", {"data": {"k": "2"}}, f.ns)
+        await f.client.delete("configmaps", "wcm", f.ns)
+        await asyncio.wait_for(t, 20)
+    finally:
+        w.close()
+        t.cancel()
+    assert [s[0] for s in seen] == ["ADDED", "MODIFIED", "DELETED"] and seen[1][2] == "2", seen
+
+
+@conformance("Services of type NodePort should get a node port in the service node-port range")
+async def service_nodeport(f):
+    svc = {"metadata": {"name": "np"}, "spec": {"type": "NodePort", "selector": {"app": "np"},
+                                                 "ports": [{"port": 80, "targetPort": 8080}]}}
+    s = await f.client.create("services", svc, f.ns)
+    port = s["spec"]["ports"][0].get("nodePort")
+    assert s["spec"].get("clusterIP") and port and 30000 <= int(port) <= 32767, s["spec"]
+    # a second service cannot take the same explicit node port
+    dup = {"metadata": {"name": "np2"}, "spec": {"type": "NodePort", "ports": [{"port": 80, "nodePort": port}]}}
+    try:
+        await f.client.create("services", dup, f.ns)
+    except Exception as e:  # noqa: BLE001
+        assert "422" in str(e) or "allocated" in str(e) or "Invalid" in str(e), e
+    else:
+        raise AssertionError("a node port was allocated twice")
+
+
+@conformance("ReplicationController should scale up and down")
+async def rc_scale(f):
+    rc = {"metadata": {"name": "rc"}, "spec": {"replicas": 1, "selector": {"app": "rc"},
+          "template": {"metadata": {"labels": {"app": "rc"}}, "spec": {"containers": [
+              {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("replicationcontrollers", rc, f.ns)
+
+    def live(pods):
+        return [p for p in pods if not p["metadata"].get("deletionTimestamp")]
+
+    for want in (3, 1):
+        await f.client.patch("replicationcontrollers", "rc", {"spec": {"replicas": want}}, f.ns)
+
+        async def settled(want=want):
+            pods = live((await f.client.list("pods", f.ns, label_selector="app=rc"))["items"])
+            return pods if len(pods) == want else None
+        await f.wait(settled, 60, f"{want} replicas")
+
+
+@conformance("Namespace deletion should remove the namespace's services")
+async def namespace_services(f):
+    ns = f.ns + "-svc"
+    await f.client.create("namespaces", {"metadata": {"name": ns}})
+    await f.client.create("services", {"metadata": {"name": "s"}, "spec": {"ports": [{"port": 80}]}}, ns)
+    await f.client.delete("namespaces", ns)
+
+    async def gone():
+        try:
+            await f.client.get("namespaces", ns)
+            return None
+        except Exception:  # noqa: BLE001
+            return True
+    await f.wait(gone, 60, "namespace finalized")
+    items = (await f.client.list("services", ns))["items"]
+    assert not items, items
+
+
+@conformance("Pods should be deleted gracefully, running the preStop hook")
+async def graceful_delete(f):
+    p = _pod("grace", "trap 'exit 0' TERM; while true; do sleep 0.1; done", restart="Always")
+    p["spec"]["terminationGracePeriodSeconds"] = 5
+    p["spec"]["containers"][0]["lifecycle"] = {"preStop": {"exec": {"command": ["sh", "-c", "true"]}}}
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("grace", ("Running",))
+    await f.client.delete("pods", "grace", f.ns)
+    mid = await f.client.get("pods", "grace", f.ns)
+    assert mid["metadata"].get("deletionTimestamp") and mid["metadata"].get("deletionGracePeriodSeconds") == 5
+
+    async def gone():
+        try:
+            await f.client.get("pods", "grace", f.ns)
+            return None
+        except Exception:  # noqa: BLE001
+            return True
+    await f.wait(gone, 30, "pod removed after graceful termination")
