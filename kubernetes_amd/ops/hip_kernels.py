@@ -2,6 +2,7 @@
 
   vector_add(a, b)             -> a + b          (GPU e2e workload kernel)
   gemm_bf16_nt(a, b, out_fp32) -> a @ b.T        (MFMA 16x16x32 bf16, LDS-tiled)
+  gemm_fp8_nt(a, b, out_fp32)  -> a @ b.T        (OCP fp8 e4m3, block-scaled MFMA 16x16x128)
   diag_mfma / diag_hbm / diag_vector_add         (device-plugin burn-in diagnostics)
   Payload(dev)                                    (warm per-GPU payload for GPU pods)
 
@@ -37,6 +38,7 @@ def load():
         L.kamd_hip_last_error.restype = ctypes.c_char_p
         L.kamd_vector_add_launch.argtypes = [vp, vp, vp, i, vp]
         L.kamd_gemm_bf16_nt_launch.argtypes = [vp, vp, vp, i, i, i, i, f, i, vp]
+        L.kamd_gemm_fp8_nt_launch.argtypes = [vp, vp, vp, i, i, i, i, f, i, vp]
         L.kamd_hbm_copy_launch.argtypes = [vp, vp, sz, vp]
         L.kamd_diag_vector_add.argtypes = [i, i, ctypes.POINTER(ctypes.c_float)]
         L.kamd_diag_mfma.argtypes = [i, i, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
@@ -94,6 +96,24 @@ def gemm_bf16_nt(a, b, out_fp32=True, alpha=1.0):
     out = torch.empty((M, N), device=a.device, dtype=torch.float32 if out_fp32 else torch.bfloat16)
     _raise(load().kamd_gemm_bf16_nt_launch(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, N, float(alpha),
                                            1 if out_fp32 else 0, _stream(a)), "gemm_bf16_nt")
+    return out
+
+
+def gemm_fp8_nt(a, b, out_fp32=True, alpha=1.0):
+    """C = alpha * a @ b.T with a: [M, K], b: [N, K] OCP fp8 e4m3 (torch.float8_e4m3fn), fp32
+    accumulate, on the block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, unit scales).
+    M, N must be multiples of 256 and K of 128."""
+    import torch
+    assert a.is_cuda and b.is_cuda and a.dtype == torch.float8_e4m3fn and b.dtype == torch.float8_e4m3fn
+    assert a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1], (a.shape, b.shape)
+    a, b = a.contiguous(), b.contiguous()
+    M, K = a.shape
+    N = b.shape[0]
+    if M % 256 or N % 256 or K % 128:
+        raise ValueError(f"gemm_fp8_nt needs M, N % 256 == 0 and K % 128 == 0, got {M}x{N}x{K}")
+    out = torch.empty((M, N), device=a.device, dtype=torch.float32 if out_fp32 else torch.bfloat16)
+    _raise(load().kamd_gemm_fp8_nt_launch(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, N, float(alpha),
+                                          1 if out_fp32 else 0, _stream(a)), "gemm_fp8_nt")
     return out
 
 

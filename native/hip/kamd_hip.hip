@@ -13,6 +13,7 @@
 // Everything is exported through a C ABI (extern "C") so the Python side binds with ctypes
 // and passes torch tensor pointers + the current HIP stream.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -22,6 +23,8 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 static thread_local char g_err[256];
 static int g_gemm_path = 0;   // 0 auto (ping-pong 256-tile kernel when the shape allows), 1 force the 128-tile
@@ -510,11 +513,23 @@ constexpr int EPI_STRIDE = 68;                    // fp32 row pitch of the LDS e
 constexpr int EPI_BYTES = 8 * 64 * EPI_STRIDE * 4;  // 8 waves x 64 x 68 fp32 = 136 KiB
 
 // VARIANT bit 0: static priority for the second half instead of per-segment setprio flips;
-// bit 1: LDS-staged 16-B epilogue
-template <typename OutT, int VARIANT>
+// bit 1: LDS-staged 16-B epilogue.
+// FP8: OCP e4m3 operands on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (scales fixed at
+// 2^0). A K-tile is still 128 B per row — 64 bf16 or 128 fp8 elements — so staging, LDS layout,
+// swizzle and fragment reads are byte-for-byte the bf16 kernel's; the two 16-B fragments a lane
+// reads for the bf16 k-steps 0 and 1 become the two halves of its 32-B fp8 operand (A and B use
+// the same byte->slot map, so every product still pairs A[i][k] with B[j][k]). One fp8 MFMA
+// takes the cycles of two bf16 ones at 4x the K: 2x the FLOPs per K-tile on the same traffic.
+template <typename OutT, int VARIANT, bool FP8 = false>
 __global__ void __launch_bounds__(THREADS, 1)
-gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, OutT* __restrict__ C,
+gemm_bf16_nt_pp_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, OutT* __restrict__ C,
                        int M, int N, int K, int ldc, float alpha) {
+  // element type of the operands: addresses below are in elements, as in the bf16 original
+  typedef typename std::conditional<FP8, unsigned char, u16>::type elem_t;
+  constexpr int EPC = 16 / sizeof(elem_t);           // elements per 16-B chunk (8 bf16, 16 fp8)
+  constexpr int BKE = 128 / sizeof(elem_t);          // elements per 128-B K-tile row
+  const elem_t* A = static_cast<const elem_t*>(Av);
+  const elem_t* B = static_cast<const elem_t*>(Bv);
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -542,14 +557,14 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
   for (int j = 0; j < 2; ++j) {
     const int q = j * THREADS + tid, r = q >> 3, slot = q & 7;
     const int kc = slot ^ ((r >> 1) & 7);
-    offA[j] = (size_t)((r >> 6) * 128 + (r & 63)) * K + (kc << 3);
-    offB[j] = (size_t)((r >> 5) * 64 + (r & 31)) * K + (kc << 3);
+    offA[j] = (size_t)((r >> 6) * 128 + (r & 63)) * K + kc * EPC;
+    offB[j] = (size_t)((r >> 5) * 64 + (r & 31)) * K + kc * EPC;
   }
-  const u16* half_src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 64) * K, B + (size_t)n0 * K,
-                            B + (size_t)(n0 + 32) * K};
+  const elem_t* half_src[4] = {A + (size_t)m0 * K, A + (size_t)(m0 + 64) * K, B + (size_t)n0 * K,
+                               B + (size_t)(n0 + 32) * K};
   auto stage = [&](int kt, const int par, int h) {
     unsigned char* dst = lds + (par * 4 + h) * HALF_BYTES + wid * 1024;
-    const u16* src = half_src[h] + (size_t)kt * BK;
+    const elem_t* src = half_src[h] + (size_t)kt * BKE;
     const size_t* off = h < 2 ? offA : offB;
     __builtin_amdgcn_global_load_lds((const void*)(src + off[0]), (lds_void*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(src + off[1]), (lds_void*)(dst + THREADS * 16), 16, 0, 0);
@@ -567,35 +582,73 @@ gemm_bf16_nt_pp_kernel(const u16* __restrict__ A, const u16* __restrict__ B, Out
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[2][2][4], bfr[2][2][2];
+  // fp8: the two 16-B reads land directly in the low / high half of one 8-VGPR operand (no copies)
+  i32x8 af8[2][4], bf8[2][2];
   auto read_a = [&](const int par, int mq) {   // half h = mq, local rows wr*64 + ...
     const unsigned char* base = lds + (par * 4 + mq) * HALF_BYTES + (wr * 64 + frow) * 128;
+    if constexpr (FP8) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int i = 0; i < 4; ++i) {
+        const unsigned char* p = base + i * 16 * 128;
+        af8[mq][i] = __builtin_shufflevector(*reinterpret_cast<const i32x4*>(p + ((fq ^ lsw) << 4)),
+                                             *reinterpret_cast<const i32x4*>(p + (((4 + fq) ^ lsw) << 4)),
+                                             0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[mq][ks][i] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[mq][ks][i] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+    }
   };
   auto read_b = [&](const int par, int nq) {   // half h = 2 + nq, local rows wc*32 + ...
     const unsigned char* base = lds + (par * 4 + 2 + nq) * HALF_BYTES + (wc * 32 + frow) * 128;
+    if constexpr (FP8) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int j = 0; j < 2; ++j) {
+        const unsigned char* p = base + j * 16 * 128;
+        bf8[nq][j] = __builtin_shufflevector(*reinterpret_cast<const i32x4*>(p + ((fq ^ lsw) << 4)),
+                                             *reinterpret_cast<const i32x4*>(p + (((4 + fq) ^ lsw) << 4)),
+                                             0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[nq][ks][j] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[nq][ks][j] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + (((ks * 4 + fq) ^ lsw) << 4));
+    }
   };
   auto mma = [&](int mq, int nq) {
     if (!(VARIANT & 1)) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    if constexpr (FP8) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mq][ks][i], bfr[nq][ks][j], acc[mq][nq][i][j], 0, 0, 0);
+          // formats A = B = 0 (fp8 e4m3), E8M0 scales 127 = 2^0
+          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af8[mq][i], bf8[nq][j], acc[mq][nq][i][j],
+                                                                                0, 0, 0, 127, 0, 127);
+      // pin the MFMAs to this phase: without a use here the compiler sinks these pure ops past
+      // the barriers (it does for the scaled fp8 form) and the ping-pong collapses
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[mq][nq][i][j]));
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mq][ks][i], bfr[nq][ks][j], acc[mq][nq][i][j], 0, 0, 0);
+    }
     if (!(VARIANT & 1)) __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nt = K / BK;
+  const int nt = K / BKE;
   // TUNED: static priority for the second-dispatched half (MI355X_MICROARCH "Two waves per
   // SIMD" item 4) instead of per-segment flips
   if ((VARIANT & 1) && wr == 1) __builtin_amdgcn_s_setprio(1);
@@ -788,6 +841,37 @@ int kamd_vector_add_launch(const float* a, const float* b, float* c, int n, hipS
   return check(hipGetLastError(), "vector_add launch");
 }
 
+// fp8 (OCP e4m3) GEMM C = alpha * A @ B^T on the ping-pong kernel: A M x K, B N x K row-major
+// bytes; M, N multiples of 256, K a multiple of 128 (no other tile path exists for fp8).
+int kamd_gemm_fp8_nt_launch(const void* A, const void* B, void* C, int M, int N, int K, int ldc, float alpha,
+                            int out_fp32, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (M % gemmpp::BM || N % gemmpp::BN || K % 128) {
+    snprintf(g_err, sizeof g_err, "gemm_fp8_nt: need M, N %% 256 == 0 and K %% 128 == 0 (got %d x %d x %d)", M, N, K);
+    return -1;
+  }
+  if ((((uintptr_t)A) | ((uintptr_t)B)) & 15) {
+    snprintf(g_err, sizeof g_err, "gemm_fp8_nt: A/B must be 16-byte aligned");
+    return -1;
+  }
+  const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
+  static bool attr = false;
+  if (!attr) {
+    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float, 0, true>,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
+    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16, 0, true>,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
+    attr = true;
+  }
+  if (out_fp32)
+    hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
+                       gemmpp::LDS_BYTES, stream, A, B, (float*)C, M, N, K, ldc, alpha);
+  else
+    hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
+                       gemmpp::LDS_BYTES, stream, A, B, (__bf16*)C, M, N, K, ldc, alpha);
+  return check(hipGetLastError(), "gemm fp8 launch");
+}
+
 int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N, int K, int ldc, float alpha,
                              int out_fp32, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
@@ -813,7 +897,7 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
       attr = true;                                                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<T, V>), dim3(tiles), dim3(gemmpp::THREADS), lds, stream, \
-                       (const u16*)A, (const u16*)B, (T*)C, M, N, K, ldc, alpha);                              \
+                       A, B, (T*)C, M, N, K, ldc, alpha);                                                      \
   } while (0)
     if (out_fp32) {
       switch (variant) {

@@ -117,3 +117,39 @@ def test_payload_batch(hk):
         assert all(p.run() for _ in range(3))
     finally:
         p.close()
+
+
+def _fp8_operands(M, N, K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    a = (torch.rand(M, K, device="cuda", generator=g) * 4 - 2).to(torch.float8_e4m3fn)
+    b = (torch.rand(N, K, device="cuda", generator=g) * 4 - 2).to(torch.float8_e4m3fn)
+    return a, b
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (256, 256, 256), (512, 768, 384), (1024, 512, 2048),
+                                   (768, 256, 640)])
+def test_gemm_fp8_matches_fp32_reference(hk, M, N, K):
+    """fp8 e4m3 x fp8 e4m3 products are exact in fp32, so the only difference from the fp32
+    reference of the same (dequantized) operands is the summation order."""
+    a, b = _fp8_operands(M, N, K)
+    ref = a.float() @ b.float().T
+    out = hk.gemm_fp8_nt(a, b)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-3 * (K ** 0.5))
+    out16 = hk.gemm_fp8_nt(a, b, out_fp32=False)
+    assert out16.dtype == torch.bfloat16
+    torch.testing.assert_close(out16.float(), ref, rtol=1e-2, atol=1e-2 * (K ** 0.5))
+
+
+def test_gemm_fp8_identity_asymmetric(hk):
+    """A = I with an asymmetric B catches a row/col swap and any A/B k-slot mispairing."""
+    n = 256
+    eye = torch.eye(n, device="cuda").to(torch.float8_e4m3fn)
+    b = (torch.arange(n * n, device="cuda").reshape(n, n) % 7 - 3).float().to(torch.float8_e4m3fn)
+    torch.testing.assert_close(hk.gemm_fp8_nt(eye, b), b.float().T, rtol=0, atol=0)
+    torch.testing.assert_close(hk.gemm_fp8_nt(b, eye), b.float(), rtol=0, atol=0)
+
+
+def test_gemm_fp8_rejects_untiled_shapes(hk):
+    a, b = _fp8_operands(256, 256, 128)
+    with pytest.raises(ValueError):
+        hk.gemm_fp8_nt(a[:, :64].contiguous(), b[:, :64].contiguous())
