@@ -26,6 +26,8 @@ def main(argv=None):
                     help="gate every GPU on the HIP acceptance test (vector_add, MFMA GEMM, HBM copy) before offering it")
     ap.add_argument("--burn-in-min-tflops", type=float, default=700.0)
     ap.add_argument("--burn-in-min-hbm-gbps", type=float, default=3000.0)
+    ap.add_argument("--burn-in-min-fp8-tflops", type=float, default=1400.0,
+                    help="fp8 (e4m3, block-scaled MFMA) GEMM floor; 0 skips the fp8 step")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -36,7 +38,8 @@ def main(argv=None):
         burn_in = None
         if a.burn_in:
             from ..deviceplugin.burnin import BurnIn
-            burn_in = BurnIn(min_tflops=a.burn_in_min_tflops, min_hbm_gbps=a.burn_in_min_hbm_gbps)
+            burn_in = BurnIn(min_tflops=a.burn_in_min_tflops, min_hbm_gbps=a.burn_in_min_hbm_gbps,
+                             min_fp8_tflops=a.burn_in_min_fp8_tflops, fp8=a.burn_in_min_fp8_tflops > 0)
         p = AMDGPUPlugin(a.plugins_dir, smi=smi, socket_name=a.socket_name, health_interval=a.health_interval,
                          rocm_mount=a.rocm_mount, burn_in=burn_in)
         await p.start()

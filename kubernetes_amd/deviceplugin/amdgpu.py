@@ -35,6 +35,7 @@ from .server import DevicePluginServer, device
 ATTR_BURN_IN = "amd.com/burn-in"          # pending / passed / failed
 ATTR_MFMA_TFLOPS = "amd.com/mfma-tflops"  # measured bf16 MFMA GEMM throughput
 ATTR_HBM_GBPS = "amd.com/hbm-gbps"        # measured HBM copy bandwidth
+ATTR_MFMA_FP8_TFLOPS = "amd.com/mfma-fp8-tflops"   # measured fp8 (e4m3, block-scaled MFMA) GEMM throughput
 
 log = logging.getLogger("amdgpu-plugin")
 
@@ -116,6 +117,8 @@ class AMDGPUPlugin(DevicePluginServer):
             if r is not None and r.tflops:
                 attrs[ATTR_MFMA_TFLOPS] = str(int(r.tflops))
                 attrs[ATTR_HBM_GBPS] = str(int(r.hbm_gbps))
+                if r.fp8_tflops:
+                    attrs[ATTR_MFMA_FP8_TFLOPS] = str(int(r.fp8_tflops))
         return device(g.device_id_str, health, attrs)
 
     def _check(self, g: amdsmi.GPU, m: amdsmi.Metrics) -> str:
@@ -159,8 +162,8 @@ class AMDGPUPlugin(DevicePluginServer):
             r = await loop.run_in_executor(pool, self.burn_in.run, g.hip_id if g.hip_id >= 0 else g.index)
             self._burn[g.device_id_str] = r
             if r.ok:
-                log.info("burn-in passed on %s: %.0f TFLOP/s MFMA bf16, %.0f GB/s HBM (%.1f s)",
-                         g.device_id_str, r.tflops, r.hbm_gbps, r.seconds)
+                log.info("burn-in passed on %s: %.0f TFLOP/s MFMA bf16, %.0f fp8, %.0f GB/s HBM (%.1f s)",
+                         g.device_id_str, r.tflops, r.fp8_tflops, r.hbm_gbps, r.seconds)
             else:
                 log.error("burn-in FAILED on %s: %s", g.device_id_str, r.reason)
             self.poll_health(force=True)

@@ -42,6 +42,7 @@ def load():
         L.kamd_hbm_copy_launch.argtypes = [vp, vp, sz, vp]
         L.kamd_diag_vector_add.argtypes = [i, i, ctypes.POINTER(ctypes.c_float)]
         L.kamd_diag_mfma.argtypes = [i, i, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.kamd_diag_mfma_fp8.argtypes = [i, i, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.kamd_diag_hbm.argtypes = [i, sz, i, ctypes.POINTER(ctypes.c_double)]
         L.kamd_payload_create.argtypes = [i, i]
         L.kamd_payload_create.restype = vp
@@ -147,6 +148,12 @@ def diag_vector_add(dev=0, n=50000) -> float:
 def diag_mfma(dev=0, size=4096, iters=20):
     tf, err = ctypes.c_double(), ctypes.c_double()
     _raise(load().kamd_diag_mfma(dev, size, iters, ctypes.byref(tf), ctypes.byref(err)), "diag_mfma")
+    return {"tflops": tf.value, "max_rel_err": err.value, "size": size, "iters": iters}
+
+
+def diag_mfma_fp8(dev=0, size=8192, iters=10):
+    tf, err = ctypes.c_double(), ctypes.c_double()
+    _raise(load().kamd_diag_mfma_fp8(dev, size, iters, ctypes.byref(tf), ctypes.byref(err)), "diag_mfma_fp8")
     return {"tflops": tf.value, "max_rel_err": err.value, "size": size, "iters": iters}
 
 

@@ -14,6 +14,7 @@
 // and passes torch tensor pointers + the current HIP stream.
 #include <hip/hip_runtime.h>
 #include <type_traits>
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -814,6 +815,24 @@ __global__ void fill_bf16_kernel(u16* p, size_t n, uint32_t seed, float scale) {
   }
 }
 
+// random OCP e4m3 bytes with exponent field 5..8 (|v| in [0.25, 3.75]): no NaN encodings, and a
+// magnitude range where fp32 accumulation of K products stays far from overflow
+__global__ void fill_fp8_kernel(unsigned char* p, size_t n, uint32_t seed) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = (unsigned char)(((x >> 8) & 0x80) | ((5 + ((x >> 3) & 3)) << 3) | (x & 7));
+  }
+}
+
+static double fp8_e4m3_to_double(unsigned char b) {
+  const int s = b >> 7, e = (b >> 3) & 15, m = b & 7;
+  const double v = e == 0 ? m / 8.0 * ldexp(1.0, -6) : (1.0 + m / 8.0) * ldexp(1.0, e - 7);
+  return s ? -v : v;
+}
+
 // ---------------------------------------------------------------------------
 extern "C" {
 
@@ -1019,6 +1038,63 @@ int kamd_diag_vector_add(int dev, int n, float* max_err) {
   hipFree(db);
   hipFree(dc);
   return 0;
+}
+
+// fp8 MFMA burn-in: the block-scaled fp8 path (v_mfma_scale_f32_16x16x128_f8f6f4), same protocol
+// as kamd_diag_mfma (size must be a multiple of 256).
+int kamd_diag_mfma_fp8(int dev, int size, int iters, double* tflops, double* max_rel_err) {
+  HC(hipSetDevice(dev));
+  const int M = size, N = size, K = size;
+  unsigned char *A = nullptr, *B = nullptr;
+  float* C = nullptr;
+  HC(hipMalloc(&A, (size_t)M * K));
+  HC(hipMalloc(&B, (size_t)N * K));
+  HC(hipMalloc(&C, (size_t)M * N * 4));
+  int rc = -1;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  do {
+    hipLaunchKernelGGL(fill_fp8_kernel, dim3(1024), dim3(256), 0, 0, A, (size_t)M * K, 0x1234u);
+    hipLaunchKernelGGL(fill_fp8_kernel, dim3(1024), dim3(256), 0, 0, B, (size_t)N * K, 0x9876u);
+    if (check(hipGetLastError(), "fill_fp8") != 0) break;
+    if (kamd_gemm_fp8_nt_launch(A, B, C, M, N, K, N, 1.f, 1, 0) != 0) break;   // warm-up
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) break;
+    hipEventRecord(e0, 0);
+    bool ok = true;
+    for (int i = 0; i < iters && ok; ++i) ok = kamd_gemm_fp8_nt_launch(A, B, C, M, N, K, N, 1.f, 1, 0) == 0;
+    if (!ok) break;
+    hipEventRecord(e1, 0);
+    if (check(hipEventSynchronize(e1), "diag_mfma_fp8 sync") != 0) break;
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    *tflops = 2.0 * M * N * (double)K * iters / (ms * 1e-3) / 1e12;
+    std::vector<unsigned char> ha((size_t)M * K), hb((size_t)N * K);
+    std::vector<float> hc((size_t)M * N);
+    if (check(hipMemcpy(ha.data(), A, ha.size(), hipMemcpyDeviceToHost), "copy A") != 0) break;
+    if (check(hipMemcpy(hb.data(), B, hb.size(), hipMemcpyDeviceToHost), "copy B") != 0) break;
+    if (check(hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost), "copy C") != 0) break;
+    double worst = 0;
+    for (int s = 0; s < 256; ++s) {
+      int i = (int)((s * 7919u) % (unsigned)M), j = (int)((s * 104729u + 13u) % (unsigned)N);
+      double ref = 0, mag = 0;
+      for (int k = 0; k < K; ++k) {
+        double pr = fp8_e4m3_to_double(ha[(size_t)i * K + k]) * fp8_e4m3_to_double(hb[(size_t)j * K + k]);
+        ref += pr;
+        mag += pr < 0 ? -pr : pr;
+      }
+      double err = hc[(size_t)i * N + j] - ref;
+      if (err < 0) err = -err;
+      double rel = err / (mag > 1e-30 ? mag : 1.0);
+      if (rel > worst) worst = rel;
+    }
+    *max_rel_err = worst;
+    rc = 0;
+  } while (0);
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipFree(A);
+  hipFree(B);
+  hipFree(C);
+  return rc;
 }
 
 // MFMA burn-in: random bf16 operands, `iters` timed GEMMs of M=N=K=`size`; result checked on

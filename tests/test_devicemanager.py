@@ -196,7 +196,8 @@ def test_burn_in_gates_devices_and_publishes_measurements(tmp_path, run):
 
         def run(self, i):
             self.release.wait(5)
-            r = BurnInResult(ok=False, tflops=1400.0 - 100 * i, hbm_gbps=6000.0, mfma_rel_err=1e-4)
+            r = BurnInResult(ok=False, tflops=1400.0 - 100 * i, hbm_gbps=6000.0, mfma_rel_err=1e-4,
+                             fp8_tflops=2800.0, fp8_rel_err=1e-5)
             if i == 3:
                 r.tflops = 350.0                       # throttled part
             r.reason = self.judge(r)
@@ -223,6 +224,7 @@ def test_burn_in_gates_devices_and_publishes_measurements(tmp_path, run):
         assert [cap[i]["health"] for i in ids] == [api.HEALTHY] * 3 + [api.UNHEALTHY]
         assert cap[ids[3]]["attributes"][ATTR_BURN_IN] == "failed" and "350" in plugin._burn[ids[3]].reason
         assert cap[ids[1]]["attributes"][ATTR_MFMA_TFLOPS] == "1300" and cap[ids[1]]["attributes"][ATTR_HBM_GBPS] == "6000"
+        assert cap[ids[1]]["attributes"]["amd.com/mfma-fp8-tflops"] == "2800"
         await m.admit_pod(_pod("u1", [ids[0]]))
         # a pod can ask for the fastest parts only
         er = ERManager()

@@ -60,7 +60,8 @@ def test_e2e_gpu_spec_on_real_mi355x(run):
 
 def test_burn_in_gates_real_gpus_then_pod_runs(run):
     """The plugin's acceptance test on the real MI355X: HIP vector_add exact, MFMA bf16 GEMM
-    8192^3 within tolerance and >= 700 TFLOP/s, HBM copy >= 3000 GB/s; only then does the GPU
+    8192^3 within tolerance and >= 700 TFLOP/s, the fp8 block-scaled MFMA GEMM >= 1400 TFLOP/s,
+    HBM copy >= 3000 GB/s; only then does the GPU
     turn Healthy, carry its measured numbers, and take a pod."""
     import asyncio
     from kubernetes_amd.api import core
@@ -80,6 +81,7 @@ def test_burn_in_gates_real_gpus_then_pod_runs(run):
             assert passed, plugin._burn
             for r in passed.values():
                 assert r.tflops >= 700 and r.hbm_gbps >= 3000 and r.mfma_rel_err < 1e-2 and r.vadd_err == 0
+                assert r.fp8_tflops >= 1400 and r.fp8_rel_err < 1e-2
             await asyncio.sleep(0.5)
             node = await cl.client.get("nodes", cl.nodes[0].name)
             devs = node["status"]["extendedResources"][core.AMD_GPU]["resources"]

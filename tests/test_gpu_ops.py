@@ -153,3 +153,9 @@ def test_gemm_fp8_rejects_untiled_shapes(hk):
     a, b = _fp8_operands(256, 256, 128)
     with pytest.raises(ValueError):
         hk.gemm_fp8_nt(a[:, :64].contiguous(), b[:, :64].contiguous())
+
+
+def test_diag_mfma_fp8(hk):
+    r = hk.diag_mfma_fp8(0, 4096, 5)
+    print(r)
+    assert r["max_rel_err"] < 1e-5 and r["tflops"] > 500
