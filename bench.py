@@ -284,7 +284,9 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     t0 = time.perf_counter()
     for k in range(args.steps):
         results.append(await runner.step(k, timeout=args.step_timeout))
-        if k + 1 < args.steps:
+        # lock-step ranks by default: measured on the 16-CPU box, free-running ranks were not
+        # faster (N=4: 3154 vs 3917 pods/s, profiles/r2_fanout_thread/) — their phases collide
+        if not args.no_step_barrier and k + 1 < args.steps:
             await abarrier()
     await abarrier()
     elapsed = time.perf_counter() - t0
@@ -373,6 +375,8 @@ def main():
     ap.add_argument("--xgmi4-steps", type=int, default=2,
                     help="untimed secondary steps of 4-GPU xGMI-hive pods (0 = skip)")
     ap.add_argument("--step-timeout", type=float, default=120.0, help="fail (with diagnostics) if a step stalls")
+    ap.add_argument("--no-step-barrier", action="store_true",
+                    help="ranks run their timed steps independently (barriers only around the timed region)")
     ap.add_argument("--scheduler-shards", type=int, default=0,
                     help="parallel scheduler shard processes (0 = auto from the CPU budget)")
     ap.add_argument("--hollow-procs", type=int, default=0,
