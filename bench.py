@@ -74,8 +74,8 @@ def control_plane_shape(world, workers=0, shards=0):
     workers read pods from the store instead of caching every pod event, 2 workers + 2
     partitioned scheduler shards beat the single in-process-store API server already at N=1
     (1946-2086 vs 1574-1793 pods/s, p99 19 vs 62-90 ms); N=4: w=4 s=4 3184 vs w=4 s=2 2727.
-    On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — one API
-    server worker and one scheduler shard per rank, up to 8 each — so per-rank work (weak
+    On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — two API
+    server workers (up to 16) and one scheduler shard (up to 8) per rank — so per-rank work (weak
     scaling) is met by per-rank control-plane capacity instead of a fixed-size control plane."""
     cpus = cpu_budget()
     spare = cpus - world - 1
@@ -84,7 +84,11 @@ def control_plane_shape(world, workers=0, shards=0):
         if spare < 3:
             workers = 1
         elif big:
-            workers = min(8, max(2, world), max(1, spare // 6))
+            # API workers are the per-pod cost that grows with the rank count (~0.7-0.9 ms of
+            # worker CPU per pod vs ~0.4-0.6 scheduler, 0.06-0.14 store): two per rank, up to 16.
+            # The store is not the limit there: kubemark/store_bench.py measures its busiest
+            # thread at 0.03-0.04 ms per pod (ceiling > 24k pods/s with 68 watches).
+            workers = min(16, max(2, 2 * world), max(1, spare // 5))
         else:
             workers = 2 if world < 4 else 4
     if shards <= 0:

@@ -39,6 +39,8 @@ def _parser():
     ap.add_argument("--storage-media-type", default=codec.JSON)
     ap.add_argument("--storage-engine", default="native", choices=["native", "python"])
     ap.add_argument("--etcd-wal", default=None, help="durable WAL path for the store")
+    ap.add_argument("--etcd-fan-threads", type=int, default=0,
+                    help="watch fan-out threads of the shared native store (0 = KAMD_ETCD_FAN_THREADS or 1)")
     ap.add_argument("--etcd-servers", default=None, help="shared native store address (unix://PATH or tcp://HOST:PORT)")
     ap.add_argument("--workers", type=int, default=1, help="API server worker processes sharing one native store")
     ap.add_argument("--reuse-port", action="store_true", help=argparse.SUPPRESS)
@@ -96,7 +98,7 @@ def load_admission_config(path):
 
 
 # flags the multi-worker supervisor sets itself for each worker
-_SUPERVISOR_OWNED = {"workers", "port", "port_file", "etcd_wal", "etcd_servers", "reuse_port", "bind_address",
+_SUPERVISOR_OWNED = {"workers", "port", "port_file", "etcd_wal", "etcd_fan_threads", "etcd_servers", "reuse_port", "bind_address",
                      "audit_log_path", "audit_policy_file", "v"}
 
 
@@ -134,7 +136,7 @@ def _free_port(host):
 
 def supervise(a):
     from ..storage.remote import StoreServer
-    store = StoreServer(wal=a.etcd_wal)
+    store = StoreServer(wal=a.etcd_wal, fan_threads=a.etcd_fan_threads or None)
     addr = store.start()
     port = a.port or _free_port(a.bind_address)
     base = [sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--bind-address", a.bind_address,

@@ -246,8 +246,10 @@ class FanoutClient:
 class StoreServer:
     """Runs `kamd-etcd` as a child process on a unix socket (or TCP port)."""
 
-    def __init__(self, socket_path=None, wal=None, history=500_000, tcp=False):
+    def __init__(self, socket_path=None, wal=None, history=500_000, tcp=False, fan_threads=None):
         self.dir = None
+        # watch fan-out threads in kamd-etcd (1..4); KAMD_ETCD_FAN_THREADS overrides the default 1
+        self.fan_threads = int(fan_threads or os.environ.get("KAMD_ETCD_FAN_THREADS") or 1)
         if socket_path is None and not tcp:
             self.dir = tempfile.mkdtemp(prefix="kamd-etcd-")
             socket_path = os.path.join(self.dir, "store.sock")
@@ -264,7 +266,7 @@ class StoreServer:
         exe = os.environ.get("KAMD_ETCD_BIN") or os.path.join(BIN_DIR, "kamd-etcd")
         if not os.path.exists(exe):
             raise StoreError(f"{exe} not built (python -m kubernetes_amd.native.build)")
-        cmd = [exe, "--history", str(self.history)]
+        cmd = [exe, "--history", str(self.history), "--fan-threads", str(self.fan_threads)]
         port_file = None
         if self.tcp:
             port_file = tempfile.mktemp(prefix="kamd-etcd-port-")

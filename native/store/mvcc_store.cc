@@ -65,9 +65,11 @@ namespace kamd {
 struct KV {
   int64_t create_rev = 0, mod_rev = 0, version = 0;
   std::string value;
-  // server-side parse cache of the value's index frame (watch fan-out): a value is immutable, so
-  // its header is parsed once — as an event's new state and again as the next event's `prev`
-  mutable std::shared_ptr<void> aux;
+  // server-side parse cache of the value's index frame, one slot per watch fan-out thread (each
+  // thread only touches its own): a value is immutable, so its header is parsed once per thread —
+  // as an event's new state and again as the next event's `prev`
+  static constexpr int kAuxSlots = 4;
+  mutable std::shared_ptr<void> aux[kAuxSlots];
 };
 
 struct Event {
@@ -603,14 +605,15 @@ static void parse_index_into(const std::string& v, Index* ix) {
   ix->ok = true;
 }
 
-// the parsed index frame of a stored value, cached on the KV
-static const Index& index_of(const KV& kv) {
-  if (!kv.aux) {
+// the parsed index frame of a stored value, cached on the KV in the calling fan-out thread's slot
+static const Index& index_of(const KV& kv, int slot) {
+  std::shared_ptr<void>& a = kv.aux[slot];
+  if (!a) {
     auto ix = std::make_shared<Index>();
     parse_index_into(kv.value, ix.get());
-    kv.aux = ix;
+    a = ix;
   }
-  return *static_cast<const Index*>(kv.aux.get());
+  return *static_cast<const Index*>(a.get());
 }
 
 static const Index& empty_index() {
@@ -618,17 +621,20 @@ static const Index& empty_index() {
   return e;
 }
 
-static uint32_t crc32_ieee(std::string_view s) {   // zlib.crc32
-  static uint32_t table[256];
-  static bool init = false;
-  if (!init) {
+struct Crc32Table {
+  uint32_t t[256];
+  Crc32Table() {
     for (uint32_t i = 0; i < 256; ++i) {
       uint32_t c = i;
       for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-      table[i] = c;
+      t[i] = c;
     }
-    init = true;
   }
+};
+
+static uint32_t crc32_ieee(std::string_view s) {   // zlib.crc32
+  static const Crc32Table tab;   // thread-safe one-time init (several fan-out threads call this)
+  const uint32_t* table = tab.t;
   uint32_t c = 0xFFFFFFFFu;
   for (unsigned char ch : s) c = table[(c ^ ch) & 0xFF] ^ (c >> 8);
   return c ^ 0xFFFFFFFFu;
@@ -741,7 +747,9 @@ static void chunk(std::string* out, const char* type, const std::string& v, size
 // nothing is lost or sent twice. The store thread never touches KV::aux (the parse cache).
 class FanOut {
  public:
+  explicit FanOut(int slot = 0) : slot_(slot) {}
   ~FanOut() { stop(); }
+  int watches() const { return watches_.load(std::memory_order_acquire); }
 
   void start() {
     ep_ = epoll_create1(EPOLL_CLOEXEC);
@@ -764,13 +772,12 @@ class FanOut {
     close(ep_);
   }
 
-  // store thread: queue a committed transaction's events / a new watch (order preserved)
-  void post(std::vector<Event>&& evs) {
+  // store thread: queue a committed transaction's events (shared by every fan-out thread) / a
+  // new watch (order preserved)
+  void post(const std::shared_ptr<const std::vector<Event>>& evs) {
     if (watches_.load(std::memory_order_acquire) == 0) return;   // nobody to tell
     if (pending_.empty() || !pending_.back().evs_only) pending_.emplace_back();
-    auto& b = pending_.back().evs;
-    if (b.empty()) b = std::move(evs);
-    else for (Event& e : evs) b.push_back(std::move(e));
+    pending_.back().chunks.push_back(evs);
   }
   void post(std::unique_ptr<FanWatch> w) {
     pending_.emplace_back();
@@ -792,7 +799,7 @@ class FanOut {
  private:
   struct Msg {
     bool evs_only = true;
-    std::vector<Event> evs;
+    std::vector<std::shared_ptr<const std::vector<Event>>> chunks;
     std::unique_ptr<FanWatch> w;
   };
 
@@ -832,9 +839,9 @@ class FanOut {
       }
       for (Msg& m : work) {
         if (m.w) adopt(std::move(m.w));
-        else if (!m.evs.empty()) {
+        else if (!m.chunks.empty()) {
           KPROF_BEGIN;
-          fan_dispatch(m.evs);
+          for (const auto& c : m.chunks) fan_dispatch(*c);
           KPROF_END(6);
         }
       }
@@ -857,7 +864,7 @@ class FanOut {
     FanWatch* raw = w.get();
     if (w->send_initial) {
       for (const auto& kv : w->initial) {
-        const Index& ix = index_of(*kv);
+        const Index& ix = index_of(*kv, slot_);
         if (w->matches(ix)) chunk(&w->out, "ADDED", kv->value, ix.body);
       }
     }
@@ -889,8 +896,8 @@ class FanOut {
   // a DELETED for that watcher, one that starts matching an ADDED)
   void fan_one(FanWatch* w, const Event& ev, const Index* cur = nullptr, const Index* prv = nullptr) {
     if (ev.key.compare(0, w->prefix.size(), w->prefix) != 0 || ev.rev <= w->min_rev) return;
-    if (!cur) cur = &index_of(*ev.kv);
-    if (!prv) prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
+    if (!cur) cur = &index_of(*ev.kv, slot_);
+    if (!prv) prv = ev.prev ? &index_of(*ev.prev, slot_) : &empty_index();
     bool now = w->matches(*cur);
     bool was = ev.prev && w->matches(*prv);
     const std::string& v = ev.kv->value;
@@ -915,8 +922,8 @@ class FanOut {
       const Index* prv = nullptr;
       auto parse = [&]() {
         if (cur) return;
-        cur = &index_of(*ev.kv);
-        prv = ev.prev ? &index_of(*ev.prev) : &empty_index();
+        cur = &index_of(*ev.kv, slot_);
+        prv = ev.prev ? &index_of(*ev.prev, slot_) : &empty_index();
       };
       for (FanWatch* w : fan_other_) {
         if (w->dead || ev.key.compare(0, w->prefix.size(), w->prefix) != 0) continue;
@@ -945,8 +952,8 @@ class FanOut {
     // a superseded value's parse is not needed again (resumed watches re-parse on demand):
     // the cache lives on current values only, so history memory does not grow with it
     for (const Event& ev : evs) {
-      if (ev.prev) ev.prev->aux.reset();
-      if (ev.type == 1) ev.kv->aux.reset();   // a tombstone is never a current value
+      if (ev.prev) ev.prev->aux[slot_].reset();
+      if (ev.type == 1) ev.kv->aux[slot_].reset();   // a tombstone is never a current value
     }
   }
 
@@ -1027,6 +1034,7 @@ class FanOut {
     }
   }
 
+  const int slot_;                // this thread's KV::aux slot
   // store thread only
   std::vector<Msg> pending_;
   // shared
@@ -1089,8 +1097,16 @@ class Server {
 
   // returns when SIGTERM/SIGINT set *stop (a clean exit: destructors run, so leak checkers and
   // the WAL's final fclose see a normal shutdown)
+  // watch fan-out threads (1..KV::kAuxSlots); watches are spread over them, events go to all
+  void set_fan_threads(int n) {
+    n = std::max(1, std::min(n, KV::kAuxSlots));
+    fans_.clear();
+    for (int i = 0; i < n; ++i) fans_.push_back(std::make_unique<FanOut>(i));
+  }
+
   void run(volatile sig_atomic_t* stop) {
-    fan_.start();
+    if (fans_.empty()) set_fan_threads(1);
+    for (auto& f : fans_) f->start();
     epoll_event evs[256];
     while (!*stop) {
       int n = epoll_wait(ep_, evs, 256, 1000);
@@ -1108,8 +1124,8 @@ class Server {
         }
         if (evs[i].events & EPOLLOUT) flush(c);
       }
-      // this pass's committed events and new watches go to the fan-out thread in one batch
-      fan_.commit();
+      // this pass's committed events and new watches go to the fan-out threads in one batch each
+      for (auto& f : fans_) f->commit();
       if (progress_pending_) {
         KPROF_BEGIN;
         send_progress();
@@ -1123,7 +1139,7 @@ class Server {
         KPROF_END(7);
       }
     }
-    fan_.stop();
+    for (auto& f : fans_) f->stop();
   }
 
  private:
@@ -1281,7 +1297,7 @@ class Server {
             dispatch(evs);
             KPROF_END(5);
           }
-          fan_.post(std::move(evs));
+          post_events(std::move(evs));
         } else {
           w.put<uint16_t>((uint16_t)failed);
           const KV* kv = eng_->get(cmps[failed].key);
@@ -1485,12 +1501,24 @@ class Server {
       }
       w->min_rev = from;
     }
-    fan_.post(std::move(w));
+    // the least loaded fan-out thread adopts the watch
+    FanOut* best = fans_[0].get();
+    for (auto& f : fans_)
+      if (f->watches() < best->watches()) best = f.get();
+    best->post(std::move(w));
+  }
+
+  void post_events(std::vector<Event>&& evs) {
+    bool any = false;
+    for (auto& f : fans_) any |= f->watches() > 0;
+    if (!any) return;
+    auto sp = std::make_shared<const std::vector<Event>>(std::move(evs));
+    for (auto& f : fans_) f->post(sp);
   }
 
   std::unordered_map<int, int> handoff_listeners_;
   std::unordered_map<int, Handoff> handoffs_;
-  FanOut fan_;
+  std::vector<std::unique_ptr<FanOut>> fans_;
 
   Engine* eng_;
   int ep_ = -1;
@@ -1517,6 +1545,7 @@ int main(int argc, char** argv) {
   const char* port_file = nullptr;
   const char* handoff_path = nullptr;
   int tcp_port = -1;
+  int fan_threads = 1;
   size_t hist = 500000;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -1527,11 +1556,13 @@ int main(int argc, char** argv) {
     else if (a == "--history") hist = (size_t)atol(val());
     else if (a == "--port-file") port_file = val();
     else if (a == "--listen-handoff") handoff_path = val();
-    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--listen-handoff PATH] [--wal FILE] [--history N]\n"); return 2; }
+    else if (a == "--fan-threads") fan_threads = atoi(val());
+    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--listen-handoff PATH] [--wal FILE] [--history N] [--fan-threads N]\n"); return 2; }
   }
   kamd::Engine eng(hist);
   if (wal && !eng.open_wal(wal)) { perror("wal"); return 1; }
   kamd::Server srv(&eng);
+  srv.set_fan_threads(fan_threads);
   if (unix_path && srv.listen_unix(unix_path) < 0) return 1;
   if (handoff_path && srv.listen_handoff(handoff_path) < 0) return 1;
   if (tcp_port >= 0) {

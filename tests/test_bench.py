@@ -85,3 +85,25 @@ def test_payload_server_batches_starts(run, tmp_path):
         for s in (srv, srv2):
             await s.stop()
     run(main())
+
+
+def test_control_plane_shape_grows_with_ranks_on_a_big_node(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
+    assert bench.control_plane_shape(1) == (2, 2)          # N=1 keeps the measured small shape
+    assert bench.control_plane_shape(4) == (8, 4)
+    assert bench.control_plane_shape(8) == (16, 8)
+    monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
+    w, s = bench.control_plane_shape(8)
+    assert w <= 11 and s <= 9
+    monkeypatch.setattr(bench, "cpu_budget", lambda: 16)
+    assert bench.control_plane_shape(1) == (2, 2) and bench.control_plane_shape(4) == (4, 4)
+
+
+def test_store_bench_small():
+    """kamd-etcd under the density write + watch pattern: every event reaches its watchers."""
+    from kubernetes_amd.kubemark.store_bench import run
+    r = run(writers=2, pods=400, nodes=8, all_watches=2, fan_threads=2, inflight=16)
+    # its node's watch sees bind (ADDED), Running and the delete; each whole-prefix watch all 4
+    assert r["pods"] == 400 and r["events_delivered"] == 400 * (3 + 4 * 2), r
+    assert r["pods_per_s"] > 0 and set(r["store_cpu_ms_per_pod"]) >= {"store", "fan0", "fan1"}

@@ -68,10 +68,12 @@ def test_shared_store_server_asan(san_build, tmp_path):
 
 
 def test_shared_store_server_tsan(san_build, tmp_path):
-    """kamd-etcd runs two threads (store + watch fan-out, sharing the event queue and the KV
-    objects' lifetimes and parse cache): the multi-worker API server suite against its TSan build."""
+    """kamd-etcd runs a store thread and watch fan-out threads (here 3) that share the event
+    queues, the KV objects' lifetimes and (per-thread slots of) their parse cache: the multi-worker
+    API server suite against its TSan build."""
     logs = tmp_path / "etcd-logs"
     env = dict(os.environ, KAMD_ETCD_BIN=os.path.join(san_build, "tsan", "kamd-etcd"), KAMD_ETCD_LOG_DIR=str(logs),
+               KAMD_ETCD_FAN_THREADS="3",
                TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
                         "tests/test_apiserver_shared.py"], cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
