@@ -229,9 +229,18 @@ def describe(obj, events=()):
             lines.append(f"Extended Resources ({rn}):")
             for did, d in sorted(((dom or {}).get("resources") or {}).items(), key=lambda kv: kv[1].get("attributes", {}).get(core.ATTR_INDEX, "")):
                 a = d.get("attributes") or {}
+                extra = ""
+                if a.get(core.ATTR_PARTITION, "SPX") != "SPX":
+                    extra += (f" partition={a.get(core.ATTR_PARTITION)}/{a.get(core.ATTR_PARTITION_ID, '?')}"
+                              f"@socket{a.get(core.ATTR_SOCKET, '?')}")
+                if a.get("amd.com/burn-in"):
+                    extra += f" burn-in={a['amd.com/burn-in']}"
+                    if a.get("amd.com/mfma-tflops"):
+                        extra += (f" (bf16 {a['amd.com/mfma-tflops']} / fp8 {a.get('amd.com/mfma-fp8-tflops', '-')} TF/s,"
+                                  f" HBM {a.get('amd.com/hbm-gbps', '-')} GB/s)")
                 lines.append(f"  {did}  {d.get('health')}  {a.get(core.ATTR_PRODUCT, '')} {a.get(core.ATTR_ARCH, '')} "
                              f"hbm={a.get(core.ATTR_HBM, '')} hive={a.get(core.ATTR_HIVE, '')} numa={a.get(core.ATTR_NUMA, '')} "
-                             f"render=renderD{a.get(core.ATTR_RENDER_MINOR, '?')}")
+                             f"render=renderD{a.get(core.ATTR_RENDER_MINOR, '?')}{extra}")
         taints = (obj.get("spec") or {}).get("taints") or []
         lines.append(f"Taints:       {', '.join(t['key'] + ':' + t['effect'] for t in taints) or '<none>'}")
         lines.append(f"Unschedulable: {bool((obj.get('spec') or {}).get('unschedulable'))}")

@@ -267,3 +267,16 @@ def test_daemonset_revisions_rolling_update_and_undo(cluster):
     wait(lambda: pods_with("agent:v1"), 60)
     revs = _get(cluster, "-n", "dsrev", "controllerrevisions")["items"]
     assert max(revs, key=lambda r: r["revision"])["data"]["spec"]["template"]["spec"]["containers"][0]["image"] == "agent:v1"
+
+
+def test_describe_node_shows_partitions_and_burn_in():
+    from kubernetes_amd.api import core
+    from kubernetes_amd.kubectl.printers import describe
+    attrs = {core.ATTR_PRODUCT: "MI355X", core.ATTR_ARCH: "gfx950", core.ATTR_HBM: "36Gi", core.ATTR_HIVE: "h",
+             core.ATTR_NUMA: "0", core.ATTR_RENDER_MINOR: "137", core.ATTR_INDEX: "9", core.ATTR_PARTITION: "CPX",
+             core.ATTR_PARTITION_ID: "1", core.ATTR_SOCKET: "1", "amd.com/burn-in": "passed",
+             "amd.com/mfma-tflops": "1188", "amd.com/mfma-fp8-tflops": "2242", "amd.com/hbm-gbps": "6199"}
+    node = {"kind": "Node", "metadata": {"name": "n"}, "spec": {},
+            "status": {"extendedResources": {core.AMD_GPU: {"resources": {"g9": {"health": "Healthy", "attributes": attrs}}}}}}
+    out = describe(node)
+    assert "partition=CPX/1@socket1" in out and "burn-in=passed (bf16 1188 / fp8 2242 TF/s, HBM 6199 GB/s)" in out
