@@ -4,13 +4,14 @@ watch pattern, without the Python API server in front of it.
 P writer processes run pod lifecycles against the store the way API server workers commit them
 (create, bind to a node, Running status, delete with a tombstone: 4 transactions and 4 watch
 events per pod, values framed with the index header the fan-out matches on). Meanwhile the
-store's fan-out serves W node-indexed watches (one per hollow kubelet, `spec.nodeName=<node>`) and
-A whole-prefix watches (scheduler shards and the density observers), each drained by a reader
-thread. Reported: pods/s, and the store's CPU per pod split by thread (the store thread commits
+store's fan-out serves the density run's watches, each drained by a reader thread: one per hollow
+kubelet (`spec.nodeName=<node>`), one per scheduler shard (unassigned pods of its shard,
+`?kamdShard=i/n`), one density observer per writer (its namespace) and optionally A unfiltered
+whole-prefix watches. Reported: pods/s, and the store's CPU per pod split by thread (the store thread commits
 and answers writers, the fan-out threads match and write watch streams) — 1 / (busiest thread's
 CPU per pod) is the store's ceiling in pods/s.
 
-    python -m kubernetes_amd.kubemark.store_bench --writers 4 --pods 20000 --fan-threads 1
+    python -m kubernetes_amd.kubemark.store_bench --writers 8 --pods 40000 --shards 8 --fan-threads 1 2
 """
 from __future__ import annotations
 
@@ -59,8 +60,12 @@ async def _writer_main(addr, wid, pods, nodes, inflight):
 
 def _writer(addr, wid, pods, nodes, inflight, q):
     t0 = time.perf_counter()
-    asyncio.run(_writer_main(addr, wid, pods, nodes, inflight))
-    q.put(time.perf_counter() - t0)
+    try:
+        asyncio.run(_writer_main(addr, wid, pods, nodes, inflight))
+    except BaseException as e:  # noqa: BLE001 - reported to the parent, which fails the run
+        q.put(("error", f"writer {wid}: {e!r}"))
+        raise
+    q.put(("ok", time.perf_counter() - t0))
 
 
 _EVENT = b'{"type":"'
@@ -97,13 +102,17 @@ def _thread_cpu(pid):
     return out
 
 
-def run(writers=4, pods=20000, nodes=64, all_watches=4, fan_threads=1, inflight=64):
+def run(writers=4, pods=20000, nodes=64, all_watches=0, fan_threads=1, inflight=64, shards=4):
     srv = StoreServer(fan_threads=fan_threads)
     addr = srv.start()
     fc = FanoutClient.for_store(addr)
     stop = threading.Event()
     readers, counters, socks = [], [], []
+    from ..api.sharding import SHARD_OFFSET_LABEL
     specs = [[(FanoutClient.FIELD, "=", "spec.nodeName", [f"node-{n}"])] for n in range(nodes)]
+    specs += [[(FanoutClient.FIELD, "=", "spec.nodeName", [""]), (FanoutClient.LABEL, "shard", SHARD_OFFSET_LABEL, [shards, i])]
+              for i in range(shards)]
+    specs += [[(FanoutClient.FIELD, "=", "metadata.namespace", [f"bench-{w}"])] for w in range(writers)]
     specs += [[] for _ in range(all_watches)]
     for reqs in specs:
         a, b = socket.socketpair()
@@ -126,8 +135,16 @@ def run(writers=4, pods=20000, nodes=64, all_watches=4, fan_threads=1, inflight=
     for p in ps:
         p.join()
     elapsed = time.perf_counter() - t0
-    # node watch: bind (ADDED), Running, delete; whole-prefix watches: all 4 events
-    want = (pods // writers) * writers * (3 + 4 * all_watches)
+    results = [q.get(timeout=5) for _ in ps]
+    errors = [r[1] for r in results if r[0] != "ok"]
+    if errors or any(p.exitcode != 0 for p in ps):
+        stop.set()
+        srv.stop()
+        raise RuntimeError(f"store bench writers failed: {errors or [p.exitcode for p in ps]}")
+    # per pod: its node's watch sees bind (ADDED), Running, delete; its shard's watch the create
+    # (ADDED) and the bind (DELETED: no longer unassigned); its namespace observer and every
+    # whole-prefix watch all 4 events
+    want = (pods // writers) * writers * (3 + (2 if shards else 0) + 4 + 4 * all_watches)
     deadline = time.time() + 10
     while sum(c[0] for c in counters) < want and time.time() < deadline:
         time.sleep(0.05)   # let the fan-out finish writing
@@ -142,7 +159,7 @@ def run(writers=4, pods=20000, nodes=64, all_watches=4, fan_threads=1, inflight=
     busiest = max(per_pod_ms.values()) if per_pod_ms else 0.0
     return {"pods": total, "elapsed_s": round(elapsed, 3), "pods_per_s": round(total / elapsed, 1),
             "events_delivered": sum(c[0] for c in counters), "bytes_delivered": sum(c[1] for c in counters),
-            "watches": len(specs), "fan_threads": fan_threads, "writers": writers,
+            "events_expected": want, "watches": len(specs), "fan_threads": fan_threads, "writers": writers,
             "store_cpu_ms_per_pod": per_pod_ms,
             "ceiling_pods_per_s": round(1e3 / busiest, 0) if busiest else None}
 
@@ -152,12 +169,13 @@ def main(argv=None):
     ap.add_argument("--writers", type=int, default=4)
     ap.add_argument("--pods", type=int, default=20000)
     ap.add_argument("--nodes", type=int, default=64)
-    ap.add_argument("--all-watches", type=int, default=4)
+    ap.add_argument("--all-watches", type=int, default=0)
+    ap.add_argument("--shards", type=int, default=4)
     ap.add_argument("--fan-threads", type=int, nargs="+", default=[1])
     ap.add_argument("--inflight", type=int, default=64)
     a = ap.parse_args(argv)
     for ft in a.fan_threads:
-        print(json.dumps(run(a.writers, a.pods, a.nodes, a.all_watches, ft, a.inflight)), flush=True)
+        print(json.dumps(run(a.writers, a.pods, a.nodes, a.all_watches, ft, a.inflight, a.shards)), flush=True)
 
 
 if __name__ == "__main__":

@@ -103,7 +103,8 @@ def test_control_plane_shape_grows_with_ranks_on_a_big_node(monkeypatch):
 def test_store_bench_small():
     """kamd-etcd under the density write + watch pattern: every event reaches its watchers."""
     from kubernetes_amd.kubemark.store_bench import run
-    r = run(writers=2, pods=400, nodes=8, all_watches=2, fan_threads=2, inflight=16)
-    # its node's watch sees bind (ADDED), Running and the delete; each whole-prefix watch all 4
-    assert r["pods"] == 400 and r["events_delivered"] == 400 * (3 + 4 * 2), r
+    r = run(writers=2, pods=400, nodes=8, all_watches=1, fan_threads=2, inflight=16, shards=2)
+    # node watch: bind, Running, delete; shard watch: create, bind (leaves); namespace observer
+    # and the whole-prefix watch: all 4
+    assert r["pods"] == 400 and r["events_delivered"] == r["events_expected"] == 400 * (3 + 2 + 4 + 4), r
     assert r["pods_per_s"] > 0 and set(r["store_cpu_ms_per_pod"]) >= {"store", "fan0", "fan1"}
