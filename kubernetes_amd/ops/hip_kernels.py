@@ -51,6 +51,7 @@ def load():
         L.kamd_payload_destroy.argtypes = [vp]
         L.kamd_hip_device_arch.argtypes = [i, ctypes.c_char_p, i]
         L.kamd_gemm_set_path.argtypes = [i]
+        L.kamd_gemm_set_group.argtypes = [i]
         L.kamd_hbm_copy_config.argtypes = [i, i]
         _lib = L
     return _lib
@@ -116,6 +117,11 @@ def gemm_fp8_nt(a, b, out_fp32=True, alpha=1.0):
     _raise(load().kamd_gemm_fp8_nt_launch(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, N, float(alpha),
                                           1 if out_fp32 else 0, _stream(a)), "gemm_fp8_nt")
     return out
+
+
+def set_gemm_group(group: int):
+    """M-tiles per group of the ping-pong GEMM's L2-friendly tile order (default 4)."""
+    load().kamd_gemm_set_group(int(group))
 
 
 def set_gemm_path(path: int):

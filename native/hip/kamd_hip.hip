@@ -28,6 +28,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 static thread_local char g_err[256];
+static int g_pp_group = 4;     // ping-pong GEMM: M-tiles per group of the L2-friendly tile order
 static int g_gemm_path = 0;   // 0 auto (ping-pong 256-tile kernel when the shape allows), 1 force the 128-tile
                               // kernel, 2 the 2-barrier 256-tile glds kernel, 3-6 ping-pong variants, 7 the 8-phase
                               // 256-tile kernel
@@ -524,7 +525,7 @@ constexpr int EPI_BYTES = 8 * 64 * EPI_STRIDE * 4;  // 8 waves x 64 x 68 fp32 = 
 template <typename OutT, int VARIANT, bool FP8 = false>
 __global__ void __launch_bounds__(THREADS, 1)
 gemm_bf16_nt_pp_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, OutT* __restrict__ C,
-                       int M, int N, int K, int ldc, float alpha) {
+                       int M, int N, int K, int ldc, float alpha, int group) {
   // element type of the operands: addresses below are in elements, as in the bf16 original
   typedef typename std::conditional<FP8, unsigned char, u16>::type elem_t;
   constexpr int EPC = 16 / sizeof(elem_t);           // elements per 16-B chunk (8 bf16, 16 fp8)
@@ -536,7 +537,7 @@ gemm_bf16_nt_pp_kernel(const void* __restrict__ Av, const void* __restrict__ Bv,
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nwg);
-  const int GROUP = 4;
+  const int GROUP = group;          // tile-rows per L2 group (swizzled tile order)
   const int group_id = t / (GROUP * tiles_n);
   const int first_m = group_id * GROUP;
   const int gsz = min(tiles_m - first_m, GROUP);
@@ -839,6 +840,7 @@ extern "C" {
 const char* kamd_hip_last_error() { return g_err; }
 
 void kamd_gemm_set_path(int path) { g_gemm_path = path; }
+void kamd_gemm_set_group(int group) { g_pp_group = group > 0 ? group : 4; }
 
 int kamd_hip_device_count() {
   int n = 0;
@@ -884,10 +886,10 @@ int kamd_gemm_fp8_nt_launch(const void* A, const void* B, void* C, int M, int N,
   }
   if (out_fp32)
     hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
-                       gemmpp::LDS_BYTES, stream, A, B, (float*)C, M, N, K, ldc, alpha);
+                       gemmpp::LDS_BYTES, stream, A, B, (float*)C, M, N, K, ldc, alpha, g_pp_group);
   else
     hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
-                       gemmpp::LDS_BYTES, stream, A, B, (__bf16*)C, M, N, K, ldc, alpha);
+                       gemmpp::LDS_BYTES, stream, A, B, (__bf16*)C, M, N, K, ldc, alpha, g_pp_group);
   return check(hipGetLastError(), "gemm fp8 launch");
 }
 
@@ -916,7 +918,7 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
       attr = true;                                                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<T, V>), dim3(tiles), dim3(gemmpp::THREADS), lds, stream, \
-                       A, B, (T*)C, M, N, K, ldc, alpha);                                                      \
+                       A, B, (T*)C, M, N, K, ldc, alpha, g_pp_group);                                          \
   } while (0)
     if (out_fp32) {
       switch (variant) {
