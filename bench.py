@@ -272,7 +272,8 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         await asyncio.sleep(0.05)
     await c.close()
     pods_per_step = args.pods_per_rank or args.nodes_per_rank * args.gpus_per_node // args.gpus_per_pod
-    runner = DensityRunner(url, d.rank, pods_per_step=pods_per_step, gpus_per_pod=args.gpus_per_pod)
+    runner = DensityRunner(url, d.rank, pods_per_step=pods_per_step, gpus_per_pod=args.gpus_per_pod,
+                           client_procs=args.client_procs, workdir=tempfile.mkdtemp(prefix="kamd-dc-"))
     await runner.start()
     from kubernetes_amd.cmd._common import tune_gc
     tune_gc()        # same GC settings as the control-plane components
@@ -283,6 +284,8 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     results = []
     await abarrier()
     hollow_pids = [("hollow", p.pid) for p in hprocs]
+    # request-issuing helpers are load generator CPU, reported beside the rank's own
+    hollow_pids += [("density_clients", p.pid) for p in (runner.pool.procs if runner.pool else ())]
     cp0 = _cp_cpu(list(cp_procs) + hollow_pids)
     my0 = time.process_time()
     t0 = time.perf_counter()
@@ -379,6 +382,8 @@ def main():
     ap.add_argument("--xgmi4-steps", type=int, default=2,
                     help="untimed secondary steps of 4-GPU xGMI-hive pods (0 = skip)")
     ap.add_argument("--step-timeout", type=float, default=120.0, help="fail (with diagnostics) if a step stalls")
+    ap.add_argument("--client-procs", type=int, default=0,
+                    help="helper processes per rank that issue the density creates/deletes (0 = the rank itself)")
     ap.add_argument("--no-step-barrier", action="store_true",
                     help="ranks run their timed steps independently (barriers only around the timed region)")
     ap.add_argument("--scheduler-shards", type=int, default=0,
@@ -455,7 +460,7 @@ def main():
         "cpu_ms_per_pod": {k: round(v * 1000 / max(pods, 1), 3) for k, v in
                            dict(sum_ranks=sum(s["cpu_s"] for s in allstats),
                                 **{c: sum(s["cp_cpu_s"].get(c, 0.0) for s in allstats)
-                                   for c in ("apiserver", "scheduler", "store", "hollow")}).items()},
+                                   for c in ("apiserver", "scheduler", "store", "hollow", "density_clients")}).items()},
     }
     print(json.dumps(out), flush=True)
 

@@ -38,8 +38,13 @@ def pct(vals, q):
 
 class DensityRunner:
     def __init__(self, master, rank=0, namespace="density", pods_per_step=64, gpus_per_pod=1, concurrency=128,
-                 annotations=None):
+                 annotations=None, client_procs=0, workdir=None):
+        self.master = master
         self.client = Client(master, max_conns=64)
+        # client_procs > 0: creates/deletes are issued by helper processes (density_client.py)
+        self.client_procs = client_procs
+        self.workdir = workdir
+        self.pool = None
         self.rank = rank
         self.ns = namespace
         self.pods_per_step = pods_per_step
@@ -66,6 +71,10 @@ class DensityRunner:
         self._stream = await self.client.watch("pods", self.ns, lst["metadata"]["resourceVersion"],
                                                label_selector=self.selector)
         self._watch_task = asyncio.ensure_future(self._watch())
+        if self.client_procs:
+            import tempfile
+            from .density_client import HelperPool
+            self.pool = await HelperPool(self.master, self.client_procs, self.workdir or tempfile.gettempdir()).start()
 
     async def _watch(self):
         async for evs in self._stream.batches():
@@ -125,7 +134,12 @@ class DensityRunner:
                                                          annotations=self.annotations), self.ns)
                 api_lat["create"].append(time.monotonic() - t)
 
-        await asyncio.gather(*(create(n) for n in names))
+        if self.pool is not None:
+            sent, api_lat["create"] = await self.pool.call("create", self.ns, names, labels=labels,
+                                                           gpus=self.gpus_per_pod, annotations=self.annotations)
+            self.created.update(sent)
+        else:
+            await asyncio.gather(*(create(n) for n in names))
         t_created = time.monotonic()
         await self._wait(lambda: all(n in self.running for n in names), timeout, names, "running")
         t_running = time.monotonic()
@@ -140,7 +154,10 @@ class DensityRunner:
                         raise
                 api_lat["delete"].append(time.monotonic() - t)
 
-        await asyncio.gather(*(delete(n) for n in names))
+        if self.pool is not None:
+            _, api_lat["delete"] = await self.pool.call("delete", self.ns, names)
+        else:
+            await asyncio.gather(*(delete(n) for n in names))
         t_deleted = time.monotonic()
         await self._wait(lambda: all(n in self.gone for n in names), timeout, names, "gone")
         t_gone = time.monotonic()
@@ -151,6 +168,8 @@ class DensityRunner:
                 "scheduled_times": [s - t0 for s in sched], "api_latencies": api_lat}
 
     async def stop(self):
+        if self.pool is not None:
+            await self.pool.stop()
         if self._stream:
             self._stream.close()
         if self._watch_task:
