@@ -88,9 +88,11 @@ def control_plane_shape(world, workers=0, shards=0):
             # worker CPU per pod vs ~0.4-0.6 scheduler, 0.06-0.14 store): two per rank, up to 16.
             # The store is not the limit there: kubemark/store_bench.py measures its busiest
             # thread at 0.03-0.04 ms per pod (ceiling > 24k pods/s with 68 watches).
-            workers = min(16, max(2, 2 * world), max(1, spare // 5))
+            workers = min(16, max(3, 2 * world), max(1, spare // 5))
         else:
-            workers = 2 if world < 4 else 4
+            # N=1, 16-CPU box (profiles/r2_density_clients/worker_sweep): w=3 2594-2611 pods/s,
+            # w=2 2363-2389, w=4 2380-2462
+            workers = 3 if world == 1 else 2 if world < 4 else 4
     if shards <= 0:
         if spare < 3:
             shards = 1

@@ -90,14 +90,14 @@ def test_payload_server_batches_starts(run, tmp_path):
 def test_control_plane_shape_grows_with_ranks_on_a_big_node(monkeypatch):
     import bench
     monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
-    assert bench.control_plane_shape(1) == (2, 2)          # N=1 keeps the measured small shape
+    assert bench.control_plane_shape(1) == (3, 2)          # N=1 keeps the measured small shape
     assert bench.control_plane_shape(4) == (8, 4)
     assert bench.control_plane_shape(8) == (16, 8)
     monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
     w, s = bench.control_plane_shape(8)
     assert w <= 11 and s <= 9
     monkeypatch.setattr(bench, "cpu_budget", lambda: 16)
-    assert bench.control_plane_shape(1) == (2, 2) and bench.control_plane_shape(4) == (4, 4)
+    assert bench.control_plane_shape(1) == (3, 2) and bench.control_plane_shape(4) == (4, 4)
 
 
 def test_store_bench_small():
