@@ -111,8 +111,13 @@ def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
         return max(1, min(want, nodes_per_rank))
     # hollow kubelets are mostly waiting on the control plane: mild oversubscription pays
     # (profiles/r2_hollow_procs, r2_scale: N=4 on 16 CPUs 1868 -> 2578 pods/s with 2 per rank)
-    spare = cpu_budget() - workers - shards - 1
-    return max(1, min(nodes_per_rank, 4, max(2, spare // max(1, world))))
+    cpus = cpu_budget()
+    spare = cpus - workers - shards - 1
+    # a whole node (>= 64 CPUs) gets up to one process per hollow node, as kubemark runs them:
+    # at ~1.2-1.4 ms of kubelet CPU per pod, 4 processes per rank would run near saturation at
+    # the N=1 rate (N=1 on the 16-CPU box: 6 processes 2601-2693 vs 4 processes 2583-2590 pods/s)
+    cap = 8 if cpus >= 64 else 4
+    return max(1, min(nodes_per_rank, cap, max(2, spare // max(1, world))))
 
 
 def spawn_hollow_procs(args, url, rank, nprocs, tmp, payload_socket):

@@ -108,3 +108,13 @@ def test_store_bench_small():
     # and the whole-prefix watch: all 4
     assert r["pods"] == 400 and r["events_delivered"] == r["events_expected"] == 400 * (3 + 2 + 4 + 4), r
     assert r["pods_per_s"] > 0 and set(r["store_cpu_ms_per_pod"]) >= {"store", "fan0", "fan1"}
+
+
+def test_hollow_procs_per_rank(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
+    assert bench.hollow_procs_for(8, 8, 16, 8) == 8          # a whole node: one per hollow node
+    monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
+    assert bench.hollow_procs_for(8, 8, 11, 8) == 5          # bounded by the spare CPUs
+    monkeypatch.setattr(bench, "cpu_budget", lambda: 16)
+    assert bench.hollow_procs_for(1, 8, 3, 2) == 4 and bench.hollow_procs_for(1, 8, 3, 2, want=6) == 6
