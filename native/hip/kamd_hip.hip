@@ -524,7 +524,7 @@ constexpr int EPI_BYTES = 8 * 64 * EPI_STRIDE * 4;  // 8 waves x 64 x 68 fp32 = 
 // takes the cycles of two bf16 ones at 4x the K: 2x the FLOPs per K-tile on the same traffic.
 template <typename OutT, int VARIANT, bool FP8 = false>
 __global__ void __launch_bounds__(THREADS, 1)
-gemm_bf16_nt_pp_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, OutT* __restrict__ C,
+gemm_nt_pp_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, OutT* __restrict__ C,
                        int M, int N, int K, int ldc, float alpha, int group) {
   // element type of the operands: addresses below are in elements, as in the bf16 original
   typedef typename std::conditional<FP8, unsigned char, u16>::type elem_t;
@@ -878,17 +878,17 @@ int kamd_gemm_fp8_nt_launch(const void* A, const void* B, void* C, int M, int N,
   const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
   static bool attr = false;
   if (!attr) {
-    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<float, 0, true>,
+    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_nt_pp_kernel<float, 0, true>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
-    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<__bf16, 0, true>,
+    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_nt_pp_kernel<__bf16, 0, true>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
     attr = true;
   }
   if (out_fp32)
-    hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<float, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
+    hipLaunchKernelGGL((gemmpp::gemm_nt_pp_kernel<float, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
                        gemmpp::LDS_BYTES, stream, A, B, (float*)C, M, N, K, ldc, alpha, g_pp_group);
   else
-    hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<__bf16, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
+    hipLaunchKernelGGL((gemmpp::gemm_nt_pp_kernel<__bf16, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
                        gemmpp::LDS_BYTES, stream, A, B, (__bf16*)C, M, N, K, ldc, alpha, g_pp_group);
   return check(hipGetLastError(), "gemm fp8 launch");
 }
@@ -913,11 +913,11 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
   do {                                                                                                         \
     static bool attr = false;                                                                                  \
     if (!attr) {                                                                                               \
-      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_bf16_nt_pp_kernel<T, V>,                                \
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_nt_pp_kernel<T, V>,                                \
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                           \
       attr = true;                                                                                             \
     }                                                                                                          \
-    hipLaunchKernelGGL((gemmpp::gemm_bf16_nt_pp_kernel<T, V>), dim3(tiles), dim3(gemmpp::THREADS), lds, stream, \
+    hipLaunchKernelGGL((gemmpp::gemm_nt_pp_kernel<T, V>), dim3(tiles), dim3(gemmpp::THREADS), lds, stream, \
                        A, B, (T*)C, M, N, K, ldc, alpha, g_pp_group);                                          \
   } while (0)
     if (out_fp32) {
