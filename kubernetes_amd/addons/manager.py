@@ -192,6 +192,19 @@ def default_addons(cluster_dns_ip="10.96.0.10", domain="cluster.local", master="
                                                                  "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
                                                         "volumeMounts": [{"name": "log", "mountPath": "/var/log"}]}],
                                         "volumes": [{"name": "log", "hostPath": {"path": "/var/log"}}]}}}},
+        # cluster/addons/dashboard: read-only web UI (GPU allocation per node/device, pods, warnings)
+        {"apiVersion": "apps/v1", "kind": "Deployment",
+         "metadata": {"name": "kubernetes-dashboard", "namespace": "kube-system",
+                      "labels": dict(lab, **{"k8s-app": "kubernetes-dashboard"})},
+         "spec": {"replicas": 1, "selector": {"matchLabels": {"k8s-app": "kubernetes-dashboard"}},
+                  "template": {"metadata": {"labels": {"k8s-app": "kubernetes-dashboard"}},
+                               "spec": {"hostNetwork": True,
+                                        "containers": [{"name": "dashboard", "image": "kubernetes-amd/hyperkube",
+                                                        "command": [sys.executable, "-m", "kubernetes_amd.cmd.dashboard",
+                                                                    "--master", master, "--port", "9090"]}]}}}},
+        {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "kubernetes-dashboard", "namespace": "kube-system",
+                                                             "labels": dict(lab, **{"k8s-app": "kubernetes-dashboard"})},
+         "spec": {"selector": {"k8s-app": "kubernetes-dashboard"}, "ports": [{"port": 80, "targetPort": 9090}]}},
         # cluster/addons/storage-class: the default class (node-local host-path provisioner)
         {"apiVersion": "storage.k8s.io/v1", "kind": "StorageClass",
          "metadata": {"name": "standard", "labels": {MODE: ENSURE},

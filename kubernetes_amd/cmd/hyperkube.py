@@ -22,6 +22,7 @@ COMPONENTS = {
     "cri": "cri", "kamd-cri": "cri",
     "device-plugin": "device_plugin", "amd-gpu-device-plugin": "device_plugin",
     "amd-smi-exporter": "amd_smi_exporter",
+    "dashboard": "dashboard",
     "hollow-node": "hollow_node", "kubemark": "hollow_node",
     "local-up": "local_up", "local-up-cluster": "local_up",
     "csi-hostpath": "csi_hostpath",

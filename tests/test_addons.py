@@ -160,3 +160,42 @@ def test_gendocs_all_components(tmp_path):
     man = gendocs.generate(str(tmp_path / "man"), "man", ["kubeadm"])
     assert any(p.endswith("kubeadm-join.1") for p in man)
     assert gendocs.generate(str(tmp_path / "y"), "yaml", ["kube-scheduler"])
+
+
+def test_dashboard_shows_gpu_allocation(run):
+    """cluster/addons/dashboard equivalent: per-device allocation, health and pods, as HTML and JSON."""
+    import json as _json
+
+    from kubernetes_amd.addons.dashboard import Dashboard
+    from kubernetes_amd.cluster import LocalCluster
+    from kubernetes_amd.utils.httpserver import HTTPServer  # noqa: F401
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=4) as cl:
+            await cl.client.create("pods", {"metadata": {"name": "g"}, "spec": {"containers": [
+                {"name": "c", "image": "x", "resources": {"limits": {"amd.com/gpu": "2"}}}]}})
+            pod = await cl.wait_pod("g")
+            d = Dashboard(cl.url)
+            port = await d.start("127.0.0.1", 0)
+            try:
+                import asyncio
+                r, w = await asyncio.open_connection("127.0.0.1", port)
+                w.write(b"GET /api/summary HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                raw = await r.read()
+                w.close()
+                body = raw.split(b"\r\n\r\n", 1)[1]
+                if b"\r\n" in body[:10]:          # chunked
+                    body = body.split(b"\r\n", 1)[1].rsplit(b"\r\n0\r\n", 1)[0]
+                s = _json.loads(body)
+                assert s["gpus"] == {"total": 4, "allocated": 2, "healthy": 4}, s["gpus"]
+                devs = {x["id"]: x["pod"] for x in s["nodes"][0]["devices"]}
+                assigned = pod["spec"]["extendedResources"][0]["assigned"]
+                assert all(devs[i] == "default/g" for i in assigned)
+                r, w = await asyncio.open_connection("127.0.0.1", port)
+                w.write(b"GET / HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                page = (await r.read()).decode()
+                w.close()
+                assert "GPUs: 2 / 4 allocated" in page and assigned[0] in page
+            finally:
+                await d.stop()
+    run(main(), timeout=60)
