@@ -725,8 +725,9 @@ gemm_nt_pp_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, OutT
         if constexpr (sizeof(OutT) == 4) {
           *reinterpret_cast<f32x4*>(dst) = v;
         } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) store_out<OutT>(dst + e, v[e]);
+          // 4 bf16 (8 B) per lane: 128 B per 16 lanes of a row
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -876,20 +877,27 @@ int kamd_gemm_fp8_nt_launch(const void* A, const void* B, void* C, int M, int N,
     return -1;
   }
   const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
-  static bool attr = false;
-  if (!attr) {
-    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_nt_pp_kernel<float, 0, true>,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
-    HC(hipFuncSetAttribute((const void*)gemmpp::gemm_nt_pp_kernel<__bf16, 0, true>,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, gemmpp::LDS_BYTES));
-    attr = true;
+  // LDS-staged vector epilogue: default for bf16 output (+1-3 %), set_gemm_path(4) forces it,
+  // any other path forces the register epilogue (A/B experiments)
+  const bool lds_epi = g_gemm_path == 4 || (g_gemm_path == 0 && !out_fp32);
+  const size_t lds = lds_epi ? gemmpp::EPI_BYTES : gemmpp::LDS_BYTES;
+#define KAMD_F8_LAUNCH(T, V)                                                                                 \
+  do {                                                                                                       \
+    static bool attr = false;                                                                                \
+    if (!attr) {                                                                                             \
+      HC(hipFuncSetAttribute((const void*)gemmpp::gemm_nt_pp_kernel<T, V, true>,                              \
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                         \
+      attr = true;                                                                                           \
+    }                                                                                                        \
+    hipLaunchKernelGGL((gemmpp::gemm_nt_pp_kernel<T, V, true>), dim3(tiles), dim3(gemmpp::THREADS), lds,      \
+                       stream, A, B, (T*)C, M, N, K, ldc, alpha, g_pp_group);                                \
+  } while (0)
+  if (out_fp32) {
+    if (lds_epi) KAMD_F8_LAUNCH(float, 2); else KAMD_F8_LAUNCH(float, 0);
+  } else {
+    if (lds_epi) KAMD_F8_LAUNCH(__bf16, 2); else KAMD_F8_LAUNCH(__bf16, 0);
   }
-  if (out_fp32)
-    hipLaunchKernelGGL((gemmpp::gemm_nt_pp_kernel<float, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
-                       gemmpp::LDS_BYTES, stream, A, B, (float*)C, M, N, K, ldc, alpha, g_pp_group);
-  else
-    hipLaunchKernelGGL((gemmpp::gemm_nt_pp_kernel<__bf16, 0, true>), dim3(tiles), dim3(gemmpp::THREADS),
-                       gemmpp::LDS_BYTES, stream, A, B, (__bf16*)C, M, N, K, ldc, alpha, g_pp_group);
+#undef KAMD_F8_LAUNCH
   return check(hipGetLastError(), "gemm fp8 launch");
 }
 
@@ -905,8 +913,10 @@ int kamd_gemm_bf16_nt_launch(const void* A, const void* B, void* C, int M, int N
     return -1;
   }
   if ((g_gemm_path == 0 || (g_gemm_path >= 3 && g_gemm_path <= 6)) && M % gemmpp::BM == 0 && N % gemmpp::BN == 0 && K % gemmpp::BK == 0) {
-    // path 3: variant 0, 4: LDS epilogue, 5: static priority, 6: both
-    const int variant = g_gemm_path <= 3 ? 0 : g_gemm_path == 4 ? 2 : g_gemm_path == 5 ? 1 : 3;
+    // path 3: variant 0, 4: LDS epilogue, 5: static priority, 6: both; auto (0) takes the LDS-staged
+    // vector epilogue for bf16 output (+1.3-1.8 %, profiles/r2_gemm_fp8/epilogue_ab.txt)
+    const int variant = g_gemm_path == 0 ? (out_fp32 ? 0 : 2)
+                        : g_gemm_path == 3 ? 0 : g_gemm_path == 4 ? 2 : g_gemm_path == 5 ? 1 : 3;
     const size_t lds = (variant & 2) ? gemmpp::EPI_BYTES : gemmpp::LDS_BYTES;
     const int tiles = (M / gemmpp::BM) * (N / gemmpp::BN);
 #define KAMD_PP_LAUNCH(T, V)                                                                                   \
