@@ -31,6 +31,15 @@
 //   kv = i64 create_rev i64 mod_rev i64 version u32 klen key u32 vlen val
 //   A kind-3 delete carries the "tombstone" (final object state) reported in the delete event
 //   instead of the last stored value; it is not stored.
+//
+// Threads (server): ONE store thread owns the engine, the worker connections and their watches
+// (epoll loop: read, commit, reply); `--fan-threads N` (1..4) fan-out threads own the Kubernetes
+// watch streams handed over by API server workers (SCM_RIGHTS on `<socket>.watch`). Once per loop
+// pass the store thread posts that pass's committed events (one shared immutable vector per txn)
+// and any newly handed-over watch to each fan-out thread, in commit order, under one mutex +
+// eventfd wake. KV values are immutable after commit; the only mutable field, the index-frame
+// parse cache `KV::aux[slot]`, is written only by fan-out thread `slot`. kubemark/store_bench.py
+// measures the capacity; tests/test_sanitizers.py runs the multi-worker suite on a TSan build.
 #include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
