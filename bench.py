@@ -116,7 +116,7 @@ def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
     # a whole node (>= 64 CPUs) gets up to one process per hollow node, as kubemark runs them:
     # at ~1.2-1.4 ms of kubelet CPU per pod, 4 processes per rank would run near saturation at
     # the N=1 rate (N=1 on the 16-CPU box: 6 processes 2601-2693 vs 4 processes 2583-2590 pods/s)
-    cap = 8 if cpus >= 64 else 4
+    cap = 8 if cpus >= 64 else 6 if world == 1 else 4
     return max(1, min(nodes_per_rank, cap, max(2, spare // max(1, world))))
 
 

@@ -117,4 +117,5 @@ def test_hollow_procs_per_rank(monkeypatch):
     monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
     assert bench.hollow_procs_for(8, 8, 11, 8) == 5          # bounded by the spare CPUs
     monkeypatch.setattr(bench, "cpu_budget", lambda: 16)
-    assert bench.hollow_procs_for(1, 8, 3, 2) == 4 and bench.hollow_procs_for(1, 8, 3, 2, want=6) == 6
+    assert bench.hollow_procs_for(1, 8, 3, 2) == 6 and bench.hollow_procs_for(2, 8, 2, 2) == 4
+    assert bench.hollow_procs_for(1, 8, 3, 2, want=3) == 3
