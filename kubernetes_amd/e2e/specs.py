@@ -602,3 +602,17 @@ async def graceful_delete(f):
         except Exception:  # noqa: BLE001
             return True
     await f.wait(gone, 30, "pod removed after graceful termination")
+
+
+@conformance("Pods should fail with DeadlineExceeded once activeDeadlineSeconds passes")
+async def active_deadline(f):
+    p = _pod("deadline", "sleep 3600", restart="Always")
+    p["spec"]["activeDeadlineSeconds"] = 2
+    await f.client.create("pods", p, f.ns)
+
+    async def failed():
+        got = await f.client.get("pods", "deadline", f.ns)
+        st = got.get("status") or {}
+        return got if st.get("phase") == "Failed" else None
+    got = await f.wait(failed, 30, "phase Failed")
+    assert got["status"].get("reason") == "DeadlineExceeded", got["status"]

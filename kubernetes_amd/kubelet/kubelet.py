@@ -54,7 +54,7 @@ BOOTSTRAP_CHECKPOINT = "node.kubernetes.io/bootstrap-checkpoint"
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
                  "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
-                 "waiting", "net_mounts", "net_setup", "previous", "backoff", "adopted")
+                 "waiting", "net_mounts", "net_setup", "previous", "backoff", "adopted", "deadline_armed")
 
     def __init__(self, pod):
         self.uid = pod["metadata"]["uid"]
@@ -80,6 +80,7 @@ class PodState:
         self.previous: dict[str, str] = {}    # container name -> last dead instance (logs --previous)
         self.backoff: dict[str, list] = {}    # container name -> [next restart allowed at, current delay]
         self.adopted = False                  # sandbox/containers found in the runtime after a kubelet restart
+        self.deadline_armed = False           # a resync is scheduled at spec.activeDeadlineSeconds
 
 
 def _field_path(pod, c):
@@ -719,7 +720,31 @@ class Kubelet:
                 return
             st.admitted = True
             st.start_time = now_rfc3339()
+        if await self._enforce_active_deadline(st):
+            return
         await self._sync_containers(st)
+
+    async def _enforce_active_deadline(self, st: PodState) -> bool:
+        """`pkg/kubelet/active_deadline.go`: a pod active on the node longer than
+        spec.activeDeadlineSeconds (counted from status.startTime) is killed and fails with reason
+        DeadlineExceeded. Before the deadline a resync is armed for the moment it passes."""
+        ads = (st.pod.get("spec") or {}).get("activeDeadlineSeconds")
+        start = parse_rfc3339(st.start_time) if st.start_time else None
+        if ads is None or start is None:
+            return False
+        left = start + float(ads) - time.time()
+        if left > 0:
+            if not st.deadline_armed:
+                st.deadline_armed = True
+                asyncio.get_running_loop().call_later(left + 0.01, self._resync, st.uid)
+            return False
+        msg = "Pod was active on the node longer than the specified deadline"
+        st.rejected = "DeadlineExceeded"
+        self.recorder.event(st.pod, "Normal", "DeadlineExceeded", msg)
+        await self._kill_pod(st, 0)
+        await self._write_status(st, {"phase": core.POD_FAILED, "reason": "DeadlineExceeded", "message": msg,
+                                      "conditions": (st.pod.get("status") or {}).get("conditions") or []})
+        return True
 
     async def _sync_containers(self, st: PodState):
         pod = st.pod
