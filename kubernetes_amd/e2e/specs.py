@@ -616,3 +616,13 @@ async def active_deadline(f):
         return got if st.get("phase") == "Failed" else None
     got = await f.wait(failed, 30, "phase Failed")
     assert got["status"].get("reason") == "DeadlineExceeded", got["status"]
+
+
+@conformance("Container Runtime should report the log tail as termination message with FallbackToLogsOnError")
+async def termination_message_from_logs(f):
+    p = _pod("termmsg", "echo DONE-FAILING; exit 3")
+    p["spec"]["containers"][0]["terminationMessagePolicy"] = "FallbackToLogsOnError"
+    await f.client.create("pods", p, f.ns)
+    got = await f.pod_phase("termmsg", ("Failed",))
+    term = got["status"]["containerStatuses"][0]["state"]["terminated"]
+    assert term["exitCode"] == 3 and "DONE-FAILING" in term.get("message", ""), term

@@ -1478,8 +1478,27 @@ def _container_status(c, cs, restarts, waiting=None):
         s["state"] = {"terminated": {"exitCode": cs.exit_code, "reason": cs.reason or ("Completed" if cs.exit_code == 0 else "Error"),
                                      "startedAt": _ts(cs.started_at), "finishedAt": _ts(cs.finished_at),
                                      "containerID": cs.id}}
-        if cs.message:
-            s["state"]["terminated"]["message"] = cs.message
+        msg = cs.message
+        if not msg and cs.exit_code and c.get("terminationMessagePolicy") == "FallbackToLogsOnError":
+            msg = _log_tail(getattr(cs, "log_path", ""))
+        if msg:
+            s["state"]["terminated"]["message"] = msg
     else:
         s["state"] = {"waiting": {"reason": "ContainerCreating"}}
     return s
+
+
+def _log_tail(path, max_bytes=2048, max_lines=80):
+    """`kuberuntime_container.go` FallbackToLogsOnError: the last 80 lines / 2 KiB of the log of a
+    container that failed without writing a termination message."""
+    if not path:
+        return ""
+    try:
+        with open(path, "rb") as f:
+            f.seek(0, os.SEEK_END)
+            size = f.tell()
+            f.seek(max(0, size - max_bytes))
+            data = f.read()
+    except OSError:
+        return ""
+    return "\n".join(data.decode(errors="replace").splitlines()[-max_lines:])
