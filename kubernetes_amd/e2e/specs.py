@@ -626,3 +626,32 @@ async def termination_message_from_logs(f):
     got = await f.pod_phase("termmsg", ("Failed",))
     term = got["status"]["containerStatuses"][0]["state"]["terminated"]
     assert term["exitCode"] == 3 and "DONE-FAILING" in term.get("message", ""), term
+
+
+@conformance("Security Context should run the container as securityContext.runAsUser")
+async def security_context_run_as_user(f):
+    import os
+    uid = 65534 if os.geteuid() == 0 else os.geteuid()    # a non-root kubelet may only keep its own uid
+    p = _pod("runas", "id -u")
+    p["spec"]["securityContext"] = {"runAsUser": 0}
+    p["spec"]["containers"][0]["securityContext"] = {"runAsUser": uid}   # the container's wins
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("runas", ("Succeeded",))
+    assert (await f.logs("runas")).strip() == str(uid)
+
+
+@conformance("Security Context should refuse runAsNonRoot with runAsUser 0")
+async def security_context_non_root(f):
+    p = _pod("nonroot", "true")
+    p["spec"]["containers"][0]["securityContext"] = {"runAsNonRoot": True, "runAsUser": 0}
+    await f.client.create("pods", p, f.ns)
+
+    async def refused():
+        got = await f.client.get("pods", "nonroot", f.ns)
+        for cs in (got.get("status") or {}).get("containerStatuses") or ():
+            w = (cs.get("state") or {}).get("waiting") or {}
+            if w.get("reason") == "CreateContainerConfigError":
+                return w
+        return None
+    w = await f.wait(refused, 30, "CreateContainerConfigError")
+    assert "non-root" in w.get("message", ""), w

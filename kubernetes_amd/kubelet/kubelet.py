@@ -917,6 +917,13 @@ class Kubelet:
             return None
         spec_c = c
         opts.attempt = st.restarts.get(c["name"], 0)
+        err = _apply_security_context(st.pod, c, opts)
+        if err:
+            # kuberuntime_container.go: verifyRunAsNonRoot fails the start with CreateContainerConfigError
+            st.waiting[c["name"]] = ("CreateContainerConfigError", err)
+            self.recorder.event(st.pod, "Warning", "Failed", f"Error: {err}", field_path=_field_path(st.pod, c))
+            await self._report(st)
+            return None
         opts.mounts.extend(st.net_mounts)
         opts.oom_score_adj = oom_score_adj(st.pod, c, parse_quantity(self.capacity["memory"]).value)
         if self.cgroups is not None:
@@ -1486,6 +1493,27 @@ def _container_status(c, cs, restarts, waiting=None):
     else:
         s["state"] = {"waiting": {"reason": "ContainerCreating"}}
     return s
+
+
+def _apply_security_context(pod, c, opts):
+    """`pkg/kubelet/kuberuntime/security_context.go`: the container's securityContext overrides the
+    pod's; runAsUser becomes the process identity (container-init setuid), the pod's fsGroup its
+    primary group, and runAsNonRoot is verified (`verifyRunAsNonRoot`). Returns an error string."""
+    psc = (pod.get("spec") or {}).get("securityContext") or {}
+    csc = c.get("securityContext") or {}
+    uid = csc.get("runAsUser", psc.get("runAsUser"))
+    non_root = csc.get("runAsNonRoot", psc.get("runAsNonRoot"))
+    if uid is not None:
+        opts.run_as_user = int(uid)
+    if psc.get("fsGroup") is not None:
+        opts.run_as_group = int(psc["fsGroup"])
+    if non_root:
+        if uid is not None and int(uid) == 0:
+            return "container's runAsUser breaks non-root policy"
+        if uid is None and os.geteuid() == 0:
+            # no image metadata here: the entrypoint would inherit the runtime's (root) identity
+            return "container has runAsNonRoot and image will run as root"
+    return ""
 
 
 def _log_tail(path, max_bytes=2048, max_lines=80):

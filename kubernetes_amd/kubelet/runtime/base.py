@@ -23,6 +23,8 @@ class RunContainerOptions:
     oom_score_adj: int | None = None                  # qos.oom_score_adj (CRI LinuxContainerResources)
     cgroup_parent: str | None = None                  # pod cgroup directory (cgroups.CgroupManager)
     attempt: int = 0                                  # restart count (CRI ContainerMetadata.attempt)
+    run_as_user: int | None = None                    # securityContext.runAsUser (CRI LinuxContainerSecurityContext)
+    run_as_group: int | None = None                   # primary group: fsGroup of the pod
 
     @classmethod
     def from_device_opts(cls, d):

@@ -127,7 +127,7 @@ def resolve_command(container):
 CONTAINER_INIT = os.path.join(BIN_DIR, "container-init")
 
 
-def _init_argv(argv, env, cpus, oom_adj, cgroup):
+def _init_argv(argv, env, cpus, oom_adj, cgroup, uid=None, gid=None):
     """Prefix argv with the native container-init helper (native/pause/container_init.cc), which
     applies the cpuset, OOM score and cgroup and then execs the entrypoint — so the spawn needs
     no Python pre-exec hook and can use vfork (a hook forces a full fork of the kubelet: ~3 ms
@@ -147,6 +147,10 @@ def _init_argv(argv, env, cpus, oom_adj, cgroup):
         pre += ["-o", str(int(oom_adj))]
     if cgroup:
         pre += ["-g", cgroup]
+    if gid is not None:
+        pre += ["-G", str(int(gid))]
+    if uid is not None:
+        pre += ["-u", str(int(uid))]
     return pre + ["--"] + list(argv)
 
 
@@ -322,7 +326,7 @@ class ProcessRuntime(Runtime):
         self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "argv": argv, "env": env,
                           "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec,
                           "oom_score_adj": opts.oom_score_adj, "cgroup": opts.cgroup_parent,
-                          "attempt": opts.attempt}
+                          "attempt": opts.attempt, "run_as_user": opts.run_as_user, "run_as_group": opts.run_as_group}
         return cid
 
     @staticmethod
@@ -341,9 +345,13 @@ class ProcessRuntime(Runtime):
         pre = None
         argv = m["argv"]
         try:
-            if cpus or m.get("oom_score_adj") is not None or m.get("cgroup"):
+            identity = m.get("run_as_user") is not None or m.get("run_as_group") is not None
+            if identity and not os.access(CONTAINER_INIT, os.X_OK):
+                raise OSError(1, "runAsUser needs the container-init helper (python -m kubernetes_amd.native.build)")
+            if cpus or m.get("oom_score_adj") is not None or m.get("cgroup") or identity:
                 if os.access(CONTAINER_INIT, os.X_OK):
-                    argv = _init_argv(argv, m["env"], cpus, m.get("oom_score_adj"), m.get("cgroup"))
+                    argv = _init_argv(argv, m["env"], cpus, m.get("oom_score_adj"), m.get("cgroup"),
+                                      m.get("run_as_user"), m.get("run_as_group"))
                 else:
                     pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
             proc = await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=m["cwd"], stdout=log,

@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <grp.h>
 #include <unistd.h>
 
 static int parse_cpus(const char* s, cpu_set_t* set) {
@@ -52,6 +53,8 @@ int main(int argc, char** argv) {
   const char* cpus = nullptr;
   const char* oom = nullptr;
   const char* cgroup = nullptr;
+  const char* uid = nullptr;   // securityContext.runAsUser
+  const char* gid = nullptr;   // primary group (runAsGroup / fsGroup)
   int i = 1;
   for (; i < argc; ++i) {
     if (strcmp(argv[i], "--") == 0) { ++i; break; }
@@ -59,6 +62,8 @@ int main(int argc, char** argv) {
     if (strcmp(argv[i], "-c") == 0) cpus = argv[++i];
     else if (strcmp(argv[i], "-o") == 0) oom = argv[++i];
     else if (strcmp(argv[i], "-g") == 0) cgroup = argv[++i];
+    else if (strcmp(argv[i], "-u") == 0) uid = argv[++i];
+    else if (strcmp(argv[i], "-G") == 0) gid = argv[++i];
     else { fprintf(stderr, "container-init: unknown option %s\n", argv[i]); return 126; }
   }
   if (i >= argc) { fprintf(stderr, "container-init: no command\n"); return 126; }
@@ -71,6 +76,19 @@ int main(int argc, char** argv) {
   if (cgroup && *cgroup) {
     char path[4096];
     if (snprintf(path, sizeof path, "%s/cgroup.procs", cgroup) < (int)sizeof path) write_file(path, "0", O_CREAT | O_TRUNC);
+  }
+  // identity last: the cgroup / OOM writes above may need the kubelet's privileges. Group before
+  // user (setuid drops the right to setgid); supplementary groups are dropped when we can.
+  if ((gid && *gid) || (uid && *uid)) {
+    if (geteuid() == 0) setgroups(0, nullptr);
+    if (gid && *gid && setgid((gid_t)strtoul(gid, nullptr, 10)) != 0) {
+      perror("container-init: setgid");
+      return 126;
+    }
+    if (uid && *uid && setuid((uid_t)strtoul(uid, nullptr, 10)) != 0) {
+      perror("container-init: setuid");
+      return 126;
+    }
   }
   execvp(argv[i], argv + i);
   fprintf(stderr, "container-init: exec %s: %s\n", argv[i], strerror(errno));
