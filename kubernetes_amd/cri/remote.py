@@ -151,8 +151,12 @@ class RemoteRuntime(Runtime):
             devices=[A.MSG["Device"](container_path=d.get("pathInContainer", ""), host_path=d.get("pathOnHost", ""),
                                      permissions=d.get("permissions", "rwm")) for d in opts.devices],
             labels=labels, annotations=ann, log_path=f"{container['name']}/0.log",
-            linux=A.MSG["LinuxContainerConfig"](resources=A.MSG["LinuxContainerResources"](
-                oom_score_adj=opts.oom_score_adj or 0)))
+            linux=A.MSG["LinuxContainerConfig"](
+                resources=A.MSG["LinuxContainerResources"](oom_score_adj=opts.oom_score_adj or 0),
+                security_context=A.MSG["LinuxContainerSecurityContext"](
+                    # securityContext.runAsUser; the pod's fsGroup travels as the first supplemental group
+                    run_as_user=(A.MSG["Int64Value"](value=opts.run_as_user) if opts.run_as_user is not None else None),
+                    supplemental_groups=[opts.run_as_group] if opts.run_as_group is not None else [])))
         r = await self._call("CreateContainer", A.MSG["CreateContainerRequest"](
             pod_sandbox_id=sid, config=cfg, sandbox_config=self._sandbox_config(pod, {})))
         st = ContainerStatus(r.container_id, container["name"], CREATED, image=container.get("image", ""))

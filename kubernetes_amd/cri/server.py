@@ -404,10 +404,13 @@ class CRIServer:
             container["env"] = [{"name": kv.key, "value": kv.value} for kv in c.envs]
             envs = []
         res = c.linux.resources if c.HasField("linux") else None
+        sc = c.linux.security_context if c.HasField("linux") and c.linux.HasField("security_context") else None
         opts = RunContainerOptions(envs=envs, devices=devices, mounts=mounts,
                                    annotations=[{"name": k, "value": v} for k, v in ann.items()],
                                    oom_score_adj=(res.oom_score_adj if res is not None and res.oom_score_adj else None),
-                                   cgroup_parent=ann.get(A.CGROUP_PARENT_ANNOTATION))
+                                   cgroup_parent=ann.get(A.CGROUP_PARENT_ANNOTATION),
+                                   run_as_user=(sc.run_as_user.value if sc is not None and sc.HasField("run_as_user") else None),
+                                   run_as_group=(sc.supplemental_groups[0] if sc is not None and sc.supplemental_groups else None))
         try:
             cid = await self.rt.create_container(req.pod_sandbox_id, sb["pod"], container, opts)
         except (FileNotFoundError, OSError, ValueError) as e:

@@ -284,3 +284,30 @@ def test_kubelet_restart_adopts_pods_over_cri(run, tmp_path):
                 await rt2.close()
             await srv.stop()
     run(main(), timeout=60)
+
+
+def test_run_as_user_over_cri(run, tmp_path):
+    """securityContext.runAsUser travels in CRI LinuxContainerSecurityContext and the process
+    runtime's container-init takes that identity before exec."""
+    import os
+
+    async def main():
+        sock = str(tmp_path / "cri.sock")
+        srv = await CRIServer(ProcessRuntime(str(tmp_path / "rt")), sock).start()
+        rt = await RemoteRuntime(sock, relist_period=0.05).connect()
+        uid = 65534 if os.geteuid() == 0 else os.geteuid()
+        try:
+            p = pod()
+            sid = await rt.run_pod_sandbox(p, {})
+            cid = await rt.create_container(sid, p, {"name": "c", "image": "busybox", "command": ["sh", "-c", "id -u"]},
+                                            RunContainerOptions(run_as_user=uid))
+            await rt.start_container(cid)
+            for _ in range(100):
+                if rt.container_status(cid).state == EXITED:
+                    break
+                await asyncio.sleep(0.05)
+            assert (await rt.container_logs(cid)).strip() == str(uid).encode()
+        finally:
+            await rt.close()
+            await srv.stop()
+    run(main())
