@@ -31,7 +31,7 @@ class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
                  health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None,
-                 partition="SPX", burn_in=None):
+                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
@@ -39,6 +39,8 @@ class LocalCluster:
         self.hives = hives
         self.partition = partition             # fake backend: SPX/DPX/QPX/CPX compute partitions
         self.burn_in = burn_in                 # deviceplugin.burnin.BurnIn: gate GPUs on the HIP acceptance test
+        self.dev_root = dev_root               # where the plugin finds /dev/kfd + /dev/dri (tests: mknod'd nodes)
+        self.isolation = isolation             # process runtime: "auto" | "required" | "off"
         self.own_dir = workdir is None
         self.dir = workdir or tempfile.mkdtemp(prefix="kamd-cluster-")
         self.emit_events = emit_events
@@ -87,7 +89,7 @@ class LocalCluster:
         if runtime is not None:
             rt = runtime
         elif self.runtime_kind == "process":
-            rt = ProcessRuntime(os.path.join(ndir, "runtime"))
+            rt = ProcessRuntime(os.path.join(ndir, "runtime"), isolation=self.isolation)
         else:
             rt = StubRuntime(payload=self.payload)
         kl = Kubelet(Client(self.url), name, rt, dm, emit_events=self.emit_events,
@@ -97,7 +99,7 @@ class LocalCluster:
         await kl.run()
         if self.gpus:
             plugin = AMDGPUPlugin(plugins_dir, smi=self.smi, health_interval=self.health_interval,
-                                  rocm_mount=self.rocm_mount, burn_in=self.burn_in)
+                                  rocm_mount=self.rocm_mount, burn_in=self.burn_in, dev_root=self.dev_root)
             await plugin.start()
         h = NodeHandle(name, kl, plugin, dm, rt, plugins_dir)
         self.nodes.append(h)
@@ -150,6 +152,10 @@ class LocalCluster:
             if n.plugin:
                 await n.plugin.stop()
             await n.kubelet.stop()
+            if hasattr(n.runtime, "kill_all"):
+                # the kubelet leaves containers running across its own restarts (adoption); a
+                # torn-down cluster must not leave them behind
+                await n.runtime.kill_all()
         if self.scheduler:
             await self.scheduler.stop()
         if self._sched_task:

@@ -195,3 +195,7 @@ CONTAINER_NAME = "io.kubernetes.container.name"
 POD_SPEC_ANNOTATION = "kubernetes-amd.io/pod"
 CONTAINER_SPEC_ANNOTATION = "kubernetes-amd.io/container"
 CGROUP_PARENT_ANNOTATION = "kubernetes-amd.io/cgroup-parent"   # pod cgroup (runtime joins it)
+# CRI v1alpha1 has no runAsGroup (added in later CRI versions): carried as an annotation
+RUN_AS_GROUP_ANNOTATION = "kamd.io/run-as-group"
+# RuntimeStatus condition: whether containers get a private /dev + device cgroup
+DEVICE_ISOLATION_CONDITION = "DeviceIsolation"

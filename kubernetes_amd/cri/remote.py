@@ -57,6 +57,10 @@ class RemoteRuntime(Runtime):
         self._relist_task = None
         self.relists = 0
         self.runtime_name = "remote"
+        self._isolation = None
+
+    def isolation_status(self):
+        return self._isolation
 
     async def connect(self):
         if self.channel is None:
@@ -65,6 +69,10 @@ class RemoteRuntime(Runtime):
             self.images = RemoteImageService(_Stub(self.channel, A.IMAGE_SERVICE, A.IMAGE_METHODS), self.timeout)
             v = await self.rs.Version(A.MSG["VersionRequest"](version="0.1.0"), timeout=self.timeout)
             self.runtime_name = v.runtime_name
+            st = await self.rs.Status(A.MSG["StatusRequest"](), timeout=self.timeout)
+            for c in st.status.conditions:
+                if c.type == A.DEVICE_ISOLATION_CONDITION:
+                    self._isolation = {"enforced": c.status, "reason": c.reason, "message": c.message}
             if self.relist_period and self._relist_task is None:
                 self._relist_task = asyncio.ensure_future(self._relist_loop())
         return self
@@ -139,6 +147,8 @@ class RemoteRuntime(Runtime):
         ann[A.CONTAINER_SPEC_ANNOTATION] = json.dumps(container, separators=(",", ":"))
         if opts.cgroup_parent:
             ann[A.CGROUP_PARENT_ANNOTATION] = opts.cgroup_parent
+        if opts.run_as_group is not None:
+            ann[A.RUN_AS_GROUP_ANNOTATION] = str(int(opts.run_as_group))
         labels = {A.POD_NAME: md.get("name", ""), A.POD_NAMESPACE: md.get("namespace", ""),
                   A.POD_UID: md.get("uid", ""), A.CONTAINER_NAME: container["name"]}
         cfg = A.MSG["ContainerConfig"](
@@ -154,9 +164,12 @@ class RemoteRuntime(Runtime):
             linux=A.MSG["LinuxContainerConfig"](
                 resources=A.MSG["LinuxContainerResources"](oom_score_adj=opts.oom_score_adj or 0),
                 security_context=A.MSG["LinuxContainerSecurityContext"](
-                    # securityContext.runAsUser; the pod's fsGroup travels as the first supplemental group
+                    # securityContext.runAsUser; the pod's fsGroup + supplementalGroups as supplemental groups
                     run_as_user=(A.MSG["Int64Value"](value=opts.run_as_user) if opts.run_as_user is not None else None),
-                    supplemental_groups=[opts.run_as_group] if opts.run_as_group is not None else [])))
+                    supplemental_groups=list(opts.supplemental_groups), privileged=bool(opts.privileged),
+                    readonly_rootfs=bool(opts.readonly_rootfs),
+                    capabilities=(A.MSG["Capability"](add_capabilities=list(opts.cap_add), drop_capabilities=list(opts.cap_drop))
+                                  if opts.cap_add or opts.cap_drop else None))))
         r = await self._call("CreateContainer", A.MSG["CreateContainerRequest"](
             pod_sandbox_id=sid, config=cfg, sandbox_config=self._sandbox_config(pod, {})))
         st = ContainerStatus(r.container_id, container["name"], CREATED, image=container.get("image", ""))

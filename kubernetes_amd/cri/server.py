@@ -294,6 +294,8 @@ class CRIServer:
         if os.path.exists(self.path):
             os.unlink(self.path)
         self._restore_checkpoints()
+        if hasattr(self.rt, "start"):
+            await self.rt.start()          # watch the containers re-adopted after a restart
         await self.streaming.start()
         self.server = grpc.aio.server()
         self.server.add_generic_rpc_handlers((generic_handler(A.RUNTIME_SERVICE, A.RUNTIME_METHODS, self),
@@ -410,7 +412,12 @@ class CRIServer:
                                    oom_score_adj=(res.oom_score_adj if res is not None and res.oom_score_adj else None),
                                    cgroup_parent=ann.get(A.CGROUP_PARENT_ANNOTATION),
                                    run_as_user=(sc.run_as_user.value if sc is not None and sc.HasField("run_as_user") else None),
-                                   run_as_group=(sc.supplemental_groups[0] if sc is not None and sc.supplemental_groups else None))
+                                   run_as_group=(int(ann[A.RUN_AS_GROUP_ANNOTATION]) if A.RUN_AS_GROUP_ANNOTATION in ann else None),
+                                   supplemental_groups=list(sc.supplemental_groups) if sc is not None else [],
+                                   privileged=bool(sc is not None and sc.privileged),
+                                   cap_add=list(sc.capabilities.add_capabilities) if sc is not None and sc.HasField("capabilities") else [],
+                                   cap_drop=list(sc.capabilities.drop_capabilities) if sc is not None and sc.HasField("capabilities") else [],
+                                   readonly_rootfs=bool(sc is not None and sc.readonly_rootfs))
         try:
             cid = await self.rt.create_container(req.pod_sandbox_id, sb["pod"], container, opts)
         except (FileNotFoundError, OSError, ValueError) as e:
@@ -534,6 +541,12 @@ class CRIServer:
     async def Status(self, req, ctx):
         conds = [A.MSG["RuntimeCondition"](type="RuntimeReady", status=True),
                  A.MSG["RuntimeCondition"](type="NetworkReady", status=True)]
+        iso = self.rt.isolation_status()
+        if iso is not None:
+            # not a CRI v1alpha1 condition: how the kubelet learns whether the runtime enforces
+            # the device view it asked for (node condition IsolationUnavailable)
+            conds.append(A.MSG["RuntimeCondition"](type=A.DEVICE_ISOLATION_CONDITION, status=bool(iso["enforced"]),
+                                                   reason=iso["reason"], message=iso["message"]))
         return A.MSG["StatusResponse"](status=A.MSG["RuntimeStatus"](conditions=conds))
 
     # ---------------------------------------------------------------- image service

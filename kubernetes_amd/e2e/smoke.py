@@ -5,12 +5,19 @@ DeviceManager → real amd.com/gpu plugin on AMD SMI (InitContainer: /dev/kfd + 
 runtime runs `hip-vector-add` (gfx950 kernel) on the allocated GPU → pod Succeeded,
 log says "Test PASSED" (the reference's cuda-vector-add e2e check,
 test/e2e/scheduling/nvidia-gpus.go:51-113).
+
+The pod's own view is checked, not only the bundle: HIP inside the pod enumerates exactly the
+allocated GPU(s). With enforced isolation (kamd-runc: private /dev) the pod's /dev/dri holds
+only its render node and HIP_VISIBLE_DEVICES is unset; on a node that cannot isolate (an
+unprivileged kubelet without user namespaces, e.g. the GPU CI box) the node must carry
+IsolationUnavailable=True and the runtime narrows HIP with HIP_VISIBLE_DEVICES instead.
 """
 from __future__ import annotations
 
 import asyncio
 import json
 import os
+import re
 
 from ..api import core
 from ..cluster import LocalCluster
@@ -52,6 +59,34 @@ async def gpu_pod_e2e(timeout=120, cri=False):
                       p["spec"]["extendedResources"][0]["assigned"][0]]["attributes"]}
         assert "Test PASSED" in logs, logs
         assert "/dev/kfd" in paths and any(x.startswith("/dev/dri/renderD") for x in paths), paths
+        m = re.search(r"(\d+) visible device", logs)
+        result["hip_visible_devices_in_pod"] = int(m.group(1)) if m else None
+        assert result["hip_visible_devices_in_pod"] == 1, logs
+        # what the pod's process sees of /dev and its environment
+        view = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "dev-view", "namespace": "default"},
+                "spec": {"restartPolicy": "Never",
+                         "containers": [{"name": "v", "image": "busybox",
+                                         "command": ["/bin/sh", "-c", "echo DRI=$(ls /dev/dri | tr '\\n' ' '); "
+                                                     "echo HIP=${HIP_VISIBLE_DEVICES-unset}"],
+                                         "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
+        await cl.client.create("pods", view)
+        pv = await cl.wait_pod("dev-view", phase="Succeeded", timeout=timeout)
+        vcs = [c for c in rt.list_containers() if c.name == "v"][0]
+        vlog = open(vcs.log_path).read()
+        node = await cl.client.get("nodes", cl.nodes[0].name)
+        cond = {c["type"]: c for c in node["status"]["conditions"]}.get("IsolationUnavailable")
+        iso = rt.isolation_status()
+        result["isolation"] = iso
+        result["dev_view"] = vlog.strip()
+        assert cond is not None and cond["status"] == ("False" if iso["enforced"] else "True"), cond
+        minor = node["status"]["extendedResources"][core.AMD_GPU]["resources"][
+            pv["spec"]["extendedResources"][0]["assigned"][0]]["attributes"].get(core.ATTR_RENDER_MINOR)
+        dri = vlog.split("DRI=", 1)[1].split("\n", 1)[0].split()
+        if iso["enforced"]:
+            assert dri == [f"renderD{minor}"], vlog
+            assert "HIP=unset" in vlog, vlog
+        else:
+            assert "HIP=unset" not in vlog and "HIP=-1" not in vlog, vlog
         if cri:
             await rt_remote.close()
             await srv.stop()

@@ -13,8 +13,10 @@ Hierarchy under the kubelet's cgroup root (cgroup v2 file names):
 A pod cgroup carries `ResourceConfigForPod`: cpu shares from the summed cpu requests (min 2),
 a cpu quota only when every container has a cpu limit (period 100 ms, min 1 ms), and a memory
 limit only when every container has one; BestEffort pods get the minimum shares. Shares are
-written as cgroup v2 weights (`1 + (shares-2)*9999/262142`, the runc conversion). Container
-processes join their pod's cgroup (`cgroup.procs`).
+written as cgroup v2 weights (`1 + (shares-2)*9999/262142`, the runc conversion). Each container
+runs in its own leaf `<pod>/ctr-<id>/` created by the runtime (container-init / kamd-runc): cgroup
+v2's no-internal-process rule forbids processes in the pod cgroup once it delegates cpu and memory
+to its children, so the pod cgroup never holds a process itself.
 
 `root` can be a real delegated cgroup v2 directory (the kubelet then enables the cpu and
 memory controllers for its children) or any directory (tests, or hosts where the kubelet may not
@@ -178,6 +180,16 @@ class CgroupManager:
             return
         q, d, _ = ent
         if self.real:
+            # container cgroups (leaves the runtime created under the pod) go first
+            try:
+                for name in os.listdir(d):
+                    if name.startswith("ctr-") and os.path.isdir(os.path.join(d, name)):
+                        try:
+                            os.rmdir(os.path.join(d, name))
+                        except OSError as e:
+                            log.warning("removing container cgroup %s/%s: %s", d, name, e)
+            except OSError:
+                pass
             try:
                 os.rmdir(d)          # a cgroup directory is removed with rmdir once empty
             except OSError as e:

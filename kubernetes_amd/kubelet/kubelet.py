@@ -212,6 +212,7 @@ class Kubelet:
         self.informer_node_labels = {}
         self._stopped = False
         self.smi = None   # set by the node agent when the real/fake AMD SMI is available (stats)
+        self.isolation = None   # runtime.isolation_status(): node condition IsolationUnavailable
 
     # ------------------------------------------------------------------
     # lifecycle
@@ -238,6 +239,12 @@ class Kubelet:
             restored = self._restore_checkpointed_pods()
             if restored:
                 log.info("started %d pods from bootstrap checkpoints", restored)
+        if hasattr(self.runtime, "start"):
+            await self.runtime.start()
+        self.isolation = self.runtime.isolation_status()
+        if self.isolation is not None and not self.isolation["enforced"]:
+            log.warning("%s: %s", self.isolation["reason"], self.isolation["message"])
+            self._status_dirty.set()
         try:
             # kubelet restart: what the runtime still runs is adopted, not started again
             self._adoptable = await self.runtime.pod_states()
@@ -365,6 +372,13 @@ class Kubelet:
                            "operatingSystem": "linux", "architecture": "amd64", "machineID": self.node_name}}
         if self.dynamic is not None:
             st["conditions"].append(dict(self.dynamic.condition, lastHeartbeatTime=now, lastTransitionTime=now))
+        iso = getattr(self, "isolation", None)
+        if iso is not None:
+            # a node whose runtime cannot give pods a private /dev says so instead of letting GPU
+            # pods silently share every render node of the host
+            st["conditions"].append({"type": "IsolationUnavailable", "status": "False" if iso["enforced"] else "True",
+                                     "reason": iso["reason"], "message": iso["message"],
+                                     "lastHeartbeatTime": now, "lastTransitionTime": now})
         if ers:
             st["extendedResources"] = ers
         return st
@@ -638,6 +652,9 @@ class Kubelet:
         st = self.pods.get(victim["metadata"]["uid"])
         if st is None:
             return
+        # before the kill: the victim's container exits re-dispatch its sync, which must neither
+        # restart them nor report the pod live again
+        st.rejected = status.get("reason") or "Preempting"
         await self._kill_pod(st, 0)
         st.terminated = True
         await self._write_status(st, dict(status, conditions=(victim.get("status") or {}).get("conditions") or []))
@@ -719,7 +736,9 @@ class Kubelet:
                                               "conditions": (pod.get("status") or {}).get("conditions") or []})
                 return
             st.admitted = True
-            st.start_time = now_rfc3339()
+            # an adopted pod (kubelet restart) keeps its status.startTime: activeDeadlineSeconds
+            # counts from it (active_deadline.go)
+            st.start_time = st.start_time or now_rfc3339()
         if await self._enforce_active_deadline(st):
             return
         await self._sync_containers(st)
@@ -1497,16 +1516,28 @@ def _container_status(c, cs, restarts, waiting=None):
 
 def _apply_security_context(pod, c, opts):
     """`pkg/kubelet/kuberuntime/security_context.go`: the container's securityContext overrides the
-    pod's; runAsUser becomes the process identity (container-init setuid), the pod's fsGroup its
-    primary group, and runAsNonRoot is verified (`verifyRunAsNonRoot`). Returns an error string."""
+    pod's. runAsUser / runAsGroup become the process identity; the pod's fsGroup and
+    supplementalGroups are supplemental groups (security_context.go:58-66), never the primary
+    group; privileged, capabilities and readOnlyRootFilesystem go to the runtime; runAsNonRoot is
+    verified (`verifyRunAsNonRoot`). Returns an error string."""
     psc = (pod.get("spec") or {}).get("securityContext") or {}
     csc = c.get("securityContext") or {}
     uid = csc.get("runAsUser", psc.get("runAsUser"))
+    gid = csc.get("runAsGroup", psc.get("runAsGroup"))
     non_root = csc.get("runAsNonRoot", psc.get("runAsNonRoot"))
     if uid is not None:
         opts.run_as_user = int(uid)
-    if psc.get("fsGroup") is not None:
-        opts.run_as_group = int(psc["fsGroup"])
+    if gid is not None:
+        opts.run_as_group = int(gid)
+    groups = [int(g) for g in psc.get("supplementalGroups") or ()]
+    if psc.get("fsGroup") is not None and int(psc["fsGroup"]) not in groups:
+        groups.append(int(psc["fsGroup"]))
+    opts.supplemental_groups = groups
+    opts.privileged = bool(csc.get("privileged"))
+    caps = csc.get("capabilities") or {}
+    opts.cap_add = list(caps.get("add") or ())
+    opts.cap_drop = list(caps.get("drop") or ())
+    opts.readonly_rootfs = bool(csc.get("readOnlyRootFilesystem"))
     if non_root:
         if uid is not None and int(uid) == 0:
             return "container's runAsUser breaks non-root policy"

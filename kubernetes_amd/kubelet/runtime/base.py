@@ -24,7 +24,12 @@ class RunContainerOptions:
     cgroup_parent: str | None = None                  # pod cgroup directory (cgroups.CgroupManager)
     attempt: int = 0                                  # restart count (CRI ContainerMetadata.attempt)
     run_as_user: int | None = None                    # securityContext.runAsUser (CRI LinuxContainerSecurityContext)
-    run_as_group: int | None = None                   # primary group: fsGroup of the pod
+    run_as_group: int | None = None                   # securityContext.runAsGroup: the primary group
+    supplemental_groups: list = field(default_factory=list)   # pod fsGroup + supplementalGroups
+    privileged: bool = False                          # securityContext.privileged: host /dev, all caps
+    cap_add: list = field(default_factory=list)       # securityContext.capabilities.add ("NET_ADMIN", ...)
+    cap_drop: list = field(default_factory=list)
+    readonly_rootfs: bool = False                     # securityContext.readOnlyRootFilesystem
 
     @classmethod
     def from_device_opts(cls, d):
@@ -104,6 +109,12 @@ class Runtime:
 
     def list_containers(self):
         return []
+
+    def isolation_status(self) -> dict | None:
+        """Whether the runtime enforces a container's device view (mount namespace + private /dev
+        + device cgroup): {"enforced": bool, "reason": str, "message": str}. None = not applicable
+        (containers are not real processes, e.g. the kubemark stub runtime)."""
+        return None
 
     async def pod_states(self) -> dict:
         """What survives a kubelet restart (kuberuntime `GetPods`): pod uid -> {"sandboxes":

@@ -1,22 +1,30 @@
 """Process runtime — runs containers as host child processes (no docker/containerd in this image).
 
-  * sandbox  = the native `pause` binary (native/pause/pause.cc) in its own session, holding the
-               pod's lifetime like the pause container of a docker sandbox;
-  * container = `command + args` as a child process in its own process group, stdout/stderr to
-               `<root>/containers/<id>/log`; an OCI `config.json` with the injected GPU devices
-               is written into the container bundle (`runtime/oci.py`) for audit/OCI runtimes;
+  * sandbox  = the native `pause` binary (native/pause/pause.cc), holding the pod's lifetime like
+               the pause container of a docker sandbox; with isolation it also holds the pod's
+               shared ipc + uts (and, unprivileged, user) namespaces that its containers join;
+  * container = `command + args`, stdout/stderr to `<root>/containers/<id>/log`, described by an
+               OCI bundle (`config.json`, `runtime/oci.py`) holding the injected GPU devices;
+  * isolation = when the host allows it (`kamd-runc features`), the bundle is EXECUTED by the
+               native OCI executor `kamd-runc` (native/runc/kamd_runc.cc): private mount / pid /
+               ipc / uts namespaces, a tmpfs `/dev` holding only the default nodes plus the
+               allocated `/dev/kfd` + `/dev/dri/renderD<minor>`, and a cgroup device filter
+               (v2 BPF or v1 devices.allow) — a pod cannot reach a render node it was not given,
+               whatever HIP_VISIBLE_DEVICES says. Where namespaces are not allowed (an
+               unprivileged kubelet on a host without user namespaces) the runtime says so
+               (`isolation_status()` → node condition IsolationUnavailable) and falls back to
+               narrowing HIP enumeration with HIP_VISIBLE_DEVICES; `isolation="required"` refuses
+               device containers instead;
   * images   = a local image map (`IMAGES`) resolves well-known images to built executables,
-               e.g. `kubernetes-amd/hip-vector-add` → native/bin/hip-vector-add;
-  * GPUs     = without device namespaces the runtime narrows HIP enumeration itself:
-               `AMD_VISIBLE_DEVICES` from the device plugin becomes `HIP_VISIBLE_DEVICES`.
+               e.g. `kubernetes-amd/hip-vector-add` → native/bin/hip-vector-add.
 Exit is observed by awaiting the child (event-driven PLEG), like a CRI event stream.
 
 Restart survival (docker keeps containers when the kubelet restarts): every sandbox and
 container writes `state.json` next to its files (pid + kernel start time, pod uid, name, CRI
 attempt, exit code once known). A runtime constructed on the same root re-adopts the processes
 that are still alive (same pid AND start time, so a recycled pid is never adopted) and watches
-them with a pidfd; their exit code is unknowable (not our children) and reads as 255
-"ExitCodeUnknown". `pod_states()` hands them to the restarted kubelet.
+them with a pidfd from `start()`; their exit code is unknowable (not our children) and reads as
+255 "ExitCodeUnknown". `pod_states()` hands them to the restarted kubelet.
 """
 from __future__ import annotations
 
@@ -26,6 +34,7 @@ import json
 import os
 import shutil
 import signal
+import subprocess
 import time
 
 from ...native import BIN_DIR
@@ -125,21 +134,33 @@ def resolve_command(container):
 
 
 CONTAINER_INIT = os.path.join(BIN_DIR, "container-init")
+KAMD_RUNC = os.path.join(BIN_DIR, "kamd-runc")
+_FEATURES: dict = {}
 
 
-def _init_argv(argv, env, cpus, oom_adj, cgroup, uid=None, gid=None):
+def runc_features(cgroup_dir=None) -> dict:
+    """`kamd-runc features`: which isolation primitives this host grants (cached per cgroup)."""
+    key = cgroup_dir or ""
+    if key not in _FEATURES:
+        if not os.access(KAMD_RUNC, os.X_OK):
+            _FEATURES[key] = {"isolation": False, "namespace_error": "kamd-runc is not built"}
+        else:
+            try:
+                r = subprocess.run([KAMD_RUNC, "features"] + (["--cgroup", cgroup_dir] if cgroup_dir else []),
+                                   capture_output=True, text=True, timeout=20)
+                _FEATURES[key] = json.loads(r.stdout)
+            except (OSError, ValueError, subprocess.SubprocessError) as e:
+                _FEATURES[key] = {"isolation": False, "namespace_error": f"kamd-runc features: {e}"}
+    return _FEATURES[key]
+
+
+def _init_argv(argv, env, cpus, oom_adj, cgroup, uid=None, gid=None, groups=()):
     """Prefix argv with the native container-init helper (native/pause/container_init.cc), which
-    applies the cpuset, OOM score and cgroup and then execs the entrypoint — so the spawn needs
-    no Python pre-exec hook and can use vfork (a hook forces a full fork of the kubelet: ~3 ms
-    of kubelet CPU per container instead of ~0.5 ms). The entrypoint is resolved here so a
-    missing binary is still a StartError rather than exit 127 of the helper."""
-    exe = argv[0]
-    if os.sep not in exe:
-        found = shutil.which(exe, path=env.get("PATH", os.defpath))
-        if found is None:
-            raise FileNotFoundError(2, "No such file or directory", exe)
-    elif not os.access(exe, os.X_OK):
-        raise FileNotFoundError(2, "No such file or directory", exe)
+    applies the cpuset, OOM score, cgroup and identity and then execs the entrypoint — so the
+    spawn needs no Python pre-exec hook and can use vfork (a hook forces a full fork of the
+    kubelet: ~3 ms of kubelet CPU per container instead of ~0.5 ms). The entrypoint is resolved
+    here so a missing binary is still a StartError rather than exit 127 of the helper."""
+    _check_entrypoint(argv, env)
     pre = [CONTAINER_INIT]
     if cpus:
         pre += ["-c", ",".join(str(c) for c in sorted(cpus))]
@@ -147,11 +168,53 @@ def _init_argv(argv, env, cpus, oom_adj, cgroup, uid=None, gid=None):
         pre += ["-o", str(int(oom_adj))]
     if cgroup:
         pre += ["-g", cgroup]
+    if groups:
+        pre += ["-S", ",".join(str(int(g)) for g in groups)]
     if gid is not None:
         pre += ["-G", str(int(gid))]
     if uid is not None:
         pre += ["-u", str(int(uid))]
     return pre + ["--"] + list(argv)
+
+
+def _check_entrypoint(argv, env):
+    exe = argv[0]
+    if os.sep not in exe:
+        if shutil.which(exe, path=env.get("PATH", os.defpath)) is None:
+            raise FileNotFoundError(2, "No such file or directory", exe)
+    elif not os.access(exe, os.X_OK):
+        raise FileNotFoundError(2, "No such file or directory", exe)
+
+
+async def _spawn_runc(bundle, stdout, timeout=30.0):
+    """Start `kamd-runc run` on a bundle; returns (process, container init pid, isolation report)
+    once the container's namespaces, /dev and identity are set up (the ready pipe), or raises
+    OSError with kamd-runc's diagnostics if the setup failed."""
+    loop = asyncio.get_running_loop()
+    r, w = os.pipe()
+    try:
+        proc = await asyncio.create_subprocess_exec(KAMD_RUNC, "run", "--bundle", bundle, "--ready-fd", str(w),
+                                                    pass_fds=(w,), stdout=stdout, stderr=asyncio.subprocess.STDOUT,
+                                                    start_new_session=True)
+    finally:
+        os.close(w)
+    reader = asyncio.StreamReader()
+    transport, _ = await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), os.fdopen(r, "rb", 0))
+    try:
+        line = await asyncio.wait_for(reader.readline(), timeout)
+    except asyncio.TimeoutError:
+        line = b""
+    finally:
+        transport.close()
+    if not line:
+        try:
+            code = await asyncio.wait_for(proc.wait(), 5)
+        except asyncio.TimeoutError:
+            proc.kill()
+            code = await proc.wait()
+        raise OSError(126, f"kamd-runc failed to set up the container (exit {code})")
+    pid, _, report = line.decode().strip().partition(" ")
+    return proc, int(pid), json.loads(report or "{}")
 
 
 def _child_setup(cpus, oom_adj, cgroup):
@@ -181,7 +244,7 @@ class ProcessRuntime(Runtime):
     name = "process"
     shares_host_network = True     # containers are host processes: pod IP = node address
 
-    def __init__(self, root_dir: str, inherit_env: bool = True):
+    def __init__(self, root_dir: str, inherit_env: bool = True, isolation: str | None = None):
         super().__init__()
         self.root = os.path.abspath(root_dir)
         os.makedirs(os.path.join(self.root, "containers"), exist_ok=True)
@@ -190,7 +253,43 @@ class ProcessRuntime(Runtime):
         self.containers: dict[str, ContainerStatus] = {}
         self.meta: dict[str, dict] = {}
         self.inherit_env = inherit_env
+        # "auto": isolate when the host allows it; "required": refuse device containers when it
+        # does not; "off": host processes narrowed by HIP_VISIBLE_DEVICES only
+        self.isolation = isolation or os.environ.get("KAMD_ISOLATION", "auto")
+        if self.isolation not in ("auto", "required", "off"):
+            raise ValueError(f"isolation must be auto, required or off, not {self.isolation!r}")
+        self.features = runc_features() if self.isolation != "off" else {}
+        self.isolated = bool(self.features.get("isolation"))
+        self._started = False
         self._ids = itertools.count(self._load_state() + 1)
+
+    def isolation_status(self):
+        if self.isolation == "off":
+            return {"enforced": False, "reason": "IsolationDisabled",
+                    "message": "container isolation is off: GPU enumeration is narrowed by HIP_VISIBLE_DEVICES only"}
+        f = self.features
+        if self.isolated:
+            dc = f.get("device_cgroup", "none")
+            return {"enforced": True, "reason": "DeviceIsolationEnforced",
+                    "message": f"mount/pid/ipc/uts namespaces{' in a user namespace' if f.get('user_ns') else ''}, "
+                               f"private /dev with only the allocated device nodes, device cgroup: {dc}"}
+        return {"enforced": False, "reason": "IsolationUnavailable",
+                "message": "no mount namespace for containers (" + (f.get("namespace_error") or "unknown") +
+                           "): a pod can open any /dev/dri/renderD* of the host; GPU enumeration is narrowed by "
+                           "HIP_VISIBLE_DEVICES only"}
+
+    async def start(self):
+        """Watch the processes re-adopted from state.json (exit of an adopted container is then
+        reported even when nobody calls pod_states(), e.g. behind kamd-cri)."""
+        if self._started:
+            return
+        self._started = True
+        for cid, m in self.meta.items():
+            if m.pop("adopted", False):
+                spawn(self._wait(cid, m["proc"]))
+        for sb in self.sandboxes.values():
+            if isinstance(sb["proc"], _AdoptedProcess) and sb["proc"].returncode is None:
+                spawn(sb["proc"].wait())
 
     def _load_state(self) -> int:
         """Re-adopt sandboxes/containers an earlier runtime instance on this root left running
@@ -206,7 +305,8 @@ class ProcessRuntime(Runtime):
             if not st:
                 continue
             self.sandboxes[sid] = {"proc": _AdoptedProcess(st["pid"], st.get("ticks")), "dir": os.path.join(sdir, sid),
-                                   "pod_uid": st["pod_uid"], "annotations": st.get("annotations") or {}}
+                                   "pod_uid": st["pod_uid"], "annotations": st.get("annotations") or {},
+                                   "init_pid": st.get("init_pid"), "user_ns": st.get("user_ns", False)}
         cdir = os.path.join(self.root, "containers")
         for name in sorted(os.listdir(cdir)):
             d = os.path.join(cdir, name)
@@ -236,6 +336,8 @@ class ProcessRuntime(Runtime):
             self.meta[cid] = {"sandbox": st["sandbox"], "pod_uid": st["pod_uid"], "argv": st.get("argv") or [],
                               "env": st.get("env") or {}, "cwd": st.get("cwd"), "proc": proc, "dir": d, "spec": None,
                               "oom_score_adj": None, "cgroup": None, "attempt": st.get("attempt", 0),
+                              "init_pid": st.get("init_pid"), "isolated": st.get("isolated", False),
+                              "user": st.get("user"),
                               "adopted": proc is not None and proc.returncode is None}
         return top
 
@@ -246,7 +348,9 @@ class ProcessRuntime(Runtime):
         proc = m.get("proc")
         st = {"id": cid, "name": cs.name, "pod_uid": m["pod_uid"], "sandbox": m["sandbox"], "attempt": m.get("attempt", 0),
               "image": cs.image, "created_at": cs.created_at, "started_at": cs.started_at, "argv": m["argv"],
-              "env": m["env"], "cwd": m["cwd"]}
+              "env": m["env"], "cwd": m["cwd"], "isolated": m.get("isolated", False)}
+        if m.get("init_pid"):
+            st["init_pid"], st["user"] = m["init_pid"], m.get("user")
         if proc is not None:
             st["pid"], st["ticks"] = proc.pid, _start_ticks(proc.pid)
         st.update(extra)
@@ -256,16 +360,27 @@ class ProcessRuntime(Runtime):
             pass
 
     async def run_pod_sandbox(self, pod, annotations):
+        await self.start()
         sid = f"sb{next(self._ids)}-{pod['metadata']['uid'][:8]}"
         d = os.path.join(self.root, "sandboxes", sid)
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "annotations.json"), "w") as f:
             json.dump(annotations or {}, f)
-        proc = await asyncio.create_subprocess_exec(os.path.join(BIN_DIR, "pause"), start_new_session=True,
-                                                    stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL)
-        self.sandboxes[sid] = {"proc": proc, "dir": d, "pod_uid": pod["metadata"]["uid"], "annotations": annotations}
+        pause = os.path.join(BIN_DIR, "pause")
+        init_pid, user_ns = None, False
+        if self.isolated:
+            with open(os.path.join(d, "config.json"), "w") as f:
+                json.dump(oci.sandbox_spec(pod, pause), f, separators=(",", ":"))
+            with open(os.path.join(d, "log"), "ab") as log:
+                proc, init_pid, report = await _spawn_runc(d, log)
+            user_ns = bool(report.get("user_ns"))
+        else:
+            proc = await asyncio.create_subprocess_exec(pause, start_new_session=True,
+                                                        stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL)
+        self.sandboxes[sid] = {"proc": proc, "dir": d, "pod_uid": pod["metadata"]["uid"], "annotations": annotations,
+                               "init_pid": init_pid, "user_ns": user_ns}
         _write_state(d, {"pod_uid": pod["metadata"]["uid"], "pid": proc.pid, "ticks": _start_ticks(proc.pid),
-                         "annotations": annotations or {}})
+                         "annotations": annotations or {}, "init_pid": init_pid, "user_ns": user_ns})
         return sid
 
     async def stop_pod_sandbox(self, sid):
@@ -300,7 +415,8 @@ class ProcessRuntime(Runtime):
 
     async def create_container(self, sid, pod, container, opts: RunContainerOptions):
         cid = f"process://{next(self._ids)}-{container['name']}"
-        d = os.path.join(self.root, "containers", cid.split("://", 1)[1])
+        leaf = cid.split("://", 1)[1]
+        d = os.path.join(self.root, "containers", leaf)
         os.makedirs(d, exist_ok=True)
         argv = resolve_command(container)
         env = dict(os.environ) if self.inherit_env else {"PATH": os.environ.get("PATH", "/usr/bin:/bin")}
@@ -311,13 +427,32 @@ class ProcessRuntime(Runtime):
         env.update(dev_env)
         env.pop("ROCR_VISIBLE_DEVICES", None)
         env.pop("CUDA_VISIBLE_DEVICES", None)
-        if "AMD_VISIBLE_DEVICES" in dev_env:
-            env["HIP_VISIBLE_DEVICES"] = dev_env["AMD_VISIBLE_DEVICES"]
-        else:
-            env["HIP_VISIBLE_DEVICES"] = "-1"   # a container without allocated GPUs sees none
+        env.pop("HIP_VISIBLE_DEVICES", None)
+        if opts.devices and not self.isolated and self.isolation == "required":
+            raise OSError(1, "IsolationUnavailable: the runtime cannot give this container a private /dev "
+                             f"({self.isolation_status()['message']})")
+        if not self.isolated:
+            # no device namespace: narrow HIP enumeration to the allocation; a container without
+            # allocated GPUs sees none. (Isolated containers see only their own render nodes, so
+            # HIP's default enumeration is already right.)
+            env["HIP_VISIBLE_DEVICES"] = dev_env.get("AMD_VISIBLE_DEVICES", "-1")
         sb = self.sandboxes.get(sid) or {}
-        spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts,
-                              sandbox_pid=getattr(sb.get("proc"), "pid", None))
+        cgroup = os.path.join(opts.cgroup_parent, f"ctr-{leaf}") if opts.cgroup_parent else None
+        cpus = None
+        if env.get("KAMD_CPUSET") and hasattr(os, "sched_setaffinity"):
+            # cpu manager's cpuset (cgroup cpuset.cpus in a real runtime): pinned before exec
+            from ..cpumanager import parse_cpulist
+            cpus = set(parse_cpulist(env["KAMD_CPUSET"])) & set(os.sched_getaffinity(0)) or None
+        ns_paths = {}
+        if self.isolated and sb.get("init_pid"):
+            ns_paths = {t: f"/proc/{sb['init_pid']}/ns/{t}" for t in ("ipc", "uts")}
+            if sb.get("user_ns"):
+                ns_paths["user"] = f"/proc/{sb['init_pid']}/ns/user"
+        spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts, rootfs="/",
+                              sandbox_pid=getattr(sb.get("proc"), "pid", None),
+                              env=env if self.isolated else None, cgroups_path=cgroup, ns_paths=ns_paths,
+                              host_network=self.shares_host_network,
+                              cpus=",".join(str(c) for c in sorted(cpus)) if cpus else None)
         with open(os.path.join(d, "config.json"), "w") as f:
             json.dump(spec, f, separators=(",", ":"))
         st = ContainerStatus(cid, container["name"], CREATED, image=container.get("image", ""),
@@ -325,8 +460,10 @@ class ProcessRuntime(Runtime):
         self.containers[cid] = st
         self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "argv": argv, "env": env,
                           "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec,
-                          "oom_score_adj": opts.oom_score_adj, "cgroup": opts.cgroup_parent,
-                          "attempt": opts.attempt, "run_as_user": opts.run_as_user, "run_as_group": opts.run_as_group}
+                          "oom_score_adj": opts.oom_score_adj, "cgroup": cgroup, "cpus": cpus,
+                          "attempt": opts.attempt, "run_as_user": opts.run_as_user, "run_as_group": opts.run_as_group,
+                          "groups": list(opts.supplemental_groups), "isolated": self.isolated,
+                          "user": f"{spec['process']['user']['uid']}:{spec['process']['user']['gid']}"}
         return cid
 
     @staticmethod
@@ -337,26 +474,12 @@ class ProcessRuntime(Runtime):
         m = self.meta[cid]
         st = self.containers[cid]
         log = open(st.log_path, "ab")
-        cpus = None
-        if m["env"].get("KAMD_CPUSET") and hasattr(os, "sched_setaffinity"):
-            # cpu manager's cpuset (cgroup cpuset.cpus in a real runtime): pin before exec
-            from ..cpumanager import parse_cpulist
-            cpus = set(parse_cpulist(m["env"]["KAMD_CPUSET"])) & set(os.sched_getaffinity(0)) or None
-        pre = None
-        argv = m["argv"]
         try:
-            identity = m.get("run_as_user") is not None or m.get("run_as_group") is not None
-            if identity and not os.access(CONTAINER_INIT, os.X_OK):
-                raise OSError(1, "runAsUser needs the container-init helper (python -m kubernetes_amd.native.build)")
-            if cpus or m.get("oom_score_adj") is not None or m.get("cgroup") or identity:
-                if os.access(CONTAINER_INIT, os.X_OK):
-                    argv = _init_argv(argv, m["env"], cpus, m.get("oom_score_adj"), m.get("cgroup"),
-                                      m.get("run_as_user"), m.get("run_as_group"))
-                else:
-                    pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
-            proc = await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=m["cwd"], stdout=log,
-                                                        stderr=asyncio.subprocess.STDOUT, start_new_session=True,
-                                                        preexec_fn=pre)
+            if m.get("isolated"):
+                _check_entrypoint(m["argv"], m["env"])
+                proc, m["init_pid"], m["isolation"] = await _spawn_runc(m["dir"], log)
+            else:
+                proc = await self._start_host_process(m, log)
         except OSError as e:
             log.close()
             st.state = EXITED
@@ -372,12 +495,27 @@ class ProcessRuntime(Runtime):
         self._container_state(cid)
         spawn(self._wait(cid, proc))
 
+    async def _start_host_process(self, m, log):
+        cpus = m.get("cpus")
+        pre = None
+        argv = m["argv"]
+        identity = m.get("run_as_user") is not None or m.get("run_as_group") is not None or m.get("groups")
+        if identity and not os.access(CONTAINER_INIT, os.X_OK):
+            raise OSError(1, "runAsUser needs the container-init helper (python -m kubernetes_amd.native.build)")
+        if cpus or m.get("oom_score_adj") is not None or m.get("cgroup") or identity:
+            if os.access(CONTAINER_INIT, os.X_OK):
+                argv = _init_argv(argv, m["env"], cpus, m.get("oom_score_adj"), m.get("cgroup"),
+                                  m.get("run_as_user"), m.get("run_as_group"), m.get("groups") or ())
+            else:
+                pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
+        return await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=m["cwd"], stdout=log,
+                                                    stderr=asyncio.subprocess.STDOUT, start_new_session=True,
+                                                    preexec_fn=pre)
+
     async def pod_states(self):
         """Sandboxes/containers of this runtime, including the ones re-adopted from state.json
-        after a restart (their exits are watched from here on)."""
-        for cid, m in self.meta.items():
-            if m.pop("adopted", False):
-                spawn(self._wait(cid, m["proc"]))
+        after a restart (their exits are watched from `start()` on)."""
+        await self.start()
         out: dict = {}
         for sid, sb in self.sandboxes.items():
             alive = sb["proc"].returncode is None
@@ -440,6 +578,22 @@ class ProcessRuntime(Runtime):
             except OSError:
                 pass
 
+    async def kill_all(self):
+        """Kill every container and sandbox process group of this runtime (cluster teardown)."""
+        procs = [m["proc"] for m in self.meta.values() if m.get("proc") is not None] + \
+            [sb["proc"] for sb in self.sandboxes.values()]
+        for p in procs:
+            if p.returncode is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        for p in procs:
+            try:
+                await asyncio.wait_for(p.wait(), 5)
+            except (asyncio.TimeoutError, ProcessLookupError):
+                pass
+
     def container_status(self, cid):
         return self.containers.get(cid)
 
@@ -448,8 +602,14 @@ class ProcessRuntime(Runtime):
         st = self.containers.get(cid)
         if m is None or st is None or st.state != RUNNING:
             return 126, b"container is not running"
+        argv, cwd = list(cmd), m["cwd"]
+        if m.get("init_pid"):
+            # into the container's namespaces (its /dev view, pid namespace) as its user
+            argv = [KAMD_RUNC, "exec", "--pid", str(m["init_pid"]), "--cwd", cwd or "/"] + \
+                (["--user", m["user"]] if m.get("user") else []) + ["--"] + argv
+            cwd = None
         try:
-            proc = await asyncio.create_subprocess_exec(*cmd, env=m["env"], cwd=m["cwd"], stdout=asyncio.subprocess.PIPE,
+            proc = await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=cwd, stdout=asyncio.subprocess.PIPE,
                                                         stderr=asyncio.subprocess.STDOUT, start_new_session=True)
         except OSError as e:
             return 127, str(e).encode()

@@ -45,6 +45,8 @@ def targets():
                   ["g++", "-Os", "-Wall", "-Werror", "-static", _s("pause", "pause.cc")]),
         "container_init": ([_s("pause", "container_init.cc")], os.path.join(BIN_DIR, "container-init"),
                            ["g++", "-O2", "-Wall", "-Werror", "-static", _s("pause", "container_init.cc")]),
+        "kamd_runc": ([_s("runc", "kamd_runc.cc")], os.path.join(BIN_DIR, "kamd-runc"),
+                      ["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-static", _s("runc", "kamd_runc.cc")]),
         "orphan": ([_s("pause", "orphan.cc")], os.path.join(BIN_DIR, "orphan"),
                    ["g++", "-Os", "-Wall", _s("pause", "orphan.cc")]),
         "kamd_hip": ([_s("hip", "kamd_hip.hip")], os.path.join(LIB_DIR, "libkamd_hip.so"),

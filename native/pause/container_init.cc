@@ -5,12 +5,17 @@
 // pre-exec hook in the forked child, so the kubelet can spawn with vfork/posix_spawn (a
 // pre-exec hook forces a full fork of the kubelet's address space, ~5x the spawn CPU).
 //
-//   container-init [-c CPULIST] [-o OOM_SCORE_ADJ] [-g CGROUP_DIR] -- argv...
+//   container-init [-c CPULIST] [-o OOM_SCORE_ADJ] [-g CGROUP_DIR] [-u UID] [-G GID] [-S G1,G2]
+//                  -- argv...
 //
 // CPULIST is a cpuset list ("0-3,8"); pinning failures are fatal (the cpu manager promised
 // those CPUs), OOM score and cgroup failures are not (an unprivileged kubelet may only raise
-// oom_score_adj and may not own a cgroup subtree). Exit 127 when the entrypoint cannot be
-// executed, like a shell.
+// oom_score_adj and may not own a cgroup subtree). CGROUP_DIR is the container's own cgroup
+// (a leaf under the pod cgroup, created here): cgroup v2 forbids processes in the pod cgroup
+// itself once it delegates controllers to children. -S sets the supplemental groups (the pod's
+// fsGroup + supplementalGroups, kuberuntime/security_context.go:58-66); a non-root caller that
+// cannot change them keeps its own and warns instead of failing. A uid/gid equal to the current
+// one needs no privilege. Exit 127 when the entrypoint cannot be executed, like a shell.
 #include <errno.h>
 #include <fcntl.h>
 #include <sched.h>
@@ -18,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <grp.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 static int parse_cpus(const char* s, cpu_set_t* set) {
@@ -54,7 +60,8 @@ int main(int argc, char** argv) {
   const char* oom = nullptr;
   const char* cgroup = nullptr;
   const char* uid = nullptr;   // securityContext.runAsUser
-  const char* gid = nullptr;   // primary group (runAsGroup / fsGroup)
+  const char* gid = nullptr;   // primary group (runAsGroup)
+  const char* groups = nullptr;  // supplemental groups
   int i = 1;
   for (; i < argc; ++i) {
     if (strcmp(argv[i], "--") == 0) { ++i; break; }
@@ -64,6 +71,7 @@ int main(int argc, char** argv) {
     else if (strcmp(argv[i], "-g") == 0) cgroup = argv[++i];
     else if (strcmp(argv[i], "-u") == 0) uid = argv[++i];
     else if (strcmp(argv[i], "-G") == 0) gid = argv[++i];
+    else if (strcmp(argv[i], "-S") == 0) groups = argv[++i];
     else { fprintf(stderr, "container-init: unknown option %s\n", argv[i]); return 126; }
   }
   if (i >= argc) { fprintf(stderr, "container-init: no command\n"); return 126; }
@@ -74,18 +82,46 @@ int main(int argc, char** argv) {
   }
   if (oom && *oom) write_file("/proc/self/oom_score_adj", oom, 0);
   if (cgroup && *cgroup) {
+    mkdir(cgroup, 0755);
     char path[4096];
     if (snprintf(path, sizeof path, "%s/cgroup.procs", cgroup) < (int)sizeof path) write_file(path, "0", O_CREAT | O_TRUNC);
   }
-  // identity last: the cgroup / OOM writes above may need the kubelet's privileges. Group before
-  // user (setuid drops the right to setgid); supplementary groups are dropped when we can.
-  if ((gid && *gid) || (uid && *uid)) {
-    if (geteuid() == 0) setgroups(0, nullptr);
-    if (gid && *gid && setgid((gid_t)strtoul(gid, nullptr, 10)) != 0) {
+  // identity last: the cgroup / OOM writes above may need the kubelet's privileges. Groups before
+  // gid before uid (setuid drops the right to change the others).
+  gid_t want[64];
+  int nwant = 0;
+  if (groups) {
+    for (const char* p = groups; *p && nwant < 64;) {
+      char* end;
+      unsigned long g = strtoul(p, &end, 10);
+      if (end == p) { fprintf(stderr, "container-init: bad group list %s\n", groups); return 126; }
+      want[nwant++] = (gid_t)g;
+      p = *end == ',' ? end + 1 : end;
+    }
+  }
+  if (groups || (gid && *gid) || (uid && *uid)) {
+    if (geteuid() == 0) {
+      if (setgroups(nwant, want) != 0) { perror("container-init: setgroups"); return 126; }
+    } else if (nwant) {
+      gid_t have[256];
+      int n = getgroups(256, have);
+      for (int k = 0; k < nwant; ++k) {
+        bool found = want[k] == getegid();
+        for (int j = 0; j < n && !found; ++j) found = have[j] == want[k];
+        if (!found) fprintf(stderr, "container-init: warning: not root, supplemental group %u not added\n", want[k]);
+      }
+    }
+  }
+  if (gid && *gid) {
+    gid_t g = (gid_t)strtoul(gid, nullptr, 10);
+    if (g != getegid() && setgid(g) != 0) {
       perror("container-init: setgid");
       return 126;
     }
-    if (uid && *uid && setuid((uid_t)strtoul(uid, nullptr, 10)) != 0) {
+  }
+  if (uid && *uid) {
+    uid_t u = (uid_t)strtoul(uid, nullptr, 10);
+    if (u != geteuid() && setuid(u) != 0) {
       perror("container-init: setuid");
       return 126;
     }

@@ -1,0 +1,261 @@
+"""Enforced GPU device isolation in the process runtime (kamd-runc).
+
+The reference relied on docker: dockershim mapped the plugin's DeviceSpecs into
+`HostConfig.Resources.Devices` (`pkg/kubelet/dockershim/docker_container.go:164-172`) and the
+e2e asserted that pods get distinct GPUs (`test/e2e_node/gpu_device_plugin.go:46-143`). Here the
+device plugin serves mknod'd stand-ins for `/dev/kfd` and `/dev/dri/renderD128..135` (char
+major 226 like real DRM render nodes, no driver behind them), so the test can tell the three
+outcomes apart from inside a pod:
+  * allocated node: present in the private /dev, the device cgroup allows it -> open() fails
+    only in the (absent) driver: ENXIO/ENODEV;
+  * another GPU's node in /dev: absent -> ENOENT;
+  * another GPU's node reached through its host path: the device cgroup denies it -> EPERM.
+Needs root with namespaces (this CI container); the GPU box runs unprivileged without user
+namespaces, which the IsolationUnavailable test covers.
+"""
+import json
+import os
+import stat
+import subprocess
+
+import pytest
+
+from kubernetes_amd.api import core
+from kubernetes_amd.cluster import LocalCluster
+from kubernetes_amd.kubelet.runtime import process as proc_rt
+from kubernetes_amd.kubelet.runtime.base import RunContainerOptions
+from kubernetes_amd.kubelet.runtime.process import ProcessRuntime, runc_features
+
+FEATURES = runc_features()
+needs_isolation = pytest.mark.skipif(not FEATURES.get("isolation") or os.geteuid() != 0,
+                                     reason=f"namespaces not available here: {FEATURES}")
+
+PROBE = r'''
+import errno, os, sys
+mine = sorted(os.listdir("/dev/dri"))
+print("DRI", ",".join(mine))
+print("DEV", ",".join(sorted(os.listdir("/dev"))))
+def probe(p):
+    try:
+        os.close(os.open(p, os.O_RDWR))
+        return "OPEN"
+    except OSError as e:
+        return errno.errorcode.get(e.errno, str(e.errno))
+print("MINE", probe("/dev/dri/" + mine[0]))
+print("KFD", probe("/dev/kfd"))
+for m in range(128, 136):
+    n = "renderD%d" % m
+    if n not in mine:
+        print("OTHER_DEV", probe("/dev/dri/" + n))
+        print("OTHER_HOST", probe(os.path.join(sys.argv[1], "dri", n)))
+        break
+print("PID1", open("/proc/1/cmdline").read().split("\0")[0])
+print("HIP", os.environ.get("HIP_VISIBLE_DEVICES", "unset"))
+'''
+
+
+def make_dev_root(d):
+    os.makedirs(os.path.join(d, "dri"), exist_ok=True)
+    os.mknod(os.path.join(d, "kfd"), stat.S_IFCHR | 0o666, os.makedev(1, 3))   # openable (/dev/null)
+    for m in range(128, 136):
+        os.mknod(os.path.join(d, "dri", f"renderD{m}"), stat.S_IFCHR | 0o666, os.makedev(226, m))
+    return d
+
+
+def parse(log):
+    out = {}
+    for line in log.splitlines():
+        k, _, v = line.partition(" ")
+        out.setdefault(k, v)
+    return out
+
+
+def test_features_json_shape():
+    f = runc_features()
+    assert {"isolation", "mount_ns", "device_cgroup"} <= set(f) or "namespace_error" in f
+
+
+@needs_isolation
+def test_gpu_pod_sees_only_its_render_node(run, tmp_path):
+    dev = make_dev_root(str(tmp_path / "dev"))
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8, runtime="process", dev_root=dev, isolation="required") as cl:
+            c = cl.client
+            node = await c.get("nodes", "node-0")
+            conds = {x["type"]: x for x in node["status"]["conditions"]}
+            assert conds["IsolationUnavailable"]["status"] == "False", conds
+            pods = []
+            for i in range(2):
+                p = {"metadata": {"name": f"iso{i}", "namespace": "default"},
+                     "spec": {"restartPolicy": "Never", "containers": [{
+                         "name": "c", "image": "busybox", "command": ["python3", "-c", PROBE, dev],
+                         "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
+                await c.create("pods", p)
+            for i in range(2):
+                pods.append(await cl.wait_pod(f"iso{i}", phase="Succeeded", timeout=30))
+            rt = cl.nodes[0].runtime
+            seen = []
+            for cs in rt.list_containers():
+                r = parse(open(cs.log_path).read())
+                seen.append(r["DRI"])
+                # exactly one render node, the allocated one, and only default nodes + kfd + dri
+                assert len(r["DRI"].split(",")) == 1, r
+                assert set(r["DEV"].split(",")) <= {"dri", "fd", "full", "kfd", "null", "ptmx", "pts", "random", "shm",
+                                                   "stderr", "stdin", "stdout", "tty", "urandom", "zero"}, r
+                assert r["MINE"] in ("ENXIO", "ENODEV"), r     # cgroup allowed; no DRM driver here
+                assert r["KFD"] == "OPEN", r
+                assert r["OTHER_DEV"] == "ENOENT", r           # not in the container's /dev
+                assert r["OTHER_HOST"] == "EPERM", r           # device cgroup denies the host node
+                assert r["HIP"] == "unset", r                  # isolation, not env narrowing
+                assert r["PID1"] != "/usr/lib/systemd/systemd"
+                iso = json.load(open(os.path.join(os.path.dirname(cs.log_path), "isolation.json")))
+                assert iso["mount_ns"] and iso["pid_ns"] and iso["dev"] == "private"
+                assert iso["device_cgroup"] in ("bpf", "v1")
+            # the two pods got distinct GPUs (gpu_device_plugin.go:46-143)
+            assert len(set(seen)) == 2, seen
+            assigned = [p["spec"]["extendedResources"][0]["assigned"][0] for p in pods]
+            assert len(set(assigned)) == 2
+    run(main(), timeout=120)
+
+
+@needs_isolation
+def test_exec_enters_the_container(run, tmp_path):
+    dev = make_dev_root(str(tmp_path / "dev"))
+
+    async def main():
+        rt = ProcessRuntime(str(tmp_path / "rt"), isolation="required")
+        pod = {"metadata": {"name": "p", "namespace": "default", "uid": "u-exec"}, "spec": {}}
+        sid = await rt.run_pod_sandbox(pod, {})
+        opts = RunContainerOptions(devices=[
+            {"pathOnHost": os.path.join(dev, "dri", "renderD130"), "pathInContainer": "/dev/dri/renderD130", "permissions": "rw"}])
+        cid = await rt.create_container(sid, pod, {"name": "c", "image": "busybox", "command": ["sleep", "30"]}, opts)
+        await rt.start_container(cid)
+        try:
+            rc, out = await rt.exec_sync(cid, ["sh", "-c", "ls /dev/dri; echo pid=$$; hostname"], 10)
+            assert rc == 0, out
+            lines = out.decode().split()
+            assert lines[0] == "renderD130"
+            # the exec'd shell lives in the container's pid namespace (sleep is pid 2 under init)
+            assert int(lines[1].split("=")[1]) < 100
+            assert lines[2] == "p"            # the sandbox's uts namespace
+            # two containers of a pod share the sandbox's ipc namespace
+            init = rt.meta[cid]["init_pid"]
+            sb = rt.sandboxes[sid]["init_pid"]
+            assert os.readlink(f"/proc/{init}/ns/ipc") == os.readlink(f"/proc/{sb}/ns/ipc")
+            assert os.readlink(f"/proc/{init}/ns/mnt") != os.readlink("/proc/self/ns/mnt")
+        finally:
+            await rt.stop_container(cid, 1)
+            await rt.remove_pod_sandbox(sid)
+    run(main(), timeout=60)
+
+
+@needs_isolation
+def test_stop_reaches_the_entrypoint(run, tmp_path):
+    """SIGTERM to the container (the kubelet signals kamd-runc's process group) is forwarded
+    to the entrypoint through the container's init; the pid namespace dies with it."""
+    async def main():
+        rt = ProcessRuntime(str(tmp_path / "rt"), isolation="required")
+        pod = {"metadata": {"name": "p", "namespace": "default", "uid": "u-stop"}, "spec": {}}
+        sid = await rt.run_pod_sandbox(pod, {})
+        script = "trap 'echo got-term; exit 7' TERM; sleep 60 & wait"
+        cid = await rt.create_container(sid, pod, {"name": "c", "image": "busybox", "command": ["sh", "-c", script]},
+                                        RunContainerOptions())
+        await rt.start_container(cid)
+        import asyncio
+        await asyncio.sleep(0.3)
+        init = rt.meta[cid]["init_pid"]
+        await rt.stop_container(cid, 5)
+        st = rt.container_status(cid)
+        assert st.exit_code == 7, (st, open(st.log_path).read())
+        assert "got-term" in open(st.log_path).read()
+        assert not os.path.exists(f"/proc/{init}")
+        await rt.remove_pod_sandbox(sid)
+    run(main(), timeout=60)
+
+
+def test_isolation_unavailable_condition(run, monkeypatch):
+    """An unprivileged runtime without user namespaces (the GPU box) reports it on the node."""
+    monkeypatch.setitem(proc_rt._FEATURES, "", {"isolation": False, "mount_ns": False, "device_cgroup": "none",
+                                                 "namespace_error": "No space left on device"})
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=2, runtime="process") as cl:
+            node = await cl.client.get("nodes", "node-0")
+            conds = {x["type"]: x for x in node["status"]["conditions"]}
+            assert conds["IsolationUnavailable"]["status"] == "True"
+            assert "No space left on device" in conds["IsolationUnavailable"]["message"]
+            # auto mode still runs the pod, narrowed by HIP_VISIBLE_DEVICES
+            await cl.client.create("pods", {"metadata": {"name": "e", "namespace": "default"},
+                                            "spec": {"restartPolicy": "Never", "containers": [{
+                                                "name": "c", "image": "busybox",
+                                                "command": ["sh", "-c", "echo HIP=$HIP_VISIBLE_DEVICES"],
+                                                "resources": {"limits": {core.AMD_GPU: "1"}}}]}})
+            await cl.wait_pod("e", phase="Succeeded", timeout=30)
+            cs = cl.nodes[0].runtime.list_containers()[0]
+            assert "HIP=" in open(cs.log_path).read() and "HIP=-1" not in open(cs.log_path).read()
+    run(main(), timeout=90)
+
+
+def test_required_isolation_refuses_device_containers(run, tmp_path, monkeypatch):
+    monkeypatch.setitem(proc_rt._FEATURES, "", {"isolation": False, "namespace_error": "no namespaces"})
+
+    async def main():
+        rt = ProcessRuntime(str(tmp_path / "rt"), isolation="required")
+        pod = {"metadata": {"name": "p", "namespace": "default", "uid": "u-req"}, "spec": {}}
+        sid = await rt.run_pod_sandbox(pod, {})
+        opts = RunContainerOptions(devices=[{"pathOnHost": "/dev/null", "pathInContainer": "/dev/dri/renderD128"}])
+        with pytest.raises(OSError, match="IsolationUnavailable"):
+            await rt.create_container(sid, pod, {"name": "c", "image": "busybox", "command": ["true"]}, opts)
+        # a container without devices still runs
+        cid = await rt.create_container(sid, pod, {"name": "d", "image": "busybox", "command": ["true"]},
+                                        RunContainerOptions())
+        await rt.start_container(cid)
+        await rt.remove_pod_sandbox(sid)
+    run(main(), timeout=60)
+
+
+def test_device_filter_program_assembles():
+    """The BPF device program is generated from the OCI allow list; a deny-all rule last in
+    evaluation order must not leave unreachable instructions (the verifier rejects them)."""
+    if not FEATURES.get("device_cgroup"):
+        pytest.skip("no kamd-runc")
+    # `features` loads a program built from the default allow list: success means the
+    # generator produced verifier-clean code on this kernel (bpf) or v1 is used
+    assert FEATURES["device_cgroup"] in ("bpf", "v1", "none")
+
+
+def test_oci_spec_security_context():
+    from kubernetes_amd.kubelet.runtime import oci
+    pod = {"metadata": {"name": "p", "uid": "u"}}
+    o = RunContainerOptions(run_as_user=1000, run_as_group=2000, supplemental_groups=[3000, 4000],
+                            cap_add=["NET_ADMIN"], cap_drop=["MKNOD"], readonly_rootfs=True, oom_score_adj=-998)
+    s = oci.build_spec(pod, {"name": "c", "command": ["x"]}, o, rootfs="/", cgroups_path="/cg/pod/ctr-1",
+                       ns_paths={"ipc": "/proc/9/ns/ipc"}, host_network=True)
+    assert s["process"]["user"] == {"uid": 1000, "gid": 2000, "additionalGids": [3000, 4000]}
+    caps = s["process"]["capabilities"]["bounding"]
+    assert "CAP_NET_ADMIN" in caps and "CAP_MKNOD" not in caps and "CAP_SYS_ADMIN" not in caps
+    assert s["root"]["readonly"] is True and s["process"]["oomScoreAdj"] == -998
+    ns = {n["type"]: n.get("path") for n in s["linux"]["namespaces"]}
+    assert ns == {"pid": None, "ipc": "/proc/9/ns/ipc", "uts": None, "mount": None}
+    assert s["linux"]["cgroupsPath"] == "/cg/pod/ctr-1"
+    assert {m["destination"] for m in s["mounts"]} >= {"/proc", "/dev", "/dev/pts", "/dev/shm", "/sys"}
+    p = oci.build_spec(pod, {"name": "c", "command": ["x"]}, RunContainerOptions(privileged=True), rootfs="/")
+    assert "/dev" not in {m["destination"] for m in p["mounts"]}
+    assert p["linux"]["resources"]["devices"] == [{"allow": True, "access": "rwm"}]
+    assert "CAP_SYS_ADMIN" in p["process"]["capabilities"]["bounding"]
+
+
+def test_kamd_runc_rejects_mismatched_device(tmp_path):
+    """A spec device whose host node is not the major:minor the kubelet recorded is refused."""
+    if not os.access(proc_rt.KAMD_RUNC, os.X_OK) or not FEATURES.get("isolation"):
+        pytest.skip("needs kamd-runc with namespaces")
+    b = tmp_path / "b"
+    b.mkdir()
+    spec = {"process": {"args": ["true"], "env": [], "cwd": "/"}, "root": {"path": "/"},
+            "mounts": [{"destination": "/dev", "type": "tmpfs", "source": "tmpfs"}],
+            "linux": {"devices": [{"path": "/dev/null", "type": "c", "major": 226, "minor": 128}],
+                      "namespaces": [{"type": "mount"}]}}
+    (b / "config.json").write_text(json.dumps(spec))
+    r = subprocess.run([proc_rt.KAMD_RUNC, "run", "--bundle", str(b)], capture_output=True, text=True, timeout=20)
+    assert r.returncode == 126 and "1:3" in r.stderr, r.stderr

@@ -169,7 +169,11 @@ def test_kubelet_cgroups_env_sysctl_and_critical_preemption(run, tmp_path):
             assert "KUBERNETES_SERVICE_HOST=" in out
             pdir = kl.cgroups.pod_dir(p)
             assert pdir.endswith(os.path.join("kubepods", "burstable", "pod" + p["metadata"]["uid"]))
-            assert os.path.exists(os.path.join(pdir, "cgroup.procs"))
+            # the container runs in its own leaf under the pod cgroup; the pod cgroup itself holds
+            # no process (cgroup v2 no-internal-process rule once it delegates cpu/memory)
+            leaves = [x for x in os.listdir(pdir) if x.startswith("ctr-")]
+            assert leaves and os.path.exists(os.path.join(pdir, leaves[0], "cgroup.procs"))
+            assert not (kl.cgroups.read(pdir, "cgroup.procs") or "").strip()
             assert kl.cgroups.read(pdir, "cpu.weight") == str(cg.shares_to_weight(1536))
 
             # unsafe sysctl without --experimental-allowed-unsafe-sysctls: rejected at admission
