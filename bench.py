@@ -54,6 +54,22 @@ def _xgmi4_summary(allstats):
             "xgmi4_single_hive_fraction": round(sum(s["single_hive"] for s in xs) / max(1, sum(s["total"] for s in xs)), 4)}
 
 
+def _interval_summary(allstats):
+    """scheduler_perf's throughput definition (`test/integration/scheduler_perf/scheduler_test.go:131-182`):
+    the count sampled once per second over the whole job, reported as the average and the WORST
+    full 1-s interval — for scheduled pods (bound) and for pods observed Running. Only full
+    intervals inside the timed region count."""
+    from kubernetes_amd.kubemark.density import interval_rates
+    start = min(s["t_start"] for s in allstats)
+    end = max(s["t_end"] for s in allstats)
+    out = {"timed_region_s": round(end - start, 3), "full_1s_intervals": int(end - start)}
+    for key, name in (("scheduled_at", "sched"), ("running_at", "running")):
+        avg, worst = interval_rates([x for s in allstats for x in s[key]], 1.0, start, end)
+        out[f"{name}_rate_avg_pods_per_s"] = round(avg, 1)
+        out[f"{name}_rate_worst_1s_pods_per_s"] = round(worst, 1) if worst is not None else None
+    return out
+
+
 def cpu_budget():
     """CPUs this job may use: affinity mask capped by the cgroup v2 quota."""
     n = len(os.sched_getaffinity(0))
@@ -132,7 +148,8 @@ def spawn_hollow_procs(args, url, rank, nprocs, tmp, payload_socket):
         if n == 0:
             continue
         cmd = [sys.executable, "-m", "kubernetes_amd.cmd.hollow_node", "--master", url, "--count", str(n),
-               "--name-prefix", f"r{rank}p{j}", "--gpus-per-node", str(args.gpus_per_node)]
+               "--name-prefix", f"r{rank}p{j}", "--gpus-per-node", str(args.gpus_per_node),
+               "--hives", str(args.hives)]
         if payload_socket:
             cmd += ["--payload-socket", payload_socket]
         if args.no_events:
@@ -235,7 +252,7 @@ def _cp_cpu(procs):
 
 async def rank_main(args, d: Dist, url, cp_procs=()):
     from kubernetes_amd.client.rest import Client
-    from kubernetes_amd.kubemark.density import DensityRunner, interval_rates, pct
+    from kubernetes_amd.kubemark.density import DensityRunner, pct
     from kubernetes_amd.kubemark.hollow import HollowCluster
 
     loop = asyncio.get_running_loop()
@@ -259,7 +276,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         hprocs = spawn_hollow_procs(args, url, d.rank, args.hollow_procs, tempfile.mkdtemp(prefix="kamd-hollow-"), sock)
     else:
         hollow = HollowCluster(url, args.nodes_per_rank, prefix=f"r{d.rank}", gpus=args.gpus_per_node,
-                               payload=payload_fn, emit_events=not args.no_events)
+                               hives=args.hives, payload=payload_fn, emit_events=not args.no_events)
         await hollow.start()
         await hollow.wait_registered()
     # wait until every rank's nodes are visible with their GPUs
@@ -295,6 +312,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     hollow_pids += [("density_clients", p.pid) for p in (runner.pool.procs if runner.pool else ())]
     cp0 = _cp_cpu(list(cp_procs) + hollow_pids)
     my0 = time.process_time()
+    t_start = time.monotonic()
     t0 = time.perf_counter()
     for k in range(args.steps):
         results.append(await runner.step(k, timeout=args.step_timeout))
@@ -307,12 +325,12 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     my_cpu = time.process_time() - my0
     cp1 = _cp_cpu(list(cp_procs) + hollow_pids)
     lat = [x for r in results for x in r["latencies"]]
-    sched_times = []
-    off = 0.0
-    for r in results:
-        sched_times += [off + s for s in r["scheduled_times"]]
-        off += r["cycle_s"]
+    t_end = time.monotonic()
     stats = {"elapsed": elapsed, "lat": lat, "pods": sum(r["pods"] for r in results),
+             # CLOCK_MONOTONIC is host-wide: the ranks' timelines merge into the cluster's
+             "t_start": t_start, "t_end": t_end,
+             "scheduled_at": [x for r in results for x in r["scheduled_at"]],
+             "running_at": [x for r in results for x in r["running_at"]],
              "to_running": [r["to_running_s"] for r in results], "cycle": [r["cycle_s"] for r in results],
              "phases": {k: [r[k] for r in results] for k in ("create_s", "to_running_s", "delete_issued_s", "cycle_s")},
              "api_lat": {v: [x for r in results for x in r["api_latencies"][v]] for v in ("create", "delete")},
@@ -320,7 +338,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
                               if hollow or psrv else 0),
              "payload_failures": (psrv.failures if psrv else sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes)
                                   if hollow or psrv else 0),
-             "sched_rates": interval_rates(sched_times), "cpu_s": my_cpu,
+             "cpu_s": my_cpu,
              "cp_cpu_s": {k: cp1.get(k, 0.0) - cp0.get(k, 0.0) for k in cp1}}
     await runner.stop()
     # secondary workload (outside the timed region, not part of `value`): 4-GPU pods that must
@@ -376,8 +394,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--nodes-per-rank", type=int, default=8)
+    # 100 hollow nodes x 8 GPUs per rank (scheduler_perf's 100-node cluster): 800 single-GPU pods
+    # per step, so --steps 20 times >= 5 s of full churn and the worst 1-s interval is measured
+    ap.add_argument("--nodes-per-rank", type=int, default=100)
     ap.add_argument("--gpus-per-node", type=int, default=8)
+    ap.add_argument("--hives", type=int, default=2,
+                    help="xGMI hives per hollow node (2 x 4 GPUs: the 4-GPU workload can land across hives)")
     ap.add_argument("--gpus-per-pod", type=int, default=1)
     ap.add_argument("--pods-per-rank", type=int, default=0)
     ap.add_argument("--percentage-of-nodes-to-score", type=int, default=100)
@@ -443,7 +465,8 @@ def main():
         if any(s["payload_runs"] for s in allstats) else "synthetic GPU-requesting pods, stub containers",
         "config": {"model": "kubemark-density/8xMI355X-hollow-nodes/1-GPU-pods", "global_batch": pods // args.steps,
                    "seq_len": None, "parallelism": f"ranks{n}", "hollow_nodes": n * args.nodes_per_rank,
-                   "gpus_per_node": args.gpus_per_node, "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
+                   "gpus_per_node": args.gpus_per_node, "xgmi_hives_per_node": args.hives,
+                   "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
                    "gpus_per_pod": args.gpus_per_pod, "apiserver_workers": d.broadcast_done_workers,
                    "scheduler_shards": d.shards, "hollow_procs_per_rank": args.hollow_procs},
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
@@ -458,7 +481,7 @@ def main():
         # test/e2e/framework/metrics_util.go:52-59)
         "api_call_ms": {v: {q: round(pct([x for s in allstats for x in s["api_lat"][v]], p) * 1000, 2)
                             for q, p in (("p50", 0.5), ("p99", 0.99))} for v in ("create", "delete")},
-        "sched_rate_avg_pods_per_s": round(sum(s["sched_rates"][0] for s in allstats), 1),
+        **_interval_summary(allstats),
         "vs_scheduler_perf_warn_threshold": round(value / BASELINE_SCHED_WARN_PODS_PER_S, 2),
         "payload_runs": sum(s["payload_runs"] for s in allstats),
         "payload_failures": sum(s["payload_failures"] for s in allstats),

@@ -165,7 +165,8 @@ class DensityRunner:
         sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)
         return {"pods": len(names), "names": names, "create_s": t_created - t0, "to_running_s": t_running - t0,
                 "delete_issued_s": t_deleted - t0, "cycle_s": t_gone - t0, "latencies": lat,
-                "scheduled_times": [s - t0 for s in sched], "api_latencies": api_lat}
+                "scheduled_times": [s - t0 for s in sched], "scheduled_at": sched,
+                "running_at": sorted(self.running[n] for n in names), "api_latencies": api_lat}
 
     async def stop(self):
         if self.pool is not None:
@@ -177,16 +178,19 @@ class DensityRunner:
         await self.client.close()
 
 
-def interval_rates(times, bucket=1.0):
-    """Scheduled pods per 1-s interval (scheduler_perf sampling); returns (avg, min) over full buckets."""
-    if not times:
-        return 0.0, 0.0
-    end = max(times)
-    n = int(end // bucket)
+def interval_rates(times, bucket=1.0, start=0.0, end=None):
+    """Pods per 1-s interval (scheduler_perf samples the scheduled count once per second,
+    `test/integration/scheduler_perf/scheduler_test.go:131-182`): (avg, min) over the FULL
+    intervals of [start, end]. With no full interval (a run shorter than one second) the min is
+    not measurable and is reported as None."""
+    if end is None:
+        end = max(times) if times else start
+    n = int((end - start) // bucket)
     if n < 1:
-        return len(times) / max(end, 1e-9), len(times) / max(end, 1e-9)
-    counts = [0] * (n + 1)
+        return (len(times) / max(end - start, 1e-9) if times else 0.0), None
+    counts = [0] * n
     for t in times:
-        counts[min(int(t // bucket), n)] += 1
-    full = counts[:n]
-    return sum(full) / (n * bucket), min(full) / bucket
+        k = int((t - start) // bucket)
+        if 0 <= k < n:
+            counts[k] += 1
+    return sum(counts) / (n * bucket), min(counts) / bucket

@@ -114,7 +114,12 @@ async def run_scheduler_perf(url, nodes=100, pods=3000, workload="cpu", gpus_per
         return {"workload": workload, "nodes": nodes, "pods": pods, "gpus_per_node": gpus_per_node if gpu else 0,
                 "gpus_per_pod": gpus_per_pod if gpu else 0, "scheduled": len(scheduled),
                 "elapsed_s": round(elapsed, 3), "throughput_pods_per_s": round(len(scheduled) / elapsed, 1),
-                "avg_interval_pods_per_s": round(avg, 1), "min_interval_pods_per_s": round(worst, 1),
-                "pass": worst >= FAIL_BELOW, "warn": worst < WARN_BELOW, "single_node_pods": hive_ok}
+                # a run shorter than one second has no full 1-s interval: its worst interval is
+                # unmeasured (None), not the average
+                "avg_interval_pods_per_s": round(avg, 1),
+                "min_interval_pods_per_s": round(worst, 1) if worst is not None else None,
+                "full_intervals": int(elapsed) if times else 0,
+                "pass": (worst >= FAIL_BELOW) if worst is not None else None,
+                "warn": (worst < WARN_BELOW) if worst is not None else None, "single_node_pods": hive_ok}
     finally:
         await c.close()

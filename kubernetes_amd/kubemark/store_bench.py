@@ -18,9 +18,11 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
-import multiprocessing as mp
 import os
+import signal
 import socket
+import subprocess
+import sys
 import threading
 import time
 
@@ -58,14 +60,40 @@ async def _writer_main(addr, wid, pods, nodes, inflight):
     await st.close()
 
 
-def _writer(addr, wid, pods, nodes, inflight, q):
+def _writer_cli(argv):
+    """`--writer ADDR WID PODS NODES INFLIGHT`: one writer process (a fresh interpreter, not a
+    fork of a process that already runs reader / asyncio / gRPC threads). Prints its elapsed
+    seconds as JSON on success."""
+    addr, wid, pods, nodes, inflight = argv[0], *map(int, argv[1:5])
     t0 = time.perf_counter()
-    try:
-        asyncio.run(_writer_main(addr, wid, pods, nodes, inflight))
-    except BaseException as e:  # noqa: BLE001 - reported to the parent, which fails the run
-        q.put(("error", f"writer {wid}: {e!r}"))
-        raise
-    q.put(("ok", time.perf_counter() - t0))
+    asyncio.run(_writer_main(addr, wid, pods, nodes, inflight))
+    print(json.dumps({"elapsed": time.perf_counter() - t0}), flush=True)
+
+
+def _spawn_writers(addr, writers, per, nodes, inflight, timeout):
+    here = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, PYTHONPATH=here + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    ps = [subprocess.Popen([sys.executable, "-m", "kubernetes_amd.kubemark.store_bench", "--writer", str(addr),
+                            str(w), str(per), str(nodes), str(inflight)],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, start_new_session=True)
+          for w in range(writers)]
+    deadline = time.time() + timeout
+    errors = []
+    for w, p in enumerate(ps):
+        try:
+            out, err = p.communicate(timeout=max(0.1, deadline - time.time()))
+            if p.returncode != 0:
+                errors.append(f"writer {w}: exit {p.returncode}: {err.decode()[-500:]}")
+        except subprocess.TimeoutExpired:
+            errors.append(f"writer {w}: no result after {timeout}s")
+    for p in ps:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait()
+    return errors
 
 
 _EVENT = b'{"type":"'
@@ -102,7 +130,7 @@ def _thread_cpu(pid):
     return out
 
 
-def run(writers=4, pods=20000, nodes=64, all_watches=0, fan_threads=1, inflight=64, shards=4):
+def run(writers=4, pods=20000, nodes=64, all_watches=0, fan_threads=1, inflight=64, shards=4, timeout=600.0):
     srv = StoreServer(fan_threads=fan_threads)
     addr = srv.start()
     fc = FanoutClient.for_store(addr)
@@ -126,21 +154,14 @@ def run(writers=4, pods=20000, nodes=64, all_watches=0, fan_threads=1, inflight=
         socks.append(b)
     time.sleep(0.3)
     cpu0 = _thread_cpu(srv.proc.pid)
-    q = mp.get_context("fork").Queue()
     per = pods // writers
     t0 = time.perf_counter()
-    ps = [mp.get_context("fork").Process(target=_writer, args=(addr, w, per, nodes, inflight, q)) for w in range(writers)]
-    for p in ps:
-        p.start()
-    for p in ps:
-        p.join()
+    errors = _spawn_writers(addr, writers, per, nodes, inflight, timeout)
     elapsed = time.perf_counter() - t0
-    results = [q.get(timeout=5) for _ in ps]
-    errors = [r[1] for r in results if r[0] != "ok"]
-    if errors or any(p.exitcode != 0 for p in ps):
+    if errors:
         stop.set()
         srv.stop()
-        raise RuntimeError(f"store bench writers failed: {errors or [p.exitcode for p in ps]}")
+        raise RuntimeError(f"store bench writers failed: {errors}")
     # per pod: its node's watch sees bind (ADDED), Running, delete; its shard's watch the create
     # (ADDED) and the bind (DELETED: no longer unassigned); its namespace observer and every
     # whole-prefix watch all 4 events
@@ -165,6 +186,9 @@ def run(writers=4, pods=20000, nodes=64, all_watches=0, fan_threads=1, inflight=
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    if argv and argv[0] == "--writer":
+        return _writer_cli(argv[1:])
     ap = argparse.ArgumentParser("store-bench")
     ap.add_argument("--writers", type=int, default=4)
     ap.add_argument("--pods", type=int, default=20000)

@@ -293,7 +293,9 @@ class StoreServer:
                     self.address = f"tcp://127.0.0.1:{int(f.read())}"
                 os.unlink(port_file)
                 return self.address
-            if not self.tcp and os.path.exists(self.socket_path):
+            # both sockets: an API server probing the fan-out socket right after start() must find
+            # it (a slow start, e.g. the TSan build, used to leave it missing)
+            if not self.tcp and os.path.exists(self.socket_path) and os.path.exists(self.socket_path + ".watch"):
                 self.address = f"unix://{self.socket_path}"
                 return self.address
             time.sleep(0.01)
