@@ -51,7 +51,9 @@ def _xgmi4_summary(allstats):
     lat = [x for s in xs for x in s["lat"]]
     return {"xgmi4_pods_per_s": round(sum(s["pods"] for s in xs) / max(max(s["t"] for s in xs), 1e-9), 2),
             "xgmi4_p50_startup_ms": round(pct(lat, 0.5) * 1000, 2),
-            "xgmi4_single_hive_fraction": round(sum(s["single_hive"] for s in xs) / max(1, sum(s["total"] for s in xs)), 4)}
+            "xgmi4_single_hive_fraction": round(sum(s["single_hive"] for s in xs) / max(1, sum(s["total"] for s in xs)), 4),
+            # every pair of the 4 packages has a direct up xGMI link (amd.com/xgmi-peers)
+            "xgmi4_fully_linked_fraction": round(sum(s["linked"] for s in xs) / max(1, sum(s["total"] for s in xs)), 4)}
 
 
 def _interval_summary(allstats):
@@ -68,6 +70,13 @@ def _interval_summary(allstats):
         out[f"{name}_rate_avg_pods_per_s"] = round(avg, 1)
         out[f"{name}_rate_worst_1s_pods_per_s"] = round(worst, 1) if worst is not None else None
     return out
+
+
+def _linked(peers, node, ids):
+    got = [peers.get((node, i)) for i in ids]
+    if any(g is None for g in got):
+        return False
+    return all(a[0] == b[0] or ((a[1] >> b[0]) & 1 and (b[1] >> a[0]) & 1) for x, a in enumerate(got) for b in got[x + 1:])
 
 
 def cpu_budget():
@@ -149,7 +158,7 @@ def spawn_hollow_procs(args, url, rank, nprocs, tmp, payload_socket):
             continue
         cmd = [sys.executable, "-m", "kubernetes_amd.cmd.hollow_node", "--master", url, "--count", str(n),
                "--name-prefix", f"r{rank}p{j}", "--gpus-per-node", str(args.gpus_per_node),
-               "--hives", str(args.hives)]
+               "--hives", str(args.hives), "--links-down", args.links_down]
         if payload_socket:
             cmd += ["--payload-socket", payload_socket]
         if args.no_events:
@@ -253,6 +262,7 @@ def _cp_cpu(procs):
 async def rank_main(args, d: Dist, url, cp_procs=()):
     from kubernetes_amd.client.rest import Client
     from kubernetes_amd.kubemark.density import DensityRunner, pct
+    from kubernetes_amd.cmd.hollow_node import parse_links
     from kubernetes_amd.kubemark.hollow import HollowCluster
 
     loop = asyncio.get_running_loop()
@@ -276,7 +286,8 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         hprocs = spawn_hollow_procs(args, url, d.rank, args.hollow_procs, tempfile.mkdtemp(prefix="kamd-hollow-"), sock)
     else:
         hollow = HollowCluster(url, args.nodes_per_rank, prefix=f"r{d.rank}", gpus=args.gpus_per_node,
-                               hives=args.hives, payload=payload_fn, emit_events=not args.no_events)
+                               hives=args.hives, payload=payload_fn, emit_events=not args.no_events,
+                               links_down=parse_links(args.links_down))
         await hollow.start()
         await hollow.wait_registered()
     # wait until every rank's nodes are visible with their GPUs
@@ -351,13 +362,16 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
         await r4.start()
         x_lat, x_pods, x_t = [], 0, 0.0
         c = Client(url)
-        hive = {}
+        hive, peers = {}, {}
         for n in (await c.list("nodes"))["items"]:
             for rn, dom in ((n.get("status") or {}).get("extendedResources") or {}).items():
                 for i, dev in ((dom or {}).get("resources") or {}).items():
-                    hive[(n["metadata"]["name"], i)] = (dev.get("attributes") or {}).get("amd.com/xgmi-hive", "")
+                    a = dev.get("attributes") or {}
+                    hive[(n["metadata"]["name"], i)] = a.get("amd.com/xgmi-hive", "")
+                    if "amd.com/xgmi-peers" in a:
+                        peers[(n["metadata"]["name"], i)] = (int(a["amd.com/xgmi-node"]), int(a["amd.com/xgmi-peers"], 16))
         await c.close()
-        single = total = 0
+        single = total = linked = 0
         for k in range(args.xgmi4_steps):
             await abarrier()
             r = await r4.step(f"x{k}", timeout=args.step_timeout)
@@ -368,8 +382,10 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
                 node, ids = r4.assigned.get(name, (None, []))
                 total += 1
                 single += len(ids) == 4 and len({hive.get((node, i)) for i in ids}) == 1
+                linked += len(ids) == 4 and _linked(peers, node, ids)
         await r4.stop()
-        stats["xgmi4"] = {"lat": x_lat, "pods": x_pods, "t": x_t, "single_hive": single, "total": total}
+        stats["xgmi4"] = {"lat": x_lat, "pods": x_pods, "t": x_t, "single_hive": single, "total": total,
+                          "linked": linked}
     allstats = await loop.run_in_executor(None, d.allgather, stats)
     # keep serving other ranks' pods until everyone is done
     await abarrier()
@@ -400,6 +416,8 @@ def main():
     ap.add_argument("--gpus-per-node", type=int, default=8)
     ap.add_argument("--hives", type=int, default=2,
                     help="xGMI hives per hollow node (2 x 4 GPUs: the 4-GPU workload can land across hives)")
+    ap.add_argument("--links-down", default="",
+                    help="failed xGMI links in every hollow node's fake packages, e.g. '2-5' (pairwise-topology variant)")
     ap.add_argument("--gpus-per-pod", type=int, default=1)
     ap.add_argument("--pods-per-rank", type=int, default=0)
     ap.add_argument("--percentage-of-nodes-to-score", type=int, default=100)

@@ -37,6 +37,8 @@ ATTR_ECC = "amd.com/ecc"                  # uncorrectable ECC count
 ATTR_CUS = "amd.com/compute-units"
 ATTR_UUID = "amd.com/uuid"
 ATTR_XGMI_LINKS = "amd.com/xgmi-links"    # number of active xGMI links
+ATTR_XGMI_NODE = "amd.com/xgmi-node"      # the package's index inside its hive (0..7)
+ATTR_XGMI_PEERS = "amd.com/xgmi-peers"    # hex bitmask of hive indices reachable over an up xGMI link
 
 POD_PENDING, POD_RUNNING, POD_SUCCEEDED, POD_FAILED, POD_UNKNOWN = (
     "Pending", "Running", "Succeeded", "Failed", "Unknown")

@@ -31,7 +31,7 @@ class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
                  health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None,
-                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None):
+                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None, links_down=()):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
@@ -41,6 +41,7 @@ class LocalCluster:
         self.burn_in = burn_in                 # deviceplugin.burnin.BurnIn: gate GPUs on the HIP acceptance test
         self.dev_root = dev_root               # where the plugin finds /dev/kfd + /dev/dri (tests: mknod'd nodes)
         self.isolation = isolation             # process runtime: "auto" | "required" | "off"
+        self.links_down = tuple(tuple(x) for x in links_down)   # fake backend: failed xGMI links
         self.own_dir = workdir is None
         self.dir = workdir or tempfile.mkdtemp(prefix="kamd-cluster-")
         self.emit_events = emit_events
@@ -68,7 +69,8 @@ class LocalCluster:
         self.url = f"http://127.0.0.1:{port}"
         self.client = Client(self.url)
         if self.gpus:
-            fixture = None if self.real else amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition)
+            fixture = None if self.real else amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition,
+                                                                 links_down=self.links_down)
             self.smi = amdsmi.SMI(fixture=fixture)
         self.scheduler = Scheduler(Client(self.url), emit_events=self.emit_events, **self.scheduler_kwargs)
         self._sched_task = asyncio.ensure_future(self.scheduler.run())

@@ -8,6 +8,11 @@ from ..kubemark.hollow import HollowCluster
 from ._common import run_until_signal, setup_logging
 
 
+def parse_links(spec):
+    """'2-5,1-6' -> ((2, 5), (1, 6))"""
+    return tuple(tuple(int(x) for x in p.split("-")) for p in spec.split(",") if p.strip())
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser("hollow-node")
     ap.add_argument("--master", required=True)
@@ -17,6 +22,8 @@ def main(argv=None):
     ap.add_argument("--hives", type=int, default=1)
     ap.add_argument("--partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"],
                     help="compute-partition mode of the fake MI355X packages (CPX: 8 logical devices each)")
+    ap.add_argument("--links-down", default="",
+                    help="failed xGMI links of the fake packages, e.g. '2-5,1-6' (pairwise-topology fixtures)")
     ap.add_argument("--morph", default="kubelet", choices=["kubelet", "proxy"],
                     help="kubelet: hollow kubelets; proxy: hollow kube-proxies over a fake iptables (hollow-node.go:139+)")
     ap.add_argument("--payload-socket", default=None,
@@ -53,7 +60,7 @@ def main(argv=None):
             payload = PayloadClient(a.payload_socket)
         h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives, payload=payload,
                           emit_events=not a.no_events, status_freq=a.node_status_update_frequency,
-                          partition=a.partition)
+                          partition=a.partition, links_down=parse_links(a.links_down))
         await h.start()
         await h.wait_registered()
         if a.ready_file:

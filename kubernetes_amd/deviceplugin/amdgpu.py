@@ -40,7 +40,35 @@ ATTR_MFMA_FP8_TFLOPS = "amd.com/mfma-fp8-tflops"   # measured fp8 (e4m3, block-s
 log = logging.getLogger("amdgpu-plugin")
 
 
-def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None) -> dict:
+def xgmi_peer_map(smi: amdsmi.SMI, gpus) -> dict:
+    """Pairwise xGMI connectivity inside each hive, from the SMI link table
+    (`amdsmi_topo_get_link_type` + `amdsmi_is_P2P_accessible`): device index ->
+    (hive-local package index, bitmask of hive-local indices it reaches over a direct xGMI link).
+    A package is indexed by its rank among the hive's packages (ordered by socket); compute
+    partitions of one package share its index and reach each other on-package."""
+    by_hive: dict = {}
+    for g in gpus:
+        by_hive.setdefault(g.xgmi_hive_id, set()).add(g.socket if g.socket >= 0 else g.index)
+    local = {h: {s: k for k, s in enumerate(sorted(socks))} for h, socks in by_hive.items()}
+    rep = {}                                  # (hive, socket) -> one device index of that package
+    for g in gpus:
+        rep.setdefault((g.xgmi_hive_id, g.socket if g.socket >= 0 else g.index), g.index)
+    out = {}
+    for g in gpus:
+        sock = g.socket if g.socket >= 0 else g.index
+        me = local[g.xgmi_hive_id][sock]
+        mask = 1 << me
+        for other, k in local[g.xgmi_hive_id].items():
+            if other == sock:
+                continue
+            lk = smi.link(g.index, rep[(g.xgmi_hive_id, other)])
+            if lk.type == amdsmi.LINK_XGMI and lk.p2p:
+                mask |= 1 << k
+        out[g.index] = (me, mask)
+    return out
+
+
+def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None, peers: tuple | None = None) -> dict:
     # usable VRAM is reported a few MiB below the 288 GB HBM3E stack size: round up to GiB
     hbm_gib = -(-g.vram_total_mb // 1024)
     attrs = {
@@ -67,6 +95,9 @@ def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None) -> dict:
     if m is not None:
         attrs[core.ATTR_ECC] = str(m.ecc_uncorrectable)
         attrs[core.ATTR_XGMI_LINKS] = str(m.xgmi_links_up)
+    if peers is not None:
+        attrs[core.ATTR_XGMI_NODE] = str(peers[0])
+        attrs[core.ATTR_XGMI_PEERS] = f"{peers[1]:x}"
     return attrs
 
 
@@ -87,6 +118,11 @@ class AMDGPUPlugin(DevicePluginServer):
         all_gpus = self.smi.gpus()
         self.gpus = [g for g in all_gpus if indices is None or g.index in indices]
         self.by_id = {g.device_id_str: g for g in self.gpus}
+        # published per device so the scheduler places a multi-GPU set on a clique of the link
+        # graph, not merely on devices with enough links (a 6/7-link GPU must not be paired with
+        # the one peer it cannot reach)
+        self._all_gpus = all_gpus
+        self.peers = xgmi_peer_map(self.smi, all_gpus)
         self._ecc_base = {}
         self._health = {}
         devs = []
@@ -110,7 +146,7 @@ class AMDGPUPlugin(DevicePluginServer):
 
     # -- health -------------------------------------------------------------
     def _device(self, g: amdsmi.GPU, m: amdsmi.Metrics, health: str):
-        attrs = gpu_attributes(g, m)
+        attrs = gpu_attributes(g, m, self.peers.get(g.index))
         if self.burn_in is not None:
             r = self._burn.get(g.device_id_str)
             attrs[ATTR_BURN_IN] = PENDING if r is None else (PASSED if r.ok else FAILED)
@@ -138,6 +174,11 @@ class AMDGPUPlugin(DevicePluginServer):
         """Re-evaluate health; push a new list if anything changed. Returns True if changed."""
         changed = False
         devs = []
+        peers = xgmi_peer_map(self.smi, self._all_gpus)
+        if peers != self.peers:
+            log.warning("xGMI peer map changed: %s -> %s", self.peers, peers)
+            self.peers = peers
+            changed = True
         for g in self.gpus:
             m = self.smi.metrics(g.index)
             h = self._check(g, m)

@@ -26,12 +26,13 @@ class HollowCluster:
     """A set of hollow nodes sharing one process / event loop / API client pool."""
 
     def __init__(self, master, count, prefix="hollow", gpus=8, hives=1, payload=None, workdir=None,
-                 emit_events=False, status_freq=10.0, max_conns=32, partition="SPX"):
+                 emit_events=False, status_freq=10.0, max_conns=32, partition="SPX", links_down=()):
         self.master = master
         self.count = count
         self.prefix = prefix
         self.gpus = gpus
         self.hives = hives
+        self.links_down = tuple(tuple(x) for x in links_down)
         self.partition = partition
         self.payload = payload
         self.own_dir = workdir is None
@@ -45,7 +46,8 @@ class HollowCluster:
 
     async def start(self):
         if self.gpus:
-            self.smi = amdsmi.SMI(fixture=amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition))
+            self.smi = amdsmi.SMI(fixture=amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition,
+                                                              links_down=self.links_down))
         for i in range(self.count):
             name = f"{self.prefix}-{i}"
             pdir = os.path.join(self.dir, name, "plugins")

@@ -167,6 +167,8 @@ def _load():
         L.kamd_process_list.argtypes = [ctypes.c_int, ctypes.POINTER(_Proc), ctypes.c_int]
         L.kamd_fake_set_ecc.argtypes = [ctypes.c_int, ctypes.c_uint64]
         L.kamd_fake_set_links_up.argtypes = [ctypes.c_int, ctypes.c_uint32]
+        L.kamd_fake_set_link.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.kamd_fake_set_procs.argtypes = [ctypes.c_int, ctypes.POINTER(_Proc), ctypes.c_int]
         L.kamd_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -225,20 +227,33 @@ class SMI:
     def fake_set_links_up(self, i, n):
         return self.L.kamd_fake_set_links_up(i, n)
 
+    def fake_set_link(self, a, b, xgmi: bool):
+        """Fake backend: bring the xGMI link between devices a and b up or down (both ways)."""
+        t = LINK_XGMI if xgmi else LINK_PCIE
+        return self.L.kamd_fake_set_link(a, b, t) | self.L.kamd_fake_set_link(b, a, t)
+
+    def fake_set_procs(self, i, procs):
+        """Fake backend: the GPU process list of device i, [(pid, name, vram_bytes, gfx_ns)]."""
+        arr = (_Proc * max(1, len(procs)))()
+        for k, (pid, name, vram, gfx) in enumerate(procs):
+            arr[k].pid, arr[k].name, arr[k].vram_bytes, arr[k].gfx_ns = pid, name.encode()[:STR - 1], vram, gfx
+        return self.L.kamd_fake_set_procs(i, arr, len(procs))
+
     def topology(self):
         n = self.count()
         return [[self.link(i, j) for j in range(n)] for i in range(n)]
 
 
 def mi355x_fixture(n=8, hive_id=0x3C4D5E6F7081, hives=1, partition="SPX", numa_per=4, seed="node0",
-                   memory_partition="NPS1") -> dict:
+                   memory_partition="NPS1", links_down=()) -> dict:
     """Fixture for an n-GPU MI355X UBB node (8 OAMs, all-to-all xGMI: 7 links per GPU).
     `hives` > 1 splits the GPUs into several hives (to exercise hive-aware allocation).
 
     `partition` is the compute-partition mode: SPX exposes each package as one device, DPX /
     QPX / CPX split its 8 XCDs into 2 / 4 / 8 logical devices, each with its own render node,
     1/k of the CUs and 1/k of the HBM (as AMD SMI reports a partition). Partitions of one
-    package share `socket` and its xGMI links."""
+    package share `socket` and its xGMI links. `links_down`: package pairs (a, b) whose direct xGMI
+    link is down (the pair is reachable over PCIe only; both report one link fewer)."""
     per = PARTITIONS_PER_SOCKET.get(partition, 1)
     devs = []
     per_hive = max(1, n // hives)
@@ -253,16 +268,22 @@ def mi355x_fixture(n=8, hive_id=0x3C4D5E6F7081, hives=1, partition="SPX", numa_p
                 "render_minor": 128 + k, "card_minor": k, "hsa_id": k, "hip_id": k, "xgmi_hive_id": h,
                 "xgmi_node_id": i, "numa_node": i // numa_per, "partition": partition, "partition_id": p,
                 "socket": i, "memory_partition": memory_partition, "serial": f"{seed}-SN{i:04d}",
-                "xgmi_links_total": 7, "xgmi_links_up": 7 if per_hive == 8 else per_hive - 1,
+                "xgmi_links_total": 7,
+                "xgmi_links_up": (7 if per_hive == 8 else per_hive - 1) - sum(1 for a, b in links_down if i in (a, b)),
             })
-    return {"devices": devs}
+    links = []
+    for a, b in links_down:
+        for pa in range(per):
+            for pb in range(per):
+                links += [[a * per + pa, b * per + pb, LINK_PCIE, 2, 40], [b * per + pb, a * per + pa, LINK_PCIE, 2, 40]]
+    return {"devices": devs, "links": links}
 
 
 _FIXTURE_CACHE = {}
 
 
 def fixture_file(n=8, **kw) -> str:
-    key = (n, tuple(sorted(kw.items())))
+    key = (n, tuple(sorted((k, tuple(map(tuple, v)) if k == "links_down" else v) for k, v in kw.items())))
     p = _FIXTURE_CACHE.get(key)
     if p and os.path.exists(p):
         return p

@@ -11,8 +11,12 @@ MI355X-first design:
   * an N-GPU request is placed inside ONE xGMI hive — RCCL rings are per-link bound, so an
     N-GPU job wants N GPUs that can drive N-1 links each. The hive with the fewest free
     devices that still fits is chosen (best fit: keeps whole hives free for big jobs);
-    inside it, a NUMA node that holds the whole set is preferred; every chosen device must
-    report at least N-1 healthy xGMI links;
+    inside it, a NUMA node that holds the whole set is preferred; the chosen packages must be
+    pairwise linked: the plugin publishes each device's hive index and the bitmask of hive
+    peers it reaches over an up xGMI link (`amd.com/xgmi-node` / `amd.com/xgmi-peers`, from
+    `amdsmi_topo_get_link_type`), and the set must be a clique of that graph — a GPU that
+    booted with 6/7 links is never paired with the peer it cannot reach. (Devices without the
+    peer attributes fall back to "at least N-1 healthy xGMI links each".)
   * single-GPU pods pack into the most-used hive / NUMA node first (anti-fragmentation);
   * compute partitions (SPX/DPX/QPX/CPX: 1/2/4/8 logical devices per package, sharing its
     `amd.com/socket`) — partitions of one package talk over the on-package fabric, so a
@@ -27,6 +31,8 @@ Returns a binding `{er_name: {"resources": [ids]}}` plus a 0..10 topology score 
 `XGMITopology` priority.
 """
 from __future__ import annotations
+
+from itertools import combinations
 
 from ..api import core
 from ..api.labels import SelectorError, node_selector_requirements_as_selector
@@ -78,6 +84,49 @@ def _need_links(dev, n):
     return n - 1 if p == 1 else -(-n // p) - 1
 
 
+def _peer(dev):
+    """(hive index, peer bitmask) or None when the plugin does not publish pairwise links."""
+    a = dev.get("attributes") or {}
+    node, peers = a.get(core.ATTR_XGMI_NODE), a.get(core.ATTR_XGMI_PEERS)
+    if node is None or peers is None:
+        return None
+    try:
+        return int(node), int(peers, 16)
+    except ValueError:
+        return None
+
+
+def _clique(devs, n):
+    """The first n-subset of devs (list of (id, dev), in preference order) whose packages are
+    pairwise xGMI-linked, preferring sets inside one NUMA node; None if there is none. Returns
+    (chosen, numa_fit). Small by construction: at most 8 packages per hive (C(8,4) = 70)."""
+    info = [_peer(d) for _, d in devs]
+    if any(x is None for x in info):
+        return None
+    numa = [(d.get("attributes") or {}).get(core.ATTR_NUMA, "") for _, d in devs]
+    best = None
+    for combo in combinations(range(len(devs)), n):
+        ok = True
+        for a, b in combinations(combo, 2):
+            na, ma = info[a]
+            nb, mb = info[b]
+            if na != nb and not ((ma >> nb) & 1 and (mb >> na) & 1):
+                ok = False
+                break
+        if not ok:
+            continue
+        fit = len({numa[k] for k in combo}) == 1
+        if fit:
+            return [devs[k] for k in combo], True
+        if best is None:
+            best = [devs[k] for k in combo]
+    return (best, False) if best is not None else None
+
+
+def _has_peers(devs):
+    return bool(devs) and all(_peer(d) is not None for _, d in devs)
+
+
 def _sock(did, dev):
     return (dev.get("attributes") or {}).get(core.ATTR_SOCKET, did)
 
@@ -111,6 +160,19 @@ def feasible(requests, er, policy=PREFERRED):
             return False, 0, f"no single xGMI hive has {n} free {r.rname}"
         return True, sc, ""
     need_links = n - 1 if n > 1 else 0
+    if n > 1 and first is not None and _peer(first) is not None:
+        # pairwise topology published: a hive qualifies if its free devices hold a clique of n
+        ok = sorted(((len(devs), h, devs) for h, devs in hives.items() if len(devs) >= n), key=lambda t: (t[0], t[1]))
+        for c, _, devs in ok:
+            items = sorted(devs.items(), key=lambda x: _idx(x[1]))
+            got = _clique(items, n)
+            if got is not None:
+                return True, _score(c, n, got[1]), ""
+        if sum(len(d) for d in hives.values()) < n:
+            return False, 0, f"Insufficient {r.rname}"
+        if policy == REQUIRED:
+            return False, 0, f"no xGMI-connected set of {n} free {r.rname} in one hive"
+        return True, 1.0, ""
     best = None
     total = 0
     for h, devs in hives.items():
@@ -158,14 +220,14 @@ def allocate(requests, er, policy=PREFERRED):
             attrs = dev.get("attributes") or {}
             if sel is not None and not sel.matches(attrs):
                 continue
-            if r.count > 1 and _links(dev) < _need_links(dev, r.count):
+            if r.count > 1 and _peer(dev) is None and _links(dev) < _need_links(dev, r.count):
                 continue
             cands.append((did, dev))
         if len(cands) < r.count:
             return None, 0, f"Insufficient {r.rname}"
         ids, s = _pick(cands, r.count, policy)
         if ids is None:
-            return None, 0, f"no single xGMI hive has {r.count} free {r.rname}"
+            return None, 0, f"no xGMI-connected set of {r.count} free {r.rname} in one hive"
         binding[r.name] = {"resources": ids}
         taken.update(ids)
         score_sum += s
@@ -182,6 +244,15 @@ def _group(cands, key):
 def _pick(cands, n, policy):
     hives = _group(cands, core.ATTR_HIVE)
     fitting = [(len(v), h, v) for h, v in hives.items() if len(v) >= n]
+    if n > 1 and fitting and all(_has_peers(v) and not any(_pps(d) > 1 for _, d in v) for _, _, v in fitting):
+        # best-fit hive first, but only a hive whose free packages hold a linked n-clique
+        fitting.sort(key=lambda t: (t[0], t[1]))
+        for free, _, devs in fitting:
+            got = _clique(sorted(devs, key=lambda x: _idx(x[1])), n)
+            if got is not None:
+                chosen, numa_fit = got
+                return [d for d, _ in chosen], _score(free, n, numa_fit)
+        fitting = []
     if fitting:
         # best fit: the hive with the fewest free devices that still holds n
         fitting.sort(key=lambda t: (t[0], t[1]))

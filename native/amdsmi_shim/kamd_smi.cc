@@ -147,6 +147,7 @@ void copy_str(char* dst, size_t n, const std::string& s) {
 struct FakeDev {
   kamd_device_info_t info;
   kamd_metrics_t m;
+  std::vector<kamd_proc_t> procs;
 };
 
 struct FakeBackend : Backend {
@@ -166,7 +167,8 @@ struct FakeBackend : Backend {
     int idx = 0;
     for (const JVal& d : ds->a) {
       FakeDev fd;
-      memset(&fd, 0, sizeof(fd));
+      memset(&fd.info, 0, sizeof fd.info);
+      memset(&fd.m, 0, sizeof fd.m);
       kamd_device_info_t& in = fd.info;
       in.index = idx;
       copy_str(in.uuid, sizeof in.uuid, d.str("uuid", ""));
@@ -242,7 +244,14 @@ struct FakeBackend : Backend {
   int info(int i, kamd_device_info_t* o) override { *o = devs[i].info; return 0; }
   int link(int s, int d, kamd_link_t* o) override { *o = links[s][d]; return 0; }
   int metrics(int i, kamd_metrics_t* o) override { *o = devs[i].m; return 0; }
-  int procs(int, kamd_proc_t*, int) override { return 0; }
+  int procs(int i, kamd_proc_t* o, int max) override {
+    int k = 0;
+    for (const kamd_proc_t& p : devs[i].procs) {
+      if (k >= max) break;
+      o[k++] = p;
+    }
+    return k;
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -582,6 +591,25 @@ int kamd_fake_set_ecc(int idx, uint64_t unc) {
   std::lock_guard<std::mutex> l(g_mu);
   if (g_backend != KAMD_BACKEND_FAKE || !valid(idx)) return -1;
   static_cast<FakeBackend*>(g_b.get())->devs[idx].m.ecc_uncorrectable = unc;
+  return 0;
+}
+
+int kamd_fake_set_procs(int idx, const kamd_proc_t* procs, int n) {
+  std::lock_guard<std::mutex> l(g_mu);
+  if (g_backend != KAMD_BACKEND_FAKE || !valid(idx) || n < 0) return -1;
+  auto& v = static_cast<FakeBackend*>(g_b.get())->devs[idx].procs;
+  v.assign(procs, procs + n);
+  return 0;
+}
+
+int kamd_fake_set_link(int s, int d, int type) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_b || g_backend != KAMD_BACKEND_FAKE) return -1;
+  auto* fb = static_cast<FakeBackend*>(g_b.get());
+  int n = (int)fb->devs.size();
+  if (s < 0 || d < 0 || s >= n || d >= n) return -1;
+  fb->links[s][d].type = type;
+  fb->links[s][d].p2p = type == 2;
   return 0;
 }
 

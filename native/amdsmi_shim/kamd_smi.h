@@ -87,6 +87,10 @@ int kamd_process_list(int idx, kamd_proc_t* out, int max_procs);
 // Fake backend only: mutate health-relevant state (for device-plugin health tests).
 int kamd_fake_set_ecc(int idx, uint64_t uncorrectable);
 int kamd_fake_set_links_up(int idx, uint32_t up);
+// type: 2 = xGMI, 1 = PCIe (a failed xGMI link between two packages of a hive)
+int kamd_fake_set_link(int src, int dst, int type);
+// replace the process list of a device (amdsmi_get_gpu_process_list of the fake backend)
+int kamd_fake_set_procs(int idx, const kamd_proc_t* procs, int n);
 const char* kamd_last_error(void);
 void kamd_shutdown(void);
 
