@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import argparse
 
-from ..monitoring.exporter import AMDSMIExporter, kubelet_pods_fn
+from ..monitoring.exporter import AMDSMIExporter, kubelet_pods_fn, kubelet_stats_fn
 from ..native import amdsmi
 from ._common import run_until_signal, setup_logging
 
@@ -20,7 +20,8 @@ def main(argv=None):
 
     async def start():
         ex = AMDSMIExporter(amdsmi.SMI(fixture=a.fixture), a.node_name,
-                            pods_fn=kubelet_pods_fn(a.kubelet) if a.kubelet else None)
+                            pods_fn=kubelet_pods_fn(a.kubelet) if a.kubelet else None,
+                            stats_fn=kubelet_stats_fn(a.kubelet) if a.kubelet else None)
         port = await ex.start("0.0.0.0", a.port)
         print(f"amd-smi exporter serving {len(ex.gpus)} GPU(s) on :{port}", flush=True)
         return ex

@@ -110,6 +110,11 @@ class Runtime:
     def list_containers(self):
         return []
 
+    def container_pids(self) -> dict:
+        """{container id: host pid of its root process} for running containers (GPU process
+        attribution in the summary API). Runtimes without host processes return {}."""
+        return {}
+
     def isolation_status(self) -> dict | None:
         """Whether the runtime enforces a container's device view (mount namespace + private /dev
         + device cgroup): {"enforced": bool, "reason": str, "message": str}. None = not applicable

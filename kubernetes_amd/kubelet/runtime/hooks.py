@@ -163,3 +163,12 @@ class HookedRuntime(Runtime):
 
     def list_containers(self):
         return [c for rt in self.runtimes.values() for c in rt.list_containers()]
+
+    def container_pids(self):
+        out = {}
+        for rt in self.runtimes.values():
+            out.update(rt.container_pids())
+        return out
+
+    def isolation_status(self):
+        return self.runtimes[self.default].isolation_status()

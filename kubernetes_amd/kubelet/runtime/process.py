@@ -578,6 +578,10 @@ class ProcessRuntime(Runtime):
             except OSError:
                 pass
 
+    def container_pids(self):
+        return {cid: m["proc"].pid for cid, m in self.meta.items()
+                if m.get("proc") is not None and m["proc"].returncode is None}
+
     async def kill_all(self):
         """Kill every container and sandbox process group of this runtime (cluster teardown)."""
         procs = [m["proc"] for m in self.meta.values() if m.get("proc") is not None] + \

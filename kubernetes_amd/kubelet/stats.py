@@ -3,15 +3,26 @@
 Parity: `pkg/kubelet/apis/stats/v1alpha1/types.go:121-122,213-234` (`ContainerStats.Accelerators`:
 make, model, id, memoryTotal, memoryUsed, dutyCycle) filled in the reference by cAdvisor's NVML
 collector (`vendor/github.com/google/cadvisor/accelerators/nvidia.go:172-222`, devices cgroup
-char major 195). Here the container -> GPU mapping comes from the allocation record itself
-(`spec.extendedResources[].assigned`), and the numbers from AMD SMI through the native shim.
+char major 195), which reports the DEVICE's memory use for every container holding it. Here:
+  * the container -> GPU mapping comes from the allocation record itself
+    (`spec.extendedResources[].assigned`);
+  * memory is attributed PER CONTAINER: AMD SMI's per-process list
+    (`amdsmi_get_gpu_process_list`: pid, VRAM, gfx engine ns) is joined with the runtime's
+    container processes (a GPU process belongs to the container whose root process is its
+    ancestor), so two pods sharing a GPU (compute partitions, or a multi-tenant device) are not
+    both charged the whole device. `memoryUsed` is the container's own VRAM, `deviceMemoryUsed`
+    the device's; `dutyCycle` is the container's share of the gfx engine over the last sampling
+    interval when its processes report engine time, else the device's activity.
 """
 from __future__ import annotations
 
+import logging
 import time
 
 from ..api import core
 from ..api.meta import now_rfc3339
+
+log = logging.getLogger("kubelet.stats")
 
 
 def _gpu_index(dm):
@@ -20,33 +31,80 @@ def _gpu_index(dm):
     return (cap.get(core.AMD_GPU) or {}).get("resources") or {}
 
 
-def accelerator_stats(kubelet, ids):
+def _ppid(pid):
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return int(f.read().rsplit(")", 1)[1].split()[1])
+    except (OSError, ValueError, IndexError):
+        return 0
+
+
+def gpu_process_usage(kubelet):
+    """{container id: {gpu index: (vram bytes, gfx engine ns)}} from AMD SMI's process lists,
+    each GPU process charged to the container whose root process is its ancestor."""
+    smi = getattr(kubelet, "smi", None)
+    pids_fn = getattr(kubelet.runtime, "container_pids", None)
+    if smi is None or pids_fn is None:
+        return {}
+    roots = {pid: cid for cid, pid in pids_fn().items()}
+    if not roots:
+        return {}
+    from ..native.amdsmi import SMIError
+    out: dict = {}
+    for i in range(smi.count()):
+        try:
+            procs = smi.processes(i)
+        except SMIError as e:
+            log.warning("AMD SMI process list of GPU %d: %s", i, e)
+            continue
+        for p in procs:
+            pid, depth = p.pid, 0
+            while pid > 1 and pid not in roots and depth < 64:
+                pid, depth = _ppid(pid), depth + 1
+            cid = roots.get(pid)
+            if cid is None:
+                continue
+            vram, gfx = out.setdefault(cid, {}).get(i, (0, 0))
+            out[cid][i] = (vram + p.vram_bytes, gfx + p.gfx_ns)
+    return out
+
+
+def accelerator_stats(kubelet, ids, usage=None, cid=None, now=None):
+    """ContainerStats.Accelerators for the device IDs a container holds. `usage`: the result of
+    gpu_process_usage() for this summary (per-container VRAM / engine time)."""
     devs = _gpu_index(kubelet.dm)
-    smi = None
-    h = getattr(kubelet.dm, "handler", None)
+    smi = getattr(kubelet, "smi", None)
+    mine = (usage or {}).get(cid, {}) if cid else {}
+    samples = kubelet.__dict__.setdefault("_gfx_samples", {})
     out = []
     for i in ids:
         d = devs.get(i)
         if d is None:
             continue
         attrs = d.get("attributes") or {}
+        idx = int(attrs.get(core.ATTR_INDEX, "0"))
         entry = {"make": "amd", "model": attrs.get(core.ATTR_PRODUCT, ""), "id": i,
                  "memoryTotal": int(attrs.get(core.ATTR_MEMORY, "0")) << 20, "memoryUsed": 0, "dutyCycle": 0}
-        try:
-            from ..native import amdsmi
-            if smi is None:
-                smi = getattr(kubelet, "smi", None)
-            if smi is not None:
-                m = smi.metrics(int(attrs.get(core.ATTR_INDEX, "0")))
-                entry["memoryUsed"] = m.vram_used_bytes
+        if smi is not None:
+            from ..native.amdsmi import SMIError
+            try:
+                m = smi.metrics(idx)
+            except SMIError as e:
+                log.warning("AMD SMI metrics of GPU %d: %s", idx, e)
+                m = None
+            if m is not None:
+                entry["deviceMemoryUsed"] = m.vram_used_bytes
                 entry["dutyCycle"] = m.gfx_activity
                 entry["powerWatts"] = m.power_w
                 entry["temperatureC"] = m.temp_hotspot_c
-            del amdsmi
-        except Exception:
-            pass
+        if idx in mine:
+            vram, gfx = mine[idx]
+            entry["memoryUsed"] = vram
+            prev = samples.get((cid, idx))
+            samples[(cid, idx)] = (now or time.time(), gfx)
+            if prev is not None and gfx and now and now > prev[0]:
+                entry["dutyCycle"] = max(0, min(100, int(round((gfx - prev[1]) / ((now - prev[0]) * 1e9) * 100))))
         out.append(entry)
-    del h
     return out
 
 
@@ -96,6 +154,7 @@ def summary(kubelet):
         kubelet._cpu_samples = {}
     pods = []
     node_cpu = node_mem = 0
+    usage = gpu_process_usage(kubelet)
     for st in kubelet.pods.values():
         pod = st.pod
         md = pod["metadata"]
@@ -110,7 +169,7 @@ def summary(kubelet):
                 cs["memory"].update(workingSetBytes=u["workingSetBytes"], usageBytes=u["workingSetBytes"])
                 node_cpu += u["usageNanoCores"]
                 node_mem += u["workingSetBytes"]
-            acc = accelerator_stats(kubelet, ids)
+            acc = accelerator_stats(kubelet, ids, usage, cid, t)
             sim_gpu = (md.get("annotations") or {}).get(SIM_GPU)
             if acc and sim_gpu is not None:
                 for a in acc:

@@ -48,12 +48,13 @@ GPU_METRICS = [
 
 
 class AMDSMIExporter:
-    def __init__(self, smi: amdsmi.SMI | None = None, node_name="", pods_fn=None, health_fn=None):
+    def __init__(self, smi: amdsmi.SMI | None = None, node_name="", pods_fn=None, health_fn=None, stats_fn=None):
         self.smi = smi or amdsmi.SMI()
         self.node = node_name
         self.gpus = self.smi.gpus()
         self.pods_fn = pods_fn          # async () -> list of pods on this node (allocation records)
         self.health_fn = health_fn      # (device id) -> "Healthy"/"Unhealthy"
+        self.stats_fn = stats_fn        # async () -> the kubelet's /stats/summary (per-container VRAM)
         self.http = None
         self.scrapes = 0
 
@@ -99,6 +100,32 @@ class AMDSMIExporter:
                         lab = {"namespace": p["metadata"].get("namespace", ""), "pod": p["metadata"]["name"],
                                "container": c["name"], "uuid": did, "gpu": g.index if g else "", "node": self.node}
                         lines.append(f"amd_gpu_pod_allocated{_labels(lab)} 1")
+        if self.stats_fn is not None:
+            # per-container attribution is the kubelet's (AMD SMI process list joined with the
+            # runtime's container processes): the exporter republishes it per pod
+            try:
+                summ = await self.stats_fn()
+            except Exception as e:  # scrape must not fail because the kubelet is down
+                log.warning("per-pod GPU usage unavailable: %s", e)
+                summ = {}
+            by_id = {g.device_id_str: g for g in self.gpus}
+            rows = []
+            for p in summ.get("pods") or ():
+                ref = p.get("podRef") or {}
+                for c in p.get("containers") or ():
+                    for a in c.get("accelerators") or ():
+                        g = by_id.get(a.get("id"))
+                        lab = {"namespace": ref.get("namespace", ""), "pod": ref.get("name", ""), "container": c.get("name", ""),
+                               "uuid": a.get("id", ""), "gpu": g.index if g else "", "node": self.node}
+                        rows.append((lab, a))
+            lines.append("# HELP amd_gpu_pod_vram_bytes HBM used by the container's own GPU processes (bytes)")
+            lines.append("# TYPE amd_gpu_pod_vram_bytes gauge")
+            for lab, a in rows:
+                lines.append(f"amd_gpu_pod_vram_bytes{_labels(lab)} {int(a.get('memoryUsed', 0))}")
+            lines.append("# HELP amd_gpu_pod_gfx_busy_percent the container's share of the gfx engine (%)")
+            lines.append("# TYPE amd_gpu_pod_gfx_busy_percent gauge")
+            for lab, a in rows:
+                lines.append(f"amd_gpu_pod_gfx_busy_percent{_labels(lab)} {int(a.get('dutyCycle', 0))}")
         lines.append("# TYPE amd_smi_exporter_scrape_seconds gauge")
         lines.append(f"amd_smi_exporter_scrape_seconds {time.perf_counter() - t0:.6f}")
         return "\n".join(lines) + "\n"
@@ -119,6 +146,19 @@ class AMDSMIExporter:
     async def stop(self):
         if self.http:
             await self.http.stop()
+
+
+def kubelet_stats_fn(kubelet_url):
+    from ..client.http import HTTPClient
+
+    async def fn():
+        c = HTTPClient(kubelet_url)
+        try:
+            st, body = await c.request("GET", "/stats/summary")
+        finally:
+            await c.close()
+        return json.loads(body) if st == 200 else {}
+    return fn
 
 
 def kubelet_pods_fn(kubelet_url):

@@ -93,3 +93,41 @@ def test_burn_in_gates_real_gpus_then_pod_runs(run):
             p = await cl.wait_pod("after-burn-in", timeout=30)
             assert p["spec"]["extendedResources"][0]["assigned"][0] in passed
     run(main(), timeout=150)
+
+
+def test_pod_vram_attribution_on_mi355x(run):
+    """A pod holding 1 GiB of HBM shows up with ~1 GiB in the kubelet summary API: AMD SMI's
+    process list (amdsmi_get_gpu_process_list) joined with the pod's container process."""
+    import asyncio
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kubernetes_amd.api import core
+    from kubernetes_amd.cluster import LocalCluster
+    from kubernetes_amd.kubelet import stats
+
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=8, runtime="process", real_gpus=True) as cl:
+            await cl.client.create("pods", {"metadata": {"name": "hold"}, "spec": {"restartPolicy": "Never", "containers": [
+                {"name": "c", "image": "kubernetes-amd/hip-vector-add", "args": ["--hold-mib", "1024", "--hold-seconds", "30"],
+                 "resources": {"limits": {core.AMD_GPU: "1"}}}]}})
+            p = await cl.wait_pod("hold", timeout=60)
+            kl = cl.nodes[0].kubelet
+            cid = kl.pods[p["metadata"]["uid"]].containers["c"]
+            log_path = kl.runtime.container_status(cid).log_path
+
+            async def holding():
+                return "HOLDING" in open(log_path).read()
+            await cl.wait_for(holding, 30, 0.1)
+            used = 0
+            for _ in range(50):
+                s = stats.summary(kl)
+                acc = [c["accelerators"][0] for q in s["pods"] for c in q["containers"] if c.get("accelerators")]
+                used = acc[0]["memoryUsed"] if acc else 0
+                if used >= 1 << 30:
+                    break
+                await asyncio.sleep(0.2)
+            print("memoryUsed", used, "deviceMemoryUsed", acc[0].get("deviceMemoryUsed") if acc else None)
+            assert (1 << 30) <= used <= (2 << 30), (used, acc)
+            await cl.client.delete("pods", "hold", "default")
+    run(main(), timeout=150)
