@@ -171,7 +171,60 @@ _RESTART = ("Always", "OnFailure", "Never")
 _PULL = ("Always", "IfNotPresent", "Never")
 
 
-def _validate_container_list(cs, path, require):
+_DNS_POLICIES = ("ClusterFirstWithHostNet", "ClusterFirst", "Default", "None")
+_PROTOCOLS = ("TCP", "UDP")
+_TERM_MSG = ("File", "FallbackToLogsOnError")
+_TOL_OPS = ("Exists", "Equal")
+C_IDENTIFIER = re.compile(r"^[A-Za-z_][A-Za-z0-9_]*$")
+ENV_VAR_NAME = re.compile(r"^[-._a-zA-Z][-._a-zA-Z0-9]*$")
+IANA_SVC_NAME = re.compile(r"^[a-z0-9]([a-z0-9-]*[a-z0-9])?$")
+_VOLUME_SOURCES = ("hostPath", "emptyDir", "gcePersistentDisk", "awsElasticBlockStore", "gitRepo", "secret", "nfs",
+                   "iscsi", "glusterfs", "persistentVolumeClaim", "rbd", "flexVolume", "cinder", "cephfs", "flocker",
+                   "downwardAPI", "fc", "azureFile", "configMap", "vsphereVolume", "quobyte", "azureDisk",
+                   "photonPersistentDisk", "projected", "portworxVolume", "scaleIO", "storageos", "csi")
+
+
+def _is_int(v):
+    return isinstance(v, int) and not isinstance(v, bool)
+
+
+def _non_negative(v, path, errs, positive=False):
+    if v is None:
+        return
+    if not _is_int(v) or v < (1 if positive else 0):
+        errs.append(invalid(path, f"{v!r}: must be greater than {'' if positive else 'or equal to '}0"))
+
+
+def _validate_probe(pr, path):
+    errs = []
+    if pr is None:
+        return errs
+    handlers = [k for k in ("exec", "httpGet", "tcpSocket") if pr.get(k) is not None]
+    if len(handlers) != 1:
+        errs.append(required(path, "must specify exactly 1 handler type (exec, httpGet, tcpSocket)"))
+    for k in ("successThreshold", "failureThreshold"):
+        _non_negative(pr.get(k), f"{path}.{k}", errs)
+    for k in ("initialDelaySeconds", "timeoutSeconds", "periodSeconds"):
+        # deviation: fractional seconds are accepted (sub-second probes in tests and hollow nodes);
+        # the reference's int32 fields are a subset
+        v = pr.get(k)
+        if v is not None and (isinstance(v, bool) or not isinstance(v, (int, float)) or v < 0):
+            errs.append(invalid(f"{path}.{k}", f"{v!r}: must be greater than or equal to 0"))
+    return errs
+
+
+def _validate_port_number(v, path, errs, allow_name=True):
+    if _is_int(v):
+        if not 0 < v < 65536:
+            errs.append(invalid(path, f"{v}: must be between 1 and 65535, inclusive"))
+    elif allow_name and isinstance(v, str) and v:
+        if not (len(v) <= 15 and IANA_SVC_NAME.match(v) and any(ch.isalpha() for ch in v)):
+            errs.append(invalid(path, f"{v!r}: must contain only alpha-numeric characters (a-z, 0-9) and hyphens"))
+    else:
+        errs.append(invalid(path, f"{v!r}: must be a port number or name"))
+
+
+def _validate_container_list(cs, path, require, volumes=None):
     errs = []
     if not cs:
         if require:
@@ -180,6 +233,9 @@ def _validate_container_list(cs, path, require):
     seen = set()
     for i, c in enumerate(cs):
         p = f"{path}[{i}]"
+        if not isinstance(c, dict):
+            errs.append(invalid(p, "must be an object"))
+            continue
         name = c.get("name", "")
         if not is_dns1123_label(name):
             errs.append(invalid(f"{p}.name", f"{name!r} must be a DNS-1123 label"))
@@ -191,28 +247,152 @@ def _validate_container_list(cs, path, require):
         pp = c.get("imagePullPolicy")
         if pp and pp not in _PULL:
             errs.append(not_supported(f"{p}.imagePullPolicy", pp))
+        tmp = c.get("terminationMessagePolicy")
+        if tmp and tmp not in _TERM_MSG:
+            errs.append(not_supported(f"{p}.terminationMessagePolicy", tmp))
         errs += _validate_resources(c.get("resources") or {}, f"{p}.resources")
+        pnames = set()
         for j, port in enumerate(c.get("ports") or ()):
             cp = port.get("containerPort")
-            if not isinstance(cp, int) or not 0 < cp < 65536:
+            if not _is_int(cp) or not 0 < cp < 65536:
                 errs.append(invalid(f"{p}.ports[{j}].containerPort", cp))
+            hp = port.get("hostPort")
+            if hp is not None and (not _is_int(hp) or not 0 <= hp < 65536):
+                errs.append(invalid(f"{p}.ports[{j}].hostPort", hp))
+            proto = port.get("protocol")
+            if proto and proto not in _PROTOCOLS:
+                errs.append(not_supported(f"{p}.ports[{j}].protocol", proto))
+            pn = port.get("name")
+            if pn:
+                if not (len(pn) <= 15 and IANA_SVC_NAME.match(pn)):
+                    errs.append(invalid(f"{p}.ports[{j}].name", pn))
+                if pn in pnames:
+                    errs.append(duplicate(f"{p}.ports[{j}].name", pn))
+                pnames.add(pn)
         for j, e in enumerate(c.get("env") or ()):
-            if not e.get("name"):
+            en = e.get("name")
+            if not en:
                 errs.append(required(f"{p}.env[{j}].name"))
+            elif not ENV_VAR_NAME.match(en):
+                errs.append(invalid(f"{p}.env[{j}].name", f"{en!r}: a valid environment variable name must consist of alphabetic characters, digits, '_', '-', or '.'"))
+            vf = e.get("valueFrom")
+            if vf is not None:
+                srcs = [k for k in ("fieldRef", "resourceFieldRef", "configMapKeyRef", "secretKeyRef") if vf.get(k) is not None]
+                if len(srcs) != 1:
+                    errs.append(invalid(f"{p}.env[{j}].valueFrom", "may not have more than one field specified at a time"))
+                if e.get("value"):
+                    errs.append(invalid(f"{p}.env[{j}].valueFrom", "may not be specified when `value` is not empty"))
+        for j, ef in enumerate(c.get("envFrom") or ()):
+            if (ef.get("configMapRef") is None) == (ef.get("secretRef") is None):
+                errs.append(invalid(f"{p}.envFrom[{j}]", "must specify exactly one of configMapRef or secretRef"))
+            if ef.get("prefix") and not ENV_VAR_NAME.match(ef["prefix"]):
+                errs.append(invalid(f"{p}.envFrom[{j}].prefix", ef["prefix"]))
+        mpaths = set()
+        for j, vm in enumerate(c.get("volumeMounts") or ()):
+            if volumes is not None and vm.get("name") not in volumes:
+                errs.append(FieldError("Not found", f"{p}.volumeMounts[{j}].name", vm.get("name")))
+            mp = vm.get("mountPath")
+            if not mp:
+                errs.append(required(f"{p}.volumeMounts[{j}].mountPath"))
+            elif mp in mpaths:
+                errs.append(invalid(f"{p}.volumeMounts[{j}].mountPath", f"{mp!r}: must be unique"))
+            mpaths.add(mp)
+            sp = vm.get("subPath") or ""
+            if sp.startswith("/") or ".." in sp.split("/"):
+                errs.append(invalid(f"{p}.volumeMounts[{j}].subPath", f"{sp!r}: must be a relative path without '..'"))
+        errs += _validate_probe(c.get("livenessProbe"), f"{p}.livenessProbe")
+        errs += _validate_probe(c.get("readinessProbe"), f"{p}.readinessProbe")
+        rp = c.get("readinessProbe")
+        if rp is not None and rp.get("successThreshold") not in (None, 1) and False:
+            pass
+        lp = c.get("livenessProbe")
+        if lp is not None and lp.get("successThreshold") not in (None, 1):
+            errs.append(invalid(f"{p}.livenessProbe.successThreshold", "must be 1"))
+        sc = c.get("securityContext") or {}
+        _non_negative(sc.get("runAsUser"), f"{p}.securityContext.runAsUser", errs)
+        if sc.get("privileged") and sc.get("allowPrivilegeEscalation") is False:
+            errs.append(invalid(f"{p}.securityContext", "cannot set allowPrivilegeEscalation to false and privileged to true"))
+    return errs
+
+
+def _validate_volumes(vols, path):
+    errs = []
+    names = set()
+    for i, v in enumerate(vols or ()):
+        p = f"{path}[{i}]"
+        n = v.get("name", "")
+        if not is_dns1123_label(n):
+            errs.append(invalid(f"{p}.name", n))
+        if n in names:
+            errs.append(duplicate(f"{p}.name", n))
+        names.add(n)
+        srcs = [k for k in _VOLUME_SOURCES if v.get(k) is not None]
+        if not srcs:
+            errs.append(required(p, "must specify a volume type"))
+        elif len(srcs) > 1:
+            errs.append(FieldError("Forbidden", f"{p}.{srcs[1]}", "may not specify more than 1 volume type"))
+        hp = v.get("hostPath")
+        if hp is not None and not hp.get("path"):
+            errs.append(required(f"{p}.hostPath.path"))
+        pvc = v.get("persistentVolumeClaim")
+        if pvc is not None and not pvc.get("claimName"):
+            errs.append(required(f"{p}.persistentVolumeClaim.claimName"))
+        for src, key in (("secret", "secretName"), ("configMap", "name")):
+            sv = v.get(src)
+            if sv is None:
+                continue
+            for j, it in enumerate(sv.get("items") or ()):
+                if not it.get("key"):
+                    errs.append(required(f"{p}.{src}.items[{j}].key"))
+                ip = it.get("path") or ""
+                if not ip or ip.startswith("/") or ".." in ip.split("/"):
+                    errs.append(invalid(f"{p}.{src}.items[{j}].path", ip))
+            dm = sv.get("defaultMode")
+            if dm is not None and (not _is_int(dm) or not 0 <= dm <= 0o777):
+                errs.append(invalid(f"{p}.{src}.defaultMode", f"{dm!r}: must be a number between 0 and 0777 (octal)"))
+    return names, errs
+
+
+def _validate_tolerations(tols, path):
+    errs = []
+    for i, t in enumerate(tols or ()):
+        p = f"{path}[{i}]"
+        key, op = t.get("key", ""), t.get("operator") or "Equal"
+        if key and not is_qualified_name(key):
+            errs.append(invalid(f"{p}.key", key))
+        if op not in _TOL_OPS:
+            errs.append(not_supported(f"{p}.operator", op))
+        if not key and op != "Exists":
+            errs.append(invalid(f"{p}.operator", "operator must be Exists when `key` is empty"))
+        if op == "Exists" and t.get("value"):
+            errs.append(invalid(f"{p}.operator", "value must be empty when `operator` is 'Exists'"))
+        eff = t.get("effect")
+        if eff and eff not in (core.TAINT_NO_SCHEDULE, core.TAINT_PREFER_NO_SCHEDULE, core.TAINT_NO_EXECUTE):
+            errs.append(not_supported(f"{p}.effect", eff))
+        if t.get("tolerationSeconds") is not None and eff != core.TAINT_NO_EXECUTE:
+            errs.append(invalid(f"{p}.effect", "effect must be 'NoExecute' when `tolerationSeconds` is set"))
     return errs
 
 
 def validate_pod_spec(spec, path="spec"):
+    """`ValidatePodSpec` (pkg/apis/core/validation/validation.go:2850-2920) + the fork's ER rules."""
+    if not isinstance(spec, dict):
+        return [invalid(path, "must be an object")]
     errs = []
-    errs += _validate_container_list(spec.get("containers"), f"{path}.containers", True)
-    errs += _validate_container_list(spec.get("initContainers"), f"{path}.initContainers", False)
-    names = {c.get("name") for c in spec.get("containers") or ()}
+    vol_names, verrs = _validate_volumes(spec.get("volumes"), f"{path}.volumes")
+    errs += verrs
+    errs += _validate_container_list(spec.get("containers"), f"{path}.containers", True, vol_names)
+    errs += _validate_container_list(spec.get("initContainers"), f"{path}.initContainers", False, vol_names)
+    names = {c.get("name") for c in spec.get("containers") or () if isinstance(c, dict)}
     for c in spec.get("initContainers") or ():
-        if c.get("name") in names:
+        if isinstance(c, dict) and c.get("name") in names:
             errs.append(duplicate(f"{path}.initContainers", c.get("name")))
     rp = spec.get("restartPolicy")
     if rp and rp not in _RESTART:
         errs.append(not_supported(f"{path}.restartPolicy", rp))
+    dp = spec.get("dnsPolicy")
+    if dp and dp not in _DNS_POLICIES:
+        errs.append(not_supported(f"{path}.dnsPolicy", dp))
     names_ref, er_errs = validate_extended_resources(spec.get("extendedResources"), f"{path}.extendedResources")
     errs += er_errs
     errs += validate_containers_extended_resources(spec.get("containers"), names_ref, f"{path}.containers")
@@ -220,17 +400,60 @@ def validate_pod_spec(spec, path="spec"):
     for k, v in (spec.get("nodeSelector") or {}).items():
         if not is_qualified_name(k):
             errs.append(invalid(f"{path}.nodeSelector", k))
-    vols = set()
-    for i, v in enumerate(spec.get("volumes") or ()):
-        n = v.get("name", "")
-        if not is_dns1123_label(n):
-            errs.append(invalid(f"{path}.volumes[{i}].name", n))
-        if n in vols:
-            errs.append(duplicate(f"{path}.volumes[{i}].name", n))
-        vols.add(n)
+        elif not isinstance(v, str) or not is_valid_label_value(v):
+            errs.append(invalid(f"{path}.nodeSelector", v))
     tgp = spec.get("terminationGracePeriodSeconds")
-    if tgp is not None and (not isinstance(tgp, int) or tgp < 0):
+    if tgp is not None and (not _is_int(tgp) or tgp < 0):
         errs.append(invalid(f"{path}.terminationGracePeriodSeconds", tgp))
+    _non_negative(spec.get("activeDeadlineSeconds"), f"{path}.activeDeadlineSeconds", errs, positive=True)
+    for k in ("hostname", "subdomain"):
+        if spec.get(k) and not is_dns1123_label(spec[k]):
+            errs.append(invalid(f"{path}.{k}", spec[k]))
+    if spec.get("serviceAccountName") and not is_dns1123_subdomain(spec["serviceAccountName"]):
+        errs.append(invalid(f"{path}.serviceAccountName", spec["serviceAccountName"]))
+    errs += _validate_tolerations(spec.get("tolerations"), f"{path}.tolerations")
+    if spec.get("hostNetwork"):
+        for i, c in enumerate(spec.get("containers") or ()):
+            for j, port in enumerate((c or {}).get("ports") or ()):
+                hp = port.get("hostPort")
+                if hp and hp != port.get("containerPort"):
+                    errs.append(invalid(f"{path}.containers[{i}].ports[{j}].hostPort", "must match `containerPort` when `hostNetwork` is true"))
+    psc = spec.get("securityContext") or {}
+    _non_negative(psc.get("runAsUser"), f"{path}.securityContext.runAsUser", errs)
+    _non_negative(psc.get("fsGroup"), f"{path}.securityContext.fsGroup", errs)
+    for i, g in enumerate(psc.get("supplementalGroups") or ()):
+        _non_negative(g, f"{path}.securityContext.supplementalGroups[{i}]", errs)
+    aff = ((spec.get("affinity") or {}).get("nodeAffinity") or {}).get("requiredDuringSchedulingIgnoredDuringExecution")
+    if aff is not None:
+        terms = aff.get("nodeSelectorTerms")
+        if not terms:
+            errs.append(required(f"{path}.affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution.nodeSelectorTerms",
+                                 "must have at least one node selector term"))
+        for i, t in enumerate(terms or ()):
+            for j, r in enumerate((t or {}).get("matchExpressions") or ()):
+                if r.get("operator") not in ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"):
+                    errs.append(not_supported(f"{path}.affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution."
+                                              f"nodeSelectorTerms[{i}].matchExpressions[{j}].operator", r.get("operator")))
+    return errs
+
+
+def validate_pod_template_spec(tpl, path, restart_policies=None):
+    """`ValidatePodTemplateSpec` (validation.go:3820): labels valid, pod spec valid; callers pass
+    the restart policies their controller supports."""
+    if not isinstance(tpl, dict):
+        return [required(path)]
+    errs = []
+    md = tpl.get("metadata") or {}
+    for k, v in (md.get("labels") or {}).items():
+        if not is_qualified_name(k) or not isinstance(v, str) or not is_valid_label_value(v):
+            errs.append(invalid(f"{path}.metadata.labels", f"{k}={v!r}"))
+    spec = tpl.get("spec")
+    if spec is None:
+        return errs + [required(f"{path}.spec")]
+    errs += validate_pod_spec(spec, f"{path}.spec")
+    rp = spec.get("restartPolicy") or "Always"
+    if restart_policies is not None and rp not in restart_policies:
+        errs.append(not_supported(f"{path}.spec.restartPolicy", rp))
     return errs
 
 
@@ -272,6 +495,16 @@ def validate_namespace(ns):
 
 def validate_generic(obj, namespaced):
     return validate_object_meta(obj, namespaced)
+
+
+def validate_object_meta_update(new, old, path="metadata"):
+    """`ValidateObjectMetaUpdate`: name, namespace, uid and creationTimestamp are immutable."""
+    errs = []
+    nm, om = new.get("metadata") or {}, old.get("metadata") or {}
+    for k in ("name", "namespace", "uid", "creationTimestamp"):
+        if (nm.get(k) or None) != (om.get(k) or None) and om.get(k) is not None:
+            errs.append(invalid(f"{path}.{k}", "field is immutable"))
+    return errs
 
 
 def is_path_segment_name(s):

@@ -15,7 +15,7 @@ from __future__ import annotations
 import random
 import time
 
-from ..api import core, validation
+from ..api import core, validation, validation_ext
 from ..api.meta import new_uid, now_rfc3339
 from ..api.quantity import parse_quantity
 
@@ -58,6 +58,11 @@ def generate_name(base):
     return base + "".join(random.choice(_GEN_CHARS) for _ in range(5))
 
 
+# per-kind create validation: core kinds (api/validation.py) and every other served kind
+# (api/validation_ext.py)
+_VALIDATORS = {**validation.VALIDATORS, **validation_ext.VALIDATORS}
+
+
 class Strategy:
     """Default strategy: spec+status updated together, no status subresource."""
     has_status = True      # exposes /status; main updates ignore status changes
@@ -90,11 +95,11 @@ class Strategy:
                 nm.pop(k, None)
 
     def validate(self, obj):
-        fn = validation.VALIDATORS.get(self.ri.kind)
+        fn = _VALIDATORS.get(self.ri.kind)
         return fn(obj) if fn else validation.validate_generic(obj, self.ri.namespaced)
 
     def validate_update(self, new, old):
-        return self.validate(new)
+        return self.validate(new) + validation_ext.validate_update(self.ri.kind, new, old)
 
     _PHASES = {"Pending", "Running", "Succeeded", "Failed", "Unknown", "Active", "Terminating", "",
                "Available", "Bound", "Released", "Lost"}   # pods, namespaces, PVs / PVCs
@@ -135,7 +140,7 @@ class PodStrategy(Strategy):
             ns["extendedResources"] = ers
 
     def validate_update(self, new, old):
-        errs = validation.validate_pod(new)
+        errs = validation.validate_pod(new) + validation.validate_object_meta_update(new, old)
         ns, os_ = new.get("spec") or {}, old.get("spec") or {}
         mutable = ("containers", "initContainers", "activeDeadlineSeconds", "tolerations")
         for k in set(ns) | set(os_):

@@ -36,7 +36,7 @@ import logging
 import secrets
 import time
 
-from ..api import codec, core, meta as m
+from ..api import codec, core, defaults, meta as m
 from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
 from ..api.meta import parse_rfc3339, fast_copy, now_rfc3339
 from ..api.sharding import QUERY_PARAM, SHARD_OFFSET_LABEL, parse_shard, shard_matches
@@ -660,6 +660,7 @@ class APIServer:
         if not isinstance(obj, dict):
             raise bad_request("body must be a JSON object")
         init_object_meta(obj, ri, namespace)
+        defaults.apply(ri.kind, obj)       # the scheme's SetDefaults_* before validation
         strat = self.strategies[ri.plural]
         strat.prepare_create(obj)
         if ri.plural == "certificatesigningrequests":
@@ -797,6 +798,7 @@ class APIServer:
         elif subresource == "status":
             strat.prepare_status_update(obj, old)
         elif subresource == "":
+            defaults.apply(ri.kind, obj)
             strat.prepare_update(obj, old)
             if strat.bump_generation and "generation" in om:
                 if {k: v for k, v in obj.items() if k not in ("metadata", "status")} != \

@@ -451,7 +451,10 @@ async def eviction_pdb(f):
         assert "429" in str(e) or "disruption budget" in str(e), e
     else:
         raise AssertionError("eviction violating the budget was allowed")
-    await f.client.patch("poddisruptionbudgets", "b", {"spec": {"minAvailable": 1}}, f.ns)
+    # a PDB's spec is immutable in this API version (ValidatePodDisruptionBudgetUpdate): replace it
+    await f.client.delete("poddisruptionbudgets", "b", f.ns)
+    await f.client.create("poddisruptionbudgets", {"metadata": {"name": "b"}, "spec": {
+        "minAvailable": 1, "selector": {"matchLabels": {"app": "pdb"}}}}, f.ns)
 
     async def allowed():
         b = await f.client.get("poddisruptionbudgets", "b", f.ns)

@@ -6,13 +6,17 @@ collector (`vendor/github.com/google/cadvisor/accelerators/nvidia.go:172-222`, d
 char major 195), which reports the DEVICE's memory use for every container holding it. Here:
   * the container -> GPU mapping comes from the allocation record itself
     (`spec.extendedResources[].assigned`);
-  * memory is attributed PER CONTAINER: AMD SMI's per-process list
-    (`amdsmi_get_gpu_process_list`: pid, VRAM, gfx engine ns) is joined with the runtime's
-    container processes (a GPU process belongs to the container whose root process is its
-    ancestor), so two pods sharing a GPU (compute partitions, or a multi-tenant device) are not
-    both charged the whole device. `memoryUsed` is the container's own VRAM, `deviceMemoryUsed`
-    the device's; `dutyCycle` is the container's share of the gfx engine over the last sampling
-    interval when its processes report engine time, else the device's activity.
+  * memory is attributed PER CONTAINER, from the container's own processes: the DRM fdinfo
+    of every open render node (`/proc/<pid>/fdinfo/<fd>`: drm-pdev, drm-client-id,
+    drm-resident-vram — amdgpu accounts KFD/HIP allocations to the render-node file whose VM
+    they share), summed over the container's process tree and deduplicated by client id. This
+    works inside pid namespaces, where AMD SMI's process list (`amdsmi_get_gpu_process_list`)
+    reports host pids the kubelet cannot see; that list is the fallback when fdinfo carries no
+    memory keys (older kernels) and the pids are the kubelet's own. Two pods sharing a GPU
+    (compute partitions, or a multi-tenant device) are therefore not both charged the whole
+    device. `memoryUsed` is the container's own VRAM, `deviceMemoryUsed` the device's;
+    `dutyCycle` is the container's share of the gfx engine over the last sampling interval when
+    its processes report engine time, else the device's activity.
 """
 from __future__ import annotations
 
@@ -39,33 +43,106 @@ def _ppid(pid):
         return 0
 
 
+def _descendants(root):
+    """root and every process below it (/proc/<pid>/task/<tid>/children)."""
+    import os
+    out, todo = [], [root]
+    while todo and len(out) < 4096:
+        pid = todo.pop()
+        out.append(pid)
+        try:
+            for tid in os.listdir(f"/proc/{pid}/task"):
+                try:
+                    with open(f"/proc/{pid}/task/{tid}/children") as f:
+                        todo.extend(int(x) for x in f.read().split())
+                except (OSError, ValueError):
+                    pass
+        except OSError:
+            pass
+    return out
+
+
+def _drm_fdinfo(pid):
+    """[(pdev, client id, resident VRAM bytes, gfx engine ns)] of the render nodes pid has open."""
+    import os
+    out = []
+    try:
+        fds = os.listdir(f"/proc/{pid}/fd")
+    except OSError:
+        return out
+    for fd in fds:
+        try:
+            if not os.readlink(f"/proc/{pid}/fd/{fd}").startswith("/dev/dri/"):
+                continue
+            with open(f"/proc/{pid}/fdinfo/{fd}") as f:
+                info = f.read()
+        except OSError:
+            continue
+        kv = {}
+        for line in info.splitlines():
+            k, _, v = line.partition(":")
+            kv[k.strip()] = v.strip()
+        if "drm-pdev" not in kv:
+            continue
+        vram = kv.get("drm-resident-vram") or kv.get("drm-memory-vram")
+        if vram is None:
+            continue
+        n, _, unit = vram.partition(" ")
+        mult = {"KiB": 1 << 10, "MiB": 1 << 20, "GiB": 1 << 30}.get(unit.strip(), 1)
+        gfx = kv.get("drm-engine-gfx", "0").split()[0]
+        try:
+            out.append((kv["drm-pdev"], kv.get("drm-client-id", f"{pid}/{fd}"), int(n) * mult, int(gfx)))
+        except ValueError:
+            continue
+    return out
+
+
 def gpu_process_usage(kubelet):
-    """{container id: {gpu index: (vram bytes, gfx engine ns)}} from AMD SMI's process lists,
-    each GPU process charged to the container whose root process is its ancestor."""
-    smi = getattr(kubelet, "smi", None)
+    """{container id: {device BDF: (vram bytes, gfx engine ns)}} — each GPU client charged to the
+    container whose root process is its ancestor."""
     pids_fn = getattr(kubelet.runtime, "container_pids", None)
-    if smi is None or pids_fn is None:
+    if pids_fn is None:
         return {}
-    roots = {pid: cid for cid, pid in pids_fn().items()}
+    roots = pids_fn()
     if not roots:
         return {}
-    from ..native.amdsmi import SMIError
     out: dict = {}
+    for cid, root in roots.items():
+        seen = set()
+        for pid in _descendants(root):
+            for pdev, client, vram, gfx in _drm_fdinfo(pid):
+                if (pdev, client) in seen:
+                    continue
+                seen.add((pdev, client))
+                v, g = out.setdefault(cid, {}).get(pdev, (0, 0))
+                out[cid][pdev] = (v + vram, g + gfx)
+    smi = getattr(kubelet, "smi", None)
+    if smi is None:
+        return out
+    # AMD SMI's process list: its pids are the host's, usable when the kubelet shares the pid
+    # namespace (and the only source without DRM fdinfo memory keys)
+    from ..native.amdsmi import SMIError
+    by_root = {pid: cid for cid, pid in roots.items()}
     for i in range(smi.count()):
         try:
             procs = smi.processes(i)
+            bdf = smi.gpu(i).bdf if procs else ""
         except SMIError as e:
             log.warning("AMD SMI process list of GPU %d: %s", i, e)
             continue
         for p in procs:
             pid, depth = p.pid, 0
-            while pid > 1 and pid not in roots and depth < 64:
+            while pid > 1 and pid not in by_root and depth < 64:
                 pid, depth = _ppid(pid), depth + 1
-            cid = roots.get(pid)
-            if cid is None:
-                continue
-            vram, gfx = out.setdefault(cid, {}).get(i, (0, 0))
-            out[cid][i] = (vram + p.vram_bytes, gfx + p.gfx_ns)
+            cid = by_root.get(pid)
+            if cid is None or bdf in out.get(cid, {}):
+                continue        # fdinfo already accounted this container on this device
+            per = out.setdefault(cid, {})
+            v, g = per.get(("smi", bdf), (0, 0))
+            per[("smi", bdf)] = (v + p.vram_bytes, g + p.gfx_ns)
+    for per in out.values():
+        for k in [k for k in per if isinstance(k, tuple)]:
+            per[k[1]] = per.pop(k)
     return out
 
 
@@ -83,6 +160,7 @@ def accelerator_stats(kubelet, ids, usage=None, cid=None, now=None):
             continue
         attrs = d.get("attributes") or {}
         idx = int(attrs.get(core.ATTR_INDEX, "0"))
+        bdf = attrs.get(core.ATTR_BDF, "")
         entry = {"make": "amd", "model": attrs.get(core.ATTR_PRODUCT, ""), "id": i,
                  "memoryTotal": int(attrs.get(core.ATTR_MEMORY, "0")) << 20, "memoryUsed": 0, "dutyCycle": 0}
         if smi is not None:
@@ -97,11 +175,11 @@ def accelerator_stats(kubelet, ids, usage=None, cid=None, now=None):
                 entry["dutyCycle"] = m.gfx_activity
                 entry["powerWatts"] = m.power_w
                 entry["temperatureC"] = m.temp_hotspot_c
-        if idx in mine:
-            vram, gfx = mine[idx]
+        if bdf in mine:
+            vram, gfx = mine[bdf]
             entry["memoryUsed"] = vram
-            prev = samples.get((cid, idx))
-            samples[(cid, idx)] = (now or time.time(), gfx)
+            prev = samples.get((cid, bdf))
+            samples[(cid, bdf)] = (now or time.time(), gfx)
             if prev is not None and gfx and now and now > prev[0]:
                 entry["dutyCycle"] = max(0, min(100, int(round((gfx - prev[1]) / ((now - prev[0]) * 1e9) * 100))))
         out.append(entry)

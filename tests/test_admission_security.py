@@ -37,10 +37,14 @@ def test_pod_security_policy(run):
             await admin.create("podsecuritypolicies", {"metadata": {"name": "restricted"}, "spec": {
                 "privileged": False, "volumes": ["configMap", "secret", "emptyDir", "persistentVolumeClaim"],
                 "runAsUser": {"rule": "MustRunAs", "ranges": [{"min": 1000, "max": 2000}]},
+                "seLinux": {"rule": "RunAsAny"}, "fsGroup": {"rule": "RunAsAny"},
+                "supplementalGroups": {"rule": "RunAsAny"},
                 "requiredDropCapabilities": ["NET_RAW"], "allowPrivilegeEscalation": False,
                 "hostPorts": [{"min": 8000, "max": 8100}]}})
             await admin.create("podsecuritypolicies", {"metadata": {"name": "z-privileged"}, "spec": {
                 "privileged": True, "volumes": ["*"], "hostNetwork": True, "runAsUser": {"rule": "RunAsAny"},
+                "seLinux": {"rule": "RunAsAny"}, "fsGroup": {"rule": "RunAsAny"},
+                "supplementalGroups": {"rule": "RunAsAny"},
                 "allowedCapabilities": ["*"], "hostPorts": [{"min": 0, "max": 65535}]}})
             await admin.create("clusterroles", {"metadata": {"name": "psp:restricted"}, "rules": [
                 {"apiGroups": ["policy"], "resources": ["podsecuritypolicies"], "resourceNames": ["restricted"], "verbs": ["use"]}]})

@@ -99,7 +99,9 @@ def test_bootstrap_and_service_account_tokens(run, tmp_path):
             assert not (await admin.create("tokenreviews", {"spec": {"token": "abcdef.0123456789abcdef"}}))["status"]["authenticated"]
             # service account JWT
             sa = await admin.create("serviceaccounts", {"metadata": {"name": "builder", "namespace": "default"}})
-            await admin.create("secrets", {"metadata": {"name": "builder-token-x", "namespace": "default"}, "type": "kubernetes.io/service-account-token"})
+            await admin.create("secrets", {"metadata": {"name": "builder-token-x", "namespace": "default",
+                                                        "annotations": {"kubernetes.io/service-account.name": "builder"}},
+                                           "type": "kubernetes.io/service-account-token"})
             tok = an.service_account_token(sa_key, sa, "builder-token-x")
             tr = await admin.create("tokenreviews", {"spec": {"token": tok}})
             assert tr["status"]["user"]["username"] == "system:serviceaccount:default:builder"
