@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import ast
+import json
 import os
 import py_compile
 import re
@@ -231,6 +232,19 @@ def check_protos(update=False):
     for modname, attr, services, name in PROTO_MODULES:
         text = render_proto(modname, attr, services)
         path = os.path.join(out, name)
+        if update:
+            with open(path, "w") as f:
+                f.write(text)
+        elif not os.path.exists(path) or open(path).read() != text:
+            errs.append(f"{rel(path)} is stale (run hack/verify.py --update)")
+    # the protobuf storage schema table, regenerated from the reference generated.proto files
+    # when that tree is present (hack/gen_proto_schema.py)
+    ref = os.environ.get("KAMD_REFERENCE", "/root/reference")
+    if os.path.isdir(os.path.join(ref, "staging", "src", "k8s.io")):
+        sys.path.insert(0, os.path.join(ROOT, "hack"))
+        import gen_proto_schema
+        text = json.dumps(gen_proto_schema.generate(ref), separators=(",", ":")) + "\n"
+        path = gen_proto_schema.DEFAULT_OUT
         if update:
             with open(path, "w") as f:
                 f.write(text)

@@ -1,190 +1,124 @@
-"""Kubernetes protobuf wire/storage format for the core/v1 objects, including the fork's
-ResourceV2 fields, and the `k8s\\x00` + runtime.Unknown envelope.
+"""Kubernetes protobuf wire / etcd storage format for every served kind, driven by the schema
+table generated from the reference's `generated.proto` files (`hack/gen_proto_schema.py` ->
+`api/generated/k8s_proto_schema.json`), including the fork's ResourceV2 fields.
 
 Parity:
   * envelope: `staging/src/k8s.io/apimachinery/pkg/runtime/serializer/protobuf/protobuf.go:42`
     (magic `0x6b 0x38 0x73 0x00`) + `runtime.Unknown{typeMeta=1{apiVersion=1,kind=2}, raw=2,
     contentEncoding=3, contentType=4}` (`staging/src/k8s.io/apimachinery/pkg/runtime/types.go:112-124`);
-  * field numbers: `staging/src/k8s.io/api/core/v1/generated.proto` — fork fields Container 22,
-    PodSpec 27, NodeStatus 11, ObjectReference 8 (`extendedResourceBinding`), PodExtendedResource
-    1..5, ExtendedResourceDomain / ExtendedResource / ExtendedResourceList;
-  * value encodings: meta/v1 Time `{seconds=1, nanos=2}`, resource.Quantity `{string=1}`,
-    intstr.IntOrString `{type=1, intVal=2, strVal=3}`; maps as repeated entry messages with
-    keys in sorted order (the generated marshalers sort map keys) and fields in ascending
-    field-number order, so encoding is deterministic.
-Gogo-embedded structs whose JSON is inlined (Volume.VolumeSource, *VolumeSource's
-LocalObjectReference, ...) are marked `inline`.
+  * field numbers and names: `staging/src/k8s.io/api/<group>/<version>/generated.proto` (e.g. the
+    fork's Container 22, PodSpec 27, NodeStatus 11, ObjectReference 8 `extendedResourceBinding`);
+    JSON names and inline embedding from the Go struct tags (`json:",inline"`: Volume.VolumeSource,
+    Probe.Handler, ... whose fields appear at the parent's level in JSON);
+  * value encodings (the types with custom JSON marshalling): meta/v1 Time / MicroTime
+    `{seconds=1, nanos=2}` <-> RFC 3339, Duration `{duration=1}` <-> Go duration string,
+    resource.Quantity `{string=1}`, intstr.IntOrString `{type=1, intVal=2, strVal=3}`,
+    runtime.RawExtension / apiextensions JSON `{raw=1}` <-> any JSON value, the
+    JSONSchemaPropsOr{Bool,Array,StringArray} unions, ExtraValue / Verbs string-slice wrappers,
+    `bytes` <-> base64; maps as repeated entries in sorted key order, fields in field-number
+    order (deterministic encoding).
 
-Pure-Python codec (no protoc in this image): a compact schema table drives both directions.
+Encoding is LOSSLESS OR AN ERROR: a field that is not in the kind's message raises
+`ProtobufError` with its JSON path (the API server answers 422 instead of silently dropping it).
+TypeMeta (`kind`, `apiVersion`) is not part of any message (Go's TypeMeta has no protobuf tag)
+and travels in the envelope. Kinds without a message in the reference schema (custom resources,
+`coordination.k8s.io` Leases) are stored as JSON, as the reference stores custom resources.
+
+`encode_message` / `decode_message` here are the reference implementation; when the native
+codec (`native/pbcodec/kamd_pbcodec.cc`, `_kamd_pbcodec`) is built the storage / wire entry
+points use it — tests cross-check the two byte for byte.
 """
 from __future__ import annotations
 
+import base64
 import datetime as _dt
+import json
+import os
+import re
 
 MAGIC = b"k8s\x00"
+SCHEMA_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "generated", "k8s_proto_schema.json")
 
-# field kinds
-S, B, I64, I32, MSG, MAPS, MAPM, RS, RM, RI64, TIME, QTY, IOS, INL, BYTES = (
-    "s", "b", "i64", "i32", "m", "mapS", "mapM", "rs", "rm", "ri64", "time", "qty", "ios", "inline", "bytes")
+META = "k8s.io.apimachinery.pkg.apis.meta.v1."
+TIME, MICROTIME, DURATION = META + "Time", META + "MicroTime", META + "Duration"
+QUANTITY = "k8s.io.apimachinery.pkg.api.resource.Quantity"
+INTORSTR = "k8s.io.apimachinery.pkg.util.intstr.IntOrString"
+RAWEXT = "k8s.io.apimachinery.pkg.runtime.RawExtension"
+_AX = "k8s.io.apiextensions_apiserver.pkg.apis.apiextensions.v1beta1."
+JSONRAW, ORBOOL, ORARRAY, ORSTRARRAY = _AX + "JSON", _AX + "JSONSchemaPropsOrBool", _AX + "JSONSchemaPropsOrArray", \
+    _AX + "JSONSchemaPropsOrStringArray"
+# string-slice wrappers: `type ExtraValue []string` marshals as a JSON array
+SLICES = {META + "Verbs"} | {f"k8s.io.api.{g}.ExtraValue" for g in (
+    "authentication.v1", "authentication.v1beta1", "authorization.v1", "authorization.v1beta1", "certificates.v1beta1")}
+SPECIAL = {TIME, MICROTIME, DURATION, QUANTITY, INTORSTR, RAWEXT, JSONRAW, ORBOOL, ORARRAY, ORSTRARRAY} | SLICES
 
-# message -> [(json name, field number, kind, message type)]
-SCHEMA: dict[str, list] = {
-    # --- meta/v1 ----------------------------------------------------------
-    "ObjectMeta": [("name", 1, S, None), ("generateName", 2, S, None), ("namespace", 3, S, None),
-                   ("selfLink", 4, S, None), ("uid", 5, S, None), ("resourceVersion", 6, S, None),
-                   ("generation", 7, I64, None), ("creationTimestamp", 8, TIME, None),
-                   ("deletionTimestamp", 9, TIME, None), ("deletionGracePeriodSeconds", 10, I64, None),
-                   ("labels", 11, MAPS, None), ("annotations", 12, MAPS, None),
-                   ("ownerReferences", 13, RM, "OwnerReference"), ("finalizers", 14, RS, None),
-                   ("clusterName", 15, S, None)],
-    "OwnerReference": [("kind", 1, S, None), ("name", 3, S, None), ("uid", 4, S, None), ("apiVersion", 5, S, None),
-                       ("controller", 6, B, None), ("blockOwnerDeletion", 7, B, None)],
-    "ListMeta": [("selfLink", 1, S, None), ("resourceVersion", 2, S, None), ("continue", 3, S, None)],
-    "LabelSelector": [("matchLabels", 1, MAPS, None), ("matchExpressions", 2, RM, "LabelSelectorRequirement")],
-    "LabelSelectorRequirement": [("key", 1, S, None), ("operator", 2, S, None), ("values", 3, RS, None)],
-    # --- core/v1 pod ------------------------------------------------------------
-    "Pod": [("metadata", 1, MSG, "ObjectMeta"), ("spec", 2, MSG, "PodSpec"), ("status", 3, MSG, "PodStatus")],
-    "PodList": [("metadata", 1, MSG, "ListMeta"), ("items", 2, RM, "Pod")],
-    "PodSpec": [("volumes", 1, RM, "Volume"), ("containers", 2, RM, "Container"), ("restartPolicy", 3, S, None),
-                ("terminationGracePeriodSeconds", 4, I64, None), ("activeDeadlineSeconds", 5, I64, None),
-                ("dnsPolicy", 6, S, None), ("nodeSelector", 7, MAPS, None), ("serviceAccountName", 8, S, None),
-                ("serviceAccount", 9, S, None), ("nodeName", 10, S, None), ("hostNetwork", 11, B, None),
-                ("hostPID", 12, B, None), ("hostIPC", 13, B, None), ("securityContext", 14, MSG, "PodSecurityContext"),
-                ("imagePullSecrets", 15, RM, "LocalObjectReference"), ("hostname", 16, S, None),
-                ("subdomain", 17, S, None), ("affinity", 18, MSG, "Affinity"), ("schedulerName", 19, S, None),
-                ("initContainers", 20, RM, "Container"), ("automountServiceAccountToken", 21, B, None),
-                ("tolerations", 22, RM, "Toleration"), ("hostAliases", 23, RM, "HostAlias"),
-                ("priorityClassName", 24, S, None), ("priority", 25, I32, None),
-                ("extendedResources", 27, RM, "PodExtendedResource")],
-    "Container": [("name", 1, S, None), ("image", 2, S, None), ("command", 3, RS, None), ("args", 4, RS, None),
-                  ("workingDir", 5, S, None), ("ports", 6, RM, "ContainerPort"), ("env", 7, RM, "EnvVar"),
-                  ("resources", 8, MSG, "ResourceRequirements"), ("volumeMounts", 9, RM, "VolumeMount"),
-                  ("livenessProbe", 10, MSG, "Probe"), ("readinessProbe", 11, MSG, "Probe"),
-                  ("terminationMessagePath", 13, S, None), ("imagePullPolicy", 14, S, None),
-                  ("securityContext", 15, MSG, "SecurityContext"), ("stdin", 16, B, None), ("stdinOnce", 17, B, None),
-                  ("tty", 18, B, None), ("terminationMessagePolicy", 20, S, None),
-                  ("extendedResourceRequests", 22, RS, None)],
-    "ContainerPort": [("name", 1, S, None), ("hostPort", 2, I32, None), ("containerPort", 3, I32, None),
-                      ("protocol", 4, S, None), ("hostIP", 5, S, None)],
-    "EnvVar": [("name", 1, S, None), ("value", 2, S, None), ("valueFrom", 3, MSG, "EnvVarSource")],
-    "EnvVarSource": [("fieldRef", 1, MSG, "ObjectFieldSelector"), ("resourceFieldRef", 2, MSG, "ResourceFieldSelector"),
-                     ("configMapKeyRef", 3, MSG, "ConfigMapKeySelector"), ("secretKeyRef", 4, MSG, "SecretKeySelector")],
-    "ObjectFieldSelector": [("apiVersion", 1, S, None), ("fieldPath", 2, S, None)],
-    "ResourceFieldSelector": [("containerName", 1, S, None), ("resource", 2, S, None), ("divisor", 3, QTY, None)],
-    "ConfigMapKeySelector": [(None, 1, INL, "LocalObjectReference"), ("key", 2, S, None), ("optional", 3, B, None)],
-    "SecretKeySelector": [(None, 1, INL, "LocalObjectReference"), ("key", 2, S, None), ("optional", 3, B, None)],
-    "LocalObjectReference": [("name", 1, S, None)],
-    "ResourceRequirements": [("limits", 1, MAPM, "Quantity"), ("requests", 2, MAPM, "Quantity")],
-    "VolumeMount": [("name", 1, S, None), ("readOnly", 2, B, None), ("mountPath", 3, S, None), ("subPath", 4, S, None),
-                    ("mountPropagation", 5, S, None)],
-    "Volume": [("name", 1, S, None), (None, 2, INL, "VolumeSource")],
-    "VolumeSource": [("hostPath", 1, MSG, "HostPathVolumeSource"), ("emptyDir", 2, MSG, "EmptyDirVolumeSource"),
-                     ("secret", 6, MSG, "SecretVolumeSource"),
-                     ("persistentVolumeClaim", 10, MSG, "PersistentVolumeClaimVolumeSource"),
-                     ("configMap", 19, MSG, "ConfigMapVolumeSource")],
-    "HostPathVolumeSource": [("path", 1, S, None), ("type", 2, S, None)],
-    "EmptyDirVolumeSource": [("medium", 1, S, None), ("sizeLimit", 2, QTY, None)],
-    "SecretVolumeSource": [("secretName", 1, S, None), ("items", 2, RM, "KeyToPath"), ("defaultMode", 3, I32, None),
-                           ("optional", 4, B, None)],
-    "ConfigMapVolumeSource": [(None, 1, INL, "LocalObjectReference"), ("items", 2, RM, "KeyToPath"),
-                              ("defaultMode", 3, I32, None), ("optional", 4, B, None)],
-    "PersistentVolumeClaimVolumeSource": [("claimName", 1, S, None), ("readOnly", 2, B, None)],
-    "KeyToPath": [("key", 1, S, None), ("path", 2, S, None), ("mode", 3, I32, None)],
-    "Probe": [(None, 1, INL, "Handler"), ("initialDelaySeconds", 2, I32, None), ("timeoutSeconds", 3, I32, None),
-              ("periodSeconds", 4, I32, None), ("successThreshold", 5, I32, None), ("failureThreshold", 6, I32, None)],
-    "Handler": [("exec", 1, MSG, "ExecAction"), ("httpGet", 2, MSG, "HTTPGetAction"), ("tcpSocket", 3, MSG, "TCPSocketAction")],
-    "ExecAction": [("command", 1, RS, None)],
-    "HTTPGetAction": [("path", 1, S, None), ("port", 2, IOS, None), ("host", 3, S, None), ("scheme", 4, S, None)],
-    "TCPSocketAction": [("port", 1, IOS, None), ("host", 2, S, None)],
-    "PodSecurityContext": [("runAsUser", 2, I64, None), ("runAsNonRoot", 3, B, None),
-                           ("supplementalGroups", 4, RI64, None), ("fsGroup", 5, I64, None)],
-    "SecurityContext": [("capabilities", 1, MSG, "Capabilities"), ("privileged", 2, B, None), ("runAsUser", 4, I64, None),
-                        ("runAsNonRoot", 5, B, None), ("readOnlyRootFilesystem", 6, B, None),
-                        ("allowPrivilegeEscalation", 7, B, None)],
-    "Capabilities": [("add", 1, RS, None), ("drop", 2, RS, None)],
-    "Toleration": [("key", 1, S, None), ("operator", 2, S, None), ("value", 3, S, None), ("effect", 4, S, None),
-                   ("tolerationSeconds", 5, I64, None)],
-    "HostAlias": [("ip", 1, S, None), ("hostnames", 2, RS, None)],
-    "Affinity": [("nodeAffinity", 1, MSG, "NodeAffinity"), ("podAffinity", 2, MSG, "PodAffinity"),
-                 ("podAntiAffinity", 3, MSG, "PodAntiAffinity")],
-    "NodeAffinity": [("requiredDuringSchedulingIgnoredDuringExecution", 1, MSG, "NodeSelector"),
-                     ("preferredDuringSchedulingIgnoredDuringExecution", 2, RM, "PreferredSchedulingTerm")],
-    "NodeSelector": [("nodeSelectorTerms", 1, RM, "NodeSelectorTerm")],
-    "NodeSelectorTerm": [("matchExpressions", 1, RM, "NodeSelectorRequirement")],
-    "NodeSelectorRequirement": [("key", 1, S, None), ("operator", 2, S, None), ("values", 3, RS, None)],
-    "PreferredSchedulingTerm": [("weight", 1, I32, None), ("preference", 2, MSG, "NodeSelectorTerm")],
-    "PodAffinity": [("requiredDuringSchedulingIgnoredDuringExecution", 1, RM, "PodAffinityTerm"),
-                    ("preferredDuringSchedulingIgnoredDuringExecution", 2, RM, "WeightedPodAffinityTerm")],
-    "PodAntiAffinity": [("requiredDuringSchedulingIgnoredDuringExecution", 1, RM, "PodAffinityTerm"),
-                        ("preferredDuringSchedulingIgnoredDuringExecution", 2, RM, "WeightedPodAffinityTerm")],
-    "PodAffinityTerm": [("labelSelector", 1, MSG, "LabelSelector"), ("namespaces", 2, RS, None), ("topologyKey", 3, S, None)],
-    "WeightedPodAffinityTerm": [("weight", 1, I32, None), ("podAffinityTerm", 2, MSG, "PodAffinityTerm")],
-    # fork ResourceV2
-    "PodExtendedResource": [("name", 1, S, None), ("resources", 2, MSG, "ResourceRequirements"),
-                            ("affinity", 3, MSG, "ExtendedResourceAffinity"), ("annotations", 4, MAPS, None),
-                            ("assigned", 5, RS, None)],
-    "ExtendedResourceAffinity": [("required", 1, RM, "NodeSelectorRequirement")],   # ResourceSelector
-    "ExtendedResourceDomain": [("resources", 1, MAPM, "ExtendedResource")],
-    "ExtendedResource": [("id", 1, S, None), ("health", 2, S, None), ("attributes", 3, MAPS, None)],
-    "ExtendedResourceList": [("resources", 1, RS, None)],
-    "PodStatus": [("phase", 1, S, None), ("conditions", 2, RM, "PodCondition"), ("message", 3, S, None),
-                  ("reason", 4, S, None), ("hostIP", 5, S, None), ("podIP", 6, S, None), ("startTime", 7, TIME, None),
-                  ("containerStatuses", 8, RM, "ContainerStatus"), ("qosClass", 9, S, None),
-                  ("initContainerStatuses", 10, RM, "ContainerStatus")],
-    "PodCondition": [("type", 1, S, None), ("status", 2, S, None), ("lastProbeTime", 3, TIME, None),
-                     ("lastTransitionTime", 4, TIME, None), ("reason", 5, S, None), ("message", 6, S, None)],
-    "ContainerStatus": [("name", 1, S, None), ("state", 2, MSG, "ContainerState"), ("lastState", 3, MSG, "ContainerState"),
-                        ("ready", 4, B, None), ("restartCount", 5, I32, None), ("image", 6, S, None),
-                        ("imageID", 7, S, None), ("containerID", 8, S, None)],
-    "ContainerState": [("waiting", 1, MSG, "ContainerStateWaiting"), ("running", 2, MSG, "ContainerStateRunning"),
-                       ("terminated", 3, MSG, "ContainerStateTerminated")],
-    "ContainerStateWaiting": [("reason", 1, S, None), ("message", 2, S, None)],
-    "ContainerStateRunning": [("startedAt", 1, TIME, None)],
-    "ContainerStateTerminated": [("exitCode", 1, I32, None), ("signal", 2, I32, None), ("reason", 3, S, None),
-                                 ("message", 4, S, None), ("startedAt", 5, TIME, None), ("finishedAt", 6, TIME, None),
-                                 ("containerID", 7, S, None)],
-    # --- node -------------------------------------------------------------------
-    "Node": [("metadata", 1, MSG, "ObjectMeta"), ("spec", 2, MSG, "NodeSpec"), ("status", 3, MSG, "NodeStatus")],
-    "NodeSpec": [("podCIDR", 1, S, None), ("externalID", 2, S, None), ("providerID", 3, S, None),
-                 ("unschedulable", 4, B, None), ("taints", 5, RM, "Taint")],
-    "Taint": [("key", 1, S, None), ("value", 2, S, None), ("effect", 3, S, None), ("timeAdded", 4, TIME, None)],
-    "NodeStatus": [("capacity", 1, MAPM, "Quantity"), ("allocatable", 2, MAPM, "Quantity"), ("phase", 3, S, None),
-                   ("conditions", 4, RM, "NodeCondition"), ("addresses", 5, RM, "NodeAddress"),
-                   ("daemonEndpoints", 6, MSG, "NodeDaemonEndpoints"), ("nodeInfo", 7, MSG, "NodeSystemInfo"),
-                   ("volumesInUse", 9, RS, None), ("extendedResources", 11, MAPM, "ExtendedResourceDomain")],
-    "NodeCondition": [("type", 1, S, None), ("status", 2, S, None), ("lastHeartbeatTime", 3, TIME, None),
-                      ("lastTransitionTime", 4, TIME, None), ("reason", 5, S, None), ("message", 6, S, None)],
-    "NodeAddress": [("type", 1, S, None), ("address", 2, S, None)],
-    "NodeDaemonEndpoints": [("kubeletEndpoint", 1, MSG, "DaemonEndpoint")],
-    "DaemonEndpoint": [("Port", 1, I32, None)],
-    "NodeSystemInfo": [("machineID", 1, S, None), ("systemUUID", 2, S, None), ("bootID", 3, S, None),
-                       ("kernelVersion", 4, S, None), ("osImage", 5, S, None), ("containerRuntimeVersion", 6, S, None),
-                       ("kubeletVersion", 7, S, None), ("kubeProxyVersion", 8, S, None), ("operatingSystem", 9, S, None),
-                       ("architecture", 10, S, None)],
-    # --- binding / refs / namespace / event / configmap --------------------------
-    "Binding": [("metadata", 1, MSG, "ObjectMeta"), ("target", 2, MSG, "ObjectReference")],
-    "ObjectReference": [("kind", 1, S, None), ("namespace", 2, S, None), ("name", 3, S, None), ("uid", 4, S, None),
-                        ("apiVersion", 5, S, None), ("resourceVersion", 6, S, None), ("fieldPath", 7, S, None),
-                        ("extendedResourceBinding", 8, MAPM, "ExtendedResourceList")],
-    "Namespace": [("metadata", 1, MSG, "ObjectMeta"), ("spec", 2, MSG, "NamespaceSpec"), ("status", 3, MSG, "NamespaceStatus")],
-    "NamespaceSpec": [("finalizers", 1, RS, None)],
-    "NamespaceStatus": [("phase", 1, S, None)],
-    "Event": [("metadata", 1, MSG, "ObjectMeta"), ("involvedObject", 2, MSG, "ObjectReference"), ("reason", 3, S, None),
-              ("message", 4, S, None), ("source", 5, MSG, "EventSource"), ("firstTimestamp", 6, TIME, None),
-              ("lastTimestamp", 7, TIME, None), ("count", 8, I32, None), ("type", 9, S, None)],
-    "EventSource": [("component", 1, S, None), ("host", 2, S, None)],
-    "ConfigMap": [("metadata", 1, MSG, "ObjectMeta"), ("data", 2, MAPS, None)],
-}
+# served kinds whose 1.9 message lives in another group/version of the same Go type
+KIND_ALIASES = {"policy/v1beta1/PodSecurityPolicy": "extensions/v1beta1/PodSecurityPolicy",
+                "policy/v1beta1/PodSecurityPolicyList": "extensions/v1beta1/PodSecurityPolicyList",
+                "storage.k8s.io/v1beta1/VolumeAttachment": "storage.k8s.io/v1alpha1/VolumeAttachment",
+                "storage.k8s.io/v1beta1/VolumeAttachmentList": "storage.k8s.io/v1alpha1/VolumeAttachmentList"}
 
-KIND_MESSAGE = {"Pod": "Pod", "Node": "Node", "Namespace": "Namespace", "Binding": "Binding", "Event": "Event",
-                "ConfigMap": "ConfigMap", "PodList": "PodList"}
-
-_BY_NUM = {m: {f[1]: f for f in fields} for m, fields in SCHEMA.items()}
-_SORTED = {m: sorted(fields, key=lambda f: f[1]) for m, fields in SCHEMA.items()}
+VARINT_TYPES = {"bool", "int32", "int64", "uint32", "uint64"}
 
 
 class ProtobufError(ValueError):
-    pass
+    def __init__(self, msg, path=""):
+        super().__init__(f"{path}: {msg}" if path else msg)
+        self.path = path
+
+
+class _Field:
+    __slots__ = ("json", "num", "label", "type", "key", "inline", "tag", "wt")
+
+    def __init__(self, json_name, num, label, typ, key, inline):
+        self.json, self.num, self.label, self.type, self.key, self.inline = json_name, num, label, typ, key, inline
+        scalar_wt = 0 if typ in VARINT_TYPES else (1 if typ == "double" else 2)
+        # packed repeated scalars are never used by the k8s protos (proto2, no [packed=true])
+        self.wt = 2 if label == "map" else scalar_wt
+        self.tag = _varint((num << 3) | self.wt)
+
+
+class Schema:
+    def __init__(self, path=SCHEMA_PATH):
+        with open(path) as f:
+            raw = json.load(f)
+        self.kinds = dict(raw["kinds"])
+        for alias, target in KIND_ALIASES.items():
+            if target in self.kinds:
+                self.kinds.setdefault(alias, self.kinds[target])
+        self.fields: dict[str, list[_Field]] = {}
+        for name, fs in raw["messages"].items():
+            self.fields[name] = sorted((_Field(*f) for f in fs), key=lambda f: f.num)
+        self.by_num = {m: {f.num: f for f in fs} for m, fs in self.fields.items()}
+        # JSON key -> field (inline embedded messages contribute their keys to the parent)
+        self.by_json: dict[str, dict[str, tuple]] = {}
+        for m in self.fields:
+            self.by_json[m] = self._json_map(m, ())
+
+    def _json_map(self, m, chain):
+        out = {}
+        for f in self.fields[m]:
+            if f.inline:
+                for k, (ff, ch) in self._json_map(f.type, chain + (f,)).items():
+                    out.setdefault(k, (ff, ch))
+            else:
+                out[f.json] = (f, chain)
+        return out
+
+    def message_for(self, api_version, kind):
+        g = api_version if "/" in api_version else ("" if api_version == "v1" else api_version)
+        key = f"{api_version}/{kind}" if g else f"v1/{kind}"
+        return self.kinds.get(key)
+
+
+_SCHEMA: Schema | None = None
+
+
+def schema() -> Schema:
+    global _SCHEMA
+    if _SCHEMA is None:
+        _SCHEMA = Schema()
+    return _SCHEMA
 
 
 # ---------------------------------------------------------------------------
@@ -222,84 +156,12 @@ def _read_varint(buf, i):
         if not b & 0x80:
             return n, i
         shift += 7
-
-
-def _parse_time(s):
-    if s is None:
-        return None
-    t = _dt.datetime.fromisoformat(s.replace("Z", "+00:00"))
-    ts = t.timestamp()
-    sec = int(ts // 1)
-    return sec, int(round((ts - sec) * 1e9)) if t.microsecond else 0
-
-
-def _fmt_time(sec, nanos):
-    t = _dt.datetime.fromtimestamp(sec, _dt.timezone.utc)
-    if nanos:
-        t = t.replace(microsecond=nanos // 1000)
-        return t.strftime("%Y-%m-%dT%H:%M:%S.%fZ")
-    return t.strftime("%Y-%m-%dT%H:%M:%SZ")
-
-
-# ---------------------------------------------------------------------------
-def encode_message(msg: str, obj: dict) -> bytes:
-    out = bytearray()
-    for name, num, kind, typ in _SORTED[msg]:
-        if kind == INL:
-            sub = encode_message(typ, obj)
-            out += _ld(num, sub)
-            continue
-        if name not in obj:
-            continue
-        v = obj[name]
-        if v is None:
-            continue
-        if kind == S:
-            out += _ld(num, str(v).encode())
-        elif kind == B:
-            out += _key(num, 0) + (b"\x01" if v else b"\x00")
-        elif kind in (I64, I32):
-            out += _key(num, 0) + _varint(int(v))
-        elif kind == MSG:
-            out += _ld(num, encode_message(typ, v))
-        elif kind == TIME:
-            sec, nanos = _parse_time(v)
-            t = _key(1, 0) + _varint(sec)
-            if nanos:
-                t += _key(2, 0) + _varint(nanos)
-            out += _ld(num, t)
-        elif kind == QTY:
-            out += _ld(num, _ld(1, str(v).encode()))
-        elif kind == IOS:
-            if isinstance(v, int):
-                out += _ld(num, _key(1, 0) + _varint(0) + _key(2, 0) + _varint(v))
-            else:
-                out += _ld(num, _key(1, 0) + _varint(1) + _key(2, 0) + _varint(0) + _ld(3, str(v).encode()))
-        elif kind == RS:
-            for x in v:
-                out += _ld(num, str(x).encode())
-        elif kind == RI64:
-            for x in v:
-                out += _key(num, 0) + _varint(int(x))
-        elif kind == RM:
-            for x in v:
-                out += _ld(num, encode_message(typ, x))
-        elif kind == MAPS:
-            for k in sorted(v):
-                out += _ld(num, _ld(1, k.encode()) + _ld(2, str(v[k]).encode()))
-        elif kind == MAPM:
-            for k in sorted(v):
-                if typ == "Quantity":
-                    val = _ld(1, str(v[k]).encode())
-                else:
-                    val = encode_message(typ, v[k])
-                out += _ld(num, _ld(1, k.encode()) + _ld(2, val))
-    return bytes(out)
+        if shift > 63:
+            raise ProtobufError("varint too long")
 
 
 def _fields(buf):
-    i = 0
-    n = len(buf)
+    i, n = 0, len(buf)
     while i < n:
         k, i = _read_varint(buf, i)
         num, wt = k >> 3, k & 7
@@ -311,84 +173,359 @@ def _fields(buf):
             if len(v) != ln:
                 raise ProtobufError("truncated field")
             i += ln
-        elif wt == 5:
-            v = buf[i:i + 4]
-            i += 4
         elif wt == 1:
             v = buf[i:i + 8]
             i += 8
+        elif wt == 5:
+            v = buf[i:i + 4]
+            i += 4
         else:
             raise ProtobufError(f"unsupported wire type {wt}")
         yield num, wt, v
 
 
 def _signed(v, bits=64):
+    v &= (1 << 64) - 1
+    if bits == 32:
+        v &= 0xFFFFFFFF
+        return v - (1 << 32) if v >= 1 << 31 else v
     return v - (1 << 64) if v >= 1 << 63 else v
 
 
-def decode_message(msg: str, buf: bytes, out=None) -> dict:
+# ---------------------------------------------------------------------------
+# special types
+_RFC3339 = re.compile(r"^(\d{4})-(\d{2})-(\d{2})[Tt ](\d{2}):(\d{2}):(\d{2})(\.\d+)?([Zz]|[+-]\d{2}:\d{2})$")
+
+
+def parse_time(s, path=""):
+    m = _RFC3339.match(s) if isinstance(s, str) else None
+    if not m:
+        raise ProtobufError(f"{s!r} is not an RFC 3339 time", path)
+    y, mo, d, h, mi, se = (int(m.group(k)) for k in range(1, 7))
+    frac = m.group(7) or ""
+    nanos = int((frac[1:] + "000000000")[:9]) if frac else 0
+    tz = m.group(8)
+    off = 0 if tz in ("Z", "z") else (1 if tz[0] == "+" else -1) * (int(tz[1:3]) * 3600 + int(tz[4:6]) * 60)
+    dt = _dt.datetime(y, mo, d, h, mi, se, tzinfo=_dt.timezone.utc)
+    return int(dt.timestamp()) - off, nanos
+
+
+def format_time(sec, nanos, micro=False):
+    t = _dt.datetime.fromtimestamp(sec, _dt.timezone.utc)
+    if micro:
+        return t.strftime("%Y-%m-%dT%H:%M:%S") + f".{nanos // 1000:06d}Z"
+    return t.strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+_DUR = re.compile(r"(\d+(?:\.\d*)?|\.\d+)(ns|us|µs|ms|s|m|h)")
+_DUR_NS = {"ns": 1, "us": 1000, "µs": 1000, "ms": 1_000_000, "s": 1_000_000_000, "m": 60_000_000_000, "h": 3_600_000_000_000}
+
+
+def parse_duration(s, path=""):
+    if not isinstance(s, str) or not s:
+        raise ProtobufError(f"{s!r} is not a duration", path)
+    neg = s.startswith("-")
+    body = s.lstrip("+-")
+    if body == "0":
+        return 0
+    pos, total = 0, 0
+    for m in _DUR.finditer(body):
+        if m.start() != pos:
+            raise ProtobufError(f"{s!r} is not a duration", path)
+        total += round(float(m.group(1)) * _DUR_NS[m.group(2)])
+        pos = m.end()
+    if pos != len(body):
+        raise ProtobufError(f"{s!r} is not a duration", path)
+    return -total if neg else total
+
+
+def format_duration(ns):
+    """Go's time.Duration.String()."""
+    if ns == 0:
+        return "0s"
+    neg, ns = ns < 0, abs(ns)
+    if ns < 1_000_000_000:
+        for unit, div in (("ms", 1_000_000), ("µs", 1000), ("ns", 1)):
+            if ns >= div:
+                v = ns / div
+                out = (f"{v:.9f}".rstrip("0").rstrip(".")) + unit
+                return ("-" if neg else "") + out
+    h, rem = divmod(ns, 3_600_000_000_000)
+    m, rem = divmod(rem, 60_000_000_000)
+    s = rem / 1e9
+    out = (f"{h}h" if h else "") + (f"{m}m" if h or m else "") + (f"{s:.9f}".rstrip("0").rstrip(".") + "s")
+    return ("-" if neg else "") + out
+
+
+# ---------------------------------------------------------------------------
+# encode
+def _scalar(f: _Field, v, path):
+    t = f.type
+    if t == "string":
+        if not isinstance(v, str):
+            raise ProtobufError(f"expected a string, got {type(v).__name__}", path)
+        b = v.encode()
+        return f.tag + _varint(len(b)) + b
+    if t == "bool":
+        if not isinstance(v, bool):
+            raise ProtobufError(f"expected a boolean, got {type(v).__name__}", path)
+        return f.tag + (b"\x01" if v else b"\x00")
+    if t in ("int32", "int64", "uint32", "uint64"):
+        if isinstance(v, bool) or not isinstance(v, (int, float)) or (isinstance(v, float) and not v.is_integer()):
+            raise ProtobufError(f"expected an integer, got {v!r}", path)
+        return f.tag + _varint(int(v))
+    if t == "bytes":
+        if not isinstance(v, str):
+            raise ProtobufError("expected a base64 string", path)
+        try:
+            b = base64.b64decode(v, validate=True)
+        except ValueError:
+            raise ProtobufError("invalid base64", path) from None
+        return f.tag + _varint(len(b)) + b
+    if t == "double":
+        import struct
+        if isinstance(v, bool) or not isinstance(v, (int, float)):
+            raise ProtobufError(f"expected a number, got {v!r}", path)
+        return f.tag + struct.pack("<d", float(v))
+    raise ProtobufError(f"unsupported scalar type {t}", path)
+
+
+def _special(t, v, path) -> bytes:
+    """The payload (message body) of a special-typed value."""
+    if t in (TIME, MICROTIME):
+        sec, nanos = parse_time(v, path)
+        if t == TIME:
+            nanos = 0      # metav1.Time is second-precision on the wire (RFC 3339 without fraction)
+        out = _key(1, 0) + _varint(sec)
+        if nanos:
+            out += _key(2, 0) + _varint(nanos)
+        return out
+    if t == QUANTITY:
+        if isinstance(v, bool) or not isinstance(v, (str, int, float)):
+            raise ProtobufError(f"expected a quantity, got {v!r}", path)
+        s = v if isinstance(v, str) else (str(int(v)) if float(v).is_integer() else repr(v))
+        return _ld(1, s.encode())
+    if t == INTORSTR:
+        if isinstance(v, bool) or not isinstance(v, (int, str)):
+            raise ProtobufError(f"expected an int or a string, got {v!r}", path)
+        if isinstance(v, int):
+            return _key(1, 0) + _varint(0) + _key(2, 0) + _varint(v) + _ld(3, b"")
+        return _key(1, 0) + _varint(1) + _key(2, 0) + _varint(0) + _ld(3, v.encode())
+    if t == DURATION:
+        return _key(1, 0) + _varint(parse_duration(v, path))
+    if t in (RAWEXT, JSONRAW):
+        return _ld(1, json.dumps(v, separators=(",", ":"), ensure_ascii=False).encode())
+    if t in SLICES:
+        if not isinstance(v, list) or not all(isinstance(x, str) for x in v):
+            raise ProtobufError("expected a list of strings", path)
+        return b"".join(_ld(1, x.encode()) for x in v)
+    if t == ORBOOL:
+        if isinstance(v, bool):
+            return _key(1, 0) + (b"\x01" if v else b"\x00")
+        return _key(1, 0) + b"\x01" + _ld(2, encode_message(_AX + "JSONSchemaProps", v, path))
+    if t == ORARRAY:
+        if isinstance(v, list):
+            return b"".join(_ld(2, encode_message(_AX + "JSONSchemaProps", x, f"{path}[{i}]")) for i, x in enumerate(v))
+        return _ld(1, encode_message(_AX + "JSONSchemaProps", v, path))
+    if t == ORSTRARRAY:
+        if isinstance(v, list):
+            return b"".join(_ld(2, str(x).encode()) for x in v)
+        return _ld(1, encode_message(_AX + "JSONSchemaProps", v, path))
+    raise ProtobufError(f"unsupported special type {t}", path)
+
+
+def _value(f: _Field, v, path) -> bytes:
+    t = f.type
+    if t in SPECIAL:
+        body = _special(t, v, path)
+        return f.tag + _varint(len(body)) + body
+    if "." in t:
+        if not isinstance(v, dict):
+            raise ProtobufError(f"expected an object, got {type(v).__name__}", path)
+        body = encode_message(t, v, path)
+        return f.tag + _varint(len(body)) + body
+    return _scalar(f, v, path)
+
+
+def _map_entry(f: _Field, k, v, path) -> bytes:
+    kf = _Field("key", 1, "opt", f.key, "", False)
+    vf = _Field("value", 2, "opt", f.type, "", False)
+    if f.key in VARINT_TYPES:
+        try:
+            k = int(k)
+        except ValueError:
+            raise ProtobufError(f"map key {k!r} is not an integer", path) from None
+    body = _scalar(kf, k, path) + _value(vf, v, f"{path}[{k}]")
+    return f.tag + _varint(len(body)) + body
+
+
+def encode_message(msg: str, obj: dict, path="") -> bytes:
+    """obj (JSON form) -> message bytes. Raises ProtobufError on a field outside the schema."""
+    s = schema()
+    fields = s.fields.get(msg)
+    if fields is None:
+        raise ProtobufError(f"no protobuf message {msg}", path)
+    jm = s.by_json[msg]
+    # group the object's keys by the top-level field they encode into (inline chains)
+    inline_parts: dict[int, dict] = {}
+    direct = {}
+    for k, v in obj.items():
+        if v is None:
+            continue
+        ent = jm.get(k)
+        if ent is None:
+            if k in ("kind", "apiVersion"):
+                continue          # TypeMeta: envelope only
+            raise ProtobufError(f"field {k!r} is not part of {msg.rsplit('.', 1)[-1]} in the API schema",
+                                f"{path}.{k}" if path else k)
+        f, chain = ent
+        if chain:
+            inline_parts.setdefault(chain[0].num, {})[k] = v
+        else:
+            direct[f.num] = (f, v)
+    out = bytearray()
+    for f in fields:
+        if f.inline:
+            part = inline_parts.get(f.num)
+            if part is not None:
+                body = encode_message(f.type, part, path)
+                out += f.tag + _varint(len(body)) + body
+            continue
+        ent = direct.get(f.num)
+        if ent is None:
+            continue
+        _, v = ent
+        p = f"{path}.{f.json}" if path else f.json
+        if f.label == "rep":
+            if not isinstance(v, list):
+                raise ProtobufError(f"expected a list, got {type(v).__name__}", p)
+            for i, x in enumerate(v):
+                if x is None:
+                    raise ProtobufError("null list element", f"{p}[{i}]")
+                out += _value(f, x, f"{p}[{i}]")
+        elif f.label == "map":
+            if not isinstance(v, dict):
+                raise ProtobufError(f"expected a map, got {type(v).__name__}", p)
+            for k in sorted(v):
+                if v[k] is None:
+                    raise ProtobufError("null map value", f"{p}[{k}]")
+                out += _map_entry(f, k, v[k], p)
+        else:
+            out += _value(f, v, p)
+    return bytes(out)
+
+
+# ---------------------------------------------------------------------------
+# decode
+def _decode_scalar(t, wt, v):
+    if t == "string":
+        return bytes(v).decode()
+    if t == "bool":
+        return bool(v)
+    if t == "int32":
+        return _signed(v, 32)
+    if t in ("int64",):
+        return _signed(v)
+    if t in ("uint32", "uint64"):
+        return v
+    if t == "bytes":
+        return base64.b64encode(bytes(v)).decode()
+    if t == "double":
+        import struct
+        return struct.unpack("<d", bytes(v))[0]
+    raise ProtobufError(f"unsupported scalar type {t}")
+
+
+def _decode_special(t, v):
+    if t in (TIME, MICROTIME):
+        sec = nanos = 0
+        for n, _, x in _fields(v):
+            if n == 1:
+                sec = _signed(x)
+            elif n == 2:
+                nanos = x
+        return format_time(sec, nanos, t == MICROTIME)
+    if t == QUANTITY:
+        return next((bytes(x).decode() for n, _, x in _fields(v) if n == 1), "0")
+    if t == INTORSTR:
+        typ, iv, sv = 0, 0, ""
+        for n, _, x in _fields(v):
+            if n == 1:
+                typ = x
+            elif n == 2:
+                iv = _signed(x, 32)
+            elif n == 3:
+                sv = bytes(x).decode()
+        return iv if typ == 0 else sv
+    if t == DURATION:
+        return format_duration(next((_signed(x) for n, _, x in _fields(v) if n == 1), 0))
+    if t in (RAWEXT, JSONRAW):
+        raw = next((bytes(x) for n, _, x in _fields(v) if n == 1), b"")
+        return json.loads(raw) if raw else None
+    if t in SLICES:
+        return [bytes(x).decode() for n, _, x in _fields(v) if n == 1]
+    if t == ORBOOL:
+        allows, sch = False, None
+        for n, _, x in _fields(v):
+            if n == 1:
+                allows = bool(x)
+            elif n == 2:
+                sch = decode_message(_AX + "JSONSchemaProps", x)
+        return sch if sch is not None else allows
+    if t in (ORARRAY, ORSTRARRAY):
+        sch, arr = None, []
+        for n, _, x in _fields(v):
+            if n == 1:
+                sch = decode_message(_AX + "JSONSchemaProps", x)
+            elif n == 2:
+                arr.append(decode_message(_AX + "JSONSchemaProps", x) if t == ORARRAY else bytes(x).decode())
+        return sch if sch is not None else arr
+    raise ProtobufError(f"unsupported special type {t}")
+
+
+def _decode_value(t, wt, v):
+    if t in SPECIAL:
+        return _decode_special(t, v)
+    if "." in t:
+        return decode_message(t, v)
+    return _decode_scalar(t, wt, v)
+
+
+def decode_message(msg: str, buf, out=None) -> dict:
+    s = schema()
+    byn = s.by_num.get(msg)
+    if byn is None:
+        raise ProtobufError(f"no protobuf message {msg}")
     out = {} if out is None else out
-    byn = _BY_NUM[msg]
     for num, wt, v in _fields(buf):
         f = byn.get(num)
         if f is None:
-            continue  # unknown field: skipped (forward compatible)
-        name, _, kind, typ = f
-        if kind == INL:
-            decode_message(typ, v, out)
-        elif kind == S:
-            out[name] = bytes(v).decode()
-        elif kind == B:
-            out[name] = bool(v)
-        elif kind in (I64, I32):
-            out[name] = _signed(v)
-        elif kind == MSG:
-            out[name] = decode_message(typ, v)
-        elif kind == TIME:
-            sec = nanos = 0
-            for n2, _, x in _fields(v):
-                if n2 == 1:
-                    sec = _signed(x)
-                elif n2 == 2:
-                    nanos = x
-            out[name] = _fmt_time(sec, nanos)
-        elif kind == QTY:
-            out[name] = next((bytes(x).decode() for n2, _, x in _fields(v) if n2 == 1), "0")
-        elif kind == IOS:
-            t = iv = 0
-            sv = ""
-            for n2, _, x in _fields(v):
-                if n2 == 1:
-                    t = x
-                elif n2 == 2:
-                    iv = _signed(x)
-                elif n2 == 3:
-                    sv = bytes(x).decode()
-            out[name] = iv if t == 0 else sv
-        elif kind == RS:
-            out.setdefault(name, []).append(bytes(v).decode())
-        elif kind == RI64:
-            out.setdefault(name, []).append(_signed(v))
-        elif kind == RM:
-            out.setdefault(name, []).append(decode_message(typ, v))
-        elif kind in (MAPS, MAPM):
+            continue  # unknown field: skipped (forward compatible, as gogo-protobuf)
+        if f.inline:
+            decode_message(f.type, v, out)
+        elif f.label == "rep":
+            out.setdefault(f.json, []).append(_decode_value(f.type, wt, v))
+        elif f.label == "map":
             k = val = None
-            for n2, _, x in _fields(v):
+            vwt = 2
+            for n2, w2, x in _fields(v):
                 if n2 == 1:
-                    k = bytes(x).decode()
+                    k = _decode_scalar(f.key, w2, x)
                 elif n2 == 2:
-                    val = x
-            m = out.setdefault(name, {})
-            if kind == MAPS:
-                m[k] = bytes(val or b"").decode()
-            elif typ == "Quantity":
-                m[k] = next((bytes(x).decode() for n2, _, x in _fields(val or b"") if n2 == 1), "0")
-            else:
-                m[k] = decode_message(typ, val or b"")
+                    val, vwt = x, w2
+            if f.key in VARINT_TYPES:
+                k = str(k)
+            m = out.setdefault(f.json, {})
+            if val is None:
+                val = b"" if vwt == 2 else 0
+            m[k if k is not None else ""] = _decode_value(f.type, vwt, val)
+        else:
+            out[f.json] = _decode_value(f.type, wt, v)
     return out
 
 
 # ---------------------------------------------------------------------------
+# envelope
 def encode_unknown(api_version: str, kind: str, raw: bytes) -> bytes:
     tm = _ld(1, api_version.encode()) + _ld(2, kind.encode())
     return MAGIC + _ld(1, tm) + _ld(2, raw) + _ld(3, b"") + _ld(4, b"")
@@ -399,7 +536,7 @@ def decode_unknown(data: bytes):
         raise ProtobufError("missing k8s protobuf magic")
     api_version = kind = ""
     raw = b""
-    for num, _, v in _fields(data[4:]):
+    for num, _, v in _fields(memoryview(data)[4:]):
         if num == 1:
             for n2, _, x in _fields(v):
                 if n2 == 1:
@@ -411,36 +548,83 @@ def decode_unknown(data: bytes):
     return api_version, kind, raw
 
 
+def message_of(obj) -> str | None:
+    return schema().message_for(obj.get("apiVersion", "v1") or "v1", obj.get("kind", ""))
+
+
+def supported(kind: str, api_version: str = "") -> bool:
+    s = schema()
+    if api_version:
+        return s.message_for(api_version, kind) is not None
+    return any(k.rsplit("/", 1)[-1] == kind for k in s.kinds)
+
+
+def _native():
+    from ..native import pbcodec
+    return pbcodec.codec()
+
+
 def encode_object(obj: dict) -> bytes:
-    kind = obj.get("kind", "")
-    msg = KIND_MESSAGE.get(kind)
+    kind, av = obj.get("kind", ""), obj.get("apiVersion", "v1") or "v1"
+    msg = schema().message_for(av, kind)
     if msg is None:
-        raise ProtobufError(f"no protobuf schema for kind {kind!r}")
-    body = {k: v for k, v in obj.items() if k not in ("kind", "apiVersion")}
-    return encode_unknown(obj.get("apiVersion", "v1"), kind, encode_message(msg, body))
+        raise ProtobufError(f"no protobuf message for {av}/{kind}")
+    nat = _native()
+    if nat is not None:
+        return nat.encode_object(obj, msg)
+    return encode_unknown(av, kind, encode_message(msg, obj))
 
 
 def decode_object(data: bytes) -> dict:
+    nat = _native()
+    if nat is not None:
+        return nat.decode_object(data)
     api_version, kind, raw = decode_unknown(data)
-    msg = KIND_MESSAGE.get(kind)
+    msg = schema().message_for(api_version, kind)
     if msg is None:
-        raise ProtobufError(f"no protobuf schema for kind {kind!r}")
+        raise ProtobufError(f"no protobuf message for {api_version}/{kind}")
     out = {"kind": kind, "apiVersion": api_version}
     out.update(decode_message(msg, raw))
     return out
 
 
-def supported(kind: str) -> bool:
-    return kind in KIND_MESSAGE
-
-
 # storage codec hooks (codec.StorageCodec)
+def _alternates(obj):
+    """Other versions of the object's kind in the reference schema, newest first: an object whose
+    fields only exist in a later version (autoscaling/v1 HPA with v2beta1 `metrics`) is stored in
+    that version's message, as the reference stores an HPA's metrics losslessly (its storage
+    version carries them as an annotation; here the version that has the fields is chosen)."""
+    from .meta import version_priority
+    av, kind = obj.get("apiVersion", "v1") or "v1", obj.get("kind", "")
+    group = av.rsplit("/", 1)[0] if "/" in av else ""
+    out = []
+    for key in schema().kinds:
+        g, _, rest = key.rpartition("/")
+        ver_group, _, ver = g.rpartition("/") if "/" in g else ("", "", g)
+        if rest == kind and ver_group == group and f"{g}" != av:
+            out.append((version_priority(ver), g))
+    return [g for _, g in sorted(out, reverse=True)]
+
+
 def encode_storage(obj):
-    if supported(obj.get("kind", "")):
+    if message_of(obj) is None:
+        from .codec import dumpb
+        return dumpb(obj)          # custom resources / kinds outside the reference schema: JSON
+    try:
         return encode_object(obj)
-    from .codec import dumpb
-    return dumpb(obj)
+    except ProtobufError as first:
+        for av in _alternates(obj):
+            try:
+                return encode_object(dict(obj, apiVersion=av))
+            except ProtobufError:
+                continue
+        raise first
 
 
 def decode_storage(data):
-    return decode_object(data)
+    obj = decode_object(data)
+    from .meta import BY_KIND
+    ri = BY_KIND.get(obj.get("kind", ""))
+    if ri is not None and obj.get("apiVersion") != ri.group_version:
+        obj["apiVersion"] = ri.group_version      # stored in another version of the same type
+    return obj

@@ -183,8 +183,8 @@ class InitialResources(Plugin):
 
 def _volume_node(pv):
     """Node name a node-pinned PV lives on: required node affinity on kubernetes.io/hostname."""
-    aff = ((pv.get("spec") or {}).get("nodeAffinity") or {}).get("required") or {}
-    for term in aff.get("nodeSelectorTerms") or []:
+    from ...scheduler.volumes import pv_node_terms
+    for term in pv_node_terms(pv) or []:
         for e in term.get("matchExpressions") or []:
             if e.get("key") == HOSTNAME_LABEL and e.get("operator") == "In" and len(e.get("values") or []) == 1:
                 return e["values"][0]

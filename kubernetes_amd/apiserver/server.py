@@ -98,6 +98,17 @@ ENC_PREFIX = b"k8s:enc:"          # encrypted-at-rest value (storage/value.py)
 _FRAME = b"\x00KH"                 # shared-store value framing (index header + object)
 
 
+def pb_to_json(body, rev) -> bytes:
+    """A protobuf-stored object (k8s\\0 envelope) as JSON bytes with resourceVersion = rev."""
+    from ..native import pbcodec
+    nat = pbcodec.codec()
+    if nat is not None:
+        return nat.to_json(body, str(rev))
+    from ..api import protobuf as pb
+    obj = pb.decode_object(body)
+    obj.setdefault("metadata", {})["resourceVersion"] = str(rev)
+    return codec.dumpb(obj)
+
 
 def _requested_gv(path):
     parts = path.split("/", 4)
@@ -124,7 +135,7 @@ def _rewrite_gv(body, canonical, served):
 class APIServer:
     def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
-                 max_mutating_inflight=2000, storage_media_type=codec.JSON, watch_window=200_000,
+                 max_mutating_inflight=2000, storage_media_type=codec.PROTOBUF, watch_window=200_000,
                  kubelet_port_resolver=None, audit=None, encryption_config=None,
                  service_cluster_ip_range="10.0.0.0/24", service_node_port_range=(30000, 32767),
                  tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
@@ -350,12 +361,22 @@ class APIServer:
         """Resources this shared-mode worker serves from the store instead of a watch cache:
         pods and events, unless something here must read them synchronously (the Node
         authorizer's pod graph) or their watches cannot be handed to the store's fan-out
-        (encrypted / non-JSON storage, TLS client connections). KAMD_SHARED_CACHE_ALL=1 keeps
+        (encrypted storage, TLS client connections). KAMD_SHARED_CACHE_ALL=1 keeps
         every resource cached."""
         if os.environ.get("KAMD_SHARED_CACHE_ALL") == "1" or self.fanout is None or self.tls[0] \
-                or self.storage_codec.media_type != codec.JSON or "Node" in self.authorization_modes:
+                or "Node" in self.authorization_modes:
             return frozenset()
         return frozenset(p for p in ("pods", "events") if p not in self.transformers)
+
+    def _storage_encode(self, ri, obj):
+        """The storage bytes of obj; a field outside the reference schema is a 422, never a silent
+        drop (the protobuf encoder refuses what it cannot represent)."""
+        from ..api.protobuf import ProtobufError
+        try:
+            return self.storage_codec.encode(obj)
+        except ProtobufError as e:
+            from ..api.validation import FieldError
+            raise invalid(ri, m.name_of(obj), [FieldError("Invalid value", e.path or "<object>", str(e).split(": ", 1)[-1])])
 
     def _entry_from_kv(self, plural, kv):
         """Entry for a stored value without decoding the object: shared-store values carry the
@@ -364,7 +385,12 @@ class APIServer:
         if v[:3] == _FRAME:
             hl = int.from_bytes(v[3:7], "little")
             fields, labels = codec.loads(v[7:7 + hl])
-            return Entry(None, v[7 + hl:], kv.mod_rev, fields, labels)
+            body = v[7 + hl:]
+            if body[:4] == codec.MAGIC:
+                # protobuf storage: JSON for GET/LIST/watch payloads, resourceVersion from the
+                # key's mod revision (etcd3 never stores it)
+                body = pb_to_json(body, kv.mod_rev)
+            return Entry(None, body, kv.mod_rev, fields, labels)
         obj, raw = self._decode_value(kv)
         return self.caches[plural].make_entry(obj, raw, kv.mod_rev)
 
@@ -528,13 +554,16 @@ class APIServer:
         else:
             md.pop("resourceVersion", None)
             raw_t = None
-            stored = self._seal(ri.plural, key, self.storage_codec.encode(obj))
+            enc = self._storage_encode(ri, obj)
+            # unsealed protobuf keeps the index frame: the store's fan-out filters on it and
+            # transcodes the object for JSON watchers
+            stored = self._seal(ri.plural, key, enc) if sealed else frame + enc
         cmps = [(wire.CMP_MOD_REV, key, prev.rev if prev is not None else 0, None)]
         if etype == DELETED and sealed:
             # no plaintext index header or tombstone for encrypted resources
             ops = [(wire.OP_DELETE_TOMBSTONE, key, self._seal(ri.plural, key, codec.dumpb(obj)), tok)]
         elif etype == DELETED:
-            tomb = raw_t if raw_t is not None else codec.dumpb(dict(obj, metadata=dict(md, resourceVersion=tok.decode())))
+            tomb = raw_t if raw_t is not None else stored[len(frame):]
             ops = [(wire.OP_DELETE_TOMBSTONE, key, frame + tomb, tok)]
         elif json_storage:
             ops = [(wire.OP_PUT_INJECT, key, stored, tok)]
@@ -556,7 +585,14 @@ class APIServer:
         def on_ok(rev):
             rs = str(rev)
             md["resourceVersion"] = rs
-            raw = raw_t.replace(tok, rs.encode()) if raw_t is not None else codec.dumpb(obj)
+            if raw_t is not None:
+                raw = raw_t.replace(tok, rs.encode())
+            elif not sealed:
+                # what every other worker (and the store's fan-out) will serve for this revision:
+                # the stored protobuf's JSON form (Go omitempty: no empty maps / lists)
+                raw = pb_to_json(stored[len(frame):], rev) if etype != DELETED else codec.dumpb(obj)
+            else:
+                raw = codec.dumpb(obj)
             entry = cache.make_entry(obj, raw, rev)
             if not uncached:
                 self._mine[(key, rev)] = entry
@@ -611,7 +647,7 @@ class APIServer:
         rev = self.store.revision + 1
         obj["metadata"]["resourceVersion"] = str(rev)
         raw = codec.dumpb(obj)
-        stored = raw if self.storage_codec.media_type == codec.JSON else self.storage_codec.encode(obj)
+        stored = raw if self.storage_codec.media_type == codec.JSON else self._storage_encode(ri, obj)
         if ri.plural in self.transformers:
             stored = self._seal(ri.plural, key, stored)
         if etype == ADDED:
@@ -1456,9 +1492,10 @@ class APIServer:
 
     def _fanout_spec(self, req, ri, ns, label_selector, field_selector, shard=None):
         """Requirements for kamd-etcd's watch fan-out, or None when this watch must stay here:
-        TLS connections (the TLS session lives in this process), encrypted or non-JSON storage
-        (the store cannot read the index frame), quantity comparisons in label selectors."""
-        if self.fanout is None or ri.plural in self.transformers or self.storage_codec.media_type != codec.JSON:
+        TLS connections (the TLS session lives in this process), encrypted storage (the store
+        cannot read the sealed index frame), quantity comparisons in label selectors. Protobuf
+        values are transcoded to JSON by the store (native/pbcodec/pb_codec.h)."""
+        if self.fanout is None or ri.plural in self.transformers:
             return None
         if req.transport is None or req.transport.get_extra_info("sslcontext") is not None:
             return None

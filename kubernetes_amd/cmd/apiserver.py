@@ -36,7 +36,8 @@ def _parser():
                     help="AdmissionConfiguration: plugins[{name, path | configuration}]")
     ap.add_argument("--authorization-mode", default="AlwaysAllow")
     ap.add_argument("--token-auth-file", default=None)
-    ap.add_argument("--storage-media-type", default=codec.JSON)
+    # the reference stores protobuf by default (cmd/kube-apiserver/app/options/options.go:117)
+    ap.add_argument("--storage-media-type", default=codec.PROTOBUF)
     ap.add_argument("--storage-engine", default="native", choices=["native", "python"])
     ap.add_argument("--etcd-wal", default=None, help="durable WAL path for the store")
     ap.add_argument("--etcd-fan-threads", type=int, default=0,

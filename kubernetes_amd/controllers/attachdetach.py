@@ -14,6 +14,8 @@ Parity:
 """
 from __future__ import annotations
 
+from ..csi.driver import volume_attributes
+
 from ..client.rest import APIStatusError, is_not_found
 from ..csi import api as CSI
 from .base import Controller
@@ -133,7 +135,7 @@ class ExternalAttacher(Controller):
             return
         try:
             info = await self.csi.controller_publish(src["volumeHandle"], va["spec"]["nodeName"], bool(src.get("readOnly")),
-                                                     src.get("volumeAttributes"), (pv.get("spec") or {}).get("accessModes"))
+                                                     volume_attributes(pv), (pv.get("spec") or {}).get("accessModes"))
         except Exception as e:  # noqa: BLE001 - reported in status.attachError, retried
             await self.client.patch(VA, key, {"status": {"attached": False, "attachError": {"message": str(e)}}}, None,
                                     "merge", "status")

@@ -3,9 +3,11 @@
 DaemonSet parity: `pkg/controller/daemon/daemon_controller.go` (nodeShouldRunDaemonPod: node
 selector / affinity / taints-tolerations, one pod per eligible node, delete pods on nodes that
 no longer qualify, status counts). Design choice: instead of the 1.9 behaviour of writing
-`spec.nodeName` directly, each daemon pod is pinned with required node affinity
-(`matchFields metadata.name`) and goes through the scheduler — so a DaemonSet requesting
-`amd.com/gpu` (e.g. a per-node GPU burn-in / xGMI probe) gets real device IDs allocated.
+`spec.nodeName` directly (`daemon_controller.go:1323` NewPod), each daemon pod is pinned with
+required node affinity on the node's `kubernetes.io/hostname` label (the 1.9 NodeSelectorTerm
+has no `matchFields`; the kubelet sets that label to the node name) and goes through the
+scheduler — so a DaemonSet requesting `amd.com/gpu` (e.g. a per-node GPU burn-in / xGMI probe)
+gets real device IDs allocated.
 
 StatefulSet parity: `pkg/controller/statefulset/stateful_set_control.go` — ordinal pods
 `<name>-<i>`, OrderedReady (create i only when 0..i-1 are Running and Ready, delete from the
@@ -22,6 +24,8 @@ from ..scheduler import predicates as P
 from ..scheduler.cache import NodeInfo, PodInfo
 from .history import REVISION_HASH, ensure_revision, revisions_of
 from .base import Controller, controller_ref, pod_from_template, pod_is_active, pod_is_ready, split_key
+
+HOSTNAME = "kubernetes.io/hostname"
 
 DS_TOLERATIONS = [
     {"key": "node.alpha.kubernetes.io/notReady", "operator": "Exists", "effect": "NoExecute"},
@@ -79,8 +83,8 @@ class DaemonSetController(Controller):
             return nn
         aff = ((pod.get("spec") or {}).get("affinity") or {}).get("nodeAffinity") or {}
         for t in (aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}).get("nodeSelectorTerms") or ():
-            for f in t.get("matchFields") or ():
-                if f.get("key") == "metadata.name" and f.get("values"):
+            for f in t.get("matchExpressions") or ():
+                if f.get("key") == HOSTNAME and f.get("operator") == "In" and f.get("values"):
                     return f["values"][0]
         return None
 
@@ -124,7 +128,7 @@ class DaemonSetController(Controller):
             spec["tolerations"] = list(spec.get("tolerations") or []) + DS_TOLERATIONS
             aff = spec.setdefault("affinity", {}).setdefault("nodeAffinity", {})
             aff["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [
-                {"matchFields": [{"key": "metadata.name", "operator": "In", "values": [node]}]}]}
+                {"matchExpressions": [{"key": HOSTNAME, "operator": "In", "values": [node]}]}]}
             creating.add(node)
             await self.client.create("pods", pod, ns)
 

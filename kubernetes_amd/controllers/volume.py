@@ -18,6 +18,7 @@ Parity: `pkg/controller/volume/persistentvolume/pv_controller.go`:
 """
 from __future__ import annotations
 
+import json
 import os
 import shutil
 
@@ -25,6 +26,9 @@ from ..api.labels import label_selector_as_selector
 from ..api.quantity import parse_quantity
 from ..client.rest import APIStatusError, is_not_found
 from .base import Controller, split_key
+
+# the 1.9 alpha PV node-affinity annotation (spec.nodeAffinity is 1.10+); read by scheduler/volumes.py
+NODE_AFFINITY_ANN = "volume.alpha.kubernetes.io/node-affinity"
 
 BIND_COMPLETED = "pv.kubernetes.io/bind-completed"
 BOUND_BY_CONTROLLER = "pv.kubernetes.io/bound-by-controller"
@@ -170,15 +174,19 @@ class PersistentVolumeController(Controller):
         path = os.path.join(self.hostpath_root, name)
         os.makedirs(path, exist_ok=True)
         sp = pvc.get("spec") or {}
+        ann = {PROVISIONED_BY: HOSTPATH_PROVISIONER}
+        if md_ann(pvc).get(SELECTED_NODE):
+            # node-pinned volume: the 1.9 alpha node-affinity annotation (v1.NodeAffinity JSON,
+            # staging/src/k8s.io/api/core/v1/types.go:464) — spec.nodeAffinity is 1.10+
+            ann[NODE_AFFINITY_ANN] = json.dumps({"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+                {"matchExpressions": [{"key": "kubernetes.io/hostname", "operator": "In",
+                                       "values": [md_ann(pvc)[SELECTED_NODE]]}]}]}})
         pv = {"apiVersion": "v1", "kind": "PersistentVolume",
-              "metadata": {"name": name, "annotations": {PROVISIONED_BY: HOSTPATH_PROVISIONER}},
+              "metadata": {"name": name, "annotations": ann},
               "spec": {"capacity": {"storage": ((sp.get("resources") or {}).get("requests") or {}).get("storage", "1Gi")},
                        "accessModes": sp.get("accessModes") or ["ReadWriteOnce"],
                        "persistentVolumeReclaimPolicy": sc.get("reclaimPolicy") or "Delete",
                        "storageClassName": cls, "hostPath": {"path": path},
-                       **({"nodeAffinity": {"required": {"nodeSelectorTerms": [{"matchExpressions": [
-                           {"key": "kubernetes.io/hostname", "operator": "In", "values": [md_ann(pvc)[SELECTED_NODE]]}]}]}}}
-                          if md_ann(pvc).get(SELECTED_NODE) else {}),
                        "claimRef": {"kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": md["namespace"],
                                     "name": md["name"], "uid": md["uid"]}}}
         try:

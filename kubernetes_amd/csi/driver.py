@@ -144,3 +144,22 @@ class CSIClient:
 
     async def close(self):
         await self.channel.close()
+
+
+# CSIPersistentVolumeSource in this API version (staging/src/k8s.io/api/core/v1/types.go:1693) has
+# driver / volumeHandle / readOnly only; the attributes handed to the driver's ControllerPublish
+# and NodePublish travel in this PV annotation (JSON map) — spec.csi.volumeAttributes is 1.10+.
+VOLUME_ATTRIBUTES_ANNOTATION = "csi.volume.kubernetes.io/volume-attributes"
+
+
+def volume_attributes(pv) -> dict:
+    import json
+    ann = ((pv or {}).get("metadata") or {}).get("annotations") or {}
+    raw = ann.get(VOLUME_ATTRIBUTES_ANNOTATION)
+    if not raw:
+        return {}
+    try:
+        v = json.loads(raw)
+    except ValueError:
+        return {}
+    return {str(k): str(x) for k, x in v.items()} if isinstance(v, dict) else {}

@@ -170,20 +170,20 @@ class VolumeManager:
             d = os.path.join(self.pod_dir(pod), "volumes", "flexvolume", vol)
             return await self._flex_mount(pod, vol, sp["flexVolume"], d)
         if sp.get("csi"):
-            return await self._csi_publish(pod, vol, sp, node_name or self.node_name)
+            return await self._csi_publish(pod, vol, sp, node_name or self.node_name, pv)
         path = (sp.get("hostPath") or {}).get("path") or (sp.get("local") or {}).get("path")
         if not path:
             raise VolumeError(f"persistentvolume {vol}: only hostPath / local volumes can be mounted on this node")
         os.makedirs(path, exist_ok=True)
         return path
 
-    async def _csi_publish(self, pod, pv_name, sp, node_name):
+    async def _csi_publish(self, pod, pv_name, sp, node_name, pv=None):
         """`pkg/volume/csi/csi_attacher.go` WaitForAttach (the VolumeAttachment the attach/detach
         controller created must report `attached`) then `csi_mounter.go` SetUpAt:
         NodePublishVolume to `<pod dir>/volumes/kubernetes.io~csi/<pv>/mount`."""
         import asyncio
         from ..csi import api as CSI
-        from ..csi.driver import CSIClient
+        from ..csi.driver import CSIClient, volume_attributes
         src = sp["csi"]
         driver, handle = src["driver"], src["volumeHandle"]
         va_name = CSI.attachment_name(pv_name, driver, node_name)
@@ -207,7 +207,7 @@ class VolumeManager:
         target = os.path.join(self.pod_dir(pod), "volumes", "kubernetes.io~csi", pv_name, "mount")
         c = CSIClient(CSI.socket_path(self.csi_dir, driver))
         try:
-            await c.node_publish(handle, target, bool(src.get("readOnly")), info, src.get("volumeAttributes"),
+            await c.node_publish(handle, target, bool(src.get("readOnly")), info, volume_attributes(pv),
                                  sp.get("accessModes"), src.get("fsType", ""))
         except Exception as e:  # noqa: BLE001 - surfaced as a mount failure, retried by the kubelet
             raise VolumeError(f"NodePublishVolume {handle} via {driver}: {e}")

@@ -26,8 +26,14 @@ def _s(*p):
     return os.path.join(SRC_DIR, *p)
 
 
+def _py_ext():
+    import sysconfig
+    return sysconfig.get_paths()["include"], sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
 def targets():
     cxx = ["g++", "-O2", "-std=c++17", "-Wall", "-fPIC"]
+    py_inc, ext = _py_ext()
     hip = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
     return {
         "kamd_smi": ([_s("amdsmi_shim", "kamd_smi.cc"), _s("amdsmi_shim", "kamd_smi.h")],
@@ -35,8 +41,12 @@ def targets():
                      cxx + ["-shared", f"-I{ROCM}/include", _s("amdsmi_shim", "kamd_smi.cc"), "-ldl"]),
         "kamd_store": ([_s("store", "mvcc_store.cc")], os.path.join(LIB_DIR, "libkamd_store.so"),
                        cxx + ["-O3", "-shared", _s("store", "mvcc_store.cc")]),
-        "kamd_etcd": ([_s("store", "mvcc_store.cc")], os.path.join(BIN_DIR, "kamd-etcd"),
+        "kamd_etcd": ([_s("store", "mvcc_store.cc"), _s("pbcodec", "pb_codec.h")], os.path.join(BIN_DIR, "kamd-etcd"),
                       cxx + ["-O3", "-pthread", "-DKAMD_STORE_SERVER", _s("store", "mvcc_store.cc")]),
+        # the API server's protobuf storage codec (CPython extension over native/pbcodec/pb_codec.h)
+        "kamd_pbcodec": ([_s("pbcodec", "kamd_pbcodec.cc"), _s("pbcodec", "pb_codec.h")],
+                         os.path.join(LIB_DIR, "_kamd_pbcodec" + ext),
+                         cxx + ["-O3", "-shared", f"-I{py_inc}", _s("pbcodec", "kamd_pbcodec.cc")]),
         "kamd_oci": ([_s("oci", "oci_devices.cc")], os.path.join(LIB_DIR, "libkamd_oci.so"),
                      cxx + ["-shared", _s("oci", "oci_devices.cc")]),
         "kamd_crypto": ([_s("crypto", "kamd_crypto.cc")], os.path.join(LIB_DIR, "libkamd_crypto.so"),
@@ -76,10 +86,10 @@ def sanitizer_targets():
     asan, tsan = os.path.join(SAN_DIR, "asan"), os.path.join(SAN_DIR, "tsan")
     store = _s("store", "mvcc_store.cc")
     return {
-        "asan_kamd_etcd": ([store], os.path.join(asan, "kamd-etcd"),
+        "asan_kamd_etcd": ([store, _s("pbcodec", "pb_codec.h")], os.path.join(asan, "kamd-etcd"),
                            base + SAN_FLAGS["asan"] + ["-pthread", "-DKAMD_STORE_SERVER", store]),
         # the store thread and the watch fan-out thread share the event queue and KV lifetimes
-        "tsan_kamd_etcd": ([store], os.path.join(tsan, "kamd-etcd"),
+        "tsan_kamd_etcd": ([store, _s("pbcodec", "pb_codec.h")], os.path.join(tsan, "kamd-etcd"),
                            base + SAN_FLAGS["tsan"] + ["-pthread", "-DKAMD_STORE_SERVER", store]),
         "asan_store_fuzz": ([store, _s("tests", "store_fuzz.cc")], os.path.join(asan, "store_fuzz"),
                             base + SAN_FLAGS["asan"] + [_s("tests", "store_fuzz.cc")]),

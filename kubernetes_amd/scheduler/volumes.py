@@ -25,11 +25,10 @@ import json
 import os
 
 from ..api.labels import SelectorError, node_selector_requirements_as_selector
-from ..controllers.volume import best_match, claim_class
+from ..controllers.volume import NODE_AFFINITY_ANN, best_match, claim_class
 
 ZONE_LABEL = "failure-domain.beta.kubernetes.io/zone"
 REGION_LABEL = "failure-domain.beta.kubernetes.io/region"
-NODE_AFFINITY_ANN = "volume.alpha.kubernetes.io/node-affinity"
 SELECTED_NODE_ANN = "volume.kubernetes.io/selected-node"
 WAIT = "WaitForFirstConsumer"
 

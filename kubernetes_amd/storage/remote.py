@@ -266,7 +266,10 @@ class StoreServer:
         exe = os.environ.get("KAMD_ETCD_BIN") or os.path.join(BIN_DIR, "kamd-etcd")
         if not os.path.exists(exe):
             raise StoreError(f"{exe} not built (python -m kubernetes_amd.native.build)")
+        from ..api.protobuf import SCHEMA_PATH
         cmd = [exe, "--history", str(self.history), "--fan-threads", str(self.fan_threads)]
+        if os.path.exists(SCHEMA_PATH):
+            cmd += ["--pb-schema", SCHEMA_PATH]     # the fan-out transcodes protobuf values for JSON watchers
         port_file = None
         if self.tcp:
             port_file = tempfile.mktemp(prefix="kamd-etcd-port-")

@@ -58,6 +58,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <string_view>
 #include <atomic>
 #include <deque>
 #include <map>
@@ -68,6 +69,13 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#ifdef KAMD_STORE_SERVER
+// protobuf-stored objects are transcoded to JSON for Kubernetes watch streams (schema-driven,
+// shared with the API server's codec)
+#include "../pbcodec/pb_codec.h"
+static pbc::Schema* g_pb_schema = nullptr;
+#endif
 
 namespace kamd {
 
@@ -526,7 +534,11 @@ struct Index {
   bool ok = false;
   SVMap fields, labels;
   std::deque<std::string> owned;
-  size_t body = 0;  // offset of the object JSON in the value
+  size_t body = 0;  // offset of the object (JSON, or a k8s\0 protobuf envelope) in the value
+  // protobuf values: the object's JSON for resourceVersion `json_rv` (transcoded once per
+  // fan-out thread and revision; the thread owning this Index is the only one touching it)
+  mutable std::string json;
+  mutable int64_t json_rv = -1;
 };
 
 struct JsonCursor {
@@ -732,18 +744,39 @@ static double mono_now() {
   return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-static void chunk(std::string* out, const char* type, const std::string& v, size_t body) {
+// the object JSON of a stored value: the bytes after the index frame, or — for a protobuf
+// (k8s\0) value — its JSON transcoding with metadata.resourceVersion = rv, cached on the Index
+static std::string_view object_json(const std::string& v, const Index& ix, int64_t rv) {
+  size_t body = ix.body;
+#ifdef KAMD_STORE_SERVER
+  if (g_pb_schema && v.size() >= body + 4 && memcmp(v.data() + body, "k8s\0", 4) == 0) {
+    if (ix.json_rv != rv) {
+      ix.json.clear();
+      char rs[24];
+      snprintf(rs, sizeof rs, "%lld", (long long)rv);
+      pbc::JsonWriter w(*g_pb_schema);
+      if (!w.object((const uint8_t*)v.data() + body, v.size() - body, ix.json, rs)) ix.json = "{}";
+      ix.json_rv = rv;
+    }
+    return ix.json;
+  }
+#endif
+  (void)rv;
+  return std::string_view(v).substr(body);
+}
+
+static void chunk(std::string* out, const char* type, std::string_view obj) {
   // {"type":"X","object":<object JSON>}\n as one HTTP chunk
   static const char pre[] = "{\"type\":\"";
   static const char mid[] = "\",\"object\":";
-  size_t n = (sizeof pre - 1) + strlen(type) + (sizeof mid - 1) + (v.size() - body) + 2;
+  size_t n = (sizeof pre - 1) + strlen(type) + (sizeof mid - 1) + obj.size() + 2;
   char hex[24];
   int hl = snprintf(hex, sizeof hex, "%zx\r\n", n);
   out->append(hex, (size_t)hl);
   out->append(pre, sizeof pre - 1);
   out->append(type);
   out->append(mid, sizeof mid - 1);
-  out->append(v, body, std::string::npos);
+  out->append(obj.data(), obj.size());
   out->append("}\n\r\n", 4);
 }
 
@@ -874,7 +907,7 @@ class FanOut {
     if (w->send_initial) {
       for (const auto& kv : w->initial) {
         const Index& ix = index_of(*kv, slot_);
-        if (w->matches(ix)) chunk(&w->out, "ADDED", kv->value, ix.body);
+        if (w->matches(ix)) chunk(&w->out, "ADDED", object_json(kv->value, ix, kv->mod_rev));
       }
     }
     for (const Event& e : w->replay) fan_one(raw, e);
@@ -911,13 +944,13 @@ class FanOut {
     bool was = ev.prev && w->matches(*prv);
     const std::string& v = ev.kv->value;
     if (ev.type == 0) {
-      if (now && was) chunk(&w->out, "MODIFIED", v, cur->body);
-      else if (now) chunk(&w->out, "ADDED", v, cur->body);
-      else if (was) chunk(&w->out, "DELETED", v, cur->body);
+      if (now && was) chunk(&w->out, "MODIFIED", object_json(v, *cur, ev.rev));
+      else if (now) chunk(&w->out, "ADDED", object_json(v, *cur, ev.rev));
+      else if (was) chunk(&w->out, "DELETED", object_json(v, *cur, ev.rev));
       else return;
     } else {
       if (!(now || was) || !cur->ok) return;
-      chunk(&w->out, "DELETED", v, cur->body);
+      chunk(&w->out, "DELETED", object_json(v, *cur, ev.rev));
     }
     mark_fan(w);
   }
@@ -1566,7 +1599,14 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = val();
     else if (a == "--listen-handoff") handoff_path = val();
     else if (a == "--fan-threads") fan_threads = atoi(val());
-    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--listen-handoff PATH] [--wal FILE] [--history N] [--fan-threads N]\n"); return 2; }
+    else if (a == "--pb-schema") {
+      g_pb_schema = new pbc::Schema();
+      if (!g_pb_schema->load(val())) {
+        fprintf(stderr, "kamd-etcd: --pb-schema: %s\n", g_pb_schema->error.c_str());
+        return 2;
+      }
+    }
+    else { fprintf(stderr, "usage: kamd-etcd [--listen-unix PATH] [--listen-tcp PORT] [--listen-handoff PATH] [--wal FILE] [--history N] [--fan-threads N] [--pb-schema FILE]\n"); return 2; }
   }
   kamd::Engine eng(hist);
   if (wal && !eng.open_wal(wal)) { perror("wal"); return 1; }

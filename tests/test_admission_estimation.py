@@ -5,6 +5,7 @@ Parity: `plugin/pkg/admission/antiaffinity/admission_test.go`,
 annotation, explicit requests/limits untouched), `persistentvolume/label/admission_test.go`
 (on-prem: node-pinned volumes take their node's zone/region), `persistentvolumeclaim/pvcprotection`.
 """
+import json
 import time
 
 import pytest
@@ -75,10 +76,11 @@ def test_admission_plugins(run, tmp_path):
             # PersistentVolumeLabel: local PV pinned to a zoned node inherits zone/region
             await c.create("nodes", {"metadata": {"name": "gpu-0", "labels": {
                 "failure-domain.beta.kubernetes.io/zone": "rack-3", "failure-domain.beta.kubernetes.io/region": "dc-1"}}})
-            pv = await c.create("persistentvolumes", {"metadata": {"name": "nvme0"}, "spec": {
-                "capacity": {"storage": "100Gi"}, "accessModes": ["ReadWriteOnce"], "local": {"path": "/mnt/nvme0"},
-                "nodeAffinity": {"required": {"nodeSelectorTerms": [{"matchExpressions": [
-                    {"key": "kubernetes.io/hostname", "operator": "In", "values": ["gpu-0"]}]}]}}}})
+            aff = {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [{"matchExpressions": [
+                {"key": "kubernetes.io/hostname", "operator": "In", "values": ["gpu-0"]}]}]}}
+            pv = await c.create("persistentvolumes", {"metadata": {"name": "nvme0", "annotations": {
+                "volume.alpha.kubernetes.io/node-affinity": json.dumps(aff)}}, "spec": {
+                "capacity": {"storage": "100Gi"}, "accessModes": ["ReadWriteOnce"], "local": {"path": "/mnt/nvme0"}}})
             assert pv["metadata"]["labels"] == {"failure-domain.beta.kubernetes.io/zone": "rack-3",
                                                 "failure-domain.beta.kubernetes.io/region": "dc-1"}
 

@@ -57,9 +57,11 @@ def test_csi_attach_publish_end_to_end(run):
         await cl.start()
         c = cl.client
         try:
-            await c.create("persistentvolumes", {"metadata": {"name": "csi-pv"}, "spec": {
+            # 1.9's CSIPersistentVolumeSource has no volumeAttributes: they ride on an annotation
+            await c.create("persistentvolumes", {"metadata": {"name": "csi-pv", "annotations": {
+                "csi.volume.kubernetes.io/volume-attributes": '{"tier": "nvme"}'}}, "spec": {
                 "capacity": {"storage": "10Gi"}, "accessModes": ["ReadWriteOnce"], "storageClassName": "",
-                "csi": {"driver": driver, "volumeHandle": "dataset-7", "volumeAttributes": {"tier": "nvme"}}}})
+                "csi": {"driver": driver, "volumeHandle": "dataset-7"}}})
             await c.create("persistentvolumeclaims", {"metadata": {"name": "data"}, "spec": {
                 "accessModes": ["ReadWriteOnce"], "storageClassName": "", "resources": {"requests": {"storage": "1Gi"}}}},
                 "default")

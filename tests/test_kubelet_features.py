@@ -78,7 +78,7 @@ def test_readiness_and_liveness_probes(run):
     async def main():
         async with LocalCluster(nodes=1, gpus_per_node=0) as cl:
             c = cl.client
-            probe = {"exec": {"command": ["check"]}, "periodSeconds": 0.05, "failureThreshold": 1}
+            probe = {"exec": {"command": ["check"]}, "periodSeconds": 1, "failureThreshold": 1}
             await c.create("pods", {"metadata": {"name": "pr", "namespace": "default"},
                                     "spec": {"containers": [{"name": "c", "image": "x", "readinessProbe": probe,
                                                              "livenessProbe": dict(probe, failureThreshold=2)}]}})
@@ -86,7 +86,7 @@ def test_readiness_and_liveness_probes(run):
             uid = p["metadata"]["uid"]
 
             async def cond(pred):
-                for _ in range(200):
+                for _ in range(600):
                     p = await c.get("pods", "pr", "default")
                     if pred(p):
                         return p

@@ -7,6 +7,8 @@ from kubernetes_amd.apiserver.server import APIServer
 from kubernetes_amd.client.rest import Client
 from kubernetes_amd.utils.protodesc import build
 
+CORE = "k8s.io.api.core.v1."
+
 POD = {
     "apiVersion": "v1", "kind": "Pod",
     "metadata": {"name": "train-0", "namespace": "ml", "uid": "9b1c", "resourceVersion": "42", "generation": 1,
@@ -56,7 +58,7 @@ def test_deterministic_map_order():
 def test_envelope_fields():
     data = pb.encode_object(NODE)
     api, kind, raw = pb.decode_unknown(data)
-    assert (api, kind) == ("v1", "Node") and raw == pb.encode_message("Node", {k: v for k, v in NODE.items() if k not in ("kind", "apiVersion")})
+    assert (api, kind) == ("v1", "Node") and raw == pb.encode_message(CORE + "Node", {k: v for k, v in NODE.items() if k not in ("kind", "apiVersion")})
 
 
 def test_cross_check_against_google_protobuf():
@@ -72,7 +74,7 @@ def test_cross_check_against_google_protobuf():
     ref = M["ObjectReference"](kind="Node", name="mi355x-0")
     ref.extendedResourceBinding["z"].resources.extend(["g3"])
     ref.extendedResourceBinding["a"].resources.extend(["g0", "g1"])
-    ours = pb.encode_message("ObjectReference", {"kind": "Node", "name": "mi355x-0",
+    ours = pb.encode_message(CORE + "ObjectReference", {"kind": "Node", "name": "mi355x-0",
                                                  "extendedResourceBinding": {"z": {"resources": ["g3"]},
                                                                              "a": {"resources": ["g0", "g1"]}}})
     assert ref.SerializeToString(deterministic=True) == ours
@@ -81,7 +83,7 @@ def test_cross_check_against_google_protobuf():
     r.id, r.health = "GPU-0", "Healthy"
     r.attributes["amd.com/arch"] = "gfx950"
     r.attributes["amd.com/hbm"] = "288Gi"
-    ours = pb.encode_message("ExtendedResourceDomain", {"resources": {"GPU-0": {
+    ours = pb.encode_message(CORE + "ExtendedResourceDomain", {"resources": {"GPU-0": {
         "id": "GPU-0", "health": "Healthy", "attributes": {"amd.com/hbm": "288Gi", "amd.com/arch": "gfx950"}}}})
     assert dom.SerializeToString(deterministic=True) == ours
     # and google.protobuf parses ours

@@ -92,12 +92,15 @@ def _pvc(name, volume=None, cls=""):
 def _pv(name, labels=None, host=None, cls="", claim_ref=None):
     sp = {"capacity": {"storage": "10Gi"}, "accessModes": ["ReadWriteOnce"], "storageClassName": cls,
           "local": {"path": "/mnt/" + name}}
+    md = {"name": name, "labels": labels or {}}
     if host:
-        sp["nodeAffinity"] = {"required": {"nodeSelectorTerms": [{"matchExpressions": [
-            {"key": "kubernetes.io/hostname", "operator": "In", "values": [host]}]}]}}
+        # the 1.9 alpha node-affinity annotation (spec.nodeAffinity is 1.10+)
+        md["annotations"] = {"volume.alpha.kubernetes.io/node-affinity": json.dumps(
+            {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [{"matchExpressions": [
+                {"key": "kubernetes.io/hostname", "operator": "In", "values": [host]}]}]}})}
     if claim_ref:
         sp["claimRef"] = claim_ref
-    return {"metadata": {"name": name, "labels": labels or {}}, "spec": sp, "status": {"phase": "Available"}}
+    return {"metadata": md, "spec": sp, "status": {"phase": "Available"}}
 
 
 def test_volume_zone_conflict():
