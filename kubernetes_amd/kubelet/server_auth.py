@@ -14,9 +14,38 @@
 from __future__ import annotations
 
 import time
+from collections import OrderedDict
 
 ANONYMOUS = ("system:anonymous", ("system:unauthenticated",))
 VERBS = {"GET": "get", "HEAD": "get", "POST": "create", "PUT": "update", "PATCH": "patch", "DELETE": "delete"}
+
+
+class TTLCache:
+    """Size-bounded LRU with per-entry expiry (the reference's webhook caches are LRUs of 1024
+    entries for authn and 10000 for authz, `staging/src/k8s.io/apiserver/pkg/authentication/token/cache`)."""
+
+    def __init__(self, size):
+        self.size = size
+        self._d: OrderedDict = OrderedDict()
+
+    def get(self, key):
+        hit = self._d.get(key)
+        if hit is None:
+            return None
+        if hit[0] <= time.monotonic():
+            del self._d[key]
+            return None
+        self._d.move_to_end(key)
+        return hit
+
+    def put(self, key, ttl, value):
+        self._d[key] = (time.monotonic() + ttl, value)
+        self._d.move_to_end(key)
+        while len(self._d) > self.size:
+            self._d.popitem(last=False)
+
+    def __len__(self):
+        return len(self._d)
 
 
 def subresource_for(path: str) -> str:
@@ -28,15 +57,16 @@ def subresource_for(path: str) -> str:
 
 class KubeletAuth:
     def __init__(self, client, node_name, anonymous=True, token_webhook=False, authz_mode="AlwaysAllow",
-                 authn_ttl=120.0, authz_allowed_ttl=300.0, authz_denied_ttl=30.0):
+                 authn_ttl=120.0, authz_allowed_ttl=300.0, authz_denied_ttl=30.0, authn_cache_size=1024,
+                 authz_cache_size=10000):
         self.client = client
         self.node = node_name
         self.anonymous = anonymous
         self.token_webhook = token_webhook
         self.authz_mode = authz_mode
         self.authn_ttl, self.allowed_ttl, self.denied_ttl = authn_ttl, authz_allowed_ttl, authz_denied_ttl
-        self._tokens: dict[str, tuple] = {}     # token -> (expiry, (user, groups) or None)
-        self._decisions: dict[tuple, tuple] = {}
+        self._tokens = TTLCache(authn_cache_size)        # token -> (user, groups) or None
+        self._decisions = TTLCache(authz_cache_size)     # (user, groups, verb, subresource) -> bool
 
     async def authenticate(self, req):
         """-> (user, groups) or None (401)."""
@@ -50,7 +80,7 @@ class KubeletAuth:
         if auth.lower().startswith("bearer ") and self.token_webhook:
             tok = auth[7:].strip()
             hit = self._tokens.get(tok)
-            if hit is not None and hit[0] > time.monotonic():
+            if hit is not None:
                 return hit[1]
             review = await self.client.create("tokenreviews", {"apiVersion": "authentication.k8s.io/v1",
                                                                "kind": "TokenReview", "spec": {"token": tok}})
@@ -59,7 +89,7 @@ class KubeletAuth:
             if st.get("authenticated"):
                 u = st.get("user") or {}
                 who = (u.get("username", ""), tuple(u.get("groups") or ()))
-            self._tokens[tok] = (time.monotonic() + self.authn_ttl, who)
+            self._tokens.put(tok, self.authn_ttl, who)
             return who
         return ANONYMOUS if self.anonymous else None
 
@@ -70,14 +100,14 @@ class KubeletAuth:
         sub = subresource_for(req.path)
         key = (user, groups, verb, sub)
         hit = self._decisions.get(key)
-        if hit is not None and hit[0] > time.monotonic():
+        if hit is not None:
             return hit[1]
         sar = await self.client.create("subjectaccessreviews", {
             "apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview",
             "spec": {"user": user, "groups": list(groups),
                      "resourceAttributes": {"verb": verb, "resource": "nodes", "subresource": sub, "name": self.node}}})
         ok = bool((sar.get("status") or {}).get("allowed"))
-        self._decisions[key] = (time.monotonic() + (self.allowed_ttl if ok else self.denied_ttl), ok)
+        self._decisions.put(key, self.allowed_ttl if ok else self.denied_ttl, ok)
         return ok
 
     async def check(self, req):

@@ -104,3 +104,19 @@ def test_anonymous_auth_disabled(run, tmp_path):
             await s.stop()
     run(main())
     assert os.path.exists(tmp_path)
+
+
+def test_auth_caches_are_bounded_lru():
+    """Webhook caches evict least-recently-used entries past their size and drop expired ones
+    (the reference's authn/authz webhook caches are size-bounded LRUs)."""
+    import time as _t
+    from kubernetes_amd.kubelet.server_auth import TTLCache
+    c = TTLCache(3)
+    for i in range(3):
+        c.put(i, 60, i)
+    assert c.get(0) == c.get(0) and c.get(0)[1] == 0       # 0 becomes most recent
+    c.put(3, 60, 3)                                         # evicts 1 (least recent)
+    assert c.get(1) is None and c.get(2)[1] == 2 and c.get(3)[1] == 3 and len(c) == 3
+    c.put("short", 0.01, True)
+    _t.sleep(0.02)
+    assert c.get("short") is None and len(c) == 2          # expired entry dropped on read
