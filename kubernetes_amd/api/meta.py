@@ -115,6 +115,7 @@ RESOURCES = [
     ResourceInfo("authorization.k8s.io", "v1", "SelfSubjectAccessReview", "selfsubjectaccessreviews", False, ()),
     ResourceInfo("authorization.k8s.io", "v1", "LocalSubjectAccessReview", "localsubjectaccessreviews", True, ()),
 ]
+BUILTIN = tuple(RESOURCES)          # the compiled-in resources (RESOURCES also gains CRDs)
 
 VIRTUAL = {"tokenreviews", "subjectaccessreviews", "selfsubjectaccessreviews", "localsubjectaccessreviews"}
 

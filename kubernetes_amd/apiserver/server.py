@@ -45,6 +45,7 @@ from ..storage.mvcc import CompactedError, MVCCStore
 from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
+from ..utils.websocket import is_websocket_request
 from . import admission as adm
 from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, build_authorizer
 from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, event_bytes
@@ -1650,14 +1651,23 @@ class APIServer:
         return pod, addr, port
 
     async def _pod_stream(self, req, ns, name, sub):
-        """pods/exec, pods/attach (framed stream) and pods/portforward (Upgrade: tcp) proxied to
-        the node's kubelet (`pkg/registry/core/pod/rest/subresources.go` ExecREST/PortForwardREST)."""
+        """pods/exec, pods/attach and pods/portforward proxied to the node's kubelet: WebSocket
+        upgrades are relayed as-is (channel.k8s.io protocols), the framed stream / `Upgrade: tcp`
+        fallback is re-framed (`pkg/registry/core/pod/rest/subresources.go` ExecREST/PortForwardREST)."""
         from urllib.parse import parse_qs, urlencode
         pod, addr, port = await self._kubelet_of(ns, name)
         a = adm.Attributes(adm.CONNECT, "pods", sub, ns, name, None, pod, getattr(req, "user", None), "Pod")
         self._admit(a)
         self._validate_admission(a)
         q = parse_qs(req.qs or "")
+        if is_websocket_request(req.headers):
+            # UpgradeAwareHandler: relay the WebSocket upgrade to the kubelet and splice
+            from ..cri.remotecommand import upgrade_proxy_response
+            if sub == "portforward":
+                return upgrade_proxy_response(req, f"http://{addr}:{port}/portForward/{ns}/{name}?{req.qs}")
+            containers = (pod.get("spec") or {}).get("containers") or [{}]
+            cname = (q.get("container") or [containers[0].get("name", "")])[0]
+            return upgrade_proxy_response(req, f"http://{addr}:{port}/{sub}/{ns}/{name}/{cname}?{req.qs}")
         if sub == "portforward":
             pport = (q.get("port") or q.get("ports") or [""])[0]
             if not pport:

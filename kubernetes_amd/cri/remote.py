@@ -245,6 +245,11 @@ class RemoteRuntime(Runtime):
                                                          stdout=True, stderr=not tty))
         return r.url
 
+    async def attach_url(self, cid, tty=False, stdin=False):
+        r = await self._call("Attach", A.MSG["AttachRequest"](container_id=cid, tty=tty, stdin=stdin,
+                                                             stdout=True, stderr=not tty))
+        return r.url
+
     async def port_forward_url(self, sid, ports):
         r = await self._call("PortForward", A.MSG["PortForwardRequest"](pod_sandbox_id=sid, port=list(ports)))
         return r.url

@@ -9,7 +9,9 @@ server (`pkg/kubelet/server/streaming/server.go`: GetExec/GetAttach/GetPortForwa
 single-use token URLs), image service (`docker_image.go`), `Status` runtime/network
 conditions (`docker_service.go:Status`).
 
-Streaming protocol (replaces SPDY/WebSocket, which need client libraries this image lacks):
+Streaming protocols: WebSocket with the Kubernetes channel sub-protocols (`channel.k8s.io`,
+`v4.channel.k8s.io`, base64 variants; `cri/remotecommand.py`) on every token URL, and a framed
+fallback for clients without WebSocket:
   exec/attach  GET /exec/<token>  -> chunked body of frames: 1 byte stream id (1 stdout,
                2 stderr, 3 exit status as ASCII) + payload
   portforward  GET /portforward/<token>?port=N with `Connection: Upgrade`, `Upgrade: tcp`
@@ -30,6 +32,7 @@ import grpc
 
 from ..deviceplugin.api import generic_handler
 from ..kubelet.runtime.base import EXITED, RUNNING, RunContainerOptions
+from ..utils.websocket import is_websocket_request
 from . import api as A
 
 log = logging.getLogger("cri.server")
@@ -184,7 +187,14 @@ class StreamingServer:
                 writer.write(b"HTTP/1.1 404 Not Found\r\nContent-Length: 0\r\n\r\n")
                 return
             kind, req, _ = t
-            if kind in ("exec", "attach"):
+            headers = {}
+            for ln in head.decode("latin-1").split("\r\n")[1:]:
+                k, _, v = ln.partition(":")
+                if k:
+                    headers[k.strip().lower()] = v.strip()
+            if is_websocket_request(headers):
+                await self._websocket(kind, req, q, headers, reader, writer)
+            elif kind in ("exec", "attach"):
                 await self._exec(kind, req, writer)
             elif kind == "portforward":
                 await self._portforward(req, int(q.get("port") or (req.port[0] if req.port else 0)), reader, writer)
@@ -195,6 +205,31 @@ class StreamingServer:
                 writer.close()
             except Exception:
                 pass
+
+    async def _websocket(self, kind, req, q, headers, reader, writer):
+        """The Kubernetes WebSocket channel protocols on a token URL (`cri/remotecommand.py`);
+        stream options come from the CRI request the token was issued for."""
+        from . import remotecommand as rcm
+        if kind == "portforward":
+            ports = [int(p) for p in (q.get("ports") or q.get("port") or "").split(",") if p] or list(req.port)
+            conn = await rcm.accept_raw(reader, writer, headers, rcm.PORTFORWARD_PROTOCOLS)
+            if conn is not None:
+                await rcm.serve_portforward(conn, ports, lambda port: asyncio.open_connection("127.0.0.1", port))
+            return
+        conn = await rcm.accept_raw(reader, writer, headers, rcm.EXEC_PROTOCOLS)
+        if conn is None:
+            return
+        opts = rcm.Options(bool(req.stdin), bool(req.stdout), bool(req.stderr), bool(req.tty))
+        rt, cid = self.runtime, req.container_id
+        if kind == "exec":
+            cmd = list(req.cmd)
+
+            async def run(stdin, stdout, stderr, tty, resize):
+                return await rt.exec_interactive(cid, cmd, stdin, stdout, stderr, tty, resize)
+        else:
+            async def run(stdin, stdout, stderr, tty, resize):
+                return await rt.attach(cid, stdin, stdout, stderr, tty, resize)
+        await rcm.serve_exec(conn, opts, run)
 
     async def _exec(self, kind, req, writer):
         writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/vnd.kamd.stream\r\nTransfer-Encoding: chunked\r\n\r\n")

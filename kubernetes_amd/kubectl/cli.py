@@ -5,8 +5,9 @@ logs, label, annotate, patch, replace, scale, cordon, uncordon, drain, taint, to
 (status / history / undo), run, expose, version, api-versions, api-resources, cluster-info,
 config (view / use-context / set-cluster / set-context / get-contexts), explain, wait,
 auth can-i; kubeconfig loading (`staging/src/k8s.io/client-go/tools/clientcmd/loader.go:52`).
-Commands that need streaming sessions (exec / attach / port-forward / cp) report that the
-runtime does not support them.
+exec / attach / port-forward / cp speak the WebSocket channel protocols (`v4.channel.k8s.io`,
+stdin and tty with `-i` / `-t`; `client/remotecommand.py`) through the API server's pod
+subresources.
 
     python -m kubernetes_amd.kubectl get pods -o wide
 """
@@ -581,24 +582,90 @@ class Kubectl(extra.ExtraCommands):
     def _pod_path(self, name, sub):
         return f"/api/v1/namespaces/{self.ns}/pods/{name}/{sub}"
 
-    async def _exec(self, pod, container, command):
-        """pods/exec stream -> (exit code, stdout, stderr) (`pkg/kubectl/cmd/exec.go`)."""
+    def _stream_path(self, pod, sub, container, command=(), stdin=False, tty=False):
         from urllib.parse import urlencode
-        from ..cri.streaming import read_frames
         q = [("command", c) for c in command] + ([("container", container)] if container else [])
-        st, hdrs, r, w = await self.client.http.open_raw("POST", self._pod_path(pod, "exec") + "?" + urlencode(q))
+        q += [("stdin", "true")] if stdin else []
+        q += [("stdout", "true")] + ([("stderr", "true")] if not tty else []) + ([("tty", "true")] if tty else [])
+        return self._pod_path(pod, sub) + "?" + urlencode(q)
+
+    async def _exec(self, pod, container, command, stdin_data=None):
+        """pods/exec over WebSocket (`v4.channel.k8s.io`) -> (exit code, stdout, stderr)
+        (`pkg/kubectl/cmd/exec.go`)."""
+        from ..client.remotecommand import StreamError, exec_collect
         try:
-            if st != 200:
-                from ..client.http import _read_body
-                body = await _read_body(r, hdrs)
-                try:
-                    msg = json.loads(body).get("message", body.decode())
-                except ValueError:
-                    msg = body.decode(errors="replace")
-                raise SystemExit(f"error: unable to exec in pod {pod}: {msg}")
-            return await read_frames(r)
+            return await exec_collect(self.client.http, self._stream_path(pod, "exec", container, command,
+                                                                          stdin=stdin_data is not None), stdin_data)
+        except StreamError as e:
+            raise SystemExit(f"error: unable to exec in pod {pod}: {e.message}")
+
+    async def _interactive(self, pod, sub, container, command, stdin, tty):
+        """exec / attach with the local stdin (and a raw-mode terminal under -t, resized on SIGWINCH)."""
+        import signal
+        from ..client.remotecommand import StreamError, exec_stream
+        loop = asyncio.get_running_loop()
+        src = resize = None
+        restore = None
+        if stdin:
+            q: asyncio.Queue = asyncio.Queue()
+            fd = sys.stdin.fileno()
+
+            def pump():
+                while True:
+                    d = os.read(fd, 65536)
+                    loop.call_soon_threadsafe(q.put_nowait, d)
+                    if not d:
+                        return
+            loop.run_in_executor(None, pump)
+
+            async def src_gen():
+                while True:
+                    d = await q.get()
+                    if not d:
+                        return
+                    yield d
+            src = src_gen()
+            if tty and os.isatty(fd):
+                import termios
+                import tty as tty_mod
+                saved = termios.tcgetattr(fd)
+                tty_mod.setraw(fd)
+                restore = lambda: termios.tcsetattr(fd, termios.TCSADRAIN, saved)   # noqa: E731
+        if tty and os.isatty(1):
+            rq: asyncio.Queue = asyncio.Queue()
+
+            def winch(*_):
+                sz = os.get_terminal_size(1)
+                rq.put_nowait((sz.columns, sz.lines))
+            winch()
+            loop.add_signal_handler(signal.SIGWINCH, winch)
+
+            async def resize_gen():
+                while True:
+                    yield await rq.get()
+            resize = resize_gen()
+        out = self.out
+
+        def write_out(d):
+            if hasattr(out, "buffer"):
+                out.buffer.write(d)
+                out.flush()
+            else:
+                out.write(d.decode(errors="replace"))
+
+        def write_err(d):
+            sys.stderr.buffer.write(d)
+            sys.stderr.flush()
+        try:
+            return await exec_stream(self.client.http, self._stream_path(pod, sub, container, command, stdin, tty),
+                                     src, write_out, write_err, resize)
+        except StreamError as e:
+            raise SystemExit(f"error: unable to {'exec in' if sub == 'exec' else 'attach to'} pod {pod}: {e.message}")
         finally:
-            w.close()
+            if restore:
+                restore()
+            if resize is not None:
+                loop.remove_signal_handler(signal.SIGWINCH)
 
     async def cmd_exec(self):
         a = self.a
@@ -617,6 +684,9 @@ class Kubectl(extra.ExtraCommands):
             cmd = rest
         if not cmd:
             raise SystemExit("error: you must specify at least one command for the container")
+        if a.stdin or a.tty:
+            self.rc = await self._interactive(a.pod, "exec", container, cmd, a.stdin, a.tty)
+            return
         rc, out, err = await self._exec(a.pod, container, cmd)
         self.out.write(out.decode(errors="replace"))
         if err:
@@ -624,21 +694,14 @@ class Kubectl(extra.ExtraCommands):
         self.rc = rc
 
     async def cmd_attach(self):
-        from ..cri.streaming import read_frames
+        """`kubectl attach`: the container's output from now on, until it exits (with -i, stdin)."""
         a = self.a
-        path = self._pod_path(a.pod, "attach") + (f"?container={a.container}" if a.container else "")
-        st, hdrs, r, w = await self.client.http.open_raw("POST", path)
-        try:
-            if st != 200:
-                raise SystemExit(f"error: unable to attach to pod {a.pod}: HTTP {st}")
-            rc, out, _ = await read_frames(r)
-            self.out.write(out.decode(errors="replace"))
-        finally:
-            w.close()
+        self.rc = await self._interactive(a.pod, "attach", a.container, (), a.stdin, a.tty)
 
     async def cmd_port_forward(self):
-        """`kubectl port-forward POD [LOCAL:]REMOTE ...` (`pkg/kubectl/cmd/portforward.go`)."""
-        from ..cri.server import splice
+        """`kubectl port-forward POD [LOCAL:]REMOTE ...` (`pkg/kubectl/cmd/portforward.go`): one
+        WebSocket (`v4.channel.k8s.io`, data + error channel per port) per local connection."""
+        from ..client.remotecommand import StreamError, forward_connection
         a = self.a
         pod = a.pod.split("/", 1)[-1]
         servers, served = [], [0]
@@ -649,14 +712,12 @@ class Kubectl(extra.ExtraCommands):
 
             def handler(remote=remote):
                 async def h(reader, writer):
-                    st, _, ur, uw = await self.client.http.open_raw(
-                        "POST", self._pod_path(pod, "portforward") + f"?port={remote}",
-                        {"Connection": "Upgrade", "Upgrade": "tcp"})
-                    if st != 101:
+                    try:
+                        await forward_connection(self.client.http, self._pod_path(pod, "portforward") +
+                                                 f"?ports={remote}", remote, reader, writer)
+                    except (StreamError, ConnectionError) as e:
+                        print(f"error forwarding port {remote}: {e}", file=sys.stderr)
                         writer.close()
-                        uw.close()
-                        return
-                    await splice(reader, writer, ur, uw)
                     served[0] += 1
                     if a.max_connections and served[0] >= a.max_connections:
                         done.set()
@@ -907,6 +968,8 @@ def build_parser():
     at = add("attach")
     at.add_argument("pod")
     at.add_argument("-c", "--container")
+    at.add_argument("-i", "--stdin", action="store_true")
+    at.add_argument("-t", "--tty", action="store_true")
     pf = add("port-forward")
     pf.add_argument("pod")
     pf.add_argument("ports", nargs="+")

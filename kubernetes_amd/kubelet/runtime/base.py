@@ -8,6 +8,7 @@ manager, `pkg/kubelet/container/runtime.go`).
 """
 from __future__ import annotations
 
+import asyncio
 import time
 from dataclasses import dataclass, field
 
@@ -106,6 +107,33 @@ class Runtime:
     async def exec_sync(self, cid: str, cmd: list, timeout: float) -> tuple:
         """CRI ExecSync: run cmd in the container's context; returns (exit code, output bytes)."""
         raise NotImplementedError(f"{self.name} runtime does not support exec")
+
+    async def exec_interactive(self, cid: str, cmd: list, stdin, stdout, stderr, tty: bool, resize) -> int:
+        """Streaming exec (`ExecInContainer`, `pkg/kubelet/server/remotecommand/exec.go:33`):
+        stdin / resize are async iterators of bytes / (width, height) or None; stdout / stderr
+        async callables or None. This default runs the command to completion through exec_sync
+        (no stdin) and sends its combined output at the end; runtimes with real processes
+        stream."""
+        rc, out = await self.exec_sync(cid, cmd, 300)
+        sink = stdout or stderr
+        if sink is not None and out:
+            await sink(out if isinstance(out, bytes) else str(out).encode())
+        return rc
+
+    async def attach(self, cid: str, stdin, stdout, stderr, tty: bool, resize) -> int:
+        """Attach to a running container (`pkg/kubelet/server/remotecommand/attach.go`): the
+        output it writes from now on, until it exits. This default follows container_logs."""
+        sent = len(await self.container_logs(cid))
+        sink = stdout or stderr
+        while True:
+            st = self.container_status(cid)
+            data = await self.container_logs(cid)
+            if sink is not None and len(data) > sent:
+                await sink(data[sent:])
+            sent = max(sent, len(data))
+            if st is None or st.state != RUNNING:
+                return 0 if st is None else int(st.exit_code or 0)
+            await asyncio.sleep(0.1)
 
     def list_containers(self):
         return []

@@ -161,6 +161,12 @@ class HookedRuntime(Runtime):
     async def exec_sync(self, cid, cmd, timeout):
         return await self._rt(cid).exec_sync(cid, cmd, timeout)
 
+    async def exec_interactive(self, cid, cmd, stdin, stdout, stderr, tty, resize):
+        return await self._rt(cid).exec_interactive(cid, cmd, stdin, stdout, stderr, tty, resize)
+
+    async def attach(self, cid, stdin, stdout, stderr, tty, resize):
+        return await self._rt(cid).attach(cid, stdin, stdout, stderr, tty, resize)
+
     def list_containers(self):
         return [c for rt in self.runtimes.values() for c in rt.list_containers()]
 

@@ -606,12 +606,7 @@ class ProcessRuntime(Runtime):
         st = self.containers.get(cid)
         if m is None or st is None or st.state != RUNNING:
             return 126, b"container is not running"
-        argv, cwd = list(cmd), m["cwd"]
-        if m.get("init_pid"):
-            # into the container's namespaces (its /dev view, pid namespace) as its user
-            argv = [KAMD_RUNC, "exec", "--pid", str(m["init_pid"]), "--cwd", cwd or "/"] + \
-                (["--user", m["user"]] if m.get("user") else []) + ["--"] + argv
-            cwd = None
+        argv, cwd = self._exec_argv(m, cmd)
         try:
             proc = await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=cwd, stdout=asyncio.subprocess.PIPE,
                                                         stderr=asyncio.subprocess.STDOUT, start_new_session=True)
@@ -627,6 +622,163 @@ class ProcessRuntime(Runtime):
             await proc.wait()
             return 124, b"timeout"
         return proc.returncode, out
+
+    @staticmethod
+    def _exec_argv(m, cmd):
+        argv, cwd = list(cmd), m["cwd"]
+        if m.get("init_pid"):
+            # into the container's namespaces (its /dev view, pid namespace) as its user
+            argv = [KAMD_RUNC, "exec", "--pid", str(m["init_pid"]), "--cwd", cwd or "/"] + \
+                (["--user", m["user"]] if m.get("user") else []) + ["--"] + argv
+            cwd = None
+        return argv, cwd
+
+    async def exec_interactive(self, cid, cmd, stdin, stdout, stderr, tty, resize):
+        """A streamed exec: pipes, or a pseudo-terminal (controlling tty of the new session,
+        resized by TIOCSWINSZ) when tty is set."""
+        m = self.meta.get(cid)
+        st = self.containers.get(cid)
+        if m is None or st is None or st.state != RUNNING:
+            raise OSError(f"container {cid} is not running")
+        argv, cwd = self._exec_argv(m, cmd)
+        if tty:
+            return await self._exec_tty(argv, cwd, m["env"], stdin, stdout or stderr, resize)
+        pipe, null = asyncio.subprocess.PIPE, asyncio.subprocess.DEVNULL
+        proc = await asyncio.create_subprocess_exec(
+            *argv, env=m["env"], cwd=cwd, stdin=pipe if stdin is not None else null,
+            stdout=pipe if stdout is not None else null, stderr=pipe if stderr is not None else null,
+            start_new_session=True)
+
+        async def pump_out(stream, sink):
+            while True:
+                d = await stream.read(65536)
+                if not d:
+                    return
+                await sink(d)
+
+        async def pump_in():
+            try:
+                async for d in stdin:
+                    proc.stdin.write(d)
+                    await proc.stdin.drain()
+            except (ConnectionError, BrokenPipeError):
+                pass
+            finally:
+                proc.stdin.close()
+        tasks = [asyncio.ensure_future(pump_in())] if stdin is not None else []
+        outs = [pump_out(s, k) for s, k in ((proc.stdout, stdout), (proc.stderr, stderr)) if k is not None]
+        try:
+            await asyncio.gather(*outs)
+            return await proc.wait()
+        finally:
+            for t in tasks:
+                t.cancel()
+            if proc.returncode is None:
+                try:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                await proc.wait()
+
+    async def _exec_tty(self, argv, cwd, env, stdin, sink, resize):
+        import fcntl
+        import pty
+        import struct
+        import termios
+        master, slave = pty.openpty()
+
+        def ctty():
+            fcntl.ioctl(0, termios.TIOCSCTTY, 0)
+        try:
+            proc = await asyncio.create_subprocess_exec(*argv, env=env, cwd=cwd, stdin=slave, stdout=slave,
+                                                        stderr=slave, start_new_session=True, preexec_fn=ctty)
+        finally:
+            os.close(slave)
+        loop = asyncio.get_running_loop()
+        os.set_blocking(master, False)
+        done = loop.create_future()
+        chunks: asyncio.Queue = asyncio.Queue()
+
+        def readable():
+            try:
+                d = os.read(master, 65536)
+            except BlockingIOError:
+                return
+            except OSError:          # EIO: every slave end is closed (the session ended)
+                d = b""
+            if not d:
+                loop.remove_reader(master)
+                if not done.done():
+                    done.set_result(None)
+            chunks.put_nowait(d)
+        loop.add_reader(master, readable)
+
+        async def pump_out():
+            while True:
+                d = await chunks.get()
+                if not d:
+                    return
+                if sink is not None:
+                    await sink(d)
+
+        async def pump_in():
+            async for d in stdin:
+                while d:
+                    try:
+                        n = os.write(master, d)
+                    except BlockingIOError:
+                        await asyncio.sleep(0.01)
+                        continue
+                    d = d[n:]
+
+        async def pump_resize():
+            async for w, h in resize:
+                fcntl.ioctl(master, termios.TIOCSWINSZ, struct.pack("HHHH", h, w, 0, 0))
+        tasks = []
+        if stdin is not None:
+            tasks.append(asyncio.ensure_future(pump_in()))
+        if resize is not None:
+            tasks.append(asyncio.ensure_future(pump_resize()))
+        out_task = asyncio.ensure_future(pump_out())
+        tasks.append(out_task)
+        try:
+            rc = await proc.wait()
+            # the rest of the output: until EIO, or briefly if a background child keeps the tty
+            await asyncio.wait([out_task], timeout=2.0)
+            return rc
+        finally:
+            for t in tasks:
+                t.cancel()
+            loop.remove_reader(master)
+            os.close(master)
+            if proc.returncode is None:
+                try:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                await proc.wait()
+
+    async def attach(self, cid, stdin, stdout, stderr, tty, resize):
+        """Follow the container's output file from its current end until the container exits."""
+        st = self.containers.get(cid)
+        if st is None:
+            raise OSError(f"container {cid} not found")
+        sink = stdout or stderr
+        pos = os.path.getsize(st.log_path) if os.path.exists(st.log_path) else 0
+        while True:
+            st = self.containers.get(cid)
+            running = st is not None and st.state == RUNNING
+            if st is not None and os.path.exists(st.log_path):
+                with open(st.log_path, "rb") as f:
+                    f.seek(pos)
+                    data = f.read()
+                if data:
+                    pos += len(data)
+                    if sink is not None:
+                        await sink(data)
+            if not running:
+                return 0 if st is None else int(st.exit_code or 0)
+            await asyncio.sleep(0.05)
 
     def list_containers(self):
         return list(self.containers.values())

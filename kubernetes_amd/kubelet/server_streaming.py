@@ -4,16 +4,26 @@ Parity: `pkg/kubelet/server/server.go:303-360` (routes `/run/{ns}/{pod}/{contain
 `/exec/{ns}/{pod}/{container}`, `/attach/...`, `/portForward/{ns}/{pod}`, with optional `{uid}`)
 and `getExec`/`getPortForward` (`:600-700`): with a CRI runtime the kubelet obtains a streaming
 URL from the runtime (`Exec`/`PortForward` RPCs) and proxies it; for the in-process runtimes it
-serves the stream itself. Exec streams use the framed protocol of `cri/server.py`; stdin is
-not supported (non-interactive exec, like `kubectl exec` without `-i`).
+serves the stream itself.
+
+Two wire protocols:
+  * WebSocket (`Upgrade: websocket`): the Kubernetes channel protocols `channel.k8s.io`,
+    `base64.channel.k8s.io`, `v4.channel.k8s.io`, `v4.base64.channel.k8s.io` (+ `v5`) for
+    exec/attach with stdin, tty and resize, and the per-port channel pairs of port-forward
+    (`cri/remotecommand.py`); with a CRI runtime the upgrade is relayed to the runtime's
+    streaming server;
+  * the framed fallback of `cri/server.py` (chunked frames for exec, `Upgrade: tcp` tunnel for
+    port-forward) for clients that do not speak WebSocket.
 """
 from __future__ import annotations
 
 import asyncio
 from urllib.parse import parse_qs
 
+from ..cri import remotecommand as rc_
 from ..cri.server import splice
 from ..utils.httpserver import Response, StreamResponse, UpgradeResponse
+from ..utils.websocket import is_websocket_request
 
 
 def _frames(rc, out):
@@ -51,6 +61,8 @@ async def handle(kubelet, req):
         return None
     parts = [x for x in p.split("/")[2:] if x]
     rt = kubelet.runtime
+    if verb != "run" and is_websocket_request(req.headers):
+        return await _websocket(kubelet, rt, req, verb, parts)
     if verb in ("exec", "run", "attach"):
         st, cid, err = _find(kubelet, parts)
         if err:
@@ -95,6 +107,43 @@ async def handle(kubelet, req):
             return
         await splice(reader, writer, ur, uw)
     return UpgradeResponse(run_local)
+
+
+async def _websocket(kubelet, rt, req, verb, parts):
+    if verb == "portForward":
+        st, _, err = _find(kubelet, parts, with_container=False)
+        if err:
+            return Response(404, err.encode(), "text/plain")
+        if hasattr(rt, "port_forward_url"):
+            try:
+                ports = rc_.ports_from_query(req.qs)
+            except ValueError as e:
+                return Response(400, str(e).encode(), "text/plain")
+            return rc_.upgrade_proxy_response(req, await rt.port_forward_url(st.sandbox, ports))
+        # in-process runtimes: pods share the host network namespace
+        return rc_.portforward_response(req, lambda port: asyncio.open_connection("127.0.0.1", port))
+    st, cid, err = _find(kubelet, parts)
+    if err:
+        return Response(404, err.encode(), "text/plain")
+    q = parse_qs(req.qs or "")
+    cmd = q.get("command") or q.get("cmd") or []
+    if verb == "exec" and not cmd:
+        return Response(400, b"command is required", "text/plain")
+    try:
+        opts = rc_.options_from_query(req.qs)
+    except ValueError as e:
+        return Response(400, str(e).encode(), "text/plain")
+    if hasattr(rt, "exec_url"):
+        url = (await rt.exec_url(cid, cmd, tty=opts.tty, stdin=opts.stdin) if verb == "exec" else
+               await rt.attach_url(cid, tty=opts.tty, stdin=opts.stdin))
+        return rc_.upgrade_proxy_response(req, url)
+    if verb == "exec":
+        async def run(stdin, stdout, stderr, tty, resize):
+            return await rt.exec_interactive(cid, cmd, stdin, stdout, stderr, tty, resize)
+    else:
+        async def run(stdin, stdout, stderr, tty, resize):
+            return await rt.attach(cid, stdin, stdout, stderr, tty, resize)
+    return rc_.exec_response(req, req.qs, run)
 
 
 def _static(raw):

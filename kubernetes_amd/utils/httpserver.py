@@ -67,13 +67,16 @@ class StreamResponse:
 class UpgradeResponse:
     """Returned by a handler that switches the connection to another protocol
     (`Connection: Upgrade`): `101 Switching Protocols` is sent, then `run(reader, writer)` owns
-    the raw byte stream (stream-style reader/writer over the same transport)."""
+    the raw byte stream (stream-style reader/writer over the same transport). `headers` are
+    added to the 101 reply (WebSocket accept key / sub-protocol); `protocol=None` writes no reply
+    at all — `run` owns the whole response (an upgrade-aware proxy relays the backend's)."""
 
-    __slots__ = ("run", "protocol")
+    __slots__ = ("run", "protocol", "headers")
 
-    def __init__(self, run, protocol="tcp"):
+    def __init__(self, run, protocol="tcp", headers=None):
         self.run = run
         self.protocol = protocol
+        self.headers = headers
 
 
 class HandoffResponse:
@@ -259,13 +262,14 @@ class _Conn(asyncio.Protocol):
         finally:
             self.busy = False
 
-
     async def _upgrade(self, resp):
         loop = asyncio.get_running_loop()
         reader = asyncio.StreamReader(loop=loop)
         proto = asyncio.StreamReaderProtocol(reader, loop=loop)
-        self.transport.write(("HTTP/1.1 101 Switching Protocols\r\nConnection: Upgrade\r\nUpgrade: %s\r\n\r\n"
-                              % resp.protocol).encode())
+        if resp.protocol is not None:
+            extra = "".join("%s: %s\r\n" % kv for kv in (resp.headers or {}).items())
+            self.transport.write(("HTTP/1.1 101 Switching Protocols\r\nConnection: Upgrade\r\nUpgrade: %s\r\n%s\r\n"
+                                  % (resp.protocol, extra)).encode())
         rest = bytes(self.buf)
         self.buf.clear()
         self.transport.set_protocol(proto)

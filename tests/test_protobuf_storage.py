@@ -10,7 +10,7 @@ import re
 import pytest
 
 from kubernetes_amd.api import protobuf as pb
-from kubernetes_amd.api.meta import BY_KIND, RESOURCES
+from kubernetes_amd.api.meta import BUILTIN, BY_KIND
 from kubernetes_amd.apiserver.server import APIServer, pb_to_json
 from kubernetes_amd.client.rest import APIStatusError, Client
 from kubernetes_amd.native import pbcodec
@@ -26,7 +26,7 @@ NOT_IN_1_9 = {("coordination.k8s.io/v1", "Lease")}
 
 def test_every_served_kind_has_a_message():
     s = pb.schema()
-    missing = {(r.group_version, r.kind) for r in RESOURCES if s.message_for(r.group_version, r.kind) is None}
+    missing = {(r.group_version, r.kind) for r in BUILTIN if s.message_for(r.group_version, r.kind) is None}
     assert missing == NOT_IN_1_9
 
 

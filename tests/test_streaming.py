@@ -31,7 +31,7 @@ ECHO = ("import socket,sys\n"
         "s=socket.socket(); s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)\n"
         "s.bind(('127.0.0.1', int(sys.argv[1]))); s.listen(8); print('listening', flush=True)\n"
         "while True:\n"
-        "    c,_=s.accept(); d=c.recv(100); c.sendall(b'pong:'+d); c.close()\n")
+        "    c,_=s.accept(); d=c.recv(100); c.sendall(b'pong:'+d); c.close(); print('served', d.decode(), flush=True)\n")
 
 
 def kubectl(url, *argv):
@@ -86,7 +86,7 @@ def test_exec_portforward_cp_inprocess(run, tmp_path):
         cl = LocalCluster(nodes=1, gpus_per_node=0, runtime="process", kubelet_http=True, workdir=str(tmp_path / "c"))
         await cl.start()
         try:
-            await _scenario(cl)
+            port = await _scenario(cl)
             # cp both ways
             src = tmp_path / "local.txt"
             src.write_bytes(b"payload \x00\x01 'quoted'\n")
@@ -98,11 +98,22 @@ def test_exec_portforward_cp_inprocess(run, tmp_path):
             await k.cmd_cp()
             await k.client.close()
             assert (tmp_path / "back.bin").read_bytes() == src.read_bytes()
-            # attach returns the container output
+            # attach streams what the running container writes from now on
             k, out = kubectl(cl.url, "attach", "srv")
-            await k.cmd_attach()
+            task = asyncio.ensure_future(k.cmd_attach())
+            await asyncio.sleep(0.5)
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            w.write(b"live")
+            await w.drain()
+            assert await asyncio.wait_for(r.read(100), 10) == b"pong:live"
+            w.close()
+            for _ in range(200):
+                if "served live" in out.getvalue():
+                    break
+                await asyncio.sleep(0.02)
+            assert "served live" in out.getvalue() and "listening" not in out.getvalue()
+            task.cancel()
             await k.client.close()
-            assert "listening" in out.getvalue()
         finally:
             await cl.stop()
     run(main(), timeout=90)
@@ -111,7 +122,8 @@ def test_exec_portforward_cp_inprocess(run, tmp_path):
 def test_exec_portforward_over_cri(run, tmp_path):
     async def main():
         sock = str(tmp_path / "cri.sock")
-        srv = await CRIServer(ProcessRuntime(str(tmp_path / "rt")), sock).start()
+        prt = ProcessRuntime(str(tmp_path / "rt"))
+        srv = await CRIServer(prt, sock).start()
         rt = await RemoteRuntime(sock, relist_period=0.1).connect()
         cl = LocalCluster(nodes=0, gpus_per_node=0, kubelet_http=True, workdir=str(tmp_path / "c"))
         await cl.start()
@@ -122,6 +134,7 @@ def test_exec_portforward_over_cri(run, tmp_path):
             await cl.stop()
             await rt.close()
             await srv.stop()
+            await prt.kill_all()     # containers outlive a CRI server stop by design
     run(main(), timeout=90)
 
 
