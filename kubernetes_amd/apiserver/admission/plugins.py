@@ -99,7 +99,7 @@ class ServiceAccount(Plugin):
 class DefaultTolerationSeconds(Plugin):
     name = "DefaultTolerationSeconds"
     operations = (CREATE,)
-    KEYS = ("node.alpha.kubernetes.io/notReady", "node.alpha.kubernetes.io/unreachable")
+    KEYS = ("node.kubernetes.io/not-ready", "node.kubernetes.io/unreachable")
 
     def admit(self, a):
         if a.resource != "pods" or a.subresource:

@@ -20,6 +20,18 @@ def main(argv=None):
     ap.add_argument("--controllers", default="*", help=f"comma list; '*' = all of {sorted(CONTROLLERS)}, '-name' disables")
     ap.add_argument("--node-monitor-grace-period", type=float, default=40.0)
     ap.add_argument("--pod-eviction-timeout", type=float, default=300.0)
+    ap.add_argument("--node-monitor-period", type=float, default=5.0)
+    ap.add_argument("--node-startup-grace-period", type=float, default=60.0)
+    ap.add_argument("--node-eviction-rate", type=float, default=0.1,
+                    help="nodes per second whose pods are deleted on node failure in a healthy zone")
+    ap.add_argument("--secondary-node-eviction-rate", type=float, default=0.01,
+                    help="the rate in an unhealthy zone (0 below --large-cluster-size-threshold)")
+    ap.add_argument("--large-cluster-size-threshold", type=int, default=50)
+    ap.add_argument("--unhealthy-zone-threshold", type=float, default=0.55,
+                    help="fraction of not-Ready nodes (at least 3) that makes a zone unhealthy")
+    ap.add_argument("--enable-taint-manager", default="true", choices=("true", "false"),
+                    help="evict pods from nodes with NoExecute taints they do not tolerate")
+    ap.add_argument("--feature-gates", default="", help="e.g. TaintBasedEvictions=true,TaintNodesByCondition=true")
     ap.add_argument("--terminated-pod-gc-threshold", type=int, default=12500)
     ap.add_argument("--leader-elect", action="store_true")
     ap.add_argument("--allocate-node-cidrs", action="store_true")
@@ -36,6 +48,8 @@ def main(argv=None):
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
+    from ..utils.features import DefaultFeatureGate
+    DefaultFeatureGate.set(a.feature_gates)
 
     async def start():
         if a.kubeconfig:
@@ -46,7 +60,13 @@ def main(argv=None):
         if a.leader_elect:
             from ..client.leaderelection import LeaderElector
             await LeaderElector(client, "kube-system", "kube-controller-manager").acquire()
-        opts = {"nodelifecycle": {"grace": a.node_monitor_grace_period, "pod_eviction_timeout": a.pod_eviction_timeout},
+        opts = {"nodelifecycle": {"grace": a.node_monitor_grace_period, "pod_eviction_timeout": a.pod_eviction_timeout,
+                                  "monitor_period": a.node_monitor_period, "startup_grace": a.node_startup_grace_period,
+                                  "eviction_rate": a.node_eviction_rate,
+                                  "secondary_eviction_rate": a.secondary_node_eviction_rate,
+                                  "large_cluster_threshold": a.large_cluster_size_threshold,
+                                  "unhealthy_zone_threshold": a.unhealthy_zone_threshold,
+                                  "taint_manager": a.enable_taint_manager == "true"},
                 "podgc": {"terminated_pod_gc_threshold": a.terminated_pod_gc_threshold},
                 "serviceaccount-token": {"private_key_file": a.service_account_private_key_file, "root_ca_file": a.root_ca_file},
                 "csrsigning": {"cert_file": a.cluster_signing_cert_file, "key_file": a.cluster_signing_key_file},

@@ -28,8 +28,8 @@ from .base import Controller, controller_ref, pod_from_template, pod_is_active, 
 HOSTNAME = "kubernetes.io/hostname"
 
 DS_TOLERATIONS = [
-    {"key": "node.alpha.kubernetes.io/notReady", "operator": "Exists", "effect": "NoExecute"},
-    {"key": "node.alpha.kubernetes.io/unreachable", "operator": "Exists", "effect": "NoExecute"},
+    {"key": "node.kubernetes.io/not-ready", "operator": "Exists", "effect": "NoExecute"},
+    {"key": "node.kubernetes.io/unreachable", "operator": "Exists", "effect": "NoExecute"},
     {"key": "node.kubernetes.io/unschedulable", "operator": "Exists", "effect": "NoSchedule"},
 ]
 

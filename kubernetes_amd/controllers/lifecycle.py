@@ -9,10 +9,8 @@ Parity:
     `foregroundDeletion` deletes dependents first, then releases the owner.
   * PodGC — `pkg/controller/podgc/gc_controller.go`: terminated pods above
     `terminated_pod_gc_threshold` (oldest first) and pods bound to nodes that no longer exist.
-  * NodeLifecycle — `pkg/controller/node/node_controller.go:420-916`: a node whose kubelet has
-    not posted status for `grace` seconds gets Ready=Unknown plus the `unreachable` NoExecute
-    taint; after `pod_eviction_timeout` its pods are evicted (deleted) unless they tolerate the
-    taint longer (`tolerationSeconds`). GPU pods evicted here free their device IDs.
+  (Node lifecycle — health, zones, rate-limited evictions, taint manager — is in
+  `nodelifecycle.py`.)
 """
 from __future__ import annotations
 
@@ -23,10 +21,6 @@ from ..api import core, meta as m
 from ..api.meta import now_rfc3339
 from ..client.rest import APIStatusError, is_conflict, is_not_found
 from .base import Controller, split_key
-
-UNREACHABLE_TAINT = "node.alpha.kubernetes.io/unreachable"
-NOT_READY_TAINT = "node.alpha.kubernetes.io/notReady"
-
 
 class NamespaceController(Controller):
     name = "namespace"
@@ -239,91 +233,4 @@ class PodGCController(Controller):
                 raise
 
 
-class NodeLifecycleController(Controller):
-    name = "nodelifecycle"
-    workers = 2
-
-    def __init__(self, client, factory, recorder=None, monitor_period=5.0, grace=40.0, pod_eviction_timeout=300.0):
-        super().__init__(client, factory, recorder)
-        self.monitor_period = monitor_period
-        self.grace = grace
-        self.eviction_timeout = pod_eviction_timeout
-        self._tick = None
-        self.observed: dict[str, tuple] = {}   # node -> (heartbeat string, local time it changed)
-
-    def setup(self):
-        self.node_inf = self.factory.get("nodes")
-        self.pod_inf = self.factory.get("pods")
-        if "nodeName" not in self.pod_inf.store.indexers:
-            self.pod_inf.store.add_indexer("nodeName", lambda p: [(p.get("spec") or {}).get("nodeName", "")])
-
-    def start(self):
-        super().start()
-        self._tick = asyncio.ensure_future(self._ticker())
-
-    def stop(self):
-        super().stop()
-        if self._tick:
-            self._tick.cancel()
-
-    async def _ticker(self):
-        while True:
-            await asyncio.sleep(self.monitor_period)
-            for n in self.node_inf.list():
-                self.enqueue(n["metadata"]["name"])
-
-    async def sync(self, key, now=None):
-        node = self.node_inf.get(key)
-        if node is None:
-            self.observed.pop(key, None)
-            return
-        now = now or time.monotonic()
-        ready = core.get_condition(node.get("status"), "Ready")
-        hb = (ready or {}).get("lastHeartbeatTime", "")
-        prev = self.observed.get(key)
-        if prev is None or prev[0] != hb:
-            self.observed[key] = (hb, now)
-            prev = self.observed[key]
-        stale = now - prev[1] > self.grace
-        taints = list((node.get("spec") or {}).get("taints") or [])
-        has_taint = any(t.get("key") == UNREACHABLE_TAINT for t in taints)
-        if stale:
-            if ready is None or ready.get("status") != "Unknown":
-                conds = []
-                for c in (node.get("status") or {}).get("conditions") or ():
-                    c = dict(c)
-                    c["status"] = "Unknown"
-                    c["reason"] = "NodeStatusUnknown"
-                    c["message"] = "Kubelet stopped posting node status."
-                    c["lastTransitionTime"] = now_rfc3339()
-                    conds.append(c)
-                await self._patch_status(key, conds)
-                self.recorder.event(node, "Normal", "NodeNotReady", f"Node {key} status is now: NodeNotReady")
-            if not has_taint:
-                taints.append({"key": UNREACHABLE_TAINT, "effect": "NoExecute", "timeAdded": now_rfc3339()})
-                await self.client.patch("nodes", key, {"spec": {"taints": taints}})
-            # evict pods that do not tolerate the taint past their tolerationSeconds
-            taint = {"key": UNREACHABLE_TAINT, "effect": "NoExecute"}
-            for p in self.pod_inf.store.by_index("nodeName", key):
-                if core.pod_is_terminal(p) or p["metadata"].get("deletionTimestamp"):
-                    continue
-                tol = [t for t in (p.get("spec") or {}).get("tolerations") or () if core.tolerates([t], taint)]
-                limit = self.eviction_timeout if not tol else min(
-                    (t.get("tolerationSeconds") if t.get("tolerationSeconds") is not None else float("inf")) for t in tol)
-                if now - prev[1] - self.grace >= limit:
-                    try:
-                        await self.client.delete("pods", p["metadata"]["name"], p["metadata"]["namespace"])
-                        self.recorder.event(p, "Normal", "TaintManagerEviction", f"Marking for deletion Pod {m.ns_name(p)}")
-                    except APIStatusError as e:
-                        if not is_not_found(e):
-                            raise
-        elif has_taint and ready is not None and ready.get("status") == "True":
-            taints = [t for t in taints if t.get("key") != UNREACHABLE_TAINT]
-            await self.client.patch("nodes", key, {"spec": {"taints": taints or None}})
-
-    async def _patch_status(self, name, conds):
-        try:
-            await self.client.patch("nodes", name, {"status": {"conditions": conds}}, None, "merge", "status")
-        except APIStatusError as e:
-            if not is_not_found(e):
-                raise
+from .nodelifecycle import NodeLifecycleController  # noqa: E402,F401  (re-export)

@@ -21,7 +21,8 @@ DEFAULTS = {
     "XGMITopologyAwareAllocation": FeatureSpec(True, BETA),
     "EventDrivenKubelet": FeatureSpec(True, BETA),         # watch/exit-event driven pod sync
     "PodPriority": FeatureSpec(False, ALPHA),
-    "TaintBasedEvictions": FeatureSpec(True, BETA),
+    "TaintBasedEvictions": FeatureSpec(False, ALPHA),     # node controller taints instead of deleting
+    "TaintNodesByCondition": FeatureSpec(False, ALPHA),   # NoSchedule taints mirror node conditions
     "ExpandPersistentVolumes": FeatureSpec(False, ALPHA),
     "CPUManager": FeatureSpec(True, BETA),
     "HugePages": FeatureSpec(True, BETA),

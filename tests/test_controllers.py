@@ -167,11 +167,12 @@ def test_namespace_deletion_cascades(run):
 
 def test_node_lifecycle_evicts_gpu_pods(run):
     async def main():
-        opts = {"nodelifecycle": {"monitor_period": 0.05, "grace": 0.3, "pod_eviction_timeout": 0.2}}
+        opts = {"nodelifecycle": {"monitor_period": 0.05, "grace": 0.3, "pod_eviction_timeout": 0.2,
+                                  "taint_based_evictions": True, "eviction_rate": 100}}
         async with LocalCluster(nodes=2, gpus_per_node=2, controllers=["nodelifecycle"], controller_options=opts) as cl:
             c = cl.client
             p = {"metadata": {"name": "g", "namespace": "default"},
-                 "spec": {"tolerations": [{"key": "node.alpha.kubernetes.io/unreachable", "operator": "Exists",
+                 "spec": {"tolerations": [{"key": "node.kubernetes.io/unreachable", "operator": "Exists",
                                            "effect": "NoExecute", "tolerationSeconds": 0}],
                           "containers": [{"name": "c", "image": "x", "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
             await c.create("pods", p)
@@ -185,7 +186,7 @@ def test_node_lifecycle_evicts_gpu_pods(run):
             async def unknown():
                 n = await c.get("nodes", victim)
                 r = core.get_condition(n["status"], "Ready")
-                tainted = any(t["key"] == "node.alpha.kubernetes.io/unreachable" for t in n["spec"].get("taints") or [])
+                tainted = any(t["key"] == "node.kubernetes.io/unreachable" for t in n["spec"].get("taints") or [])
                 return r["status"] == "Unknown" and tainted
             await cl.wait_for(unknown, timeout=20)
 

@@ -98,7 +98,7 @@ POD = {
                                                                  "values": ["gfx950"]}]}}]},
                      "podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
                          {"labelSelector": {"matchLabels": {"app": "x"}}, "topologyKey": "kubernetes.io/hostname"}]}},
-        "tolerations": [{"key": "node.alpha.kubernetes.io/unreachable", "operator": "Exists",
+        "tolerations": [{"key": "node.kubernetes.io/unreachable", "operator": "Exists",
                          "effect": "NoExecute", "tolerationSeconds": 30}],
         "securityContext": {"fsGroup": 2000, "supplementalGroups": [3000, 3001], "runAsNonRoot": True},
         "activeDeadlineSeconds": 600, "automountServiceAccountToken": False,
