@@ -31,7 +31,7 @@ class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
                  health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None,
-                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None, links_down=()):
+                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None, links_down=(), image_service=None):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
@@ -42,6 +42,8 @@ class LocalCluster:
         self.dev_root = dev_root               # where the plugin finds /dev/kfd + /dev/dri (tests: mknod'd nodes)
         self.isolation = isolation             # process runtime: "auto" | "required" | "off"
         self.links_down = tuple(tuple(x) for x in links_down)   # fake backend: failed xGMI links
+        # process runtime: node dir -> images.service.ImageService (OCI store + registry pulls)
+        self.image_service = image_service
         self.own_dir = workdir is None
         self.dir = workdir or tempfile.mkdtemp(prefix="kamd-cluster-")
         self.emit_events = emit_events
@@ -91,7 +93,8 @@ class LocalCluster:
         if runtime is not None:
             rt = runtime
         elif self.runtime_kind == "process":
-            rt = ProcessRuntime(os.path.join(ndir, "runtime"), isolation=self.isolation)
+            rt = ProcessRuntime(os.path.join(ndir, "runtime"), isolation=self.isolation,
+                                images=self.image_service(os.path.join(ndir, "images")) if self.image_service else None)
         else:
             rt = StubRuntime(payload=self.payload)
         kl = Kubelet(Client(self.url), name, rt, dm, emit_events=self.emit_events,

@@ -25,12 +25,20 @@ def main(argv=None):
     ap.add_argument("--hooks-dir", default=None,
                     help="runtime hooks (JSON {runtime, annotations, images}) choosing a runtime per container "
                          "(the fork's dockershim hooks.d); both runtimes are then available")
+    ap.add_argument("--image-service", default="oci", choices=["oci", "builtin"],
+                    help="'oci' = OCI store + registry pulls, 'builtin' = built-in images / host root only")
+    ap.add_argument("--insecure-registry", action="append", default=[])
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
 
     async def start():
-        rt = ProcessRuntime(os.path.join(a.root_dir, "containers")) if a.runtime == "process" else StubRuntime()
+        images = None
+        if a.image_service == "oci" and a.runtime == "process":
+            from ..images.service import node_image_service
+            images = node_image_service(os.path.join(a.root_dir, "images"), True, a.insecure_registry)
+        rt = ProcessRuntime(os.path.join(a.root_dir, "containers"), images=images) if a.runtime == "process" \
+            else StubRuntime()
         hook_task = None
         if a.hooks_dir:
             import asyncio

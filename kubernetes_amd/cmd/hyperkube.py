@@ -28,6 +28,7 @@ COMPONENTS = {
     "csi-hostpath": "csi_hostpath",
     "node-problem-detector": "npd", "npd": "npd", "log-shipper": "log_shipper", "fluentd": "log_shipper",
     "gendocs": "gendocs",
+    "image": "image", "kamd-image": "image", "registry": "image",
 }
 
 

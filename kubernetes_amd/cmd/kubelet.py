@@ -31,6 +31,11 @@ def main(argv=None):
     ap.add_argument("--pleg-relist-period", type=float, default=1.0, help="generic PLEG relist period (remote runtime)")
     ap.add_argument("--image-gc-high-threshold", type=int, default=85)
     ap.add_argument("--image-gc-low-threshold", type=int, default=80)
+    ap.add_argument("--image-service", default="oci", choices=["oci", "builtin"],
+                    help="process runtime images: 'oci' = OCI store + registry pulls (overlay root "
+                         "filesystems under isolation), 'builtin' = built-in images / host root only")
+    ap.add_argument("--insecure-registry", action="append", default=[],
+                    help="registry host[:port] reached over plain HTTP (loopback registries always are)")
     ap.add_argument("--image-fs-capacity", default="0", help="image filesystem size for image GC (e.g. 100Gi; 0 = off)")
     ap.add_argument("--port", type=int, default=10250)
     ap.add_argument("--address", default="127.0.0.1")
@@ -105,7 +110,11 @@ def main(argv=None):
             from ..cri.remote import RemoteRuntime
             rt = await RemoteRuntime(a.container_runtime_endpoint, a.runtime_request_timeout, a.pleg_relist_period).connect()
         elif a.container_runtime == "process":
-            rt = ProcessRuntime(os.path.join(a.root_dir, "runtime"))
+            images = None
+            if a.image_service == "oci":
+                from ..images.service import node_image_service
+                images = node_image_service(os.path.join(a.root_dir, "images"), True, a.insecure_registry)
+            rt = ProcessRuntime(os.path.join(a.root_dir, "runtime"), images=images)
         else:
             rt = StubRuntime()
         from ..api.quantity import parse_quantity

@@ -321,14 +321,20 @@ class RemoteImageService:
         except grpc.aio.AioRpcError as e:
             raise RuntimeError_(f"{name}: {e.details() or e.code().name}") from None
 
-    async def pull_image(self, image):
-        return (await self._call("PullImage", A.MSG["PullImageRequest"](image=A.MSG["ImageSpec"](image=image)))).image_ref
+    async def pull_image(self, image, auth=None):
+        req = A.MSG["PullImageRequest"](image=A.MSG["ImageSpec"](image=image))
+        if auth is not None:
+            req.auth.CopyFrom(A.MSG["AuthConfig"](username=auth.username, password=auth.password,
+                                                  identity_token=auth.identity_token,
+                                                  registry_token=auth.registry_token))
+        return (await self._call("PullImage", req)).image_ref
 
     async def image_status(self, image):
         r = await self._call("ImageStatus", A.MSG["ImageStatusRequest"](image=A.MSG["ImageSpec"](image=image)))
         if not r.HasField("image"):
             return None
-        return {"id": r.image.id, "repoTags": list(r.image.repo_tags), "size": r.image.size}
+        return {"id": r.image.id, "repoTags": list(r.image.repo_tags), "repoDigests": list(r.image.repo_digests),
+                "size": r.image.size}
 
     async def list_images(self):
         r = await self._call("ListImages", A.MSG["ListImagesRequest"]())

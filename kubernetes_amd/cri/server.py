@@ -31,7 +31,7 @@ import time
 import grpc
 
 from ..deviceplugin.api import generic_handler
-from ..kubelet.runtime.base import EXITED, RUNNING, RunContainerOptions
+from ..kubelet.runtime.base import EXITED, RUNNING, RunContainerOptions, RuntimeError_
 from ..utils.websocket import is_websocket_request
 from . import api as A
 
@@ -91,31 +91,11 @@ class ImageStore:
         return sum(i["size"] for i in self.images.values())
 
 
-class LocalImageService:
-    """The remote image service API over an in-process ImageStore (in-process runtimes)."""
-
-    def __init__(self, store: ImageStore):
-        self.store = store
-
-    async def pull_image(self, image):
-        try:
-            return self.store.pull(image)
-        except LookupError as e:
-            from ..kubelet.runtime.base import RuntimeError_
-            raise RuntimeError_(str(e)) from None
-
-    async def image_status(self, image):
-        i = self.store.status(image)
-        return None if i is None else {"id": i["id"], "repoTags": list(i["repo_tags"]), "size": i["size"]}
-
-    async def list_images(self):
-        return [{"id": i["id"], "repoTags": list(i["repo_tags"]), "size": i["size"]} for i in self.store.images.values()]
-
-    async def remove_image(self, image):
-        self.store.remove(image)
-
-    async def image_fs_info(self):
-        return {"usedBytes": self.store.used_bytes(), "inodesUsed": len(self.store.images)}
+def LocalImageService(store: ImageStore):
+    """The CRI image-service API over built-in images only (in-process runtimes without an OCI
+    store); see `images.service.ImageService`."""
+    from ..images.service import ImageService
+    return ImageService(builtins=store)
 
 
 def process_image_resolver(ref):
@@ -301,7 +281,11 @@ class CRIServer:
         if checkpoint_dir:
             from ..utils.checkpoint import CheckpointManager
             self.checkpoints = CheckpointManager(checkpoint_dir)
-        self.images = ImageStore(image_resolver or (stub_image_resolver if runtime.name == "stub" else host_image_resolver))
+        # the runtime's own image service (OCI store + registry) when it has one, else built-ins
+        from ..images.service import ImageService
+        svc = getattr(runtime, "images", None)
+        self.images = svc if isinstance(svc, ImageService) else ImageService(builtins=ImageStore(
+            image_resolver or (stub_image_resolver if runtime.name == "stub" else host_image_resolver)))
         self.sandboxes: dict[str, dict] = {}
         self.cmeta: dict[str, dict] = {}
         self.streaming = StreamingServer(runtime)
@@ -586,31 +570,41 @@ class CRIServer:
 
     # ---------------------------------------------------------------- image service
     def _image(self, img):
-        return A.MSG["Image"](id=img["id"], repo_tags=img["repo_tags"], size=img["size"])
+        return A.MSG["Image"](id=img["id"], repo_tags=img.get("repoTags") or [], repo_digests=img.get("repoDigests") or [],
+                              size=img.get("size", 0))
 
     async def ListImages(self, req, ctx):
         ref = req.filter.image.image if req.HasField("filter") else ""
-        imgs = [i for i in self.images.images.values() if not ref or self.images.normalize(ref) in i["repo_tags"]]
+        imgs = await self.images.list_images()
+        if ref:
+            want = await self.images.image_status(ref)
+            imgs = [i for i in imgs if want is not None and i["id"] == want["id"]]
         return A.MSG["ListImagesResponse"](images=[self._image(i) for i in imgs])
 
     async def ImageStatus(self, req, ctx):
-        img = self.images.status(req.image.image)
+        img = await self.images.image_status(req.image.image)
         return A.MSG["ImageStatusResponse"](image=self._image(img)) if img else A.MSG["ImageStatusResponse"]()
 
     async def PullImage(self, req, ctx):
+        from ..images.registry import Auth, RegistryError
+        auth = None
+        if req.HasField("auth"):
+            a = req.auth
+            auth = Auth(a.username, a.password, a.auth, a.identity_token, a.registry_token)
         try:
-            return A.MSG["PullImageResponse"](image_ref=self.images.pull(req.image.image))
-        except LookupError as e:
+            return A.MSG["PullImageResponse"](image_ref=await self.images.pull_image(req.image.image, auth))
+        except (LookupError, RegistryError, RuntimeError_, OSError, ValueError) as e:
             await ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
 
     async def RemoveImage(self, req, ctx):
-        self.images.remove(req.image.image)
+        await self.images.remove_image(req.image.image)
         return A.MSG["RemoveImageResponse"]()
 
     async def ImageFsInfo(self, req, ctx):
+        info = await self.images.image_fs_info()
         fs = A.MSG["FilesystemUsage"](timestamp=time.time_ns(), storage_id=A.MSG["StorageIdentifier"](uuid="kamd-images"),
-                                      used_bytes=A.MSG["UInt64Value"](value=self.images.used_bytes()),
-                                      inodes_used=A.MSG["UInt64Value"](value=len(self.images.images)))
+                                      used_bytes=A.MSG["UInt64Value"](value=info["usedBytes"]),
+                                      inodes_used=A.MSG["UInt64Value"](value=info["inodesUsed"]))
         return A.MSG["ImageFsInfoResponse"](image_filesystems=[fs])
 
 

@@ -33,8 +33,11 @@ def default_pull_policy(image: str) -> str:
 
 
 class ImageManager:
-    def __init__(self, service, recorder=None, backoff_initial=10.0, backoff_max=300.0, clock=time.monotonic):
+    def __init__(self, service, recorder=None, backoff_initial=10.0, backoff_max=300.0, clock=time.monotonic,
+                 secret_getter=None):
         self.service = service
+        # async (namespace, name) -> Secret, for the pod's imagePullSecrets keyring
+        self.secret_getter = secret_getter
         self.recorder = recorder
         self.backoff_initial = backoff_initial
         self.backoff_max = backoff_max
@@ -70,7 +73,7 @@ class ImageManager:
             raise ImagePullError("ImagePullBackOff", msg)
         self._event(pod, "Normal", "Pulling", f'pulling image "{image}"')
         try:
-            ref = await self.service.pull_image(image)
+            ref = await self._pull(pod, image)
         except Exception as e:
             period = min(self.backoff_max, b[1] * 2) if b else self.backoff_initial
             self._backoff[image] = (now + period, period)
@@ -81,6 +84,33 @@ class ImageManager:
         self.last_used[ref] = time.time()
         self._event(pod, "Normal", "Pulled", f'Successfully pulled image "{image}"')
         return ref
+
+    async def _pull(self, pod, image):
+        """`kuberuntime_image.go PullImage`: try every matching pull-secret credential in turn
+        (then none), like the reference keyring lookup."""
+        auths = []
+        names = [s.get("name") for s in (pod.get("spec") or {}).get("imagePullSecrets") or () if s.get("name")]
+        if names and self.secret_getter is not None:
+            from ..images.credentials import keyring_from_secrets
+            secrets = []
+            for n in names:
+                try:
+                    secrets.append(await self.secret_getter(pod["metadata"].get("namespace", "default"), n))
+                except Exception:   # noqa: BLE001 - a missing pull secret only removes a credential
+                    continue
+            try:
+                auths = keyring_from_secrets(secrets).lookup(image)
+            except ValueError:
+                auths = []
+        if not auths:
+            return await self.service.pull_image(image)
+        err = None
+        for a in auths:
+            try:
+                return await self.service.pull_image(image, a)
+            except Exception as e:  # noqa: BLE001 - the next credential may work
+                err = e
+        raise err
 
     def retry_after(self, image):
         b = self._backoff.get(image)

@@ -199,7 +199,8 @@ class Kubelet:
             image_service = LocalImageService(ImageStore(stub_image_resolver if runtime.name == "stub" else host_image_resolver))
         from .images import ImageGCManager, ImageManager
         self.image_service = image_service
-        self.images = ImageManager(image_service, self.recorder, backoff_initial=image_backoff)
+        self.images = ImageManager(image_service, self.recorder, backoff_initial=image_backoff,
+                                   secret_getter=lambda ns, name: self.client.get("secrets", name, ns))
         self.image_gc = None
         if image_gc:
             self.image_gc = ImageGCManager(image_service, int(image_gc.get("capacity_bytes", 0)), self._images_in_use,

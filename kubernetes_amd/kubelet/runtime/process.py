@@ -244,8 +244,12 @@ class ProcessRuntime(Runtime):
     name = "process"
     shares_host_network = True     # containers are host processes: pod IP = node address
 
-    def __init__(self, root_dir: str, inherit_env: bool = True, isolation: str | None = None):
+    def __init__(self, root_dir: str, inherit_env: bool = True, isolation: str | None = None, images=None):
         super().__init__()
+        # an images.service.ImageService: OCI images (pulled or imported) run on an overlay of
+        # their unpacked layers; without one, images resolve to built binaries / the host root
+        if images is not None:
+            self.images = images
         self.root = os.path.abspath(root_dir)
         os.makedirs(os.path.join(self.root, "containers"), exist_ok=True)
         os.makedirs(os.path.join(self.root, "sandboxes"), exist_ok=True)
@@ -418,11 +422,33 @@ class ProcessRuntime(Runtime):
         leaf = cid.split("://", 1)[1]
         d = os.path.join(self.root, "containers", leaf)
         os.makedirs(d, exist_ok=True)
-        argv = resolve_command(container)
-        env = dict(os.environ) if self.inherit_env else {"PATH": os.environ.get("PATH", "/usr/bin:/bin")}
-        for e in container.get("env") or ():
-            if "value" in e:
-                env[e["name"]] = str(e["value"])
+        image = container.get("image") or ""
+        svc = getattr(self, "images", None)
+        cfg = svc.image_config(image) if svc is not None and hasattr(svc, "image_config") else None
+        image_root = None
+        if cfg is not None:
+            from ...images.service import command_for, env_for, user_for
+            argv = command_for(container, cfg)
+            if not argv:
+                raise OSError(2, f"image {image!r} has no entrypoint and the container gives no command")
+            image_root = svc.rootfs(image)
+            own = {e["name"]: str(e["value"]) for e in container.get("env") or () if "value" in e}
+            env = env_for(cfg, own)
+            env.setdefault("PATH", "/usr/local/sbin:/usr/local/bin:/usr/sbin:/usr/bin:/sbin:/bin")
+            if opts.run_as_user is None:
+                ug = user_for(cfg, image_root)
+                if ug is not None:
+                    import dataclasses
+                    opts = dataclasses.replace(opts, run_as_user=ug[0],
+                                               run_as_group=opts.run_as_group if opts.run_as_group is not None else ug[1])
+            if not container.get("workingDir") and cfg.get("WorkingDir") and self.isolated:
+                container = dict(container, workingDir=cfg["WorkingDir"])
+        else:
+            argv = resolve_command(container)
+            env = dict(os.environ) if self.inherit_env else {"PATH": os.environ.get("PATH", "/usr/bin:/bin")}
+            for e in container.get("env") or ():
+                if "value" in e:
+                    env[e["name"]] = str(e["value"])
         dev_env = opts.env_dict()
         env.update(dev_env)
         env.pop("ROCR_VISIBLE_DEVICES", None)
@@ -448,11 +474,22 @@ class ProcessRuntime(Runtime):
             ns_paths = {t: f"/proc/{sb['init_pid']}/ns/{t}" for t in ("ipc", "uts")}
             if sb.get("user_ns"):
                 ns_paths["user"] = f"/proc/{sb['init_pid']}/ns/user"
-        spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts, rootfs="/",
+        rootfs, overlay = "/", None
+        if image_root is not None and self.isolated:
+            # copy-on-write root: the image's unpacked layers under this container's upper dir,
+            # mounted by kamd-runc inside the container's mount namespace
+            overlay = {k: os.path.join(d, k) for k in ("rootfs", "upper", "work")}
+            for p in overlay.values():
+                os.makedirs(p, exist_ok=True)
+            rootfs = overlay["rootfs"]
+        spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts, rootfs=rootfs,
                               sandbox_pid=getattr(sb.get("proc"), "pid", None),
                               env=env if self.isolated else None, cgroups_path=cgroup, ns_paths=ns_paths,
                               host_network=self.shares_host_network,
                               cpus=",".join(str(c) for c in sorted(cpus)) if cpus else None)
+        if overlay is not None:
+            spec["annotations"].update({"kamd.io/rootfs-lower": image_root, "kamd.io/rootfs-upper": overlay["upper"],
+                                        "kamd.io/rootfs-work": overlay["work"]})
         with open(os.path.join(d, "config.json"), "w") as f:
             json.dump(spec, f, separators=(",", ":"))
         st = ContainerStatus(cid, container["name"], CREATED, image=container.get("image", ""),
@@ -463,6 +500,7 @@ class ProcessRuntime(Runtime):
                           "oom_score_adj": opts.oom_score_adj, "cgroup": cgroup, "cpus": cpus,
                           "attempt": opts.attempt, "run_as_user": opts.run_as_user, "run_as_group": opts.run_as_group,
                           "groups": list(opts.supplemental_groups), "isolated": self.isolated,
+                          "image_rootfs": overlay is not None,
                           "user": f"{spec['process']['user']['uid']}:{spec['process']['user']['gid']}"}
         return cid
 
@@ -476,7 +514,8 @@ class ProcessRuntime(Runtime):
         log = open(st.log_path, "ab")
         try:
             if m.get("isolated"):
-                _check_entrypoint(m["argv"], m["env"])
+                if not m.get("image_rootfs"):      # (an image's entrypoint lives in its own root)
+                    _check_entrypoint(m["argv"], m["env"])
                 proc, m["init_pid"], m["isolation"] = await _spawn_runc(m["dir"], log)
             else:
                 proc = await self._start_host_process(m, log)

@@ -1018,7 +1018,15 @@ int cmd_run(const std::string& bundle, int ready_fd) {
     setpgid(0, 0);
     if (rep.mount_ns) {
       if (mount(nullptr, "/", nullptr, MS_REC | MS_PRIVATE, nullptr) != 0) die(126, "making / private: %s", strerror(errno));
-      if (root != "/") {
+      const J& ann = spec["annotations"];
+      if (root != "/" && ann.has("kamd.io/rootfs-lower")) {
+        // image rootfs: a copy-on-write overlay of the unpacked image (read-only lower) and the
+        // container's own upper layer, mounted only inside this mount namespace
+        std::string opts = "lowerdir=" + ann["kamd.io/rootfs-lower"].str() + ",upperdir=" +
+                           ann["kamd.io/rootfs-upper"].str() + ",workdir=" + ann["kamd.io/rootfs-work"].str();
+        if (mount("overlay", root.c_str(), "overlay", 0, opts.c_str()) != 0)
+          die(126, "overlay rootfs %s: %s", root.c_str(), strerror(errno));
+      } else if (root != "/") {
         if (mount(root.c_str(), root.c_str(), nullptr, MS_BIND | MS_REC, nullptr) != 0)
           die(126, "bind rootfs %s: %s", root.c_str(), strerror(errno));
       }
