@@ -80,7 +80,10 @@ def _linked(peers, node, ids):
 
 
 def cpu_budget():
-    """CPUs this job may use: affinity mask capped by the cgroup v2 quota."""
+    """CPUs this job may use: affinity mask capped by the cgroup v2 quota. KAMD_BENCH_CPUS
+    overrides it (rehearsing the whole-node control-plane shape on a smaller machine)."""
+    if os.environ.get("KAMD_BENCH_CPUS"):
+        return int(os.environ["KAMD_BENCH_CPUS"])
     n = len(os.sched_getaffinity(0))
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:

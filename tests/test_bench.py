@@ -51,6 +51,23 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 32                 # weak scaling: 2 ranks x 2 nodes x 8 GPUs
 
 
+def test_bench_eight_ranks_whole_node_shape():
+    """The N=8 path the driver runs on a whole MI355X node, rehearsed with gloo on CPU: 8 ranks
+    under torch.distributed.run with the >= 64-CPU control-plane shape (KAMD_BENCH_CPUS=128:
+    16 API server workers, 8 scheduler shards) and small per-rank work."""
+    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1", KAMD_BENCH_CPUS="128")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", "29747", "bench.py", "--gpus", "8",
+                        "--steps", "2", "--warmup", "1", "--nodes-per-rank", "1", "--xgmi4-steps", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    _check(d, 8, 2, 1)
+    assert d["config"]["parallelism"] == "ranks8" and d["config"]["hollow_nodes"] == 8
+    assert d["config"]["global_batch"] == 64
+    assert d["config"]["apiserver_workers"] == 16 and d["config"]["scheduler_shards"] == 8
+
+
 def test_payload_server_batches_starts(run, tmp_path):
     """Hollow-node processes ask the rank's PayloadServer for GPU payload runs: starts issued
     together are answered as one batch (run_batch), failures are reported per start."""
