@@ -45,7 +45,6 @@ from ..storage.mvcc import CompactedError, MVCCStore
 from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
-from ..utils.websocket import is_websocket_request
 from . import admission as adm
 from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, build_authorizer
 from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, event_bytes
@@ -1660,8 +1659,9 @@ class APIServer:
         self._admit(a)
         self._validate_admission(a)
         q = parse_qs(req.qs or "")
-        if is_websocket_request(req.headers):
-            # UpgradeAwareHandler: relay the WebSocket upgrade to the kubelet and splice
+        from ..cri.remotecommand import is_upgrade_request
+        if is_upgrade_request(req.headers):
+            # UpgradeAwareHandler: relay the WebSocket / SPDY upgrade to the kubelet and splice
             from ..cri.remotecommand import upgrade_proxy_response
             if sub == "portforward":
                 return upgrade_proxy_response(req, f"http://{addr}:{port}/portForward/{ns}/{name}?{req.qs}")

@@ -240,14 +240,14 @@ class RemoteRuntime(Runtime):
         r = await self._call("ExecSync", A.MSG["ExecSyncRequest"](container_id=cid, cmd=list(cmd), timeout=int(max(1, timeout))))
         return r.exit_code, bytes(r.stdout) + bytes(r.stderr)
 
-    async def exec_url(self, cid, cmd, tty=False, stdin=False):
+    async def exec_url(self, cid, cmd, tty=False, stdin=False, stdout=True, stderr=None):
         r = await self._call("Exec", A.MSG["ExecRequest"](container_id=cid, cmd=list(cmd), tty=tty, stdin=stdin,
-                                                         stdout=True, stderr=not tty))
+                                                         stdout=stdout, stderr=(not tty) if stderr is None else stderr))
         return r.url
 
-    async def attach_url(self, cid, tty=False, stdin=False):
-        r = await self._call("Attach", A.MSG["AttachRequest"](container_id=cid, tty=tty, stdin=stdin,
-                                                             stdout=True, stderr=not tty))
+    async def attach_url(self, cid, tty=False, stdin=False, stdout=True, stderr=None):
+        r = await self._call("Attach", A.MSG["AttachRequest"](container_id=cid, tty=tty, stdin=stdin, stdout=stdout,
+                                                             stderr=(not tty) if stderr is None else stderr))
         return r.url
 
     async def port_forward_url(self, sid, ports):

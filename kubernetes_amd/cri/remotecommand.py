@@ -336,3 +336,235 @@ def upgrade_proxy_response(req, url: str, extra_headers=None):
 __all__ = ["Options", "options_from_query", "ports_from_query", "exit_status", "rc_from_status", "serve_exec",
            "serve_portforward", "exec_response", "portforward_response", "accept_raw", "upgrade_proxy_response",
            "is_websocket_request", "EXEC_PROTOCOLS", "PORTFORWARD_PROTOCOLS", "V5_CHANNEL"]
+
+
+# -- SPDY/3.1 (what kubectl and client-go of 1.9 speak) ---------------------------------------------
+SPDY_EXEC_PROTOCOLS = ("v4.channel.k8s.io", "v3.channel.k8s.io", "v2.channel.k8s.io", "channel.k8s.io")
+SPDY_PORTFORWARD_PROTOCOL = "portforward.k8s.io"
+STREAM_CREATION_TIMEOUT = 30.0
+
+
+def is_spdy_request(headers) -> bool:
+    return "upgrade" in headers.get("connection", "").lower() and \
+        headers.get("upgrade", "").lower().startswith("spdy/3.1")
+
+
+def is_upgrade_request(headers) -> bool:
+    """A WebSocket or SPDY upgrade (what the API server relays to the kubelet untouched)."""
+    return is_websocket_request(headers) or is_spdy_request(headers)
+
+
+def spdy_negotiate(headers, supported):
+    """`httpstream.Handshake`: the first client protocol (in the client's order) the server
+    supports; "" when the client asked for none (Kubernetes 1.0 clients); None = no match."""
+    offered = [p.strip() for p in headers.get("x-stream-protocol-version", "").split(",") if p.strip()]
+    if not offered:
+        return ""
+    for p in offered:
+        if p in supported:
+            return p
+    return None
+
+
+def _refuse(offered, supported):
+    body = (f"unable to upgrade: unable to negotiate protocol: client supports {offered}, "
+            f"server accepts {list(supported)}").encode()
+    return Response(403, body, "text/plain", {"X-Accepted-Stream-Protocol-Versions": ", ".join(supported)})
+
+
+async def _json_objects(stream):
+    """Consecutive JSON values on a stream (the resize stream of remotecommand v3+)."""
+    dec = json.JSONDecoder()
+    buf = ""
+    while True:
+        d = await stream.read()
+        if not d:
+            return
+        buf += d.decode(errors="replace")
+        while buf.strip():
+            try:
+                obj, end = dec.raw_decode(buf.lstrip())
+            except ValueError:
+                break
+            buf = buf.lstrip()[end:]
+            yield obj
+
+
+async def serve_spdy_exec(reader, writer, proto: str, opts: Options, executor):
+    """One exec/attach session over SPDY (`remotecommand/httpstream.go` v1-v4 handlers): the
+    client opens an error stream plus one per requested stdio stream (and `resize` under a tty
+    for v3+), told apart by their `streamType` header."""
+    from ..utils import spdy
+    want = {"error"} | ({"stdin"} if opts.stdin else set()) | ({"stdout"} if opts.stdout else set()) | \
+        ({"stderr"} if opts.stderr else set()) | ({"resize"} if opts.tty and proto in SPDY_EXEC_PROTOCOLS[:2] else set())
+    streams: dict = {}
+    ready = asyncio.Event()
+
+    async def on_stream(st):
+        await st.reply()
+        streams[st.header("streamtype")] = st
+        if want <= set(streams):
+            ready.set()
+    conn = spdy.Connection(reader, writer, server=True, on_stream=on_stream)
+    serving = asyncio.ensure_future(conn.serve())
+    try:
+        try:
+            await asyncio.wait_for(ready.wait(), STREAM_CREATION_TIMEOUT)
+        except asyncio.TimeoutError:
+            log.warning("exec: timed out waiting for client streams (have %s, want %s)", sorted(streams), sorted(want))
+            return
+
+        async def stdin_chunks():
+            while True:
+                d = await streams["stdin"].read()
+                if not d:
+                    return
+                yield d
+
+        async def sizes():
+            async for obj in _json_objects(streams["resize"]):
+                try:
+                    yield int(obj.get("Width", 0)), int(obj.get("Height", 0))
+                except (TypeError, ValueError, AttributeError):
+                    continue
+
+        def sink(name):
+            async def w(data):
+                if data:
+                    await streams[name].write(data)
+            return w
+        rc, err = None, None
+        try:
+            rc = await executor(stdin_chunks() if opts.stdin else None, sink("stdout") if opts.stdout else None,
+                                sink("stderr") if opts.stderr else None, opts.tty,
+                                sizes() if "resize" in want else None)
+        except (ConnectionError, asyncio.CancelledError):
+            raise
+        except Exception as e:  # noqa: BLE001 - reported on the error stream
+            log.warning("exec failed: %s", e)
+            err = f"error executing command in container: {e}"
+        try:
+            if proto == "v4.channel.k8s.io":
+                await streams["error"].write(json.dumps(exit_status(rc, err)).encode())
+            elif err is not None or rc:
+                await streams["error"].write((err or f"command terminated with non-zero exit code: {rc}").encode())
+            for name in ("stdout", "stderr", "error"):
+                if name in streams:
+                    await streams[name].close()
+        except (ConnectionError, RuntimeError):
+            pass
+    finally:
+        await conn.close()
+        serving.cancel()
+
+
+async def serve_spdy_portforward(reader, writer, dial):
+    """Port forwarding over SPDY (`portforward/httpstream.go`): the client opens a `data` and an
+    `error` stream per connection, paired by the `requestID` header, for the port in `port`."""
+    from ..utils import spdy
+    pairs: dict = {}
+    tasks = []
+
+    async def forward(port, data, error):
+        try:
+            r, w = await dial(port)
+        except OSError as e:
+            try:
+                await error.write(f"error forwarding port {port} to pod: {e}".encode())
+                await error.close()
+                await data.close()
+            except (ConnectionError, RuntimeError):
+                pass
+            return
+
+        async def up():
+            try:
+                while True:
+                    d = await data.read()
+                    if not d:
+                        break
+                    w.write(d)
+                    await w.drain()
+            except (ConnectionError, RuntimeError):
+                pass
+            finally:
+                try:
+                    w.write_eof()
+                except (OSError, RuntimeError):
+                    pass
+        t = asyncio.ensure_future(up())
+        try:
+            while True:
+                d = await r.read(65536)
+                if not d:
+                    break
+                await data.write(d)
+        except (ConnectionError, RuntimeError):
+            pass
+        finally:
+            try:
+                await data.close()
+                await error.close()
+            except (ConnectionError, RuntimeError):
+                pass
+            await asyncio.wait([t], timeout=5)
+            w.close()
+
+    async def on_stream(st):
+        await st.reply()
+        rid = st.header("requestid") or str(st.id)
+        p = pairs.setdefault(rid, {})
+        p[st.header("streamtype")] = st
+        if "data" in p and "error" in p:
+            try:
+                port = int(p["data"].header("port") or p["error"].header("port"))
+            except ValueError:
+                await p["error"].write(b"invalid port")
+                await p["error"].close()
+                return
+            tasks.append(asyncio.ensure_future(forward(port, p["data"], p["error"])))
+    conn = spdy.Connection(reader, writer, server=True, on_stream=on_stream)
+    try:
+        await conn.serve()
+    finally:
+        for t in tasks:
+            t.cancel()
+        await conn.close()
+
+
+def spdy_exec_response(req, executor):
+    try:
+        opts = options_from_query(req.qs)
+    except ValueError as e:
+        return Response(400, str(e).encode(), "text/plain")
+    proto = spdy_negotiate(req.headers, SPDY_EXEC_PROTOCOLS)
+    if proto is None:
+        return _refuse(req.headers.get("x-stream-protocol-version", ""), SPDY_EXEC_PROTOCOLS)
+
+    async def run(reader, writer):
+        await serve_spdy_exec(reader, writer, proto or "channel.k8s.io", opts, executor)
+    return UpgradeResponse(run, "SPDY/3.1", {"X-Stream-Protocol-Version": proto} if proto else None)
+
+
+def spdy_portforward_response(req, dial):
+    proto = spdy_negotiate(req.headers, (SPDY_PORTFORWARD_PROTOCOL,))
+    if proto is None:
+        return _refuse(req.headers.get("x-stream-protocol-version", ""), (SPDY_PORTFORWARD_PROTOCOL,))
+
+    async def run(reader, writer):
+        await serve_spdy_portforward(reader, writer, dial)
+    return UpgradeResponse(run, "SPDY/3.1", {"X-Stream-Protocol-Version": proto} if proto else None)
+
+
+async def accept_raw_spdy(writer, headers, supported):
+    """SPDY upgrade on a raw connection (CRI streaming server) -> protocol, or None after 403."""
+    proto = spdy_negotiate(headers, supported)
+    if proto is None:
+        r = _refuse(headers.get("x-stream-protocol-version", ""), supported)
+        writer.write(b"HTTP/1.1 403 Forbidden\r\nContent-Length: %d\r\n\r\n%s" % (len(r.body), r.body))
+        await writer.drain()
+        return None
+    extra = f"X-Stream-Protocol-Version: {proto}\r\n" if proto else ""
+    writer.write(f"HTTP/1.1 101 Switching Protocols\r\nConnection: Upgrade\r\nUpgrade: SPDY/3.1\r\n{extra}\r\n".encode())
+    await writer.drain()
+    return proto

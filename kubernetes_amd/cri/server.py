@@ -170,10 +170,14 @@ class StreamingServer:
             headers = {}
             for ln in head.decode("latin-1").split("\r\n")[1:]:
                 k, _, v = ln.partition(":")
+                k = k.strip().lower()
                 if k:
-                    headers[k.strip().lower()] = v.strip()
+                    headers[k] = headers[k] + ", " + v.strip() if k in headers else v.strip()
+            from .remotecommand import is_spdy_request
             if is_websocket_request(headers):
                 await self._websocket(kind, req, q, headers, reader, writer)
+            elif is_spdy_request(headers):
+                await self._spdy(kind, req, headers, reader, writer)
             elif kind in ("exec", "attach"):
                 await self._exec(kind, req, writer)
             elif kind == "portforward":
@@ -210,6 +214,27 @@ class StreamingServer:
             async def run(stdin, stdout, stderr, tty, resize):
                 return await rt.attach(cid, stdin, stdout, stderr, tty, resize)
         await rcm.serve_exec(conn, opts, run)
+
+    async def _spdy(self, kind, req, headers, reader, writer):
+        from . import remotecommand as rcm
+        if kind == "portforward":
+            if await rcm.accept_raw_spdy(writer, headers, (rcm.SPDY_PORTFORWARD_PROTOCOL,)) is not None:
+                await rcm.serve_spdy_portforward(reader, writer, lambda port: asyncio.open_connection("127.0.0.1", port))
+            return
+        proto = await rcm.accept_raw_spdy(writer, headers, rcm.SPDY_EXEC_PROTOCOLS)
+        if proto is None:
+            return
+        opts = rcm.Options(bool(req.stdin), bool(req.stdout), bool(req.stderr), bool(req.tty))
+        rt, cid = self.runtime, req.container_id
+        if kind == "exec":
+            cmd = list(req.cmd)
+
+            async def run(stdin, stdout, stderr, tty, resize):
+                return await rt.exec_interactive(cid, cmd, stdin, stdout, stderr, tty, resize)
+        else:
+            async def run(stdin, stdout, stderr, tty, resize):
+                return await rt.attach(cid, stdin, stdout, stderr, tty, resize)
+        await rcm.serve_spdy_exec(reader, writer, proto or "channel.k8s.io", opts, run)
 
     async def _exec(self, kind, req, writer):
         writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/vnd.kamd.stream\r\nTransfer-Encoding: chunked\r\n\r\n")

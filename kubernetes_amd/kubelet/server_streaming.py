@@ -6,7 +6,10 @@ and `getExec`/`getPortForward` (`:600-700`): with a CRI runtime the kubelet obta
 URL from the runtime (`Exec`/`PortForward` RPCs) and proxies it; for the in-process runtimes it
 serves the stream itself.
 
-Two wire protocols:
+Three wire protocols:
+  * SPDY/3.1 (`Upgrade: SPDY/3.1`, sub-protocol in `X-Stream-Protocol-Version`): what kubectl and
+    client-go of 1.9 use — remotecommand v1-v4 (`streamType` error/stdin/stdout/stderr/resize
+    streams) and `portforward.k8s.io` (data/error stream pairs per `requestID`);
   * WebSocket (`Upgrade: websocket`): the Kubernetes channel protocols `channel.k8s.io`,
     `base64.channel.k8s.io`, `v4.channel.k8s.io`, `v4.base64.channel.k8s.io` (+ `v5`) for
     exec/attach with stdin, tty and resize, and the per-port channel pairs of port-forward
@@ -61,8 +64,8 @@ async def handle(kubelet, req):
         return None
     parts = [x for x in p.split("/")[2:] if x]
     rt = kubelet.runtime
-    if verb != "run" and is_websocket_request(req.headers):
-        return await _websocket(kubelet, rt, req, verb, parts)
+    if verb != "run" and (is_websocket_request(req.headers) or rc_.is_spdy_request(req.headers)):
+        return await _upgraded(kubelet, rt, req, verb, parts, spdy=rc_.is_spdy_request(req.headers))
     if verb in ("exec", "run", "attach"):
         st, cid, err = _find(kubelet, parts)
         if err:
@@ -109,19 +112,21 @@ async def handle(kubelet, req):
     return UpgradeResponse(run_local)
 
 
-async def _websocket(kubelet, rt, req, verb, parts):
+async def _upgraded(kubelet, rt, req, verb, parts, spdy=False):
+    """WebSocket or SPDY/3.1 sessions (the transport is chosen by the client's Upgrade header)."""
     if verb == "portForward":
         st, _, err = _find(kubelet, parts, with_container=False)
         if err:
             return Response(404, err.encode(), "text/plain")
         if hasattr(rt, "port_forward_url"):
             try:
-                ports = rc_.ports_from_query(req.qs)
+                ports = [] if spdy else rc_.ports_from_query(req.qs)     # SPDY names ports per stream
             except ValueError as e:
                 return Response(400, str(e).encode(), "text/plain")
             return rc_.upgrade_proxy_response(req, await rt.port_forward_url(st.sandbox, ports))
         # in-process runtimes: pods share the host network namespace
-        return rc_.portforward_response(req, lambda port: asyncio.open_connection("127.0.0.1", port))
+        dial = lambda port: asyncio.open_connection("127.0.0.1", port)   # noqa: E731
+        return rc_.spdy_portforward_response(req, dial) if spdy else rc_.portforward_response(req, dial)
     st, cid, err = _find(kubelet, parts)
     if err:
         return Response(404, err.encode(), "text/plain")
@@ -134,8 +139,8 @@ async def _websocket(kubelet, rt, req, verb, parts):
     except ValueError as e:
         return Response(400, str(e).encode(), "text/plain")
     if hasattr(rt, "exec_url"):
-        url = (await rt.exec_url(cid, cmd, tty=opts.tty, stdin=opts.stdin) if verb == "exec" else
-               await rt.attach_url(cid, tty=opts.tty, stdin=opts.stdin))
+        kw = dict(tty=opts.tty, stdin=opts.stdin, stdout=opts.stdout, stderr=opts.stderr)
+        url = await rt.exec_url(cid, cmd, **kw) if verb == "exec" else await rt.attach_url(cid, **kw)
         return rc_.upgrade_proxy_response(req, url)
     if verb == "exec":
         async def run(stdin, stdout, stderr, tty, resize):
@@ -143,7 +148,7 @@ async def _websocket(kubelet, rt, req, verb, parts):
     else:
         async def run(stdin, stdout, stderr, tty, resize):
             return await rt.attach(cid, stdin, stdout, stderr, tty, resize)
-    return rc_.exec_response(req, req.qs, run)
+    return rc_.spdy_exec_response(req, run) if spdy else rc_.exec_response(req, req.qs, run)
 
 
 def _static(raw):

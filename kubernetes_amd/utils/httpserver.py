@@ -191,7 +191,10 @@ class _Conn(asyncio.Protocol):
         headers = {}
         for ln in lines[1:]:
             k, _, v = ln.partition(":")
-            headers[k.strip().lower()] = v.strip()
+            k = k.strip().lower()
+            # repeated headers combine into one comma-separated list (RFC 7230 §3.2.2), e.g.
+            # several X-Stream-Protocol-Version offers
+            headers[k] = headers[k] + ", " + v.strip() if k in headers else v.strip()
         clen = int(headers.get("content-length", "0") or 0)
         if len(buf) < end + 4 + clen:
             return None
