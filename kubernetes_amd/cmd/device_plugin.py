@@ -28,6 +28,10 @@ def main(argv=None):
     ap.add_argument("--burn-in-min-hbm-gbps", type=float, default=3000.0)
     ap.add_argument("--burn-in-min-fp8-tflops", type=float, default=1400.0,
                     help="fp8 (e4m3, block-scaled MFMA) GEMM floor; 0 skips the fp8 step")
+    ap.add_argument("--xgmi-link-probe", action="store_true",
+                    help="measure peer copies between the node's GPUs (xgmi-probe --p2p) after burn-in; "
+                         "links below --xgmi-link-min-gbps leave the published link graph")
+    ap.add_argument("--xgmi-link-min-gbps", type=float, default=25.0)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -40,8 +44,13 @@ def main(argv=None):
             from ..deviceplugin.burnin import BurnIn
             burn_in = BurnIn(min_tflops=a.burn_in_min_tflops, min_hbm_gbps=a.burn_in_min_hbm_gbps,
                              min_fp8_tflops=a.burn_in_min_fp8_tflops, fp8=a.burn_in_min_fp8_tflops > 0)
+        probe = None
+        if a.xgmi_link_probe and not smi.is_fake:
+            from ..deviceplugin.linkprobe import run_probe
+            probe = run_probe
         p = AMDGPUPlugin(a.plugins_dir, smi=smi, socket_name=a.socket_name, health_interval=a.health_interval,
-                         rocm_mount=a.rocm_mount, burn_in=burn_in)
+                         rocm_mount=a.rocm_mount, burn_in=burn_in, link_probe=probe,
+                         link_min_gbps=a.xgmi_link_min_gbps)
         await p.start()
         print(f"amd.com/gpu plugin serving {len(p.gpus)} GPU(s) on {p.socket_path}", flush=True)
         if a.exporter_port is not None:

@@ -36,6 +36,7 @@ ATTR_BURN_IN = "amd.com/burn-in"          # pending / passed / failed
 ATTR_MFMA_TFLOPS = "amd.com/mfma-tflops"  # measured bf16 MFMA GEMM throughput
 ATTR_HBM_GBPS = "amd.com/hbm-gbps"        # measured HBM copy bandwidth
 ATTR_MFMA_FP8_TFLOPS = "amd.com/mfma-fp8-tflops"   # measured fp8 (e4m3, block-scaled MFMA) GEMM throughput
+ATTR_XGMI_P2P_GBPS = "amd.com/xgmi-p2p-gbps"        # slowest measured peer copy to a hive peer
 
 log = logging.getLogger("amdgpu-plugin")
 
@@ -104,8 +105,17 @@ def gpu_attributes(g: amdsmi.GPU, m: amdsmi.Metrics | None = None, peers: tuple 
 class AMDGPUPlugin(DevicePluginServer):
     def __init__(self, plugins_dir: str, smi: amdsmi.SMI | None = None, socket_name="amdgpu.sock",
                  health_interval=5.0, dev_root="/dev", rocm_mount: str | None = None, indices=None,
-                 check_dev_nodes: bool | None = None, init_timeout=10, burn_in=None):
+                 check_dev_nodes: bool | None = None, init_timeout=10, burn_in=None, link_probe=None,
+                 link_min_gbps=None):
         self.smi = smi or amdsmi.SMI()
+        # optional xGMI link probe (deviceplugin/linkprobe.py): hip ordinals -> ProbeResult;
+        # links measured below link_min_gbps leave the published link graph
+        from .linkprobe import DEFAULT_MIN_GBPS
+        self.link_probe = link_probe
+        self.link_min_gbps = DEFAULT_MIN_GBPS if link_min_gbps is None else link_min_gbps
+        self._weak: set = set()
+        self._p2p: dict = {}                      # device index -> slowest measured peer copy GB/s
+        self._probe_task = None
         # optional acceptance test (deviceplugin/burnin.py): devices stay Unhealthy until it
         # passes; `burn_in` is a BurnIn or any object with run(hip_index) -> BurnInResult
         self.burn_in = burn_in
@@ -122,7 +132,7 @@ class AMDGPUPlugin(DevicePluginServer):
         # graph, not merely on devices with enough links (a 6/7-link GPU must not be paired with
         # the one peer it cannot reach)
         self._all_gpus = all_gpus
-        self.peers = xgmi_peer_map(self.smi, all_gpus)
+        self.peers = self._peer_map()
         self._ecc_base = {}
         self._health = {}
         devs = []
@@ -145,8 +155,44 @@ class AMDGPUPlugin(DevicePluginServer):
         self._health_task = None
 
     # -- health -------------------------------------------------------------
+    def _peer_map(self):
+        from .linkprobe import prune_peers
+        peers = xgmi_peer_map(self.smi, self._all_gpus)
+        hip_of = {g.index: (g.hip_id if g.hip_id >= 0 else g.index) for g in self._all_gpus}
+        return prune_peers(peers, hip_of, self._weak)
+
+    async def run_link_probe(self):
+        """Measure peer-to-peer copies inside each hive of this plugin's GPUs; weak links leave
+        the peer map (pushed to the kubelet like any health change). Returns the weak pairs."""
+        loop = asyncio.get_running_loop()
+        by_hive: dict = {}
+        for g in self.gpus:
+            by_hive.setdefault(g.xgmi_hive_id, []).append(g)
+        weak = set()
+        for hive, gs in by_hive.items():
+            hips = sorted({g.hip_id if g.hip_id >= 0 else g.index for g in gs})
+            r = await loop.run_in_executor(None, self.link_probe, hips)
+            if r.error:
+                log.warning("xGMI link probe of hive %x skipped: %s", hive, r.error)
+                continue
+            w = r.weak_pairs(self.link_min_gbps)
+            for pair in w:
+                log.error("xGMI link %s measured below %.0f GB/s: removed from the link graph",
+                          "<->".join(str(x) for x in sorted(pair)), self.link_min_gbps)
+            weak |= w
+            for g in gs:
+                h = g.hip_id if g.hip_id >= 0 else g.index
+                vals = [v for (a, b), v in r.pairs.items() if a == h or b == h]
+                if vals:
+                    self._p2p[g.index] = min(vals)
+        self._weak = weak
+        self.poll_health(force=True)
+        return weak
+
     def _device(self, g: amdsmi.GPU, m: amdsmi.Metrics, health: str):
         attrs = gpu_attributes(g, m, self.peers.get(g.index))
+        if g.index in self._p2p:
+            attrs[ATTR_XGMI_P2P_GBPS] = str(int(self._p2p[g.index]))
         if self.burn_in is not None:
             r = self._burn.get(g.device_id_str)
             attrs[ATTR_BURN_IN] = PENDING if r is None else (PASSED if r.ok else FAILED)
@@ -174,7 +220,7 @@ class AMDGPUPlugin(DevicePluginServer):
         """Re-evaluate health; push a new list if anything changed. Returns True if changed."""
         changed = False
         devs = []
-        peers = xgmi_peer_map(self.smi, self._all_gpus)
+        peers = self._peer_map()
         if peers != self.peers:
             log.warning("xGMI peer map changed: %s -> %s", self.peers, peers)
             self.peers = peers
@@ -226,9 +272,16 @@ class AMDGPUPlugin(DevicePluginServer):
         await super().start()
         if self.health_interval:
             self._health_task = asyncio.ensure_future(self._health_loop())
-        if self.burn_in is not None:
-            self._burn_task = asyncio.ensure_future(self.run_burn_in())
+        if self.burn_in is not None or self.link_probe is not None:
+            self._burn_task = asyncio.ensure_future(self._acceptance())
         return self
+
+    async def _acceptance(self):
+        """Burn-in first (it owns the GPUs while it runs), then the link probe."""
+        if self.burn_in is not None:
+            await self.run_burn_in()
+        if self.link_probe is not None:
+            await self.run_link_probe()
 
     async def stop(self, grace=0.1):
         if self._health_task:

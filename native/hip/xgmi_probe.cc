@@ -14,7 +14,74 @@
 #define HIPCHK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 #define NCCLCHK(x) do { ncclResult_t r = (x); if (r != ncclSuccess) { fprintf(stderr, "%s: %s\n", #x, ncclGetErrorString(r)); return 1; } } while (0)
 
+// --p2p [MiB] [iters]: pairwise peer-to-peer copy bandwidth (hipMemcpyPeerAsync, src stream
+// timed with events) for every ordered pair of visible GPUs, plus each GPU's local
+// device-to-device copy bandwidth; one JSON object. The device plugin turns pairs that are far
+// below a healthy xGMI link into missing edges of the published link graph.
+static int p2p(size_t mib, int iters) {
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (n < 1) { fprintf(stderr, "no devices\n"); return 2; }
+  size_t bytes = mib << 20;
+  std::vector<void*> a(n), b(n);
+  std::vector<hipStream_t> st(n);
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(i));
+    HIPCHK(hipMalloc(&a[i], bytes));
+    HIPCHK(hipMalloc(&b[i], bytes));
+    HIPCHK(hipMemset(a[i], i + 1, bytes));
+    HIPCHK(hipStreamCreate(&st[i]));
+  }
+  auto timed = [&](int dev, auto&& op, double* gbps) -> int {
+    hipEvent_t e0, e1;
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    if (op()) return 1;                                   // warm-up (maps peer memory)
+    HIPCHK(hipStreamSynchronize(st[dev]));
+    HIPCHK(hipEventRecord(e0, st[dev]));
+    for (int k = 0; k < iters; ++k) if (op()) return 1;
+    HIPCHK(hipEventRecord(e1, st[dev]));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    *gbps = (double)bytes * iters / (ms / 1e3) / 1e9;
+    HIPCHK(hipEventDestroy(e0));
+    HIPCHK(hipEventDestroy(e1));
+    return 0;
+  };
+  printf("{\"mode\": \"p2p\", \"devices\": %d, \"bytes\": %zu, \"local\": [", n, bytes);
+  for (int i = 0; i < n; ++i) {
+    double g = 0;
+    if (timed(i, [&]() -> int { HIPCHK(hipMemcpyAsync(b[i], a[i], bytes, hipMemcpyDeviceToDevice, st[i])); return 0; }, &g)) return 1;
+    printf("%s{\"dev\": %d, \"GBps\": %.1f}", i ? ", " : "", i, g);
+  }
+  printf("], \"pairs\": [");
+  bool first = true;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (i == j) continue;
+      int can = 0;
+      HIPCHK(hipDeviceCanAccessPeer(&can, i, j));
+      double g = 0;
+      if (can) {
+        HIPCHK(hipSetDevice(i));
+        hipError_t e = hipDeviceEnablePeerAccess(j, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { fprintf(stderr, "peer %d->%d: %s\n", i, j, hipGetErrorString(e)); return 1; }
+        (void)hipGetLastError();
+      }
+      if (timed(i, [&]() -> int { HIPCHK(hipMemcpyPeerAsync(b[j], j, a[i], i, bytes, st[i])); return 0; }, &g)) return 1;
+      printf("%s{\"src\": %d, \"dst\": %d, \"peer\": %s, \"GBps\": %.1f}", first ? "" : ", ", i, j, can ? "true" : "false", g);
+      first = false;
+    }
+  printf("]}\n");
+  for (int i = 0; i < n; ++i) { hipSetDevice(i); hipFree(a[i]); hipFree(b[i]); hipStreamDestroy(st[i]); }
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && strcmp(argv[1], "--p2p") == 0)
+    return p2p(argc > 2 ? (size_t)atol(argv[2]) : 256, argc > 3 ? atoi(argv[3]) : 10);
   size_t mib = argc > 1 ? (size_t)atol(argv[1]) : 256;
   int iters = argc > 2 ? atoi(argv[2]) : 20;
   int n = 0;

@@ -131,3 +131,26 @@ def test_pod_vram_attribution_on_mi355x(run):
             assert (1 << 30) <= used <= (2 << 30), (used, acc)
             await cl.client.delete("pods", "hold", "default")
     run(main(), timeout=150)
+
+
+def test_xgmi_link_probe_on_mi355x(run, tmp_path):
+    """`xgmi-probe --p2p` on the box's GPUs: local copy bandwidth of an HBM3E device, one JSON
+    object; the plugin's link probe over the real SMI publishes no weak link."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kubernetes_amd.deviceplugin.amdgpu import AMDGPUPlugin
+    from kubernetes_amd.deviceplugin.linkprobe import run_probe
+    from kubernetes_amd.native import amdsmi
+    smi = amdsmi.SMI()
+    hips = sorted(g.hip_id if g.hip_id >= 0 else g.index for g in smi.gpus())
+    r = run_probe(hips, mib=256, iters=10)
+    print(r.local, r.pairs)
+    assert not r.error, r.error
+    assert set(r.local) == set(hips) and all(v > 500 for v in r.local.values())
+    assert len(r.pairs) == len(hips) * (len(hips) - 1)
+
+    async def main():
+        p = AMDGPUPlugin(str(tmp_path), smi=smi, health_interval=0, link_probe=run_probe)
+        assert await p.run_link_probe() == set()
+    run(main(), timeout=120)

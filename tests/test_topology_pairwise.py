@@ -154,3 +154,37 @@ def test_runtime_link_failure_updates_peers(run):
             finally:
                 plugin.smi.fake_set_link(0, 7, xgmi=True)
     run(main(), timeout=60)
+
+
+def test_link_probe_prunes_weak_links_from_peer_map(run, tmp_path):
+    """A link the SMI reports up but that measures far below a healthy xGMI link (p2p copy)
+    leaves the published link graph; the slowest peer copy is published per device."""
+    from kubernetes_amd.deviceplugin.amdgpu import ATTR_XGMI_P2P_GBPS, AMDGPUPlugin
+    from kubernetes_amd.deviceplugin.linkprobe import ProbeResult, parse
+    from kubernetes_amd.native import amdsmi
+
+    def probe(hips):
+        pairs = {(a, b): 60.0 for a in hips for b in hips if a != b}
+        pairs[(1, 2)] = 3.5                     # degraded link, one direction is enough
+        return ProbeResult(pairs, {h: 2500.0 for h in hips})
+
+    async def main():
+        smi = amdsmi.SMI(fixture=amdsmi.fixture_file(8))
+        p = AMDGPUPlugin(str(tmp_path), smi=smi, health_interval=0, link_probe=probe, link_min_gbps=25)
+        before = dict(p.peers)
+        weak = await p.run_link_probe()
+        assert weak == {frozenset((1, 2))}
+        g = {x.index: x for x in smi.gpus()}
+        l1, l2 = p.peers[1][0], p.peers[2][0]
+        assert not (p.peers[1][1] >> l2) & 1 and not (p.peers[2][1] >> l1) & 1
+        assert (before[1][1] >> l2) & 1                                  # it was there before
+        assert p.peers[0] == before[0]
+        attrs = {d.ID: dict(d.Attributes) for d in p.devices}
+        assert attrs[g[1].device_id_str][ATTR_XGMI_P2P_GBPS] == "3"
+        assert attrs[g[0].device_id_str][ATTR_XGMI_P2P_GBPS] == "60"
+    run(main())
+    # the native probe's JSON
+    r = parse('{"mode": "p2p", "devices": 2, "bytes": 1, "local": [{"dev": 0, "GBps": 2400.0}, '
+              '{"dev": 1, "GBps": 2390.5}], "pairs": [{"src": 0, "dst": 1, "peer": true, "GBps": 51.2}, '
+              '{"src": 1, "dst": 0, "peer": true, "GBps": 50.9}]}', [4, 6])
+    assert r.pairs == {(4, 6): 51.2, (6, 4): 50.9} and r.local == {4: 2400.0, 6: 2390.5}
