@@ -29,6 +29,7 @@ COMPONENTS = {
     "node-problem-detector": "npd", "npd": "npd", "log-shipper": "log_shipper", "fluentd": "log_shipper",
     "gendocs": "gendocs",
     "image": "image", "kamd-image": "image", "registry": "image",
+    "etcd-gateway": "etcd_gateway", "kamd-etcd-gateway": "etcd_gateway",
 }
 
 
