@@ -223,23 +223,30 @@ class GenericScheduler:
         start = self._next_start % n
         preds = preds_for_pod
         checked = 0
-        for off in range(n):
-            ni = nodes[(start + off) % n]
+        hits = misses = 0
+        # hot loop (every node, every pod): locals only; equivalence-cache failures are not
+        # recorded per node here — FitError rebuilds the reasons on its (rare) path
+        ec_get = ec.get if ec is not None else None
+        ec_failed = [] if ec is not None else None
+        topo = ctx.topo_scores
+        f_append, r_append = fnodes.append, raws.append
+        order = nodes[start:] + nodes[:start] if start else nodes
+        for ni in order:
             checked += 1
-            if ec is not None:
-                ent = ec.get(ni.name)
+            if ec_get is not None:
+                ent = ec_get(ni.name)
                 if ent is not None and ent[0] == ni.generation:
-                    self.ecache_hits += 1
+                    hits += 1
                     if ent[1]:
-                        failed[ni.name] = ent[1]
+                        ec_failed.append(ni)
                         continue
-                    ctx.topo_scores[ni.name] = ent[2]
-                    fnodes.append(ni)
-                    raws.append(ent[3])
+                    topo[ni.name] = ent[2]
+                    f_append(ni)
+                    r_append(ent[3])
                     if len(fnodes) >= want:
                         break
                     continue
-                self.ecache_misses += 1
+                misses += 1
             reason = None
             score = None
             for rn, cnt in need.items():
@@ -276,6 +283,8 @@ class GenericScheduler:
             if len(fnodes) >= want:
                 break
         self._next_start = start + checked
+        self.ecache_hits += hits
+        self.ecache_misses += misses
         for ext in self.extenders:
             keep, efailed = ext.filter(pod, fnodes)
             failed.update(efailed)
@@ -283,6 +292,8 @@ class GenericScheduler:
             raws = [r for f, r in zip(fnodes, raws) if f.name in keepset]
             fnodes = [f for f in fnodes if f.name in keepset]
         if not fnodes:
+            for ni in ec_failed or ():
+                failed[ni.name] = ec[ni.name][1]
             raise FitError(pod, n, failed)
         if self.prefer is not None and len(fnodes) > 1:
             own = [i for i, ni in enumerate(fnodes) if self.prefer(ni.name)]
