@@ -221,7 +221,7 @@ class Connection:
                         await self._send(control_frame(RST_STREAM, 0, struct.pack(">II", sid, RST_INVALID_STREAM)))
                         continue
                     st._feed(payload, flags & FLAG_FIN)
-        except (asyncio.IncompleteReadError, ConnectionError, SpdyError, zlib.error, struct.error):
+        except (asyncio.IncompleteReadError, ConnectionError, RuntimeError, SpdyError, zlib.error, struct.error):
             pass
         finally:
             for st in self.streams.values():
@@ -240,9 +240,16 @@ class Connection:
             if flags & FLAG_FIN:
                 st._feed(b"", True)
             if self.on_stream is not None:
-                r = self.on_stream(st)
-                if asyncio.iscoroutine(r):
-                    await r
+                try:
+                    r = self.on_stream(st)
+                    if asyncio.iscoroutine(r):
+                        await r
+                except (ConnectionError, RuntimeError):
+                    raise
+                except Exception:  # noqa: BLE001 - a handler bug refuses the stream, not the session
+                    import logging
+                    logging.getLogger("spdy").exception("stream %d handler failed", sid)
+                    await st.reset_stream(RST_REFUSED_STREAM)
         elif ftype == SYN_REPLY:
             sid = struct.unpack_from(">I", body, 0)[0] & 0x7FFFFFFF
             decode_block(self._decompress(body[4:]))      # keep the shared zlib stream in step
