@@ -1,6 +1,7 @@
 """Pod volumes and container environment, kubelet side.
 
 Parity:
+  * network / block volumes (nfs, cephfs, glusterfs, iscsi, fc, rbd) in `volume_plugins.py`;
   * `pkg/kubelet/volumemanager` + the in-tree plugins that need no cloud or network storage:
     `pkg/volume/empty_dir` (node disk or `medium: Memory` = tmpfs, here /dev/shm),
     `pkg/volume/host_path` (with `type: DirectoryOrCreate|FileOrCreate|Directory|File`),
@@ -24,10 +25,32 @@ import shutil
 
 from ..api.quantity import parse_quantity
 from ..client.rest import APIStatusError
+from .volume_plugins import NETWORK_KINDS
 
 
 class VolumeError(Exception):
     pass
+
+
+def _rmtree_no_mounts(path, mounter):
+    """Remove a pod directory but never descend into a mount point (a network volume that failed
+    to unmount must not lose its remote files)."""
+    if not os.path.lexists(path):
+        return
+    if mounter.is_mount_point(path):
+        return
+    if os.path.isdir(path) and not os.path.islink(path):
+        for e in os.listdir(path):
+            _rmtree_no_mounts(os.path.join(path, e), mounter)
+        try:
+            os.rmdir(path)
+        except OSError:
+            pass
+    else:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
 
 
 def _write_files(d, data: dict, items=None, mode=0o644, binary=False):
@@ -88,7 +111,10 @@ def _resource_field(container, ref):
 
 class VolumeManager:
     def __init__(self, client, root, csi_plugins_dir=None, node_name=None, attach_timeout=60.0,
-                 flex_plugins_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec"):
+                 flex_plugins_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec", mounter=None):
+        from .volume_plugins import Mounter
+        self.mounter = mounter or Mounter()               # nfs / cephfs / glusterfs / iscsi / fc / rbd
+        self.net_mounted: dict[str, list] = {}           # pod uid -> [plugin state]
         self.flex_dir = flex_plugins_dir
         self.flex_mounted: dict[str, list] = {}      # pod uid -> [(driver path, target)]
         self.flex_inited: dict[str, dict] = {}       # driver path -> init capabilities
@@ -145,6 +171,9 @@ class VolumeManager:
                 d = await self._flex_mount(pod, name, v["flexVolume"], d)
             elif "gitRepo" in v:
                 await self._git_repo(v["gitRepo"], d)
+            elif any(k in v for k in NETWORK_KINDS):
+                kind = next(k for k in NETWORK_KINDS if k in v)
+                d = await self._net_mount(pod, kind, v[kind], d)
             elif "projected" in v:
                 for src in v["projected"].get("sources") or ():
                     if "configMap" in src or "secret" in src:
@@ -171,6 +200,15 @@ class VolumeManager:
             return await self._flex_mount(pod, vol, sp["flexVolume"], d)
         if sp.get("csi"):
             return await self._csi_publish(pod, vol, sp, node_name or self.node_name, pv)
+        kind = next((k for k in NETWORK_KINDS if sp.get(k)), None)
+        if kind is not None and pod is not None:
+            # PV mount options: spec.mountOptions, or the 1.9 beta annotation
+            opts = list(sp.get("mountOptions") or ())
+            ann = ((pv.get("metadata") or {}).get("annotations") or {}).get("volume.beta.kubernetes.io/mount-options")
+            if ann and not opts:
+                opts = [o.strip() for o in ann.split(",") if o.strip()]
+            target = os.path.join(self.pod_dir(pod), "volumes", f"kubernetes.io~{kind}", vol)
+            return await self._net_mount(pod, kind, sp[kind], target, opts)
         path = (sp.get("hostPath") or {}).get("path") or (sp.get("local") or {}).get("path")
         if not path:
             raise VolumeError(f"persistentvolume {vol}: only hostPath / local volumes can be mounted on this node")
@@ -214,6 +252,21 @@ class VolumeManager:
         finally:
             await c.close()
         self.csi_published.setdefault(pod["metadata"]["uid"], []).append((driver, handle, target))
+        return target
+
+    async def _net_mount(self, pod, kind, src, target, mount_options=()):
+        """nfs / cephfs / glusterfs / iscsi / fc / rbd (`kubelet/volume_plugins.py`)."""
+        from .volume_plugins import MOUNT, MountError, PluginContext
+        ctx = PluginContext(self.client, pod["metadata"].get("namespace", "default"), self.mounter,
+                            os.path.join(self.root, "..", "plugins", f"kubernetes.io~{kind}"), mount_options)
+        if self.mounter.is_mount_point(target):
+            return target                          # already set up (pod resync)
+        try:
+            state = await MOUNT[kind](src, target, ctx)
+        except (MountError, APIStatusError, KeyError, ValueError) as e:
+            raise VolumeError(f"{kind} volume: {e}")
+        state["kind"] = kind
+        self.net_mounted.setdefault(pod["metadata"]["uid"], []).append(state)
         return target
 
     async def _flex_call(self, driver_path, *args):
@@ -285,7 +338,23 @@ class VolumeManager:
                     raise VolumeError(f"git {' '.join(cmd)}: {err.decode(errors='replace').strip()}")
 
     async def unpublish(self, pod):
-        """FlexVolume `unmount` and CSI NodeUnpublishVolume for the pod's volumes (TearDownAt)."""
+        """FlexVolume `unmount`, CSI NodeUnpublishVolume and network/block unmount + detach for
+        the pod's volumes (TearDownAt / UnmountDevice)."""
+        from .volume_plugins import MountError, PluginContext, detach
+        states = self.net_mounted.pop(pod["metadata"]["uid"], [])
+
+        def still_used(key):
+            for sts in self.net_mounted.values():
+                for st in sts:
+                    if ("iscsi", st.get("iscsi", (None, None))[1]) == key or ("rbd", st.get("rbd")) == key:
+                        return True
+            return False
+        for st in states:
+            ctx = PluginContext(self.client, pod["metadata"].get("namespace", "default"), self.mounter, "")
+            try:
+                await detach(ctx, st, still_used)
+            except MountError:
+                pass
         for path, target in self.flex_mounted.pop(pod["metadata"]["uid"], []):
             try:
                 await self._flex_call(path, "unmount", target)
@@ -342,7 +411,7 @@ class VolumeManager:
         return out
 
     def teardown(self, pod):
-        shutil.rmtree(self.pod_dir(pod), ignore_errors=True)
+        _rmtree_no_mounts(self.pod_dir(pod), self.mounter)
         shm = os.path.join("/dev/shm", "kamd-" + pod["metadata"]["uid"])
         if os.path.isdir(shm):
             shutil.rmtree(shm, ignore_errors=True)
