@@ -287,3 +287,25 @@ def parse_field_selector(s: str | None) -> FieldSelector:
         else:
             raise SelectorError(f"invalid field selector term {part!r}")
     return FieldSelector(terms)
+
+
+def selector_to_string(sel) -> str:
+    """A LabelSelector (or a plain label map, as RC selectors are) in the query-string form
+    `metav1.FormatLabelSelector` prints (`a=b,c in (d,e),!f`)."""
+    if not sel:
+        return ""
+    if "matchLabels" not in sel and "matchExpressions" not in sel:
+        sel = {"matchLabels": sel}
+    parts = [f"{k}={v}" for k, v in sorted((sel.get("matchLabels") or {}).items())]
+    for e in sel.get("matchExpressions") or ():
+        op = e.get("operator")
+        vals = ",".join(e.get("values") or ())
+        if op == "In":
+            parts.append(f"{e['key']} in ({vals})")
+        elif op == "NotIn":
+            parts.append(f"{e['key']} notin ({vals})")
+        elif op == "Exists":
+            parts.append(e["key"])
+        elif op == "DoesNotExist":
+            parts.append(f"!{e['key']}")
+    return ",".join(parts)

@@ -67,6 +67,7 @@ class Strategy:
     """Default strategy: spec+status updated together, no status subresource."""
     has_status = True      # exposes /status; main updates ignore status changes
     bump_generation = True
+    generation_on_annotations = False
 
     def __init__(self, ri):
         self.ri = ri
@@ -191,6 +192,64 @@ class NoStatusStrategy(Strategy):
     has_status = False
 
 
+class WorkloadStrategy(Strategy):
+    """Kinds whose status only controllers write: a client's status is dropped on create
+    (`PrepareForCreate`: `Status = {}` in pkg/registry/{apps,extensions,batch,autoscaling,policy,
+    networking}/*/strategy.go) and kept from the stored object on a main-resource update."""
+    initial_status: dict = {}
+
+    def prepare_create(self, obj):
+        obj["status"] = dict(self.initial_status)
+
+
+class VolumeStrategy(WorkloadStrategy):
+    """PV / PVC: status reset on create, phase Pending until the binder moves it
+    (`pkg/registry/core/persistentvolume{,claim}/strategy.go` + SetDefaults)."""
+    initial_status = {"phase": "Pending"}
+
+
+class JobStrategy(WorkloadStrategy):
+    """`pkg/registry/batch/job/strategy.go`: unless `spec.manualSelector` is true the selector is
+    generated — `controller-uid=<uid>` is added to the selector and `controller-uid` + `job-name`
+    to the template's labels (`generateSelector`), and validation then requires exactly that
+    (`validateGeneratedSelector`)."""
+
+    def prepare_create(self, job):
+        super().prepare_create(job)
+        spec = job.setdefault("spec", {})
+        if spec.get("manualSelector"):
+            return
+        md = job["metadata"]
+        uid = md.get("uid", "")
+        sel = spec["selector"] = dict(spec.get("selector") or {})
+        ml = sel["matchLabels"] = dict(sel.get("matchLabels") or {})
+        ml.setdefault("controller-uid", uid)
+        tpl = spec["template"] = dict(spec.get("template") or {})
+        tmd = tpl["metadata"] = dict(tpl.get("metadata") or {})
+        labels = tmd["labels"] = dict(tmd.get("labels") or {})
+        labels.setdefault("controller-uid", uid)
+        labels.setdefault("job-name", md.get("name", ""))
+
+    def validate(self, job):
+        errs = super().validate(job)
+        spec = job.get("spec") or {}
+        if spec.get("manualSelector"):
+            return errs
+        uid = job["metadata"].get("uid", "")
+        labels = ((spec.get("template") or {}).get("metadata") or {}).get("labels") or {}
+        if labels.get("controller-uid") != uid:
+            errs.append(validation.invalid("spec.template.metadata.labels", "`selector` does not match template `labels`"))
+        if ((spec.get("selector") or {}).get("matchLabels") or {}).get("controller-uid") != uid:
+            errs.append(validation.invalid("spec.selector", "`selector` not auto-generated"))
+        return errs
+
+
+class DeploymentStrategy(WorkloadStrategy):
+    """`pkg/registry/extensions/deployment/strategy.go` PrepareForUpdate: a change of the spec or
+    of the annotations (rollback records there) bumps metadata.generation."""
+    generation_on_annotations = True
+
+
 def qos_class(pod) -> str:
     """`qos.GetPodQOS`."""
     requests, limits, guaranteed = {}, {}, True
@@ -214,6 +273,9 @@ def qos_class(pod) -> str:
 class ServiceStrategy(Strategy):
     """`pkg/registry/core/service/strategy.go`: status subresource (load balancer ingress);
     allocation lives in `service_alloc` (done by the API server before validation)."""
+
+    def prepare_create(self, svc):
+        svc["status"] = {"loadBalancer": {}}
 
     def prepare_update(self, new, old):
         super().prepare_update(new, old)
@@ -244,7 +306,12 @@ STRATEGIES = {"pods": PodStrategy, "services": ServiceStrategy, "nodes": NodeStr
               "controllerrevisions": NoStatusStrategy, "storageclasses": NoStatusStrategy,
               "mutatingwebhookconfigurations": NoStatusStrategy, "validatingwebhookconfigurations": NoStatusStrategy,
               "networkpolicies": NoStatusStrategy, "podsecuritypolicies": NoStatusStrategy,
-              "podpresets": NoStatusStrategy}
+              "podpresets": NoStatusStrategy,
+              "deployments": DeploymentStrategy, "replicasets": WorkloadStrategy, "statefulsets": WorkloadStrategy,
+              "daemonsets": WorkloadStrategy, "replicationcontrollers": WorkloadStrategy, "jobs": JobStrategy,
+              "cronjobs": WorkloadStrategy, "horizontalpodautoscalers": WorkloadStrategy,
+              "poddisruptionbudgets": WorkloadStrategy, "ingresses": WorkloadStrategy,
+              "persistentvolumes": VolumeStrategy, "persistentvolumeclaims": VolumeStrategy}
 
 
 def strategy_for(ri):

@@ -838,7 +838,8 @@ class APIServer:
             strat.prepare_update(obj, old)
             if strat.bump_generation and "generation" in om:
                 if {k: v for k, v in obj.items() if k not in ("metadata", "status")} != \
-                        {k: v for k, v in old.items() if k not in ("metadata", "status")}:
+                        {k: v for k, v in old.items() if k not in ("metadata", "status")} or \
+                        (strat.generation_on_annotations and (nm.get("annotations") or {}) != (om.get("annotations") or {})):
                     nm["generation"] = om["generation"] + 1
         a = adm.Attributes(adm.UPDATE, ri.plural, subresource, namespace, name, obj, old, user, ri.kind)
         self._admit(a)
@@ -1170,6 +1171,9 @@ class APIServer:
                     req.body = codec.dumpb(pb.decode_object(req.body))
                 except pb.ProtobufError as e:
                     raise APIError(415, "UnsupportedMediaType", str(e))
+            if p.startswith("/api/v1/proxy/"):
+                from .subresources import legacy_proxy_path
+                p = legacy_proxy_path(p) or p
             parsed = self._parse_path(p)
             if parsed is None:
                 code = 404
@@ -1289,9 +1293,24 @@ class APIServer:
         if not ok:
             raise APIError(403, "Forbidden", why or "forbidden")
 
+    # subresources this server serves; anything else under a named object is 404, never a write
+    # of the request body to the object itself
+    _SUBRESOURCES = frozenset(("", "status", "binding", "eviction", "log", "exec", "attach", "portforward",
+                               "approval", "finalize", "scale", "rollback"))
+
     async def _dispatch(self, req, ri, ns, name, sub, is_watch, user):
         method = req.method
         q = req.query
+        if sub:
+            from . import subresources as sr
+            if (sub == "proxy" or sub.startswith("proxy/")) and ri.plural in ("pods", "services", "nodes"):
+                return await sr.handle_proxy(self, req, ri, ns, name, sub, user)
+            if sub == "scale" and ri.plural in sr.SCALABLE:
+                return await sr.handle_scale(self, req, ri, ns, name, user)
+            if sub == "rollback" and ri.plural == "deployments" and method == "POST":
+                return await sr.handle_rollback(self, req, ri, ns, name, user)
+            if sub not in self._SUBRESOURCES or sub in ("scale", "rollback"):
+                raise APIError(404, "NotFound", f"the server could not find the requested resource ({req.path})")
         if method in ("GET", "HEAD"):
             if is_watch:
                 self._authorize(user, "watch", ns, ri.plural, sub, name, ri.group, req.path)
@@ -1792,6 +1811,17 @@ class APIServer:
             if self.strategies[ri.plural].has_status:
                 res.append({"name": ri.plural + "/status", "singularName": "", "namespaced": ri.namespaced,
                             "kind": ri.kind, "verbs": ["get", "patch", "update"]})
+            if ri.plural in ("deployments", "replicasets", "statefulsets", "replicationcontrollers"):
+                sgv = "autoscaling/v1" if ri.plural == "replicationcontrollers" or \
+                    f"{group}/{version}" not in ("extensions/v1beta1", "apps/v1beta1", "apps/v1beta2") else f"{group}/{version}"
+                res.append({"name": ri.plural + "/scale", "singularName": "", "namespaced": True, "group": sgv.split("/")[0],
+                            "version": sgv.split("/")[1], "kind": "Scale", "verbs": ["get", "patch", "update"]})
+            if ri.plural == "deployments" and f"{group}/{version}" in ("extensions/v1beta1", "apps/v1beta1"):
+                res.append({"name": "deployments/rollback", "singularName": "", "namespaced": True,
+                            "kind": "DeploymentRollback", "verbs": ["create"]})
+            if ri.plural in ("pods", "services", "nodes"):
+                res.append({"name": ri.plural + "/proxy", "singularName": "", "namespaced": ri.namespaced,
+                            "kind": ri.kind + "ProxyOptions", "verbs": ["create", "delete", "get", "patch", "update"]})
             if ri.plural == "pods":
                 res.append({"name": "pods/binding", "singularName": "", "namespaced": True, "kind": "Binding", "verbs": ["create"]})
                 res.append({"name": "pods/eviction", "singularName": "", "namespaced": True, "kind": "Eviction", "verbs": ["create"]})

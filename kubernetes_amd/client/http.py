@@ -114,6 +114,12 @@ class HTTPClient:
         return (h + "\r\n").encode()
 
     async def request(self, method, path, body: bytes | None = None, content_type="application/json", headers=None):
+        status, _hdrs, data = await self.request_full(method, path, body, content_type, headers)
+        return status, data
+
+    async def request_full(self, method, path, body: bytes | None = None, content_type="application/json",
+                           headers=None):
+        """Like request(), also returning the response headers (lower-case names)."""
         async with self._sem:
             for attempt in range(2):
                 conn = self._idle.pop() if self._idle else None
@@ -136,7 +142,7 @@ class HTTPClient:
                     conn.close()
                 else:
                     self._idle.append(conn)
-                return status, data
+                return status, hdrs, data
 
     async def open_raw(self, method, path, headers=None, body=None):
         """Send one request on a dedicated connection and return (status, headers, reader,

@@ -175,15 +175,19 @@ class DeploymentController(Controller):
             target = revs[-2] if len(revs) >= 2 else None
         else:
             target = next((r for r in rss if (r["metadata"].get("annotations") or {}).get(REVISION) == str(revision)), None)
-        patch = {"spec": {"rollbackTo": None}}
+        # the template is replaced as a whole (a merge patch would keep labels the target lacks),
+        # guarded by the resourceVersion the decision was made on
+        ops = [{"op": "test", "path": "/metadata/resourceVersion", "value": d["metadata"]["resourceVersion"]},
+               {"op": "remove", "path": "/spec/rollbackTo"}]
         if target is not None:
             t = m.fast_copy((target.get("spec") or {}).get("template") or {})
             (t.get("metadata") or {}).get("labels", {}).pop(HASH_LABEL, None)
-            patch["spec"]["template"] = t
-            self.recorder.event(d, "Normal", "DeploymentRollback", f"Rolled back deployment to revision {revision}")
+            ops.append({"op": "replace", "path": "/spec/template", "value": t})
+            rev = (target["metadata"].get("annotations") or {}).get(REVISION, str(revision))
+            self.recorder.event(d, "Normal", "DeploymentRollback", f"Rolled back deployment {d['metadata']['name']} to revision {rev}")
         else:
-            self.recorder.event(d, "Warning", "DeploymentRollbackRevisionNotFound", f"Unable to find revision {revision}")
-        await self.client.patch("deployments", d["metadata"]["name"], patch, d["metadata"]["namespace"])
+            self.recorder.event(d, "Warning", "DeploymentRollbackRevisionNotFound", "Unable to find the revision to rollback to.")
+        await self.client.patch("deployments", d["metadata"]["name"], ops, d["metadata"]["namespace"], "json")
 
     async def _status(self, d, new_rs, old):
         allrs = [new_rs] + old

@@ -12,7 +12,8 @@ Parity: `pkg/controller/podautoscaler/horizontal.go` + `replica_calculator.go`:
     clamped to [minReplicas (default 1), maxReplicas]; no rescale inside the up-/down-scale
     forbidden windows (3 min / 5 min) after `lastScaleTime` (`shouldScale` :553-575);
   * status: currentReplicas, desiredReplicas, currentCPUUtilizationPercentage, lastScaleTime;
-  * scaling writes `spec.replicas` of the target (Deployment, ReplicaSet, RC, StatefulSet).
+  * the target is read and scaled through its `scale` subresource (autoscaling/v1 Scale:
+    replicas + selector string), as `horizontal.go` does with its ScaleNamespacer.
 Metrics come from `metrics.k8s.io/v1beta1` PodMetrics through the API server (metrics-server).
 MI355X: the resource name `amd.com/gpu` scales on GPU utilization — the per-pod GPU duty cycle
 in percent, so `targetAverageUtilization: 70` keeps the pods' MI355Xs ~70 % busy.
@@ -24,7 +25,7 @@ import json
 import math
 import time
 
-from ..api.labels import label_selector_as_selector
+from ..api.labels import parse as parse_labels, selector_to_string
 from ..api.meta import now_rfc3339, parse_rfc3339
 from ..api.quantity import parse_quantity
 from ..client.rest import APIStatusError
@@ -35,25 +36,7 @@ TARGETS = {"Deployment": "deployments", "ReplicaSet": "replicasets", "Replicatio
 GPU = "amd.com/gpu"
 
 
-def selector_string(sel):
-    """LabelSelector -> query string."""
-    if not sel:
-        return ""
-    if "matchLabels" not in sel and "matchExpressions" not in sel:
-        sel = {"matchLabels": sel}
-    parts = [f"{k}={v}" for k, v in sorted((sel.get("matchLabels") or {}).items())]
-    for e in sel.get("matchExpressions") or ():
-        op = e.get("operator")
-        vals = ",".join(e.get("values") or ())
-        if op == "In":
-            parts.append(f"{e['key']} in ({vals})")
-        elif op == "NotIn":
-            parts.append(f"{e['key']} notin ({vals})")
-        elif op == "Exists":
-            parts.append(e["key"])
-        elif op == "DoesNotExist":
-            parts.append(f"!{e['key']}")
-    return ",".join(parts)
+selector_string = selector_to_string
 
 
 def utilization_replicas(current, target_util, usage, requests, ready, unready, missing, tolerance):
@@ -141,15 +124,16 @@ class HorizontalController(Controller):
             self.recorder.event(hpa, "Warning", "FailedGetScale", f"unsupported scale target kind {ref.get('kind')}")
             return
         try:
-            target = await self.client.get(plural, ref.get("name"), ns)
+            scale = await self.client.get(plural, ref.get("name"), ns, subresource="scale")
         except APIStatusError as e:
             self.recorder.event(hpa, "Warning", "FailedGetScale", str(e))
             return
-        current = int((target.get("spec") or {}).get("replicas", 1))
-        sel_obj = (target.get("spec") or {}).get("selector")
-        sel_str = selector_string(sel_obj)
-        sel = label_selector_as_selector(sel_obj if sel_obj and ("matchLabels" in sel_obj or "matchExpressions" in sel_obj)
-                                         else {"matchLabels": sel_obj or {}})
+        current = int((scale.get("spec") or {}).get("replicas", 1))
+        sel_str = (scale.get("status") or {}).get("selector") or ""
+        if not sel_str:
+            self.recorder.event(hpa, "Warning", "SelectorRequired", "selector is required")
+            return
+        sel = parse_labels(sel_str)
         pods = [p for p in self.pod_inf.list() if p["metadata"].get("namespace") == ns and
                 sel.matches(p["metadata"].get("labels") or {}) and not p["metadata"].get("deletionTimestamp")
                 and (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
@@ -189,7 +173,12 @@ class HorizontalController(Controller):
         if cpu_util is not None:
             new_st["currentCPUUtilizationPercentage"] = cpu_util
         if rescale:
-            await self.client.patch(plural, ref["name"], {"spec": {"replicas": desired}}, ns)
+            scale["spec"] = {"replicas": desired}
+            try:
+                await self.client.update(plural, scale, ns, subresource="scale")
+            except APIStatusError as e:
+                self.recorder.event(hpa, "Warning", "FailedRescale", f"New size: {desired}; error: {e}")
+                raise
             self.recorder.event(hpa, "Normal", "SuccessfulRescale", f"New size: {desired}; reason: metric above/below target")
             new_st["lastScaleTime"] = now_rfc3339()
             new_st["currentReplicas"] = current

@@ -325,10 +325,28 @@ class Kubectl(extra.ExtraCommands):
         self.p(f"{ri.kind.lower()}/{name} patched")
 
     async def cmd_scale(self):
+        """`kubectl scale` (pkg/kubectl/scale.go): through the scale subresource, with the
+        --current-replicas / --resource-version preconditions checked against the Scale; Jobs
+        (parallelism) are patched directly."""
         a = self.a
         for ri, name in split_targets(a.targets):
-            await self.client.patch(ri.plural, name, {"spec": {"replicas": a.replicas}}, self.ns)
-            self.p(f"{ri.kind.lower()}/{name} scaled")
+            if ri.plural == "jobs":
+                job = await self.client.get("jobs", name, self.ns)
+                cur = (job.get("spec") or {}).get("parallelism", 1)
+                if a.current_replicas is not None and a.current_replicas != cur:
+                    raise SystemExit(f"error: Expected replicas to be {a.current_replicas}, was {cur}")
+                await self.client.patch("jobs", name, {"spec": {"parallelism": a.replicas}}, self.ns)
+            else:
+                scale = await self.client.get(ri.plural, name, self.ns, subresource="scale")
+                cur = (scale.get("spec") or {}).get("replicas", 0)
+                if a.current_replicas is not None and a.current_replicas != cur:
+                    raise SystemExit(f"error: Expected replicas to be {a.current_replicas}, was {cur}")
+                if a.resource_version and a.resource_version != scale["metadata"].get("resourceVersion"):
+                    raise SystemExit(f"error: Expected resourceVersion to be {a.resource_version}, "
+                                     f"was {scale['metadata'].get('resourceVersion')}")
+                scale["spec"] = {"replicas": a.replicas}
+                await self.client.update(ri.plural, scale, self.ns, subresource="scale")
+            self.p(f"{ri.kind.lower()} \"{name}\" scaled")
 
     async def _cordon(self, name, flag):
         await self.client.patch("nodes", name, {"spec": {"unschedulable": flag or None}})
@@ -483,7 +501,13 @@ class Kubectl(extra.ExtraCommands):
             rows = sorted([[int((r["metadata"].get("annotations") or {}).get("deployment.kubernetes.io/revision", 0)), "<none>"] for r in rss])
             self.p(printers.table(rows, ["REVISION", "CHANGE-CAUSE"]))
         elif a.action == "undo":
-            await self.client.patch(ri.plural, name, {"spec": {"rollbackTo": {"revision": a.to_revision}}}, self.ns)
+            # DeploymentRollbacker: the extensions/v1beta1 rollback subresource
+            body = {"kind": "DeploymentRollback", "apiVersion": "extensions/v1beta1", "name": name,
+                    "rollbackTo": {"revision": a.to_revision or 0}}
+            st, resp = await self.client.raw("POST", f"/apis/extensions/v1beta1/namespaces/{self.ns}/deployments/{name}/rollback",
+                                             json.dumps(body).encode())
+            if st != 200:
+                raise SystemExit(f"error: {resp.decode(errors='replace')}")
             self.p(f"deployment.apps/{name} rolled back")
 
     async def cmd_run(self):
@@ -914,6 +938,8 @@ def build_parser():
     sc = add("scale")
     sc.add_argument("targets", nargs="+")
     sc.add_argument("--replicas", type=int, required=True)
+    sc.add_argument("--current-replicas", type=int, default=None)
+    sc.add_argument("--resource-version", default="")
     for name in ("cordon", "uncordon"):
         add(name).add_argument("node")
     dr = add("drain")

@@ -96,6 +96,8 @@ def test_deployment_scale_rollout(cluster, tmp_path):
     rc, out = k(cluster, "rollout", "status", "deployment/svc", "--timeout", "30")
     assert "successfully rolled out" in out
     assert k(cluster, "scale", "deployment", "svc", "--replicas", "3")[0] == 0
+    with pytest.raises(SystemExit, match="Expected replicas to be 7, was 3"):   # --current-replicas precondition
+        k(cluster, "scale", "deployment", "svc", "--current-replicas", "7", "--replicas", "1")
     rc, out = k(cluster, "rollout", "status", "deployment/svc", "--timeout", "30")
     assert "successfully rolled out" in out
     d["spec"]["template"]["metadata"]["labels"]["v"] = "2"
@@ -106,6 +108,14 @@ def test_deployment_scale_rollout(cluster, tmp_path):
     wait(lambda: "2" in k(cluster, "rollout", "history", "deployment/svc")[1])
     rc, out = k(cluster, "get", "deploy")
     assert "svc" in out
+    # undo through the rollback subresource: the controller restores revision 1's template
+    rc, out = k(cluster, "rollout", "undo", "deployment/svc")
+    assert rc == 0 and "rolled back" in out
+
+    def restored():
+        d = json.loads(k(cluster, "get", "deployment", "svc", "-o", "json")[1])
+        return "v" not in d["spec"]["template"]["metadata"]["labels"] and not d["spec"].get("rollbackTo")
+    wait(restored)
 
 
 def test_cordon_taint_drain(cluster):
