@@ -1,6 +1,6 @@
-"""`kubeadm` command line: init, join, token, reset, config, phase, version.
+"""`kubeadm` command line: init, join, token, reset, upgrade, config, phase, version.
 
-Parity: `cmd/kubeadm/app/cmd/{init,join,token,reset,config,version}.go` and `cmd/phases/*` (each
+Parity: `cmd/kubeadm/app/cmd/{init,join,token,reset,config,version}.go`, `cmd/upgrade/*` and `cmd/phases/*` (each
 init phase is runnable on its own as `kubeadm phase <name>`).
 """
 from __future__ import annotations
@@ -222,6 +222,41 @@ def cmd_phase(a):
     return 0
 
 
+def cmd_upgrade(a):
+    """`kubeadm upgrade plan|apply` (kubeadm/upgrade.py)."""
+    from . import upgrade as U
+
+    def confirm():
+        if a.yes:
+            return True
+        ans = input("[upgrade/confirm] Are you sure you want to proceed with the upgrade? [y/N]: ")
+        return ans.strip().lower() in ("y", "yes")
+
+    async def go():
+        c = clientcmd.client_from(a.kubeconfig)
+        try:
+            cfg = await U.fetch_config(c, a.config)
+            if a.op == "plan":
+                if not a.skip_preflight_checks:
+                    errs = await U.health_checks(c, cfg)
+                    if errs:
+                        raise U.UpgradeError("[upgrade/health] FATAL: " + "; ".join(errs))
+                await U.plan(c, cfg)
+            else:
+                await U.apply(c, cfg, a.version, force=a.force, dry_run=a.dry_run,
+                              allow_experimental=a.allow_experimental_upgrades,
+                              allow_rc=a.allow_release_candidate_upgrades, skip_preflight=a.skip_preflight_checks,
+                              timeout=a.timeout, confirm=confirm)
+        finally:
+            await c.close()
+    try:
+        asyncio.run(go())
+    except U.UpgradeError as e:
+        print(str(e), file=sys.stderr)
+        return 1
+    return 0
+
+
 def _common(p):
     p.add_argument("--config", default=None, help="MasterConfiguration YAML")
     p.add_argument("--kubernetes-dir", default=None)
@@ -277,6 +312,21 @@ def main(argv=None):
     p.add_argument("phase", choices=["preflight", "certs", "kubeconfig", "controlplane", "upload-config", "mark-master",
                                      "bootstrap-token", "addons"])
     _common(p)
+    p = sub.add_parser("upgrade")
+    usub = p.add_subparsers(dest="op", required=True)
+    for op in ("plan", "apply"):
+        q = usub.add_parser(op)
+        if op == "apply":
+            q.add_argument("version")
+            q.add_argument("-f", "--force", action="store_true")
+            q.add_argument("-y", "--yes", action="store_true")
+            q.add_argument("--dry-run", action="store_true")
+            q.add_argument("--timeout", type=float, default=300.0, help="seconds to wait for each static pod")
+        q.add_argument("--config", default=None)
+        q.add_argument("--kubeconfig", default="/etc/kubernetes/admin.conf")
+        q.add_argument("--allow-experimental-upgrades", action="store_true")
+        q.add_argument("--allow-release-candidate-upgrades", action="store_true")
+        q.add_argument("--skip-preflight-checks", action="store_true")
     p = sub.add_parser("config")
     p.add_argument("op", choices=["view", "print-default"])
     p.add_argument("--kubeconfig", default="/etc/kubernetes/admin.conf")
@@ -297,6 +347,8 @@ def main(argv=None):
         return 0
     if a.cmd == "phase":
         return cmd_phase(a)
+    if a.cmd == "upgrade":
+        return cmd_upgrade(a)
     if a.cmd == "config":
         if a.op == "print-default":
             print(yaml.safe_dump(P.default_config(), sort_keys=False))

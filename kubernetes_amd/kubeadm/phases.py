@@ -164,7 +164,7 @@ def phase_kubeconfig(cfg):
 
 
 # ------------------------------------------------------------------------------------ manifests
-def _static_pod(name, command, host_paths=()):
+def _static_pod(name, command, host_paths=(), version=VERSION):
     vols, mounts = [], []
     for i, p in enumerate(host_paths):
         vols.append({"name": f"v{i}", "hostPath": {"path": p, "type": "DirectoryOrCreate"}})
@@ -173,7 +173,7 @@ def _static_pod(name, command, host_paths=()):
             "metadata": {"name": name, "namespace": "kube-system", "labels": {"component": name, "tier": "control-plane"},
                          "annotations": {"scheduler.alpha.kubernetes.io/critical-pod": ""}},
             "spec": {"hostNetwork": True, "priorityClassName": "system-cluster-critical",
-                     "containers": [{"name": name, "image": f"kubernetes-amd/hyperkube:{VERSION}", "command": command,
+                     "containers": [{"name": name, "image": f"kubernetes-amd/hyperkube:{version}", "command": command,
                                      "volumeMounts": mounts,
                                      "livenessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz",
                                                                    "port": 0}, "initialDelaySeconds": 15,
@@ -197,9 +197,10 @@ def control_plane_manifests(cfg):
                "--cluster-signing-cert-file", os.path.join(d, "ca.crt"), "--cluster-signing-key-file", os.path.join(d, "ca.key"),
                "--controllers", "*,bootstrapsigner,tokencleaner"]
     sched = py + ["kubernetes_amd.cmd.scheduler", "--kubeconfig", os.path.join(kd, SCHED_CONF), "--leader-elect"]
-    out = {"kube-apiserver": _static_pod("kube-apiserver", api, (d, cfg["etcd"]["dataDir"])),
-           "kube-controller-manager": _static_pod("kube-controller-manager", cm, (d, kd)),
-           "kube-scheduler": _static_pod("kube-scheduler", sched, (kd,))}
+    v = cfg.get("kubernetesVersion") or VERSION
+    out = {"kube-apiserver": _static_pod("kube-apiserver", api, (d, cfg["etcd"]["dataDir"]), v),
+           "kube-controller-manager": _static_pod("kube-controller-manager", cm, (d, kd), v),
+           "kube-scheduler": _static_pod("kube-scheduler", sched, (kd,), v)}
     return out
 
 
@@ -274,6 +275,11 @@ async def phase_bootstrap_token(client, cfg, token):
     await _ensure(client, "secrets", token_secret(token, parse_ttl(cfg.get("tokenTTL", "24h")),
                                                   description="The default bootstrap token generated by 'kubeadm init'."),
                   "kube-system")
+    await phase_bootstrap_token_rbac(client)
+
+
+async def phase_bootstrap_token_rbac(client):
+    """RBAC for bootstrap tokens: post CSRs, auto-approve node client CSRs and their rotation."""
     rb = lambda name, role, group: {"metadata": {"name": name},  # noqa: E731
                                     "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": role},
                                     "subjects": [{"kind": "Group", "name": group, "apiGroup": "rbac.authorization.k8s.io"}]}
@@ -315,9 +321,11 @@ async def phase_mark_master(client, node_name):
                                             "spec": {"taints": taints}})
 
 
-async def phase_addons(client, cfg):
-    """kube-proxy (ConfigMap + DaemonSet + its RBAC) and the amd.com/gpu device plugin DaemonSet."""
+async def phase_addons(client, cfg, update=False):
+    """kube-proxy (ConfigMap + DaemonSet + its RBAC) and the amd.com/gpu device plugin DaemonSet;
+    `update` replaces existing DaemonSets (kubeadm upgrade moves them to the new version)."""
     py = [sys.executable, "-m"]
+    version = cfg.get("kubernetesVersion") or VERSION
     await _ensure(client, "serviceaccounts", {"metadata": {"name": "kube-proxy", "namespace": "kube-system"}}, "kube-system")
     await _ensure(client, "clusterrolebindings", {"metadata": {"name": "kubeadm:node-proxier"},
                                                   "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
@@ -335,15 +343,15 @@ async def phase_addons(client, cfg):
                                                           "spec": {"hostNetwork": True, "serviceAccountName": name,
                                                                    "tolerations": [{"key": "node-role.kubernetes.io/master",
                                                                                     "effect": "NoSchedule"}],
-                                                                   "containers": [{"name": name, "image": f"kubernetes-amd/hyperkube:{VERSION}",
+                                                                   "containers": [{"name": name, "image": f"kubernetes-amd/hyperkube:{version}",
                                                                                    "command": cmd}]}}}}
     await _ensure(client, "daemonsets", ds("kube-proxy", py + ["kubernetes_amd.cmd.proxy", "--kubeconfig",
                                                                "/var/lib/kube-proxy/kubeconfig.conf"], {"k8s-app": "kube-proxy"}),
-                  "kube-system")
+                  "kube-system", update=update)
     await _ensure(client, "serviceaccounts", {"metadata": {"name": "amd-gpu-device-plugin", "namespace": "kube-system"}},
                   "kube-system")
     await _ensure(client, "daemonsets", ds("amd-gpu-device-plugin", py + ["kubernetes_amd.cmd.device_plugin"],
-                                           {"k8s-app": "amd-gpu-device-plugin"}), "kube-system")
+                                           {"k8s-app": "amd-gpu-device-plugin"}), "kube-system", update=update)
 
 
 # ------------------------------------------------------------------------------------ join
