@@ -198,7 +198,12 @@ def cmd_phase(a):
     elif a.phase == "kubeconfig":
         print("\n".join(P.phase_kubeconfig(cfg)))
     elif a.phase == "controlplane":
-        print("\n".join(P.phase_manifests(cfg)))
+        print("\n".join(p for p in P.phase_manifests(cfg) if not p.endswith("/etcd.yaml")))
+    elif a.phase == "etcd":
+        if cfg["etcd"].get("endpoints"):
+            print("external store configured (etcd.endpoints): no local etcd manifest")
+        else:
+            print(P.phase_etcd_local(cfg))
     else:
         admin = os.path.join(cfg["kubernetesDir"], P.ADMIN_CONF)
 
@@ -309,8 +314,8 @@ def main(argv=None):
     p = sub.add_parser("reset")
     _common(p)
     p = sub.add_parser("phase")
-    p.add_argument("phase", choices=["preflight", "certs", "kubeconfig", "controlplane", "upload-config", "mark-master",
-                                     "bootstrap-token", "addons"])
+    p.add_argument("phase", choices=["preflight", "certs", "kubeconfig", "etcd", "controlplane", "upload-config",
+                                     "mark-master", "bootstrap-token", "addons"])
     _common(p)
     p = sub.add_parser("upgrade")
     usub = p.add_subparsers(dest="op", required=True)

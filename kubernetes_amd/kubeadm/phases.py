@@ -181,9 +181,29 @@ def _static_pod(name, command, host_paths=(), version=VERSION):
                      "volumes": vols}}
 
 
+def etcd_socket(cfg):
+    return os.path.join(cfg["etcd"]["dataDir"], "kamd-etcd.sock")
+
+
+def etcd_manifest(cfg):
+    """Local store static pod (`phases/etcd/local.go` CreateLocalEtcdStaticPodManifestFile): the
+    native kamd-etcd on a unix socket in its data dir, WAL beside it; skipped when
+    `etcd.endpoints` names an external store."""
+    from ..api.protobuf import SCHEMA_PATH
+    from ..native import BIN_DIR
+    data = cfg["etcd"]["dataDir"]
+    cmd = [os.path.join(BIN_DIR, "kamd-etcd"), "--listen-unix", etcd_socket(cfg), "--wal", os.path.join(data, "wal"),
+           "--pb-schema", SCHEMA_PATH]
+    pod = _static_pod("etcd", cmd, (data,), cfg.get("kubernetesVersion") or VERSION)
+    pod["spec"]["containers"][0].pop("livenessProbe", None)   # no HTTP endpoint: the kubelet restarts it on exit
+    return pod
+
+
 def control_plane_manifests(cfg):
     d, kd = cfg["certificatesDir"], cfg["kubernetesDir"]
     py = [sys.executable, "-m"]
+    external = list(cfg["etcd"].get("endpoints") or ())
+    store = ["--etcd-servers", external[0]] if external else ["--etcd-servers", "unix://" + etcd_socket(cfg)]
     api = py + ["kubernetes_amd.cmd.apiserver", "--bind-address", cfg["api"]["advertiseAddress"],
                 "--port", str(cfg["api"]["bindPort"]),
                 "--tls-cert-file", os.path.join(d, "apiserver.crt"), "--tls-private-key-file", os.path.join(d, "apiserver.key"),
@@ -191,7 +211,7 @@ def control_plane_manifests(cfg):
                 "--enable-bootstrap-token-auth", "--authorization-mode", ",".join(cfg["authorizationModes"]),
                 "--admission-control", ",".join(DEFAULT_ADMISSION),
                 "--service-cluster-ip-range", cfg["networking"]["serviceSubnet"],
-                "--etcd-wal", os.path.join(cfg["etcd"]["dataDir"], "wal"), "--storage-media-type", "application/vnd.kubernetes.protobuf"]
+                "--storage-media-type", "application/vnd.kubernetes.protobuf"] + store
     cm = py + ["kubernetes_amd.cmd.controller_manager", "--kubeconfig", os.path.join(kd, CM_CONF), "--leader-elect",
                "--service-account-private-key-file", os.path.join(d, "sa.key"), "--root-ca-file", os.path.join(d, "ca.crt"),
                "--cluster-signing-cert-file", os.path.join(d, "ca.crt"), "--cluster-signing-key-file", os.path.join(d, "ca.key"),
@@ -201,7 +221,16 @@ def control_plane_manifests(cfg):
     out = {"kube-apiserver": _static_pod("kube-apiserver", api, (d, cfg["etcd"]["dataDir"]), v),
            "kube-controller-manager": _static_pod("kube-controller-manager", cm, (d, kd), v),
            "kube-scheduler": _static_pod("kube-scheduler", sched, (kd,), v)}
+    if not external:
+        out["etcd"] = etcd_manifest(cfg)
     return out
+
+
+def phase_etcd_local(cfg):
+    mdir = os.path.join(cfg["kubernetesDir"], "manifests")
+    path = os.path.join(mdir, "etcd.yaml")
+    _write(path, yaml.safe_dump(etcd_manifest(cfg), sort_keys=False))
+    return path
 
 
 def phase_manifests(cfg):

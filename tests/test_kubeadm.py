@@ -12,6 +12,7 @@ import yaml
 
 from kubernetes_amd.apiserver.server import APIServer
 from kubernetes_amd.client import clientcmd
+from kubernetes_amd.client.rest import Client
 from kubernetes_amd.controllers.manager import ControllerManager
 from kubernetes_amd.kubeadm import cli, phases as P
 from kubernetes_amd.native import crypto
@@ -61,6 +62,15 @@ def test_phases_offline(tmp_path):
     adm = cmd[cmd.index("--admission-control") + 1].split(",")
     assert "ResourceV2" in adm and adm.index("NodeRestriction") < adm.index("ResourceQuota")
     assert api["spec"]["hostNetwork"] and api["metadata"]["namespace"] == "kube-system"
+    # local store static pod; the API server joins it over its unix socket
+    etcd = yaml.safe_load(open([f for f in files if f.endswith("etcd.yaml")][0]))
+    ecmd = etcd["spec"]["containers"][0]["command"]
+    assert ecmd[0].endswith("kamd-etcd") and ecmd[ecmd.index("--wal") + 1] == str(tmp_path / "etcd" / "wal")
+    assert cmd[cmd.index("--etcd-servers") + 1] == "unix://" + ecmd[ecmd.index("--listen-unix") + 1]
+    ext = P.control_plane_manifests(dict(cfg, etcd={"dataDir": "/x", "endpoints": ["tcp://10.0.0.5:2379"]}))
+    assert "etcd" not in ext
+    ecmd_api = ext["kube-apiserver"]["spec"]["containers"][0]["command"]
+    assert ecmd_api[ecmd_api.index("--etcd-servers") + 1] == "tcp://10.0.0.5:2379"
 
     tok = P.generate_token()
     assert len(tok) == 23 and tok[6] == "."
@@ -164,3 +174,65 @@ def test_init_join_tls_bootstrap(run, tmp_path):
             await s.stop()
 
     run(main(), timeout=90)
+
+
+def test_local_etcd_manifest_runs(tmp_path):
+    """The etcd and API server manifests' commands work together: objects written through the
+    API server survive its restart because they live in the separate store process."""
+    import subprocess
+    import sys
+    import time
+    from kubernetes_amd.native import BIN_DIR
+    if not os.path.exists(os.path.join(BIN_DIR, "kamd-etcd")):
+        pytest.skip("kamd-etcd not built")
+    cfg = _cfg(tmp_path, 0)
+    (tmp_path / "etcd").mkdir()
+    m = P.control_plane_manifests(cfg)
+    store = subprocess.Popen(m["etcd"]["spec"]["containers"][0]["command"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    api_cmd = m["kube-apiserver"]["spec"]["containers"][0]["command"]
+    srv = api_cmd[api_cmd.index("--etcd-servers") + 1]
+    procs = [store]
+    try:
+        sock = srv[len("unix://"):]
+        for _ in range(100):
+            if os.path.exists(sock):
+                break
+            time.sleep(0.05)
+
+        def api():
+            pf = tmp_path / "port"
+            if pf.exists():
+                pf.unlink()
+            p = subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", str(pf),
+                                  "--etcd-servers", srv], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            procs.append(p)
+            for _ in range(600):
+                if pf.exists() and pf.read_text().strip():
+                    return p, f"http://127.0.0.1:{pf.read_text().strip()}"
+                time.sleep(0.05)
+            raise TimeoutError("apiserver did not start")
+
+        async def put(url):
+            c = Client(url)
+            try:
+                await c.create("configmaps", {"metadata": {"name": "kept", "namespace": "default"}, "data": {"a": "1"}})
+            finally:
+                await c.close()
+
+        async def get(url):
+            c = Client(url)
+            try:
+                return (await c.get("configmaps", "kept", "default"))["data"]
+            finally:
+                await c.close()
+        p1, url = api()
+        asyncio.run(put(url))
+        p1.terminate()
+        p1.wait(10)
+        p2, url = api()
+        assert asyncio.run(get(url)) == {"a": "1"}
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            p.wait(10)
