@@ -658,3 +658,65 @@ async def security_context_non_root(f):
         return None
     w = await f.wait(refused, 30, "CreateContainerConfigError")
     assert "non-root" in w.get("message", ""), w
+
+
+@conformance("Deployment should be scaled through the scale subresource")
+async def deployment_scale_subresource(f):
+    """`test/e2e/apps/deployment.go` scale via the autoscaling/v1 Scale of a deployment."""
+    d = {"metadata": {"name": "sc"}, "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "sc"}},
+         "template": {"metadata": {"labels": {"app": "sc"}}, "spec": {"containers": [
+             {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("deployments", d, f.ns)
+    scale = await f.client.get("deployments", "sc", f.ns, subresource="scale")
+    assert scale["kind"] == "Scale" and scale["spec"]["replicas"] == 1 and scale["status"]["selector"] == "app=sc"
+    scale["spec"] = {"replicas": 3}
+    await f.client.update("deployments", scale, f.ns, subresource="scale")
+
+    async def three():
+        pods = [p for p in (await f.client.list("pods", f.ns, label_selector="app=sc"))["items"]
+                if not p["metadata"].get("deletionTimestamp")]
+        return pods if len(pods) == 3 else None
+    await f.wait(three, 60, "3 replicas after scaling through the subresource")
+    got = await f.client.get("deployments", "sc", f.ns, subresource="scale")
+    assert got["spec"]["replicas"] == 3
+
+
+@conformance("Deployment should roll back to the previous template through the rollback subresource")
+async def deployment_rollback(f):
+    """`test/e2e/apps/deployment.go` testRollbackDeployment: a DeploymentRollback restores the
+    previous revision's template."""
+    d = {"metadata": {"name": "rb"}, "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "rb"}},
+         "template": {"metadata": {"labels": {"app": "rb"}}, "spec": {"containers": [
+             {"name": "c", "image": BUSYBOX, "command": ["sh", "-c", "sleep 3600"]}]}}}}
+    await f.client.create("deployments", d, f.ns)
+
+    async def revision(n):
+        rss = (await f.client.list("replicasets", f.ns, label_selector="app=rb"))["items"]
+        revs = {(r["metadata"].get("annotations") or {}).get("deployment.kubernetes.io/revision") for r in rss}
+        return rss if str(n) in revs else None
+    await f.wait(lambda: revision(1), 60, "revision 1")
+    await f.client.patch("deployments", "rb", {"spec": {"template": {"metadata": {"labels": {"app": "rb", "v": "2"}}}}}, f.ns)
+    await f.wait(lambda: revision(2), 60, "revision 2")
+    st, body = await f.client.raw("POST", f"/apis/extensions/v1beta1/namespaces/{f.ns}/deployments/rb/rollback",
+                                  b'{"kind":"DeploymentRollback","apiVersion":"extensions/v1beta1","name":"rb",'
+                                  b'"rollbackTo":{"revision":0}}')
+    assert st == 200, body
+
+    async def rolled_back():
+        cur = await f.client.get("deployments", "rb", f.ns)
+        labels = cur["spec"]["template"]["metadata"]["labels"]
+        return cur if "v" not in labels and not cur["spec"].get("rollbackTo") else None
+    await f.wait(rolled_back, 60, "template of revision 1 restored")
+
+
+@conformance("Proxy should proxy to the kubelet through the node proxy subresource")
+async def node_proxy(f):
+    """`test/e2e/network/proxy.go` "should proxy logs on node using proxy subresource": the API
+    server relays to the node's kubelet endpoint."""
+    nodes = (await f.client.list("nodes"))["items"]
+    assert nodes, "no nodes"
+    node = nodes[0]["metadata"]["name"]
+    st, body = await f.client.raw("GET", f"/api/v1/nodes/{node}/proxy/healthz")
+    assert st == 200 and body.strip() == b"ok", (st, body[:200])
+    st, body = await f.client.raw("GET", f"/api/v1/proxy/nodes/{node}/healthz")     # deprecated form
+    assert st == 200 and body.strip() == b"ok", (st, body[:200])
