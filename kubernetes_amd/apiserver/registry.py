@@ -118,6 +118,11 @@ class Strategy:
         """0 = delete immediately."""
         return 0
 
+    def export(self, obj):
+        """`?export=true` without `exact`: strip cluster-specific state (the reference falls back
+        to PrepareForCreate when a kind has no ExportStrategy)."""
+        self.prepare_create(obj)
+
 
 class PodStrategy(Strategy):
     def prepare_create(self, pod):
@@ -164,6 +169,13 @@ class PodStrategy(Strategy):
                     errs.append(validation.FieldError("Forbidden", f"spec.{key}", "pod updates may only change the image"))
         return errs
 
+    def export(self, pod):
+        self.prepare_create(pod)
+        spec = pod.get("spec") or {}
+        spec.pop("nodeName", None)                      # where it ran, and which devices, is cluster state
+        for er in spec.get("extendedResources") or ():
+            er.pop("assigned", None)
+
     def graceful_seconds(self, pod, opts):
         spec = pod.get("spec") or {}
         if not spec.get("nodeName") or core.pod_is_terminal(pod):
@@ -190,6 +202,15 @@ class NamespaceStrategy(Strategy):
 
 class NoStatusStrategy(Strategy):
     has_status = False
+
+
+class SecretStrategy(NoStatusStrategy):
+    def export(self, secret):
+        """Service-account token secrets are minted per cluster: exported without their data."""
+        ann = (secret.get("metadata") or {}).get("annotations") or {}
+        if secret.get("type") == "kubernetes.io/service-account-token" or ann.get("kubernetes.io/service-account.uid"):
+            secret.pop("data", None)
+            ann.pop("kubernetes.io/service-account.uid", None)
 
 
 class WorkloadStrategy(Strategy):
@@ -288,6 +309,15 @@ class ServiceStrategy(Strategy):
                 if not p.get("nodePort") and old_np.get((p.get("port"), p.get("protocol", "TCP"))):
                     p["nodePort"] = old_np[(p.get("port"), p.get("protocol", "TCP"))]
 
+    def export(self, svc):
+        """`svcStrategy.Export`: drop the allocated cluster IP (unless headless) and node ports."""
+        spec = svc.get("spec") or {}
+        if spec.get("clusterIP") and spec["clusterIP"] != "None":
+            spec.pop("clusterIP")
+        if spec.get("type") == "NodePort":
+            for p in spec.get("ports") or ():
+                p.pop("nodePort", None)
+
     def validate(self, obj):
         from .service_alloc import validate_service
         return validate_service(obj)
@@ -298,7 +328,7 @@ class ServiceStrategy(Strategy):
 
 
 STRATEGIES = {"pods": PodStrategy, "services": ServiceStrategy, "nodes": NodeStrategy, "namespaces": NamespaceStrategy,
-              "events": NoStatusStrategy, "configmaps": NoStatusStrategy, "secrets": NoStatusStrategy,
+              "events": NoStatusStrategy, "configmaps": NoStatusStrategy, "secrets": SecretStrategy,
               "serviceaccounts": NoStatusStrategy, "endpoints": NoStatusStrategy,
               "limitranges": NoStatusStrategy, "priorityclasses": NoStatusStrategy,
               "leases": NoStatusStrategy, "roles": NoStatusStrategy, "rolebindings": NoStatusStrategy,
@@ -312,6 +342,21 @@ STRATEGIES = {"pods": PodStrategy, "services": ServiceStrategy, "nodes": NodeStr
               "cronjobs": WorkloadStrategy, "horizontalpodautoscalers": WorkloadStrategy,
               "poddisruptionbudgets": WorkloadStrategy, "ingresses": WorkloadStrategy,
               "persistentvolumes": VolumeStrategy, "persistentvolumeclaims": VolumeStrategy}
+
+
+def export_object(strat, obj, exact=False):
+    """`genericregistry.Store.Export` + `exportObjectMeta`."""
+    from ..api.meta import fast_copy
+    out = fast_copy(obj)
+    md = out.setdefault("metadata", {})
+    for k in ("uid", "creationTimestamp", "deletionTimestamp", "resourceVersion", "selfLink"):
+        md.pop(k, None)
+    if not exact:
+        md.pop("namespace", None)
+        if md.get("generateName"):
+            md.pop("name", None)
+        strat.export(out)
+    return out
 
 
 def strategy_for(ri):

@@ -1328,14 +1328,18 @@ class APIServer:
                 return await self._pod_stream(req, ns, name, sub)
             self._authorize(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
             if ri.plural in self.uncached:
-                return Response(200, (await self._aexisting(ri, ns, name))[1].raw)
-            key = m.key_for(ri, ns, name)
-            e = self.caches[ri.plural].get(key)
-            if e is None and self.rstore is not None:
-                # shared mode: a miss may only mean this worker lags the writer — ask the store
-                _, e = await self._retrying(lambda: self._async_existing(ri, ns, name))
-            if e is None:
-                raise not_found(ri, name)
+                e = (await self._aexisting(ri, ns, name))[1]
+            else:
+                key = m.key_for(ri, ns, name)
+                e = self.caches[ri.plural].get(key)
+                if e is None and self.rstore is not None:
+                    # shared mode: a miss may only mean this worker lags the writer — ask the store
+                    _, e = await self._retrying(lambda: self._async_existing(ri, ns, name))
+                if e is None:
+                    raise not_found(ri, name)
+            if q.get("export") in ("true", "1"):
+                from .registry import export_object
+                return _json(200, export_object(self.strategies[ri.plural], e.obj, q.get("exact") in ("true", "1")))
             return Response(200, e.raw)
         body = req.body
         if method == "POST":

@@ -23,7 +23,7 @@ import time
 import yaml
 
 from ..api import core, meta as m
-from ..client.rest import APIStatusError, Client, is_already_exists, is_not_found
+from ..client.rest import APIStatusError, Client, is_already_exists, is_not_found, resource_path
 from . import extra, printers
 
 DEFAULT_KUBECONFIG = os.path.expanduser("~/.kube/config")
@@ -178,7 +178,13 @@ class Kubectl(extra.ExtraCommands):
         for ri, name in split_targets(a.targets):
             ns = None if (a.all_namespaces or not ri.namespaced) else self.ns
             if name:
-                obj = await self.client.get(ri.plural, name, ns)
+                if a.export:
+                    st, body = await self.client.raw("GET", resource_path(ri.plural, ns, name) + "?export=true")
+                    if st != 200:
+                        raise SystemExit(f"error: {body.decode(errors='replace')}")
+                    obj = json.loads(body)
+                else:
+                    obj = await self.client.get(ri.plural, name, ns)
                 self.p(printers.render([obj], a.output, ri.kind, a.output == "wide"))
                 continue
             lst = await self.client.list(ri.plural, ns, a.selector, a.field_selector)
@@ -903,6 +909,7 @@ def build_parser():
     g.add_argument("-A", "--all-namespaces", action="store_true")
     g.add_argument("-w", "--watch", action="store_true")
     g.add_argument("-f", "--filename", action="append")
+    g.add_argument("--export", action="store_true", help="strip cluster-specific fields (single objects)")
     d = add("describe")
     d.add_argument("targets", nargs="+")
     d.add_argument("-l", "--selector")

@@ -246,3 +246,34 @@ def test_workload_strategies(run):
             await c.close()
             await api.stop()
     run(main())
+
+
+def test_export(run):
+    """`?export=true` (`genericregistry.Store.Export`): cluster-specific metadata stripped;
+    without `exact` also the namespace, status, allocated cluster IPs / node ports, a pod's node
+    and devices, and service-account token data."""
+    async def main():
+        api, c = await _api()
+        try:
+            await c.create("services", {"metadata": {"name": "np", "namespace": "default"}, "spec": {
+                "type": "NodePort", "ports": [{"port": 80}]}})
+            st, e = await _req(c, "GET", f"{NS}/services/np?export=true")
+            assert st == 200 and "uid" not in e["metadata"] and "resourceVersion" not in e["metadata"]
+            assert "namespace" not in e["metadata"] and "clusterIP" not in e["spec"]
+            assert "nodePort" not in e["spec"]["ports"][0]
+            st, e = await _req(c, "GET", f"{NS}/services/np?export=true&exact=true")
+            assert e["metadata"]["namespace"] == "default" and e["spec"]["clusterIP"]
+            await c.create("pods", {"metadata": {"name": "p", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "c", "image": "x"}]}})
+            await c.patch("pods", "p", {"status": {"phase": "Running", "podIP": "10.1.2.3"}}, "default", "merge", "status")
+            st, e = await _req(c, "GET", f"{NS}/pods/p?export=true")
+            assert e["status"]["phase"] == "Pending" and "podIP" not in e["status"]
+            await c.create("secrets", {"metadata": {"name": "tok", "namespace": "default",
+                                                    "annotations": {"kubernetes.io/service-account.name": "default"}},
+                                       "type": "kubernetes.io/service-account-token", "data": {"token": "YWJj"}})
+            st, e = await _req(c, "GET", f"{NS}/secrets/tok?export=true")
+            assert "data" not in e
+        finally:
+            await c.close()
+            await api.stop()
+    run(main())
