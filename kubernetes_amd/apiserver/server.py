@@ -75,6 +75,10 @@ class _Stale(Exception):
         self.rev = rev
 
 
+def q_include(req):
+    return (req.query.get("includeObject") or "Metadata") if hasattr(req, "query") else "Metadata"
+
+
 class _Missing(Exception):
     """Shared-store cache miss: the object may exist in the store already (this worker lags)."""
 
@@ -1265,6 +1269,12 @@ class APIServer:
             gv = getattr(req, "served_gv", None)
             if gv and isinstance(resp, Response) and resp.body[:1] == b"{" and code < 300:
                 resp = Response(resp.status, _rewrite_gv(resp.body, ri.group_version, gv), resp.content_type)
+            if verb == "GET" and code == 200 and isinstance(resp, Response) and resp.body[:1] == b"{" and \
+                    "as=Table" in req.headers.get("accept", "") and not sub:
+                from .subresources import to_table, wants_table
+                if wants_table(req.headers["accept"]):
+                    resp = _json(200, to_table(codec.loads(resp.body), ri.kind, q_include(req)))
+                    return resp
             if codec.PROTOBUF in req.headers.get("accept", "") and isinstance(resp, Response) and resp.body[:1] == b"{":
                 from ..api import protobuf as pb
                 obj = codec.loads(resp.body)

@@ -249,3 +249,38 @@ async def handle_proxy(server, req, ri, ns, ident, sub, user):
     finally:
         await c.close()
     return Response(st, body, rh.get("content-type") or "application/octet-stream")
+
+
+# ------------------------------------------------------------------------------------------------
+# server-side printing
+def wants_table(accept: str) -> bool:
+    """`Accept: application/json;as=Table;v=v1alpha1;g=meta.k8s.io` (kubectl get
+    --experimental-server-print, `endpoints/handlers/rest.go` transformResponseObject)."""
+    return "as=Table" in accept.replace(" ", "")
+
+
+def to_table(obj: dict, kind: str, include: str = "Metadata") -> dict:
+    """A GET / LIST response as a meta.k8s.io/v1alpha1 Table: the same columns `kubectl get`
+    prints (`kubectl/printers.py`, the TableGenerator of `pkg/printers`), one row per object
+    carrying the object (`includeObject=Object`), its PartialObjectMetadata (the default) or
+    nothing (`None`)."""
+    from ..kubectl import printers
+    is_list = isinstance(obj.get("items"), list)
+    items = obj["items"] if is_list else [obj]
+    rows, headers = printers.rows_for(kind, items)
+    cols = [{"name": h.title() if h != "NAME" else "Name", "type": "string", "format": "name" if h == "NAME" else "",
+             "description": "", "priority": 0} for h in headers]
+    out_rows = []
+    for cells, o in zip(rows, items):
+        row = {"cells": [str(c) for c in cells]}
+        if include == "Object":
+            row["object"] = o
+        elif include != "None":
+            row["object"] = {"kind": "PartialObjectMetadata", "apiVersion": "meta.k8s.io/v1alpha1",
+                             "metadata": o.get("metadata") or {}}
+        out_rows.append(row)
+    md = {"resourceVersion": (obj.get("metadata") or {}).get("resourceVersion", "")}
+    if is_list and (obj.get("metadata") or {}).get("continue"):
+        md["continue"] = obj["metadata"]["continue"]
+    return {"kind": "Table", "apiVersion": "meta.k8s.io/v1alpha1", "metadata": md, "columnDefinitions": cols,
+            "rows": out_rows}

@@ -177,6 +177,19 @@ class Kubectl(extra.ExtraCommands):
             return
         for ri, name in split_targets(a.targets):
             ns = None if (a.all_namespaces or not ri.namespaced) else self.ns
+            if a.experimental_server_print and not a.output and not a.watch:
+                # the server renders the columns (meta.k8s.io Table); kubectl only aligns them
+                path = resource_path(ri.plural, ns, name)
+                if a.selector:
+                    from urllib.parse import quote
+                    path += "?labelSelector=" + quote(a.selector)
+                st, body = await self.client.http.request(
+                    "GET", path, None, headers={"Accept": "application/json;as=Table;v=v1alpha1;g=meta.k8s.io"})
+                if st != 200:
+                    raise SystemExit(f"error: {body.decode(errors='replace')}")
+                t = json.loads(body)
+                self.p(printers.table([r["cells"] for r in t["rows"]], [c["name"].upper() for c in t["columnDefinitions"]]))
+                continue
             if name:
                 if a.export:
                     st, body = await self.client.raw("GET", resource_path(ri.plural, ns, name) + "?export=true")
@@ -910,6 +923,7 @@ def build_parser():
     g.add_argument("-w", "--watch", action="store_true")
     g.add_argument("-f", "--filename", action="append")
     g.add_argument("--export", action="store_true", help="strip cluster-specific fields (single objects)")
+    g.add_argument("--experimental-server-print", action="store_true", help="columns rendered by the API server")
     d = add("describe")
     d.add_argument("targets", nargs="+")
     d.add_argument("-l", "--selector")

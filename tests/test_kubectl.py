@@ -66,6 +66,8 @@ def test_create_apply_describe_delete(cluster, tmp_path):
     rc, out = k(cluster, "create", "-f", str(f))
     assert rc == 0 and "pod/vadd created" in out
     wait(lambda: "Running" in k(cluster, "get", "pods", "vadd")[1])
+    rc, out = k(cluster, "get", "pods", "vadd", "--experimental-server-print")   # columns from the API server
+    assert rc == 0 and out.splitlines()[0].split()[:3] == ["NAME", "READY", "STATUS"] and "Running" in out
     rc, out = k(cluster, "describe", "pod", "vadd")
     assert "Extended Resources:" in out and "Assigned:  GPU-" in out and "amd.com/gpu=2" in out
     rc, out = k(cluster, "get", "pod", "vadd", "-o", "jsonpath={.spec.extendedResources[0].assigned}")

@@ -277,3 +277,33 @@ def test_export(run):
             await c.close()
             await api.stop()
     run(main())
+
+
+def test_server_side_table(run):
+    """`Accept: ...;as=Table` turns GET / LIST into a meta.k8s.io Table with kubectl's columns."""
+    async def main():
+        api, c = await _api()
+        try:
+            for n in ("a", "b"):
+                await c.create("pods", {"metadata": {"name": n, "namespace": "default", "labels": {"x": "y"}},
+                                        "spec": {"containers": [{"name": "c", "image": "x"}]}})
+            tbl = {"Accept": "application/json;as=Table;v=v1alpha1;g=meta.k8s.io"}
+            st, body = await c.http.request("GET", f"{NS}/pods", None, headers=tbl)
+            t = json.loads(body)
+            assert st == 200 and t["kind"] == "Table" and t["apiVersion"] == "meta.k8s.io/v1alpha1"
+            names = [col["name"] for col in t["columnDefinitions"]]
+            assert names[0] == "Name" and "Status" in names
+            assert [r["cells"][0] for r in t["rows"]] == ["a", "b"]
+            assert t["rows"][0]["object"]["kind"] == "PartialObjectMetadata"
+            assert t["rows"][0]["object"]["metadata"]["labels"] == {"x": "y"}
+            st, body = await c.http.request("GET", f"{NS}/pods/a?includeObject=Object", None, headers=tbl)
+            t = json.loads(body)
+            assert len(t["rows"]) == 1 and t["rows"][0]["object"]["kind"] == "Pod"
+            st, body = await c.http.request("GET", f"{NS}/pods?includeObject=None", None, headers=tbl)
+            assert "object" not in json.loads(body)["rows"][0]
+            # plain JSON clients are unaffected
+            assert (await c.get("pods", "a", "default"))["kind"] == "Pod"
+        finally:
+            await c.close()
+            await api.stop()
+    run(main())
