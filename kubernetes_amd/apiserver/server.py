@@ -145,8 +145,17 @@ class APIServer:
                  tls_cert_file=None, tls_private_key_file=None, client_ca_file=None, service_account_key_files=(),
                  service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
                  anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None, oidc=None,
-                 component_endpoints=None, event_ttl=3600.0):
+                 component_endpoints=None, event_ttl=3600.0, kubelet_https=False, kubelet_certificate_authority=None,
+                 kubelet_client_certificate=None, kubelet_client_key=None):
         self.abac_policy_file = authorization_policy_file
+        # kubelet connections (--kubelet-https, --kubelet-certificate-authority,
+        # --kubelet-client-certificate/key; `pkg/kubelet/client` MakeTransport): without a CA the
+        # kubelet's serving certificate is not verified, as in the reference
+        self.kubelet_ssl = None
+        if kubelet_https:
+            from ..utils.tlsutil import client_context
+            self.kubelet_ssl = client_context(kubelet_certificate_authority, kubelet_client_certificate, kubelet_client_key)
+        self.kubelet_scheme = "https" if kubelet_https else "http"
         # --event-ttl: events expire this long after their last write (the reference stores them
         # with an etcd lease, `pkg/registry/core/event/storage/storage.go` ttlFunc)
         self.event_ttl = event_ttl
@@ -1696,11 +1705,12 @@ class APIServer:
         if is_upgrade_request(req.headers):
             # UpgradeAwareHandler: relay the WebSocket / SPDY upgrade to the kubelet and splice
             from ..cri.remotecommand import upgrade_proxy_response
+            kb = f"{self.kubelet_scheme}://{addr}:{port}"
             if sub == "portforward":
-                return upgrade_proxy_response(req, f"http://{addr}:{port}/portForward/{ns}/{name}?{req.qs}")
+                return upgrade_proxy_response(req, f"{kb}/portForward/{ns}/{name}?{req.qs}", ssl_context=self.kubelet_ssl)
             containers = (pod.get("spec") or {}).get("containers") or [{}]
             cname = (q.get("container") or [containers[0].get("name", "")])[0]
-            return upgrade_proxy_response(req, f"http://{addr}:{port}/{sub}/{ns}/{name}/{cname}?{req.qs}")
+            return upgrade_proxy_response(req, f"{kb}/{sub}/{ns}/{name}/{cname}?{req.qs}", ssl_context=self.kubelet_ssl)
         if sub == "portforward":
             pport = (q.get("port") or q.get("ports") or [""])[0]
             if not pport:
@@ -1709,10 +1719,10 @@ class APIServer:
                 raise bad_request("port-forward needs Connection: Upgrade")
             from ..cri.server import splice
             from ..cri.streaming import open_port_forward
-            url = f"http://{addr}:{port}/portForward/{ns}/{name}"
+            url = f"{self.kubelet_scheme}://{addr}:{port}/portForward/{ns}/{name}"
 
             async def run(reader, writer):
-                ur, uw = await open_port_forward(url, int(pport))
+                ur, uw = await open_port_forward(url, int(pport), ssl_context=self.kubelet_ssl)
                 await splice(reader, writer, ur, uw)
             return UpgradeResponse(run)
         containers = (pod.get("spec") or {}).get("containers") or [{}]
@@ -1720,13 +1730,13 @@ class APIServer:
         names = {c.get("name") for c in containers} | {c.get("name") for c in (pod.get("spec") or {}).get("initContainers") or ()}
         if cname not in names:
             raise bad_request(f"container {cname} is not valid for pod {name}")
-        target = f"http://{addr}:{port}/{sub}/{ns}/{name}/{cname}"
+        target = f"{self.kubelet_scheme}://{addr}:{port}/{sub}/{ns}/{name}/{cname}"
         if q.get("command"):
             target += "?" + urlencode([("command", c) for c in q["command"]])
         from ..cri.streaming import _open
 
         async def relay(w):
-            r, uw, status, _ = await _open(target)
+            r, uw, status, _ = await _open(target, ssl_context=self.kubelet_ssl)
             try:
                 if status != 200:
                     body = await r.read(4096)
@@ -1782,7 +1792,7 @@ class APIServer:
     async def _pod_log(self, ns, name, q):
         _, addr, port = await self._kubelet_of(ns, name)
         from ..client.http import HTTPClient
-        c = HTTPClient(f"http://{addr}:{port}")
+        c = HTTPClient(f"{self.kubelet_scheme}://{addr}:{port}", ssl_context=self.kubelet_ssl)
         try:
             qs = "&".join(f"{k}={v}" for k, v in q.items())
             st, body = await c.request("GET", f"/containerLogs/{ns}/{name}/{q.get('container', '')}" + (f"?{qs}" if qs else ""))

@@ -164,7 +164,7 @@ def legacy_proxy_path(path: str) -> str | None:
 async def resolve_proxy_target(server, ri, ns, ident):
     """-> base URL (scheme://host:port) for `<ri>/<ident>/proxy`."""
     scheme, name, port = split_scheme_name_port(ident)
-    scheme = scheme or "http"
+    scheme = scheme or (server.kubelet_scheme if ri.plural == "nodes" else "http")
     if ri.plural == "pods":
         _, e = await server._aexisting(ri, ns, name)
         ip = ((e.obj.get("status") or {}).get("podIP") or "")
@@ -234,12 +234,16 @@ async def handle_proxy(server, req, ri, ns, ident, sub, user):
         path += "/"
     target = base + path + (f"?{req.qs}" if req.qs else "")
     from ..cri.remotecommand import is_upgrade_request, upgrade_proxy_response
-    if is_upgrade_request(req.headers):
-        return upgrade_proxy_response(req, target)
+    # kubelets: the configured kubelet TLS; https pods / services: not verified (the reference's
+    # proxy transport for those has no CA to check against either)
+    ctx = None
     if base.startswith("https://"):
-        raise APIError(503, "ServiceUnavailable", "https backends are not proxied by this server")
+        from ..utils.tlsutil import unverified_client_context
+        ctx = server.kubelet_ssl if (ri.plural == "nodes" and server.kubelet_ssl is not None) else unverified_client_context()
+    if is_upgrade_request(req.headers):
+        return upgrade_proxy_response(req, target, ssl_context=ctx)
     from ..client.http import HTTPClient, HTTPError
-    c = HTTPClient(base, timeout=30.0)
+    c = HTTPClient(base, ssl_context=ctx, timeout=30.0)
     try:
         hdrs = {k: v for k, v in req.headers.items() if k.lower() not in _HOP and k.lower() != "content-type"}
         st, rh, body = await c.request_full(req.method, path + (f"?{req.qs}" if req.qs else ""), req.body or None,

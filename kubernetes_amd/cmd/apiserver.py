@@ -53,6 +53,12 @@ def _parser():
     ap.add_argument("--audit-policy-file", default=None, help="audit policy YAML (rules: level/users/verbs/resources)")
     ap.add_argument("--experimental-encryption-provider-config", dest="encryption_config", default=None,
                     help="EncryptionConfig YAML: encrypt the listed resources at rest (aescbc/aesgcm/secretbox/kms)")
+    ap.add_argument("--kubelet-https", type=lambda v: v.lower() != "false", default=True,
+                    help="use https for kubelet connections (logs, exec/attach/port-forward, node proxy)")
+    ap.add_argument("--kubelet-certificate-authority", default=None,
+                    help="CA that signs kubelet serving certificates (unset: they are not verified)")
+    ap.add_argument("--kubelet-client-certificate", default=None, help="client certificate presented to kubelets")
+    ap.add_argument("--kubelet-client-key", default=None)
     ap.add_argument("--tls-cert-file", default=None)
     ap.add_argument("--tls-private-key-file", default=None)
     ap.add_argument("--client-ca-file", default=None, help="enable x509 client certificate authentication")
@@ -232,6 +238,8 @@ def main(argv=None):
                       audit=audit, encryption_config=a.encryption_config,
                       service_cluster_ip_range=a.service_cluster_ip_range,
                       service_node_port_range=tuple(int(x) for x in a.service_node_port_range.split("-")),
+                      kubelet_https=a.kubelet_https, kubelet_certificate_authority=a.kubelet_certificate_authority,
+                      kubelet_client_certificate=a.kubelet_client_certificate, kubelet_client_key=a.kubelet_client_key,
                       tls_cert_file=a.tls_cert_file, tls_private_key_file=a.tls_private_key_file,
                       client_ca_file=a.client_ca_file, service_account_key_files=a.service_account_key_file,
                       service_account_lookup=a.service_account_lookup,

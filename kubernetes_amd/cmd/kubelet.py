@@ -2,7 +2,9 @@
 from __future__ import annotations
 
 import argparse
+import logging
 import os
+import sys
 
 from ..client.rest import Client
 from ..deviceplugin import api
@@ -89,25 +91,34 @@ def main(argv=None):
                     help="Webhook: SubjectAccessReview per request (resource nodes, subresource by path)")
     ap.add_argument("--event-qps", type=float, default=5.0, help="limit event creations per second (0 = unlimited)")
     ap.add_argument("--event-burst", type=int, default=10, help="burst of event creations (with --event-qps > 0)")
+    _reference_flags(ap)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
     setup_logging(a.v)
     DefaultFeatureGate.set(a.feature_gates)
+    _host_checks(a)
 
     async def start():
+        if a.experimental_bootstrap_kubeconfig and not a.bootstrap_kubeconfig:
+            a.bootstrap_kubeconfig = a.experimental_bootstrap_kubeconfig
         if a.bootstrap_kubeconfig and a.kubeconfig and not os.path.exists(a.kubeconfig):
             from ..kubelet.certificate import bootstrap_client_certificate
             await bootstrap_client_certificate(a.bootstrap_kubeconfig, a.kubeconfig, a.hostname_override,
                                                os.path.join(a.root_dir, "pki"))
         if a.kubeconfig:
             from ..client.clientcmd import client_from
-            client = client_from(a.kubeconfig, max_conns=32)
+            client = client_from(a.kubeconfig, max_conns=32, qps=a.kube_api_qps, burst=a.kube_api_burst)
         else:
-            client = Client(a.master or "http://127.0.0.1:8080", token=a.token, max_conns=32)
+            client = Client(a.master or "http://127.0.0.1:8080", token=a.token, max_conns=32, qps=a.kube_api_qps,
+                            burst=a.kube_api_burst)
         pdir = a.device_plugins_dir or os.path.join(a.root_dir, "device-plugin", "plugins")
         dm = ManagerImpl(pdir) if DefaultFeatureGate("DevicePlugins") else ManagerStub()
         if a.container_runtime == "remote":
             from ..cri.remote import RemoteRuntime
+            if a.image_service_endpoint and a.image_service_endpoint != a.container_runtime_endpoint:
+                print("kubelet: --image-service-endpoint must equal --container-runtime-endpoint here "
+                      "(one CRI server serves both services)", file=sys.stderr)
+                sys.exit(1)
             rt = await RemoteRuntime(a.container_runtime_endpoint, a.runtime_request_timeout, a.pleg_relist_period).connect()
         elif a.container_runtime == "process":
             images = None
@@ -119,7 +130,8 @@ def main(argv=None):
             rt = StubRuntime()
         from ..api.quantity import parse_quantity
         cap = int(parse_quantity(a.image_fs_capacity).value) if a.image_fs_capacity not in ("", "0") else 0
-        image_gc = {"capacity_bytes": cap, "high": a.image_gc_high_threshold, "low": a.image_gc_low_threshold} if cap else None
+        image_gc = {"capacity_bytes": cap, "high": a.image_gc_high_threshold, "low": a.image_gc_low_threshold,
+                    "min_age": _duration(a.minimum_image_ttl_duration)} if cap else None
         labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
         from ..kubelet import network as net
         plugin = net.new_plugin(a.network_plugin, os.path.join(a.root_dir, "network"), a.cni_conf_dir, a.cni_bin_dir)
@@ -141,7 +153,10 @@ def main(argv=None):
             if ck is not None:
                 extra.update(to_kwargs(ck))
             extra["dynamic_config_dir"] = a.dynamic_config_dir
-        base = dict(pods=a.max_pods, node_status_update_frequency=a.node_status_update_frequency,
+        max_pods = a.max_pods
+        if a.pods_per_core > 0:
+            max_pods = min(max_pods, a.pods_per_core * (os.cpu_count() or 1))
+        base = dict(pods=max_pods, node_status_update_frequency=a.node_status_update_frequency,
                     cpu_manager_policy=a.cpu_manager_policy, eviction_hard=a.eviction_hard, dns=dns,
                     pod_manifest_path=a.pod_manifest_path, container_gc=container_gc,
                     bootstrap_checkpoint_path=a.bootstrap_checkpoint_path, volume_plugin_dir=a.volume_plugin_dir,
@@ -149,14 +164,32 @@ def main(argv=None):
                     manifest_url_headers=dict(h.split(":", 1) for h in a.manifest_url_header if ":" in h),
                     kube_reserved=dict(kv.split("=", 1) for kv in a.kube_reserved.split(",") if "=" in kv),
                     system_reserved=dict(kv.split("=", 1) for kv in a.system_reserved.split(",") if "=" in kv),
-                    event_qps=a.event_qps, event_burst=a.event_burst)
-        if not a.anonymous_auth or a.authentication_token_webhook or a.authorization_mode != "AlwaysAllow":
+                    event_qps=a.event_qps, event_burst=a.event_burst,
+                    tls=_tls(a), read_only_port=a.read_only_port or None,
+                    healthz_port=a.healthz_port or None, healthz_address=a.healthz_bind_address,
+                    debugging_handlers=a.enable_debugging_handlers, node_ip=a.node_ip or None,
+                    register_taints=_taints(a.register_with_taints), register_schedulable=a.register_schedulable,
+                    provider_id=a.provider_id, allow_privileged=a.allow_privileged,
+                    host_sources={"hostNetwork": _sources(a.host_network_sources), "hostPID": _sources(a.host_pid_sources),
+                                  "hostIPC": _sources(a.host_ipc_sources)},
+                    eviction_soft=a.eviction_soft or None, eviction_soft_grace_period=a.eviction_soft_grace_period,
+                    eviction_minimum_reclaim=a.eviction_minimum_reclaim,
+                    eviction_max_pod_grace_period=a.eviction_max_pod_grace_period,
+                    eviction_pressure_transition_period=_duration(a.eviction_pressure_transition_period),
+                    allocatable_ignore_eviction=a.experimental_allocatable_ignore_eviction,
+                    serialize_image_pulls=a.serialize_image_pulls, registry_qps=a.registry_qps,
+                    registry_burst=a.registry_burst, file_check_frequency=_duration(a.file_check_frequency),
+                    http_check_frequency=_duration(a.http_check_frequency), register=a.register_node)
+        if not a.anonymous_auth or a.authentication_token_webhook or a.authorization_mode != "AlwaysAllow" or a.client_ca_file:
             from ..kubelet.server_auth import KubeletAuth
             base["auth"] = KubeletAuth(client, a.hostname_override, a.anonymous_auth,
-                                       a.authentication_token_webhook, a.authorization_mode)
+                                       a.authentication_token_webhook, a.authorization_mode,
+                                       authn_ttl=_duration(a.authentication_token_webhook_cache_ttl),
+                                       authz_allowed_ttl=_duration(a.authorization_webhook_cache_authorized_ttl),
+                                       authz_denied_ttl=_duration(a.authorization_webhook_cache_unauthorized_ttl))
         base.update(extra)
         kl = Kubelet(client, a.hostname_override, rt, dm, labels=labels,
-                     http_port=a.port, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,
+                     http_port=a.port if a.enable_server else None, address=a.address, root_dir=a.root_dir, reserved_cpus=a.reserved_cpus,
                      image_gc=image_gc, network_plugin=plugin, hostports=hostports,
                      cgroup_root=a.cgroup_root if a.cgroups_per_qos else None,
                      container_log_dir=a.container_log_dir or None,
@@ -167,10 +200,177 @@ def main(argv=None):
             from ..kubelet.certificate import CertificateRotator
             rot = CertificateRotator(a.kubeconfig, a.hostname_override, os.path.join(a.root_dir, "pki"), client)
             kl._tasks.append(asyncio.ensure_future(rot.run()))
-        print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port})", flush=True)
+        print(f"kubelet {a.hostname_override} running (runtime={rt.name}, plugins={pdir}, port={kl.http_port}, "
+              f"{'https' if kl.tls else 'http'})", flush=True)
         return kl
 
     run_until_signal(start)
+
+
+def _duration(v) -> float:
+    from ..kubelet.eviction import parse_duration
+    if isinstance(v, (int, float)):
+        return float(v)
+    v = str(v).strip()
+    return float(v) if v.replace(".", "", 1).isdigit() else parse_duration(v)
+
+
+def _sources(v):
+    return [x.strip() for x in (v or "").split(",") if x.strip()]
+
+
+def _taints(spec):
+    """`key=value:Effect` / `key:Effect`, comma separated (`--register-with-taints`)."""
+    out = []
+    for part in _sources(spec):
+        kv, _, effect = part.rpartition(":")
+        if effect not in ("NoSchedule", "PreferNoSchedule", "NoExecute") or not kv:
+            raise SystemExit(f"kubelet: invalid taint {part!r} (want key=value:Effect)")
+        key, _, value = kv.partition("=")
+        t = {"key": key, "effect": effect}
+        if value:
+            t["value"] = value
+        out.append(t)
+    return out
+
+
+def _tls(a):
+    """--tls-cert-file/--tls-private-key-file, else a self-signed pair in --cert-dir
+    (InitializeTLS); --client-ca-file enables x509 client authentication."""
+    if not a.enable_server:
+        return None
+    if a.tls_cert_file:
+        return (a.tls_cert_file, a.tls_private_key_file or a.tls_cert_file, a.client_ca_file)
+    from ..utils.tlsutil import self_signed_serving_cert
+    cert_dir = a.cert_dir or os.path.join(a.root_dir, "pki")
+    cert, key = self_signed_serving_cert(cert_dir, a.hostname_override, [a.node_ip, a.address])
+    return (cert, key, a.client_ca_file)
+
+
+def _host_checks(a):
+    from ..kubelet import hostchecks as H
+    if a.cloud_provider not in ("", "external"):
+        print(f"kubelet: --cloud-provider={a.cloud_provider}: cloud providers are out of scope here "
+              "(use '' or 'external')", file=sys.stderr)
+        sys.exit(1)
+    if a.cgroup_driver not in ("cgroupfs", "systemd"):
+        print(f"kubelet: unknown --cgroup-driver {a.cgroup_driver!r}", file=sys.stderr)
+        sys.exit(1)
+    if a.runonce:
+        print("kubelet: --runonce is not supported (run the static pods with a normal kubelet)", file=sys.stderr)
+        sys.exit(1)
+    if a.cadvisor_port:
+        logging.getLogger("kubelet").warning("--cadvisor-port: container stats are served by /stats/summary; "
+                                             "no standalone cAdvisor endpoint is started")
+    try:
+        H.check_swap(a.fail_swap_on and a.experimental_fail_swap_on)
+        H.check_kernel_defaults(a.protect_kernel_defaults)
+    except H.HostCheckError as e:
+        print(f"kubelet: {e}", file=sys.stderr)
+        sys.exit(1)
+    H.set_max_open_files(a.max_open_files)
+    H.set_oom_score_adj(a.oom_score_adj)
+    if a.lock_file:
+        lk = H.LockFile(a.lock_file).acquire()
+        if a.exit_on_lock_contention:
+            lk.watch_contention(lambda: os._exit(0))
+
+
+def _bool(v):
+    return str(v).lower() not in ("false", "0", "no")
+
+
+def _reference_flags(ap):
+    """The rest of the reference kubelet's flags (cmd/kubelet/app/options/options.go). Flags whose
+    subsystem does not exist here are accepted and documented as such."""
+    g = ap.add_argument_group("serving")
+    g.add_argument("--tls-cert-file", default=None, help="x509 serving certificate (default: self-signed in --cert-dir)")
+    g.add_argument("--tls-private-key-file", default=None)
+    g.add_argument("--cert-dir", default=None, help="where the self-signed serving pair goes (default <root-dir>/pki)")
+    g.add_argument("--client-ca-file", default=None, help="authenticate API clients by x509 certificates of this CA")
+    g.add_argument("--read-only-port", type=int, default=0,
+                   help="unauthenticated read-only port (no debugging handlers); 0 = off (the reference defaults to 10255)")
+    g.add_argument("--healthz-port", type=int, default=0, help="localhost /healthz port; 0 = off (reference: 10248)")
+    g.add_argument("--healthz-bind-address", default="127.0.0.1")
+    g.add_argument("--enable-server", type=_bool, default=True)
+    g.add_argument("--enable-debugging-handlers", type=_bool, default=True,
+                   help="exec/attach/port-forward/run/logs/containerLogs/pprof/configz on the server")
+    g.add_argument("--authentication-token-webhook-cache-ttl", default="2m")
+    g.add_argument("--authorization-webhook-cache-authorized-ttl", default="5m")
+    g.add_argument("--authorization-webhook-cache-unauthorized-ttl", default="30s")
+    g.add_argument("--streaming-connection-idle-timeout", default="4h",
+                   help="accepted; streams end when either side closes")
+    g = ap.add_argument_group("registration")
+    g.add_argument("--register-node", type=_bool, default=True)
+    g.add_argument("--register-with-taints", default="", help="key=value:Effect,... applied at registration")
+    g.add_argument("--register-schedulable", type=_bool, default=True)
+    g.add_argument("--node-ip", default="", help="the node's InternalIP (default: --address)")
+    g.add_argument("--provider-id", default="")
+    g.add_argument("--cloud-provider", default="", help="'' or 'external' (cloud providers are out of scope)")
+    g.add_argument("--cloud-config", default="")
+    g = ap.add_argument_group("admission")
+    g.add_argument("--allow-privileged", type=_bool, default=False)
+    g.add_argument("--host-network-sources", default="*", help="pod sources (api,file,http) allowed hostNetwork")
+    g.add_argument("--host-pid-sources", default="*")
+    g.add_argument("--host-ipc-sources", default="*")
+    g.add_argument("--pods-per-core", type=int, default=0)
+    g = ap.add_argument_group("eviction")
+    g.add_argument("--eviction-soft", default="", help="e.g. memory.available<1.5Gi")
+    g.add_argument("--eviction-soft-grace-period", default="", help="e.g. memory.available=1m30s")
+    g.add_argument("--eviction-max-pod-grace-period", type=int, default=0)
+    g.add_argument("--eviction-minimum-reclaim", default="", help="e.g. memory.available=0Mi,nodefs.available=500Mi")
+    g.add_argument("--eviction-pressure-transition-period", default="5m")
+    g.add_argument("--experimental-allocatable-ignore-eviction", type=_bool, default=False)
+    g = ap.add_argument_group("images and pod sources")
+    g.add_argument("--serialize-image-pulls", type=_bool, default=True)
+    g.add_argument("--registry-qps", type=float, default=5.0)
+    g.add_argument("--registry-burst", type=int, default=10)
+    g.add_argument("--minimum-image-ttl-duration", default="2m")
+    g.add_argument("--image-service-endpoint", default="")
+    g.add_argument("--file-check-frequency", default="20s")
+    g.add_argument("--http-check-frequency", default="20s")
+    g.add_argument("--sync-frequency", default="1m", help="accepted; pods resync on every watch event and status loop")
+    g = ap.add_argument_group("API client")
+    g.add_argument("--kube-api-qps", type=float, default=5.0)
+    g.add_argument("--kube-api-burst", type=int, default=10)
+    g.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
+                   help="accepted; this kubelet's client speaks JSON")
+    g.add_argument("--experimental-bootstrap-kubeconfig", default=None, help="deprecated alias of --bootstrap-kubeconfig")
+    g.add_argument("--require-kubeconfig", type=_bool, default=False, help="deprecated no-op, as in the reference")
+    g = ap.add_argument_group("host")
+    g.add_argument("--fail-swap-on", type=_bool, default=True)
+    g.add_argument("--experimental-fail-swap-on", type=_bool, default=True, help="deprecated alias of --fail-swap-on")
+    g.add_argument("--protect-kernel-defaults", type=_bool, default=False)
+    g.add_argument("--max-open-files", type=int, default=1000000)
+    g.add_argument("--oom-score-adj", type=int, default=-999)
+    g.add_argument("--lock-file", default="")
+    g.add_argument("--exit-on-lock-contention", type=_bool, default=False)
+    g.add_argument("--cgroup-driver", default="cgroupfs", help="cgroupfs or systemd (both manage the cgroup v2 tree directly)")
+    g.add_argument("--enforce-node-allocatable", default="pods",
+                   help="accepted; node allocatable is enforced on the pods (kubepods) cgroup with --cgroups-per-qos")
+    for f in ("--kubelet-cgroups", "--system-cgroups", "--kube-reserved-cgroup", "--system-reserved-cgroup"):
+        g.add_argument(f, default="", help="accepted; system daemons are not moved into cgroups by this kubelet")
+    g.add_argument("--cpu-cfs-quota", type=_bool, default=True, help="accepted; CPU limits are always enforced via cpu.max")
+    g.add_argument("--cpu-manager-reconcile-period", default="10s", help="accepted; assignments are applied at container start")
+    g.add_argument("--experimental-qos-reserved", default="", help="accepted (alpha QOSReserved)")
+    g.add_argument("--seccomp-profile-root", default="", help="accepted; seccomp profiles are not applied by this runtime")
+    g = ap.add_argument_group("networking")
+    g.add_argument("--hairpin-mode", default="promiscuous-bridge", help="accepted; kubenet's bridge handles hairpin traffic")
+    g.add_argument("--non-masquerade-cidr", default="10.0.0.0/8", help="accepted")
+    g.add_argument("--make-iptables-util-chains", type=_bool, default=True, help="accepted")
+    g.add_argument("--iptables-masquerade-bit", type=int, default=14, help="accepted")
+    g.add_argument("--iptables-drop-bit", type=int, default=15, help="accepted")
+    g = ap.add_argument_group("no-ops kept for command-line compatibility")
+    for f, d in (("--cadvisor-port", 0), ("--chaos-chance", 0.0)):
+        g.add_argument(f, type=type(d), default=d)
+    for f in ("--containerized", "--contention-profiling", "--enable-custom-metrics", "--really-crash-for-testing",
+              "--experimental-check-node-capabilities-before-mount", "--experimental-kernel-memcg-notification",
+              "--keep-terminated-pod-volumes", "--runonce"):
+        g.add_argument(f, type=_bool, default=False)
+    g.add_argument("--enable-controller-attach-detach", type=_bool, default=True)
+    for f in ("--experimental-mounter-path", "--init-config-dir", "--master-service-namespace",
+              "--volume-stats-agg-period"):
+        g.add_argument(f, default="")
 
 
 if __name__ == "__main__":

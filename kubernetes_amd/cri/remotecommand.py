@@ -284,7 +284,7 @@ async def accept_raw(reader, writer, headers, supported):
 HOP_HEADERS = {"host", "content-length", "transfer-encoding"}
 
 
-def upgrade_proxy_response(req, url: str, extra_headers=None):
+def upgrade_proxy_response(req, url: str, extra_headers=None, ssl_context=None):
     """Relay an upgrade request (WebSocket) to `url` — path and query of the next hop — and
     splice both directions once the backend answered; the backend's reply (101 or an error) goes
     to the client verbatim."""
@@ -293,7 +293,11 @@ def upgrade_proxy_response(req, url: str, extra_headers=None):
 
     async def run(reader, writer):
         try:
-            ur, uw = await asyncio.open_connection(u.hostname, u.port or 80)
+            tls = None
+            if u.scheme == "https":
+                from ..utils.tlsutil import unverified_client_context
+                tls = ssl_context or unverified_client_context()
+            ur, uw = await asyncio.open_connection(u.hostname, u.port or (443 if tls else 80), ssl=tls)
         except OSError as e:
             msg = f"error dialing backend: {e}".encode()
             writer.write(b"HTTP/1.1 503 Service Unavailable\r\nContent-Type: text/plain\r\nContent-Length: %d\r\n\r\n%s"

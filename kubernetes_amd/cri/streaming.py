@@ -10,9 +10,13 @@ import asyncio
 from urllib.parse import urlsplit
 
 
-async def _open(url, headers=""):
+async def _open(url, headers="", ssl_context=None):
     u = urlsplit(url)
-    r, w = await asyncio.open_connection(u.hostname, u.port)
+    ssl = None
+    if u.scheme == "https":
+        from ..utils.tlsutil import unverified_client_context
+        ssl = ssl_context or unverified_client_context()
+    r, w = await asyncio.open_connection(u.hostname, u.port or (443 if ssl else 80), ssl=ssl)
     target = u.path + (("?" + u.query) if u.query else "")
     w.write(f"GET {target} HTTP/1.1\r\nHost: {u.hostname}:{u.port}\r\n{headers}\r\n".encode())
     await w.drain()
@@ -52,10 +56,10 @@ async def read_exec_stream(url):
         w.close()
 
 
-async def open_port_forward(url, port):
+async def open_port_forward(url, port, ssl_context=None):
     """Upgrade a port-forward URL into a raw tunnel -> (reader, writer)."""
     sep = "&" if "?" in url else "?"
-    r, w, status, _ = await _open(f"{url}{sep}port={port}", "Connection: Upgrade\r\nUpgrade: tcp\r\n")
+    r, w, status, _ = await _open(f"{url}{sep}port={port}", "Connection: Upgrade\r\nUpgrade: tcp\r\n", ssl_context)
     if status != 101:
         w.close()
         raise ConnectionError(f"port-forward refused: HTTP {status}")

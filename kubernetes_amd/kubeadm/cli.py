@@ -123,7 +123,8 @@ def cmd_init(a):
         log = open(os.path.join(kd, "kubelet.log"), "ab")
         subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.kubelet", "--kubeconfig", os.path.join(kd, P.KUBELET_CONF),
                           "--pod-manifest-path", os.path.join(kd, "manifests"), "--hostname-override", cfg["nodeName"],
-                          "--root-dir", os.path.join(kd, "kubelet")], stdout=log, stderr=log, start_new_session=True)
+                          "--root-dir", os.path.join(kd, "kubelet")] + P.kubelet_flags(cfg["certificatesDir"]),
+                         stdout=log, stderr=log, start_new_session=True)
         print("[kubelet] started kubelet (static pods will bring up the control plane)")
     asyncio.run(post_control_plane(cfg, os.path.join(cfg["kubernetesDir"], P.ADMIN_CONF), token, a.timeout,
                                    mark_master=not a.skip_mark_master))
@@ -145,8 +146,8 @@ def cmd_join(a):
     print(f"[join] TLS bootstrap complete, kubelet credentials in {conf}\n\nThis node has joined the cluster.")
     if a.start_kubelet:
         subprocess.Popen([sys.executable, "-m", "kubernetes_amd.cmd.kubelet", "--kubeconfig", conf,
-                          "--hostname-override", node, "--root-dir", os.path.join(a.kubernetes_dir, "kubelet")],
-                         start_new_session=True)
+                          "--hostname-override", node, "--root-dir", os.path.join(a.kubernetes_dir, "kubelet")]
+                         + P.kubelet_flags(os.path.join(a.kubernetes_dir, "pki")), start_new_session=True)
     return 0
 
 

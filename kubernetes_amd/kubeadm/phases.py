@@ -181,6 +181,14 @@ def _static_pod(name, command, host_paths=(), version=VERSION):
                      "volumes": vols}}
 
 
+def kubelet_flags(pki_dir):
+    """The kubelet drop-in kubeadm installs (10-kubeadm.conf): privileged pods allowed (the
+    control plane and add-ons need them), x509 client authentication against the cluster CA,
+    requests authorized by the API server (Webhook)."""
+    return ["--allow-privileged=true", "--client-ca-file", os.path.join(pki_dir, "ca.crt"),
+            "--authorization-mode", "Webhook", "--authentication-token-webhook"]
+
+
 def etcd_socket(cfg):
     return os.path.join(cfg["etcd"]["dataDir"], "kamd-etcd.sock")
 
@@ -211,7 +219,9 @@ def control_plane_manifests(cfg):
                 "--enable-bootstrap-token-auth", "--authorization-mode", ",".join(cfg["authorizationModes"]),
                 "--admission-control", ",".join(DEFAULT_ADMISSION),
                 "--service-cluster-ip-range", cfg["networking"]["serviceSubnet"],
-                "--storage-media-type", "application/vnd.kubernetes.protobuf"] + store
+                "--storage-media-type", "application/vnd.kubernetes.protobuf",
+                "--kubelet-client-certificate", os.path.join(d, APISERVER_KUBELET_CLIENT + ".crt"),
+                "--kubelet-client-key", os.path.join(d, APISERVER_KUBELET_CLIENT + ".key")] + store
     cm = py + ["kubernetes_amd.cmd.controller_manager", "--kubeconfig", os.path.join(kd, CM_CONF), "--leader-elect",
                "--service-account-private-key-file", os.path.join(d, "sa.key"), "--root-ca-file", os.path.join(d, "ca.crt"),
                "--cluster-signing-cert-file", os.path.join(d, "ca.crt"), "--cluster-signing-key-file", os.path.join(d, "ca.key"),

@@ -33,9 +33,19 @@ def default_pull_policy(image: str) -> str:
 
 
 class ImageManager:
+    """`serialize` (--serialize-image-pulls, default true): one pull at a time
+    (`serialImagePuller`), else concurrent pulls (`parallelImagePuller`); `qps`/`burst`
+    (--registry-qps 5 / --registry-burst 10; qps 0 = unlimited): pulls go through a token bucket
+    (`throttleImagePulling`), and a pull over the limit fails with "pull QPS exceeded" so the
+    pod retries after its back-off, as in the reference."""
+
     def __init__(self, service, recorder=None, backoff_initial=10.0, backoff_max=300.0, clock=time.monotonic,
-                 secret_getter=None):
+                 secret_getter=None, serialize=False, qps=0.0, burst=10):
+        import asyncio
         self.service = service
+        self._serial = asyncio.Lock() if serialize else None
+        self.qps, self.burst = float(qps or 0), int(burst)
+        self._tokens, self._t = float(burst), clock()
         # async (namespace, name) -> Secret, for the pod's imagePullSecrets keyring
         self.secret_getter = secret_getter
         self.recorder = recorder
@@ -73,7 +83,13 @@ class ImageManager:
             raise ImagePullError("ImagePullBackOff", msg)
         self._event(pod, "Normal", "Pulling", f'pulling image "{image}"')
         try:
-            ref = await self._pull(pod, image)
+            if not self._take_token():
+                raise RuntimeError("pull QPS exceeded")
+            if self._serial is not None:
+                async with self._serial:
+                    ref = await self._pull(pod, image)
+            else:
+                ref = await self._pull(pod, image)
         except Exception as e:
             period = min(self.backoff_max, b[1] * 2) if b else self.backoff_initial
             self._backoff[image] = (now + period, period)
@@ -84,6 +100,17 @@ class ImageManager:
         self.last_used[ref] = time.time()
         self._event(pod, "Normal", "Pulled", f'Successfully pulled image "{image}"')
         return ref
+
+    def _take_token(self) -> bool:
+        if self.qps <= 0:
+            return True
+        now = self.clock()
+        self._tokens = min(float(self.burst), self._tokens + (now - self._t) * self.qps)
+        self._t = now
+        if self._tokens < 1.0:
+            return False
+        self._tokens -= 1.0
+        return True
 
     async def _pull(self, pod, image):
         """`kuberuntime_image.go PullImage`: try every matching pull-secret credential in turn

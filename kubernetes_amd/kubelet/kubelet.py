@@ -102,8 +102,32 @@ class Kubelet:
                  bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
                  manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None,
                  cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, container_log_dir=None,
-                 event_qps=5.0, event_burst=10, auth=None, node_log_dir="/var/log"):
+                 event_qps=5.0, event_burst=10, auth=None, node_log_dir="/var/log", tls=None, read_only_port=None,
+                 healthz_port=None, healthz_address="127.0.0.1", debugging_handlers=True, node_ip=None,
+                 register_taints=(), register_schedulable=True, provider_id="", allow_privileged=True,
+                 host_sources=None, eviction_soft=None, eviction_soft_grace_period=None, eviction_minimum_reclaim=None,
+                 eviction_max_pod_grace_period=0, eviction_pressure_transition_period=0.0,
+                 allocatable_ignore_eviction=False, serialize_image_pulls=False, registry_qps=0.0, registry_burst=10,
+                 file_check_frequency=20.0, http_check_frequency=20.0):
+        self.file_check_frequency, self.http_check_frequency = file_check_frequency, http_check_frequency
         self.client = client
+        # :10250 serving (cmd/kubelet/app/server.go): TLS = (cert file, key file, client CA file or
+        # None) or None for plain HTTP; --read-only-port (unauthenticated, no debugging handlers)
+        # and --healthz-port listeners; --enable-debugging-handlers=false drops exec/attach/
+        # port-forward/run/logs/containerLogs/pprof/configz from the server
+        self.tls = tls
+        self.read_only_port, self.healthz_port, self.healthz_address = read_only_port, healthz_port, healthz_address
+        self.debugging_handlers = debugging_handlers
+        self.ro_http = self.healthz_http = None
+        # registration: --node-ip, --register-with-taints, --register-schedulable, --provider-id
+        self.node_ip = node_ip
+        self.register_taints = [dict(t) for t in register_taints or ()]
+        self.register_schedulable = register_schedulable
+        self.provider_id = provider_id
+        # --allow-privileged and --host-{network,pid,ipc}-sources (pkg/kubelet/util/capabilities):
+        # which pod sources ("api", "file", "http"; "*" = all) may use host namespaces
+        self.allow_privileged = allow_privileged
+        self.host_sources = host_sources or {}
         self.auth = auth                      # server_auth.KubeletAuth for the :10250 API (None: open)
         self.node_log_dir = node_log_dir      # served read-only under /logs/
         self._last_status_loop = time.monotonic()
@@ -139,9 +163,14 @@ class Kubelet:
         self.static_pods = None
         self.eviction = None
         self.eviction_interval = eviction_interval
-        if eviction_hard:
-            from .eviction import EvictionManager, parse_thresholds
-            self.eviction = EvictionManager(parse_thresholds(eviction_hard), eviction_signals)
+        self.allocatable_ignore_eviction = allocatable_ignore_eviction
+        if eviction_hard or eviction_soft:
+            from .eviction import EvictionManager, parse_soft_thresholds, parse_thresholds
+            th = parse_thresholds(eviction_hard or "", eviction_minimum_reclaim or "")
+            if eviction_soft:
+                th += parse_soft_thresholds(eviction_soft, eviction_soft_grace_period or "", eviction_minimum_reclaim or "")
+            self.eviction = EvictionManager(th, eviction_signals, pressure_transition_period=eviction_pressure_transition_period,
+                                            max_pod_grace=eviction_max_pod_grace_period)
         self.cpu_manager = None
         if cpu_manager_policy == "static":
             from .cpumanager import CPUTopology, StaticPolicy
@@ -200,7 +229,8 @@ class Kubelet:
         from .images import ImageGCManager, ImageManager
         self.image_service = image_service
         self.images = ImageManager(image_service, self.recorder, backoff_initial=image_backoff,
-                                   secret_getter=lambda ns, name: self.client.get("secrets", name, ns))
+                                   secret_getter=lambda ns, name: self.client.get("secrets", name, ns),
+                                   serialize=serialize_image_pulls, qps=registry_qps, burst=registry_burst)
         self.image_gc = None
         if image_gc:
             self.image_gc = ImageGCManager(image_service, int(image_gc.get("capacity_bytes", 0)), self._images_in_use,
@@ -221,8 +251,18 @@ class Kubelet:
         """Start everything; returns once the node is registered and pods are syncing."""
         self.recorder.start()
         if self.http_port is not None:
+            ctx = None
+            if self.tls:
+                from ..utils.tlsutil import server_context
+                ctx = server_context(*self.tls)
             self.http = HTTPServer(self._http)
-            self.http_port = await self.http.start(self.address, self.http_port)
+            self.http_port = await self.http.start(self.address, self.http_port, ssl=ctx)
+        if self.read_only_port is not None:
+            self.ro_http = HTTPServer(self._http_readonly)
+            self.read_only_port = await self.ro_http.start(self.address, self.read_only_port)
+        if self.healthz_port is not None:
+            self.healthz_http = HTTPServer(self._http_healthz)
+            self.healthz_port = await self.healthz_http.start(self.healthz_address, self.healthz_port)
         await self.dm.start(self.active_pods)
         self.dm.add_capacity_listener(lambda r: self._status_dirty.set())
         if self.cgroup_root:
@@ -260,7 +300,9 @@ class Kubelet:
             self._tasks.append(asyncio.ensure_future(self._remove_orphans(self.orphan_grace)))
         if self.pod_manifest_path or self.manifest_url:
             from .config import StaticPodSource
-            self.static_pods = StaticPodSource(self, self.pod_manifest_path, url=self.manifest_url,
+            period = min([f for f, on in ((self.file_check_frequency, self.pod_manifest_path),
+                                          (self.http_check_frequency, self.manifest_url)) if on])
+            self.static_pods = StaticPodSource(self, self.pod_manifest_path, period=period, url=self.manifest_url,
                                                url_headers=self.manifest_url_headers)
             self.static_pods.start()
         if self.eviction is not None:
@@ -292,7 +334,7 @@ class Kubelet:
         last_conds = set()
         while not self._stopped:
             running = [s.pod for s in self.pods.values() if s.admitted and not s.terminated and not s.rejected]
-            victim, msg = self.eviction.select_victim(running)
+            victim, msg, grace = self.eviction.select_victim_with_grace(running)
             conds = set(self.eviction.conditions)
             if conds != last_conds:
                 last_conds = conds
@@ -301,7 +343,7 @@ class Kubelet:
                 st = self.pods.get(victim["metadata"]["uid"])
                 if st is not None:
                     self.recorder.event(victim, "Warning", "Evicted", msg)
-                    await self._kill_pod(st, 0)
+                    await self._kill_pod(st, grace)
                     await self._write_status(st, {"phase": core.POD_FAILED, "reason": "Evicted", "message": msg,
                                                   "conditions": (victim.get("status") or {}).get("conditions") or []})
             await asyncio.sleep(self.eviction_interval)
@@ -323,8 +365,9 @@ class Kubelet:
             self.hostports.close()
         await self.dm.stop()
         self.recorder.stop()
-        if self.http:
-            await self.http.stop()
+        for srv in (self.http, self.ro_http, self.healthz_http):
+            if srv:
+                await srv.stop()
 
     def active_pods(self):
         return [s.pod for s in self.pods.values() if not s.terminated and not s.rejected]
@@ -336,8 +379,15 @@ class Kubelet:
                   "beta.kubernetes.io/arch": "amd64"}
         labels.update(self.plugin_labels)
         labels.update(self.labels)
+        spec = {}
+        if self.register_taints:
+            spec["taints"] = [dict(t) for t in self.register_taints]
+        if not self.register_schedulable:
+            spec["unschedulable"] = True
+        if self.provider_id:
+            spec["providerID"] = self.provider_id
         node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node_name, "labels": labels},
-                "spec": {}, "status": self._node_status()}
+                "spec": spec, "status": self._node_status()}
         return node
 
     def _node_status(self):
@@ -367,7 +417,8 @@ class Kubelet:
                   {"type": "DiskPressure", "status": "True" if disk_p else "False",
                    "reason": "KubeletHasDiskPressure" if disk_p else "KubeletHasNoDiskPressure",
                    "lastHeartbeatTime": now, "lastTransitionTime": now}],
-              "addresses": [{"type": "InternalIP", "address": self.address}, {"type": "Hostname", "address": self.node_name}],
+              "addresses": [{"type": "InternalIP", "address": self.node_ip or self.address},
+                            {"type": "Hostname", "address": self.node_name}],
               "daemonEndpoints": {"kubeletEndpoint": {"Port": self.http_port or 0}},
               "nodeInfo": {"kubeletVersion": "v1.9.0-amd.0", "containerRuntimeVersion": f"{self.runtime.name}://1.0",
                            "operatingSystem": "linux", "architecture": "amd64", "machineID": self.node_name}}
@@ -388,7 +439,7 @@ class Kubelet:
         """`pkg/kubelet/cm/node_container_manager.go` GetNodeAllocatableReservation:
         allocatable = capacity − kube-reserved − system-reserved − hard eviction threshold
         (memory.available), floored at zero."""
-        if not any(self.reserved) and self.eviction is None:
+        if not any(self.reserved) and (self.eviction is None or self.allocatable_ignore_eviction):
             return dict(capacity)
         out = dict(capacity)
         for res in ("cpu", "memory", "ephemeral-storage"):
@@ -396,7 +447,7 @@ class Kubelet:
                 continue
             total = parse_quantity(str(capacity[res]))
             cut = sum(parse_quantity(str(r[res])).milli_value() for r in self.reserved if res in r)
-            if res == "memory" and self.eviction is not None:
+            if res == "memory" and self.eviction is not None and not self.allocatable_ignore_eviction:
                 cut += self.eviction.hard_memory_bytes() * 1000
             left = max(0, total.milli_value() - cut)
             out[res] = f"{left}m" if res == "cpu" else str(left // 1000)
@@ -660,8 +711,27 @@ class Kubelet:
         st.terminated = True
         await self._write_status(st, dict(status, conditions=(victim.get("status") or {}).get("conditions") or []))
 
+    def _can_run_pod(self, pod):
+        """`canRunPod`: privileged containers need --allow-privileged; host network / PID / IPC
+        need the pod's source in --host-{network,pid,ipc}-sources."""
+        spec = pod.get("spec") or {}
+        uid = pod["metadata"].get("uid", "")
+        if not self.allow_privileged:
+            for c in list(spec.get("containers") or ()) + list(spec.get("initContainers") or ()):
+                if (c.get("securityContext") or {}).get("privileged"):
+                    return "Forbidden", f"pod with UID {uid!r} specified privileged container, but is disallowed"
+        source = ((pod["metadata"].get("annotations") or {}).get("kubernetes.io/config.source") or "api")
+        for field, what in (("hostNetwork", "host networking"), ("hostPID", "host PID"), ("hostIPC", "host ipc")):
+            allowed = self.host_sources.get(field)
+            if spec.get(field) and allowed is not None and "*" not in allowed and source not in allowed:
+                return "Forbidden", f"pod with UID {uid!r} specified {what}, but is disallowed"
+        return None
+
     async def _admit(self, st: PodState):
         pod = st.pod
+        r = self._can_run_pod(pod)
+        if r is not None:
+            return r
         r = self.sysctls.admit(pod)
         if r is not None:
             return r
@@ -1403,12 +1473,33 @@ class Kubelet:
 
     # ------------------------------------------------------------------
     # HTTP (kubelet server :10250 subset)
+    # debugging handlers (`server.go` InstallDebuggingHandlers): absent from the read-only server
+    # and with --enable-debugging-handlers=false
+    DEBUG_PATHS = ("/run/", "/exec/", "/attach/", "/portForward/", "/containerLogs/", "/logs", "/runningpods",
+                   "/debug/pprof", "/configz", "/cri/")
+
     async def _http(self, req):
-        p = req.path
         if self.auth is not None:
             denied = await self.auth.check(req)
             if denied is not None:
                 return Response(denied[0], denied[1].encode(), "text/plain")
+        return await self._serve(req, self.debugging_handlers)
+
+    async def _http_readonly(self, req):
+        """--read-only-port: no authentication, GET only, no debugging handlers."""
+        if req.method not in ("GET", "HEAD"):
+            return Response(405, b"method not allowed", "text/plain")
+        return await self._serve(req, False)
+
+    async def _http_healthz(self, req):
+        if req.path in ("/healthz", "/healthz/ping"):
+            return Response(200, b"ok", "text/plain")
+        return Response(404, b"not found", "text/plain")
+
+    async def _serve(self, req, debugging):
+        p = req.path
+        if not debugging and p.startswith(self.DEBUG_PATHS):
+            return Response(404, b"not found", "text/plain")
         if p in ("/healthz", "/healthz/ping"):
             return Response(200, b"ok", "text/plain")
         if p == "/healthz/syncloop":

@@ -141,7 +141,10 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             rt_args = ["--container-runtime", "remote", "--container-runtime-endpoint", f"unix://{sock}"]
         kl = _spawn(["kubernetes_amd.cmd.kubelet", "--api-servers", url, "--hostname-override", "density-node",
                      "--root-dir", os.path.join(tmp, "kubelet"), "--port", "0",
-                     "--container-log-dir", "", "--max-pods", str(background + batch + sequential + 10)] + rt_args,
+                     "--container-log-dir", "", "--max-pods", str(background + batch + sequential + 10),
+                     # the run measures the kubelet's own CPU and startup latency, not the default
+                     # 5-QPS API client / registry throttles
+                     "--kube-api-qps", "100", "--kube-api-burst", "200", "--registry-qps", "0"] + rt_args,
                     tmp, "kubelet")
         procs.append(kl)
         c = Client(url)
