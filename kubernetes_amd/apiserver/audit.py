@@ -72,7 +72,19 @@ class Policy:
 
 
 class AuditLogger:
-    def __init__(self, path, policy: Policy | None = None, max_body=64 << 10, webhook=None):
+    """Log backend (`plugin/pkg/audit/log`): `format` json (one audit.k8s.io Event per line) or
+    legacy (the pre-1.8 `AUDIT: id=... ip=... method=... user=...` request line plus a
+    `response="<code>"` line); rotation like the reference's lumberjack writer — past
+    `max_size_mb` the file moves to `<name>-<UTC timestamp><ext>`, at most `max_backups` such
+    backups are kept and those older than `max_age_days` are removed (0 = no limit)."""
+
+    def __init__(self, path, policy: Policy | None = None, max_body=64 << 10, webhook=None, format="json",
+                 max_size_mb=0, max_backups=0, max_age_days=0):
+        if format not in ("json", "legacy"):
+            raise ValueError(f"unknown audit log format {format!r}")
+        self.format = format
+        self.max_size = int(max_size_mb) << 20
+        self.max_backups, self.max_age = int(max_backups), float(max_age_days) * 86400
         self.path = path
         self.policy = policy or Policy()
         self.max_body = max_body
@@ -131,16 +143,27 @@ class AuditLogger:
                 ev["responseObject"] = json.loads(response_body)
             except ValueError:
                 pass
-        line = json.dumps(ev, separators=(",", ":"))
+        if self.format == "legacy":
+            u = ev["user"]
+            groups = ",".join(f'\\"{g}\\"' for g in u["groups"])
+            line = (f'{ev["requestReceivedTimestamp"]} AUDIT: id="{ev["auditID"]}" ip="{ev["sourceIPs"][0]}" '
+                    f'method="{method}" user="{u["username"]}" groups="{groups}" as="<self>" asgroups="<lookup>" '
+                    f'namespace="{parsed_ns or "<none>"}" uri="{uri}"\n'
+                    f'{ev["stageTimestamp"]} AUDIT: id="{ev["auditID"]}" response="{code}"')
+        else:
+            line = json.dumps(ev, separators=(",", ":"))
+        flush_now = False
         with self._lock:
             self._buf.append(line)
             if not self._scheduled:
                 self._scheduled = True
                 try:
                     asyncio.get_running_loop().call_soon(self.flush)
-                except RuntimeError:
+                except RuntimeError:       # no event loop (tools, tests): write through
                     self._scheduled = False
-                    self.flush()
+                    flush_now = True
+        if flush_now:
+            self.flush()                   # outside the (non-reentrant) lock flush() takes
 
     def flush(self):
         with self._lock:
@@ -150,12 +173,31 @@ class AuditLogger:
             return
         data = "\n".join(buf) + "\n"
         if self.f is not None:
+            if self.max_size and self.f.tell() + len(data) > self.max_size and self.f.tell() > 0:
+                self._rotate()
             self.f.write(data)
             self.f.flush()
         elif self.stdout:
             os.write(1, data.encode())
         if self.webhook is not None:
             self.webhook.enqueue(buf)
+
+    def _rotate(self):
+        import glob
+        import time as _time
+        self.f.close()
+        base, ext = os.path.splitext(self.path)
+        stamp = _time.strftime("%Y-%m-%dT%H-%M-%S", _time.gmtime()) + f".{int(_time.time() * 1000) % 1000:03d}"
+        os.replace(self.path, f"{base}-{stamp}{ext}")
+        backups = sorted(glob.glob(f"{glob.escape(base)}-*{ext}"), key=os.path.getmtime, reverse=True)
+        now = _time.time()
+        for i, b in enumerate(backups):
+            if (self.max_backups and i >= self.max_backups) or (self.max_age and now - os.path.getmtime(b) > self.max_age):
+                try:
+                    os.unlink(b)
+                except OSError:
+                    pass
+        self.f = open(self.path, "a", buffering=1 << 16)
 
     def close(self):
         self.flush()

@@ -88,6 +88,8 @@ class RBACAuthorizer:
 
     def __init__(self, server):
         self.server = server
+        # --authorization-rbac-super-user: this user passes every RBAC check
+        self.super_user = getattr(server, "rbac_super_user", None)
 
     def _subject_matches(self, s, user):
         k = s.get("kind")
@@ -109,7 +111,7 @@ class RBACAuthorizer:
 
     def authorize(self, a):
         u = a.user
-        if "system:masters" in (u.groups or []):
+        if "system:masters" in (u.groups or []) or (self.super_user and u.name == self.super_user):
             return True, ""
         for b in self.server.list_objects("clusterrolebindings"):
             if any(self._subject_matches(s, u) for s in b.get("subjects") or ()):
@@ -305,7 +307,11 @@ def build_authorizer(modes, server):
         elif m == "ABAC":
             azs.append(ABACAuthorizer(getattr(server, "abac_policy_file", None)))
         elif m == "Webhook":
-            azs.append(WebhookAuthorizer(getattr(server, "authorization_webhook_url", None)))
+            cfg = getattr(server, "authz_webhook", None)
+            if cfg is not None:       # --authorization-webhook-config-file (kubeconfig format)
+                azs.append(WebhookAuthorizer(cfg[0], cfg[2], cfg[3], cfg[1]))
+            else:
+                azs.append(WebhookAuthorizer(getattr(server, "authorization_webhook_url", None)))
         else:
             raise ValueError(f"unknown authorization mode {m}")
     return UnionAuthorizer(azs)

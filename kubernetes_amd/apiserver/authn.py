@@ -97,12 +97,40 @@ def jwt_verify(pub_pems, token: str):
     return None
 
 
+def _peer_pem(req):
+    t = getattr(req, "transport", None)
+    so = t.get_extra_info("ssl_object") if t is not None else None
+    der = so.getpeercert(binary_form=True) if so is not None else None
+    if not der:
+        return None
+    import ssl as _ssl
+    return _ssl.DER_cert_to_PEM_cert(der)
+
+
+def _cn(cert):
+    for rdn in cert.get("subject") or ():
+        for k, v in rdn:
+            if k == "commonName":
+                return v
+    return ""
+
+
 class X509Authenticator:
+    """`--client-ca-file`. With `ca_pem` the peer certificate must chain to that CA (the TLS
+    listener also trusts the front-proxy CA, whose certificates are not user credentials)."""
+
+    def __init__(self, ca_pem=None):
+        self.ca_pem = ca_pem
+
     def authenticate_request(self, req):
         t = getattr(req, "transport", None)
         cert = t.get_extra_info("peercert") if t is not None else None
         if not cert:
             return None
+        if self.ca_pem:
+            pem = _peer_pem(req)
+            if pem is None or not crypto.verify_cert(pem, self.ca_pem)[0]:
+                return None
         cn, orgs = "", []
         for rdn in cert.get("subject") or ():
             for k, v in rdn:
@@ -113,6 +141,69 @@ class X509Authenticator:
         if not cn:
             return None
         return User(cn, "", orgs + ["system:authenticated"])
+
+
+class RequestHeaderAuthenticator:
+    """Front-proxy authentication (`--requestheader-*`, `authenticatorfactory/requestheader.go`):
+    a client certificate signed by `--requestheader-client-ca-file` (with a CN in
+    `--requestheader-allowed-names`, when given) vouches for the user named in the first
+    non-empty `--requestheader-username-headers` header (X-Remote-User), its groups
+    (X-Remote-Group, repeatable) and extras (X-Remote-Extra-<key>)."""
+
+    def __init__(self, ca_pem, allowed_names=(), username_headers=("X-Remote-User",),
+                 group_headers=("X-Remote-Group",), extra_prefixes=("X-Remote-Extra-",)):
+        self.ca_pem = ca_pem
+        self.allowed = set(allowed_names or ())
+        self.user_h = [h.lower() for h in username_headers]
+        self.group_h = [h.lower() for h in group_headers]
+        self.extra_p = [h.lower() for h in extra_prefixes]
+
+    def authenticate_request(self, req):
+        t = getattr(req, "transport", None)
+        cert = t.get_extra_info("peercert") if t is not None else None
+        if not cert:
+            return None
+        name = next((req.headers.get(h) for h in self.user_h if req.headers.get(h)), None)
+        if not name:
+            return None
+        pem = _peer_pem(req)
+        if pem is None or not crypto.verify_cert(pem, self.ca_pem)[0]:
+            return None
+        if self.allowed and _cn(cert) not in self.allowed:
+            return None
+        groups = []
+        for h in self.group_h:
+            v = req.headers.get(h)
+            if v:
+                groups += [g.strip() for g in v.split(",") if g.strip()]   # repeated headers arrive joined
+        return User(name, "", groups + ["system:authenticated"])
+
+
+class BasicAuthenticator:
+    """`--basic-auth-file`: CSV password,user,uid[,"group1,group2"]; `Authorization: Basic`."""
+
+    def __init__(self, path):
+        import csv
+        self.users = {}
+        with open(path) as f:
+            for row in csv.reader(f):
+                if len(row) < 3 or row[0].startswith("#"):
+                    continue
+                groups = [g for g in (row[3].split(",") if len(row) > 3 else []) if g]
+                self.users[row[1]] = (row[0], User(row[1], row[2], groups + ["system:authenticated"]))
+
+    def authenticate_request(self, req):
+        h = req.headers.get("authorization", "")
+        if not h.lower().startswith("basic "):
+            return None
+        try:
+            user, _, pw = base64.b64decode(h[6:].strip()).decode().partition(":")
+        except (ValueError, UnicodeDecodeError):
+            return False
+        rec = self.users.get(user)
+        if rec is None or not hmac.compare_digest(rec[0], pw):
+            return False
+        return rec[1]
 
 
 def _secret_data(sec, key):
@@ -226,6 +317,8 @@ class UnionAuthenticator:
     def authenticate_request(self, req):
         for a in self.req_auth:
             u = a.authenticate_request(req)
+            if u is False:
+                return None          # credentials presented and rejected (basic auth): 401
             if u is not None:
                 return u
         return self.authenticate(req.headers)

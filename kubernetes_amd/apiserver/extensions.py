@@ -352,11 +352,15 @@ class Aggregator:
         if scheme == "https":
             ctx = ssl.create_default_context(cadata=base64.b64decode(sp["caBundle"]).decode())
             ctx.check_hostname = False
+            pc = getattr(self.server, "proxy_client_cert", None)
+            if pc:       # --proxy-client-cert-file/--proxy-client-key-file: the front-proxy identity
+                ctx.load_cert_chain(pc[0], pc[1])
         c = HTTPClient(f"{scheme}://{be[0]}:{be[1]}", ssl_context=ctx)
         u = getattr(req, "user", None)
         hdrs = {"X-Remote-User": getattr(u, "name", "") or ""}
-        for g in getattr(u, "groups", ()) or ():
-            hdrs.setdefault("X-Remote-Group", g)
+        groups = list(getattr(u, "groups", ()) or ())
+        if groups:       # one header, values comma-joined (what repeated headers become on the wire)
+            hdrs["X-Remote-Group"] = ", ".join(groups)
         try:
             path = req.raw_path + (("?" + req.qs) if req.qs else "")
             st, body = await c.request(req.method, path, req.body or None,

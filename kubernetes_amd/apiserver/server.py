@@ -46,7 +46,7 @@ from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResp
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
 from . import admission as adm
-from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, build_authorizer
+from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, User, build_authorizer
 from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, event_bytes
 from .registry import (APIError, already_exists, apply_binding, bad_request, conflict, deletion_stamp,
                        init_object_meta, invalid, not_found, strategy_for)
@@ -73,6 +73,63 @@ class _Stale(Exception):
     def __init__(self, rev):
         super().__init__(rev)
         self.rev = rev
+
+
+# the insecure port's user (`insecure_handler.go`: no authentication, no authorization)
+UNSECURED = User("system:unsecured", "", ["system:masters", "system:authenticated"])
+SWAGGER_UI_PAGE = (b"<!DOCTYPE html><html><head><title>kube-apiserver API</title></head><body>"
+                   b"<h1>kube-apiserver</h1><p>OpenAPI: <a href=\"/swagger.json\">/swagger.json</a> "
+                   b"(<a href=\"/openapi/v2\">/openapi/v2</a>)</p></body></html>")
+
+
+_TIMEOUT_RESPONSE = Response(504, codec.dumpb({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
+                                              "message": "Timeout: request did not complete within allowed duration",
+                                              "reason": "Timeout", "details": {}, "code": 504}))
+
+
+def node_address(node, preferred=("InternalIP", "ExternalIP", "Hostname")):
+    """`--kubelet-preferred-address-types`: the first node address of the first listed type."""
+    addrs = ((node or {}).get("status") or {}).get("addresses") or ()
+    for t in preferred:
+        for a in addrs:
+            if a.get("type") == t and a.get("address"):
+                return a["address"]
+    return "127.0.0.1"
+
+
+def parse_runtime_config(spec):
+    """`--runtime-config` (`pkg/master/master.go` DefaultAPIResourceConfigSource + overrides):
+    `api/all=false`, `api/legacy=false` (core v1), `<group>/<version>=false|true`,
+    `extensions/v1beta1/<resource>=false`; a bare key means true. -> (disabled {(group, version)},
+    disabled {(group, version, resource)})."""
+    if isinstance(spec, dict):
+        items = list(spec.items())
+    else:
+        items = []
+        for part in (spec or "").split(","):
+            part = part.strip()
+            if part:
+                k, _, v = part.partition("=")
+                items.append((k, v or "true"))
+    all_gv = {(g, v) for g, vs in m.served_versions().items() for v in vs}
+    disabled, disabled_res = set(), set()
+    for k, v in items:
+        on = str(v).lower() in ("true", "1", "")
+        if k in ("api/all", "api/*"):
+            disabled = set() if on else set(all_gv)
+            continue
+        if k in ("api/legacy", "api/v1", "v1"):
+            gvs = {("", "v1")}
+        else:
+            bits = k.split("/")
+            if len(bits) == 3:
+                (disabled_res.discard if on else disabled_res.add)((bits[0], bits[1], bits[2]))
+                continue
+            if len(bits) != 2:
+                raise ValueError(f"invalid --runtime-config key {k!r}")
+            gvs = {(bits[0], bits[1])}
+        disabled = (disabled - gvs) if on else (disabled | gvs)
+    return disabled, disabled_res
 
 
 def q_include(req):
@@ -146,8 +203,48 @@ class APIServer:
                  service_account_lookup=True, enable_bootstrap_token_auth=False, authentication_token_webhook=None,
                  anonymous_auth=True, authorization_policy_file=None, authorization_webhook_url=None, oidc=None,
                  component_endpoints=None, event_ttl=3600.0, kubelet_https=False, kubelet_certificate_authority=None,
-                 kubelet_client_certificate=None, kubelet_client_key=None):
+                 kubelet_client_certificate=None, kubelet_client_key=None, basic_auth_file=None, requestheader=None,
+                 authentication_token_webhook_config_file=None, authentication_token_webhook_cache_ttl=120.0,
+                 authorization_webhook_config_file=None, authorization_webhook_cache_authorized_ttl=300.0,
+                 authorization_webhook_cache_unauthorized_ttl=30.0, authorization_rbac_super_user=None,
+                 cors_allowed_origins=(), request_timeout=None, min_request_timeout=1800.0, enable_logs_handler=True,
+                 enable_swagger_ui=False, log_dir="/var/log", runtime_config=None, allow_privileged=True,
+                 kubelet_preferred_address_types=("InternalIP", "ExternalIP", "Hostname", "InternalDNS", "ExternalDNS"),
+                 kubelet_port=10250, kubelet_timeout=5.0, advertise_address=None, apiserver_count=1,
+                 endpoint_reconciler_type="master-count", kubernetes_service_node_port=0, proxy_client_cert=None):
+        self.proxy_client_cert = proxy_client_cert          # (cert file, key file) for aggregated API servers
         self.abac_policy_file = authorization_policy_file
+        # --runtime-config: group/versions (and extensions/v1beta1 resources) switched off; every
+        # served version is on by default here (the reference leaves alpha versions off)
+        self.disabled_gv, self.disabled_res = parse_runtime_config(runtime_config)
+        # --allow-privileged=false: privileged containers fail validation ("disallowed by cluster policy")
+        self.allow_privileged = allow_privileged
+        self.kubelet_address_types = tuple(kubelet_preferred_address_types)
+        self.kubelet_port, self.kubelet_timeout = kubelet_port, kubelet_timeout
+        # master endpoints (`pkg/master/controller.go`, reconcilers.go): --advertise-address,
+        # --apiserver-count (master-count keeps that many addresses), none = not reconciled
+        self.advertise_address = advertise_address
+        self.apiserver_count = max(1, int(apiserver_count))
+        if endpoint_reconciler_type not in ("master-count", "lease", "none"):
+            raise ValueError(f"unknown endpoint reconciler {endpoint_reconciler_type!r}")
+        self.endpoint_reconciler = endpoint_reconciler_type
+        self.kubernetes_service_node_port = kubernetes_service_node_port
+        # --cors-allowed-origins (regular expressions), --request-timeout (non-long-running requests
+        # answer 504 after it; None = off), --min-request-timeout (watches without timeoutSeconds
+        # end after a random time in [t, 2t)), --enable-logs-handler, --enable-swagger-ui
+        import re as _re
+        self.cors = [_re.compile(o) for o in cors_allowed_origins or ()]
+        self.request_timeout = request_timeout
+        self.min_request_timeout = min_request_timeout
+        self.enable_logs_handler, self.enable_swagger_ui, self.log_dir = enable_logs_handler, enable_swagger_ui, log_dir
+        self.requestheader = requestheader or None
+        self.rbac_super_user = authorization_rbac_super_user
+        self.authz_webhook = None
+        if authorization_webhook_config_file:
+            from ..client import clientcmd
+            r = clientcmd.resolve(clientcmd.load(authorization_webhook_config_file)[0])
+            self.authz_webhook = (r.server, r.ssl_context, authorization_webhook_cache_authorized_ttl,
+                                  authorization_webhook_cache_unauthorized_ttl)
         # kubelet connections (--kubelet-https, --kubelet-certificate-authority,
         # --kubelet-client-certificate/key; `pkg/kubelet/client` MakeTransport): without a CA the
         # kubelet's serving certificate is not verified, as in the reference
@@ -205,7 +302,8 @@ class APIServer:
         self.initializers_enabled = "Initializers" in names
         self.authn = None
         if token_file or tokens or client_ca_file or service_account_key_files or enable_bootstrap_token_auth \
-                or authentication_token_webhook or not anonymous_auth or oidc:
+                or authentication_token_webhook or not anonymous_auth or oidc or basic_auth_file or requestheader \
+                or authentication_token_webhook_config_file:
             from . import authn as an
             from ..native import crypto as _crypto
             toks = [TokenAuthenticator(token_file, tokens)] if (token_file or tokens) else []
@@ -218,16 +316,41 @@ class APIServer:
                         keys.append(_crypto.public_key(fh.read()))
                 toks.append(an.ServiceAccountAuthenticator(keys, self, service_account_lookup))
             if authentication_token_webhook:
-                toks.append(an.WebhookTokenAuthenticator(authentication_token_webhook))
+                toks.append(an.WebhookTokenAuthenticator(authentication_token_webhook, authentication_token_webhook_cache_ttl))
+            if authentication_token_webhook_config_file:
+                from ..client import clientcmd
+                r = clientcmd.resolve(clientcmd.load(authentication_token_webhook_config_file)[0])
+                toks.append(an.WebhookTokenAuthenticator(r.server, authentication_token_webhook_cache_ttl, r.ssl_context))
             if oidc:
                 toks.append(oidc if isinstance(oidc, an.OIDCAuthenticator) else an.OIDCAuthenticator(**oidc))
-            self.authn = an.UnionAuthenticator([an.X509Authenticator()] if client_ca_file else [], toks, anonymous_auth)
+            # request authenticators in the reference's order: front proxy, x509, basic auth
+            reqs = []
+            if requestheader:
+                with open(requestheader["client_ca_file"]) as f:
+                    rh_ca = f.read()
+                reqs.append(an.RequestHeaderAuthenticator(
+                    rh_ca, requestheader.get("allowed_names") or (),
+                    requestheader.get("username_headers") or ("X-Remote-User",),
+                    requestheader.get("group_headers") or ("X-Remote-Group",),
+                    requestheader.get("extra_headers_prefix") or ("X-Remote-Extra-",)))
+            if client_ca_file:
+                ca_pem = None
+                if requestheader:       # the listener trusts both CAs: bind x509 users to the client CA
+                    with open(client_ca_file) as f:
+                        ca_pem = f.read()
+                reqs.append(an.X509Authenticator(ca_pem))
+            if basic_auth_file:
+                reqs.append(an.BasicAuthenticator(basic_auth_file))
+            self.authn = an.UnionAuthenticator(reqs, toks, anonymous_auth)
         self.authz = build_authorizer(authorization_modes, self)
         self.max_inflight = max_requests_inflight
         self.max_mutating = max_mutating_inflight
         self.inflight = 0
         self.inflight_mut = 0
-        self.http = HTTPServer(self.handle)
+        self.http = HTTPServer(self._entry if self.cors else self.handle, request_timeout=self.request_timeout,
+                               long_running=self._long_running, timeout_response=_TIMEOUT_RESPONSE)
+        self.insecure_http = None
+        self.insecure_port = None
         self.kubelet_port_resolver = kubelet_port_resolver
         self.audit = audit            # audit.AuditLogger or None
         self.enable_profiling = True  # --profiling (reference default true)
@@ -344,6 +467,9 @@ class APIServer:
                                 "labels": {"component": "apiserver", "provider": "kubernetes"}},
                    "spec": {"clusterIP": self.svc_alloc.kubernetes_ip, "type": "ClusterIP", "sessionAffinity": "None",
                             "ports": [{"name": "https", "port": 443, "protocol": "TCP", "targetPort": 6443}]}}
+            if self.kubernetes_service_node_port:     # --kubernetes-service-node-port
+                svc["spec"]["type"] = "NodePort"
+                svc["spec"]["ports"][0]["nodePort"] = self.kubernetes_service_node_port
             try:
                 await self._retrying(lambda: self.create(m.BY_PLURAL["services"], "default", svc, admit=False))
             except APIError as e:
@@ -752,6 +878,14 @@ class APIServer:
             await self.webhooks.run(a, ri, False)
 
     def _validate_new(self, ri, strat, obj, old=None):
+        if not self.allow_privileged and ri.plural == "pods":
+            from ..api.validation import FieldError
+            spec = obj.get("spec") or {}
+            bad = [FieldError("Forbidden", f"spec.{key}[{i}].securityContext.privileged", "disallowed by cluster policy")
+                   for key in ("initContainers", "containers") for i, c in enumerate(spec.get(key) or ())
+                   if (c.get("securityContext") or {}).get("privileged")]
+            if bad:
+                return bad + list(strat.validate(obj) if old is None else strat.validate_update(obj, old))
         if ri.plural == "customresourcedefinitions":
             from .extensions import validate_crd
             errs = validate_crd(obj)
@@ -1021,11 +1155,52 @@ class APIServer:
             if ca:
                 ctx.verify_mode = ssl.CERT_OPTIONAL    # x509 client-certificate authentication
                 ctx.load_verify_locations(ca)
+            if self.requestheader:
+                ctx.verify_mode = ssl.CERT_OPTIONAL    # front-proxy client certificates
+                ctx.load_verify_locations(self.requestheader["client_ca_file"])
         port = await self.http.start(host, port, ssl=ctx, reuse_port=reuse_port)
         await self._reconcile_master_endpoints("127.0.0.1" if host in ("0.0.0.0", "") else host, port)
         if self.event_ttl and self._reaper is None:
             self._reaper = asyncio.ensure_future(self._event_reaper())
         return port
+
+    async def start_insecure(self, host="127.0.0.1", port=0, reuse_port=False):
+        """--insecure-port / --insecure-bind-address: plain HTTP with no authentication or
+        authorization (requests run as system:unsecured in system:masters), served beside the
+        secure port (`pkg/kubeapiserver/server/insecure_handler.go`)."""
+        async def handler(req):
+            req.insecure = True
+            return await self._entry(req)
+        self.insecure_http = HTTPServer(handler, request_timeout=self.request_timeout, long_running=self._long_running,
+                                        timeout_response=_TIMEOUT_RESPONSE)
+        self.insecure_port = await self.insecure_http.start(host, port, reuse_port=reuse_port)
+        return self.insecure_port
+
+    # long-running requests (`server/filters/longrunning.go`): no --request-timeout
+    _LONG_RUNNING = frozenset(("proxy", "log", "exec", "attach", "portforward"))
+
+    def _long_running(self, req):
+        if req.query.get("watch") in ("true", "1") or "/watch/" in req.path or req.query.get("follow") in ("true", "1"):
+            return True
+        return any(seg in self._LONG_RUNNING for seg in req.path.split("/")) or \
+            "upgrade" in req.headers.get("connection", "").lower()
+
+    def _cors_headers(self, origin):
+        if not any(r.search(origin) for r in self.cors):
+            return None
+        return {"Access-Control-Allow-Origin": origin,
+                "Access-Control-Allow-Methods": "POST, GET, OPTIONS, PUT, DELETE, PATCH",
+                "Access-Control-Allow-Headers": "Content-Type, Content-Length, Accept-Encoding, X-CSRF-Token, Authorization",
+                "Access-Control-Expose-Headers": "Date", "Access-Control-Allow-Credentials": "true"}
+
+    async def _entry(self, req):
+        """HTTP entry with the CORS filter (the request timeout lives in the HTTP server)."""
+        resp = await self.handle(req)
+        if self.cors and req.headers.get("origin") and isinstance(resp, Response):
+            extra = self._cors_headers(req.headers["origin"])
+            if extra:
+                resp.headers = dict(resp.headers or {}, **extra)
+        return resp
 
     def expired_events(self, now=None):
         """Events whose last write (lastTimestamp, else creationTimestamp) is older than the TTL."""
@@ -1068,10 +1243,21 @@ class APIServer:
                 log.warning("event TTL reaper pass failed: %s", e)
 
     async def _reconcile_master_endpoints(self, ip, port):
-        """Endpoints of the `kubernetes` service = this API server (master EndpointReconciler)."""
-        subsets = [{"addresses": [{"ip": ip}], "ports": [{"name": "https", "port": port, "protocol": "TCP"}]}]
-        ri = m.BY_PLURAL["endpoints"]
+        """Endpoints of the `kubernetes` service = the API servers (master-count reconciler: this
+        server's advertise address joins the existing ones, at most --apiserver-count kept)."""
+        if self.endpoint_reconciler == "none":
+            return
+        ip = self.advertise_address or ip
         cur = self.get_object("endpoints", "default", "kubernetes")
+        addrs = [{"ip": ip}]
+        if cur is not None and self.apiserver_count > 1:
+            for ss in cur.get("subsets") or ():
+                for a in ss.get("addresses") or ():
+                    if a.get("ip") != ip and len(addrs) < self.apiserver_count:
+                        addrs.append({"ip": a["ip"]})
+        addrs.sort(key=lambda a: a["ip"])
+        subsets = [{"addresses": addrs, "ports": [{"name": "https", "port": port, "protocol": "TCP"}]}]
+        ri = m.BY_PLURAL["endpoints"]
         try:
             if cur is None:
                 await self._retrying(lambda: self.create(ri, "default", {"metadata": {"name": "kubernetes", "namespace": "default"},
@@ -1088,6 +1274,8 @@ class APIServer:
             self._reaper.cancel()
             self._reaper = None
         await self.http.stop()
+        if self.insecure_http is not None:
+            await self.insecure_http.stop()
         if self.rstore is not None:
             self.store_healthy = False   # a deliberate close, not a store failure
             await self.rstore.close()
@@ -1135,6 +1323,9 @@ class APIServer:
             return None
         if ri.version != version and not aliased:
             return None
+        if self.disabled_gv and (group, version) in self.disabled_gv or \
+                self.disabled_res and (group, version, plural) in self.disabled_res:
+            return None                 # --runtime-config switched it off
         name = rest[1] if len(rest) > 1 else None
         sub = "/".join(rest[2:]) if len(rest) > 2 else ""
         return (ri, ns, name, sub, watch)
@@ -1161,14 +1352,34 @@ class APIServer:
                 resp = await handle_debug(req)
                 code = resp.status
                 return resp
+            if self.cors and req.headers.get("origin"):
+                cors = self._cors_headers(req.headers["origin"])
+                if cors is not None and verb == "OPTIONS":
+                    code = 204
+                    return Response(204, b"", "text/plain", headers=cors)
+            if p == "/logs" or p.startswith("/logs/"):
+                if not self.enable_logs_handler:
+                    code = 404
+                    return _json(404, m.status_obj(404, "NotFound", "the server could not find the requested resource"))
+            if p.rstrip("/") == "/swagger-ui" and self.enable_swagger_ui:
+                code = 200
+                return Response(200, SWAGGER_UI_PAGE, "text/html")
             user = ANONYMOUS
-            if self.authn is not None:
+            if getattr(req, "insecure", False):
+                user = UNSECURED
+            elif self.authn is not None:
                 ar = getattr(self.authn, "authenticate_request", None)
                 user = ar(req) if ar is not None else self.authn.authenticate(req.headers)
                 if user is None:
                     code = 401
                     return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))
             req.user = user
+            if p == "/logs" or p.startswith("/logs/"):
+                self._authorize(user, "get", None, "", "", "", "", p, resource_request=False)
+                from ..utils.httpserver import log_dir_response
+                resp = log_dir_response(self.log_dir, p[len("/logs"):].lstrip("/"))
+                code = resp.status
+                return resp
             if p in ("/openapi/v2", "/swagger.json", "/swagger-2.0.0.json"):
                 schemas = {}
                 for plural, sch in self.crds.schemas.items():
@@ -1307,8 +1518,11 @@ class APIServer:
             if self.audit is not None and resource:
                 self.audit.log(req, verb, resource, sub, code)
 
-    def _authorize(self, user, verb, ns, resource, sub, name, group, path):
-        ok, why = self.authz.authorize(AttributesRecord(user, verb, ns or "", resource, sub, name or "", group, path))
+    def _authorize(self, user, verb, ns, resource, sub, name, group, path, resource_request=True):
+        if user is UNSECURED:
+            return                  # the insecure port has no authorization
+        ok, why = self.authz.authorize(AttributesRecord(user, verb, ns or "", resource, sub, name or "", group, path,
+                                                        resource_request))
         if not ok:
             raise APIError(403, "Forbidden", why or "forbidden")
 
@@ -1630,6 +1844,10 @@ class APIServer:
             fsel = (fsel + "," if fsel else "") + f"metadata.name={name}"
         fsel = self._hide_uninitialized(q, fsel)
         timeout = float(q.get("timeoutSeconds") or 0) or None
+        if timeout is None and self.min_request_timeout:
+            # `watch.go` serveWatch: timeout = minRequestTimeout * (1 + rand) when unspecified
+            import random
+            timeout = self.min_request_timeout * (1.0 + random.random())
         shard = self._shard(q)
         reqs = self._fanout_spec(req, ri, ns, q.get("labelSelector"), fsel, shard)
         if reqs is not None:
@@ -1682,11 +1900,9 @@ class APIServer:
         if not node:
             raise bad_request(f"pod {name} is not scheduled")
         nobj = self.get_object("nodes", None, node)
-        port = ((nobj or {}).get("status") or {}).get("daemonEndpoints", {}).get("kubeletEndpoint", {}).get("Port")
-        addr = "127.0.0.1"
-        for a in ((nobj or {}).get("status") or {}).get("addresses") or ():
-            if a.get("type") == "InternalIP":
-                addr = a.get("address")
+        port = ((nobj or {}).get("status") or {}).get("daemonEndpoints", {}).get("kubeletEndpoint", {}).get("Port") \
+            or (self.kubelet_port if nobj is not None else None)
+        addr = node_address(nobj, self.kubelet_address_types)
         if not port:
             raise APIError(503, "ServiceUnavailable", f"node {node} has no kubelet endpoint")
         return pod, addr, port
@@ -1792,7 +2008,8 @@ class APIServer:
     async def _pod_log(self, ns, name, q):
         _, addr, port = await self._kubelet_of(ns, name)
         from ..client.http import HTTPClient
-        c = HTTPClient(f"{self.kubelet_scheme}://{addr}:{port}", ssl_context=self.kubelet_ssl)
+        c = HTTPClient(f"{self.kubelet_scheme}://{addr}:{port}", ssl_context=self.kubelet_ssl,
+                       timeout=max(self.kubelet_timeout, 30.0))
         try:
             qs = "&".join(f"{k}={v}" for k, v in q.items())
             st, body = await c.request("GET", f"/containerLogs/{ns}/{name}/{q.get('container', '')}" + (f"?{qs}" if qs else ""))
@@ -1803,9 +2020,12 @@ class APIServer:
     def _discovery(self, parsed):
         kind = parsed[1]
         if kind == "api":
+            if ("", "v1") in self.disabled_gv:
+                return _json(200, {"kind": "APIVersions", "versions": [], "serverAddressByClientCIDRs": []})
             return _json(200, {"kind": "APIVersions", "versions": ["v1"],
                                "serverAddressByClientCIDRs": [{"clientCIDR": "0.0.0.0/0", "serverAddress": "127.0.0.1"}]})
-        groups = {g: set(vs) for g, vs in m.served_versions().items() if g}
+        groups = {g: {v for v in vs if (g, v) not in self.disabled_gv} for g, vs in m.served_versions().items() if g}
+        groups = {g: vs for g, vs in groups.items() if vs}
         for g, vs in self.aggregator.groups().items():
             groups.setdefault(g, set()).update(vs)
 
@@ -1826,8 +2046,12 @@ class APIServer:
                                "preferredVersion": {"groupVersion": f"{g}/{vs[0]}", "version": vs[0]}})
         group, version = parsed[2], parsed[3]
         res = []
+        if (group, version) in self.disabled_gv:
+            raise APIError(404, "NotFound", f"{group}/{version} not found")
         for ri in m.RESOURCES:
             if not ((ri.group == group and ri.version == version) or (group, version, ri.plural) in m.ALIASES):
+                continue
+            if (group, version, ri.plural) in self.disabled_res:
                 continue
             verbs = ["create", "delete", "deletecollection", "get", "list", "patch", "update", "watch"]
             res.append({"name": ri.plural, "singularName": "", "namespaced": ri.namespaced, "kind": ri.kind,

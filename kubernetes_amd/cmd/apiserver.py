@@ -82,6 +82,7 @@ def _parser():
     ap.add_argument("--audit-webhook-config-file", default=None, help="kubeconfig naming the audit webhook")
     ap.add_argument("--audit-webhook-batch-max-size", type=int, default=400)
     ap.add_argument("--audit-webhook-batch-max-wait", type=float, default=1.0)
+    _reference_flags(ap)
     ap.add_argument("-v", type=int, default=0)
     return ap
 
@@ -199,6 +200,127 @@ def _duration(v):
     return parse_duration(v)
 
 
+def _bool(v):
+    return str(v).lower() not in ("false", "0", "no")
+
+
+def _csv(v):
+    return [x.strip() for x in (v or "").split(",") if x.strip()]
+
+
+def _reference_flags(ap):
+    """The rest of kube-apiserver's flags (cmd/kube-apiserver/app/options, generic server and
+    kubeapiserver options). Flags for subsystems that do not exist here are accepted and marked."""
+    g = ap.add_argument_group("serving")
+    g.add_argument("--secure-port", type=int, default=0,
+                   help="TLS listener with authentication (0 = single-listener mode on --port; the reference defaults to 6443)")
+    g.add_argument("--insecure-port", dest="port", type=int, help="alias of --port (the insecure listener)")
+    g.add_argument("--insecure-bind-address", "--address", dest="insecure_bind_address", default="127.0.0.1")
+    g.add_argument("--cert-dir", default="/var/run/kubernetes", help="self-signed serving pair when --tls-cert-file is unset")
+    g.add_argument("--advertise-address", default=None, help="IP published in the kubernetes service endpoints")
+    g.add_argument("--apiserver-count", type=int, default=1)
+    g.add_argument("--endpoint-reconciler-type", default="master-count", choices=["master-count", "lease", "none"])
+    g.add_argument("--kubernetes-service-node-port", type=int, default=0)
+    g.add_argument("--cors-allowed-origins", default="", help="comma-separated origin regular expressions")
+    g.add_argument("--request-timeout", default="1m", help="non-long-running requests answer 504 after this ('0' = off)")
+    g.add_argument("--min-request-timeout", type=int, default=1800,
+                   help="watches without timeoutSeconds end after a random time in [t, 2t)")
+    g.add_argument("--enable-logs-handler", type=_bool, default=True, help="/logs serves the API server's /var/log")
+    g.add_argument("--enable-swagger-ui", type=_bool, default=False)
+    g.add_argument("--profiling", type=_bool, default=True)
+    g.add_argument("--runtime-config", default="", help="api/all=false, <group>/<version>=true|false, ...")
+    g.add_argument("--allow-privileged", type=_bool, default=False)
+    g = ap.add_argument_group("authentication / authorization")
+    g.add_argument("--basic-auth-file", default=None)
+    g.add_argument("--requestheader-client-ca-file", default=None)
+    g.add_argument("--requestheader-allowed-names", default="")
+    g.add_argument("--requestheader-username-headers", default="")
+    g.add_argument("--requestheader-group-headers", default="")
+    g.add_argument("--requestheader-extra-headers-prefix", default="")
+    g.add_argument("--proxy-client-cert-file", default=None, help="client certificate for aggregated API servers")
+    g.add_argument("--proxy-client-key-file", default=None)
+    g.add_argument("--authentication-token-webhook-config-file", default=None, help="kubeconfig of the TokenReview webhook")
+    g.add_argument("--authentication-token-webhook-cache-ttl", default="2m")
+    g.add_argument("--authorization-webhook-config-file", default=None, help="kubeconfig of the SubjectAccessReview webhook")
+    g.add_argument("--authorization-webhook-cache-authorized-ttl", default="5m")
+    g.add_argument("--authorization-webhook-cache-unauthorized-ttl", default="30s")
+    g.add_argument("--authorization-rbac-super-user", default=None)
+    g = ap.add_argument_group("kubelet connections")
+    g.add_argument("--kubelet-preferred-address-types", default="InternalIP,ExternalIP,Hostname,InternalDNS,ExternalDNS")
+    g.add_argument("--kubelet-port", type=int, default=10250)
+    g.add_argument("--kubelet-read-only-port", type=int, default=10255, help="accepted; the authenticated port is used")
+    g.add_argument("--kubelet-timeout", default="5s")
+    g = ap.add_argument_group("audit")
+    g.add_argument("--audit-log-format", default="json", choices=["json", "legacy"])
+    g.add_argument("--audit-log-maxsize", type=int, default=0, help="MB before the audit log rotates")
+    g.add_argument("--audit-log-maxbackup", type=int, default=0)
+    g.add_argument("--audit-log-maxage", type=int, default=0, help="days a rotated audit log is kept")
+    g.add_argument("--audit-webhook-mode", default="batch", choices=["batch", "blocking"],
+                   help="accepted; events are always delivered by the batching backend")
+    for f in ("--audit-webhook-batch-buffer-size", "--audit-webhook-batch-throttle-burst"):
+        g.add_argument(f, type=int, default=0, help="accepted")
+    for f in ("--audit-webhook-batch-initial-backoff", "--audit-webhook-batch-throttle-qps"):
+        g.add_argument(f, default="", help="accepted")
+    g = ap.add_argument_group("storage")
+    g.add_argument("--storage-backend", default="etcd3", choices=["etcd3"])
+    g.add_argument("--etcd-prefix", default="/registry", help="only /registry is supported")
+    g.add_argument("--etcd-compaction-interval", default="5m", help="accepted; the store keeps a bounded history window")
+    g.add_argument("--watch-cache", type=_bool, default=True, help="accepted; the watch cache is always on")
+    g.add_argument("--watch-cache-sizes", default="", help="accepted; one window (--watch-cache-size) serves all resources")
+    g.add_argument("--default-watch-cache-size", type=int, default=None, help="alias of --watch-cache-size")
+    for f in ("--storage-versions", "--storage-version", "--etcd-servers-overrides", "--etcd-cafile", "--etcd-certfile",
+              "--etcd-keyfile"):
+        g.add_argument(f, default="")
+    g.add_argument("--etcd-quorum-read", type=_bool, default=True, help="accepted; the store is linearizable")
+    g.add_argument("--deserialization-cache-size", type=int, default=0, help="accepted")
+    g.add_argument("--delete-collection-workers", type=int, default=1, help="accepted")
+    g.add_argument("--target-ram-mb", type=int, default=0, help="accepted")
+    g = ap.add_argument_group("no-ops kept for command-line compatibility")
+    for f in ("--cloud-provider", "--cloud-config", "--external-hostname", "--public-address-override", "--ssh-user",
+              "--ssh-keyfile", "--experimental-keystone-url", "--experimental-keystone-ca-file", "--master-service-namespace",
+              "--tls-ca-file", "--tls-sni-cert-key", "--kubeconfig", "--authentication-kubeconfig",
+              "--authorization-kubeconfig", "--max-connection-bytes-per-sec", "--http2-max-streams-per-connection"):
+        g.add_argument(f, default="")
+    for f in ("--enable-garbage-collector", "--enable-aggregator-routing", "--repair-malformed-updates",
+              "--contention-profiling", "--authentication-skip-lookup"):
+        g.add_argument(f, type=_bool, default=False)
+
+
+def _reference_kwargs(a):
+    if a.cloud_provider:
+        raise SystemExit(f"kube-apiserver: --cloud-provider={a.cloud_provider}: cloud providers are out of scope here")
+    if a.etcd_prefix.rstrip("/") != "/registry":
+        raise SystemExit("kube-apiserver: only --etcd-prefix=/registry is supported")
+    if a.etcd_cafile or a.etcd_certfile or a.etcd_keyfile:
+        raise SystemExit("kube-apiserver: the kamd-etcd protocol has no TLS; reach the store over a unix socket "
+                         "or a loopback/cluster-private TCP port")
+    rh = None
+    if a.requestheader_client_ca_file:
+        rh = {"client_ca_file": a.requestheader_client_ca_file, "allowed_names": _csv(a.requestheader_allowed_names),
+              "username_headers": _csv(a.requestheader_username_headers) or ["X-Remote-User"],
+              "group_headers": _csv(a.requestheader_group_headers) or ["X-Remote-Group"],
+              "extra_headers_prefix": _csv(a.requestheader_extra_headers_prefix) or ["X-Remote-Extra-"]}
+    rt = _duration(a.request_timeout) if a.request_timeout not in ("0", "0s", "") else None
+    return dict(basic_auth_file=a.basic_auth_file, requestheader=rh,
+                authentication_token_webhook_config_file=a.authentication_token_webhook_config_file,
+                authentication_token_webhook_cache_ttl=_duration(a.authentication_token_webhook_cache_ttl),
+                authorization_webhook_config_file=a.authorization_webhook_config_file,
+                authorization_webhook_cache_authorized_ttl=_duration(a.authorization_webhook_cache_authorized_ttl),
+                authorization_webhook_cache_unauthorized_ttl=_duration(a.authorization_webhook_cache_unauthorized_ttl),
+                authorization_rbac_super_user=a.authorization_rbac_super_user,
+                cors_allowed_origins=_csv(a.cors_allowed_origins), request_timeout=rt,
+                min_request_timeout=float(a.min_request_timeout), enable_logs_handler=a.enable_logs_handler,
+                enable_swagger_ui=a.enable_swagger_ui, runtime_config=a.runtime_config or None,
+                allow_privileged=a.allow_privileged,
+                kubelet_preferred_address_types=_csv(a.kubelet_preferred_address_types),
+                kubelet_port=a.kubelet_port, kubelet_timeout=_duration(a.kubelet_timeout),
+                advertise_address=a.advertise_address, apiserver_count=a.apiserver_count,
+                endpoint_reconciler_type=a.endpoint_reconciler_type,
+                kubernetes_service_node_port=a.kubernetes_service_node_port,
+                proxy_client_cert=(a.proxy_client_cert_file, a.proxy_client_key_file or a.proxy_client_cert_file)
+                if a.proxy_client_cert_file else None)
+
+
 def main(argv=None):
     a = _parser().parse_args(argv)
     setup_logging(a.v)
@@ -223,7 +345,8 @@ def main(argv=None):
             wh = (WebhookBackend(a.audit_webhook_config_file, a.audit_webhook_batch_max_size, a.audit_webhook_batch_max_wait)
                   if a.audit_webhook_config_file else None)
             audit = AuditLogger(a.audit_log_path, Policy.load(a.audit_policy_file) if a.audit_policy_file else None,
-                                webhook=wh)
+                                webhook=wh, format=a.audit_log_format, max_size_mb=a.audit_log_maxsize,
+                                max_backups=a.audit_log_maxbackup, max_age_days=a.audit_log_maxage)
         oidc = None
         if a.oidc_issuer_url:
             oidc = {"issuer_url": a.oidc_issuer_url, "client_id": a.oidc_client_id,
@@ -233,7 +356,7 @@ def main(argv=None):
         s = APIServer(store=store, admission_plugins=plugins, admission_config=adm_cfg, token_file=a.token_auth_file,
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
-                      max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.watch_cache_size,
+                      max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.default_watch_cache_size or a.watch_cache_size,
                       event_ttl=_duration(a.event_ttl),
                       audit=audit, encryption_config=a.encryption_config,
                       service_cluster_ip_range=a.service_cluster_ip_range,
@@ -246,11 +369,29 @@ def main(argv=None):
                       enable_bootstrap_token_auth=a.enable_bootstrap_token_auth,
                       authentication_token_webhook=a.authentication_token_webhook_url, anonymous_auth=a.anonymous_auth,
                       authorization_policy_file=a.authorization_policy_file,
-                      authorization_webhook_url=a.authorization_webhook_url, oidc=oidc)
+                      authorization_webhook_url=a.authorization_webhook_url, oidc=oidc, **_reference_kwargs(a))
+        s.enable_profiling = a.profiling
+        if a.secure_port:
+            # the reference's two listeners: TLS + authn/authz on --bind-address:--secure-port
+            # (self-signed in --cert-dir without --tls-cert-file), plain HTTP without either on
+            # --insecure-bind-address:--port/--insecure-port (0 = off)
+            if not a.tls_cert_file:
+                from ..utils.tlsutil import self_signed_serving_cert
+                cert, key = self_signed_serving_cert(a.cert_dir, "kube-apiserver",
+                                                     [a.advertise_address, "kubernetes", "kubernetes.default",
+                                                      "kubernetes.default.svc"], basename="apiserver")
+                s.tls = (cert, key, a.client_ca_file)
+            sport = await s.start(a.bind_address, a.secure_port, reuse_port=a.reuse_port)
+            iport = await s.start_insecure(a.insecure_bind_address, a.port, reuse_port=a.reuse_port) if a.port else None
+            write_port_file(a.port_file, iport or sport)
+            if not a.reuse_port:
+                print(f"kube-apiserver listening on https://{a.bind_address}:{sport}"
+                      + (f" and http://{a.insecure_bind_address}:{iport} (insecure)" if iport else ""), flush=True)
+            return s
         port = await s.start(a.bind_address, a.port, reuse_port=a.reuse_port)
         write_port_file(a.port_file, port)
         if not a.reuse_port:
-            print(f"kube-apiserver listening on http://{a.bind_address}:{port}", flush=True)
+            print(f"kube-apiserver listening on http{'s' if a.tls_cert_file else ''}://{a.bind_address}:{port}", flush=True)
         return s
 
     run_until_signal(start)

@@ -966,22 +966,8 @@ class Kubelet:
 
     def _node_logs(self, rel):
         """/logs/: read-only view of the node's log directory (`server.go` getLogs)."""
-        base = os.path.realpath(self.node_log_dir)
-        target = os.path.realpath(os.path.join(base, rel))
-        if target != base and not target.startswith(base + os.sep):
-            return Response(403, b"path escapes the log directory", "text/plain")
-        if os.path.isdir(target):
-            try:
-                names = sorted(os.listdir(target))
-            except OSError as e:
-                return Response(403, str(e).encode(), "text/plain")
-            return Response(200, "".join(n + ("/" if os.path.isdir(os.path.join(target, n)) else "") + "\n"
-                                         for n in names).encode(), "text/plain")
-        try:
-            with open(target, "rb") as f:
-                return Response(200, f.read(), "text/plain")
-        except OSError:
-            return Response(404, b"not found", "text/plain")
+        from ..utils.httpserver import log_dir_response
+        return log_dir_response(self.node_log_dir, rel)
 
     def _service_env(self, pod):
         if self.svc_informer is None or not self.svc_informer.synced.is_set():

@@ -8,6 +8,7 @@ allocations beyond the header dict, responses written with a single `transport.w
 from __future__ import annotations
 
 import asyncio
+import time
 import logging
 from urllib.parse import parse_qs, unquote
 
@@ -23,7 +24,8 @@ REASONS = {
 
 
 class Request:
-    __slots__ = ("method", "path", "raw_path", "query", "qs", "headers", "body", "transport", "user", "info", "served_gv")
+    __slots__ = ("method", "path", "raw_path", "query", "qs", "headers", "body", "transport", "user", "info", "served_gv",
+                 "insecure")
 
     def __init__(self, method, target, headers, body, transport):
         self.method = method
@@ -41,6 +43,7 @@ class Request:
         self.user = None
         self.info = None
         self.served_gv = None
+        self.insecure = False      # arrived on the API server's insecure listener
 
 
 class Response:
@@ -134,6 +137,7 @@ class _Conn(asyncio.Protocol):
         self._paused = False
         self._drain_waiter = None
         self.close_fut = None
+        self.deadline = 0.0         # loop time the in-flight request must answer by (0 = none)
 
     def connection_made(self, transport):
         self.transport = transport
@@ -206,13 +210,17 @@ class _Conn(asyncio.Protocol):
         try:
             while self.pending:
                 req = self.pending.pop(0)
+                srv = self.server
+                if srv.request_timeout and not (srv.long_running is not None and srv.long_running(req)):
+                    self.deadline = srv.loop_time() + srv.request_timeout
                 try:
                     resp = await self.server.handler(req)
                 except Exception as e:  # pragma: no cover - defensive
                     log.exception("handler error")
                     resp = Response(500, b'{"kind":"Status","status":"Failure","message":%s,"code":500}' % repr(str(e)).encode())
+                self.deadline = 0.0
                 if self.transport.is_closing():
-                    return
+                    return              # includes a request the timeout sweeper already answered
                 if isinstance(resp, UpgradeResponse):
                     await self._upgrade(resp)
                     return
@@ -295,12 +303,37 @@ class _Conn(asyncio.Protocol):
 
 
 class HTTPServer:
-    def __init__(self, handler):
+    """`request_timeout` (seconds): a request not answered in time gets `timeout_response` and its
+    connection is closed, while the handler runs on and its late response is dropped (Go's
+    http.TimeoutHandler, the API server's --request-timeout); `long_running(req)` exempts
+    watches, streams and proxies. One sweeper per server checks the deadlines, so a request pays
+    only a clock read."""
+
+    def __init__(self, handler, request_timeout=None, long_running=None, timeout_response=None):
         self.handler = handler
         self._server = None
         self._conns = set()
         self._tasks = set()
         self.port = None
+        self.request_timeout = request_timeout
+        self.long_running = long_running
+        self.timeout_response = timeout_response or Response(504, b"request timed out", "text/plain")
+        self._sweeper = None
+        self.loop_time = time.monotonic
+
+    async def _sweep(self):
+        period = max(0.05, min(1.0, self.request_timeout / 4))
+        while True:
+            await asyncio.sleep(period)
+            now = self.loop_time()
+            for c in list(self._conns):
+                if c.deadline and now > c.deadline and c.transport is not None and not c.transport.is_closing():
+                    r = self.timeout_response
+                    c.transport.write(("HTTP/1.1 %d %s\r\nContent-Type: %s\r\nContent-Length: %d\r\nConnection: close\r\n\r\n"
+                                       % (r.status, REASONS.get(r.status, "OK"), r.content_type, len(r.body))).encode()
+                                      + r.body)
+                    c.deadline = 0.0
+                    c.transport.close()
 
     async def start(self, host="127.0.0.1", port=0, ssl=None, reuse_port=False):
         """reuse_port: several worker processes listen on one port; the kernel spreads
@@ -309,6 +342,8 @@ class HTTPServer:
         self._server = await loop.create_server(lambda: _Conn(self), host, port, ssl=ssl, backlog=4096,
                                                 reuse_address=True, reuse_port=reuse_port or None)
         self.port = self._server.sockets[0].getsockname()[1]
+        if self.request_timeout and self._sweeper is None:
+            self._sweeper = asyncio.ensure_future(self._sweep())
         return self.port
 
     async def start_unix(self, path):
@@ -317,9 +352,35 @@ class HTTPServer:
         return path
 
     async def stop(self):
+        if self._sweeper is not None:
+            self._sweeper.cancel()
+            self._sweeper = None
         if self._server:
             self._server.close()
             for c in list(self._conns):
                 if c.transport:
                     c.transport.close()
             await self._server.wait_closed()
+
+
+def log_dir_response(base_dir: str, rel: str) -> "Response":
+    """Read-only view of a log directory (`/logs/` of the kubelet and the API server,
+    `server.go` getLogs / `routes.Logs`): directory listings and file contents, never a path
+    outside `base_dir`."""
+    import os
+    base = os.path.realpath(base_dir)
+    target = os.path.realpath(os.path.join(base, rel))
+    if target != base and not target.startswith(base + os.sep):
+        return Response(403, b"path escapes the log directory", "text/plain")
+    if os.path.isdir(target):
+        try:
+            names = sorted(os.listdir(target))
+        except OSError as e:
+            return Response(403, str(e).encode(), "text/plain")
+        return Response(200, "".join(n + ("/" if os.path.isdir(os.path.join(target, n)) else "") + "\n"
+                                     for n in names).encode(), "text/plain")
+    try:
+        with open(target, "rb") as f:
+            return Response(200, f.read(), "text/plain")
+    except OSError:
+        return Response(404, b"not found", "text/plain")

@@ -48,10 +48,11 @@ def unverified_client_context() -> ssl.SSLContext:
     return client_context()
 
 
-def self_signed_serving_cert(cert_dir: str, host: str, addresses=()) -> tuple[str, str]:
-    """-> (cert path, key path), generating them on first use."""
+def self_signed_serving_cert(cert_dir: str, host: str, addresses=(), basename="kubelet") -> tuple[str, str]:
+    """-> (cert path, key path), generating them on first use (`<basename>.crt/.key`; the API
+    server's `--cert-dir` pair is `apiserver.crt/.key`)."""
     from ..native import crypto
-    cert_path, key_path = os.path.join(cert_dir, "kubelet.crt"), os.path.join(cert_dir, "kubelet.key")
+    cert_path, key_path = os.path.join(cert_dir, basename + ".crt"), os.path.join(cert_dir, basename + ".key")
     if os.path.exists(cert_path) and os.path.exists(key_path):
         return cert_path, key_path
     os.makedirs(cert_dir, exist_ok=True)
