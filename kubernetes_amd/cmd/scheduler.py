@@ -42,6 +42,21 @@ def _parser():
     ap.add_argument("--algorithm-provider", default=None, help="DefaultProvider | ClusterAutoscalerProvider")
     ap.add_argument("--policy-configmap", default=None, help="ConfigMap holding the Policy under policy.cfg")
     ap.add_argument("--policy-configmap-namespace", default="kube-system")
+    ap.add_argument("--port", type=int, default=10251, help="/healthz and /metrics (0 = off; shard i uses port+i)")
+    ap.add_argument("--address", default="0.0.0.0")
+    ap.add_argument("--kube-api-burst", type=int, default=None)
+    ap.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
+                    help="accepted; the client speaks JSON")
+    ap.add_argument("--lock-object-name", default="kube-scheduler")
+    ap.add_argument("--lock-object-namespace", default="kube-system")
+    ap.add_argument("--hard-pod-affinity-symmetric-weight", type=int, default=1,
+                    help="score an existing pod's required pod affinity gives a matching incoming pod (0-100)")
+    ap.add_argument("--failure-domains", default="kubernetes.io/hostname,failure-domain.beta.kubernetes.io/zone,"
+                    "failure-domain.beta.kubernetes.io/region", help="accepted (deprecated in 1.9)")
+    ap.add_argument("--use-legacy-policy-config", action="store_true",
+                    help="read --policy-config-file even when --config is given")
+    ap.add_argument("--profiling", default="true")
+    ap.add_argument("--contention-profiling", default="false", help="accepted")
     ap.add_argument("-v", type=int, default=0)
     return ap
 
@@ -83,6 +98,11 @@ def main(argv=None):
     if a.shards > 1:
         sys.exit(supervise(argv, a.shards))
     from ..scheduler import policy as SP
+    if not 0 <= a.hard_pod_affinity_symmetric_weight <= 100:
+        raise SystemExit("kube-scheduler: --hard-pod-affinity-symmetric-weight must be in 0..100")
+    if a.metrics_port is None and a.port:
+        a.metrics_port = a.port + a.shard_index
+    legacy_policy = a.policy_config_file
     if a.config:
         with open(a.config) as f:
             cc = SP.load_component_config(f.read())
@@ -103,26 +123,32 @@ def main(argv=None):
         mb = cc.get("metricsBindAddress")
         if mb and ":" in mb:
             a.metrics_port = int(mb.rsplit(":", 1)[1])
+        a.hard_pod_affinity_symmetric_weight = cc.get("hardPodAffinitySymmetricWeight", a.hard_pod_affinity_symmetric_weight)
+        if a.use_legacy_policy_config and legacy_policy:
+            a.policy_config_file = legacy_policy
 
     async def start():
         from ..scheduler.extender import HTTPExtender
         if a.kubeconfig:
             from ..client.clientcmd import client_from
-            client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
+            client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=a.kube_api_burst or int(a.kube_api_qps or 10),
+                                 max_conns=64)
         else:
-            client = Client(a.master or "http://127.0.0.1:8080", qps=a.kube_api_qps, burst=int(a.kube_api_qps or 10), max_conns=64)
+            client = Client(a.master or "http://127.0.0.1:8080", qps=a.kube_api_qps,
+                            burst=a.kube_api_burst or int(a.kube_api_qps or 10), max_conns=64)
         preds, prios, ext_cfgs = await SP.resolve_algorithm(client, a.algorithm_provider, a.policy_config_file,
                                                             a.policy_configmap, a.policy_configmap_namespace)
         extenders = [HTTPExtender.from_config(e) for e in ext_cfgs]
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
                       emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,
-                      shard_count=a.shard_count, preemption=not a.disable_preemption)
+                      shard_count=a.shard_count, preemption=not a.disable_preemption,
+                      hard_pod_affinity_symmetric_weight=a.hard_pod_affinity_symmetric_weight)
         if a.leader_elect:
             from ..client.leaderelection import LeaderElector
-            lock = "kube-scheduler" if a.shard_count == 1 else f"kube-scheduler-shard-{a.shard_index}"
-            le = LeaderElector(client, "kube-system", lock)
+            lock = a.lock_object_name if a.shard_count == 1 else f"{a.lock_object_name}-shard-{a.shard_index}"
+            le = LeaderElector(client, a.lock_object_namespace, lock)
             await le.acquire()
-        spawn(s.run(metrics_port=a.metrics_port))
+        spawn(s.run(metrics_port=a.metrics_port, metrics_address=a.address))
         return s
 
     run_until_signal(start)

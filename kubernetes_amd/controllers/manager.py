@@ -81,14 +81,20 @@ def resolve(enabled):
 
 
 class ControllerManager:
-    def __init__(self, client, controllers=None, options=None):
+    """`workers`: {controller name: worker count} (--concurrent-*-syncs); `start_interval`:
+    seconds between controller starts (--controller-start-interval)."""
+
+    def __init__(self, client, controllers=None, options=None, workers=None, start_interval=0.0):
         self.client = client
         self.factory = InformerFactory(client)
         self.controllers = []
+        self.start_interval = start_interval
         options = options or {}
         for name in resolve(controllers):
             cls = CONTROLLERS[name]
             c = cls(client, self.factory, **options.get(name, {}))
+            if workers and workers.get(name):
+                c.workers = int(workers[name])
             c.setup()
             self.controllers.append(c)
 
@@ -97,7 +103,22 @@ class ControllerManager:
         await self.factory.wait_for_cache_sync(60)
         for c in self.controllers:
             c.start()
+            if self.start_interval:
+                await asyncio.sleep(self.start_interval)
         return self
+
+    def render_metrics(self) -> bytes:
+        """Work-queue metrics per controller (`workqueue/metrics.go`: depth, adds)."""
+        out = ["# TYPE workqueue_depth gauge"]
+        out += [f'workqueue_depth{{name="{c.name}"}} {len(c.queue._queue)}' for c in self.controllers]
+        out.append("# TYPE workqueue_adds counter")
+        out += [f'workqueue_adds{{name="{c.name}"}} {c.queue.adds}' for c in self.controllers]
+        out.append("# TYPE controller_syncs_total counter")
+        out += [f'controller_syncs_total{{name="{c.name}"}} {c.syncs}' for c in self.controllers]
+        return ("\n".join(out) + "\n").encode()
+
+    def render(self):
+        return self.render_metrics()
 
     def get(self, name):
         for c in self.controllers:

@@ -71,15 +71,16 @@ class ServiceHealthServer:
 class ProxyServer:
     def __init__(self, client, hostname, mode="iptables", cluster_cidr="", masquerade_all=False, sync_period=30.0,
                  min_sync_period=0.0, node_ips=("127.0.0.1",), healthz_port=None, metrics_port=None,
-                 iptables=None, ipvs=None, ipvs_scheduler="rr", bind="127.0.0.1", open_node_ports=True):
+                 iptables=None, ipvs=None, ipvs_scheduler="rr", bind="127.0.0.1", open_node_ports=True,
+                 masquerade_bit=14):
         self.client = client
         self.hostname = hostname
         self.mode = mode
         self.state = ProxyState(hostname)
         if mode == "iptables":
             from .iptables import IptablesProxier
-            self.proxier = IptablesProxier(self.state, iptables, cluster_cidr, masquerade_all, node_ips=node_ips,
-                                           min_sync_period=min_sync_period)
+            self.proxier = IptablesProxier(self.state, iptables, cluster_cidr, masquerade_all, masquerade_bit=masquerade_bit,
+                                           node_ips=node_ips, min_sync_period=min_sync_period)
         elif mode == "ipvs":
             from .ipvs import IPVSProxier
             self.proxier = IPVSProxier(self.state, ipvs, ipvs_scheduler, node_ips, min_sync_period)

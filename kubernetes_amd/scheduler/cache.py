@@ -284,14 +284,23 @@ class SchedulerCache:
         self.assumed: dict[str, float] = {}      # key -> deadline (0 until binding finished)
         self.ttl = assumed_ttl
         self.anti_pods: dict[str, dict] = {}     # pods with required anti-affinity (symmetry check)
+        # pods whose own affinity terms score incoming pods (interpod_affinity.go "existing pod"
+        # branch): any podAffinity, or preferred podAntiAffinity
+        self.affinity_pods: dict[str, dict] = {}
+        self.hard_pod_affinity_weight = 1        # --hard-pod-affinity-symmetric-weight
         self.volumes = VolumeLister()
 
     def _track(self, key, pod):
-        aff = ((pod.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
-        if aff.get("requiredDuringSchedulingIgnoredDuringExecution"):
+        aff = (pod.get("spec") or {}).get("affinity") or {}
+        anti = aff.get("podAntiAffinity") or {}
+        if anti.get("requiredDuringSchedulingIgnoredDuringExecution"):
             self.anti_pods[key] = pod
         else:
             self.anti_pods.pop(key, None)
+        if aff.get("podAffinity") or anti.get("preferredDuringSchedulingIgnoredDuringExecution"):
+            self.affinity_pods[key] = pod
+        else:
+            self.affinity_pods.pop(key, None)
 
     def _node(self, name):
         ni = self.nodes.get(name)
@@ -324,6 +333,7 @@ class SchedulerCache:
         del self.pod_states[key]
         del self.assumed[key]
         self.anti_pods.pop(key, None)
+        self.affinity_pods.pop(key, None)
 
     def add_pod(self, pod):
         """Confirmed (bound) pod from the informer. An assumed pod is replaced by the API
@@ -362,6 +372,7 @@ class SchedulerCache:
         st = self.pod_states.pop(key, None)
         self.assumed.pop(key, None)
         self.anti_pods.pop(key, None)
+        self.affinity_pods.pop(key, None)
         if st is not None:
             ni = self.nodes.get(st[1])
             if ni is not None:
@@ -384,6 +395,8 @@ class SchedulerCache:
                 self._node(node).remove_pod(key)
                 del self.pod_states[key]
                 del self.assumed[key]
+                self.anti_pods.pop(key, None)
+                self.affinity_pods.pop(key, None)
 
     # -- nodes --------------------------------------------------------------
     def add_node(self, node):

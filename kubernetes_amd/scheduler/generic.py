@@ -85,8 +85,41 @@ class CycleContext:
                         if P._pod_matches_term(p["metadata"].get("labels") or {}, p["metadata"].get("namespace"), term, ns):
                             counts[v] = counts.get(v, 0) + 1
                 out.append((w, key, counts))
+            out += self._existing_pod_terms(ns)
             self._aff_counts = out
         return self._aff_counts
+
+    def _existing_pod_terms(self, ns):
+        """Existing pods' terms that match the incoming pod (`interpod_affinity.go` symmetry):
+        their required pod affinity scores `hard_pod_affinity_weight`, their preferred affinity
+        +weight and preferred anti-affinity −weight, in their own topology domain."""
+        cache = self.cache
+        if not cache.affinity_pods:
+            return []
+        labels = self.pod["metadata"].get("labels") or {}
+        hw = cache.hard_pod_affinity_weight
+        out = []
+        for key, p in cache.affinity_pods.items():
+            st = cache.pod_states.get(key)
+            ni = cache.nodes.get(st[1]) if st else None
+            if ni is None:
+                continue
+            aff = (p.get("spec") or {}).get("affinity") or {}
+            pns = p["metadata"].get("namespace", "default")
+            terms = []
+            pa = aff.get("podAffinity") or {}
+            if hw:
+                terms += [(float(hw), t) for t in pa.get("requiredDuringSchedulingIgnoredDuringExecution") or ()]
+            terms += [(float(t.get("weight", 0)), t.get("podAffinityTerm") or {})
+                      for t in pa.get("preferredDuringSchedulingIgnoredDuringExecution") or ()]
+            terms += [(-float(t.get("weight", 0)), t.get("podAffinityTerm") or {})
+                      for t in (aff.get("podAntiAffinity") or {}).get("preferredDuringSchedulingIgnoredDuringExecution") or ()]
+            for w, term in terms:
+                tkey = term.get("topologyKey", "")
+                v = ni.labels.get(tkey)
+                if v is not None and w and P._pod_matches_term(labels, ns, term, pns):
+                    out.append((w, tkey, {v: 1}))
+        return out
 
     def pods_by_topology(self, key, val):
         for ni in self.cache.nodes.values():
@@ -182,7 +215,7 @@ class GenericScheduler:
                 continue
             if name == "NodeAffinityPriority" and not ctx.node_affinity_prefs:
                 continue
-            if name == "InterPodAffinityPriority" and not ctx.affinity_prefs:
+            if name == "InterPodAffinityPriority" and not ctx.affinity_prefs and not self.cache.affinity_pods:
                 continue
             out.append((name, w, fn, reverse, norm))
         return out

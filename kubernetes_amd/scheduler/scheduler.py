@@ -59,10 +59,11 @@ class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
                  update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True,
-                 rehandoff_period=0.2):
+                 rehandoff_period=0.2, hard_pod_affinity_symmetric_weight=1):
         self.client = client
         self.name = scheduler_name
         self.cache = SchedulerCache()
+        self.cache.hard_pod_affinity_weight = hard_pod_affinity_symmetric_weight
         self.queue = SchedulingQueue()
         self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
         self.shard_index, self.shard_count = shard_index, shard_count
@@ -290,7 +291,7 @@ class Scheduler:
         self.sc_informer.add_handler(put(vl.classes), put(vl.classes), drop(vl.classes))
 
     # -- scheduling loop ---------------------------------------------------------
-    async def run(self, metrics_port=None):
+    async def run(self, metrics_port=None, metrics_address="127.0.0.1"):
         self.recorder.start()
         if self.partitioned:
             self.node_informer.add_handler(self._on_part_node_add, self._on_part_node_update, self._on_part_node_delete)
@@ -315,7 +316,11 @@ class Scheduler:
         await self.pod_informer.wait_synced(60)
         if metrics_port is not None:
             self.http = HTTPServer(self._http)
-            await self.http.start("127.0.0.1", metrics_port)
+            try:
+                await self.http.start(metrics_address, metrics_port)
+            except OSError as e:     # another scheduler on this host holds the port: not fatal
+                log.warning("healthz/metrics endpoint %s:%s not started: %s", metrics_address, metrics_port, e)
+                self.http = None
         self._tasks.append(asyncio.ensure_future(self._housekeeping()))
         while True:
             ent = await self.queue.pop()

@@ -211,3 +211,27 @@ def test_policy_names_resolve():
     for n in ("ImageLocalityPriority", "ResourceLimitsPriority", "InterPodAffinityPriority"):
         assert n in PR.PRIORITIES
     json.dumps(P.DEFAULT_PREDICATES)
+
+
+def test_inter_pod_affinity_symmetry():
+    """`interpod_affinity.go` existing-pod branch: an existing pod's REQUIRED affinity to the
+    incoming pod scores `--hard-pod-affinity-symmetric-weight` in its domain, its preferred
+    anti-affinity scores -weight; the incoming pod has no affinity terms of its own."""
+    z = "topology.kubernetes.io/zone"
+    term = {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": z}
+    db = pod("db", node_name="a", labels={"app": "db"},
+             affinity={"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [term]}})
+    cache, gs = sched(node("a", {z: "z1"}), node("b", {z: "z2"}), pods=[db])
+    assert cache.affinity_pods
+    assert all(gs.schedule(pod(f"w{i}", labels={"app": "web"}))[0] == "a" for i in range(3))
+    cache.hard_pod_affinity_weight = 0                     # the symmetric term is off: no pull to z1
+    from kubernetes_amd.scheduler.generic import CycleContext
+    assert CycleContext(cache, pod("x", labels={"app": "web"})).pod_affinity_counts() == []
+    # preferred anti-affinity of an existing pod pushes matching pods out of its zone
+    lonely = pod("lonely", node_name="a", labels={"app": "lonely"}, affinity={"podAntiAffinity": {
+        "preferredDuringSchedulingIgnoredDuringExecution": [{"weight": 50, "podAffinityTerm": term}]}})
+    _, gs = sched(node("a", {z: "z1"}), node("b", {z: "z2"}), pods=[lonely])
+    assert all(gs.schedule(pod(f"v{i}", labels={"app": "web"}))[0] == "b" for i in range(3))
+    # pods that do not match the existing pod's terms are unaffected by them
+    ctx = CycleContext(gs.cache, pod("other", labels={"app": "other"}))
+    assert ctx.pod_affinity_counts() == []
