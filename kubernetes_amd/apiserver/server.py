@@ -2006,13 +2006,45 @@ class APIServer:
         return _json(200, {"kind": "ComponentStatusList", "apiVersion": "v1", "metadata": {}, "items": list(items)})
 
     async def _pod_log(self, ns, name, q):
+        """pods/log relayed to the kubelet (`pkg/registry/core/pod/rest/log.go`); with follow the
+        kubelet's stream is relayed as it arrives."""
+        from urllib.parse import urlencode
         _, addr, port = await self._kubelet_of(ns, name)
         from ..client.http import HTTPClient
         c = HTTPClient(f"{self.kubelet_scheme}://{addr}:{port}", ssl_context=self.kubelet_ssl,
                        timeout=max(self.kubelet_timeout, 30.0))
+        qs = urlencode(q)
+        path = f"/containerLogs/{ns}/{name}/{q.get('container', '')}" + (f"?{qs}" if qs else "")
+        if q.get("follow") in ("true", "1"):
+            st, hdrs, r, w = await c.open_raw("GET", path)
+            if st != 200:
+                body = await r.read(1 << 16)
+                w.close()
+                await c.close()
+                return Response(st, body, "text/plain")
+
+            async def relay(cw):
+                try:
+                    if hdrs.get("transfer-encoding", "").lower() == "chunked":
+                        while True:
+                            n = int((await r.readuntil(b"\r\n")).split(b";")[0].strip() or b"0", 16)
+                            if n == 0:
+                                return
+                            cw.write(await r.readexactly(n))
+                            await r.readexactly(2)
+                    while True:
+                        chunk = await r.read(1 << 16)
+                        if not chunk:
+                            return
+                        cw.write(chunk)
+                except (asyncio.IncompleteReadError, ConnectionError):
+                    return
+                finally:
+                    w.close()
+                    await c.close()
+            return StreamResponse(relay, "text/plain")
         try:
-            qs = "&".join(f"{k}={v}" for k, v in q.items())
-            st, body = await c.request("GET", f"/containerLogs/{ns}/{name}/{q.get('container', '')}" + (f"?{qs}" if qs else ""))
+            st, body = await c.request("GET", path)
         finally:
             await c.close()
         return Response(st, body, "text/plain")

@@ -287,6 +287,10 @@ class RemoteRuntime(Runtime):
                 (name, c.id, c.metadata.attempt, c.created_at / 1e9 if c.created_at else 0.0, c.pod_sandbox_id))
         return out
 
+    def log_path(self, cid):
+        st = self.cache.get(cid)
+        return (st.log_path or None) if st is not None else None
+
     async def container_logs(self, cid, tail=None):
         st = self.cache.get(cid)
         if st is None or not st.log_path:

@@ -154,7 +154,15 @@ def jsonpath(obj, expr):
     return "".join(out)
 
 
-def render(objs, output, kind=None, wide=False, all_ns=False, list_obj=None):
+def render(objs, output, kind=None, wide=False, all_ns=False, list_obj=None, sort_by="", no_headers=False,
+           show_labels=False, label_columns=(), show_kind=False):
+    """Objects in `-o` form. Table options (`pkg/printers/humanreadable.go` PrintOptions):
+    --sort-by (JSONPath; numbers and quantities compare as numbers), --no-headers,
+    --show-labels, -L label columns, --show-kind (kind/name)."""
+    if sort_by:
+        objs = sort_objects(objs, sort_by)
+        if list_obj is not None:
+            list_obj = dict(list_obj, items=objs)
     if output == "json":
         return json.dumps(list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else {"kind": "List", "apiVersion": "v1", "items": objs}), indent=4)
     if output == "yaml":
@@ -171,7 +179,42 @@ def render(objs, output, kind=None, wide=False, all_ns=False, list_obj=None):
     if not objs:
         return "No resources found."
     rows, h = rows_for(kind or objs[0].get("kind"), objs, wide or output == "wide", all_ns)
-    return table(rows, h)
+    name_col = h.index("NAME") if "NAME" in h else None
+    if show_kind and name_col is not None:
+        k = (kind or objs[0].get("kind") or "").lower()
+        rows = [r[:name_col] + [f"{k}/{r[name_col]}"] + r[name_col + 1:] for r in rows]
+    cols = []
+    for spec in label_columns or ():
+        cols += [c for c in spec.split(",") if c]
+    if cols:
+        h = h + [c.rsplit("/", 1)[-1].upper() for c in cols]
+        rows = [list(r) + [((o.get("metadata") or {}).get("labels") or {}).get(c, "") for c in cols]
+                for r, o in zip(rows, objs)]
+    if show_labels:
+        h = h + ["LABELS"]
+        rows = [list(r) + [",".join(f"{k}={v}" for k, v in sorted(((o.get("metadata") or {}).get("labels") or {}).items()))
+                           or "<none>"] for r, o in zip(rows, objs)]
+    text = table(rows, h)
+    if no_headers:
+        text = "\n".join(text.splitlines()[1:])
+    return text
+
+
+def sort_objects(objs, expr):
+    from ..api.quantity import parse_quantity
+    path = expr if expr.startswith("{") else "{" + expr + "}"
+
+    def key(o):
+        v = jsonpath(o, path)
+        try:
+            return (0, float(v), "")
+        except (TypeError, ValueError):
+            pass
+        try:
+            return (0, float(parse_quantity(str(v)).milli_value()) / 1000.0, "")
+        except (ValueError, AttributeError):
+            return (1, 0.0, str(v))
+    return sorted(objs, key=key)
 
 
 def describe(obj, events=()):

@@ -34,7 +34,7 @@ from ..api.quantity import parse_quantity
 from ..client.events import EventRecorder
 from ..client.informer import Informer
 from ..client.rest import APIStatusError, is_conflict, is_not_found
-from ..utils.httpserver import HTTPServer, Response
+from ..utils.httpserver import HTTPServer, Response, StreamResponse
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from .devicemanager.manager import AdmitError, ManagerStub
 from .prober import ProbeManager
@@ -89,6 +89,11 @@ def _field_path(pod, c):
     if any(ic.get("name") == c["name"] for ic in spec.get("initContainers") or ()):
         return f"spec.initContainers{{{c['name']}}}"
     return f"spec.containers{{{c['name']}}}"
+
+
+def now_rfc3339_nano(t=None):
+    t = time.time() if t is None else t
+    return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t)) + f".{int((t % 1) * 1e9):09d}Z"
 
 
 class Kubelet:
@@ -969,6 +974,68 @@ class Kubelet:
         from ..utils.httpserver import log_dir_response
         return log_dir_response(self.node_log_dir, rel)
 
+    async def _container_logs(self, cid, tail, q):
+        """`/containerLogs` (`server.go` getContainerLogs + kuberuntime ReadLogs): tailLines,
+        limitBytes, follow (the file is followed while the container runs), timestamps (lines
+        read while following carry their arrival time: the runtimes write raw output files with
+        no per-line times), sinceSeconds / sinceTime (a file not written since then yields
+        nothing, otherwise all of it: the same file-level granularity)."""
+        from ..api.meta import parse_rfc3339
+        data = await self.runtime.container_logs(cid, tail)
+        limit = int(q.get("limitBytes") or 0)
+        path = getattr(self.runtime, "log_path", lambda c: None)(cid)
+        since = None
+        if q.get("sinceSeconds"):
+            since = time.time() - float(q["sinceSeconds"])
+        elif q.get("sinceTime"):
+            since = parse_rfc3339(q["sinceTime"])
+        if since is not None and path and os.path.exists(path) and os.path.getmtime(path) < since:
+            data = b""
+        stamp = q.get("timestamps") in ("true", "1")
+        if stamp and data:
+            # lines already written carry the file's last write time (file-level granularity)
+            mt = os.path.getmtime(path) if path and os.path.exists(path) else time.time()
+            ts = now_rfc3339_nano(mt).encode() + b" "
+            data = b"".join(ts + ln for ln in data.splitlines(keepends=True))
+        if limit:
+            data = data[:limit]
+        if q.get("follow") not in ("true", "1") or not path:
+            return Response(200, data, "text/plain")
+        runtime = self.runtime
+
+        async def follow(w):
+            sent = len(data)
+            if data:
+                w.write(data)
+            pos = os.path.getsize(path) if os.path.exists(path) else 0
+            while True:
+                try:
+                    st = runtime.container_status(cid)
+                except (KeyError, OSError):
+                    st = None
+                running = st is not None and st.state == RUNNING
+                if os.path.exists(path):
+                    with open(path, "rb") as f:
+                        f.seek(pos)
+                        chunk = f.read(1 << 20)
+                    if chunk:
+                        pos += len(chunk)
+                        if stamp:
+                            now = now_rfc3339_nano()
+                            chunk = b"".join(now.encode() + b" " + ln for ln in chunk.splitlines(keepends=True))
+                        if limit:
+                            chunk = chunk[:max(0, limit - sent)]
+                        if chunk:
+                            w.write(chunk)
+                            sent += len(chunk)
+                        if limit and sent >= limit:
+                            return
+                        continue
+                if not running:
+                    return
+                await asyncio.sleep(0.1)
+        return StreamResponse(follow, "text/plain")
+
     def _service_env(self, pod):
         if self.svc_informer is None or not self.svc_informer.synced.is_set():
             return []
@@ -1528,7 +1595,7 @@ class Kubelet:
                 if cid is None:
                     return Response(404, b"container not found", "text/plain")
                 tail = int(req.query["tailLines"]) if "tailLines" in req.query else None
-                return Response(200, await self.runtime.container_logs(cid, tail), "text/plain")
+                return await self._container_logs(cid, tail, req.query)
         if p == "/stats/summary":
             from .stats import summary
             return Response(200, codec.dumpb(summary(self)))

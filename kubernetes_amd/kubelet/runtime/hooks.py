@@ -158,6 +158,10 @@ class HookedRuntime(Runtime):
     async def container_logs(self, cid, tail=None):
         return await self._rt(cid).container_logs(cid, tail)
 
+    def log_path(self, cid):
+        rt = self._rt(cid)
+        return rt.log_path(cid) if hasattr(rt, "log_path") else None
+
     async def exec_sync(self, cid, cmd, timeout):
         return await self._rt(cid).exec_sync(cid, cmd, timeout)
 

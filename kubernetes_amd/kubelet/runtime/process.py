@@ -822,6 +822,10 @@ class ProcessRuntime(Runtime):
     def list_containers(self):
         return list(self.containers.values())
 
+    def log_path(self, cid):
+        st = self.containers.get(cid)
+        return st.log_path if st is not None else None
+
     async def container_logs(self, cid, tail=None):
         st = self.containers.get(cid)
         if st is None or not os.path.exists(st.log_path):

@@ -170,3 +170,20 @@ def apply_patch(content_type: str, target, patch):
     if ct in ("application/strategic-merge-patch+json", "application/apply-patch+yaml"):
         return strategic_merge_patch(target, patch)
     raise ValueError(f"unsupported patch type {ct!r}")
+
+
+def create_merge_patch(original, modified):
+    """The RFC 7386 merge patch turning `original` into `modified` (what `kubectl edit
+    --output-patch` prints; `jsonmergepatch.CreateThreeWayJSONMergePatch` with no base)."""
+    if not isinstance(original, dict) or not isinstance(modified, dict):
+        return modified
+    out = {}
+    for k in original:
+        if k not in modified:
+            out[k] = None
+    for k, v in modified.items():
+        if k not in original:
+            out[k] = v
+        elif original[k] != v:
+            out[k] = create_merge_patch(original[k], v) if isinstance(v, dict) and isinstance(original[k], dict) else v
+    return out

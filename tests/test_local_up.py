@@ -59,7 +59,7 @@ def test_node_registers_gpus_across_processes(local_up):
 def test_gpu_pod_through_separate_processes(local_up):
     url, _ = local_up
     wait(lambda: "8/8" in k(url, "get", "nodes")[1])
-    rc, out = k(url, "run", "gpujob", "--image", "kubernetes-amd/hip-vector-add", "--gpus", "2")
+    rc, out = k(url, "run", "gpujob", "--image", "kubernetes-amd/hip-vector-add", "--gpus", "2", "--restart", "Never")
     assert rc == 0
     wait(lambda: "Running" in k(url, "get", "pod", "gpujob")[1])
     rc, out = k(url, "describe", "pod", "gpujob")
