@@ -24,7 +24,7 @@ import yaml
 
 from ..api import core, meta as m
 from ..client.rest import APIStatusError, Client, is_already_exists, is_not_found, resource_path
-from . import extra, printers
+from . import config_cmd, extra, printers
 
 DEFAULT_KUBECONFIG = os.path.expanduser("~/.kube/config")
 
@@ -32,11 +32,9 @@ DEFAULT_KUBECONFIG = os.path.expanduser("~/.kube/config")
 # ---------------------------------------------------------------------------
 # kubeconfig
 def load_kubeconfig(path=None):
-    path = path or os.environ.get("KUBECONFIG") or DEFAULT_KUBECONFIG
-    if not os.path.exists(path):
-        return {"apiVersion": "v1", "kind": "Config", "clusters": [], "contexts": [], "users": [], "current-context": ""}, path
-    with open(path) as f:
-        return yaml.safe_load(f) or {}, path
+    """-> (merged kubeconfig, the file writes go to); KUBECONFIG may list several files."""
+    cfg, files = config_cmd.load(path)
+    return cfg, files[0][0]
 
 
 def save_kubeconfig(cfg, path):
@@ -1576,38 +1574,8 @@ class Kubectl(extra.ExtraCommands):
         self.p(f"{ri.kind.lower()}/{name} edited")
 
 
-def cmd_config(a):
-    cfg, path = load_kubeconfig(a.kubeconfig)
-    if a.action == "view":
-        print(yaml.safe_dump(cfg, sort_keys=False).rstrip())
-    elif a.action == "current-context":
-        print(cfg.get("current-context", ""))
-    elif a.action == "get-contexts":
-        rows = [["*" if c["name"] == cfg.get("current-context") else "", c["name"], c["context"].get("cluster", ""),
-                 c["context"].get("user", ""), c["context"].get("namespace", "")] for c in cfg.get("contexts") or ()]
-        print(printers.table(rows, ["CURRENT", "NAME", "CLUSTER", "AUTHINFO", "NAMESPACE"]))
-    elif a.action == "use-context":
-        cfg["current-context"] = a.name
-        save_kubeconfig(cfg, path)
-        print(f'Switched to context "{a.name}".')
-    elif a.action == "set-cluster":
-        cl = [c for c in cfg.setdefault("clusters", []) if c["name"] != a.name]
-        cl.append({"name": a.name, "cluster": {"server": a.server_url}})
-        cfg["clusters"] = cl
-        save_kubeconfig(cfg, path)
-        print(f'Cluster "{a.name}" set.')
-    elif a.action == "set-credentials":
-        us = [u for u in cfg.setdefault("users", []) if u["name"] != a.name]
-        us.append({"name": a.name, "user": {"token": a.user_token}})
-        cfg["users"] = us
-        save_kubeconfig(cfg, path)
-        print(f'User "{a.name}" set.')
-    elif a.action == "set-context":
-        cs = [c for c in cfg.setdefault("contexts", []) if c["name"] != a.name]
-        cs.append({"name": a.name, "context": {"cluster": a.cluster, "user": a.user, "namespace": a.ctx_namespace or "default"}})
-        cfg["contexts"] = cs
-        save_kubeconfig(cfg, path)
-        print(f'Context "{a.name}" modified.')
+def cmd_config(a, out=sys.stdout):
+    return config_cmd.run(a, out)
 
 
 def _bool(v):
@@ -1922,15 +1890,7 @@ def build_parser():
     cert.add_argument("action", choices=["approve", "deny"])
     cert.add_argument("names", nargs="+")
     extra.add_parsers(add)
-    cf = add("config")
-    cf.add_argument("action", choices=["view", "current-context", "get-contexts", "use-context", "set-cluster",
-                                       "set-context", "set-credentials"])
-    cf.add_argument("name", nargs="?")
-    cf.add_argument("--server", dest="server_url")
-    cf.add_argument("--cluster")
-    cf.add_argument("--user")
-    cf.add_argument("--token", dest="user_token")
-    cf.add_argument("--namespace", dest="ctx_namespace")
+    config_cmd.add_parser(add)
     return ap
 
 
@@ -1944,16 +1904,21 @@ GLOBAL_FLAGS = {"-s", "--server", "--token", "--kubeconfig", "--context", "-n", 
 def hoist_global_flags(argv):
     """kubectl accepts its persistent flags anywhere (cobra); move them before the command."""
     front, rest, i = [], [], 0
+    flags = GLOBAL_FLAGS
     while i < len(argv):
         t = argv[i]
+        if t == "config" and not rest:
+            # config's own --server / --token / --namespace (set-cluster, set-credentials,
+            # set-context) shadow the global ones
+            flags = {"--kubeconfig", "--context"}
         if t == "--":
             rest += argv[i:]
             break
-        if t in GLOBAL_FLAGS and i + 1 < len(argv):
+        if t in flags and i + 1 < len(argv):
             front += [t, argv[i + 1]]
             i += 2
             continue
-        if t.split("=", 1)[0] in GLOBAL_FLAGS and "=" in t:
+        if t.split("=", 1)[0] in flags and "=" in t:
             front.append(t)
             i += 1
             continue
@@ -1980,8 +1945,7 @@ def main(argv=None, out=sys.stdout):
             ap.error("unrecognized arguments: " + " ".join(bad or extras))
         setattr(a, dest, list(getattr(a, dest) or []) + extras)
     if a.command == "config":
-        cmd_config(a)
-        return 0
+        return cmd_config(a, out)
     if a.command == "completion":
         print(extra.completion(a.shell, ap), file=out)
         return 0
