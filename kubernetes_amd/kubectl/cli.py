@@ -266,8 +266,10 @@ class Kubectl(extra.ExtraCommands):
             for o in objs:
                 o.setdefault("kind", ri.kind)
                 evs = []
+                from .describe import gather
+                ctx = await gather(self.client, o)
                 if not a.show_events:
-                    self.p(printers.describe(o, []))
+                    self.p(printers.describe(o, [], ctx))
                     self.p("")
                     continue
                 try:
@@ -275,7 +277,7 @@ class Kubectl(extra.ExtraCommands):
                     evs = (await self.client.list("events", o["metadata"].get("namespace") or "default", field_selector=fs))["items"]
                 except APIStatusError:
                     pass
-                self.p(printers.describe(o, evs))
+                self.p(printers.describe(o, evs, ctx))
                 self.p("")
 
     LAST_APPLIED = "kubectl.kubernetes.io/last-applied-configuration"

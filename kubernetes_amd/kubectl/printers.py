@@ -217,7 +217,9 @@ def sort_objects(objs, expr):
     return sorted(objs, key=key)
 
 
-def describe(obj, events=()):
+def describe(obj, events=(), ctx=None):
+    """`kubectl describe` text; `ctx` carries related objects from `describe.gather()`."""
+    from . import describe as dsc
     kind = obj.get("kind")
     md = obj["metadata"]
     lines = [f"Name:         {md['name']}"]
@@ -257,6 +259,7 @@ def describe(obj, events=()):
         lines.append("Conditions:")
         for cd in st.get("conditions") or ():
             lines.append(f"  {cd.get('type'):<16} {cd.get('status')}")
+        lines += dsc.pod_extra(obj, ctx or {})
     elif kind == "Node":
         st = obj.get("status") or {}
         lines.append("Conditions:")
@@ -287,11 +290,10 @@ def describe(obj, events=()):
         taints = (obj.get("spec") or {}).get("taints") or []
         lines.append(f"Taints:       {', '.join(t['key'] + ':' + t['effect'] for t in taints) or '<none>'}")
         lines.append(f"Unschedulable: {bool((obj.get('spec') or {}).get('unschedulable'))}")
+        lines += dsc.node_extra(obj, ctx or {})
     else:
-        for k in ("spec", "status"):
-            if k in obj:
-                lines.append(f"{k.capitalize()}:")
-                lines += ["  " + ln for ln in yaml.safe_dump(obj[k], sort_keys=False).rstrip().splitlines()]
+        extra = dsc.sections(obj, ctx)
+        lines += extra if extra is not None else dsc.fallback(obj)
     if events:
         lines.append("Events:")
         rows, h = rows_for("Event", list(events))

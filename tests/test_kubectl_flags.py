@@ -132,7 +132,8 @@ def test_patch_scale_rollout_pause(cluster, tmp_path):
     assert json.loads(out)["spec"]["replicas"] == 5
     assert json.loads(k(cluster, "get", "deployment", "web", "-o", "json")[1])["spec"]["replicas"] == 1
     rc, out = k(cluster, "scale", "deployments", "-l", "tier=fe", "--replicas", "2", "--timeout", "30")
-    assert rc == 0 and 'deployment "web" scaled' in out
+    assert rc == 0, out
+    assert 'deployment "web" scaled' in out, out
     assert k(cluster, "rollout", "pause", "deployment/web")[1].strip() == 'deployment "web" paused'
     assert json.loads(k(cluster, "get", "deployment", "web", "-o", "json")[1])["spec"]["paused"] is True
     assert "already paused" in k(cluster, "rollout", "pause", "deployment/web")[1]
@@ -144,7 +145,8 @@ def test_patch_scale_rollout_pause(cluster, tmp_path):
     assert svc["spec"]["selector"] == {"app": "web"} and svc["metadata"]["labels"] == {"tier": "fe"}
     rc, out = k(cluster, "expose", "deployment", "web", "--port", "80", "--target-port", "8080", "--type", "NodePort",
                 "--name", "web-np")
-    assert rc == 0 and "service/web-np exposed" in out
+    assert rc == 0, out
+    assert "service/web-np exposed" in out, out
     s = json.loads(k(cluster, "get", "svc", "web-np", "-o", "json")[1])
     assert s["spec"]["type"] == "NodePort" and s["spec"]["ports"][0]["targetPort"] == 8080
 
@@ -264,3 +266,31 @@ def test_logs_flags(run, tmp_path):
         finally:
             await cl.stop()
     run(main())
+
+
+def test_describe_kinds(cluster, tmp_path):
+    """Per-kind describers (`pkg/printers/internalversion/describe.go`)."""
+    dep = {"apiVersion": "apps/v1beta1", "kind": "Deployment", "metadata": {"name": "dsc"},
+           "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "dsc"}},
+                    "template": {"metadata": {"labels": {"app": "dsc"}},
+                                 "spec": {"containers": [{"name": "c", "image": "busybox", "env": [{"name": "A", "value": "1"}],
+                                                          "ports": [{"containerPort": 7000}],
+                                                          "resources": {"limits": {"cpu": "100m"}}}]}}}}
+    _create(cluster, tmp_path, dep)
+    wait(lambda: "2 available" in k(cluster, "describe", "deployment", "dsc")[1])
+    out = k(cluster, "describe", "deployment", "dsc")[1]
+    assert "2 desired | 2 updated | 2 total | 2 available" in out and "RollingUpdateStrategy:  25% max unavailable" in out
+    assert "NewReplicaSet:   dsc-" in out and "A:  1" in out and "Port:       7000/TCP" in out
+    rs = json.loads(k(cluster, "get", "rs", "-l", "app=dsc", "-o", "json")[1])["items"][0]["metadata"]["name"]
+    assert "Pods Status:  2 Running / 0 Waiting" in k(cluster, "describe", "rs", rs)[1]
+    k(cluster, "expose", "deployment", "dsc", "--port", "80", "--target-port", "7000")
+    out = wait(lambda: (lambda o: o if "Endpoints:         <none>" not in o else None)(k(cluster, "describe", "svc", "dsc")[1]))
+    assert "Type:              ClusterIP" in out and "TargetPort:        7000/TCP" in out and ":7000" in out
+    sec = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "dsc-s"}, "data": {"pw": "aHVudGVyMg=="}}
+    _create(cluster, tmp_path, sec)
+    out = k(cluster, "describe", "secret", "dsc-s")[1]
+    assert "pw:  7 bytes" in out and "hunter2" not in out and "aHVudGVyMg" not in out
+    out = k(cluster, "describe", "namespace", "default")[1]
+    assert "Status:  Active" in out and "No resource quota." in out
+    out = k(cluster, "describe", "node", "node-0")[1]
+    assert "Non-terminated Pods:" in out and "Allocated resources:" in out and "amd.com/gpu" in out
