@@ -651,15 +651,24 @@ class Kubectl(extra.ExtraCommands):
                     raise SystemExit(f"error: Expected replicas to be {a.current_replicas}, was {cur}")
                 await self.client.patch("jobs", name, {"spec": {"parallelism": a.replicas}}, self.ns)
             else:
-                scale = await self.client.get(ri.plural, name, self.ns, subresource="scale")
-                cur = (scale.get("spec") or {}).get("replicas", 0)
-                if a.current_replicas is not None and a.current_replicas != cur:
-                    raise SystemExit(f"error: Expected replicas to be {a.current_replicas}, was {cur}")
-                if a.resource_version and a.resource_version != scale["metadata"].get("resourceVersion"):
-                    raise SystemExit(f"error: Expected resourceVersion to be {a.resource_version}, "
-                                     f"was {scale['metadata'].get('resourceVersion')}")
-                scale["spec"] = {"replicas": a.replicas}
-                await self.client.update(ri.plural, scale, self.ns, subresource="scale")
+                # ScaleWithRetries (pkg/kubectl/scale.go): a conflict from a concurrent status
+                # write is retried against the fresh Scale; the preconditions are re-checked
+                for attempt in range(8):
+                    scale = await self.client.get(ri.plural, name, self.ns, subresource="scale")
+                    cur = (scale.get("spec") or {}).get("replicas", 0)
+                    if a.current_replicas is not None and a.current_replicas != cur:
+                        raise SystemExit(f"error: Expected replicas to be {a.current_replicas}, was {cur}")
+                    if a.resource_version and a.resource_version != scale["metadata"].get("resourceVersion"):
+                        raise SystemExit(f"error: Expected resourceVersion to be {a.resource_version}, "
+                                         f"was {scale['metadata'].get('resourceVersion')}")
+                    scale["spec"] = {"replicas": a.replicas}
+                    try:
+                        await self.client.update(ri.plural, scale, self.ns, subresource="scale")
+                        break
+                    except APIStatusError as e:
+                        if e.code != 409 or a.resource_version or attempt == 7:
+                            raise
+                        await asyncio.sleep(0.01 * (attempt + 1))
             self.p(f"{ri.kind.lower()} \"{name}\" scaled")
             if a.timeout and ri.plural != "jobs":
                 end = time.monotonic() + a.timeout

@@ -169,6 +169,29 @@ def render(objs, output, kind=None, wide=False, all_ns=False, list_obj=None, sor
         return yaml.safe_dump(list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else {"kind": "List", "apiVersion": "v1", "items": objs}), sort_keys=False).rstrip()
     if output == "name":
         return "\n".join(f"{(o.get('kind') or kind or '').lower()}/{o['metadata']['name']}" for o in objs)
+    for pre in ("jsonpath-file=", "custom-columns-file=", "go-template-file=", "templatefile="):
+        if output and output.startswith(pre):
+            with open(output[len(pre):]) as f:
+                body = f.read()
+            if pre == "custom-columns-file=":
+                # a header line of names and a line of JSONPath specs (`customcolumn.go`)
+                lines = [ln.split() for ln in body.splitlines() if ln.strip()]
+                if len(lines) != 2 or len(lines[0]) != len(lines[1]):
+                    raise SystemExit("error: custom-columns-file needs a header line and a spec line of equal width")
+                output = "custom-columns=" + ",".join(f"{h}:{p}" for h, p in zip(*lines))
+            else:
+                output = {"jsonpath-file=": "jsonpath=", "go-template-file=": "go-template=",
+                          "templatefile=": "go-template="}[pre] + body
+            break
+    if output and output.startswith(("go-template=", "template=")):
+        from .gotemplate import TemplateError
+        from .gotemplate import render as gotemplate
+        target = list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else
+                                                         {"kind": "List", "apiVersion": "v1", "items": objs})
+        try:
+            return gotemplate(output.split("=", 1)[1], target)
+        except TemplateError as e:
+            raise SystemExit(f"error: error executing template {output.split('=', 1)[1]!r}: {e}")
     if output and output.startswith("jsonpath="):
         target = list_obj if list_obj is not None else (objs[0] if len(objs) == 1 else {"items": objs})
         return jsonpath(target, output[len("jsonpath="):])

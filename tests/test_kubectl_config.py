@@ -89,3 +89,32 @@ def test_config_flatten_and_kubeconfig_merge(tmp_path, monkeypatch):
     kubectl(["config", "set-context", "ctx-b", "--namespace", "x"], out=out)
     assert yaml.safe_load(b.read_text())["contexts"][0]["context"]["namespace"] == "x"    # written where it lives
     assert "ctx-b" not in a.read_text()
+
+
+def test_go_template_and_file_outputs(tmp_path):
+    """`-o go-template=` / `template=` / `*-file=` (`pkg/printers/template.go`, customcolumn.go)."""
+    from kubernetes_amd.kubectl.gotemplate import TemplateError, render as gt
+    from kubernetes_amd.kubectl.printers import render
+    pods = [{"kind": "Pod", "metadata": {"name": "a", "labels": {"app": "x"}}, "status": {"phase": "Running"}},
+            {"kind": "Pod", "metadata": {"name": "b"}, "status": {"phase": "Pending"}}]
+    lst = {"kind": "List", "items": pods}
+    assert render(pods, 'go-template={{range .items}}{{.metadata.name}}{{"\\n"}}{{end}}', list_obj=lst) == "a\nb\n"
+    t = ('{{range $i, $p := .items}}{{if eq $p.status.phase "Running"}}{{$i}}:up{{else if eq $p.status.phase "Pending"}}'
+         '{{$i}}:wait{{else}}?{{end}} {{end}}')
+    assert gt(t, lst) == "0:up 1:wait "
+    assert gt('{{(index .items 0).metadata.labels}} {{len .items}} {{printf "%s=%d" "n" 2}}', lst) == "map[app:x] 2 n=2"
+    assert gt('{{.data.pw | base64decode}}{{with .nope}}x{{else}}-none{{end}} {{.missing}}', {"data": {"pw": "aGk="}}) == \
+        "hi-none <no value>"
+    assert gt('{{- range .items -}}\n  {{ .metadata.name }}\n{{- end }}', lst) == "ab"
+    with pytest.raises(TemplateError):
+        gt("{{if .x}}unterminated", {})
+    f = tmp_path / "t.tmpl"
+    f.write_text("{{range .items}}<{{.metadata.name}}>{{end}}")
+    assert render(pods, f"go-template-file={f}", list_obj=lst) == "<a><b>"
+    cc = tmp_path / "cols"
+    cc.write_text("NAME PHASE\n.metadata.name .status.phase\n")
+    out = render(pods, f"custom-columns-file={cc}").splitlines()
+    assert out[0].split() == ["NAME", "PHASE"] and out[1].split() == ["a", "Running"]
+    jp = tmp_path / "jp"
+    jp.write_text("{.items[*].metadata.name}")
+    assert render(pods, f"jsonpath-file={jp}", list_obj=lst) == "a b"
