@@ -45,6 +45,7 @@ from ..storage.mvcc import CompactedError, MVCCStore
 from ..utils.httpserver import HandoffResponse, HTTPServer, Response, StreamResponse, UpgradeResponse
 from ..utils.metrics import Registry
 from ..utils.patch import JSONPatchError, apply_patch
+from . import impersonation
 from . import admission as adm
 from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, User, build_authorizer
 from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, event_bytes
@@ -1373,6 +1374,14 @@ class APIServer:
                 if user is None:
                     code = 401
                     return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))
+            if user is not UNSECURED and impersonation.requested(req.headers):
+                try:
+                    user = impersonation.impersonate(
+                        req.headers, user, lambda u, verb, ns, res, sub, name, grp:
+                        self._authorize(u, verb, ns, res, sub, name, grp, p))
+                except impersonation.ImpersonationError as e:
+                    code = e.code
+                    return _json(e.code, m.status_obj(e.code, "BadRequest", e.message))
             req.user = user
             if p == "/logs" or p.startswith("/logs/"):
                 self._authorize(user, "get", None, "", "", "", "", p, resource_request=False)

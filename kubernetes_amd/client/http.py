@@ -83,10 +83,14 @@ class HTTPClient:
             self.ssl.check_hostname = False
             self.ssl.verify_mode = _ssl.CERT_NONE
         self.token = token
+        self.default_headers = ""      # preformatted lines sent on every request (impersonation, basic auth)
         self._idle: list[_Conn] = []
         self._sem = asyncio.Semaphore(max_conns)
         self.timeout = timeout
         self._closed = False
+
+    def set_default_headers(self, headers: dict):
+        self.default_headers = "".join(f"{k}: {v}\r\n" for k, v in headers.items() if v)
 
     def set_ssl_context(self, ctx):
         """Swap the TLS context (client-certificate rotation): idle connections made with the
@@ -107,6 +111,8 @@ class HTTPClient:
         h = f"{method} {self.path_prefix}{path} HTTP/1.1\r\nHost: {self.host_header}\r\n"
         if self.token:
             h += f"Authorization: Bearer {self.token}\r\n"
+        if self.default_headers:
+            h += self.default_headers
         if body is not None:
             h += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n"
         if extra:

@@ -45,11 +45,34 @@ def save_kubeconfig(cfg, path):
 
 def resolve_server(args):
     """-> (server, token, namespace, ssl context) from flags or the kubeconfig (client-go clientcmd)."""
+    server, token, ns, ctx = _resolve_kubeconfig(args)
+    # --insecure-skip-tls-verify / --certificate-authority / --client-certificate / --client-key
+    # override the kubeconfig's TLS material (clientcmd ConfigOverrides)
+    ca, cert, key = (getattr(args, f, None) for f in ("certificate_authority", "client_certificate", "client_key"))
+    if server.startswith("https") and (getattr(args, "insecure_skip_tls_verify", False) or ca or cert):
+        from ..utils.tlsutil import client_context
+        ctx = client_context(None if getattr(args, "insecure_skip_tls_verify", False) else ca, cert, key)
+    return server, token, ns, ctx
+
+
+def _resolve_kubeconfig(args):
     if args.server:
         return args.server, args.token, args.namespace, None
     from ..client import clientcmd
     cfg, path = load_kubeconfig(args.kubeconfig)
-    r = clientcmd.resolve(cfg, args.context, os.path.dirname(os.path.abspath(path)))
+    ctx_name = args.context
+    if getattr(args, "cluster", None) or getattr(args, "user", None):
+        # --cluster / --user override the chosen context's entries
+        base = next((c for c in cfg.get("contexts") or () if c["name"] == (ctx_name or cfg.get("current-context"))),
+                    {"context": {}})
+        ov = dict(base.get("context") or {})
+        if getattr(args, "cluster", None):
+            ov["cluster"] = args.cluster
+        if getattr(args, "user", None):
+            ov["user"] = args.user
+        cfg = dict(cfg, contexts=list(cfg.get("contexts") or ()) + [{"name": "\0override", "context": ov}])
+        ctx_name = "\0override"
+    r = clientcmd.resolve(cfg, ctx_name, os.path.dirname(os.path.abspath(path)))
     if r is None:
         return os.environ.get("KUBERNETES_MASTER", "http://127.0.0.1:8080"), args.token, args.namespace, None
     return r.server, args.token or r.token, args.namespace or r.namespace, r.ssl_context
@@ -115,6 +138,17 @@ def split_targets(targets):
     return out
 
 
+def _duration_s(v) -> float:
+    """--request-timeout: `0` (none), a bare number of seconds, or 1s / 2m / 3h."""
+    v = str(v or "0").strip()
+    if v in ("", "0"):
+        return 0.0
+    if v[-1].isdigit():
+        return float(v)
+    from ..kubelet.eviction import parse_duration
+    return float(parse_duration(v))
+
+
 class Kubectl(extra.ExtraCommands):
     def __init__(self, args, out=sys.stdout):
         self.a = args
@@ -122,7 +156,19 @@ class Kubectl(extra.ExtraCommands):
         server, token, ns, ctx = resolve_server(args)
         self.server = server
         self.ns = ns or "default"
-        self.client = Client(server, token=token, ssl_context=ctx)
+        self.client = Client(server, token=token, ssl_context=ctx,
+                             timeout=_duration_s(getattr(args, "request_timeout", "0")) or 60.0)
+        hdrs = {}
+        if getattr(args, "as_user", None):
+            hdrs["Impersonate-User"] = args.as_user
+        if getattr(args, "as_group", None):
+            hdrs["Impersonate-Group"] = ",".join(args.as_group)
+        if getattr(args, "username", None) and not token:
+            import base64
+            hdrs["Authorization"] = "Basic " + base64.b64encode(
+                f"{args.username}:{args.password or ''}".encode()).decode()
+        if hdrs:
+            self.client.http.set_default_headers(hdrs)
 
     def p(self, *s):
         print(*s, file=self.out)
@@ -1600,11 +1646,24 @@ def _common(p):
 
 
 def build_parser():
-    ap = argparse.ArgumentParser("kubectl")
+    ap = argparse.ArgumentParser("kubectl", allow_abbrev=False)   # `version --client` is no prefix of --client-key
     ap.add_argument("-s", "--server")
     ap.add_argument("--token")
     ap.add_argument("--kubeconfig")
     ap.add_argument("--context")
+    ap.add_argument("--as", dest="as_user", help="impersonate this user")
+    ap.add_argument("--as-group", action="append", default=[], help="impersonate this group (repeatable)")
+    ap.add_argument("--cluster", dest="cluster", help="kubeconfig cluster to use")
+    ap.add_argument("--user", dest="user", help="kubeconfig user to use")
+    ap.add_argument("--insecure-skip-tls-verify", action="store_true")
+    ap.add_argument("--certificate-authority")
+    ap.add_argument("--client-certificate")
+    ap.add_argument("--client-key")
+    ap.add_argument("--request-timeout", default="0")
+    ap.add_argument("--username")
+    ap.add_argument("--password")
+    ap.add_argument("-v", "--v", dest="verbosity", type=int, default=0)
+    ap.add_argument("--match-server-version", action="store_true")
     ap.add_argument("-n", "--namespace")
     sub = ap.add_subparsers(dest="command", required=True)
 
@@ -1909,7 +1968,10 @@ _TRAILING = {"label": "pairs", "annotate": "pairs", "taint": "taints", "get": "t
              "delete": "targets", "patch": "targets", "scale": "targets", "expose": "targets", "edit": "targets",
              "rollout": "targets", "autoscale": "targets", "wait": "targets", "port-forward": "ports"}
 
-GLOBAL_FLAGS = {"-s", "--server", "--token", "--kubeconfig", "--context", "-n", "--namespace"}
+GLOBAL_FLAGS = {"-s", "--server", "--token", "--kubeconfig", "--context", "-n", "--namespace", "--as", "--as-group",
+                "--cluster", "--user", "--certificate-authority", "--client-certificate", "--client-key",
+                "--request-timeout", "--username", "--password", "-v", "--v"}
+GLOBAL_SWITCHES = {"--insecure-skip-tls-verify", "--match-server-version"}
 
 
 def hoist_global_flags(argv):
@@ -1922,12 +1984,18 @@ def hoist_global_flags(argv):
             # config's own --server / --token / --namespace (set-cluster, set-credentials,
             # set-context) shadow the global ones
             flags = {"--kubeconfig", "--context"}
+        elif t == "create" and not rest:
+            flags = flags - {"--user"}        # create (cluster)rolebinding --user is a subject
         if t == "--":
             rest += argv[i:]
             break
         if t in flags and i + 1 < len(argv):
             front += [t, argv[i + 1]]
             i += 2
+            continue
+        if t in GLOBAL_SWITCHES and flags is not None and "--context" in flags and len(flags) > 2:
+            front.append(t)
+            i += 1
             continue
         if t.split("=", 1)[0] in flags and "=" in t:
             front.append(t)
