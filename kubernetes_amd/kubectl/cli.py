@@ -458,6 +458,86 @@ class Kubectl(extra.ExtraCommands):
         for d in read_manifests(self.a.filename, self.a.recursive):
             await self._apply_one(d, "replace")
 
+    async def _last_applied_targets(self):
+        a = self.a
+        if a.filename:
+            return [(ri_for_obj(d), d) for d in read_manifests(a.filename, a.recursive)]
+        out = []
+        for ri, name in split_targets(a.targets):
+            ns = self.ns if ri.namespaced else None
+            if name:
+                out.append((ri, await self.client.get(ri.plural, name, ns)))
+            elif a.all or a.selector:
+                out += [(ri, o) for o in (await self.client.list(ri.plural, ns, a.selector))["items"]]
+            else:
+                raise SystemExit("error: a resource name, -l or --all is required")
+        return out
+
+    async def cmd_apply_view_last_applied(self):
+        """`kubectl apply view-last-applied` (pkg/kubectl/cmd/apply_view_last_applied.go)."""
+        a = self.a
+        for ri, o in await self._last_applied_targets():
+            if a.filename:
+                o = await self.client.get(ri.plural, o["metadata"]["name"], self.ns_for(ri, o))
+            ann = (o["metadata"].get("annotations") or {}).get(self.LAST_APPLIED)
+            if ann is None:
+                raise SystemExit(f"error: no last-applied-configuration annotation found on resource: {o['metadata']['name']}")
+            cfg = json.loads(ann)
+            self.p(json.dumps(cfg, indent=2) if a.output == "json" else yaml.safe_dump(cfg, sort_keys=False).rstrip())
+
+    async def cmd_apply_set_last_applied(self):
+        """`kubectl apply set-last-applied -f FILE`: overwrite the annotation with the file's
+        content; without --create-annotation the object must already carry one."""
+        a = self.a
+        if not a.filename:
+            raise SystemExit("error: -f is required for set-last-applied")
+        for ri, d in await self._last_applied_targets():
+            ns = self.ns_for(ri, d)
+            cur = await self.client.get(ri.plural, d["metadata"]["name"], ns)
+            if self.LAST_APPLIED not in (cur["metadata"].get("annotations") or {}) and not a.create_annotation:
+                raise SystemExit(f"error: no last-applied-configuration annotation found on resource: "
+                                 f"{d['metadata']['name']}, to create the annotation, run the command with --create-annotation")
+            d = json.loads(json.dumps(d))
+            (d["metadata"].get("annotations") or {}).pop(self.LAST_APPLIED, None)
+            patch = {"metadata": {"annotations": {self.LAST_APPLIED: json.dumps(d, sort_keys=True, separators=(",", ":"))}}}
+            if a.dry_run:
+                self.p(f"{ri.kind.lower()}/{d['metadata']['name']} configured (dry run)")
+                continue
+            out = await self.client.patch(ri.plural, d["metadata"]["name"], patch, ns, "merge")
+            self.p(printers.render([out], a.output, ri.kind) if a.output else f"{ri.kind.lower()}/{d['metadata']['name']} configured")
+
+    async def cmd_apply_edit_last_applied(self):
+        """`kubectl apply edit-last-applied`: $EDITOR over the annotation, written back."""
+        import subprocess
+        import tempfile
+        a = self.a
+        for ri, o in await self._last_applied_targets():
+            if a.filename:
+                o = await self.client.get(ri.plural, o["metadata"]["name"], self.ns_for(ri, o))
+            ann = (o["metadata"].get("annotations") or {}).get(self.LAST_APPLIED)
+            if ann is None:
+                raise SystemExit(f"error: no last-applied-configuration annotation found on resource: {o['metadata']['name']}")
+            cfg = json.loads(ann)
+            text = json.dumps(cfg, indent=2) + "\n" if a.output == "json" else yaml.safe_dump(cfg, sort_keys=False)
+            with tempfile.NamedTemporaryFile("w", suffix="." + a.output, delete=False) as f:
+                f.write(text)
+                path = f.name
+            try:
+                editor = os.environ.get("KUBE_EDITOR") or os.environ.get("EDITOR") or "vi"
+                if subprocess.call(editor.split() + [path]) != 0:
+                    raise SystemExit("error: editor failed")
+                with open(path) as f:
+                    new_text = f.read()
+            finally:
+                os.unlink(path)
+            if new_text == text:
+                self.p("Edit cancelled, no changes made.")
+                continue
+            new = yaml.safe_load(new_text)
+            patch = {"metadata": {"annotations": {self.LAST_APPLIED: json.dumps(new, sort_keys=True, separators=(",", ":"))}}}
+            await self.client.patch(ri.plural, o["metadata"]["name"], patch, o["metadata"].get("namespace"), "merge")
+            self.p(f"{ri.kind.lower()}/{o['metadata']['name']} edited")
+
     async def cmd_delete(self):
         a = self.a
         targets = []
@@ -1340,10 +1420,32 @@ class Kubectl(extra.ExtraCommands):
             for d in read_manifests(a.filename or []):
                 await self._reconcile(d)
             return
-        ri = m.lookup(a.resource)
-        st, body = await self.client.raw("GET", f"{'/api/v1' if not ri.group else f'/apis/{ri.group}/{ri.version}'}"
-                                         f"{'/namespaces/' + self.ns if ri.namespaced else ''}/{ri.plural}?limit=1")
-        self.p("yes" if st == 200 else "no")
+        # `kubectl auth can-i VERB TYPE[/NAME] | NONRESOURCEURL` (pkg/kubectl/cmd/auth/cani.go):
+        # a SelfSubjectAccessReview, so it answers for the caller's (or --as) identity
+        if not a.verb or not a.resource:
+            raise SystemExit("error: you must specify two or three arguments: verb, resource, and optional resourceName")
+        attrs = {}
+        if a.resource.startswith("/"):
+            attrs = {"nonResourceAttributes": {"verb": a.verb, "path": a.resource}}
+        else:
+            kind, _, name = a.resource.partition("/")
+            name = name or a.resource_name or ""
+            ri = m.lookup(kind)
+            group, plural = (ri.group, ri.plural) if ri is not None else (kind.partition(".")[2], kind.partition(".")[0])
+            ra = {"verb": a.verb, "resource": plural, "group": group, "name": name,
+                  "namespace": "" if a.all_namespaces or (ri is not None and not ri.namespaced) else self.ns}
+            if a.subresource:
+                ra["subresource"] = a.subresource
+            attrs = {"resourceAttributes": ra}
+        body = {"apiVersion": "authorization.k8s.io/v1", "kind": "SelfSubjectAccessReview", "spec": attrs}
+        st, resp = await self.client.raw("POST", "/apis/authorization.k8s.io/v1/selfsubjectaccessreviews",
+                                         json.dumps(body).encode())
+        if st not in (200, 201):
+            raise SystemExit(f"error: {resp.decode(errors='replace')}")
+        allowed = bool((json.loads(resp).get("status") or {}).get("allowed"))
+        if not a.quiet:
+            self.p("yes" if allowed else "no")
+        self.rc = 0 if allowed else 1
 
     # -- streaming: exec / attach / port-forward / cp / proxy / edit ------------------------
     def _pod_path(self, name, sub):
@@ -1725,6 +1827,18 @@ def build_parser():
             c.add_argument("--prune-whitelist", action="append", default=[])
             c.add_argument("--overwrite", type=_bool, default=True)
             c.add_argument("--openapi-patch", type=_bool, default=True)
+    for sub_ in ("view-last-applied", "set-last-applied", "edit-last-applied"):
+        la_ = add("apply-" + sub_, help=argparse.SUPPRESS)
+        la_.add_argument("targets", nargs="*")
+        la_.add_argument("-f", "--filename", action="append")
+        la_.add_argument("-o", "--output", default="yaml" if sub_ != "set-last-applied" else "",
+                         choices=["yaml", "json"] if sub_ != "set-last-applied" else None)
+        la_.add_argument("--all", action="store_true")
+        la_.add_argument("-l", "--selector")
+        la_.add_argument("--create-annotation", action="store_true")
+        la_.add_argument("--dry-run", action="store_true")
+        la_.add_argument("--record", action="store_true")
+        _common(la_)
     de = add("delete")
     de.add_argument("targets", nargs="*")
     de.add_argument("-f", "--filename", action="append")
@@ -1901,7 +2015,11 @@ def build_parser():
     au.add_argument("action", choices=["can-i", "reconcile"])
     au.add_argument("verb", nargs="?")
     au.add_argument("resource", nargs="?")
+    au.add_argument("resource_name", nargs="?")
     au.add_argument("-f", "--filename", action="append")
+    au.add_argument("-A", "--all-namespaces", action="store_true")
+    au.add_argument("-q", "--quiet", action="store_true")
+    au.add_argument("--subresource", default="")
     exq = add("exec")
     exq.add_argument("pod")
     exq.add_argument("-c", "--container")
@@ -2009,6 +2127,12 @@ def hoist_global_flags(argv):
 def main(argv=None, out=sys.stdout):
     ap = build_parser()
     argv = hoist_global_flags(list(sys.argv[1:] if argv is None else argv))
+    for i_, t_ in enumerate(argv[:-1]):
+        if t_ == "apply" and argv[i_ + 1] in ("view-last-applied", "set-last-applied", "edit-last-applied"):
+            argv = argv[:i_] + ["apply-" + argv[i_ + 1]] + argv[i_ + 2:]   # `apply view-last-applied ...`
+            break
+        if not t_.startswith("-") and (i_ == 0 or not argv[i_ - 1].startswith("-")):
+            break
     tail = None
     if "--" in argv and "run" in argv[:argv.index("--")]:
         argv, tail = argv[:argv.index("--")], argv[argv.index("--") + 1:]     # `run NAME ... -- CMD ARGS`

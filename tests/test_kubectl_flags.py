@@ -294,3 +294,29 @@ def test_describe_kinds(cluster, tmp_path):
     assert "Status:  Active" in out and "No resource quota." in out
     out = k(cluster, "describe", "node", "node-0")[1]
     assert "Non-terminated Pods:" in out and "Allocated resources:" in out and "amd.com/gpu" in out
+
+
+def test_apply_last_applied_and_can_i(cluster, tmp_path):
+    cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "lac"}, "data": {"a": "1"}}
+    f = tmp_path / "cm.yaml"
+    f.write_text(yaml.safe_dump(cm))
+    assert k(cluster, "apply", "-f", str(f))[0] == 0
+    rc, out = k(cluster, "apply", "view-last-applied", "configmap", "lac", "-o", "json")
+    assert json.loads(out)["data"] == {"a": "1"}
+    cm["data"] = {"a": "2", "b": "3"}
+    f.write_text(yaml.safe_dump(cm))
+    assert "configmap/lac configured" in k(cluster, "apply", "set-last-applied", "-f", str(f))[1]
+    assert yaml.safe_load(k(cluster, "apply", "view-last-applied", "configmap/lac")[1])["data"] == {"a": "2", "b": "3"}
+    assert json.loads(k(cluster, "get", "cm", "lac", "-o", "json")[1])["data"] == {"a": "1"}   # only the annotation
+    bare = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "bare"}, "data": {}}
+    _create(cluster, tmp_path, bare)
+    g = tmp_path / "bare.yaml"
+    g.write_text(yaml.safe_dump(bare))
+    with pytest.raises(SystemExit, match="--create-annotation"):
+        k(cluster, "apply", "set-last-applied", "-f", str(g))
+    assert k(cluster, "apply", "set-last-applied", "-f", str(g), "--create-annotation")[0] == 0
+    # auth can-i answers through a SelfSubjectAccessReview (the local cluster allows everything)
+    rc, out = k(cluster, "auth", "can-i", "create", "pods")
+    assert rc == 0 and out.strip() == "yes"
+    rc, out = k(cluster, "auth", "can-i", "get", "/healthz", "-q")
+    assert rc == 0 and out == ""
