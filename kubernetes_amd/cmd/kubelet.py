@@ -134,7 +134,8 @@ def main(argv=None):
                     "min_age": _duration(a.minimum_image_ttl_duration)} if cap else None
         labels = dict(kv.split("=", 1) for kv in a.node_labels.split(",") if "=" in kv)
         from ..kubelet import network as net
-        plugin = net.new_plugin(a.network_plugin, os.path.join(a.root_dir, "network"), a.cni_conf_dir, a.cni_bin_dir)
+        plugin = net.new_plugin(a.network_plugin, os.path.join(a.root_dir, "network"), a.cni_conf_dir, a.cni_bin_dir,
+                                hairpin_mode=a.hairpin_mode, mtu=getattr(a, "network_plugin_mtu", 0) or 1460)
         if a.pod_cidr:
             plugin.set_pod_cidr(a.pod_cidr)
         dns = net.DNSConfigurer(a.cluster_dns.split(","), a.cluster_domain, a.resolv_conf)
@@ -355,7 +356,9 @@ def _reference_flags(ap):
     g.add_argument("--experimental-qos-reserved", default="", help="accepted (alpha QOSReserved)")
     g.add_argument("--seccomp-profile-root", default="", help="accepted; seccomp profiles are not applied by this runtime")
     g = ap.add_argument_group("networking")
-    g.add_argument("--hairpin-mode", default="promiscuous-bridge", help="accepted; kubenet's bridge handles hairpin traffic")
+    g.add_argument("--network-plugin-mtu", type=int, default=0, help="kubenet bridge MTU (0: 1460)")
+    g.add_argument("--hairpin-mode", default="promiscuous-bridge", choices=["promiscuous-bridge", "hairpin-veth", "none"],
+                   help="kubenet: bridge promiscuous mode, or hairpin on each pod's veth port")
     g.add_argument("--non-masquerade-cidr", default="10.0.0.0/8", help="accepted")
     g.add_argument("--make-iptables-util-chains", type=_bool, default=True, help="accepted")
     g.add_argument("--iptables-masquerade-bit", type=int, default=14, help="accepted")

@@ -26,6 +26,7 @@ namespaces gets the same calls with a real netns path.
 from __future__ import annotations
 
 import asyncio
+import shutil
 import base64
 import hashlib
 import ipaddress
@@ -128,31 +129,93 @@ class NetworkPlugin:
 
 
 class KubenetPlugin(NetworkPlugin):
+    """kubenet (`pkg/kubelet/network/kubenet/kubenet_linux.go`): a Linux bridge (`cbr0`) over the
+    node's pod CIDR. With a network namespace and the CNI `bridge` / `host-local` / `loopback`
+    binaries in `--cni-bin-dir` it delegates exactly as the reference does — the generated
+    bridge config (isGateway, ipMasq off, hairpinMode, host-local IPAM over the pod CIDR, the
+    bridge MTU) and a loopback ADD — and `--hairpin-mode=promiscuous-bridge` puts the bridge in
+    promiscuous mode. Without a namespace (the process runtime shares the host network) it
+    allocates from the same host-local range in process."""
     name = "kubenet"
 
-    def __init__(self, data_dir, bridge="cbr0", mtu=1460):
+    def __init__(self, data_dir, bridge="cbr0", mtu=1460, cni_bin_dirs=(), hairpin_mode="promiscuous-bridge",
+                 non_masquerade_cidr="10.0.0.0/8"):
         self.ipam = HostLocalIPAM(os.path.join(data_dir, "networks", "kubenet"))
         self.bridge, self.mtu = bridge, mtu
         self.cidr = None
+        self.bin_dirs = [d for d in cni_bin_dirs if d]
+        if hairpin_mode not in ("promiscuous-bridge", "hairpin-veth", "none"):
+            raise ValueError(f"invalid hairpin mode {hairpin_mode!r}")
+        self.hairpin_mode = hairpin_mode
+        self.non_masquerade_cidr = non_masquerade_cidr
+        self._promisc_done = False
+        self._delegate = None
 
     def set_pod_cidr(self, cidr):
         if cidr and cidr != self.cidr:
             self.cidr = cidr
             self.ipam.set_cidr(cidr)
+            self._delegate = None
             log.info("kubenet: pod CIDR %s, bridge %s gateway %s", cidr, self.bridge, self.ipam.gateway)
+
+    def net_config(self):
+        """The bridge network kubenet hands to CNI (NET_CONFIG_TEMPLATE)."""
+        return {"cniVersion": "0.1.0", "name": "kubenet", "plugins": [
+            {"type": "bridge", "bridge": self.bridge, "mtu": self.mtu, "addIf": "eth0", "isGateway": True,
+             "ipMasq": False, "hairpinMode": self.hairpin_mode == "hairpin-veth",
+             "ipam": {"type": "host-local", "subnet": self.cidr, "gateway": self.ipam.gateway,
+                      "routes": [{"dst": "0.0.0.0/0"}]}}]}
+
+    def _cni(self):
+        if self._delegate is None and self.bin_dirs and self.cidr:
+            c = CNIPlugin.__new__(CNIPlugin)
+            c.conf_dir, c.bin_dirs, c.pod_cidr = None, list(self.bin_dirs), self.cidr
+            c.net = self.net_config()
+            c._load = lambda: None
+            try:
+                for typ in ("bridge", "host-local", "loopback"):
+                    c._find(typ)
+            except NetworkError:
+                return None
+            self._delegate = c
+        return self._delegate
 
     def status(self):
         if self.cidr is None:
             return "Kubenet does not have netConfig. This is most likely due to lack of PodCIDR"
         return None
 
+    async def _promiscuous(self):
+        # PromiscuousBridge: the bridge sees its own pods' hairpin traffic
+        if self._promisc_done or self.hairpin_mode != "promiscuous-bridge":
+            return
+        self._promisc_done = True
+        ip = shutil.which("ip")
+        if ip:
+            p = await asyncio.create_subprocess_exec(ip, "link", "set", self.bridge, "promisc", "on",
+                                                     stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.DEVNULL)
+            await p.wait()
+
     async def setup_pod(self, pod, sandbox_id, netns=""):
         if self.cidr is None:
             raise NetworkError(self.status())
-        return self.ipam.allocate(sandbox_id)
+        cni = self._cni() if netns else None
+        if cni is None:
+            return self.ipam.allocate(sandbox_id)
+        res = await cni._exec("ADD", cni.net["plugins"][0], pod, sandbox_id, netns)
+        await cni._exec("ADD", {"type": "loopback"}, pod, sandbox_id, netns)
+        await self._promiscuous()
+        return result_ip(res)
 
     async def teardown_pod(self, pod, sandbox_id, netns=""):
-        self.ipam.release(sandbox_id)
+        cni = self._cni() if netns else None
+        if cni is None:
+            self.ipam.release(sandbox_id)
+            return
+        try:
+            await cni._exec("DEL", cni.net["plugins"][0], pod, sandbox_id, netns)
+        except NetworkError as e:
+            log.warning("%s", e)
 
 
 class CNIPlugin(NetworkPlugin):
@@ -255,11 +318,12 @@ def result_ip(res):
     return ip4.split("/")[0] if ip4 else None
 
 
-def new_plugin(name, data_dir, cni_conf_dir="/etc/cni/net.d", cni_bin_dir="/opt/cni/bin"):
+def new_plugin(name, data_dir, cni_conf_dir="/etc/cni/net.d", cni_bin_dir="/opt/cni/bin", hairpin_mode="promiscuous-bridge",
+               mtu=1460):
     if name in (None, "", "noop"):
         return NetworkPlugin()
     if name == "kubenet":
-        return KubenetPlugin(data_dir)
+        return KubenetPlugin(data_dir, mtu=mtu or 1460, cni_bin_dirs=cni_bin_dir.split(","), hairpin_mode=hairpin_mode)
     if name == "cni":
         return CNIPlugin(cni_conf_dir, cni_bin_dir.split(","))
     raise ValueError(f"unknown network plugin {name!r}")

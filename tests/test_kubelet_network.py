@@ -266,3 +266,41 @@ async def kl_http_logs(cl, name, previous=False):
         method = "GET"
     r = await kl._http(Req())
     return r.status, r.body
+
+
+def test_kubenet_delegates_to_cni_bridge(run, tmp_path):
+    """kubenet with a netns and CNI binaries: the generated bridge config (hairpin, MTU, host-local
+    over the pod CIDR) then loopback, as in `kubenet_linux.go` setUpPod."""
+    import json as _json
+    import stat
+    import sys as _sys
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    calls = tmp_path / "calls.jsonl"
+    script = ("#!" + _sys.executable + "\nimport json,os,sys\nconf=json.load(sys.stdin)\n"
+              f"open({str(calls)!r},'a').write(json.dumps({{'cmd':os.environ['CNI_COMMAND'],'conf':conf,"
+              "'netns':os.environ['CNI_NETNS']})+'\\n')\n"
+              "if os.environ['CNI_COMMAND']=='ADD' and conf['type']=='bridge':\n"
+              "    print(json.dumps({'ip4':{'ip':'10.244.1.7/24'}}))\n")
+    for name in ("bridge", "host-local", "loopback"):
+        f = bindir / name
+        f.write_text(script)
+        f.chmod(f.stat().st_mode | stat.S_IEXEC)
+
+    async def main():
+        k = net.KubenetPlugin(str(tmp_path / "d"), mtu=9000, cni_bin_dirs=[str(bindir)], hairpin_mode="hairpin-veth")
+        k.set_pod_cidr("10.244.1.0/24")
+        pod = {"metadata": {"name": "p", "namespace": "default"}}
+        assert await k.setup_pod(pod, "sb1", "/var/run/netns/x") == "10.244.1.7"
+        await k.teardown_pod(pod, "sb1", "/var/run/netns/x")
+        recs = [_json.loads(line) for line in calls.read_text().splitlines()]
+        assert [(r["cmd"], r["conf"]["type"]) for r in recs] == [("ADD", "bridge"), ("ADD", "loopback"), ("DEL", "bridge")]
+        b = recs[0]["conf"]
+        assert b["bridge"] == "cbr0" and b["mtu"] == 9000 and b["hairpinMode"] is True and b["isGateway"] is True
+        assert b["ipam"]["subnet"] == "10.244.1.0/24" and b["ipMasq"] is False
+        # no namespace (process runtime): in-process host-local allocation
+        ip = await k.setup_pod(pod, "sb2", "")
+        assert ip.startswith("10.244.1.") and len(calls.read_text().splitlines()) == 3
+        with pytest.raises(ValueError):
+            net.KubenetPlugin(str(tmp_path / "e"), hairpin_mode="bogus")
+    run(main())
