@@ -133,6 +133,10 @@ class AuditLogger:
                             "subresource": sub or None},
               "responseStatus": {"metadata": {}, "code": code},
               "requestReceivedTimestamp": _ts(), "stageTimestamp": _ts()}
+        real = getattr(user, "impersonated_by", None)
+        if real is not None:      # the event's user is who asked; impersonatedUser who it ran as
+            ev["impersonatedUser"] = ev["user"]
+            ev["user"] = {"username": real.name, "groups": list(real.groups or ())}
         if lvl >= 2 and req.body and len(req.body) <= self.max_body:
             try:
                 ev["requestObject"] = json.loads(req.body)

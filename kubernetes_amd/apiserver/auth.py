@@ -15,6 +15,7 @@ class User:
     name: str
     uid: str = ""
     groups: list = field(default_factory=list)
+    impersonated_by: object = field(default=None, repr=False, compare=False)   # the requesting user
 
 
 ANONYMOUS = User("system:anonymous", groups=["system:unauthenticated"])

@@ -60,7 +60,7 @@ def impersonate(headers, user, authorize):
             authorize(user, "impersonate", None, "userextras", key, v, "authentication.k8s.io")
     if name != "system:anonymous" and "system:authenticated" not in new_groups:
         new_groups.append("system:authenticated")
-    out = User(name, "", new_groups)
+    out = User(name, "", new_groups, impersonated_by=user)
     if extras:
         out.extra = extras          # carried for SubjectAccessReview-style consumers
     return out
