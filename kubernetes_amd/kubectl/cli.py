@@ -149,6 +149,58 @@ def _duration_s(v) -> float:
     return float(parse_duration(v))
 
 
+def rollout_status(obj, revision=0):
+    """-> (message, done) for a Deployment, DaemonSet or StatefulSet (`pkg/kubectl/rollout_status.go`
+    DeploymentStatusViewer / DaemonSetStatusViewer / StatefulSetStatusViewer)."""
+    kind, name = obj.get("kind"), obj["metadata"]["name"]
+    spec, st = obj.get("spec") or {}, obj.get("status") or {}
+    gen, observed = obj["metadata"].get("generation", 0), st.get("observedGeneration", 0)
+    if observed < gen:
+        return f"Waiting for {kind.lower()} spec update to be observed...", False
+    if kind == "DaemonSet":
+        if (spec.get("updateStrategy") or {}).get("type", "OnDelete") != "RollingUpdate":
+            return "rollout status is only available for RollingUpdate strategy type", True
+        want, upd, avail = st.get("desiredNumberScheduled", 0), st.get("updatedNumberScheduled", 0), st.get("numberAvailable", 0)
+        if upd < want:
+            return f'Waiting for daemon set "{name}" rollout to finish: {upd} out of {want} new pods have been updated...', False
+        if avail < want:
+            return f'Waiting for daemon set "{name}" rollout to finish: {avail} of {want} updated pods are available...', False
+        return f'daemon set "{name}" successfully rolled out', True
+    if kind == "StatefulSet":
+        us = spec.get("updateStrategy") or {}
+        if us.get("type", "OnDelete") != "RollingUpdate":
+            return "rollout status is only available for RollingUpdate strategy type", True
+        want = spec.get("replicas", 1)
+        if st.get("readyReplicas", 0) < want:
+            return f"Waiting for {want - st.get('readyReplicas', 0)} pods to be ready...", False
+        part = (us.get("rollingUpdate") or {}).get("partition")
+        if part:
+            if st.get("updatedReplicas", 0) < want - part:
+                return (f"Waiting for partitioned roll out to finish: {st.get('updatedReplicas', 0)} out of "
+                        f"{want - part} new pods have been updated..."), False
+            return f"partitioned roll out complete: {st.get('updatedReplicas', 0)} new pods have been updated...", True
+        if st.get("updateRevision") != st.get("currentRevision"):
+            return (f"waiting for statefulset rolling update to complete {st.get('updatedReplicas', 0)} pods at "
+                    f"revision {st.get('updateRevision')}..."), False
+        return f"statefulset rolling update complete {st.get('currentReplicas', want)} pods at revision {st.get('currentRevision')}...", True
+    if revision:
+        cur = int((obj["metadata"].get("annotations") or {}).get("deployment.kubernetes.io/revision") or 0)
+        if cur < revision:
+            return f"Waiting for deployment \"{name}\" to reach revision {revision}...", False
+    for c in st.get("conditions") or ():
+        if c.get("type") == "Progressing" and c.get("reason") == "ProgressDeadlineExceeded":
+            raise SystemExit(f'error: deployment "{name}" exceeded its progress deadline')
+    want = spec.get("replicas", 1)
+    upd, total, avail = st.get("updatedReplicas", 0), st.get("replicas", 0), st.get("availableReplicas", 0)
+    if upd < want:
+        return f'Waiting for rollout to finish: {upd} out of {want} new replicas have been updated...', False
+    if total > upd:
+        return f"Waiting for rollout to finish: {total - upd} old replicas are pending termination...", False
+    if avail < upd:
+        return f"Waiting for rollout to finish: {avail} of {upd} updated replicas are available...", False
+    return f'deployment "{name}" successfully rolled out', True
+
+
 class Kubectl(extra.ExtraCommands):
     def __init__(self, args, out=sys.stdout):
         self.a = args
@@ -1006,18 +1058,20 @@ class Kubectl(extra.ExtraCommands):
         (ri, name), = split_targets(a.targets)
         if a.action == "status":
             t = time.time()
+            last = None
             while True:
                 d = await self.client.get(ri.plural, name, self.ns)
-                st, spec = d.get("status") or {}, d.get("spec") or {}
-                want = spec.get("replicas", 1)
-                if st.get("updatedReplicas") == want and st.get("availableReplicas") == want and st.get("replicas") == want:
-                    self.p(f'deployment "{name}" successfully rolled out')
+                msg, done = rollout_status(d, a.revision)
+                if done:
+                    self.p(msg)
                     return
-                if not a.watch or time.time() - t > a.timeout:
-                    self.p(f"Waiting for rollout to finish: {st.get('updatedReplicas', 0)} of {want} updated replicas are available...")
-                    if not a.watch:
-                        return
-                    raise SystemExit(1)
+                if msg != last:
+                    self.p(msg)
+                    last = msg
+                if not a.watch:
+                    return
+                if time.time() - t > a.timeout:
+                    raise SystemExit(f"error: timed out waiting for the rollout of {ri.kind.lower()} \"{name}\"")
                 await asyncio.sleep(0.2)
         elif a.action in ("history", "undo") and ri.kind in ("DaemonSet", "StatefulSet"):
             from ..controllers.history import revisions_of
@@ -1935,6 +1989,7 @@ def build_parser():
     ro.add_argument("action", choices=["status", "history", "undo", "pause", "resume"])
     ro.add_argument("targets", nargs="+")
     ro.add_argument("--to-revision", type=int, default=0)
+    ro.add_argument("--revision", type=int, default=0, help="status: the revision to wait for; history: show its template")
     ro.add_argument("-w", "--watch", type=lambda s: s.lower() != "false", default=True)
     ro.add_argument("--timeout", type=float, default=300)
     rn = add("run")

@@ -118,3 +118,25 @@ def test_go_template_and_file_outputs(tmp_path):
     jp = tmp_path / "jp"
     jp.write_text("{.items[*].metadata.name}")
     assert render(pods, f"jsonpath-file={jp}", list_obj=lst) == "a b"
+
+
+def test_rollout_status_viewers():
+    """DeploymentStatusViewer / DaemonSetStatusViewer / StatefulSetStatusViewer messages."""
+    from kubernetes_amd.kubectl.cli import rollout_status
+    md = {"name": "x", "generation": 2}
+    d = {"kind": "Deployment", "metadata": md, "spec": {"replicas": 3},
+         "status": {"observedGeneration": 1}}
+    assert rollout_status(d) == ("Waiting for deployment spec update to be observed...", False)
+    d["status"] = {"observedGeneration": 2, "updatedReplicas": 3, "replicas": 4, "availableReplicas": 3}
+    assert rollout_status(d) == ("Waiting for rollout to finish: 1 old replicas are pending termination...", False)
+    d["status"]["replicas"] = 3
+    assert rollout_status(d) == ('deployment "x" successfully rolled out', True)
+    ds = {"kind": "DaemonSet", "metadata": md, "spec": {"updateStrategy": {"type": "RollingUpdate"}},
+          "status": {"observedGeneration": 2, "desiredNumberScheduled": 4, "updatedNumberScheduled": 4, "numberAvailable": 2}}
+    assert rollout_status(ds)[0].endswith("2 of 4 updated pods are available...")
+    ss = {"kind": "StatefulSet", "metadata": md,
+          "spec": {"replicas": 3, "updateStrategy": {"type": "RollingUpdate", "rollingUpdate": {"partition": 1}}},
+          "status": {"observedGeneration": 2, "readyReplicas": 3, "updatedReplicas": 2}}
+    assert rollout_status(ss) == ("partitioned roll out complete: 2 new pods have been updated...", True)
+    ss["spec"]["updateStrategy"] = {"type": "OnDelete"}
+    assert rollout_status(ss)[1] is True and "only available for RollingUpdate" in rollout_status(ss)[0]
