@@ -1077,6 +1077,14 @@ class Kubectl(extra.ExtraCommands):
             from ..controllers.history import revisions_of
             obj = await self.client.get(ri.plural, name, self.ns)
             revs = revisions_of((await self.client.list("controllerrevisions", self.ns))["items"], obj["metadata"]["uid"])
+            if a.action == "history" and a.revision:
+                from .describe import _template
+                r = next((r for r in revs if int(r.get("revision", 0)) == a.revision), None)
+                if r is None:
+                    raise SystemExit(f"error: unable to find the specified revision")
+                self.p(f'{ri.kind.lower()} "{name}" with revision #{a.revision}\nPod Template:')
+                self.p("\n".join(_template(((r.get("data") or {}).get("spec") or {}).get("template") or {})))
+                return
             if a.action == "history":
                 rows = [[int(r.get("revision", 0)), (r["metadata"].get("annotations") or {}).get(
                     "kubernetes.io/change-cause", "<none>")] for r in revs]
@@ -1104,6 +1112,17 @@ class Kubectl(extra.ExtraCommands):
         elif a.action == "history":
             uid = (await self.client.get(ri.plural, name, self.ns))["metadata"]["uid"]
             rss = [r for r in (await self.client.list("replicasets", self.ns))["items"] if (m.controller_of(r) or {}).get("uid") == uid]
+            if a.revision:
+                from .describe import _template
+                r = next((r for r in rss if int((r["metadata"].get("annotations") or {}).get(
+                    "deployment.kubernetes.io/revision", 0)) == a.revision), None)
+                if r is None:
+                    raise SystemExit(f"error: unable to find the specified revision")
+                tpl = json.loads(json.dumps((r.get("spec") or {}).get("template") or {}))
+                ((tpl.get("metadata") or {}).get("labels") or {}).pop("pod-template-hash", None)
+                self.p(f'deployment "{name}" with revision #{a.revision}\nPod Template:')
+                self.p("\n".join(_template(tpl)))
+                return
             rows = sorted([[int((r["metadata"].get("annotations") or {}).get("deployment.kubernetes.io/revision", 0)), "<none>"] for r in rss])
             self.p(printers.table(rows, ["REVISION", "CHANGE-CAUSE"]))
         elif a.action == "undo":

@@ -138,6 +138,8 @@ def test_patch_scale_rollout_pause(cluster, tmp_path):
     assert json.loads(k(cluster, "get", "deployment", "web", "-o", "json")[1])["spec"]["paused"] is True
     assert "already paused" in k(cluster, "rollout", "pause", "deployment/web")[1]
     assert k(cluster, "rollout", "resume", "deployment/web")[1].strip() == 'deployment "web" resumed'
+    rc, out = k(cluster, "rollout", "history", "deployment/web", "--revision", "1")
+    assert rc == 0 and 'deployment "web" with revision #1' in out and "Image:      busybox" in out
     # expose derives the port from the pod template
     rc, out = k(cluster, "expose", "deployment", "web", "--dry-run", "-o", "json")
     svc = json.loads(out)
