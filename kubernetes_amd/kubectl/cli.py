@@ -2158,7 +2158,7 @@ def build_parser():
 
 _TRAILING = {"label": "pairs", "annotate": "pairs", "taint": "taints", "get": "targets", "describe": "targets",
              "delete": "targets", "patch": "targets", "scale": "targets", "expose": "targets", "edit": "targets",
-             "rollout": "targets", "autoscale": "targets", "wait": "targets", "port-forward": "ports"}
+             "rollout": "targets", "autoscale": "targets", "wait": "targets", "port-forward": "ports", "set": "targets"}
 
 GLOBAL_FLAGS = {"-s", "--server", "--token", "--kubeconfig", "--context", "-n", "--namespace", "--as", "--as-group",
                 "--cluster", "--user", "--certificate-authority", "--client-certificate", "--client-key",

@@ -325,8 +325,123 @@ class ExtraCommands:
                     raise
         raise SystemExit("error: too many conflicts")
 
+    async def _set_split(self):
+        """`set` positionals: TYPE/NAME... or TYPE NAME... (or -f / -l / --all), then KEY=VALUE /
+        KEY- pairs (`serviceaccount`: the last word is the account) -> ([(ri, name|obj)], pairs)."""
+        from .cli import read_manifests, ri_for_obj
+        a = self.a
+        toks = list(a.targets)
+        if a.what == "serviceaccount":
+            toks, pairs = toks[:-1], toks[-1:]
+        else:
+            cut = next((i for i, t in enumerate(toks) if "=" in t or (t.endswith("-") and "/" not in t)), len(toks))
+            toks, pairs = toks[:cut], toks[cut:]
+        out = []
+        if a.filename:
+            for d in read_manifests(a.filename, a.recursive):
+                d.setdefault("metadata", {})
+                out.append((ri_for_obj(d), d if a.local else d["metadata"]["name"]))
+        elif toks and "/" in toks[0]:
+            for t in toks:
+                r, _, n = t.partition("/")
+                ri = m.lookup(r)
+                if ri is None:
+                    raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
+                out.append((ri, n))
+        elif toks:
+            ri = m.lookup(toks[0])
+            if ri is None:
+                raise SystemExit(f'error: the server doesn\'t have a resource type "{toks[0]}"')
+            if toks[1:]:
+                out += [(ri, n) for n in toks[1:]]
+            elif a.all or a.label_selector:
+                items = (await self.client.list(ri.plural, self.ns_for(ri), a.label_selector))["items"]
+                out += [(ri, o["metadata"]["name"]) for o in items]
+            else:
+                raise SystemExit("error: resource(s) were provided, but no name, label selector, or --all flag specified")
+        else:
+            raise SystemExit("error: one or more resources must be specified as <resource> <name> or <resource>/<name>")
+        return out, pairs
+
+    async def _set_apply(self, targets, fn, verb):
+        """Run `fn` on each target: --local (files only), --dry-run (fetched, not written) or a
+        conflict-retried update; print `-o` output or `<kind>/<name> <verb>`."""
+        a = self.a
+        for ri, t in targets:
+            if isinstance(t, dict) or a.dry_run:
+                obj = t if isinstance(t, dict) else await self.client.get(ri.plural, t, self.ns_for(ri))
+                obj.setdefault("kind", ri.kind)
+                fn(obj)
+            else:
+                if a.resource_version:
+                    cur = await self.client.get(ri.plural, t, self.ns_for(ri))
+                    if cur["metadata"].get("resourceVersion") != a.resource_version:
+                        raise SystemExit(f"error: Operation cannot be fulfilled on {ri.plural} \"{t}\": "
+                                         f"the object has been modified")
+                ri, obj, _ = await self._mutate(f"{ri.plural}/{t}", fn)
+            if a.output:
+                from . import printers
+                self.p(printers.render([obj], a.output, ri.kind))
+            else:
+                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} {verb}" + (" (dry run)" if a.dry_run else ""))
+
+    async def _set_env(self, targets):
+        """`kubectl set env` (pkg/kubectl/cmd/set/set_env.go): KEY=VAL / -e, KEY- removal,
+        --from=configmap/NAME|secret/NAME (one valueFrom per key, --prefix, --keys), --list,
+        --overwrite=false refuses to change an existing variable."""
+        a = self.a
+        pairs = list(a.pairs) + list(a.env_pairs)
+        sets = {}
+        for p_ in pairs:
+            if "=" in p_:
+                k_, v_ = p_.split("=", 1)
+                sets[k_] = {"name": k_, "value": v_}
+        drops = {p_[:-1] for p_ in pairs if p_.endswith("-") and "=" not in p_}
+        if a.env_from:
+            kind, _, src = a.env_from.partition("/")
+            kind = {"cm": "configmap", "configmaps": "configmap", "secrets": "secret"}.get(kind, kind)
+            if kind not in ("configmap", "secret") or not src:
+                raise SystemExit("error: --from must be configmap/NAME or secret/NAME")
+            o = await self.client.get("configmaps" if kind == "configmap" else "secrets", src, self.ns)
+            keys = [k_ for k_ in sorted((o.get("data") or {})) if not a.keys or k_ in a.keys.split(",")]
+            ref = "configMapKeyRef" if kind == "configmap" else "secretKeyRef"
+            for key in keys:
+                name = (a.prefix + key).upper().replace("-", "_").replace(".", "_")
+                sets[name] = {"name": name, "valueFrom": {ref: {"name": src, "key": key}}}
+        if a.list:
+            for ri, t in targets:
+                obj = t if isinstance(t, dict) else await self.client.get(ri.plural, t, self.ns_for(ri))
+                self.p(f"# {ri.kind} {obj['metadata']['name']}")
+                for c in _containers(_pod_spec(obj), a.containers):
+                    self.p(f"# container {c['name']}")
+                    for e in c.get("env") or ():
+                        if "value" in e:
+                            self.p(f"{e['name']}={e['value']}")
+                        else:
+                            vf = e.get("valueFrom") or {}
+                            r = vf.get("configMapKeyRef") or vf.get("secretKeyRef") or {}
+                            what = "configmap" if "configMapKeyRef" in vf else "secret" if "secretKeyRef" in vf else "field"
+                            self.p(f"# {e['name']} from {what} {r.get('name', '')}, key {r.get('key', '')}")
+            return
+
+        def fn(obj):
+            for c in _containers(_pod_spec(obj), a.containers):
+                cur = {e["name"]: e for e in c.get("env") or ()}
+                if not a.overwrite:
+                    for k_, e in sets.items():
+                        if k_ in cur and cur[k_] != e:
+                            raise SystemExit(f"error: '{k_}' already has a value ({cur[k_].get('value', '')}), and --overwrite is false")
+                env = [e for e in c.get("env") or () if e["name"] not in drops and e["name"] not in sets]
+                env += list(sets.values())
+                c["env"] = env
+        await self._set_apply(targets, fn, "env updated")
+
     async def cmd_set(self):
         a = self.a
+        targets, a.pairs = await self._set_split()
+        if a.what == "env":
+            await self._set_env(targets)
+            return
         if a.what == "image":
             pairs = _kv(a.pairs)
 
@@ -334,14 +449,12 @@ class ExtraCommands:
                 spec = _pod_spec(obj)
                 hit = False
                 for cname, img in pairs.items():
-                    for c in _containers(spec, cname):
+                    for c in _containers(spec, None if cname == "*" else cname):
                         c["image"] = img
                         hit = True
                 if not hit:
                     raise SystemExit(f"error: unable to find container(s) {', '.join(pairs)}")
-            for t in a.targets:
-                ri, obj, _ = await self._mutate(t, fn)
-                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} image updated")
+            await self._set_apply(targets, fn, "image updated")
         elif a.what == "resources":
             def fn(obj):
                 for c in _containers(_pod_spec(obj), a.containers):
@@ -350,29 +463,13 @@ class ExtraCommands:
                         r.setdefault("limits", {}).update(_res_list(a.limits))
                     if a.requests:
                         r.setdefault("requests", {}).update(_res_list(a.requests))
-            for t in a.targets:
-                ri, obj, _ = await self._mutate(t, fn)
-                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} resource requirements updated")
-        elif a.what == "env":
-            sets = {p.split("=", 1)[0]: p.split("=", 1)[1] for p in a.pairs if "=" in p}
-            drops = {p[:-1] for p in a.pairs if p.endswith("-") and "=" not in p}
-
-            def fn(obj):
-                for c in _containers(_pod_spec(obj), a.containers):
-                    env = [e for e in c.get("env") or () if e["name"] not in drops and e["name"] not in sets]
-                    env += [{"name": k, "value": v} for k, v in sets.items()]
-                    c["env"] = env
-            for t in a.targets:
-                ri, obj, _ = await self._mutate(t, fn)
-                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} env updated")
+            await self._set_apply(targets, fn, "resource requirements updated")
         elif a.what == "serviceaccount":
             sa = a.pairs[0]
 
             def fn(obj):
                 _pod_spec(obj)["serviceAccountName"] = sa
-            for t in a.targets:
-                ri, obj, _ = await self._mutate(t, fn)
-                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} serviceaccount updated")
+            await self._set_apply(targets, fn, "serviceaccount updated")
         elif a.what == "selector":
             sel = _kv(a.pairs)
 
@@ -381,18 +478,14 @@ class ExtraCommands:
                     obj["spec"]["selector"] = sel
                 else:
                     obj["spec"]["selector"] = {"matchLabels": sel}
-            for t in a.targets:
-                ri, obj, _ = await self._mutate(t, fn)
-                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} selector updated")
+            await self._set_apply(targets, fn, "selector updated")
         elif a.what == "subject":
             def fn(obj):
                 subs = obj.setdefault("subjects", [])
                 for s in _subjects(a, self.ns):
                     if s not in subs:
                         subs.append(s)
-            for t in a.targets:
-                ri, obj, _ = await self._mutate(t, fn)
-                self.p(f"{ri.kind.lower()}/{obj['metadata']['name']} subjects updated")
+            await self._set_apply(targets, fn, "subjects updated")
 
     # -------------------------------------------------------------------------- rolling-update
     async def _ready(self, rc_name):
@@ -617,8 +710,23 @@ def add_parsers(add):
     ss = s.add_subparsers(dest="what", required=True)
     for what in ("image", "resources", "env", "serviceaccount", "selector", "subject"):
         x = ss.add_parser(what)
-        x.add_argument("targets", nargs=1)
-        x.add_argument("pairs", nargs="*")
+        x.add_argument("targets", nargs="*", help="TYPE/NAME ... or TYPE NAME ..., then KEY=VALUE pairs")
+        x.add_argument("--all", action="store_true")
+        x.add_argument("-l", "--selector", dest="label_selector")
+        x.add_argument("-f", "--filename", action="append")
+        x.add_argument("-R", "--recursive", action="store_true")
+        x.add_argument("--local", action="store_true")
+        x.add_argument("--dry-run", action="store_true")
+        x.add_argument("-o", "--output", default="")
+        x.add_argument("--record", action="store_true")
+        x.add_argument("--resource-version", default="")
+        if what == "env":
+            x.add_argument("-e", "--env", dest="env_pairs", action="append", default=[])
+            x.add_argument("--list", action="store_true")
+            x.add_argument("--from", dest="env_from", default="")
+            x.add_argument("--prefix", default="")
+            x.add_argument("--keys", default="")
+            x.add_argument("--overwrite", type=lambda v: v.lower() != "false", default=True)
         x.add_argument("-c", "--containers", default=None)
         x.add_argument("--limits", default="")
         x.add_argument("--requests", default="")

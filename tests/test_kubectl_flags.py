@@ -322,3 +322,34 @@ def test_apply_last_applied_and_can_i(cluster, tmp_path):
     assert rc == 0 and out.strip() == "yes"
     rc, out = k(cluster, "auth", "can-i", "get", "/healthz", "-q")
     assert rc == 0 and out == ""
+
+
+def test_set_flags(cluster, tmp_path):
+    """`kubectl set` (pkg/kubectl/cmd/set): TYPE NAME form, -l, --local -f, --dry-run -o, image
+    `*=`, env -e / --from / --list / --overwrite=false."""
+    dep = {"apiVersion": "apps/v1beta1", "kind": "Deployment", "metadata": {"name": "setd", "labels": {"grp": "set"}},
+           "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "setd"}},
+                    "template": {"metadata": {"labels": {"app": "setd"}},
+                                 "spec": {"containers": [{"name": "a", "image": "busybox"},
+                                                         {"name": "b", "image": "busybox"}]}}}}
+    f = _create(cluster, tmp_path, dep)
+    rc, out = k(cluster, "set", "image", "deployments", "-l", "grp=set", "*=img:2")
+    assert rc == 0 and "deployment/setd image updated" in out
+    d = json.loads(k(cluster, "get", "deploy", "setd", "-o", "json")[1])
+    assert [c["image"] for c in d["spec"]["template"]["spec"]["containers"]] == ["img:2", "img:2"]
+    rc, out = k(cluster, "set", "image", "--local", "-f", str(f), "a=local:1", "-o", "json")
+    assert json.loads(out)["spec"]["template"]["spec"]["containers"][0]["image"] == "local:1"
+    rc, out = k(cluster, "set", "resources", "deployment", "setd", "--limits", "cpu=2", "--dry-run", "-o", "yaml")
+    assert yaml.safe_load(out)["spec"]["template"]["spec"]["containers"][0]["resources"]["limits"]["cpu"] == "2"
+    d = json.loads(k(cluster, "get", "deploy", "setd", "-o", "json")[1])
+    assert "resources" not in d["spec"]["template"]["spec"]["containers"][0]            # dry run wrote nothing
+    cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "envsrc"}, "data": {"db-host": "x", "port": "1"}}
+    _create(cluster, tmp_path, cm)
+    assert k(cluster, "set", "env", "deployment/setd", "-e", "MODE=fast", "--from", "configmap/envsrc", "--prefix",
+             "app_")[0] == 0
+    rc, out = k(cluster, "set", "env", "deployment/setd", "--list", "-c", "a")
+    assert "MODE=fast" in out and "# APP_DB_HOST from configmap envsrc, key db-host" in out
+    with pytest.raises(SystemExit, match="--overwrite is false"):
+        k(cluster, "set", "env", "deployment/setd", "MODE=slow", "--overwrite=false")
+    assert k(cluster, "set", "env", "deployment/setd", "MODE-")[0] == 0
+    assert "MODE=" not in k(cluster, "set", "env", "deployment/setd", "--list")[1]
