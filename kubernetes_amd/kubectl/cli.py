@@ -1681,29 +1681,61 @@ class Kubectl(extra.ExtraCommands):
                 srv.close()
 
     async def cmd_cp(self):
-        """`kubectl cp` over exec: pod->local streams `cat`; local->pod ships the file base64-encoded
-        in the exec command (files up to 1 MiB; the reference pipes a tar stream over stdin)."""
+        """`kubectl cp` (pkg/kubectl/cmd/cp.go): a tar stream over exec — local->pod feeds
+        `tar xf - -C DIR` on stdin, pod->local reads `tar cf - PATH`; files and directories, with
+        the source's base name re-rooted at the destination. Entries that would escape the
+        destination are refused."""
+        import io as _io
+        import posixpath
+        import tarfile
         a = self.a
         src, dst = a.src, a.dst
         if ":" in src and not os.path.exists(src):
             pod, path = src.split(":", 1)
-            rc, out, err = await self._exec(pod.split("/")[-1], a.container, ["cat", path])
+            ns = self.ns
+            if "/" in pod:
+                ns, pod = pod.split("/", 1)
+            saved, self.ns = self.ns, ns
+            try:
+                rc, out, err = await self._exec(pod, a.container, ["tar", "cf", "-", "-C", posixpath.dirname(path) or "/",
+                                                                   posixpath.basename(path.rstrip("/")) or "."])
+            finally:
+                self.ns = saved
             if rc != 0:
-                raise SystemExit(f"error: {err.decode() or out.decode()}")
-            with open(dst, "wb") as f:
-                f.write(out)
+                raise SystemExit(f"error: {err.decode(errors='replace') or out.decode(errors='replace')}")
+            base = posixpath.basename(path.rstrip("/"))
+            dest_root = os.path.abspath(dst)
+            with tarfile.open(fileobj=_io.BytesIO(out), mode="r:") as tf:
+                for mem in tf.getmembers():
+                    rel = mem.name[len(base):].lstrip("/") if mem.name == base or mem.name.startswith(base + "/") else mem.name
+                    target = os.path.abspath(os.path.join(dest_root, rel)) if rel else dest_root
+                    if target != dest_root and not target.startswith(dest_root + os.sep):
+                        raise SystemExit(f"error: refusing to write outside {dst}: {mem.name}")
+                    if mem.isdir():
+                        os.makedirs(target, exist_ok=True)
+                    elif mem.isfile():
+                        os.makedirs(os.path.dirname(target) or ".", exist_ok=True)
+                        with open(target, "wb") as f:
+                            f.write(tf.extractfile(mem).read())
+                        os.chmod(target, mem.mode & 0o777)
             return
         pod, path = dst.split(":", 1)
-        with open(src, "rb") as f:
-            data = f.read()
-        if len(data) > 1 << 20:
-            raise SystemExit("error: kubectl cp into a pod supports files up to 1 MiB")
-        import base64
-        b64 = base64.b64encode(data).decode()
-        rc, out, err = await self._exec(pod.split("/")[-1], a.container,
-                                        ["sh", "-c", f"printf %s '{b64}' | base64 -d > '{path}'"])
+        ns = self.ns
+        if "/" in pod:
+            ns, pod = pod.split("/", 1)
+        if not os.path.exists(src):
+            raise SystemExit(f"error: {src} doesn't exist in local filesystem")
+        buf = _io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w:") as tf:
+            tf.add(src, arcname=posixpath.basename(path.rstrip("/")) or os.path.basename(src))
+        dest_dir = posixpath.dirname(path.rstrip("/")) or "/"
+        saved, self.ns = self.ns, ns
+        try:
+            rc, out, err = await self._exec(pod, a.container, ["tar", "xf", "-", "-C", dest_dir], stdin_data=buf.getvalue())
+        finally:
+            self.ns = saved
         if rc != 0:
-            raise SystemExit(f"error: {err.decode() or out.decode()}")
+            raise SystemExit(f"error: {err.decode(errors='replace') or out.decode(errors='replace')}")
 
     async def cmd_proxy(self):
         """`kubectl proxy`: a local HTTP endpoint forwarding to the API server with this

@@ -98,6 +98,21 @@ def test_exec_portforward_cp_inprocess(run, tmp_path):
             await k.cmd_cp()
             await k.client.close()
             assert (tmp_path / "back.bin").read_bytes() == src.read_bytes()
+            # directories and files past the old 1 MiB limit travel as tar streams
+            tree = tmp_path / "tree"
+            (tree / "sub").mkdir(parents=True)
+            big = os.urandom(3 << 20)
+            (tree / "sub" / "big.bin").write_bytes(big)
+            (tree / "a.txt").write_text("A")
+            k, _ = kubectl(cl.url, "cp", str(tree), f"srv:{tmp_path}/pod-tree")
+            await k.cmd_cp()
+            await k.client.close()
+            assert (tmp_path / "pod-tree" / "sub" / "big.bin").read_bytes() == big
+            k, _ = kubectl(cl.url, "cp", f"default/srv:{tmp_path}/pod-tree", str(tmp_path / "tree-back"))
+            await k.cmd_cp()
+            await k.client.close()
+            assert (tmp_path / "tree-back" / "a.txt").read_text() == "A"
+            assert (tmp_path / "tree-back" / "sub" / "big.bin").read_bytes() == big
             # attach streams what the running container writes from now on
             k, out = kubectl(cl.url, "attach", "srv")
             task = asyncio.ensure_future(k.cmd_attach())
