@@ -70,6 +70,7 @@ def _create_parser():
     g.add_argument("--from-literal", action="append", default=[])
     g.add_argument("--from-file", action="append", default=[])
     g.add_argument("--type", default="Opaque")
+    g.add_argument("--from-env-file")
     t = ss.add_parser("tls")
     t.add_argument("name")
     t.add_argument("--cert", required=True)
@@ -132,6 +133,26 @@ def _create_parser():
     return ap
 
 
+def _env_file(path):
+    """`--from-env-file` (`pkg/kubectl/cmd/util/env_file.go`): KEY=VALUE lines, `#` comments
+    and blank lines skipped, a bare KEY takes its value from the environment, keys must be
+    valid environment variable names."""
+    import re as _re
+    out = {}
+    if not path:
+        return out
+    with open(path) as f:
+        for n, line in enumerate(f, 1):
+            line = line.lstrip()
+            if not line.strip() or line.startswith("#"):
+                continue
+            kk, eq, vv = line.rstrip("\n").partition("=")
+            if not _re.fullmatch(r"[-._a-zA-Z][-._a-zA-Z0-9]*", kk):
+                raise SystemExit(f"error: {kk!r} at line {n} of {path} is not a valid key name")
+            out[kk] = vv if eq else os.environ.get(kk, "")
+    return out
+
+
 def _b64(v):
     return base64.b64encode(v if isinstance(v, bytes) else v.encode()).decode()
 
@@ -179,12 +200,7 @@ def generate(argv, ns):
                 data[key] = v.decode()
             except UnicodeDecodeError:
                 binary[key] = _b64(v)
-        if a.from_env_file:
-            for line in open(a.from_env_file):
-                line = line.strip()
-                if line and not line.startswith("#"):
-                    kk, _, vv = line.partition("=")
-                    data[kk] = vv
+        data.update(_env_file(a.from_env_file))
         o = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": md, "data": data}
         if binary:
             o["binaryData"] = binary
@@ -193,6 +209,7 @@ def generate(argv, ns):
         if a.secret_type == "generic":
             data = {kk: _b64(v) for kk, v in _kv(a.from_literal).items()}
             data.update({kk: _b64(v) for kk, v in _from_files(a.from_file).items()})
+            data.update({kk: _b64(v) for kk, v in _env_file(a.from_env_file).items()})
             return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": a.type, "data": data}
         if a.secret_type == "tls":
             return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": "kubernetes.io/tls",

@@ -140,3 +140,14 @@ def test_rollout_status_viewers():
     assert rollout_status(ss) == ("partitioned roll out complete: 2 new pods have been updated...", True)
     ss["spec"]["updateStrategy"] = {"type": "OnDelete"}
     assert rollout_status(ss)[1] is True and "only available for RollingUpdate" in rollout_status(ss)[0]
+
+
+def test_env_file_parsing(tmp_path, monkeypatch):
+    from kubernetes_amd.kubectl.extra import _env_file
+    f = tmp_path / "e.env"
+    f.write_text("# comment\n\nA=1\n  B=two words \nFROM_ENV\nC=x=y\n")
+    monkeypatch.setenv("FROM_ENV", "inherited")
+    assert _env_file(str(f)) == {"A": "1", "B": "two words ", "FROM_ENV": "inherited", "C": "x=y"}
+    f.write_text("1bad key=v\n")
+    with pytest.raises(SystemExit, match="not a valid key name"):
+        _env_file(str(f))
