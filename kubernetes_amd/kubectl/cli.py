@@ -1643,7 +1643,8 @@ class Kubectl(extra.ExtraCommands):
     async def cmd_attach(self):
         """`kubectl attach`: the container's output from now on, until it exits (with -i, stdin)."""
         a = self.a
-        self.rc = await self._interactive(a.pod, "attach", a.container, (), a.stdin, a.tty)
+        pod = (await self._pods_for(a.pod))[0] if "/" in a.pod else a.pod    # TYPE/NAME: its first pod
+        self.rc = await self._interactive(pod, "attach", a.container, (), a.stdin, a.tty)
 
     async def cmd_port_forward(self):
         """`kubectl port-forward POD [LOCAL:]REMOTE ...` (`pkg/kubectl/cmd/portforward.go`): one
