@@ -864,11 +864,31 @@ class Kubectl(extra.ExtraCommands):
         await self.client.patch("nodes", name, {"spec": {"unschedulable": flag or None}})
         self.p(f"node/{name} {'cordoned' if flag else 'uncordoned'}")
 
+    async def _cordon_all(self, flag):
+        """cordon / uncordon NODE, or every node matching -l; --dry-run only reports; a node
+        already in the wanted state is reported as such (`drain.go` RunCordonOrUncordon)."""
+        a = self.a
+        if a.selector:
+            nodes = (await self.client.list("nodes", None, a.selector))["items"]
+        elif a.node:
+            nodes = [await self.client.get("nodes", a.node)]
+        else:
+            raise SystemExit("error: USAGE: cordon NODE [flags] (or -l SELECTOR)")
+        word = "cordoned" if flag else "uncordoned"
+        for n in nodes:
+            name = n["metadata"]["name"]
+            if bool((n.get("spec") or {}).get("unschedulable")) == flag:
+                self.p(f"node/{name} already {word}")
+            elif a.dry_run:
+                self.p(f"node/{name} {word} (dry run)")
+            else:
+                await self._cordon(name, flag)
+
     async def cmd_cordon(self):
-        await self._cordon(self.a.node, True)
+        await self._cordon_all(True)
 
     async def cmd_uncordon(self):
-        await self._cordon(self.a.node, False)
+        await self._cordon_all(False)
 
     async def cmd_drain(self):
         """`kubectl drain` (pkg/kubectl/cmd/drain.go): cordon, then evict every pod except mirror
@@ -2011,7 +2031,10 @@ def build_parser():
     sc.add_argument("--record", action="store_true")
     _common(sc)
     for name in ("cordon", "uncordon"):
-        add(name).add_argument("node")
+        co = add(name)
+        co.add_argument("node", nargs="?")
+        co.add_argument("-l", "--selector")
+        co.add_argument("--dry-run", action="store_true")
     dr = add("drain")
     dr.add_argument("node", nargs="?")
     dr.add_argument("--ignore-daemonsets", action="store_true")

@@ -163,6 +163,9 @@ def test_taint_flags(cluster):
     with pytest.raises(SystemExit, match="invalid taint effect"):
         k(cluster, "taint", "nodes", "node-1", "a=b:Sometimes")
     assert k(cluster, "taint", "nodes", "node-1", "gpu:NoSchedule-")[0] == 0
+    assert "node/node-1 cordoned (dry run)" in k(cluster, "cordon", "node-1", "--dry-run")[1]
+    assert not json.loads(k(cluster, "get", "node", "node-1", "-o", "json")[1])["spec"].get("unschedulable")
+    assert "already uncordoned" in k(cluster, "uncordon", "node-1")[1]
     n = json.loads(k(cluster, "get", "node", "node-1", "-o", "json")[1])
     assert not [t for t in (n["spec"].get("taints") or ()) if t["key"] == "gpu"]
 
