@@ -205,6 +205,7 @@ class Dist:
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.torch = None
         self.cuda = False
+        self.backend = None
 
     def init(self):
         import torch
@@ -216,7 +217,8 @@ class Dist:
             torch.cuda.set_device(self.local_rank)
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("nccl" if self.cuda else "gloo")
+            self.backend = "nccl" if self.cuda else "gloo"   # "nccl" is RCCL on ROCm
+            dist.init_process_group(self.backend)
             self.dist = dist
 
     def broadcast(self, obj):
@@ -408,9 +410,34 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     return allstats
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Run this script as `n` ranks under torch.distributed.run in a child process; its rank 0
+    prints the JSON line to our stdout (inherited). Returns the launcher's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log("bench.py: launching", " ".join(cmd[1:]))
+    p = subprocess.Popen(cmd, env=env)
+    try:
+        return p.wait()
+    except KeyboardInterrupt:
+        p.terminate()
+        return p.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks = GPUs (default: WORLD_SIZE, else 1); without a launcher N > 1 starts "
+                         "torch.distributed.run as a child process")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     # 100 hollow nodes x 8 GPUs per rank (scheduler_perf's 100-node cluster): 800 single-GPU pods
@@ -441,6 +468,26 @@ def main():
     ap.add_argument("--hollow-procs", type=int, default=0,
                     help="hollow-node processes per rank (0 = auto from the CPU budget; 1 = in the rank process)")
     args = ap.parse_args()
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus is None:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if not launched and args.gpus > 1:
+        # --gpus is authoritative: without a launcher, start one rank per GPU under
+        # torch.distributed.run as a CHILD process (nothing here has touched the GPU yet, and an
+        # exec after GPU init is not allowed on the pool), relay its output, exit with its code
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        log(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        sys.exit(2)
+    if not os.environ.get("KAMD_BENCH_FORCE_CPU"):
+        import torch   # device_count() does not initialise HIP on this image
+        ndev = torch.cuda.device_count()
+        if ndev and ndev < world:
+            log(f"bench.py: {world} ranks need {world} GPUs, only {ndev} visible")
+            sys.exit(2)
     d = Dist()
     tmp = tempfile.mkdtemp(prefix="kamd-bench-")
     procs = []
@@ -481,7 +528,9 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "pods/s", "n_gpus": n, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": round(value / BASELINE_DENSITY_PODS_PER_S, 2), "dtype": "bf16",
+        "scaling": "weak", "vs_baseline": round(value / BASELINE_DENSITY_PODS_PER_S, 2),
+        # an orchestrator has no compute dtype; the only GPU arithmetic is the fp32 vector_add payload
+        "dtype": "fp32",
         "data": "synthetic GPU-requesting pods, stub containers (HIP vector_add payload on the rank's MI355X)"
         if any(s["payload_runs"] for s in allstats) else "synthetic GPU-requesting pods, stub containers",
         "config": {"model": "kubemark-density/8xMI355X-hollow-nodes/1-GPU-pods", "global_batch": pods // args.steps,
@@ -489,7 +538,11 @@ def main():
                    "gpus_per_node": args.gpus_per_node, "xgmi_hives_per_node": args.hives,
                    "advertised_gpus": n * args.nodes_per_rank * args.gpus_per_node,
                    "gpus_per_pod": args.gpus_per_pod, "apiserver_workers": d.broadcast_done_workers,
-                   "scheduler_shards": d.shards, "hollow_procs_per_rank": args.hollow_procs},
+                   "scheduler_shards": d.shards, "hollow_procs_per_rank": args.hollow_procs,
+                   "world_size": n, "backend": d.backend,
+                   "topology": f"synthetic fake-AMD-SMI fixture: {args.hives} xGMI hive(s) x "
+                               f"{args.gpus_per_node // max(1, args.hives)} GPUs per hollow node"
+                               + (" (a real 8xMI355X node is one fully connected 8-GPU hive)" if args.hives > 1 else "")},
         "p50_startup_ms": round(pct(lat, 0.50) * 1000, 2), "p90_startup_ms": round(pct(lat, 0.90) * 1000, 2),
         "p99_startup_ms": round(pct(lat, 0.99) * 1000, 2),
         "to_running_s_per_step": [round(max(s["to_running"][k] for s in allstats), 4) for k in range(args.steps)],

@@ -51,6 +51,30 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 32                 # weak scaling: 2 ranks x 2 nodes x 8 GPUs
 
 
+def test_bench_gpus_flag_launches_ranks_without_a_launcher():
+    """--gpus N is authoritative: `python bench.py --gpus 2` (no torch.distributed.run) starts
+    the two ranks itself as a child launcher and reports n_gpus 2."""
+    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--nodes-per-rank", "2", "--xgmi4-steps", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    _check(d, 2, 2, 1)
+    assert d["config"]["parallelism"] == "ranks2" and d["config"]["world_size"] == 2
+    assert d["config"]["backend"] == "gloo" and d["dtype"] == "fp32"
+    assert "synthetic" in d["config"]["topology"]
+
+
+def test_bench_gpus_mismatch_fails():
+    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1", WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]
+
+
 def test_bench_eight_ranks_whole_node_shape():
     """The N=8 path the driver runs on a whole MI355X node, rehearsed with gloo on CPU: 8 ranks
     under torch.distributed.run with the >= 64-CPU control-plane shape (KAMD_BENCH_CPUS=128:
