@@ -483,15 +483,50 @@ def _decode_special(t, v):
     raise ProtobufError(f"unsupported special type {t}")
 
 
-def _decode_value(t, wt, v):
+def _decode_value(t, wt, v, depth=0):
     if t in SPECIAL:
-        return _decode_special(t, v)
+        try:
+            return _decode_special(t, v)
+        except (TypeError, ValueError, UnicodeDecodeError) as e:
+            if isinstance(e, ProtobufError):
+                raise
+            raise ProtobufError(f"malformed {t.rsplit('.', 1)[-1]}: {e}") from None
     if "." in t:
-        return decode_message(t, v)
-    return _decode_scalar(t, wt, v)
+        return decode_message(t, v, None, depth + 1)
+    try:
+        return _decode_scalar(t, wt, v)
+    except UnicodeDecodeError as e:
+        raise ProtobufError(f"invalid UTF-8 in a string field: {e}") from None
 
 
-def decode_message(msg: str, buf, out=None) -> dict:
+MAX_DEPTH = 100    # nesting bound for untrusted input (recursive JSONSchemaProps, ...)
+
+
+def _wire_of(t):
+    return 0 if t in VARINT_TYPES else (1 if t == "double" else 2)
+
+
+def _packed(t, wt, v):
+    """A packed run of repeated varint / double scalars."""
+    out, i = [], 0
+    while i < len(v):
+        if wt == 0:
+            x, i = _read_varint(v, i)
+        else:
+            x = v[i:i + 8]
+            if len(x) != 8:
+                raise ProtobufError("truncated packed field")
+            i += 8
+        out.append(_decode_scalar(t, wt, x))
+    return out
+
+
+def decode_message(msg: str, buf, out=None, _depth=0) -> dict:
+    """Decode one message. Every occurrence's wire type must match its field's type (a repeated
+    varint/double field may also be packed): corrupt or hostile input raises ProtobufError, never
+    a TypeError deeper down. Nesting is bounded by MAX_DEPTH."""
+    if _depth > MAX_DEPTH:
+        raise ProtobufError("protobuf nesting too deep")
     s = schema()
     byn = s.by_num.get(msg)
     if byn is None:
@@ -501,14 +536,22 @@ def decode_message(msg: str, buf, out=None) -> dict:
         f = byn.get(num)
         if f is None:
             continue  # unknown field: skipped (forward compatible, as gogo-protobuf)
+        if wt != f.wt and not (f.label == "rep" and wt == 2 and f.wt != 2):
+            raise ProtobufError(f"wire type {wt} does not match the field's type", f.json)
         if f.inline:
-            decode_message(f.type, v, out)
+            decode_message(f.type, v, out, _depth + 1)
         elif f.label == "rep":
-            out.setdefault(f.json, []).append(_decode_value(f.type, wt, v))
+            if wt == 2 and f.wt != 2:
+                out.setdefault(f.json, []).extend(_packed(f.type, f.wt, v))
+            else:
+                out.setdefault(f.json, []).append(_decode_value(f.type, wt, v, _depth))
         elif f.label == "map":
             k = val = None
-            vwt = 2
+            kwt, ewt = _wire_of(f.key), (2 if "." in f.type else _wire_of(f.type))
+            vwt = ewt
             for n2, w2, x in _fields(v):
+                if (n2 == 1 and w2 != kwt) or (n2 == 2 and w2 != ewt):
+                    raise ProtobufError("map entry: wrong wire type", f.json)
                 if n2 == 1:
                     k = _decode_scalar(f.key, w2, x)
                 elif n2 == 2:
@@ -517,10 +560,10 @@ def decode_message(msg: str, buf, out=None) -> dict:
                 k = str(k)
             m = out.setdefault(f.json, {})
             if val is None:
-                val = b"" if vwt == 2 else 0
-            m[k if k is not None else ""] = _decode_value(f.type, vwt, val)
+                val = b"" if vwt == 2 else (bytes(8) if vwt == 1 else 0)
+            m[k if k is not None else ""] = _decode_value(f.type, vwt, val, _depth)
         else:
-            out[f.json] = _decode_value(f.type, wt, v)
+            out[f.json] = _decode_value(f.type, wt, v, _depth)
     return out
 
 

@@ -4,10 +4,12 @@ Parity: `staging/src/k8s.io/apiserver/pkg/endpoints/filters/impersonation.go` Wi
 Every impersonated attribute is authorized for the requesting user with verb `impersonate`:
 users (`users`, core group), groups (`groups`), service accounts (`serviceaccounts` in the
 account's namespace, when the user name is `system:serviceaccount:<ns>:<name>`) and extra
-values (`userextras/<key>` in authentication.k8s.io). The request then runs as the new user:
-a service account gains `system:serviceaccounts` and `system:serviceaccounts:<ns>`, and every
-impersonated user except `system:anonymous` is in `system:authenticated`. Group or extra
-headers without Impersonate-User are rejected.
+values (`userextras/<key>` in authentication.k8s.io). The request then runs as the new user.
+When Impersonate-Group headers are sent they are the COMPLETE group list (each one authorized
+above); only when none are sent does a service account gain `system:serviceaccounts` and
+`system:serviceaccounts:<ns>` and every impersonated user except `system:anonymous` join
+`system:authenticated` (`impersonation.go:66-124`, `groupsSpecified`). Group or extra headers
+without Impersonate-User are rejected.
 """
 from __future__ import annotations
 
@@ -44,13 +46,15 @@ def impersonate(headers, user, authorize):
         if groups or extras:
             raise ImpersonationError(400, "requested impersonation of groups or extra fields without a user")
         return user
+    groups_specified = bool(groups)
+    new_groups = []
     if name.startswith(SA_PREFIX) and name.count(":") == 3:
         _, _, ns, sa = name.split(":")
         authorize(user, "impersonate", ns, "serviceaccounts", "", sa, "")
-        new_groups = ["system:serviceaccounts", f"system:serviceaccounts:{ns}"]
+        if not groups_specified:
+            new_groups = ["system:serviceaccounts", f"system:serviceaccounts:{ns}"]
     else:
         authorize(user, "impersonate", None, "users", "", name, "")
-        new_groups = []
     for g in groups:
         authorize(user, "impersonate", None, "groups", "", g, "")
         if g not in new_groups:
@@ -58,7 +62,7 @@ def impersonate(headers, user, authorize):
     for key, vals in extras.items():
         for v in vals:
             authorize(user, "impersonate", None, "userextras", key, v, "authentication.k8s.io")
-    if name != "system:anonymous" and "system:authenticated" not in new_groups:
+    if not groups_specified and name != "system:anonymous" and "system:authenticated" not in new_groups:
         new_groups.append("system:authenticated")
     out = User(name, "", new_groups, impersonated_by=user)
     if extras:

@@ -519,10 +519,15 @@ struct Decoder {
   const Schema& s;
   CodecObject* self;
   std::string err;
+  int depth = 0;
 
   PyObject* str(const uint8_t* p, size_t n) { return PyUnicode_DecodeUTF8((const char*)p, (Py_ssize_t)n, "replace"); }
 
   PyObject* value(const Field& f, uint8_t wt, uint64_t v, const uint8_t* p, size_t n) {
+    if (wt != (f.type == pbc::S_MSG ? 2 : pbc::wire_of(f.type))) {
+      err = "wire type " + std::to_string(wt) + " does not match the field's type";
+      return nullptr;
+    }
     switch (f.type) {
       case pbc::S_STRING: return str(p, n);
       case pbc::S_BYTES: { std::string b; pbc::base64(b, p, n); return PyUnicode_FromStringAndSize(b.data(), (Py_ssize_t)b.size()); }
@@ -533,7 +538,6 @@ struct Decoder {
       case pbc::S_DOUBLE: { double d = 0; if (n == 8) memcpy(&d, p, 8); return PyFloat_FromDouble(d); }
       case pbc::S_MSG: break;
     }
-    (void)wt;
     if (f.sp == pbc::SP_NONE) {
       PyObject* d = PyDict_New();
       if (!message(f.msg, p, n, d)) { Py_DECREF(d); return nullptr; }
@@ -543,6 +547,8 @@ struct Decoder {
   }
 
   PyObject* special(pbc::Special sp, const uint8_t* p, size_t n) {
+    pbc::DepthGuard g(depth);
+    if (!g.ok) { err = "protobuf nesting too deep"; return nullptr; }
     // the JSON writer renders special types exactly as api/protobuf.py; reuse it, then parse the
     // (tiny) JSON text for the container-typed ones
     pbc::Reader r{p, p + n};
@@ -669,7 +675,30 @@ struct Decoder {
     }
   }
 
+  // a packed run of repeated varint / double scalars
+  bool packed(const Field& f, const uint8_t* q, size_t l, PyObject* lst) {
+    pbc::Reader pr{q, q + l};
+    while (!pr.done()) {
+      uint64_t x = 0;
+      const uint8_t* xp = (const uint8_t*)"";
+      size_t xn = 0;
+      if (f.wt == 0) {
+        if (!pr.varint(&x)) { err = "truncated packed field"; return false; }
+      } else {
+        if (pr.e - pr.p < 8) { err = "truncated packed field"; return false; }
+        xp = pr.p; xn = 8; pr.p += 8;
+      }
+      PyObject* o = value(f, f.wt, x, xp, xn);
+      if (!o) return false;
+      PyList_Append(lst, o);
+      Py_DECREF(o);
+    }
+    return true;
+  }
+
   bool message(int mi, const uint8_t* p, size_t n, PyObject* out) {
+    pbc::DepthGuard g(depth);
+    if (!g.ok) { err = "protobuf nesting too deep"; return false; }
     const Message& m = s.msgs[mi];
     pbc::Reader r{p, p + n};
     uint32_t num; uint8_t wt; uint64_t v; const uint8_t* q; size_t l;
@@ -677,6 +706,10 @@ struct Decoder {
       if (!r.next(&num, &wt, &v, &q, &l)) { err = "truncated protobuf"; return false; }
       if (num >= m.by_num.size() || m.by_num[num] < 0) continue;
       const Field& f = m.fields[m.by_num[num]];
+      if (!pbc::wire_ok(f, wt)) {
+        err = "field " + f.json + ": wire type " + std::to_string(wt) + " does not match its type";
+        return false;
+      }
       if (f.inl) {
         if (!message(f.msg, q, l, out)) return false;
         continue;
@@ -689,10 +722,14 @@ struct Decoder {
           PyDict_SetItem(out, key, lst);
           Py_DECREF(lst);
         }
-        PyObject* x = value(f, wt, v, q, l);
-        if (!x) { Py_DECREF(key); return false; }
-        PyList_Append(lst, x);
-        Py_DECREF(x);
+        if (wt == 2 && f.wt != 2) {
+          if (!packed(f, q, l, lst)) { Py_DECREF(key); return false; }
+        } else {
+          PyObject* x = value(f, wt, v, q, l);
+          if (!x) { Py_DECREF(key); return false; }
+          PyList_Append(lst, x);
+          Py_DECREF(x);
+        }
       } else if (f.label == pbc::L_MAP) {
         PyObject* d = PyDict_GetItem(out, key);
         if (!d) {
@@ -702,13 +739,17 @@ struct Decoder {
         }
         pbc::Reader e{q, q + l};
         PyObject* mk = nullptr;
-        uint8_t vwt = 2;
+        const uint8_t kwt = pbc::wire_of(f.key), ewt = f.type == pbc::S_MSG ? 2 : pbc::wire_of(f.type);
+        uint8_t vwt = ewt;
         uint64_t vv = 0;
         const uint8_t* vp = (const uint8_t*)"";
         size_t vl = 0;
         uint32_t n2; uint8_t w2; uint64_t v2; const uint8_t* q2; size_t l2;
         while (!e.done()) {
           if (!e.next(&n2, &w2, &v2, &q2, &l2)) { Py_XDECREF(mk); Py_DECREF(key); err = "truncated map entry"; return false; }
+          if ((n2 == 1 && w2 != kwt) || (n2 == 2 && w2 != ewt)) {
+            Py_XDECREF(mk); Py_DECREF(key); err = "map entry " + f.json + ": wrong wire type"; return false;
+          }
           if (n2 == 1) {
             Py_XDECREF(mk);
             if (w2 == 2) mk = str(q2, l2);

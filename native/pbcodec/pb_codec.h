@@ -318,6 +318,11 @@ struct Reader {
   }
   // next field: number, wire type, varint value or [ptr, len)
   bool next(uint32_t* num, uint8_t* wt, uint64_t* v, const uint8_t** ptr, size_t* len) {
+    // every output is defined whatever the wire type: a caller that reads [ptr, len) of a varint
+    // field, or v of a length-delimited one, sees an empty value, never stale stack memory
+    *v = 0;
+    *ptr = (const uint8_t*)"";
+    *len = 0;
     uint64_t k;
     if (!varint(&k)) return false;
     *num = (uint32_t)(k >> 3);
@@ -339,6 +344,27 @@ struct Reader {
     return ok = false;
   }
   bool done() const { return p >= e; }
+};
+
+// wire type a scalar (or message) value is encoded with
+inline uint8_t wire_of(Scalar t) {
+  return (t == S_BOOL || t == S_INT32 || t == S_INT64 || t == S_UINT32 || t == S_UINT64) ? 0 : (t == S_DOUBLE ? 1 : 2);
+}
+
+// does an occurrence with wire type `wt` fit field f? A repeated varint/double field may also
+// arrive packed (one length-delimited run of values).
+inline bool wire_ok(const Field& f, uint8_t wt) {
+  if (wt == f.wt) return true;
+  return f.label == L_REP && wt == 2 && f.wt != 2;
+}
+
+// nesting bound for untrusted input (recursive message types: JSONSchemaProps, ...)
+constexpr int kMaxDepth = 100;
+struct DepthGuard {
+  int& d;
+  bool ok;
+  explicit DepthGuard(int& depth) : d(depth), ok(++depth <= kMaxDepth) {}
+  ~DepthGuard() { --d; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -470,6 +496,8 @@ class JsonWriter {
 
   // body of message mi as a JSON object; inject_rv (non-null) replaces metadata.resourceVersion
   bool message(int mi, const uint8_t* p, size_t n, std::string& out, const char* inject_rv = nullptr) {
+    DepthGuard g(depth_);
+    if (!g.ok) return false;
     out += '{';
     bool first = true;
     if (!members(mi, p, n, out, first, inject_rv)) return false;
@@ -522,6 +550,7 @@ class JsonWriter {
 
  private:
   const Schema& s_;
+  int depth_ = 0;
   struct Occ { int16_t fi; uint8_t wt; uint64_t v; const uint8_t* p; size_t n; };
 
   void key(std::string& out, bool& first, const std::string& k) {
@@ -540,6 +569,7 @@ class JsonWriter {
     while (!r.done()) {
       if (!r.next(&num, &wt, &v, &q, &l)) return false;
       if (num >= m.by_num.size() || m.by_num[num] < 0) continue;   // unknown field: skipped
+      if (!wire_ok(m.fields[m.by_num[num]], wt)) return false;     // wrong wire type: corrupt
       occ.push_back(Occ{m.by_num[num], wt, v, q, l});
     }
     std::stable_sort(occ.begin(), occ.end(), [](const Occ& a, const Occ& b) { return a.fi < b.fi; });
@@ -561,6 +591,8 @@ class JsonWriter {
       }
       if (j == i) continue;
       if (f.inl) {
+        DepthGuard g(depth_);
+        if (!g.ok) return false;
         for (size_t k = i; k < j; ++k)
           if (!members(f.msg, occ[k].p, occ[k].n, out, first, nullptr)) return false;
         i = j;
@@ -570,8 +602,14 @@ class JsonWriter {
       const char* sub_rv = (m.metadata == (int)fi) ? inject_rv : nullptr;
       if (f.label == L_REP) {
         out += '[';
+        bool firstel = true;
         for (size_t k = i; k < j; ++k) {
-          if (k > i) out += ',';
+          if (occ[k].wt == 2 && f.wt != 2) {   // packed run of scalars
+            if (!packed(f, occ[k], out, firstel)) return false;
+            continue;
+          }
+          if (!firstel) out += ',';
+          firstel = false;
           if (!value(f, occ[k], out, nullptr)) return false;
         }
         out += ']';
@@ -594,14 +632,33 @@ class JsonWriter {
     return true;
   }
 
+  bool packed(const Field& f, const Occ& o, std::string& out, bool& first) {
+    Reader r{o.p, o.p + o.n};
+    while (!r.done()) {
+      Occ e{o.fi, f.wt, 0, (const uint8_t*)"", 0};
+      if (f.wt == 0) {
+        if (!r.varint(&e.v)) return false;
+      } else {
+        if (r.e - r.p < 8) return false;
+        e.p = r.p; e.n = 8; r.p += 8;
+      }
+      if (!first) out += ',';
+      first = false;
+      if (!value(f, e, out, nullptr)) return false;
+    }
+    return true;
+  }
+
   bool map_entry(const Field& f, const uint8_t* p, size_t n, std::string& out) {
     Reader r{p, p + n};
     std::string k;
-    Occ val{0, 2, 0, (const uint8_t*)"", 0};
+    const uint8_t kwt = wire_of(f.key), vwt = f.type == S_MSG ? 2 : wire_of(f.type);
+    Occ val{0, vwt, 0, (const uint8_t*)"", 0};
     bool have = false;
     uint32_t num; uint8_t wt; uint64_t v; const uint8_t* q; size_t l;
     while (!r.done()) {
       if (!r.next(&num, &wt, &v, &q, &l)) return false;
+      if ((num == 1 && wt != kwt) || (num == 2 && wt != vwt)) return false;
       if (num == 1) {
         if (wt == 2) k.assign((const char*)q, l);
         else k = std::to_string(f.key == S_INT32 ? (int64_t)(int32_t)v : (int64_t)v);
@@ -619,6 +676,7 @@ class JsonWriter {
   }
 
   bool value(const Field& f, const Occ& o, std::string& out, const char* inject_rv) {
+    if (o.wt != (f.type == S_MSG ? 2 : wire_of(f.type))) return false;
     switch (f.type) {
       case S_STRING: json_escape(out, (const char*)o.p, o.n); return true;
       case S_BYTES: out += '"'; base64(out, o.p, o.n); out += '"'; return true;
@@ -640,6 +698,8 @@ class JsonWriter {
   }
 
   bool special(Special sp, const uint8_t* p, size_t n, std::string& out) {
+    DepthGuard g(depth_);
+    if (!g.ok) return false;
     Reader r{p, p + n};
     uint32_t num; uint8_t wt; uint64_t v; const uint8_t* q; size_t l;
     switch (sp) {

@@ -94,6 +94,25 @@ def test_layers_whiteouts_and_confinement(tmp_path):
     assert os.stat(root / "etc" / "link").st_ino == os.stat(root / "etc" / "keep").st_ino
 
 
+@pytest.mark.parametrize("entry", [".wh..", ".wh...", "..", "a/..", "a/.wh..", "a/.wh...", "./..", "a/b/../.."])
+def test_dot_entries_cannot_touch_the_store(tmp_path, entry):
+    """A hostile layer naming '.', '..' or a whiteout of them must not remove or write the
+    directory above the layer root (the store's other unpacked images)."""
+    store = tmp_path / "rootfs"
+    root = store / "img1"
+    sibling = store / "img2"
+    root.mkdir(parents=True)
+    sibling.mkdir()
+    (sibling / "bin").write_bytes(b"other image")
+    (root / "a").mkdir()
+    (root / "a" / "f").write_bytes(b"keep")
+    with pytest.raises(ValueError):
+        apply_layer(str(root), io.BytesIO(_layer([(entry, "file", b"x")])))
+    assert (sibling / "bin").read_bytes() == b"other image"
+    assert (root / "a" / "f").read_bytes() == b"keep"
+    assert sorted(os.listdir(store)) == ["img1", "img2"]
+
+
 def test_store_tags_gc_and_layout_import(tmp_path):
     st = OCIStore(str(tmp_path / "s"))
     md = build_image(st, "registry.local/base:1", {"bin/tool": (b"#!x", 0o755)}, {"Entrypoint": ["/bin/tool"]})

@@ -88,3 +88,26 @@ def test_impersonation_filter_and_kubectl_as(run, tmp_path):
             await admin.close()
             await api.stop()
     run(main())
+
+
+def test_specified_groups_are_the_complete_group_list():
+    """`impersonation.go:66-124`: with Impersonate-Group headers the specified groups are the
+    whole list — system:authenticated and the service-account groups are added only when no
+    group is specified."""
+    from kubernetes_amd.apiserver.impersonation import impersonate
+    calls = []
+
+    def allow(*a):
+        calls.append(a[1:])
+    me = User("imp", "3", ["system:authenticated"])
+    u = impersonate({"impersonate-user": "dev", "impersonate-group": "gpu-team"}, me, allow)
+    assert u.name == "dev" and list(u.groups) == ["gpu-team"]
+    u = impersonate({"impersonate-user": "dev"}, me, allow)
+    assert list(u.groups) == ["system:authenticated"]
+    u = impersonate({"impersonate-user": "system:serviceaccount:ns1:sa"}, me, allow)
+    assert list(u.groups) == ["system:serviceaccounts", "system:serviceaccounts:ns1", "system:authenticated"]
+    u = impersonate({"impersonate-user": "system:serviceaccount:ns1:sa", "impersonate-group": "g1, g2"}, me, allow)
+    assert list(u.groups) == ["g1", "g2"]
+    u = impersonate({"impersonate-user": "system:anonymous"}, me, allow)
+    assert list(u.groups) == []
+    assert ("impersonate", None, "groups", "", "g2", "") in calls
