@@ -136,8 +136,12 @@ def main(argv=None):
         else:
             client = Client(a.master or "http://127.0.0.1:8080", qps=a.kube_api_qps,
                             burst=a.kube_api_burst or int(a.kube_api_qps or 10), max_conns=64)
-        preds, prios, ext_cfgs = await SP.resolve_algorithm(client, a.algorithm_provider, a.policy_config_file,
-                                                            a.policy_configmap, a.policy_configmap_namespace)
+        algo = await SP.resolve_algorithm(client, a.algorithm_provider, a.policy_config_file,
+                                          a.policy_configmap, a.policy_configmap_namespace)
+        preds, prios, ext_cfgs = algo
+        if algo.hard_pod_affinity_symmetric_weight is not None:
+            # the Policy's value wins over the flag (`factory.go:847` CreateFromConfig)
+            a.hard_pod_affinity_symmetric_weight = algo.hard_pod_affinity_symmetric_weight
         extenders = [HTTPExtender.from_config(e) for e in ext_cfgs]
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
                       emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,

@@ -289,6 +289,21 @@ class SchedulerCache:
         self.affinity_pods: dict[str, dict] = {}
         self.hard_pod_affinity_weight = 1        # --hard-pod-affinity-symmetric-weight
         self.volumes = VolumeLister()
+        self.services: dict[str, dict[str, dict | None]] = {}   # namespace -> service -> selector
+
+    # -- services (spreading / service affinity) -----------------------------
+    def set_service(self, svc):
+        md = svc["metadata"]
+        self.services.setdefault(md.get("namespace", "default"), {})[md["name"]] = \
+            (svc.get("spec") or {}).get("selector")
+
+    def remove_service(self, svc):
+        md = svc["metadata"]
+        d = self.services.get(md.get("namespace", "default"))
+        if d is not None:
+            d.pop(md["name"], None)
+            if not d:
+                self.services.pop(md.get("namespace", "default"), None)
 
     def _track(self, key, pod):
         aff = (pod.get("spec") or {}).get("affinity") or {}

@@ -65,8 +65,70 @@ class CycleContext:
         self.any_anti_affinity = bool(self.anti_affinity_terms)
         self.volumes = cache.volumes
         self.pod = pod
+        self.namespace = pod["metadata"].get("namespace", "default")
         self.affinity_prefs = _preferred_pod_affinity(pod)
         self._aff_counts = None
+        self._svc = None
+        self._svc_counts = {}
+        self._svc_first = False
+
+    # -- services selecting the pod (SelectorSpread, ServiceSpreading, ServiceAffinity, ...) ----
+    @property
+    def service_items(self):
+        """[(service name, selector)] of the services in the pod's namespace that select it, by
+        name (`GetPodServices`: a service without a selector selects nothing)."""
+        if self._svc is None:
+            svcs = self.cache.services.get(self.namespace)
+            if not svcs:
+                self._svc = ()
+            else:
+                labels = self.pod["metadata"].get("labels") or {}
+                self._svc = [(n, sel) for n, sel in sorted(svcs.items())
+                             if sel is not None and all(labels.get(k) == v for k, v in sel.items())]
+        return self._svc
+
+    @property
+    def service_selectors(self):
+        return [sel for _, sel in self.service_items]
+
+    def service_label_counts(self, label):
+        """({node label value: pods of the pod's first service there}, pods of that service)."""
+        got = self._svc_counts.get(label)
+        if got is None:
+            counts, total = {}, 0
+            items = self.service_items
+            if items:
+                sel = items[0][1]
+                for pod, node in self.cache.pod_states.values():
+                    if pod["metadata"].get("namespace", "default") != self.namespace:
+                        continue
+                    lbl = pod["metadata"].get("labels") or {}
+                    if not all(lbl.get(k) == v for k, v in sel.items()):
+                        continue
+                    total += 1
+                    ni = self.cache.nodes.get(node)
+                    v = ni.labels.get(label) if ni is not None else None
+                    if v is not None:
+                        counts[v] = counts.get(v, 0) + 1
+            got = self._svc_counts[label] = (counts, total)
+        return got
+
+    def service_affinity_first_node(self):
+        """Node of the first placed pod whose labels carry this pod's labels (same namespace),
+        when a service selects the pod (`serviceAffinityMetadataProducer`)."""
+        if self._svc_first is False:
+            self._svc_first = None
+            if self.service_items:
+                want = self.pod["metadata"].get("labels") or {}
+                for pod, node in self.cache.pod_states.values():
+                    if pod["metadata"].get("namespace", "default") != self.namespace or pod is self.pod:
+                        continue
+                    lbl = pod["metadata"].get("labels") or {}
+                    if all(lbl.get(k) == v for k, v in want.items()):
+                        self._svc_first = self.cache.nodes.get(node)
+                        if self._svc_first is not None:
+                            break
+        return self._svc_first
 
     def pod_affinity_counts(self):
         """[(signed weight, topology key, {topology value: matching pods})] for the pod's
@@ -184,10 +246,21 @@ class GenericScheduler:
     def __init__(self, cache: SchedulerCache, predicates=None, priorities=None, percentage_of_nodes_to_score=100,
                  extenders=None, equivalence_cache=True, ecache_classes=256):
         self.cache = cache
-        names = predicates or P.DEFAULT_PREDICATES
-        self.predicates = [(n, P.PREDICATES[n]) for n in names]
+        # predicates: names from the registry, or (name, fn) for a Policy's argument-based
+        # custom predicate; priorities: name -> weight, or name -> (weight, fn, reverse, normalize)
+        self.predicates = [(n, P.PREDICATES[n]) if isinstance(n, str) else tuple(n)
+                           for n in (predicates or P.DEFAULT_PREDICATES)]
+        names = [n for n, _ in self.predicates]
         prios = priorities if priorities is not None else PR.DEFAULT_PRIORITIES
-        self.priorities = [(n, w, *PR.PRIORITIES[n]) for n, w in prios.items() if w]
+        self.priorities = []
+        for n, w in prios.items():
+            entry = (n, w, *PR.PRIORITIES[n]) if not isinstance(w, (tuple, list)) else (n, *w)
+            if entry[1]:
+                self.priorities.append(entry)
+        # plugins whose answer for one node depends on pods on OTHER nodes (ServiceAffinity,
+        # ServiceAntiAffinity): a node's cached evaluation would go stale, so no equivalence cache
+        self.global_view = any(getattr(f, "global_view", False) for _, f in self.predicates) or \
+            any(getattr(e[2], "global_view", False) for e in self.priorities)
         self.pct = percentage_of_nodes_to_score
         self.extenders = extenders or []
         self._next_start = 0
@@ -211,7 +284,9 @@ class GenericScheduler:
         for name, w, fn, reverse, norm in self.priorities:
             if name in ("XGMITopologyPriority", "GPUBinPackingPriority") and not pi.er:
                 continue
-            if name == "SelectorSpreadPriority" and not ctx.owner_uid:
+            if name == "SelectorSpreadPriority" and not ctx.owner_uid and not ctx.service_items:
+                continue
+            if name == "ServiceSpreadingPriority" and not ctx.service_items:
                 continue
             if name == "NodeAffinityPriority" and not ctx.node_affinity_prefs:
                 continue
@@ -241,8 +316,11 @@ class GenericScheduler:
         else:
             preds_for_pod = self.predicates_novol
         if self.use_ecache and not affinity_sensitive and not self.extenders and (fast or not reqs) \
-                and not pi.volumes and not ctx.affinity_prefs:
+                and not pi.volumes and not ctx.affinity_prefs and not self.global_view:
             key = equivalence_key(pod)
+            if self.cache.services:
+                # service-based spreading reads the pod's labels: the class includes its services
+                key += "|svc:" + ",".join(n for n, _ in ctx.service_items)
             ec = self.ecache.get(key)
             if ec is None:
                 ec = self.ecache[key] = {}

@@ -171,6 +171,58 @@ def match_inter_pod_affinity(pod, pi, ni, ctx):
     return None
 
 
+def general_predicates(pod, pi, ni, ctx):
+    """`predicates.go:965` GeneralPredicates: the non-critical PodFitsResources plus the
+    essential PodFitsHost, PodFitsHostPorts and PodMatchNodeSelector (`:1000-1040`) in one."""
+    for fn in (pod_fits_resources, pod_fits_host, pod_fits_host_ports, match_node_selector):
+        r = fn(pod, pi, ni, ctx)
+        if r:
+            return r
+    return None
+
+
+# -- argument-based custom predicates (Policy `predicates[].argument`) ------------------------
+# `plugin/pkg/scheduler/factory/plugins.go:198-240` RegisterCustomFitPredicate; each Policy
+# entry registers a fresh closure under its own name.
+
+def make_labels_presence(labels, presence):
+    """`predicates.go` NewNodeLabelPredicate / CheckNodeLabelPresence: with presence=true every
+    label must exist on the node, with presence=false none may (values are not looked at)."""
+    labels = list(labels or ())
+
+    def labels_presence(pod, pi, ni, ctx):
+        for lbl in labels:
+            if (lbl in ni.labels) != presence:
+                return "node(s) didn't have the requested labels"
+        return None
+    return labels_presence
+
+
+def make_service_affinity(labels):
+    """`predicates.go:829-922` ServiceAffinity: the pod's service-mates share the values of
+    `labels`. Values come first from the pod's own nodeSelector; the missing ones are taken from
+    the node of the first already-placed pod of the pod's services (pods in the namespace whose
+    labels carry the pod's labels, when any service selects the pod); the node must then match
+    them all. The first pod of a service may land anywhere."""
+    labels = list(labels or ())
+
+    def service_affinity(pod, pi, ni, ctx):
+        sel = (pod.get("spec") or {}).get("nodeSelector") or {}
+        want = {lbl: sel[lbl] for lbl in labels if lbl in sel}
+        if len(want) < len(labels):
+            first = ctx.service_affinity_first_node()
+            if first is not None:
+                for lbl in labels:
+                    if lbl not in want and lbl in first.labels:
+                        want[lbl] = first.labels[lbl]
+        for k, v in want.items():
+            if ni.labels.get(k) != v:
+                return "node(s) didn't match service affinity"
+        return None
+    service_affinity.global_view = True
+    return service_affinity
+
+
 from . import volumes as V  # noqa: E402
 
 PREDICATES = {
@@ -178,6 +230,8 @@ PREDICATES = {
     "HostName": pod_fits_host,
     "PodFitsResources": pod_fits_resources,
     "PodFitsHostPorts": pod_fits_host_ports,
+    "PodFitsPorts": pod_fits_host_ports,          # the deprecated name (defaults.go:67), same predicate
+    "GeneralPredicates": general_predicates,
     "MatchNodeSelector": match_node_selector,
     "PodToleratesNodeTaints": pod_tolerates_node_taints,
     "CheckNodeMemoryPressure": check_node_memory_pressure,

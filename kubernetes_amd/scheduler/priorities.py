@@ -42,18 +42,72 @@ def balanced_resource_allocation(pod, pi, ni, ctx):
     return MAX - abs(c - m) * MAX
 
 
+def _service_match(p, ns, sels):
+    if p["metadata"].get("namespace", "default") != ns:
+        return False
+    lbl = p["metadata"].get("labels") or {}
+    return any(all(lbl.get(k) == v for k, v in sel.items()) for sel in sels)
+
+
 def selector_spread(pod, pi, ni, ctx):
-    """Raw count of sibling pods (same controller) on the node; normalized reversed later."""
+    """`selector_spreading.go` CalculateSpreadPriorityMap: raw count of the pod's siblings on the
+    node — pods of the same controller, or pods any of the pod's services select; normalized
+    reversed later."""
     owner = ctx.owner_uid
-    if not owner:
+    sels = ctx.service_selectors
+    if not owner and not sels:
         return 0.0
+    ns = ctx.namespace
     n = 0
     for p, _ in ni.pods.values():
-        for ref in p["metadata"].get("ownerReferences") or ():
-            if ref.get("uid") == owner:
-                n += 1
-                break
+        if owner and any(ref.get("uid") == owner for ref in p["metadata"].get("ownerReferences") or ()):
+            n += 1
+        elif sels and _service_match(p, ns, sels):
+            n += 1
     return float(n)
+
+
+def service_spreading(pod, pi, ni, ctx):
+    """`ServiceSpreadingPriority` (defaults.go:95-106): SelectorSpread over services only (no
+    controller listers) — raw count of pods the pod's services select on the node."""
+    sels = ctx.service_selectors
+    if not sels:
+        return 0.0
+    ns = ctx.namespace
+    return float(sum(1 for p, _ in ni.pods.values() if _service_match(p, ns, sels)))
+
+
+def equal(pod, pi, ni, ctx):
+    """`EqualPriorityMap`: every node scores 1."""
+    return 1.0
+
+
+# -- argument-based custom priorities (Policy `priorities[].argument`) ------------------------
+# `plugin/pkg/scheduler/factory/plugins.go:299-340` RegisterCustomPriorityFunction
+
+def make_service_anti_affinity(label):
+    """`selector_spreading.go:209-254` ServiceAntiAffinity: spread the pods of the pod's first
+    service over the values of `label`. A node with the label scores
+    10 * (servicePods - podsOnItsLabelValue) / servicePods (10 when the service has no pods);
+    a node without it scores 0."""
+    def service_anti_affinity(pod, pi, ni, ctx):
+        v = ni.labels.get(label)
+        if v is None:
+            return 0.0
+        counts, total = ctx.service_label_counts(label)
+        if not total:
+            return MAX
+        return float(int(MAX * (total - counts.get(v, 0)) / total))
+    service_anti_affinity.global_view = True
+    return service_anti_affinity
+
+
+def make_label_preference(label, presence):
+    """`node_label.go` NodeLabelPrioritizer: 10 when the node has (presence) / lacks (not
+    presence) the label, else 0."""
+    def label_preference(pod, pi, ni, ctx):
+        return MAX if (label in ni.labels) == presence else 0.0
+    return label_preference
 
 
 def node_affinity(pod, pi, ni, ctx):
@@ -148,6 +202,8 @@ PRIORITIES = {
     "ImageLocalityPriority": (image_locality, False, False),
     "ResourceLimitsPriority": (resource_limits, False, False),
     "InterPodAffinityPriority": (inter_pod_affinity, False, "minmax"),
+    "ServiceSpreadingPriority": (service_spreading, True, True),
+    "EqualPriority": (equal, False, False),
 }
 
 DEFAULT_PRIORITIES = {

@@ -103,6 +103,8 @@ class Scheduler:
         self.pvc_informer = Informer(client, "persistentvolumeclaims")
         self.pv_informer = Informer(client, "persistentvolumes")
         self.sc_informer = Informer(client, "storageclasses")
+        # services: SelectorSpread / ServiceSpreading / ServiceAffinity / ServiceAntiAffinity
+        self.svc_informer = Informer(client, "services")
 
     # -- informer handlers -------------------------------------------------
     def _responsible(self, pod):
@@ -289,6 +291,8 @@ class Scheduler:
         self.pvc_informer.add_handler(put(vl.pvcs), put(vl.pvcs), drop(vl.pvcs))
         self.pv_informer.add_handler(put(vl.pvs), put(vl.pvs), drop(vl.pvs))
         self.sc_informer.add_handler(put(vl.classes), put(vl.classes), drop(vl.classes))
+        self.svc_informer.add_handler(self.cache.set_service, lambda old, new: self.cache.set_service(new),
+                                      self.cache.remove_service)
 
     # -- scheduling loop ---------------------------------------------------------
     async def run(self, metrics_port=None, metrics_address="127.0.0.1"):
@@ -302,7 +306,7 @@ class Scheduler:
             self.node_informer.add_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
             self.pod_informer.add_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
         self._volume_handlers()
-        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
+        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer):
             inf.start()
         self.node_informer.start()
         await self.node_informer.wait_synced(60)
@@ -310,7 +314,7 @@ class Scheduler:
             t = time.monotonic()
             while len(self._owned_ready) < len(self.owned) and time.monotonic() - t < 60:
                 await asyncio.sleep(0.01)
-        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
+        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer):
             await inf.wait_synced(60)
         self.pod_informer.start()
         await self.pod_informer.wait_synced(60)
@@ -499,7 +503,7 @@ class Scheduler:
         self.node_informer.stop()
         for inf in self.owned.values():
             inf.stop()
-        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer):
+        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer):
             inf.stop()
         self.recorder.stop()
         if self.http:

@@ -82,6 +82,7 @@ def test_remote_process_runtime_exec_logs_stats(run, tmp_path):
         sock = str(tmp_path / "cri.sock")
         srv = await CRIServer(ProcessRuntime(str(tmp_path / "rt")), sock).start()
         rt = await RemoteRuntime(sock, relist_period=0.05).connect()
+        sid = None
         try:
             p = pod()
             sid = await rt.run_pod_sandbox(p, {})
@@ -106,6 +107,9 @@ def test_remote_process_runtime_exec_logs_stats(run, tmp_path):
             await rt.stop_container(cid, 1)
             assert rt.container_status(cid).state == EXITED
         finally:
+            if sid is not None:       # the sandbox (pause) outlives the CRI server by design
+                await rt.stop_pod_sandbox(sid)
+                await rt.remove_pod_sandbox(sid)
             await rt.close()
             await srv.stop()
     run(main())
@@ -296,6 +300,7 @@ def test_run_as_user_over_cri(run, tmp_path):
         srv = await CRIServer(ProcessRuntime(str(tmp_path / "rt")), sock).start()
         rt = await RemoteRuntime(sock, relist_period=0.05).connect()
         uid = 65534 if os.geteuid() == 0 else os.geteuid()
+        sid = None
         try:
             p = pod()
             sid = await rt.run_pod_sandbox(p, {})
@@ -308,6 +313,9 @@ def test_run_as_user_over_cri(run, tmp_path):
                 await asyncio.sleep(0.05)
             assert (await rt.container_logs(cid)).strip() == str(uid).encode()
         finally:
+            if sid is not None:
+                await rt.stop_pod_sandbox(sid)
+                await rt.remove_pod_sandbox(sid)
             await rt.close()
             await srv.stop()
     run(main())
