@@ -104,8 +104,19 @@ def main(argv=None):
                    "garbagecollector": a.concurrent_gc_syncs, "namespace": a.concurrent_namespace_syncs,
                    "resourcequota": a.concurrent_resource_quota_syncs, "service": a.concurrent_service_syncs,
                    "serviceaccount-token": a.concurrent_serviceaccount_token_syncs}
+        sa_factory = None
+        if a.use_service_account_credentials:
+            if not a.service_account_private_key_file:
+                raise SystemExit("kube-controller-manager: --use-service-account-credentials needs "
+                                 "--service-account-private-key-file (the token controller mints the tokens)")
+            root = client
+
+            def sa_factory(token):
+                return Client(root.url, token=token, ssl_context=root.http.ssl, max_conns=16,
+                              qps=a.kube_api_qps, burst=a.kube_api_burst)
         cm = await ControllerManager(client, enabled, opts, workers=workers,
-                                     start_interval=_dur(a.controller_start_interval)).start()
+                                     start_interval=_dur(a.controller_start_interval),
+                                     sa_client_factory=sa_factory).start()
         health.metrics = cm
         return cm
 
@@ -161,7 +172,8 @@ def _reference_flags(ap):
     g.add_argument("--flex-volume-plugin-dir", default="/usr/libexec/kubernetes/kubelet-plugins/volume/exec/",
                    help="accepted (FlexVolume attach runs in the kubelet)")
     g.add_argument("--use-service-account-credentials", type=_bool, default=False,
-                   help="accepted; controllers share the manager's credentials")
+                   help="run each controller as its own kube-system service account "
+                        "(bound to its system:controller:<name> role)")
     for f in ("--pv-recycler-pod-template-filepath-nfs", "--pv-recycler-pod-template-filepath-hostpath"):
         g.add_argument(f, default="", help="accepted")
     for f in ("--pv-recycler-minimum-timeout-nfs", "--pv-recycler-increment-timeout-nfs",

@@ -114,7 +114,15 @@ class TokensController(Controller):
         refs = [r.get("name") for r in sa.get("secrets") or ()]
         want = refs + [t["metadata"]["name"] for t in live if t["metadata"]["name"] not in refs]
         if want != refs:
-            await self.client.patch("serviceaccounts", name, {"secrets": [{"name": n} for n in want]}, ns)
+            # an update of the live object (`tokens_controller.go` ensureReferencedToken): the
+            # system:kube-controller-manager role may update service accounts, not patch them;
+            # a conflict re-queues the key
+            live_sa = await self.client.get("serviceaccounts", name, ns)
+            have = [r.get("name") for r in live_sa.get("secrets") or ()]
+            add = [n for n in want if n not in have]
+            if add:
+                live_sa["secrets"] = (live_sa.get("secrets") or []) + [{"name": n} for n in add]
+                await self.client.update("serviceaccounts", live_sa, ns)
 
 
 def jws_detached(token_id, token_secret, payload: str) -> str:

@@ -225,7 +225,7 @@ def control_plane_manifests(cfg):
     cm = py + ["kubernetes_amd.cmd.controller_manager", "--kubeconfig", os.path.join(kd, CM_CONF), "--leader-elect",
                "--service-account-private-key-file", os.path.join(d, "sa.key"), "--root-ca-file", os.path.join(d, "ca.crt"),
                "--cluster-signing-cert-file", os.path.join(d, "ca.crt"), "--cluster-signing-key-file", os.path.join(d, "ca.key"),
-               "--controllers", "*,bootstrapsigner,tokencleaner"]
+               "--controllers", "*,bootstrapsigner,tokencleaner", "--use-service-account-credentials", "true"]
     sched = py + ["kubernetes_amd.cmd.scheduler", "--kubeconfig", os.path.join(kd, SCHED_CONF), "--leader-elect"]
     v = cfg.get("kubernetesVersion") or VERSION
     out = {"kube-apiserver": _static_pod("kube-apiserver", api, (d, cfg["etcd"]["dataDir"]), v),

@@ -274,7 +274,14 @@ async def apply(client, cfg, new_version, *, force=False, dry_run=False, allow_e
     out(f"[upgrade/staticpods] Writing new Static Pod manifests to {paths.new!r}")
     recover: dict[str, str] = {}
     for comp in COMPONENTS:
-        before = await static_pod_hash(client, cfg["nodeName"], comp)
+        # the current hash must be known: a mirror pod caught mid-recreation (no hash yet) would
+        # make ANY later hash look like a restart (`WaitForStaticPodHash` reads it first too)
+        before = None
+        end = time.monotonic() + min(timeout, 10.0)
+        while before is None and time.monotonic() < end:
+            before = await static_pod_hash(client, cfg["nodeName"], comp)
+            if before is None:
+                await asyncio.sleep(0.1)
         try:
             await upgrade_component(client, cfg, comp, paths, before, recover, timeout, out)
         except (UpgradeError, OSError) as e:

@@ -79,19 +79,26 @@ class StaticPodSource:
         self.period = period
         self.known: dict[tuple, str] = {}     # (ns, name) -> hash
         self._task = None
+        self._stopped = False
 
     def start(self):
+        self._stopped = False
         self._task = asyncio.ensure_future(self._loop())
 
     def stop(self):
+        # the flag as well as the cancel: a cancellation that lands inside an HTTP call can be
+        # turned into an ordinary error by the client, which the loop below would survive
+        self._stopped = True
         if self._task:
             self._task.cancel()
 
     async def _loop(self):
-        while True:
+        while not self._stopped:
             try:
                 await self.sync()
             except Exception:
+                if self._stopped:
+                    return
                 log.exception("static pod sync failed")
             await asyncio.sleep(self.period)
 
