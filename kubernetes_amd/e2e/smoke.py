@@ -7,10 +7,15 @@ log says "Test PASSED" (the reference's cuda-vector-add e2e check,
 test/e2e/scheduling/nvidia-gpus.go:51-113).
 
 The pod's own view is checked, not only the bundle: HIP inside the pod enumerates exactly the
-allocated GPU(s). With enforced isolation (kamd-runc: private /dev) the pod's /dev/dri holds
-only its render node and HIP_VISIBLE_DEVICES is unset; on a node that cannot isolate (an
-unprivileged kubelet without user namespaces, e.g. the GPU CI box) the node must carry
-IsolationUnavailable=True and the runtime narrows HIP with HIP_VISIBLE_DEVICES instead.
+allocated GPU(s). Which enforcement tier is in force is decided by the node's own
+`kamd-runc features` output and reported:
+  * namespaces — private /dev: the pod's /dev/dri holds only its render node;
+  * landlock   — no namespaces (an unprivileged kubelet without user namespaces, e.g. the GPU CI
+                 box): /dev/dri lists everything, but the pod can open only its allocated node;
+                 every node the kubelet itself can open but did not allocate must be denied;
+  * none       — the node carries IsolationUnavailable=True and HIP is narrowed with
+                 HIP_VISIBLE_DEVICES only.
+In the enforced tiers HIP_VISIBLE_DEVICES stays unset.
 """
 from __future__ import annotations
 
@@ -67,6 +72,9 @@ async def gpu_pod_e2e(timeout=120, cri=False):
                 "spec": {"restartPolicy": "Never",
                          "containers": [{"name": "v", "image": "busybox",
                                          "command": ["/bin/sh", "-c", "echo DRI=$(ls /dev/dri | tr '\\n' ' '); "
+                                                     "for n in /dev/dri/*; do if [ -c \"$n\" ]; then "
+                                                     "if (exec 3<>\"$n\") 2>/dev/null; then echo \"OPEN $n\"; "
+                                                     "else echo \"DENIED $n\"; fi; fi; done; "
                                                      "echo HIP=${HIP_VISIBLE_DEVICES-unset}"],
                                          "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
         await cl.client.create("pods", view)
@@ -82,9 +90,33 @@ async def gpu_pod_e2e(timeout=120, cri=False):
         minor = node["status"]["extendedResources"][core.AMD_GPU]["resources"][
             pv["spec"]["extendedResources"][0]["assigned"][0]]["attributes"].get(core.ATTR_RENDER_MINOR)
         dri = vlog.split("DRI=", 1)[1].split("\n", 1)[0].split()
+        mine = f"/dev/dri/renderD{minor}"
+        opened = {ln.split()[1] for ln in vlog.splitlines() if ln.startswith("OPEN ")}
+        denied = {ln.split()[1] for ln in vlog.splitlines() if ln.startswith("DENIED ")}
+        # what the kubelet itself may open: a node the pod is denied only proves confinement if
+        # the same user could open it outside the pod
+        host_openable = set()
+        for n in sorted(os.listdir("/dev/dri")) if os.path.isdir("/dev/dri") else ():
+            p = os.path.join("/dev/dri", n)
+            try:
+                os.close(os.open(p, os.O_RDWR))
+                host_openable.add(p)
+            except OSError:
+                pass
+        result["tier"] = iso.get("tier")
+        result["pod_opened"], result["pod_denied"] = sorted(opened), sorted(denied)
+        result["host_openable"] = sorted(host_openable)
+        result["confinement_demonstrated"] = bool(iso["enforced"] and (host_openable - {mine}) and
+                                                  (host_openable - {mine}) <= denied)
         if iso["enforced"]:
-            assert dri == [f"renderD{minor}"], vlog
             assert "HIP=unset" in vlog, vlog
+            assert mine in opened or iso.get("tier") == "namespaces" and dri == [f"renderD{minor}"], vlog
+            if iso.get("tier") == "namespaces":
+                assert dri == [f"renderD{minor}"], vlog
+            else:
+                # Landlock: every node this user could open that is not the pod's is denied
+                assert not (opened - {mine}), vlog
+                assert (host_openable - {mine}) <= denied, (vlog, host_openable)
         else:
             assert "HIP=unset" not in vlog and "HIP=-1" not in vlog, vlog
         if cri:

@@ -12,7 +12,11 @@
                (v2 BPF or v1 devices.allow) — a pod cannot reach a render node it was not given,
                whatever HIP_VISIBLE_DEVICES says. Where namespaces are not allowed (an
                unprivileged kubelet on a host without user namespaces) the runtime says so
-               (`isolation_status()` → node condition IsolationUnavailable) and falls back to
+               and uses the next tier when the kernel has it: Landlock — kamd-runc runs the
+               container without namespaces but restricts it (no_new_privs + a Landlock ruleset)
+               so that under /dev/dri only the allocated render node(s) can be opened (EACCES for
+               the others). Only when neither tier works does the runtime say so
+               (`isolation_status()` → node condition IsolationUnavailable) and fall back to
                narrowing HIP enumeration with HIP_VISIBLE_DEVICES; `isolation="required"` refuses
                device containers instead;
   * images   = a local image map (`IMAGES`) resolves well-known images to built executables,
@@ -244,7 +248,8 @@ class ProcessRuntime(Runtime):
     name = "process"
     shares_host_network = True     # containers are host processes: pod IP = node address
 
-    def __init__(self, root_dir: str, inherit_env: bool = True, isolation: str | None = None, images=None):
+    def __init__(self, root_dir: str, inherit_env: bool = True, isolation: str | None = None, images=None,
+                 tier: str | None = None, landlock_dir: str = "/dev/dri"):
         super().__init__()
         # an images.service.ImageService: OCI images (pulled or imported) run on an overlay of
         # their unpacked layers; without one, images resolve to built binaries / the host root
@@ -264,21 +269,53 @@ class ProcessRuntime(Runtime):
             raise ValueError(f"isolation must be auto, required or off, not {self.isolation!r}")
         self.features = runc_features() if self.isolation != "off" else {}
         self.isolated = bool(self.features.get("isolation"))
+        # enforcement tier: "namespaces" (private /dev + device cgroup), "landlock" (no
+        # namespaces; /dev/dri opens limited to the allocation) or "none". KAMD_ISOLATION_TIER /
+        # `tier` pins one (tests rehearse the unprivileged tier on a host that has namespaces).
+        want = tier or os.environ.get("KAMD_ISOLATION_TIER", "auto")
+        has_ll = int(self.features.get("landlock") or 0) > 0 and os.access(KAMD_RUNC, os.X_OK)
+        if self.isolation == "off":
+            self.tier = "none"
+        elif want == "auto":
+            self.tier = "namespaces" if self.isolated else ("landlock" if has_ll else "none")
+        elif want == "landlock":
+            if not has_ll:
+                raise ValueError("isolation tier landlock requested, but " +
+                                 (self.features.get("landlock_error") or "kamd-runc reports no Landlock support"))
+            self.tier = "landlock"
+        elif want in ("namespaces", "none"):
+            if want == "namespaces" and not self.isolated:
+                raise ValueError("isolation tier namespaces requested, but " +
+                                 (self.features.get("namespace_error") or "namespaces are unavailable"))
+            self.tier = want
+        else:
+            raise ValueError(f"isolation tier must be auto, namespaces, landlock or none, not {want!r}")
+        self.isolated = self.tier == "namespaces"
+        self.landlocked = self.tier == "landlock"
+        self.landlock_dir = landlock_dir
         self._started = False
         self._ids = itertools.count(self._load_state() + 1)
 
     def isolation_status(self):
         if self.isolation == "off":
-            return {"enforced": False, "reason": "IsolationDisabled",
+            return {"enforced": False, "tier": "none", "reason": "IsolationDisabled",
                     "message": "container isolation is off: GPU enumeration is narrowed by HIP_VISIBLE_DEVICES only"}
         f = self.features
         if self.isolated:
             dc = f.get("device_cgroup", "none")
-            return {"enforced": True, "reason": "DeviceIsolationEnforced",
-                    "message": f"mount/pid/ipc/uts namespaces{' in a user namespace' if f.get('user_ns') else ''}, "
+            return {"enforced": True, "tier": "namespaces", "reason": "DeviceIsolationEnforced",
+                    "message": f"tier namespaces: mount/pid/ipc/uts namespaces"
+                               f"{' in a user namespace' if f.get('user_ns') else ''}, "
                                f"private /dev with only the allocated device nodes, device cgroup: {dc}"}
-        return {"enforced": False, "reason": "IsolationUnavailable",
+        if self.landlocked:
+            return {"enforced": True, "tier": "landlock", "reason": "DeviceIsolationEnforced",
+                    "message": f"tier landlock (ABI {f.get('landlock')}): no container namespaces here ("
+                               + (f.get("namespace_error") or "unavailable") + f"), but each container opens "
+                               f"only its allocated nodes under {self.landlock_dir} (Landlock ruleset under "
+                               f"no_new_privs, EACCES for the others)"}
+        return {"enforced": False, "tier": "none", "reason": "IsolationUnavailable",
                 "message": "no mount namespace for containers (" + (f.get("namespace_error") or "unknown") +
+                           ") and no Landlock (" + (f.get("landlock_error") or "unknown") +
                            "): a pod can open any /dev/dri/renderD* of the host; GPU enumeration is narrowed by "
                            "HIP_VISIBLE_DEVICES only"}
 
@@ -341,7 +378,7 @@ class ProcessRuntime(Runtime):
                               "env": st.get("env") or {}, "cwd": st.get("cwd"), "proc": proc, "dir": d, "spec": None,
                               "oom_score_adj": None, "cgroup": None, "attempt": st.get("attempt", 0),
                               "init_pid": st.get("init_pid"), "isolated": st.get("isolated", False),
-                              "user": st.get("user"),
+                              "user": st.get("user"), "landlock": st.get("landlock"),
                               "adopted": proc is not None and proc.returncode is None}
         return top
 
@@ -355,6 +392,8 @@ class ProcessRuntime(Runtime):
               "env": m["env"], "cwd": m["cwd"], "isolated": m.get("isolated", False)}
         if m.get("init_pid"):
             st["init_pid"], st["user"] = m["init_pid"], m.get("user")
+        if m.get("landlock"):
+            st["landlock"] = m["landlock"]
         if proc is not None:
             st["pid"], st["ticks"] = proc.pid, _start_ticks(proc.pid)
         st.update(extra)
@@ -454,13 +493,13 @@ class ProcessRuntime(Runtime):
         env.pop("ROCR_VISIBLE_DEVICES", None)
         env.pop("CUDA_VISIBLE_DEVICES", None)
         env.pop("HIP_VISIBLE_DEVICES", None)
-        if opts.devices and not self.isolated and self.isolation == "required":
+        if opts.devices and self.tier == "none" and self.isolation == "required":
             raise OSError(1, "IsolationUnavailable: the runtime cannot give this container a private /dev "
                              f"({self.isolation_status()['message']})")
-        if not self.isolated:
-            # no device namespace: narrow HIP enumeration to the allocation; a container without
-            # allocated GPUs sees none. (Isolated containers see only their own render nodes, so
-            # HIP's default enumeration is already right.)
+        if self.tier == "none":
+            # no enforcement: narrow HIP enumeration to the allocation; a container without
+            # allocated GPUs sees none. (In the enforced tiers a container can open only its own
+            # render nodes, so HIP's default enumeration is already right.)
             env["HIP_VISIBLE_DEVICES"] = dev_env.get("AMD_VISIBLE_DEVICES", "-1")
         sb = self.sandboxes.get(sid) or {}
         cgroup = os.path.join(opts.cgroup_parent, f"ctr-{leaf}") if opts.cgroup_parent else None
@@ -484,9 +523,16 @@ class ProcessRuntime(Runtime):
             rootfs = overlay["rootfs"]
         spec = oci.build_spec(pod, dict(container, command=argv, args=[]), opts, rootfs=rootfs,
                               sandbox_pid=getattr(sb.get("proc"), "pid", None),
-                              env=env if self.isolated else None, cgroups_path=cgroup, ns_paths=ns_paths,
-                              host_network=self.shares_host_network,
+                              env=env if (self.isolated or self.landlocked) else None, cgroups_path=cgroup,
+                              ns_paths=ns_paths, host_network=self.shares_host_network,
                               cpus=",".join(str(c) for c in sorted(cpus)) if cpus else None)
+        landlock = None
+        if self.landlocked:
+            # no namespaces at all: kamd-runc restricts the process itself before exec
+            spec["linux"]["namespaces"] = []
+            spec["annotations"].update({"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": self.landlock_dir})
+            nodes = [d.get("kamd.io/host-path") or d["path"] for d in spec["linux"]["devices"]]
+            landlock = self.landlock_dir + ":" + ",".join(nodes)
         if overlay is not None:
             spec["annotations"].update({"kamd.io/rootfs-lower": image_root, "kamd.io/rootfs-upper": overlay["upper"],
                                         "kamd.io/rootfs-work": overlay["work"]})
@@ -499,7 +545,8 @@ class ProcessRuntime(Runtime):
                           "cwd": container.get("workingDir") or None, "proc": None, "dir": d, "spec": spec,
                           "oom_score_adj": opts.oom_score_adj, "cgroup": cgroup, "cpus": cpus,
                           "attempt": opts.attempt, "run_as_user": opts.run_as_user, "run_as_group": opts.run_as_group,
-                          "groups": list(opts.supplemental_groups), "isolated": self.isolated,
+                          "groups": list(opts.supplemental_groups), "isolated": self.isolated or self.landlocked,
+                          "landlock": landlock,
                           "image_rootfs": overlay is not None,
                           "user": f"{spec['process']['user']['uid']}:{spec['process']['user']['gid']}"}
         return cid
@@ -668,7 +715,8 @@ class ProcessRuntime(Runtime):
         if m.get("init_pid"):
             # into the container's namespaces (its /dev view, pid namespace) as its user
             argv = [KAMD_RUNC, "exec", "--pid", str(m["init_pid"]), "--cwd", cwd or "/"] + \
-                (["--user", m["user"]] if m.get("user") else []) + ["--"] + argv
+                (["--user", m["user"]] if m.get("user") else []) + \
+                (["--landlock", m["landlock"]] if m.get("landlock") else []) + ["--"] + argv
             cwd = None
         return argv, cwd
 

@@ -3,7 +3,8 @@
 //
 //   kamd-runc features                         JSON: which isolation primitives work here
 //   kamd-runc run --bundle DIR [--ready-fd N]  run DIR/config.json in the foreground
-//   kamd-runc exec --pid PID [--cwd D] [--user U:G] -- argv   enter a running container
+//   kamd-runc exec --pid PID [--cwd D] [--user U:G] [--landlock DIR:NODE,...] -- argv
+//                                              enter a running container
 //
 // Parity target: what dockershim + docker/runc gave the reference's GPU pods
 // (`pkg/kubelet/dockershim/docker_container.go:164-172` maps the device plugin's DeviceSpecs
@@ -25,15 +26,21 @@
 // Device cgroup: cgroup v2 -> a BPF_PROG_TYPE_CGROUP_DEVICE program generated from
 // linux.resources.devices, attached to the container cgroup; cgroup v1 -> devices.deny /
 // devices.allow in the devices hierarchy. Unprivileged (no CAP_SYS_ADMIN): a user namespace
-// maps the container uid onto the caller's uid. When neither is possible `features` says so
-// and the kubelet reports the node condition IsolationUnavailable instead of degrading
-// silently.
+// maps the container uid onto the caller's uid.
+// Landlock tier (an unprivileged host without user namespaces, e.g. the MI355X CI pool): no
+// namespaces at all, but before exec the container process restricts itself with a Landlock
+// ruleset under no_new_privs — opening anything under /dev/dri other than its allocated render
+// node(s) fails with EACCES, while the rest of the filesystem keeps its normal permissions.
+// When no tier works `features` says so and the kubelet reports the node condition
+// IsolationUnavailable instead of degrading silently.
 #include <errno.h>
 #include <fcntl.h>
 #include <grp.h>
 #include <limits.h>
 #include <linux/bpf.h>
 #include <linux/capability.h>
+#include <linux/landlock.h>
+#include <dirent.h>
 #include <sched.h>
 #include <signal.h>
 #include <stdarg.h>
@@ -697,7 +704,82 @@ struct HostNode {
   unsigned maj = 0, min = 0;
 };
 
+// ---------------------------------------------------------------------------------------------
+// Landlock (unprivileged device confinement)
+int landlock_abi() {
+  long r = syscall(__NR_landlock_create_ruleset, nullptr, 0, LANDLOCK_CREATE_RULESET_VERSION);
+  return r < 0 ? 0 : (int)r;
+}
+
+// Restrict this process (and its future children) so that files under `dir` can be opened for
+// reading or writing only when they are in `allowed`; everywhere else opens behave as before.
+// Landlock rules only ever ALLOW, so the ruleset allows every sibling on the way from / down to
+// `dir` and, inside `dir`, just the allowed entries. What is not an open (readdir, stat, exec,
+// mkdir, ...) is not handled by the ruleset and stays unrestricted. Returns "" or an error.
+std::string landlock_restrict(const std::string& dir_in, const std::vector<std::string>& allowed, int* nrules) {
+  const uint64_t rights = LANDLOCK_ACCESS_FS_READ_FILE | LANDLOCK_ACCESS_FS_WRITE_FILE;
+  char real[PATH_MAX];
+  if (!realpath(dir_in.c_str(), real)) return "realpath " + dir_in + ": " + strerror(errno);
+  std::string dir = real;
+  if (dir == "/") return "refusing to restrict /";
+  struct landlock_ruleset_attr ra;
+  memset(&ra, 0, sizeof ra);
+  ra.handled_access_fs = rights;
+  int rs = (int)syscall(__NR_landlock_create_ruleset, &ra, sizeof ra, 0);
+  if (rs < 0) return std::string("landlock_create_ruleset: ") + strerror(errno);
+  int n = 0;
+  std::string err;
+  auto allow = [&](const std::string& path) {
+    int fd = open(path.c_str(), O_PATH | O_CLOEXEC);
+    if (fd < 0) return;                      // dangling link / vanished: nothing to allow
+    struct landlock_path_beneath_attr pb;
+    memset(&pb, 0, sizeof pb);
+    pb.allowed_access = rights;              // file rights: valid on files and directories
+    pb.parent_fd = fd;
+    if (syscall(__NR_landlock_add_rule, rs, LANDLOCK_RULE_PATH_BENEATH, &pb, 0) == 0) ++n;
+    else if (err.empty()) err = "landlock_add_rule " + path + ": " + strerror(errno);
+    close(fd);
+  };
+  std::vector<std::string> comps = split_path(dir);
+  std::string level = "/";
+  for (size_t k = 0; k < comps.size(); ++k) {
+    DIR* d = opendir(level.c_str());
+    if (!d) { close(rs); return "opendir " + level + ": " + strerror(errno); }
+    while (struct dirent* e = readdir(d)) {
+      std::string name = e->d_name;
+      if (name == "." || name == ".." || name == comps[k]) continue;
+      allow((level == "/" ? "/" : level + "/") + name);
+    }
+    closedir(d);
+    level = (level == "/" ? "/" : level + "/") + comps[k];
+  }
+  std::vector<std::string> inside;
+  for (auto& a : allowed) {
+    char ar[PATH_MAX];
+    if (!realpath(a.c_str(), ar)) continue;
+    std::string r = ar;
+    if (r.compare(0, dir.size() + 1, dir + "/") == 0) {
+      allow(r);
+      inside.push_back(r);
+    }
+  }
+  if (!err.empty()) { close(rs); return err; }
+  // restrict_self needs no_new_privs (or CAP_SYS_ADMIN): set it either way — a setuid binary in
+  // the container could otherwise regain what the ruleset takes away
+  if (prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0) != 0) { close(rs); return std::string("no_new_privs: ") + strerror(errno); }
+  if (syscall(__NR_landlock_restrict_self, rs, 0) != 0) {
+    std::string e = std::string("landlock_restrict_self: ") + strerror(errno);
+    close(rs);
+    return e;
+  }
+  close(rs);
+  if (nrules) *nrules = n;
+  return "";
+}
+
 struct Report {
+  std::string tier = "none";               // namespaces | landlock | none
+  int landlock_rules = 0;
   bool user_ns = false, mount_ns = false, pid_ns = false, ipc_ns = false, uts_ns = false;
   std::string proc = "host", dev = "host", sys = "host";
   std::vector<std::string> devices;
@@ -995,6 +1077,8 @@ std::string report_json(const Report& r, const CgroupState& cg) {
   b("pid_ns", r.pid_ns);
   b("ipc_ns", r.ipc_ns);
   b("uts_ns", r.uts_ns);
+  o += "\"tier\":" + json_str(r.tier) + ",";
+  if (r.tier == "landlock") o += "\"landlock_rules\":" + std::to_string(r.landlock_rules) + ",";
   o += "\"proc\":" + json_str(r.proc) + ",\"dev\":" + json_str(r.dev) + ",\"sys\":" + json_str(r.sys);
   o += ",\"device_cgroup\":" + json_str(cg.mode);
   if (!cg.error.empty()) o += ",\"device_cgroup_error\":" + json_str(cg.error);
@@ -1156,6 +1240,22 @@ int cmd_run(const std::string& bundle, int ready_fd) {
       std::string h = spec["hostname"].str();
       if (sethostname(h.c_str(), h.size()) != 0) warn("sethostname: %s", strerror(errno));
     }
+    if (rep.mount_ns && rep.dev == "private") rep.tier = "namespaces";
+    const J& ann2 = spec["annotations"];
+    if (!rep.mount_ns && ann2["kamd.io/isolation-tier"].str() == "landlock") {
+      // Landlock tier: the spec's device nodes under the restricted directory are the only
+      // ones there this container may open
+      std::string dir = ann2["kamd.io/landlock-dir"].str("/dev/dri");
+      std::vector<std::string> allowed;
+      for (auto& d : spec["linux"]["devices"].a) {
+        allowed.push_back(d["kamd.io/host-path"].str(d["path"].str().c_str()));
+        rep.devices.push_back(d["path"].str());
+      }
+      std::string e = landlock_restrict(dir, allowed, &rep.landlock_rules);
+      if (!e.empty()) die(126, "landlock: %s", e.c_str());
+      rep.tier = "landlock";
+      rep.dev = "host (landlock: " + dir + " limited to the allocated nodes)";
+    }
     // the bundle path may be gone after pivot_root: the report goes to P over the sync pipe
     std::string report = report_json(rep, cg);
     // bounding set first: dropping needs CAP_SETPCAP, which a setuid away from root loses
@@ -1213,7 +1313,8 @@ int cmd_run(const std::string& bundle, int ready_fd) {
 
 // enter a running container (CRI ExecSync / streaming exec): its user namespace first (when it
 // has one of its own), then ipc, uts, net, pid and mount; fork so the pid namespace applies.
-int cmd_exec(pid_t target, const std::string& cwd, const std::string& user, char** argv) {
+int cmd_exec(pid_t target, const std::string& cwd, const std::string& user, const std::string& landlock,
+             char** argv) {
   const char* order[] = {"user", "ipc", "uts", "net", "pid", "mnt"};
   const int flags[] = {CLONE_NEWUSER, CLONE_NEWIPC, CLONE_NEWUTS, CLONE_NEWNET, CLONE_NEWPID, CLONE_NEWNS};
   int fds[6];
@@ -1255,6 +1356,24 @@ int cmd_exec(pid_t target, const std::string& cwd, const std::string& user, char
     }
 
     prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0);
+    if (!landlock.empty()) {
+      // a Landlock-tier container: the exec'd process gets the container's ruleset
+      size_t c2 = landlock.find(':');
+      std::string dir = landlock.substr(0, c2);
+      std::vector<std::string> allowed;
+      if (c2 != std::string::npos) {
+        std::string rest = landlock.substr(c2 + 1);
+        size_t i = 0;
+        while (i <= rest.size()) {
+          size_t j = rest.find(',', i);
+          if (j == std::string::npos) j = rest.size();
+          if (j > i) allowed.push_back(rest.substr(i, j - i));
+          i = j + 1;
+        }
+      }
+      std::string e = landlock_restrict(dir, allowed, nullptr);
+      if (!e.empty()) die(126, "landlock: %s", e.c_str());
+    }
     if (chdir(cwd.empty() ? "/" : cwd.c_str()) != 0) die(126, "chdir %s: %s", cwd.c_str(), strerror(errno));
     execvp(argv[0], argv);
     fprintf(stderr, "kamd-runc: exec %s: %s\n", argv[0], strerror(errno));
@@ -1322,7 +1441,38 @@ int cmd_features(const std::string& cgroup_dir) {
          json_str(dc).c_str());
   if (!err.empty()) printf(",\"namespace_error\":%s", json_str(err).c_str());
   if (!dc_err.empty()) printf(",\"device_cgroup_error\":%s", json_str(dc_err).c_str());
-  printf(",\"isolation\":%s}\n", (ns && tmpfs) ? "true" : "false");
+  // Landlock is probed in the same throwaway way: a ruleset restricting a scratch directory is
+  // created and enforced in a child (no_new_privs, nothing else) — a kernel that lists the LSM
+  // but refuses restrict_self (seccomp, old ABI) reads as unavailable
+  int abi = landlock_abi();
+  std::string ll_err;
+  if (abi > 0) {
+    int q[2];
+    if (pipe(q) == 0) {
+      pid_t lc = fork();
+      if (lc == 0) {
+        close(q[0]);
+        std::string e = landlock_restrict("/dev", {}, nullptr);
+        if (write(q[1], e.data(), e.size()) < 0) _exit(1);
+        _exit(0);
+      }
+      close(q[1]);
+      char eb[256] = {0};
+      ssize_t er = read(q[0], eb, sizeof eb - 1);
+      (void)er;
+      close(q[0]);
+      int lst;
+      waitpid(lc, &lst, 0);
+      ll_err = eb;
+      if (!ll_err.empty()) abi = 0;
+    }
+  } else {
+    ll_err = "landlock_create_ruleset: not supported by this kernel";
+  }
+  printf(",\"landlock\":%d", abi);
+  if (!ll_err.empty()) printf(",\"landlock_error\":%s", json_str(ll_err).c_str());
+  const char* tier = (ns && tmpfs) ? "namespaces" : abi > 0 ? "landlock" : "none";
+  printf(",\"tier\":\"%s\",\"isolation\":%s}\n", tier, (ns && tmpfs) ? "true" : "false");
   return 0;
 }
 
@@ -1330,7 +1480,7 @@ void usage() {
   fprintf(stderr,
           "usage: kamd-runc features [--cgroup DIR]\n"
           "       kamd-runc run --bundle DIR [--ready-fd N]\n"
-          "       kamd-runc exec --pid PID [--cwd DIR] [--user UID[:GID]] -- argv...\n");
+          "       kamd-runc exec --pid PID [--cwd DIR] [--user UID[:GID]] [--landlock DIR:NODE,...] -- argv...\n");
   _exit(126);
 }
 
@@ -1360,7 +1510,7 @@ int main(int argc, char** argv) {
   }
   if (cmd == "exec") {
     pid_t pid = 0;
-    std::string cwd, user;
+    std::string cwd, user, landlock;
     int i = 2;
     for (; i < argc; ++i) {
       if (!strcmp(argv[i], "--")) { ++i; break; }
@@ -1368,10 +1518,11 @@ int main(int argc, char** argv) {
       if (!strcmp(argv[i], "--pid")) pid = (pid_t)atoi(argv[++i]);
       else if (!strcmp(argv[i], "--cwd")) cwd = argv[++i];
       else if (!strcmp(argv[i], "--user")) user = argv[++i];
+      else if (!strcmp(argv[i], "--landlock")) landlock = argv[++i];
       else usage();
     }
     if (pid <= 0 || i >= argc) usage();
-    return cmd_exec(pid, cwd, user, argv + i);
+    return cmd_exec(pid, cwd, user, landlock, argv + i);
   }
   usage();
 }

@@ -296,3 +296,163 @@ def test_image_symlinks_cannot_redirect_mounts_to_the_host(tmp_path):
     # the mountpoints landed inside the rootfs, at the re-rooted symlink targets
     inside = rootfs / str(host_data).lstrip("/")
     assert (inside / "f.txt").exists() and (inside / "sub" / "dir").is_dir()
+
+
+# -- Landlock tier (unprivileged host without user namespaces) --------------------------------
+needs_landlock = pytest.mark.skipif(not FEATURES.get("landlock") or os.geteuid() != 0,
+                                    reason=f"Landlock not available here (or not root to set up stand-ins): {FEATURES}")
+
+LL_PROBE = r'''
+import errno, os, sys
+def probe(p, flags=os.O_RDWR):
+    try:
+        os.close(os.open(p, flags))
+        return "OPEN"
+    except OSError as e:
+        return errno.errorcode.get(e.errno, str(e.errno))
+d = sys.argv[1]
+print("LIST", ",".join(sorted(os.listdir(d))))
+for n in sorted(os.listdir(d)):
+    print("NODE", n, probe(os.path.join(d, n)))
+print("ETC", probe("/etc/passwd", os.O_RDONLY))
+print("UID", os.getuid())
+'''
+
+
+def _ll_tree(tmp):
+    """A world-traversable stand-in for /dev/dri: three char nodes that open like /dev/null."""
+    import tempfile
+    base = tempfile.mkdtemp(prefix="kamd-ll-", dir="/tmp")
+    os.chmod(base, 0o755)
+    dri = os.path.join(base, "dri")
+    os.makedirs(dri)
+    os.chmod(dri, 0o755)
+    for m in (128, 129, 130):
+        p = os.path.join(dri, f"renderD{m}")
+        os.mknod(p, stat.S_IFCHR | 0o666, os.makedev(1, 3))
+        os.chmod(p, 0o666)
+    return base, dri
+
+
+def _as_nobody():
+    os.setgroups([])
+    os.setgid(65534)
+    os.setuid(65534)
+
+
+@needs_landlock
+def test_landlock_tier_unprivileged_container(tmp_path):
+    """kamd-runc, run as a NON-ROOT uid with no namespaces (the MI355X pool's situation): the
+    container can open its allocated stand-in render node and ordinary files, and gets EACCES for
+    the other nodes of the restricted directory; `kamd-runc exec --landlock` gives an exec'd
+    process the same ruleset."""
+    import shutil
+    import sys
+    base, dri = _ll_tree(tmp_path)
+    try:
+        b = os.path.join(base, "bundle")
+        os.makedirs(b)
+        os.chmod(b, 0o777)
+        probe = os.path.join(base, "probe.py")
+        with open(probe, "w") as f:
+            f.write(LL_PROBE)
+        os.chmod(probe, 0o644)
+        mine = os.path.join(dri, "renderD129")
+        runc = os.path.join(base, "kamd-runc")          # /root is not traversable for nobody
+        shutil.copy(proc_rt.KAMD_RUNC, runc)
+        os.chmod(runc, 0o755)
+        spec = {"process": {"args": [sys.executable, probe, dri], "env": ["PATH=/usr/bin:/bin"], "cwd": "/",
+                            "user": {"uid": 65534, "gid": 65534}},
+                "root": {"path": "/"}, "mounts": [],
+                "annotations": {"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": dri},
+                "linux": {"devices": [{"path": mine, "type": "c", "major": 1, "minor": 3}], "namespaces": []}}
+        with open(os.path.join(b, "config.json"), "w") as f:
+            json.dump(spec, f)
+        r = subprocess.run([runc, "run", "--bundle", b], capture_output=True, text=True, timeout=30,
+                           preexec_fn=_as_nobody)
+        assert r.returncode == 0, r.stderr
+        out = r.stdout.splitlines()
+        assert "LIST renderD128,renderD129,renderD130" in out              # listing is not restricted
+        assert "NODE renderD129 OPEN" in out                              # the allocated node
+        assert "NODE renderD128 EACCES" in out and "NODE renderD130 EACCES" in out
+        assert "ETC OPEN" in out and "UID 65534" in out
+        rep = json.load(open(os.path.join(b, "isolation.json")))
+        assert rep["tier"] == "landlock" and rep["landlock_rules"] > 0 and not rep["mount_ns"]
+        # exec into such a container: same restriction for the exec'd process
+        target = subprocess.Popen(["sleep", "30"], preexec_fn=_as_nobody)      # "the container" to enter
+        try:
+            r = subprocess.run([runc, "exec", "--pid", str(target.pid), "--landlock", f"{dri}:{mine}",
+                                "--", sys.executable, probe, dri], capture_output=True, text=True, timeout=30,
+                               preexec_fn=_as_nobody)
+        finally:
+            target.kill()
+            target.wait()
+        assert r.returncode == 0, r.stderr
+        assert "NODE renderD129 OPEN" in r.stdout and "NODE renderD130 EACCES" in r.stdout
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+
+
+@needs_landlock
+def test_landlock_tier_in_the_process_runtime(run, tmp_path):
+    """ProcessRuntime pinned to the Landlock tier: a GPU container (allocated stand-in node)
+    runs without namespaces, opens only its node, HIP_VISIBLE_DEVICES is left unset (the tier
+    enforces), exec_sync is restricted too, and isolation_status() names the tier."""
+    import shutil
+    import sys
+    base, dri = _ll_tree(tmp_path)
+    try:
+        rt = ProcessRuntime(str(tmp_path / "rt"), tier="landlock", landlock_dir=dri)
+        st = rt.isolation_status()
+        assert st["enforced"] and st["tier"] == "landlock" and "landlock" in st["message"]
+        probe = os.path.join(base, "probe.py")
+        with open(probe, "w") as f:
+            f.write(LL_PROBE + 'print("HIP", os.environ.get("HIP_VISIBLE_DEVICES", "unset"))\n')
+        pod = {"metadata": {"name": "p", "namespace": "default", "uid": "uid-ll"}, "spec": {}}
+
+        async def main():
+            sid = await rt.run_pod_sandbox(pod, {})
+            opts = RunContainerOptions(devices=[
+                {"pathOnHost": os.path.join(dri, "renderD130"), "pathInContainer": os.path.join(dri, "renderD130"),
+                 "permissions": "rw"}])
+            cid = await rt.create_container(sid, pod, {"name": "c", "image": "busybox",
+                                                       "command": [sys.executable, probe, dri]}, opts)
+            await rt.start_container(cid)
+            from kubernetes_amd.kubelet.runtime.base import RUNNING
+            import asyncio
+            for _ in range(200):
+                if rt.container_status(cid).state != RUNNING:
+                    break
+                await asyncio.sleep(0.05)
+            log = open(rt.container_status(cid).log_path).read()
+            assert "NODE renderD130 OPEN" in log and "NODE renderD128 EACCES" in log, log
+            assert "HIP unset" in log
+            assert rt.meta[cid]["spec"]["linux"]["namespaces"] == []
+            # a long-running container to exec into
+            cid2 = await rt.create_container(sid, pod, {"name": "s", "image": "busybox",
+                                                        "command": ["sleep", "30"]}, opts)
+            await rt.start_container(cid2)
+            rc, out = await rt.exec_sync(cid2, [sys.executable, probe, dri], 20)
+            assert rc == 0 and b"NODE renderD130 OPEN" in out and b"NODE renderD129 EACCES" in out, out
+            await rt.stop_container(cid2, 1)
+            await rt.stop_pod_sandbox(sid)
+            await rt.remove_pod_sandbox(sid)
+        run(main())
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+
+
+def test_tier_selection_and_condition_message(monkeypatch, tmp_path):
+    """auto: namespaces when available, else landlock, else none; the IsolationUnavailable
+    condition is only raised for tier none."""
+    monkeypatch.setitem(proc_rt._FEATURES, "", {"isolation": False, "namespace_error": "ENOSPC", "landlock": 4})
+    rt = ProcessRuntime(str(tmp_path / "a"))
+    assert rt.tier == "landlock" and rt.isolation_status()["enforced"]
+    monkeypatch.setitem(proc_rt._FEATURES, "", {"isolation": False, "namespace_error": "ENOSPC", "landlock": 0,
+                                                "landlock_error": "not supported"})
+    rt = ProcessRuntime(str(tmp_path / "b"))
+    st = rt.isolation_status()
+    assert rt.tier == "none" and not st["enforced"] and st["reason"] == "IsolationUnavailable"
+    assert "not supported" in st["message"]
+    with pytest.raises(ValueError):
+        ProcessRuntime(str(tmp_path / "c"), tier="landlock")
