@@ -195,7 +195,7 @@ def _rewrite_gv(body, canonical, served):
     return codec.dumpb(o)
 
 class APIServer:
-    def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None,
+    def __init__(self, store=None, admission_plugins=None, admission_config=None, token_file=None, etcd_tls=None,
                  tokens=None, authorization_modes=("AlwaysAllow",), max_requests_inflight=4000,
                  max_mutating_inflight=2000, storage_media_type=codec.PROTOBUF, watch_window=200_000,
                  kubelet_port_resolver=None, audit=None, encryption_config=None,
@@ -277,10 +277,21 @@ class APIServer:
             from ..storage.value import load_encryption_config
             self.transformers = (encryption_config if isinstance(encryption_config, dict)
                                  and "kind" not in encryption_config else load_encryption_config(encryption_config))
+        if store is None and os.environ.get("KAMD_APISERVER_DEFAULT_STORE"):
+            # test plumbing: run an unchanged suite against another backend (an etcd v3 endpoint:
+            # each API server under a key namespace of its own)
+            from ..storage.etcd3_client import is_etcd3_address
+            store = os.environ["KAMD_APISERVER_DEFAULT_STORE"]
+            if is_etcd3_address(store):
+                store += "#/kamd-" + secrets.token_hex(6)
         self.remote_address = store if isinstance(store, str) else None
-        self.rstore = None            # RemoteStore once started (shared mode)
+        self.etcd_tls = etcd_tls      # (cafile, certfile, keyfile) for an https etcd endpoint
+        self.rstore = None            # RemoteStore / Etcd3Store once started (shared mode)
         self.fanout = None            # FanoutClient: watches served by kamd-etcd (shared mode)
-        self.fanout_enabled = os.environ.get("KAMD_WATCH_FANOUT", "1") != "0"
+        from ..storage.etcd3_client import is_etcd3_address
+        # the socket hand-off fan-out is a kamd-etcd feature; an etcd endpoint serves plain watches
+        self.fanout_enabled = os.environ.get("KAMD_WATCH_FANOUT", "1") != "0" and \
+            not is_etcd3_address(self.remote_address)
         # `store or ...` would be wrong: an empty store has len() == 0 and is falsy
         self.store = None if self.remote_address else (store if store is not None else MVCCStore())
         self._applied_rev = 0
@@ -480,8 +491,8 @@ class APIServer:
     # ------------------------------------------------------------------
     # shared-store mode
     async def _start_remote(self):
-        from ..storage.remote import RemoteStore
-        self.rstore = await RemoteStore(self.remote_address).connect()
+        from ..storage.etcd3_client import connect_store
+        self.rstore = await connect_store(self.remote_address, self.etcd_tls)
         from ..storage.remote import FanoutClient
         self.fanout = FanoutClient.for_store(self.remote_address) if self.fanout_enabled else None
         self.uncached = self._uncached_resources()
@@ -658,7 +669,10 @@ class APIServer:
             if kv is None:
                 raise not_found(ri, name)
             return key, self._entry_from_kv(ri.plural, kv)
-        return self._existing(ri, namespace, name)
+        if self.rstore is None:
+            return self._existing(ri, namespace, name)
+        # shared store: a cache miss may only mean this worker lags the store
+        return await self._retrying(lambda: asyncio.sleep(0, self._existing(ri, namespace, name)), attempts=4)
 
     def _claim_keys(self, ri, obj):
         """Keys that must be absent in the store for `obj` to be written (shared mode): GPU device
@@ -684,6 +698,10 @@ class APIServer:
         cache = self.caches[ri.plural]
         sealed = ri.plural in self.transformers
         json_storage = self.storage_codec.media_type == codec.JSON and not sealed
+        if not json_storage and not sealed and self.storage_codec.media_type == codec.PROTOBUF:
+            from ..api import protobuf as _pbm
+            # kinds outside the protobuf schema (custom resources) are stored as JSON
+            json_storage = _pbm.message_of(obj) is None
         # value framing: [00 'K' 'H' | u32 len | index header (fields, labels) | object]
         hdr = codec.dumpb([cache.index_fields(obj), md.get("labels") or {}])
         frame = _FRAME + len(hdr).to_bytes(4, "little") + hdr
@@ -1783,7 +1801,7 @@ class APIServer:
         quantity label selectors): a store watch of its own, filtered here. Without the previous
         object state, a change that leaves the selector is reported as DELETED even if the
         client never had the object (informers ignore unknown deletes)."""
-        from ..storage.remote import RemoteStore
+        from ..storage.etcd3_client import connect_store
         ls = parse_labels(label_selector) if label_selector else None
         fs = parse_field_selector(field_selector) if field_selector else None
         prefix = m.prefix_for(ri, ns if ri.namespaced else None)
@@ -1794,7 +1812,7 @@ class APIServer:
                 (shard is None or shard_matches(e.fields, e.labels, *shard))
 
         async def run(writer):
-            st = await RemoteStore(server.remote_address).connect()
+            st = await connect_store(server.remote_address, server.etcd_tls)
             done = asyncio.get_running_loop().create_future()
             seen: dict = {}
             try:
@@ -1987,10 +2005,15 @@ class APIServer:
         async def probe(comp, url):
             if url is None:
                 try:
-                    ok = self.store is not None
+                    if self.rstore is not None:
+                        # shared / etcd store: it must answer, and this worker's watch be alive
+                        await asyncio.wait_for(self.rstore.revision(), 1.5)
+                        ok = self.store_healthy
+                    else:
+                        ok = self.store is not None
                     msg = '{"health": "true"}' if ok else "no store"
                 except Exception as e:  # noqa: BLE001
-                    ok, msg = False, str(e)
+                    ok, msg = False, str(e) or type(e).__name__
             else:
                 base, _, path = url.partition("/healthz")
                 c = HTTPClient(base, timeout=1.0)

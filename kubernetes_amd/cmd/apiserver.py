@@ -42,7 +42,9 @@ def _parser():
     ap.add_argument("--etcd-wal", default=None, help="durable WAL path for the store")
     ap.add_argument("--etcd-fan-threads", type=int, default=0,
                     help="watch fan-out threads of the shared native store (0 = KAMD_ETCD_FAN_THREADS or 1)")
-    ap.add_argument("--etcd-servers", default=None, help="shared native store address (unix://PATH or tcp://HOST:PORT)")
+    ap.add_argument("--etcd-servers", default=None,
+                    help="the store: an etcd v3 cluster (comma-separated http(s)://HOST:PORT endpoints) or the "
+                         "shared native store (unix://PATH or tcp://HOST:PORT)")
     ap.add_argument("--workers", type=int, default=1, help="API server worker processes sharing one native store")
     ap.add_argument("--reuse-port", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--max-requests-inflight", type=int, default=4000)
@@ -263,14 +265,18 @@ def _reference_flags(ap):
         g.add_argument(f, default="", help="accepted")
     g = ap.add_argument_group("storage")
     g.add_argument("--storage-backend", default="etcd3", choices=["etcd3"])
-    g.add_argument("--etcd-prefix", default="/registry", help="only /registry is supported")
+    g.add_argument("--etcd-prefix", default="/registry",
+                   help="key prefix in etcd: anything but /registry puts the keys under that namespace "
+                        "(etcd v3 endpoints only)")
     g.add_argument("--etcd-compaction-interval", default="5m", help="accepted; the store keeps a bounded history window")
     g.add_argument("--watch-cache", type=_bool, default=True, help="accepted; the watch cache is always on")
     g.add_argument("--watch-cache-sizes", default="", help="accepted; one window (--watch-cache-size) serves all resources")
     g.add_argument("--default-watch-cache-size", type=int, default=None, help="alias of --watch-cache-size")
-    for f in ("--storage-versions", "--storage-version", "--etcd-servers-overrides", "--etcd-cafile", "--etcd-certfile",
-              "--etcd-keyfile"):
+    for f in ("--storage-versions", "--storage-version", "--etcd-servers-overrides"):
         g.add_argument(f, default="")
+    g.add_argument("--etcd-cafile", default="", help="CA of an https etcd endpoint")
+    g.add_argument("--etcd-certfile", default="", help="client certificate for an https etcd endpoint")
+    g.add_argument("--etcd-keyfile", default="", help="client key for an https etcd endpoint")
     g.add_argument("--etcd-quorum-read", type=_bool, default=True, help="accepted; the store is linearizable")
     g.add_argument("--deserialization-cache-size", type=int, default=0, help="accepted")
     g.add_argument("--delete-collection-workers", type=int, default=1, help="accepted")
@@ -289,11 +295,13 @@ def _reference_flags(ap):
 def _reference_kwargs(a):
     if a.cloud_provider:
         raise SystemExit(f"kube-apiserver: --cloud-provider={a.cloud_provider}: cloud providers are out of scope here")
-    if a.etcd_prefix.rstrip("/") != "/registry":
-        raise SystemExit("kube-apiserver: only --etcd-prefix=/registry is supported")
-    if a.etcd_cafile or a.etcd_certfile or a.etcd_keyfile:
+    from ..storage.etcd3_client import is_etcd3_address
+    etcd3 = is_etcd3_address(a.etcd_servers or "")
+    if a.etcd_prefix.rstrip("/") != "/registry" and not etcd3:
+        raise SystemExit("kube-apiserver: --etcd-prefix other than /registry needs an etcd v3 endpoint in --etcd-servers")
+    if (a.etcd_cafile or a.etcd_certfile or a.etcd_keyfile) and not etcd3:
         raise SystemExit("kube-apiserver: the kamd-etcd protocol has no TLS; reach the store over a unix socket "
-                         "or a loopback/cluster-private TCP port")
+                         "or a loopback/cluster-private TCP port (TLS flags apply to https etcd endpoints)")
     rh = None
     if a.requestheader_client_ca_file:
         rh = {"client_ca_file": a.requestheader_client_ca_file, "allowed_names": _csv(a.requestheader_allowed_names),
@@ -329,6 +337,13 @@ def main(argv=None):
 
     async def start():
         store = a.etcd_servers
+        etcd_tls = None
+        from ..storage.etcd3_client import is_etcd3_address
+        if store and is_etcd3_address(store):
+            if a.etcd_prefix.rstrip("/") != "/registry":
+                store = store.split("#", 1)[0] + "#" + a.etcd_prefix.rstrip("/")
+            if a.etcd_cafile or a.etcd_certfile or a.etcd_keyfile:
+                etcd_tls = (a.etcd_cafile or None, a.etcd_certfile or None, a.etcd_keyfile or None)
         if store is None and a.storage_engine == "native":
             try:
                 from ..storage.native_store import NativeMVCCStore
@@ -353,7 +368,7 @@ def main(argv=None):
                     "username_claim": a.oidc_username_claim, "username_prefix": a.oidc_username_prefix,
                     "groups_claim": a.oidc_groups_claim, "groups_prefix": a.oidc_groups_prefix, "ca_file": a.oidc_ca_file,
                     "required_claims": dict(x.split("=", 1) for x in a.oidc_required_claim)}
-        s = APIServer(store=store, admission_plugins=plugins, admission_config=adm_cfg, token_file=a.token_auth_file,
+        s = APIServer(store=store, etcd_tls=etcd_tls, admission_plugins=plugins, admission_config=adm_cfg, token_file=a.token_auth_file,
                       authorization_modes=a.authorization_mode.split(","), storage_media_type=a.storage_media_type,
                       max_requests_inflight=a.max_requests_inflight,
                       max_mutating_inflight=a.max_mutating_requests_inflight, watch_window=a.default_watch_cache_size or a.watch_cache_size,

@@ -18,9 +18,11 @@ pkg/storage/etcd3`, wire schema `vendor/github.com/coreos/etcd/etcdserver/etcdse
 Txn atomicity: the compares are evaluated on a read of their keys, and the chosen branch commits
 in ONE store transaction guarded by the mod revisions that read saw (absent keys guarded as
 absent); a concurrent change fails the guard and the Txn is re-evaluated — the same outcome as
-etcd's serialized Txn for the keys it compares. Reads at a past `revision` are not supported
-(the store serves its current state; history is available through Watch from a start revision
->= 2: the store's watch replays events after `start_revision - 1`, and 0 means "from now").
+etcd's serialized Txn for the keys it compares. Range at a past `revision` is served by the
+store (its retained history undone from the current state): "required revision has been
+compacted" below it, "required revision is a future revision" above the current one. Watch
+replays events after `start_revision - 1` (0 = from now); `prev_kv` is filled for DELETE events
+(the deleted key's last value, as clientv3 users such as the API server's watcher expect).
 """
 from __future__ import annotations
 
@@ -200,21 +202,28 @@ class EtcdV3Gateway:
                              version=kv.version, value=b"" if keys_only else kv.value, lease=lease)
 
     # -- reads ------------------------------------------------------------------------------------
-    async def _range_kvs(self, key: bytes, end: bytes):
-        if not end:
+    async def _range_kvs(self, key: bytes, end: bytes, revision=0):
+        if not end and not revision:
             kv = await self.store.get(key.decode())
             return [kv] if kv is not None else []
+        if not end:
+            kvs, _more, _rev = await self.store.range(key.decode(errors="surrogateescape"), revision=revision)
+            return [kv for kv in kvs if kv.key.encode() == key]
         prefix = key if end == b"\x00" else _common_prefix(key, end)
-        kvs, _more, _rev = await self.store.range(prefix.decode(errors="surrogateescape"))
+        kvs, _more, _rev = await self.store.range(prefix.decode(errors="surrogateescape"), revision=revision)
         return [kv for kv in kvs if _in_range(kv.key.encode(), key, end)]
 
     async def Range(self, req, ctx):
-        if req.revision:
-            rev = await self.store.revision()
-            if req.revision != rev:
-                await ctx.abort(grpc.StatusCode.UNIMPLEMENTED,
-                                "etcdserver: reads at a past revision are not supported by this store (use Watch)")
-        kvs = await self._range_kvs(req.key, req.range_end)
+        rev = await self.store.revision()
+        at = 0
+        if req.revision and req.revision < rev:
+            at = req.revision
+        elif req.revision > rev:
+            await ctx.abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision is a future revision")
+        try:
+            kvs = await self._range_kvs(req.key, req.range_end, at)
+        except CompactedError:
+            await ctx.abort(grpc.StatusCode.OUT_OF_RANGE, "etcdserver: mvcc: required revision has been compacted")
         kvs = [kv for kv in kvs if (not req.min_mod_revision or kv.mod_rev >= req.min_mod_revision)
                and (not req.max_mod_revision or kv.mod_rev <= req.max_mod_revision)
                and (not req.min_create_revision or kv.create_rev >= req.min_create_revision)
@@ -227,7 +236,7 @@ class EtcdV3Gateway:
         more = bool(req.limit) and count > req.limit
         if req.limit:
             kvs = kvs[:req.limit]
-        return M["RangeResponse"](header=await self._header(), count=count, more=more,
+        return M["RangeResponse"](header=await self._header(at or None), count=count, more=more,
                                   kvs=[] if req.count_only else [self._kv(kv, req.keys_only) for kv in kvs])
 
     # -- writes -------------------------------------------------------------------------------------
@@ -348,6 +357,9 @@ class EtcdV3Gateway:
             prefix = start if end == b"\x00" else (_common_prefix(start, end) if end else start)
             filters = set(cr.filters)
             active[wid] = (start, end)
+            # replayed events can arrive before the store's watch reply is processed: hold them
+            # until `created` is out (etcd sends `created` first)
+            held = []
 
             def cb(t, kv):
                 if t is None or wid not in active or t == wire.PROGRESS:
@@ -359,20 +371,34 @@ class EtcdV3Gateway:
                     return
                 ev = M["Event"](type=etype, kv=self._kv(kv))
                 if etype == DELETE:
+                    if cr.prev_kv:
+                        # the store's delete event carries the key's last value
+                        ev.prev_kv.CopyFrom(self._kv(kv))
+                        ev.prev_kv.version = max(1, kv.version)
                     ev.kv.value = b""
-                out.put_nowait(M["WatchResponse"](header=M["ResponseHeader"](
+                    ev.kv.version = 0
+                    ev.kv.create_revision = 0
+                resp = M["WatchResponse"](header=M["ResponseHeader"](
                     cluster_id=CLUSTER_ID, member_id=MEMBER_ID, revision=kv.mod_rev, raft_term=1),
-                    watch_id=wid, events=[ev]))
+                    watch_id=wid, events=[ev])
+                if held is not None:
+                    held.append(resp)
+                else:
+                    out.put_nowait(resp)
             try:
                 rev = await conn.watch(prefix.decode(errors="surrogateescape"),
                                        max(0, cr.start_revision - 1) if cr.start_revision else 0, cb)
                 out.put_nowait(M["WatchResponse"](header=await self._header(rev), watch_id=wid, created=True))
+                pending, held = held, None
+                for resp in pending:
+                    out.put_nowait(resp)
             except CompactedError:
                 active.pop(wid, None)
-                out.put_nowait(M["WatchResponse"](header=await self._header(), watch_id=wid, created=True))
-                # the compaction point the client must resume from (the store's compaction
-                # revision when this gateway performed it; at least the requested start)
-                out.put_nowait(M["WatchResponse"](header=await self._header(), watch_id=wid, canceled=True,
+                # created and canceled at once, with the compaction point the client must resume
+                # from (the store's compaction revision when this gateway performed it; at least
+                # the requested start)
+                out.put_nowait(M["WatchResponse"](header=await self._header(), watch_id=wid, created=True,
+                                                  canceled=True,
                                                   compact_revision=max(self.compacted, cr.start_revision)))
         task = asyncio.ensure_future(reader())
         try:

@@ -159,7 +159,19 @@ class RemoteStore:
             return None
         return wire.decode_kv(p)[0]
 
-    async def range(self, prefix, limit=0, start_after=None):
+    async def range(self, prefix, limit=0, start_after=None, revision=0):
+        """(kvs, more, revision). `revision` > 0 reads the keys as they were at that revision
+        (CompactedError below the retained history, StoreError for a future revision)."""
+        if revision:
+            payload = wire.encode_range(prefix, limit, start_after) + struct.pack("<q", revision)
+            _, fut = self._send(wire.RANGE_AT, payload)
+            st, p = await fut
+            if st == wire.COMPACTED:
+                raise CompactedError(revision)
+            if st != wire.OK:
+                raise StoreError(f"revision {revision} is a future revision" if st == wire.BAD and p else
+                                 f"range at {revision} failed with status {st}")
+            return wire.decode_range(p)
         _, fut = self._send(wire.RANGE, wire.encode_range(prefix, limit, start_after))
         st, p = await fut
         return wire.decode_range(p)

@@ -14,7 +14,7 @@ CMP_MOD_REV, CMP_EXISTS, CMP_ABSENT, CMP_VALUE = 0, 1, 2, 3
 # op kinds
 OP_PUT, OP_DELETE, OP_PUT_INJECT, OP_DELETE_TOMBSTONE = 0, 1, 2, 3
 # request ops
-TXN, GET, RANGE, WATCH, REV, COMPACT = 1, 2, 3, 4, 5, 6
+TXN, GET, RANGE, WATCH, REV, COMPACT, RANGE_AT = 1, 2, 3, 4, 5, 6, 7
 # statuses
 OK, FAILED, COMPACTED, NOT_FOUND, EVENT, BAD, PROGRESS = 0, 1, 3, 4, 8, 9, 10
 

@@ -228,6 +228,35 @@ class Engine {
     return rev_;
   }
 
+  // the keys with `prefix` as they were at revision `at` (etcd Range with `revision`): the current
+  // state with every later event undone, newest first — each event keeps the state before it.
+  // False when `at` is older than the retained history (compacted).
+  bool range_at(const std::string& prefix, int64_t at, uint32_t limit, const std::string& start_after,
+                std::vector<std::pair<std::string, std::shared_ptr<KV>>>* out, bool* more) const {
+    if (at < compact_rev_) return false;
+    std::map<std::string, std::shared_ptr<KV>> st;
+    for (auto it = data_.lower_bound(prefix); it != data_.end(); ++it) {
+      if (it->first.compare(0, prefix.size(), prefix) != 0) break;
+      st.emplace(it->first, it->second);
+    }
+    for (size_t i = hist_.size(); i-- > 0 && hist_[i].rev > at;) {
+      const Event& e = hist_[i];
+      if (e.key.compare(0, prefix.size(), prefix) != 0) continue;
+      if (e.prev) st[e.key] = e.prev;
+      else st.erase(e.key);
+    }
+    *more = false;
+    auto it = start_after.empty() ? st.lower_bound(prefix) : st.upper_bound(start_after);
+    for (; it != st.end(); ++it) {
+      if (limit && out->size() >= limit) {
+        *more = true;
+        break;
+      }
+      out->push_back(*it);
+    }
+    return true;
+  }
+
   // events with rev > from; false if compacted
   bool since(int64_t from, const std::string& prefix, std::vector<const Event*>* out) const {
     if (from < compact_rev_) return false;
@@ -1380,6 +1409,27 @@ class Server {
         w.put<uint8_t>(more ? 1 : 0);
         w.put<uint32_t>((uint32_t)res.size());
         for (auto& kv : res) w.kv(*kv.first, *kv.second);
+        reply(c, id, 0, w.b);
+        return;
+      }
+      case 7: {  // RANGE at a past revision: prefix, limit, start_after, revision
+        std::string prefix = r.str();
+        uint32_t limit = r.get<uint32_t>();
+        std::string sa = r.str();
+        int64_t at = r.get<int64_t>();
+        if (!r.ok) { reply(c, id, 9, ""); return; }
+        if (at > eng_->rev()) { w.put<int64_t>(eng_->rev()); reply(c, id, 9, w.b); return; }   // future
+        std::vector<std::pair<std::string, std::shared_ptr<KV>>> res;
+        bool more;
+        if (!eng_->range_at(prefix, at, limit, sa, &res, &more)) {
+          w.put<int64_t>(eng_->compacted());
+          reply(c, id, 3, w.b);
+          return;
+        }
+        w.put<int64_t>(at);
+        w.put<uint8_t>(more ? 1 : 0);
+        w.put<uint32_t>((uint32_t)res.size());
+        for (auto& kv : res) w.kv(kv.first, *kv.second);
         reply(c, id, 0, w.b);
         return;
       }
