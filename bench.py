@@ -95,37 +95,53 @@ def cpu_budget():
     return n
 
 
+# Per-pod host CPU of each control-plane component at the N=1 headline rate, measured by the
+# driver's own run (BENCH_r03 `cpu_ms_per_pod`: API server 0.98 ms, scheduler 0.56 ms, hollow
+# kubelets 1.64 ms per pod at 2727 pods/s). A whole node sizes each component for the load of
+# `world` ranks at that rate, at most ~70 % busy, instead of a fixed-size control plane.
+N1_RATE_PODS_PER_S = 2800.0
+CPU_MS_PER_POD = {"apiserver": 0.98, "scheduler": 0.56, "hollow": 1.64}
+TARGET_UTIL = 0.7
+
+
+def demand(component, world):
+    """Processes `component` needs so that `world` ranks at the N=1 rate keep it <= 70 % busy."""
+    import math
+    return max(1, math.ceil(world * N1_RATE_PODS_PER_S * CPU_MS_PER_POD[component] / 1000.0 / TARGET_UTIL))
+
+
 def control_plane_shape(world, workers=0, shards=0):
     """API server workers and scheduler shards for `world` ranks (0 = auto).
 
-    Measured on a 16-CPU MI355X box (profiles/r2_partitioned: n1_shapes, scale_r2d): since API
-    workers read pods from the store instead of caching every pod event, 2 workers + 2
-    partitioned scheduler shards beat the single in-process-store API server already at N=1
-    (1946-2086 vs 1574-1793 pods/s, p99 19 vs 62-90 ms); N=4: w=4 s=4 3184 vs w=4 s=2 2727.
-    On a whole 8-GPU node (>= 64 CPUs) the control plane grows with the rank count — two API
-    server workers (up to 16) and one scheduler shard (up to 8) per rank — so per-rank work (weak
-    scaling) is met by per-rank control-plane capacity instead of a fixed-size control plane."""
+    Small boxes (< 64 CPUs, e.g. the 16-CPU MI355X CI lease) keep the measured shapes
+    (profiles/r2_partitioned: n1_shapes, scale_r2d; profiles/r2_density_clients/worker_sweep):
+    N=1 w=3 s=2 (2594-2611 pods/s; w=2 2363-2389, w=4 2380-2462), N=4 w=4 s=4 (3184 vs w=4 s=2
+    2727). A whole 8-GPU node (>= 64 CPUs) is sized from the per-pod CPU of each component
+    (`demand`): at N=8 that is 32 API workers and 18 scheduler shards — ceilings of ~32.6 k and
+    ~32 k pods/s against the 22.4 k that linear weak scaling needs (the round-3 caps of 16 / 8
+    capped it at ~14 k) — scaled down together with the hollow-node processes when the CPU
+    budget is smaller (`cpus - ranks - store threads`)."""
     cpus = cpu_budget()
     spare = cpus - world - 1
     big = cpus >= 64
+    if big:
+        want_w, want_s = demand("apiserver", world), demand("scheduler", world)
+        want_h = demand("hollow", world)
+        budget = max(4, spare - 2)                         # 2: the store's commit + fan-out threads
+        scale = min(1.0, budget / float(want_w + want_s + want_h))
+        if workers <= 0:
+            workers = max(3, int(want_w * scale))
+        if shards <= 0:
+            shards = max(2, int(want_s * scale))
+        return workers, shards
     if workers <= 0:
         if spare < 3:
             workers = 1
-        elif big:
-            # API workers are the per-pod cost that grows with the rank count (~0.7-0.9 ms of
-            # worker CPU per pod vs ~0.4-0.6 scheduler, 0.06-0.14 store): two per rank, up to 16.
-            # The store is not the limit there: kubemark/store_bench.py measures its busiest
-            # thread at 0.03-0.04 ms per pod (ceiling > 24k pods/s with 68 watches).
-            workers = min(16, max(3, 2 * world), max(1, spare // 5))
         else:
-            # N=1, 16-CPU box (profiles/r2_density_clients/worker_sweep): w=3 2594-2611 pods/s,
-            # w=2 2363-2389, w=4 2380-2462
             workers = 3 if world == 1 else 2 if world < 4 else 4
     if shards <= 0:
         if spare < 3:
             shards = 1
-        elif big:
-            shards = min(8, max(2, world), max(1, spare // 6))
         else:
             shards = 2 if world < 4 else 4
     return workers, shards
@@ -133,18 +149,21 @@ def control_plane_shape(world, workers=0, shards=0):
 
 def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
     """Hollow-node processes per rank (0 = auto): kubemark runs one process per hollow node;
-    here the rank's nodes are spread over up to 4 processes so kubelet work uses several cores,
+    here the rank's nodes are spread over several processes so kubelet work uses several cores,
     bounded by the CPUs left after ranks and the control plane."""
     if want > 0:
         return max(1, min(want, nodes_per_rank))
-    # hollow kubelets are mostly waiting on the control plane: mild oversubscription pays
-    # (profiles/r2_hollow_procs, r2_scale: N=4 on 16 CPUs 1868 -> 2578 pods/s with 2 per rank)
     cpus = cpu_budget()
     spare = cpus - workers - shards - 1
-    # a whole node (>= 64 CPUs) gets up to one process per hollow node, as kubemark runs them:
-    # at ~1.2-1.4 ms of kubelet CPU per pod, 4 processes per rank would run near saturation at
-    # the N=1 rate (N=1 on the 16-CPU box: 6 processes 2601-2693 vs 4 processes 2583-2590 pods/s)
-    cap = 8 if cpus >= 64 else 6 if world == 1 else 4
+    if cpus >= 64:
+        # a whole node: the hollow kubelets' share of the per-pod demand model, per rank
+        # (~7 processes per rank at 1.64 ms per pod), within the CPUs left
+        per_rank = -(-demand("hollow", world) // world)
+        return max(1, min(nodes_per_rank, per_rank, max(2, (spare - world) // max(1, world))))
+    # hollow kubelets are mostly waiting on the control plane: mild oversubscription pays
+    # (profiles/r2_hollow_procs, r2_scale: N=4 on 16 CPUs 1868 -> 2578 pods/s with 2 per rank;
+    # N=1 on the 16-CPU box: 6 processes 2601-2693 vs 4 processes 2583-2590 pods/s)
+    cap = 6 if world == 1 else 4
     return max(1, min(nodes_per_rank, cap, max(2, spare // max(1, world))))
 
 

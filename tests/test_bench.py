@@ -77,9 +77,10 @@ def test_bench_gpus_mismatch_fails():
 
 def test_bench_eight_ranks_whole_node_shape():
     """The N=8 path the driver runs on a whole MI355X node, rehearsed with gloo on CPU: 8 ranks
-    under torch.distributed.run with the >= 64-CPU control-plane shape (KAMD_BENCH_CPUS=128:
-    16 API server workers, 8 scheduler shards) and small per-rank work."""
-    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1", KAMD_BENCH_CPUS="128")
+    under torch.distributed.run with the >= 64-CPU control-plane shape (KAMD_BENCH_CPUS=64:
+    the demand model scaled to that budget — 16 API server workers, 9 scheduler shards) and
+    small per-rank work."""
+    env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1", KAMD_BENCH_CPUS="64")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
                         "--master-addr", "127.0.0.1", "--master-port", "29747", "bench.py", "--gpus", "8",
                         "--steps", "2", "--warmup", "1", "--nodes-per-rank", "1", "--xgmi4-steps", "0"],
@@ -89,7 +90,7 @@ def test_bench_eight_ranks_whole_node_shape():
     _check(d, 8, 2, 1)
     assert d["config"]["parallelism"] == "ranks8" and d["config"]["hollow_nodes"] == 8
     assert d["config"]["global_batch"] == 64
-    assert d["config"]["apiserver_workers"] == 16 and d["config"]["scheduler_shards"] == 8
+    assert d["config"]["apiserver_workers"] == 16 and d["config"]["scheduler_shards"] == 9
 
 
 def test_payload_server_batches_starts(run, tmp_path):
@@ -129,14 +130,23 @@ def test_payload_server_batches_starts(run, tmp_path):
 
 
 def test_control_plane_shape_grows_with_ranks_on_a_big_node(monkeypatch):
+    """Whole node: each component sized for world x the N=1 rate at <= 70 % busy from its
+    measured per-pod CPU; the ceilings (processes / ms per pod) exceed linear weak scaling."""
     import bench
     monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
-    assert bench.control_plane_shape(1) == (3, 2)          # N=1 keeps the measured small shape
-    assert bench.control_plane_shape(4) == (8, 4)
-    assert bench.control_plane_shape(8) == (16, 8)
+    assert bench.control_plane_shape(1) == (4, 3)
+    assert bench.control_plane_shape(4) == (16, 9)
+    w, s = bench.control_plane_shape(8)
+    assert (w, s) == (32, 18)
+    need = 8 * bench.N1_RATE_PODS_PER_S
+    assert w / bench.CPU_MS_PER_POD["apiserver"] * 1000 > need
+    assert s / bench.CPU_MS_PER_POD["scheduler"] * 1000 > need
+    h = bench.hollow_procs_for(8, 100, w, s)
+    assert 8 * h / bench.CPU_MS_PER_POD["hollow"] * 1000 > need
+    assert 8 + w + s + 8 * h + 2 <= 192
     monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
     w, s = bench.control_plane_shape(8)
-    assert w <= 11 and s <= 9
+    assert 8 + w + s + 8 * bench.hollow_procs_for(8, 100, w, s) + 2 <= 64 + 8   # scaled to the budget
     monkeypatch.setattr(bench, "cpu_budget", lambda: 16)
     assert bench.control_plane_shape(1) == (3, 2) and bench.control_plane_shape(4) == (4, 4)
 
@@ -154,9 +164,10 @@ def test_store_bench_small():
 def test_hollow_procs_per_rank(monkeypatch):
     import bench
     monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
-    assert bench.hollow_procs_for(8, 8, 16, 8) == 8          # a whole node: one per hollow node
+    assert bench.hollow_procs_for(8, 100, 32, 18) == 7       # a whole node: the demand model
+    assert bench.hollow_procs_for(8, 4, 32, 18) == 4         # never more than the rank's nodes
     monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
-    assert bench.hollow_procs_for(8, 8, 11, 8) == 5          # bounded by the spare CPUs
+    assert bench.hollow_procs_for(8, 100, 16, 9) == 3        # bounded by the spare CPUs
     monkeypatch.setattr(bench, "cpu_budget", lambda: 16)
     assert bench.hollow_procs_for(1, 8, 3, 2) == 6 and bench.hollow_procs_for(2, 8, 2, 2) == 4
     assert bench.hollow_procs_for(1, 8, 3, 2, want=3) == 3
