@@ -456,3 +456,36 @@ def test_tier_selection_and_condition_message(monkeypatch, tmp_path):
     assert "not supported" in st["message"]
     with pytest.raises(ValueError):
         ProcessRuntime(str(tmp_path / "c"), tier="landlock")
+
+
+@pytest.mark.gpu
+def test_landlock_enforced_on_this_host(tmp_path):
+    """On the GPU box itself (unprivileged, no user namespaces: the Landlock tier): kamd-runc,
+    as this non-root user, confines a container to its allowed entries of a restricted tree.
+    Regular files stand in for render nodes (an unprivileged user cannot mknod); Landlock
+    checks opens the same way for both. The real /dev/dri of a one-GPU lease holds only the
+    allocated node, so this is where denial is shown non-vacuously."""
+    import sys
+    f = runc_features()
+    if f.get("tier") != "landlock":
+        pytest.skip(f"this host's tier is {f.get('tier')}, not landlock: {f}")
+    base = tmp_path / "ll"
+    dri = base / "dri"
+    dri.mkdir(parents=True)
+    for n in ("renderD128", "renderD129", "card0"):
+        (dri / n).write_text("x")
+    probe = base / "probe.py"
+    probe.write_text(LL_PROBE)
+    b = base / "bundle"
+    b.mkdir()
+    spec = {"process": {"args": [sys.executable, str(probe), str(dri)], "env": ["PATH=/usr/bin:/bin"], "cwd": "/"},
+            "root": {"path": "/"}, "mounts": [],
+            "annotations": {"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": str(dri)},
+            "linux": {"devices": [{"path": str(dri / "renderD129")}], "namespaces": []}}
+    (b / "config.json").write_text(json.dumps(spec))
+    r = subprocess.run([proc_rt.KAMD_RUNC, "run", "--bundle", str(b)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "NODE renderD129 OPEN" in r.stdout, r.stdout
+    assert "NODE renderD128 EACCES" in r.stdout and "NODE card0 EACCES" in r.stdout, r.stdout
+    rep = json.loads((b / "isolation.json").read_text())
+    assert rep["tier"] == "landlock"
