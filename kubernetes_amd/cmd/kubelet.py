@@ -179,7 +179,7 @@ def main(argv=None):
                     eviction_pressure_transition_period=_duration(a.eviction_pressure_transition_period),
                     allocatable_ignore_eviction=a.experimental_allocatable_ignore_eviction,
                     serialize_image_pulls=a.serialize_image_pulls, registry_qps=a.registry_qps,
-                    registry_burst=a.registry_burst, file_check_frequency=_duration(a.file_check_frequency),
+                    registry_burst=a.registry_burst, file_check_frequency=_duration(a.file_check_frequency), sync_frequency=_duration(a.sync_frequency),
                     http_check_frequency=_duration(a.http_check_frequency), register=a.register_node)
         if not a.anonymous_auth or a.authentication_token_webhook or a.authorization_mode != "AlwaysAllow" or a.client_ca_file:
             from ..kubelet.server_auth import KubeletAuth
@@ -330,7 +330,9 @@ def _reference_flags(ap):
     g.add_argument("--image-service-endpoint", default="")
     g.add_argument("--file-check-frequency", default="20s")
     g.add_argument("--http-check-frequency", default="20s")
-    g.add_argument("--sync-frequency", default="1m", help="accepted; pods resync on every watch event and status loop")
+    g.add_argument("--sync-frequency", default="1m",
+                   help="period of the pod sync that re-projects configMap/secret/downwardAPI/projected volumes "
+                        "(pod changes themselves resync on every watch event)")
     g = ap.add_argument_group("API client")
     g.add_argument("--kube-api-qps", type=float, default=5.0)
     g.add_argument("--kube-api-burst", type=int, default=10)

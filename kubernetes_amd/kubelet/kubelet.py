@@ -51,6 +51,14 @@ _ip_counter = itertools.count(2)
 BOOTSTRAP_CHECKPOINT = "node.kubernetes.io/bootstrap-checkpoint"
 
 
+_REF = __import__("re").compile(r"\$\$|\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
+
+
+def _expand_ref(s, env):
+    """`third_party/forked/golang/expansion`: $(VAR) -> env value (kept when undefined), $$ -> $."""
+    return _REF.sub(lambda m: "$" if m.group(0) == "$$" else env.get(m.group(1), m.group(0)), str(s))
+
+
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
                  "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
@@ -113,8 +121,11 @@ class Kubelet:
                  host_sources=None, eviction_soft=None, eviction_soft_grace_period=None, eviction_minimum_reclaim=None,
                  eviction_max_pod_grace_period=0, eviction_pressure_transition_period=0.0,
                  allocatable_ignore_eviction=False, serialize_image_pulls=False, registry_qps=0.0, registry_burst=10,
-                 file_check_frequency=20.0, http_check_frequency=20.0):
+                 file_check_frequency=20.0, http_check_frequency=20.0, sync_frequency=60.0):
         self.file_check_frequency, self.http_check_frequency = file_check_frequency, http_check_frequency
+        # --sync-frequency: how often running pods' configMap / secret / downwardAPI / projected
+        # volumes are re-projected (`kubelet.go` syncLoop's periodic sync, 1m)
+        self.sync_frequency = sync_frequency
         self.client = client
         # :10250 serving (cmd/kubelet/app/server.go): TLS = (cert file, key file, client CA file or
         # None) or None for plain HTTP; --read-only-port (unauthenticated, no debugging handlers)
@@ -300,6 +311,8 @@ class Kubelet:
         self.informer.add_handler(self._on_add, self._on_update, self._on_delete)
         self.informer.start()
         self._tasks.append(asyncio.ensure_future(self._node_status_loop()))
+        if self.sync_frequency and self.sync_frequency > 0:
+            self._tasks.append(asyncio.ensure_future(self._volume_sync_loop()))
         await self.informer.wait_synced(60)
         if self._adoptable:
             self._tasks.append(asyncio.ensure_future(self._remove_orphans(self.orphan_grace)))
@@ -413,7 +426,10 @@ class Kubelet:
                  {"type": "Ready", "status": "False", "reason": "KubeletNotReady",
                   "message": f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady message:{net_err}",
                   "lastHeartbeatTime": now, "lastTransitionTime": now})
-        st = {"capacity": capacity, "allocatable": self._allocatable(capacity),
+        alloc = self._allocatable(capacity)
+        self.volumes.allocatable = alloc        # downward API: a missing limit reads as allocatable
+        self.volumes.host_ip = self.node_ip or self.address
+        st = {"capacity": capacity, "allocatable": alloc,
               "conditions": [
                   ready,
                   {"type": "MemoryPressure", "status": "True" if mem_p else "False",
@@ -1086,6 +1102,12 @@ class Kubelet:
                 self.recorder.event(st.pod, "Warning", "Failed", f"Error: {e}")
                 asyncio.get_running_loop().call_later(2.0, self._resync, st.uid)
                 return None
+        if any("$(" in str(x) for x in (spec_c.get("command") or []) + (spec_c.get("args") or [])):
+            # `kubecontainer.ExpandContainerCommandAndArgs`: $(VAR) from the container's resolved
+            # environment; unknown references stay as written, $$ escapes
+            envmap = {e["name"]: str(e.get("value", "")) for e in spec_c.get("env") or () if "value" in e}
+            spec_c = dict(spec_c, command=[_expand_ref(x, envmap) for x in spec_c.get("command") or ()],
+                          args=[_expand_ref(x, envmap) for x in spec_c.get("args") or ()])
         if self.cpu_manager is not None:
             from .cpumanager import format_cpulist
             try:
@@ -1136,6 +1158,24 @@ class Kubelet:
                 if n is not None and str(n).isdigit():
                     out.add(int(n))
         return tuple(sorted(out))
+
+    _PROJECTED = ("configMap", "secret", "downwardAPI", "projected")
+
+    async def _volume_sync_loop(self):
+        """Periodic pod sync of projected volumes: ConfigMap / Secret updates (and optional
+        sources appearing), label / annotation changes reach running containers' files."""
+        while True:
+            await asyncio.sleep(self.sync_frequency)
+            for st in list(self.pods.values()):
+                if st.terminated or not st.volumes:
+                    continue
+                vols = (st.pod.get("spec") or {}).get("volumes") or ()
+                if not any(k in v for v in vols for k in self._PROJECTED):
+                    continue
+                try:
+                    await self.volumes.refresh(st.pod, self.node_name, st.ip)
+                except (VolumeError, APIStatusError, OSError) as e:
+                    log.debug("volume refresh of %s failed: %s", st.pod["metadata"].get("name"), e)
 
     def _resync(self, uid):
         st = self.pods.get(uid)

@@ -122,10 +122,18 @@ IMAGES = {
     "kubernetes-amd/xgmi-probe": [os.path.join(BIN_DIR, "xgmi-probe")],
     "kubernetes-amd/pause": [os.path.join(BIN_DIR, "pause")],
     "busybox": ["/bin/sh"],
+    # the e2e image of `test/e2e/common/docker_containers.go`: an ENTRYPOINT and a CMD
+    "kubernetes-amd/entrypoint-tester": ["/bin/echo", "entrypoint"],
+}
+# image CMD (default arguments), used only when the container sets neither command nor args
+IMAGE_CMD = {
+    "kubernetes-amd/entrypoint-tester": ["default", "arguments"],
 }
 
 
 def resolve_command(container):
+    """ENTRYPOINT/CMD semantics (`pkg/kubelet/kuberuntime` + docker): `command` replaces the
+    image's entrypoint AND drops its CMD; `args` alone replaces the CMD; neither runs both."""
     cmd = list(container.get("command") or [])
     args = list(container.get("args") or [])
     if not cmd:
@@ -134,6 +142,8 @@ def resolve_command(container):
         cmd = list(IMAGES.get(base, []))
         if not cmd:
             raise FileNotFoundError(f"image {img!r} has no local entrypoint and no command was given")
+        if not args:
+            args = list(IMAGE_CMD.get(base, []))
     return cmd + args
 
 

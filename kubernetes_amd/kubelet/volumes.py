@@ -53,24 +53,61 @@ def _rmtree_no_mounts(path, mounter):
             pass
 
 
-def _write_files(d, data: dict, items=None, mode=0o644, binary=False):
+def _write_files(d, data: dict, items=None, mode=0o644, binary=False, optional=False) -> set:
+    """Project `data` into files under d: every key, or `items` ({key, path, mode}) — an item's
+    own `mode` beats `defaultMode` (`pkg/volume/util/atomic_writer.go` payloads). A file is only
+    rewritten when its content or mode changed (atomic rename). Returns the relative paths."""
     os.makedirs(d, exist_ok=True)
-    keys = {i["key"]: i.get("path", i["key"]) for i in items} if items else {k: k for k in data}
-    for k, rel in keys.items():
+    if items:
+        keys = [(i["key"], i.get("path", i["key"]), i.get("mode")) for i in items]
+    else:
+        keys = [(k, k, None) for k in data]
+    out = set()
+    for k, rel, item_mode in keys:
         if k not in data:
+            if optional:
+                continue
             raise VolumeError(f"key {k!r} not found")
         p = os.path.join(d, rel)
         os.makedirs(os.path.dirname(p), exist_ok=True)
         v = data[k]
         raw = base64.b64decode(v) if binary else str(v).encode()
+        want = int(item_mode) if item_mode is not None else mode
+        out.add(rel)
+        try:
+            st = os.stat(p)
+            with open(p, "rb") as f:
+                if f.read() == raw and (st.st_mode & 0o7777) == want:
+                    continue
+        except OSError:
+            pass
         tmp = p + ".tmp"
         with open(tmp, "wb") as f:
             f.write(raw)
-        os.chmod(tmp, mode)
+        os.chmod(tmp, want)
         os.replace(tmp, p)
+    return out
 
 
-def _field(pod, path, node_name=None, pod_ip=None):
+def _prune(d, keep: set):
+    """Remove projected files no longer in the payload (a key deleted from its ConfigMap, an
+    optional source that went away)."""
+    for root, _dirs, files in os.walk(d, topdown=False):
+        for f in files:
+            rel = os.path.relpath(os.path.join(root, f), d)
+            if rel not in keep:
+                try:
+                    os.unlink(os.path.join(root, f))
+                except OSError:
+                    pass
+        if root != d and not os.listdir(root):
+            try:
+                os.rmdir(root)
+            except OSError:
+                pass
+
+
+def _field(pod, path, node_name=None, pod_ip=None, host_ip=None):
     md = pod.get("metadata") or {}
     if path == "metadata.name":
         return md.get("name", "")
@@ -85,7 +122,8 @@ def _field(pod, path, node_name=None, pod_ip=None):
     if path == "status.podIP":
         return pod_ip or (pod.get("status") or {}).get("podIP", "")
     if path == "status.hostIP":
-        return (pod.get("status") or {}).get("hostIP", "")
+        # the kubelet's own node address: the status carrying hostIP may not be written yet
+        return (pod.get("status") or {}).get("hostIP") or host_ip or ""
     if path in ("metadata.labels", "metadata.annotations"):
         m = md.get(path.split(".")[1]) or {}
         return "\n".join(f'{k}="{v}"' for k, v in sorted(m.items()))
@@ -95,13 +133,18 @@ def _field(pod, path, node_name=None, pod_ip=None):
     raise VolumeError(f"unsupported fieldRef {path!r}")
 
 
-def _resource_field(container, ref):
+def _resource_field(container, ref, allocatable=None):
+    """`resourceFieldRef` (`pkg/api/v1/resource/helpers.go` ExtractContainerResourceValue): a
+    missing limit is the node's allocatable (`kubelet_resources.go` defaultPodLimitsForDownwardAPI),
+    a missing request falls back to the limit."""
     res = container.get("resources") or {}
     r = ref["resource"]
     kind, name = r.split(".", 1)
     q = (res.get(kind) or {}).get(name)
     if q is None and kind == "requests":
         q = (res.get("limits") or {}).get(name)
+    if q is None and kind == "limits" and allocatable:
+        q = allocatable.get(name)
     if q is None:
         return "0"
     v = parse_quantity(str(q)).value / parse_quantity(str(ref.get("divisor", "1"))).value   # Fractions
@@ -124,6 +167,23 @@ class VolumeManager:
         self.node_name = node_name
         self.attach_timeout = attach_timeout
         self.csi_published: dict[str, list] = {}     # pod uid -> [(driver, volume handle, target)]
+        self.allocatable = None                      # node allocatable: default downward-API limits
+        self.host_ip = None                          # the node's address (status.hostIP)
+
+    def _traversable(self, path):
+        """Make the kubelet-owned directories above a volume traversable (0711: no listing) so a
+        container running as another uid can reach the volume at its host path — the process
+        runtime's containers on the host root read volumes there (KUBERNETES_VOLUME_<NAME>)."""
+        stop = os.path.dirname(os.path.dirname(os.path.abspath(self.root)))    # up to the kubelet root
+        p = os.path.abspath(path)
+        while p.startswith(stop + os.sep) and p != stop:
+            try:
+                st = os.stat(p)
+                if st.st_uid == os.geteuid() and (st.st_mode & 0o111) != 0o111:
+                    os.chmod(p, (st.st_mode & 0o7777) | 0o111)
+            except OSError:
+                pass
+            p = os.path.dirname(p)
 
     def pod_dir(self, pod):
         return os.path.join(self.root, pod["metadata"]["uid"])
@@ -145,9 +205,10 @@ class VolumeManager:
             name = v["name"]
             d = os.path.join(base, name)
             if "emptyDir" in v:
-                if (v["emptyDir"] or {}).get("medium") == "Memory" and os.path.isdir("/dev/shm"):
-                    d = os.path.join("/dev/shm", "kamd-" + pod["metadata"]["uid"], name)
+                if (v["emptyDir"] or {}).get("medium") == "Memory":
+                    d = await self._memory_dir(pod, name, d, (v["emptyDir"] or {}).get("sizeLimit"))
                 os.makedirs(d, exist_ok=True)
+                os.chmod(d, 0o777)          # `empty_dir.go` setupDir: world-writable, any runAsUser
             elif "hostPath" in v:
                 hp = v["hostPath"]
                 d = hp["path"]
@@ -175,14 +236,18 @@ class VolumeManager:
                 kind = next(k for k in NETWORK_KINDS if k in v)
                 d = await self._net_mount(pod, kind, v[kind], d)
             elif "projected" in v:
+                dm = v["projected"].get("defaultMode")
+                os.makedirs(d, exist_ok=True)
                 for src in v["projected"].get("sources") or ():
                     if "configMap" in src or "secret" in src:
-                        await self._cm_secret(ns, src, d)
+                        await self._cm_secret(ns, src, d, dm)
                     elif "downwardAPI" in src:
-                        self._downward(pod, src["downwardAPI"], d, node_name, pod_ip)
+                        self._downward(pod, src["downwardAPI"], d, node_name, pod_ip, dm)
             else:
                 raise VolumeError(f"volume {name}: unsupported volume source {sorted(k for k in v if k != 'name')}")
             out[name] = d
+        if out:
+            self._traversable(base)
         return out
 
     async def _pvc_path(self, ns, src, pod=None, vol_name=None, node_name=None):
@@ -371,7 +436,32 @@ class VolumeManager:
             finally:
                 await c.close()
 
-    async def _cm_secret(self, ns, v, d):
+    async def refresh(self, pod, node_name=None, pod_ip=None):
+        """Re-project the pod's configMap / secret / downwardAPI / projected volumes into their
+        directories (the kubelet's periodic pod sync, `--sync-frequency`): updated keys, new
+        keys, removed keys, an optional source that appeared or went away, changed labels and
+        annotations all reach the running container."""
+        ns = pod["metadata"].get("namespace", "default")
+        base = os.path.join(self.pod_dir(pod), "volumes")
+        for v in (pod.get("spec") or {}).get("volumes") or ():
+            d = os.path.join(base, v["name"])
+            if not os.path.isdir(d):
+                continue
+            if "configMap" in v or "secret" in v:
+                _prune(d, await self._cm_secret(ns, v, d))
+            elif "downwardAPI" in v:
+                _prune(d, self._downward(pod, v["downwardAPI"], d, node_name, pod_ip))
+            elif "projected" in v:
+                keep = set()
+                for src in v["projected"].get("sources") or ():
+                    if "configMap" in src or "secret" in src:
+                        keep |= await self._cm_secret(ns, src, d, v["projected"].get("defaultMode"))
+                    elif "downwardAPI" in src:
+                        keep |= self._downward(pod, src["downwardAPI"], d, node_name, pod_ip,
+                                               v["projected"].get("defaultMode"))
+                _prune(d, keep)
+
+    async def _cm_secret(self, ns, v, d, default_mode=None):
         if "configMap" in v:
             src = v["configMap"]
             obj = await self._get("configmaps", ns, src["name"], src.get("optional"))
@@ -387,16 +477,23 @@ class VolumeManager:
             for k, s in ((obj or {}).get("stringData") or {}).items():
                 data[k] = base64.b64encode(s.encode()).decode()
             binary = True
-        _write_files(d, data, src.get("items"), int(src.get("defaultMode", 0o644)), binary)
+        mode = src.get("defaultMode", default_mode if default_mode is not None else 0o644)
+        return _write_files(d, data, src.get("items"), int(mode), binary, optional=bool(src.get("optional")))
 
-    def _downward(self, pod, spec, d, node_name, pod_ip):
+    def _downward(self, pod, spec, d, node_name, pod_ip, default_mode=None):
         data = {}
         items = []
+        ctrs = {c["name"]: c for c in (pod.get("spec") or {}).get("containers") or ()}
         for it in spec.get("items") or ():
             if "fieldRef" in it:
-                data[it["path"]] = _field(pod, it["fieldRef"]["fieldPath"], node_name, pod_ip)
-            items.append({"key": it["path"], "path": it["path"]})
-        _write_files(d, data, items, int(spec.get("defaultMode", 0o644)))
+                data[it["path"]] = _field(pod, it["fieldRef"]["fieldPath"], node_name, pod_ip, self.host_ip)
+            elif "resourceFieldRef" in it:
+                ref = it["resourceFieldRef"]
+                c = ctrs.get(ref.get("containerName")) or next(iter(ctrs.values()), {})
+                data[it["path"]] = _resource_field(c, ref, self.allocatable)
+            items.append({"key": it["path"], "path": it["path"], "mode": it.get("mode")})
+        mode = spec.get("defaultMode", default_mode if default_mode is not None else 0o644)
+        return _write_files(d, data, items, int(mode))
 
     def mounts_for(self, container, vols: dict):
         out = []
@@ -410,7 +507,33 @@ class VolumeManager:
             out.append({"containerPath": m["mountPath"], "hostPath": hp, "readOnly": bool(m.get("readOnly"))})
         return out
 
+    async def _memory_dir(self, pod, name, d, size_limit=None):
+        """`medium: Memory` (`empty_dir.go` setupTmpfs): a tmpfs mounted on the volume directory
+        when the kubelet may mount (root) — visible at the same path to every container, also
+        one whose /dev is private — else a directory under /dev/shm."""
+        if os.geteuid() == 0 and shutil.which("mount"):
+            os.makedirs(d, exist_ok=True)
+            if self.mounter.is_mount_point(d):
+                return d
+            opts = ["mode=0777"]
+            if size_limit:
+                opts.append(f"size={int(parse_quantity(str(size_limit)).value)}")
+            try:
+                await self.mounter.mount("tmpfs", d, "tmpfs", opts)
+                return d
+            except Exception:  # noqa: BLE001 - no mount privilege after all: /dev/shm below
+                pass
+        if os.path.isdir("/dev/shm"):
+            return os.path.join("/dev/shm", "kamd-" + pod["metadata"]["uid"], name)
+        return d
+
     def teardown(self, pod):
+        vdir = os.path.join(self.pod_dir(pod), "volumes")
+        for v in (pod.get("spec") or {}).get("volumes") or ():
+            p = os.path.join(vdir, v["name"])
+            if "emptyDir" in v and (v["emptyDir"] or {}).get("medium") == "Memory" and self.mounter.is_mount_point(p):
+                import subprocess
+                subprocess.run(["umount", p], capture_output=True, timeout=10)
         _rmtree_no_mounts(self.pod_dir(pod), self.mounter)
         shm = os.path.join("/dev/shm", "kamd-" + pod["metadata"]["uid"])
         if os.path.isdir(shm):
@@ -450,9 +573,9 @@ class VolumeManager:
                 continue
             vf = e.get("valueFrom") or {}
             if "fieldRef" in vf:
-                put(name, _field(pod, vf["fieldRef"]["fieldPath"], node_name, pod_ip))
+                put(name, _field(pod, vf["fieldRef"]["fieldPath"], node_name, pod_ip, self.host_ip))
             elif "resourceFieldRef" in vf:
-                put(name, _resource_field(container, vf["resourceFieldRef"]))
+                put(name, _resource_field(container, vf["resourceFieldRef"], self.allocatable))
             elif "configMapKeyRef" in vf:
                 r = vf["configMapKeyRef"]
                 obj = await self._get("configmaps", ns, r["name"], r.get("optional"))
