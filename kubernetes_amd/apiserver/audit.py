@@ -89,6 +89,7 @@ class AuditLogger:
         self.policy = policy or Policy()
         self.max_body = max_body
         self._buf = []
+        self._wbuf = []               # JSON events for a batching webhook
         self._lock = threading.Lock()
         self._scheduled = False
         self.stdout = path == "-"
@@ -147,6 +148,7 @@ class AuditLogger:
                 ev["responseObject"] = json.loads(response_body)
             except ValueError:
                 pass
+        js = json.dumps(ev, separators=(",", ":"))     # the webhook always gets JSON events
         if self.format == "legacy":
             u = ev["user"]
             groups = ",".join(f'\\"{g}\\"' for g in u["groups"])
@@ -155,10 +157,24 @@ class AuditLogger:
                     f'namespace="{parsed_ns or "<none>"}" uri="{uri}"\n'
                     f'{ev["stageTimestamp"]} AUDIT: id="{ev["auditID"]}" response="{code}"')
         else:
-            line = json.dumps(ev, separators=(",", ":"))
+            line = js
+        self._append(line, js)
+        return js
+
+    @property
+    def blocking(self):
+        return self.webhook is not None and self.webhook.blocking
+
+    async def deliver(self, line):
+        """Blocking webhook mode: the request waits until its event was POSTed."""
+        await asyncio.to_thread(self.webhook.post_now, [line])
+
+    def _append(self, line, js):
         flush_now = False
         with self._lock:
             self._buf.append(line)
+            if self.webhook is not None and not self.webhook.blocking:
+                self._wbuf.append(js)
             if not self._scheduled:
                 self._scheduled = True
                 try:
@@ -172,7 +188,10 @@ class AuditLogger:
     def flush(self):
         with self._lock:
             buf, self._buf = self._buf, []
+            wbuf, self._wbuf = self._wbuf, []
             self._scheduled = False
+        if wbuf:
+            self.webhook.enqueue(wbuf)
         if not buf:
             return
         data = "\n".join(buf) + "\n"
@@ -183,8 +202,6 @@ class AuditLogger:
             self.f.flush()
         elif self.stdout:
             os.write(1, data.encode())
-        if self.webhook is not None:
-            self.webhook.enqueue(buf)
 
     def _rotate(self):
         import glob
@@ -213,13 +230,20 @@ class AuditLogger:
 
 
 class WebhookBackend:
-    """Batching audit webhook (`staging/src/k8s.io/apiserver/plugin/pkg/audit/webhook/webhook.go`,
-    `--audit-webhook-config-file` kubeconfig naming the remote server): events are buffered
-    (10 000) and POSTed as an `audit.k8s.io/v1beta1` EventList in batches of up to 400, at
-    least every `max_wait` seconds, from a background thread so request handling never blocks;
-    a failed batch is retried with backoff, then dropped."""
+    """Audit webhook (`staging/src/k8s.io/apiserver/plugin/pkg/audit/webhook/webhook.go`,
+    `--audit-webhook-config-file` kubeconfig naming the remote server).
 
-    def __init__(self, kubeconfig, max_batch=400, max_wait=1.0, buffer=10000, retries=3):
+    mode "batch": events are buffered (`buffer`, 10 000) and POSTed as an `audit.k8s.io/v1beta1`
+    EventList in batches of up to `max_batch`, at least every `max_wait` seconds, from a
+    background thread so request handling never blocks; batches are throttled to `throttle_qps`
+    per second with bursts of `throttle_burst` (0 = unthrottled); a failed batch is retried with
+    exponential backoff from `initial_backoff`, then dropped.
+    mode "blocking": every request's event is POSTed before its response is sent."""
+
+    def __init__(self, kubeconfig, max_batch=400, max_wait=1.0, buffer=10000, retries=3, mode="batch",
+                 throttle_qps=0.0, throttle_burst=0, initial_backoff=0.1):
+        if mode not in ("batch", "blocking"):
+            raise ValueError(f"unknown audit webhook mode {mode!r}")
         from ..client import clientcmd
         cfg, p = clientcmd.load(kubeconfig)
         r = clientcmd.resolve(cfg, None, os.path.dirname(os.path.abspath(p)))
@@ -227,12 +251,35 @@ class WebhookBackend:
             raise ValueError(f"audit webhook kubeconfig {kubeconfig}: no usable context")
         self.url, self.token, self.ssl = r.server, r.token, r.ssl_context
         self.max_batch, self.max_wait, self.buffer, self.retries = max_batch, max_wait, buffer, retries
+        self.blocking = mode == "blocking"
+        self.initial_backoff = initial_backoff
+        self.qps, self.burst = float(throttle_qps or 0), max(1, int(throttle_burst or 1))
+        self._tokens, self._last = float(self.burst), time.monotonic()
         self._q = []
         self._cv = threading.Condition()
         self._closed = False
-        self.sent = self.dropped = 0
-        self._t = threading.Thread(target=self._run, name="audit-webhook", daemon=True)
-        self._t.start()
+        self.sent = self.dropped = self.posts = 0
+        self._t = None
+        if not self.blocking:
+            self._t = threading.Thread(target=self._run, name="audit-webhook", daemon=True)
+            self._t.start()
+
+    def _throttle(self):
+        """Token bucket over batch POSTs (`--audit-webhook-batch-throttle-qps/-burst`)."""
+        if self.qps <= 0:
+            return
+        now = time.monotonic()
+        self._tokens = min(float(self.burst), self._tokens + (now - self._last) * self.qps)
+        self._last = now
+        if self._tokens < 1.0:
+            time.sleep((1.0 - self._tokens) / self.qps)
+            self._tokens = 0.0
+            self._last = time.monotonic()
+        else:
+            self._tokens -= 1.0
+
+    def post_now(self, lines):
+        self._post(lines)
 
     def enqueue(self, lines):
         with self._cv:
@@ -251,13 +298,14 @@ class WebhookBackend:
         hdr = {"Content-Type": "application/json"}
         if self.token:
             hdr["Authorization"] = f"Bearer {self.token}"
-        delay = 0.1
+        delay = self.initial_backoff
         for _ in range(self.retries):
             try:
                 req = urllib.request.Request(self.url, data=body, headers=hdr, method="POST")
                 with urllib.request.urlopen(req, timeout=10, context=self.ssl) as r:
                     r.read()
                 self.sent += len(batch)
+                self.posts += 1
                 return
             except OSError:
                 time.sleep(delay)
@@ -272,6 +320,7 @@ class WebhookBackend:
                 batch, self._q = self._q[:self.max_batch], self._q[self.max_batch:]
                 done = self._closed and not self._q
             if batch:
+                self._throttle()
                 self._post(batch)
             if done:
                 return
@@ -280,7 +329,8 @@ class WebhookBackend:
         with self._cv:
             self._closed = True
             self._cv.notify()
-        self._t.join(timeout)
+        if self._t is not None:
+            self._t.join(timeout)
 
 
 def now():

@@ -212,8 +212,18 @@ class APIServer:
                  enable_swagger_ui=False, log_dir="/var/log", runtime_config=None, allow_privileged=True,
                  kubelet_preferred_address_types=("InternalIP", "ExternalIP", "Hostname", "InternalDNS", "ExternalDNS"),
                  kubelet_port=10250, kubelet_timeout=5.0, advertise_address=None, apiserver_count=1,
-                 endpoint_reconciler_type="master-count", kubernetes_service_node_port=0, proxy_client_cert=None):
+                 endpoint_reconciler_type="master-count", kubernetes_service_node_port=0, proxy_client_cert=None,
+                 watch_cache_sizes=None, compaction_interval=0.0, delete_collection_workers=1):
         self.proxy_client_cert = proxy_client_cert          # (cert file, key file) for aggregated API servers
+        # --watch-cache-sizes / --target-ram-mb: per-resource watch windows (plural -> events)
+        self.watch_cache_sizes = dict(watch_cache_sizes or {})
+        # --etcd-compaction-interval (`storage/etcd3/compact.go`): every interval the store's
+        # history is compacted to the revision seen one interval earlier; 0 = never
+        self.compaction_interval = float(compaction_interval or 0)
+        self._compactor = None
+        self.compactions = 0
+        # --delete-collection-workers: concurrent deletes of one DELETE-collection call
+        self.delete_collection_workers = max(1, int(delete_collection_workers))
         self.abac_policy_file = authorization_policy_file
         # --runtime-config: group/versions (and extensions/v1beta1 resources) switched off; every
         # served version is on by default here (the reference leaves alpha versions off)
@@ -393,7 +403,7 @@ class APIServer:
 
     # ------------------------------------------------------------------
     def _install(self, ri):
-        self.caches[ri.plural] = ResourceCache(ri.plural, self.watch_window)
+        self.caches[ri.plural] = ResourceCache(ri.plural, self.watch_cache_sizes.get(ri.plural, self.watch_window))
         self.strategies[ri.plural] = strategy_for(ri)
         self._store_res[m.prefix_for(ri).split("/")[2]] = ri.plural
 
@@ -1181,7 +1191,33 @@ class APIServer:
         await self._reconcile_master_endpoints("127.0.0.1" if host in ("0.0.0.0", "") else host, port)
         if self.event_ttl and self._reaper is None:
             self._reaper = asyncio.ensure_future(self._event_reaper())
+        if self.compaction_interval > 0 and self._compactor is None:
+            self._compactor = asyncio.ensure_future(self._compact_loop())
         return port
+
+    async def _store_revision(self):
+        return await self.rstore.revision() if self.rstore is not None else self.store.revision
+
+    async def compact_to(self, rev):
+        if rev <= 0:
+            return
+        if self.rstore is not None:
+            await self.rstore.compact(rev)
+        else:
+            self.store.compact(rev)
+        self.compactions += 1
+
+    async def _compact_loop(self):
+        prev = await self._store_revision()
+        while True:
+            await asyncio.sleep(self.compaction_interval)
+            try:
+                cur = await self._store_revision()
+                await self.compact_to(prev)
+                log.info("compacted storage history to revision %d", prev)
+                prev = cur
+            except Exception as e:  # noqa: BLE001 - the next pass retries
+                log.warning("storage compaction failed: %s", e)
 
     async def start_insecure(self, host="127.0.0.1", port=0, reuse_port=False):
         """--insecure-port / --insecure-bind-address: plain HTTP with no authentication or
@@ -1292,6 +1328,9 @@ class APIServer:
         if self._reaper is not None:
             self._reaper.cancel()
             self._reaper = None
+        if self._compactor is not None:
+            self._compactor.cancel()
+            self._compactor = None
         await self.http.stop()
         if self.insecure_http is not None:
             await self.insecure_http.stop()
@@ -1543,7 +1582,9 @@ class APIServer:
                     # utiltrace LogIfLong (registry/store.go: 500 ms) for slow mutating calls
                     log.warning('Trace "%s %s" (code %s) total %.1f ms', verb, req.path, code, dt * 1e3)
             if self.audit is not None and resource:
-                self.audit.log(req, verb, resource, sub, code)
+                line = self.audit.log(req, verb, resource, sub, code)
+                if line is not None and self.audit.blocking:
+                    await self.audit.deliver(line)
 
     def _authorize(self, user, verb, ns, resource, sub, name, group, path, resource_request=True):
         if user is UNSECURED:
@@ -1703,18 +1744,26 @@ class APIServer:
         ls = parse_labels(req.query.get("labelSelector")) if req.query.get("labelSelector") else None
         fs = parse_field_selector(req.query.get("fieldSelector")) if req.query.get("fieldSelector") else None
         opts = codec.loads(req.body) if req.body else {}
-        items = []
         if ri.plural in self.uncached:
             entries = (await self._store_entries(ri, ns, ls, fs))[0]
         else:
             entries = self.caches[ri.plural].list(m.prefix_for(ri, ns), ls, fs)
-        for e in entries:
-            try:
-                d, _ = await self.delete(ri, m.namespace_of(e.obj) or None, m.name_of(e.obj), opts, user)
-                items.append(d.obj)
-            except APIError as err:
-                if err.code != 404:
-                    raise
+        # `DeleteCollection` of registry/generic/registry/store.go: --delete-collection-workers
+        # goroutines take items off a shared queue; results keep the listing order
+        results = [None] * len(entries)
+        nxt = iter(range(len(entries)))
+
+        async def worker():
+            for i in nxt:
+                e = entries[i]
+                try:
+                    d, _ = await self.delete(ri, m.namespace_of(e.obj) or None, m.name_of(e.obj), opts, user)
+                    results[i] = d.obj
+                except APIError as err:
+                    if err.code != 404:
+                        raise
+        await asyncio.gather(*(worker() for _ in range(min(self.delete_collection_workers, len(entries)) or 1)))
+        items = [o for o in results if o is not None]
         return _json(200, {"kind": ri.list_kind, "apiVersion": ri.group_version,
                            "metadata": {"resourceVersion": str(self.revision)}, "items": items})
 

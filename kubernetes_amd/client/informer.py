@@ -81,8 +81,13 @@ class Indexer:
 
 class Informer:
     def __init__(self, client, resource, namespace=None, label_selector=None, field_selector=None,
-                 indexers=None, watch_timeout=300, extra_query=None):
+                 indexers=None, watch_timeout=300, extra_query=None, resync_period=0.0):
         self.client = client
+        # resync (`sharedIndexInformer` resyncCheckPeriod): every period each cached object is
+        # re-delivered as an update with old == new, so level-driven handlers re-examine state
+        # that no watch event touched; 0 = off
+        self.resync_period = resync_period
+        self._resync_task = None
         self.extra_query = extra_query
         self.resource = resource
         self.namespace = namespace
@@ -187,8 +192,17 @@ class Informer:
                 await asyncio.sleep(backoff)
                 backoff = min(backoff * 2, 2)
 
+    async def _resync_loop(self):
+        while not self._stopped:
+            await asyncio.sleep(self.resync_period)
+            if self.synced.is_set():
+                for o in self.store.list():
+                    self._fire(1, o, o)
+
     def start(self):
         self._task = asyncio.ensure_future(self.run())
+        if self.resync_period > 0:
+            self._resync_task = asyncio.ensure_future(self._resync_loop())
         return self._task
 
     async def wait_synced(self, timeout=30):
@@ -200,20 +214,32 @@ class Informer:
             self._stream.close()
         if self._task:
             self._task.cancel()
+        if self._resync_task:
+            self._resync_task.cancel()
+
+
+def resync_period(min_resync):
+    """`ResyncPeriod(s)` of cmd/kube-controller-manager/app/controllermanager.go: a random period
+    in [min, 2*min), so the informers of one process do not resync in lockstep."""
+    import random
+    return min_resync * (1.0 + random.random()) if min_resync > 0 else 0.0
 
 
 class InformerFactory:
-    """SharedInformerFactory: one informer per (resource, namespace, selectors)."""
+    """SharedInformerFactory: one informer per (resource, namespace, selectors); `resync` is the
+    default resync period of the informers it makes (0 = none)."""
 
-    def __init__(self, client):
+    def __init__(self, client, resync=0.0):
         self.client = client
         self.informers = {}
+        self.resync = resync
 
     def get(self, resource, namespace=None, label_selector=None, field_selector=None):
         k = (resource, namespace, label_selector, field_selector)
         inf = self.informers.get(k)
         if inf is None:
-            inf = self.informers[k] = Informer(self.client, resource, namespace, label_selector, field_selector)
+            inf = self.informers[k] = Informer(self.client, resource, namespace, label_selector, field_selector,
+                                               resync_period=self.resync)
         return inf
 
     def start(self):

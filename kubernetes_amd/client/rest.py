@@ -73,13 +73,33 @@ def resource_path(resource: str, namespace=None, name=None, subresource="", watc
     return p
 
 
+JSON, PROTOBUF = "application/json", "application/vnd.kubernetes.protobuf"
+
+
 class Client:
+    """`content_type` is the wire format (`--kube-api-content-type`, `rest.Config.ContentType`):
+    with protobuf, objects of kinds the protobuf schema covers are sent protobuf-encoded and
+    responses are asked for as protobuf (falling back to JSON per response, as the reference's
+    negotiated serializer does — lists, CRs and Status bodies come back as JSON); watches stay
+    JSON framed."""
+
     def __init__(self, url: str, token=None, qps: float | None = None, burst: int = 10, max_conns=16,
-                 user_agent="kubernetes-amd", ssl_context=None, timeout=60.0):
+                 user_agent="kubernetes-amd", ssl_context=None, timeout=60.0, content_type=JSON):
+        if content_type not in (JSON, PROTOBUF):
+            raise ValueError(f"unsupported content type {content_type!r} (use {JSON} or {PROTOBUF})")
         self.url = url
         self.http = HTTPClient(url, token=token, ssl_context=ssl_context, max_conns=max_conns, timeout=timeout)
         self.limiter = TokenBucket(qps, burst) if qps else None
         self.user_agent = user_agent
+        self.content_type = content_type
+        self._accept = {"Accept": f"{PROTOBUF}, {JSON}"} if content_type == PROTOBUF else None
+
+    @staticmethod
+    def _decode(resp):
+        if resp[:4] == b"k8s\x00":
+            from ..api import protobuf as pb
+            return pb.decode_object(resp)
+        return codec.loads(resp)
 
     async def close(self):
         await self.http.close()
@@ -87,15 +107,24 @@ class Client:
     async def _do(self, method, path, body=None, content_type="application/json", ok=(200, 201)):
         if self.limiter:
             await self.limiter.wait()
-        data = None if body is None else (body if isinstance(body, (bytes, bytearray)) else codec.dumpb(body))
-        st, resp = await self.http.request(method, path, data, content_type)
+        if body is None or isinstance(body, (bytes, bytearray)):
+            data = body
+        elif self._accept is not None and content_type == JSON and body.get("kind"):
+            from ..api import protobuf as pb
+            if pb.supported(body["kind"], body.get("apiVersion") or "v1"):
+                data, content_type = pb.encode_object(body), PROTOBUF
+            else:
+                data = codec.dumpb(body)
+        else:
+            data = codec.dumpb(body)
+        st, resp = await self.http.request(method, path, data, content_type, self._accept)
         if st not in ok:
             try:
-                status = codec.loads(resp)
+                status = self._decode(resp)
             except Exception:
                 status = {"message": resp.decode(errors="replace")}
             raise APIStatusError(st, status)
-        return codec.loads(resp) if resp else None
+        return self._decode(resp) if resp else None
 
     async def raw(self, method, path, body=None, content_type="application/json"):
         return await self.http.request(method, path, body, content_type)

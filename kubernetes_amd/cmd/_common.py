@@ -69,3 +69,32 @@ def run_until_signal(main_coro_factory):
             pr.dump_stats(os.path.join(prof_dir, os.path.basename(sys.argv[0]).replace(".py", "") + f".{os.getpid()}.prof"))
         return
     asyncio.run(runner())
+
+
+def unsupported(group, flag, default, type=str, why=""):
+    """A reference flag whose subsystem this component does not have: the default still parses
+    (reference command lines keep working), any other value is refused by `check_unsupported`
+    instead of being silently ignored."""
+    a = group.add_argument(flag, type=type, default=default,
+                           help=f"unsupported: only the default ({default!r}) is accepted — {why}")
+    a.kamd_unsupported = why
+    return a
+
+
+def check_unsupported(parser, args):
+    """parser.error() for the first `unsupported` flag set to a non-default value."""
+    for a in parser._actions:
+        why = getattr(a, "kamd_unsupported", None)
+        if why is None:
+            continue
+        v = getattr(args, a.dest, a.default)
+        default = a.type(a.default) if isinstance(a.default, str) and a.type not in (None, str) else a.default
+        if v != default:
+            parser.error(f"{a.option_strings[0]}={v!r} is not supported here: {why}")
+
+
+def deprecated_noop(group, flag, default, type=str, ref=""):
+    """A flag the reference itself marks deprecated and ignores (its `MarkDeprecated(...,
+    "...no-op...")`): accepted with any value, as there."""
+    return group.add_argument(flag, type=type, default=default,
+                              help=f"deprecated; a no-op in the reference too ({ref})")

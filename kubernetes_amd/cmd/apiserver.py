@@ -23,7 +23,7 @@ import time
 from ..api import codec
 from ..apiserver.server import APIServer
 from ..storage.mvcc import MVCCStore
-from ._common import run_until_signal, setup_logging, write_port_file
+from ._common import check_unsupported, deprecated_noop, run_until_signal, setup_logging, unsupported, write_port_file
 
 
 def _parser():
@@ -250,7 +250,7 @@ def _reference_flags(ap):
     g = ap.add_argument_group("kubelet connections")
     g.add_argument("--kubelet-preferred-address-types", default="InternalIP,ExternalIP,Hostname,InternalDNS,ExternalDNS")
     g.add_argument("--kubelet-port", type=int, default=10250)
-    g.add_argument("--kubelet-read-only-port", type=int, default=10255, help="accepted; the authenticated port is used")
+    deprecated_noop(g, "--kubelet-read-only-port", 10255, int, "options.go:202-203, 'DEPRECATED: kubelet port.'")
     g.add_argument("--kubelet-timeout", default="5s")
     g = ap.add_argument_group("audit")
     g.add_argument("--audit-log-format", default="json", choices=["json", "legacy"])
@@ -258,38 +258,82 @@ def _reference_flags(ap):
     g.add_argument("--audit-log-maxbackup", type=int, default=0)
     g.add_argument("--audit-log-maxage", type=int, default=0, help="days a rotated audit log is kept")
     g.add_argument("--audit-webhook-mode", default="batch", choices=["batch", "blocking"],
-                   help="accepted; events are always delivered by the batching backend")
-    for f in ("--audit-webhook-batch-buffer-size", "--audit-webhook-batch-throttle-burst"):
-        g.add_argument(f, type=int, default=0, help="accepted")
-    for f in ("--audit-webhook-batch-initial-backoff", "--audit-webhook-batch-throttle-qps"):
-        g.add_argument(f, default="", help="accepted")
+                   help="batch: buffered, sent from a background thread; blocking: each request waits for its event")
+    g.add_argument("--audit-webhook-batch-buffer-size", type=int, default=10000, help="events buffered before dropping")
+    g.add_argument("--audit-webhook-batch-throttle-qps", type=float, default=10.0, help="batches per second (0 = off)")
+    g.add_argument("--audit-webhook-batch-throttle-burst", type=int, default=15, help="batch burst above the qps")
+    g.add_argument("--audit-webhook-batch-initial-backoff", default="10s", help="first retry delay of a failed batch")
     g = ap.add_argument_group("storage")
     g.add_argument("--storage-backend", default="etcd3", choices=["etcd3"])
     g.add_argument("--etcd-prefix", default="/registry",
                    help="key prefix in etcd: anything but /registry puts the keys under that namespace "
                         "(etcd v3 endpoints only)")
-    g.add_argument("--etcd-compaction-interval", default="5m", help="accepted; the store keeps a bounded history window")
-    g.add_argument("--watch-cache", type=_bool, default=True, help="accepted; the watch cache is always on")
-    g.add_argument("--watch-cache-sizes", default="", help="accepted; one window (--watch-cache-size) serves all resources")
+    g.add_argument("--etcd-compaction-interval", default="5m",
+                   help="compact the store's history to the revision of one interval ago, every interval (0 = never)")
+    unsupported(g, "--watch-cache", True, _bool, "every resource is served from its watch cache")
+    g.add_argument("--watch-cache-sizes", default="",
+                   help="per-resource watch windows, resource#size,... (e.g. pods#5000,nodes#1000)")
     g.add_argument("--default-watch-cache-size", type=int, default=None, help="alias of --watch-cache-size")
     for f in ("--storage-versions", "--storage-version", "--etcd-servers-overrides"):
         g.add_argument(f, default="")
     g.add_argument("--etcd-cafile", default="", help="CA of an https etcd endpoint")
     g.add_argument("--etcd-certfile", default="", help="client certificate for an https etcd endpoint")
     g.add_argument("--etcd-keyfile", default="", help="client key for an https etcd endpoint")
-    g.add_argument("--etcd-quorum-read", type=_bool, default=True, help="accepted; the store is linearizable")
-    g.add_argument("--deserialization-cache-size", type=int, default=0, help="accepted")
-    g.add_argument("--delete-collection-workers", type=int, default=1, help="accepted")
-    g.add_argument("--target-ram-mb", type=int, default=0, help="accepted")
-    g = ap.add_argument_group("no-ops kept for command-line compatibility")
-    for f in ("--cloud-provider", "--cloud-config", "--external-hostname", "--public-address-override", "--ssh-user",
-              "--ssh-keyfile", "--experimental-keystone-url", "--experimental-keystone-ca-file", "--master-service-namespace",
-              "--tls-ca-file", "--tls-sni-cert-key", "--kubeconfig", "--authentication-kubeconfig",
-              "--authorization-kubeconfig", "--max-connection-bytes-per-sec", "--http2-max-streams-per-connection"):
-        g.add_argument(f, default="")
-    for f in ("--enable-garbage-collector", "--enable-aggregator-routing", "--repair-malformed-updates",
-              "--contention-profiling", "--authentication-skip-lookup"):
-        g.add_argument(f, type=_bool, default=False)
+    unsupported(g, "--etcd-quorum-read", True, _bool, "every read is linearizable")
+    unsupported(g, "--deserialization-cache-size", 0, int, "objects are decoded once into the watch cache")
+    g.add_argument("--delete-collection-workers", type=int, default=1, help="concurrent deletes per DELETE-collection call")
+    g.add_argument("--target-ram-mb", type=int, default=0,
+                   help="size the watch windows for ~target/60 nodes (cachesize.go heuristics); "
+                        "--watch-cache-sizes entries win")
+    g = ap.add_argument_group("subsystems this API server does not have")
+    g.add_argument("--cloud-provider", default="", help="'' only: cloud providers are out of scope")
+    for f, why in (("--cloud-config", "cloud providers are out of scope"),
+                   ("--external-hostname", "no cloud-derived external address; set --advertise-address"),
+                   ("--experimental-keystone-url", "Keystone authentication is not implemented"),
+                   ("--experimental-keystone-ca-file", "Keystone authentication is not implemented"),
+                   ("--tls-ca-file", "the serving chain comes from --tls-cert-file"),
+                   ("--tls-sni-cert-key", "one serving certificate (no SNI selection)"),
+                   ("--kubeconfig", "kube-apiserver is not an aggregated API server"),
+                   ("--authentication-kubeconfig", "kube-apiserver is not an aggregated API server"),
+                   ("--authorization-kubeconfig", "kube-apiserver is not an aggregated API server")):
+        unsupported(g, f, "", str, why)
+    g.add_argument("--public-address-override", default="", help="deprecated alias of --bind-address")
+    deprecated_noop(g, "--ssh-user", "", str, "options.go:159, SSH tunnels")
+    deprecated_noop(g, "--ssh-keyfile", "", str, "options.go:164, SSH tunnels")
+    unsupported(g, "--master-service-namespace", "default", str, "the kubernetes service lives in 'default'")
+    unsupported(g, "--max-connection-bytes-per-sec", 0, int, "no per-connection rate limit")
+    unsupported(g, "--http2-max-streams-per-connection", 0, int, "the server speaks HTTP/1.1")
+    unsupported(g, "--enable-garbage-collector", True, _bool, "ownerReferences are always honoured")
+    unsupported(g, "--enable-aggregator-routing", False, _bool, "aggregated APIs are reached through their service")
+    unsupported(g, "--repair-malformed-updates", True, _bool, "updates are always defaulted from the stored object")
+    unsupported(g, "--authentication-skip-lookup", False, _bool, "kube-apiserver is not an aggregated API server")
+    g.add_argument("--contention-profiling", type=_bool, default=False,
+                   help="sample where the event loop blocks, served at /debug/pprof/block (with --profiling)")
+
+
+# `pkg/registry/cachesize/cachesize.go:25-44` NewHeuristicWatchCacheSizes: ~60 MB per node
+_HEURISTIC = {"replicationcontrollers": (5, 100), "endpoints": (10, 1000), "nodes": (5, 1000),
+              "pods": (50, 1000), "services": (5, 1000), "apiservices": (5, 1000)}
+
+
+def watch_cache_sizes(target_ram_mb, spec):
+    """--target-ram-mb heuristics, then --watch-cache-sizes `resource#size` entries on top
+    (`ParseWatchCacheSizes`); plural -> window size."""
+    sizes = {}
+    if target_ram_mb and target_ram_mb > 0:
+        cluster = target_ram_mb // 60
+        sizes = {r: max(k * cluster, floor) for r, (k, floor) in _HEURISTIC.items()}
+    for item in (x.strip() for x in (spec or "").split(",")):
+        if not item:
+            continue
+        res, sep, n = item.partition("#")
+        if not sep or not n.strip().lstrip("-").isdigit():
+            raise ValueError(f"invalid --watch-cache-sizes entry {item!r} (want resource#size)")
+        if int(n) <= 0:
+            raise ValueError(f"--watch-cache-sizes {item!r}: the size must be positive "
+                             "(every resource is served from its watch cache here)")
+        sizes[res.strip().split(".", 1)[0]] = int(n)
+    return sizes
 
 
 def _reference_kwargs(a):
@@ -326,11 +370,22 @@ def _reference_kwargs(a):
                 endpoint_reconciler_type=a.endpoint_reconciler_type,
                 kubernetes_service_node_port=a.kubernetes_service_node_port,
                 proxy_client_cert=(a.proxy_client_cert_file, a.proxy_client_key_file or a.proxy_client_cert_file)
-                if a.proxy_client_cert_file else None)
+                if a.proxy_client_cert_file else None,
+                watch_cache_sizes=getattr(a, "watch_cache_sizes_map", None),
+                compaction_interval=_duration(a.etcd_compaction_interval),
+                delete_collection_workers=a.delete_collection_workers)
 
 
 def main(argv=None):
-    a = _parser().parse_args(argv)
+    ap = _parser()
+    a = ap.parse_args(argv)
+    check_unsupported(ap, a)
+    if a.public_address_override:
+        a.bind_address = a.public_address_override
+    try:
+        a.watch_cache_sizes_map = watch_cache_sizes(a.target_ram_mb, a.watch_cache_sizes)
+    except ValueError as e:
+        ap.error(str(e))
     setup_logging(a.v)
     if a.workers > 1 and not a.etcd_servers:
         sys.exit(supervise(a))
@@ -357,7 +412,11 @@ def main(argv=None):
         audit = None
         if a.audit_log_path or a.audit_webhook_config_file:
             from ..apiserver.audit import AuditLogger, Policy, WebhookBackend
-            wh = (WebhookBackend(a.audit_webhook_config_file, a.audit_webhook_batch_max_size, a.audit_webhook_batch_max_wait)
+            wh = (WebhookBackend(a.audit_webhook_config_file, a.audit_webhook_batch_max_size, a.audit_webhook_batch_max_wait,
+                                 buffer=a.audit_webhook_batch_buffer_size, mode=a.audit_webhook_mode,
+                                 throttle_qps=a.audit_webhook_batch_throttle_qps,
+                                 throttle_burst=a.audit_webhook_batch_throttle_burst,
+                                 initial_backoff=_duration(a.audit_webhook_batch_initial_backoff))
                   if a.audit_webhook_config_file else None)
             audit = AuditLogger(a.audit_log_path, Policy.load(a.audit_policy_file) if a.audit_policy_file else None,
                                 webhook=wh, format=a.audit_log_format, max_size_mb=a.audit_log_maxsize,
@@ -386,6 +445,9 @@ def main(argv=None):
                       authorization_policy_file=a.authorization_policy_file,
                       authorization_webhook_url=a.authorization_webhook_url, oidc=oidc, **_reference_kwargs(a))
         s.enable_profiling = a.profiling
+        if a.contention_profiling and a.profiling:
+            from ..utils.profiling import enable_contention_profiling
+            enable_contention_profiling()
         if a.secure_port:
             # the reference's two listeners: TLS + authn/authz on --bind-address:--secure-port
             # (self-signed in --cert-dir without --tls-cert-file), plain HTTP without either on

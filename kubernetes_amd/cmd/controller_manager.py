@@ -5,7 +5,7 @@ import argparse
 
 from ..client.rest import Client
 from ..controllers.manager import CONTROLLERS, ControllerManager
-from ._common import run_until_signal, setup_logging
+from ._common import check_unsupported, deprecated_noop, run_until_signal, setup_logging, unsupported
 
 
 def main(argv=None):
@@ -48,6 +48,7 @@ def main(argv=None):
     _reference_flags(ap)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
+    check_unsupported(ap, a)
     setup_logging(a.v)
     if a.cloud_provider:
         raise SystemExit(f"kube-controller-manager: --cloud-provider={a.cloud_provider}: cloud providers are out of "
@@ -58,9 +59,11 @@ def main(argv=None):
     async def start():
         if a.kubeconfig:
             from ..client.clientcmd import client_from
-            client = client_from(a.kubeconfig, max_conns=64, qps=a.kube_api_qps, burst=a.kube_api_burst)
+            client = client_from(a.kubeconfig, max_conns=64, qps=a.kube_api_qps, burst=a.kube_api_burst,
+                                 content_type=a.kube_api_content_type)
         else:
-            client = Client(a.master or "http://127.0.0.1:8080", max_conns=64, qps=a.kube_api_qps, burst=a.kube_api_burst)
+            client = Client(a.master or "http://127.0.0.1:8080", max_conns=64, qps=a.kube_api_qps, burst=a.kube_api_burst,
+                            content_type=a.kube_api_content_type)
         from ..utils.componentserver import ComponentServer
         health = ComponentServer("componentconfig", profiling=a.profiling, configz=lambda: {
             k: v for k, v in vars(a).items() if not k.startswith("_")})
@@ -88,8 +91,11 @@ def main(argv=None):
                 "route": {"cluster_cidr": a.cluster_cidr, "routes": a.route_table,
                           "reconcile_period": a.route_reconciliation_period},
                 "service": {"ip_range": a.loadbalancer_ip_range}}
+        opts["persistentvolume-binder"] = {"enable_dynamic_provisioning": a.enable_dynamic_provisioning}
         if a.enable_hostpath_provisioner:
-            opts["persistentvolume-binder"] = {"hostpath_root": "/tmp/hostpath_pv"}
+            opts["persistentvolume-binder"]["hostpath_root"] = "/tmp/hostpath_pv"
+        opts["nodeipam"]["service_cluster_ip_range"] = a.service_cluster_ip_range
+        resync = {ctl: _dur(getattr(a, f[2:].replace("-", "_"))) for f, (ctl, _) in RESYNC_FLAGS.items()}
         enabled = a.controllers.split(",")
         if not a.enable_garbage_collector:
             enabled.append("-garbagecollector")
@@ -113,10 +119,15 @@ def main(argv=None):
 
             def sa_factory(token):
                 return Client(root.url, token=token, ssl_context=root.http.ssl, max_conns=16,
-                              qps=a.kube_api_qps, burst=a.kube_api_burst)
+                              qps=a.kube_api_qps, burst=a.kube_api_burst, content_type=a.kube_api_content_type)
+        if a.contention_profiling and a.profiling:
+            from ..utils.profiling import enable_contention_profiling
+            enable_contention_profiling()
         cm = await ControllerManager(client, enabled, opts, workers=workers,
                                      start_interval=_dur(a.controller_start_interval),
-                                     sa_client_factory=sa_factory).start()
+                                     sa_client_factory=sa_factory, resync=_dur(a.min_resync_period),
+                                     resync_periods=resync,
+                                     attach_detach_reconcile=not a.disable_attach_detach_reconcile_sync).start()
         health.metrics = cm
         return cm
 
@@ -133,19 +144,32 @@ def _bool(v):
     return str(v).lower() not in ("false", "0", "no")
 
 
+# flag -> (controller, reference default)
+RESYNC_FLAGS = {"--deployment-controller-sync-period": ("deployment", "30s"),
+                "--namespace-sync-period": ("namespace", "5m"),
+                "--pvclaimbinder-sync-period": ("persistentvolume-binder", "15s"),
+                "--resource-quota-sync-period": ("resourcequota", "5m"),
+                "--service-sync-period": ("service", "5m"),
+                "--attach-detach-reconcile-sync-period": ("attachdetach", "1m")}
+
+
 def _reference_flags(ap):
     """The rest of kube-controller-manager's flags (cmd/kube-controller-manager/app/options)."""
     g = ap.add_argument_group("serving")
     g.add_argument("--port", type=int, default=10252, help="/healthz, /metrics, /configz (0 = off)")
     g.add_argument("--address", default="0.0.0.0")
     g.add_argument("--profiling", type=_bool, default=True)
-    g.add_argument("--contention-profiling", type=_bool, default=False, help="accepted")
+    g.add_argument("--contention-profiling", type=_bool, default=False,
+                   help="sample where the event loop blocks, served at /debug/pprof/block (with --profiling)")
     g.add_argument("--kube-api-qps", type=float, default=20.0)
     g.add_argument("--kube-api-burst", type=int, default=30)
-    g.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
-                   help="accepted; the client speaks JSON")
+    g.add_argument("--kube-api-content-type", default="application/json",
+                   choices=["application/json", "application/vnd.kubernetes.protobuf"],
+                   help="wire format of API requests (the reference defaults to protobuf; JSON is this "
+                        "client's faster path)")
     g.add_argument("--controller-start-interval", default="0s")
-    g.add_argument("--min-resync-period", default="12h", help="accepted; informers resync on watch restarts")
+    g.add_argument("--min-resync-period", default="12h",
+                   help="the shared informers re-deliver every cached object every [min, 2*min)")
     g = ap.add_argument_group("controller workers")
     for name, d in (("deployment", 5), ("replicaset", 5), ("rc", 5), ("endpoint", 5), ("gc", 20), ("namespace", 10),
                     ("resource-quota", 5), ("service", 1), ("serviceaccount-token", 5)):
@@ -154,39 +178,42 @@ def _reference_flags(ap):
     g.add_argument("--horizontal-pod-autoscaler-upscale-delay", default="3m")
     g.add_argument("--horizontal-pod-autoscaler-downscale-delay", default="5m")
     g.add_argument("--horizontal-pod-autoscaler-tolerance", type=float, default=0.1)
-    g.add_argument("--horizontal-pod-autoscaler-use-rest-clients", type=_bool, default=True,
-                   help="accepted; metrics always come through the metrics API")
+    unsupported(g, "--horizontal-pod-autoscaler-use-rest-clients", True, _bool,
+                "metrics always come through the resource metrics API (the Heapster client is not built)")
     g.add_argument("--experimental-cluster-signing-duration", default="8760h")
     g.add_argument("--enable-garbage-collector", type=_bool, default=True)
     g.add_argument("--enable-hostpath-provisioner", type=_bool, default=False,
                    help="dynamic hostPath volumes under /tmp/hostpath_pv (single-node testing)")
-    g.add_argument("--enable-dynamic-provisioning", type=_bool, default=True, help="accepted")
-    g.add_argument("--service-cluster-ip-range", default="", help="accepted")
+    g.add_argument("--enable-dynamic-provisioning", type=_bool, default=True,
+                   help="false: claims only bind to existing PersistentVolumes")
+    g.add_argument("--service-cluster-ip-range", default="",
+                   help="node CIDR allocation (--allocate-node-cidrs) never hands out blocks overlapping it")
     g.add_argument("--cidr-allocator-type", default="RangeAllocator", choices=["RangeAllocator", "CloudAllocator"])
     g.add_argument("--cluster-name", default="kubernetes")
-    for f in ("--deployment-controller-sync-period", "--namespace-sync-period", "--pvclaimbinder-sync-period",
-              "--resource-quota-sync-period", "--service-sync-period", "--node-sync-period",
-              "--attach-detach-reconcile-sync-period"):
-        g.add_argument(f, default="", help="accepted; controllers resync from watch events")
-    g.add_argument("--disable-attach-detach-reconcile-sync", type=_bool, default=False, help="accepted")
-    g.add_argument("--flex-volume-plugin-dir", default="/usr/libexec/kubernetes/kubelet-plugins/volume/exec/",
-                   help="accepted (FlexVolume attach runs in the kubelet)")
+    for f, d in RESYNC_FLAGS.items():
+        g.add_argument(f, default=d[1], help=f"period of the {d[0]} controller's full resync (0 = only on events)")
+    deprecated_noop(g, "--node-sync-period", "0s", str, "options.go:158-161")
+    g.add_argument("--disable-attach-detach-reconcile-sync", type=_bool, default=False,
+                   help="the attach/detach controller reconciles on events only")
+    unsupported(g, "--flex-volume-plugin-dir", "/usr/libexec/kubernetes/kubelet-plugins/volume/exec/", str,
+                "FlexVolume attach/detach runs in the kubelet, not the controller manager")
     g.add_argument("--use-service-account-credentials", type=_bool, default=False,
                    help="run each controller as its own kube-system service account "
                         "(bound to its system:controller:<name> role)")
+    why = "volumes are recycled in-process by the PV controller (no recycler pod)"
     for f in ("--pv-recycler-pod-template-filepath-nfs", "--pv-recycler-pod-template-filepath-hostpath"):
-        g.add_argument(f, default="", help="accepted")
-    for f in ("--pv-recycler-minimum-timeout-nfs", "--pv-recycler-increment-timeout-nfs",
-              "--pv-recycler-minimum-timeout-hostpath", "--pv-recycler-timeout-increment-hostpath"):
-        g.add_argument(f, type=int, default=0, help="accepted")
-    g = ap.add_argument_group("no-ops kept for command-line compatibility")
-    g.add_argument("--cloud-provider", default="")
-    g.add_argument("--cloud-config", default="")
-    g.add_argument("--allow-untagged-cloud", type=_bool, default=False)
-    g.add_argument("--insecure-experimental-approve-all-kubelet-csrs-for-group", default="")
-    g.add_argument("--deleting-pods-qps", type=float, default=0.1)
-    g.add_argument("--deleting-pods-burst", type=int, default=0)
-    g.add_argument("--register-retry-count", type=int, default=10)
+        unsupported(g, f, "", str, why)
+    for f, d in (("--pv-recycler-minimum-timeout-nfs", 300), ("--pv-recycler-increment-timeout-nfs", 30),
+                 ("--pv-recycler-minimum-timeout-hostpath", 60), ("--pv-recycler-timeout-increment-hostpath", 30)):
+        unsupported(g, f, d, int, why)
+    g = ap.add_argument_group("cloud provider and deprecated flags")
+    g.add_argument("--cloud-provider", default="", help="'' only: cloud providers are out of scope")
+    unsupported(g, "--cloud-config", "", str, "cloud providers are out of scope")
+    unsupported(g, "--allow-untagged-cloud", False, _bool, "cloud providers are out of scope")
+    deprecated_noop(g, "--insecure-experimental-approve-all-kubelet-csrs-for-group", "", str, "options.go:203-204")
+    deprecated_noop(g, "--deleting-pods-qps", 0.1, float, "options.go:183-184")
+    deprecated_noop(g, "--deleting-pods-burst", 0, int, "options.go:185-186")
+    deprecated_noop(g, "--register-retry-count", 10, int, "options.go:187-189")
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@ from ..kubelet.kubelet import Kubelet
 from ..kubelet.runtime.process import ProcessRuntime
 from ..kubelet.runtime.stub import StubRuntime
 from ..utils.features import DefaultFeatureGate
-from ._common import run_until_signal, setup_logging
+from ._common import check_unsupported, deprecated_noop, run_until_signal, setup_logging, unsupported
 
 
 def main(argv=None):
@@ -94,11 +94,19 @@ def main(argv=None):
     _reference_flags(ap)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
+    check_unsupported(ap, a)
+    enforce = {x.strip() for x in a.enforce_node_allocatable.split(",") if x.strip()}
+    if not enforce <= {"pods", "none"} or ("none" in enforce and len(enforce) > 1):
+        ap.error(f"--enforce-node-allocatable={a.enforce_node_allocatable!r}: only 'pods' or 'none' are supported "
+                 "(system-reserved/kube-reserved need their cgroups, which this kubelet does not manage)")
     setup_logging(a.v)
     DefaultFeatureGate.set(a.feature_gates)
     _host_checks(a)
 
     async def start():
+        if a.contention_profiling:
+            from ..utils.profiling import enable_contention_profiling
+            enable_contention_profiling()
         if a.experimental_bootstrap_kubeconfig and not a.bootstrap_kubeconfig:
             a.bootstrap_kubeconfig = a.experimental_bootstrap_kubeconfig
         if a.bootstrap_kubeconfig and a.kubeconfig and not os.path.exists(a.kubeconfig):
@@ -107,10 +115,11 @@ def main(argv=None):
                                                os.path.join(a.root_dir, "pki"))
         if a.kubeconfig:
             from ..client.clientcmd import client_from
-            client = client_from(a.kubeconfig, max_conns=32, qps=a.kube_api_qps, burst=a.kube_api_burst)
+            client = client_from(a.kubeconfig, max_conns=32, qps=a.kube_api_qps, burst=a.kube_api_burst,
+                                 content_type=a.kube_api_content_type)
         else:
             client = Client(a.master or "http://127.0.0.1:8080", token=a.token, max_conns=32, qps=a.kube_api_qps,
-                            burst=a.kube_api_burst)
+                            burst=a.kube_api_burst, content_type=a.kube_api_content_type)
         pdir = a.device_plugins_dir or os.path.join(a.root_dir, "device-plugin", "plugins")
         dm = ManagerImpl(pdir) if DefaultFeatureGate("DevicePlugins") else ManagerStub()
         if a.container_runtime == "remote":
@@ -180,6 +189,7 @@ def main(argv=None):
                     allocatable_ignore_eviction=a.experimental_allocatable_ignore_eviction,
                     serialize_image_pulls=a.serialize_image_pulls, registry_qps=a.registry_qps,
                     registry_burst=a.registry_burst, file_check_frequency=_duration(a.file_check_frequency), sync_frequency=_duration(a.sync_frequency),
+                    cpu_cfs_quota=a.cpu_cfs_quota, enforce_node_allocatable="none" not in enforce,
                     http_check_frequency=_duration(a.http_check_frequency), register=a.register_node)
         if not a.anonymous_auth or a.authentication_token_webhook or a.authorization_mode != "AlwaysAllow" or a.client_ca_file:
             from ..kubelet.server_auth import KubeletAuth
@@ -299,8 +309,8 @@ def _reference_flags(ap):
     g.add_argument("--authentication-token-webhook-cache-ttl", default="2m")
     g.add_argument("--authorization-webhook-cache-authorized-ttl", default="5m")
     g.add_argument("--authorization-webhook-cache-unauthorized-ttl", default="30s")
-    g.add_argument("--streaming-connection-idle-timeout", default="4h",
-                   help="accepted; streams end when either side closes")
+    unsupported(g, "--streaming-connection-idle-timeout", "4h", str, "exec/attach/port-forward streams end when "
+                "either side closes; no idle timer")
     g = ap.add_argument_group("registration")
     g.add_argument("--register-node", type=_bool, default=True)
     g.add_argument("--register-with-taints", default="", help="key=value:Effect,... applied at registration")
@@ -336,8 +346,10 @@ def _reference_flags(ap):
     g = ap.add_argument_group("API client")
     g.add_argument("--kube-api-qps", type=float, default=5.0)
     g.add_argument("--kube-api-burst", type=int, default=10)
-    g.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
-                   help="accepted; this kubelet's client speaks JSON")
+    g.add_argument("--kube-api-content-type", default="application/json",
+                   choices=["application/json", "application/vnd.kubernetes.protobuf"],
+                   help="wire format of API requests (the reference defaults to protobuf; JSON is this "
+                        "client's faster path)")
     g.add_argument("--experimental-bootstrap-kubeconfig", default=None, help="deprecated alias of --bootstrap-kubeconfig")
     g.add_argument("--require-kubeconfig", type=_bool, default=False, help="deprecated no-op, as in the reference")
     g = ap.add_argument_group("host")
@@ -350,32 +362,42 @@ def _reference_flags(ap):
     g.add_argument("--exit-on-lock-contention", type=_bool, default=False)
     g.add_argument("--cgroup-driver", default="cgroupfs", help="cgroupfs or systemd (both manage the cgroup v2 tree directly)")
     g.add_argument("--enforce-node-allocatable", default="pods",
-                   help="accepted; node allocatable is enforced on the pods (kubepods) cgroup with --cgroups-per-qos")
+                   help="'pods': node allocatable caps the kubepods cgroup (with --cgroups-per-qos); 'none': no cap")
     for f in ("--kubelet-cgroups", "--system-cgroups", "--kube-reserved-cgroup", "--system-reserved-cgroup"):
-        g.add_argument(f, default="", help="accepted; system daemons are not moved into cgroups by this kubelet")
-    g.add_argument("--cpu-cfs-quota", type=_bool, default=True, help="accepted; CPU limits are always enforced via cpu.max")
-    g.add_argument("--cpu-manager-reconcile-period", default="10s", help="accepted; assignments are applied at container start")
-    g.add_argument("--experimental-qos-reserved", default="", help="accepted (alpha QOSReserved)")
-    g.add_argument("--seccomp-profile-root", default="", help="accepted; seccomp profiles are not applied by this runtime")
+        unsupported(g, f, "", str, "system daemons are not moved into cgroups by this kubelet")
+    g.add_argument("--cpu-cfs-quota", type=_bool, default=True,
+                   help="enforce CPU limits with a CFS quota (cpu.max); false: limits only shape requests")
+    unsupported(g, "--cpu-manager-reconcile-period", "10s", str, "CPU assignments are applied at container start")
+    unsupported(g, "--experimental-qos-reserved", "", str, "alpha QOSReserved is not implemented")
+    unsupported(g, "--seccomp-profile-root", "/var/lib/kubelet/seccomp", str,
+                "localhost seccomp profiles are not applied by this runtime")
     g = ap.add_argument_group("networking")
     g.add_argument("--network-plugin-mtu", type=int, default=0, help="kubenet bridge MTU (0: 1460)")
     g.add_argument("--hairpin-mode", default="promiscuous-bridge", choices=["promiscuous-bridge", "hairpin-veth", "none"],
                    help="kubenet: bridge promiscuous mode, or hairpin on each pod's veth port")
-    g.add_argument("--non-masquerade-cidr", default="10.0.0.0/8", help="accepted")
-    g.add_argument("--make-iptables-util-chains", type=_bool, default=True, help="accepted")
-    g.add_argument("--iptables-masquerade-bit", type=int, default=14, help="accepted")
-    g.add_argument("--iptables-drop-bit", type=int, default=15, help="accepted")
-    g = ap.add_argument_group("no-ops kept for command-line compatibility")
-    for f, d in (("--cadvisor-port", 0), ("--chaos-chance", 0.0)):
-        g.add_argument(f, type=type(d), default=d)
-    for f in ("--containerized", "--contention-profiling", "--enable-custom-metrics", "--really-crash-for-testing",
-              "--experimental-check-node-capabilities-before-mount", "--experimental-kernel-memcg-notification",
-              "--keep-terminated-pod-volumes", "--runonce"):
-        g.add_argument(f, type=_bool, default=False)
-    g.add_argument("--enable-controller-attach-detach", type=_bool, default=True)
-    for f in ("--experimental-mounter-path", "--init-config-dir", "--master-service-namespace",
-              "--volume-stats-agg-period"):
-        g.add_argument(f, default="")
+    why = "the kubelet does not program KUBE-MARK-* iptables chains (kube-proxy owns the NAT rules)"
+    unsupported(g, "--non-masquerade-cidr", "10.0.0.0/8", str, why)
+    unsupported(g, "--make-iptables-util-chains", True, _bool, why)
+    unsupported(g, "--iptables-masquerade-bit", 14, int, why)
+    unsupported(g, "--iptables-drop-bit", 15, int, why)
+    g = ap.add_argument_group("subsystems this kubelet does not have")
+    unsupported(g, "--cadvisor-port", 0, int, "no embedded cAdvisor; stats come from the summary API")
+    unsupported(g, "--chaos-chance", 0.0, float, "no fault-injecting client")
+    for f, why in (("--containerized", "the kubelet runs on the host"),
+                   ("--really-crash-for-testing", "test-only panic mode"),
+                   ("--experimental-check-node-capabilities-before-mount", "mount utilities are not probed"),
+                   ("--experimental-kernel-memcg-notification", "eviction polls memory; no memcg threshold events"),
+                   ("--runonce", "run-once mode is not implemented")):
+        unsupported(g, f, False, _bool, why)
+    g.add_argument("--contention-profiling", type=_bool, default=False,
+                   help="sample where the event loop blocks, served at /debug/pprof/block")
+    deprecated_noop(g, "--enable-custom-metrics", False, _bool, "options.go:368")
+    unsupported(g, "--keep-terminated-pod-volumes", False, _bool, "volumes of terminated pods are torn down")
+    unsupported(g, "--enable-controller-attach-detach", True, _bool,
+                "attach/detach is always the controller's (the kubelet only mounts)")
+    for f, d in (("--experimental-mounter-path", ""), ("--init-config-dir", ""),
+                 ("--master-service-namespace", "default"), ("--volume-stats-agg-period", "1m")):
+        unsupported(g, f, d, str, "not implemented by this kubelet")
 
 
 if __name__ == "__main__":

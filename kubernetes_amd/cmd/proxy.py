@@ -6,7 +6,7 @@ import os
 
 from ..client.rest import Client
 from ..proxy.server import ProxyServer
-from ._common import run_until_signal, setup_logging
+from ._common import check_unsupported, run_until_signal, setup_logging, unsupported
 
 
 def main(argv=None):
@@ -30,6 +30,7 @@ def main(argv=None):
     _reference_flags(ap)
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
+    check_unsupported(ap, a)
     setup_logging(a.v)
     if a.config:
         apply_config_file(a, a.config)
@@ -67,13 +68,15 @@ def main(argv=None):
                 ipvs = ExecIPVS()
         if a.kubeconfig:
             from ..client.clientcmd import client_from
-            client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=a.kube_api_burst)
+            client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=a.kube_api_burst, content_type=a.kube_api_content_type)
         else:
-            client = Client(a.master or "http://127.0.0.1:8080", token=a.token, qps=a.kube_api_qps, burst=a.kube_api_burst)
+            client = Client(a.master or "http://127.0.0.1:8080", token=a.token, qps=a.kube_api_qps, burst=a.kube_api_burst,
+                            content_type=a.kube_api_content_type)
         ps = ProxyServer(client, a.hostname_override, a.proxy_mode, a.cluster_cidr,
                          a.masquerade_all, a.iptables_sync_period, a.iptables_min_sync_period,
                          healthz_port=a.healthz_port, metrics_port=a.metrics_port, iptables=iptables, ipvs=ipvs,
-                         ipvs_scheduler=a.ipvs_scheduler, bind=a.bind_address, masquerade_bit=a.iptables_masquerade_bit)
+                         ipvs_scheduler=a.ipvs_scheduler, bind=a.bind_address, masquerade_bit=a.iptables_masquerade_bit,
+                         resync=_dur(a.config_sync_period), profiling=a.profiling)
         await ps.start()
         print(f"kube-proxy {a.hostname_override} running (mode={a.proxy_mode})", flush=True)
         return ps
@@ -110,13 +113,16 @@ def _reference_flags(ap):
     ap.add_argument("--oom-score-adj", type=int, default=-999)
     ap.add_argument("--kube-api-qps", type=float, default=5.0)
     ap.add_argument("--kube-api-burst", type=int, default=10)
-    ap.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
-                    help="accepted; the client speaks JSON")
-    ap.add_argument("--config-sync-period", default="15m", help="accepted; informers resync on watch restarts")
-    ap.add_argument("--proxy-port-range", default="", help="userspace mode: accepted (ports come from the OS)")
-    ap.add_argument("--udp-timeout", default="250ms", help="userspace mode: accepted")
-    ap.add_argument("--resource-container", default="/kube-proxy", help="deprecated; accepted")
-    ap.add_argument("--profiling", type=_bool, default=False, help="accepted")
+    ap.add_argument("--kube-api-content-type", default="application/json",
+                    choices=["application/json", "application/vnd.kubernetes.protobuf"],
+                    help="wire format of API requests (the reference defaults to protobuf; JSON is this "
+                         "client's faster path)")
+    ap.add_argument("--config-sync-period", default="15m",
+                    help="the service/endpoints informers re-deliver every object every [p, 2p), re-syncing the rules")
+    unsupported(ap, "--proxy-port-range", "", str, "userspace-mode proxy ports come from the OS")
+    unsupported(ap, "--udp-timeout", "250ms", str, "the userspace proxier keeps no UDP sessions")
+    unsupported(ap, "--resource-container", "", str, "kube-proxy is not moved into a cgroup of its own")
+    ap.add_argument("--profiling", type=_bool, default=False, help="serve /debug/pprof on the metrics port")
 
 
 def write_config(a, path):

@@ -45,20 +45,29 @@ def _parser():
     ap.add_argument("--port", type=int, default=10251, help="/healthz and /metrics (0 = off; shard i uses port+i)")
     ap.add_argument("--address", default="0.0.0.0")
     ap.add_argument("--kube-api-burst", type=int, default=None)
-    ap.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
-                    help="accepted; the client speaks JSON")
+    ap.add_argument("--kube-api-content-type", default="application/json",
+                    choices=["application/json", "application/vnd.kubernetes.protobuf"],
+                    help="wire format of API requests (the reference defaults to protobuf; JSON is this "
+                         "client's faster path, protobuf is served for the kinds the schema covers)")
     ap.add_argument("--lock-object-name", default="kube-scheduler")
     ap.add_argument("--lock-object-namespace", default="kube-system")
     ap.add_argument("--hard-pod-affinity-symmetric-weight", type=int, default=1,
                     help="score an existing pod's required pod affinity gives a matching incoming pod (0-100)")
     ap.add_argument("--failure-domains", default="kubernetes.io/hostname,failure-domain.beta.kubernetes.io/zone,"
-                    "failure-domain.beta.kubernetes.io/region", help="accepted (deprecated in 1.9)")
+                    "failure-domain.beta.kubernetes.io/region",
+                    help="labels an empty topologyKey in a preferred pod (anti-)affinity term stands for "
+                         "(deprecated in 1.9)")
     ap.add_argument("--use-legacy-policy-config", action="store_true",
                     help="read --policy-config-file even when --config is given")
-    ap.add_argument("--profiling", default="true")
-    ap.add_argument("--contention-profiling", default="false", help="accepted")
+    ap.add_argument("--profiling", default="true", help="serve /debug/pprof on the metrics port")
+    ap.add_argument("--contention-profiling", default="false",
+                    help="sample where the event loop blocks, served at /debug/pprof/block")
     ap.add_argument("-v", type=int, default=0)
     return ap
+
+
+def _true(v):
+    return str(v).lower() in ("true", "1", "yes")
 
 
 def supervise(argv, n):
@@ -132,10 +141,11 @@ def main(argv=None):
         if a.kubeconfig:
             from ..client.clientcmd import client_from
             client = client_from(a.kubeconfig, qps=a.kube_api_qps, burst=a.kube_api_burst or int(a.kube_api_qps or 10),
-                                 max_conns=64)
+                                 max_conns=64, content_type=a.kube_api_content_type)
         else:
             client = Client(a.master or "http://127.0.0.1:8080", qps=a.kube_api_qps,
-                            burst=a.kube_api_burst or int(a.kube_api_qps or 10), max_conns=64)
+                            burst=a.kube_api_burst or int(a.kube_api_qps or 10), max_conns=64,
+                            content_type=a.kube_api_content_type)
         algo = await SP.resolve_algorithm(client, a.algorithm_provider, a.policy_config_file,
                                           a.policy_configmap, a.policy_configmap_namespace)
         preds, prios, ext_cfgs = algo
@@ -146,7 +156,12 @@ def main(argv=None):
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
                       emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,
                       shard_count=a.shard_count, preemption=not a.disable_preemption,
-                      hard_pod_affinity_symmetric_weight=a.hard_pod_affinity_symmetric_weight)
+                      hard_pod_affinity_symmetric_weight=a.hard_pod_affinity_symmetric_weight,
+                      failure_domains=[d for d in a.failure_domains.split(",") if d])
+        s.profiling = _true(a.profiling)
+        if _true(a.contention_profiling):
+            from ..utils.profiling import enable_contention_profiling
+            enable_contention_profiling()
         if a.leader_elect:
             from ..client.leaderelection import LeaderElector
             lock = a.lock_object_name if a.shard_count == 1 else f"{a.lock_object_name}-shard-{a.shard_index}"

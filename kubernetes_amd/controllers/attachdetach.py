@@ -30,6 +30,10 @@ def csi_source(pv):
 class AttachDetachController(Controller):
     name = "attachdetach"
     workers = 1
+    disable_reconcile_sync = False   # --disable-attach-detach-reconcile-sync
+
+    def resync_keys(self):
+        return [] if self.disable_reconcile_sync else ["reconcile"]
 
     def setup(self):
         self.pods = self.factory.get("pods")

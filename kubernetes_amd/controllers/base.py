@@ -61,6 +61,12 @@ class Expectations:
 class Controller:
     name = "controller"
     workers = 4
+    # full resync (`--deployment-controller-sync-period`, `--namespace-sync-period`,
+    # `--resource-quota-sync-period`, `--pvclaimbinder-sync-period`, `--service-sync-period`,
+    # `--attach-detach-reconcile-sync-period`): every `resync_period` seconds each key from
+    # resync_keys() is queued again, whether or not a watch event touched it; 0 = off
+    resync_period = 0.0
+    primary = None            # resource whose objects are the controller's keys
 
     def __init__(self, client, factory, recorder: EventRecorder | None = None):
         self.client = client
@@ -98,9 +104,22 @@ class Controller:
             finally:
                 self.queue.done(key)
 
+    def resync_keys(self):
+        if self.primary is None:
+            return []
+        return [m.ns_name(o) for o in self.factory.get(self.primary).list()]
+
+    async def _resync(self):
+        while True:
+            await asyncio.sleep(self.resync_period)
+            for k in self.resync_keys():
+                self.queue.add(k)
+
     def start(self):
         self.recorder.start()
         self._tasks = [asyncio.ensure_future(self._worker()) for _ in range(self.workers)]
+        if self.resync_period > 0:
+            self._tasks.append(asyncio.ensure_future(self._resync()))
 
     def stop(self):
         self.queue.shutdown()

@@ -36,6 +36,7 @@ def _resolve(v, total, round_up):
 
 class DeploymentController(Controller):
     name = "deployment"
+    primary = "deployments"
     workers = 2
 
     def setup(self):

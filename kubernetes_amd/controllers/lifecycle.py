@@ -24,6 +24,7 @@ from .base import Controller, split_key
 
 class NamespaceController(Controller):
     name = "namespace"
+    primary = "namespaces"
     workers = 2
 
     def setup(self):

@@ -17,7 +17,7 @@ from __future__ import annotations
 import asyncio
 import logging
 
-from ..client.informer import InformerFactory
+from ..client.informer import InformerFactory, resync_period
 from .daemonset import DaemonSetController, StatefulSetController
 from .deployment import DeploymentController
 from .job import CronJobController, JobController
@@ -163,16 +163,20 @@ class ServiceAccountClients:
 class ControllerManager:
     """`workers`: {controller name: worker count} (--concurrent-*-syncs); `start_interval`:
     seconds between controller starts (--controller-start-interval); `sa_client_factory`:
-    token -> client, set for --use-service-account-credentials."""
+    token -> client, set for --use-service-account-credentials; `resync`: --min-resync-period
+    in seconds (0 = informers never resync)."""
 
     def __init__(self, client, controllers=None, options=None, workers=None, start_interval=0.0,
-                 sa_client_factory=None):
+                 sa_client_factory=None, resync=0.0, resync_periods=None, attach_detach_reconcile=True):
         self.client = client
-        self.factory = InformerFactory(client)
+        # --min-resync-period: the shared informers resync every [min, 2*min)
+        self.factory = InformerFactory(client, resync_period(resync))
         self.controllers = []
         self.start_interval = start_interval
         self.options = options or {}
         self.workers = workers or {}
+        self.resync_periods = resync_periods or {}      # controller -> full-resync seconds
+        self.attach_detach_reconcile = attach_detach_reconcile
         self.names = resolve(controllers)
         self.sa_clients = ServiceAccountClients(client, sa_client_factory) if sa_client_factory else None
         self.identities = {}          # controller name -> the identity it runs as
@@ -186,6 +190,10 @@ class ControllerManager:
         c = cls(client, self.factory, **self.options.get(name, {}))
         if self.workers.get(name):
             c.workers = int(self.workers[name])
+        if self.resync_periods.get(name):
+            c.resync_period = float(self.resync_periods[name])
+        if name == "attachdetach":
+            c.disable_reconcile_sync = not self.attach_detach_reconcile
         c.setup()
         self.controllers.append(c)
         return c

@@ -109,6 +109,7 @@ class EndpointsController(Controller):
 
 class ResourceQuotaController(Controller):
     name = "resourcequota"
+    primary = "resourcequotas"
     workers = 2
 
     def setup(self):

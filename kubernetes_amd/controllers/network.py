@@ -51,6 +51,20 @@ class CIDRSet:
         self.used.add(i)
         return True
 
+    def exclude(self, cidr):
+        """Mark every node block that overlaps `cidr` used (`filterOutServiceRange` of
+        pkg/controller/node/ipam/range_allocator.go: the service range is never a pod CIDR)."""
+        other = ipaddress.ip_network(cidr, strict=False)
+        if other.version != self.net.version or not self.net.overlaps(other):
+            return 0
+        lo = max(int(self.net.network_address), int(other.network_address))
+        hi = min(int(self.net.broadcast_address), int(other.broadcast_address))
+        shift = self.net.max_prefixlen - self.mask
+        first = (lo - int(self.net.network_address)) >> shift
+        last = (hi - int(self.net.network_address)) >> shift
+        self.used.update(range(first, last + 1))
+        return last - first + 1
+
     def release(self, cidr):
         i = self._index(cidr)
         if i is not None:
@@ -70,9 +84,12 @@ class NodeIPAMController(Controller):
     name = "nodeipam"
     workers = 1
 
-    def __init__(self, client, factory, cluster_cidr="10.244.0.0/16", node_cidr_mask_size=24, **kw):
+    def __init__(self, client, factory, cluster_cidr="10.244.0.0/16", node_cidr_mask_size=24,
+                 service_cluster_ip_range="", **kw):
         super().__init__(client, factory, **kw)
         self.cidrs = CIDRSet(cluster_cidr, node_cidr_mask_size)
+        if service_cluster_ip_range:          # --service-cluster-ip-range
+            self.cidrs.exclude(service_cluster_ip_range)
         self.owner: dict[str, str] = {}          # node name -> allocated CIDR
 
     def setup(self):
@@ -122,6 +139,7 @@ def _range(spec):
 
 class ServiceLBController(Controller):
     name = "service"
+    primary = "services"
     workers = 1
 
     def __init__(self, client, factory, ip_range="", **kw):

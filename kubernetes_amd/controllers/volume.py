@@ -87,9 +87,15 @@ class PersistentVolumeController(Controller):
     name = "persistentvolume-binder"
     workers = 1      # binding decisions are serialized, like the reference's single sync loop
 
-    def __init__(self, client, factory, hostpath_root=None, **kw):
+    def __init__(self, client, factory, hostpath_root=None, enable_dynamic_provisioning=True, **kw):
         super().__init__(client, factory, **kw)
         self.hostpath_root = hostpath_root or os.path.join(os.environ.get("TMPDIR", "/tmp"), "kamd-hostpath-pv")
+        # --enable-dynamic-provisioning=false: claims only bind to existing volumes
+        self.enable_dynamic_provisioning = enable_dynamic_provisioning
+
+    def resync_keys(self):
+        return (["claim:" + _key(c) for c in self.pvc_inf.list()] +
+                ["volume:" + v["metadata"]["name"] for v in self.pv_inf.list()])
 
     def setup(self):
         self.pv_inf = self.factory.get("persistentvolumes")
@@ -165,6 +171,8 @@ class PersistentVolumeController(Controller):
                                     pvc["metadata"]["namespace"], "merge", "status")
 
     async def _provision(self, pvc):
+        if not self.enable_dynamic_provisioning:
+            return None
         cls = claim_class(pvc)
         sc = self.sc_inf.get(cls) if cls else None
         if sc is None or sc.get("provisioner") != HOSTPATH_PROVISIONER:

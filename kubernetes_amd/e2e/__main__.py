@@ -17,7 +17,9 @@ def main(argv=None):
     a = ap.parse_args(argv)
     results = asyncio.run(run_specs(a.server, a.focus, a.skip, a.token, timeout=a.timeout))
     failed = [r for r in results if not r.ok]
-    print(f"\nRan {len(results)} specs: {len(results) - len(failed)} passed, {len(failed)} failed")
+    skipped = sum(r.skipped for r in results)
+    print(f"\nRan {len(results)} specs: {len(results) - len(failed) - skipped} passed, {len(failed)} failed, "
+          f"{skipped} skipped")
     for r in failed:
         print(f"--- {r.name}\n{r.error}")
     return 1 if failed else 0

@@ -31,6 +31,11 @@ def conformance(name, *tags):
     return spec(f"[Conformance] {name}", "Conformance", *tags)
 
 
+class Skip(Exception):
+    """Raised by a spec whose prerequisites the cluster lacks (ginkgo's `framework.Skipf`, e.g.
+    `SkipUnlessNodeCountIsAtLeast`): reported as SKIP, neither pass nor failure."""
+
+
 class Framework:
     def __init__(self, client, base_name="e2e"):
         self.client = client
@@ -77,8 +82,9 @@ class Framework:
 
 
 class Result:
-    def __init__(self, name, ok, seconds, error=""):
+    def __init__(self, name, ok, seconds, error="", skipped=False):
         self.name, self.ok, self.seconds, self.error = name, ok, seconds, error
+        self.skipped = skipped
 
 
 async def run_specs(server, focus=None, skip=None, token=None, ssl_context=None, timeout=180.0, out=print):
@@ -98,6 +104,9 @@ async def run_specs(server, focus=None, skip=None, token=None, ssl_context=None,
                 await asyncio.wait_for(fn(f), timeout)
                 results.append(Result(label, True, time.monotonic() - t0))
                 out(f"  PASS  {label} ({time.monotonic() - t0:.2f}s)")
+            except Skip as e:
+                results.append(Result(label, True, time.monotonic() - t0, str(e), skipped=True))
+                out(f"  SKIP  {label}: {e}")
             except Exception as e:  # noqa: BLE001 - a failing spec is a result, not a crash
                 results.append(Result(label, False, time.monotonic() - t0, f"{type(e).__name__}: {e}\n"
                                                                           f"{traceback.format_exc(limit=3)}"))

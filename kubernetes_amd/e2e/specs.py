@@ -6,7 +6,7 @@ from __future__ import annotations
 import base64
 
 from ..api import core
-from .framework import conformance, spec
+from .framework import Skip, conformance, spec
 
 BUSYBOX = "busybox"
 
@@ -148,6 +148,66 @@ async def gpu_vector_add(f):
     assert all(assigned), assigned
     if n == 2:
         assert set(assigned[0]).isdisjoint(assigned[1]), assigned
+
+
+def _linked(devs):
+    """True when every pair of the devices' packages is joined by an up xGMI link, read from the
+    attributes the plugin publishes (`amd.com/xgmi-node` index + `amd.com/xgmi-peers` bitmask)."""
+    info = []
+    for d in devs:
+        a = d.get("attributes") or {}
+        info.append((a.get(core.ATTR_HIVE), int(a[core.ATTR_XGMI_NODE]), int(a[core.ATTR_XGMI_PEERS], 16)))
+    for i, (hi, ni, mi) in enumerate(info):
+        for hj, nj, mj in info[i + 1:]:
+            if hi != hj or (ni != nj and not ((mi >> nj) & 1 and (mj >> ni) & 1)):
+                return False
+    return True
+
+
+XGMI_RANKS = 4
+XGMI_MIN_BUSBW_GBPS = 100.0     # an all-reduce that fell back to PCIe (~50 GB/s) fails this floor
+
+
+@spec("GPU: a 4-GPU pod with amd.com/xgmi-policy required gets a pairwise-linked xGMI set and its "
+      "RCCL all-reduce is correct on every rank", "Feature:GPU", "Feature:MultiGPU")
+async def gpu_xgmi_allreduce(f):
+    """Multi-GPU counterpart of nvidia-gpus.go: skipped unless some node has >= 4 healthy GPUs.
+    The pod runs `xgmi-probe` (native/hip/xgmi_probe.cc): a 4-rank RCCL all-reduce over the
+    allocated devices, every element of every rank's buffer checked on the GPU. On a hollow node
+    (stub runtime, fake AMD SMI) no container process runs — the run-seconds annotation ends it —
+    and the spec checks the placement only; on a real node it also checks the probe's result."""
+    import json
+    import os
+    nodes = (await f.client.list("nodes"))["items"]
+
+    def healthy(n):
+        res = (((n.get("status") or {}).get("extendedResources") or {}).get(core.AMD_GPU) or {}).get("resources") or {}
+        return sum(1 for d in res.values() if d.get("health", "Healthy") == "Healthy")
+    if not any(healthy(n) >= XGMI_RANKS for n in nodes):
+        raise Skip(f"no node has {XGMI_RANKS} healthy {core.AMD_GPU}")
+    p = {"metadata": {"name": "xgmi", "annotations": {"amd.com/xgmi-policy": "required",
+                                                       "kubemark.amd.com/run-seconds": "0.2"}},
+         "spec": {"restartPolicy": "Never", "containers": [
+             {"name": "c", "image": "kubernetes-amd/xgmi-probe", "args": ["256", "20"],
+              "resources": {"limits": {core.AMD_GPU: str(XGMI_RANKS)}}}]}}
+    await f.client.create("pods", p, f.ns)
+    pod = await f.pod_phase("xgmi", ("Succeeded",), 240)
+    ids = [d for per in pod["spec"].get("extendedResources") or () for d in per.get("assigned") or ()]
+    assert len(ids) == XGMI_RANKS and len(set(ids)) == XGMI_RANKS, ids
+    node = await f.client.get("nodes", pod["spec"]["nodeName"])
+    devs = node["status"]["extendedResources"][core.AMD_GPU]["resources"]
+    assert _linked([devs[i] for i in ids]), {i: devs[i].get("attributes") for i in ids}
+    log = await f.logs("xgmi")
+    lines = [ln for ln in log.splitlines() if ln.startswith("{") and "busbw_GBps" in ln]
+    if not lines:
+        assert log.startswith("stub container"), f"no probe result in the pod log: {log[-400:]!r}"
+        return
+    r = json.loads(lines[-1])
+    floor = float(os.environ.get("KAMD_E2E_XGMI_MIN_BUSBW_GBPS", XGMI_MIN_BUSBW_GBPS))
+    assert r["ranks"] == XGMI_RANKS, r
+    assert r["elements_checked_per_rank"] * 4 == r["bytes"], r
+    assert r["correct"] and r["bad_elements"] == [0] * XGMI_RANKS, r
+    assert r["busbw_GBps"] >= floor, r
 
 
 @conformance("Pods should be updated (labels) and the update observed by a watch")

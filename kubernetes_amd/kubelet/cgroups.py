@@ -95,8 +95,9 @@ def resource_config_for_pod(pod) -> dict:
 
 
 class CgroupManager:
-    def __init__(self, root, node_allocatable=None):
+    def __init__(self, root, node_allocatable=None, cpu_cfs_quota=True):
         self.root = os.path.abspath(root)
+        self.cpu_cfs_quota = cpu_cfs_quota        # False: cpu limits are not enforced (no cpu.max)
         self.kubepods = os.path.join(self.root, "kubepods")
         self.node_allocatable = node_allocatable or {}      # {"cpu": milli, "memory": bytes}
         self.pods: dict[str, tuple] = {}                     # uid -> (qos, path, pod)
@@ -164,7 +165,7 @@ class CgroupManager:
         if uid not in self.pods:
             self._mkdir(d)
             cfg = resource_config_for_pod(pod)
-            self._apply(d, cfg["cpu_shares"], cfg["cpu_quota"], cfg["memory_limit"])
+            self._apply(d, cfg["cpu_shares"], cfg["cpu_quota"] if self.cpu_cfs_quota else None, cfg["memory_limit"])
             self.pods[uid] = (q, d, pod)
             if q == BURSTABLE:
                 self.update_qos()

@@ -121,11 +121,14 @@ class Kubelet:
                  host_sources=None, eviction_soft=None, eviction_soft_grace_period=None, eviction_minimum_reclaim=None,
                  eviction_max_pod_grace_period=0, eviction_pressure_transition_period=0.0,
                  allocatable_ignore_eviction=False, serialize_image_pulls=False, registry_qps=0.0, registry_burst=10,
-                 file_check_frequency=20.0, http_check_frequency=20.0, sync_frequency=60.0):
+                 file_check_frequency=20.0, http_check_frequency=20.0, sync_frequency=60.0, cpu_cfs_quota=True,
+                 enforce_node_allocatable=True):
         self.file_check_frequency, self.http_check_frequency = file_check_frequency, http_check_frequency
         # --sync-frequency: how often running pods' configMap / secret / downwardAPI / projected
         # volumes are re-projected (`kubelet.go` syncLoop's periodic sync, 1m)
         self.sync_frequency = sync_frequency
+        self.cpu_cfs_quota = cpu_cfs_quota      # --cpu-cfs-quota=false: CPU limits set no cpu.max
+        self.enforce_node_allocatable = enforce_node_allocatable   # --enforce-node-allocatable=none: False
         self.client = client
         # :10250 serving (cmd/kubelet/app/server.go): TLS = (cert file, key file, client CA file or
         # None) or None for plain HTTP; --read-only-port (unauthenticated, no debugging handlers)
@@ -286,7 +289,8 @@ class Kubelet:
             alloc = self._allocatable(self.capacity)
             self.cgroups = CgroupManager(self.cgroup_root, {
                 "cpu": parse_quantity(str(alloc["cpu"])).milli_value(),
-                "memory": parse_quantity(str(alloc["memory"])).value}).start()
+                "memory": parse_quantity(str(alloc["memory"])).value} if self.enforce_node_allocatable else {},
+                cpu_cfs_quota=self.cpu_cfs_quota).start()
         if self.service_env:
             self.svc_informer = Informer(self.client, "services")
             self.svc_informer.start()

@@ -15,7 +15,7 @@ import json
 import logging
 import time
 
-from ..client.informer import InformerFactory
+from ..client.informer import InformerFactory, resync_period
 from ..utils.httpserver import HTTPServer, Response
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from ..utils.tasks import spawn
@@ -72,7 +72,7 @@ class ProxyServer:
     def __init__(self, client, hostname, mode="iptables", cluster_cidr="", masquerade_all=False, sync_period=30.0,
                  min_sync_period=0.0, node_ips=("127.0.0.1",), healthz_port=None, metrics_port=None,
                  iptables=None, ipvs=None, ipvs_scheduler="rr", bind="127.0.0.1", open_node_ports=True,
-                 masquerade_bit=14):
+                 masquerade_bit=14, resync=0.0, profiling=False):
         self.client = client
         self.hostname = hostname
         self.mode = mode
@@ -98,7 +98,9 @@ class ProxyServer:
         self.metrics = Registry()
         self.m_sync = self.metrics.histogram("kubeproxy_sync_proxy_rules_latency_microseconds",
                                              "SyncProxyRules latency", (), MICRO_BUCKETS)
-        self.factory = InformerFactory(client)
+        # --config-sync-period: the service/endpoints informers resync every [p, 2p)
+        self.factory = InformerFactory(client, resync_period(resync))
+        self.profiling = profiling
         self._dirty = asyncio.Event()
         self._task = None
         self._http = []
@@ -160,6 +162,9 @@ class ProxyServer:
         return Response(200 if ok else 503, body)
 
     async def _metrics(self, req):
+        if req.path.startswith("/debug/pprof") and self.profiling:     # --profiling
+            from ..utils.profiling import handle_debug
+            return await handle_debug(req)
         return Response(200, self.metrics.render(), "text/plain; version=0.0.4")
 
     async def stop(self):

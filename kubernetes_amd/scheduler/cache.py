@@ -169,6 +169,10 @@ class ERManager:
         return len(self.available.get(rname) or ())
 
 
+DEFAULT_FAILURE_DOMAINS = ("kubernetes.io/hostname", "failure-domain.beta.kubernetes.io/zone",
+                           "failure-domain.beta.kubernetes.io/region")
+
+
 class NodeInfo:
     __slots__ = ("node", "name", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
                  "req_cpu", "req_mem", "req_eph", "req_scalars", "nz_cpu", "nz_mem", "pods", "ports", "er", "generation",
@@ -288,6 +292,10 @@ class SchedulerCache:
         # branch): any podAffinity, or preferred podAntiAffinity
         self.affinity_pods: dict[str, dict] = {}
         self.hard_pod_affinity_weight = 1        # --hard-pod-affinity-symmetric-weight
+        # --failure-domains: the topology an EMPTY topologyKey of a preferred pod (anti-)affinity
+        # term stands for — nodes are in one domain when they share any of these labels' values
+        # (`algorithm/priorities/util/topologies.go` NodesHaveSameTopologyKey)
+        self.failure_domains = DEFAULT_FAILURE_DOMAINS
         self.volumes = VolumeLister()
         self.services: dict[str, dict[str, dict | None]] = {}   # namespace -> service -> selector
 

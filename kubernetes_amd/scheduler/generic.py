@@ -138,6 +138,9 @@ class CycleContext:
             ns = self.pod["metadata"].get("namespace", "default")
             for w, term in self.affinity_prefs:
                 key = term.get("topologyKey", "")
+                if not key:
+                    out.append((w, "", self._any_domain_counts(term, ns)))
+                    continue
                 counts = {}
                 for ni in self.cache.nodes.values():
                     v = ni.labels.get(key)
@@ -150,6 +153,29 @@ class CycleContext:
             out += self._existing_pod_terms(ns)
             self._aff_counts = out
         return self._aff_counts
+
+    def _shares_domain(self, a, b):
+        for k in self.cache.failure_domains:
+            v = a.labels.get(k)
+            if v is not None and b.labels.get(k) == v:
+                return True
+        return False
+
+    def _any_domain_counts(self, term, ns):
+        """Empty topologyKey: {node name: matching pods on nodes sharing any failure domain}."""
+        where = []
+        for ni in self.cache.nodes.values():
+            n = sum(1 for p, _ in ni.pods.values()
+                    if P._pod_matches_term(p["metadata"].get("labels") or {}, p["metadata"].get("namespace"), term, ns))
+            if n:
+                where.append((ni, n))
+        counts = {}
+        if where:
+            for ni in self.cache.nodes.values():
+                c = sum(n for src, n in where if self._shares_domain(ni, src))
+                if c:
+                    counts[ni.name] = c
+        return counts
 
     def _existing_pod_terms(self, ns):
         """Existing pods' terms that match the incoming pod (`interpod_affinity.go` symmetry):
@@ -178,6 +204,10 @@ class CycleContext:
                       for t in (aff.get("podAntiAffinity") or {}).get("preferredDuringSchedulingIgnoredDuringExecution") or ()]
             for w, term in terms:
                 tkey = term.get("topologyKey", "")
+                if not tkey:
+                    if w and P._pod_matches_term(labels, ns, term, pns):
+                        out.append((w, "", {o.name: 1 for o in cache.nodes.values() if self._shares_domain(o, ni)}))
+                    continue
                 v = ni.labels.get(tkey)
                 if v is not None and w and P._pod_matches_term(labels, ns, term, pns):
                     out.append((w, tkey, {v: 1}))

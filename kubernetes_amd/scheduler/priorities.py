@@ -182,6 +182,9 @@ def inter_pod_affinity(pod, pi, ni, ctx):
     min-max normalized to 0..10."""
     s = 0.0
     for weight, key, counts in ctx.pod_affinity_counts():
+        if not key:                       # empty topologyKey: counts per node (--failure-domains)
+            s += weight * counts.get(ni.name, 0)
+            continue
         v = ni.labels.get(key)
         if v is not None:
             s += weight * counts.get(v, 0)

@@ -59,11 +59,14 @@ class Scheduler:
     def __init__(self, client, scheduler_name=DEFAULT_SCHEDULER, predicates=None, priorities=None,
                  percentage_of_nodes_to_score=100, emit_events=True, extenders=None, max_binds_in_flight=256,
                  update_unschedulable_status=True, shard_index=0, shard_count=1, preemption=True,
-                 rehandoff_period=0.2, hard_pod_affinity_symmetric_weight=1):
+                 rehandoff_period=0.2, hard_pod_affinity_symmetric_weight=1, failure_domains=None):
         self.client = client
         self.name = scheduler_name
+        self.profiling = True         # --profiling: /debug/pprof on the metrics port
         self.cache = SchedulerCache()
         self.cache.hard_pod_affinity_weight = hard_pod_affinity_symmetric_weight
+        if failure_domains:
+            self.cache.failure_domains = tuple(failure_domains)
         self.queue = SchedulingQueue()
         self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
         self.shard_index, self.shard_count = shard_index, shard_count
@@ -490,7 +493,7 @@ class Scheduler:
             return Response(200, self.metrics.render(), "text/plain; version=0.0.4")
         if req.path == "/healthz":
             return Response(200, b"ok", "text/plain")
-        if req.path.startswith("/debug/pprof"):
+        if req.path.startswith("/debug/pprof") and self.profiling:
             from ..utils.profiling import handle_debug
             return await handle_debug(req)
         return Response(404, b"not found", "text/plain")

@@ -11,6 +11,22 @@
 
 #include <vector>
 
+// rank r starts from x[e] = (r + 1) + (e % 8): after the sum every element of every rank must be
+// n(n+1)/2 + n*(e % 8) — exact in fp32 for these small integers, and a mis-placed or missing
+// chunk shows as a wrong value at its offset
+__global__ void init_pattern(float* x, size_t n, int rank) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    x[e] = (float)(rank + 1) + (float)(e % 8);
+}
+
+__global__ void count_bad(const float* x, size_t n, int ranks, unsigned long long* bad) {
+  unsigned long long mine = 0;
+  const float base = (float)ranks * (ranks + 1) / 2;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    mine += x[e] != base + (float)ranks * (float)(e % 8);
+  if (mine) atomicAdd(bad, mine);
+}
+
 #define HIPCHK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 #define NCCLCHK(x) do { ncclResult_t r = (x); if (r != ncclSuccess) { fprintf(stderr, "%s: %s\n", #x, ncclGetErrorString(r)); return 1; } } while (0)
 
@@ -87,6 +103,7 @@ int main(int argc, char** argv) {
   int n = 0;
   HIPCHK(hipGetDeviceCount(&n));
   if (n < 1) { fprintf(stderr, "no devices\n"); return 2; }
+  if (mib < 1) mib = 1;
   size_t count = mib * (1 << 20) / sizeof(float);
   std::vector<int> devs(n);
   for (int i = 0; i < n; ++i) devs[i] = i;
@@ -94,13 +111,14 @@ int main(int argc, char** argv) {
   NCCLCHK(ncclCommInitAll(comms.data(), n, devs.data()));
   std::vector<float*> buf(n);
   std::vector<hipStream_t> st(n);
+  const int kBlocks = 1024, kThreads = 256;   // >> 256 CUs, grid-stride over the buffer
   for (int i = 0; i < n; ++i) {
     HIPCHK(hipSetDevice(i));
     HIPCHK(hipMalloc(&buf[i], count * sizeof(float)));
     HIPCHK(hipStreamCreate(&st[i]));
-    std::vector<float> h(1024, (float)(i + 1));
-    for (size_t off = 0; off < count; off += 1024)
-      HIPCHK(hipMemcpy(buf[i] + off, h.data(), sizeof(float) * (count - off < 1024 ? count - off : 1024), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(init_pattern, dim3(kBlocks), dim3(kThreads), 0, st[i], buf[i], count, i);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st[i]));
   }
   auto run = [&](int k) -> int {
     for (int it = 0; it < k; ++it) {
@@ -112,10 +130,22 @@ int main(int argc, char** argv) {
     return 0;
   };
   if (run(1)) return 1;
-  // correctness after one all-reduce: every element == n(n+1)/2
-  float expect = (float)n * (n + 1) / 2, got = 0;
-  HIPCHK(hipSetDevice(0));
-  HIPCHK(hipMemcpy(&got, buf[0] + count / 2, sizeof(float), hipMemcpyDeviceToHost));
+  // correctness after one all-reduce: the WHOLE buffer, on EVERY rank
+  std::vector<unsigned long long> bad(n, 0);
+  unsigned long long total_bad = 0;
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(i));
+    unsigned long long* d_bad = nullptr;
+    HIPCHK(hipMalloc(&d_bad, sizeof(unsigned long long)));
+    HIPCHK(hipMemset(d_bad, 0, sizeof(unsigned long long)));
+    hipLaunchKernelGGL(count_bad, dim3(kBlocks), dim3(kThreads), 0, st[i], buf[i], count, n, d_bad);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st[i]));
+    HIPCHK(hipMemcpy(&bad[i], d_bad, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(d_bad));
+    total_bad += bad[i];
+  }
+  bool correct = total_bad == 0;
   hipEvent_t e0, e1;
   HIPCHK(hipSetDevice(0));
   HIPCHK(hipEventCreate(&e0));
@@ -130,8 +160,11 @@ int main(int argc, char** argv) {
   double t = ms / 1e3 / iters;
   double algbw = (double)count * sizeof(float) / t / 1e9;
   double busbw = n > 1 ? algbw * 2.0 * (n - 1) / n : 0.0;
-  printf("{\"ranks\": %d, \"bytes\": %zu, \"time_us\": %.1f, \"algbw_GBps\": %.2f, \"busbw_GBps\": %.2f, \"correct\": %s}\n",
-         n, count * sizeof(float), t * 1e6, algbw, busbw, got == expect ? "true" : "false");
+  printf("{\"ranks\": %d, \"bytes\": %zu, \"time_us\": %.1f, \"algbw_GBps\": %.2f, \"busbw_GBps\": %.2f, "
+         "\"elements_checked_per_rank\": %zu, \"bad_elements\": [",
+         n, count * sizeof(float), t * 1e6, algbw, busbw, count);
+  for (int i = 0; i < n; ++i) printf("%s%llu", i ? ", " : "", bad[i]);
+  printf("], \"correct\": %s}\n", correct ? "true" : "false");
   for (int i = 0; i < n; ++i) { ncclCommDestroy(comms[i]); hipSetDevice(i); hipFree(buf[i]); }
-  return got == expect ? 0 : 3;
+  return correct ? 0 : 3;
 }

@@ -1,10 +1,13 @@
 #!/bin/bash
-# GPU box: GPU tests, driver smoke, 1-GPU bench. Each GPU step has its own time limit.
-set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R" && mkdir -p gpurun_out
-step() { local name=$1; shift; echo "== $name"; "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; tail -5 "gpurun_out/$name.log"; if [ $rc -ne 0 ]; then echo "$name FAILED rc=$rc"; tail -40 "gpurun_out/$name.log"; exit $rc; fi; }
-step pytest_gpu timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-step smoke timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()"
-step bench1 timeout -k 10 600 python bench.py --steps 5 --warmup 2
-echo ALL_OK
+# One GPU-box pass: GPU tests, the xGMI probe, a short bench. Later GPU steps run only when the
+# earlier one ended normally (pytest 0 = pass, 1 = test failures); a timeout (124/137), an abort
+# (134) or a crash (139) ends the pass there.
+out=${1:-gpurun_out/pass}
+mkdir -p "$out"
+timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > "$out/gputests.log" 2>&1
+rc=$?
+echo "pytest rc=$rc" > "$out/status.txt"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 60 kubernetes_amd/native/bin/xgmi-probe 64 > "$out/xgmi.json" 2>&1 || exit $?
+timeout -k 10 240 python bench.py --steps 20 --warmup 5 > "$out/bench.json" 2> "$out/bench.err" || exit $?
+exit $rc

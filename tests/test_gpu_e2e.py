@@ -54,7 +54,9 @@ def test_e2e_gpu_spec_on_real_mi355x(run):
     async def main():
         async with LocalCluster(nodes=1, gpus_per_node=8, runtime="process", real_gpus=True, kubelet_http=True) as cl:
             res = await run_specs(cl.url, focus="Feature:GPU", timeout=150)
-        assert len(res) == 1 and res[0].ok, res[0].error if res else "no spec ran"
+        # the [Feature:MultiGPU] spec skips on a box with fewer than 4 GPUs
+        ran = [r for r in res if not r.skipped]
+        assert ran and all(r.ok for r in res), [(r.name, r.error) for r in res]
     run(main(), timeout=200)
 
 
