@@ -27,6 +27,7 @@ class Indexer:
         self.items: dict[str, dict] = {}
         self.indexers = dict(indexers or {})
         self.indices: dict[str, dict[str, set]] = {n: {} for n in self.indexers}
+        self.generation = 0       # bumped on every change: derived views can be cached against it
 
     def add_indexer(self, name, fn):
         self.indexers[name] = fn
@@ -52,6 +53,7 @@ class Indexer:
                 idx.setdefault(v, set()).add(key)
 
     def put(self, key, obj):
+        self.generation += 1
         old = self.items.get(key)
         if old is not None and self.indexers:
             self._unindex(key, old)
@@ -61,6 +63,7 @@ class Indexer:
         return old
 
     def delete(self, key):
+        self.generation += 1
         old = self.items.pop(key, None)
         if old is not None and self.indexers:
             self._unindex(key, old)

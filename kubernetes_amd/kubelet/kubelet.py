@@ -62,7 +62,8 @@ def _expand_ref(s, env):
 class PodState:
     __slots__ = ("uid", "pod", "sandbox", "containers", "init_containers", "admitted", "rejected", "start_time",
                  "restarts", "ip", "terminated", "deleted", "last_status", "running_at", "first_seen", "volumes",
-                 "waiting", "net_mounts", "net_setup", "previous", "backoff", "adopted", "deadline_armed")
+                 "waiting", "net_mounts", "net_setup", "previous", "backoff", "adopted", "deadline_armed",
+                 "final_deleted", "requests")
 
     def __init__(self, pod):
         self.uid = pod["metadata"]["uid"]
@@ -89,6 +90,8 @@ class PodState:
         self.backoff: dict[str, list] = {}    # container name -> [next restart allowed at, current delay]
         self.adopted = False                  # sandbox/containers found in the runtime after a kubelet restart
         self.deadline_armed = False           # a resync is scheduled at spec.activeDeadlineSeconds
+        self.final_deleted = False            # the grace-0 delete was accepted; later events need no other
+        self.requests = None                  # core.pod_requests, once: container resources are immutable
 
 
 def _field_path(pod, c):
@@ -161,6 +164,7 @@ class Kubelet:
         self.cgroups = None
         self.service_env = service_env            # inject {SVC}_SERVICE_HOST/... (pkg/kubelet/envvars)
         self.svc_informer = None
+        self._svc_env_cache: dict = {}        # namespace -> ((ns, services generation), env vars)
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
         self.dns = dns                       # network.DNSConfigurer or None
@@ -675,16 +679,24 @@ class Kubelet:
 
     # ------------------------------------------------------------------
     # admission
+    @staticmethod
+    def _requests(st):
+        if st.requests is None:
+            st.requests = core.pod_requests(st.pod)
+        return st.requests
+
     def _general_predicates(self, pod):
         """GeneralPredicates against this node's capacity and the other active pods."""
-        need = core.pod_requests(pod)
+        uid = pod["metadata"]["uid"]
+        me = self.pods.get(uid)
+        need = self._requests(me) if me is not None else core.pod_requests(pod)
         used: dict = {}
         n = 0
-        for other in self.active_pods():
-            if other["metadata"]["uid"] == pod["metadata"]["uid"]:
+        for other in self.pods.values():
+            if other.terminated or other.rejected or other.uid == uid:
                 continue
             n += 1
-            for k, v in core.pod_requests(other).items():
+            for k, v in self._requests(other).items():
                 used[k] = used[k] + v if k in used else v
         if n + 1 > int(self.capacity["pods"]):
             return "OutOfpods", "Node didn't have enough resource: pods"
@@ -1060,7 +1072,14 @@ class Kubelet:
         if self.svc_informer is None or not self.svc_informer.synced.is_set():
             return []
         from .envvars import service_env
-        return service_env(self.svc_informer.list(), pod["metadata"].get("namespace", "default"))
+        ns = pod["metadata"].get("namespace", "default")
+        key = (ns, self.svc_informer.store.generation)
+        hit = self._svc_env_cache.get(ns)
+        if hit is not None and hit[0] == key:
+            return list(hit[1])
+        env = service_env(self.svc_informer.list(), ns)
+        self._svc_env_cache[ns] = (key, env)
+        return list(env)
 
     async def _start(self, st, c):
         from .images import ImagePullError
@@ -1440,10 +1459,18 @@ class Kubelet:
             await self.volumes.unpublish(pod)
             self.volumes.teardown(pod)
             st.volumes = None
+        if st.final_deleted:
+            # every later update of the terminating pod (our own status write, the delete's
+            # MODIFIED) lands here again; one accepted grace-0 delete is enough (status_manager
+            # deletes once the pod `canBeDeleted`)
+            return
         try:
             await self.client.delete("pods", md["name"], md.get("namespace"), grace_period=0, uid=md["uid"])
+            st.final_deleted = True
         except APIStatusError as e:
-            if not (is_not_found(e) or is_conflict(e)):
+            if is_not_found(e) or is_conflict(e):
+                st.final_deleted = True
+            else:
                 log.warning("final delete of %s failed: %s", md["name"], e)
 
     # ------------------------------------------------------------------

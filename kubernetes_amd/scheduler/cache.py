@@ -72,6 +72,15 @@ class PodInfo:
                 lim_mem += _q(lim["memory"]).int_value()
         self.limits = (lim_cpu, lim_mem)
 
+    def with_assigned(self, pod):
+        """This pod's info for its assumed copy: everything parsed stays, only the devices the
+        scheduler just assigned change (no second parse per scheduled pod)."""
+        out = object.__new__(PodInfo)
+        for s in PodInfo.__slots__:
+            setattr(out, s, getattr(self, s))
+        out.assigned = core.pod_assigned_devices(pod)
+        return out
+
 
 def _hive(dev):
     return (dev.get("attributes") or {}).get(core.ATTR_HIVE, "")
@@ -332,12 +341,12 @@ class SchedulerCache:
         return ni
 
     # -- pods ---------------------------------------------------------------
-    def assume_pod(self, pod):
+    def assume_pod(self, pod, pi=None):
         key = ns_name(pod)
         if key in self.pod_states:
             raise ValueError(f"pod {key} is in the cache, so can't be assumed")
         node = pod["spec"]["nodeName"]
-        self._node(node).add_pod(key, pod, PodInfo(pod))
+        self._node(node).add_pod(key, pod, pi.with_assigned(pod) if pi is not None else PodInfo(pod))
         self.pod_states[key] = (pod, node)
         self.assumed[key] = 0.0
         self._track(key, pod)

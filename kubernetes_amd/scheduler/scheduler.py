@@ -35,7 +35,7 @@ import time
 import zlib
 
 from ..api import core
-from ..api.meta import fast_copy, ns_name, now_rfc3339
+from ..api.meta import ns_name, now_rfc3339
 from ..api.sharding import QUERY_PARAM, SHARD_OFFSET_LABEL, offset_of
 from ..client.events import EventRecorder
 from ..client.informer import Informer
@@ -372,14 +372,17 @@ class Scheduler:
             self.recorder.event(pod, "Warning", "FailedScheduling", str(e))
             return None
         self.m_algo.observe((time.perf_counter() - t0) * 1e6)
-        assumed = fast_copy(pod)
-        assumed["spec"]["nodeName"] = host
-        for per in assumed["spec"].get("extendedResources") or ():
-            got = erb.get(per.get("name"))
-            if got is not None:
-                per["assigned"] = list(got["resources"])
+        # the assumed copy shares everything but spec (nodeName) and the per-resource entries
+        # that get device IDs: the cache never mutates a pod it holds
+        assumed = dict(pod)
+        spec = assumed["spec"] = dict(pod["spec"])
+        spec["nodeName"] = host
+        ers = spec.get("extendedResources")
+        if ers:
+            spec["extendedResources"] = [dict(per, assigned=list(erb[per.get("name")]["resources"]))
+                                         if per.get("name") in erb else per for per in ers]
         try:
-            self.cache.assume_pod(assumed)
+            self.cache.assume_pod(assumed, pi)
         except ValueError as e:
             log.warning("assume failed: %s", e)
             return None
