@@ -19,13 +19,17 @@ as `KUBERNETES_VOLUME_<NAME>` to the process.
 from __future__ import annotations
 
 import base64
+import logging
 import os
 import re
 import shutil
+import stat
 
 from ..api.quantity import parse_quantity
 from ..client.rest import APIStatusError
 from .volume_plugins import NETWORK_KINDS
+
+log = logging.getLogger("kubelet.volumes")
 
 
 class VolumeError(Exception):
@@ -87,6 +91,35 @@ def _write_files(d, data: dict, items=None, mode=0o644, binary=False, optional=F
         os.chmod(tmp, want)
         os.replace(tmp, p)
     return out
+
+
+# volume kinds whose files the kubelet owns, so `fsGroup` applies (SetVolumeOwnership callers)
+_OWNED = ("emptyDir", "configMap", "secret", "downwardAPI", "projected")
+_READONLY = ("configMap", "secret", "downwardAPI", "projected")
+
+
+def set_volume_ownership(d, fs_group, readonly):
+    """`pkg/volume/volume_linux.go` SetVolumeOwnership: every file and directory of the volume
+    gets group `fs_group` and group access (rw, r for the read-only kinds); directories get the
+    setgid bit (new files inherit the group) and group search."""
+    mask = 0o440 if readonly else 0o660
+    for root, dirs, files in os.walk(d):
+        for p in [root] + [os.path.join(root, x) for x in files]:
+            try:
+                st = os.lstat(p)
+                if stat.S_ISLNK(st.st_mode):
+                    continue
+                os.lchown(p, -1, int(fs_group))
+                m = stat.S_IMODE(st.st_mode) | mask
+                if stat.S_ISDIR(st.st_mode):
+                    m |= stat.S_ISGID | 0o110
+                os.chmod(p, m)
+            except OSError as e:       # not permitted (an unprivileged kubelet outside the group)
+                log.debug("fsGroup ownership of %s: %s", p, e)
+
+
+def _fs_group(pod):
+    return ((pod.get("spec") or {}).get("securityContext") or {}).get("fsGroup")
 
 
 def _prune(d, keep: set):
@@ -245,6 +278,8 @@ class VolumeManager:
                         self._downward(pod, src["downwardAPI"], d, node_name, pod_ip, dm)
             else:
                 raise VolumeError(f"volume {name}: unsupported volume source {sorted(k for k in v if k != 'name')}")
+            if _fs_group(pod) is not None and any(k in v for k in _OWNED):
+                set_volume_ownership(d, _fs_group(pod), any(k in v for k in _READONLY))
             out[name] = d
         if out:
             self._traversable(base)
@@ -460,6 +495,8 @@ class VolumeManager:
                         keep |= self._downward(pod, src["downwardAPI"], d, node_name, pod_ip,
                                                v["projected"].get("defaultMode"))
                 _prune(d, keep)
+            if _fs_group(pod) is not None and any(k in v for k in _READONLY):
+                set_volume_ownership(d, _fs_group(pod), True)
 
     async def _cm_secret(self, ns, v, d, default_mode=None):
         if "configMap" in v:

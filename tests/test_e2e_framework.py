@@ -2,7 +2,7 @@
 the way test/e2e runs against a real cluster; the GPU spec is skipped on CPU and runs in the GPU
 tier (tests/test_gpu_e2e.py)."""
 from kubernetes_amd.cluster import LocalCluster
-from kubernetes_amd.e2e import specs, specs_common  # noqa: F401
+from kubernetes_amd.e2e import specs, specs_common, specs_storage  # noqa: F401
 from kubernetes_amd.e2e.framework import SPECS, run_specs
 
 
@@ -25,6 +25,6 @@ def test_conformance_specs_pass(run, tmp_path):
             import shutil
             shutil.rmtree(wd, ignore_errors=True)
         failed = [r for r in res if not r.ok]
-        assert len(res) >= 80 and not failed, "\n".join(r.name + ": " + r.error for r in failed)
+        assert len(res) >= 120 and not failed, "\n".join(r.name + ": " + r.error for r in failed)
     run(main(), timeout=900)
     assert any("Feature:GPU" in t for _, _, tags in SPECS for t in tags)
