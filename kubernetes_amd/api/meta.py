@@ -12,18 +12,30 @@ import copy
 import datetime as _dt
 import os
 import time
-import uuid as _uuid
 from dataclasses import dataclass
 
 
 def new_uid() -> str:
-    return str(_uuid.UUID(bytes=os.urandom(16), version=4))
+    """A random (version 4) UUID string."""
+    b = bytearray(os.urandom(16))
+    b[6] = (b[6] & 0x0F) | 0x40
+    b[8] = (b[8] & 0x3F) | 0x80
+    h = b.hex()
+    return f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:]}"
+
+
+_NOW = [-1, ""]        # (second, its RFC 3339 text): every write stamps the current second
 
 
 def now_rfc3339(t: float | None = None) -> str:
     """metav1.Time JSON form (second precision, UTC, 'Z')."""
-    t = time.time() if t is None else t
-    return _dt.datetime.fromtimestamp(int(t), _dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+    s = int(time.time() if t is None else t)
+    if s == _NOW[0]:
+        return _NOW[1]
+    text = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(s))
+    if t is None:
+        _NOW[0], _NOW[1] = s, text
+    return text
 
 
 def now_rfc3339_micro(t: float | None = None) -> str:

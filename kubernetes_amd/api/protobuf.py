@@ -602,9 +602,14 @@ def supported(kind: str, api_version: str = "") -> bool:
     return any(k.rsplit("/", 1)[-1] == kind for k in s.kinds)
 
 
+_NAT = []
+
+
 def _native():
-    from ..native import pbcodec
-    return pbcodec.codec()
+    if not _NAT:
+        from ..native import pbcodec
+        _NAT.append(pbcodec)
+    return _NAT[0].codec()
 
 
 def encode_object(obj: dict) -> bytes:

@@ -83,8 +83,18 @@ class NamespaceLifecycle(Plugin):
             raise AdmissionError(f"unable to create new content in namespace {a.namespace} because it is being terminated")
 
 
+SA_MOUNT_PATH = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
 @register
 class ServiceAccount(Plugin):
+    """`plugin/pkg/admission/serviceaccount/admission.go`: the pod runs as `default` unless it
+    names an account, and — unless `automountServiceAccountToken` is false on the pod or, when
+    the pod does not say, on the account — gets the account's API token secret as a volume
+    mounted read-only at /var/run/secrets/kubernetes.io/serviceaccount in every container.
+    Unlike the reference (which rejects the pod until the token controller has made a token),
+    a pod whose account or token does not exist yet is admitted without the mount: a cluster
+    without a token controller (no --service-account-private-key-file) still runs pods."""
     name = "ServiceAccount"
     operations = (CREATE,)
 
@@ -92,7 +102,41 @@ class ServiceAccount(Plugin):
         if a.resource != "pods" or a.subresource:
             return
         spec = a.obj.setdefault("spec", {})
-        spec.setdefault("serviceAccountName", "default")
+        name = spec.setdefault("serviceAccountName", "default")
+        if spec.get("automountServiceAccountToken") is False or not self.server:
+            return
+        if (a.obj.get("metadata") or {}).get("annotations", {}).get("kubernetes.io/config.mirror"):
+            return                                   # mirror pods do not reference API objects
+        try:
+            sa = self.server.get_object("serviceaccounts", a.namespace, name)
+        except RuntimeError:
+            return
+        if sa is None:
+            return
+        if spec.get("automountServiceAccountToken") is None and sa.get("automountServiceAccountToken") is False:
+            return
+        token = None
+        for ref in sa.get("secrets") or ():
+            try:
+                sec = self.server.get_object("secrets", a.namespace, ref.get("name", ""))
+            except RuntimeError:
+                return
+            if sec is not None and sec.get("type") == "kubernetes.io/service-account-token":
+                token = sec["metadata"]["name"]
+                break
+        if token is None:
+            return
+        vols = spec.setdefault("volumes", [])
+        vol = next((v["name"] for v in vols if (v.get("secret") or {}).get("secretName") == token), None)
+        if vol is None:
+            vol = token
+            # written as defaulting would leave it (admission runs after defaulting): an update
+            # of the pod then carries the same volume and is not refused as a spec change
+            vols.append({"name": vol, "secret": {"secretName": token, "defaultMode": 0o644}})
+        for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+            mounts = c.setdefault("volumeMounts", [])
+            if not any(m.get("mountPath") == SA_MOUNT_PATH for m in mounts):
+                mounts.append({"name": vol, "readOnly": True, "mountPath": SA_MOUNT_PATH})
 
 
 @register

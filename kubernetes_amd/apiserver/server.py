@@ -37,6 +37,7 @@ import secrets
 import time
 
 from ..api import codec, core, defaults, meta as m
+from ..api import protobuf as pb
 from ..api.labels import SelectorError, parse as parse_labels, parse_field_selector
 from ..api.meta import parse_rfc3339, fast_copy, now_rfc3339
 from ..api.sharding import QUERY_PARAM, SHARD_OFFSET_LABEL, parse_shard, shard_matches
@@ -54,7 +55,25 @@ from .registry import (APIError, already_exists, apply_binding, bad_request, con
 
 log = logging.getLogger("apiserver")
 
-VERSION = {"major": "1", "minor": "9", "gitVersion": "v1.9.0-amd.0", "platform": "linux/amd64",
+def _build_info():
+    """gitCommit / gitTreeState / buildDate of `version.Info` (pkg/version/base.go), from the
+    package's git checkout when there is one."""
+    import subprocess
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    commit, state = "", "unknown"
+    try:
+        commit = subprocess.run(["git", "-C", here, "rev-parse", "HEAD"], capture_output=True, text=True,
+                                timeout=5).stdout.strip()
+        dirty = subprocess.run(["git", "-C", here, "status", "--porcelain", "--untracked-files=no"],
+                               capture_output=True, text=True, timeout=5).stdout.strip()
+        state = "dirty" if dirty else "clean" if commit else "unknown"
+    except (OSError, subprocess.SubprocessError):
+        pass
+    built = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(os.path.getmtime(__file__)))
+    return {"gitCommit": commit or "unknown", "gitTreeState": state, "buildDate": built}
+
+
+VERSION = {"major": "1", "minor": "9", "gitVersion": "v1.9.0-amd.0", **_build_info(), "platform": "linux/amd64",
            "goVersion": "n/a", "compiler": "cpython"}
 
 _READ_VERBS = {"GET": "get", "HEAD": "get"}
@@ -162,11 +181,9 @@ _FRAME = b"\x00KH"                 # shared-store value framing (index header + 
 
 def pb_to_json(body, rev) -> bytes:
     """A protobuf-stored object (k8s\\0 envelope) as JSON bytes with resourceVersion = rev."""
-    from ..native import pbcodec
-    nat = pbcodec.codec()
+    nat = pb._native()
     if nat is not None:
         return nat.to_json(body, str(rev))
-    from ..api import protobuf as pb
     obj = pb.decode_object(body)
     obj.setdefault("metadata", {})["resourceVersion"] = str(rev)
     return codec.dumpb(obj)
@@ -532,10 +549,9 @@ class APIServer:
     def _storage_encode(self, ri, obj):
         """The storage bytes of obj; a field outside the reference schema is a 422, never a silent
         drop (the protobuf encoder refuses what it cannot represent)."""
-        from ..api.protobuf import ProtobufError
         try:
             return self.storage_codec.encode(obj)
-        except ProtobufError as e:
+        except pb.ProtobufError as e:
             from ..api.validation import FieldError
             raise invalid(ri, m.name_of(obj), [FieldError("Invalid value", e.path or "<object>", str(e).split(": ", 1)[-1])])
 
@@ -709,9 +725,8 @@ class APIServer:
         sealed = ri.plural in self.transformers
         json_storage = self.storage_codec.media_type == codec.JSON and not sealed
         if not json_storage and not sealed and self.storage_codec.media_type == codec.PROTOBUF:
-            from ..api import protobuf as _pbm
             # kinds outside the protobuf schema (custom resources) are stored as JSON
-            json_storage = _pbm.message_of(obj) is None
+            json_storage = pb.message_of(obj) is None
         # value framing: [00 'K' 'H' | u32 len | index header (fields, labels) | object]
         hdr = codec.dumpb([cache.index_fields(obj), md.get("labels") or {}])
         frame = _FRAME + len(hdr).to_bytes(4, "little") + hdr
@@ -1456,7 +1471,6 @@ class APIServer:
                 return Response(200, self.openapi.get(schemas), "application/json")
             if req.body and req.headers.get("content-type", "").startswith(codec.PROTOBUF):
                 # protobuf request bodies (`application/vnd.kubernetes.protobuf`, k8s\0 envelope)
-                from ..api import protobuf as pb
                 try:
                     req.body = codec.dumpb(pb.decode_object(req.body))
                 except pb.ProtobufError as e:
@@ -1562,7 +1576,6 @@ class APIServer:
                     resp = _json(200, to_table(codec.loads(resp.body), ri.kind, q_include(req)))
                     return resp
             if codec.PROTOBUF in req.headers.get("accept", "") and isinstance(resp, Response) and resp.body[:1] == b"{":
-                from ..api import protobuf as pb
                 obj = codec.loads(resp.body)
                 if pb.supported(obj.get("kind", "")):
                     resp = Response(resp.status, pb.encode_object(obj), codec.PROTOBUF)

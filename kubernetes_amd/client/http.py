@@ -46,7 +46,7 @@ async def _read_response(reader):
     return status, headers
 
 
-async def _read_body(reader, headers):
+async def _read_body(reader, headers, status=200, method="GET"):
     if headers.get("transfer-encoding", "").lower() == "chunked":
         out = bytearray()
         while True:
@@ -58,6 +58,11 @@ async def _read_body(reader, headers):
             out += await reader.readexactly(n)
             await reader.readline()
         return bytes(out)
+    if "content-length" not in headers and method != "HEAD" and status >= 200 and status not in (204, 304):
+        # no length and not chunked: the body runs to the end of the connection (RFC 7230
+        # 3.3.3 rule 7 — HTTP/1.0 servers such as Python's http.server); never reuse it
+        headers["connection"] = "close"
+        return await reader.read()
     n = int(headers.get("content-length", "0") or 0)
     return await reader.readexactly(n) if n else b""
 
@@ -135,7 +140,7 @@ class HTTPClient:
                 try:
                     conn.writer.write(self._head(method, path, body, content_type, headers) + (body or b""))
                     status, hdrs = await asyncio.wait_for(_read_response(conn.reader), self.timeout)
-                    data = await _read_body(conn.reader, hdrs)
+                    data = await _read_body(conn.reader, hdrs, status, method)
                 except (ConnectionError, asyncio.IncompleteReadError, OSError):
                     conn.close()
                     if fresh or attempt:

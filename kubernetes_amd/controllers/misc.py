@@ -71,21 +71,29 @@ class EndpointsController(Controller):
         if not sel:
             return
         s = selector_from_set(sel)
-        ready, not_ready = [], []
+        svc_ports = (svc.get("spec") or {}).get("ports") or ()
+        groups: dict = {}          # resolved port set -> ([ready], [not ready])  (RepackSubsets)
         for p in self.pod_inf.list():
             if p["metadata"].get("namespace") != ns or not s.matches(p["metadata"].get("labels") or {}):
                 continue
             ip = (p.get("status") or {}).get("podIP")
             if not ip or p["metadata"].get("deletionTimestamp"):
                 continue
+            ports = []
+            for sp in svc_ports:
+                port = find_port(p, sp)
+                if port is not None:          # a named port the pod lacks: not an endpoint for it
+                    ports.append((sp.get("name", ""), port, sp.get("protocol", "TCP")))
+            if not ports:
+                continue
             addr = {"ip": ip, "nodeName": (p.get("spec") or {}).get("nodeName"),
                     "targetRef": {"kind": "Pod", "namespace": ns, "name": p["metadata"]["name"], "uid": p["metadata"]["uid"]}}
-            (ready if pod_is_ready(p) else not_ready).append(addr)
-        ports = [{"name": pt.get("name", ""), "port": pt.get("targetPort", pt.get("port")), "protocol": pt.get("protocol", "TCP")}
-                 for pt in (svc.get("spec") or {}).get("ports") or ()]
+            g = groups.setdefault(tuple(sorted(ports)), ([], []))
+            g[0 if pod_is_ready(p) else 1].append(addr)
         subsets = []
-        if ready or not_ready:
-            ss = {"ports": ports}
+        for key_ports in sorted(groups):
+            ready, not_ready = groups[key_ports]
+            ss = {"ports": [{"name": n, "port": port, "protocol": proto} for n, port, proto in key_ports]}
             if ready:
                 ss["addresses"] = sorted(ready, key=lambda a: a["ip"])
             if not_ready:
@@ -105,6 +113,23 @@ class EndpointsController(Controller):
                 if not is_already_exists(e):
                     raise
         await self.client.patch("endpoints", name, {"subsets": subsets}, ns)
+
+
+def find_port(pod, svc_port):
+    """`podutil.FindPort`: the service port's targetPort as a number — an int (or digits) as
+    is, a name looked up among the pod's container ports of the same protocol; None when the
+    pod has no such named port."""
+    tp = svc_port.get("targetPort", svc_port.get("port"))
+    if isinstance(tp, int):
+        return tp
+    if isinstance(tp, str) and tp.isdigit():
+        return int(tp)
+    proto = svc_port.get("protocol", "TCP")
+    for c in (pod.get("spec") or {}).get("containers") or ():
+        for cp in c.get("ports") or ():
+            if cp.get("name") == tp and cp.get("protocol", "TCP") == proto:
+                return int(cp["containerPort"])
+    return None
 
 
 class ResourceQuotaController(Controller):

@@ -99,9 +99,9 @@ def LocalImageService(store: ImageStore):
 
 
 def process_image_resolver(ref):
-    from ..kubelet.runtime.process import IMAGES
+    from ..kubelet.runtime.process import builtin_argv
     base = ImageStore.normalize(ref).rsplit(":", 1)[0]
-    argv = IMAGES.get(base)
+    argv = builtin_argv(base)
     if not argv:
         return None
     try:

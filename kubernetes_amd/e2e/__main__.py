@@ -3,7 +3,7 @@ import argparse
 import asyncio
 import sys
 
-from . import specs, specs_common, specs_storage  # noqa: F401 - registers the specs
+from . import specs, specs_common, specs_more, specs_storage  # noqa: F401 - registers the specs
 from .framework import run_specs
 
 

@@ -631,7 +631,15 @@ async def pods_updated(f):
 async def _kubectl(f, *args):
     from ..kubectl.cli import main as kubectl
     out = io.StringIO()
-    rc = await asyncio.to_thread(kubectl, ["-s", f.client.url, *args], out=out)
+
+    def call():
+        try:
+            return kubectl(["-s", f.client.url, *args], out=out)
+        except SystemExit as e:             # kubectl's error exits: a non-zero status, not a crash
+            if e.code not in (None, 0) and not isinstance(e.code, int):
+                out.write(str(e.code))
+            return e.code if isinstance(e.code, int) else (0 if e.code is None else 1)
+    rc = await asyncio.to_thread(call)
     return rc, out.getvalue()
 
 

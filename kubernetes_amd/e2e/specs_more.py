@@ -1,0 +1,809 @@
+"""Conformance specs from the reference's `test/e2e/kubectl/kubectl.go` (run generators, expose,
+scale, rolling-update, replace, logs filters, annotate through patch, version, the proxy on
+port 0 and on a unix socket), `test/e2e/common/{container_probe,secrets,host_path,
+kubelet_etc_hosts,networking}.go`, `test/e2e/network/{service,proxy}.go`,
+`test/e2e/auth/service_accounts.go`, `test/e2e/apps/{rc,replica_set}.go` and
+`test/e2e/scheduling/predicates.go`.
+
+Container workloads are the host's `sh` and `python3` (the process runtime's `busybox` image is
+the host shell); servers in pods bind an ephemeral port chosen by the spec, since pods of the
+process runtime may share the node's network.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import re
+import socket
+import sys
+import tempfile
+import time
+
+from .framework import Skip, conformance
+from .specs_common import BUSYBOX, _at, _kubectl, _lines, _mount, _pod, _run_and_log, _secret
+
+PY = sys.executable
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rc(name, replicas=1, cmd="sleep 3600", labels=None, image=BUSYBOX):
+    labels = labels or {"app": name}
+    return {"metadata": {"name": name, "labels": dict(labels)}, "spec": {
+        "replicas": replicas, "selector": dict(labels), "template": {"metadata": {"labels": dict(labels)}, "spec": {
+            "containers": [{"name": name, "image": image, "command": ["sh", "-c", cmd]}]}}}}
+
+
+async def _pods(f, selector, phase=None):
+    items = (await f.client.list("pods", f.ns, label_selector=selector))["items"]
+    items = [p for p in items if not p["metadata"].get("deletionTimestamp")]
+    if phase:
+        items = [p for p in items if (p.get("status") or {}).get("phase") == phase]
+    return items
+
+
+async def _wait_pods(f, selector, n, phase="Running", timeout=90.0):
+    async def check():
+        ps = await _pods(f, selector, phase)
+        return ps if len(ps) == n else None
+    return await f.wait(check, timeout, f"{n} {phase} pods matching {selector}")
+
+
+async def _kubectl_proc(f, *args, stdin=None, timeout=60.0):
+    """kubectl as its own process (for --stdin/--attach and long-running proxies)."""
+    p = await asyncio.create_subprocess_exec(PY, "-m", "kubernetes_amd.kubectl", "-s", f.client.url, *args,
+                                             stdin=asyncio.subprocess.PIPE if stdin is not None else None,
+                                             stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.STDOUT)
+    out, _ = await asyncio.wait_for(p.communicate(stdin.encode() if stdin is not None else None), timeout)
+    return p.returncode, out.decode(errors="replace")
+
+
+# ---------------------------------------------------------------------------------------------
+# kubectl (kubectl.go)
+@conformance("Kubectl client Kubectl patch should add annotations for pods in rc")
+async def kubectl_patch_annotations(f):
+    await f.client.create("replicationcontrollers", _rc("redis-master"), f.ns)
+    pods = await _wait_pods(f, "app=redis-master", 1)
+    for p in pods:
+        rc, out = await _kubectl(f, "patch", "pod", p["metadata"]["name"], "-n", f.ns, "-p",
+                                 json.dumps({"metadata": {"annotations": {"x": "y"}}}))
+        assert rc == 0, out
+    for p in await _pods(f, "app=redis-master"):
+        assert (p["metadata"].get("annotations") or {}).get("x") == "y", p["metadata"]
+
+
+@conformance("Kubectl client Kubectl logs should be able to retrieve and filter logs")
+async def kubectl_logs_filter(f):
+    p = _pod("logs-generator", "for i in 1 2 3 4 5; do echo \"line $i of 5\"; done; sleep 3600", restart="Always")
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("logs-generator", ("Running",))
+
+    async def five():
+        return (await f.logs("logs-generator")).count("of 5") == 5
+    await f.wait(five, 30, "five log lines")
+    rc, out = await _kubectl(f, "logs", "-n", f.ns, "logs-generator", "c")
+    assert rc == 0 and len(_lines(out)) == 5, out
+    rc, out = await _kubectl(f, "logs", "-n", f.ns, "logs-generator", "c", "--tail=1")
+    assert _lines(out) == ["line 5 of 5"], out
+    rc, out = await _kubectl(f, "logs", "-n", f.ns, "logs-generator", "c", "--limit-bytes=1")
+    assert out == "l", repr(out)
+    rc, out = await _kubectl(f, "logs", "-n", f.ns, "logs-generator", "c", "--tail=1", "--timestamps")
+    ts = _lines(out)[0].split(" ", 1)[0]
+    assert re.match(r"\d{4}-\d\d-\d\dT\d\d:\d\d:\d\d", ts), out
+    await asyncio.sleep(1.5)
+    rc, out = await _kubectl(f, "logs", "-n", f.ns, "logs-generator", "c", "--since=1s")
+    assert _lines(out) == [], out
+    rc, out = await _kubectl(f, "logs", "-n", f.ns, "logs-generator", "c", "--since=24h")
+    assert len(_lines(out)) == 5, out
+
+
+@conformance("Kubectl client Kubectl version should check is all data is printed")
+async def kubectl_version_all(f):
+    rc, out = await _kubectl(f, "version")
+    assert rc == 0, out
+    for field in ("Major:", "Minor:", "GitCommit:", "GitTreeState:", "BuildDate:", "GoVersion:", "Compiler:",
+                  "Platform:"):
+        assert out.count(field) == 2, (field, out)       # client and server
+
+
+@conformance("Kubectl client Kubectl run --rm job should create a job from an image, then delete the job")
+async def kubectl_run_rm_job(f):
+    rc, out = await _kubectl_proc(f, "run", "-n", f.ns, "e2e-test-rm-busybox-job", f"--image={BUSYBOX}", "--rm=true",
+                                  "--generator=job/v1", "--restart=OnFailure", "--attach=true", "--stdin", "--",
+                                  "sh", "-c", "cat && echo 'stdin closed'", stdin="abcd1234", timeout=90)
+    assert rc == 0 and "abcd1234" in out and "stdin closed" in out, out
+
+    async def gone():
+        try:
+            await f.client.get("jobs", "e2e-test-rm-busybox-job", f.ns)
+            return False
+        except Exception:  # noqa: BLE001
+            return True
+    await f.wait(gone, 30, "the job deleted by --rm")
+
+
+@conformance("Kubectl client Kubectl run job should create a job from an image when restart is OnFailure")
+async def kubectl_run_job(f):
+    rc, out = await _kubectl(f, "run", "-n", f.ns, "e2e-test-job", "--restart=OnFailure", "--generator=job/v1",
+                             f"--image={BUSYBOX}", "--command", "--", "sh", "-c", "echo ok")
+    assert rc == 0, out
+    job = await f.client.get("jobs", "e2e-test-job", f.ns)
+    tmpl = job["spec"]["template"]["spec"]
+    assert tmpl["containers"][0]["image"] == BUSYBOX and tmpl["restartPolicy"] == "OnFailure", job
+
+
+@conformance("Kubectl client Kubectl run rc should create an rc from an image")
+async def kubectl_run_rc(f):
+    rc, out = await _kubectl(f, "run", "-n", f.ns, "e2e-test-rc", f"--image={BUSYBOX}", "--generator=run/v1",
+                             "--command", "--", "sh", "-c", "sleep 3600")
+    assert rc == 0, out
+    obj = await f.client.get("replicationcontrollers", "e2e-test-rc", f.ns)
+    assert obj["spec"]["template"]["spec"]["containers"][0]["image"] == BUSYBOX
+    await _wait_pods(f, "run=e2e-test-rc", 1)
+
+
+@conformance("Kubectl client Kubectl run default should create an rc or deployment from an image")
+async def kubectl_run_default(f):
+    rc, out = await _kubectl(f, "run", "-n", f.ns, "e2e-test-default", f"--image={BUSYBOX}", "--command", "--",
+                             "sh", "-c", "sleep 3600")
+    assert rc == 0, out
+    kinds = []
+    for res in ("deployments", "replicationcontrollers"):
+        try:
+            await f.client.get(res, "e2e-test-default", f.ns)
+            kinds.append(res)
+        except Exception:  # noqa: BLE001
+            pass
+    assert kinds, out
+    await _wait_pods(f, "run=e2e-test-default", 1)
+
+
+@conformance("Kubectl client Update Demo should create and stop a replication controller")
+async def kubectl_create_stop_rc(f):
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as tf:
+        json.dump(dict(_rc("update-demo", 2, labels={"name": "update-demo"}), kind="ReplicationController",
+                       apiVersion="v1"), tf)
+    try:
+        rc, out = await _kubectl(f, "create", "-n", f.ns, "-f", tf.name)
+        assert rc == 0, out
+        await _wait_pods(f, "name=update-demo", 2)
+        rc, out = await _kubectl(f, "delete", "-n", f.ns, "--grace-period=0", "-f", tf.name)
+        assert rc == 0, out
+
+        async def stopped():
+            return not await _pods(f, "name=update-demo")
+        await f.wait(stopped, 90, "the rc's pods gone")
+    finally:
+        os.unlink(tf.name)
+
+
+@conformance("Kubectl client Update Demo should scale a replication controller")
+async def kubectl_scale_rc(f):
+    await f.client.create("replicationcontrollers", _rc("update-demo", 2, labels={"name": "update-demo"}), f.ns)
+    await _wait_pods(f, "name=update-demo", 2)
+    rc, out = await _kubectl(f, "scale", "-n", f.ns, "rc", "update-demo", "--replicas=1", "--timeout=5m")
+    assert rc == 0, out
+    await _wait_pods(f, "name=update-demo", 1)
+    rc, out = await _kubectl(f, "scale", "-n", f.ns, "rc", "update-demo", "--replicas=2", "--timeout=5m")
+    assert rc == 0, out
+    await _wait_pods(f, "name=update-demo", 2)
+
+
+@conformance("Kubectl client Update Demo should do a rolling update of a replication controller")
+async def kubectl_rolling_update(f):
+    await f.client.create("replicationcontrollers", _rc("update-demo", 2, labels={"name": "update-demo"}), f.ns)
+    await _wait_pods(f, "name=update-demo", 2)
+    rc, out = await _kubectl(f, "rolling-update", "-n", f.ns, "update-demo", "--update-period=1s",
+                             f"--image={BUSYBOX}:next", "--timeout=3m")
+    assert rc == 0, out
+    pods = await _wait_pods(f, "name=update-demo", 2)
+    assert all(p["spec"]["containers"][0]["image"] == f"{BUSYBOX}:next" for p in pods), pods
+
+
+@conformance("Kubectl client Kubectl rolling-update should support rolling-update to same image")
+async def kubectl_rolling_update_same(f):
+    await _kubectl(f, "run", "-n", f.ns, "e2e-test-rc", f"--image={BUSYBOX}", "--generator=run/v1",
+                   "--command", "--", "sh", "-c", "sleep 3600")
+    await _wait_pods(f, "run=e2e-test-rc", 1)
+    rc, out = await _kubectl(f, "rolling-update", "-n", f.ns, "e2e-test-rc", "--update-period=1s",
+                             f"--image={BUSYBOX}", "--image-pull-policy=IfNotPresent", "--timeout=3m")
+    assert rc == 0, out
+    pods = await _wait_pods(f, "run=e2e-test-rc", 1)
+    assert pods[0]["spec"]["containers"][0]["image"] == BUSYBOX
+
+
+@conformance("Kubectl client Kubectl replace should update a single-container pod's image")
+async def kubectl_replace_image(f):
+    rc, out = await _kubectl(f, "run", "-n", f.ns, "e2e-test-pod", "--generator=run-pod/v1", f"--image={BUSYBOX}",
+                             "--restart=Always", "--labels=run=e2e-test-pod", "--command", "--", "sh", "-c",
+                             "sleep 3600")
+    assert rc == 0, out
+    await f.pod_phase("e2e-test-pod", ("Running",))
+    for attempt in range(5):
+        # `kubectl get -o json | sed | kubectl replace -f -`: the object carries its
+        # resourceVersion, so a kubelet status write in between is a conflict — fetch again
+        pod = await f.client.get("pods", "e2e-test-pod", f.ns)
+        pod["spec"]["containers"][0]["image"] = f"{BUSYBOX}:replaced"
+        with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as tf:
+            json.dump(pod, tf)
+        try:
+            rc, out = await _kubectl(f, "replace", "-n", f.ns, "-f", tf.name)
+        finally:
+            os.unlink(tf.name)
+        if rc == 0:
+            break
+        await asyncio.sleep(0.2)
+    assert rc == 0, out
+    got = await f.client.get("pods", "e2e-test-pod", f.ns)
+    assert got["spec"]["containers"][0]["image"] == f"{BUSYBOX}:replaced"
+
+
+@conformance("Kubectl client Kubectl expose should create services for rc")
+async def kubectl_expose_rc(f):
+    port = _free_port()
+    srv = f"{PY} -c \"import http.server as h; h.HTTPServer(('0.0.0.0', {port}), h.SimpleHTTPRequestHandler).serve_forever()\""
+    rc_obj = _rc("redis-master", 1, cmd=srv, labels={"app": "redis", "role": "master"})
+    rc_obj["spec"]["template"]["spec"]["containers"][0]["ports"] = [{"containerPort": port}]
+    await f.client.create("replicationcontrollers", rc_obj, f.ns)
+    await _wait_pods(f, "app=redis", 1)
+    rc, out = await _kubectl(f, "expose", "-n", f.ns, "rc", "redis-master", "--name=rm2", "--port=1234",
+                             f"--target-port={port}")
+    assert rc == 0, out
+
+    async def endpoints(name):
+        try:
+            ep = await f.client.get("endpoints", name, f.ns)
+        except Exception:  # noqa: BLE001
+            return None
+        ports = [p["port"] for ss in ep.get("subsets") or () for p in ss.get("ports") or ()]
+        return ep if port in ports else None
+    await f.wait(lambda: endpoints("rm2"), 60, "endpoints of rm2")
+    svc = await f.client.get("services", "rm2", f.ns)
+    assert svc["spec"]["ports"][0]["port"] == 1234
+    rc, out = await _kubectl(f, "expose", "-n", f.ns, "service", "rm2", "--name=rm3", "--port=2345",
+                             f"--target-port={port}")
+    assert rc == 0, out
+    await f.wait(lambda: endpoints("rm3"), 60, "endpoints of rm3")
+
+
+async def _proxy_get(reader_writer, path):
+    reader, writer = reader_writer
+    writer.write(f"GET {path} HTTP/1.1\r\nHost: localhost\r\nConnection: close\r\n\r\n".encode())
+    await writer.drain()
+    data = await asyncio.wait_for(reader.read(), 15)
+    writer.close()
+    return data.decode(errors="replace")
+
+
+@conformance("Kubectl client Proxy server should support proxy with --port 0")
+async def kubectl_proxy_port0(f):
+    p = await asyncio.create_subprocess_exec(PY, "-m", "kubernetes_amd.kubectl", "-s", f.client.url, "proxy",
+                                             "-p", "0", "--disable-filter", stdout=asyncio.subprocess.PIPE,
+                                             stderr=asyncio.subprocess.STDOUT)
+    try:
+        line = (await asyncio.wait_for(p.stdout.readline(), 30)).decode()
+        m = re.search(r"Starting to serve on [^:]+:(\d+)", line)
+        assert m, line
+        body = await _proxy_get(await asyncio.open_connection("127.0.0.1", int(m.group(1))), "/api/")
+        assert '"versions"' in body and "v1" in body, body
+    finally:
+        p.kill()
+        await p.wait()
+
+
+@conformance("Kubectl client Proxy server should support --unix-socket=/path")
+async def kubectl_proxy_unix(f):
+    d = tempfile.mkdtemp(prefix="kamd-proxy-")
+    path = os.path.join(d, "test")
+    p = await asyncio.create_subprocess_exec(PY, "-m", "kubernetes_amd.kubectl", "-s", f.client.url, "proxy",
+                                             f"--unix-socket={path}", stdout=asyncio.subprocess.PIPE,
+                                             stderr=asyncio.subprocess.STDOUT)
+    try:
+        line = (await asyncio.wait_for(p.stdout.readline(), 30)).decode()
+        assert path in line, line
+        body = await _proxy_get(await asyncio.open_unix_connection(path), "/api/")
+        assert '"versions"' in body, body
+    finally:
+        p.kill()
+        await p.wait()
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# Probes (container_probe.go): HTTP liveness, readiness initial delay
+def _http_health_pod(name, port, healthy_for):
+    """A pod serving /healthz: 200 for `healthy_for` seconds after start, then 500 (None: always 200)."""
+    code = ("import http.server as h, time\n"
+            "t0 = time.time()\n"
+            "class H(h.BaseHTTPRequestHandler):\n"
+            "    def do_GET(self):\n"
+            f"        ok = {healthy_for!r} is None or time.time() - t0 < {healthy_for!r}\n"
+            "        self.send_response(200 if ok else 500); self.end_headers(); self.wfile.write(b'ok')\n"
+            "    def log_message(self, *a): pass\n"
+            f"h.HTTPServer(('0.0.0.0', {port}), H).serve_forever()\n")
+    p = {"metadata": {"name": name}, "spec": {"restartPolicy": "Always", "containers": [
+        {"name": "c", "image": BUSYBOX, "command": [PY, "-c", code],
+         "livenessProbe": {"httpGet": {"path": "/healthz", "port": port}, "initialDelaySeconds": 2,
+                           "periodSeconds": 1, "failureThreshold": 1}}]}}
+    return p
+
+
+async def _restarts(f, name):
+    p = await f.client.get("pods", name, f.ns)
+    return sum(c.get("restartCount", 0) for c in (p.get("status") or {}).get("containerStatuses") or ())
+
+
+@conformance("Probing container should be restarted with a /healthz http liveness probe")
+async def probe_http_restart(f):
+    await f.client.create("pods", _http_health_pod("liveness-http", _free_port(), 3), f.ns)
+    await f.pod_phase("liveness-http", ("Running",))
+
+    async def restarted():
+        return await _restarts(f, "liveness-http") >= 1
+    await f.wait(restarted, 60, "a liveness restart")
+
+
+@conformance("Probing container should *not* be restarted with a /healthz http liveness probe")
+async def probe_http_no_restart(f):
+    await f.client.create("pods", _http_health_pod("liveness-http-ok", _free_port(), None), f.ns)
+    await f.pod_phase("liveness-http-ok", ("Running",))
+    await asyncio.sleep(8)
+    assert await _restarts(f, "liveness-http-ok") == 0
+
+
+@conformance("Probing container with readiness probe should not be ready before initial delay and never restart")
+async def probe_readiness_initial_delay(f):
+    p = _pod("ready-delay", "sleep 3600", restart="Always")
+    p["spec"]["containers"][0]["readinessProbe"] = {"exec": {"command": ["true"]}, "initialDelaySeconds": 4,
+                                                    "periodSeconds": 1}
+    await f.client.create("pods", p, f.ns)
+    pod = await f.pod_phase("ready-delay", ("Running",))
+    started = time.time()
+
+    async def ready():
+        x = await f.client.get("pods", "ready-delay", f.ns)
+        return x if any(c.get("type") == "Ready" and c.get("status") == "True"
+                        for c in (x.get("status") or {}).get("conditions") or ()) else None
+    x = await f.wait(ready, 60, "readiness")
+    from ..api.meta import parse_rfc3339
+    cs = x["status"]["containerStatuses"][0]
+    run_at = parse_rfc3339(cs["state"]["running"]["startedAt"])
+    ready_at = max(parse_rfc3339(c["lastTransitionTime"]) for c in x["status"]["conditions"] if c["type"] == "Ready")
+    assert ready_at - run_at >= 3.0, (run_at, ready_at, pod["status"])
+    assert cs.get("restartCount", 0) == 0 and time.time() - started < 60
+
+
+# ---------------------------------------------------------------------------------------------
+# secrets.go, host_path.go, kubelet_etc_hosts.go
+@conformance("Secrets should be consumable from pods in env vars")
+async def secret_env_key_ref(f):
+    await _secret(f)
+    p = _pod("secenvref", "echo SECRET_DATA=$SECRET_DATA")
+    p["spec"]["containers"][0]["env"] = [{"name": "SECRET_DATA",
+                                          "valueFrom": {"secretKeyRef": {"name": "sec", "key": "data-1"}}}]
+    assert "SECRET_DATA=value-1" in await _run_and_log(f, p)
+
+
+@conformance("HostPath should give a volume the correct mode")
+async def hostpath_mode(f):
+    p = _mount(_pod("hostpath-mode", f"stat -c %a {_at('test-volume', '/test-volume', '.')}"),
+               "test-volume", {"hostPath": {"path": "/tmp"}}, "/test-volume")
+    assert _lines(await _run_and_log(f, p)) == ["1777"]
+
+
+@conformance("KubeletManagedEtcHosts should test kubelet managed /etc/hosts file")
+async def kubelet_etc_hosts(f):
+    p = _pod("test-pod", "cat /etc/hosts", restart="Never")
+    p["spec"]["hostAliases"] = [{"ip": "123.45.67.89", "hostnames": ["foo.e2e", "bar.e2e"]}]
+    out = await _run_and_log(f, p)
+    node = (await f.client.list("nodes"))["items"][0]
+    iso = [c for c in node["status"].get("conditions") or () if c["type"] == "IsolationUnavailable"]
+    if "# Kubernetes-managed hosts file" not in out:
+        # without a mount namespace the container sees the node's /etc/hosts
+        if iso and iso[0]["status"] == "True":
+            raise Skip("the node's runtime has no mount namespace: /etc/hosts cannot be managed per pod")
+        if not any("tier landlock" in (c.get("message") or "") for c in iso):
+            raise AssertionError(out)
+        raise Skip("landlock tier: no mount namespace, /etc/hosts is the node's")
+    assert "foo.e2e" in out and "123.45.67.89" in out, out
+    hn = _pod("test-host-network-pod", "cat /etc/hosts", hostNetwork=True)
+    out2 = await _run_and_log(f, hn)
+    assert "# Kubernetes-managed hosts file" not in out2, out2
+
+
+# ---------------------------------------------------------------------------------------------
+# networking.go: pods reach each other and the node over http and udp
+_UDP_SERVER = ("import socket\n"
+               "s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM); s.bind(('0.0.0.0', {port}))\n"
+               "while True:\n"
+               "    d, a = s.recvfrom(1024); s.sendto(b'hostName:' + socket.gethostname().encode() + b':' + d, a)\n")
+_HTTP_SERVER = ("import http.server as h, socket\n"
+                "class H(h.BaseHTTPRequestHandler):\n"
+                "    def do_GET(self):\n"
+                "        self.send_response(200); self.end_headers()\n"
+                "        self.wfile.write(('hostName:' + socket.gethostname()).encode())\n"
+                "    def log_message(self, *a): pass\n"
+                "h.HTTPServer(('0.0.0.0', {port}), H).serve_forever()\n")
+_HTTP_CLIENT = ("import urllib.request, sys\n"
+                "print(urllib.request.urlopen('http://{ip}:{port}/hostName', timeout=5).read().decode())\n")
+_UDP_CLIENT = ("import socket\n"
+               "s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM); s.settimeout(5)\n"
+               "s.sendto(b'hello', ('{ip}', {port})); print(s.recvfrom(1024)[0].decode())\n")
+
+
+async def _server_pod(f, name, proto):
+    port = _free_port()
+    code = (_HTTP_SERVER if proto == "http" else _UDP_SERVER).format(port=port)
+    p = {"metadata": {"name": name, "labels": {"selector": name}}, "spec": {"restartPolicy": "Always",
+                                                                          "hostname": name, "containers": [
+        {"name": "webserver", "image": BUSYBOX, "command": [PY, "-c", code],
+         "ports": [{"containerPort": port, "protocol": "TCP" if proto == "http" else "UDP"}]}]}}
+    await f.client.create("pods", p, f.ns)
+    pod = await f.pod_phase(name, ("Running",))
+    return pod["status"].get("podIP"), port
+
+
+async def _client_reaches(f, name, proto, ip, port):
+    code = (_HTTP_CLIENT if proto == "http" else _UDP_CLIENT).format(ip=ip, port=port)
+    p = {"metadata": {"name": name}, "spec": {"restartPolicy": "OnFailure", "containers": [
+        {"name": "c", "image": BUSYBOX, "command": [PY, "-c", code]}]}}
+    out = await _run_and_log(f, p, 90)
+    assert "hostName:" in out, out
+
+
+@conformance("Networking Granular Checks: Pods should function for intra-pod communication: http")
+async def net_intra_pod_http(f):
+    ip, port = await _server_pod(f, "netserver-0", "http")
+    await _client_reaches(f, "test-container-pod", "http", ip, port)
+
+
+@conformance("Networking Granular Checks: Pods should function for intra-pod communication: udp")
+async def net_intra_pod_udp(f):
+    ip, port = await _server_pod(f, "netserver-0", "udp")
+    await _client_reaches(f, "test-container-pod", "udp", ip, port)
+
+
+@conformance("Networking Granular Checks: Pods should function for node-pod communication: http")
+async def net_node_pod_http(f):
+    ip, port = await _server_pod(f, "netserver-0", "http")
+    # the node side: a hostNetwork pod is the node's network namespace
+    code = _HTTP_CLIENT.format(ip=ip, port=port)
+    p = {"metadata": {"name": "host-test-container-pod"}, "spec": {"restartPolicy": "OnFailure", "hostNetwork": True,
+                                                                   "containers": [{"name": "c", "image": BUSYBOX,
+                                                                                   "command": [PY, "-c", code]}]}}
+    assert "hostName:" in await _run_and_log(f, p, 90)
+
+
+@conformance("Networking Granular Checks: Pods should function for node-pod communication: udp")
+async def net_node_pod_udp(f):
+    ip, port = await _server_pod(f, "netserver-0", "udp")
+    code = _UDP_CLIENT.format(ip=ip, port=port)
+    p = {"metadata": {"name": "host-test-container-pod"}, "spec": {"restartPolicy": "OnFailure", "hostNetwork": True,
+                                                                   "containers": [{"name": "c", "image": BUSYBOX,
+                                                                                   "command": [PY, "-c", code]}]}}
+    assert "hostName:" in await _run_and_log(f, p, 90)
+
+
+# ---------------------------------------------------------------------------------------------
+# service.go
+@conformance("Services should provide secure master service")
+async def svc_master(f):
+    svc = await f.client.get("services", "kubernetes", "default")
+    assert any(p.get("port") == 443 and p.get("name") == "https" for p in svc["spec"]["ports"]), svc
+
+
+async def _eps(f, name):
+    try:
+        ep = await f.client.get("endpoints", name, f.ns)
+    except Exception:  # noqa: BLE001
+        return {}
+    out = {}
+    for ss in ep.get("subsets") or ():
+        for a in ss.get("addresses") or ():
+            ref = (a.get("targetRef") or {}).get("name")
+            out.setdefault(ref, set()).update(p["port"] for p in ss.get("ports") or ())
+    return out
+
+
+async def _expect_eps(f, name, want, timeout=60.0):
+    async def check():
+        got = await _eps(f, name)
+        return got == want
+    await f.wait(check, timeout, f"endpoints {name} == {want}")
+
+
+def _pause_pod(name, labels, ports):
+    p = _pod(name, "sleep 3600", restart="Always")
+    p["metadata"]["labels"] = labels
+    p["spec"]["containers"][0]["ports"] = [{"containerPort": x, "name": f"p{x}"} for x in ports]
+    return p
+
+
+@conformance("Services should serve a basic endpoint from pods")
+async def svc_basic_endpoint(f):
+    await f.client.create("services", {"metadata": {"name": "endpoint-test2"}, "spec": {
+        "selector": {"name": "endpoint-test2"}, "ports": [{"port": 80, "targetPort": 80}]}}, f.ns)
+    await _expect_eps(f, "endpoint-test2", {})
+    lbl = {"name": "endpoint-test2"}
+    await f.client.create("pods", _pause_pod("pod1", lbl, [80]), f.ns)
+    await _expect_eps(f, "endpoint-test2", {"pod1": {80}})
+    await f.client.create("pods", _pause_pod("pod2", lbl, [80]), f.ns)
+    await _expect_eps(f, "endpoint-test2", {"pod1": {80}, "pod2": {80}})
+    await f.client.delete("pods", "pod1", f.ns, grace_period=0)
+    await _expect_eps(f, "endpoint-test2", {"pod2": {80}})
+    await f.client.delete("pods", "pod2", f.ns, grace_period=0)
+    await _expect_eps(f, "endpoint-test2", {})
+
+
+@conformance("Services should serve multiport endpoints from pods")
+async def svc_multiport(f):
+    await f.client.create("services", {"metadata": {"name": "multi-endpoint-test"}, "spec": {
+        "selector": {"name": "multi"}, "ports": [{"name": "portname1", "port": 80, "targetPort": "svc1"},
+                                                 {"name": "portname2", "port": 81, "targetPort": "svc2"}]}}, f.ns)
+    p1 = _pause_pod("pod1", {"name": "multi"}, [])
+    p1["spec"]["containers"][0]["ports"] = [{"name": "svc1", "containerPort": 100}]
+    p2 = _pause_pod("pod2", {"name": "multi"}, [])
+    p2["spec"]["containers"][0]["ports"] = [{"name": "svc2", "containerPort": 101}]
+    await f.client.create("pods", p1, f.ns)
+    await _expect_eps(f, "multi-endpoint-test", {"pod1": {100}})
+    await f.client.create("pods", p2, f.ns)
+    await _expect_eps(f, "multi-endpoint-test", {"pod1": {100}, "pod2": {101}})
+    await f.client.delete("pods", "pod1", f.ns, grace_period=0)
+    await _expect_eps(f, "multi-endpoint-test", {"pod2": {101}})
+
+
+# ---------------------------------------------------------------------------------------------
+# proxy.go: node logs through the apiserver proxy, with and without the explicit kubelet port
+async def _node_logs(f, path):
+    st, body = await f.client.raw("GET", path)
+    assert st == 200, (path, st, body[:300])
+    return body
+
+
+async def _first_node(f):
+    node = (await f.client.list("nodes"))["items"][0]
+    return node["metadata"]["name"], node["status"]["daemonEndpoints"]["kubeletEndpoint"]["Port"]
+
+
+@conformance("Proxy version v1 should proxy logs on node")
+async def proxy_node_logs(f):
+    name, _ = await _first_node(f)
+    await _node_logs(f, f"/api/v1/proxy/nodes/{name}/logs/")
+
+
+@conformance("Proxy version v1 should proxy logs on node with explicit kubelet port")
+async def proxy_node_logs_port(f):
+    name, port = await _first_node(f)
+    await _node_logs(f, f"/api/v1/proxy/nodes/{name}:{port}/logs/")
+
+
+@conformance("Proxy version v1 should proxy logs on node with explicit kubelet port using proxy subresource")
+async def proxy_node_logs_port_sub(f):
+    name, port = await _first_node(f)
+    await _node_logs(f, f"/api/v1/nodes/{name}:{port}/proxy/logs/")
+
+
+# ---------------------------------------------------------------------------------------------
+# service_accounts.go
+@conformance("ServiceAccounts should allow opting out of API token automount")
+async def sa_opt_out(f):
+    await f.client.create("serviceaccounts", {"metadata": {"name": "mount"}}, f.ns)
+    await f.client.create("serviceaccounts", {"metadata": {"name": "nomount"}, "automountServiceAccountToken": False},
+                          f.ns)
+
+    async def token(name):
+        sa = await f.client.get("serviceaccounts", name, f.ns)
+        return sa if sa.get("secrets") else None
+    try:
+        await f.wait(lambda: token("mount"), 20, "a token for the service account")
+    except TimeoutError:
+        raise Skip("no token controller runs in this cluster (--service-account-private-key-file)")
+    cases = [("pod-service-account-defaultsa", "default", None, True),
+             ("pod-service-account-mountsa", "mount", None, True),
+             ("pod-service-account-nomountsa", "nomount", None, False),
+             ("pod-service-account-defaultsa-mountspec", "default", True, True),
+             ("pod-service-account-nomountsa-mountspec", "nomount", True, True),
+             ("pod-service-account-defaultsa-nomountspec", "default", False, False),
+             ("pod-service-account-nomountsa-nomountspec", "nomount", False, False)]
+    for name, sa, spec_mount, want in cases:
+        try:
+            await f.wait(lambda sa=sa: token(sa), 20, f"token of {sa}")
+        except TimeoutError:
+            pass
+        p = _pod(name, "sleep 3600", restart="Always", serviceAccountName=sa)
+        if spec_mount is not None:
+            p["spec"]["automountServiceAccountToken"] = spec_mount
+        got = await f.client.create("pods", p, f.ns)
+        mounted = any(m.get("mountPath") == "/var/run/secrets/kubernetes.io/serviceaccount"
+                      for m in got["spec"]["containers"][0].get("volumeMounts") or ())
+        assert mounted == want, (name, got["spec"])
+
+
+@conformance("ServiceAccounts should mount an API token into pods")
+async def sa_mount_token(f):
+    async def default_sa():
+        try:
+            sa = await f.client.get("serviceaccounts", "default", f.ns)
+        except Exception:  # noqa: BLE001
+            return None
+        return sa if sa.get("secrets") else None
+    try:
+        sa = await f.wait(default_sa, 20, "the default service account's token")
+    except TimeoutError:
+        raise Skip("no token controller runs in this cluster (--service-account-private-key-file)")
+    sec = await f.client.get("secrets", sa["secrets"][0]["name"], f.ns)
+    base = "/var/run/secrets/kubernetes.io/serviceaccount"
+    # at the mount path with a mount namespace, else at the host path the runtime exports for the
+    # admission-generated volume (KUBERNETES_VOLUME_DEFAULT_TOKEN_<suffix>)
+    cmd = (f'd={base}; [ -e "$d/token" ] || d=$(env | sed -n "s/^KUBERNETES_VOLUME_DEFAULT_TOKEN_[^=]*=//p" | head -1); '
+           'for n in token ca.crt namespace; do cat "$d/$n"; echo; done')
+    got = await f.client.create("pods", _pod("pod-service-account", cmd), f.ns)
+    assert any(m.get("mountPath") == base for m in got["spec"]["containers"][0].get("volumeMounts") or ()), got["spec"]
+    await f.pod_phase("pod-service-account", ("Succeeded",), 60)
+    out = await f.logs("pod-service-account")
+    import base64
+    assert base64.b64decode(sec["data"]["token"]).decode() in out, out
+    assert f.ns in out, out
+    if sec["data"].get("ca.crt"):                 # the token controller's root CA, when it has one
+        assert base64.b64decode(sec["data"]["ca.crt"]).decode().strip() in out, out
+
+
+# ---------------------------------------------------------------------------------------------
+# rc.go / replica_set.go: every replica serves
+async def _serve_each_replica(f, kind):
+    port = _free_port()
+    code = _HTTP_SERVER.format(port=port)
+    name = "my-hostname-basic"
+    tmpl = {"metadata": {"labels": {"name": name}}, "spec": {"containers": [
+        {"name": name, "image": BUSYBOX, "command": [PY, "-c", code], "ports": [{"containerPort": port}]}]}}
+    if kind == "replicationcontrollers":
+        obj = {"metadata": {"name": name}, "spec": {"replicas": 1, "selector": {"name": name}, "template": tmpl}}
+    else:
+        obj = {"apiVersion": "extensions/v1beta1", "kind": "ReplicaSet", "metadata": {"name": name},
+               "spec": {"replicas": 1, "selector": {"matchLabels": {"name": name}}, "template": tmpl}}
+    await f.client.create(kind, obj, f.ns)
+    pods = await _wait_pods(f, f"name={name}", 1)
+    for p in pods:
+        path = f"/api/v1/namespaces/{f.ns}/pods/{p['metadata']['name']}:{port}/proxy/"
+
+        async def answers(path=path):
+            st, body = await f.client.raw("GET", path)
+            return body if st == 200 and b"hostName:" in body else None
+        await f.wait(answers, 60, f"the replica {p['metadata']['name']} answering through the proxy")
+
+
+@conformance("ReplicationController should serve a basic image on each replica with a public image")
+async def rc_serve(f):
+    await _serve_each_replica(f, "replicationcontrollers")
+
+
+@conformance("ReplicaSet should serve a basic image on each replica with a public image")
+async def rs_serve(f):
+    await _serve_each_replica(f, "replicasets")
+
+
+# ---------------------------------------------------------------------------------------------
+# predicates.go
+@conformance("SchedulerPredicates validates that NodeSelector is respected if matching")
+async def nodeselector_matching(f):
+    nodes = (await f.client.list("nodes"))["items"]
+    node = nodes[0]["metadata"]["name"]
+    key = "kubernetes.io/e2e-" + f.ns
+    await f.client.patch("nodes", node, {"metadata": {"labels": {key: "42"}}})
+    try:
+        p = _pod("with-labels", "sleep 3600", restart="Always", nodeSelector={key: "42"})
+        await f.client.create("pods", p, f.ns)
+        pod = await f.pod_phase("with-labels", ("Running",))
+        assert pod["spec"]["nodeName"] == node
+    finally:
+        await f.client.patch("nodes", node, {"metadata": {"labels": {key: None}}})
+
+
+
+# ---------------------------------------------------------------------------------------------
+# proxy.go: through a service and a pod (the http rows of the reference's table; ports are
+# ephemeral since the process runtime's pods may share the node's network)
+_PORTER = ("import http.server as h, threading, sys\n"
+           "def serve(port, body):\n"
+           "    class H(h.BaseHTTPRequestHandler):\n"
+           "        def do_GET(self):\n"
+           "            b = body.encode(); self.send_response(200)\n"
+           "            self.send_header('Content-Length', str(len(b))); self.end_headers(); self.wfile.write(b)\n"
+           "        def log_message(self, *a): pass\n"
+           "    h.ThreadingHTTPServer(('0.0.0.0', port), H).serve_forever()\n"
+           "ports = {ports!r}\n"
+           "for p, b in ports.items():\n"
+           "    threading.Thread(target=serve, args=(p, b), daemon=True).start()\n"
+           "threading.Event().wait()\n")
+
+
+@conformance("Proxy version v1 should proxy through a service and a pod")
+async def proxy_service_and_pod(f):
+    p80, p160, p162 = _free_port(), _free_port(), _free_port()
+    bodies = {p80: '<a href="/rewriteme">test</a>', p160: "foo", p162: "bar"}
+    labels = {"proxy-service-target": "true"}
+    svc = await f.client.create("services", {"metadata": {"generateName": "proxy-service-"}, "spec": {
+        "selector": labels, "ports": [{"name": "portname1", "port": 80, "targetPort": "dest1"},
+                                      {"name": "portname2", "port": 81, "targetPort": p162}]}}, f.ns)
+    name = svc["metadata"]["name"]
+    tmpl = {"metadata": {"labels": labels}, "spec": {"containers": [
+        {"name": "porter", "image": BUSYBOX, "command": [PY, "-c", _PORTER.format(ports=bodies)],
+         "ports": [{"name": "dest1", "containerPort": p160}, {"name": "dest2", "containerPort": p162},
+                   {"containerPort": p80}],
+         "readinessProbe": {"httpGet": {"port": p80}, "initialDelaySeconds": 1, "periodSeconds": 1}}]}}
+    await f.client.create("replicationcontrollers", {"metadata": {"name": name}, "spec": {
+        "replicas": 1, "selector": labels, "template": tmpl}}, f.ns)
+    pod = (await _wait_pods(f, "proxy-service-target=true", 1))[0]["metadata"]["name"]
+
+    async def ready_endpoints():
+        try:
+            ep = await f.client.get("endpoints", name, f.ns)
+        except Exception:  # noqa: BLE001
+            return None
+        return any(ss.get("addresses") for ss in ep.get("subsets") or ())
+    await f.wait(ready_endpoints, 60, "the service's ready endpoint")
+    ns = f.ns
+    expect = {}
+    for scheme in ("", "http:"):
+        for port, body in (("portname1", "foo"), ("portname2", "bar")):
+            expect[f"/api/v1/proxy/namespaces/{ns}/services/{scheme}{name}:{port}/"] = body
+            expect[f"/api/v1/namespaces/{ns}/services/{scheme}{name}:{port}/proxy/"] = body
+        for port, body in ((p80, bodies[p80]), (p160, "foo"), (p162, "bar")):
+            expect[f"/api/v1/proxy/namespaces/{ns}/pods/{scheme}{pod}:{port}/"] = body
+            expect[f"/api/v1/namespaces/{ns}/pods/{scheme}{pod}:{port}/proxy/"] = body
+    errors = []
+    for _ in range(3):           # the reference retries each URL a few times, then reports all misses
+        errors = []
+        for path, want in expect.items():
+            st, body = await f.client.raw("GET", path)
+            if st != 200 or body.decode(errors="replace") != want:
+                errors.append(f"{path}: {st} {body[:120]!r} (want {want!r})")
+        if not errors:
+            break
+        await asyncio.sleep(1)
+    assert not errors, "\n".join(errors)
+
+
+# ---------------------------------------------------------------------------------------------
+# service_latency.go: endpoints follow new services quickly (the reference creates 200 services
+# against one pod and bounds the p50 / p99 of service creation -> endpoints seen)
+@conformance("Service endpoints latency should not be very high")
+async def service_endpoint_latency(f):
+    await f.client.create("replicationcontrollers", _rc("svc-latency-rc", 1, labels={"name": "svc-latency-rc"}), f.ns)
+    await _wait_pods(f, "name=svc-latency-rc", 1)
+    n, lat = 50, []
+    w = await f.client.watch("endpoints", f.ns)
+    created: dict = {}
+
+    async def one(i):
+        svc = await f.client.create("services", {"metadata": {"generateName": "latency-svc-"}, "spec": {
+            "selector": {"name": "svc-latency-rc"}, "ports": [{"port": 80, "targetPort": 9376}]}}, f.ns)
+        created[svc["metadata"]["name"]] = time.monotonic()
+    t0 = time.monotonic()
+    creators = asyncio.gather(*(one(i) for i in range(n)))
+    seen = set()
+    try:
+        async def drain():
+            async for _, ep in w:
+                nm = ep["metadata"]["name"]
+                if nm in seen or not any(ss.get("addresses") for ss in ep.get("subsets") or ()):
+                    continue
+                seen.add(nm)
+                lat.append(time.monotonic() - created.get(nm, t0))
+                if len(seen) >= n:
+                    return
+        await asyncio.wait_for(asyncio.gather(creators, drain()), 120)
+    finally:
+        w.close()
+    lat.sort()
+    p50, p99 = lat[len(lat) // 2], lat[min(len(lat) - 1, int(len(lat) * 0.99))]
+    # the reference's limits: p50 <= 20 s, p99 <= 50 s
+    assert len(lat) == n and p50 <= 20 and p99 <= 50, (p50, p99, len(lat))

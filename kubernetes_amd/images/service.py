@@ -52,8 +52,8 @@ class ImageService:
     def _builtin(self, image) -> bool:
         if self.builtins is None:
             return False
-        from ..kubelet.runtime.process import IMAGES
-        return self.builtins.normalize(image).rsplit(":", 1)[0] in IMAGES
+        from ..kubelet.runtime.process import builtin_argv
+        return builtin_argv(self.builtins.normalize(image).rsplit(":", 1)[0]) is not None
 
     async def image_status(self, image):
         img = self._oci(image)

@@ -1199,6 +1199,13 @@ class Kubectl(extra.ExtraCommands):
             obj = {"apiVersion": "apps/v1beta1" if "apps" in gen else "extensions/v1beta1", "kind": "Deployment",
                    "metadata": md, "spec": {"replicas": a.replicas, "selector": {"matchLabels": labels},
                                             "template": {"metadata": {"labels": labels}, "spec": pod_spec}}}
+        elif gen == "run/v1":
+            # BasicReplicationController (pkg/kubectl/run.go)
+            if a.restart != "Always":
+                raise SystemExit(f"error: --restart={a.restart} is not valid for a ReplicationController")
+            obj = {"apiVersion": "v1", "kind": "ReplicationController", "metadata": md,
+                   "spec": {"replicas": a.replicas, "selector": dict(labels),
+                            "template": {"metadata": {"labels": labels}, "spec": pod_spec}}}
         elif gen.startswith("job"):
             obj = {"apiVersion": "batch/v1", "kind": "Job", "metadata": md,
                    "spec": {"template": {"metadata": {"labels": labels},
@@ -1944,7 +1951,7 @@ def build_parser():
         else:
             c.add_argument("--force", action="store_true")
             c.add_argument("--grace-period", type=int, default=-1)
-            c.add_argument("--timeout", type=float, default=0)
+            c.add_argument("--timeout", type=extra.duration, default=0)
             c.add_argument("--cascade", type=_bool, default=True)
         if name == "apply":
             c.add_argument("--prune", action="store_true")
@@ -1975,7 +1982,7 @@ def build_parser():
     de.add_argument("--ignore-not-found", action="store_true")
     de.add_argument("--force", action="store_true", help="immediate deletion (--grace-period=0)")
     de.add_argument("--now", action="store_true", help="grace period 1")
-    de.add_argument("--timeout", type=float, default=0, help="wait this long for the objects to be gone")
+    de.add_argument("--timeout", type=extra.duration, default=0, help="wait this long for the objects to be gone")
     de.add_argument("-o", "--output", default="")
     _common(de)
     lg = add("logs")
@@ -1990,7 +1997,7 @@ def build_parser():
     lg.add_argument("--timestamps", action="store_true")
     lg.add_argument("--limit-bytes", type=int, default=0)
     lg.add_argument("-l", "--selector")
-    lg.add_argument("--pod-running-timeout", type=float, default=20.0)
+    lg.add_argument("--pod-running-timeout", type=extra.duration, default=20.0)
     lg.add_argument("--interactive", action="store_true", help="deprecated; ignored")
     for name in ("label", "annotate"):
         la = add(name)
@@ -2026,7 +2033,7 @@ def build_parser():
     sc.add_argument("--resource-version", default="")
     sc.add_argument("--all", action="store_true")
     sc.add_argument("-l", "--selector")
-    sc.add_argument("--timeout", type=float, default=0, help="wait for the new size to be ready")
+    sc.add_argument("--timeout", type=extra.duration, default=0, help="wait for the new size to be ready")
     sc.add_argument("-f", "--filename", action="append")
     sc.add_argument("--record", action="store_true")
     _common(sc)
@@ -2042,7 +2049,7 @@ def build_parser():
     dr.add_argument("--grace-period", type=int, default=None)
     dr.add_argument("--delete-local-data", action="store_true", help="also evict pods with emptyDir volumes")
     dr.add_argument("--dry-run", action="store_true")
-    dr.add_argument("--timeout", type=float, default=0, help="give up after this many seconds (0 = never)")
+    dr.add_argument("--timeout", type=extra.duration, default=0, help="give up after this many seconds (0 = never)")
     dr.add_argument("-l", "--selector", help="drain every node matching this label selector")
     ta = add("taint")
     ta.add_argument("nodes_kw", choices=["nodes", "node", "no"])
@@ -2066,7 +2073,7 @@ def build_parser():
     ro.add_argument("--to-revision", type=int, default=0)
     ro.add_argument("--revision", type=int, default=0, help="status: the revision to wait for; history: show its template")
     ro.add_argument("-w", "--watch", type=lambda s: s.lower() != "false", default=True)
-    ro.add_argument("--timeout", type=float, default=300)
+    ro.add_argument("--timeout", type=extra.duration, default=300)
     rn = add("run")
     rn.add_argument("name")
     rn.add_argument("--image", required=True)
@@ -2095,7 +2102,7 @@ def build_parser():
     rn.add_argument("--serviceaccount", default="")
     rn.add_argument("--quiet", action="store_true")
     rn.add_argument("--record", action="store_true")
-    rn.add_argument("--pod-running-timeout", type=float, default=60.0)
+    rn.add_argument("--pod-running-timeout", type=extra.duration, default=60.0)
     rn.add_argument("--service-generator", default="")
     rn.add_argument("--service-overrides", default="")
     rn.add_argument("run_command", nargs="*", metavar="command")
@@ -2132,7 +2139,7 @@ def build_parser():
     ci.add_argument("--namespaces", default="")
     ci.add_argument("--output-directory", default="")
     ci.add_argument("-o", "--output", default="json")
-    ci.add_argument("--pod-running-timeout", type=float, default=20.0)
+    ci.add_argument("--pod-running-timeout", type=extra.duration, default=20.0)
     e = add("explain")
     e.add_argument("resource")
     e.add_argument("--recursive", action="store_true")
@@ -2140,7 +2147,7 @@ def build_parser():
     w = add("wait")
     w.add_argument("targets", nargs="+")
     w.add_argument("--for", dest="for_", required=True)
-    w.add_argument("--timeout", type=float, default=30)
+    w.add_argument("--timeout", type=extra.duration, default=30)
     au = add("auth")
     au.add_argument("action", choices=["can-i", "reconcile"])
     au.add_argument("verb", nargs="?")
@@ -2162,7 +2169,7 @@ def build_parser():
     at.add_argument("-c", "--container")
     at.add_argument("-i", "--stdin", action="store_true")
     at.add_argument("-t", "--tty", action="store_true")
-    at.add_argument("--pod-running-timeout", type=float, default=20.0)
+    at.add_argument("--pod-running-timeout", type=extra.duration, default=20.0)
     pf = add("port-forward")
     pf.add_argument("pod")
     pf.add_argument("ports", nargs="+")
@@ -2254,6 +2261,42 @@ def hoist_global_flags(argv):
     return front + rest
 
 
+def _bool_flag_values(ap, argv):
+    """pflag booleans take `--flag=true|false`; argparse's store_true does not: rewrite those
+    tokens (before any `--`) for the flags that are booleans in some subcommand."""
+    table = getattr(ap, "_kamd_bools", None)
+    if table is None:
+        def flags(p, nested):
+            out = set()
+            for act in p._actions:
+                if isinstance(act, (argparse._StoreTrueAction, argparse._StoreFalseAction)):
+                    out.update(o for o in act.option_strings if o.startswith("--"))
+                if nested and isinstance(act, argparse._SubParsersAction):
+                    for sp in act.choices.values():
+                        out |= flags(sp, True)
+            return out
+        table = {None: flags(ap, False)}          # global flags; then per subcommand
+        for act in ap._actions:
+            if isinstance(act, argparse._SubParsersAction):
+                for name, sp in act.choices.items():
+                    table[name] = table[None] | flags(sp, True)
+        ap._kamd_bools = table
+    cmd = next((t for t in argv if not t.startswith("-") and t in table), None)
+    bools = table.get(cmd, table[None])
+    out = []
+    for i, t in enumerate(argv):
+        if t == "--":
+            return out + argv[i:]
+        if t.startswith("--") and "=" in t:
+            k, v = t.split("=", 1)
+            if k in bools and v.lower() in ("true", "false"):
+                if v.lower() == "true":
+                    out.append(k)
+                continue
+        out.append(t)
+    return out
+
+
 def main(argv=None, out=sys.stdout):
     ap = build_parser()
     argv = hoist_global_flags(list(sys.argv[1:] if argv is None else argv))
@@ -2263,6 +2306,7 @@ def main(argv=None, out=sys.stdout):
             break
         if not t_.startswith("-") and (i_ == 0 or not argv[i_ - 1].startswith("-")):
             break
+    argv = _bool_flag_values(ap, argv)
     tail = None
     if "--" in argv and "run" in argv[:argv.index("--")]:
         argv, tail = argv[:argv.index("--")], argv[argv.index("--") + 1:]     # `run NAME ... -- CMD ARGS`

@@ -18,6 +18,7 @@ import difflib
 import hashlib
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -26,6 +27,21 @@ import yaml
 
 from ..api import meta as m
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
+
+
+def duration(v):
+    """A kubectl duration flag: seconds as a number, or a Go duration ("1s", "5m", "1m30s",
+    "500ms", "1h")."""
+    v = str(v).strip()
+    try:
+        return float(v)
+    except ValueError:
+        pass
+    units = {"ns": 1e-9, "us": 1e-6, "µs": 1e-6, "ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0}
+    parts = re.findall(r"(\d+(?:\.\d+)?)(ns|us|µs|ms|s|m|h)", v)
+    if not parts or "".join(n + u for n, u in parts) != v:
+        raise argparse.ArgumentTypeError(f"invalid duration {v!r}")
+    return sum(float(n) * units[u] for n, u in parts)
 
 
 # ------------------------------------------------------------------------------------ generators
@@ -520,8 +536,14 @@ class ExtraCommands:
             new.setdefault("metadata", {})["namespace"] = self.ns
         else:
             new = json.loads(json.dumps(old))
+            same = all(c.get("image") == a.image for c in _containers(new["spec"]["template"]["spec"], a.container))
+            if same and not a.image_pull_policy:
+                raise SystemExit("error: --image-pull-policy (Always|Never|IfNotPresent) must be provided when "
+                                 "--image is the same as existing container image")
             for c in _containers(new["spec"]["template"]["spec"], a.container):
                 c["image"] = a.image
+                if a.image_pull_policy:
+                    c["imagePullPolicy"] = a.image_pull_policy
             new["metadata"] = {"name": a.new_name or "", "namespace": self.ns,
                                "labels": old["metadata"].get("labels") or {}}
             new.pop("status", None)
@@ -529,7 +551,11 @@ class ExtraCommands:
         h_old = hashlib.sha256(json.dumps(old["spec"]["template"], sort_keys=True).encode()).hexdigest()[:10]
         h_new = hashlib.sha256(json.dumps(new["spec"]["template"], sort_keys=True).encode()).hexdigest()[:10]
         if h_old == h_new:
-            raise SystemExit("error: the new controller's template is identical to the old one")
+            if not getattr(a, "image_pull_policy", ""):
+                raise SystemExit("error: the new controller's template is identical to the old one")
+            # the same image and pull policy on purpose (roll the pods): a fresh hash still
+            # separates the new controller's pods from the old ones
+            h_new = hashlib.sha256(f"{h_old}-{time.time()}".encode()).hexdigest()[:10]
         rename = not new["metadata"].get("name")
         if rename:
             new["metadata"]["name"] = f"{a.old}-{h_new[:5]}"
@@ -754,11 +780,12 @@ def add_parsers(add):
     ru.add_argument("old")
     ru.add_argument("new_name", nargs="?", default=None)
     ru.add_argument("--image")
+    ru.add_argument("--image-pull-policy", default="", choices=["", "Always", "Never", "IfNotPresent"])
     ru.add_argument("-c", "--container", default=None)
     ru.add_argument("-f", "--filename", action="append")
     ru.add_argument("--deployment-label-key", default="deployment")
-    ru.add_argument("--timeout", type=float, default=300)
-    ru.add_argument("--update-period", dest="poll_interval", type=float, default=0.1)
+    ru.add_argument("--timeout", type=duration, default=300)
+    ru.add_argument("--update-period", dest="poll_interval", type=duration, default=0.1)
     cv = add("convert")
     cv.add_argument("-f", "--filename", action="append", required=True)
     cv.add_argument("--output-version", default=None)

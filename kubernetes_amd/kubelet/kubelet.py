@@ -685,7 +685,7 @@ class Kubelet:
             st.requests = core.pod_requests(st.pod)
         return st.requests
 
-    def _general_predicates(self, pod):
+    def _general_predicates(self, pod, node_labels=None):
         """GeneralPredicates against this node's capacity and the other active pods."""
         uid = pod["metadata"]["uid"]
         me = self.pods.get(uid)
@@ -706,7 +706,7 @@ class Kubelet:
                 if (used[k] + v if k in used else v) > cap:
                     return f"OutOf{k}", f"Node didn't have enough resource: {k}"
         sel = (pod.get("spec") or {}).get("nodeSelector") or {}
-        labels = {**self._node_object()["metadata"]["labels"]}
+        labels = node_labels if node_labels is not None else self._node_object()["metadata"]["labels"]
         for k, v in sel.items():
             if labels.get(k) != v:
                 return "MatchNodeSelector", "Predicate MatchNodeSelector failed"
@@ -777,6 +777,14 @@ class Kubelet:
         except AdmitError as e:
             return "UnexpectedAdmissionError", f"Pod admission failed: {e}"
         r = self._general_predicates(pod)
+        if r is not None and r[0] == "MatchNodeSelector":
+            # labels set on the Node object through the API (kubectl label node ...) count too:
+            # the reference admits against the node from its lister, not its registration labels
+            try:
+                api_node = await self.client.get("nodes", self.node_name)
+                r = self._general_predicates(pod, (api_node.get("metadata") or {}).get("labels") or {})
+            except (APIStatusError, ConnectionError, OSError):
+                pass
         if r is not None and r[0] in ("OutOfcpu", "OutOfmemory", "OutOfpods"):
             # `pkg/kubelet/preemption`: a critical pod evicts lower-QoS pods instead of failing
             try:
@@ -1350,8 +1358,7 @@ class Kubelet:
             st.ip = ip or status.get("podIP") or st.ip
             if self.hostports is not None:
                 self.hostports.add(st.pod, st.ip)
-        if self.dns is not None:
-            st.net_mounts = self.dns.write_pod_files(os.path.join(self.root_dir, "pods", st.uid), st.pod, st.ip)
+        st.net_mounts = self._pod_net_files(st, st.pod)
         st.net_setup = True
         log.info("adopted running pod %s (sandbox %s, %d containers)", st.pod["metadata"].get("name"), sid,
                  len(st.containers))
@@ -1391,10 +1398,20 @@ class Kubelet:
             await self._report(st)
             asyncio.get_running_loop().call_later(2.0, self._resync, st.uid)
             return False
-        if self.dns is not None:
-            st.net_mounts = self.dns.write_pod_files(os.path.join(self.root_dir, "pods", st.uid), pod, st.ip)
+        st.net_mounts = self._pod_net_files(st, pod)
         st.net_setup = True
         return True
+
+    def _pod_net_files(self, st, pod):
+        """The kubelet-managed /etc/hosts (+ resolv.conf with cluster DNS) of the pod's containers;
+        a runtime that never applies mounts (the hollow stub) gets none written."""
+        pod_dir = os.path.join(self.root_dir, "pods", st.uid)
+        if self.dns is not None:
+            return self.dns.write_pod_files(pod_dir, pod, st.ip)
+        if getattr(self.runtime, "name", "") == "stub":
+            return []
+        from .network import DNSConfigurer
+        return DNSConfigurer(resolv_conf=None).write_pod_files(pod_dir, pod, st.ip, hosts_only=True)
 
     async def _teardown_network(self, st: PodState):
         if not st.net_setup:

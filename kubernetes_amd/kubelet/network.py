@@ -420,8 +420,10 @@ class DNSConfigurer:
                 lines.append(f"{a.get('ip')}\t" + "\t".join(a.get("hostnames") or ()))
         return "\n".join(lines) + "\n"
 
-    def write_pod_files(self, pod_dir, pod, ip):
-        """Write `etc-hosts` and `resolv.conf` under the pod dir; returns the container mounts."""
+    def write_pod_files(self, pod_dir, pod, ip, hosts_only=False):
+        """Write `etc-hosts` and `resolv.conf` under the pod dir; returns the container mounts.
+        hosts_only: no cluster DNS is configured — the kubelet still manages /etc/hosts of every
+        non-hostNetwork pod (`makeHostsMount`), resolv.conf stays the runtime's."""
         os.makedirs(pod_dir, exist_ok=True)
         mounts = []
         spec = pod.get("spec") or {}
@@ -430,6 +432,8 @@ class DNSConfigurer:
             with open(hp, "w") as f:
                 f.write(self.hosts_text(pod, ip))
             mounts.append({"containerPath": "/etc/hosts", "hostPath": hp, "readOnly": False})
+        if hosts_only:
+            return mounts
         rp = os.path.join(pod_dir, "resolv.conf")
         with open(rp, "w") as f:
             f.write(self.resolv_text(pod))

@@ -121,14 +121,20 @@ IMAGES = {
     "kubernetes-amd/hip-vector-add": [os.path.join(BIN_DIR, "hip-vector-add")],
     "kubernetes-amd/xgmi-probe": [os.path.join(BIN_DIR, "xgmi-probe")],
     "kubernetes-amd/pause": [os.path.join(BIN_DIR, "pause")],
-    "busybox": ["/bin/sh"],
     # the e2e image of `test/e2e/common/docker_containers.go`: an ENTRYPOINT and a CMD
     "kubernetes-amd/entrypoint-tester": ["/bin/echo", "entrypoint"],
 }
 # image CMD (default arguments), used only when the container sets neither command nor args
 IMAGE_CMD = {
     "kubernetes-amd/entrypoint-tester": ["default", "arguments"],
+    # the busybox image has no ENTRYPOINT and CMD ["sh"]: `args: [sh, -c, ...]` replaces the CMD
+    "busybox": ["/bin/sh"],
 }
+
+
+def builtin_argv(base):
+    """The executable a built-in image runs (its ENTRYPOINT, else its CMD); None if not built in."""
+    return IMAGES.get(base) or IMAGE_CMD.get(base)
 
 
 def resolve_command(container):
@@ -139,11 +145,13 @@ def resolve_command(container):
     if not cmd:
         img = (container.get("image") or "").split("@")[0]
         base = img.rsplit(":", 1)[0] if ":" in img.split("/")[-1] else img
-        cmd = list(IMAGES.get(base, []))
-        if not cmd:
+        if base not in IMAGES and base not in IMAGE_CMD:
             raise FileNotFoundError(f"image {img!r} has no local entrypoint and no command was given")
+        cmd = list(IMAGES.get(base, []))
         if not args:
             args = list(IMAGE_CMD.get(base, []))
+    if not cmd + args:
+        raise FileNotFoundError("the container has neither a command nor arguments")
     return cmd + args
 
 
@@ -200,7 +208,7 @@ def _check_entrypoint(argv, env):
         raise FileNotFoundError(2, "No such file or directory", exe)
 
 
-async def _spawn_runc(bundle, stdout, timeout=30.0):
+async def _spawn_runc(bundle, stdout, timeout=30.0, stdin=None):
     """Start `kamd-runc run` on a bundle; returns (process, container init pid, isolation report)
     once the container's namespaces, /dev and identity are set up (the ready pipe), or raises
     OSError with kamd-runc's diagnostics if the setup failed."""
@@ -209,6 +217,7 @@ async def _spawn_runc(bundle, stdout, timeout=30.0):
     try:
         proc = await asyncio.create_subprocess_exec(KAMD_RUNC, "run", "--bundle", bundle, "--ready-fd", str(w),
                                                     pass_fds=(w,), stdout=stdout, stderr=asyncio.subprocess.STDOUT,
+                                                    stdin=stdin if stdin is not None else asyncio.subprocess.DEVNULL,
                                                     start_new_session=True)
     finally:
         os.close(w)
@@ -548,6 +557,13 @@ class ProcessRuntime(Runtime):
                                         "kamd.io/rootfs-work": overlay["work"]})
         with open(os.path.join(d, "config.json"), "w") as f:
             json.dump(spec, f, separators=(",", ":"))
+        stdin_fifo = None
+        if container.get("stdin"):
+            # `stdin: true`: the container reads a FIFO that attach writes into; the runtime holds
+            # a write end so the process sees no EOF before an attach (stdinOnce: after the first)
+            stdin_fifo = os.path.join(d, "stdin")
+            if not os.path.exists(stdin_fifo):
+                os.mkfifo(stdin_fifo, 0o600)
         st = ContainerStatus(cid, container["name"], CREATED, image=container.get("image", ""),
                              log_path=os.path.join(d, "log"))
         self.containers[cid] = st
@@ -557,6 +573,7 @@ class ProcessRuntime(Runtime):
                           "attempt": opts.attempt, "run_as_user": opts.run_as_user, "run_as_group": opts.run_as_group,
                           "groups": list(opts.supplemental_groups), "isolated": self.isolated or self.landlocked,
                           "landlock": landlock,
+                          "stdin_fifo": stdin_fifo, "stdin_once": bool(container.get("stdinOnce")), "stdin_w": None,
                           "image_rootfs": overlay is not None,
                           "user": f"{spec['process']['user']['uid']}:{spec['process']['user']['gid']}"}
         return cid
@@ -569,14 +586,21 @@ class ProcessRuntime(Runtime):
         m = self.meta[cid]
         st = self.containers[cid]
         log = open(st.log_path, "ab")
+        rfd = None
         try:
+            if m.get("stdin_fifo"):
+                rfd = os.open(m["stdin_fifo"], os.O_RDONLY | os.O_NONBLOCK)
+                m["stdin_w"] = os.open(m["stdin_fifo"], os.O_WRONLY | os.O_NONBLOCK)
+                os.set_blocking(rfd, True)
             if m.get("isolated"):
                 if not m.get("image_rootfs"):      # (an image's entrypoint lives in its own root)
                     _check_entrypoint(m["argv"], m["env"])
-                proc, m["init_pid"], m["isolation"] = await _spawn_runc(m["dir"], log)
+                proc, m["init_pid"], m["isolation"] = await _spawn_runc(m["dir"], log, stdin=rfd)
             else:
-                proc = await self._start_host_process(m, log)
+                proc = await self._start_host_process(m, log, stdin=rfd)
         except OSError as e:
+            if rfd is not None:
+                os.close(rfd)
             log.close()
             st.state = EXITED
             st.exit_code = 128
@@ -585,13 +609,15 @@ class ProcessRuntime(Runtime):
             st.finished_at = time.time()
             raise
         log.close()
+        if rfd is not None:
+            os.close(rfd)
         m["proc"] = proc
         st.state = RUNNING
         st.started_at = time.time()
         self._container_state(cid)
         spawn(self._wait(cid, proc))
 
-    async def _start_host_process(self, m, log):
+    async def _start_host_process(self, m, log, stdin=None):
         cpus = m.get("cpus")
         pre = None
         argv = m["argv"]
@@ -606,6 +632,7 @@ class ProcessRuntime(Runtime):
                 pre = _child_setup(cpus, m.get("oom_score_adj"), m.get("cgroup"))
         return await asyncio.create_subprocess_exec(*argv, env=m["env"], cwd=m["cwd"], stdout=log,
                                                     stderr=asyncio.subprocess.STDOUT, start_new_session=True,
+                                                    stdin=stdin if stdin is not None else asyncio.subprocess.DEVNULL,
                                                     preexec_fn=pre)
 
     async def pod_states(self):
@@ -625,6 +652,8 @@ class ProcessRuntime(Runtime):
 
     async def _wait(self, cid, proc):
         code = await proc.wait()
+        if cid in self.meta:
+            self._close_stdin(self.meta[cid])
         st = self.containers.get(cid)
         if st is None:
             return
@@ -855,11 +884,44 @@ class ProcessRuntime(Runtime):
                     pass
                 await proc.wait()
 
+    def _close_stdin(self, m):
+        fd, m["stdin_w"] = m.get("stdin_w"), None
+        if fd is not None:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+
+    async def _pump_stdin(self, m, stdin):
+        """Attach's stdin into the container's FIFO; stdinOnce closes it when the stream ends."""
+        try:
+            async for data in stdin:
+                fd = m.get("stdin_w")
+                if fd is None:
+                    break
+                view = memoryview(data)
+                while view:
+                    try:
+                        n = os.write(fd, view)
+                        view = view[n:]
+                    except BlockingIOError:
+                        await asyncio.sleep(0.01)
+                    except OSError:          # the container closed its stdin / exited
+                        return
+        finally:
+            if m.get("stdin_once"):
+                self._close_stdin(m)
+
     async def attach(self, cid, stdin, stdout, stderr, tty, resize):
-        """Follow the container's output file from its current end until the container exits."""
+        """Follow the container's output file from its current end until the container exits;
+        with `stdin: true` the attach's input goes to the container's stdin FIFO."""
         st = self.containers.get(cid)
         if st is None:
             raise OSError(f"container {cid} not found")
+        m = self.meta.get(cid) or {}
+        pump = None
+        if stdin is not None and m.get("stdin_w") is not None:
+            pump = asyncio.ensure_future(self._pump_stdin(m, stdin))
         sink = stdout or stderr
         pos = os.path.getsize(st.log_path) if os.path.exists(st.log_path) else 0
         while True:
@@ -874,6 +936,8 @@ class ProcessRuntime(Runtime):
                     if sink is not None:
                         await sink(data)
             if not running:
+                if pump is not None:
+                    pump.cancel()
                 return 0 if st is None else int(st.exit_code or 0)
             await asyncio.sleep(0.05)
 

@@ -16,7 +16,7 @@ timeout -k 10 240 python bench.py --steps 20 --warmup 5 > "$out/bench.json" 2> "
 echo "bench ok" >> "$out/status.txt"
 if [ -n "$PROFILE" ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/rocprof" -o run -- python3 bench.py --steps 5 --warmup 2 > "$out/rocprof_bench.json" 2> "$out/rocprof.err" || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/rocprof" -o run -- python3 bench.py --steps 5 --warmup 2 > "$out/rocprof_bench.json" 2> "$out/rocprof.err" || exit $?
   echo "rocprof ok" >> "$out/status.txt"
 fi
 exit $rc
