@@ -452,7 +452,22 @@ def launch_ranks(n, argv):
         return p.wait()
 
 
+def raise_fd_limit():
+    """The whole-node control plane holds a socket per watch (hundreds of hollow kubelets per
+    rank, scheduler shards, API workers): lift the soft RLIMIT_NOFILE to the hard limit for this
+    process and every component it starts."""
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    want = hard if hard != resource.RLIM_INFINITY else 1 << 20
+    if soft < want:
+        try:
+            resource.setrlimit(resource.RLIMIT_NOFILE, (want, hard))
+        except (ValueError, OSError):
+            pass
+
+
 def main():
+    raise_fd_limit()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks = GPUs (default: WORLD_SIZE, else 1); without a launcher N > 1 starts "

@@ -27,11 +27,15 @@ class NodeHandle:
             name, kubelet, plugin, dm, runtime, plugins_dir)
 
 
+DNS_ADDR = "127.0.0.153"     # a loopback address of its own: the cluster DNS of LocalCluster(dns=True)
+
+
 class LocalCluster:
     def __init__(self, nodes=1, gpus_per_node=8, runtime="stub", real_gpus=False, hives=1, workdir=None,
                  emit_events=True, payload=None, admission_plugins=None, scheduler_kwargs=None, kubelet_http=False,
                  health_interval=0.0, rocm_mount=None, controllers=None, controller_options=None, kubelet_kwargs=None,
-                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None, links_down=(), image_service=None):
+                 partition="SPX", burn_in=None, dev_root="/dev", isolation=None, links_down=(), image_service=None,
+                 dns=False):
         self.n_nodes = nodes
         self.gpus = gpus_per_node
         self.runtime_kind = runtime
@@ -64,6 +68,10 @@ class LocalCluster:
         self.controller_options = controller_options or {}
         self.kubelet_kwargs = kubelet_kwargs or {}
         self.cm = None
+        # dns=True: the cluster DNS add-on on DNS_ADDR:53 (needs root to bind port 53; without
+        # it no DNS runs) and every kubelet writes pods' resolv.conf for it (--cluster-dns)
+        self.dns = dns
+        self.dns_server = None
 
     async def start(self):
         self.api = APIServer(admission_plugins=self.admission)
@@ -74,6 +82,17 @@ class LocalCluster:
             fixture = None if self.real else amdsmi.fixture_file(self.gpus, hives=self.hives, partition=self.partition,
                                                                  links_down=self.links_down)
             self.smi = amdsmi.SMI(fixture=fixture)
+        if self.dns and os.geteuid() == 0:
+            from .addons.dns import DNSServer
+            from .kubelet.network import DNSConfigurer
+            self.dns_server = DNSServer(Client(self.url))
+            await self.dns_server.start(DNS_ADDR, 53)
+            self.kubelet_kwargs.setdefault("dns", DNSConfigurer(cluster_dns=[DNS_ADDR]))
+            await self.client.create("services", {"metadata": {"name": "kube-dns", "namespace": "kube-system",
+                                                               "labels": {"k8s-app": "kube-dns"}},
+                                                  "spec": {"ports": [{"name": "dns", "port": 53, "protocol": "UDP"},
+                                                                     {"name": "dns-tcp", "port": 53}]}},
+                                     "kube-system")
         self.scheduler = Scheduler(Client(self.url), emit_events=self.emit_events, **self.scheduler_kwargs)
         self._sched_task = asyncio.ensure_future(self.scheduler.run())
         for i in range(self.n_nodes):
@@ -163,6 +182,8 @@ class LocalCluster:
                 await n.runtime.kill_all()
         if self.scheduler:
             await self.scheduler.stop()
+        if self.dns_server is not None:
+            await self.dns_server.stop()
         if self._sched_task:
             self._sched_task.cancel()
         if self.client:

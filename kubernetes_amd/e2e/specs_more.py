@@ -807,3 +807,80 @@ async def service_endpoint_latency(f):
     p50, p99 = lat[len(lat) // 2], lat[min(len(lat) - 1, int(len(lat) * 0.99))]
     # the reference's limits: p50 <= 20 s, p99 <= 50 s
     assert len(lat) == n and p50 <= 20 and p99 <= 50, (p50, p99, len(lat))
+
+
+# ---------------------------------------------------------------------------------------------
+# dns.go: names resolve from inside pods through the cluster DNS their resolv.conf names
+_DNS_PROBE = r'''
+import socket, struct, sys
+conf = open("/etc/resolv.conf").read()
+if "svc.cluster.local" not in conf:
+    print("NO-CLUSTER-RESOLV"); sys.exit(0)
+ns = [l.split()[1] for l in conf.splitlines() if l.startswith("nameserver")][0]
+def srv(name):
+    q = struct.pack("!HHHHHH", 7, 0x0100, 1, 0, 0, 0) + b"".join(
+        bytes([len(p)]) + p.encode() for p in name.split(".")) + b"\0" + struct.pack("!HH", 33, 1)
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM); s.settimeout(5); s.sendto(q, (ns, 53))
+    r = s.recv(4096)
+    return struct.unpack_from("!H", r, 6)[0]
+for name in {names!r}:
+    try:
+        print("OK", name, socket.gethostbyname(name))
+    except OSError as e:
+        print("FAIL", name, e)
+for name in {srv_names!r}:
+    n = srv(name)
+    print("OK" if n else "FAIL", "SRV", name, n)
+'''
+
+
+async def _dns_probe(f, name, names, srv_names=()):
+    try:
+        await f.client.get("services", "kube-dns", "kube-system")
+    except Exception:  # noqa: BLE001
+        raise Skip("no cluster DNS add-on (kube-system/kube-dns) in this cluster")
+    p = {"metadata": {"name": name}, "spec": {"restartPolicy": "Never", "containers": [
+        {"name": "c", "image": BUSYBOX, "command": [PY, "-c", _DNS_PROBE.format(names=list(names),
+                                                                              srv_names=list(srv_names))]}]}}
+    out = await _run_and_log(f, p, 90)
+    if "NO-CLUSTER-RESOLV" in out:
+        raise Skip("pods here share the node's /etc/resolv.conf (no mount namespace): cluster DNS is not theirs")
+    bad = [ln for ln in _lines(out) if not ln.startswith("OK")]
+    assert not bad and out.count("OK") == len(names) + len(srv_names), out
+    return {ln.split()[1]: ln.split()[2] for ln in _lines(out) if ln.startswith("OK ") and " SRV " not in ln}
+
+
+@conformance("DNS should provide DNS for the cluster")
+async def dns_cluster(f):
+    kube = await f.client.get("services", "kubernetes", "default")
+    got = await _dns_probe(f, "dns-test-cluster", ["kubernetes.default", "kubernetes.default.svc",
+                                                   "kubernetes.default.svc.cluster.local"])
+    assert set(got.values()) == {kube["spec"]["clusterIP"]}, got
+
+
+@conformance("DNS should provide DNS for services")
+async def dns_services(f):
+    lbl = {"dns-test": "true"}
+    await f.client.create("pods", dict(_pod("dns-target", "sleep 3600", restart="Always"),
+                                       metadata={"name": "dns-target", "labels": lbl}), f.ns)
+    target = await f.pod_phase("dns-target", ("Running",))
+    reg = await f.client.create("services", {"metadata": {"name": "test-service"}, "spec": {
+        "selector": lbl, "ports": [{"name": "http", "port": 80, "protocol": "TCP"}]}}, f.ns)
+    await f.client.create("services", {"metadata": {"name": "dns-test-service"}, "spec": {
+        "clusterIP": "None", "selector": lbl, "ports": [{"name": "http", "port": 80, "protocol": "TCP"}]}}, f.ns)
+
+    async def endpoints():
+        try:
+            ep = await f.client.get("endpoints", "dns-test-service", f.ns)
+        except Exception:  # noqa: BLE001
+            return None
+        return any(ss.get("addresses") for ss in ep.get("subsets") or ())
+    await f.wait(endpoints, 60, "the headless service's endpoints")
+    ns = f.ns
+    got = await _dns_probe(f, "dns-test-services",
+                           [f"test-service.{ns}.svc.cluster.local", f"dns-test-service.{ns}.svc.cluster.local",
+                            "test-service", f"dns-test-service.{ns}"],
+                           [f"_http._tcp.test-service.{ns}.svc.cluster.local",
+                            f"_http._tcp.dns-test-service.{ns}.svc.cluster.local"])
+    assert got[f"test-service.{ns}.svc.cluster.local"] == reg["spec"]["clusterIP"], got
+    assert got[f"dns-test-service.{ns}.svc.cluster.local"] == target["status"]["podIP"], got
