@@ -274,8 +274,10 @@ def _reference_flags(ap):
     g.add_argument("--watch-cache-sizes", default="",
                    help="per-resource watch windows, resource#size,... (e.g. pods#5000,nodes#1000)")
     g.add_argument("--default-watch-cache-size", type=int, default=None, help="alias of --watch-cache-size")
-    for f in ("--storage-versions", "--storage-version", "--etcd-servers-overrides"):
-        g.add_argument(f, default="")
+    unsupported(g, "--storage-versions", "", str, "each kind is stored in the version of its reference protobuf "
+                "message (JSON for kinds outside the schema)")
+    unsupported(g, "--storage-version", "", str, "see --storage-versions")
+    unsupported(g, "--etcd-servers-overrides", "", str, "one store serves every resource")
     g.add_argument("--etcd-cafile", default="", help="CA of an https etcd endpoint")
     g.add_argument("--etcd-certfile", default="", help="client certificate for an https etcd endpoint")
     g.add_argument("--etcd-keyfile", default="", help="client key for an https etcd endpoint")

@@ -188,8 +188,8 @@ def _reference_flags(ap):
                    help="false: claims only bind to existing PersistentVolumes")
     g.add_argument("--service-cluster-ip-range", default="",
                    help="node CIDR allocation (--allocate-node-cidrs) never hands out blocks overlapping it")
-    g.add_argument("--cidr-allocator-type", default="RangeAllocator", choices=["RangeAllocator", "CloudAllocator"])
-    g.add_argument("--cluster-name", default="kubernetes")
+    unsupported(g, "--cidr-allocator-type", "RangeAllocator", str, "CloudAllocator needs a cloud provider")
+    unsupported(g, "--cluster-name", "kubernetes", str, "it names cloud resources; cloud providers are out of scope")
     for f, d in RESYNC_FLAGS.items():
         g.add_argument(f, default=d[1], help=f"period of the {d[0]} controller's full resync (0 = only on events)")
     deprecated_noop(g, "--node-sync-period", "0s", str, "options.go:158-161")

@@ -318,7 +318,7 @@ def _reference_flags(ap):
     g.add_argument("--node-ip", default="", help="the node's InternalIP (default: --address)")
     g.add_argument("--provider-id", default="")
     g.add_argument("--cloud-provider", default="", help="'' or 'external' (cloud providers are out of scope)")
-    g.add_argument("--cloud-config", default="")
+    unsupported(g, "--cloud-config", "", str, "cloud providers are out of scope")
     g = ap.add_argument_group("admission")
     g.add_argument("--allow-privileged", type=_bool, default=False)
     g.add_argument("--host-network-sources", default="*", help="pod sources (api,file,http) allowed hostNetwork")
@@ -351,7 +351,7 @@ def _reference_flags(ap):
                    help="wire format of API requests (the reference defaults to protobuf; JSON is this "
                         "client's faster path)")
     g.add_argument("--experimental-bootstrap-kubeconfig", default=None, help="deprecated alias of --bootstrap-kubeconfig")
-    g.add_argument("--require-kubeconfig", type=_bool, default=False, help="deprecated no-op, as in the reference")
+    deprecated_noop(g, "--require-kubeconfig", False, _bool, "options.go:298")
     g = ap.add_argument_group("host")
     g.add_argument("--fail-swap-on", type=_bool, default=True)
     g.add_argument("--experimental-fail-swap-on", type=_bool, default=True, help="deprecated alias of --fail-swap-on")

@@ -1,0 +1,13 @@
+#!/bin/bash
+# N=1 control-plane shape sweep on the one-GPU box: the driver's bench command per
+# (API workers, scheduler shards, hollow processes); each run under its own time limit, the
+# sweep stops at the first abnormal exit.
+out=${1:-gpurun_out/sweep}
+mkdir -p "$out"
+for shape in "0 0 0" "4 2 5" "4 2 6" "3 3 5" "4 3 5" "0 0 0"; do
+  set -- $shape
+  tag="w$1-s$2-h$3"
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --apiserver-workers $1 --scheduler-shards $2 \
+      --hollow-procs $3 > "$out/$tag.json" 2> "$out/$tag.err" || exit $?
+  echo "$tag $(python -c "import json,sys; d=json.loads(open('$out/$tag.json').read().strip().splitlines()[-1]); print(d['value'], d['p50_startup_ms'], d['config']['apiserver_workers'], d['config']['scheduler_shards'], d['config']['hollow_procs_per_rank'])")" >> "$out/summary.txt"
+done
