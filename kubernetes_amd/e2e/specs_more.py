@@ -884,3 +884,19 @@ async def dns_services(f):
                             f"_http._tcp.dns-test-service.{ns}.svc.cluster.local"])
     assert got[f"test-service.{ns}.svc.cluster.local"] == reg["spec"]["clusterIP"], got
     assert got[f"dns-test-service.{ns}.svc.cluster.local"] == target["status"]["podIP"], got
+
+
+@conformance("Probing container should be restarted with a docker exec liveness probe with timeout")
+async def probe_exec_timeout(f):
+    """The reference skips this case (its docker exec handler could not time out); exec probes
+    here are killed at timeoutSeconds, and a probe that outlives it counts as a failure."""
+    p = _pod("liveness-exec", "sleep 600", restart="Always")
+    p["spec"]["containers"][0]["livenessProbe"] = {"exec": {"command": ["/bin/sh", "-c", "sleep 10"]},
+                                                   "initialDelaySeconds": 2, "timeoutSeconds": 1,
+                                                   "periodSeconds": 2, "failureThreshold": 1}
+    await f.client.create("pods", p, f.ns)
+    await f.pod_phase("liveness-exec", ("Running",))
+
+    async def restarted():
+        return await _restarts(f, "liveness-exec") >= 1
+    await f.wait(restarted, 60, "a restart after the exec probe timed out")
