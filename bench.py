@@ -225,6 +225,7 @@ class Dist:
         self.torch = None
         self.cuda = False
         self.backend = None
+        self.dist = None
 
     def init(self):
         import torch
@@ -234,10 +235,17 @@ class Dist:
         self.cuda = torch.cuda.is_available() and not os.environ.get("KAMD_BENCH_FORCE_CPU")
         if self.cuda:
             torch.cuda.set_device(self.local_rank)
-        if self.world > 1:
+        # KAMD_BENCH_FORCE_PG=1 (under a launcher): a process group even for one rank, so a
+        # one-GPU box exercises the RCCL init, device binding and barrier path of N > 1
+        if self.world > 1 or (os.environ.get("KAMD_BENCH_FORCE_PG") and "MASTER_ADDR" in os.environ):
             import torch.distributed as dist
             self.backend = "nccl" if self.cuda else "gloo"   # "nccl" is RCCL on ROCm
-            dist.init_process_group(self.backend)
+            if self.cuda:
+                # bind the process group to this rank's GPU: barriers also run on executor
+                # threads, whose current device would otherwise be GPU 0 for every rank
+                dist.init_process_group(self.backend, device_id=torch.device("cuda", self.local_rank))
+            else:
+                dist.init_process_group(self.backend)
             self.dist = dist
 
     def broadcast(self, obj):
@@ -248,8 +256,13 @@ class Dist:
         return lst[0]
 
     def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
+        if self.cuda:
+            self.torch.cuda.set_device(self.local_rank)      # current device is per thread
+        if self.dist is not None:
+            if self.cuda:
+                self.dist.barrier(device_ids=[self.local_rank])
+            else:
+                self.dist.barrier()
         if self.cuda:
             self.torch.cuda.synchronize()
 
