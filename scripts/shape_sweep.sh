@@ -4,6 +4,10 @@
 # sweep stops at the first abnormal exit.
 out=${1:-gpurun_out/sweep}
 mkdir -p "$out"
+# the RCCL process-group path of N > 1 on this one GPU: device binding + barriers from threads
+KAMD_BENCH_FORCE_PG=1 timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+    --master-addr 127.0.0.1 --master-port 29641 bench.py --steps 5 --warmup 2 > "$out/pg1.json" 2> "$out/pg1.err" || exit $?
+echo "pg1 $(tail -1 "$out/pg1.json" | cut -c1-160)" >> "$out/summary.txt"
 for shape in "0 0 0" "4 2 5" "4 2 6" "3 3 5" "4 3 5" "0 0 0"; do
   set -- $shape
   tag="w$1-s$2-h$3"
