@@ -1,4 +1,8 @@
-"""Device plugin server base: serves DevicePlugin + Identity (grpc.aio) on one unix socket.
+"""Device plugin server base: serves DevicePlugin + Identity on one unix socket.
+
+Transport: `utils/grpclite` (gRPC over HTTP/2 on the event loop; a unary call costs a fraction
+of grpc.aio's CPU, which matters because AdmitPod/InitContainer run for every GPU pod) or
+`transport="grpc"` (grpc.aio). Both speak the same wire protocol to any gRPC kubelet.
 
 Parity: the reference's test double `DevicePluginStub` (pkg/kubelet/cm/devicemanager/device_plugin_stub.go:41-276)
 doubles as the production base class here: `update(devices)` pushes a new device list to every
@@ -16,6 +20,7 @@ import os
 
 import grpc
 
+from ..utils import grpclite
 from . import api
 
 log = logging.getLogger("deviceplugin")
@@ -27,13 +32,14 @@ def device(id_, health=api.HEALTHY, attributes=None):
 
 class DevicePluginServer:
     def __init__(self, resource_name: str, socket_path: str, devices=None, init_timeout=10,
-                 supported_versions=(api.VERSION,), labels=None):
+                 supported_versions=(api.VERSION,), labels=None, transport="lite"):
         self.resource_name = resource_name
         self.socket_path = socket_path
         self.devices = list(devices or [])
         self.init_timeout = init_timeout
         self.supported_versions = list(supported_versions)
         self.labels = dict(labels or {})
+        self.transport = transport
         self.registration_status = None      # last PluginRegistrationStatus from the kubelet
         self.registered = asyncio.Event()
         self._streams: set[asyncio.Queue] = set()
@@ -108,11 +114,16 @@ class DevicePluginServer:
         os.makedirs(os.path.dirname(self.socket_path), exist_ok=True)
         if os.path.exists(self.socket_path):
             os.unlink(self.socket_path)
-        self._server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
-        self._server.add_generic_rpc_handlers((
-            api.generic_handler(api.DP_SERVICE, api.DP_METHODS, self),
-            api.generic_handler(api.ID_SERVICE, api.ID_METHODS, self),
-        ))
+        if self.transport == "grpc":
+            self._server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
+            self._server.add_generic_rpc_handlers((
+                api.generic_handler(api.DP_SERVICE, api.DP_METHODS, self),
+                api.generic_handler(api.ID_SERVICE, api.ID_METHODS, self),
+            ))
+        else:
+            self._server = grpclite.Server()
+            self._server.add_service(api.DP_SERVICE, api.DP_METHODS, self)
+            self._server.add_service(api.ID_SERVICE, api.ID_METHODS, self)
         self._server.add_insecure_port("unix://" + self.socket_path)
         await self._server.start()
         return self

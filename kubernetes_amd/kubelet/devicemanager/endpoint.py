@@ -18,10 +18,9 @@ from __future__ import annotations
 import asyncio
 import logging
 
-import grpc
-
 from ...api.core import is_extended_resource_name
 from ...deviceplugin import api
+from ...utils import grpclite
 from .stores import AlwaysEmptyDeviceStore, DeviceStore
 
 log = logging.getLogger("devicemanager")
@@ -39,10 +38,12 @@ class Validator:
         self.domain = domain
 
     async def connect(self, socket_path: str, timeout=1.0):
-        ch = grpc.aio.insecure_channel("unix://" + socket_path)
+        # grpclite: gRPC over HTTP/2 on the kubelet's loop (utils/grpclite.py); any gRPC plugin
+        # server answers it
+        ch = grpclite.Channel("unix://" + socket_path)
         try:
             await asyncio.wait_for(ch.channel_ready(), timeout)
-        except asyncio.TimeoutError:
+        except (asyncio.TimeoutError, grpclite.RpcError):
             await ch.close()
             raise RegistrationError(f"failed to dial device plugin {socket_path}")
         return ch
@@ -64,7 +65,7 @@ class Validator:
         ident = api.identity_stub(ch)
         try:
             await ident.PluginRegistrationStatus(api.PR["RegistrationStatus"](success=err is None, error=str(err or "")), timeout=1.0)
-        except grpc.aio.AioRpcError as e:
+        except grpclite.RpcError as e:
             log.warning("could not notify plugin of registration status: %s", e.code())
 
 
@@ -94,7 +95,7 @@ class Endpoint:
                 added, updated, deleted = self.store.update(resp.devices)
                 if added or updated or deleted:
                     self.store.fire(self.resource_name, added, updated, deleted)
-        except grpc.aio.AioRpcError as e:
+        except grpclite.RpcError as e:
             if not self._stopped:
                 log.warning("ListAndWatch %s ended: %s", self.resource_name, e.code())
         except asyncio.CancelledError:
@@ -136,7 +137,7 @@ class EndpointHandler:
         ch = await v.connect(socket_path, 1.0)
         try:
             name = await v.validate_endpoint(ch)
-        except (RegistrationError, grpc.aio.AioRpcError) as e:
+        except (RegistrationError, grpclite.RpcError) as e:
             await v.notify(ch, e)
             await ch.close()
             raise RegistrationError(str(e)) from e
@@ -144,7 +145,7 @@ class EndpointHandler:
         e = Endpoint(ch, name, socket_path)
         try:
             await e.init()
-        except grpc.aio.AioRpcError as err:
+        except grpclite.RpcError as err:
             await ch.close()
             raise RegistrationError(f"GetPluginInfo failed: {err.code()}") from err
         old = self.endpoints.get(name)
