@@ -53,6 +53,10 @@ class EventRecorder:
             del self.emitted[:500]
         if not self.enabled:
             return
+        if self.q.full():
+            # the bounded queue drops new events (record.maxQueuedEvents); do not build them
+            self.dropped += 1
+            return
         md = obj.get("metadata") or {}
         ns = md.get("namespace") or "default"
         key = (md.get("uid"), field_path, reason, message)

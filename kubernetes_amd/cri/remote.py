@@ -23,6 +23,7 @@ import time
 import grpc
 
 from ..deviceplugin.api import _Stub
+from ..utils import grpclite
 from ..kubelet.sysctl import SysctlAdmitHandler
 from ..kubelet.runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, ContainerStatus, Runtime, RuntimeError_
 from . import api as A
@@ -31,6 +32,9 @@ log = logging.getLogger("cri.remote")
 
 _STATES = {A.CONTAINER_CREATED: CREATED, A.CONTAINER_RUNNING: RUNNING, A.CONTAINER_EXITED: EXITED,
            A.CONTAINER_UNKNOWN: UNKNOWN}
+
+
+_RPC_ERRORS = (grpc.aio.AioRpcError, grpclite.RpcError)
 
 
 def _target(endpoint):
@@ -44,9 +48,12 @@ def _target(endpoint):
 class RemoteRuntime(Runtime):
     name = "remote"
 
-    def __init__(self, endpoint: str, timeout: float = 10.0, relist_period: float = 1.0):
+    def __init__(self, endpoint: str, timeout: float = 10.0, relist_period: float = 1.0, transport: str = "lite"):
         super().__init__()
         self.endpoint = endpoint
+        # "lite": gRPC over HTTP/2 on the kubelet's loop (utils/grpclite.py), the kubelet's
+        # 1-s relist and every pod's sandbox/container calls; "grpc": grpc.aio
+        self.transport = transport
         self.timeout = timeout
         self.relist_period = relist_period
         self.channel = None
@@ -64,7 +71,8 @@ class RemoteRuntime(Runtime):
 
     async def connect(self):
         if self.channel is None:
-            self.channel = grpc.aio.insecure_channel(_target(self.endpoint))
+            self.channel = (grpclite.Channel(_target(self.endpoint)) if self.transport == "lite"
+                            else grpc.aio.insecure_channel(_target(self.endpoint)))
             self.rs = _Stub(self.channel, A.RUNTIME_SERVICE, A.RUNTIME_METHODS)
             self.images = RemoteImageService(_Stub(self.channel, A.IMAGE_SERVICE, A.IMAGE_METHODS), self.timeout)
             v = await self.rs.Version(A.MSG["VersionRequest"](version="0.1.0"), timeout=self.timeout)
@@ -94,7 +102,7 @@ class RemoteRuntime(Runtime):
             await self.connect()
         try:
             return await getattr(self.rs, name)(req, timeout=self.timeout)
-        except grpc.aio.AioRpcError as e:
+        except _RPC_ERRORS as e:
             raise RuntimeError_(f"{name}: {e.details() or e.code().name}") from None
 
     # ---------------------------------------------------------------- Runtime interface
@@ -201,7 +209,7 @@ class RemoteRuntime(Runtime):
     async def _refresh(self, cid):
         try:
             r = await self.rs.ContainerStatus(A.MSG["ContainerStatusRequest"](container_id=cid), timeout=self.timeout)
-        except grpc.aio.AioRpcError:
+        except _RPC_ERRORS:
             return None
         return self._apply(r.status)
 
@@ -326,7 +334,7 @@ class RemoteImageService:
     async def _call(self, name, req):
         try:
             return await getattr(self.stub, name)(req, timeout=self.timeout)
-        except grpc.aio.AioRpcError as e:
+        except _RPC_ERRORS as e:
             raise RuntimeError_(f"{name}: {e.details() or e.code().name}") from None
 
     async def pull_image(self, image, auth=None):

@@ -31,6 +31,7 @@ import time
 import grpc
 
 from ..deviceplugin.api import generic_handler
+from ..utils import grpclite
 from ..kubelet.runtime.base import EXITED, RUNNING, RunContainerOptions, RuntimeError_
 from ..utils.websocket import is_websocket_request
 from . import api as A
@@ -299,9 +300,10 @@ def _pairs(d):
 class CRIServer:
     """Serves RuntimeService + ImageService for `runtime` on `socket_path`."""
 
-    def __init__(self, runtime, socket_path, image_resolver=None, checkpoint_dir=None):
+    def __init__(self, runtime, socket_path, image_resolver=None, checkpoint_dir=None, transport="lite"):
         self.rt = runtime
         self.path = socket_path
+        self.transport = transport
         self.checkpoints = None
         if checkpoint_dir:
             from ..utils.checkpoint import CheckpointManager
@@ -341,9 +343,14 @@ class CRIServer:
         if hasattr(self.rt, "start"):
             await self.rt.start()          # watch the containers re-adopted after a restart
         await self.streaming.start()
-        self.server = grpc.aio.server()
-        self.server.add_generic_rpc_handlers((generic_handler(A.RUNTIME_SERVICE, A.RUNTIME_METHODS, self),
-                                              generic_handler(A.IMAGE_SERVICE, A.IMAGE_METHODS, self)))
+        if self.transport == "grpc":
+            self.server = grpc.aio.server()
+            self.server.add_generic_rpc_handlers((generic_handler(A.RUNTIME_SERVICE, A.RUNTIME_METHODS, self),
+                                                  generic_handler(A.IMAGE_SERVICE, A.IMAGE_METHODS, self)))
+        else:       # utils/grpclite.py: same wire protocol, served on the event loop
+            self.server = grpclite.Server()
+            self.server.add_service(A.RUNTIME_SERVICE, A.RUNTIME_METHODS, self)
+            self.server.add_service(A.IMAGE_SERVICE, A.IMAGE_METHODS, self)
         self.server.add_insecure_port("unix://" + self.path)
         await self.server.start()
         return self

@@ -19,8 +19,9 @@ Wire compatibility (tested against grpc-core peers in both directions, tests/tes
     `grpc-status` / percent-encoded `grpc-message` trailers, trailers-only responses,
     HTTP status -> gRPC code mapping.
 
-The device-plugin services (deviceplugin/api.py) are served and called through it; CRI, CSI,
-KMS and the etcd v3 paths keep grpc.aio (not per pod, or third-party wire features).
+The device-plugin services (deviceplugin/api.py) and the CRI runtime/image services are served
+and called through it by default (`transport="grpc"` selects grpc.aio); CSI, KMS and the etcd v3
+paths keep grpc.aio (not per pod, bidirectional streams, TLS).
 """
 from __future__ import annotations
 
@@ -71,8 +72,11 @@ class RpcError(Exception):
     """A failed call (grpc.aio.AioRpcError's `code()` / `details()` interface)."""
 
     def __init__(self, code, details=""):
-        super().__init__(f"{StatusCode(code).name}: {details}")
-        self._code = StatusCode(code)
+        v = getattr(code, "value", code)
+        if isinstance(v, tuple):            # a grpc.StatusCode (handlers written for grpc.aio)
+            v = v[0]
+        super().__init__(f"{StatusCode(v).name}: {details}")
+        self._code = StatusCode(v)
         self._details = details
 
     def code(self):

@@ -34,11 +34,13 @@ def test_messages_roundtrip_field_numbers():
     assert len(A.RUNTIME_METHODS) == 21 and len(A.IMAGE_METHODS) == 5
 
 
-def test_remote_runtime_over_stub(run, tmp_path):
+@pytest.mark.parametrize("server_t,client_t", [("lite", "lite"), ("grpc", "lite"), ("lite", "grpc")])
+def test_remote_runtime_over_stub(run, tmp_path, server_t, client_t):
+    # CRI over utils/grpclite by default; each side also interoperates with a grpc-core peer
     async def main():
         sock = str(tmp_path / "cri.sock")
-        srv = await CRIServer(StubRuntime(), sock).start()
-        rt = await RemoteRuntime(sock, relist_period=0.05).connect()
+        srv = await CRIServer(StubRuntime(), sock, transport=server_t).start()
+        rt = await RemoteRuntime(sock, relist_period=0.05, transport=client_t).connect()
         exits = []
         rt.on_exit(lambda uid, cid: exits.append((uid, cid)))
         try:
