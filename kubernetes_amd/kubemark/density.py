@@ -141,7 +141,7 @@ class DensityRunner:
         else:
             await asyncio.gather(*(create(n) for n in names))
         t_created = time.monotonic()
-        await self._wait(lambda: all(n in self.running for n in names), timeout, names, "running")
+        await self._wait(_all_in(names, self.running), timeout, names, "running")
         t_running = time.monotonic()
 
         async def delete(n):
@@ -159,7 +159,7 @@ class DensityRunner:
         else:
             await asyncio.gather(*(delete(n) for n in names))
         t_deleted = time.monotonic()
-        await self._wait(lambda: all(n in self.gone for n in names), timeout, names, "gone")
+        await self._wait(_all_in(names, self.gone), timeout, names, "gone")
         t_gone = time.monotonic()
         lat = [self.running[n] - self.created[n] for n in names]
         sched = sorted(self.scheduled[n] for n in names if n in self.scheduled)
@@ -194,3 +194,14 @@ def interval_rates(times, bucket=1.0, start=0.0, end=None):
         if 0 <= k < n:
             counts[k] += 1
     return sum(counts) / (n * bucket), min(counts) / bucket
+
+
+def _all_in(names, seen):
+    """A predicate "every name is in `seen`" that re-checks only the names still missing (it is
+    evaluated after every watch batch)."""
+    pending = list(names)
+
+    def pred():
+        pending[:] = [n for n in pending if n not in seen]
+        return not pending
+    return pred
