@@ -8,7 +8,9 @@ mkdir -p "$out"
 KAMD_BENCH_FORCE_PG=1 timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
     --master-addr 127.0.0.1 --master-port 29641 bench.py --steps 5 --warmup 2 > "$out/pg1.json" 2> "$out/pg1.err" || exit $?
 echo "pg1 $(tail -1 "$out/pg1.json" | cut -c1-160)" >> "$out/summary.txt"
-for shape in "0 0 0" "4 2 5" "4 2 6" "3 3 5" "4 3 5" "0 0 0"; do
+# CPU per device-plugin RPC on this box (grpc.aio vs grpclite; no GPU use)
+timeout -k 10 120 python -m kubernetes_amd.kubemark.rpc_bench > "$out/rpc_bench.jsonl" 2> "$out/rpc_bench.err" || exit $?
+for shape in "0 0 0" "4 2 4" "4 3 4" "5 3 4" "3 2 4" "4 2 6" "0 0 0"; do
   set -- $shape
   tag="w$1-s$2-h$3"
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 --apiserver-workers $1 --scheduler-shards $2 \
