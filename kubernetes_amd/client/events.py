@@ -108,9 +108,9 @@ class EventRecorder:
                 if upd:
                     await self.client.patch("events", ev["metadata"]["name"],
                                             {"count": ev["count"], "lastTimestamp": ev["lastTimestamp"]},
-                                            ev["metadata"]["namespace"])
+                                            ev["metadata"]["namespace"], decode=False)
                 else:
-                    await self.client.create("events", ev, ev["metadata"]["namespace"])
+                    await self.client.create("events", ev, ev["metadata"]["namespace"], decode=False)
                 self.sent += 1
             except Exception as e:  # events are best effort
                 log.debug("event write failed: %s", e)

@@ -180,7 +180,7 @@ class FakeClient:
         lst = await self.list(resource, namespace, label_selector, field_selector)
         return lst["items"], lst["metadata"]["resourceVersion"]
 
-    async def create(self, resource, obj, namespace=None):
+    async def create(self, resource, obj, namespace=None, decode=True):
         obj = copy.deepcopy(obj)
         md = obj.setdefault("metadata", {})
         if namespace and m.BY_PLURAL.get(resource, m.BY_PLURAL["pods"]).namespaced:
@@ -215,7 +215,7 @@ class FakeClient:
     async def update_status(self, resource, obj, namespace=None):
         return await self.update(resource, obj, namespace, "status")
 
-    async def patch(self, resource, name, patch, namespace=None, patch_type="merge", subresource=""):
+    async def patch(self, resource, name, patch, namespace=None, patch_type="merge", subresource="", decode=True):
         h, r = self._react(Action("patch", resource, namespace, name, subresource, patch))
         if h:
             return r
@@ -223,7 +223,8 @@ class FakeClient:
         new = apply_patch(_PATCH_TYPES.get(patch_type, patch_type), cur, patch)
         return self._store(resource, new, "MODIFIED")
 
-    async def delete(self, resource, name, namespace=None, grace_period=None, propagation=None, uid=None):
+    async def delete(self, resource, name, namespace=None, grace_period=None, propagation=None, uid=None,
+                     decode=True):
         h, r = self._react(Action("delete", resource, namespace, name))
         if h:
             return r
@@ -238,7 +239,8 @@ class FakeClient:
         for o in (await self.list(resource, namespace, label_selector))["items"]:
             await self.delete(resource, o["metadata"]["name"], o["metadata"].get("namespace"))
 
-    async def bind(self, namespace, name, node, extended_resource_binding=None, annotations=None, uid=None):
+    async def bind(self, namespace, name, node, extended_resource_binding=None, annotations=None, uid=None,
+                   decode=True):
         h, r = self._react(Action("create", "pods", namespace, name, "binding",
                                   {"target": {"name": node}, "extendedResources": extended_resource_binding}))
         if h:

@@ -104,7 +104,9 @@ class Client:
     async def close(self):
         await self.http.close()
 
-    async def _do(self, method, path, body=None, content_type="application/json", ok=(200, 201)):
+    async def _do(self, method, path, body=None, content_type="application/json", ok=(200, 201), decode=True):
+        """`decode=False`: the caller ignores the response object (an event write, a final
+        delete, a binding): skip parsing it; errors are still decoded."""
         if self.limiter:
             await self.limiter.wait()
         if body is None or isinstance(body, (bytes, bytearray)):
@@ -124,7 +126,7 @@ class Client:
             except Exception:
                 status = {"message": resp.decode(errors="replace")}
             raise APIStatusError(st, status)
-        return self._decode(resp) if resp else None
+        return self._decode(resp) if resp and decode else None
 
     async def raw(self, method, path, body=None, content_type="application/json"):
         return await self.http.request(method, path, body, content_type)
@@ -163,9 +165,9 @@ class Client:
             if not cont:
                 return out, rv
 
-    async def create(self, resource, obj, namespace=None):
+    async def create(self, resource, obj, namespace=None, decode=True):
         ns = namespace or (obj.get("metadata") or {}).get("namespace")
-        return await self._do("POST", resource_path(resource, ns), obj)
+        return await self._do("POST", resource_path(resource, ns), obj, decode=decode)
 
     async def update(self, resource, obj, namespace=None, subresource=""):
         md = obj.get("metadata") or {}
@@ -175,12 +177,13 @@ class Client:
     async def update_status(self, resource, obj, namespace=None):
         return await self.update(resource, obj, namespace, "status")
 
-    async def patch(self, resource, name, patch, namespace=None, patch_type="merge", subresource=""):
+    async def patch(self, resource, name, patch, namespace=None, patch_type="merge", subresource="", decode=True):
         ct = {"merge": "application/merge-patch+json", "strategic": "application/strategic-merge-patch+json",
               "json": "application/json-patch+json"}[patch_type]
-        return await self._do("PATCH", resource_path(resource, namespace, name, subresource), patch, ct)
+        return await self._do("PATCH", resource_path(resource, namespace, name, subresource), patch, ct, decode=decode)
 
-    async def delete(self, resource, name, namespace=None, grace_period=None, propagation=None, uid=None):
+    async def delete(self, resource, name, namespace=None, grace_period=None, propagation=None, uid=None,
+                     decode=True):
         opts = {"kind": "DeleteOptions", "apiVersion": "v1"}
         if grace_period is not None:
             opts["gracePeriodSeconds"] = grace_period
@@ -188,7 +191,7 @@ class Client:
             opts["propagationPolicy"] = propagation
         if uid:
             opts["preconditions"] = {"uid": uid}
-        return await self._do("DELETE", resource_path(resource, namespace, name), opts)
+        return await self._do("DELETE", resource_path(resource, namespace, name), opts, decode=decode)
 
     async def delete_collection(self, resource, namespace=None, label_selector=None):
         path = resource_path(resource, namespace)
@@ -196,7 +199,8 @@ class Client:
             path += "?" + urlencode({"labelSelector": label_selector})
         return await self._do("DELETE", path)
 
-    async def bind(self, namespace, name, node, extended_resource_binding=None, annotations=None, uid=None):
+    async def bind(self, namespace, name, node, extended_resource_binding=None, annotations=None, uid=None,
+                   decode=True):
         target = {"kind": "Node", "apiVersion": "v1", "name": node}
         if extended_resource_binding:
             target["extendedResourceBinding"] = extended_resource_binding
@@ -206,7 +210,7 @@ class Client:
             body["metadata"]["annotations"] = annotations
         if uid:
             body["metadata"]["uid"] = uid
-        return await self._do("POST", resource_path("pods", namespace, name, "binding"), body)
+        return await self._do("POST", resource_path("pods", namespace, name, "binding"), body, decode=decode)
 
     async def evict(self, namespace, name, grace_period=None):
         body = {"kind": "Eviction", "apiVersion": "policy/v1beta1", "metadata": {"name": name, "namespace": namespace}}

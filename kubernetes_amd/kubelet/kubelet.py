@@ -1482,7 +1482,8 @@ class Kubelet:
             # deletes once the pod `canBeDeleted`)
             return
         try:
-            await self.client.delete("pods", md["name"], md.get("namespace"), grace_period=0, uid=md["uid"])
+            await self.client.delete("pods", md["name"], md.get("namespace"), grace_period=0, uid=md["uid"],
+                                     decode=False)
             st.final_deleted = True
         except APIStatusError as e:
             if is_not_found(e) or is_conflict(e):

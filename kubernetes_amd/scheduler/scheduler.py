@@ -417,7 +417,7 @@ class Scheduler:
             try:
                 if vplan:
                     await self._bind_volumes(vplan, host)
-                await self.client.bind(md.get("namespace", "default"), md["name"], host, erb or None)
+                await self.client.bind(md.get("namespace", "default"), md["name"], host, erb or None, decode=False)
             except (APIStatusError, ConnectionError, OSError, asyncio.TimeoutError) as e:
                 self.cache.forget_pod(assumed)
                 for kind, _pvc, pv in vplan or ():
