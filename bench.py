@@ -95,12 +95,13 @@ def cpu_budget():
     return n
 
 
-# Per-pod host CPU of each control-plane component at the N=1 headline rate, measured by the
-# driver's own run (BENCH_r03 `cpu_ms_per_pod`: API server 0.98 ms, scheduler 0.56 ms, hollow
-# kubelets 1.64 ms per pod at 2727 pods/s). A whole node sizes each component for the load of
-# `world` ranks at that rate, at most ~70 % busy, instead of a fixed-size control plane.
-N1_RATE_PODS_PER_S = 2800.0
-CPU_MS_PER_POD = {"apiserver": 0.98, "scheduler": 0.56, "hollow": 1.64}
+# Per-pod host CPU of each control-plane component at the N=1 headline rate, measured on the
+# MI355X box (profiles/r4_gpu/bench_r4g.json `cpu_ms_per_pod`: API server 0.80 ms, scheduler
+# 0.46 ms, hollow kubelets 0.69 ms per pod at 3416 pods/s; the hollow kubelets were 1.55 ms
+# before the device-plugin RPCs moved to utils/grpclite). A whole node sizes each component for
+# the load of `world` ranks at that rate, at most ~70 % busy, instead of a fixed-size control plane.
+N1_RATE_PODS_PER_S = 3400.0
+CPU_MS_PER_POD = {"apiserver": 0.80, "scheduler": 0.46, "hollow": 0.69}
 TARGET_UTIL = 0.7
 
 
@@ -117,8 +118,8 @@ def control_plane_shape(world, workers=0, shards=0):
     (profiles/r2_partitioned: n1_shapes, scale_r2d; profiles/r2_density_clients/worker_sweep):
     N=1 w=3 s=2 (2594-2611 pods/s; w=2 2363-2389, w=4 2380-2462), N=4 w=4 s=4 (3184 vs w=4 s=2
     2727). A whole 8-GPU node (>= 64 CPUs) is sized from the per-pod CPU of each component
-    (`demand`): at N=8 that is 32 API workers and 18 scheduler shards — ceilings of ~32.6 k and
-    ~32 k pods/s against the 22.4 k that linear weak scaling needs (the round-3 caps of 16 / 8
+    (`demand`): at N=8 that is 32 API workers and 18 scheduler shards — ceilings of ~40 k and
+    ~39 k pods/s against the 27.2 k that linear weak scaling needs (the round-3 caps of 16 / 8
     capped it at ~14 k) — scaled down together with the hollow-node processes when the CPU
     budget is smaller (`cpus - ranks - store threads`)."""
     cpus = cpu_budget()
@@ -157,7 +158,7 @@ def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
     spare = cpus - workers - shards - 1
     if cpus >= 64:
         # a whole node: the hollow kubelets' share of the per-pod demand model, per rank
-        # (~7 processes per rank at 1.64 ms per pod), within the CPUs left
+        # (4 processes per rank at 0.69 ms per pod), within the CPUs left
         per_rank = -(-demand("hollow", world) // world)
         return max(1, min(nodes_per_rank, per_rank, max(2, (spare - world) // max(1, world))))
     # hollow kubelets are mostly waiting on the control plane: mild oversubscription pays

@@ -78,7 +78,7 @@ def test_bench_gpus_mismatch_fails():
 def test_bench_eight_ranks_whole_node_shape():
     """The N=8 path the driver runs on a whole MI355X node, rehearsed with gloo on CPU: 8 ranks
     under torch.distributed.run with the >= 64-CPU control-plane shape (KAMD_BENCH_CPUS=64:
-    the demand model scaled to that budget — 16 API server workers, 9 scheduler shards) and
+    the demand model scaled to that budget — 22 API server workers, 12 scheduler shards) and
     small per-rank work."""
     env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1", KAMD_BENCH_CPUS="64")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
@@ -90,7 +90,7 @@ def test_bench_eight_ranks_whole_node_shape():
     _check(d, 8, 2, 1)
     assert d["config"]["parallelism"] == "ranks8" and d["config"]["hollow_nodes"] == 8
     assert d["config"]["global_batch"] == 64
-    assert d["config"]["apiserver_workers"] == 16 and d["config"]["scheduler_shards"] == 9
+    assert d["config"]["apiserver_workers"] == 22 and d["config"]["scheduler_shards"] == 12
 
 
 def test_payload_server_batches_starts(run, tmp_path):
@@ -164,7 +164,7 @@ def test_store_bench_small():
 def test_hollow_procs_per_rank(monkeypatch):
     import bench
     monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
-    assert bench.hollow_procs_for(8, 100, 32, 18) == 7       # a whole node: the demand model
+    assert bench.hollow_procs_for(8, 100, 32, 18) == 4       # a whole node: the demand model
     assert bench.hollow_procs_for(8, 4, 32, 18) == 4         # never more than the rank's nodes
     monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
     assert bench.hollow_procs_for(8, 100, 16, 9) == 3        # bounded by the spare CPUs
