@@ -226,3 +226,45 @@ def test_lite_client_errors_on_missing_server_and_server_stop():
             pass
         await ch.close()
     asyncio.run(main())
+
+
+def test_lite_server_survives_malformed_peers():
+    """A bad preface, a garbage frame, an HPACK block with an invalid index or a bad Huffman
+    string ends only that connection (GOAWAY PROTOCOL_ERROR); the server keeps serving."""
+    async def main():
+        d = tempfile.mkdtemp()
+        sock = os.path.join(d, "p.sock")
+        plugin = await _Plugin("amd.com/gpu", sock, [device("g0")]).start()
+        try:
+            bad = [b"GET / HTTP/1.1\r\nHost: x\r\n\r\n" + b"\0" * 32,
+                   gl.PREFACE + gl._HDR.pack((4 << 8) | gl.HEADERS, gl.F_END_HEADERS, 2) + b"\xff\xff\xff\xff",
+                   gl.PREFACE + gl._HDR.pack((1 << 8) | gl.HEADERS, gl.F_END_HEADERS | gl.F_END_STREAM, 1) + b"\xfe",
+                   gl.PREFACE + gl._HDR.pack((3 << 8) | gl.HEADERS, gl.F_END_HEADERS, 1) + b"\x00\x81\x00",
+                   gl.PREFACE + gl._HDR.pack((6 << 8) | gl.WINDOW_UPDATE, 0, 0) + b"\x00" * 6]
+            for payload in bad:
+                r, w = await asyncio.open_unix_connection(sock)
+                w.write(payload)
+                await w.drain()
+                data = b""
+                while True:                       # the server closes the connection
+                    chunk = await asyncio.wait_for(r.read(1 << 16), 5)
+                    if not chunk:
+                        break
+                    data += chunk
+                w.close()
+                if payload.startswith(gl.PREFACE):
+                    # SETTINGS, then GOAWAY(PROTOCOL_ERROR) before the close
+                    frames, pos = [], 0
+                    while pos + 9 <= len(data):
+                        lt, _, _ = gl._HDR.unpack_from(data, pos)
+                        frames.append((lt & 0xFF, data[pos + 9:pos + 9 + (lt >> 8)]))
+                        pos += 9 + (lt >> 8)
+                    goaway = [p for t, p in frames if t == gl.GOAWAY]
+                    assert goaway and int.from_bytes(goaway[0][4:8], "big") == gl.E_PROTOCOL, frames
+            ch = gl.Channel("unix://" + sock)
+            info = await api.device_plugin_stub(ch).GetPluginInfo(api.DP["GetPluginInfoRequest"](), timeout=2)
+            assert info.init_timeout == 10
+            await ch.close()
+        finally:
+            await plugin.stop()
+    asyncio.run(main())
