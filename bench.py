@@ -249,16 +249,23 @@ class Dist:
                 dist.init_process_group(self.backend)
             self.dist = dist
 
+    def _bind_thread(self):
+        # the current GPU is per thread: object collectives and barriers also run on executor
+        # threads, where it would be GPU 0 for every rank (a rank's RCCL communicator is on its
+        # own GPU)
+        if self.cuda:
+            self.torch.cuda.set_device(self.local_rank)
+
     def broadcast(self, obj):
         if self.world == 1:
             return obj
+        self._bind_thread()
         lst = [obj]
         self.dist.broadcast_object_list(lst, src=0)
         return lst[0]
 
     def barrier(self):
-        if self.cuda:
-            self.torch.cuda.set_device(self.local_rank)      # current device is per thread
+        self._bind_thread()
         if self.dist is not None:
             if self.cuda:
                 self.dist.barrier(device_ids=[self.local_rank])
@@ -270,6 +277,7 @@ class Dist:
     def allgather(self, obj):
         if self.world == 1:
             return [obj]
+        self._bind_thread()
         out = [None] * self.world
         self.dist.all_gather_object(out, obj)
         return out
