@@ -257,7 +257,7 @@ class Dist:
             self.torch.cuda.set_device(self.local_rank)
 
     def broadcast(self, obj):
-        if self.world == 1:
+        if self.dist is None:
             return obj
         self._bind_thread()
         lst = [obj]
@@ -275,7 +275,7 @@ class Dist:
             self.torch.cuda.synchronize()
 
     def allgather(self, obj):
-        if self.world == 1:
+        if self.dist is None:       # one rank without a process group (KAMD_BENCH_FORCE_PG makes one)
             return [obj]
         self._bind_thread()
         out = [None] * self.world
