@@ -33,6 +33,18 @@ async def run(url, a, proc, start_at):
     async def worker(ci, c):
         for i in range(n_per):
             name = f"p{proc}-{ci}-{i}"
+            if a.events_only:
+                # the kubelet/scheduler event mix: 5 events per pod (Scheduled, Pulled, Created,
+                # Started, Killing), each a POST of a new Event
+                for reason in ("Scheduled", "Pulled", "Created", "Started", "Killing"):
+                    await c.create("events", {
+                        "metadata": {"name": f"{name}.{reason.lower()}", "namespace": "default"},
+                        "involvedObject": {"kind": "Pod", "namespace": "default", "name": name,
+                                           "uid": "u-" + name, "apiVersion": "v1", "resourceVersion": "1"},
+                        "reason": reason, "message": f"{reason} pod {name}", "type": "Normal",
+                        "source": {"component": "kubelet", "host": "n0"}, "count": 1,
+                        "firstTimestamp": "2026-01-01T00:00:00Z", "lastTimestamp": "2026-01-01T00:00:00Z"})
+                continue
             p = await c.create("pods", {"metadata": {"name": name, "namespace": "default"},
                                         "spec": {"containers": [{"name": "c", "image": "x",
                                                                  "resources": {"limits": {"amd.com/gpu": "1"}}}]}})
@@ -59,6 +71,20 @@ async def _setup(url):
     await c.close()
 
 
+def _server_cpu(pid):
+    """User+system CPU seconds of the API server and every process under it (workers, store)."""
+    import psutil
+    root = psutil.Process(pid)
+    tot = 0.0
+    for q in [root] + root.children(recursive=True):
+        try:
+            t = q.cpu_times()
+            tot += t.user + t.system
+        except psutil.NoSuchProcess:
+            pass
+    return tot
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pods", type=int, default=4000)
@@ -66,6 +92,7 @@ def main():
     ap.add_argument("--client-procs", type=int, default=1)
     ap.add_argument("--watchers", type=int, default=3)
     ap.add_argument("--extra", default="")
+    ap.add_argument("--events-only", action="store_true", help="5 Event creates per pod instead of the pod lifecycle")
     a = ap.parse_args()
     d = tempfile.mkdtemp()
     pf = os.path.join(d, "port")
@@ -78,12 +105,15 @@ def main():
         url = f"http://127.0.0.1:{open(pf).read()}"
         asyncio.run(_setup(url))
         start_at = time.time() + 1.0 + 0.2 * a.client_procs
+        cpu0 = _server_cpu(p.pid)
         with mp.get_context("spawn").Pool(a.client_procs) as pool:
             res = pool.map(_proc, [(url, a, i, start_at) for i in range(a.client_procs)])
+        cpu = _server_cpu(p.pid) - cpu0
         dt = max(r[0] for r in res)
         pods = sum(r[1] for r in res)
         print(f"{a.extra or 'single process'}: {pods / dt:.0f} pod-cycles/s, {pods * 5 / dt:.0f} writes/s, "
-              f"{dt * 1e6 / (pods * 5):.1f} us/write")
+              f"{dt * 1e6 / (pods * 5):.1f} us/write, server CPU {cpu * 1e3 / pods:.3f} ms per pod-cycle "
+              f"(all API server processes, store included)")
     finally:
         p.terminate()
         p.wait()
