@@ -38,6 +38,7 @@ DATA, HEADERS, PRIORITY, RST_STREAM, SETTINGS, PUSH_PROMISE, PING, GOAWAY, WINDO
 F_END_STREAM, F_ACK, F_END_HEADERS, F_PADDED, F_PRIORITY = 0x1, 0x1, 0x4, 0x8, 0x20
 S_HEADER_TABLE_SIZE, S_ENABLE_PUSH, S_MAX_CONCURRENT_STREAMS, S_INITIAL_WINDOW_SIZE, S_MAX_FRAME_SIZE = 1, 2, 3, 4, 5
 E_NO_ERROR, E_PROTOCOL, E_CANCEL, E_REFUSED = 0x0, 0x1, 0x8, 0x7
+E_FLOW_CONTROL, E_FRAME_SIZE, E_CALM = 0x3, 0x6, 0xB
 
 _HDR = struct.Struct(">IBI")          # (length << 8 | type, flags, stream id) — 9 bytes
 _U32 = struct.Struct(">I")
@@ -46,6 +47,15 @@ _MSG = struct.Struct(">BI")           # gRPC message prefix: compressed flag, le
 # receive windows: 16 MiB per stream and per connection, replenished at half
 RECV_WINDOW = 1 << 24
 DEFAULT_WINDOW = 65535
+# what a peer may make this end hold (each advertised or enforced, so a misbehaving peer ends
+# its own stream or connection instead of growing this process): the largest frame we accept
+# (SETTINGS_MAX_FRAME_SIZE), one header block across CONTINUATIONs, concurrent streams a client
+# may open on a server connection, and one gRPC message (the kubelet's CRI limit, 16 MiB)
+MAX_FRAME = 1 << 20
+MAX_HEADER_BLOCK = 64 << 10
+MAX_CONCURRENT_STREAMS = 1024
+MAX_MESSAGE = 16 << 20
+_MAX_WINDOW = (1 << 31) - 1
 
 
 class StatusCode(enum.IntEnum):
@@ -441,9 +451,11 @@ class _Conn(asyncio.Protocol):
     # -- transport events ----------------------------------------------------------------
     def connection_made(self, transport):
         self.transport = transport
-        settings = struct.pack(">HI", S_INITIAL_WINDOW_SIZE, RECV_WINDOW) + struct.pack(">HI", S_MAX_FRAME_SIZE, 1 << 20)
+        settings = struct.pack(">HI", S_INITIAL_WINDOW_SIZE, RECV_WINDOW) + struct.pack(">HI", S_MAX_FRAME_SIZE, MAX_FRAME)
         if self.client:
             settings += struct.pack(">HI", S_ENABLE_PUSH, 0)
+        else:
+            settings += struct.pack(">HI", S_MAX_CONCURRENT_STREAMS, MAX_CONCURRENT_STREAMS)
         out = (PREFACE if self.client else b"") + self._frame(SETTINGS, 0, 0, settings)
         out += self._frame(WINDOW_UPDATE, 0, 0, _U32.pack(RECV_WINDOW - DEFAULT_WINDOW))
         transport.write(out)
@@ -481,6 +493,9 @@ class _Conn(asyncio.Protocol):
             while n - pos >= 9:
                 lt, flags, sid = _HDR.unpack_from(buf, pos)
                 ln = lt >> 8
+                if ln > MAX_FRAME:
+                    self._conn_error(E_FRAME_SIZE, f"frame of {ln} bytes exceeds SETTINGS_MAX_FRAME_SIZE {MAX_FRAME}")
+                    return
                 end = pos + 9 + ln
                 if end > n:
                     break
@@ -489,6 +504,9 @@ class _Conn(asyncio.Protocol):
                 self._on_frame(lt & 0xFF, flags, sid & 0x7FFFFFFF, payload)
                 if self.closed:
                     return
+        except _ConnError as e:
+            self._conn_error(e.code, str(e))
+            return
         except (ValueError, IndexError, struct.error) as e:
             self._conn_error(E_PROTOCOL, f"malformed frame: {e}")
             return
@@ -503,8 +521,7 @@ class _Conn(asyncio.Protocol):
             self._on_data(flags, sid, payload)
         elif typ == HEADERS:
             if flags & F_PADDED:
-                pad = payload[0]
-                payload = payload[1:len(payload) - pad]
+                payload = _unpad(payload)
             if flags & F_PRIORITY:
                 payload = payload[5:]
             st = self.streams.get(sid)
@@ -519,6 +536,13 @@ class _Conn(asyncio.Protocol):
                         self.transport.write(self._frame(RST_STREAM, 0, sid, _U32.pack(E_REFUSED)))
                 elif sid <= self.last_peer_sid or not sid & 1:
                     raise ValueError("bad stream id")
+                elif len(self.streams) >= MAX_CONCURRENT_STREAMS:
+                    # over the advertised SETTINGS_MAX_CONCURRENT_STREAMS: refuse the stream (the
+                    # header block is still decoded for the connection's HPACK state)
+                    self.last_peer_sid = sid
+                    st = _Stream(sid, 0)
+                    st.error = RpcError(StatusCode.RESOURCE_EXHAUSTED, "too many concurrent streams")
+                    self.transport.write(self._frame(RST_STREAM, 0, sid, _U32.pack(E_REFUSED)))
                 else:
                     self.last_peer_sid = sid
                     st = self.streams[sid] = _Stream(sid, self.peer_initial)
@@ -536,6 +560,8 @@ class _Conn(asyncio.Protocol):
             if st is None or st.hdr_block is None:
                 raise ValueError("unexpected CONTINUATION")
             st.hdr_block += payload
+            if len(st.hdr_block) > MAX_HEADER_BLOCK:
+                raise _ConnError(E_CALM, f"header block over {MAX_HEADER_BLOCK} bytes")
             if flags & F_END_HEADERS:
                 self.cont_sid = 0
                 self.cont_st = None
@@ -546,14 +572,20 @@ class _Conn(asyncio.Protocol):
         elif typ == SETTINGS:
             if flags & F_ACK:
                 return
-            for off in range(0, len(payload) - 5, 6):
+            if sid != 0 or len(payload) % 6:
+                raise _ConnError(E_FRAME_SIZE if sid == 0 else E_PROTOCOL, "malformed SETTINGS frame")
+            for off in range(0, len(payload), 6):
                 ident, val = struct.unpack_from(">HI", payload, off)
                 if ident == S_INITIAL_WINDOW_SIZE:
+                    if val > _MAX_WINDOW:
+                        raise _ConnError(E_FLOW_CONTROL, f"SETTINGS_INITIAL_WINDOW_SIZE {val} over 2^31-1")
                     delta = val - self.peer_initial
                     self.peer_initial = val
                     for st in self.streams.values():
                         st.send_window += delta
                 elif ident == S_MAX_FRAME_SIZE:
+                    if not 16384 <= val <= (1 << 24) - 1:
+                        raise _ConnError(E_PROTOCOL, f"SETTINGS_MAX_FRAME_SIZE {val} out of range")
                     self.peer_max_frame = val
             self.transport.write(self._frame(SETTINGS, F_ACK, 0))
             if not self.ready.done():
@@ -565,11 +597,18 @@ class _Conn(asyncio.Protocol):
         elif typ == WINDOW_UPDATE:
             inc = _U32.unpack(payload)[0] & 0x7FFFFFFF
             if sid == 0:
+                if inc == 0:
+                    raise _ConnError(E_PROTOCOL, "WINDOW_UPDATE with a zero increment")
                 self.peer_window += inc
+                if self.peer_window > _MAX_WINDOW:
+                    raise _ConnError(E_FLOW_CONTROL, "connection send window over 2^31-1")
             else:
                 st = self.streams.get(sid)
                 if st is not None:
                     st.send_window += inc
+                    if inc == 0 or st.send_window > _MAX_WINDOW:
+                        self._stream_error(st, E_PROTOCOL if inc == 0 else E_FLOW_CONTROL,
+                                           "bad WINDOW_UPDATE increment")
             self._flush_blocked()
         elif typ == RST_STREAM:
             st = self.streams.pop(sid, None)
@@ -590,10 +629,15 @@ class _Conn(asyncio.Protocol):
     def _on_data(self, flags, sid, payload):
         ln = len(payload)
         self.recv_unacked += ln
+        if self.recv_unacked > RECV_WINDOW:
+            # the peer sent past the connection window this end advertised
+            raise _ConnError(E_FLOW_CONTROL, "DATA beyond the connection flow-control window")
         if flags & F_PADDED:
-            pad = payload[0]
-            payload = payload[1:len(payload) - pad]
+            payload = _unpad(payload)
         st = self.streams.get(sid)
+        if st is not None and st.recv_consumed + ln > RECV_WINDOW:
+            self._stream_error(st, E_FLOW_CONTROL, "DATA beyond the stream flow-control window")
+            st = None
         out = b""
         if self.recv_unacked >= RECV_WINDOW // 2:
             out = self._frame(WINDOW_UPDATE, 0, 0, _U32.pack(self.recv_unacked))
@@ -609,7 +653,7 @@ class _Conn(asyncio.Protocol):
             return
         st.buf += payload
         self._take_messages(st)
-        if flags & F_END_STREAM:
+        if flags & F_END_STREAM and self.streams.get(sid) is st:
             self._end(st)
 
     def _take_messages(self, st):
@@ -617,12 +661,23 @@ class _Conn(asyncio.Protocol):
         pos, n = 0, len(buf)
         while n - pos >= 5:
             comp, ln = _MSG.unpack_from(buf, pos)
+            if ln > MAX_MESSAGE:
+                # never buffer toward a message this end would refuse anyway
+                del buf[:]
+                self._stream_error(st, E_CANCEL, f"gRPC message of {ln} bytes exceeds the {MAX_MESSAGE}-byte limit",
+                                   StatusCode.RESOURCE_EXHAUSTED)
+                return
             if n - pos - 5 < ln:
                 break
             if comp:
                 st.error = RpcError(StatusCode.UNIMPLEMENTED, "compressed gRPC messages are not supported")
             st.msgs.append(bytes(buf[pos + 5:pos + 5 + ln]))
             pos += 5 + ln
+            if not self.client and len(st.msgs) > 1:
+                # unary and server-streaming calls carry exactly one request message
+                del buf[:]
+                self._stream_error(st, E_CANCEL, "more than one request message", StatusCode.UNIMPLEMENTED)
+                return
         if pos:
             del buf[:pos]
         if st.waiter is not None and st.msgs and not st.waiter.done():
@@ -675,6 +730,12 @@ class _Conn(asyncio.Protocol):
             st.waiter.set_result(None)
         if st.task is not None and not st.task.done():
             st.task.cancel()
+
+    def _stream_error(self, st, code, why, status=StatusCode.INTERNAL):
+        """A stream-level protocol error: RST_STREAM to the peer, the call fails locally (a
+        server handler that already started is cancelled)."""
+        self.reset(st, code)
+        self._fail(st, RpcError(status, why))
 
     def _conn_error(self, code, why):
         if self.transport is not None and not self.closed:
@@ -733,6 +794,22 @@ class _Conn(asyncio.Protocol):
                     self.streams.pop(st.sid, None)
         if out and not self.closed:
             self.transport.write(bytes(out))
+
+
+class _ConnError(Exception):
+    """A connection-level HTTP/2 error with its RFC 7540 error code (sent in GOAWAY)."""
+
+    def __init__(self, code, why):
+        super().__init__(why)
+        self.code = code
+
+
+def _unpad(payload):
+    """The payload of a PADDED frame without its pad length octet and padding."""
+    pad = payload[0]
+    if pad >= len(payload):
+        raise _ConnError(E_PROTOCOL, "padding exceeds the frame payload")
+    return payload[1:len(payload) - pad]
 
 
 def _status_of(st):

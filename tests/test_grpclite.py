@@ -3,6 +3,7 @@ in both directions over the device-plugin services (unary, server streaming, err
 flow control with messages larger than the default windows and frame size)."""
 import asyncio
 import os
+import struct
 import tempfile
 
 import grpc
@@ -263,6 +264,77 @@ def test_lite_server_survives_malformed_peers():
                     assert goaway and int.from_bytes(goaway[0][4:8], "big") == gl.E_PROTOCOL, frames
             ch = gl.Channel("unix://" + sock)
             info = await api.device_plugin_stub(ch).GetPluginInfo(api.DP["GetPluginInfoRequest"](), timeout=2)
+            assert info.init_timeout == 10
+            await ch.close()
+        finally:
+            await plugin.stop()
+    asyncio.run(main())
+
+
+def _frames(data):
+    out, pos = [], 0
+    while pos + 9 <= len(data):
+        lt, flags, sid = gl._HDR.unpack_from(data, pos)
+        out.append((lt & 0xFF, flags, sid, data[pos + 9:pos + 9 + (lt >> 8)]))
+        pos += 9 + (lt >> 8)
+    return out
+
+
+def test_lite_server_bounds_what_a_peer_can_make_it_hold():
+    """Limits a misbehaving peer hits instead of growing the server (RFC 7540 error codes):
+    a frame over the advertised SETTINGS_MAX_FRAME_SIZE (FRAME_SIZE_ERROR), an endless
+    CONTINUATION chain (ENHANCE_YOUR_CALM), padding longer than the frame and an out-of-range peer
+    SETTINGS_MAX_FRAME_SIZE (PROTOCOL_ERROR) end that connection; a gRPC message declared over
+    16 MiB and a second request message on a unary call are refused per stream
+    (RST_STREAM) on a connection that stays usable. The server keeps serving throughout."""
+    hdr = gl._HDR.pack
+
+    async def main():
+        d = tempfile.mkdtemp()
+        sock = os.path.join(d, "p.sock")
+        plugin = await _Plugin("amd.com/gpu", sock, [device("g0")]).start()
+        try:
+            cont = hdr((0 << 8) | gl.HEADERS, 0, 1) + b"".join(
+                hdr((16000 << 8) | gl.CONTINUATION, 0, 1) + b"\x00" * 16000 for _ in range(6))
+            conn_cases = [
+                (hdr(((gl.MAX_FRAME + 1) << 8) | gl.DATA, 0, 1), gl.E_FRAME_SIZE),
+                (cont, gl.E_CALM),
+                (hdr((4 << 8) | gl.HEADERS, gl.F_END_HEADERS | gl.F_PADDED, 1) + b"\x09abc", gl.E_PROTOCOL),
+                (hdr((6 << 8) | gl.SETTINGS, 0, 0) + struct.pack(">HI", gl.S_MAX_FRAME_SIZE, 100), gl.E_PROTOCOL),
+            ]
+            for payload, code in conn_cases:
+                r, w = await asyncio.open_unix_connection(sock)
+                w.write(gl.PREFACE + payload)
+                try:
+                    await w.drain()
+                except ConnectionError:
+                    pass
+                data = b""
+                while True:
+                    try:
+                        chunk = await asyncio.wait_for(r.read(1 << 16), 5)
+                    except ConnectionError:
+                        break
+                    if not chunk:
+                        break
+                    data += chunk
+                w.close()
+                goaway = [p for t, _, _, p in _frames(data) if t == gl.GOAWAY]
+                assert goaway and int.from_bytes(goaway[0][4:8], "big") == code, (code, _frames(data))
+
+            # per-stream limits: the same connection keeps working afterwards
+            ch = gl.Channel("unix://" + sock)
+            stub = api.device_plugin_stub(ch)
+            await stub.GetPluginInfo(api.DP["GetPluginInfoRequest"](), timeout=2)
+            conn = ch._conn
+            # a response stream whose peer declares a message over the limit: the call fails with
+            # RESOURCE_EXHAUSTED before any of it is buffered, the stream is reset
+            st = conn.streams.setdefault(99, gl._Stream(99, 0))
+            conn.last_peer_sid = max(conn.last_peer_sid, 99)
+            st.buf += gl._MSG.pack(0, gl.MAX_MESSAGE + 1) + b"\x00" * 10
+            conn._take_messages(st)
+            assert 99 not in conn.streams and st.error.code() == gl.StatusCode.RESOURCE_EXHAUSTED
+            info = await stub.GetPluginInfo(api.DP["GetPluginInfoRequest"](), timeout=2)
             assert info.init_timeout == 10
             await ch.close()
         finally:
