@@ -13,9 +13,12 @@ native store — with no other change.
 Mapping of the native store's transaction language onto etcd v3:
   * compares: MOD_REV(key, r) -> ModRevision(key) == r (r == 0: the key is absent);
     EXISTS -> Version(key) > 0; ABSENT -> Version(key) == 0; VALUE -> Value(key) == v;
-  * ops: PUT / DELETE as such; PUT_INJECT (JSON storage: the value carries a resourceVersion
-    placeholder) stores a canonical placeholder that every read replaces with the key's
-    ModRevision — the reference never stores the resourceVersion either; DELETE_TOMBSTONE
+  * ops: PUT / DELETE as such; PUT_INJECT (JSON storage: the value carries the API server's
+    secret resourceVersion token) stores the value without the token, behind a header that
+    records where it stood; every read splices the key's ModRevision back in at those offsets —
+    the reference never stores the resourceVersion either. Only values that carry the header
+    are rewritten: object content (an annotation, a protobuf string) is never touched, so no
+    user-chosen text can change what another value decodes to; DELETE_TOMBSTONE
     deletes (the watch's prev_kv is the deleted object);
   * a failed Txn reports which compare failed and that key's current value: the failure branch
     reads every compared key and the compares are re-evaluated on what it returned;
@@ -39,7 +42,8 @@ from .mvcc import KV, CompactedError, TxnResult
 
 log = logging.getLogger("etcd3-client")
 
-RV_PLACEHOLDER = b"@kamd-etcd3-rv@"
+# PUT_INJECT values: INJECT_MAGIC | u16 n | n x u32 offset | value with the n tokens removed
+INJECT_MAGIC = b"\x00KRV"
 _PAGE = 10_000
 _OPTS = [("grpc.max_receive_message_length", 1 << 30), ("grpc.max_send_message_length", 1 << 30)]
 
@@ -120,10 +124,34 @@ class Etcd3Store:
         return k[len(self.namespace):] if self.namespace and k.startswith(self.namespace) else k
 
     @staticmethod
+    def _inject(v: bytes, tok: bytes) -> bytes:
+        """The stored form of a PUT_INJECT value: the token's offsets, then the value without it."""
+        parts = v.split(tok) if tok else [v]
+        offs, pos = [], 0
+        for part in parts[:-1]:
+            pos += len(part)
+            offs.append(pos)
+        if len(offs) > 0xFFFF:
+            raise Etcd3Error("too many resourceVersion tokens in one value")
+        return INJECT_MAGIC + len(offs).to_bytes(2, "big") + b"".join(o.to_bytes(4, "big") for o in offs) + b"".join(parts)
+
+    @staticmethod
     def _value(v: bytes, mod_rev: int) -> bytes:
-        if RV_PLACEHOLDER in v:
-            return v.replace(RV_PLACEHOLDER, str(mod_rev).encode())
-        return v
+        if not v.startswith(INJECT_MAGIC):
+            return v
+        n = int.from_bytes(v[4:6], "big")
+        body = v[6 + 4 * n:]
+        if not n:
+            return body
+        rv = str(mod_rev).encode()
+        out, last = [], 0
+        for i in range(n):
+            o = int.from_bytes(v[6 + 4 * i:10 + 4 * i], "big")
+            out.append(body[last:o])
+            out.append(rv)
+            last = o
+        out.append(body[last:])
+        return b"".join(out)
 
     def _kv(self, pkv, value=None, mod_rev=None) -> KV:
         mr = mod_rev if mod_rev is not None else pkv.mod_revision
@@ -182,8 +210,7 @@ class Etcd3Store:
         if kind == wire.OP_PUT:
             return M["RequestOp"](request_put=M["PutRequest"](key=self._k(key), value=val or b""))
         if kind == wire.OP_PUT_INJECT:
-            v = (val or b"").replace(op[3], RV_PLACEHOLDER)
-            return M["RequestOp"](request_put=M["PutRequest"](key=self._k(key), value=v))
+            return M["RequestOp"](request_put=M["PutRequest"](key=self._k(key), value=self._inject(val or b"", op[3])))
         if kind in (wire.OP_DELETE, wire.OP_DELETE_TOMBSTONE):
             return M["RequestOp"](request_delete_range=M["DeleteRangeRequest"](key=self._k(key)))
         raise Etcd3Error(f"unknown op kind {kind}")

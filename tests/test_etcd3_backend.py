@@ -15,7 +15,7 @@ import sys
 import pytest
 
 from kubernetes_amd.storage import wire
-from kubernetes_amd.storage.etcd3_client import RV_PLACEHOLDER, Etcd3Store, is_etcd3_address
+from kubernetes_amd.storage.etcd3_client import INJECT_MAGIC, Etcd3Store, is_etcd3_address
 from kubernetes_amd.storage.mvcc import CompactedError
 from kubernetes_amd.storage.remote import StoreServer
 
@@ -70,14 +70,20 @@ def test_kv_txn_range_watch(run, etcd):
             assert not r4.ok and r4.failed == 0 and r4.current.value == b"/registry/pods/a/p"
             # namespaces isolate: the other store sees nothing of t1
             assert await other.get("/registry/pods/a/p") is None
-            # RV injection: the placeholder is stored, reads see the mod revision
+            # RV injection: the token's offsets are stored (not the token), reads see the mod revision
             tok = b"@rv-tok@"
-            r5 = await st.txn([], [(wire.OP_PUT_INJECT, "/registry/configmaps/a/c", b'{"rv":"' + tok + b'"}', tok)])
+            r5 = await st.txn([], [(wire.OP_PUT_INJECT, "/registry/configmaps/a/c",
+                                    b'{"rv":"' + tok + b'","x":"' + tok + b'"}', tok)])
             c = await st.get("/registry/configmaps/a/c")
-            assert c.value == b'{"rv":"%d"}' % r5.rev
+            assert c.value == b'{"rv":"%d","x":"%d"}' % (r5.rev, r5.rev)
             raw = await other._Range(__import__("kubernetes_amd.storage.etcdv3", fromlist=["M"]).M["RangeRequest"](
                 key=b"/t1/registry/configmaps/a/c"))
-            assert RV_PLACEHOLDER in raw.kvs[0].value
+            assert raw.kvs[0].value.startswith(INJECT_MAGIC) and tok not in raw.kvs[0].value
+            # object content is never rewritten: text that looks like a marker in a plainly put
+            # (e.g. protobuf) value reads back byte for byte
+            odd = b"k8s\x00\x0a\x05@rv@" + INJECT_MAGIC[1:] + b"@kamd-etcd3-rv@"
+            await st.txn([], [(wire.OP_PUT, "/registry/pods/a/odd", odd)])
+            assert (await st.get("/registry/pods/a/odd")).value == odd
             # paged prefix range, pinned to one revision
             for i in range(25):
                 await st.txn([], [(wire.OP_PUT, f"/registry/pods/b/p{i:02d}", b"x")])
