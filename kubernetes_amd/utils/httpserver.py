@@ -14,12 +14,17 @@ from urllib.parse import parse_qs, unquote
 
 log = logging.getLogger("httpserver")
 
+# largest request body read into memory (Content-Length or chunked); larger is a 413 and the
+# connection closes. Objects are far smaller (the store keeps values under ~1.5 MiB like etcd);
+# this bounds what one connection can make the server buffer.
+MAX_BODY = 64 << 20
+
 REASONS = {
     200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
     401: "Unauthorized", 403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed",
     406: "Not Acceptable", 409: "Conflict", 410: "Gone", 413: "Payload Too Large",
     415: "Unsupported Media Type", 422: "Unprocessable Entity", 429: "Too Many Requests",
-    500: "Internal Server Error", 503: "Service Unavailable", 504: "Gateway Timeout",
+    431: "Request Header Fields Too Large", 500: "Internal Server Error", 501: "Not Implemented", 503: "Service Unavailable", 504: "Gateway Timeout",
 }
 
 
@@ -178,12 +183,54 @@ class _Conn(asyncio.Protocol):
             self.server._tasks.add(t)
             t.add_done_callback(self.server._tasks.discard)
 
+    def _reject(self, status, why):
+        """Answer a request this server will not read (bad framing, too large) and close: after
+        a framing error nothing later on the connection can be trusted to start a request."""
+        body = b'{"kind":"Status","apiVersion":"v1","metadata":{},"status":"Failure","message":"%s","code":%d}' % (
+            why.encode(), status)
+        self.transport.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n"
+                             b"Connection: close\r\n\r\n%s" % (status, REASONS.get(status, "Error").encode(), len(body), body))
+        self.transport.close()
+        del self.buf[:]
+
+    def _chunked_body(self, start):
+        """(body, end offset) of a complete chunked request body at buf[start:], None while
+        incomplete; raises ValueError on bad framing or a body over the size limit."""
+        buf, pos, parts, size = self.buf, start, [], 0
+        limit = self.server.max_body
+        while True:
+            eol = buf.find(b"\r\n", pos)
+            if eol < 0:
+                if len(buf) - pos > 1024:
+                    raise ValueError("chunk size line too long")
+                return None
+            n = int(bytes(buf[pos:eol]).split(b";", 1)[0].strip(), 16)
+            if n < 0:
+                raise ValueError("negative chunk size")
+            size += n
+            if size > limit:
+                raise OverflowError
+            if n == 0:
+                # trailer section: header lines up to an empty line
+                tend = buf.find(b"\r\n\r\n", eol) if buf[eol + 2:eol + 4] != b"\r\n" else eol
+                if tend < 0:
+                    if len(buf) - eol > 8192:
+                        raise ValueError("trailer section too long")
+                    return None
+                return b"".join(parts), tend + 4
+            if len(buf) < eol + 2 + n + 2:
+                return None
+            if buf[eol + 2 + n:eol + 4 + n] != b"\r\n":
+                raise ValueError("chunk not terminated by CRLF")
+            parts.append(bytes(buf[eol + 2:eol + 2 + n]))
+            pos = eol + 4 + n
+
     def _parse(self):
         buf = self.buf
         end = buf.find(b"\r\n\r\n")
         if end < 0:
             if len(buf) > 1 << 20:
-                self.transport.close()
+                self._reject(431, "request header fields too large")
             return None
         head = bytes(buf[:end]).decode("latin-1")
         lines = head.split("\r\n")
@@ -199,7 +246,36 @@ class _Conn(asyncio.Protocol):
             # repeated headers combine into one comma-separated list (RFC 7230 §3.2.2), e.g.
             # several X-Stream-Protocol-Version offers
             headers[k] = headers[k] + ", " + v.strip() if k in headers else v.strip()
-        clen = int(headers.get("content-length", "0") or 0)
+        te = headers.get("transfer-encoding")
+        if te is not None:
+            # RFC 7230 §3.3.3: chunked must be the final coding; it overrides Content-Length
+            if te.strip().lower() != "chunked":         # other codings are not implemented
+                self._reject(501, "unsupported transfer-encoding")
+                return None
+            try:
+                got = self._chunked_body(end + 4)
+            except OverflowError:
+                self._reject(413, "request body too large")
+                return None
+            except ValueError:
+                self._reject(400, "malformed chunked request body")
+                return None
+            if got is None:
+                return None
+            body, stop = got
+            del buf[:stop]
+            headers.pop("transfer-encoding", None)
+            headers["content-length"] = str(len(body))
+            return Request(method, target, headers, body, self.transport)
+        cl = headers.get("content-length", "0") or "0"
+        if not cl.isdigit():
+            # negative, non-numeric or differing repeated values: the body's end is unknown
+            self._reject(400, "invalid content-length")
+            return None
+        clen = int(cl)
+        if clen > self.server.max_body:
+            self._reject(413, "request body too large")
+            return None
         if len(buf) < end + 4 + clen:
             return None
         body = bytes(buf[end + 4:end + 4 + clen])
@@ -320,6 +396,7 @@ class HTTPServer:
         self.timeout_response = timeout_response or Response(504, b"request timed out", "text/plain")
         self._sweeper = None
         self.loop_time = time.monotonic
+        self.max_body = MAX_BODY
 
     async def _sweep(self):
         period = max(0.05, min(1.0, self.request_timeout / 4))

@@ -1,0 +1,77 @@
+"""HTTP/1.1 request framing in utils/httpserver.py (the API server's and kubelet's listener):
+chunked request bodies are decoded (Go clients send them when the length is unknown), a body
+over the size limit is a 413, a bad or negative Content-Length or an unsupported
+Transfer-Encoding is refused and the connection closed — never guessed at, so no bytes of one
+request can be read as the start of another."""
+import asyncio
+
+from kubernetes_amd.utils import httpserver as hs
+
+
+async def _exchange(port, raw, read_all=True):
+    r, w = await asyncio.open_connection("127.0.0.1", port)
+    w.write(raw)
+    await w.drain()
+    data = b""
+    while True:
+        try:
+            chunk = await asyncio.wait_for(r.read(1 << 16), 1.0 if read_all else 0.3)
+        except asyncio.TimeoutError:
+            break
+        if not chunk:
+            break
+        data += chunk
+    w.close()
+    return data
+
+
+def test_request_framing():
+    async def main():
+        seen = []
+
+        async def handler(req):
+            seen.append((req.method, req.path, req.body))
+            return hs.Response(200, b"%d" % len(req.body), "text/plain")
+        srv = hs.HTTPServer(handler)
+        srv.max_body = 1000
+        await srv.start()
+        port = srv.port
+        try:
+            # chunked body (with an extension and a trailer), then a pipelined plain request
+            d = await _exchange(port, b"POST /a HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+                                      b"5;ext=1\r\nhello\r\n6\r\n world\r\n0\r\nX-T: 1\r\n\r\n"
+                                      b"POST /b HTTP/1.1\r\nHost: x\r\nContent-Length: 2\r\n\r\nok", read_all=False)
+            assert seen == [("POST", "/a", b"hello world"), ("POST", "/b", b"ok")], seen
+            assert d.count(b"HTTP/1.1 200") == 2
+            # chunked body arriving in pieces
+            seen.clear()
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            for part in (b"PUT /c HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n3\r", b"\nabc\r\n", b"0\r\n\r\n"):
+                w.write(part)
+                await w.drain()
+                await asyncio.sleep(0.05)
+            assert (await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 2)).startswith(b"HTTP/1.1 200")
+            w.close()
+            assert seen == [("PUT", "/c", b"abc")]
+            # refusals: each answers once and closes; the handler never runs
+            seen.clear()
+            for raw, code in [
+                (b"POST /d HTTP/1.1\r\nContent-Length: 5000\r\n\r\n", b"413"),
+                (b"POST /d HTTP/1.1\r\nContent-Length: -3\r\n\r\nabc", b"400"),
+                (b"POST /d HTTP/1.1\r\nContent-Length: 3, 4\r\n\r\nabcd", b"400"),
+                (b"POST /d HTTP/1.1\r\nTransfer-Encoding: gzip\r\n\r\n", b"501"),
+                (b"POST /d HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n", b"400"),
+                (b"POST /d HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabcXY0\r\n\r\n", b"400"),
+                (b"POST /d HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n" + b"200\r\n" + b"a" * 512 + b"\r\n"
+                 + b"300\r\n" + b"b" * 768 + b"\r\n0\r\n\r\n", b"413"),
+            ]:
+                d = await _exchange(port, raw)
+                assert d.startswith(b"HTTP/1.1 " + code), (raw[:60], d[:80])
+                assert b"Connection: close" in d
+            assert seen == []
+            # the server still serves
+            d = await _exchange(port, b"GET /e HTTP/1.1\r\nContent-Length: 0\r\n\r\n", read_all=False)
+            assert d.startswith(b"HTTP/1.1 200") and seen == [("GET", "/e", b"")]
+        finally:
+            await srv.stop()
+    asyncio.run(main())
