@@ -28,6 +28,10 @@ SYN_STREAM, SYN_REPLY, RST_STREAM, SETTINGS, PING, GOAWAY, HEADERS, WINDOW_UPDAT
 FLAG_FIN = 0x01
 RST_PROTOCOL_ERROR, RST_INVALID_STREAM, RST_REFUSED_STREAM, RST_CANCEL = 1, 2, 3, 5
 MAX_FRAME = (1 << 24) - 1
+# one decompressed header block (a compressed frame could otherwise inflate ~1000x) and the
+# streams one session may hold open (exec/attach use 3-5, port-forward 2 per port)
+MAX_HEADER_BLOCK = 1 << 20
+MAX_STREAMS = 1024
 
 # The SPDY/3 header-compression dictionary (draft-mbelshe-httpbis-spdy-00 §2.6.10.1): the common
 # header names and values, each as a 32-bit big-endian length + bytes, then a run of status
@@ -167,7 +171,10 @@ class Connection:
         return self._zc.compress(block) + self._zc.flush(zlib.Z_SYNC_FLUSH)
 
     def _decompress(self, data: bytes) -> bytes:
-        return self._zd.decompress(data)
+        out = self._zd.decompress(data, MAX_HEADER_BLOCK)
+        if self._zd.unconsumed_tail:
+            raise SpdyError(f"header block inflates past {MAX_HEADER_BLOCK} bytes")
+        return out
 
     async def _send(self, frame: bytes):
         async with self._wlock:
@@ -234,6 +241,9 @@ class Connection:
             headers = decode_block(self._decompress(body[10:]))
             if sid in self.streams or self.goaway:
                 await self._send(control_frame(RST_STREAM, 0, struct.pack(">II", sid, RST_PROTOCOL_ERROR)))
+                return
+            if len(self.streams) >= MAX_STREAMS:
+                await self._send(control_frame(RST_STREAM, 0, struct.pack(">II", sid, RST_REFUSED_STREAM)))
                 return
             st = Stream(self, sid, headers)
             self.streams[sid] = st

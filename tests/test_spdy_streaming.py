@@ -54,6 +54,28 @@ def test_frame_layout():
     assert rst[:8] == b"\x80\x03\x00\x03\x00\x00\x00\x08"
 
 
+def test_header_block_bomb_ends_the_session():
+    """A SYN_STREAM whose compressed header block inflates past MAX_HEADER_BLOCK ends the session
+    (no stream is created, nothing is inflated past the limit); a normal block is still read."""
+    async def main(block_bytes):
+        c = spdy.Connection(None, None)
+        reader = asyncio.StreamReader()
+        peer = spdy.Connection(None, None)
+        blk = peer._compress(block_bytes)
+        reader.feed_data(spdy.control_frame(spdy.SYN_STREAM, 0, struct.pack(">IIBB", 1, 0, 0, 0) + blk))
+        reader.feed_eof()
+        c.reader = reader
+        c.server = True
+        seen = []
+        c.on_stream = seen.append
+        await asyncio.wait_for(c.serve(), 5)
+        return seen
+    big = spdy.encode_block({"x": ["a" * (2 * spdy.MAX_HEADER_BLOCK)]})
+    assert asyncio.run(main(big)) == []
+    ok = asyncio.run(main(spdy.encode_block({"streamtype": ["error"]})))
+    assert len(ok) == 1 and ok[0].headers["streamtype"] == ["error"]
+
+
 SLEEPER = "import time\nwhile True: time.sleep(1)\n"
 ECHO = ("import socket,sys\n"
         "s=socket.socket(); s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)\n"
