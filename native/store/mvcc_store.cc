@@ -343,6 +343,10 @@ class Engine {
 
 // ---------------------------------------------------------------------------
 // wire helpers
+// largest request frame a client may send (values are bounded far below this, like etcd's
+// 1.5 MiB request limit; a txn carries a handful of them)
+static constexpr uint32_t kMaxFrame = 256u << 20;
+
 struct Reader {
   const char* p;
   const char* e;
@@ -1267,6 +1271,9 @@ class Server {
     while (c->in.size() - off >= 9) {
       uint32_t len;
       memcpy(&len, c->in.data() + off, 4);
+      // a frame is id(4) + op(1) + body: shorter is malformed, longer than kMaxFrame would only
+      // make this connection buffer without bound — either ends the connection
+      if (len < 5 || len > kMaxFrame) return false;
       if (c->in.size() - off - 4 < len) break;
       uint32_t id;
       memcpy(&id, c->in.data() + off + 4, 4);
@@ -1525,6 +1532,12 @@ class Server {
       if (h.buf.size() >= 4) {
         uint32_t len;
         memcpy(&len, h.buf.data(), 4);
+        if (len > kMaxFrame) {                  // a watch spec is a few hundred bytes
+          if (h.client >= 0) close(h.client);
+          h.client = -1;
+          drop_handoff(fd);
+          return;
+        }
         if (h.buf.size() >= 4 + (size_t)len) {
           int client = h.client;
           std::string msg = h.buf.substr(4, len);

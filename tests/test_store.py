@@ -153,3 +153,32 @@ def test_remote_store_server(run):
         run(main())
     finally:
         srv.stop()
+
+
+def test_store_server_drops_malformed_frames(run):
+    """A request frame shorter than its id+op header, or one declaring more than the server's
+    frame limit, ends only that connection; the store keeps serving other clients. (A zero
+    length used to reach the request handler as a body length of 2^32 - 5.)"""
+    import socket
+    import struct as st
+    srv = StoreServer()
+    addr = srv.start()
+    try:
+        for frame in (st.pack("<I", 0) + b"\0" * 16, st.pack("<I", 4) + b"\0" * 16,
+                      st.pack("<I", 0xFFFFFFF0) + b"\0" * 16):
+            s = socket.socket(socket.AF_UNIX)
+            s.connect(srv.socket_path)
+            s.sendall(frame)
+            s.settimeout(5)
+            assert s.recv(64) == b""          # closed by the server, nothing answered
+            s.close()
+        assert srv.proc.poll() is None
+
+        async def main():
+            c = await RemoteStore(addr).connect()
+            r = await c.txn([], [(wire.OP_PUT, "/registry/x", b"v")])
+            assert r.ok and (await c.get("/registry/x")).value == b"v"
+            await c.close()
+        run(main())
+    finally:
+        srv.stop()
