@@ -158,8 +158,10 @@ def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
     spare = cpus - workers - shards - 1
     if cpus >= 64:
         # a whole node: the hollow kubelets' share of the per-pod demand model, per rank
-        # (4 processes per rank at 0.69 ms per pod), within the CPUs left
-        per_rank = -(-demand("hollow", world) // world)
+        # (4 processes per rank at 0.69 ms per pod), but at least 6 — hollow kubelets wait on
+        # the control plane, and 6 beat 4 per rank in interleaved box runs at both API shapes
+        # (profiles/r4_gpu/sweep: w4 s3 h6 3982-4062 vs h4 3537-3828 pods/s) — within the CPUs left
+        per_rank = max(6, -(-demand("hollow", world) // world))
         return max(1, min(nodes_per_rank, per_rank, max(2, (spare - world) // max(1, world))))
     # hollow kubelets are mostly waiting on the control plane: mild oversubscription pays
     # (profiles/r2_hollow_procs, r2_scale: N=4 on 16 CPUs 1868 -> 2578 pods/s with 2 per rank;

@@ -164,7 +164,7 @@ def test_store_bench_small():
 def test_hollow_procs_per_rank(monkeypatch):
     import bench
     monkeypatch.setattr(bench, "cpu_budget", lambda: 192)
-    assert bench.hollow_procs_for(8, 100, 32, 18) == 4       # a whole node: the demand model
+    assert bench.hollow_procs_for(8, 100, 32, 18) == 6       # a whole node: demand model, at least 6
     assert bench.hollow_procs_for(8, 4, 32, 18) == 4         # never more than the rank's nodes
     monkeypatch.setattr(bench, "cpu_budget", lambda: 64)
     assert bench.hollow_procs_for(8, 100, 16, 9) == 3        # bounded by the spare CPUs
