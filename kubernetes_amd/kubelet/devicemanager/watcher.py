@@ -145,7 +145,12 @@ class PluginWatcher:
                 asyncio.get_event_loop().remove_reader(self._fd)
             except Exception:
                 pass
-            os.close(self._fd)
+            # closing an inotify descriptor waits out a kernel SRCU grace period (~50 ms on the
+            # MI355X box, profiles/r4_gpu/cprofile): close it off the event loop so a process
+            # stopping many watchers (a hollow-node process with 16+ kubelets) does not
+            # serialise those waits; concurrent closes share grace periods
+            import threading
+            threading.Thread(target=os.close, args=(self._fd,), name="inotify-close", daemon=True).start()
             self._fd = None
         if self._poll_task:
             self._poll_task.cancel()
