@@ -27,6 +27,10 @@ _PATCH_TYPES = {"merge": "application/merge-patch+json", "strategic": "applicati
                 "json": "application/json-patch+json"}
 
 
+def _plural(resource):
+    return resource.plural if isinstance(resource, m.ResourceInfo) else resource
+
+
 def _status(code, reason, msg):
     return APIStatusError(code, {"kind": "Status", "apiVersion": "v1", "status": "Failure", "code": code,
                                  "reason": reason, "message": msg})
@@ -96,6 +100,8 @@ class FakeClient:
         self.actions.clear()
 
     def _react(self, action):
+        if isinstance(action.resource, m.ResourceInfo):
+            action.resource = action.resource.plural
         self.actions.append(action)
         for verb, res, fn in self.reactors:
             if verb in ("*", action.verb) and res in ("*", action.resource):
@@ -106,6 +112,7 @@ class FakeClient:
 
     # -- tracker -------------------------------------------------------------------------
     def _key(self, plural, ns, name):
+        plural = _plural(plural)
         ri = m.BY_PLURAL.get(plural)
         return ((ns or "default") if ri is None or ri.namespaced else None, name)
 
@@ -142,6 +149,7 @@ class FakeClient:
                 q.put_nowait(None)
 
     async def get(self, resource, name, namespace=None, subresource=""):
+        resource = _plural(resource)
         h, r = self._react(Action("get", resource, namespace, name, subresource))
         if h:
             return r
@@ -149,6 +157,7 @@ class FakeClient:
 
     async def list(self, resource, namespace=None, label_selector=None, field_selector=None, limit=0, continue_=None,
                    **_kw):
+        resource = _plural(resource)
         h, r = self._react(Action("list", resource, namespace))
         if h:
             return r
@@ -177,10 +186,12 @@ class FakeClient:
                 "metadata": {"resourceVersion": str(next(self.rv))}, "items": items}
 
     async def list_all(self, resource, namespace=None, label_selector=None, field_selector=None, chunk=500, **_kw):
+        resource = _plural(resource)
         lst = await self.list(resource, namespace, label_selector, field_selector)
         return lst["items"], lst["metadata"]["resourceVersion"]
 
     async def create(self, resource, obj, namespace=None, decode=True):
+        resource = _plural(resource)
         obj = copy.deepcopy(obj)
         md = obj.setdefault("metadata", {})
         if namespace and m.BY_PLURAL.get(resource, m.BY_PLURAL["pods"]).namespaced:
@@ -195,6 +206,7 @@ class FakeClient:
         return self._store(resource, obj)
 
     async def update(self, resource, obj, namespace=None, subresource=""):
+        resource = _plural(resource)
         obj = copy.deepcopy(obj)
         md = obj["metadata"]
         ns = namespace or md.get("namespace")
@@ -216,6 +228,7 @@ class FakeClient:
         return await self.update(resource, obj, namespace, "status")
 
     async def patch(self, resource, name, patch, namespace=None, patch_type="merge", subresource="", decode=True):
+        resource = _plural(resource)
         h, r = self._react(Action("patch", resource, namespace, name, subresource, patch))
         if h:
             return r
@@ -225,6 +238,7 @@ class FakeClient:
 
     async def delete(self, resource, name, namespace=None, grace_period=None, propagation=None, uid=None,
                      decode=True):
+        resource = _plural(resource)
         h, r = self._react(Action("delete", resource, namespace, name))
         if h:
             return r
@@ -236,6 +250,7 @@ class FakeClient:
         return {"kind": "Status", "status": "Success"}
 
     async def delete_collection(self, resource, namespace=None, label_selector=None):
+        resource = _plural(resource)
         for o in (await self.list(resource, namespace, label_selector))["items"]:
             await self.delete(resource, o["metadata"]["name"], o["metadata"].get("namespace"))
 
@@ -264,6 +279,7 @@ class FakeClient:
 
     async def watch(self, resource, namespace=None, resource_version=None, label_selector=None, field_selector=None,
                     timeout_seconds=None, **_kw):
+        resource = _plural(resource)
         self._react(Action("watch", resource, namespace))
         q: asyncio.Queue = asyncio.Queue()
         ent = (namespace, q)

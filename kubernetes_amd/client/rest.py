@@ -55,8 +55,10 @@ class TokenBucket:
             await asyncio.sleep((1 - self.tokens) / self.qps)
 
 
-def resource_path(resource: str, namespace=None, name=None, subresource="", watch=False):
-    ri = m.lookup(resource)
+def resource_path(resource, namespace=None, name=None, subresource="", watch=False):
+    """`resource`: a registered name (plural, kind, short name) or a `ResourceInfo` (a resource
+    found through discovery, e.g. a custom resource this process never registered)."""
+    ri = resource if isinstance(resource, m.ResourceInfo) else m.lookup(resource)
     if ri is None:
         raise ValueError(f"unknown resource {resource!r}")
     base = "/api/v1" if not ri.group else f"/apis/{ri.group}/{ri.version}"

@@ -4,9 +4,7 @@ Parity:
   * NamespaceController — `pkg/controller/namespace/deletion/namespaced_resources_deleter.go`:
     a Terminating namespace has all its namespaced content deleted, then its `kubernetes`
     finalizer is removed through `/finalize` and the namespace disappears.
-  * GarbageCollector — `pkg/controller/garbagecollector`: dependents whose owner (by UID) is
-    gone are deleted (background); `orphan` finalizer strips ownerReferences from dependents;
-    `foregroundDeletion` deletes dependents first, then releases the owner.
+  * GarbageCollector — `pkg/controller/garbagecollector`: in `garbagecollector.py`.
   * PodGC — `pkg/controller/podgc/gc_controller.go`: terminated pods above
     `terminated_pod_gc_threshold` (oldest first) and pods bound to nodes that no longer exist.
   (Node lifecycle — health, zones, rate-limited evictions, taint manager — is in
@@ -73,118 +71,6 @@ def _dump(o):
     return codec.dumpb(o)
 
 
-class GarbageCollector(Controller):
-    """Owner-reference graph over the informer caches of every served resource."""
-    name = "garbagecollector"
-    workers = 4
-    RESOURCES = ("pods", "replicasets", "deployments", "jobs", "cronjobs", "daemonsets", "statefulsets",
-                 "replicationcontrollers", "controllerrevisions", "configmaps", "secrets", "services",
-                 "endpoints", "poddisruptionbudgets")
-
-    def setup(self):
-        self.infs = {r: self.factory.get(r) for r in self.RESOURCES}
-        self.uids: dict[str, tuple] = {}          # uid -> (resource, key)
-        self.children: dict[str, set] = {}        # owner uid -> {(resource, key)}
-        for r, inf in self.infs.items():
-            inf.add_handler(lambda o, r=r: self._add(r, o), lambda old, new, r=r: self._update(r, old, new),
-                            lambda o, r=r: self._delete(r, o))
-
-    def _refs(self, o):
-        return [ref["uid"] for ref in (o["metadata"].get("ownerReferences") or ()) if ref.get("uid")]
-
-    def _add(self, r, o):
-        key = m.ns_name(o)
-        uid = o["metadata"].get("uid")
-        self.uids[uid] = (r, key)
-        for ou in self._refs(o):
-            self.children.setdefault(ou, set()).add((r, key))
-            if ou not in self.uids:
-                self.enqueue(f"dep|{r}|{key}")
-        fins = o["metadata"].get("finalizers") or ()
-        if o["metadata"].get("deletionTimestamp") and ("orphan" in fins or "foregroundDeletion" in fins):
-            self.enqueue(f"own|{r}|{key}")
-
-    def _update(self, r, old, new):
-        for ou in self._refs(old):
-            s = self.children.get(ou)
-            if s:
-                s.discard((r, m.ns_name(old)))
-        self._add(r, new)
-
-    def _delete(self, r, o):
-        uid = o["metadata"].get("uid")
-        self.uids.pop(uid, None)
-        for ou in self._refs(o):
-            s = self.children.get(ou)
-            if s:
-                s.discard((r, m.ns_name(o)))
-        for child in list(self.children.get(uid, ())):
-            self.enqueue(f"dep|{child[0]}|{child[1]}")
-        owner_fg = [ou for ou in self._refs(o) if ou in self.uids]
-        for ou in owner_fg:
-            r2, k2 = self.uids[ou]
-            self.enqueue(f"own|{r2}|{k2}")
-
-    async def sync(self, key):
-        kind, r, okey = key.split("|", 2)
-        obj = self.infs[r].get(okey)
-        if obj is None:
-            return
-        ns, name = split_key(okey)
-        if kind == "dep":
-            refs = obj["metadata"].get("ownerReferences") or []
-            if not refs:
-                return
-            alive = [ref for ref in refs if ref.get("uid") in self.uids]
-            if alive:
-                # owner still exists; if it is being deleted in the foreground, delete the dependent
-                for ref in alive:
-                    r2, k2 = self.uids[ref["uid"]]
-                    owner = self.infs[r2].get(k2)
-                    if owner and owner["metadata"].get("deletionTimestamp") and "foregroundDeletion" in (owner["metadata"].get("finalizers") or ()):
-                        await self._del(r, name, ns)
-                return
-            await self._del(r, name, ns)
-            return
-        # owner with orphan / foreground finalizer
-        fins = list(obj["metadata"].get("finalizers") or [])
-        uid = obj["metadata"]["uid"]
-        kids = [c for c in self.children.get(uid, ()) if self.infs[c[0]].get(c[1]) is not None]
-        if "orphan" in fins:
-            for cr, ck in kids:
-                child = self.infs[cr].get(ck)
-                refs = [x for x in child["metadata"].get("ownerReferences") or () if x.get("uid") != uid]
-                cns, cname = split_key(ck)
-                try:
-                    await self.client.patch(cr, cname, {"metadata": {"ownerReferences": refs or None}}, cns)
-                except APIStatusError as e:
-                    if not is_not_found(e):
-                        raise
-            fins.remove("orphan")
-        elif "foregroundDeletion" in fins:
-            if kids:
-                for cr, ck in kids:
-                    cns, cname = split_key(ck)
-                    await self._del(cr, cname, cns)
-                self.queue.add_after(key, 0.2)
-                return
-            fins.remove("foregroundDeletion")
-        else:
-            return
-        try:
-            await self.client.patch(r, name, {"metadata": {"finalizers": fins or None}}, ns)
-        except APIStatusError as e:
-            if not (is_not_found(e) or is_conflict(e)):
-                raise
-
-    async def _del(self, r, name, ns):
-        try:
-            await self.client.delete(r, name, ns, propagation="Background")
-        except APIStatusError as e:
-            if not is_not_found(e):
-                raise
-
-
 class PodGCController(Controller):
     name = "podgc"
     workers = 1
@@ -235,3 +121,4 @@ class PodGCController(Controller):
 
 
 from .nodelifecycle import NodeLifecycleController  # noqa: E402,F401  (re-export)
+from .garbagecollector import GarbageCollector  # noqa: E402,F401  (re-export)
