@@ -153,100 +153,4 @@ class DaemonSetController(Controller):
                     raise
 
 
-class StatefulSetController(Controller):
-    name = "statefulset"
-    workers = 2
-
-    def setup(self):
-        self.ss_inf = self.factory.get("statefulsets")
-        self.pod_inf = self.factory.get("pods")
-        self.rev_inf = self.factory.get("controllerrevisions")
-        self.ss_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
-        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
-
-    def _pod(self, pod):
-        ref = controller_ref(pod)
-        if ref and ref.get("kind") == "StatefulSet":
-            self.enqueue(f"{pod['metadata']['namespace']}/{ref['name']}")
-
-    async def sync(self, key):
-        ss = self.ss_inf.get(key)
-        if ss is None or ss["metadata"].get("deletionTimestamp"):
-            return
-        ns, name = split_key(key)
-        spec = ss.get("spec") or {}
-        replicas = int(spec.get("replicas", 1))
-        parallel = spec.get("podManagementPolicy") == "Parallel"
-        tmpl = spec.get("template") or {}
-        rev_obj = await ensure_revision(self.client, ss, "StatefulSet", tmpl,
-                                        revisions_of(self.rev_inf.list(), ss["metadata"]["uid"]),
-                                        int(spec.get("revisionHistoryLimit", 10)))
-        rev_name = rev_obj["metadata"]["name"]
-        uid = ss["metadata"]["uid"]
-        pods = {}
-        for p in self.pod_inf.list():
-            if p["metadata"].get("namespace") == ns and (controller_ref(p) or {}).get("uid") == uid:
-                try:
-                    pods[int(p["metadata"]["name"].rsplit("-", 1)[1])] = p
-                except (ValueError, IndexError):
-                    continue
-        # create / replace missing ordinals
-        for i in range(replicas):
-            p = pods.get(i)
-            if p is not None and (p.get("status") or {}).get("phase") in ("Failed", "Succeeded"):
-                await self._delete(p)
-                return
-            if p is None:
-                pod = pod_from_template(tmpl, ss, "", ns)
-                pod["metadata"].pop("generateName")
-                pod["metadata"]["name"] = f"{name}-{i}"
-                pod["metadata"]["labels"]["statefulset.kubernetes.io/pod-name"] = f"{name}-{i}"
-                pod["metadata"]["labels"]["controller-revision-hash"] = rev_name
-                pod["spec"]["hostname"] = f"{name}-{i}"
-                if spec.get("serviceName"):
-                    pod["spec"]["subdomain"] = spec["serviceName"]
-                try:
-                    await self.client.create("pods", pod, ns)
-                except APIStatusError as e:
-                    if not is_already_exists(e):
-                        raise
-                if not parallel:
-                    break
-            elif not parallel and not (pod_is_ready(p) and (p.get("status") or {}).get("phase") == "Running"):
-                break
-        # scale down from the highest ordinal
-        extra = sorted((i for i in pods if i >= replicas), reverse=True)
-        for i in extra:
-            p = pods[i]
-            if not p["metadata"].get("deletionTimestamp"):
-                await self._delete(p)
-            if not parallel:
-                break
-        # rolling update: replace the highest-ordinal pod on an old revision, one at a time
-        if (spec.get("updateStrategy") or {}).get("type", "RollingUpdate") == "RollingUpdate" and not extra:
-            all_ready = all(pods.get(i) is not None and pod_is_ready(pods[i]) for i in range(replicas))
-            if all_ready:
-                for i in sorted(range(replicas), reverse=True):
-                    p = pods[i]
-                    if (p["metadata"].get("labels") or {}).get("controller-revision-hash") != rev_name:
-                        await self._delete(p)
-                        break
-        cur = [p for i, p in pods.items() if i < replicas]
-        st = {"replicas": len(cur), "readyReplicas": sum(1 for p in cur if pod_is_ready(p)),
-              "currentReplicas": sum(1 for p in cur if (p["metadata"].get("labels") or {}).get("controller-revision-hash") == rev_name),
-              "updatedReplicas": sum(1 for p in cur if (p["metadata"].get("labels") or {}).get("controller-revision-hash") == rev_name),
-              "currentRevision": rev_name, "updateRevision": rev_name,
-              "observedGeneration": ss["metadata"].get("generation", 1)}
-        if {k: (ss.get("status") or {}).get(k) for k in st} != st:
-            try:
-                await self.client.patch("statefulsets", name, {"status": st}, ns, "merge", "status")
-            except APIStatusError as e:
-                if not is_not_found(e):
-                    raise
-
-    async def _delete(self, p):
-        try:
-            await self.client.delete("pods", p["metadata"]["name"], p["metadata"]["namespace"])
-        except APIStatusError as e:
-            if not is_not_found(e):
-                raise
+from .statefulset import StatefulSetController  # noqa: E402,F401  (re-export)

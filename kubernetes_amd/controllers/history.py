@@ -28,7 +28,8 @@ def revisions_of(lister_items, owner_uid):
 
 
 async def ensure_revision(client, owner, kind, template, existing, limit=10):
-    """The ControllerRevision for `template` (created or promoted), pruning old history."""
+    """The ControllerRevision for `template` (created or promoted), pruning old history beyond
+    `limit` (None: no pruning here — the caller truncates with `truncate_history`)."""
     md = owner["metadata"]
     ns, h = md["namespace"], revision_hash(template)
     name = f"{md['name']}-{h}"
@@ -49,6 +50,8 @@ async def ensure_revision(client, owner, kind, template, existing, limit=10):
     elif int(cur.get("revision", 0)) < newest:
         # rolled back to an older template: it becomes the newest revision again
         cur = await client.patch("controllerrevisions", name, {"revision": newest + 1}, ns)
+    if limit is None:
+        return cur
     keep = [r for r in existing if r["metadata"]["name"] != name]
     excess = len(keep) + 1 - max(1, limit)
     for r in sorted(keep, key=lambda r: int(r.get("revision", 0)))[:max(0, excess)]:
@@ -58,3 +61,17 @@ async def ensure_revision(client, owner, kind, template, existing, limit=10):
             if not is_not_found(e):
                 raise
     return cur
+
+
+async def truncate_history(client, revisions, live, limit):
+    """`truncateHistory` (stateful_set_control.go:124) / `cleanupHistory` (daemon/update.go:110):
+    delete non-live revisions (live = the current and update revisions and every pod's), oldest
+    first, until at most `limit` of them remain."""
+    history = sorted((r for r in revisions if r["metadata"]["name"] not in live),
+                     key=lambda r: int(r.get("revision", 0)))
+    for r in history[:max(0, len(history) - max(0, int(limit)))]:
+        try:
+            await client.delete("controllerrevisions", r["metadata"]["name"], r["metadata"]["namespace"])
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise

@@ -1,0 +1,517 @@
+"""StatefulSet controller: tables ported from `pkg/controller/statefulset/stateful_set_utils_test.go`
+and `stateful_set_control_test.go` (scale up / down with the monotonic and burst invariants,
+replaced and failed pods, RollingUpdate, RollingUpdate with partition, OnDelete, revision history
+limit, rollback), run against the in-memory fake client with a simulated kubelet; plus the live
+"web" StatefulSet with volumeClaimTemplates end to end.
+"""
+import asyncio
+import copy
+
+import pytest
+
+from kubernetes_amd.api import meta as m
+from kubernetes_amd.api.validation_ext import validate_stateful_set
+from kubernetes_amd.client.fake import FakeClient
+from kubernetes_amd.client.rest import APIStatusError
+from kubernetes_amd.client.informer import InformerFactory
+from kubernetes_amd.cluster import LocalCluster
+from kubernetes_amd.controllers import statefulset as S
+
+
+def new_set(replicas=3, name="foo", claims=("datadir",), parallel=False, strategy=None):
+    ss = {"apiVersion": "apps/v1", "kind": "StatefulSet",
+          "metadata": {"name": name, "namespace": "default", "uid": f"uid-{name}", "generation": 1},
+          "spec": {"replicas": replicas, "serviceName": "governingsvc",
+                   "selector": {"matchLabels": {"foo": "bar"}},
+                   "podManagementPolicy": "Parallel" if parallel else "OrderedReady",
+                   "updateStrategy": strategy or {"type": "RollingUpdate"}, "revisionHistoryLimit": 2,
+                   "template": {"metadata": {"labels": {"foo": "bar"}},
+                                "spec": {"containers": [{"name": "nginx", "image": "nginx",
+                                                         "volumeMounts": [{"name": c, "mountPath": f"/{c}"}
+                                                                          for c in claims]}]}},
+                   "volumeClaimTemplates": [{"metadata": {"name": c}, "spec": {
+                       "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}}
+                       for c in claims]}}
+    return ss
+
+
+def _pod(name, ns="default", labels=None, volumes=None):
+    return {"metadata": {"name": name, "namespace": ns, "labels": dict(labels or {})},
+            "spec": {"volumes": list(volumes or [])}}
+
+
+# -- stateful_set_utils_test.go -----------------------------------------------------------------
+def test_get_parent_name_and_ordinal():
+    ss = new_set()
+    pod = S.new_stateful_pod(ss, 1)
+    assert S.parent_and_ordinal(pod) == ("foo", 1)
+    pod["metadata"]["name"] = "1-bar"
+    assert S.parent_and_ordinal(pod) == ("", -1)
+    assert S.parent_and_ordinal(_pod("web-x")) == ("", -1)
+
+
+def test_is_member_of():
+    ss, ss2 = new_set(name="foo"), new_set(name="foo2")
+    pod = S.new_stateful_pod(ss, 1)
+    assert S.is_member_of(ss, pod) and not S.is_member_of(ss2, pod)
+
+
+def test_identity_matches():
+    ss = new_set()
+    pod = S.new_stateful_pod(ss, 1)
+    assert S.identity_matches(ss, pod)
+    for mutate in (lambda p: p["metadata"].__setitem__("name", "foo"),
+                   lambda p: p["metadata"].__setitem__("namespace", ""),
+                   lambda p: p["metadata"]["labels"].pop(S.POD_NAME_LABEL)):
+        p = copy.deepcopy(pod)
+        mutate(p)
+        assert not S.identity_matches(ss, p)
+
+
+def test_storage_matches():
+    ss = new_set()
+    pod = S.new_stateful_pod(ss, 1)
+    assert S.storage_matches(ss, pod)
+    p = copy.deepcopy(pod)
+    p["spec"]["volumes"][0]["name"] = "really-bad-name"
+    assert not S.storage_matches(ss, p)
+    p = copy.deepcopy(pod)
+    p["spec"]["volumes"] = []
+    assert not S.storage_matches(ss, p)
+    p = copy.deepcopy(pod)
+    p["spec"]["volumes"][0]["persistentVolumeClaim"]["claimName"] = "really-bad-name"
+    assert not S.storage_matches(ss, p)
+
+
+def test_update_identity():
+    ss = new_set()
+    pod = S.new_stateful_pod(ss, 1)
+    pod["metadata"]["namespace"] = ""
+    assert not S.identity_matches(ss, pod)
+    S.update_identity(ss, pod)
+    assert S.identity_matches(ss, pod)
+    pod["metadata"]["labels"].pop(S.POD_NAME_LABEL)
+    S.update_identity(ss, pod)
+    assert S.identity_matches(ss, pod)
+
+
+def test_update_storage():
+    ss = new_set()
+    pod = S.new_stateful_pod(ss, 1)
+    pod["spec"]["volumes"] = [{"name": "datadir", "emptyDir": {}}, {"name": "scratch", "emptyDir": {}}]
+    assert not S.storage_matches(ss, pod)
+    S.update_storage(ss, pod)
+    assert S.storage_matches(ss, pod)
+    assert {v["name"] for v in pod["spec"]["volumes"]} == {"datadir", "scratch"}   # local volumes kept
+    assert S.claim_name(ss, ss["spec"]["volumeClaimTemplates"][0], 1) == "datadir-foo-1"
+
+
+def test_is_running_and_ready():
+    pod = _pod("foo-0")
+    assert not S.is_running_and_ready(pod)
+    pod["status"] = {"phase": "Running"}
+    assert not S.is_running_and_ready(pod)
+    pod["status"]["conditions"] = [{"type": "Ready", "status": "True"}]
+    assert S.is_running_and_ready(pod)
+
+
+def test_ascending_ordinal():
+    ss = new_set()
+    pods = [S.new_stateful_pod(ss, i) for i in (3, 0, 2, 1)]
+    assert [S.ordinal_of(p) for p in sorted(pods, key=S.ordinal_of)] == [0, 1, 2, 3]
+
+
+def test_new_pod_controller_ref_and_claims():
+    ss = new_set()
+    pod = S.new_stateful_pod(ss, 0)
+    ref = m.controller_of(pod)
+    assert ref["uid"] == "uid-foo" and ref["kind"] == "StatefulSet" and ref["blockOwnerDeletion"]
+    claims = S.persistent_volume_claims(ss, 0)
+    c = claims["datadir"]
+    assert c["metadata"]["name"] == "datadir-foo-0" and c["metadata"]["labels"] == {"foo": "bar"}
+    assert "ownerReferences" not in c["metadata"]          # claims outlive the set
+    assert pod["spec"]["hostname"] == "foo-0" and pod["spec"]["subdomain"] == "governingsvc"
+
+
+def test_create_apply_revision():
+    ss = new_set()
+    rev = {"metadata": {"name": "foo-1"}, "data": {"spec": {"template": copy.deepcopy(ss["spec"]["template"])}}}
+    ss2 = copy.deepcopy(ss)
+    ss2["spec"]["template"]["spec"]["containers"][0]["image"] = "foo"
+    restored = S.apply_revision(ss2, rev)
+    assert restored["spec"]["template"] == ss["spec"]["template"]
+    assert ss2["spec"]["template"]["spec"]["containers"][0]["image"] == "foo"     # input untouched
+
+
+def test_canonical_statefulset_validates():
+    """Round-4 probe: the canonical "web" set (mount of a claim template) was rejected with 422."""
+    ss = new_set(claims=("www",))
+    assert validate_stateful_set(ss) == []
+    bad = copy.deepcopy(ss)
+    bad["spec"]["template"]["spec"]["containers"][0]["volumeMounts"].append({"name": "nope", "mountPath": "/x"})
+    assert any("volumeMounts" in str(e) for e in validate_stateful_set(bad))
+
+
+# -- stateful_set_control_test.go over the fake client ------------------------------------------
+class Harness:
+    def __init__(self, ss):
+        self.key = f"default/{ss['metadata']['name']}"
+        self.c = FakeClient(ss)
+        self.f = InformerFactory(self.c)
+        self.ctl = S.StatefulSetController(self.c, self.f)
+        self.ctl.setup()
+        self.creates, self.deletes = [], []
+        self.c.prepend_reactor("create", "pods", lambda a: (self.creates.append(a.name), (False, None))[1])
+        self.c.prepend_reactor("delete", "pods", lambda a: (self.deletes.append(a.name), (False, None))[1])
+
+    async def start(self):
+        self.f.start()
+        await self.f.wait_for_cache_sync()
+        return self
+
+    async def settle(self):
+        for _ in range(3):
+            await asyncio.sleep(0.002)
+
+    def set(self):
+        return self.ctl.ss_inf.get(self.key)
+
+    def pods(self):
+        return sorted((p for p in self.c.objects.get("pods", {}).values()), key=S.ordinal_of)
+
+    def claims(self):
+        return sorted(p["metadata"]["name"] for p in self.c.objects.get("persistentvolumeclaims", {}).values())
+
+    def revisions(self):
+        return list(self.c.objects.get("controllerrevisions", {}).values())
+
+    async def sync(self):
+        await self.ctl.sync(self.key)
+        await self.settle()
+
+    async def make_ready(self, pod):
+        p = copy.deepcopy(pod)
+        p["status"] = {"phase": "Running", "conditions": [{"type": "Ready", "status": "True"}]}
+        await self.c.update("pods", p, "default")
+
+    async def fail(self, pod):
+        p = copy.deepcopy(pod)
+        p["status"] = {"phase": "Failed"}
+        await self.c.update("pods", p, "default")
+
+    async def update_set(self, fn):
+        ss = copy.deepcopy(self.set())
+        fn(ss)
+        ss["metadata"]["generation"] = ss["metadata"].get("generation", 1) + 1
+        await self.c.update("statefulsets", ss, "default")
+        await self.settle()
+
+    async def converge(self, invariants=None, steps=200):
+        """Sync; bring the lowest not-ready pod up (the kubelet); check invariants; until the set
+        has spec.replicas pods, all Running and Ready and on the update revision (or OnDelete)."""
+        for _ in range(steps):
+            await self.sync()
+            if invariants:
+                invariants(self)
+            pods = self.pods()
+            pending = [p for p in pods if not S.is_running_and_ready(p)]
+            if pending:
+                await self.make_ready(pending[0])
+                await self.settle()
+                continue
+            ss = self.set()
+            st = ss.get("status") or {}
+            want = ss["spec"]["replicas"]
+            # (a pod on the current revision counts as current only, even when current == update:
+            # stateful_set_control.go:293-299)
+            rolled = st.get("currentRevision") == st.get("updateRevision") and st.get("currentReplicas") == want
+            if len(pods) == want and st.get("readyReplicas") == want and st.get("replicas") == want and \
+                    (ss["spec"]["updateStrategy"]["type"] == "OnDelete" or rolled or
+                     (st.get("currentReplicas", 0) + st.get("updatedReplicas", 0) == want and _partitioned(ss))):
+                await self.sync()
+                return
+        raise AssertionError(f"did not converge: {[m.name_of(p) for p in self.pods()]} {self.set().get('status')}")
+
+
+def _partitioned(ss):
+    return int(((ss["spec"]["updateStrategy"].get("rollingUpdate") or {}).get("partition")) or 0) > 0
+
+
+def monotonic_invariants(h):
+    """assertMonotonicInvariants: no Ready successor of an unready pod, ordinals dense, identity and
+    storage hold, every claim exists."""
+    ss, pods = h.set(), h.pods()
+    for i, p in enumerate(pods):
+        if i > 0 and S.is_running_and_ready(p) and not S.is_running_and_ready(pods[i - 1]):
+            raise AssertionError(f"successor {m.name_of(p)} Running and Ready while {m.name_of(pods[i - 1])} is not")
+        assert S.ordinal_of(p) == i, f"pod {m.name_of(p)} deployed in the wrong order"
+        burst_invariants(h, [p])
+
+
+def burst_invariants(h, pods=None):
+    ss = h.set()
+    for p in pods if pods is not None else h.pods():
+        assert S.storage_matches(ss, p) and S.identity_matches(ss, p), m.name_of(p)
+        for c in S.persistent_volume_claims(ss, S.ordinal_of(p)).values():
+            assert c["metadata"]["name"] in h.claims(), f"claim {c['metadata']['name']} missing"
+
+
+def _run(coro_fn, run):
+    async def main():
+        return await coro_fn()
+    return run(main(), timeout=60)
+
+
+@pytest.mark.parametrize("parallel", [False, True], ids=["monotonic", "burst"])
+def test_creates_pods_scales_up_and_down(parallel, run):
+    async def main():
+        h = await Harness(new_set(3, parallel=parallel)).start()
+        inv = burst_invariants if parallel else monotonic_invariants
+        await h.converge(inv)
+        assert [m.name_of(p) for p in h.pods()] == ["foo-0", "foo-1", "foo-2"]
+        assert h.claims() == ["datadir-foo-0", "datadir-foo-1", "datadir-foo-2"]
+        if not parallel:
+            assert h.creates == ["foo-0", "foo-1", "foo-2"]
+        st = h.set()["status"]
+        assert (st["replicas"], st["readyReplicas"], st["currentReplicas"]) == (3, 3, 3)
+        assert st["currentRevision"] == st["updateRevision"] and st["observedGeneration"] == 1
+        # scale up
+        await h.update_set(lambda s: s["spec"].__setitem__("replicas", 4))
+        await h.converge(inv)
+        assert len(h.pods()) == 4
+        # scale down to 0: highest ordinal first, claims kept
+        await h.update_set(lambda s: s["spec"].__setitem__("replicas", 0))
+        for _ in range(20):
+            await h.sync()
+        assert h.pods() == []
+        if not parallel:
+            assert h.deletes == ["foo-3", "foo-2", "foo-1", "foo-0"]
+        assert h.claims() == ["datadir-foo-0", "datadir-foo-1", "datadir-foo-2", "datadir-foo-3"]
+        assert h.set()["status"]["replicas"] == 0
+    run(main(), timeout=60)
+
+
+def test_replaces_deleted_and_failed_pods(run):
+    async def main():
+        h = await Harness(new_set(3)).start()
+        await h.converge(monotonic_invariants)
+        await h.c.delete("pods", "foo-0", "default")
+        await h.c.delete("pods", "foo-2", "default")
+        await h.settle()
+        await h.converge(burst_invariants)      # foo-1 stays Ready while its predecessor is recreated
+        assert [m.name_of(p) for p in h.pods()] == ["foo-0", "foo-1", "foo-2"]
+        # a Failed pod is deleted and recreated
+        await h.fail(h.pods()[1])
+        await h.settle()
+        h.deletes.clear()
+        await h.converge(burst_invariants)
+        assert "foo-1" in h.deletes and all(S.is_running_and_ready(p) for p in h.pods())
+    run(main(), timeout=60)
+
+
+def test_monotonic_waits_for_ready_predecessor(run):
+    async def main():
+        h = await Harness(new_set(3)).start()
+        for _ in range(5):
+            await h.sync()
+        assert [m.name_of(p) for p in h.pods()] == ["foo-0"]       # foo-1 waits for foo-0
+        h2 = await Harness(new_set(3, parallel=True)).start()
+        await h2.sync()
+        assert [m.name_of(p) for p in h2.pods()] == ["foo-0", "foo-1", "foo-2"]
+    run(main(), timeout=30)
+
+
+def _image(p):
+    return p["spec"]["containers"][0]["image"]
+
+
+def update_invariants(h):
+    burst_invariants(h)
+    ss = h.set()
+    st = ss.get("status") or {}
+    if ss["spec"]["updateStrategy"]["type"] != "RollingUpdate":
+        return
+    pods = h.pods()
+    for i in range(min(int(st.get("currentReplicas") or 0), len(pods))):
+        assert S.pod_revision(pods[i]) == st["currentRevision"], m.name_of(pods[i])
+    for j in range(int(st.get("updatedReplicas") or 0)):
+        assert S.pod_revision(pods[len(pods) - 1 - j]) == st["updateRevision"], m.name_of(pods[len(pods) - 1 - j])
+
+
+@pytest.mark.parametrize("parallel", [False, True], ids=["monotonic", "burst"])
+def test_rolling_update(parallel, run):
+    async def main():
+        h = await Harness(new_set(3, parallel=parallel)).start()
+        await h.converge()
+        first = h.set()["status"]["currentRevision"]
+        await h.update_set(lambda s: s["spec"]["template"]["spec"]["containers"][0].__setitem__("image", "foo"))
+        await h.converge(update_invariants)
+        assert [_image(p) for p in h.pods()] == ["foo"] * 3
+        st = h.set()["status"]
+        assert st["currentRevision"] == st["updateRevision"] != first
+        assert st["currentReplicas"] == 3
+        if not parallel:   # replaced from the highest ordinal down
+            assert [d for d in h.deletes] == ["foo-2", "foo-1", "foo-0"]
+    run(main(), timeout=60)
+
+
+@pytest.mark.parametrize("replicas,parallel", [(3, False), (5, False), (3, True)],
+                         ids=["monotonic image update", "monotonic image update and scale up", "burst image update"])
+def test_rolling_update_with_partition(replicas, parallel, run):
+    async def main():
+        h = await Harness(new_set(3, parallel=parallel, strategy={
+            "type": "RollingUpdate", "rollingUpdate": {"partition": 2}})).start()
+        await h.converge()
+        old = h.set()["status"]["currentRevision"]
+
+        def upd(s):
+            s["spec"]["replicas"] = replicas
+            s["spec"]["template"]["spec"]["containers"][0]["image"] = "foo"
+        await h.update_set(upd)
+        await h.converge(update_invariants)
+        pods = h.pods()
+        assert len(pods) == replicas
+        for i, p in enumerate(pods):
+            assert _image(p) == ("nginx" if i < 2 else "foo"), (m.name_of(p), _image(p))
+        st = h.set()["status"]
+        assert st["currentRevision"] == old != st["updateRevision"]
+        assert (st["currentReplicas"], st["updatedReplicas"]) == (2, replicas - 2)
+        # lowering the partition finishes the rollout; the current revision rolls forward
+        await h.update_set(lambda s: s["spec"]["updateStrategy"]["rollingUpdate"].__setitem__("partition", 0))
+        await h.converge(update_invariants)
+        assert [_image(p) for p in h.pods()] == ["foo"] * replicas
+        st = h.set()["status"]
+        assert st["currentRevision"] == st["updateRevision"] and st["currentReplicas"] == replicas
+    run(main(), timeout=60)
+
+
+def test_on_delete_update(run):
+    async def main():
+        h = await Harness(new_set(3, strategy={"type": "OnDelete"})).start()
+        await h.converge()
+        h.deletes.clear()
+        await h.update_set(lambda s: s["spec"]["template"]["spec"]["containers"][0].__setitem__("image", "foo"))
+        for _ in range(5):
+            await h.sync()
+        assert h.deletes == [] and [_image(p) for p in h.pods()] == ["nginx"] * 3
+        st = h.set()["status"]
+        assert st["currentRevision"] != st["updateRevision"] and st["currentReplicas"] == 3
+        # a manually deleted pod comes back at the update revision
+        await h.c.delete("pods", "foo-1", "default")
+        await h.settle()
+        await h.converge()
+        assert [_image(p) for p in h.pods()] == ["nginx", "foo", "nginx"]
+        st = h.set()["status"]
+        assert (st["currentReplicas"], st["updatedReplicas"]) == (2, 1)
+    run(main(), timeout=60)
+
+
+def test_limits_history_and_rollback(run):
+    """TestStatefulSetControlLimitsHistory + TestStatefulSetControlRollback."""
+    async def main():
+        h = await Harness(new_set(2)).start()
+        await h.converge()
+        for img in ("a", "b", "c", "d", "e"):
+            await h.update_set(lambda s, img=img: s["spec"]["template"]["spec"]["containers"][0].__setitem__("image", img))
+            await h.converge()
+            live = {h.set()["status"]["currentRevision"], h.set()["status"]["updateRevision"]} | \
+                {S.pod_revision(p) for p in h.pods()}
+            hist = [r for r in h.revisions() if r["metadata"]["name"] not in live]
+            assert len(hist) <= 2, [r["metadata"]["name"] for r in h.revisions()]
+        revs = sorted(h.revisions(), key=lambda r: r["revision"])
+        assert revs[-1]["data"]["spec"]["template"]["spec"]["containers"][0]["image"] == "e"
+        # roll back to "d": its revision is reused and renumbered as the newest
+        d = next(r for r in revs if r["data"]["spec"]["template"]["spec"]["containers"][0]["image"] == "d")
+        await h.update_set(lambda s: s["spec"]["template"]["spec"]["containers"][0].__setitem__("image", "d"))
+        await h.converge()
+        st = h.set()["status"]
+        assert st["updateRevision"] == d["metadata"]["name"] == st["currentRevision"]
+        newest = max(h.revisions(), key=lambda r: r["revision"])
+        assert newest["metadata"]["name"] == d["metadata"]["name"]
+        assert [_image(p) for p in h.pods()] == ["d", "d"]
+    run(main(), timeout=90)
+
+
+def test_adopts_orphans_and_releases_non_matching(run):
+    async def main():
+        ss = new_set(2, strategy={"type": "OnDelete"})   # no revision label: RollingUpdate would replace it
+        h = await Harness(ss).start()
+        orphan = S.new_stateful_pod(ss, 0)
+        orphan["metadata"].pop("ownerReferences")
+        orphan["status"] = {"phase": "Running", "conditions": [{"type": "Ready", "status": "True"}]}
+        await h.c.create("pods", orphan, "default")
+        await h.settle()
+        await h.converge()
+        p0 = next(p for p in h.pods() if m.name_of(p) == "foo-0")
+        assert m.controller_of(p0)["uid"] == "uid-foo"
+        assert h.creates.count("foo-0") == 1        # adopted, not recreated
+        # relabel -> released; the set cannot recreate foo-1 while the released pod holds the name
+        # (the reference behaves the same: CreateStatefulPod returns AlreadyExists)
+        rel = copy.deepcopy(next(p for p in h.pods() if m.name_of(p) == "foo-1"))
+        rel["metadata"]["labels"]["foo"] = "other"
+        await h.c.update("pods", rel, "default")
+        await h.settle()
+        with pytest.raises(APIStatusError) as ei:     # the name is taken: sync fails and is retried
+            await h.sync()
+        assert ei.value.code == 409
+        got = next(p for p in h.pods() if m.name_of(p) == "foo-1")
+        assert not got["metadata"].get("ownerReferences")
+    run(main(), timeout=60)
+
+
+# -- live cluster -------------------------------------------------------------------------------
+WEB = {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "web", "namespace": "default"},
+       "spec": {"serviceName": "nginx", "replicas": 2, "selector": {"matchLabels": {"app": "nginx"}},
+                "template": {"metadata": {"labels": {"app": "nginx"}},
+                             "spec": {"containers": [{"name": "nginx", "image": "k8s.gcr.io/nginx-slim:0.8",
+                                                      "volumeMounts": [{"name": "www",
+                                                                        "mountPath": "/usr/share/nginx/html"}]}]}},
+                "volumeClaimTemplates": [{"metadata": {"name": "www"}, "spec": {
+                    "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}}]}}
+
+
+def test_web_statefulset_claims_and_partition_live(run, tmp_path):
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=0, controllers=["statefulset", "persistentvolume-binder"],
+                                controller_options={"persistentvolume-binder": {"hostpath_root": str(tmp_path)}}) as cl:
+            c = cl.client
+            await c.create("storageclasses", {"metadata": {"name": "local", "annotations": {
+                "storageclass.kubernetes.io/is-default-class": "true"}}, "provisioner": "kubernetes.io/host-path"})
+            await c.create("statefulsets", copy.deepcopy(WEB))      # no 422
+
+            async def ready(n, image=None):
+                ss = await c.get("statefulsets", "web", "default")
+                st = ss.get("status") or {}
+                ps = (await c.list("pods", "default", label_selector="app=nginx"))["items"]
+                ok = st.get("readyReplicas") == n and len(ps) == n and all(
+                    S.is_running_and_ready(p) and not p["metadata"].get("deletionTimestamp") for p in ps)
+                if ok and image:
+                    ok = all(_image(p) == image for p in ps if m.name_of(p) == f"web-{n - 1}")
+                return (ss, ps) if ok else None
+            ss, pods = await cl.wait_for(lambda: ready(2), timeout=60)
+            claims = {m.name_of(p) for p in (await c.list("persistentvolumeclaims", "default"))["items"]}
+            assert claims == {"www-web-0", "www-web-1"}
+            for p in pods:
+                vol = next(v for v in p["spec"]["volumes"] if v["name"] == "www")
+                assert vol["persistentVolumeClaim"]["claimName"] == f"www-{m.name_of(p)}"
+                assert p["spec"]["hostname"] == m.name_of(p) and p["spec"]["subdomain"] == "nginx"
+            old_rev = ss["status"]["currentRevision"]
+            # partitioned update: ordinal 0 stays on the old revision
+            await c.patch("statefulsets", "web", {"spec": {
+                "updateStrategy": {"type": "RollingUpdate", "rollingUpdate": {"partition": 1}},
+                "template": {"spec": {"containers": [{"name": "nginx", "image": "k8s.gcr.io/nginx-slim:0.9"}]}}}},
+                "default", patch_type="strategic")
+
+            async def partitioned():
+                got = await ready(2, "k8s.gcr.io/nginx-slim:0.9")
+                if not got:
+                    return None
+                ss, ps = got
+                st = ss["status"]
+                return got if st.get("updatedReplicas") == 1 and st.get("currentReplicas") == 1 else None
+            ss, pods = await cl.wait_for(partitioned, timeout=60)
+            by = {m.name_of(p): p for p in pods}
+            assert _image(by["web-0"]) == "k8s.gcr.io/nginx-slim:0.8"
+            assert S.pod_revision(by["web-0"]) == old_rev == ss["status"]["currentRevision"]
+            assert S.pod_revision(by["web-1"]) == ss["status"]["updateRevision"] != old_rev
+    run(main(), timeout=150)
