@@ -155,6 +155,21 @@ def pod_is_ready(pod):
     return False
 
 
+def pod_is_available(pod, min_ready_seconds=0, now=None):
+    """`podutil.IsPodAvailable`: Ready, and Ready for at least minReadySeconds."""
+    for c in (pod.get("status") or {}).get("conditions") or ():
+        if c.get("type") == "Ready":
+            if c.get("status") != "True":
+                return False
+            if not min_ready_seconds:
+                return True
+            since = m.parse_rfc3339(c.get("lastTransitionTime"))
+            if since is None:
+                return False
+            return since + int(min_ready_seconds) < (time.time() if now is None else now)
+    return False
+
+
 def pod_from_template(template, owner, generate_name, namespace):
     tmd = (template or {}).get("metadata") or {}
     pod = {"apiVersion": "v1", "kind": "Pod",

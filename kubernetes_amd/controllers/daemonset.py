@@ -1,18 +1,18 @@
-"""DaemonSet and StatefulSet controllers.
+"""DaemonSet controller.
 
-DaemonSet parity: `pkg/controller/daemon/daemon_controller.go` (nodeShouldRunDaemonPod: node
-selector / affinity / taints-tolerations, one pod per eligible node, delete pods on nodes that
-no longer qualify, status counts). Design choice: instead of the 1.9 behaviour of writing
-`spec.nodeName` directly (`daemon_controller.go:1323` NewPod), each daemon pod is pinned with
-required node affinity on the node's `kubernetes.io/hostname` label (the 1.9 NodeSelectorTerm
-has no `matchFields`; the kubelet sets that label to the node name) and goes through the
-scheduler — so a DaemonSet requesting `amd.com/gpu` (e.g. a per-node GPU burn-in / xGMI probe)
-gets real device IDs allocated.
+Parity: `pkg/controller/daemon/daemon_controller.go` (nodeShouldRunDaemonPod: node selector /
+affinity / taints-tolerations; `manage`: one pod per eligible node, failed pods replaced,
+duplicates and pods on nodes that no longer qualify deleted; `updateDaemonSetStatus`: counts over
+each node's oldest pod, numberAvailable honouring minReadySeconds) and `update.go` (RollingUpdate:
+every old unavailable pod goes at once, old available pods go while fewer than maxUnavailable —
+an int or a percentage of the desired count, rounded up (`getUnavailableNumbers`, `:386-422`) —
+nodes are unavailable; ControllerRevision history with `cleanupHistory`).
 
-StatefulSet parity: `pkg/controller/statefulset/stateful_set_control.go` — ordinal pods
-`<name>-<i>`, OrderedReady (create i only when 0..i-1 are Running and Ready, delete from the
-highest ordinal) or Parallel pod management, RollingUpdate by revision hash in reverse
-ordinal order, status replicas / readyReplicas / currentRevision / updateRevision.
+Design choice: instead of the 1.9 behaviour of writing `spec.nodeName` directly
+(`daemon_controller.go:1323` NewPod), each daemon pod is pinned with required node affinity on the
+node's `kubernetes.io/hostname` label (the 1.9 NodeSelectorTerm has no `matchFields`; the kubelet
+sets that label to the node name) and goes through the scheduler — so a DaemonSet requesting
+`amd.com/gpu` (e.g. a per-node GPU burn-in / xGMI probe) gets real device IDs allocated.
 """
 from __future__ import annotations
 
@@ -22,8 +22,9 @@ from ..api import meta as m
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
 from ..scheduler import predicates as P
 from ..scheduler.cache import NodeInfo, PodInfo
-from .history import REVISION_HASH, ensure_revision, revisions_of
-from .base import Controller, controller_ref, pod_from_template, pod_is_active, pod_is_ready, split_key
+from .deployment_util import value_from_int_or_percent
+from .history import REVISION_HASH, ensure_revision, revisions_of, truncate_history
+from .base import Controller, controller_ref, pod_from_template, pod_is_available, pod_is_ready, split_key
 
 HOSTNAME = "kubernetes.io/hostname"
 
@@ -89,37 +90,69 @@ class DaemonSetController(Controller):
         return None
 
     async def sync(self, key):
+        """`syncDaemonSet` (daemon_controller.go:1090): history, manage, rolling update, history
+        cleanup, status."""
         ds = self.ds_inf.get(key)
-        if ds is None or ds["metadata"].get("deletionTimestamp"):
+        if ds is None:
             return
-        ns, name = split_key(key)
-        pods = [p for p in self.pod_inf.store.by_index("controllerUID", ds["metadata"]["uid"]) if pod_is_active(p)]
-        by_node: dict[str, list] = {}
-        for p in pods:
-            by_node.setdefault(self._target_node(p), []).append(p)
-        want = {n["metadata"]["name"] for n in self.node_inf.list() if node_should_run(ds, n)}
-        creating = self._inflight.setdefault(key, set())
-        creating &= want - set(by_node)
-        tmpl = (ds.get("spec") or {}).get("template") or {}
+        sel = (ds.get("spec") or {}).get("selector") or {}
+        if not (sel.get("matchLabels") or sel.get("matchExpressions")):
+            self.recorder.event(ds, "Warning", "SelectingAll",
+                                "This daemon set is selecting all pods. A non-empty selector is required.")
+            return
         spec = ds.get("spec") or {}
-        rev = await ensure_revision(self.client, ds, "DaemonSet", tmpl,
-                                    revisions_of(self.rev_inf.list(), ds["metadata"]["uid"]),
-                                    int(spec.get("revisionHistoryLimit", 10)))
+        tmpl = spec.get("template") or {}
+        revisions = revisions_of(self.rev_inf.list(), ds["metadata"]["uid"])
+        rev = await ensure_revision(self.client, ds, "DaemonSet", tmpl, revisions, limit=None)
         h = rev["metadata"]["labels"][REVISION_HASH]
-        todo = [n for n in sorted(want) if n not in by_node and n not in creating]
-        dels = [p for node, ps in by_node.items() if node not in want for p in ps]
-        dels += [p for node, ps in by_node.items() if node in want for p in ps[1:]]
-        # RollingUpdate (apps/v1 default): replace pods of older revisions, at most maxUnavailable
-        # (default 1) nodes without a ready pod at a time; OnDelete waits for manual deletion
-        strategy = spec.get("updateStrategy") or {}
-        if strategy.get("type", "RollingUpdate") == "RollingUpdate" and not todo:
-            max_unavail = int(((strategy.get("rollingUpdate") or {}).get("maxUnavailable")) or 1)
-            unavailable = sum(1 for n in want if not any(pod_is_ready(p) for p in by_node.get(n, ())))
-            stale = [ps[0] for node, ps in sorted(by_node.items()) if node in want and ps
-                     and (ps[0]["metadata"].get("labels") or {}).get(REVISION_HASH) != h
-                     and not ps[0]["metadata"].get("deletionTimestamp")]
-            budget = max(0, max_unavail - unavailable)
-            dels += [p for p in stale if not pod_is_ready(p)] + [p for p in stale if pod_is_ready(p)][:budget]
+        nodes = self.node_inf.list()
+        want = {n["metadata"]["name"] for n in nodes if node_should_run(ds, n)}
+        by_node = self.nodes_to_daemon_pods(ds)
+        if not ds["metadata"].get("deletionTimestamp"):
+            await self.manage(ds, key, want, by_node, h)
+            if (spec.get("updateStrategy") or {}).get("type", "RollingUpdate") == "RollingUpdate":
+                await self.rolling_update(ds, want, self.nodes_to_daemon_pods(ds), h)
+            live = {m.name_of(rev)} | {r["metadata"]["name"] for r in revisions
+                                       if (r["metadata"].get("labels") or {}).get(REVISION_HASH) in
+                                       {(p["metadata"].get("labels") or {}).get(REVISION_HASH)
+                                        for ps in by_node.values() for p in ps}}
+            await truncate_history(self.client, revisions, live, int(spec.get("revisionHistoryLimit", 10)))
+        await self.update_status(ds, want, self.nodes_to_daemon_pods(ds), h)
+
+    def nodes_to_daemon_pods(self, ds):
+        out: dict[str, list] = {}
+        for p in self.pod_inf.store.by_index("controllerUID", ds["metadata"]["uid"]):
+            if p["metadata"].get("deletionTimestamp") and (p.get("status") or {}).get("phase") in ("Failed", "Succeeded"):
+                continue
+            out.setdefault(self._target_node(p), []).append(p)
+        for ps in out.values():
+            ps.sort(key=lambda p: (m.parse_rfc3339(p["metadata"].get("creationTimestamp")) or 0, m.name_of(p)))
+        return out
+
+    async def manage(self, ds, key, want, by_node, h):
+        """`manage` / `podsShouldBeOnNode`: one pod per eligible node; failed pods are replaced;
+        duplicates (all but the oldest) and pods on ineligible nodes are deleted."""
+        ns, name = split_key(key)
+        creating = self._inflight.setdefault(key, set())
+        creating &= want - {n for n, ps in by_node.items() if any(not _terminating(p) for p in ps)}
+        todo, dels = [], []
+        for node in sorted(want):
+            pods = by_node.get(node, [])
+            running = []
+            for p in pods:
+                if _terminating(p):
+                    continue
+                if (p.get("status") or {}).get("phase") == "Failed":
+                    self.recorder.event(ds, "Warning", "FailedDaemonPod",
+                                        f"Found failed daemon pod {ns}/{m.name_of(p)} on node {node}, will try to kill it")
+                    dels.append(p)
+                else:
+                    running.append(p)
+            if not running and node not in creating:
+                todo.append(node)
+            dels += running[1:]
+        dels += [p for node, ps in by_node.items() if node not in want for p in ps if not _terminating(p)]
+        tmpl = (ds.get("spec") or {}).get("template") or {}
 
         async def create(node):
             pod = pod_from_template(tmpl, ds, f"{name}-", ns)
@@ -130,27 +163,93 @@ class DaemonSetController(Controller):
             aff["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [
                 {"matchExpressions": [{"key": HOSTNAME, "operator": "In", "values": [node]}]}]}
             creating.add(node)
-            await self.client.create("pods", pod, ns)
-
-        await asyncio.gather(*(create(n) for n in todo), return_exceptions=True)
-        for p in dels:
             try:
-                await self.client.delete("pods", p["metadata"]["name"], ns)
+                await self.client.create("pods", pod, ns)
             except APIStatusError:
-                pass
-        ready = sum(1 for ps in by_node.values() for p in ps if pod_is_ready(p))
-        st = {"desiredNumberScheduled": len(want), "currentNumberScheduled": len([n for n in by_node if n in want]),
-              "numberMisscheduled": len([n for n in by_node if n not in want and n]), "numberReady": ready,
-              "numberAvailable": ready,
-              "updatedNumberScheduled": len([n for n, ps in by_node.items() if n in want and ps and
-                                             (ps[0]["metadata"].get("labels") or {}).get(REVISION_HASH) == h]),
-              "observedGeneration": ds["metadata"].get("generation", 1)}
-        if {k: (ds.get("status") or {}).get(k) for k in st} != st:
+                creating.discard(node)
+                raise
+        res = await asyncio.gather(*(create(n) for n in todo), return_exceptions=True)
+        for p in dels:
+            await self._delete_pod(p)
+        errs = [r for r in res if isinstance(r, Exception)]
+        if errs:
+            self.recorder.event(ds, "Warning", "FailedCreate", f"Error creating: {errs[0]}")
+            raise errs[0]
+
+    async def _delete_pod(self, p):
+        try:
+            await self.client.delete("pods", m.name_of(p), m.namespace_of(p))
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise
+
+    def unavailable_numbers(self, ds, want, by_node):
+        """`getUnavailableNumbers` (update.go:386): (maxUnavailable resolved against the desired
+        count, rounding up; nodes without an available, non-terminating pod)."""
+        mrs = int((ds.get("spec") or {}).get("minReadySeconds") or 0)
+        unavailable = 0
+        for node in want:
+            if not any(pod_is_available(p, mrs) and not _terminating(p) for p in by_node.get(node, ())):
+                unavailable += 1
+        mu = (((ds.get("spec") or {}).get("updateStrategy") or {}).get("rollingUpdate") or {}).get("maxUnavailable", 1)
+        return value_from_int_or_percent(mu, len(want), True), unavailable
+
+    async def rolling_update(self, ds, want, by_node, h):
+        """`rollingUpdate` (update.go:44): delete every old unavailable pod, then old available
+        pods while fewer than maxUnavailable nodes are unavailable."""
+        mrs = int((ds.get("spec") or {}).get("minReadySeconds") or 0)
+        old = [p for ps in by_node.values() for p in ps
+               if (p["metadata"].get("labels") or {}).get(REVISION_HASH) != h]
+        max_unavail, num_unavail = self.unavailable_numbers(ds, want, by_node)
+        dels = [p for p in old if not pod_is_available(p, mrs) and not _terminating(p)]
+        for p in old:
+            if not pod_is_available(p, mrs) or _terminating(p):
+                continue
+            if num_unavail >= max_unavail:
+                break
+            dels.append(p)
+            num_unavail += 1
+        for p in dels:
+            await self._delete_pod(p)
+        return [m.name_of(p) for p in dels]
+
+    async def update_status(self, ds, want, by_node, h):
+        """`updateDaemonSetStatus` (daemon_controller.go:1025): counts over each node's oldest
+        pod; numberAvailable honours minReadySeconds."""
+        mrs = int((ds.get("spec") or {}).get("minReadySeconds") or 0)
+        desired = current = mis = ready = updated = available = 0
+        nodes = {n["metadata"]["name"] for n in self.node_inf.list()}
+        for node in nodes | set(want):
+            pods = by_node.get(node) or []
+            if node in want:
+                desired += 1
+                if pods:
+                    current += 1
+                    pod = pods[0]
+                    if pod_is_ready(pod):
+                        ready += 1
+                        if pod_is_available(pod, mrs):
+                            available += 1
+                    if (pod["metadata"].get("labels") or {}).get(REVISION_HASH) == h:
+                        updated += 1
+            elif pods:
+                mis += 1
+        st = {"desiredNumberScheduled": desired, "currentNumberScheduled": current, "numberMisscheduled": mis,
+              "numberReady": ready, "numberAvailable": available, "numberUnavailable": desired - available,
+              "updatedNumberScheduled": updated, "observedGeneration": ds["metadata"].get("generation", 1)}
+        if mrs and ready != available:
+            self.queue.add_after(m.ns_name(ds), float(mrs))
+        if {k: (ds.get("status") or {}).get(k, 0) for k in st} != st:
             try:
-                await self.client.patch("daemonsets", name, {"status": st}, ns, "merge", "status")
+                await self.client.patch("daemonsets", m.name_of(ds), {"status": st}, m.namespace_of(ds),
+                                        "merge", "status")
             except APIStatusError as e:
                 if not is_not_found(e):
                     raise
+
+
+def _terminating(p):
+    return bool(p["metadata"].get("deletionTimestamp"))
 
 
 from .statefulset import StatefulSetController  # noqa: E402,F401  (re-export)

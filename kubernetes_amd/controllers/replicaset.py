@@ -12,7 +12,8 @@ import asyncio
 from ..api import meta as m
 from ..api.labels import selector_from_set
 from ..client.rest import APIStatusError, is_not_found
-from .base import Controller, Expectations, controller_ref, pod_from_template, pod_is_active, pod_is_ready, selector_of, split_key
+from .base import (Controller, Expectations, controller_ref, pod_from_template, pod_is_active, pod_is_available,
+                   pod_is_ready, selector_of, split_key)
 
 BURST = 500  # slowStartBatch upper bound per sync
 
@@ -104,9 +105,15 @@ class ReplicaSetController(Controller):
                 except APIStatusError:
                     pass
         active = [p for p in owned if pod_is_active(p)]
+        err = None
         if self.exp.satisfied(key) and not rs["metadata"].get("deletionTimestamp"):
-            await self._manage(rs, active, key)
-        await self._update_status(rs, owned, active)
+            try:
+                await self._manage(rs, active, key)
+            except APIStatusError as e:
+                err = e
+        await self._update_status(rs, owned, active, err)
+        if err is not None:
+            raise err
 
     async def _manage(self, rs, active, key):
         ns = rs["metadata"]["namespace"]
@@ -148,15 +155,32 @@ class ReplicaSetController(Controller):
             await asyncio.gather(*(rm(p) for p in victims))
             self.recorder.event(rs, "Normal", "SuccessfulDelete", f"Deleted {len(victims)} pods")
 
-    async def _update_status(self, rs, owned, active):
+    async def _update_status(self, rs, owned, active, manage_err=None):
         tmpl_labels = ((rs.get("spec") or {}).get("template") or {}).get("metadata", {}).get("labels") or {}
         ready = [p for p in active if pod_is_ready(p)]
+        # availableReplicas: Ready for minReadySeconds (replica_set_utils.go calculateStatus)
+        mrs = int((rs.get("spec") or {}).get("minReadySeconds") or 0)
+        available = sum(1 for p in ready if pod_is_available(p, mrs))
         st = {"replicas": len(active),
               "fullyLabeledReplicas": sum(1 for p in active if all((p["metadata"].get("labels") or {}).get(k) == v for k, v in tmpl_labels.items())),
-              "readyReplicas": len(ready), "availableReplicas": len(ready),
+              "readyReplicas": len(ready), "availableReplicas": available,
               "observedGeneration": rs["metadata"].get("generation", 1)}
+        if mrs and len(ready) != available:
+            # look again once the newest ready pod has been ready for minReadySeconds
+            self.queue.add_after(m.ns_name(rs), float(mrs))
         cur = rs.get("status") or {}
-        if all(cur.get(k, 0) == v for k, v in st.items()):
+        # ReplicaFailure while pods cannot be created / deleted (replica_set_utils.go:105-118)
+        conds = [c for c in cur.get("conditions") or ()]
+        failure = next((c for c in conds if c.get("type") == "ReplicaFailure"), None)
+        if manage_err is not None and failure is None:
+            reason = "FailedCreate" if len(active) < int((rs.get("spec") or {}).get("replicas", 1)) else "FailedDelete"
+            conds = conds + [{"type": "ReplicaFailure", "status": "True", "reason": reason,
+                              "message": str(manage_err), "lastTransitionTime": m.now_rfc3339()}]
+        elif manage_err is None and failure is not None:
+            conds = [c for c in conds if c.get("type") != "ReplicaFailure"]
+        if conds != (cur.get("conditions") or []):
+            st["conditions"] = conds or None
+        if all(cur.get(k, 0) == v for k, v in st.items() if k != "conditions") and "conditions" not in st:
             return
         try:
             await self.client.patch(self.resource, rs["metadata"]["name"], {"status": st}, rs["metadata"]["namespace"], "merge", "status")
