@@ -595,11 +595,20 @@ def message_of(obj) -> str | None:
     return schema().message_for(obj.get("apiVersion", "v1") or "v1", obj.get("kind", ""))
 
 
+_SUPPORTED: dict = {}
+
+
 def supported(kind: str, api_version: str = "") -> bool:
-    s = schema()
-    if api_version:
-        return s.message_for(api_version, kind) is not None
-    return any(k.rsplit("/", 1)[-1] == kind for k in s.kinds)
+    key = (kind, api_version)
+    r = _SUPPORTED.get(key)
+    if r is None:
+        s = schema()
+        if api_version:
+            r = s.message_for(api_version, kind) is not None
+        else:
+            r = any(k.rsplit("/", 1)[-1] == kind for k in s.kinds)
+        _SUPPORTED[key] = r
+    return r
 
 
 _NAT = []
@@ -676,3 +685,44 @@ def decode_storage(data):
     if ri is not None and obj.get("apiVersion") != ri.group_version:
         obj["apiVersion"] = ri.group_version      # stored in another version of the same type
     return obj
+
+
+# -- protobuf watch streams (`application/vnd.kubernetes.protobuf;stream=watch`) ----------------
+WATCH_STREAM = "application/vnd.kubernetes.protobuf;stream=watch"
+
+
+def envelope_with_rv(envelope: bytes, rv: str):
+    """The stored envelope with metadata.resourceVersion set (etcd3 stores objects without
+    it), or None when it is not a protobuf envelope of a known kind."""
+    if envelope[:4] != b"k8s\x00":
+        return None
+    return _native_codec().with_rv(envelope, rv)
+
+
+def to_json(envelope: bytes, rv) -> bytes:
+    """A stored envelope as the object's JSON bytes with metadata.resourceVersion = rv."""
+    nat = _native()
+    if nat is not None:
+        return nat.to_json(envelope, str(rv))
+    from .codec import dumpb
+    obj = decode_object(envelope)
+    obj.setdefault("metadata", {})["resourceVersion"] = str(rv)
+    return dumpb(obj)
+
+
+def watch_frame(etype: str, raw: bytes) -> bytes:
+    """One length-delimited metav1.WatchEvent frame (4-byte big-endian length) embedding `raw`
+    (`runtime/serializer/protobuf/protobuf.go:436`, `endpoints/handlers/watch.go:166-226`)."""
+    return _native_codec().watch_frame(etype, raw)
+
+
+def decode_watch_frames(buf):
+    """([(type, object)], bytes consumed) for the complete frames at the start of `buf`."""
+    return _native_codec().decode_watch_frames(buf)
+
+
+def _native_codec():
+    nat = _native()
+    if nat is None:
+        raise ProtobufError("protobuf watch streams need the native codec (native/pbcodec)")
+    return nat

@@ -26,18 +26,53 @@ ADDED, MODIFIED, DELETED, BOOKMARK, ERROR = "ADDED", "MODIFIED", "DELETED", "BOO
 class Entry:
     """One cached object version. `obj` may be decoded lazily: an API server worker that only
     relays another worker's write needs the raw bytes (GET/LIST/watch payload) and the index
-    fields/labels (watch + list filtering) — not the decoded object."""
-    __slots__ = ("_obj", "raw", "rev", "fields", "labels")
+    fields/labels (watch + list filtering) — not the decoded object. `pbv`: the stored protobuf
+    envelope when there is one (without resourceVersion, as etcd3 stores it); `pb_envelope()`
+    is what protobuf watchers are sent."""
+    __slots__ = ("_obj", "_raw", "rev", "fields", "labels", "pbv", "_pb")
 
-    def __init__(self, obj, raw, rev, fields, labels=None):
-        self._obj, self.raw, self.rev, self.fields = obj, raw, rev, fields
+    def __init__(self, obj, raw, rev, fields, labels=None, pbv=None):
+        # raw may be None when pbv is set: the JSON form is then made on first use (a write
+        # answered to a protobuf client never needs it)
+        self._obj, self._raw, self.rev, self.fields = obj, raw, rev, fields
         self.labels = labels if obj is None else ((obj.get("metadata") or {}).get("labels") or {})
+        self.pbv = pbv
+        self._pb = None
+
+    @property
+    def raw(self):
+        r = self._raw
+        if r is None:
+            from ..api import protobuf as pb
+            r = self._raw = pb.to_json(self.pbv, self.rev) if self.pbv is not None else codec.dumpb(self._obj)
+        return r
+
+    def pb_envelope(self):
+        """The object as a `k8s\\x00` protobuf envelope with its resourceVersion, or its JSON bytes
+        for kinds outside the protobuf schema (a protobuf watch embeds those as-is; clients tell
+        them apart by the magic)."""
+        b = self._pb
+        if b is None:
+            from ..api import protobuf as pb
+            if self.pbv is not None:
+                b = pb.envelope_with_rv(self.pbv, str(self.rev))
+            if b is None:
+                o = self.obj
+                b = pb.encode_object(o) if pb.supported(o.get("kind", ""), o.get("apiVersion") or "v1") else self.raw
+            self._pb = b
+        return b
 
     @property
     def obj(self):
         o = self._obj
         if o is None:
-            o = self._obj = codec.loads(self.raw)
+            if self._raw is None and self.pbv is not None:
+                from ..api import protobuf as pb
+                o = pb.decode_storage(self.pbv)
+                o.setdefault("metadata", {})["resourceVersion"] = str(self.rev)
+            else:
+                o = codec.loads(self.raw)
+            self._obj = o
         return o
 
     @property
@@ -94,7 +129,7 @@ FIELD_FUNCS = {"pods": pod_fields, "nodes": node_fields}
 
 class Watcher:
     __slots__ = ("writer", "namespace", "label_sel", "field_sel", "closed", "index_value", "cache", "bookmarks",
-                 "_pending", "_loop", "min_rev", "shard")
+                 "_pending", "_loop", "min_rev", "shard", "pb")
 
     def __init__(self, cache, writer, namespace, label_sel, field_sel, index_value):
         self.cache = cache
@@ -111,6 +146,10 @@ class Watcher:
         self.bookmarks = False
         self._pending = None   # events coalesced until the end of this loop iteration
         self._loop = None
+        self.pb = False        # protobuf watch stream (length-delimited WatchEvent frames)
+
+    def event(self, etype, entry):
+        return pb_event_bytes(etype, entry) if self.pb else event_bytes(etype, entry.raw)
 
     def matches(self, e: Entry) -> bool:
         if self.namespace and e.fields.get("metadata.namespace") != self.namespace:
@@ -160,6 +199,19 @@ class Watcher:
 
 def event_bytes(etype: str, raw: bytes) -> bytes:
     return b'{"type":"' + etype.encode() + b'","object":' + raw + b"}\n"
+
+
+def pb_event_bytes(etype: str, entry: Entry) -> bytes:
+    """One `application/vnd.kubernetes.protobuf;stream=watch` frame (watch.go:166-226)."""
+    from ..api import protobuf as pb
+    return pb.watch_frame(etype, entry.pb_envelope())
+
+
+def error_event(status: dict, protobuf=False) -> bytes:
+    if protobuf:
+        from ..api import protobuf as pb
+        return pb.watch_frame(ERROR, codec.dumpb(status))
+    return codec.dumpb({"type": ERROR, "object": status}) + b"\n"
 
 
 class ResourceCache:
@@ -218,10 +270,10 @@ class ResourceCache:
     def _dispatch(self, etype, entry, prev):
         data = {}
 
-        def enc(t):
-            b = data.get(t)
+        def enc(t, pbw=False):
+            b = data.get((t, pbw))
             if b is None:
-                b = data[t] = event_bytes(t, entry.raw)
+                b = data[(t, pbw)] = pb_event_bytes(t, entry) if pbw else event_bytes(t, entry.raw)
             return b
 
         if self.indexed:
@@ -241,33 +293,34 @@ class ResourceCache:
             was = prev is not None and w.matches(prev)
             if etype == ADDED:
                 if cur:
-                    w.send(enc(ADDED))
+                    w.send(enc(ADDED, w.pb))
             elif etype == MODIFIED:
                 if cur and was:
-                    w.send(enc(MODIFIED))
+                    w.send(enc(MODIFIED, w.pb))
                 elif cur:
-                    w.send(enc(ADDED))
+                    w.send(enc(ADDED, w.pb))
                 elif was:
-                    w.send(enc(DELETED))
+                    w.send(enc(DELETED, w.pb))
             else:  # DELETED
                 if w.matches(entry) or was:
-                    w.send(enc(DELETED))
+                    w.send(enc(DELETED, w.pb))
 
     # -- watchers ---------------------------------------------------------
     def add_watcher(self, writer, namespace, label_selector, field_selector, from_rev: int | None, send_initial: bool,
-                    shard=None):
+                    shard=None, protobuf=False):
         ls = parse_labels(label_selector) if label_selector else None
         fs = parse_field_selector(field_selector) if field_selector else None
         idx = fs.requires("spec.nodeName") if (fs is not None and self.resource == "pods") else None
         w = Watcher(self, writer, namespace, ls, fs, idx)
         w.shard = shard
+        w.pb = protobuf
         if from_rev is not None and not send_initial:
             w.min_rev = from_rev
         # initial state / replay (synchronous, so no event can interleave)
         if send_initial:
             for e in self.by_key.values():
                 if w.matches(e):
-                    w.send(event_bytes(ADDED, e.raw))
+                    w.send(w.event(ADDED, e))
         elif from_rev is not None:
             if self.events and from_rev < self.events[0][0] - 1 and len(self.events) == self.events.maxlen:
                 raise GoneError(f"too old resource version: {from_rev} ({self.events[0][0] - 1})")
@@ -278,11 +331,11 @@ class ResourceCache:
                 was = prev is not None and w.matches(prev)
                 if etype == DELETED:
                     if w.matches(entry) or was:
-                        w.send(event_bytes(DELETED, entry.raw))
+                        w.send(w.event(DELETED, entry))
                 elif cur:
-                    w.send(event_bytes(MODIFIED if (was and etype == MODIFIED) else ADDED, entry.raw))
+                    w.send(w.event(MODIFIED if (was and etype == MODIFIED) else ADDED, entry))
                 elif was:
-                    w.send(event_bytes(DELETED, entry.raw))
+                    w.send(w.event(DELETED, entry))
         self.watchers.add(w)
         if idx is not None:
             self.indexed.setdefault(idx, set()).add(w)

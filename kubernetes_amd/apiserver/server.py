@@ -49,7 +49,7 @@ from ..utils.patch import JSONPatchError, apply_patch
 from . import impersonation
 from . import admission as adm
 from .auth import ANONYMOUS, AttributesRecord, TokenAuthenticator, User, build_authorizer
-from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, event_bytes
+from .cacher import ADDED, DELETED, MODIFIED, Entry, GoneError, ResourceCache, error_event, event_bytes, pb_event_bytes
 from .registry import (APIError, already_exists, apply_binding, bad_request, conflict, deletion_stamp,
                        init_object_meta, invalid, not_found, strategy_for)
 
@@ -77,6 +77,20 @@ VERSION = {"major": "1", "minor": "9", "gitVersion": "v1.9.0-amd.0", **_build_in
            "goVersion": "n/a", "compiler": "cpython"}
 
 _READ_VERBS = {"GET": "get", "HEAD": "get"}
+
+
+def _body(req):
+    """The request body as an object: decoded from protobuf already, or JSON."""
+    return req.obj if req.obj is not None else codec.loads(req.body)
+
+
+def _entry_resp(req, ri, status, e):
+    """A cached object as the response body: its protobuf envelope when the client negotiated
+    protobuf (no JSON made or parsed), else its JSON bytes."""
+    if req.served_gv is None and codec.PROTOBUF in req.headers.get("accept", "") and \
+            "as=Table" not in req.headers.get("accept", "") and pb.supported(ri.kind, ri.group_version):
+        return Response(status, e.pb_envelope(), codec.PROTOBUF)
+    return Response(status, e.raw, entry=e)
 
 
 def _json(status, obj):
@@ -181,12 +195,7 @@ _FRAME = b"\x00KH"                 # shared-store value framing (index header + 
 
 def pb_to_json(body, rev) -> bytes:
     """A protobuf-stored object (k8s\\0 envelope) as JSON bytes with resourceVersion = rev."""
-    nat = pb._native()
-    if nat is not None:
-        return nat.to_json(body, str(rev))
-    obj = pb.decode_object(body)
-    obj.setdefault("metadata", {})["resourceVersion"] = str(rev)
-    return codec.dumpb(obj)
+    return pb.to_json(body, rev)
 
 
 def _requested_gv(path):
@@ -564,9 +573,10 @@ class APIServer:
             fields, labels = codec.loads(v[7:7 + hl])
             body = v[7 + hl:]
             if body[:4] == codec.MAGIC:
-                # protobuf storage: JSON for GET/LIST/watch payloads, resourceVersion from the
-                # key's mod revision (etcd3 never stores it)
-                body = pb_to_json(body, kv.mod_rev)
+                # protobuf storage: the JSON for GET/LIST/watch payloads (resourceVersion from the
+                # key's mod revision — etcd3 never stores it) is made on first use; protobuf
+                # clients get the envelope itself
+                return Entry(None, None, kv.mod_rev, fields, labels, body)
             return Entry(None, body, kv.mod_rev, fields, labels)
         obj, raw = self._decode_value(kv)
         return self.caches[plural].make_entry(obj, raw, kv.mod_rev)
@@ -768,15 +778,18 @@ class APIServer:
         def on_ok(rev):
             rs = str(rev)
             md["resourceVersion"] = rs
+            pbv = None
             if raw_t is not None:
                 raw = raw_t.replace(tok, rs.encode())
-            elif not sealed:
-                # what every other worker (and the store's fan-out) will serve for this revision:
-                # the stored protobuf's JSON form (Go omitempty: no empty maps / lists)
-                raw = pb_to_json(stored[len(frame):], rev) if etype != DELETED else codec.dumpb(obj)
+            elif not sealed and etype != DELETED:
+                # what every other worker (and the store's fan-out) serves for this revision: the
+                # stored envelope (protobuf clients) or its JSON form (Go omitempty: no empty maps
+                # / lists), made only if a JSON client asks (Entry.raw)
+                raw, pbv = None, stored[len(frame):]
             else:
                 raw = codec.dumpb(obj)
             entry = cache.make_entry(obj, raw, rev)
+            entry.pbv = pbv
             if not uncached:
                 self._mine[(key, rev)] = entry
             done.append(entry)
@@ -1470,9 +1483,10 @@ class APIServer:
                 code = 200
                 return Response(200, self.openapi.get(schemas), "application/json")
             if req.body and req.headers.get("content-type", "").startswith(codec.PROTOBUF):
-                # protobuf request bodies (`application/vnd.kubernetes.protobuf`, k8s\0 envelope)
+                # protobuf request bodies (`application/vnd.kubernetes.protobuf`, k8s\0 envelope):
+                # decoded once, natively; handlers take the object (`_body`)
                 try:
-                    req.body = codec.dumpb(pb.decode_object(req.body))
+                    req.obj = pb.decode_object(req.body)
                 except pb.ProtobufError as e:
                     raise APIError(415, "UnsupportedMediaType", str(e))
             if p.startswith("/api/v1/proxy/"):
@@ -1497,7 +1511,7 @@ class APIServer:
                 return resp
             if parsed[0] == "bindings":
                 resource, sub = "pods", "binding"
-                body = codec.loads(req.body)
+                body = _body(req)
                 self._authorize(user, "create", parsed[1], "pods", "binding", m.name_of(body), "", p)
                 await self._retrying(lambda: self.bind(parsed[1], m.name_of(body), body, user))
                 code = 201
@@ -1508,7 +1522,10 @@ class APIServer:
             if served != ri.group_version:
                 # served under an alias group/version: store canonical, answer in the requested one
                 req.served_gv = served
-                if req.body and req.body[:1] == b"{":
+                if req.obj is not None:
+                    if req.obj.get("apiVersion") == served:
+                        req.obj["apiVersion"] = ri.group_version
+                elif req.body and req.body[:1] == b"{":
                     try:
                         bo = codec.loads(req.body)
                         if bo.get("apiVersion") == served:
@@ -1576,9 +1593,15 @@ class APIServer:
                     resp = _json(200, to_table(codec.loads(resp.body), ri.kind, q_include(req)))
                     return resp
             if codec.PROTOBUF in req.headers.get("accept", "") and isinstance(resp, Response) and resp.body[:1] == b"{":
-                obj = codec.loads(resp.body)
-                if pb.supported(obj.get("kind", "")):
-                    resp = Response(resp.status, pb.encode_object(obj), codec.PROTOBUF)
+                e = resp.entry
+                if e is not None and gv in (None, ri.group_version) and pb.supported(ri.kind, ri.group_version):
+                    # the cached object's envelope (the stored bytes + resourceVersion when this
+                    # worker has them): no JSON decode, no re-encode from a dict
+                    resp = Response(resp.status, e.pb_envelope(), codec.PROTOBUF)
+                else:
+                    obj = codec.loads(resp.body)
+                    if pb.supported(obj.get("kind", "")):
+                        resp = Response(resp.status, pb.encode_object(obj), codec.PROTOBUF)
             return resp
         except APIError as e:
             code = e.code
@@ -1654,30 +1677,30 @@ class APIServer:
             if q.get("export") in ("true", "1"):
                 from .registry import export_object
                 return _json(200, export_object(self.strategies[ri.plural], e.obj, q.get("exact") in ("true", "1")))
-            return Response(200, e.raw)
+            return _entry_resp(req, ri, 200, e)
         body = req.body
         if method == "POST":
             if name is not None and sub == "binding" and ri.plural == "pods":
                 self._authorize(user, "create", ns, "pods", "binding", name, "", req.path)
-                await self.bind(ns, name, codec.loads(body), user)
+                await self.bind(ns, name, _body(req), user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None and sub in ("exec", "attach", "portforward") and ri.plural == "pods":
                 self._authorize(user, "create", ns, "pods", sub, name, "", req.path)
                 return await self._pod_stream(req, ns, name, sub)
             if name is not None and sub == "eviction" and ri.plural == "pods":
                 self._authorize(user, "create", ns, "pods", "eviction", name, "", req.path)
-                await self.evict(ns, name, codec.loads(body) if body else {}, user)
+                await self.evict(ns, name, _body(req) if body else {}, user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None:
                 raise APIError(405, "MethodNotAllowed", "POST to a named resource is not allowed")
             if ri.plural in m.VIRTUAL:
-                return self._review(ri, ns, codec.loads(body), user, req)
+                return self._review(ri, ns, _body(req), user, req)
             self._authorize(user, "create", ns, ri.plural, "", "", ri.group, req.path)
-            obj = codec.loads(body)
+            obj = _body(req)
             if ri.namespaced and ns is None:
                 ns = (obj.get("metadata") or {}).get("namespace") or "default"
             e = await self.create(ri, ns, obj, user)
-            return Response(201, e.raw)
+            return _entry_resp(req, ri, 201, e)
         if name is None:
             if method == "DELETE":
                 return await self._delete_collection(req, ri, ns, user)
@@ -1685,23 +1708,23 @@ class APIServer:
         if method == "PUT":
             if ri.plural == "namespaces" and sub == "finalize":
                 self._authorize(user, "update", None, "namespaces", "finalize", name, "", req.path)
-                return await self._finalize_namespace(name, codec.loads(body), user)
+                return await self._finalize_namespace(name, _body(req), user)
             self._authorize(user, "update", ns, ri.plural, sub, name, ri.group, req.path)
-            e = await self.update(ri, ns, name, codec.loads(body), user, sub)
-            return Response(200, e.raw)
+            e = await self.update(ri, ns, name, _body(req), user, sub)
+            return _entry_resp(req, ri, 200, e)
         if method == "PATCH":
             self._authorize(user, "patch", ns, ri.plural, sub, name, ri.group, req.path)
             e = await self.patch(ri, ns, name, req.headers.get("content-type", "application/merge-patch+json"), body, user, sub)
-            return Response(200, e.raw)
+            return _entry_resp(req, ri, 200, e)
         if method == "DELETE":
             self._authorize(user, "delete", ns, ri.plural, "", name, ri.group, req.path)
-            opts = codec.loads(body) if body else {}
+            opts = _body(req) if body else {}
             if "gracePeriodSeconds" in q:
                 opts["gracePeriodSeconds"] = int(q["gracePeriodSeconds"])
             if "propagationPolicy" in q:
                 opts["propagationPolicy"] = q["propagationPolicy"]
             e, _ = await self.delete(ri, ns, name, opts, user)
-            return Response(200, e.raw)
+            return _entry_resp(req, ri, 200, e)
         raise APIError(405, "MethodNotAllowed", f"method {method} not allowed")
 
     def _review(self, ri, ns, body, user, req):
@@ -1858,7 +1881,24 @@ class APIServer:
             reqs.append((0, "shard", SHARD_OFFSET_LABEL, [shard[1], shard[0]]))
         return reqs
 
-    def _watch_store(self, ri, ns, label_selector, field_selector, rv, timeout, shard=None):
+    @staticmethod
+    def _wants_pb_watch(req, ri):
+        """Content negotiation of a watch (`negotiation.NegotiateOutputStreamSerializer`): the
+        first media type of the Accept header this server streams decides; protobuf only for
+        kinds in the protobuf schema, served in their storage group/version."""
+        accept = req.headers.get("accept", "")
+        if "protobuf" not in accept:
+            return False
+        for part in accept.split(","):
+            mt = part.split(";", 1)[0].strip().lower()
+            if mt == codec.PROTOBUF:
+                gv = getattr(req, "served_gv", None)
+                return (gv is None or gv == ri.group_version) and pb.supported(ri.kind, ri.group_version)
+            if mt in (codec.JSON, "*/*", "application/*"):
+                return False
+        return False
+
+    def _watch_store(self, ri, ns, label_selector, field_selector, rv, timeout, shard=None, protobuf=False):
         """Watch of an uncached resource that the store's fan-out cannot serve (a TLS client,
         quantity label selectors): a store watch of its own, filtered here. Without the previous
         object state, a change that leaves the selector is reported as DELETED even if the
@@ -1873,6 +1913,9 @@ class APIServer:
             return (ls is None or ls.matches(e.labels)) and (fs is None or fs.matches(e.fields)) and \
                 (shard is None or shard_matches(e.fields, e.labels, *shard))
 
+        def ev(t, e):
+            return pb_event_bytes(t, e) if protobuf else event_bytes(t, e.raw)
+
         async def run(writer):
             st = await connect_store(server.remote_address, server.etcd_tls)
             done = asyncio.get_running_loop().create_future()
@@ -1884,7 +1927,7 @@ class APIServer:
                         e = server._entry_from_kv(ri.plural, kv)
                         if ok(e):
                             seen[kv.key] = True
-                            writer.write(event_bytes(ADDED, e.raw))
+                            writer.write(ev(ADDED, e))
                 else:
                     frm = int(rv)
 
@@ -1900,18 +1943,18 @@ class APIServer:
                     was = seen.get(kv.key, kv.version > 1 or t == wire.OP_DELETE)
                     if t == wire.OP_DELETE:
                         if was or ok(e):
-                            writer.write(event_bytes(DELETED, e.raw))
+                            writer.write(ev(DELETED, e))
                         seen.pop(kv.key, None)
                     elif cur:
-                        writer.write(event_bytes(MODIFIED if was and kv.version > 1 else ADDED, e.raw))
+                        writer.write(ev(MODIFIED if was and kv.version > 1 else ADDED, e))
                         seen[kv.key] = True
                     elif was:
-                        writer.write(event_bytes(DELETED, e.raw))
+                        writer.write(ev(DELETED, e))
                         seen[kv.key] = False
                 try:
                     await st.watch(prefix, frm, on_event)
                 except CompactedError:
-                    writer.write(codec.dumpb({"type": "ERROR", "object": m.status_obj(410, "Expired", f"too old resource version: {frm}")}) + b"\n")
+                    writer.write(error_event(m.status_obj(410, "Expired", f"too old resource version: {frm}"), protobuf))
                     return
                 server.m_watchers.labels(ri.kind).inc()
                 try:
@@ -1923,7 +1966,7 @@ class APIServer:
             finally:
                 await st.close()
 
-        return StreamResponse(run)
+        return StreamResponse(run, pb.WATCH_STREAM if protobuf else "application/json")
 
     def _watch(self, req, ri, ns, name):
         q = req.query
@@ -1938,15 +1981,18 @@ class APIServer:
             import random
             timeout = self.min_request_timeout * (1.0 + random.random())
         shard = self._shard(q)
+        protobuf = self._wants_pb_watch(req, ri)
         reqs = self._fanout_spec(req, ri, ns, q.get("labelSelector"), fsel, shard)
         if reqs is not None:
-            # shared-store mode: the store streams this watch itself (C++ fan-out)
+            # shared-store mode: the store streams this watch itself (C++ fan-out), JSON lines or
+            # protobuf frames
             send_initial = not rv or rv == "0"
-            msg = self.fanout.encode(m.prefix_for(ri, ns), send_initial, 0 if send_initial else int(rv), timeout, reqs)
+            msg = self.fanout.encode(m.prefix_for(ri, ns), send_initial, 0 if send_initial else int(rv), timeout, reqs,
+                                     protobuf=protobuf)
             self.m_fanout.labels(ri.plural).inc()
             return HandoffResponse(lambda fd: self.fanout.handoff(fd, msg))
         if ri.plural in self.uncached:
-            return self._watch_store(ri, ns, q.get("labelSelector"), fsel, rv, timeout, shard)
+            return self._watch_store(ri, ns, q.get("labelSelector"), fsel, rv, timeout, shard, protobuf)
         cache = self.caches[ri.plural]
         send_initial = not rv or rv == "0"
         from_rev = int(rv) if rv and rv != "0" else None
@@ -1957,9 +2003,9 @@ class APIServer:
 
         async def run(writer):
             try:
-                w = cache.add_watcher(writer, ns, q.get("labelSelector"), fsel, from_rev, send_initial, shard)
+                w = cache.add_watcher(writer, ns, q.get("labelSelector"), fsel, from_rev, send_initial, shard, protobuf)
             except GoneError as e:
-                writer.write(codec.dumpb({"type": "ERROR", "object": m.status_obj(410, "Expired", str(e))}) + b"\n")
+                writer.write(error_event(m.status_obj(410, "Expired", str(e)), protobuf))
                 return
             server.m_watchers.labels(ri.kind).inc()
             try:
@@ -1974,7 +2020,7 @@ class APIServer:
                 w.stop()
                 server.m_watchers.labels(ri.kind).dec()
 
-        return StreamResponse(run)
+        return StreamResponse(run, pb.WATCH_STREAM if protobuf else "application/json")
 
     async def _kubelet_of(self, ns, name):
         """(pod, kubelet host, kubelet port) — the node connection info the reference resolves in

@@ -164,8 +164,11 @@ class HTTPClient:
         status, hdrs = await _read_response(conn.reader)
         return status, hdrs, conn.reader, conn.writer
 
-    async def stream(self, method, path, headers=None):
-        """Open a streaming GET; returns (status, async iterator of line batches, closer)."""
+    async def stream(self, method, path, headers=None, frames=None):
+        """Open a streaming GET; returns (status, async iterator of batches, closer, content
+        type). A batch is a list of complete lines — or, when the response is a
+        length-delimited stream (`...;stream=watch` protobuf) and `frames` is given, whatever
+        `frames(buffer) -> (items, bytes consumed)` makes of the complete frames received."""
         conn = await self._open()
         conn.writer.write(self._head(method, path, None, None, headers))
         status, hdrs = await _read_response(conn.reader)
@@ -174,12 +177,14 @@ class HTTPClient:
             conn.close()
             raise HTTPError(status, body)
         chunked = hdrs.get("transfer-encoding", "").lower() == "chunked"
+        ctype = hdrs.get("content-type", "")
+        framed = frames is not None and "stream=watch" in ctype and "protobuf" in ctype
         reader = conn.reader
 
         async def batches():
-            """Lists of complete lines: everything that arrived in one read is parsed and handed
-            over at once (a watch server coalesces events per send), so a consumer pays one
-            await per batch, not per event."""
+            """Lists of complete lines (or frames): everything that arrived in one read is
+            parsed and handed over at once (a watch server coalesces events per send), so a
+            consumer pays one await per batch, not per event."""
             raw = bytearray()
             pay = bytearray()
             done = False
@@ -208,6 +213,14 @@ class HTTPClient:
                             del raw[:pos]
                     else:
                         pay += data
+                    if framed:
+                        if len(pay) >= 4:
+                            items, used = frames(pay)
+                            if used:
+                                del pay[:used]
+                            if items:
+                                yield items
+                        continue
                     k = pay.rfind(b"\n")
                     if k >= 0:
                         out = [ln for ln in bytes(pay[:k]).split(b"\n") if ln.strip()]
@@ -217,7 +230,7 @@ class HTTPClient:
             except (ConnectionError, asyncio.IncompleteReadError, OSError, ValueError):
                 return
 
-        return status, batches(), conn.close
+        return status, batches(), conn.close, ctype
 
     async def close(self):
         self._closed = True

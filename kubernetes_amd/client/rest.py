@@ -82,8 +82,9 @@ class Client:
     """`content_type` is the wire format (`--kube-api-content-type`, `rest.Config.ContentType`):
     with protobuf, objects of kinds the protobuf schema covers are sent protobuf-encoded and
     responses are asked for as protobuf (falling back to JSON per response, as the reference's
-    negotiated serializer does — lists, CRs and Status bodies come back as JSON); watches stay
-    JSON framed."""
+    negotiated serializer does — lists, CRs and Status bodies come back as JSON), and watches
+    are protobuf streams (`application/vnd.kubernetes.protobuf;stream=watch`: length-delimited
+    WatchEvent frames, decoded by the native codec)."""
 
     def __init__(self, url: str, token=None, qps: float | None = None, burst: int = 10, max_conns=16,
                  user_agent="kubernetes-amd", ssl_context=None, timeout=60.0, content_type=JSON):
@@ -235,8 +236,16 @@ class Client:
         if timeout_seconds:
             q["timeoutSeconds"] = str(int(timeout_seconds))
         path = resource_path(resource, namespace) + "?" + urlencode(q)
+        headers, frames = None, None
+        if self._accept is not None:
+            # protobuf watch streams (the reference client negotiates the same): length-delimited
+            # WatchEvent frames decoded natively; the server answers JSON for kinds protobuf
+            # cannot carry (custom resources)
+            from ..api import protobuf as pb
+            headers = {"Accept": f"{PROTOBUF}, {JSON}"}
+            frames = pb.decode_watch_frames
         try:
-            _, lines, closer = await self.http.stream("GET", path)
+            _, lines, closer, ctype = await self.http.stream("GET", path, headers, frames)
         except Exception as e:
             from .http import HTTPError
             if isinstance(e, HTTPError):
@@ -246,7 +255,7 @@ class Client:
                     st = {"message": e.body.decode(errors="replace")}
                 raise APIStatusError(e.status, st)
             raise
-        return _WatchStream(lines, closer)
+        return _WatchStream(lines, closer, frames is not None and "protobuf" in ctype)
 
 
 def _event(line):
@@ -257,14 +266,23 @@ def _event(line):
     return ev["type"], ev["object"]
 
 
+def _pb_event(ev):
+    """An already-decoded protobuf watch event (type, object)."""
+    if ev[0] == "ERROR":
+        obj = ev[1] or {}
+        raise APIStatusError(obj.get("code", 500), obj)
+    return ev
+
 class _WatchStream:
     """Watch events, one at a time (`async for typ, obj in stream`) or per received batch
     (`async for evs in stream.batches()`, what informers use: one await per network read)."""
 
-    def __init__(self, batches, closer):
+    def __init__(self, batches, closer, protobuf=False):
         self._batches = batches
         self._closer = closer
         self._pending = collections.deque()
+        self._ev = _pb_event if protobuf else _event
+        self.protobuf = protobuf
 
     def __aiter__(self):
         return self
@@ -272,17 +290,18 @@ class _WatchStream:
     async def __anext__(self):
         while not self._pending:
             self._pending.extend(await self._batches.__anext__())
-        return _event(self._pending.popleft())
+        return self._ev(self._pending.popleft())
 
     async def batches(self):
+        ev = self._ev
         if self._pending:
             lines, self._pending = list(self._pending), collections.deque()
-            yield [_event(ln) for ln in lines]
+            yield [ev(ln) for ln in lines]
         async for lines in self._batches:
             out = []
             for ln in lines:
                 try:
-                    out.append(_event(ln))
+                    out.append(ev(ln))
                 except APIStatusError:
                     if out:
                         yield out

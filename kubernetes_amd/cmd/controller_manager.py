@@ -163,10 +163,11 @@ def _reference_flags(ap):
                    help="sample where the event loop blocks, served at /debug/pprof/block (with --profiling)")
     g.add_argument("--kube-api-qps", type=float, default=20.0)
     g.add_argument("--kube-api-burst", type=int, default=30)
-    g.add_argument("--kube-api-content-type", default="application/json",
+    g.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
                    choices=["application/json", "application/vnd.kubernetes.protobuf"],
-                   help="wire format of API requests (the reference defaults to protobuf; JSON is this "
-                        "client's faster path)")
+                   help="wire format of API requests and watch streams (reference default protobuf, "
+                         "`pkg/apis/componentconfig/v1alpha1/defaults.go:75`: protobuf bodies and "
+                         "length-delimited protobuf watch frames, decoded natively)")
     g.add_argument("--controller-start-interval", default="0s")
     g.add_argument("--min-resync-period", default="12h",
                    help="the shared informers re-deliver every cached object every [min, 2*min)")

@@ -30,6 +30,9 @@ def main(argv=None):
                     help="run each GPU container's payload through this PayloadServer (the rank holding the GPU)")
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--node-status-update-frequency", type=float, default=10.0)
+    ap.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
+                    choices=["application/json", "application/vnd.kubernetes.protobuf"],
+                    help="the hollow kubelets' wire format (the kubelet's default: protobuf)")
     ap.add_argument("--ready-file", default=None, help="touched once every node's device plugin registered")
     ap.add_argument("-v", type=int, default=0)
     a = ap.parse_args(argv)
@@ -60,7 +63,8 @@ def main(argv=None):
             payload = PayloadClient(a.payload_socket)
         h = HollowCluster(a.master, a.count, a.name_prefix, a.gpus_per_node, a.hives, payload=payload,
                           emit_events=not a.no_events, status_freq=a.node_status_update_frequency,
-                          partition=a.partition, links_down=parse_links(a.links_down))
+                          partition=a.partition, links_down=parse_links(a.links_down),
+                          content_type=a.kube_api_content_type)
         await h.start()
         await h.wait_registered()
         if a.ready_file:

@@ -346,10 +346,11 @@ def _reference_flags(ap):
     g = ap.add_argument_group("API client")
     g.add_argument("--kube-api-qps", type=float, default=5.0)
     g.add_argument("--kube-api-burst", type=int, default=10)
-    g.add_argument("--kube-api-content-type", default="application/json",
+    g.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
                    choices=["application/json", "application/vnd.kubernetes.protobuf"],
-                   help="wire format of API requests (the reference defaults to protobuf; JSON is this "
-                        "client's faster path)")
+                   help="wire format of API requests and watch streams (reference default protobuf, "
+                         "`pkg/apis/componentconfig/v1alpha1/defaults.go:75`: protobuf bodies and "
+                         "length-delimited protobuf watch frames, decoded natively)")
     g.add_argument("--experimental-bootstrap-kubeconfig", default=None, help="deprecated alias of --bootstrap-kubeconfig")
     deprecated_noop(g, "--require-kubeconfig", False, _bool, "options.go:298")
     g = ap.add_argument_group("host")

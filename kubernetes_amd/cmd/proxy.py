@@ -113,10 +113,11 @@ def _reference_flags(ap):
     ap.add_argument("--oom-score-adj", type=int, default=-999)
     ap.add_argument("--kube-api-qps", type=float, default=5.0)
     ap.add_argument("--kube-api-burst", type=int, default=10)
-    ap.add_argument("--kube-api-content-type", default="application/json",
+    ap.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
                     choices=["application/json", "application/vnd.kubernetes.protobuf"],
-                    help="wire format of API requests (the reference defaults to protobuf; JSON is this "
-                         "client's faster path)")
+                    help="wire format of API requests and watch streams (reference default protobuf, "
+                         "`pkg/apis/componentconfig/v1alpha1/defaults.go:75`: protobuf bodies and "
+                         "length-delimited protobuf watch frames, decoded natively)")
     ap.add_argument("--config-sync-period", default="15m",
                     help="the service/endpoints informers re-deliver every object every [p, 2p), re-syncing the rules")
     unsupported(ap, "--proxy-port-range", "", str, "userspace-mode proxy ports come from the OS")

@@ -45,10 +45,11 @@ def _parser():
     ap.add_argument("--port", type=int, default=10251, help="/healthz and /metrics (0 = off; shard i uses port+i)")
     ap.add_argument("--address", default="0.0.0.0")
     ap.add_argument("--kube-api-burst", type=int, default=None)
-    ap.add_argument("--kube-api-content-type", default="application/json",
+    ap.add_argument("--kube-api-content-type", default="application/vnd.kubernetes.protobuf",
                     choices=["application/json", "application/vnd.kubernetes.protobuf"],
-                    help="wire format of API requests (the reference defaults to protobuf; JSON is this "
-                         "client's faster path, protobuf is served for the kinds the schema covers)")
+                    help="wire format of API requests and watch streams (reference default protobuf, "
+                         "`pkg/apis/componentconfig/v1alpha1/defaults.go:75`: protobuf bodies and "
+                         "length-delimited protobuf watch frames, decoded natively)")
     ap.add_argument("--lock-object-name", default="kube-scheduler")
     ap.add_argument("--lock-object-namespace", default="kube-system")
     ap.add_argument("--hard-pod-affinity-symmetric-weight", type=int, default=1,

@@ -101,21 +101,33 @@ _READONLY = ("configMap", "secret", "downwardAPI", "projected")
 def set_volume_ownership(d, fs_group, readonly):
     """`pkg/volume/volume_linux.go` SetVolumeOwnership: every file and directory of the volume
     gets group `fs_group` and group access (rw, r for the read-only kinds); directories get the
-    setgid bit (new files inherit the group) and group search."""
+    setgid bit (new files inherit the group) and group search.
+
+    Every entry is opened with O_PATH | O_NOFOLLOW and changed through that descriptor
+    (`/proc/self/fd/N`), never by path: a container that can write the volume cannot swap a file
+    for a symlink between the check and the chmod and have the kubelet change a host file."""
     mask = 0o440 if readonly else 0o660
     for root, dirs, files in os.walk(d):
         for p in [root] + [os.path.join(root, x) for x in files]:
             try:
-                st = os.lstat(p)
-                if stat.S_ISLNK(st.st_mode):
-                    continue
-                os.lchown(p, -1, int(fs_group))
+                fd = os.open(p, os.O_PATH | os.O_NOFOLLOW | os.O_CLOEXEC)
+            except OSError as e:
+                log.debug("fsGroup ownership of %s: %s", p, e)
+                continue
+            try:
+                st = os.fstat(fd)
+                if stat.S_ISLNK(st.st_mode) or not (stat.S_ISDIR(st.st_mode) or stat.S_ISREG(st.st_mode)):
+                    continue          # O_PATH|O_NOFOLLOW on a symlink opens the link itself
+                via = f"/proc/self/fd/{fd}"
+                os.chown(via, -1, int(fs_group))
                 m = stat.S_IMODE(st.st_mode) | mask
                 if stat.S_ISDIR(st.st_mode):
                     m |= stat.S_ISGID | 0o110
-                os.chmod(p, m)
+                os.chmod(via, m)
             except OSError as e:       # not permitted (an unprivileged kubelet outside the group)
                 log.debug("fsGroup ownership of %s: %s", p, e)
+            finally:
+                os.close(fd)
 
 
 def _fs_group(pod):

@@ -26,7 +26,8 @@ class HollowCluster:
     """A set of hollow nodes sharing one process / event loop / API client pool."""
 
     def __init__(self, master, count, prefix="hollow", gpus=8, hives=1, payload=None, workdir=None,
-                 emit_events=False, status_freq=10.0, max_conns=32, partition="SPX", links_down=()):
+                 emit_events=False, status_freq=10.0, max_conns=32, partition="SPX", links_down=(),
+                 content_type="application/vnd.kubernetes.protobuf"):
         self.master = master
         self.count = count
         self.prefix = prefix
@@ -39,7 +40,7 @@ class HollowCluster:
         self.dir = workdir or tempfile.mkdtemp(prefix=f"kamd-{prefix}-")
         self.emit_events = emit_events
         self.status_freq = status_freq
-        self.client = Client(master, max_conns=max_conns)
+        self.client = Client(master, max_conns=max_conns, content_type=content_type)
         self.nodes = []
         self.plugins = []
         self.smi = None

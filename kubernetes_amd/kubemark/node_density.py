@@ -114,11 +114,28 @@ async def _wait_running(client, ns, names, timeout):
     return seen
 
 
+async def _drain_pods(url):
+    """Delete every pod and wait until the kubelet has confirmed each one gone (a graceful
+    delete stays visible until its containers are stopped)."""
+    c = Client(url)
+    try:
+        for p in (await c.list("pods"))["items"]:
+            try:
+                await c.delete("pods", p["metadata"]["name"], p["metadata"]["namespace"], grace_period=1)
+            except Exception:      # noqa: BLE001 - already gone
+                pass
+        while (await c.list("pods"))["items"]:
+            await asyncio.sleep(0.2)
+    finally:
+        await c.close()
+
+
 async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0, monitor=10.0, period=1.0,
               runtime="process"):
     tmp = tempfile.mkdtemp(prefix="kamd-node-density-")
     pf = os.path.join(tmp, "api.port")
     procs = [_spawn(["kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf], tmp, "apiserver")]
+    url = None
     try:
         t = time.time()
         while not os.path.exists(pf):
@@ -231,6 +248,13 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
                                     and out["runtime_rss_mib"] <= THRESHOLDS["runtime_rss_mib"])))
         return out
     finally:
+        # the kubelet leaves containers running when it stops (by design: a restarted kubelet
+        # adopts them), so the pods go first and the kubelet kills their containers
+        try:
+            if url is not None:
+                await asyncio.wait_for(_drain_pods(url), 60)
+        except Exception:          # noqa: BLE001 - best effort; the processes are stopped anyway
+            pass
         for p in procs:
             p.terminate()
         for p in procs:

@@ -233,15 +233,19 @@ class FanoutClient:
     def _s(b: bytes) -> bytes:
         return struct.pack("<I", len(b)) + b
 
-    def encode(self, prefix, send_initial, from_rev, timeout, reqs) -> bytes:
-        """reqs: [(target, op, key, [values])] with op one of OPS."""
-        out = struct.pack("<BBqd", 1, 1 if send_initial else 0, int(from_rev or 0), float(timeout or 0))
+    def encode(self, prefix, send_initial, from_rev, timeout, reqs, protobuf=False) -> bytes:
+        """reqs: [(target, op, key, [values])] with op one of OPS. Version 2 adds a trailing
+        format byte: 1 = protobuf watch frames (`...protobuf;stream=watch`), 0 = JSON lines."""
+        out = struct.pack("<BBqd", 2 if protobuf else 1, 1 if send_initial else 0, int(from_rev or 0),
+                          float(timeout or 0))
         out += self._s(prefix.encode())
         out += struct.pack("<H", len(reqs))
         for target, op, key, vals in reqs:
             out += struct.pack("<BB", target, self.OPS[op]) + self._s(key.encode()) + struct.pack("<H", len(vals))
             for v in vals:
                 out += self._s(str(v).encode())
+        if protobuf:
+            out += b"\x01"
         return struct.pack("<I", len(out)) + out
 
     def handoff(self, fd, msg: bytes):

@@ -424,6 +424,21 @@ class _Stream:
         self.error = None
 
 
+class _Streams(dict):
+    """The connection's open streams; removing one frees a slot for a queued client call."""
+    __slots__ = ("conn",)
+
+    def __init__(self, conn):
+        super().__init__()
+        self.conn = conn
+
+    def pop(self, *a):
+        r = super().pop(*a)
+        if self.conn.slot_waiters:
+            self.conn._slot_free()
+        return r
+
+
 class _Conn(asyncio.Protocol):
     """One HTTP/2 connection (client or server side)."""
 
@@ -432,7 +447,9 @@ class _Conn(asyncio.Protocol):
         self.client = server is None
         self.transport = None
         self.buf = bytearray()
-        self.streams: dict[int, _Stream] = {}
+        self.streams: dict[int, _Stream] = _Streams(self)
+        self.peer_max_streams = None                 # peer's SETTINGS_MAX_CONCURRENT_STREAMS
+        self.slot_waiters: deque = deque()           # client calls queued for a stream slot
         self.dec = HpackDecoder()
         self.next_sid = 1
         self.last_peer_sid = 0
@@ -447,6 +464,24 @@ class _Conn(asyncio.Protocol):
         self.cont_sid = 0                            # stream expecting CONTINUATION
         self.cont_st = None
         self.blocked: deque = deque()                # streams with DATA waiting for window
+
+    # -- client stream slots (the peer's SETTINGS_MAX_CONCURRENT_STREAMS) ----------------
+    async def stream_slot(self):
+        """Wait until opening one more stream stays within the peer's limit (calls over it queue
+        here, as grpc-core's do, instead of being refused)."""
+        while self.peer_max_streams is not None and len(self.streams) >= self.peer_max_streams and not self.closed:
+            fut = asyncio.get_running_loop().create_future()
+            self.slot_waiters.append(fut)
+            await fut
+
+    def _slot_free(self):
+        while self.slot_waiters and (self.peer_max_streams is None or len(self.streams) < self.peer_max_streams
+                                     or self.closed):
+            f = self.slot_waiters.popleft()
+            if not f.done():
+                f.set_result(None)
+                if not self.closed:
+                    break
 
     # -- transport events ----------------------------------------------------------------
     def connection_made(self, transport):
@@ -464,6 +499,7 @@ class _Conn(asyncio.Protocol):
 
     def connection_lost(self, exc):
         self.closed = True
+        self._slot_free()
         if not self.ready.done():
             self.ready.set_exception(RpcError(StatusCode.UNAVAILABLE, "connection closed before HTTP/2 settings"))
             self.ready.exception()
@@ -583,6 +619,12 @@ class _Conn(asyncio.Protocol):
                     self.peer_initial = val
                     for st in self.streams.values():
                         st.send_window += delta
+                        if st.send_window > _MAX_WINDOW:      # RFC 7540 §6.9.2
+                            raise _ConnError(E_FLOW_CONTROL, "SETTINGS_INITIAL_WINDOW_SIZE change overflows a "
+                                                             "stream's flow-control window")
+                elif ident == S_MAX_CONCURRENT_STREAMS:
+                    self.peer_max_streams = val
+                    self._slot_free()
                 elif ident == S_MAX_FRAME_SIZE:
                     if not 16384 <= val <= (1 << 24) - 1:
                         raise _ConnError(E_PROTOCOL, f"SETTINGS_MAX_FRAME_SIZE {val} out of range")
@@ -932,6 +974,10 @@ class Channel:
                     conn = await asyncio.wait_for(self._connection(), timeout)
                 except asyncio.TimeoutError:
                     raise RpcError(StatusCode.DEADLINE_EXCEEDED, "Deadline Exceeded while connecting")
+        if conn.peer_max_streams is not None and len(conn.streams) >= conn.peer_max_streams:
+            await conn.stream_slot()
+            if conn.closed:
+                raise RpcError(StatusCode.UNAVAILABLE, "connection closed")
         st = self._open(conn, path, payload, timeout)
         st.fut = asyncio.get_running_loop().create_future()
         if st.ended:                                  # failed while sending
@@ -986,6 +1032,7 @@ class _StreamCall:
             raise asyncio.CancelledError()
         if self.st is None:
             self.conn = await self.channel._connection()
+            await self.conn.stream_slot()
             self.st = self.channel._open(self.conn, self.path, self.payload, self.timeout)
         st = self.st
         while True:

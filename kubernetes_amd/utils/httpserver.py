@@ -30,7 +30,7 @@ REASONS = {
 
 class Request:
     __slots__ = ("method", "path", "raw_path", "query", "qs", "headers", "body", "transport", "user", "info", "served_gv",
-                 "insecure")
+                 "insecure", "obj")
 
     def __init__(self, method, target, headers, body, transport):
         self.method = method
@@ -49,16 +49,18 @@ class Request:
         self.info = None
         self.served_gv = None
         self.insecure = False      # arrived on the API server's insecure listener
+        self.obj = None            # the body, already decoded (protobuf request bodies)
 
 
 class Response:
-    __slots__ = ("status", "body", "content_type", "headers")
+    __slots__ = ("status", "body", "content_type", "headers", "entry")
 
-    def __init__(self, status=200, body=b"", content_type="application/json", headers=None):
+    def __init__(self, status=200, body=b"", content_type="application/json", headers=None, entry=None):
         self.status = status
         self.body = body if isinstance(body, (bytes, bytearray)) else str(body).encode()
         self.content_type = content_type
         self.headers = headers
+        self.entry = entry         # the cache entry the body came from (protobuf negotiation)
 
 
 class StreamResponse:
@@ -131,6 +133,24 @@ class ChunkWriter:
         return p.close_fut
 
 
+_CHUNK_SIZE = __import__("re").compile(rb"[0-9A-Fa-f]{1,16}")
+MAX_CHUNKS = 1 << 16          # chunks per request body
+
+
+class _ChunkState:
+    """Where a chunked body's parse stopped: `pos` = next unparsed byte, `need` = bytes of the
+    current chunk still to arrive (None: a size line is next)."""
+    __slots__ = ("start", "pos", "need", "parts", "size", "chunks", "framing", "trailer", "eol")
+
+    def __init__(self, start):
+        self.start = self.pos = start
+        self.need = None
+        self.parts = []
+        self.size = self.chunks = self.framing = 0
+        self.trailer = False
+        self.eol = 0
+
+
 class _Conn(asyncio.Protocol):
     def __init__(self, server):
         self.server = server
@@ -143,6 +163,8 @@ class _Conn(asyncio.Protocol):
         self._drain_waiter = None
         self.close_fut = None
         self.deadline = 0.0         # loop time the in-flight request must answer by (0 = none)
+        self.chunked = None         # _ChunkState of a chunked request body being received
+        self.rejected = None        # (status, why) answered after the pipelined requests before it
 
     def connection_made(self, transport):
         self.transport = transport
@@ -170,6 +192,8 @@ class _Conn(asyncio.Protocol):
             await self._drain_waiter
 
     def data_received(self, data):
+        if self.rejected is not None:
+            return                  # nothing after a framing error starts a request
         self.buf += data
         while True:
             req = self._parse()
@@ -185,45 +209,75 @@ class _Conn(asyncio.Protocol):
 
     def _reject(self, status, why):
         """Answer a request this server will not read (bad framing, too large) and close: after
-        a framing error nothing later on the connection can be trusted to start a request."""
+        a framing error nothing later on the connection can be trusted to start a request. The
+        answer goes out after the responses of requests pipelined before it (HTTP/1.1 keeps
+        responses in request order); reading stops now."""
+        self.rejected = (status, why)
+        self.chunked = None
+        del self.buf[:]
+        self.transport.pause_reading()
+        if not self.pending and not self.busy:
+            self._write_reject()
+
+    def _write_reject(self):
+        status, why = self.rejected
         body = b'{"kind":"Status","apiVersion":"v1","metadata":{},"status":"Failure","message":"%s","code":%d}' % (
             why.encode(), status)
-        self.transport.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n"
-                             b"Connection: close\r\n\r\n%s" % (status, REASONS.get(status, "Error").encode(), len(body), body))
-        self.transport.close()
-        del self.buf[:]
+        if not self.transport.is_closing():
+            self.transport.write(b"HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %d\r\n"
+                                 b"Connection: close\r\n\r\n%s" % (status, REASONS.get(status, "Error").encode(),
+                                                                      len(body), body))
+            self.transport.close()
 
     def _chunked_body(self, start):
         """(body, end offset) of a complete chunked request body at buf[start:], None while
-        incomplete; raises ValueError on bad framing or a body over the size limit."""
-        buf, pos, parts, size = self.buf, start, [], 0
+        incomplete; raises ValueError on bad framing, OverflowError over the size limit. The
+        parse state lives on the connection (`_ChunkState`), so every byte is parsed once however
+        many reads the body arrives in."""
+        st = self.chunked
+        if st is None or st.start != start:
+            st = self.chunked = _ChunkState(start)
+        buf = self.buf
         limit = self.server.max_body
         while True:
-            eol = buf.find(b"\r\n", pos)
-            if eol < 0:
-                if len(buf) - pos > 1024:
-                    raise ValueError("chunk size line too long")
-                return None
-            n = int(bytes(buf[pos:eol]).split(b";", 1)[0].strip(), 16)
-            if n < 0:
-                raise ValueError("negative chunk size")
-            size += n
-            if size > limit:
-                raise OverflowError
-            if n == 0:
-                # trailer section: header lines up to an empty line
-                tend = buf.find(b"\r\n\r\n", eol) if buf[eol + 2:eol + 4] != b"\r\n" else eol
+            pos = st.pos
+            if st.trailer:
+                tend = buf.find(b"\r\n\r\n", st.eol) if buf[st.eol + 2:st.eol + 4] != b"\r\n" else st.eol
                 if tend < 0:
-                    if len(buf) - eol > 8192:
+                    if len(buf) - st.eol > 8192:
                         raise ValueError("trailer section too long")
                     return None
-                return b"".join(parts), tend + 4
-            if len(buf) < eol + 2 + n + 2:
+                self.chunked = None
+                return b"".join(st.parts), tend + 4
+            if st.need is None:
+                eol = buf.find(b"\r\n", pos, pos + 1026)
+                if eol < 0:
+                    if len(buf) - pos > 1024:
+                        raise ValueError("chunk size line too long")
+                    return None
+                tok = bytes(buf[pos:eol]).split(b";", 1)[0].strip()
+                if not _CHUNK_SIZE.fullmatch(tok):       # RFC 7230 §4.1: 1*HEXDIG, nothing else
+                    raise ValueError("malformed chunk size")
+                n = int(tok, 16)
+                st.size += n
+                st.framing += eol + 2 - pos
+                if st.size > limit:
+                    raise OverflowError
+                st.chunks += 1
+                if st.chunks > MAX_CHUNKS or st.framing > max(64 << 10, limit // 4):
+                    raise OverflowError
+                if n == 0:
+                    st.trailer, st.eol = True, eol
+                    continue
+                st.need, st.pos = n, eol + 2
+                continue
+            n = st.need
+            if len(buf) < pos + n + 2:
                 return None
-            if buf[eol + 2 + n:eol + 4 + n] != b"\r\n":
+            if buf[pos + n:pos + n + 2] != b"\r\n":
                 raise ValueError("chunk not terminated by CRLF")
-            parts.append(bytes(buf[eol + 2:eol + 2 + n]))
-            pos = eol + 4 + n
+            st.parts.append(bytes(buf[pos:pos + n]))
+            st.need, st.pos = None, pos + n + 2
 
     def _parse(self):
         buf = self.buf
@@ -263,6 +317,7 @@ class _Conn(asyncio.Protocol):
             if got is None:
                 return None
             body, stop = got
+            self.chunked = None
             del buf[:stop]
             headers.pop("transfer-encoding", None)
             headers["content-length"] = str(len(body))
@@ -348,6 +403,8 @@ class _Conn(asyncio.Protocol):
                     return
         finally:
             self.busy = False
+            if self.rejected is not None and not self.pending:
+                self._write_reject()
 
     async def _upgrade(self, resp):
         loop = asyncio.get_running_loop()

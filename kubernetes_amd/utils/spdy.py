@@ -31,7 +31,7 @@ MAX_FRAME = (1 << 24) - 1
 # one decompressed header block (a compressed frame could otherwise inflate ~1000x) and the
 # streams one session may hold open (exec/attach use 3-5, port-forward 2 per port)
 MAX_HEADER_BLOCK = 1 << 20
-MAX_STREAMS = 1024
+MAX_STREAMS = 1024          # concurrently OPEN streams per session (closed ones are forgotten)
 
 # The SPDY/3 header-compression dictionary (draft-mbelshe-httpbis-spdy-00 §2.6.10.1): the common
 # header names and values, each as a 32-bit big-endian length + bytes, then a run of status
@@ -117,6 +117,10 @@ class Stream:
         if fin and not self.remote_closed:
             self.remote_closed = True
             self._q.put_nowait(b"")
+            self.conn._forget(self)
+
+    def _done(self):
+        return self.reset or (self.remote_closed and self.local_closed)
 
     async def read(self) -> bytes:
         """Next chunk, b"" once the peer half-closed (or reset) the stream."""
@@ -133,11 +137,13 @@ class Stream:
             await self.conn._send(data_frame(self.id, FLAG_FIN if (fin and last) else 0, data[i:i + MAX_FRAME]))
         if fin:
             self.local_closed = True
+            self.conn._forget(self)
 
     async def close(self):
         """Half-close (FIN) our direction."""
         if not self.local_closed and not self.reset:
             self.local_closed = True
+            self.conn._forget(self)
             await self.conn._send(data_frame(self.id, FLAG_FIN, b""))
 
     async def reply(self, headers=None, fin=False):
@@ -145,10 +151,12 @@ class Stream:
         await self.conn._send(control_frame(SYN_REPLY, FLAG_FIN if fin else 0, struct.pack(">I", self.id) + block))
         if fin:
             self.local_closed = True
+            self.conn._forget(self)
 
     async def reset_stream(self, status=RST_CANCEL):
         if not self.reset:
             self.reset = True
+            self.conn._forget(self)
             await self.conn._send(control_frame(RST_STREAM, 0, struct.pack(">II", self.id, status)))
 
 
@@ -166,6 +174,13 @@ class Connection:
         self._wlock = asyncio.Lock()
         self.closed = asyncio.Event()
         self.goaway = False
+        self.last_peer_sid = 0       # highest stream id the peer opened (GOAWAY's last-good-stream)
+
+    def _forget(self, st):
+        """A stream both sides closed (or either reset) no longer counts against MAX_STREAMS:
+        the session holds open streams only."""
+        if st._done() and self.streams.get(st.id) is st:
+            del self.streams[st.id]
 
     def _compress(self, block: bytes) -> bytes:
         return self._zc.compress(block) + self._zc.flush(zlib.Z_SYNC_FLUSH)
@@ -198,7 +213,7 @@ class Connection:
     async def close(self, status=0):
         if not self.goaway:
             self.goaway = True
-            last = max([s for s in self.streams if (s % 2 == 1) == self.server] or [0])
+            last = max([s for s in self.streams if (s % 2 == 1) == self.server] + [self.last_peer_sid])
             try:
                 await self._send(control_frame(GOAWAY, 0, struct.pack(">II", last, status)))
             except (ConnectionError, RuntimeError):
@@ -231,7 +246,7 @@ class Connection:
         except (asyncio.IncompleteReadError, ConnectionError, RuntimeError, SpdyError, zlib.error, struct.error):
             pass
         finally:
-            for st in self.streams.values():
+            for st in list(self.streams.values()):
                 st._feed(b"", True)
             self.closed.set()
 
@@ -247,6 +262,7 @@ class Connection:
                 return
             st = Stream(self, sid, headers)
             self.streams[sid] = st
+            self.last_peer_sid = max(self.last_peer_sid, sid)
             if flags & FLAG_FIN:
                 st._feed(b"", True)
             if self.on_stream is not None:
@@ -283,6 +299,7 @@ class Connection:
             if st is not None:
                 st.reset = True
                 st._feed(b"", True)
+                self._forget(st)
         elif ftype == PING:
             pid = struct.unpack_from(">I", body, 0)[0]
             if (pid % 2 == 1) == self.server:          # the peer's ping: echo it

@@ -146,23 +146,47 @@ int main(int argc, char** argv) {
     total_bad += bad[i];
   }
   bool correct = total_bad == 0;
-  hipEvent_t e0, e1;
-  HIPCHK(hipSetDevice(0));
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventRecord(e0, st[0]));
-  if (run(iters)) return 1;
-  HIPCHK(hipSetDevice(0));
-  HIPCHK(hipEventRecord(e1, st[0]));
-  HIPCHK(hipEventSynchronize(e1));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  double t = ms / 1e3 / iters;
-  double algbw = (double)count * sizeof(float) / t / 1e9;
+  // timing on EVERY rank's stream: a slow peer shows up as its own (and everyone's) longer
+  // time, not only through the final host sync; the reported time is the slowest rank's
+  std::vector<hipEvent_t> e0(n), e1(n);
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(i));
+    HIPCHK(hipEventCreate(&e0[i]));
+    HIPCHK(hipEventCreate(&e1[i]));
+    HIPCHK(hipEventRecord(e0[i], st[i]));
+  }
+  for (int it = 0; it < iters; ++it) {
+    NCCLCHK(ncclGroupStart());
+    for (int i = 0; i < n; ++i) NCCLCHK(ncclAllReduce(buf[i], buf[i], count, ncclFloat, ncclSum, comms[i], st[i]));
+    NCCLCHK(ncclGroupEnd());
+  }
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(i));
+    HIPCHK(hipEventRecord(e1[i], st[i]));
+  }
+  std::vector<double> rank_s(n, 0.0);
+  double t = 0, tmin = 1e30;
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(i));
+    HIPCHK(hipEventSynchronize(e1[i]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0[i], e1[i]));
+    rank_s[i] = ms / 1e3 / iters;
+    if (rank_s[i] > t) t = rank_s[i];
+    if (rank_s[i] < tmin) tmin = rank_s[i];
+    HIPCHK(hipEventDestroy(e0[i]));
+    HIPCHK(hipEventDestroy(e1[i]));
+  }
+  double bytes = (double)count * sizeof(float);
+  double algbw = bytes / t / 1e9;
   double busbw = n > 1 ? algbw * 2.0 * (n - 1) / n : 0.0;
-  printf("{\"ranks\": %d, \"bytes\": %zu, \"time_us\": %.1f, \"algbw_GBps\": %.2f, \"busbw_GBps\": %.2f, "
+  double busbw_fast = n > 1 ? bytes / tmin / 1e9 * 2.0 * (n - 1) / n : 0.0;
+  printf("{\"ranks\": %d, \"bytes\": %zu, \"time_us\": %.1f, \"time_us_min_rank\": %.1f, \"rank_time_us\": [",
+         n, count * sizeof(float), t * 1e6, tmin * 1e6);
+  for (int i = 0; i < n; ++i) printf("%s%.1f", i ? ", " : "", rank_s[i] * 1e6);
+  printf("], \"algbw_GBps\": %.2f, \"busbw_GBps\": %.2f, \"busbw_GBps_fastest_rank\": %.2f, "
          "\"elements_checked_per_rank\": %zu, \"bad_elements\": [",
-         n, count * sizeof(float), t * 1e6, algbw, busbw, count);
+         algbw, busbw, busbw_fast, count);
   for (int i = 0; i < n; ++i) printf("%s%llu", i ? ", " : "", bad[i]);
   printf("], \"correct\": %s}\n", correct ? "true" : "false");
   for (int i = 0; i < n; ++i) { ncclCommDestroy(comms[i]); hipSetDevice(i); hipFree(buf[i]); }

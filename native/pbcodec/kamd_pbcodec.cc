@@ -24,6 +24,23 @@ using pbc::Field;
 using pbc::Message;
 using pbc::Schema;
 
+// Decode caches (all touched under the GIL only). Watch streams decode the same few hundred
+// short strings (namespaces, node names, phases, condition types, images, quantities) and the
+// same timestamps over and over: a hit hands back a new reference to the existing str instead
+// of allocating and UTF-8-decoding another one.
+struct StrSlot {
+  uint64_t h = 0;
+  uint32_t n = 0;
+  char b[32];
+  PyObject* o = nullptr;
+};
+struct TimeSlot {
+  int64_t sec = 0, nanos = -1;
+  bool micro = false;
+  PyObject* o = nullptr;
+};
+constexpr size_t kStrSlots = 4096, kTimeSlots = 256;
+
 struct CodecObject {
   PyObject_HEAD
   Schema* schema;
@@ -31,7 +48,46 @@ struct CodecObject {
   PyObject* dumps;   // json.dumps(obj) -> str (RawExtension / JSON values)
   PyObject* loads;   // json.loads(bytes) -> object
   std::unordered_map<std::string, std::string>* canon;   // kind -> served apiVersion
+  std::vector<std::vector<PyObject*>>* keys;              // [message][field] -> interned JSON key
+  StrSlot* strs;
+  TimeSlot* times;
 };
+
+void clear_caches(CodecObject* self) {
+  if (self->keys) {
+    for (auto& v : *self->keys)
+      for (PyObject* o : v) Py_XDECREF(o);
+    delete self->keys;
+    self->keys = nullptr;
+  }
+  if (self->strs) {
+    for (size_t i = 0; i < kStrSlots; ++i) Py_XDECREF(self->strs[i].o);
+    delete[] self->strs;
+    self->strs = nullptr;
+  }
+  if (self->times) {
+    for (size_t i = 0; i < kTimeSlots; ++i) Py_XDECREF(self->times[i].o);
+    delete[] self->times;
+    self->times = nullptr;
+  }
+}
+
+void init_caches(CodecObject* self) {
+  clear_caches(self);
+  self->keys = new std::vector<std::vector<PyObject*>>(self->schema->msgs.size());
+  for (size_t mi = 0; mi < self->schema->msgs.size(); ++mi) {
+    auto& fs = self->schema->msgs[mi].fields;
+    auto& ks = (*self->keys)[mi];
+    ks.resize(fs.size(), nullptr);
+    for (size_t fi = 0; fi < fs.size(); ++fi) {
+      PyObject* k = PyUnicode_FromStringAndSize(fs[fi].json.data(), (Py_ssize_t)fs[fi].json.size());
+      if (k) PyUnicode_InternInPlace(&k);
+      ks[fi] = k;
+    }
+  }
+  self->strs = new StrSlot[kStrSlots];
+  self->times = new TimeSlot[kTimeSlots];
+}
 
 // ---------------------------------------------------------------------------------------------
 // wire writing
@@ -521,7 +577,52 @@ struct Decoder {
   std::string err;
   int depth = 0;
 
-  PyObject* str(const uint8_t* p, size_t n) { return PyUnicode_DecodeUTF8((const char*)p, (Py_ssize_t)n, "replace"); }
+  PyObject* str(const uint8_t* p, size_t n) {
+    if (n == 0 || n > sizeof(StrSlot::b) || !self->strs)
+      return PyUnicode_DecodeUTF8((const char*)p, (Py_ssize_t)n, "replace");
+    uint64_t h = 1469598103934665603ull;           // FNV-1a
+    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+    StrSlot& e = self->strs[h & (kStrSlots - 1)];
+    if (e.o && e.h == h && e.n == n && memcmp(e.b, p, n) == 0) {
+      Py_INCREF(e.o);
+      return e.o;
+    }
+    PyObject* o = PyUnicode_DecodeUTF8((const char*)p, (Py_ssize_t)n, "replace");
+    if (!o) return nullptr;
+    Py_XDECREF(e.o);
+    Py_INCREF(o);
+    e.o = o; e.h = h; e.n = (uint32_t)n;
+    memcpy(e.b, p, n);
+    return o;
+  }
+
+  PyObject* time_str(int64_t sec, int64_t nanos, bool micro) {
+    if (!self->times) {
+      std::string t = pbc::format_time(sec, nanos, micro);
+      return PyUnicode_FromStringAndSize(t.data(), (Py_ssize_t)t.size());
+    }
+    uint64_t h = ((uint64_t)sec * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)nanos * 31) ^ (micro ? 1 : 0);
+    TimeSlot& e = self->times[(h >> 7) & (kTimeSlots - 1)];
+    if (e.o && e.sec == sec && e.nanos == nanos && e.micro == micro) {
+      Py_INCREF(e.o);
+      return e.o;
+    }
+    std::string t = pbc::format_time(sec, nanos, micro);
+    PyObject* o = PyUnicode_FromStringAndSize(t.data(), (Py_ssize_t)t.size());
+    if (!o) return nullptr;
+    Py_XDECREF(e.o);
+    Py_INCREF(o);
+    e.o = o; e.sec = sec; e.nanos = nanos; e.micro = micro;
+    return o;
+  }
+
+  PyObject* key_of(int mi, int fi, const Field& f) {
+    if (self->keys) {
+      PyObject* k = (*self->keys)[mi][fi];
+      if (k) { Py_INCREF(k); return k; }
+    }
+    return PyUnicode_FromStringAndSize(f.json.data(), (Py_ssize_t)f.json.size());
+  }
 
   PyObject* value(const Field& f, uint8_t wt, uint64_t v, const uint8_t* p, size_t n) {
     if (wt != (f.type == pbc::S_MSG ? 2 : pbc::wire_of(f.type))) {
@@ -583,8 +684,7 @@ struct Decoder {
           if (num == 1) sec = (int64_t)v;
           else if (num == 2) nanos = (int64_t)v;
         }
-        std::string t = pbc::format_time(sec, nanos, sp == pbc::SP_MICROTIME);
-        return PyUnicode_FromStringAndSize(t.data(), (Py_ssize_t)t.size());
+        return time_str(sec, nanos, sp == pbc::SP_MICROTIME);
       }
       case pbc::SP_DURATION: {
         int64_t d = 0;
@@ -705,7 +805,8 @@ struct Decoder {
     while (!r.done()) {
       if (!r.next(&num, &wt, &v, &q, &l)) { err = "truncated protobuf"; return false; }
       if (num >= m.by_num.size() || m.by_num[num] < 0) continue;
-      const Field& f = m.fields[m.by_num[num]];
+      const int fi = m.by_num[num];
+      const Field& f = m.fields[fi];
       if (!pbc::wire_ok(f, wt)) {
         err = "field " + f.json + ": wire type " + std::to_string(wt) + " does not match its type";
         return false;
@@ -714,7 +815,7 @@ struct Decoder {
         if (!message(f.msg, q, l, out)) return false;
         continue;
       }
-      PyObject* key = PyUnicode_FromStringAndSize(f.json.data(), (Py_ssize_t)f.json.size());
+      PyObject* key = key_of(mi, fi, f);
       if (f.label == pbc::L_REP) {
         PyObject* lst = PyDict_GetItem(out, key);
         if (!lst) {
@@ -933,6 +1034,118 @@ PyObject* c_to_json(CodecObject* self, PyObject* args) {
   return PyBytes_FromStringAndSize(out.data(), (Py_ssize_t)out.size());
 }
 
+// watch_frame(type, value, rv=None) -> one length-delimited protobuf WatchEvent frame
+PyObject* c_watch_frame(CodecObject* self, PyObject* args) {
+  const char* type;
+  Py_buffer buf;
+  const char* rv = nullptr;
+  if (!PyArg_ParseTuple(args, "sy*|z", &type, &buf, &rv)) return nullptr;
+  std::string env, out;
+  const uint8_t* p = (const uint8_t*)buf.buf;
+  size_t n = (size_t)buf.len;
+  if (rv && pbc::envelope_with_rv(*self->schema, p, n, rv, env))
+    pbc::watch_event_frame(out, type, env.data(), env.size());
+  else
+    pbc::watch_event_frame(out, type, p, n);
+  PyBuffer_Release(&buf);
+  return PyBytes_FromStringAndSize(out.data(), (Py_ssize_t)out.size());
+}
+
+// with_rv(envelope, rv) -> the envelope with metadata.resourceVersion = rv, or None
+PyObject* c_with_rv(CodecObject* self, PyObject* args) {
+  Py_buffer buf;
+  const char* rv;
+  if (!PyArg_ParseTuple(args, "y*s", &buf, &rv)) return nullptr;
+  std::string out;
+  bool ok = pbc::envelope_with_rv(*self->schema, (const uint8_t*)buf.buf, (size_t)buf.len, rv, out);
+  PyBuffer_Release(&buf);
+  if (!ok) Py_RETURN_NONE;
+  return PyBytes_FromStringAndSize(out.data(), (Py_ssize_t)out.size());
+}
+
+// decode_watch_frames(buffer) -> (events [(type, object)], bytes consumed). Objects are decoded
+// from their envelope (JSON raw values through json.loads).
+PyObject* c_decode_watch_frames(CodecObject* self, PyObject* args) {
+  Py_buffer buf;
+  if (!PyArg_ParseTuple(args, "y*", &buf)) return nullptr;
+  const uint8_t* p = (const uint8_t*)buf.buf;
+  size_t n = (size_t)buf.len, pos = 0;
+  PyObject* lst = PyList_New(0);
+  std::string err;
+  while (n - pos >= 4) {
+    uint32_t fl = ((uint32_t)p[pos] << 24) | ((uint32_t)p[pos + 1] << 16) | ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
+    if (fl > (64u << 20)) { err = "watch frame too large"; break; }
+    if (n - pos - 4 < fl) break;
+    const uint8_t* f = p + pos + 4;
+    pbc::Reader r{f, f + fl};
+    const uint8_t *tp = nullptr, *raw = nullptr;
+    size_t tn = 0, rn = 0;
+    uint32_t num; uint8_t wt; uint64_t v; const uint8_t* q; size_t l;
+    bool bad = false;
+    while (!r.done()) {
+      if (!r.next(&num, &wt, &v, &q, &l)) { bad = true; break; }
+      if (num == 1 && wt == 2) { tp = q; tn = l; }
+      else if (num == 2 && wt == 2) {
+        pbc::Reader e{q, q + l};
+        uint32_t n2; uint8_t w2; uint64_t v2; const uint8_t* q2; size_t l2;
+        while (!e.done()) {
+          if (!e.next(&n2, &w2, &v2, &q2, &l2)) { bad = true; break; }
+          if (n2 == 1 && w2 == 2) { raw = q2; rn = l2; }
+        }
+      }
+    }
+    if (bad || !tp) { err = "malformed watch frame"; break; }
+    PyObject* obj = nullptr;
+    if (raw && rn >= 4 && memcmp(raw, "k8s\0", 4) == 0) {
+      std::string av, kind;
+      const uint8_t* body;
+      size_t bn;
+      if (!read_envelope(raw, rn, &av, &kind, &body, &bn)) { err = "malformed envelope in watch frame"; break; }
+      int mi = self->schema->message_for(av, kind);
+      if (mi < 0) { err = "no protobuf message for " + av + "/" + kind; break; }
+      obj = PyDict_New();
+      auto cit = self->canon ? self->canon->find(kind) : decltype(self->canon->end()){};
+      const std::string& shown = (self->canon && cit != self->canon->end()) ? cit->second : av;
+      PyObject* k = PyUnicode_FromStringAndSize(kind.data(), (Py_ssize_t)kind.size());
+      PyObject* a = PyUnicode_FromStringAndSize(shown.data(), (Py_ssize_t)shown.size());
+      PyDict_SetItemString(obj, "kind", k);
+      PyDict_SetItemString(obj, "apiVersion", a);
+      Py_DECREF(k);
+      Py_DECREF(a);
+      Decoder d{*self->schema, self, {}};
+      if (!d.message(mi, body, bn, obj)) {
+        Py_DECREF(obj);
+        if (PyErr_Occurred()) { Py_DECREF(lst); PyBuffer_Release(&buf); return nullptr; }
+        err = d.err;
+        obj = nullptr;
+        break;
+      }
+    } else {
+      PyObject* b = PyBytes_FromStringAndSize((const char*)(raw ? raw : (const uint8_t*)""), (Py_ssize_t)rn);
+      obj = PyObject_CallFunctionObjArgs(self->loads, b, nullptr);
+      Py_DECREF(b);
+      if (!obj) { Py_DECREF(lst); PyBuffer_Release(&buf); return nullptr; }
+    }
+    PyObject* t = PyUnicode_FromStringAndSize((const char*)tp, (Py_ssize_t)tn);
+    PyObject* tup = PyTuple_Pack(2, t, obj);
+    Py_DECREF(t);
+    Py_DECREF(obj);
+    PyList_Append(lst, tup);
+    Py_DECREF(tup);
+    pos += 4 + fl;
+  }
+  PyBuffer_Release(&buf);
+  if (!err.empty()) {
+    Py_DECREF(lst);
+    return raise_err(self, "", err);
+  }
+  PyObject* consumed = PyLong_FromSize_t(pos);
+  PyObject* res = PyTuple_Pack(2, lst, consumed);
+  Py_DECREF(lst);
+  Py_DECREF(consumed);
+  return res;
+}
+
 PyObject* c_set_canonical(CodecObject* self, PyObject* args) {
   PyObject* d;
   if (!PyArg_ParseTuple(args, "O!", &PyDict_Type, &d)) return nullptr;
@@ -970,6 +1183,7 @@ int codec_init(CodecObject* self, PyObject* args, PyObject*) {
   }
   delete self->schema;
   self->schema = s;
+  init_caches(self);
   Py_XINCREF(err); Py_XDECREF(self->error); self->error = err;
   Py_XINCREF(dumps); Py_XDECREF(self->dumps); self->dumps = dumps;
   Py_XINCREF(loads); Py_XDECREF(self->loads); self->loads = loads;
@@ -977,6 +1191,7 @@ int codec_init(CodecObject* self, PyObject* args, PyObject*) {
 }
 
 void codec_dealloc(CodecObject* self) {
+  clear_caches(self);
   delete self->schema;
   delete self->canon;
   Py_XDECREF(self->error);
@@ -993,6 +1208,10 @@ PyMethodDef codec_methods[] = {
     {"to_json", (PyCFunction)c_to_json, METH_VARARGS, "JSON bytes with metadata.resourceVersion injected"},
     {"message_for", (PyCFunction)c_message_for, METH_VARARGS, "message name or None"},
     {"set_canonical", (PyCFunction)c_set_canonical, METH_VARARGS, "kind -> apiVersion reported by to_json"},
+    {"with_rv", (PyCFunction)c_with_rv, METH_VARARGS, "envelope with metadata.resourceVersion set, or None"},
+    {"watch_frame", (PyCFunction)c_watch_frame, METH_VARARGS, "length-delimited protobuf WatchEvent frame"},
+    {"decode_watch_frames", (PyCFunction)c_decode_watch_frames, METH_VARARGS,
+     "(events [(type, object)], bytes consumed) from a buffer of watch frames"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyTypeObject CodecType = {PyVarObject_HEAD_INIT(nullptr, 0)};

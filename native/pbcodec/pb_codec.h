@@ -813,4 +813,117 @@ class JsonWriter {
   }
 };
 
+// ---------------------------------------------------------------------------------------------
+// Protobuf watch streams (`application/vnd.kubernetes.protobuf;stream=watch`): apimachinery's
+// RawSerializer + LengthDelimitedFramer (`runtime/serializer/protobuf/protobuf.go:436`,
+// `endpoints/handlers/watch.go:166-226`). A frame is a 4-byte big-endian length followed by
+// metav1.WatchEvent{1: type, 2: RawExtension{1: raw}}, raw = the object in the embedded
+// (`k8s\0` envelope) encoding. etcd3 stores objects without their resourceVersion, so the
+// envelope is rewritten with ObjectMeta.resourceVersion (field 6) = the revision.
+inline void pb_put_varint(std::string& o, uint64_t v) {
+  while (v >= 0x80) {
+    o += (char)((v & 0x7F) | 0x80);
+    v >>= 7;
+  }
+  o += (char)v;
+}
+
+inline void pb_put_ld(std::string& o, uint32_t num, const void* p, size_t n) {
+  pb_put_varint(o, ((uint64_t)num << 3) | 2);
+  pb_put_varint(o, n);
+  o.append((const char*)p, n);
+}
+
+// `k8s\0` envelope -> the same envelope with metadata.resourceVersion = rv. False when the
+// value is not an envelope of a kind in the schema.
+inline bool envelope_with_rv(const Schema& s, const uint8_t* p, size_t n, const char* rv, std::string& out) {
+  if (n < 4 || memcmp(p, "k8s\0", 4) != 0) return false;
+  Reader r{p + 4, p + n};
+  std::string av, kind;
+  const uint8_t *tm = nullptr, *raw = nullptr;
+  size_t tm_n = 0, raw_n = 0;
+  std::string tail;   // contentEncoding / contentType, kept as they were
+  uint32_t num; uint8_t wt; uint64_t v; const uint8_t* q; size_t l;
+  while (!r.done()) {
+    if (!r.next(&num, &wt, &v, &q, &l)) return false;
+    if (num == 1 && wt == 2) {
+      tm = q; tm_n = l;
+      Reader t{q, q + l};
+      uint32_t n2; uint8_t w2; uint64_t v2; const uint8_t* q2; size_t l2;
+      while (!t.done()) {
+        if (!t.next(&n2, &w2, &v2, &q2, &l2)) return false;
+        if (n2 == 1 && w2 == 2) av.assign((const char*)q2, l2);
+        else if (n2 == 2 && w2 == 2) kind.assign((const char*)q2, l2);
+      }
+    } else if (num == 2 && wt == 2) {
+      raw = q; raw_n = l;
+    } else if (wt == 2) {
+      pb_put_ld(tail, num, q, l);
+    }
+  }
+  int mi = s.message_for(av, kind);
+  if (mi < 0) return false;
+  const Message& m = s.msgs[mi];
+  uint32_t meta_num = m.metadata >= 0 ? m.fields[m.metadata].num : 0;
+  size_t rvn = strlen(rv);
+  std::string body;
+  body.reserve(raw_n + rvn + 16);
+  bool had_meta = false;
+  const uint8_t* rb = raw ? raw : p + n;      // an empty range when the envelope has no raw field
+  Reader b{rb, rb + raw_n};
+  const uint8_t* last = b.p;
+  while (!b.done()) {
+    const uint8_t* start = b.p;
+    if (!b.next(&num, &wt, &v, &q, &l)) return false;
+    if (meta_num && num == meta_num && wt == 2 && !had_meta) {
+      body.append((const char*)last, (size_t)(start - last));
+      std::string meta;
+      meta.reserve(l + rvn + 4);
+      Reader mr{q, q + l};
+      const uint8_t* mlast = mr.p;
+      uint32_t n3; uint8_t w3; uint64_t v3; const uint8_t* q3; size_t l3;
+      while (!mr.done()) {
+        const uint8_t* ms = mr.p;
+        if (!mr.next(&n3, &w3, &v3, &q3, &l3)) return false;
+        if (n3 == 6) {               // drop any stored resourceVersion
+          meta.append((const char*)mlast, (size_t)(ms - mlast));
+          mlast = mr.p;
+        }
+      }
+      meta.append((const char*)mlast, (size_t)(mr.p - mlast));
+      pb_put_ld(meta, 6, rv, rvn);
+      pb_put_ld(body, meta_num, meta.data(), meta.size());
+      had_meta = true;
+      last = b.p;
+    }
+  }
+  body.append((const char*)last, (size_t)(b.p - last));
+  if (meta_num && !had_meta) {
+    std::string meta;
+    pb_put_ld(meta, 6, rv, rvn);
+    pb_put_ld(body, meta_num, meta.data(), meta.size());
+  }
+  out.assign("k8s\0", 4);
+  if (tm) pb_put_ld(out, 1, tm, tm_n);
+  pb_put_ld(out, 2, body.data(), body.size());
+  out += tail;
+  return true;
+}
+
+// one length-delimited WatchEvent frame carrying `raw` (an envelope, or JSON bytes for values
+// this schema cannot express — clients decode by the `k8s\0` magic)
+inline void watch_event_frame(std::string& out, const char* type, const void* raw, size_t raw_n) {
+  std::string ext;
+  ext.reserve(raw_n + 8);
+  pb_put_ld(ext, 1, raw, raw_n);
+  std::string ev;
+  ev.reserve(ext.size() + 24);
+  pb_put_ld(ev, 1, type, strlen(type));
+  pb_put_ld(ev, 2, ext.data(), ext.size());
+  uint32_t n = (uint32_t)ev.size();
+  char hdr[4] = {(char)(n >> 24), (char)(n >> 16), (char)(n >> 8), (char)n};
+  out.append(hdr, 4);
+  out += ev;
+}
+
 }  // namespace pbc

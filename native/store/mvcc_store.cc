@@ -572,6 +572,9 @@ struct Index {
   // fan-out thread and revision; the thread owning this Index is the only one touching it)
   mutable std::string json;
   mutable int64_t json_rv = -1;
+  // protobuf watchers: the stored envelope with metadata.resourceVersion = pb_rv
+  mutable std::string pbenv;
+  mutable int64_t pb_rv = -1;
 };
 
 struct JsonCursor {
@@ -749,6 +752,7 @@ struct Requirement {
 
 struct FanWatch {
   int fd = -1;
+  bool pb = false;        // protobuf watch frames instead of JSON lines
   std::string prefix;
   int64_t min_rev = 0;
   std::vector<Requirement> reqs;
@@ -798,6 +802,42 @@ static std::string_view object_json(const std::string& v, const Index& ix, int64
   return std::string_view(v).substr(body);
 }
 
+// the embedded object of a protobuf watch frame: the envelope with its resourceVersion (cached
+// on the Index like the JSON form), or the stored JSON for values that are not protobuf
+static std::string_view object_pb(const std::string& v, const Index& ix, int64_t rv) {
+  size_t body = ix.body;
+#ifdef KAMD_STORE_SERVER
+  if (g_pb_schema && v.size() >= body + 4 && memcmp(v.data() + body, "k8s\0", 4) == 0) {
+    if (ix.pb_rv != rv) {
+      ix.pbenv.clear();
+      char rs[24];
+      snprintf(rs, sizeof rs, "%lld", (long long)rv);
+      if (!pbc::envelope_with_rv(*g_pb_schema, (const uint8_t*)v.data() + body, v.size() - body, rs, ix.pbenv))
+        ix.pbenv.assign(v.data() + body, v.size() - body);
+      ix.pb_rv = rv;
+    }
+    return ix.pbenv;
+  }
+#endif
+  (void)rv;
+  return std::string_view(v).substr(body);
+}
+
+static void chunk_pb(std::string* out, const char* type, std::string_view obj) {
+  std::string fr;
+#ifdef KAMD_STORE_SERVER
+  pbc::watch_event_frame(fr, type, obj.data(), obj.size());
+#endif
+  char hex[24];
+  int hl = snprintf(hex, sizeof hex, "%zx\r\n", fr.size());
+  out->append(hex, (size_t)hl);
+  out->append(fr);
+  out->append("\r\n", 2);
+}
+
+// one event of watch w (JSON line or protobuf frame)
+static void emit(FanWatch* w, const char* type, const std::string& v, const Index& ix, int64_t rv);
+
 static void chunk(std::string* out, const char* type, std::string_view obj) {
   // {"type":"X","object":<object JSON>}\n as one HTTP chunk
   static const char pre[] = "{\"type\":\"";
@@ -811,6 +851,11 @@ static void chunk(std::string* out, const char* type, std::string_view obj) {
   out->append(mid, sizeof mid - 1);
   out->append(obj.data(), obj.size());
   out->append("}\n\r\n", 4);
+}
+
+static void emit(FanWatch* w, const char* type, const std::string& v, const Index& ix, int64_t rv) {
+  if (w->pb) chunk_pb(&w->out, type, object_pb(v, ix, rv));
+  else chunk(&w->out, type, object_json(v, ix, rv));
 }
 
 // Watch fan-out thread. Kubernetes watch streams handed over by the API server workers are
@@ -940,7 +985,7 @@ class FanOut {
     if (w->send_initial) {
       for (const auto& kv : w->initial) {
         const Index& ix = index_of(*kv, slot_);
-        if (w->matches(ix)) chunk(&w->out, "ADDED", object_json(kv->value, ix, kv->mod_rev));
+        if (w->matches(ix)) emit(raw, "ADDED", kv->value, ix, kv->mod_rev);
       }
     }
     for (const Event& e : w->replay) fan_one(raw, e);
@@ -977,13 +1022,13 @@ class FanOut {
     bool was = ev.prev && w->matches(*prv);
     const std::string& v = ev.kv->value;
     if (ev.type == 0) {
-      if (now && was) chunk(&w->out, "MODIFIED", object_json(v, *cur, ev.rev));
-      else if (now) chunk(&w->out, "ADDED", object_json(v, *cur, ev.rev));
-      else if (was) chunk(&w->out, "DELETED", object_json(v, *cur, ev.rev));
+      if (now && was) emit(w, "MODIFIED", v, *cur, ev.rev);
+      else if (now) emit(w, "ADDED", v, *cur, ev.rev);
+      else if (was) emit(w, "DELETED", v, *cur, ev.rev);
       else return;
     } else {
       if (!(now || was) || !cur->ok) return;
-      chunk(&w->out, "DELETED", object_json(v, *cur, ev.rev));
+      emit(w, "DELETED", v, *cur, ev.rev);
     }
     mark_fan(w);
   }
@@ -1569,7 +1614,8 @@ class Server {
       for (uint16_t j = 0; j < nv && r.ok; ++j) q.vals.push_back(r.str());
       w->reqs.push_back(std::move(q));
     }
-    if (!r.ok || ver != 1) { close(client); return; }
+    if (ver == 2) w->pb = r.get<uint8_t>() == 1;   // v2: trailing format byte
+    if (!r.ok || (ver != 1 && ver != 2)) { close(client); return; }
     for (const Requirement& q : w->reqs)
       if (q.target == 1 && q.op == 0 && q.vals.size() == 1 && q.key == "spec.nodeName") {
         // kubelets watch their own node's pods (cacher.go's nodeName-indexed watchers)
@@ -1582,8 +1628,9 @@ class Server {
     int one = 1;
     setsockopt(client, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     if (timeout > 0) w->deadline = mono_now() + timeout;
-    w->out = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n"
-             "Cache-Control: no-cache, private\r\n\r\n";
+    w->out = std::string("HTTP/1.1 200 OK\r\nContent-Type: ") +
+             (w->pb ? "application/vnd.kubernetes.protobuf;stream=watch" : "application/json") +
+             "\r\nTransfer-Encoding: chunked\r\nCache-Control: no-cache, private\r\n\r\n";
     if (send_initial) {
       // the snapshot is taken here, in commit order; the fan-out thread parses and formats it
       w->send_initial = true;
@@ -1596,9 +1643,18 @@ class Server {
                  "{\"type\":\"ERROR\",\"object\":{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"metadata\":{},"
                  "\"status\":\"Failure\",\"message\":\"too old resource version: %lld (%lld)\",\"reason\":\"Expired\","
                  "\"code\":410}}\n", (long long)from, (long long)eng_->compacted());
-        char hex[24];
-        int hl = snprintf(hex, sizeof hex, "%zx\r\n", strlen(b));
-        w->out.append(hex, (size_t)hl).append(b).append("\r\n0\r\n\r\n");
+        if (w->pb) {
+          // the Status object, embedded as JSON in an ERROR frame (clients decode by magic)
+          std::string st(b);
+          size_t o = st.find("\"object\":") + 9;
+          st = st.substr(o, st.size() - o - 2);
+          chunk_pb(&w->out, "ERROR", st);
+          w->out.append("0\r\n\r\n");
+        } else {
+          char hex[24];
+          int hl = snprintf(hex, sizeof hex, "%zx\r\n", strlen(b));
+          w->out.append(hex, (size_t)hl).append(b).append("\r\n0\r\n\r\n");
+        }
         w->dead = true;   // close once written
       } else {
         w->replay.reserve(evs.size());

@@ -340,3 +340,33 @@ def test_lite_server_bounds_what_a_peer_can_make_it_hold():
         finally:
             await plugin.stop()
     asyncio.run(main())
+
+
+def test_lite_client_queues_calls_over_peer_max_concurrent_streams(monkeypatch):
+    """a grpclite client honours the peer's SETTINGS_MAX_CONCURRENT_STREAMS — calls over
+    it wait for a free stream instead of being refused (UNAVAILABLE); and an
+    INITIAL_WINDOW_SIZE change that overflows an open stream's window is a FLOW_CONTROL_ERROR."""
+    monkeypatch.setattr(gl, "MAX_CONCURRENT_STREAMS", 4)
+
+    async def main():
+        d = tempfile.mkdtemp()
+        sock = os.path.join(d, "p.sock")
+        plugin = await _Plugin("amd.com/gpu", sock, [device("g0")]).start()
+        ch = gl.Channel("unix://" + sock)
+        try:
+            dp = api.device_plugin_stub(ch)
+            reqs = [api.DP["AdmitPodRequest"](pod_name=f"q{i}") for i in range(40)]
+            resps = await asyncio.gather(*[dp.AdmitPod(r, timeout=10) for r in reqs])
+            assert [r.pod.annotations["amd.com/admitted"] for r in resps] == [f"q{i}" for i in range(40)]
+            assert ch._conn.peer_max_streams == 4 and not ch._conn.slot_waiters
+            # window overflow through a SETTINGS delta
+            conn = ch._conn
+            st = conn.streams.setdefault(201, gl._Stream(201, gl._MAX_WINDOW - 10))
+            with pytest.raises(gl._ConnError) as ei:
+                conn._on_frame(gl.SETTINGS, 0, 0, struct.pack(">HI", gl.S_INITIAL_WINDOW_SIZE, conn.peer_initial + 100))
+            assert ei.value.code == gl.E_FLOW_CONTROL
+            conn.streams.pop(201, None)
+        finally:
+            await ch.close()
+            await plugin.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))

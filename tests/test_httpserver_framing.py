@@ -75,3 +75,55 @@ def test_request_framing():
         finally:
             await srv.stop()
     asyncio.run(main())
+
+
+def test_chunked_body_in_many_reads_is_linear_and_sizes_are_strict():
+    """a chunked body sent as many small chunks over many reads is parsed once per
+    byte (the parse state lives on the connection), chunk sizes are 1*HEXDIG only, and a
+    rejection queued behind an earlier pipelined request is answered after it."""
+    async def main():
+        seen = []
+
+        async def handler(req):
+            seen.append(len(req.body))
+            await asyncio.sleep(0.05 if req.path == "/slow" else 0)
+            return hs.Response(200, b"%d" % len(req.body), "text/plain")
+        srv = hs.HTTPServer(handler)
+        srv.max_body = 8 << 20
+        await srv.start()
+        port = srv.port
+        try:
+            import time
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            w.write(b"POST /big HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n")
+            chunk = b"8\r\n" + b"x" * 8 + b"\r\n"
+            n = 40000                                   # 320 KiB in 8-byte chunks, 400 writes
+            t0 = time.perf_counter()
+            for i in range(0, n, 100):
+                w.write(chunk * 100)
+                await w.drain()
+                await asyncio.sleep(0)
+            w.write(b"0\r\n\r\n")
+            await w.drain()
+            head = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 10)
+            assert head.startswith(b"HTTP/1.1 200") and seen == [8 * n]
+            assert time.perf_counter() - t0 < 5.0
+            w.close()
+            # too many chunks: refused (framing bytes / chunk count are bounded)
+            seen.clear()
+            d = await _exchange(port, b"POST /many HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n" +
+                                b"1\r\nx\r\n" * (hs.MAX_CHUNKS + 5) + b"0\r\n\r\n")
+            assert d.startswith(b"HTTP/1.1 413") and seen == []
+            # sizes Go's strconv.ParseInt(.., 16, 64) would refuse
+            for bad in (b"0x1f", b"+1f", b"1_f", b" ", b"12345678901234567"):
+                d = await _exchange(port, b"POST /e HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n" + bad +
+                                    b"\r\n" + b"a" * 31 + b"\r\n0\r\n\r\n")
+                assert d.startswith(b"HTTP/1.1 400"), (bad, d[:40])
+            assert seen == []
+            # a slow request, then a bad one pipelined behind it: responses stay in order
+            d = await _exchange(port, b"POST /slow HTTP/1.1\r\nContent-Length: 2\r\n\r\nok"
+                                      b"POST /bad HTTP/1.1\r\nContent-Length: -1\r\n\r\n")
+            assert d.index(b"HTTP/1.1 200") < d.index(b"HTTP/1.1 400"), d
+        finally:
+            await srv.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))

@@ -76,6 +76,48 @@ def test_header_block_bomb_ends_the_session():
     assert len(ok) == 1 and ok[0].headers["streamtype"] == ["error"]
 
 
+def test_session_outlives_max_streams_sequential_streams():
+    """the MAX_STREAMS cap counts open streams only. One session opens and closes
+    2 * MAX_STREAMS + 10 streams one after another (client FIN + server FIN, or a reset) and
+    every one is served; the session tracks no closed stream."""
+    async def main():
+        served = []
+
+        async def on_stream(st):
+            async def echo():
+                d = await st.read()
+                if not st.reset:
+                    await st.write(b"re:" + d, fin=True)
+            served.append(asyncio.ensure_future(echo()))
+
+        srv_box = {}
+
+        async def handler(r, w):
+            c = spdy.Connection(r, w, server=True, on_stream=on_stream)
+            srv_box["c"] = c
+            await c.serve()
+        server = await asyncio.start_server(handler, "127.0.0.1", 0)
+        port = server.sockets[0].getsockname()[1]
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        cli = spdy.Connection(r, w, server=False)
+        task = asyncio.ensure_future(cli.serve())
+        n = 2 * spdy.MAX_STREAMS + 10
+        for i in range(n):
+            st = await cli.create_stream({"streamtype": "data", "i": str(i)})
+            if i % 7 == 3:
+                await st.reset_stream()
+                continue
+            await st.write(b"x%d" % i, fin=True)
+            assert await st.read() == b"re:x%d" % i
+        await asyncio.sleep(0.05)
+        assert len(srv_box["c"].streams) == 0 and len(cli.streams) == 0
+        assert len(served) == n
+        await cli.close()
+        task.cancel()
+        server.close()
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
 SLEEPER = "import time\nwhile True: time.sleep(1)\n"
 ECHO = ("import socket,sys\n"
         "s=socket.socket(); s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)\n"

@@ -89,3 +89,24 @@ def test_flexvolume_and_git_repo(run, tmp_path):
         finally:
             await cl.stop()
     run(main(), timeout=90)
+
+
+def test_fs_group_ownership_never_follows_symlinks(tmp_path):
+    """the fsGroup walk changes entries through O_PATH|O_NOFOLLOW descriptors, so a
+    symlink a container planted in its volume never makes the kubelet chmod the target."""
+    import os
+    import stat
+    from kubernetes_amd.kubelet.volumes import set_volume_ownership
+    outside = tmp_path / "host-secret"
+    outside.write_text("x")
+    os.chmod(outside, 0o600)
+    vol = tmp_path / "vol"
+    (vol / "sub").mkdir(parents=True)
+    (vol / "sub" / "f").write_text("y")
+    os.chmod(vol / "sub" / "f", 0o600)
+    os.symlink(outside, vol / "sub" / "link")
+    set_volume_ownership(str(vol), os.getgid(), readonly=False)
+    assert stat.S_IMODE(os.stat(outside).st_mode) == 0o600          # untouched
+    assert stat.S_IMODE(os.stat(vol / "sub" / "f").st_mode) == 0o660
+    d = os.stat(vol / "sub").st_mode
+    assert d & stat.S_ISGID and d & 0o010
