@@ -93,8 +93,10 @@ class Controller:
             if shutdown:
                 return
             try:
-                await self.sync(key)
-                self.queue.forget(key)
+                # a sync returning False keeps the key's backoff history (the job controller counts
+                # consecutive failed-pod retries against backoffLimit); anything else forgets it
+                if await self.sync(key) is not False:
+                    self.queue.forget(key)
                 self.syncs += 1
             except asyncio.CancelledError:
                 raise

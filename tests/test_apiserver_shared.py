@@ -264,7 +264,7 @@ def test_native_watch_fanout_semantics(run, store):
             er = p["spec"]["extendedResources"][0]["name"]
             await a.bind("default", "x2", "gpu-node-1", {er: {"resources": ["g0"]}})
             await a.delete("pods", "x2", "default", grace_period=0)
-            await _eventually(lambda: asyncio.sleep(0, len(sel_events) >= 4 and len(node_events) >= 2))
+            await _eventually(lambda: asyncio.sleep(0, len(sel_events) >= 5 and len(node_events) >= 2))
             assert sel_events == [("ADDED", "x1"), ("ADDED", "x2"), ("DELETED", "x1"), ("MODIFIED", "x2"),
                                   ("DELETED", "x2")][:len(sel_events)] and len(sel_events) == 5
             assert node_events == [("ADDED", "x2"), ("DELETED", "x2")]

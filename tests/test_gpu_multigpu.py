@@ -58,3 +58,65 @@ def test_multigpu_e2e_spec_on_real_mi355x(run):
             res = await run_specs(cl.url, focus="Feature:MultiGPU", timeout=240)
         assert len(res) == 1 and res[0].ok and not res[0].skipped, res[0].error if res else "no spec ran"
     run(main(), timeout=300)
+
+
+HIP_PROBE = r'''
+import ctypes, glob, json, os
+out = {"open": {}}
+for p in sorted(glob.glob("/dev/dri/renderD*")):
+    try:
+        os.close(os.open(p, os.O_RDWR))
+        out["open"][os.path.basename(p)] = "OPEN"
+    except OSError as e:
+        out["open"][os.path.basename(p)] = __import__("errno").errorcode.get(e.errno, str(e.errno))
+hip = ctypes.CDLL("libamdhip64.so")
+n = ctypes.c_int(-1)
+out["hipGetDeviceCount"] = hip.hipGetDeviceCount(ctypes.byref(n))
+out["devices"] = n.value
+if n.value == 1:
+    a, b, c = (ctypes.POINTER(ctypes.c_float)() for _ in range(3))
+    out["hipMalloc"] = hip.hipMalloc(ctypes.byref(a), ctypes.c_size_t(1 << 20))
+    out["hipFree"] = hip.hipFree(a)
+print("HIP " + json.dumps(out, sort_keys=True))
+'''
+
+
+def test_landlock_pod_on_a_multi_gpu_node_sees_exactly_its_gpu(tmp_path):
+    """Confinement on a real multi-GPU node (skips on the one-GPU lease): for every GPU k, a
+    Landlock-tier container allowed only renderD(k) runs HIP (init + an allocation), counts
+    exactly one device, and gets EACCES opening every sibling render node. This is the case the
+    one-GPU lease cannot show: ROCr must skip the EACCES'd siblings rather than fail to start."""
+    import glob
+    import json
+    import os
+    import subprocess
+    import sys
+    from kubernetes_amd.kubelet.runtime import process as proc_rt
+    nodes = sorted(glob.glob("/dev/dri/renderD*"))
+    if len(nodes) < 2:
+        pytest.skip(f"needs >= 2 render nodes (this host has {len(nodes)})")
+    if proc_rt.runc_features().get("tier") != "landlock":
+        pytest.skip("this host is not on the Landlock tier")
+    probe = tmp_path / "hip_probe.py"
+    probe.write_text(HIP_PROBE)
+    for k, node in enumerate(nodes):
+        b = tmp_path / f"b{k}"
+        b.mkdir()
+        spec = {"process": {"args": [sys.executable, str(probe)], "cwd": "/",
+                            "env": ["PATH=/usr/bin:/bin", "HSA_ENABLE_IPC_MODE_LEGACY=0",
+                                    "LD_LIBRARY_PATH=/opt/rocm/lib"]},
+                "root": {"path": "/"}, "mounts": [],
+                "annotations": {"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": "/dev/dri"},
+                "linux": {"devices": [{"path": node}], "namespaces": []}}
+        (b / "config.json").write_text(json.dumps(spec))
+        r = subprocess.run([proc_rt.KAMD_RUNC, "run", "--bundle", str(b)], capture_output=True, text=True,
+                           timeout=120)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HIP ")]
+        assert r.returncode == 0 and line, (node, r.stdout[-1500:], r.stderr[-1500:])
+        res = json.loads(line[0][4:])
+        print("GPU", k, node, res)
+        mine = os.path.basename(node)
+        assert res["open"][mine] == "OPEN", res
+        assert all(v == "EACCES" for n, v in res["open"].items() if n != mine), res
+        assert res["hipGetDeviceCount"] == 0 and res["devices"] == 1, res
+        assert res["hipMalloc"] == 0, res

@@ -497,3 +497,80 @@ def test_landlock_enforced_on_this_host(tmp_path):
     assert "NODE renderD128 EACCES" in r.stdout and "NODE card0 EACCES" in r.stdout, r.stdout
     rep = json.loads((b / "isolation.json").read_text())
     assert rep["tier"] == "landlock"
+
+
+HSA_PROBE = r'''
+import ctypes, glob, json, os, sys
+out = {"render_nodes": sorted(os.path.basename(p) for p in glob.glob("/dev/dri/renderD*"))}
+opened = {}
+for p in out["render_nodes"]:
+    try:
+        os.close(os.open("/dev/dri/" + p, os.O_RDWR))
+        opened[p] = "OPEN"
+    except OSError as e:
+        opened[p] = __import__("errno").errorcode.get(e.errno, str(e.errno))
+out["open"] = opened
+lib = None
+for cand in ("libhsa-runtime64.so.1", "/opt/rocm/lib/libhsa-runtime64.so.1"):
+    try:
+        lib = ctypes.CDLL(cand)
+        break
+    except OSError:
+        pass
+st = lib.hsa_init()
+kinds = []
+CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p)
+def cb(agent, data):
+    t = ctypes.c_int(-1)
+    lib.hsa_agent_get_info(ctypes.c_uint64(agent), 17, ctypes.byref(t))   # HSA_AGENT_INFO_DEVICE
+    kinds.append(t.value)
+    return 0
+keep = CB(cb)
+if st == 0:
+    lib.hsa_iterate_agents(keep, None)
+    lib.hsa_shut_down()
+out["hsa_init"] = st
+out["gpu_agents"] = kinds.count(1)
+out["cpu_agents"] = kinds.count(0)
+print("HSA " + json.dumps(out, sort_keys=True))
+'''
+
+
+@pytest.mark.gpu
+def test_rocr_start_under_landlock_denial(tmp_path):
+    """What the MI355X runtime does when Landlock denies render nodes (EACCES, not the device
+    cgroup's EPERM): a container allowed its node sees that GPU; a container denied every node
+    must start HSA cleanly with zero GPU agents (the thunk skips the node) — the behaviour a
+    confined pod on an 8-GPU node relies on for its sibling GPUs. Measured on the box, printed."""
+    import sys
+    f = runc_features()
+    if f.get("tier") != "landlock":
+        pytest.skip(f"this host's tier is {f.get('tier')}, not landlock: {f}")
+    nodes = sorted(glob_render())
+    if not nodes:
+        pytest.skip("no /dev/dri/renderD* on this host")
+    probe = tmp_path / "hsa_probe.py"
+    probe.write_text(HSA_PROBE)
+    results = {}
+    for label, allowed in (("allowed", [nodes[0]]), ("denied", [])):
+        b = tmp_path / f"bundle-{label}"
+        b.mkdir()
+        spec = {"process": {"args": [sys.executable, str(probe)],
+                            "env": ["PATH=/usr/bin:/bin", "HSA_ENABLE_IPC_MODE_LEGACY=0"], "cwd": "/"},
+                "root": {"path": "/"}, "mounts": [],
+                "annotations": {"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": "/dev/dri"},
+                "linux": {"devices": [{"path": p} for p in allowed], "namespaces": []}}
+        (b / "config.json").write_text(json.dumps(spec))
+        r = subprocess.run([proc_rt.KAMD_RUNC, "run", "--bundle", str(b)], capture_output=True, text=True, timeout=120)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HSA ")]
+        assert r.returncode == 0 and line, (label, r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        results[label] = json.loads(line[0][4:])
+    print("LANDLOCK_ROCR", json.dumps(results, sort_keys=True))
+    assert results["allowed"]["hsa_init"] == 0 and results["allowed"]["gpu_agents"] == 1, results
+    assert results["denied"]["open"][os.path.basename(nodes[0])] == "EACCES", results
+    assert results["denied"]["hsa_init"] == 0 and results["denied"]["gpu_agents"] == 0, results
+
+
+def glob_render():
+    import glob
+    return glob.glob("/dev/dri/renderD*")
