@@ -1184,18 +1184,51 @@ class APIServer:
                         raise APIError(409, "Conflict", f"device {node}/{rn}/{i} is already assigned to {owner.rsplit('/', 2)[-2]}/{owner.rsplit('/', 1)[-1]}")
         return await self._commit(ri, key, MODIFIED, pod, prev)
 
+    MAX_DISRUPTED_PODS = 2000          # eviction.go MaxDisruptedPodSize
+
     async def evict(self, namespace, name, eviction, user=None):
+        """`pkg/registry/core/pod/storage/eviction.go`: an eviction is checked against the pod's
+        PodDisruptionBudget and, when allowed, DECREMENTS it — disruptionsAllowed - 1 and the pod
+        recorded in status.disruptedPods, written with the budget's resourceVersion (a conflict
+        re-reads and re-checks), so concurrent evictions can never spend one disruption twice —
+        before the pod is deleted. More than one matching budget is refused (500), as is a
+        budget whose status the disruption controller has not caught up with (429)."""
         ri = m.BY_PLURAL["pods"]
-        # PodDisruptionBudget check
         pod = (await self._aexisting(ri, namespace, name))[1].obj
         labels = (pod.get("metadata") or {}).get("labels") or {}
         from ..api.labels import label_selector_as_selector
-        for pdb in self.list_objects("poddisruptionbudgets", namespace):
-            sel = label_selector_as_selector((pdb.get("spec") or {}).get("selector"))
-            if sel.matches(labels):
-                allowed = (pdb.get("status") or {}).get("disruptionsAllowed", (pdb.get("status") or {}).get("podDisruptionsAllowed", 0))
-                if allowed <= 0:
-                    raise APIError(429, "TooManyRequests", "Cannot evict pod as it would violate the pod's disruption budget.")
+        pri = m.BY_PLURAL["poddisruptionbudgets"]
+        for attempt in range(8):
+            pdbs = [p for p in self.list_objects("poddisruptionbudgets", namespace)
+                    if label_selector_as_selector((p.get("spec") or {}).get("selector")).matches(labels)]
+            if not pdbs:
+                break
+            if len(pdbs) > 1:
+                raise APIError(500, "InternalError",
+                               "This pod has more than one PodDisruptionBudget, which the eviction subresource does not support.")
+            pdb = pdbs[0]
+            st = dict(pdb.get("status") or {})
+            too_many = APIError(429, "TooManyRequests", "Cannot evict pod as it would violate the pod's disruption budget.")
+            if int(st.get("observedGeneration") or 0) < int(pdb["metadata"].get("generation") or 0):
+                raise too_many
+            allowed = st.get("disruptionsAllowed", st.get("podDisruptionsAllowed", 0)) or 0
+            if allowed <= 0:
+                raise too_many
+            disrupted = dict(st.get("disruptedPods") or {})
+            if len(disrupted) > self.MAX_DISRUPTED_PODS:
+                raise APIError(403, "Forbidden", "DisruptedPods map too big - too many evictions not confirmed by PDB controller")
+            disrupted[name] = now_rfc3339()
+            st["disruptionsAllowed"] = allowed - 1
+            st["disruptedPods"] = disrupted
+            upd = dict(pdb, status=st)
+            upd["metadata"] = dict(pdb["metadata"])
+            try:
+                await self.update(pri, namespace, m.name_of(pdb), upd, None, "status")
+                break
+            except APIError as e:
+                if e.code != 409 or attempt == 7:
+                    raise
+                await asyncio.sleep(0)
         return await self.delete(ri, namespace, name, (eviction or {}).get("deleteOptions") or {}, user)
 
     # ------------------------------------------------------------------

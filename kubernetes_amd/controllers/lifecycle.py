@@ -33,17 +33,47 @@ class NamespaceController(Controller):
         if ns["metadata"].get("deletionTimestamp"):
             self.enqueue(ns["metadata"]["name"])
 
+    async def namespaced_resources(self):
+        """Every namespaced resource that supports list + delete, from discovery (custom
+        resources included — `namespaced_resources_deleter.go` uses the discovery client too);
+        the compiled-in set when discovery is unavailable."""
+        if hasattr(self.client, "raw"):
+            from .garbagecollector import discover
+            try:
+                lists = await discover(self.client)
+            except (APIStatusError, OSError, ConnectionError):
+                lists = None
+            if lists:
+                out, seen = [], set()
+                for rl in lists:
+                    gv = rl.get("groupVersion") or ""
+                    group, _, version = gv.rpartition("/")
+                    for r in rl.get("resources") or ():
+                        name = r.get("name") or ""
+                        if "/" in name or not r.get("namespaced") or (group, name) in seen:
+                            continue
+                        seen.add((group, name))
+                        if not {"list", "delete"}.issubset(r.get("verbs") or ()):
+                            continue
+                        canon = m.BY_PLURAL.get(name) if (group, version, name) in m.ALIASES else None
+                        if canon is not None and canon.group != group:
+                            continue
+                        if group == "" and name == "events":
+                            continue            # events go last, with the namespace
+                        out.append(m.ResourceInfo(group, version, r.get("kind") or "", name, True))
+                return out
+        return [ri for ri in m.RESOURCES if ri.namespaced and ri.plural not in m.VIRTUAL]
+
     async def sync(self, key):
         ns = self.ns_inf.get(key)
         if ns is None or not ns["metadata"].get("deletionTimestamp"):
             return
         name = ns["metadata"]["name"]
         remaining = 0
-        for ri in m.RESOURCES:
-            if not ri.namespaced:
-                continue
+        for ri in await self.namespaced_resources():
+            handle = ri.plural if (m.BY_PLURAL.get(ri.plural) or ri).group == ri.group else ri
             try:
-                lst = await self.client.list(ri.plural, name)
+                lst = await self.client.list(handle, name)
             except APIStatusError:
                 continue
             for o in lst.get("items") or ():
@@ -51,7 +81,7 @@ class NamespaceController(Controller):
                 if o["metadata"].get("deletionTimestamp") and ri.plural != "pods":
                     continue
                 try:
-                    await self.client.delete(ri.plural, o["metadata"]["name"], name,
+                    await self.client.delete(handle, o["metadata"]["name"], name,
                                              grace_period=0 if ri.plural != "pods" else None)
                 except APIStatusError as e:
                     if not is_not_found(e):
@@ -59,6 +89,10 @@ class NamespaceController(Controller):
         if remaining:
             self.queue.add_after(key, 0.2)   # wait for graceful pod deletion, then finalize
             return
+        try:
+            await self.client.delete_collection("events", name)
+        except APIStatusError:
+            pass
         fins = [f for f in (ns.get("spec") or {}).get("finalizers") or [] if f != "kubernetes"]
         st, body = await self.client.raw("PUT", f"/api/v1/namespaces/{name}/finalize",
                                          _dump({"metadata": {"name": name}, "spec": {"finalizers": fins}}))

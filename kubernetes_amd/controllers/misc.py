@@ -9,11 +9,14 @@ disruptionsAllowed).
 """
 from __future__ import annotations
 
+import time
+
+from ..api import meta as m
 from ..api.labels import label_selector_as_selector, selector_from_set
 from ..api.quantity import Quantity
 from ..apiserver.admission.plugins import pod_usage
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
-from .base import Controller, pod_is_ready, split_key
+from .base import Controller, controller_ref, pod_is_ready, split_key
 
 
 class ServiceAccountController(Controller):
@@ -168,12 +171,24 @@ class ResourceQuotaController(Controller):
 
 
 class DisruptionController(Controller):
+    """`pkg/controller/disruption/disruption.go`: a budget's expected pod count is the pods it
+    selects for an integer minAvailable, and the summed scale of their controllers
+    (ReplicaSet / ReplicationController / StatefulSet / Deployment) for a percentage or any
+    maxUnavailable (`getExpectedPodCount`, `getExpectedScale`); healthy pods are Ready ones not
+    already counted as disrupted; status.disruptedPods entries (written by the eviction
+    subresource) are dropped once the pod is deleted or after DeletionTimeout (2 min), when the
+    budget is looked at again."""
     name = "disruption"
     workers = 2
+    DELETION_TIMEOUT = 120.0
 
     def setup(self):
         self.pdb_inf = self.factory.get("poddisruptionbudgets")
         self.pod_inf = self.factory.get("pods")
+        self.infs = {k: self.factory.get(r) for k, r in (("ReplicaSet", "replicasets"),
+                                                           ("ReplicationController", "replicationcontrollers"),
+                                                           ("StatefulSet", "statefulsets"),
+                                                           ("Deployment", "deployments"))}
         self.pdb_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
         self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
 
@@ -182,33 +197,100 @@ class DisruptionController(Controller):
             if pdb["metadata"].get("namespace") == pod["metadata"].get("namespace"):
                 self.enqueue(pdb)
 
+    def expected_scale(self, pods):
+        """Sum of the scale of every controller that owns a selected pod (each counted once);
+        a pod without a (known) controller makes the count unknowable -> None."""
+        seen = {}
+        for p in pods:
+            ref = controller_ref(p)
+            if ref is None:
+                return None
+            kind = ref.get("kind")
+            key = (kind, ref.get("uid"))
+            if key in seen:
+                continue
+            ctl = None
+            if kind == "ReplicaSet":
+                rs = self.infs["ReplicaSet"].get(f"{m.namespace_of(p)}/{ref['name']}")
+                dref = controller_ref(rs) if rs is not None else None
+                if dref is not None and dref.get("kind") == "Deployment":
+                    d = self.infs["Deployment"].get(f"{m.namespace_of(p)}/{dref['name']}")
+                    if d is not None and m.uid_of(d) == dref.get("uid"):
+                        key, ctl = ("Deployment", m.uid_of(d)), d
+                        if key in seen:
+                            continue
+                if ctl is None:
+                    ctl = rs
+            elif kind in self.infs:
+                ctl = self.infs[kind].get(f"{m.namespace_of(p)}/{ref['name']}")
+            if ctl is None or m.uid_of(ctl) != key[1]:
+                return None
+            seen[key] = int((ctl.get("spec") or {}).get("replicas", 1))
+        return sum(seen.values())
+
     async def sync(self, key):
         pdb = self.pdb_inf.get(key)
         if pdb is None:
             return
         ns, name = split_key(key)
         spec = pdb.get("spec") or {}
-        sel = label_selector_as_selector(spec.get("selector"))
-        pods = [p for p in self.pod_inf.list() if p["metadata"].get("namespace") == ns
-                and sel.matches(p["metadata"].get("labels") or {}) and not p["metadata"].get("deletionTimestamp")]
-        healthy = sum(1 for p in pods if pod_is_ready(p))
-        expected = len(pods)
-        if "minAvailable" in spec:
-            v = spec["minAvailable"]
-            desired = _abs(v, expected)
-        elif "maxUnavailable" in spec:
-            desired = max(0, expected - _abs(spec["maxUnavailable"], expected))
+        raw_sel = spec.get("selector") or {}
+        sel = label_selector_as_selector(raw_sel)
+        # getPodsForPdb: an empty selector selects nothing
+        pods = [] if not (raw_sel.get("matchLabels") or raw_sel.get("matchExpressions")) else \
+            [p for p in self.pod_inf.list() if p["metadata"].get("namespace") == ns
+             and sel.matches(p["metadata"].get("labels") or {})]
+        now = time.time()
+        st0 = pdb.get("status") or {}
+        # disruptedPods: kept while the evicted pod still exists, undeleted, within the timeout
+        by_name = {m.name_of(p): p for p in pods}
+        disrupted, recheck = {}, None
+        for pname, ts in (st0.get("disruptedPods") or {}).items():
+            p = by_name.get(pname)
+            t = m.parse_rfc3339(ts) or 0
+            if p is None or p["metadata"].get("deletionTimestamp") or t + self.DELETION_TIMEOUT < now:
+                continue
+            disrupted[pname] = ts
+            left = t + self.DELETION_TIMEOUT - now
+            recheck = left if recheck is None else min(recheck, left)
+        healthy = sum(1 for p in pods if not p["metadata"].get("deletionTimestamp")
+                      and pod_is_ready(p) and m.name_of(p) not in disrupted)
+        min_avail, max_unavail = spec.get("minAvailable"), spec.get("maxUnavailable")
+        failed = False
+        if max_unavail is not None:
+            expected = self.expected_scale(pods)
+            failed = expected is None
+            expected = expected or 0
+            desired = max(0, expected - _abs(max_unavail, expected, round_up=True))
+        elif min_avail is not None and isinstance(min_avail, str) and min_avail.endswith("%"):
+            expected = self.expected_scale(pods)
+            failed = expected is None
+            expected = expected or 0
+            desired = _abs(min_avail, expected, round_up=True)
         else:
-            desired = expected
+            expected = len(pods)
+            desired = _abs(min_avail, expected) if min_avail is not None else expected
+        allowed = 0 if failed else max(0, healthy - desired)
         st = {"currentHealthy": healthy, "desiredHealthy": desired, "expectedPods": expected,
-              "disruptionsAllowed": max(0, healthy - desired), "observedGeneration": pdb["metadata"].get("generation", 1)}
-        if {k: (pdb.get("status") or {}).get(k) for k in st} == st:
+              "disruptionsAllowed": allowed, "observedGeneration": pdb["metadata"].get("generation", 1),
+              "disruptedPods": disrupted or None}
+        if recheck is not None:
+            self.queue.add_after(key, recheck + 0.05)
+        cur = {k: st0.get(k) for k in st}
+        if cur.get("disruptedPods") == {}:
+            cur["disruptedPods"] = None
+        if cur == st:
             return
-        await self.client.patch("poddisruptionbudgets", name, {"status": st}, ns, "merge", "status")
+        patch = dict(st)
+        if disrupted:          # a merge patch merges maps: dropped entries are nulled explicitly
+            patch["disruptedPods"] = dict({k: None for k in st0.get("disruptedPods") or ()}, **disrupted)
+        await self.client.patch("poddisruptionbudgets", name, {"status": patch}, ns, "merge", "status")
 
 
-def _abs(v, total):
+def _abs(v, total, round_up=True):
+    """intstr.GetValueFromIntOrPercent (the disruption controller rounds up)."""
     if isinstance(v, str) and v.endswith("%"):
         import math
-        return int(math.ceil(float(v[:-1]) * total / 100.0))
+        x = float(v[:-1]) * total / 100.0
+        return int(math.ceil(x) if round_up else math.floor(x))
     return int(v)

@@ -337,3 +337,29 @@ def test_foreground_and_orphan_propagation(run):
                 return not await _exists(c, "replicasets", "fg") and not await pods("fg")
             await cl.wait_for(fg_done, timeout=60)
     run(main(), timeout=150)
+
+
+def test_namespace_deletion_removes_custom_resources(run):
+    """The namespace controller finds what to delete through discovery, so custom resources in
+    a terminating namespace are deleted too (namespaced_resources_deleter.go)."""
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=1, controllers=["namespace"]) as cl:
+            c = cl.client
+            await c.create("customresourcedefinitions", copy.deepcopy(WIDGET_CRD))
+            await c.create("namespaces", {"metadata": {"name": "doomed"}})
+            st, body = await c.raw("POST", "/apis/example.com/v1/namespaces/doomed/widgets", json.dumps(
+                {"apiVersion": "example.com/v1", "kind": "Widget", "metadata": {"name": "w"}}).encode())
+            assert st == 201, body
+            await c.create("configmaps", {"metadata": {"name": "cm", "namespace": "doomed"}})
+            await c.delete("namespaces", "doomed")
+
+            async def gone():
+                try:
+                    await c.get("namespaces", "doomed")
+                    return False
+                except Exception:
+                    return True
+            await cl.wait_for(gone, timeout=30)
+            st, body = await c.raw("GET", "/apis/example.com/v1/namespaces/doomed/widgets")
+            assert st == 200 and json.loads(body)["items"] == []
+    run(main(), timeout=60)
