@@ -71,11 +71,14 @@ class Quantity:
         return float(self.value)
 
     # -- arithmetic ----------------------------------------------------
+    # Quantity.Add / Sub: a zero receiver adopts the operand's format (0 + 1Gi prints "1Gi")
     def __add__(self, o):
-        return Quantity(self.value + _val(o), self.format)
+        fmt = o.format if self.value == 0 and isinstance(o, Quantity) else self.format
+        return Quantity(self.value + _val(o), fmt)
 
     def __sub__(self, o):
-        return Quantity(self.value - _val(o), self.format)
+        fmt = o.format if self.value == 0 and isinstance(o, Quantity) else self.format
+        return Quantity(self.value - _val(o), fmt)
 
     def __neg__(self):
         return Quantity(-self.value, self.format)

@@ -66,6 +66,7 @@ class Chain:
         self.plugins = plugins
         self._mut = [p for p in plugins if type(p).admit is not Plugin.admit]
         self._val = [p for p in plugins if type(p).validate is not Plugin.validate]
+        self._charge = [p for p in plugins if hasattr(p, "charge")]
 
     def admit(self, a: Attributes):
         for p in self._mut:
@@ -76,6 +77,13 @@ class Chain:
         for p in self._val:
             if p.handles(a.operation):
                 p.validate(a)
+
+    async def charge(self, a: Attributes):
+        """Validating plugins whose decision needs an API round trip (ResourceQuota writes the
+        charged usage to the quota object); the last step before the object is committed."""
+        for p in self._charge:
+            if p.handles(a.operation):
+                await p.charge(a)
 
 
 DEFAULT_PLUGINS = [

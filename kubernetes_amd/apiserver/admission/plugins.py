@@ -14,7 +14,9 @@ from __future__ import annotations
 
 import os
 
+from ... import quota
 from ...api import core
+from ...api import meta as m
 from ...api.meta import new_uid
 from ...api.quantity import Quantity, parse_quantity
 from . import CREATE, DELETE, UPDATE, AdmissionError, Attributes, Plugin, register
@@ -424,53 +426,140 @@ class AlwaysDeny(Plugin):
         raise AdmissionError("admission control is denying all modifications")
 
 
+_POD_EVALUATOR = quota.PodEvaluator()
+
+
 def pod_usage(pod) -> dict[str, Quantity]:
-    """Quota usage of a pod, including the fork's pod-level extended resources."""
-    if core.pod_is_terminal(pod):
-        return {}
-    use: dict[str, Quantity] = {"pods": Quantity(1), "count/pods": Quantity(1)}
-    for k, v in core.pod_requests(pod).items():
-        use["requests." + k] = v
-        if k in ("cpu", "memory"):
-            use[k] = v
-        if core.is_extended_resource_name(k):
-            use[k] = v
-    for per in (pod.get("spec") or {}).get("extendedResources") or ():
-        try:
-            rn = core.pod_extended_resource_name(per)
-            n = Quantity(core.pod_extended_resource_count(per))
-        except (ValueError, KeyError):
-            continue
-        for key in ("requests." + rn, rn):
-            use[key] = use[key] + n if key in use else n
-    return use
+    """Quota usage of a pod (`quota.PodEvaluator.usage`), including the fork's pod-level
+    extended resources."""
+    return _POD_EVALUATOR.usage(pod)
 
 
 @register
 class ResourceQuota(Plugin):
-    name = "ResourceQuota"
-    operations = (CREATE,)
+    """`plugin/pkg/admission/resourcequota` (`controller.go` checkRequest / checkQuotas):
 
-    def validate(self, a):
-        if a.resource != "pods" or a.subresource or not self.server:
+      * the evaluator for the request's group/resource decides whether the operation can
+        change usage at all (pods / object counts: CREATE; services: CREATE and UPDATE);
+      * every quota in the namespace that names a matching resource and whose scopes all match
+        is "interesting": its per-kind constraints must hold (pods must state cpu/memory when
+        those are quota'd) and it must already carry usage for every hard name ("status unknown
+        for quota" until the controller has counted);
+      * the request's usage (on UPDATE, the non-negative delta over the old object) is added to
+        status.used, masked to each quota's hard names, and must stay within hard;
+      * the new status.used is written back with the quota's resourceVersion — concurrent
+        admissions therefore serialise on the quota object — and quotas whose write conflicted
+        are re-read and re-checked (3 retries), exactly as the reference's evaluator loop;
+      * `limitedResources` (plugin config) names resources that may only be consumed when some
+        quota covers them ("insufficient quota to consume").
+
+    The check runs in `charge()`, the chain's asynchronous last step before the object is
+    committed, because the status write is an API round trip."""
+    name = "ResourceQuota"
+    operations = (CREATE, UPDATE)
+    RETRIES = 3
+
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        self.registry = quota.Registry()
+        self.limited = list((self.config or {}).get("limitedResources") or ())
+
+    @staticmethod
+    def _group(plural):
+        ri = m.BY_PLURAL.get(plural)
+        return ri.group if ri is not None else ""
+
+    def _limited_names(self, group, resource, usage):
+        """`limitedByDefault`: consumed names matching a configured limitedResources entry."""
+        out = set()
+        for lr in self.limited:
+            if lr.get("resource") != resource or (lr.get("apiGroup") or "") != group:
+                continue
+            for k, v in usage.items():
+                if quota.qty(v) > quota.ZERO and any(mc in k for mc in lr.get("matchContains") or ()):
+                    out.add(k)
+        return out
+
+    def check_request(self, quotas, ev, a, group):
+        """Returns the quotas with status.used as it would be if the request were admitted."""
+        obj = a.obj
+        limited = set()
+        if any(lr.get("resource") == a.resource and (lr.get("apiGroup") or "") == group for lr in self.limited):
+            limited = self._limited_names(group, a.resource, ev.usage(obj))
+        interesting, restricted = [], set()
+        for i, q in enumerate(quotas):
+            if not ev.matches(q, obj):
+                continue
+            st = q.get("status") or {}
+            hard = st.get("hard") or {}
+            names = ev.matching_resources(list(hard))
+            msg = ev.constraints(names, obj)
+            if msg:
+                raise AdmissionError(f"failed quota: {m.name_of(q)}: {msg}")
+            used = st.get("used") or {}
+            if any(k not in used for k in hard):
+                raise AdmissionError(f"status unknown for quota: {m.name_of(q)}")
+            interesting.append(i)
+            restricted.update(names)
+        uncovered = limited - restricted
+        if uncovered:
+            raise AdmissionError(f"insufficient quota to consume: {','.join(sorted(uncovered))}")
+        if not interesting:
+            return quotas
+        delta = ev.usage(obj)
+        neg = quota.is_negative(delta)
+        if neg:
+            raise AdmissionError(f"quota usage is negative for resource(s): {','.join(neg)}")
+        if a.operation == UPDATE:
+            if a.old is None:
+                raise AdmissionError("unable to get previous usage since prior version of object was not found")
+            if (a.old.get("metadata") or {}).get("resourceVersion"):
+                delta = quota.subtract_non_negative(delta, ev.usage(a.old))
+        if quota.is_zero(delta):
+            return quotas
+        out = list(quotas)
+        for i in interesting:
+            q = quotas[i]
+            st = q.get("status") or {}
+            hard = st.get("hard") or {}
+            requested = quota.mask(delta, hard)
+            new_used = quota.add(st.get("used") or {}, requested)
+            ok, exceeded = quota.less_than_or_equal(quota.mask(new_used, requested), hard)
+            if not ok:
+                raise AdmissionError(
+                    f"exceeded quota: {m.name_of(q)}, requested: {quota.pretty(quota.mask(requested, exceeded))}, "
+                    f"used: {quota.pretty(quota.mask(st.get('used') or {}, exceeded))}, "
+                    f"limited: {quota.pretty(quota.mask(hard, exceeded))}")
+            nq = dict(q, status=dict(st, used=quota.to_strings(new_used)))
+            out[i] = nq
+        return out
+
+    async def charge(self, a):
+        if a.subresource or self.server is None or not a.namespace:
             return
-        quotas = self.server.list_objects("resourcequotas", a.namespace)
-        if not quotas:
+        group = self._group(a.resource)
+        ev = self.registry.get(group, a.resource)
+        if not ev.handles(a.operation):
             return
-        new = pod_usage(a.obj)
-        used: dict[str, Quantity] = {}
-        pods = a.prefetched["pods"] if a.prefetched and "pods" in a.prefetched else \
-            self.server.list_objects("pods", a.namespace)
-        for p in pods:
-            for k, v in pod_usage(p).items():
-                used[k] = used[k] + v if k in used else v
-        for qo in quotas:
-            hard = (qo.get("spec") or {}).get("hard") or {}
-            for k, hv in hard.items():
-                if k not in new:
+        quotas = await self.server.quota_objects(a.namespace)
+        if not quotas and not self.limited:
+            return
+        for attempt in range(self.RETRIES + 1):
+            new = self.check_request(quotas, ev, a, group)
+            failed = []
+            for old, nq in zip(quotas, new):
+                if nq is old:
                     continue
-                total = used.get(k, Quantity(0)) + new[k]
-                if total > parse_quantity(str(hv)):
-                    raise AdmissionError(
-                        f"exceeded quota: {qo['metadata']['name']}, requested: {k}={new[k]}, "
-                        f"used: {k}={used.get(k, Quantity(0))}, limited: {k}={hv}")
+                try:
+                    await self.server.write_quota_status(nq)
+                except Exception as e:   # noqa: BLE001 - a conflicting writer: re-read and re-check
+                    if getattr(e, "code", None) != 409:
+                        raise
+                    failed.append(m.name_of(nq))
+            if not failed:
+                return
+            if attempt == self.RETRIES:
+                raise AdmissionError(f"Operation cannot be fulfilled on resourcequotas \"{failed[0]}\": "
+                                     "the object has been modified; please apply your changes to the latest version "
+                                     "and try again", 409, "Conflict")
+            quotas = [q for q in await self.server.quota_objects(a.namespace, fresh=True) if m.name_of(q) in failed]

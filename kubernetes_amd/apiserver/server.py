@@ -904,9 +904,6 @@ class APIServer:
         ns = m.namespace_of(obj) if ri.namespaced else None
         if admit:
             a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
-            if ri.plural == "pods" and "pods" in self.uncached and self.list_objects("resourcequotas", ns):
-                # ResourceQuota sums the namespace's pods: hand it the store's current list
-                a.prefetched = {"pods": [e.obj for e in (await self._store_entries(ri, ns))[0]]}
             self._admit(a)
             obj = await self._mutating_webhooks(a, ri)
         if ri.plural == "services":
@@ -914,10 +911,13 @@ class APIServer:
         errs = self._validate_new(ri, strat, obj)
         if errs:
             raise invalid(ri, m.name_of(obj), errs)
+        key = m.key_for(ri, ns, m.name_of(obj))
         if admit:
             self._validate_admission(a)
             await self._validating_webhooks(a, ri)
-        key = m.key_for(ri, ns, m.name_of(obj))
+            if key in self.caches[ri.plural].by_key:
+                raise already_exists(ri, m.name_of(obj))
+            await self._charge_admission(a)
         if key in self.caches[ri.plural].by_key:
             raise already_exists(ri, m.name_of(obj))
         return await self._commit(ri, key, ADDED, obj, None)
@@ -972,11 +972,13 @@ class APIServer:
             errs = strat.validate(obj)
             if errs:
                 raise invalid(ri, m.name_of(obj), errs)
+            if key in self.caches[ri.plural].by_key:
+                raise already_exists(ri, m.name_of(obj))
             if a is not None:
                 a.obj = obj
                 self._validate_admission(a)
-            if key in self.caches[ri.plural].by_key:
-                raise already_exists(ri, m.name_of(obj))
+                if attempt == 0:
+                    await self._charge_admission(a)
             try:
                 return await self._commit(ri, key, ADDED, obj, None)
             except APIError as e:
@@ -995,6 +997,24 @@ class APIServer:
             self.admission.validate(a)
         except adm.AdmissionError as e:
             raise APIError(e.code, e.reason, str(e))
+
+    async def _charge_admission(self, a):
+        try:
+            await self.admission.charge(a)
+        except adm.AdmissionError as e:
+            raise APIError(e.code, e.reason, str(e))
+
+    async def quota_objects(self, namespace, fresh=False):
+        """The namespace's ResourceQuotas for quota admission; `fresh` re-reads them from the
+        store (a shared-store worker's cache may lag a quota another worker just charged)."""
+        if fresh and self.rstore is not None:
+            return [e.obj for e in (await self._store_entries(m.BY_PLURAL["resourcequotas"], namespace))[0]]
+        return self.list_objects("resourcequotas", namespace)
+
+    async def write_quota_status(self, q):
+        """Persist admission's charged status.used with the quota's resourceVersion (409 when
+        another request charged it first)."""
+        await self.update(m.BY_PLURAL["resourcequotas"], m.namespace_of(q), m.name_of(q), q, None, "status")
 
     def _existing(self, ri, namespace, name):
         key = m.key_for(ri, namespace, name)
@@ -1056,6 +1076,8 @@ class APIServer:
             raise invalid(ri, name, errs)
         self._validate_admission(a)
         await self._validating_webhooks(a, ri)
+        if subresource == "":
+            await self._charge_admission(a)
         # finalizers drained on an object that is being deleted -> delete it now
         if nm.get("deletionTimestamp") and not nm.get("finalizers") and self._grace_expired(ri, obj):
             return await self._commit(ri, key, DELETED, obj, prev)

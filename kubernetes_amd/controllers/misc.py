@@ -14,7 +14,6 @@ import time
 from ..api import meta as m
 from ..api.labels import label_selector_as_selector, selector_from_set
 from ..api.quantity import Quantity
-from ..apiserver.admission.plugins import pod_usage
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
 from .base import Controller, controller_ref, pod_is_ready, split_key
 
@@ -136,38 +135,103 @@ def find_port(pod, svc_port):
 
 
 class ResourceQuotaController(Controller):
+    """`pkg/controller/resourcequota/resource_quota_controller.go` syncResourceQuota: status.hard
+    mirrors spec.hard and status.used is recounted for every hard name by the quota evaluators
+    (`kubernetes_amd.quota`), respecting the quota's scopes, then masked to the hard names; the
+    status is written only when hard or used changed. Replenishment: any change to an object
+    the static evaluators count (pods, services, PVCs, configmaps, secrets,
+    replicationcontrollers, resourcequotas) re-queues the quotas of its namespace; other
+    `count/<resource>.<group>` names are recounted from a live list at sync time and on the
+    periodic resync (`--resource-quota-sync-period`, 5 min)."""
     name = "resourcequota"
     primary = "resourcequotas"
     workers = 2
+    resync_period = 300.0
+    WATCHED = ("pods", "services", "persistentvolumeclaims", "configmaps", "secrets", "replicationcontrollers")
 
     def setup(self):
+        from ..quota import Registry
+        self.registry = Registry()
         self.rq_inf = self.factory.get("resourcequotas")
-        self.pod_inf = self.factory.get("pods")
-        self.rq_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
-        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), self._pod)
+        self.rq_inf.add_handler(self.enqueue, self._rq_update, None)
+        self.infs = {"resourcequotas": self.rq_inf}
+        for r in self.WATCHED:
+            inf = self.infs[r] = self.factory.get(r)
+            inf.add_handler(self._obj, lambda o, n: self._obj(n), self._obj)
 
-    def _pod(self, pod):
-        ns = pod["metadata"].get("namespace")
+    def _rq_update(self, old, new):
+        # our own status writes come back as updates: only spec changes need a recount
+        if (old.get("spec") or {}) != (new.get("spec") or {}) or not (new.get("status") or {}).get("used"):
+            self.enqueue(new)
+
+    def _obj(self, obj):
+        ns = (obj.get("metadata") or {}).get("namespace")
+        if not ns:
+            return
         for q in self.rq_inf.list():
             if q["metadata"].get("namespace") == ns:
                 self.enqueue(q)
 
+    async def _objects(self, ns, hard):
+        """{(group, resource): objects in ns} for every kind some hard name counts."""
+        out = {}
+        for n in hard:
+            ev = self.registry.for_name(n)
+            if ev is None or (ev.group, ev.resource) in out:
+                continue
+            if not ev.group and ev.resource in self.infs:
+                out[("", ev.resource)] = [o for o in self.infs[ev.resource].list()
+                                          if o["metadata"].get("namespace") == ns]
+                continue
+            ri = await self._resource_info(ev.group, ev.resource)
+            if ri is None:
+                out[(ev.group, ev.resource)] = []
+                continue
+            try:
+                out[(ev.group, ev.resource)] = (await self.client.list(ri, ns if ri.namespaced else None))["items"]
+            except APIStatusError as e:
+                if e.code not in (403, 404, 405):
+                    raise
+                out[(ev.group, ev.resource)] = []
+        return out
+
+    async def _resource_info(self, group, resource):
+        """Built-in resources from the local table; anything else (custom resources) through
+        API discovery, cached per resync."""
+        ri = m.BY_PLURAL.get(resource)
+        if ri is not None and ri.group == group:
+            return ri
+        cache = getattr(self, "_discovered", None)
+        if cache is None or time.monotonic() - cache[0] > self.resync_period:
+            from .garbagecollector import deletable_resources, discover
+            try:
+                infos = deletable_resources(await discover(self.client), ignored=())
+            except APIStatusError:
+                infos = []
+            cache = self._discovered = (time.monotonic(), {(r.group, r.plural): r for r in infos})
+        return cache[1].get((group, resource))
+
     async def sync(self, key):
+        from .. import quota
         q = self.rq_inf.get(key)
         if q is None:
             return
         ns, name = split_key(key)
-        hard = (q.get("spec") or {}).get("hard") or {}
-        used: dict[str, Quantity] = {}
-        for p in self.pod_inf.list():
-            if p["metadata"].get("namespace") != ns:
-                continue
-            for k, v in pod_usage(p).items():
-                used[k] = used[k] + v if k in used else v
-        st = {"hard": dict(hard), "used": {k: str(used.get(k, Quantity(0))) for k in hard}}
-        if (q.get("status") or {}) == st:
+        spec = q.get("spec") or {}
+        hard = dict(spec.get("hard") or {})
+        st0 = q.get("status") or {}
+        objs = await self._objects(ns, hard)
+        used = dict(st0.get("used") or {})
+        used.update(quota.calculate_usage(lambda g, r: objs.get((g, r), ()), spec.get("scopes") or (), hard,
+                                          self.registry))
+        used = quota.to_strings(quota.mask(used, hard))
+        dirty = (st0.get("hard") is None or st0.get("used") is None
+                 or not quota.equals(st0.get("hard") or {}, hard)
+                 or not quota.equals(st0.get("used") or {}, used))
+        if not dirty:
             return
-        await self.client.patch("resourcequotas", name, {"status": st}, ns, "merge", "status")
+        body = dict(q, status={"hard": hard, "used": used})
+        await self.client.update_status("resourcequotas", body, ns)
 
 
 class DisruptionController(Controller):

@@ -331,7 +331,8 @@ class ProcessRuntime(Runtime):
                     "message": f"tier landlock (ABI {f.get('landlock')}): no container namespaces here ("
                                + (f.get("namespace_error") or "unavailable") + f"), but each container opens "
                                f"only its allocated nodes under {self.landlock_dir} (Landlock ruleset under "
-                               f"no_new_privs, EACCES for the others)"}
+                               f"no_new_privs; the others are refused, reported EPERM by the preloaded errno "
+                               f"shim so ROCr skips them as under a device cgroup)"}
         return {"enforced": False, "tier": "none", "reason": "IsolationUnavailable",
                 "message": "no mount namespace for containers (" + (f.get("namespace_error") or "unknown") +
                            ") and no Landlock (" + (f.get("landlock_error") or "unknown") +

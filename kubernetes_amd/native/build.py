@@ -57,6 +57,9 @@ def targets():
                            ["g++", "-O2", "-Wall", "-Werror", "-static", _s("pause", "container_init.cc")]),
         "kamd_runc": ([_s("runc", "kamd_runc.cc")], os.path.join(BIN_DIR, "kamd-runc"),
                       ["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-static", _s("runc", "kamd_runc.cc")]),
+        # preloaded by kamd-runc into Landlock-tier containers (EACCES -> EPERM on /dev/dri)
+        "kamd_devshim": ([_s("runc", "kamd_devshim.cc")], os.path.join(LIB_DIR, "libkamd_devshim.so"),
+                         cxx + ["-shared", "-Wextra", "-Werror", _s("runc", "kamd_devshim.cc"), "-ldl"]),
         "orphan": ([_s("pause", "orphan.cc")], os.path.join(BIN_DIR, "orphan"),
                    ["g++", "-Os", "-Wall", _s("pause", "orphan.cc")]),
         "kamd_hip": ([_s("hip", "kamd_hip.hip")], os.path.join(LIB_DIR, "libkamd_hip.so"),

@@ -360,6 +360,36 @@ struct Pinned {
 
 std::string g_root_real;   // realpath of the rootfs ("" = the host root: nothing to check)
 
+// Landlock tier: the errno shim preloaded into the container (libkamd_devshim.so, next to this
+// binary's bin/ in ../lib/). Landlock refuses DRM nodes with EACCES, which ROCr's thunk treats as
+// fatal where the device cgroup's EPERM means "skip this GPU"; the shim reports EPERM instead.
+// "" = not preloaded (no shim built, or the spec opted out with kamd.io/devshim: "false").
+std::string g_devshim;
+std::string g_devshim_dir;
+
+std::string devshim_path() {
+  char exe[PATH_MAX];
+  ssize_t n = readlink("/proc/self/exe", exe, sizeof exe - 1);
+  if (n <= 0) return "";
+  exe[n] = 0;
+  std::string d(exe);
+  size_t s = d.rfind('/');
+  if (s == std::string::npos) return "";
+  d.resize(s);                               // .../bin
+  s = d.rfind('/');
+  if (s == std::string::npos) return "";
+  std::string lib = d.substr(0, s) + "/lib/libkamd_devshim.so";
+  return access(lib.c_str(), R_OK) == 0 ? lib : "";
+}
+
+// LD_PRELOAD with the shim first (an existing preload list is kept after it)
+std::string with_devshim(const char* current) {
+  if (g_devshim.empty()) return current ? current : "";
+  if (current == nullptr || !*current) return g_devshim;
+  if (strstr(current, g_devshim.c_str()) != nullptr) return current;
+  return g_devshim + ":" + current;
+}
+
 void pin(Pinned& p, const std::string& path) {
   p.fd = open(path.c_str(), O_PATH | O_NOFOLLOW | O_CLOEXEC);
   if (p.fd < 0) die(126, "open mountpoint %s: %s", path.c_str(), strerror(errno));
@@ -809,6 +839,7 @@ std::string landlock_restrict(const std::string& dir_in, const std::vector<std::
 struct Report {
   std::string tier = "none";               // namespaces | landlock | none
   int landlock_rules = 0;
+  bool devshim = false;                    // Landlock tier: EACCES->EPERM errno shim preloaded
   bool user_ns = false, mount_ns = false, pid_ns = false, ipc_ns = false, uts_ns = false;
   std::string proc = "host", dev = "host", sys = "host";
   std::vector<std::string> devices;
@@ -1086,7 +1117,17 @@ void exec_entrypoint(const J& spec) {
   const J& proc = spec["process"];
   std::vector<std::string> args, env;
   for (auto& a : proc["args"].a) args.push_back(a.s);
-  for (auto& e : proc["env"].a) env.push_back(e.s);
+  bool preload_set = false;
+  for (auto& e : proc["env"].a) {
+    if (!g_devshim.empty() && e.s.compare(0, 11, "LD_PRELOAD=") == 0) {
+      env.push_back("LD_PRELOAD=" + with_devshim(e.s.c_str() + 11));
+      preload_set = true;
+    } else {
+      env.push_back(e.s);
+    }
+  }
+  if (!g_devshim.empty() && !preload_set) env.push_back("LD_PRELOAD=" + g_devshim);
+  if (!g_devshim.empty()) env.push_back("KAMD_DEVSHIM_DIR=" + g_devshim_dir);
   if (args.empty()) die(126, "process.args is empty");
   std::vector<char*> argv, envp;
   for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
@@ -1129,6 +1170,7 @@ std::string report_json(const Report& r, const CgroupState& cg) {
   b("uts_ns", r.uts_ns);
   o += "\"tier\":" + json_str(r.tier) + ",";
   if (r.tier == "landlock") o += "\"landlock_rules\":" + std::to_string(r.landlock_rules) + ",";
+  if (r.tier == "landlock") b("devshim", r.devshim);
   o += "\"proc\":" + json_str(r.proc) + ",\"dev\":" + json_str(r.dev) + ",\"sys\":" + json_str(r.sys);
   o += ",\"device_cgroup\":" + json_str(cg.mode);
   if (!cg.error.empty()) o += ",\"device_cgroup_error\":" + json_str(cg.error);
@@ -1305,6 +1347,12 @@ int cmd_run(const std::string& bundle, int ready_fd) {
       if (!e.empty()) die(126, "landlock: %s", e.c_str());
       rep.tier = "landlock";
       rep.dev = "host (landlock: " + dir + " limited to the allocated nodes)";
+      if (ann2["kamd.io/devshim"].str("true") != "false") {
+        g_devshim = devshim_path();
+        g_devshim_dir = dir;
+        if (g_devshim.empty()) rep.notes.push_back("devshim: libkamd_devshim.so not found; denied GPU nodes read EACCES");
+      }
+      rep.devshim = !g_devshim.empty();
     }
     // the bundle path may be gone after pivot_root: the report goes to P over the sync pipe
     std::string report = report_json(rep, cg);
@@ -1423,6 +1471,11 @@ int cmd_exec(pid_t target, const std::string& cwd, const std::string& user, cons
       }
       std::string e = landlock_restrict(dir, allowed, nullptr);
       if (!e.empty()) die(126, "landlock: %s", e.c_str());
+      g_devshim = devshim_path();
+      if (!g_devshim.empty()) {
+        setenv("LD_PRELOAD", with_devshim(getenv("LD_PRELOAD")).c_str(), 1);
+        setenv("KAMD_DEVSHIM_DIR", dir.c_str(), 1);
+      }
     }
     if (chdir(cwd.empty() ? "/" : cwd.c_str()) != 0) die(126, "chdir %s: %s", cwd.c_str(), strerror(errno));
     execvp(argv[0], argv);

@@ -195,11 +195,17 @@ def test_gpu_quota_enforced(run):
         try:
             await c.create("resourcequotas", {"metadata": {"name": "q", "namespace": "default"},
                                               "spec": {"hard": {"requests.amd.com/gpu": "3"}}})
+            # no quota controller here: publish the initial count it would write
+            await c.patch("resourcequotas", "q", {"status": {"hard": {"requests.amd.com/gpu": "3"},
+                                                             "used": {"requests.amd.com/gpu": "0"}}},
+                          "default", "merge", "status")
             await c.create("pods", gpu_pod("q1", 2))
             with pytest.raises(APIStatusError) as ei:
                 await c.create("pods", gpu_pod("q2", 2))
             assert ei.value.code == 403 and "exceeded quota" in ei.value.status["message"]
             await c.create("pods", gpu_pod("q3", 1))
+            q = await c.get("resourcequotas", "q", "default")
+            assert q["status"]["used"] == {"requests.amd.com/gpu": "3"}     # admission charged both pods
         finally:
             await c.close()
             await s.stop()

@@ -334,11 +334,16 @@ def test_uncached_pods_and_events_read_from_store(run, store):
             with pytest.raises(APIStatusError) as ei:
                 await b.bind("default", "u1", "n0", {p1["spec"]["extendedResources"][0]["name"]: {"resources": ["G0"]}})
             assert ei.value.code == 409
-            # quota admission sums the namespace's pods read from the store
+            # quota admission charges status.used with the quota's resourceVersion, across workers
             await a.create("namespaces", {"metadata": {"name": "q"}})
             await a.create("resourcequotas", {"metadata": {"name": "rq", "namespace": "q"},
                                               "spec": {"hard": {"pods": "2"}}}, "q")
-            await _eventually(lambda: b.get("resourcequotas", "rq", "q"))
+            await a.patch("resourcequotas", "rq", {"status": {"hard": {"pods": "2"}, "used": {"pods": "0"}}}, "q",
+                          "merge", "status")
+
+            async def counted():
+                return ((await b.get("resourcequotas", "rq", "q")).get("status") or {}).get("used")
+            await _eventually(counted)
             for i in range(2):
                 await b.create("pods", {"metadata": {"name": f"q{i}", "namespace": "q"},
                                         "spec": {"containers": [{"name": "c", "image": "x"}]}}, "q")
