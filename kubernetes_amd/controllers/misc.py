@@ -41,7 +41,74 @@ class ServiceAccountController(Controller):
                 raise
 
 
+def _semantic(o):
+    """apiequality.Semantic.DeepEqual for wire objects: empty values (omitted on the wire, e.g.
+    by the protobuf codec) compare equal to absent ones."""
+    if isinstance(o, dict):
+        return {k: _semantic(v) for k, v in o.items() if v not in (None, "", [], {})}
+    if isinstance(o, list):
+        return [_semantic(v) for v in o]
+    return o
+
+
+TOLERATE_UNREADY = "service.alpha.kubernetes.io/tolerate-unready-endpoints"
+LEADER_ANNOTATION = "control-plane.alpha.kubernetes.io/leader"
+
+
+def should_pod_be_in_endpoints(pod) -> bool:
+    """`shouldPodBeInEndpoints`: a not-ready pod is listed as notReady unless it can never run
+    again (Never: Failed/Succeeded; OnFailure: Succeeded)."""
+    policy = (pod.get("spec") or {}).get("restartPolicy", "Always")
+    phase = (pod.get("status") or {}).get("phase")
+    if policy == "Never":
+        return phase not in ("Failed", "Succeeded")
+    if policy == "OnFailure":
+        return phase != "Succeeded"
+    return True
+
+
+def repack_subsets(entries):
+    """`endpoints.RepackSubsets` + `SortSubsets`: entries are (address, port, ready); addresses
+    are de-duplicated by (ip, targetRef uid) keeping "ready" once seen ready; ports offered by
+    the same set of addresses (with the same readiness) share one subset."""
+    addrs, by_port = {}, {}
+    for addr, port, ready in entries:
+        key = (addr["ip"], (addr.get("targetRef") or {}).get("uid"))
+        addrs.setdefault(key, addr)
+        pk = (port.get("name", ""), port["port"], port.get("protocol", "TCP"))
+        cur = by_port.setdefault(pk, {})
+        cur[key] = cur.get(key, False) or ready
+    groups = {}
+    for pk, amap in by_port.items():
+        groups.setdefault(tuple(sorted(amap.items())), []).append(pk)
+    out = []
+    for amap, ports in groups.items():
+        ss = {}
+        ready = sorted((addrs[k] for k, r in amap if r), key=lambda a: (a["ip"], (a.get("targetRef") or {}).get("uid", "")))
+        not_ready = sorted((addrs[k] for k, r in amap if not r),
+                           key=lambda a: (a["ip"], (a.get("targetRef") or {}).get("uid", "")))
+        if ready:
+            ss["addresses"] = ready
+        if not_ready:
+            ss["notReadyAddresses"] = not_ready
+        ss["ports"] = [{"name": n, "port": p, "protocol": pr} if n else {"port": p, "protocol": pr}
+                       for n, p, pr in sorted(ports)]
+        out.append(ss)
+    out.sort(key=lambda ss: repr(ss["ports"]))
+    return out
+
+
 class EndpointsController(Controller):
+    """`pkg/controller/endpoint/endpoints_controller.go` syncService: for a service with a
+    selector, every selected pod with an IP becomes an address for each service port it has
+    (`FindPort`; a headless service without ports gets port-less addresses), ready or
+    notReady (`shouldPodBeInEndpoints`) — all ready when the service tolerates unready
+    endpoints (the `tolerate-unready-endpoints` annotation or spec.publishNotReadyAddresses),
+    which also keeps terminating pods; the hostname is published when the pod's
+    hostname/subdomain name this service; subsets are repacked (`RepackSubsets`). Endpoints
+    carry the service's labels and are written only on a change; a deleted service's endpoints
+    are deleted, and leftover endpoints (no service, not a leader-election record) are queued at
+    start (`checkLeftoverEndpoints`)."""
     name = "endpoint"
 
     def setup(self):
@@ -49,15 +116,34 @@ class EndpointsController(Controller):
         self.pod_inf = self.factory.get("pods")
         self.ep_inf = self.factory.get("endpoints")
         self.svc_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), self.enqueue)
-        self.pod_inf.add_handler(self._pod, lambda o, n: (self._pod(o), self._pod(n)), self._pod)
+        self.pod_inf.add_handler(self._pod, self._pod_update, self._pod)
 
-    def _pod(self, pod):
+    def start(self):
+        super().start()
+        for ep in self.ep_inf.list():
+            if LEADER_ANNOTATION not in ((ep.get("metadata") or {}).get("annotations") or {}):
+                self.enqueue(ep)
+
+    def _services_for(self, pod):
         ns = pod["metadata"].get("namespace")
         labels = pod["metadata"].get("labels") or {}
         for svc in self.svc_inf.list():
             sel = (svc.get("spec") or {}).get("selector")
-            if svc["metadata"].get("namespace") == ns and sel and selector_from_set(sel).matches(labels):
-                self.enqueue(svc)
+            if svc["metadata"].get("namespace") == ns and sel is not None and selector_from_set(sel).matches(labels):
+                yield svc
+
+    def _pod(self, pod):
+        for svc in self._services_for(pod):
+            self.enqueue(svc)
+
+    def _pod_update(self, old, new):
+        """`updatePod`: nothing to do unless something endpoints show changed; a label change
+        re-syncs the services of both label sets."""
+        if old.get("metadata", {}).get("resourceVersion") == new.get("metadata", {}).get("resourceVersion"):
+            return
+        if (old["metadata"].get("labels") or {}) != (new["metadata"].get("labels") or {}):
+            self._pod(old)
+        self._pod(new)
 
     async def sync(self, key):
         ns, name = split_key(key)
@@ -69,52 +155,61 @@ class EndpointsController(Controller):
                 if not is_not_found(e):
                     raise
             return
-        sel = (svc.get("spec") or {}).get("selector")
-        if not sel:
-            return
+        spec = svc.get("spec") or {}
+        sel = spec.get("selector")
+        if sel is None:
+            return          # endpoints of a selector-less service are managed by the user
+        ann = svc["metadata"].get("annotations") or {}
+        tolerate = str(ann.get(TOLERATE_UNREADY, "")).lower() in ("true", "1", "t") or \
+            bool(spec.get("publishNotReadyAddresses"))
         s = selector_from_set(sel)
-        svc_ports = (svc.get("spec") or {}).get("ports") or ()
-        groups: dict = {}          # resolved port set -> ([ready], [not ready])  (RepackSubsets)
+        svc_ports = spec.get("ports") or ()
+        entries = []
         for p in self.pod_inf.list():
-            if p["metadata"].get("namespace") != ns or not s.matches(p["metadata"].get("labels") or {}):
+            md = p["metadata"]
+            if md.get("namespace") != ns or not s.matches(md.get("labels") or {}):
                 continue
             ip = (p.get("status") or {}).get("podIP")
-            if not ip or p["metadata"].get("deletionTimestamp"):
+            if not ip or (not tolerate and md.get("deletionTimestamp")):
                 continue
-            ports = []
+            pspec = p.get("spec") or {}
+            addr = {"ip": ip, "nodeName": pspec.get("nodeName"),
+                    "targetRef": {"kind": "Pod", "namespace": ns, "name": md["name"], "uid": md.get("uid"),
+                                  "resourceVersion": md.get("resourceVersion")}}
+            if pspec.get("hostname") and pspec.get("subdomain") == name:
+                addr["hostname"] = pspec["hostname"]
+            ready = tolerate or pod_is_ready(p)
+            if not ready and not should_pod_be_in_endpoints(p):
+                continue
+            if not svc_ports:
+                if spec.get("clusterIP") == "None":
+                    entries.append((addr, {"port": 0, "protocol": "TCP"}, ready))
+                continue
             for sp in svc_ports:
                 port = find_port(p, sp)
-                if port is not None:          # a named port the pod lacks: not an endpoint for it
-                    ports.append((sp.get("name", ""), port, sp.get("protocol", "TCP")))
-            if not ports:
-                continue
-            addr = {"ip": ip, "nodeName": (p.get("spec") or {}).get("nodeName"),
-                    "targetRef": {"kind": "Pod", "namespace": ns, "name": p["metadata"]["name"], "uid": p["metadata"]["uid"]}}
-            g = groups.setdefault(tuple(sorted(ports)), ([], []))
-            g[0 if pod_is_ready(p) else 1].append(addr)
-        subsets = []
-        for key_ports in sorted(groups):
-            ready, not_ready = groups[key_ports]
-            ss = {"ports": [{"name": n, "port": port, "protocol": proto} for n, port, proto in key_ports]}
-            if ready:
-                ss["addresses"] = sorted(ready, key=lambda a: a["ip"])
-            if not_ready:
-                ss["notReadyAddresses"] = sorted(not_ready, key=lambda a: a["ip"])
-            subsets.append(ss)
+                if port is None:          # a named port the pod lacks: not an endpoint for it
+                    continue
+                entries.append((addr, {"name": sp.get("name", ""), "port": port,
+                                       "protocol": sp.get("protocol", "TCP")}, ready))
+        subsets = repack_subsets(entries)
+        labels = svc["metadata"].get("labels") or {}
         cur = self.ep_inf.get(key)
-        if cur is not None and (cur.get("subsets") or []) == subsets:
+        if cur is not None and _semantic(cur.get("subsets") or []) == _semantic(subsets) and \
+                (cur["metadata"].get("labels") or {}) == labels:
             return
-        ep = {"apiVersion": "v1", "kind": "Endpoints", "metadata": {"name": name, "namespace": ns,
-                                                                    "labels": svc["metadata"].get("labels") or {}},
-              "subsets": subsets}
         if cur is None:
+            ep = {"apiVersion": "v1", "kind": "Endpoints",
+                  "metadata": {"name": name, "namespace": ns, "labels": labels}, "subsets": subsets}
             try:
                 await self.client.create("endpoints", ep, ns)
                 return
             except APIStatusError as e:
                 if not is_already_exists(e):
                     raise
-        await self.client.patch("endpoints", name, {"subsets": subsets}, ns)
+                cur = await self.client.get("endpoints", name, ns)
+        new = dict(cur, subsets=subsets)
+        new["metadata"] = dict(cur["metadata"], labels=labels)
+        await self.client.update("endpoints", new, ns)
 
 
 def find_port(pod, svc_port):
