@@ -17,6 +17,7 @@ import time
 from ..api import meta as m
 from ..api.meta import now_rfc3339, parse_rfc3339
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
+from ..api.labels import selector_to_string
 from .base import Controller, Expectations, controller_ref, pod_from_template, split_key
 
 
@@ -292,18 +293,36 @@ class JobController(Controller):
 
 
 # ---------------------------------------------------------------------------
-def _field_match(spec, value, lo, hi):
+_MONTHS = {n: i + 1 for i, n in enumerate(("jan", "feb", "mar", "apr", "may", "jun", "jul", "aug", "sep", "oct",
+                                            "nov", "dec"))}
+_DOWS = {n: i for i, n in enumerate(("sun", "mon", "tue", "wed", "thu", "fri", "sat"))}
+
+
+def _field_match(spec, value, lo, hi, names=None):
+    """One cron field (robfig/cron `ParseStandard`): `*` / `?`, lists, ranges, steps and, for
+    month and day-of-week, three-letter names."""
+    def num(x):
+        x = x.strip().lower()
+        if names and x in names:
+            return names[x]
+        v = int(x)
+        if not lo <= v <= hi:
+            raise ValueError(f"cron value {v} out of range [{lo}, {hi}]")
+        return v
     for part in spec.split(","):
         step = 1
         if "/" in part:
             part, s = part.split("/", 1)
             step = int(s)
-        if part == "*":
+            if step <= 0:
+                raise ValueError(f"invalid cron step {s!r}")
+        if part in ("*", "?"):
             a, b = lo, hi
         elif "-" in part:
-            a, b = (int(x) for x in part.split("-", 1))
+            a, b = (num(x) for x in part.split("-", 1))
         else:
-            a = b = int(part)
+            a = num(part)
+            b = hi if step > 1 else a
         if a <= value <= b and (value - a) % step == 0:
             return True
     return False
@@ -319,24 +338,92 @@ def cron_matches(expr: str, t: dt.datetime) -> bool:
         raise ValueError(f"invalid cron schedule {expr!r}")
     dow = (t.weekday() + 1) % 7
     return (_field_match(f[0], t.minute, 0, 59) and _field_match(f[1], t.hour, 0, 23) and
-            _field_match(f[2], t.day, 1, 31) and _field_match(f[3], t.month, 1, 12) and _field_match(f[4], dow, 0, 6))
+            _field_match(f[2], t.day, 1, 31) and _field_match(f[3], t.month, 1, 12, _MONTHS) and
+            _field_match(f[4], dow, 0, 6, _DOWS))
+
+
+class TooManyMissed(ValueError):
+    pass
 
 
 def missed_schedules(expr, since: float, now: float, cap=100):
-    """Scheduled times in (since, now], minute resolution (getRecentUnmetScheduleTimes)."""
+    """Scheduled times in (since, now], minute resolution (`getRecentUnmetScheduleTimes`);
+    more than `cap` raises TooManyMissed — the reference refuses to guess which to start."""
     out = []
     t = dt.datetime.fromtimestamp(since, dt.timezone.utc).replace(second=0, microsecond=0) + dt.timedelta(minutes=1)
     end = dt.datetime.fromtimestamp(now, dt.timezone.utc)
-    while t <= end and len(out) < cap:
+    while t <= end:
         if cron_matches(expr, t):
             out.append(t)
+            if len(out) > cap:
+                raise TooManyMissed("Too many missed start time (> 100). Set or decrease .spec.startingDeadlineSeconds "
+                                    "or check clock skew.")
         t += dt.timedelta(minutes=1)
     return out
 
 
+def unmet_schedule_times(cj, now: float):
+    """`getRecentUnmetScheduleTimes`: from lastScheduleTime (else creation), but no earlier than
+    now - startingDeadlineSeconds."""
+    spec = cj.get("spec") or {}
+    try:                      # cron.ParseStandard first: an unparseable schedule is an error
+        cron_matches(spec.get("schedule", ""), dt.datetime.fromtimestamp(now, dt.timezone.utc))
+    except ValueError as e:
+        raise ValueError(f"Unparseable schedule: {spec.get('schedule', '')} : {e}") from None
+    earliest = parse_rfc3339((cj.get("status") or {}).get("lastScheduleTime")) or \
+        parse_rfc3339(cj["metadata"].get("creationTimestamp")) or now
+    sds = spec.get("startingDeadlineSeconds")
+    if sds is not None:
+        earliest = max(earliest, now - int(sds))
+    if earliest > now:
+        return []
+    return missed_schedules(spec.get("schedule", ""), earliest, now)
+
+
+def finished_status(job):
+    """(finished, "Complete" | "Failed" | None) — `getFinishedStatus`."""
+    for c in (job.get("status") or {}).get("conditions") or ():
+        if c.get("type") in ("Complete", "Failed") and c.get("status") == "True":
+            return True, c["type"]
+    return False, None
+
+
+def job_from_template(cj, scheduled: dt.datetime):
+    """`getJobFromTemplate`: the template's labels and annotations, a name deterministic in the
+    scheduled time (`<cronjob>-<unix seconds>`: the same start is never created twice), and a
+    controller reference to the CronJob."""
+    jt = (cj.get("spec") or {}).get("jobTemplate") or {}
+    md = jt.get("metadata") or {}
+    return {"apiVersion": "batch/v1", "kind": "Job",
+            "metadata": {"name": f"{m.name_of(cj)}-{int(scheduled.timestamp())}", "namespace": m.namespace_of(cj),
+                         "labels": dict(md.get("labels") or {}), "annotations": dict(md.get("annotations") or {}),
+                         "ownerReferences": [m.owner_reference(cj)]},
+            "spec": m.fast_copy(jt.get("spec") or {})}
+
+
+def _job_ref(job):
+    md = job["metadata"]
+    return {"kind": "Job", "namespace": md.get("namespace"), "name": md["name"], "uid": md.get("uid"),
+            "apiVersion": "batch/v1", "resourceVersion": md.get("resourceVersion")}
+
+
 class CronJobController(Controller):
+    """`pkg/controller/cronjob/cronjob_controller.go`: every 10 s each CronJob is synced
+    (`syncAll` → `syncOne` + `cleanupFinishedJobs`):
+
+      * status.active is reconciled with the jobs the CronJob controls — finished ones leave it
+        (SawCompletedJob), vanished ones too (MissingJob), unknown running ones are reported
+        (UnexpectedJob);
+      * deleting or suspended: nothing starts;
+      * the latest unmet schedule time starts, unless it is past startingDeadlineSeconds, more than
+        100 were missed (FailedNeedsStart), or a run is active under Forbid; under Replace the
+        active jobs are deleted first (parallelism 0, their pods, then the job);
+      * the created job joins status.active and lastScheduleTime advances;
+      * finished jobs beyond successful/failedJobsHistoryLimit are deleted oldest first
+        (by status.startTime, then name)."""
     name = "cronjob"
     workers = 1
+    SYNC_PERIOD = 10.0
 
     def setup(self):
         self.cj_inf = self.factory.get("cronjobs")
@@ -355,61 +442,127 @@ class CronJobController(Controller):
 
     async def _ticker(self):
         while True:
-            await asyncio.sleep(10)   # reference syncs every 10 s
+            await asyncio.sleep(self.SYNC_PERIOD)
             for cj in self.cj_inf.list():
                 self.enqueue(cj)
+
+    async def _update_status(self, cj, status):
+        if (cj.get("status") or {}) == status:
+            return cj
+        body = dict(cj, status=status)
+        return await self.client.update_status("cronjobs", body, m.namespace_of(cj))
+
+    async def delete_job(self, cj, job, reason=""):
+        """`deleteJob`: stop the job (parallelism 0), delete its pods, then the job."""
+        ns = m.namespace_of(job)
+        try:
+            if ((job.get("spec") or {}).get("parallelism", 1)) != 0:
+                job = m.fast_copy(job)
+                job["spec"]["parallelism"] = 0
+                job = await self.client.update("jobs", job, ns)
+            sel = selector_to_string((job.get("spec") or {}).get("selector") or {})
+            for pod in (await self.client.list("pods", ns, label_selector=sel))["items"] if sel else ():
+                try:
+                    await self.client.delete("pods", m.name_of(pod), ns)
+                except APIStatusError as e:
+                    if not is_not_found(e):
+                        raise
+            await self.client.delete("jobs", m.name_of(job), ns)
+        except APIStatusError as e:
+            self.recorder.event(cj, "Warning", "FailedDelete", f"Deleted job: {e}")
+            return False
+        self.recorder.event(cj, "Normal", "SuccessfulDelete", f"Deleted job {m.name_of(job)}")
+        return True
 
     async def sync(self, key, now=None):
         cj = self.cj_inf.get(key)
         if cj is None:
             return
-        ns, name = split_key(key)
-        spec = cj.get("spec") or {}
         now = now or time.time()
-        uid = cj["metadata"]["uid"]
+        uid = m.uid_of(cj)
         jobs = [j for j in self.job_inf.list() if (controller_ref(j) or {}).get("uid") == uid]
-        running = [j for j in jobs if not any(c.get("type") in ("Complete", "Failed") and c.get("status") == "True"
-                                             for c in (j.get("status") or {}).get("conditions") or ())]
-        # history limits
-        for kind, lim in (("Complete", spec.get("successfulJobsHistoryLimit", 3)), ("Failed", spec.get("failedJobsHistoryLimit", 1))):
-            done = [j for j in jobs if any(c.get("type") == kind and c.get("status") == "True" for c in (j.get("status") or {}).get("conditions") or ())]
-            done.sort(key=lambda j: j["metadata"].get("creationTimestamp", ""))
-            for j in done[:max(0, len(done) - int(lim))]:
-                try:
-                    await self.client.delete("jobs", j["metadata"]["name"], ns, propagation="Background")
-                except APIStatusError:
-                    pass
-        if spec.get("suspend"):
+        await self.sync_one(cj, jobs, now)
+        await self.cleanup_finished_jobs(cj, jobs)
+
+    async def sync_one(self, cj, jobs, now):
+        status = m.fast_copy(cj.get("status") or {})
+        active = list(status.get("active") or ())
+        active_uids = {a.get("uid") for a in active}
+        children = set()
+        for j in jobs:
+            children.add(m.uid_of(j))
+            done, _ = finished_status(j)
+            found = m.uid_of(j) in active_uids
+            if not found and not done:
+                self.recorder.event(cj, "Warning", "UnexpectedJob",
+                                    f"Saw a job that the controller did not create or forgot: {m.name_of(j)}")
+            elif found and done:
+                active = [a for a in active if a.get("uid") != m.uid_of(j)]
+                self.recorder.event(cj, "Normal", "SawCompletedJob", f"Saw completed job: {m.name_of(j)}")
+        for a in list(active):
+            if a.get("uid") not in children:
+                self.recorder.event(cj, "Normal", "MissingJob", f"Active job went missing: {a.get('name')}")
+                active = [x for x in active if x.get("uid") != a.get("uid")]
+        if active:
+            status["active"] = active
+        else:
+            status.pop("active", None)
+        cj = await self._update_status(cj, status)
+        spec = cj.get("spec") or {}
+        if cj["metadata"].get("deletionTimestamp") or spec.get("suspend"):
             return
-        last = parse_rfc3339((cj.get("status") or {}).get("lastScheduleTime")) or parse_rfc3339(cj["metadata"].get("creationTimestamp")) or now
-        times = missed_schedules(spec.get("schedule", ""), last, now)
+        try:
+            times = unmet_schedule_times(cj, now)
+        except ValueError as e:
+            self.recorder.event(cj, "Warning", "FailedNeedsStart", f"Cannot determine if job needs to be started: {e}")
+            return
         if not times:
             return
         sched = times[-1]
         sds = spec.get("startingDeadlineSeconds")
-        if sds is not None and now - sched.timestamp() > int(sds):
-            return
+        if sds is not None and sched.timestamp() + int(sds) < now:
+            return             # missed the starting window
         pol = spec.get("concurrencyPolicy", "Allow")
-        if running and pol == "Forbid":
+        if pol == "Forbid" and active:
             return
-        if running and pol == "Replace":
-            for j in running:
-                try:
-                    await self.client.delete("jobs", j["metadata"]["name"], ns, propagation="Background")
-                except APIStatusError:
-                    pass
-        jt = spec.get("jobTemplate") or {}
-        jname = f"{name}-{int(sched.timestamp() // 60)}"
-        job = {"apiVersion": "batch/v1", "kind": "Job",
-               "metadata": {"name": jname, "namespace": ns, "labels": dict((jt.get("metadata") or {}).get("labels") or {}),
-                            "annotations": {"cronjob.kubernetes.io/scheduled-time": sched.strftime("%Y-%m-%dT%H:%M:%SZ")},
-                            "ownerReferences": [m.owner_reference(cj)]},
-               "spec": m.fast_copy(jt.get("spec") or {})}
+        if pol == "Replace":
+            for a in list(active):
+                job = self.job_inf.get(f"{a.get('namespace')}/{a.get('name')}")
+                if job is None:
+                    try:
+                        job = await self.client.get("jobs", a.get("name"), a.get("namespace"))
+                    except APIStatusError as e:
+                        self.recorder.event(cj, "Warning", "FailedGet", f"Get job: {e}")
+                        return
+                if not await self.delete_job(cj, job):
+                    return
+                active = [x for x in active if x.get("uid") != m.uid_of(job)]
+        job = job_from_template(cj, sched)
         try:
-            await self.client.create("jobs", job, ns)
-            self.recorder.event(cj, "Normal", "SuccessfulCreate", f"Created job {jname}")
+            created = await self.client.create("jobs", job, m.namespace_of(cj))
         except APIStatusError as e:
-            if not is_already_exists(e):
-                raise
-        await self.client.patch("cronjobs", name, {"status": {"lastScheduleTime": sched.strftime("%Y-%m-%dT%H:%M:%SZ")}},
-                                ns, "merge", "status")
+            self.recorder.event(cj, "Warning", "FailedCreate", f"Error creating job: {e}")
+            if is_already_exists(e):
+                return
+            raise
+        self.recorder.event(cj, "Normal", "SuccessfulCreate", f"Created job {m.name_of(created)}")
+        status = m.fast_copy(cj.get("status") or {})
+        status["active"] = active + [_job_ref(created)]
+        status["lastScheduleTime"] = sched.strftime("%Y-%m-%dT%H:%M:%SZ")
+        await self._update_status(cj, status)
+
+    async def cleanup_finished_jobs(self, cj, jobs):
+        spec = cj.get("spec") or {}
+        for kind, field in (("Complete", "successfulJobsHistoryLimit"), ("Failed", "failedJobsHistoryLimit")):
+            lim = spec.get(field)
+            if lim is None:
+                continue
+            done = [j for j in jobs if finished_status(j) == (True, kind)]
+            extra = len(done) - int(lim)
+            if extra <= 0:
+                continue
+            # byJobStartTime: started jobs by start time (unstarted last), then name
+            done.sort(key=lambda j: (parse_rfc3339((j.get("status") or {}).get("startTime")) is None,
+                                     parse_rfc3339((j.get("status") or {}).get("startTime")) or 0, m.name_of(j)))
+            for j in done[:extra]:
+                await self.delete_job(cj, j, "history limit reached")
