@@ -157,6 +157,72 @@ def pod_is_ready(pod):
     return False
 
 
+async def claim_objects(client, owner, resource, candidates, matches, ignore=None):
+    """`ControllerRefManager.ClaimObject` over `candidates` (same namespace as `owner`):
+    objects the owner controls stay claimed while they match and are released (their owner
+    reference patched away) when they stop matching; orphans that match are adopted unless the
+    owner is being deleted. `ignore(obj)` skips objects (e.g. terminating pods) for adoption and
+    release. Returns the claimed objects (adopted ones as patched)."""
+    uid = m.uid_of(owner)
+    out = []
+    for o in candidates:
+        ref = controller_ref(o)
+        ok = matches(o)
+        if ref is not None:
+            if ref.get("uid") != uid:
+                continue
+            if ok:
+                out.append(o)
+            elif not o["metadata"].get("deletionTimestamp") and not (ignore and ignore(o)):
+                refs = [r for r in o["metadata"].get("ownerReferences") or () if r.get("uid") != uid]
+                try:
+                    await client.patch(resource, m.name_of(o), {"metadata": {"ownerReferences": refs or None,
+                                                                             "uid": m.uid_of(o)}}, m.namespace_of(o))
+                except Exception as e:      # noqa: BLE001 - a vanished or changed object is simply not ours
+                    if getattr(e, "code", None) not in (404, 409, 422):
+                        raise
+            continue
+        if not ok or owner["metadata"].get("deletionTimestamp") or o["metadata"].get("deletionTimestamp") or \
+                (ignore and ignore(o)):
+            continue
+        refs = list(o["metadata"].get("ownerReferences") or ()) + [m.owner_reference(owner)]
+        try:
+            out.append(await client.patch(resource, m.name_of(o), {"metadata": {"ownerReferences": refs,
+                                                                                "uid": m.uid_of(o)}},
+                                          m.namespace_of(o)))
+        except Exception as e:              # noqa: BLE001
+            if getattr(e, "code", None) not in (404, 409, 422):
+                raise
+    return out
+
+
+def _ready_time(pod):
+    for c in (pod.get("status") or {}).get("conditions") or ():
+        if c.get("type") == "Ready" and c.get("status") == "True":
+            return m.parse_rfc3339(c.get("lastTransitionTime"))
+    return None
+
+
+def active_pods_key(pod):
+    """Sort key of `controller.ActivePods` (`controller_utils.go:731`): pods to delete first
+    sort first — unassigned < assigned; Pending < Unknown < Running; not ready < ready; among
+    ready pods, ready for less time first (no transition time first of all); more container
+    restarts first; newer first (no creation time first of all)."""
+    st = pod.get("status") or {}
+    ready = pod_is_ready(pod)
+    phase = {"Pending": 0, "Unknown": 1, "Running": 2}.get(st.get("phase"), 0)
+    if ready:
+        rt = _ready_time(pod)
+        ready_key = (0, 0.0) if rt is None else (1, -rt)
+    else:
+        ready_key = (0, 0.0)
+    restarts = max((int(cs.get("restartCount") or 0) for cs in st.get("containerStatuses") or ()), default=0)
+    ct = m.parse_rfc3339((pod.get("metadata") or {}).get("creationTimestamp"))
+    created_key = (0, 0.0) if ct is None else (1, -ct)
+    return (1 if (pod.get("spec") or {}).get("nodeName") else 0, phase, 1 if ready else 0, ready_key, -restarts,
+            created_key)
+
+
 def pod_is_available(pod, min_ready_seconds=0, now=None):
     """`podutil.IsPodAvailable`: Ready, and Ready for at least minReadySeconds."""
     for c in (pod.get("status") or {}).get("conditions") or ():

@@ -18,7 +18,7 @@ from ..api import meta as m
 from ..api.meta import now_rfc3339, parse_rfc3339
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
 from ..api.labels import selector_to_string
-from .base import Controller, Expectations, controller_ref, pod_from_template, split_key
+from .base import Controller, Expectations, active_pods_key, controller_ref, pod_from_template, split_key
 
 
 DEFAULT_JOB_BACKOFF = 10.0       # job_controller.go DefaultJobBackOff
@@ -31,13 +31,8 @@ def job_finished(job):
 
 
 def active_pod_rank(p):
-    """`controller.ActivePods` order: unassigned < assigned, pending < unknown < running,
-    not-ready < ready, newer first — the pods to delete first come first."""
-    st = p.get("status") or {}
-    phase = {"Pending": 0, "Unknown": 1, "Running": 2}.get(st.get("phase"), 0)
-    ready = any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or ())
-    return (1 if (p.get("spec") or {}).get("nodeName") else 0, phase, 1 if ready else 0,
-            -(parse_rfc3339(p["metadata"].get("creationTimestamp")) or 0))
+    """`controller.ActivePods` order (the pods to delete first come first)."""
+    return active_pods_key(p)
 
 
 class JobController(Controller):

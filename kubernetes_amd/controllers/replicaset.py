@@ -1,8 +1,9 @@
 """ReplicaSet / ReplicationController controller.
 
-Parity: `pkg/controller/replicaset/replica_set.go` (manageReplicas with expectations, adoption
-of orphans via ControllerRefManager, deletion ranking: unscheduled < pending < not-ready <
-ready, status calculation) and `pkg/controller/replication` (same logic over
+Parity: `pkg/controller/replicaset/replica_set.go` (manageReplicas with expectations and
+slow-start batches, adoption of orphans and release of non-matching pods via
+ControllerRefManager, deletion order `controller.ActivePods`: unscheduled < pending < not-ready <
+ready for less time < more restarts < newer, status calculation with ReplicaFailure) and `pkg/controller/replication` (same logic over
 ReplicationController with a map selector).
 """
 from __future__ import annotations
@@ -12,8 +13,8 @@ import asyncio
 from ..api import meta as m
 from ..api.labels import selector_from_set
 from ..client.rest import APIStatusError, is_not_found
-from .base import (Controller, Expectations, controller_ref, pod_from_template, pod_is_active, pod_is_available,
-                   pod_is_ready, selector_of, split_key)
+from .base import (Controller, Expectations, active_pods_key, claim_objects, controller_ref, pod_from_template,
+                   pod_is_active, pod_is_available, pod_is_ready, selector_of, split_key)
 
 BURST = 500  # slowStartBatch upper bound per sync
 
@@ -85,25 +86,12 @@ class ReplicaSetController(Controller):
             self.exp.delete(key)
             return
         ns, name = split_key(key)
-        uid = rs["metadata"]["uid"]
         sel = self._selector(rs)
-        owned = []
-        # claim pods: owned by uid, or orphans that match (adopt)
-        for p in self.pod_inf.store.by_index("namespace", ns):
-            ref = controller_ref(p)
-            if ref is not None:
-                if ref.get("uid") == uid:
-                    owned.append(p)
-                continue
-            if rs["metadata"].get("deletionTimestamp") or not sel.matches(p["metadata"].get("labels") or {}):
-                continue
-            if pod_is_active(p):
-                try:
-                    refs = list(p["metadata"].get("ownerReferences") or []) + [m.owner_reference(rs)]
-                    p = await self.client.patch("pods", p["metadata"]["name"], {"metadata": {"ownerReferences": refs, "uid": p["metadata"]["uid"]}}, ns)
-                    owned.append(p)
-                except APIStatusError:
-                    pass
+        # claim pods (ControllerRefManager): keep matching owned pods, release owned pods whose
+        # labels stopped matching, adopt matching active orphans
+        owned = await claim_objects(self.client, rs, "pods", self.pod_inf.store.by_index("namespace", ns),
+                                    lambda p: sel.matches(p["metadata"].get("labels") or {}),
+                                    ignore=lambda p: not pod_is_active(p))
         active = [p for p in owned if pod_is_active(p)]
         err = None
         if self.exp.satisfied(key) and not rs["metadata"].get("deletionTimestamp"):
@@ -142,7 +130,7 @@ class ReplicaSetController(Controller):
                 batch *= 2
             self.recorder.event(rs, "Normal", "SuccessfulCreate", f"Created {n} pods")
         elif diff > 0:
-            victims = sorted(active, key=_deletion_rank)[:min(diff, BURST)]
+            victims = sorted(active, key=active_pods_key)[:min(diff, BURST)]
             self.exp.expect(key, dels=len(victims))
 
             async def rm(p):
@@ -187,14 +175,6 @@ class ReplicaSetController(Controller):
         except APIStatusError as e:
             if not is_not_found(e):
                 raise
-
-
-def _deletion_rank(p):
-    """Prefer deleting: unassigned < pending < unknown < running; not-ready < ready; newer first."""
-    st = p.get("status") or {}
-    assigned = 1 if (p.get("spec") or {}).get("nodeName") else 0
-    phase = {"Pending": 0, "Unknown": 1, "Running": 2}.get(st.get("phase"), 0)
-    return (assigned, phase, 1 if pod_is_ready(p) else 0, -(m.parse_rfc3339(p["metadata"].get("creationTimestamp")) or 0))
 
 
 class ReplicationControllerController(ReplicaSetController):
