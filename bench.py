@@ -96,19 +96,23 @@ def cpu_budget():
 
 
 # Per-pod host CPU of each control-plane component at the N=1 headline rate, measured on the
-# MI355X box (profiles/r4_gpu/bench_r4g.json `cpu_ms_per_pod`: API server 0.80 ms, scheduler
-# 0.46 ms, hollow kubelets 0.69 ms per pod at 3416 pods/s; the hollow kubelets were 1.55 ms
-# before the device-plugin RPCs moved to utils/grpclite). A whole node sizes each component for
-# the load of `world` ranks at that rate, at most ~70 % busy, instead of a fixed-size control plane.
-N1_RATE_PODS_PER_S = 3400.0
-CPU_MS_PER_POD = {"apiserver": 0.80, "scheduler": 0.46, "hollow": 0.69}
+# MI355X box in round 5 (profiles/r5_gpu/bench_r5{b,c}*.json `cpu_ms_per_pod`, protobuf watch
+# streams: API server 0.61-0.63 ms, scheduler 0.29-0.33 ms, hollow kubelets 0.50-0.53 ms per pod
+# at 4613-4864 pods/s). A whole node sizes each component for the load of `world` ranks at that
+# rate so that at linear weak scaling every process is at most 70 % busy with HEADROOM to spare
+# (ceilings at 70 % busy >= 1.3x the linear rate: profiles/r5_gpu/whole_node_ceiling.md),
+# instead of a fixed-size control plane.
+N1_RATE_PODS_PER_S = 4700.0
+CPU_MS_PER_POD = {"apiserver": 0.62, "scheduler": 0.32, "hollow": 0.51}
 TARGET_UTIL = 0.7
+HEADROOM = 1.3
 
 
 def demand(component, world):
-    """Processes `component` needs so that `world` ranks at the N=1 rate keep it <= 70 % busy."""
+    """Processes `component` needs so that `world` ranks at HEADROOM x the N=1 rate keep it
+    <= 70 % busy."""
     import math
-    return max(1, math.ceil(world * N1_RATE_PODS_PER_S * CPU_MS_PER_POD[component] / 1000.0 / TARGET_UTIL))
+    return max(1, math.ceil(world * N1_RATE_PODS_PER_S * HEADROOM * CPU_MS_PER_POD[component] / 1000.0 / TARGET_UTIL))
 
 
 def control_plane_shape(world, workers=0, shards=0):
@@ -118,10 +122,12 @@ def control_plane_shape(world, workers=0, shards=0):
     (profiles/r2_partitioned: n1_shapes, scale_r2d; profiles/r2_density_clients/worker_sweep):
     N=1 w=3 s=2 (2594-2611 pods/s; w=2 2363-2389, w=4 2380-2462), N=4 w=4 s=4 (3184 vs w=4 s=2
     2727). A whole 8-GPU node (>= 64 CPUs) is sized from the per-pod CPU of each component
-    (`demand`): at N=8 that is 32 API workers and 18 scheduler shards — ceilings of ~40 k and
-    ~39 k pods/s against the 27.2 k that linear weak scaling needs (the round-3 caps of 16 / 8
-    capped it at ~14 k) — scaled down together with the hollow-node processes when the CPU
-    budget is smaller (`cpus - ranks - store threads`)."""
+    (`demand`): at N=8 that is 44 API workers and 23 scheduler shards — ceilings at 70 % busy of
+    ~49.7 k and ~50.3 k pods/s against the 37.6 k that linear weak scaling needs (the round-3 caps
+    of 16 / 8 capped it at ~14 k) — scaled down together with the hollow-node processes when the
+    CPU budget is smaller (`cpus - ranks - store threads`). Pods and events are not cached by the
+    API workers (the store's fan-out serves their watches) and scheduler shards only see their
+    own unassigned pods and their own nodes' pods, so adding processes does not add per-pod work."""
     cpus = cpu_budget()
     spare = cpus - world - 1
     big = cpus >= 64
@@ -158,7 +164,7 @@ def hollow_procs_for(world, nodes_per_rank, workers, shards, want=0):
     spare = cpus - workers - shards - 1
     if cpus >= 64:
         # a whole node: the hollow kubelets' share of the per-pod demand model, per rank
-        # (4 processes per rank at 0.69 ms per pod), but at least 6 — hollow kubelets wait on
+        # (5 processes per rank at 0.51 ms per pod with headroom), but at least 6 — hollow kubelets wait on
         # the control plane, and 6 beat 4 per rank in interleaved box runs at both API shapes
         # (profiles/r4_gpu/sweep: w4 s3 h6 3982-4062 vs h4 3537-3828 pods/s) — within the CPUs left
         per_rank = max(6, -(-demand("hollow", world) // world))
