@@ -48,7 +48,20 @@ def run_until_signal(main_coro_factory):
                 loop.add_signal_handler(s, stop.set)
             except NotImplementedError:
                 pass
-        comp = await main_coro_factory()
+        # a signal during startup (informer syncs, leader election) ends the process too,
+        # without waiting for the component to finish starting
+        starting = asyncio.ensure_future(main_coro_factory())
+        stopping = asyncio.ensure_future(stop.wait())
+        await asyncio.wait({starting, stopping}, return_when=asyncio.FIRST_COMPLETED)
+        if not starting.done():
+            starting.cancel()
+            try:
+                await starting
+            except BaseException:       # noqa: BLE001 - cancelled startup, exiting anyway
+                pass
+            return
+        stopping.cancel()
+        comp = starting.result()
         tune_gc()
         await stop.wait()
         closer = getattr(comp, "stop", None)

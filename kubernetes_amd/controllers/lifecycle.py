@@ -106,6 +106,11 @@ def _dump(o):
 
 
 class PodGCController(Controller):
+    """`pkg/controller/podgc/gc_controller.go`, every 20 s: `gcTerminated` (the oldest
+    terminated pods beyond `--terminated-pod-gc-threshold`; <= 0 disables it), `gcOrphaned`
+    (pods bound to a node that no longer exists, checked against a live node list) and
+    `gcUnscheduledTerminating` (terminating pods that were never scheduled: no kubelet will
+    finish their deletion) — all force-deleted (grace period 0)."""
     name = "podgc"
     workers = 1
 
@@ -135,15 +140,23 @@ class PodGCController(Controller):
 
     async def sync(self, key):
         pods = self.pod_inf.list()
-        term = [p for p in pods if core.pod_is_terminal(p)]
-        if len(term) > self.threshold:
-            term.sort(key=lambda p: p["metadata"].get("creationTimestamp", ""))
-            for p in term[:len(term) - self.threshold]:
-                await self._force(p)
-        nodes = {n["metadata"]["name"] for n in self.node_inf.list()}
+        if self.threshold > 0:
+            term = [p for p in pods if core.pod_is_terminal(p)]
+            if len(term) > self.threshold:
+                term.sort(key=lambda p: p["metadata"].get("creationTimestamp", ""))
+                await asyncio.gather(*(self._force(p) for p in term[:len(term) - self.threshold]))
+        bound = [p for p in pods if (p.get("spec") or {}).get("nodeName")]
+        if bound:
+            try:      # the reference lists nodes from the API server, not a possibly lagging cache
+                nodes = {n["metadata"]["name"] for n in (await self.client.list("nodes"))["items"]}
+            except APIStatusError:
+                nodes = None
+            if nodes is not None:
+                for p in bound:
+                    if p["spec"]["nodeName"] not in nodes:
+                        await self._force(p)
         for p in pods:
-            nn = (p.get("spec") or {}).get("nodeName")
-            if nn and nn not in nodes and self.node_inf.has_synced():
+            if p["metadata"].get("deletionTimestamp") and not (p.get("spec") or {}).get("nodeName"):
                 await self._force(p)
 
     async def _force(self, p):

@@ -298,7 +298,9 @@ def test_dynamic_provisioning_switch(run):
 
     async def main():
         pv = PersistentVolumeController(None, None, enable_dynamic_provisioning=False)
-        assert await pv._provision({"metadata": {"name": "c", "namespace": "d", "uid": "u"}, "spec": {}}) is None
+        # provisionClaim returns before touching the class, the claim or the API
+        assert await pv.provision_claim({"metadata": {"name": "c", "namespace": "d", "uid": "u"},
+                                         "spec": {"storageClassName": "gold"}}) is None
     run(main(), timeout=10)
 
 
