@@ -44,6 +44,7 @@ from .volumes import VolumeError, VolumeManager
 from ..utils.tasks import spawn
 
 log = logging.getLogger("kubelet")
+CONTROLLER_MANAGED_ATTACH = "volumes.kubernetes.io/controller-managed-attach-detach"
 
 _ip_counter = itertools.count(2)
 
@@ -222,6 +223,7 @@ class Kubelet:
         self.orphan_grace = 10.0   # s after the first sync before unknown runtime pods are removed
         self.adopted_pods = 0
         self._status_dirty = asyncio.Event()
+        self.volumes.on_in_use_change = self._status_dirty.set
         self._status_sem = asyncio.Semaphore(max_status_inflight)
         self._status_inflight: dict[str, asyncio.Task] = {}
         self._status_next: dict[str, tuple] = {}
@@ -412,7 +414,11 @@ class Kubelet:
             spec["unschedulable"] = True
         if self.provider_id:
             spec["providerID"] = self.provider_id
-        node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node_name, "labels": labels},
+        # --enable-controller-attach-detach (always on here): the attach/detach controller, not
+        # this kubelet, attaches the node's volumes (`kubelet_node_status.go` initialNode)
+        node = {"apiVersion": "v1", "kind": "Node",
+                "metadata": {"name": self.node_name, "labels": labels,
+                             "annotations": {CONTROLLER_MANAGED_ATTACH: "true"}},
                 "spec": spec, "status": self._node_status()}
         return node
 
@@ -462,6 +468,9 @@ class Kubelet:
                                      "lastHeartbeatTime": now, "lastTransitionTime": now})
         if ers:
             st["extendedResources"] = ers
+        # volumes this node has mounted (or is about to): the attach/detach controller does not
+        # detach them (`kubelet_node_status.go` setNodeVolumesInUseStatus)
+        st["volumesInUse"] = self.volumes.volumes_in_use() or None
         return st
 
     def _allocatable(self, capacity):
@@ -504,6 +513,8 @@ class Kubelet:
                 if e.code == 409:
                     cur = await self.client.get("nodes", self.node_name)
                     cur["metadata"]["labels"] = {**(cur["metadata"].get("labels") or {}), **node["metadata"]["labels"]}
+                    cur["metadata"]["annotations"] = {**(cur["metadata"].get("annotations") or {}),
+                                                      **node["metadata"]["annotations"]}
                     cur["status"] = node["status"]
                     await self.client.update("nodes", cur)
                     await self.client.update_status("nodes", cur)

@@ -212,6 +212,8 @@ class VolumeManager:
         self.node_name = node_name
         self.attach_timeout = attach_timeout
         self.csi_published: dict[str, list] = {}     # pod uid -> [(driver, volume handle, target)]
+        self.in_use: dict[str, set] = {}             # pod uid -> unique names of its attachable volumes
+        self.on_in_use_change = None                 # callback: node status should report volumesInUse
         self.allocatable = None                      # node allocatable: default downward-API limits
         self.host_ip = None                          # the node's address (status.hostIP)
 
@@ -336,6 +338,9 @@ class VolumeManager:
         from ..csi.driver import CSIClient, volume_attributes
         src = sp["csi"]
         driver, handle = src["driver"], src["volumeHandle"]
+        # reported in use before the mount (`MarkVolumesAsReportedInUse`): from now on the
+        # attach/detach controller will not detach it under us
+        self._mark_in_use(pod, f"kubernetes.io/csi/{driver}^{handle}")
         va_name = CSI.attachment_name(pv_name, driver, node_name)
         deadline = asyncio.get_running_loop().time() + self.attach_timeout
         info = {}
@@ -482,6 +487,20 @@ class VolumeManager:
                 pass
             finally:
                 await c.close()
+        if self.in_use.pop(pod["metadata"]["uid"], None) and self.on_in_use_change:
+            self.on_in_use_change()
+
+    def _mark_in_use(self, pod, name):
+        s = self.in_use.setdefault(pod["metadata"]["uid"], set())
+        if name not in s:
+            s.add(name)
+            if self.on_in_use_change:
+                self.on_in_use_change()
+
+    def volumes_in_use(self):
+        """node.status.volumesInUse: unique names of the attachable volumes mounted (or being
+        mounted) for this node's pods."""
+        return sorted(set().union(*self.in_use.values())) if self.in_use else []
 
     async def refresh(self, pod, node_name=None, pod_ip=None):
         """Re-project the pod's configMap / secret / downwardAPI / projected volumes into their
