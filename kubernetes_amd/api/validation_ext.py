@@ -278,11 +278,38 @@ def validate_limit_range(lr):
 _QUOTA_SCOPES = ("Terminating", "NotTerminating", "BestEffort", "NotBestEffort")
 
 
+_STANDARD_QUOTA_RESOURCES = frozenset((
+    "cpu", "memory", "ephemeral-storage", "requests.cpu", "requests.memory", "requests.storage",
+    "requests.ephemeral-storage", "limits.cpu", "limits.memory", "limits.ephemeral-storage", "pods", "resourcequotas",
+    "services", "replicationcontrollers", "secrets", "persistentvolumeclaims", "configmaps", "services.nodeports",
+    "services.loadbalancers"))
+_POD_COMPUTE_QUOTA = frozenset(("cpu", "memory", "limits.cpu", "limits.memory", "requests.cpu", "requests.memory"))
+
+
+def _quota_scope_valid_for(scope, resource):
+    """`helper.IsResourceQuotaScopeValidForResource` (the fork's pod extended resources are
+    pod-tracked too, so the compute scopes accept them)."""
+    if scope == "BestEffort":
+        return resource == "pods"
+    if scope in ("Terminating", "NotTerminating", "NotBestEffort"):
+        return resource == "pods" or resource in _POD_COMPUTE_QUOTA or (
+            "/" in resource and not resource.startswith("count/") and ".storageclass.storage.k8s.io/" not in resource)
+    return True
+
+
 def validate_resource_quota(rq):
+    """`ValidateResourceQuota`: hard names are standard quota resources, hugepages or fully
+    qualified (`count/<resource>[.<group>]`, `<class>.storageclass.storage.k8s.io/...`, extended
+    resources); quantities are non-negative; scopes are standard, not contradictory, and every
+    hard name is one the scopes can track."""
     errs = _meta(rq)
     spec = rq.get("spec") or {}
-    for k, v in (spec.get("hard") or {}).items():
-        if not (is_qualified_name(k) or "." in k or "/" in k):
+    hard = spec.get("hard") or {}
+    for k, v in hard.items():
+        if "/" not in k:
+            if not (k in _STANDARD_QUOTA_RESOURCES or k.startswith(("hugepages-", "requests.hugepages-"))):
+                errs.append(invalid(f"spec.hard[{k}]", "must be a standard resource for quota"))
+        elif not is_qualified_name(k):
             errs.append(invalid(f"spec.hard[{k}]", "must be a standard resource for quota"))
         try:
             if parse_quantity(str(v)).value < 0:
@@ -293,10 +320,21 @@ def validate_resource_quota(rq):
     for i, sc in enumerate(scopes):
         if sc not in _QUOTA_SCOPES:
             errs.append(not_supported(f"spec.scopes[{i}]", sc))
+            continue
+        for k in hard:
+            if not _quota_scope_valid_for(sc, k):
+                errs.append(invalid("spec.scopes", f"unsupported scope applied to resource {k}"))
     for a, b in (("Terminating", "NotTerminating"), ("BestEffort", "NotBestEffort")):
         if a in scopes and b in scopes:
             errs.append(invalid("spec.scopes", f"conflicting scopes {a} and {b}"))
     return errs
+
+
+def validate_resource_quota_update(new, old):
+    """`ValidateResourceQuotaUpdate`: scopes are immutable."""
+    if sorted((new.get("spec") or {}).get("scopes") or ()) != sorted((old.get("spec") or {}).get("scopes") or ()):
+        return [invalid("spec.scopes", "field is immutable")]
+    return []
 
 
 def validate_service_account(sa):
@@ -1073,6 +1111,7 @@ UPDATE_VALIDATORS = {
     "Job": validate_job_update, "PodDisruptionBudget": validate_pdb_update,
     "RoleBinding": validate_role_binding_update, "ClusterRoleBinding": validate_role_binding_update,
     "StorageClass": validate_storage_class_update, "PriorityClass": validate_priority_class_update,
+    "ResourceQuota": validate_resource_quota_update,
 }
 
 
