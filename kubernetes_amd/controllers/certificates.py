@@ -322,32 +322,53 @@ class ClusterRoleAggregationController(Controller):
 
 
 TTL_ANN = "node.alpha.kubernetes.io/ttl"
-TTL_BOUNDARIES = ((100, 0), (500, 15), (1000, 30), (2000, 60))
+# `ttl_controller.go` ttlBoundaries: (sizeMin, sizeMax, ttlSeconds); the overlapping ranges are
+# the hysteresis that keeps a cluster near a boundary from flapping
+TTL_BOUNDARIES = ((0, 100, 0), (90, 500, 15), (450, 1000, 30), (900, 2000, 60), (1800, 10000, 300),
+                  (9000, 2 ** 31 - 1, 600))
 
 
 def ttl_for(n):
-    for limit, ttl in TTL_BOUNDARIES:
-        if n <= limit:
-            return ttl
-    return 300
+    """The TTL a cluster grown node by node from zero to n nodes settles on."""
+    step = 0
+    while n > TTL_BOUNDARIES[step][1]:
+        step += 1
+    return TTL_BOUNDARIES[step][2]
 
 
 class TTLController(Controller):
+    """`pkg/controller/ttl/ttl_controller.go`: every node carries
+    `node.alpha.kubernetes.io/ttl` — how long a kubelet may cache secrets/configmaps — set from
+    the cluster size; node adds move the boundary step up past sizeMax, deletes move it down
+    below sizeMin (hysteresis), and a node is patched when its annotation differs."""
     name = "ttl"
     workers = 1
 
     def setup(self):
         self.node_inf = self.factory.get("nodes")
-        self.node_inf.add_handler(self._all, lambda o, n: self.enqueue(n), self._all)
+        self.node_count = 0
+        self.step = 0
+        self.node_inf.add_handler(self._add, lambda o, n: self.enqueue(n), self._delete)
 
-    def _all(self, _):
-        for n in self.node_inf.list():
-            self.enqueue(n)
+    @property
+    def desired_ttl(self):
+        return TTL_BOUNDARIES[self.step][2]
+
+    def _add(self, node):
+        self.node_count += 1
+        if self.node_count > TTL_BOUNDARIES[self.step][1]:
+            self.step += 1
+        self.enqueue(node)
+
+    def _delete(self, node):
+        self.node_count -= 1
+        if self.step > 0 and self.node_count < TTL_BOUNDARIES[self.step][0]:
+            self.step -= 1
 
     async def sync(self, key):
         node = self.node_inf.get(key)
         if node is None:
             return
-        want = str(ttl_for(len(self.node_inf.list())))
+        want = str(self.desired_ttl)
         if (node["metadata"].get("annotations") or {}).get(TTL_ANN) != want:
             await self.client.patch("nodes", key, {"metadata": {"annotations": {TTL_ANN: want}}})

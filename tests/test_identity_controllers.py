@@ -157,3 +157,22 @@ async def _get_sa_with_secret(c, ns, name):
     except Exception:
         return None
     return sa if sa.get("secrets") else None
+
+
+def test_ttl_boundaries_hysteresis():
+    """ttl_controller_test.go TestDesiredTTL: adding past sizeMax steps up, deleting below
+    sizeMin steps down — in between the TTL holds."""
+    from kubernetes_amd.controllers.certificates import TTLController
+    t = TTLController.__new__(TTLController)
+    t.node_count, t.step = 0, 0
+    t.enqueue = lambda n: None
+    for _ in range(101):
+        t._add({})
+    assert t.desired_ttl == 15
+    for _ in range(6):
+        t._delete({})                 # 95 nodes: above sizeMin 90 of the 15 s step
+    assert t.desired_ttl == 15
+    for _ in range(6):
+        t._delete({})                 # 89 nodes
+    assert t.desired_ttl == 0
+    assert ttl_for(20000) == 600
