@@ -29,6 +29,7 @@ import json
 import random
 import time
 
+from ..api import meta as m
 from ..api.labels import label_selector_as_selector
 from ..api.meta import parse_rfc3339
 from ..client.rest import APIStatusError, is_already_exists, is_not_found
@@ -66,25 +67,52 @@ class TokensController(Controller):
                 root_ca = f.read()
         self.key = private_key
         self.root_ca = root_ca or ""
+        self._deleted_refs: dict = {}          # deleted token secret -> (account name, account uid)
 
     def setup(self):
         self.sa_inf = self.factory.get("serviceaccounts")
         self.sec_inf = self.factory.get("secrets")
-        self.sa_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), self.enqueue)
-        self.sec_inf.add_handler(self._secret, None, self._secret)
+        self.sa_inf.add_handler(self._sa, lambda o, n: self._sa(n), self._sa)
+        self.sec_inf.add_handler(self._secret, lambda o, n: self._secret(n), self._secret_deleted)
+
+    def _sa(self, sa):
+        self.queue.add("sa:" + m.ns_name(sa))
 
     def _secret(self, sec):
         if sec.get("type") == SA_TOKEN:
+            self.queue.add("secret:" + m.ns_name(sec))
+
+    def _secret_deleted(self, sec):
+        """`deleteSecret`: the service account must stop referencing it."""
+        if sec.get("type") == SA_TOKEN:
             ann = sec["metadata"].get("annotations") or {}
-            self.enqueue(f"{sec['metadata']['namespace']}/{ann.get(SA_NAME_ANN, '')}")
+            self._deleted_refs[m.ns_name(sec)] = (ann.get(SA_NAME_ANN, ""), ann.get(SA_UID_ANN, ""))
+            self.queue.add("secret:" + m.ns_name(sec))
 
     def _tokens_of(self, ns, name, uid):
         return [s for s in self.sec_inf.list() if s.get("type") == SA_TOKEN and s["metadata"].get("namespace") == ns
                 and (s["metadata"].get("annotations") or {}).get(SA_NAME_ANN) == name]
 
+    def resync_keys(self):
+        return ["sa:" + m.ns_name(sa) for sa in self.sa_inf.list()]
+
     async def sync(self, key):
         if not self.key:
             return
+        kind, _, k = key.partition(":")
+        if kind == "secret":
+            await self.sync_secret(k)
+        else:
+            await self.sync_service_account(k if kind == "sa" else key)
+
+    def _token_data(self, sa, ns, secret_name):
+        from ..apiserver.authn import service_account_token
+        return {"token": _b64(service_account_token(self.key, sa, secret_name)), "namespace": _b64(ns),
+                "ca.crt": _b64(self.root_ca)}
+
+    async def sync_service_account(self, key):
+        """`syncServiceAccount`: a deleted account's tokens are deleted; a live one gets a token
+        secret if it references none (`ensureReferencedToken`)."""
         ns, name = split_key(key)
         sa = self.sa_inf.get(key)
         toks = self._tokens_of(ns, name, None)
@@ -98,20 +126,19 @@ class TokensController(Controller):
             return
         uid = sa["metadata"].get("uid", "")
         live = [t for t in toks if (t["metadata"].get("annotations") or {}).get(SA_UID_ANN) == uid]
+        refs = [r.get("name") for r in sa.get("secrets") or ()]
+        if any(t["metadata"]["name"] in refs for t in live):
+            return                 # hasReferencedToken
         if not live:
-            from ..apiserver.authn import service_account_token
             sname = f"{name}-token-{''.join(random.choice('bcdfghjklmnpqrstvwxz2456789') for _ in range(5))}"
             sec = {"metadata": {"name": sname, "namespace": ns, "annotations": {SA_NAME_ANN: name, SA_UID_ANN: uid}},
-                   "type": SA_TOKEN,
-                   "data": {"token": _b64(service_account_token(self.key, sa, sname)), "namespace": _b64(ns),
-                            "ca.crt": _b64(self.root_ca)}}
+                   "type": SA_TOKEN, "data": self._token_data(sa, ns, sname)}
             try:
                 await self.client.create("secrets", sec, ns)
             except APIStatusError as e:
                 if not is_already_exists(e):
                     raise
             live = [sec]
-        refs = [r.get("name") for r in sa.get("secrets") or ()]
         want = refs + [t["metadata"]["name"] for t in live if t["metadata"]["name"] not in refs]
         if want != refs:
             # an update of the live object (`tokens_controller.go` ensureReferencedToken): the
@@ -123,6 +150,47 @@ class TokensController(Controller):
             if add:
                 live_sa["secrets"] = (live_sa.get("secrets") or []) + [{"name": n} for n in add]
                 await self.client.update("serviceaccounts", live_sa, ns)
+
+    async def sync_secret(self, key):
+        """`syncSecret`: a deleted token secret is removed from its account's references; a token
+        secret whose account is gone (or is another account by UID) is deleted; one missing its
+        token, namespace or CA data gets them (`generateTokenIfNeeded`)."""
+        ns, name = split_key(key)
+        sec = self.sec_inf.get(key)
+        if sec is None:
+            sa_name, sa_uid = self._deleted_refs.pop(key, ("", ""))
+            sa = self.sa_inf.get(f"{ns}/{sa_name}") if sa_name else None
+            if sa is None or (sa_uid and sa["metadata"].get("uid") != sa_uid):
+                return
+            if any(r.get("name") == name for r in sa.get("secrets") or ()):
+                live_sa = await self.client.get("serviceaccounts", sa_name, ns)
+                live_sa["secrets"] = [r for r in live_sa.get("secrets") or () if r.get("name") != name]
+                await self.client.update("serviceaccounts", live_sa, ns)
+            self.queue.add(f"sa:{ns}/{sa_name}")       # it may need a new token
+            return
+        ann = sec["metadata"].get("annotations") or {}
+        sa = self.sa_inf.get(f"{ns}/{ann.get(SA_NAME_ANN, '')}")
+        if sa is None or (ann.get(SA_UID_ANN) and sa["metadata"].get("uid") != ann.get(SA_UID_ANN)):
+            try:
+                await self.client.delete("secrets", name, ns)
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise
+            return
+        data = sec.get("data") or {}
+        want_ns, want_ca = _b64(ns), _b64(self.root_ca)
+        needs = (not data.get("token"), data.get("namespace") != want_ns, bool(self.root_ca) and data.get("ca.crt") != want_ca)
+        if not any(needs):
+            return
+        live = await self.client.get("secrets", name, ns)
+        d = dict(live.get("data") or {})
+        if needs[0]:
+            d["token"] = self._token_data(sa, ns, name)["token"]
+        d["namespace"] = want_ns
+        if self.root_ca:
+            d["ca.crt"] = want_ca
+        live["data"] = d
+        await self.client.update("secrets", live, ns)
 
 
 def jws_detached(token_id, token_secret, payload: str) -> str:
