@@ -359,6 +359,59 @@ class CSRSigningController(Controller):
         await self.client.update_status("certificatesigningrequests", csr)
 
 
+class CSRCleanerController(Controller):
+    """`pkg/controller/certificates/cleaner/cleaner.go`: every pollingInterval (1 h) each CSR is
+    deleted when it was approved and issued more than an hour ago, denied more than an hour ago,
+    left unhandled (no conditions) for a day, or carries an issued certificate that has expired."""
+    name = "csrcleaner"
+    workers = 1
+    resync_period = 3600.0          # pollingInterval
+    APPROVED_EXPIRATION = 3600.0
+    DENIED_EXPIRATION = 3600.0
+    PENDING_EXPIRATION = 24 * 3600.0
+
+    primary = "certificatesigningrequests"
+
+    def setup(self):
+        self.csr_inf = self.factory.get("certificatesigningrequests")
+        self.csr_inf.add_handler(self.enqueue, None, None)      # the initial list: wait.Until runs at once
+
+    @classmethod
+    def should_clean(cls, csr, now=None):
+        now = time.time() if now is None else now
+
+        def older(ts, d):
+            t = parse_rfc3339(ts) if ts else None
+            return t is not None and t < now - d
+        conds = (csr.get("status") or {}).get("conditions") or []
+        cert = (csr.get("status") or {}).get("certificate")
+        if not conds and older(csr["metadata"].get("creationTimestamp"), cls.PENDING_EXPIRATION):
+            return "pending"
+        for c in conds:
+            if c.get("type") == "Denied" and older(c.get("lastUpdateTime"), cls.DENIED_EXPIRATION):
+                return "denied"
+            if c.get("type") == "Approved" and cert:
+                if older(c.get("lastUpdateTime"), cls.APPROVED_EXPIRATION):
+                    return "approved"
+                from ..native import crypto
+                try:
+                    if crypto.cert_not_after(base64.b64decode(cert).decode()) < now:
+                        return "expired"
+                except Exception:      # noqa: BLE001 - `isExpired`: an unparsable certificate is an error, not a clean
+                    return None
+        return None
+
+    async def sync(self, key):
+        csr = self.csr_inf.get(key)
+        if csr is None or not self.should_clean(csr):
+            return
+        try:
+            await self.client.delete("certificatesigningrequests", key)
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise
+
+
 class ClusterRoleAggregationController(Controller):
     name = "clusterroleaggregation"
     workers = 1

@@ -23,11 +23,12 @@ from .deployment import DeploymentController
 from .job import CronJobController, JobController
 from .lifecycle import GarbageCollector, NamespaceController, NodeLifecycleController, PodGCController
 from .certificates import (BootstrapSignerController, ClusterRoleAggregationController, CSRApprovingController,
-                           CSRSigningController, TokenCleanerController, TokensController, TTLController)
+                           CSRCleanerController, CSRSigningController, TokenCleanerController, TokensController,
+                           TTLController)
 from .podautoscaler import HorizontalController
 from .attachdetach import AttachDetachController, ExternalAttacher
 from .network import NodeIPAMController, RouteController, ServiceLBController
-from .volume import ExpandController, PersistentVolumeController, PVCProtectionController
+from .volume import ExpandController, PersistentVolumeController, PVCProtectionController, PVProtectionController
 from .misc import DisruptionController, EndpointsController, ResourceQuotaController, ServiceAccountController
 from .replicaset import ReplicaSetController, ReplicationControllerController
 
@@ -55,10 +56,12 @@ CONTROLLERS = {
     "tokencleaner": TokenCleanerController,
     "csrapproving": CSRApprovingController,
     "csrsigning": CSRSigningController,
+    "csrcleaner": CSRCleanerController,
     "clusterroleaggregation": ClusterRoleAggregationController,
     "ttl": TTLController,
     "persistentvolume-binder": PersistentVolumeController,
     "pvc-protection": PVCProtectionController,
+    "pv-protection": PVProtectionController,
     "nodeipam": NodeIPAMController,
     "route": RouteController,
     "service": ServiceLBController,
@@ -73,18 +76,26 @@ CONTROLLERS = {
 DISABLED_BY_DEFAULT = {"nodeipam", "route", "service", "csi-attacher"}
 
 
+# the reference's `--controllers` names (`controllermanager.go:334-363`) for controllers this
+# manager runs under a different name or splits: "node" is the lifecycle half of the reference's
+# node controller (CIDR allocation is `nodeipam`, enabled by --allocate-node-cidrs)
+ALIASES = {"node": ("nodelifecycle",), "clusterrole-aggregation": ("clusterroleaggregation",)}
+
+
 def resolve(enabled):
+    def expand(e):
+        return ALIASES.get(e, (e,))
     names = set()
     for e in enabled or ["*"]:
         if e == "*":
             names |= set(CONTROLLERS) - DISABLED_BY_DEFAULT
         elif e.startswith("-"):
-            names.discard(e[1:])
+            names.difference_update(expand(e[1:]))
         else:
-            names.add(e)
+            names.update(expand(e))
     for e in enabled or []:
         if e.startswith("-"):
-            names.discard(e[1:])
+            names.difference_update(expand(e[1:]))
     return sorted(names)
 
 
@@ -100,8 +111,10 @@ SERVICE_ACCOUNTS = {
     "resourcequota": "resourcequota-controller", "disruption": "disruption-controller",
     "horizontalpodautoscaling": "horizontal-pod-autoscaler", "bootstrapsigner": "bootstrap-signer",
     "tokencleaner": "token-cleaner", "csrapproving": "certificate-controller", "csrsigning": "certificate-controller",
+    "csrcleaner": "certificate-controller",
     "clusterroleaggregation": "clusterrole-aggregation-controller", "ttl": "ttl-controller",
     "persistentvolume-binder": "persistent-volume-binder", "pvc-protection": "pvc-protection-controller",
+    "pv-protection": "pv-protection-controller",
     "route": "route-controller", "service": "service-controller", "attachdetach": "attachdetach-controller",
     "persistentvolume-expander": "expand-controller", "csi-attacher": "csi-attacher",
 }

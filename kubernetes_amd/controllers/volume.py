@@ -36,6 +36,7 @@ BOUND_BY_CONTROLLER = "pv.kubernetes.io/bound-by-controller"
 PROVISIONED_BY = "pv.kubernetes.io/provisioned-by"
 HOSTPATH_PROVISIONER = "kubernetes.io/host-path"
 PVC_PROTECTION = "kubernetes.io/pvc-protection"
+PV_PROTECTION = "kubernetes.io/pv-protection"      # `pkg/volume/util/finalizer.go:28`
 SELECTED_NODE = "volume.kubernetes.io/selected-node"
 
 
@@ -620,7 +621,24 @@ class ExpandController(Controller):
         self.recorder.event(pvc, "Normal", "VolumeResizeSuccessful", f"volume {pv['metadata']['name']} resized to {want}")
 
 
+def pod_is_terminated(pod):
+    """`volumehelper.IsPodTerminated`: Failed/Succeeded, or deleted with no container running."""
+    st = pod.get("status") or {}
+    if st.get("phase") in ("Failed", "Succeeded"):
+        return True
+    if not pod["metadata"].get("deletionTimestamp"):
+        return False
+    return all((cs.get("state") or {}).get("terminated") is not None or (cs.get("state") or {}).get("waiting") is not None
+               for cs in st.get("containerStatuses") or ())
+
+
 class PVCProtectionController(Controller):
+    """`pkg/controller/volume/pvcprotection/pvc_protection_controller.go`: a claim being deleted
+    keeps its `kubernetes.io/pvc-protection` finalizer while a scheduled, non-terminated pod in
+    its namespace uses it (`isBeingUsed` :213 — unscheduled pods do not block); a live claim
+    without the finalizer gets it (the admission plugin normally adds it, :174). Pod events
+    only enqueue claims when the pod could unblock them: deleted, terminated or unscheduled
+    (`podAddedDeletedUpdated` :272)."""
     name = "pvc-protection"
     workers = 1
 
@@ -628,9 +646,13 @@ class PVCProtectionController(Controller):
         self.pvc_inf = self.factory.get("persistentvolumeclaims")
         self.pod_inf = self.factory.get("pods")
         self.pvc_inf.add_handler(self.enqueue, lambda o, n: self.enqueue(n), None)
-        self.pod_inf.add_handler(None, lambda o, n: self._pod(n), self._pod)
+        self.pod_inf.add_handler(self._pod, lambda o, n: self._pod(n), lambda p: self._pod(p, deleted=True))
+        if "namespace" not in self.pod_inf.store.indexers:
+            self.pod_inf.store.add_indexer("namespace", lambda p: [p["metadata"].get("namespace", "")])
 
-    def _pod(self, pod):
+    def _pod(self, pod, deleted=False):
+        if not deleted and not pod_is_terminated(pod) and (pod.get("spec") or {}).get("nodeName"):
+            return
         ns = pod["metadata"].get("namespace")
         for v in (pod.get("spec") or {}).get("volumes") or ():
             c = (v.get("persistentVolumeClaim") or {}).get("claimName")
@@ -638,8 +660,8 @@ class PVCProtectionController(Controller):
                 self.enqueue(f"{ns}/{c}")
 
     def _in_use(self, ns, name):
-        for p in self.pod_inf.list():
-            if p["metadata"].get("namespace") != ns or (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+        for p in self.pod_inf.store.by_index("namespace", ns):
+            if not (p.get("spec") or {}).get("nodeName") or pod_is_terminated(p):
                 continue
             if any((v.get("persistentVolumeClaim") or {}).get("claimName") == name for v in (p.get("spec") or {}).get("volumes") or ()):
                 return True
@@ -658,6 +680,38 @@ class PVCProtectionController(Controller):
             return
         if PVC_PROTECTION not in fins:
             await self.client.patch("persistentvolumeclaims", name, {"metadata": {"finalizers": fins + [PVC_PROTECTION]}}, ns)
+
+
+class PVProtectionController(Controller):
+    """`pkg/controller/volume/pvprotection/pv_protection_controller.go`: a PersistentVolume being
+    deleted keeps its `kubernetes.io/pv-protection` finalizer while it is Bound (`isBeingUsed`);
+    once released the finalizer is removed with an update of the live object so the deletion
+    completes. Only deletion candidates are queued (`pvAddedUpdated`)."""
+    name = "pv-protection"
+    workers = 1
+
+    def setup(self):
+        self.pv_inf = self.factory.get("persistentvolumes")
+        self.pv_inf.add_handler(self._pv, lambda o, n: self._pv(n), None)
+
+    def _pv(self, pv):
+        if pv["metadata"].get("deletionTimestamp") and PV_PROTECTION in (pv["metadata"].get("finalizers") or ()):
+            self.enqueue(pv["metadata"]["name"])
+
+    async def sync(self, key):
+        pv = self.pv_inf.get(key)
+        if pv is None or not pv["metadata"].get("deletionTimestamp") or \
+                PV_PROTECTION not in (pv["metadata"].get("finalizers") or ()):
+            return
+        if (pv.get("status") or {}).get("phase") == "Bound":
+            return
+        live = dict(pv, metadata=dict(pv["metadata"]))
+        live["metadata"]["finalizers"] = [f for f in pv["metadata"]["finalizers"] if f != PV_PROTECTION]
+        try:
+            await self.client.update("persistentvolumes", live)
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise
 
 
 def _key(o):

@@ -176,3 +176,34 @@ def test_ttl_boundaries_hysteresis():
         t._delete({})                 # 89 nodes
     assert t.desired_ttl == 0
     assert ttl_for(20000) == 600
+
+
+def test_csr_cleaner_criteria():
+    """cleaner_test.go TestCleanerWithApprovedExpiredCSR table: approved+issued > 1 h, denied
+    > 1 h, pending > 24 h and expired certificates are cleaned; fresh ones are kept."""
+    from kubernetes_amd.controllers.certificates import CSRCleanerController as C
+    now = time.time()
+
+    def csr(created_ago, conds=(), cert=None):
+        c = {"metadata": {"name": "c", "creationTimestamp": now_rfc3339(now - created_ago)},
+             "status": {"conditions": [{"type": t, "lastUpdateTime": now_rfc3339(now - ago)} for t, ago in conds]}}
+        if cert:
+            c["status"]["certificate"] = base64.b64encode(cert.encode()).decode()
+        return c
+    ca, ca_key = crypto.self_signed_ca("kubernetes")
+    good = crypto.issue_cert(key_pem=crypto.generate_key(), cn="system:node:a", ca_cert=ca, ca_key=ca_key, days=30)
+    assert C.should_clean(csr(60)) is None
+    assert C.should_clean(csr(25 * 3600)) == "pending"
+    assert C.should_clean(csr(7200, [("Denied", 1800)])) is None
+    assert C.should_clean(csr(7200, [("Denied", 5400)])) == "denied"
+    assert C.should_clean(csr(7200, [("Approved", 5400)])) is None           # approved, not issued
+    assert C.should_clean(csr(7200, [("Approved", 1800)], good)) is None
+    assert C.should_clean(csr(7200, [("Approved", 5400)], good)) == "approved"
+    assert C.should_clean(csr(7200, [("Approved", 1800)], good), now=now + 40 * 86400) == "approved"
+
+
+def test_controller_manager_accepts_reference_controller_names():
+    from kubernetes_amd.controllers.manager import CONTROLLERS, resolve
+    assert {"csrcleaner", "pv-protection"} <= set(CONTROLLERS)
+    assert "nodelifecycle" in resolve(["node"]) and "clusterroleaggregation" in resolve(["clusterrole-aggregation"])
+    assert "nodelifecycle" not in resolve(["*", "-node"])
