@@ -283,7 +283,10 @@ CONTROLLER_ROLES = {
         rule(["get", "create"], [CORE], ["persistentvolumeclaims"]), events_rule()],
     "ttl-controller": [rule(["update", "patch", "list", "watch"], [CORE], ["nodes"]), events_rule()],
     "certificate-controller": [
-        rule(READ, [CERTS], ["certificatesigningrequests"]),
+        # + delete: the CSR cleaner runs as this account too (the 1.9 role lacks it, so the
+        # reference's cleaner is refused under --use-service-account-credentials; later
+        # releases add it)
+        rule(READ + ["delete"], [CERTS], ["certificatesigningrequests"]),
         rule(["update"], [CERTS], ["certificatesigningrequests/status", "certificatesigningrequests/approval"]),
         rule(["create"], [AUTHZ], ["subjectaccessreviews"]), events_rule()],
     "pvc-protection-controller": [rule(["get", "list", "watch", "update"], [CORE], ["persistentvolumeclaims"]),

@@ -676,10 +676,20 @@ class PVCProtectionController(Controller):
         if pvc["metadata"].get("deletionTimestamp"):
             if PVC_PROTECTION in fins and not self._in_use(ns, name):
                 fins.remove(PVC_PROTECTION)
-                await self.client.patch("persistentvolumeclaims", name, {"metadata": {"finalizers": fins}}, ns)
+                await self._write(pvc, fins)
             return
         if PVC_PROTECTION not in fins:
-            await self.client.patch("persistentvolumeclaims", name, {"metadata": {"finalizers": fins + [PVC_PROTECTION]}}, ns)
+            await self._write(pvc, fins + [PVC_PROTECTION])
+
+    async def _write(self, pvc, fins):
+        """An update of the cached object (the controller's role may update claims, not patch
+        them); a conflict re-queues the key."""
+        upd = dict(pvc, metadata=dict(pvc["metadata"], finalizers=fins))
+        try:
+            await self.client.update("persistentvolumeclaims", upd, pvc["metadata"].get("namespace"))
+        except APIStatusError as e:
+            if not is_not_found(e):
+                raise
 
 
 class PVProtectionController(Controller):
