@@ -25,7 +25,10 @@ class ServiceAccountController(Controller):
     def setup(self):
         self.ns_inf = self.factory.get("namespaces")
         self.sa_inf = self.factory.get("serviceaccounts")
-        self.ns_inf.add_handler(lambda n: self.enqueue(n["metadata"]["name"]), None, None)
+        # `serviceaccounts_controller.go`: namespace adds and updates (a namespace that stopped
+        # terminating), account deletions re-create the default account
+        self.ns_inf.add_handler(lambda n: self.enqueue(n["metadata"]["name"]),
+                                lambda o, n: self.enqueue(n["metadata"]["name"]), None)
         self.sa_inf.add_handler(None, None, lambda sa: self.enqueue(sa["metadata"]["namespace"]))
 
     async def sync(self, key):
