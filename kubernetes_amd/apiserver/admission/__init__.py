@@ -67,6 +67,15 @@ class Chain:
         self._mut = [p for p in plugins if type(p).admit is not Plugin.admit]
         self._val = [p for p in plugins if type(p).validate is not Plugin.validate]
         self._charge = [p for p in plugins if hasattr(p, "charge")]
+        self._prepare = [p for p in plugins if hasattr(p, "prepare")]
+        self.names = {getattr(p, "name", "") for p in plugins}
+
+    async def prepare(self, a: Attributes):
+        """Mutating plugins that need an API round trip before the rest of the chain
+        (NamespaceAutoProvision creates the namespace)."""
+        for p in self._prepare:
+            if p.handles(a.operation):
+                await p.prepare(a)
 
     def admit(self, a: Attributes):
         for p in self._mut:
@@ -88,7 +97,8 @@ class Chain:
 
 DEFAULT_PLUGINS = [
     "NamespaceLifecycle", "LimitRanger", "ServiceAccount", "DefaultTolerationSeconds",
-    "Priority", "ResourceV2", "ExtendedResourceToleration", "DefaultStorageClass", "NodeRestriction", "ResourceQuota",
+    "Priority", "ResourceV2", "ExtendedResourceToleration", "DefaultStorageClass", "NodeRestriction",
+    "MutatingAdmissionWebhook", "ValidatingAdmissionWebhook", "ResourceQuota",
 ]
 
 

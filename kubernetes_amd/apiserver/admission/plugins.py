@@ -85,6 +85,57 @@ class NamespaceLifecycle(Plugin):
             raise AdmissionError(f"unable to create new content in namespace {a.namespace} because it is being terminated")
 
 
+@register
+class NamespaceExists(Plugin):
+    """`plugin/pkg/admission/namespace/exists`: create, update and delete of namespaced objects
+    are refused (404) unless the namespace exists."""
+    name = "NamespaceExists"
+    operations = (CREATE, UPDATE, DELETE)
+
+    def validate(self, a: Attributes):
+        if not a.namespace or a.resource == "namespaces" or not self.server:
+            return
+        if self.server.get_object("namespaces", None, a.namespace) is None:
+            raise AdmissionError(f"namespaces \"{a.namespace}\" not found", 404, "NotFound")
+
+
+@register
+class NamespaceAutoProvision(Plugin):
+    """`plugin/pkg/admission/namespace/autoprovision`: creating an object in a namespace that
+    does not exist creates the namespace first (AlreadyExists from a racing request is fine;
+    any other failure is 403)."""
+    name = "NamespaceAutoProvision"
+    operations = (CREATE,)
+
+    async def prepare(self, a: Attributes):
+        if not a.namespace or a.resource == "namespaces" or not self.server:
+            return
+        if self.server.get_object("namespaces", None, a.namespace) is not None:
+            return
+        from ...api import meta as _m
+        try:
+            await self.server.create(_m.BY_PLURAL["namespaces"], None,
+                                     {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": a.namespace}},
+                                     user=a.user)
+        except Exception as e:       # noqa: BLE001 - APIError from the server
+            if getattr(e, "code", None) != 409:
+                raise AdmissionError(f"{a.resource} \"{a.name}\" is forbidden: {e}", 403, "Forbidden")
+
+
+@register
+class MutatingAdmissionWebhook(Plugin):
+    """`staging/src/k8s.io/apiserver/pkg/admission/plugin/webhook/mutating`: enables calling
+    the MutatingWebhookConfiguration hooks (dispatched by `extensions.WebhookDispatcher`)."""
+    name = "MutatingAdmissionWebhook"
+
+
+@register
+class ValidatingAdmissionWebhook(Plugin):
+    """`.../admission/plugin/webhook/validating`: enables the ValidatingWebhookConfiguration
+    hooks."""
+    name = "ValidatingAdmissionWebhook"
+
+
 SA_MOUNT_PATH = "/var/run/secrets/kubernetes.io/serviceaccount"
 
 

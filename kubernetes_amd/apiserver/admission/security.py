@@ -328,6 +328,20 @@ class DenyEscalatingExec(Plugin):
 
 
 @register
+class DenyExecOnPrivileged(DenyEscalatingExec):
+    """`plugin/pkg/admission/exec` NewDenyExecOnPrivileged (deprecated): only privileged
+    containers are protected, host-namespace pods are not."""
+    name = "DenyExecOnPrivileged"
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource not in ("exec", "attach"):
+            return
+        pod = a.old if a.old is not None else (self.server.get_object("pods", a.namespace, a.name) if self.server else None)
+        if pod is not None and any(_sc(c).get("privileged") for c in _containers(pod.get("spec") or {})):
+            raise AdmissionError("cannot exec into or attach to a privileged container")
+
+
+@register
 class SecurityContextDeny(Plugin):
     name = "SecurityContextDeny"
     operations = (CREATE, UPDATE)

@@ -348,6 +348,9 @@ class APIServer:
         names = adm.DEFAULT_PLUGINS if admission_plugins is None else admission_plugins
         self.admission = adm.new_chain(names, self, admission_config)
         self.initializers_enabled = "Initializers" in names
+        # admission webhooks are called only when their plugins are on the admission list
+        self.mutating_webhooks_enabled = "MutatingAdmissionWebhook" in names
+        self.validating_webhooks_enabled = "ValidatingAdmissionWebhook" in names
         self.authn = None
         if token_file or tokens or client_ca_file or service_account_key_files or enable_bootstrap_token_auth \
                 or authentication_token_webhook or not anonymous_auth or oidc or basic_auth_file or requestheader \
@@ -904,6 +907,11 @@ class APIServer:
         ns = m.namespace_of(obj) if ri.namespaced else None
         if admit:
             a = adm.Attributes(adm.CREATE, ri.plural, subresource, ns, m.name_of(obj), obj, None, user, ri.kind)
+            if self.admission._prepare:
+                try:
+                    await self.admission.prepare(a)
+                except adm.AdmissionError as e:
+                    raise APIError(e.code, e.reason, str(e))
             self._admit(a)
             obj = await self._mutating_webhooks(a, ri)
         if ri.plural == "services":
@@ -926,12 +934,12 @@ class APIServer:
     _NO_WEBHOOKS = ("mutatingwebhookconfigurations", "validatingwebhookconfigurations")
 
     async def _mutating_webhooks(self, a, ri):
-        if ri.plural not in self._NO_WEBHOOKS and self.webhooks.has_any():
+        if self.mutating_webhooks_enabled and ri.plural not in self._NO_WEBHOOKS and self.webhooks.has_any():
             await self.webhooks.run(a, ri, True)
         return a.obj
 
     async def _validating_webhooks(self, a, ri):
-        if ri.plural not in self._NO_WEBHOOKS and self.webhooks.has_any():
+        if self.validating_webhooks_enabled and ri.plural not in self._NO_WEBHOOKS and self.webhooks.has_any():
             await self.webhooks.run(a, ri, False)
 
     def _validate_new(self, ri, strat, obj, old=None):
