@@ -935,16 +935,42 @@ class Kubectl(extra.ExtraCommands):
                 self.p(f"node/{node} drained (dry run)")
                 continue
             await self._cordon(node, True)
-            for p in victims:
-                if end is not None and time.monotonic() > end:
-                    raise SystemExit(f"error: drain did not complete within {a.timeout}s")
-                try:
-                    await self.client.evict(p["metadata"]["namespace"], p["metadata"]["name"], a.grace_period)
-                    self.p(f"pod/{p['metadata']['name']} evicted")
-                except APIStatusError as e:
-                    if not is_not_found(e):
-                        raise
+            left = None if end is None else max(0.0, end - time.monotonic())
+            try:
+                await asyncio.wait_for(asyncio.gather(*(self._evict_and_wait(p) for p in victims)), left)
+            except asyncio.TimeoutError:
+                raise SystemExit(f"error: Drain did not complete within {a.timeout}s")
             self.p(f"node/{node} drained")
+
+    DRAIN_RETRY = 5.0           # drain.go evictPods: sleep after 429 TooManyRequests
+    DRAIN_POLL = 1.0            # kubectl.Interval for waitForDelete
+
+    async def _evict_and_wait(self, p):
+        """`evictPods` / `waitForDelete`: evict, retrying while a disruption budget refuses (429);
+        then wait until the pod is gone or replaced by a new pod of the same name (UID)."""
+        ns, name, uid = p["metadata"]["namespace"], p["metadata"]["name"], p["metadata"].get("uid")
+        while True:
+            try:
+                await self.client.evict(ns, name, self.a.grace_period)
+                break
+            except APIStatusError as e:
+                if is_not_found(e):
+                    self.p(f"pod/{name} evicted")
+                    return
+                if e.code != 429:
+                    raise SystemExit(f"error: error when evicting pod {name!r}: {e}")
+                await asyncio.sleep(self.DRAIN_RETRY)
+        while True:
+            try:
+                cur = await self.client.get("pods", name, ns)
+            except APIStatusError as e:
+                if not is_not_found(e):
+                    raise SystemExit(f"error: error when waiting for pod {name!r} terminating: {e}")
+                break
+            if cur["metadata"].get("uid") != uid:
+                break
+            await asyncio.sleep(self.DRAIN_POLL)
+        self.p(f"pod/{name} evicted")
 
     async def cmd_taint(self):
         """`kubectl taint` (pkg/kubectl/cmd/taint.go): KEY=VAL:EFFECT adds (an existing key+effect

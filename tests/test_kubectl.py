@@ -292,3 +292,27 @@ def test_describe_node_shows_partitions_and_burn_in():
             "status": {"extendedResources": {core.AMD_GPU: {"resources": {"g9": {"health": "Healthy", "attributes": attrs}}}}}}
     out = describe(node)
     assert "partition=CPX/1@socket1" in out and "burn-in=passed (bf16 1188 / fp8 2242 TF/s, HBM 6199 GB/s)" in out
+
+
+def test_drain_retries_while_a_budget_refuses(cluster, tmp_path, monkeypatch):
+    """drain.go evictPods: 429 from the eviction API is retried until the budget allows it (or
+    --timeout), then the pod's deletion is awaited."""
+    from kubernetes_amd.kubectl.cli import Kubectl
+    monkeypatch.setattr(Kubectl, "DRAIN_RETRY", 0.2)
+    monkeypatch.setattr(Kubectl, "DRAIN_POLL", 0.1)
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "guarded", "labels": {"app": "guarded"}},
+           "spec": {"nodeName": "node-0", "containers": [{"name": "c", "image": "x"}]}}
+    pdb = {"apiVersion": "policy/v1beta1", "kind": "PodDisruptionBudget", "metadata": {"name": "guard"},
+           "spec": {"minAvailable": 1, "selector": {"matchLabels": {"app": "guarded"}}}}
+    for name, obj in (("pod.json", pod), ("pdb.json", pdb)):
+        (tmp_path / name).write_text(json.dumps(obj))
+        assert k(cluster, "create", "-f", str(tmp_path / name))[0] == 0
+    wait(lambda: "Running" in k(cluster, "get", "pods", "guarded")[1])
+    wait(lambda: json.loads(k(cluster, "get", "pdb", "guard", "-o", "json")[1]).get("status", {}).get("currentHealthy") == 1)
+    with pytest.raises(SystemExit, match="Drain did not complete"):
+        k(cluster, "drain", "node-0", "--force", "--ignore-daemonsets", "--timeout", "1")
+    assert "guarded" in k(cluster, "get", "pods", "guarded")[1]
+    assert k(cluster, "delete", "pdb", "guard")[0] == 0          # a budget's spec is immutable in 1.9
+    rc, out = k(cluster, "drain", "node-0", "--force", "--ignore-daemonsets", "--timeout", "20")
+    assert rc == 0 and "pod/guarded evicted" in out and "node/node-0 drained" in out
+    assert k(cluster, "uncordon", "node-0")[0] == 0
