@@ -24,31 +24,48 @@ from ..client.rest import APIStatusError, is_not_found
 from .base import Controller, split_key
 
 
+CLUSTER_SUBNET_MAX_DIFF = 16      # `cidrset.clusterSubnetMaxDiff` (IPv6 only)
+
+
 class CIDRSet:
+    """`pkg/controller/node/ipam/cidrset/cidr_set.go`: the cluster CIDR cut into /mask node
+    blocks, allocated round-robin from the last allocation; Occupy / Release take any CIDR and
+    mark every block it overlaps (`getBeginingAndEndIndices`), refusing one outside the
+    cluster range."""
+
     def __init__(self, cluster_cidr, mask):
         self.net = ipaddress.ip_network(cluster_cidr, strict=False)
         if mask < self.net.prefixlen:
             raise ValueError(f"node CIDR mask /{mask} is larger than the cluster CIDR {cluster_cidr}")
+        if self.net.version == 6 and mask - self.net.prefixlen > CLUSTER_SUBNET_MAX_DIFF:
+            raise ValueError("New CIDR set failed; the node CIDR size is too big")
         self.mask = mask
         self.max = 1 << (mask - self.net.prefixlen)
         self.used: set[int] = set()
         self.next = 0
+        self._net_cls = ipaddress.IPv4Network if self.net.version == 4 else ipaddress.IPv6Network
 
-    def _index(self, cidr):
-        sub = ipaddress.ip_network(cidr, strict=False)
-        if sub.prefixlen != self.mask or not sub.subnet_of(self.net):
+    def _indices(self, cidr):
+        """(first, last) block indices `cidr` overlaps, or None when it is outside the cluster
+        range (neither contains the other's base address)."""
+        other = ipaddress.ip_network(cidr, strict=False)
+        if other.version != self.net.version or not (other.network_address in self.net or
+                                                     self.net.network_address in other):
             return None
-        return (int(sub.network_address) - int(self.net.network_address)) >> (sub.max_prefixlen - self.mask)
+        lo = max(int(self.net.network_address), int(other.network_address))
+        hi = min(int(self.net.broadcast_address), int(other.broadcast_address))
+        shift = self.net.max_prefixlen - self.mask
+        return (lo - int(self.net.network_address)) >> shift, (hi - int(self.net.network_address)) >> shift
 
     def _cidr(self, i):
         base = int(self.net.network_address) + (i << (self.net.max_prefixlen - self.mask))
-        return str(ipaddress.ip_network((base, self.mask)))
+        return str(self._net_cls((base, self.mask)))
 
     def occupy(self, cidr):
-        i = self._index(cidr)
-        if i is None:
+        r = self._indices(cidr)
+        if r is None:
             return False
-        self.used.add(i)
+        self.used.update(range(r[0], r[1] + 1))
         return True
 
     def exclude(self, cidr):
@@ -57,18 +74,14 @@ class CIDRSet:
         other = ipaddress.ip_network(cidr, strict=False)
         if other.version != self.net.version or not self.net.overlaps(other):
             return 0
-        lo = max(int(self.net.network_address), int(other.network_address))
-        hi = min(int(self.net.broadcast_address), int(other.broadcast_address))
-        shift = self.net.max_prefixlen - self.mask
-        first = (lo - int(self.net.network_address)) >> shift
-        last = (hi - int(self.net.network_address)) >> shift
+        first, last = self._indices(cidr)
         self.used.update(range(first, last + 1))
         return last - first + 1
 
     def release(self, cidr):
-        i = self._index(cidr)
-        if i is not None:
-            self.used.discard(i)
+        r = self._indices(cidr)
+        if r is not None:
+            self.used.difference_update(range(r[0], r[1] + 1))
 
     def allocate(self):
         for k in range(self.max):
@@ -115,7 +128,12 @@ class NodeIPAMController(Controller):
         node = self.node_inf.get(key)
         if node is None or (node.get("spec") or {}).get("podCIDR"):
             return
-        cidr = self.owner.get(key) or self.cidrs.allocate()
+        try:
+            cidr = self.owner.get(key) or self.cidrs.allocate()
+        except RuntimeError:
+            # `AllocateOrOccupyCIDR`: recordNodeStatusChange(CIDRNotAvailable), then retried
+            self.recorder.event(node, "Normal", "CIDRNotAvailable", f"Node {key} status is now: CIDRNotAvailable")
+            raise
         self.owner[key] = cidr
         try:
             await self.client.patch("nodes", key, {"spec": {"podCIDR": cidr}})
