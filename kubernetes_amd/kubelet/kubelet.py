@@ -189,10 +189,10 @@ class Kubelet:
         self.eviction_interval = eviction_interval
         self.allocatable_ignore_eviction = allocatable_ignore_eviction
         if eviction_hard or eviction_soft:
-            from .eviction import EvictionManager, parse_soft_thresholds, parse_thresholds
-            th = parse_thresholds(eviction_hard or "", eviction_minimum_reclaim or "")
-            if eviction_soft:
-                th += parse_soft_thresholds(eviction_soft, eviction_soft_grace_period or "", eviction_minimum_reclaim or "")
+            from .eviction import EvictionManager, parse_threshold_config
+            th = parse_threshold_config(("pods",) if enforce_node_allocatable else (), eviction_hard or "",
+                                        eviction_soft or "", eviction_soft_grace_period or "",
+                                        eviction_minimum_reclaim or "")
             self.eviction = EvictionManager(th, eviction_signals, pressure_transition_period=eviction_pressure_transition_period,
                                             max_pod_grace=eviction_max_pod_grace_period)
         self.cpu_manager = None
@@ -357,12 +357,45 @@ class Kubelet:
             except Exception as e:
                 log.warning("image garbage collection failed: %s", e)
 
+    def _wire_eviction_reclaim(self):
+        """`buildResourceToNodeReclaimFuncs` (no dedicated image fs): the disk resources are
+        reclaimed by deleting terminated containers, then unused images (bytes freed counted for
+        the space signals only); node events go to the node."""
+        ev = self.eviction
+        if getattr(ev, "_kubelet_stats", False) is False and ev.usage_fn is None:
+            from .stats import pod_eviction_stats
+            ev.stats_fn = lambda pod: pod_eviction_stats(self, pod)
+            ev._kubelet_stats = True
+        if ev.recorder is None:
+            node_ref = {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}}
+            ev.recorder = lambda obj, typ, reason, msg: self.recorder.event(obj or node_ref, typ, reason, msg)
+        if ev.reclaim_fns:
+            return
+        fns_space, fns_inodes = [], []
+
+        async def containers():
+            # `DeleteAllUnusedContainers`: every dead container, whatever the GC policy keeps
+            await self.garbage_collect_containers(policy={"min_age": 0.0, "max_per_pod_container": 0,
+                                                          "max_containers": 0})
+            return 0
+        fns_space.append(containers)
+        fns_inodes.append(containers)
+        if getattr(self, "image_gc", None) is not None:
+            async def images(report=True):
+                freed = await self.image_gc.free_space(1 << 62)        # `DeleteUnusedImages`
+                return freed if report else 0
+            fns_space.append(images)
+            fns_inodes.append(lambda: images(False))
+        ev.reclaim_fns = {"nodefs": fns_space, "imagefs": fns_space, "nodefsInodes": fns_inodes,
+                          "imagefsInodes": fns_inodes}
+
     async def _eviction_loop(self):
         """eviction_manager.go synchronize(): observe, set pressure conditions, evict <= 1 pod."""
         last_conds = set()
         while not self._stopped:
             running = [s.pod for s in self.pods.values() if s.admitted and not s.terminated and not s.rejected]
-            victim, msg, grace = self.eviction.select_victim_with_grace(running)
+            self._wire_eviction_reclaim()
+            victim, msg, grace, event_msg = await self.eviction.synchronize(running)
             conds = set(self.eviction.conditions)
             if conds != last_conds:
                 last_conds = conds
@@ -370,7 +403,7 @@ class Kubelet:
             if victim is not None:
                 st = self.pods.get(victim["metadata"]["uid"])
                 if st is not None:
-                    self.recorder.event(victim, "Warning", "Evicted", msg)
+                    self.recorder.event(victim, "Warning", "Evicted", event_msg or msg)
                     await self._kill_pod(st, grace)
                     await self._write_status(st, {"phase": core.POD_FAILED, "reason": "Evicted", "message": msg,
                                                   "conditions": (victim.get("status") or {}).get("conditions") or []})
@@ -1267,12 +1300,12 @@ class Kubelet:
         st.waiting.pop(c["name"], None)
         return False
 
-    async def garbage_collect_containers(self, now=None):
+    async def garbage_collect_containers(self, now=None, policy=None):
         """`pkg/kubelet/container_gc.go` + `kuberuntime_gc.go`: dead containers older than
         `min_age` are evictable; keep at most `max_per_pod_container` per (pod, container) and
         `max_containers` overall (oldest first); containers of pods the kubelet no longer
         tracks are always removed. Returns the removed container ids."""
-        pol = self.container_gc or {}
+        pol = policy if policy is not None else (self.container_gc or {})
         now = now or time.time()
         min_age = float(pol.get("min_age", 0.0))
         per = int(pol.get("max_per_pod_container", 1))

@@ -306,3 +306,68 @@ def machine_info(kubelet):
             "system_uuid": _read("/sys/class/dmi/id/product_uuid") or kubelet.node_name,
             "boot_id": _read("/proc/sys/kernel/random/boot_id"),
             "topology": topo, "accelerators": accels, "cloud_provider": "None", "instance_type": "Unknown"}
+
+
+def _du(path):
+    """(bytes, inodes) under `path` (no symlink following)."""
+    import os
+    total = files = 0
+    for root, dirs, names in os.walk(path, followlinks=False):
+        for n in names + dirs:
+            try:
+                st = os.lstat(os.path.join(root, n))
+            except OSError:
+                continue
+            total += st.st_blocks * 512 if st.st_blocks else st.st_size
+            files += 1
+    return total, files
+
+
+def pod_eviction_stats(kubelet, pod):
+    """Per-pod usage for the eviction manager's ranking (`makeSignalObservations` statsFunc):
+    memory = the containers' working set; disk / inodes = local emptyDir volumes plus container
+    logs (no dedicated image fs); volumes = emptyDir usage by name. None when the pod is not
+    tracked (ranked first, like the reference's missing stats)."""
+    import os
+    st = kubelet.pods.get(pod["metadata"].get("uid"))
+    if st is None:
+        return None
+    ann = pod["metadata"].get("annotations") or {}
+    mem = 0
+    if SIM_MEM in ann:
+        mem = int(float(ann.get(SIM_MEM, 0)))
+    else:
+        meta = getattr(kubelet.runtime, "meta", {}) or {}
+        for cid in st.containers.values():
+            proc = (meta.get(cid) or {}).get("proc") if cid else None
+            if proc is not None and getattr(proc, "returncode", 1) is None:
+                u = _proc_usage(proc.pid)
+                if u is not None:
+                    mem += u[1]
+    disk = inodes = 0
+    vols, per_container = {}, {}
+    base = os.path.join(kubelet.volumes.pod_dir(pod), "volumes")
+    for v in (pod.get("spec") or {}).get("volumes") or ():
+        if "emptyDir" in v and (v.get("emptyDir") or {}).get("medium") != "Memory":
+            b, n = _du(os.path.join(base, v["name"]))
+            vols[v["name"]] = b
+            disk += b
+            inodes += n
+    logs = getattr(kubelet, "container_log_dir", None)
+    if logs and os.path.isdir(logs):
+        md = pod["metadata"]
+        prefix = f"{md['name']}_{md.get('namespace', 'default')}_"
+        try:
+            for name in os.listdir(logs):
+                if name.startswith(prefix):
+                    try:
+                        size = os.stat(os.path.join(logs, name)).st_size
+                    except OSError:
+                        continue
+                    disk += size
+                    inodes += 1
+                    cname = name[len(prefix):].rsplit("-", 1)[0]
+                    per_container[cname] = per_container.get(cname, 0) + size
+        except OSError:
+            pass
+    return {"memory": mem, "disk": disk, "inodes": inodes, "volumes": vols, "containers": per_container}

@@ -27,6 +27,12 @@ DEFAULTS = {
     "CPUManager": FeatureSpec(True, BETA),
     "HugePages": FeatureSpec(True, BETA),
     "Accelerators": FeatureSpec(False, ALPHA),             # legacy in-kubelet NVIDIA path: not provided
+    # critical pods (kube-system + critical-pod annotation) are admitted under node pressure, are
+    # never evicted when static, and may preempt on admission. On by default here (the
+    # reference's alpha default is off): the AMD device-plugin DaemonSet is a critical pod, and a
+    # node must not evict the agent that advertises its GPUs.
+    "ExperimentalCriticalPodAnnotation": FeatureSpec(True, ALPHA),
+    "LocalStorageCapacityIsolation": FeatureSpec(False, ALPHA),   # emptyDir sizeLimit / ephemeral-storage limits
 }
 
 

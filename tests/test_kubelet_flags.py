@@ -82,7 +82,7 @@ def test_soft_eviction_grace_and_minimum_reclaim():
     assert v is None and em.has("MemoryPressure")          # condition at once, eviction after the grace period
     now[0] = 91.0
     v, msg, grace = em.select_victim_with_grace([pod])
-    assert v is pod and grace == 20 and "memory.available<1073741824" in msg       # soft: pod grace capped by max-pod-grace-period
+    assert v is pod and grace == 20 and msg == "The node was low on resource: memory."   # soft: --eviction-max-pod-grace-period
     avail[0] = 50 << 20                                      # under the hard threshold: immediate, grace 0
     v, msg, grace = em.select_victim_with_grace([pod])
     assert v is pod and grace == 0
