@@ -203,7 +203,8 @@ class Kubelet:
         self.root_dir = root_dir or os.path.join(tempfile.gettempdir(), f"kamd-kubelet-{node_name}")
         self.volumes = VolumeManager(client, os.path.join(self.root_dir, "pods"), os.path.join(self.root_dir, "plugins"),
                                      node_name, flex_plugins_dir=volume_plugin_dir)
-        self.probes = ProbeManager(runtime, self._on_readiness, self._on_liveness_failure)
+        self.probes = ProbeManager(runtime, self._on_readiness, self._on_liveness_failure,
+                                   on_probe_failure=self._on_probe_failure)
         self.node_name = node_name
         self.runtime = runtime
         self.dm = device_manager or ManagerStub()
@@ -1262,11 +1263,16 @@ class Kubelet:
         if st is not None:
             self._resync(uid)
 
+    def _on_probe_failure(self, uid, cname, kind, msg):
+        st = self.pods.get(uid)
+        if st is not None:
+            self.recorder.event(st.pod, "Warning", "Unhealthy", f"{kind.capitalize()} probe failed: {msg}",
+                                field_path=f"spec.containers{{{cname}}}")
+
     def _on_liveness_failure(self, uid, cname, cid, msg):
         st = self.pods.get(uid)
         if st is None or st.containers.get(cname) != cid:
             return
-        self.recorder.event(st.pod, "Warning", "Unhealthy", f"Liveness probe failed: {msg}")
         self.recorder.event(st.pod, "Normal", "Killing", f"Killing container {cname}: failed liveness probe")
 
         async def kill():

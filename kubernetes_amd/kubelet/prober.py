@@ -80,6 +80,7 @@ class _Worker:
             else:
                 self.fail_run += 1
                 self.ok_run = 0
+                self.mgr.failed(self, msg)
             new = self.result
             if ok and self.ok_run >= succ_th:
                 new = True
@@ -97,8 +98,10 @@ class _Worker:
 
 
 class ProbeManager:
-    def __init__(self, runtime, on_readiness, on_liveness_failure, pod_ip=lambda uid: "127.0.0.1"):
+    def __init__(self, runtime, on_readiness, on_liveness_failure, pod_ip=lambda uid: "127.0.0.1",
+                 on_probe_failure=None):
         self.runtime = runtime
+        self.on_probe_failure = on_probe_failure
         self.on_readiness = on_readiness
         self.on_liveness_failure = on_liveness_failure
         self.pod_ip = pod_ip
@@ -118,6 +121,12 @@ class ProbeManager:
         """None when the container has no readiness probe."""
         w = self.workers.get((uid, cname, "readiness"))
         return None if w is None else w.result
+
+    def failed(self, w, msg):
+        """`prober.probe`: every failed probe is a Warning `Unhealthy` event on the container
+        ("Liveness probe failed: <output>")."""
+        if self.on_probe_failure is not None:
+            self.on_probe_failure(w.uid, w.container["name"], w.kind, msg)
 
     def changed(self, w, msg):
         if w.kind == "readiness":

@@ -102,4 +102,8 @@ def test_readiness_and_liveness_probes(run):
             p = await cond(lambda p: p["status"]["containerStatuses"][0]["restartCount"] >= 1)
             rt.exec_codes[(uid, "c")] = 0
             await cond(lambda p: ready(p) and p["status"]["containerStatuses"][0]["state"].get("running"))
+            # prober.go: every failed probe is an Unhealthy event naming the probe type
+            emitted = cl.nodes[0].kubelet.recorder.emitted
+            assert any(r == "Unhealthy" and m.startswith("Readiness probe failed") for _t, r, m in emitted)
+            assert any(r == "Unhealthy" and m.startswith("Liveness probe failed") for _t, r, m in emitted)
     run(main(), timeout=60)
