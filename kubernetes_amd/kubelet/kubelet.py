@@ -254,6 +254,8 @@ class Kubelet:
             image_service = LocalImageService(ImageStore(stub_image_resolver if runtime.name == "stub" else host_image_resolver))
         from .images import ImageGCManager, ImageManager
         self.image_service = image_service
+        self._node_images: list = []
+        self._cond_transitions: dict = {}      # condition type -> (status, lastTransitionTime)
         self.images = ImageManager(image_service, self.recorder, backoff_initial=image_backoff,
                                    secret_getter=lambda ns, name: self.client.get("secrets", name, ns),
                                    serialize=serialize_image_pulls, qps=registry_qps, burst=registry_burst)
@@ -469,28 +471,30 @@ class Kubelet:
         mem_p = self.eviction is not None and self.eviction.has("MemoryPressure")
         disk_p = self.eviction is not None and self.eviction.has("DiskPressure")
         net_err = self.network.status()
-        ready = ({"type": "Ready", "status": "True", "reason": "KubeletReady", "message": "kubelet is posting ready status",
-                  "lastHeartbeatTime": now, "lastTransitionTime": now} if not net_err else
-                 {"type": "Ready", "status": "False", "reason": "KubeletNotReady",
-                  "message": f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady message:{net_err}",
-                  "lastHeartbeatTime": now, "lastTransitionTime": now})
+        cond = self._condition
+        ready = (cond("Ready", "True", "KubeletReady", "kubelet is posting ready status", now) if not net_err else
+                 cond("Ready", "False", "KubeletNotReady",
+                      f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady message:{net_err}", now))
         alloc = self._allocatable(capacity)
         self.volumes.allocatable = alloc        # downward API: a missing limit reads as allocatable
         self.volumes.host_ip = self.node_ip or self.address
         st = {"capacity": capacity, "allocatable": alloc,
               "conditions": [
-                  ready,
-                  {"type": "MemoryPressure", "status": "True" if mem_p else "False",
-                   "reason": "KubeletHasInsufficientMemory" if mem_p else "KubeletHasSufficientMemory",
-                   "lastHeartbeatTime": now, "lastTransitionTime": now},
-                  {"type": "DiskPressure", "status": "True" if disk_p else "False",
-                   "reason": "KubeletHasDiskPressure" if disk_p else "KubeletHasNoDiskPressure",
-                   "lastHeartbeatTime": now, "lastTransitionTime": now}],
+                  cond("OutOfDisk", "False", "KubeletHasSufficientDisk", "kubelet has sufficient disk space available", now),
+                  cond("MemoryPressure", "True", "KubeletHasInsufficientMemory", "kubelet has insufficient memory available", now)
+                  if mem_p else
+                  cond("MemoryPressure", "False", "KubeletHasSufficientMemory", "kubelet has sufficient memory available", now),
+                  cond("DiskPressure", "True", "KubeletHasDiskPressure", "kubelet has disk pressure", now) if disk_p else
+                  cond("DiskPressure", "False", "KubeletHasNoDiskPressure", "kubelet has no disk pressure", now),
+                  ready],
               "addresses": [{"type": "InternalIP", "address": self.node_ip or self.address},
                             {"type": "Hostname", "address": self.node_name}],
               "daemonEndpoints": {"kubeletEndpoint": {"Port": self.http_port or 0}},
-              "nodeInfo": {"kubeletVersion": "v1.9.0-amd.0", "containerRuntimeVersion": f"{self.runtime.name}://1.0",
-                           "operatingSystem": "linux", "architecture": "amd64", "machineID": self.node_name}}
+              "nodeInfo": dict(self._host_info(), kubeletVersion="v1.9.0-amd.0", kubeProxyVersion="v1.9.0-amd.0",
+                               containerRuntimeVersion=f"{self.runtime.name}://1.0", operatingSystem="linux",
+                               architecture="amd64")}
+        if self._node_images:
+            st["images"] = self._node_images
         if self.dynamic is not None:
             st["conditions"].append(dict(self.dynamic.condition, lastHeartbeatTime=now, lastTransitionTime=now))
         iso = getattr(self, "isolation", None)
@@ -506,6 +510,56 @@ class Kubelet:
         # detach them (`kubelet_node_status.go` setNodeVolumesInUseStatus)
         st["volumesInUse"] = self.volumes.volumes_in_use() or None
         return st
+
+    def _condition(self, ctype, status, reason, message, now):
+        """A node condition whose lastTransitionTime moves only when its status changes
+        (`kubelet_node_status.go` setNodeReadyCondition / setNodeMemoryPressureCondition / ...);
+        lastHeartbeatTime is every update."""
+        prev = self._cond_transitions.get(ctype)
+        transition = prev[1] if prev is not None and prev[0] == status else now
+        self._cond_transitions[ctype] = (status, transition)
+        return {"type": ctype, "status": status, "reason": reason, "message": message,
+                "lastHeartbeatTime": now, "lastTransitionTime": transition}
+
+    _HOST_INFO = None
+
+    @classmethod
+    def _host_info(cls):
+        """`setNodeStatusMachineInfo` / `setNodeStatusVersionInfo`: machine, boot and OS
+        identity of the host (read once)."""
+        if cls._HOST_INFO is None:
+            def read(path):
+                try:
+                    with open(path) as f:
+                        return f.read().strip()
+                except OSError:
+                    return ""
+            os_image = ""
+            for line in read("/etc/os-release").splitlines():
+                if line.startswith("PRETTY_NAME="):
+                    os_image = line.split("=", 1)[1].strip().strip('"')
+            cls._HOST_INFO = {"machineID": read("/etc/machine-id"), "systemUUID": read("/sys/class/dmi/id/product_uuid"),
+                              "bootID": read("/proc/sys/kernel/random/boot_id"), "kernelVersion": os.uname().release,
+                              "osImage": os_image}
+        return dict(cls._HOST_INFO)
+
+    async def _refresh_node_images(self):
+        """`setNodeStatusImages`: the node's images, largest first, at most 50
+        (`maxImagesInNodeStatus`), each with its tags and digests."""
+        lister = getattr(self.image_service, "list_images", None)
+        if lister is None:
+            return
+        try:
+            imgs = await lister()
+        except Exception as e:      # noqa: BLE001 - the reference logs and keeps the old list
+            log.debug("listing images for node status failed: %s", e)
+            return
+        out = []
+        for i in sorted(imgs or (), key=lambda i: -int(i.get("size", 0) or 0))[:50]:
+            names = list(i.get("repoTags") or ()) + list(i.get("repoDigests") or ())
+            if names:
+                out.append({"names": names, "sizeBytes": int(i.get("size", 0) or 0)})
+        self._node_images = out
 
     def _allocatable(self, capacity):
         """`pkg/kubelet/cm/node_container_manager.go` GetNodeAllocatableReservation:
@@ -625,6 +679,7 @@ class Kubelet:
 
     async def update_node_status(self):
         self._collect_plugin_labels()
+        await self._refresh_node_images()
         st = self._node_status()
         try:
             # strategic merge (conditions keyed by type), as the reference's PatchNodeStatus, so

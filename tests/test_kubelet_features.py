@@ -107,3 +107,30 @@ def test_readiness_and_liveness_probes(run):
             assert any(r == "Unhealthy" and m.startswith("Readiness probe failed") for _t, r, m in emitted)
             assert any(r == "Unhealthy" and m.startswith("Liveness probe failed") for _t, r, m in emitted)
     run(main(), timeout=60)
+
+
+def test_node_status_transitions_images_and_machine_info(run):
+    """`kubelet_node_status.go`: lastTransitionTime moves only when a condition's status changes
+    (the node controller's NotReady eviction timer depends on it), OutOfDisk is reported, images
+    are listed largest first, and the machine / boot identity is filled in."""
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=0) as cl:
+            c, k = cl.client, cl.nodes[0].kubelet
+            await c.create("pods", {"metadata": {"name": "img", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "c", "image": "busybox"}]}})
+            await cl.wait_pod("img")
+
+            async def status():
+                await k.update_node_status()
+                return (await c.get("nodes", k.node_name))["status"]
+            s1 = await status()
+            await asyncio.sleep(1.1)                       # RFC 3339 timestamps have 1 s resolution
+            s2 = await status()
+            by = lambda s: {x["type"]: x for x in s["conditions"]}  # noqa: E731
+            r1, r2 = by(s1)["Ready"], by(s2)["Ready"]
+            assert r1["lastTransitionTime"] == r2["lastTransitionTime"]
+            assert r2["lastHeartbeatTime"] > r1["lastHeartbeatTime"]
+            assert by(s2)["OutOfDisk"]["status"] == "False"
+            assert any(any("busybox" in n for n in i["names"]) for i in s2.get("images") or ())
+            assert s2["nodeInfo"]["bootID"] and s2["nodeInfo"]["kernelVersion"]
+    run(main(), timeout=60)
