@@ -43,9 +43,15 @@ class PodInfo:
         self.ephemeral = req["ephemeral-storage"].int_value() if "ephemeral-storage" in req else 0
         self.scalars = {k: v.int_value() for k, v in req.items()
                         if k not in ("cpu", "memory", "ephemeral-storage", "pods")}
-        self.nz_cpu = self.milli_cpu or DEFAULT_MILLI_CPU
-        self.nz_mem = self.memory or DEFAULT_MEMORY
         spec = pod.get("spec") or {}
+        # `priorities/util/non_zero.go` GetNonzeroRequests: per container, a request that is not
+        # set counts as 100m / 200Mi (an explicit zero stays zero); init containers do not count
+        nzc = nzm = 0
+        for c in spec.get("containers") or ():
+            r = (c.get("resources") or {}).get("requests") or {}
+            nzc += _q(r["cpu"]).milli_value() if "cpu" in r else DEFAULT_MILLI_CPU
+            nzm += _q(r["memory"]).int_value() if "memory" in r else DEFAULT_MEMORY
+        self.nz_cpu, self.nz_mem = nzc, nzm
         ports = []
         for c in spec.get("containers") or ():
             for p in c.get("ports") or ():

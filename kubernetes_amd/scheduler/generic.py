@@ -464,6 +464,8 @@ class GenericScheduler:
             col = [r[j] for r in raws]
             if norm == "minmax":
                 col = PR.normalize_minmax(col)
+            elif norm == "spread":
+                col = PR.normalize_spread(col, nodes)
             elif norm:
                 col = PR.normalize(col, reverse)
             for i, s in enumerate(col):

@@ -16,30 +16,36 @@ from ..api.labels import SelectorError, node_selector_requirements_as_selector
 MAX = 10.0
 
 
+def _unused(req, cap):
+    """`calculateUnusedScore`: integer ((capacity - requested) * 10) / capacity."""
+    if cap == 0 or req > cap:
+        return 0
+    return (cap - req) * 10 // cap
+
+
+def _used(req, cap):
+    """`calculateUsedScore`: integer (requested * 10) / capacity."""
+    if cap == 0 or req > cap:
+        return 0
+    return req * 10 // cap
+
+
 def least_requested(pod, pi, ni, ctx):
-    def f(req, cap):
-        if cap == 0 or req > cap:
-            return 0.0
-        return (cap - req) * MAX / cap
-    return (f(ni.nz_cpu + pi.nz_cpu, ni.alloc_cpu) + f(ni.nz_mem + pi.nz_mem, ni.alloc_mem)) / 2
+    return (_unused(ni.nz_cpu + pi.nz_cpu, ni.alloc_cpu) + _unused(ni.nz_mem + pi.nz_mem, ni.alloc_mem)) // 2
 
 
 def most_requested(pod, pi, ni, ctx):
-    def f(req, cap):
-        if cap == 0 or req > cap:
-            return 0.0
-        return req * MAX / cap
-    return (f(ni.nz_cpu + pi.nz_cpu, ni.alloc_cpu) + f(ni.nz_mem + pi.nz_mem, ni.alloc_mem)) / 2
+    return (_used(ni.nz_cpu + pi.nz_cpu, ni.alloc_cpu) + _used(ni.nz_mem + pi.nz_mem, ni.alloc_mem)) // 2
 
 
 def balanced_resource_allocation(pod, pi, ni, ctx):
-    if not ni.alloc_cpu or not ni.alloc_mem:
-        return 0.0
-    c = (ni.nz_cpu + pi.nz_cpu) / ni.alloc_cpu
-    m = (ni.nz_mem + pi.nz_mem) / ni.alloc_mem
+    """`calculateBalancedResourceAllocation`: int((1 - |cpuFraction - memFraction|) * 10); a
+    fraction of a zero capacity is 1, and any fraction >= 1 scores 0."""
+    c = (ni.nz_cpu + pi.nz_cpu) / ni.alloc_cpu if ni.alloc_cpu else 1.0
+    m = (ni.nz_mem + pi.nz_mem) / ni.alloc_mem if ni.alloc_mem else 1.0
     if c >= 1 or m >= 1:
-        return 0.0
-    return MAX - abs(c - m) * MAX
+        return 0
+    return int((1 - abs(c - m)) * MAX)
 
 
 def _service_match(p, ns, sels):
@@ -60,11 +66,14 @@ def selector_spread(pod, pi, ni, ctx):
     ns = ctx.namespace
     n = 0
     for p, _ in ni.pods.values():
-        if owner and any(ref.get("uid") == owner for ref in p["metadata"].get("ownerReferences") or ()):
+        md = p["metadata"]
+        if md.get("namespace", "default") != ns or md.get("deletionTimestamp"):
+            continue            # a deleted predecessor does not count for spreading
+        if owner and any(ref.get("uid") == owner for ref in md.get("ownerReferences") or ()):
             n += 1
         elif sels and _service_match(p, ns, sels):
             n += 1
-    return float(n)
+    return n
 
 
 def service_spreading(pod, pi, ni, ctx):
@@ -196,7 +205,7 @@ PRIORITIES = {
     "LeastRequestedPriority": (least_requested, False, False),
     "MostRequestedPriority": (most_requested, False, False),
     "BalancedResourceAllocation": (balanced_resource_allocation, False, False),
-    "SelectorSpreadPriority": (selector_spread, True, True),
+    "SelectorSpreadPriority": (selector_spread, True, "spread"),
     "NodeAffinityPriority": (node_affinity, False, True),
     "TaintTolerationPriority": (taint_toleration, True, True),
     "NodePreferAvoidPodsPriority": (node_prefer_avoid_pods, False, False),
@@ -205,7 +214,7 @@ PRIORITIES = {
     "ImageLocalityPriority": (image_locality, False, False),
     "ResourceLimitsPriority": (resource_limits, False, False),
     "InterPodAffinityPriority": (inter_pod_affinity, False, "minmax"),
-    "ServiceSpreadingPriority": (service_spreading, True, True),
+    "ServiceSpreadingPriority": (service_spreading, True, "spread"),
     "EqualPriority": (equal, False, False),
 }
 
@@ -230,16 +239,59 @@ def compile_node_affinity_prefs(pod):
 
 
 def normalize_minmax(scores):
+    """`CalculateInterPodAffinityPriority` reduce: int(10 * (v - min) / (max - min)), 0 when all
+    equal."""
     lo, hi = min(scores), max(scores)
     if hi == lo:
-        return [0.0 for _ in scores]
-    return [MAX * (v - lo) / (hi - lo) for v in scores]
+        return [0 for _ in scores]
+    return [int(MAX * (v - lo) / (hi - lo)) for v in scores]
 
 
 def normalize(scores, reverse):
+    """`NormalizeReduce(MaxPriority, reverse)`: integer 10 * score / max (reversed: 10 minus
+    that); with every score 0, reverse gives everyone 10."""
     mx = max(scores) if scores else 0
     if mx <= 0:
-        return [MAX if reverse else 0.0 for _ in scores]
-    if reverse:
-        return [MAX * (mx - s) / mx for s in scores]
-    return [MAX * s / mx for s in scores]
+        return [int(MAX) if reverse else 0 for _ in scores]
+    out = []
+    for s in scores:
+        v = int(MAX) * int(s) // int(mx) if float(s).is_integer() and float(mx).is_integer() else int(MAX * s / mx)
+        out.append(int(MAX) - v if reverse else v)
+    return out
+
+
+ZONE_WEIGHTING = 2.0 / 3.0      # selector_spreading.go zoneWeighting
+
+
+def zone_key(ni):
+    """`utilnode.GetZoneKey`: region + ":\x00:" + zone from the failure-domain labels; "" when
+    neither is set."""
+    region = ni.labels.get("failure-domain.beta.kubernetes.io/region", "")
+    zone = ni.labels.get("failure-domain.beta.kubernetes.io/zone", "")
+    if not region and not zone:
+        return ""
+    return region + ":\x00:" + zone
+
+
+def normalize_spread(counts, nodes):
+    """`CalculateSpreadPriorityReduce`: 10 * (maxByNode - count) / maxByNode, blended 1/3 : 2/3
+    with the same score over zones when the nodes carry zone labels; int() at the end."""
+    max_node = max(counts) if counts else 0
+    by_zone: dict = {}
+    zones = [zone_key(ni) for ni in nodes]
+    for z, c in zip(zones, counts):
+        if z:
+            by_zone[z] = by_zone.get(z, 0) + c
+    max_zone = max(by_zone.values()) if by_zone else 0
+    out = []
+    for z, c in zip(zones, counts):
+        f = MAX
+        if max_node > 0:
+            f = MAX * ((max_node - c) / max_node)
+        if by_zone and z:
+            zs = MAX
+            if max_zone > 0:
+                zs = MAX * ((max_zone - by_zone[z]) / max_zone)
+            f = f * (1.0 - ZONE_WEIGHTING) + ZONE_WEIGHTING * zs
+        out.append(int(f))
+    return out
