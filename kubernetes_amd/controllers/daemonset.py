@@ -108,6 +108,8 @@ def node_should_run(ds, node, node_pods=()):
             return False, False, False, None
         want = sched = False
     short = P.pod_fits_resources(pod, pi, ni, ctx)
+    if isinstance(short, tuple):
+        short = ", ".join(short)
     if sched and short:
         return want, False, cont, f"failed to place pod on {name!r}: {short}"
     return want, sched, cont, None

@@ -39,8 +39,9 @@ class FitError(Exception):
         self.num_nodes = num_nodes
         self.failed = failed
         counts = {}
-        for r in failed.values():
-            counts[r] = counts.get(r, 0) + 1
+        for rs in failed.values():
+            for r in (rs if isinstance(rs, tuple) else (rs,)):
+                counts[r] = counts.get(r, 0) + 1
         reasons = ", ".join(f"{n} {r}" for r, n in sorted(counts.items(), key=lambda kv: (-kv[1], kv[0])))
         super().__init__(f"0/{num_nodes} nodes are available: {reasons}.")
 

@@ -21,18 +21,24 @@ def check_node_condition(pod, pi, ni, ctx):
 
 
 def pod_fits_resources(pod, pi, ni, ctx):
+    """`PodFitsResources` (predicates.go:583-690): the pod count, then every resource the pod
+    requests that does not fit — all of them, as the reference's InsufficientResourceError
+    list (a tuple when more than one)."""
     if len(ni.pods) + 1 > ni.alloc_pods:
         return "Insufficient pods"
+    short = []
     if pi.milli_cpu and ni.req_cpu + pi.milli_cpu > ni.alloc_cpu:
-        return "Insufficient cpu"
+        short.append("Insufficient cpu")
     if pi.memory and ni.req_mem + pi.memory > ni.alloc_mem:
-        return "Insufficient memory"
+        short.append("Insufficient memory")
     if pi.ephemeral and ni.alloc_eph and ni.req_eph + pi.ephemeral > ni.alloc_eph:
-        return "Insufficient ephemeral-storage"
+        short.append("Insufficient ephemeral-storage")
     for k, v in pi.scalars.items():
         if ni.req_scalars.get(k, 0) + v > ni.alloc_scalars.get(k, 0):
-            return f"Insufficient {k}"
-    return None
+            short.append(f"Insufficient {k}")
+    if not short:
+        return None
+    return short[0] if len(short) == 1 else tuple(short)
 
 
 def pod_fits_host(pod, pi, ni, ctx):
