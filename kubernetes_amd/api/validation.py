@@ -455,18 +455,70 @@ def validate_pod(pod):
     return validate_object_meta(pod, True) + validate_pod_spec(pod.get("spec") or {})
 
 
+def _sem(o):
+    """Semantic equality view: empty values compare equal to absent ones."""
+    if isinstance(o, dict):
+        return {k: _sem(v) for k, v in o.items() if v not in (None, "", [], {})}
+    if isinstance(o, list):
+        return [_sem(v) for v in o]
+    return o
+
+
+POD_UPDATE_FORBIDDEN = ("pod updates may not change fields other than `spec.containers[*].image`, "
+                        "`spec.initContainers[*].image`, `spec.activeDeadlineSeconds` or `spec.tolerations` "
+                        "(only additions to existing tolerations)")
+
+
 def validate_pod_update(new, old):
-    """Pod spec is immutable except for image / activeDeadlineSeconds / tolerations
-    (validation.go `ValidatePodUpdate`). The scheduler-owned fields nodeName and
-    extendedResources[].assigned may only be set through pods/binding."""
+    """`ValidatePodUpdate` (validation.go): the pod spec is immutable except container and init
+    container images, activeDeadlineSeconds (set, or lowered — never removed) and tolerations
+    (existing ones kept, only their tolerationSeconds may change; new ones may be added). The
+    scheduler-owned fields nodeName and extendedResources[].assigned may only be set through
+    pods/binding."""
     errs = validate_pod(new)
     ns, os_ = new.get("spec") or {}, old.get("spec") or {}
+    for key in ("containers", "initContainers"):
+        nc, oc = ns.get(key) or [], os_.get(key) or []
+        if len(nc) != len(oc):
+            errs.append(FieldError("Forbidden", f"spec.{key}", "pod updates may not add or remove containers"))
+            return errs
+        for i, c in enumerate(nc):
+            if not c.get("image"):
+                errs.append(required(f"spec.{key}[{i}].image"))
+    nad, oad = ns.get("activeDeadlineSeconds"), os_.get("activeDeadlineSeconds")
+    if nad is not None:
+        if not isinstance(nad, int) or nad < 0 or nad > 2 ** 31 - 1:
+            errs.append(invalid("spec.activeDeadlineSeconds", "must be between 0 and 2147483647, inclusive"))
+            return errs
+        if oad is not None and oad < nad:
+            errs.append(invalid("spec.activeDeadlineSeconds", "must be less than or equal to previous value"))
+            return errs
+    elif oad is not None:
+        errs.append(invalid("spec.activeDeadlineSeconds", "must not update from a positive integer to nil value"))
+    new_tols = [{k: v for k, v in t.items() if k != "tolerationSeconds"} for t in ns.get("tolerations") or ()]
+    for t in os_.get("tolerations") or ():
+        if {k: v for k, v in t.items() if k != "tolerationSeconds"} not in new_tols:
+            errs.append(FieldError("Forbidden", "spec.tolerations",
+                                   "existing toleration can not be modified except its tolerationSeconds"))
+            break
+    munged = dict(ns)
+    for key in ("containers", "initContainers"):
+        if key in munged:
+            munged[key] = [dict(c, image=o.get("image")) for c, o in zip(ns.get(key) or [], os_.get(key) or [])]
+    munged.pop("activeDeadlineSeconds", None)
+    if oad is not None:
+        munged["activeDeadlineSeconds"] = oad
+    munged["tolerations"] = os_.get("tolerations")
     if ns.get("nodeName", "") != os_.get("nodeName", ""):
         errs.append(FieldError("Forbidden", "spec.nodeName", "may only be set through pods/binding"))
     na = [r.get("assigned") for r in ns.get("extendedResources") or ()]
     oa = [r.get("assigned") for r in os_.get("extendedResources") or ()]
     if na != oa:
         errs.append(FieldError("Forbidden", "spec.extendedResources.assigned", "may only be set through pods/binding"))
+    munged["nodeName"] = os_.get("nodeName")
+    munged["extendedResources"] = os_.get("extendedResources")
+    if _sem(munged) != _sem(os_):
+        errs.append(FieldError("Forbidden", "spec", POD_UPDATE_FORBIDDEN))
     return errs
 
 

@@ -1,0 +1,62 @@
+"""`ValidatePodUpdate` (`pkg/apis/core/validation/validation_test.go` TestValidatePodUpdate):
+only images, activeDeadlineSeconds (set or lowered) and tolerations (additions; existing ones
+may only change tolerationSeconds) are mutable."""
+import copy
+
+import pytest
+
+from kubernetes_amd.api.validation import validate_pod_update
+
+
+def pod(**spec):
+    base = {"containers": [{"name": "c", "image": "foo:V1"}], "restartPolicy": "Always", "dnsPolicy": "ClusterFirst"}
+    base.update(spec)
+    return {"metadata": {"name": "p", "namespace": "default", "uid": "u"}, "spec": base}
+
+
+def errs(new, old):
+    return [f"{e.field}: {e.detail}" for e in validate_pod_update(new, old)]
+
+
+def test_image_change_is_allowed():
+    assert errs(pod(containers=[{"name": "c", "image": "foo:V2"}]), pod()) == []
+
+
+def test_other_container_fields_are_forbidden():
+    new = pod(containers=[{"name": "c", "image": "foo:V1", "env": [{"name": "A", "value": "b"}]}])
+    assert any("pod updates may not change fields" in e for e in errs(new, pod()))
+
+
+def test_containers_may_not_be_added_or_removed():
+    new = pod(containers=[{"name": "c", "image": "foo:V1"}, {"name": "d", "image": "bar"}])
+    assert errs(new, pod()) == ["spec.containers: pod updates may not add or remove containers"]
+
+
+def test_image_must_stay_set():
+    assert any(e.startswith("spec.containers[0].image") for e in errs(pod(containers=[{"name": "c", "image": ""}]), pod()))
+
+
+@pytest.mark.parametrize("old_ad,new_ad,ok", [
+    (None, 30, True), (30, 20, True), (30, 30, True), (20, 30, False), (30, None, False), (None, -1, False),
+])
+def test_active_deadline_seconds(old_ad, new_ad, ok):
+    old = pod() if old_ad is None else pod(activeDeadlineSeconds=old_ad)
+    new = pod() if new_ad is None else pod(activeDeadlineSeconds=new_ad)
+    assert (errs(new, old) == []) == ok
+
+
+def test_tolerations_only_additions_and_seconds():
+    t = {"key": "node.kubernetes.io/not-ready", "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": 300}
+    old = pod(tolerations=[t])
+    added = pod(tolerations=[t, {"key": "gpu", "operator": "Exists", "effect": "NoSchedule"}])
+    assert errs(added, old) == []
+    shorter = pod(tolerations=[dict(t, tolerationSeconds=60)])
+    assert errs(shorter, old) == []
+    removed = pod(tolerations=[])
+    assert any("existing toleration can not be modified" in e for e in errs(removed, old))
+
+
+def test_node_name_only_through_binding():
+    new = copy.deepcopy(pod())
+    new["spec"]["nodeName"] = "n1"
+    assert any(e.startswith("spec.nodeName") for e in errs(new, pod()))
