@@ -1103,6 +1103,37 @@ VALIDATORS = {
     "Lease": validate_lease,
 }
 
+def validate_node_update(new, old):
+    """`ValidateNodeUpdate`: podCIDR and providerID may only go from "" to a value; status
+    addresses are unique."""
+    errs = []
+    ns, os_ = new.get("spec") or {}, old.get("spec") or {}
+    for k in ("podCIDR", "providerID"):
+        if os_.get(k) and ns.get(k) != os_.get(k):
+            errs.append(FieldError("Forbidden", f"spec.{k}", f"node updates may not change {k} except from \"\" to valid"))
+    seen = set()
+    for i, a in enumerate((new.get("status") or {}).get("addresses") or ()):
+        key = (a.get("type"), a.get("address"))
+        if key in seen:
+            errs.append(duplicate(f"status.addresses[{i}]", a))
+        seen.add(key)
+    return errs
+
+
+_PV_NOT_SOURCE = {"capacity", "accessModes", "claimRef", "persistentVolumeReclaimPolicy", "storageClassName",
+                  "mountOptions", "volumeMode", "nodeAffinity"}
+
+
+def validate_persistent_volume_update(new, old):
+    """`ValidatePersistentVolumeUpdate`: the volume source (hostPath, nfs, csi, local, ...) is
+    immutable after creation."""
+    ns, os_ = new.get("spec") or {}, old.get("spec") or {}
+    src = lambda sp: {k: v for k, v in sp.items() if k not in _PV_NOT_SOURCE}  # noqa: E731
+    if src(ns) != src(os_):
+        return [FieldError("Forbidden", "spec.persistentvolumesource", "is immutable after creation")]
+    return []
+
+
 UPDATE_VALIDATORS = {
     "Secret": validate_secret_update,
     "PersistentVolumeClaim": validate_persistent_volume_claim_update,
@@ -1112,6 +1143,7 @@ UPDATE_VALIDATORS = {
     "RoleBinding": validate_role_binding_update, "ClusterRoleBinding": validate_role_binding_update,
     "StorageClass": validate_storage_class_update, "PriorityClass": validate_priority_class_update,
     "ResourceQuota": validate_resource_quota_update,
+    "Node": validate_node_update, "PersistentVolume": validate_persistent_volume_update,
 }
 
 

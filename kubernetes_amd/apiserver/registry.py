@@ -146,28 +146,8 @@ class PodStrategy(Strategy):
             ns["extendedResources"] = ers
 
     def validate_update(self, new, old):
-        errs = validation.validate_pod(new) + validation.validate_object_meta_update(new, old)
-        ns, os_ = new.get("spec") or {}, old.get("spec") or {}
-        mutable = ("containers", "initContainers", "activeDeadlineSeconds", "tolerations")
-        for k in set(ns) | set(os_):
-            if k in mutable:
-                continue
-            if ns.get(k) != os_.get(k):
-                errs.append(validation.FieldError("Forbidden", f"spec.{k}", "pod updates may not change fields other than "
-                                                  "`spec.containers[*].image`, `spec.initContainers[*].image`, "
-                                                  "`spec.activeDeadlineSeconds` or `spec.tolerations`"))
-        for key in ("containers", "initContainers"):
-            a, b = ns.get(key) or [], os_.get(key) or []
-            if len(a) != len(b):
-                errs.append(validation.FieldError("Forbidden", f"spec.{key}", "may not add or remove containers"))
-                continue
-            for x, y in zip(a, b):
-                x2, y2 = dict(x), dict(y)
-                x2.pop("image", None)
-                y2.pop("image", None)
-                if x2 != y2:
-                    errs.append(validation.FieldError("Forbidden", f"spec.{key}", "pod updates may only change the image"))
-        return errs
+        # `ValidatePodUpdate`: images, activeDeadlineSeconds and tolerations only
+        return validation.validate_pod_update(new, old) + validation.validate_object_meta_update(new, old)
 
     def export(self, pod):
         self.prepare_create(pod)
