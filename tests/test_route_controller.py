@@ -98,7 +98,7 @@ def test_ip_routes_lists_kernel_table():
 
 
 def test_route_follows_pod_cidr_change_and_periodic_reconcile(run):
-    """A node whose podCIDR changes keeps one route (the re-created route under the same name
+    """A node re-created with another podCIDR keeps one route (the re-created route under the same name
     hint is not deleted as stale), and a route removed outside the controller comes back on the
     periodic reconcile without any node event."""
     table = MemoryRoutes()
@@ -117,9 +117,9 @@ def test_route_follows_pod_cidr_change_and_periodic_reconcile(run):
             async for d in dests():
                 if d == ["10.244.1.0/24"]:
                     break
-            n = await c.get("nodes", "n1")
-            n["spec"]["podCIDR"] = "10.244.5.0/24"
-            await c.update("nodes", n)
+            # podCIDR is set-once (ValidateNodeUpdate): the node is re-created with another one
+            await c.delete("nodes", "n1")
+            await c.create("nodes", {"metadata": {"name": "n1"}, "spec": {"podCIDR": "10.244.5.0/24"}, "status": {}})
             async for d in dests():
                 if d == ["10.244.5.0/24"]:
                     break
