@@ -1634,11 +1634,15 @@ class Kubelet:
         policy = spec.get("restartPolicy", "Always")
         n = len(spec.get("containers") or ())
         init_failed = any((s.get("state") or {}).get("terminated", {}).get("exitCode", 0) != 0 for s in init_statuses)
+        # `GetPhase` (kubelet_pods.go:1270): a failed init container fails a Never pod; pending
+        # initialization or ANY waiting container keeps the pod Pending; then Running while a
+        # container runs; all stopped -> Running (Always), Succeeded (all exit 0), Failed (Never)
+        # or Running (OnFailure restarts the failed ones)
         if init_failed and policy == "Never":
             phase = core.POD_FAILED
         elif not init_done:
             phase = core.POD_PENDING
-        elif waiting and not (running or terminated_ok or terminated_bad):
+        elif waiting:
             phase = core.POD_PENDING
         elif running:
             phase = core.POD_RUNNING

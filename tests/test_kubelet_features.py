@@ -134,3 +134,24 @@ def test_node_status_transitions_images_and_machine_info(run):
             assert any(any("busybox" in n for n in i["names"]) for i in s2.get("images") or ())
             assert s2["nodeInfo"]["bootID"] and s2["nodeInfo"]["kernelVersion"]
     run(main(), timeout=60)
+
+
+def test_pod_is_pending_while_any_container_waits(run):
+    """`GetPhase`: one running container does not make the pod Running while another waits
+    (here: an image that may never be pulled)."""
+    async def main():
+        async with LocalCluster(nodes=1, gpus_per_node=0) as cl:
+            c = cl.client
+            await c.create("pods", {"metadata": {"name": "half", "namespace": "default"},
+                                    "spec": {"containers": [{"name": "ok", "image": "busybox"},
+                                                            {"name": "stuck", "image": "never-pulled:1",
+                                                             "imagePullPolicy": "Never"}]}})
+            for _ in range(200):
+                p = await c.get("pods", "half", "default")
+                cs = {s["name"]: s for s in (p.get("status") or {}).get("containerStatuses") or ()}
+                if cs.get("ok", {}).get("state", {}).get("running") and cs.get("stuck", {}).get("state", {}).get("waiting"):
+                    break
+                await asyncio.sleep(0.02)
+            assert cs["stuck"]["state"]["waiting"]["reason"] == "ErrImageNeverPull"
+            assert p["status"]["phase"] == "Pending"
+    run(main(), timeout=60)
