@@ -67,6 +67,21 @@ def run_until_signal(main_coro_factory):
         closer = getattr(comp, "stop", None)
         if closer is not None:
             await closer()
+        # cancel what is left and give it a bounded time: a task that swallows its cancellation
+        # (asyncio.wait_for on 3.10 can) must not keep a SIGTERMed component alive
+        rest = [t for t in asyncio.all_tasks() if t is not asyncio.current_task() and not t.done()]
+        for t in rest:
+            t.cancel()
+        if rest:
+            _done, pending = await asyncio.wait(rest, timeout=5.0)
+            if pending:
+                import logging
+                import sys
+                for t in pending:
+                    logging.getLogger("shutdown").warning("task ignored cancellation at shutdown: %r", t)
+                    t.print_stack(file=sys.stderr)
+                sys.stderr.flush()
+                os._exit(0)
     prof_dir = os.environ.get("KAMD_PROFILE_DIR")
     if prof_dir:
         # pprof-equivalent: whole-process cProfile dump at shutdown (reference: /debug/pprof)

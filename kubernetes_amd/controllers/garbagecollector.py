@@ -288,7 +288,10 @@ class GarbageCollector(Controller):
         return True
 
     async def _discovery_loop(self):
-        while True:
+        # exits on the stop flag as well as on cancellation: on Python 3.10 asyncio.wait_for can
+        # swallow a CancelledError that races with the event being set, and a loop that then
+        # carries on would hang the process's shutdown (asyncio.run cancels and awaits all tasks)
+        while not self._gc_stopped:
             await self.resync_discovery()
             try:
                 await asyncio.wait_for(self._resync_now.wait(), self.discovery_period)
@@ -303,10 +306,12 @@ class GarbageCollector(Controller):
             if owned and inf._task is None:
                 inf.start()
         self._resync_now = asyncio.Event()
+        self._gc_stopped = False
         super().start()
         self._sync_task = asyncio.ensure_future(self._discovery_loop())
 
     def stop(self):
+        self._gc_stopped = True
         super().stop()
         if self._sync_task:
             self._sync_task.cancel()

@@ -71,9 +71,10 @@ CONTROLLERS = {
 }
 
 
-# like ControllersDisabledByDefault: "*" does not start these (name them explicitly, or the
-# command line enables them from --allocate-node-cidrs / --loadbalancer-ip-range)
-DISABLED_BY_DEFAULT = {"nodeipam", "route", "service", "csi-attacher"}
+# `ControllersDisabledByDefault` (controllermanager.go:321: bootstrapsigner, tokencleaner — kubeadm
+# names them explicitly) plus the controllers the command line enables from --allocate-node-cidrs
+# / --loadbalancer-ip-range and the in-tree CSI attacher: "*" does not start these
+DISABLED_BY_DEFAULT = {"bootstrapsigner", "tokencleaner", "nodeipam", "route", "service", "csi-attacher"}
 
 
 # the reference's `--controllers` names (`controllermanager.go:334-363`) for controllers this
