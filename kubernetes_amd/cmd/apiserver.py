@@ -32,6 +32,7 @@ def _parser():
     ap.add_argument("--port", type=int, default=8080)
     ap.add_argument("--port-file", default=None, help="write the bound port here (use with --port 0)")
     ap.add_argument("--admission-control", default=None, help="comma separated ordered plugin list")
+    ap.add_argument("--feature-gates", default="", help="e.g. PodPriority=true,ExpandPersistentVolumes=true")
     ap.add_argument("--admission-control-config-file", default=None,
                     help="AdmissionConfiguration: plugins[{name, path | configuration}]")
     ap.add_argument("--authorization-mode", default="AlwaysAllow")
@@ -381,6 +382,8 @@ def _reference_kwargs(a):
 def main(argv=None):
     ap = _parser()
     a = ap.parse_args(argv)
+    from ..utils.features import DefaultFeatureGate
+    DefaultFeatureGate.set(a.feature_gates)
     check_unsupported(ap, a)
     if a.public_address_override:
         a.bind_address = a.public_address_override

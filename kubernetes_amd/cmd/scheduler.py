@@ -19,12 +19,14 @@ import time
 
 from ..client.rest import Client
 from ..scheduler.scheduler import Scheduler
+from ..utils.features import DefaultFeatureGate
 from ._common import run_until_signal, setup_logging
 from ..utils.tasks import spawn
 
 
 def _parser():
     ap = argparse.ArgumentParser("kube-scheduler")
+    ap.add_argument("--feature-gates", default="", help="e.g. PodPriority=false (turns scheduler preemption off)")
     ap.add_argument("--master", default=None)
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--scheduler-name", default="default-scheduler")
@@ -105,6 +107,7 @@ def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     a = _parser().parse_args(argv)
     setup_logging(a.v)
+    DefaultFeatureGate.set(a.feature_gates)
     if a.shards > 1:
         sys.exit(supervise(argv, a.shards))
     from ..scheduler import policy as SP
@@ -156,7 +159,7 @@ def main(argv=None):
         extenders = [HTTPExtender.from_config(e) for e in ext_cfgs]
         s = Scheduler(client, a.scheduler_name, preds, prios, a.percentage_of_nodes_to_score,
                       emit_events=not a.no_events, extenders=extenders, shard_index=a.shard_index,
-                      shard_count=a.shard_count, preemption=not a.disable_preemption,
+                      shard_count=a.shard_count, preemption=not a.disable_preemption and DefaultFeatureGate("PodPriority"),
                       hard_pod_affinity_symmetric_weight=a.hard_pod_affinity_symmetric_weight,
                       failure_domains=[d for d in a.failure_domains.split(",") if d])
         s.profiling = _true(a.profiling)

@@ -20,7 +20,10 @@ DEFAULTS = {
     "ResourceV2": FeatureSpec(True, BETA),                 # pod-level extended resources (fork F1/F2)
     "XGMITopologyAwareAllocation": FeatureSpec(True, BETA),
     "EventDrivenKubelet": FeatureSpec(True, BETA),         # watch/exit-event driven pod sync
-    "PodPriority": FeatureSpec(False, ALPHA),
+    # pod priority and scheduler preemption: alpha and off in the reference; on by default here
+    # (a GPU cluster's high-priority training jobs preempt batch work), PodPriority=false turns
+    # scheduler preemption and priority-aware eviction ranking off
+    "PodPriority": FeatureSpec(True, ALPHA),
     "TaintBasedEvictions": FeatureSpec(False, ALPHA),     # node controller taints instead of deleting
     "TaintNodesByCondition": FeatureSpec(False, ALPHA),   # NoSchedule taints mirror node conditions
     "ExpandPersistentVolumes": FeatureSpec(False, ALPHA),
