@@ -15,6 +15,7 @@ from __future__ import annotations
 import os
 
 from ... import quota
+from ...utils.features import DefaultFeatureGate
 from ...api import core
 from ...api import meta as m
 from ...api.meta import new_uid
@@ -247,7 +248,8 @@ class Priority(Plugin):
     operations = (CREATE,)
 
     def admit(self, a):
-        if a.resource != "pods" or a.subresource:
+        # `plugin/pkg/admission/priority`: a no-op while the PodPriority feature is off
+        if a.resource != "pods" or a.subresource or not DefaultFeatureGate("PodPriority"):
             return
         spec = a.obj.setdefault("spec", {})
         pcn = spec.get("priorityClassName")
