@@ -34,25 +34,19 @@ async def ensure_revision(client, owner, kind, template, existing, limit=10):
     ns, h = md["namespace"], revision_hash(template)
     name = f"{md['name']}-{h}"
     newest = max((int(r.get("revision", 0)) for r in existing), default=0)
-    cur = next((r for r in existing if r["metadata"]["name"] == name), None)
+    # `FindEqualRevisions`: one of ours with this hash and this template (its name may carry a
+    # collision suffix)
+    cur = next((r for r in existing if r["metadata"]["name"] == name
+                or ((r["metadata"].get("labels") or {}).get(REVISION_HASH) == h
+                    and ((r.get("data") or {}).get("spec") or {}).get("template") == template)), None)
     if cur is None:
-        rev = {"apiVersion": "apps/v1", "kind": "ControllerRevision",
-               "metadata": {"name": name, "namespace": ns, "labels": {REVISION_HASH: h},
-                            "ownerReferences": [{"apiVersion": "apps/v1", "kind": kind, "name": md["name"],
-                                                 "uid": md["uid"], "controller": True, "blockOwnerDeletion": True}]},
-               "data": {"spec": {"template": template}}, "revision": newest + 1}
-        try:
-            cur = await client.create("controllerrevisions", rev, ns)
-        except APIStatusError as e:
-            if not is_already_exists(e):
-                raise
-            cur = await client.get("controllerrevisions", name, ns)
+        cur = await _create_revision(client, owner, kind, template, name, h, newest + 1)
     elif int(cur.get("revision", 0)) < newest:
         # rolled back to an older template: it becomes the newest revision again
-        cur = await client.patch("controllerrevisions", name, {"revision": newest + 1}, ns)
+        cur = await client.patch("controllerrevisions", cur["metadata"]["name"], {"revision": newest + 1}, ns)
     if limit is None:
         return cur
-    keep = [r for r in existing if r["metadata"]["name"] != name]
+    keep = [r for r in existing if r["metadata"]["name"] != cur["metadata"]["name"]]
     excess = len(keep) + 1 - max(1, limit)
     for r in sorted(keep, key=lambda r: int(r.get("revision", 0)))[:max(0, excess)]:
         try:
@@ -61,6 +55,41 @@ async def ensure_revision(client, owner, kind, template, existing, limit=10):
             if not is_not_found(e):
                 raise
     return cur
+
+
+async def _create_revision(client, owner, kind, template, name, h, number):
+    """`CreateControllerRevision` with collision handling: an existing revision of the same name
+    is reused when it holds the same template and is ours or an orphan (then adopted —
+    `AdoptControllerRevision`, e.g. the history of a set deleted with orphan propagation and
+    re-created); one owned by another controller, or holding other data, bumps a collision
+    count into the name and the create is retried."""
+    md = owner["metadata"]
+    ns = md["namespace"]
+    ref = {"apiVersion": "apps/v1", "kind": kind, "name": md["name"], "uid": md["uid"], "controller": True,
+           "blockOwnerDeletion": True}
+    collision = 0
+    while True:
+        rname = name if collision == 0 else f"{name}-{collision}"
+        rev = {"apiVersion": "apps/v1", "kind": "ControllerRevision",
+               "metadata": {"name": rname, "namespace": ns, "labels": {REVISION_HASH: h}, "ownerReferences": [ref]},
+               "data": {"spec": {"template": template}}, "revision": number}
+        try:
+            return await client.create("controllerrevisions", rev, ns)
+        except APIStatusError as e:
+            if not is_already_exists(e):
+                raise
+        got = await client.get("controllerrevisions", rname, ns)
+        same = ((got.get("data") or {}).get("spec") or {}).get("template") == template
+        owner_ref = next((r for r in got["metadata"].get("ownerReferences") or () if r.get("controller")), None)
+        if same and owner_ref is not None and owner_ref.get("uid") == md["uid"]:
+            return got
+        if same and owner_ref is None:
+            refs = list(got["metadata"].get("ownerReferences") or ()) + [ref]
+            return await client.patch("controllerrevisions", rname,
+                                      {"metadata": {"ownerReferences": refs, "uid": got["metadata"].get("uid")}}, ns)
+        collision += 1
+        if collision > 16:
+            raise RuntimeError(f"controller revision {name}: too many hash collisions")
 
 
 async def truncate_history(client, revisions, live, limit):

@@ -515,3 +515,31 @@ def test_web_statefulset_claims_and_partition_live(run, tmp_path):
             assert S.pod_revision(by["web-0"]) == old_rev == ss["status"]["currentRevision"]
             assert S.pod_revision(by["web-1"]) == ss["status"]["updateRevision"] != old_rev
     run(main(), timeout=150)
+
+
+def test_controller_revision_adoption_and_collision():
+    """`CreateControllerRevision` / `AdoptControllerRevision`: an orphaned revision with the same
+    template (a set deleted with orphan propagation and re-created) is adopted; one owned by
+    another controller makes the new revision take a collision-suffixed name."""
+    import asyncio as _a
+
+    from kubernetes_amd.client.fake import FakeClient
+    from kubernetes_amd.controllers.history import REVISION_HASH, ensure_revision, revision_hash
+    tmpl = {"metadata": {"labels": {"app": "web"}}, "spec": {"containers": [{"name": "c", "image": "x"}]}}
+    h = revision_hash(tmpl)
+    owner = {"metadata": {"name": "web", "namespace": "default", "uid": "new-uid"}}
+    orphan = {"apiVersion": "apps/v1", "kind": "ControllerRevision",
+              "metadata": {"name": f"web-{h}", "namespace": "default", "labels": {REVISION_HASH: h}},
+              "data": {"spec": {"template": tmpl}}, "revision": 1}
+
+    async def run(existing_obj):
+        c = FakeClient(existing_obj)
+        rev = await ensure_revision(c, owner, "StatefulSet", tmpl, [], limit=None)
+        return rev, c
+    rev, c = _a.run(run(orphan))
+    assert rev["metadata"]["name"] == f"web-{h}"
+    assert rev["metadata"]["ownerReferences"][0]["uid"] == "new-uid"
+    foreign = dict(orphan, metadata=dict(orphan["metadata"], ownerReferences=[
+        {"apiVersion": "apps/v1", "kind": "StatefulSet", "name": "web", "uid": "old-uid", "controller": True}]))
+    rev, c = _a.run(run(foreign))
+    assert rev["metadata"]["name"] == f"web-{h}-1" and rev["metadata"]["ownerReferences"][0]["uid"] == "new-uid"
