@@ -112,6 +112,10 @@ def ri_for_obj(o):
     return ri
 
 
+ALL_CATEGORY = ["pods", "replicationcontrollers", "services", "daemonsets", "deployments", "replicasets",
+                "statefulsets", "horizontalpodautoscalers", "jobs", "cronjobs"]
+
+
 def split_targets(targets):
     """['pods', 'a', 'b'] / ['pods/a', 'nodes/b'] / ['pod,node'] -> [(ri, name|None)]"""
     out = []
@@ -125,7 +129,10 @@ def split_targets(targets):
                 raise SystemExit(f'error: the server doesn\'t have a resource type "{r}"')
             out.append((ri, n))
         return out
-    kinds = targets[0].split(",")
+    kinds = []
+    for k in targets[0].split(","):
+        # the `all` category (`pkg/kubectl/categories.go` legacyUserResources)
+        kinds += ALL_CATEGORY if k == "all" else [k]
     names = targets[1:]
     for k in kinds:
         ri = m.lookup(k)
@@ -290,7 +297,10 @@ class Kubectl(extra.ExtraCommands):
                         raise
             self.p(self._render(objs))
             return
-        for ri, name in split_targets(a.targets):
+        targets = split_targets(a.targets)
+        multi = len({ri.plural for ri, _ in targets}) > 1 and not any(n for _, n in targets)
+        printed = False
+        for ri, name in targets:
             ns = None if (a.all_namespaces or not ri.namespaced) else self.ns
             if a.experimental_server_print and not a.output and not a.watch:
                 # the server renders the columns (meta.k8s.io Table); kubectl only aligns them
@@ -343,8 +353,20 @@ class Kubectl(extra.ExtraCommands):
                     rows, h = printers.rows_for(ri.kind, [o], a.output == "wide")
                     self.p(printers.table(rows, h).splitlines()[-1])
                 return
+            if multi and (not a.output or a.output == "wide"):
+                # several kinds (`get all`, `get po,svc`): each non-empty table, names as kind/name
+                if items:
+                    shown = [dict(o, metadata=dict(o["metadata"], name=f"{ri.kind.lower()}/{o['metadata']['name']}"))
+                             for o in items]
+                    if printed:
+                        self.p("")
+                    self.p(self._render(shown, ri.kind, all_ns=a.all_namespaces))
+                    printed = True
+                continue
             self.p(self._render(items, ri.kind, list_obj=lst if a.output in ("json", "yaml") else None,
                                 all_ns=a.all_namespaces))
+        if multi and not printed and (not a.output or a.output == "wide"):
+            self.p("No resources found.")
 
     async def cmd_describe(self):
         a = self.a

@@ -59,6 +59,125 @@ def table(rows, headers):
     return "\n".join(out)
 
 
+def _g(o, *path, default=None):
+    for k in path:
+        o = (o or {}).get(k) if isinstance(o, dict) else None
+    return default if o is None else o
+
+
+def _svc_external(o):
+    spec = o.get("spec") or {}
+    ips = list(spec.get("externalIPs") or ())
+    if spec.get("type") == "LoadBalancer":
+        ing = [i.get("ip") or i.get("hostname") for i in _g(o, "status", "loadBalancer", "ingress", default=[])]
+        ips = ing + ips if ing else (ips or ["<pending>"])
+    elif spec.get("type") == "ExternalName":
+        return spec.get("externalName", "")
+    return ",".join(ips) or "<none>"
+
+
+def _svc_ports(o):
+    out = []
+    for p in _g(o, "spec", "ports", default=[]):
+        s = str(p.get("port"))
+        if p.get("nodePort"):
+            s += f":{p['nodePort']}"
+        out.append(f"{s}/{p.get('protocol', 'TCP')}")
+    return ",".join(out) or "<none>"
+
+
+def _endpoints(o):
+    addrs = []
+    for ss in o.get("subsets") or ():
+        ports = [p.get("port") for p in ss.get("ports") or ()] or [None]
+        for a in ss.get("addresses") or ():
+            for port in ports:
+                addrs.append(a.get("ip") + (f":{port}" if port is not None else ""))
+    if not addrs:
+        return "<none>"
+    shown = ",".join(addrs[:3])
+    return shown + (f" + {len(addrs) - 3} more..." if len(addrs) > 3 else "")
+
+
+def _modes(modes):
+    short = {"ReadWriteOnce": "RWO", "ReadOnlyMany": "ROX", "ReadWriteMany": "RWX"}
+    return ",".join(short.get(m, m) for m in modes or ())
+
+
+def _hpa_targets(o):
+    st, spec = o.get("status") or {}, o.get("spec") or {}
+    want = spec.get("targetCPUUtilizationPercentage")
+    cur = st.get("currentCPUUtilizationPercentage")
+    if want is None:
+        return "<none>"
+    return f"{'<unknown>' if cur is None else f'{cur}%'}/{want}%"
+
+
+def _csr_condition(o):
+    conds = [c.get("type") for c in _g(o, "status", "conditions", default=[])]
+    if _g(o, "status", "certificate") and "Approved" in conds:
+        conds.append("Issued")
+    return ",".join(conds) or "Pending"
+
+
+def _pdb_val(v):
+    return "N/A" if v is None else str(v)
+
+
+# `pkg/printers/internalversion/printers.go` column sets (NAME first, AGE last)
+_COLUMNS = {
+    "Service": (["NAME", "TYPE", "CLUSTER-IP", "EXTERNAL-IP", "PORT(S)", "AGE"],
+                lambda o: [_g(o, "spec", "type", default="ClusterIP"), _g(o, "spec", "clusterIP", default="<none>") or "<none>",
+                           _svc_external(o), _svc_ports(o)]),
+    "Endpoints": (["NAME", "ENDPOINTS", "AGE"], lambda o: [_endpoints(o)]),
+    "ServiceAccount": (["NAME", "SECRETS", "AGE"], lambda o: [len(o.get("secrets") or ())]),
+    "Secret": (["NAME", "TYPE", "DATA", "AGE"], lambda o: [o.get("type", "Opaque"), len(o.get("data") or {})]),
+    "ConfigMap": (["NAME", "DATA", "AGE"], lambda o: [len(o.get("data") or {}) + len(o.get("binaryData") or {})]),
+    "DaemonSet": (["NAME", "DESIRED", "CURRENT", "READY", "UP-TO-DATE", "AVAILABLE", "NODE SELECTOR", "AGE"],
+                  lambda o: [_g(o, "status", "desiredNumberScheduled", default=0), _g(o, "status", "currentNumberScheduled", default=0),
+                             _g(o, "status", "numberReady", default=0), _g(o, "status", "updatedNumberScheduled", default=0),
+                             _g(o, "status", "numberAvailable", default=0),
+                             ",".join(f"{k}={v}" for k, v in sorted(_g(o, "spec", "template", "spec", "nodeSelector", default={}).items()))
+                             or "<none>"]),
+    "StatefulSet": (["NAME", "DESIRED", "CURRENT", "AGE"],
+                    lambda o: [_g(o, "spec", "replicas", default=1), _g(o, "status", "replicas", default=0)]),
+    "CronJob": (["NAME", "SCHEDULE", "SUSPEND", "ACTIVE", "LAST SCHEDULE", "AGE"],
+                lambda o: [_g(o, "spec", "schedule", default=""), str(bool(_g(o, "spec", "suspend", default=False))),
+                           len(_g(o, "status", "active", default=[])),
+                           age(_g(o, "status", "lastScheduleTime")) if _g(o, "status", "lastScheduleTime") else "<none>"]),
+    "HorizontalPodAutoscaler": (["NAME", "REFERENCE", "TARGETS", "MINPODS", "MAXPODS", "REPLICAS", "AGE"],
+                                lambda o: [f"{_g(o, 'spec', 'scaleTargetRef', 'kind', default='')}/{_g(o, 'spec', 'scaleTargetRef', 'name', default='')}",
+                                           _hpa_targets(o), _g(o, "spec", "minReplicas", default=1),
+                                           _g(o, "spec", "maxReplicas", default=0), _g(o, "status", "currentReplicas", default=0)]),
+    "PodDisruptionBudget": (["NAME", "MIN AVAILABLE", "MAX UNAVAILABLE", "ALLOWED DISRUPTIONS", "AGE"],
+                            lambda o: [_pdb_val(_g(o, "spec", "minAvailable")), _pdb_val(_g(o, "spec", "maxUnavailable")),
+                                       _g(o, "status", "disruptionsAllowed", default=0)]),
+    "PersistentVolume": (["NAME", "CAPACITY", "ACCESS MODES", "RECLAIM POLICY", "STATUS", "CLAIM", "STORAGECLASS", "REASON", "AGE"],
+                         lambda o: [_g(o, "spec", "capacity", "storage", default=""), _modes(_g(o, "spec", "accessModes")),
+                                    _g(o, "spec", "persistentVolumeReclaimPolicy", default="Retain"),
+                                    _g(o, "status", "phase", default=""),
+                                    (f"{_g(o, 'spec', 'claimRef', 'namespace')}/{_g(o, 'spec', 'claimRef', 'name')}"
+                                     if _g(o, "spec", "claimRef") else ""),
+                                    _g(o, "spec", "storageClassName", default=""), _g(o, "status", "reason", default="")]),
+    "PersistentVolumeClaim": (["NAME", "STATUS", "VOLUME", "CAPACITY", "ACCESS MODES", "STORAGECLASS", "AGE"],
+                              lambda o: [_g(o, "status", "phase", default=""), _g(o, "spec", "volumeName", default=""),
+                                         _g(o, "status", "capacity", "storage", default=""),
+                                         _modes(_g(o, "status", "accessModes")), _g(o, "spec", "storageClassName", default="")]),
+    "StorageClass": (["NAME", "PROVISIONER", "AGE"],
+                     lambda o: [o.get("provisioner", "")]),
+    "CertificateSigningRequest": (["NAME", "REQUESTOR", "CONDITION", "AGE"],
+                                  lambda o: [_g(o, "spec", "username", default=""), _csr_condition(o)]),
+    "Ingress": (["NAME", "HOSTS", "ADDRESS", "PORTS", "AGE"],
+                lambda o: [",".join(r.get("host", "") for r in _g(o, "spec", "rules", default=[]) if r.get("host")) or "*",
+                           ",".join(i.get("ip", "") for i in _g(o, "status", "loadBalancer", "ingress", default=[])),
+                           "80, 443" if _g(o, "spec", "tls") else "80"]),
+    "PriorityClass": (["NAME", "VALUE", "GLOBAL-DEFAULT", "AGE"],
+                      lambda o: [o.get("value", 0), str(bool(o.get("globalDefault", False))).lower()]),
+}
+_CLUSTER_SCOPED = {"Node", "Namespace", "PersistentVolume", "StorageClass", "CertificateSigningRequest", "PriorityClass",
+                   "ClusterRole", "ClusterRoleBinding", "PodSecurityPolicy", "CustomResourceDefinition", "APIService"}
+
+
 def rows_for(kind, items, wide=False, all_ns=False):
     if kind == "Pod":
         h = ["NAME", "READY", "STATUS", "RESTARTS", "AGE"]
@@ -116,10 +235,19 @@ def rows_for(kind, items, wide=False, all_ns=False):
     elif kind == "Namespace":
         h = ["NAME", "STATUS", "AGE"]
         rows = [[o["metadata"]["name"], (o.get("status") or {}).get("phase", ""), age(o["metadata"].get("creationTimestamp"))] for o in items]
+    elif kind in _COLUMNS:
+        h, fn = _COLUMNS[kind]
+        h = list(h)
+        rows = [[o["metadata"]["name"]] + fn(o) + [age(o["metadata"].get("creationTimestamp"))] for o in items]
+        if wide and kind == "Service":
+            h.append("SELECTOR")
+            for o, r in zip(items, rows):
+                sel = (o.get("spec") or {}).get("selector") or {}
+                r.append(",".join(f"{k}={v}" for k, v in sorted(sel.items())) or "<none>")
     else:
         h = ["NAME", "AGE"]
         rows = [[o["metadata"]["name"], age(o["metadata"].get("creationTimestamp"))] for o in items]
-    if all_ns and kind != "Node":
+    if all_ns and kind not in _CLUSTER_SCOPED:
         h = ["NAMESPACE"] + h
         rows = [[o["metadata"].get("namespace", "")] + r for o, r in zip(items, rows)]
     return rows, h

@@ -316,3 +316,16 @@ def test_drain_retries_while_a_budget_refuses(cluster, tmp_path, monkeypatch):
     rc, out = k(cluster, "drain", "node-0", "--force", "--ignore-daemonsets", "--timeout", "20")
     assert rc == 0 and "pod/guarded evicted" in out and "node/node-0 drained" in out
     assert k(cluster, "uncordon", "node-0")[0] == 0
+
+
+def test_get_all_and_reference_columns(cluster):
+    """`kubectl get all` (the legacy user-resource category) and the reference printers'
+    columns for services, endpoints, service accounts and namespaces."""
+    rc, out = k(cluster, "get", "all")
+    assert rc == 0 and "service/kubernetes" in out and "CLUSTER-IP" in out and "443/TCP" in out
+    rc, out = k(cluster, "get", "ep", "kubernetes")
+    assert out.splitlines()[0].split() == ["NAME", "ENDPOINTS", "AGE"]
+    rc, out = k(cluster, "get", "sa", "-n", "kube-system")
+    assert out.splitlines()[0].split()[:2] == ["NAME", "SECRETS"]
+    rc, out = k(cluster, "get", "ns", "--all-namespaces")
+    assert out.splitlines()[0].split() == ["NAME", "STATUS", "AGE"]          # cluster-scoped: no NAMESPACE column
