@@ -30,20 +30,59 @@ def age(ts):
     return f"{d // 86400}d"
 
 
-def pod_status(p):
+def pod_status_and_restarts(p):
+    """`printPod` (pkg/printers/internalversion/printers.go): the STATUS column — Init:i/n,
+    Init:<reason>, Init:ExitCode:n while initializing; otherwise the last container's waiting
+    or terminated reason (ExitCode:n / Signal:n without one), Completed shown as Running while a
+    container still runs; Terminating (Unknown for a pod on an unreachable node) once deleted —
+    and the RESTARTS count of the containers it looked at."""
     st = p.get("status") or {}
+    spec = p.get("spec") or {}
+    reason = st.get("reason") or st.get("phase") or "Unknown"
+    restarts = 0
+    initializing = False
+    n_init = len(spec.get("initContainers") or ())
+    for i, c in enumerate(st.get("initContainerStatuses") or ()):
+        restarts += int(c.get("restartCount", 0))
+        s = c.get("state") or {}
+        term, wait = s.get("terminated"), s.get("waiting")
+        if term is not None and term.get("exitCode", 0) == 0:
+            continue
+        if term is not None:
+            if not term.get("reason"):
+                reason = f"Init:Signal:{term['signal']}" if term.get("signal") else f"Init:ExitCode:{term.get('exitCode', 0)}"
+            else:
+                reason = "Init:" + term["reason"]
+        elif wait is not None and wait.get("reason") and wait["reason"] != "PodInitializing":
+            reason = "Init:" + wait["reason"]
+        else:
+            reason = f"Init:{i}/{n_init}"
+        initializing = True
+        break
+    if not initializing:
+        restarts = 0
+        has_running = False
+        for c in reversed(st.get("containerStatuses") or ()):
+            restarts += int(c.get("restartCount", 0))
+            s = c.get("state") or {}
+            term, wait = s.get("terminated"), s.get("waiting")
+            if wait is not None and wait.get("reason"):
+                reason = wait["reason"]
+            elif term is not None and term.get("reason"):
+                reason = term["reason"]
+            elif term is not None:
+                reason = f"Signal:{term['signal']}" if term.get("signal") else f"ExitCode:{term.get('exitCode', 0)}"
+            elif c.get("ready") and s.get("running") is not None:
+                has_running = True
+        if reason == "Completed" and has_running:
+            reason = "Running"
     if p["metadata"].get("deletionTimestamp"):
-        return "Terminating"
-    reason = st.get("reason")
-    if reason:
-        return reason
-    for cs in st.get("containerStatuses") or ():
-        s = cs.get("state") or {}
-        if "waiting" in s and s["waiting"].get("reason"):
-            return s["waiting"]["reason"]
-        if "terminated" in s and st.get("phase") not in ("Succeeded",):
-            return s["terminated"].get("reason", "Terminated")
-    return st.get("phase", "Unknown")
+        reason = "Unknown" if st.get("reason") == "NodeLost" else "Terminating"
+    return reason, restarts
+
+
+def pod_status(p):
+    return pod_status_and_restarts(p)[0]
 
 
 def pod_gpus(p):
@@ -187,8 +226,9 @@ def rows_for(kind, items, wide=False, all_ns=False):
         for p in items:
             cs = (p.get("status") or {}).get("containerStatuses") or []
             n = len((p.get("spec") or {}).get("containers") or [])
-            r = [p["metadata"]["name"], f"{sum(1 for c in cs if c.get('ready'))}/{n}", pod_status(p),
-                 sum(c.get("restartCount", 0) for c in cs), age(p["metadata"].get("creationTimestamp"))]
+            status, restarts = pod_status_and_restarts(p)
+            r = [p["metadata"]["name"], f"{sum(1 for c in cs if c.get('ready'))}/{n}", status,
+                 restarts, age(p["metadata"].get("creationTimestamp"))]
             if wide:
                 g = pod_gpus(p)
                 r += [(p.get("status") or {}).get("podIP", "<none>"), (p.get("spec") or {}).get("nodeName") or "<none>",

@@ -329,3 +329,30 @@ def test_get_all_and_reference_columns(cluster):
     assert out.splitlines()[0].split()[:2] == ["NAME", "SECRETS"]
     rc, out = k(cluster, "get", "ns", "--all-namespaces")
     assert out.splitlines()[0].split() == ["NAME", "STATUS", "AGE"]          # cluster-scoped: no NAMESPACE column
+
+
+@pytest.mark.parametrize("status,deleting,expect", [
+    ({"phase": "Running", "containerStatuses": [{"ready": True, "state": {"running": {}}, "restartCount": 2}]}, False, ("Running", 2)),
+    ({"phase": "Pending", "initContainerStatuses": [{"state": {"waiting": {"reason": "PodInitializing"}}}]}, False, ("Init:0/1", 0)),
+    ({"phase": "Pending", "initContainerStatuses": [{"state": {"terminated": {"exitCode": 3}}, "restartCount": 1}]}, False,
+     ("Init:ExitCode:3", 1)),
+    ({"phase": "Running", "containerStatuses": [{"state": {"waiting": {"reason": "CrashLoopBackOff"}}, "restartCount": 4}]},
+     False, ("CrashLoopBackOff", 4)),
+    ({"phase": "Succeeded", "containerStatuses": [{"state": {"terminated": {"exitCode": 0, "reason": "Completed"}}}]},
+     False, ("Completed", 0)),
+    ({"phase": "Running", "containerStatuses": [{"ready": True, "state": {"running": {}}},
+                                                {"state": {"terminated": {"exitCode": 0, "reason": "Completed"}}}]},
+     False, ("Running", 0)),
+    ({"phase": "Failed", "containerStatuses": [{"state": {"terminated": {"exitCode": 137, "signal": 9}}}]}, False, ("Signal:9", 0)),
+    ({"phase": "Running"}, True, ("Terminating", 0)),
+    ({"phase": "Failed", "reason": "Evicted"}, False, ("Evicted", 0)),
+])
+def test_pod_status_column(status, deleting, expect):
+    """printPod's STATUS / RESTARTS columns (`pkg/printers/internalversion/printers_test.go`
+    TestPrintPod cases)."""
+    from kubernetes_amd.kubectl.printers import pod_status_and_restarts
+    p = {"metadata": {"name": "p"}, "spec": {"initContainers": [{"name": "i"}]} if "initContainerStatuses" in status else {},
+         "status": status}
+    if deleting:
+        p["metadata"]["deletionTimestamp"] = "2000-01-01T00:00:00Z"
+    assert pod_status_and_restarts(p) == expect
