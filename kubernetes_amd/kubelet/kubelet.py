@@ -1603,7 +1603,7 @@ class Kubelet:
         spec = pod.get("spec") or {}
         rt = self.runtime
         statuses, init_statuses = [], []
-        running = terminated_ok = terminated_bad = waiting = 0
+        running = terminated_ok = terminated_bad = waiting = restarting = 0
         not_ready = 0
         for c in spec.get("containers") or ():
             cid = st.containers.get(c["name"])
@@ -1611,7 +1611,12 @@ class Kubelet:
             s = _container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"]))
             statuses.append(s)
             if cs is None:
-                waiting += 1
+                if st.restarts.get(c["name"], 0) > 0:
+                    # between a restart's kill and the new container: the reference's "waiting with
+                    # a last termination state" counts as stopped, so the pod does not flap to Pending
+                    restarting += 1
+                else:
+                    waiting += 1
             elif cs.state == RUNNING:
                 running += 1
                 if c.get("readinessProbe") and not self.probes.ready(st.uid, c["name"]):
@@ -1646,15 +1651,15 @@ class Kubelet:
             phase = core.POD_PENDING
         elif running:
             phase = core.POD_RUNNING
-        elif terminated_ok + terminated_bad == n:
+        elif terminated_ok + terminated_bad + restarting == n:
             if policy == "Always":
                 phase = core.POD_RUNNING
-            elif terminated_bad and policy == "Never":
-                phase = core.POD_FAILED
-            elif terminated_bad:
-                phase = core.POD_RUNNING
-            else:
+            elif terminated_ok == n:
                 phase = core.POD_SUCCEEDED
+            elif policy == "Never":
+                phase = core.POD_FAILED
+            else:
+                phase = core.POD_RUNNING
         else:
             phase = core.POD_PENDING if waiting else core.POD_RUNNING
         ready = phase == core.POD_RUNNING and running == n and not not_ready
