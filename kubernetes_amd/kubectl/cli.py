@@ -112,6 +112,11 @@ def ri_for_obj(o):
     return ri
 
 
+# kubectl 1.9 prefixes names in multi-kind tables with the short resource name (po/…, svc/…)
+_SHORT_KIND = {"Pod": "po", "Service": "svc", "Deployment": "deploy", "ReplicaSet": "rs", "ReplicationController": "rc",
+               "DaemonSet": "ds", "StatefulSet": "statefulsets", "Job": "jobs", "CronJob": "cronjobs",
+               "HorizontalPodAutoscaler": "hpa", "Node": "no", "Namespace": "ns", "ConfigMap": "cm", "Secret": "secrets",
+               "Endpoints": "ep", "ServiceAccount": "sa", "PersistentVolume": "pv", "PersistentVolumeClaim": "pvc"}
 ALL_CATEGORY = ["pods", "replicationcontrollers", "services", "daemonsets", "deployments", "replicasets",
                 "statefulsets", "horizontalpodautoscalers", "jobs", "cronjobs"]
 
@@ -356,7 +361,8 @@ class Kubectl(extra.ExtraCommands):
             if multi and (not a.output or a.output == "wide"):
                 # several kinds (`get all`, `get po,svc`): each non-empty table, names as kind/name
                 if items:
-                    shown = [dict(o, metadata=dict(o["metadata"], name=f"{ri.kind.lower()}/{o['metadata']['name']}"))
+                    prefix = _SHORT_KIND.get(ri.kind, ri.kind.lower())
+                    shown = [dict(o, metadata=dict(o["metadata"], name=f"{prefix}/{o['metadata']['name']}"))
                              for o in items]
                     if printed:
                         self.p("")

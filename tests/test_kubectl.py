@@ -322,7 +322,7 @@ def test_get_all_and_reference_columns(cluster):
     """`kubectl get all` (the legacy user-resource category) and the reference printers'
     columns for services, endpoints, service accounts and namespaces."""
     rc, out = k(cluster, "get", "all")
-    assert rc == 0 and "service/kubernetes" in out and "CLUSTER-IP" in out and "443/TCP" in out
+    assert rc == 0 and "svc/kubernetes" in out and "CLUSTER-IP" in out and "443/TCP" in out
     rc, out = k(cluster, "get", "ep", "kubernetes")
     assert out.splitlines()[0].split() == ["NAME", "ENDPOINTS", "AGE"]
     rc, out = k(cluster, "get", "sa", "-n", "kube-system")
