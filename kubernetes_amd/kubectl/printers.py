@@ -421,8 +421,14 @@ def describe(obj, events=(), ctx=None):
     lines.append(f"CreationTimestamp: {md.get('creationTimestamp')}")
     if kind == "Pod":
         spec, st = obj.get("spec") or {}, obj.get("status") or {}
-        lines += [f"Node:         {spec.get('nodeName') or '<none>'}", f"Status:       {pod_status(obj)}",
-                  f"IP:           {st.get('podIP', '')}", f"QoS Class:    {st.get('qosClass', '')}"]
+        # `describePod`: the phase (Terminating once deleted), then Reason / Message when set
+        phase = "Terminating" if md.get("deletionTimestamp") else st.get("phase", "")
+        lines += [f"Node:         {spec.get('nodeName') or '<none>'}", f"Status:       {phase}"]
+        if st.get("reason"):
+            lines.append(f"Reason:       {st['reason']}")
+        if st.get("message"):
+            lines.append(f"Message:      {st['message']}")
+        lines += [f"IP:           {st.get('podIP', '')}", f"QoS Class:    {st.get('qosClass', '')}"]
         ers = spec.get("extendedResources") or []
         if ers:
             lines.append("Extended Resources:")
