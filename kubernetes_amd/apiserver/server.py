@@ -84,6 +84,25 @@ def _body(req):
     return req.obj if req.obj is not None else codec.loads(req.body)
 
 
+def _log_container(pod, container):
+    """`pkg/registry/core/pod/rest/log.go` validateContainer: the only container when none is
+    named, else the name must be one of the pod's (init) containers."""
+    spec = pod.get("spec") or {}
+    names = [c.get("name") for c in spec.get("containers") or ()]
+    init = [c.get("name") for c in spec.get("initContainers") or ()]
+    name = pod["metadata"].get("name")
+    if not container:
+        if len(names) == 1:
+            return names[0]
+        msg = f"a container name must be specified for pod {name}, choose one of: [{' '.join(names)}]"
+        if init:
+            msg += f" or one of the init containers: [{' '.join(init)}]"
+        raise bad_request(msg)
+    if container not in names and container not in init:
+        raise bad_request(f"container {container} is not valid for pod {name}")
+    return container
+
+
 def _entry_resp(req, ri, status, e):
     """A cached object as the response body: its protobuf envelope when the client negotiated
     protobuf (no JSON made or parsed), else its JSON bytes."""
@@ -2212,7 +2231,9 @@ class APIServer:
         """pods/log relayed to the kubelet (`pkg/registry/core/pod/rest/log.go`); with follow the
         kubelet's stream is relayed as it arrives."""
         from urllib.parse import urlencode
-        _, addr, port = await self._kubelet_of(ns, name)
+        pod, addr, port = await self._kubelet_of(ns, name)
+        q = dict(q)
+        q["container"] = _log_container(pod, q.get("container", ""))
         from ..client.http import HTTPClient
         c = HTTPClient(f"{self.kubelet_scheme}://{addr}:{port}", ssl_context=self.kubelet_ssl,
                        timeout=max(self.kubelet_timeout, 30.0))

@@ -356,3 +356,19 @@ def test_pod_status_column(status, deleting, expect):
     if deleting:
         p["metadata"]["deletionTimestamp"] = "2000-01-01T00:00:00Z"
     assert pod_status_and_restarts(p) == expect
+
+
+def test_logs_need_a_container_name_for_multi_container_pods(cluster):
+    """`log.go` validateContainer: a multi-container pod's logs need a container name."""
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "two"},
+           "spec": {"containers": [{"name": "a", "image": "x"}, {"name": "b", "image": "x"}]}}
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(pod, f)
+    assert k(cluster, "create", "-f", f.name)[0] == 0
+    wait(lambda: "Running" in k(cluster, "get", "pods", "two")[1])
+    with pytest.raises(SystemExit, match="a container name must be specified for pod two, choose one of: \\[a b\\]"):
+        k(cluster, "logs", "two")
+    with pytest.raises(SystemExit, match="container c is not valid for pod two"):
+        k(cluster, "logs", "two", "-c", "c")
+    k(cluster, "delete", "pod", "two", "--grace-period", "0")
