@@ -347,6 +347,11 @@ class Kubectl(extra.ExtraCommands):
                 if not cont or not a.chunk_size:
                     break
             lst["apiVersion"] = page.get("apiVersion", "v1")
+            if ri.kind == "Pod" and not getattr(a, "show_all", False):
+                # `resource_filter.go` filterPods: a list hides terminated (Succeeded / Failed)
+                # pods unless --show-all; a named pod is always shown
+                lst["items"] = [p for p in lst["items"]
+                                if (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
             items = lst["items"]
             for o in items:
                 o.setdefault("kind", ri.kind)
@@ -1979,7 +1984,8 @@ def build_parser():
     g.add_argument("--raw", default="", help="GET this API path verbatim")
     g.add_argument("--chunk-size", type=int, default=500)
     g.add_argument("--include-uninitialized", action="store_true")
-    g.add_argument("-a", "--show-all", action="store_true", help="deprecated; terminated pods are always shown")
+    g.add_argument("-a", "--show-all", action="store_true",
+                   help="show all resources (by default terminated pods are hidden from lists)")
     _common(g)
     d = add("describe")
     d.add_argument("targets", nargs="*")

@@ -372,3 +372,18 @@ def test_logs_need_a_container_name_for_multi_container_pods(cluster):
     with pytest.raises(SystemExit, match="container c is not valid for pod two"):
         k(cluster, "logs", "two", "-c", "c")
     k(cluster, "delete", "pod", "two", "--grace-period", "0")
+
+
+def test_get_pods_hides_terminated_unless_show_all(cluster):
+    """kubectl 1.9 `filterPods`: lists hide Succeeded / Failed pods unless --show-all; a named
+    pod is always printed."""
+    import tempfile
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "done", "annotations": {"kubemark.amd.com/run-seconds": "0"}},
+           "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "image": "x"}]}}
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(pod, f)
+    assert k(cluster, "create", "-f", f.name)[0] == 0
+    wait(lambda: "Completed" in k(cluster, "get", "pod", "done")[1])
+    assert "done" not in k(cluster, "get", "pods")[1]
+    assert "done" in k(cluster, "get", "pods", "--show-all")[1]
+    k(cluster, "delete", "pod", "done", "--grace-period", "0")
