@@ -246,7 +246,11 @@ def rows_for(kind, items, wide=False, all_ns=False):
                 s += ",SchedulingDisabled"
             cap = (n.get("status") or {}).get("capacity") or {}
             devs = ((n.get("status") or {}).get("extendedResources") or {}).get(core.AMD_GPU, {}).get("resources") or {}
-            r = [n["metadata"]["name"], s, "<none>", age(n["metadata"].get("creationTimestamp")),
+            # `findNodeRoles`: node-role.kubernetes.io/<role> labels and the kubernetes.io/role label
+            labels = n["metadata"].get("labels") or {}
+            roles = sorted({k.split("/", 1)[1] for k in labels if k.startswith("node-role.kubernetes.io/") and "/" in k}
+                           | ({labels["kubernetes.io/role"]} if labels.get("kubernetes.io/role") else set()))
+            r = [n["metadata"]["name"], s, ",".join(r_ for r_ in roles if r_) or "<none>", age(n["metadata"].get("creationTimestamp")),
                  ((n.get("status") or {}).get("nodeInfo") or {}).get("kubeletVersion", ""),
                  f"{cap.get(core.AMD_GPU, '0')}/{len(devs)}"]
             if wide:
