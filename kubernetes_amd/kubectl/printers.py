@@ -272,10 +272,15 @@ def rows_for(kind, items, wide=False, all_ns=False):
         rows = [[o["metadata"]["name"], (o.get("spec") or {}).get("completions", 1), (o.get("status") or {}).get("succeeded", 0),
                  age(o["metadata"].get("creationTimestamp"))] for o in items]
     elif kind == "Event":
-        h = ["LAST SEEN", "TYPE", "REASON", "OBJECT", "MESSAGE"]
-        rows = [[age(o.get("lastTimestamp")), o.get("type", ""), o.get("reason", ""),
-                 f"{(o.get('involvedObject') or {}).get('kind', '').lower()}/{(o.get('involvedObject') or {}).get('name', '')}",
-                 o.get("message", "")] for o in items]
+        # kubectl 1.9 `printEvent` columns
+        h = ["LAST SEEN", "FIRST SEEN", "COUNT", "NAME", "KIND", "SUBOBJECT", "TYPE", "REASON", "SOURCE", "MESSAGE"]
+        rows = []
+        for o in items:
+            io, src = o.get("involvedObject") or {}, o.get("source") or {}
+            rows.append([age(o.get("lastTimestamp")), age(o.get("firstTimestamp")), o.get("count", 1), io.get("name", ""),
+                         io.get("kind", ""), io.get("fieldPath", ""), o.get("type", ""), o.get("reason", ""),
+                         ", ".join(x for x in (src.get("component", ""), src.get("host", "")) if x),
+                         o.get("message", "")])
     elif kind == "Namespace":
         h = ["NAME", "STATUS", "AGE"]
         rows = [[o["metadata"]["name"], (o.get("status") or {}).get("phase", ""), age(o["metadata"].get("creationTimestamp"))] for o in items]
@@ -496,9 +501,12 @@ def describe(obj, events=(), ctx=None):
         extra = dsc.sections(obj, ctx)
         lines += extra if extra is not None else dsc.fallback(obj)
     if events:
+        # `DescribeEvents`: Type, Reason, Age, From, Message
         lines.append("Events:")
-        rows, h = rows_for("Event", list(events))
-        lines += ["  " + ln for ln in table(rows, h).splitlines()]
+        rows = [[e.get("type", ""), e.get("reason", ""), age(e.get("lastTimestamp")),
+                 ", ".join(x for x in ((e.get("source") or {}).get("component", ""), (e.get("source") or {}).get("host", "")) if x),
+                 e.get("message", "")] for e in events]
+        lines += ["  " + ln for ln in table(rows, ["Type", "Reason", "Age", "From", "Message"]).splitlines()]
     else:
         lines.append("Events:       <none>")
     return "\n".join(lines)
