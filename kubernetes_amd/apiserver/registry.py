@@ -145,6 +145,21 @@ class PodStrategy(Strategy):
                 ers.append(r)
             ns["extendedResources"] = ers
 
+    def prepare_status_update(self, new, old):
+        """`podStatusStrategy.PrepareForUpdate` (pkg/registry/core/pod/strategy.go:184-193): the
+        spec, deletion timestamp and owner references stay the old ones; the rest of the
+        metadata may change — the scheduler writes its `NominatedNodeName` annotation this way
+        (factory.go:1271-1287)."""
+        nm = dict(new.get("metadata") or {})
+        super().prepare_status_update(new, old)
+        md = new["metadata"] = dict(new.get("metadata") or {})
+        for k in ("labels", "annotations"):
+            if k in nm:
+                if nm[k] is None:
+                    md.pop(k, None)
+                else:
+                    md[k] = nm[k]
+
     def validate_update(self, new, old):
         # `ValidatePodUpdate`: images, activeDeadlineSeconds and tolerations only
         return validation.validate_pod_update(new, old) + validation.validate_object_meta_update(new, old)

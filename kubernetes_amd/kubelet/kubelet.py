@@ -50,6 +50,7 @@ _ip_counter = itertools.count(2)
 
 
 BOOTSTRAP_CHECKPOINT = "node.kubernetes.io/bootstrap-checkpoint"
+MIN_KILL_GRACE_SECONDS = 2.0        # kuberuntime minimumGracePeriodInSeconds
 
 
 _REF = __import__("re").compile(r"\$\$|\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
@@ -1542,10 +1543,14 @@ class Kubelet:
         pre = [(name, cid, (by_name[name].get("lifecycle") or {}).get("preStop")) for name, cid in st.containers.items()
                if cid is not None and name in by_name]
         hooks = [(name, cid, h) for name, cid, h in pre if h]
-        if hooks:
+        # kuberuntime_container.go killContainer (:574-599): the grace period is the deletion's
+        # (else the pod's terminationGracePeriodSeconds), minus the preStop hook's run time, and
+        # never below 2 s; grace 0 is this kubelet's internal immediate kill (the reference's
+        # gracePeriodOverride)
+        budget = float(grace if grace is not None else spec.get("terminationGracePeriodSeconds", 30))
+        t_hooks = time.monotonic()
+        if hooks and budget > 0:
             # preStop handlers run (concurrently) within the grace period before the stop signal
-            budget = float(grace if grace is not None else spec.get("terminationGracePeriodSeconds", 30))
-
             async def hook(name, cid, h):
                 ok, msg = await run_probe(rt, st.pod, by_name[name], cid, dict(h, timeoutSeconds=max(budget, 1.0)), st.ip)
                 if not ok:
@@ -1554,6 +1559,8 @@ class Kubelet:
                 await asyncio.wait_for(asyncio.gather(*(hook(*x) for x in hooks)), max(budget, 0.5))
             except asyncio.TimeoutError:
                 pass
+        timeout = 0.0 if budget <= 0 else max(budget - (time.monotonic() - t_hooks), MIN_KILL_GRACE_SECONDS)
+        stops = []
         for name, cid in list(st.containers.items()) + list(st.init_containers.items()):
             if cid is not None:
                 cs = rt.container_status(cid)
@@ -1561,7 +1568,10 @@ class Kubelet:
                     # kuberuntime_container.go killContainer: KillingContainer event
                     self.recorder.event(st.pod, "Normal", "Killing", f"Killing container with id {cid}:Need to kill Pod",
                                         field_path=_field_path(st.pod, {"name": name}))
-                await rt.stop_container(cid, min(float(grace or 0), 2.0))
+                stops.append(rt.stop_container(cid, timeout))
+        if stops:
+            # killContainersWithSyncResult: every container is stopped in parallel
+            await asyncio.gather(*stops)
         if st.sandbox is not None:
             await rt.stop_pod_sandbox(st.sandbox)
         st.terminated = True

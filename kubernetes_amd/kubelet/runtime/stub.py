@@ -9,6 +9,13 @@ makes the container exit with code 1, like a real GPU container crashing at star
 
 Containers may declare a run time with the annotation `kubemark.amd.com/run-seconds` (or a
 `["sleep", N]` command); otherwise they run until stopped.
+
+Stopping honours the grace period the kubelet passes (the pod's deletion grace /
+terminationGracePeriodSeconds, `kuberuntime_container.go:574-599`): a container whose pod
+carries `kubemark.amd.com/stop-seconds: S` keeps running for S seconds after the stop signal —
+a workload draining on SIGTERM — and exits 0 then; when S reaches the grace period it is killed
+at the grace period (137), like a workload that ignores SIGTERM. Without the annotation the stop
+is immediate, as with kubemark's fake docker.
 """
 from __future__ import annotations
 
@@ -20,6 +27,7 @@ import time
 from .base import CREATED, EXITED, RUNNING, ContainerStatus, Runtime, RunContainerOptions
 
 RUN_SECONDS = "kubemark.amd.com/run-seconds"
+STOP_SECONDS = "kubemark.amd.com/stop-seconds"
 
 
 class StubRuntime(Runtime):
@@ -68,8 +76,9 @@ class StubRuntime(Runtime):
             run_s = float(ann)
         elif len(cmd) == 2 and cmd[0] == "sleep":
             run_s = float(cmd[1])
+        stop_s = float((pod["metadata"].get("annotations") or {}).get(STOP_SECONDS) or 0)
         self.meta[cid] = {"sandbox": sid, "pod_uid": pod["metadata"]["uid"], "opts": opts, "run_s": run_s,
-                          "container": container,
+                          "container": container, "stop_s": stop_s,
                           "exec_code": (pod["metadata"].get("annotations") or {}).get("kubemark.amd.com/exec-exit-code", 0)}
         return cid
 
@@ -111,14 +120,22 @@ class StubRuntime(Runtime):
         self._fire_exit(self.meta[cid]["pod_uid"], cid)
 
     async def stop_container(self, cid, timeout):
+        st = self.containers.get(cid)
+        m = self.meta.get(cid) or {}
+        stop_s = m.get("stop_s") or 0.0
+        if st is not None and st.state != EXITED and timeout > 0 and stop_s > 0:
+            # SIGTERM sent: the workload drains for stop_s, or is SIGKILLed at the grace period
+            await asyncio.sleep(min(stop_s, timeout))
+            killed = stop_s >= timeout
+        else:
+            killed = timeout == 0
         h = self._timers.pop(cid, None)
         if h:
             h.cancel()
-        st = self.containers.get(cid)
         if st is not None and st.state != EXITED:
             st.state = EXITED
-            st.exit_code = 137 if timeout == 0 else 0
-            st.reason = "Killed" if timeout == 0 else "Completed"
+            st.exit_code = 137 if killed else 0
+            st.reason = "Killed" if killed else "Completed"
             st.finished_at = time.time()
 
     async def remove_container(self, cid):

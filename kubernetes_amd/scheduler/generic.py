@@ -16,7 +16,13 @@ Differences by design:
     until that node's generation changes. A bind touches one node, so the next pod of the
     class re-evaluates one node instead of all of them. Disabled for pods whose placement
     depends on other nodes' pods (inter-pod affinity) and when extenders are configured;
-  * `percentage_of_nodes_to_score` (later-Kubernetes knob), default 100 = reference behaviour.
+  * `percentage_of_nodes_to_score` (later-Kubernetes knob), default 100 = reference behaviour;
+  * nominated pods (`podFitsOnNode` + `addNominatedPods`, generic_scheduler.go:367-486): a node
+    with queued pods of equal or higher priority nominated to it (preemptors waiting for their
+    victims to terminate) is checked twice — with those nominees accounted, including the device
+    IDs they would take, and without — and bypasses the equivalence cache; the device binding
+    comes from the first pass, so GPUs freed for a preemptor are never handed to a lower-priority
+    pod. Nodes without such nominees take the usual path.
 """
 from __future__ import annotations
 
@@ -29,6 +35,7 @@ from . import predicates as P
 from . import priorities as PR
 from .cache import PodInfo, SchedulerCache
 from .topology import POLICY_ANNOTATION, PREFERRED, Request, allocate, fast_path, feasible
+from .whatif import WhatIfCache, nominated_view
 
 log = logging.getLogger("scheduler")
 
@@ -304,6 +311,7 @@ class GenericScheduler:
         self.ecache_hits = 0
         self.ecache_misses = 0
         self.prefer = None   # node name -> bool: a scheduler shard's own nodes win among feasible ones
+        self.queue = None    # SchedulingQueue: its nominated pods are accounted in the fit check
 
     def num_feasible_to_find(self, n):
         if self.pct >= 100 or n < 100:
@@ -373,8 +381,30 @@ class GenericScheduler:
         topo = ctx.topo_scores
         f_append, r_append = fnodes.append, raws.append
         order = nodes[start:] + nodes[:start] if start else nodes
+        nom = self.queue.nominated_pods if self.queue is not None else None
         for ni in order:
             checked += 1
+            if nom:
+                nominees = nom.get(ni.name)
+                view = nominated_view(pod, ni, nominees) if nominees else None
+                if view is not None:
+                    vctx = CycleContext(WhatIfCache(self.cache, ni, view), pod, with_affinity=True) \
+                        if affinity_sensitive else ctx
+                    reason, score, binding = self._fit(pod, pi, view, vctx, preds, need, reqs, policy)
+                    if reason is None:
+                        reason = self._fit(pod, pi, ni, ctx, preds, need, reqs, policy)[0]
+                    if reason:
+                        failed[ni.name] = reason
+                        continue
+                    if binding is not None:
+                        bindings[ni.name] = binding
+                    if score is not None:
+                        ctx.topo_scores[ni.name] = score
+                    fnodes.append(ni)
+                    raws.append(tuple(fn(pod, pi, ni, ctx) for _, _, fn, _, _ in prios))
+                    if len(fnodes) >= want:
+                        break
+                    continue
             if ec_get is not None:
                 ent = ec_get(ni.name)
                 if ent is not None and ent[0] == ni.generation:
@@ -450,13 +480,32 @@ class GenericScheduler:
                 for name, s in ext.prioritize(pod, fnodes).items():
                     scores[name] = scores.get(name, 0) + s
             host = self.select_host(scores, fnodes)
+        if host in bindings:
+            return host, bindings[host]
         if fast:
             # materialise the device binding for the chosen node only
             binding, _, reason = allocate(reqs, self.cache.nodes[host].er, policy)
             if binding is None:  # cannot happen: feasible() and allocate() agree
                 raise FitError(pod, n, {host: reason})
             return host, binding
-        return host, bindings.get(host, {})
+        return host, {}
+
+    @staticmethod
+    def _fit(pod, pi, ni, ctx, preds, need, reqs, policy):
+        """(reason, topology score, device binding) of one node, device binding materialised."""
+        for rn, cnt in need.items():
+            if ni.er.free_count(rn) < cnt:
+                return f"Insufficient {rn}", None, None
+        for _, fn in preds:
+            reason = fn(pod, pi, ni, ctx)
+            if reason:
+                return reason, None, None
+        if reqs:
+            binding, score, reason = allocate(reqs, ni.er, policy)
+            if binding is None:
+                return reason, None, None
+            return None, score, binding
+        return None, None, None
 
     @staticmethod
     def _combine(prios, nodes, raws):

@@ -69,6 +69,7 @@ class Scheduler:
             self.cache.failure_domains = tuple(failure_domains)
         self.queue = SchedulingQueue()
         self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
+        self.algo.queue = self.queue
         self.shard_index, self.shard_count = shard_index, shard_count
         self.partitioned = shard_count > 1
         self.rehandoff_period = rehandoff_period
@@ -108,6 +109,9 @@ class Scheduler:
         self.sc_informer = Informer(client, "storageclasses")
         # services: SelectorSpread / ServiceSpreading / ServiceAffinity / ServiceAntiAffinity
         self.svc_informer = Informer(client, "services")
+        # preemption: PDB-aware victim selection (the reference scheduler cache's ListPDBs)
+        self.pdbs: dict[str, dict] = {}
+        self.pdb_informer = Informer(client, "poddisruptionbudgets") if preemption else None
 
     # -- informer handlers -------------------------------------------------
     def _responsible(self, pod):
@@ -134,6 +138,10 @@ class Scheduler:
         if (pod.get("spec") or {}).get("nodeName") or pod["metadata"].get("deletionTimestamp"):
             self._rehandoff_delay.pop(ns_name(pod), None)
 
+    def _on_owned_pod_add(self, pod):
+        self.cache.add_pod(pod)
+        self.queue.assigned_pod_added(pod)
+
     def _on_owned_pod_delete(self, pod):
         self.cache.remove_pod(pod)
         self.queue.move_all_to_active()   # capacity was freed
@@ -152,7 +160,7 @@ class Scheduler:
                 continue
             inf = Informer(self.client, "pods", field_selector=f"spec.nodeName={name},status.phase!=Succeeded,"
                                                                "status.phase!=Failed")
-            inf.add_handler(self.cache.add_pod, lambda old, new: self.cache.add_pod(new), self._on_owned_pod_delete)
+            inf.add_handler(self._on_owned_pod_add, lambda old, new: self._on_owned_pod_add(new), self._on_owned_pod_delete)
             self.owned[name] = inf
             inf.start()
             spawn(self._node_ready(name, inf))
@@ -233,6 +241,7 @@ class Scheduler:
     def _on_pod_add(self, pod):
         if (pod.get("spec") or {}).get("nodeName"):
             self.cache.add_pod(pod)
+            self.queue.assigned_pod_added(pod)
             return
         if self._responsible(pod) and not pod["metadata"].get("deletionTimestamp"):
             self.queue.add(pod)
@@ -243,6 +252,7 @@ class Scheduler:
             if not (old.get("spec") or {}).get("nodeName"):
                 self.queue.delete(old)
             self.cache.add_pod(new)
+            self.queue.assigned_pod_added(new)
             return
         if self._responsible(new):
             if new["metadata"].get("deletionTimestamp"):
@@ -296,6 +306,14 @@ class Scheduler:
         self.sc_informer.add_handler(put(vl.classes), put(vl.classes), drop(vl.classes))
         self.svc_informer.add_handler(self.cache.set_service, lambda old, new: self.cache.set_service(new),
                                       self.cache.remove_service)
+        if self.pdb_informer is not None:
+            self.pdb_informer.add_handler(put(self.pdbs, False), put(self.pdbs, False), drop(self.pdbs))
+
+    def _aux_informers(self):
+        out = [self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer]
+        if self.pdb_informer is not None:
+            out.append(self.pdb_informer)
+        return out
 
     # -- scheduling loop ---------------------------------------------------------
     async def run(self, metrics_port=None, metrics_address="127.0.0.1"):
@@ -309,7 +327,7 @@ class Scheduler:
             self.node_informer.add_handler(self._on_node_add, self._on_node_update, self._on_node_delete)
             self.pod_informer.add_handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete)
         self._volume_handlers()
-        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer):
+        for inf in self._aux_informers():
             inf.start()
         self.node_informer.start()
         await self.node_informer.wait_synced(60)
@@ -317,7 +335,7 @@ class Scheduler:
             t = time.monotonic()
             while len(self._owned_ready) < len(self.owned) and time.monotonic() - t < 60:
                 await asyncio.sleep(0.01)
-        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer):
+        for inf in self._aux_informers():
             await inf.wait_synced(60)
         self.pod_informer.start()
         await self.pod_informer.wait_synced(60)
@@ -363,7 +381,7 @@ class Scheduler:
             if self.update_unschedulable_status:
                 spawn(self._set_unschedulable(pod, str(e)))
             if self.preemption:
-                self._try_preempt(pod, pi)
+                self._try_preempt(pod, pi, e)
             return None
         except Exception as e:  # pragma: no cover - defensive
             log.exception("scheduling %s failed", ns_name(pod))
@@ -443,33 +461,59 @@ class Scheduler:
         self.queue.conflict_backoff.forget(ns_name(pod))
         self.recorder.event(pod, "Normal", "Scheduled", f"Successfully assigned {md['name']} to {host}")
 
-    def _try_preempt(self, pod, pi):
-        """scheduler.go preempt(): pick a node + minimal lower-priority victims, nominate the
-        node on the preemptor and delete the victims; the preemptor is retried when the
-        victims' deletions free their resources (pod delete events re-activate the queue)."""
+    def _try_preempt(self, pod, pi, fit_error=None):
+        """scheduler.go preempt() (:209-253): pick a node and the minimal lower-priority victims
+        (`preemption.preempt`), then — in order — write the `NominatedNodeName` annotation on
+        the preemptor, delete the victims, and clear the nominations of lower-priority pods
+        nominated to that node. The preemptor is retried when the victims' deletions free their
+        resources (pod delete events re-activate the queue); meanwhile the queue's nominated
+        index holds the freed devices for it."""
         from .preemption import preempt
         try:
-            node, victims = preempt(self.algo, pod, pi)
+            node, victims, clear = preempt(self.algo, pod, pi, fit_error, list(self.pdbs.values()), self.queue)
         except Exception:  # pragma: no cover - defensive
             log.exception("preemption for %s failed", ns_name(pod))
             return
-        if node is None or not victims:
-            return
-        self.m_preemptions.inc()
-        md = pod["metadata"]
-        spawn(self._nominate(pod, node))
-        for v in victims:
-            vmd = v["metadata"]
-            self.recorder.event(v, "Normal", "Preempted", f"by {md.get('namespace')}/{md['name']} on node {node}")
-            spawn(self._delete_victim(vmd.get("namespace"), vmd["name"]))
+        if node is not None:
+            if victims:
+                self.m_preemptions.inc()
+            # index the nomination now; the informer's copy of the annotated pod replaces it
+            self.queue.nominate(pod, node)
+        if node is not None or clear:
+            spawn(self._preempt_writes(pod, node, victims, clear))
 
-    async def _nominate(self, pod, node):
+    async def _preempt_writes(self, pod, node, victims, clear):
+        md = pod["metadata"]
+        if node is not None:
+            if not await self._set_nomination(pod, node):
+                self.queue.nominate(pod, "")
+                return
+            for v in victims:
+                vmd = v["metadata"]
+                if not await self._delete_victim(vmd.get("namespace"), vmd["name"]):
+                    return
+                self.recorder.event(v, "Normal", "Preempted", f"by {md.get('namespace')}/{md['name']} on node {node}")
+        for p in clear:
+            # a failure here is not critical (scheduler.go:245-251)
+            self.queue.nominate(p, "")
+            await self._set_nomination(p, "")
+
+    async def _set_nomination(self, pod, node):
+        """podPreemptor.UpdatePodAnnotations / RemoveNominatedNodeAnnotation
+        (factory.go:1271-1300): a merge patch of the annotation through pods/status; "" clears."""
+        from .preemption import NOMINATED_ANNOTATION
         md = pod["metadata"]
         try:
-            await self.client.patch("pods", md["name"], {"status": {"nominatedNodeName": node}}, md.get("namespace"),
-                                    "merge", "status")
-        except Exception as e:
-            log.debug("could not nominate %s: %s", md["name"], e)
+            await self.client.patch("pods", md["name"], {"metadata": {"annotations": {NOMINATED_ANNOTATION: node}}},
+                                    md.get("namespace"), "merge", "status")
+            return True
+        except APIStatusError as e:
+            if not is_not_found(e):
+                log.warning("could not %s nominated node of %s/%s: %s", "set" if node else "clear",
+                            md.get("namespace"), md["name"], e)
+        except Exception as e:  # noqa: BLE001 - connection errors: the pod is retried anyway
+            log.warning("could not update nominated node of %s/%s: %s", md.get("namespace"), md["name"], e)
+        return False
 
     async def _delete_victim(self, ns, name):
         try:
@@ -477,6 +521,11 @@ class Scheduler:
         except APIStatusError as e:
             if not is_not_found(e):
                 log.warning("deleting preemption victim %s/%s: %s", ns, name, e)
+                return False
+        except Exception as e:  # noqa: BLE001
+            log.warning("deleting preemption victim %s/%s: %s", ns, name, e)
+            return False
+        return True
 
     async def _set_unschedulable(self, pod, msg):
         md = pod["metadata"]
@@ -509,7 +558,7 @@ class Scheduler:
         self.node_informer.stop()
         for inf in self.owned.values():
             inf.stop()
-        for inf in (self.pvc_informer, self.pv_informer, self.sc_informer, self.svc_informer):
+        for inf in self._aux_informers():
             inf.stop()
         self.recorder.stop()
         if self.http:

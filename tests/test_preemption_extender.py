@@ -42,12 +42,12 @@ def test_victims_are_minimal_and_respect_hives():
     # a priority-10 pod may not evict priority-50 pods, and 2 low pods suffice
     mid = gpu_pod("m", 2)
     mid["spec"]["priority"] = 10
-    n, v = preempt(gs, mid, PodInfo(mid))
+    n, v, _ = preempt(gs, mid, PodInfo(mid))
     assert n == "n0" and len(v) == 2 and all(x["spec"]["priority"] == 0 for x in v)
     # an equal-priority pod preempts nothing
     same = gpu_pod("s", 1)
     same["spec"]["priority"] = 0
-    assert preempt(gs, same, PodInfo(same)) == (None, [])
+    assert preempt(gs, same, PodInfo(same)) == (None, [], [])
 
 
 def test_preemption_end_to_end(run):
