@@ -221,3 +221,39 @@ def tolerates(tolerations, taint) -> bool:
         if op == "Exists" or t.get("value", "") == taint.get("value", ""):
             return True
     return False
+
+
+_VOLUME_SECRET_REFS = ("cephfs", "flexVolume", "rbd", "scaleIO", "iscsi", "storageos")
+
+
+def pod_secret_names(pod) -> list[str]:
+    """Every secret a pod references, in `VisitPodSecretNames` order
+    (`pkg/api/v1/pod/util.go:58-145`): image pull secrets; envFrom / secretKeyRef of init
+    containers then containers; secret, projected, azureFile and the secretRef of cephfs /
+    flexVolume / rbd / scaleIO / iscsi / storageos volumes."""
+    spec = pod.get("spec") or {}
+    out = [r.get("name", "") for r in spec.get("imagePullSecrets") or ()]
+    for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+        for ef in c.get("envFrom") or ():
+            if ef.get("secretRef") is not None:
+                out.append(ef["secretRef"].get("name", ""))
+        for e in c.get("env") or ():
+            ref = (e.get("valueFrom") or {}).get("secretKeyRef")
+            if ref is not None:
+                out.append(ref.get("name", ""))
+    for v in spec.get("volumes") or ():
+        if v.get("secret") is not None:
+            out.append(v["secret"].get("secretName", ""))
+        elif v.get("projected") is not None:
+            out += [s["secret"].get("name", "") for s in v["projected"].get("sources") or () if s.get("secret") is not None]
+        elif v.get("azureFile") is not None:
+            if v["azureFile"].get("secretName"):
+                out.append(v["azureFile"]["secretName"])
+        else:
+            for k in _VOLUME_SECRET_REFS:
+                if v.get(k) is not None:
+                    ref = v[k].get("secretRef")
+                    if ref is not None:
+                        out.append(ref.get("name", ""))
+                    break
+    return out

@@ -103,7 +103,7 @@ DEFAULT_PLUGINS = [
 
 
 def new_chain(names, server=None, configs=None):
-    from . import estimation, plugins, security  # noqa: F401 - registers built-ins
+    from . import estimation, limitranger, plugins, security  # noqa: F401 - registers built-ins
     configs = configs or {}
     out = []
     for n in names:

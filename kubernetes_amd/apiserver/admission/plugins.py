@@ -6,7 +6,8 @@
   * ResourceQuota — also counts pod-level ExtendedResources, closing the reference's gap
     where GPU quota went unenforced after ResourceV2 stripped container limits
     (`pkg/quota/evaluator/core/pods.go:299-335`).
-  * NamespaceLifecycle, LimitRanger, ServiceAccount, DefaultTolerationSeconds, Priority,
+  * LimitRanger — `limitranger.py`.
+  * NamespaceLifecycle, ServiceAccount, DefaultTolerationSeconds, Priority,
     ExtendedResourceToleration, NodeRestriction, AlwaysPullImages, AlwaysAdmit, AlwaysDeny,
     PodNodeSelector — per `plugin/pkg/admission/*`.
 """
@@ -138,37 +139,79 @@ class ValidatingAdmissionWebhook(Plugin):
 
 
 SA_MOUNT_PATH = "/var/run/secrets/kubernetes.io/serviceaccount"
+ENFORCE_MOUNTABLE_SECRETS = "kubernetes.io/enforce-mountable-secrets"
+MIRROR_POD_ANNOTATION = "kubernetes.io/config.mirror"
+
+
+def _parse_bool(v) -> bool:
+    """strconv.ParseBool (an unparsable value is false)."""
+    return str(v) in ("1", "t", "T", "TRUE", "true", "True")
 
 
 @register
 class ServiceAccount(Plugin):
-    """`plugin/pkg/admission/serviceaccount/admission.go`: the pod runs as `default` unless it
-    names an account, and — unless `automountServiceAccountToken` is false on the pod or, when
-    the pod does not say, on the account — gets the account's API token secret as a volume
-    mounted read-only at /var/run/secrets/kubernetes.io/serviceaccount in every container.
-    Unlike the reference (which rejects the pod until the token controller has made a token),
-    a pod whose account or token does not exist yet is admitted without the mount: a cluster
-    without a token controller (no --service-account-private-key-file) still runs pods."""
+    """`plugin/pkg/admission/serviceaccount/admission.go`:
+      * the pod runs as `default` unless it names an account (:158-161);
+      * unless `automountServiceAccountToken` is false on the pod or, when the pod does not say,
+        on the account (:245-256), the account's first referenced API token secret is a volume
+        mounted read-only at /var/run/secrets/kubernetes.io/serviceaccount in every container
+        and init container that has nothing mounted there (:402-490);
+      * a pod without `imagePullSecrets` gets the account's (:175-178);
+      * an account annotated `kubernetes.io/enforce-mountable-secrets: "true"` limits the pod to
+        the secrets it references — secret volumes, `secretKeyRef` env of containers and init
+        containers, and image pull secrets against the account's `imagePullSecrets`
+        (:220-224, :258-271, :352-400);
+      * mirror pods are not mutated and may reference neither an account nor a secret
+        (:151-156, :198-212).
+    The reference rejects the pod until the account (`DeniesInvalidServiceAccount`) and its
+    token (`RequireAPIToken`, a 504 ServerTimeout) exist; here both are plugin config
+    (`requireServiceAccount`, `requireAPIToken`, default off): by default a pod whose account
+    or token does not exist yet is admitted without the mount and without the account's pull
+    secrets, so a cluster without the service-account and token controllers (no
+    --service-account-private-key-file) still runs pods."""
     name = "ServiceAccount"
     operations = (CREATE,)
 
-    def admit(self, a):
-        if a.resource != "pods" or a.subresource:
-            return
-        spec = a.obj.setdefault("spec", {})
-        name = spec.setdefault("serviceAccountName", "default")
-        if spec.get("automountServiceAccountToken") is False or not self.server:
-            return
-        if (a.obj.get("metadata") or {}).get("annotations", {}).get("kubernetes.io/config.mirror"):
-            return                                   # mirror pods do not reference API objects
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        self.require_account = bool(self.config.get("requireServiceAccount", False))
+        self.require_token = bool(self.config.get("requireAPIToken", False))
+
+    def _forbid(self, a, msg):
+        md = a.obj.get("metadata") or {}
+        return AdmissionError(f'pods "{md.get("name") or md.get("generateName", "")}" is forbidden: {msg}')
+
+    def _account(self, namespace, name):
         try:
-            sa = self.server.get_object("serviceaccounts", a.namespace, name)
+            return self.server.get_object("serviceaccounts", namespace, name)
         except RuntimeError:
+            return None
+
+    def admit(self, a):
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
             return
+        if ((a.obj.get("metadata") or {}).get("annotations") or {}).get(MIRROR_POD_ANNOTATION) is not None:
+            return                                   # mirror pods are only validated
+        spec = a.obj.setdefault("spec", {})
+        if not spec.get("serviceAccountName"):
+            spec["serviceAccountName"] = "default"
+        if not self.server:
+            return
+        sa = self._account(a.namespace, spec["serviceAccountName"])
         if sa is None:
+            if self.require_account:
+                raise self._forbid(a, f"error looking up service account {a.namespace}/{spec['serviceAccountName']}: "
+                                      f"serviceaccount \"{spec['serviceAccountName']}\" not found")
             return
-        if spec.get("automountServiceAccountToken") is None and sa.get("automountServiceAccountToken") is False:
-            return
+        automount = spec.get("automountServiceAccountToken")
+        if automount is None:
+            automount = sa.get("automountServiceAccountToken")
+        if automount is not False:
+            self._mount_token(a, sa, spec)
+        if not spec.get("imagePullSecrets") and sa.get("imagePullSecrets"):
+            spec["imagePullSecrets"] = [dict(r) for r in sa["imagePullSecrets"]]
+
+    def _mount_token(self, a, sa, spec):
         token = None
         for ref in sa.get("secrets") or ():
             try:
@@ -179,18 +222,79 @@ class ServiceAccount(Plugin):
                 token = sec["metadata"]["name"]
                 break
         if token is None:
+            if self.require_token:
+                raise AdmissionError(f"No API token found for service account \"{sa['metadata']['name']}\", retry after "
+                                     "the token is automatically created and added to the service account",
+                                     504, "ServerTimeout")
             return
-        vols = spec.setdefault("volumes", [])
+        vols = spec.get("volumes") or []
         vol = next((v["name"] for v in vols if (v.get("secret") or {}).get("secretName") == token), None)
+        has_volume = vol is not None
         if vol is None:
             vol = token
-            # written as defaulting would leave it (admission runs after defaulting): an update
-            # of the pod then carries the same volume and is not refused as a spec change
-            vols.append({"name": vol, "secret": {"secretName": token, "defaultMode": 0o644}})
+            if any(v.get("name") == vol for v in vols):
+                vol = f"{token}-{new_uid()[:5]}"     # names.SimpleNameGenerator
+        needs = False
         for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
             mounts = c.setdefault("volumeMounts", [])
             if not any(m.get("mountPath") == SA_MOUNT_PATH for m in mounts):
                 mounts.append({"name": vol, "readOnly": True, "mountPath": SA_MOUNT_PATH})
+                needs = True
+        if needs and not has_volume:
+            # written as defaulting would leave it (admission runs after defaulting): an update
+            # of the pod then carries the same volume and is not refused as a spec change
+            vols.append({"name": vol, "secret": {"secretName": token, "defaultMode": 0o644}})
+            spec["volumes"] = vols
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
+            return
+        md = a.obj.get("metadata") or {}
+        spec = a.obj.get("spec") or {}
+        if (md.get("annotations") or {}).get(MIRROR_POD_ANNOTATION) is not None:
+            if spec.get("serviceAccountName"):
+                raise AdmissionError(f'pods "{md.get("name", "")}" is forbidden: a mirror pod may not reference '
+                                     "service accounts")
+            if core.pod_secret_names(a.obj):
+                raise AdmissionError(f'pods "{md.get("name", "")}" is forbidden: a mirror pod may not reference secrets')
+            return
+        if not self.server or not spec.get("serviceAccountName"):
+            return
+        sa = self._account(a.namespace, spec["serviceAccountName"])
+        if sa is None or not _parse_bool((sa["metadata"].get("annotations") or {}).get(ENFORCE_MOUNTABLE_SECRETS)):
+            return
+        err = limit_secret_references(sa, a.obj)
+        if err:
+            raise AdmissionError(f'pods "{md.get("name") or md.get("generateName", "")}" is forbidden: {err}')
+
+
+def limit_secret_references(sa, pod):
+    """serviceaccount/admission.go:352-400 — the first secret reference the account does not
+    allow, as the reference's error message, or None."""
+    spec = pod.get("spec") or {}
+    mountable = {s.get("name") for s in sa.get("secrets") or ()}
+    sa_name = sa["metadata"]["name"]
+    for v in spec.get("volumes") or ():
+        src = v.get("secret")
+        if src is None:
+            continue
+        if src.get("secretName") not in mountable:
+            return (f'volume with secret.secretName="{src.get("secretName", "")}" is not allowed because service '
+                    f"account {sa_name} does not reference that secret")
+    for kind, ctrs in (("init container", spec.get("initContainers")), ("container", spec.get("containers"))):
+        for c in ctrs or ():
+            for env in c.get("env") or ():
+                ref = (env.get("valueFrom") or {}).get("secretKeyRef")
+                if ref is not None and ref.get("name") not in mountable:
+                    return (f'{kind} {c.get("name", "")} with envVar {env.get("name", "")} referencing '
+                            f'secret.secretName="{ref.get("name", "")}" is not allowed because service account '
+                            f"{sa_name} does not reference that secret")
+    pull = {s.get("name") for s in sa.get("imagePullSecrets") or ()}
+    for i, ref in enumerate(spec.get("imagePullSecrets") or ()):
+        if ref.get("name") not in pull:
+            return (f'imagePullSecrets[{i}].name="{ref.get("name", "")}" is not allowed because service account '
+                    f"{sa_name} does not reference that imagePullSecret")
+    return None
 
 
 @register
@@ -268,35 +372,6 @@ class Priority(Plugin):
         if pc is None:
             raise AdmissionError(f"no PriorityClass with name {pcn} was found", 403)
         spec["priority"] = int(pc.get("value", 0))
-
-
-@register
-class LimitRanger(Plugin):
-    """Applies Container default requests/limits from LimitRange objects and enforces max."""
-    name = "LimitRanger"
-    operations = (CREATE, UPDATE)
-
-    def admit(self, a):
-        if a.resource != "pods" or a.subresource or not self.server:
-            return
-        lrs = self.server.list_objects("limitranges", a.namespace)
-        if not lrs:
-            return
-        for lr in lrs:
-            for item in (lr.get("spec") or {}).get("limits") or ():
-                if item.get("type") != "Container":
-                    continue
-                for c in a.obj.get("spec", {}).get("containers") or ():
-                    res = c.setdefault("resources", {})
-                    lim = res.setdefault("limits", {})
-                    req = res.setdefault("requests", {})
-                    for k, v in (item.get("default") or {}).items():
-                        lim.setdefault(k, v)
-                    for k, v in (item.get("defaultRequest") or {}).items():
-                        req.setdefault(k, v)
-                    for k, v in (item.get("max") or {}).items():
-                        if k in lim and parse_quantity(str(lim[k])) > parse_quantity(str(v)):
-                            raise AdmissionError(f"maximum {k} usage per Container is {v}, but limit is {lim[k]}")
 
 
 @register

@@ -9,6 +9,8 @@ from __future__ import annotations
 import csv
 from dataclasses import dataclass, field
 
+from ..api import core
+
 
 @dataclass
 class User:
@@ -157,16 +159,7 @@ class NodeAuthorizer:
             if ns != a.namespace:
                 continue
             if a.resource == "secrets":
-                names = {v["secret"].get("secretName") for v in sp.get("volumes") or () if "secret" in v}
-                names |= {r.get("name") for r in sp.get("imagePullSecrets") or ()}
-                for c in (sp.get("containers") or []) + (sp.get("initContainers") or []):
-                    for e in c.get("env") or ():
-                        names.add(((e.get("valueFrom") or {}).get("secretKeyRef") or {}).get("name"))
-                    for ef in c.get("envFrom") or ():
-                        names.add((ef.get("secretRef") or {}).get("name"))
-                for v in sp.get("volumes") or ():
-                    for src in (v.get("projected") or {}).get("sources") or ():
-                        names.add((src.get("secret") or {}).get("name"))
+                names = set(core.pod_secret_names(p))
             elif a.resource == "configmaps":
                 names = {(v.get("configMap") or {}).get("name") for v in sp.get("volumes") or ()}
                 for c in (sp.get("containers") or []) + (sp.get("initContainers") or []):
