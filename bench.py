@@ -376,6 +376,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     # request-issuing helpers are load generator CPU, reported beside the rank's own
     hollow_pids += [("density_clients", p.pid) for p in (runner.pool.procs if runner.pool else ())]
     cp0 = _cp_cpu(list(cp_procs) + hollow_pids)
+    load0 = os.getloadavg()
     my0 = time.process_time()
     t_start = time.monotonic()
     t0 = time.perf_counter()
@@ -389,6 +390,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
     elapsed = time.perf_counter() - t0
     my_cpu = time.process_time() - my0
     cp1 = _cp_cpu(list(cp_procs) + hollow_pids)
+    load1 = os.getloadavg()
     lat = [x for r in results for x in r["latencies"]]
     t_end = time.monotonic()
     stats = {"elapsed": elapsed, "lat": lat, "pods": sum(r["pods"] for r in results),
@@ -404,6 +406,7 @@ async def rank_main(args, d: Dist, url, cp_procs=()):
              "payload_failures": (psrv.failures if psrv else sum(getattr(k.runtime, "payload_failures", 0) for k in hollow.nodes)
                                   if hollow or psrv else 0),
              "cpu_s": my_cpu,
+             "loadavg": {"before": [round(x, 2) for x in load0], "after": [round(x, 2) for x in load1]},
              "cp_cpu_s": {k: cp1.get(k, 0.0) - cp0.get(k, 0.0) for k in cp1}}
     await runner.stop()
     # secondary workload (outside the timed region, not part of `value`): 4-GPU pods that must
@@ -522,6 +525,9 @@ def main():
                     help="API server processes over one native store (0 = auto from the CPU budget)")
     ap.add_argument("--xgmi4-steps", type=int, default=2,
                     help="untimed secondary steps of 4-GPU xGMI-hive pods (0 = skip)")
+    ap.add_argument("--topology-pods", type=int, default=4000,
+                    help="untimed secondary: mixed 1/2/4-GPU pod stream through the real scheduler on the real "
+                         "8xMI355X node shape and its CPX variant (kubemark.topology_stream; 0 = skip)")
     ap.add_argument("--step-timeout", type=float, default=120.0, help="fail (with diagnostics) if a step stalls")
     ap.add_argument("--client-procs", type=int, default=0,
                     help="helper processes per rank that issue the density creates/deletes (0 = the rank itself)")
@@ -630,6 +636,18 @@ def main():
                                 **{c: sum(s["cp_cpu_s"].get(c, 0.0) for s in allstats)
                                    for c in ("apiserver", "scheduler", "store", "hollow", "density_clients")}).items()},
     }
+    # host contention context for `value` (the lease shares its host): 1/5/15-min load averages
+    # around the timed region and the CPUs this job may use
+    out["host"] = {"cpus": cpu_budget(), "loadavg_before": allstats[0]["loadavg"]["before"],
+                   "loadavg_after": allstats[0]["loadavg"]["after"]}
+    if args.topology_pods:
+        # secondary, after the timed region and not part of `value`: fragmentation / NUMA fit /
+        # multi-GPU wait on the real node shape (one 8-package hive) and CPX, against the
+        # reference's spreading + first-N placement on the same seeded stream
+        from kubernetes_amd.kubemark import topology_stream
+        t = time.perf_counter()
+        out["topology_stream"] = topology_stream.run(16, args.topology_pods)
+        out["topology_stream"]["wall_s"] = round(time.perf_counter() - t, 2)
     print(json.dumps(out), flush=True)
 
 

@@ -18,7 +18,14 @@ Two workloads, as in the reference:
     RSS ≤ 200 MiB), plus kubelet CPU-seconds spent per started pod;
   * `--runtime remote`: the kubelet talks CRI to a separate `kamd-cri` process (the reference's
     dockershim/docker split), whose CPU and RSS are tracked too (thresholds p50 ≤ 0.40 / p95 ≤
-    0.60 cores, RSS ≤ 500 MiB, `density_test.go:76-83`).
+    0.60 cores, RSS ≤ 500 MiB, `density_test.go:76-83`);
+  * `--gpu-pods N` (MI355X): the real `amd.com/gpu` device plugin runs as its own process on the
+    node's GPUs (AMD SMI), and with the background pods running N pods requesting one GPU each
+    run the HIP `vector_add` kernel (`kubernetes-amd/hip-vector-add`) through ResourceV2, the
+    scheduler's device binding, the DeviceManager and kamd-runc's device injection — first one
+    after the other (create → Running and create → Succeeded per pod, the sequential SLO applied
+    to create → Running), then all N at once (each waits for the GPU the previous one frees:
+    the makespan and per-pod completion percentiles).
 
     python -m kubernetes_amd.kubemark.node_density --batch 10 --sequential 10 --background 50
 """
@@ -91,6 +98,85 @@ def _pod(name, sleep=3600):
                      "containers": [{"name": "c", "image": "busybox", "command": ["sleep", str(sleep)]}]}}
 
 
+def _gpu_pod(name):
+    from ..api import core
+    return {"metadata": {"name": name, "labels": {"density": "gpu"}},
+            "spec": {"restartPolicy": "Never", "terminationGracePeriodSeconds": 1,
+                     "containers": [{"name": "vector-add", "image": "kubernetes-amd/hip-vector-add",
+                                     "resources": {"limits": {core.AMD_GPU: "1"}}}]}}
+
+
+async def _wait_phases(client, ns, names, phases, timeout):
+    """{name: {phase: first time observed}} for the given phases, until every name reached the
+    last one (or failed) or `timeout`."""
+    seen = {n: {} for n in names}
+    last = phases[-1]
+    lst = await client.list("pods", ns)
+    now = time.monotonic()
+    for p in lst["items"]:
+        ph = (p.get("status") or {}).get("phase")
+        if p["metadata"]["name"] in seen and ph in phases:
+            seen[p["metadata"]["name"]].setdefault(ph, now)
+    w = await client.watch("pods", ns, lst["metadata"]["resourceVersion"])
+    end = time.monotonic() + timeout
+
+    def done():
+        return all(last in v or "Failed" in v for v in seen.values())
+
+    async def drain():
+        if done():
+            return
+        async for _, p in w:
+            n = p["metadata"]["name"]
+            ph = (p.get("status") or {}).get("phase")
+            if n in seen and (ph in phases or ph == "Failed"):
+                t = time.monotonic()
+                seen[n].setdefault(ph, t)
+                if ph in (last, "Failed"):
+                    for q in phases:                # a phase the watch skipped counts as reached then
+                        seen[n].setdefault(q, t)
+            if done():
+                return
+    try:
+        await asyncio.wait_for(drain(), max(0.1, end - time.monotonic()))
+    except asyncio.TimeoutError:
+        pass
+    finally:
+        w.close()
+    return seen
+
+
+async def _gpu_phase(c, ns, n, timeout):
+    """Sequential then concurrent single-GPU HIP pods (see the module docstring)."""
+    seq_run, seq_done, failed = [], [], []
+    for i in range(n):
+        name = f"gpu-seq-{i}"
+        t0 = time.monotonic()
+        await c.create("pods", _gpu_pod(name), ns)
+        seen = (await _wait_phases(c, ns, [name], ("Running", "Succeeded"), timeout))[name]
+        if "Failed" in seen or "Succeeded" not in seen:
+            failed.append(name)
+        else:
+            seq_run.append(seen["Running"] - t0)
+            seq_done.append(seen["Succeeded"] - t0)
+        await c.delete("pods", name, ns, grace_period=0)
+    names = [f"gpu-batch-{i}" for i in range(n)]
+    t0 = time.monotonic()
+    for name in names:
+        await c.create("pods", _gpu_pod(name), ns)
+    seen = await _wait_phases(c, ns, names, ("Running", "Succeeded"), timeout * max(1, n))
+    done = [seen[x]["Succeeded"] - t0 for x in names if "Succeeded" in seen[x] and "Failed" not in seen[x]]
+    failed += [x for x in names if "Succeeded" not in seen[x] or "Failed" in seen[x]]
+    return {"pods": n, "failed": failed,
+            "sequential": {"running_p50_s": round(pct(seq_run, .5), 3), "running_p90_s": round(pct(seq_run, .9), 3),
+                           "running_p99_s": round(pct(seq_run, .99), 3),
+                           "succeeded_p50_s": round(pct(seq_done, .5), 3),
+                           "succeeded_p99_s": round(pct(seq_done, .99), 3)},
+            "batch": {"makespan_s": round(max(done), 3) if len(done) == n else float("inf"),
+                      "succeeded_p50_s": round(pct(done, .5), 3), "succeeded_p99_s": round(pct(done, .99), 3),
+                      "gpu_pods_per_s": round(n / max(done), 2) if len(done) == n and max(done) > 0 else 0.0}}
+
+
 async def _wait_running(client, ns, names, timeout):
     """name -> time observed Running (watch), within timeout."""
     seen = {}
@@ -131,7 +217,7 @@ async def _drain_pods(url):
 
 
 async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0, monitor=10.0, period=1.0,
-              runtime="process"):
+              runtime="process", gpu_pods=0):
     tmp = tempfile.mkdtemp(prefix="kamd-node-density-")
     pf = os.path.join(tmp, "api.port")
     procs = [_spawn(["kubernetes_amd.cmd.apiserver", "--port", "0", "--port-file", pf], tmp, "apiserver")]
@@ -164,15 +250,21 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
                      "--kube-api-qps", "100", "--kube-api-burst", "200", "--registry-qps", "0"] + rt_args,
                     tmp, "kubelet")
         procs.append(kl)
+        plugin = None
+        if gpu_pods:
+            plugin = _spawn(["kubernetes_amd.cmd.device_plugin", "--plugins-dir",
+                             os.path.join(tmp, "kubelet", "device-plugin", "plugins")], tmp, "device-plugin")
+            procs.append(plugin)
         c = Client(url)
         t = time.time()
         while True:
             nodes = (await c.list("nodes"))["items"]
             if nodes and any(x.get("type") == "Ready" and x.get("status") == "True"
                              for x in nodes[0]["status"].get("conditions") or ()):
-                break
-            if time.time() - t > 60:
-                raise TimeoutError("kubelet did not register")
+                if not gpu_pods or int((nodes[0]["status"].get("capacity") or {}).get("amd.com/gpu", "0")) >= 1:
+                    break
+            if time.time() - t > 90:
+                raise TimeoutError("kubelet did not register" + (" its GPUs" if nodes else ""))
             await asyncio.sleep(0.1)
         sampler = Sampler(kl.pid, period).start()
         rts = Sampler(rt_proc.pid, period).start() if rt_proc is not None else None
@@ -203,6 +295,7 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             if n in s2:
                 seq_lat.append(s2[n] - t1)
         cpu_per_pod = (sampler.cpu_seconds() - cpu0) / max(1, batch + background + sequential)
+        gpu = await _gpu_phase(c, ns, gpu_pods, timeout) if gpu_pods else None
         await asyncio.sleep(period)        # the sample covering the last start
         cpu = sorted(sampler.cpu) or [0.0]
         rss = max(sampler.rss or [0])
@@ -231,6 +324,8 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             "runtime": runtime,
             "thresholds": THRESHOLDS,
         }
+        if gpu is not None:
+            out["gpu"] = gpu
         if rt_cpu is not None:
             rt_cpu = rt_cpu or [0.0]
             out["runtime_cpu_cores"] = {"p50": round(pct(rt_cpu, .5), 3), "p95": round(pct(rt_cpu, .95), 3)}
@@ -245,7 +340,9 @@ async def run(batch=10, sequential=10, background=50, timeout=120.0, settle=2.0,
             and out["steady"]["kubelet_cpu_cores"]["p95"] <= THRESHOLDS["steady_kubelet_cpu"]["p95"]
             and out["steady"]["kubelet_rss_mib"] <= THRESHOLDS["steady_kubelet_rss_mib"]
             and (rt_cpu is None or (out["runtime_cpu_cores"]["p95"] <= THRESHOLDS["runtime_cpu"]["p95"]
-                                    and out["runtime_rss_mib"] <= THRESHOLDS["runtime_rss_mib"])))
+                                    and out["runtime_rss_mib"] <= THRESHOLDS["runtime_rss_mib"]))
+            and (gpu is None or (not gpu["failed"]
+                                 and gpu["sequential"]["running_p99_s"] <= THRESHOLDS["sequential"]["p99"])))
         return out
     finally:
         # the kubelet leaves containers running when it stops (by design: a restarted kubelet
@@ -273,9 +370,11 @@ def main(argv=None):
     ap.add_argument("--period", type=float, default=1.0, help="CPU/RSS sampling period (cAdvisor housekeeping)")
     ap.add_argument("--runtime", default="process", choices=["process", "remote"],
                     help="remote: kubelet -> CRI -> a separate kamd-cri process (tracked as the runtime)")
+    ap.add_argument("--gpu-pods", type=int, default=0,
+                    help="run N single-GPU HIP vector_add pods through the real amd.com/gpu plugin (needs a GPU)")
     a = ap.parse_args(argv)
     print(json.dumps(asyncio.run(run(a.batch, a.sequential, a.background, monitor=a.monitor, period=a.period,
-                                     runtime=a.runtime))))
+                                     runtime=a.runtime, gpu_pods=a.gpu_pods))))
 
 
 if __name__ == "__main__":

@@ -69,54 +69,92 @@ for p in sorted(glob.glob("/dev/dri/renderD*")):
         out["open"][os.path.basename(p)] = "OPEN"
     except OSError as e:
         out["open"][os.path.basename(p)] = __import__("errno").errorcode.get(e.errno, str(e.errno))
-hip = ctypes.CDLL("libamdhip64.so")
-n = ctypes.c_int(-1)
-out["hipGetDeviceCount"] = hip.hipGetDeviceCount(ctypes.byref(n))
-out["devices"] = n.value
-if n.value == 1:
-    a, b, c = (ctypes.POINTER(ctypes.c_float)() for _ in range(3))
-    out["hipMalloc"] = hip.hipMalloc(ctypes.byref(a), ctypes.c_size_t(1 << 20))
-    out["hipFree"] = hip.hipFree(a)
+hsa = ctypes.CDLL("libhsa-runtime64.so.1")
+out["hsa_init"] = hsa.hsa_init()
+if out["hsa_init"] == 0:
+    hsa.hsa_shut_down()
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = ctypes.c_int(-1)
+    out["hipGetDeviceCount"] = hip.hipGetDeviceCount(ctypes.byref(n))
+    out["devices"] = n.value
+    if n.value == 1:
+        a = ctypes.POINTER(ctypes.c_float)()
+        out["hipMalloc"] = hip.hipMalloc(ctypes.byref(a), ctypes.c_size_t(1 << 20))
+        out["hipFree"] = hip.hipFree(a)
 print("HIP " + json.dumps(out, sort_keys=True))
 '''
 
 
-def test_landlock_pod_on_a_multi_gpu_node_sees_exactly_its_gpu(tmp_path):
-    """Confinement on a real multi-GPU node (skips on the one-GPU lease): for every GPU k, a
-    Landlock-tier container allowed only renderD(k) runs HIP (init + an allocation), counts
-    exactly one device, and gets EACCES opening every sibling render node. This is the case the
-    one-GPU lease cannot show: ROCr must skip the EACCES'd siblings rather than fail to start."""
-    import glob
+def confinement_problems(res, mine, shim=True):
+    """What is wrong with one confined container's probe output `res` (HIP_PROBE) when it was
+    given the render node `mine` (None: no GPU) under kamd-runc's Landlock tier.
+
+    With the errno shim (the default, `kamd.io/devshim` unset or "true") every sibling render
+    node reads EPERM — as under a device cgroup — and ROCr starts with exactly the allowed GPU;
+    with `kamd.io/devshim: "false"` siblings read raw Landlock EACCES, which ROCr's thunk treats
+    as fatal, so hsa_init fails (HSA_STATUS_ERROR_OUT_OF_RESOURCES on this pool, round 5)."""
+    out = []
+    opened = res.get("open") or {}
+    if mine is not None and opened.get(mine) != "OPEN":
+        out.append(f"own node {mine} not OPEN: {opened.get(mine)}")
+    want = "EPERM" if shim else "EACCES"
+    bad = {n: v for n, v in opened.items() if n != mine and v != want}
+    if bad:
+        out.append(f"sibling render nodes should read {want}: {bad}")
+    siblings = [n for n in opened if n != mine]
+    if shim:
+        if res.get("hsa_init") != 0:
+            out.append(f"hsa_init failed under the shim: {res.get('hsa_init')}")
+        elif mine is not None and (res.get("hipGetDeviceCount") != 0 or res.get("devices") != 1
+                                   or res.get("hipMalloc") != 0):
+            out.append(f"HIP should see exactly its one GPU and allocate: {res}")
+    elif siblings and res.get("hsa_init") == 0:
+        out.append("raw EACCES on siblings should fail hsa_init")
+    return out
+
+
+def _run_probe(tmp_path, label, devices, shim):
     import json
-    import os
     import subprocess
     import sys
+    from kubernetes_amd.kubelet.runtime import process as proc_rt
+    probe = tmp_path / "hip_probe.py"
+    probe.write_text(HIP_PROBE)
+    b = tmp_path / label
+    b.mkdir()
+    ann = {"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": "/dev/dri"}
+    if not shim:
+        ann["kamd.io/devshim"] = "false"
+    spec = {"process": {"args": [sys.executable, str(probe)], "cwd": "/",
+                        "env": ["PATH=/usr/bin:/bin", "HSA_ENABLE_IPC_MODE_LEGACY=0", "LD_LIBRARY_PATH=/opt/rocm/lib"]},
+            "root": {"path": "/"}, "mounts": [], "annotations": ann,
+            "linux": {"devices": [{"path": d} for d in devices], "namespaces": []}}
+    (b / "config.json").write_text(json.dumps(spec))
+    r = subprocess.run([proc_rt.KAMD_RUNC, "run", "--bundle", str(b)], capture_output=True, text=True, timeout=120)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("HIP ")]
+    assert r.returncode == 0 and line, (label, r.stdout[-1500:], r.stderr[-1500:])
+    return json.loads(line[0][4:])
+
+
+def test_landlock_pod_on_a_multi_gpu_node_sees_exactly_its_gpu(tmp_path):
+    """Confinement on a real multi-GPU node (skips on the one-GPU lease): for every GPU k, a
+    Landlock-tier container allowed only renderD(k) — with kamd-runc's default errno shim —
+    reads EPERM on every sibling render node, and HIP initialises with exactly one device and
+    allocates on it. This is the case the one-GPU lease cannot show: ROCr must skip the denied
+    siblings rather than fail to start. The same container with the shim opted out reads raw
+    EACCES on the siblings and ROCr's hsa_init fails, which is why the shim is the default."""
+    import glob
+    import os
     from kubernetes_amd.kubelet.runtime import process as proc_rt
     nodes = sorted(glob.glob("/dev/dri/renderD*"))
     if len(nodes) < 2:
         pytest.skip(f"needs >= 2 render nodes (this host has {len(nodes)})")
     if proc_rt.runc_features().get("tier") != "landlock":
         pytest.skip("this host is not on the Landlock tier")
-    probe = tmp_path / "hip_probe.py"
-    probe.write_text(HIP_PROBE)
     for k, node in enumerate(nodes):
-        b = tmp_path / f"b{k}"
-        b.mkdir()
-        spec = {"process": {"args": [sys.executable, str(probe)], "cwd": "/",
-                            "env": ["PATH=/usr/bin:/bin", "HSA_ENABLE_IPC_MODE_LEGACY=0",
-                                    "LD_LIBRARY_PATH=/opt/rocm/lib"]},
-                "root": {"path": "/"}, "mounts": [],
-                "annotations": {"kamd.io/isolation-tier": "landlock", "kamd.io/landlock-dir": "/dev/dri"},
-                "linux": {"devices": [{"path": node}], "namespaces": []}}
-        (b / "config.json").write_text(json.dumps(spec))
-        r = subprocess.run([proc_rt.KAMD_RUNC, "run", "--bundle", str(b)], capture_output=True, text=True,
-                           timeout=120)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HIP ")]
-        assert r.returncode == 0 and line, (node, r.stdout[-1500:], r.stderr[-1500:])
-        res = json.loads(line[0][4:])
+        res = _run_probe(tmp_path, f"b{k}", [node], shim=True)
         print("GPU", k, node, res)
-        mine = os.path.basename(node)
-        assert res["open"][mine] == "OPEN", res
-        assert all(v == "EACCES" for n, v in res["open"].items() if n != mine), res
-        assert res["hipGetDeviceCount"] == 0 and res["devices"] == 1, res
-        assert res["hipMalloc"] == 0, res
+        assert confinement_problems(res, os.path.basename(node), shim=True) == [], res
+    raw = _run_probe(tmp_path, "raw", [nodes[0]], shim=False)
+    print("RAW", nodes[0], raw)
+    assert confinement_problems(raw, os.path.basename(nodes[0]), shim=False) == [], raw
