@@ -144,6 +144,12 @@ def generate(reference):
                                         (meta.endswith("meta.v1.ListMeta") and "items" in types)):
                 g = GROUPS[group_dir]
                 kinds[f"{g + '/' if g else ''}{version}/{name}"] = fq
+    # metav1.Status is registered unversioned in every group and served as `apiVersion: v1,
+    # kind: Status` (apimachinery/pkg/apis/meta/v1/register.go): protobuf ERROR watch frames and
+    # error responses carry it in a k8s envelope
+    status = "k8s.io.apimachinery.pkg.apis.meta.v1.Status"
+    if status in messages:
+        kinds["v1/Status"] = status
     return {"messages": dict(sorted(messages.items())), "kinds": dict(sorted(kinds.items()))}
 
 

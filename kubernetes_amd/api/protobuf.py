@@ -694,9 +694,18 @@ WATCH_STREAM = "application/vnd.kubernetes.protobuf;stream=watch"
 def envelope_with_rv(envelope: bytes, rv: str):
     """The stored envelope with metadata.resourceVersion set (etcd3 stores objects without
     it), or None when it is not a protobuf envelope of a known kind."""
-    if envelope[:4] != b"k8s\x00":
+    if envelope[:4] != MAGIC:
         return None
-    return _native_codec().with_rv(envelope, rv)
+    nat = _native()
+    if nat is not None:
+        return nat.with_rv(envelope, rv)
+    try:
+        obj = decode_object(envelope)
+    except ProtobufError:
+        return None
+    obj.setdefault("metadata", {})["resourceVersion"] = str(rv)
+    api_version, kind, _ = decode_unknown(envelope)
+    return encode_unknown(api_version, kind, encode_message(schema().message_for(api_version, kind), obj))
 
 
 def to_json(envelope: bytes, rv) -> bytes:
@@ -713,16 +722,54 @@ def to_json(envelope: bytes, rv) -> bytes:
 def watch_frame(etype: str, raw: bytes) -> bytes:
     """One length-delimited metav1.WatchEvent frame (4-byte big-endian length) embedding `raw`
     (`runtime/serializer/protobuf/protobuf.go:436`, `endpoints/handlers/watch.go:166-226`)."""
-    return _native_codec().watch_frame(etype, raw)
+    nat = _native()
+    if nat is not None:
+        return nat.watch_frame(etype, raw)
+    ev = _ld(1, etype.encode()) + _ld(2, _ld(1, bytes(raw)))
+    return len(ev).to_bytes(4, "big") + ev
+
+
+MAX_WATCH_FRAME = 64 << 20
 
 
 def decode_watch_frames(buf):
     """([(type, object)], bytes consumed) for the complete frames at the start of `buf`."""
-    return _native_codec().decode_watch_frames(buf)
-
-
-def _native_codec():
     nat = _native()
-    if nat is None:
-        raise ProtobufError("protobuf watch streams need the native codec (native/pbcodec)")
-    return nat
+    if nat is not None:
+        return nat.decode_watch_frames(buf)
+    from .meta import BY_KIND
+    events, pos, n = [], 0, len(buf)
+    mv = memoryview(buf)
+    while n - pos >= 4:
+        fl = int.from_bytes(bytes(mv[pos:pos + 4]), "big")
+        if fl > MAX_WATCH_FRAME:
+            raise ProtobufError("watch frame too large")
+        if n - pos - 4 < fl:
+            break
+        etype, raw = None, b""
+        for num, wt, v in _fields(mv[pos + 4:pos + 4 + fl]):
+            if num == 1 and wt == 2:
+                etype = bytes(v).decode()
+            elif num == 2 and wt == 2:
+                for n2, w2, x in _fields(v):
+                    if n2 == 1 and w2 == 2:
+                        raw = bytes(x)
+        if etype is None:
+            raise ProtobufError("malformed watch frame")
+        if raw[:4] == MAGIC:
+            obj = decode_object(raw)
+            ri = BY_KIND.get(obj.get("kind", ""))
+            if ri is not None:
+                obj["apiVersion"] = ri.group_version     # the native codec's canonical version
+        else:
+            obj = json.loads(raw) if raw else None
+        events.append((etype, obj))
+        pos += 4 + fl
+    return events, pos
+
+
+def status_envelope(status: dict) -> bytes:
+    """A metav1.Status as a protobuf envelope (`apiVersion: v1, kind: Status`), what client-go's
+    protobuf stream decoder expects in an ERROR frame (watch.go:166-226 encodes the error
+    object with the stream's serializer)."""
+    return encode_object(dict(status, kind="Status", apiVersion="v1"))

@@ -210,7 +210,7 @@ def pb_event_bytes(etype: str, entry: Entry) -> bytes:
 def error_event(status: dict, protobuf=False) -> bytes:
     if protobuf:
         from ..api import protobuf as pb
-        return pb.watch_frame(ERROR, codec.dumpb(status))
+        return pb.watch_frame(ERROR, pb.status_envelope(status))
     return codec.dumpb({"type": ERROR, "object": status}) + b"\n"
 
 

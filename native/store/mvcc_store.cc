@@ -835,6 +835,31 @@ static void chunk_pb(std::string* out, const char* type, std::string_view obj) {
   out->append("\r\n", 2);
 }
 
+// metav1.Status{status: Failure, message, reason, code} in a `k8s\0` envelope (TypeMeta v1/Status;
+// field numbers of k8s.io.apimachinery.pkg.apis.meta.v1.Status and runtime.Unknown)
+static std::string status_envelope(const char* message, const char* reason, int code) {
+  std::string st;
+#ifdef KAMD_STORE_SERVER
+  pbc::pb_put_ld(st, 1, "", 0);                              // metadata: ListMeta{}
+  pbc::pb_put_ld(st, 2, "Failure", 7);
+  pbc::pb_put_ld(st, 3, message, strlen(message));
+  pbc::pb_put_ld(st, 4, reason, strlen(reason));
+  pbc::pb_put_varint(st, (6u << 3) | 0);
+  pbc::pb_put_varint(st, (uint64_t)code);
+  std::string tm, env("k8s\0", 4);
+  pbc::pb_put_ld(tm, 1, "v1", 2);
+  pbc::pb_put_ld(tm, 2, "Status", 6);
+  pbc::pb_put_ld(env, 1, tm.data(), tm.size());
+  pbc::pb_put_ld(env, 2, st.data(), st.size());
+  pbc::pb_put_ld(env, 3, "", 0);
+  pbc::pb_put_ld(env, 4, "", 0);
+  return env;
+#else
+  (void)message; (void)reason; (void)code;
+  return st;
+#endif
+}
+
 // one event of watch w (JSON line or protobuf frame)
 static void emit(FanWatch* w, const char* type, const std::string& v, const Index& ix, int64_t rv);
 
@@ -1644,11 +1669,12 @@ class Server {
                  "\"status\":\"Failure\",\"message\":\"too old resource version: %lld (%lld)\",\"reason\":\"Expired\","
                  "\"code\":410}}\n", (long long)from, (long long)eng_->compacted());
         if (w->pb) {
-          // the Status object, embedded as JSON in an ERROR frame (clients decode by magic)
-          std::string st(b);
-          size_t o = st.find("\"object\":") + 9;
-          st = st.substr(o, st.size() - o - 2);
-          chunk_pb(&w->out, "ERROR", st);
+          // the metav1.Status as a protobuf envelope (v1/Status), what a protobuf stream
+          // decoder expects in an ERROR frame (watch.go:166-226)
+          char msg[160];
+          snprintf(msg, sizeof msg, "too old resource version: %lld (%lld)", (long long)from,
+                   (long long)eng_->compacted());
+          chunk_pb(&w->out, "ERROR", status_envelope(msg, "Expired", 410));
           w->out.append("0\r\n\r\n");
         } else {
           char hex[24];

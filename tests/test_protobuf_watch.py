@@ -15,8 +15,22 @@ import pytest
 
 from kubernetes_amd.api import protobuf as pb
 from kubernetes_amd.apiserver.server import APIServer
+from kubernetes_amd.native import pbcodec
 from kubernetes_amd.client.rest import JSON, PROTOBUF, APIStatusError, Client
 from kubernetes_amd.storage.remote import StoreServer
+
+
+@pytest.fixture(autouse=True, params=["native", "python"])
+def codec(request, monkeypatch):
+    """Every test runs with the native codec and with the pure-Python one (KAMD_PBCODEC=python:
+    no native library), whose watch frames must be byte-identical."""
+    monkeypatch.setenv("KAMD_PBCODEC", request.param)
+    pbcodec.reset()
+    if request.param == "native" and pbcodec.codec() is None:
+        pytest.skip("native pbcodec not built")
+    yield request.param
+    monkeypatch.delenv("KAMD_PBCODEC", raising=False)
+    pbcodec.reset()
 
 
 def _pod(name, node=None):
@@ -118,10 +132,15 @@ def test_protobuf_watch_gone(run):
                 async for _ in w:
                     pass
             assert ei.value.code == 410
-            # the ERROR frame itself decodes to the Status
+            # the ERROR frame carries the Status as a protobuf envelope (v1/Status), as client-go's
+            # protobuf stream decoder expects
             from kubernetes_amd.apiserver.cacher import error_event
-            evs, _ = pb.decode_watch_frames(error_event({"kind": "Status", "code": 410, "reason": "Expired"}, True))
-            assert evs == [("ERROR", {"kind": "Status", "code": 410, "reason": "Expired"})]
+            fr = error_event({"kind": "Status", "status": "Failure", "code": 410, "reason": "Expired"}, True)
+            assert pb.MAGIC + b"\x0a\x0c\x0a\x02v1\x12\x06Status" in fr
+            evs, _ = pb.decode_watch_frames(fr)
+            assert evs[0][0] == "ERROR"
+            assert {k: evs[0][1][k] for k in ("kind", "apiVersion", "status", "code", "reason")} == {
+                "kind": "Status", "apiVersion": "v1", "status": "Failure", "code": 410, "reason": "Expired"}
         finally:
             await c.close()
             await s.stop()
@@ -181,6 +200,55 @@ def test_protobuf_watch_resume_from_resource_version_fanout(run, store):
             await pc.close()
             await s.stop()
     run(main())
+
+
+def test_protobuf_fanout_410_is_a_protobuf_status(run, store):
+    """kamd-etcd's fan-out answers a compacted resourceVersion with an ERROR frame whose object
+    is a protobuf v1/Status envelope (decodable without JSON sniffing)."""
+    from kubernetes_amd.storage.remote import RemoteStore
+
+    async def main():
+        s = APIServer(store=store)
+        port = await s.start()
+        url = f"http://127.0.0.1:{port}"
+        c, pc = Client(url), Client(url, content_type=PROTOBUF)
+        try:
+            assert s.fanout is not None
+            for i in range(3):
+                await c.create("pods", _pod(f"g{i}"))
+            rv = (await c.list("pods", "default"))["metadata"]["resourceVersion"]
+            rs = await RemoteStore(store).connect()
+            await rs.compact(int(rv))
+            w = await pc.watch("pods", "default", resource_version="2", timeout_seconds=2)
+            with pytest.raises(APIStatusError) as ei:
+                [x async for x in w]
+            assert ei.value.code == 410 and "too old resource version" in str(ei.value)
+        finally:
+            await c.close()
+            await pc.close()
+            await s.stop()
+    run(main())
+
+
+def test_python_frames_match_native(monkeypatch):
+    """The pure-Python fallbacks produce the native codec's bytes."""
+    if pbcodec.codec() is None:
+        pytest.skip("native pbcodec not built")
+    env = pb.encode_object({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "d"},
+                            "spec": {"nodeName": "n"}})
+    st = {"kind": "Status", "status": "Failure", "message": "m", "reason": "Expired", "code": 410}
+    nat = (pb.watch_frame("ADDED", env), pb.envelope_with_rv(env, "77"), pb.status_envelope(st))
+    monkeypatch.setenv("KAMD_PBCODEC", "python")
+    pbcodec.reset()
+    try:
+        py = (pb.watch_frame("ADDED", env), pb.envelope_with_rv(env, "77"), pb.status_envelope(st))
+        assert py[0] == nat[0]
+        assert pb.decode_object(py[1]) == pb.decode_object(nat[1])
+        assert pb.decode_object(py[2]) == pb.decode_object(nat[2])
+        assert pb.decode_watch_frames(nat[0] + nat[0][:5]) == pb.decode_watch_frames(py[0] + py[0][:5])
+    finally:
+        monkeypatch.setenv("KAMD_PBCODEC", "native")
+        pbcodec.reset()
 
 
 def test_json_clients_unchanged(run):
