@@ -1278,7 +1278,12 @@ class APIServer:
                 if e.code != 409 or attempt == 7:
                     raise
                 await asyncio.sleep(0)
-        return await self.delete(ri, namespace, name, (eviction or {}).get("deleteOptions") or {}, user)
+        # the budget is spent: retry only the delete. A stale cache or a miss on this shared-store
+        # worker must not bubble up to the request-level retry, which would re-run the whole
+        # eviction and decrement the budget a second time (the reference retries only the
+        # check-and-decrement, eviction.go:84-131)
+        opts = (eviction or {}).get("deleteOptions") or {}
+        return await self._retrying(lambda: self.delete(ri, namespace, name, opts, user))
 
     # ------------------------------------------------------------------
     # HTTP

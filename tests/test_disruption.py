@@ -216,3 +216,49 @@ def test_eviction_records_the_pod_and_refuses_stale_or_spent_budgets(run):
                 await c.evict("default", "w1")
             assert ei.value.code == 429
     run(main(), timeout=90)
+
+
+def test_eviction_retries_only_the_delete_on_a_stale_worker(run):
+    """Shared store: when the worker's view of the pod is stale at the delete (another worker
+    changed it after the budget check), only the delete is retried — the budget is decremented
+    once, not again by a re-run of the whole eviction."""
+    from kubernetes_amd.apiserver import server as srv_mod
+    from kubernetes_amd.apiserver.server import APIServer
+    from kubernetes_amd.client.rest import Client
+    from kubernetes_amd.storage.remote import StoreServer
+
+    async def main():
+        store = StoreServer()
+        addr = store.start()
+        s = APIServer(store=addr)
+        port = await s.start()
+        c = Client(f"http://127.0.0.1:{port}")
+        try:
+            for i in range(2):
+                await c.create("pods", _bare_pod(f"w{i}"))
+            b = await c.create("poddisruptionbudgets", _pdb_obj("web", 0))
+            st = {"observedGeneration": b["metadata"].get("generation", 1), "disruptionsAllowed": 2,
+                  "currentHealthy": 2, "desiredHealthy": 0, "expectedPods": 2}
+            await c.patch("poddisruptionbudgets", "web", {"status": st}, "default", "merge", "status")
+            orig = s.delete
+            calls = []
+
+            async def stale_once(ri, ns, name, opts, user=None):
+                calls.append(name)
+                if len(calls) == 1 and ri.plural == "pods":
+                    raise srv_mod._Stale(0)        # the pod changed under this worker's cache
+                return await orig(ri, ns, name, opts, user)
+            s.delete = stale_once
+            await c.evict("default", "w0")
+            st = (await c.get("poddisruptionbudgets", "web", "default"))["status"]
+            assert st["disruptionsAllowed"] == 1, st          # spent once, not twice
+            assert list(st["disruptedPods"]) == ["w0"]
+            assert calls == ["w0", "w0"]
+            names = [p["metadata"]["name"] for p in (await c.list("pods", "default"))["items"]]
+            assert "w0" not in names or any(p["metadata"].get("deletionTimestamp")
+                                            for p in (await c.list("pods", "default"))["items"])
+        finally:
+            await c.close()
+            await s.stop()
+            store.stop()
+    run(main(), timeout=60)
