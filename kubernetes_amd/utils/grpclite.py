@@ -466,13 +466,37 @@ class _Conn(asyncio.Protocol):
         self.blocked: deque = deque()                # streams with DATA waiting for window
 
     # -- client stream slots (the peer's SETTINGS_MAX_CONCURRENT_STREAMS) ----------------
-    async def stream_slot(self):
+    async def stream_slot(self, timeout=None):
         """Wait until opening one more stream stays within the peer's limit (calls over it queue
-        here, as grpc-core's do, instead of being refused)."""
+        here, as grpc-core's do, instead of being refused). `timeout`: the call's deadline —
+        DEADLINE_EXCEEDED when no slot frees in time. A waiter that is woken and then cancelled
+        (or times out) before using its slot hands the slot to the next waiter, so no queued
+        call is left waiting for a wakeup that was already spent."""
+        loop = asyncio.get_running_loop()
+        deadline = None if timeout is None else loop.time() + timeout
         while self.peer_max_streams is not None and len(self.streams) >= self.peer_max_streams and not self.closed:
-            fut = asyncio.get_running_loop().create_future()
+            fut = loop.create_future()
             self.slot_waiters.append(fut)
-            await fut
+            try:
+                if deadline is None:
+                    await fut
+                else:
+                    left = deadline - loop.time()
+                    if left <= 0:
+                        raise asyncio.TimeoutError()
+                    await asyncio.wait_for(asyncio.shield(fut), left)
+            except (asyncio.CancelledError, asyncio.TimeoutError) as e:
+                if fut.done() and not fut.cancelled():
+                    self._slot_free()          # woken for a slot this call will not use: pass it on
+                else:
+                    fut.cancel()
+                    try:
+                        self.slot_waiters.remove(fut)
+                    except ValueError:
+                        pass
+                if isinstance(e, asyncio.TimeoutError):
+                    raise RpcError(StatusCode.DEADLINE_EXCEEDED, "Deadline Exceeded waiting for a stream slot")
+                raise
 
     def _slot_free(self):
         while self.slot_waiters and (self.peer_max_streams is None or len(self.streams) < self.peer_max_streams
@@ -975,9 +999,12 @@ class Channel:
                 except asyncio.TimeoutError:
                     raise RpcError(StatusCode.DEADLINE_EXCEEDED, "Deadline Exceeded while connecting")
         if conn.peer_max_streams is not None and len(conn.streams) >= conn.peer_max_streams:
-            await conn.stream_slot()
+            t0 = asyncio.get_running_loop().time()
+            await conn.stream_slot(timeout)
             if conn.closed:
                 raise RpcError(StatusCode.UNAVAILABLE, "connection closed")
+            if timeout is not None:                   # the deadline covers the queueing too
+                timeout = max(0.001, timeout - (asyncio.get_running_loop().time() - t0))
         st = self._open(conn, path, payload, timeout)
         st.fut = asyncio.get_running_loop().create_future()
         if st.ended:                                  # failed while sending

@@ -370,3 +370,47 @@ def test_lite_client_queues_calls_over_peer_max_concurrent_streams(monkeypatch):
             await ch.close()
             await plugin.stop()
     asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_stream_slot_hand_off_on_cancel_and_deadline(monkeypatch):
+    """a queued call that is woken for a free stream and cancelled before it opens one
+    passes the slot to the next waiter (no lost wakeup), and a queued unary call honours its
+    deadline while waiting for a slot (DEADLINE_EXCEEDED, nothing left queued)."""
+    monkeypatch.setattr(gl, "MAX_CONCURRENT_STREAMS", 4)
+
+    async def main():
+        d = tempfile.mkdtemp()
+        sock = os.path.join(d, "p.sock")
+        plugin = await _Plugin("amd.com/gpu", sock, [device("g0")]).start()
+        ch = gl.Channel("unix://" + sock)
+        try:
+            dp = api.device_plugin_stub(ch)
+            await dp.AdmitPod(api.DP["AdmitPodRequest"](pod_name="warm"), timeout=5)
+            conn = ch._conn
+            assert conn.peer_max_streams == 4
+            for sid in (1001, 1003, 1005, 1007):            # every stream slot taken
+                conn.streams[sid] = gl._Stream(sid, 0)
+            a = asyncio.ensure_future(conn.stream_slot())
+            b = asyncio.ensure_future(conn.stream_slot())
+            await asyncio.sleep(0.01)
+            assert len(conn.slot_waiters) == 2
+            conn.streams.pop(1001)
+            conn._slot_free()                               # wakes a ...
+            a.cancel()                                      # ... which is cancelled before it runs
+            await asyncio.wait_for(b, 1)                    # b got the slot a never used
+            assert a.cancelled() and not conn.slot_waiters
+            conn.streams[1001] = gl._Stream(1001, 0)
+            with pytest.raises(gl.RpcError) as ei:
+                await conn.stream_slot(0.05)
+            assert ei.value.code() == gl.StatusCode.DEADLINE_EXCEEDED and not conn.slot_waiters
+            t0 = asyncio.get_running_loop().time()
+            with pytest.raises(gl.RpcError) as ei:          # a unary call queued past its deadline
+                await dp.AdmitPod(api.DP["AdmitPodRequest"](pod_name="late"), timeout=0.1)
+            assert ei.value.code() == gl.StatusCode.DEADLINE_EXCEEDED
+            assert asyncio.get_running_loop().time() - t0 < 1.0
+            for sid in (1001, 1003, 1005, 1007):
+                conn.streams.pop(sid, None)
+        finally:
+            await ch.close()
+            await plugin.stop()
+    asyncio.run(asyncio.wait_for(main(), 30))
