@@ -96,14 +96,14 @@ def cpu_budget():
 
 
 # Per-pod host CPU of each control-plane component at the N=1 headline rate, measured on the
-# MI355X box in round 5 (profiles/r5_gpu/bench_r5{b,c}*.json `cpu_ms_per_pod`, protobuf watch
-# streams: API server 0.61-0.63 ms, scheduler 0.29-0.33 ms, hollow kubelets 0.50-0.53 ms per pod
-# at 4613-4864 pods/s). A whole node sizes each component for the load of `world` ranks at that
+# MI355X box (`cpu_ms_per_pod`): round 5 profiles/r5_gpu/bench_r5{b,c}*.json — API server
+# 0.61-0.63 ms, scheduler 0.29-0.33 ms, hollow kubelets 0.50-0.53 ms per pod at 4613-4864 pods/s;
+# round 6 profiles/r6_gpu/bench_r6a.json — 0.627 / 0.321 / 0.557 ms at 4614 pods/s. A whole node sizes each component for the load of `world` ranks at that
 # rate so that at linear weak scaling every process is at most 70 % busy with HEADROOM to spare
 # (ceilings at 70 % busy >= 1.3x the linear rate: profiles/r5_gpu/whole_node_ceiling.md),
 # instead of a fixed-size control plane.
 N1_RATE_PODS_PER_S = 4700.0
-CPU_MS_PER_POD = {"apiserver": 0.62, "scheduler": 0.32, "hollow": 0.51}
+CPU_MS_PER_POD = {"apiserver": 0.63, "scheduler": 0.32, "hollow": 0.56}
 TARGET_UTIL = 0.7
 HEADROOM = 1.3
 

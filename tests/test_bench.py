@@ -78,7 +78,7 @@ def test_bench_gpus_mismatch_fails():
 def test_bench_eight_ranks_whole_node_shape():
     """The N=8 path the driver runs on a whole MI355X node, rehearsed with gloo on CPU: 8 ranks
     under torch.distributed.run with the >= 64-CPU control-plane shape (KAMD_BENCH_CPUS=64:
-    the demand model scaled to that budget — 22 API server workers, 11 scheduler shards) and
+    the demand model scaled to that budget — 21 API server workers, 11 scheduler shards) and
     small per-rank work."""
     env = dict(os.environ, KAMD_BENCH_FORCE_CPU="1", KAMD_BENCH_CPUS="64")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
@@ -90,7 +90,7 @@ def test_bench_eight_ranks_whole_node_shape():
     _check(d, 8, 2, 1)
     assert d["config"]["parallelism"] == "ranks8" and d["config"]["hollow_nodes"] == 8
     assert d["config"]["global_batch"] == 64
-    assert d["config"]["apiserver_workers"] == 22 and d["config"]["scheduler_shards"] == 11
+    assert d["config"]["apiserver_workers"] == 21 and d["config"]["scheduler_shards"] == 11
 
 
 def test_payload_server_batches_starts(run, tmp_path):
