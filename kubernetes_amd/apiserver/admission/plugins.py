@@ -374,21 +374,140 @@ class Priority(Plugin):
         spec["priority"] = int(pc.get("value", 0))
 
 
+def node_identity(user):
+    """`pkg/auth/nodeidentifier/default.go`: (node name, True) for a user named
+    `system:node:<name>` in the `system:nodes` group, else ("", False)."""
+    if user is None or not user.name.startswith("system:node:") or "system:nodes" not in (user.groups or ()):
+        return "", False
+    return user.name[len("system:node:"):], True
+
+
+def pod_configmap_names(pod) -> list[str]:
+    """`VisitPodConfigmapNames` (pkg/api/pod/util.go): envFrom / configMapKeyRef, configMap and
+    projected configMap volumes."""
+    spec = pod.get("spec") or {}
+    out = []
+    for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
+        out += [ef["configMapRef"].get("name", "") for ef in c.get("envFrom") or () if ef.get("configMapRef") is not None]
+        out += [e["valueFrom"]["configMapKeyRef"].get("name", "") for e in c.get("env") or ()
+                if (e.get("valueFrom") or {}).get("configMapKeyRef") is not None]
+    for v in spec.get("volumes") or ():
+        if v.get("configMap") is not None:
+            out.append(v["configMap"].get("name", ""))
+        for src in (v.get("projected") or {}).get("sources") or ():
+            if src.get("configMap") is not None:
+                out.append(src["configMap"].get("name", ""))
+    return out
+
+
 @register
 class NodeRestriction(Plugin):
-    """Nodes (users `system:node:<name>`) may only modify their own Node and pods bound to them."""
+    """`plugin/pkg/admission/noderestriction/admission.go`: a kubelet (`system:node:<name>`,
+    group `system:nodes`) may
+      * create only mirror pods bound to itself that reference no service account, secret,
+        configmap or persistent volume claim (:133-172), and delete only pods bound to itself
+        (:174-191); no other pod write, and no pod subresource but status / eviction (:104-115);
+      * update the status of, and evict, only pods bound to itself (:198-254);
+      * create and modify only its own Node, never setting a new `spec.configSource` (:300-342);
+      * update only `status.capacity` / `status.conditions` of PVCs, with the
+        ExpandPersistentVolumes gate (:256-298).
+    Requests from a node identity whose node name is empty are refused (:99-102)."""
     name = "NodeRestriction"
+    operations = (CREATE, UPDATE, DELETE)
 
     def validate(self, a):
-        u = a.user
-        if not u or not u.name.startswith("system:node:"):
+        node, is_node = node_identity(a.user)
+        if not is_node:
             return
-        node = u.name[len("system:node:"):]
-        if a.resource == "nodes" and a.name and a.name != node:
-            raise AdmissionError(f"node {node!r} cannot modify node {a.name!r}")
-        if a.resource == "pods" and a.operation in (UPDATE, DELETE) and a.old is not None:
-            if (a.old.get("spec") or {}).get("nodeName") != node:
-                raise AdmissionError(f"node {node!r} can only modify pods bound to it")
+        if not node:
+            raise self._forbid(a, f"could not determine node from user {a.user.name!r}")
+        if a.resource == "pods":
+            if a.subresource == "":
+                self._pod(node, a)
+            elif a.subresource == "status":
+                if a.operation != UPDATE:
+                    raise self._forbid(a, f"unexpected operation {a.operation!r}")
+                if ((a.old or {}).get("spec") or {}).get("nodeName") != node:
+                    raise self._forbid(a, f"node {node!r} can only update pod status for pods with spec.nodeName set "
+                                          "to itself")
+            elif a.subresource == "eviction":
+                self._eviction(node, a)
+            else:
+                raise self._forbid(a, f"unexpected pod subresource {a.subresource!r}")
+        elif a.resource == "nodes":
+            self._node(node, a)
+        elif a.resource == "persistentvolumeclaims":
+            if a.subresource != "status":
+                raise self._forbid(a, "may only update PVC status")
+            self._pvc_status(node, a)
+
+    @staticmethod
+    def _forbid(a, msg):
+        return AdmissionError(f'{a.resource} "{a.name or ""}" is forbidden: {msg}')
+
+    def _pod(self, node, a):
+        if a.operation == CREATE:
+            pod = a.obj or {}
+            md, spec = pod.get("metadata") or {}, pod.get("spec") or {}
+            if MIRROR_POD_ANNOTATION not in (md.get("annotations") or {}):
+                raise self._forbid(a, f"pod does not have \"{MIRROR_POD_ANNOTATION}\" annotation, node \"{node}\" "
+                                      "can only create mirror pods")
+            if spec.get("nodeName") != node:
+                raise self._forbid(a, f"node {node!r} can only create pods with spec.nodeName set to itself")
+            if spec.get("serviceAccountName"):
+                raise self._forbid(a, f"node {node!r} can not create pods that reference a service account")
+            if core.pod_secret_names(pod):
+                raise self._forbid(a, f"node {node!r} can not create pods that reference secrets")
+            if pod_configmap_names(pod):
+                raise self._forbid(a, f"node {node!r} can not create pods that reference configmaps")
+            if any(v.get("persistentVolumeClaim") is not None for v in spec.get("volumes") or ()):
+                raise self._forbid(a, f"node {node!r} can not create pods that reference persistentvolumeclaims")
+        elif a.operation == DELETE:
+            if ((a.old or {}).get("spec") or {}).get("nodeName") != node:
+                raise self._forbid(a, f"node {node!r} can only delete pods with spec.nodeName set to itself")
+        else:
+            raise self._forbid(a, f"unexpected operation {a.operation!r}")
+
+    def _eviction(self, node, a):
+        if a.operation != CREATE:
+            raise self._forbid(a, f"unexpected operation {a.operation}")
+        pod = a.old
+        if pod is None and self.server is not None:
+            name = a.name or ((a.obj or {}).get("metadata") or {}).get("name")
+            if not name:
+                raise self._forbid(a, "could not determine pod from request data")
+            pod = self.server.get_object("pods", a.namespace, name)
+        if pod is None:
+            raise AdmissionError(f'pods "{a.name}" not found', 404, "NotFound")
+        if (pod.get("spec") or {}).get("nodeName") != node:
+            raise self._forbid(a, f"node {node} can only evict pods with spec.nodeName set to itself")
+
+    def _node(self, node, a):
+        requested = a.name
+        if a.operation == CREATE:
+            if ((a.obj or {}).get("spec") or {}).get("configSource") is not None:
+                raise self._forbid(a, "cannot create with non-nil configSource")
+            requested = requested or ((a.obj or {}).get("metadata") or {}).get("name")
+        if requested != node:
+            raise self._forbid(a, f"node {node!r} cannot modify node {requested!r}")
+        if a.operation == UPDATE:
+            new = ((a.obj or {}).get("spec") or {}).get("configSource")
+            if new is not None and new != ((a.old or {}).get("spec") or {}).get("configSource"):
+                raise self._forbid(a, "cannot update configSource to a new non-nil configSource")
+
+    def _pvc_status(self, node, a):
+        if a.operation != UPDATE:
+            raise self._forbid(a, f"unexpected operation {a.operation!r}")
+        if not DefaultFeatureGate("ExpandPersistentVolumes"):
+            raise self._forbid(a, f"node {node!r} may not update persistentvolumeclaim metadata")
+
+        def strip(o):
+            o = dict(o or {})
+            o["metadata"] = {k: v for k, v in (o.get("metadata") or {}).items() if k != "resourceVersion"}
+            o["status"] = {k: v for k, v in (o.get("status") or {}).items() if k not in ("capacity", "conditions")}
+            return o
+        if strip(a.old) != strip(a.obj):
+            raise self._forbid(a, f"node {node!r} may not update fields other than status.capacity and status.conditions")
 
 
 @register

@@ -1244,6 +1244,13 @@ class APIServer:
         budget whose status the disruption controller has not caught up with (429)."""
         ri = m.BY_PLURAL["pods"]
         pod = (await self._aexisting(ri, namespace, name))[1].obj
+        # pods/eviction is a CREATE of an Eviction through admission (NodeRestriction: a kubelet
+        # evicts only its own pods), before the budget is touched
+        ev = dict(eviction or {})
+        ev.setdefault("metadata", {"name": name, "namespace": namespace})
+        a = adm.Attributes(adm.CREATE, "pods", "eviction", namespace, name, ev, pod, user, "Eviction")
+        self._admit(a)
+        self._validate_admission(a)
         labels = (pod.get("metadata") or {}).get("labels") or {}
         from ..api.labels import label_selector_as_selector
         pri = m.BY_PLURAL["poddisruptionbudgets"]
