@@ -523,28 +523,93 @@ class AlwaysPullImages(Plugin):
             c["imagePullPolicy"] = "Always"
 
 
+def selector_to_labels_map(text) -> dict:
+    """`labels.ConvertSelectorToLabelsMap`: "k1=v1,k2=v2" (`==` accepted) -> {k: v}; an
+    unparsable term is an error."""
+    out = {}
+    for term in (text or "").split(","):
+        term = term.strip()
+        if not term:
+            continue
+        k, sep, v = term.partition("==") if "==" in term else term.partition("=")
+        k, v = k.strip(), v.strip()
+        if not sep or not k or "!" in k:
+            raise ValueError(f"invalid selector: {term!r}")
+        out[k] = v
+    return out
+
+
+def labels_conflict(a: dict, b: dict) -> bool:
+    """`labels.Conflicts`: a key both sets have, with different values."""
+    return any(k in b and b[k] != v for k, v in a.items())
+
+
 @register
 class PodNodeSelector(Plugin):
-    """Merges the namespace annotation `scheduler.alpha.kubernetes.io/node-selector`."""
+    """`plugin/pkg/admission/podnodeselector/admission.go`: the namespace's node selector —
+    the `scheduler.alpha.kubernetes.io/node-selector` annotation, else the plugin config's
+    `clusterDefaultNodeSelector` — is merged into the pod's `nodeSelector` (the pod's own
+    labels win, a conflicting value is refused), and the result must stay within the
+    namespace's whitelist from the plugin config (`podNodeSelectorPluginConfig: {<namespace>:
+    "k=v,..."}`). Create and update of pods proper; subresources are ignored."""
     name = "PodNodeSelector"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE)
     ANN = "scheduler.alpha.kubernetes.io/node-selector"
 
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        cfg = self.config
+        self.cluster = dict(cfg.get("podNodeSelectorPluginConfig") or cfg.get("PodNodeSelectorPluginConfig") or
+                            {k: v for k, v in cfg.items() if isinstance(v, str)})
+
+    def _ignore(self, a):
+        return a.resource != "pods" or a.subresource or not isinstance(a.obj, dict)
+
+    def _namespace_selector(self, a):
+        ns = self.server.get_object("namespaces", None, a.namespace) if self.server else None
+        if ns is None:
+            if self.server is not None and a.namespace not in SYSTEM_NAMESPACES:
+                raise AdmissionError(f"namespace {a.namespace} does not exist", 404, "NotFound")
+            ns = {"metadata": {"name": a.namespace}}
+        ann = (ns.get("metadata") or {}).get("annotations") or {}
+        try:
+            if self.ANN in ann:
+                return selector_to_labels_map(ann[self.ANN])
+            return selector_to_labels_map(self.cluster.get("clusterDefaultNodeSelector", ""))
+        except ValueError as e:
+            raise AdmissionError(str(e), 500, "InternalError")
+
+    def _forbid(self, a, msg):
+        return AdmissionError(f'pods "{(a.obj.get("metadata") or {}).get("name", "")}" is forbidden: {msg}')
+
     def admit(self, a):
-        if a.resource != "pods" or a.subresource or not self.server:
+        if self._ignore(a):
             return
-        ns = self.server.get_object("namespaces", None, a.namespace)
-        sel = ((ns or {}).get("metadata") or {}).get("annotations", {}).get(self.ANN)
-        if not sel:
-            return
+        if a.operation == UPDATE and a.old is not None and \
+                not ((a.old.get("metadata") or {}).get("initializers") or {}).get("pending"):
+            return                  # the node selector of an initialized pod is immutable (:101-108)
+        nsel = self._namespace_selector(a)
         spec = a.obj.setdefault("spec", {})
-        nsel = spec.setdefault("nodeSelector", {})
-        for term in sel.split(","):
-            if "=" in term:
-                k, v = term.split("=", 1)
-                if k.strip() in nsel and nsel[k.strip()] != v.strip():
-                    raise AdmissionError("pod node label selector conflicts with its project node label selector")
-                nsel[k.strip()] = v.strip()
+        pod_sel = spec.get("nodeSelector") or {}
+        if labels_conflict(nsel, pod_sel):
+            raise self._forbid(a, "pod node label selector conflicts with its namespace node label selector")
+        if nsel:
+            spec["nodeSelector"] = {**nsel, **pod_sel}
+
+    def validate(self, a):
+        if self._ignore(a):
+            return
+        nsel = self._namespace_selector(a)
+        pod_sel = (a.obj.get("spec") or {}).get("nodeSelector") or {}
+        if labels_conflict(nsel, pod_sel):
+            raise self._forbid(a, "pod node label selector conflicts with its namespace node label selector")
+        try:
+            white = selector_to_labels_map(self.cluster.get(a.namespace, ""))
+        except ValueError as e:
+            raise AdmissionError(str(e), 500, "InternalError")
+        # labels.AreLabelsInWhiteList: an empty whitelist allows everything
+        if white and any(white.get(k) != v for k, v in pod_sel.items()):
+            raise self._forbid(a, "pod node label selector labels conflict with its namespace whitelist")
 
 
 @register
