@@ -346,32 +346,68 @@ class ExtendedResourceToleration(Plugin):
         spec["tolerations"] = tols
 
 
+SYSTEM_CRITICAL_PRIORITY = 2 * 1000000000                  # scheduling.SystemCriticalPriority
+SYSTEM_PRIORITY_CLASSES = {"system-cluster-critical": SYSTEM_CRITICAL_PRIORITY,
+                           "system-node-critical": SYSTEM_CRITICAL_PRIORITY + 1000}
+HIGHEST_USER_DEFINABLE_PRIORITY = 1000000000
+
+
 @register
 class Priority(Plugin):
+    """`plugin/pkg/admission/priority/admission.go`:
+      * pods (create, PodPriority gate): a client may not set `spec.priority` itself; it is
+        resolved from `priorityClassName` — the system classes first, then user classes ("no
+        PriorityClass with name X was found" otherwise) — or, without a class name, from the
+        globalDefault class, else 0 (:147-185);
+      * PriorityClasses (create / update): the value may not exceed 1e9, the system class names
+        are reserved, and at most one class is the globalDefault (:187-215)."""
     name = "Priority"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE, DELETE)
+
+    def _classes(self):
+        return self.server.list_objects("priorityclasses") if self.server else []
 
     def admit(self, a):
-        # `plugin/pkg/admission/priority`: a no-op while the PodPriority feature is off
-        if a.resource != "pods" or a.subresource or not DefaultFeatureGate("PodPriority"):
+        if a.subresource or a.resource != "pods" or a.operation != CREATE or not isinstance(a.obj, dict):
             return
         spec = a.obj.setdefault("spec", {})
+        if spec.get("priority") is not None:
+            raise AdmissionError(f'pods "{(a.obj.get("metadata") or {}).get("name", "")}" is forbidden: the integer '
+                                 "value of priority must not be provided in pod spec. Priority admission controller "
+                                 "populates the value from the given PriorityClass name")
+        if not DefaultFeatureGate("PodPriority"):
+            return
         pcn = spec.get("priorityClassName")
         if not pcn:
-            default = None
-            if self.server:
-                for pc in self.server.list_objects("priorityclasses"):
-                    if pc.get("globalDefault"):
-                        default = pc
-                spec.setdefault("priority", int(default.get("value", 0)) if default else 0)
+            default = next((pc for pc in self._classes() if pc.get("globalDefault")), None)
+            spec["priority"] = int(default.get("value", 0)) if default else 0
             return
-        if pcn in ("system-cluster-critical", "system-node-critical"):
-            spec["priority"] = 2000000000 if pcn == "system-cluster-critical" else 2000001000
+        if pcn in SYSTEM_PRIORITY_CLASSES:
+            spec["priority"] = SYSTEM_PRIORITY_CLASSES[pcn]
             return
         pc = self.server.get_object("priorityclasses", None, pcn) if self.server else None
         if pc is None:
-            raise AdmissionError(f"no PriorityClass with name {pcn} was found", 403)
+            raise AdmissionError(f'pods "{(a.obj.get("metadata") or {}).get("name", "")}" is forbidden: no '
+                                 f"PriorityClass with name {pcn} was found")
         spec["priority"] = int(pc.get("value", 0))
+
+    def validate(self, a):
+        if a.subresource or a.resource != "priorityclasses" or a.operation not in (CREATE, UPDATE):
+            return
+        pc = a.obj or {}
+        name = (pc.get("metadata") or {}).get("name", "")
+
+        def forbid(msg):
+            return AdmissionError(f'priorityclasses.scheduling.k8s.io "{name}" is forbidden: {msg}')
+        if int(pc.get("value", 0) or 0) > HIGHEST_USER_DEFINABLE_PRIORITY:
+            raise forbid(f"maximum allowed value of a user defined priority is {HIGHEST_USER_DEFINABLE_PRIORITY}")
+        if name in SYSTEM_PRIORITY_CLASSES:
+            raise forbid(f"the name of the priority class is a reserved name for system use only: {name}")
+        if pc.get("globalDefault"):
+            other = next((c for c in self._classes() if c.get("globalDefault")), None)
+            if other is not None and (a.operation == CREATE or other["metadata"]["name"] != name):
+                raise forbid(f"PriorityClass {other['metadata']['name']} is already marked as default. "
+                             "Only one default can exist")
 
 
 def node_identity(user):
