@@ -297,22 +297,51 @@ def limit_secret_references(sa, pod):
     return None
 
 
+def add_or_update_toleration(spec, tol) -> bool:
+    """`helper.AddOrUpdateTolerationInPod`: replace the toleration matching `tol` (same key,
+    operator, value, effect — `Toleration.MatchToleration`) or append it."""
+    key = lambda t: (t.get("key", ""), t.get("operator", "Equal") or "Equal", t.get("value", ""), t.get("effect", ""))  # noqa: E731
+    out, updated = [], False
+    for t in spec.get("tolerations") or ():
+        if key(t) == key(tol):
+            if t == tol:
+                return False
+            out.append(dict(tol))
+            updated = True
+        else:
+            out.append(t)
+    if not updated:
+        out.append(dict(tol))
+    spec["tolerations"] = out
+    return True
+
+
 @register
 class DefaultTolerationSeconds(Plugin):
+    """`plugin/pkg/admission/defaulttolerationseconds/admission.go`: a pod that does not tolerate
+    `node.kubernetes.io/not-ready:NoExecute` (resp. `unreachable`) — a toleration with that key
+    or an empty key, and effect NoExecute or empty — gets one with tolerationSeconds 300
+    (plugin config `defaultNotReadyTolerationSeconds` / `defaultUnreachableTolerationSeconds`,
+    the reference's --default-*-toleration-seconds flags). Create and update of pods proper."""
     name = "DefaultTolerationSeconds"
-    operations = (CREATE,)
-    KEYS = ("node.kubernetes.io/not-ready", "node.kubernetes.io/unreachable")
+    operations = (CREATE, UPDATE)
+    NOT_READY, UNREACHABLE = "node.kubernetes.io/not-ready", "node.kubernetes.io/unreachable"
+
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        self.seconds = {self.NOT_READY: int(self.config.get("defaultNotReadyTolerationSeconds", 300)),
+                        self.UNREACHABLE: int(self.config.get("defaultUnreachableTolerationSeconds", 300))}
 
     def admit(self, a):
-        if a.resource != "pods" or a.subresource:
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
             return
         spec = a.obj.setdefault("spec", {})
         tols = spec.get("tolerations") or []
-        have = {t.get("key") for t in tols}
-        for k in self.KEYS:
-            if k not in have:
-                tols.append({"key": k, "operator": "Exists", "effect": "NoExecute", "tolerationSeconds": 300})
-        spec["tolerations"] = tols
+        for k in (self.NOT_READY, self.UNREACHABLE):
+            if any(t.get("key", "") in (k, "") and t.get("effect", "") in ("NoExecute", "") for t in tols):
+                continue
+            add_or_update_toleration(spec, {"key": k, "operator": "Exists", "effect": "NoExecute",
+                                            "tolerationSeconds": self.seconds[k]})
 
 
 @register
