@@ -577,15 +577,29 @@ class NodeRestriction(Plugin):
 
 @register
 class AlwaysPullImages(Plugin):
+    """`plugin/pkg/admission/alwayspullimages/admission.go`: every container and init container
+    of a created or updated pod pulls Always (a node's cached image is not trusted across
+    tenants); validation refuses any other policy that a later mutating step put back."""
     name = "AlwaysPullImages"
     operations = (CREATE, UPDATE)
 
     def admit(self, a):
-        if a.resource != "pods" or a.subresource:
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
             return
         spec = a.obj.get("spec") or {}
-        for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
+        for c in (spec.get("initContainers") or []) + (spec.get("containers") or []):
             c["imagePullPolicy"] = "Always"
+
+    def validate(self, a):
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
+            return
+        spec = a.obj.get("spec") or {}
+        for kind in ("initContainers", "containers"):
+            for i, c in enumerate(spec.get(kind) or ()):
+                if c.get("imagePullPolicy") != "Always":
+                    raise AdmissionError(f'pods "{(a.obj.get("metadata") or {}).get("name", "")}" is forbidden: '
+                                         f"spec.{kind}[{i}].imagePullPolicy: Unsupported value: "
+                                         f"\"{c.get('imagePullPolicy', '')}\": supported values: \"Always\"")
 
 
 def selector_to_labels_map(text) -> dict:

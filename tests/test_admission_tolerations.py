@@ -52,3 +52,22 @@ def test_configured_seconds_and_subresources():
     other = {"metadata": {"name": "p"}, "spec": {}}
     chain.admit(Attributes(CREATE, "pods", "binding", "foo", "p", other))
     assert other == {"metadata": {"name": "p"}, "spec": {}}
+
+
+def test_always_pull_images_admit_and_validate():
+    """`alwayspullimages/admission_test.go`: TestAdmission sets Always on every container and
+    init container; TestValidate refuses any other policy; subresources are ignored."""
+    import pytest as _pt
+    from kubernetes_amd.apiserver.admission import AdmissionError, UPDATE
+    chain = new_chain(["AlwaysPullImages"])
+    pod = {"metadata": {"name": "p"}, "spec": {
+        "initContainers": [{"name": "i1"}, {"name": "i2", "imagePullPolicy": "IfNotPresent"}],
+        "containers": [{"name": "c1", "imagePullPolicy": "Never"}, {"name": "c2", "imagePullPolicy": "Always"}]}}
+    a = Attributes(CREATE, "pods", "", "ns", "p", pod)
+    chain.admit(a)
+    chain.validate(a)
+    assert all(c["imagePullPolicy"] == "Always" for k in ("initContainers", "containers") for c in pod["spec"][k])
+    bad = {"metadata": {"name": "p"}, "spec": {"containers": [{"name": "c", "imagePullPolicy": "Never"}]}}
+    with _pt.raises(AdmissionError, match=r"spec.containers\[0\].imagePullPolicy: Unsupported value: \"Never\""):
+        chain.validate(Attributes(UPDATE, "pods", "", "ns", "p", bad, bad))
+    chain.validate(Attributes(UPDATE, "pods", "status", "ns", "p", bad, bad))
