@@ -345,7 +345,9 @@ class ExtraCommands:
         if ri is None or not name:
             raise SystemExit(f"error: expected TYPE/NAME, got {target!r}")
         ns = self.ns_for(ri)
-        for _ in range(5):
+        # client-go RetryOnConflict with a growing pause: a controller writing the object's status
+        # (a Deployment right after it was created) can win several read-modify-write races
+        for attempt in range(12):
             obj = await self.client.get(ri.plural, name, ns)
             obj.setdefault("kind", ri.kind)
             if fn(obj) is False:
@@ -356,6 +358,7 @@ class ExtraCommands:
             except APIStatusError as e:
                 if e.code != 409:
                     raise
+                await asyncio.sleep(min(0.01 * (attempt + 1), 0.1))
         raise SystemExit("error: too many conflicts")
 
     async def _set_split(self):
