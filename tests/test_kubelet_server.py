@@ -27,7 +27,8 @@ def test_kubelet_endpoints_and_webhook_auth(run, tmp_path):
     async def main():
         s = APIServer(authorization_modes=("RBAC",), tokens={
             "kubelet-tok": User("system:node:n1", "1", ["system:nodes", "system:masters"]),
-            "alice-tok": User("alice", "2", []), "ops-tok": User("ops", "3", [])})
+            "alice-tok": User("alice", "2", []), "ops-tok": User("ops", "3", []),
+            "root-tok": User("root", "4", ["system:masters"])})
         url = f"http://127.0.0.1:{await s.start()}"
         admin = Client(url, token="kubelet-tok")
         # ops may read node stats and proxy; alice nothing
@@ -44,8 +45,11 @@ def test_kubelet_endpoints_and_webhook_auth(run, tmp_path):
         await kl.run()
         k = f"http://127.0.0.1:{kl.http_port}"
         try:
-            await admin.create("pods", {"metadata": {"name": "p", "namespace": "default"},
-                                        "spec": {"nodeName": "n1", "containers": [{"name": "c", "image": "busybox"}]}})
+            # a node may create only mirror pods (NodeRestriction): a cluster admin creates the pod
+            root = Client(url, token="root-tok")
+            await root.create("pods", {"metadata": {"name": "p", "namespace": "default"},
+                                       "spec": {"nodeName": "n1", "containers": [{"name": "c", "image": "busybox"}]}})
+            await root.close()
             ops, alice, anon = Client(k, token="ops-tok"), Client(k, token="alice-tok"), Client(k)
 
             async def get(c, path):
