@@ -41,8 +41,11 @@ class PodInfo:
         self.milli_cpu = req["cpu"].milli_value() if "cpu" in req else 0
         self.memory = req["memory"].int_value() if "memory" in req else 0
         self.ephemeral = req["ephemeral-storage"].int_value() if "ephemeral-storage" in req else 0
+        # `calculateResource`: scalar resources are extended (domain-qualified) names and
+        # hugepages; any other key a container names is not accounted
         self.scalars = {k: v.int_value() for k, v in req.items()
-                        if k not in ("cpu", "memory", "ephemeral-storage", "pods")}
+                        if k not in ("cpu", "memory", "ephemeral-storage", "pods")
+                        and (core.is_extended_resource_name(k) or k.startswith("hugepages-"))}
         spec = pod.get("spec") or {}
         # `priorities/util/non_zero.go` GetNonzeroRequests: per container, a request that is not
         # set counts as 100m / 200Mi (an explicit zero stays zero); init containers do not count
@@ -362,12 +365,19 @@ class SchedulerCache:
         if key in self.assumed:
             self.assumed[key] = time.monotonic() + self.ttl
 
+    def _drop_empty(self, name):
+        """`removePod`: a NodeInfo with neither a node nor pods is deleted."""
+        ni = self.nodes.get(name)
+        if ni is not None and ni.node is None and not ni.pods:
+            del self.nodes[name]
+
     def forget_pod(self, pod):
         key = ns_name(pod)
         st = self.pod_states.get(key)
         if st is None or key not in self.assumed:
             return
         self._node(st[1]).remove_pod(key)
+        self._drop_empty(st[1])
         del self.pod_states[key]
         del self.assumed[key]
         self.anti_pods.pop(key, None)
@@ -397,6 +407,7 @@ class SchedulerCache:
                     return
         if st is not None:
             self._node(st[1]).remove_pod(key)
+            self._drop_empty(st[1])
         self._node(node).add_pod(key, pod, PodInfo(pod))
         self.pod_states[key] = (pod, node)
         self.assumed.pop(key, None)
@@ -431,6 +442,7 @@ class SchedulerCache:
             if dl and dl < now:
                 pod, node = self.pod_states[key]
                 self._node(node).remove_pod(key)
+                self._drop_empty(node)
                 del self.pod_states[key]
                 del self.assumed[key]
                 self.anti_pods.pop(key, None)
