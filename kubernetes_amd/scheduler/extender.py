@@ -3,10 +3,14 @@
 Parity: `plugin/pkg/scheduler/core/extender.go` (`HTTPExtender`: `Filter` POSTs ExtenderArgs
 {pod, nodes | nodenames} to `<urlPrefix>/<filterVerb>` and gets ExtenderFilterResult {nodes |
 nodenames, failedNodes, error}; `Prioritize` gets a HostPriorityList whose scores are multiplied
-by `weight`; `IsInterested` via `managedResources`; `ignorable`) and the Policy config
-`plugin/pkg/scheduler/api/types.go:129` (`ExtenderConfig`).
+by `weight`; `IsInterested` via `managedResources`; `ignorable`; `Bind` / `IsBinder`, :198-223)
+and the Policy config `plugin/pkg/scheduler/api/types.go:129` (`ExtenderConfig`, `BindVerb`).
 
-Calls are synchronous with a timeout, like the reference's (the scheduling loop is serial).
+Calls are synchronous with a timeout, like the reference's (the scheduling loop is serial);
+the scheduler runs `bind` off the event loop. A binder extender takes over writing the binding
+(`factory.go:886` getBinder): ExtenderBindingArgs keeps the reference's untagged Go field names
+(`PodName`, `PodNamespace`, `PodUID`, `Node`) and, GPU-aware, adds `ExtendedResourceBindings` —
+the device IDs the scheduler allocated — so the extender can write a complete binding.
 """
 from __future__ import annotations
 
@@ -26,7 +30,7 @@ class ExtenderError(Exception):
 
 class HTTPExtender:
     def __init__(self, url_prefix, filter_verb="", prioritize_verb="", weight=1, http_timeout=5.0,
-                 node_cache_capable=False, managed_resources=None, ignorable=False):
+                 node_cache_capable=False, managed_resources=None, ignorable=False, bind_verb=""):
         u = urlparse(url_prefix)
         self.host, self.port = u.hostname or "127.0.0.1", u.port or (443 if u.scheme == "https" else 80)
         self.https = u.scheme == "https"
@@ -37,6 +41,7 @@ class HTTPExtender:
         self.node_cache_capable = node_cache_capable
         self.managed = {m["name"] if isinstance(m, dict) else m for m in (managed_resources or ())}
         self.ignorable = ignorable
+        self.bind_verb = bind_verb
 
     @classmethod
     def from_config(cls, cfg: dict):
@@ -45,7 +50,23 @@ class HTTPExtender:
             to = to / 1e9
         return cls(cfg["urlPrefix"], cfg.get("filterVerb", ""), cfg.get("prioritizeVerb", ""),
                    int(cfg.get("weight", 1)), float(to or 5.0), bool(cfg.get("nodeCacheCapable")),
-                   cfg.get("managedResources"), bool(cfg.get("ignorable")))
+                   cfg.get("managedResources"), bool(cfg.get("ignorable")),
+                   cfg.get("bindVerb") or cfg.get("BindVerb") or "")
+
+    def is_binder(self) -> bool:
+        return bool(self.bind_verb)
+
+    def bind(self, namespace, name, uid, node, erb=None):
+        """Delegate the binding (extender.go:198 Bind); raises ExtenderError on failure."""
+        if not self.is_binder():
+            raise ExtenderError("Unexpected empty bindVerb in extender")
+        args = {"PodName": name, "PodNamespace": namespace, "PodUID": uid or "", "Node": node}
+        if erb:
+            args["ExtendedResourceBindings"] = erb
+        res = self._post(self.bind_verb, args) or {}
+        err = res.get("Error") or res.get("error")
+        if err:
+            raise ExtenderError(err)
 
     def is_interested(self, pod) -> bool:
         if not self.managed:

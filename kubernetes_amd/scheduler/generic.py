@@ -477,7 +477,12 @@ class GenericScheduler:
         else:
             scores = self._combine(prios, fnodes, raws)
             for ext in self.extenders:
-                for name, s in ext.prioritize(pod, fnodes).items():
+                try:
+                    escores = ext.prioritize(pod, fnodes)
+                except Exception:   # generic_scheduler.go PrioritizeNodes: extender errors are ignored
+                    log.warning("extender prioritize failed; ignoring its scores", exc_info=True)
+                    continue
+                for name, s in escores.items():
                     scores[name] = scores.get(name, 0) + s
             host = self.select_host(scores, fnodes)
         if host in bindings:

@@ -121,11 +121,16 @@ def parse_policy(pol):
     hw = pol.get("hardPodAffinitySymmetricWeight")
     if hw is not None and not 0 <= int(hw) <= 100:
         raise PolicyError("hardPodAffinitySymmetricWeight must be in the range 0-100")
+    binders = 0
     for e in pol.get("extenders") or []:
         if not e.get("urlPrefix"):
             raise PolicyError("extender needs a urlPrefix")
         if int(e.get("weight", 1)) <= 0 and e.get("prioritizeVerb"):
             raise PolicyError(f"extender {e['urlPrefix']}: weight must be positive")
+        if e.get("bindVerb") or e.get("BindVerb"):
+            binders += 1
+    if binders > 1:     # api/validation/validation.go:37-48
+        raise PolicyError(f"Only one extender can implement bind, found {binders}")
     return Algorithm(preds, prios, list(pol.get("extenders") or []), None if hw is None else int(hw))
 
 

@@ -44,6 +44,7 @@ from ..utils.httpserver import HTTPServer, Response
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from ..utils.trace import Trace
 from .cache import PodInfo, SchedulerCache
+from .extender import ExtenderError
 from .generic import FitError, GenericScheduler
 from .queue import SchedulingQueue
 from .volumes import SELECTED_NODE_ANN, plan_bindings
@@ -69,6 +70,8 @@ class Scheduler:
             self.cache.failure_domains = tuple(failure_domains)
         self.queue = SchedulingQueue()
         self.algo = GenericScheduler(self.cache, predicates, priorities, percentage_of_nodes_to_score, extenders)
+        # factory.go:886 getBinder: the first extender with a bindVerb writes bindings
+        self.binder = next((e for e in extenders or () if getattr(e, "is_binder", lambda: False)()), None)
         self.algo.queue = self.queue
         self.shard_index, self.shard_count = shard_index, shard_count
         self.partitioned = shard_count > 1
@@ -435,8 +438,13 @@ class Scheduler:
             try:
                 if vplan:
                     await self._bind_volumes(vplan, host)
-                await self.client.bind(md.get("namespace", "default"), md["name"], host, erb or None, decode=False)
-            except (APIStatusError, ConnectionError, OSError, asyncio.TimeoutError) as e:
+                if self.binder is not None:
+                    await asyncio.get_running_loop().run_in_executor(
+                        None, self.binder.bind, md.get("namespace", "default"), md["name"], md.get("uid"), host,
+                        erb or None)
+                else:
+                    await self.client.bind(md.get("namespace", "default"), md["name"], host, erb or None, decode=False)
+            except (APIStatusError, ExtenderError, ConnectionError, OSError, asyncio.TimeoutError) as e:
                 self.cache.forget_pod(assumed)
                 for kind, _pvc, pv in vplan or ():
                     if kind == "bind":
