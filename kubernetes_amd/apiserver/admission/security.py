@@ -27,7 +27,8 @@
   * OwnerReferencesPermissionEnforcement — `plugin/pkg/admission/gc`: setting
     `blockOwnerDeletion` requires `update` on the owner's `finalizers` subresource.
   * ImagePolicyWebhook — `plugin/pkg/admission/imagepolicy`: an ImageReview is POSTed to a
-    backend; default-deny on backend failure unless `defaultAllow`.
+    kubeconfig-named backend, answers cached per allow/deny TTL, transient failures retried;
+    default-deny on backend failure unless `defaultAllow` (failed-open annotation).
 """
 from __future__ import annotations
 
@@ -386,34 +387,174 @@ class OwnerReferencesPermissionEnforcement(Plugin):
                                      f"finalizers on: User \"{getattr(a.user, 'name', '')}\" cannot update {ri.plural}/finalizers")
 
 
+# ImagePolicyWebhook config bounds, seconds (imagepolicy/config.go:27-41)
+DEFAULT_RETRY_BACKOFF, MIN_RETRY_BACKOFF, MAX_RETRY_BACKOFF = 0.5, 1e-9, 300.0
+DEFAULT_ALLOW_TTL, MIN_ALLOW_TTL, MAX_ALLOW_TTL = 300.0, 1.0, 1800.0
+DEFAULT_DENY_TTL, MIN_DENY_TTL, MAX_DENY_TTL = 30.0, 1.0, 1800.0
+IMAGE_POLICY_FAILED_OPEN = "alpha.image-policy.k8s.io/failed-open"
+
+
+def normalize_config_duration(name, scale, value, lo, hi, default):
+    """config.go normalizeConfigDuration: -1 disables (0), 0 takes the default, otherwise the
+    number is in units of `scale` seconds and must land in [lo, hi]."""
+    value = int(value or 0)
+    if value == -1:
+        return 0.0
+    if value == 0:
+        return default
+    v = value * scale
+    if v < lo or v > hi:
+        raise ValueError(f"image policy webhook {name}: valid value is between {lo}s and {hi}s, got {v}s")
+    return v
+
+
+def normalize_image_policy_config(cfg: dict) -> dict:
+    """config.go normalizeWebhookConfig: retryBackoff in ms, allowTTL / denyTTL in seconds."""
+    out = dict(cfg)
+    out["retryBackoff"] = normalize_config_duration("backoff", 1e-3, cfg.get("retryBackoff"), MIN_RETRY_BACKOFF,
+                                                    MAX_RETRY_BACKOFF, DEFAULT_RETRY_BACKOFF)
+    out["allowTTL"] = normalize_config_duration("allow cache", 1.0, cfg.get("allowTTL"), MIN_ALLOW_TTL,
+                                                MAX_ALLOW_TTL, DEFAULT_ALLOW_TTL)
+    out["denyTTL"] = normalize_config_duration("deny cache", 1.0, cfg.get("denyTTL"), MIN_DENY_TTL,
+                                               MAX_DENY_TTL, DEFAULT_DENY_TTL)
+    return out
+
+
+class _WebhookFailure(Exception):
+    def __init__(self, message, transient=False):
+        super().__init__(message)
+        self.transient = transient
+
+
 @register
 class ImagePolicyWebhook(Plugin):
+    """`plugin/pkg/admission/imagepolicy/admission.go`.
+
+    Config (`--admission-control-config-file`, :190-260): `{"imagePolicy": {kubeConfigFile,
+    allowTTL, denyTTL, retryBackoff, defaultAllow}}`; the kubeconfig names the backend and its TLS
+    material, resolved like a webhook kubeconfig (the current context, or the unnamed cluster and
+    user when there is none). For each pod CREATE / UPDATE an ImageReview (containers then init
+    containers, annotations filtered to `*.image-policy.k8s.io/*`, namespace) is POSTed; answers
+    are cached in a 1024-entry LRU keyed by the review spec for allowTTL / denyTTL; transport
+    errors, 5xx and 429 are retried with exponential backoff (`util/webhook` factor 1.5, 5
+    steps); a non-2xx answer is an error. On backend failure the pod is refused, unless
+    `defaultAllow`, which admits it annotated `alpha.image-policy.k8s.io/failed-open: "true"`.
+
+    The backend call runs in the async `charge` step (off the event loop, like the reference's
+    per-request goroutine), so a slow backend never stalls other requests; list the plugin before
+    ResourceQuota so a refused pod is not charged. A flat `{"url": ...}` config is accepted for
+    plain-HTTP test backends.
+    """
     name = "ImagePolicyWebhook"
     operations = (CREATE, UPDATE)
 
     def __init__(self, server=None, config=None):
         super().__init__(server, config)
-        cfg = config or {}
+        if config is None:
+            raise ValueError("ImagePolicyWebhook: no config specified")
+        cfg = normalize_image_policy_config(config.get("imagePolicy", config))
+        self.ssl = None
         self.url = cfg.get("url")
+        if cfg.get("kubeConfigFile"):
+            from ...client import clientcmd
+            r = clientcmd.resolve_webhook(cfg["kubeConfigFile"])
+            self.url, self.ssl = r.server, r.ssl_context
+        if not self.url:
+            raise ValueError("ImagePolicyWebhook: no backend (kubeConfigFile) configured")
+        self.allow_ttl, self.deny_ttl = cfg["allowTTL"], cfg["denyTTL"]
+        self.retry_backoff = cfg["retryBackoff"]
         self.default_allow = bool(cfg.get("defaultAllow", False))
+        self.timeout = float(cfg.get("timeout", 30.0))
+        from collections import OrderedDict
+        self.cache: OrderedDict[str, tuple] = OrderedDict()
+        self.cache_size = 1024
 
-    def validate(self, a):
-        if a.resource != "pods" or a.subresource or a.obj is None or not self.url:
+    def _review(self, a):
+        pod = a.obj
+        spec = pod.get("spec") or {}
+        ctrs = list(spec.get("containers") or ()) + list(spec.get("initContainers") or ())
+        anns = (pod.get("metadata") or {}).get("annotations") or {}
+        return {"containers": [{"image": c.get("image", "")} for c in ctrs],
+                "annotations": {k: v for k, v in anns.items() if ".image-policy.k8s.io/" in k},
+                "namespace": a.namespace or ""}
+
+    def _cached(self, key):
+        hit = self.cache.get(key)
+        if hit is None:
+            return None
+        status, expires = hit
+        if time.monotonic() >= expires:
+            del self.cache[key]
+            return None
+        self.cache.move_to_end(key)
+        return status
+
+    def _remember(self, key, status):
+        ttl = self.allow_ttl if status.get("allowed") else self.deny_ttl
+        if ttl <= 0:
             return
+        self.cache[key] = (status, time.monotonic() + ttl)
+        self.cache.move_to_end(key)
+        while len(self.cache) > self.cache_size:
+            self.cache.popitem(last=False)
+
+    def _post(self, body: bytes) -> dict:
+        import urllib.error
         import urllib.request
-        spec = a.obj.get("spec") or {}
-        review = {"apiVersion": "imagepolicy.k8s.io/v1alpha1", "kind": "ImageReview",
-                  "spec": {"containers": [{"image": c.get("image", "")} for c in _containers(spec)],
-                           "annotations": {k: v for k, v in ((a.obj.get("metadata") or {}).get("annotations") or {}).items()
-                                           if ".image-policy.k8s.io/" in k},
-                           "namespace": a.namespace}}
+        req = urllib.request.Request(self.url, body, {"Content-Type": "application/json",
+                                                      "Accept": "application/json"})
         try:
-            req = urllib.request.Request(self.url, json.dumps(review).encode(), {"Content-Type": "application/json"})
-            with urllib.request.urlopen(req, timeout=10) as r:
-                st = json.loads(r.read()).get("status") or {}
-        except OSError as e:
-            if self.default_allow:
-                return
-            raise AdmissionError(f"image policy webhook backend denied one or more images: {e}")
-        if not st.get("allowed"):
-            raise AdmissionError(f"image policy webhook backend denied one or more images: {st.get('reason', '')}")
+            with urllib.request.urlopen(req, timeout=self.timeout, context=self.ssl) as r:
+                data = r.read()
+        except urllib.error.HTTPError as e:
+            raise _WebhookFailure(f"Error contacting webhook: {e.code}",
+                                  transient=e.code >= 500 or e.code == 429 or bool(e.headers.get("Retry-After")))
+        except (OSError, ValueError) as e:
+            raise _WebhookFailure(f"error contacting webhook: {e}", transient=True)
+        try:
+            return json.loads(data).get("status") or {}
+        except (ValueError, AttributeError) as e:
+            raise _WebhookFailure(f"bad webhook response: {e}")
+
+    def _post_with_backoff(self, body: bytes) -> dict:
+        """util/webhook WithExponentialBackoff: transient failures are retried."""
+        import random
+        delay = self.retry_backoff
+        for step in range(5):
+            try:
+                return self._post(body)
+            except _WebhookFailure as e:
+                if not e.transient or step == 4:
+                    raise
+            time.sleep(delay * (1 + 0.2 * random.random()))
+            delay *= 1.5
+        raise AssertionError("unreachable")
+
+    async def charge(self, a):
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
+            return
+        spec = self._review(a)
+        key = json.dumps(spec, sort_keys=True)
+        status = self._cached(key)
+        if status is None:
+            body = json.dumps({"apiVersion": "imagepolicy.k8s.io/v1alpha1", "kind": "ImageReview",
+                               "spec": spec}).encode()
+            import asyncio
+            try:
+                status = await asyncio.get_running_loop().run_in_executor(None, self._post_with_backoff, body)
+            except _WebhookFailure as e:
+                if self.default_allow:
+                    md = a.obj.setdefault("metadata", {})
+                    md["annotations"] = dict(md.get("annotations") or {}, **{IMAGE_POLICY_FAILED_OPEN: "true"})
+                    return
+                raise AdmissionError(f'pods "{_pod_name(a)}" is forbidden: {e}')
+            self._remember(key, status)
+        if not status.get("allowed"):
+            why = (f"image policy webhook backend denied one or more images: {status['reason']}"
+                   if status.get("reason") else "one or more images rejected by webhook backend")
+            raise AdmissionError(f'pods "{_pod_name(a)}" is forbidden: {why}')
+
+
+def _pod_name(a):
+    md = a.obj.get("metadata") or {}
+    return md.get("name") or md.get("generateName") or a.name or ""

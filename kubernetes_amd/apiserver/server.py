@@ -298,7 +298,7 @@ class APIServer:
         self.authz_webhook = None
         if authorization_webhook_config_file:
             from ..client import clientcmd
-            r = clientcmd.resolve(clientcmd.load(authorization_webhook_config_file)[0])
+            r = clientcmd.resolve_webhook(authorization_webhook_config_file)
             self.authz_webhook = (r.server, r.ssl_context, authorization_webhook_cache_authorized_ttl,
                                   authorization_webhook_cache_unauthorized_ttl)
         # kubelet connections (--kubelet-https, --kubelet-certificate-authority,
@@ -389,7 +389,7 @@ class APIServer:
                 toks.append(an.WebhookTokenAuthenticator(authentication_token_webhook, authentication_token_webhook_cache_ttl))
             if authentication_token_webhook_config_file:
                 from ..client import clientcmd
-                r = clientcmd.resolve(clientcmd.load(authentication_token_webhook_config_file)[0])
+                r = clientcmd.resolve_webhook(authentication_token_webhook_config_file)
                 toks.append(an.WebhookTokenAuthenticator(r.server, authentication_token_webhook_cache_ttl, r.ssl_context))
             if oidc:
                 toks.append(oidc if isinstance(oidc, an.OIDCAuthenticator) else an.OIDCAuthenticator(**oidc))

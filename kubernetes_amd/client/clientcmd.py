@@ -119,6 +119,25 @@ def resolve(cfg, context=None, base_dir="."):
     return Resolved(server, us.get("token"), ctx_ssl, ctx.get("namespace"), ca)
 
 
+def resolve_webhook(path):
+    """A webhook kubeconfig (`--*-webhook-config-file`, ImagePolicyWebhook's kubeConfigFile):
+    the current context, or — with none set — the cluster and user named "" (client-go's
+    non-interactive loading with empty overrides). Missing server or unreadable TLS files raise."""
+    with open(path) as f:
+        cfg = yaml.safe_load(f) or {}
+    base = os.path.dirname(os.path.abspath(path))
+    cfg = dict(cfg)
+    for k in ("clusters", "users", "contexts"):
+        cfg[k] = [dict(e, name=e.get("name") or "") for e in cfg.get(k) or ()]
+    cur = cfg["current-context"] = cfg.get("current-context") or ""
+    if not any(c["name"] == cur for c in cfg["contexts"]):
+        cfg["contexts"].append({"name": cur, "context": {"cluster": "", "user": ""}})
+    r = resolve(cfg, cur, base)
+    if r is None or not r.server:
+        raise ValueError(f"webhook kubeconfig {path}: invalid configuration: no server found")
+    return r
+
+
 def client_from(path=None, context=None, **kw):
     from .rest import Client
     cfg, p = load(path)
