@@ -347,7 +347,11 @@ class DefaultTolerationSeconds(Plugin):
 @register
 class ExtendedResourceToleration(Plugin):
     """Pods requesting an extended resource tolerate the taint named after it
-    (`plugin/pkg/admission/extendedresourcetoleration`). Considers pod-level ERs too."""
+    (`plugin/pkg/admission/extendedresourcetoleration/admission.go:55-94`): for every extended
+    resource in a (init) container's requests, `{key: <name>, operator: Exists, effect:
+    NoSchedule}` is added or updated with `AddOrUpdateTolerationInPod`. GPU-aware: the pod-level
+    `spec.extendedResources` entries count too, since ResourceV2 (earlier in the chain) moves
+    `amd.com/gpu` out of the container resources."""
     name = "ExtendedResourceToleration"
     operations = (CREATE, UPDATE)
 
@@ -365,14 +369,8 @@ class ExtendedResourceToleration(Plugin):
                 names.add(core.pod_extended_resource_name(per))
             except ValueError:
                 pass
-        if not names:
-            return
-        tols = spec.get("tolerations") or []
-        have = {(t.get("key"), t.get("operator")) for t in tols}
-        for n in sorted(names):
-            if (n, "Exists") not in have:
-                tols.append({"key": n, "operator": "Exists", "effect": "NoSchedule"})
-        spec["tolerations"] = tols
+        for n in sorted(names):     # sets.String.List(): stable sorted order (admission.go:84-91)
+            add_or_update_toleration(spec, {"key": n, "operator": "Exists", "effect": "NoSchedule"})
 
 
 SYSTEM_CRITICAL_PRIORITY = 2 * 1000000000                  # scheduling.SystemCriticalPriority

@@ -71,3 +71,63 @@ def test_always_pull_images_admit_and_validate():
     with _pt.raises(AdmissionError, match=r"spec.containers\[0\].imagePullPolicy: Unsupported value: \"Never\""):
         chain.validate(Attributes(UPDATE, "pods", "", "ns", "p", bad, bad))
     chain.validate(Attributes(UPDATE, "pods", "status", "ns", "p", bad, bad))
+
+
+# -- ExtendedResourceToleration: `plugin/pkg/admission/extendedresourcetoleration/admission_test.go`
+
+ER1, ER2 = "example.com/device-ek", "example.com/device-do"
+
+
+CPU_C = {"name": "c", "image": "x", "resources": {"requests": {"cpu": "2"}}}
+MEM_C = {"name": "m", "image": "x", "resources": {"requests": {"memory": "2048"}}}
+ER1_C = {"name": "e1", "image": "x", "resources": {"requests": {ER1: "1"}}}
+ER2_C = {"name": "e2", "image": "x", "resources": {"requests": {ER2: "2"}}}
+ER1_TOL = {"key": ER1, "operator": "Exists", "effect": "NoSchedule"}
+ER2_TOL = {"key": ER2, "operator": "Exists", "effect": "NoSchedule"}
+FOO_TOL = {"key": "foo", "operator": "Equal", "value": "bar", "effect": "NoSchedule"}
+
+ERT_CASES = [
+    ("empty pod without any extended resources", {}, None),
+    ("container without any extended resources", {"containers": [CPU_C]}, None),
+    ("init container without any extended resources", {"containers": [CPU_C], "initContainers": [MEM_C]}, None),
+    ("container with extended resource", {"containers": [CPU_C, ER1_C]}, [ER1_TOL]),
+    ("init container with extended resource", {"containers": [CPU_C], "initContainers": [ER2_C]}, [ER2_TOL]),
+    ("existing tolerations preserved", {"containers": [ER1_C], "tolerations": [FOO_TOL]}, [FOO_TOL, ER1_TOL]),
+    ("multiple extended resources, sorted", {"containers": [ER1_C, CPU_C], "initContainers": [ER2_C, MEM_C]},
+     [ER2_TOL, ER1_TOL]),
+    ("existing correct toleration: no change", {"containers": [ER1_C], "tolerations": [ER1_TOL]}, [ER1_TOL]),
+    ("same key, different effect and value: both kept",
+     {"containers": [ER1_C], "tolerations": [{"key": ER1, "operator": "Equal", "value": "foo", "effect": "NoExecute"}]},
+     [{"key": ER1, "operator": "Equal", "value": "foo", "effect": "NoExecute"}, ER1_TOL]),
+    ("wildcard toleration preserved", {"containers": [ER1_C], "tolerations": [{"operator": "Exists"}]},
+     [{"operator": "Exists"}, ER1_TOL]),
+]
+
+
+@pytest.mark.parametrize("name,spec,want", ERT_CASES, ids=[c[0] for c in ERT_CASES])
+def test_extended_resource_toleration(name, spec, want):
+    import copy
+    chain = new_chain(["ExtendedResourceToleration"])
+    pod = {"metadata": {"name": "p", "namespace": "default"}, "spec": copy.deepcopy(spec)}
+    chain.admit(Attributes(CREATE, "pods", "", "default", "p", pod))
+    assert pod["spec"].get("tolerations") == want
+
+
+def test_extended_resource_toleration_sees_resourcev2_gpus():
+    """GPU-aware: after ResourceV2 moved `amd.com/gpu` to spec.extendedResources, the pod still
+    tolerates the `amd.com/gpu` taint that keeps CPU-only pods off GPU nodes."""
+    from kubernetes_amd.api import core
+    chain = new_chain(["ResourceV2", "ExtendedResourceToleration"])
+    pod = {"metadata": {"name": "g", "namespace": "default"},
+           "spec": {"containers": [{"name": "c", "image": "x", "resources": {"limits": {core.AMD_GPU: "2"}}}]}}
+    chain.admit(Attributes(CREATE, "pods", "", "default", "g", pod))
+    assert pod["spec"]["extendedResources"] and core.AMD_GPU not in pod["spec"]["containers"][0]["resources"].get(
+        "limits", {})
+    assert pod["spec"]["tolerations"] == [{"key": core.AMD_GPU, "operator": "Exists", "effect": "NoSchedule"}]
+
+
+def test_extended_resource_toleration_ignores_subresources():
+    chain = new_chain(["ExtendedResourceToleration"])
+    pod = {"metadata": {"name": "p"}, "spec": {"containers": [ER1_C]}}
+    chain.admit(Attributes(CREATE, "pods", "status", "default", "p", pod))
+    assert "tolerations" not in pod["spec"]
