@@ -17,9 +17,9 @@
     opt-out annotation `podpreset.admission.kubernetes.io/exclude: "true"`.
   * EventRateLimit — `plugin/pkg/admission/eventratelimit`: token buckets on event creation per
     Server / Namespace / User (qps, burst); over the limit -> 429.
-  * PodTolerationRestriction — `plugin/pkg/admission/podtolerationrestriction`: namespace
-    annotations `scheduler.alpha.kubernetes.io/defaultTolerations` are merged in and
-    `.../tolerationsWhitelist` is enforced.
+  * PodTolerationRestriction — `plugin/pkg/admission/podtolerationrestriction`: namespace (or
+    cluster-config) default tolerations are merged in (conflicts refuse the pod), non-BestEffort
+    pods tolerate memory pressure, and the tolerations whitelist is enforced in both phases.
   * DenyEscalatingExec / DenyExecOnPrivileged — `plugin/pkg/admission/exec`: no exec/attach into
     privileged or host-namespace pods.
   * SecurityContextDeny — `plugin/pkg/admission/securitycontext/scdeny`: rejects pods setting
@@ -278,36 +278,132 @@ class EventRateLimit(Plugin):
                 raise AdmissionError("limit reached on type %s for key %s" % (t, key[1]), 429, "TooManyRequests")
 
 
+MEMORY_PRESSURE_TAINT = "node.kubernetes.io/memory-pressure"
+
+
+def _tol_key(t):
+    return (t.get("key", ""), t.get("effect", ""))
+
+
+def _tol_equal(a, b):
+    """pkg/util/tolerations AreEqual: key, operator, value, effect and tolerationSeconds."""
+    return (a.get("key", ""), a.get("operator", "") or "", a.get("value", ""), a.get("effect", ""),
+            a.get("tolerationSeconds")) == (b.get("key", ""), b.get("operator", "") or "", b.get("value", ""),
+                                            b.get("effect", ""), b.get("tolerationSeconds"))
+
+
+def tolerations_conflict(first, second) -> bool:
+    """IsConflict: a (key, effect) present in both with different tolerations."""
+    sm = {_tol_key(t): t for t in second}
+    return any(_tol_key(t) in sm and not _tol_equal(t, sm[_tol_key(t)]) for t in first)
+
+
+def merge_tolerations(first, second) -> list:
+    """MergeTolerations: `second`, plus the (key, effect) entries of `first` it lacks."""
+    have = {_tol_key(t) for t in second}
+    out = list(second)
+    for k, t in {_tol_key(t): t for t in first}.items():
+        if k not in have:
+            out.append(t)
+    return out
+
+
+def verify_against_whitelist(tolerations, whitelist) -> bool:
+    """VerifyAgainstWhitelist: every (key, effect) of the pod is whitelisted with an equal toleration."""
+    if not whitelist:
+        return True
+    w = {_tol_key(t): t for t in whitelist}
+    return all(_tol_key(t) in w and _tol_equal(t, w[_tol_key(t)]) for t in tolerations)
+
+
 @register
 class PodTolerationRestriction(Plugin):
+    """`plugin/pkg/admission/podtolerationrestriction/admission.go`.
+
+    Admit (CREATE, or UPDATE of a pod whose initializers are pending): the namespace's
+    `scheduler.alpha.kubernetes.io/defaultTolerations` — or, when the annotation is absent, the
+    cluster `default` from the plugin config (an empty annotation overrides it) — is merged into
+    the pod's tolerations; a (key, effect) both define differently refuses the pod ("namespace
+    tolerations and pod tolerations conflict"). Non-BestEffort pods also tolerate
+    `node.kubernetes.io/memory-pressure:NoSchedule`. Validate (CREATE and UPDATE): the pod's
+    tolerations must be in the namespace's `tolerationsWhitelist` (cluster `whitelist` when the
+    annotation is absent; an empty list allows everything). Config (`--admission-control-config-
+    file`): `{"default": [...], "whitelist": [...]}`.
+    """
     name = "PodTolerationRestriction"
     operations = (CREATE, UPDATE)
     DEFAULT = "scheduler.alpha.kubernetes.io/defaultTolerations"
     WHITELIST = "scheduler.alpha.kubernetes.io/tolerationsWhitelist"
 
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        cfg = config or {}
+        self.cluster_default = list(cfg.get("default") or ())
+        self.cluster_whitelist = list(cfg.get("whitelist") or ())
+
+    @staticmethod
+    def _ignore(a):
+        return a.resource != "pods" or a.subresource or not isinstance(a.obj, dict)
+
+    def _namespace(self, name):
+        ns = self.server.get_object("namespaces", None, name) if self.server else None
+        if ns is None and self.server is not None:
+            raise AdmissionError(f'namespaces "{name}" not found', 404, "NotFound")
+        return ns or {}
+
+    def _ns_tolerations(self, ns, key):
+        """extractNSTolerations: None when unset, [] when empty, else the parsed list."""
+        ann = (ns.get("metadata") or {}).get("annotations") or {}
+        if key not in ann:
+            return None
+        if not ann[key]:
+            return []
+        try:
+            ts = json.loads(ann[key])
+        except ValueError as e:
+            raise AdmissionError(f"invalid {key} annotation: {e}", 500, "InternalError")
+        if not isinstance(ts, list):
+            raise AdmissionError(f"invalid {key} annotation: not a list", 500, "InternalError")
+        return ts
+
     def admit(self, a):
-        if a.resource != "pods" or a.subresource or a.operation != CREATE:
+        if self._ignore(a):
             return
-        ns = self.server.get_object("namespaces", None, a.namespace) if self.server else None
-        ann = ((ns or {}).get("metadata") or {}).get("annotations") or {}
         spec = a.obj.setdefault("spec", {})
-        if self.DEFAULT in ann:
-            have = spec.get("tolerations") or []
-            for t in json.loads(ann[self.DEFAULT]):
-                if not any(x.get("key") == t.get("key") and x.get("effect") == t.get("effect") for x in have):
-                    have.append(t)
-            spec["tolerations"] = have
-        # whitelist verification right after the merge, in the mutating phase like the reference
-        # (`admission.go:149-167`): plugins later in the chain may still add tolerations
-        if self.WHITELIST not in ann:
+        final = list(spec.get("tolerations") or ())
+        updating_uninit = a.operation == UPDATE and a.old is not None and \
+            ((a.old.get("metadata") or {}).get("initializers") or {}).get("pending")
+        if a.operation == CREATE or updating_uninit:
+            ts = self._ns_tolerations(self._namespace(a.namespace), self.DEFAULT)
+            if ts is None:
+                ts = self.cluster_default
+            if ts:
+                if final:
+                    if tolerations_conflict(ts, final):
+                        raise AdmissionError("namespace tolerations and pod tolerations conflict")
+                    final = merge_tolerations(ts, final)
+                else:
+                    final = list(ts)
+        from ..registry import qos_class
+        if qos_class(a.obj) != "BestEffort":
+            final = merge_tolerations(final, [{"key": MEMORY_PRESSURE_TAINT, "operator": "Exists",
+                                               "effect": "NoSchedule"}])
+        if final or "tolerations" in spec:
+            spec["tolerations"] = final
+        self.validate(a)
+
+    def validate(self, a):
+        if self._ignore(a):
             return
-        wl = json.loads(ann[self.WHITELIST])
-        for t in (a.obj.get("spec") or {}).get("tolerations") or ():
-            ok = any(w.get("key") == t.get("key") and w.get("operator", "Equal") == t.get("operator", "Equal")
-                     and w.get("value") == t.get("value") and w.get("effect") == t.get("effect") for w in wl)
-            if not ok:
-                raise AdmissionError("pod tolerations (possibly merged with namespace default tolerations) conflict "
-                                     "with its namespace whitelist")
+        tols = (a.obj.get("spec") or {}).get("tolerations") or ()
+        if not tols:
+            return
+        wl = self._ns_tolerations(self._namespace(a.namespace), self.WHITELIST)
+        if wl is None:
+            wl = self.cluster_whitelist
+        if wl and not verify_against_whitelist(tols, wl):
+            raise AdmissionError("pod tolerations (possibly merged with namespace default tolerations) conflict "
+                                 "with its namespace whitelist")
 
 
 @register

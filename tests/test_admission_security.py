@@ -105,7 +105,11 @@ def test_podpreset_toleration_restriction_ratelimit_scdeny(run):
             # namespace default tolerations + whitelist
             await c.create("namespaces", {"metadata": {"name": "gpu-team", "annotations": {
                 "scheduler.alpha.kubernetes.io/defaultTolerations": json.dumps([{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]),
-                "scheduler.alpha.kubernetes.io/tolerationsWhitelist": json.dumps([{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}])}}})
+                # the whitelist is checked again in the validating phase, after DefaultTolerationSeconds
+                "scheduler.alpha.kubernetes.io/tolerationsWhitelist": json.dumps(
+                    [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}] +
+                    [{"key": f"node.kubernetes.io/{k}", "operator": "Exists", "effect": "NoExecute",
+                      "tolerationSeconds": 300} for k in ("not-ready", "unreachable")])}}})
             gp = pod("g")
             gp["metadata"]["namespace"] = "gpu-team"
             got = await c.create("pods", gp, "gpu-team")

@@ -131,3 +131,107 @@ def test_extended_resource_toleration_ignores_subresources():
     pod = {"metadata": {"name": "p"}, "spec": {"containers": [ER1_C]}}
     chain.admit(Attributes(CREATE, "pods", "status", "default", "p", pod))
     assert "tolerations" not in pod["spec"]
+
+
+# -- PodTolerationRestriction: `plugin/pkg/admission/podtolerationrestriction/admission_test.go`
+
+import json as _json  # noqa: E402
+
+from kubernetes_amd.apiserver.admission import UPDATE, AdmissionError  # noqa: E402
+from kubernetes_amd.apiserver.admission.security import (MEMORY_PRESSURE_TAINT, PodTolerationRestriction,  # noqa: E402
+                                                         merge_tolerations, tolerations_conflict,
+                                                         verify_against_whitelist)
+
+
+class _NsServer:
+    def __init__(self, annotations):
+        self.ns = {"metadata": {"name": "testNamespace", "annotations": annotations}}
+
+    def get_object(self, resource, namespace, name):
+        return self.ns if resource == "namespaces" and name == "testNamespace" else None
+
+
+def tv(value="testValue", key="testKey"):
+    return {"key": key, "operator": "Equal", "value": value, "effect": "NoSchedule"}
+
+
+MP = {"key": MEMORY_PRESSURE_TAINT, "operator": "Exists", "effect": "NoSchedule"}
+BEST_EFFORT = [{"name": "test"}]
+BURSTABLE = [{"name": "test", "resources": {"limits": {"cpu": "1000m"}, "requests": {"cpu": "500m"}}}]
+GUARANTEED = [{"name": "test", "resources": {"limits": {"cpu": "1000m"}, "requests": {"cpu": "1000m"}}}]
+
+# (name, containers, cluster default, ns default, ns whitelist, cluster whitelist, pod tolerations, merged, admit)
+PTR_CASES = [
+    ("default cluster tolerations with empty pod tolerations and nil namespace tolerations",
+     BEST_EFFORT, [tv()], None, None, None, [], [tv()], True),
+    ("default cluster tolerations with pod tolerations specified",
+     BEST_EFFORT, [tv()], [], None, None, [tv()], [tv()], True),
+    ("namespace tolerations", BEST_EFFORT, [], [tv()], None, None, [tv()], [tv()], True),
+    ("no pod tolerations", BEST_EFFORT, [], [tv()], None, None, [], [tv()], True),
+    ("conflicting pod and namespace tolerations", BEST_EFFORT, [], [tv()], None, None, [tv("testValue1")], None,
+     False),
+    ("conflicting pod and default cluster tolerations but overridden by empty namespace tolerations",
+     BEST_EFFORT, [tv("testValue2")], [], None, None, [tv("testValue1")], [tv("testValue1")], True),
+    ("merged pod tolerations satisfy whitelist", BEST_EFFORT, [], [tv()], [tv()], None, [], [tv()], True),
+    ("Override default cluster toleration by empty namespace level toleration",
+     BEST_EFFORT, [tv()], [], None, None, [], [], True),
+    ("pod toleration conflicts with default cluster white list which is overridden by empty namespace whitelist",
+     BEST_EFFORT, None, [], [], [tv("testValue1")], [tv()], [tv()], True),
+    ("merged pod tolerations conflict with the whitelist", BEST_EFFORT, [], [tv()], [tv("testValue1")], None, [],
+     None, False),
+    ("added memoryPressure/DiskPressure for Burstable pod", BURSTABLE, [], [tv()], [], None, [], [MP, tv()], True),
+    ("added memoryPressure/DiskPressure for Guaranteed pod", GUARANTEED, [], [tv()], [], None, [], [MP, tv()], True),
+]
+
+
+def _same(a, b):
+    """tolerations.EqualTolerations: order-insensitive by (key, effect)."""
+    key = lambda t: (t.get("key", ""), t.get("effect", ""))  # noqa: E731
+    return len(a) == len(b) and {key(t): t for t in a} == {key(t): t for t in b}
+
+
+@pytest.mark.parametrize("case", PTR_CASES, ids=[c[0] for c in PTR_CASES])
+def test_pod_toleration_restriction(case):
+    import copy
+    name, ctrs, cdefault, ns_default, ns_wl, cwl, pod_tols, merged, admit = case
+    ann = {}
+    if ns_default is not None:
+        ann[PodTolerationRestriction.DEFAULT] = _json.dumps(ns_default)
+    if ns_wl is not None:
+        ann[PodTolerationRestriction.WHITELIST] = _json.dumps(ns_wl)
+    plugin = PodTolerationRestriction(_NsServer(ann), {"default": cdefault, "whitelist": cwl})
+    for op in (CREATE, UPDATE):
+        pod = {"metadata": {"name": "testPod", "namespace": "testNamespace"},
+               "spec": {"containers": copy.deepcopy(ctrs), "tolerations": copy.deepcopy(pod_tols)}}
+        old = None
+        if op == UPDATE:   # an update of an uninitialized pod is handled like a create
+            old = copy.deepcopy(pod)
+            old["metadata"]["initializers"] = {"pending": [{"name": "init"}]}
+            old["spec"]["tolerations"] = [tv("testValue1")]
+        a = Attributes(op, "pods", "", "testNamespace", "testPod", pod, old)
+        if admit:
+            plugin.admit(a)
+            assert _same(pod["spec"]["tolerations"], merged), (name, op)
+        else:
+            with pytest.raises(AdmissionError):
+                plugin.admit(a)
+
+
+def test_pod_toleration_restriction_ignores_updating_initialized_pod():
+    """TestIgnoreUpdatingInitializedPod: no default merge (and so no conflict) on a plain update."""
+    ann = {PodTolerationRestriction.DEFAULT: _json.dumps([tv("testValue2")])}
+    plugin = PodTolerationRestriction(_NsServer(ann), {})
+    pod = {"metadata": {"name": "testPod", "namespace": "testNamespace"},
+           "spec": {"containers": [{"name": "c"}], "tolerations": [tv("testValue1")]}}
+    plugin.admit(Attributes(UPDATE, "pods", "", "testNamespace", "testPod", pod, dict(pod)))
+    assert pod["spec"]["tolerations"] == [tv("testValue1")]
+    assert PodTolerationRestriction(None, {}).handles(CREATE) and PodTolerationRestriction(None, {}).handles(UPDATE)
+    assert not PodTolerationRestriction(None, {}).handles("DELETE")
+
+
+def test_toleration_set_helpers():
+    assert tolerations_conflict([tv("a")], [tv("b")]) and not tolerations_conflict([tv("a")], [tv("a")])
+    assert not tolerations_conflict([tv("a", key="k1")], [tv("b", key="k2")])
+    assert merge_tolerations([tv("a"), tv("x", key="k2")], [tv("b")]) == [tv("b"), tv("x", key="k2")]
+    assert verify_against_whitelist([tv()], []) and verify_against_whitelist([tv()], [tv(), tv(key="o")])
+    assert not verify_against_whitelist([tv("other")], [tv()])
