@@ -15,8 +15,8 @@
     the pod's labels merge env / envFrom / volumes / volumeMounts into every container (conflicts
     reject the preset), annotation `podpreset.admission.kubernetes.io/podpreset-<name>: <rv>`;
     opt-out annotation `podpreset.admission.kubernetes.io/exclude: "true"`.
-  * EventRateLimit — `plugin/pkg/admission/eventratelimit`: token buckets on event creation per
-    Server / Namespace / User (qps, burst); over the limit -> 429.
+  * EventRateLimit — `plugin/pkg/admission/eventratelimit`: token buckets on event writes per
+    Server / Namespace / User / SourceAndObject (qps, burst, LRU cacheSize); over the limit -> 429.
   * PodTolerationRestriction — `plugin/pkg/admission/podtolerationrestriction`: namespace (or
     cluster-config) default tolerations are merged in (conflicts refuse the pod), non-BestEffort
     pods tolerate memory pressure, and the tolerations whitelist is enforced in both phases.
@@ -241,12 +241,14 @@ class PodPreset(Plugin):
 
 
 class _Bucket:
-    def __init__(self, qps, burst):
-        self.qps, self.burst = float(qps), float(burst)
-        self.tokens, self.t = float(burst), time.monotonic()
+    """flowcontrol token bucket (qps refill, `burst` capacity, starts full)."""
+
+    def __init__(self, qps, burst, clock=time.monotonic):
+        self.qps, self.burst, self.clock = float(qps), float(burst), clock
+        self.tokens, self.t = float(burst), clock()
 
     def take(self):
-        now = time.monotonic()
+        now = self.clock()
         self.tokens = min(self.burst, self.tokens + (now - self.t) * self.qps)
         self.t = now
         if self.tokens >= 1:
@@ -255,27 +257,95 @@ class _Bucket:
         return False
 
 
+EVENT_LIMIT_TYPES = ("Server", "Namespace", "User", "SourceAndObject")
+DEFAULT_EVENT_CACHE_SIZE = 4096
+
+
+def validate_event_rate_limit_config(cfg) -> list[str]:
+    """eventratelimit/apis/eventratelimit/validation ValidateConfiguration."""
+    errs = []
+    limits = (cfg or {}).get("limits") or []
+    if not limits:
+        errs.append("limits: Invalid value: must not be empty")
+    for i, lim in enumerate(limits):
+        t = lim.get("type")
+        if t not in EVENT_LIMIT_TYPES:
+            errs.append(f"limits[{i}].type: Unsupported value: {t!r}: supported values: "
+                        + ", ".join(f'"{x}"' for x in EVENT_LIMIT_TYPES))
+        if int(lim.get("burst") or 0) <= 0:
+            errs.append(f"limits[{i}].burst: Invalid value: {lim.get('burst')}: must be positive")
+        if float(lim.get("qps") or 0) <= 0:     # int32 in the reference; fractions allowed here
+            errs.append(f"limits[{i}].qps: Invalid value: {lim.get('qps')}: must be positive")
+        if t != "Server" and int(lim.get("cacheSize") or 0) < 0:
+            errs.append(f"limits[{i}].cacheSize: Invalid value: {lim.get('cacheSize')}: must not be negative")
+    return errs
+
+
+def _source_and_object_key(a):
+    ev = a.obj if isinstance(a.obj, dict) else {}
+    src, io = ev.get("source") or {}, ev.get("involvedObject") or {}
+    return "".join(str(x or "") for x in (src.get("component"), src.get("host"), io.get("kind"), io.get("namespace"),
+                                           io.get("name"), io.get("uid"), io.get("apiVersion")))
+
+
+class _LimitEnforcer:
+    """eventratelimit/limitenforcer.go: one bucket (Server) or an LRU of per-key buckets."""
+
+    KEYS = {"Server": lambda a: "", "Namespace": lambda a: a.namespace or "",
+            "User": lambda a: getattr(a.user, "name", "") if a.user is not None else "",
+            "SourceAndObject": _source_and_object_key}
+
+    def __init__(self, lim, clock):
+        from collections import OrderedDict
+        self.type = lim["type"]
+        self.qps, self.burst, self.clock = lim["qps"], lim["burst"], clock
+        self.key = self.KEYS[self.type]
+        self.size = int(lim.get("cacheSize") or 0) or DEFAULT_EVENT_CACHE_SIZE
+        self.single = _Bucket(self.qps, self.burst, clock) if self.type == "Server" else None
+        self.cache: OrderedDict = OrderedDict()
+
+    def accept(self, a):
+        k = self.key(a)
+        b = self.single
+        if b is None:
+            b = self.cache.get(k)
+            if b is None:
+                b = self.cache[k] = _Bucket(self.qps, self.burst, self.clock)
+                if len(self.cache) > self.size:
+                    self.cache.popitem(last=False)
+            else:
+                self.cache.move_to_end(k)
+        if not b.take():
+            return f"limit reached on type {self.type} for key {k}"
+        return None
+
+
 @register
 class EventRateLimit(Plugin):
+    """`plugin/pkg/admission/eventratelimit`: events (CREATE and UPDATE) pass one token bucket
+    per configured limit — Server, per Namespace, per User or per SourceAndObject (the event's
+    source component + host and involved object kind / namespace / name / uid / apiVersion),
+    the per-key buckets held in an LRU of `cacheSize` (default 4096). Every limit is charged
+    even when an earlier one refuses; any refusal is a 429. The config is validated like the
+    reference (at least one limit, known types, positive qps / burst, non-negative cacheSize)."""
     name = "EventRateLimit"
-    operations = (CREATE,)
+    operations = (CREATE, UPDATE)
 
-    def __init__(self, server=None, config=None):
+    def __init__(self, server=None, config=None, clock=time.monotonic):
         super().__init__(server, config)
-        self.limits = (config or {}).get("limits") or [{"type": "Server", "qps": 5000, "burst": 20000}]
-        self.buckets: dict = {}
+        errs = validate_event_rate_limit_config(config)
+        if errs:
+            raise ValueError("EventRateLimit: " + "; ".join(errs))
+        self.enforcers = [_LimitEnforcer(lim, clock) for lim in config["limits"]]
 
     def validate(self, a):
-        if a.resource != "events":
+        if a.resource != "events" or a.subresource:
             return
-        for lim in self.limits:
-            t = lim.get("type", "Server")
-            key = (t, "" if t == "Server" else a.namespace if t == "Namespace" else getattr(a.user, "name", ""))
-            b = self.buckets.get(key)
-            if b is None:
-                b = self.buckets[key] = _Bucket(lim.get("qps", 10), lim.get("burst", 100))
-            if not b.take():
-                raise AdmissionError("limit reached on type %s for key %s" % (t, key[1]), 429, "TooManyRequests")
+        err = None
+        for e in self.enforcers:
+            err = e.accept(a) or err
+        if err:
+            raise AdmissionError(err, 429, "TooManyRequests")
 
 
 MEMORY_PRESSURE_TAINT = "node.kubernetes.io/memory-pressure"

@@ -131,3 +131,112 @@ def test_podpreset_toleration_restriction_ratelimit_scdeny(run):
             await c.close()
             await s.stop()
     run(main())
+
+
+# -- EventRateLimit: `plugin/pkg/admission/eventratelimit/admission_test.go` TestEventRateLimiting
+
+class _FakeClock:
+    def __init__(self):
+        self.t = 1000.0
+
+    def __call__(self):
+        return self.t
+
+
+def _ev(ns="", user="", event=None, kind="Event", delay=0, ok=True):
+    return {"ns": ns, "user": user, "event": event or {}, "kind": kind, "delay": delay, "ok": ok}
+
+
+def _comp(c, **kw):
+    return _ev(event={"source": {"component": c}}, **kw)
+
+
+def _inclusion(factory):
+    return [_ev(event=factory("A")), _ev(event=factory("A"), ok=False), _ev(event=factory("B"))]
+
+
+ERL_CASES = [
+    ("event not blocked when tokens available", dict(server=3), [_ev()]),
+    ("non-event not blocked", dict(server=3), [_ev(kind="NonEvent")]),
+    ("event blocked after tokens exhausted", dict(server=3), [_ev(), _ev(), _ev(), _ev(ok=False)]),
+    ("non-event not blocked after tokens exhausted", dict(server=3), [_ev(), _ev(), _ev(), _ev(kind="NonEvent")]),
+    ("non-events should not count against limit", dict(server=3), [_ev(), _ev(), _ev(kind="NonEvent"), _ev()]),
+    ("event accepted after token refill", dict(server=3), [_ev(), _ev(), _ev(), _ev(ok=False), _ev(delay=1)]),
+    ("event blocked by namespace limits", dict(server=100, ns=3, ns_cache=10),
+     [_ev("A"), _ev("A"), _ev("A"), _ev("A", ok=False)]),
+    ("event from other namespace not blocked", dict(server=100, ns=3, ns_cache=10),
+     [_ev("A"), _ev("A"), _ev("A"), _ev("B")]),
+    ("events from other namespaces should not count against limit", dict(server=100, ns=3, ns_cache=10),
+     [_ev("A"), _ev("A"), _ev("B"), _ev("A")]),
+    ("event accepted after namespace token refill", dict(server=100, ns=3, ns_cache=10),
+     [_ev("A"), _ev("A"), _ev("A"), _ev("A", ok=False), _ev("A", delay=1)]),
+    ("event from other namespaces should not clear namespace limits", dict(server=100, ns=3, ns_cache=10),
+     [_ev("A"), _ev("A"), _ev("A"), _ev("B"), _ev("A", ok=False)]),
+    ("namespace limits from lru namespace should clear when cache size exceeded", dict(server=100, ns=3, ns_cache=2),
+     [_ev("A"), _ev("A"), _ev("B"), _ev("B"), _ev("B"), _ev("A"), _ev("B", ok=False), _ev("A", ok=False),
+      _ev("C"), _ev("A", ok=False), _ev("B")]),
+    ("event blocked by source+object limits", dict(server=100, so=3, so_cache=10),
+     [_comp("A"), _comp("A"), _comp("A"), _comp("A", ok=False)]),
+    ("event from other source+object not blocked", dict(server=100, so=3, so_cache=10),
+     [_comp("A"), _comp("A"), _comp("A"), _comp("B")]),
+    ("events from other source+object should not count against limit", dict(server=100, so=3, so_cache=10),
+     [_comp("A"), _comp("A"), _comp("B"), _comp("A")]),
+    ("event accepted after source+object token refill", dict(server=100, so=3, so_cache=10),
+     [_comp("A"), _comp("A"), _comp("A"), _comp("A", ok=False), _comp("A", delay=1)]),
+    ("event from other source+object should not clear source+object limits", dict(server=100, so=3, so_cache=10),
+     [_comp("A"), _comp("A"), _comp("A"), _comp("B"), _comp("A", ok=False)]),
+    ("source+object limits from lru source+object should clear when cache size exceeded",
+     dict(server=100, so=3, so_cache=2),
+     [_comp("A"), _comp("A"), _comp("B"), _comp("B"), _comp("B"), _comp("A"), _comp("B", ok=False),
+      _comp("A", ok=False), _comp("C"), _comp("A", ok=False), _comp("B")]),
+    ("source host should be included in source+object key", dict(server=100, so=1, so_cache=10),
+     _inclusion(lambda x: {"source": {"host": x}})),
+    ("involved object kind should be included in source+object key", dict(server=100, so=1, so_cache=10),
+     _inclusion(lambda x: {"involvedObject": {"kind": x}})),
+    ("involved object namespace should be included in source+object key", dict(server=100, so=1, so_cache=10),
+     _inclusion(lambda x: {"involvedObject": {"namespace": x}})),
+    ("involved object name should be included in source+object key", dict(server=100, so=1, so_cache=10),
+     _inclusion(lambda x: {"involvedObject": {"name": x}})),
+    ("involved object UID should be included in source+object key", dict(server=100, so=1, so_cache=10),
+     _inclusion(lambda x: {"involvedObject": {"uid": x}})),
+    ("involved object APIVersion should be included in source+object key", dict(server=100, so=1, so_cache=10),
+     _inclusion(lambda x: {"involvedObject": {"apiVersion": x}})),
+    ("event blocked by user limits", dict(user=3, user_cache=10),
+     [_ev(user="A"), _ev(user="A"), _ev(user="A"), _ev(user="A", ok=False)]),
+]
+
+
+@pytest.mark.parametrize("name,cfg,requests", ERL_CASES, ids=[c[0] for c in ERL_CASES])
+def test_event_rate_limiting(name, cfg, requests):
+    from kubernetes_amd.apiserver.admission import CREATE, AdmissionError, Attributes
+    from kubernetes_amd.apiserver.admission.security import EventRateLimit
+    from kubernetes_amd.apiserver.auth import User
+    limits = []
+    for key, t in (("server", "Server"), ("ns", "Namespace"), ("user", "User"), ("so", "SourceAndObject")):
+        if cfg.get(key):
+            limits.append({"type": t, "qps": 1, "burst": cfg[key], "cacheSize": cfg.get(f"{key}_cache", 0)})
+    clock = _FakeClock()
+    plugin = EventRateLimit(None, {"limits": limits}, clock=clock)
+    for i, rq in enumerate(requests):
+        clock.t += rq["delay"]
+        res = "events" if rq["kind"] == "Event" else "configmaps"
+        a = Attributes(CREATE, res, "", rq["ns"], "name", rq["event"], user=User(rq["user"]))
+        if rq["ok"]:
+            plugin.validate(a)
+        else:
+            with pytest.raises(AdmissionError) as e:
+                plugin.validate(a)
+            assert e.value.code == 429, (name, i)
+
+
+@pytest.mark.parametrize("cfg,match", [
+    (None, "must not be empty"), ({"limits": []}, "must not be empty"),
+    ({"limits": [{"type": "Galaxy", "qps": 1, "burst": 1}]}, "Unsupported value"),
+    ({"limits": [{"type": "Server", "qps": 1, "burst": 0}]}, "burst: Invalid value"),
+    ({"limits": [{"type": "Server", "qps": 0, "burst": 1}]}, "qps: Invalid value"),
+    ({"limits": [{"type": "User", "qps": 1, "burst": 1, "cacheSize": -1}]}, "must not be negative"),
+])
+def test_event_rate_limit_config_validation(cfg, match):
+    from kubernetes_amd.apiserver.admission.security import EventRateLimit
+    with pytest.raises(ValueError, match=match):
+        EventRateLimit(None, cfg)
