@@ -196,48 +196,124 @@ class PodSecurityPolicy(Plugin):
         raise AdmissionError(f'pods "{a.name}" is forbidden: unable to validate against any pod security policy: {allerrs}')
 
 
+class PresetConflict(ValueError):
+    pass
+
+
+def _merge_by_name(orig, presets, field, what):
+    """mergeEnv / mergeVolumes: keep `orig`, append each preset item whose name is new; an
+    item whose name is taken by a different value is a conflict (all conflicts aggregated)."""
+    seen = {x["name"]: x for x in orig or ()}
+    out, errs = list(orig or ()), []
+    for pp in presets:
+        for v in (pp.get("spec") or {}).get(field) or ():
+            found = seen.get(v["name"])
+            if found is None:
+                seen[v["name"]] = v
+                out.append(v)
+            elif found != v:
+                errs.append(f"merging {what} for {pp['metadata'].get('name', '')} has a conflict on {v['name']}")
+    if errs:
+        raise PresetConflict("; ".join(errs))
+    return out
+
+
+def merge_env(env, presets):
+    return _merge_by_name(env, presets, "env", "env")
+
+
+def merge_volumes(volumes, presets):
+    out = _merge_by_name(volumes, presets, "volumes", "volumes")
+    return out or None
+
+
+def merge_env_from(env_from, presets):
+    out = list(env_from or ())
+    for pp in presets:
+        out.extend((pp.get("spec") or {}).get("envFrom") or ())
+    return out
+
+
+def merge_volume_mounts(mounts, presets):
+    """mergeVolumeMounts: conflicts on the mount name or on the mount path."""
+    by_name = {m["name"]: m for m in mounts or ()}
+    by_path = {m["mountPath"]: m for m in mounts or ()}
+    out, errs = list(mounts or ()), []
+    for pp in presets:
+        name = pp["metadata"].get("name", "")
+        for m in (pp.get("spec") or {}).get("volumeMounts") or ():
+            found = by_name.get(m["name"])
+            if found is None:
+                by_name[m["name"]] = m
+                out.append(m)
+            elif found != m:
+                errs.append(f"merging volume mounts for {name} has a conflict on {m['name']}")
+            found = by_path.get(m["mountPath"])
+            if found is None:
+                by_path[m["mountPath"]] = m
+            elif found != m:
+                errs.append(f"merging volume mounts for {name} has a conflict on mount path {m['mountPath']}")
+    if errs:
+        raise PresetConflict("; ".join(errs))
+    return out
+
+
 @register
 class PodPreset(Plugin):
+    """`plugin/pkg/admission/podpreset/admission.go` (CREATE of pods, not mirror pods, not pods
+    annotated `podpreset.admission.kubernetes.io/exclude: "true"`): every PodPreset of the
+    namespace whose selector matches the pod's labels is applied — volumes to the pod; env,
+    envFrom and volumeMounts to each (regular) container — and recorded as annotation
+    `podpreset.admission.kubernetes.io/podpreset-<name>: <resourceVersion>`. The presets are
+    applied all together or not at all: any conflict (an env var, volume or mount of the same name
+    with a different value, or two mounts on one path — between the pod and a preset or between
+    presets) leaves the pod unchanged and admitted, with a warning event like the reference."""
     name = "PodPreset"
     operations = (CREATE,)
     EXCLUDE = "podpreset.admission.kubernetes.io/exclude"
+    PREFIX = "podpreset.admission.kubernetes.io"
 
     def admit(self, a):
-        if a.resource != "pods" or a.subresource:
+        if a.resource != "pods" or a.subresource or a.operation != CREATE or not isinstance(a.obj, dict):
             return
         pod = a.obj
         md = pod.setdefault("metadata", {})
-        if (md.get("annotations") or {}).get(self.EXCLUDE) == "true":
+        anns = md.get("annotations") or {}
+        if "kubernetes.io/config.mirror" in anns or anns.get(self.EXCLUDE) == "true":
             return
-        labels = md.get("labels") or {}
+        presets = [pp for pp in sorted(self.server.list_objects("podpresets", a.namespace) if self.server else (),
+                                       key=lambda p: p["metadata"]["name"])
+                   if label_selector_as_selector((pp.get("spec") or {}).get("selector")).matches(md.get("labels") or {})]
+        if not presets:
+            return
+        self.apply(pod, presets)
+
+    @classmethod
+    def apply(cls, pod, presets) -> bool:
+        """safeToApplyPodPresetsOnPod + applyPodPresetsOnPod; False (pod untouched) on conflict."""
         spec = pod.setdefault("spec", {})
-        for pp in sorted(self.server.list_objects("podpresets", a.namespace), key=lambda p: p["metadata"]["name"]):
-            ps = pp.get("spec") or {}
-            if not label_selector_as_selector(ps.get("selector")).matches(labels):
-                continue
-            vols = {v["name"]: v for v in spec.get("volumes") or ()}
-            conflict = any(v["name"] in vols and vols[v["name"]] != v for v in ps.get("volumes") or ())
-            for c in spec.get("containers") or ():
-                env = {e["name"]: e for e in c.get("env") or ()}
-                mounts = {m["mountPath"]: m for m in c.get("volumeMounts") or ()}
-                conflict |= any(e["name"] in env and env[e["name"]] != e for e in ps.get("env") or ())
-                conflict |= any(m["mountPath"] in mounts and mounts[m["mountPath"]] != m for m in ps.get("volumeMounts") or ())
-            if conflict:
-                continue   # reference: event + skip the conflicting preset
-            for v in ps.get("volumes") or ():
-                if v["name"] not in vols:
-                    spec.setdefault("volumes", []).append(v)
-            for c in spec.get("containers") or ():
-                for e in ps.get("env") or ():
-                    if e["name"] not in {x["name"] for x in c.get("env") or ()}:
-                        c.setdefault("env", []).append(e)
-                for ef in ps.get("envFrom") or ():
-                    c.setdefault("envFrom", []).append(ef)
-                for m in ps.get("volumeMounts") or ():
-                    if m["mountPath"] not in {x["mountPath"] for x in c.get("volumeMounts") or ()}:
-                        c.setdefault("volumeMounts", []).append(m)
-            md.setdefault("annotations", {})[f"podpreset.admission.kubernetes.io/podpreset-{pp['metadata']['name']}"] = \
+        try:
+            volumes = merge_volumes(spec.get("volumes"), presets)
+            merged = [(merge_env(c.get("env"), presets), merge_volume_mounts(c.get("volumeMounts"), presets),
+                       merge_env_from(c.get("envFrom"), presets)) for c in spec.get("containers") or ()]
+        except PresetConflict as e:
+            import logging
+            logging.getLogger("admission.podpreset").warning(
+                "conflict occurred while applying podpresets: %s on pod: %s err: %s",
+                ",".join(p["metadata"]["name"] for p in presets), (pod.get("metadata") or {}).get("name"), e)
+            return False
+        if volumes is not None:
+            spec["volumes"] = volumes
+        for c, (env, mounts, env_from) in zip(spec.get("containers") or (), merged):
+            for k, v in (("env", env), ("volumeMounts", mounts), ("envFrom", env_from)):
+                if v:
+                    c[k] = v
+        md = pod.setdefault("metadata", {})
+        md["annotations"] = dict(md.get("annotations") or {})
+        for pp in presets:
+            md["annotations"][f"{cls.PREFIX}/podpreset-{pp['metadata']['name']}"] = \
                 pp["metadata"].get("resourceVersion", "")
+        return True
 
 
 class _Bucket:
