@@ -53,147 +53,136 @@ def _in_ranges(v, ranges):
     return any(int(r.get("min", 0)) <= v <= int(r.get("max", 0)) for r in ranges or ())
 
 
-class PSPEvaluator:
-    """Validate (and default) one pod against one PodSecurityPolicy. Returns (errors, mutated pod)."""
+def _only_gc_fields_changed(new, old):
+    """rbacregistry.IsOnlyMutatingGCFields: an update touching only ownerReferences / finalizers."""
+    if old is None:
+        return False
 
-    def __init__(self, psp):
-        self.psp = psp
-        self.sp = psp.get("spec") or {}
-
-    def check(self, pod):
-        import copy
-        pod = copy.deepcopy(pod)
-        sp, errs = self.sp, []
-        spec = pod.setdefault("spec", {})
-        name = self.psp["metadata"]["name"]
-        for f in ("hostNetwork", "hostPID", "hostIPC"):
-            if spec.get(f) and not sp.get(f):
-                errs.append(f"{f}: Invalid value: true: {f} is not allowed to be used")
-        vols = sp.get("volumes") or []
-        for v in spec.get("volumes") or ():
-            kind = next((k for k in v if k != "name"), "")
-            if "*" not in vols and kind not in vols:
-                errs.append(f"volumes: {kind} volumes are not allowed to be used")
-            if kind == "hostPath" and sp.get("allowedHostPaths"):
-                p = v["hostPath"].get("path", "")
-                if not any(p == a.get("pathPrefix") or p.startswith(a.get("pathPrefix", "").rstrip("/") + "/")
-                           for a in sp["allowedHostPaths"]):
-                    errs.append(f"volumes.hostPath.path: {p} is not allowed to be used")
-        host_ports = sp.get("hostPorts") or []
-        allowed_caps = set(sp.get("allowedCapabilities") or [])
-        required_drop = set(sp.get("requiredDropCapabilities") or [])
-        default_add = list(sp.get("defaultAddCapabilities") or [])
-        rau = sp.get("runAsUser") or {"rule": "RunAsAny"}
-        for c in _containers(spec):
-            sc = c.setdefault("securityContext", {})
-            cn = c.get("name", "")
-            if sc.get("privileged") and not sp.get("privileged"):
-                errs.append(f"containers[{cn}].securityContext.privileged: Privileged containers are not allowed")
-            for port in c.get("ports") or ():
-                hp = port.get("hostPort")
-                if hp and not _in_ranges(int(hp), host_ports):
-                    errs.append(f"containers[{cn}].hostPort: Invalid value: {hp}: Host port {hp} is not allowed to be used")
-            caps = sc.setdefault("capabilities", {}) if (default_add or required_drop or sc.get("capabilities")) else {}
-            if caps is not None and (default_add or required_drop):
-                add = list(caps.get("add") or [])
-                for d in default_add:
-                    if d not in add:
-                        add.append(d)
-                if add:
-                    caps["add"] = add
-                drop = list(caps.get("drop") or [])
-                for d in sorted(required_drop):
-                    if d not in drop:
-                        drop.append(d)
-                if drop:
-                    caps["drop"] = drop
-            for cap in (sc.get("capabilities") or {}).get("add") or ():
-                if cap in required_drop:
-                    errs.append(f"containers[{cn}].capabilities.add: capability {cap} may not be added")
-                elif "*" not in allowed_caps and cap not in allowed_caps and cap not in default_add:
-                    errs.append(f"containers[{cn}].capabilities.add: capability may not be added: {cap}")
-            rule = rau.get("rule", "RunAsAny")
-            uid = sc.get("runAsUser", _sc(spec).get("runAsUser"))
-            if rule == "MustRunAs":
-                if uid is None:
-                    rng = (rau.get("ranges") or [{"min": 1}])[0]
-                    sc["runAsUser"] = int(rng["min"])
-                elif not _in_ranges(int(uid), rau.get("ranges")):
-                    errs.append(f"containers[{cn}].runAsUser: Invalid value: {uid}: UID on container {cn} does not match required range")
-            elif rule == "MustRunAsNonRoot":
-                if uid == 0 or (uid is None and not sc.get("runAsNonRoot") and not _sc(spec).get("runAsNonRoot")):
-                    if uid == 0:
-                        errs.append(f"containers[{cn}].runAsUser: Invalid value: 0: running with the root UID is forbidden")
-                    else:
-                        sc["runAsNonRoot"] = True
-            if sp.get("readOnlyRootFilesystem"):
-                if sc.get("readOnlyRootFilesystem") is False:
-                    errs.append(f"containers[{cn}].securityContext.readOnlyRootFilesystem: Invalid value: false: "
-                                "ReadOnlyRootFilesystem must be set to true")
-                sc.setdefault("readOnlyRootFilesystem", True)
-            if sp.get("allowPrivilegeEscalation") is False:
-                if sc.get("allowPrivilegeEscalation"):
-                    errs.append(f"containers[{cn}].securityContext.allowPrivilegeEscalation: Invalid value: true: "
-                                "Allowing privilege escalation for containers is not allowed")
-                sc.setdefault("allowPrivilegeEscalation", False)
-            if not sc:
-                c.pop("securityContext", None)
-        pod.setdefault("metadata", {}).setdefault("annotations", {})[PSP_ANN] = name
-        return [f"{name}: {e}" for e in errs], pod
+    def strip(o):
+        o = dict(o)
+        md = dict(o.get("metadata") or {})
+        for k in ("ownerReferences", "finalizers", "resourceVersion", "generation"):
+            md.pop(k, None)
+        o["metadata"] = md
+        return o
+    return strip(new) == strip(old)
 
 
 @register
 class PodSecurityPolicy(Plugin):
+    """`plugin/pkg/admission/security/podsecuritypolicy/admission.go`.
+
+    Policies are taken in name order and each is tried on a copy of the pod (`psp.Provider`:
+    default, then validate). Admit (CREATE) keeps the first policy that validates the pod without
+    changing it, else the first that validates it after defaulting, among the policies the
+    requesting user — or the pod's service account — may `use` (RBAC verb `use` on
+    `podsecuritypolicies` in the pod's namespace); the winner is recorded in annotation
+    `kubernetes.io/psp`. Validate (CREATE and UPDATE, after every mutating plugin) requires a
+    usable policy that accepts the pod unchanged, so a later plugin cannot smuggle in what the
+    policy forbids. Updates touching only ownerReferences / finalizers are ignored. With no
+    policy at all the pod is refused (failOnNoPolicies, the default; config
+    `{"failOnNoPolicies": false}` admits instead). Refusals aggregate the errors of the usable
+    policies only.
+    """
     name = "PodSecurityPolicy"
     operations = (CREATE, UPDATE)
 
-    def _can_use(self, user, psp, ns, sa_name):
+    def __init__(self, server=None, config=None):
+        super().__init__(server, config)
+        self.fail_on_no_policies = (config or {}).get("failOnNoPolicies", True) is not False
+
+    def _can_use(self, user, name, ns, sa_name):
         from ..auth import AttributesRecord, User
         az = getattr(self.server, "authz", None)
         if az is None:
             return True
-        name = psp["metadata"]["name"]
-        subjects = [user] if user is not None else []
+        subjects = []
         if sa_name:
             subjects.append(User(f"system:serviceaccount:{ns}:{sa_name}", "",
                                  ["system:serviceaccounts", f"system:serviceaccounts:{ns}", "system:authenticated"]))
+        if user is not None:
+            subjects.append(user)
+        # 1.9 checks the `extensions` group; `policy` (where later releases moved PSPs) is honoured too
         for u in subjects:
-            for scope in (ns, ""):
-                ok, _ = az.authorize(AttributesRecord(u, "use", scope, "podsecuritypolicies", "", name, "policy", "", True))
+            for group in ("extensions", "policy"):
+                ok, _ = az.authorize(AttributesRecord(u, "use", ns, "podsecuritypolicies", "", name, group, "", True))
                 if ok:
                     return True
         return False
 
-    def admit(self, a):
-        if a.resource != "pods" or a.subresource:
-            return
-        if a.operation == UPDATE:
-            return   # the reference re-validates only on create for pods (spec is immutable)
-        psps = sorted(self.server.list_objects("podsecuritypolicies"), key=lambda p: p["metadata"]["name"])
-        spec = a.obj.get("spec") or {}
-        usable = [p for p in psps if self._can_use(a.user, p, a.namespace, spec.get("serviceAccountName"))]
-        if not usable:
-            raise AdmissionError(f'pods "{a.name}" is forbidden: no providers available to validate pod request')
+    @staticmethod
+    def _ignore(a):
+        if a.resource != "pods" or a.subresource or not isinstance(a.obj, dict):
+            return True
+        return a.operation == UPDATE and _only_gc_fields_changed(a.obj, a.old)
+
+    def _compute(self, a, mutation_allowed):
+        """computeSecurityContext: (allowed pod | None, policy name, errors, fatal message)."""
         import copy
-        orig = copy.deepcopy(a.obj)
-        allerrs, fallback = [], None
-        for p in usable:
-            errs, mutated = PSPEvaluator(p).check(a.obj)
-            if errs:
-                allerrs += errs
+        from .psp import Provider, ProviderError
+        pod = a.obj
+        policies = sorted(self.server.list_objects("podsecuritypolicies") if self.server else (),
+                          key=lambda p: p["metadata"]["name"])
+        if not policies and not self.fail_on_no_policies:
+            return pod, "", [], None
+        providers = []
+        for p in policies:
+            try:
+                providers.append(Provider(p))
+            except ProviderError:
                 continue
-            unchanged = {k: v for k, v in mutated.items() if k != "metadata"} == {k: v for k, v in orig.items() if k != "metadata"}
-            if unchanged:
-                a.obj.clear()
-                a.obj.update(mutated)
-                return
-            if fallback is None:
-                fallback = mutated
-        if fallback is not None:
-            a.obj.clear()
-            a.obj.update(fallback)
+        if not providers:
+            return None, "", [], "no providers available to validate pod request"
+        sa = (pod.get("spec") or {}).get("serviceAccountName")
+        mutated_pod, mutated_name, errors = None, "", {}
+        for prov in providers:
+            cp = copy.deepcopy(pod)
+            errs = prov.assign(cp)
+            if errs:
+                errors[prov.name] = errs
+                continue
+            mutated = cp != pod
+            if mutated and not mutation_allowed:
+                continue
+            if not self._can_use(a.user, prov.name, a.namespace, sa):
+                continue
+            if not mutated:
+                return cp, prov.name, [], None
+            if mutated_pod is None:
+                mutated_pod, mutated_name = cp, prov.name
+        if mutated_pod is not None:
+            return mutated_pod, mutated_name, [], None
+        agg = [f"provider {n}: {e}" for n, errs in errors.items() if self._can_use(a.user, n, a.namespace, sa)
+               for e in errs]
+        return None, "", agg, None
+
+    def _forbid(self, a, msg):
+        md = a.obj.get("metadata") or {}
+        raise AdmissionError(f'pods "{md.get("name") or md.get("generateName") or a.name}" is forbidden: {msg}')
+
+    def admit(self, a):
+        if self._ignore(a) or a.operation != CREATE:
             return
-        raise AdmissionError(f'pods "{a.name}" is forbidden: unable to validate against any pod security policy: {allerrs}')
+        allowed, name, errs, fatal = self._compute(a, True)
+        if fatal:
+            self._forbid(a, fatal)
+        if allowed is None:
+            self._forbid(a, f"unable to validate against any pod security policy: [{', '.join(errs)}]")
+        if allowed is not a.obj:
+            a.obj.clear()
+            a.obj.update(allowed)
+        if name:
+            md = a.obj.setdefault("metadata", {})
+            md["annotations"] = dict(md.get("annotations") or {}, **{PSP_ANN: name})
+
+    def validate(self, a):
+        if self._ignore(a):
+            return
+        allowed, _, errs, fatal = self._compute(a, False)
+        if fatal:
+            self._forbid(a, fatal)
+        if allowed is None or allowed != a.obj:
+            self._forbid(a, f"unable to validate against any pod security policy: [{', '.join(errs)}]")
 
 
 class PresetConflict(ValueError):
