@@ -1549,7 +1549,10 @@ class APIServer:
                 user = UNSECURED
             elif self.authn is not None:
                 ar = getattr(self.authn, "authenticate_request", None)
-                user = ar(req) if ar is not None else self.authn.authenticate(req.headers)
+                if ar is not None and self._blocking_auth()[0]:
+                    user = await asyncio.to_thread(ar, req)
+                else:
+                    user = ar(req) if ar is not None else self.authn.authenticate(req.headers)
                 if user is None:
                     code = 401
                     return _json(401, m.status_obj(401, "Unauthorized", "Unauthorized"))
@@ -1563,7 +1566,7 @@ class APIServer:
                     return _json(e.code, m.status_obj(e.code, "BadRequest", e.message))
             req.user = user
             if p == "/logs" or p.startswith("/logs/"):
-                self._authorize(user, "get", None, "", "", "", "", p, resource_request=False)
+                await self._authz(user, "get", None, "", "", "", "", p, resource_request=False)
                 from ..utils.httpserver import log_dir_response
                 resp = log_dir_response(self.log_dir, p[len("/logs"):].lstrip("/"))
                 code = resp.status
@@ -1599,14 +1602,14 @@ class APIServer:
                 return resp
             if parsed[0] == "componentstatuses":
                 resource = "componentstatuses"
-                self._authorize(user, "get" if parsed[1] else "list", None, "componentstatuses", "", parsed[1] or "", "", p)
+                await self._authz(user, "get" if parsed[1] else "list", None, "componentstatuses", "", parsed[1] or "", "", p)
                 resp = await self._component_statuses(parsed[1])
                 code = resp.status
                 return resp
             if parsed[0] == "bindings":
                 resource, sub = "pods", "binding"
                 body = _body(req)
-                self._authorize(user, "create", parsed[1], "pods", "binding", m.name_of(body), "", p)
+                await self._authz(user, "create", parsed[1], "pods", "binding", m.name_of(body), "", p)
                 await self._retrying(lambda: self.bind(parsed[1], m.name_of(body), body, user))
                 code = 201
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
@@ -1716,6 +1719,25 @@ class APIServer:
                 if line is not None and self.audit.blocking:
                     await self.audit.deliver(line)
 
+    def _blocking_auth(self):
+        """Webhook authenticators / authorizers answer over HTTP: their cache misses run off the
+        event loop so one slow backend never stalls every other request."""
+        flags = getattr(self, "_blocking_flags", None)
+        if flags is None:
+            from .auth import WebhookAuthorizer
+            from .authn import WebhookTokenAuthenticator
+            azs = getattr(self.authz, "authorizers", None) or [self.authz]
+            toks = getattr(self.authn, "tok_auth", None) or ()
+            flags = self._blocking_flags = (any(isinstance(t, WebhookTokenAuthenticator) for t in toks),
+                                            any(isinstance(a, WebhookAuthorizer) for a in azs))
+        return flags
+
+    async def _authz(self, user, verb, ns, resource, sub, name, group, path, resource_request=True):
+        if user is not UNSECURED and self._blocking_auth()[1]:
+            return await asyncio.to_thread(self._authorize, user, verb, ns, resource, sub, name, group, path,
+                                           resource_request)
+        return self._authorize(user, verb, ns, resource, sub, name, group, path, resource_request)
+
     def _authorize(self, user, verb, ns, resource, sub, name, group, path, resource_request=True):
         if user is UNSECURED:
             return                  # the insecure port has no authorization
@@ -1744,20 +1766,20 @@ class APIServer:
                 raise APIError(404, "NotFound", f"the server could not find the requested resource ({req.path})")
         if method in ("GET", "HEAD"):
             if is_watch:
-                self._authorize(user, "watch", ns, ri.plural, sub, name, ri.group, req.path)
+                await self._authz(user, "watch", ns, ri.plural, sub, name, ri.group, req.path)
                 return self._watch(req, ri, ns, name)
             if name is None:
-                self._authorize(user, "list", ns, ri.plural, "", "", ri.group, req.path)
+                await self._authz(user, "list", ns, ri.plural, "", "", ri.group, req.path)
                 if ri.plural in self.uncached:
                     return await self._list_store(req, ri, ns)
                 return self._list(req, ri, ns)
             if sub == "log" and ri.plural == "pods":
-                self._authorize(user, "get", ns, "pods", "log", name, "", req.path)
+                await self._authz(user, "get", ns, "pods", "log", name, "", req.path)
                 return await self._pod_log(ns, name, q)
             if sub in ("exec", "attach", "portforward") and ri.plural == "pods":
-                self._authorize(user, "get", ns, "pods", sub, name, "", req.path)
+                await self._authz(user, "get", ns, "pods", sub, name, "", req.path)
                 return await self._pod_stream(req, ns, name, sub)
-            self._authorize(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
+            await self._authz(user, "get", ns, ri.plural, sub, name, ri.group, req.path)
             if ri.plural in self.uncached:
                 e = (await self._aexisting(ri, ns, name))[1]
             else:
@@ -1775,21 +1797,21 @@ class APIServer:
         body = req.body
         if method == "POST":
             if name is not None and sub == "binding" and ri.plural == "pods":
-                self._authorize(user, "create", ns, "pods", "binding", name, "", req.path)
+                await self._authz(user, "create", ns, "pods", "binding", name, "", req.path)
                 await self.bind(ns, name, _body(req), user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None and sub in ("exec", "attach", "portforward") and ri.plural == "pods":
-                self._authorize(user, "create", ns, "pods", sub, name, "", req.path)
+                await self._authz(user, "create", ns, "pods", sub, name, "", req.path)
                 return await self._pod_stream(req, ns, name, sub)
             if name is not None and sub == "eviction" and ri.plural == "pods":
-                self._authorize(user, "create", ns, "pods", "eviction", name, "", req.path)
+                await self._authz(user, "create", ns, "pods", "eviction", name, "", req.path)
                 await self.evict(ns, name, _body(req) if body else {}, user)
                 return _json(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
             if name is not None:
                 raise APIError(405, "MethodNotAllowed", "POST to a named resource is not allowed")
             if ri.plural in m.VIRTUAL:
                 return self._review(ri, ns, _body(req), user, req)
-            self._authorize(user, "create", ns, ri.plural, "", "", ri.group, req.path)
+            await self._authz(user, "create", ns, ri.plural, "", "", ri.group, req.path)
             obj = _body(req)
             if ri.namespaced and ns is None:
                 ns = (obj.get("metadata") or {}).get("namespace") or "default"
@@ -1801,17 +1823,17 @@ class APIServer:
             raise APIError(405, "MethodNotAllowed", f"{method} requires a name")
         if method == "PUT":
             if ri.plural == "namespaces" and sub == "finalize":
-                self._authorize(user, "update", None, "namespaces", "finalize", name, "", req.path)
+                await self._authz(user, "update", None, "namespaces", "finalize", name, "", req.path)
                 return await self._finalize_namespace(name, _body(req), user)
-            self._authorize(user, "update", ns, ri.plural, sub, name, ri.group, req.path)
+            await self._authz(user, "update", ns, ri.plural, sub, name, ri.group, req.path)
             e = await self.update(ri, ns, name, _body(req), user, sub)
             return _entry_resp(req, ri, 200, e)
         if method == "PATCH":
-            self._authorize(user, "patch", ns, ri.plural, sub, name, ri.group, req.path)
+            await self._authz(user, "patch", ns, ri.plural, sub, name, ri.group, req.path)
             e = await self.patch(ri, ns, name, req.headers.get("content-type", "application/merge-patch+json"), body, user, sub)
             return _entry_resp(req, ri, 200, e)
         if method == "DELETE":
-            self._authorize(user, "delete", ns, ri.plural, "", name, ri.group, req.path)
+            await self._authz(user, "delete", ns, ri.plural, "", name, ri.group, req.path)
             opts = _body(req) if body else {}
             if "gracePeriodSeconds" in q:
                 opts["gracePeriodSeconds"] = int(q["gracePeriodSeconds"])
@@ -1870,7 +1892,7 @@ class APIServer:
         return Response(200, e.raw)
 
     async def _delete_collection(self, req, ri, ns, user):
-        self._authorize(user, "deletecollection", ns, ri.plural, "", "", ri.group, req.path)
+        await self._authz(user, "deletecollection", ns, ri.plural, "", "", ri.group, req.path)
         ls = parse_labels(req.query.get("labelSelector")) if req.query.get("labelSelector") else None
         fs = parse_field_selector(req.query.get("fieldSelector")) if req.query.get("fieldSelector") else None
         opts = codec.loads(req.body) if req.body else {}

@@ -100,3 +100,42 @@ def test_rbac_bootstrap_policy(run):
         finally:
             await s.stop()
     run(main())
+
+
+def test_webhook_authorizer_does_not_block_the_server(run, tmp_path):
+    """A slow SubjectAccessReview backend answers in a worker thread: concurrent requests from
+    different users overlap instead of queueing behind one blocked event loop."""
+    import asyncio
+    import threading
+    import time
+
+    async def h(req):
+        await asyncio.sleep(0.5)
+        return Response(200, json.dumps({"status": {"allowed": True}}).encode())
+    loop = asyncio.new_event_loop()
+    srv = HTTPServer(h)
+    port = loop.run_until_complete(srv.start("127.0.0.1", 0))
+    t = threading.Thread(target=loop.run_forever, daemon=True)
+    t.start()
+    kc = tmp_path / "authz.kubeconfig"
+    kc.write_text(json.dumps({"clusters": [{"name": "", "cluster": {"server": f"http://127.0.0.1:{port}/authorize"}}],
+                              "users": [{"name": "", "user": {}}]}))
+
+    async def main():
+        users = {f"tok{i}": User(f"user{i}", str(i), ["system:authenticated"]) for i in range(4)}
+        s = APIServer(authorization_modes=("Webhook",), tokens=users, authorization_webhook_config_file=str(kc))
+        p = await s.start()
+        clients = [Client(f"http://127.0.0.1:{p}", token=tok) for tok in users]
+        try:
+            t0 = time.monotonic()
+            await asyncio.gather(*(c.list("configmaps", "default") for c in clients))
+            assert time.monotonic() - t0 < 1.5          # serial would take >= 2 s
+        finally:
+            for c in clients:
+                await c.close()
+            await s.stop()
+    try:
+        run(main())
+    finally:
+        loop.call_soon_threadsafe(loop.stop)
+        t.join(5)
