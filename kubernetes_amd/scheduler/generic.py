@@ -521,6 +521,8 @@ class GenericScheduler:
                 col = PR.normalize_minmax(col)
             elif norm == "spread":
                 col = PR.normalize_spread(col, nodes)
+            elif callable(norm):          # a Policy / plugin reduce over the feasible nodes
+                col = norm(col, nodes)
             elif norm:
                 col = PR.normalize(col, reverse)
             for i, s in enumerate(col):

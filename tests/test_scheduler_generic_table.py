@@ -1,0 +1,177 @@
+"""Ported generic-scheduler tables.
+
+Reference: `plugin/pkg/scheduler/core/generic_scheduler_test.go` — TestSelectHost (:117),
+TestGenericScheduler (:183, tests 1-8), TestFindFitAllError / TestFindFitSomeError (:326-408),
+TestHumanReadableFitError (:410), TestZeroRequest (:433). Function-style priorities that see the
+whole node list (`reverseNumericPriority`) use a callable reduce step. SelectorSpreadPriority is
+skipped for a pod with no owner and no service (every node would score 10): TestZeroRequest's
+expected 25 is therefore 15 here — the same ranking, shifted by a constant.
+"""
+import pytest
+
+from kubernetes_amd.scheduler.cache import PodInfo, SchedulerCache
+from kubernetes_amd.scheduler.generic import CycleContext, FitError, GenericScheduler
+
+FAKE = "FakePredicateError"
+
+
+def false_pred(pod, pi, ni, ctx):
+    return FAKE
+
+
+def true_pred(pod, pi, ni, ctx):
+    return None
+
+
+def matches_pred(pod, pi, ni, ctx):
+    return None if pod["metadata"]["name"] == ni.name else FAKE
+
+
+def has_no_pods_pred(pod, pi, ni, ctx):
+    return None if not ni.pods else FAKE
+
+
+def numeric(pod, pi, ni, ctx):
+    return int(ni.name)
+
+
+def reverse_reduce(col, nodes):
+    """reverseNumericPriority: max + min - score over the feasible nodes."""
+    return [max(col) + min(col) - s for s in col]
+
+
+NUMERIC = ("numeric", (1, numeric, False, None))
+REVERSE2 = ("reverse", (2, numeric, False, reverse_reduce))
+EQUAL = ("EqualPriority", 1)
+
+
+def _node(name, cpu_m=None, mem=None):
+    alloc = {"pods": "100"}
+    if cpu_m is not None:
+        alloc.update(cpu=f"{cpu_m}m", memory=str(mem))
+    else:
+        alloc.update(cpu="4", memory="8Gi")
+    return {"metadata": {"name": name}, "spec": {},
+            "status": {"allocatable": alloc, "capacity": dict(alloc), "conditions": [{"type": "Ready", "status": "True"}]}}
+
+
+def _pod(name, node=None, requests=None):
+    c = {"name": "c", "image": "x"}
+    if requests:
+        c["resources"] = {"requests": requests}
+    spec = {"containers": [c]}
+    if node:
+        spec["nodeName"] = node
+    return {"metadata": {"name": name, "namespace": "default", "uid": f"u-{name}-{node}"}, "spec": spec,
+            "status": {"phase": "Running"}}
+
+
+CASES = [
+    ("test 1", [("false", false_pred)], [EQUAL], ["machine1", "machine2"], "2", [], None,
+     {"machine1": FAKE, "machine2": FAKE}),
+    ("test 2", [("true", true_pred)], [EQUAL], ["machine1", "machine2"], "ignore", [], {"machine1", "machine2"}, None),
+    ("test 3", [("matches", matches_pred)], [EQUAL], ["machine1", "machine2"], "machine2", [], {"machine2"}, None),
+    ("test 4", [("true", true_pred)], [NUMERIC], ["3", "2", "1"], "ignore", [], {"3"}, None),
+    ("test 5", [("matches", matches_pred)], [NUMERIC], ["3", "2", "1"], "2", [], {"2"}, None),
+    ("test 6", [("true", true_pred)], [NUMERIC, REVERSE2], ["3", "2", "1"], "2", [], {"1"}, None),
+    ("test 7", [("true", true_pred), ("false", false_pred)], [NUMERIC], ["3", "2", "1"], "2", [], None,
+     {"3": FAKE, "2": FAKE, "1": FAKE}),
+    ("test 8", [("nopods", has_no_pods_pred), ("matches", matches_pred)], [NUMERIC], ["1", "2"], "2",
+     [_pod("2", node="2")], None, {"1": FAKE, "2": FAKE}),
+]
+
+
+@pytest.mark.parametrize("name,preds,prios,nodes,pod_name,pods,expected,want_failed", CASES, ids=[c[0] for c in CASES])
+def test_generic_scheduler(name, preds, prios, nodes, pod_name, pods, expected, want_failed):
+    cache = SchedulerCache()
+    for n in nodes:
+        cache.add_node(_node(n))
+    for p in pods:
+        cache.add_pod(p)
+    gs = GenericScheduler(cache, preds, dict(prios), equivalence_cache=False)
+    pod = _pod(pod_name)
+    if want_failed is not None:
+        with pytest.raises(FitError) as e:
+            gs.schedule(pod)
+        assert e.value.num_nodes == len(nodes)
+        assert e.value.failed == want_failed
+    else:
+        for _ in range(4):       # ties rotate; every answer must be an expected host
+            host, _ = gs.schedule(pod)
+            assert host in expected, name
+
+
+@pytest.mark.parametrize("scores,possible", [
+    ({"machine1.1": 1, "machine2.1": 2}, {"machine2.1"}),
+    ({"machine1.1": 1, "machine1.2": 2, "machine1.3": 2, "machine2.1": 2}, {"machine1.2", "machine1.3", "machine2.1"}),
+    ({"machine1.1": 3, "machine1.2": 3, "machine2.1": 2, "machine3.1": 1, "machine1.3": 3},
+     {"machine1.1", "machine1.2", "machine1.3"}),
+])
+def test_select_host(scores, possible):
+    gs = GenericScheduler(SchedulerCache(), [], {})
+
+    class N:
+        def __init__(self, name):
+            self.name = name
+    nodes = [N(n) for n in scores]
+    seen = {gs.select_host(scores, nodes) for _ in range(10)}
+    assert seen <= possible
+    if len(possible) > 1:
+        assert len(seen) > 1            # equal scores are spread round-robin
+
+
+def test_select_host_empty_list_is_an_error():
+    with pytest.raises(ValueError):
+        GenericScheduler(SchedulerCache(), [], {}).select_host({}, [])
+
+
+def test_find_fit_all_error_and_some_error():
+    cache = SchedulerCache()
+    for n in ("3", "2", "1"):
+        cache.add_node(_node(n))
+    gs = GenericScheduler(cache, [("true", true_pred), ("false", false_pred)], {}, equivalence_cache=False)
+    with pytest.raises(FitError) as e:
+        gs.schedule(_pod("x"))
+    assert e.value.failed == {"3": FAKE, "2": FAKE, "1": FAKE}
+    # TestFindFitSomeError: only node "1" matches; the other two report the fake predicate
+    gs = GenericScheduler(cache, [("true", true_pred), ("match", matches_pred)], {}, equivalence_cache=False)
+    host, _ = gs.schedule(_pod("1"))
+    assert host == "1"
+    gs2 = GenericScheduler(cache, [("match", matches_pred), ("false", false_pred)], {}, equivalence_cache=False)
+    with pytest.raises(FitError) as e:
+        gs2.schedule(_pod("1"))
+    assert set(e.value.failed) == {"1", "2", "3"} and e.value.failed["2"] == FAKE
+
+
+def test_human_readable_fit_error():
+    err = FitError(_pod("2"), 3, {"1": "NodeUnderMemoryPressure", "2": "NodeUnderDiskPressure",
+                                  "3": "NodeUnderDiskPressure"})
+    s = str(err)
+    assert "0/3 nodes are available" in s and "2 NodeUnderDiskPressure" in s and "1 NodeUnderMemoryPressure" in s
+
+
+DEFAULT_CPU_M, DEFAULT_MEM = 100, 200 * 1024 * 1024
+
+
+@pytest.mark.parametrize("case", ["zero-request pod", "nonzero-request pod", "larger pod"])
+def test_zero_request(case):
+    """A zero-request pod counts as the default request (100m, 200Mi) in LeastRequested and
+    BalancedResourceAllocation, whether it is being scheduled or already on the node."""
+    small = {"cpu": f"{DEFAULT_CPU_M}m", "memory": str(DEFAULT_MEM)}
+    large = {"cpu": f"{DEFAULT_CPU_M * 3}m", "memory": str(DEFAULT_MEM * 3)}
+    cache = SchedulerCache()
+    for n in ("machine1", "machine2"):
+        cache.add_node(_node(n, 1000, DEFAULT_MEM * 10))
+    for p in (_pod("large1", "machine1", large), _pod("zero1", "machine1"), _pod("large2", "machine2", large),
+              _pod("small2", "machine2", small)):
+        cache.add_pod(p)
+    pod = {"zero-request pod": _pod("new"), "nonzero-request pod": _pod("new", requests=small),
+           "larger pod": _pod("new", requests=large)}[case]
+    gs = GenericScheduler(cache, [], {"LeastRequestedPriority": 1, "BalancedResourceAllocation": 1,
+                                      "SelectorSpreadPriority": 1}, equivalence_cache=False)
+    nodes = [cache.nodes["machine1"], cache.nodes["machine2"]]
+    scores = gs.prioritize(pod, PodInfo(pod), nodes, CycleContext(cache, pod))
+    if case == "larger pod":
+        assert all(s != 15 for s in scores.values()), scores
+    else:
+        assert all(s == 15 for s in scores.values()), scores
