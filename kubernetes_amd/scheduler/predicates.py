@@ -57,9 +57,13 @@ def pod_fits_host_ports(pod, pi, ni, ctx):
 
 
 def _node_affinity_terms(pod):
+    """None without a required node selector; else its terms — an empty / missing term list
+    matches no node (`predicates.go` podMatchesNodeLabels / nodeMatchesNodeSelectorTerms)."""
     aff = ((pod.get("spec") or {}).get("affinity") or {}).get("nodeAffinity") or {}
-    req = aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}
-    return req.get("nodeSelectorTerms")
+    req = aff.get("requiredDuringSchedulingIgnoredDuringExecution")
+    if req is None:
+        return None
+    return req.get("nodeSelectorTerms") or []
 
 
 def _term_matches(term, ni):

@@ -175,3 +175,57 @@ def test_zero_request(case):
         assert all(s != 15 for s in scores.values()), scores
     else:
         assert all(s == 15 for s in scores.values()), scores
+
+
+# -- predicates_test.go TestPodFitsSelector ------------------------------------------------------
+
+def _req(*terms):
+    return {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": list(terms)}}}
+
+
+def _term(*exprs):
+    return {"matchExpressions": [dict(zip(("key", "operator", "values"), e)) if len(e) == 3 else
+                                 {"key": e[0], "operator": e[1]} for e in exprs]}
+
+
+SELECTOR_CASES = [
+    ("no selector", {}, {}, True),
+    ("missing labels", {"nodeSelector": {"foo": "bar"}}, {}, False),
+    ("same labels", {"nodeSelector": {"foo": "bar"}}, {"foo": "bar"}, True),
+    ("node labels are superset", {"nodeSelector": {"foo": "bar"}}, {"foo": "bar", "baz": "blah"}, True),
+    ("node labels are subset", {"nodeSelector": {"foo": "bar", "baz": "blah"}}, {"foo": "bar"}, False),
+    ("In matches", {"affinity": _req(_term(("foo", "In", ["bar", "value2"])))}, {"foo": "bar"}, True),
+    ("Gt matches", {"affinity": _req(_term(("kernel-version", "Gt", ["0204"])))}, {"kernel-version": "0206"}, True),
+    ("NotIn matches", {"affinity": _req(_term(("mem-type", "NotIn", ["DDR", "DDR2"])))}, {"mem-type": "DDR3"}, True),
+    ("Exists matches", {"affinity": _req(_term(("GPU", "Exists")))}, {"GPU": "NVIDIA-GRID-K1"}, True),
+    ("affinity does not match", {"affinity": _req(_term(("foo", "In", ["value1", "value2"])))}, {"foo": "bar"}, False),
+    ("nil NodeSelectorTerms", {"affinity": {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {}}}},
+     {"foo": "bar"}, False),
+    ("empty NodeSelectorTerms", {"affinity": _req()}, {"foo": "bar"}, False),
+    ("empty MatchExpressions", {"affinity": _req({"matchExpressions": []})}, {"foo": "bar"}, False),
+    ("no Affinity", {}, {"foo": "bar"}, True),
+    ("Affinity but nil NodeSelector", {"affinity": {"nodeAffinity": {}}}, {"foo": "bar"}, True),
+    ("multiple matchExpressions ANDed, match",
+     {"affinity": _req(_term(("GPU", "Exists"), ("GPU", "NotIn", ["AMD", "INTER"])))}, {"GPU": "NVIDIA-GRID-K1"}, True),
+    ("multiple matchExpressions ANDed, no match",
+     {"affinity": _req(_term(("GPU", "Exists"), ("GPU", "In", ["AMD", "INTER"])))}, {"GPU": "NVIDIA-GRID-K1"}, False),
+    ("multiple NodeSelectorTerms ORed",
+     {"affinity": _req(_term(("foo", "In", ["bar", "value2"])), _term(("diffkey", "In", ["wrong", "value2"])))},
+     {"foo": "bar"}, True),
+    ("Affinity and NodeSelector both satisfied",
+     {"nodeSelector": {"foo": "bar"}, "affinity": _req(_term(("foo", "Exists")))}, {"foo": "bar"}, True),
+    ("Affinity matches but NodeSelector does not",
+     {"nodeSelector": {"foo": "bar"}, "affinity": _req(_term(("foo", "Exists")))}, {"foo": "barrrrrr"}, False),
+]
+
+
+@pytest.mark.parametrize("name,spec,labels,fits", SELECTOR_CASES, ids=[c[0] for c in SELECTOR_CASES])
+def test_pod_fits_selector(name, spec, labels, fits):
+    from kubernetes_amd.scheduler.predicates import match_node_selector
+    cache = SchedulerCache()
+    node = _node("machine1")
+    node["metadata"]["labels"] = labels
+    cache.add_node(node)
+    pod = {"metadata": {"name": "p", "namespace": "default"}, "spec": dict(spec, containers=[{"name": "c"}])}
+    got = match_node_selector(pod, PodInfo(pod), cache.nodes["machine1"], None)
+    assert (got is None) == fits, (name, got)
