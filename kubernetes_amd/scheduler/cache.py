@@ -194,7 +194,7 @@ DEFAULT_FAILURE_DOMAINS = ("kubernetes.io/hostname", "failure-domain.beta.kubern
 class NodeInfo:
     __slots__ = ("node", "name", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
                  "req_cpu", "req_mem", "req_eph", "req_scalars", "nz_cpu", "nz_mem", "pods", "ports", "er", "generation",
-                 "ready", "unschedulable", "mem_pressure", "disk_pressure", "gpu_total", "images")
+                 "ready", "unschedulable", "mem_pressure", "disk_pressure", "gpu_total", "images", "cond_reason")
 
     def __init__(self, name=""):
         self.node = None
@@ -211,6 +211,7 @@ class NodeInfo:
         self.er = ERManager()
         self.generation = 0
         self.ready = True
+        self.cond_reason = None     # OutOfDisk / NetworkUnavailable not False (CheckNodeConditionPredicate)
         self.unschedulable = False
         self.mem_pressure = False
         self.disk_pressure = False
@@ -233,11 +234,16 @@ class NodeInfo:
         self.alloc_scalars = {k: _q(v).int_value() for k, v in alloc.items()
                               if k not in ("cpu", "memory", "ephemeral-storage", "pods")}
         self.ready = True
+        self.cond_reason = None
         self.mem_pressure = self.disk_pressure = False
         for c in st.get("conditions") or ():
             t, s = c.get("type"), c.get("status")
             if t == "Ready":
                 self.ready = s == "True"
+            elif t == "OutOfDisk" and s != "False":
+                self.cond_reason = self.cond_reason or "node(s) were out of disk space"
+            elif t == "NetworkUnavailable" and s != "False":
+                self.cond_reason = self.cond_reason or "node(s) had unavailable network"
             elif t == "MemoryPressure":
                 self.mem_pressure = s == "True"
             elif t == "DiskPressure":
@@ -256,7 +262,7 @@ class NodeInfo:
         c = NodeInfo(self.name)
         for s in ("node", "labels", "taints", "alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalars",
                   "req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "generation", "ready", "unschedulable",
-                  "mem_pressure", "disk_pressure", "gpu_total", "images"):
+                  "mem_pressure", "disk_pressure", "gpu_total", "images", "cond_reason"):
             setattr(c, s, getattr(self, s))
         c.req_scalars = dict(self.req_scalars)
         c.pods = dict(self.pods)

@@ -13,8 +13,15 @@ from ..api.labels import SelectorError, label_selector_as_selector, node_selecto
 
 
 def check_node_condition(pod, pi, ni, ctx):
+    """`predicates.go:1414` CheckNodeConditionPredicate: Ready must be True, OutOfDisk and
+    NetworkUnavailable False, and the node schedulable (a pod tolerating the
+    `node.kubernetes.io/unschedulable` taint may still go there, as later releases allow)."""
+    if ni.node is None:
+        return "node(s) had unknown conditions"
     if not ni.ready:
         return "node(s) were not ready"
+    if ni.cond_reason:
+        return ni.cond_reason
     if ni.unschedulable and not ctx.tolerates_unschedulable:
         return "node(s) were unschedulable"
     return None

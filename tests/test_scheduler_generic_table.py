@@ -229,3 +229,244 @@ def test_pod_fits_selector(name, spec, labels, fits):
     pod = {"metadata": {"name": "p", "namespace": "default"}, "spec": dict(spec, containers=[{"name": "c"}])}
     got = match_node_selector(pod, PodInfo(pod), cache.nodes["machine1"], None)
     assert (got is None) == fits, (name, got)
+
+
+# -- predicates_test.go TestInterPodAffinity -----------------------------------------------------
+
+SEC = {"service": "securityscan"}
+SEC2 = {"security": "S1"}
+
+
+def _sel(*exprs):
+    return {"matchExpressions": [{"key": k, "operator": op, **({"values": v} if v is not None else {})}
+                                 for k, op, v in exprs]}
+
+
+def _aff_term(*exprs, key="region", namespaces=None):
+    t = {"labelSelector": _sel(*exprs)}
+    if key:
+        t["topologyKey"] = key
+    if namespaces:
+        t["namespaces"] = namespaces
+    return t
+
+
+def _affinity(aff=(), anti=()):
+    out = {}
+    if aff:
+        out["podAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": list(aff)}
+    if anti:
+        out["podAntiAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": list(anti)}
+    return out
+
+
+def _apod(name, labels, node=None, affinity=None, ns="default"):
+    spec = {"containers": [{"name": "c"}]}
+    if node:
+        spec["nodeName"] = node
+    if affinity:
+        spec["affinity"] = affinity
+    return {"metadata": {"name": name, "namespace": ns, "uid": f"u-{name}", "labels": labels}, "spec": spec,
+            "status": {"phase": "Running"}}
+
+
+IN_SEC = ("service", "In", ["securityscan", "value2"])
+IN_AV = ("service", "In", ["antivirusscan", "value2"])
+AFFINITY_CASES = [
+    ("no required pod affinity, empty node", _apod("p", {}), [], True),
+    ("PodAffinity In matches the existing pod",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(IN_SEC)])), [_apod("e", SEC, "machine1")], True),
+    ("PodAffinity NotIn matches the existing pod",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(("service", "NotIn", ["securityscan3", "value3"]))])),
+     [_apod("e", SEC, "machine1")], True),
+    ("diff Namespace",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(IN_SEC, key="", namespaces=["DiffNameSpace"])])),
+     [_apod("e", SEC, "machine1", ns="ns")], False),
+    ("unmatching labelSelector", _apod("p", SEC, affinity=_affinity([_aff_term(IN_AV, key="")])),
+     [_apod("e", SEC, "machine1")], False),
+    ("different label operators in multiple terms",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(("service", "Exists", None), ("wrongkey", "DoesNotExist", None)),
+                                          _aff_term(("service", "In", ["securityscan"]),
+                                                    ("service", "NotIn", ["WrongValue"]))])),
+     [_apod("e", SEC, "machine1")], True),
+    ("matchExpressions are ANDed",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(("service", "Exists", None), ("wrongkey", "DoesNotExist", None)),
+                                          _aff_term(("service", "In", ["securityscan2"]),
+                                                    ("service", "NotIn", ["WrongValue"]))])),
+     [_apod("e", SEC, "machine1")], False),
+    ("PodAffinity and PodAntiAffinity",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(IN_SEC)], [_aff_term(IN_AV, key="node")])),
+     [_apod("e", SEC, "machine1")], True),
+    ("PodAffinity, PodAntiAffinity and symmetry",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(IN_SEC)], [_aff_term(IN_AV, key="node")])),
+     [_apod("e", SEC, "machine1", affinity=_affinity(anti=[_aff_term(IN_AV, key="node")]))], True),
+    ("PodAffinity but not PodAntiAffinity",
+     _apod("p", SEC2, affinity=_affinity([_aff_term(IN_SEC)], [_aff_term(IN_SEC, key="zone")])),
+     [_apod("e", SEC, "machine1")], False),
+    ("existing pod's anti-affinity symmetry violated",
+     _apod("p", SEC, affinity=_affinity([_aff_term(IN_SEC)], [_aff_term(IN_AV, key="node")])),
+     [_apod("e", SEC, "machine1", affinity=_affinity(anti=[_aff_term(IN_SEC, key="zone")]))], False),
+    ("pod matches its own label NotIn",
+     _apod("p", SEC, affinity=_affinity([_aff_term(("service", "NotIn", ["securityscan", "value2"]))])),
+     [_apod("e", SEC, "machine2")], False),
+    ("existing pod anti-affinity respected without own constraints",
+     _apod("p", SEC), [_apod("e", SEC, "machine1", affinity=_affinity(anti=[_aff_term(IN_SEC, key="zone")]))], False),
+    ("existing pod anti-affinity satisfied without own constraints",
+     _apod("p", SEC), [_apod("e", SEC, "machine1", affinity=_affinity(
+         anti=[_aff_term(("service", "NotIn", ["securityscan", "value2"]), key="zone")]))], True),
+]
+
+
+@pytest.mark.parametrize("name,pod,pods,fits", AFFINITY_CASES, ids=[c[0] for c in AFFINITY_CASES])
+def test_inter_pod_affinity(name, pod, pods, fits):
+    from kubernetes_amd.scheduler.predicates import match_inter_pod_affinity
+    cache = SchedulerCache()
+    node = _node("machine1")
+    node["metadata"]["labels"] = {"region": "r1", "zone": "z11"}
+    cache.add_node(node)
+    for p in pods:
+        cache.add_pod(p)
+    got = match_inter_pod_affinity(pod, PodInfo(pod), cache.nodes["machine1"], CycleContext(cache, pod))
+    assert (got is None) == fits, (name, got)
+
+
+# -- predicates_test.go TestInterPodAffinityWithMultipleNodes ------------------------------------
+
+CN, CN_AZ, IN_, US = {"region": "China"}, {"region": "China", "az": "az1"}, {"region": "India"}, {"region": "US"}
+MULTI_CASES = [
+    ("same topology value as a node with a matching pod",
+     _apod("p", {}, affinity=_affinity([_aff_term(("foo", "In", ["bar"]))])),
+     [_apod("e", {"foo": "bar"}, "machine1")], [("machine1", CN), ("machine2", CN_AZ), ("machine3", IN_)],
+     {"machine1": True, "machine2": True, "machine3": False}),
+    ("node affinity excludes nodeA, pod affinity satisfied through nodeB's region",
+     dict(_apod("p", {}, affinity=dict(_affinity([_aff_term(("foo", "In", ["abc"]))]),
+                                        **_req(_term(("hostname", "NotIn", ["h1"])))))),
+     [_apod("a", {"foo": "abc"}, "nodeA"), _apod("b", {"foo": "def"}, "nodeB")],
+     [("nodeA", {"region": "r1", "hostname": "h1"}), ("nodeB", {"region": "r1", "hostname": "h2"})],
+     {"nodeA": False, "nodeB": True}),
+    ("first pod of a collection may go anywhere",
+     _apod("p", {"foo": "bar"}, affinity=_affinity([_aff_term(("foo", "In", ["bar"]), key="zone")])), [],
+     [("nodeA", {"zone": "az1", "hostname": "h1"}), ("nodeB", {"zone": "az2", "hostname": "h2"})],
+     {"nodeA": True, "nodeB": True}),
+    ("anti-affinity blocks the whole region",
+     _apod("p", {}, affinity=_affinity(anti=[_aff_term(("foo", "In", ["abc"]))])), [_apod("a", {"foo": "abc"}, "nodeA")],
+     [("nodeA", {"region": "r1", "hostname": "nodeA"}), ("nodeB", {"region": "r1", "hostname": "nodeB"})],
+     {"nodeA": False, "nodeB": False}),
+    ("anti-affinity blocks China, India is free",
+     _apod("p", {}, affinity=_affinity(anti=[_aff_term(("foo", "In", ["abc"]))])), [_apod("a", {"foo": "abc"}, "nodeA")],
+     [("nodeA", CN), ("nodeB", CN_AZ), ("nodeC", IN_)], {"nodeA": False, "nodeB": False, "nodeC": True}),
+    ("own anti-affinity plus an existing pod's anti-affinity",
+     _apod("p", {"foo": "123"}, affinity=_affinity(anti=[_aff_term(("foo", "In", ["bar"]))])),
+     [_apod("a", {"foo": "bar"}, "nodeA"),
+      _apod("c", {}, "nodeC", affinity=_affinity(anti=[_aff_term(("foo", "In", ["123"]))]))],
+     [("nodeA", CN), ("nodeB", CN_AZ), ("nodeC", IN_), ("nodeD", US)],
+     {"nodeA": False, "nodeB": False, "nodeC": False, "nodeD": True}),
+    ("an existing pod's anti-affinity in another namespace does not apply",
+     _apod("p", {"foo": "123"}, ns="NS1", affinity=_affinity(anti=[_aff_term(("foo", "In", ["bar"]))])),
+     [_apod("a", {"foo": "bar"}, "nodeA", ns="NS1"),
+      _apod("c", {}, "nodeC", ns="NS2", affinity=_affinity(anti=[_aff_term(("foo", "In", ["123"]))]))],
+     [("nodeA", CN), ("nodeB", CN_AZ), ("nodeC", IN_)], {"nodeA": False, "nodeB": False, "nodeC": True}),
+]
+
+
+@pytest.mark.parametrize("name,pod,pods,nodes,fits", MULTI_CASES, ids=[c[0] for c in MULTI_CASES])
+def test_inter_pod_affinity_with_multiple_nodes(name, pod, pods, nodes, fits):
+    from kubernetes_amd.scheduler.predicates import match_inter_pod_affinity, match_node_selector
+    cache = SchedulerCache()
+    for n, labels in nodes:
+        node = _node(n)
+        node["metadata"]["labels"] = labels
+        cache.add_node(node)
+    for p in pods:
+        cache.add_pod(p)
+    ctx = CycleContext(cache, pod)
+    for n, _ in nodes:
+        ni = cache.nodes[n]
+        ok = match_inter_pod_affinity(pod, PodInfo(pod), ni, ctx) is None and \
+            match_node_selector(pod, PodInfo(pod), ni, ctx) is None
+        assert ok == fits[n], (name, n)
+
+
+# -- predicates_test.go TestPodToleratesTaints / pressure conditions / TestNodeConditionPredicate -
+
+def _tol(key, value=None, effect=None, op=None):
+    t = {"key": key}
+    for k, v in (("value", value), ("effect", effect), ("operator", op)):
+        if v is not None:
+            t[k] = v
+    return t
+
+
+TAINT_CASES = [
+    ("no tolerations vs taint", [], [{"key": "dedicated", "value": "user1", "effect": "NoSchedule"}], False),
+    ("dedicated to user1", [_tol("dedicated", "user1", "NoSchedule")],
+     [{"key": "dedicated", "value": "user1", "effect": "NoSchedule"}], True),
+    ("dedicated to user2", [_tol("dedicated", "user2", "NoSchedule", "Equal")],
+     [{"key": "dedicated", "value": "user1", "effect": "NoSchedule"}], False),
+    ("Exists tolerates", [_tol("foo", None, "NoSchedule", "Exists")],
+     [{"key": "foo", "value": "bar", "effect": "NoSchedule"}], True),
+    ("all taints tolerated", [_tol("dedicated", "user2", "NoSchedule", "Equal"), _tol("foo", None, "NoSchedule", "Exists")],
+     [{"key": "dedicated", "value": "user2", "effect": "NoSchedule"}, {"key": "foo", "value": "bar", "effect": "NoSchedule"}],
+     True),
+    ("non-empty effect mismatch", [_tol("foo", "bar", "PreferNoSchedule", "Equal")],
+     [{"key": "foo", "value": "bar", "effect": "NoSchedule"}], False),
+    ("empty effect tolerates all effects", [_tol("foo", "bar", None, "Equal")],
+     [{"key": "foo", "value": "bar", "effect": "NoSchedule"}], True),
+    ("PreferNoSchedule is not enforced", [_tol("dedicated", "user2", "NoSchedule", "Equal")],
+     [{"key": "dedicated", "value": "user1", "effect": "PreferNoSchedule"}], True),
+    ("no toleration, only PreferNoSchedule", [], [{"key": "dedicated", "value": "user1", "effect": "PreferNoSchedule"}],
+     True),
+]
+
+
+@pytest.mark.parametrize("name,tols,taints,fits", TAINT_CASES, ids=[c[0] for c in TAINT_CASES])
+def test_pod_tolerates_taints(name, tols, taints, fits):
+    from kubernetes_amd.scheduler.predicates import pod_tolerates_node_taints
+    cache = SchedulerCache()
+    node = _node("n")
+    node["spec"]["taints"] = taints
+    cache.add_node(node)
+    pod = {"metadata": {"name": "p", "namespace": "default"}, "spec": {"containers": [{"name": "c"}],
+                                                                       "tolerations": tols}}
+    assert (pod_tolerates_node_taints(pod, PodInfo(pod), cache.nodes["n"], None) is None) == fits
+
+
+@pytest.mark.parametrize("best_effort,pressure,fits", [(True, False, True), (True, True, False), (False, True, True),
+                                                       (False, False, True)])
+def test_memory_pressure(best_effort, pressure, fits):
+    from kubernetes_amd.scheduler.predicates import check_node_memory_pressure
+    cache = SchedulerCache()
+    node = _node("n")
+    node["status"]["conditions"].append({"type": "MemoryPressure", "status": "True" if pressure else "False"})
+    cache.add_node(node)
+    pod = _pod("p", requests=None if best_effort else {"cpu": "100m", "memory": "100"})
+    assert (check_node_memory_pressure(pod, PodInfo(pod), cache.nodes["n"], None) is None) == fits
+
+
+@pytest.mark.parametrize("pressure,fits", [(False, True), (True, False)])
+def test_disk_pressure(pressure, fits):
+    from kubernetes_amd.scheduler.predicates import check_node_disk_pressure
+    cache = SchedulerCache()
+    node = _node("n")
+    node["status"]["conditions"].append({"type": "DiskPressure", "status": "True" if pressure else "False"})
+    cache.add_node(node)
+    pod = _pod("p")
+    assert (check_node_disk_pressure(pod, PodInfo(pod), cache.nodes["n"], None) is None) == fits
+
+
+@pytest.mark.parametrize("conditions,unschedulable,fits", [
+    ([("Ready", "True")], False, True), ([("Ready", "False")], False, False), ([("OutOfDisk", "True")], False, False),
+    ([("OutOfDisk", "False")], False, True), ([("Ready", "True"), ("OutOfDisk", "True")], False, False),
+    ([("Ready", "True"), ("OutOfDisk", "False")], False, True), ([("Ready", "False"), ("OutOfDisk", "True")], False, False),
+    ([("Ready", "False"), ("OutOfDisk", "False")], False, False), ([], True, False), ([], False, True),
+    ([("Ready", "True"), ("NetworkUnavailable", "True")], False, False),
+])
+def test_node_condition_predicate(conditions, unschedulable, fits):
+    from kubernetes_amd.scheduler.predicates import check_node_condition
+    cache = SchedulerCache()
+    node = {"metadata": {"name": "n"}, "spec": {"unschedulable": unschedulable},
+            "status": {"allocatable": {"cpu": "1", "memory": "1Gi", "pods": "10"},
+                       "conditions": [{"type": t, "status": s} for t, s in conditions]}}
+    cache.add_node(node)
+    pod = _pod("p")
+    assert (check_node_condition(pod, PodInfo(pod), cache.nodes["n"], CycleContext(cache, pod)) is None) == fits
