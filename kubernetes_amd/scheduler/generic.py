@@ -62,11 +62,12 @@ class CycleContext:
         self.tolerates_unschedulable = any(
             t.get("key") == "node.kubernetes.io/unschedulable" and t.get("operator") == "Exists"
             for t in spec.get("tolerations") or ())
-        ref = None
+        ref = kind = None
         for r in pod["metadata"].get("ownerReferences") or ():
             if r.get("controller"):
-                ref = r.get("uid")
+                ref, kind = r.get("uid"), r.get("kind")
         self.owner_uid = ref
+        self.owner_kind = kind
         self.node_affinity_prefs = PR.compile_node_affinity_prefs(pod)
         self.topo_scores = {}
         self.anti_affinity_terms = cache_anti_affinity(cache) if with_affinity else []

@@ -137,11 +137,40 @@ def taint_toleration(pod, pi, ni, ctx):
     return float(sum(1 for t in ni.taints if t.get("effect") == core.TAINT_PREFER_NO_SCHEDULE and not core.tolerates(tols, t)))
 
 
+_AVOID_CACHE: dict = {}
+
+
+def _avoided_controllers(raw):
+    """{(kind, uid)} of a node's `scheduler.alpha.kubernetes.io/preferAvoidPods` annotation
+    (`v1helper.GetAvoidPodsFromNodeAnnotations`); a malformed annotation avoids nothing."""
+    hit = _AVOID_CACHE.get(raw)
+    if hit is None:
+        import json
+        hit = set()
+        try:
+            for a in (json.loads(raw) or {}).get("preferAvoidPods") or ():
+                pc = (a.get("podSignature") or {}).get("podController")
+                if pc:
+                    hit.add((pc.get("kind"), pc.get("uid")))
+        except (ValueError, AttributeError, TypeError):
+            hit = set()
+        if len(_AVOID_CACHE) > 1024:
+            _AVOID_CACHE.clear()
+        _AVOID_CACHE[raw] = hit
+    return hit
+
+
 def node_prefer_avoid_pods(pod, pi, ni, ctx):
-    ann = ((ni.node or {}).get("metadata") or {}).get("annotations") or {}
-    if "scheduler.alpha.kubernetes.io/preferAvoidPods" not in ann or not ctx.owner_uid:
+    """`node_prefer_avoid_pods.go` NodePreferAvoidPodsPriorityMap: 0 on a node whose
+    preferAvoidPods annotation names the pod's controlling ReplicationController / ReplicaSet
+    (by kind and uid), else 10; other controller kinds are ignored."""
+    if ctx.owner_kind not in ("ReplicationController", "ReplicaSet") or not ctx.owner_uid:
         return MAX
-    return 0.0 if ctx.owner_uid in ann["scheduler.alpha.kubernetes.io/preferAvoidPods"] else MAX
+    anns = ((ni.node or {}).get("metadata") or {}).get("annotations") or {}
+    raw = anns.get("scheduler.alpha.kubernetes.io/preferAvoidPods")
+    if not raw:
+        return MAX
+    return 0.0 if (ctx.owner_kind, ctx.owner_uid) in _avoided_controllers(raw) else MAX
 
 
 def xgmi_topology(pod, pi, ni, ctx):

@@ -1,0 +1,165 @@
+"""Ported resource-priority tables.
+
+Reference: `plugin/pkg/scheduler/algorithm/priorities/least_requested_test.go`,
+`most_requested_test.go` and `balanced_resource_allocation_test.go`: the same fixtures
+(`cpuOnly`, `cpuAndMemory`, `bigCpuAndMemory`, pods with no containers) and the expected
+per-node integer scores. A container request set explicitly to 0 counts as 0; only a missing
+request takes the non-zero default (priorities/util/non_zero.go).
+"""
+import pytest
+
+from kubernetes_amd.scheduler.cache import PodInfo, SchedulerCache
+from kubernetes_amd.scheduler.generic import CycleContext, GenericScheduler
+
+
+def _ctr(cpu, mem):
+    return {"name": "c", "resources": {"requests": {"cpu": cpu, "memory": mem}}}
+
+
+CPU_ONLY = [_ctr("1000m", "0"), _ctr("2000m", "0")]
+CPU_AND_MEM = [_ctr("1000m", "2000"), _ctr("2000m", "3000")]
+BIG = [_ctr("2000m", "4000"), _ctr("3000m", "5000")]
+NONE = []
+
+
+def _pod(containers, node=None, i=0):
+    spec = {"containers": containers}
+    if node:
+        spec["nodeName"] = node
+    return {"metadata": {"name": f"p{i}", "namespace": "default", "uid": f"u{i}"}, "spec": spec,
+            "status": {"phase": "Running"}}
+
+
+def _node(name, cpu_m, mem):
+    alloc = {"cpu": f"{cpu_m}m", "memory": str(mem), "pods": "100"}
+    return {"metadata": {"name": name}, "spec": {},
+            "status": {"allocatable": alloc, "capacity": dict(alloc), "conditions": [{"type": "Ready", "status": "True"}]}}
+
+
+M1 = ("machine1", "machine1")
+
+# (name, pod containers, nodes [(cpu_m, mem)], existing pods [(containers, node)], {priority: [s1, s2]})
+CASES = [
+    ("nothing scheduled, nothing requested", NONE, [(4000, 10000), (4000, 10000)], [],
+     {"LeastRequestedPriority": [10, 10], "MostRequestedPriority": [0, 0], "BalancedResourceAllocation": [10, 10]}),
+    ("nothing scheduled, resources requested, differently sized machines", CPU_AND_MEM,
+     [(4000, 10000), (6000, 10000)], [],
+     {"LeastRequestedPriority": [3, 5], "MostRequestedPriority": [6, 5], "BalancedResourceAllocation": [7, 10]}),
+    ("no resources requested, pods scheduled", NONE, [(4000, 10000), (4000, 10000)],
+     [(NONE, "machine1"), (NONE, "machine1"), (NONE, "machine2"), (NONE, "machine2")],
+     {"LeastRequestedPriority": [10, 10], "BalancedResourceAllocation": [10, 10]}),
+    ("no resources requested, pods scheduled with resources", NONE, [(10000, 20000), (10000, 20000)],
+     [(CPU_ONLY, "machine1"), (CPU_ONLY, "machine1"), (CPU_ONLY, "machine2"), (CPU_AND_MEM, "machine2")],
+     {"LeastRequestedPriority": [7, 5], "MostRequestedPriority": [3, 4], "BalancedResourceAllocation": [4, 6]}),
+    ("resources requested, pods scheduled with resources", CPU_AND_MEM, [(10000, 20000), (10000, 20000)],
+     [(CPU_ONLY, "machine1"), (CPU_AND_MEM, "machine2")],
+     {"LeastRequestedPriority": [5, 4], "MostRequestedPriority": [4, 5], "BalancedResourceAllocation": [6, 9]}),
+    ("resources requested, pods scheduled with resources, differently sized machines", CPU_AND_MEM,
+     [(10000, 20000), (10000, 50000)], [(CPU_ONLY, "machine1"), (CPU_AND_MEM, "machine2")],
+     {"LeastRequestedPriority": [5, 6], "BalancedResourceAllocation": [6, 6]}),
+    ("requested resources exceed node capacity", CPU_ONLY, [(4000, 10000), (4000, 10000)],
+     [(CPU_ONLY, "machine1"), (CPU_AND_MEM, "machine2")],
+     {"LeastRequestedPriority": [5, 2], "BalancedResourceAllocation": [0, 0]}),
+    ("zero node resources, pods scheduled with resources", NONE, [(0, 0), (0, 0)],
+     [(CPU_ONLY, "machine1"), (CPU_AND_MEM, "machine2")],
+     {"LeastRequestedPriority": [0, 0], "BalancedResourceAllocation": [0, 0]}),
+    ("resources requested with more than the node", BIG, [(4000, 10000), (10000, 8000)], [],
+     {"MostRequestedPriority": [4, 2]}),
+]
+
+
+@pytest.mark.parametrize("name,ctrs,nodes,pods,expected", CASES, ids=[c[0] for c in CASES])
+def test_resource_priorities(name, ctrs, nodes, pods, expected):
+    cache = SchedulerCache()
+    for i, (cpu, mem) in enumerate(nodes):
+        cache.add_node(_node(f"machine{i + 1}", cpu, mem))
+    for i, (c, n) in enumerate(pods):
+        cache.add_pod(_pod(c, n, i + 1))
+    pod = _pod(ctrs)
+    infos = [cache.nodes["machine1"], cache.nodes["machine2"]]
+    for prio, want in expected.items():
+        gs = GenericScheduler(cache, [], {prio: 1}, equivalence_cache=False)
+        scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
+        assert [scores["machine1"], scores["machine2"]] == want, (name, prio)
+
+
+# -- image_locality_test.go ----------------------------------------------------------------------
+
+MB = 1024 * 1024
+NODE_40_140_2000 = [(["gcr.io/40", "gcr.io/40:v1"], 40 * MB), (["gcr.io/140", "gcr.io/140:v1"], 140 * MB),
+                    (["gcr.io/2000"], 2000 * MB)]
+NODE_250_10 = [(["gcr.io/250"], 250 * MB), (["gcr.io/10", "gcr.io/10:v1"], 10 * MB)]
+
+
+@pytest.mark.parametrize("images,want", [
+    (["gcr.io/40", "gcr.io/250"], [1, 3]),          # two images spread on two nodes, prefer the larger one
+    (["gcr.io/40", "gcr.io/140"], [2, 0]),          # two images on one node, prefer this node
+    (["gcr.io/10", "gcr.io/2000"], [10, 0]),        # if exceed limit, use limit
+])
+def test_image_locality(images, want):
+    cache = SchedulerCache()
+    for name, imgs in (("machine1", NODE_40_140_2000), ("machine2", NODE_250_10)):
+        n = _node(name, 4000, 10000)
+        n["status"]["images"] = [{"names": names, "sizeBytes": size} for names, size in imgs]
+        cache.add_node(n)
+    pod = _pod([{"name": f"c{i}", "image": im} for i, im in enumerate(images)])
+    gs = GenericScheduler(cache, [], {"ImageLocalityPriority": 1}, equivalence_cache=False)
+    scores = gs.prioritize(pod, PodInfo(pod), [cache.nodes["machine1"], cache.nodes["machine2"]],
+                           CycleContext(cache, pod))
+    assert [scores["machine1"], scores["machine2"]] == want
+
+
+# -- node_prefer_avoid_pods_test.go --------------------------------------------------------------
+
+def _avoid(kind, uid):
+    import json
+    return {"scheduler.alpha.kubernetes.io/preferAvoidPods": json.dumps({"preferAvoidPods": [{
+        "podSignature": {"podController": {"apiVersion": "v1", "kind": kind, "name": "foo", "uid": uid,
+                                           "controller": True}},
+        "reason": "some reason", "message": "some message"}]})}
+
+
+@pytest.mark.parametrize("owner,want", [
+    ({"kind": "ReplicationController", "name": "foo", "uid": "abcdef123456", "controller": True}, [0, 10, 10]),
+    ({"kind": "RandomController", "name": "foo", "uid": "abcdef123456", "controller": True}, [10, 10, 10]),
+    ({"kind": "ReplicationController", "name": "foo", "uid": "abcdef123456"}, [10, 10, 10]),
+    ({"kind": "ReplicaSet", "name": "foo", "uid": "qwert12345", "controller": True}, [10, 0, 10]),
+])
+def test_node_prefer_avoid_pods(owner, want):
+    cache = SchedulerCache()
+    for name, ann in (("machine1", _avoid("ReplicationController", "abcdef123456")),
+                      ("machine2", _avoid("ReplicaSet", "qwert12345")), ("machine3", None)):
+        n = _node(name, 4000, 10000)
+        if ann:
+            n["metadata"]["annotations"] = ann
+        cache.add_node(n)
+    pod = _pod([])
+    pod["metadata"]["ownerReferences"] = [dict(owner, apiVersion="v1")]
+    gs = GenericScheduler(cache, [], {"NodePreferAvoidPodsPriority": 1}, equivalence_cache=False)
+    infos = [cache.nodes[f"machine{i}"] for i in (1, 2, 3)]
+    scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
+    assert [scores[f"machine{i}"] for i in (1, 2, 3)] == want
+
+
+# -- resource_limits_test.go ---------------------------------------------------------------------
+
+def _lim(cpu, mem):
+    return {"name": "c", "resources": {"limits": {"cpu": cpu, "memory": mem}}}
+
+
+@pytest.mark.parametrize("ctrs,nodes,want", [
+    ([], [(4000, 10000), (4000, 0), (0, 10000), (0, 0)], [0, 0, 0, 0]),
+    ([_lim("1000m", "0"), _lim("2000m", "0")], [(3000, 10000), (2000, 10000)], [1, 0]),
+    ([_lim("0", "2000"), _lim("0", "3000")], [(4000, 4000), (5000, 10000)], [0, 1]),
+    ([_lim("1000m", "2000"), _lim("2000m", "3000")], [(4000, 4000), (5000, 10000)], [1, 1]),
+    ([_lim("1000m", "2000"), _lim("2000m", "3000")], [(0, 0)], [0]),
+], ids=["no limits", "cpu limits only", "mem limits only", "cpu and mem limits", "zero node"])
+def test_resource_limits(ctrs, nodes, want):
+    cache = SchedulerCache()
+    for i, (cpu, mem) in enumerate(nodes):
+        cache.add_node(_node(f"machine{i + 1}", cpu, mem))
+    pod = _pod(ctrs)
+    gs = GenericScheduler(cache, [], {"ResourceLimitsPriority": 1}, equivalence_cache=False)
+    infos = [cache.nodes[f"machine{i + 1}"] for i in range(len(nodes))]
+    scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
+    assert [scores[f"machine{i + 1}"] for i in range(len(nodes))] == want
