@@ -268,9 +268,10 @@ def compile_node_affinity_prefs(pod):
 
 
 def normalize_minmax(scores):
-    """`CalculateInterPodAffinityPriority` reduce: int(10 * (v - min) / (max - min)), 0 when all
-    equal."""
-    lo, hi = min(scores), max(scores)
+    """`CalculateInterPodAffinityPriority` reduce: int(10 * (v - min) / (max - min)) where min and
+    max start at 0 (interpod_affinity.go: `var maxCount, minCount float64`), so with only
+    positive counts a node scores in proportion to its count; 0 when all equal."""
+    lo, hi = min(0, min(scores, default=0)), max(0, max(scores, default=0))
     if hi == lo:
         return [0 for _ in scores]
     return [int(MAX * (v - lo) / (hi - lo)) for v in scores]

@@ -163,3 +163,111 @@ def test_resource_limits(ctrs, nodes, want):
     infos = [cache.nodes[f"machine{i + 1}"] for i in range(len(nodes))]
     scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
     assert [scores[f"machine{i + 1}"] for i in range(len(nodes))] == want
+
+
+# -- interpod_affinity_test.go TestInterPodAffinityPriority / TestHardPodAffinitySymmetricWeight -
+
+S1, S2 = {"security": "S1"}, {"security": "S2"}
+RG_CN, RG_IN, AZ1, AZ2 = {"region": "China"}, {"region": "India"}, {"az": "az1"}, {"az": "az2"}
+RG_CN_AZ1 = {"region": "China", "az": "az1"}
+
+
+def _wterm(weight, key, *exprs):
+    return {"weight": weight, "podAffinityTerm": {"labelSelector": {"matchExpressions": [
+        {"key": k, "operator": op, **({"values": v} if v is not None else {})} for k, op, v in exprs]},
+        "topologyKey": key}}
+
+
+STAY_S1_REGION = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(5, "region", ("security", "In", ["S1"]))]}}
+STAY_S2_REGION = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(6, "region", ("security", "In", ["S2"]))]}}
+AFFINITY3 = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(8, "region", ("security", "NotIn", ["S1"]), ("security", "In", ["S2"])),
+    _wterm(2, "region", ("security", "Exists", None), ("wrongkey", "DoesNotExist", None))]}}
+HARD = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(0, "region", ("security", "In", ["S1", "value2"]))["podAffinityTerm"],
+    _wterm(0, "region", ("security", "Exists", None), ("wrongkey", "DoesNotExist", None))["podAffinityTerm"]]}}
+AWAY_S1_AZ = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(5, "az", ("security", "In", ["S1"]))]}}
+AWAY_S2_AZ = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(5, "az", ("security", "In", ["S2"]))]}}
+STAY_S1_AWAY_S2 = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _wterm(8, "region", ("security", "In", ["S1"]))]},
+    "podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+        _wterm(5, "az", ("security", "In", ["S2"]))]}}
+
+
+def _ap(labels=None, node=None, affinity=None, i=0):
+    spec = {"containers": [{"name": "c"}]}
+    if node:
+        spec["nodeName"] = node
+    if affinity:
+        spec["affinity"] = affinity
+    return {"metadata": {"name": f"a{i}", "namespace": "default", "uid": f"a{i}", "labels": labels or {}},
+            "spec": spec, "status": {"phase": "Running"}}
+
+
+IPA_CASES = [
+    ("affinity is nil", _ap(S1), [], [RG_CN, RG_IN, AZ1], [0, 0, 0]),
+    ("matches topology key and pods", _ap(S1, affinity=STAY_S1_REGION),
+     [(S1, "machine1", None), (S2, "machine2", None), (S1, "machine3", None)], [RG_CN, RG_IN, AZ1], [10, 0, 0]),
+    ("same topology value, same score", _ap(None, affinity=STAY_S1_REGION), [(S1, "machine1", None)],
+     [RG_CN, RG_CN_AZ1, RG_IN], [10, 10, 0]),
+    ("region with more matches scores higher", _ap(S1, affinity=STAY_S2_REGION),
+     [(S2, "machine1", None), (S2, "machine1", None), (S2, "machine2", None), (S2, "machine3", None),
+      (S2, "machine4", None), (S2, "machine5", None)], [RG_CN, RG_IN, RG_CN, RG_CN, RG_IN], [10, 5, 10, 10, 5]),
+    ("different label operators", _ap(S1, affinity=AFFINITY3),
+     [(S1, "machine1", None), (S2, "machine2", None), (S1, "machine3", None)], [RG_CN, RG_IN, AZ1], [2, 10, 0]),
+    ("symmetry of preferred affinity", _ap(S2),
+     [(S1, "machine1", STAY_S1_REGION), (S2, "machine2", STAY_S2_REGION)], [RG_CN, RG_IN, AZ1], [0, 10, 0]),
+    ("symmetry of required affinity", _ap(S1),
+     [(S1, "machine1", HARD), (S2, "machine2", HARD)], [RG_CN, RG_IN, AZ1], [10, 10, 0]),
+    ("anti affinity: no matching pods scores high", _ap(S1, affinity=AWAY_S1_AZ),
+     [(S1, "machine1", None), (S2, "machine2", None)], [AZ1, RG_CN], [0, 10]),
+    ("anti affinity: topology key missing scores high", _ap(S1, affinity=AWAY_S1_AZ),
+     [(S1, "machine1", None), (S1, "machine2", None)], [AZ1, RG_CN], [0, 10]),
+    ("anti affinity: more matches scores low", _ap(S1, affinity=AWAY_S1_AZ),
+     [(S1, "machine1", None), (S1, "machine1", None), (S2, "machine2", None)], [AZ1, RG_IN], [0, 10]),
+    ("anti affinity symmetry", _ap(S2), [(S1, "machine1", AWAY_S2_AZ), (S2, "machine2", AWAY_S1_AZ)], [AZ1, AZ2],
+     [0, 10]),
+    ("affinity and anti affinity", _ap(S1, affinity=STAY_S1_AWAY_S2),
+     [(S1, "machine1", None), (S1, "machine2", None)], [RG_CN, AZ1], [10, 0]),
+    ("affinity and anti affinity, same labels", _ap(S1, affinity=STAY_S1_AWAY_S2),
+     [(S1, "machine1", None), (S1, "machine1", None), (S1, "machine2", None), (S1, "machine3", None),
+      (S1, "machine3", None), (S1, "machine4", None), (S1, "machine5", None)],
+     [RG_CN_AZ1, RG_IN, RG_CN, RG_CN, RG_IN], [10, 4, 10, 10, 4]),
+    ("affinity, anti affinity and symmetry", _ap(S1, affinity=STAY_S1_AWAY_S2),
+     [(S1, "machine1", None), (S2, "machine2", None), (None, "machine3", STAY_S1_AWAY_S2),
+      (None, "machine4", AWAY_S1_AZ)], [RG_CN, AZ1, RG_IN, AZ2], [10, 0, 10, 0]),
+]
+
+
+def _ipa_scores(pod, pods, node_labels, hard_weight=1):
+    cache = SchedulerCache()
+    cache.hard_pod_affinity_weight = hard_weight
+    for i, labels in enumerate(node_labels):
+        n = _node(f"machine{i + 1}", 4000, 10000)
+        n["metadata"]["labels"] = labels
+        cache.add_node(n)
+    for i, (labels, node, aff) in enumerate(pods):
+        cache.add_pod(_ap(labels, node, aff, i + 1))
+    gs = GenericScheduler(cache, [], {"InterPodAffinityPriority": 1}, equivalence_cache=False)
+    infos = [cache.nodes[f"machine{i + 1}"] for i in range(len(node_labels))]
+    scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
+    return [int(scores[f"machine{i + 1}"]) for i in range(len(node_labels))]
+
+
+@pytest.mark.parametrize("name,pod,pods,node_labels,want", IPA_CASES, ids=[c[0] for c in IPA_CASES])
+def test_inter_pod_affinity_priority(name, pod, pods, node_labels, want):
+    assert _ipa_scores(pod, pods, node_labels) == want
+
+
+@pytest.mark.parametrize("weight,want", [(1, [10, 10, 0]), (0, [0, 0, 0])])
+def test_hard_pod_affinity_symmetric_weight(weight, want):
+    hard = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchExpressions": [{"key": "service", "operator": "In", "values": ["S1"]}]},
+         "topologyKey": "region"}]}}
+    got = _ipa_scores(_ap({"service": "S1"}), [(None, "machine1", hard), (None, "machine2", hard)],
+                      [RG_CN, RG_IN, AZ1], hard_weight=weight)
+    assert got == want
