@@ -271,3 +271,23 @@ def test_hard_pod_affinity_symmetric_weight(weight, want):
     got = _ipa_scores(_ap({"service": "S1"}), [(None, "machine1", hard), (None, "machine2", hard)],
                       [RG_CN, RG_IN, AZ1], hard_weight=weight)
     assert got == want
+
+
+# -- node_label_test.go TestNewNodeLabelPriority (Policy labelPreference) ------------------------
+
+@pytest.mark.parametrize("label,presence,want", [
+    ("baz", True, [0, 0, 0]), ("baz", False, [10, 10, 10]), ("foo", True, [10, 0, 0]), ("foo", False, [0, 10, 10]),
+    ("bar", True, [0, 10, 10]), ("bar", False, [10, 0, 0])])
+def test_node_label_priority(label, presence, want):
+    from kubernetes_amd.scheduler import priorities as PR
+    cache = SchedulerCache()
+    for i, labels in enumerate(({"foo": "bar"}, {"bar": "foo"}, {"bar": "baz"})):
+        n = _node(f"machine{i + 1}", 4000, 10000)
+        n["metadata"]["labels"] = labels
+        cache.add_node(n)
+    pod = _pod([])
+    gs = GenericScheduler(cache, [], {"label": (1, PR.make_label_preference(label, presence), False, False)},
+                          equivalence_cache=False)
+    infos = [cache.nodes[f"machine{i}"] for i in (1, 2, 3)]
+    scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
+    assert [scores[f"machine{i}"] for i in (1, 2, 3)] == want
