@@ -101,53 +101,75 @@ class CPUTopology:
 
 
 def take_by_topology(topo: CPUTopology, available: set, n: int, prefer_numa=()):
-    """Pick n CPUs from `available`: restricted to the preferred NUMA nodes first (if they can
-    hold all n), then whole sockets, whole physical cores, single threads."""
+    """`cpu_assignment.go:149` takeByTopology (topology-aware best fit), with the reference's
+    `cpuAccumulator` orderings read lexicographically:
+
+      1. whole free sockets, ascending id, while at least a socket's worth is still needed;
+      2. whole free cores while at least a core's worth is needed — sockets with fewer free
+         cores first (best fit), then by id;
+      3. single threads, ordering cores by: most CPUs already taken by this request on the
+         core's socket, fewest free CPUs on the socket, fewest free CPUs on the core (fill
+         partially used cores before splitting whole ones), socket id, core id.
+
+    MI355X addition: with `prefer_numa` (the NUMA nodes of the pod's GPUs) the CPUs are taken
+    from those nodes when they can hold all n."""
     if n > len(available):
-        raise ValueError(f"not enough cpus available: want {n}, have {len(available)}")
-    pools = []
+        raise ValueError("not enough cpus available to satisfy request")
+    if n <= 0:
+        return []
+    pool = set(available)
     if prefer_numa:
         pref = {c for c in available if topo.cpus[c].numa in set(prefer_numa)}
         if len(pref) >= n:
-            pools.append(pref)
-    pools.append(set(available))
-    pool = pools[0]
-    taken: list[int] = []
-    need = n
-    by_socket = {}
-    for c in pool:
-        by_socket.setdefault(topo.cpus[c].socket, set()).add(c)
-    all_socket = {}
+            pool = pref
+    socket_cpus, core_cpus = {}, {}
     for c in topo.cpus.values():
-        all_socket.setdefault(c.socket, set()).add(c.cpu)
-    # 1) whole free sockets
-    for s in sorted(by_socket, key=lambda s: -len(by_socket[s])):
-        if need >= len(all_socket[s]) and by_socket[s] == all_socket[s]:
-            taken += sorted(by_socket[s])
-            need -= len(by_socket[s])
-    rest = pool - set(taken)
-    # 2) whole physical cores, from the socket with the most free cpus
-    if need:
-        cores = topo.cores(rest)
-        all_cores = topo.cores(topo.cpus)
-        free_cores = [k for k, v in cores.items() if len(v) == len(all_cores[k])]
-        sock_free = {}
-        for c in rest:
-            sock_free[topo.cpus[c].socket] = sock_free.get(topo.cpus[c].socket, 0) + 1
-        free_cores.sort(key=lambda k: (-sock_free[topo.cpus[cores[k][0]].socket], k))
-        for k in free_cores:
-            if need >= len(cores[k]):
-                taken += sorted(cores[k])
-                need -= len(cores[k])
-    # 3) single threads (siblings of already-taken cores first)
-    if need:
-        rest = pool - set(taken)
-        taken_cores = {topo.cpus[c].core for c in taken}
-        taken_sockets = {topo.cpus[c].socket for c in taken}
-        cands = sorted(rest, key=lambda c: (topo.cpus[c].core not in taken_cores, topo.cpus[c].socket not in taken_sockets,
-                                            topo.cpus[c].socket, c))
-        taken += cands[:need]
-    return sorted(taken)
+        socket_cpus.setdefault(c.socket, set()).add(c.cpu)
+        core_cpus.setdefault(c.core, set()).add(c.cpu)
+    per_socket = max(len(v) for v in socket_cpus.values())
+    per_core = max(len(v) for v in core_cpus.values())
+    free = set(pool)
+    result: set = set()
+
+    def take(cpus):
+        nonlocal n
+        result.update(cpus)
+        free.difference_update(cpus)
+        n -= len(cpus)
+
+    def free_in(group):
+        return group & free
+
+    # 1) whole sockets
+    for s in sorted(socket_cpus):
+        if n >= per_socket and free_in(socket_cpus[s]) == socket_cpus[s] and len(socket_cpus[s]) == per_socket:
+            take(socket_cpus[s])
+            if n <= 0:
+                return sorted(result)
+    # 2) whole cores, best-fit sockets first
+    if n >= per_core:
+        def free_cores(s):
+            return [k for k, v in core_cpus.items() if topo.cpus[next(iter(v))].socket == s
+                    and len(v) == per_core and free_in(v) == v]
+        for s in sorted({topo.cpus[c].socket for c in free}, key=lambda s: (len(free_cores(s)), s)):
+            for k in sorted(free_cores(s)):
+                if n >= per_core and free_in(core_cpus[k]) == core_cpus[k]:
+                    take(core_cpus[k])
+                    if n <= 0:
+                        return sorted(result)
+    # 3) single threads
+    cores = sorted({topo.cpus[c].core for c in free}, key=lambda k: (
+        -len(socket_cpus[topo.cpus[next(iter(core_cpus[k]))].socket] & result),
+        len(free_in(socket_cpus[topo.cpus[next(iter(core_cpus[k]))].socket])),
+        len(free_in(core_cpus[k])),
+        topo.cpus[next(iter(core_cpus[k]))].socket, k))
+    for k in cores:
+        for c in sorted(free_in(core_cpus[k])):
+            if n > 0:
+                take({c})
+        if n <= 0:
+            return sorted(result)
+    raise ValueError("failed to allocate cpus")
 
 
 class StaticPolicy:

@@ -3,6 +3,8 @@ import asyncio
 import json
 import os
 
+import pytest
+
 from kubernetes_amd.api import core
 from kubernetes_amd.cluster import LocalCluster
 from kubernetes_amd.kubelet.cpumanager import CPUTopology, StaticPolicy, format_cpulist, parse_cpulist, take_by_topology
@@ -160,3 +162,75 @@ def test_static_pods_mirror(run, tmp_path):
             else:
                 raise AssertionError("mirror pod not deleted")
     run(main(), timeout=60)
+
+
+# -- cpu_assignment_test.go TestTakeByTopology --------------------------------------------------
+
+def _topo(details):
+    from kubernetes_amd.kubelet.cpumanager import CPUInfo, CPUTopology
+    return CPUTopology([CPUInfo(cpu, core, sock, sock) for cpu, (core, sock) in details.items()])
+
+
+SINGLE_SOCKET_HT = {0: (0, 0), 1: (1, 0), 2: (2, 0), 3: (3, 0), 4: (0, 0), 5: (1, 0), 6: (2, 0), 7: (3, 0)}
+DUAL_SOCKET_HT = {0: (0, 0), 1: (1, 1), 2: (2, 0), 3: (3, 1), 4: (4, 0), 5: (5, 1),
+                  6: (0, 0), 7: (1, 1), 8: (2, 0), 9: (3, 1), 10: (4, 0), 11: (5, 1)}
+DUAL_SOCKET_NO_HT = {0: (0, 0), 1: (1, 0), 2: (2, 0), 3: (3, 0), 4: (4, 1), 5: (5, 1), 6: (6, 1), 7: (7, 1)}
+
+
+@pytest.mark.parametrize("topo,avail,n,want", [
+    (SINGLE_SOCKET_HT, {0, 2, 4, 6}, 5, None),
+    (SINGLE_SOCKET_HT, set(range(8)), 0, []),
+    (SINGLE_SOCKET_HT, set(range(8)), 1, [0]),
+    (SINGLE_SOCKET_HT, {1, 3, 5, 6, 7}, 1, [6]),
+    (SINGLE_SOCKET_HT, set(range(8)), 2, [0, 4]),
+    (SINGLE_SOCKET_HT, set(range(8)), 8, list(range(8))),
+    (SINGLE_SOCKET_HT, {0, 1, 2, 3, 6}, 2, [2, 6]),
+    (DUAL_SOCKET_HT, {1, 2, 3, 4, 5, 7, 8, 9, 10, 11}, 1, [2]),
+    (DUAL_SOCKET_HT, set(range(12)), 6, [0, 2, 4, 6, 8, 10]),
+    (DUAL_SOCKET_NO_HT, set(range(8)), 4, [0, 1, 2, 3]),
+    (DUAL_SOCKET_NO_HT, {1, 2, 3, 4, 5, 6, 7}, 1, [1]),
+], ids=["more than available", "zero", "one", "one, some taken", "two", "all", "two, one free core",
+        "dual socket one cpu", "dual socket a socket", "no HT a socket", "no HT one"])
+def test_take_by_topology(topo, avail, n, want):
+    from kubernetes_amd.kubelet.cpumanager import take_by_topology
+    if want is None:
+        with pytest.raises(ValueError, match="not enough cpus available to satisfy request"):
+            take_by_topology(_topo(topo), avail, n)
+    else:
+        assert take_by_topology(_topo(topo), avail, n) == want
+
+
+# -- policy_static_test.go TestStaticPolicyAdd (allocation from the default set minus reserved) --
+
+@pytest.mark.parametrize("topo,default,req,lim,want", [
+    (SINGLE_SOCKET_HT, set(range(8)), "8000m", "8000m", "error"),
+    (SINGLE_SOCKET_HT, set(range(8)), "1000m", "1000m", [4]),          # sibling of the partial core
+    (SINGLE_SOCKET_HT, {0, 1, 4, 5}, "2000m", "2000m", [1, 5]),
+    (DUAL_SOCKET_HT, {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11}, "6000m", "6000m", [1, 3, 5, 7, 9, 11]),
+    (DUAL_SOCKET_HT, {0, 2, 3, 4, 6, 7, 8, 9, 10, 11}, "6000m", "6000m", [2, 3, 4, 8, 9, 10]),
+    (DUAL_SOCKET_NO_HT, {0, 1, 3, 4, 5, 6, 7}, "4000m", "4000m", [4, 5, 6, 7]),
+    (DUAL_SOCKET_NO_HT, {0, 1, 3, 6, 7}, "4000m", "4000m", [1, 3, 6, 7]),
+    (DUAL_SOCKET_HT, {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11}, "8000m", "8000m", [1, 3, 4, 5, 7, 9, 10, 11]),
+    (SINGLE_SOCKET_HT, set(range(8)), "1000m", "2000m", None),           # not Guaranteed
+    (SINGLE_SOCKET_HT, set(range(8)), "977m", "977m", None),             # non-integer CPUs
+    (SINGLE_SOCKET_HT, {0, 7}, "2000m", "2000m", "error"),
+    (DUAL_SOCKET_HT, {0, 4, 5, 6, 7, 8, 9, 10, 11}, "10000m", "10000m", "error"),
+], ids=["SingleCore expect error", "alloc one cpu", "alloc one core", "dual HT one socket", "dual HT three cores",
+        "no HT one socket", "no HT four cores", "dual HT socket + core", "non-Gu pod", "non-integer", "no alloc error",
+        "dual HT error"])
+def test_static_policy_add(topo, default, req, lim, want):
+    t = _topo(topo)
+    pod = {"metadata": {"uid": "u"}, "spec": {"containers": [{"name": "c", "resources": {
+        "requests": {"cpu": req, "memory": "1G"}, "limits": {"cpu": lim, "memory": "1G"}}}]},
+        "status": {"qosClass": "Guaranteed" if req == lim else "Burstable"}}
+    n = StaticPolicy.guaranteed_cpus(pod, pod["spec"]["containers"][0])
+    if want is None:
+        assert n == 0
+        return
+    reserved = set(take_by_topology(t, set(t.cpus), 1))      # NewStaticPolicy(topo, 1): cpu 0
+    assert reserved == {0}
+    if want == "error":
+        with pytest.raises(ValueError, match="not enough cpus available to satisfy request"):
+            take_by_topology(t, default - reserved, n)
+    else:
+        assert take_by_topology(t, default - reserved, n) == want
