@@ -18,7 +18,14 @@ Parity (reference paths):
   * Job / CronJob: `pkg/apis/batch/v1/defaults.go` (completions/parallelism 1, backoffLimit 6),
     `pkg/apis/batch/v1beta1/defaults.go` (concurrencyPolicy Allow, suspend false, history 3/1);
   * HorizontalPodAutoscaler: `pkg/apis/autoscaling/v1/defaults.go` (minReplicas 1);
-  * Service / Secret / PV / PVC small defaults.
+  * Service (sessionAffinity None / ClientIP timeout, type ClusterIP, port protocol and
+    targetPort, externalTrafficPolicy), Endpoints, Namespace status, Node externalID and
+    allocatable, LimitRangeItem defaults from max/min, volume sources (emptyDir when none,
+    iscsi/rbd/azureDisk), field refs, lifecycle httpGet: `pkg/apis/core/v1/defaults.go`;
+  * StorageClass, webhook configurations (failurePolicy Ignore, empty namespaceSelector),
+    RBAC binding apiGroups, CSR usages, PodSecurityPolicy allowPrivilegeEscalation: their
+    groups' `defaults.go`;
+  * Secret / PV / PVC small defaults.
 """
 from __future__ import annotations
 
@@ -44,6 +51,14 @@ def _probe(p):
 
 
 def _container(c):
+    for e in c.get("env") or ():
+        fr = ((e or {}).get("valueFrom") or {}).get("fieldRef")
+        if isinstance(fr, dict):
+            _default(fr, "apiVersion", "v1")                  # SetDefaults_ObjectFieldSelector
+    for h in ((c.get("lifecycle") or {}).get("postStart"), (c.get("lifecycle") or {}).get("preStop")):
+        if isinstance(h, dict) and isinstance(h.get("httpGet"), dict):
+            _default(h["httpGet"], "path", "/")               # SetDefaults_HTTPGetAction
+            _default(h["httpGet"], "scheme", "HTTP")
     _default(c, "terminationMessagePath", "/dev/termination-log")
     _default(c, "terminationMessagePolicy", "File")
     for p in c.get("ports") or ():
@@ -71,6 +86,19 @@ def pod_spec(spec):
                 _default(v[src], "defaultMode", 0o644)
         if isinstance(v.get("hostPath"), dict):
             _default(v["hostPath"], "type", "")
+        if not any(k != "name" and isinstance(val, dict) for k, val in v.items()):
+            v["emptyDir"] = {}                                  # SetDefaults_Volume
+        if isinstance(v.get("iscsi"), dict):
+            _default(v["iscsi"], "iscsiInterface", "default")
+        if isinstance(v.get("rbd"), dict):
+            for k, d in (("pool", "rbd"), ("user", "admin"), ("keyring", "/etc/ceph/keyring")):
+                _default(v["rbd"], k, d)
+        if isinstance(v.get("azureDisk"), dict):
+            for k, d in (("cachingMode", "ReadWrite"), ("kind", "Shared"), ("fsType", "ext4"), ("readOnly", False)):
+                _default(v["azureDisk"], k, d)
+        for item in (v.get("downwardAPI") or {}).get("items") or () if isinstance(v.get("downwardAPI"), dict) else ():
+            if isinstance(item.get("fieldRef"), dict):
+                _default(item["fieldRef"], "apiVersion", "v1")
 
 
 def _template(spec):
@@ -218,12 +246,114 @@ def pod(obj):
     pod_spec(obj.setdefault("spec", {}))
 
 
+def service(obj):
+    """SetDefaults_Service (core/v1/defaults.go:94-130)."""
+    spec = obj.setdefault("spec", {})
+    _default(spec, "sessionAffinity", "None")
+    if spec["sessionAffinity"] == "None":
+        spec.pop("sessionAffinityConfig", None)
+    elif spec["sessionAffinity"] == "ClientIP":
+        cfg = spec.get("sessionAffinityConfig") or {}
+        if (cfg.get("clientIP") or {}).get("timeoutSeconds") is None:
+            spec["sessionAffinityConfig"] = {"clientIP": {"timeoutSeconds": 10800}}   # 3 hours
+    _default(spec, "type", "ClusterIP")
+    for p in spec.get("ports") or ():
+        if not isinstance(p, dict):
+            continue
+        _default(p, "protocol", "TCP")
+        if p.get("targetPort") in (None, 0, "") and p.get("port") is not None:
+            p["targetPort"] = p["port"]
+    if spec["type"] in ("NodePort", "LoadBalancer"):
+        _default(spec, "externalTrafficPolicy", "Cluster")
+
+
+def endpoints(obj):
+    """SetDefaults_Endpoints: port protocol TCP."""
+    for ss in obj.get("subsets") or ():
+        for p in (ss or {}).get("ports") or ():
+            _default(p, "protocol", "TCP")
+
+
+def namespace(obj):
+    """SetDefaults_NamespaceStatus: phase Active."""
+    _default(obj.setdefault("status", {}), "phase", "Active")
+
+
+def node(obj):
+    """SetDefaults_Node (externalID = name) and SetDefaults_NodeStatus (allocatable = capacity)."""
+    spec = obj.setdefault("spec", {})
+    if not spec.get("externalID") and (obj.get("metadata") or {}).get("name"):
+        spec["externalID"] = obj["metadata"]["name"]
+    st = obj.get("status")
+    if isinstance(st, dict) and st.get("allocatable") is None and st.get("capacity") is not None:
+        st["allocatable"] = dict(st["capacity"])
+
+
+def limitrange(obj):
+    """SetDefaults_LimitRangeItem: for Container items, default <- max, defaultRequest <- default,
+    then defaultRequest <- min, key by key where unset."""
+    for item in (obj.get("spec") or {}).get("limits") or ():
+        if item.get("type") != "Container":
+            continue
+        dflt = item.setdefault("default", {}) if item.get("default") is None else item["default"]
+        dreq = item.setdefault("defaultRequest", {}) if item.get("defaultRequest") is None else item["defaultRequest"]
+        for k, v in (item.get("max") or {}).items():
+            dflt.setdefault(k, v)
+        for k, v in dflt.items():
+            dreq.setdefault(k, v)
+        for k, v in (item.get("min") or {}).items():
+            dreq.setdefault(k, v)
+
+
+def storageclass(obj):
+    """storage/v1 SetDefaults_StorageClass: reclaimPolicy Delete, volumeBindingMode Immediate."""
+    _default(obj, "reclaimPolicy", "Delete")
+    _default(obj, "volumeBindingMode", "Immediate")
+
+
+def webhook_configuration(obj):
+    """admissionregistration/v1beta1 SetDefaults_Webhook: failurePolicy Ignore, an empty
+    (match-everything) namespaceSelector."""
+    for w in obj.get("webhooks") or ():
+        if isinstance(w, dict):
+            _default(w, "failurePolicy", "Ignore")
+            _default(w, "namespaceSelector", {})
+
+
+def _rbac_subjects(obj):
+    """rbac/v1 SetDefaults_Subject: User / Group subjects get apiGroup rbac.authorization.k8s.io;
+    SetDefaults_(Cluster)RoleBinding: roleRef apiGroup likewise."""
+    rr = obj.get("roleRef")
+    if isinstance(rr, dict) and not rr.get("apiGroup"):
+        rr["apiGroup"] = "rbac.authorization.k8s.io"
+    for sub in obj.get("subjects") or ():
+        if isinstance(sub, dict) and not sub.get("apiGroup") and sub.get("kind") in ("User", "Group"):
+            sub["apiGroup"] = "rbac.authorization.k8s.io"
+
+
+def csr(obj):
+    """certificates/v1beta1 SetDefaults_CertificateSigningRequestSpec: usages."""
+    spec = obj.setdefault("spec", {})
+    if not spec.get("usages"):
+        spec["usages"] = ["digital signature", "key encipherment"]
+
+
+def psp(obj):
+    """extensions/v1beta1 SetDefaults_PodSecurityPolicySpec: allowPrivilegeEscalation true."""
+    _default(obj.setdefault("spec", {}), "allowPrivilegeEscalation", True)
+
+
+
 BY_KIND = {
     "Pod": pod, "Deployment": deployment, "ReplicaSet": replicaset, "DaemonSet": daemonset, "StatefulSet": statefulset,
     "ReplicationController": replicationcontroller, "Job": job, "CronJob": cronjob,
     "HorizontalPodAutoscaler": hpa, "PodTemplate": podtemplate, "Secret": secret,
     "PersistentVolume": persistentvolume, "PersistentVolumeClaim": persistentvolumeclaim,
-    "NetworkPolicy": networkpolicy,
+    "NetworkPolicy": networkpolicy, "Service": service, "Endpoints": endpoints, "Namespace": namespace,
+    "Node": node, "LimitRange": limitrange, "StorageClass": storageclass,
+    "MutatingWebhookConfiguration": webhook_configuration, "ValidatingWebhookConfiguration": webhook_configuration,
+    "RoleBinding": _rbac_subjects, "ClusterRoleBinding": _rbac_subjects,
+    "CertificateSigningRequest": csr, "PodSecurityPolicy": psp,
 }
 
 

@@ -70,15 +70,19 @@ def test_admission_webhooks(run):
                  "clientConfig": {"url": f"http://127.0.0.1:{wport}/mutate"}}]})
             cm2 = await c.create("configmaps", {"metadata": {"name": "plain", "namespace": "default"}})
             assert "labels" not in cm2["metadata"]
-            # failurePolicy: an unreachable hook fails closed by default, open with Ignore
-            await c.create("validatingwebhookconfigurations", {"metadata": {"name": "dead"}, "webhooks": [
-                {"name": "dead.amd.com", "rules": rules, "clientConfig": {"url": "http://127.0.0.1:1/x"}}]})
+            # failurePolicy: an unreachable hook fails closed with Fail, open with Ignore — the
+            # v1beta1 default (SetDefaults_Webhook), which the stored object carries
+            dead = await c.create("validatingwebhookconfigurations", {"metadata": {"name": "dead"}, "webhooks": [
+                {"name": "dead.amd.com", "failurePolicy": "Fail", "rules": rules,
+                 "clientConfig": {"url": "http://127.0.0.1:1/x"}}]})
+            assert dead["webhooks"][0]["namespaceSelector"] == {}
             with pytest.raises(APIStatusError) as e:
                 await c.create("configmaps", {"metadata": {"name": "x1", "namespace": "default"}})
             assert e.value.code == 500
-            await c.patch("validatingwebhookconfigurations", "dead", {"webhooks": [
-                {"name": "dead.amd.com", "failurePolicy": "Ignore", "rules": rules,
-                 "clientConfig": {"url": "http://127.0.0.1:1/x"}}]})
+            await c.delete("validatingwebhookconfigurations", "dead")
+            dflt = await c.create("validatingwebhookconfigurations", {"metadata": {"name": "dead2"}, "webhooks": [
+                {"name": "dead.amd.com", "rules": rules, "clientConfig": {"url": "http://127.0.0.1:1/x"}}]})
+            assert dflt["webhooks"][0]["failurePolicy"] == "Ignore"
             await c.create("configmaps", {"metadata": {"name": "x2", "namespace": "default"}})
         finally:
             await c.close()

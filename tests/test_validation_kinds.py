@@ -84,12 +84,14 @@ INVALID = [
     ("ingresses", {"metadata": {"name": "ing"}, "spec": {"rules": [{"host": "1.2.3.4", "http": {"paths": [
         {"path": "rel", "backend": {"serviceName": "Svc", "servicePort": 80}}]}}]}},
      ["spec.rules[0].host", "spec.rules[0].http.paths[0].path", "spec.rules[0].http.paths[0].backend.serviceName"]),
-    ("pods", {"metadata": {"name": "p"}, "spec": {"dnsPolicy": "Sometimes", "volumes": [{"name": "v"}],
+    ("pods", {"metadata": {"name": "p"}, "spec": {"dnsPolicy": "Sometimes",
+                                                  # (a source-less volume is defaulted to emptyDir, SetDefaults_Volume)
+                                                  "volumes": [{"name": "v", "emptyDir": {}, "hostPath": {"path": "/x"}}],
                                                   "tolerations": [{"operator": "Equal", "value": "x"}],
                                                   "containers": [{"name": "c", "image": "i", "env": [{"name": "1BAD=X"}],
                                                                   "volumeMounts": [{"name": "w", "mountPath": "/w"}],
                                                                   "livenessProbe": {"periodSeconds": 1}}]}},
-     ["spec.dnsPolicy", "spec.volumes[0]", "spec.tolerations[0].operator", "spec.containers[0].env[0].name",
+     ["spec.dnsPolicy", "spec.volumes[0].emptyDir", "spec.tolerations[0].operator", "spec.containers[0].env[0].name",
       "spec.containers[0].volumeMounts[0].name", "spec.containers[0].livenessProbe"]),
 ]
 
@@ -190,3 +192,43 @@ def test_update_rules_immutable_fields(run):
                                      ("61 * * * *", False), ("* * *", False), ("0 25 * * *", False), ("a b c d e", False)])
 def test_cron_expressions(expr, ok):
     assert vx.valid_cron(expr) is ok
+
+
+# -- SetDefaults_* (pkg/apis/*/v1*/defaults.go) --------------------------------------------------
+
+def test_scheme_defaults():
+    from kubernetes_amd.api import defaults as D
+    svc = D.apply("Service", {"spec": {"ports": [{"port": 80}], "type": "NodePort", "sessionAffinity": "ClientIP"}})
+    sp = svc["spec"]
+    assert sp["ports"][0] == {"port": 80, "protocol": "TCP", "targetPort": 80}
+    assert sp["sessionAffinityConfig"] == {"clientIP": {"timeoutSeconds": 10800}} and sp["externalTrafficPolicy"] == "Cluster"
+    assert D.apply("Service", {"spec": {}})["spec"] == {"sessionAffinity": "None", "type": "ClusterIP"}
+    assert D.apply("Endpoints", {"subsets": [{"ports": [{"port": 1}]}]})["subsets"][0]["ports"][0]["protocol"] == "TCP"
+    assert D.apply("Namespace", {"metadata": {"name": "n"}})["status"] == {"phase": "Active"}
+    n = D.apply("Node", {"metadata": {"name": "n1"}, "status": {"capacity": {"cpu": "4"}}})
+    assert n["spec"]["externalID"] == "n1" and n["status"]["allocatable"] == {"cpu": "4"}
+    lr = D.apply("LimitRange", {"spec": {"limits": [
+        {"type": "Container", "max": {"cpu": "2"}, "min": {"memory": "1Mi"}, "default": {"memory": "1Gi"}},
+        {"type": "Pod", "max": {"cpu": "4"}}]}})
+    c, p = lr["spec"]["limits"]
+    assert c["default"] == {"memory": "1Gi", "cpu": "2"} and c["defaultRequest"] == {"memory": "1Gi", "cpu": "2"}
+    assert "default" not in p
+    assert D.apply("StorageClass", {})["reclaimPolicy"] == "Delete"
+    wh = D.apply("ValidatingWebhookConfiguration", {"webhooks": [{"name": "w"}]})["webhooks"][0]
+    assert wh["failurePolicy"] == "Ignore" and wh["namespaceSelector"] == {}
+    rb = D.apply("RoleBinding", {"roleRef": {"kind": "Role", "name": "r"}, "subjects": [
+        {"kind": "User", "name": "u"}, {"kind": "ServiceAccount", "name": "s"}]})
+    assert rb["roleRef"]["apiGroup"] == "rbac.authorization.k8s.io"
+    assert rb["subjects"][0]["apiGroup"] == "rbac.authorization.k8s.io" and "apiGroup" not in rb["subjects"][1]
+    assert D.apply("CertificateSigningRequest", {"spec": {}})["spec"]["usages"] == ["digital signature",
+                                                                                    "key encipherment"]
+    assert D.apply("PodSecurityPolicy", {"spec": {}})["spec"]["allowPrivilegeEscalation"] is True
+    pod = D.apply("Pod", {"spec": {"containers": [{"name": "c", "env": [
+        {"name": "N", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}}]}],
+        "volumes": [{"name": "a"}, {"name": "b", "rbd": {"monitors": ["m"], "image": "i"}},
+                    {"name": "c", "iscsi": {"targetPortal": "t", "iqn": "q", "lun": 0}}]}})
+    assert pod["spec"]["containers"][0]["env"][0]["valueFrom"]["fieldRef"]["apiVersion"] == "v1"
+    a, b, c = pod["spec"]["volumes"]
+    assert a == {"name": "a", "emptyDir": {}}
+    assert (b["rbd"]["pool"], b["rbd"]["user"], b["rbd"]["keyring"]) == ("rbd", "admin", "/etc/ceph/keyring")
+    assert c["iscsi"]["iscsiInterface"] == "default"
