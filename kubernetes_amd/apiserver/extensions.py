@@ -11,8 +11,9 @@ Admission webhooks — `staging/src/k8s.io/apiserver/pkg/admission/plugin/webhoo
     HTTPS verified against `caBundle`);
   * mutating hooks run in order and apply the returned base64 JSONPatch
     (`mutating/admission.go:199-321`); validating hooks run after all mutation and validation
-    (`validating/admission.go`); `failurePolicy: Ignore` fails open on call errors, `Fail`
-    (default) rejects; a denial returns the hook's `result` status (403 by default).
+    (`validating/admission.go`), all relevant ones in parallel; `failurePolicy: Ignore` (the
+    v1beta1 default) fails open on call errors, `Fail` rejects; a denial returns the hook's
+    `result` status (403 by default).
 CustomResourceDefinitions — `staging/src/k8s.io/apiextensions-apiserver`:
   * a CRD named `<plural>.<group>` installs `/apis/<group>/<version>/[namespaces/<ns>/]<plural>`
     with discovery; names are checked against existing resources and the CRD's status gets
@@ -140,22 +141,37 @@ class WebhookDispatcher:
             raise ConnectionError(f"webhook returned HTTP {st}")
         return (json.loads(body) or {}).get("response") or {}
 
+    async def _ask(self, hook, a, ri):
+        """One webhook call: its response, or None when it failed open."""
+        self.calls += 1
+        try:
+            resp = await self._call(hook, self._review(a, ri))
+        except (ConnectionError, OSError, asyncio.TimeoutError, ValueError) as e:
+            if hook.get("failurePolicy", "Ignore") != "Fail":
+                log.warning("failed calling webhook %s, failing open: %s", hook.get("name"), e)
+                return None
+            raise APIError(500, "InternalError", f'Internal error occurred: failed calling admission webhook "{hook.get("name")}": {e}')
+        if not resp.get("allowed"):
+            res = resp.get("result") or {}
+            raise APIError(int(res.get("code") or 403), res.get("reason") or "Forbidden",
+                           f'admission webhook "{hook.get("name")}" denied the request: {res.get("message", "without explanation")}')
+        return resp
+
     async def run(self, a, ri, mutating):
         hooks = [h for h in self._hooks(MUTATING if mutating else VALIDATING) if self._relevant(h, a, ri)]
+        if not mutating:
+            # validating/admission.go: every relevant hook is called in parallel; the first
+            # error (in hook order) is returned
+            results = await asyncio.gather(*(self._ask(h, a, ri) for h in hooks), return_exceptions=True)
+            for r in results:
+                if isinstance(r, BaseException):
+                    raise r
+            return
         for hook in hooks:
-            self.calls += 1
-            try:
-                resp = await self._call(hook, self._review(a, ri))
-            except (ConnectionError, OSError, asyncio.TimeoutError, ValueError) as e:
-                if hook.get("failurePolicy") == "Ignore":
-                    log.warning("failed calling webhook %s, failing open: %s", hook.get("name"), e)
-                    continue
-                raise APIError(500, "InternalError", f'Internal error occurred: failed calling admission webhook "{hook.get("name")}": {e}')
-            if not resp.get("allowed"):
-                res = resp.get("result") or {}
-                raise APIError(int(res.get("code") or 403), res.get("reason") or "Forbidden",
-                               f'admission webhook "{hook.get("name")}" denied the request: {res.get("message", "without explanation")}')
-            if mutating and resp.get("patch"):
+            resp = await self._ask(hook, a, ri)
+            if resp is None:
+                continue
+            if resp.get("patch"):
                 from ..utils.patch import json_patch
                 try:
                     a.obj = json_patch(a.obj, json.loads(base64.b64decode(resp["patch"])))
