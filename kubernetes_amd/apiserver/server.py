@@ -1632,22 +1632,25 @@ class APIServer:
                         pass
             is_watch = watch or req.query.get("watch") in ("true", "1")
             mutating = verb not in ("GET", "HEAD")
-            # max-in-flight (WithMaxInFlightLimit): non-watch requests only
-            if not is_watch:
-                if mutating:
-                    if self.inflight_mut >= self.max_mutating:
-                        self.m_dropped.labels("mutating").inc()
+            # max-in-flight (filters/maxinflight.go WithMaxInFlightLimit): long-running requests
+            # (watch, proxy, exec / attach / portforward / log — BasicLongRunningRequestCheck) are
+            # not counted; a limit of 0 disables its budget; system:masters pass when over it
+            long_running = is_watch or (sub or "").split("/")[0] in ("proxy", "exec", "attach", "portforward", "log")
+            limited = False
+            if not long_running:
+                lim, cur, kind = ((self.max_mutating, self.inflight_mut, "mutating") if mutating
+                                  else (self.max_inflight, self.inflight, "readOnly"))
+                if lim and cur >= lim:
+                    self.m_dropped.labels(kind).inc()
+                    if "system:masters" not in (getattr(user, "groups", None) or ()):
                         code = 429
-                        return Response(429, codec.dumpb(m.status_obj(429, "TooManyRequests", "Too many requests, please try again later.")),
+                        return Response(429, codec.dumpb(m.status_obj(429, "TooManyRequests",
+                                                                      "Too many requests, please try again later.")),
                                         headers={"Retry-After": "1"})
-                elif self.inflight >= self.max_inflight:
-                    self.m_dropped.labels("readOnly").inc()
-                    code = 429
-                    return Response(429, codec.dumpb(m.status_obj(429, "TooManyRequests", "Too many requests, please try again later.")),
-                                    headers={"Retry-After": "1"})
+                limited = True
             if ri.namespaced is False:
                 ns = None
-            if not is_watch:
+            if limited:                              # only budgeted requests are counted
                 if mutating:
                     self.inflight_mut += 1
                 else:
@@ -1674,7 +1677,7 @@ class APIServer:
                 else:
                     resp = await self._dispatch(req, ri, ns, name, sub, is_watch, user)
             finally:
-                if not is_watch:
+                if limited:
                     if mutating:
                         self.inflight_mut -= 1
                     else:

@@ -277,3 +277,38 @@ def test_secure_and_insecure_listeners_from_cli(tmp_path):
     finally:
         p.terminate()
         p.wait(10)
+
+
+def test_max_in_flight_limits(run):
+    """filters/maxinflight.go: 429 + Retry-After over the budget; long-running requests (watch)
+    are not counted; system:masters pass; a limit of 0 disables that budget."""
+    from kubernetes_amd.apiserver.auth import User
+    from kubernetes_amd.apiserver.server import APIServer
+    from kubernetes_amd.client.rest import APIStatusError, Client
+
+    async def main():
+        toks = {"admin": User("admin", "0", ["system:masters"]), "dev": User("dev", "1", ["system:authenticated"])}
+        s = APIServer(tokens=toks, authorization_modes=("AlwaysAllow",), max_requests_inflight=5,
+                      max_mutating_inflight=0)
+        port = await s.start()
+        dev, admin = Client(f"http://127.0.0.1:{port}", token="dev"), Client(f"http://127.0.0.1:{port}", token="admin")
+        try:
+            s.inflight = s.max_inflight                 # the read-only budget is exhausted
+            with pytest.raises(APIStatusError) as e:
+                await dev.list("configmaps", "default")
+            assert e.value.code == 429
+            await admin.list("configmaps", "default")  # system:masters pass
+            await dev.create("configmaps", {"metadata": {"name": "c", "namespace": "default"}})   # mutating: no limit
+            events = []
+            async for ev in await dev.watch("configmaps", "default", resource_version="0", timeout_seconds=1):
+                events.append(ev)      # long-running: served although the read-only budget is full
+                break
+            assert events
+            s.inflight = 0
+            await dev.list("configmaps", "default")
+            assert s.inflight == 0 and s.inflight_mut == 0
+        finally:
+            await dev.close()
+            await admin.close()
+            await s.stop()
+    run(main())
