@@ -312,3 +312,63 @@ def test_max_in_flight_limits(run):
             await admin.close()
             await s.stop()
     run(main())
+
+
+REQUEST_INFO_CASES = [
+    # (method, path, verb, namespace, resource, subresource, name) — requestinfo_test.go TestGetAPIRequestInfo
+    ("GET", "/api/v1/namespaces", "list", "", "namespaces", "", ""),
+    ("GET", "/api/v1/namespaces/other", "get", "", "namespaces", "", "other"),
+    ("GET", "/api/v1/namespaces/other/pods", "list", "other", "pods", "", ""),
+    ("GET", "/api/v1/namespaces/other/pods/foo", "get", "other", "pods", "", "foo"),
+    ("HEAD", "/api/v1/namespaces/other/pods/foo", "get", "other", "pods", "", "foo"),
+    ("GET", "/api/v1/pods", "list", "", "pods", "", ""),
+    ("GET", "/api/v1/watch/pods", "watch", "", "pods", "", ""),
+    ("GET", "/api/v1/pods?watch=true", "watch", "", "pods", "", ""),
+    ("GET", "/api/v1/pods?watch=false", "list", "", "pods", "", ""),
+    ("GET", "/api/v1/watch/namespaces/other/pods", "watch", "other", "pods", "", ""),
+    ("GET", "/api/v1/namespaces/other/pods?watch=1", "watch", "other", "pods", "", ""),
+    ("GET", "/api/v1/namespaces/other/pods?watch=0", "list", "other", "pods", "", ""),
+    ("GET", "/api/v1/namespaces/other/pods/foo/status", "get", "other", "pods", "status", "foo"),
+    ("PUT", "/api/v1/namespaces/other/finalize", "update", "", "namespaces", "finalize", "other"),
+    ("PUT", "/api/v1/namespaces/other/status", "update", "", "namespaces", "status", "other"),
+    ("PATCH", "/api/v1/namespaces/other/pods/foo", "patch", "other", "pods", "", "foo"),
+    ("DELETE", "/api/v1/namespaces/other/pods/foo", "delete", "other", "pods", "", "foo"),
+    ("POST", "/api/v1/namespaces/other/pods", "create", "other", "pods", "", ""),
+    ("DELETE", "/api/v1/nodes", "deletecollection", "", "nodes", "", ""),
+    ("DELETE", "/api/v1/namespaces/other/pods", "deletecollection", "other", "pods", "", ""),
+    ("POST", "/apis/extensions/v1beta1/namespaces/other/deployments", "create", "other", "deployments", "", ""),
+]
+
+
+@pytest.mark.parametrize("method,path,verb,ns,resource,sub,name", REQUEST_INFO_CASES,
+                         ids=[f"{c[0]} {c[1]}" for c in REQUEST_INFO_CASES])
+def test_request_info_reaches_the_authorizer(run, method, path, verb, ns, resource, sub, name):
+    """The attributes the authorizer sees for each request shape (RequestInfoFactory)."""
+    from kubernetes_amd.client.http import HTTPClient
+
+    class Recorder:
+        def __init__(self):
+            self.seen = []
+
+        def authorize(self, a):
+            if a.resource_request:
+                self.seen.append((a.verb, a.namespace or "", a.resource, a.subresource or "", a.name or ""))
+            return False, "recorded"
+
+    async def main():
+        from kubernetes_amd.apiserver.auth import User
+        s = APIServer(authorization_modes=("AlwaysAllow",), tokens={"t": User("u", "1", ["system:authenticated"])})
+        rec = s.authz = Recorder()
+        port = await s.start()
+        c = HTTPClient(f"http://127.0.0.1:{port}")
+        try:
+            body = b"{}" if method in ("POST", "PUT", "PATCH") else None
+            ctype = "application/merge-patch+json" if method == "PATCH" else "application/json"
+            await c.request(method, path, body, ctype, {"Authorization": "Bearer t"})
+        except Exception:
+            pass
+        finally:
+            await c.close()
+            await s.stop()
+        assert rec.seen and rec.seen[0] == (verb, ns, resource, sub, name), rec.seen
+    run(main())
