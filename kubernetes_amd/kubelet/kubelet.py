@@ -1613,32 +1613,19 @@ class Kubelet:
         spec = pod.get("spec") or {}
         rt = self.runtime
         statuses, init_statuses = [], []
-        running = terminated_ok = terminated_bad = waiting = restarting = 0
-        not_ready = 0
+        running = not_ready = 0
         for c in spec.get("containers") or ():
             cid = st.containers.get(c["name"])
             cs = rt.container_status(cid) if cid else None
-            s = _container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"]))
+            prev = st.previous.get(c["name"])
+            pcs = rt.container_status(prev) if prev and prev != cid else None
+            s = _container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"]), pcs)
             statuses.append(s)
-            if cs is None:
-                if st.restarts.get(c["name"], 0) > 0:
-                    # between a restart's kill and the new container: the reference's "waiting with
-                    # a last termination state" counts as stopped, so the pod does not flap to Pending
-                    restarting += 1
-                else:
-                    waiting += 1
-            elif cs.state == RUNNING:
+            if cs is not None and cs.state == RUNNING:
                 running += 1
                 if c.get("readinessProbe") and not self.probes.ready(st.uid, c["name"]):
                     s["ready"] = False
                     not_ready += 1
-            elif cs.state == EXITED:
-                if cs.exit_code == 0:
-                    terminated_ok += 1
-                else:
-                    terminated_bad += 1
-            else:
-                waiting += 1
         init_done = True
         for c in spec.get("initContainers") or ():
             cid = st.init_containers.get(c["name"])
@@ -1646,32 +1633,8 @@ class Kubelet:
             init_statuses.append(_container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"])))
             if cs is None or cs.state != EXITED or cs.exit_code != 0:
                 init_done = False
-        policy = spec.get("restartPolicy", "Always")
         n = len(spec.get("containers") or ())
-        init_failed = any((s.get("state") or {}).get("terminated", {}).get("exitCode", 0) != 0 for s in init_statuses)
-        # `GetPhase` (kubelet_pods.go:1270): a failed init container fails a Never pod; pending
-        # initialization or ANY waiting container keeps the pod Pending; then Running while a
-        # container runs; all stopped -> Running (Always), Succeeded (all exit 0), Failed (Never)
-        # or Running (OnFailure restarts the failed ones)
-        if init_failed and policy == "Never":
-            phase = core.POD_FAILED
-        elif not init_done:
-            phase = core.POD_PENDING
-        elif waiting:
-            phase = core.POD_PENDING
-        elif running:
-            phase = core.POD_RUNNING
-        elif terminated_ok + terminated_bad + restarting == n:
-            if policy == "Always":
-                phase = core.POD_RUNNING
-            elif terminated_ok == n:
-                phase = core.POD_SUCCEEDED
-            elif policy == "Never":
-                phase = core.POD_FAILED
-            else:
-                phase = core.POD_RUNNING
-        else:
-            phase = core.POD_PENDING if waiting else core.POD_RUNNING
+        phase = get_phase(spec, statuses, init_statuses)
         ready = phase == core.POD_RUNNING and running == n and not not_ready
         now = now_rfc3339()
         old_conds = {c["type"]: c for c in (pod.get("status") or {}).get("conditions") or ()}
@@ -1839,7 +1802,90 @@ def _ts(t):
     return now_rfc3339(t) if t else None
 
 
-def _container_status(c, cs, restarts, waiting=None):
+def get_phase(spec, statuses, init_statuses=()):
+    """`kubelet_pods.go` GetPhase over v1 container statuses: a failed init container fails a
+    Never pod; initialization in progress or a waiting container (one with no previous
+    termination) keeps it Pending; running containers with none unknown -> Running; all stopped
+    (a waiting container with a last termination counts as stopped) -> Running for Always,
+    Succeeded when every one exited 0, Failed for Never, else Running (OnFailure restarts)."""
+    by_name = {s["name"]: s for s in statuses or ()}
+    init_by_name = {s["name"]: s for s in init_statuses or ()}
+    pending_init = failed_init = 0
+    for c in spec.get("initContainers") or ():
+        s = init_by_name.get(c["name"])
+        st = (s or {}).get("state") or {}
+        last = ((s or {}).get("lastState") or {}).get("terminated")
+        if s is None or "running" in st:
+            pending_init += 1
+        elif "terminated" in st:
+            if st["terminated"].get("exitCode", 0) != 0:
+                failed_init += 1
+        elif "waiting" in st and last is not None:
+            if last.get("exitCode", 0) != 0:
+                failed_init += 1
+        else:
+            pending_init += 1
+    unknown = running = waiting = stopped = succeeded = 0
+    for c in spec.get("containers") or ():
+        s = by_name.get(c["name"])
+        st = (s or {}).get("state") or {}
+        if s is None or not st:
+            unknown += 1
+        elif "running" in st:
+            running += 1
+        elif "terminated" in st:
+            stopped += 1
+            if st["terminated"].get("exitCode", 0) == 0:
+                succeeded += 1
+        elif "waiting" in st:
+            if ((s.get("lastState") or {}).get("terminated")) is not None:
+                stopped += 1
+            else:
+                waiting += 1
+        else:
+            unknown += 1
+    policy = spec.get("restartPolicy", "Always")
+    if failed_init and policy == "Never":
+        return core.POD_FAILED
+    if pending_init or waiting:
+        return core.POD_PENDING
+    if running and not unknown:
+        return core.POD_RUNNING
+    if not running and stopped and not unknown:
+        if policy == "Always":
+            return core.POD_RUNNING
+        if stopped == succeeded:
+            return core.POD_SUCCEEDED
+        if policy == "Never":
+            return core.POD_FAILED
+        return core.POD_RUNNING
+    return core.POD_PENDING
+
+
+def _last_state(pcs):
+    """lastState.terminated from the previous (dead) instance of a restarted container."""
+    if pcs is None or pcs.state != EXITED:
+        return None
+    return {"terminated": {"exitCode": pcs.exit_code, "reason": pcs.reason or ("Completed" if pcs.exit_code == 0
+                                                                               else "Error"),
+                           "startedAt": _ts(pcs.started_at), "finishedAt": _ts(pcs.finished_at),
+                           "containerID": pcs.id}}
+
+
+def _container_status(c, cs, restarts, waiting=None, pcs=None):
+    s = _container_status_now(c, cs, restarts, waiting)
+    if "lastState" not in s:
+        last = _last_state(pcs)
+        if last is not None:
+            s["lastState"] = last
+        elif cs is None and restarts > 0:
+            # between a restart's kill and the new container: the previous instance is gone from
+            # the runtime, but the container did terminate (keeps the pod from flapping to Pending)
+            s["lastState"] = {"terminated": {"exitCode": 0, "reason": "Unknown"}}
+    return s
+
+
+def _container_status_now(c, cs, restarts, waiting=None):
     s = {"name": c["name"], "image": c.get("image", ""), "imageID": "", "restartCount": restarts, "ready": False}
     if cs is not None and waiting and waiting[0] == "CrashLoopBackOff" and cs.state == EXITED:
         s["containerID"] = cs.id

@@ -101,7 +101,10 @@ def test_readiness_and_liveness_probes(run):
             # liveness failed twice -> container killed and restarted
             p = await cond(lambda p: p["status"]["containerStatuses"][0]["restartCount"] >= 1)
             rt.exec_codes[(uid, "c")] = 0
-            await cond(lambda p: ready(p) and p["status"]["containerStatuses"][0]["state"].get("running"))
+            p = await cond(lambda p: ready(p) and p["status"]["containerStatuses"][0]["state"].get("running"))
+            # the killed instance is the restarted container's lastState (kubectl describe "Last State")
+            last = p["status"]["containerStatuses"][0].get("lastState", {}).get("terminated")
+            assert last is not None and "exitCode" in last, p["status"]["containerStatuses"][0]
             # prober.go: every failed probe is an Unhealthy event naming the probe type
             emitted = cl.nodes[0].kubelet.recorder.emitted
             assert any(r == "Unhealthy" and m.startswith("Readiness probe failed") for _t, r, m in emitted)

@@ -234,3 +234,58 @@ def test_static_policy_add(topo, default, req, lim, want):
             take_by_topology(t, default - reserved, n)
     else:
         assert take_by_topology(t, default - reserved, n) == want
+
+
+# -- kubelet_pods_test.go TestPodPhaseWithRestart{Always,Never,OnFailure} ------------------------
+
+def _running(n):
+    return {"name": n, "state": {"running": {}}}
+
+
+def _stopped(n, code=0):
+    return {"name": n, "state": {"terminated": {"exitCode": code}}}
+
+
+def _waiting(n):
+    return {"name": n, "state": {"waiting": {}}}
+
+
+def _waiting_last(n):
+    return {"name": n, "state": {"waiting": {}}, "lastState": {"terminated": {"exitCode": 0}}}
+
+
+PHASE_CASES = {
+    "Always": [([], "Pending"), ([_running("A"), _running("B")], "Running"),
+               ([_stopped("A"), _stopped("B")], "Running"), ([_running("A"), _stopped("B")], "Running"),
+               ([_running("A")], "Pending"), ([_running("A"), _waiting("B")], "Pending"),
+               ([_running("A"), _waiting_last("B")], "Running")],
+    "Never": [([], "Pending"), ([_running("A"), _running("B")], "Running"),
+              ([_stopped("A"), _stopped("B")], "Succeeded"), ([_stopped("A", -1), _stopped("B", -1)], "Failed"),
+              ([_running("A"), _stopped("B")], "Running"), ([_running("A")], "Pending"),
+              ([_running("A"), _waiting("B")], "Pending")],
+    "OnFailure": [([], "Pending"), ([_running("A"), _running("B")], "Running"),
+                  ([_stopped("A"), _stopped("B")], "Succeeded"), ([_stopped("A", -1), _stopped("B", -1)], "Running"),
+                  ([_running("A"), _stopped("B")], "Running"), ([_running("A")], "Pending"),
+                  ([_running("A"), _waiting("B")], "Pending"), ([_running("A"), _waiting_last("B")], "Running")],
+}
+
+
+@pytest.mark.parametrize("policy,statuses,want", [(p, s, w) for p, cases in PHASE_CASES.items() for s, w in cases])
+def test_pod_phase(policy, statuses, want):
+    from kubernetes_amd.kubelet.kubelet import get_phase
+    spec = {"containers": [{"name": "A"}, {"name": "B"}], "restartPolicy": policy}
+    assert get_phase(spec, statuses) == want
+
+
+@pytest.mark.parametrize("policy,init,want", [
+    ("Never", [_stopped("i", 1)], "Failed"), ("Always", [_stopped("i", 1)], "Pending"),
+    ("Always", [_running("i")], "Pending"), ("Always", [_stopped("i")], "Running"),
+    ("OnFailure", [{"name": "i", "state": {"waiting": {}}, "lastState": {"terminated": {"exitCode": 2}}}], "Pending"),
+])
+def test_pod_phase_with_init_containers(policy, init, want):
+    """GetPhase's init-container accounting (kubelet_pods.go: pendingInitialization /
+    failedInitialization); the regular containers run once initialization is done."""
+    from kubernetes_amd.kubelet.kubelet import get_phase
+    spec = {"initContainers": [{"name": "i"}], "containers": [{"name": "A"}], "restartPolicy": policy}
+    statuses = [_running("A")] if want == "Running" else []
+    assert get_phase(spec, statuses, init) == want
