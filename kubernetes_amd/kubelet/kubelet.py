@@ -53,12 +53,48 @@ BOOTSTRAP_CHECKPOINT = "node.kubernetes.io/bootstrap-checkpoint"
 MIN_KILL_GRACE_SECONDS = 2.0        # kuberuntime minimumGracePeriodInSeconds
 
 
-_REF = __import__("re").compile(r"\$\$|\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
+
+
+def expand(s, *contexts):
+    """`third_party/forked/golang/expansion` Expand: a single left-to-right scan — `$$` is an
+    escaped `$`, `$(NAME)` (NAME = everything up to the next `)`) is replaced from the first
+    context that defines it and kept verbatim otherwise, an unclosed `$(` and any other `$x` are
+    literal; values are not re-expanded."""
+    s = str(s)
+    out, i, n = [], 0, len(s)
+    while i < n:
+        ch = s[i]
+        if ch != "$" or i + 1 >= n:
+            out.append(ch)
+            i += 1
+            continue
+        nxt = s[i + 1]
+        if nxt == "$":
+            out.append("$")
+            i += 2
+        elif nxt == "(":
+            close = s.find(")", i + 2)
+            if close < 0:
+                out.append("$(")
+                i += 2
+            else:
+                name = s[i + 2:close]
+                for ctx in contexts:
+                    if name in ctx:
+                        out.append(ctx[name])
+                        break
+                else:
+                    out.append(f"$({name})")
+                i = close + 1
+        else:
+            out.append("$" + nxt)
+            i += 2
+    return "".join(out)
 
 
 def _expand_ref(s, env):
-    """`third_party/forked/golang/expansion`: $(VAR) -> env value (kept when undefined), $$ -> $."""
-    return _REF.sub(lambda m: "$" if m.group(0) == "$$" else env.get(m.group(1), m.group(0)), str(s))
+    """$(VAR) references in command / args (kubecontainer.ExpandContainerCommandAndArgs)."""
+    return expand(s, env)
 
 
 class PodState:

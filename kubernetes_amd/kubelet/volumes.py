@@ -29,6 +29,7 @@ from ..api.quantity import parse_quantity
 from ..client.rest import APIStatusError
 from .volume_plugins import NETWORK_KINDS
 
+_ENV_NAME = re.compile(r"^[-._a-zA-Z][-._a-zA-Z0-9]*$")   # IsEnvVarName (1.9 C_IDENTIFIER relaxed)
 log = logging.getLogger("kubelet.volumes")
 
 
@@ -615,29 +616,34 @@ class VolumeManager:
         env: dict[str, str] = {}
         order = []
 
+        from .kubelet import expand
+        svc = {e["name"]: e["value"] for e in base_env}
+
         def put(k, v):
             if k not in env:
                 order.append(k)
             env[k] = v
-        for e in base_env:
-            put(e["name"], e["value"])
         for ef in container.get("envFrom") or ():
             pre = ef.get("prefix", "")
-            if "configMapRef" in ef:
-                r = ef["configMapRef"]
-                obj = await self._get("configmaps", ns, r["name"], r.get("optional"))
-                for k, v in ((obj or {}).get("data") or {}).items():
-                    put(pre + k, str(v))
-            elif "secretRef" in ef:
-                r = ef["secretRef"]
-                obj = await self._get("secrets", ns, r["name"], r.get("optional"))
-                for k, v in ((obj or {}).get("data") or {}).items():
-                    put(pre + k, base64.b64decode(v).decode(errors="replace"))
+            kind, ref = ("configmaps", ef["configMapRef"]) if "configMapRef" in ef else \
+                (("secrets", ef["secretRef"]) if "secretRef" in ef else (None, None))
+            if kind is None:
+                continue
+            obj = await self._get(kind, ns, ref["name"], ref.get("optional"))
+            invalid = []
+            for k, v in sorted(((obj or {}).get("data") or {}).items()):
+                if not _ENV_NAME.match(pre + k):
+                    invalid.append(k)       # makeEnvironmentVariables: skipped, not fatal
+                    continue
+                put(pre + k, base64.b64decode(v).decode(errors="replace") if kind == "secrets" else str(v))
+            if invalid:
+                log.warning("Keys [%s] from the EnvFrom %s %s/%s were skipped since they are considered invalid "
+                            "environment variable names.", ", ".join(invalid), kind[:-1], ns, ref["name"])
         for e in container.get("env") or ():
             name = e["name"]
             if "value" in e:
-                val = re.sub(r"\$\(([A-Za-z_][A-Za-z0-9_]*)\)", lambda m: env.get(m.group(1), m.group(0)), str(e["value"]))
-                put(name, val)
+                # expansion.MappingFuncFor(env so far, service env): `$(VAR)` from earlier entries
+                put(name, expand(e["value"], env, svc))
                 continue
             vf = e.get("valueFrom") or {}
             if "fieldRef" in vf:
@@ -662,4 +668,8 @@ class VolumeManager:
                             raise VolumeError(f"secret {r['name']} has no key {r['key']}")
                     else:
                         put(name, base64.b64decode(obj["data"][r["key"]]).decode(errors="replace"))
+        # the service variables come last and never override the container's own (kubelet_pods.go)
+        for k, v in svc.items():
+            if k not in env:
+                put(k, v)
         return [{"name": k, "value": env[k]} for k in order]

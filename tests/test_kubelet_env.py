@@ -1,0 +1,81 @@
+"""Container environment and `$(VAR)` expansion.
+
+Reference: `third_party/forked/golang/expansion/expand_test.go` (TestMapping, TestMappingDual:
+the full doExpansionTest table, with one and with two mapping contexts) and
+`pkg/kubelet/kubelet_pods.go` makeEnvironmentVariables (envFrom prefixes, invalid keys skipped,
+`$(VAR)` against earlier entries and the service variables, service variables never overriding).
+"""
+import base64
+
+import pytest
+
+from kubernetes_amd.kubelet.kubelet import expand
+
+CTX = {"VAR_A": "A", "VAR_B": "B", "VAR_C": "C", "VAR_REF": "$(VAR_A)", "VAR_EMPTY": ""}
+CTX1 = {"VAR_A": "A", "VAR_EMPTY": ""}
+CTX2 = {"VAR_B": "B", "VAR_C": "C", "VAR_REF": "$(VAR_A)"}
+
+CASES = [
+    ("$(VAR_A)", "A"), ("$(VAR_A)-$(VAR_A)", "A-A"), ("$(VAR_A)-1", "A-1"), ("___$(VAR_B)___", "___B___"),
+    ("___$(VAR_C)", "___C"), ("$(VAR_A)_$(VAR_B)_$(VAR_C)", "A_B_C"), ("$$(VAR_B)_$(VAR_A)", "$(VAR_B)_A"),
+    ("$$(VAR_A)_$$(VAR_B)", "$(VAR_A)_$(VAR_B)"), ("f000-$$VAR_A", "f000-$VAR_A"),
+    ("foo\\$(VAR_C)bar", "foo\\Cbar"), ("foo\\\\$(VAR_C)bar", "foo\\\\Cbar"),
+    ("foo\\\\\\\\$(VAR_A)bar", "foo\\\\\\\\Abar"), ("$(VAR_A$(VAR_B))", "$(VAR_A$(VAR_B))"),
+    ("$(VAR_A$(VAR_B)", "$(VAR_A$(VAR_B)"), ("$(VAR_REF)", "$(VAR_A)"),
+    ("%%$(VAR_REF)--$(VAR_REF)%%", "%%$(VAR_A)--$(VAR_A)%%"), ("foo$(VAR_EMPTY)bar", "foobar"),
+    ("foo$(VAR_Awhoops!", "foo$(VAR_Awhoops!"), ("f00__(VAR_A)__", "f00__(VAR_A)__"), ("$?_boo_$!", "$?_boo_$!"),
+    ("$VAR_A", "$VAR_A"), ("$(VAR_DNE)", "$(VAR_DNE)"), ("$$$$$$(BIG_MONEY)", "$$$(BIG_MONEY)"),
+    ("$$$$$$(VAR_A)", "$$$(VAR_A)"), ("$$$$$$$(GOOD_ODDS)", "$$$$(GOOD_ODDS)"), ("$$$$$$$(VAR_A)", "$$$A"),
+    ("$VAR_A)", "$VAR_A)"), ("${VAR_A}", "${VAR_A}"), ("$(VAR_B)_______$(A", "B_______$(A"),
+    ("$(VAR_C)_______$(", "C_______$("), ("$(VAR_A)foobarzab$", "Afoobarzab$"), ("foo-\\$(VAR_A", "foo-\\$(VAR_A"),
+    ("--$($($($($--", "--$($($($($--"), ("$($($($($--foo$(", "$($($($($--foo$("), ("foo0--$($($($(", "foo0--$($($($("),
+    ("$(foo$$var)", "$(foo$$var)"), ("\n", "\n"),
+]
+
+
+@pytest.mark.parametrize("inp,want", CASES, ids=[repr(c[0]) for c in CASES])
+def test_mapping(inp, want):
+    assert expand(inp, CTX) == want
+
+
+@pytest.mark.parametrize("inp,want", CASES, ids=[repr(c[0]) for c in CASES])
+def test_mapping_dual(inp, want):
+    assert expand(inp, CTX1, CTX2) == want
+
+
+def test_make_environment_variables(run, tmp_path):
+    from kubernetes_amd.kubelet.volumes import VolumeManager
+
+    class FakeClient:
+        objs = {("configmaps", "ns", "cm"): {"data": {"A": "1", "B": "2", "1bad": "x", "ok.dotted": "3"}},
+                ("secrets", "ns", "sec"): {"data": {"S": base64.b64encode(b"s3cr3t").decode()}}}
+
+        async def get(self, resource, name, namespace=None):
+            return self.objs[(resource, namespace, name)]
+
+    vm = VolumeManager.__new__(VolumeManager)
+    vm.client = FakeClient()
+    vm.host_ip = "10.0.0.1"
+    vm.allocatable = {}
+
+    async def _get(resource, ns, name, optional=None):
+        return FakeClient.objs.get((resource, ns, name))
+    vm._get = _get
+    pod = {"metadata": {"name": "p", "namespace": "ns", "uid": "u"}, "spec": {}}
+    ctr = {"name": "c", "envFrom": [{"configMapRef": {"name": "cm"}, "prefix": "P_"}, {"secretRef": {"name": "sec"}}],
+           "env": [{"name": "X", "value": "$(P_A)-$(SVC_HOST)-$(MISSING)"}, {"name": "SVC_PORT", "value": "override"}]}
+    base = [{"name": "SVC_HOST", "value": "10.1.1.1"}, {"name": "SVC_PORT", "value": "80"}]
+
+    async def main():
+        return await vm.env_for(pod, ctr, "node", "1.2.3.4", base_env=base)
+    env = {e["name"]: e["value"] for e in run(main())}
+    assert env["P_A"] == "1" and env["P_B"] == "2" and env["S"] == "s3cr3t" and env["P_ok.dotted"] == "3"
+    assert "P_1bad" in env             # prefixed, the key becomes a valid name
+    assert env["X"] == "1-10.1.1.1-$(MISSING)"
+    assert env["SVC_PORT"] == "override" and env["SVC_HOST"] == "10.1.1.1"
+    ctr2 = {"name": "c", "envFrom": [{"configMapRef": {"name": "cm"}}]}
+
+    async def main2():
+        return await vm.env_for(pod, ctr2)
+    env2 = {e["name"]: e["value"] for e in run(main2())}
+    assert "1bad" not in env2 and env2["A"] == "1"     # an invalid name is skipped, not fatal
