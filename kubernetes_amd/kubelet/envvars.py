@@ -42,11 +42,16 @@ def service_map(services, namespace) -> dict:
 
 
 def from_services(services) -> list:
+    """`envvars.FromServices`: in the given order, services without a cluster IP skipped; IPv6
+    addresses are bracketed in the URL forms (`net.JoinHostPort`)."""
     env = []
-    for svc in sorted(services, key=lambda s: s["metadata"]["name"]):
+    for svc in services:
+        if not _ip_set(svc):
+            continue
         name = _upper(svc["metadata"]["name"])
         spec = svc.get("spec") or {}
         ip = spec["clusterIP"]
+        host = f"[{ip}]" if ":" in ip else ip
         ports = spec.get("ports") or []
         env.append({"name": f"{name}_SERVICE_HOST", "value": ip})
         if ports:
@@ -56,7 +61,7 @@ def from_services(services) -> list:
                 env.append({"name": f"{name}_SERVICE_PORT_{_upper(p['name'])}", "value": str(p["port"])})
         for i, p in enumerate(ports):
             proto = (p.get("protocol") or "TCP").lower()
-            url = f"{proto}://{ip}:{p['port']}"
+            url = f"{proto}://{host}:{p['port']}"
             prefix = f"{name}_PORT_{p['port']}_{proto.upper()}"
             if i == 0:
                 env.append({"name": f"{name}_PORT", "value": url})
@@ -66,4 +71,4 @@ def from_services(services) -> list:
 
 
 def service_env(services, namespace) -> list:
-    return from_services(service_map(services, namespace).values())
+    return from_services(sorted(service_map(services, namespace).values(), key=lambda s: s["metadata"]["name"]))

@@ -79,3 +79,45 @@ def test_make_environment_variables(run, tmp_path):
         return await vm.env_for(pod, ctr2)
     env2 = {e["name"]: e["value"] for e in run(main2())}
     assert "1bad" not in env2 and env2["A"] == "1"     # an invalid name is skipped, not fatal
+
+
+def test_from_services():
+    """envvars_test.go TestFromServices: the docker-link style variables, IPv6 bracketed in URLs,
+    headless / IP-less services skipped."""
+    from kubernetes_amd.kubelet.envvars import from_services
+
+    def svc(name, ip, *ports):
+        return {"metadata": {"name": name}, "spec": {"clusterIP": ip, "ports": [
+            dict({"port": p, "protocol": proto}, **({"name": n} if n else {})) for n, p, proto in ports]}}
+    services = [svc("foo-bar", "1.2.3.4", (None, 8080, "TCP")),
+                svc("abc-123", "5.6.7.8", ("u-d-p", 8081, "UDP"), ("t-c-p", 8081, "TCP")),
+                svc("q-u-u-x", "9.8.7.6", (None, 8082, "TCP"), ("8083", 8083, "TCP")),
+                svc("svrc-clusterip-none", "None", (None, 8082, "TCP")),
+                svc("svrc-clusterip-empty", "", (None, 8082, "TCP")),
+                svc("super-ipv6", "2001:DB8::", ("u-d-p", 8084, "UDP"), ("t-c-p", 8084, "TCP"))]
+    got = [(e["name"], e["value"]) for e in from_services(services)]
+    want = [
+        ("FOO_BAR_SERVICE_HOST", "1.2.3.4"), ("FOO_BAR_SERVICE_PORT", "8080"), ("FOO_BAR_PORT", "tcp://1.2.3.4:8080"),
+        ("FOO_BAR_PORT_8080_TCP", "tcp://1.2.3.4:8080"), ("FOO_BAR_PORT_8080_TCP_PROTO", "tcp"),
+        ("FOO_BAR_PORT_8080_TCP_PORT", "8080"), ("FOO_BAR_PORT_8080_TCP_ADDR", "1.2.3.4"),
+        ("ABC_123_SERVICE_HOST", "5.6.7.8"), ("ABC_123_SERVICE_PORT", "8081"), ("ABC_123_SERVICE_PORT_U_D_P", "8081"),
+        ("ABC_123_SERVICE_PORT_T_C_P", "8081"), ("ABC_123_PORT", "udp://5.6.7.8:8081"),
+        ("ABC_123_PORT_8081_UDP", "udp://5.6.7.8:8081"), ("ABC_123_PORT_8081_UDP_PROTO", "udp"),
+        ("ABC_123_PORT_8081_UDP_PORT", "8081"), ("ABC_123_PORT_8081_UDP_ADDR", "5.6.7.8"),
+        ("ABC_123_PORT_8081_TCP", "tcp://5.6.7.8:8081"), ("ABC_123_PORT_8081_TCP_PROTO", "tcp"),
+        ("ABC_123_PORT_8081_TCP_PORT", "8081"), ("ABC_123_PORT_8081_TCP_ADDR", "5.6.7.8"),
+        ("Q_U_U_X_SERVICE_HOST", "9.8.7.6"), ("Q_U_U_X_SERVICE_PORT", "8082"), ("Q_U_U_X_SERVICE_PORT_8083", "8083"),
+        ("Q_U_U_X_PORT", "tcp://9.8.7.6:8082"), ("Q_U_U_X_PORT_8082_TCP", "tcp://9.8.7.6:8082"),
+        ("Q_U_U_X_PORT_8082_TCP_PROTO", "tcp"), ("Q_U_U_X_PORT_8082_TCP_PORT", "8082"),
+        ("Q_U_U_X_PORT_8082_TCP_ADDR", "9.8.7.6"), ("Q_U_U_X_PORT_8083_TCP", "tcp://9.8.7.6:8083"),
+        ("Q_U_U_X_PORT_8083_TCP_PROTO", "tcp"), ("Q_U_U_X_PORT_8083_TCP_PORT", "8083"),
+        ("Q_U_U_X_PORT_8083_TCP_ADDR", "9.8.7.6"),
+        ("SUPER_IPV6_SERVICE_HOST", "2001:DB8::"), ("SUPER_IPV6_SERVICE_PORT", "8084"),
+        ("SUPER_IPV6_SERVICE_PORT_U_D_P", "8084"), ("SUPER_IPV6_SERVICE_PORT_T_C_P", "8084"),
+        ("SUPER_IPV6_PORT", "udp://[2001:DB8::]:8084"), ("SUPER_IPV6_PORT_8084_UDP", "udp://[2001:DB8::]:8084"),
+        ("SUPER_IPV6_PORT_8084_UDP_PROTO", "udp"), ("SUPER_IPV6_PORT_8084_UDP_PORT", "8084"),
+        ("SUPER_IPV6_PORT_8084_UDP_ADDR", "2001:DB8::"), ("SUPER_IPV6_PORT_8084_TCP", "tcp://[2001:DB8::]:8084"),
+        ("SUPER_IPV6_PORT_8084_TCP_PROTO", "tcp"), ("SUPER_IPV6_PORT_8084_TCP_PORT", "8084"),
+        ("SUPER_IPV6_PORT_8084_TCP_ADDR", "2001:DB8::"),
+    ]
+    assert got == want
