@@ -15,13 +15,42 @@ import logging
 log = logging.getLogger("kubelet.prober")
 
 
-def _port(container, port):
-    if isinstance(port, int) or (isinstance(port, str) and port.isdigit()):
-        return int(port)
+def extract_port(port, container) -> int:
+    """`prober.go` extractPort: an int, a numeric string or a named container port; the result
+    must be in 1..65535."""
+    if isinstance(port, int) and not isinstance(port, bool):
+        n = port
+    elif isinstance(port, str) and port.lstrip("-").isdigit():
+        n = int(port)
+    elif isinstance(port, str):
+        n = find_port_by_name(container, port)
+    else:
+        raise ValueError(f"invalid port {port!r}")
+    if 0 < n < 65536:
+        return n
+    raise ValueError(f"invalid port number: {n}")
+
+
+def find_port_by_name(container, name) -> int:
     for p in container.get("ports") or ():
-        if p.get("name") == port:
+        if p.get("name") == name:
             return int(p["containerPort"])
-    raise ValueError(f"unknown named port {port!r}")
+    raise ValueError(f"port {name} not found")
+
+
+_port = extract_port       # the old name
+
+
+def format_url(scheme, host, port, path) -> str:
+    """`prober.go` formatURL: scheme://host:port plus the path (and its query)."""
+    h = f"[{host}]" if ":" in host and not host.startswith("[") else host
+    return f"{scheme.lower()}://{h}:{port}{path}"
+
+
+def _request_target(path) -> str:
+    if not path:
+        return "/"
+    return path if path.startswith("/") else "/" + path
 
 
 async def run_probe(runtime, pod, container, cid, probe, pod_ip="127.0.0.1"):
@@ -34,13 +63,21 @@ async def run_probe(runtime, pod, container, cid, probe, pod_ip="127.0.0.1"):
         if "httpGet" in probe:
             h = probe["httpGet"]
             host = h.get("host") or pod_ip
-            port = _port(container, h.get("port"))
-            path = h.get("path") or "/"
-            hdrs = "".join(f"{x['name']}: {x['value']}\r\n" for x in h.get("httpHeaders") or ())
-            r, w = await asyncio.wait_for(asyncio.open_connection(host, port), timeout)
+            port = extract_port(h.get("port"), container)
+            path = _request_target(h.get("path") or "")
+            ssl_ctx = None
+            if (h.get("scheme") or "HTTP").upper() == "HTTPS":
+                import ssl
+                ssl_ctx = ssl.create_default_context()      # http.go: InsecureSkipVerify
+                ssl_ctx.check_hostname = False
+                ssl_ctx.verify_mode = ssl.CERT_NONE
+            headers = {"Host": f"{host}:{port}", "User-Agent": "kube-probe/1.9"}
+            for x in h.get("httpHeaders") or ():
+                headers[x["name"]] = x["value"]             # a user Host header replaces the default
+            hdrs = "".join(f"{k}: {v}\r\n" for k, v in headers.items())
+            r, w = await asyncio.wait_for(asyncio.open_connection(host, port, ssl=ssl_ctx), timeout)
             try:
-                w.write(f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nUser-Agent: kube-probe/1.9\r\n{hdrs}"
-                        f"Connection: close\r\n\r\n".encode())
+                w.write(f"GET {path} HTTP/1.1\r\n{hdrs}Connection: close\r\n\r\n".encode())
                 line = await asyncio.wait_for(r.readline(), timeout)
             finally:
                 w.close()
@@ -49,8 +86,8 @@ async def run_probe(runtime, pod, container, cid, probe, pod_ip="127.0.0.1"):
             return 200 <= code < 400, f"HTTP probe status {code}"
         if "tcpSocket" in probe:
             t = probe["tcpSocket"]
-            r, w = await asyncio.wait_for(asyncio.open_connection(t.get("host") or pod_ip, _port(container, t["port"])),
-                                          timeout)
+            r, w = await asyncio.wait_for(asyncio.open_connection(t.get("host") or pod_ip,
+                                                                  extract_port(t.get("port"), container)), timeout)
             w.close()
             return True, ""
     except (OSError, asyncio.TimeoutError, ValueError, NotImplementedError) as e:
