@@ -144,56 +144,141 @@ class ImageManager:
         return max(0.0, b[0] - self.clock()) if b else 0.0
 
 
+def validate_image_gc_policy(high, low):
+    """image_gc_manager.go NewImageGCManager checks."""
+    if not 0 <= high <= 100:
+        raise ValueError(f"invalid HighThresholdPercent {high}, must be in range [0-100]")
+    if not 0 <= low <= 100:
+        raise ValueError(f"invalid LowThresholdPercent {low}, must be in range [0-100]")
+    if low > high:
+        raise ValueError(f"LowThresholdPercent {low} can not be higher than HighThresholdPercent {high}")
+
+
+class ImageGCError(Exception):
+    pass
+
+
 class ImageGCManager:
+    """`pkg/kubelet/images/image_gc_manager.go` realImageGCManager.
+
+    Records per image ID: first detected (the zero time for images present at the first
+    detection, so a restarted kubelet can reclaim them at once), last used (refreshed whenever a
+    container on the node uses it) and size; records of images that disappeared are dropped.
+    `free_space(n)` removes unused images least-recently-used first (ties: earliest detected),
+    skipping those used at or after the free time and those younger than `min_age`, until n bytes
+    are freed; removal errors are collected and raised after the pass. `garbage_collect()` runs
+    when image-fs usage reaches `high`% and frees down to `low`%; freeing less than that is an
+    error, as is a zero-capacity filesystem.
+    """
+
     def __init__(self, service, capacity_bytes, in_use, high=85, low=80, min_age=120.0, clock=time.time,
-                 last_used=None):
-        """in_use() -> set of image refs/tags used by containers that exist on the node."""
-        if not 0 <= low < high <= 100:
-            raise ValueError("LowThresholdPercent must be less than HighThresholdPercent")
+                 last_used=None, recorder=None):
+        """in_use() -> set of image IDs / refs used by containers that exist on the node."""
+        validate_image_gc_policy(high, low)
         self.service = service
         self.capacity = capacity_bytes
         self.in_use = in_use
         self.high, self.low = high, low
         self.min_age = min_age
         self.clock = clock
-        self.first_seen: dict[str, float] = {}
-        self.last_used = last_used if last_used is not None else {}
+        self.records: dict[str, dict] = {}
+        self.initialized = False
         self.freed_total = 0
+        self.recorder = recorder          # (type, reason, message) -> None
+        for iid, t in (last_used or {}).items():
+            self.records[iid] = {"first": 0.0, "last": t, "size": 0}
 
-    async def detect(self):
+    # back-compat views used by the kubelet / tests
+    @property
+    def first_seen(self):
+        return {k: r["first"] for k, r in self.records.items()}
+
+    @property
+    def last_used(self):
+        return {k: r["last"] for k, r in self.records.items()}
+
+    @staticmethod
+    def _used(img, used):
+        return img["id"] in used or any(t in used for t in img.get("repoTags") or ())
+
+    async def detect(self, detect_time=None):
+        """detectImages: a first detection stamps images with the zero time."""
+        if detect_time is None:
+            detect_time = self.clock() if self.initialized else 0.0
+        self.initialized = True
         imgs = await self.service.list_images()
         now = self.clock()
         used = self.in_use()
+        current = set()
         for i in imgs:
-            self.first_seen.setdefault(i["id"], now)
-            if i["id"] in used or any(t in used for t in i["repoTags"]):
-                self.last_used[i["id"]] = now
+            current.add(i["id"])
+            rec = self.records.setdefault(i["id"], {"first": detect_time, "last": 0.0, "size": 0})
+            if self._used(i, used):
+                rec["last"] = now
+            rec["size"] = int(i.get("size") or 0)
+        for k in list(self.records):
+            if k not in current:
+                del self.records[k]
         return imgs
 
-    async def garbage_collect(self):
-        """Returns bytes freed."""
-        fs = await self.service.image_fs_info()
-        usage = fs["usedBytes"]
-        if self.capacity <= 0 or usage * 100 < self.high * self.capacity:
-            return 0
-        target = usage - self.low * self.capacity // 100
-        return await self.free_space(target)
-
-    async def free_space(self, want):
-        imgs = await self.detect()
+    async def free_space(self, want, free_time=None):
+        """freeSpace: returns bytes freed; raises ImageGCError after the pass if removals failed."""
+        if free_time is None:
+            free_time = self.clock()
+        imgs = {i["id"]: i for i in await self.detect(free_time)}
         used = self.in_use()
-        now = self.clock()
-        cands = [i for i in imgs if i["id"] not in used and not any(t in used for t in i["repoTags"])]
-        cands.sort(key=lambda i: (self.last_used.get(i["id"], 0.0), self.first_seen.get(i["id"], now)))
-        freed = 0
-        for i in cands:
+        cands = [(k, r) for k, r in self.records.items() if not (k in imgs and self._used(imgs[k], used))]
+        cands.sort(key=lambda kr: (kr[1]["last"], kr[1]["first"]))
+        freed, errors = 0, []
+        for k, r in cands:
+            if r["last"] >= free_time:
+                continue                  # used since the free started
+            if free_time - r["first"] < self.min_age:
+                continue
+            try:
+                await self.service.remove_image(k)
+            except Exception as e:        # continue despite errors
+                errors.append(f"{k}: {e}")
+                continue
+            del self.records[k]
+            freed += r["size"]
             if freed >= want:
                 break
-            if now - self.first_seen.get(i["id"], now) < self.min_age:
-                continue
-            await self.service.remove_image(i["id"])
-            self.first_seen.pop(i["id"], None)
-            self.last_used.pop(i["id"], None)
-            freed += i["size"]
         self.freed_total += freed
+        if errors:
+            raise ImageGCError(f"wanted to free {want} bytes, but freed {freed} bytes space with errors in image "
+                               f"deletion: {errors}")
+        return freed
+
+    async def delete_unused_images(self):
+        """DeleteUnusedImages: free every unused image (eviction's image reclaim)."""
+        return await self.free_space(1 << 62, self.clock())
+
+    async def _fs_stats(self):
+        fs = await self.service.image_fs_info()
+        cap = int(fs.get("capacityBytes") or self.capacity or 0)
+        if fs.get("availableBytes") is not None:
+            avail = int(fs["availableBytes"])
+        else:
+            avail = cap - int(fs.get("usedBytes") or 0)
+        return cap, min(max(avail, 0), cap)
+
+    async def garbage_collect(self):
+        """GarbageCollect: returns bytes freed (0 below the high threshold)."""
+        cap, avail = await self._fs_stats()
+        if cap <= 0:
+            if self.recorder:
+                self.recorder("Warning", "InvalidDiskCapacity", "invalid capacity 0 on image filesystem")
+            raise ImageGCError("invalid capacity 0 on image filesystem")
+        usage_pct = 100 - avail * 100 // cap
+        if usage_pct < self.high:
+            return 0
+        amount = cap * (100 - self.low) // 100 - avail
+        freed = await self.free_space(amount, self.clock())
+        if freed < amount:
+            msg = (f"failed to garbage collect required amount of images. Wanted to free {amount} bytes, "
+                   f"but freed {freed} bytes")
+            if self.recorder:
+                self.recorder("Warning", "FreeDiskSpaceFailed", msg)
+            raise ImageGCError(msg)
         return freed

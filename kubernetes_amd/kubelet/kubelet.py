@@ -387,7 +387,16 @@ class Kubelet:
                 list((s.pod.get("spec") or {}).get("initContainers") or ())}
 
     async def _image_gc_loop(self):
-        """image_gc_manager.go: GarbageCollect every ImageGCPeriod (5 min)."""
+        """image_gc_manager.go: `Start` detects images right away (stamped with the zero time, so
+        images present before a kubelet restart are reclaimable at once) and then every period;
+        `kubelet.StartGarbageCollection` runs GarbageCollect every ImageGCPeriod (5 min)."""
+        if self.image_gc.recorder is None:
+            node_ref = {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}}
+            self.image_gc.recorder = lambda typ, reason, msg: self.recorder.event(node_ref, typ, reason, msg)
+        try:
+            await self.image_gc.detect()
+        except Exception as e:
+            log.warning("image detection failed: %s", e)
         while not self._stopped:
             await asyncio.sleep(self.image_gc_period)
             try:
@@ -422,7 +431,7 @@ class Kubelet:
         fns_inodes.append(containers)
         if getattr(self, "image_gc", None) is not None:
             async def images(report=True):
-                freed = await self.image_gc.free_space(1 << 62)        # `DeleteUnusedImages`
+                freed = await self.image_gc.delete_unused_images()
                 return freed if report else 0
             fns_space.append(images)
             fns_inodes.append(lambda: images(False))

@@ -13,7 +13,7 @@ import pytest
 from kubernetes_amd.cri import api as A
 from kubernetes_amd.cri.remote import RemoteRuntime
 from kubernetes_amd.cri.server import CRIServer, ImageStore, LocalImageService, stub_image_resolver
-from kubernetes_amd.kubelet.images import ImageGCManager, ImageManager, ImagePullError, default_pull_policy
+from kubernetes_amd.kubelet.images import ImageGCError, ImageGCManager, ImageManager, ImagePullError, default_pull_policy
 from kubernetes_amd.kubelet.runtime.base import EXITED, RUNNING, RunContainerOptions, RuntimeError_
 from kubernetes_amd.kubelet.runtime.process import ProcessRuntime
 from kubernetes_amd.kubelet.runtime.stub import StubRuntime
@@ -194,14 +194,15 @@ def test_image_gc_frees_lru_unused(run):
         t = [1000.0]
         in_use = {"d:1"}
         gc = ImageGCManager(svc, capacity_bytes=100, in_use=lambda: in_use, high=85, low=50, min_age=10, clock=lambda: t[0])
-        await gc.detect()
-        assert await gc.garbage_collect() == 0            # all images younger than min_age
+        await gc.detect(t[0])
+        with pytest.raises(ImageGCError, match="but freed 0 bytes"):
+            await gc.garbage_collect()                     # all images younger than min_age
         t[0] += 20
-        gc.last_used[store.by_tag["a:1"]] = 990.0         # a used most recently among the unused ones
-        freed = await gc.garbage_collect()                 # usage 120 > 85 -> free down to 50 (need 70)
-        assert freed == 90
+        gc.records[store.by_tag["a:1"]]["last"] = 990.0   # a used most recently among the unused ones
+        freed = await gc.garbage_collect()                 # fs full (0 available) -> free down to 50% (need 50)
+        assert freed == 60                                 # b and c (never used) go first, then it stops
         left = sorted(t for i in store.images.values() for t in i["repo_tags"])
-        assert left == ["d:1"]                             # in-use image kept
+        assert left == ["a:1", "d:1"]                      # in-use image kept, a used more recently
     run(main())
 
 
