@@ -266,22 +266,47 @@ class DeploymentStrategy(WorkloadStrategy):
     generation_on_annotations = True
 
 
+_QOS_RESOURCES = ("cpu", "memory")
+
+
+def _qos_resource(name) -> bool:
+    """isSupportedQoSComputeResource: cpu, memory and hugepages-<size>."""
+    return name in _QOS_RESOURCES or name.startswith("hugepages-")
+
+
 def qos_class(pod) -> str:
-    """`qos.GetPodQOS`."""
+    """`qos.GetPodQOS` (pkg/apis/core/v1/helper/qos/qos.go): positive cpu/memory requests and
+    limits are summed over the app containers; BestEffort without any, Guaranteed when every
+    container limits both and the summed requests equal the summed limits for each resource
+    (requests left unset by the client were defaulted to the limits), else Burstable. Other
+    resources (GPUs) never affect the class; hugepages are summed like cpu/memory, and a container
+    limiting hugepages as well counts 3 limited resources against the 2 the rule expects, so it is
+    Burstable, as in the reference."""
     requests, limits, guaranteed = {}, {}, True
     for c in (pod.get("spec") or {}).get("containers") or ():
         res = c.get("resources") or {}
-        r, lim = res.get("requests") or {}, res.get("limits") or {}
-        for k in ("cpu", "memory"):
-            if k in r and parse_quantity(str(r[k])).value != 0:
-                requests[k] = True
-            if k in lim and parse_quantity(str(lim[k])).value != 0:
-                limits[k] = True
-            if k not in lim or (k in r and str(r[k]) != str(lim[k]) and parse_quantity(str(r[k])) != parse_quantity(str(lim[k]))):
-                guaranteed = False
+        for k, v in (res.get("requests") or {}).items():
+            if _qos_resource(k):
+                qv = parse_quantity(str(v))
+                if qv.value > 0:
+                    requests[k] = requests[k] + qv if k in requests else qv
+        found = 0
+        for k, v in (res.get("limits") or {}).items():
+            if _qos_resource(k):
+                qv = parse_quantity(str(v))
+                if qv.value > 0:
+                    found += 1
+                    limits[k] = limits[k] + qv if k in limits else qv
+        if found != len(_QOS_RESOURCES):
+            guaranteed = False
     if not requests and not limits:
         return "BestEffort"
-    if guaranteed and len(limits) == 2:
+    if guaranteed:
+        for k, req in requests.items():
+            if k not in limits or limits[k] != req:
+                guaranteed = False
+                break
+    if guaranteed and len(requests) == len(limits):
         return "Guaranteed"
     return "Burstable"
 

@@ -37,8 +37,9 @@ from ..client.rest import APIStatusError, is_conflict, is_not_found
 from ..utils.httpserver import HTTPServer, Response, StreamResponse
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from .devicemanager.manager import AdmitError, ManagerStub
+from .podstatus import generate_pod_initialized_condition, generate_pod_ready_condition, normalize_status
 from .prober import ProbeManager
-from .runtime.base import EXITED, RUNNING, RunContainerOptions
+from .runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, RunContainerOptions
 from .qos import oom_score_adj
 from .volumes import VolumeError, VolumeManager
 from ..utils.tasks import spawn
@@ -90,11 +91,6 @@ def expand(s, *contexts):
             out.append("$" + nxt)
             i += 2
     return "".join(out)
-
-
-def _expand_ref(s, env):
-    """$(VAR) references in command / args (kubecontainer.ExpandContainerCommandAndArgs)."""
-    return expand(s, env)
 
 
 class PodState:
@@ -423,9 +419,8 @@ class Kubelet:
         fns_space, fns_inodes = [], []
 
         async def containers():
-            # `DeleteAllUnusedContainers`: every dead container, whatever the GC policy keeps
-            await self.garbage_collect_containers(policy={"min_age": 0.0, "max_per_pod_container": 0,
-                                                          "max_containers": 0})
+            # `DeleteAllUnusedContainers`: the GC policy, plus every dead container of terminated pods
+            await self.garbage_collect_containers(evict_terminated=True)
             return 0
         fns_space.append(containers)
         fns_inodes.append(containers)
@@ -1084,8 +1079,8 @@ class Kubelet:
             cid = st.containers.get(c["name"])
             if cid is not None:
                 cs = rt.container_status(cid)
-                if cs is not None and cs.state == EXITED:
-                    restart = policy == "Always" or (policy == "OnFailure" and cs.exit_code != 0)
+                if cs is not None and cs.state != RUNNING:
+                    restart = should_container_be_restarted(policy, cs)
                     if restart and not md_deleting(pod) and self._in_backoff(st, c, cs):
                         continue
                     if restart and not md_deleting(pod):
@@ -1282,9 +1277,8 @@ class Kubelet:
         if any("$(" in str(x) for x in (spec_c.get("command") or []) + (spec_c.get("args") or [])):
             # `kubecontainer.ExpandContainerCommandAndArgs`: $(VAR) from the container's resolved
             # environment; unknown references stay as written, $$ escapes
-            envmap = {e["name"]: str(e.get("value", "")) for e in spec_c.get("env") or () if "value" in e}
-            spec_c = dict(spec_c, command=[_expand_ref(x, envmap) for x in spec_c.get("command") or ()],
-                          args=[_expand_ref(x, envmap) for x in spec_c.get("args") or ()])
+            cmd, args = expand_container_command_and_args(spec_c, spec_c.get("env") or ())
+            spec_c = dict(spec_c, command=cmd or [], args=args or [])
         if self.cpu_manager is not None:
             from .cpumanager import format_cpulist
             try:
@@ -1407,53 +1401,52 @@ class Kubelet:
         st.waiting.pop(c["name"], None)
         return False
 
-    async def garbage_collect_containers(self, now=None, policy=None):
-        """`pkg/kubelet/container_gc.go` + `kuberuntime_gc.go`: dead containers older than
-        `min_age` are evictable; keep at most `max_per_pod_container` per (pod, container) and
-        `max_containers` overall (oldest first); containers of pods the kubelet no longer
-        tracks are always removed. Returns the removed container ids."""
+    async def garbage_collect_containers(self, now=None, policy=None, evict_terminated=False):
+        """`pkg/kubelet/kuberuntime/kuberuntime_gc.go` evictContainers over the runtime's
+        containers (see `containers_to_evict`). Instances the kubelet still reports a live pod's
+        status from (the latest of each container) count toward the limits but are never removed
+        here; they go with the pod. Containers of no tracked pod belong to deleted pods. Returns
+        the removed container ids."""
         pol = policy if policy is not None else (self.container_gc or {})
         now = now or time.time()
-        min_age = float(pol.get("min_age", 0.0))
-        per = int(pol.get("max_per_pod_container", 1))
-        total = int(pol.get("max_containers", -1))
-        live = set()
-        evictable = []            # (finished_at, cid, st, name)
+        rt = self.runtime
+        recs, owner, current = [], {}, set()
         for st in self.pods.values():
-            live.update(x for x in st.containers.values() if x)
-            live.update(x for x in st.init_containers.values() if x)
-            for name, cid in list(st.previous.items()):
-                cs = self.runtime.container_status(cid)
-                if cs is None:
-                    st.previous.pop(name, None)
+            for name, cid in list(st.containers.items()) + list(st.init_containers.items()):
+                if cid:
+                    current.add(cid)
+            for name, cid in list(st.containers.items()) + list(st.init_containers.items()) + list(st.previous.items()):
+                if not cid or cid in owner:
                     continue
-                if now - (cs.finished_at or cs.created_at) >= min_age:
-                    evictable.append((cs.finished_at or cs.created_at, cid, st, name))
-        removed = []
-        keep = evictable
-        if per >= 0:
-            keep = []
-            by_key = {}
-            for ent in sorted(evictable, reverse=True):
-                k = (ent[2].uid, ent[3])
-                by_key[k] = by_key.get(k, 0) + 1
-                (keep if by_key[k] <= per else removed).append(ent)
-        if total >= 0 and len(keep) > total:
-            keep.sort()
-            removed += keep[:len(keep) - total]
+                cs = rt.container_status(cid)
+                if cs is None:
+                    if st.previous.get(name) == cid:
+                        st.previous.pop(name, None)
+                    continue
+                owner[cid] = (st, name)
+                recs.append((cid, st.uid, name, cs.created_at, cs.state))
+        for cs in list(rt.list_containers()):
+            if cs.id not in owner:
+                recs.append((cs.id, "", cs.name, cs.created_at, cs.state))
+
+        def deleted(uid):
+            st = self.pods.get(uid) if uid else None
+            return st is None or st.deleted
+
+        def terminated(uid):
+            st = self.pods.get(uid)
+            return st is not None and st.terminated
+
         out = []
-        for _, cid, st, name in removed:
-            await self.runtime.remove_container(cid)
+        for cid in containers_to_evict(recs, pol, now, deleted, terminated, evict_terminated):
+            if cid in current:
+                continue
+            await rt.remove_container(cid)
             self._unlink_log(cid)
-            if st.previous.get(name) == cid:
-                st.previous.pop(name, None)
+            ent = owner.get(cid)
+            if ent is not None and ent[0].previous.get(ent[1]) == cid:
+                ent[0].previous.pop(ent[1], None)
             out.append(cid)
-        for cs in list(self.runtime.list_containers()):
-            if cs.state == EXITED and cs.id not in live and not any(cs.id in st.previous.values() for st in self.pods.values()) \
-                    and now - (cs.finished_at or cs.created_at) >= min_age:
-                await self.runtime.remove_container(cs.id)
-                self._unlink_log(cs.id)
-                out.append(cs.id)
         return out
 
     async def _container_gc_loop(self):
@@ -1658,7 +1651,6 @@ class Kubelet:
         spec = pod.get("spec") or {}
         rt = self.runtime
         statuses, init_statuses = [], []
-        running = not_ready = 0
         for c in spec.get("containers") or ():
             cid = st.containers.get(c["name"])
             cs = rt.container_status(cid) if cid else None
@@ -1667,36 +1659,31 @@ class Kubelet:
             s = _container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"]), pcs)
             statuses.append(s)
             if cs is not None and cs.state == RUNNING:
-                running += 1
                 if c.get("readinessProbe") and not self.probes.ready(st.uid, c["name"]):
                     s["ready"] = False
-                    not_ready += 1
-        init_done = True
         for c in spec.get("initContainers") or ():
             cid = st.init_containers.get(c["name"])
             cs = rt.container_status(cid) if cid else None
-            init_statuses.append(_container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"])))
-            if cs is None or cs.state != EXITED or cs.exit_code != 0:
-                init_done = False
-        n = len(spec.get("containers") or ())
+            ics = _container_status(c, cs, st.restarts.get(c["name"], 0), st.waiting.get(c["name"]))
+            # prober_manager.go UpdatePodStatus: an init container is ready once it exited 0
+            ics["ready"] = cs is not None and cs.state == EXITED and cs.exit_code == 0
+            init_statuses.append(ics)
         phase = get_phase(spec, statuses, init_statuses)
-        ready = phase == core.POD_RUNNING and running == n and not not_ready
         now = now_rfc3339()
         old_conds = {c["type"]: c for c in (pod.get("status") or {}).get("conditions") or ()}
 
-        def cond(t, ok, reason=None):
-            s = "True" if ok else "False"
-            prev = old_conds.get(t)
-            c = {"type": t, "status": s, "lastProbeTime": None,
-                 "lastTransitionTime": prev["lastTransitionTime"] if prev and prev.get("status") == s else now}
-            if reason and not ok:
-                c["reason"] = reason
+        def cond(c):
+            prev = old_conds.get(c["type"])
+            c["lastProbeTime"] = None
+            c["lastTransitionTime"] = prev["lastTransitionTime"] if prev and prev.get("status") == c["status"] else now
             return c
 
-        conds = [cond(core.COND_INITIALIZED, init_done, "ContainersNotInitialized"),
-                 cond(core.COND_READY, ready, "ContainersNotReady"),
-                 cond(core.COND_CONTAINERS_READY, ready, "ContainersNotReady"),
-                 cond(core.COND_POD_SCHEDULED, True)]
+        # status_manager.go SetPodStatus: Initialized and Ready from generate.go
+        ready_c = generate_pod_ready_condition(spec, statuses, phase)
+        conds = [cond(generate_pod_initialized_condition(spec, init_statuses, phase)),
+                 cond(ready_c),
+                 cond({**ready_c, "type": core.COND_CONTAINERS_READY}),
+                 cond({"type": core.COND_POD_SCHEDULED, "status": "True"})]
         status = {"phase": phase, "conditions": conds, "hostIP": self.address, "podIP": st.ip,
                   "startTime": st.start_time, "containerStatuses": statuses,
                   "qosClass": (pod.get("status") or {}).get("qosClass", "BestEffort")}
@@ -1704,7 +1691,7 @@ class Kubelet:
             status["initContainerStatuses"] = init_statuses
         if phase in (core.POD_SUCCEEDED, core.POD_FAILED):
             st.terminated = True
-        return status
+        return normalize_status(pod, status)
 
     async def _report(self, st: PodState):
         status = self._compute_status(st)
@@ -1845,6 +1832,84 @@ def _key(pod):
 
 def _ts(t):
     return now_rfc3339(t) if t else None
+
+
+def containers_to_evict(containers, policy, now, is_deleted, is_terminated, evict_terminated=False,
+                        all_sources_ready=True):
+    """`containerGC.evictContainers` (pkg/kubelet/kuberuntime/kuberuntime_gc.go) as a pure
+    selection. `containers`: (id, pod uid, container name, createdAt, state). Non-running
+    containers created at least `min_age` ago form evict units per (pod, container), newest
+    first. Units of deleted pods (and of terminated ones with `evict_terminated`) go entirely;
+    then each unit keeps `max_per_pod_container` (if >= 0); then, over `max_containers` (if >=
+    0), every unit is cut to max(1, max_containers // units) and, still over, the oldest
+    containers across units go. Returns the ids to remove, in removal order."""
+    min_age = float(policy.get("min_age", 0.0))
+    per = int(policy.get("max_per_pod_container", 1))
+    total = int(policy.get("max_containers", -1))
+    units: dict = {}
+    for cid, uid, name, created, state in containers:
+        if state == RUNNING or created > now - min_age:
+            continue
+        units.setdefault((uid, name) if uid else ("", cid), []).append((created, cid))
+    for lst in units.values():
+        lst.sort(key=lambda e: e[0], reverse=True)
+    out = []
+
+    def remove_oldest(lst, n):
+        if n <= 0:
+            return lst
+        keep = len(lst) - n
+        out.extend(cid for _, cid in reversed(lst[keep:]))
+        return lst[:keep]
+
+    if all_sources_ready:
+        for key in list(units):
+            uid = key[0]
+            if is_deleted(uid) or (evict_terminated and is_terminated(uid)):
+                lst = units.pop(key)
+                remove_oldest(lst, len(lst))
+    if per >= 0:
+        for key in units:
+            units[key] = remove_oldest(units[key], len(units[key]) - per)
+    n = sum(len(v) for v in units.values())
+    if total >= 0 and n > total:
+        each = max(1, total // len(units)) if units else 1
+        for key in units:
+            units[key] = remove_oldest(units[key], len(units[key]) - each)
+        flat = sorted((e for v in units.values() for e in v), key=lambda e: e[0], reverse=True)
+        remove_oldest(flat, len(flat) - total)
+    return out
+
+
+def expand_container_command_and_args(container, envs):
+    """`kubecontainer.ExpandContainerCommandAndArgs` (helpers.go:130): every command and args
+    entry through `expand` with the container's resolved environment (`EnvVarsToMap`: a later
+    variable of the same name wins). Returns (command, args), each None when the container has
+    none."""
+    m = {}
+    for e in envs:
+        m[e["name"]] = str(e.get("value", ""))
+    cmd = [expand(str(x), m) for x in container.get("command") or ()] or None
+    args = [expand(str(x), m) for x in container.get("args") or ()] or None
+    return cmd, args
+
+
+def should_container_be_restarted(policy, status) -> bool:
+    """`kubecontainer.ShouldContainerBeRestarted` (pkg/kubelet/container/helpers.go:58) over the
+    latest instance's status (an object with `.state` / `.exit_code`, or None): never started ->
+    start; running -> no; unknown or created-but-not-started -> always; dead -> by restartPolicy
+    (Never: no, OnFailure: only a non-zero exit, Always: yes)."""
+    if status is None:
+        return True
+    if status.state == RUNNING:
+        return False
+    if status.state in (UNKNOWN, CREATED):
+        return True
+    if policy == "Never":
+        return False
+    if policy == "OnFailure" and status.exit_code == 0:
+        return False
+    return True
 
 
 def get_phase(spec, statuses, init_statuses=()):

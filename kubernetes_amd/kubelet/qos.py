@@ -3,7 +3,7 @@
   * `pod_qos(pod)`          — `qos.GetPodQOS` (Guaranteed / Burstable / BestEffort), the same rule
                               the API server uses to fill `status.qosClass`;
   * `oom_score_adj(...)`    — `qos.GetContainerOOMScoreAdjust` (`pkg/kubelet/qos/policy.go`):
-                              Guaranteed and critical pods -998, BestEffort 1000, Burstable
+                              Guaranteed -998, BestEffort 1000, Burstable
                               `1000 - 1000*memoryRequest/memoryCapacity` clamped to [2, 999] so a
                               Burstable container is never killed after a Guaranteed one and
                               always after BestEffort; the pause container -998;
@@ -42,15 +42,14 @@ def is_critical_pod(pod) -> bool:
 
 
 def _mem_request(container) -> int:
+    """`Requests.Memory().Value()`: the (defaulted) request only, 0 when unset."""
     r = ((container.get("resources") or {}).get("requests") or {}).get("memory")
-    if r is None:
-        r = ((container.get("resources") or {}).get("limits") or {}).get("memory")
     return parse_quantity(str(r)).value if r is not None else 0
 
 
 def oom_score_adj(pod, container, memory_capacity_bytes: int) -> int:
-    if is_critical_pod(pod):
-        return GUARANTEED_OOM_SCORE_ADJ
+    """`GetContainerOOMScoreAdjust` (pkg/kubelet/qos/policy.go:43): by QoS class only, so a
+    critical pod's containers score like any other pod of their class."""
     q = pod_qos(pod)
     if q == GUARANTEED:
         return GUARANTEED_OOM_SCORE_ADJ
@@ -62,4 +61,4 @@ def oom_score_adj(pod, container, memory_capacity_bytes: int) -> int:
     floor = 1000 + GUARANTEED_OOM_SCORE_ADJ      # 2: a Guaranteed pod at 100% memory scores ~2 too
     if adj < floor:
         return floor
-    return BESTEFFORT_OOM_SCORE_ADJ - 1 if adj >= BESTEFFORT_OOM_SCORE_ADJ else adj
+    return BESTEFFORT_OOM_SCORE_ADJ - 1 if adj == BESTEFFORT_OOM_SCORE_ADJ else adj

@@ -43,7 +43,7 @@ def test_qos_classes_and_oom_score_bands():
     tiny = pod("tiny", cpu_req="1m", mem_req="1")
     assert qos.oom_score_adj(tiny, c(tiny), 16 * GI) == 999                   # never as high as BestEffort
     crit = pod("dp", ns="kube-system", ann={qos.CRITICAL_POD_ANNOTATION: ""})
-    assert qos.is_critical_pod(crit) and qos.oom_score_adj(crit, c(crit), 16 * GI) == -998
+    assert qos.is_critical_pod(crit) and qos.oom_score_adj(crit, c(crit), 16 * GI) == 1000   # by class only
     assert not qos.is_critical_pod(pod("x", ann={qos.CRITICAL_POD_ANNOTATION: ""}))   # only in kube-system
     assert qos.is_critical_pod(pod("p", prio=2000001000))
 
