@@ -640,12 +640,22 @@ class Kubelet:
                 return
             except APIStatusError as e:
                 if e.code == 409:
+                    # tryRegisterWithAPIServer: the node was registered before; reconcile the
+                    # default labels and the controller-managed attach-detach annotation (plus
+                    # the device plugins' labels, which describe this node's hardware)
                     cur = await self.client.get("nodes", self.node_name)
-                    cur["metadata"]["labels"] = {**(cur["metadata"].get("labels") or {}), **node["metadata"]["labels"]}
-                    cur["metadata"]["annotations"] = {**(cur["metadata"].get("annotations") or {}),
-                                                      **node["metadata"]["annotations"]}
+                    md = cur["metadata"]
+                    md["labels"] = dict(md.get("labels") or {})
+                    md["annotations"] = dict(md.get("annotations") or {})
+                    changed = reconcile_cmad_annotation(node, cur)
+                    changed = update_default_labels(node, cur) or changed
+                    for k, v in self.plugin_labels.items():
+                        if md["labels"].get(k) != v:
+                            md["labels"][k] = v
+                            changed = True
+                    if changed:
+                        cur = await self.client.update("nodes", cur)
                     cur["status"] = node["status"]
-                    await self.client.update("nodes", cur)
                     await self.client.update_status("nodes", cur)
                     self.node_uid = cur["metadata"]["uid"]
                     return
@@ -1832,6 +1842,43 @@ def _key(pod):
 
 def _ts(t):
     return now_rfc3339(t) if t else None
+
+
+DEFAULT_NODE_LABELS = ("kubernetes.io/hostname", "failure-domain.beta.kubernetes.io/zone",
+                       "failure-domain.beta.kubernetes.io/region", "beta.kubernetes.io/instance-type",
+                       "beta.kubernetes.io/os", "beta.kubernetes.io/arch")
+
+
+def update_default_labels(initial, existing) -> bool:
+    """`Kubelet.updateDefaultLabels` (kubelet_node_status.go:159): each default label the kubelet
+    has an opinion on is copied onto the existing node (an empty value deletes it); other labels
+    stay. Returns whether the existing node changed."""
+    want = (initial.get("metadata") or {}).get("labels") or {}
+    have = existing["metadata"].setdefault("labels", {})
+    changed = False
+    for k in DEFAULT_NODE_LABELS:
+        if k not in want:
+            continue
+        if have.get(k, "") != want[k]:
+            have[k] = want[k]
+            changed = True
+        if have.get(k, "") == "":
+            have.pop(k, None)
+    return changed
+
+
+def reconcile_cmad_annotation(node, existing) -> bool:
+    """`reconcileCMADAnnotationWithExistingNode`: the controller-managed attach-detach annotation
+    of the existing node follows the one just built (removed when the kubelet does not set it)."""
+    new = (node.get("metadata") or {}).get("annotations") or {}
+    have = existing["metadata"].setdefault("annotations", {})
+    if new.get(CONTROLLER_MANAGED_ATTACH, "") == have.get(CONTROLLER_MANAGED_ATTACH, ""):
+        return False
+    if CONTROLLER_MANAGED_ATTACH in new:
+        have[CONTROLLER_MANAGED_ATTACH] = new[CONTROLLER_MANAGED_ATTACH]
+    else:
+        have.pop(CONTROLLER_MANAGED_ATTACH, None)
+    return True
 
 
 def containers_to_evict(containers, policy, now, is_deleted, is_terminated, evict_terminated=False,
