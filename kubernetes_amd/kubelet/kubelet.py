@@ -39,6 +39,7 @@ from ..utils.metrics import MICRO_BUCKETS, Registry
 from .devicemanager.manager import AdmitError, ManagerStub
 from .podstatus import generate_pod_initialized_condition, generate_pod_ready_condition, normalize_status
 from .prober import ProbeManager
+from .runtimestate import NETWORK_READY, RUNTIME_READY, RuntimeState, ready_condition, update_runtime_up
 from .runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, RunContainerOptions
 from .qos import oom_score_adj
 from .volumes import VolumeError, VolumeManager
@@ -46,6 +47,12 @@ from ..utils.tasks import spawn
 
 log = logging.getLogger("kubelet")
 CONTROLLER_MANAGED_ATTACH = "volumes.kubernetes.io/controller-managed-attach-detach"
+# setNode*Condition -> recordNodeStatusEvent reasons
+_NODE_STATUS_EVENTS = {("Ready", "True"): "NodeReady", ("Ready", "False"): "NodeNotReady",
+                       ("MemoryPressure", "True"): "NodeHasInsufficientMemory",
+                       ("MemoryPressure", "False"): "NodeHasSufficientMemory",
+                       ("DiskPressure", "True"): "NodeHasDiskPressure", ("DiskPressure", "False"): "NodeHasNoDiskPressure",
+                       ("OutOfDisk", "True"): "NodeOutOfDisk", ("OutOfDisk", "False"): "NodeHasSufficientDisk"}
 
 _ip_counter = itertools.count(2)
 
@@ -289,6 +296,7 @@ class Kubelet:
         self.image_service = image_service
         self._node_images: list = []
         self._cond_transitions: dict = {}      # condition type -> (status, lastTransitionTime)
+        self.runtime_state = RuntimeState()     # runtime.go: NodeReady's runtime/network errors
         self.images = ImageManager(image_service, self.recorder, backoff_initial=image_backoff,
                                    secret_getter=lambda ns, name: self.client.get("secrets", name, ns),
                                    serialize=serialize_image_pulls, qps=registry_qps, burst=registry_burst)
@@ -336,6 +344,7 @@ class Kubelet:
         if self.service_env:
             self.svc_informer = Informer(self.client, "services")
             self.svc_informer.start()
+        await self.update_runtime_up()
         if self.register:
             await self._register_node()
         if self.pod_checkpoints is not None:
@@ -357,6 +366,7 @@ class Kubelet:
         self.informer.add_handler(self._on_add, self._on_update, self._on_delete)
         self.informer.start()
         self._tasks.append(asyncio.ensure_future(self._node_status_loop()))
+        self._tasks.append(asyncio.ensure_future(self._runtime_up_loop()))
         if self.sync_frequency and self.sync_frequency > 0:
             self._tasks.append(asyncio.ensure_future(self._volume_sync_loop()))
         await self.informer.wait_synced(60)
@@ -511,11 +521,8 @@ class Kubelet:
         now = now_rfc3339()
         mem_p = self.eviction is not None and self.eviction.has("MemoryPressure")
         disk_p = self.eviction is not None and self.eviction.has("DiskPressure")
-        net_err = self.network.status()
         cond = self._condition
-        ready = (cond("Ready", "True", "KubeletReady", "kubelet is posting ready status", now) if not net_err else
-                 cond("Ready", "False", "KubeletNotReady",
-                      f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady message:{net_err}", now))
+        ready = cond("Ready", *ready_condition(self._ready_errors()), now)
         alloc = self._allocatable(capacity)
         self.volumes.allocatable = alloc        # downward API: a missing limit reads as allocatable
         self.volumes.host_ip = self.node_ip or self.address
@@ -559,6 +566,12 @@ class Kubelet:
         prev = self._cond_transitions.get(ctype)
         transition = prev[1] if prev is not None and prev[0] == status else now
         self._cond_transitions[ctype] = (status, transition)
+        if prev is None or prev[0] != status:
+            ev = _NODE_STATUS_EVENTS.get((ctype, status))
+            # recordNodeStatusEvent: "Node <name> status is now: <event>" (Ready only on a change)
+            if ev and (ctype != "Ready" or prev is not None):
+                node_ref = {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}}
+                self.recorder.event(node_ref, "Normal", ev, f"Node {self.node_name} status is now: {ev}")
         return {"type": ctype, "status": status, "reason": reason, "message": message,
                 "lastHeartbeatTime": now, "lastTransitionTime": transition}
 
@@ -751,6 +764,45 @@ class Kubelet:
                 log.warning("node status update failed: %s", e)
         except (ConnectionError, OSError) as e:
             log.warning("node status update failed: %s", e)
+
+    def _ready_errors(self):
+        """runtimeErrors() + networkErrors(); the network plugin lives in the kubelet here, so its
+        status stands in for the runtime's NetworkReady when the runtime reports none."""
+        rs = self.runtime_state
+        errs = rs.runtime_errors() + rs.network_errors()
+        if not rs.network_errors():
+            net_err = self.network.status()
+            if net_err:
+                errs.append(f"runtime network not ready: NetworkReady=false reason:NetworkPluginNotReady "
+                            f"message:{net_err}")
+        return errs
+
+    async def update_runtime_up(self):
+        """`Kubelet.updateRuntimeUp`: the runtime's Status() conditions (an in-process runtime
+        without one is up whenever the kubelet runs)."""
+        fn = getattr(self.runtime, "status", None)
+        status = err = None
+        if fn is None:
+            status = {RUNTIME_READY: (True, "", ""), NETWORK_READY: (True, "", "")}
+        else:
+            try:
+                raw = await fn()
+                status = None if raw is None else {
+                    k: (v if isinstance(v, tuple) else (bool(v), "", "")) for k, v in raw.items()}
+            except Exception as e:  # noqa: BLE001 - a failed sanity check only goes stale
+                err = e
+                log.warning("container runtime sanity check failed: %s", e)
+        before = ready_condition(self._ready_errors())[0]
+        update_runtime_up(self.runtime_state, status, error=err)
+        if ready_condition(self._ready_errors())[0] != before:
+            self._status_dirty.set()
+
+    async def _runtime_up_loop(self):
+        while not self._stopped:
+            await asyncio.sleep(5.0)
+            await self.update_runtime_up()
+            if self.runtime_state.last_sync + self.runtime_state.threshold <= time.time() + 5.0:
+                self._status_dirty.set()        # about to go stale: report it on time
 
     async def _node_status_loop(self):
         # exits on the _stopped flag, not only on cancellation: on Python 3.10 asyncio.wait_for
