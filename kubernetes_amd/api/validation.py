@@ -172,6 +172,69 @@ _PULL = ("Always", "IfNotPresent", "Never")
 
 
 _DNS_POLICIES = ("ClusterFirstWithHostNet", "ClusterFirst", "Default", "None")
+MAX_DNS_NAMESERVERS, MAX_DNS_SEARCH_PATHS, MAX_DNS_SEARCH_LIST_CHARS = 3, 6, 256
+
+
+def _inv(path, value, msg):
+    v = value if isinstance(value, str) else str(value)
+    return invalid(path, f'"{v}": {msg}' if isinstance(value, str) else f"{v}: {msg}")
+
+
+def validate_dns_policy(dp, path):
+    """validateDNSPolicy: None only with the CustomPodDNS gate."""
+    from ..utils.features import DefaultFeatureGate
+    if dp in ("ClusterFirstWithHostNet", "ClusterFirst", "Default"):
+        return []
+    if dp == "None":
+        if not DefaultFeatureGate("CustomPodDNS"):
+            return [_inv(path, dp, "DNSPolicy: can not use 'None', custom pod DNS is disabled by feature gate")]
+        return []
+    if dp == "":
+        return [required(path)]
+    return [not_supported(path, dp)]
+
+
+def validate_pod_dns_config(cfg, dp, path):
+    """validatePodDNSConfig: dnsPolicy None needs a dnsConfig with a nameserver; a dnsConfig
+    needs the CustomPodDNS gate and fits libc's resolver limits."""
+    import ipaddress
+
+    from ..utils.features import DefaultFeatureGate
+    errs = []
+    gate = DefaultFeatureGate("CustomPodDNS")
+    if gate and dp == "None":
+        if cfg is None:
+            return [required(path, "must provide `dnsConfig` when `dnsPolicy` is None")]
+        if not cfg.get("nameservers"):
+            return [required(f"{path}.nameservers", "must provide at least one DNS nameserver when `dnsPolicy` is None")]
+    if cfg is None:
+        return errs
+    if not gate:
+        return [FieldError("Forbidden", path, "DNSConfig: custom pod DNS is disabled by feature gate")]
+    ns = cfg.get("nameservers") or []
+    if len(ns) > MAX_DNS_NAMESERVERS:
+        errs.append(_inv(f"{path}.nameservers", ns, f"must not have more than {MAX_DNS_NAMESERVERS} nameservers"))
+    for i, x in enumerate(ns):
+        try:
+            ipaddress.ip_address(str(x))
+        except ValueError:
+            errs.append(_inv(f"{path}.nameservers[{i}]", x, "must be valid IP address"))
+    se = cfg.get("searches") or []
+    if len(se) > MAX_DNS_SEARCH_PATHS:
+        errs.append(_inv(f"{path}.searches", se, f"must not have more than {MAX_DNS_SEARCH_PATHS} search paths"))
+    if len(" ".join(se)) > MAX_DNS_SEARCH_LIST_CHARS:
+        errs.append(_inv(f"{path}.searches", se,
+                         "must not have more than 256 characters (including spaces) in the search list"))
+    for i, x in enumerate(se):
+        if not is_dns1123_subdomain(str(x)):
+            errs.append(_inv(f"{path}.searches[{i}]", x, "a DNS-1123 subdomain must consist of lower case "
+                                                           "alphanumeric characters, '-' or '.'"))
+    for i, o in enumerate(cfg.get("options") or ()):
+        if not (o or {}).get("name"):
+            errs.append(required(f"{path}.options[{i}]", "must not be empty"))
+    return errs
+
+
 _PROTOCOLS = ("TCP", "UDP")
 _TERM_MSG = ("File", "FallbackToLogsOnError")
 _TOL_OPS = ("Exists", "Equal")
@@ -385,8 +448,9 @@ def validate_pod_spec(spec, path="spec"):
     if rp and rp not in _RESTART:
         errs.append(not_supported(f"{path}.restartPolicy", rp))
     dp = spec.get("dnsPolicy")
-    if dp and dp not in _DNS_POLICIES:
-        errs.append(not_supported(f"{path}.dnsPolicy", dp))
+    if dp is not None:
+        errs += validate_dns_policy(dp, f"{path}.dnsPolicy")
+    errs += validate_pod_dns_config(spec.get("dnsConfig"), dp, f"{path}.dnsConfig")
     names_ref, er_errs = validate_extended_resources(spec.get("extendedResources"), f"{path}.extendedResources")
     errs += er_errs
     errs += validate_containers_extended_resources(spec.get("containers"), names_ref, f"{path}.containers")

@@ -344,6 +344,7 @@ class Kubelet:
         if self.service_env:
             self.svc_informer = Informer(self.client, "services")
             self.svc_informer.start()
+        self._wire_dns()
         await self.update_runtime_up()
         if self.register:
             await self._register_node()
@@ -686,6 +687,7 @@ class Kubelet:
             lc = self._local_config
             self.capacity["pods"], self.status_freq = lc["pods"], lc["status_freq"]
             self.eviction, self.container_gc, self.dns = lc["eviction"], lc["container_gc"], lc["dns"]
+            self._wire_dns()
             if self.image_gc is not None and lc["image_gc"]:
                 self.image_gc.high, self.image_gc.low = lc["image_gc"]
             self._status_dirty.set()
@@ -697,6 +699,7 @@ class Kubelet:
         self.container_gc = kw["container_gc"]
         if "dns" in kw:
             self.dns = kw["dns"]
+            self._wire_dns()
         if self.image_gc is not None:
             self.image_gc.high = int(cfg["imageGCHighThresholdPercent"])
             self.image_gc.low = int(cfg["imageGCLowThresholdPercent"])
@@ -764,6 +767,22 @@ class Kubelet:
                 log.warning("node status update failed: %s", e)
         except (ConnectionError, OSError) as e:
             log.warning("node status update failed: %s", e)
+
+    def _wire_dns(self):
+        """The DNS configurer reports on this node (`dns.NewConfigurer(recorder, nodeRef, nodeIP,
+        ...)`); a configurer shared between kubelets is copied first. A configured resolv.conf is
+        checked against the search-line limits once (`CheckLimitsForResolvConf`)."""
+        if self.dns is None or getattr(self.dns, "_owner", None) is self:
+            return
+        import copy
+        self.dns = copy.copy(self.dns)
+        self.dns._owner = self
+        node_ref = {"kind": "Node", "metadata": {"name": self.node_name, "uid": self.node_name}}
+        self.dns.node_ref = node_ref
+        self.dns.node_ip = self.node_ip or self.address
+        self.dns.recorder = lambda obj, typ, reason, msg: self.recorder.event(obj or node_ref, typ, reason, msg)
+        if self.dns.resolv_conf:
+            self.dns.check_limits_for_resolv_conf()
 
     def _ready_errors(self):
         """runtimeErrors() + networkErrors(); the network plugin lives in the kubelet here, so its

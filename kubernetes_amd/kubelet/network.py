@@ -330,68 +330,180 @@ def new_plugin(name, data_dir, cni_conf_dir="/etc/cni/net.d", cni_bin_dir="/opt/
 
 
 # ------------------------------------------------------------------------------------ DNS
-def parse_resolv_conf(path):
+def parse_resolv_conf_text(data: str):
+    """`parseResolvConf` (pkg/kubelet/network/dns/dns.go): nameserver lines accumulate; the last
+    search line and the last options line win; lines starting with '#' are comments."""
     ns, search, opts = [], [], []
-    try:
-        with open(path) as f:
-            for line in f:
-                parts = line.split("#", 1)[0].split()
-                if not parts:
-                    continue
-                if parts[0] == "nameserver" and len(parts) > 1:
-                    ns.append(parts[1])
-                elif parts[0] == "search":
-                    search = parts[1:]
-                elif parts[0] == "options":
-                    opts += parts[1:]
-    except OSError:
-        pass
+    for line in data.split("\n"):
+        t = line.strip()
+        if t.startswith("#"):
+            continue
+        f = t.split()
+        if not f:
+            continue
+        if f[0] == "nameserver" and len(f) >= 2:
+            ns.append(f[1])
+        if f[0] == "search":
+            search = f[1:]
+        if f[0] == "options":
+            opts = f[1:]
     return ns, search, opts
 
 
-def _fit_search(search):
-    out, n = [], 0
-    for s in search:
-        if s in out:
-            continue
-        if len(out) >= MAX_SEARCH or n + len(s) + (1 if out else 0) > MAX_SEARCH_CHARS:
-            break
-        out.append(s)
-        n += len(s) + (1 if len(out) > 1 else 0)
+def parse_resolv_conf(path):
+    try:
+        with open(path) as f:
+            return parse_resolv_conf_text(f.read())
+    except OSError:
+        return [], [], []
+
+
+def omit_duplicates(items):
+    seen, out = set(), []
+    for x in items:
+        if x not in seen:
+            seen.add(x)
+            out.append(x)
     return out
 
 
+def merge_dns_options(existing, options):
+    """`mergeDNSOptions`: pod dnsConfig options override same-named existing ones."""
+    m = {}
+    for op in existing:
+        k, sep, v = op.partition(":")
+        m[k] = v if sep else ""
+    for o in options or ():
+        m[o.get("name")] = "" if o.get("value") is None else str(o["value"])
+    return [k + (":" + v if v else "") for k, v in m.items()]
+
+
+POD_DNS_CLUSTER, POD_DNS_HOST, POD_DNS_NONE = "cluster", "host", "none"
+
+
+def get_pod_dns_type(pod):
+    """`getPodDNSType`: returns (type, error); None needs the CustomPodDNS gate; ClusterFirst on
+    the host network falls back to the host's resolver."""
+    from ..utils.features import DefaultFeatureGate
+    spec = pod.get("spec") or {}
+    policy = spec.get("dnsPolicy") or "ClusterFirst"        # the API default for objects not defaulted
+    if policy == "None":
+        if DefaultFeatureGate("CustomPodDNS"):
+            return POD_DNS_NONE, None
+        return POD_DNS_CLUSTER, f"invalid DNSPolicy={policy}: custom pod DNS is disabled"
+    if policy == "ClusterFirstWithHostNet":
+        return POD_DNS_CLUSTER, None
+    if policy == "ClusterFirst":
+        return (POD_DNS_HOST if spec.get("hostNetwork") else POD_DNS_CLUSTER), None
+    if policy == "Default":
+        return POD_DNS_HOST, None
+    return POD_DNS_CLUSTER, f"invalid DNSPolicy={policy}"
+
+
 class DNSConfigurer:
-    def __init__(self, cluster_dns=(), cluster_domain="cluster.local", resolv_conf="/etc/resolv.conf"):
+    """`pkg/kubelet/network/dns/dns.go` Configurer. `recorder(obj, type, reason, message)` (set
+    by the kubelet) receives the DNSConfigForming / MissingClusterDNS / CheckLimitsForResolvConf
+    warnings; `node_ref` is the node's object reference."""
+
+    def __init__(self, cluster_dns=(), cluster_domain="cluster.local", resolv_conf="/etc/resolv.conf", node_ip=None,
+                 recorder=None, node_ref=None):
         self.cluster_dns = [x for x in cluster_dns if x]
         self.domain = cluster_domain
         self.resolv_conf = resolv_conf
+        self.node_ip = node_ip
+        self.recorder = recorder
+        self.node_ref = node_ref
+
+    def _event(self, obj, reason, msg):
+        if self.recorder is not None:
+            self.recorder(obj, "Warning", reason, msg)
+        else:
+            log.warning("%s: %s", reason, msg)
+
+    def form_dns_search_fits_limits(self, search, pod):
+        exceeded = False
+        if len(search) > MAX_SEARCH:
+            search = search[:MAX_SEARCH]
+            exceeded = True
+        line_len = len(" ".join(search))
+        if line_len > MAX_SEARCH_CHARS:
+            cut_n = cut_len = 0
+            for d in reversed(search):
+                cut_len += len(d) + 1
+                cut_n += 1
+                if line_len - cut_len <= MAX_SEARCH_CHARS:
+                    break
+            search = search[:len(search) - cut_n]
+            exceeded = True
+        if exceeded:
+            self._event(pod, "DNSConfigForming", "Search Line limits were exceeded, some search paths have been omitted, "
+                                                 f"the applied search line is: {' '.join(search)}")
+        return search
+
+    def form_dns_nameservers_fits_limits(self, ns, pod):
+        if len(ns) > MAX_NS:
+            ns = ns[:MAX_NS]
+            self._event(pod, "DNSConfigForming", "Nameserver limits were exceeded, some nameservers have been omitted, "
+                                                 f"the applied nameserver line is: {' '.join(ns)}")
+        return ns
+
+    def _cluster_searches(self, host_search, pod):
+        if not self.domain:
+            return list(host_search)
+        ns = pod["metadata"].get("namespace", "")
+        return omit_duplicates([f"{ns}.svc.{self.domain}", f"svc.{self.domain}", self.domain] + list(host_search))
+
+    def check_limits_for_resolv_conf(self):
+        """`CheckLimitsForResolvConf`: warn (on the node) when the host's search line leaves no
+        room for the cluster domains."""
+        try:
+            with open(self.resolv_conf) as f:
+                _, search, _ = parse_resolv_conf_text(f.read())
+        except OSError as e:
+            self._event(self.node_ref, "CheckLimitsForResolvConf", str(e))
+            return
+        limit = MAX_SEARCH - (3 if self.domain else 0)
+        if len(search) > limit:
+            self._event(self.node_ref, "CheckLimitsForResolvConf",
+                        f"Resolv.conf file '{self.resolv_conf}' contains search line consisting of more than {limit} domains!")
+        elif len(" ".join(search)) > MAX_SEARCH_CHARS:
+            self._event(self.node_ref, "CheckLimitsForResolvConf",
+                        f"Resolv.conf file '{self.resolv_conf}' contains search line which length is more than allowed "
+                        f"{MAX_SEARCH_CHARS} chars!")
 
     def pod_dns(self, pod):
+        """`GetPodDNS`: (nameservers, searches, options)."""
+        from ..utils.features import DefaultFeatureGate
         spec = pod.get("spec") or {}
-        policy = spec.get("dnsPolicy") or "ClusterFirst"
-        host_ns, host_search, host_opts = parse_resolv_conf(self.resolv_conf) if self.resolv_conf else ([], [], [])
-        if policy == "ClusterFirst" and spec.get("hostNetwork"):
-            policy = "Default"
-        if policy == "ClusterFirstWithHostNet":
-            policy = "ClusterFirst"
-        if policy == "None":
-            ns, search, opts = [], [], []
-        elif policy == "Default" or not self.cluster_dns:
-            ns, search, opts = list(host_ns), list(host_search), list(host_opts)
+        if self.resolv_conf:
+            ns, search, opts = parse_resolv_conf(self.resolv_conf)
         else:
-            pns = pod["metadata"].get("namespace", "default")
-            ns = list(self.cluster_dns)
-            search = [f"{pns}.svc.{self.domain}", f"svc.{self.domain}", self.domain] + host_search
-            opts = ["ndots:5"]
-        cfg = spec.get("dnsConfig") or {}
-        ns += [x for x in cfg.get("nameservers") or () if x not in ns]
-        search += [x for x in cfg.get("searches") or () if x not in search]
-        for o in cfg.get("options") or ():
-            name = o.get("name")
-            opts = [x for x in opts if x.split(":")[0] != name]
-            opts.append(f"{name}:{o['value']}" if o.get("value") is not None else name)
-        return ns[:MAX_NS], _fit_search(search), opts
+            ns, search, opts = [], [], []
+        typ, err = get_pod_dns_type(pod)
+        if err:
+            log.warning("failed to get DNS type for pod %s: %s; falling back to ClusterFirst", pod["metadata"].get("name"),
+                        err)
+        if typ == POD_DNS_NONE:
+            ns, search, opts = [], [], []
+        elif typ == POD_DNS_CLUSTER and self.cluster_dns:
+            ns, search, opts = list(self.cluster_dns), self._cluster_searches(search, pod), ["ndots:5"]
+        else:
+            if typ == POD_DNS_CLUSTER:
+                msg = ('kubelet does not have ClusterDNS IP configured and cannot create Pod using "ClusterFirst" '
+                       'policy. Falling back to "Default" policy.')
+                self._event(self.node_ref, "MissingClusterDNS", msg)
+                md = pod["metadata"]
+                self._event(pod, "MissingClusterDNS", f'pod: "{md.get("name")}_{md.get("namespace", "")}'
+                                                      f'({md.get("uid", "")})". {msg}')
+            if not self.resolv_conf:
+                ns = ["::1"] if self.node_ip and ":" in str(self.node_ip) else ["127.0.0.1"]
+                search = ["."]
+        cfg = spec.get("dnsConfig")
+        if cfg is not None and DefaultFeatureGate("CustomPodDNS"):
+            ns = omit_duplicates(ns + list(cfg.get("nameservers") or ()))
+            search = omit_duplicates(search + list(cfg.get("searches") or ()))
+            opts = merge_dns_options(opts, cfg.get("options"))
+        return self.form_dns_nameservers_fits_limits(ns, pod), self.form_dns_search_fits_limits(search, pod), opts
 
     def resolv_text(self, pod):
         ns, search, opts = self.pod_dns(pod)

@@ -36,6 +36,7 @@ DEFAULTS = {
     # node must not evict the agent that advertises its GPUs.
     "ExperimentalCriticalPodAnnotation": FeatureSpec(True, ALPHA),
     "LocalStorageCapacityIsolation": FeatureSpec(False, ALPHA),   # emptyDir sizeLimit / ephemeral-storage limits
+    "CustomPodDNS": FeatureSpec(False, ALPHA),            # dnsPolicy None and spec.dnsConfig
 }
 
 

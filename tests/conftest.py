@@ -25,6 +25,15 @@ def run():
 _SESSION_START = [0.0]
 
 
+@pytest.fixture
+def feature_gate():
+    """The process-wide feature gate, restored after the test (`--feature-gates` in-process)."""
+    from kubernetes_amd.utils.features import DefaultFeatureGate
+    saved = dict(DefaultFeatureGate.enabled)
+    yield DefaultFeatureGate
+    DefaultFeatureGate.enabled = saved
+
+
 def pytest_sessionstart(session):
     import time
     _SESSION_START[0] = time.time()

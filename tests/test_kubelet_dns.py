@@ -1,0 +1,203 @@
+"""Pod DNS ported from `pkg/kubelet/network/dns/dns_test.go` (TestParseResolvConf,
+TestFormDNSSearchFitsLimits, TestFormDNSNameserversFitsLimits, TestMergeDNSOptions,
+TestGetPodDNSType, TestGetPodDNS, TestGetPodDNSCustom) plus the API validation of
+dnsPolicy None / dnsConfig behind the CustomPodDNS gate."""
+import pytest
+
+from kubernetes_amd.kubelet import network as net
+
+PARSE = [
+    ("", [], [], []), (" ", [], [], []), ("\n", [], [], []), ("\t\n\t", [], [], []),
+    ("#comment\n", [], [], []), (" #comment\n", [], [], []), ("#comment\n#comment", [], [], []),
+    ("#comment\nnameserver", [], [], []), ("#comment\nnameserver\nsearch", [], [], []),
+    ("nameserver 1.2.3.4", ["1.2.3.4"], [], []), (" nameserver 1.2.3.4", ["1.2.3.4"], [], []),
+    ("\tnameserver 1.2.3.4", ["1.2.3.4"], [], []), ("nameserver\t1.2.3.4", ["1.2.3.4"], [], []),
+    ("nameserver \t 1.2.3.4", ["1.2.3.4"], [], []),
+    ("nameserver 1.2.3.4\nnameserver 5.6.7.8", ["1.2.3.4", "5.6.7.8"], [], []),
+    ("nameserver 1.2.3.4 #comment", ["1.2.3.4"], [], []),
+    ("search foo", [], ["foo"], []), ("search foo bar", [], ["foo", "bar"], []),
+    ("search foo bar bat\n", [], ["foo", "bar", "bat"], []), ("search foo\nsearch bar", [], ["bar"], []),
+    ("nameserver 1.2.3.4\nsearch foo bar", ["1.2.3.4"], ["foo", "bar"], []),
+    ("nameserver 1.2.3.4\nsearch foo\nnameserver 5.6.7.8\nsearch bar", ["1.2.3.4", "5.6.7.8"], ["bar"], []),
+    ("#comment\nnameserver 1.2.3.4\n#comment\nsearch foo\ncomment", ["1.2.3.4"], ["foo"], []),
+    ("options ndots:5 attempts:2", [], [], ["ndots:5", "attempts:2"]),
+    ("options ndots:1\noptions ndots:5 attempts:3", [], [], ["ndots:5", "attempts:3"]),
+    ("nameserver 1.2.3.4\nsearch foo\nnameserver 5.6.7.8\nsearch bar\noptions ndots:5 attempts:4",
+     ["1.2.3.4", "5.6.7.8"], ["bar"], ["ndots:5", "attempts:4"]),
+]
+
+
+@pytest.mark.parametrize("data,ns,search,opts", PARSE)
+def test_parse_resolv_conf(data, ns, search, opts):
+    assert net.parse_resolv_conf_text(data) == (ns, search, opts)
+
+
+def configurer(cluster_dns=(), domain="TEST", resolv=""):
+    events = []
+    c = net.DNSConfigurer(list(cluster_dns), domain, resolv, recorder=lambda obj, t, r, m: events.append((t, r, m)),
+                          node_ref={"kind": "Node", "metadata": {"name": "testNode"}})
+    return c, events
+
+
+POD = {"metadata": {"name": "test_pod", "namespace": "testNS", "uid": ""}, "spec": {}}
+
+
+@pytest.mark.parametrize("names,want,event", [
+    (["testNS.svc.TEST", "svc.TEST", "TEST"], ["testNS.svc.TEST", "svc.TEST", "TEST"], None),
+    (["testNS.svc.TEST", "svc.TEST", "TEST", "AAA", "BBB"], ["testNS.svc.TEST", "svc.TEST", "TEST", "AAA", "BBB"], None),
+    (["testNS.svc.TEST", "svc.TEST", "TEST", "AAA", "B" * 256, "BBB"], ["testNS.svc.TEST", "svc.TEST", "TEST", "AAA"],
+     "Search Line limits were exceeded, some search paths have been omitted, the applied search line is: "
+     "testNS.svc.TEST svc.TEST TEST AAA"),
+    (["testNS.svc.TEST", "svc.TEST", "TEST", "AAA", "BBB", "CCC", "DDD"],
+     ["testNS.svc.TEST", "svc.TEST", "TEST", "AAA", "BBB", "CCC"],
+     "Search Line limits were exceeded, some search paths have been omitted, the applied search line is: "
+     "testNS.svc.TEST svc.TEST TEST AAA BBB CCC"),
+])
+def test_form_dns_search_fits_limits(names, want, event):
+    c, events = configurer()
+    assert c.form_dns_search_fits_limits(names, POD) == want
+    assert events == ([("Warning", "DNSConfigForming", event)] if event else [])
+
+
+@pytest.mark.parametrize("ns,want,event", [
+    (["127.0.0.1"], ["127.0.0.1"], False),
+    (["127.0.0.1", "10.0.0.10", "8.8.8.8"], ["127.0.0.1", "10.0.0.10", "8.8.8.8"], False),
+    (["127.0.0.1", "10.0.0.10", "8.8.8.8", "1.2.3.4"], ["127.0.0.1", "10.0.0.10", "8.8.8.8"], True),
+])
+def test_form_dns_nameservers_fits_limits(ns, want, event):
+    c, events = configurer()
+    assert c.form_dns_nameservers_fits_limits(ns, POD) == want
+    assert bool(events) == event
+
+
+@pytest.mark.parametrize("existing,options,want", [
+    (["ndots:5", "debug"], None, ["ndots:5", "debug"]),
+    (["ndots:5", "debug"], [{"name": "single-request"}, {"name": "attempts", "value": "3"}],
+     ["ndots:5", "debug", "single-request", "attempts:3"]),
+    (["ndots:5", "debug"], [{"name": "ndots", "value": "3"}, {"name": "debug"}, {"name": "single-request"},
+                            {"name": "attempts", "value": "3"}], ["ndots:3", "debug", "single-request", "attempts:3"]),
+])
+def test_merge_dns_options(existing, options, want):
+    assert sorted(net.merge_dns_options(existing, options)) == sorted(want)
+
+
+@pytest.mark.parametrize("gate,host_net,policy,want,err", [
+    (False, False, "ClusterFirst", net.POD_DNS_CLUSTER, False),
+    (False, True, "ClusterFirstWithHostNet", net.POD_DNS_CLUSTER, False),
+    (False, False, "ClusterFirstWithHostNet", net.POD_DNS_CLUSTER, False),
+    (False, False, "Default", net.POD_DNS_HOST, False),
+    (False, True, "Default", net.POD_DNS_HOST, False),
+    (False, True, "ClusterFirst", net.POD_DNS_HOST, False),
+    (True, False, "None", net.POD_DNS_NONE, False),
+    (False, False, "None", None, True),
+    (False, False, "invalidPolicy", None, True),
+])
+def test_get_pod_dns_type(feature_gate, gate, host_net, policy, want, err):
+    feature_gate.set(f"CustomPodDNS={str(gate).lower()}")
+    typ, e = net.get_pod_dns_type({"metadata": {}, "spec": {"dnsPolicy": policy, "hostNetwork": host_net}})
+    assert bool(e) == err
+    if not err:
+        assert typ == want
+
+
+def pods4():
+    pods = [{"metadata": {"name": f"pod{i}", "uid": str(10000 + i)}, "spec": {"hostNetwork": True}} for i in range(4)]
+    pods[0]["spec"]["dnsPolicy"] = "ClusterFirstWithHostNet"
+    pods[1]["spec"]["dnsPolicy"] = "ClusterFirst"
+    pods[2]["spec"]["dnsPolicy"] = "ClusterFirst"
+    pods[2]["spec"]["hostNetwork"] = False
+    pods[3]["spec"]["dnsPolicy"] = "Default"
+    return pods
+
+
+def test_get_pod_dns(tmp_path):
+    cluster_ns = "203.0.113.1"
+    c, _ = configurer([cluster_ns], "kubernetes.io", "")
+    out = [c.pod_dns(p) for p in pods4()]
+    assert out[0][0] == [cluster_ns] and out[0][1][0] == ".svc.kubernetes.io"
+    assert out[1][0] == ["127.0.0.1"] and out[1][1] == ["."]           # no resolv.conf: localhost, "."
+    assert out[2][0] == [cluster_ns] and out[2][1][0] == ".svc.kubernetes.io"
+    assert out[3][0] == ["127.0.0.1"] and out[3][1] == ["."]
+    rc = tmp_path / "resolv.conf"
+    rc.write_text("nameserver 192.0.2.53\nsearch a.example b.example c.example d.example\n")
+    c, _ = configurer([cluster_ns], "kubernetes.io", str(rc))
+    out = [c.pod_dns(p) for p in pods4()]
+    assert out[0][0] == [cluster_ns]
+    exp = min(len(out[1][1]) + 3, 6)
+    assert len(out[0][1]) == exp and out[0][1][0] == ".svc.kubernetes.io"
+    assert out[2][0] == [cluster_ns] and len(out[2][1]) == exp
+    assert out[1][0] == ["192.0.2.53"]
+
+
+def test_ipv6_node_without_resolv_conf_uses_ipv6_loopback():
+    c, _ = configurer([], "kubernetes.io", "")
+    c.node_ip = "fd00::1"
+    assert c.pod_dns({"metadata": {"name": "p"}, "spec": {"dnsPolicy": "Default"}})[:2] == (["::1"], ["."])
+
+
+def test_missing_cluster_dns_falls_back_with_events():
+    c, events = configurer([], "kubernetes.io", "")
+    ns, search, _ = c.pod_dns({"metadata": {"name": "p", "namespace": "d", "uid": "u"}, "spec": {"dnsPolicy": "ClusterFirst"}})
+    assert (ns, search) == (["127.0.0.1"], ["."])
+    assert [e[1] for e in events] == ["MissingClusterDNS", "MissingClusterDNS"]
+
+
+def test_get_pod_dns_custom(feature_gate):
+    cluster_ns = "203.0.113.1"
+    c, _ = configurer([cluster_ns], "kubernetes.io", "")
+    pod = {"metadata": {"name": "test_pod", "namespace": "testNS"}, "spec": {"dnsPolicy": "ClusterFirst"}}
+    cluster_first = c.pod_dns(pod)
+    pod["spec"]["dnsPolicy"] = "None"
+    # gate disabled: None falls back to ClusterFirst
+    feature_gate.set("CustomPodDNS=false")
+    assert c.pod_dns(pod) == cluster_first
+    feature_gate.set("CustomPodDNS=true")
+    assert c.pod_dns(pod) == ([], [], [])
+    pod["spec"]["dnsConfig"] = {"nameservers": ["10.0.0.10"], "searches": ["my.domain", "second.domain"],
+                                "options": [{"name": "ndots", "value": "3"}, {"name": "debug"}]}
+    ns, search, opts = c.pod_dns(pod)
+    assert ns == ["10.0.0.10"] and search == ["my.domain", "second.domain"] and sorted(opts) == ["debug", "ndots:3"]
+
+
+def test_check_limits_for_resolv_conf(tmp_path):
+    rc = tmp_path / "resolv.conf"
+    rc.write_text("search " + " ".join(f"d{i}.example" for i in range(4)) + "\n")
+    c, events = configurer([], "cluster.local", str(rc))
+    c.check_limits_for_resolv_conf()
+    assert events and "more than 3 domains" in events[0][2]
+    events.clear()
+    c, events = configurer([], "", str(rc))
+    c.check_limits_for_resolv_conf()
+    assert events == []
+    c, events = configurer([], "", str(tmp_path / "missing"))
+    c.check_limits_for_resolv_conf()
+    assert events[0][1] == "CheckLimitsForResolvConf"
+
+
+def _spec(**kw):
+    return {"containers": [{"name": "c", "image": "busybox"}], "restartPolicy": "Always", **kw}
+
+
+@pytest.mark.parametrize("gate,spec,want", [
+    (False, _spec(dnsPolicy="None", dnsConfig={"nameservers": ["1.1.1.1"]}), ["can not use 'None'", "Forbidden"]),
+    (False, _spec(dnsPolicy="ClusterFirst"), []),
+    (True, _spec(dnsPolicy="None"), ["must provide `dnsConfig`"]),
+    (True, _spec(dnsPolicy="None", dnsConfig={}), ["must provide at least one DNS nameserver"]),
+    (True, _spec(dnsPolicy="None", dnsConfig={"nameservers": ["1.1.1.1"]}), []),
+    (True, _spec(dnsPolicy="ClusterFirst", dnsConfig={"nameservers": ["1.1.1.1", "2.2.2.2", "3.3.3.3", "4.4.4.4"]}),
+     ["must not have more than 3 nameservers"]),
+    (True, _spec(dnsPolicy="ClusterFirst", dnsConfig={"nameservers": ["not-an-ip"]}), ["must be valid IP address"]),
+    (True, _spec(dnsPolicy="ClusterFirst", dnsConfig={"searches": [f"s{i}" for i in range(7)]}),
+     ["must not have more than 6 search paths"]),
+    (True, _spec(dnsPolicy="ClusterFirst", dnsConfig={"searches": ["Bad_Domain"]}), ["DNS-1123 subdomain"]),
+    (True, _spec(dnsPolicy="ClusterFirst", dnsConfig={"options": [{"value": "1"}]}), ["must not be empty"]),
+    (True, _spec(dnsPolicy="bogus"), ["Unsupported value"]),
+])
+def test_validate_pod_dns(feature_gate, gate, spec, want):
+    from kubernetes_amd.api.validation import validate_pod_spec
+    feature_gate.set(f"CustomPodDNS={str(gate).lower()}")
+    errs = [str(e) for e in validate_pod_spec(spec, "spec") if "dns" in str(e).lower()]
+    for w in want:
+        assert any(w in e for e in errs), (w, errs)
+    if not want:
+        assert errs == []

@@ -39,7 +39,7 @@ def test_host_local_ipam(tmp_path):
         again.allocate("other")
 
 
-def test_dns_and_hosts(tmp_path):
+def test_dns_and_hosts(tmp_path, feature_gate):
     rc = tmp_path / "resolv.conf"
     rc.write_text("nameserver 192.168.1.1\nsearch corp.example\noptions timeout:2\n")
     d = net.DNSConfigurer(["10.96.0.10"], "cluster.local", str(rc))
@@ -50,8 +50,9 @@ def test_dns_and_hosts(tmp_path):
     assert "nameserver 192.168.1.1" in d.resolv_text(pod(dnsPolicy="Default"))
     assert "nameserver 192.168.1.1" in d.resolv_text(pod(hostNetwork=True))           # ClusterFirst + hostNetwork
     assert "nameserver 10.96.0.10" in d.resolv_text(pod(hostNetwork=True, dnsPolicy="ClusterFirstWithHostNet"))
-    custom = d.resolv_text(pod(dnsPolicy="None", dnsConfig={"nameservers": ["1.1.1.1"], "searches": ["a.b"],
-                                                            "options": [{"name": "ndots", "value": "2"}, {"name": "edns0"}]}))
+    feature_gate.set("CustomPodDNS=true")
+    custom = d.resolv_text(pod(dnsPolicy="None", dnsConfig={
+        "nameservers": ["1.1.1.1"], "searches": ["a.b"], "options": [{"name": "ndots", "value": "2"}, {"name": "edns0"}]}))
     assert custom == "nameserver 1.1.1.1\nsearch a.b\noptions ndots:2 edns0\n"
     many = d.pod_dns(pod(dnsConfig={"nameservers": ["1.1.1.1", "2.2.2.2", "3.3.3.3"],
                                     "searches": [f"s{i}.example" for i in range(10)]}))

@@ -171,9 +171,10 @@ def store():
     s.stop()
 
 
-def test_rich_pod_survives_store_round_trip_and_restart(run, store):
+def test_rich_pod_survives_store_round_trip_and_restart(run, store, feature_gate):
     """Create through one worker, restart, read through another: nothing dropped. The store holds
     protobuf (no resourceVersion inside), and the C++ watch fan-out serves the same JSON."""
+    feature_gate.set("CustomPodDNS=true")          # the pod uses dnsPolicy None + dnsConfig
     async def main():
         s1 = APIServer(store=store)
         c1 = Client(f"http://127.0.0.1:{await s1.start()}")
