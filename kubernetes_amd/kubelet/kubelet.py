@@ -38,6 +38,7 @@ from ..utils.httpserver import HTTPServer, Response, StreamResponse
 from ..utils.metrics import MICRO_BUCKETS, Registry
 from .devicemanager.manager import AdmitError, ManagerStub
 from .podstatus import generate_pod_initialized_condition, generate_pod_ready_condition, normalize_status
+from .lifecycle import HandlerRunner
 from .prober import ProbeManager
 from .runtimestate import NETWORK_READY, RUNTIME_READY, RuntimeState, ready_condition, update_runtime_up
 from .runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, RunContainerOptions
@@ -1384,11 +1385,11 @@ class Kubelet:
             self._link_log(st.pod, c["name"], cid)
         post = ((c.get("lifecycle") or {}).get("postStart"))
         if post:
-            # `pkg/kubelet/lifecycle/handlers.go` RunHandler: a failed postStart kills the container
-            from .prober import run_probe
-            ok, msg = await run_probe(self.runtime, st.pod, c, cid, dict(post, timeoutSeconds=30), st.ip)
-            if not ok:
-                self.recorder.event(st.pod, "Warning", "FailedPostStartHook", f"PostStart hook failed: {msg}")
+            # kuberuntime_container.go startContainer: a failed postStart handler is reported on
+            # the container and kills it
+            msg, err = await HandlerRunner(self.runtime).run(cid, st.pod, c, post, st.ip)
+            if err is not None:
+                self.recorder.event(st.pod, "Warning", "FailedPostStartHook", msg, field_path=_field_path(st.pod, c))
                 await self.runtime.stop_container(cid, 0)
                 return cid
         if c.get("livenessProbe") or c.get("readinessProbe"):
@@ -1658,7 +1659,7 @@ class Kubelet:
         rt = self.runtime
         spec = st.pod.get("spec") or {}
         by_name = {c["name"]: c for c in spec.get("containers") or ()}
-        from .prober import run_probe
+        runner = HandlerRunner(rt)
         pre = [(name, cid, (by_name[name].get("lifecycle") or {}).get("preStop")) for name, cid in st.containers.items()
                if cid is not None and name in by_name]
         hooks = [(name, cid, h) for name, cid, h in pre if h]
@@ -1671,9 +1672,10 @@ class Kubelet:
         if hooks and budget > 0:
             # preStop handlers run (concurrently) within the grace period before the stop signal
             async def hook(name, cid, h):
-                ok, msg = await run_probe(rt, st.pod, by_name[name], cid, dict(h, timeoutSeconds=max(budget, 1.0)), st.ip)
-                if not ok:
-                    self.recorder.event(st.pod, "Warning", "FailedPreStopHook", f"PreStop hook failed: {msg}")
+                msg, err = await runner.run(cid, st.pod, by_name[name], h, st.ip)
+                if err is not None:
+                    self.recorder.event(st.pod, "Warning", "FailedPreStopHook", msg,
+                                        field_path=_field_path(st.pod, by_name[name]))
             try:
                 await asyncio.wait_for(asyncio.gather(*(hook(*x) for x in hooks)), max(budget, 0.5))
             except asyncio.TimeoutError:
