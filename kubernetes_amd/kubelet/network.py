@@ -400,6 +400,73 @@ def get_pod_dns_type(pod):
     return POD_DNS_CLUSTER, f"invalid DNSPolicy={policy}"
 
 
+ETC_HOSTS_PATH = "/etc/hosts"
+_HOSTNAME_MAX = 63
+
+
+def truncate_pod_hostname(pod_name, hostname):
+    """`truncatePodHostnameIfNeeded`: at most 63 characters, never ending in '-' or '.'."""
+    if len(hostname) <= _HOSTNAME_MAX:
+        return hostname
+    t = hostname[:_HOSTNAME_MAX].rstrip("-.")
+    if not t:
+        raise ValueError(f'hostname for pod "{pod_name}" was invalid: "{hostname}"')
+    log.error('hostname for pod:"%s" was longer than %d. Truncated hostname to :"%s"', pod_name, _HOSTNAME_MAX, t)
+    return t
+
+
+def generate_pod_hostname_and_domain(pod, cluster_domain):
+    """`GeneratePodHostNameAndDomain` (kubelet_pods.go:418): spec.hostname (a DNS label) or the
+    pod name, truncated; the domain `<subdomain>.<namespace>.svc.<cluster domain>` with a
+    subdomain."""
+    from ..api.validation import is_dns1123_label
+    md, spec = pod.get("metadata") or {}, pod.get("spec") or {}
+    hostname = md.get("name", "")
+    if spec.get("hostname"):
+        if not is_dns1123_label(spec["hostname"]):
+            raise ValueError(f'Pod Hostname "{spec["hostname"]}" is not a valid DNS label')
+        hostname = spec["hostname"]
+    hostname = truncate_pod_hostname(md.get("name", ""), hostname)
+    domain = ""
+    if spec.get("subdomain"):
+        if not is_dns1123_label(spec["subdomain"]):
+            raise ValueError(f'Pod Subdomain "{spec["subdomain"]}" is not a valid DNS label')
+        domain = f"{spec['subdomain']}.{md.get('namespace', '')}.svc.{cluster_domain}"
+    return hostname, domain
+
+
+def host_aliases_entries(aliases):
+    """`hostsEntriesFromHostAliases`: one "<ip>\t<hostname>" line per hostname."""
+    if not aliases:
+        return ""
+    out = ["", "# Entries added by HostAliases."]
+    for a in aliases:
+        for h in a.get("hostnames") or ():
+            out.append(f"{a.get('ip')}\t{h}")
+    return "\n".join(out) + "\n"
+
+
+def managed_hosts_file_content(ip, hostname, domain, aliases):
+    """`managedHostsFileContent`."""
+    lines = ["# Kubernetes-managed hosts file.", "127.0.0.1\tlocalhost", "::1\tlocalhost ip6-localhost ip6-loopback",
+             "fe00::0\tip6-localnet", "fe00::0\tip6-mcastprefix", "fe00::1\tip6-allnodes", "fe00::2\tip6-allrouters"]
+    if domain:
+        lines.append(f"{ip}\t{hostname}.{domain}\t{hostname}")
+    else:
+        lines.append(f"{ip}\t{hostname}")
+    return "\n".join(lines) + "\n" + host_aliases_entries(aliases)
+
+
+def node_hosts_file_content(path, aliases):
+    """`nodeHostsFileContent`: the node's hosts file plus the HostAliases entries."""
+    try:
+        with open(path) as f:
+            data = f.read()
+    except OSError:
+        data = ""
+    return data + host_aliases_entries(aliases)
+
+
 class DNSConfigurer:
     """`pkg/kubelet/network/dns/dns.go` Configurer. `recorder(obj, type, reason, message)` (set
     by the kubelet) receives the DNSConfigForming / MissingClusterDNS / CheckLimitsForResolvConf
@@ -514,32 +581,32 @@ class DNSConfigurer:
             lines.append("options " + " ".join(opts))
         return "\n".join(lines) + "\n"
 
+    def pod_hostname_and_domain(self, pod):
+        """`GeneratePodHostNameAndDomain`."""
+        return generate_pod_hostname_and_domain(pod, self.domain)
+
     def hosts_text(self, pod, ip):
+        """`ensureHostsFile`: the kubelet-managed file, or for a host-network pod the node's own
+        /etc/hosts; HostAliases appended either way."""
         spec = pod.get("spec") or {}
-        md = pod["metadata"]
-        lines = ["# Kubernetes-managed hosts file.", "127.0.0.1\tlocalhost", "::1\tlocalhost ip6-localhost ip6-loopback",
-                 "fe00::0\tip6-localnet", "fe00::0\tip6-mcastprefix", "fe00::1\tip6-allnodes", "fe00::2\tip6-allrouters"]
-        host = spec.get("hostname") or md["name"]
-        if ip:
-            if spec.get("subdomain"):
-                fqdn = f"{host}.{spec['subdomain']}.{md.get('namespace', 'default')}.svc.{self.domain}"
-                lines.append(f"{ip}\t{fqdn}\t{host}")
-            else:
-                lines.append(f"{ip}\t{host}")
-        if spec.get("hostAliases"):
-            lines.append("\n# Entries added by HostAliases.")
-            for a in spec["hostAliases"]:
-                lines.append(f"{a.get('ip')}\t" + "\t".join(a.get("hostnames") or ()))
-        return "\n".join(lines) + "\n"
+        if spec.get("hostNetwork"):
+            return node_hosts_file_content(ETC_HOSTS_PATH, spec.get("hostAliases"))
+        try:
+            host, domain = self.pod_hostname_and_domain(pod)
+        except ValueError as e:         # validation keeps these out; never fail the sync over it
+            log.warning("%s", e)
+            host, domain = (pod.get("metadata") or {}).get("name", ""), ""
+        return managed_hosts_file_content(ip, host, domain, spec.get("hostAliases"))
 
     def write_pod_files(self, pod_dir, pod, ip, hosts_only=False):
         """Write `etc-hosts` and `resolv.conf` under the pod dir; returns the container mounts.
         hosts_only: no cluster DNS is configured — the kubelet still manages /etc/hosts of every
-        non-hostNetwork pod (`makeHostsMount`), resolv.conf stays the runtime's."""
+        pod (`makeHostsMount`), resolv.conf stays the runtime's."""
         os.makedirs(pod_dir, exist_ok=True)
         mounts = []
-        spec = pod.get("spec") or {}
-        if not spec.get("hostNetwork"):
+        # makeMounts: every pod with an IP gets a kubelet-written /etc/hosts (a host-network pod
+        # the node's own plus its HostAliases)
+        if ip:
             hp = os.path.join(pod_dir, "etc-hosts")
             with open(hp, "w") as f:
                 f.write(self.hosts_text(pod, ip))

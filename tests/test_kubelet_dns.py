@@ -201,3 +201,64 @@ def test_validate_pod_dns(feature_gate, gate, spec, want):
         assert any(w in e for e in errs), (w, errs)
     if not want:
         assert errs == []
+
+
+# -- pkg/kubelet/kubelet_pods_test.go: hosts files and hostnames ------------------------------------
+HEADER = ("127.0.0.1\tlocalhost\n::1\tlocalhost ip6-localhost ip6-loopback\nfe00::0\tip6-localnet\n"
+          "fe00::0\tip6-mcastprefix\nfe00::1\tip6-allnodes\nfe00::2\tip6-allrouters\n")
+ALIASES1 = [{"ip": "123.45.67.89", "hostnames": ["foo", "bar", "baz"]}]
+ALIASES2 = ALIASES1 + [{"ip": "456.78.90.123", "hostnames": ["park", "doo", "boo"]}]
+ALIAS_TEXT1 = "\n# Entries added by HostAliases.\n123.45.67.89\tfoo\n123.45.67.89\tbar\n123.45.67.89\tbaz\n"
+ALIAS_TEXT2 = ALIAS_TEXT1 + "456.78.90.123\tpark\n456.78.90.123\tdoo\n456.78.90.123\tboo\n"
+
+
+@pytest.mark.parametrize("raw,aliases,want_tail", [
+    ("# hosts file for testing.\n" + HEADER + "123.45.67.89\tsome.domain\n", [], ""),
+    ("# another hosts file for testing.\n" + HEADER + "12.34.56.78\tanother.domain\n", [], ""),
+    ("# hosts file for testing.\n" + HEADER + "123.45.67.89\tsome.domain\n", ALIASES1, ALIAS_TEXT1),
+    ("# another hosts file for testing.\n" + HEADER + "12.34.56.78\tanother.domain\n", ALIASES2, ALIAS_TEXT2),
+])
+def test_node_hosts_file_content(tmp_path, raw, aliases, want_tail):
+    f = tmp_path / "hosts"
+    f.write_text(raw)
+    assert net.node_hosts_file_content(str(f), aliases) == raw + want_tail
+
+
+@pytest.mark.parametrize("ip,host,domain,aliases,entry,tail", [
+    ("123.45.67.89", "podFoo", "", [], "123.45.67.89\tpodFoo\n", ""),
+    ("203.0.113.1", "podFoo", "domainFoo", [], "203.0.113.1\tpodFoo.domainFoo\tpodFoo\n", ""),
+    ("203.0.113.1", "podFoo", "domainFoo", ALIASES1, "203.0.113.1\tpodFoo.domainFoo\tpodFoo\n", ALIAS_TEXT1),
+    ("203.0.113.1", "podFoo", "domainFoo", ALIASES2, "203.0.113.1\tpodFoo.domainFoo\tpodFoo\n", ALIAS_TEXT2),
+])
+def test_managed_hosts_file_content(ip, host, domain, aliases, entry, tail):
+    assert net.managed_hosts_file_content(ip, host, domain, aliases) == \
+        "# Kubernetes-managed hosts file.\n" + HEADER + entry + tail
+
+
+@pytest.mark.parametrize("inp,out", [
+    ("test.pod.hostname", "test.pod.hostname"),
+    ("1234567." * 9, "1234567." * 7 + "1234567"),
+    ("1234567." * 7 + "123456.1234567.", "1234567." * 7 + "123456"),
+    ("1234567." * 7 + "123456-1234567.", "1234567." * 7 + "123456"),
+])
+def test_truncate_pod_hostname(inp, out):
+    assert net.truncate_pod_hostname("test-pod", inp) == out
+
+
+def test_generate_pod_hostname_and_domain():
+    p = {"metadata": {"name": "web-0", "namespace": "ml"}, "spec": {"hostname": "w0", "subdomain": "workers"}}
+    assert net.generate_pod_hostname_and_domain(p, "cluster.local") == ("w0", "workers.ml.svc.cluster.local")
+    assert net.generate_pod_hostname_and_domain({"metadata": {"name": "x"}, "spec": {}}, "c") == ("x", "")
+    with pytest.raises(ValueError, match="not a valid DNS label"):
+        net.generate_pod_hostname_and_domain({"metadata": {"name": "x"}, "spec": {"hostname": "Bad_Name"}}, "c")
+
+
+def test_host_network_pod_gets_node_hosts_plus_aliases(tmp_path, monkeypatch):
+    node_hosts = tmp_path / "node-hosts"
+    node_hosts.write_text("127.0.0.1\tlocalhost\n10.0.0.5\tnode-a\n")
+    monkeypatch.setattr(net, "ETC_HOSTS_PATH", str(node_hosts))
+    d = net.DNSConfigurer([], "cluster.local", "")
+    pod = {"metadata": {"name": "h", "namespace": "d"}, "spec": {"hostNetwork": True, "hostAliases": ALIASES1}}
+    mounts = d.write_pod_files(str(tmp_path / "pod"), pod, "10.0.0.5", hosts_only=True)
+    assert mounts[0]["containerPath"] == "/etc/hosts"
+    assert (tmp_path / "pod" / "etc-hosts").read_text() == node_hosts.read_text() + ALIAS_TEXT1
