@@ -204,6 +204,7 @@ def main(argv=None):
                      image_gc=image_gc, network_plugin=plugin, hostports=hostports,
                      cgroup_root=a.cgroup_root if a.cgroups_per_qos else None,
                      container_log_dir=a.container_log_dir or None,
+                     master_service_namespace=a.master_service_namespace,
                      allowed_unsafe_sysctls=[x for x in a.experimental_allowed_unsafe_sysctls.split(",") if x], **base)
         await kl.run()
         if a.rotate_certificates and a.kubeconfig:
@@ -393,11 +394,13 @@ def _reference_flags(ap):
     g.add_argument("--contention-profiling", type=_bool, default=False,
                    help="sample where the event loop blocks, served at /debug/pprof/block")
     deprecated_noop(g, "--enable-custom-metrics", False, _bool, "options.go:368")
+    g.add_argument("--master-service-namespace", default="default",
+                   help="the namespace whose kubernetes service is injected into every pod's environment")
     unsupported(g, "--keep-terminated-pod-volumes", False, _bool, "volumes of terminated pods are torn down")
     unsupported(g, "--enable-controller-attach-detach", True, _bool,
                 "attach/detach is always the controller's (the kubelet only mounts)")
     for f, d in (("--experimental-mounter-path", ""), ("--init-config-dir", ""),
-                 ("--master-service-namespace", "default"), ("--volume-stats-agg-period", "1m")):
+                 ("--volume-stats-agg-period", "1m")):
         unsupported(g, f, d, str, "not implemented by this kubelet")
 
 

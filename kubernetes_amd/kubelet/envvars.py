@@ -2,7 +2,7 @@
 `kubelet_pods.go` getServiceEnvVarMap).
 
 Every container sees, for each service of its namespace plus the `kubernetes` master service of
-the `default` namespace (headless services, whose ClusterIP is None, are skipped):
+the master service namespace (`--master-service-namespace`, `default`; headless services, whose ClusterIP is None, are skipped):
 
     {NAME}_SERVICE_HOST=<clusterIP>          {NAME}_SERVICE_PORT=<first port>
     {NAME}_SERVICE_PORT_{PORTNAME}=<port>    (named ports)
@@ -27,7 +27,9 @@ def _ip_set(svc) -> bool:
     return bool(ip) and ip != "None"
 
 
-def service_map(services, namespace) -> dict:
+def service_map(services, namespace, master_namespace=MASTER_NAMESPACE) -> dict:
+    """getServiceEnvVarMap: every service of the pod's namespace, plus the master services of
+    `--master-service-namespace` unless the pod's namespace has its own of that name."""
     out = {}
     for svc in services:
         if not _ip_set(svc):
@@ -36,7 +38,7 @@ def service_map(services, namespace) -> dict:
         name, ns = md["name"], md.get("namespace", "default")
         if ns == namespace:
             out[name] = svc
-        elif ns == MASTER_NAMESPACE and name in MASTER_SERVICES:
+        elif ns == master_namespace and name in MASTER_SERVICES:
             out.setdefault(name, svc)
     return out
 
@@ -70,5 +72,6 @@ def from_services(services) -> list:
     return env
 
 
-def service_env(services, namespace) -> list:
-    return from_services(sorted(service_map(services, namespace).values(), key=lambda s: s["metadata"]["name"]))
+def service_env(services, namespace, master_namespace=MASTER_NAMESPACE) -> list:
+    return from_services(sorted(service_map(services, namespace, master_namespace).values(),
+                                key=lambda s: s["metadata"]["name"]))

@@ -159,7 +159,7 @@ class Kubelet:
                  hostports=None, container_gc=None, crash_backoff=(10.0, 300.0), dynamic_config_dir=None,
                  bootstrap_checkpoint_path=None, volume_plugin_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec",
                  manifest_url=None, manifest_url_headers=None, kube_reserved=None, system_reserved=None,
-                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, container_log_dir=None,
+                 cgroup_root=None, allowed_unsafe_sysctls=(), service_env=True, master_service_namespace="default", container_log_dir=None,
                  event_qps=5.0, event_burst=10, auth=None, node_log_dir="/var/log", tls=None, read_only_port=None,
                  healthz_port=None, healthz_address="127.0.0.1", debugging_handlers=True, node_ip=None,
                  register_taints=(), register_schedulable=True, provider_id="", allow_privileged=True,
@@ -210,6 +210,7 @@ class Kubelet:
         from .network import NetworkPlugin
         self.network = network_plugin or NetworkPlugin()
         self.dns = dns                       # network.DNSConfigurer or None
+        self.master_service_namespace = master_service_namespace   # --master-service-namespace
         self.hostports = hostports           # network.HostportManager or None
         self.container_gc = container_gc     # ContainerGC policy dict or None
         self.crash_backoff = crash_backoff   # (initial, max) restart back-off, kubelet.go backOffPeriod/MaxContainerBackOff
@@ -346,6 +347,8 @@ class Kubelet:
             self.svc_informer = Informer(self.client, "services")
             self.svc_informer.start()
         self._wire_dns()
+        if self.volumes.recorder is None:
+            self.volumes.recorder = lambda obj, typ, reason, msg: self.recorder.event(obj, typ, reason, msg)
         await self.update_runtime_up()
         if self.register:
             await self._register_node()
@@ -1308,7 +1311,7 @@ class Kubelet:
         hit = self._svc_env_cache.get(ns)
         if hit is not None and hit[0] == key:
             return list(hit[1])
-        env = service_env(self.svc_informer.list(), ns)
+        env = service_env(self.svc_informer.list(), ns, self.master_service_namespace)
         self._svc_env_cache[ns] = (key, env)
         return list(env)
 

@@ -217,6 +217,7 @@ class VolumeManager:
         self.on_in_use_change = None                 # callback: node status should report volumesInUse
         self.allocatable = None                      # node allocatable: default downward-API limits
         self.host_ip = None                          # the node's address (status.hostIP)
+        self.recorder = None                         # (obj, type, reason, message): pod events
 
     def _traversable(self, path):
         """Make the kubelet-owned directories above a volume traversable (0711: no listing) so a
@@ -637,8 +638,14 @@ class VolumeManager:
                     continue
                 put(pre + k, base64.b64decode(v).decode(errors="replace") if kind == "secrets" else str(v))
             if invalid:
-                log.warning("Keys [%s] from the EnvFrom %s %s/%s were skipped since they are considered invalid "
-                            "environment variable names.", ", ".join(invalid), kind[:-1], ns, ref["name"])
+                what = "configMap" if kind == "configmaps" else "secret"
+                msg = (f"Keys [{', '.join(sorted(invalid))}] from the EnvFrom {what} {ns}/{ref['name']} were skipped "
+                       f"since they are considered invalid environment variable names.")
+                rec = getattr(self, "recorder", None)
+                if rec is not None:
+                    rec(pod, "Warning", "InvalidEnvironmentVariableNames", msg)
+                else:
+                    log.warning("%s", msg)
         for e in container.get("env") or ():
             name = e["name"]
             if "value" in e:
@@ -656,7 +663,7 @@ class VolumeManager:
                 if obj is not None:
                     if r["key"] not in (obj.get("data") or {}):
                         if not r.get("optional"):
-                            raise VolumeError(f"configmap {r['name']} has no key {r['key']}")
+                            raise VolumeError(f"Couldn't find key {r['key']} in ConfigMap {ns}/{r['name']}")
                     else:
                         put(name, str(obj["data"][r["key"]]))
             elif "secretKeyRef" in vf:
@@ -665,7 +672,7 @@ class VolumeManager:
                 if obj is not None:
                     if r["key"] not in (obj.get("data") or {}):
                         if not r.get("optional"):
-                            raise VolumeError(f"secret {r['name']} has no key {r['key']}")
+                            raise VolumeError(f"Couldn't find key {r['key']} in Secret {ns}/{r['name']}")
                     else:
                         put(name, base64.b64decode(obj["data"][r["key"]]).decode(errors="replace"))
         # the service variables come last and never override the container's own (kubelet_pods.go)

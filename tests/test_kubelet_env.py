@@ -121,3 +121,76 @@ def test_from_services():
         ("SUPER_IPV6_PORT_8084_TCP_ADDR", "2001:DB8::"),
     ]
     assert got == want
+
+
+# -- pkg/kubelet/kubelet_pods_test.go TestMakeEnvironmentVariables: the service cases -------------
+def _svc(name, ns, ip, port):
+    return {"metadata": {"name": name, "namespace": ns}, "spec": {"clusterIP": ip, "ports": [{"protocol": "TCP",
+                                                                                              "port": port}]}}
+
+
+MEV_SERVICES = [_svc("kubernetes", "default", "1.2.3.1", 8081), _svc("test", "test1", "1.2.3.3", 8083),
+                _svc("kubernetes", "test2", "1.2.3.4", 8084), _svc("test", "test2", "1.2.3.5", 8085),
+                _svc("test", "test2", "None", 8085), _svc("test", "test2", "", 8085),
+                _svc("kubernetes", "kubernetes", "1.2.3.6", 8086), _svc("not-special", "kubernetes", "1.2.3.8", 8088),
+                _svc("not-special", "kubernetes", "None", 8088), _svc("not-special", "kubernetes", "", 8088)]
+
+
+def _svc_vars(prefix, ip, port):
+    return {f"{prefix}_SERVICE_HOST": ip, f"{prefix}_SERVICE_PORT": str(port), f"{prefix}_PORT": f"tcp://{ip}:{port}",
+            f"{prefix}_PORT_{port}_TCP": f"tcp://{ip}:{port}", f"{prefix}_PORT_{port}_TCP_PROTO": "tcp",
+            f"{prefix}_PORT_{port}_TCP_PORT": str(port), f"{prefix}_PORT_{port}_TCP_ADDR": ip}
+
+
+@pytest.mark.parametrize("ns,master_ns,want", [
+    ("test1", "default", {**_svc_vars("TEST", "1.2.3.3", 8083), **_svc_vars("KUBERNETES", "1.2.3.1", 8081)}),
+    # master service in pod ns: the namespace's own "kubernetes" wins over the master one
+    ("test2", "kubernetes", {**_svc_vars("TEST", "1.2.3.5", 8085), **_svc_vars("KUBERNETES", "1.2.3.4", 8084)}),
+    # pod in master service ns: every service there, with the master kubernetes service
+    ("kubernetes", "kubernetes", {**_svc_vars("NOT_SPECIAL", "1.2.3.8", 8088), **_svc_vars("KUBERNETES", "1.2.3.6", 8086)}),
+    ("downward-api", "nothing", {}),
+])
+def test_make_environment_variables_services(ns, master_ns, want):
+    from kubernetes_amd.kubelet.envvars import service_env
+    got = {e["name"]: e["value"] for e in service_env(MEV_SERVICES, ns, master_ns)}
+    assert got == want
+
+
+def test_make_environment_variables_missing_keys_and_invalid_names(run):
+    """configmapkeyref / secretkeyref with missing keys (optional or not), envFrom with invalid
+    key names reported by an InvalidEnvironmentVariableNames event."""
+    import base64
+
+    from kubernetes_amd.kubelet.volumes import VolumeError, VolumeManager
+
+    class FakeClient:
+        objs = {("configmaps", "ns", "cm"): {"data": {"REAL": "1", "1bad": "x", "also bad": "y"}},
+                ("secrets", "ns", "sec"): {"data": {"S": base64.b64encode(b"s3").decode()}}}
+
+        async def get(self, kind, name, ns=None, **kw):
+            from kubernetes_amd.client.rest import APIStatusError
+            o = self.objs.get((kind, ns, name))
+            if o is None:
+                raise APIStatusError(404, {"reason": "NotFound", "message": f"{kind} {name} not found"})
+            return o
+
+    events = []
+    vm = VolumeManager(FakeClient(), "/tmp/unused")
+    vm.recorder = lambda obj, t, r, m: events.append((t, r, m))
+    pod = {"metadata": {"name": "p", "namespace": "ns"}, "spec": {}}
+
+    async def main():
+        env = await vm.env_for(pod, {"envFrom": [{"configMapRef": {"name": "cm"}}]})
+        assert env == [{"name": "REAL", "value": "1"}]
+        assert events == [("Warning", "InvalidEnvironmentVariableNames",
+                           "Keys [1bad, also bad] from the EnvFrom configMap ns/cm were skipped since they are "
+                           "considered invalid environment variable names.")]
+        optional = {"env": [{"name": "A", "valueFrom": {"configMapKeyRef": {"name": "cm", "key": "nope", "optional": True}}},
+                            {"name": "B", "valueFrom": {"secretKeyRef": {"name": "sec", "key": "nope", "optional": True}}},
+                            {"name": "C", "valueFrom": {"configMapKeyRef": {"name": "gone", "key": "k", "optional": True}}}]}
+        assert await vm.env_for(pod, optional) == []
+        with pytest.raises(VolumeError, match="Couldn't find key nope in ConfigMap ns/cm"):
+            await vm.env_for(pod, {"env": [{"name": "A", "valueFrom": {"configMapKeyRef": {"name": "cm", "key": "nope"}}}]})
+        with pytest.raises(VolumeError, match="Couldn't find key nope in Secret ns/sec"):
+            await vm.env_for(pod, {"env": [{"name": "A", "valueFrom": {"secretKeyRef": {"name": "sec", "key": "nope"}}}]})
+    run(main())
