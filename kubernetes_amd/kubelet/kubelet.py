@@ -43,7 +43,7 @@ from .prober import ProbeManager
 from .runtimestate import NETWORK_READY, RUNTIME_READY, RuntimeState, ready_condition, update_runtime_up
 from .runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, RunContainerOptions
 from .qos import oom_score_adj
-from .volumes import VolumeError, VolumeManager
+from .volumes import VolumeError, VolumeManager, make_absolute_path
 from ..utils.tasks import spawn
 
 log = logging.getLogger("kubelet")
@@ -1340,7 +1340,9 @@ class Kubelet:
             self.recorder.event(st.pod, "Warning", "Failed", f"Error: {err}", field_path=_field_path(st.pod, c))
             await self._report(st)
             return None
-        opts.mounts.extend(st.net_mounts)
+        # makeMounts: no kubelet /etc/hosts (or resolv.conf) over a path the container mounts itself
+        own = {make_absolute_path(m.get("mountPath", "")) for m in c.get("volumeMounts") or ()}
+        opts.mounts.extend(m for m in st.net_mounts if m["containerPath"] not in own)
         opts.oom_score_adj = oom_score_adj(st.pod, c, parse_quantity(self.capacity["memory"]).value)
         if self.cgroups is not None:
             opts.cgroup_parent = self.cgroups.pod_dir(st.pod)

@@ -198,6 +198,67 @@ def _resource_field(container, ref, allocatable=None):
     return str(-(-v.numerator // v.denominator))
 
 
+def validate_path_no_backsteps(p):
+    """`volumevalidation.ValidatePathNoBacksteps`."""
+    if ".." in p.split(os.sep):
+        raise VolumeError("must not contain '..'")
+
+
+def make_absolute_path(p):
+    """`makeAbsolutePath` (linux): a relative container path is taken from the root."""
+    return p if p.startswith("/") else "/" + p
+
+
+def _within(path, root):
+    return path == root or path.startswith(root.rstrip(os.sep) + os.sep)
+
+
+def make_mounts(container, vols: dict):
+    """Each volumeMount becomes {containerPath, hostPath, readOnly}. A subPath must be relative,
+    without '..', and must resolve (symlinks included) inside the volume; a missing subPath
+    directory is created with the volume directory's mode (`SafeMakeDir`), never through a
+    symlink that leaves the volume (the reference's `PrepareSafeSubpath` guarantee)."""
+    out = []
+    name = container.get("name", "")
+    for m in container.get("volumeMounts") or ():
+        hp = vols.get(m["name"])
+        if hp is None:
+            raise VolumeError(f'cannot find volume "{m["name"]}" to mount into container "{name}"')
+        sub = m.get("subPath") or ""
+        if sub:
+            if os.path.isabs(sub):
+                raise VolumeError(f"error SubPath `{sub}` must not be an absolute path")
+            try:
+                validate_path_no_backsteps(sub)
+            except VolumeError as e:
+                raise VolumeError(f"unable to provision SubPath `{sub}`: {e}") from None
+            try:
+                perm = os.lstat(hp).st_mode & 0o7777
+            except OSError as e:
+                raise VolumeError(str(e)) from None
+            vol = os.path.realpath(hp)
+            target = os.path.join(vol, sub)
+            fail = VolumeError(f'failed to prepare subPath for volumeMount "{m["name"]}" of container "{name}"')
+            if not os.path.lexists(target):
+                # create component by component, refusing any existing symlink on the way
+                cur = vol
+                for part in sub.split(os.sep):
+                    if not part or part == ".":
+                        continue
+                    cur = os.path.join(cur, part)
+                    if os.path.islink(cur) and not _within(os.path.realpath(cur), vol):
+                        raise fail
+                    if not os.path.lexists(cur):
+                        os.mkdir(cur)
+                        os.chmod(cur, perm or 0o755)
+            if not _within(os.path.realpath(target), vol):
+                raise fail
+            hp = os.path.realpath(target)
+        out.append({"containerPath": make_absolute_path(m["mountPath"]), "hostPath": hp,
+                    "readOnly": bool(m.get("readOnly"))})
+    return out
+
+
 class VolumeManager:
     def __init__(self, client, root, csi_plugins_dir=None, node_name=None, attach_timeout=60.0,
                  flex_plugins_dir="/usr/libexec/kubernetes/kubelet-plugins/volume/exec", mounter=None):
@@ -566,16 +627,8 @@ class VolumeManager:
         return _write_files(d, data, items, int(mode))
 
     def mounts_for(self, container, vols: dict):
-        out = []
-        for m in container.get("volumeMounts") or ():
-            hp = vols.get(m["name"])
-            if hp is None:
-                raise VolumeError(f"volumeMount {m['name']!r} refers to no pod volume")
-            if m.get("subPath"):
-                hp = os.path.join(hp, m["subPath"])
-                os.makedirs(hp, exist_ok=True)
-            out.append({"containerPath": m["mountPath"], "hostPath": hp, "readOnly": bool(m.get("readOnly"))})
-        return out
+        """`makeMounts` (kubelet_pods.go:167) for the container's volumeMounts."""
+        return make_mounts(container, vols)
 
     async def _memory_dir(self, pod, name, d, size_limit=None):
         """`medium: Memory` (`empty_dir.go` setupTmpfs): a tmpfs mounted on the volume directory
