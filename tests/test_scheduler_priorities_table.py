@@ -291,3 +291,73 @@ def test_node_label_priority(label, presence, want):
     infos = [cache.nodes[f"machine{i}"] for i in (1, 2, 3)]
     scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
     assert [scores[f"machine{i}"] for i in (1, 2, 3)] == want
+
+
+# -- taint_toleration_test.go / node_affinity_test.go --------------------------------------------
+
+def _prioritize(prio, pod, nodes):
+    cache = SchedulerCache()
+    for n in nodes:
+        cache.add_node(n)
+    gs = GenericScheduler(cache, [], {prio: 1}, equivalence_cache=False)
+    infos = [cache.nodes[n["metadata"]["name"]] for n in nodes]
+    scores = gs.prioritize(pod, PodInfo(pod), infos, CycleContext(cache, pod))
+    return [scores[n["metadata"]["name"]] for n in nodes]
+
+
+def _tnode(name, taints=(), labels=None):
+    n = _node(name, 4000, 10000)
+    n["spec"]["taints"] = [{"key": k, "value": v, "effect": e} for k, v, e in taints]
+    n["metadata"]["labels"] = dict(labels or {})
+    return n
+
+
+def _tpod(tolerations=(), affinity=None):
+    p = _pod([])
+    p["spec"]["tolerations"] = [{"key": k, "operator": "Equal", "value": v, "effect": e} for k, v, e in tolerations]
+    if affinity:
+        p["spec"]["affinity"] = affinity
+    return p
+
+
+PNS, NS = "PreferNoSchedule", "NoSchedule"
+CPU, DISK = ("cpu-type", "arm64", PNS), ("disk-type", "ssd", PNS)
+
+
+@pytest.mark.parametrize("tolerations,nodes,want", [
+    # node with taints tolerated by the pod gets a higher score than those with intolerable taints
+    ([("foo", "bar", PNS)], [("nodeA", [("foo", "bar", PNS)]), ("nodeB", [("foo", "blah", PNS)])], [10, 0]),
+    # the count of tolerated taints does not matter
+    ([CPU, DISK], [("nodeA", []), ("nodeB", [CPU]), ("nodeC", [CPU, DISK])], [10, 10, 10]),
+    # the more intolerable taints, the lower the score
+    ([("foo", "bar", PNS)], [("nodeA", []), ("nodeB", [CPU]), ("nodeC", [CPU, DISK])], [10, 5, 0]),
+    # only PreferNoSchedule taints and tolerations count
+    ([("cpu-type", "arm64", NS), ("disk-type", "ssd", NS)],
+     [("nodeA", []), ("nodeB", [("cpu-type", "arm64", NS)]), ("nodeC", [CPU, DISK])], [10, 10, 0]),
+    # default: no taints and tolerations, lands on the node without taints
+    ([], [("nodeA", []), ("nodeB", [CPU])], [10, 0]),
+])
+def test_taint_and_toleration(tolerations, nodes, want):
+    assert _prioritize("TaintTolerationPriority", _tpod(tolerations), [_tnode(n, t) for n, t in nodes]) == want
+
+
+def _pref(weight, *exprs):
+    return {"weight": weight, "preference": {"matchExpressions": [
+        {"key": k, "operator": "In", "values": [v]} for k, v in exprs]}}
+
+
+AFF1 = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [_pref(2, ("foo", "bar"))]}}
+AFF2 = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    _pref(2, ("foo", "bar")), _pref(4, ("key", "value")), _pref(5, ("foo", "bar"), ("key", "value"), ("az", "az1"))]}}
+L1, L2, L3 = {"foo": "bar"}, {"key": "value"}, {"az": "az1"}
+L4, L5 = {"abc": "az11", "def": "az22"}, {"foo": "bar", "key": "value", "az": "az1"}
+
+
+@pytest.mark.parametrize("affinity,nodes,want", [
+    (None, [("machine1", L1), ("machine2", L2), ("machine3", L3)], [0, 0, 0]),
+    (AFF1, [("machine1", L4), ("machine2", L2), ("machine3", L3)], [0, 0, 0]),
+    (AFF1, [("machine1", L1), ("machine2", L2), ("machine3", L3)], [10, 0, 0]),
+    (AFF2, [("machine1", L1), ("machine5", L5), ("machine2", L2)], [1, 10, 3]),
+])
+def test_node_affinity_priority(affinity, nodes, want):
+    assert _prioritize("NodeAffinityPriority", _tpod(affinity=affinity), [_tnode(n, labels=lb) for n, lb in nodes]) == want
