@@ -1333,7 +1333,9 @@ class Kubelet:
             return None
         spec_c = c
         opts.attempt = st.restarts.get(c["name"], 0)
-        err = _apply_security_context(st.pod, c, opts)
+        cfg_fn = getattr(self.image_service, "image_config", None)
+        cfg = cfg_fn(c.get("image", "")) if cfg_fn is not None else None
+        err = _apply_security_context(st.pod, c, opts, image_user(cfg) if cfg is not None else None)
         if err:
             # kuberuntime_container.go: verifyRunAsNonRoot fails the start with CreateContainerConfigError
             st.waiting[c["name"]] = ("CreateContainerConfigError", err)
@@ -2153,7 +2155,7 @@ def _container_status_now(c, cs, restarts, waiting=None):
     return s
 
 
-def _apply_security_context(pod, c, opts):
+def _apply_security_context(pod, c, opts, image_user=None):
     """`pkg/kubelet/kuberuntime/security_context.go`: the container's securityContext overrides the
     pod's. runAsUser / runAsGroup become the process identity; the pod's fsGroup and
     supplementalGroups are supplemental groups (security_context.go:58-66), never the primary
@@ -2177,12 +2179,36 @@ def _apply_security_context(pod, c, opts):
     opts.cap_add = list(caps.get("add") or ())
     opts.cap_drop = list(caps.get("drop") or ())
     opts.readonly_rootfs = bool(csc.get("readOnlyRootFilesystem"))
-    if non_root:
-        if uid is not None and int(uid) == 0:
-            return "container's runAsUser breaks non-root policy"
-        if uid is None and os.geteuid() == 0:
-            # no image metadata here: the entrypoint would inherit the runtime's (root) identity
-            return "container has runAsNonRoot and image will run as root"
+    if image_user is None:
+        # no image metadata: the entrypoint inherits the runtime's identity
+        image_user = (os.geteuid(), "")
+    return verify_run_as_non_root(non_root, uid, *image_user)
+
+
+def image_user(config) -> tuple:
+    """`getImageUser`: (uid, username) from an image config's User ("uid", "uid:gid" or a name);
+    (None, "") when the image sets none, which runs as root (uid 0)."""
+    user = str((config or {}).get("User") or "").split(":", 1)[0]
+    if not user:
+        return 0, ""
+    try:
+        return int(user), ""
+    except ValueError:
+        return None, user
+
+
+def verify_run_as_non_root(run_as_non_root, run_as_user, image_uid, image_username="") -> str:
+    """`verifyRunAsNonRoot` (kuberuntime/security_context.go:78) over the effective security
+    context: "" when allowed, else the error."""
+    if not run_as_non_root:
+        return ""
+    if run_as_user is not None:
+        return "container's runAsUser breaks non-root policy" if int(run_as_user) == 0 else ""
+    if image_uid is not None and int(image_uid) == 0:
+        return "container has runAsNonRoot and image will run as root"
+    if image_uid is None and image_username:
+        return (f"container has runAsNonRoot and image has non-numeric user ({image_username}), cannot verify user "
+                f"is non-root")
     return ""
 
 

@@ -166,3 +166,28 @@ EXPAND_CASES = [
 def test_expand_container_command_and_args(name, c, envs, cmd, args):
     got = expand_container_command_and_args(c, [{"name": n, "value": v} for n, v in envs])
     assert got == (cmd, args)
+
+
+# -- pkg/kubelet/kuberuntime/security_context_test.go TestVerifyRunAsNonRoot ---------------------
+from kubernetes_amd.kubelet.kubelet import image_user, verify_run_as_non_root  # noqa: E402
+
+
+@pytest.mark.parametrize("non_root,run_as,image_uid,fail", [
+    (None, None, 0, False),          # no SecurityContext
+    (None, 0, 0, False),             # RunAsNonRoot not set
+    (False, None, 0, False),         # RunAsNonRoot false, image user root
+    (False, 0, 123, False),          # RunAsNonRoot false, RunAsUser root
+    (True, 0, 123, True),            # RunAsUser root with RunAsNonRoot
+    (True, None, 0, True),           # image user root with RunAsNonRoot
+    (True, None, 123, False),
+    (True, 1000, 0, False),
+])
+def test_verify_run_as_non_root(non_root, run_as, image_uid, fail):
+    assert bool(verify_run_as_non_root(non_root, run_as, image_uid)) == fail
+
+
+def test_image_user_and_non_numeric_name():
+    assert image_user({}) == (0, "") and image_user(None) == (0, "")
+    assert image_user({"User": "123"}) == (123, "") and image_user({"User": "123:456"}) == (123, "")
+    assert image_user({"User": "nobody"}) == (None, "nobody")
+    assert "non-numeric user (nobody)" in verify_run_as_non_root(True, None, None, "nobody")
