@@ -83,7 +83,9 @@ async def run_probe(runtime, pod, container, cid, probe, pod_ip="127.0.0.1"):
                 w.close()
             parts = line.split()
             code = int(parts[1]) if len(parts) > 1 else 0
-            return 200 <= code < 400, f"HTTP probe status {code}"
+            if 200 <= code < 400:
+                return True, ""
+            return False, f"HTTP probe failed with statuscode: {code}"
         if "tcpSocket" in probe:
             t = probe["tcpSocket"]
             r, w = await asyncio.wait_for(asyncio.open_connection(t.get("host") or pod_ip,

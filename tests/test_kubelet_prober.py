@@ -99,3 +99,30 @@ def test_https_probe_skips_verification(run, tmp_path):
             s.srv.close()
     ok, msg = run(main())
     assert ok, msg
+
+
+def test_http_probe_failure_message_and_success(run):
+    """`pkg/probe/http/http.go` DoHTTPProbe: 200 <= code < 400 succeeds; otherwise the output is
+    "HTTP probe failed with statuscode: <code>"."""
+    import asyncio
+
+    from kubernetes_amd.kubelet.prober import run_probe
+
+    async def main():
+        codes = iter([500, 302])
+
+        async def serve(r, w):
+            await r.readuntil(b"\r\n\r\n")
+            w.write(f"HTTP/1.1 {next(codes)} X\r\nContent-Length: 0\r\nConnection: close\r\n\r\n".encode())
+            await w.drain()
+            w.close()
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        try:
+            probe = {"httpGet": {"port": port, "path": "/healthz"}, "timeoutSeconds": 5}
+            assert await run_probe(None, {}, {}, "cid", probe, "127.0.0.1") == (
+                False, "HTTP probe failed with statuscode: 500")
+            assert (await run_probe(None, {}, {}, "cid", probe, "127.0.0.1"))[0] is True
+        finally:
+            srv.close()
+    run(main())
