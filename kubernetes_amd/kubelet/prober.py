@@ -12,6 +12,8 @@ from __future__ import annotations
 import asyncio
 import logging
 
+from .runtime.base import EXITED, RUNNING
+
 log = logging.getLogger("kubelet.prober")
 
 
@@ -112,6 +114,19 @@ class _Worker:
         fail_th = int(p.get("failureThreshold") or 3)
         await asyncio.sleep(float(p.get("initialDelaySeconds") or 0))
         while True:
+            status_fn = getattr(self.mgr.runtime, "container_status", None)
+            cs = status_fn(self.cid) if status_fn is not None else None
+            if cs is not None and cs.state != RUNNING:
+                # worker.go doProbe: a non-running container is not probed; readiness fails at
+                # once (no threshold), and the worker ends if the container will not restart
+                if self.kind == "readiness" and self.result:
+                    self.result = False
+                    self.ok_run = 0
+                    self.mgr.changed(self, "container is not running")
+                if cs.state == EXITED and (self.pod.get("spec") or {}).get("restartPolicy") == "Never":
+                    return
+                await asyncio.sleep(period)
+                continue
             ok, msg = await run_probe(self.mgr.runtime, self.pod, self.container, self.cid, p, self.mgr.pod_ip(self.uid))
             if ok:
                 self.ok_run += 1

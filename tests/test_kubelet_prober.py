@@ -126,3 +126,49 @@ def test_http_probe_failure_message_and_success(run):
         finally:
             srv.close()
     run(main())
+
+
+def test_worker_non_running_container_fails_readiness_without_threshold(run):
+    """`worker.go` doProbe: a container that is not running is not probed; its readiness result
+    becomes Failure at once, and with restartPolicy Never the worker stops."""
+    import asyncio
+    from types import SimpleNamespace
+
+    from kubernetes_amd.kubelet.prober import ProbeManager
+    from kubernetes_amd.kubelet.runtime.base import EXITED, RUNNING
+
+    class RT:
+        state = RUNNING
+        execs = 0
+
+        def container_status(self, cid):
+            return SimpleNamespace(state=self.state)
+
+        async def exec_sync(self, cid, cmd, timeout):
+            self.execs += 1
+            return 0, b""
+
+    async def main():
+        rt, changes = RT(), []
+        pm = ProbeManager(rt, lambda uid, c, ready: changes.append(ready), lambda *a: None)
+        c = {"name": "c", "readinessProbe": {"exec": {"command": ["true"]}, "periodSeconds": 0.02,
+                                             "failureThreshold": 3}}
+        pod = {"spec": {"restartPolicy": "Never"}}
+        pm.start("u", pod, c, "cid")
+        for _ in range(100):
+            if pm.ready("u", "c"):
+                break
+            await asyncio.sleep(0.01)
+        assert pm.ready("u", "c") is True
+        rt.state = EXITED
+        n = rt.execs
+        for _ in range(100):
+            if pm.ready("u", "c") is False:
+                break
+            await asyncio.sleep(0.01)
+        assert pm.ready("u", "c") is False and changes[-1] is False       # no 3-probe threshold
+        w = pm.workers[("u", "c", "readiness")]
+        await asyncio.sleep(0.1)
+        assert w.task.done() and rt.execs == n                            # Never: the worker ended unprobed
+        pm.stop()
+    run(main())
