@@ -911,12 +911,29 @@ class Kubelet:
             st.requests = core.pod_requests(st.pod)
         return st.requests
 
+    def _admit_allocatable(self):
+        """Node allocatable as quantities, recomputed when capacity or reservations change."""
+        key = (tuple(sorted(self.capacity.items())), id(self.eviction))
+        hit = getattr(self, "_alloc_cache", None)
+        if hit is None or hit[0] != key:
+            alloc = self._allocatable(dict(self.capacity))
+            hit = (key, {k: parse_quantity(str(v)) for k, v in alloc.items()})
+            self._alloc_cache = hit
+        return hit[1]
+
     def _general_predicates(self, pod, node_labels=None):
-        """GeneralPredicates against this node's capacity and the other active pods."""
+        """`lifecycle/predicate.go` predicateAdmitHandler with `GeneralPredicates` against this
+        node's allocatable and the other active pods: the pod count, cpu / memory /
+        ephemeral-storage (extended resources are the device manager's, as the reference
+        removes the ones the node does not advertise), HostName, host ports and the node
+        selector plus required node affinity. Returns (reason, message) or None."""
         uid = pod["metadata"]["uid"]
         me = self.pods.get(uid)
         need = self._requests(me) if me is not None else core.pod_requests(pod)
+        spec = pod.get("spec") or {}
+        want_ports = _host_ports(spec)
         used: dict = {}
+        ports = set()
         n = 0
         for other in self.pods.values():
             if other.terminated or other.rejected or other.uid == uid:
@@ -924,17 +941,36 @@ class Kubelet:
             n += 1
             for k, v in self._requests(other).items():
                 used[k] = used[k] + v if k in used else v
-        if n + 1 > int(self.capacity["pods"]):
-            return "OutOfpods", "Node didn't have enough resource: pods"
-        for k, v in need.items():
-            if k in ("cpu", "memory") and k in self.capacity:
-                cap = parse_quantity(self.capacity[k])
-                if (used[k] + v if k in used else v) > cap:
-                    return f"OutOf{k}", f"Node didn't have enough resource: {k}"
-        sel = (pod.get("spec") or {}).get("nodeSelector") or {}
-        labels = node_labels if node_labels is not None else self._node_object()["metadata"]["labels"]
-        for k, v in sel.items():
-            if labels.get(k) != v:
+            if want_ports:
+                ports.update(_host_ports(other.pod.get("spec") or {}))
+        alloc = self._admit_allocatable()
+        pods_cap = int(alloc["pods"].value) if "pods" in alloc else int(self.capacity["pods"])
+        if n + 1 > pods_cap:
+            return "OutOfpods", (f"Node didn't have enough resource: pods, requested: 1, used: {n}, "
+                                 f"capacity: {pods_cap}")
+        for k in ("cpu", "memory", "ephemeral-storage"):
+            v = need.get(k)
+            if v is None or k not in alloc or not v.value:
+                continue
+            u = used.get(k)
+            total = u + v if u is not None else v
+            if total > alloc[k]:
+                milli = k == "cpu"
+                f = (lambda q: q.milli_value()) if milli else (lambda q: int(q.value))
+                return f"OutOf{k}", (f"Node didn't have enough resource: {k}, requested: {f(v)}, used: "
+                                     f"{f(u) if u is not None else 0}, capacity: {f(alloc[k])}")
+        if spec.get("nodeName") and spec["nodeName"] != self.node_name:
+            return "HostName", "Predicate HostName failed"
+        for ip, proto, port in want_ports:
+            for oip, oproto, oport in ports:
+                if oport == port and oproto == proto and (ip == oip or "0.0.0.0" in (ip, oip)):
+                    return "PodFitsHostPorts", "Predicate PodFitsHostPorts failed"
+        sel = spec.get("nodeSelector") or {}
+        terms = _node_affinity_required(spec)
+        if sel or terms is not None:
+            labels = node_labels if node_labels is not None else self._node_object()["metadata"]["labels"]
+            if any(labels.get(k) != v for k, v in sel.items()) or (
+                    terms is not None and not _node_affinity_matches(terms, labels, self.node_name)):
                 return "MatchNodeSelector", "Predicate MatchNodeSelector failed"
         return None
 
@@ -1073,8 +1109,9 @@ class Kubelet:
                 st.rejected = reason
                 if st.adopted:
                     await self._kill_pod(st, 0)
+                # rejectPod: the event carries the message, the status "Pod " + message
                 self.recorder.event(pod, "Warning", reason, msg)
-                await self._write_status(st, {"phase": core.POD_FAILED, "reason": reason, "message": msg,
+                await self._write_status(st, {"phase": core.POD_FAILED, "reason": reason, "message": "Pod " + msg,
                                               "conditions": (pod.get("status") or {}).get("conditions") or []})
                 return
             st.admitted = True
@@ -2019,6 +2056,43 @@ def expand_container_command_and_args(container, envs):
     cmd = [expand(str(x), m) for x in container.get("command") or ()] or None
     args = [expand(str(x), m) for x in container.get("args") or ()] or None
     return cmd, args
+
+
+def _host_ports(spec):
+    """(hostIP, protocol, hostPort) of every container port with a hostPort."""
+    out = []
+    for c in spec.get("containers") or ():
+        for p in c.get("ports") or ():
+            if p.get("hostPort"):
+                out.append((p.get("hostIP") or "0.0.0.0", p.get("protocol") or "TCP", int(p["hostPort"])))
+    return out
+
+
+def _node_affinity_required(spec):
+    aff = (spec.get("affinity") or {}).get("nodeAffinity") or {}
+    req = aff.get("requiredDuringSchedulingIgnoredDuringExecution")
+    return None if req is None else (req.get("nodeSelectorTerms") or [])
+
+
+def _node_affinity_matches(terms, labels, node_name):
+    """`nodeMatchesNodeSelectorTerms`: any term whose expressions (and metadata.name fields)
+    all match; a term with neither matches nothing."""
+    from ..api.labels import SelectorError, node_selector_requirements_as_selector
+    for t in terms:
+        exprs, fields = t.get("matchExpressions") or [], t.get("matchFields") or []
+        if not exprs and not fields:
+            continue
+        try:
+            if exprs and not node_selector_requirements_as_selector(exprs).matches(labels):
+                continue
+        except SelectorError:
+            continue
+        if any(f.get("key") == "metadata.name" and (
+                (f.get("operator") == "In" and node_name not in (f.get("values") or [])) or
+                (f.get("operator") == "NotIn" and node_name in (f.get("values") or []))) for f in fields):
+            continue
+        return True
+    return False
 
 
 def should_container_be_restarted(policy, status) -> bool:
