@@ -167,44 +167,49 @@ def rollout_status(obj, revision=0):
     kind, name = obj.get("kind"), obj["metadata"]["name"]
     spec, st = obj.get("spec") or {}, obj.get("status") or {}
     gen, observed = obj["metadata"].get("generation", 0), st.get("observedGeneration", 0)
-    if observed < gen:
-        return f"Waiting for {kind.lower()} spec update to be observed...", False
     if kind == "DaemonSet":
         if (spec.get("updateStrategy") or {}).get("type", "OnDelete") != "RollingUpdate":
-            return "rollout status is only available for RollingUpdate strategy type", True
+            raise SystemExit("error: Status is available only for RollingUpdate strategy type")
+        if gen > (observed or 0):
+            return "Waiting for daemon set spec update to be observed...", False
         want, upd, avail = st.get("desiredNumberScheduled", 0), st.get("updatedNumberScheduled", 0), st.get("numberAvailable", 0)
         if upd < want:
-            return f'Waiting for daemon set "{name}" rollout to finish: {upd} out of {want} new pods have been updated...', False
+            return f"Waiting for rollout to finish: {upd} out of {want} new pods have been updated...", False
         if avail < want:
-            return f'Waiting for daemon set "{name}" rollout to finish: {avail} of {want} updated pods are available...', False
+            return f"Waiting for rollout to finish: {avail} of {want} updated pods are available...", False
         return f'daemon set "{name}" successfully rolled out', True
     if kind == "StatefulSet":
         us = spec.get("updateStrategy") or {}
-        if us.get("type", "OnDelete") != "RollingUpdate":
-            return "rollout status is only available for RollingUpdate strategy type", True
-        want = spec.get("replicas", 1)
-        if st.get("readyReplicas", 0) < want:
+        if us.get("type", "RollingUpdate") == "OnDelete":
+            raise SystemExit("error: OnDelete updateStrategy does not have a Status`")
+        if st.get("observedGeneration") is None or gen > st["observedGeneration"]:
+            return "Waiting for statefulset spec update to be observed...", False
+        want = spec.get("replicas")
+        if want is not None and st.get("readyReplicas", 0) < want:
             return f"Waiting for {want - st.get('readyReplicas', 0)} pods to be ready...", False
-        part = (us.get("rollingUpdate") or {}).get("partition")
-        if part:
-            if st.get("updatedReplicas", 0) < want - part:
+        if us.get("type") == "RollingUpdate" and us.get("rollingUpdate") is not None:
+            part = us["rollingUpdate"].get("partition")
+            if want is not None and part is not None and st.get("updatedReplicas", 0) < want - part:
                 return (f"Waiting for partitioned roll out to finish: {st.get('updatedReplicas', 0)} out of "
                         f"{want - part} new pods have been updated..."), False
             return f"partitioned roll out complete: {st.get('updatedReplicas', 0)} new pods have been updated...", True
         if st.get("updateRevision") != st.get("currentRevision"):
             return (f"waiting for statefulset rolling update to complete {st.get('updatedReplicas', 0)} pods at "
                     f"revision {st.get('updateRevision')}..."), False
-        return f"statefulset rolling update complete {st.get('currentReplicas', want)} pods at revision {st.get('currentRevision')}...", True
+        return (f"statefulset rolling update complete {st.get('currentReplicas', 0)} pods at revision "
+                f"{st.get('currentRevision')}..."), True
     if revision:
         cur = int((obj["metadata"].get("annotations") or {}).get("deployment.kubernetes.io/revision") or 0)
-        if cur < revision:
-            return f"Waiting for deployment \"{name}\" to reach revision {revision}...", False
+        if cur != revision:
+            raise SystemExit(f"error: desired revision ({revision}) is different from the running revision ({cur})")
+    if gen > observed:
+        return "Waiting for deployment spec update to be observed...", False
     for c in st.get("conditions") or ():
         if c.get("type") == "Progressing" and c.get("reason") == "ProgressDeadlineExceeded":
             raise SystemExit(f'error: deployment "{name}" exceeded its progress deadline')
-    want = spec.get("replicas", 1)
+    want = spec.get("replicas")
     upd, total, avail = st.get("updatedReplicas", 0), st.get("replicas", 0), st.get("availableReplicas", 0)
-    if upd < want:
+    if want is not None and upd < want:
         return f'Waiting for rollout to finish: {upd} out of {want} new replicas have been updated...', False
     if total > upd:
         return f"Waiting for rollout to finish: {total - upd} old replicas are pending termination...", False

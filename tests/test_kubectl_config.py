@@ -139,7 +139,8 @@ def test_rollout_status_viewers():
           "status": {"observedGeneration": 2, "readyReplicas": 3, "updatedReplicas": 2}}
     assert rollout_status(ss) == ("partitioned roll out complete: 2 new pods have been updated...", True)
     ss["spec"]["updateStrategy"] = {"type": "OnDelete"}
-    assert rollout_status(ss)[1] is True and "only available for RollingUpdate" in rollout_status(ss)[0]
+    with pytest.raises(SystemExit, match="OnDelete updateStrategy does not have a Status"):
+        rollout_status(ss)
 
 
 def test_env_file_parsing(tmp_path, monkeypatch):
