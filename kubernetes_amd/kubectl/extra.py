@@ -79,6 +79,7 @@ def _create_parser():
     x.add_argument("--from-literal", action="append", default=[])
     x.add_argument("--from-file", action="append", default=[])
     x.add_argument("--from-env-file")
+    x.add_argument("--append-hash", action="store_true", help="Append a hash of the configmap to its name.")
     x = sub.add_parser("secret")
     ss = x.add_subparsers(dest="secret_type", required=True)
     g = ss.add_parser("generic")
@@ -92,6 +93,8 @@ def _create_parser():
     t.add_argument("--cert", required=True)
     t.add_argument("--key", required=True)
     d = ss.add_parser("docker-registry")
+    for q in (g, t, d):
+        q.add_argument("--append-hash", action="store_true", help="Append a hash of the secret to its name.")
     d.add_argument("name")
     d.add_argument("--docker-server", default="https://index.docker.io/v1/")
     d.add_argument("--docker-username", required=True)
@@ -198,6 +201,22 @@ def _labels_sel(s):
     return dict(p.split("=", 1) for p in s.split(",") if p)
 
 
+def _secret(a, md):
+    """The Secret of `kubectl create secret generic|tls|docker-registry`."""
+    if a.secret_type == "generic":
+        data = {kk: _b64(v) for kk, v in _kv(a.from_literal).items()}
+        data.update({kk: _b64(v) for kk, v in _from_files(a.from_file).items()})
+        data.update({kk: _b64(v) for kk, v in _env_file(a.from_env_file).items()})
+        return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": a.type, "data": data}
+    if a.secret_type == "tls":
+        return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": "kubernetes.io/tls",
+                           "data": {"tls.crt": _b64(open(a.cert, "rb").read()), "tls.key": _b64(open(a.key, "rb").read())}}
+    auth = _b64(f"{a.docker_username}:{a.docker_password}")
+    cfg = {"auths": {a.docker_server: {"username": a.docker_username, "password": a.docker_password,
+                                       "email": a.docker_email, "auth": auth}}}
+    return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": "kubernetes.io/dockerconfigjson",
+                       "data": {".dockerconfigjson": _b64(json.dumps(cfg))}}
+
 def generate(argv, ns):
     """Object built by a `kubectl create <generator>` command line (no server round trip)."""
     a = _create_parser().parse_args(argv)
@@ -220,21 +239,17 @@ def generate(argv, ns):
         o = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": md, "data": data}
         if binary:
             o["binaryData"] = binary
+        if a.append_hash:
+            from .hash import config_map_hash
+            md["name"] = f"{a.name}-{config_map_hash(o)}"
         return "configmaps", o
     if k == "secret":
-        if a.secret_type == "generic":
-            data = {kk: _b64(v) for kk, v in _kv(a.from_literal).items()}
-            data.update({kk: _b64(v) for kk, v in _from_files(a.from_file).items()})
-            data.update({kk: _b64(v) for kk, v in _env_file(a.from_env_file).items()})
-            return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": a.type, "data": data}
-        if a.secret_type == "tls":
-            return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": "kubernetes.io/tls",
-                               "data": {"tls.crt": _b64(open(a.cert, "rb").read()), "tls.key": _b64(open(a.key, "rb").read())}}
-        auth = _b64(f"{a.docker_username}:{a.docker_password}")
-        cfg = {"auths": {a.docker_server: {"username": a.docker_username, "password": a.docker_password,
-                                           "email": a.docker_email, "auth": auth}}}
-        return "secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": md, "type": "kubernetes.io/dockerconfigjson",
-                           "data": {".dockerconfigjson": _b64(json.dumps(cfg))}}
+        plural, o = _secret(a, md)
+        if a.append_hash:
+            from .hash import secret_hash
+            md["name"] = f"{a.name}-{secret_hash(o)}"
+        return plural, o
+
     if k in ("deployment", "deploy"):
         labels = {"app": a.name}
         ctrs = []
