@@ -1807,9 +1807,9 @@ class Kubelet:
 
         # status_manager.go SetPodStatus: Initialized and Ready from generate.go
         ready_c = generate_pod_ready_condition(spec, statuses, phase)
+        # generateAPIPodStatus: Initialized, Ready, PodScheduled (1.9 has no ContainersReady)
         conds = [cond(generate_pod_initialized_condition(spec, init_statuses, phase)),
                  cond(ready_c),
-                 cond({**ready_c, "type": core.COND_CONTAINERS_READY}),
                  cond({"type": core.COND_POD_SCHEDULED, "status": "True"})]
         status = {"phase": phase, "conditions": conds, "hostIP": self.address, "podIP": st.ip,
                   "startTime": st.start_time, "containerStatuses": statuses,
