@@ -27,6 +27,7 @@ from ..utils import grpclite
 from ..kubelet.sysctl import SysctlAdmitHandler
 from ..kubelet.runtime.base import CREATED, EXITED, RUNNING, UNKNOWN, ContainerStatus, Runtime, RuntimeError_
 from . import api as A
+from . import labels as L
 
 log = logging.getLogger("cri.remote")
 
@@ -112,15 +113,11 @@ class RemoteRuntime(Runtime):
                 "runtimeApiVersion": v.runtime_api_version}
 
     def _pod_labels(self, pod):
-        md = pod["metadata"]
-        labels = dict(md.get("labels") or {})
-        labels.update({A.POD_NAME: md.get("name", ""), A.POD_NAMESPACE: md.get("namespace", ""),
-                       A.POD_UID: md.get("uid", "")})
-        return labels
+        return L.new_pod_labels(pod)
 
     def _sandbox_config(self, pod, annotations):
         md = pod["metadata"]
-        ann = dict(md.get("annotations") or {})
+        ann = L.new_pod_annotations(pod)
         ann.update(annotations or {})
         ann[A.POD_SPEC_ANNOTATION] = json.dumps(pod, separators=(",", ":"))
         ports = [A.MSG["PortMapping"](protocol=A.UDP if p.get("protocol") == "UDP" else A.TCP,
@@ -155,14 +152,13 @@ class RemoteRuntime(Runtime):
         md = pod["metadata"]
         envs = [A.MSG["KeyValue"](key=e["name"], value=str(e["value"])) for e in container.get("env") or () if "value" in e]
         envs += [A.MSG["KeyValue"](key=e["name"], value=str(e["value"])) for e in opts.envs]
-        ann = {a["name"]: a["value"] for a in opts.annotations}
+        ann = L.new_container_annotations(container, pod, int(opts.attempt or 0), opts.annotations)
         ann[A.CONTAINER_SPEC_ANNOTATION] = json.dumps(container, separators=(",", ":"))
         if opts.cgroup_parent:
             ann[A.CGROUP_PARENT_ANNOTATION] = opts.cgroup_parent
         if opts.run_as_group is not None:
             ann[A.RUN_AS_GROUP_ANNOTATION] = str(int(opts.run_as_group))
-        labels = {A.POD_NAME: md.get("name", ""), A.POD_NAMESPACE: md.get("namespace", ""),
-                  A.POD_UID: md.get("uid", ""), A.CONTAINER_NAME: container["name"]}
+        labels = L.new_container_labels(container, pod)
         cfg = A.MSG["ContainerConfig"](
             metadata=A.MSG["ContainerMetadata"](name=container["name"], attempt=int(opts.attempt or 0)),
             image=A.MSG["ImageSpec"](image=container.get("image", "")),
@@ -172,7 +168,7 @@ class RemoteRuntime(Runtime):
                                    readonly=bool(m.get("readOnly"))) for m in opts.mounts],
             devices=[A.MSG["Device"](container_path=d.get("pathInContainer", ""), host_path=d.get("pathOnHost", ""),
                                      permissions=d.get("permissions", "rwm")) for d in opts.devices],
-            labels=labels, annotations=ann, log_path=f"{container['name']}/0.log",
+            labels=labels, annotations=ann, log_path=L.container_log_path(container["name"], opts.attempt or 0),
             linux=A.MSG["LinuxContainerConfig"](
                 resources=A.MSG["LinuxContainerResources"](oom_score_adj=opts.oom_score_adj or 0),
                 security_context=A.MSG["LinuxContainerSecurityContext"](
