@@ -289,3 +289,17 @@ def test_pod_phase_with_init_containers(policy, init, want):
     spec = {"initContainers": [{"name": "i"}], "containers": [{"name": "A"}], "restartPolicy": policy}
     statuses = [_running("A")] if want == "Running" else []
     assert get_phase(spec, statuses, init) == want
+
+
+# -- pkg/kubelet/cm/cpuset/cpuset_test.go TestCPUSetString / TestParse ---------------------------
+@pytest.mark.parametrize("cpus,text", [((), ""), ((5,), "5"), ((1, 2, 3, 4, 5), "1-5"), ((1, 2, 3, 5, 6, 8), "1-3,5-6,8")])
+def test_cpuset_string(cpus, text):
+    from kubernetes_amd.kubelet.cpumanager import format_cpulist
+    assert format_cpulist(cpus) == text
+
+
+@pytest.mark.parametrize("text,cpus", [("", set()), ("5", {5}), ("1,2,3,4,5", {1, 2, 3, 4, 5}), ("1-5", {1, 2, 3, 4, 5}),
+                                       ("1-2,3-5", {1, 2, 3, 4, 5})])
+def test_cpuset_parse(text, cpus):
+    from kubernetes_amd.kubelet.cpumanager import parse_cpulist
+    assert set(parse_cpulist(text)) == cpus
