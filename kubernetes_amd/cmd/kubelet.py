@@ -102,6 +102,13 @@ def main(argv=None):
     setup_logging(a.v)
     DefaultFeatureGate.set(a.feature_gates)
     _host_checks(a)
+    if a.node_ip:
+        # setNodeAddress -> validateNodeIP: an unusable --node-ip fails here, not on every status
+        from ..kubelet.network import validate_node_ip
+        try:
+            validate_node_ip(a.node_ip)
+        except ValueError as e:
+            ap.error(f"failed to validate nodeIP: {e}")
 
     async def start():
         if a.contention_profiling:

@@ -698,3 +698,57 @@ class HostportManager:
         for s in self.held.values():
             s.close()
         self.held.clear()
+
+
+# ------------------------------------------------------------------------------------ node IP
+def host_ip_addresses():
+    """The addresses assigned to this host's interfaces (`net.InterfaceAddrs`): IPv4 through
+    SIOCGIFADDR on each interface, IPv6 from /proc/net/if_inet6."""
+    import fcntl
+    import ipaddress
+    import struct
+    out = set()
+    try:
+        names = [n for _, n in socket.if_nameindex()]
+    except OSError:
+        names = []
+    s4 = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        for n in names:
+            try:
+                raw = fcntl.ioctl(s4.fileno(), 0x8915, struct.pack("256s", n[:15].encode()))    # SIOCGIFADDR
+                out.add(socket.inet_ntoa(raw[20:24]))
+            except OSError:
+                continue
+    finally:
+        s4.close()
+    try:
+        with open("/proc/net/if_inet6") as f:
+            for line in f:
+                h = line.split()[0]
+                out.add(str(ipaddress.IPv6Address(int(h, 16))))
+    except OSError:
+        pass
+    return out
+
+
+def validate_node_ip(node_ip, host_addrs=None):
+    """`validateNodeIP` (kubelet_node_status.go): a valid unicast address that is neither
+    loopback, multicast, link-local nor unspecified, and is assigned to this host. Raises
+    ValueError with the reference message."""
+    import ipaddress
+    try:
+        ip = ipaddress.ip_address(str(node_ip or "").strip())
+    except ValueError:
+        raise ValueError("nodeIP must be a valid IP address") from None
+    if ip.is_loopback:
+        raise ValueError("nodeIP can't be loopback address")
+    if ip.is_multicast:
+        raise ValueError("nodeIP can't be a multicast address")
+    if ip.is_link_local:
+        raise ValueError("nodeIP can't be a link-local unicast address")
+    if ip.is_unspecified:
+        raise ValueError("nodeIP can't be an all zeros address")
+    addrs = host_ip_addresses() if host_addrs is None else host_addrs
+    if not any(ipaddress.ip_address(a) == ip for a in addrs if a):
+        raise ValueError(f'Node IP: "{ip}" not found in the host\'s network interfaces')

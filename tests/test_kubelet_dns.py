@@ -262,3 +262,22 @@ def test_host_network_pod_gets_node_hosts_plus_aliases(tmp_path, monkeypatch):
     mounts = d.write_pod_files(str(tmp_path / "pod"), pod, "10.0.0.5", hosts_only=True)
     assert mounts[0]["containerPath"] == "/etc/hosts"
     assert (tmp_path / "pod" / "etc-hosts").read_text() == node_hosts.read_text() + ALIAS_TEXT1
+
+
+# -- pkg/kubelet/kubelet_network_test.go TestNodeIPParam -------------------------------------------
+@pytest.mark.parametrize("ip,msg", [
+    ("", "must be a valid IP address"), ("127.0.0.1", "loopback"), ("::1", "loopback"),
+    ("224.0.0.1", "multicast"), ("ff00::1", "multicast"), ("169.254.0.1", "link-local"),
+    ("fe80::0202:b3ff:fe1e:8329", "link-local"), ("0.0.0.0", "all zeros"), ("::", "all zeros"),
+    ("1.2.3.4", "not found in the host's network interfaces"),
+])
+def test_node_ip_param_rejected(ip, msg):
+    with pytest.raises(ValueError, match=msg):
+        net.validate_node_ip(ip, host_addrs={"10.0.0.5", "fd00::2"})
+
+
+def test_node_ip_param_host_addresses_accepted():
+    usable = [a for a in net.host_ip_addresses() if not a.startswith(("127.", "::1", "fe80"))]
+    for a in usable:
+        net.validate_node_ip(a)
+    net.validate_node_ip("10.0.0.5", host_addrs={"10.0.0.5"})
