@@ -35,7 +35,8 @@ def pod_qos(pod) -> str:
 
 def is_critical_pod(pod) -> bool:
     md = pod.get("metadata") or {}
-    if md.get("namespace") == "kube-system" and CRITICAL_POD_ANNOTATION in (md.get("annotations") or {}):
+    # IsCritical: kube-system only, and the annotation's value must be empty
+    if md.get("namespace") == "kube-system" and (md.get("annotations") or {}).get(CRITICAL_POD_ANNOTATION) == "":
         return True
     prio = (pod.get("spec") or {}).get("priority")
     return prio is not None and int(prio) >= SYSTEM_CRITICAL_PRIORITY

@@ -89,3 +89,12 @@ def test_hugepages_limit_makes_pod_burstable():
     """Reference quirk: qosLimitsFound counts hugepages, compared against the 2 cpu/memory names."""
     p = pod(ctr({**rl("1", "1Gi"), "hugepages-2Mi": "2Mi"}, {**rl("1", "1Gi"), "hugepages-2Mi": "2Mi"}))
     assert qos_class(p) == "Burstable"
+
+
+# -- pkg/kubelet/types/pod_update_test.go TestIsCriticalPod ---------------------------------------
+@pytest.mark.parametrize("ns,value,want", [("ns", "", False), ("ns", "abc", False), ("kube-system", "abc", False),
+                                          ("kube-system", "", True)])
+def test_is_critical_pod(ns, value, want):
+    from kubernetes_amd.kubelet.qos import CRITICAL_POD_ANNOTATION, is_critical_pod
+    pod = {"metadata": {"name": "p", "namespace": ns, "annotations": {CRITICAL_POD_ANNOTATION: value}}, "spec": {}}
+    assert is_critical_pod(pod) is want
