@@ -105,13 +105,23 @@ class StaticPodSource:
     def _mirror(self, doc, h, source="file"):
         pod = json.loads(json.dumps(doc))
         md = pod.setdefault("metadata", {})
-        md["name"] = f"{md.get('name', 'static')}-{self.kl.node_name}"
-        md.setdefault("namespace", "default")
+        # common.go applyDefaults: generatePodName (lower-cased node name), namespace default
+        md["name"] = f"{md.get('name', 'static')}-{str(self.kl.node_name).lower()}"
+        if not md.get("namespace"):
+            md["namespace"] = "default"
         ann = md.setdefault("annotations", {})
         ann.update({CONFIG_SOURCE: source, CONFIG_HASH: h, CONFIG_MIRROR: h})
         for k in ("uid", "resourceVersion", "creationTimestamp"):
             md.pop(k, None)
         pod.setdefault("spec", {})["nodeName"] = self.kl.node_name
+        if source == "file":
+            # static pods from files tolerate every NoExecute taint, so node problems do not
+            # evict them (AddOrUpdateTolerationInPod)
+            tols = pod["spec"].setdefault("tolerations", [])
+            want = {"operator": "Exists", "effect": "NoExecute"}
+            if not any(t.get("operator") == "Exists" and t.get("effect") == "NoExecute" and not t.get("key")
+                       for t in tols):
+                tols.append(want)
         pod.pop("status", None)
         pod["apiVersion"], pod["kind"] = "v1", "Pod"
         return pod

@@ -303,3 +303,23 @@ def test_cpuset_string(cpus, text):
 def test_cpuset_parse(text, cpus):
     from kubernetes_amd.kubelet.cpumanager import parse_cpulist
     assert set(parse_cpulist(text)) == cpus
+
+
+def test_static_pod_defaults_like_apply_defaults():
+    """`pkg/kubelet/config/common.go` applyDefaults: `<name>-<lower-cased node>`, namespace
+    default for an empty one, bound to the node, and file pods tolerate every NoExecute taint
+    (added once); pods from a URL do not get the toleration."""
+    from types import SimpleNamespace
+
+    from kubernetes_amd.kubelet.config import CONFIG_HASH, CONFIG_SOURCE, StaticPodSource
+    src = StaticPodSource(SimpleNamespace(node_name="Node-A"), None)
+    doc = {"metadata": {"name": "etcd", "namespace": ""}, "spec": {"containers": [{"name": "c", "image": "i"}],
+                                                                   "tolerations": [{"key": "k", "operator": "Exists"}]}}
+    pod = src._mirror(doc, "h1", "file")
+    assert pod["metadata"]["name"] == "etcd-node-a" and pod["metadata"]["namespace"] == "default"
+    assert pod["spec"]["nodeName"] == "Node-A"
+    assert pod["metadata"]["annotations"][CONFIG_SOURCE] == "file" and pod["metadata"]["annotations"][CONFIG_HASH] == "h1"
+    assert pod["spec"]["tolerations"] == [{"key": "k", "operator": "Exists"}, {"operator": "Exists", "effect": "NoExecute"}]
+    again = src._mirror(pod, "h1", "file")
+    assert again["spec"]["tolerations"].count({"operator": "Exists", "effect": "NoExecute"}) == 1
+    assert "tolerations" not in src._mirror({"metadata": {"name": "x"}, "spec": {}}, "h2", "http")["spec"]
