@@ -1284,7 +1284,7 @@ class Kubelet:
         no per-line times), sinceSeconds / sinceTime (a file not written since then yields
         nothing, otherwise all of it: the same file-level granularity)."""
         from ..api.meta import parse_rfc3339
-        data = await self.runtime.container_logs(cid, tail)
+        from .logs import is_structured, read_logs
         limit = int(q.get("limitBytes") or 0)
         path = getattr(self.runtime, "log_path", lambda c: None)(cid)
         since = None
@@ -1292,6 +1292,17 @@ class Kubelet:
             since = time.time() - float(q["sinceSeconds"])
         elif q.get("sinceTime"):
             since = parse_rfc3339(q["sinceTime"])
+        if path and q.get("follow") not in ("true", "1") and os.path.exists(path):
+            # a CRI runtime's own log file (`<time> <stream> <tag> <log>` or docker JSON):
+            # ReadLogs with per-record times
+            with open(path, "rb") as f:
+                first = f.readline()
+            if first and is_structured(first):
+                with open(path, "rb") as f:
+                    raw = f.read()
+                return Response(200, read_logs(raw, tail, since, q.get("timestamps") in ("true", "1"), limit or None),
+                                "text/plain")
+        data = await self.runtime.container_logs(cid, tail)
         if since is not None and path and os.path.exists(path) and os.path.getmtime(path) < since:
             data = b""
         stamp = q.get("timestamps") in ("true", "1")
