@@ -626,6 +626,24 @@ def _chain(name, proto, port):
     return "KUBE-HP-" + base64.b32encode(h).decode()[:16]
 
 
+def make_port_mappings(container):
+    """`kubecontainer.MakePortMappings`: one mapping per container port, named
+    `<container>-<name>` or `<container>-<PROTO>:<port>`; a repeated name is dropped (the same
+    protocol/port exposed twice)."""
+    out, names = [], set()
+    for p in container.get("ports") or ():
+        proto = p.get("protocol") or "TCP"
+        name = (f"{container.get('name', '')}-{p['name']}" if p.get("name")
+                else f"{container.get('name', '')}-{proto}:{int(p.get('containerPort') or 0)}")
+        if name in names:
+            log.warning("Port name conflicted, %r is defined more than once", name)
+            continue
+        names.add(name)
+        out.append({"name": name, "protocol": proto, "containerPort": int(p.get("containerPort") or 0),
+                    "hostPort": int(p.get("hostPort") or 0), "hostIP": p.get("hostIP") or ""})
+    return out
+
+
 class HostportManager:
     def __init__(self, hold_sockets=True):
         self.hold = hold_sockets
@@ -638,10 +656,9 @@ class HostportManager:
         md = pod["metadata"]
         full = f"{md['name']}_{md.get('namespace', 'default')}"
         for c in (pod.get("spec") or {}).get("containers") or ():
-            for p in c.get("ports") or ():
-                if p.get("hostPort"):
-                    out.append((p.get("protocol", "TCP").lower(), p.get("hostIP", ""), int(p["hostPort"]),
-                                int(p["containerPort"]), ip, full))
+            for pm in make_port_mappings(c):
+                if pm["hostPort"]:
+                    out.append((pm["protocol"].lower(), pm["hostIP"], pm["hostPort"], pm["containerPort"], ip, full))
         return out
 
     def add(self, pod, ip):

@@ -307,3 +307,16 @@ def test_kubenet_delegates_to_cni_bridge(run, tmp_path):
         with pytest.raises(ValueError):
             net.KubenetPlugin(str(tmp_path / "e"), hairpin_mode="bogus")
     run(main())
+
+
+def test_make_port_mappings():
+    """`pkg/kubelet/container/helpers_test.go` TestMakePortMappings."""
+    def port(name, proto, cport, hport, ip):
+        return {"name": name, "protocol": proto, "containerPort": cport, "hostPort": hport, "hostIP": ip}
+    c = {"name": "fooContainer", "ports": [port("", "TCP", 80, 8080, "127.0.0.1"), port("", "TCP", 443, 4343, "192.168.0.1"),
+                                           port("foo", "UDP", 555, 5555, ""), port("foo", "UDP", 888, 8888, ""),
+                                           port("", "TCP", 80, 8888, "")]}
+    got = net.make_port_mappings(c)
+    assert [(m["name"], m["protocol"], m["containerPort"], m["hostPort"], m["hostIP"]) for m in got] == [
+        ("fooContainer-TCP:80", "TCP", 80, 8080, "127.0.0.1"), ("fooContainer-TCP:443", "TCP", 443, 4343, "192.168.0.1"),
+        ("fooContainer-foo", "UDP", 555, 5555, "")]
