@@ -32,18 +32,35 @@ def nominated_node_name(pod) -> str:
 
 
 class PodBackoff:
-    def __init__(self, initial=1.0, maximum=60.0):
+    """`plugin/pkg/scheduler/util/backoff_utils.go` PodBackoff: per-pod exponential backoff
+    (initial, doubling, capped at maximum); entries untouched for longer than the maximum are
+    garbage-collected (`Gc`, also run every 1024 updates), so a pod seen again later starts over."""
+
+    def __init__(self, initial=1.0, maximum=60.0, clock=time.monotonic):
         self.initial, self.maximum = initial, maximum
+        self.clock = clock
         self.entries: dict[str, float] = {}
+        self.updated: dict[str, float] = {}
+        self._ops = 0
 
     def next(self, key):
         d = self.entries.get(key, self.initial / 2) * 2
         d = min(d, self.maximum)
         self.entries[key] = d
+        self.updated[key] = self.clock()
+        self._ops += 1
+        if self._ops & 1023 == 0:
+            self.gc()
         return d
 
     def forget(self, key):
         self.entries.pop(key, None)
+        self.updated.pop(key, None)
+
+    def gc(self):
+        now = self.clock()
+        for key in [k for k, t in self.updated.items() if now - t > self.maximum]:
+            self.forget(key)
 
 
 class SchedulingQueue:

@@ -470,3 +470,17 @@ def test_node_condition_predicate(conditions, unschedulable, fits):
     cache.add_node(node)
     pod = _pod("p")
     assert (check_node_condition(pod, PodInfo(pod), cache.nodes["n"], CycleContext(cache, pod)) is None) == fits
+
+
+def test_pod_backoff():
+    """`plugin/pkg/scheduler/util/backoff_utils_test.go` TestBackoff."""
+    from kubernetes_amd.scheduler.queue import PodBackoff
+    now = [0.0]
+    b = PodBackoff(1.0, 60.0, clock=lambda: now[0])
+    for key, want, advance in (("default/foo", 1, 0), ("default/foo", 2, 0), ("default/foo", 4, 0),
+                               ("default/bar", 1, 120), ("default/foo", 1, 0)):      # foo gc'd after 120 s
+        assert b.next(key) == want, key
+        now[0] += advance
+        b.gc()
+    b.entries["default/foo"] = 60.0
+    assert b.next("default/foo") == 60.0                                            # capped
