@@ -60,11 +60,27 @@ class _Ctx:
     tolerates_unschedulable = True
 
 
-def _with_tolerations(spec):
-    tols = list(spec.get("tolerations") or [])
-    for t in DS_TOLERATIONS:
-        if t not in tols:
-            tols.append(t)
+OUT_OF_DISK_TOLERATION = {"key": "node.kubernetes.io/out-of-disk", "operator": "Exists", "effect": "NoExecute"}
+CRITICAL_POD_ANNOTATION = "scheduler.alpha.kubernetes.io/critical-pod"     # kubelettypes.CriticalPodAnnotationKey
+
+
+def _with_tolerations(spec, meta=None):
+    """CreatePodTemplate's tolerations (`AddOrUpdateTolerationInPodSpec`: a toleration with the
+    same key and effect is replaced); a critical daemon pod (ExperimentalCriticalPodAnnotation,
+    kube-system + empty critical-pod annotation) also tolerates the out-of-disk NoExecute taint."""
+    tols = [dict(t) for t in spec.get("tolerations") or []]
+    want = list(DS_TOLERATIONS)
+    md = meta or {}
+    from ..utils.features import DefaultFeatureGate
+    if DefaultFeatureGate("ExperimentalCriticalPodAnnotation") and md.get("namespace") == "kube-system" and \
+            (md.get("annotations") or {}).get(CRITICAL_POD_ANNOTATION) == "":
+        want.append(OUT_OF_DISK_TOLERATION)
+    for t in want:
+        same = [i for i, x in enumerate(tols) if x.get("key") == t["key"] and x.get("effect") == t["effect"]]
+        if same:
+            tols[same[0]] = dict(t)
+        else:
+            tols.append(dict(t))
     return tols
 
 
@@ -85,7 +101,8 @@ def node_should_run(ds, node, node_pods=()):
         return False, False, False, None
     spec = m.fast_copy(tspec)
     spec["nodeName"] = name
-    spec["tolerations"] = _with_tolerations(spec)
+    spec["tolerations"] = _with_tolerations(spec, {"namespace": ds["metadata"].get("namespace"),
+                                                   "annotations": (tmpl.get("metadata") or {}).get("annotations")})
     pod = {"metadata": {"name": "probe", "namespace": ds["metadata"].get("namespace"),
                         "labels": dict((tmpl.get("metadata") or {}).get("labels") or {})}, "spec": spec}
     ni = NodeInfo()
@@ -361,7 +378,7 @@ class DaemonSetController(Controller):
             if generation is not None:
                 pod["metadata"]["labels"][TEMPLATE_GENERATION] = str(generation)
             spec = pod["spec"]
-            spec["tolerations"] = _with_tolerations(spec)
+            spec["tolerations"] = _with_tolerations(spec, pod["metadata"])
             aff = spec.setdefault("affinity", {}).setdefault("nodeAffinity", {})
             aff["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [
                 {"matchExpressions": [{"key": HOSTNAME, "operator": "In", "values": [node]}]}]}

@@ -542,3 +542,21 @@ def test_update_node_enqueues_only_on_relevant_changes(run):
         b = node("node1", conditions=[{"type": "Ready", "status": "True", "lastHeartbeatTime": "2"}])
         assert not enqueued(a, b)
     run(main())
+
+
+def test_create_pod_template_tolerations(feature_gate):
+    """`pkg/controller/daemon/util/daemonset_util_test.go` TestCreatePodTemplate: the not-ready /
+    unreachable NoExecute and pressure NoSchedule tolerations (replacing same key+effect ones), and
+    out-of-disk only for a critical pod."""
+    from kubernetes_amd.controllers.daemonset import OUT_OF_DISK_TOLERATION, _with_tolerations
+    spec = {"tolerations": [{"key": "node.kubernetes.io/not-ready", "operator": "Equal", "value": "x",
+                             "effect": "NoExecute", "tolerationSeconds": 5}]}
+    tols = _with_tolerations(spec, {"namespace": "default"})
+    keys = [(t["key"], t["effect"]) for t in tols]
+    assert keys.count(("node.kubernetes.io/not-ready", "NoExecute")) == 1
+    assert {"key": "node.kubernetes.io/not-ready", "operator": "Exists", "effect": "NoExecute"} in tols
+    assert OUT_OF_DISK_TOLERATION not in tols
+    crit = {"namespace": "kube-system", "annotations": {"scheduler.alpha.kubernetes.io/critical-pod": ""}}
+    assert OUT_OF_DISK_TOLERATION in _with_tolerations({}, crit)
+    feature_gate.set("ExperimentalCriticalPodAnnotation=false")
+    assert OUT_OF_DISK_TOLERATION not in _with_tolerations({}, crit)
