@@ -21,10 +21,36 @@ def revision_hash(template) -> str:
     return hashlib.sha256(json.dumps(template or {}, sort_keys=True).encode()).hexdigest()[:10]
 
 
+def sort_controller_revisions(revisions):
+    """`SortControllerRevisions`: by revision number (stable for equal numbers)."""
+    return sorted(revisions or (), key=lambda r: int(r.get("revision", 0)))
+
+
+def next_revision(revisions) -> int:
+    """`NextRevision`: one past the highest revision, 1 for an empty history."""
+    return max((int(r.get("revision", 0)) for r in revisions or ()), default=0) + 1
+
+
+def equal_revision(a, b) -> bool:
+    """`EqualRevision`: the same hash label (when both carry one) and the same data."""
+    if a is None or b is None:
+        return a is b
+    ha = (a["metadata"].get("labels") or {}).get(REVISION_HASH)
+    hb = (b["metadata"].get("labels") or {}).get(REVISION_HASH)
+    if ha is not None and hb is not None and ha != hb:
+        return False
+    return (a.get("data") or {}) == (b.get("data") or {})
+
+
+def find_equal_revisions(revisions, needle):
+    """`FindEqualRevisions`: the revisions equal to `needle`."""
+    return [r for r in revisions or () if equal_revision(r, needle)]
+
+
 def revisions_of(lister_items, owner_uid):
     out = [r for r in lister_items
            if any(o.get("uid") == owner_uid and o.get("controller") for o in r["metadata"].get("ownerReferences") or ())]
-    return sorted(out, key=lambda r: int(r.get("revision", 0)))
+    return sort_controller_revisions(out)
 
 
 async def ensure_revision(client, owner, kind, template, existing, limit=10):

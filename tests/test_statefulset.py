@@ -543,3 +543,28 @@ def test_controller_revision_adoption_and_collision():
         {"apiVersion": "apps/v1", "kind": "StatefulSet", "name": "web", "uid": "old-uid", "controller": True}]))
     rev, c = _a.run(run(foreign))
     assert rev["metadata"]["name"] == f"web-{h}-1" and rev["metadata"]["ownerReferences"][0]["uid"] == "new-uid"
+
+
+# -- pkg/controller/history/controller_history_test.go TestSortControllerRevisions /
+#    TestFindEqualRevisions, plus NextRevision --------------------------------------------------
+def _rev(name, number, data, h="h"):
+    return {"metadata": {"name": name, "labels": {"controller-revision-hash": h}}, "revision": number, "data": data}
+
+
+def test_sort_and_next_revision():
+    from kubernetes_amd.controllers.history import next_revision, sort_controller_revisions
+    r1, r2, r3 = _rev("r1", 1, {}), _rev("r2", 2, {}), _rev("r3", 2, {})
+    for order in ([r2, r1, r3], [r1, r2, r3], [r3, r2, r1]):
+        assert [r["revision"] for r in sort_controller_revisions(order)] == [1, 2, 2]
+    assert sort_controller_revisions(None) == []
+    assert next_revision([]) == 1 and next_revision([r1, r3]) == 3
+
+
+def test_find_equal_revisions():
+    from kubernetes_amd.controllers.history import find_equal_revisions
+    a1 = _rev("a1", 1, {"spec": {"template": {"x": 1}}}, "ha")
+    a2 = _rev("a2", 2, {"spec": {"template": {"x": 1}}}, "ha")
+    b1 = _rev("b1", 1, {"spec": {"template": {"x": 2}}}, "hb")
+    collide = _rev("c", 3, {"spec": {"template": {"x": 3}}}, "ha")        # same hash, other data
+    assert [r["metadata"]["name"] for r in find_equal_revisions([a1, b1, a2, collide], a1)] == ["a1", "a2"]
+    assert find_equal_revisions([b1], a1) == [] and find_equal_revisions([], a1) == []
