@@ -72,3 +72,15 @@ def test_kubelet_reregisters_over_existing_node(run):
         finally:
             await cl.stop()
     run(main(), timeout=60)
+
+
+def test_too_large_reservation_floors_allocatable_at_zero():
+    """`kubelet_node_status_test.go` TestUpdateNewNodeStatusTooLargeReservation: a reservation
+    above capacity leaves allocatable 0, never negative."""
+    from types import SimpleNamespace
+
+    from kubernetes_amd.kubelet.kubelet import Kubelet
+    kl = SimpleNamespace(reserved=({"cpu": "40000m", "memory": "10Gi"}, {}), eviction=None,
+                         allocatable_ignore_eviction=True)
+    alloc = Kubelet._allocatable(kl, {"cpu": "2", "memory": "1Gi", "pods": "110"})
+    assert alloc["cpu"] == "0m" and alloc["memory"] == "0" and alloc["pods"] == "110"
